@@ -1,0 +1,196 @@
+"""Typed property-key registry.
+
+Parity: core/common/src/main/java/alluxio/conf/PropertyKey.java (504 named keys + templates),
+core/common/src/main/java/alluxio/conf/Source.java:30-80 (source priority).  Every reference key
+name and default is registered from :mod:`keys_table`; this module adds the per-tier templates
+(``alluxio.worker.tieredstore.level{N}.*``, PropertyKey.java:2933-2985) and the MI355X-specific
+keys (HBM arena sizing, page size, GPU device selection, RCCL data plane).
+"""
+from __future__ import annotations
+
+import enum
+import re
+import threading
+
+from .keys_table import KEYS as _REFERENCE_KEYS
+
+
+class Scope(enum.Flag):
+    MASTER = 1
+    WORKER = 2
+    CLIENT = 4
+    SERVER = MASTER | WORKER
+    ALL = MASTER | WORKER | CLIENT
+    NONE = 0
+
+
+class PropertyKey:
+    __slots__ = ("name", "default", "scope", "aliases", "description", "template")
+
+    def __init__(self, name, default=None, scope=Scope.ALL, aliases=(), description="",
+                 template=None):
+        self.name = name
+        self.default = None if default is None else str(default)
+        self.scope = scope
+        self.aliases = tuple(aliases)
+        self.description = description
+        self.template = template
+
+    def __str__(self) -> str:
+        return self.name
+
+    def __repr__(self) -> str:
+        return f"PropertyKey({self.name!r})"
+
+    def __hash__(self) -> int:
+        return hash(self.name)
+
+    def __eq__(self, other) -> bool:
+        if isinstance(other, str):
+            return self.name == other
+        return isinstance(other, PropertyKey) and other.name == self.name
+
+
+_REGISTRY: dict[str, PropertyKey] = {}
+_ALIASES: dict[str, str] = {}
+_LOCK = threading.Lock()
+
+
+def register(key: PropertyKey) -> PropertyKey:
+    with _LOCK:
+        _REGISTRY[key.name] = key
+        for a in key.aliases:
+            _ALIASES[a] = key.name
+    return key
+
+
+for _name, _default, _scope, _aliases in _REFERENCE_KEYS:
+    register(PropertyKey(_name, _default, Scope[_scope], _aliases))
+
+
+class Template:
+    """Parametrised key families (reference ``PropertyKey.Template``)."""
+
+    def __init__(self, fmt: str, regex: str, default_fn=None, scope=Scope.ALL):
+        self.fmt = fmt
+        self.regex = re.compile(regex)
+        self.default_fn = default_fn
+        self.scope = scope
+
+    def format(self, *args) -> PropertyKey:
+        name = self.fmt % args
+        with _LOCK:
+            k = _REGISTRY.get(name)
+        if k is not None:
+            return k
+        default = self.default_fn(*args) if self.default_fn else None
+        return register(PropertyKey(name, default, self.scope, template=self))
+
+    def match(self, name: str):
+        return self.regex.fullmatch(name)
+
+
+_TIER_ALIAS_DEFAULTS = {0: "MEM", 1: "SSD", 2: "HDD"}
+_TIER_MEDIUM_DEFAULTS = {0: "HBM", 1: "DRAM", 2: "SSD"}
+
+
+class Templates:
+    WORKER_TIERED_STORE_LEVEL_ALIAS = Template(
+        "alluxio.worker.tieredstore.level%d.alias", r"alluxio\.worker\.tieredstore\.level(\d+)\.alias",
+        lambda i: _TIER_ALIAS_DEFAULTS.get(i), Scope.WORKER)
+    WORKER_TIERED_STORE_LEVEL_DIRS_PATH = Template(
+        "alluxio.worker.tieredstore.level%d.dirs.path",
+        r"alluxio\.worker\.tieredstore\.level(\d+)\.dirs\.path",
+        lambda i: {0: "hbm:0"}.get(i, "/tmp/alluxio_amd/tier%d" % i), Scope.WORKER)
+    WORKER_TIERED_STORE_LEVEL_DIRS_QUOTA = Template(
+        "alluxio.worker.tieredstore.level%d.dirs.quota",
+        r"alluxio\.worker\.tieredstore\.level(\d+)\.dirs\.quota",
+        lambda i: {0: "4GB", 1: "8GB"}.get(i, "16GB"), Scope.WORKER)
+    WORKER_TIERED_STORE_LEVEL_DIRS_MEDIUMTYPE = Template(
+        "alluxio.worker.tieredstore.level%d.dirs.mediumtype",
+        r"alluxio\.worker\.tieredstore\.level(\d+)\.dirs\.mediumtype",
+        lambda i: _TIER_MEDIUM_DEFAULTS.get(i, "SSD"), Scope.WORKER)
+    WORKER_TIERED_STORE_LEVEL_HIGH_WATERMARK_RATIO = Template(
+        "alluxio.worker.tieredstore.level%d.watermark.high.ratio",
+        r"alluxio\.worker\.tieredstore\.level(\d+)\.watermark\.high\.ratio",
+        lambda i: "0.95", Scope.WORKER)
+    WORKER_TIERED_STORE_LEVEL_LOW_WATERMARK_RATIO = Template(
+        "alluxio.worker.tieredstore.level%d.watermark.low.ratio",
+        r"alluxio\.worker\.tieredstore\.level(\d+)\.watermark\.low\.ratio",
+        lambda i: "0.7", Scope.WORKER)
+    WORKER_TIERED_STORE_LEVEL_RESERVED_RATIO = Template(
+        "alluxio.worker.tieredstore.level%d.reserved.ratio",
+        r"alluxio\.worker\.tieredstore\.level(\d+)\.reserved\.ratio",
+        lambda i: None, Scope.WORKER)
+    MASTER_TIERED_STORE_GLOBAL_LEVEL_ALIAS = Template(
+        "alluxio.master.tieredstore.global.level%d.alias",
+        r"alluxio\.master\.tieredstore\.global\.level(\d+)\.alias",
+        lambda i: _TIER_ALIAS_DEFAULTS.get(i), Scope.MASTER)
+    LOCALITY_TIER = Template("alluxio.locality.%s", r"alluxio\.locality\.(\w+)")
+    MASTER_MOUNT_TABLE_OPTION = Template(
+        "alluxio.master.mount.table.%s.option", r"alluxio\.master\.mount\.table\.(\w+)\.option")
+    USER_NETWORK_KEEPALIVE_TIME = Template(
+        "alluxio.user.network.%s.keepalive.time", r"alluxio\.user\.network\.(\w+)\.keepalive\.time")
+
+
+# --- MI355X-specific keys --------------------------------------------------------------------
+K = {}
+
+
+def _k(attr: str, name: str, default, scope=Scope.ALL, description=""):
+    key = register(PropertyKey(name, default, scope, description=description))
+    K[attr] = key
+    return key
+
+
+_k("WORKER_GPU_DEVICE", "alluxio.worker.gpu.device", "-1", Scope.WORKER,
+   "HIP device index this worker owns (-1: LOCAL_RANK or 0).")
+_k("WORKER_HBM_PAGE_SIZE", "alluxio.worker.hbm.page.size", "2MB", Scope.WORKER,
+   "Fixed page size of the HBM arena; blocks are ceil(len/page) pages.")
+_k("WORKER_HBM_ARENA_FRACTION", "alluxio.worker.hbm.arena.fraction", "0.0", Scope.WORKER,
+   "If >0, size the HBM tier as this fraction of free device memory (overrides the quota).")
+_k("WORKER_DATA_CRC_ENABLED", "alluxio.worker.data.crc.enabled", "false", Scope.WORKER,
+   "Compute a CRC32C per page when a block is committed (HIP kernel).")
+_k("WORKER_DATA_COMPRESSION", "alluxio.worker.data.compression", "NONE", Scope.WORKER,
+   "Block codec for the host tiers: NONE | LZ4.")
+_k("WORKER_RCCL_ENABLED", "alluxio.worker.rccl.enabled", "true", Scope.WORKER,
+   "Use RCCL over xGMI for worker<->worker block transfer when ranks share a node.")
+_k("WORKER_IPC_ENABLED", "alluxio.worker.ipc.enabled", "true", Scope.WORKER,
+   "Hand out HIP IPC handles for short-circuit reads of HBM pages.")
+_k("WORKER_STAGING_BUFFER_SIZE", "alluxio.worker.staging.buffer.size", "64MB", Scope.WORKER,
+   "Pinned host staging ring used for UFS->HBM and HBM->host copies.")
+_k("WORKER_EVICTION_KERNEL_MIN_BLOCKS", "alluxio.worker.eviction.kernel.min.blocks", "1", Scope.WORKER,
+   "Use the device eviction-ordering kernel when a dir holds at least this many blocks.")
+_k("USER_READ_BATCH_SIZE", "alluxio.user.read.batch.size", "256", Scope.CLIENT,
+   "Max read requests coalesced into one page-gather launch.")
+_k("USER_FILE_READ_DEVICE", "alluxio.user.file.read.device", "cuda", Scope.CLIENT,
+   "Preferred destination of client reads: cuda (HBM) or cpu (pinned host).")
+
+
+def get(name: str) -> PropertyKey:
+    """Resolve a key by name, alias or template match."""
+    with _LOCK:
+        k = _REGISTRY.get(name)
+        if k is None and name in _ALIASES:
+            k = _REGISTRY[_ALIASES[name]]
+    if k is not None:
+        return k
+    for t in vars(Templates).values():
+        if isinstance(t, Template):
+            m = t.match(name)
+            if m:
+                arg = m.group(1)
+                return t.format(int(arg) if arg.isdigit() else arg)
+    return register(PropertyKey(name, None, Scope.ALL))
+
+
+def is_valid(name: str) -> bool:
+    with _LOCK:
+        if name in _REGISTRY or name in _ALIASES:
+            return True
+    return any(isinstance(t, Template) and t.match(name) for t in vars(Templates).values())
+
+
+def all_keys() -> list[PropertyKey]:
+    with _LOCK:
+        return list(_REGISTRY.values())

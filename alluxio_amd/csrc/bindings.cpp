@@ -1,0 +1,295 @@
+// pybind11 bindings of the native worker data plane (module alluxio_amd._C).
+// All entry points release the GIL: the Python worker serves many concurrent gRPC streams.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <vector>
+
+#include "block_store.h"
+#include "cpu_codecs.h"
+#include "kernels.h"
+
+namespace py = pybind11;
+using namespace amdx;
+
+namespace {
+
+#define HIP_CHECK(expr)                                                                   \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess) throw StoreError(kErrHip, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  explicit DevBuf(size_t n) { HIP_CHECK(hipMalloc(&p, n ? n : 1)); }
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+int hip_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+std::vector<uint32_t> crc32c_device(uint64_t ptr, uint64_t len, uint64_t piece, uint64_t stream) {
+  if (piece == 0) piece = len ? len : 1;
+  const uint64_t np = len ? (len + piece - 1) / piece : 0;
+  std::vector<uint32_t> out(np);
+  if (!np) return out;
+  const uint64_t sw = crc32c_scratch_words(len, piece);
+  DevBuf d((np + sw) * 4);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_CHECK(launch_crc32c_pieces(reinterpret_cast<const uint8_t*>(ptr), len, piece, (uint32_t*)d.p,
+                                 (uint32_t*)d.p + np, sw, st));
+  HIP_CHECK(hipMemcpyAsync(out.data(), d.p, np * 4, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  return out;
+}
+
+// chunks: list of (src_ptr, dst_ptr, src_bytes, dst_capacity) on the device
+std::vector<int32_t> lz4_device(const std::vector<std::tuple<uint64_t, uint64_t, uint32_t, uint32_t>>& chunks,
+                                bool compress, uint64_t stream) {
+  const int n = (int)chunks.size();
+  std::vector<int32_t> sizes(n, 0);
+  if (!n) return sizes;
+  std::vector<Lz4Chunk> h(n);
+  for (int i = 0; i < n; ++i) {
+    h[i].src = std::get<0>(chunks[i]);
+    h[i].dst = std::get<1>(chunks[i]);
+    h[i].src_bytes = std::get<2>(chunks[i]);
+    h[i].dst_capacity = std::get<3>(chunks[i]);
+  }
+  DevBuf dch(sizeof(Lz4Chunk) * n), dsz(sizeof(int32_t) * n);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_CHECK(hipMemcpyAsync(dch.p, h.data(), sizeof(Lz4Chunk) * n, hipMemcpyHostToDevice, st));
+  if (compress) HIP_CHECK(launch_lz4_compress((Lz4Chunk*)dch.p, n, (int32_t*)dsz.p, st));
+  else HIP_CHECK(launch_lz4_decompress((Lz4Chunk*)dch.p, n, (int32_t*)dsz.p, st));
+  HIP_CHECK(hipMemcpyAsync(sizes.data(), dsz.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  return sizes;
+}
+
+void batched_copy(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>>& segs, uint64_t stream, bool sync) {
+  const size_t n = segs.size();
+  if (!n) return;
+  std::vector<CopySeg> h(n);
+  uint64_t chunks = 0;
+  for (size_t i = 0; i < n; ++i) {
+    h[i] = CopySeg{std::get<0>(segs[i]), std::get<1>(segs[i]), std::get<2>(segs[i]), chunks};
+    chunks += (h[i].bytes + kCopyChunk - 1) / kCopyChunk;
+  }
+  DevBuf d(sizeof(CopySeg) * n);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_CHECK(hipMemcpyAsync(d.p, h.data(), sizeof(CopySeg) * n, hipMemcpyHostToDevice, st));
+  HIP_CHECK(launch_batched_copy((const CopySeg*)d.p, (int)n, chunks, st));
+  // the descriptor buffer is freed on return: always wait for the launch
+  HIP_CHECK(hipStreamSynchronize(st));
+  (void)sync;
+}
+
+py::tuple evict_select_device(const std::vector<float>& crf, const std::vector<uint64_t>& last,
+                              const std::vector<uint64_t>& bytes, const std::vector<uint8_t>& evictable,
+                              uint64_t now, float step, float att, int policy, uint64_t need) {
+  const size_t n = crf.size();
+  if (last.size() != n || bytes.size() != n || evictable.size() != n)
+    throw StoreError(kErrInvalidArgument, "evict_select_device: array length mismatch");
+  std::vector<uint32_t> out;
+  uint64_t freed = 0;
+  {
+    py::gil_scoped_release rel;
+    DevBuf dc(n * 4), dl(n * 8), db(n * 8), de(n), dk(n * 4), dout(n * 4), dcnt(16);
+    HIP_CHECK(hipMemcpy(dc.p, crf.data(), n * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dl.p, last.data(), n * 8, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(db.p, bytes.data(), n * 8, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(de.p, evictable.data(), n, hipMemcpyHostToDevice));
+    EvictInput in{(const float*)dc.p, (const uint64_t*)dl.p, (const uint64_t*)db.p, (const uint8_t*)de.p,
+                  (uint32_t)n, now, step, att, policy, need};
+    HIP_CHECK(launch_evict_select(in, (uint32_t*)dk.p, (uint32_t*)dout.p, (uint32_t*)dcnt.p,
+                                  (uint64_t*)((char*)dcnt.p + 8), nullptr));
+    uint32_t cnt = 0;
+    HIP_CHECK(hipMemcpy(&cnt, dcnt.p, 4, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(&freed, (char*)dcnt.p + 8, 8, hipMemcpyDeviceToHost));
+    out.resize(cnt);
+    if (cnt) HIP_CHECK(hipMemcpy(out.data(), dout.p, cnt * 4, hipMemcpyDeviceToHost));
+  }
+  return py::make_tuple(out, freed);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native worker data plane: HBM page store + CDNA4 kernels";
+
+  static py::exception<StoreError> store_error(m, "StoreError");
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const StoreError& e) {
+      // args = (code, message); alluxio_amd/ops/native.py maps code -> status exception
+      py::object inst = py::reinterpret_steal<py::object>(
+          PyObject_CallFunction(store_error.ptr(), "is", e.code, e.what()));
+      PyErr_SetObject(store_error.ptr(), inst.ptr());
+    }
+  });
+
+  py::enum_<DirKind>(m, "DirKind").value("DEVICE", DirKind::kDevice).value("HOST", DirKind::kHost)
+      .value("FILE", DirKind::kFile);
+
+  py::class_<DirSpec>(m, "DirSpec")
+      .def(py::init<>())
+      .def_readwrite("tier", &DirSpec::tier)
+      .def_readwrite("tier_alias", &DirSpec::tier_alias)
+      .def_readwrite("medium", &DirSpec::medium)
+      .def_readwrite("kind", &DirSpec::kind)
+      .def_readwrite("base", &DirSpec::base)
+      .def_readwrite("capacity", &DirSpec::capacity)
+      .def_readwrite("page_size", &DirSpec::page_size)
+      .def_readwrite("device", &DirSpec::device)
+      .def_readwrite("path", &DirSpec::path)
+      .def_readwrite("reserved", &DirSpec::reserved);
+
+  py::class_<BlockInfoOut>(m, "BlockInfo")
+      .def_readonly("id", &BlockInfoOut::id)
+      .def_readonly("length", &BlockInfoOut::length)
+      .def_readonly("tier", &BlockInfoOut::tier)
+      .def_readonly("dir", &BlockInfoOut::dir)
+      .def_readonly("tier_alias", &BlockInfoOut::tier_alias)
+      .def_readonly("medium", &BlockInfoOut::medium)
+      .def_readonly("temp", &BlockInfoOut::temp)
+      .def_readonly("session", &BlockInfoOut::session)
+      .def_readonly("readers", &BlockInfoOut::readers)
+      .def_readonly("writer", &BlockInfoOut::writer);
+
+  py::class_<Event>(m, "Event")
+      .def_readonly("kind", &Event::kind)
+      .def_readonly("block_id", &Event::block_id)
+      .def_readonly("tier_alias", &Event::tier_alias)
+      .def_readonly("medium", &Event::medium);
+
+  using G = py::call_guard<py::gil_scoped_release>;
+  py::class_<BlockStore>(m, "BlockStore")
+      .def(py::init<const std::vector<DirSpec>&, int, int, float, float, int>(), py::arg("dirs"),
+           py::arg("annotator") = 0, py::arg("alloc_policy") = 0, py::arg("lrfu_step") = 0.25f,
+           py::arg("lrfu_attenuation") = 2.0f, py::arg("device") = 0)
+      .def("create_block", &BlockStore::create_block, G(), py::arg("session"), py::arg("block_id"),
+           py::arg("tier") = -1, py::arg("medium") = "", py::arg("initial") = 1 << 20,
+           py::arg("evict") = true, py::arg("pin") = false)
+      .def("request_space", &BlockStore::request_space, G())
+      .def("write", &BlockStore::write, G(), py::arg("session"), py::arg("block_id"), py::arg("offset"),
+           py::arg("src"), py::arg("length"), py::arg("src_kind"), py::arg("stream") = 0,
+           py::arg("sync") = true)
+      .def("commit_block", &BlockStore::commit_block, G(), py::arg("session"), py::arg("block_id"),
+           py::arg("pin") = false)
+      .def("abort_block", &BlockStore::abort_block, G())
+      .def("remove_block", &BlockStore::remove_block, G())
+      .def("move_block", &BlockStore::move_block, G(), py::arg("session"), py::arg("block_id"),
+           py::arg("tier"), py::arg("medium") = "", py::arg("evict") = true)
+      .def("lock_block", &BlockStore::lock_block, G(), py::arg("session"), py::arg("block_id"),
+           py::arg("write") = false, py::arg("timeout_ms") = -1)
+      .def("unlock", &BlockStore::unlock, G())
+      .def("cleanup_session", &BlockStore::cleanup_session, G())
+      .def("access_block", &BlockStore::access_block, G())
+      .def("access_blocks", &BlockStore::access_blocks, G())
+      .def("read_batch",
+           [](BlockStore& s, const std::vector<std::tuple<int64_t, uint64_t, uint64_t, uint64_t, int>>& reqs,
+              uint64_t stream, bool sync) {
+             std::vector<ReadReq> rs;
+             rs.reserve(reqs.size());
+             for (auto& t : reqs)
+               rs.push_back(ReadReq{std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t), std::get<4>(t)});
+             py::gil_scoped_release rel;
+             s.read_batch(rs, stream, sync);
+           },
+           py::arg("reqs"), py::arg("stream") = 0, py::arg("sync") = true)
+      .def("read", [](BlockStore& s, int64_t id, uint64_t off, uint64_t len, uint64_t dst, int kind,
+                      uint64_t stream, bool sync) {
+             std::vector<ReadReq> rs{ReadReq{id, off, len, dst, kind}};
+             py::gil_scoped_release rel;
+             s.read_batch(rs, stream, sync);
+           },
+           py::arg("block_id"), py::arg("offset"), py::arg("length"), py::arg("dst"), py::arg("dst_kind"),
+           py::arg("stream") = 0, py::arg("sync") = true)
+      .def("checksum", &BlockStore::checksum, G(), py::arg("block_id"), py::arg("piece_bytes") = 0)
+      .def("fill_pattern", &BlockStore::fill_pattern, G())
+      .def("free_space", &BlockStore::free_space, G(), py::arg("session"), py::arg("bytes"),
+           py::arg("tier") = -1, py::arg("dir") = -1)
+      .def("eviction_order", &BlockStore::eviction_order, G(), py::arg("tier") = -1, py::arg("need_bytes") = 0)
+      .def("set_pinned_files", &BlockStore::set_pinned_files, G())
+      .def("set_use_device_evict", &BlockStore::set_use_device_evict)
+      .def("has_block", &BlockStore::has_block, G())
+      .def("has_temp_block", &BlockStore::has_temp_block, G())
+      .def("block_info", &BlockStore::block_info, G())
+      .def("block_ids", &BlockStore::block_ids, G(), py::arg("tier") = -1)
+      .def("block_pages", [](BlockStore& s, int64_t id) {
+             int dir = 0;
+             uint64_t ps = 0, base = 0;
+             std::vector<int64_t> pages;
+             {
+               py::gil_scoped_release rel;
+               pages = s.block_pages(id, &dir, &ps, &base);
+             }
+             return py::make_tuple(pages, dir, ps, base);
+           })
+      .def("drain_events", &BlockStore::drain_events, G())
+      .def("num_dirs", &BlockStore::num_dirs)
+      .def("dir_spec", &BlockStore::dir_spec)
+      .def("dir_capacity", &BlockStore::dir_capacity, G())
+      .def("dir_available", &BlockStore::dir_available, G())
+      .def("dir_committed", &BlockStore::dir_committed, G())
+      .def("set_dir_healthy", &BlockStore::set_dir_healthy, G())
+      .def("dir_healthy", &BlockStore::dir_healthy, G())
+      .def("clock", &BlockStore::clock)
+      .def("device", &BlockStore::device)
+      .def("stats", &BlockStore::stats, G());
+
+  // ---- codecs / kernels ------------------------------------------------------------------
+  m.def("device_count", &hip_device_count);
+  m.def("crc32c", [](py::bytes data, uint32_t crc) {
+          std::string s = data;
+          py::gil_scoped_release rel;
+          return crc32c_sw(s.data(), s.size(), crc);
+        }, py::arg("data"), py::arg("crc") = 0);
+  m.def("crc32c_ptr", [](uint64_t ptr, uint64_t n, uint32_t crc) {
+          py::gil_scoped_release rel;
+          return crc32c_sw(reinterpret_cast<const void*>(ptr), n, crc);
+        }, py::arg("ptr"), py::arg("n"), py::arg("crc") = 0);
+  m.def("crc32c_combine", &crc32c_combine);
+  m.def("crc32c_device", &crc32c_device, G(), py::arg("ptr"), py::arg("length"), py::arg("piece") = 0,
+        py::arg("stream") = 0);
+  m.def("lz4_compress", [](py::bytes data) {
+          std::string s = data;
+          std::string out(lz4_compress_bound(s.size()), '\0');
+          int64_t n;
+          {
+            py::gil_scoped_release rel;
+            n = lz4_compress_block((const uint8_t*)s.data(), s.size(), (uint8_t*)&out[0], out.size());
+          }
+          if (n < 0) throw StoreError(kErrInvalidArgument, "lz4 compression failed");
+          out.resize((size_t)n);
+          return py::bytes(out);
+        });
+  m.def("lz4_decompress", [](py::bytes data, size_t capacity) {
+          std::string s = data;
+          std::string out(capacity, '\0');
+          int64_t n;
+          {
+            py::gil_scoped_release rel;
+            n = lz4_decompress_block((const uint8_t*)s.data(), s.size(), (uint8_t*)&out[0], out.size());
+          }
+          if (n < 0) throw StoreError(kErrInvalidArgument, "malformed lz4 block (" + std::to_string(n) + ")");
+          out.resize((size_t)n);
+          return py::bytes(out);
+        });
+  m.def("lz4_compress_bound", &lz4_compress_bound);
+  m.def("lz4_device", &lz4_device, G(), py::arg("chunks"), py::arg("compress"), py::arg("stream") = 0);
+  m.def("batched_copy", &batched_copy, G(), py::arg("segments"), py::arg("stream") = 0, py::arg("sync") = true);
+  m.def("fill_pattern", [](uint64_t ptr, uint64_t bytes, uint64_t seed, uint64_t word_offset, uint64_t stream) {
+          py::gil_scoped_release rel;
+          HIP_CHECK(launch_fill_pattern(reinterpret_cast<uint8_t*>(ptr), bytes, seed, word_offset,
+                                        reinterpret_cast<hipStream_t>(stream)));
+        }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("word_offset") = 0, py::arg("stream") = 0);
+  m.def("evict_select_device", &evict_select_device);
+  m.attr("COPY_CHUNK") = kCopyChunk;
+}

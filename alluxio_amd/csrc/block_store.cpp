@@ -1,0 +1,1082 @@
+#include "block_store.h"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <sstream>
+
+#include "cpu_codecs.h"
+
+namespace amdx {
+
+#define HIP_OK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      throw StoreError(kErrHip, std::string("HIP error: ") + hipGetErrorString(_e) + " at " \
+                                    + #expr);                                              \
+  } while (0)
+
+static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+uint64_t StorageDir::available() const {
+  if (!healthy) return 0;
+  if (spec.kind == DirKind::kFile) {
+    const uint64_t cap = capacity();
+    return file_used >= cap ? 0 : cap - file_used;
+  }
+  const uint64_t free_b = (uint64_t)free_pages * spec.page_size;
+  return free_b;
+}
+
+uint64_t StorageDir::capacity() const {
+  if (spec.kind == DirKind::kFile) return spec.capacity > spec.reserved ? spec.capacity - spec.reserved : 0;
+  return (uint64_t)num_pages * spec.page_size;
+}
+
+// -------------------------------------------------------------------------------------------
+BlockStore::BlockStore(const std::vector<DirSpec>& dirs, int annotator, int alloc_policy,
+                       float lrfu_step, float lrfu_attenuation, int device)
+    : annotator_(static_cast<Annotator>(annotator)),
+      alloc_policy_(static_cast<AllocPolicy>(alloc_policy)),
+      lrfu_step_(lrfu_step),
+      lrfu_att_(lrfu_attenuation),
+      device_(device) {
+  int max_tier = 0;
+  for (size_t i = 0; i < dirs.size(); ++i) {
+    auto d = std::make_unique<StorageDir>();
+    d->spec = dirs[i];
+    d->index = (int)i;
+    if (d->spec.kind != DirKind::kFile) {
+      if (d->spec.page_size == 0) throw StoreError(kErrInvalidArgument, "page size must be > 0");
+      const uint64_t usable = d->spec.capacity > d->spec.reserved ? d->spec.capacity - d->spec.reserved : 0;
+      d->num_pages = (int64_t)(usable / d->spec.page_size);
+      d->free_bits.assign(ceil_div((uint64_t)d->num_pages, 64), 0);
+      for (int64_t p = 0; p < d->num_pages; ++p) d->free_bits[p >> 6] |= 1ull << (p & 63);
+      d->free_pages = d->num_pages;
+      if (d->spec.kind == DirKind::kDevice) has_device_ = true;
+    } else {
+      ::mkdir(d->spec.path.c_str(), 0755);
+      ::mkdir((d->spec.path + "/.tmp_blocks").c_str(), 0755);
+    }
+    max_tier = std::max(max_tier, d->spec.tier);
+    dirs_.push_back(std::move(d));
+  }
+  rr_index_.assign(max_tier + 1, 0);
+  if (has_device_) {
+    set_device();
+    HIP_OK(hipStreamCreateWithFlags(&internal_stream_, hipStreamNonBlocking));
+    HIP_OK(hipHostMalloc((void**)&host_ring_, sizeof(CopySeg) * kRing * kRingSegs, hipHostMallocDefault));
+    HIP_OK(hipMalloc((void**)&dev_ring_, sizeof(CopySeg) * kRing * kRingSegs));
+    for (int i = 0; i < kRing; ++i) HIP_OK(hipEventCreateWithFlags(&ring_ev_[i], hipEventDisableTiming));
+  }
+}
+
+BlockStore::~BlockStore() {
+  if (has_device_) {
+    hipSetDevice(device_);
+    for (int i = 0; i < kRing; ++i)
+      if (ring_ev_[i]) hipEventDestroy(ring_ev_[i]);
+    if (host_ring_) hipHostFree(host_ring_);
+    if (dev_ring_) hipFree(dev_ring_);
+    if (ev_dev_) hipFree(ev_dev_);
+    if (crc_dev_) hipFree(crc_dev_);
+    if (internal_stream_) hipStreamDestroy(internal_stream_);
+  }
+}
+
+void BlockStore::set_device() const {
+  if (has_device_) {
+    hipError_t e = hipSetDevice(device_);
+    if (e != hipSuccess) throw StoreError(kErrHip, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  }
+}
+
+hipStream_t BlockStore::stream_or_default(uint64_t s) const {
+  return s ? reinterpret_cast<hipStream_t>(s) : internal_stream_;
+}
+
+// -------------------------------------------------------------------------------------------
+// metadata helpers
+BlockMeta* BlockStore::find(int64_t id) {
+  auto it = blocks_.find(id);
+  return it == blocks_.end() ? nullptr : &it->second;
+}
+
+BlockMeta& BlockStore::get_committed(int64_t id) {
+  BlockMeta* b = find(id);
+  if (!b || b->temp) throw StoreError(kErrNotFound, "block " + std::to_string(id) + " does not exist");
+  return *b;
+}
+
+bool BlockStore::dir_matches(const StorageDir& d, int tier, const std::string& medium) const {
+  if (!d.healthy) return false;
+  if (tier >= 0 && d.spec.tier != tier) return false;
+  if (!medium.empty() && d.spec.medium != medium) return false;
+  return true;
+}
+
+uint32_t BlockStore::alloc_slot() {
+  if (!free_slots_.empty()) {
+    const uint32_t s = free_slots_.back();
+    free_slots_.pop_back();
+    return s;
+  }
+  crf_.push_back(0.f);
+  last_.push_back(0);
+  slot_block_.push_back(0);
+  return (uint32_t)(crf_.size() - 1);
+}
+
+void BlockStore::touch_slot(uint32_t slot) {
+  const uint64_t now = ++clock_;
+  if (annotator_ == Annotator::kLRFU) {
+    const double age = (double)(now - last_[slot]);
+    crf_[slot] = (float)(crf_[slot] * std::pow(1.0 / lrfu_att_, age * lrfu_step_) + 1.0);
+  }
+  last_[slot] = now;
+}
+
+bool BlockStore::evictable(const BlockMeta& b) const {
+  if (b.temp || b.readers > 0 || b.writer || b.evicting || b.pinned_on_create) return false;
+  // file id = container id with the max 24-bit sequence number (reference BlockId.getFileId)
+  const int64_t file_id = (int64_t)(((uint64_t)b.id & ~0xFFFFFFull) | 0xFFFFFFull);
+  return pinned_files_.find(file_id) == pinned_files_.end();
+}
+
+void BlockStore::emit(int kind, const BlockMeta& b) {
+  const auto& d = dirs_[b.dir]->spec;
+  events_.push_back(Event{kind, b.id, d.tier_alias, d.medium});
+}
+
+void BlockStore::file_path(const StorageDir& d, int64_t id, std::string& out) const {
+  out = d.spec.path + "/" + std::to_string(id);
+}
+
+// -------------------------------------------------------------------------------------------
+// page allocation
+static bool bit_free(const std::vector<uint64_t>& bits, int64_t p) { return (bits[p >> 6] >> (p & 63)) & 1; }
+static void bit_take(std::vector<uint64_t>& bits, int64_t p) { bits[p >> 6] &= ~(1ull << (p & 63)); }
+static void bit_give(std::vector<uint64_t>& bits, int64_t p) { bits[p >> 6] |= 1ull << (p & 63); }
+
+// First run of `n` free pages (returns -1 if none).
+static int64_t find_run(const std::vector<uint64_t>& bits, int64_t num_pages, int64_t n) {
+  int64_t run = 0, start = 0;
+  for (int64_t w = 0; w < (int64_t)bits.size(); ++w) {
+    const uint64_t word = bits[w];
+    if (word == 0) { run = 0; continue; }
+    if (word == ~0ull && (w + 1) * 64 <= num_pages) {
+      if (run == 0) start = w * 64;
+      run += 64;
+      if (run >= n) return start;
+      continue;
+    }
+    for (int b = 0; b < 64; ++b) {
+      const int64_t p = w * 64 + b;
+      if (p >= num_pages) break;
+      if ((word >> b) & 1) {
+        if (run == 0) start = p;
+        if (++run >= n) return start;
+      } else {
+        run = 0;
+      }
+    }
+  }
+  return -1;
+}
+
+bool BlockStore::grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved) {
+  if (d.spec.kind == DirKind::kFile) {
+    const uint64_t add = new_reserved > b.reserved ? new_reserved - b.reserved : 0;
+    if (add > d.available()) return false;
+    d.file_used += add;
+    b.reserved = std::max(b.reserved, new_reserved);
+    return true;
+  }
+  const int64_t want = (int64_t)ceil_div(new_reserved, d.spec.page_size);
+  int64_t need = want - (int64_t)b.pages.size();
+  if (need <= 0) {
+    b.reserved = std::max(b.reserved, new_reserved);
+    return true;
+  }
+  if (need > d.free_pages) return false;
+  // 1) extend the block's current run in place
+  if (!b.pages.empty()) {
+    int64_t p = b.pages.back() + 1;
+    while (need > 0 && p < d.num_pages && bit_free(d.free_bits, p)) {
+      bit_take(d.free_bits, p);
+      b.pages.push_back(p++);
+      --d.free_pages;
+      --need;
+    }
+  }
+  // 2) a fresh contiguous run
+  if (need > 0) {
+    const int64_t s = find_run(d.free_bits, d.num_pages, need);
+    if (s >= 0) {
+      for (int64_t p = s; p < s + need; ++p) {
+        bit_take(d.free_bits, p);
+        b.pages.push_back(p);
+      }
+      d.free_pages -= need;
+      need = 0;
+    }
+  }
+  // 3) scattered pages
+  for (int64_t w = 0; need > 0 && w < (int64_t)d.free_bits.size(); ++w) {
+    uint64_t word = d.free_bits[w];
+    while (word && need > 0) {
+      const int b0 = __builtin_ctzll(word);
+      const int64_t p = w * 64 + b0;
+      if (p >= d.num_pages) break;
+      bit_take(d.free_bits, p);
+      b.pages.push_back(p);
+      --d.free_pages;
+      --need;
+      word &= word - 1;
+    }
+  }
+  b.reserved = std::max(b.reserved, new_reserved);
+  return need == 0;
+}
+
+void BlockStore::release_storage(BlockMeta& b) {
+  StorageDir& d = *dirs_[b.dir];
+  if (d.spec.kind == DirKind::kFile) {
+    d.file_used -= std::min(d.file_used, b.reserved);
+    std::string p;
+    if (b.temp) {
+      p = d.spec.path + "/.tmp_blocks/" + std::to_string(b.session) + "-" + std::to_string(b.id);
+    } else {
+      file_path(d, b.id, p);
+    }
+    ::unlink(p.c_str());
+  } else {
+    for (int64_t p : b.pages) bit_give(d.free_bits, p);
+    d.free_pages += (int64_t)b.pages.size();
+    b.pages.clear();
+  }
+  if (!b.temp) d.committed_bytes -= std::min(d.committed_bytes, b.length);
+  b.reserved = 0;
+}
+
+int BlockStore::allocate_dir(int tier, const std::string& medium, uint64_t bytes) {
+  // tier < 0: top-down over tiers, first tier with a fitting dir wins (MaxFreeAllocator anyTier)
+  int max_tier = (int)rr_index_.size() - 1;
+  const int t0 = tier < 0 ? 0 : tier, t1 = tier < 0 ? max_tier : tier;
+  for (int t = t0; t <= t1; ++t) {
+    std::vector<int> cands;
+    for (auto& d : dirs_)
+      if (dir_matches(*d, t, medium)) cands.push_back(d->index);
+    if (cands.empty()) continue;
+    int pick = -1;
+    if (alloc_policy_ == AllocPolicy::kGreedy) {
+      for (int c : cands)
+        if (dirs_[c]->available() >= bytes) { pick = c; break; }
+    } else if (alloc_policy_ == AllocPolicy::kRoundRobin) {
+      const int n = (int)cands.size();
+      for (int k = 0; k < n; ++k) {
+        const int c = cands[(rr_index_[t] + k) % n];
+        if (dirs_[c]->available() >= bytes) {
+          pick = c;
+          rr_index_[t] = (rr_index_[t] + k + 1) % n;
+          break;
+        }
+      }
+    } else {
+      uint64_t best = 0;
+      for (int c : cands) {
+        const uint64_t a = dirs_[c]->available();
+        if (a >= bytes && (pick < 0 || a > best)) { pick = c; best = a; }
+      }
+    }
+    if (pick >= 0) return pick;
+  }
+  return -1;
+}
+
+// -------------------------------------------------------------------------------------------
+// lifecycle
+int BlockStore::create_block(int64_t session, int64_t block_id, int tier, const std::string& medium,
+                             uint64_t initial, bool evict, bool pin) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (blocks_.count(block_id))
+    throw StoreError(kErrAlreadyExists, "block " + std::to_string(block_id) + " already exists");
+  int d = allocate_dir(tier, medium, initial);
+  if (d < 0 && evict) {
+    free_space_locked(lk, session, initial, tier, -1, medium);
+    d = allocate_dir(tier, medium, initial);
+  }
+  if (d < 0)
+    throw StoreError(kErrOutOfSpace, "no space for " + std::to_string(initial) + " bytes in tier " +
+                                         std::to_string(tier));
+  BlockMeta b;
+  b.id = block_id;
+  b.dir = d;
+  b.temp = true;
+  b.session = session;
+  b.pinned_on_create = pin;
+  if (!grow_pages(*dirs_[d], b, std::max<uint64_t>(initial, 1))) {
+    release_storage(b);
+    throw StoreError(kErrOutOfSpace, "allocation raced for block " + std::to_string(block_id));
+  }
+  b.slot = alloc_slot();
+  slot_block_[b.slot] = block_id;
+  crf_[b.slot] = 0.f;
+  last_[b.slot] = clock_.load();
+  if (dirs_[d]->spec.kind == DirKind::kFile) {
+    const std::string p = dirs_[d]->spec.path + "/.tmp_blocks/" + std::to_string(session) + "-" +
+                          std::to_string(block_id);
+    int fd = ::open(p.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+    if (fd < 0) throw StoreError(kErrIo, "cannot create " + p);
+    ::close(fd);
+  }
+  blocks_.emplace(block_id, std::move(b));
+  session_temps_[session].insert(block_id);
+  return d;
+}
+
+void BlockStore::request_space(int64_t session, int64_t block_id, uint64_t additional) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(block_id);
+  if (!b || !b->temp) throw StoreError(kErrNotFound, "temp block " + std::to_string(block_id) + " not found");
+  if (b->session != session) throw StoreError(kErrInvalidState, "temp block owned by another session");
+  StorageDir& d = *dirs_[b->dir];
+  const uint64_t target = b->reserved + additional;
+  if (grow_pages(d, *b, target)) return;
+  free_space_locked(lk, session, additional, d.spec.tier, b->dir, "");
+  b = find(block_id);
+  if (!b || !grow_pages(*dirs_[b->dir], *b, target))
+    throw StoreError(kErrOutOfSpace, "cannot reserve " + std::to_string(additional) + " more bytes");
+}
+
+void BlockStore::write(int64_t session, int64_t block_id, uint64_t offset, uint64_t src, uint64_t len,
+                       int src_kind, uint64_t stream, bool sync) {
+  if (len == 0) return;
+  set_device();
+  std::vector<CopySeg> dev_segs;
+  hipStream_t st = stream_or_default(stream);
+  BlockMeta snapshot;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    BlockMeta* b = find(block_id);
+    if (!b || !b->temp) throw StoreError(kErrNotFound, "temp block " + std::to_string(block_id) + " not found");
+    if (b->session != session) throw StoreError(kErrInvalidState, "temp block owned by another session");
+    if (offset + len > b->reserved) {
+      const uint64_t add = offset + len - b->reserved;
+      lk.unlock();
+      request_space(session, block_id, add);
+      lk.lock();
+      b = find(block_id);
+      if (!b || !b->temp) throw StoreError(kErrNotFound, "temp block vanished during write");
+    }
+    b->length = std::max(b->length, offset + len);
+    snapshot = *b;
+  }
+  plan_block_range(snapshot, offset, len, src, src_kind, /*to_block=*/true, dev_segs, st);
+  if (!dev_segs.empty()) copy_segments(dev_segs, st);
+  if (sync && has_device_) HIP_OK(hipStreamSynchronize(st));
+}
+
+void BlockStore::commit_block(int64_t session, int64_t block_id, bool pin) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(block_id);
+  if (!b || !b->temp) throw StoreError(kErrNotFound, "temp block " + std::to_string(block_id) + " not found");
+  if (b->session != session) throw StoreError(kErrInvalidState, "temp block owned by another session");
+  StorageDir& d = *dirs_[b->dir];
+  // return over-reserved pages
+  if (d.spec.kind != DirKind::kFile) {
+    const size_t keep = (size_t)ceil_div(std::max<uint64_t>(b->length, 1), d.spec.page_size);
+    while (b->pages.size() > keep) {
+      bit_give(d.free_bits, b->pages.back());
+      b->pages.pop_back();
+      ++d.free_pages;
+    }
+    b->reserved = b->pages.size() * d.spec.page_size;
+  } else {
+    const std::string tmp = d.spec.path + "/.tmp_blocks/" + std::to_string(session) + "-" + std::to_string(block_id);
+    std::string fin;
+    file_path(d, block_id, fin);
+    if (::rename(tmp.c_str(), fin.c_str()) != 0) throw StoreError(kErrIo, "rename failed for " + tmp);
+    d.file_used -= std::min(d.file_used, b->reserved);
+    b->reserved = b->length;
+    d.file_used += b->reserved;
+  }
+  b->temp = false;
+  b->pinned_on_create = b->pinned_on_create || pin;
+  d.committed_bytes += b->length;
+  session_temps_[session].erase(block_id);
+  touch_slot(b->slot);
+  emit(0, *b);
+}
+
+void BlockStore::abort_block(int64_t session, int64_t block_id) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(block_id);
+  if (!b || !b->temp) throw StoreError(kErrNotFound, "temp block " + std::to_string(block_id) + " not found");
+  if (b->session != session) throw StoreError(kErrInvalidState, "temp block owned by another session");
+  release_storage(*b);
+  free_slots_.push_back(b->slot);
+  session_temps_[session].erase(block_id);
+  blocks_.erase(block_id);
+}
+
+void BlockStore::remove_locked(BlockMeta& b, bool emit_event) {
+  if (emit_event) emit(1, b);
+  release_storage(b);
+  free_slots_.push_back(b.slot);
+  crf_[b.slot] = 0.f;
+  blocks_.erase(b.id);
+}
+
+void BlockStore::remove_block(int64_t session, int64_t block_id) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(block_id);
+  if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(block_id) + " does not exist");
+  if (b->temp) throw StoreError(kErrInvalidState, "cannot remove temp block " + std::to_string(block_id));
+  // wait for readers/writers held by *other* sessions (reference: removeBlock takes a write lock)
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+  while (true) {
+    b = find(block_id);
+    if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(block_id) + " does not exist");
+    if (b->readers == 0 && !b->writer) break;
+    if (lock_cv_.wait_until(lk, deadline) == std::cv_status::timeout)
+      throw StoreError(kErrTimeout, "timed out waiting to remove locked block " + std::to_string(block_id));
+  }
+  remove_locked(*b, true);
+  lock_cv_.notify_all();
+}
+
+int BlockStore::move_block(int64_t session, int64_t block_id, int dst_tier, const std::string& medium,
+                           bool evict) {
+  set_device();
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(block_id);
+  if (!b || b->temp) throw StoreError(kErrNotFound, "block " + std::to_string(block_id) + " does not exist");
+  if (b->writer || b->readers > 0) throw StoreError(kErrInvalidState, "block is locked");
+  if (dir_matches(*dirs_[b->dir], dst_tier, medium)) return b->dir;
+  const uint64_t len = b->length;
+  int d = allocate_dir(dst_tier, medium, std::max<uint64_t>(len, 1));
+  if (d < 0 && evict) {
+    b->evicting = true;  // never pick the block being moved as its own victim
+    free_space_locked(lk, session, len, dst_tier, -1, medium);
+    b = find(block_id);
+    if (b) b->evicting = false;
+    d = allocate_dir(dst_tier, medium, std::max<uint64_t>(len, 1));
+  }
+  if (!b) throw StoreError(kErrNotFound, "block vanished during move");
+  if (d < 0) throw StoreError(kErrOutOfSpace, "no space in destination tier for move");
+  BlockMeta nb;
+  nb.id = block_id;
+  nb.dir = d;
+  nb.temp = false;
+  nb.length = len;
+  if (!grow_pages(*dirs_[d], nb, std::max<uint64_t>(len, 1))) throw StoreError(kErrOutOfSpace, "move allocation failed");
+  b->writer = true;  // hold the block while copying
+  BlockMeta src_snap = *b;
+  lk.unlock();
+  // copy: src -> staging/dst using the same planners (block->external, external->block)
+  hipStream_t st = internal_stream_;
+  std::vector<CopySeg> dev_segs;
+  StorageDir& sd = *dirs_[src_snap.dir];
+  StorageDir& dd = *dirs_[d];
+  const bool src_dev = sd.spec.kind == DirKind::kDevice, dst_dev = dd.spec.kind == DirKind::kDevice;
+  std::vector<uint8_t> bounce;
+  try {
+    if (sd.spec.kind != DirKind::kFile && dd.spec.kind != DirKind::kFile &&
+        (sd.spec.kind == DirKind::kHost || dd.spec.kind == DirKind::kHost || src_dev)) {
+      // arena -> arena: walk destination pages, reading source range into each
+      uint64_t off = 0;
+      size_t i = 0;
+      while (off < len) {
+        const int64_t p0 = nb.pages[i];
+        size_t j = i + 1;
+        while (j < nb.pages.size() && nb.pages[j] == nb.pages[j - 1] + 1) ++j;
+        const uint64_t run = std::min<uint64_t>((j - i) * dd.spec.page_size, len - off);
+        const uint64_t dst_addr = dd.spec.base + (uint64_t)p0 * dd.spec.page_size;
+        plan_block_range(src_snap, off, run, dst_addr, dst_dev ? (int)MemKind::kDevice : (int)MemKind::kHost,
+                         false, dev_segs, st);
+        off += run;
+        i = j;
+      }
+      if (!dev_segs.empty()) copy_segments(dev_segs, st);
+      if (has_device_) HIP_OK(hipStreamSynchronize(st));
+    } else {
+      // via host bounce buffer (file tiers)
+      bounce.resize(len);
+      plan_block_range(src_snap, 0, len, (uint64_t)bounce.data(), (int)MemKind::kHost, false, dev_segs, st);
+      if (has_device_) HIP_OK(hipStreamSynchronize(st));
+      if (dd.spec.kind == DirKind::kFile) {
+        std::string fin;
+        file_path(dd, block_id, fin);
+        int fd = ::open(fin.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+        if (fd < 0) throw StoreError(kErrIo, "cannot create " + fin);
+        ssize_t w = ::pwrite(fd, bounce.data(), len, 0);
+        ::close(fd);
+        if (w != (ssize_t)len) throw StoreError(kErrIo, "short write to " + fin);
+      } else {
+        plan_block_range(nb, 0, len, (uint64_t)bounce.data(), (int)MemKind::kHost, true, dev_segs, st);
+        if (!dev_segs.empty()) copy_segments(dev_segs, st);
+        if (has_device_) HIP_OK(hipStreamSynchronize(st));
+      }
+    }
+  } catch (...) {
+    lk.lock();
+    release_storage(nb);
+    BlockMeta* bb = find(block_id);
+    if (bb) bb->writer = false;
+    lock_cv_.notify_all();
+    throw;
+  }
+  lk.lock();
+  b = find(block_id);
+  // swap storage
+  BlockMeta old = *b;
+  old.temp = false;
+  release_storage(old);
+  b->dir = d;
+  b->pages = nb.pages;
+  b->reserved = nb.reserved;
+  b->writer = false;
+  dirs_[d]->committed_bytes += len;
+  if (dd.spec.kind == DirKind::kFile) dd.file_used += 0;  // reserved already counted by grow_pages
+  emit(2, *b);
+  lock_cv_.notify_all();
+  return d;
+}
+
+// -------------------------------------------------------------------------------------------
+// locks
+int64_t BlockStore::lock_block(int64_t session, int64_t block_id, bool write, int64_t timeout_ms) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
+  while (true) {
+    BlockMeta* b = find(block_id);
+    if (!b || b->temp) throw StoreError(kErrNotFound, "block " + std::to_string(block_id) + " does not exist");
+    const bool ok = write ? (b->readers == 0 && !b->writer) : !b->writer;
+    if (ok && !b->evicting) {
+      if (write) b->writer = true; else ++b->readers;
+      const int64_t id = next_lock_++;
+      locks_[id] = LockRec{block_id, session, write};
+      session_locks_[session].insert(id);
+      return id;
+    }
+    if (timeout_ms < 0) {
+      lock_cv_.wait(lk);
+    } else if (lock_cv_.wait_until(lk, deadline) == std::cv_status::timeout) {
+      return -1;
+    }
+  }
+}
+
+void BlockStore::unlock(int64_t lock_id) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto it = locks_.find(lock_id);
+  if (it == locks_.end()) throw StoreError(kErrNotFound, "lock " + std::to_string(lock_id) + " not held");
+  BlockMeta* b = find(it->second.block);
+  if (b) {
+    if (it->second.write) b->writer = false; else if (b->readers > 0) --b->readers;
+  }
+  auto sit = session_locks_.find(it->second.session);
+  if (sit != session_locks_.end()) {
+    sit->second.erase(lock_id);
+    if (sit->second.empty()) session_locks_.erase(sit);
+  }
+  locks_.erase(it);
+  lock_cv_.notify_all();
+}
+
+void BlockStore::cleanup_session(int64_t session) {
+  std::vector<int64_t> lock_ids, temps;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto sit = session_locks_.find(session);
+    if (sit != session_locks_.end()) lock_ids.assign(sit->second.begin(), sit->second.end());
+    auto tit = session_temps_.find(session);
+    if (tit != session_temps_.end()) temps.assign(tit->second.begin(), tit->second.end());
+  }
+  for (int64_t l : lock_ids) {
+    try { unlock(l); } catch (const StoreError&) {}
+  }
+  for (int64_t t : temps) {
+    try { abort_block(session, t); } catch (const StoreError&) {}
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  session_temps_.erase(session);
+}
+
+void BlockStore::access_block(int64_t session, int64_t block_id) {
+  (void)session;
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(block_id);
+  if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(block_id) + " does not exist");
+  touch_slot(b->slot);
+}
+
+void BlockStore::access_blocks(const std::vector<int64_t>& ids) {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (int64_t id : ids) {
+    BlockMeta* b = find(id);
+    if (b) touch_slot(b->slot);
+  }
+}
+
+void BlockStore::set_pinned_files(const std::vector<int64_t>& file_ids) {
+  std::unique_lock<std::mutex> lk(mu_);
+  pinned_files_.clear();
+  pinned_files_.insert(file_ids.begin(), file_ids.end());
+}
+
+// -------------------------------------------------------------------------------------------
+// data plane
+void BlockStore::plan_block_range(const BlockMeta& b, uint64_t offset, uint64_t len, uint64_t ext,
+                                  int ext_kind, bool to_block, std::vector<CopySeg>& dev_segs,
+                                  hipStream_t stream) {
+  const StorageDir& d = *dirs_[b.dir];
+  const bool ext_dev = ext_kind == (int)MemKind::kDevice;
+  if (d.spec.kind == DirKind::kFile) {
+    std::string p;
+    if (b.temp) p = d.spec.path + "/.tmp_blocks/" + std::to_string(b.session) + "-" + std::to_string(b.id);
+    else file_path(d, b.id, p);
+    int fd = ::open(p.c_str(), to_block ? O_WRONLY : O_RDONLY);
+    if (fd < 0) throw StoreError(kErrIo, "cannot open block file " + p);
+    std::vector<uint8_t> bounce;
+    uint8_t* host = reinterpret_cast<uint8_t*>(ext);
+    if (ext_dev) {
+      bounce.resize(len);
+      host = bounce.data();
+      if (to_block) {
+        hipError_t e = hipMemcpy(host, reinterpret_cast<void*>(ext), len, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) { ::close(fd); HIP_OK(e); }
+      }
+    }
+    uint64_t done = 0;
+    while (done < len) {
+      ssize_t r = to_block ? ::pwrite(fd, host + done, len - done, offset + done)
+                           : ::pread(fd, host + done, len - done, offset + done);
+      if (r <= 0) { ::close(fd); throw StoreError(kErrIo, "block file I/O failed on " + p); }
+      done += (uint64_t)r;
+    }
+    ::close(fd);
+    if (ext_dev && !to_block) HIP_OK(hipMemcpy(reinterpret_cast<void*>(ext), host, len, hipMemcpyHostToDevice));
+    return;
+  }
+  const uint64_t ps = d.spec.page_size;
+  const bool arena_dev = d.spec.kind == DirKind::kDevice;
+  uint64_t pos = offset, done = 0;
+  while (done < len) {
+    const size_t pi = (size_t)(pos / ps);
+    if (pi >= b.pages.size()) throw StoreError(kErrInvalidArgument, "range beyond block reservation");
+    uint64_t in_page = pos % ps;
+    // merge physically contiguous pages into one segment
+    size_t pj = pi + 1;
+    while (pj < b.pages.size() && b.pages[pj] == b.pages[pj - 1] + 1) ++pj;
+    const uint64_t run_bytes = (uint64_t)(pj - pi) * ps - in_page;
+    const uint64_t n = std::min(run_bytes, len - done);
+    const uint64_t arena_addr = d.spec.base + (uint64_t)b.pages[pi] * ps + in_page;
+    const uint64_t ext_addr = ext + done;
+    const uint64_t src = to_block ? ext_addr : arena_addr;
+    const uint64_t dst = to_block ? arena_addr : ext_addr;
+    if (arena_dev && ext_dev) {
+      dev_segs.push_back(CopySeg{src, dst, n, 0});
+    } else if (!arena_dev && !ext_dev) {
+      std::memcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n);
+    } else {
+      const hipMemcpyKind kind = to_block ? (arena_dev ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost)
+                                          : (arena_dev ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice);
+      HIP_OK(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, kind, stream));
+    }
+    pos += n;
+    done += n;
+  }
+}
+
+void BlockStore::copy_segments(std::vector<CopySeg>& segs, hipStream_t stream) {
+  std::lock_guard<std::mutex> g(ring_mu_);
+  size_t base = 0;
+  while (base < segs.size()) {
+    const size_t cnt = std::min<size_t>(segs.size() - base, kRingSegs);
+    const int slot = ring_pos_;
+    ring_pos_ = (ring_pos_ + 1) % kRing;
+    HIP_OK(hipEventSynchronize(ring_ev_[slot]));
+    CopySeg* h = host_ring_ + (size_t)slot * kRingSegs;
+    CopySeg* dv = dev_ring_ + (size_t)slot * kRingSegs;
+    uint64_t chunks = 0;
+    for (size_t i = 0; i < cnt; ++i) {
+      h[i] = segs[base + i];
+      h[i].chunk0 = chunks;
+      chunks += ceil_div(h[i].bytes, kCopyChunk);
+    }
+    HIP_OK(hipMemcpyAsync(dv, h, sizeof(CopySeg) * cnt, hipMemcpyHostToDevice, stream));
+    HIP_OK(launch_batched_copy(dv, (int)cnt, chunks, stream));
+    HIP_OK(hipEventRecord(ring_ev_[slot], stream));
+    base += cnt;
+  }
+  segs.clear();
+}
+
+void BlockStore::read_batch(const std::vector<ReadReq>& reqs, uint64_t stream, bool sync) {
+  set_device();
+  hipStream_t st = stream_or_default(stream);
+  std::vector<CopySeg> dev_segs;
+  dev_segs.reserve(reqs.size() * 2);
+  // Snapshot the (small) page lists under the lock; callers hold block read locks, so the
+  // pages cannot be released while the copies are in flight.
+  std::vector<BlockMeta> snaps;
+  snaps.reserve(reqs.size());
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (const auto& r : reqs) {
+      BlockMeta* b = find(r.block_id);
+      if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(r.block_id) + " does not exist");
+      if (r.offset + r.length > b->length)
+        throw StoreError(kErrInvalidArgument, "read [" + std::to_string(r.offset) + ", +" +
+                                                  std::to_string(r.length) + ") beyond block length " +
+                                                  std::to_string(b->length));
+      snaps.push_back(*b);
+    }
+  }
+  for (size_t i = 0; i < reqs.size(); ++i)
+    plan_block_range(snaps[i], reqs[i].offset, reqs[i].length, reqs[i].dst, reqs[i].dst_kind, false,
+                     dev_segs, st);
+  if (!dev_segs.empty()) copy_segments(dev_segs, st);
+  if (sync && has_device_) HIP_OK(hipStreamSynchronize(st));
+}
+
+std::vector<uint32_t> BlockStore::checksum(int64_t block_id, uint64_t piece_bytes) {
+  set_device();
+  BlockMeta snap;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    BlockMeta* b = find(block_id);
+    if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(block_id) + " does not exist");
+    snap = *b;
+  }
+  const StorageDir& d = *dirs_[snap.dir];
+  const uint64_t ps = d.spec.kind == DirKind::kFile ? (piece_bytes ? piece_bytes : (2ull << 20)) : d.spec.page_size;
+  if (piece_bytes == 0) piece_bytes = ps;
+  if (d.spec.kind != DirKind::kFile && ps % piece_bytes != 0)
+    throw StoreError(kErrInvalidArgument, "piece size must divide the page size");
+  const uint64_t len = snap.length;
+  std::vector<uint32_t> out(len ? ceil_div(len, piece_bytes) : 0);
+  if (len == 0) return out;
+  if (d.spec.kind != DirKind::kDevice) {
+    std::vector<uint8_t> buf(len);
+    std::vector<CopySeg> none;
+    plan_block_range(snap, 0, len, (uint64_t)buf.data(), (int)MemKind::kHost, false, none, internal_stream_);
+    for (size_t i = 0; i < out.size(); ++i) {
+      const uint64_t o = i * piece_bytes;
+      out[i] = crc32c_sw(buf.data() + o, std::min(piece_bytes, len - o));
+    }
+    return out;
+  }
+  std::lock_guard<std::mutex> g(ev_mu_);
+  const size_t need = out.size() + crc32c_scratch_words(len, piece_bytes) + 64;
+  if (crc_cap_ < need) {
+    if (crc_dev_) hipFree(crc_dev_);
+    crc_dev_ = nullptr;
+    HIP_OK(hipMalloc((void**)&crc_dev_, need * sizeof(uint32_t)));
+    crc_cap_ = need;
+  }
+  // contiguous page runs, each a whole number of pieces
+  uint64_t off = 0;
+  size_t i = 0, piece_idx = 0;
+  while (off < len) {
+    size_t j = i + 1;
+    while (j < snap.pages.size() && snap.pages[j] == snap.pages[j - 1] + 1) ++j;
+    const uint64_t run = std::min<uint64_t>((j - i) * ps, len - off);
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(d.spec.base + (uint64_t)snap.pages[i] * ps);
+    const uint64_t np = ceil_div(run, piece_bytes);
+    uint32_t* scratch = crc_dev_ + out.size();
+    HIP_OK(launch_crc32c_pieces(base, run, piece_bytes, crc_dev_ + piece_idx, scratch,
+                                crc_cap_ - out.size(), internal_stream_));
+    piece_idx += np;
+    off += run;
+    i = j;
+  }
+  HIP_OK(hipMemcpyAsync(out.data(), crc_dev_, out.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, internal_stream_));
+  HIP_OK(hipStreamSynchronize(internal_stream_));
+  return out;
+}
+
+void BlockStore::fill_pattern(int64_t session, int64_t block_id, uint64_t length, uint64_t seed) {
+  set_device();
+  BlockMeta snap;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    BlockMeta* b = find(block_id);
+    if (!b || !b->temp || b->session != session) throw StoreError(kErrNotFound, "temp block not found");
+    if (length > b->reserved) {
+      lk.unlock();
+      request_space(session, block_id, length - b->reserved);
+      lk.lock();
+      b = find(block_id);
+    }
+    b->length = std::max(b->length, length);
+    snap = *b;
+  }
+  const StorageDir& d = *dirs_[snap.dir];
+  if (d.spec.kind != DirKind::kDevice) throw StoreError(kErrInvalidArgument, "fill_pattern needs a device dir");
+  uint64_t off = 0;
+  size_t i = 0;
+  const uint64_t ps = d.spec.page_size;
+  while (off < length) {
+    size_t j = i + 1;
+    while (j < snap.pages.size() && snap.pages[j] == snap.pages[j - 1] + 1) ++j;
+    const uint64_t run = std::min<uint64_t>((j - i) * ps, length - off);
+    uint8_t* base = reinterpret_cast<uint8_t*>(d.spec.base + (uint64_t)snap.pages[i] * ps);
+    HIP_OK(launch_fill_pattern(base, run, seed, off >> 3, internal_stream_));
+    off += run;
+    i = j;
+  }
+  HIP_OK(hipStreamSynchronize(internal_stream_));
+}
+
+// -------------------------------------------------------------------------------------------
+// eviction
+std::vector<uint32_t> BlockStore::select_victims(const std::vector<uint32_t>& cand, uint64_t need) {
+  const size_t n = cand.size();
+  std::vector<uint32_t> picked;
+  if (n == 0 || need == 0) return picked;
+  const uint64_t now = clock_.load();
+  std::vector<uint64_t> bytes(n);
+  for (size_t i = 0; i < n; ++i) {
+    const BlockMeta* b = find(slot_block_[cand[i]]);
+    bytes[i] = b ? b->length : 0;
+  }
+  if (has_device_ && use_device_evict_) {
+    std::lock_guard<std::mutex> g(ev_mu_);
+    set_device();
+    // layout: crf f32[n] | last u64[n] | bytes u64[n] | evictable u8[n] | keys u32[n] | out u32[n] | cnt | freed
+    const size_t off_last = ((n * 4 + 15) / 16) * 16;
+    const size_t off_bytes = off_last + n * 8;
+    const size_t off_ev = off_bytes + n * 8;
+    const size_t off_keys = ((off_ev + n + 15) / 16) * 16;
+    const size_t off_out = off_keys + n * 4;
+    const size_t off_cnt = ((off_out + n * 4 + 15) / 16) * 16;
+    const size_t total = off_cnt + 32;
+    if (ev_cap_ < total) {
+      if (ev_dev_) hipFree(ev_dev_);
+      ev_dev_ = nullptr;
+      HIP_OK(hipMalloc(&ev_dev_, total));
+      ev_cap_ = total;
+    }
+    std::vector<uint8_t> host(off_keys, 0);
+    float* hc = reinterpret_cast<float*>(host.data());
+    uint64_t* hl = reinterpret_cast<uint64_t*>(host.data() + off_last);
+    uint64_t* hb = reinterpret_cast<uint64_t*>(host.data() + off_bytes);
+    uint8_t* he = host.data() + off_ev;
+    for (size_t i = 0; i < n; ++i) {
+      hc[i] = crf_[cand[i]];
+      hl[i] = last_[cand[i]];
+      hb[i] = bytes[i];
+      he[i] = 1;
+    }
+    uint8_t* dv = static_cast<uint8_t*>(ev_dev_);
+    HIP_OK(hipMemcpyAsync(dv, host.data(), off_keys, hipMemcpyHostToDevice, internal_stream_));
+    EvictInput in;
+    in.crf = reinterpret_cast<const float*>(dv);
+    in.last = reinterpret_cast<const uint64_t*>(dv + off_last);
+    in.bytes = reinterpret_cast<const uint64_t*>(dv + off_bytes);
+    in.evictable = dv + off_ev;
+    in.n = (uint32_t)n;
+    in.now = now;
+    in.step_factor = lrfu_step_;
+    in.attenuation = lrfu_att_;
+    in.policy = annotator_ == Annotator::kLRFU ? 1 : 0;
+    in.need_bytes = need;
+    HIP_OK(launch_evict_select(in, reinterpret_cast<uint32_t*>(dv + off_keys),
+                               reinterpret_cast<uint32_t*>(dv + off_out),
+                               reinterpret_cast<uint32_t*>(dv + off_cnt),
+                               reinterpret_cast<uint64_t*>(dv + off_cnt + 8), internal_stream_));
+    uint32_t count = 0;
+    HIP_OK(hipMemcpyAsync(&count, dv + off_cnt, 4, hipMemcpyDeviceToHost, internal_stream_));
+    HIP_OK(hipStreamSynchronize(internal_stream_));
+    std::vector<uint32_t> idx(count);
+    if (count) {
+      HIP_OK(hipMemcpyAsync(idx.data(), dv + off_out, count * 4, hipMemcpyDeviceToHost, internal_stream_));
+      HIP_OK(hipStreamSynchronize(internal_stream_));
+    }
+    for (uint32_t k : idx) picked.push_back(cand[k]);
+    return picked;
+  }
+  // CPU path: identical keys, full sort
+  std::vector<std::pair<uint32_t, uint32_t>> keyed(n);
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t s = cand[i];
+    const uint64_t age = now > last_[s] ? now - last_[s] : 0;
+    uint32_t key;
+    if (annotator_ == Annotator::kLRU) {
+      key = 0xFFFFFFFEu - (uint32_t)std::min<uint64_t>(age, 0xFFFFFFFEull);
+    } else {
+      float crf = crf_[s] * std::pow(1.0f / lrfu_att_, (float)age * lrfu_step_);
+      if (!(crf >= 0.f)) crf = 0.f;
+      std::memcpy(&key, &crf, 4);
+      if (key >= 0xFFFFFFFEu) key = 0xFFFFFFFDu;
+    }
+    keyed[i] = {key, (uint32_t)i};
+  }
+  std::sort(keyed.begin(), keyed.end());
+  uint64_t got = 0;
+  for (auto& kv : keyed) {
+    if (got >= need) break;
+    picked.push_back(cand[kv.second]);
+    got += bytes[kv.second];
+  }
+  return picked;
+}
+
+void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
+                                   int tier, int dir, const std::string& medium) {
+  (void)session;
+  (void)lk;
+  // choose the target dir: the one that can reach `bytes` with the most (available + evictable)
+  int target = -1;
+  uint64_t best = 0;
+  std::vector<uint64_t> ev_bytes(dirs_.size(), 0);
+  for (auto& kv : blocks_)
+    if (evictable(kv.second)) ev_bytes[kv.second.dir] += kv.second.length;
+  for (auto& d : dirs_) {
+    if (dir >= 0 && d->index != dir) continue;
+    if (!dir_matches(*d, tier, medium)) continue;
+    const uint64_t reach = d->available() + ev_bytes[d->index];
+    if (target < 0 || reach > best) { target = d->index; best = reach; }
+  }
+  if (target < 0) throw StoreError(kErrOutOfSpace, "no storage dir matches the eviction location");
+  StorageDir& td = *dirs_[target];
+  if (td.available() >= bytes) return;
+  // arena dirs free whole pages: convert the shortfall into page-rounded bytes
+  uint64_t need = bytes - td.available();
+  if (td.spec.kind != DirKind::kFile) need = ceil_div(need, td.spec.page_size) * td.spec.page_size;
+  std::vector<uint32_t> cand;
+  for (auto& kv : blocks_)
+    if (kv.second.dir == target && evictable(kv.second)) cand.push_back(kv.second.slot);
+  // page-rounded victim sizes: a block frees ceil(len/page) pages
+  std::vector<uint32_t> victims = select_victims(cand, need);
+  for (uint32_t s : victims) {
+    BlockMeta* b = find(slot_block_[s]);
+    if (b && evictable(*b)) remove_locked(*b, true);
+  }
+  if (td.available() < bytes)
+    throw StoreError(kErrOutOfSpace, "failed to free " + std::to_string(bytes) + " bytes in dir " +
+                                         std::to_string(target) + " (available " +
+                                         std::to_string(td.available()) + ")");
+}
+
+std::vector<int64_t> BlockStore::free_space(int64_t session, uint64_t bytes, int tier, int dir) {
+  set_device();
+  std::unique_lock<std::mutex> lk(mu_);
+  std::unordered_set<int64_t> before;
+  for (auto& kv : blocks_) before.insert(kv.first);
+  free_space_locked(lk, session, bytes, tier, dir, "");
+  std::vector<int64_t> gone;
+  for (int64_t id : before)
+    if (!blocks_.count(id)) gone.push_back(id);
+  return gone;
+}
+
+std::vector<int64_t> BlockStore::eviction_order(int tier, uint64_t need_bytes) {
+  std::unique_lock<std::mutex> lk(mu_);
+  std::vector<uint32_t> cand;
+  for (auto& kv : blocks_)
+    if ((tier < 0 || dirs_[kv.second.dir]->spec.tier == tier) && evictable(kv.second)) cand.push_back(kv.second.slot);
+  if (need_bytes == 0) need_bytes = ~0ull;
+  std::vector<uint32_t> v = select_victims(cand, need_bytes);
+  std::vector<int64_t> out;
+  out.reserve(v.size());
+  for (uint32_t s : v) out.push_back(slot_block_[s]);
+  return out;
+}
+
+// -------------------------------------------------------------------------------------------
+// introspection
+bool BlockStore::has_block(int64_t id) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(id);
+  return b && !b->temp;
+}
+
+bool BlockStore::has_temp_block(int64_t id) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(id);
+  return b && b->temp;
+}
+
+BlockInfoOut BlockStore::block_info(int64_t id) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(id);
+  if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(id) + " does not exist");
+  const auto& s = dirs_[b->dir]->spec;
+  return BlockInfoOut{b->id, b->length, s.tier, b->dir, s.tier_alias, s.medium, b->temp, b->session,
+                      b->readers, b->writer};
+}
+
+std::vector<int64_t> BlockStore::block_ids(int tier) {
+  std::unique_lock<std::mutex> lk(mu_);
+  std::vector<int64_t> out;
+  for (auto& kv : blocks_)
+    if (!kv.second.temp && (tier < 0 || dirs_[kv.second.dir]->spec.tier == tier)) out.push_back(kv.first);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+std::vector<int64_t> BlockStore::block_pages(int64_t id, int* dir_out, uint64_t* ps_out, uint64_t* base_out) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(id);
+  if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(id) + " does not exist");
+  const auto& s = dirs_[b->dir]->spec;
+  *dir_out = b->dir;
+  *ps_out = s.page_size;
+  *base_out = s.base;
+  return b->pages;
+}
+
+std::vector<Event> BlockStore::drain_events() {
+  std::unique_lock<std::mutex> lk(mu_);
+  std::vector<Event> out;
+  out.swap(events_);
+  return out;
+}
+
+uint64_t BlockStore::dir_capacity(int d) {
+  std::unique_lock<std::mutex> lk(mu_);
+  return dirs_.at(d)->capacity();
+}
+uint64_t BlockStore::dir_available(int d) {
+  std::unique_lock<std::mutex> lk(mu_);
+  return dirs_.at(d)->available();
+}
+uint64_t BlockStore::dir_committed(int d) {
+  std::unique_lock<std::mutex> lk(mu_);
+  return dirs_.at(d)->committed_bytes;
+}
+void BlockStore::set_dir_healthy(int d, bool healthy) {
+  std::unique_lock<std::mutex> lk(mu_);
+  dirs_.at(d)->healthy = healthy;
+}
+bool BlockStore::dir_healthy(int d) {
+  std::unique_lock<std::mutex> lk(mu_);
+  return dirs_.at(d)->healthy;
+}
+
+std::string BlockStore::stats() {
+  std::unique_lock<std::mutex> lk(mu_);
+  std::ostringstream os;
+  os << "{\"blocks\":" << blocks_.size() << ",\"locks\":" << locks_.size() << ",\"clock\":" << clock_.load()
+     << ",\"dirs\":[";
+  for (size_t i = 0; i < dirs_.size(); ++i) {
+    const auto& d = *dirs_[i];
+    os << (i ? "," : "") << "{\"tier\":" << d.spec.tier << ",\"alias\":\"" << d.spec.tier_alias
+       << "\",\"medium\":\"" << d.spec.medium << "\",\"capacity\":" << d.capacity()
+       << ",\"available\":" << d.available() << ",\"committed\":" << d.committed_bytes << "}";
+  }
+  os << "]}";
+  return os.str();
+}
+
+}  // namespace amdx

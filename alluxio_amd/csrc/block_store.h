@@ -1,0 +1,259 @@
+// Native tiered block store for one worker (= one MI355X).
+//
+// Re-designs the reference TieredBlockStore (core/server/worker/src/main/java/alluxio/worker/
+// block/TieredBlockStore.java:85-1009) around page arenas:
+//   * tier 0 ("MEM", medium HBM) is a hipMalloc arena on the worker's GPU cut into fixed pages
+//     (default 2 MiB); a block is a list of pages, normally one contiguous run;
+//   * further tiers are pinned-host arenas (medium DRAM) or file directories (SSD/HDD);
+//   * allocation = host bitmap scan for a contiguous run, falling back to scattered pages
+//     (reference MaxFree/Greedy/RoundRobin allocators choose the dir, allocator/*.java);
+//   * eviction ordering = LRU or LRFU annotations (annotator/LRFUAnnotator.java:81-95) scored and
+//     selected on the GPU by a fused radix-select kernel (kernels.hip, evict_select_kernel);
+//   * reads/writes are planned into page-contiguous segments and executed by one batched copy
+//     kernel launch per batch (kernels.hip, batched_copy_kernel) or by DMA for host endpoints.
+// Block locks (BlockLockManager.java), sessions (Sessions.java) and temp->committed lifecycle
+// (createBlock/commitBlock/abortBlock) keep the reference semantics.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "kernels.h"
+
+namespace amdx {
+
+struct StoreError : std::runtime_error {
+  int code;
+  StoreError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+// error codes mirrored in Python (alluxio_amd/ops/native.py)
+enum ErrCode {
+  kErrNotFound = 1,
+  kErrAlreadyExists = 2,
+  kErrOutOfSpace = 3,
+  kErrInvalidState = 4,
+  kErrHip = 5,
+  kErrInvalidArgument = 6,
+  kErrIo = 7,
+  kErrTimeout = 8,
+};
+
+enum class DirKind : int { kDevice = 0, kHost = 1, kFile = 2 };
+enum class MemKind : int { kHost = 0, kDevice = 1 };
+enum class AllocPolicy : int { kMaxFree = 0, kGreedy = 1, kRoundRobin = 2 };
+enum class Annotator : int { kLRU = 0, kLRFU = 1 };
+
+struct DirSpec {
+  int tier = 0;
+  std::string tier_alias = "MEM";
+  std::string medium = "HBM";
+  DirKind kind = DirKind::kDevice;
+  uint64_t base = 0;       // arena base (device or host pointer) for arena kinds
+  uint64_t capacity = 0;   // bytes
+  uint64_t page_size = 2ull << 20;
+  int device = 0;
+  std::string path;        // file dirs
+  uint64_t reserved = 0;   // reserved bytes (watermark headroom) not used by allocation
+};
+
+struct StorageDir {
+  DirSpec spec;
+  int index = 0;  // global dir index
+  int64_t num_pages = 0;
+  std::vector<uint64_t> free_bits;  // arena kinds: 1 = free
+  int64_t free_pages = 0;
+  uint64_t file_used = 0;  // file dirs: bytes reserved
+  uint64_t committed_bytes = 0;
+  bool healthy = true;
+  uint64_t available() const;
+  uint64_t capacity() const;
+};
+
+struct BlockMeta {
+  int64_t id = 0;
+  int dir = -1;
+  uint64_t length = 0;     // bytes written (temp) / final length (committed)
+  uint64_t reserved = 0;   // bytes reserved (>= length)
+  std::vector<int64_t> pages;
+  bool temp = true;
+  int64_t session = 0;
+  bool pinned_on_create = false;
+  int readers = 0;
+  bool writer = false;
+  bool evicting = false;
+  uint32_t slot = 0;
+  std::vector<uint32_t> crc;
+  uint64_t crc_piece = 0;
+};
+
+struct ReadReq {
+  int64_t block_id;
+  uint64_t offset;
+  uint64_t length;
+  uint64_t dst;
+  int dst_kind;  // MemKind
+};
+
+struct BlockInfoOut {
+  int64_t id;
+  uint64_t length;
+  int tier;
+  int dir;
+  std::string tier_alias;
+  std::string medium;
+  bool temp;
+  int64_t session;
+  int readers;
+  bool writer;
+};
+
+struct Event {
+  int kind;  // 0 added/committed, 1 removed, 2 moved
+  int64_t block_id;
+  std::string tier_alias;
+  std::string medium;
+};
+
+class BlockStore {
+ public:
+  BlockStore(const std::vector<DirSpec>& dirs, int annotator, int alloc_policy, float lrfu_step,
+             float lrfu_attenuation, int device);
+  ~BlockStore();
+
+  // ---- lifecycle --------------------------------------------------------------------------
+  // Creates a temp block with `initial` reserved bytes.  tier < 0 = any tier (top-down),
+  // medium non-empty selects dirs of that medium.  Evicts if allowed and needed.
+  int create_block(int64_t session, int64_t block_id, int tier, const std::string& medium,
+                   uint64_t initial, bool evict, bool pin);
+  void request_space(int64_t session, int64_t block_id, uint64_t additional);
+  // Append/overwrite bytes of a temp block (auto-grows).  src_kind: MemKind.
+  void write(int64_t session, int64_t block_id, uint64_t offset, uint64_t src, uint64_t len,
+             int src_kind, uint64_t stream, bool sync);
+  void commit_block(int64_t session, int64_t block_id, bool pin);
+  void abort_block(int64_t session, int64_t block_id);
+  void remove_block(int64_t session, int64_t block_id);
+  // move a committed block to another tier/medium; returns new dir index
+  int move_block(int64_t session, int64_t block_id, int dst_tier, const std::string& medium,
+                 bool evict);
+
+  // ---- locks / sessions -------------------------------------------------------------------
+  int64_t lock_block(int64_t session, int64_t block_id, bool write, int64_t timeout_ms);
+  void unlock(int64_t lock_id);
+  void cleanup_session(int64_t session);
+  void access_block(int64_t session, int64_t block_id);
+  void access_blocks(const std::vector<int64_t>& ids);
+
+  // ---- data plane -------------------------------------------------------------------------
+  // Batched read of committed (or own temp) blocks into caller buffers.  Device-arena ->
+  // device-dst segments are executed by one batched copy launch per ring slot.
+  void read_batch(const std::vector<ReadReq>& reqs, uint64_t stream, bool sync);
+  // CRC32C per piece (piece = page size when 0).
+  std::vector<uint32_t> checksum(int64_t block_id, uint64_t piece_bytes);
+  void fill_pattern(int64_t session, int64_t block_id, uint64_t length, uint64_t seed);
+
+  // ---- eviction ---------------------------------------------------------------------------
+  // Free at least `bytes` in the location (tier < 0 = all tiers, dir >= 0 pins one dir).
+  // Returns evicted block ids; throws OutOfSpace when impossible.
+  std::vector<int64_t> free_space(int64_t session, uint64_t bytes, int tier, int dir);
+  // The annotator's eviction order of up to `limit` evictable blocks in a tier (for tests and
+  // tier management), computed by the same kernel/CPU path.
+  std::vector<int64_t> eviction_order(int tier, uint64_t need_bytes);
+  void set_pinned_files(const std::vector<int64_t>& file_ids);
+  void set_use_device_evict(bool v) { use_device_evict_ = v; }
+
+  // ---- introspection ----------------------------------------------------------------------
+  bool has_block(int64_t block_id);
+  bool has_temp_block(int64_t block_id);
+  BlockInfoOut block_info(int64_t block_id);
+  std::vector<int64_t> block_ids(int tier);
+  std::vector<int64_t> block_pages(int64_t block_id, int* dir_out, uint64_t* page_size_out,
+                                   uint64_t* base_out);
+  std::vector<Event> drain_events();
+  int num_dirs() const { return (int)dirs_.size(); }
+  DirSpec dir_spec(int d) const { return dirs_.at(d)->spec; }
+  uint64_t dir_capacity(int d);
+  uint64_t dir_available(int d);
+  uint64_t dir_committed(int d);
+  void set_dir_healthy(int d, bool healthy);
+  bool dir_healthy(int d);
+  uint64_t clock() const { return clock_.load(); }
+  int device() const { return device_; }
+  std::string stats();
+
+ private:
+  BlockMeta& get_committed(int64_t id);
+  BlockMeta* find(int64_t id);
+  int allocate_dir(int tier, const std::string& medium, uint64_t bytes);
+  bool dir_matches(const StorageDir& d, int tier, const std::string& medium) const;
+  bool grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved);
+  void release_storage(BlockMeta& b);
+  void free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
+                         int tier, int dir, const std::string& medium);
+  std::vector<uint32_t> select_victims(const std::vector<uint32_t>& cand_slots, uint64_t need);
+  void remove_locked(BlockMeta& b, bool emit_event);
+  uint32_t alloc_slot();
+  void touch_slot(uint32_t slot);
+  bool evictable(const BlockMeta& b) const;
+  void emit(int kind, const BlockMeta& b);
+  void copy_segments(std::vector<CopySeg>& dev_segs, hipStream_t stream);
+  void plan_block_range(const BlockMeta& b, uint64_t offset, uint64_t len, uint64_t ext,
+                        int ext_kind, bool to_block, std::vector<CopySeg>& dev_segs,
+                        hipStream_t stream);
+  void file_path(const StorageDir& d, int64_t id, std::string& out) const;
+  void set_device() const;
+  hipStream_t stream_or_default(uint64_t s) const;
+
+  std::mutex mu_;
+  std::condition_variable lock_cv_;
+  std::vector<std::unique_ptr<StorageDir>> dirs_;
+  std::unordered_map<int64_t, BlockMeta> blocks_;
+  std::unordered_set<int64_t> pinned_files_;
+  // lock table
+  struct LockRec { int64_t block; int64_t session; bool write; };
+  std::unordered_map<int64_t, LockRec> locks_;
+  std::unordered_map<int64_t, std::unordered_set<int64_t>> session_locks_;
+  std::unordered_map<int64_t, std::unordered_set<int64_t>> session_temps_;
+  int64_t next_lock_ = 1;
+  // annotator SoA (slot-indexed)
+  Annotator annotator_;
+  AllocPolicy alloc_policy_;
+  float lrfu_step_, lrfu_att_;
+  std::vector<float> crf_;
+  std::vector<uint64_t> last_;
+  std::vector<int64_t> slot_block_;
+  std::vector<uint32_t> free_slots_;
+  std::atomic<uint64_t> clock_{0};
+  std::vector<int> rr_index_;  // round-robin cursor per tier
+  std::vector<Event> events_;
+  // device resources
+  int device_ = -1;
+  bool has_device_ = false;
+  bool use_device_evict_ = true;
+  hipStream_t internal_stream_ = nullptr;
+  static constexpr int kRing = 8;
+  static constexpr int kRingSegs = 8192;
+  CopySeg* host_ring_ = nullptr;   // pinned
+  CopySeg* dev_ring_ = nullptr;
+  hipEvent_t ring_ev_[kRing] = {};
+  int ring_pos_ = 0;
+  std::mutex ring_mu_;
+  // eviction kernel scratch (grown on demand)
+  size_t ev_cap_ = 0;
+  void* ev_dev_ = nullptr;
+  std::mutex ev_mu_;
+  // checksum scratch
+  uint32_t* crc_dev_ = nullptr;
+  size_t crc_cap_ = 0;
+};
+
+}  // namespace amdx

@@ -1,0 +1,78 @@
+// Host-side launch interface of the CDNA4 (gfx950) kernels used by the worker data plane.
+//
+// Reference hot loops these replace:
+//   K1/K2  block read/write chunk copy   W/grpc/BlockReadHandler.java:124-130, BlockWriteHandler.java:124-149
+//   K4-K6  LRU/LRFU ordering + free-space loop  W/block/annotator/LRFUAnnotator.java:81-95,
+//          W/block/TieredBlockStore.java:740-815
+//   K10    CRC32C (new; reference only has whole-file MD5 in ChecksumCommand.java:78-88)
+//   K11    LZ4 block codec (new)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace amdx {
+
+// One contiguous copy piece (never crosses a page boundary on the arena side).
+struct CopySeg {
+  uint64_t src;      // byte address (device or host-pinned mapped)
+  uint64_t dst;      // byte address
+  uint64_t bytes;
+  uint64_t chunk0;   // exclusive prefix of chunk counts (filled by the planner)
+};
+
+// Tile (bytes) one workgroup moves per work item of the batched copy.
+constexpr uint64_t kCopyChunk = 256 * 1024;
+
+// Batched gather/scatter copy.  `segs` must be device-visible; `total_chunks` = sum of
+// ceil(bytes / kCopyChunk).  Grid is capped and grid-strided.
+hipError_t launch_batched_copy(const CopySeg* segs, int nseg, uint64_t total_chunks,
+                               hipStream_t stream);
+
+// CRC32C (Castagnoli, reflected, init/xorout 0xFFFFFFFF) of `n` equal-length pieces
+// (piece i = base + i*piece_bytes, last may be shorter: total_bytes).  `out` device array.
+hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint64_t piece_bytes,
+                                uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
+                                hipStream_t stream);
+// Scratch words needed by launch_crc32c_pieces.
+uint64_t crc32c_scratch_words(uint64_t total_bytes, uint64_t piece_bytes);
+
+// LZ4 block decompression of `n` independent chunks.
+struct Lz4Chunk {
+  uint64_t src;       // compressed bytes (device)
+  uint64_t dst;       // output (device)
+  uint32_t src_bytes;
+  uint32_t dst_capacity;
+};
+hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
+                                 hipStream_t stream);
+// LZ4 block compression (greedy, one wave per chunk, LDS hash table).  out_sizes[i] = -1 if
+// the chunk does not fit dst_capacity (caller then stores it raw).
+hipError_t launch_lz4_compress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
+                               hipStream_t stream);
+
+// Eviction candidate selection (fused LRU/LRFU scoring + byte-weighted radix select).
+struct EvictInput {
+  const float* crf;         // LRFU combined recency-frequency (per slot)
+  const uint64_t* last;     // logical access clock (per slot)
+  const uint64_t* bytes;    // block bytes (per slot)
+  const uint8_t* evictable; // 1 if the slot may be evicted (committed, unlocked, unpinned)
+  uint32_t n;
+  uint64_t now;             // current logical clock
+  float step_factor;        // LRFU step
+  float attenuation;        // LRFU attenuation (>1)
+  int policy;               // 0 = LRU, 1 = LRFU
+  uint64_t need_bytes;      // stop once the selected set frees this much
+};
+// Writes selected slots to out_slots (ascending score order is NOT guaranteed) and their count
+// to *out_count; out_bytes receives the bytes freed.
+hipError_t launch_evict_select(const EvictInput& in, uint32_t* keys_scratch,
+                               uint32_t* out_slots, uint32_t* out_count, uint64_t* out_bytes,
+                               hipStream_t stream);
+
+// Fill `bytes` at dst with 64-bit words w[i] = splitmix64(seed ^ ((i + word_offset) * K)):
+// synthetic bench/test data that is a pure function of the byte offset inside a block.
+hipError_t launch_fill_pattern(uint8_t* dst, uint64_t bytes, uint64_t seed, uint64_t word_offset,
+                               hipStream_t stream);
+
+}  // namespace amdx

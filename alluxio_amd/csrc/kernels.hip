@@ -1,0 +1,627 @@
+// CDNA4 (gfx950) kernels for the HBM block store.  Wave64 throughout; all grids grid-stride
+// and are capped so a launch always drains.  See kernels.h for the reference hot loops each
+// kernel replaces.
+#include "kernels.h"
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+namespace amdx {
+
+// ---------------------------------------------------------------------------------------------
+// K1/K2: batched gather/scatter copy.
+//
+// The host planner splits every read/write request into page-contiguous segments (a request
+// never spans a page boundary inside a segment) and computes an exclusive prefix of
+// ceil(bytes / kCopyChunk) per segment.  Each workgroup iteration owns one <=256 KiB chunk: a
+// wave-uniform binary search (scalar loads) finds its segment, then 256 lanes stream the chunk
+// with 16-B loads, 8 in flight per lane (128 B/lane, 32 KiB per workgroup round).
+// ---------------------------------------------------------------------------------------------
+constexpr int kCopyThreads = 256;
+constexpr int kCopyUnroll = 8;
+
+__device__ __forceinline__ void copy_bytes(const uint8_t* __restrict__ s, uint8_t* __restrict__ d,
+                                           uint64_t n, int tid) {
+  for (uint64_t i = tid; i < n; i += kCopyThreads) d[i] = s[i];
+}
+
+__device__ __forceinline__ void copy_range(uint64_t src, uint64_t dst, uint64_t n, int tid) {
+  if (((src | dst) & 15) == 0) {
+    const uint4* __restrict__ s = reinterpret_cast<const uint4*>(src);
+    uint4* __restrict__ d = reinterpret_cast<uint4*>(dst);
+    const uint64_t n16 = n >> 4;
+    uint64_t i = tid;
+    constexpr uint64_t kStep = (uint64_t)kCopyThreads * kCopyUnroll;
+    for (; i + (kCopyUnroll - 1) * kCopyThreads < n16; i += kStep) {
+      uint4 v[kCopyUnroll];
+#pragma unroll
+      for (int u = 0; u < kCopyUnroll; ++u) v[u] = s[i + (uint64_t)u * kCopyThreads];
+#pragma unroll
+      for (int u = 0; u < kCopyUnroll; ++u) d[i + (uint64_t)u * kCopyThreads] = v[u];
+    }
+    for (; i < n16; i += kCopyThreads) d[i] = s[i];
+    const uint64_t done = n16 << 4;
+    if (done < n) copy_bytes(reinterpret_cast<const uint8_t*>(src) + done,
+                             reinterpret_cast<uint8_t*>(dst) + done, n - done, tid);
+  } else if (((src | dst) & 3) == 0) {
+    const uint32_t* __restrict__ s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* __restrict__ d = reinterpret_cast<uint32_t*>(dst);
+    const uint64_t n4 = n >> 2;
+    for (uint64_t i = tid; i < n4; i += kCopyThreads) d[i] = s[i];
+    const uint64_t done = n4 << 2;
+    if (done < n) copy_bytes(reinterpret_cast<const uint8_t*>(src) + done,
+                             reinterpret_cast<uint8_t*>(dst) + done, n - done, tid);
+  } else {
+    copy_bytes(reinterpret_cast<const uint8_t*>(src), reinterpret_cast<uint8_t*>(dst), n, tid);
+  }
+}
+
+__global__ __launch_bounds__(kCopyThreads) void batched_copy_kernel(
+    const CopySeg* __restrict__ segs, int nseg, uint64_t total_chunks) {
+  const int tid = threadIdx.x;
+  for (uint64_t c = blockIdx.x; c < total_chunks; c += gridDim.x) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (segs[mid].chunk0 <= c) lo = mid; else hi = mid - 1;
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    const uint64_t src = segs[lo].src, dst = segs[lo].dst, bytes = segs[lo].bytes;
+    const uint64_t off = (c - segs[lo].chunk0) * kCopyChunk;
+    const uint64_t n = bytes - off < kCopyChunk ? bytes - off : kCopyChunk;
+    copy_range(src + off, dst + off, n, tid);
+  }
+}
+
+hipError_t launch_batched_copy(const CopySeg* segs, int nseg, uint64_t total_chunks,
+                               hipStream_t stream) {
+  if (nseg <= 0 || total_chunks == 0) return hipSuccess;
+  // 256 CUs x 8 resident 256-thread workgroups; more chunks are grid-strided.
+  const uint64_t grid = std::min<uint64_t>(total_chunks, 2048);
+  hipLaunchKernelGGL(batched_copy_kernel, dim3((unsigned)grid), dim3(kCopyThreads), 0, stream,
+                     segs, nseg, total_chunks);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// K10: CRC32C.  Phase 1: one workgroup per 64 KiB segment; each lane runs slicing-by-8 over its
+// own 256 B with the 8 KiB table resident in LDS, then the 256 lane CRCs are folded with a
+// log-depth GF(2) "shift" combine (x^(8L) mod P multipliers).  Phase 2: one workgroup per piece
+// folds its segment CRCs (variable-length right operands) and applies init/xorout.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kCrcPoly = 0x82F63B78u;  // reflected Castagnoli
+constexpr uint64_t kCrcSeg = 64 * 1024;
+constexpr int kCrcThreads = 256;
+constexpr uint64_t kCrcLane = kCrcSeg / kCrcThreads;  // 256 B per lane
+
+__constant__ uint32_t c_crc_tab[8][256];
+__constant__ uint32_t c_x2n[64];  // x^(2^k) mod P, k = 0..63
+
+static void host_crc_tables(uint32_t tab[8][256], uint32_t x2n[64]) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+    tab[0][i] = c;
+  }
+  for (int t = 1; t < 8; ++t)
+    for (uint32_t i = 0; i < 256; ++i) tab[t][i] = (tab[t - 1][i] >> 8) ^ tab[0][tab[t - 1][i] & 0xFF];
+  // x^1 in reflected representation is 0x40000000; square repeatedly.
+  auto mult = [](uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+      if (a & m) { p ^= b; if ((a & (m - 1)) == 0) break; }
+      m >>= 1;
+      b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+    }
+    return p;
+  };
+  uint32_t p = 1u << 30;
+  x2n[0] = p;
+  for (int k = 1; k < 64; ++k) { p = mult(p, p); x2n[k] = p; }
+}
+
+static std::once_flag g_crc_once;
+static hipError_t g_crc_init_err = hipSuccess;
+
+static hipError_t ensure_crc_tables() {
+  std::call_once(g_crc_once, [] {
+    static uint32_t tab[8][256];
+    static uint32_t x2n[64];
+    host_crc_tables(tab, x2n);
+    g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab));
+    if (g_crc_init_err == hipSuccess)
+      g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), x2n, sizeof(x2n));
+  });
+  return g_crc_init_err;
+}
+
+__device__ __forceinline__ uint32_t gf2_mult(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (int i = 0; i < 32; ++i) {
+    if (a & m) p ^= b;
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+
+// x^(8*nbytes) mod P by square-and-multiply over the bits of 8*nbytes.
+__device__ __forceinline__ uint32_t xpow8n(uint64_t nbytes) {
+  uint64_t n = nbytes << 3;
+  uint32_t p = 1u << 31;  // x^0
+  int k = 0;
+  while (n) {
+    if (n & 1) p = gf2_mult(c_x2n[k & 63], p);
+    n >>= 1;
+    ++k;
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(kCrcThreads) void crc32c_segments_kernel(
+    const uint8_t* __restrict__ base, uint64_t total_bytes, uint64_t piece_bytes,
+    uint64_t segs_per_piece, uint64_t nsegs, uint32_t* __restrict__ seg_crc) {
+  __shared__ uint32_t tab[8][256];
+  __shared__ uint32_t part[kCrcThreads];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 8 * 256; i += kCrcThreads) tab[i >> 8][i & 255] = c_crc_tab[i >> 8][i & 255];
+  __syncthreads();
+  const uint32_t k_lane = xpow8n(kCrcLane);  // shift by one lane's bytes (uniform)
+  for (uint64_t g = blockIdx.x; g < nsegs; g += gridDim.x) {
+    const uint64_t piece = g / segs_per_piece;
+    const uint64_t seg_in_piece = g % segs_per_piece;
+    const uint64_t piece_start = piece * piece_bytes;
+    const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
+    const uint64_t seg_start = piece_start + seg_in_piece * kCrcSeg;
+    const uint64_t seg_len = std::min(kCrcSeg, piece_start + piece_len - seg_start);
+    // lane range inside the segment
+    const uint64_t lo = std::min<uint64_t>((uint64_t)tid * kCrcLane, seg_len);
+    const uint64_t hi = std::min<uint64_t>(lo + kCrcLane, seg_len);
+    const uint8_t* p = base + seg_start + lo;
+    uint32_t c = 0;
+    uint64_t n = hi - lo;
+    if ((((uintptr_t)p) & 15) == 0) {
+      while (n >= 16) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        uint32_t a = v.x ^ c, b = v.y;
+        c = tab[7][a & 255] ^ tab[6][(a >> 8) & 255] ^ tab[5][(a >> 16) & 255] ^ tab[4][a >> 24] ^
+            tab[3][b & 255] ^ tab[2][(b >> 8) & 255] ^ tab[1][(b >> 16) & 255] ^ tab[0][b >> 24];
+        a = v.z ^ c;
+        b = v.w;
+        c = tab[7][a & 255] ^ tab[6][(a >> 8) & 255] ^ tab[5][(a >> 16) & 255] ^ tab[4][a >> 24] ^
+            tab[3][b & 255] ^ tab[2][(b >> 8) & 255] ^ tab[1][(b >> 16) & 255] ^ tab[0][b >> 24];
+        p += 16;
+        n -= 16;
+      }
+    }
+    while (n--) c = (c >> 8) ^ tab[0][(c ^ *p++) & 255];
+    part[tid] = c;
+    __syncthreads();
+    // Fold lane CRCs: level s merges (t, t+s); right operand length = bytes of lanes [t+s, t+2s).
+    for (int s = 1; s < kCrcThreads; s <<= 1) {
+      if ((tid & (2 * s - 1)) == 0 && tid + s < kCrcThreads) {
+        const uint64_t r_lo = std::min<uint64_t>((uint64_t)(tid + s) * kCrcLane, seg_len);
+        const uint64_t r_hi = std::min<uint64_t>((uint64_t)(tid + 2 * s) * kCrcLane, seg_len);
+        const uint64_t rlen = r_hi - r_lo;
+        if (rlen) {
+          const uint32_t k = (rlen == (uint64_t)s * kCrcLane && s == 1) ? k_lane : xpow8n(rlen);
+          part[tid] = gf2_mult(k, part[tid]) ^ part[tid + s];
+        }
+      }
+      __syncthreads();
+    }
+    if (tid == 0) seg_crc[g] = part[0];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kCrcThreads) void crc32c_pieces_kernel(
+    const uint32_t* __restrict__ seg_crc, uint64_t total_bytes, uint64_t piece_bytes,
+    uint64_t segs_per_piece, uint64_t npieces, uint32_t* __restrict__ out) {
+  __shared__ uint32_t part[kCrcThreads];
+  __shared__ uint64_t plen[kCrcThreads];
+  const int tid = threadIdx.x;
+  for (uint64_t pc = blockIdx.x; pc < npieces; pc += gridDim.x) {
+    const uint64_t piece_start = pc * piece_bytes;
+    const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
+    const uint64_t nseg = (piece_len + kCrcSeg - 1) / kCrcSeg;
+    const uint64_t per = (nseg + kCrcThreads - 1) / kCrcThreads;
+    const uint64_t s0 = std::min<uint64_t>((uint64_t)tid * per, nseg);
+    const uint64_t s1 = std::min<uint64_t>(s0 + per, nseg);
+    uint32_t c = 0;
+    uint64_t len = 0;
+    for (uint64_t s = s0; s < s1; ++s) {
+      const uint64_t sl = std::min(kCrcSeg, piece_len - s * kCrcSeg);
+      c = gf2_mult(xpow8n(sl), c) ^ seg_crc[pc * segs_per_piece + s];
+      len += sl;
+    }
+    part[tid] = c;
+    plen[tid] = len;
+    __syncthreads();
+    for (int s = 1; s < kCrcThreads; s <<= 1) {
+      if ((tid & (2 * s - 1)) == 0 && tid + s < kCrcThreads) {
+        const uint64_t rlen = plen[tid + s];
+        if (rlen) part[tid] = gf2_mult(xpow8n(rlen), part[tid]) ^ part[tid + s];
+        plen[tid] += rlen;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      // standard CRC = raw ^ shift(0xFFFFFFFF, len) ^ 0xFFFFFFFF
+      out[pc] = part[0] ^ gf2_mult(xpow8n(piece_len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+    }
+    __syncthreads();
+  }
+}
+
+uint64_t crc32c_scratch_words(uint64_t total_bytes, uint64_t piece_bytes) {
+  if (total_bytes == 0 || piece_bytes == 0) return 0;
+  const uint64_t npieces = (total_bytes + piece_bytes - 1) / piece_bytes;
+  const uint64_t spp = (piece_bytes + kCrcSeg - 1) / kCrcSeg;
+  return npieces * spp;
+}
+
+hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint64_t piece_bytes,
+                                uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
+                                hipStream_t stream) {
+  if (total_bytes == 0) return hipSuccess;
+  hipError_t e = ensure_crc_tables();
+  if (e != hipSuccess) return e;
+  const uint64_t npieces = (total_bytes + piece_bytes - 1) / piece_bytes;
+  const uint64_t spp = (piece_bytes + kCrcSeg - 1) / kCrcSeg;
+  const uint64_t nsegs = npieces * spp;
+  if (scratch_words < nsegs) return hipErrorInvalidValue;
+  const unsigned g1 = (unsigned)std::min<uint64_t>(nsegs, 4096);
+  hipLaunchKernelGGL(crc32c_segments_kernel, dim3(g1), dim3(kCrcThreads), 0, stream, base,
+                     total_bytes, piece_bytes, spp, nsegs, scratch);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const unsigned g2 = (unsigned)std::min<uint64_t>(npieces, 4096);
+  hipLaunchKernelGGL(crc32c_pieces_kernel, dim3(g2), dim3(kCrcThreads), 0, stream, scratch,
+                     total_bytes, piece_bytes, spp, npieces, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// K11: LZ4 block-format codec, one 64-lane workgroup per <=64 KiB chunk, output window in LDS.
+// All control flow is wave-uniform (every lane parses the same token stream); literal runs and
+// match copies are lane-parallel, overlapping matches proceed in rounds of min(offset, 64).
+// ---------------------------------------------------------------------------------------------
+constexpr int kLzThreads = 64;
+constexpr uint32_t kLzWindow = 64 * 1024;
+
+__global__ __launch_bounds__(kLzThreads) void lz4_decompress_kernel(const Lz4Chunk* __restrict__ ch,
+                                                                   int n, int32_t* __restrict__ out_sizes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t win[];
+  const int lane = threadIdx.x;
+  for (int w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint8_t* __restrict__ ip = reinterpret_cast<const uint8_t*>(ch[w].src);
+    const uint8_t* const iend = ip + ch[w].src_bytes;
+    const uint32_t cap = ch[w].dst_capacity < kLzWindow ? ch[w].dst_capacity : kLzWindow;
+    uint32_t op = 0;
+    int32_t status = 0;
+    while (ip < iend) {
+      const uint32_t token = *ip++;
+      uint32_t lit = token >> 4;
+      if (lit == 15) {
+        uint32_t b;
+        do {
+          if (ip >= iend) { status = -1; break; }
+          b = *ip++;
+          lit += b;
+        } while (b == 255);
+        if (status) break;
+      }
+      if (ip + lit > iend || op + lit > cap) { status = -2; break; }
+      for (uint32_t i = lane; i < lit; i += kLzThreads) win[op + i] = ip[i];
+      ip += lit;
+      op += lit;
+      if (ip >= iend) break;  // last sequence carries literals only
+      if (ip + 2 > iend) { status = -3; break; }
+      const uint32_t off = (uint32_t)ip[0] | ((uint32_t)ip[1] << 8);
+      ip += 2;
+      uint32_t ml = token & 15;
+      if (ml == 15) {
+        uint32_t b;
+        do {
+          if (ip >= iend) { status = -4; break; }
+          b = *ip++;
+          ml += b;
+        } while (b == 255);
+        if (status) break;
+      }
+      ml += 4;
+      if (off == 0 || off > op || op + ml > cap) { status = -5; break; }
+      __syncthreads();  // literal/match writes of the previous step visible to all lanes
+      const uint32_t stride = off < (uint32_t)kLzThreads ? off : (uint32_t)kLzThreads;
+      for (uint32_t base = 0; base < ml; base += stride) {
+        const uint32_t i = base + lane;
+        uint8_t v = 0;
+        if (lane < (int)stride && i < ml) v = win[op - off + i];
+        __syncthreads();
+        if (lane < (int)stride && i < ml) win[op + i] = v;
+        __syncthreads();
+      }
+      op += ml;
+    }
+    __syncthreads();
+    if (status == 0) {
+      uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(ch[w].dst);
+      for (uint32_t i = lane; i < op; i += kLzThreads) dst[i] = win[i];
+    }
+    if (lane == 0) out_sizes[w] = status ? status : (int32_t)op;
+    __syncthreads();
+  }
+}
+
+hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
+                                 hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min(n, 4096);
+  hipLaunchKernelGGL(lz4_decompress_kernel, dim3(grid), dim3(kLzThreads), kLzWindow, stream,
+                     chunks, n, out_sizes);
+  return hipGetLastError();
+}
+
+// Compression: chunk staged into LDS, 4096-entry u16 hash table in LDS.  Lanes evaluate 64
+// candidate positions at once (hash, probe, match length) against the table state at batch
+// start; a wave ballot then drives the greedy parse.  Output is standard LZ4 block format.
+constexpr int kLzHashLog = 12;
+constexpr uint32_t kLzMinMatch = 4;
+constexpr uint32_t kLzLastLiterals = 5;
+constexpr uint32_t kLzMfLimit = 12;
+
+__device__ __forceinline__ uint32_t lz_read32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ uint32_t lz_hash(uint32_t v) {
+  return (v * 2654435761u) >> (32 - kLzHashLog);
+}
+
+__global__ __launch_bounds__(kLzThreads) void lz4_compress_kernel(const Lz4Chunk* __restrict__ ch,
+                                                                 int n, int32_t* __restrict__ out_sizes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* src = smem;                                            // 64 KiB
+  uint16_t* table = reinterpret_cast<uint16_t*>(smem + kLzWindow);  // 8 KiB
+  const int lane = threadIdx.x;
+  for (int w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint8_t* __restrict__ gsrc = reinterpret_cast<const uint8_t*>(ch[w].src);
+    uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(ch[w].dst);
+    const uint32_t len = ch[w].src_bytes < kLzWindow ? ch[w].src_bytes : kLzWindow;
+    const uint32_t cap = ch[w].dst_capacity;
+    for (uint32_t i = lane; i < len; i += kLzThreads) src[i] = gsrc[i];
+    for (uint32_t i = lane; i < (1u << kLzHashLog); i += kLzThreads) table[i] = 0xFFFF;
+    __syncthreads();
+    uint32_t op = 0, anchor = 0, ip = 0;
+    int32_t status = 0;
+    const uint32_t match_limit = len > kLzMfLimit ? len - kLzMfLimit : 0;   // last match start
+    const uint32_t end_match = len > kLzLastLiterals ? len - kLzLastLiterals : 0;
+    while (ip < match_limit && status == 0) {
+      // each lane probes position ip + lane
+      const uint32_t pos = ip + lane;
+      uint32_t cand = 0xFFFFFFFFu, mlen = 0;
+      uint32_t h = 0;
+      if (pos < match_limit) {
+        const uint32_t v = lz_read32(src + pos);
+        h = lz_hash(v);
+        const uint32_t c = table[h];
+        if (c != 0xFFFF && c < pos && pos - c <= 65535 && lz_read32(src + c) == v) {
+          cand = c;
+          mlen = kLzMinMatch;
+          while (pos + mlen < end_match && src[c + mlen] == src[pos + mlen]) ++mlen;
+        }
+      }
+      __syncthreads();
+      if (pos < match_limit) table[h] = (uint16_t)pos;  // last writer wins: any entry is valid
+      __syncthreads();
+      const unsigned long long hits = __ballot(cand != 0xFFFFFFFFu);
+      if (hits == 0) { ip += kLzThreads; continue; }
+      const int first = __ffsll((long long)hits) - 1;
+      const uint32_t mpos = ip + first;
+      const uint32_t moff = mpos - __shfl(cand, first);
+      const uint32_t ml = __shfl(mlen, first);
+      // emit sequence: literals [anchor, mpos) + match (moff, ml)
+      const uint32_t lit = mpos - anchor;
+      const uint32_t need = 1 + (lit >= 15 ? (lit - 15) / 255 + 1 : 0) + lit + 2 +
+                            ((ml - 4) >= 15 ? (ml - 4 - 15) / 255 + 1 : 0);
+      if (op + need > cap) { status = -1; break; }
+      uint32_t o = op;
+      if (lane == 0) {
+        const uint32_t mcode = ml - 4;
+        dst[o] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | (mcode >= 15 ? 15 : mcode));
+        uint32_t q = o + 1;
+        if (lit >= 15) { uint32_t r = lit - 15; while (r >= 255) { dst[q++] = 255; r -= 255; } dst[q++] = (uint8_t)r; }
+        op = q;  // lane-0 local; broadcast below
+      }
+      o = __shfl(op, 0);
+      for (uint32_t i = lane; i < lit; i += kLzThreads) dst[o + i] = src[anchor + i];
+      o += lit;
+      if (lane == 0) {
+        dst[o] = (uint8_t)(moff & 255);
+        dst[o + 1] = (uint8_t)(moff >> 8);
+        uint32_t q = o + 2;
+        const uint32_t mcode = ml - 4;
+        if (mcode >= 15) { uint32_t r = mcode - 15; while (r >= 255) { dst[q++] = 255; r -= 255; } dst[q++] = (uint8_t)r; }
+        op = q;
+      }
+      op = __shfl(op, 0);
+      ip = mpos + ml;
+      anchor = ip;
+    }
+    if (status == 0) {
+      const uint32_t lit = len - anchor;
+      const uint32_t need = 1 + (lit >= 15 ? (lit - 15) / 255 + 1 : 0) + lit;
+      if (op + need > cap) {
+        status = -1;
+      } else {
+        uint32_t o = op;
+        if (lane == 0) {
+          dst[o] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+          uint32_t q = o + 1;
+          if (lit >= 15) { uint32_t r = lit - 15; while (r >= 255) { dst[q++] = 255; r -= 255; } dst[q++] = (uint8_t)r; }
+          op = q;
+        }
+        o = __shfl(op, 0);
+        for (uint32_t i = lane; i < lit; i += kLzThreads) dst[o + i] = src[anchor + i];
+        op = o + lit;
+      }
+    }
+    if (lane == 0) out_sizes[w] = status ? -1 : (int32_t)op;
+    __syncthreads();
+  }
+}
+
+hipError_t launch_lz4_compress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
+                               hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min(n, 4096);
+  const size_t lds = kLzWindow + (sizeof(uint16_t) << kLzHashLog);
+  hipLaunchKernelGGL(lz4_compress_kernel, dim3(grid), dim3(kLzThreads), lds, stream, chunks, n,
+                     out_sizes);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// K4-K6: fused eviction scoring + byte-weighted radix select (single 1024-thread workgroup).
+// Key = LRU: 0xFFFFFFFE - min(age, 0xFFFFFFFE); LRFU: float bits of the decayed CRF
+// (CRF * (1/att)^(age*step)); non-evictable = 0xFFFFFFFF.  Four 8-bit MSB-first passes find the
+// smallest threshold T with bytes(key < T) + bytes(key == T) >= need; compaction emits every
+// key < T plus enough ties.  This is the reference's "iterate the annotator order until enough
+// contiguous/available space" loop (TieredBlockStore.freeSpaceInternal) done in one launch.
+// ---------------------------------------------------------------------------------------------
+constexpr int kEvThreads = 1024;
+
+__global__ __launch_bounds__(kEvThreads) void evict_select_kernel(
+    EvictInput in, uint32_t* __restrict__ keys, uint32_t* __restrict__ out_slots,
+    uint32_t* __restrict__ out_count, uint64_t* __restrict__ out_bytes) {
+  __shared__ unsigned long long hist[256];
+  __shared__ uint32_t s_prefix, s_mask;
+  __shared__ unsigned long long s_acc, s_tie_acc;
+  __shared__ uint32_t s_count;
+  __shared__ int s_all;
+  const int tid = threadIdx.x;
+  const float inv_att = 1.0f / in.attenuation;
+  // pass 0: keys + total evictable bytes
+  unsigned long long local_total = 0;
+  for (uint32_t i = tid; i < in.n; i += kEvThreads) {
+    uint32_t key = 0xFFFFFFFFu;
+    if (in.evictable[i]) {
+      const uint64_t age = in.now > in.last[i] ? in.now - in.last[i] : 0;
+      if (in.policy == 0) {
+        key = 0xFFFFFFFEu - (uint32_t)(age < 0xFFFFFFFEull ? age : 0xFFFFFFFEull);
+      } else {
+        float crf = in.crf[i] * powf(inv_att, (float)age * in.step_factor);
+        if (!(crf >= 0.0f)) crf = 0.0f;
+        key = __float_as_uint(crf);
+        if (key >= 0xFFFFFFFEu) key = 0xFFFFFFFDu;
+      }
+      local_total += in.bytes[i];
+    }
+    keys[i] = key;
+  }
+  if (tid == 0) { s_prefix = 0; s_mask = 0; s_acc = 0; s_count = 0; s_tie_acc = 0; s_all = 0; }
+  __shared__ unsigned long long s_total;
+  if (tid == 0) s_total = 0;
+  __syncthreads();
+  atomicAdd(&s_total, local_total);
+  __syncthreads();
+  if (s_total <= in.need_bytes) {
+    if (tid == 0) { s_all = 1; s_prefix = 0xFFFFFFFFu; s_mask = 0xFFFFFFFFu; }
+  }
+  __syncthreads();
+  if (!s_all) {
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      for (int b = tid; b < 256; b += kEvThreads) hist[b] = 0;
+      __syncthreads();
+      const uint32_t prefix = s_prefix, mask = s_mask;
+      for (uint32_t i = tid; i < in.n; i += kEvThreads) {
+        const uint32_t k = keys[i];
+        if (k != 0xFFFFFFFFu && (k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], (unsigned long long)in.bytes[i]);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        unsigned long long acc = s_acc;
+        int d = 0;
+        for (; d < 256; ++d) {
+          if (acc + hist[d] >= in.need_bytes) break;
+          acc += hist[d];
+        }
+        if (d == 256) d = 255;
+        s_acc = acc;
+        s_prefix = prefix | ((uint32_t)d << shift);
+        s_mask = mask | (255u << shift);
+      }
+      __syncthreads();
+    }
+  }
+  const uint32_t T = s_prefix;
+  const bool all = s_all != 0;
+  const unsigned long long below = s_acc;  // bytes strictly below T
+  // compaction
+  for (uint32_t i = tid; i < in.n; i += kEvThreads) {
+    const uint32_t k = keys[i];
+    if (k == 0xFFFFFFFFu) continue;
+    bool take = all || k < T;
+    if (!take && k == T) {
+      const unsigned long long prev = atomicAdd(&s_tie_acc, (unsigned long long)in.bytes[i]);
+      take = below + prev < in.need_bytes;
+    }
+    if (take) {
+      const uint32_t slot = atomicAdd(&s_count, 1u);
+      out_slots[slot] = i;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    *out_count = s_count;
+    unsigned long long freed = 0;
+    for (uint32_t j = 0; j < s_count; ++j) freed += in.bytes[out_slots[j]];
+    *out_bytes = freed;
+  }
+}
+
+hipError_t launch_evict_select(const EvictInput& in, uint32_t* keys_scratch, uint32_t* out_slots,
+                               uint32_t* out_count, uint64_t* out_bytes, hipStream_t stream) {
+  hipLaunchKernelGGL(evict_select_kernel, dim3(1), dim3(kEvThreads), 0, stream, in, keys_scratch,
+                     out_slots, out_count, out_bytes);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Synthetic data generator (bench / tests): splitmix64 of (seed, 8-byte word index).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_pattern_kernel(uint8_t* __restrict__ dst, uint64_t bytes,
+                                                           uint64_t seed, uint64_t word_offset) {
+  const uint64_t nwords = bytes >> 3;
+  uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    d[i] = splitmix64(seed ^ ((i + word_offset) * 0xD1B54A32D192ED03ull));
+  const uint64_t tail = bytes & 7;
+  if (tail && blockIdx.x == 0 && threadIdx.x < tail) {
+    const uint64_t w = splitmix64(seed ^ ((nwords + word_offset) * 0xD1B54A32D192ED03ull));
+    dst[(nwords << 3) + threadIdx.x] = (uint8_t)(w >> (8 * threadIdx.x));
+  }
+}
+
+hipError_t launch_fill_pattern(uint8_t* dst, uint64_t bytes, uint64_t seed, uint64_t word_offset,
+                               hipStream_t stream) {
+  if (bytes == 0) return hipSuccess;
+  if (((uintptr_t)dst & 7) != 0) return hipErrorInvalidValue;
+  const uint64_t words = (bytes + 7) >> 3;
+  const unsigned grid = (unsigned)std::min<uint64_t>((words + 255) / 256, 4096);
+  hipLaunchKernelGGL(fill_pattern_kernel, dim3(grid), dim3(256), 0, stream, dst, bytes, seed,
+                     word_offset);
+  return hipGetLastError();
+}
+
+}  // namespace amdx

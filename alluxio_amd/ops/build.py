@@ -1,0 +1,87 @@
+"""In-tree build of the native extension ``alluxio_amd._C`` for gfx950.
+
+Compiles ``csrc/kernels.hip`` with ``hipcc --offload-arch=gfx950`` and the host C++ (block
+store, codecs, pybind11 bindings) with ``hipcc`` in host mode, then links one shared object next
+to the package so it travels with the repository snapshot to the GPU box.  Rebuilds only when a
+source is newer than the ``.so``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD = os.path.join(os.path.dirname(PKG_DIR), "build", "native")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+
+SOURCES = ["kernels.hip", "block_store.cpp", "cpu_codecs.cpp", "bindings.cpp"]
+HEADERS = ["kernels.h", "block_store.h", "cpu_codecs.h"]
+
+
+def ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG_DIR, "_C" + suffix)
+
+
+def _includes() -> list[str]:
+    import pybind11
+    return ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-I" + CSRC]
+
+
+def _needs_build(target: str) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    for f in SOURCES + HEADERS:
+        if os.path.getmtime(os.path.join(CSRC, f)) > t:
+            return True
+    return os.path.getmtime(os.path.abspath(__file__)) > t
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"native build failed: {os.path.basename(cmd[-1])}")
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    target = ext_path()
+    if not force and not _needs_build(target):
+        return target
+    os.makedirs(BUILD, exist_ok=True)
+    common = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-Wno-unused-result",
+              "-Wno-unused-variable", "-fvisibility=hidden"] + _includes()
+    jobs = []
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(BUILD, src.replace(".", "_") + ".o")
+        objs.append(obj)
+        path = os.path.join(CSRC, src)
+        if src.endswith(".hip"):
+            cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common,
+                   "-c", path, "-o", obj]
+        else:
+            cmd = [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", *common, "-c", path,
+                   "-o", obj]
+        jobs.append(cmd)
+    with cf.ThreadPoolExecutor(max_workers=min(4, len(jobs))) as ex:
+        for fut in [ex.submit(_run, j) for j in jobs]:
+            fut.result()
+    tmp = target + ".tmp"
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp,
+          f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
+    os.replace(tmp, target)
+    if verbose:
+        print("built", target)
+    return target
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)
