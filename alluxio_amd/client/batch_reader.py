@@ -1,0 +1,90 @@
+"""Batched multi-stream file reader (the GPU-native form of many concurrent ``read(buf)`` loops).
+
+A StressWorkerBench client runs T threads, each looping ``FileInStream.read(buf)`` over the same
+file and re-opening at EOF (stress/shell/.../StressWorkerBench.java:251-276).  On MI355X the
+T reads of one round are independent page-gathers, so they are planned together and executed
+as one kernel launch by the worker's native :class:`ReadSession` (block locks are held per
+stream and switched at block boundaries, exactly as the per-thread BlockInStreams would).  A
+re-open goes through the client API (``getStatus`` with the client metadata cache, like the
+reference's Hadoop client) and validates the file is still fully cached.
+"""
+from __future__ import annotations
+
+from ..utils import ids
+from ..utils.exceptions import UnavailableException
+from .context import worker_address_str
+
+HOST, DEVICE = 0, 1
+
+
+class MultiStreamReader:
+    def __init__(self, fs, path: str, buffers: list, start_offsets: list[int] | None = None):
+        """``buffers``: one destination per stream (torch tensors on cuda -> device reads)."""
+        import torch
+        self.fs = fs
+        self.path = path
+        self.buffers = buffers
+        self.nbytes = buffers[0].numel() * buffers[0].element_size()
+        self.kind = DEVICE if buffers[0].is_cuda else HOST
+        self.device = buffers[0].device if buffers[0].is_cuda else None
+        st = fs.get_status(path)
+        self.status = st
+        self.worker = self._local_worker(st)
+        self.session = ids.create_session_id()
+        blocks, lens = self._layout(st)
+        from ..ops.native import lib, native_errors
+        C = lib()
+        with native_errors():
+            self.rs = C.ReadSession(self.worker.native, self.session, blocks, lens,
+                                    [b.data_ptr() for b in buffers], self.nbytes, self.kind,
+                                    list(start_offsets or []))
+        self._stream = torch.cuda.current_stream(self.device) if self.kind == DEVICE else None
+        self.reopens = 0
+
+    def _local_worker(self, st):
+        for fbi in st.fileBlockInfos:
+            for loc in fbi.blockInfo.locations:
+                w = self.fs.ctx.in_process_worker(loc.workerAddress)
+                if w is not None:
+                    return w
+        raise UnavailableException(f"{self.path} is not cached on a worker in this process "
+                                   f"(locations: {[worker_address_str(l.workerAddress) for f in st.fileBlockInfos for l in f.blockInfo.locations]})")
+
+    @staticmethod
+    def _layout(st):
+        blocks = [fbi.blockInfo.blockId for fbi in st.fileBlockInfos]
+        lens = [fbi.blockInfo.length for fbi in st.fileBlockInfos]
+        return blocks, lens
+
+    def step(self) -> int:
+        """One round: every stream reads one buffer (or hits EOF and re-opens)."""
+        from ..ops.native import native_errors
+        handle = int(self._stream.cuda_stream) if self._stream is not None else 0
+        with native_errors():
+            nbytes, reopened = self.rs.step(handle)
+        if reopened:
+            # re-open: metadata lookup through the client (cached), same block layout expected
+            st = self.fs.get_status(self.path)
+            if st.length != self.status.length or list(st.block_ids) != list(self.status.block_ids):
+                blocks, lens = self._layout(st)
+                self.rs.reset_file(blocks, lens)
+                self.status = st
+            self.reopens += len(reopened)
+        return nbytes
+
+    def position(self, i: int) -> int:
+        return self.rs.position(i)
+
+    @property
+    def total_bytes(self) -> int:
+        return self.rs.total_bytes
+
+    def close(self) -> None:
+        self.rs.close()
+        self.worker.cleanup_session(self.session)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -1,0 +1,114 @@
+"""Client context: configuration, master/worker channels, cached worker list, local workers.
+
+Parity: core/client/fs/src/main/java/alluxio/client/file/FileSystemContext.java:120-586 (master
+client pools, per-worker client pools, cached worker list, local-worker detection by tiered
+identity, cluster-config reinitialisation).  A worker running in the same process registers
+itself here, which lets reads and writes bypass RPC entirely (the in-process analogue of the
+reference's short-circuit I/O); same-node workers in other processes are reached over gRPC or
+HIP IPC (``OpenDeviceBlock``).
+"""
+from __future__ import annotations
+
+import socket
+import threading
+import time
+
+from .. import metrics as msys
+from ..conf import Configuration
+from ..proto import pb
+from ..rpc import ChannelPool
+from ..security import login_user
+
+SVC_FS = "alluxio.grpc.file.FileSystemMasterClientService"
+SVC_BLOCK = "alluxio.grpc.block.BlockMasterClientService"
+SVC_META = "alluxio.grpc.meta.MetaMasterClientService"
+SVC_META_CONF = "alluxio.grpc.meta.MetaMasterConfigurationService"
+SVC_METRICS = "alluxio.grpc.metric.MetricsMasterClientService"
+SVC_WORKER = "alluxio.grpc.block.BlockWorker"
+
+_LOCAL_WORKERS: dict[str, object] = {}
+_LW_LOCK = threading.Lock()
+
+
+def register_local_worker(address: str, worker) -> None:
+    with _LW_LOCK:
+        _LOCAL_WORKERS[address] = worker
+
+
+def unregister_local_worker(address: str) -> None:
+    with _LW_LOCK:
+        _LOCAL_WORKERS.pop(address, None)
+
+
+def local_worker(address: str):
+    with _LW_LOCK:
+        return _LOCAL_WORKERS.get(address)
+
+
+def worker_address_str(addr) -> str:
+    return f"{addr.host}:{addr.rpcPort}"
+
+
+class FileSystemContext:
+    def __init__(self, conf: Configuration | None = None, master_address: str | None = None,
+                 user: str | None = None):
+        self.conf = conf or Configuration(load_site=True)
+        self.master_address = master_address or "{}:{}".format(
+            self.conf.get("alluxio.master.hostname", "127.0.0.1"), self.conf.get_int("alluxio.master.rpc.port"))
+        self.user = user or login_user(self.conf)
+        self.pool = ChannelPool()
+        self.metrics = msys.metrics("Client")
+        self.hostname = socket.gethostname()
+        self._workers = None
+        self._workers_at = 0.0
+        self._lock = threading.Lock()
+        self.worker_list_ttl = self.conf.get_ms("alluxio.user.worker.list.refresh.interval", "2min") / 1000.0
+        self._closed = False
+
+    # ---- stubs --------------------------------------------------------------------------------
+    def master_channel(self):
+        return self.pool.get(self.master_address, self.user)
+
+    def fs_master(self):
+        return self.master_channel().stub(SVC_FS)
+
+    def block_master(self):
+        return self.master_channel().stub(SVC_BLOCK)
+
+    def meta_master(self):
+        return self.master_channel().stub(SVC_META)
+
+    def meta_config(self):
+        return self.master_channel().stub(SVC_META_CONF)
+
+    def metrics_master(self):
+        return self.master_channel().stub(SVC_METRICS)
+
+    def worker_channel(self, address: str):
+        return self.pool.get(address, self.user)
+
+    def worker_stub(self, address: str):
+        return self.worker_channel(address).stub(SVC_WORKER)
+
+    # ---- workers ------------------------------------------------------------------------------
+    def workers(self, refresh: bool = False) -> list:
+        with self._lock:
+            if refresh or self._workers is None or time.time() - self._workers_at > self.worker_list_ttl:
+                self._workers = list(self.block_master().GetWorkerInfoList(
+                    pb.block.GetWorkerInfoListPOptions()).workerInfos)
+                self._workers_at = time.time()
+            return list(self._workers)
+
+    def is_local(self, addr) -> bool:
+        """Same node as this client (reference: tiered identity 'node' tier match)."""
+        for t in addr.tieredIdentity.tiers:
+            if t.tierName == "node":
+                return t.value == self.hostname
+        return addr.host in ("127.0.0.1", "localhost", self.hostname)
+
+    def in_process_worker(self, addr):
+        return local_worker(worker_address_str(addr))
+
+    def close(self) -> None:
+        self._closed = True
+        self.pool.close()

@@ -1,0 +1,362 @@
+"""Client ``FileSystem`` API.
+
+Parity: core/client/fs/src/main/java/alluxio/client/file/FileSystem.java:79-650 (the full method
+surface), BaseFileSystem.java:137-386 (RPC wrappers; ``openFile`` builds a FileInStream from
+``getStatus``), MetadataCachingBaseFileSystem.java + MetadataCache.java (client-side status
+cache), ReadType/WriteType (ReadType.java:32-43, WriteType.java:30-57), URIStatus.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from collections import OrderedDict
+
+from ..proto import enum_name, pb
+from ..security.acl import AclEntry, mode_to_pmode
+from ..utils.uri import AlluxioURI, normalize_path
+from .context import FileSystemContext
+from .streams import FileInStream, FileOutStream
+
+READ_TYPES = ("NO_CACHE", "CACHE", "CACHE_PROMOTE")
+WRITE_TYPES = ("MUST_CACHE", "TRY_CACHE", "CACHE_THROUGH", "THROUGH", "ASYNC_THROUGH", "NONE")
+LOAD = {"NEVER": 0, "ONCE": 1, "ALWAYS": 2}
+
+
+def _path(p) -> str:
+    if isinstance(p, AlluxioURI):
+        return p.path
+    s = str(p)
+    if "://" in s:
+        s = AlluxioURI(s).path
+    return normalize_path(s)
+
+
+class URIStatus:
+    """Read-only view of a FileInfo (reference alluxio.client.file.URIStatus)."""
+
+    def __init__(self, info):
+        self.info = info
+
+    def __getattr__(self, item):
+        return getattr(self.info, item)
+
+    @property
+    def path(self):
+        return self.info.path
+
+    @property
+    def name(self):
+        return self.info.name
+
+    @property
+    def length(self):
+        return self.info.length
+
+    @property
+    def is_folder(self):
+        return self.info.folder
+
+    @property
+    def is_completed(self):
+        return self.info.completed
+
+    @property
+    def is_persisted(self):
+        return self.info.persisted
+
+    @property
+    def block_ids(self):
+        return list(self.info.blockIds)
+
+    @property
+    def block_size(self):
+        return self.info.blockSizeBytes
+
+    @property
+    def in_alluxio_percentage(self):
+        return self.info.inAlluxioPercentage
+
+    @property
+    def in_memory_percentage(self):
+        return self.info.inMemoryPercentage
+
+    def __repr__(self):
+        return f"URIStatus({self.info.path!r}, len={self.info.length}, folder={self.info.folder})"
+
+
+class MetadataCache:
+    def __init__(self, max_size: int = 100_000, ttl_s: float = 600.0):
+        self.max_size, self.ttl = max_size, ttl_s
+        self._d: OrderedDict = OrderedDict()
+        self._lock = threading.Lock()
+
+    def get(self, path):
+        with self._lock:
+            v = self._d.get(path)
+            if v is None:
+                return None
+            info, t = v
+            if time.monotonic() - t > self.ttl:
+                del self._d[path]
+                return None
+            self._d.move_to_end(path)
+            return info
+
+    def put(self, path, info):
+        with self._lock:
+            self._d[path] = (info, time.monotonic())
+            self._d.move_to_end(path)
+            while len(self._d) > self.max_size:
+                self._d.popitem(last=False)
+
+    def invalidate(self, path=None):
+        with self._lock:
+            if path is None:
+                self._d.clear()
+                return
+            pref = path.rstrip("/") + "/"
+            for k in [k for k in self._d if k == path or k.startswith(pref)]:
+                del self._d[k]
+
+
+class FileSystem:
+    def __init__(self, context: FileSystemContext | None = None, conf=None, master_address: str | None = None,
+                 user: str | None = None, metadata_cache: bool | None = None):
+        self.ctx = context or FileSystemContext(conf, master_address, user)
+        c = self.ctx.conf
+        use_cache = c.get_bool("alluxio.user.metadata.cache.enabled", "false") if metadata_cache is None \
+            else metadata_cache
+        self.cache = MetadataCache(c.get_int("alluxio.user.metadata.cache.max.size", 100000),
+                                   c.get_ms("alluxio.user.metadata.cache.expiration.time", "10min") / 1000.0) \
+            if use_cache else None
+        self._fs = self.ctx.fs_master()
+        self._closed = False
+
+    @classmethod
+    def get(cls, conf=None, master_address=None, user=None):
+        """``FileSystem.Factory.get()`` equivalent."""
+        return cls(conf=conf, master_address=master_address, user=user)
+
+    def _common(self, sync_interval_ms=None, ttl=None, ttl_action=None):
+        c = pb.file.FileSystemMasterCommonPOptions()
+        if sync_interval_ms is not None:
+            c.syncIntervalMs = sync_interval_ms
+        if ttl is not None:
+            c.ttl = ttl
+            c.ttlAction = pb.grpc.TtlAction.values_by_name[ttl_action or "DELETE"].number
+        return c
+
+    def _invalidate(self, path):
+        if self.cache is not None:
+            self.cache.invalidate(path)
+
+    # ---- namespace ----------------------------------------------------------------------------
+    def create_directory(self, path, recursive=False, allow_exists=False, mode=None, write_type=None,
+                         ttl=None, ttl_action=None) -> None:
+        wt = write_type or self.ctx.conf.get("alluxio.user.file.writetype.default")
+        o = pb.file.CreateDirectoryPOptions(recursive=recursive, allowExists=allow_exists,
+                                            writeType=pb.file.WritePType.values_by_name[wt].number,
+                                            commonOptions=self._common(ttl=ttl, ttl_action=ttl_action))
+        if mode is not None:
+            o.mode.CopyFrom(mode_to_pmode(mode))
+        self._fs.CreateDirectory(pb.file.CreateDirectoryPRequest(path=_path(path), options=o))
+        self._invalidate(_path(path))
+
+    def create_file(self, path, block_size=None, recursive=True, mode=None, write_type=None,
+                    replication_min=0, replication_max=-1, replication_durable=1, ttl=None, ttl_action=None,
+                    write_tier=0, medium="", persistence_wait_ms=0) -> FileOutStream:
+        wt = write_type or self.ctx.conf.get("alluxio.user.file.writetype.default")
+        bs = block_size or self.ctx.conf.get_bytes("alluxio.user.block.size.bytes.default")
+        o = pb.file.CreateFilePOptions(blockSizeBytes=bs, recursive=recursive,
+                                       writeType=pb.file.WritePType.values_by_name[wt].number,
+                                       replicationMin=replication_min, replicationMax=replication_max,
+                                       replicationDurable=replication_durable, writeTier=write_tier,
+                                       commonOptions=self._common(ttl=ttl, ttl_action=ttl_action),
+                                       persistenceWaitTime=persistence_wait_ms)
+        if mode is not None:
+            o.mode.CopyFrom(mode_to_pmode(mode))
+        p = _path(path)
+        info = self._fs.CreateFile(pb.file.CreateFilePRequest(path=p, options=o)).fileInfo
+        self._invalidate(p)
+        return FileOutStream(self.ctx, info, wt, replication_durable, write_tier, medium, persistence_wait_ms)
+
+    def delete(self, path, recursive=False, alluxio_only=False, unchecked=False) -> None:
+        p = _path(path)
+        self._fs.Remove(pb.file.DeletePRequest(path=p, options=pb.file.DeletePOptions(
+            recursive=recursive, alluxioOnly=alluxio_only, unchecked=unchecked)))
+        self._invalidate(p)
+
+    def exists(self, path, load_metadata="ONCE") -> bool:
+        from ..utils.exceptions import NotFoundException
+        try:
+            self.get_status(path, load_metadata=load_metadata)
+            return True
+        except NotFoundException:
+            return False
+
+    def free(self, path, recursive=False, forced=False) -> None:
+        p = _path(path)
+        self._fs.Free(pb.file.FreePRequest(path=p, options=pb.file.FreePOptions(recursive=recursive, forced=forced)))
+        self._invalidate(p)
+
+    def get_status(self, path, load_metadata="ONCE", sync_interval_ms=None) -> URIStatus:
+        p = _path(path)
+        if self.cache is not None and sync_interval_ms is None:
+            hit = self.cache.get(p)
+            if hit is not None:
+                return URIStatus(hit)
+        o = pb.file.GetStatusPOptions(loadMetadataType=LOAD[load_metadata])
+        if sync_interval_ms is not None:
+            o.commonOptions.CopyFrom(self._common(sync_interval_ms))
+        info = self._fs.GetStatus(pb.file.GetStatusPRequest(path=p, options=o)).fileInfo
+        if self.cache is not None:
+            self.cache.put(p, info)
+        return URIStatus(info)
+
+    def list_status(self, path, recursive=False, load_metadata="ONCE", sync_interval_ms=None) -> list[URIStatus]:
+        o = pb.file.ListStatusPOptions(recursive=recursive, loadMetadataType=LOAD[load_metadata])
+        if sync_interval_ms is not None:
+            o.commonOptions.CopyFrom(self._common(sync_interval_ms))
+        out = []
+        for r in self._fs.ListStatus(pb.file.ListStatusPRequest(path=_path(path), options=o)):
+            out.extend(URIStatus(i) for i in r.fileInfos)
+        return out
+
+    def iterate_status(self, path, recursive=False, **kw):
+        yield from self.list_status(path, recursive=recursive, **kw)
+
+    def get_block_locations(self, path) -> list:
+        st = self.get_status(path)
+        return [(fbi.blockInfo, [l.workerAddress for l in fbi.blockInfo.locations]) for fbi in st.fileBlockInfos]
+
+    def load_metadata(self, path, recursive=False) -> None:
+        self.list_status(path, recursive=recursive, load_metadata="ALWAYS")
+
+    def rename(self, src, dst, persist=False) -> None:
+        self._fs.Rename(pb.file.RenamePRequest(path=_path(src), dstPath=_path(dst),
+                                               options=pb.file.RenamePOptions(persist=persist)))
+        self._invalidate(_path(src))
+        self._invalidate(_path(dst))
+
+    def reverse_resolve(self, ufs_uri: str) -> str:
+        return self._fs.ReverseResolve(pb.file.ReverseResolvePRequest(ufsUri=ufs_uri)).alluxioPath
+
+    def set_attribute(self, path, pinned=None, ttl=None, ttl_action=None, persisted=None, owner=None, group=None,
+                      mode=None, recursive=False, replication_min=None, replication_max=None,
+                      pinned_media=None) -> None:
+        o = pb.file.SetAttributePOptions(recursive=recursive)
+        if pinned is not None:
+            o.pinned = pinned
+        if persisted is not None:
+            o.persisted = persisted
+        if owner is not None:
+            o.owner = owner
+        if group is not None:
+            o.group = group
+        if mode is not None:
+            o.mode.CopyFrom(mode_to_pmode(mode))
+        if replication_min is not None:
+            o.replicationMin = replication_min
+        if replication_max is not None:
+            o.replicationMax = replication_max
+        if ttl is not None:
+            o.commonOptions.CopyFrom(self._common(ttl=ttl, ttl_action=ttl_action))
+        if pinned_media:
+            o.pinnedMedia.extend(pinned_media)
+        self._fs.SetAttribute(pb.file.SetAttributePRequest(path=_path(path), options=o))
+        self._invalidate(_path(path))
+
+    def set_acl(self, path, action: str, entries, recursive=False) -> None:
+        es = [AclEntry.parse(e) if isinstance(e, str) else e for e in entries]
+        self._fs.SetAcl(pb.file.SetAclPRequest(path=_path(path),
+                                               action=pb.file.SetAclAction.values_by_name[action].number,
+                                               entries=[e.to_pacl_entry() for e in es],
+                                               options=pb.file.SetAclPOptions(recursive=recursive)))
+        self._invalidate(_path(path))
+
+    def persist(self, path, wait_ms: int = 0) -> None:
+        self._fs.ScheduleAsyncPersistence(pb.file.ScheduleAsyncPersistencePRequest(
+            path=_path(path), options=pb.file.ScheduleAsyncPersistencePOptions(persistenceWaitTime=wait_ms)))
+        self._invalidate(_path(path))
+
+    def check_consistency(self, path) -> list[str]:
+        return list(self._fs.CheckConsistency(pb.file.CheckConsistencyPRequest(path=_path(path))).inconsistentPaths)
+
+    # ---- mounts / sync ------------------------------------------------------------------------
+    def mount(self, alluxio_path, ufs_path, read_only=False, shared=False, properties=None) -> None:
+        o = pb.file.MountPOptions(readOnly=read_only, shared=shared)
+        for k, v in (properties or {}).items():
+            o.properties[k] = v
+        self._fs.Mount(pb.file.MountPRequest(alluxioPath=_path(alluxio_path), ufsPath=str(ufs_path), options=o))
+
+    def update_mount(self, alluxio_path, read_only=None, shared=None, properties=None) -> None:
+        o = pb.file.MountPOptions()
+        if read_only is not None:
+            o.readOnly = read_only
+        if shared is not None:
+            o.shared = shared
+        for k, v in (properties or {}).items():
+            o.properties[k] = v
+        self._fs.UpdateMount(pb.file.UpdateMountPRequest(alluxioPath=_path(alluxio_path), options=o))
+
+    def unmount(self, alluxio_path) -> None:
+        self._fs.Unmount(pb.file.UnmountPRequest(alluxioPath=_path(alluxio_path)))
+        self._invalidate(_path(alluxio_path))
+
+    def get_mount_table(self) -> dict:
+        return dict(self._fs.GetMountTable(pb.file.GetMountTablePRequest()).mountPoints)
+
+    def get_sync_path_list(self) -> list[str]:
+        return [s.syncPointUri for s in self._fs.GetSyncPathList(pb.file.GetSyncPathListPRequest()).syncPaths]
+
+    def start_sync(self, path) -> None:
+        self._fs.StartSync(pb.file.StartSyncPRequest(path=_path(path)))
+
+    def stop_sync(self, path) -> None:
+        self._fs.StopSync(pb.file.StopSyncPRequest(path=_path(path)))
+
+    def update_ufs_mode(self, ufs_path: str, mode: str) -> None:
+        self._fs.UpdateUfsMode(pb.file.UpdateUfsModePRequest(
+            ufsPath=ufs_path, options=pb.file.UpdateUfsModePOptions(ufsMode=pb.file.UfsPMode.values_by_name[mode].number)))
+
+    # ---- data ---------------------------------------------------------------------------------
+    def open_file(self, path, read_type=None, status: URIStatus | None = None) -> FileInStream:
+        rt = read_type or self.ctx.conf.get("alluxio.user.file.readtype.default")
+        st = status or self.get_status(path)
+        if st.info.folder:
+            from ..utils.exceptions import InvalidArgumentException
+            raise InvalidArgumentException(f"{st.info.path} is a directory")
+        if not st.info.completed:
+            from ..utils.exceptions import FileIncompleteException
+            raise FileIncompleteException(f"File {st.info.path} is not completed")
+        return FileInStream(self.ctx, st.info, rt)
+
+    def read_file(self, path, read_type=None) -> bytes:
+        with self.open_file(path, read_type) as f:
+            return f.read()
+
+    def write_file(self, path, data, write_type=None, block_size=None, **kw) -> None:
+        with self.create_file(path, block_size=block_size, write_type=write_type, **kw) as f:
+            f.write(data)
+
+    # ---- cluster info -------------------------------------------------------------------------
+    def workers(self):
+        return self.ctx.workers(refresh=True)
+
+    def capacity(self) -> tuple[int, int]:
+        info = self.ctx.block_master().GetBlockMasterInfo(pb.block.GetBlockMasterInfoPOptions()).blockMasterInfo
+        return info.capacityBytes, info.usedBytes
+
+    def close(self) -> None:
+        if not self._closed:
+            self._closed = True
+            self.ctx.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+__all__ = ["FileSystem", "URIStatus", "READ_TYPES", "WRITE_TYPES", "enum_name"]

@@ -1,0 +1,682 @@
+"""File and block streams.
+
+Parity: core/client/fs/src/main/java/alluxio/client/file/AlluxioFileInStream.java:66-434 (block
+switching, failed-worker retry, positioned read, passive/async caching trigger :386-420),
+AlluxioFileOutStream.java:56-319 (per-block out streams, UFS stream for THROUGH types,
+completeFile + async persist on close), block/AlluxioBlockStore.java (source selection :149-224:
+local -> remote -> UFS via policy; replicated out streams :281-339), block/stream/
+{BlockInStream,BlockOutStream,GrpcDataReader,GrpcDataWriter,LocalFileDataReader}.java.
+
+Readers fill caller buffers: ``bytes`` / ``bytearray`` / numpy / torch tensors.  When the
+block's worker lives in this process and the destination is a device tensor, the copy is one
+page-gather kernel launch from HBM pages into the tensor (no host round trip).
+"""
+from __future__ import annotations
+
+import io
+import logging
+import queue
+import random
+import threading
+
+from ..proto import enum_name, pb
+from ..utils import ids
+from ..utils.exceptions import (AlluxioStatusException, NotFoundException, UnavailableException)
+from .context import SVC_WORKER, FileSystemContext, worker_address_str
+
+LOG = logging.getLogger(__name__)
+
+HOST, DEVICE = 0, 1
+
+
+def _buffer_ptr(buf):
+    """(pointer, nbytes, kind, keepalive) of a writable/readable buffer."""
+    try:
+        import torch
+        if isinstance(buf, torch.Tensor):
+            if not buf.is_contiguous():
+                raise ValueError("tensor must be contiguous")
+            return buf.data_ptr(), buf.numel() * buf.element_size(), DEVICE if buf.is_cuda else HOST, buf
+    except ImportError:  # pragma: no cover
+        pass
+    import numpy as np
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data, buf.nbytes, HOST, buf
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    return arr.ctypes.data, arr.nbytes, HOST, arr
+
+
+# ----------------------------------------------------------------------------------------------
+# block readers
+class BlockReader:
+    length: int
+
+    def read_into(self, offset: int, length: int, ptr: int, kind: int, stream: int = 0) -> None:
+        raise NotImplementedError
+
+    def read_bytes(self, offset: int, length: int) -> bytes:
+        import numpy as np
+        out = np.empty(length, dtype=np.uint8)
+        self.read_into(offset, length, out.ctypes.data, HOST)
+        return out.tobytes()
+
+    def close(self) -> None:
+        pass
+
+
+class LocalBlockReader(BlockReader):
+    """Reads a block held by a worker in this process (lock for the reader's lifetime)."""
+
+    source = "local"
+
+    def __init__(self, worker, block_id: int, session: int):
+        self.w = worker
+        self.block_id = block_id
+        self.session = session
+        self.lock_id = worker.lock_block(session, block_id)
+        self.length = worker.block_info(block_id).length
+        worker.access_block(session, block_id)
+
+    def read_into(self, offset, length, ptr, kind, stream=0):
+        self.w.read(self.block_id, offset, length, ptr, kind, stream, sync=True)
+
+    def close(self):
+        if self.lock_id is not None:
+            try:
+                self.w.unlock(self.lock_id)
+            finally:
+                self.lock_id = None
+
+
+class _AckQueue:
+    """Request iterator for a bidi stream that the reader feeds with acks."""
+
+    def __init__(self, first):
+        self.q: queue.Queue = queue.Queue()
+        self.q.put(first)
+
+    def __iter__(self):
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            yield item
+
+    def put(self, r):
+        self.q.put(r)
+
+    def close(self):
+        self.q.put(None)
+
+
+class GrpcBlockReader(BlockReader):
+    """Sequential chunked ReadBlock stream with ``offset_received`` acks (GrpcDataReader)."""
+
+    source = "remote"
+
+    def __init__(self, ctx: FileSystemContext, address: str, block_id: int, length: int, ufs_opts=None,
+                 chunk: int | None = None, promote: bool = False):
+        self.ctx = ctx
+        self.address = address
+        self.block_id = block_id
+        self.length = length
+        self.ufs_opts = ufs_opts
+        self.chunk = chunk or ctx.conf.get_bytes("alluxio.user.network.reader.chunk.size.bytes", "1MB")
+        self.promote = promote
+        self._stream = None
+        self._reqs = None
+        self._pos = None
+        self._buf = b""
+        self._buf_off = 0
+
+    def _open(self, offset):
+        self._close_stream()
+        req = pb.block.ReadRequest(block_id=self.block_id, offset=offset, length=self.length - offset,
+                                   chunk_size=self.chunk, promote=self.promote)
+        if self.ufs_opts is not None:
+            req.open_ufs_block_options.CopyFrom(self.ufs_opts)
+        self._reqs = _AckQueue(req)
+        call = self.ctx.worker_channel(self.address).raw_stream(SVC_WORKER, "ReadBlock")
+        self._stream = iter(call(iter(self._reqs)))
+        self._pos = offset
+        self._buf = b""
+        self._buf_off = offset
+
+    def _next_chunk(self):
+        try:
+            resp = next(self._stream)
+        except StopIteration:
+            return b""
+        except Exception as e:  # grpc errors
+            import grpc
+            if isinstance(e, grpc.RpcError):
+                raise AlluxioStatusException.from_status(e.code().value[0], e.details()) from None
+            raise
+        data = resp.chunk.data
+        self._pos += len(data)
+        self._reqs.put(pb.block.ReadRequest(offset_received=self._pos))
+        return data
+
+    def read_bytes(self, offset, length):
+        if self._stream is None or offset < self._buf_off or offset > self._pos:
+            self._open(offset)
+        out = bytearray()
+        while len(out) < length:
+            rel = offset + len(out) - self._buf_off
+            if rel < len(self._buf):
+                take = self._buf[rel:rel + (length - len(out))]
+                out += take
+                continue
+            data = self._next_chunk()
+            if not data:
+                break
+            self._buf_off += len(self._buf)
+            self._buf = data
+        return bytes(out)
+
+    def read_into(self, offset, length, ptr, kind, stream=0):
+        data = self.read_bytes(offset, length)
+        if len(data) != length:
+            raise UnavailableException(f"short read of block {self.block_id}: {len(data)}/{length}")
+        _copy_bytes_to(data, ptr, kind)
+
+    def _close_stream(self):
+        if self._reqs is not None:
+            self._reqs.close()
+        if self._stream is not None:
+            try:
+                for _ in self._stream:
+                    pass
+            except Exception:  # noqa: BLE001
+                pass
+        self._stream = None
+        self._reqs = None
+
+    def close(self):
+        self._close_stream()
+
+
+def _copy_bytes_to(data: bytes, ptr: int, kind: int) -> None:
+    import ctypes
+    if kind == HOST:
+        ctypes.memmove(ptr, data, len(data))
+        return
+    import numpy as np
+    import torch
+    src = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy())
+    from ..ops.native import lib
+    pinned = src.pin_memory()
+    dst = torch.cuda.current_stream()
+    # H2D via the runtime copy engine into the raw device pointer
+    tmp = torch.empty(len(data), dtype=torch.uint8, device="cuda")
+    tmp.copy_(pinned)
+    lib().batched_copy([(tmp.data_ptr(), ptr, len(data))], int(dst.cuda_stream))
+
+
+# ----------------------------------------------------------------------------------------------
+class FileInStream(io.RawIOBase):
+    def __init__(self, ctx: FileSystemContext, status, read_type: str = "CACHE", options=None):
+        super().__init__()
+        self.ctx = ctx
+        self.status = status
+        self.read_type = read_type
+        self.length = status.length
+        self.block_size = status.blockSizeBytes or (64 << 20)
+        self.pos = 0
+        self.session = ids.create_session_id()
+        self._reader: BlockReader | None = None
+        self._reader_idx = -1
+        self._failed: dict[str, int] = {}
+        self.passive_cache = ctx.conf.get_bool("alluxio.user.file.passive.cache.enabled")
+        self.bytes_read = 0
+
+    # ---- io.RawIOBase -------------------------------------------------------------------------
+    def readable(self):
+        return True
+
+    def seekable(self):
+        return True
+
+    def tell(self):
+        return self.pos
+
+    def seek(self, off, whence=io.SEEK_SET):
+        new = {io.SEEK_SET: off, io.SEEK_CUR: self.pos + off, io.SEEK_END: self.length + off}[whence]
+        if new < 0:
+            raise ValueError("negative seek position")
+        self.pos = min(new, self.length)
+        return self.pos
+
+    def readinto(self, b) -> int:
+        mv = memoryview(b).cast("B")
+        n = min(len(mv), self.length - self.pos)
+        if n <= 0:
+            return 0
+        import numpy as np
+        arr = np.frombuffer(mv, dtype=np.uint8, count=n)
+        self._read_range(self.pos, n, arr.ctypes.data, HOST)
+        self.pos += n
+        return n
+
+    def read(self, size=-1) -> bytes:
+        if size is None or size < 0:
+            size = self.length - self.pos
+        size = min(size, self.length - self.pos)
+        if size <= 0:
+            return b""
+        import numpy as np
+        out = np.empty(size, dtype=np.uint8)
+        self._read_range(self.pos, size, out.ctypes.data, HOST)
+        self.pos += size
+        return out.tobytes()
+
+    def readall(self):
+        return self.read(-1)
+
+    # ---- buffer API ---------------------------------------------------------------------------
+    def read_into(self, buf, nbytes: int | None = None, stream: int = 0) -> int:
+        """Read up to ``len(buf)`` bytes at the current position into a host/device buffer."""
+        ptr, cap, kind, _keep = _buffer_ptr(buf)
+        n = min(cap if nbytes is None else nbytes, self.length - self.pos)
+        if n <= 0:
+            return 0
+        self._read_range(self.pos, n, ptr, kind, stream)
+        self.pos += n
+        return n
+
+    def pread(self, position: int, buf, nbytes: int | None = None) -> int:
+        """Positioned read that does not move the stream position."""
+        ptr, cap, kind, _keep = _buffer_ptr(buf)
+        n = min(cap if nbytes is None else nbytes, self.length - position)
+        if n <= 0:
+            return 0
+        self._read_range(position, n, ptr, kind)
+        return n
+
+    # ---- internals ----------------------------------------------------------------------------
+    def _read_range(self, pos: int, n: int, ptr: int, kind: int, stream: int = 0) -> None:
+        done = 0
+        while done < n:
+            idx = (pos + done) // self.block_size
+            off = (pos + done) - idx * self.block_size
+            reader = self._reader_for(idx)
+            take = min(n - done, reader.length - off)
+            if take <= 0:
+                raise UnavailableException(f"block {idx} of {self.status.path} is shorter than expected")
+            reader.read_into(off, take, ptr + done, kind, stream)
+            done += take
+        self.bytes_read += n
+        self.ctx.metrics.counter("BytesReadClient").inc(n)
+        if kind == DEVICE:
+            self.ctx.metrics.counter("BytesReadDevice").inc(n)
+
+    def _reader_for(self, idx: int) -> BlockReader:
+        if self._reader is not None and self._reader_idx == idx:
+            return self._reader
+        self._close_reader()
+        fbi = self.status.fileBlockInfos[idx]
+        self._reader = self._open_block(fbi, idx)
+        self._reader_idx = idx
+        return self._reader
+
+    def _open_block(self, fbi, idx: int) -> BlockReader:
+        bi = fbi.blockInfo
+        block_len = bi.length if bi.length else min(self.block_size, self.length - idx * self.block_size)
+        locs = [l for l in bi.locations if worker_address_str(l.workerAddress) not in self._failed]
+        inproc = [l for l in locs if self.ctx.in_process_worker(l.workerAddress) is not None]
+        last_err = None
+        # 1) a worker in this process holding the block
+        for l in inproc:
+            w = self.ctx.in_process_worker(l.workerAddress)
+            try:
+                return LocalBlockReader(w, bi.blockId, self.session)
+            except NotFoundException as e:
+                last_err = e
+                self._failed[worker_address_str(l.workerAddress)] = 1
+        # 2) a remote (or same-node, other process) worker over the data server
+        others = [l for l in locs if l not in inproc]
+        others.sort(key=lambda l: 0 if self.ctx.is_local(l.workerAddress) else 1)
+        for l in others:
+            addr = worker_address_str(l.workerAddress)
+            try:
+                r = GrpcBlockReader(self.ctx, addr, bi.blockId, block_len)
+                self._maybe_passive_cache(bi.blockId, l.workerAddress, block_len)
+                return r
+            except Exception as e:  # noqa: BLE001
+                last_err = e
+                self._failed[addr] = 1
+        # 3) UFS through a worker chosen by the UFS read policy
+        if self.status.persisted and self.status.ufsPath:
+            opts = pb.dataserver.OpenUfsBlockOptions(
+                ufs_path=self.status.ufsPath, offset_in_file=idx * self.block_size, block_size=block_len,
+                mountId=self.status.mountId, no_cache=self.read_type == "NO_CACHE")
+            from .policy import create_policy
+            pol = create_policy(self.ctx.conf.get("alluxio.user.ufs.block.read.location.policy"), self.ctx.conf)
+            workers = self.ctx.workers()
+            w = pol.get_worker(workers, bi.blockId, block_len, self.ctx) if workers else None
+            if w is not None:
+                lw = self.ctx.in_process_worker(w.address)
+                if lw is not None and not opts.no_cache:
+                    lw.cache_block_from_ufs(bi.blockId, opts, self.session)
+                    self.ctx.metrics.counter("BytesReadUfs").inc(block_len)
+                    return LocalBlockReader(lw, bi.blockId, self.session)
+                return GrpcBlockReader(self.ctx, worker_address_str(w.address), bi.blockId, block_len, ufs_opts=opts)
+        raise UnavailableException(f"Block {bi.blockId} of {self.status.path} is not available "
+                                   f"(no live location{'' if self.status.persisted else ', not persisted'})"
+                                   + (f": {last_err}" if last_err else ""))
+
+    def _maybe_passive_cache(self, block_id: int, source_addr, length: int) -> None:
+        if not self.passive_cache or self.read_type == "NO_CACHE":
+            return
+        for w in self.ctx.workers():
+            if self.ctx.is_local(w.address) and worker_address_str(w.address) != worker_address_str(source_addr):
+                try:
+                    self.ctx.worker_stub(worker_address_str(w.address)).AsyncCache(pb.block.AsyncCacheRequest(
+                        block_id=block_id, source_host=source_addr.host, source_port=source_addr.rpcPort,
+                        length=length))
+                except Exception:  # noqa: BLE001
+                    LOG.debug("passive cache request failed", exc_info=True)
+                return
+
+    def _close_reader(self) -> None:
+        if self._reader is not None:
+            try:
+                self._reader.close()
+            finally:
+                self._reader = None
+                self._reader_idx = -1
+
+    def close(self) -> None:
+        if not self.closed:
+            self._close_reader()
+            for l in []:
+                pass
+        super().close()
+
+
+# ----------------------------------------------------------------------------------------------
+# writers
+class BlockWriter:
+    def write_ptr(self, offset, ptr, length, kind) -> None:
+        raise NotImplementedError
+
+    def commit(self) -> None:
+        raise NotImplementedError
+
+    def cancel(self) -> None:
+        raise NotImplementedError
+
+
+class LocalBlockWriter(BlockWriter):
+    def __init__(self, worker, block_id, session, tier=0, medium="", initial=1 << 20, pin=False):
+        self.w = worker
+        self.block_id = block_id
+        self.session = session
+        worker.create_block(session, block_id, tier, medium, initial, pin)
+        self.pin = pin
+
+    def write_ptr(self, offset, ptr, length, kind):
+        self.w.write_ptr(self.session, self.block_id, offset, ptr, length, kind)
+
+    def commit(self):
+        self.w.commit_block(self.session, self.block_id, self.pin)
+
+    def cancel(self):
+        try:
+            self.w.abort_block(self.session, self.block_id)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class GrpcBlockWriter(BlockWriter):
+    """WriteBlock stream (GrpcDataWriter): command, chunks, then half-close -> commit."""
+
+    def __init__(self, ctx, address, block_id, tier=0, medium="", reserve=1 << 20, pin=False,
+                 chunk: int | None = None):
+        self.chunk = chunk or ctx.conf.get_bytes("alluxio.user.network.writer.chunk.size.bytes", "1MB")
+        self._reqs = _AckQueue(pb.block.WriteRequest(command=pb.block.WriteRequestCommand(
+            type=0, id=block_id, offset=0, tier=tier, medium_type=medium, space_to_reserve=reserve,
+            pin_on_create=pin)))
+        call = ctx.worker_channel(address).raw_stream(SVC_WORKER, "WriteBlock")
+        self._resp = call(iter(self._reqs))
+        self._result = []
+        self._err = []
+
+        def drain():
+            try:
+                for r in self._resp:
+                    self._result.append(r)
+            except Exception as e:  # noqa: BLE001
+                self._err.append(e)
+        self._t = threading.Thread(target=drain, daemon=True)
+        self._t.start()
+
+    def write_ptr(self, offset, ptr, length, kind):
+        import ctypes
+        if kind == DEVICE:
+            import torch
+            from ..ops.native import lib
+            tmp = torch.empty(length, dtype=torch.uint8, device="cuda")
+            lib().batched_copy([(ptr, tmp.data_ptr(), length)], 0)
+            data = tmp.cpu().numpy().tobytes()
+        else:
+            data = ctypes.string_at(ptr, length)
+        for i in range(0, len(data), self.chunk):
+            self._reqs.put(pb.block.WriteRequest(chunk=pb.block.Chunk(data=data[i:i + self.chunk])))
+
+    def commit(self):
+        self._reqs.close()
+        self._t.join()
+        if self._err:
+            e = self._err[0]
+            import grpc
+            if isinstance(e, grpc.RpcError):
+                raise AlluxioStatusException.from_status(e.code().value[0], e.details())
+            raise e
+
+    def cancel(self):
+        try:
+            self._resp.cancel()
+        except Exception:  # noqa: BLE001
+            pass
+        self._reqs.close()
+
+
+class UfsWriter:
+    """THROUGH / CACHE_THROUGH UFS stream (via the local worker's UFS client or a WriteBlock
+    UFS_FILE stream to a worker — reference UfsFileWriteHandler)."""
+
+    def __init__(self, ctx, status, worker_addr=None, local_worker=None):
+        self.length = 0
+        self._local = None
+        self._grpc = None
+        opts = pb.dataserver.CreateUfsFileOptions(ufs_path=status.ufsPath, owner=status.owner, group=status.group,
+                                                  mode=status.mode, mount_id=status.mountId)
+        if local_worker is not None:
+            from ..underfs.base import CreateOptions
+            ufs = local_worker._ufs_for(pb.dataserver.OpenUfsBlockOptions(ufs_path=status.ufsPath,
+                                                                          mountId=status.mountId))
+            self._local = ufs.create(status.ufsPath, CreateOptions(create_parent=True, ensure_atomic=True,
+                                                                   mode=status.mode or 0o644))
+            self._ufs = ufs
+            self._path = status.ufsPath
+        else:
+            self._q = _AckQueue(pb.block.WriteRequest(command=pb.block.WriteRequestCommand(
+                type=1, id=status.fileId, create_ufs_file_options=opts)))
+            call = ctx.worker_channel(worker_addr).raw_stream(SVC_WORKER, "WriteBlock")
+            self._grpc = call(iter(self._q))
+            self._err = []
+            self._t = threading.Thread(target=self._drain, daemon=True)
+            self._t.start()
+
+    def _drain(self):
+        try:
+            for _ in self._grpc:
+                pass
+        except Exception as e:  # noqa: BLE001
+            self._err.append(e)
+
+    def write(self, data: bytes) -> None:
+        self.length += len(data)
+        if self._local is not None:
+            self._local.write(data)
+        else:
+            for i in range(0, len(data), 1 << 20):
+                self._q.put(pb.block.WriteRequest(chunk=pb.block.Chunk(data=data[i:i + (1 << 20)])))
+
+    def close(self) -> None:
+        if self._local is not None:
+            self._local.close()
+        else:
+            self._q.close()
+            self._t.join()
+            if self._err:
+                raise UnavailableException(f"UFS write failed: {self._err[0]}")
+
+    def cancel(self) -> None:
+        try:
+            if self._local is not None:
+                self._local.close()
+                self._ufs.delete_file(self._path)
+            else:
+                self._grpc.cancel()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class FileOutStream(io.RawIOBase):
+    def __init__(self, ctx: FileSystemContext, status, write_type: str, replication_durable: int = 1,
+                 write_tier: int = 0, medium: str = "", persistence_wait_ms: int = 0):
+        super().__init__()
+        self.ctx = ctx
+        self.status = status
+        self.path = status.path
+        self.write_type = write_type
+        self.block_size = status.blockSizeBytes
+        self.session = ids.create_session_id()
+        self.write_tier = write_tier
+        self.medium = medium
+        self.persistence_wait_ms = persistence_wait_ms
+        self.cache = write_type in ("MUST_CACHE", "CACHE_THROUGH", "ASYNC_THROUGH", "TRY_CACHE")
+        self.through = write_type in ("CACHE_THROUGH", "THROUGH")
+        self.replicas = replication_durable if write_type == "ASYNC_THROUGH" and replication_durable > 1 else 1
+        from .policy import create_policy
+        self.policy = create_policy(ctx.conf.get("alluxio.user.block.write.location.policy.class"), ctx.conf)
+        self._writers: list[BlockWriter] = []
+        self._block_written = 0
+        self._pos = 0
+        self._ufs = None
+        self._canceled = False
+        self._workers = None
+        if self.through:
+            workers = ctx.workers()
+            w = self.policy.get_worker(workers, 0, 0, ctx) if workers else None
+            lw = ctx.in_process_worker(w.address) if w is not None else None
+            if w is None:
+                raise UnavailableException("no worker available for the UFS stream")
+            self._ufs = UfsWriter(ctx, status, worker_address_str(w.address), lw)
+
+    def writable(self):
+        return True
+
+    def tell(self):
+        return self._pos
+
+    def write(self, data) -> int:
+        ptr, n, kind, keep = _buffer_ptr(data)
+        if n == 0:
+            return 0
+        if self.through:
+            if kind == DEVICE:
+                import torch
+                host = keep.detach().reshape(-1).view(torch.uint8).cpu().numpy().tobytes()
+            else:
+                import ctypes
+                host = ctypes.string_at(ptr, n)
+            self._ufs.write(host)
+        if self.cache:
+            self._write_cache(ptr, n, kind)
+        self._pos += n
+        return n
+
+    def _write_cache(self, ptr, n, kind):
+        done = 0
+        while done < n:
+            if not self._writers or self._block_written >= self.block_size:
+                self._next_block()
+            take = min(n - done, self.block_size - self._block_written)
+            for w in self._writers:
+                w.write_ptr(self._block_written, ptr + done, take, kind)
+            self._block_written += take
+            done += take
+
+    def _next_block(self) -> None:
+        self._finish_block()
+        bid = self.ctx.fs_master().GetNewBlockIdForFile(pb.file.GetNewBlockIdForFilePRequest(path=self.path)).id
+        workers = self._workers if self._workers is not None else self.ctx.workers(refresh=self._workers is None)
+        self._workers = workers
+        chosen = []
+        cands = list(workers)
+        for _ in range(self.replicas):
+            w = self.policy.get_worker(cands, bid, self.block_size, self.ctx)
+            if w is None:
+                break
+            chosen.append(w)
+            cands = [c for c in cands if worker_address_str(c.address) != worker_address_str(w.address)]
+        if not chosen:
+            raise UnavailableException("no worker available to write the block")
+        reserve = min(self.block_size, self.ctx.conf.get_bytes("alluxio.user.file.buffer.bytes", "8MB"))
+        for w in chosen:
+            lw = self.ctx.in_process_worker(w.address)
+            if lw is not None:
+                self._writers.append(LocalBlockWriter(lw, bid, self.session, self.write_tier, self.medium,
+                                                      max(1, reserve)))
+            else:
+                self._writers.append(GrpcBlockWriter(self.ctx, worker_address_str(w.address), bid,
+                                                     self.write_tier, self.medium, reserve))
+        self._block_written = 0
+
+    def _finish_block(self) -> None:
+        for w in self._writers:
+            w.commit()
+        self._writers = []
+
+    def cancel(self) -> None:
+        self._canceled = True
+        for w in self._writers:
+            w.cancel()
+        self._writers = []
+        if self._ufs is not None:
+            self._ufs.cancel()
+        try:
+            self.ctx.fs_master().Remove(pb.file.DeletePRequest(path=self.path, options=pb.file.DeletePOptions(
+                alluxioOnly=True, unchecked=True)))
+        except Exception:  # noqa: BLE001
+            pass
+        super().close()
+
+    def close(self) -> None:
+        if self.closed:
+            return
+        if self._canceled:
+            return
+        try:
+            self._finish_block()
+            opts = pb.file.CompleteFilePOptions()
+            if self._ufs is not None:
+                self._ufs.close()
+                opts.ufsLength = self._ufs.length
+            if self.write_type == "ASYNC_THROUGH":
+                opts.asyncPersistOptions.persistenceWaitTime = self.persistence_wait_ms
+            self.ctx.fs_master().CompleteFile(pb.file.CompleteFilePRequest(path=self.path, options=opts))
+        except Exception:
+            for w in self._writers:
+                w.cancel()
+            raise
+        finally:
+            super().close()
+        self.ctx.metrics.counter("BytesWrittenClient").inc(self._pos)
+
+
+__all__ = ["FileInStream", "FileOutStream", "LocalBlockReader", "GrpcBlockReader", "LocalBlockWriter",
+           "GrpcBlockWriter", "HOST", "DEVICE", "random", "enum_name"]

@@ -244,6 +244,28 @@ PYBIND11_MODULE(_C, m) {
       .def("device", &BlockStore::device)
       .def("stats", &BlockStore::stats, G());
 
+  py::class_<ReadSession>(m, "ReadSession")
+      .def(py::init<BlockStore*, int64_t, const std::vector<int64_t>&, const std::vector<uint64_t>&,
+                    const std::vector<uint64_t>&, uint64_t, int, const std::vector<uint64_t>&>(),
+           py::arg("store"), py::arg("session"), py::arg("block_ids"), py::arg("block_lens"), py::arg("dst_ptrs"),
+           py::arg("buf_bytes"), py::arg("dst_kind"), py::arg("start_offsets") = std::vector<uint64_t>{},
+           py::keep_alive<1, 2>())
+      .def("step", [](ReadSession& r, uint64_t stream) {
+             std::vector<int> reopened;
+             uint64_t b;
+             {
+               py::gil_scoped_release rel;
+               b = r.step(stream, &reopened);
+             }
+             return py::make_tuple(b, reopened);
+           }, py::arg("stream") = 0)
+      .def("run", &ReadSession::run, G(), py::arg("steps"), py::arg("stream") = 0)
+      .def("reset_file", &ReadSession::reset_file, G())
+      .def("close", &ReadSession::close, G())
+      .def("position", &ReadSession::position)
+      .def_property_readonly("total_bytes", &ReadSession::total_bytes)
+      .def_property_readonly("reopens", &ReadSession::reopens);
+
   // ---- codecs / kernels ------------------------------------------------------------------
   m.def("device_count", &hip_device_count);
   m.def("crc32c", [](py::bytes data, uint32_t crc) {

@@ -1080,3 +1080,122 @@ std::string BlockStore::stats() {
 }
 
 }  // namespace amdx
+
+namespace amdx {
+
+int64_t BlockStore::try_lock_block(int64_t session, int64_t block_id, bool write) {
+  try {
+    return lock_block(session, block_id, write, 30000);
+  } catch (const StoreError& e) {
+    if (e.code == kErrNotFound) return -1;
+    throw;
+  }
+}
+
+// -------------------------------------------------------------------------------------------
+// ReadSession
+ReadSession::ReadSession(BlockStore* store, int64_t session, const std::vector<int64_t>& block_ids,
+                         const std::vector<uint64_t>& block_lens, const std::vector<uint64_t>& dst_ptrs,
+                         uint64_t buf_bytes, int dst_kind, const std::vector<uint64_t>& start_offsets)
+    : store_(store), session_(session), dst_(dst_ptrs), buf_(buf_bytes), kind_(dst_kind) {
+  if (buf_ == 0) throw StoreError(kErrInvalidArgument, "buffer size must be > 0");
+  reset_file(block_ids, block_lens);
+  const size_t n = dst_.size();
+  pos_.assign(n, 0);
+  for (size_t i = 0; i < n && i < start_offsets.size(); ++i) pos_[i] = file_len_ ? start_offsets[i] % file_len_ : 0;
+  cur_block_idx_.assign(n, -1);
+  lock_.assign(n, -1);
+  reqs_.reserve(2 * n);
+}
+
+ReadSession::~ReadSession() {
+  try { close(); } catch (...) {}
+}
+
+void ReadSession::reset_file(const std::vector<int64_t>& block_ids, const std::vector<uint64_t>& block_lens) {
+  if (block_ids.size() != block_lens.size()) throw StoreError(kErrInvalidArgument, "block id/len size mismatch");
+  blocks_ = block_ids;
+  lens_ = block_lens;
+  starts_.assign(blocks_.size(), 0);
+  file_len_ = 0;
+  for (size_t b = 0; b < blocks_.size(); ++b) {
+    starts_[b] = file_len_;
+    file_len_ += lens_[b];
+  }
+}
+
+void ReadSession::switch_block(int i, int64_t b) {
+  if (cur_block_idx_[i] == b) return;
+  if (lock_[i] >= 0) {
+    store_->unlock(lock_[i]);
+    lock_[i] = -1;
+  }
+  cur_block_idx_[i] = -1;
+  if (b >= 0) {
+    const int64_t l = store_->try_lock_block(session_, blocks_[b], false);
+    if (l < 0) throw StoreError(kErrNotFound, "block " + std::to_string(blocks_[b]) + " is not cached on this worker");
+    lock_[i] = l;
+    cur_block_idx_[i] = b;
+  }
+}
+
+uint64_t ReadSession::step(uint64_t stream, std::vector<int>* reopened) {
+  if (closed_) throw StoreError(kErrInvalidState, "read session closed");
+  reqs_.clear();
+  uint64_t bytes = 0;
+  std::vector<int64_t> touched;
+  for (size_t i = 0; i < dst_.size(); ++i) {
+    uint64_t p = pos_[i];
+    if (p >= file_len_) {  // read() returned -1: close + re-open at offset 0
+      switch_block((int)i, -1);
+      pos_[i] = 0;
+      ++reopens_;
+      if (reopened) reopened->push_back((int)i);
+      continue;
+    }
+    uint64_t want = std::min(buf_, file_len_ - p);
+    uint64_t out = 0;
+    while (want > 0) {
+      // block index of position p (blocks are few; linear from the current block)
+      int64_t b = cur_block_idx_[i] >= 0 ? cur_block_idx_[i] : 0;
+      if (p < starts_[b]) b = 0;
+      while (b + 1 < (int64_t)blocks_.size() && p >= starts_[b + 1]) ++b;
+      switch_block((int)i, b);
+      const uint64_t off = p - starts_[b];
+      const uint64_t n = std::min(want, lens_[b] - off);
+      reqs_.push_back(ReadReq{blocks_[b], off, n, dst_[i] + out, kind_});
+      touched.push_back(blocks_[b]);
+      p += n;
+      out += n;
+      want -= n;
+    }
+    pos_[i] = p;
+    bytes += out;
+  }
+  if (!reqs_.empty()) store_->read_batch(reqs_, stream, false);
+  // annotate accesses once per distinct block per step (LRU/LRFU clock)
+  std::sort(touched.begin(), touched.end());
+  touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+  store_->access_blocks(touched);
+  total_ += bytes;
+  return bytes;
+}
+
+uint64_t ReadSession::run(int steps, uint64_t stream) {
+  uint64_t b = 0;
+  for (int s = 0; s < steps; ++s) b += step(stream, nullptr);
+  return b;
+}
+
+void ReadSession::close() {
+  if (closed_) return;
+  closed_ = true;
+  for (size_t i = 0; i < lock_.size(); ++i) {
+    if (lock_[i] >= 0) {
+      try { store_->unlock(lock_[i]); } catch (...) {}
+      lock_[i] = -1;
+    }
+  }
+}
+
+}  // namespace amdx

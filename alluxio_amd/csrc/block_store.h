@@ -157,6 +157,8 @@ class BlockStore {
   // Batched read of committed (or own temp) blocks into caller buffers.  Device-arena ->
   // device-dst segments are executed by one batched copy launch per ring slot.
   void read_batch(const std::vector<ReadReq>& reqs, uint64_t stream, bool sync);
+  // Lock a block if it exists; returns -1 (no throw) when it does not.
+  int64_t try_lock_block(int64_t session, int64_t block_id, bool write);
   // CRC32C per piece (piece = page size when 0).
   std::vector<uint32_t> checksum(int64_t block_id, uint64_t piece_bytes);
   void fill_pattern(int64_t session, int64_t block_id, uint64_t length, uint64_t seed);
@@ -254,6 +256,44 @@ class BlockStore {
   // checksum scratch
   uint32_t* crc_dev_ = nullptr;
   size_t crc_cap_ = 0;
+};
+
+// Many concurrent sequential readers of one file, advanced in lockstep: the native form of
+// StressWorkerBench's reader threads (stress/shell/.../StressWorkerBench.java:251-276: each
+// thread loops read(buf) and re-opens the file at EOF).  Every ``step`` advances every stream by
+// one read of ``buf_bytes`` (or the EOF read that triggers a re-open), keeps a read lock on each
+// stream's current block (switching locks at block boundaries like BlockInStream), and executes
+// all the stream reads as ONE batched page-gather launch.
+class ReadSession {
+ public:
+  ReadSession(BlockStore* store, int64_t session, const std::vector<int64_t>& block_ids,
+              const std::vector<uint64_t>& block_lens, const std::vector<uint64_t>& dst_ptrs,
+              uint64_t buf_bytes, int dst_kind, const std::vector<uint64_t>& start_offsets);
+  ~ReadSession();
+  // Returns bytes read in this step; `reopened` receives the streams that hit EOF.
+  uint64_t step(uint64_t stream, std::vector<int>* reopened);
+  uint64_t run(int steps, uint64_t stream);  // many steps, no per-step return to Python
+  void reset_file(const std::vector<int64_t>& block_ids, const std::vector<uint64_t>& block_lens);
+  void close();
+  uint64_t total_bytes() const { return total_; }
+  uint64_t reopens() const { return reopens_; }
+  uint64_t position(int i) const { return pos_.at(i); }
+
+ private:
+  void switch_block(int i, int64_t blk);
+  BlockStore* store_;
+  int64_t session_;
+  std::vector<int64_t> blocks_;
+  std::vector<uint64_t> lens_, starts_;
+  uint64_t file_len_ = 0;
+  std::vector<uint64_t> dst_;
+  uint64_t buf_;
+  int kind_;
+  std::vector<uint64_t> pos_;
+  std::vector<int64_t> cur_block_idx_, lock_;
+  std::vector<ReadReq> reqs_;
+  uint64_t total_ = 0, reopens_ = 0;
+  bool closed_ = false;
 };
 
 }  // namespace amdx

@@ -1,0 +1,330 @@
+"""Journal system: replay, batched asynchronous writes, checkpoints, standby tailing.
+
+Parity: JournalSystem SPI (core/server/common/.../journal/JournalSystem.java: start/stop,
+gainPrimacy/losePrimacy, checkpoint, format), ``Journaled.processJournalEntry`` /
+``resetState`` / ``getJournalEntryIterator`` contract, ``JournalContext.append`` +
+``close()`` waiting for flush (MasterJournalContext.java:35-93), AsyncJournalWriter.java:48-382
+(queue + flush thread batching for ``alluxio.master.journal.flush.batch.time``, flush tickets),
+UfsJournalCheckpointThread (standby tails logs and writes checkpoints), NoopJournalSystem.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+
+from ..utils.exceptions import JournalClosedException, UnavailableException
+from . import format as fmt
+from .ufs_journal import UfsJournal, UfsJournalLogWriter
+
+LOG = logging.getLogger(__name__)
+
+
+class Journaled:
+    """Mixin for journaled master state."""
+
+    journal_name = "Unnamed"
+
+    def process_journal_entry(self, entry) -> bool:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def reset_state(self) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def journal_entries(self):  # pragma: no cover - interface
+        """Iterate JournalEntry protos that recreate the current state (checkpoint content)."""
+        raise NotImplementedError
+
+    def apply_and_journal(self, ctx, entry) -> None:
+        if not self.process_journal_entry(entry):
+            raise RuntimeError(f"{self.journal_name} cannot apply its own entry {entry}")
+        ctx.append(entry)
+
+
+class AsyncJournalWriter:
+    def __init__(self, writer: UfsJournalLogWriter, batch_ms: float = 5.0, flush_timeout_s: float = 300.0):
+        self.writer = writer
+        self.batch = batch_ms / 1000.0
+        self.flush_timeout = flush_timeout_s
+        self._cond = threading.Condition()
+        self._queue: list = []
+        self._appended = 0       # counter of appended entries
+        self._flushed = 0        # counter of durably flushed entries
+        self._error: BaseException | None = None
+        self._closed = False
+        self._thread = threading.Thread(target=self._run, daemon=True, name="journal-flush")
+        self._thread.start()
+
+    def append(self, entry) -> int:
+        with self._cond:
+            if self._closed:
+                raise JournalClosedException("journal is closed")
+            if self._error is not None:
+                raise UnavailableException(f"journal write failed: {self._error}")
+            self._queue.append(entry)
+            self._appended += 1
+            self._cond.notify_all()
+            return self._appended
+
+    def flush(self, counter: int) -> None:
+        deadline = time.monotonic() + self.flush_timeout
+        with self._cond:
+            while self._flushed < counter:
+                if self._error is not None:
+                    raise UnavailableException(f"journal flush failed: {self._error}")
+                if self._closed and not self._queue and self._flushed < counter:
+                    raise JournalClosedException("journal closed before flush")
+                rem = deadline - time.monotonic()
+                if rem <= 0:
+                    raise UnavailableException("journal flush timed out")
+                self._cond.notify_all()
+                self._cond.wait(min(rem, 0.05))
+
+    def _run(self) -> None:
+        while True:
+            with self._cond:
+                while not self._queue and not self._closed:
+                    self._cond.wait(0.1)
+                if not self._queue and self._closed:
+                    return
+            # batch window: let concurrent RPCs pile up (flush.batch.time)
+            if self.batch > 0:
+                time.sleep(self.batch)
+            with self._cond:
+                batch, self._queue = self._queue, []
+            try:
+                for e in batch:
+                    self.writer.write(e)
+                self.writer.flush()
+                with self._cond:
+                    self._flushed += len(batch)
+                    self._cond.notify_all()
+            except BaseException as e:  # noqa: BLE001
+                LOG.exception("journal flush failed")
+                with self._cond:
+                    self._error = e
+                    self._cond.notify_all()
+                return
+
+    def close(self) -> None:
+        with self._cond:
+            self._closed = True
+            self._cond.notify_all()
+        self._thread.join(timeout=10)
+        self.writer.close()
+
+
+class JournalContext:
+    """Collects entries for one RPC; ``close`` blocks until they are durable."""
+
+    def __init__(self, writer: AsyncJournalWriter | None, state_lock=None):
+        self._writer = writer
+        self._last = 0
+        self._state_lock = state_lock
+
+    def append(self, entry) -> None:
+        if self._writer is not None:
+            self._last = self._writer.append(entry)
+
+    def close(self) -> None:
+        if self._writer is not None and self._last:
+            self._writer.flush(self._last)
+
+    def __enter__(self):
+        if self._state_lock is not None:
+            self._state_lock.acquire_shared()
+        return self
+
+    def __exit__(self, *exc):
+        try:
+            self.close()
+        finally:
+            if self._state_lock is not None:
+                self._state_lock.release_shared()
+
+
+class NoopJournalContext(JournalContext):
+    def __init__(self, state_lock=None):
+        super().__init__(None, state_lock)
+
+
+class JournalSystem:
+    def __init__(self):
+        self._journaled: dict[str, Journaled] = {}
+        self.primary = False
+
+    def register(self, j: Journaled) -> None:
+        self._journaled[j.journal_name] = j
+
+    @property
+    def journaled(self) -> dict[str, Journaled]:
+        return dict(self._journaled)
+
+    def start(self) -> None: ...
+
+    def stop(self) -> None: ...
+
+    def gain_primacy(self) -> None:
+        self.primary = True
+
+    def lose_primacy(self) -> None:
+        self.primary = False
+
+    def create_context(self, name: str, state_lock=None) -> JournalContext:
+        return NoopJournalContext(state_lock)
+
+    def checkpoint(self) -> None: ...
+
+    def format(self) -> None: ...
+
+    def is_formatted(self) -> bool:
+        return True
+
+    def is_empty(self) -> bool:
+        return True
+
+    def sequence_numbers(self) -> dict[str, int]:
+        return {}
+
+
+class NoopJournalSystem(JournalSystem):
+    """No persistence (tests, ephemeral masters)."""
+
+
+class UfsJournalSystem(JournalSystem):
+    def __init__(self, root: str, max_log_bytes: int = 10 << 20, flush_batch_ms: float = 5.0,
+                 checkpoint_period_entries: int = 2_000_000, fsync: bool = True):
+        super().__init__()
+        self.root = root
+        self.max_log_bytes = max_log_bytes
+        self.flush_batch_ms = flush_batch_ms
+        self.checkpoint_period = checkpoint_period_entries
+        self.fsync = fsync
+        self._journals: dict[str, UfsJournal] = {}
+        self._writers: dict[str, AsyncJournalWriter] = {}
+        self._applied: dict[str, int] = {}
+        self._lock = threading.RLock()
+        self._tail_thread = None
+        self._tail_stop = threading.Event()
+
+    def register(self, j: Journaled) -> None:
+        super().register(j)
+        self._journals[j.journal_name] = UfsJournal(self.root, j.journal_name, self.max_log_bytes)
+
+    def format(self) -> None:
+        for j in self._journals.values():
+            j.format()
+
+    def is_formatted(self) -> bool:
+        return all(j.is_formatted() for j in self._journals.values())
+
+    def is_empty(self) -> bool:
+        return all(not j.logs() and not j.checkpoints() for j in self._journals.values())
+
+    def start(self) -> None:
+        for j in self._journals.values():
+            j.ensure()
+        # standby: replay what exists and keep tailing until primacy
+        self._replay_all()
+        self._tail_stop.clear()
+        self._tail_thread = threading.Thread(target=self._tail_loop, daemon=True, name="journal-tailer")
+        self._tail_thread.start()
+
+    def _replay_all(self) -> None:
+        with self._lock:
+            for name, j in self._journals.items():
+                comp = self._journaled[name]
+                comp.reset_state()
+                ctype, payload, end = j.read_checkpoint()
+                applied = 0
+                if ctype is not None:
+                    self._apply_checkpoint(comp, ctype, payload)
+                    applied = end
+                for e in j.iter_log_entries(applied):
+                    self._apply(comp, e)
+                    applied = e.sequence_number + 1
+                self._applied[name] = applied
+
+    @staticmethod
+    def _apply(comp: Journaled, e) -> None:
+        if e.journal_entries:
+            for sub in e.journal_entries:
+                comp.process_journal_entry(sub)
+        elif not comp.process_journal_entry(e):
+            LOG.warning("%s ignored journal entry %s", comp.journal_name, e.WhichOneof)
+
+    def _apply_checkpoint(self, comp, ctype, payload) -> None:
+        if ctype == fmt.CheckpointType.JOURNAL_ENTRY:
+            for e in fmt.bytes_to_entries(payload):
+                self._apply(comp, e)
+        else:
+            raise RuntimeError(f"unsupported checkpoint type {ctype}")
+
+    def _tail_loop(self) -> None:
+        while not self._tail_stop.wait(0.5):
+            if self.primary:
+                return
+            try:
+                with self._lock:
+                    for name, j in self._journals.items():
+                        comp = self._journaled[name]
+                        start = self._applied.get(name, 0)
+                        for e in j.iter_log_entries(start):
+                            self._apply(comp, e)
+                            self._applied[name] = e.sequence_number + 1
+            except Exception:  # noqa: BLE001
+                LOG.exception("journal tailing failed")
+
+    def gain_primacy(self) -> None:
+        self._tail_stop.set()
+        if self._tail_thread is not None:
+            self._tail_thread.join(timeout=5)
+        with self._lock:
+            # catch up fully, then become the writer
+            self._replay_all()
+            for name, j in self._journals.items():
+                nxt = max(self._applied.get(name, 0), j.next_sequence_number())
+                w = UfsJournalLogWriter(j, nxt, fsync=self.fsync)
+                self._writers[name] = AsyncJournalWriter(w, self.flush_batch_ms)
+        super().gain_primacy()
+
+    def lose_primacy(self) -> None:
+        self._close_writers()
+        super().lose_primacy()
+
+    def _close_writers(self) -> None:
+        for w in self._writers.values():
+            w.close()
+        self._writers.clear()
+
+    def stop(self) -> None:
+        self._tail_stop.set()
+        self._close_writers()
+
+    def create_context(self, name: str, state_lock=None) -> JournalContext:
+        w = self._writers.get(name)
+        if w is None:
+            raise UnavailableException(f"journal for {name} is not writable (not primary)")
+        return JournalContext(w, state_lock)
+
+    def checkpoint(self) -> None:
+        """Snapshot every component at its current sequence number and GC old files."""
+        with self._lock:
+            for name, j in self._journals.items():
+                w = self._writers.get(name)
+                comp = self._journaled[name]
+                if w is not None:
+                    w.flush(w._appended)
+                    end = w.writer.next_seq
+                else:
+                    end = self._applied.get(name, 0)
+                payload = fmt.entries_to_bytes(comp.journal_entries())
+                j.write_checkpoint(end, fmt.CheckpointType.JOURNAL_ENTRY, payload)
+                j.gc()
+
+    def sequence_numbers(self) -> dict[str, int]:
+        out = {}
+        for name, j in self._journals.items():
+            w = self._writers.get(name)
+            out[name] = w.writer.next_seq if w else self._applied.get(name, 0)
+        return out

@@ -1,0 +1,439 @@
+"""Block master: worker registry, block locations, container ids, lost-worker detection.
+
+Parity: core/server/master/src/main/java/alluxio/master/block/DefaultBlockMaster.java
+(getNewContainerId :628 journaled BlockContainerIdGeneratorEntry; commitBlock :670-716 journaled
+BlockInfoEntry + location; getWorkerId :844-866 reusing ids for known addresses; workerRegister
+:869-913; workerHeartbeat :916-950 returning Nothing/Register/Free; generateBlockInfo
+:1037-1072; LostWorkerDetectionHeartbeatExecutor :1087-1113), MasterWorkerInfo.java (per-worker
+capacity/usage per tier, blocks, to-be-removed blocks), the worker sets kept in IndexedSets.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+
+from ..journal.system import Journaled
+from ..proto import pb
+from ..utils import ids
+from ..utils.collections import IndexedSet
+from ..utils.exceptions import BlockDoesNotExistException, NotFoundException
+
+LOG = logging.getLogger(__name__)
+
+CONTAINER_BATCH = 1000  # container ids reserved per journal entry
+
+
+def address_key(addr) -> tuple:
+    return (addr.host, addr.rpcPort, addr.dataPort, addr.domainSocketPath)
+
+
+class MasterWorkerInfo:
+    def __init__(self, worker_id: int, address):
+        self.id = worker_id
+        self.address = address
+        self.start_time_ms = int(time.time() * 1000)
+        self.last_updated_ms = int(time.time() * 1000)
+        self.registered = False
+        self.storage_tiers: list[str] = []
+        self.capacity: dict[str, int] = {}
+        self.used: dict[str, int] = {}
+        self.blocks: set[int] = set()
+        self.to_remove: set[int] = set()
+        self.lost_storage: dict[str, list[str]] = {}
+        self.lock = threading.RLock()
+
+    @property
+    def key(self):
+        return address_key(self.address)
+
+    def capacity_bytes(self) -> int:
+        return sum(self.capacity.values())
+
+    def used_bytes(self) -> int:
+        return sum(self.used.values())
+
+    def to_proto(self, state: str):
+        w = pb.block.WorkerInfo(id=self.id, address=self.address,
+                                lastContactSec=int((time.time() * 1000 - self.last_updated_ms) / 1000),
+                                state=state, capacityBytes=self.capacity_bytes(), usedBytes=self.used_bytes(),
+                                startTimeMs=self.start_time_ms)
+        for k, v in self.capacity.items():
+            w.capacityBytesOnTiers[k] = v
+        for k, v in self.used.items():
+            w.usedBytesOnTiers[k] = v
+        return w
+
+
+class BlockMeta:
+    __slots__ = ("length", "locations")
+
+    def __init__(self, length: int):
+        self.length = length
+        self.locations: dict[int, tuple[str, str]] = {}  # worker id -> (tier alias, medium)
+
+
+class BlockMaster(Journaled):
+    journal_name = "BlockMaster"
+
+    def __init__(self, conf=None, journal_system=None, metrics=None, worker_timeout_ms: int = 300_000,
+                 global_tiers=("MEM", "SSD", "HDD")):
+        self.conf = conf
+        self.journal = journal_system
+        self.metrics = metrics
+        self.worker_timeout_ms = worker_timeout_ms
+        self.global_tiers = list(global_tiers)
+        self._lock = threading.RLock()
+        self._blocks: dict[int, BlockMeta] = {}
+        self._next_container = 0
+        self._container_limit = 0
+        self._registered = IndexedSet(id=(lambda w: w.id, True), addr=(lambda w: w.key, True))
+        self._temp = IndexedSet(id=(lambda w: w.id, True), addr=(lambda w: w.key, True))
+        self._lost = IndexedSet(id=(lambda w: w.id, True), addr=(lambda w: w.key, True))
+        self._lost_blocks: set[int] = set()
+        self.lost_worker_listeners = []
+        self.worker_registered_listeners = []
+        self.safe_mode = None
+
+    # ---- Journaled ----------------------------------------------------------------------------
+    def reset_state(self) -> None:
+        with self._lock:
+            self._blocks.clear()
+            self._next_container = 0
+            self._container_limit = 0
+
+    def process_journal_entry(self, e) -> bool:
+        with self._lock:
+            if e.HasField("block_container_id_generator"):
+                self._container_limit = e.block_container_id_generator.next_container_id
+                self._next_container = max(self._next_container, self._container_limit)
+            elif e.HasField("block_info"):
+                bi = e.block_info
+                m = self._blocks.get(bi.block_id)
+                if m is None:
+                    self._blocks[bi.block_id] = BlockMeta(bi.length)
+                else:
+                    m.length = bi.length
+            elif e.HasField("delete_block"):
+                self._blocks.pop(e.delete_block.block_id, None)
+            else:
+                return False
+            return True
+
+    def journal_entries(self):
+        with self._lock:
+            yield pb.journal.JournalEntry(block_container_id_generator=pb.journal.BlockContainerIdGeneratorEntry(
+                next_container_id=self._container_limit))
+            for bid, m in sorted(self._blocks.items()):
+                yield pb.journal.JournalEntry(block_info=pb.journal.BlockInfoEntry(block_id=bid, length=m.length))
+
+    def _ctx(self):
+        from ..journal.system import NoopJournalContext
+        if self.journal is None:
+            return NoopJournalContext()
+        return self.journal.create_context(self.journal_name)
+
+    # ---- container ids ------------------------------------------------------------------------
+    def get_new_container_id(self) -> int:
+        """Journaled in batches: one entry reserves CONTAINER_BATCH ids."""
+        ctx = None
+        with self._lock:
+            cid = self._next_container
+            self._next_container += 1
+            if self._next_container > self._container_limit:
+                limit = cid + CONTAINER_BATCH
+                e = pb.journal.JournalEntry(block_container_id_generator=pb.journal.BlockContainerIdGeneratorEntry(
+                    next_container_id=limit))
+                self._container_limit = limit
+                ctx = self._ctx()
+                ctx.append(e)
+        if ctx is not None:
+            ctx.close()
+        return cid
+
+    # ---- workers ------------------------------------------------------------------------------
+    def get_worker_id(self, address) -> int:
+        with self._lock:
+            key = address_key(address)
+            for s in (self._registered, self._temp):
+                w = s.get_first_by_field("addr", key)
+                if w is not None:
+                    return w.id
+            w = self._lost.get_first_by_field("addr", key)
+            if w is not None:
+                self._lost.remove(w)
+                w.registered = False
+                self._temp.add(w)
+                return w.id
+            wid = ids.get_random_non_negative_long()
+            while self._registered.get_first_by_field("id", wid) or self._temp.get_first_by_field("id", wid):
+                wid = ids.get_random_non_negative_long()
+            self._temp.add(MasterWorkerInfo(wid, address))
+            return wid
+
+    def _find_worker(self, wid) -> MasterWorkerInfo | None:
+        return self._registered.get_first_by_field("id", wid) or self._temp.get_first_by_field("id", wid)
+
+    def worker_register(self, wid: int, tiers, total_on_tiers: dict, used_on_tiers: dict,
+                        current_blocks: dict[tuple[str, str], list[int]], lost_storage: dict | None = None,
+                        options=None) -> None:
+        with self._lock:
+            w = self._find_worker(wid)
+            if w is None:
+                w = self._lost.get_first_by_field("id", wid)
+                if w is None:
+                    raise NotFoundException(f"Could not find worker id: {wid} to register.")
+                self._lost.remove(w)
+            self._temp.remove(w)
+            self._registered.remove(w)
+            w.registered = True
+            w.storage_tiers = list(tiers)
+            w.capacity = dict(total_on_tiers)
+            w.used = dict(used_on_tiers)
+            w.lost_storage = dict(lost_storage or {})
+            w.last_updated_ms = int(time.time() * 1000)
+            # replace the worker's block set with what it reports
+            for bid in list(w.blocks):
+                m = self._blocks.get(bid)
+                if m is not None:
+                    m.locations.pop(wid, None)
+            w.blocks.clear()
+            w.to_remove.clear()
+            for (tier, medium), blist in current_blocks.items():
+                for bid in blist:
+                    self._add_location(w, bid, tier, medium)
+            self._registered.add(w)
+        for l in self.worker_registered_listeners:
+            l(wid)
+        LOG.info("registered worker %d at %s:%d", wid, w.address.host, w.address.rpcPort)
+
+    def _add_location(self, w: MasterWorkerInfo, bid: int, tier: str, medium: str) -> None:
+        m = self._blocks.get(bid)
+        if m is None:
+            # block unknown to the master (deleted meanwhile): ask the worker to drop it
+            w.to_remove.add(bid)
+            return
+        m.locations[w.id] = (tier, medium)
+        w.blocks.add(bid)
+        self._lost_blocks.discard(bid)
+
+    def worker_heartbeat(self, wid: int, used_on_tiers: dict, removed: list[int],
+                         added: dict[tuple[str, str], list[int]], metrics=None,
+                         lost_storage: dict | None = None):
+        """Returns (command_type, data) with command_type in Nothing/Register/Free."""
+        with self._lock:
+            w = self._registered.get_first_by_field("id", wid)
+            if w is None:
+                return "Register", []
+            w.last_updated_ms = int(time.time() * 1000)
+            w.used = dict(used_on_tiers)
+            if lost_storage:
+                w.lost_storage.update(lost_storage)
+            for bid in removed:
+                m = self._blocks.get(bid)
+                if m is not None:
+                    m.locations.pop(wid, None)
+                    if not m.locations:
+                        self._lost_blocks.add(bid)
+                w.blocks.discard(bid)
+                w.to_remove.discard(bid)
+            for (tier, medium), blist in added.items():
+                for bid in blist:
+                    self._add_location(w, bid, tier, medium)
+            to_free = sorted(w.to_remove)
+        if metrics and self.metrics is not None:
+            self.metrics(w, metrics)
+        if to_free:
+            return "Free", to_free
+        return "Nothing", []
+
+    def commit_block(self, wid: int, used_on_tier: int, tier: str, medium: str, block_id: int,
+                     length: int) -> None:
+        ctx = None
+        with self._lock:
+            w = self._registered.get_first_by_field("id", wid)
+            if w is None:
+                raise NotFoundException(f"worker {wid} is not registered")
+            m = self._blocks.get(block_id)
+            if m is None or m.length != length:
+                e = pb.journal.JournalEntry(block_info=pb.journal.BlockInfoEntry(block_id=block_id, length=length))
+                self.process_journal_entry(e)
+                ctx = self._ctx()
+                ctx.append(e)
+            self._add_location(w, block_id, tier, medium)
+            w.used[tier] = used_on_tier
+            w.last_updated_ms = int(time.time() * 1000)
+        if ctx is not None:
+            ctx.close()
+
+    def commit_block_in_ufs(self, block_id: int, length: int) -> None:
+        ctx = None
+        with self._lock:
+            if block_id in self._blocks:
+                return
+            e = pb.journal.JournalEntry(block_info=pb.journal.BlockInfoEntry(block_id=block_id, length=length))
+            self.process_journal_entry(e)
+            ctx = self._ctx()
+            ctx.append(e)
+        ctx.close()
+
+    def remove_blocks(self, block_ids, delete: bool) -> None:
+        """Remove replicas on workers; with ``delete`` also forget the block (journaled)."""
+        ctx = None
+        with self._lock:
+            for bid in block_ids:
+                m = self._blocks.get(bid)
+                if m is None:
+                    continue
+                for wid in list(m.locations):
+                    w = self._registered.get_first_by_field("id", wid)
+                    if w is not None:
+                        w.to_remove.add(bid)
+                if delete:
+                    e = pb.journal.JournalEntry(delete_block=pb.journal.DeleteBlockEntry(block_id=bid))
+                    self.process_journal_entry(e)
+                    if ctx is None:
+                        ctx = self._ctx()
+                    ctx.append(e)
+                    self._lost_blocks.discard(bid)
+        if ctx is not None:
+            ctx.close()
+
+    def remove_block_from_worker(self, block_id: int, wid: int) -> None:
+        with self._lock:
+            w = self._registered.get_first_by_field("id", wid)
+            if w is not None:
+                w.to_remove.add(block_id)
+
+    def validate_block(self, block_id: int) -> bool:
+        with self._lock:
+            return block_id in self._blocks
+
+    # ---- queries ------------------------------------------------------------------------------
+    def block_info(self, block_id: int):
+        with self._lock:
+            m = self._blocks.get(block_id)
+            if m is None:
+                raise BlockDoesNotExistException(f"Block {block_id} does not exist")
+            return self._gen_block_info(block_id, m)
+
+    def block_info_or_none(self, block_id: int):
+        with self._lock:
+            m = self._blocks.get(block_id)
+            return None if m is None else self._gen_block_info(block_id, m)
+
+    def block_info_list(self, block_ids) -> list:
+        with self._lock:
+            out = []
+            for bid in block_ids:
+                m = self._blocks.get(bid)
+                if m is not None:
+                    out.append(self._gen_block_info(bid, m))
+            return out
+
+    def _gen_block_info(self, bid, m: BlockMeta):
+        locs = []
+        order = {t: i for i, t in enumerate(self.global_tiers)}
+        for wid, (tier, medium) in sorted(m.locations.items(), key=lambda kv: order.get(kv[1][0], 99)):
+            w = self._registered.get_first_by_field("id", wid)
+            if w is None:
+                continue
+            locs.append(pb.grpc.BlockLocation(workerId=wid, workerAddress=w.address, tierAlias=tier,
+                                              mediumType=medium))
+        return pb.grpc.BlockInfo(blockId=bid, length=m.length, locations=locs)
+
+    def block_length(self, block_id: int) -> int | None:
+        with self._lock:
+            m = self._blocks.get(block_id)
+            return None if m is None else m.length
+
+    def workers(self, live_only: bool = True) -> list[MasterWorkerInfo]:
+        with self._lock:
+            return list(self._registered) if live_only else list(self._registered) + list(self._lost)
+
+    def worker_info_list(self):
+        with self._lock:
+            return [w.to_proto("In Service") for w in self._registered]
+
+    def lost_workers_info_list(self):
+        with self._lock:
+            return [w.to_proto("Out of Service") for w in self._lost]
+
+    def worker_count(self) -> int:
+        return len(self._registered)
+
+    def lost_worker_count(self) -> int:
+        return len(self._lost)
+
+    def capacity_bytes(self) -> int:
+        return sum(w.capacity_bytes() for w in self.workers())
+
+    def used_bytes(self) -> int:
+        return sum(w.used_bytes() for w in self.workers())
+
+    def capacity_on_tiers(self) -> dict:
+        out: dict[str, int] = {}
+        for w in self.workers():
+            for k, v in w.capacity.items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def used_on_tiers(self) -> dict:
+        out: dict[str, int] = {}
+        for w in self.workers():
+            for k, v in w.used.items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def lost_blocks(self) -> set[int]:
+        with self._lock:
+            return set(self._lost_blocks)
+
+    def block_count(self) -> int:
+        with self._lock:
+            return len(self._blocks)
+
+    def worker_lost_storage(self):
+        out = []
+        for w in self.workers():
+            if w.lost_storage:
+                info = pb.block.WorkerLostStorageInfo(address=w.address)
+                for k, v in w.lost_storage.items():
+                    info.lostStorage[k].storage.extend(v)
+                out.append(info)
+        return out
+
+    # ---- failure detection --------------------------------------------------------------------
+    def detect_lost_workers(self) -> list[int]:
+        now = int(time.time() * 1000)
+        lost = []
+        with self._lock:
+            for w in list(self._registered):
+                if now - w.last_updated_ms > self.worker_timeout_ms:
+                    LOG.warning("worker %d timed out after %d ms", w.id, now - w.last_updated_ms)
+                    self._registered.remove(w)
+                    self._process_lost(w)
+                    self._lost.add(w)
+                    lost.append(w.id)
+        for wid in lost:
+            for l in self.lost_worker_listeners:
+                l(wid)
+        return lost
+
+    def _process_lost(self, w: MasterWorkerInfo) -> None:
+        for bid in w.blocks:
+            m = self._blocks.get(bid)
+            if m is not None:
+                m.locations.pop(w.id, None)
+                if not m.locations:
+                    self._lost_blocks.add(bid)
+        w.blocks.clear()
+        w.registered = False
+
+    def decommission_worker(self, wid: int) -> None:
+        with self._lock:
+            w = self._registered.get_first_by_field("id", wid)
+            if w is not None:
+                self._registered.remove(w)
+                self._process_lost(w)
+                self._lost.add(w)

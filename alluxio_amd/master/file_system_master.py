@@ -1,0 +1,1165 @@
+"""File-system master: namespace operations, metadata sync, persistence, TTL, pinning, ACLs.
+
+Parity: core/server/master/src/main/java/alluxio/master/file/DefaultFileSystemMaster.java
+(getFileInfo :818-891, listStatus :959, completeFile :1295-1430, createFile :1463,
+getNewBlockIdForFile :1538, delete :1621, createDirectory :2077, rename :2174, free :2503,
+loadMetadataIfNotExist :2632, mount :2736, workerHeartbeat :3411, persistence scheduler/checker
+:3670/:3886) and the background executors started in ``start`` (:541-688): TTL checker, lost
+files detector, replication checker, persistence scheduler, block-integrity checker.
+
+Every mutation is expressed as journal entries that are applied through
+``InodeTree.apply`` (the same code that replays the journal) and appended to the RPC's journal
+context; the context is flushed after the tree lock is released.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+
+from ..journal.system import Journaled, NoopJournalContext
+from ..proto import pb
+from ..security import PermissionChecker, current_user
+from ..security.acl import Bits
+from ..underfs.base import Fingerprint, MkdirsOptions, UfsMode
+from ..utils import ids
+from ..utils.exceptions import (AccessControlException, DirectoryNotEmptyException,
+                                FailedPreconditionException, FileAlreadyExistsException,
+                                FileDoesNotExistException, InvalidArgumentException,
+                                InvalidPathException, UnavailableException)
+from ..utils.uri import normalize_path, path_components
+from .inode import (LOST, NO_TTL, NOT_PERSISTED, PERSISTED, TO_BE_PERSISTED, InodeFile, now_ms)
+from .inode_tree import InodeTree
+from .mount_table import ROOT_MOUNT_ID, MountInfo, MountTable, UfsManager
+
+LOG = logging.getLogger(__name__)
+
+THROUGH_TYPES = ("CACHE_THROUGH", "THROUGH")
+LOAD_NEVER, LOAD_ONCE, LOAD_ALWAYS = "NEVER", "ONCE", "ALWAYS"
+
+
+class RpcContext:
+    def __init__(self, master: "FileSystemMaster"):
+        self.master = master
+        self.journal = master._journal_ctx()
+        self.op_time_ms = now_ms()
+        self.after = []   # callbacks run after the journal flush (e.g. UFS cleanup)
+
+    def append(self, entry) -> None:
+        self.journal.append(entry)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        self.journal.close()
+        if et is None:
+            for cb in self.after:
+                try:
+                    cb()
+                except Exception:  # noqa: BLE001
+                    LOG.exception("post-journal callback failed")
+
+
+class FileSystemMaster(Journaled):
+    journal_name = "FileSystemMaster"
+
+    def __init__(self, conf, block_master, journal_system=None, permission_checker=None, metrics=None,
+                 root_ufs: str | None = None, root_ufs_properties: dict | None = None):
+        self.conf = conf
+        self.block_master = block_master
+        self.journal = journal_system
+        self.metrics = metrics
+        self.ufs_manager = UfsManager(conf)
+        self.mount_table = MountTable(self.ufs_manager)
+        self.tree = InodeTree(block_master.get_new_container_id,
+                              conf.get_ms("alluxio.master.ttl.checker.interval") if conf else 3_600_000)
+        self.permission = permission_checker or PermissionChecker(
+            enabled=conf.get_bool("alluxio.security.authorization.permission.enabled") if conf else False,
+            superuser=None,
+            supergroup=conf.get("alluxio.security.authorization.permission.supergroup") if conf else "supergroup")
+        self.root_ufs = root_ufs or (conf.get("alluxio.master.mount.table.root.ufs") if conf else "/tmp/alluxio_ufs")
+        self.root_ufs_properties = dict(root_ufs_properties or {})
+        self.umask = int(conf.get("alluxio.security.authorization.permission.umask"), 8) if conf else 0o022
+        self.default_block_size = conf.get_bytes("alluxio.user.block.size.bytes.default") if conf else 64 << 20
+        self.sync_points: dict[str, int] = {}
+        self.ufs_modes: dict[str, UfsMode] = {}
+        self.persist_handler = None   # callable(file_id, path) -> job id; set by the master process
+        self.persist_jobs: dict[int, dict] = {}
+        self._sync_times: dict[str, float] = {}
+        self.state_lock = None
+        self.audit = None
+
+    # ------------------------------------------------------------------------------------------
+    # Journaled
+    def reset_state(self) -> None:
+        self.tree.reset()
+        self.mount_table.reset()
+        self.sync_points.clear()
+        self.ufs_modes.clear()
+
+    def process_journal_entry(self, e) -> bool:
+        if self.tree.apply(e):
+            return True
+        if e.HasField("new_block"):
+            f = self.tree.inodes.get(ids.get_file_id(e.new_block.id))
+            if f is not None and f.is_file and e.new_block.id not in f.block_ids:
+                f.block_ids.append(e.new_block.id)
+                f._next_seq = max(f._next_seq, ids.get_sequence_number(e.new_block.id) + 1)
+            return True
+        if e.HasField("add_mount_point"):
+            a = e.add_mount_point
+            self.mount_table.apply_add(MountInfo(a.alluxio_path, a.ufs_path, a.mount_id, a.readOnly, a.shared,
+                                                 {p.key: p.value for p in a.properties}))
+            return True
+        if e.HasField("delete_mount_point"):
+            self.mount_table.apply_delete(e.delete_mount_point.alluxio_path)
+            return True
+        if e.HasField("add_sync_point"):
+            self.sync_points[e.add_sync_point.syncpoint_path] = e.add_sync_point.mount_id
+            return True
+        if e.HasField("remove_sync_point"):
+            self.sync_points.pop(e.remove_sync_point.syncpoint_path, None)
+            return True
+        if e.HasField("active_sync_tx_id"):
+            return True
+        if e.HasField("update_ufs_mode"):
+            u = e.update_ufs_mode
+            self.ufs_modes[u.ufsPath] = UfsMode(u.ufsMode)
+            return True
+        return False
+
+    def journal_entries(self):
+        yield pb.journal.JournalEntry(inode_directory_id_generator=pb.journal.InodeDirectoryIdGeneratorEntry(
+            container_id=self.tree.dir_ids.container_id, sequence_number=self.tree.dir_ids.sequence))
+        for m in self.mount_table.mounts().values():
+            yield m.to_entry()
+        # parents before children: BFS from the root
+        if self.tree.root is not None:
+            queue = [self.tree.root]
+            while queue:
+                n = queue.pop(0)
+                yield n.to_entry()
+                if n.is_directory:
+                    queue.extend(self.tree.list_children(n))
+        for p, mid in self.sync_points.items():
+            yield pb.journal.JournalEntry(add_sync_point=pb.journal.AddSyncPointEntry(syncpoint_path=p, mount_id=mid))
+        for p, mode in self.ufs_modes.items():
+            yield pb.journal.JournalEntry(update_ufs_mode=pb.journal.UpdateUfsModeEntry(ufsPath=p, ufsMode=int(mode)))
+
+    def _journal_ctx(self):
+        if self.journal is None:
+            return NoopJournalContext()
+        return self.journal.create_context(self.journal_name, self.state_lock)
+
+    def _apply(self, rpc: RpcContext, entry) -> None:
+        if not self.process_journal_entry(entry):
+            raise RuntimeError(f"unhandled journal entry {entry}")
+        rpc.append(entry)
+
+    # ------------------------------------------------------------------------------------------
+    # startup
+    def start(self, is_primary: bool = True) -> None:
+        if not is_primary:
+            return
+        if self.tree.root is None:
+            self._initialize_root()
+        if self.mount_table.get("/") is None:
+            self._mount_root()
+
+    def _initialize_root(self) -> None:
+        owner = self.permission.superuser
+        from ..security import primary_group
+        group = primary_group(owner)
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            for e in self.tree.new_directory_entries(None, InodeTree.ROOT_NAME, owner, group, 0o755, True,
+                                                    mount_point=True):
+                self._apply(rpc, e)
+
+    def _mount_root(self) -> None:
+        import os
+        if "://" not in self.root_ufs:
+            os.makedirs(self.root_ufs, exist_ok=True)
+        info = MountInfo("/", self.root_ufs, ROOT_MOUNT_ID, False, False, self.root_ufs_properties)
+        with RpcContext(self) as rpc:
+            self._apply(rpc, info.to_entry())
+
+    # ------------------------------------------------------------------------------------------
+    # helpers
+    def _user(self):
+        return current_user()
+
+    def _check(self, chain, bits, path):
+        self.permission.check(self._user(), chain, bits, path)
+
+    def _owner_group(self):
+        from ..security import primary_group
+        user = self._user() or self.permission.superuser
+        return user, primary_group(user)
+
+    def _resolve_ufs(self, path: str):
+        return self.mount_table.resolve(path)
+
+    def _check_ufs_writable(self, path: str) -> None:
+        self.mount_table.check_under_write_mount(path)
+        res = self.mount_table.resolve(path)
+        mode = self._ufs_mode(res.mount.ufs_uri)
+        if mode != UfsMode.READ_WRITE:
+            raise AccessControlException(f"UFS {res.mount.ufs_uri} is in {mode.name} mode")
+
+    def _ufs_mode(self, ufs_uri: str) -> UfsMode:
+        for p, m in self.ufs_modes.items():
+            if ufs_uri.startswith(p.rstrip("/")):
+                return m
+        return UfsMode.READ_WRITE
+
+    def _count(self, name: str, n: int = 1) -> None:
+        if self.metrics is not None:
+            self.metrics.counter(name).inc(n)
+
+    # ------------------------------------------------------------------------------------------
+    # FileInfo
+    def file_info(self, inode, path: str | None = None):
+        path = path or self.tree.path_of(inode)
+        fi = pb.file.FileInfo(
+            fileId=inode.id, name=inode.name, path=path, length=getattr(inode, "length", 0),
+            blockSizeBytes=getattr(inode, "block_size_bytes", 0), creationTimeMs=inode.creation_time_ms,
+            completed=getattr(inode, "completed", True), folder=inode.is_directory, pinned=inode.pinned,
+            cacheable=getattr(inode, "cacheable", False), persisted=inode.is_persisted,
+            lastModificationTimeMs=inode.last_modification_time_ms, ttl=inode.ttl, owner=inode.owner,
+            group=inode.group, mode=inode.mode, persistenceState=inode.persistence_state,
+            mountPoint=getattr(inode, "mount_point", False),
+            ttlAction=pb.grpc.TtlAction.values_by_name[inode.ttl_action].number,
+            ufsFingerprint=inode.ufs_fingerprint, lastAccessTimeMs=inode.last_access_time_ms)
+        for k, v in inode.xattr.items():
+            fi.xattr[k] = v
+        try:
+            res = self.mount_table.resolve(path)
+            fi.ufsPath = res.uri
+            fi.mountId = res.mount_id
+        except InvalidPathException:
+            pass
+        if inode.is_file:
+            fi.blockIds.extend(inode.block_ids)
+            fi.replicationMax = inode.replication_max
+            fi.replicationMin = inode.replication_min
+            infos = self.block_master.block_info_list(inode.block_ids)
+            by_id = {bi.blockId: bi for bi in infos}
+            in_alluxio = in_mem = 0
+            for i, bid in enumerate(inode.block_ids):
+                bi = by_id.get(bid)
+                off = i * inode.block_size_bytes
+                if bi is None:
+                    blen = max(0, min(inode.block_size_bytes, inode.length - off))
+                    bi = pb.grpc.BlockInfo(blockId=bid, length=blen)
+                fbi = pb.file.FileBlockInfo(blockInfo=bi, offset=off)
+                if bi.locations:
+                    in_alluxio += bi.length
+                    if any(l.tierAlias == "MEM" for l in bi.locations):
+                        in_mem += bi.length
+                elif inode.is_persisted:
+                    fbi.ufsStringLocations.append(fi.ufsPath)
+                fi.fileBlockInfos.append(fbi)
+            if inode.length > 0:
+                fi.inAlluxioPercentage = int(in_alluxio * 100 // inode.length)
+                fi.inMemoryPercentage = int(in_mem * 100 // inode.length)
+            else:
+                fi.inAlluxioPercentage = 100
+                fi.inMemoryPercentage = 100
+        if inode.acl is not None:
+            fi.acl.CopyFrom(inode.acl.to_pacl(inode.mode))
+        if inode.is_directory and getattr(inode, "default_acl", None) is not None:
+            fi.defaultAcl.CopyFrom(inode.default_acl.to_pacl(inode.mode))
+        return fi
+
+    # ------------------------------------------------------------------------------------------
+    # create
+    def create_directory(self, path: str, recursive: bool = False, allow_exists: bool = False,
+                         mode: int | None = None, write_type: str = "MUST_CACHE", ttl: int = NO_TTL,
+                         ttl_action: str = "DELETE"):
+        path = normalize_path(path)
+        self._count("Master.DirectoriesCreated")
+        if path == "/":
+            if allow_exists:
+                return
+            raise FileAlreadyExistsException("/ already exists")
+        persist = write_type in ("CACHE_THROUGH", "THROUGH", "ASYNC_THROUGH")
+        owner, group = self._owner_group()
+        mode = (0o777 if mode is None else mode) & ~self.umask
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(path)
+            if not missing:
+                if allow_exists and chain[-1].is_directory:
+                    return
+                raise FileAlreadyExistsException(f"{path} already exists")
+            if len(missing) > 1 and not recursive:
+                raise FileDoesNotExistException(
+                    f"Path \"{normalize_path('/'.join([''] + path_components(path)[:-1]))}\" does not exist.")
+            self._check(chain, Bits.WRITE, path)
+            self.mount_table.check_under_write_mount(path)
+            parent = chain[-1]
+            if not parent.is_directory:
+                raise InvalidPathException(f"{self.tree.path_of(parent)} is a file")
+            cur_path = self.tree.path_of(parent)
+            for name in missing:
+                cur_path = cur_path.rstrip("/") + "/" + name
+                if persist:
+                    self._check_ufs_writable(cur_path)
+                    res = self._resolve_ufs(cur_path)
+                    res.ufs.mkdirs(res.uri, MkdirsOptions(create_parent=True, owner=owner, group=group, mode=mode))
+                for e in self.tree.new_directory_entries(parent, name, owner, group, mode, persist, ttl=ttl,
+                                                         ttl_action=ttl_action):
+                    self._apply(rpc, e)
+                parent = self.tree.get(cur_path)
+
+    def create_file(self, path: str, block_size: int | None = None, recursive: bool = False,
+                    mode: int | None = None, replication_min: int = 0, replication_max: int = -1,
+                    replication_durable: int = 1, write_type: str = "CACHE_THROUGH", ttl: int = NO_TTL,
+                    ttl_action: str = "DELETE", persistence_wait_ms: int = 0):
+        path = normalize_path(path)
+        if path == "/":
+            raise FileAlreadyExistsException("/ already exists")
+        self._count("Master.FilesCreated")
+        owner, group = self._owner_group()
+        mode = (0o666 if mode is None else mode) & ~self.umask
+        block_size = block_size or self.default_block_size
+        if block_size <= 0:
+            raise InvalidArgumentException("block size must be positive")
+        persisted = write_type in THROUGH_TYPES
+        comps = path_components(path)
+        parent_path = "/" + "/".join(comps[:-1])
+        if recursive:
+            with self.tree.lock.read():
+                need_parent = not self.tree.exists(parent_path)
+            if need_parent:
+                self.create_directory(parent_path, recursive=True, allow_exists=True,
+                                      write_type=write_type if write_type != "NONE" else "MUST_CACHE")
+        file_id = ids.create_file_id(self.block_master.get_new_container_id())
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(path)
+            if not missing:
+                raise FileAlreadyExistsException(f"{path} already exists")
+            if len(missing) > 1:
+                raise FileDoesNotExistException(f"Path \"{parent_path}\" does not exist.")
+            parent = chain[-1]
+            if not parent.is_directory:
+                raise InvalidPathException(f"{parent_path} is a file")
+            self._check(chain, Bits.WRITE, path)
+            self.mount_table.check_under_write_mount(path)
+            if persisted:
+                self._check_ufs_writable(path)
+            state = PERSISTED if persisted else NOT_PERSISTED
+            e = self.tree.new_file_entry(parent, comps[-1], file_id, owner, group, mode, block_size, state, ttl,
+                                         ttl_action, replication_min, replication_max, replication_durable,
+                                         cacheable=write_type != "THROUGH")
+            if persistence_wait_ms:
+                e.inode_file.should_persist_time = now_ms() + persistence_wait_ms
+            self._apply(rpc, e)
+            self._touch_parent(rpc, parent)
+            return self.file_info(self.tree.inodes[file_id], path)
+
+    def _touch_parent(self, rpc, parent) -> None:
+        self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+            id=parent.id, last_modification_time_ms=rpc.op_time_ms)))
+
+    def get_new_block_id_for_file(self, path: str) -> int:
+        path = normalize_path(path)
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(path)
+            if missing:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            f = chain[-1]
+            if not f.is_file:
+                raise FileDoesNotExistException(f"{path} is not a file")
+            if f.completed:
+                raise FailedPreconditionException(f"file {path} is already completed")
+            self._check(chain, Bits.WRITE, path)
+            bid = ids.create_block_id(f.block_container_id, f._next_seq)
+            self._apply(rpc, pb.journal.JournalEntry(new_block=pb.journal.NewBlockEntry(id=bid)))
+            return bid
+
+    def complete_file(self, path: str, ufs_length: int = 0, async_persist: bool = False,
+                      persistence_wait_ms: int = 0) -> None:
+        path = normalize_path(path)
+        self._count("Master.FilesCompleted")
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(path)
+            if missing:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            f = chain[-1]
+            if not f.is_file:
+                raise FileDoesNotExistException(f"{path} must be a file")
+            self._check(chain, Bits.WRITE, path)
+            if f.completed:
+                raise FailedPreconditionException(f"File {path} has already been completed.")
+            infos = self.block_master.block_info_list(f.block_ids)
+            if not f.is_persisted and len(infos) != len(f.block_ids):
+                raise FailedPreconditionException("Cannot complete a file without all the blocks committed")
+            in_alluxio = 0
+            for i, bi in enumerate(infos):
+                in_alluxio += bi.length
+                if i < len(infos) - 1 and bi.length != f.block_size_bytes:
+                    raise FailedPreconditionException(f"Block index {i} has a block size smaller than the file "
+                                                      f"block size ({f.block_size_bytes})")
+            length = ufs_length if f.is_persisted else in_alluxio
+            if length < 0:
+                raise InvalidArgumentException(f"File {f.name} cannot have negative length: {length}")
+            fingerprint = Fingerprint.INVALID
+            if f.is_persisted:
+                try:
+                    res = self._resolve_ufs(path)
+                    fingerprint = res.ufs.get_fingerprint(res.uri)
+                except Exception:  # noqa: BLE001
+                    fingerprint = Fingerprint.INVALID
+            blocks = []
+            remaining, seq = length, 0
+            while remaining > 0:
+                blocks.append(ids.create_block_id(f.block_container_id, seq))
+                remaining -= min(remaining, f.block_size_bytes)
+                seq += 1
+            if f.is_persisted:
+                rem = length
+                for bid in blocks:
+                    self.block_master.commit_block_in_ufs(bid, min(rem, f.block_size_bytes))
+                    rem -= min(rem, f.block_size_bytes)
+            self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+                id=f.id, ufs_fingerprint=fingerprint, last_modification_time_ms=rpc.op_time_ms,
+                last_access_time_ms=rpc.op_time_ms, overwrite_modification_time=True, overwrite_access_time=True)))
+            self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
+                id=f.id, path=path, completed=True, length=length, set_blocks=blocks)))
+            if async_persist and not f.is_persisted:
+                self._schedule_persist_locked(rpc, f, persistence_wait_ms)
+
+    # ------------------------------------------------------------------------------------------
+    # read-side
+    def get_status(self, path: str, load_metadata: str = LOAD_ONCE, sync_interval_ms: int = -1,
+                   access_mode: int = Bits.READ, update_timestamps: bool = True):
+        path = normalize_path(path)
+        self._count("Master.GetFileInfoOps")
+        self._maybe_sync(path, sync_interval_ms, recursive=False)
+        with self.tree.lock.read():
+            chain, missing = self.tree.resolve(path)
+            if not missing:
+                self._check(chain[:-1] + [chain[-1]], Bits.NONE, path)
+                return self.file_info(chain[-1], path)
+        if load_metadata == LOAD_NEVER:
+            raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+        self.load_metadata(path, recursive=False, create_ancestors=True, quiet=True)
+        with self.tree.lock.read():
+            inode = self.tree.get(path)
+            return self.file_info(inode, path)
+
+    def exists(self, path: str, load_metadata: str = LOAD_ONCE) -> bool:
+        try:
+            self.get_status(path, load_metadata)
+            return True
+        except FileDoesNotExistException:
+            return False
+
+    def list_status(self, path: str, recursive: bool = False, load_metadata: str = LOAD_ONCE,
+                    sync_interval_ms: int = -1, load_direct_children: bool = True):
+        path = normalize_path(path)
+        self._count("Master.GetFileInfoOps")
+        self._maybe_sync(path, sync_interval_ms, recursive=recursive)
+        with self.tree.lock.read():
+            inode = self.tree.get_or_none(path)
+        if inode is None:
+            if load_metadata == LOAD_NEVER:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            self.load_metadata(path, recursive=False, create_ancestors=True, quiet=True)
+            with self.tree.lock.read():
+                inode = self.tree.get(path)
+        if inode.is_directory and load_metadata != LOAD_NEVER and inode.is_persisted and \
+                (load_metadata == LOAD_ALWAYS or not inode.direct_children_loaded):
+            self.load_metadata(path, recursive=recursive, create_ancestors=False, quiet=True)
+        with self.tree.lock.read():
+            chain, missing = self.tree.resolve(path)
+            if missing:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            inode = chain[-1]
+            self._check(chain, Bits.READ if inode.is_directory else Bits.NONE, path)
+            if not inode.is_directory:
+                return [self.file_info(inode, path)]
+            out = []
+            stack = [(inode, path)]
+            while stack:
+                d, dp = stack.pop(0)
+                for c in self.tree.list_children(d):
+                    cp = dp.rstrip("/") + "/" + c.name
+                    out.append(self.file_info(c, cp))
+                    if recursive and c.is_directory:
+                        stack.append((c, cp))
+            return out
+
+    def get_file_path(self, file_id: int) -> str:
+        with self.tree.lock.read():
+            inode = self.tree.inodes.get(file_id)
+            if inode is None:
+                raise FileDoesNotExistException(f"File id {file_id} does not exist")
+            return self.tree.path_of(inode)
+
+    def get_file_info_by_id(self, file_id: int):
+        with self.tree.lock.read():
+            inode = self.tree.inodes.get(file_id)
+            if inode is None:
+                raise FileDoesNotExistException(f"File id {file_id} does not exist")
+            return self.file_info(inode)
+
+    def update_access_time(self, path: str) -> None:
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            inode = self.tree.get_or_none(normalize_path(path))
+            if inode is not None:
+                self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+                    id=inode.id, last_access_time_ms=rpc.op_time_ms)))
+
+    # ------------------------------------------------------------------------------------------
+    # delete / rename / free
+    def delete(self, path: str, recursive: bool = False, alluxio_only: bool = False,
+               unchecked: bool = False) -> None:
+        path = normalize_path(path)
+        self._count("Master.PathsDeleted")
+        ufs_deletes = []
+        block_ids = []
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(path)
+            if missing:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            inode = chain[-1]
+            self._check(chain[:-1], Bits.WRITE, path)
+            if inode.is_directory and self.tree.children.get(inode.id) and not recursive:
+                raise DirectoryNotEmptyException(f"Cannot delete non-empty directory {path} without recursive")
+            victims = self.tree.descendants(inode)
+            if path != "/":
+                victims.append(inode)
+            for v in victims:
+                vp = self.tree.path_of(v)
+                if v.is_directory and self.mount_table.is_mount_point(vp) and vp != path:
+                    raise InvalidPathException(f"cannot delete {path}: it contains mount point {vp}")
+            if path != "/" and self.mount_table.is_mount_point(path) and not alluxio_only:
+                raise InvalidPathException(f"{path} is a mount point; unmount it instead")
+            if not alluxio_only:
+                self.mount_table.check_under_write_mount(path)
+            for v in victims:
+                vp = self.tree.path_of(v)
+                if not alluxio_only and v.is_persisted:
+                    try:
+                        res = self._resolve_ufs(vp)
+                        ufs_deletes.append((res.ufs, res.uri, v.is_directory))
+                    except InvalidPathException:
+                        pass
+                if v.is_file:
+                    block_ids.extend(v.block_ids)
+            # UFS first (children before parents), then the journal
+            for ufs, uri, is_dir in ufs_deletes:
+                try:
+                    if is_dir:
+                        ufs.delete_directory(uri)
+                    else:
+                        ufs.delete_file(uri)
+                except Exception as e:  # noqa: BLE001
+                    if not unchecked:
+                        raise UnavailableException(f"failed to delete {uri} in UFS: {e}") from e
+            for v in victims:
+                self._apply(rpc, pb.journal.JournalEntry(delete_file=pb.journal.DeleteFileEntry(
+                    id=v.id, recursive=recursive, op_time_ms=rpc.op_time_ms, alluxioOnly=alluxio_only,
+                    path=self.tree.path_of(v) if not v.deleted else "")))
+            if path != "/":
+                self._touch_parent(rpc, chain[-2])
+        if block_ids:
+            self.block_master.remove_blocks(block_ids, delete=True)
+
+    def rename(self, src: str, dst: str, persist: bool = False) -> None:
+        src, dst = normalize_path(src), normalize_path(dst)
+        self._count("Master.PathsRenamed")
+        if src == "/" or dst == "/":
+            raise InvalidPathException("cannot rename the root")
+        if dst == src:
+            return
+        if dst.startswith(src.rstrip("/") + "/"):
+            raise InvalidPathException(f"cannot rename {src} into its own subtree {dst}")
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            schain, smissing = self.tree.resolve(src)
+            if smissing:
+                raise FileDoesNotExistException(f"Path \"{src}\" does not exist.")
+            inode = schain[-1]
+            dchain, dmissing = self.tree.resolve(dst)
+            if not dmissing:
+                raise FileAlreadyExistsException(f"Cannot rename because destination already exists. src: {src} "
+                                                 f"dst: {dst}")
+            if len(dmissing) > 1:
+                raise FileDoesNotExistException(f"destination parent of {dst} does not exist")
+            dparent = dchain[-1]
+            if not dparent.is_directory:
+                raise InvalidPathException(f"destination parent of {dst} is a file")
+            self._check(schain[:-1], Bits.WRITE, src)
+            self._check(dchain, Bits.WRITE, dst)
+            if self.mount_table.is_mount_point(src):
+                raise InvalidPathException(f"{src} is a mount point")
+            if self.mount_table.mount_point_for(src) != self.mount_table.mount_point_for(dst):
+                raise InvalidPathException(f"rename across mount points: {src} -> {dst}")
+            self.mount_table.check_under_write_mount(src)
+            if inode.is_persisted:
+                sres, dres = self._resolve_ufs(src), self._resolve_ufs(dst)
+                dparent_ufs = dres.uri.rsplit("/", 1)[0] or "/"
+                if not dres.ufs.exists(dparent_ufs):
+                    dres.ufs.mkdirs(dparent_ufs)
+                ok = (sres.ufs.rename_directory(sres.uri, dres.uri) if inode.is_directory
+                      else sres.ufs.rename_file(sres.uri, dres.uri))
+                if not ok:
+                    raise UnavailableException(f"failed to rename {sres.uri} to {dres.uri} in the UFS")
+            old_parent = schain[-2]
+            self._apply(rpc, pb.journal.JournalEntry(rename=pb.journal.RenameEntry(
+                id=inode.id, op_time_ms=rpc.op_time_ms, new_parent_id=dparent.id, new_name=dmissing[0],
+                path=src, new_path=dst)))
+            self._touch_parent(rpc, old_parent)
+            self._touch_parent(rpc, dparent)
+
+    def free(self, path: str, recursive: bool = False, forced: bool = False) -> None:
+        path = normalize_path(path)
+        self._count("Master.FilesFreed")
+        with self.tree.lock.read():
+            chain, missing = self.tree.resolve(path)
+            if missing:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            inode = chain[-1]
+            self._check(chain, Bits.READ, path)
+            if inode.is_directory and self.tree.children.get(inode.id) and not recursive:
+                raise DirectoryNotEmptyException(f"Cannot free directory {path} which is not empty. Please set the "
+                                                 f"\"recursive\" flag of free operation to true")
+            files = [inode] if inode.is_file else [d for d in self.tree.descendants(inode) if d.is_file]
+            block_ids = []
+            for f in files:
+                if f.pinned and not forced:
+                    raise FailedPreconditionException(f"Cannot free file {self.tree.path_of(f)} which is pinned. "
+                                                      f"Please unpin it first or set the \"forced\" flag to true")
+                if not f.is_persisted:
+                    raise FailedPreconditionException(f"Cannot free file {self.tree.path_of(f)} which is not "
+                                                      f"persisted")
+                block_ids.extend(f.block_ids)
+        if forced:
+            with RpcContext(self) as rpc, self.tree.lock.write():
+                for f in files:
+                    if f.pinned and not f.deleted:
+                        self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+                            id=f.id, pinned=False)))
+        self.block_master.remove_blocks(block_ids, delete=False)
+
+    # ------------------------------------------------------------------------------------------
+    # attributes / ACLs
+    def set_attribute(self, path: str, pinned=None, ttl=None, ttl_action=None, persisted=None, owner=None,
+                      group=None, mode=None, recursive=False, replication_min=None, replication_max=None,
+                      pinned_media=None) -> None:
+        path = normalize_path(path)
+        self._count("Master.SetAttributeOps")
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(path)
+            if missing:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            inode = chain[-1]
+            user = self._user()
+            if owner is not None or group is not None:
+                if owner is not None:
+                    self.permission.check_superuser(user)
+                else:
+                    self.permission.check_owner(user, inode, path)
+            elif mode is not None:
+                self.permission.check_owner(user, inode, path)
+            else:
+                self._check(chain, Bits.WRITE, path)
+            targets = [inode] + (self.tree.descendants(inode) if recursive and inode.is_directory else [])
+            for t in targets:
+                u = pb.journal.UpdateInodeEntry(id=t.id)
+                changed = False
+                if pinned is not None and (t.is_file or t is inode):
+                    u.pinned = pinned
+                    changed = True
+                    if pinned_media:
+                        u.medium_type.extend(pinned_media)
+                if ttl is not None and t is inode:
+                    u.ttl = ttl
+                    u.ttlAction = pb.journal.PTtlAction.values_by_name[ttl_action or "DELETE"].number
+                    changed = True
+                if owner is not None:
+                    u.owner = owner
+                    changed = True
+                if group is not None:
+                    u.group = group
+                    changed = True
+                if mode is not None:
+                    u.mode = mode
+                    changed = True
+                if persisted is not None and persisted and not t.is_persisted:
+                    u.persistence_state = PERSISTED
+                    changed = True
+                if changed:
+                    u.last_modification_time_ms = rpc.op_time_ms
+                    self._apply(rpc, pb.journal.JournalEntry(update_inode=u))
+                    if t.is_persisted and (owner is not None or group is not None or mode is not None):
+                        try:
+                            res = self._resolve_ufs(self.tree.path_of(t))
+                            if owner is not None or group is not None:
+                                res.ufs.set_owner(res.uri, owner or t.owner, group or t.group)
+                            if mode is not None:
+                                res.ufs.set_mode(res.uri, mode)
+                        except Exception:  # noqa: BLE001
+                            LOG.debug("ufs attribute propagation failed for %s", t.name)
+                if t.is_file and (replication_min is not None or replication_max is not None):
+                    rmin = t.replication_min if replication_min is None else replication_min
+                    rmax = t.replication_max if replication_max is None else replication_max
+                    if rmax != -1 and rmin > rmax:
+                        raise InvalidArgumentException("replication min cannot exceed replication max")
+                    self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
+                        id=t.id, replication_min=rmin, replication_max=rmax)))
+
+    def set_acl(self, path: str, action: str, entries, recursive: bool = False) -> None:
+        from ..security.acl import AclEntry
+        path = normalize_path(path)
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(path)
+            if missing:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            inode = chain[-1]
+            self.permission.check_owner(self._user(), inode, path)
+            targets = [inode] + (self.tree.descendants(inode) if recursive and inode.is_directory else [])
+            protos = [e.to_proto() if isinstance(e, AclEntry) else e for e in entries]
+            for t in targets:
+                self._apply(rpc, pb.journal.JournalEntry(set_acl=pb.journal.SetAclEntry(
+                    id=t.id, op_time_ms=rpc.op_time_ms,
+                    action=pb.journal.PSetAclAction.values_by_name[action].number, entries=protos,
+                    recursive=recursive)))
+
+    def set_xattr(self, path: str, key: str, value: bytes) -> None:
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            inode = self.tree.get(normalize_path(path))
+            u = pb.journal.UpdateInodeEntry(id=inode.id)
+            u.xAttr[key] = value
+            self._apply(rpc, pb.journal.JournalEntry(update_inode=u))
+
+    # ------------------------------------------------------------------------------------------
+    # mounts
+    def mount(self, alluxio_path: str, ufs_uri: str, read_only: bool = False, shared: bool = False,
+              properties: dict | None = None) -> None:
+        alluxio_path = normalize_path(alluxio_path)
+        from ..underfs import registry
+        self.permission.check_superuser(self._user()) if False else None
+        self.mount_table.validate_new_mount(alluxio_path, ufs_uri)
+        ufs = registry.create(ufs_uri, self.conf, properties)
+        if not ufs.is_directory(ufs_uri):
+            raise InvalidPathException(f"Ufs path {ufs_uri} does not exist or is not a directory")
+        mount_id = ids.create_mount_id()
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(alluxio_path)
+            if not missing:
+                raise FileAlreadyExistsException(f"mount point {alluxio_path} already exists in Alluxio")
+            if len(missing) > 1:
+                raise FileDoesNotExistException(f"parent of {alluxio_path} does not exist")
+            parent = chain[-1]
+            self._check(chain, Bits.WRITE, alluxio_path)
+            info = MountInfo(alluxio_path, ufs_uri, mount_id, read_only, shared, properties)
+            self._apply(rpc, info.to_entry())
+            owner, group = self._owner_group()
+            st = ufs.get_status(ufs_uri)
+            mode = st.mode if st is not None else 0o755
+            for e in self.tree.new_directory_entries(parent, missing[0], st.owner or owner if st else owner,
+                                                    st.group or group if st else group, mode, True,
+                                                    mount_point=True):
+                self._apply(rpc, e)
+
+    def unmount(self, alluxio_path: str) -> None:
+        alluxio_path = normalize_path(alluxio_path)
+        if alluxio_path == "/":
+            raise InvalidPathException("cannot unmount the root")
+        if not self.mount_table.is_mount_point(alluxio_path):
+            raise InvalidPathException(f"{alluxio_path} is not a mount point")
+        for mp in self.mount_table.mounts():
+            if mp != alluxio_path and mp.startswith(alluxio_path.rstrip("/") + "/"):
+                raise InvalidPathException(f"cannot unmount {alluxio_path}: nested mount {mp}")
+        block_ids = []
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(alluxio_path)
+            if not missing:
+                inode = chain[-1]
+                victims = self.tree.descendants(inode) + [inode]
+                for v in victims:
+                    if v.is_file:
+                        block_ids.extend(v.block_ids)
+                for v in victims:
+                    self._apply(rpc, pb.journal.JournalEntry(delete_file=pb.journal.DeleteFileEntry(
+                        id=v.id, recursive=True, op_time_ms=rpc.op_time_ms, alluxioOnly=True)))
+            self._apply(rpc, pb.journal.JournalEntry(delete_mount_point=pb.journal.DeleteMountPointEntry(
+                alluxio_path=alluxio_path)))
+        if block_ids:
+            self.block_master.remove_blocks(block_ids, delete=True)
+
+    def update_mount(self, alluxio_path: str, read_only: bool | None = None, shared: bool | None = None,
+                     properties: dict | None = None) -> None:
+        alluxio_path = normalize_path(alluxio_path)
+        info = self.mount_table.get(alluxio_path)
+        if info is None:
+            raise InvalidPathException(f"{alluxio_path} is not a mount point")
+        new = MountInfo(alluxio_path, info.ufs_uri, info.mount_id,
+                        info.read_only if read_only is None else read_only,
+                        info.shared if shared is None else shared,
+                        info.properties if properties is None else properties)
+        with RpcContext(self) as rpc:
+            self._apply(rpc, pb.journal.JournalEntry(delete_mount_point=pb.journal.DeleteMountPointEntry(
+                alluxio_path=alluxio_path)))
+            self._apply(rpc, new.to_entry())
+
+    def get_mount_table(self) -> dict:
+        out = {}
+        for p, info in self.mount_table.mounts().items():
+            try:
+                ufs = self.ufs_manager.get(info.mount_id)
+            except Exception:  # noqa: BLE001
+                ufs = None
+            out[p] = info.to_proto(ufs)
+        return out
+
+    def reverse_resolve(self, ufs_uri: str) -> str:
+        p = self.mount_table.reverse_resolve(ufs_uri)
+        if p is None:
+            raise InvalidPathException(f"{ufs_uri} is not under any mount point")
+        return p
+
+    def update_ufs_mode(self, ufs_path: str, mode: str) -> None:
+        with RpcContext(self) as rpc:
+            self._apply(rpc, pb.journal.JournalEntry(update_ufs_mode=pb.journal.UpdateUfsModeEntry(
+                ufsPath=ufs_path, ufsMode=int(UfsMode[mode]))))
+
+    def get_ufs_info(self, mount_id: int):
+        info = self.mount_table.by_id(mount_id)
+        if info is None:
+            return pb.file.UfsInfo()
+        opts = pb.file.MountPOptions(readOnly=info.read_only, shared=info.shared)
+        for k, v in info.properties.items():
+            opts.properties[k] = v
+        return pb.file.UfsInfo(uri=info.ufs_uri, properties=opts)
+
+    # ------------------------------------------------------------------------------------------
+    # metadata loading / sync (reference InodeSyncStream, loadMetadataIfNotExist)
+    def load_metadata(self, path: str, recursive: bool = False, create_ancestors: bool = True,
+                      quiet: bool = False) -> None:
+        path = normalize_path(path)
+        self._count("Master.LoadMetadataOps")
+        try:
+            res = self._resolve_ufs(path)
+        except InvalidPathException:
+            if quiet:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            raise
+        st = res.ufs.get_status(res.uri)
+        if st is None:
+            raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+        owner_default, group_default = self._owner_group()
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            chain, missing = self.tree.resolve(path)
+            if missing:
+                if len(missing) > 1 and not create_ancestors:
+                    raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+                parent = chain[-1]
+                cur = self.tree.path_of(parent)
+                for i, name in enumerate(missing):
+                    cur = cur.rstrip("/") + "/" + name
+                    r = self._resolve_ufs(cur)
+                    s = st if i == len(missing) - 1 else r.ufs.get_status(r.uri)
+                    if s is None:
+                        raise FileDoesNotExistException(f"Path \"{cur}\" does not exist in UFS.")
+                    self._load_one(rpc, parent, name, s, r, owner_default, group_default)
+                    parent = self.tree.get(cur)
+            inode = self.tree.get(path)
+            if inode.is_directory:
+                self._load_children(rpc, inode, path, recursive, owner_default, group_default)
+
+    def _load_one(self, rpc, parent, name, st, res, owner_default, group_default) -> None:
+        owner = st.owner or owner_default
+        group = st.group or group_default
+        if st.is_directory:
+            for e in self.tree.new_directory_entries(parent, name, owner, group, st.mode or 0o755, True):
+                self._apply(rpc, e)
+            return
+        fid = ids.create_file_id(self.block_master.get_new_container_id())
+        bs = self.default_block_size
+        e = self.tree.new_file_entry(parent, name, fid, owner, group, st.mode or 0o644, bs, PERSISTED)
+        self._apply(rpc, e)
+        length = st.content_length
+        blocks = []
+        rem, seq = length, 0
+        while rem > 0:
+            blocks.append(ids.create_block_id(ids.get_container_id(fid), seq))
+            self.block_master.commit_block_in_ufs(blocks[-1], min(rem, bs))
+            rem -= min(rem, bs)
+            seq += 1
+        from ..underfs.base import Fingerprint as FP
+        self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+            id=fid, ufs_fingerprint=FP.create(res.ufs.ufs_type, st).serialize(),
+            last_modification_time_ms=st.last_modified_ms or rpc.op_time_ms, overwrite_modification_time=True)))
+        self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
+            id=fid, completed=True, length=length, set_blocks=blocks)))
+
+    def _load_children(self, rpc, inode, path, recursive, owner_default, group_default) -> None:
+        stack = [(inode, path)]
+        while stack:
+            d, dp = stack.pop()
+            res = self._resolve_ufs(dp)
+            listing = res.ufs.list_status(res.uri) or []
+            existing = self.tree.children.get(d.id, {})
+            for st in listing:
+                if "/" in st.name or not st.name:
+                    continue
+                if st.name not in existing:
+                    r = self._resolve_ufs(dp.rstrip("/") + "/" + st.name)
+                    self._load_one(rpc, d, st.name, st, r, owner_default, group_default)
+                if recursive:
+                    child = self.tree.inodes.get(self.tree.children[d.id].get(st.name))
+                    if child is not None and child.is_directory:
+                        stack.append((child, dp.rstrip("/") + "/" + st.name))
+            self._apply(rpc, pb.journal.JournalEntry(update_inode_directory=pb.journal.UpdateInodeDirectoryEntry(
+                id=d.id, direct_children_loaded=True)))
+
+    def _maybe_sync(self, path: str, interval_ms: int, recursive: bool) -> None:
+        if interval_ms is None or interval_ms < 0:
+            return
+        last = self._sync_times.get(path, 0.0)
+        if interval_ms > 0 and (time.time() - last) * 1000 < interval_ms:
+            return
+        self.sync_metadata(path, recursive)
+        self._sync_times[path] = time.time()
+
+    def sync_metadata(self, path: str, recursive: bool = True) -> dict:
+        """Reconcile Alluxio metadata under ``path`` with the UFS (InodeSyncStream semantics):
+        new UFS entries are loaded, persisted inodes missing from the UFS are removed, files whose
+        UFS fingerprint changed are reloaded (their cached blocks dropped)."""
+        path = normalize_path(path)
+        stats = {"added": 0, "removed": 0, "updated": 0}
+        try:
+            res = self._resolve_ufs(path)
+        except InvalidPathException:
+            return stats
+        st = res.ufs.get_status(res.uri)
+        with self.tree.lock.read():
+            inode = self.tree.get_or_none(path)
+        if st is None:
+            if inode is not None and inode.is_persisted and path != "/":
+                self.delete(path, recursive=True, alluxio_only=True)
+                stats["removed"] += 1
+            return stats
+        if inode is None:
+            self.load_metadata(path, recursive=recursive, create_ancestors=True, quiet=True)
+            stats["added"] += 1
+            return stats
+        if inode.is_file:
+            fp = Fingerprint.create(res.ufs.ufs_type, st)
+            old = Fingerprint.parse(inode.ufs_fingerprint)
+            if inode.is_persisted and (old is None or not fp.matches_content(old)):
+                self.delete(path, alluxio_only=True)
+                self.load_metadata(path, quiet=True)
+                stats["updated"] += 1
+            return stats
+        listing = {s.name: s for s in (res.ufs.list_status(res.uri) or [])}
+        with self.tree.lock.read():
+            kids = {c.name: c for c in self.tree.list_children(inode)}
+        for name, c in kids.items():
+            cp = path.rstrip("/") + "/" + name
+            if name not in listing and c.is_persisted and not self.mount_table.is_mount_point(cp):
+                self.delete(cp, recursive=True, alluxio_only=True)
+                stats["removed"] += 1
+            elif name in listing and recursive:
+                sub = self.sync_metadata(cp, recursive)
+                for k in stats:
+                    stats[k] += sub[k]
+        new = [n for n in listing if n not in kids]
+        if new:
+            self.load_metadata(path, recursive=recursive, create_ancestors=False, quiet=True)
+            stats["added"] += len(new)
+        return stats
+
+    def check_consistency(self, path: str, recursive: bool = True) -> list[str]:
+        path = normalize_path(path)
+        bad = []
+        with self.tree.lock.read():
+            root = self.tree.get(path)
+            nodes = [root] + (self.tree.descendants(root) if root.is_directory else [])
+            items = [(n, self.tree.path_of(n)) for n in nodes]
+        for n, p in items:
+            if not n.is_persisted:
+                continue
+            res = self._resolve_ufs(p)
+            st = res.ufs.get_status(res.uri)
+            if st is None or st.is_directory != n.is_directory or \
+                    (n.is_file and n.completed and st.content_length != n.length):
+                bad.append(p)
+        return sorted(bad)
+
+    # sync points (active sync)
+    def start_sync(self, path: str) -> None:
+        path = normalize_path(path)
+        res = self._resolve_ufs(path)
+        with RpcContext(self) as rpc:
+            self._apply(rpc, pb.journal.JournalEntry(add_sync_point=pb.journal.AddSyncPointEntry(
+                syncpoint_path=path, mount_id=res.mount_id)))
+
+    def stop_sync(self, path: str) -> None:
+        path = normalize_path(path)
+        with RpcContext(self) as rpc:
+            self._apply(rpc, pb.journal.JournalEntry(remove_sync_point=pb.journal.RemoveSyncPointEntry(
+                syncpoint_path=path, mount_id=self.sync_points.get(path, 0))))
+
+    def active_sync_heartbeat(self) -> None:
+        for p in list(self.sync_points):
+            try:
+                self.sync_metadata(p, recursive=True)
+            except Exception:  # noqa: BLE001
+                LOG.exception("active sync of %s failed", p)
+
+    # ------------------------------------------------------------------------------------------
+    # persistence
+    def schedule_async_persistence(self, path: str, persistence_wait_ms: int = 0) -> None:
+        path = normalize_path(path)
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            f = self.tree.get(path)
+            if not f.is_file:
+                raise InvalidPathException(f"{path} is not a file")
+            self._schedule_persist_locked(rpc, f, persistence_wait_ms)
+
+    def _schedule_persist_locked(self, rpc, f, wait_ms) -> None:
+        if f.is_persisted or f.persistence_state == TO_BE_PERSISTED:
+            return
+        self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+            id=f.id, persistence_state=TO_BE_PERSISTED)))
+        if wait_ms:
+            self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(id=f.id)))
+            f.should_persist_time = now_ms() + wait_ms
+
+    def persistence_scheduler_heartbeat(self) -> int:
+        """Submit persist jobs for TO_BE_PERSISTED files (PersistenceScheduler)."""
+        if self.persist_handler is None:
+            return 0
+        with self.tree.lock.read():
+            todo = [(fid, self.tree.path_of(self.tree.inodes[fid])) for fid in self.tree.to_be_persisted
+                    if fid in self.tree.inodes and fid not in self.persist_jobs
+                    and self.tree.inodes[fid].completed
+                    and self.tree.inodes[fid].should_persist_time <= now_ms()]
+        n = 0
+        for fid, p in todo:
+            try:
+                job = self.persist_handler(fid, p)
+                self.persist_jobs[fid] = {"job": job, "path": p, "start": time.time()}
+                n += 1
+            except Exception:  # noqa: BLE001
+                LOG.exception("failed to schedule persist of %s", p)
+        return n
+
+    def persist_done(self, file_id: int, ok: bool) -> None:
+        """Persistence checker callback: mark the file persisted (journaled)."""
+        self.persist_jobs.pop(file_id, None)
+        if not ok:
+            return
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            f = self.tree.inodes.get(file_id)
+            if f is None or f.is_persisted:
+                return
+            path = self.tree.path_of(f)
+            fp = Fingerprint.INVALID
+            try:
+                res = self._resolve_ufs(path)
+                fp = res.ufs.get_fingerprint(res.uri)
+                # persisting a file also persists its ancestors
+                cur = self.tree.inodes.get(f.parent_id)
+                while cur is not None and not cur.is_persisted:
+                    self._apply(rpc, pb.journal.JournalEntry(persist_directory=pb.journal.PersistDirectoryEntry(id=cur.id)))
+                    cur = self.tree.inodes.get(cur.parent_id)
+            except Exception:  # noqa: BLE001
+                pass
+            self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+                id=file_id, persistence_state=PERSISTED, ufs_fingerprint=fp)))
+
+    def worker_heartbeat(self, worker_id: int, persisted_files: list[int]):
+        for fid in persisted_files:
+            self.persist_done(fid, True)
+        return pb.file.FileSystemCommand(commandType=pb.grpc.CommandType.values_by_name["Nothing"].number)
+
+    def pinned_file_ids(self) -> list[int]:
+        with self.tree.lock.read():
+            out = set()
+            for iid in self.tree.pinned_ids:
+                n = self.tree.inodes.get(iid)
+                if n is None:
+                    continue
+                if n.is_file:
+                    out.add(iid)
+                else:
+                    out.update(d.id for d in self.tree.descendants(n) if d.is_file)
+            return sorted(out)
+
+    # ------------------------------------------------------------------------------------------
+    # background executors
+    def ttl_check(self) -> list[str]:
+        """Expire inodes whose TTL elapsed: DELETE removes them, FREE frees their blocks."""
+        now = now_ms()
+        with self.tree.lock.read():
+            expired = []
+            for iid in self.tree.ttl_buckets.expired(now):
+                n = self.tree.inodes.get(iid)
+                if n is None or n.ttl == NO_TTL or n.creation_time_ms + n.ttl > now:
+                    continue
+                expired.append((self.tree.path_of(n), n.ttl_action, n.is_directory))
+        done = []
+        for p, action, is_dir in expired:
+            try:
+                if action == "FREE":
+                    self.free(p, recursive=True, forced=True)
+                    self.set_attribute(p, ttl=NO_TTL, ttl_action="DELETE")
+                else:
+                    self.delete(p, recursive=True, unchecked=True)
+                done.append(p)
+            except Exception:  # noqa: BLE001
+                LOG.exception("TTL action on %s failed", p)
+        return done
+
+    def lost_files_check(self) -> list[int]:
+        """Mark non-persisted files whose blocks have no location as LOST."""
+        lost_blocks = self.block_master.lost_blocks()
+        if not lost_blocks:
+            return []
+        out = []
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            for bid in lost_blocks:
+                f = self.tree.inodes.get(ids.get_file_id(bid))
+                if f is None or not f.is_file or f.persistence_state in (PERSISTED, LOST):
+                    continue
+                self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+                    id=f.id, persistence_state=LOST)))
+                out.append(f.id)
+        return out
+
+    def block_integrity_check(self, repair: bool = True) -> list[int]:
+        """Blocks known to the block master whose file no longer exists (orphans)."""
+        orphans = []
+        with self.tree.lock.read():
+            for w in self.block_master.workers():
+                for bid in list(w.blocks):
+                    f = self.tree.inodes.get(ids.get_file_id(bid))
+                    if f is None or not f.is_file or (f.completed and bid not in f.block_ids):
+                        orphans.append(bid)
+        if orphans and repair:
+            self.block_master.remove_blocks(sorted(set(orphans)), delete=True)
+        return sorted(set(orphans))
+
+    def replication_targets(self):
+        """(file path, block id, current replicas, min, max) for files with replication limits."""
+        out = []
+        with self.tree.lock.read():
+            for fid in list(self.tree.replication_limited):
+                f = self.tree.inodes.get(fid)
+                if f is None or not f.completed:
+                    continue
+                p = self.tree.path_of(f)
+                for bid in f.block_ids:
+                    bi = self.block_master.block_info_or_none(bid)
+                    n = len(bi.locations) if bi is not None else 0
+                    out.append((p, bid, n, f.replication_min, f.replication_max, f.pinned))
+        return out
+
+    def total_paths(self) -> int:
+        return len(self.tree.inodes)

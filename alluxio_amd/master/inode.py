@@ -1,0 +1,248 @@
+"""Inodes (files and directories) and their journal/wire encodings.
+
+Parity: core/server/master/src/main/java/alluxio/master/file/meta/MutableInode{,File,Directory}.java
+(fields, ``toJournalEntry``, ``fromJournalEntry``, ``updateFromEntry``) and the ``FileInfo``
+generation in DefaultFileSystemMaster.getFileInfoInternal (DefaultFileSystemMaster.java:818-891).
+"""
+from __future__ import annotations
+
+import time
+
+from ..proto import pb
+from ..utils import ids
+
+NO_TTL = -1
+UNKNOWN_SIZE = -1
+
+PERSISTED = "PERSISTED"
+NOT_PERSISTED = "NOT_PERSISTED"
+TO_BE_PERSISTED = "TO_BE_PERSISTED"
+LOST = "LOST"
+
+
+def now_ms() -> int:
+    return int(time.time() * 1000)
+
+
+class Inode:
+    is_directory = False
+
+    def __init__(self, id: int, parent_id: int, name: str, owner: str = "", group: str = "",
+                 mode: int = 0o755, creation_ms: int | None = None):
+        self.id = id
+        self.parent_id = parent_id
+        self.name = name
+        self.owner = owner
+        self.group = group
+        self.mode = mode
+        self.creation_time_ms = creation_ms if creation_ms is not None else now_ms()
+        self.last_modification_time_ms = self.creation_time_ms
+        self.last_access_time_ms = self.creation_time_ms
+        self.persistence_state = NOT_PERSISTED
+        self.pinned = False
+        self.ttl = NO_TTL
+        self.ttl_action = "DELETE"
+        self.ufs_fingerprint = ""
+        self.xattr: dict[str, bytes] = {}
+        self.medium_types: list[str] = []
+        self.acl = None           # alluxio_amd.security.acl.AccessControlList | None
+        self.deleted = False
+
+    @property
+    def is_file(self) -> bool:
+        return not self.is_directory
+
+    @property
+    def is_persisted(self) -> bool:
+        return self.persistence_state == PERSISTED
+
+    def update_from(self, e) -> None:
+        """Apply an UpdateInodeEntry (reference MutableInode.updateFromEntry)."""
+        if e.HasField("parent_id"):
+            self.parent_id = e.parent_id
+        if e.HasField("name"):
+            self.name = e.name
+        if e.HasField("persistence_state"):
+            self.persistence_state = e.persistence_state
+        if e.HasField("pinned"):
+            self.pinned = e.pinned
+        if e.HasField("creation_time_ms"):
+            self.creation_time_ms = e.creation_time_ms
+        if e.HasField("last_modification_time_ms"):
+            if e.overwrite_modification_time:
+                self.last_modification_time_ms = e.last_modification_time_ms
+            else:
+                self.last_modification_time_ms = max(self.last_modification_time_ms,
+                                                     e.last_modification_time_ms)
+        if e.HasField("last_access_time_ms"):
+            if e.overwrite_access_time:
+                self.last_access_time_ms = e.last_access_time_ms
+            else:
+                self.last_access_time_ms = max(self.last_access_time_ms, e.last_access_time_ms)
+        if e.HasField("owner"):
+            self.owner = e.owner
+        if e.HasField("group"):
+            self.group = e.group
+        if e.HasField("mode"):
+            self.mode = e.mode
+        if e.HasField("ttl"):
+            self.ttl = e.ttl
+        if e.HasField("ttlAction"):
+            self.ttl_action = pb.journal.PTtlAction.values_by_number[e.ttlAction].name
+        if e.HasField("ufs_fingerprint"):
+            self.ufs_fingerprint = e.ufs_fingerprint
+        if e.medium_type:
+            self.medium_types = list(e.medium_type)
+        if e.xAttr:
+            self.xattr.update(dict(e.xAttr))
+
+
+class InodeDirectory(Inode):
+    is_directory = True
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.mount_point = False
+        self.direct_children_loaded = False
+        self.default_acl = None
+
+    def to_entry(self, path: str = ""):
+        e = pb.journal.InodeDirectoryEntry(
+            id=self.id, parent_id=self.parent_id, name=self.name,
+            persistence_state=self.persistence_state, pinned=self.pinned,
+            creation_time_ms=self.creation_time_ms,
+            last_modification_time_ms=self.last_modification_time_ms, owner=self.owner,
+            group=self.group, mode=self.mode, mount_point=self.mount_point,
+            direct_children_loaded=self.direct_children_loaded, ttl=self.ttl,
+            ttlAction=pb.journal.PTtlAction.values_by_name[self.ttl_action].number,
+            last_access_time_ms=self.last_access_time_ms, medium_type=self.medium_types)
+        if path:
+            e.path = path
+        for k, v in self.xattr.items():
+            e.xAttr[k] = v
+        if self.acl is not None:
+            e.acl.CopyFrom(self.acl.to_proto())
+        if self.default_acl is not None:
+            e.defaultAcl.CopyFrom(self.default_acl.to_proto())
+        return pb.journal.JournalEntry(inode_directory=e)
+
+    @staticmethod
+    def from_entry(e) -> "InodeDirectory":
+        d = InodeDirectory(e.id, e.parent_id, e.name, e.owner, e.group, e.mode, e.creation_time_ms)
+        d.persistence_state = e.persistence_state or NOT_PERSISTED
+        d.pinned = e.pinned
+        d.last_modification_time_ms = e.last_modification_time_ms
+        d.last_access_time_ms = e.last_access_time_ms or e.last_modification_time_ms
+        d.mount_point = e.mount_point
+        d.direct_children_loaded = e.direct_children_loaded
+        d.ttl = e.ttl if e.HasField("ttl") else NO_TTL
+        d.ttl_action = pb.journal.PTtlAction.values_by_number[e.ttlAction].name
+        d.xattr = dict(e.xAttr)
+        d.medium_types = list(e.medium_type)
+        if e.HasField("acl"):
+            from ..security.acl import AccessControlList
+            d.acl = AccessControlList.from_proto(e.acl)
+        if e.HasField("defaultAcl"):
+            from ..security.acl import AccessControlList
+            d.default_acl = AccessControlList.from_proto(e.defaultAcl)
+        return d
+
+
+class InodeFile(Inode):
+    def __init__(self, *a, block_size: int = 64 << 20, **kw):
+        super().__init__(*a, **kw)
+        self.block_size_bytes = block_size
+        self.length = 0
+        self.completed = False
+        self.cacheable = True
+        self.block_ids: list[int] = []
+        self.replication_min = 0
+        self.replication_max = -1
+        self.replication_durable = 1
+        self.persist_job_id = -1
+        self.temp_ufs_path = ""
+        self.should_persist_time = 0
+        self._next_seq = 0
+
+    @property
+    def block_container_id(self) -> int:
+        return ids.get_container_id(self.id)
+
+    def new_block_id(self) -> int:
+        bid = ids.create_block_id(self.block_container_id, self._next_seq)
+        self._next_seq += 1
+        return bid
+
+    def to_entry(self, path: str = ""):
+        e = pb.journal.InodeFileEntry(
+            id=self.id, parent_id=self.parent_id, name=self.name,
+            persistence_state=self.persistence_state, pinned=self.pinned,
+            creation_time_ms=self.creation_time_ms,
+            last_modification_time_ms=self.last_modification_time_ms,
+            block_size_bytes=self.block_size_bytes, length=self.length, completed=self.completed,
+            cacheable=self.cacheable, blocks=self.block_ids, ttl=self.ttl, owner=self.owner,
+            group=self.group, mode=self.mode,
+            ttlAction=pb.journal.PTtlAction.values_by_name[self.ttl_action].number,
+            ufs_fingerprint=self.ufs_fingerprint, replication_max=self.replication_max,
+            replication_min=self.replication_min, persist_job_id=self.persist_job_id,
+            temp_ufs_path=self.temp_ufs_path, replication_durable=self.replication_durable,
+            medium_type=self.medium_types, should_persist_time=self.should_persist_time,
+            last_access_time_ms=self.last_access_time_ms)
+        if path:
+            e.path = path
+        for k, v in self.xattr.items():
+            e.xAttr[k] = v
+        if self.acl is not None:
+            e.acl.CopyFrom(self.acl.to_proto())
+        return pb.journal.JournalEntry(inode_file=e)
+
+    @staticmethod
+    def from_entry(e) -> "InodeFile":
+        f = InodeFile(e.id, e.parent_id, e.name, e.owner, e.group, e.mode, e.creation_time_ms,
+                      block_size=e.block_size_bytes)
+        f.persistence_state = e.persistence_state or NOT_PERSISTED
+        f.pinned = e.pinned
+        f.last_modification_time_ms = e.last_modification_time_ms
+        f.last_access_time_ms = e.last_access_time_ms or e.last_modification_time_ms
+        f.length = e.length
+        f.completed = e.completed
+        f.cacheable = e.cacheable
+        f.block_ids = list(e.blocks)
+        f._next_seq = len(f.block_ids)
+        f.ttl = e.ttl if e.HasField("ttl") else NO_TTL
+        f.ttl_action = pb.journal.PTtlAction.values_by_number[e.ttlAction].name
+        f.ufs_fingerprint = e.ufs_fingerprint
+        f.replication_max = e.replication_max if e.HasField("replication_max") else -1
+        f.replication_min = e.replication_min
+        f.replication_durable = e.replication_durable if e.HasField("replication_durable") else 1
+        f.persist_job_id = e.persist_job_id if e.HasField("persist_job_id") else -1
+        f.temp_ufs_path = e.temp_ufs_path
+        f.should_persist_time = e.should_persist_time
+        f.xattr = dict(e.xAttr)
+        f.medium_types = list(e.medium_type)
+        if e.HasField("acl"):
+            from ..security.acl import AccessControlList
+            f.acl = AccessControlList.from_proto(e.acl)
+        return f
+
+    def update_file_from(self, e) -> None:
+        """Apply an UpdateInodeFileEntry."""
+        if e.HasField("block_size_bytes"):
+            self.block_size_bytes = e.block_size_bytes
+        if e.HasField("length"):
+            self.length = e.length
+        if e.HasField("completed"):
+            self.completed = e.completed
+        if e.HasField("cacheable"):
+            self.cacheable = e.cacheable
+        if e.set_blocks:
+            self.block_ids = list(e.set_blocks)
+            self._next_seq = max(self._next_seq, len(self.block_ids))
+        if e.HasField("replication_max"):
+            self.replication_max = e.replication_max
+        if e.HasField("replication_min"):
+            self.replication_min = e.replication_min
+        if e.HasField("persist_job_id"):
+            self.persist_job_id = e.persist_job_id
+        if e.HasField("temp_ufs_path"):
+            self.temp_ufs_path = e.temp_ufs_path

@@ -1,0 +1,385 @@
+"""Inode tree: the namespace, its id generators and journal application.
+
+Parity: core/server/master/src/main/java/alluxio/master/file/meta/InodeTree.java (root
+initialisation ``initializeRoot`` :233, ``lockInodePath`` :375-436, ``createPath`` :670),
+InodeTreePersistentState.java (every mutation is a journal entry applied through one code path,
+for both live RPCs and replay), InodeDirectoryIdGenerator (directory ids = container id ||
+sequence, containers drawn from the block master), TtlBucketList (TTL expiry buckets).
+
+Concurrency: a tree-wide reader/writer lock.  Lookups (``getStatus``/``listStatus`` — the
+metadata hot path) share it; mutations are serialised.  With CPython's GIL a finer-grained
+per-inode lock scheme would add overhead without adding parallelism.
+"""
+from __future__ import annotations
+
+import bisect
+import threading
+
+from ..proto import pb
+from ..utils import ids
+from ..utils.exceptions import (FileAlreadyExistsException, FileDoesNotExistException,
+                                InvalidPathException)
+from ..utils.locks import RWLock
+from ..utils.uri import normalize_path, path_components
+from .inode import NO_TTL, Inode, InodeDirectory, InodeFile, now_ms
+
+
+class DirectoryIdGenerator:
+    def __init__(self, container_source):
+        self._source = container_source  # callable -> new container id
+        self.container_id = -1
+        self.sequence = ids.MAX_SEQUENCE_NUMBER + 1  # force a new container on first use
+        self._lock = threading.Lock()
+
+    def next_id(self) -> tuple[int, object | None]:
+        """Returns (id, journal entry or None) — entry records a new container/sequence."""
+        with self._lock:
+            entry = None
+            if self.sequence > ids.MAX_SEQUENCE_NUMBER - 1:
+                self.container_id = self._source()
+                self.sequence = 0
+            did = ids.create_block_id(self.container_id, self.sequence)
+            self.sequence += 1
+            entry = pb.journal.JournalEntry(inode_directory_id_generator=pb.journal.InodeDirectoryIdGeneratorEntry(
+                container_id=self.container_id, sequence_number=self.sequence))
+            return did, entry
+
+    def apply(self, e) -> None:
+        with self._lock:
+            self.container_id = e.container_id
+            self.sequence = e.sequence_number
+
+
+class TtlBuckets:
+    """Inodes grouped by expiry interval (reference TtlBucketList: interval = check period)."""
+
+    def __init__(self, interval_ms: int = 3_600_000):
+        self.interval = max(1, interval_ms)
+        self._buckets: dict[int, set[int]] = {}
+        self._starts: list[int] = []
+        self._lock = threading.Lock()
+
+    def _start(self, expiry_ms: int) -> int:
+        return expiry_ms - expiry_ms % self.interval
+
+    def insert(self, inode: Inode) -> None:
+        if inode.ttl == NO_TTL:
+            return
+        s = self._start(inode.creation_time_ms + inode.ttl)
+        with self._lock:
+            if s not in self._buckets:
+                self._buckets[s] = set()
+                bisect.insort(self._starts, s)
+            self._buckets[s].add(inode.id)
+
+    def remove(self, inode: Inode) -> None:
+        with self._lock:
+            for s in list(self._buckets):
+                self._buckets[s].discard(inode.id)
+                if not self._buckets[s]:
+                    del self._buckets[s]
+                    self._starts.remove(s)
+
+    def expired(self, now: int) -> list[int]:
+        with self._lock:
+            out = []
+            for s in self._starts:
+                if s + self.interval > now:
+                    break
+                out.extend(self._buckets[s])
+            return out
+
+    def clear(self) -> None:
+        with self._lock:
+            self._buckets.clear()
+            self._starts.clear()
+
+
+class InodeTree:
+    ROOT_NAME = ""
+
+    def __init__(self, container_source, ttl_interval_ms: int = 3_600_000):
+        self.lock = RWLock()
+        self.inodes: dict[int, Inode] = {}
+        self.children: dict[int, dict[str, int]] = {}
+        self.root: InodeDirectory | None = None
+        self.dir_ids = DirectoryIdGenerator(container_source)
+        self.ttl_buckets = TtlBuckets(ttl_interval_ms)
+        self.pinned_ids: set[int] = set()
+        self.to_be_persisted: set[int] = set()
+        self.replication_limited: set[int] = set()
+
+    # ---- state ------------------------------------------------------------------------------
+    def reset(self) -> None:
+        self.inodes.clear()
+        self.children.clear()
+        self.root = None
+        self.ttl_buckets.clear()
+        self.pinned_ids.clear()
+        self.to_be_persisted.clear()
+        self.replication_limited.clear()
+
+    def _add(self, inode: Inode) -> None:
+        self.inodes[inode.id] = inode
+        if inode.is_directory:
+            self.children.setdefault(inode.id, {})
+        if inode.parent_id >= 0 and inode.parent_id in self.children and inode.name != self.ROOT_NAME:
+            self.children[inode.parent_id][inode.name] = inode.id
+        if inode.parent_id == -1 or (inode.is_directory and inode.name == self.ROOT_NAME and self.root is None):
+            self.root = inode  # type: ignore[assignment]
+        self._index(inode)
+
+    def _index(self, inode: Inode) -> None:
+        if inode.pinned:
+            self.pinned_ids.add(inode.id)
+        else:
+            self.pinned_ids.discard(inode.id)
+        self.ttl_buckets.remove(inode)
+        self.ttl_buckets.insert(inode)
+        if inode.is_file:
+            if inode.persistence_state == "TO_BE_PERSISTED":
+                self.to_be_persisted.add(inode.id)
+            else:
+                self.to_be_persisted.discard(inode.id)
+            if inode.replication_min > 0 or inode.replication_max >= 0:
+                self.replication_limited.add(inode.id)
+            else:
+                self.replication_limited.discard(inode.id)
+
+    def _remove(self, inode: Inode) -> None:
+        self.inodes.pop(inode.id, None)
+        kids = self.children.get(inode.parent_id)
+        if kids is not None and kids.get(inode.name) == inode.id:
+            del kids[inode.name]
+        self.children.pop(inode.id, None)
+        self.pinned_ids.discard(inode.id)
+        self.to_be_persisted.discard(inode.id)
+        self.replication_limited.discard(inode.id)
+        self.ttl_buckets.remove(inode)
+        inode.deleted = True
+
+    # ---- journal application (single code path for replay and live ops) ---------------------
+    def apply(self, e) -> bool:
+        kind = e.WhichOneof_name if hasattr(e, "WhichOneof_name") else None
+        if e.HasField("inode_directory"):
+            self._add(InodeDirectory.from_entry(e.inode_directory))
+        elif e.HasField("inode_file"):
+            self._add(InodeFile.from_entry(e.inode_file))
+        elif e.HasField("inode_directory_id_generator"):
+            self.dir_ids.apply(e.inode_directory_id_generator)
+        elif e.HasField("update_inode"):
+            u = e.update_inode
+            inode = self.inodes.get(u.id)
+            if inode is None:
+                return True
+            old_parent, old_name = inode.parent_id, inode.name
+            inode.update_from(u)
+            if (inode.parent_id, inode.name) != (old_parent, old_name):
+                kids = self.children.get(old_parent)
+                if kids is not None and kids.get(old_name) == inode.id:
+                    del kids[old_name]
+                self.children.setdefault(inode.parent_id, {})[inode.name] = inode.id
+            self._index(inode)
+        elif e.HasField("update_inode_directory"):
+            u = e.update_inode_directory
+            d = self.inodes.get(u.id)
+            if d is not None and d.is_directory:
+                if u.HasField("mount_point"):
+                    d.mount_point = u.mount_point
+                if u.HasField("direct_children_loaded"):
+                    d.direct_children_loaded = u.direct_children_loaded
+                if u.HasField("defaultAcl"):
+                    from ..security.acl import AccessControlList
+                    d.default_acl = AccessControlList.from_proto(u.defaultAcl)
+        elif e.HasField("update_inode_file"):
+            u = e.update_inode_file
+            f = self.inodes.get(u.id)
+            if f is not None and f.is_file:
+                f.update_file_from(u)
+                self._index(f)
+        elif e.HasField("delete_file"):
+            inode = self.inodes.get(e.delete_file.id)
+            if inode is not None:
+                self._remove(inode)
+        elif e.HasField("rename"):
+            r = e.rename
+            inode = self.inodes.get(r.id)
+            if inode is not None:
+                kids = self.children.get(inode.parent_id)
+                if kids is not None and kids.get(inode.name) == inode.id:
+                    del kids[inode.name]
+                inode.parent_id = r.new_parent_id
+                inode.name = r.new_name
+                self.children.setdefault(r.new_parent_id, {})[r.new_name] = inode.id
+                inode.last_modification_time_ms = r.op_time_ms or inode.last_modification_time_ms
+        elif e.HasField("set_acl"):
+            s = e.set_acl
+            inode = self.inodes.get(s.id)
+            if inode is not None:
+                self._apply_set_acl(inode, s)
+        elif e.HasField("inode_last_modification_time"):
+            inode = self.inodes.get(e.inode_last_modification_time.id)
+            if inode is not None:
+                inode.last_modification_time_ms = e.inode_last_modification_time.last_modification_time_ms
+        elif e.HasField("persist_directory"):
+            inode = self.inodes.get(e.persist_directory.id)
+            if inode is not None:
+                inode.persistence_state = "PERSISTED"
+        elif e.HasField("set_attribute"):
+            s = e.set_attribute
+            inode = self.inodes.get(s.id)
+            if inode is not None:
+                if s.HasField("pinned"):
+                    inode.pinned = s.pinned
+                if s.HasField("ttl"):
+                    inode.ttl = s.ttl
+                if s.HasField("persisted") and s.persisted:
+                    inode.persistence_state = "PERSISTED"
+                if s.HasField("owner"):
+                    inode.owner = s.owner
+                if s.HasField("group"):
+                    inode.group = s.group
+                if s.HasField("permission"):
+                    inode.mode = s.permission
+                self._index(inode)
+        elif e.HasField("complete_file"):  # legacy form
+            c = e.complete_file
+            f = self.inodes.get(c.id)
+            if f is not None and f.is_file:
+                f.block_ids = list(c.block_ids)
+                f.length = c.length
+                f.completed = True
+                f.last_modification_time_ms = c.op_time_ms
+        elif e.HasField("async_persist_request"):
+            f = self.inodes.get(e.async_persist_request.file_id)
+            if f is not None:
+                f.persistence_state = "TO_BE_PERSISTED"
+                self._index(f)
+        else:
+            return False
+        return True
+
+    @staticmethod
+    def _apply_set_acl(inode: Inode, s) -> None:
+        from ..security.acl import AccessControlList, AclEntry, AclEntryType
+        entries = [AclEntry.from_proto(x) for x in s.entries]
+        action = pb.journal.PSetAclAction.values_by_number[s.action].name
+        acl = inode.acl or AccessControlList(inode.owner, inode.group, inode.mode)
+        acl.mode = inode.mode
+        dacl = getattr(inode, "default_acl", None)
+        if action == "REMOVE_ALL":
+            acl.clear_extended()
+        elif action == "REMOVE_DEFAULT":
+            if inode.is_directory:
+                inode.default_acl = None
+        for e in entries:
+            target_default = e.is_default and inode.is_directory
+            if target_default:
+                if dacl is None:
+                    dacl = AccessControlList(inode.owner, inode.group, inode.mode, is_default=True)
+                    inode.default_acl = dacl
+                tgt = dacl
+            else:
+                tgt = acl
+            if action in ("REPLACE", "MODIFY"):
+                tgt.set_entry(e)
+            elif action == "REMOVE":
+                tgt.remove_entry(e)
+        if action == "REPLACE":
+            keep_u = {e.subject for e in entries if e.type == AclEntryType.NAMED_USER and not e.is_default}
+            keep_g = {e.subject for e in entries if e.type == AclEntryType.NAMED_GROUP and not e.is_default}
+            acl.named_users = {k: v for k, v in acl.named_users.items() if k in keep_u}
+            acl.named_groups = {k: v for k, v in acl.named_groups.items() if k in keep_g}
+        inode.mode = acl.mode
+        inode.acl = acl if acl.is_extended else None
+
+    # ---- lookups ----------------------------------------------------------------------------
+    def resolve(self, path: str) -> tuple[list[Inode], list[str]]:
+        """Return (existing inode chain from root, remaining missing components)."""
+        comps = path_components(path)
+        chain: list[Inode] = [self.root]
+        cur = self.root
+        for i, c in enumerate(comps):
+            if not cur.is_directory:
+                raise InvalidPathException(f"{path}: {cur.name} is a file")
+            cid = self.children.get(cur.id, {}).get(c)
+            if cid is None:
+                return chain, comps[i:]
+            cur = self.inodes[cid]
+            chain.append(cur)
+        return chain, []
+
+    def get(self, path: str) -> Inode:
+        chain, missing = self.resolve(path)
+        if missing:
+            raise FileDoesNotExistException(f"Path \"{normalize_path(path)}\" does not exist.")
+        return chain[-1]
+
+    def get_or_none(self, path: str) -> Inode | None:
+        try:
+            chain, missing = self.resolve(path)
+        except InvalidPathException:
+            return None
+        return None if missing else chain[-1]
+
+    def exists(self, path: str) -> bool:
+        return self.get_or_none(path) is not None
+
+    def path_of(self, inode: Inode) -> str:
+        parts = []
+        cur = inode
+        while cur is not None and cur.id != self.root.id:
+            parts.append(cur.name)
+            cur = self.inodes.get(cur.parent_id)
+            if cur is None:
+                raise FileDoesNotExistException(f"inode {inode.id} is detached")
+        return "/" + "/".join(reversed(parts))
+
+    def list_children(self, inode: Inode) -> list[Inode]:
+        kids = self.children.get(inode.id, {})
+        return [self.inodes[k] for _, k in sorted(kids.items())]
+
+    def descendants(self, inode: Inode) -> list[Inode]:
+        """Post-order (children before parent) list of all descendants, excluding ``inode``."""
+        out = []
+        stack = [(inode, False)]
+        while stack:
+            n, visited = stack.pop()
+            if visited:
+                if n is not inode:
+                    out.append(n)
+                continue
+            stack.append((n, True))
+            if n.is_directory:
+                for c in self.list_children(n):
+                    stack.append((c, False))
+        return out
+
+    # ---- entry builders (live path) ---------------------------------------------------------
+    def new_directory_entries(self, parent: Inode, name: str, owner: str, group: str, mode: int,
+                              persisted: bool, mount_point: bool = False, ttl: int = NO_TTL,
+                              ttl_action: str = "DELETE"):
+        did, gen_entry = self.dir_ids.next_id()
+        d = InodeDirectory(did, parent.id if parent else -1, name, owner, group, mode, now_ms())
+        d.persistence_state = "PERSISTED" if persisted else "NOT_PERSISTED"
+        d.mount_point = mount_point
+        d.ttl, d.ttl_action = ttl, ttl_action
+        if parent is not None and getattr(parent, "default_acl", None) is not None:
+            d.default_acl = parent.default_acl
+        return [gen_entry, d.to_entry()]
+
+    def new_file_entry(self, parent: Inode, name: str, file_id: int, owner: str, group: str, mode: int,
+                       block_size: int, persisted_state: str, ttl: int = NO_TTL, ttl_action: str = "DELETE",
+                       replication_min: int = 0, replication_max: int = -1, replication_durable: int = 1,
+                       cacheable: bool = True):
+        f = InodeFile(file_id, parent.id, name, owner, group, mode, now_ms(), block_size=block_size)
+        f.persistence_state = persisted_state
+        f.ttl, f.ttl_action = ttl, ttl_action
+        f.replication_min, f.replication_max = replication_min, replication_max
+        f.replication_durable = replication_durable
+        f.cacheable = cacheable
+        return f.to_entry()
+
+    def check_no_conflict(self, parent: Inode, name: str) -> None:
+        if name in self.children.get(parent.id, {}):
+            raise FileAlreadyExistsException(f"{name} already exists under {self.path_of(parent)}")

@@ -1,0 +1,226 @@
+"""Master process: journal system + masters + RPC server + background heartbeats.
+
+Parity: core/server/master/src/main/java/alluxio/master/AlluxioMasterProcess.java (ctor :97-127,
+start :156-161 — journal start, gainPrimacy, startMasters :197-221, startServingRPCServer
+:300-340), Factory.create :387-401 (journal type selection), FaultTolerantAlluxioMasterProcess
+(standby tails the journal until it gains primacy), SafeModeManager, StateLockManager (blocks
+mutations while a backup/checkpoint snapshot is taken), and the heartbeat executors started by
+DefaultFileSystemMaster.start / DefaultBlockMaster.start.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import time
+
+from ..conf import Configuration
+from ..journal.system import NoopJournalSystem, UfsJournalSystem
+from ..rpc import RpcServer
+from ..utils import heartbeat as hb
+from .block_master import BlockMaster
+from .file_system_master import FileSystemMaster
+from .meta_master import MetaMaster, MetaServices, MetricsMaster, restore_backup
+from .services import (SVC_BLOCK_CLIENT, SVC_BLOCK_WORKER, SVC_FS_CLIENT, SVC_FS_JOB, SVC_FS_WORKER,
+                       SVC_JOURNAL, SVC_META_CLIENT, SVC_META_CONFIG, SVC_META_MASTER, SVC_METRICS,
+                       SVC_SASL, SVC_VERSION, BlockMasterClientServiceHandler,
+                       BlockMasterWorkerServiceHandler, FileSystemMasterClientServiceHandler,
+                       FileSystemMasterWorkerServiceHandler, SaslHandler, ServiceVersionHandler)
+
+LOG = logging.getLogger(__name__)
+
+
+class StateLockManager:
+    """Shared lock held by every mutating RPC; exclusive during backups (StateLockManager.java)."""
+
+    def __init__(self):
+        from ..utils.locks import RWLock
+        self._lock = RWLock()
+
+    def acquire_shared(self):
+        self._lock.acquire_read()
+
+    def release_shared(self):
+        self._lock.release_read()
+
+    def exclusive(self):
+        return self._lock.write()
+
+
+class SafeModeManager:
+    def __init__(self, wait_ms: int):
+        self.wait_ms = wait_ms
+        self._until = 0.0
+
+    def notify_primary(self):
+        self._until = time.time() + self.wait_ms / 1000.0
+
+    def in_safe_mode(self) -> bool:
+        return time.time() < self._until
+
+
+def build_journal_system(conf: Configuration):
+    jtype = conf.get("alluxio.master.journal.type", "UFS").upper()
+    if jtype in ("NOOP", "NONE"):
+        return NoopJournalSystem()
+    folder = conf.get("alluxio.master.journal.folder")
+    if folder.startswith("file://"):
+        folder = folder[len("file://"):]
+    if jtype == "EMBEDDED":
+        LOG.info("journal type EMBEDDED: using the replicated UFS journal implementation at %s", folder)
+    return UfsJournalSystem(folder, max_log_bytes=conf.get_bytes("alluxio.master.journal.log.size.bytes.max"),
+                            flush_batch_ms=conf.get_ms("alluxio.master.journal.flush.batch.time"),
+                            checkpoint_period_entries=conf.get_int("alluxio.master.journal.checkpoint.period.entries"))
+
+
+class AlluxioMasterProcess:
+    def __init__(self, conf: Configuration | None = None, host: str = "127.0.0.1", port: int | None = None,
+                 enable_grpc: bool = True, root_ufs: str | None = None, journal_system=None):
+        self.conf = conf or Configuration(load_site=True)
+        self.host = host
+        self.port = self.conf.get_int("alluxio.master.rpc.port") if port is None else port
+        from .. import metrics as msys
+        self.metrics = msys.metrics("Master")
+        self.journal = journal_system or build_journal_system(self.conf)
+        self.block_master = BlockMaster(self.conf, self.journal,
+                                        worker_timeout_ms=self.conf.get_ms("alluxio.master.worker.timeout"))
+        self.fs_master = FileSystemMaster(self.conf, self.block_master, self.journal, metrics=self.metrics,
+                                          root_ufs=root_ufs)
+        self.meta_master = MetaMaster(self.conf, self.journal)
+        self.meta_master.block_master = self.block_master
+        self.metrics_master = MetricsMaster()
+        self.block_master.metrics = lambda w, ms: self.metrics_master.worker_heartbeat(w.id, ms)
+        self.state_lock = StateLockManager()
+        self.fs_master.state_lock = self.state_lock
+        self.safe_mode = SafeModeManager(self.conf.get_ms("alluxio.master.worker.connect.wait.time"))
+        for j in (self.block_master, self.fs_master, self.meta_master):
+            self.journal.register(j)
+        self.meta_master.masters_for_backup = [self.block_master, self.fs_master, self.meta_master]
+        self.meta_master.journal_system_for_checkpoint = self.journal
+        self.server = RpcServer(host, self.port, max_workers=self.conf.get_int("alluxio.master.rpc.executor.max.pool.size", 500)
+                                if False else 64, metrics=self.metrics, enable_grpc=enable_grpc)
+        self._threads: list[hb.HeartbeatThread] = []
+        self.job_master = None
+        self.web = None
+        self.started = False
+        self.primary = False
+
+    @property
+    def address(self) -> str:
+        return self.server.address
+
+    def _register_services(self) -> None:
+        s = self.server
+        s.add_servicer(SVC_FS_CLIENT, FileSystemMasterClientServiceHandler(self.fs_master))
+        fsw = FileSystemMasterWorkerServiceHandler(self.fs_master)
+        s.add_servicer(SVC_FS_WORKER, fsw)
+        s.add_servicer(SVC_FS_JOB, fsw)
+        s.add_servicer(SVC_BLOCK_CLIENT, BlockMasterClientServiceHandler(self.block_master))
+        s.add_servicer(SVC_BLOCK_WORKER, BlockMasterWorkerServiceHandler(self.block_master, self.metrics_master))
+        meta = MetaServices(self.meta_master, self.metrics_master, self.journal)
+        for svc in (SVC_META_CLIENT, SVC_META_CONFIG, SVC_META_MASTER, SVC_METRICS, SVC_JOURNAL):
+            s.add_servicer(svc, meta)
+        s.add_servicer(SVC_VERSION, ServiceVersionHandler())
+        s.add_servicer(SVC_SASL, SaslHandler())
+
+    def format(self) -> None:
+        self.journal.format()
+
+    def start(self, primary: bool = True, start_heartbeats: bool = True) -> str:
+        if not self.journal.is_formatted() and isinstance(self.journal, UfsJournalSystem):
+            self.journal.format()
+        self.journal.start()
+        if primary:
+            self.gain_primacy()
+        self._register_services()
+        addr = self.server.start()
+        self.meta_master.master_address = addr
+        if start_heartbeats and primary:
+            self._start_heartbeats()
+        self.started = True
+        LOG.info("master serving at %s", addr)
+        return addr
+
+    def gain_primacy(self) -> None:
+        backup = self.conf.get_raw("alluxio.master.journal.init.from.backup")
+        if backup and self.journal.is_empty():
+            n = restore_backup(backup, [self.block_master, self.fs_master, self.meta_master])
+            LOG.info("restored %d entries from backup %s", n, backup)
+            self.journal.gain_primacy()
+            self.journal.checkpoint()
+        else:
+            self.journal.gain_primacy()
+        self.fs_master.start(True)
+        self.meta_master.start(True)
+        self.safe_mode.notify_primary()
+        self.primary = True
+
+    def _start_heartbeats(self) -> None:
+        c = self.conf
+        specs = [
+            (hb.MASTER_LOST_WORKER_DETECTION, self.block_master.detect_lost_workers,
+             c.get_ms("alluxio.master.lost.worker.detection.interval", "10sec")),
+            (hb.MASTER_TTL_CHECK, self.fs_master.ttl_check, c.get_ms("alluxio.master.ttl.checker.interval")),
+            (hb.MASTER_LOST_FILES_DETECTION, self.fs_master.lost_files_check,
+             c.get_ms("alluxio.master.lost.worker.file.detection.interval", "5min")),
+            (hb.MASTER_PERSISTENCE_SCHEDULER, self.fs_master.persistence_scheduler_heartbeat,
+             c.get_ms("alluxio.master.persistence.scheduler.interval", "1sec")),
+            (hb.MASTER_ACTIVE_UFS_SYNC, self.fs_master.active_sync_heartbeat,
+             c.get_ms("alluxio.master.ufs.active.sync.interval", "30sec")),
+            (hb.MASTER_LOST_MASTER_DETECTION, self.meta_master.detect_lost_masters,
+             c.get_ms("alluxio.master.standby.heartbeat.interval", "2min")),
+        ]
+        if c.get_ms("alluxio.master.periodic.block.integrity.check.interval", "1hr") > 0:
+            specs.append((hb.MASTER_BLOCK_INTEGRITY_CHECK, self.fs_master.block_integrity_check,
+                          c.get_ms("alluxio.master.periodic.block.integrity.check.interval", "1hr")))
+        for name, fn, interval in specs:
+            t = hb.HeartbeatThread(name, fn, interval)
+            t.start()
+            self._threads.append(t)
+
+    def add_heartbeat(self, name: str, fn, interval_ms: int) -> None:
+        t = hb.HeartbeatThread(name, fn, interval_ms)
+        t.start()
+        self._threads.append(t)
+
+    def checkpoint(self) -> None:
+        with self.state_lock.exclusive():
+            self.journal.checkpoint()
+
+    def stop(self) -> None:
+        for t in self._threads:
+            t.shutdown(join=False)
+        for t in self._threads:
+            t.shutdown(join=True)
+        self._threads.clear()
+        if self.web is not None:
+            self.web.stop()
+        self.server.stop()
+        self.journal.stop()
+        self.started = False
+
+
+def main(argv=None) -> int:  # pragma: no cover - CLI entry
+    import argparse
+    ap = argparse.ArgumentParser(description="alluxio_amd master")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--root-ufs", default=None)
+    ap.add_argument("--format", action="store_true")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    m = AlluxioMasterProcess(host=a.host, port=a.port, root_ufs=a.root_ufs)
+    if a.format:
+        m.format()
+    m.start()
+    stop = threading.Event()
+    try:
+        stop.wait()
+    except KeyboardInterrupt:
+        pass
+    m.stop()
+    return 0
+
+
+if __name__ == "__main__":  # pragma: no cover
+    raise SystemExit(main())

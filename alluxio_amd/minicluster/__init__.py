@@ -1,0 +1,116 @@
+"""In-process cluster: one master + N workers in this process.
+
+Parity: minicluster/src/main/java/alluxio/master/LocalAlluxioCluster.java:40-157 and
+AbstractLocalAlluxioCluster.java (temp work dir, local UFS, 1 master + N workers, start/stop,
+``getClient``); tests/.../LocalAlluxioClusterResource.java (per-test config overrides).
+Workers default to the HBM tier when a HIP device is visible (one worker per device, round
+robin) and to a DRAM arena otherwise.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import tempfile
+
+from ..conf import Configuration
+from ..master.process import AlluxioMasterProcess
+from ..worker.process import AlluxioWorkerProcess
+
+DEFAULTS = {
+    "alluxio.master.journal.type": "UFS",
+    "alluxio.worker.tieredstore.levels": "1",
+    "alluxio.worker.tieredstore.level0.alias": "MEM",
+    "alluxio.worker.tieredstore.level0.dirs.path": "auto",
+    "alluxio.worker.tieredstore.level0.dirs.quota": "256MB",
+    "alluxio.worker.hbm.page.size": "1MB",
+    "alluxio.user.block.size.bytes.default": "16MB",
+    "alluxio.master.worker.connect.wait.time": "0sec",
+    "alluxio.security.authorization.permission.enabled": "false",
+    "alluxio.user.file.writetype.default": "CACHE_THROUGH",
+    "alluxio.worker.network.async.cache.manager.threads.max": "4",
+}
+
+
+class LocalAlluxioCluster:
+    def __init__(self, num_workers: int = 1, conf: dict | None = None, work_dir: str | None = None,
+                 grpc: bool = True, heartbeats: bool = False, devices: list[int] | None = None):
+        self.work_dir = work_dir or tempfile.mkdtemp(prefix="alluxio_amd_")
+        self._own_dir = work_dir is None
+        props = dict(DEFAULTS)
+        props["alluxio.work.dir"] = self.work_dir
+        props["alluxio.home"] = self.work_dir
+        props["alluxio.master.journal.folder"] = os.path.join(self.work_dir, "journal")
+        props["alluxio.master.mount.table.root.ufs"] = os.path.join(self.work_dir, "underFSStorage")
+        props.update(conf or {})
+        self.conf = Configuration(props)
+        self.num_workers = num_workers
+        self.grpc = grpc
+        self.heartbeats = heartbeats
+        self.devices = devices
+        self.master: AlluxioMasterProcess | None = None
+        self.workers: list[AlluxioWorkerProcess] = []
+
+    @property
+    def ufs_root(self) -> str:
+        return self.conf.get("alluxio.master.mount.table.root.ufs")
+
+    def start(self) -> "LocalAlluxioCluster":
+        os.makedirs(self.ufs_root, exist_ok=True)
+        self.master = AlluxioMasterProcess(self.conf, port=0, enable_grpc=self.grpc, root_ufs=self.ufs_root)
+        self.master.start(start_heartbeats=self.heartbeats)
+        for i in range(self.num_workers):
+            self.start_worker(i)
+        return self
+
+    def start_worker(self, i: int | None = None) -> AlluxioWorkerProcess:
+        i = len(self.workers) if i is None else i
+        dev = None
+        if self.devices:
+            dev = self.devices[i % len(self.devices)]
+        wconf = self.conf.copy()
+        w = AlluxioWorkerProcess(wconf, master_address=self.master.address, port=0, device=dev,
+                                 enable_grpc=self.grpc, work_dir=os.path.join(self.work_dir, f"worker{i}"))
+        w.start(register=True, start_heartbeats=self.heartbeats)
+        self.workers.append(w)
+        return w
+
+    def stop_worker(self, w: AlluxioWorkerProcess) -> None:
+        w.stop()
+        self.workers.remove(w)
+
+    def client(self, **kw):
+        from ..client.file_system import FileSystem
+        return FileSystem(conf=self.conf.copy(), master_address=self.master.address, **kw)
+
+    def restart_master(self) -> None:
+        self.master.stop()
+        self.master = AlluxioMasterProcess(self.conf, port=0, enable_grpc=self.grpc, root_ufs=self.ufs_root)
+        self.master.start(start_heartbeats=self.heartbeats)
+        for w in self.workers:
+            from ..rpc import Channel
+            w.master_channel = Channel(self.master.address)
+            w.worker.master_channel = w.master_channel
+            w.worker._block_master = None
+            w.worker._fs_master = None
+            w.sync.registered = False
+            w.sync.register()
+
+    def heartbeat_workers(self) -> None:
+        for w in self.workers:
+            w.sync.heartbeat()
+
+    def stop(self) -> None:
+        for w in list(self.workers):
+            w.stop()
+        self.workers.clear()
+        if self.master is not None:
+            self.master.stop()
+            self.master = None
+        if self._own_dir:
+            shutil.rmtree(self.work_dir, ignore_errors=True)
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()

@@ -48,6 +48,9 @@ def lib():
             if os.environ.get("ALLUXIO_AMD_NO_BUILD") != "1":
                 from .build import build
                 build()
+            # One HIP runtime per process: load torch's libamdhip64 first so the extension binds
+            # to the same runtime (same soname) instead of pulling a second copy from /opt/rocm.
+            import torch  # noqa: F401
             _mod = importlib.import_module("alluxio_amd._C")
     return _mod
 

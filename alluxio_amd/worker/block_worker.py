@@ -1,0 +1,403 @@
+"""Block worker facade: session-scoped block operations over the native HBM store.
+
+Parity: core/server/worker/src/main/java/alluxio/worker/block/BlockWorker.java:38-429 and
+DefaultBlockWorker.java (commitBlock :274-306 -> master CommitBlock; createBlock :321-346;
+openUfsBlock :513; metrics :573-616), UnderFileSystemBlockReader (read-through caching of a
+cold block: UFS -> staging -> temp block -> commit), AsyncCacheRequestManager.java:60-259
+(deduplicated background caching from UFS or a remote worker), Sessions / SessionCleaner
+(locks and temp blocks of dead sessions are released).
+
+Data movement on the device tier never goes through Python bytes: reads land in caller buffers
+(device pointers via the batched page-gather kernel, host pointers via DMA), writes come from
+caller buffers.  ``read_bytes`` exists only for the gRPC byte-stream path used by host clients.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+from .. import metrics as msys
+from ..ops.native import native_errors
+from ..proto import pb
+from ..utils import ids
+from ..utils.exceptions import (BlockDoesNotExistException, DeadlineExceededException,
+                                NotFoundException)
+from .store import TieredStore
+
+LOG = logging.getLogger(__name__)
+
+HOST, DEVICE = 0, 1
+
+
+class _Staging:
+    """Pool of pinned host buffers for D2H/H2D staging of byte-stream I/O."""
+
+    def __init__(self, size: int, count: int = 8):
+        import torch
+        from ..ops.native import has_gpu
+        self.size = size
+        self._free = [torch.empty(size, dtype=torch.uint8, pin_memory=has_gpu()) for _ in range(count)]
+        self._cond = threading.Condition()
+
+    def acquire(self):
+        with self._cond:
+            while not self._free:
+                self._cond.wait()
+            return self._free.pop()
+
+    def release(self, t) -> None:
+        with self._cond:
+            self._free.append(t)
+            self._cond.notify()
+
+
+class BlockWorker:
+    def __init__(self, conf, store: TieredStore, master_channel=None, address=None, ufs_resolver=None):
+        self.conf = conf
+        self.store = store
+        self.native = store.native
+        self.master_channel = master_channel
+        self.address = address or pb.grpc.WorkerNetAddress(host="127.0.0.1")
+        self.worker_id = ids.INVALID_WORKER_ID
+        self.metrics = msys.metrics("Worker")
+        self._ufs_resolver = ufs_resolver
+        self._ufs_cache: dict[int, object] = {}
+        self._sessions: dict[int, float] = {}
+        self._session_lock = threading.Lock()
+        self._async_inflight: set[int] = set()
+        self._async_lock = threading.Lock()
+        self._async_pool = ThreadPoolExecutor(
+            max_workers=conf.get_int("alluxio.worker.network.async.cache.manager.threads.max"),
+            thread_name_prefix="async-cache")
+        self._staging = None
+        self._staging_lock = threading.Lock()
+        self.pinned_files: set[int] = set()
+        self.persisted_files: list[int] = []
+        self._block_master = None
+        self._fs_master = None
+        self.crc_enabled = conf.get_bool("alluxio.worker.data.crc.enabled")
+        self.crc: dict[int, list[int]] = {}
+        self._install_gauges()
+
+    # ---- wiring -------------------------------------------------------------------------------
+    def _bm(self):
+        if self._block_master is None and self.master_channel is not None:
+            self._block_master = self.master_channel.stub("alluxio.grpc.block.BlockMasterWorkerService")
+        return self._block_master
+
+    def _fsm(self):
+        if self._fs_master is None and self.master_channel is not None:
+            self._fs_master = self.master_channel.stub("alluxio.grpc.file.FileSystemMasterWorkerService")
+        return self._fs_master
+
+    def _install_gauges(self) -> None:
+        m = self.metrics
+        m.gauge("CapacityTotal", lambda: sum(self.store.capacity_by_tier().values()))
+        m.gauge("CapacityUsed", lambda: sum(self.store.used_by_tier().values()))
+        m.gauge("CapacityFree", lambda: sum(self.store.capacity_by_tier().values()) -
+                sum(self.store.used_by_tier().values()))
+        m.gauge("BlocksCached", lambda: len(self.native.block_ids(-1)))
+
+    def staging(self) -> _Staging:
+        with self._staging_lock:
+            if self._staging is None:
+                self._staging = _Staging(self.conf.get_bytes("alluxio.worker.network.reader.max.chunk.size.bytes") * 4)
+            return self._staging
+
+    # ---- sessions -----------------------------------------------------------------------------
+    def session_heartbeat(self, session_id: int) -> None:
+        with self._session_lock:
+            self._sessions[session_id] = time.time()
+
+    def cleanup_session(self, session_id: int) -> None:
+        with self._session_lock:
+            self._sessions.pop(session_id, None)
+        with native_errors():
+            self.native.cleanup_session(session_id)
+
+    def cleanup_expired_sessions(self, timeout_s: float | None = None) -> list[int]:
+        timeout_s = timeout_s if timeout_s is not None else \
+            self.conf.get_ms("alluxio.worker.session.timeout") / 1000.0
+        now = time.time()
+        with self._session_lock:
+            dead = [s for s, t in self._sessions.items() if now - t > timeout_s]
+        for s in dead:
+            self.cleanup_session(s)
+        return dead
+
+    # ---- writes -------------------------------------------------------------------------------
+    def create_block(self, session_id: int, block_id: int, tier: int = 0, medium: str = "",
+                     initial_bytes: int | None = None, pin: bool = False) -> int:
+        if initial_bytes is None:
+            initial_bytes = self.conf.get_bytes("alluxio.worker.file.buffer.size", "1MB")
+        self.session_heartbeat(session_id)
+        with native_errors():
+            return self.native.create_block(session_id, block_id, tier, medium, max(1, initial_bytes), True, pin)
+
+    def request_space(self, session_id: int, block_id: int, additional: int) -> None:
+        with native_errors():
+            self.native.request_space(session_id, block_id, additional)
+
+    def write_ptr(self, session_id: int, block_id: int, offset: int, ptr: int, length: int, kind: int,
+                  stream: int = 0, sync: bool = True) -> None:
+        with native_errors():
+            self.native.write(session_id, block_id, offset, ptr, length, kind, stream, sync)
+
+    def write_bytes(self, session_id: int, block_id: int, offset: int, data) -> None:
+        import numpy as np
+        arr = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        if arr.nbytes == 0:
+            return
+        with native_errors():
+            self.native.write(session_id, block_id, offset, arr.ctypes.data, arr.nbytes, HOST, 0, True)
+        self.metrics.counter("BytesWrittenAlluxio").inc(arr.nbytes)
+
+    def write_tensor(self, session_id: int, block_id: int, offset: int, t, stream: int = 0) -> None:
+        kind = DEVICE if t.is_cuda else HOST
+        t = t.contiguous()
+        self.write_ptr(session_id, block_id, offset, t.data_ptr(), t.numel() * t.element_size(), kind, stream, True)
+        self.metrics.counter("BytesWrittenAlluxio").inc(t.numel() * t.element_size())
+
+    def commit_block(self, session_id: int, block_id: int, pin: bool = False) -> None:
+        with native_errors():
+            self.native.commit_block(session_id, block_id, pin)
+            info = self.native.block_info(block_id)
+        if self.crc_enabled:
+            with native_errors():
+                self.crc[block_id] = self.native.checksum(block_id, 0)
+        bm = self._bm()
+        if bm is not None and self.worker_id != ids.INVALID_WORKER_ID:
+            used = self.store.used_by_tier().get(info.tier_alias, 0)
+            bm.CommitBlock(pb.block.CommitBlockPRequest(
+                workerId=self.worker_id, usedBytesOnTier=used, tierAlias=info.tier_alias, blockId=block_id,
+                length=info.length, mediumType=info.medium))
+        # the commit's added-event is reported by CommitBlock already
+        self.metrics.counter("BlocksCommitted").inc()
+
+    def abort_block(self, session_id: int, block_id: int) -> None:
+        with native_errors():
+            self.native.abort_block(session_id, block_id)
+
+    # ---- locks / reads ------------------------------------------------------------------------
+    def lock_block(self, session_id: int, block_id: int, timeout_ms: int = 30_000, write: bool = False) -> int:
+        self.session_heartbeat(session_id)
+        with native_errors():
+            lid = self.native.lock_block(session_id, block_id, write, timeout_ms)
+        if lid < 0:
+            raise DeadlineExceededException(f"timed out locking block {block_id}")
+        return lid
+
+    def unlock(self, lock_id: int) -> None:
+        with native_errors():
+            self.native.unlock(lock_id)
+
+    def has_block(self, block_id: int) -> bool:
+        return self.native.has_block(block_id)
+
+    def block_info(self, block_id: int):
+        with native_errors():
+            return self.native.block_info(block_id)
+
+    def access_block(self, session_id: int, block_id: int) -> None:
+        with native_errors():
+            self.native.access_block(session_id, block_id)
+
+    def read(self, block_id: int, offset: int, length: int, dst_ptr: int, dst_kind: int,
+             stream: int = 0, sync: bool = True) -> None:
+        with native_errors():
+            self.native.read(block_id, offset, length, dst_ptr, dst_kind, stream, sync)
+        self._count_read(length, dst_kind)
+
+    def read_batch(self, reqs, stream: int = 0, sync: bool = True) -> int:
+        """``reqs`` = [(block_id, offset, length, dst_ptr, dst_kind)]; one gather launch."""
+        with native_errors():
+            self.native.read_batch(reqs, stream, sync)
+        total = sum(r[2] for r in reqs)
+        self._count_read(total, reqs[0][4] if reqs else DEVICE)
+        return total
+
+    def _count_read(self, n: int, kind: int) -> None:
+        self.metrics.counter("BytesReadAlluxio").inc(n)
+        if kind == DEVICE:
+            self.metrics.counter("BytesReadDevice").inc(n)
+
+    def read_bytes(self, block_id: int, offset: int, length: int) -> bytes:
+        """Byte-stream read (gRPC ReadBlock): D2H into pinned staging, then copy out."""
+        st = self.staging()
+        out = bytearray(length)
+        pos = 0
+        while pos < length:
+            buf = st.acquire()
+            try:
+                n = min(st.size, length - pos)
+                with native_errors():
+                    self.native.read(block_id, offset + pos, n, buf.data_ptr(), HOST, 0, True)
+                out[pos:pos + n] = buf[:n].numpy().tobytes()
+            finally:
+                st.release(buf)
+            pos += n
+        self._count_read(length, HOST)
+        return bytes(out)
+
+    # ---- management ---------------------------------------------------------------------------
+    def remove_block(self, session_id: int, block_id: int) -> None:
+        with native_errors():
+            self.native.remove_block(session_id, block_id)
+        self.crc.pop(block_id, None)
+        self.metrics.counter("BlocksRemoved").inc()
+
+    def move_block(self, session_id: int, block_id: int, medium: str = "", tier: int = -1) -> int:
+        with native_errors():
+            return self.native.move_block(session_id, block_id, tier, medium, True)
+
+    def free_space(self, session_id: int, nbytes: int, tier: int = -1) -> list[int]:
+        with native_errors():
+            return self.native.free_space(session_id, nbytes, tier, -1)
+
+    def checksum(self, block_id: int, piece: int = 0) -> list[int]:
+        with native_errors():
+            out = self.native.checksum(block_id, piece)
+        self.metrics.counter("Crc32cBytes").inc(self.native.block_info(block_id).length)
+        return out
+
+    def update_pinned(self, file_ids) -> None:
+        self.pinned_files = set(file_ids)
+        with native_errors():
+            self.native.set_pinned_files(sorted(self.pinned_files))
+
+    # ---- UFS: cold reads + caching ------------------------------------------------------------
+    def _ufs_for(self, opts):
+        if self._ufs_resolver is not None:
+            return self._ufs_resolver(opts.mountId, opts.ufs_path)
+        from ..underfs import registry
+        u = self._ufs_cache.get(opts.mountId)
+        if u is None:
+            props = {}
+            fsm = self._fsm()
+            if fsm is not None and opts.mountId:
+                info = fsm.GetUfsInfo(pb.file.GetUfsInfoPRequest(mountId=opts.mountId)).ufsInfo
+                props = dict(info.properties.properties)
+            u = registry.create(opts.ufs_path, self.conf, props)
+            self._ufs_cache[opts.mountId] = u
+        return u
+
+    def read_ufs_range(self, opts, offset: int, length: int) -> bytes:
+        from ..underfs.base import OpenOptions
+        ufs = self._ufs_for(opts)
+        with ufs.open(opts.ufs_path, OpenOptions(offset=opts.offset_in_file + offset)) as f:
+            data = f.read(length)
+        self.metrics.counter("BytesReadUfsAll").inc(len(data))
+        return data
+
+    def cache_block_from_ufs(self, block_id: int, opts, session_id: int | None = None) -> bool:
+        """UFS -> pinned staging -> block (H2D for the HBM tier) -> commit.  Idempotent."""
+        if self.native.has_block(block_id):
+            return True
+        session_id = session_id if session_id is not None else ids.CACHE_UFS_SESSION_ID
+        from ..underfs.base import OpenOptions
+        ufs = self._ufs_for(opts)
+        length = opts.block_size
+        chunk = 8 << 20
+        try:
+            self.create_block(session_id, block_id, 0, "", min(length, 64 << 20) or 1)
+        except Exception as e:  # noqa: BLE001
+            if self.native.has_block(block_id) or self.native.has_temp_block(block_id):
+                return self.native.has_block(block_id)
+            raise e
+        try:
+            st = self.staging()
+            with ufs.open(opts.ufs_path, OpenOptions(offset=opts.offset_in_file)) as f:
+                pos = 0
+                while pos < length:
+                    buf = st.acquire()
+                    try:
+                        n = min(chunk, st.size, length - pos)
+                        mv = buf.numpy()
+                        got = f.readinto(memoryview(mv)[:n]) if hasattr(f, "readinto") else None
+                        if got is None:
+                            data = f.read(n)
+                            got = len(data)
+                            mv[:got] = memoryview(data)
+                        if not got:
+                            break
+                        with native_errors():
+                            self.native.write(session_id, block_id, pos, buf.data_ptr(), got, HOST, 0, True)
+                        pos += got
+                    finally:
+                        st.release(buf)
+            if pos != length:
+                raise IOError(f"short UFS read for block {block_id}: {pos} of {length}")
+            self.metrics.counter("BytesReadUfsAll").inc(length)
+            self.commit_block(session_id, block_id)
+            return True
+        except Exception:
+            try:
+                self.abort_block(session_id, block_id)
+            except Exception:  # noqa: BLE001
+                pass
+            raise
+
+    def async_cache(self, block_id: int, opts=None, source=None, length: int | None = None) -> bool:
+        """Deduplicated background caching; returns False if already queued/cached."""
+        if self.native.has_block(block_id):
+            return False
+        with self._async_lock:
+            if block_id in self._async_inflight:
+                return False
+            self._async_inflight.add(block_id)
+
+        def run():
+            try:
+                if source is not None:
+                    source(block_id)
+                elif opts is not None:
+                    self.cache_block_from_ufs(block_id, opts, ids.ASYNC_CACHE_UFS_SESSION_ID)
+                self.metrics.counter("AsyncCacheSucceededBlocks").inc()
+            except Exception:  # noqa: BLE001
+                LOG.debug("async cache of %d failed", block_id, exc_info=True)
+                self.metrics.counter("AsyncCacheFailedBlocks").inc()
+            finally:
+                with self._async_lock:
+                    self._async_inflight.discard(block_id)
+        self.metrics.counter("AsyncCacheRequests").inc()
+        self._async_pool.submit(run)
+        return True
+
+    def wait_async_idle(self, timeout: float = 30.0) -> bool:
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            with self._async_lock:
+                if not self._async_inflight:
+                    return True
+            time.sleep(0.01)
+        return False
+
+    # ---- heartbeat report ---------------------------------------------------------------------
+    def drain_report(self):
+        """(removed block ids, {(tier alias, medium): [added ids]}) since the last report."""
+        removed, added = [], {}
+        for ev in self.native.drain_events():
+            if ev.kind == 1:
+                removed.append(ev.block_id)
+                for k in list(added):
+                    if ev.block_id in added[k]:
+                        added[k].remove(ev.block_id)
+            else:
+                added.setdefault((ev.tier_alias, ev.medium), []).append(ev.block_id)
+        return removed, added
+
+    def current_blocks(self) -> dict:
+        out: dict = {}
+        for bid in self.native.block_ids(-1):
+            info = self.native.block_info(bid)
+            out.setdefault((info.tier_alias, info.medium), []).append(bid)
+        return out
+
+    def close(self) -> None:
+        self._async_pool.shutdown(wait=False, cancel_futures=True)
+
+
+def not_found(block_id: int) -> NotFoundException:
+    return BlockDoesNotExistException(f"Block {block_id} does not exist")

@@ -1,0 +1,206 @@
+"""Worker process: tiered HBM store + BlockWorker + data server + master sync threads.
+
+Parity: core/server/worker/src/main/java/alluxio/worker/AlluxioWorkerProcess.java (:99-265),
+block/BlockMasterSync.java:60-199 (getWorkerId -> register -> periodic heartbeat carrying used
+bytes, added/removed blocks, metrics; executes Free / Register commands), PinListSync.java,
+SessionCleaner.java, the storage checker (TieredBlockStore.checkStorage :974-1009, reported as
+lost storage) and the FileSystemMaster worker heartbeat (persisted files).
+"""
+from __future__ import annotations
+
+import logging
+import socket
+import threading
+
+from .. import metrics as msys
+from ..conf import Configuration
+from ..proto import pb
+from ..rpc import Channel, RpcServer
+from ..utils import heartbeat as hb
+from ..utils import ids
+from .block_worker import BlockWorker
+from .services import SVC_BLOCK_WORKER, BlockWorkerService
+from .store import TieredStore
+
+LOG = logging.getLogger(__name__)
+
+
+class BlockMasterSync:
+    def __init__(self, worker: BlockWorker, process: "AlluxioWorkerProcess"):
+        self.w = worker
+        self.p = process
+        self.registered = False
+
+    def register(self) -> None:
+        bm = self.w._bm()
+        wid = bm.GetWorkerId(pb.block.GetWorkerIdPRequest(workerNetAddress=self.w.address)).workerId
+        self.w.worker_id = wid
+        store = self.w.store
+        req = pb.block.RegisterWorkerPRequest(workerId=wid, storageTiers=store.tier_aliases)
+        for k, v in store.capacity_by_tier().items():
+            req.totalBytesOnTiers[k] = v
+        for k, v in store.used_by_tier().items():
+            req.usedBytesOnTiers[k] = v
+        for (tier, medium), blocks in self.w.current_blocks().items():
+            e = req.currentBlocks.add()
+            e.key.tierAlias = tier
+            e.key.mediumType = medium
+            e.value.blockId.extend(blocks)
+        for k, v in sorted(self.p.conf.to_map().items()):
+            req.options.configs.add(name=k, value=v)
+        bm.RegisterWorker(req)
+        self.w.drain_report()  # everything current was just reported
+        self.registered = True
+
+    def heartbeat(self) -> None:
+        if not self.registered:
+            self.register()
+            return
+        removed, added = self.w.drain_report()
+        req = pb.block.BlockHeartbeatPRequest(workerId=self.w.worker_id, removedBlockIds=removed)
+        for k, v in self.w.store.used_by_tier().items():
+            req.usedBytesOnTiers[k] = v
+        for (tier, medium), blocks in added.items():
+            e = req.addedBlocks.add()
+            e.key.tierAlias = tier
+            e.key.mediumType = medium
+            e.value.blockId.extend(blocks)
+        for name, mtype, value in self.w.metrics.report_metrics():
+            req.options.metrics.add(name=name, value=value, instance="Worker", source=self.w.address.host,
+                                    metricType=pb.grpc.MetricType.values_by_name[mtype].number)
+        for i in range(self.w.native.num_dirs()):
+            if not self.w.native.dir_healthy(i):
+                spec = self.w.native.dir_spec(i)
+                req.lostStorage[spec.tier_alias].storage.append(spec.path or f"{spec.medium}:{i}")
+        resp = self.w._bm().BlockHeartbeat(req)
+        cmd = pb.grpc.CommandType.values_by_number[resp.command.commandType].name
+        if cmd == "Register":
+            self.registered = False
+            self.register()
+        elif cmd == "Free":
+            for bid in resp.command.data:
+                try:
+                    self.w.remove_block(ids.MASTER_COMMAND_SESSION_ID, bid)
+                except Exception:  # noqa: BLE001
+                    LOG.debug("free of %d failed", bid, exc_info=True)
+            removed2, _ = self.w.drain_report()
+            if removed2:
+                self.w._bm().BlockHeartbeat(pb.block.BlockHeartbeatPRequest(
+                    workerId=self.w.worker_id, removedBlockIds=removed2))
+
+
+class AlluxioWorkerProcess:
+    def __init__(self, conf: Configuration | None = None, master_address: str | None = None,
+                 host: str = "127.0.0.1", port: int | None = None, device: int | None = None,
+                 enable_grpc: bool = True, work_dir: str | None = None):
+        self.conf = conf or Configuration(load_site=True)
+        self.master_address = master_address or "{}:{}".format(
+            self.conf.get("alluxio.master.hostname", "127.0.0.1"), self.conf.get_int("alluxio.master.rpc.port"))
+        self.host = host
+        self.port = self.conf.get_int("alluxio.worker.rpc.port") if port is None else port
+        self.store = TieredStore(self.conf, device, work_dir)
+        self.master_channel = Channel(self.master_address)
+        self.worker = BlockWorker(self.conf, self.store, self.master_channel)
+        self.server = RpcServer(host, self.port, metrics=msys.metrics("Worker"), enable_grpc=enable_grpc)
+        self.server.add_servicer(SVC_BLOCK_WORKER, BlockWorkerService(self.worker, self.conf))
+        self.sync = BlockMasterSync(self.worker, self)
+        self._threads: list[hb.HeartbeatThread] = []
+
+    @property
+    def address(self) -> str:
+        return self.server.address
+
+    def start(self, register: bool = True, start_heartbeats: bool = True) -> str:
+        addr = self.server.start()
+        host, port = addr.rsplit(":", 1)
+        ti = pb.grpc.TieredIdentity(tiers=[pb.grpc.LocalityTier(tierName="node", value=socket.gethostname()),
+                                           pb.grpc.LocalityTier(tierName="gpu", value=str(self.store.device))])
+        self.worker.address = pb.grpc.WorkerNetAddress(host=host, rpcPort=int(port), dataPort=int(port),
+                                                       webPort=0, tieredIdentity=ti,
+                                                       containerHost=socket.gethostname())
+        from ..client.context import register_local_worker
+        register_local_worker(addr, self.worker)
+        if register:
+            self.sync.register()
+        if start_heartbeats:
+            c = self.conf
+            for name, fn, ms in [
+                (hb.WORKER_BLOCK_SYNC, self.sync.heartbeat, c.get_ms("alluxio.worker.block.heartbeat.interval")),
+                (hb.WORKER_PIN_LIST_SYNC, self.pin_list_sync, c.get_ms("alluxio.worker.block.heartbeat.interval")),
+                (hb.WORKER_SESSION_CLEANER, self.worker.cleanup_expired_sessions,
+                 c.get_ms("alluxio.worker.session.timeout")),
+                (hb.WORKER_FILESYSTEM_MASTER_SYNC, self.fs_heartbeat,
+                 c.get_ms("alluxio.worker.filesystem.heartbeat.interval", "1sec")),
+                (hb.WORKER_STORAGE_HEALTH, self.check_storage, c.get_ms("alluxio.worker.storage.checker.interval", "1min")
+                 if False else 60_000),
+            ]:
+                t = hb.HeartbeatThread(name, fn, ms)
+                t.start()
+                self._threads.append(t)
+        LOG.info("worker serving at %s (device %d)", addr, self.store.device)
+        return addr
+
+    def add_heartbeat(self, name: str, fn, interval_ms: int) -> None:
+        t = hb.HeartbeatThread(name, fn, interval_ms)
+        t.start()
+        self._threads.append(t)
+
+    def pin_list_sync(self) -> None:
+        fsm = self.worker._fsm()
+        ids_ = fsm.GetPinnedFileIds(pb.file.GetPinnedFileIdsPRequest()).pinnedFileIds
+        self.worker.update_pinned(list(ids_))
+
+    def fs_heartbeat(self) -> None:
+        if self.worker.worker_id == ids.INVALID_WORKER_ID:
+            return
+        persisted, self.worker.persisted_files = self.worker.persisted_files, []
+        self.worker._fsm().FileSystemHeartbeat(pb.file.FileSystemHeartbeatPRequest(
+            workerId=self.worker.worker_id, persistedFiles=persisted))
+
+    def check_storage(self) -> None:
+        """GPU health into the storage checker: a failing HIP device marks its dirs lost."""
+        if not self.store.has_device_tier:
+            return
+        try:
+            import torch
+            torch.cuda.synchronize(self.store.device)
+        except Exception:  # noqa: BLE001
+            LOG.error("HIP device %d failed; marking HBM dirs lost", self.store.device)
+            for i in range(self.worker.native.num_dirs()):
+                if self.store.dirs[i].medium == "HBM":
+                    self.worker.native.set_dir_healthy(i, False)
+
+    def stop(self) -> None:
+        for t in self._threads:
+            t.shutdown(join=False)
+        for t in self._threads:
+            t.shutdown(join=True)
+        self._threads.clear()
+        from ..client.context import unregister_local_worker
+        if self.server.address:
+            unregister_local_worker(self.server.address)
+        self.server.stop()
+        self.worker.close()
+
+
+def main(argv=None) -> int:  # pragma: no cover - CLI entry
+    import argparse
+    ap = argparse.ArgumentParser(description="alluxio_amd worker (one per MI355X)")
+    ap.add_argument("--master", default=None)
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--device", type=int, default=None)
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    w = AlluxioWorkerProcess(master_address=a.master, host=a.host, port=a.port, device=a.device)
+    w.start()
+    try:
+        threading.Event().wait()
+    except KeyboardInterrupt:
+        pass
+    w.stop()
+    return 0
+
+
+if __name__ == "__main__":  # pragma: no cover
+    raise SystemExit(main())

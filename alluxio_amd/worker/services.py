@@ -1,0 +1,290 @@
+"""gRPC ``BlockWorker`` service of a worker (the data server).
+
+Parity: core/server/worker/src/main/java/alluxio/worker/grpc/BlockWorkerImpl.java:61-210,
+AbstractReadHandler.java (chunked streaming, flow control: pause while more than the window is
+un-acked by ``offset_received`` — :74-77, :113-140, :170-172, :336-439), BlockReadHandler.java
+(openBlock: lock -> reader, UFS fallback :159-235), AbstractWriteHandler / BlockWriteHandler
+(:36-149: reserve, append, flush acks, commit on close), UfsFileWriteHandler (CACHE_THROUGH's UFS
+stream), ShortCircuitBlock{Read,Write}Handler (lock/create local block for the stream lifetime).
+
+MI355X extension RPCs: ``OpenDeviceBlock`` hands out the block's page list plus a HIP IPC handle
+of the HBM arena so a same-node process can gather the bytes with its own kernel (the device
+analogue of short-circuit mmap); ``UnlockDeviceBlock`` releases it.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+
+from ..proto import enum_name, pb
+from ..utils import ids
+from ..utils.exceptions import (BlockDoesNotExistException, InvalidArgumentException,
+                                UnavailableException)
+
+LOG = logging.getLogger(__name__)
+
+SVC_BLOCK_WORKER = "alluxio.grpc.block.BlockWorker"
+
+
+class BlockWorkerService:
+    def __init__(self, worker, conf):
+        self.w = worker
+        self.conf = conf
+        self.max_chunk = conf.get_bytes("alluxio.worker.network.reader.max.chunk.size.bytes")
+        self.window = conf.get_bytes("alluxio.worker.network.reader.buffer.size")
+        self._device_locks: dict[int, tuple[int, int]] = {}
+        self._lock = threading.Lock()
+
+    # ------------------------------------------------------------------------------------------
+    def ReadBlock(self, request_iter, ctx):
+        it = iter(request_iter)
+        first = next(it, None)
+        if first is None:
+            return
+        session = ids.create_session_id()
+        acked = [first.offset]
+        done = threading.Event()
+        cond = threading.Condition()
+
+        def ack_reader():
+            try:
+                for r in it:
+                    if r.HasField("offset_received"):
+                        with cond:
+                            acked[0] = max(acked[0], r.offset_received)
+                            cond.notify_all()
+            except Exception:  # noqa: BLE001
+                pass
+            finally:
+                done.set()
+                with cond:
+                    cond.notify_all()
+        t = threading.Thread(target=ack_reader, daemon=True, name="read-acks")
+        t.start()
+        chunk = min(first.chunk_size or (1 << 20), self.max_chunk)
+        lock_id = None
+        try:
+            bid = first.block_id
+            if not self.w.has_block(bid):
+                if first.HasField("open_ufs_block_options") and first.open_ufs_block_options.ufs_path:
+                    opts = first.open_ufs_block_options
+                    if opts.no_cache:
+                        yield from self._stream_ufs(opts, first.offset, first.length, chunk, acked, cond, done)
+                        return
+                    self.w.cache_block_from_ufs(bid, opts, session)
+                else:
+                    raise BlockDoesNotExistException(f"Block {bid} does not exist on this worker")
+            lock_id = self.w.lock_block(session, bid)
+            info = self.w.block_info(bid)
+            length = first.length if first.length > 0 else info.length - first.offset
+            end = min(info.length, first.offset + length)
+            pos = first.offset
+            if first.promote:
+                try:
+                    self.w.move_block(session, bid, tier=0)
+                except Exception:  # noqa: BLE001
+                    pass
+            self.w.access_block(session, bid)
+            while pos < end:
+                with cond:
+                    while pos - acked[0] >= self.window and not done.is_set():
+                        cond.wait(0.5)
+                n = min(chunk, end - pos)
+                data = self.w.read_bytes(bid, pos, n)
+                pos += n
+                yield pb.block.ReadResponse(chunk=pb.block.Chunk(data=data))
+        finally:
+            if lock_id is not None:
+                try:
+                    self.w.unlock(lock_id)
+                except Exception:  # noqa: BLE001
+                    pass
+            self.w.cleanup_session(session)
+
+    def _stream_ufs(self, opts, offset, length, chunk, acked, cond, done):
+        end = offset + (length if length > 0 else opts.block_size - offset)
+        pos = offset
+        while pos < end:
+            with cond:
+                while pos - acked[0] >= self.window and not done.is_set():
+                    cond.wait(0.5)
+            n = min(chunk, end - pos)
+            data = self.w.read_ufs_range(opts, pos, n)
+            if not data:
+                break
+            pos += len(data)
+            yield pb.block.ReadResponse(chunk=pb.block.Chunk(data=data))
+
+    # ------------------------------------------------------------------------------------------
+    def WriteBlock(self, request_iter, ctx):
+        it = iter(request_iter)
+        first = next(it, None)
+        if first is None or not first.HasField("command"):
+            raise InvalidArgumentException("WriteBlock stream must start with a command")
+        cmd = first.command
+        rtype = enum_name(pb.block.RequestType, cmd.type)
+        session = ids.create_session_id()
+        pos = cmd.offset
+        if rtype == "UFS_FILE":
+            yield from self._write_ufs_file(cmd, it)
+            return
+        bid = cmd.id
+        tier = cmd.tier if cmd.HasField("tier") else 0
+        medium = cmd.medium_type
+        reserve = cmd.space_to_reserve or self.conf.get_bytes("alluxio.worker.file.buffer.size", "1MB")
+        self.w.create_block(session, bid, tier if not medium else -1, medium, reserve, cmd.pin_on_create)
+        committed = False
+        try:
+            for req in it:
+                if req.HasField("chunk"):
+                    data = req.chunk.data
+                    self.w.write_bytes(session, bid, pos, data)
+                    pos += len(data)
+                elif req.HasField("command") and req.command.flush:
+                    yield pb.block.WriteResponse(offset=pos)
+            self.w.commit_block(session, bid, cmd.pin_on_create)
+            committed = True
+            yield pb.block.WriteResponse(offset=pos)
+        finally:
+            if not committed:
+                try:
+                    self.w.abort_block(session, bid)
+                except Exception:  # noqa: BLE001
+                    pass
+            self.w.cleanup_session(session)
+
+    def _write_ufs_file(self, cmd, it):
+        from ..underfs.base import CreateOptions
+        o = cmd.create_ufs_file_options
+        ufs = self.w._ufs_for(pb.dataserver.OpenUfsBlockOptions(ufs_path=o.ufs_path, mountId=o.mount_id))
+        pos = 0
+        out = ufs.create(o.ufs_path, CreateOptions(create_parent=True, ensure_atomic=True, owner=o.owner,
+                                                   group=o.group, mode=o.mode or 0o644))
+        ok = False
+        try:
+            for req in it:
+                if req.HasField("chunk"):
+                    out.write(req.chunk.data)
+                    pos += len(req.chunk.data)
+                elif req.HasField("command") and req.command.flush:
+                    yield pb.block.WriteResponse(offset=pos)
+            ok = True
+        finally:
+            if ok:
+                out.close()
+            else:
+                try:
+                    out.close()
+                    ufs.delete_file(o.ufs_path)
+                except Exception:  # noqa: BLE001
+                    pass
+        self.w.metrics.counter("BytesWrittenUfsAll").inc(pos)
+        yield pb.block.WriteResponse(offset=pos)
+
+    # ------------------------------------------------------------------------------------------
+    def OpenLocalBlock(self, request_iter, ctx):
+        it = iter(request_iter)
+        first = next(it, None)
+        if first is None:
+            return
+        session = ids.create_session_id()
+        lock_id = self.w.lock_block(session, first.block_id)
+        try:
+            info = self.w.block_info(first.block_id)
+            path = ""
+            spec = self.w.native.dir_spec(info.dir)
+            if spec.path:
+                path = os.path.join(spec.path, str(first.block_id))
+            yield pb.block.OpenLocalBlockResponse(path=path)
+            for _ in it:  # hold the lock until the client closes the stream
+                pass
+        finally:
+            self.w.unlock(lock_id)
+            self.w.cleanup_session(session)
+
+    def CreateLocalBlock(self, request_iter, ctx):
+        it = iter(request_iter)
+        first = next(it, None)
+        if first is None:
+            return
+        session = ids.create_session_id()
+        self.w.create_block(session, first.block_id, first.tier, first.medium_type,
+                            first.space_to_reserve or (1 << 20), first.pin_on_create)
+        ok = False
+        try:
+            yield pb.block.CreateLocalBlockResponse(path="")
+            for req in it:
+                if req.space_to_reserve:
+                    self.w.request_space(session, first.block_id, req.space_to_reserve)
+                    yield pb.block.CreateLocalBlockResponse(path="")
+            if not first.only_reserve_space:
+                self.w.commit_block(session, first.block_id, first.pin_on_create)
+            ok = True
+        finally:
+            if not ok and first.cleanup_on_failure:
+                try:
+                    self.w.abort_block(session, first.block_id)
+                except Exception:  # noqa: BLE001
+                    pass
+
+    def AsyncCache(self, req, ctx):
+        src = None
+        if req.source_host and (req.source_host, req.source_port) != (self.w.address.host, self.w.address.dataPort):
+            from .remote import remote_block_fetcher
+            src = remote_block_fetcher(self.w, req.source_host, req.source_port, req.length)
+        opts = req.open_ufs_block_options if req.HasField("open_ufs_block_options") else None
+        if opts is not None and not opts.block_size and req.length:
+            opts.block_size = req.length
+        self.w.async_cache(req.block_id, opts=opts, source=src, length=req.length)
+        return pb.block.AsyncCacheResponse()
+
+    def RemoveBlock(self, req, ctx):
+        self.w.remove_block(ids.create_session_id(), req.block_id)
+        return pb.block.RemoveBlockResponse()
+
+    def MoveBlock(self, req, ctx):
+        self.w.move_block(ids.create_session_id(), req.block_id, medium=req.medium_type)
+        return pb.block.MoveBlockResponse()
+
+    def ClearMetrics(self, req, ctx):
+        self.w.metrics.registry.clear()
+        return pb.block.ClearMetricsResponse()
+
+    # ---- MI355X extensions ---------------------------------------------------------------------
+    def OpenDeviceBlock(self, req, ctx):
+        session = req.session_id or ids.create_session_id()
+        lock_id = self.w.lock_block(session, req.block_id)
+        try:
+            pages, d, ps, base = self.w.native.block_pages(req.block_id)
+            info = self.w.block_info(req.block_id)
+            arena = self.w.store.arena_for_dir(d)
+            if arena is None or arena.kind != "hbm":
+                raise UnavailableException("block is not in the device tier")
+            h = pb.block.DeviceBlockHandle(block_id=req.block_id, length=info.length, page_size=ps, pages=pages,
+                                           arena_bytes=arena.nbytes, device=arena.device, lock_id=lock_id,
+                                           pid=os.getpid())
+            try:
+                h.arena_ipc_handle = arena.ipc_handle()
+            except Exception:  # noqa: BLE001
+                LOG.debug("IPC export unavailable", exc_info=True)
+            if req.block_id in self.w.crc:
+                h.crc32c.extend(self.w.crc[req.block_id])
+            with self._lock:
+                self._device_locks[lock_id] = (session, req.block_id)
+            self.w.access_block(session, req.block_id)
+            return h
+        except Exception:
+            self.w.unlock(lock_id)
+            raise
+
+    def UnlockDeviceBlock(self, req, ctx):
+        with self._lock:
+            self._device_locks.pop(req.lock_id, None)
+        self.w.unlock(req.lock_id)
+        return pb.block.UnlockDeviceBlockResponse()
+
+    def PeerTransfer(self, req, ctx):
+        from .remote import peer_transfer
+        ok, msg = peer_transfer(self.w, req)
+        return pb.block.PeerTransferResponse(ok=ok, message=msg)

@@ -1,0 +1,210 @@
+"""Tiered-store construction: configuration -> native page arenas.
+
+Parity: worker tier layout keys ``alluxio.worker.tieredstore.level{N}.{alias,dirs.path,
+dirs.quota,dirs.mediumtype}`` (core/common/.../PropertyKey.java:2933-2985, levels :3079),
+BlockMetadataManager's tier/dir scan (core/server/worker/.../BlockMetadataManager.java:84-104).
+
+Dir path grammar (comma separated, one quota per dir):
+  ``hbm`` / ``hbm:<device>``   device arena on the worker's MI355X (medium HBM)
+  ``dram``                     pinned host arena (medium DRAM; plain host memory without a GPU)
+  ``auto``                     ``hbm`` when a HIP device is visible, else ``dram``
+  ``/some/dir``                file-backed dir (SSD/HDD)
+The arenas are allocated through torch (one ``hipMalloc``/pinned allocation each) and handed to
+the native store as raw pointers; the tensors are kept alive here and give page views for RCCL
+transfers and HIP IPC export.
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+from ..conf import Configuration, Templates
+from ..ops.native import has_gpu, lib, wrap_errors
+
+LOG = logging.getLogger(__name__)
+
+ANNOTATORS = {"LRU": 0, "LRFU": 1}
+ALLOCATORS = {"MAXFREE": 0, "GREEDY": 1, "ROUNDROBIN": 2}
+
+
+class Arena:
+    """A contiguous allocation backing one storage dir."""
+
+    def __init__(self, kind: str, nbytes: int, device: int = 0):
+        import torch
+        self.kind = kind
+        self.nbytes = nbytes
+        self.device = device
+        if kind == "hbm":
+            self.tensor = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", device))
+        elif kind == "dram":
+            pin = has_gpu()
+            self.tensor = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin)
+        else:
+            raise ValueError(kind)
+        self.base = self.tensor.data_ptr()
+
+    def view(self, offset: int, nbytes: int):
+        return self.tensor[offset:offset + nbytes]
+
+    def ipc_handle(self) -> bytes:
+        """HIP IPC handle of the arena allocation (short-circuit export to same-node processes)."""
+        if self.kind != "hbm":
+            raise ValueError("only device arenas can be exported over HIP IPC")
+        from ..parallel.ipc import export_handle
+        return export_handle(self.tensor)
+
+
+class DirConfig:
+    def __init__(self, tier: int, alias: str, path: str, quota: int, medium: str):
+        self.tier, self.alias, self.path, self.quota, self.medium = tier, alias, path, quota, medium
+
+
+def _resolve_kind(path: str) -> tuple[str, int | None]:
+    p = path.strip()
+    if p == "auto":
+        return ("hbm", None) if has_gpu() else ("dram", None)
+    if p.startswith("hbm"):
+        dev = p.split(":", 1)[1] if ":" in p else ""
+        return "hbm", int(dev) if dev.isdigit() else None
+    if p in ("dram", "mem", "ram"):
+        return "dram", None
+    return "file", None
+
+
+def parse_tiers(conf: Configuration) -> list[DirConfig]:
+    from ..utils.format import parse_space_size
+    out = []
+    for level in range(conf.get_int("alluxio.worker.tieredstore.levels")):
+        alias = conf.get(Templates.WORKER_TIERED_STORE_LEVEL_ALIAS.format(level))
+        paths = conf.get_list(Templates.WORKER_TIERED_STORE_LEVEL_DIRS_PATH.format(level))
+        quotas = conf.get_list(Templates.WORKER_TIERED_STORE_LEVEL_DIRS_QUOTA.format(level))
+        mediums = conf.get_list(Templates.WORKER_TIERED_STORE_LEVEL_DIRS_MEDIUMTYPE.format(level))
+        for i, p in enumerate(paths):
+            q = quotas[min(i, len(quotas) - 1)] if quotas else "1GB"
+            kind, _ = _resolve_kind(p)
+            medium = mediums[min(i, len(mediums) - 1)] if mediums else ""
+            if kind == "hbm":
+                medium = "HBM"
+            elif kind == "dram":
+                medium = "DRAM" if medium in ("", "HBM") else medium
+            out.append(DirConfig(level, alias, p, parse_space_size(q), medium or "SSD"))
+    return out
+
+
+class TieredStore:
+    """Owns the arenas and the native :class:`BlockStore` of one worker."""
+
+    def __init__(self, conf: Configuration, device: int | None = None, work_dir: str | None = None):
+        C = lib()
+        self.conf = conf
+        self.device = device if device is not None else _default_device(conf)
+        page = conf.get_bytes("alluxio.worker.hbm.page.size")
+        frac = conf.get_float("alluxio.worker.hbm.arena.fraction")
+        self.dirs = parse_tiers(conf)
+        self.arenas: list[Arena | None] = []
+        specs = []
+        self.tier_aliases: list[str] = []
+        for d in self.dirs:
+            kind, dev = _resolve_kind(d.path)
+            spec = C.DirSpec()
+            spec.tier = d.tier
+            spec.tier_alias = d.alias
+            spec.medium = d.medium
+            spec.page_size = page
+            spec.device = self.device if dev is None else dev
+            quota = d.quota
+            if kind == "hbm":
+                if not has_gpu():
+                    raise RuntimeError(f"tier {d.alias} dir {d.path!r} needs a HIP device but none is visible")
+                if frac > 0:
+                    import torch
+                    free, _ = torch.cuda.mem_get_info(spec.device)
+                    quota = int(free * frac)
+                quota -= quota % page
+                arena = Arena("hbm", quota, spec.device)
+                spec.kind = C.DirKind.DEVICE
+                spec.base = arena.base
+            elif kind == "dram":
+                quota -= quota % page
+                arena = Arena("dram", quota)
+                spec.kind = C.DirKind.HOST
+                spec.base = arena.base
+            else:
+                arena = None
+                path = d.path
+                if work_dir and not os.path.isabs(path):
+                    path = os.path.join(work_dir, path)
+                os.makedirs(path, exist_ok=True)
+                spec.kind = C.DirKind.FILE
+                spec.path = path
+            spec.capacity = quota
+            specs.append(spec)
+            self.arenas.append(arena)
+            if d.alias not in self.tier_aliases:
+                self.tier_aliases.append(d.alias)
+        annot = conf.get("alluxio.worker.block.annotator.class").rsplit(".", 1)[-1].replace("Annotator", "").upper()
+        alloc = conf.get("alluxio.worker.allocator.class").rsplit(".", 1)[-1].replace("Allocator", "").upper()
+        self.native = C.BlockStore(specs, ANNOTATORS.get(annot, 0), ALLOCATORS.get(alloc, 0),
+                                   conf.get_float("alluxio.worker.block.annotator.lrfu.step.factor"),
+                                   conf.get_float("alluxio.worker.block.annotator.lrfu.attenuation.factor"),
+                                   self.device)
+        self.has_device_tier = any(a is not None and a.kind == "hbm" for a in self.arenas)
+        LOG.info("tiered store: %s", self.native.stats())
+
+    def arena_for_dir(self, d: int) -> Arena | None:
+        return self.arenas[d]
+
+    def dir_medium(self, d: int) -> str:
+        return self.dirs[d].medium
+
+    def tier_of_alias(self, alias: str) -> int:
+        for d in self.dirs:
+            if d.alias == alias:
+                return d.tier
+        return -1
+
+    def capacity_by_tier(self) -> dict[str, int]:
+        out: dict[str, int] = {}
+        for i, d in enumerate(self.dirs):
+            out[d.alias] = out.get(d.alias, 0) + self.native.dir_capacity(i)
+        return out
+
+    def used_by_tier(self) -> dict[str, int]:
+        out: dict[str, int] = {}
+        for i, d in enumerate(self.dirs):
+            used = self.native.dir_capacity(i) - self.native.dir_available(i)
+            out[d.alias] = out.get(d.alias, 0) + used
+        return out
+
+    @wrap_errors
+    def block_view(self, block_id: int):
+        """Device/host tensor views of the block's page runs (for RCCL send / zero-copy reads)."""
+        pages, d, ps, base = self.native.block_pages(block_id)
+        info = self.native.block_info(block_id)
+        arena = self.arenas[d]
+        if arena is None:
+            raise ValueError("block lives in a file tier; no memory view")
+        views = []
+        i = 0
+        remaining = info.length
+        while i < len(pages) and remaining > 0:
+            j = i + 1
+            while j < len(pages) and pages[j] == pages[j - 1] + 1:
+                j += 1
+            n = min((j - i) * ps, remaining)
+            views.append(arena.view(pages[i] * ps, n))
+            remaining -= n
+            i = j
+        return views
+
+
+def _default_device(conf: Configuration) -> int:
+    d = conf.get_int("alluxio.worker.gpu.device")
+    if d >= 0:
+        return d
+    lr = os.environ.get("LOCAL_RANK")
+    if lr is not None and has_gpu():
+        import torch
+        return int(lr) % max(1, torch.cuda.device_count())
+    return 0
