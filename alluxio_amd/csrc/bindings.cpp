@@ -169,7 +169,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("medium", &Event::medium);
 
   using G = py::call_guard<py::gil_scoped_release>;
-  py::class_<BlockStore>(m, "BlockStore")
+  py::class_<BlockStore>(m, "BlockStore", py::dynamic_attr())
       .def(py::init<const std::vector<DirSpec>&, int, int, float, float, int>(), py::arg("dirs"),
            py::arg("annotator") = 0, py::arg("alloc_policy") = 0, py::arg("lrfu_step") = 0.25f,
            py::arg("lrfu_attenuation") = 2.0f, py::arg("device") = 0)

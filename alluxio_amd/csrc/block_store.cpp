@@ -1172,7 +1172,9 @@ uint64_t ReadSession::step(uint64_t stream, std::vector<int>* reopened) {
     pos_[i] = p;
     bytes += out;
   }
-  if (!reqs_.empty()) store_->read_batch(reqs_, stream, false);
+  // host destinations are consumed by the CPU as soon as read() returns: complete the DMA;
+  // device destinations stay ordered on the caller's stream
+  if (!reqs_.empty()) store_->read_batch(reqs_, stream, kind_ == (int)MemKind::kHost);
   // annotate accesses once per distinct block per step (LRU/LRFU clock)
   std::sort(touched.begin(), touched.end());
   touched.erase(std::unique(touched.begin(), touched.end()), touched.end());

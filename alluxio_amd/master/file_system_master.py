@@ -638,7 +638,8 @@ class FileSystemMaster(Journaled):
                 block_ids.extend(f.block_ids)
         if forced:
             with RpcContext(self) as rpc, self.tree.lock.write():
-                for f in files:
+                nodes = [inode] + (self.tree.descendants(inode) if inode.is_directory else [])
+                for f in nodes:
                     if f.pinned and not f.deleted:
                         self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
                             id=f.id, pinned=False)))
@@ -741,7 +742,6 @@ class FileSystemMaster(Journaled):
               properties: dict | None = None) -> None:
         alluxio_path = normalize_path(alluxio_path)
         from ..underfs import registry
-        self.permission.check_superuser(self._user()) if False else None
         self.mount_table.validate_new_mount(alluxio_path, ufs_uri)
         ufs = registry.create(ufs_uri, self.conf, properties)
         if not ufs.is_directory(ufs_uri):

@@ -160,7 +160,6 @@ class InodeTree:
 
     # ---- journal application (single code path for replay and live ops) ---------------------
     def apply(self, e) -> bool:
-        kind = e.WhichOneof_name if hasattr(e, "WhichOneof_name") else None
         if e.HasField("inode_directory"):
             self._add(InodeDirectory.from_entry(e.inode_directory))
         elif e.HasField("inode_file"):

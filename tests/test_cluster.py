@@ -1,0 +1,144 @@
+"""End-to-end integration over an in-process cluster (reference LocalAlluxioClusterResource-based
+integration tests: FileInStreamIntegrationTest, RemoteReadIntegrationTest, FreeIntegrationTest,
+and TestRunner's ReadType x WriteType matrix from ``bin/alluxio runTests``)."""
+import os
+
+import numpy as np
+import pytest
+
+from alluxio_amd.minicluster import LocalAlluxioCluster
+from alluxio_amd.utils import exceptions as ex
+
+MB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    c = LocalAlluxioCluster(num_workers=2, grpc=True, conf={
+        "alluxio.worker.tieredstore.level0.dirs.path": "dram",
+        "alluxio.worker.tieredstore.level0.dirs.quota": "64MB",
+        "alluxio.user.block.size.bytes.default": "4MB"}).start()
+    yield c
+    c.stop()
+
+
+@pytest.mark.parametrize("write_type", ["MUST_CACHE", "CACHE_THROUGH", "THROUGH", "ASYNC_THROUGH"])
+@pytest.mark.parametrize("read_type", ["NO_CACHE", "CACHE", "CACHE_PROMOTE"])
+def test_read_write_type_matrix(cluster, write_type, read_type):
+    fs = cluster.client()
+    path = f"/matrix/{write_type}-{read_type}"
+    data = os.urandom(9 * MB + 123)
+    fs.write_file(path, data, write_type=write_type)
+    st = fs.get_status(path)
+    assert st.length == len(data) and st.completed
+    assert st.persisted == (write_type in ("CACHE_THROUGH", "THROUGH"))
+    assert fs.read_file(path, read_type=read_type) == data
+    with fs.open_file(path, read_type=read_type) as f:
+        f.seek(5 * MB - 7)
+        assert f.read(100) == data[5 * MB - 7:5 * MB + 93]
+        buf = bytearray(1000)
+        assert f.pread(4 * MB - 500, buf) == 1000 and bytes(buf) == data[4 * MB - 500:4 * MB + 500]
+    fs.close()
+
+
+def test_through_then_cache_read_populates_workers(cluster):
+    fs = cluster.client()
+    data = os.urandom(6 * MB)
+    fs.write_file("/t/through", data, write_type="THROUGH")
+    assert fs.get_status("/t/through").in_alluxio_percentage == 0
+    assert fs.read_file("/t/through", read_type="CACHE") == data
+    assert fs.get_status("/t/through").in_alluxio_percentage == 100
+    fs.free("/t/through")
+    cluster.heartbeat_workers()
+    assert fs.get_status("/t/through").in_alluxio_percentage == 0
+    assert fs.read_file("/t/through", read_type="NO_CACHE") == data
+    assert fs.get_status("/t/through").in_alluxio_percentage == 0
+
+
+def test_remote_grpc_read_path(cluster):
+    """Force the gRPC ReadBlock path by dropping the in-process worker shortcut."""
+    from alluxio_amd.client import context as cctx
+    fs = cluster.client()
+    data = os.urandom(5 * MB + 9)
+    fs.write_file("/r/remote", data, write_type="MUST_CACHE")
+    saved = dict(cctx._LOCAL_WORKERS)
+    cctx._LOCAL_WORKERS.clear()
+    try:
+        assert fs.read_file("/r/remote") == data
+    finally:
+        cctx._LOCAL_WORKERS.update(saved)
+    fs.close()
+
+
+def test_device_read_into_tensor(cluster):
+    import torch
+    fs = cluster.client()
+    data = np.random.default_rng(3).integers(0, 256, 3 * MB + 11, dtype=np.uint8)
+    fs.write_file("/dev/x", data, write_type="MUST_CACHE")
+    out = torch.empty(len(data), dtype=torch.uint8)
+    with fs.open_file("/dev/x") as f:
+        assert f.read_into(out) == len(data)
+    assert np.array_equal(out.numpy(), data)
+
+
+def test_namespace_ops_through_client(cluster):
+    fs = cluster.client()
+    fs.create_directory("/ns/a/b", recursive=True, write_type="CACHE_THROUGH")
+    fs.write_file("/ns/a/b/f", b"hello", write_type="CACHE_THROUGH")
+    assert [s.name for s in fs.list_status("/ns/a")] == ["b"]
+    fs.rename("/ns/a/b/f", "/ns/a/g")
+    assert fs.read_file("/ns/a/g") == b"hello"
+    assert os.path.exists(os.path.join(cluster.ufs_root, "ns", "a", "g"))
+    with pytest.raises(ex.NotFoundException):
+        fs.get_status("/ns/nope")
+    fs.set_attribute("/ns/a/g", pinned=True)
+    assert fs.get_status("/ns/a/g").pinned
+    with pytest.raises(ex.AlluxioStatusException):
+        fs.free("/ns/a/g")
+    fs.set_attribute("/ns/a/g", pinned=False)
+    fs.delete("/ns", recursive=True)
+    assert not fs.exists("/ns")
+    assert not os.path.exists(os.path.join(cluster.ufs_root, "ns"))
+
+
+def test_mount_external_ufs(cluster, tmp_path):
+    ext = tmp_path / "ext"
+    ext.mkdir()
+    (ext / "data.bin").write_bytes(b"z" * 4096)
+    fs = cluster.client()
+    fs.mount("/ext", str(ext))
+    assert fs.read_file("/ext/data.bin") == b"z" * 4096
+    assert "/ext" in fs.get_mount_table()
+    fs.unmount("/ext")
+    assert not fs.exists("/ext", load_metadata="NEVER")
+
+
+def test_worker_heartbeat_reports_eviction(tmp_path):
+    with LocalAlluxioCluster(num_workers=1, conf={
+            "alluxio.worker.tieredstore.level0.dirs.path": "dram",
+            "alluxio.worker.tieredstore.level0.dirs.quota": "8MB",
+            "alluxio.user.block.size.bytes.default": "2MB"}) as c:
+        fs = c.client()
+        for i in range(6):
+            fs.write_file(f"/ev/f{i}", os.urandom(2 * MB), write_type="CACHE_THROUGH")
+        c.heartbeat_workers()
+        cached = [fs.get_status(f"/ev/f{i}").in_alluxio_percentage for i in range(6)]
+        assert cached[:2] == [0, 0] and cached[2:] == [100] * 4
+        assert fs.read_file("/ev/f0")  # re-cached from the UFS
+        fs.close()
+
+
+def test_async_persist(tmp_path):
+    with LocalAlluxioCluster(num_workers=1, conf={
+            "alluxio.worker.tieredstore.level0.dirs.path": "dram"}) as c:
+        fs = c.client()
+        fs.write_file("/ap/f", b"persist me", write_type="ASYNC_THROUGH")
+        st = fs.get_status("/ap/f")
+        assert st.persistence_state if False else st.info.persistenceState == "TO_BE_PERSISTED"
+        from alluxio_amd.job.persist import inline_persist_handler
+        c.master.fs_master.persist_handler = inline_persist_handler(c.master.fs_master, fs)
+        c.master.fs_master.persistence_scheduler_heartbeat()
+        st = fs.get_status("/ap/f")
+        assert st.persisted
+        with open(os.path.join(c.ufs_root, "ap", "f"), "rb") as f:
+            assert f.read() == b"persist me"

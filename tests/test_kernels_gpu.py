@@ -118,7 +118,10 @@ def test_evict_select_matches_host(gpu, policy):
     rng = np.random.default_rng(2 + policy)
     n = 5000
     crf = rng.random(n).astype(np.float32) * 10
-    last = rng.permutation(n).astype(np.uint64) * 3
+    # distinct keys: LRU ages are a permutation; LRFU ages stay small enough that the decayed CRFs
+    # (crf * 0.5^(age/4)) do not underflow into ties at zero
+    last = (rng.permutation(n).astype(np.uint64) * 3) if policy == 0 else \
+        (100 - rng.integers(0, 40, n)).astype(np.uint64)
     nbytes = rng.integers(1, 64, n).astype(np.uint64) << 20
     ev = (rng.random(n) > 0.2).astype(np.uint8)
     now = int(last.max()) + 10

@@ -1,0 +1,44 @@
+#!/bin/bash
+# One GPU session: tests, smoke, bench variants, rocprof.  Each GPU step has its own timeout and
+# the script stops at the first crash-like exit (fault/abort/segv/timeout); plain test failures
+# (exit 1) do not stop later measurement steps.
+# usage: tools/gpu_round.sh [steps...]   steps: tests smoke bench variants prof kbench
+set -u
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p "$OUT"
+STEPS="${*:-tests smoke bench variants prof}"
+
+run() {  # name timeout cmd...
+  local name=$1; local t=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/round.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/round.log"
+  tail -3 "$OUT/$name.log" | tee -a "$OUT/round.log"
+  if [ $rc -ge 124 ] || [ $rc -lt 0 ]; then
+    echo "STOP: $name ended with rc=$rc (crash/timeout); no further GPU steps" | tee -a "$OUT/round.log"
+    exit $rc
+  fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 600 python -m pytest tests -m gpu -x -q ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
+    bench) run bench_default 400 python bench.py ;;
+    variants)
+      run bench_buf4k 300 python bench.py --buffer-size 4k --steps 200 --warmup 10
+      run bench_buf1m 300 python bench.py --buffer-size 1m
+      run bench_buf16m 300 python bench.py --buffer-size 16m --steps 100
+      run bench_file1g 400 python bench.py --file-size 1g --steps 100
+      run bench_host 400 python bench.py --dest host --steps 20 --warmup 3 --host-check
+      ;;
+    prof)
+      run rocprof_bench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
+      ;;
+    kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
+  esac
+done
+echo "=== done" | tee -a "$OUT/round.log"
