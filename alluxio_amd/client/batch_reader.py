@@ -42,12 +42,16 @@ class MultiStreamReader:
         self.reopens = 0
 
     def _local_worker(self, st):
+        """The in-process worker holding every block of the file (one session reads one store)."""
+        holders = None
         for fbi in st.fileBlockInfos:
-            for loc in fbi.blockInfo.locations:
-                w = self.fs.ctx.in_process_worker(loc.workerAddress)
-                if w is not None:
-                    return w
-        raise UnavailableException(f"{self.path} is not cached on a worker in this process "
+            here = {worker_address_str(l.workerAddress): l.workerAddress for l in fbi.blockInfo.locations}
+            holders = here if holders is None else {k: v for k, v in holders.items() if k in here}
+        for addr in sorted(holders or {}):
+            w = self.fs.ctx.in_process_worker(holders[addr])
+            if w is not None:
+                return w
+        raise UnavailableException(f"{self.path} is not fully cached on one worker in this process "
                                    f"(locations: {[worker_address_str(l.workerAddress) for f in st.fileBlockInfos for l in f.blockInfo.locations]})")
 
     @staticmethod

@@ -29,9 +29,11 @@ class LocalFirstPolicy(BlockLocationPolicy):
             inproc = [w for w in local if context.in_process_worker(w.address) is not None]
             if inproc:
                 local = inproc
+        # deterministic among several local workers (one per GPU): a file's blocks stay together
+        local = sorted(local, key=lambda w: (w.address.host, w.address.rpcPort))
         cands = [w for w in local if _free(w) >= block_size] or local
         if cands:
-            return random.choice(cands)
+            return cands[0]
         fit = [w for w in workers if _free(w) >= block_size]
         return random.choice(fit or workers) if workers else None
 

@@ -166,6 +166,12 @@ _k("USER_READ_BATCH_SIZE", "alluxio.user.read.batch.size", "256", Scope.CLIENT,
 _k("USER_FILE_READ_DEVICE", "alluxio.user.file.read.device", "cuda", Scope.CLIENT,
    "Preferred destination of client reads: cuda (HBM) or cpu (pinned host).")
 
+_k("JOB_MASTER_EMBEDDED_ENABLED", "alluxio.job.master.embedded.enabled", "true", Scope.MASTER,
+   "Serve the job master from the file-system master process (same RPC port) instead of a "
+   "separate job-master process.")
+_k("JOB_WORKER_ENABLED", "alluxio.job.worker.enabled", "true", Scope.WORKER,
+   "Run a job worker inside each block-worker process (tasks share the worker's HBM store).")
+
 
 def get(name: str) -> PropertyKey:
     """Resolve a key by name, alias or template match."""

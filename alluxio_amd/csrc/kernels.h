@@ -28,6 +28,8 @@ constexpr uint64_t kCopyChunk = 256 * 1024;
 // ceil(bytes / kCopyChunk).  Grid is capped and grid-strided.
 hipError_t launch_batched_copy(const CopySeg* segs, int nseg, uint64_t total_chunks,
                                hipStream_t stream);
+// Select the copy kernel variant (cache policy / unroll) and grid cap; used for A/B tuning.
+void set_copy_variant(int variant, unsigned grid_cap);
 
 // CRC32C (Castagnoli, reflected, init/xorout 0xFFFFFFFF) of `n` equal-length pieces
 // (piece i = base + i*piece_bytes, last may be shorter: total_bytes).  `out` device array.

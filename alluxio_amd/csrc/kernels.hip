@@ -19,28 +19,42 @@ namespace amdx {
 // with 16-B loads, 8 in flight per lane (128 B/lane, 32 KiB per workgroup round).
 // ---------------------------------------------------------------------------------------------
 constexpr int kCopyThreads = 256;
-constexpr int kCopyUnroll = 8;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Load/store cache policies (A/B-able at run time, see set_copy_variant):
+//   0 = default, 1 = nontemporal (``nt``: stream past the caches).
+template <int P>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+  if constexpr (P == 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int P>
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+  if constexpr (P == 1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 
 __device__ __forceinline__ void copy_bytes(const uint8_t* __restrict__ s, uint8_t* __restrict__ d,
                                            uint64_t n, int tid) {
   for (uint64_t i = tid; i < n; i += kCopyThreads) d[i] = s[i];
 }
 
+template <int UNROLL, int LP, int SP>
 __device__ __forceinline__ void copy_range(uint64_t src, uint64_t dst, uint64_t n, int tid) {
   if (((src | dst) & 15) == 0) {
-    const uint4* __restrict__ s = reinterpret_cast<const uint4*>(src);
-    uint4* __restrict__ d = reinterpret_cast<uint4*>(dst);
+    const u32x4* __restrict__ s = reinterpret_cast<const u32x4*>(src);
+    u32x4* __restrict__ d = reinterpret_cast<u32x4*>(dst);
     const uint64_t n16 = n >> 4;
     uint64_t i = tid;
-    constexpr uint64_t kStep = (uint64_t)kCopyThreads * kCopyUnroll;
-    for (; i + (kCopyUnroll - 1) * kCopyThreads < n16; i += kStep) {
-      uint4 v[kCopyUnroll];
+    constexpr uint64_t kStep = (uint64_t)kCopyThreads * UNROLL;
+    for (; i + (UNROLL - 1) * kCopyThreads < n16; i += kStep) {
+      u32x4 v[UNROLL];
 #pragma unroll
-      for (int u = 0; u < kCopyUnroll; ++u) v[u] = s[i + (uint64_t)u * kCopyThreads];
+      for (int u = 0; u < UNROLL; ++u) v[u] = ld16<LP>(s + i + (uint64_t)u * kCopyThreads);
 #pragma unroll
-      for (int u = 0; u < kCopyUnroll; ++u) d[i + (uint64_t)u * kCopyThreads] = v[u];
+      for (int u = 0; u < UNROLL; ++u) st16<SP>(d + i + (uint64_t)u * kCopyThreads, v[u]);
     }
-    for (; i < n16; i += kCopyThreads) d[i] = s[i];
+    for (; i < n16; i += kCopyThreads) st16<SP>(d + i, ld16<LP>(s + i));
     const uint64_t done = n16 << 4;
     if (done < n) copy_bytes(reinterpret_cast<const uint8_t*>(src) + done,
                              reinterpret_cast<uint8_t*>(dst) + done, n - done, tid);
@@ -57,6 +71,7 @@ __device__ __forceinline__ void copy_range(uint64_t src, uint64_t dst, uint64_t 
   }
 }
 
+template <int UNROLL, int LP, int SP>
 __global__ __launch_bounds__(kCopyThreads) void batched_copy_kernel(
     const CopySeg* __restrict__ segs, int nseg, uint64_t total_chunks) {
   const int tid = threadIdx.x;
@@ -70,17 +85,39 @@ __global__ __launch_bounds__(kCopyThreads) void batched_copy_kernel(
     const uint64_t src = segs[lo].src, dst = segs[lo].dst, bytes = segs[lo].bytes;
     const uint64_t off = (c - segs[lo].chunk0) * kCopyChunk;
     const uint64_t n = bytes - off < kCopyChunk ? bytes - off : kCopyChunk;
-    copy_range(src + off, dst + off, n, tid);
+    copy_range<UNROLL, LP, SP>(src + off, dst + off, n, tid);
   }
+}
+
+// variant = unroll_sel * 4 + load_policy * 2 + store_policy; unroll_sel: 0 -> 8, 1 -> 4, 2 -> 16
+// Default from tools/copy_tune.py on MI355X (profiles/r1_copy_tune.jsonl): 16-deep unroll,
+// cached loads+stores, grid cap 4096 won the bench shape (5.42 TB/s vs 5.24 for 8-deep/2048).
+static int g_copy_variant = 8;
+static unsigned g_copy_grid_cap = 4096;
+
+void set_copy_variant(int variant, unsigned grid_cap) {
+  g_copy_variant = variant;
+  if (grid_cap) g_copy_grid_cap = grid_cap;
 }
 
 hipError_t launch_batched_copy(const CopySeg* segs, int nseg, uint64_t total_chunks,
                                hipStream_t stream) {
   if (nseg <= 0 || total_chunks == 0) return hipSuccess;
   // 256 CUs x 8 resident 256-thread workgroups; more chunks are grid-strided.
-  const uint64_t grid = std::min<uint64_t>(total_chunks, 2048);
-  hipLaunchKernelGGL(batched_copy_kernel, dim3((unsigned)grid), dim3(kCopyThreads), 0, stream,
-                     segs, nseg, total_chunks);
+  const dim3 grid((unsigned)std::min<uint64_t>(total_chunks, g_copy_grid_cap));
+  const dim3 block(kCopyThreads);
+#define AMDX_COPY(U, L, S) hipLaunchKernelGGL((batched_copy_kernel<U, L, S>), grid, block, 0, stream, segs, nseg, total_chunks)
+  switch (g_copy_variant) {
+    case 1: AMDX_COPY(8, 0, 1); break;
+    case 2: AMDX_COPY(8, 1, 0); break;
+    case 3: AMDX_COPY(8, 1, 1); break;
+    case 4: AMDX_COPY(4, 0, 0); break;
+    case 5: AMDX_COPY(4, 0, 1); break;
+    case 8: AMDX_COPY(16, 0, 0); break;
+    case 9: AMDX_COPY(16, 0, 1); break;
+    default: AMDX_COPY(8, 0, 0); break;
+  }
+#undef AMDX_COPY
   return hipGetLastError();
 }
 

@@ -1,0 +1,372 @@
+"""Job plans: configs + PlanDefinition SPI (selectExecutors / runTask / join).
+
+Parity: job/server/src/main/java/alluxio/job/plan/PlanDefinition.java and the plans under
+job/server/src/main/java/alluxio/job/plan/: load/LoadDefinition.java (:60-150 — distribute the
+non-cached blocks of a path over workers, each task reads its blocks through the local worker
+with CACHE), persist/PersistDefinition.java, replicate/{Replicate,Evict,Move}Definition.java,
+migrate/MigrateDefinition.java (distributed cp/mv), stress/StressBenchDefinition.java (:60-130 —
+run a stress bench on N job workers, merge results).  Job configs travel as JSON in the
+``jobConfig`` bytes of RunPRequest / RunTaskCommand.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import logging
+import random
+
+from ..proto import pb
+from ..utils import exceptions as ex
+
+LOG = logging.getLogger(__name__)
+
+_REGISTRY: dict[str, type] = {}
+
+
+def plan(name):
+    def deco(cls):
+        cls.type_name = name
+        _REGISTRY[name] = cls
+        return cls
+    return deco
+
+
+@dataclasses.dataclass
+class JobConfig:
+    type_name = "base"
+
+    def to_bytes(self) -> bytes:
+        d = dataclasses.asdict(self)
+        d["@type"] = self.type_name
+        return json.dumps(d).encode()
+
+    @staticmethod
+    def from_bytes(b: bytes) -> "JobConfig":
+        d = json.loads(b.decode())
+        t = d.pop("@type")
+        cls = CONFIGS[t]
+        if cls is CompositeConfig:
+            d["jobs"] = [JobConfig.from_bytes(json.dumps(j).encode()) if isinstance(j, dict) else j
+                         for j in d["jobs"]]
+        return cls(**d)
+
+    def definition(self) -> "PlanDefinition":
+        return _REGISTRY[self.type_name]()
+
+
+CONFIGS: dict[str, type] = {}
+
+
+def config(name):
+    def deco(cls):
+        cls.type_name = name
+        CONFIGS[name] = cls
+        return cls
+    return deco
+
+
+@config("load")
+@dataclasses.dataclass
+class LoadConfig(JobConfig):
+    path: str = "/"
+    replication: int = 1
+    worker_set: list = dataclasses.field(default_factory=list)
+    excluded_worker_set: list = dataclasses.field(default_factory=list)
+    local_only: bool = False
+
+
+@config("persist")
+@dataclasses.dataclass
+class PersistConfig(JobConfig):
+    path: str = "/"
+    mount_id: int = 0
+    overwrite: bool = True
+    ufs_path: str = ""
+
+
+@config("replicate")
+@dataclasses.dataclass
+class ReplicateConfig(JobConfig):
+    block_id: int = 0
+    replicas: int = 1
+    path: str = ""
+    medium: str = ""
+
+
+@config("evict")
+@dataclasses.dataclass
+class EvictConfig(JobConfig):
+    block_id: int = 0
+    replicas: int = 1
+
+
+@config("move")
+@dataclasses.dataclass
+class MoveConfig(JobConfig):
+    block_id: int = 0
+    worker_host: str = ""
+    medium: str = ""
+
+
+@config("migrate")
+@dataclasses.dataclass
+class MigrateConfig(JobConfig):
+    source: str = "/"
+    destination: str = "/"
+    write_type: str = "ASYNC_THROUGH"
+    overwrite: bool = False
+    delete_source: bool = False
+
+
+@config("stress")
+@dataclasses.dataclass
+class StressBenchConfig(JobConfig):
+    bench: str = "worker"          # worker | client-io | master | ufs-io
+    args: list = dataclasses.field(default_factory=list)
+    cluster_limit: int = 0
+
+
+@config("composite")
+@dataclasses.dataclass
+class CompositeConfig(JobConfig):
+    jobs: list = dataclasses.field(default_factory=list)
+    sequential: bool = True
+
+    def to_bytes(self) -> bytes:
+        return json.dumps({"@type": "composite", "sequential": self.sequential,
+                           "jobs": [json.loads(j.to_bytes()) for j in self.jobs]}).encode()
+
+
+class RunTaskContext:
+    """What a task sees on the job worker: a client FileSystem and the co-located block worker."""
+
+    def __init__(self, fs, worker=None, worker_address=None, job_id=0, task_id=0):
+        self.fs = fs
+        self.worker = worker
+        self.worker_address = worker_address
+        self.job_id = job_id
+        self.task_id = task_id
+
+
+class PlanDefinition:
+    def select_executors(self, cfg, job_workers: list, fs) -> list[tuple[object, object]]:
+        """[(job worker info, task args)] — one task per entry."""
+        raise NotImplementedError
+
+    def run_task(self, cfg, args, ctx: RunTaskContext):
+        raise NotImplementedError
+
+    def join(self, cfg, task_results: dict):
+        return {"tasks": len(task_results)}
+
+
+def _worker_key(addr) -> str:
+    return f"{addr.host}:{addr.rpcPort}"
+
+
+def _find_job_worker(job_workers, block_worker_addr):
+    for jw in job_workers:
+        if jw.address.host == block_worker_addr.host and jw.block_worker_port == block_worker_addr.rpcPort:
+            return jw
+    return None
+
+
+# ----------------------------------------------------------------------------------------------
+@plan("load")
+class LoadDefinition(PlanDefinition):
+    def select_executors(self, cfg, job_workers, fs):
+        statuses = [s for s in fs.list_status(cfg.path, recursive=True) if not s.info.folder] \
+            if fs.get_status(cfg.path).info.folder else [fs.get_status(cfg.path)]
+        usable = [jw for jw in job_workers
+                  if (not cfg.worker_set or jw.address.host in cfg.worker_set)
+                  and jw.address.host not in cfg.excluded_worker_set]
+        if not usable:
+            raise ex.FailedPreconditionException("no job worker available for load")
+        assign: dict[int, list] = {}
+        for st in statuses:
+            for fbi in st.info.fileBlockInfos:
+                have = {(l.workerAddress.host, l.workerAddress.rpcPort) for l in fbi.blockInfo.locations}
+                need = cfg.replication - len(have)
+                if need <= 0:
+                    continue
+                cands = [jw for jw in usable if (jw.address.host, jw.block_worker_port) not in have]
+                random.shuffle(cands)
+                for jw in cands[:need]:
+                    assign.setdefault(jw.id, []).append((st.info.path, fbi.blockInfo.blockId))
+        by_id = {jw.id: jw for jw in usable}
+        return [(by_id[w], blocks) for w, blocks in assign.items()]
+
+    def run_task(self, cfg, args, ctx):
+        loaded = 0
+        for path, block_id in args:
+            st = ctx.fs.get_status(path)
+            idx = list(st.info.blockIds).index(block_id)
+            opts = pb.dataserver.OpenUfsBlockOptions(
+                ufs_path=st.info.ufsPath, offset_in_file=idx * st.info.blockSizeBytes,
+                block_size=st.info.fileBlockInfos[idx].blockInfo.length, mountId=st.info.mountId)
+            if ctx.worker is not None and ctx.worker.has_block(block_id):
+                continue
+            locs = st.info.fileBlockInfos[idx].blockInfo.locations
+            if ctx.worker is not None and locs:
+                from ..worker.remote import remote_block_fetcher
+                src = locs[0].workerAddress
+                remote_block_fetcher(ctx.worker, src.host, src.rpcPort, opts.block_size)(block_id)
+            elif ctx.worker is not None:
+                ctx.worker.cache_block_from_ufs(block_id, opts)
+            loaded += opts.block_size
+        return loaded
+
+    def join(self, cfg, task_results):
+        return {"bytes_loaded": sum(v or 0 for v in task_results.values())}
+
+
+@plan("persist")
+class PersistDefinition(PlanDefinition):
+    def select_executors(self, cfg, job_workers, fs):
+        if not job_workers:
+            raise ex.FailedPreconditionException("no job worker available for persist")
+        st = fs.get_status(cfg.path)
+        # prefer the worker holding the most bytes of the file
+        score = {}
+        for fbi in st.info.fileBlockInfos:
+            for l in fbi.blockInfo.locations:
+                jw = _find_job_worker(job_workers, l.workerAddress)
+                if jw is not None:
+                    score[jw.id] = score.get(jw.id, 0) + fbi.blockInfo.length
+        best = max(job_workers, key=lambda jw: score.get(jw.id, 0))
+        return [(best, cfg.path)]
+
+    def run_task(self, cfg, args, ctx):
+        from .persist import persist_file
+        return persist_file(ctx.fs, args)
+
+
+@plan("replicate")
+class ReplicateDefinition(PlanDefinition):
+    def select_executors(self, cfg, job_workers, fs):
+        bi = fs.ctx.block_master().GetBlockInfo(pb.block.GetBlockInfoPRequest(blockId=cfg.block_id)).blockInfo
+        have = {(l.workerAddress.host, l.workerAddress.rpcPort) for l in bi.locations}
+        cands = [jw for jw in job_workers if (jw.address.host, jw.block_worker_port) not in have]
+        random.shuffle(cands)
+        src = (bi.locations[0].workerAddress.host, bi.locations[0].workerAddress.rpcPort) if bi.locations else None
+        return [(jw, {"src": src, "length": bi.length, "path": cfg.path}) for jw in cands[:cfg.replicas]]
+
+    def run_task(self, cfg, args, ctx):
+        if ctx.worker is None or ctx.worker.has_block(cfg.block_id):
+            return 0
+        plane = getattr(ctx.worker, "transfer_plane", None)
+        if plane is not None and args["src"] is not None and plane.can_reach(args["src"]):
+            plane.pull_block(cfg.block_id, args["src"], args["length"])
+        elif args["src"] is not None:
+            from ..worker.remote import remote_block_fetcher
+            remote_block_fetcher(ctx.worker, args["src"][0], args["src"][1], args["length"])(cfg.block_id)
+        elif args["path"]:
+            st = ctx.fs.get_status(args["path"])
+            idx = list(st.info.blockIds).index(cfg.block_id)
+            ctx.worker.cache_block_from_ufs(cfg.block_id, pb.dataserver.OpenUfsBlockOptions(
+                ufs_path=st.info.ufsPath, offset_in_file=idx * st.info.blockSizeBytes, block_size=args["length"],
+                mountId=st.info.mountId))
+        return args["length"]
+
+
+@plan("evict")
+class EvictDefinition(PlanDefinition):
+    def select_executors(self, cfg, job_workers, fs):
+        bi = fs.ctx.block_master().GetBlockInfo(pb.block.GetBlockInfoPRequest(blockId=cfg.block_id)).blockInfo
+        holders = [jw for l in bi.locations for jw in [_find_job_worker(job_workers, l.workerAddress)] if jw]
+        random.shuffle(holders)
+        return [(jw, None) for jw in holders[:cfg.replicas]]
+
+    def run_task(self, cfg, args, ctx):
+        from ..utils import ids
+        if ctx.worker is not None and ctx.worker.has_block(cfg.block_id):
+            ctx.worker.remove_block(ids.MIGRATE_DATA_SESSION_ID, cfg.block_id)
+            return 1
+        return 0
+
+
+@plan("move")
+class MoveDefinition(PlanDefinition):
+    def select_executors(self, cfg, job_workers, fs):
+        return [(jw, None) for jw in job_workers if not cfg.worker_host or jw.address.host == cfg.worker_host][:1]
+
+    def run_task(self, cfg, args, ctx):
+        from ..utils import ids
+        if ctx.worker is not None and ctx.worker.has_block(cfg.block_id):
+            ctx.worker.move_block(ids.MIGRATE_DATA_SESSION_ID, cfg.block_id, medium=cfg.medium)
+            return 1
+        return 0
+
+
+@plan("migrate")
+class MigrateDefinition(PlanDefinition):
+    def select_executors(self, cfg, job_workers, fs):
+        if not job_workers:
+            raise ex.FailedPreconditionException("no job worker available for migrate")
+        src = fs.get_status(cfg.source)
+        if src.info.folder:
+            pairs = []
+            base = cfg.source.rstrip("/")
+            for s in fs.list_status(cfg.source, recursive=True):
+                if not s.info.folder:
+                    pairs.append((s.info.path, cfg.destination.rstrip("/") + s.info.path[len(base):]))
+        else:
+            dst = cfg.destination
+            try:
+                if fs.get_status(dst).info.folder:
+                    dst = dst.rstrip("/") + "/" + src.info.name
+            except ex.NotFoundException:
+                pass
+            pairs = [(src.info.path, dst)]
+        out = []
+        for i, pair in enumerate(pairs):
+            out.append((job_workers[i % len(job_workers)], pair))
+        return out
+
+    def run_task(self, cfg, args, ctx):
+        src, dst = args
+        if ctx.fs.exists(dst, load_metadata="NEVER"):
+            if not cfg.overwrite:
+                raise ex.FileAlreadyExistsException(f"{dst} already exists")
+            ctx.fs.delete(dst)
+        n = 0
+        with ctx.fs.open_file(src) as fin, ctx.fs.create_file(dst, write_type=cfg.write_type) as fout:
+            while True:
+                data = fin.read(8 << 20)
+                if not data:
+                    break
+                fout.write(data)
+                n += len(data)
+        if cfg.delete_source:
+            ctx.fs.delete(src)
+        return n
+
+    def join(self, cfg, task_results):
+        return {"files": len(task_results), "bytes": sum(v or 0 for v in task_results.values())}
+
+
+@plan("stress")
+class StressBenchDefinition(PlanDefinition):
+    def select_executors(self, cfg, job_workers, fs):
+        ws = list(job_workers)
+        if cfg.cluster_limit > 0:
+            ws = ws[:cfg.cluster_limit]
+        out = []
+        for i, jw in enumerate(ws):
+            args = list(cfg.args)
+            # each task gets its own base directory (reference BaseParameters --id / task id)
+            if "--base" in args:
+                j = args.index("--base") + 1
+                args[j] = f"{args[j].rstrip('/')}/task{i}"
+            elif cfg.bench != "ufs-io":
+                args += ["--base", f"/stress-{cfg.bench}-base/task{i}"]
+            out.append((jw, args))
+        return out
+
+    def run_task(self, cfg, args, ctx):
+        from ..stress import run_local
+        return run_local(cfg.bench, args, ctx.fs)
+
+    def join(self, cfg, task_results):
+        from ..stress import merge_results
+        return merge_results(cfg.bench, list(task_results.values()))

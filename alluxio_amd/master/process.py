@@ -101,6 +101,11 @@ class AlluxioMasterProcess:
                                 if False else 64, metrics=self.metrics, enable_grpc=enable_grpc)
         self._threads: list[hb.HeartbeatThread] = []
         self.job_master = None
+        if self.conf.get_bool("alluxio.job.master.embedded.enabled", "true"):
+            from ..job.master import JobMaster
+            self.job_master = JobMaster(self._job_fs, self.conf.get_ms("alluxio.job.master.worker.timeout") / 1000.0,
+                                        self.conf.get_int("alluxio.job.master.job.capacity"))
+        self._job_client_fs = None
         self.web = None
         self.started = False
         self.primary = False
@@ -108,6 +113,36 @@ class AlluxioMasterProcess:
     @property
     def address(self) -> str:
         return self.server.address
+
+    def _job_fs(self):
+        from ..client.file_system import FileSystem
+        if self._job_client_fs is None:
+            self._job_client_fs = FileSystem(conf=self.conf, master_address=self.address)
+        return self._job_client_fs
+
+    def _persist_via_job(self, file_id: int, path: str) -> int:
+        from ..job import PersistConfig
+        return self.job_master.run(PersistConfig(path=path))
+
+    def persistence_checker(self) -> int:
+        """PersistenceChecker: poll persist jobs; mark files persisted or reschedule failures."""
+        if self.job_master is None:
+            return 0
+        done = 0
+        for fid, info in list(self.fs_master.persist_jobs.items()):
+            jid = info.get("job", -1)
+            if jid is None or jid < 0:
+                continue
+            try:
+                st = self.job_master.status(jid).status
+            except Exception:  # noqa: BLE001 - job purged or unknown: retry the persist
+                st = "FAILED"
+            if st == "COMPLETED":
+                self.fs_master.persist_done(fid, True)
+                done += 1
+            elif st in ("FAILED", "CANCELED"):
+                self.fs_master.persist_done(fid, False)
+        return done
 
     def _register_services(self) -> None:
         s = self.server
@@ -120,6 +155,12 @@ class AlluxioMasterProcess:
         meta = MetaServices(self.meta_master, self.metrics_master, self.journal)
         for svc in (SVC_META_CLIENT, SVC_META_CONFIG, SVC_META_MASTER, SVC_METRICS, SVC_JOURNAL):
             s.add_servicer(svc, meta)
+        if self.job_master is not None:
+            from ..job import SVC_JOB_CLIENT, SVC_JOB_WORKER
+            from ..job.master import JobMasterService
+            jsvc = JobMasterService(self.job_master)
+            s.add_servicer(SVC_JOB_CLIENT, jsvc)
+            s.add_servicer(SVC_JOB_WORKER, jsvc)
         s.add_servicer(SVC_VERSION, ServiceVersionHandler())
         s.add_servicer(SVC_SASL, SaslHandler())
 
@@ -132,6 +173,8 @@ class AlluxioMasterProcess:
         self.journal.start()
         if primary:
             self.gain_primacy()
+        if self.job_master is not None and self.fs_master.persist_handler is None:
+            self.fs_master.persist_handler = self._persist_via_job
         self._register_services()
         addr = self.server.start()
         self.meta_master.master_address = addr
@@ -170,6 +213,14 @@ class AlluxioMasterProcess:
             (hb.MASTER_LOST_MASTER_DETECTION, self.meta_master.detect_lost_masters,
              c.get_ms("alluxio.master.standby.heartbeat.interval", "2min")),
         ]
+        if self.job_master is not None:
+            specs.append((hb.MASTER_PERSISTENCE_CHECKER, self.persistence_checker,
+                          c.get_ms("alluxio.master.persistence.checker.interval", "1sec")))
+            specs.append((hb.JOB_MASTER_LOST_WORKER_DETECTION, self.job_master.detect_lost_workers,
+                          c.get_ms("alluxio.job.master.lost.worker.interval")))
+            retention = c.get_ms("alluxio.job.master.finished.job.retention.time") / 1000.0
+            specs.append(("Job Master Finished Job Purge",
+                          lambda: self.job_master.purge_finished(retention), 10_000))
         if c.get_ms("alluxio.master.periodic.block.integrity.check.interval", "1hr") > 0:
             specs.append((hb.MASTER_BLOCK_INTEGRITY_CHECK, self.fs_master.block_integrity_check,
                           c.get_ms("alluxio.master.periodic.block.integrity.check.interval", "1hr")))
@@ -196,6 +247,9 @@ class AlluxioMasterProcess:
         if self.web is not None:
             self.web.stop()
         self.server.stop()
+        if self._job_client_fs is not None:
+            self._job_client_fs.close()
+            self._job_client_fs = None
         self.journal.stop()
         self.started = False
 

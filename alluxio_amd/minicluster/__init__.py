@@ -99,6 +99,21 @@ class LocalAlluxioCluster:
         for w in self.workers:
             w.sync.heartbeat()
 
+    def drive_jobs(self) -> None:
+        """One job-worker heartbeat per worker plus the master persistence checker (tests run
+        without background heartbeat threads)."""
+        for w in self.workers:
+            if w.job_worker is not None:
+                w.job_worker.heartbeat()
+        self.master.persistence_checker()
+
+    def run_job(self, cfg, timeout: float = 120.0):
+        """Submit a job through the JobMasterClientService and drive it to completion."""
+        from ..job import JobClient
+        from ..rpc import Channel
+        client = JobClient(Channel(self.master.address))
+        return client.run_and_wait(cfg, timeout=timeout, on_poll=self.drive_jobs)
+
     def stop(self) -> None:
         for w in list(self.workers):
             w.stop()

@@ -105,6 +105,8 @@ class AlluxioWorkerProcess:
         self.server.add_servicer(SVC_BLOCK_WORKER, BlockWorkerService(self.worker, self.conf))
         self.sync = BlockMasterSync(self.worker, self)
         self._threads: list[hb.HeartbeatThread] = []
+        self.job_worker = None
+        self._job_fs = None
 
     @property
     def address(self) -> str:
@@ -137,8 +139,35 @@ class AlluxioWorkerProcess:
                 t = hb.HeartbeatThread(name, fn, ms)
                 t.start()
                 self._threads.append(t)
+        if self.conf.get_bool("alluxio.job.worker.enabled", "true"):
+            self._start_job_worker(start_heartbeats)
         LOG.info("worker serving at %s (device %d)", addr, self.store.device)
         return addr
+
+    def _start_job_worker(self, start_heartbeat: bool) -> None:
+        """Job worker co-located with the block worker (reference AlluxioJobWorkerProcess runs
+        beside each worker; here it shares the process so tasks read/write the local HBM store
+        directly)."""
+        from ..client.file_system import FileSystem
+        from ..job.master import JobWorker
+        self._job_fs = FileSystem(conf=self.conf, master_address=self.master_address)
+        self.job_worker = JobWorker(self.master_channel, self.worker.address, self._job_fs, self.worker,
+                                    pool_size=self.conf.get_int("alluxio.job.worker.threadpool.size"))
+        try:
+            self.job_worker.register()
+        except Exception:  # noqa: BLE001 - job master may be absent; heartbeat retries
+            LOG.info("job master not reachable at %s; job worker will retry", self.master_address)
+        if start_heartbeat:
+            self.add_heartbeat(hb.JOB_WORKER_COMMAND_HANDLING, self._job_heartbeat,
+                               self.conf.get_ms("alluxio.job.master.worker.heartbeat.interval"))
+
+    def _job_heartbeat(self) -> None:
+        try:
+            self.job_worker.heartbeat()
+        except Exception as e:  # noqa: BLE001
+            if "UNIMPLEMENTED" in str(e) or "not found" in str(e).lower():
+                return
+            raise
 
     def add_heartbeat(self, name: str, fn, interval_ms: int) -> None:
         t = hb.HeartbeatThread(name, fn, interval_ms)
@@ -180,6 +209,10 @@ class AlluxioWorkerProcess:
         if self.server.address:
             unregister_local_worker(self.server.address)
         self.server.stop()
+        if self.job_worker is not None:
+            self.job_worker.close()
+        if self._job_fs is not None:
+            self._job_fs.close()
         self.worker.close()
 
 

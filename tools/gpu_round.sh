@@ -39,6 +39,7 @@ for s in $STEPS; do
       run rocprof_bench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
       ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
+    tune) run copy_tune 600 python tools/copy_tune.py --out "$OUT/copy_tune.json" ;;
   esac
 done
 echo "=== done" | tee -a "$OUT/round.log"
