@@ -1,0 +1,58 @@
+"""``alluxio readJournal`` — dump a UFS journal as text.
+
+Parity: core/server/master/src/main/java/alluxio/master/journal/tool/JournalTool.java (dumps
+the latest checkpoint and the log entries in [start, end) of one master's journal into an
+output directory: ``checkpoints/`` and ``edits.txt``).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+from google.protobuf import text_format
+
+
+def dump_journal(journal_dir: str, master: str, output_dir: str, start: int = 0, end: int = 2 ** 63 - 1,
+                 out=None) -> int:
+    from ..journal.ufs_journal import UfsJournal
+    out = out or sys.stdout
+    j = UfsJournal(journal_dir, master)
+    if not j.is_formatted():
+        raise FileNotFoundError(f"no journal for {master} under {journal_dir}")
+    os.makedirs(output_dir, exist_ok=True)
+    ctype, payload, cp_end = j.read_checkpoint()
+    if ctype is not None:
+        cdir = os.path.join(output_dir, "checkpoints")
+        os.makedirs(cdir, exist_ok=True)
+        with open(os.path.join(cdir, f"0x0-0x{cp_end:x}.{ctype.name}"), "wb") as f:
+            f.write(payload)
+        print(f"Checkpoint type {ctype.name} covering [0, {cp_end}) written to {cdir}", file=out)
+    n = 0
+    with open(os.path.join(output_dir, "edits.txt"), "w") as f:
+        for e in j.iter_log_entries(max(start, cp_end if ctype is not None and start < cp_end else start)):
+            if e.sequence_number >= end:
+                break
+            f.write(text_format.MessageToString(e))
+            f.write("\n")
+            n += 1
+    print(f"Dumped {n} journal entries of {master} to {output_dir}/edits.txt", file=out)
+    return n
+
+
+def main(argv=None, out=None) -> int:
+    import argparse
+    ap = argparse.ArgumentParser(prog="alluxio readJournal")
+    ap.add_argument("-master", "--master", default="FileSystemMaster")
+    ap.add_argument("-start", "--start", type=int, default=0)
+    ap.add_argument("-end", "--end", type=int, default=2 ** 63 - 1)
+    ap.add_argument("-inputDir", "--inputDir", default=None)
+    ap.add_argument("-outputDir", "--outputDir", default=None)
+    a = ap.parse_args(argv)
+    from ..conf import Configuration
+    conf = Configuration(load_site=True)
+    jdir = a.inputDir or conf.get("alluxio.master.journal.folder")
+    if jdir.startswith("file://"):
+        jdir = jdir[len("file://"):]
+    outdir = a.outputDir or os.path.join(os.getcwd(), f"journal_dump-{os.getpid()}")
+    dump_journal(jdir, a.master, outdir, a.start, a.end, out)
+    return 0

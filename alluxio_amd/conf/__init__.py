@@ -38,6 +38,12 @@ def _keyname(key) -> str:
     return key.name if isinstance(key, PropertyKey) else str(key)
 
 
+def site_properties_path() -> str:
+    """Where ``bootstrapConf`` writes / the first site-properties location searched."""
+    d = os.environ.get("ALLUXIO_CONF_DIR") or os.path.expanduser("~/.alluxio")
+    return os.path.join(d, SITE_PROPERTIES)
+
+
 class Configuration:
     def __init__(self, props: dict | None = None, load_site: bool = False):
         self._lock = threading.RLock()

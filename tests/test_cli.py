@@ -1,0 +1,245 @@
+"""Shell / CLI tests (reference shell/src/test and tests/.../cli/fs/command/*CommandIntegrationTest:
+run a command against a LocalAlluxioCluster, check output + namespace effects)."""
+import io
+import os
+
+import pytest
+
+from alluxio_amd.cli.fs_shell import COMMANDS, FileSystemShell
+from alluxio_amd.cli.fsadmin import FileSystemAdminShell
+from alluxio_amd.cli.job_shell import JobShell
+from alluxio_amd.minicluster import LocalAlluxioCluster
+from alluxio_amd.rpc import Channel
+
+CONF = {"alluxio.worker.tieredstore.level0.dirs.path": "dram", "alluxio.user.block.size.bytes.default": "1MB"}
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    with LocalAlluxioCluster(num_workers=2, conf=CONF) as c:
+        yield c
+
+
+@pytest.fixture
+def sh(cluster):
+    out = io.StringIO()
+    fs = cluster.client()
+    s = FileSystemShell(fs, out)
+    yield s
+    fs.close()
+
+
+def run(sh, cmd):
+    sh.out.seek(0)
+    sh.out.truncate()
+    rc = sh.run(cmd)
+    return rc, sh.out.getvalue()
+
+
+def test_all_reference_commands_registered():
+    ref = ["cat", "checkConsistency", "checksum", "chgrp", "chmod", "chown", "copyFromLocal", "copyToLocal",
+           "count", "cp", "distributedCp", "distributedLoad", "distributedMv", "du", "free", "getCapacityBytes",
+           "getfacl", "getSyncPathList", "getUsedBytes", "head", "help", "leader", "load", "loadMetadata",
+           "location", "ls", "masterInfo", "mkdir", "mount", "mv", "persist", "pin", "rm", "setfacl",
+           "setReplication", "setTtl", "startSync", "stat", "stopSync", "tail", "test", "touch", "unmount",
+           "unpin", "unsetTtl", "updateMount"]
+    assert sorted(set(ref) - set(COMMANDS)) == []
+
+
+def test_mkdir_ls_stat_rm(sh):
+    assert run(sh, "mkdir /cli/a /cli/b")[0] == 0
+    sh.fs.write_file("/cli/a/f", b"hello world", write_type="CACHE_THROUGH")
+    rc, out = run(sh, "ls -R /cli")
+    assert rc == 0 and "/cli/a/f" in out and "100%" in out and "PERSISTED" in out
+    rc, out = run(sh, "ls -h /cli/a")
+    assert "11.00B" in out
+    rc, out = run(sh, "stat -f %N:%z /cli/a/f")
+    assert out.strip() == "f:11"
+    rc, out = run(sh, "cat /cli/a/f")
+    assert out == "hello world"
+    assert run(sh, "head -c 5 /cli/a/f")[1] == "hello"
+    assert run(sh, "tail -c 5 /cli/a/f")[1] == "world"
+    assert run(sh, "test -d /cli/a")[0] == 0 and run(sh, "test -f /cli/a")[0] == 1
+    assert run(sh, "test -e /cli/nope")[0] == 1
+    rc, out = run(sh, "rm /cli/a")
+    assert rc == -1 and "is a directory" in out
+    assert run(sh, "rm -R /cli/a")[0] == 0
+    assert not sh.fs.exists("/cli/a")
+
+
+def test_copy_local_roundtrip(sh, tmp_path):
+    src = tmp_path / "in"
+    src.mkdir()
+    (src / "x.bin").write_bytes(os.urandom(3 << 20))
+    (src / "sub").mkdir()
+    (src / "sub" / "y.txt").write_text("yy")
+    assert run(sh, f"copyFromLocal {src} /cp/in")[0] == 0
+    assert sh.fs.read_file("/cp/in/sub/y.txt") == b"yy"
+    dst = tmp_path / "out"
+    assert run(sh, f"copyToLocal /cp/in {dst}")[0] == 0
+    assert (dst / "x.bin").read_bytes() == (src / "x.bin").read_bytes()
+    assert run(sh, "cp -R /cp/in /cp/copy")[0] == 0
+    assert sh.fs.read_file("/cp/copy/sub/y.txt") == b"yy"
+    assert run(sh, "mv /cp/copy /cp/moved")[0] == 0
+    assert sh.fs.exists("/cp/moved/x.bin") and not sh.fs.exists("/cp/copy")
+    rc, out = run(sh, "checksum /cp/in/x.bin")
+    import hashlib
+    assert out.strip() == "md5sum: " + hashlib.md5((src / "x.bin").read_bytes()).hexdigest()
+    rc, out = run(sh, "count /cp/in")
+    assert out.splitlines()[1].split()[:3] == ["2", "2", str((3 << 20) + 2)]
+    rc, out = run(sh, "du -s /cp/in")
+    assert str((3 << 20) + 2) in out
+
+
+def test_attributes(sh):
+    sh.fs.write_file("/attr/f", b"x", write_type="MUST_CACHE")
+    assert run(sh, "chmod 640 /attr/f")[0] == 0
+    assert sh.fs.get_status("/attr/f").info.mode == 0o640
+    assert run(sh, "chmod u+x,o+r /attr/f")[0] == 0
+    assert sh.fs.get_status("/attr/f").info.mode == 0o744
+    assert run(sh, "chown alice:staff /attr/f")[0] == 0
+    i = sh.fs.get_status("/attr/f").info
+    assert (i.owner, i.group) == ("alice", "staff")
+    assert run(sh, "chgrp -R eng /attr")[0] == 0
+    assert sh.fs.get_status("/attr/f").info.group == "eng"
+    assert run(sh, "pin /attr/f")[0] == 0 and sh.fs.get_status("/attr/f").info.pinned
+    assert "/attr/f" in run(sh, "ls -p /attr")[1]
+    assert run(sh, "unpin /attr/f")[0] == 0 and not sh.fs.get_status("/attr/f").info.pinned
+    assert run(sh, "setTtl /attr/f 1h")[0] == 0 and sh.fs.get_status("/attr/f").info.ttl == 3_600_000
+    assert run(sh, "unsetTtl /attr/f")[0] == 0 and sh.fs.get_status("/attr/f").info.ttl == -1
+    assert run(sh, "setReplication --min 1 --max 2 /attr/f")[0] == 0
+    i = sh.fs.get_status("/attr/f").info
+    assert (i.replicationMin, i.replicationMax) == (1, 2)
+    assert run(sh, "setfacl -m user:bob:rw- /attr/f")[0] == 0
+    assert "user:bob:rw-" in run(sh, "getfacl /attr/f")[1]
+
+
+def test_cache_commands(cluster, sh):
+    sh.fs.write_file("/cache/f", os.urandom(2 << 20), write_type="CACHE_THROUGH")
+    cluster.heartbeat_workers()
+    assert run(sh, "free /cache/f")[0] == 0
+    cluster.heartbeat_workers()
+    assert sh.fs.get_status("/cache/f", sync_interval_ms=-1).in_alluxio_percentage == 0
+    assert run(sh, "load /cache/f")[0] == 0
+    cluster.heartbeat_workers()
+    assert sh.fs.get_status("/cache/f").in_alluxio_percentage == 100
+    rc, out = run(sh, "location /cache/f")
+    assert "127.0.0.1" in out
+    assert run(sh, "getCapacityBytes")[1].startswith("Capacity Bytes: ")
+    assert run(sh, "getUsedBytes")[1].startswith("Used Bytes: ")
+    assert ":" in run(sh, "leader")[1]
+    assert "Current leader master" in run(sh, "masterInfo")[1]
+
+
+def test_mount_and_consistency(cluster, sh, tmp_path):
+    ufs = tmp_path / "mnt"
+    ufs.mkdir()
+    (ufs / "a.txt").write_text("abc")
+    assert run(sh, f"mount --readonly /mnt {ufs}")[0] == 0
+    assert "readonly" in run(sh, "mount")[1]
+    assert sh.fs.read_file("/mnt/a.txt") == b"abc"
+    (ufs / "b.txt").write_text("b")
+    assert run(sh, "loadMetadata -F /mnt")[0] == 0
+    assert sh.fs.exists("/mnt/b.txt")
+    os.remove(ufs / "b.txt")
+    rc, out = run(sh, "checkConsistency /mnt")
+    assert "/mnt/b.txt" in out
+    rc, out = run(sh, "checkConsistency -r /mnt")
+    assert "repaired /mnt/b.txt" in out
+    assert run(sh, "updateMount --shared /mnt")[0] == 0
+    assert run(sh, "unmount /mnt")[0] == 0
+    assert not sh.fs.exists("/mnt")
+
+
+def test_persist_and_distributed(cluster, sh):
+    sh.fs.write_file("/dist/f", b"p" * 1000, write_type="MUST_CACHE")
+    import threading
+    stop = threading.Event()
+
+    def pump():
+        while not stop.is_set():
+            cluster.drive_jobs()
+            cluster.master.fs_master.persistence_scheduler_heartbeat()
+            stop.wait(0.02)
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    try:
+        rc, out = run(sh, "persist --timeout 60s /dist/f")
+        assert rc == 0, out
+        assert sh.fs.get_status("/dist/f", sync_interval_ms=-1).is_persisted
+        rc, out = run(sh, "distributedCp /dist /dist2")
+        assert rc == 0, out
+        assert sh.fs.read_file("/dist2/f") == b"p" * 1000
+        rc, out = run(sh, "distributedMv /dist2 /dist3")
+        assert rc == 0, out
+        assert sh.fs.read_file("/dist3/f") == b"p" * 1000 and not sh.fs.exists("/dist2")
+        sh.fs.free("/dist3/f")
+        rc, out = run(sh, "distributedLoad /dist3")
+        assert rc == 0, out
+    finally:
+        stop.set()
+        t.join()
+    js = JobShell(Channel(cluster.master.address), io.StringIO())
+    assert js.run(["ls"]) == 0 and "migrate" in js.out.getvalue()
+    jid = int(js.out.getvalue().split()[0])
+    assert js.run(["stat", "-v", str(jid)]) == 0 and "Status:" in js.out.getvalue()
+
+
+def test_help_and_unknown(sh):
+    rc, out = run(sh, "help ls")
+    assert rc == 0 and "ls [" in out
+    rc, out = run(sh, "bogus")
+    assert rc == 1 and "unknown command" in out
+
+
+def test_fsadmin(cluster):
+    fs = cluster.client()
+    out = io.StringIO()
+    adm = FileSystemAdminShell(fs, out)
+    assert adm.run(["report"]) == 0 and "Live Workers: 2" in out.getvalue()
+    assert adm.run(["report", "capacity"]) == 0 and "Worker Name" in out.getvalue()
+    assert adm.run(["report", "metrics"]) == 0
+    assert adm.run(["report", "ufs"]) == 0 and " on / " in out.getvalue()
+    assert adm.run(["report", "jobservice"]) == 0 and "Task Pool Size" in out.getvalue()
+    assert adm.run(["doctor"]) == 0 and "All worker storage paths are in working state" in out.getvalue()
+    assert adm.run(["pathConf", "add", "--property", "alluxio.user.file.writetype.default=THROUGH", "/pc"]) == 0
+    out.truncate(0)
+    out.seek(0)
+    assert adm.run(["pathConf", "list"]) == 0 and "/pc" in out.getvalue()
+    assert adm.run(["pathConf", "show", "/pc"]) == 0 and "THROUGH" in out.getvalue()
+    assert adm.run(["pathConf", "remove", "/pc"]) == 0
+    fs.write_file("/adm/f", b"z", write_type="MUST_CACHE")
+    bid = fs.get_status("/adm/f").block_ids[0]
+    assert adm.run(["getBlockInfo", str(bid)]) == 0 and "/adm/f" in out.getvalue()
+    assert adm.run(["backup", str(cluster.work_dir), "--local"]) == 0 and "Backup URI" in out.getvalue()
+    assert adm.run(["checkpoint"]) == 0
+    assert adm.run(["metrics", "clear", "--master"]) == 0
+    fs.close()
+
+
+def test_run_tests_all_combinations(cluster):
+    from alluxio_amd.cli.test_runner import run_tests
+    fs = cluster.client()
+    out = io.StringIO()
+    failed = run_tests(fs, "/rt", out=out)
+    assert failed == 0, out.getvalue()
+    assert out.getvalue().count("Passed the test!") == 2 * 3 * 4
+    fs.close()
+
+
+def test_read_journal_and_launcher(cluster, tmp_path):
+    from alluxio_amd.cli.journal_tool import dump_journal
+    from alluxio_amd.cli.main import main
+    fs = cluster.client()
+    fs.create_directory("/journaled/dir", recursive=True)
+    fs.close()
+    jdir = cluster.conf.get("alluxio.master.journal.folder")
+    out = io.StringIO()
+    n = dump_journal(jdir, "FileSystemMaster", str(tmp_path / "dump"), out=out)
+    assert n > 0
+    assert "journaled" in (tmp_path / "dump" / "edits.txt").read_text()
+    out = io.StringIO()
+    assert main(["version"], out) == 0 and "version" in out.getvalue()
+    assert main(["getConf", "alluxio.worker.hbm.page.size"], out) == 0 and "2MB" in out.getvalue()
+    assert main(["validateConf"], out) == 0
+    assert main(["nope"], out) == 1
