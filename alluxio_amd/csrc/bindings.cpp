@@ -8,6 +8,7 @@
 
 #include "block_store.h"
 #include "cpu_codecs.h"
+#include "ipc.h"
 #include "kernels.h"
 
 namespace py = pybind11;
@@ -180,6 +181,8 @@ PYBIND11_MODULE(_C, m) {
       .def("write", &BlockStore::write, G(), py::arg("session"), py::arg("block_id"), py::arg("offset"),
            py::arg("src"), py::arg("length"), py::arg("src_kind"), py::arg("stream") = 0,
            py::arg("sync") = true)
+      .def("external_write", &BlockStore::external_write, G(), py::arg("session"), py::arg("block_id"),
+           py::arg("offset"), py::arg("length"))
       .def("commit_block", &BlockStore::commit_block, G(), py::arg("session"), py::arg("block_id"),
            py::arg("pin") = false)
       .def("abort_block", &BlockStore::abort_block, G())
@@ -268,6 +271,20 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- codecs / kernels ------------------------------------------------------------------
   m.def("device_count", &hip_device_count);
+
+  // ---- HIP IPC (short-circuit device reads) -------------------------------------------------
+  m.def("ipc_export", [](uint64_t ptr) {
+          IpcExport e = ipc_export(ptr);
+          return py::make_tuple(py::bytes(e.handle), e.offset, e.alloc_bytes);
+        }, py::arg("ptr"));
+  m.def("ipc_open", [](py::bytes handle, int device) {
+          std::string h = handle;
+          py::gil_scoped_release rel;
+          return ipc_open(h, device);
+        }, py::arg("handle"), py::arg("device"));
+  m.def("ipc_close", [](uint64_t base) { py::gil_scoped_release rel; ipc_close(base); });
+  m.def("enable_peer_access", &enable_peer_access, py::arg("device"), py::arg("peer"));
+  m.def("can_access_peer", &can_access_peer, py::arg("device"), py::arg("peer"));
   m.def("crc32c", [](py::bytes data, uint32_t crc) {
           std::string s = data;
           py::gil_scoped_release rel;

@@ -355,6 +355,26 @@ void BlockStore::request_space(int64_t session, int64_t block_id, uint64_t addit
     throw StoreError(kErrOutOfSpace, "cannot reserve " + std::to_string(additional) + " more bytes");
 }
 
+std::vector<int64_t> BlockStore::external_write(int64_t session, int64_t block_id, uint64_t offset,
+                                                uint64_t len) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(block_id);
+  if (!b || !b->temp) throw StoreError(kErrNotFound, "temp block " + std::to_string(block_id) + " not found");
+  if (b->session != session) throw StoreError(kErrInvalidState, "temp block owned by another session");
+  if (dirs_[b->dir]->spec.kind == DirKind::kFile)
+    throw StoreError(kErrInvalidArgument, "external writes need a memory (HBM/DRAM) dir");
+  if (offset + len > b->reserved) {
+    const uint64_t add = offset + len - b->reserved;
+    lk.unlock();
+    request_space(session, block_id, add);
+    lk.lock();
+    b = find(block_id);
+    if (!b || !b->temp) throw StoreError(kErrNotFound, "temp block vanished during reserve");
+  }
+  b->length = std::max(b->length, offset + len);
+  return b->pages;
+}
+
 void BlockStore::write(int64_t session, int64_t block_id, uint64_t offset, uint64_t src, uint64_t len,
                        int src_kind, uint64_t stream, bool sync) {
   if (len == 0) return;

@@ -137,6 +137,10 @@ class BlockStore {
                    uint64_t initial, bool evict, bool pin);
   void request_space(int64_t session, int64_t block_id, uint64_t additional);
   // Append/overwrite bytes of a temp block (auto-grows).  src_kind: MemKind.
+  // Reserve pages for [offset, offset+len) of a temp block and mark those bytes as written by
+  // an external producer (RCCL recv / peer DMA straight into the block's pages). Returns the
+  // page list so the caller can target the pages directly. Memory dirs only.
+  std::vector<int64_t> external_write(int64_t session, int64_t block_id, uint64_t offset, uint64_t len);
   void write(int64_t session, int64_t block_id, uint64_t offset, uint64_t src, uint64_t len,
              int src_kind, uint64_t stream, bool sync);
   void commit_block(int64_t session, int64_t block_id, bool pin);

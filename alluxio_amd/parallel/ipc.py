@@ -1,6 +1,80 @@
-"""HIP IPC export/import of HBM arenas (placeholder; filled in with the RCCL data plane)."""
+"""HIP IPC short-circuit reads of HBM blocks held by a same-node worker process.
+
+The reference short-circuit path (core/server/worker/.../grpc/ShortCircuitBlockReadHandler.java,
+core/client/fs/.../block/stream/LocalFileDataReader.java:58-70) gives a local client the block
+file path to mmap.  On MI355X the block lives in a worker's HBM arena, so the worker exports the
+arena allocation once as a HIP IPC handle (``OpenDeviceBlock`` returns handle + arena offset +
+the block's page list, with the block read-locked); the client maps the arena into its own
+address space and gathers the pages into its destination with the batched copy kernel running
+on *its* GPU — over xGMI when the worker owns a different GPU of the node.  No bytes cross the
+host or the RPC channel.
+"""
 from __future__ import annotations
 
+import threading
 
-def export_handle(tensor) -> bytes:
-    raise NotImplementedError
+from ..ops.native import lib
+
+
+def export_handle(tensor) -> tuple[bytes, int]:
+    """(IPC handle bytes, offset of the tensor's data inside the exported allocation)."""
+    handle, offset, _ = lib().ipc_export(tensor.data_ptr())
+    return bytes(handle), int(offset)
+
+
+class IpcMappings:
+    """Per-process cache of opened arena mappings keyed by (handle bytes, device)."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._maps: dict[tuple[bytes, int], int] = {}
+
+    def open(self, handle: bytes, device: int) -> int:
+        key = (bytes(handle), device)
+        with self._lock:
+            base = self._maps.get(key)
+            if base is None:
+                base = lib().ipc_open(key[0], device)
+                self._maps[key] = base
+            return base
+
+    def close_all(self) -> None:
+        with self._lock:
+            for base in self._maps.values():
+                lib().ipc_close(base)
+            self._maps.clear()
+
+
+MAPPINGS = IpcMappings()
+
+
+def page_segments(src_base: int, pages, page_size: int, offset: int, length: int, dst_ptr: int):
+    """Copy segments (src, dst, bytes) for bytes [offset, offset+length) of a paged block,
+    merging physically adjacent pages into one segment."""
+    segs = []
+    pos, end, dst = offset, offset + length, dst_ptr
+    while pos < end:
+        pi, po = divmod(pos, page_size)
+        take = min(page_size - po, end - pos)
+        src = src_base + pages[pi] * page_size + po
+        if segs and segs[-1][0] + segs[-1][2] == src and segs[-1][1] + segs[-1][2] == dst:
+            s = segs[-1]
+            segs[-1] = (s[0], s[1], s[2] + take)
+        else:
+            segs.append((src, dst, take))
+        pos += take
+        dst += take
+    return segs
+
+
+def gather_block(handle_msg, offset: int, length: int, dst_ptr: int, device: int, stream: int = 0) -> int:
+    """Copy part of a device block described by a ``DeviceBlockHandle`` into ``dst_ptr`` (device
+    memory of ``device``) with one batched-copy launch; returns bytes copied."""
+    if offset < 0 or offset + length > handle_msg.length:
+        raise ValueError(f"range [{offset}, {offset + length}) outside block of {handle_msg.length} bytes")
+    if not handle_msg.arena_ipc_handle:
+        raise RuntimeError("worker did not export an IPC handle for this block")
+    base = MAPPINGS.open(handle_msg.arena_ipc_handle, device) + handle_msg.arena_offset
+    segs = page_segments(base, list(handle_msg.pages), handle_msg.page_size, offset, length, dst_ptr)
+    lib().batched_copy(segs, stream, True)
+    return length

@@ -1,0 +1,211 @@
+"""Worker-to-worker block movement on one node: xGMI peer copies and RCCL collectives.
+
+Reference data movement between workers is a gRPC ``ReadBlock`` stream copied chunk by chunk
+(core/server/worker/.../block/RemoteBlockReader.java, AsyncCacheRequestManager.java:213-240,
+job/server/.../plan/replicate/ReplicateDefinition.java + JobUtils.loadBlock).  On an MI355X node
+every worker owns one GPU and the workers are ranks of one ``torch.distributed`` group, so:
+
+* **on-demand moves** (async cache from a peer, replicate, passive cache) are *pulls over xGMI*:
+  the destination asks the source for the block's device handle (``OpenDeviceBlock``: read lock +
+  HIP IPC handle of the source arena + page list), reserves its own pages
+  (``BlockStore.external_write``) and runs the batched page-gather kernel on its own GPU reading
+  the peer's HBM directly.  No host staging, no RPC payload, and — unlike RCCL send/recv — no
+  cross-process op ordering to get wrong: any number of pulls in any direction can be in flight.
+* **bulk moves where every worker participates** (replicate a dataset onto every GPU, the
+  ``distributedLoad --replication=all`` shape) are RCCL collectives: each rank contributes the
+  blocks it holds to one ``all_gather_into_tensor`` per round, so all xGMI links carry traffic at
+  once (C2/C4 in SURVEY §2.10).  Collectives are issued by every rank in the same order, so they
+  cannot deadlock.
+
+On CPU (gloo, DRAM tiers) pulls fall back to the gRPC block stream and collectives run on gloo,
+which keeps the whole control flow testable without GPUs.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+
+from ..proto import pb
+from ..utils import ids
+
+LOG = logging.getLogger(__name__)
+
+
+def _addr_key(addr) -> str:
+    if isinstance(addr, (tuple, list)):
+        return f"{addr[0]}:{addr[1]}"
+    if isinstance(addr, str):
+        return addr
+    return f"{addr.host}:{addr.rpcPort}"
+
+
+def cross_page_segments(src_base: int, src_pages, src_ps: int, dst_base: int, dst_pages, dst_ps: int,
+                        offset: int, length: int) -> list[tuple[int, int, int]]:
+    """(src_ptr, dst_ptr, nbytes) segments copying block bytes [offset, offset+length) between two
+    paged layouts (possibly different page sizes), merging runs contiguous on both sides."""
+    segs: list[tuple[int, int, int]] = []
+    pos, end = offset, offset + length
+    while pos < end:
+        spi, spo = divmod(pos, src_ps)
+        dpi, dpo = divmod(pos, dst_ps)
+        take = min(src_ps - spo, dst_ps - dpo, end - pos)
+        s = src_base + src_pages[spi] * src_ps + spo
+        d = dst_base + dst_pages[dpi] * dst_ps + dpo
+        if segs and segs[-1][0] + segs[-1][2] == s and segs[-1][1] + segs[-1][2] == d:
+            a, b, n = segs[-1]
+            segs[-1] = (a, b, n + take)
+        else:
+            segs.append((s, d, take))
+        pos += take
+    return segs
+
+
+class TransferPlane:
+    """Peer block mover bound to one worker (one rank of the node's worker group)."""
+
+    def __init__(self, worker, rank: int, world: int, addr_to_rank: dict[str, int], group=None):
+        import torch.distributed as dist
+        self.w = worker
+        self.rank = rank
+        self.world = world
+        self.group = group
+        self.addr_to_rank = dict(addr_to_rank)
+        self.rank_to_addr = {r: a for a, r in self.addr_to_rank.items()}
+        self.backend = dist.get_backend(group)
+        self._collective_lock = threading.Lock()
+        self.bytes_pulled = 0
+        self.bytes_gathered = 0
+
+    # ---- setup --------------------------------------------------------------------------------
+    @classmethod
+    def establish(cls, worker, group=None) -> "TransferPlane":
+        """Collective: every rank of ``group`` calls this once after its worker has started."""
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        allv = [None] * world
+        dist.all_gather_object(allv, _addr_key(worker.address), group=group)
+        plane = cls(worker, rank, world, {a: r for r, a in enumerate(allv)}, group)
+        worker.transfer_plane = plane
+        if plane.backend == "nccl":
+            import torch
+            from ..ops.native import lib
+            me = torch.cuda.current_device()
+            for d in range(torch.cuda.device_count()):
+                if d != me:
+                    try:
+                        lib().enable_peer_access(me, d)
+                    except Exception:  # noqa: BLE001
+                        LOG.debug("peer access %d->%d unavailable", me, d)
+        return plane
+
+    def rank_of(self, addr) -> int | None:
+        return self.addr_to_rank.get(_addr_key(addr))
+
+    def can_reach(self, addr) -> bool:
+        r = self.rank_of(addr)
+        return r is not None and r != self.rank
+
+    @property
+    def device_plane(self) -> bool:
+        """Pulls go GPU-to-GPU (IPC-mapped peer arena + copy kernel) when this worker has an HBM
+        tier; independent of the collective backend, so gloo-coordinated workers sharing one
+        GPU use it too."""
+        return bool(self.w.store.has_device_tier) and self.w.conf.get_bool("alluxio.worker.ipc.enabled", "true")
+
+    # ---- on-demand pulls ------------------------------------------------------------------------
+    def pull_block(self, block_id: int, src, length: int, tier: int = 0, medium: str = "") -> int:
+        """Copy ``block_id`` from peer worker ``src`` into this worker; returns bytes moved."""
+        if self.w.has_block(block_id):
+            return 0
+        if not self.can_reach(src):
+            raise ValueError(f"worker {_addr_key(src)} is not a peer in this transfer group")
+        host, port = _addr_key(src).rsplit(":", 1)
+        if not self.device_plane:
+            from ..worker.remote import remote_block_fetcher
+            remote_block_fetcher(self.w, host, int(port), length)(block_id)
+            self.bytes_pulled += length
+            return length
+        from ..ops.native import lib
+        from .ipc import MAPPINGS
+        stub = self.w.peer_stub(_addr_key(src))
+        session = ids.create_session_id()
+        h = stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session))
+        try:
+            if not h.arena_ipc_handle:
+                raise RuntimeError(f"peer {_addr_key(src)} holds block {block_id} outside its HBM tier")
+            n = h.length
+            self.w.create_block(session, block_id, tier, medium, max(n, 1))
+            try:
+                dst_pages = self.w.native.external_write(session, block_id, 0, n)
+                _p, d, dps, dbase = self.w.native.block_pages(block_id)
+                import torch
+                dev = self.w.store.device
+                src_base = MAPPINGS.open(h.arena_ipc_handle, dev) + h.arena_offset
+                segs = cross_page_segments(src_base, list(h.pages), h.page_size, dbase, list(dst_pages), dps, 0, n)
+                with torch.cuda.device(dev):   # the copy kernel runs on this worker's GPU, reading the peer
+                    lib().batched_copy(segs, 0, True)
+                self.w.commit_block(session, block_id)
+            except Exception:
+                self.w.abort_block(session, block_id)
+                raise
+        finally:
+            stub.UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(block_id=block_id, lock_id=h.lock_id,
+                                                                     session_id=session))
+        self.bytes_pulled += n
+        return n
+
+    def serve(self, req) -> None:
+        """``PeerTransfer`` RPC: the requester (the block's holder, ``src_rank``) asks this worker to
+        pull the block — used to fan a freshly written block out to replicas in parallel."""
+        src = self.rank_to_addr.get(req.src_rank)
+        if src is None:
+            raise ValueError(f"unknown source rank {req.src_rank}")
+        self.pull_block(req.block_id, src, req.length)
+
+    # ---- collectives ----------------------------------------------------------------------------
+    def replicate_all(self, blocks: list[tuple[int, int, int]]) -> int:
+        """Collective: ``blocks`` = [(block_id, length, owner_rank)], identical on every rank.
+        Afterwards every rank's worker holds every block.  One ``all_gather_into_tensor`` per
+        round moves one block from each owner to everyone (rounds = max blocks per owner)."""
+        import torch
+        import torch.distributed as dist
+        by_owner: dict[int, list[tuple[int, int]]] = {r: [] for r in range(self.world)}
+        for bid, length, owner in blocks:
+            by_owner[owner].append((bid, length))
+        rounds = max((len(v) for v in by_owner.values()), default=0)
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+        moved = 0
+        with self._collective_lock:
+            for k in range(rounds):
+                entries = [by_owner[r][k] if k < len(by_owner[r]) else (None, 0) for r in range(self.world)]
+                shard = max(n for _, n in entries)
+                if shard == 0:
+                    continue
+                send = torch.zeros(shard, dtype=torch.uint8, device=dev)
+                mine = entries[self.rank]
+                if mine[0] is not None:
+                    self._copy_block_out(mine[0], mine[1], send)
+                out = torch.empty(shard * self.world, dtype=torch.uint8, device=dev)
+                dist.all_gather_into_tensor(out, send, group=self.group)
+                for r, (bid, n) in enumerate(entries):
+                    if bid is None or r == self.rank or self.w.has_block(bid):
+                        continue
+                    self._store_block(bid, out[r * shard:r * shard + n])
+                    moved += n
+        self.bytes_gathered += moved
+        return moved
+
+    def _copy_block_out(self, block_id: int, n: int, dst) -> None:
+        kind = 1 if dst.is_cuda else 0
+        self.w.read(block_id, 0, n, dst.data_ptr(), kind, 0, sync=True)
+
+    def _store_block(self, block_id: int, src) -> None:
+        session = ids.create_session_id()
+        n = src.numel()
+        self.w.create_block(session, block_id, 0, "", max(n, 1))
+        try:
+            self.w.write_ptr(session, block_id, 0, src.data_ptr(), n, 1 if src.is_cuda else 0)
+            self.w.commit_block(session, block_id)
+        except Exception:
+            self.w.abort_block(session, block_id)
+            raise

@@ -41,7 +41,7 @@ msg ClearMetricsResponse
 msg PageRun first_page=1:i64 num_pages=2:i64
 msg DeviceBlockHandle block_id=1:i64 length=2:i64 page_size=3:i64 pages=4:i64*
     arena_ipc_handle=5:bytes arena_bytes=6:i64 device=7:i32 lock_id=8:i64 crc32c=9:u32*
-    node_id=10:str pid=11:i32
+    node_id=10:str pid=11:i32 arena_offset=12:i64
 msg OpenDeviceBlockRequest block_id=1:i64 promote=2:bool session_id=3:i64
 msg UnlockDeviceBlockRequest block_id=1:i64 lock_id=2:i64 session_id=3:i64
 msg UnlockDeviceBlockResponse

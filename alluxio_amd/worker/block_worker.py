@@ -77,6 +77,9 @@ class BlockWorker:
         self.persisted_files: list[int] = []
         self._block_master = None
         self._fs_master = None
+        self.transfer_plane = None   # parallel.transfer.TransferPlane when ranks form a node group
+        self._peer_channels: dict = {}
+        self._peer_lock = threading.Lock()
         self.crc_enabled = conf.get_bool("alluxio.worker.data.crc.enabled")
         self.crc: dict[int, list[int]] = {}
         self._install_gauges()
@@ -91,6 +94,24 @@ class BlockWorker:
         if self._fs_master is None and self.master_channel is not None:
             self._fs_master = self.master_channel.stub("alluxio.grpc.file.FileSystemMasterWorkerService")
         return self._fs_master
+
+    def peer_stub(self, address: str):
+        """BlockWorker stub of another worker (pooled channels)."""
+        from ..rpc import Channel
+        with self._peer_lock:
+            ch = self._peer_channels.get(address)
+            if ch is None:
+                ch = self._peer_channels[address] = Channel(address)
+        return ch.stub("alluxio.grpc.block.BlockWorker")
+
+    def peer_fetcher(self, host: str, port: int, length: int | None):
+        """Block source for async caching from a peer: xGMI pull through the transfer plane when
+        the peer is in this node's worker group, else the gRPC block stream."""
+        plane = self.transfer_plane
+        if plane is not None and plane.can_reach((host, port)):
+            return lambda block_id: plane.pull_block(block_id, (host, port), length or 0)
+        from .remote import remote_block_fetcher
+        return remote_block_fetcher(self, host, port, length)
 
     def _install_gauges(self) -> None:
         m = self.metrics

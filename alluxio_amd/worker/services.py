@@ -231,8 +231,7 @@ class BlockWorkerService:
     def AsyncCache(self, req, ctx):
         src = None
         if req.source_host and (req.source_host, req.source_port) != (self.w.address.host, self.w.address.dataPort):
-            from .remote import remote_block_fetcher
-            src = remote_block_fetcher(self.w, req.source_host, req.source_port, req.length)
+            src = self.w.peer_fetcher(req.source_host, req.source_port, req.length)
         opts = req.open_ufs_block_options if req.HasField("open_ufs_block_options") else None
         if opts is not None and not opts.block_size and req.length:
             opts.block_size = req.length
@@ -265,7 +264,7 @@ class BlockWorkerService:
                                            arena_bytes=arena.nbytes, device=arena.device, lock_id=lock_id,
                                            pid=os.getpid())
             try:
-                h.arena_ipc_handle = arena.ipc_handle()
+                h.arena_ipc_handle, h.arena_offset = arena.ipc_handle()
             except Exception:  # noqa: BLE001
                 LOG.debug("IPC export unavailable", exc_info=True)
             if req.block_id in self.w.crc:

@@ -47,12 +47,15 @@ class Arena:
     def view(self, offset: int, nbytes: int):
         return self.tensor[offset:offset + nbytes]
 
-    def ipc_handle(self) -> bytes:
-        """HIP IPC handle of the arena allocation (short-circuit export to same-node processes)."""
+    def ipc_handle(self) -> tuple[bytes, int]:
+        """(HIP IPC handle of the arena's allocation, arena offset inside it) — exported once
+        and cached (short-circuit export to same-node processes)."""
         if self.kind != "hbm":
             raise ValueError("only device arenas can be exported over HIP IPC")
-        from ..parallel.ipc import export_handle
-        return export_handle(self.tensor)
+        if getattr(self, "_ipc", None) is None:
+            from ..parallel.ipc import export_handle
+            self._ipc = export_handle(self.tensor)
+        return self._ipc
 
 
 class DirConfig:

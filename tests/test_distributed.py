@@ -104,3 +104,92 @@ def test_bench_cpu_smoke(tmp_path, capsys):
               "vs_baseline", "dtype", "data", "config"):
         assert k in out
     assert out["config"]["verified"] and out["value"] > 0
+
+
+PLANE_SCRIPT = r"""
+import os, sys, json
+sys.path.insert(0, %(root)r)
+import numpy as np, torch, torch.distributed as dist
+from alluxio_amd.conf import Configuration
+from alluxio_amd.master.process import AlluxioMasterProcess
+from alluxio_amd.worker.process import AlluxioWorkerProcess
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.parallel.transfer import TransferPlane
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=world)
+work = %(work)r
+conf = Configuration({"alluxio.master.journal.folder": work + "/journal",
+    "alluxio.worker.tieredstore.level0.dirs.path": "dram", "alluxio.worker.tieredstore.level0.dirs.quota": "128MB",
+    "alluxio.worker.hbm.page.size": "1MB", "alluxio.user.block.size.bytes.default": "4MB"})
+box = [None]
+if rank == 0:
+    m = AlluxioMasterProcess(conf, host="127.0.0.1", port=0, root_ufs=work + "/ufs"); box[0] = m.start(start_heartbeats=False)
+dist.broadcast_object_list(box, src=0)
+w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, work_dir=work + "/w%%d" %% rank)
+w.start(start_heartbeats=False)
+plane = TransferPlane.establish(w.worker)
+fs = FileSystem(conf=conf.copy(), master_address=box[0])
+sizes = [9 * (1 << 20) + 7, 5 * (1 << 20) + 1]
+data = np.random.default_rng(10 + rank).integers(0, 256, sizes[rank %% 2], dtype=np.uint8)
+fs.write_file("/plane/f%%d" %% rank, data, write_type="MUST_CACHE")
+st = fs.get_status("/plane/f%%d" %% rank)
+mine = [(b.blockInfo.blockId, b.blockInfo.length, rank) for b in st.info.fileBlockInfos]
+allb = [None] * world
+dist.all_gather_object(allb, mine)
+blocks = [x for part in allb for x in part]
+moved = plane.replicate_all(blocks)
+ok_all = all(w.worker.has_block(b) for b, _, _ in blocks)
+# bytes of the other rank's first block now readable from this worker's own store
+other = (rank + 1) %% world
+odata = np.random.default_rng(10 + other).integers(0, 256, sizes[other %% 2], dtype=np.uint8)
+ob, olen, _ = allb[other][0]
+ok_bytes = w.worker.read_bytes(ob, 0, olen) == odata[:olen].tobytes()
+dist.barrier()
+w.sync.heartbeat()
+dist.barrier()
+locs = len(fs.get_status("/plane/f%%d" %% other).info.fileBlockInfos[0].blockInfo.locations)
+# on-demand pull of a block that only the peer holds (gRPC fallback on CPU)
+fs.write_file("/plane/g%%d" %% rank, data[:(1 << 20) + 3], write_type="MUST_CACHE")
+dist.barrier()
+g = fs.get_status("/plane/g%%d" %% other).info.fileBlockInfos[0].blockInfo
+pulled = plane.pull_block(g.blockId, g.locations[0].workerAddress, g.length)
+ok_pull = w.worker.read_bytes(g.blockId, 0, g.length) == odata[:(1 << 20) + 3].tobytes()
+print(json.dumps({"rank": rank, "all": ok_all, "bytes": bool(ok_bytes), "moved": moved, "locs": locs,
+                  "pulled": pulled, "pull_ok": bool(ok_pull), "reach": plane.can_reach(g.locations[0].workerAddress)}), flush=True)
+dist.barrier()
+fs.close(); w.stop()
+dist.barrier()
+if rank == 0:
+    m.stop()
+dist.destroy_process_group()
+"""
+
+
+def test_transfer_plane_gloo(tmp_path):
+    script = PLANE_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path)}
+    path = tmp_path / "plane.py"
+    path.write_text(script)
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, str(path)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            pytest.fail("transfer plane rank timed out")
+        assert p.returncode == 0, err[-3000:]
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+    for o in outs:
+        assert o["all"] and o["bytes"] and o["pull_ok"] and o["reach"], o
+        assert o["locs"] == 2 and o["pulled"] > 0 and o["moved"] > 0, o
+
+
+def test_cross_page_segments():
+    from alluxio_amd.parallel.transfer import cross_page_segments
+    # src pages of 4 bytes [2, 3] (contiguous), dst pages of 2 bytes [0, 5, 6, 7]
+    segs = cross_page_segments(100, [2, 3], 4, 1000, [0, 5, 6, 7], 2, 0, 8)
+    assert segs == [(108, 1000, 2), (110, 1010, 6)]

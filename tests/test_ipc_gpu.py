@@ -1,0 +1,151 @@
+"""HIP IPC short-circuit reads across processes on one MI355X.
+
+A child process runs master + worker with an HBM tier and caches a file; this (client) process
+has no worker of its own, so reads of that file go through ``OpenDeviceBlock`` + the IPC-mapped
+arena + this process's batched copy kernel.  Compared against the bytes the child wrote
+(reference analogue: short-circuit read tests, tests/.../client/fs/LocalBlockInStreamIntegrationTest).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SERVER = r"""
+import os, sys, json
+sys.path.insert(0, %(root)r)
+import torch
+import numpy as np
+from alluxio_amd.minicluster import LocalAlluxioCluster
+conf = {"alluxio.worker.tieredstore.level0.dirs.path": "hbm:0", "alluxio.worker.tieredstore.level0.dirs.quota": "256MB",
+        "alluxio.worker.hbm.page.size": "1MB", "alluxio.user.block.size.bytes.default": "8MB"}
+with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=%(work)r) as c:
+    fs = c.client()
+    data = np.random.default_rng(7).integers(0, 256, 20 * (1 << 20) + 333, dtype=np.uint8)
+    fs.write_file("/ipc/f", data, write_type="MUST_CACHE")
+    print(json.dumps({"master": c.master.address}), flush=True)
+    sys.stdin.readline()
+    fs.close()
+"""
+
+
+@pytest.mark.gpu
+def test_ipc_read_from_other_process(gpu, tmp_path):
+    import torch
+
+    from alluxio_amd.client.file_system import FileSystem
+    from alluxio_amd.conf import Configuration
+    script = tmp_path / "server.py"
+    script.write_text(SERVER % {"root": ROOT, "work": str(tmp_path / "work")})
+    p = subprocess.Popen([sys.executable, str(script)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        line = p.stdout.readline()
+        assert line, p.stderr.read()[-3000:]
+        master = json.loads(line)["master"]
+        expect = np.random.default_rng(7).integers(0, 256, 20 * (1 << 20) + 333, dtype=np.uint8)
+        fs = FileSystem(conf=Configuration({"alluxio.user.file.passive.cache.enabled": "false"}),
+                        master_address=master)
+        dst = torch.empty(len(expect), dtype=torch.uint8, device="cuda")
+        with fs.open_file("/ipc/f") as f:
+            n = f.read_into(dst)
+            assert f._reader is not None and f._reader.source == "ipc"
+        torch.cuda.synchronize()
+        assert n == len(expect)
+        assert np.array_equal(dst.cpu().numpy(), expect)
+        # unaligned positioned read into a host buffer through the same mapping
+        host = np.empty(3 << 20, dtype=np.uint8)
+        with fs.open_file("/ipc/f") as f:
+            assert f.pread(5 * (1 << 20) + 17, host) == len(host)
+        assert np.array_equal(host, expect[5 * (1 << 20) + 17:5 * (1 << 20) + 17 + len(host)])
+        fs.close()
+    finally:
+        p.stdin.write("\n")
+        p.stdin.flush()
+        try:
+            p.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+
+
+def test_page_segments_merge_adjacent():
+    from alluxio_amd.parallel.ipc import page_segments
+    segs = page_segments(1000, [0, 1, 5], 100, 50, 200, 0)
+    # bytes 50..150 from pages 0,1 (adjacent -> one seg), 150..250 page1 tail + page 5 head
+    assert segs == [(1050, 0, 150), (1500, 150, 50)]
+
+
+PLANE = r"""
+import os, sys, json
+sys.path.insert(0, %(root)r)
+import numpy as np, torch, torch.distributed as dist
+from alluxio_amd.conf import Configuration
+from alluxio_amd.master.process import AlluxioMasterProcess
+from alluxio_amd.worker.process import AlluxioWorkerProcess
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.parallel.transfer import TransferPlane
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=world)
+work = %(work)r
+conf = Configuration({"alluxio.master.journal.folder": work + "/journal",
+    "alluxio.worker.tieredstore.level0.dirs.path": "hbm:0", "alluxio.worker.tieredstore.level0.dirs.quota": "256MB",
+    "alluxio.worker.hbm.page.size": "1MB", "alluxio.user.block.size.bytes.default": "8MB"})
+box = [None]
+if rank == 0:
+    m = AlluxioMasterProcess(conf, host="127.0.0.1", port=0, root_ufs=work + "/ufs"); box[0] = m.start(start_heartbeats=False)
+dist.broadcast_object_list(box, src=0)
+w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, device=0, work_dir=work + "/w%%d" %% rank)
+w.start(start_heartbeats=False)
+plane = TransferPlane.establish(w.worker)
+fs = FileSystem(conf=conf.copy(), master_address=box[0])
+n = 20 * (1 << 20) + 11
+data = np.random.default_rng(20 + rank).integers(0, 256, n, dtype=np.uint8)
+fs.write_file("/gp/f%%d" %% rank, data, write_type="MUST_CACHE")
+dist.barrier()
+other = (rank + 1) %% world
+odata = np.random.default_rng(20 + other).integers(0, 256, n, dtype=np.uint8)
+st = fs.get_status("/gp/f%%d" %% other).info
+ok = True
+pulled = 0
+for i, fbi in enumerate(st.fileBlockInfos):
+    b = fbi.blockInfo
+    pulled += plane.pull_block(b.blockId, b.locations[0].workerAddress, b.length)
+    got = w.worker.read_bytes(b.blockId, 0, b.length)
+    ok = ok and got == odata[i * (8 << 20):i * (8 << 20) + b.length].tobytes()
+dist.barrier()
+print(json.dumps({"rank": rank, "ok": bool(ok), "pulled": pulled, "device_plane": plane.device_plane}), flush=True)
+dist.barrier()
+fs.close(); w.stop()
+dist.barrier()
+if rank == 0:
+    m.stop()
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.gpu
+def test_transfer_plane_device_pull(gpu, tmp_path):
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    path = tmp_path / "plane.py"
+    path.write_text(PLANE % {"root": ROOT, "port": port, "work": str(tmp_path)})
+    procs = [subprocess.Popen([sys.executable, str(path)], env=dict(os.environ, RANK=str(r), WORLD_SIZE="2"),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            pytest.fail("device pull rank timed out")
+        assert p.returncode == 0, err[-3000:]
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+    for o in outs:
+        assert o["ok"] and o["device_plane"] and o["pulled"] == 20 * (1 << 20) + 11, o
