@@ -166,6 +166,9 @@ _k("USER_READ_BATCH_SIZE", "alluxio.user.read.batch.size", "256", Scope.CLIENT,
 _k("USER_FILE_READ_DEVICE", "alluxio.user.file.read.device", "cuda", Scope.CLIENT,
    "Preferred destination of client reads: cuda (HBM) or cpu (pinned host).")
 
+_k("WEB_SERVER_ENABLED", "alluxio.web.server.enabled", "true", Scope.SERVER,
+   "Serve the HTTP endpoints (/metrics/json, /metrics/prometheus, /api/v1/...) from master and "
+   "worker processes.")
 _k("JOB_MASTER_EMBEDDED_ENABLED", "alluxio.job.master.embedded.enabled", "true", Scope.MASTER,
    "Serve the job master from the file-system master process (same RPC port) instead of a "
    "separate job-master process.")

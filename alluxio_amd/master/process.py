@@ -107,6 +107,8 @@ class AlluxioMasterProcess:
                                         self.conf.get_int("alluxio.job.master.job.capacity"))
         self._job_client_fs = None
         self.web = None
+        self.web_port = 0
+        self.start_time = time.time()
         self.started = False
         self.primary = False
 
@@ -178,6 +180,13 @@ class AlluxioMasterProcess:
         self._register_services()
         addr = self.server.start()
         self.meta_master.master_address = addr
+        self.start_time = time.time()
+        if self.conf.get_bool("alluxio.web.server.enabled", "true"):
+            from ..web import WebServer, master_routes
+            self.web = WebServer(self.conf.get("alluxio.master.web.bind.host", "0.0.0.0"),
+                                 self.conf.get_int("alluxio.master.web.port"), master_routes(self), "master")
+            self.web_port = self.web.start()
+            self.meta_master.web_port = self.web_port
         if start_heartbeats and primary:
             self._start_heartbeats()
         self.started = True
@@ -246,6 +255,7 @@ class AlluxioMasterProcess:
         self._threads.clear()
         if self.web is not None:
             self.web.stop()
+            self.web = None
         self.server.stop()
         if self._job_client_fs is not None:
             self._job_client_fs.close()

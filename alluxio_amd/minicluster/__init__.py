@@ -28,6 +28,10 @@ DEFAULTS = {
     "alluxio.security.authorization.permission.enabled": "false",
     "alluxio.user.file.writetype.default": "CACHE_THROUGH",
     "alluxio.worker.network.async.cache.manager.threads.max": "4",
+    "alluxio.master.web.port": "0",
+    "alluxio.worker.web.port": "0",
+    "alluxio.master.web.bind.host": "127.0.0.1",
+    "alluxio.worker.web.bind.host": "127.0.0.1",
 }
 
 

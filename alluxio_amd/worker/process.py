@@ -107,6 +107,8 @@ class AlluxioWorkerProcess:
         self._threads: list[hb.HeartbeatThread] = []
         self.job_worker = None
         self._job_fs = None
+        self.web = None
+        self.web_port = 0
 
     @property
     def address(self) -> str:
@@ -120,6 +122,12 @@ class AlluxioWorkerProcess:
         self.worker.address = pb.grpc.WorkerNetAddress(host=host, rpcPort=int(port), dataPort=int(port),
                                                        webPort=0, tieredIdentity=ti,
                                                        containerHost=socket.gethostname())
+        if self.conf.get_bool("alluxio.web.server.enabled", "true"):
+            from ..web import WebServer, worker_routes
+            self.web = WebServer(self.conf.get("alluxio.worker.web.bind.host", "0.0.0.0"),
+                                 self.conf.get_int("alluxio.worker.web.port"), worker_routes(self), "worker")
+            self.web_port = self.web.start()
+            self.worker.address.webPort = self.web_port
         from ..client.context import register_local_worker
         register_local_worker(addr, self.worker)
         if register:
@@ -209,6 +217,9 @@ class AlluxioWorkerProcess:
         if self.server.address:
             unregister_local_worker(self.server.address)
         self.server.stop()
+        if self.web is not None:
+            self.web.stop()
+            self.web = None
         if self.job_worker is not None:
             self.job_worker.close()
         if self._job_fs is not None:

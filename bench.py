@@ -88,6 +88,10 @@ def main(argv=None):
         "alluxio.user.block.size.bytes.default": str(block_size),
         "alluxio.user.file.writetype.default": "CACHE_THROUGH",
         "alluxio.user.block.write.location.policy.class": "alluxio.client.block.policy.LocalFirstPolicy",
+        "alluxio.master.web.port": "0",
+        "alluxio.worker.web.port": "0",
+        "alluxio.master.web.bind.host": "127.0.0.1",
+        "alluxio.worker.web.bind.host": "127.0.0.1",
         "alluxio.user.metadata.cache.enabled": "true",
         "alluxio.security.authorization.permission.enabled": "false",
         "alluxio.master.worker.connect.wait.time": "0sec",

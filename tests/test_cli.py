@@ -243,3 +243,26 @@ def test_read_journal_and_launcher(cluster, tmp_path):
     assert main(["getConf", "alluxio.worker.hbm.page.size"], out) == 0 and "2MB" in out.getvalue()
     assert main(["validateConf"], out) == 0
     assert main(["nope"], out) == 1
+
+
+def test_web_endpoints(cluster):
+    import json
+    import urllib.request
+    port = cluster.master.web_port
+    base = f"http://127.0.0.1:{port}"
+    info = json.loads(urllib.request.urlopen(base + "/api/v1/master/get_info", timeout=10).read())
+    assert len(info["workers"]) == 2 and "/" in info["mountPoints"] and info["primary"]
+    m = json.loads(urllib.request.urlopen(base + "/metrics/json", timeout=10).read())
+    assert "counters" in m and "gauges" in m
+    prom = urllib.request.urlopen(base + "/metrics/prometheus", timeout=10).read().decode()
+    assert "# TYPE" in prom
+    req = urllib.request.Request(base + "/api/v1/master/log_level?logName=alluxio_amd.test&level=DEBUG", method="POST")
+    assert json.loads(urllib.request.urlopen(req, timeout=10).read())["level"] == "DEBUG"
+    w = cluster.workers[0]
+    winfo = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{w.web_port}/api/v1/worker/get_info",
+                                              timeout=10).read())
+    assert winfo["dirs"] and winfo["dirs"][0]["medium"] in ("DRAM", "HBM")
+    from alluxio_amd.cli.main import main
+    out = io.StringIO()
+    assert main(["logLevel", "--logName", "x.y", "--level", "INFO", "--target", f"127.0.0.1:{port}"], out) == 0
+    assert "INFO" in out.getvalue()
