@@ -382,6 +382,18 @@ class FileSystemMaster(Journaled):
                       persistence_wait_ms: int = 0) -> None:
         path = normalize_path(path)
         self._count("Master.FilesCompleted")
+        # UFS fingerprint of a persisted file is fetched before the tree write lock (UFS latency
+        # must not stall the namespace; the proxy-backed S3 UFS even calls back into this master)
+        pre_fp = None
+        with self.tree.lock.read():
+            chain, missing = self.tree.resolve(path)
+            persisted = not missing and chain[-1].is_file and chain[-1].is_persisted
+        if persisted:
+            try:
+                res = self._resolve_ufs(path)
+                pre_fp = res.ufs.get_fingerprint(res.uri)
+            except Exception:  # noqa: BLE001
+                pre_fp = Fingerprint.INVALID
         with RpcContext(self) as rpc, self.tree.lock.write():
             chain, missing = self.tree.resolve(path)
             if missing:
@@ -404,13 +416,7 @@ class FileSystemMaster(Journaled):
             length = ufs_length if f.is_persisted else in_alluxio
             if length < 0:
                 raise InvalidArgumentException(f"File {f.name} cannot have negative length: {length}")
-            fingerprint = Fingerprint.INVALID
-            if f.is_persisted:
-                try:
-                    res = self._resolve_ufs(path)
-                    fingerprint = res.ufs.get_fingerprint(res.uri)
-                except Exception:  # noqa: BLE001
-                    fingerprint = Fingerprint.INVALID
+            fingerprint = pre_fp if (f.is_persisted and pre_fp is not None) else Fingerprint.INVALID
             blocks = []
             remaining, seq = length, 0
             while remaining > 0:
@@ -747,6 +753,7 @@ class FileSystemMaster(Journaled):
         if not ufs.is_directory(ufs_uri):
             raise InvalidPathException(f"Ufs path {ufs_uri} does not exist or is not a directory")
         mount_id = ids.create_mount_id()
+        st = ufs.get_status(ufs_uri)  # UFS I/O stays outside the tree lock
         with RpcContext(self) as rpc, self.tree.lock.write():
             chain, missing = self.tree.resolve(alluxio_path)
             if not missing:
@@ -758,7 +765,6 @@ class FileSystemMaster(Journaled):
             info = MountInfo(alluxio_path, ufs_uri, mount_id, read_only, shared, properties)
             self._apply(rpc, info.to_entry())
             owner, group = self._owner_group()
-            st = ufs.get_status(ufs_uri)
             mode = st.mode if st is not None else 0o755
             for e in self.tree.new_directory_entries(parent, missing[0], st.owner or owner if st else owner,
                                                     st.group or group if st else group, mode, True,

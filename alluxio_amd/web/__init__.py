@@ -73,7 +73,8 @@ class WebServer:
         return self.httpd.server_address[1]
 
     def start(self) -> int:
-        self._t = threading.Thread(target=self.httpd.serve_forever, name=f"{self.name}-http", daemon=True)
+        self._t = threading.Thread(target=self.httpd.serve_forever, kwargs={"poll_interval": 0.05},
+                                   name=f"{self.name}-http", daemon=True)
         self._t.start()
         return self.port
 
