@@ -53,8 +53,11 @@ class FileSystemContext:
     def __init__(self, conf: Configuration | None = None, master_address: str | None = None,
                  user: str | None = None):
         self.conf = conf or Configuration(load_site=True)
-        self.master_address = master_address or "{}:{}".format(
+        addrs = master_address or self.conf.get_raw("alluxio.master.rpc.addresses") or "{}:{}".format(
             self.conf.get("alluxio.master.hostname", "127.0.0.1"), self.conf.get_int("alluxio.master.rpc.port"))
+        self.master_addresses = [a.strip() for a in str(addrs).split(",") if a.strip()]
+        self.master_address = self.master_addresses[0]
+        self._master_ch = None
         self.user = user or login_user(self.conf)
         self.pool = ChannelPool()
         self.metrics = msys.metrics("Client")
@@ -67,7 +70,14 @@ class FileSystemContext:
 
     # ---- stubs --------------------------------------------------------------------------------
     def master_channel(self):
-        return self.pool.get(self.master_address, self.user)
+        """Channel to the (primary) master; an HA address list yields a failover channel."""
+        if len(self.master_addresses) == 1:
+            return self.pool.get(self.master_address, self.user)
+        if self._master_ch is None:
+            from ..rpc import FailoverChannel
+            self._master_ch = FailoverChannel(self.master_addresses, self.user, self.pool,
+                                              self.conf.get_ms("alluxio.user.rpc.retry.max.duration", "2min") / 1000)
+        return self._master_ch
 
     def fs_master(self):
         return self.master_channel().stub(SVC_FS)

@@ -166,6 +166,11 @@ _k("USER_READ_BATCH_SIZE", "alluxio.user.read.batch.size", "256", Scope.CLIENT,
 _k("USER_FILE_READ_DEVICE", "alluxio.user.file.read.device", "cuda", Scope.CLIENT,
    "Preferred destination of client reads: cuda (HBM) or cpu (pinned host).")
 
+_k("MASTER_HA_PRIMARY_SELECTOR", "alluxio.master.ha.primary.selector", "NONE", Scope.MASTER,
+   "NONE (single master) or FILE_LOCK (HA: masters sharing the journal folder elect a primary "
+   "with an exclusive lock on alluxio.master.ha.lock.file).")
+_k("MASTER_HA_LOCK_FILE", "alluxio.master.ha.lock.file", "${alluxio.master.journal.folder}/.primary.lock",
+   Scope.MASTER, "Election lock file for FILE_LOCK primary selection.")
 _k("WEB_SERVER_ENABLED", "alluxio.web.server.enabled", "true", Scope.SERVER,
    "Serve the HTTP endpoints (/metrics/json, /metrics/prometheus, /api/v1/...) from master and "
    "worker processes.")

@@ -107,6 +107,7 @@ class AlluxioMasterProcess:
                                         self.conf.get_int("alluxio.job.master.job.capacity"))
         self._job_client_fs = None
         self.web = None
+        self.selector = None
         self.web_port = 0
         self.start_time = time.time()
         self.started = False
@@ -170,14 +171,25 @@ class AlluxioMasterProcess:
         self.journal.format()
 
     def start(self, primary: bool = True, start_heartbeats: bool = True) -> str:
+        """Single master: become primary now.  HA (``alluxio.master.ha.primary.selector`` =
+        FILE_LOCK): start as a standby tailing the journal behind an RPC gate that answers
+        UNAVAILABLE, and gain primacy when elected (FaultTolerantAlluxioMasterProcess)."""
         if not self.journal.is_formatted() and isinstance(self.journal, UfsJournalSystem):
             self.journal.format()
         self.journal.start()
-        if primary:
+        ha = self.conf.get("alluxio.master.ha.primary.selector", "NONE").upper() == "FILE_LOCK"
+        if primary and not ha:
             self.gain_primacy()
         if self.job_master is not None and self.fs_master.persist_handler is None:
             self.fs_master.persist_handler = self._persist_via_job
         self._register_services()
+        if ha:
+            from ..utils.exceptions import UnavailableException
+
+            def standby_gate(spec):
+                if not self.primary:
+                    raise UnavailableException("master is a standby (not primary)")
+            self.server.gate = standby_gate
         addr = self.server.start()
         self.meta_master.master_address = addr
         self.start_time = time.time()
@@ -187,7 +199,16 @@ class AlluxioMasterProcess:
                                  self.conf.get_int("alluxio.master.web.port"), master_routes(self), "master")
             self.web_port = self.web.start()
             self.meta_master.web_port = self.web_port
-        if start_heartbeats and primary:
+        if ha:
+            from .ha import FileLockPrimarySelector
+            self.selector = FileLockPrimarySelector(self.conf.get("alluxio.master.ha.lock.file"))
+
+            def on_primary():
+                self.gain_primacy()
+                if start_heartbeats:
+                    self._start_heartbeats()
+            self.selector.start(on_primary)
+        elif start_heartbeats and primary:
             self._start_heartbeats()
         self.started = True
         LOG.info("master serving at %s", addr)
@@ -248,6 +269,9 @@ class AlluxioMasterProcess:
             self.journal.checkpoint()
 
     def stop(self) -> None:
+        if self.selector is not None:
+            self.selector.stop()
+        self.primary = False
         for t in self._threads:
             t.shutdown(join=False)
         for t in self._threads:

@@ -133,3 +133,79 @@ class LocalAlluxioCluster:
 
     def __exit__(self, *exc):
         self.stop()
+
+
+class MultiMasterLocalAlluxioCluster(LocalAlluxioCluster):
+    """N masters sharing one journal (FILE_LOCK election) + workers; masters can be killed and
+    the standby takes over (reference minicluster/.../MultiMasterLocalAlluxioCluster.java)."""
+
+    def __init__(self, num_masters: int = 2, num_workers: int = 1, conf: dict | None = None, **kw):
+        c = {"alluxio.master.ha.primary.selector": "FILE_LOCK", "alluxio.user.rpc.retry.max.duration": "20sec"}
+        c.update(conf or {})
+        super().__init__(num_workers=num_workers, conf=c, **kw)
+        self.num_masters = num_masters
+        self.masters: list[AlluxioMasterProcess] = []
+
+    @property
+    def master_addresses(self) -> str:
+        return ",".join(m.address for m in self.masters)
+
+    def start(self) -> "MultiMasterLocalAlluxioCluster":
+        import time
+        os.makedirs(self.ufs_root, exist_ok=True)
+        for _ in range(self.num_masters):
+            m = AlluxioMasterProcess(self.conf, port=0, enable_grpc=self.grpc, root_ufs=self.ufs_root)
+            m.start(start_heartbeats=self.heartbeats)
+            self.masters.append(m)
+        deadline = time.time() + 30
+        while self.primary() is None and time.time() < deadline:
+            time.sleep(0.02)
+        self.master = self.primary()
+        for i in range(self.num_workers):
+            self.start_worker(i)
+        return self
+
+    def primary(self):
+        for m in self.masters:
+            if m.primary:
+                return m
+        return None
+
+    def start_worker(self, i: int | None = None) -> AlluxioWorkerProcess:
+        i = len(self.workers) if i is None else i
+        wconf = self.conf.copy()
+        w = AlluxioWorkerProcess(wconf, master_address=self.master_addresses, port=0,
+                                 enable_grpc=self.grpc, work_dir=os.path.join(self.work_dir, f"worker{i}"))
+        w.start(register=True, start_heartbeats=self.heartbeats)
+        self.workers.append(w)
+        return w
+
+    def client(self, **kw):
+        from ..client.file_system import FileSystem
+        return FileSystem(conf=self.conf.copy(), master_address=self.master_addresses, **kw)
+
+    def kill_primary(self, wait_new: float = 30.0):
+        """Stop the primary; wait until a standby has been elected and is serving."""
+        import time
+        old = self.primary()
+        old.stop()
+        deadline = time.time() + wait_new
+        while time.time() < deadline:
+            p = self.primary()
+            if p is not None and p is not old:
+                self.master = p
+                return p
+            time.sleep(0.02)
+        raise TimeoutError("no standby master gained primacy")
+
+    def stop(self) -> None:
+        for w in list(self.workers):
+            w.stop()
+        self.workers.clear()
+        for m in self.masters:
+            if m.started:
+                m.stop()
+        self.masters.clear()
+        self.master = None
+        if self._own_dir:
+            shutil.rmtree(self.work_dir, ignore_errors=True)

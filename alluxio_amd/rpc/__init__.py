@@ -25,7 +25,15 @@ from ..utils import exceptions as ex
 
 LOG = logging.getLogger(__name__)
 
-_LOCAL: dict[str, dict[str, object]] = {}   # address -> {service full name -> servicer}
+class _LocalRegistry(dict):
+    """service full name -> servicer, plus liveness/gate shared with the owning RpcServer."""
+
+    def __init__(self, servicers, server):
+        super().__init__(servicers)
+        self.server = server
+
+
+_LOCAL: dict[str, _LocalRegistry] = {}   # address -> registry
 _LOCAL_LOCK = threading.Lock()
 
 MAX_MESSAGE = 100 << 20
@@ -76,11 +84,12 @@ def _user_from_metadata(context) -> str | None:
 class _Handler:
     """Wraps servicer methods: user propagation, error mapping, metrics."""
 
-    def __init__(self, servicer, spec, metrics=None):
+    def __init__(self, servicer, spec, metrics=None, gate=None):
         self.servicer = servicer
         self.spec = spec
         self.fn = getattr(servicer, spec.name)
         self.metrics = metrics
+        self.gate = gate
 
     def _enter(self, context):
         from ..security import as_user
@@ -89,6 +98,8 @@ class _Handler:
     def unary(self, request, context):
         t0 = time.perf_counter()
         try:
+            if self.gate is not None:
+                self.gate(self.spec)
             with self._enter(context):
                 return self.fn(request, context)
         except ex.AlluxioStatusException as e:
@@ -104,6 +115,8 @@ class _Handler:
 
     def stream(self, request_or_iter, context):
         try:
+            if self.gate is not None:
+                self.gate(self.spec)
             with self._enter(context):
                 yield from self.fn(request_or_iter, context)
         except ex.AlluxioStatusException as e:
@@ -126,6 +139,15 @@ class RpcServer:
         self._servicers: dict[str, object] = {}
         self._server = None
         self.address = None
+        self.alive = False
+        # gate(spec) raises (e.g. UnavailableException on an HA standby) to refuse an RPC
+        self.gate = None
+
+    def check(self, spec) -> None:
+        if not self.alive:
+            raise ex.UnavailableException(f"server {self.address} is not serving")
+        if self.gate is not None:
+            self.gate(spec)
 
     def add_servicer(self, service_full_name: str, servicer) -> None:
         if service_full_name not in SERVICES:
@@ -144,7 +166,7 @@ class RpcServer:
                 for name, spec in SERVICES[svc].items():
                     if not hasattr(servicer, name):
                         continue
-                    h = _Handler(servicer, spec, self.metrics)
+                    h = _Handler(servicer, spec, self.metrics, self.check)
                     des, ser = spec.request.FromString, spec.response.SerializeToString
                     if spec.client_streaming and spec.server_streaming:
                         handlers[name] = grpc.stream_stream_rpc_method_handler(h.stream, des, ser)
@@ -163,11 +185,13 @@ class RpcServer:
         elif self.port == 0:
             self.port = _alloc_local_port()
         self.address = f"{self.host}:{self.port}"
+        self.alive = True
         with _LOCAL_LOCK:
-            _LOCAL[self.address] = dict(self._servicers)
+            _LOCAL[self.address] = _LocalRegistry(self._servicers, self)
         return self.address
 
     def stop(self, grace: float = 0.5) -> None:
+        self.alive = False
         with _LOCAL_LOCK:
             if self.address is not None:
                 _LOCAL.pop(self.address, None)
@@ -186,13 +210,16 @@ def _alloc_local_port() -> int:
 
 
 class _LocalMethod:
-    def __init__(self, servicer, spec, user):
+    def __init__(self, servicer, spec, user, server=None):
         self.fn = getattr(servicer, spec.name)
         self.spec = spec
         self.user = user
+        self.server = server
 
     def __call__(self, request, timeout=None, metadata=None):
         from ..security import as_user
+        if self.server is not None:
+            self.server.check(self.spec)
         ctx = RpcContext(metadata)
         with as_user(self.user):
             if self.spec.server_streaming:
@@ -255,7 +282,7 @@ class Channel:
                 def missing(*a, **kw):
                     raise ex.UnimplementedException(f"{spec.path} not served at {self.address}")
                 return missing
-            return _LocalMethod(servicer, spec, self.user)
+            return _LocalMethod(servicer, spec, self.user, getattr(self.local, "server", None))
         ch = self._channel()
         ser, des = spec.request.SerializeToString, spec.response.FromString
         if spec.client_streaming and spec.server_streaming:
@@ -278,7 +305,13 @@ class Channel:
         if self.local is not None:
             servicer = self.local[service]
             fn = getattr(servicer, method)
-            return lambda it: fn(it, RpcContext())
+            server = getattr(self.local, "server", None)
+
+            def call(it):
+                if server is not None:
+                    server.check(spec)
+                return fn(it, RpcContext())
+            return call
         ch = self._channel()
         c = ch.stream_stream(spec.path, spec.request.SerializeToString, spec.response.FromString)
         md = (("alluxio-user", self.user),) if self.user else None
@@ -306,6 +339,12 @@ class ChannelPool:
                 c = self._chans[key] = Channel(address, user)
             return c
 
+    def drop(self, address: str, user: str | None = None) -> None:
+        with self._lock:
+            c = self._chans.pop((address, user), None)
+        if c is not None:
+            c.close()
+
     def close(self) -> None:
         with self._lock:
             for c in self._chans.values():
@@ -321,3 +360,92 @@ def is_local_address(address: str) -> bool:
 def local_servicer(address: str, service: str):
     with _LOCAL_LOCK:
         return _LOCAL.get(address, {}).get(service)
+
+
+class _FailoverStub:
+    def __init__(self, fch: "FailoverChannel", service: str):
+        self._f = fch
+        self._service = service
+
+    def __getattr__(self, name):
+        if name not in SERVICES[self._service]:
+            raise AttributeError(name)
+        f = self._f
+
+        def call(request, timeout=None, metadata=None):
+            deadline = time.time() + f.max_duration_s
+            delay = 0.02
+            while True:
+                addr = f.current
+                try:
+                    return getattr(f.channel(addr).stub(self._service), name)(request, timeout=timeout)
+                except (ex.UnavailableException, ex.UnimplementedException) as e:
+                    if time.time() > deadline or len(f.addresses) == 0:
+                        raise
+                    LOG.debug("master %s unavailable for %s (%s); trying next", addr, name, e)
+                    f.rotate(addr)
+                    time.sleep(delay)
+                    delay = min(delay * 2, 0.5)
+        return call
+
+
+class FailoverChannel:
+    """A channel to whichever of several HA masters is primary.
+
+    Reference: core/client/fs/.../PollingMasterInquireClient.java (probe each configured master
+    address until one answers as primary) + AbstractClient.retryRPC (reconnect and retry on
+    UNAVAILABLE).  Standby masters refuse every RPC with UNAVAILABLE (their RpcServer gate), so
+    "answers" == "is primary"; calls rotate through the addresses with backoff until one does.
+    """
+
+    def __init__(self, addresses, user: str | None = None, pool: "ChannelPool | None" = None,
+                 max_duration_s: float = 120.0):
+        if isinstance(addresses, str):
+            addresses = [a.strip() for a in addresses.split(",") if a.strip()]
+        self.addresses = list(addresses)
+        self.user = user
+        self.pool = pool or ChannelPool()
+        self.max_duration_s = max_duration_s
+        self._i = 0
+        self._lock = threading.Lock()
+
+    @property
+    def current(self) -> str:
+        with self._lock:
+            return self.addresses[self._i % len(self.addresses)]
+
+    @property
+    def address(self) -> str:
+        return self.current
+
+    @property
+    def is_local(self) -> bool:
+        return self.channel(self.current).is_local
+
+    def rotate(self, failed: str) -> None:
+        with self._lock:
+            if self.addresses[self._i % len(self.addresses)] == failed:
+                self._i += 1
+                # refresh: a restarted in-process server re-registers under the same address
+                self.pool.drop(failed, self.user)
+
+    def channel(self, address: str) -> Channel:
+        return self.pool.get(address, self.user)
+
+    def stub(self, service: str) -> _FailoverStub:
+        return _FailoverStub(self, service)
+
+    def raw_stream(self, service: str, method: str):
+        return self.channel(self.current).raw_stream(service, method)
+
+    def close(self) -> None:
+        pass
+
+
+def master_channel(addresses, user: str | None = None, pool: "ChannelPool | None" = None,
+                   max_duration_s: float = 120.0):
+    """A plain Channel for one master address, a FailoverChannel for an HA address list."""
+    addrs = [a.strip() for a in addresses.split(",")] if isinstance(addresses, str) else list(addresses)
+    if len(addrs) == 1:
+        return (pool or ChannelPool()).get(addrs[0], user) if pool else Channel(addrs[0], user)
+    return FailoverChannel(addrs, user, pool, max_duration_s)

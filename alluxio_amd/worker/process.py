@@ -99,7 +99,8 @@ class AlluxioWorkerProcess:
         self.host = host
         self.port = self.conf.get_int("alluxio.worker.rpc.port") if port is None else port
         self.store = TieredStore(self.conf, device, work_dir)
-        self.master_channel = Channel(self.master_address)
+        from ..rpc import master_channel
+        self.master_channel = master_channel(self.master_address)
         self.worker = BlockWorker(self.conf, self.store, self.master_channel)
         self.server = RpcServer(host, self.port, metrics=msys.metrics("Worker"), enable_grpc=enable_grpc)
         self.server.add_servicer(SVC_BLOCK_WORKER, BlockWorkerService(self.worker, self.conf))
