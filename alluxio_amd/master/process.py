@@ -106,6 +106,10 @@ class AlluxioMasterProcess:
             self.job_master = JobMaster(self._job_fs, self.conf.get_ms("alluxio.job.master.worker.timeout") / 1000.0,
                                         self.conf.get_int("alluxio.job.master.job.capacity"))
         self._job_client_fs = None
+        self.replication_checker = None
+        if self.job_master is not None:
+            from .replication import ReplicationChecker
+            self.replication_checker = ReplicationChecker(self.fs_master, self.job_master)
         self.web = None
         self.selector = None
         self.web_port = 0
@@ -248,6 +252,8 @@ class AlluxioMasterProcess:
                           c.get_ms("alluxio.master.persistence.checker.interval", "1sec")))
             specs.append((hb.JOB_MASTER_LOST_WORKER_DETECTION, self.job_master.detect_lost_workers,
                           c.get_ms("alluxio.job.master.lost.worker.interval")))
+            specs.append((hb.MASTER_REPLICATION_CHECK, self.replication_checker.heartbeat,
+                          c.get_ms("alluxio.master.replication.check.interval", "1min")))
             retention = c.get_ms("alluxio.job.master.finished.job.retention.time") / 1000.0
             specs.append(("Job Master Finished Job Purge",
                           lambda: self.job_master.purge_finished(retention), 10_000))

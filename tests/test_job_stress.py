@@ -195,3 +195,29 @@ def test_max_throughput(cluster):
               "--hi", "400", "--iterations", "3"], fs=fs, print_result=False)
     assert r["max_ops"] > 0 and len(r["trace"]) >= 1
     fs.close()
+
+
+def test_replication_checker(cluster):
+    fs = cluster.client()
+    fs.write_file("/rep/f", os.urandom(MB), write_type="MUST_CACHE", replication_min=2)
+    cluster.heartbeat_workers()
+    bid = fs.get_status("/rep/f").block_ids[0]
+    rc = cluster.master.replication_checker
+    assert rc.heartbeat() == 1
+    for _ in range(300):
+        cluster.drive_jobs()
+        if sum(w.worker.has_block(bid) for w in cluster.workers) == 2:
+            break
+        time.sleep(0.01)
+    assert sum(w.worker.has_block(bid) for w in cluster.workers) == 2
+    cluster.heartbeat_workers()
+    assert rc.heartbeat() == 0   # satisfied
+    fs.set_attribute("/rep/f", replication_min=0, replication_max=1)
+    assert rc.heartbeat() == 1
+    for _ in range(300):
+        cluster.drive_jobs()
+        if sum(w.worker.has_block(bid) for w in cluster.workers) == 1:
+            break
+        time.sleep(0.01)
+    assert sum(w.worker.has_block(bid) for w in cluster.workers) == 1
+    fs.close()
