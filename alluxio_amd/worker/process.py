@@ -148,6 +148,12 @@ class AlluxioWorkerProcess:
                 t = hb.HeartbeatThread(name, fn, ms)
                 t.start()
                 self._threads.append(t)
+        from .management import TierManager
+        self.tier_manager = TierManager(self.worker, self.conf)
+        if start_heartbeats and len(self.tier_manager.tiers()) > 1:
+            self.add_heartbeat(hb.WORKER_TIER_MANAGEMENT, self.tier_manager.run_once,
+                               self.conf.get_ms("alluxio.worker.management.task.interval", "1sec")
+                               if self.conf.get_raw("alluxio.worker.management.task.interval") else 1000)
         if self.conf.get_bool("alluxio.job.worker.enabled", "true"):
             self._start_job_worker(start_heartbeats)
         LOG.info("worker serving at %s (device %d)", addr, self.store.device)
