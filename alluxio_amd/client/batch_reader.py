@@ -92,3 +92,55 @@ class MultiStreamReader:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class RingStreamReader(MultiStreamReader):
+    """``S`` streams x ``depth`` read(buf) calls per step, delivered into a ring
+    ``ring[s, k, :]`` (uint8 tensor ``[S, depth, buf]``) by ONE device-cursor kernel launch
+    (native ``RingReadSession``; file page table resident on the GPU, host work O(1) per step).
+
+    Same semantics as ``depth`` consecutive ``MultiStreamReader`` steps — every call reads the next
+    ``buf`` bytes of its stream, EOF calls reopen the file — except that each call lands in its own
+    ring slot instead of overwriting one buffer, so a consumer can use every slot.  This is the
+    small-read (4 KiB) shape of StressWorkerBench made launch-bound-free.
+    """
+
+    def __init__(self, fs, path: str, ring, start_offsets: list[int] | None = None):
+        import torch
+        if ring.dim() != 3 or ring.dtype != torch.uint8 or not ring.is_contiguous():
+            raise ValueError("ring must be a contiguous uint8 tensor [streams, depth, buf]")
+        self.fs = fs
+        self.path = path
+        self.ring = ring
+        self.streams, self.depth, self.nbytes = (int(x) for x in ring.shape)
+        self.kind = DEVICE if ring.is_cuda else HOST
+        self.device = ring.device if ring.is_cuda else None
+        st = fs.get_status(path)
+        self.status = st
+        self.worker = self._local_worker(st)
+        self.session = ids.create_session_id()
+        blocks, lens = self._layout(st)
+        from ..ops.native import lib, native_errors
+        with native_errors():
+            self.rs = lib().RingReadSession(self.worker.native, self.session, blocks, lens, ring.data_ptr(),
+                                            self.depth * self.nbytes, self.nbytes, self.depth, self.streams,
+                                            self.kind, list(start_offsets or []))
+        self._stream = torch.cuda.current_stream(self.device) if self.kind == DEVICE else None
+        self.reopens = 0
+
+    def step(self) -> int:
+        from ..ops.native import native_errors
+        handle = int(self._stream.cuda_stream) if self._stream is not None else 0
+        with native_errors():
+            nbytes, eofs = self.rs.step(handle)
+        if eofs:
+            # reopen = metadata lookup through the client (cached); the layout must be unchanged
+            st = self.fs.get_status(self.path)
+            if st.length != self.status.length or list(st.block_ids) != list(self.status.block_ids):
+                raise UnavailableException(f"{self.path} changed while being read")
+            self.reopens += eofs
+        return nbytes
+
+    def last_call(self, s: int, k: int) -> tuple[int, int]:
+        """(file offset, length) of stream ``s``'s ``k``-th call of the last step (0 length = EOF)."""
+        return self.rs.last_call(s, k)

@@ -9,6 +9,7 @@
 #include "block_store.h"
 #include "cpu_codecs.h"
 #include "ipc.h"
+#include "ring_read.h"
 #include "kernels.h"
 
 namespace py = pybind11;
@@ -268,6 +269,33 @@ PYBIND11_MODULE(_C, m) {
       .def("position", &ReadSession::position)
       .def_property_readonly("total_bytes", &ReadSession::total_bytes)
       .def_property_readonly("reopens", &ReadSession::reopens);
+
+  py::class_<RingReadSession>(m, "RingReadSession")
+      .def(py::init([](BlockStore& store, int64_t session, const std::vector<int64_t>& blocks,
+                       const std::vector<uint64_t>& lens, uint64_t dst_base, uint64_t stride, uint64_t buf,
+                       uint32_t depth, uint32_t streams, int kind, const std::vector<uint64_t>& starts) {
+             py::gil_scoped_release rel;
+             return new RingReadSession(&store, session, blocks, lens, dst_base, stride, buf, depth, streams, kind,
+                                        starts);
+           }),
+           py::arg("store"), py::arg("session"), py::arg("block_ids"), py::arg("block_lens"), py::arg("dst_base"),
+           py::arg("stream_stride"), py::arg("buf_bytes"), py::arg("depth"), py::arg("streams"),
+           py::arg("dst_kind"), py::arg("start_offsets") = std::vector<uint64_t>{}, py::keep_alive<1, 2>())
+      .def("step", [](RingReadSession& r, uint64_t stream) {
+             uint64_t eofs = 0, n;
+             {
+               py::gil_scoped_release rel;
+               n = r.step(stream, &eofs);
+             }
+             return py::make_tuple(n, eofs);
+           }, py::arg("stream") = 0)
+      .def("close", &RingReadSession::close, G())
+      .def("position", &RingReadSession::position)
+      .def("last_call", &RingReadSession::last_call)
+      .def_property_readonly("total_bytes", &RingReadSession::total_bytes)
+      .def_property_readonly("reopens", &RingReadSession::reopens)
+      .def_property_readonly("calls", &RingReadSession::calls)
+      .def_property_readonly("file_len", &RingReadSession::file_len);
 
   // ---- codecs / kernels ------------------------------------------------------------------
   m.def("device_count", &hip_device_count);

@@ -194,6 +194,8 @@ class BlockStore {
   bool dir_healthy(int d);
   uint64_t clock() const { return clock_.load(); }
   int device() const { return device_; }
+  bool has_device() const { return has_device_; }
+  void use_device() const { set_device(); }
   std::string stats();
 
  private:

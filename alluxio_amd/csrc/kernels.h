@@ -31,6 +31,31 @@ hipError_t launch_batched_copy(const CopySeg* segs, int nseg, uint64_t total_chu
 // Select the copy kernel variant (cache policy / unroll) and grid cap; used for A/B tuning.
 void set_copy_variant(int variant, unsigned grid_cap);
 
+// Device-cursor sequential multi-stream read (StressWorkerBench shape, K1 without per-read
+// descriptors).  S streams each issue `depth` consecutive read(buf) calls per launch over one
+// cached file whose pages are listed in `ftab` (file page -> arena page).  Stream s's call
+// index of launch L is g = c_init[s] + launch_base + k; with cycle = ceil(file_len/buf) + 1
+// calls per pass (the last call of a pass hits EOF and reopens), call c = g % cycle reads
+// [c*buf, min(file_len, (c+1)*buf)) into dst + s*stream_stride + k*buf (a ring of `depth`
+// slots per stream).  Everything the kernel needs is computed from scalars: O(1) host work
+// per launch regardless of S and depth.
+struct SeqReadArgs {
+  const uint8_t* arena;
+  const int64_t* ftab;
+  const uint64_t* c_init;
+  uint8_t* dst;
+  uint64_t stream_stride;
+  uint64_t file_len;
+  uint64_t buf;
+  uint64_t launch_base;
+  uint32_t cycle;
+  uint32_t streams;
+  uint32_t depth;
+  uint32_t page_shift;
+};
+constexpr uint32_t kSeqReadMaxStreams = 8192;
+hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream);
+
 // CRC32C (Castagnoli, reflected, init/xorout 0xFFFFFFFF) of `n` equal-length pieces
 // (piece i = base + i*piece_bytes, last may be shorter: total_bytes).  `out` device array.
 hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint64_t piece_bytes,

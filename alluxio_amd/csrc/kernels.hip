@@ -122,6 +122,83 @@ hipError_t launch_batched_copy(const CopySeg* segs, int nseg, uint64_t total_chu
 }
 
 // ---------------------------------------------------------------------------------------------
+// K1': device-cursor multi-stream sequential read (see SeqReadArgs in kernels.h).
+//
+// The flattened index space is (stream, call k, 16-B vector v).  Each workgroup first computes
+// every stream's first call index of this launch (c0[s] = (c_init[s] + launch_base) % cycle) into
+// LDS — one 64-bit modulo per stream instead of per vector — then grid-strides over vectors with
+// 8 independent 16-B loads in flight per lane before the stores (latency hiding for the
+// short, page-table-indirected reads).  Consecutive lanes touch consecutive vectors of the same
+// read, so both the arena gather and the ring store coalesce.  A read whose length is not a
+// multiple of 16 (the last read of a pass) finishes its tail bytes in the owning lane.
+// ---------------------------------------------------------------------------------------------
+constexpr int kSeqThreads = 256;
+constexpr int kSeqUnroll = 8;
+
+__global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a) {
+  extern __shared__ uint32_t c0[];  // streams entries (dynamic LDS: 1 KiB for 256 streams)
+  for (uint32_t s = threadIdx.x; s < a.streams; s += kSeqThreads)
+    c0[s] = (uint32_t)((a.c_init[s] + a.launch_base) % a.cycle);
+  __syncthreads();
+  const uint64_t vpr = (a.buf + 15) >> 4;  // vectors per read slot
+  const uint64_t nvec = (uint64_t)a.streams * a.depth * vpr;
+  const uint64_t pmask = (1ull << a.page_shift) - 1;
+  const uint64_t gstride = (uint64_t)gridDim.x * kSeqThreads;
+  for (uint64_t base = (uint64_t)blockIdx.x * kSeqThreads + threadIdx.x; base < nvec;
+       base += gstride * kSeqUnroll) {
+    u32x4 v[kSeqUnroll];
+    uint8_t* d[kSeqUnroll];
+    uint32_t nb[kSeqUnroll];  // bytes this lane moves for vector u (16, tail, or 0)
+#pragma unroll
+    for (int u = 0; u < kSeqUnroll; ++u) {
+      const uint64_t i = base + (uint64_t)u * gstride;
+      nb[u] = 0;
+      d[u] = nullptr;
+      if (i >= nvec) continue;
+      const uint64_t r = i / vpr, vi = i - r * vpr;
+      const uint32_t s = (uint32_t)(r / a.depth), k = (uint32_t)(r - (uint64_t)s * a.depth);
+      uint64_t c = (uint64_t)c0[s] + k;
+      if (c >= a.cycle) c %= a.cycle;
+      if (c == a.cycle - 1) continue;                    // EOF call: reopen, no bytes
+      const uint64_t off = c * a.buf + vi * 16;
+      const uint64_t end = (c + 1) * a.buf < a.file_len ? (c + 1) * a.buf : a.file_len;
+      if (off >= end) continue;
+      const uint64_t page = (uint64_t)a.ftab[off >> a.page_shift];
+      const uint8_t* src = a.arena + (page << a.page_shift) + (off & pmask);
+      d[u] = a.dst + (uint64_t)s * a.stream_stride + (uint64_t)k * a.buf + vi * 16;
+      if (end - off >= 16) {
+        nb[u] = 16;
+        v[u] = *reinterpret_cast<const u32x4*>(src);
+      } else {
+        nb[u] = (uint32_t)(end - off);
+        // tail of the pass: byte-wise, may cross into the next page
+        for (uint32_t b = 0; b < nb[u]; ++b) {
+          const uint64_t o = off + b;
+          d[u][b] = a.arena[((uint64_t)a.ftab[o >> a.page_shift] << a.page_shift) + (o & pmask)];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kSeqUnroll; ++u)
+      if (nb[u] == 16) *reinterpret_cast<u32x4*>(d[u]) = v[u];
+  }
+}
+
+hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream) {
+  if (a.streams == 0 || a.depth == 0 || a.buf == 0 || a.file_len == 0) return hipSuccess;
+  if (a.streams > kSeqReadMaxStreams || (a.buf & 15) || (a.stream_stride & 15) ||
+      ((uint64_t)a.dst & 15) || ((uint64_t)a.arena & 15))
+    return hipErrorInvalidValue;
+  const uint64_t nvec = (uint64_t)a.streams * a.depth * ((a.buf + 15) >> 4);
+  uint64_t blocks = (nvec + (uint64_t)kSeqThreads * kSeqUnroll - 1) / ((uint64_t)kSeqThreads * kSeqUnroll);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(seq_read_kernel, dim3((unsigned)blocks), dim3(kSeqThreads), a.streams * sizeof(uint32_t),
+                     stream, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // K10: CRC32C.  Phase 1: one workgroup per 64 KiB segment; each lane runs slicing-by-8 over its
 // own 256 B with the 8 KiB table resident in LDS, then the 256 lane CRCs are folded with a
 // log-depth GF(2) "shift" combine (x^(8L) mod P multipliers).  Phase 2: one workgroup per piece

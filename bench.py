@@ -37,6 +37,9 @@ def parse_args(argv=None):
     ap.add_argument("--block-size", default="64m")
     ap.add_argument("--buffer-size", default="4m")
     ap.add_argument("--page-size", default="2m")
+    ap.add_argument("--depth", type=int, default=0,
+                    help="read calls per stream per step into a per-stream ring (device-cursor reader); "
+                         "0 = auto (1 MiB of calls per stream for buffers < 1 MiB, else 1)")
     ap.add_argument("--dest", choices=["device", "host"], default="device")
     ap.add_argument("--host-check", action="store_true", help="also time a short host-reader (D2H) run")
     ap.add_argument("--work-dir", default=None)
@@ -67,7 +70,7 @@ def main(argv=None):
     work = a.work_dir or os.path.join("/tmp", f"alluxio_amd_bench_{os.getpid() if not distributed else 'dist'}")
     os.makedirs(work, exist_ok=True)
 
-    from alluxio_amd.client.batch_reader import MultiStreamReader
+    from alluxio_amd.client.batch_reader import MultiStreamReader, RingStreamReader
     from alluxio_amd.client.file_system import FileSystem
     from alluxio_amd.conf import Configuration
     from alluxio_amd.master.process import AlluxioMasterProcess
@@ -137,12 +140,20 @@ def main(argv=None):
 
     # ---- reader streams -----------------------------------------------------------------------
     dev = torch.device("cuda", local_rank) if (gpu and a.dest == "device") else None
-    if dev is not None:
-        bufs_all = torch.empty(a.threads * buf, dtype=torch.uint8, device=dev)
+    depth = a.depth or (max(1, (1 << 20) // buf) if buf < (1 << 20) else 1)
+    if depth > 1:
+        # device-cursor ring reader: each step = `depth` read(buf) calls per stream, one launch
+        ring = torch.empty((a.threads, depth, buf), dtype=torch.uint8, device=dev,
+                           pin_memory=(gpu and dev is None))
+        reader = RingStreamReader(fs, path, ring)
+        bufs = None
     else:
-        bufs_all = torch.empty(a.threads * buf, dtype=torch.uint8, pin_memory=gpu)
-    bufs = [bufs_all[i * buf:(i + 1) * buf] for i in range(a.threads)]
-    reader = MultiStreamReader(fs, path, bufs)
+        if dev is not None:
+            bufs_all = torch.empty(a.threads * buf, dtype=torch.uint8, device=dev)
+        else:
+            bufs_all = torch.empty(a.threads * buf, dtype=torch.uint8, pin_memory=gpu)
+        bufs = [bufs_all[i * buf:(i + 1) * buf] for i in range(a.threads)]
+        reader = MultiStreamReader(fs, path, bufs)
 
     def sync():
         if gpu:
@@ -164,18 +175,25 @@ def main(argv=None):
     if distributed:
         dist.barrier()
 
-    # ---- verify: every stream's last buffer equals the file bytes at its last read ------------
+    # ---- verify: sampled streams' last reads equal the file bytes at their offsets ------------
     ok = True
     check = [0, a.threads // 2, a.threads - 1]
-    for i in check:
-        pos = reader.position(i)
-        if pos == 0:
-            continue
-        n = min(buf, pos - ((pos - 1) // buf) * buf) if pos % buf else buf
-        start = pos - n
-        got = bufs[i][:n].cpu().numpy()
-        if not np.array_equal(got, data[start:start + n]):
-            ok = False
+    if bufs is None:
+        for i in check:
+            for k in (0, depth // 2, depth - 1):
+                off, n = reader.last_call(i, k)
+                if n and not np.array_equal(ring[i, k, :n].cpu().numpy(), data[off:off + n]):
+                    ok = False
+    else:
+        for i in check:
+            pos = reader.position(i)
+            if pos == 0:
+                continue
+            n = min(buf, pos - ((pos - 1) // buf) * buf) if pos % buf else buf
+            start = pos - n
+            got = bufs[i][:n].cpu().numpy()
+            if not np.array_equal(got, data[start:start + n]):
+                ok = False
     reader.close()
 
     host_gbps = None
@@ -232,8 +250,11 @@ def main(argv=None):
                 "file_size": file_size,
                 "block_size": block_size,
                 "buffer_size": buf,
+                "calls_per_stream_per_step": depth,
+                "reads_per_step": a.threads * depth,
                 "page_size": page,
-                "reader": "gpu-consumer (same-GPU device buffers)" if dev is not None else "host (pinned)",
+                "reader": ("gpu-consumer (same-GPU device buffers)" if dev is not None else "host (pinned)")
+                + (f", device-cursor ring x{depth}" if depth > 1 else ""),
                 "verified": bool(ok),
                 "host_reader_GBps": round(host_gbps, 3) if host_gbps else None,
                 "write_GBps_per_worker": round(file_size / write_s / 1e9, 3),

@@ -38,6 +38,14 @@ for s in $STEPS; do
     prof)
       run rocprof_bench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
       ;;
+    ring)
+      run bench_ring4k 300 python bench.py --buffer-size 4k --steps 200 --warmup 20
+      run bench_ring4k_d64 300 python bench.py --buffer-size 4k --depth 64 --steps 200 --warmup 20
+      run bench_ring4k_d1024 300 python bench.py --buffer-size 4k --depth 1024 --steps 100 --warmup 10
+      run bench_ring64k 300 python bench.py --buffer-size 64k --steps 200 --warmup 20
+      run bench_ring4k_f1g 300 python bench.py --buffer-size 4k --file-size 1g --steps 200 --warmup 20
+      run rocprof_ring 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ring" -o ring --output-format csv -- python3 bench.py --buffer-size 4k --steps 50 --warmup 5
+      ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
     tune) run copy_tune 600 python tools/copy_tune.py --out "$OUT/copy_tune.json" ;;
   esac
