@@ -55,6 +55,8 @@ struct SeqReadArgs {
 };
 constexpr uint32_t kSeqReadMaxStreams = 8192;
 hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream);
+// A/B switch for the sequential-read kernel (bit0: nontemporal ring stores, bit1: unroll 16).
+void set_seq_read_variant(int variant, unsigned grid_cap);
 
 // CRC32C (Castagnoli, reflected, init/xorout 0xFFFFFFFF) of `n` equal-length pieces
 // (piece i = base + i*piece_bytes, last may be shorter: total_bytes).  `out` device array.

@@ -133,35 +133,52 @@ hipError_t launch_batched_copy(const CopySeg* segs, int nseg, uint64_t total_chu
 // multiple of 16 (the last read of a pass) finishes its tail bytes in the owning lane.
 // ---------------------------------------------------------------------------------------------
 constexpr int kSeqThreads = 256;
-constexpr int kSeqUnroll = 8;
 
-__global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a) {
+// POW2: vectors-per-read and depth are powers of two -> index math is shifts/masks (the common
+// case: 4 KiB reads x 256 calls); otherwise 64-bit division.  SP: store policy of the ring
+// writes (1 = nontemporal: the ring is written once and consumed elsewhere, so keep the file's
+// pages, not the ring, resident in L2/MALL).
+template <bool POW2, int UNROLL, int SP>
+__global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a, uint32_t vpr_shift,
+                                                               uint32_t depth_shift) {
   extern __shared__ uint32_t c0[];  // streams entries (dynamic LDS: 1 KiB for 256 streams)
   for (uint32_t s = threadIdx.x; s < a.streams; s += kSeqThreads)
     c0[s] = (uint32_t)((a.c_init[s] + a.launch_base) % a.cycle);
   __syncthreads();
-  const uint64_t vpr = (a.buf + 15) >> 4;  // vectors per read slot
+  const uint64_t vpr = a.buf >> 4;  // vectors per read slot (buf % 16 == 0)
   const uint64_t nvec = (uint64_t)a.streams * a.depth * vpr;
   const uint64_t pmask = (1ull << a.page_shift) - 1;
   const uint64_t gstride = (uint64_t)gridDim.x * kSeqThreads;
   for (uint64_t base = (uint64_t)blockIdx.x * kSeqThreads + threadIdx.x; base < nvec;
-       base += gstride * kSeqUnroll) {
-    u32x4 v[kSeqUnroll];
-    uint8_t* d[kSeqUnroll];
-    uint32_t nb[kSeqUnroll];  // bytes this lane moves for vector u (16, tail, or 0)
+       base += gstride * UNROLL) {
+    u32x4 v[UNROLL];
+    uint8_t* d[UNROLL];
+    uint32_t nb[UNROLL];  // bytes this lane moves for vector u (16, tail, or 0)
 #pragma unroll
-    for (int u = 0; u < kSeqUnroll; ++u) {
+    for (int u = 0; u < UNROLL; ++u) {
       const uint64_t i = base + (uint64_t)u * gstride;
       nb[u] = 0;
       d[u] = nullptr;
       if (i >= nvec) continue;
-      const uint64_t r = i / vpr, vi = i - r * vpr;
-      const uint32_t s = (uint32_t)(r / a.depth), k = (uint32_t)(r - (uint64_t)s * a.depth);
-      uint64_t c = (uint64_t)c0[s] + k;
-      if (c >= a.cycle) c %= a.cycle;
+      uint64_t r, vi;
+      uint32_t s, k;
+      if constexpr (POW2) {
+        r = i >> vpr_shift;
+        vi = i & (vpr - 1);
+        s = (uint32_t)(r >> depth_shift);
+        k = (uint32_t)(r & (a.depth - 1));
+      } else {
+        r = i / vpr;
+        vi = i - r * vpr;
+        s = (uint32_t)(r / a.depth);
+        k = (uint32_t)(r - (uint64_t)s * a.depth);
+      }
+      uint32_t c = c0[s] + k;
+      if (c >= a.cycle) c = (uint32_t)(((uint64_t)c0[s] + k) % a.cycle);
       if (c == a.cycle - 1) continue;                    // EOF call: reopen, no bytes
-      const uint64_t off = c * a.buf + vi * 16;
-      const uint64_t end = (c + 1) * a.buf < a.file_len ? (c + 1) * a.buf : a.file_len;
+      const uint64_t off = (uint64_t)c * a.buf + vi * 16;
+      const uint64_t rend = ((uint64_t)c + 1) * a.buf;
+      const uint64_t end = rend < a.file_len ? rend : a.file_len;
       if (off >= end) continue;
       const uint64_t page = (uint64_t)a.ftab[off >> a.page_shift];
       const uint8_t* src = a.arena + (page << a.page_shift) + (off & pmask);
@@ -179,9 +196,24 @@ __global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < kSeqUnroll; ++u)
-      if (nb[u] == 16) *reinterpret_cast<u32x4*>(d[u]) = v[u];
+    for (int u = 0; u < UNROLL; ++u)
+      if (nb[u] == 16) st16<SP>(reinterpret_cast<u32x4*>(d[u]), v[u]);
   }
+}
+
+static int g_seq_variant = 0;   // 0: cached stores, 1: nontemporal stores, +2: unroll 16
+static unsigned g_seq_grid_cap = 4096;
+
+void set_seq_read_variant(int variant, unsigned grid_cap) {
+  g_seq_variant = variant;
+  if (grid_cap) g_seq_grid_cap = grid_cap;
+}
+
+static inline bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+static inline uint32_t log2u(uint64_t x) {
+  uint32_t s = 0;
+  while ((1ull << s) < x) ++s;
+  return s;
 }
 
 hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream) {
@@ -189,12 +221,26 @@ hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream) {
   if (a.streams > kSeqReadMaxStreams || (a.buf & 15) || (a.stream_stride & 15) ||
       ((uint64_t)a.dst & 15) || ((uint64_t)a.arena & 15))
     return hipErrorInvalidValue;
-  const uint64_t nvec = (uint64_t)a.streams * a.depth * ((a.buf + 15) >> 4);
-  uint64_t blocks = (nvec + (uint64_t)kSeqThreads * kSeqUnroll - 1) / ((uint64_t)kSeqThreads * kSeqUnroll);
-  if (blocks > 4096) blocks = 4096;
+  const uint64_t vpr = a.buf >> 4;
+  const uint64_t nvec = (uint64_t)a.streams * a.depth * vpr;
+  const int unroll = (g_seq_variant & 2) ? 16 : 8;
+  uint64_t blocks = (nvec + (uint64_t)kSeqThreads * unroll - 1) / ((uint64_t)kSeqThreads * unroll);
+  if (blocks > g_seq_grid_cap) blocks = g_seq_grid_cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(seq_read_kernel, dim3((unsigned)blocks), dim3(kSeqThreads), a.streams * sizeof(uint32_t),
-                     stream, a);
+  const bool p2 = is_pow2(vpr) && is_pow2(a.depth);
+  const uint32_t vs = log2u(vpr), ds = log2u(a.depth);
+  const size_t lds = a.streams * sizeof(uint32_t);
+  const dim3 g((unsigned)blocks), b(kSeqThreads);
+#define AMDX_SEQ(P2, U, SP) \
+  hipLaunchKernelGGL((seq_read_kernel<P2, U, SP>), g, b, lds, stream, a, vs, ds)
+  const int sp = g_seq_variant & 1;
+  if (p2) {
+    if (unroll == 16) { if (sp) AMDX_SEQ(true, 16, 1); else AMDX_SEQ(true, 16, 0); }
+    else { if (sp) AMDX_SEQ(true, 8, 1); else AMDX_SEQ(true, 8, 0); }
+  } else {
+    if (sp) AMDX_SEQ(false, 8, 1); else AMDX_SEQ(false, 8, 0);
+  }
+#undef AMDX_SEQ
   return hipGetLastError();
 }
 
