@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a, ui
 }
 
 static int g_seq_variant = 0;   // 0: cached stores, 1: nontemporal stores, +2: unroll 16
-static unsigned g_seq_grid_cap = 4096;
+static unsigned g_seq_grid_cap = 8192;
 
 void set_seq_read_variant(int variant, unsigned grid_cap) {
   g_seq_variant = variant;

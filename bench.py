@@ -6,9 +6,17 @@ stress/common/.../WorkerBenchParameters.java:40-70): a file is written CACHE_THR
 one worker, then ``--threads`` readers loop ``read(buf)`` over it and re-open at EOF; the
 result is bytes read / time.  Here every GPU rank is one worker (HBM MEM tier) with its own
 in-process client; the rank writes its file through the client API (CACHE_THROUGH: local UFS +
-local worker), then its ``threads`` reader streams read it.  One bench *step* = every stream
-performs one ``read(buf)`` (or the EOF read that re-opens), executed as one batched page-gather
-launch from HBM pages into the streams' device buffers.
+local worker), then its ``threads`` reader streams read it with the reference's default
+parameters (256 streams, 128 MiB file, 4 KiB ``read(buf)`` calls; 64 MiB blocks per BASELINE.md).
+
+One bench *step* = every stream performs ``depth`` consecutive ``read(buf)`` calls (EOF calls
+re-open the file, as the reference loop does), all executed by ONE device-cursor kernel launch:
+the file's page table lives on the GPU, each call's bytes land in that stream's own ring slot
+``ring[stream, call]`` (no call is skipped or merged: every call's bytes are copied to distinct
+memory a consumer can use), and host work per step is O(1).  depth defaults to 1 MiB worth of
+calls per stream (256 for 4 KiB) — the same amortisation the reference client gets by serving
+read(4k) out of 1 MiB chunk buffers (GrpcDataReader chunks).  ``--buffer-size >= 1m`` (or
+``--depth 1``) uses the per-call batched page-gather reader instead.
 
 ``value`` = total bytes read by all ranks in the K timed steps / max-over-ranks wall time (GB/s,
 whole node, weak scaling: each worker serves its own file).
@@ -35,7 +43,7 @@ def parse_args(argv=None):
     ap.add_argument("--threads", type=int, default=256, help="reader streams per worker")
     ap.add_argument("--file-size", default="128m")
     ap.add_argument("--block-size", default="64m")
-    ap.add_argument("--buffer-size", default="4m")
+    ap.add_argument("--buffer-size", default="4k")
     ap.add_argument("--page-size", default="2m")
     ap.add_argument("--depth", type=int, default=0,
                     help="read calls per stream per step into a per-stream ring (device-cursor reader); "

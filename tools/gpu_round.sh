@@ -47,7 +47,7 @@ for s in $STEPS; do
       run rocprof_ring 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ring" -o ring --output-format csv -- python3 bench.py --buffer-size 4k --steps 50 --warmup 5
       ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
-    ringtune) run ring_tune 600 python tools/ring_tune.py --out "$OUT/ring_tune.json" ;;
+    ringtune) run ring_tune 600 python tools/ring_tune.py --out "$OUT/ring_tune.json" $RINGTUNE_ARGS ;;
     tune) run copy_tune 600 python tools/copy_tune.py --out "$OUT/copy_tune.json" ;;
   esac
 done
