@@ -29,11 +29,12 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
     bench) run bench_default 400 python bench.py ;;
     variants)
-      run bench_buf4k 300 python bench.py --buffer-size 4k --steps 200 --warmup 10
+      run bench_buf4m 300 python bench.py --buffer-size 4m --steps 200 --warmup 20
       run bench_buf1m 300 python bench.py --buffer-size 1m
-      run bench_buf16m 300 python bench.py --buffer-size 16m --steps 100
-      run bench_file1g 400 python bench.py --file-size 1g --steps 100
-      run bench_host 400 python bench.py --dest host --steps 20 --warmup 3 --host-check
+      run bench_buf64k 300 python bench.py --buffer-size 64k
+      run bench_file1g 400 python bench.py --file-size 1g --steps 200
+      run bench_host 400 python bench.py --dest host --steps 20 --warmup 3
+      run bench_host4m 400 python bench.py --dest host --buffer-size 4m --steps 20 --warmup 3
       ;;
     prof)
       run rocprof_bench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
