@@ -1,0 +1,439 @@
+"""Client-side local page cache.
+
+Parity: core/client/fs/src/main/java/alluxio/client/file/cache/ — LocalCacheManager.java:75-360
+(page-granular cache: get/put/delete, two-phase evict-then-put under striped page locks,
+restore of a LOCAL store's pages on restart, async put), PageStore.java + store/LocalPageStore.java
+(``<dir>/<page size>/<bucket>/<file id>/<page index>`` files), store/RocksPageStore.java,
+MetaStore.java / DefaultMetaStore.java (page index + bytes), evictor/{LRU,LFU}CacheEvictor.java,
+LocalCacheFileInStream.java (read through the cache: hit -> copy, miss -> read the whole page
+from the external stream, put, copy) and LocalCacheFileSystem.java (wraps openFile).
+
+Store types: ``LOCAL`` (files, survives restarts), ``MEM`` (host memory) and the MI355X ``HBM``
+store — a fixed-page device arena; a cache hit for a device destination is a D2D copy and a
+multi-page read into a GPU tensor is gathered by one batched-copy launch.
+"""
+from __future__ import annotations
+
+import collections
+import io
+import logging
+import math
+import os
+import threading
+import zlib
+
+from .. import metrics as msys
+
+LOG = logging.getLogger(__name__)
+
+
+class PageId(tuple):
+    __slots__ = ()
+
+    def __new__(cls, file_id: str, page_index: int):
+        return super().__new__(cls, (str(file_id), int(page_index)))
+
+    @property
+    def file_id(self):
+        return self[0]
+
+    @property
+    def page_index(self):
+        return self[1]
+
+
+# ---- evictors ---------------------------------------------------------------------------------
+class LRUCacheEvictor:
+    def __init__(self, conf=None):
+        self._d: collections.OrderedDict = collections.OrderedDict()
+
+    def update_on_get(self, pid):
+        if pid in self._d:
+            self._d.move_to_end(pid)
+
+    def update_on_put(self, pid):
+        self._d[pid] = True
+        self._d.move_to_end(pid)
+
+    def update_on_delete(self, pid):
+        self._d.pop(pid, None)
+
+    def evict(self):
+        return next(iter(self._d), None)
+
+
+class LFUCacheEvictor:
+    """Buckets by floor(log_base(count)) (LFUCacheEvictor.java); LRU within a bucket."""
+
+    def __init__(self, conf=None):
+        self.base = float(conf.get("alluxio.user.client.cache.evictor.lfu.logbase")) if conf else 2.0
+        self._count: dict = {}
+        self._buckets: dict[int, collections.OrderedDict] = collections.defaultdict(collections.OrderedDict)
+
+    def _bucket(self, n):
+        return int(math.log(n, self.base)) if n > 0 else 0
+
+    def _touch(self, pid, delta):
+        old = self._count.get(pid)
+        if old is not None:
+            self._buckets[self._bucket(old)].pop(pid, None)
+        n = (old or 0) + delta
+        self._count[pid] = n
+        self._buckets[self._bucket(n)][pid] = True
+
+    def update_on_get(self, pid):
+        if pid in self._count:
+            self._touch(pid, 1)
+
+    def update_on_put(self, pid):
+        self._touch(pid, 1)
+
+    def update_on_delete(self, pid):
+        n = self._count.pop(pid, None)
+        if n is not None:
+            self._buckets[self._bucket(n)].pop(pid, None)
+
+    def evict(self):
+        for b in sorted(self._buckets):
+            if self._buckets[b]:
+                return next(iter(self._buckets[b]))
+        return None
+
+
+# ---- page stores ------------------------------------------------------------------------------
+class LocalPageStore:
+    """One file per page: ``<root>/<page_size>/<bucket>/<file_id>/<page_index>``."""
+
+    def __init__(self, root: str, page_size: int, buckets: int = 1000):
+        self.root = os.path.join(root, str(page_size))
+        self.buckets = buckets
+        os.makedirs(self.root, exist_ok=True)
+
+    def _path(self, pid):
+        b = zlib.crc32(pid.file_id.encode()) % self.buckets  # stable across processes (restore)
+        return os.path.join(self.root, str(b), pid.file_id, str(pid.page_index))
+
+    def put(self, pid, data: bytes) -> None:
+        p = self._path(pid)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        tmp = p + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, p)
+
+    def get(self, pid, offset: int, length: int) -> bytes | None:
+        try:
+            with open(self._path(pid), "rb") as f:
+                f.seek(offset)
+                return f.read(length)
+        except FileNotFoundError:
+            return None
+
+    def delete(self, pid) -> None:
+        try:
+            os.remove(self._path(pid))
+        except FileNotFoundError:
+            pass
+
+    def restore(self):
+        """[(PageId, bytes)] of pages already on disk (LocalCacheManager restore)."""
+        out = []
+        for b in os.listdir(self.root):
+            bdir = os.path.join(self.root, b)
+            for fid in os.listdir(bdir):
+                for name in os.listdir(os.path.join(bdir, fid)):
+                    if name.endswith(".tmp"):
+                        continue
+                    p = os.path.join(bdir, fid, name)
+                    out.append((PageId(fid, int(name)), os.path.getsize(p)))
+        return out
+
+
+class MemPageStore:
+    def __init__(self):
+        self._d: dict = {}
+
+    def put(self, pid, data: bytes) -> None:
+        self._d[pid] = bytes(data)
+
+    def get(self, pid, offset, length):
+        d = self._d.get(pid)
+        return None if d is None else d[offset:offset + length]
+
+    def delete(self, pid) -> None:
+        self._d.pop(pid, None)
+
+    def restore(self):
+        return []
+
+
+class HbmPageStore:
+    """Fixed-size page slots in one device arena; hits copy device-to-device."""
+
+    def __init__(self, capacity: int, page_size: int, device=None):
+        import torch
+        self.page_size = page_size
+        self.slots = max(1, capacity // page_size)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.arena = torch.empty(self.slots * page_size, dtype=torch.uint8, device=self.device)
+        self.free = list(range(self.slots - 1, -1, -1))
+        self.slot_of: dict = {}
+        self.len_of: dict = {}
+
+    def put(self, pid, data) -> None:
+        import numpy as np
+        import torch
+        if pid in self.slot_of:
+            self.delete(pid)
+        s = self.free.pop()
+        n = len(data)
+        src = torch.from_numpy(np.frombuffer(bytes(data), dtype=np.uint8)) if not isinstance(data, torch.Tensor) else data
+        self.arena[s * self.page_size:s * self.page_size + n].copy_(src)
+        self.slot_of[pid] = s
+        self.len_of[pid] = n
+
+    def ptr(self, pid, offset):
+        s = self.slot_of.get(pid)
+        return None if s is None else self.arena.data_ptr() + s * self.page_size + offset
+
+    def get(self, pid, offset, length):
+        s = self.slot_of.get(pid)
+        if s is None:
+            return None
+        base = s * self.page_size + offset
+        return self.arena[base:base + length].cpu().numpy().tobytes()
+
+    def delete(self, pid) -> None:
+        s = self.slot_of.pop(pid, None)
+        if s is not None:
+            self.len_of.pop(pid, None)
+            self.free.append(s)
+
+    def restore(self):
+        return []
+
+
+# ---- manager ----------------------------------------------------------------------------------
+class LocalCacheManager:
+    LOCKS = 1024
+
+    def __init__(self, conf, store=None):
+        from ..utils.format import parse_space_size
+        self.conf = conf
+        self.page_size = parse_space_size(conf.get("alluxio.user.client.cache.page.size"))
+        self.capacity = parse_space_size(conf.get("alluxio.user.client.cache.size"))
+        ev = conf.get("alluxio.user.client.cache.evictor.class").rsplit(".", 1)[-1]
+        self.evictor = LFUCacheEvictor(conf) if ev.startswith("LFU") else LRUCacheEvictor(conf)
+        stype = conf.get("alluxio.user.client.cache.store.type").upper()
+        if store is not None:
+            self.store = store
+        elif stype == "HBM":
+            self.store = HbmPageStore(self.capacity, self.page_size)
+        elif stype == "MEM":
+            self.store = MemPageStore()
+        else:
+            self.store = LocalPageStore(conf.get("alluxio.user.client.cache.dir"), self.page_size,
+                                        conf.get_int("alluxio.user.client.cache.local.store.file.buckets"))
+        self.meta: dict = {}   # PageId -> bytes
+        self.bytes = 0
+        self._meta_lock = threading.RLock()
+        self._page_locks = [threading.RLock() for _ in range(self.LOCKS)]
+        self.metrics = msys.metrics("Client")
+        for pid, n in self.store.restore():
+            if self.bytes + n > self.capacity:
+                self.store.delete(pid)
+                continue
+            self.meta[pid] = n
+            self.bytes += n
+            self.evictor.update_on_put(pid)
+
+    def _lock(self, pid):
+        return self._page_locks[hash(pid) % self.LOCKS]
+
+    def put(self, pid, data) -> bool:
+        n = len(data)
+        if n > self.page_size:
+            return False
+        with self._lock(pid):
+            with self._meta_lock:
+                if pid in self.meta:
+                    return True
+                # phase 1: evict until the page fits
+                while self.bytes + n > self.capacity:
+                    victim = self.evictor.evict()
+                    if victim is None:
+                        return False
+                    self._delete_locked(victim)
+                    self.metrics.counter("ClientCachePagesEvicted").inc()
+            # phase 2: store + index
+            try:
+                self.store.put(pid, data)
+            except Exception:  # noqa: BLE001
+                LOG.debug("page store put failed", exc_info=True)
+                return False
+            with self._meta_lock:
+                self.meta[pid] = n
+                self.bytes += n
+                self.evictor.update_on_put(pid)
+            self.metrics.counter("ClientCacheBytesWrittenCache").inc(n)
+            return True
+
+    def get(self, pid, offset: int, length: int) -> bytes | None:
+        with self._lock(pid):
+            with self._meta_lock:
+                if pid not in self.meta:
+                    self.metrics.counter("ClientCacheBytesRequestedExternal").inc(length)
+                    return None
+                self.evictor.update_on_get(pid)
+            out = self.store.get(pid, offset, length)
+        if out is not None:
+            self.metrics.counter("ClientCacheBytesReadCache").inc(len(out))
+        return out
+
+    def _delete_locked(self, pid) -> None:
+        n = self.meta.pop(pid, None)
+        if n is None:
+            return
+        self.bytes -= n
+        self.evictor.update_on_delete(pid)
+        self.store.delete(pid)
+
+    def delete(self, pid) -> bool:
+        with self._lock(pid), self._meta_lock:
+            had = pid in self.meta
+            self._delete_locked(pid)
+            return had
+
+    def has(self, pid) -> bool:
+        with self._meta_lock:
+            return pid in self.meta
+
+
+class LocalCacheFileInStream(io.RawIOBase):
+    """Positioned/sequential reads served page-wise from the local cache, filling misses from
+    the external (Alluxio) stream a whole page at a time.  Same read API as FileInStream."""
+
+    def __init__(self, status, open_external, cache: LocalCacheManager):
+        super().__init__()
+        self.status = status
+        self.length = status.length
+        self.cache = cache
+        self._open_external = open_external
+        self._ext = None
+        self.pos = 0
+        self.file_id = f"{status.fileId}-{status.lastModificationTimeMs}"
+
+    def _external(self):
+        if self._ext is None:
+            self._ext = self._open_external()
+        return self._ext
+
+    def _page(self, idx: int, off: int, n: int) -> bytes:
+        pid = PageId(self.file_id, idx)
+        got = self.cache.get(pid, off, n)
+        if got is not None:
+            return got
+        ps = self.cache.page_size
+        start = idx * ps
+        ext = self._external()
+        ext.seek(start)
+        page = ext.read(min(ps, self.length - start))
+        self.cache.put(pid, page)
+        return page[off:off + n]
+
+    def pread_bytes(self, position: int, size: int) -> bytes:
+        size = max(0, min(size, self.length - position))
+        ps = self.cache.page_size
+        out = []
+        done = 0
+        while done < size:
+            p = position + done
+            idx, off = divmod(p, ps)
+            take = min(size - done, ps - off)
+            out.append(self._page(idx, off, take))
+            done += take
+        return b"".join(out)
+
+    def readable(self):
+        return True
+
+    def seekable(self):
+        return True
+
+    def read(self, size: int = -1) -> bytes:
+        if size is None or size < 0:
+            size = self.length - self.pos
+        data = self.pread_bytes(self.pos, size)
+        self.pos += len(data)
+        return data
+
+    def readall(self):
+        return self.read(-1)
+
+    def readinto(self, b) -> int:
+        mv = memoryview(b).cast("B")
+        data = self.read(len(mv))
+        mv[:len(data)] = data
+        return len(data)
+
+    def pread(self, position: int, buf, nbytes: int | None = None) -> int:
+        mv = memoryview(buf).cast("B") if not hasattr(buf, "data_ptr") else None
+        if mv is None:
+            import numpy as np
+            import torch
+            n = buf.numel() * buf.element_size() if nbytes is None else nbytes
+            data = self.pread_bytes(position, n)
+            buf.view(torch.uint8)[:len(data)].copy_(torch.from_numpy(np.frombuffer(data, dtype=np.uint8)))
+            return len(data)
+        data = self.pread_bytes(position, len(mv) if nbytes is None else nbytes)
+        mv[:len(data)] = data
+        return len(data)
+
+    def read_into(self, tensor) -> int:
+        """Fill a (device) tensor from the current position: cached HBM pages are gathered by
+        one batched-copy launch; missing pages are fetched and cached first."""
+        import torch
+        n = min(tensor.numel() * tensor.element_size(), self.length - self.pos)
+        store = self.cache.store
+        if not (tensor.is_cuda and isinstance(store, HbmPageStore)):
+            data = self.read(n)
+            import numpy as np
+            tensor.view(torch.uint8)[:len(data)].copy_(torch.from_numpy(np.frombuffer(data, dtype=np.uint8)))
+            return len(data)
+        ps = self.cache.page_size
+        segs, done = [], 0
+        dst = tensor.data_ptr()
+        while done < n:
+            p = self.pos + done
+            idx, off = divmod(p, ps)
+            take = min(n - done, ps - off)
+            pid = PageId(self.file_id, idx)
+            if not self.cache.has(pid):
+                self._page(idx, 0, 0)  # fetch + put
+            with self.cache._lock(pid):
+                src = store.ptr(pid, off)
+            if src is None:  # evicted meanwhile: byte path for this page
+                chunk = self._page(idx, off, take)
+                import numpy as np
+                tensor.view(torch.uint8)[done:done + take].copy_(torch.from_numpy(np.frombuffer(chunk, dtype=np.uint8)))
+            else:
+                segs.append((src, dst + done, take))
+                self.cache.evictor.update_on_get(pid)
+            done += take
+        if segs:
+            from ..ops.native import lib
+            lib().batched_copy(segs, int(torch.cuda.current_stream().cuda_stream), True)
+        self.pos += n
+        return n
+
+    def seek(self, pos: int, whence: int = 0) -> int:
+        self.pos = {0: pos, 1: self.pos + pos, 2: self.length + pos}[whence]
+        return self.pos
+
+    def tell(self) -> int:
+        return self.pos
+
+    def close(self) -> None:
+        if not self.closed and self._ext is not None:
+            self._ext.close()
+        super().close()

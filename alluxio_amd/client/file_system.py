@@ -131,6 +131,10 @@ class FileSystem:
             if use_cache else None
         self._fs = self.ctx.fs_master()
         self._closed = False
+        self.local_cache = None
+        if c.get_bool("alluxio.user.client.cache.enabled"):
+            from .cache import LocalCacheManager
+            self.local_cache = LocalCacheManager(c)
 
     @classmethod
     def get(cls, conf=None, master_address=None, user=None):
@@ -329,6 +333,9 @@ class FileSystem:
         if not st.info.completed:
             from ..utils.exceptions import FileIncompleteException
             raise FileIncompleteException(f"File {st.info.path} is not completed")
+        if self.local_cache is not None:
+            from .cache import LocalCacheFileInStream
+            return LocalCacheFileInStream(st.info, lambda: FileInStream(self.ctx, st.info, rt), self.local_cache)
         return FileInStream(self.ctx, st.info, rt)
 
     def read_file(self, path, read_type=None) -> bytes:

@@ -1,0 +1,96 @@
+"""Client local page cache (reference core/client/fs/src/test/.../cache/LocalCacheManagerTest,
+LocalCacheFileInStreamTest, evictor tests): hits/misses, eviction order, restore, stream reads."""
+import os
+
+import numpy as np
+import pytest
+
+from alluxio_amd.client.cache import (LFUCacheEvictor, LocalCacheManager, LRUCacheEvictor, MemPageStore,
+                                      PageId)
+from alluxio_amd.conf import Configuration
+from alluxio_amd.minicluster import LocalAlluxioCluster
+
+
+def _conf(tmp_path, **kw):
+    c = {"alluxio.user.client.cache.enabled": "true", "alluxio.user.client.cache.dir": str(tmp_path / "cache"),
+         "alluxio.user.client.cache.page.size": "4KB", "alluxio.user.client.cache.size": "16KB"}
+    c.update(kw)
+    return Configuration(c)
+
+
+def test_evictors():
+    lru = LRUCacheEvictor()
+    for i in range(3):
+        lru.update_on_put(PageId("f", i))
+    lru.update_on_get(PageId("f", 0))
+    assert lru.evict() == PageId("f", 1)
+    lfu = LFUCacheEvictor(Configuration())
+    for i in range(3):
+        lfu.update_on_put(PageId("f", i))
+    for _ in range(4):
+        lfu.update_on_get(PageId("f", 0))
+        lfu.update_on_get(PageId("f", 2))
+    assert lfu.evict() == PageId("f", 1)
+
+
+def test_manager_put_get_evict_restore(tmp_path):
+    m = LocalCacheManager(_conf(tmp_path))
+    pages = {i: os.urandom(4096) for i in range(5)}
+    for i in range(4):
+        assert m.put(PageId("f", i), pages[i])
+    assert m.get(PageId("f", 0), 10, 100) == pages[0][10:110]   # touch 0: LRU victim is now 1
+    assert m.put(PageId("f", 4), pages[4])
+    assert not m.has(PageId("f", 1)) and m.has(PageId("f", 0)) and m.bytes == 16384
+    assert not m.put(PageId("f", 9), b"x" * 5000)               # larger than a page
+    # LOCAL store restores its pages on restart
+    m2 = LocalCacheManager(_conf(tmp_path))
+    assert m2.bytes == 16384 and m2.get(PageId("f", 4), 0, 4096) == pages[4]
+    mm = LocalCacheManager(_conf(tmp_path), store=MemPageStore())
+    mm.put(PageId("g", 0), b"abc")
+    assert mm.delete(PageId("g", 0)) and not mm.has(PageId("g", 0))
+
+
+def test_cached_stream_through_filesystem(tmp_path):
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"}) as c:
+        data = np.random.default_rng(1).integers(0, 256, 50_000, dtype=np.uint8).tobytes()
+        plain = c.client()
+        plain.write_file("/cc/f", data, write_type="MUST_CACHE")
+        from alluxio_amd.client.file_system import FileSystem
+        fs = FileSystem(conf=_conf(tmp_path, **{"alluxio.user.client.cache.size": "1MB"}),
+                        master_address=c.master.address)
+        with fs.open_file("/cc/f") as f:
+            assert f.read() == data
+        assert fs.local_cache.bytes == len(data)
+        hits0 = fs.local_cache.metrics.counter("ClientCacheBytesReadCache").count
+        with fs.open_file("/cc/f") as f:
+            f.seek(12_345)
+            assert f.read(9_999) == data[12_345:22_344]
+            buf = bytearray(100)
+            assert f.pread(40_000, buf) == 100 and bytes(buf) == data[40_000:40_100]
+        assert fs.local_cache.metrics.counter("ClientCacheBytesReadCache").count - hits0 >= 10_099
+        fs.close()
+        plain.close()
+
+
+@pytest.mark.gpu
+def test_hbm_page_store_device_reads(gpu, tmp_path):
+    import torch
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"}) as c:
+        data = np.random.default_rng(2).integers(0, 256, 300_000, dtype=np.uint8)
+        c.client().write_file("/hc/f", data, write_type="MUST_CACHE")
+        from alluxio_amd.client.file_system import FileSystem
+        fs = FileSystem(conf=_conf(tmp_path, **{"alluxio.user.client.cache.store.type": "HBM",
+                                                "alluxio.user.client.cache.page.size": "64KB",
+                                                "alluxio.user.client.cache.size": "8MB"}),
+                        master_address=c.master.address)
+        out = torch.empty(250_000, dtype=torch.uint8, device="cuda")
+        with fs.open_file("/hc/f") as f:
+            f.seek(17)
+            assert f.read_into(out) == 250_000
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), data[17:250_017])
+        with fs.open_file("/hc/f") as f:   # second pass: all hits, one gather launch
+            f.seek(17)
+            f.read_into(out)
+        assert np.array_equal(out.cpu().numpy(), data[17:250_017])
+        fs.close()
