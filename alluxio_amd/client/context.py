@@ -67,6 +67,25 @@ class FileSystemContext:
         self._lock = threading.Lock()
         self.worker_list_ttl = self.conf.get_ms("alluxio.user.worker.list.refresh.interval", "2min") / 1000.0
         self._closed = False
+        self._metrics_hb = None
+        if self.conf.get_bool("alluxio.user.metrics.collection.enabled"):
+            from ..utils import heartbeat as hb
+            self._metrics_hb = hb.HeartbeatThread(hb.CLIENT_METRICS_SYNC, self.sync_metrics,
+                                                  self.conf.get_ms("alluxio.user.metrics.heartbeat.interval"))
+            self._metrics_hb.start()
+
+    def sync_metrics(self) -> int:
+        """ClientMasterSync: send this client's metric deltas to the metrics master."""
+        ms = self.metrics.report_metrics()
+        if not ms:
+            return 0
+        cm = pb.metric.ClientMetrics(source=f"{self.hostname}:{self.user}")
+        for name, mtype, value in ms:
+            cm.metrics.add(instance="Client", source=cm.source, name=name, value=value,
+                           metricType=pb.grpc.MetricType.values_by_name[mtype].number)
+        self.metrics_master().MetricsHeartbeat(pb.metric.MetricsHeartbeatPRequest(
+            options=pb.metric.MetricsHeartbeatPOptions(clientMetrics=[cm])))
+        return len(ms)
 
     # ---- stubs --------------------------------------------------------------------------------
     def master_channel(self):
@@ -120,5 +139,8 @@ class FileSystemContext:
         return local_worker(worker_address_str(addr))
 
     def close(self) -> None:
+        if self._metrics_hb is not None:
+            self._metrics_hb.shutdown(join=False)
+            self._metrics_hb = None
         self._closed = True
         self.pool.close()

@@ -142,3 +142,14 @@ def test_async_persist(tmp_path):
         assert st.persisted
         with open(os.path.join(c.ufs_root, "ap", "f"), "rb") as f:
             assert f.read() == b"persist me"
+
+
+def test_client_metrics_sync():
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"}) as c:
+        fs = c.client()
+        fs.write_file("/m/f", b"x" * 1000, write_type="MUST_CACHE")
+        fs.read_file("/m/f")
+        assert fs.ctx.sync_metrics() > 0
+        ms = c.master.metrics_master.get_metrics()
+        assert any("BytesReadClient" in k for k in ms), sorted(ms)[:20]
+        fs.close()
