@@ -303,6 +303,9 @@ def main(argv=None) -> int:  # pragma: no cover - CLI entry
     ap.add_argument("--format", action="store_true")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
+    from ..conf import Configuration as _C
+    from ..web.logserver import attach
+    attach("MASTER", _C(load_site=True))
     m = AlluxioMasterProcess(host=a.host, port=a.port, root_ufs=a.root_ufs)
     if a.format:
         m.format()

@@ -243,6 +243,9 @@ def main(argv=None) -> int:  # pragma: no cover - CLI entry
     ap.add_argument("--device", type=int, default=None)
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
+    from ..conf import Configuration as _C
+    from ..web.logserver import attach
+    attach("WORKER", _C(load_site=True))
     w = AlluxioWorkerProcess(master_address=a.master, host=a.host, port=a.port, device=a.device)
     w.start()
     try:

@@ -266,3 +266,29 @@ def test_web_endpoints(cluster):
     out = io.StringIO()
     assert main(["logLevel", "--logName", "x.y", "--level", "INFO", "--target", f"127.0.0.1:{port}"], out) == 0
     assert "INFO" in out.getvalue()
+
+
+def test_log_server(tmp_path):
+    import logging
+    import time
+    from alluxio_amd.web.logserver import LogServer, RemoteLogHandler
+    srv = LogServer(str(tmp_path / "logs"))
+    port = srv.start()
+    h = RemoteLogHandler("127.0.0.1", port, "MASTER")
+    lg = logging.getLogger("alluxio_amd.test.remote")
+    lg.addHandler(h)
+    lg.setLevel(logging.INFO)
+    lg.info("hello from the master")
+    deadline = time.time() + 5
+    path = None
+    while time.time() < deadline:
+        d = tmp_path / "logs" / "master"
+        files = list(d.glob("*.log")) if d.exists() else []
+        if files and "hello from the master" in files[0].read_text():
+            path = files[0]
+            break
+        time.sleep(0.02)
+    lg.removeHandler(h)
+    h.close()
+    srv.stop()
+    assert path is not None
