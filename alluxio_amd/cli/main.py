@@ -23,6 +23,7 @@ COMMAND is one of:
   fsadmin               Command line tool for use by Alluxio filesystem admins.
   getConf [key]         Look up a configuration key, or print all configuration.
   job                   Command line tool for interacting with the job service.
+  table                 Command line tool for interacting with the table (catalog) service.
   logLevel              Set or get log level of Alluxio servers.
   readJournal           Read an Alluxio journal file from stdin and write a human-readable version of it to stdout.
   runTests              Run all end-to-end tests on an Alluxio cluster.
@@ -143,6 +144,9 @@ def main(argv=None, out=None) -> int:
     if cmd == "fs":
         from .fs_shell import main as m
         return m(rest, out)
+    if cmd == "table":
+        from ..table import TableShell
+        return TableShell(out=out).run(rest)
     if cmd == "fsadmin":
         from .fsadmin import main as m
         return m(rest, out)

@@ -9,7 +9,7 @@ import time
 
 from ..proto import enum_name, pb
 from .plans import (CompositeConfig, EvictConfig, JobConfig, LoadConfig, MigrateConfig, MoveConfig,  # noqa: F401
-                    PersistConfig, ReplicateConfig, StressBenchConfig)
+                    PersistConfig, ReplicateConfig, StressBenchConfig, TransformConfig)
 
 SVC_JOB_CLIENT = "alluxio.grpc.job.JobMasterClientService"
 SVC_JOB_WORKER = "alluxio.grpc.job.JobMasterWorkerService"

@@ -118,6 +118,15 @@ class MigrateConfig(JobConfig):
     delete_source: bool = False
 
 
+@config("transform")
+@dataclasses.dataclass
+class TransformConfig(JobConfig):
+    db: str = ""
+    table: str = ""
+    transform: str = ""      # the transformation definition, e.g. "file.count.max=100"
+    partitions: list = dataclasses.field(default_factory=list)   # [{spec, files, format, dst}]
+
+
 @config("stress")
 @dataclasses.dataclass
 class StressBenchConfig(JobConfig):
@@ -343,6 +352,58 @@ class MigrateDefinition(PlanDefinition):
 
     def join(self, cfg, task_results):
         return {"files": len(task_results), "bytes": sum(v or 0 for v in task_results.values())}
+
+
+@plan("transform")
+class TransformDefinition(PlanDefinition):
+    """Table transformation (reference job/server/.../plan/transform/CompactDefinition.java +
+    format/{csv,parquet}: rewrite each partition's files as at most ``file.count.max`` Parquet
+    files under the transformation's location)."""
+
+    @staticmethod
+    def _max_files(defn: str) -> int:
+        for kv in defn.replace(";", " ").split():
+            k, _, v = kv.partition("=")
+            if k.strip() == "file.count.max":
+                return max(1, int(v))
+        return 100
+
+    def select_executors(self, cfg, job_workers, fs):
+        if not job_workers:
+            raise ex.FailedPreconditionException("no job worker available for transform")
+        return [(job_workers[i % len(job_workers)], p) for i, p in enumerate(cfg.partitions)]
+
+    def run_task(self, cfg, args, ctx):
+        import io
+        import posixpath
+
+        import pyarrow as pa
+        import pyarrow.csv as pcsv
+        import pyarrow.parquet as pq
+        tables = []
+        for f in args["files"]:
+            data = ctx.fs.read_file(f)
+            tables.append(pcsv.read_csv(io.BytesIO(data)) if args["format"] == "csv" else pq.read_table(io.BytesIO(data)))
+        tbl = pa.concat_tables(tables, promote_options="default") if len(tables) > 1 else tables[0]
+        n = min(self._max_files(cfg.transform), max(1, tbl.num_rows))
+        ctx.fs.create_directory(args["dst"], recursive=True, allow_exists=True)
+        per = -(-tbl.num_rows // n)
+        out = []
+        for i in range(n):
+            part = tbl.slice(i * per, per)
+            if part.num_rows == 0 and i > 0:
+                break
+            buf = io.BytesIO()
+            pq.write_table(part, buf)
+            path = posixpath.join(args["dst"], f"part-{i:05d}.parquet")
+            if ctx.fs.exists(path):
+                ctx.fs.delete(path)
+            ctx.fs.write_file(path, buf.getvalue())
+            out.append(path)
+        return {"spec": args["spec"] or "_", "files": out}
+
+    def join(self, cfg, task_results):
+        return {r["spec"]: r["files"] for r in task_results.values() if r}
 
 
 @plan("stress")

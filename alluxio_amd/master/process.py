@@ -93,9 +93,15 @@ class AlluxioMasterProcess:
         self.state_lock = StateLockManager()
         self.fs_master.state_lock = self.state_lock
         self.safe_mode = SafeModeManager(self.conf.get_ms("alluxio.master.worker.connect.wait.time"))
-        for j in (self.block_master, self.fs_master, self.meta_master):
-            self.journal.register(j)
-        self.meta_master.masters_for_backup = [self.block_master, self.fs_master, self.meta_master]
+        self.table_master = None
+        if self.conf.get_bool("alluxio.table.enabled", "true"):
+            from ..table.master import TableMaster
+            self.table_master = TableMaster(self.conf, self.journal, fs_factory=lambda: self._job_fs())
+        for j in (self.block_master, self.fs_master, self.meta_master, self.table_master):
+            if j is not None:
+                self.journal.register(j)
+        self.meta_master.masters_for_backup = [m for m in (self.block_master, self.fs_master, self.meta_master,
+                                                            self.table_master) if m is not None]
         self.meta_master.journal_system_for_checkpoint = self.journal
         self.server = RpcServer(host, self.port, max_workers=self.conf.get_int("alluxio.master.rpc.executor.max.pool.size", 500)
                                 if False else 64, metrics=self.metrics, enable_grpc=enable_grpc)
@@ -107,6 +113,8 @@ class AlluxioMasterProcess:
                                         self.conf.get_int("alluxio.job.master.job.capacity"))
         self._job_client_fs = None
         self.replication_checker = None
+        if self.table_master is not None:
+            self.table_master.job_master = self.job_master
         if self.job_master is not None:
             from .replication import ReplicationChecker
             self.replication_checker = ReplicationChecker(self.fs_master, self.job_master)
@@ -168,6 +176,9 @@ class AlluxioMasterProcess:
             jsvc = JobMasterService(self.job_master)
             s.add_servicer(SVC_JOB_CLIENT, jsvc)
             s.add_servicer(SVC_JOB_WORKER, jsvc)
+        if self.table_master is not None:
+            from ..table.master import SVC_TABLE, TableMasterService
+            s.add_servicer(SVC_TABLE, TableMasterService(self.table_master))
         s.add_servicer(SVC_VERSION, ServiceVersionHandler())
         s.add_servicer(SVC_SASL, SaslHandler())
 
@@ -221,7 +232,7 @@ class AlluxioMasterProcess:
     def gain_primacy(self) -> None:
         backup = self.conf.get_raw("alluxio.master.journal.init.from.backup")
         if backup and self.journal.is_empty():
-            n = restore_backup(backup, [self.block_master, self.fs_master, self.meta_master])
+            n = restore_backup(backup, self.meta_master.masters_for_backup)
             LOG.info("restored %d entries from backup %s", n, backup)
             self.journal.gain_primacy()
             self.journal.checkpoint()
@@ -252,6 +263,9 @@ class AlluxioMasterProcess:
                           c.get_ms("alluxio.master.persistence.checker.interval", "1sec")))
             specs.append((hb.JOB_MASTER_LOST_WORKER_DETECTION, self.job_master.detect_lost_workers,
                           c.get_ms("alluxio.job.master.lost.worker.interval")))
+            if self.table_master is not None:
+                specs.append(("Master Table Transformation Monitor", self.table_master.transform_heartbeat,
+                              c.get_ms("alluxio.table.transform.manager.job.monitor.interval", "10sec")))
             specs.append((hb.MASTER_REPLICATION_CHECK, self.replication_checker.heartbeat,
                           c.get_ms("alluxio.master.replication.check.interval", "1min")))
             retention = c.get_ms("alluxio.job.master.finished.job.retention.time") / 1000.0

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import types
 
-from .defs import block, common, file, journal, meta, metric
+from .defs import block, common, file, journal, meta, metric, table
 from .dsl import Schema
 
 _ALIASES = {
@@ -27,10 +27,11 @@ _ALIASES = {
     "alluxio.grpc.meta": "meta",
     "alluxio.grpc.job": "job",
     "alluxio.grpc.journal": "journal_master",
+    "alluxio.grpc.table": "table",
 }
 
 SCHEMA = Schema()
-for _mod in (common, block, file, journal, metric, meta):
+for _mod in (common, block, file, journal, metric, meta, table):
     SCHEMA.add(_mod.SCHEMA)
 SCHEMA.build()
 
