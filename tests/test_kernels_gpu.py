@@ -55,9 +55,11 @@ def test_crc32c_matches_host(gpu):
         assert got == want, (nbytes, piece)
 
 
-def test_lz4_device_roundtrip(gpu):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_lz4_device_roundtrip(gpu, variant):
     import torch
     C = lib()
+    C.set_lz4_decode_variant(variant)
     rng = np.random.default_rng(1)
     chunks = []
     for i in range(12):
@@ -89,6 +91,7 @@ def test_lz4_device_roundtrip(gpu):
     for raw, e, sz in zip(chunks, enc, sizes):
         assert sz > 0
         assert C.lz4_decompress(e[:sz].cpu().numpy().tobytes(), len(raw)) == raw
+    C.set_lz4_decode_variant(1)
 
 
 def _host_select(crf, last, nbytes, ev, now, step, att, policy, need):

@@ -87,9 +87,23 @@ def main():
     csrc = torch.tensor(list(comp) * 1, dtype=torch.uint8, device=dev)
     out = torch.empty(nchunks * 65536, dtype=torch.uint8, device=dev)
     chunks = [(csrc.data_ptr(), out.data_ptr() + i * 65536, len(comp), 65536) for i in range(nchunks)]
-    t = timeit(lambda: C.lz4_device(chunks, False, 0), 5, 1)
-    emit(case="lz4_decode", chunks=nchunks, ratio=len(raw) / len(comp), ms=t * 1e3,
-         out_GBps=nchunks * 65536 / t / 1e9)
+    for variant in (0, 1):
+        C.set_lz4_decode_variant(variant)
+        t = timeit(lambda: C.lz4_device(chunks, False, 0), 5, 1)
+        emit(case="lz4_decode", variant=variant, data="random 0..7", chunks=nchunks, ratio=len(raw) / len(comp),
+             ms=t * 1e3, out_GBps=nchunks * 65536 / t / 1e9)
+    # text-like data with long repeats (typical log/CSV blocks)
+    words = [b"alluxio", b"worker", b"block", b"hbm", b"page", b"read", b"mi355x", b"cache", b"\n", b",", b" "]
+    txt = b"".join(words[i] for i in rng.integers(0, len(words), 40000))[:1 << 16]
+    tcomp = C.lz4_compress(txt)
+    tsrc = torch.tensor(list(tcomp), dtype=torch.uint8, device=dev)
+    tchunks = [(tsrc.data_ptr(), out.data_ptr() + i * 65536, len(tcomp), 65536) for i in range(nchunks)]
+    for variant in (0, 1):
+        C.set_lz4_decode_variant(variant)
+        t = timeit(lambda: C.lz4_device(tchunks, False, 0), 5, 1)
+        emit(case="lz4_decode", variant=variant, data="text", chunks=nchunks, ratio=len(txt) / len(tcomp),
+             ms=t * 1e3, out_GBps=nchunks * 65536 / t / 1e9)
+    C.set_lz4_decode_variant(1)
     enc = torch.empty(nchunks * C.lz4_compress_bound(65536), dtype=torch.uint8, device=dev)
     cb = C.lz4_compress_bound(65536)
     echunks = [(out.data_ptr() + i * 65536, enc.data_ptr() + i * cb, 65536, cb) for i in range(nchunks)]
