@@ -585,7 +585,95 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_direct_kernel(const
   }
 }
 
-static int g_lz4_decode_variant = 1;  // 0: LDS-window kernel, 1: direct-to-HBM kernel
+// Variant 2: as the direct kernel, but the token/length/offset parse reads the compressed stream
+// from a 4 KiB LDS staging buffer refilled lane-parallel (one 64-byte strip per lane), so each
+// sequence costs LDS latency instead of 3-4 dependent HBM/L2 round trips; literal runs are
+// still copied lane-parallel straight from HBM.
+constexpr uint32_t kLzIn = 4096;
+
+__global__ __launch_bounds__(kLzThreads) void lz4_decompress_staged_kernel(const Lz4Chunk* __restrict__ ch,
+                                                                          int n, int32_t* __restrict__ out_sizes) {
+  __shared__ uint8_t inb[kLzIn];
+  const int lane = threadIdx.x;
+  for (int w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(ch[w].src);
+    const uint32_t slen = ch[w].src_bytes;
+    uint8_t* const dst = reinterpret_cast<uint8_t*>(ch[w].dst);
+    const uint32_t cap = ch[w].dst_capacity;
+    uint32_t base = 0, valid = 0;
+    auto refill = [&](uint32_t pos) {
+      __syncthreads();
+      const uint32_t avail = slen - pos < kLzIn ? slen - pos : kLzIn;
+      for (uint32_t i = lane; i < avail; i += kLzThreads) inb[i] = src[pos + i];
+      base = pos;
+      valid = avail;
+      __syncthreads();
+    };
+    auto at = [&](uint32_t pos) -> uint32_t {
+      if (pos - base >= valid) refill(pos);
+      return inb[pos - base];
+    };
+    uint32_t ip = 0, op = 0, fenced = 0;
+    int32_t status = 0;
+    while (ip < slen) {
+      const uint32_t token = at(ip++);
+      uint32_t lit = token >> 4;
+      if (lit == 15) {
+        uint32_t b;
+        do {
+          if (ip >= slen) { status = -1; break; }
+          b = at(ip++);
+          lit += b;
+        } while (b == 255);
+        if (status) break;
+      }
+      if (ip + lit > slen || op + lit > cap) { status = -2; break; }
+      if (ip - base + lit <= valid) {
+        for (uint32_t i = lane; i < lit; i += kLzThreads) dst[op + i] = inb[ip - base + i];
+      } else {
+        for (uint32_t i = lane; i < lit; i += kLzThreads) dst[op + i] = src[ip + i];
+      }
+      ip += lit;
+      op += lit;
+      if (ip >= slen) break;  // last sequence carries literals only
+      if (ip + 2 > slen) { status = -3; break; }
+      const uint32_t off = at(ip) | (at(ip + 1) << 8);
+      ip += 2;
+      uint32_t ml = token & 15;
+      if (ml == 15) {
+        uint32_t b;
+        do {
+          if (ip >= slen) { status = -4; break; }
+          b = at(ip++);
+          ml += b;
+        } while (b == 255);
+        if (status) break;
+      }
+      ml += 4;
+      if (off == 0 || off > op || op + ml > cap) { status = -5; break; }
+      if (op - off + (ml < off ? ml : off) > fenced) {
+        __threadfence_block();
+        fenced = op;
+      }
+      if (off >= ml) {
+        for (uint32_t i = lane; i < ml; i += kLzThreads) dst[op + i] = dst[op - off + i];
+      } else {
+        const uint32_t stride = off < (uint32_t)kLzThreads ? off : (uint32_t)kLzThreads;
+        for (uint32_t b0 = 0; b0 < ml; b0 += stride) {
+          const uint32_t i = b0 + lane;
+          if (lane < (int)stride && i < ml) dst[op + i] = dst[op - off + i];
+          __threadfence_block();
+        }
+        fenced = op + ml;
+      }
+      op += ml;
+    }
+    if (lane == 0) out_sizes[w] = status ? status : (int32_t)op;
+    __syncthreads();
+  }
+}
+
+static int g_lz4_decode_variant = 2;  // 0: LDS window, 1: direct-to-HBM, 2: direct + LDS-staged parse
 
 void set_lz4_decode_variant(int v) { g_lz4_decode_variant = v; }
 
@@ -596,9 +684,13 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
     const unsigned grid = (unsigned)std::min(n, 4096);
     hipLaunchKernelGGL(lz4_decompress_kernel, dim3(grid), dim3(kLzThreads), kLzWindow, stream,
                        chunks, n, out_sizes);
-  } else {
+  } else if (g_lz4_decode_variant == 1) {
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL(lz4_decompress_direct_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
+                       chunks, n, out_sizes);
+  } else {
+    const unsigned grid = (unsigned)std::min(n, 65536);
+    hipLaunchKernelGGL(lz4_decompress_staged_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
                        chunks, n, out_sizes);
   }
   return hipGetLastError();
