@@ -673,7 +673,109 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_staged_kernel(const
   }
 }
 
-static int g_lz4_decode_variant = 2;  // 0: LDS window, 1: direct-to-HBM, 2: direct + LDS-staged parse
+// Variant 3: variant 2 plus an 8 KiB LDS ring mirroring the most recent output, so matches with
+// offset <= 8 KiB (the bulk of real LZ4 streams) read their source from LDS: the per-sequence
+// dependency chain has no HBM load left (output still streams to HBM with plain stores).
+constexpr uint32_t kLzRing = 8192;
+
+__global__ __launch_bounds__(kLzThreads) void lz4_decompress_ring_kernel(const Lz4Chunk* __restrict__ ch,
+                                                                        int n, int32_t* __restrict__ out_sizes) {
+  __shared__ uint8_t inb[kLzIn];
+  __shared__ uint8_t ring[kLzRing];
+  constexpr uint32_t rmask = kLzRing - 1;
+  const int lane = threadIdx.x;
+  for (int w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(ch[w].src);
+    const uint32_t slen = ch[w].src_bytes;
+    uint8_t* const dst = reinterpret_cast<uint8_t*>(ch[w].dst);
+    const uint32_t cap = ch[w].dst_capacity;
+    uint32_t base = 0, valid = 0;
+    auto refill = [&](uint32_t pos) {
+      __syncthreads();
+      const uint32_t avail = slen - pos < kLzIn ? slen - pos : kLzIn;
+      for (uint32_t i = lane; i < avail; i += kLzThreads) inb[i] = src[pos + i];
+      base = pos;
+      valid = avail;
+      __syncthreads();
+    };
+    auto at = [&](uint32_t pos) -> uint32_t {
+      if (pos - base >= valid) refill(pos);
+      return inb[pos - base];
+    };
+    uint32_t ip = 0, op = 0, fenced = 0;
+    int32_t status = 0;
+    while (ip < slen) {
+      const uint32_t token = at(ip++);
+      uint32_t lit = token >> 4;
+      if (lit == 15) {
+        uint32_t b;
+        do {
+          if (ip >= slen) { status = -1; break; }
+          b = at(ip++);
+          lit += b;
+        } while (b == 255);
+        if (status) break;
+      }
+      if (ip + lit > slen || op + lit > cap) { status = -2; break; }
+      const bool in_lds = ip - base + lit <= valid;
+      for (uint32_t i = lane; i < lit; i += kLzThreads) {
+        const uint8_t v = in_lds ? inb[ip - base + i] : src[ip + i];
+        dst[op + i] = v;
+        ring[(op + i) & rmask] = v;
+      }
+      ip += lit;
+      op += lit;
+      if (ip >= slen) break;  // last sequence carries literals only
+      if (ip + 2 > slen) { status = -3; break; }
+      const uint32_t off = at(ip) | (at(ip + 1) << 8);
+      ip += 2;
+      uint32_t ml = token & 15;
+      if (ml == 15) {
+        uint32_t b;
+        do {
+          if (ip >= slen) { status = -4; break; }
+          b = at(ip++);
+          ml += b;
+        } while (b == 255);
+        if (status) break;
+      }
+      ml += 4;
+      if (off == 0 || off > op || op + ml > cap) { status = -5; break; }
+      __syncthreads();  // ring writes of the literals visible to every lane
+      if (off <= kLzRing - kLzThreads) {
+        const uint32_t stride = off < (uint32_t)kLzThreads ? off : (uint32_t)kLzThreads;
+        for (uint32_t b0 = 0; b0 < ml; b0 += stride) {
+          const uint32_t i = b0 + lane;
+          uint8_t v = 0;
+          if (lane < (int)stride && i < ml) v = ring[(op - off + i) & rmask];
+          __syncthreads();
+          if (lane < (int)stride && i < ml) {
+            dst[op + i] = v;
+            ring[(op + i) & rmask] = v;
+          }
+          __syncthreads();
+        }
+      } else {
+        // far match (> ring): source is older output in HBM; fence only if it is unfenced
+        if (op - off + ml > fenced) {
+          __threadfence_block();
+          fenced = op;
+        }
+        for (uint32_t i = lane; i < ml; i += kLzThreads) {
+          const uint8_t v = dst[op - off + i];
+          dst[op + i] = v;
+          ring[(op + i) & rmask] = v;
+        }
+        __syncthreads();
+      }
+      op += ml;
+    }
+    if (lane == 0) out_sizes[w] = status ? status : (int32_t)op;
+    __syncthreads();
+  }
+}
+
+static int g_lz4_decode_variant = 3;  // 0: LDS window, 1: direct, 2: direct + staged parse, 3: + LDS ring
 
 void set_lz4_decode_variant(int v) { g_lz4_decode_variant = v; }
 
@@ -688,9 +790,13 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL(lz4_decompress_direct_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
                        chunks, n, out_sizes);
-  } else {
+  } else if (g_lz4_decode_variant == 2) {
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL(lz4_decompress_staged_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
+                       chunks, n, out_sizes);
+  } else {
+    const unsigned grid = (unsigned)std::min(n, 65536);
+    hipLaunchKernelGGL(lz4_decompress_ring_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
                        chunks, n, out_sizes);
   }
   return hipGetLastError();

@@ -87,7 +87,7 @@ def main():
     csrc = torch.tensor(list(comp) * 1, dtype=torch.uint8, device=dev)
     out = torch.empty(nchunks * 65536, dtype=torch.uint8, device=dev)
     chunks = [(csrc.data_ptr(), out.data_ptr() + i * 65536, len(comp), 65536) for i in range(nchunks)]
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, 3):
         C.set_lz4_decode_variant(variant)
         t = timeit(lambda: C.lz4_device(chunks, False, 0), 5, 1)
         emit(case="lz4_decode", variant=variant, data="random 0..7", chunks=nchunks, ratio=len(raw) / len(comp),
@@ -98,12 +98,12 @@ def main():
     tcomp = C.lz4_compress(txt)
     tsrc = torch.tensor(list(tcomp), dtype=torch.uint8, device=dev)
     tchunks = [(tsrc.data_ptr(), out.data_ptr() + i * 65536, len(tcomp), 65536) for i in range(nchunks)]
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, 3):
         C.set_lz4_decode_variant(variant)
         t = timeit(lambda: C.lz4_device(tchunks, False, 0), 5, 1)
         emit(case="lz4_decode", variant=variant, data="text", chunks=nchunks, ratio=len(txt) / len(tcomp),
              ms=t * 1e3, out_GBps=nchunks * 65536 / t / 1e9)
-    C.set_lz4_decode_variant(2)
+    C.set_lz4_decode_variant(3)
     enc = torch.empty(nchunks * C.lz4_compress_bound(65536), dtype=torch.uint8, device=dev)
     cb = C.lz4_compress_bound(65536)
     echunks = [(out.data_ptr() + i * 65536, enc.data_ptr() + i * cb, 65536, cb) for i in range(nchunks)]
