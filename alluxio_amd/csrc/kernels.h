@@ -75,7 +75,7 @@ struct Lz4Chunk {
 };
 hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
                                  hipStream_t stream);
-// 0: LDS-window decoder, 1: direct-to-HBM, 2: direct + LDS-staged parse, 3 (default): + LDS ring
+// 0: LDS-window decoder, 1: direct-to-HBM, 2 (default): direct + LDS-staged parse, 3: + LDS ring
 // of recent output for near matches.
 void set_lz4_decode_variant(int v);
 // LZ4 block compression (greedy, one wave per chunk, LDS hash table).  out_sizes[i] = -1 if

@@ -775,7 +775,7 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_ring_kernel(const L
   }
 }
 
-static int g_lz4_decode_variant = 3;  // 0: LDS window, 1: direct, 2: direct + staged parse, 3: + LDS ring
+static int g_lz4_decode_variant = 2;  // 0: LDS window, 1: direct, 2: direct + staged parse (fastest, default), 3: + LDS ring
 
 void set_lz4_decode_variant(int v) { g_lz4_decode_variant = v; }
 
