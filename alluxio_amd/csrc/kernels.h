@@ -63,7 +63,9 @@ void set_seq_read_variant(int variant, unsigned grid_cap);
 hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint64_t piece_bytes,
                                 uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
                                 hipStream_t stream);
-// Scratch words needed by launch_crc32c_pieces.
+// 0: per-lane contiguous strips, 1 (default): interleaved coalesced lanes.
+void set_crc_variant(int v);
+// Scratch words needed by launch_crc32c_pieces (an upper bound for every variant).
 uint64_t crc32c_scratch_words(uint64_t total_bytes, uint64_t piece_bytes);
 
 // LZ4 block decompression of `n` independent chunks.

@@ -257,6 +257,8 @@ constexpr uint64_t kCrcLane = kCrcSeg / kCrcThreads;  // 256 B per lane
 
 __constant__ uint32_t c_crc_tab[8][256];
 __constant__ uint32_t c_x2n[64];  // x^(2^k) mod P, k = 0..63
+__constant__ uint32_t c_crc16[16][256];   // slicing-by-16 (zero-init CRC of a 16-byte word)
+__constant__ uint32_t c_shift4k[4][256];  // c -> c * x^(8*4096) mod P, byte-sliced
 
 static void host_crc_tables(uint32_t tab[8][256], uint32_t x2n[64]) {
   for (uint32_t i = 0; i < 256; ++i) {
@@ -281,6 +283,26 @@ static void host_crc_tables(uint32_t tab[8][256], uint32_t x2n[64]) {
   for (int k = 1; k < 64; ++k) { p = mult(p, p); x2n[k] = p; }
 }
 
+static uint32_t host_gf2_mult(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (uint32_t m = 1u << 31; m; m >>= 1) {
+    if (a & m) p ^= b;
+    b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+
+static void host_crc16_tables(const uint32_t tab8[8][256], const uint32_t x2n[64], uint32_t t16[16][256],
+                              uint32_t sh[4][256]) {
+  for (uint32_t i = 0; i < 256; ++i) t16[0][i] = tab8[0][i];
+  for (int t = 1; t < 16; ++t)
+    for (uint32_t i = 0; i < 256; ++i) t16[t][i] = (t16[t - 1][i] >> 8) ^ t16[0][t16[t - 1][i] & 0xFF];
+  // x^(8*4096) = x^(2^15)
+  const uint32_t k = x2n[15];
+  for (int b = 0; b < 4; ++b)
+    for (uint32_t i = 0; i < 256; ++i) sh[b][i] = host_gf2_mult(k, i << (8 * b));
+}
+
 static std::once_flag g_crc_once;
 static hipError_t g_crc_init_err = hipSuccess;
 
@@ -289,9 +311,16 @@ static hipError_t ensure_crc_tables() {
     static uint32_t tab[8][256];
     static uint32_t x2n[64];
     host_crc_tables(tab, x2n);
+    static uint32_t t16[16][256];
+    static uint32_t sh[4][256];
+    host_crc16_tables(tab, x2n, t16, sh);
     g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_crc_tab), tab, sizeof(tab));
     if (g_crc_init_err == hipSuccess)
       g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), x2n, sizeof(x2n));
+    if (g_crc_init_err == hipSuccess)
+      g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_crc16), t16, sizeof(t16));
+    if (g_crc_init_err == hipSuccess)
+      g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_shift4k), sh, sizeof(sh));
   });
   return g_crc_init_err;
 }
@@ -376,8 +405,87 @@ __global__ __launch_bounds__(kCrcThreads) void crc32c_segments_kernel(
   }
 }
 
+// v2: interleaved lanes.  Lane l reads 16-B words l, l+256, l+512, ... of the segment (a wave
+// reads 1 KiB contiguous per instruction: fully coalesced), keeping c_l = sum_k crc16(w_k) *
+// x^(8*4096*(K-1-k)) via c = shift4k(c) ^ crc16(w) (4 + 16 LDS lookups per 16 B, no dependency
+// on other lanes).  At the end each lane's contribution is moved to its final position with one
+// multiply by x^(8*bytes-after-its-last-word) and the block XOR-reduces; the <16-B tail is folded
+// in by lane 0.  Produces the same raw (zero-init) segment CRC as v1.
+constexpr uint64_t kCrcSeg2 = 256 * 1024;
+
+__global__ __launch_bounds__(kCrcThreads) void crc32c_segments_v2_kernel(
+    const uint8_t* __restrict__ base, uint64_t total_bytes, uint64_t piece_bytes, uint64_t seg_bytes,
+    uint64_t segs_per_piece, uint64_t nsegs, uint32_t* __restrict__ seg_crc) {
+  __shared__ uint32_t t16[16][256];
+  __shared__ uint32_t sh[4][256];
+  __shared__ uint32_t part[kCrcThreads];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 16 * 256; i += kCrcThreads) t16[i >> 8][i & 255] = c_crc16[i >> 8][i & 255];
+  for (int i = tid; i < 4 * 256; i += kCrcThreads) sh[i >> 8][i & 255] = c_shift4k[i >> 8][i & 255];
+  __syncthreads();
+  for (uint64_t g = blockIdx.x; g < nsegs; g += gridDim.x) {
+    const uint64_t piece = g / segs_per_piece;
+    const uint64_t seg_in_piece = g % segs_per_piece;
+    const uint64_t piece_start = piece * piece_bytes;
+    const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
+    const uint64_t seg_start = piece_start + seg_in_piece * seg_bytes;
+    const uint64_t seg_len = std::min(seg_bytes, piece_start + piece_len - seg_start);
+    const uint8_t* seg = base + seg_start;
+    const uint64_t nwords = seg_len >> 4;
+    uint32_t c = 0;
+    uint64_t last = ~0ull;
+    if ((((uintptr_t)seg) & 15) == 0) {
+      for (uint64_t wi = tid; wi < nwords; wi += kCrcThreads) {
+        const uint4 v = *reinterpret_cast<const uint4*>(seg + (wi << 4));
+        const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+        const uint32_t w = t16[15][v.x & 255] ^ t16[14][(v.x >> 8) & 255] ^ t16[13][(v.x >> 16) & 255] ^
+                           t16[12][v.x >> 24] ^ t16[11][v.y & 255] ^ t16[10][(v.y >> 8) & 255] ^
+                           t16[9][(v.y >> 16) & 255] ^ t16[8][v.y >> 24] ^ t16[7][v.z & 255] ^
+                           t16[6][(v.z >> 8) & 255] ^ t16[5][(v.z >> 16) & 255] ^ t16[4][v.z >> 24] ^
+                           t16[3][v.w & 255] ^ t16[2][(v.w >> 8) & 255] ^ t16[1][(v.w >> 16) & 255] ^
+                           t16[0][v.w >> 24];
+        c = (wi < (uint64_t)kCrcThreads ? 0u : s) ^ w;
+        last = wi;
+      }
+    } else {
+      // unaligned segment: same schedule with byte loads
+      for (uint64_t wi = tid; wi < nwords; wi += kCrcThreads) {
+        const uint8_t* q = seg + (wi << 4);
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) w ^= t16[15 - b][q[b]];
+        const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+        c = (wi < (uint64_t)kCrcThreads ? 0u : s) ^ w;
+        last = wi;
+      }
+    }
+    // move the lane's contribution to its position: bytes after its last word inside the words area
+    uint32_t contrib = 0;
+    if (last != ~0ull) contrib = gf2_mult(xpow8n((nwords - 1 - last) << 4), c);
+    part[tid] = contrib;
+    __syncthreads();
+    for (int s2 = kCrcThreads / 2; s2 > 0; s2 >>= 1) {
+      if (tid < s2) part[tid] ^= part[tid + s2];
+      __syncthreads();
+    }
+    if (tid == 0) {
+      uint32_t acc = part[0];
+      const uint64_t tail = seg_len & 15;
+      if (tail) {
+        acc = gf2_mult(xpow8n(tail), acc);
+        uint32_t t = 0;
+        const uint8_t* q = seg + (nwords << 4);
+        for (uint64_t b = 0; b < tail; ++b) t = (t >> 8) ^ t16[0][(t ^ q[b]) & 255];
+        acc ^= t;
+      }
+      seg_crc[g] = acc;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(kCrcThreads) void crc32c_pieces_kernel(
-    const uint32_t* __restrict__ seg_crc, uint64_t total_bytes, uint64_t piece_bytes,
+    const uint32_t* __restrict__ seg_crc, uint64_t total_bytes, uint64_t piece_bytes, uint64_t seg_bytes,
     uint64_t segs_per_piece, uint64_t npieces, uint32_t* __restrict__ out) {
   __shared__ uint32_t part[kCrcThreads];
   __shared__ uint64_t plen[kCrcThreads];
@@ -385,14 +493,14 @@ __global__ __launch_bounds__(kCrcThreads) void crc32c_pieces_kernel(
   for (uint64_t pc = blockIdx.x; pc < npieces; pc += gridDim.x) {
     const uint64_t piece_start = pc * piece_bytes;
     const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
-    const uint64_t nseg = (piece_len + kCrcSeg - 1) / kCrcSeg;
+    const uint64_t nseg = (piece_len + seg_bytes - 1) / seg_bytes;
     const uint64_t per = (nseg + kCrcThreads - 1) / kCrcThreads;
     const uint64_t s0 = std::min<uint64_t>((uint64_t)tid * per, nseg);
     const uint64_t s1 = std::min<uint64_t>(s0 + per, nseg);
     uint32_t c = 0;
     uint64_t len = 0;
     for (uint64_t s = s0; s < s1; ++s) {
-      const uint64_t sl = std::min(kCrcSeg, piece_len - s * kCrcSeg);
+      const uint64_t sl = std::min(seg_bytes, piece_len - s * seg_bytes);
       c = gf2_mult(xpow8n(sl), c) ^ seg_crc[pc * segs_per_piece + s];
       len += sl;
     }
@@ -422,6 +530,10 @@ uint64_t crc32c_scratch_words(uint64_t total_bytes, uint64_t piece_bytes) {
   return npieces * spp;
 }
 
+static int g_crc_variant = 1;  // 0: per-lane contiguous strips (v1), 1: interleaved lanes (v2)
+
+void set_crc_variant(int v) { g_crc_variant = v; }
+
 hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint64_t piece_bytes,
                                 uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
                                 hipStream_t stream) {
@@ -429,17 +541,23 @@ hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint6
   hipError_t e = ensure_crc_tables();
   if (e != hipSuccess) return e;
   const uint64_t npieces = (total_bytes + piece_bytes - 1) / piece_bytes;
-  const uint64_t spp = (piece_bytes + kCrcSeg - 1) / kCrcSeg;
+  const uint64_t seg = g_crc_variant == 0 ? kCrcSeg : kCrcSeg2;
+  const uint64_t spp = (piece_bytes + seg - 1) / seg;
   const uint64_t nsegs = npieces * spp;
   if (scratch_words < nsegs) return hipErrorInvalidValue;
-  const unsigned g1 = (unsigned)std::min<uint64_t>(nsegs, 4096);
-  hipLaunchKernelGGL(crc32c_segments_kernel, dim3(g1), dim3(kCrcThreads), 0, stream, base,
-                     total_bytes, piece_bytes, spp, nsegs, scratch);
+  const unsigned g1 = (unsigned)std::min<uint64_t>(nsegs, 8192);
+  if (g_crc_variant == 0) {
+    hipLaunchKernelGGL(crc32c_segments_kernel, dim3(g1), dim3(kCrcThreads), 0, stream, base,
+                       total_bytes, piece_bytes, spp, nsegs, scratch);
+  } else {
+    hipLaunchKernelGGL(crc32c_segments_v2_kernel, dim3(g1), dim3(kCrcThreads), 0, stream, base,
+                       total_bytes, piece_bytes, seg, spp, nsegs, scratch);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const unsigned g2 = (unsigned)std::min<uint64_t>(npieces, 4096);
   hipLaunchKernelGGL(crc32c_pieces_kernel, dim3(g2), dim3(kCrcThreads), 0, stream, scratch,
-                     total_bytes, piece_bytes, spp, npieces, out);
+                     total_bytes, piece_bytes, seg, spp, npieces, out);
   return hipGetLastError();
 }
 

@@ -42,17 +42,20 @@ def test_batched_copy_exact(gpu):
         assert torch.equal(src[o:o + n], dst[o:o + n])
 
 
-def test_crc32c_matches_host(gpu):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_crc32c_matches_host(gpu, variant):
     import torch
     C = lib()
-    for nbytes, piece in [(1, 0), (1000, 0), (65536, 0), ((2 << 20) + 13, 1 << 20), (5 << 20, 2 << 20),
-                          (3 << 20, 64 << 10)]:
+    C.set_crc_variant(variant)
+    for nbytes, piece in [(1, 0), (15, 0), (1000, 0), (65536, 0), (4111, 0), ((2 << 20) + 13, 1 << 20),
+                          (5 << 20, 2 << 20), (3 << 20, 64 << 10), ((1 << 20) + 4097, 300_001)]:
         t = _t(nbytes, gpu)
         host = t.cpu().numpy().tobytes()
         got = C.crc32c_device(t.data_ptr(), nbytes, piece, 0)
         p = piece or nbytes
         want = [C.crc32c(host[i:i + p]) for i in range(0, nbytes, p)]
-        assert got == want, (nbytes, piece)
+        assert got == want, (variant, nbytes, piece)
+    C.set_crc_variant(1)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
