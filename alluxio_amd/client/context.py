@@ -59,7 +59,7 @@ class FileSystemContext:
         self.master_address = self.master_addresses[0]
         self._master_ch = None
         self.user = user or login_user(self.conf)
-        self.pool = ChannelPool()
+        self.pool = ChannelPool(self.conf)
         self.metrics = msys.metrics("Client")
         self.hostname = socket.gethostname()
         self._workers = None

@@ -104,7 +104,8 @@ class AlluxioMasterProcess:
                                                             self.table_master) if m is not None]
         self.meta_master.journal_system_for_checkpoint = self.journal
         self.server = RpcServer(host, self.port, max_workers=self.conf.get_int("alluxio.master.rpc.executor.max.pool.size", 500)
-                                if False else 64, metrics=self.metrics, enable_grpc=enable_grpc)
+                                if False else 64, metrics=self.metrics, enable_grpc=enable_grpc,
+                                conf=self.conf)
         self._threads: list[hb.HeartbeatThread] = []
         self.job_master = None
         if self.conf.get_bool("alluxio.job.master.embedded.enabled", "true"):

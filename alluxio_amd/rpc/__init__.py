@@ -71,29 +71,42 @@ def _status_of(e: BaseException) -> tuple[grpc.StatusCode, str]:
     return code, se.message or str(se)
 
 
-def _user_from_metadata(context) -> str | None:
+def _metadata(context, key: str) -> str | None:
     try:
         for k, v in context.invocation_metadata() or ():
-            if k == "alluxio-user":
+            if k == key:
                 return v
     except Exception:  # noqa: BLE001
         return None
     return None
 
 
+def _user_from_metadata(context) -> str | None:
+    return _metadata(context, "alluxio-user")
+
+
+_UNAUTH_SERVICES = ("alluxio.grpc.sasl.SaslAuthenticationService", "alluxio.grpc.version.ServiceVersionClientService")
+
+
 class _Handler:
     """Wraps servicer methods: user propagation, error mapping, metrics."""
 
-    def __init__(self, servicer, spec, metrics=None, gate=None):
+    def __init__(self, servicer, spec, metrics=None, gate=None, authenticator=None):
         self.servicer = servicer
         self.spec = spec
         self.fn = getattr(servicer, spec.name)
         self.metrics = metrics
         self.gate = gate
+        self.auth = authenticator
 
     def _enter(self, context):
         from ..security import as_user
-        return as_user(_user_from_metadata(context))
+        if self.auth is None:
+            return as_user(_user_from_metadata(context))
+        if self.spec.service in _UNAUTH_SERVICES:
+            return as_user(None)
+        # the user comes from the authenticated channel, never from a per-call claim
+        return as_user(self.auth.user_for(_metadata(context, "channel-id")))
 
     def unary(self, request, context):
         t0 = time.perf_counter()
@@ -130,8 +143,13 @@ class _Handler:
 
 class RpcServer:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, max_workers: int = 64, metrics=None,
-                 enable_grpc: bool = True):
+                 enable_grpc: bool = True, conf=None):
         self.host = host
+        # SASL channel authentication (None = NOSASL: trust the alluxio-user header)
+        self.authenticator = None
+        if conf is not None:
+            from ..security.authentication import ServerAuthenticator
+            self.authenticator = ServerAuthenticator.from_conf(conf)
         self.port = port
         self.max_workers = max_workers
         self.metrics = metrics
@@ -155,6 +173,8 @@ class RpcServer:
         self._servicers[service_full_name] = servicer
 
     def start(self) -> str:
+        if self.authenticator is not None:
+            self._servicers["alluxio.grpc.sasl.SaslAuthenticationService"] = self.authenticator
         if self.enable_grpc:
             self._server = grpc.server(futures.ThreadPoolExecutor(max_workers=self.max_workers,
                                                                   thread_name_prefix="rpc"),
@@ -166,7 +186,7 @@ class RpcServer:
                 for name, spec in SERVICES[svc].items():
                     if not hasattr(servicer, name):
                         continue
-                    h = _Handler(servicer, spec, self.metrics, self.check)
+                    h = _Handler(servicer, spec, self.metrics, self.check, self.authenticator)
                     des, ser = spec.request.FromString, spec.response.SerializeToString
                     if spec.client_streaming and spec.server_streaming:
                         handlers[name] = grpc.stream_stream_rpc_method_handler(h.stream, des, ser)
@@ -254,9 +274,14 @@ class Stub:
 
 
 class Channel:
-    def __init__(self, address: str, user: str | None = None, force_grpc: bool = False):
+    def __init__(self, address: str, user: str | None = None, force_grpc: bool = False, auth="default"):
         self.address = address
         self.user = user
+        if auth == "default":      # SIMPLE as the login user (servers without SASL are tolerated)
+            from ..security import login_user
+            auth = ("SIMPLE", user or login_user(), "")
+        self.auth = auth            # (type, user, password) or None (NOSASL)
+        self.channel_id = None
         with _LOCAL_LOCK:
             local = None if force_grpc else _LOCAL.get(address)
         self.local = local
@@ -273,7 +298,40 @@ class Channel:
                 self._grpc = grpc.insecure_channel(self.address, options=[
                     ("grpc.max_receive_message_length", MAX_MESSAGE),
                     ("grpc.max_send_message_length", MAX_MESSAGE)])
+                if self.auth is not None:
+                    self._authenticate(self._grpc)
             return self._grpc
+
+    def _authenticate(self, ch) -> None:
+        """SASL PLAIN handshake once per channel (ChannelAuthenticator.authenticate)."""
+        import uuid
+        from ..proto import pb
+        from ..security.authentication import SCHEMES, plain_payload
+        atype, user, password = self.auth
+        cid = str(uuid.uuid4())
+        spec = SERVICES["alluxio.grpc.sasl.SaslAuthenticationService"]["authenticate"]
+        call = ch.stream_stream(spec.path, spec.request.SerializeToString, spec.response.FromString)
+        msg = pb.sasl.SaslMessage(messageType=0, message=plain_payload(user or self.user or "", password),
+                                  clientId=cid, channelRef=cid, authenticationScheme=SCHEMES[atype])
+        try:
+            for resp in call(iter([msg]), timeout=30):
+                if resp.messageType == 1:
+                    self.channel_id = cid
+                break
+        except grpc.RpcError as e:
+            if e.code() == grpc.StatusCode.UNIMPLEMENTED:
+                return  # NOSASL server: no channel authentication
+            raise ex.AlluxioStatusException.from_status(e.code().value[0], e.details() or str(e)) from None
+        if self.channel_id is None:
+            raise ex.UnauthenticatedException(f"authentication with {self.address} failed")
+
+    def _md(self):
+        md = []
+        if self.user:
+            md.append(("alluxio-user", self.user))
+        if self.channel_id:
+            md.append(("channel-id", self.channel_id))
+        return tuple(md) or None
 
     def method(self, service, spec):
         if self.local is not None:
@@ -293,8 +351,7 @@ class Channel:
             c = ch.unary_stream(spec.path, ser, des)
         else:
             c = ch.unary_unary(spec.path, ser, des)
-        md = (("alluxio-user", self.user),) if self.user else None
-        return _GrpcMethod(c, spec, md)
+        return _GrpcMethod(c, spec, self._md())
 
     def stub(self, service: str) -> Stub:
         return Stub(self, service)
@@ -314,7 +371,7 @@ class Channel:
             return call
         ch = self._channel()
         c = ch.stream_stream(spec.path, spec.request.SerializeToString, spec.response.FromString)
-        md = (("alluxio-user", self.user),) if self.user else None
+        md = self._md()
         return lambda it: c(it, metadata=md)
 
     def close(self) -> None:
@@ -327,16 +384,18 @@ class Channel:
 class ChannelPool:
     """One channel per (address, user) (reference GrpcConnectionPool keyed by address)."""
 
-    def __init__(self):
+    def __init__(self, conf=None):
         self._lock = threading.Lock()
         self._chans: dict[tuple, Channel] = {}
+        self.conf = conf
 
     def get(self, address: str, user: str | None = None) -> Channel:
         key = (address, user)
         with self._lock:
             c = self._chans.get(key)
             if c is None:
-                c = self._chans[key] = Channel(address, user)
+                from ..security.authentication import client_auth_from_conf
+                c = self._chans[key] = Channel(address, user, auth=client_auth_from_conf(self.conf, user))
             return c
 
     def drop(self, address: str, user: str | None = None) -> None:

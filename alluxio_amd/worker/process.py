@@ -102,7 +102,8 @@ class AlluxioWorkerProcess:
         from ..rpc import master_channel
         self.master_channel = master_channel(self.master_address)
         self.worker = BlockWorker(self.conf, self.store, self.master_channel)
-        self.server = RpcServer(host, self.port, metrics=msys.metrics("Worker"), enable_grpc=enable_grpc)
+        self.server = RpcServer(host, self.port, metrics=msys.metrics("Worker"), enable_grpc=enable_grpc,
+                                conf=self.conf)
         self.server.add_servicer(SVC_BLOCK_WORKER, BlockWorkerService(self.worker, self.conf))
         self.sync = BlockMasterSync(self.worker, self)
         self._threads: list[hb.HeartbeatThread] = []
