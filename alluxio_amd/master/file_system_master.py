@@ -72,8 +72,10 @@ class FileSystemMaster(Journaled):
         self.metrics = metrics
         self.ufs_manager = UfsManager(conf)
         self.mount_table = MountTable(self.ufs_manager)
+        from .metastore import create_inode_store
         self.tree = InodeTree(block_master.get_new_container_id,
-                              conf.get_ms("alluxio.master.ttl.checker.interval") if conf else 3_600_000)
+                              conf.get_ms("alluxio.master.ttl.checker.interval") if conf else 3_600_000,
+                              store=create_inode_store(conf))
         self.permission = permission_checker or PermissionChecker(
             enabled=conf.get_bool("alluxio.security.authorization.permission.enabled") if conf else False,
             superuser=None,
@@ -99,6 +101,13 @@ class FileSystemMaster(Journaled):
         self.ufs_modes.clear()
 
     def process_journal_entry(self, e) -> bool:
+        self.tree.inodes.begin()   # metastore write-back scope (no-op for HEAP)
+        try:
+            return self._process_journal_entry(e)
+        finally:
+            self.tree.inodes.end()
+
+    def _process_journal_entry(self, e) -> bool:
         if self.tree.apply(e):
             return True
         if e.HasField("new_block"):
@@ -1036,6 +1045,7 @@ class FileSystemMaster(Journaled):
         if wait_ms:
             self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(id=f.id)))
             f.should_persist_time = now_ms() + wait_ms
+            self.tree.inodes[f.id] = f   # not journaled separately: persist the field to the metastore
 
     def persistence_scheduler_heartbeat(self) -> int:
         """Submit persist jobs for TO_BE_PERSISTED files (PersistenceScheduler)."""

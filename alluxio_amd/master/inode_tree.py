@@ -98,9 +98,10 @@ class TtlBuckets:
 class InodeTree:
     ROOT_NAME = ""
 
-    def __init__(self, container_source, ttl_interval_ms: int = 3_600_000):
+    def __init__(self, container_source, ttl_interval_ms: int = 3_600_000, store=None):
+        from .metastore import HeapInodeStore
         self.lock = RWLock()
-        self.inodes: dict[int, Inode] = {}
+        self.inodes = store if store is not None else HeapInodeStore()   # InodeStore SPI (HEAP / ROCKS)
         self.children: dict[int, dict[str, int]] = {}
         self.root: InodeDirectory | None = None
         self.dir_ids = DirectoryIdGenerator(container_source)
@@ -160,6 +161,13 @@ class InodeTree:
 
     # ---- journal application (single code path for replay and live ops) ---------------------
     def apply(self, e) -> bool:
+        self.inodes.begin()
+        try:
+            return self._apply(e)
+        finally:
+            self.inodes.end()
+
+    def _apply(self, e) -> bool:
         if e.HasField("inode_directory"):
             self._add(InodeDirectory.from_entry(e.inode_directory))
         elif e.HasField("inode_file"):

@@ -93,6 +93,7 @@ class AlluxioMasterProcess:
         self.state_lock = StateLockManager()
         self.fs_master.state_lock = self.state_lock
         self.safe_mode = SafeModeManager(self.conf.get_ms("alluxio.master.worker.connect.wait.time"))
+        self._register_gauges()
         self.table_master = None
         if self.conf.get_bool("alluxio.table.enabled", "true"):
             from ..table.master import TableMaster
@@ -129,6 +130,17 @@ class AlluxioMasterProcess:
     @property
     def address(self) -> str:
         return self.server.address
+
+    def _register_gauges(self) -> None:
+        """Master/Cluster gauges (DefaultFileSystemMaster.java:4321 registerGauges,
+        DefaultBlockMaster.java:1209 registerGauges)."""
+        reg, bm, tree = self.metrics.registry, self.block_master, self.fs_master.tree
+        reg.gauge("Master.FilesPinned", lambda: len(tree.pinned_ids))
+        reg.gauge("Master.TotalPaths", lambda: len(tree.inodes))
+        reg.gauge("Cluster.CapacityTotal", bm.capacity_bytes)
+        reg.gauge("Cluster.CapacityUsed", bm.used_bytes)
+        reg.gauge("Cluster.CapacityFree", lambda: bm.capacity_bytes() - bm.used_bytes())
+        reg.gauge("Cluster.Workers", bm.worker_count)
 
     def _job_fs(self):
         from ..client.file_system import FileSystem
