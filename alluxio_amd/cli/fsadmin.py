@@ -218,9 +218,20 @@ class FileSystemAdminShell:
                 self.p(f"{enum_name(pb.journal_master.QuorumServerState, s.serverState):<12}"
                        f"{s.serverAddress.host}:{s.serverAddress.rpcPort}")
             return 0
+        if args[:2] == ["quorum", "remove"]:
+            # QuorumRemoveCommand: journal quorum remove -address <host:port> [-domain MASTER]
+            if "-address" not in args:
+                raise ValueError("usage: journal quorum remove -address <host:port>")
+            host, _, port = args[args.index("-address") + 1].rpartition(":")
+            self.ctx.master_channel().stub("alluxio.grpc.journal.JournalMasterClientService").RemoveQuorumServer(
+                pb.journal_master.RemoveQuorumServerPRequest(
+                    options=pb.journal_master.RemoveQuorumServerPOptions(),
+                    serverAddress=pb.grpc.NetAddress(host=host, rpcPort=int(port))))
+            self.p(f"Removed server at: {host}:{port} from quorum")
+            return 0
         if args[:1] == ["checkpoint"]:
             return self.cmd_checkpoint([])
-        raise ValueError("usage: journal [quorum info | checkpoint]")
+        raise ValueError("usage: journal [quorum info | quorum remove -address <host:port> | checkpoint]")
 
     def cmd_metrics(self, args) -> int:
         if args[:1] != ["clear"]:

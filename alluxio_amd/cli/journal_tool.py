@@ -1,8 +1,9 @@
-"""``alluxio readJournal`` — dump a UFS journal as text.
+"""``alluxio readJournal`` — dump a UFS or embedded (Raft) journal as text.
 
 Parity: core/server/master/src/main/java/alluxio/master/journal/tool/JournalTool.java (dumps
 the latest checkpoint and the log entries in [start, end) of one master's journal into an
-output directory: ``checkpoints/`` and ``edits.txt``).
+output directory: ``checkpoints/`` and ``edits.txt``) and RaftJournalDumper.java (embedded
+journal: the latest snapshot + the committed Raft log, one master's entries or all of them).
 """
 from __future__ import annotations
 
@@ -39,6 +40,49 @@ def dump_journal(journal_dir: str, master: str, output_dir: str, start: int = 0,
     return n
 
 
+def dump_raft_journal(journal_dir: str, master: str | None, output_dir: str, start: int = 0,
+                      end: int = 2 ** 63 - 1, out=None) -> int:
+    """Embedded journal under ``<journal_dir>/raft``: snapshot parts + log entries (by global SN)."""
+    from ..journal import format as fmt
+    from ..journal.raft import KIND_JOURNAL, RaftStorage
+    from ..proto import pb
+    out = out or sys.stdout
+    root = os.path.join(journal_dir, "raft")
+    if not os.path.isdir(root):
+        raise FileNotFoundError(f"no embedded journal under {journal_dir}")
+    st = RaftStorage(root, fsync=False)
+    os.makedirs(output_dir, exist_ok=True)
+    try:
+        if st.snapshot_path:
+            cdir = os.path.join(output_dir, "checkpoints")
+            os.makedirs(cdir, exist_ok=True)
+            with open(st.snapshot_path, "rb") as f:
+                hdr = fmt.read_delimited(f, pb.raft.RaftSnapshotHeader)
+                for name, data in fmt.read_compound(f):
+                    if master in (None, "", name):
+                        with open(os.path.join(cdir, f"{name}-0x0-0x{hdr.nextSequenceNumber:x}"), "wb") as g:
+                            g.write(data)
+            print(f"Snapshot at raft index {hdr.index} (term {hdr.term}, next SN {hdr.nextSequenceNumber}, "
+                  f"peers {list(hdr.peers)}) written to {cdir}", file=out)
+        n = 0
+        with open(os.path.join(output_dir, "edits.txt"), "w") as f:
+            for idx, term, payload in st.entries(st.base_index + 1):
+                if payload[:1] != KIND_JOURNAL:
+                    continue
+                for ne in pb.raft.RaftCommand.FromString(payload[1:]).entries:
+                    sn = ne.entry.sequence_number
+                    if sn < start or sn >= end or master not in (None, "", ne.master):
+                        continue
+                    f.write(f"# raft index {idx} term {term} master {ne.master}\n")
+                    f.write(text_format.MessageToString(ne.entry))
+                    f.write("\n")
+                    n += 1
+    finally:
+        st.close()
+    print(f"Dumped {n} journal entries to {output_dir}/edits.txt", file=out)
+    return n
+
+
 def main(argv=None, out=None) -> int:
     import argparse
     ap = argparse.ArgumentParser(prog="alluxio readJournal")
@@ -54,5 +98,8 @@ def main(argv=None, out=None) -> int:
     if jdir.startswith("file://"):
         jdir = jdir[len("file://"):]
     outdir = a.outputDir or os.path.join(os.getcwd(), f"journal_dump-{os.getpid()}")
-    dump_journal(jdir, a.master, outdir, a.start, a.end, out)
+    if os.path.isdir(os.path.join(jdir, "raft")):
+        dump_raft_journal(jdir, a.master, outdir, a.start, a.end, out)
+    else:
+        dump_journal(jdir, a.master, outdir, a.start, a.end, out)
     return 0

@@ -371,11 +371,23 @@ class MetaServices:
             r.metrics[k].doubleValue = v
         return r
 
-    # JournalMasterClientService
+    # JournalMasterClientService (RaftJournalSystem.getQuorumServerInfoList / removeQuorumServer)
     def GetQuorumInfo(self, req, ctx):
-        host, _, port = self.meta.master_address.partition(":")
-        return pb.journal_master.GetQuorumInfoPResponse(domain=1, serverInfo=[pb.journal_master.QuorumServerInfo(
-            serverAddress=pb.grpc.NetAddress(host=host, rpcPort=int(port or 0)), serverState=1)])
+        qi = getattr(self.js, "quorum_info", None)
+        if qi is None:      # UFS journal: the "quorum" is this master
+            host, _, port = self.meta.master_address.partition(":")
+            members = [(host, int(port or 0), True)]
+        else:
+            members = [(a.rsplit(":", 1)[0], int(a.rsplit(":", 1)[1]), ok) for a, ok in qi()]
+        return pb.journal_master.GetQuorumInfoPResponse(domain=1, serverInfo=[
+            pb.journal_master.QuorumServerInfo(serverAddress=pb.grpc.NetAddress(host=h, rpcPort=p),
+                                               serverState=1 if ok else 2) for h, p, ok in members])
 
     def RemoveQuorumServer(self, req, ctx):
+        rm = getattr(self.js, "remove_quorum_server", None)
+        if rm is None:
+            from ..utils.exceptions import InvalidArgumentException
+            raise InvalidArgumentException("quorum membership needs the EMBEDDED journal")
+        a = req.serverAddress
+        rm(f"{a.host}:{a.rpcPort}")
         return pb.journal_master.RemoveQuorumServerPResponse()

@@ -59,7 +59,9 @@ class SafeModeManager:
         return time.time() < self._until
 
 
-def build_journal_system(conf: Configuration):
+def build_journal_system(conf: Configuration, host: str | None = None, enable_grpc: bool = True,
+                         ephemeral: bool = False):
+    """UFS / EMBEDDED (Raft among the masters) / NOOP (JournalSystem factory)."""
     jtype = conf.get("alluxio.master.journal.type", "UFS").upper()
     if jtype in ("NOOP", "NONE"):
         return NoopJournalSystem()
@@ -67,7 +69,9 @@ def build_journal_system(conf: Configuration):
     if folder.startswith("file://"):
         folder = folder[len("file://"):]
     if jtype == "EMBEDDED":
-        LOG.info("journal type EMBEDDED: using the replicated UFS journal implementation at %s", folder)
+        from ..journal.raft_system import RaftJournalSystem
+        return RaftJournalSystem.from_conf(conf, folder, host=host, enable_grpc=enable_grpc,
+                                           ephemeral_port=ephemeral)
     return UfsJournalSystem(folder, max_log_bytes=conf.get_bytes("alluxio.master.journal.log.size.bytes.max"),
                             flush_batch_ms=conf.get_ms("alluxio.master.journal.flush.batch.time"),
                             checkpoint_period_entries=conf.get_int("alluxio.master.journal.checkpoint.period.entries"))
@@ -81,7 +85,8 @@ class AlluxioMasterProcess:
         self.port = self.conf.get_int("alluxio.master.rpc.port") if port is None else port
         from .. import metrics as msys
         self.metrics = msys.metrics("Master")
-        self.journal = journal_system or build_journal_system(self.conf)
+        self.journal = journal_system or build_journal_system(self.conf, host=host, enable_grpc=enable_grpc,
+                                                              ephemeral=self.port == 0)
         self.block_master = BlockMaster(self.conf, self.journal,
                                         worker_timeout_ms=self.conf.get_ms("alluxio.master.worker.timeout"))
         self.fs_master = FileSystemMaster(self.conf, self.block_master, self.journal, metrics=self.metrics,
@@ -103,7 +108,7 @@ class AlluxioMasterProcess:
                 self.journal.register(j)
         self.meta_master.masters_for_backup = [m for m in (self.block_master, self.fs_master, self.meta_master,
                                                             self.table_master) if m is not None]
-        self.meta_master.journal_system_for_checkpoint = self.journal
+        self.meta_master.journal_system_for_checkpoint = self   # checkpoint() under the state lock
         self.server = RpcServer(host, self.port, max_workers=self.conf.get_int("alluxio.master.rpc.executor.max.pool.size", 500)
                                 if False else 64, metrics=self.metrics, enable_grpc=enable_grpc,
                                 conf=self.conf)
@@ -202,10 +207,12 @@ class AlluxioMasterProcess:
         """Single master: become primary now.  HA (``alluxio.master.ha.primary.selector`` =
         FILE_LOCK): start as a standby tailing the journal behind an RPC gate that answers
         UNAVAILABLE, and gain primacy when elected (FaultTolerantAlluxioMasterProcess)."""
-        if not self.journal.is_formatted() and isinstance(self.journal, UfsJournalSystem):
+        from ..journal.raft_system import RaftJournalSystem
+        raft = isinstance(self.journal, RaftJournalSystem)
+        if not self.journal.is_formatted() and isinstance(self.journal, (UfsJournalSystem, RaftJournalSystem)):
             self.journal.format()
         self.journal.start()
-        ha = self.conf.get("alluxio.master.ha.primary.selector", "NONE").upper() == "FILE_LOCK"
+        ha = raft or self.conf.get("alluxio.master.ha.primary.selector", "NONE").upper() == "FILE_LOCK"
         if primary and not ha:
             self.gain_primacy()
         if self.job_master is not None and self.fs_master.persist_handler is None:
@@ -228,14 +235,17 @@ class AlluxioMasterProcess:
             self.web_port = self.web.start()
             self.meta_master.web_port = self.web_port
         if ha:
-            from .ha import FileLockPrimarySelector
-            self.selector = FileLockPrimarySelector(self.conf.get("alluxio.master.ha.lock.file"))
+            if raft:       # primacy follows Raft leadership (RaftPrimarySelector)
+                self.selector = self.journal.selector
+            else:
+                from .ha import FileLockPrimarySelector
+                self.selector = FileLockPrimarySelector(self.conf.get("alluxio.master.ha.lock.file"))
 
             def on_primary():
                 self.gain_primacy()
                 if start_heartbeats:
                     self._start_heartbeats()
-            self.selector.start(on_primary)
+            self.selector.start(on_primary, self.lose_primacy)
         elif start_heartbeats and primary:
             self._start_heartbeats()
         self.started = True
@@ -255,6 +265,19 @@ class AlluxioMasterProcess:
         self.meta_master.start(True)
         self.safe_mode.notify_primary()
         self.primary = True
+
+    def lose_primacy(self) -> None:
+        """Step down to standby: refuse RPCs, stop primary-only heartbeats, and let the journal
+        rebuild the masters' state from what was committed (FaultTolerantAlluxioMasterProcess)."""
+        if not self.primary:
+            return
+        LOG.info("master %s lost primacy", getattr(self.server, "address", "?"))
+        self.primary = False
+        threads, self._threads = self._threads, []
+        for t in threads:
+            t.shutdown(join=False)
+        with self.state_lock.exclusive():
+            self.journal.lose_primacy()
 
     def _start_heartbeats(self) -> None:
         c = self.conf

@@ -139,12 +139,54 @@ class MultiMasterLocalAlluxioCluster(LocalAlluxioCluster):
     """N masters sharing one journal (FILE_LOCK election) + workers; masters can be killed and
     the standby takes over (reference minicluster/.../MultiMasterLocalAlluxioCluster.java)."""
 
-    def __init__(self, num_masters: int = 2, num_workers: int = 1, conf: dict | None = None, **kw):
-        c = {"alluxio.master.ha.primary.selector": "FILE_LOCK", "alluxio.user.rpc.retry.max.duration": "20sec"}
+    def __init__(self, num_masters: int = 2, num_workers: int = 1, conf: dict | None = None,
+                 journal_type: str = "UFS", **kw):
+        c = {"alluxio.user.rpc.retry.max.duration": "20sec"}
+        if journal_type.upper() == "EMBEDDED":
+            # every master keeps its own Raft log; short timeouts keep failover tests quick
+            c.update({"alluxio.master.embedded.journal.election.timeout": "400ms",
+                      "alluxio.master.embedded.journal.heartbeat.interval": "50ms"})
+        else:
+            c["alluxio.master.ha.primary.selector"] = "FILE_LOCK"
         c.update(conf or {})
         super().__init__(num_workers=num_workers, conf=c, **kw)
+        self.journal_type = journal_type.upper()
+        if self.journal_type == "EMBEDDED":
+            self.conf.set("alluxio.master.journal.type", "EMBEDDED")
         self.num_masters = num_masters
         self.masters: list[AlluxioMasterProcess] = []
+        self.master_confs: list = []
+
+    def _embedded_confs(self) -> list:
+        ports = []
+        for _ in range(self.num_masters):
+            if self.grpc:
+                import socket
+                with socket.socket() as so:
+                    so.bind(("127.0.0.1", 0))
+                    ports.append(so.getsockname()[1])
+            else:
+                from ..rpc import _alloc_local_port
+                ports.append(_alloc_local_port())
+        addrs = ",".join(f"127.0.0.1:{p}" for p in ports)
+        confs = []
+        for i, p in enumerate(ports):
+            c = self.conf.copy()
+            c.set("alluxio.master.journal.folder", os.path.join(self.work_dir, f"journal{i}"))
+            c.set("alluxio.master.embedded.journal.port", str(p))
+            c.set("alluxio.master.embedded.journal.addresses", addrs)
+            confs.append(c)
+        return confs
+
+    def start_master(self, i: int) -> AlluxioMasterProcess:
+        """(Re)start master ``i`` with its own configuration (embedded journal: same Raft id)."""
+        m = AlluxioMasterProcess(self.master_confs[i], port=0, enable_grpc=self.grpc, root_ufs=self.ufs_root)
+        m.start(start_heartbeats=self.heartbeats)
+        if i < len(self.masters):
+            self.masters[i] = m
+        else:
+            self.masters.append(m)
+        return m
 
     @property
     def master_addresses(self) -> str:
@@ -153,10 +195,12 @@ class MultiMasterLocalAlluxioCluster(LocalAlluxioCluster):
     def start(self) -> "MultiMasterLocalAlluxioCluster":
         import time
         os.makedirs(self.ufs_root, exist_ok=True)
-        for _ in range(self.num_masters):
-            m = AlluxioMasterProcess(self.conf, port=0, enable_grpc=self.grpc, root_ufs=self.ufs_root)
-            m.start(start_heartbeats=self.heartbeats)
-            self.masters.append(m)
+        if self.journal_type == "EMBEDDED":
+            self.master_confs = self._embedded_confs()
+        else:
+            self.master_confs = [self.conf] * self.num_masters
+        for i in range(self.num_masters):
+            self.start_master(i)
         deadline = time.time() + 30
         while self.primary() is None and time.time() < deadline:
             time.sleep(0.02)
@@ -167,9 +211,20 @@ class MultiMasterLocalAlluxioCluster(LocalAlluxioCluster):
 
     def primary(self):
         for m in self.masters:
-            if m.primary:
+            if m.primary and m.started:
                 return m
         return None
+
+    def wait_primary(self, timeout: float = 30.0):
+        import time
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            p = self.primary()
+            if p is not None:
+                self.master = p
+                return p
+            time.sleep(0.02)
+        raise TimeoutError("no master gained primacy")
 
     def start_worker(self, i: int | None = None) -> AlluxioWorkerProcess:
         i = len(self.workers) if i is None else i

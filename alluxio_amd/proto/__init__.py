@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import types
 
-from .defs import block, common, file, journal, meta, metric, table
+from .defs import block, common, file, journal, meta, metric, raft, table
 from .dsl import Schema
 
 _ALIASES = {
@@ -28,10 +28,12 @@ _ALIASES = {
     "alluxio.grpc.job": "job",
     "alluxio.grpc.journal": "journal_master",
     "alluxio.grpc.table": "table",
+    "alluxio.grpc.messaging": "messaging",
+    "alluxio.grpc.raft": "raft",
 }
 
 SCHEMA = Schema()
-for _mod in (common, block, file, journal, metric, meta, table):
+for _mod in (common, block, file, journal, metric, meta, table, raft):
     SCHEMA.add(_mod.SCHEMA)
 SCHEMA.build()
 
