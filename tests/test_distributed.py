@@ -193,3 +193,21 @@ def test_cross_page_segments():
     # src pages of 4 bytes [2, 3] (contiguous), dst pages of 2 bytes [0, 5, 6, 7]
     segs = cross_page_segments(100, [2, 3], 4, 1000, [0, 5, 6, 7], 2, 0, 8)
     assert segs == [(108, 1000, 2), (110, 1010, 6)]
+
+
+def test_bench_two_ranks_gloo(tmp_path):
+    """The driver's multi-GPU launch shape (torch.distributed.run, one rank per worker), on gloo."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--threads", "4", "--file-size", "8m",
+           "--block-size", "4m", "--work-dir", str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1                      # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "workers2" and out["config"]["verified"]
