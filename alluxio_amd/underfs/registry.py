@@ -57,7 +57,7 @@ def _load_builtin() -> None:
     from .memory import MemoryUnderFileSystem
     register_factory(_ClassFactory("file", LocalUnderFileSystem))
     register_factory(_ClassFactory("mem", MemoryUnderFileSystem))
-    from . import s3, web, hdfs  # noqa: F401  (self-registering)
+    from . import s3, web, hdfs, swift, wasb, webhdfs, ozone  # noqa: F401  (self-registering)
     try:
         from importlib.metadata import entry_points
         for ep in entry_points().select(group="alluxio_amd.underfs"):

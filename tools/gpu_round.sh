@@ -47,6 +47,10 @@ for s in $STEPS; do
       run bench_ring4k_f1g 300 python bench.py --buffer-size 4k --file-size 1g --steps 200 --warmup 20
       run rocprof_ring 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ring" -o ring --output-format csv -- python3 bench.py --buffer-size 4k --steps 50 --warmup 5
       ;;
+    pmc)
+      run rocprof_list 120 rocprofv3 -L
+      run rocprof_pmc 500 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --kernel-trace --stats -d "$OUT/pmc" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2
+      ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
     ringtune) run ring_tune 600 python tools/ring_tune.py --out "$OUT/ring_tune.json" $RINGTUNE_ARGS ;;
