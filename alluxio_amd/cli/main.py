@@ -26,7 +26,9 @@ COMMAND is one of:
   table                 Command line tool for interacting with the table (catalog) service.
   logLevel              Set or get log level of Alluxio servers.
   readJournal           Read an Alluxio journal file from stdin and write a human-readable version of it to stdout.
+  runClass              Run the main function of a module (``pkg.module`` or ``pkg.module:function``).
   runTests              Run all end-to-end tests on an Alluxio cluster.
+  upgradeJournal        Upgrade an Alluxio journal from v0 to v1 (-journalDirectoryV0 <dir>).
   stress                Run a stress benchmark (master|worker|client-io|ufs-io|max-throughput).
   validateConf          Validate Alluxio conf and exit.
   validateEnv           Validate Alluxio environment.
@@ -50,6 +52,18 @@ def _master_journal(conf):
         stub.journal_name = name
         j.register(stub)
     return j
+
+
+def run_class(args, out=None) -> int:
+    """``alluxio runClass <module[:function]> [args]`` (bin/alluxio runClass)."""
+    import importlib
+    if not args:
+        print("Usage: alluxio runClass <module[:function]> [args...]", file=out or sys.stdout)
+        return 1
+    mod, _, fn = args[0].partition(":")
+    target = getattr(importlib.import_module(mod), fn or "main")
+    rc = target(args[1:])
+    return rc if isinstance(rc, int) else 0
 
 
 def format_journal(conf=None, out=None) -> None:
@@ -188,6 +202,11 @@ def main(argv=None, out=None) -> int:
     if cmd == "runTests":
         from .test_runner import main as m
         return m(rest, out)
+    if cmd == "upgradeJournal":
+        from ..journal.upgrade import main as m
+        return m(rest, out)
+    if cmd == "runClass":
+        return run_class(rest, out)
     if cmd == "validateEnv":
         from .validate import main_env
         return main_env(rest, out)

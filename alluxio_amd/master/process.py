@@ -207,7 +207,9 @@ class AlluxioMasterProcess:
         """Single master: become primary now.  HA (``alluxio.master.ha.primary.selector`` =
         FILE_LOCK): start as a standby tailing the journal behind an RPC gate that answers
         UNAVAILABLE, and gain primacy when elected (FaultTolerantAlluxioMasterProcess)."""
+        from .. import metrics as msys
         from ..journal.raft_system import RaftJournalSystem
+        self._sinks = msys.load_sinks(self.conf, self.metrics)
         raft = isinstance(self.journal, RaftJournalSystem)
         if not self.journal.is_formatted() and isinstance(self.journal, (UfsJournalSystem, RaftJournalSystem)):
             self.journal.format()
@@ -325,6 +327,8 @@ class AlluxioMasterProcess:
             self.journal.checkpoint()
 
     def stop(self) -> None:
+        for sk in getattr(self, "_sinks", []):
+            sk.stop()
         if self.selector is not None:
             self.selector.stop()
         self.primary = False

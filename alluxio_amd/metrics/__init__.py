@@ -10,6 +10,7 @@ from __future__ import annotations
 import bisect
 import csv
 import json
+import logging
 import math
 import os
 import re
@@ -376,6 +377,82 @@ class CsvSink(_PeriodicSink):
                 w.writerow([f"{now:.3f}", v])
 
 
+class GraphiteSink(_PeriodicSink):
+    """Plaintext Graphite protocol over TCP: ``<prefix.name> <value> <epoch>\n`` (GraphiteSink.java)."""
+
+    def __init__(self, host: str, port: int, period_s: float = 10.0, prefix: str = ""):
+        super().__init__(period_s)
+        self.host, self.port, self.prefix = host, int(port), prefix
+
+    def report(self, system):
+        import socket
+        now = int(time.time())
+        lines = []
+        for k, v in sorted(system.registry.snapshot().items()):
+            if isinstance(v, (int, float)) and not math.isnan(v):
+                name = (self.prefix + "." if self.prefix else "") + re.sub(r"[\s]", "_", k)
+                lines.append(f"{name} {v} {now}\n")
+        if lines:
+            with socket.create_connection((self.host, self.port), timeout=5) as so:
+                so.sendall("".join(lines).encode())
+
+
+class LoggingSink(_PeriodicSink):
+    """Slf4jSink: metrics to the ``alluxio_amd.metrics`` logger, optionally regex-filtered."""
+
+    def __init__(self, period_s: float = 10.0, filter_regex: str | None = None):
+        super().__init__(period_s)
+        self.filter = re.compile(filter_regex) if filter_regex else None
+        self.log = logging.getLogger("alluxio_amd.metrics")
+
+    def report(self, system):
+        for k, v in sorted(system.registry.snapshot().items()):
+            if self.filter is None or self.filter.search(k):
+                self.log.info("type=METRIC name=%s value=%s", k, v)
+
+
+_UNITS = {"milliseconds": 0.001, "seconds": 1.0, "minutes": 60.0, "hours": 3600.0}
+
+
+def sinks_from_properties(props: dict) -> list:
+    """``sink.<name>.class`` / ``.period`` / ``.unit`` / sink options (conf/metrics.properties)."""
+    groups: dict[str, dict] = {}
+    for k, v in props.items():
+        if k.startswith("sink.") and k.count(".") >= 2:
+            _, name, opt = k.split(".", 2)
+            groups.setdefault(name, {})[opt] = v
+    out = []
+    for name, o in sorted(groups.items()):
+        cls = o.get("class", "").rsplit(".", 1)[-1]
+        period = float(o.get("period", 10)) * _UNITS.get(o.get("unit", "seconds").lower(), 1.0)
+        if cls == "ConsoleSink":
+            out.append(ConsoleSink(period))
+        elif cls == "CsvSink":
+            out.append(CsvSink(o.get("directory", "/tmp"), period))
+        elif cls == "GraphiteSink":
+            out.append(GraphiteSink(o["host"], int(o["port"]), period, o.get("prefix", "")))
+        elif cls == "Slf4jSink":
+            out.append(LoggingSink(period, o.get("filter-regex")))
+        # MetricsServlet / PrometheusMetricsServlet are the web endpoints; JmxSink has no analogue
+    return out
+
+
+def load_sinks(conf, system: "MetricsSystem") -> list:
+    """Attach the sinks configured in ``alluxio.metrics.conf.file`` to ``system`` and start them."""
+    try:
+        path = conf.get("alluxio.metrics.conf.file") if conf is not None else None
+    except Exception:  # noqa: BLE001  (unresolvable ${alluxio.conf.dir})
+        return []
+    if not path or not os.path.isfile(path):
+        return []
+    from ..conf import load_properties_file
+    sinks = sinks_from_properties(load_properties_file(path))
+    for s in sinks:
+        system.add_sink(s)
+        s.start(system)
+    return sinks
+
+
 _SYSTEMS: dict[str, MetricsSystem] = {}
 _SYS_LOCK = threading.Lock()
 
@@ -397,4 +474,5 @@ def reset_all() -> None:
 
 
 __all__ = ["Counter", "Meter", "Timer", "Gauge", "MetricsRegistry", "MetricsSystem", "metrics",
-           "prometheus_text", "ConsoleSink", "CsvSink", "metric_name", "reset_all", "bisect"]
+           "prometheus_text", "ConsoleSink", "CsvSink", "GraphiteSink", "LoggingSink", "sinks_from_properties",
+           "load_sinks", "metric_name", "reset_all", "bisect"]

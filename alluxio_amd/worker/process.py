@@ -117,6 +117,8 @@ class AlluxioWorkerProcess:
         return self.server.address
 
     def start(self, register: bool = True, start_heartbeats: bool = True) -> str:
+        from .. import metrics as msys
+        self._sinks = msys.load_sinks(self.conf, self.worker.metrics)
         addr = self.server.start()
         host, port = addr.rsplit(":", 1)
         ti = pb.grpc.TieredIdentity(tiers=[pb.grpc.LocalityTier(tierName="node", value=socket.gethostname()),
@@ -216,6 +218,8 @@ class AlluxioWorkerProcess:
                     self.worker.native.set_dir_healthy(i, False)
 
     def stop(self) -> None:
+        for sk in getattr(self, "_sinks", []):
+            sk.stop()
         for t in self._threads:
             t.shutdown(join=False)
         for t in self._threads:

@@ -116,3 +116,47 @@ def test_journal_system_replay_checkpoint_and_standby(tmp_path):
     assert c2.values == list(range(15))
     js2.stop()
     assert os.listdir(tmp_path / "Counter" / "v1" / "checkpoints") == ["0x0-0xa"]
+
+
+def test_upgrade_v0_journal(tmp_path):
+    """A 1.x (v0) journal is upgraded in place and replays into a working master."""
+    from alluxio_amd.cli.main import main as cli
+    from alluxio_amd.journal.upgrade import write_v0_journal
+    from alluxio_amd.proto import pb
+    import io
+
+    def e(sn, cid):
+        return pb.journal.JournalEntry(sequence_number=sn, block_container_id_generator=
+                                       pb.journal.BlockContainerIdGeneratorEntry(next_container_id=cid))
+    root = str(tmp_path / "journal")
+    write_v0_journal(root, "BlockMaster", [e(0, 5)], [[e(1, 6), e(2, 7)], [e(3, 8)]], current=[e(4, 9)])
+    conf_env = {"ALLUXIO_OPTS": f"-Dalluxio.master.journal.folder={root}"}
+    import os
+    old = {k: os.environ.get(k) for k in conf_env}
+    os.environ.update(conf_env)
+    try:
+        out = io.StringIO()
+        assert cli(["upgradeJournal", "-journalDirectoryV0", root], out) == 0
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert "BlockMaster: upgraded 3 log(s)" in out.getvalue()
+    from alluxio_amd.journal.ufs_journal import UfsJournal
+    j = UfsJournal(root, "BlockMaster")
+    assert [(f.start, f.end) for f in j.logs()] == [(1, 3), (3, 4), (4, 5)]
+    ctype, payload, end = j.read_checkpoint()
+    assert end == 1 and [x.block_container_id_generator.next_container_id
+                         for x in j.iter_log_entries(end)] == [6, 7, 8, 9]
+    # a block master replays it
+    from alluxio_amd.journal.system import UfsJournalSystem
+    from alluxio_amd.master.block_master import BlockMaster
+    from alluxio_amd.conf import Configuration
+    js = UfsJournalSystem(root)
+    bm = BlockMaster(Configuration(), js)
+    js.register(bm)
+    js.start()
+    assert bm._container_limit == 9
+    js.stop()

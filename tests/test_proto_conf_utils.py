@@ -183,3 +183,41 @@ def test_indexed_set():
     assert len(s.get_by_field("addr", "h1")) == 2
     s.remove(a)
     assert s.get_first_by_field("id", 1) is None and len(s) == 1
+
+
+def test_metrics_sinks_from_properties(tmp_path):
+    import socket
+    import threading
+    from alluxio_amd.metrics import (CsvSink, GraphiteSink, LoggingSink, MetricsSystem, load_sinks,
+                                     sinks_from_properties)
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    got = []
+
+    def accept():
+        c, _ = srv.accept()
+        got.append(c.recv(65536).decode())
+        c.close()
+    t = threading.Thread(target=accept, daemon=True)
+    t.start()
+    props = tmp_path / "metrics.properties"
+    props.write_text(f"sink.graphite.class=alluxio.metrics.sink.GraphiteSink\nsink.graphite.host=127.0.0.1\n"
+                     f"sink.graphite.port={srv.getsockname()[1]}\nsink.graphite.prefix=amd\n"
+                     f"sink.graphite.period=50\nsink.graphite.unit=milliseconds\n"
+                     f"sink.csv.class=alluxio.metrics.sink.CsvSink\nsink.csv.directory={tmp_path / 'csv'}\n"
+                     f"sink.slf4j.class=alluxio.metrics.sink.Slf4jSink\nsink.jmx.class=alluxio.metrics.sink.JmxSink\n")
+    from alluxio_amd.conf import Configuration, load_properties_file
+    kinds = sorted(type(s).__name__ for s in sinks_from_properties(load_properties_file(str(props))))
+    assert kinds == ["CsvSink", "GraphiteSink", "LoggingSink"]
+    m = MetricsSystem("Master")
+    m.counter("FilesCreated").inc(3)
+    sinks = load_sinks(Configuration({"alluxio.metrics.conf.file": str(props)}), m)
+    try:
+        t.join(5)
+        assert got and "amd.Master.FilesCreated 3" in got[0]
+    finally:
+        for s in sinks:
+            s.stop()
+        srv.close()
+    assert all(isinstance(s, (CsvSink, GraphiteSink, LoggingSink)) for s in sinks)

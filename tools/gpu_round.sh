@@ -48,8 +48,10 @@ for s in $STEPS; do
       run rocprof_ring 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ring" -o ring --output-format csv -- python3 bench.py --buffer-size 4k --steps 50 --warmup 5
       ;;
     pmc)
-      run rocprof_list 120 rocprofv3 -L
-      run rocprof_pmc 500 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --kernel-trace --stats -d "$OUT/pmc" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2
+      # one small counter group per pass (a big derived set aborts with "exceeds the capabilities")
+      run rocprof_pmc_rd 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --kernel-trace --stats -d "$OUT/pmc_rd" -o pmc --output-format csv -- python3 bench.py --steps 10 --warmup 1
+      run rocprof_pmc_wr 240 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-trace --stats -d "$OUT/pmc_wr" -o pmc --output-format csv -- python3 bench.py --steps 10 --warmup 1
+      run rocprof_pmc_dram 240 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram" -o pmc --output-format csv -- python3 bench.py --steps 10 --warmup 1
       ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
