@@ -104,10 +104,33 @@ class LFUCacheEvictor:
 class LocalPageStore:
     """One file per page: ``<root>/<page_size>/<bucket>/<file_id>/<page_index>``."""
 
-    def __init__(self, root: str, page_size: int, buckets: int = 1000):
+    OPTIONS_FILE = "options.pb"
+
+    def __init__(self, root: str, page_size: int, buckets: int = 1000, cache_size: int = 0):
         self.root = os.path.join(root, str(page_size))
         self.buckets = buckets
         os.makedirs(self.root, exist_ok=True)
+        self._check_options(page_size, cache_size)
+
+    def _check_options(self, page_size: int, cache_size: int) -> None:
+        """Store-wide options (proto/client/cache.proto PPageStoreCommonOptions): a store written
+        with a different page size or by another version is discarded instead of restored."""
+        from .. import __version__
+        from ..proto import pb
+        want = pb.client_cache.PPageStoreCommonOptions(pageSize=page_size, cacheSize=cache_size,
+                                                      alluxioVersion=__version__)
+        path = os.path.join(self.root, self.OPTIONS_FILE)
+        if os.path.exists(path):
+            with open(path, "rb") as f:
+                have = pb.client_cache.PPageStoreCommonOptions.FromString(f.read())
+            if have.pageSize == want.pageSize and have.alluxioVersion == want.alluxioVersion:
+                return
+            import shutil
+            for n in os.listdir(self.root):
+                q = os.path.join(self.root, n)
+                shutil.rmtree(q) if os.path.isdir(q) else os.remove(q)
+        with open(path, "wb") as f:
+            f.write(want.SerializeToString())
 
     def _path(self, pid):
         b = zlib.crc32(pid.file_id.encode()) % self.buckets  # stable across processes (restore)
@@ -140,6 +163,8 @@ class LocalPageStore:
         out = []
         for b in os.listdir(self.root):
             bdir = os.path.join(self.root, b)
+            if not os.path.isdir(bdir):
+                continue
             for fid in os.listdir(bdir):
                 for name in os.listdir(os.path.join(bdir, fid)):
                     if name.endswith(".tmp"):
@@ -233,7 +258,8 @@ class LocalCacheManager:
             self.store = MemPageStore()
         else:
             self.store = LocalPageStore(conf.get("alluxio.user.client.cache.dir"), self.page_size,
-                                        conf.get_int("alluxio.user.client.cache.local.store.file.buckets"))
+                                        conf.get_int("alluxio.user.client.cache.local.store.file.buckets"),
+                                        self.capacity)
         self.meta: dict = {}   # PageId -> bytes
         self.bytes = 0
         self._meta_lock = threading.RLock()

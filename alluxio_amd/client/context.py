@@ -126,7 +126,19 @@ class FileSystemContext:
                 self._workers = list(self.block_master().GetWorkerInfoList(
                     pb.block.GetWorkerInfoListPOptions()).workerInfos)
                 self._workers_at = time.time()
+                for w in self._workers:
+                    self._note_domain_socket(w.address)
             return list(self._workers)
+
+    def _note_domain_socket(self, addr) -> None:
+        """Same-node worker with a domain socket: its gRPC traffic skips TCP
+        (alluxio.user.short.circuit / domain socket data server)."""
+        import os
+        from ..rpc import register_domain_socket
+        p = addr.domainSocketPath
+        if p and self.is_local(addr) and os.path.exists(p) and \
+                self.conf.get_bool("alluxio.user.short.circuit.enabled", "true"):
+            register_domain_socket(worker_address_str(addr), p)
 
     def is_local(self, addr) -> bool:
         """Same node as this client (reference: tiered identity 'node' tier match)."""

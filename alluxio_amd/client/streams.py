@@ -385,6 +385,8 @@ class FileInStream(io.RawIOBase):
                     return IpcBlockReader(self.ctx, addr, bi.blockId, self.session)
                 except Exception:  # noqa: BLE001 - not in the HBM tier / IPC unsupported: use gRPC
                     LOG.debug("IPC read of block %d from %s unavailable", bi.blockId, addr, exc_info=True)
+            if self.ctx.is_local(l.workerAddress):
+                self.ctx._note_domain_socket(l.workerAddress)
             try:
                 r = GrpcBlockReader(self.ctx, addr, bi.blockId, block_len)
                 self._maybe_passive_cache(bi.blockId, l.workerAddress, block_len)

@@ -179,6 +179,12 @@ _k("JOB_MASTER_EMBEDDED_ENABLED", "alluxio.job.master.embedded.enabled", "true",
    "separate job-master process.")
 _k("JOB_WORKER_ENABLED", "alluxio.job.worker.enabled", "true", Scope.WORKER,
    "Run a job worker inside each block-worker process (tasks share the worker's HBM store).")
+_k("USER_INPROCESS_TRANSPORT_ENABLED", "alluxio.user.network.inprocess.transport.enabled", "true", Scope.CLIENT,
+   "Call servers that live in the same process directly instead of through gRPC (false forces "
+   "every RPC over the network stack, as a client in another process would).")
+_k("UNDERFS_OZONE_S3G_ENDPOINT", "alluxio.underfs.ozone.s3g.endpoint", None, Scope.SERVER,
+   "Ozone S3 gateway endpoint used by the o3fs:// and ofs:// connectors (default "
+   "http://<om-host>:9878).")
 
 
 def get(name: str) -> PropertyKey:

@@ -29,6 +29,7 @@ _ALIASES = {
     "alluxio.grpc.journal": "journal_master",
     "alluxio.grpc.table": "table",
     "alluxio.grpc.messaging": "messaging",
+    "alluxio.proto.client": "client_cache",
     "alluxio.grpc.raft": "raft",
 }
 

@@ -70,4 +70,8 @@ enum ChannelAuthenticationScheme NOSASL=0 SIMPLE=1 CUSTOM=2
 msg SaslMessage messageType=1:SaslMessageType message=2:bytes clientId=3:str
     authenticationScheme=4:ChannelAuthenticationScheme channelRef=5:str
 rpc SaslAuthenticationService authenticate *SaslMessage *SaslMessage
+
+package alluxio.proto.client
+msg PPageStoreCommonOptions pageSize=1:i64 cacheSize=2:i64 alluxioVersion=3:str
+msg PRocksPageStoreOptions commonOptions=1:PPageStoreCommonOptions
 """

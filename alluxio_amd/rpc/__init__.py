@@ -143,8 +143,10 @@ class _Handler:
 
 class RpcServer:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, max_workers: int = 64, metrics=None,
-                 enable_grpc: bool = True, conf=None):
+                 enable_grpc: bool = True, conf=None, domain_socket: str | None = None):
         self.host = host
+        # gRPC over a Unix domain socket next to TCP (AlluxioWorkerProcess domain-socket data server)
+        self.domain_socket = domain_socket
         # SASL channel authentication (None = NOSASL: trust the alluxio-user header)
         self.authenticator = None
         if conf is not None:
@@ -201,6 +203,13 @@ class RpcServer:
             if bound == 0:
                 raise OSError(f"cannot bind {self.host}:{self.port}")
             self.port = bound
+            if self.domain_socket:
+                import os
+                os.makedirs(os.path.dirname(self.domain_socket) or ".", exist_ok=True)
+                if os.path.exists(self.domain_socket):
+                    os.remove(self.domain_socket)
+                if not self._server.add_insecure_port(f"unix:{self.domain_socket}"):
+                    raise OSError(f"cannot bind unix:{self.domain_socket}")
             self._server.start()
         elif self.port == 0:
             self.port = _alloc_local_port()
@@ -221,6 +230,18 @@ class RpcServer:
 
 
 _port_counter = [40000]
+_DOMAIN_SOCKETS: dict[str, str] = {}
+
+
+def register_domain_socket(address: str, path: str) -> None:
+    """Route new gRPC channels for ``address`` over the worker's Unix domain socket."""
+    with _LOCAL_LOCK:
+        _DOMAIN_SOCKETS[address] = path
+
+
+def domain_socket_for(address: str) -> str | None:
+    with _LOCAL_LOCK:
+        return _DOMAIN_SOCKETS.get(address)
 
 
 def _alloc_local_port() -> int:
@@ -295,7 +316,12 @@ class Channel:
     def _channel(self):
         with self._lock:
             if self._grpc is None:
-                self._grpc = grpc.insecure_channel(self.address, options=[
+                target = self.address
+                with _LOCAL_LOCK:
+                    uds = _DOMAIN_SOCKETS.get(self.address)
+                if uds:
+                    target = f"unix:{uds}"
+                self._grpc = grpc.insecure_channel(target, options=[
                     ("grpc.max_receive_message_length", MAX_MESSAGE),
                     ("grpc.max_send_message_length", MAX_MESSAGE)])
                 if self.auth is not None:
@@ -395,7 +421,10 @@ class ChannelPool:
             c = self._chans.get(key)
             if c is None:
                 from ..security.authentication import client_auth_from_conf
-                c = self._chans[key] = Channel(address, user, auth=client_auth_from_conf(self.conf, user))
+                force = self.conf is not None and not self.conf.get_bool(
+                    "alluxio.user.network.inprocess.transport.enabled", "true")
+                c = self._chans[key] = Channel(address, user, force_grpc=force,
+                                               auth=client_auth_from_conf(self.conf, user))
             return c
 
     def drop(self, address: str, user: str | None = None) -> None:

@@ -9,6 +9,7 @@ lost storage) and the FileSystemMaster worker heartbeat (persisted files).
 from __future__ import annotations
 
 import logging
+import os
 import socket
 import threading
 
@@ -102,8 +103,9 @@ class AlluxioWorkerProcess:
         from ..rpc import master_channel
         self.master_channel = master_channel(self.master_address)
         self.worker = BlockWorker(self.conf, self.store, self.master_channel)
+        self.domain_socket = self._domain_socket_path() if enable_grpc else None
         self.server = RpcServer(host, self.port, metrics=msys.metrics("Worker"), enable_grpc=enable_grpc,
-                                conf=self.conf)
+                                conf=self.conf, domain_socket=self.domain_socket)
         self.server.add_servicer(SVC_BLOCK_WORKER, BlockWorkerService(self.worker, self.conf))
         self.sync = BlockMasterSync(self.worker, self)
         self._threads: list[hb.HeartbeatThread] = []
@@ -116,6 +118,17 @@ class AlluxioWorkerProcess:
     def address(self) -> str:
         return self.server.address
 
+    def _domain_socket_path(self) -> str | None:
+        """``alluxio.worker.data.server.domain.socket.address`` (a directory when
+        ``...as.uuid`` is true: one socket file per worker)."""
+        a = self.conf.get_raw("alluxio.worker.data.server.domain.socket.address")
+        if not a:
+            return None
+        if self.conf.get_bool("alluxio.worker.data.server.domain.socket.as.uuid", "false"):
+            import uuid
+            return os.path.join(a, uuid.uuid4().hex)
+        return a
+
     def start(self, register: bool = True, start_heartbeats: bool = True) -> str:
         from .. import metrics as msys
         self._sinks = msys.load_sinks(self.conf, self.worker.metrics)
@@ -124,6 +137,7 @@ class AlluxioWorkerProcess:
         ti = pb.grpc.TieredIdentity(tiers=[pb.grpc.LocalityTier(tierName="node", value=socket.gethostname()),
                                            pb.grpc.LocalityTier(tierName="gpu", value=str(self.store.device))])
         self.worker.address = pb.grpc.WorkerNetAddress(host=host, rpcPort=int(port), dataPort=int(port),
+                                                       domainSocketPath=self.domain_socket or "",
                                                        webPort=0, tieredIdentity=ti,
                                                        containerHost=socket.gethostname())
         if self.conf.get_bool("alluxio.web.server.enabled", "true"):

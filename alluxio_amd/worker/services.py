@@ -86,6 +86,10 @@ class BlockWorkerService:
                 except Exception:  # noqa: BLE001
                     pass
             self.w.access_block(session, bid)
+            # BytesReadDomain vs BytesReadRemote (DefaultBlockWorker metrics by transport)
+            peer = ctx.peer() if hasattr(ctx, "peer") else ""
+            read_counter = self.w.metrics.counter(
+                "BytesReadDomain" if str(peer).startswith("unix:") else "BytesReadRemote")
             while pos < end:
                 with cond:
                     while pos - acked[0] >= self.window and not done.is_set():
@@ -93,6 +97,7 @@ class BlockWorkerService:
                 n = min(chunk, end - pos)
                 data = self.w.read_bytes(bid, pos, n)
                 pos += n
+                read_counter.inc(n)
                 yield pb.block.ReadResponse(chunk=pb.block.Chunk(data=data))
         finally:
             if lock_id is not None:

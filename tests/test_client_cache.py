@@ -94,3 +94,15 @@ def test_hbm_page_store_device_reads(gpu, tmp_path):
             f.read_into(out)
         assert np.array_equal(out.cpu().numpy(), data[17:250_017])
         fs.close()
+
+
+def test_local_page_store_options_mismatch_discards(tmp_path):
+    from alluxio_amd.client.cache import LocalPageStore, PageId
+    st = LocalPageStore(str(tmp_path), 4096, buckets=4, cache_size=1 << 20)
+    st.put(PageId("f1", 0), b"a" * 10)
+    assert [p for p, _ in LocalPageStore(str(tmp_path), 4096, 4, 1 << 20).restore()] == [PageId("f1", 0)]
+    opts = tmp_path / "4096" / "options.pb"
+    from alluxio_amd.proto import pb
+    opts.write_bytes(pb.client_cache.PPageStoreCommonOptions(pageSize=4096, alluxioVersion="0.0.0-old")
+                     .SerializeToString())
+    assert LocalPageStore(str(tmp_path), 4096, 4, 1 << 20).restore() == []   # other version: wiped

@@ -153,3 +153,33 @@ def test_client_metrics_sync():
         ms = c.master.metrics_master.get_metrics()
         assert any("BytesReadClient" in k for k in ms), sorted(ms)[:20]
         fs.close()
+
+
+def test_domain_socket_data_server(tmp_path):
+    """A same-node client reaches the worker's data server over its Unix domain socket
+    (AlluxioWorkerProcess domain-socket server; BytesReadDomain metric)."""
+    import os
+    from alluxio_amd.client.context import unregister_local_worker, worker_address_str
+    from alluxio_amd.rpc import domain_socket_for
+    uds_dir = tmp_path / "uds"
+    with LocalAlluxioCluster(num_workers=1, grpc=True, work_dir=str(tmp_path / "c"), conf={
+            "alluxio.worker.tieredstore.level0.dirs.path": "dram",
+            "alluxio.worker.data.server.domain.socket.address": str(uds_dir),
+            "alluxio.worker.data.server.domain.socket.as.uuid": "true"}) as c:
+        w = c.workers[0]
+        path = w.worker.address.domainSocketPath
+        assert path.startswith(str(uds_dir)) and os.path.exists(path)
+        data = os.urandom(3 << 20)
+        fs = c.client()
+        fs.write_file("/uds/f", data, write_type="MUST_CACHE")
+        addr = worker_address_str(w.worker.address)
+        unregister_local_worker(addr)            # no in-process shortcut: go through the data server
+        from alluxio_amd.client.file_system import FileSystem
+        conf2 = c.conf.copy()
+        conf2.set("alluxio.user.network.inprocess.transport.enabled", "false")
+        fs2 = FileSystem(conf=conf2, master_address=c.master.address)
+        assert fs2.read_file("/uds/f") == data
+        assert domain_socket_for(addr) == path
+        assert w.worker.metrics.counter("BytesReadDomain").count >= len(data)
+        fs.close()
+        fs2.close()
