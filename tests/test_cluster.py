@@ -161,14 +161,15 @@ def test_domain_socket_data_server(tmp_path):
     import os
     from alluxio_amd.client.context import unregister_local_worker, worker_address_str
     from alluxio_amd.rpc import domain_socket_for
-    uds_dir = tmp_path / "uds"
+    import tempfile
+    uds_dir = tempfile.mkdtemp(prefix="uds", dir="/tmp")   # sun_path is limited to 108 bytes
     with LocalAlluxioCluster(num_workers=1, grpc=True, work_dir=str(tmp_path / "c"), conf={
             "alluxio.worker.tieredstore.level0.dirs.path": "dram",
             "alluxio.worker.data.server.domain.socket.address": str(uds_dir),
             "alluxio.worker.data.server.domain.socket.as.uuid": "true"}) as c:
         w = c.workers[0]
         path = w.worker.address.domainSocketPath
-        assert path.startswith(str(uds_dir)) and os.path.exists(path)
+        assert path.startswith(uds_dir) and os.path.exists(path)
         data = os.urandom(3 << 20)
         fs = c.client()
         fs.write_file("/uds/f", data, write_type="MUST_CACHE")
@@ -183,3 +184,5 @@ def test_domain_socket_data_server(tmp_path):
         assert w.worker.metrics.counter("BytesReadDomain").count >= len(data)
         fs.close()
         fs2.close()
+    import shutil
+    shutil.rmtree(uds_dir, ignore_errors=True)
