@@ -146,6 +146,8 @@ def master_routes(master) -> dict:
         ("POST", "/api/v1/logLevel"): log_level_route,
         ("GET", "/api/v1/master/ping"): lambda q, b: _json({"ok": True}),
     })
+    from .ui import master_ui_routes
+    r.update(master_ui_routes(master))
     del pb
     return r
 
@@ -174,4 +176,6 @@ def worker_routes(wp) -> dict:
         ("POST", "/api/v1/worker/log_level"): log_level_route,
         ("POST", "/api/v1/logLevel"): log_level_route,
     })
+    from .ui import worker_ui_routes
+    r.update(worker_ui_routes(wp))
     return r

@@ -292,3 +292,24 @@ def test_log_server(tmp_path):
     h.close()
     srv.stop()
     assert path is not None
+
+
+
+def test_web_ui_pages(cluster):
+    import urllib.request
+    fs = cluster.client()
+    fs.write_file("/ui/a <b>.txt", b"hello", write_type="MUST_CACHE")
+    base = f"http://127.0.0.1:{cluster.master.web_port}"
+    for path, needle in [("/", "Live Workers"), ("/browse?path=/ui", "a &lt;b&gt;.txt"),
+                         ("/browse?path=/ui/a%20%3Cb%3E.txt", "In Alluxio"), ("/workers", "In Service"),
+                         ("/config", "alluxio.master.journal.folder"), ("/metrics", "Cluster"),
+                         ("/mounttable", "UFS URI"), ("/jobs", "Status")]:
+        r = urllib.request.urlopen(base + path, timeout=10)
+        body = r.read().decode()
+        assert r.status == 200 and r.headers["Content-Type"].startswith("text/html") and needle in body, path
+    w = cluster.workers[0]
+    wbase = f"http://127.0.0.1:{w.web_port}"
+    for path, needle in [("/", "Storage Directories"), ("/blockinfo", "Block Id"), ("/metrics", "Metric")]:
+        body = urllib.request.urlopen(wbase + path, timeout=10).read().decode()
+        assert needle in body, path
+    fs.close()
