@@ -216,7 +216,10 @@ class UfsJournalSystem(JournalSystem):
             j.format()
 
     def is_formatted(self) -> bool:
-        return all(j.is_formatted() for j in self._journals.values())
+        """Formatted when any master's journal is: a journal written by an older release lacks the
+        directories of masters added since (e.g. TableMaster in a 1.8 journal); ``start`` creates
+        them empty."""
+        return any(j.is_formatted() for j in self._journals.values())
 
     def is_empty(self) -> bool:
         return all(not j.logs() and not j.checkpoints() for j in self._journals.values())

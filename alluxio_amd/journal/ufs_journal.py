@@ -28,6 +28,7 @@ from . import format as fmt
 LOG = logging.getLogger(__name__)
 
 VERSION = "v1"
+FORMAT_FILE_PREFIX = "_format_"   # alluxio.master.format.file.prefix
 
 
 class UfsJournalFile:
@@ -57,13 +58,23 @@ class UfsJournal:
 
     # ---- format -----------------------------------------------------------------------------
     def format(self) -> None:
+        """Empty the journal location and drop a ``_format_<ms>`` marker (UfsJournal.java:424-443)."""
         import shutil
+        import time
         if os.path.isdir(self.location):
             shutil.rmtree(self.location)
         for d in (self.log_dir, self.checkpoint_dir, self.tmp_dir):
             os.makedirs(d, exist_ok=True)
+        with open(os.path.join(self.location, f"{FORMAT_FILE_PREFIX}{int(time.time() * 1000)}"), "wb"):
+            pass
 
     def is_formatted(self) -> bool:
+        """A ``_format_*`` marker in the location (UfsJournal.java:399-414), as the Java masters
+        write it; directories laid out before markers existed count as formatted as well."""
+        if not os.path.isdir(self.location):
+            return False
+        if any(n.startswith(FORMAT_FILE_PREFIX) for n in os.listdir(self.location)):
+            return True
         return os.path.isdir(self.log_dir) and os.path.isdir(self.checkpoint_dir)
 
     def ensure(self) -> None:

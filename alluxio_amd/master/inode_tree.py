@@ -212,12 +212,18 @@ class InodeTree:
             r = e.rename
             inode = self.inodes.get(r.id)
             if inode is not None:
+                new_parent, new_name = r.new_parent_id, r.new_name
+                if r.HasField("dst_path") and not r.HasField("new_parent_id"):
+                    # 1.x entries name the destination by path; resolve it against the tree as
+                    # replayed so far (InodeTreePersistentState.rewriteDeprecatedRenameEntry)
+                    parent_path, _, new_name = r.dst_path.rstrip("/").rpartition("/")
+                    new_parent = self.get(parent_path or "/").id
                 kids = self.children.get(inode.parent_id)
                 if kids is not None and kids.get(inode.name) == inode.id:
                     del kids[inode.name]
-                inode.parent_id = r.new_parent_id
-                inode.name = r.new_name
-                self.children.setdefault(r.new_parent_id, {})[r.new_name] = inode.id
+                inode.parent_id = new_parent
+                inode.name = new_name
+                self.children.setdefault(new_parent, {})[new_name] = inode.id
                 inode.last_modification_time_ms = r.op_time_ms or inode.last_modification_time_ms
         elif e.HasField("set_acl"):
             s = e.set_acl

@@ -257,9 +257,11 @@ class AlluxioMasterProcess:
     def gain_primacy(self) -> None:
         backup = self.conf.get_raw("alluxio.master.journal.init.from.backup")
         if backup and self.journal.is_empty():
+            # become the writer first (that replays the empty journal), then load the backup and
+            # checkpoint it so it is durable (BackupManager.initFromBackup journals every entry)
+            self.journal.gain_primacy()
             n = restore_backup(backup, self.meta_master.masters_for_backup)
             LOG.info("restored %d entries from backup %s", n, backup)
-            self.journal.gain_primacy()
             self.journal.checkpoint()
         else:
             self.journal.gain_primacy()
