@@ -148,6 +148,10 @@ class FileSystemContext:
         return addr.host in ("127.0.0.1", "localhost", self.hostname)
 
     def in_process_worker(self, addr):
+        # the in-process transport switch also turns off direct calls into a same-process worker,
+        # so every byte goes through the worker's data server
+        if not self.conf.get_bool("alluxio.user.network.inprocess.transport.enabled", "true"):
+            return None
         return local_worker(worker_address_str(addr))
 
     def close(self) -> None:

@@ -20,6 +20,7 @@ import random
 import threading
 
 from ..proto import enum_name, pb
+from ..rpc import marshal
 from ..utils import ids
 from ..utils.exceptions import (AlluxioStatusException, NotFoundException, UnavailableException)
 from .context import SVC_WORKER, FileSystemContext, worker_address_str
@@ -516,8 +517,9 @@ class GrpcBlockWriter(BlockWriter):
             data = tmp.cpu().numpy().tobytes()
         else:
             data = ctypes.string_at(ptr, length)
+        mv = memoryview(data)
         for i in range(0, len(data), self.chunk):
-            self._reqs.put(pb.block.WriteRequest(chunk=pb.block.Chunk(data=data[i:i + self.chunk])))
+            self._reqs.put(marshal.write_request_frame(mv[i:i + self.chunk]))
 
     def commit(self):
         self._reqs.close()
@@ -576,8 +578,9 @@ class UfsWriter:
         if self._local is not None:
             self._local.write(data)
         else:
+            mv = memoryview(data)
             for i in range(0, len(data), 1 << 20):
-                self._q.put(pb.block.WriteRequest(chunk=pb.block.Chunk(data=data[i:i + (1 << 20)])))
+                self._q.put(marshal.write_request_frame(mv[i:i + (1 << 20)]))
 
     def close(self) -> None:
         if self._local is not None:

@@ -215,6 +215,26 @@ PYBIND11_MODULE(_C, m) {
            },
            py::arg("block_id"), py::arg("offset"), py::arg("length"), py::arg("dst"), py::arg("dst_kind"),
            py::arg("stream") = 0, py::arg("sync") = true)
+      // One gRPC data frame: ``header`` (hand-encoded protobuf prefix) followed by ``length`` block
+      // bytes, built in a single bytes object the transport sends as-is -- the block bytes are
+      // copied once (HBM/DRAM -> frame), not through a protobuf message (ReadResponseMarshaller).
+      .def("read_frame", [](BlockStore& s, int64_t id, uint64_t off, uint64_t len, py::bytes header) {
+             char* hp = nullptr;
+             Py_ssize_t hn = 0;
+             PyBytes_AsStringAndSize(header.ptr(), &hp, &hn);
+             PyObject* out = PyBytes_FromStringAndSize(nullptr, hn + static_cast<Py_ssize_t>(len));
+             if (out == nullptr) throw py::error_already_set();
+             py::bytes frame = py::reinterpret_steal<py::bytes>(out);
+             char* dst = PyBytes_AS_STRING(out);
+             std::memcpy(dst, hp, static_cast<size_t>(hn));
+             std::vector<ReadReq> rs{ReadReq{id, off, len, reinterpret_cast<uint64_t>(dst + hn), 0}};
+             {
+               py::gil_scoped_release rel;
+               s.read_batch(rs, 0, true);
+             }
+             return frame;
+           },
+           py::arg("block_id"), py::arg("offset"), py::arg("length"), py::arg("header"))
       .def("checksum", &BlockStore::checksum, G(), py::arg("block_id"), py::arg("piece_bytes") = 0)
       .def("fill_pattern", &BlockStore::fill_pattern, G())
       .def("free_space", &BlockStore::free_space, G(), py::arg("session"), py::arg("bytes"),

@@ -22,6 +22,7 @@ import grpc
 
 from ..proto import SERVICES
 from ..utils import exceptions as ex
+from . import marshal
 
 LOG = logging.getLogger(__name__)
 
@@ -157,6 +158,8 @@ class RpcServer:
         self.metrics = metrics
         self.enable_grpc = enable_grpc
         self._servicers: dict[str, object] = {}
+        # zero-copy data frames for ReadBlock/WriteBlock (alluxio.worker.network.zerocopy.enabled)
+        self.zero_copy = conf is None or conf.get_bool("alluxio.worker.network.zerocopy.enabled", "true")
         self._server = None
         self.address = None
         self.alive = False
@@ -189,7 +192,7 @@ class RpcServer:
                     if not hasattr(servicer, name):
                         continue
                     h = _Handler(servicer, spec, self.metrics, self.check, self.authenticator)
-                    des, ser = spec.request.FromString, spec.response.SerializeToString
+                    _, des, ser, _ = marshal.marshallers(spec, self.zero_copy)
                     if spec.client_streaming and spec.server_streaming:
                         handlers[name] = grpc.stream_stream_rpc_method_handler(h.stream, des, ser)
                     elif spec.client_streaming:
@@ -295,7 +298,8 @@ class Stub:
 
 
 class Channel:
-    def __init__(self, address: str, user: str | None = None, force_grpc: bool = False, auth="default"):
+    def __init__(self, address: str, user: str | None = None, force_grpc: bool = False, auth="default",
+                 zero_copy: bool = True):
         self.address = address
         self.user = user
         if auth == "default":      # SIMPLE as the login user (servers without SASL are tolerated)
@@ -303,6 +307,8 @@ class Channel:
             auth = ("SIMPLE", user or login_user(), "")
         self.auth = auth            # (type, user, password) or None (NOSASL)
         self.channel_id = None
+        # alluxio.user.streaming.zerocopy.enabled: frame-aware codecs on the block data streams
+        self.zero_copy = zero_copy
         with _LOCAL_LOCK:
             local = None if force_grpc else _LOCAL.get(address)
         self.local = local
@@ -396,7 +402,8 @@ class Channel:
                 return fn(it, RpcContext())
             return call
         ch = self._channel()
-        c = ch.stream_stream(spec.path, spec.request.SerializeToString, spec.response.FromString)
+        ser, _, _, des = marshal.marshallers(spec, self.zero_copy)
+        c = ch.stream_stream(spec.path, ser, des)
         md = self._md()
         return lambda it: c(it, metadata=md)
 
@@ -423,8 +430,9 @@ class ChannelPool:
                 from ..security.authentication import client_auth_from_conf
                 force = self.conf is not None and not self.conf.get_bool(
                     "alluxio.user.network.inprocess.transport.enabled", "true")
+                zc = self.conf is None or self.conf.get_bool("alluxio.user.streaming.zerocopy.enabled", "true")
                 c = self._chans[key] = Channel(address, user, force_grpc=force,
-                                               auth=client_auth_from_conf(self.conf, user))
+                                               auth=client_auth_from_conf(self.conf, user), zero_copy=zc)
             return c
 
     def drop(self, address: str, user: str | None = None) -> None:

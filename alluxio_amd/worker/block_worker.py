@@ -22,6 +22,7 @@ from .. import metrics as msys
 from ..ops.native import native_errors
 from ..proto import pb
 from ..utils import ids
+from ..rpc import marshal
 from ..utils.exceptions import (BlockDoesNotExistException, DeadlineExceededException,
                                 NotFoundException)
 from .store import TieredStore
@@ -245,22 +246,20 @@ class BlockWorker:
             self.metrics.counter("BytesReadDevice").inc(n)
 
     def read_bytes(self, block_id: int, offset: int, length: int) -> bytes:
-        """Byte-stream read (gRPC ReadBlock): D2H into pinned staging, then copy out."""
-        st = self.staging()
-        out = bytearray(length)
-        pos = 0
-        while pos < length:
-            buf = st.acquire()
-            try:
-                n = min(st.size, length - pos)
-                with native_errors():
-                    self.native.read(block_id, offset + pos, n, buf.data_ptr(), HOST, 0, True)
-                out[pos:pos + n] = buf[:n].numpy().tobytes()
-            finally:
-                st.release(buf)
-            pos += n
+        """Byte-stream read: the block bytes land directly in a new ``bytes`` object (one copy)."""
+        with native_errors():
+            out = self.native.read_frame(block_id, offset, length, b"")
         self._count_read(length, HOST)
-        return bytes(out)
+        return out
+
+    def read_frame(self, block_id: int, offset: int, length: int):
+        """One zero-copy ``ReadResponse`` frame of block bytes for the gRPC data server
+        (rpc/marshal.py; reference ReadResponseMarshaller)."""
+        hdr = marshal.read_response_header(length)
+        with native_errors():
+            frame = self.native.read_frame(block_id, offset, length, hdr)
+        self._count_read(length, HOST)
+        return marshal.DataFrame(frame, len(hdr))
 
     # ---- management ---------------------------------------------------------------------------
     def remove_block(self, session_id: int, block_id: int) -> None:

@@ -18,6 +18,7 @@ import os
 import threading
 
 from ..proto import enum_name, pb
+from ..rpc import marshal
 from ..utils import ids
 from ..utils.exceptions import (BlockDoesNotExistException, InvalidArgumentException,
                                 UnavailableException)
@@ -95,10 +96,10 @@ class BlockWorkerService:
                     while pos - acked[0] >= self.window and not done.is_set():
                         cond.wait(0.5)
                 n = min(chunk, end - pos)
-                data = self.w.read_bytes(bid, pos, n)
+                frame = self.w.read_frame(bid, pos, n)      # header + bytes, sent as-is
                 pos += n
                 read_counter.inc(n)
-                yield pb.block.ReadResponse(chunk=pb.block.Chunk(data=data))
+                yield frame
         finally:
             if lock_id is not None:
                 try:
@@ -119,7 +120,7 @@ class BlockWorkerService:
             if not data:
                 break
             pos += len(data)
-            yield pb.block.ReadResponse(chunk=pb.block.Chunk(data=data))
+            yield marshal.read_response_frame(data)
 
     # ------------------------------------------------------------------------------------------
     def WriteBlock(self, request_iter, ctx):
