@@ -147,7 +147,11 @@ class FileSystemAdminShell:
     # ---- other commands ---------------------------------------------------------------------
     def cmd_backup(self, args) -> int:
         target = next((a for a in args if not a.startswith("-")), "")
-        req = pb.meta.BackupPRequest(options=pb.meta.BackupPOptions(localFileSystem="--local" in args),
+        # [directory] [--local] [--allow-leader] (BackupCommand: delegated to a standby in HA
+        # clusters when alluxio.master.backup.delegation.enabled; --allow-leader permits the
+        # primary to take it when no standby is available)
+        req = pb.meta.BackupPRequest(options=pb.meta.BackupPOptions(localFileSystem="--local" in args,
+                                                                    allowLeader="--allow-leader" in args),
                                      targetDirectory=target)
         st = self.ctx.meta_master().Backup(req)
         state = enum_name(pb.meta.BackupState, st.backupState)

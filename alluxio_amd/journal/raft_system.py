@@ -48,6 +48,12 @@ class JournalStateMachine:
         self.ignore_applies = False
         self.last_primary_start = 0
         self.applied_entries = 0
+        # delegated backup on a follower: entries are parked instead of applied, so the masters'
+        # state can be brought to exactly the sequence the primary chose (JournalStateMachine
+        # suspend / catchup / resume)
+        self.suspended = False
+        self._parked: list = []
+        self._susp_lock = threading.Condition()
 
     def apply(self, index: int, payload: bytes) -> None:
         kind = payload[:1]
@@ -68,13 +74,55 @@ class JournalStateMachine:
         self.applied_entries += 1
         if self.ignore_applies:
             return
+        with self._susp_lock:
+            if self.suspended:
+                self._parked.append((master, e))
+                self._susp_lock.notify_all()
+                return
+        self._apply_to_master(master, e)
+
+    def _apply_to_master(self, master: str, e) -> None:
         comp = self.system._journaled.get(master)
         if comp is None:
             LOG.warning("journal entry for unknown master %s", master)
             return
         UfsJournalSystem._apply(comp, e)
 
+    def suspend(self) -> None:
+        with self._susp_lock:
+            self.suspended = True
+
+    def catchup(self, target_sn: int, timeout: float) -> None:
+        """Apply parked entries with sequence number < ``target_sn``, waiting for them to arrive."""
+        deadline = time.monotonic() + timeout
+        with self._susp_lock:
+            if not self.suspended:
+                raise RuntimeError("catchup needs a suspended state machine")
+            while True:
+                keep = []
+                for master, e in self._parked:
+                    if e.sequence_number < target_sn:
+                        self._apply_to_master(master, e)
+                    else:
+                        keep.append((master, e))
+                self._parked = keep
+                if self.next_sn >= target_sn:
+                    return
+                rem = deadline - time.monotonic()
+                if rem <= 0:
+                    raise TimeoutError(f"state machine catch-up to {target_sn} timed out at {self.next_sn}")
+                self._susp_lock.wait(min(rem, 0.1))
+
+    def resume(self) -> None:
+        with self._susp_lock:
+            for master, e in self._parked:
+                self._apply_to_master(master, e)
+            self._parked = []
+            self.suspended = False
+
     def write_snapshot(self, path: str, index: int, term: int, peers) -> None:
+        if self.suspended:
+            raise RuntimeError("journal application is suspended (backup in progress)")
         comps = self.system.journaled
         hdr = pb.raft.RaftSnapshotHeader(index=index, term=term, peers=list(peers),
                                          nextSequenceNumber=self.next_sn, masters=sorted(comps))
@@ -243,6 +291,8 @@ class RaftPrimarySelector:
         self._on_primary = self._on_secondary = None
         self._state = self.SECONDARY
 
+    halt = stop       # no lock to hold: just stop reacting to leadership changes
+
 
 class RaftJournalSystem(JournalSystem):
     def __init__(self, root: str, local_address: str, cluster_addresses, *, conf=None, bind_host: str | None = None,
@@ -397,6 +447,8 @@ class RaftJournalSystem(JournalSystem):
         """Catch up on everything committed before this term, then take over writing."""
         node = self.node
         timeout = max(30.0, 20 * node.T)
+        if self.sm.suspended:           # a delegated backup was in flight on this follower
+            self.sm.resume()
         self._snapshot_allowed = False
         while True:
             if not node.is_leader():
@@ -479,6 +531,20 @@ class RaftJournalSystem(JournalSystem):
     def sequence_numbers(self) -> dict[str, int]:
         sn = (self._writer.next_sn if self._writer is not None else self.sm.next_sn)
         return {name: sn for name in self.journaled}
+
+    def suspend(self) -> None:
+        if self._writer is not None:
+            raise RuntimeError("cannot suspend the primary's journal")
+        self._snapshot_allowed = False
+        self.sm.suspend()
+
+    def catchup(self, sequences: dict[str, int], timeout: float = 60.0) -> None:
+        # one global sequence across masters: the requested point is the largest of them
+        self.sm.catchup(max(sequences.values(), default=0), timeout)
+
+    def resume(self) -> None:
+        self.sm.resume()
+        self._snapshot_allowed = True
 
     # ---- quorum management -----------------------------------------------------------------------
     def quorum_info(self) -> list[tuple[str, bool]]:

@@ -186,6 +186,17 @@ class JournalSystem:
     def sequence_numbers(self) -> dict[str, int]:
         return {}
 
+    # ---- standby journal application control (JournalSystem.suspend/catchup/resume, used by
+    # the backup-worker role to take a backup at a sequence chosen by the primary) ----------------
+    def suspend(self) -> None:
+        raise NotImplementedError(f"{type(self).__name__} cannot suspend journal application")
+
+    def catchup(self, sequences: dict[str, int], timeout: float = 60.0) -> None:
+        raise NotImplementedError(f"{type(self).__name__} cannot catch up to given sequences")
+
+    def resume(self) -> None:
+        raise NotImplementedError(f"{type(self).__name__} cannot resume journal application")
+
 
 class NoopJournalSystem(JournalSystem):
     """No persistence (tests, ephemeral masters)."""
@@ -206,6 +217,7 @@ class UfsJournalSystem(JournalSystem):
         self._lock = threading.RLock()
         self._tail_thread = None
         self._tail_stop = threading.Event()
+        self._suspended = False        # standby: tailing paused for a delegated backup
 
     def register(self, j: Journaled) -> None:
         super().register(j)
@@ -269,6 +281,8 @@ class UfsJournalSystem(JournalSystem):
                 return
             try:
                 with self._lock:
+                    if self._suspended:
+                        continue
                     for name, j in self._journals.items():
                         comp = self._journaled[name]
                         start = self._applied.get(name, 0)
@@ -278,12 +292,53 @@ class UfsJournalSystem(JournalSystem):
             except Exception:  # noqa: BLE001
                 LOG.exception("journal tailing failed")
 
+    def suspend(self) -> None:
+        """Stop applying tailed entries (UfsJournalSystem.suspend)."""
+        with self._lock:
+            if self.primary:
+                raise RuntimeError("cannot suspend the primary's journal")
+            self._suspended = True
+
+    def catchup(self, sequences: dict[str, int], timeout: float = 60.0) -> None:
+        """Apply tailed entries exactly up to ``sequences`` (exclusive, per master) while
+        suspended, waiting for the primary's logs to reach them (UfsJournalSystem.catchup)."""
+        deadline = time.monotonic() + timeout
+        while True:
+            with self._lock:
+                if not self._suspended:
+                    raise RuntimeError("catchup needs a suspended journal")
+                behind = False
+                for name, target in sequences.items():
+                    j, comp = self._journals.get(name), self._journaled.get(name)
+                    if j is None or comp is None:
+                        continue
+                    start = self._applied.get(name, 0)
+                    if start > target:
+                        raise RuntimeError(f"{name} already applied {start} > requested {target}")
+                    if start < target:
+                        for e in j.iter_log_entries(start):
+                            if e.sequence_number >= target:
+                                break
+                            self._apply(comp, e)
+                            self._applied[name] = e.sequence_number + 1
+                    behind = behind or self._applied.get(name, 0) < target
+                if not behind:
+                    return
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"journal catch-up to {sequences} timed out")
+            time.sleep(0.05)
+
+    def resume(self) -> None:
+        with self._lock:
+            self._suspended = False
+
     def gain_primacy(self) -> None:
         self._tail_stop.set()
         if self._tail_thread is not None:
             self._tail_thread.join(timeout=5)
         with self._lock:
             # catch up fully, then become the writer
+            self._suspended = False
             self._replay_all()
             for name, j in self._journals.items():
                 nxt = max(self._applied.get(name, 0), j.next_sequence_number())

@@ -112,9 +112,13 @@ class FileLockPrimarySelector(PrimarySelector):
                 os.close(self._fd)
                 self._fd = None
 
-    def stop(self) -> None:
+    def halt(self) -> None:
+        """Stop contending for primacy but keep a held lock (shutdown closes the journal first)."""
         self._stop.set()
         if self._t is not None and self._t is not threading.current_thread():
             self._t.join(timeout=5)
+
+    def stop(self) -> None:
+        self.halt()
         self._release()
         self._state = self.SECONDARY

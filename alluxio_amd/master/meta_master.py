@@ -11,7 +11,6 @@ metrics/DefaultMetricsMaster.java + MetricsStore.java (worker/client metrics agg
 from __future__ import annotations
 
 import gzip
-import io
 import logging
 import os
 import threading
@@ -43,7 +42,7 @@ class MetaMaster(Journaled):
         self.safe_mode = False
         self._standbys: dict[int, dict] = {}
         self._worker_configs: dict[str, dict] = {}
-        self._backups: dict[str, pb.meta.BackupPStatus] = {}
+        self.backup_role = None          # master.backup.BackupLeaderRole
         self._lock = threading.RLock()
         self.masters_for_backup: list[Journaled] = []
         self.journal_system_for_checkpoint = None
@@ -198,33 +197,21 @@ class MetaMaster(Journaled):
                 info.workerAddresses.append(pb.grpc.NetAddress(host=w.address.host, rpcPort=w.address.rpcPort))
         return info
 
-    # ---- backup / restore (BackupManager + BackupLeaderRole) ----------------------------------
-    def backup(self, target_dir: str | None = None, local: bool = True) -> pb.meta.BackupPStatus:
-        bid = uuid.uuid4().hex
-        target_dir = target_dir or self.conf.get("alluxio.master.backup.directory", "/tmp/alluxio_backups")
-        os.makedirs(target_dir, exist_ok=True)
-        name = time.strftime("alluxio-backup-%Y-%m-%d-%H%M%S", time.gmtime()) + f"-{bid[:6]}.gz"
-        path = os.path.join(target_dir, name)
-        status = pb.meta.BackupPStatus(backupId=bid, backupState=4, backupHost=self.master_address.split(":")[0])
-        self._backups[bid] = status
-        count = 0
-        buf = io.BytesIO()
-        for m in self.masters_for_backup:
-            for e in m.journal_entries():
-                jfmt.write_delimited(buf, e)
-                count += 1
-        with gzip.open(path, "wb") as f:
-            f.write(buf.getvalue())
-        status.backupState = 5
-        status.backupUri = path
-        status.entryCount = count
-        return status
+    # ---- backup (master/backup.py BackupLeaderRole) ---------------------------------------------
+    def backup(self, req: pb.meta.BackupPRequest) -> pb.meta.BackupPStatus:
+        if self.backup_role is None:
+            raise RuntimeError("backups need a master process (no backup role attached)")
+        return self.backup_role.backup(req)
 
     def backup_status(self, backup_id: str):
-        s = self._backups.get(backup_id)
-        if s is None:
+        if self.backup_role is None:
             return pb.meta.BackupPStatus(backupId=backup_id, backupState=1)
-        return s
+        return self.backup_role.status(backup_id)
+
+    def standby_rpc_addresses(self) -> list[str]:
+        """RPC addresses of the standby masters registered through MetaMasterSync."""
+        with self._lock:
+            return [f"{i['address'].host}:{i['address'].rpcPort}" for i in self._standbys.values()]
 
     def checkpoint(self) -> str:
         if self.journal_system_for_checkpoint is not None:
@@ -314,7 +301,7 @@ class MetaServices:
 
     # MetaMasterClientService
     def Backup(self, req, ctx):
-        return self.meta.backup(req.targetDirectory or None, req.options.localFileSystem)
+        return self.meta.backup(req)
 
     def GetBackupStatus(self, req, ctx):
         return self.meta.backup_status(req.backupId)

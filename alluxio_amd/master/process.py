@@ -109,6 +109,14 @@ class AlluxioMasterProcess:
         self.meta_master.masters_for_backup = [m for m in (self.block_master, self.fs_master, self.meta_master,
                                                             self.table_master) if m is not None]
         self.meta_master.journal_system_for_checkpoint = self   # checkpoint() under the state lock
+        from .backup import BackupLeaderRole, BackupWorkerRole, DailyMetadataBackup, MetaMasterSync
+        self.backup_leader = BackupLeaderRole(self)
+        self.backup_worker = BackupWorkerRole(self)
+        self.meta_master.backup_role = self.backup_leader
+        self.daily_backup = (DailyMetadataBackup(self.backup_leader, self.conf)
+                             if self.conf.get_bool("alluxio.master.daily.backup.enabled", "false") else None)
+        self.meta_sync = MetaMasterSync(self, self._primary_candidates)
+        self._peer_channels = None
         self.server = RpcServer(host, self.port, max_workers=self.conf.get_int("alluxio.master.rpc.executor.max.pool.size", 500)
                                 if False else 64, metrics=self.metrics, enable_grpc=enable_grpc,
                                 conf=self.conf)
@@ -127,6 +135,7 @@ class AlluxioMasterProcess:
             self.replication_checker = ReplicationChecker(self.fs_master, self.job_master)
         self.web = None
         self.selector = None
+        self._standby_hb = None
         self.web_port = 0
         self.start_time = time.time()
         self.started = False
@@ -146,6 +155,16 @@ class AlluxioMasterProcess:
         reg.gauge("Cluster.CapacityUsed", bm.used_bytes)
         reg.gauge("Cluster.CapacityFree", lambda: bm.capacity_bytes() - bm.used_bytes())
         reg.gauge("Cluster.Workers", bm.worker_count)
+
+    def _primary_candidates(self) -> list[str]:
+        return [a.strip() for a in (self.conf.get_raw("alluxio.master.rpc.addresses") or "").split(",") if a.strip()]
+
+    def peer_stub(self, address: str, service: str):
+        """Stub of another master's service over the pooled channels (delegated backups)."""
+        from ..rpc import ChannelPool
+        if self._peer_channels is None:
+            self._peer_channels = ChannelPool(self.conf)
+        return self._peer_channels.get(address).stub(service)
 
     def _job_fs(self):
         from ..client.file_system import FileSystem
@@ -197,6 +216,8 @@ class AlluxioMasterProcess:
         if self.table_master is not None:
             from ..table.master import SVC_TABLE, TableMasterService
             s.add_servicer(SVC_TABLE, TableMasterService(self.table_master))
+        from .backup import SVC_BACKUP_WORKER
+        s.add_servicer(SVC_BACKUP_WORKER, self.backup_worker)
         s.add_servicer(SVC_VERSION, ServiceVersionHandler())
         s.add_servicer(SVC_SASL, SaslHandler())
 
@@ -223,8 +244,10 @@ class AlluxioMasterProcess:
         if ha:
             from ..utils.exceptions import UnavailableException
 
+            from .backup import SVC_BACKUP_WORKER
+
             def standby_gate(spec):
-                if not self.primary:
+                if not self.primary and spec.service != SVC_BACKUP_WORKER:
                     raise UnavailableException("master is a standby (not primary)")
             self.server.gate = standby_gate
         addr = self.server.start()
@@ -248,6 +271,11 @@ class AlluxioMasterProcess:
                 if start_heartbeats:
                     self._start_heartbeats()
             self.selector.start(on_primary, self.lose_primacy)
+            # standbys register with and heartbeat the primary (MetaMasterSync)
+            self._standby_hb = hb.HeartbeatThread(
+                hb.META_MASTER_SYNC,
+                self.meta_sync.heartbeat, self.conf.get_ms("alluxio.master.standby.heartbeat.interval", "2min"))
+            self._standby_hb.start()
         elif start_heartbeats and primary:
             self._start_heartbeats()
         self.started = True
@@ -269,6 +297,8 @@ class AlluxioMasterProcess:
         self.meta_master.start(True)
         self.safe_mode.notify_primary()
         self.primary = True
+        if self.daily_backup is not None:
+            self.daily_backup.start()
 
     def lose_primacy(self) -> None:
         """Step down to standby: refuse RPCs, stop primary-only heartbeats, and let the journal
@@ -277,6 +307,8 @@ class AlluxioMasterProcess:
             return
         LOG.info("master %s lost primacy", getattr(self.server, "address", "?"))
         self.primary = False
+        if self.daily_backup is not None:
+            self.daily_backup.stop()
         threads, self._threads = self._threads, []
         for t in threads:
             t.shutdown(join=False)
@@ -331,8 +363,19 @@ class AlluxioMasterProcess:
     def stop(self) -> None:
         for sk in getattr(self, "_sinks", []):
             sk.stop()
-        if self.selector is not None:
-            self.selector.stop()
+        # no new elections from here on, but keep the primary lock until the journal writers are
+        # closed: releasing it first lets a standby start writing the same logs while this
+        # master still completes its current log file
+        if self.selector is not None and hasattr(self.selector, "halt"):
+            self.selector.halt()
+        if getattr(self, "_standby_hb", None) is not None:
+            self._standby_hb.shutdown(join=True)
+            self._standby_hb = None
+        if self.daily_backup is not None:
+            self.daily_backup.stop()
+        if self._peer_channels is not None:
+            self._peer_channels.close()
+            self._peer_channels = None
         self.primary = False
         for t in self._threads:
             t.shutdown(join=False)
@@ -347,6 +390,8 @@ class AlluxioMasterProcess:
             self._job_client_fs.close()
             self._job_client_fs = None
         self.journal.stop()
+        if self.selector is not None:
+            self.selector.stop()
         self.started = False
 
 

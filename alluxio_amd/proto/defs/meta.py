@@ -52,6 +52,14 @@ msg RegisterMasterPResponse
 msg MasterHeartbeatPOptions
 msg MasterHeartbeatPRequest masterId=1:i64 options=2:MasterHeartbeatPOptions
 msg MasterHeartbeatPResponse command=1:MetaCommand
+msg JournalSequence master=1:str sequence=2:i64
+msg BackupSuspendPRequest
+msg BackupSuspendPResponse
+msg BackupDelegatePRequest backupId=1:str request=2:BackupPRequest sequences=3:JournalSequence*
+msg BackupDelegatePResponse
+rpc BackupWorkerService SuspendJournals BackupSuspendPRequest BackupSuspendPResponse
+rpc BackupWorkerService DelegateBackup BackupDelegatePRequest BackupDelegatePResponse
+rpc BackupWorkerService GetBackupStatus BackupStatusPRequest BackupPStatus
 rpc MetaMasterClientService Backup BackupPRequest BackupPStatus
 rpc MetaMasterClientService GetBackupStatus BackupStatusPRequest BackupPStatus
 rpc MetaMasterClientService GetConfigReport GetConfigReportPOptions GetConfigReportPResponse
