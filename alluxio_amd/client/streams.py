@@ -17,7 +17,10 @@ import io
 import logging
 import queue
 import random
+import sys
 import threading
+
+import numpy as np
 
 from ..proto import enum_name, pb
 from ..rpc import marshal
@@ -32,15 +35,13 @@ HOST, DEVICE = 0, 1
 
 def _buffer_ptr(buf):
     """(pointer, nbytes, kind, keepalive) of a writable/readable buffer."""
-    try:
-        import torch
-        if isinstance(buf, torch.Tensor):
-            if not buf.is_contiguous():
-                raise ValueError("tensor must be contiguous")
-            return buf.data_ptr(), buf.numel() * buf.element_size(), DEVICE if buf.is_cuda else HOST, buf
-    except ImportError:  # pragma: no cover
-        pass
-    import numpy as np
+    # a tensor can only exist once torch is imported: never import it here (a multi-second
+    # first import under the module lock would stall every writer thread)
+    torch = sys.modules.get("torch")
+    if torch is not None and isinstance(buf, torch.Tensor):
+        if not buf.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return buf.data_ptr(), buf.numel() * buf.element_size(), DEVICE if buf.is_cuda else HOST, buf
     if isinstance(buf, np.ndarray):
         return buf.ctypes.data, buf.nbytes, HOST, buf
     arr = np.frombuffer(buf, dtype=np.uint8)
@@ -56,7 +57,6 @@ class BlockReader:
         raise NotImplementedError
 
     def read_bytes(self, offset: int, length: int) -> bytes:
-        import numpy as np
         out = np.empty(length, dtype=np.uint8)
         self.read_into(offset, length, out.ctypes.data, HOST)
         return out.tobytes()
@@ -244,7 +244,6 @@ def _copy_bytes_to(data: bytes, ptr: int, kind: int) -> None:
     if kind == HOST:
         ctypes.memmove(ptr, data, len(data))
         return
-    import numpy as np
     import torch
     src = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy())
     from ..ops.native import lib
@@ -295,7 +294,6 @@ class FileInStream(io.RawIOBase):
         n = min(len(mv), self.length - self.pos)
         if n <= 0:
             return 0
-        import numpy as np
         arr = np.frombuffer(mv, dtype=np.uint8, count=n)
         self._read_range(self.pos, n, arr.ctypes.data, HOST)
         self.pos += n
@@ -307,7 +305,6 @@ class FileInStream(io.RawIOBase):
         size = min(size, self.length - self.pos)
         if size <= 0:
             return b""
-        import numpy as np
         out = np.empty(size, dtype=np.uint8)
         self._read_range(self.pos, size, out.ctypes.data, HOST)
         self.pos += size

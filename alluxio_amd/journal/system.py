@@ -42,6 +42,11 @@ class Journaled:
 
 
 class AsyncJournalWriter:
+    """Group commit (AsyncJournalWriter.doFlush): the flush thread wakes as soon as a caller asks
+    for a flush (or ``flush.batch.time`` after entries were queued without one), writes everything
+    queued -- for at most one batch time per session -- and flushes once; entries arriving during
+    that flush ride the next one.  Latency is one write+flush, not a fixed batch window."""
+
     def __init__(self, writer: UfsJournalLogWriter, batch_ms: float = 5.0, flush_timeout_s: float = 300.0):
         self.writer = writer
         self.batch = batch_ms / 1000.0
@@ -49,7 +54,9 @@ class AsyncJournalWriter:
         self._cond = threading.Condition()
         self._queue: list = []
         self._appended = 0       # counter of appended entries
+        self._written = 0        # counter of entries handed to the writer
         self._flushed = 0        # counter of durably flushed entries
+        self._requested = 0      # highest counter a caller is waiting for
         self._error: BaseException | None = None
         self._closed = False
         self._thread = threading.Thread(target=self._run, daemon=True, name="journal-flush")
@@ -63,12 +70,14 @@ class AsyncJournalWriter:
                 raise UnavailableException(f"journal write failed: {self._error}")
             self._queue.append(entry)
             self._appended += 1
-            self._cond.notify_all()
             return self._appended
 
     def flush(self, counter: int) -> None:
         deadline = time.monotonic() + self.flush_timeout
         with self._cond:
+            if counter > self._requested:
+                self._requested = counter
+                self._cond.notify_all()
             while self._flushed < counter:
                 if self._error is not None:
                     raise UnavailableException(f"journal flush failed: {self._error}")
@@ -77,27 +86,44 @@ class AsyncJournalWriter:
                 rem = deadline - time.monotonic()
                 if rem <= 0:
                     raise UnavailableException("journal flush timed out")
-                self._cond.notify_all()
                 self._cond.wait(min(rem, 0.05))
 
     def _run(self) -> None:
         while True:
             with self._cond:
-                while not self._queue and not self._closed:
-                    self._cond.wait(0.1)
-                if not self._queue and self._closed:
-                    return
-            # batch window: let concurrent RPCs pile up (flush.batch.time)
-            if self.batch > 0:
-                time.sleep(self.batch)
-            with self._cond:
+                # stand still until entries are queued and someone waits for them (or the batch
+                # time passed since they were queued, to flush proactively)
+                waited_since = None
+                while True:
+                    if self._closed and not self._queue:
+                        return
+                    if self._queue and (self._requested > self._written or self._closed):
+                        break
+                    if self._queue:
+                        now = time.monotonic()
+                        waited_since = waited_since or now
+                        if now - waited_since >= self.batch:
+                            break
+                        self._cond.wait(self.batch - (now - waited_since))
+                    else:
+                        waited_since = None
+                        self._cond.wait(0.1)
                 batch, self._queue = self._queue, []
             try:
+                t0 = time.monotonic()
+                n = 0
                 for e in batch:
                     self.writer.write(e)
+                    n += 1
+                    if self.batch and n % 256 == 0 and time.monotonic() - t0 >= self.batch:
+                        break
+                if n < len(batch):       # session over: the rest goes first next time
+                    with self._cond:
+                        self._queue[:0] = batch[n:]
                 self.writer.flush()
                 with self._cond:
-                    self._flushed += len(batch)
+                    self._written += n
+                    self._flushed = self._written
                     self._cond.notify_all()
             except BaseException as e:  # noqa: BLE001
                 LOG.exception("journal flush failed")

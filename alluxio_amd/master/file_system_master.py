@@ -365,7 +365,10 @@ class FileSystemMaster(Journaled):
                 e.inode_file.should_persist_time = now_ms() + persistence_wait_ms
             self._apply(rpc, e)
             self._touch_parent(rpc, parent)
-            return self.file_info(self.tree.inodes[file_id], path)
+            inode = self.tree.inodes[file_id]
+        # the reply is built outside the namespace write lock
+        with self.tree.lock.read():
+            return self.file_info(inode, path)
 
     def _touch_parent(self, rpc, parent) -> None:
         self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(

@@ -99,31 +99,38 @@ class MountTable:
         with self._lock:
             for m in self._mounts.values():
                 self.ufs_manager.remove_mount(m.mount_id)
-            self._mounts.clear()
+            self._mounts = {}
 
     # ---- state changes (called from journal application) ------------------------------------
     def apply_add(self, info: MountInfo) -> None:
         with self._lock:
-            self._mounts[info.alluxio_path] = info
+            # copy-on-write: readers use the dict they loaded without taking the lock
+            m = dict(self._mounts)
+            m[info.alluxio_path] = info
+            self._mounts = m
             self.ufs_manager.add_mount(info.mount_id, info.ufs_uri, info.properties)
 
     def apply_delete(self, alluxio_path: str) -> MountInfo | None:
         with self._lock:
-            info = self._mounts.pop(alluxio_path, None)
+            m = dict(self._mounts)
+            info = m.pop(alluxio_path, None)
+            self._mounts = m
         if info is not None:
             self.ufs_manager.remove_mount(info.mount_id)
         return info
 
     # ---- queries ----------------------------------------------------------------------------
     def mount_point_for(self, path: str) -> str | None:
-        path = normalize_path(path)
-        with self._lock:
-            best = None
-            for mp in self._mounts:
-                if path == mp or path.startswith(mp.rstrip("/") + "/") or mp == "/":
-                    if best is None or len(mp) > len(best):
-                        best = mp
-            return best
+        """Deepest mount point at or above ``path``: one dict probe per path level, lock-free
+        (``_mounts`` is replaced, never mutated)."""
+        mounts = self._mounts
+        p = normalize_path(path)
+        while True:
+            if p in mounts:
+                return p
+            if p == "/":
+                return None
+            p = p[:p.rfind("/")] or "/"
 
     def is_mount_point(self, path: str) -> bool:
         with self._lock:
@@ -142,11 +149,13 @@ class MountTable:
 
     def resolve(self, path: str) -> Resolution:
         path = normalize_path(path)
+        mounts = self._mounts
         mp = self.mount_point_for(path)
-        if mp is None:
+        info = mounts.get(mp) if mp is not None else None
+        if info is None:
+            info = self._mounts.get(mp) if mp is not None else None
+        if info is None:
             raise InvalidPathException(f"no mount point for {path}")
-        with self._lock:
-            info = self._mounts[mp]
         rel = path[len(mp):] if mp != "/" else path
         rel = rel.lstrip("/")
         base = info.ufs_uri.rstrip("/")

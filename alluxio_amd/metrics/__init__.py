@@ -8,6 +8,7 @@ core/server/common/.../metrics/sink/{MetricsServlet,PrometheusMetricsServlet}.ja
 from __future__ import annotations
 
 import bisect
+import collections
 import csv
 import json
 import logging
@@ -21,54 +22,72 @@ from .keys import CATALOG, TYPES  # noqa: F401
 
 
 class Counter:
-    __slots__ = ("_v", "_lock")
+    """LongAdder-style counter: ``inc`` is one GIL-atomic deque append (no lock, so hot RPC paths
+    never convoy on it); pending increments are folded in under a lock when read or every 4096."""
+
+    __slots__ = ("_v", "_pending", "_lock")
 
     def __init__(self):
         self._v = 0
+        self._pending = collections.deque()
         self._lock = threading.Lock()
 
     def inc(self, n: int = 1) -> None:
-        with self._lock:
-            self._v += n
+        self._pending.append(n)
+        if len(self._pending) > 4096:
+            self._fold()
 
     def dec(self, n: int = 1) -> None:
+        self.inc(-n)
+
+    def _fold(self) -> int:
         with self._lock:
-            self._v -= n
+            q = self._pending
+            s = 0
+            for _ in range(len(q)):
+                s += q.popleft()
+            self._v += s
+            return self._v
 
     @property
     def count(self) -> int:
-        return self._v
+        return self._fold()
 
     def value(self):
-        return self._v
+        return self._fold()
 
 
 class Meter:
-    """Exponentially-weighted 1/5/15-minute rates + mean rate (Codahale semantics)."""
+    """Exponentially-weighted 1/5/15-minute rates + mean rate (Codahale semantics: marks go to an
+    uncounted adder, folded into the rates on 5 s ticks)."""
 
     _TICK = 5.0
 
     def __init__(self):
         self._lock = threading.Lock()
-        self._count = 0
+        self._count = Counter()
         self._start = time.monotonic()
         self._last_tick = self._start
-        self._uncounted = 0
+        self._uncounted = Counter()
         self._rates = [0.0, 0.0, 0.0]
         self._init = [False, False, False]
         self._alphas = [1 - math.exp(-self._TICK / 60.0 / m) for m in (1, 5, 15)]
 
     def mark(self, n: int = 1) -> None:
-        with self._lock:
-            self._tick()
-            self._count += n
-            self._uncounted += n
+        if time.monotonic() - self._last_tick >= self._TICK:
+            with self._lock:
+                self._tick()
+        self._count.inc(n)
+        self._uncounted.inc(n)
 
     def _tick(self):
         now = time.monotonic()
         while now - self._last_tick >= self._TICK:
-            inst = self._uncounted / self._TICK
-            self._uncounted = 0
+            with self._uncounted._lock:
+                q = self._uncounted._pending
+                pend = sum(q.popleft() for _ in range(len(q))) + self._uncounted._v
+                self._uncounted._v = 0
+            inst = pend / self._TICK
             for i, a in enumerate(self._alphas):
                 if self._init[i]:
                     self._rates[i] += a * (inst - self._rates[i])
@@ -79,7 +98,7 @@ class Meter:
 
     @property
     def count(self) -> int:
-        return self._count
+        return self._count.count
 
     def one_minute_rate(self) -> float:
         with self._lock:
@@ -88,32 +107,37 @@ class Meter:
 
     def mean_rate(self) -> float:
         el = time.monotonic() - self._start
-        return self._count / el if el > 0 else 0.0
+        return self.count / el if el > 0 else 0.0
 
     def value(self):
         return self.one_minute_rate()
 
 
 class Timer:
-    """Duration histogram (reservoir of the last 1028 samples) + meter."""
+    """Duration histogram (reservoir of the last 1028 samples) + meter; ``update`` is lock-free."""
 
     def __init__(self, reservoir: int = 1028):
-        self._lock = threading.Lock()
-        self._samples: list[float] = []
-        self._cap = reservoir
-        self._i = 0
+        self._samples = collections.deque(maxlen=reservoir)
         self.meter = Meter()
-        self._sum = 0.0
+        self._sum = collections.deque()
+        self._sum_v = 0.0
+        self._lock = threading.Lock()
 
     def update(self, seconds: float) -> None:
-        with self._lock:
-            if len(self._samples) < self._cap:
-                self._samples.append(seconds)
-            else:
-                self._samples[self._i % self._cap] = seconds
-                self._i += 1
-            self._sum += seconds
+        self._samples.append(seconds)
+        self._sum.append(seconds)
+        if len(self._sum) > 4096:
+            self._fold_sum()
         self.meter.mark()
+
+    def _fold_sum(self) -> float:
+        with self._lock:
+            q = self._sum
+            s = 0.0
+            for _ in range(len(q)):
+                s += q.popleft()
+            self._sum_v += s
+            return self._sum_v
 
     def time(self):
         t = self
@@ -132,14 +156,15 @@ class Timer:
         return self.meter.count
 
     def percentile(self, p: float) -> float:
-        with self._lock:
-            s = sorted(self._samples)
+        s = sorted(list(self._samples))
         if not s:
             return 0.0
         return s[min(len(s) - 1, int(p * len(s)))]
 
     def mean(self) -> float:
-        return self._sum / self.count if self.count else 0.0
+        total = self._fold_sum()
+        c = self.count
+        return total / c if c else 0.0
 
     def value(self):
         return self.mean()
@@ -177,6 +202,9 @@ class MetricsRegistry:
         self._m: dict[str, object] = {}
 
     def _get(self, name, factory):
+        m = self._m.get(name)          # lock-free hit (dict reads are atomic)
+        if m is not None:
+            return m
         with self._lock:
             m = self._m.get(name)
             if m is None:

@@ -26,6 +26,7 @@ from . import marshal
 
 LOG = logging.getLogger(__name__)
 
+
 class _LocalRegistry(dict):
     """service full name -> servicer, plus liveness/gate shared with the owning RpcServer."""
 
@@ -314,6 +315,7 @@ class Channel:
         self.local = local
         self._grpc = None
         self._lock = threading.Lock()
+        self._stubs: dict[str, Stub] = {}
 
     @property
     def is_local(self) -> bool:
@@ -386,7 +388,11 @@ class Channel:
         return _GrpcMethod(c, spec, self._md())
 
     def stub(self, service: str) -> Stub:
-        return Stub(self, service)
+        # stubs are immutable bundles of bound methods: build one per service, not per call
+        st = self._stubs.get(service)
+        if st is None:
+            st = self._stubs[service] = Stub(self, service)
+        return st
 
     def raw_stream(self, service: str, method: str):
         """Direct access to a streaming callable (for flow-controlled data streams)."""
@@ -409,6 +415,7 @@ class Channel:
 
     def close(self) -> None:
         with self._lock:
+            self._stubs = {}
             if self._grpc is not None:
                 self._grpc.close()
                 self._grpc = None
@@ -424,6 +431,9 @@ class ChannelPool:
 
     def get(self, address: str, user: str | None = None) -> Channel:
         key = (address, user)
+        c = self._chans.get(key)       # lock-free hit: every RPC comes through here
+        if c is not None:
+            return c
         with self._lock:
             c = self._chans.get(key)
             if c is None:
@@ -507,8 +517,8 @@ class FailoverChannel:
 
     @property
     def current(self) -> str:
-        with self._lock:
-            return self.addresses[self._i % len(self.addresses)]
+        # lock-free read (one int + list index, GIL-atomic); rotate() mutates under the lock
+        return self.addresses[self._i % len(self.addresses)]
 
     @property
     def address(self) -> str:

@@ -14,6 +14,8 @@ import getpass
 import grp
 import os
 import pwd
+import threading
+import time
 
 from ..utils.exceptions import AccessControlException
 from .acl import AccessControlList, Bits  # noqa: F401
@@ -55,7 +57,26 @@ class as_user:
 
 
 class GroupMapping:
+    """Unix shell-style group lookup with a TTL cache (CachedGroupMapping,
+    ``alluxio.security.group.mapping.cache.timeout``, 1min): group lookups scan the whole group
+    database, and every namespace mutation asks for the caller's primary group."""
+
+    cache_ttl_s = 60.0
+    _cache: dict = {}
+    _cache_lock = threading.Lock()
+
     def groups(self, user: str) -> list[str]:
+        now = time.monotonic()
+        key = (type(self), user)
+        hit = GroupMapping._cache.get(key)
+        if hit is not None and now - hit[0] < self.cache_ttl_s:
+            return list(hit[1])
+        out = self._lookup(user)
+        with GroupMapping._cache_lock:
+            GroupMapping._cache[key] = (now, tuple(out))
+        return out
+
+    def _lookup(self, user: str) -> list[str]:
         out = []
         try:
             pw = pwd.getpwnam(user)

@@ -10,6 +10,7 @@ operations are in docs/en/operation/Scalability-Tuning.md:142-148.
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import threading
 import time
@@ -83,10 +84,10 @@ def main(argv=None, fs=None, print_result=True) -> dict:
     end = record_from + dur_s
     results = []
 
+    ids_ = itertools.count(1)
+
     def next_id():
-        with lock:
-            counter[0] += 1
-            return counter[0]
+        return next(ids_)        # GIL-atomic; a shared mutex here would throttle the clients
 
     def op_once(c, tid):
         i = next_id()

@@ -8,6 +8,7 @@ master inode tree and the control plane.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import threading
 import time
@@ -15,32 +16,54 @@ from collections import defaultdict
 
 
 class RWLock:
-    """Writer-preferring reentrant-for-readers RW lock with timeouts."""
+    """Writer-preferring RW lock, reentrant for readers, with timeouts.
+
+    Readers take a lock-free fast path: one GIL-atomic ``deque.append`` plus a check of the writer
+    gate (Dekker-style: a writer raises the gate, then waits for the reader deque to drain; a
+    reader appends, then backs out if the gate is up).  Uncontended read-mostly namespaces (every
+    getStatus / listStatus) therefore never serialise on a mutex the way a Condition-based lock
+    does under the GIL.  Writers, and readers that meet a writer, use the condition variable.
+    """
 
     def __init__(self):
         self._cond = threading.Condition(threading.Lock())
-        self._readers = 0
+        self._readers = collections.deque()   # one token per held read (all threads)
         self._writer: int | None = None
         self._writer_depth = 0
         self._waiting_writers = 0
+        self._gate = False                    # a writer holds or waits for the lock
+        self._tls = threading.local()         # this thread's read depth
+
+    def _depth(self) -> int:
+        return getattr(self._tls, "d", 0)
 
     def acquire_read(self, timeout: float | None = None) -> bool:
-        me = threading.get_ident()
+        d = self._depth()
+        if d or self._writer == threading.get_ident():
+            # nested read, or the write holder reading: never blocks
+            self._readers.append(1)
+            self._tls.d = d + 1
+            return True
+        self._readers.append(1)
+        if not self._gate:
+            self._tls.d = 1
+            return True
+        self._readers.pop()                   # a writer is in: back out and wait for it
         deadline = None if timeout is None else time.monotonic() + timeout
         with self._cond:
-            if self._writer == me:  # write lock holder may read
-                self._readers += 1
-                return True
-            while self._writer is not None or self._waiting_writers:
+            self._cond.notify_all()
+            while self._gate:
                 if not self._wait(deadline):
                     return False
-            self._readers += 1
-            return True
+            self._readers.append(1)
+        self._tls.d = 1
+        return True
 
     def release_read(self) -> None:
-        with self._cond:
-            self._readers -= 1
-            if self._readers == 0:
+        self._readers.pop()
+        self._tls.d = self._depth() - 1
+        if self._gate:
+            with self._cond:
                 self._cond.notify_all()
 
     def acquire_write(self, timeout: float | None = None) -> bool:
@@ -51,14 +74,22 @@ class RWLock:
                 self._writer_depth += 1
                 return True
             self._waiting_writers += 1
+            self._gate = True
+            ok = True
             try:
                 while self._writer is not None or self._readers:
                     if not self._wait(deadline):
-                        return False
+                        ok = False
+                        break
             finally:
                 self._waiting_writers -= 1
+            if not ok:                        # timed out: reopen the gate unless others need it
+                self._gate = self._writer is not None or self._waiting_writers > 0
+                self._cond.notify_all()
+                return False
             self._writer = me
             self._writer_depth = 1
+            self._gate = True
             return True
 
     def release_write(self) -> None:
@@ -66,6 +97,7 @@ class RWLock:
             self._writer_depth -= 1
             if self._writer_depth == 0:
                 self._writer = None
+                self._gate = self._waiting_writers > 0
                 self._cond.notify_all()
 
     def _wait(self, deadline) -> bool:
@@ -100,7 +132,7 @@ class RWLock:
 
     @property
     def reader_count(self) -> int:
-        return self._readers
+        return len(self._readers)
 
 
 class LockPool:

@@ -15,9 +15,20 @@ ROOT = "/"
 SCHEME = "alluxio"
 
 
+def _is_normal(path: str) -> bool:
+    """Already canonical: absolute, no empty / ``.`` / ``..`` components, no trailing slash."""
+    if path == ROOT:
+        return True
+    if path[0] != SEPARATOR or path[-1] == SEPARATOR or "//" in path:
+        return False
+    return "/." not in path or all(c not in (".", "..") for c in path.split(SEPARATOR))
+
+
 def normalize_path(path: str) -> str:
     if not path:
         return ROOT
+    if _is_normal(path):           # the common case on every RPC: no normpath work
+        return path
     if not path.startswith(SEPARATOR):
         path = SEPARATOR + path
     out = posixpath.normpath(path)
@@ -112,7 +123,8 @@ def as_uri(path) -> AlluxioURI:
 
 
 def path_components(path: str) -> list[str]:
-    return [c for c in normalize_path(path).split(SEPARATOR) if c]
+    p = normalize_path(path)
+    return p.split(SEPARATOR)[1:] if p != ROOT else []
 
 
 def join_path(*parts: str) -> str:

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""StressMasterBench against a standalone master process over gRPC, with the client threads spread
+over several client processes -- the setup of the reference's published master numbers
+(docs/en/operation/Scalability-Tuning.md:142-148: one master, 32 clients on other hosts).
+
+    python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile \
+        --procs 4 --threads 8 --duration 5s --out profiles/master_bench.json
+
+Each client process runs ``alluxio_amd.stress.master_bench`` with ``--threads`` threads; the
+result is the sum of the processes' throughputs (they run the same timed window).  CPU only: no
+GPU is touched.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CLIENT = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.stress import master_bench
+fs = FileSystem(master_address={addr!r})
+r = master_bench.main({args!r}, fs=fs, print_result=False)
+print("RESULT " + json.dumps(r))
+fs.close()
+"""
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run(ops, procs, threads, duration, warmup, journal_dir=None) -> list[dict]:
+    work = tempfile.mkdtemp(prefix="mbench_")
+    port, web = _free_port(), _free_port()
+    conf_dir = os.path.join(work, "conf")
+    os.makedirs(conf_dir)
+    with open(os.path.join(conf_dir, "alluxio-site.properties"), "w") as f:
+        f.write(f"alluxio.master.journal.folder={journal_dir or os.path.join(work, 'journal')}\n")
+        f.write(f"alluxio.master.mount.table.root.ufs={os.path.join(work, 'ufs')}\n")
+        f.write(f"alluxio.master.web.port={web}\n")
+        f.write("alluxio.master.journal.type=UFS\n")
+    env = dict(os.environ, ALLUXIO_CONF_DIR=conf_dir, PYTHONPATH=ROOT)
+    master = subprocess.Popen([sys.executable, "-m", "alluxio_amd.master.process", "--host", "127.0.0.1",
+                               "--port", str(port), "--format"], env=env, cwd=work,
+                              stdout=subprocess.DEVNULL, stderr=open(os.path.join(work, "master.log"), "w"))
+    addr = f"127.0.0.1:{port}"
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            with socket.socket() as s:
+                if s.connect_ex(("127.0.0.1", port)) == 0:
+                    break
+            time.sleep(0.2)
+        time.sleep(1.0)
+        out = []
+        for op in ops:
+            args = ["--operation", op, "--threads", str(threads), "--duration", duration, "--warmup", warmup,
+                    "--base", f"/stress-{op}"]
+            ps = []
+            for i in range(procs):
+                a = args + ["--base", f"/stress-{op}-{i}"]
+                ps.append(subprocess.Popen([sys.executable, "-c", CLIENT.format(root=ROOT, addr=addr, args=a)],
+                                           env=env, cwd=work, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                           text=True))
+            res = []
+            for p in ps:
+                so, _ = p.communicate(timeout=600)
+                line = next((ln for ln in so.splitlines() if ln.startswith("RESULT ")), None)
+                if line:
+                    res.append(json.loads(line[7:]))
+            total = sum(r["throughput_ops"] for r in res)
+            p50 = sorted(r["latency_ms"]["p50"] for r in res)[len(res) // 2] if res else None
+            errs = sum(len(r["errors"]) for r in res)
+            row = {"operation": op, "procs": procs, "threads_per_proc": threads, "ops_per_s": round(total, 1),
+                   "p50_ms": p50, "errors": errs}
+            print(json.dumps(row), flush=True)
+            out.append(row)
+        return out
+    finally:
+        master.terminate()
+        try:
+            master.wait(10)
+        except subprocess.TimeoutExpired:
+            master.kill()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="CreateFile,GetFileStatus,ListDir,DeleteFile")
+    ap.add_argument("--procs", type=int, default=4)
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--duration", default="5s")
+    ap.add_argument("--warmup", default="1s")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    rows = run(a.ops.split(","), a.procs, a.threads, a.duration, a.warmup)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"setup": f"1 master process + {a.procs} client processes x {a.threads} threads, gRPC, "
+                                f"UFS journal on local disk, {os.cpu_count()} CPUs", "results": rows}, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
