@@ -193,49 +193,117 @@ class MemPageStore:
 
 
 class HbmPageStore:
-    """Fixed-size page slots in one device arena; hits copy device-to-device."""
+    """Fixed page slots in one HBM arena, indexed by the native device hash table (K9).
 
-    def __init__(self, capacity: int, page_size: int, device=None):
-        import torch
+    Backed by ``_C.PageCache`` (csrc/page_cache.{h,cpp}): page ``(file_id, index)`` has the key
+    ``(interned file id << 24) | index``.  The open-addressing table keeps an authoritative host
+    mirror plus a device copy probed by ``page_lookup_gather_kernel`` (csrc/kernels.hip), so a batch
+    of pages whose keys are computed ON the GPU (a device-side sampler) is resolved and copied by
+    one launch (:meth:`gather`) with no host round trip.  Pages shorter than the page size can use
+    up the slots before the manager's byte budget does: the native store then evicts its least
+    recently used pages (host gets and device gathers both count as uses) and reports them through
+    ``on_evict`` so the manager's metastore stays exact.  Without a HIP device the same table and
+    arena live in host memory (CPU builds and tests).
+    """
+
+    INDEX_BITS = 24
+
+    def __init__(self, capacity: int, page_size: int, device=None, use_device: bool | None = None):
+        from ..ops.native import has_gpu, lib
         self.page_size = page_size
-        self.slots = max(1, capacity // page_size)
-        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
-        self.arena = torch.empty(self.slots * page_size, dtype=torch.uint8, device=self.device)
-        self.free = list(range(self.slots - 1, -1, -1))
-        self.slot_of: dict = {}
-        self.len_of: dict = {}
+        self.use_device = has_gpu() if use_device is None else bool(use_device)
+        self.device = None
+        dev = 0
+        if self.use_device:
+            import torch
+            self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+            dev = self.device.index
+        self.cache = lib().PageCache(dev, max(1, capacity // page_size) * page_size, page_size, self.use_device)
+        self.slots = self.cache.slots
+        self._fid: dict = {}
+        self._fname: list = []
+        self._lock = threading.Lock()
+        self.on_evict = None
+
+    def file_key(self, file_id) -> int:
+        file_id = str(file_id)
+        k = self._fid.get(file_id)
+        if k is None:
+            with self._lock:
+                k = self._fid.get(file_id)
+                if k is None:
+                    k = len(self._fname)
+                    self._fname.append(file_id)
+                    self._fid[file_id] = k
+        return k
+
+    def key(self, pid) -> int:
+        if not 0 <= pid.page_index < (1 << self.INDEX_BITS):
+            raise ValueError(f"page index {pid.page_index} does not fit an HBM page key")
+        return (self.file_key(pid.file_id) << self.INDEX_BITS) | pid.page_index
+
+    def pid_of(self, key: int):
+        return PageId(self._fname[key >> self.INDEX_BITS], key & ((1 << self.INDEX_BITS) - 1))
+
+    def _stream(self) -> int:
+        if not self.use_device:
+            return 0
+        import torch
+        return int(torch.cuda.current_stream(self.device).cuda_stream)
 
     def put(self, pid, data) -> None:
-        import numpy as np
-        import torch
-        if pid in self.slot_of:
-            self.delete(pid)
-        s = self.free.pop()
-        n = len(data)
-        src = torch.from_numpy(np.frombuffer(bytes(data), dtype=np.uint8)) if not isinstance(data, torch.Tensor) else data
-        self.arena[s * self.page_size:s * self.page_size + n].copy_(src)
-        self.slot_of[pid] = s
-        self.len_of[pid] = n
+        k = self.key(pid)
+        if hasattr(data, "data_ptr"):
+            import torch
+            t = data.contiguous().view(-1).view(torch.uint8)
+            if t.is_cuda and self.use_device:
+                evicted = self.cache.put(k, t.data_ptr(), t.numel(), 1, self._stream(), True)
+            else:
+                evicted = self.cache.put_bytes(k, t.cpu().numpy(), True)
+        else:
+            evicted = self.cache.put_bytes(k, data, True)
+        if self.on_evict is not None:
+            for e in evicted:
+                self.on_evict(self.pid_of(e))
 
     def ptr(self, pid, offset):
-        s = self.slot_of.get(pid)
-        return None if s is None else self.arena.data_ptr() + s * self.page_size + offset
+        slot, _ = self.cache.lookup(self.key(pid))
+        return None if slot < 0 else self.cache.slot_ptr(slot) + offset
 
     def get(self, pid, offset, length):
-        s = self.slot_of.get(pid)
-        if s is None:
+        k = self.key(pid)
+        slot, n = self.cache.lookup(k)
+        if slot < 0:
             return None
-        base = s * self.page_size + offset
-        return self.arena[base:base + length].cpu().numpy().tobytes()
+        if offset >= n:
+            return b""
+        return self.cache.get_bytes(k, offset, min(length, n - offset))
 
     def delete(self, pid) -> None:
-        s = self.slot_of.pop(pid, None)
-        if s is not None:
-            self.len_of.pop(pid, None)
-            self.free.append(s)
+        self.cache.erase(self.key(pid))
 
     def restore(self):
         return []
+
+    def gather(self, file_id, page_indices, out):
+        """Fused lookup + copy of whole pages ``page_indices`` (integer tensor; on the GPU for a
+        device store) of ``file_id`` into the rows of ``out`` (uint8 ``[n, >= page_size]``, where
+        the store lives).  One kernel launch, no host sync.  Returns int32 tensors ``(slots,
+        lens)``; slot -1 / len 0 marks a miss (that row is left untouched)."""
+        import torch
+        keys = (page_indices.reshape(-1).to(torch.int64) | (self.file_key(file_id) << self.INDEX_BITS)).contiguous()
+        n = keys.numel()
+        if out.dim() != 2 or out.dtype != torch.uint8 or out.stride(1) != 1 or out.shape[0] < n \
+                or out.shape[1] < self.page_size:
+            raise ValueError("out must be a uint8 [n, >= page_size] tensor with contiguous rows")
+        if keys.is_cuda != self.use_device or out.is_cuda != self.use_device:
+            raise ValueError("page indices and out must live where the page store does")
+        slots = torch.empty(n, dtype=torch.int32, device=keys.device)
+        lens = torch.empty_like(slots)
+        if n:
+            self.cache.gather(keys.data_ptr(), n, out.data_ptr(), out.stride(0), slots.data_ptr(),
+                              lens.data_ptr(), self._stream())
+        return slots, lens
 
 
 # ---- manager ----------------------------------------------------------------------------------
@@ -265,6 +333,8 @@ class LocalCacheManager:
         self._meta_lock = threading.RLock()
         self._page_locks = [threading.RLock() for _ in range(self.LOCKS)]
         self.metrics = msys.metrics("Client")
+        if hasattr(self.store, "on_evict"):
+            self.store.on_evict = self._on_store_evict
         for pid, n in self.store.restore():
             if self.bytes + n > self.capacity:
                 self.store.delete(pid)
@@ -329,6 +399,23 @@ class LocalCacheManager:
             had = pid in self.meta
             self._delete_locked(pid)
             return had
+
+    def _on_store_evict(self, pid) -> None:
+        """The store dropped ``pid`` by itself (HBM slot pressure): forget it here too."""
+        with self._meta_lock:
+            n = self.meta.pop(pid, None)
+            if n is None:
+                return
+            self.bytes -= n
+            self.evictor.update_on_delete(pid)
+        self.metrics.counter("ClientCachePagesEvicted").inc()
+
+    def gather(self, file_id, page_indices, out):
+        """Batched page read from the HBM store: one fused hash-lookup + copy launch for pages
+        whose indices may be computed on the GPU (see :meth:`HbmPageStore.gather`)."""
+        if not hasattr(self.store, "gather"):
+            raise ValueError("batched page gather needs the HBM page store")
+        return self.store.gather(file_id, page_indices, out)
 
     def has(self, pid) -> bool:
         with self._meta_lock:
@@ -451,6 +538,30 @@ class LocalCacheFileInStream(io.RawIOBase):
             lib().batched_copy(segs, int(torch.cuda.current_stream().cuda_stream), True)
         self.pos += n
         return n
+
+    def read_pages(self, page_indices, out, fill_misses: bool = True):
+        """Read whole pages ``page_indices`` (integer tensor, e.g. drawn by a sampler on the GPU)
+        into the rows of ``out`` with one fused hash-lookup + gather launch on the HBM page store.
+        With ``fill_misses`` (one host sync) pages that missed are read through the external
+        stream, cached and gathered again; without it the call never waits and misses keep
+        length 0.  Returns the valid bytes of every row (int32 tensor)."""
+        import torch
+        slots, lens = self.cache.gather(self.file_id, page_indices, out)
+        if not fill_misses:
+            return lens
+        miss = (slots < 0).nonzero().flatten()
+        if miss.numel() == 0:
+            return lens
+        idx = page_indices.reshape(-1).to(torch.int64)[miss]
+        ps = self.cache.page_size
+        for p in sorted(set(idx.cpu().tolist())):
+            if 0 <= p and p * ps < self.length:
+                self._page(p, 0, 0)
+        tmp = torch.zeros((idx.numel(), ps), dtype=torch.uint8, device=out.device)
+        _, got = self.cache.gather(self.file_id, idx, tmp)
+        out[miss, :ps] = tmp
+        lens[miss] = got
+        return lens
 
     def seek(self, pos: int, whence: int = 0) -> int:
         self.pos = {0: pos, 1: self.pos + pos, 2: self.length + pos}[whence]

@@ -121,8 +121,11 @@ py::tuple evict_select_device(const std::vector<float>& crf, const std::vector<u
 
 }  // namespace
 
+#include "page_cache_bind.h"
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native worker data plane: HBM page store + CDNA4 kernels";
+  bind_page_cache(m);
 
   static py::exception<StoreError> store_error(m, "StoreError");
   py::register_exception_translator([](std::exception_ptr p) {

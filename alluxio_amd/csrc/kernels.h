@@ -104,6 +104,45 @@ hipError_t launch_evict_select(const EvictInput& in, uint32_t* keys_scratch,
                                uint32_t* out_slots, uint32_t* out_count, uint64_t* out_bytes,
                                hipStream_t stream);
 
+// K9: client page cache lookup.  Open-addressing (linear probing) table of page keys in HBM;
+// `key` = (interned file id << 24) | page index, so keys are exact (no hash collisions to
+// verify).  Empty slots hold kPageKeyEmpty, erased ones kPageKeyTomb (probing continues).
+struct PageTableEntry {
+  uint64_t key;
+  int32_t slot;    // arena slot of the page
+  uint32_t len;    // valid bytes in the page
+};
+constexpr uint64_t kPageKeyEmpty = ~0ull;
+constexpr uint64_t kPageKeyTomb = ~0ull - 1;
+__host__ __device__ inline uint64_t page_key_hash(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+// Fused lookup + gather of `n` pages whose keys live in device memory: request i copies the
+// valid bytes of page keys[i] from arena slot to dst + i*dst_stride, writes slot_out[i] (-1 on a
+// miss) and len_out[i], and stamps[slot] = epoch on a hit (device-side LRU recency).  One wave
+// probes 64 table entries per step with a ballot; `chunk_bytes` splits big pages over gridDim.y.
+struct PageGatherArgs {
+  const PageTableEntry* table;
+  uint64_t mask;           // table size - 1 (power of two)
+  const uint64_t* keys;
+  uint32_t n;
+  const uint8_t* arena;
+  uint64_t page_size;
+  uint8_t* dst;
+  uint64_t dst_stride;
+  int32_t* slot_out;
+  uint32_t* len_out;
+  uint32_t* stamps;
+  uint32_t epoch;
+};
+hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream);
+// Apply table updates (idx, entry) pairs uploaded by the host mirror.
+hipError_t launch_page_table_update(PageTableEntry* table, const uint64_t* idx,
+                                    const PageTableEntry* entries, uint32_t n, hipStream_t stream);
+
 // Fill `bytes` at dst with 64-bit words w[i] = splitmix64(seed ^ ((i + word_offset) * K)):
 // synthetic bench/test data that is a pure function of the byte offset inside a block.
 hipError_t launch_fill_pattern(uint8_t* dst, uint64_t bytes, uint64_t seed, uint64_t word_offset,

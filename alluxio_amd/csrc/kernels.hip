@@ -1180,4 +1180,91 @@ hipError_t launch_fill_pattern(uint8_t* dst, uint64_t bytes, uint64_t seed, uint
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// K9: client page cache -- fused device hash lookup + page gather.
+//
+// Grid (x = request, y = chunk of the page).  Wave 0 of each workgroup resolves the key: every
+// lane loads one of 64 consecutive table entries (16 B each, one coalesced 1 KiB read), a ballot
+// finds the first matching key and the first empty entry; a match before the first empty entry
+// is a hit (linear probing never places a key past an empty slot; tombstones keep probing).  The
+// slot is broadcast through LDS and the 256 lanes copy this workgroup's chunk with 16-B vectors.
+// ---------------------------------------------------------------------------------------------
+constexpr int kPgThreads = 256;
+constexpr uint64_t kPgChunk = 128 * 1024;
+
+__global__ __launch_bounds__(kPgThreads) void page_lookup_gather_kernel(PageGatherArgs a) {
+  __shared__ int32_t s_slot;
+  __shared__ uint32_t s_len;
+  const int tid = threadIdx.x;
+  const uint64_t chunk0 = (uint64_t)blockIdx.y * kPgChunk;
+  for (uint32_t req = blockIdx.x; req < a.n; req += gridDim.x) {
+    if (tid < 64) {
+      const uint64_t key = a.keys[req];
+      const uint64_t h = page_key_hash(key);
+      int32_t slot = -1;
+      uint32_t len = 0;
+      for (uint64_t probe = 0; probe <= a.mask; probe += 64) {
+        const PageTableEntry e = a.table[(h + probe + tid) & a.mask];
+        const uint64_t hit = __ballot(e.key == key);
+        const uint64_t empty = __ballot(e.key == kPageKeyEmpty);
+        if (hit) {
+          const int first_hit = __ffsll((unsigned long long)hit) - 1;
+          const int first_empty = empty ? __ffsll((unsigned long long)empty) - 1 : 64;
+          if (first_hit < first_empty) {
+            slot = __shfl(e.slot, first_hit, 64);
+            len = __shfl(e.len, first_hit, 64);
+          }
+          break;
+        }
+        if (empty) break;
+      }
+      if (tid == 0) {
+        s_slot = slot;
+        s_len = len;
+      }
+    }
+    __syncthreads();
+    const int32_t slot = s_slot;
+    const uint64_t len = s_len;
+    if (blockIdx.y == 0 && tid == 0) {
+      a.slot_out[req] = slot;
+      a.len_out[req] = slot >= 0 ? (uint32_t)len : 0u;
+      if (slot >= 0 && a.stamps) a.stamps[slot] = a.epoch;
+    }
+    if (slot >= 0 && chunk0 < len) {
+      const uint64_t rem = len - chunk0;
+      const uint64_t n = rem < kPgChunk ? rem : kPgChunk;
+      const uint64_t src = (uint64_t)(a.arena + (uint64_t)slot * a.page_size + chunk0);
+      const uint64_t dst = (uint64_t)(a.dst + (uint64_t)req * a.dst_stride + chunk0);
+      copy_range<4, 0, 0>(src, dst, n, tid);
+    }
+    __syncthreads();      // s_slot is rewritten by the next request of this workgroup
+  }
+}
+
+hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream) {
+  if (a.n == 0) return hipSuccess;
+  if ((a.mask & (a.mask + 1)) != 0) return hipErrorInvalidValue;
+  const unsigned gy = (unsigned)std::max<uint64_t>(1, (a.page_size + kPgChunk - 1) / kPgChunk);
+  const unsigned gx = (unsigned)std::min<uint64_t>(a.n, 65535);
+  hipLaunchKernelGGL(page_lookup_gather_kernel, dim3(gx, gy), dim3(kPgThreads), 0, stream, a);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void page_table_update_kernel(PageTableEntry* __restrict__ table,
+                                                                const uint64_t* __restrict__ idx,
+                                                                const PageTableEntry* __restrict__ e,
+                                                                uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    table[idx[i]] = e[i];
+}
+
+hipError_t launch_page_table_update(PageTableEntry* table, const uint64_t* idx,
+                                    const PageTableEntry* entries, uint32_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const unsigned grid = std::min<unsigned>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(page_table_update_kernel, dim3(grid), dim3(256), 0, stream, table, idx, entries, n);
+  return hipGetLastError();
+}
+
 }  // namespace amdx

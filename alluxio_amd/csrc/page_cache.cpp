@@ -1,0 +1,368 @@
+// HBM client page cache with a device hash table (see page_cache.h).
+#include "page_cache.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "block_store.h"   // StoreError, MemKind, error codes
+
+namespace amdx {
+
+#define PC_HIP_OK(expr)                                                                       \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      throw StoreError(kErrHip, std::string("HIP error: ") + hipGetErrorString(_e) + " at " + #expr); \
+  } while (0)
+
+static uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 64;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+DevicePageCache::DevicePageCache(int device, uint64_t capacity_bytes, uint64_t page_size, bool use_device)
+    : device_(device), use_device_(use_device), page_size_(page_size) {
+  if (page_size == 0 || page_size % 16 != 0)
+    throw StoreError(kErrInvalidArgument, "page size must be a positive multiple of 16");
+  const uint64_t n = capacity_bytes / page_size;
+  if (n == 0 || n > (1u << 30)) throw StoreError(kErrInvalidArgument, "cache must hold 1..2^30 pages");
+  nslots_ = (uint32_t)n;
+  table_h_.assign(next_pow2(2 * n), PageTableEntry{kPageKeyEmpty, -1, 0});
+  dirty_flag_.assign(table_h_.size(), 0);
+  slot_key_.assign(nslots_, kPageKeyEmpty);
+  stamp_h_.assign(nslots_, 0);
+  free_.reserve(nslots_);
+  for (uint32_t s = nslots_; s-- > 0;) free_.push_back(s);
+  if (use_device_) {
+    PC_HIP_OK(hipSetDevice(device_));
+    void* p = nullptr;
+    PC_HIP_OK(hipMalloc(&p, nslots_ * page_size_));
+    arena_ = (uint64_t)p;
+    PC_HIP_OK(hipMalloc((void**)&table_d_, table_h_.size() * sizeof(PageTableEntry)));
+    PC_HIP_OK(hipMalloc((void**)&stamps_d_, nslots_ * sizeof(uint32_t)));
+    PC_HIP_OK(hipMemset(stamps_d_, 0, nslots_ * sizeof(uint32_t)));
+    PC_HIP_OK(hipEventCreateWithFlags(&last_gather_, hipEventDisableTiming));
+  } else {
+    void* p = std::aligned_alloc(64, ((nslots_ * page_size_ + 63) / 64) * 64);
+    if (!p) throw StoreError(kErrOutOfSpace, "host page cache arena allocation failed");
+    arena_ = (uint64_t)p;
+  }
+  full_upload_ = true;
+}
+
+DevicePageCache::~DevicePageCache() {
+  if (use_device_) {
+    hipSetDevice(device_);
+    if (gather_pending_) hipEventSynchronize(last_gather_);
+    hipFree((void*)arena_);
+    hipFree(table_d_);
+    hipFree(stamps_d_);
+    hipFree(upd_idx_d_);
+    hipFree(upd_ent_d_);
+    hipFree(keys_d_);
+    hipFree(slots_d_);
+    hipFree(lens_d_);
+    if (last_gather_) hipEventDestroy(last_gather_);
+  } else {
+    std::free((void*)arena_);
+  }
+}
+
+// ---- host mirror -----------------------------------------------------------------------------
+int64_t DevicePageCache::find_index(uint64_t key) const {
+  const uint64_t mask = table_h_.size() - 1;
+  uint64_t i = page_key_hash(key) & mask;
+  for (uint64_t probe = 0; probe <= mask; ++probe, i = (i + 1) & mask) {
+    const uint64_t k = table_h_[i].key;
+    if (k == key) return (int64_t)i;
+    if (k == kPageKeyEmpty) return -1;
+  }
+  return -1;
+}
+
+void DevicePageCache::mark_dirty(uint64_t idx) {
+  if (!use_device_ || full_upload_) return;
+  if (!dirty_flag_[idx]) {
+    dirty_flag_[idx] = 1;
+    dirty_.push_back(idx);
+    if (dirty_.size() > table_h_.size() / 8) full_upload_ = true;   // cheaper as one copy
+  }
+}
+
+void DevicePageCache::table_insert(uint64_t key, int32_t slot, uint32_t len) {
+  const uint64_t mask = table_h_.size() - 1;
+  uint64_t i = page_key_hash(key) & mask;
+  int64_t tomb = -1;
+  for (uint64_t probe = 0; probe <= mask; ++probe, i = (i + 1) & mask) {
+    const uint64_t k = table_h_[i].key;
+    if (k == key) {                   // overwrite in place
+      table_h_[i].slot = slot;
+      table_h_[i].len = len;
+      mark_dirty(i);
+      return;
+    }
+    if (k == kPageKeyTomb && tomb < 0) tomb = (int64_t)i;
+    if (k == kPageKeyEmpty) break;
+  }
+  const uint64_t at = tomb >= 0 ? (uint64_t)tomb : i;
+  if (tomb >= 0) --tombstones_;
+  table_h_[at] = PageTableEntry{key, slot, len};
+  mark_dirty(at);
+}
+
+void DevicePageCache::table_erase_at(uint64_t idx) {
+  table_h_[idx] = PageTableEntry{kPageKeyTomb, -1, 0};
+  ++tombstones_;
+  mark_dirty(idx);
+  if (tombstones_ > table_h_.size() / 4) rebuild_table();
+}
+
+void DevicePageCache::rebuild_table() {
+  std::vector<PageTableEntry> old;
+  old.swap(table_h_);
+  table_h_.assign(old.size(), PageTableEntry{kPageKeyEmpty, -1, 0});
+  tombstones_ = 0;
+  const bool saved = full_upload_;
+  full_upload_ = true;               // everything moves: one full upload
+  for (const auto& e : old)
+    if (e.key != kPageKeyEmpty && e.key != kPageKeyTomb) table_insert(e.key, e.slot, e.len);
+  (void)saved;
+  dirty_.clear();
+  std::fill(dirty_flag_.begin(), dirty_flag_.end(), 0);
+}
+
+void DevicePageCache::flush_table(hipStream_t stream) {
+  if (!use_device_) return;
+  if (full_upload_) {
+    PC_HIP_OK(hipMemcpyAsync(table_d_, table_h_.data(), table_h_.size() * sizeof(PageTableEntry),
+                             hipMemcpyHostToDevice, stream));
+    PC_HIP_OK(hipStreamSynchronize(stream));   // the host mirror may change right after
+    full_upload_ = false;
+    for (uint64_t i : dirty_) dirty_flag_[i] = 0;
+    dirty_.clear();
+    return;
+  }
+  if (dirty_.empty()) return;
+  const uint32_t n = (uint32_t)dirty_.size();
+  if (n > upd_cap_) {
+    hipFree(upd_idx_d_);
+    hipFree(upd_ent_d_);
+    upd_cap_ = std::max<uint32_t>(n, 1024);
+    PC_HIP_OK(hipMalloc((void**)&upd_idx_d_, upd_cap_ * sizeof(uint64_t)));
+    PC_HIP_OK(hipMalloc((void**)&upd_ent_d_, upd_cap_ * sizeof(PageTableEntry)));
+  }
+  std::vector<PageTableEntry> ents(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    ents[i] = table_h_[dirty_[i]];
+    dirty_flag_[dirty_[i]] = 0;
+  }
+  PC_HIP_OK(hipMemcpyAsync(upd_idx_d_, dirty_.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+  PC_HIP_OK(hipMemcpyAsync(upd_ent_d_, ents.data(), n * sizeof(PageTableEntry), hipMemcpyHostToDevice, stream));
+  PC_HIP_OK(launch_page_table_update(table_d_, upd_idx_d_, upd_ent_d_, n, stream));
+  PC_HIP_OK(hipStreamSynchronize(stream));     // pageable sources: keep them alive until copied
+  dirty_.clear();
+}
+
+// ---- recency / eviction ---------------------------------------------------------------------
+void DevicePageCache::sync_device_stamps() {
+  if (!use_device_ || !device_stamps_dirty_) return;
+  std::vector<uint32_t> dev(nslots_);
+  wait_gathers();
+  PC_HIP_OK(hipMemcpy(dev.data(), stamps_d_, nslots_ * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  for (uint32_t s = 0; s < nslots_; ++s) stamp_h_[s] = std::max(stamp_h_[s], dev[s]);
+  device_stamps_dirty_ = false;
+}
+
+std::vector<uint64_t> DevicePageCache::evict_lru(uint32_t need) {
+  sync_device_stamps();
+  std::vector<uint32_t> used;
+  used.reserve(nslots_ - free_.size());
+  for (uint32_t s = 0; s < nslots_; ++s)
+    if (slot_key_[s] != kPageKeyEmpty) used.push_back(s);
+  need = std::min<uint32_t>(need, (uint32_t)used.size());
+  std::nth_element(used.begin(), used.begin() + need, used.end(),
+                   [&](uint32_t a, uint32_t b) { return stamp_h_[a] < stamp_h_[b]; });
+  std::vector<uint64_t> out;
+  for (uint32_t i = 0; i < need; ++i) {
+    const uint32_t s = used[i];
+    const uint64_t k = slot_key_[s];
+    const int64_t idx = find_index(k);
+    if (idx >= 0) table_erase_at((uint64_t)idx);
+    slot_key_[s] = kPageKeyEmpty;
+    free_.push_back(s);
+    out.push_back(k);
+  }
+  return out;
+}
+
+void DevicePageCache::wait_gathers() {
+  if (use_device_ && gather_pending_) {
+    PC_HIP_OK(hipEventSynchronize(last_gather_));
+    gather_pending_ = false;
+  }
+}
+
+// ---- public API -------------------------------------------------------------------------------
+std::vector<uint64_t> DevicePageCache::put(uint64_t key, uint64_t src, uint64_t len, int src_kind, uint64_t stream,
+                                           bool evict) {
+  if (key == kPageKeyEmpty || key == kPageKeyTomb) throw StoreError(kErrInvalidArgument, "reserved page key");
+  if (len > page_size_) throw StoreError(kErrInvalidArgument, "page larger than the page size");
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<uint64_t> evicted;
+  int32_t slot;
+  const int64_t idx = find_index(key);
+  if (idx >= 0) {
+    slot = table_h_[idx].slot;
+  } else {
+    if (free_.empty()) {
+      if (!evict) throw StoreError(kErrOutOfSpace, "page cache is full");
+      evicted = evict_lru(std::max<uint32_t>(1, nslots_ / 64));   // evict in batches
+    }
+    slot = (int32_t)free_.back();
+    free_.pop_back();
+  }
+  // a queued gather may still read this slot's previous page (overwritten, evicted or erased
+  // and reused): let queued gathers finish before the slot is rewritten
+  wait_gathers();
+  const uint64_t dst = arena_ + (uint64_t)slot * page_size_;
+  if (len) {
+    if (use_device_) {
+      const hipMemcpyKind kind = src_kind == (int)MemKind::kDevice ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+      PC_HIP_OK(hipMemcpyAsync((void*)dst, (const void*)src, len, kind, (hipStream_t)stream));
+      PC_HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+    } else {
+      std::memcpy((void*)dst, (const void*)src, len);
+    }
+  }
+  slot_key_[slot] = key;
+  stamp_h_[slot] = ++epoch_;
+  table_insert(key, slot, (uint32_t)len);
+  return evicted;
+}
+
+bool DevicePageCache::erase(uint64_t key) {
+  std::lock_guard<std::mutex> g(mu_);
+  const int64_t idx = find_index(key);
+  if (idx < 0) return false;
+  const int32_t slot = table_h_[idx].slot;
+  table_erase_at((uint64_t)idx);
+  slot_key_[slot] = kPageKeyEmpty;
+  free_.push_back((uint32_t)slot);
+  return true;
+}
+
+bool DevicePageCache::contains(uint64_t key) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return find_index(key) >= 0;
+}
+
+std::pair<int32_t, uint32_t> DevicePageCache::lookup(uint64_t key) {
+  std::lock_guard<std::mutex> g(mu_);
+  const int64_t idx = find_index(key);
+  if (idx < 0) return {-1, 0};
+  const auto& e = table_h_[idx];
+  stamp_h_[e.slot] = ++epoch_;
+  return {e.slot, e.len};
+}
+
+bool DevicePageCache::read(uint64_t key, uint64_t offset, uint64_t len, uint64_t dst, int dst_kind,
+                           uint64_t stream) {
+  std::lock_guard<std::mutex> g(mu_);
+  const int64_t idx = find_index(key);
+  if (idx < 0) return false;
+  const auto& e = table_h_[idx];
+  if (offset + len > e.len) throw StoreError(kErrInvalidArgument, "read past the end of the page");
+  stamp_h_[e.slot] = ++epoch_;
+  const uint64_t src = arena_ + (uint64_t)e.slot * page_size_ + offset;
+  if (len == 0) return true;
+  if (use_device_) {
+    const hipMemcpyKind kind = dst_kind == (int)MemKind::kDevice ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    PC_HIP_OK(hipMemcpyAsync((void*)dst, (const void*)src, len, kind, (hipStream_t)stream));
+    PC_HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  } else {
+    std::memcpy((void*)dst, (const void*)src, len);
+  }
+  return true;
+}
+
+void DevicePageCache::gather(uint64_t keys, uint32_t n, uint64_t dst, uint64_t dst_stride, uint64_t slot_out,
+                             uint64_t len_out, uint64_t stream) {
+  if (n == 0) return;
+  if (dst_stride < page_size_ && n > 1) throw StoreError(kErrInvalidArgument, "dst stride below the page size");
+  std::lock_guard<std::mutex> g(mu_);
+  const uint32_t epoch = ++epoch_;
+  if (!use_device_) {
+    const uint64_t* k = (const uint64_t*)keys;
+    int32_t* so = (int32_t*)slot_out;
+    uint32_t* lo = (uint32_t*)len_out;
+    for (uint32_t i = 0; i < n; ++i) {
+      const int64_t idx = find_index(k[i]);
+      if (idx < 0) {
+        so[i] = -1;
+        lo[i] = 0;
+        continue;
+      }
+      const auto& e = table_h_[idx];
+      so[i] = e.slot;
+      lo[i] = e.len;
+      stamp_h_[e.slot] = epoch;
+      std::memcpy((void*)(dst + (uint64_t)i * dst_stride), (const void*)(arena_ + (uint64_t)e.slot * page_size_), e.len);
+    }
+    return;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  flush_table(s);
+  PageGatherArgs a{table_d_, table_h_.size() - 1, (const uint64_t*)keys, n, (const uint8_t*)arena_, page_size_,
+                   (uint8_t*)dst, dst_stride, (int32_t*)slot_out, (uint32_t*)len_out, stamps_d_, epoch};
+  PC_HIP_OK(launch_page_lookup_gather(a, s));
+  PC_HIP_OK(hipEventRecord(last_gather_, s));
+  gather_pending_ = true;
+  device_stamps_dirty_ = true;
+}
+
+std::vector<int32_t> DevicePageCache::gather_host_keys(const std::vector<uint64_t>& keys, uint64_t dst,
+                                                       uint64_t dst_stride, uint64_t stream) {
+  const uint32_t n = (uint32_t)keys.size();
+  std::vector<int32_t> slots(n, -1);
+  if (n == 0) return slots;
+  if (!use_device_) {
+    std::vector<uint32_t> lens(n);
+    gather((uint64_t)keys.data(), n, dst, dst_stride, (uint64_t)slots.data(), (uint64_t)lens.data(), stream);
+    return slots;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (n > keys_cap_) {
+      wait_gathers();
+      hipFree(keys_d_);
+      hipFree(slots_d_);
+      hipFree(lens_d_);
+      keys_cap_ = std::max<uint32_t>(n, 4096);
+      PC_HIP_OK(hipMalloc((void**)&keys_d_, keys_cap_ * sizeof(uint64_t)));
+      PC_HIP_OK(hipMalloc((void**)&slots_d_, keys_cap_ * sizeof(int32_t)));
+      PC_HIP_OK(hipMalloc((void**)&lens_d_, keys_cap_ * sizeof(uint32_t)));
+    }
+    PC_HIP_OK(hipMemcpyAsync(keys_d_, keys.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  }
+  gather((uint64_t)keys_d_, n, dst, dst_stride, (uint64_t)slots_d_, (uint64_t)lens_d_, stream);
+  PC_HIP_OK(hipMemcpyAsync(slots.data(), slots_d_, n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  PC_HIP_OK(hipStreamSynchronize(s));
+  return slots;
+}
+
+void DevicePageCache::clear() {
+  std::lock_guard<std::mutex> g(mu_);
+  wait_gathers();
+  std::fill(table_h_.begin(), table_h_.end(), PageTableEntry{kPageKeyEmpty, -1, 0});
+  tombstones_ = 0;
+  std::fill(slot_key_.begin(), slot_key_.end(), kPageKeyEmpty);
+  free_.clear();
+  for (uint32_t s = nslots_; s-- > 0;) free_.push_back(s);
+  dirty_.clear();
+  std::fill(dirty_flag_.begin(), dirty_flag_.end(), 0);
+  full_upload_ = true;
+}
+
+}  // namespace amdx

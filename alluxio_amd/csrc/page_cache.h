@@ -1,0 +1,100 @@
+// K9: HBM-resident client page cache with a device hash table (LocalCacheManager's page store on
+// MI355X).  Reference: core/client/fs/src/main/java/alluxio/client/file/cache/LocalCacheManager.java
+// (put :249-347 two-phase evict + put, get :360), store/LocalPageStore.java, evictor/LRUCacheEvictor.java.
+//
+// Pages live in fixed slots of one device arena.  The key -> slot index is an open-addressing
+// table kept twice: an authoritative host mirror (puts, erases, host lookups) and a device copy
+// that the fused lookup+gather kernel probes, so a batch of page keys produced ON the GPU (a
+// device-side sampler/shuffle) is served by one launch with no host round trip.  Dirty table
+// entries are pushed to the device before every gather on the gather's stream.  Recency: host
+// gets bump a host stamp, device gathers write stamps[slot] = epoch; eviction folds both.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "kernels.h"
+
+namespace amdx {
+
+class DevicePageCache {
+ public:
+  // use_device=false keeps the arena and table in host memory (CPU builds and tests): every
+  // operation has the same semantics, the gather runs the same probe on the CPU.
+  DevicePageCache(int device, uint64_t capacity_bytes, uint64_t page_size, bool use_device);
+  ~DevicePageCache();
+  DevicePageCache(const DevicePageCache&) = delete;
+  DevicePageCache& operator=(const DevicePageCache&) = delete;
+
+  // Store `len` bytes from `src` (MemKind) as page `key`.  When every slot is taken and `evict`
+  // is set, least-recently-used pages are dropped first (returned); otherwise full -> throws.
+  std::vector<uint64_t> put(uint64_t key, uint64_t src, uint64_t len, int src_kind, uint64_t stream, bool evict);
+  bool erase(uint64_t key);
+  bool contains(uint64_t key) const;
+  // (slot, len) or (-1, 0); bumps recency.
+  std::pair<int32_t, uint32_t> lookup(uint64_t key);
+  uint64_t slot_ptr(int32_t slot) const { return arena_ + (uint64_t)slot * page_size_; }
+  // Copy `len` bytes at `offset` of page `key` to dst (MemKind); false on a miss.
+  bool read(uint64_t key, uint64_t offset, uint64_t len, uint64_t dst, int dst_kind, uint64_t stream);
+
+  // Fused lookup + gather: keys/slot_out/len_out are device (or, host mode, host) arrays.
+  void gather(uint64_t keys, uint32_t n, uint64_t dst, uint64_t dst_stride, uint64_t slot_out,
+              uint64_t len_out, uint64_t stream);
+  // Host keys: uploaded, gathered, slots returned (-1 = miss).
+  std::vector<int32_t> gather_host_keys(const std::vector<uint64_t>& keys, uint64_t dst, uint64_t dst_stride,
+                                        uint64_t stream);
+
+  uint64_t page_size() const { return page_size_; }
+  uint32_t slots() const { return nslots_; }
+  uint32_t used() const { return (uint32_t)(nslots_ - free_.size()); }
+  uint64_t table_size() const { return table_h_.size(); }
+  uint64_t arena() const { return arena_; }
+  bool on_device() const { return use_device_; }
+  void clear();
+
+ private:
+  int64_t find_index(uint64_t key) const;       // table index or -1
+  void table_insert(uint64_t key, int32_t slot, uint32_t len);
+  void table_erase_at(uint64_t idx);
+  void mark_dirty(uint64_t idx);
+  void flush_table(hipStream_t stream);         // push dirty entries to the device copy
+  void rebuild_table();                          // drop tombstones
+  std::vector<uint64_t> evict_lru(uint32_t need);
+  void sync_device_stamps();
+  void wait_gathers();
+
+  int device_;
+  bool use_device_;
+  uint64_t page_size_;
+  uint32_t nslots_;
+  uint64_t arena_ = 0;                           // device or host address
+  std::vector<PageTableEntry> table_h_;          // host mirror (authoritative)
+  PageTableEntry* table_d_ = nullptr;            // device copy
+  uint64_t tombstones_ = 0;
+  std::vector<uint64_t> dirty_;
+  std::vector<uint8_t> dirty_flag_;
+  bool full_upload_ = true;
+  std::vector<uint32_t> free_;
+  std::vector<uint64_t> slot_key_;               // slot -> key (kPageKeyEmpty if free)
+  std::vector<uint32_t> stamp_h_;                // host-side recency stamps per slot
+  uint32_t* stamps_d_ = nullptr;                 // device-side recency stamps per slot
+  uint32_t epoch_ = 1;
+  bool device_stamps_dirty_ = false;
+  // scratch for uploads (pinned when on the device)
+  uint64_t* upd_idx_d_ = nullptr;
+  PageTableEntry* upd_ent_d_ = nullptr;
+  uint32_t upd_cap_ = 0;
+  uint64_t* keys_d_ = nullptr;
+  int32_t* slots_d_ = nullptr;
+  uint32_t* lens_d_ = nullptr;
+  uint32_t keys_cap_ = 0;
+  hipEvent_t last_gather_ = nullptr;
+  bool gather_pending_ = false;
+  mutable std::mutex mu_;
+};
+
+}  // namespace amdx

@@ -106,3 +106,43 @@ def test_local_page_store_options_mismatch_discards(tmp_path):
     opts.write_bytes(pb.client_cache.PPageStoreCommonOptions(pageSize=4096, alluxioVersion="0.0.0-old")
                      .SerializeToString())
     assert LocalPageStore(str(tmp_path), 4096, 4, 1 << 20).restore() == []   # other version: wiped
+
+
+def test_hbm_store_host_mode_slot_pressure(tmp_path):
+    """HBM store on the native page table (host mode here): short pages use up the slots before
+    the byte budget; the store's own LRU evictions reach the manager's metastore."""
+    import torch
+    from alluxio_amd.client.cache import HbmPageStore
+    m = LocalCacheManager(_conf(tmp_path), store=HbmPageStore(16384, 4096, use_device=False))
+    for i in range(6):
+        assert m.put(PageId("f", i), bytes([i]) * 100)
+    assert len(m.meta) == 4 == m.store.cache.used and m.bytes == 400
+    assert not m.has(PageId("f", 0)) and not m.has(PageId("f", 1)) and m.has(PageId("f", 5))
+    assert m.get(PageId("f", 5), 10, 20) == bytes([5]) * 20
+    out = torch.zeros((3, 4096), dtype=torch.uint8)
+    slots, lens = m.gather("f", torch.tensor([5, 0, 3]), out)
+    assert slots.tolist()[1] == -1 and lens.tolist() == [100, 0, 100]
+    assert bytes(out[0, :100].numpy()) == bytes([5]) * 100 and bytes(out[2, :100].numpy()) == bytes([3]) * 100
+
+
+def test_read_pages_through_filesystem(tmp_path):
+    import torch
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"}) as c:
+        data = np.random.default_rng(3).integers(0, 256, 10 * 4096 + 77, dtype=np.uint8)
+        c.client().write_file("/rp/f", data, write_type="MUST_CACHE")
+        from alluxio_amd.client.file_system import FileSystem
+        fs = FileSystem(conf=_conf(tmp_path, **{"alluxio.user.client.cache.store.type": "HBM",
+                                                "alluxio.user.client.cache.size": "1MB"}),
+                        master_address=c.master.address)
+        dev = fs.local_cache.store.device or torch.device("cpu")
+        pages = [3, 10, 0, 3]
+        out = torch.zeros((4, 4096), dtype=torch.uint8, device=dev)
+        with fs.open_file("/rp/f") as f:
+            lens = f.read_pages(torch.tensor(pages, device=dev), out)            # cold: misses filled
+            lens2 = f.read_pages(torch.tensor(pages, device=dev), out, fill_misses=False)   # warm
+        assert lens.tolist() == lens2.tolist() == [4096, 77, 4096, 4096]
+        host = out.cpu().numpy()
+        for r, p in enumerate(pages):
+            n = int(lens[r])
+            assert np.array_equal(host[r, :n], data[p * 4096:p * 4096 + n])
+        fs.close()

@@ -1,0 +1,110 @@
+"""K9 native HBM client page cache (csrc/page_cache.{h,cpp} + page_lookup_gather_kernel).
+
+Parity: core/client/fs/src/main/java/alluxio/client/file/cache/LocalCacheManager.java:249-347 (put with
+two-phase evict), :360 (get), evictor/LRUCacheEvictor.java.  The host-mode cache (use_device=False) runs
+the same table and eviction logic on the CPU; the GPU tests check the fused device lookup+gather kernel
+against a plain PyTorch gather of the same pages.
+"""
+import numpy as np
+import pytest
+
+from alluxio_amd.ops.native import lib
+
+
+def _key(fid, idx):
+    return (fid << 24) | idx
+
+
+def test_host_put_get_erase_evict():
+    C = lib()
+    pc = C.PageCache(0, 8 * 4096, 4096, False)
+    assert pc.slots == 8 and pc.used == 0
+    pages = {i: np.random.default_rng(i).integers(0, 256, 4096, dtype=np.uint8) for i in range(12)}
+    for i in range(8):
+        assert pc.put_bytes(_key(1, i), pages[i], False) == []
+    assert pc.used == 8
+    with pytest.raises(Exception):
+        pc.put_bytes(_key(1, 8), pages[8], False)          # full, eviction off
+    assert pc.get_bytes(_key(1, 3), 100, 50) == pages[3][100:150].tobytes()
+    assert pc.get_bytes(_key(2, 3), 0, 10) is None
+    # touch 0..6 (host gets bump recency): page 7 is the LRU victim
+    for i in range(7):
+        assert pc.lookup(_key(1, i))[0] >= 0
+    ev = pc.put_bytes(_key(1, 8), pages[8], True)
+    assert ev == [_key(1, 7)] and not pc.contains(_key(1, 7)) and pc.contains(_key(1, 8))
+    assert pc.erase(_key(1, 0)) and not pc.erase(_key(1, 0)) and pc.used == 7
+    # overwrite in place keeps one slot
+    pc.put_bytes(_key(1, 1), pages[11][:100], True)
+    assert pc.lookup(_key(1, 1))[1] == 100 and pc.used == 7
+    pc.clear()
+    assert pc.used == 0 and not pc.contains(_key(1, 1))
+
+
+def test_host_gather_and_tombstone_churn():
+    C = lib()
+    ps = 256
+    pc = C.PageCache(0, 64 * ps, ps, False)
+    rng = np.random.default_rng(7)
+    live = {}
+    for step in range(2000):                   # churn: tombstones force table rebuilds
+        k = _key(int(rng.integers(1, 5)), int(rng.integers(0, 40)))
+        if rng.random() < 0.3 and live:
+            victim = list(live)[int(rng.integers(0, len(live)))]
+            assert pc.erase(victim)
+            del live[victim]
+            continue
+        data = rng.integers(0, 256, int(rng.integers(1, ps + 1)), dtype=np.uint8)
+        for e in pc.put_bytes(k, data, True):
+            live.pop(e, None)
+        live[k] = data
+    assert pc.used == len(live)
+    keys = list(live)[:20] + [_key(99, 1)]
+    dst = np.zeros((len(keys), ps), dtype=np.uint8)
+    slots = pc.gather_host_keys(keys, dst.ctypes.data, ps, 0)
+    assert slots[-1] == -1
+    for i, k in enumerate(keys[:-1]):
+        assert slots[i] >= 0
+        assert np.array_equal(dst[i, :len(live[k])], live[k])
+
+
+@pytest.mark.gpu
+def test_device_gather_matches_torch(gpu):
+    import torch
+    C = lib()
+    ps = 64 << 10
+    n_pages = 96
+    pc = C.PageCache(0, n_pages * ps, ps, True)
+    assert pc.on_device
+    src = torch.randint(0, 256, (n_pages, ps), dtype=torch.uint8, device=gpu)
+    stream = torch.cuda.current_stream().cuda_stream
+    for i in range(n_pages):
+        ln = ps if i % 5 else ps - 4096 * (i % 7 + 1)
+        pc.put(_key(3, i), src[i].data_ptr(), ln, 1, stream, False)
+    torch.cuda.synchronize()
+    # device-generated keys (a sampler on the GPU): pages 0..n-1 shuffled + misses
+    perm = torch.randperm(n_pages + 8, device=gpu)
+    keys = ((torch.full_like(perm, 3) << 24) | perm).to(torch.int64)
+    n = keys.numel()
+    out = torch.zeros((n, ps), dtype=torch.uint8, device=gpu)
+    slot = torch.empty(n, dtype=torch.int32, device=gpu)
+    lens = torch.empty(n, dtype=torch.int32, device=gpu)
+    pc.gather(keys.data_ptr(), n, out.data_ptr(), ps, slot.data_ptr(), lens.data_ptr(), stream)
+    torch.cuda.synchronize()
+    p = perm.cpu()
+    for r in range(n):
+        i = int(p[r])
+        if i >= n_pages:
+            assert int(slot[r]) == -1 and int(lens[r]) == 0
+            continue
+        ln = ps if i % 5 else ps - 4096 * (i % 7 + 1)
+        assert int(lens[r]) == ln
+        assert torch.equal(out[r, :ln], src[i, :ln]), r
+    # evict after device gathers: device stamps take part in the LRU choice
+    hot = perm[:8].cpu().tolist()
+    hot_keys = torch.tensor([(3 << 24) | k for k in hot if k < n_pages], dtype=torch.int64, device=gpu)
+    for _ in range(3):
+        pc.gather(hot_keys.data_ptr(), hot_keys.numel(), out.data_ptr(), ps, slot.data_ptr(), lens.data_ptr(),
+                  stream)
+    ev = pc.put(_key(4, 0), src[0].data_ptr(), ps, 1, stream, True)
+    assert ev and not (set(ev) & set(hot_keys.cpu().tolist()))
+    torch.cuda.synchronize()
