@@ -55,6 +55,10 @@ for s in $STEPS; do
       ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
+    pc)
+      run page_cache_bench 300 python tools/page_cache_bench.py --out "$OUT/page_cache_bench.jsonl"
+      run rocprof_pc 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pc" -o pc --output-format csv -- python3 tools/page_cache_bench.py --page-sizes 4k,64k,2m --iters 5
+      ;;
     ringtune) run ring_tune 600 python tools/ring_tune.py --out "$OUT/ring_tune.json" $RINGTUNE_ARGS ;;
     tune) run copy_tune 600 python tools/copy_tune.py --out "$OUT/copy_tune.json" ;;
   esac
