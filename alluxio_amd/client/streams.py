@@ -413,7 +413,8 @@ class FileInStream(io.RawIOBase):
                                    + (f": {last_err}" if last_err else ""))
 
     def _ipc_enabled(self) -> bool:
-        if not self.ctx.conf.get_bool("alluxio.worker.ipc.enabled", "true"):
+        if not self.ctx.conf.get_bool("alluxio.worker.ipc.enabled", "true") or \
+                not self.ctx.conf.get_bool("alluxio.user.short.circuit.enabled", "true"):
             return False
         from ..ops.native import has_gpu
         return has_gpu()

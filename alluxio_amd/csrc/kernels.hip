@@ -1242,9 +1242,114 @@ __global__ __launch_bounds__(kPgThreads) void page_lookup_gather_kernel(PageGath
   }
 }
 
+// Small pages (<= 64 KiB, 16-B aligned rows): one wave per request and kPgPW requests per wave,
+// no LDS and no barriers.  The wave first issues the keys and the first 64-entry probe window of
+// all kPgPW requests back to back (independent loads in flight together), resolves them with
+// ballots (a chain longer than 64 entries falls back to the loop), then copies the pages with
+// kPgPW x kPgUnr 16-B loads in flight per lane before the stores.
+constexpr uint64_t kPgSmallMax = 64 * 1024;
+constexpr int kPgPW = 4;
+constexpr int kPgUnr = 4;
+
+__device__ __forceinline__ void pg_resolve(const PageGatherArgs& a, uint64_t key, uint64_t h,
+                                           PageTableEntry e, int lane, int32_t& slot, uint32_t& len) {
+  slot = -1;
+  len = 0;
+  for (uint64_t probe = 0;;) {
+    const uint64_t hit = __ballot(e.key == key);
+    const uint64_t empty = __ballot(e.key == kPageKeyEmpty);
+    if (hit) {
+      const int fh = __ffsll((unsigned long long)hit) - 1;
+      const int fe = empty ? __ffsll((unsigned long long)empty) - 1 : 64;
+      if (fh < fe) {
+        slot = __shfl(e.slot, fh, 64);
+        len = __shfl(e.len, fh, 64);
+      }
+      return;
+    }
+    if (empty) return;
+    probe += 64;
+    if (probe > a.mask) return;
+    e = a.table[(h + probe + lane) & a.mask];
+  }
+}
+
+__global__ __launch_bounds__(256) void page_lookup_gather_small_kernel(PageGatherArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * 4;
+  for (uint32_t r0 = wave * kPgPW; r0 < a.n; r0 += nwaves * kPgPW) {
+    uint64_t key[kPgPW], h[kPgPW];
+    PageTableEntry e[kPgPW];
+#pragma unroll
+    for (int u = 0; u < kPgPW; ++u) key[u] = (r0 + u < a.n) ? a.keys[r0 + u] : kPageKeyEmpty;
+#pragma unroll
+    for (int u = 0; u < kPgPW; ++u) {
+      h[u] = page_key_hash(key[u]);
+      e[u] = a.table[(h[u] + lane) & a.mask];
+    }
+    int32_t slot[kPgPW];
+    uint32_t len[kPgPW];
+    uint32_t maxlen = 0;
+#pragma unroll
+    for (int u = 0; u < kPgPW; ++u) {
+      slot[u] = -1;
+      len[u] = 0;
+      if (r0 + u < a.n) pg_resolve(a, key[u], h[u], e[u], lane, slot[u], len[u]);
+      if (slot[u] < 0) len[u] = 0;
+      maxlen = len[u] > maxlen ? len[u] : maxlen;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < kPgPW; ++u) {
+        if (r0 + u >= a.n) continue;
+        a.slot_out[r0 + u] = slot[u];
+        a.len_out[r0 + u] = len[u];
+        if (slot[u] >= 0 && a.stamps) a.stamps[slot[u]] = a.epoch;
+      }
+    }
+    const uint8_t* src[kPgPW];
+    uint8_t* dst[kPgPW];
+#pragma unroll
+    for (int u = 0; u < kPgPW; ++u) {
+      src[u] = a.arena + (uint64_t)(slot[u] < 0 ? 0 : slot[u]) * a.page_size;
+      dst[u] = a.dst + (uint64_t)(r0 + u) * a.dst_stride;
+    }
+    for (uint64_t base = 0; base + 16 <= maxlen; base += 64 * 16 * kPgUnr) {
+      u32x4 v[kPgPW][kPgUnr];
+#pragma unroll
+      for (int u = 0; u < kPgPW; ++u)
+#pragma unroll
+        for (int k = 0; k < kPgUnr; ++k) {
+          const uint64_t off = base + (uint64_t)(k * 64 + lane) * 16;
+          if (off + 16 <= len[u]) v[u][k] = *reinterpret_cast<const u32x4*>(src[u] + off);
+        }
+#pragma unroll
+      for (int u = 0; u < kPgPW; ++u)
+#pragma unroll
+        for (int k = 0; k < kPgUnr; ++k) {
+          const uint64_t off = base + (uint64_t)(k * 64 + lane) * 16;
+          if (off + 16 <= len[u]) *reinterpret_cast<u32x4*>(dst[u] + off) = v[u][k];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kPgPW; ++u) {
+      const uint32_t full = len[u] & ~15u;
+      if ((uint32_t)lane < len[u] - full) dst[u][full + lane] = src[u][full + lane];
+    }
+  }
+}
+
 hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   if ((a.mask & (a.mask + 1)) != 0) return hipErrorInvalidValue;
+  if (a.page_size <= kPgSmallMax && a.page_size % 16 == 0 && a.dst_stride % 16 == 0 &&
+      ((uintptr_t)a.dst & 15) == 0 && ((uintptr_t)a.arena & 15) == 0) {
+    const uint64_t waves = (a.n + kPgPW - 1) / kPgPW;
+    const unsigned grid = (unsigned)std::min<uint64_t>((waves + 3) / 4, 8192);
+    hipLaunchKernelGGL(page_lookup_gather_small_kernel, dim3(grid), dim3(256), 0, stream, a);
+    return hipGetLastError();
+  }
   const unsigned gy = (unsigned)std::max<uint64_t>(1, (a.page_size + kPgChunk - 1) / kPgChunk);
   const unsigned gx = (unsigned)std::min<uint64_t>(a.n, 65535);
   hipLaunchKernelGGL(page_lookup_gather_kernel, dim3(gx, gy), dim3(kPgThreads), 0, stream, a);

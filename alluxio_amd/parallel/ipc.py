@@ -16,9 +16,15 @@ import threading
 from ..ops.native import lib
 
 
+# Allocations this process exported: handle bytes -> allocation base.  HIP refuses to open a
+# process's own IPC handle ("invalid device context"), and a same-process client needs no mapping.
+_LOCAL_EXPORTS: dict[bytes, int] = {}
+
+
 def export_handle(tensor) -> tuple[bytes, int]:
     """(IPC handle bytes, offset of the tensor's data inside the exported allocation)."""
     handle, offset, _ = lib().ipc_export(tensor.data_ptr())
+    _LOCAL_EXPORTS[bytes(handle)] = tensor.data_ptr() - int(offset)
     return bytes(handle), int(offset)
 
 
@@ -31,6 +37,9 @@ class IpcMappings:
 
     def open(self, handle: bytes, device: int) -> int:
         key = (bytes(handle), device)
+        local = _LOCAL_EXPORTS.get(key[0])
+        if local is not None:
+            return local
         with self._lock:
             base = self._maps.get(key)
             if base is None:

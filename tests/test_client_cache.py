@@ -126,6 +126,17 @@ def test_hbm_store_host_mode_slot_pressure(tmp_path):
 
 
 def test_read_pages_through_filesystem(tmp_path):
+    _read_pages_body(tmp_path)
+
+
+@pytest.mark.gpu
+def test_read_pages_device_store(gpu, tmp_path):
+    """Same reads with the store in HBM: GPU page indices, the small-page gather kernel (4 KiB
+    pages, one 77-byte tail page)."""
+    _read_pages_body(tmp_path)
+
+
+def _read_pages_body(tmp_path):
     import torch
     with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"}) as c:
         data = np.random.default_rng(3).integers(0, 256, 10 * 4096 + 77, dtype=np.uint8)
