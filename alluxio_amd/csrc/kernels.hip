@@ -1242,12 +1242,15 @@ __global__ __launch_bounds__(kPgThreads) void page_lookup_gather_kernel(PageGath
   }
 }
 
-// Small pages (<= 64 KiB, 16-B aligned rows): one wave per request and kPgPW requests per wave,
+// Small pages (<= g_pg_small_max, 16-B aligned rows): one wave per request and kPgPW requests per wave,
 // no LDS and no barriers.  The wave first issues the keys and the first 64-entry probe window of
 // all kPgPW requests back to back (independent loads in flight together), resolves them with
 // ballots (a chain longer than 64 entries falls back to the loop), then copies the pages with
 // kPgPW x kPgUnr 16-B loads in flight per lane before the stores.
-constexpr uint64_t kPgSmallMax = 64 * 1024;
+// Page sizes up to g_pg_small_max take the wave-per-request kernel (tools/page_cache_bench.py
+// --variants both on MI355X: 4 KiB pages 2.56 vs 2.40 TB/s, 64 KiB pages 2.25 vs 2.59 TB/s).
+static uint64_t g_pg_small_max = 16 * 1024;
+void set_page_gather_small_max(uint64_t bytes) { g_pg_small_max = bytes; }
 constexpr int kPgPW = 4;
 constexpr int kPgUnr = 4;
 
@@ -1343,7 +1346,7 @@ __global__ __launch_bounds__(256) void page_lookup_gather_small_kernel(PageGathe
 hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   if ((a.mask & (a.mask + 1)) != 0) return hipErrorInvalidValue;
-  if (a.page_size <= kPgSmallMax && a.page_size % 16 == 0 && a.dst_stride % 16 == 0 &&
+  if (a.page_size <= g_pg_small_max && a.page_size % 16 == 0 && a.dst_stride % 16 == 0 &&
       ((uintptr_t)a.dst & 15) == 0 && ((uintptr_t)a.arena & 15) == 0) {
     const uint64_t waves = (a.n + kPgPW - 1) / kPgPW;
     const unsigned grid = (unsigned)std::min<uint64_t>((waves + 3) / 4, 8192);

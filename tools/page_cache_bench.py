@@ -45,6 +45,8 @@ def main(argv=None):
     ap.add_argument("--max-pages", type=int, default=1 << 18)
     ap.add_argument("--batch-bytes", default="1g", help="bytes gathered per launch")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--variants", choices=["auto", "both"], default="auto",
+                    help="both: time the wave-per-request and the chunked kernel at every page size")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import torch
@@ -54,8 +56,12 @@ def main(argv=None):
     assert torch.cuda.is_available(), "needs a HIP device"
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
-    for ps_s in a.page_sizes.split(","):
-        ps = parse_space_size(ps_s)
+    runs = [(parse_space_size(p), None) for p in a.page_sizes.split(",")]
+    if a.variants == "both":
+        runs = [(ps, v) for ps, _ in runs for v in ("wave", "chunk")]
+    for ps, variant in runs:
+        if variant is not None:
+            C.set_page_gather_small_max(1 << 40 if variant == "wave" else 0)
         slots = max(1, min(parse_space_size(a.cache) // ps, a.max_pages))
         pc = C.PageCache(0, slots * ps, ps, True)
         src = torch.zeros(ps, dtype=torch.uint8, device=dev)
@@ -89,8 +95,8 @@ def main(argv=None):
         flat = arena.view(-1)[: n * ps] if n <= slots else None
         ms_cp = _time_ms(lambda: out2.view(-1).copy_(flat), a.iters) if flat is not None else None
         nbytes = n * ps
-        r = {"bench": "page_cache_gather", "page_size": ps, "pages_cached": slots, "batch_pages": n,
-             "batch_bytes": nbytes, "fused_lookup_gather_ms": round(ms, 4),
+        r = {"bench": "page_cache_gather", "kernel": variant or "auto", "page_size": ps, "pages_cached": slots,
+             "batch_pages": n, "batch_bytes": nbytes, "fused_lookup_gather_ms": round(ms, 4),
              "fused_GBps": round(nbytes / ms / 1e6, 1),
              "torch_index_select_resolved_ms": round(ms_ix, 4),
              "torch_index_select_GBps": round(nbytes / ms_ix / 1e6, 1),
