@@ -1251,8 +1251,10 @@ __global__ __launch_bounds__(kPgThreads) void page_lookup_gather_kernel(PageGath
 // --variants both on MI355X: 4 KiB pages 2.56 vs 2.40 TB/s, 64 KiB pages 2.25 vs 2.59 TB/s).
 static uint64_t g_pg_small_max = 16 * 1024;
 void set_page_gather_small_max(uint64_t bytes) { g_pg_small_max = bytes; }
-constexpr int kPgPW = 4;
-constexpr int kPgUnr = 4;
+// Wave-kernel variant (requests per wave, 16-B loads per lane per page, store policy):
+// 0 = 4/4/plain, 1 = 8/2/plain, 2 = 4/4/nontemporal, 3 = 8/4/plain.
+static int g_pg_wave_variant = 0;
+void set_page_gather_wave_variant(int v) { g_pg_wave_variant = v; }
 
 __device__ __forceinline__ void pg_resolve(const PageGatherArgs& a, uint64_t key, uint64_t h,
                                            PageTableEntry e, int lane, int32_t& slot, uint32_t& len) {
@@ -1277,6 +1279,7 @@ __device__ __forceinline__ void pg_resolve(const PageGatherArgs& a, uint64_t key
   }
 }
 
+template <int kPgPW, int kPgUnr, int SP>
 __global__ __launch_bounds__(256) void page_lookup_gather_small_kernel(PageGatherArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1332,7 +1335,7 @@ __global__ __launch_bounds__(256) void page_lookup_gather_small_kernel(PageGathe
 #pragma unroll
         for (int k = 0; k < kPgUnr; ++k) {
           const uint64_t off = base + (uint64_t)(k * 64 + lane) * 16;
-          if (off + 16 <= len[u]) *reinterpret_cast<u32x4*>(dst[u] + off) = v[u][k];
+          if (off + 16 <= len[u]) st16<SP>(reinterpret_cast<u32x4*>(dst[u] + off), v[u][k]);
         }
     }
 #pragma unroll
@@ -1348,9 +1351,17 @@ hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream
   if ((a.mask & (a.mask + 1)) != 0) return hipErrorInvalidValue;
   if (a.page_size <= g_pg_small_max && a.page_size % 16 == 0 && a.dst_stride % 16 == 0 &&
       ((uintptr_t)a.dst & 15) == 0 && ((uintptr_t)a.arena & 15) == 0) {
-    const uint64_t waves = (a.n + kPgPW - 1) / kPgPW;
+    const int pw = (g_pg_wave_variant == 1 || g_pg_wave_variant == 3) ? 8 : 4;
+    const uint64_t waves = (a.n + pw - 1) / pw;
     const unsigned grid = (unsigned)std::min<uint64_t>((waves + 3) / 4, 8192);
-    hipLaunchKernelGGL(page_lookup_gather_small_kernel, dim3(grid), dim3(256), 0, stream, a);
+#define AMDX_PG(PW, U, S) hipLaunchKernelGGL((page_lookup_gather_small_kernel<PW, U, S>), dim3(grid), dim3(256), 0, stream, a)
+    switch (g_pg_wave_variant) {
+      case 1: AMDX_PG(8, 2, 0); break;
+      case 2: AMDX_PG(4, 4, 1); break;
+      case 3: AMDX_PG(8, 4, 0); break;
+      default: AMDX_PG(4, 4, 0); break;
+    }
+#undef AMDX_PG
     return hipGetLastError();
   }
   const unsigned gy = (unsigned)std::max<uint64_t>(1, (a.page_size + kPgChunk - 1) / kPgChunk);

@@ -53,6 +53,7 @@ inline void bind_page_cache(pybind11::module_& m) {
       .def_property_readonly("on_device", &DevicePageCache::on_device);
   m.attr("PAGE_KEY_EMPTY") = kPageKeyEmpty;
   m.def("set_page_gather_small_max", &set_page_gather_small_max, py::arg("bytes"));
+  m.def("set_page_gather_wave_variant", &set_page_gather_wave_variant, py::arg("variant"));
 }
 
 }  // namespace amdx

@@ -55,7 +55,8 @@ for s in $STEPS; do
       ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
-    pcsweep) run page_cache_sweep 400 python tools/page_cache_bench.py --variants both --page-sizes 4k,8k,16k,32k,64k,256k --out "$OUT/page_cache_sweep.jsonl" ;;
+    pcsweep) run page_cache_sweep 400 python tools/page_cache_bench.py --variants both --passes 2 --page-sizes 4k,8k,16k,32k,64k,256k --out "$OUT/page_cache_sweep.jsonl" ;;
+    pcwave) run page_cache_wave 400 python tools/page_cache_bench.py --variants both --passes 2 --wave-variants 0,1,2,3 --page-sizes 4k,16k --iters 30 --out "$OUT/page_cache_wave.jsonl" ;;
     pc)
       run page_cache_bench 300 python tools/page_cache_bench.py --out "$OUT/page_cache_bench.jsonl"
       run rocprof_pc 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pc" -o pc --output-format csv -- python3 tools/page_cache_bench.py --page-sizes 4k,64k,2m --iters 5

@@ -47,6 +47,9 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", choices=["auto", "both"], default="auto",
                     help="both: time the wave-per-request and the chunked kernel at every page size")
+    ap.add_argument("--wave-variants", default="0",
+                    help="wave-kernel variants timed with --variants both (see set_page_gather_wave_variant)")
+    ap.add_argument("--passes", type=int, default=1, help="repeat the whole run list; every pass is reported")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import torch
@@ -58,10 +61,20 @@ def main(argv=None):
     stream = torch.cuda.current_stream().cuda_stream
     runs = [(parse_space_size(p), None) for p in a.page_sizes.split(",")]
     if a.variants == "both":
-        runs = [(ps, v) for ps, _ in runs for v in ("wave", "chunk")]
-    for ps, variant in runs:
+        waves = ["wave%s" % w for w in a.wave_variants.split(",")]
+        runs = [(ps, v) for ps, _ in runs for v in waves + ["chunk"]]
+    # clocks and caches warm before the first timed case, so case order does not bias the sweep
+    warm = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    warm2 = torch.empty_like(warm)
+    for _ in range(50):
+        warm2.copy_(warm)
+    torch.cuda.synchronize()
+    del warm, warm2
+    for pas, (ps, variant) in [(p, r) for p in range(a.passes) for r in runs]:
         if variant is not None:
-            C.set_page_gather_small_max(1 << 40 if variant == "wave" else 0)
+            C.set_page_gather_small_max(0 if variant == "chunk" else 1 << 40)
+            if variant != "chunk":
+                C.set_page_gather_wave_variant(int(variant[4:]))
         slots = max(1, min(parse_space_size(a.cache) // ps, a.max_pages))
         pc = C.PageCache(0, slots * ps, ps, True)
         src = torch.zeros(ps, dtype=torch.uint8, device=dev)
@@ -95,7 +108,7 @@ def main(argv=None):
         flat = arena.view(-1)[: n * ps] if n <= slots else None
         ms_cp = _time_ms(lambda: out2.view(-1).copy_(flat), a.iters) if flat is not None else None
         nbytes = n * ps
-        r = {"bench": "page_cache_gather", "kernel": variant or "auto", "page_size": ps, "pages_cached": slots,
+        r = {"bench": "page_cache_gather", "pass": pas, "kernel": variant or "auto", "page_size": ps, "pages_cached": slots,
              "batch_pages": n, "batch_bytes": nbytes, "fused_lookup_gather_ms": round(ms, 4),
              "fused_GBps": round(nbytes / ms / 1e6, 1),
              "torch_index_select_resolved_ms": round(ms_ix, 4),
