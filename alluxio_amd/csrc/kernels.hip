@@ -1253,7 +1253,7 @@ static uint64_t g_pg_small_max = 16 * 1024;
 void set_page_gather_small_max(uint64_t bytes) { g_pg_small_max = bytes; }
 // Wave-kernel variant (requests per wave, 16-B loads per lane per page, store policy):
 // 0 = 4/4/plain, 1 = 8/2/plain, 2 = 4/4/nontemporal, 3 = 8/4/plain.
-static int g_pg_wave_variant = 0;
+static int g_pg_wave_variant = 2;  // nt stores: 4 KiB 3.03 vs 2.56 TB/s, 16 KiB 2.64 vs 2.42 TB/s (profiles/r1_page_cache_wave.jsonl)
 void set_page_gather_wave_variant(int v) { g_pg_wave_variant = v; }
 
 __device__ __forceinline__ void pg_resolve(const PageGatherArgs& a, uint64_t key, uint64_t h,
