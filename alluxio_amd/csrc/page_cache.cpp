@@ -241,6 +241,74 @@ std::vector<uint64_t> DevicePageCache::put(uint64_t key, uint64_t src, uint64_t 
   return evicted;
 }
 
+// Batched fill: the table work runs on the host for the whole batch and the page bytes move in
+// one batched_copy_kernel launch (device sources) instead of one hipMemcpy + sync per page.
+// Pending copies are launched before any eviction, so a slot reused later in the batch is written
+// by a later launch on the same stream.
+std::vector<uint64_t> DevicePageCache::put_many(const std::vector<uint64_t>& keys, uint64_t src,
+                                                uint64_t src_stride, uint64_t len, int src_kind,
+                                                uint64_t stream, bool evict) {
+  if (len > page_size_) throw StoreError(kErrInvalidArgument, "page larger than the page size");
+  for (uint64_t k : keys)
+    if (k == kPageKeyEmpty || k == kPageKeyTomb) throw StoreError(kErrInvalidArgument, "reserved page key");
+  std::lock_guard<std::mutex> g(mu_);
+  wait_gathers();
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<uint64_t> evicted;
+  std::vector<CopySeg> segs;
+  uint64_t chunks = 0;
+  auto flush = [&]() {
+    if (segs.empty()) return;
+    if (!use_device_) {
+      for (const auto& s : segs) std::memcpy((void*)s.dst, (const void*)s.src, s.bytes);
+    } else if (src_kind == (int)MemKind::kDevice) {
+      CopySeg* d = nullptr;
+      PC_HIP_OK(hipMalloc((void**)&d, segs.size() * sizeof(CopySeg)));
+      PC_HIP_OK(hipMemcpyAsync(d, segs.data(), segs.size() * sizeof(CopySeg), hipMemcpyHostToDevice, st));
+      const hipError_t e = launch_batched_copy(d, (int)segs.size(), chunks, st);
+      const hipError_t e2 = hipStreamSynchronize(st);
+      hipFree(d);
+      PC_HIP_OK(e);
+      PC_HIP_OK(e2);
+    } else {
+      for (const auto& s : segs)
+        PC_HIP_OK(hipMemcpyAsync((void*)s.dst, (const void*)s.src, s.bytes, hipMemcpyHostToDevice, st));
+      PC_HIP_OK(hipStreamSynchronize(st));
+    }
+    segs.clear();
+    chunks = 0;
+  };
+  for (size_t i = 0; i < keys.size(); ++i) {
+    const uint64_t key = keys[i];
+    int32_t slot;
+    const int64_t idx = find_index(key);
+    if (idx >= 0) {
+      slot = table_h_[idx].slot;
+    } else {
+      if (free_.empty()) {
+        if (!evict) {
+          flush();
+          throw StoreError(kErrOutOfSpace, "page cache is full");
+        }
+        flush();
+        const auto ev = evict_lru(std::max<uint32_t>(1, nslots_ / 64));
+        evicted.insert(evicted.end(), ev.begin(), ev.end());
+      }
+      slot = (int32_t)free_.back();
+      free_.pop_back();
+    }
+    if (len) {
+      segs.push_back(CopySeg{src + i * src_stride, arena_ + (uint64_t)slot * page_size_, len, chunks});
+      chunks += (len + kCopyChunk - 1) / kCopyChunk;
+    }
+    slot_key_[slot] = key;
+    stamp_h_[slot] = ++epoch_;
+    table_insert(key, slot, (uint32_t)len);
+  }
+  flush();
+  return evicted;
+}
+
 bool DevicePageCache::erase(uint64_t key) {
   std::lock_guard<std::mutex> g(mu_);
   const int64_t idx = find_index(key);

@@ -33,6 +33,10 @@ class DevicePageCache {
   // Store `len` bytes from `src` (MemKind) as page `key`.  When every slot is taken and `evict`
   // is set, least-recently-used pages are dropped first (returned); otherwise full -> throws.
   std::vector<uint64_t> put(uint64_t key, uint64_t src, uint64_t len, int src_kind, uint64_t stream, bool evict);
+  // Store keys[i] <- src + i * src_stride (len bytes each; stride 0 repeats one page) with one
+  // batched copy launch; evicted keys are returned as for put().
+  std::vector<uint64_t> put_many(const std::vector<uint64_t>& keys, uint64_t src, uint64_t src_stride,
+                                 uint64_t len, int src_kind, uint64_t stream, bool evict);
   bool erase(uint64_t key);
   bool contains(uint64_t key) const;
   // (slot, len) or (-1, 0); bumps recency.

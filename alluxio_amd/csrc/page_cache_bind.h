@@ -24,6 +24,9 @@ inline void bind_page_cache(pybind11::module_& m) {
              py::gil_scoped_release rel;
              return c.put(key, (uint64_t)bi.ptr, n, (int)MemKind::kHost, 0, evict);
            }, py::arg("key"), py::arg("data"), py::arg("evict") = true)
+      .def("put_many", &DevicePageCache::put_many, G(), py::arg("keys"), py::arg("src"),
+           py::arg("src_stride"), py::arg("length"), py::arg("src_kind"), py::arg("stream"),
+           py::arg("evict"))
       .def("erase", &DevicePageCache::erase, G())
       .def("contains", &DevicePageCache::contains, G())
       .def("lookup", &DevicePageCache::lookup, G())

@@ -108,3 +108,43 @@ def test_device_gather_matches_torch(gpu):
     ev = pc.put(_key(4, 0), src[0].data_ptr(), ps, 1, stream, True)
     assert ev and not (set(ev) & set(hot_keys.cpu().tolist()))
     torch.cuda.synchronize()
+
+
+def test_host_put_many_matches_put_and_evicts():
+    C = lib()
+    ps = 4096
+    pc = C.PageCache(0, 16 * ps, ps, False)
+    rng = np.random.default_rng(7)
+    buf = rng.integers(0, 256, (12, ps), dtype=np.uint8)
+    keys = [_key(3, i) for i in range(12)]
+    assert pc.put_many(keys, buf.ctypes.data, ps, ps, 0, 0, False) == []
+    assert pc.used == 12
+    for i in (0, 5, 11):
+        assert pc.get_bytes(keys[i], 0, ps) == buf[i].tobytes()
+    # stride 0 repeats one source page; overflowing the 16 slots evicts the LRU pages
+    more = [_key(4, i) for i in range(8)]
+    with pytest.raises(Exception):
+        pc.put_many(more, buf.ctypes.data, 0, ps, 0, 0, False)
+    ev = pc.put_many([_key(5, i) for i in range(8)], buf[2].ctypes.data, 0, ps, 0, 0, True)
+    assert len(ev) >= 4 and all(pc.contains(k) is False for k in ev)
+    for i in range(8):
+        assert pc.get_bytes(_key(5, i), 0, ps) == buf[2].tobytes()
+
+
+@pytest.mark.gpu
+def test_device_put_many_matches_torch(gpu):
+    import torch
+    C = lib()
+    ps, n = 8192, 300
+    pc = C.PageCache(0, 512 * ps, ps, True)
+    src = torch.randint(0, 256, (n, ps), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    keys = [_key(9, i) for i in range(n)]
+    assert pc.put_many(keys, src.data_ptr(), ps, ps, 1, stream, False) == []
+    out = torch.empty_like(src)
+    kd = torch.tensor(keys, dtype=torch.int64, device="cuda")
+    so = torch.empty(n, dtype=torch.int32, device="cuda")
+    lo = torch.empty(n, dtype=torch.int32, device="cuda")
+    pc.gather(kd.data_ptr(), n, out.data_ptr(), ps, so.data_ptr(), lo.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert bool((so >= 0).all()) and torch.equal(out, src)

@@ -14,6 +14,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -78,8 +79,10 @@ def main(argv=None):
         slots = max(1, min(parse_space_size(a.cache) // ps, a.max_pages))
         pc = C.PageCache(0, slots * ps, ps, True)
         src = torch.zeros(ps, dtype=torch.uint8, device=dev)
-        for i in range(slots):
-            pc.put((1 << 24) | i, src.data_ptr(), ps, 1, stream, False)
+        torch.cuda.synchronize()
+        t_fill = time.perf_counter()
+        pc.put_many([(1 << 24) | i for i in range(slots)], src.data_ptr(), 0, ps, 1, stream, False)
+        fill_GBps = slots * ps / (time.perf_counter() - t_fill) / 1e9
         C.fill_pattern(pc.arena, slots * ps, 1234, 0, stream)      # distinct bytes in every page
         arena = torch.as_tensor(_DevArray(pc.arena, slots * ps), device=dev).view(slots, ps)
         n = max(1, min(parse_space_size(a.batch_bytes) // ps, 1 << 20))
@@ -114,6 +117,7 @@ def main(argv=None):
              "torch_index_select_resolved_ms": round(ms_ix, 4),
              "torch_index_select_GBps": round(nbytes / ms_ix / 1e6, 1),
              "contiguous_copy_GBps": round(nbytes / ms_cp / 1e6, 1) if ms_cp else None,
+             "fill_put_many_GBps": round(fill_GBps, 1),
              "verified": True}
         print(json.dumps(r), flush=True)
         if a.out:
