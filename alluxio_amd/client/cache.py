@@ -270,6 +270,15 @@ class HbmPageStore:
         slot, _ = self.cache.lookup(self.key(pid))
         return None if slot < 0 else self.cache.slot_ptr(slot) + offset
 
+    def read_segments(self, pids, offsets, lengths, dsts, on_device: bool = True):
+        """Copy ``lengths[i]`` bytes at ``offsets[i]`` of page ``pids[i]`` to address ``dsts[i]``
+        (device memory when ``on_device``, else host), one batched launch on the current stream.
+        Returns the indices that missed; their destinations are untouched."""
+        keys = [self.key(p) for p in pids]
+        kind = 1 if (on_device and self.use_device) else 0
+        return list(self.cache.read_segments(keys, list(offsets), list(lengths), list(dsts), kind,
+                                             self._stream()))
+
     def get(self, pid, offset, length):
         k = self.key(pid)
         slot, n = self.cache.lookup(k)
@@ -503,39 +512,47 @@ class LocalCacheFileInStream(io.RawIOBase):
         return len(data)
 
     def read_into(self, tensor) -> int:
-        """Fill a (device) tensor from the current position: cached HBM pages are gathered by
-        one batched-copy launch; missing pages are fetched and cached first."""
+        """Fill a (device) tensor from the current position.  Cached HBM pages are copied by the
+        native store in one batched launch per group of pages: slots are resolved and the copy
+        queued under the store lock, so no concurrent put can recycle a slot before its bytes were
+        read.  Missing pages are fetched and cached first, a group at a time (a group is capped at
+        a quarter of the cache, so a read longer than the cache still works); a page evicted
+        between fill and copy is served through the byte path."""
+        import numpy as np
         import torch
         n = min(tensor.numel() * tensor.element_size(), self.length - self.pos)
         store = self.cache.store
-        if not (tensor.is_cuda and isinstance(store, HbmPageStore)):
+        flat = tensor.view(-1).view(torch.uint8) if tensor.is_contiguous() else None
+        if flat is None or not (tensor.is_cuda and isinstance(store, HbmPageStore)):
             data = self.read(n)
-            import numpy as np
-            tensor.view(torch.uint8)[:len(data)].copy_(torch.from_numpy(np.frombuffer(data, dtype=np.uint8)))
+            tensor.view(torch.uint8).view(-1)[:len(data)].copy_(torch.from_numpy(np.frombuffer(data, dtype=np.uint8)))
             return len(data)
         ps = self.cache.page_size
-        segs, done = [], 0
-        dst = tensor.data_ptr()
+        group = max(1, store.slots // 4)
+        dst = flat.data_ptr()
+        done = 0
         while done < n:
-            p = self.pos + done
-            idx, off = divmod(p, ps)
-            take = min(n - done, ps - off)
-            pid = PageId(self.file_id, idx)
-            if not self.cache.has(pid):
-                self._page(idx, 0, 0)  # fetch + put
-            with self.cache._lock(pid):
-                src = store.ptr(pid, off)
-            if src is None:  # evicted meanwhile: byte path for this page
+            pieces = []                      # (page index, offset in page, bytes, dst offset)
+            while done < n and len(pieces) < group:
+                p = self.pos + done
+                idx, off = divmod(p, ps)
+                take = min(n - done, ps - off)
+                pieces.append((idx, off, take, done))
+                done += take
+            for idx, _, _, _ in pieces:
+                pid = PageId(self.file_id, idx)
+                if not self.cache.has(pid):
+                    self._page(idx, 0, 0)   # fetch + put
+            missed = store.read_segments([PageId(self.file_id, i) for i, _, _, _ in pieces],
+                                         [o for _, o, _, _ in pieces], [t for _, _, t, _ in pieces],
+                                         [dst + d for _, _, _, d in pieces])
+            hit = set(range(len(pieces))) - set(missed)
+            for j in hit:
+                self.cache.evictor.update_on_get(PageId(self.file_id, pieces[j][0]))
+            for j in missed:                 # evicted meanwhile: byte path for this page
+                idx, off, take, d = pieces[j]
                 chunk = self._page(idx, off, take)
-                import numpy as np
-                tensor.view(torch.uint8)[done:done + take].copy_(torch.from_numpy(np.frombuffer(chunk, dtype=np.uint8)))
-            else:
-                segs.append((src, dst + done, take))
-                self.cache.evictor.update_on_get(pid)
-            done += take
-        if segs:
-            from ..ops.native import lib
-            lib().batched_copy(segs, int(torch.cuda.current_stream().cuda_stream), True)
+                flat[d:d + len(chunk)].copy_(torch.from_numpy(np.frombuffer(chunk, dtype=np.uint8)))
         self.pos += n
         return n
 

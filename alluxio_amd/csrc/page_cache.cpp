@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <unordered_map>
 
 #include "block_store.h"   // StoreError, MemKind, error codes
 
@@ -42,7 +43,7 @@ DevicePageCache::DevicePageCache(int device, uint64_t capacity_bytes, uint64_t p
     PC_HIP_OK(hipMalloc((void**)&table_d_, table_h_.size() * sizeof(PageTableEntry)));
     PC_HIP_OK(hipMalloc((void**)&stamps_d_, nslots_ * sizeof(uint32_t)));
     PC_HIP_OK(hipMemset(stamps_d_, 0, nslots_ * sizeof(uint32_t)));
-    PC_HIP_OK(hipEventCreateWithFlags(&last_gather_, hipEventDisableTiming));
+    ring_.init();
   } else {
     void* p = std::aligned_alloc(64, ((nslots_ * page_size_ + 63) / 64) * 64);
     if (!p) throw StoreError(kErrOutOfSpace, "host page cache arena allocation failed");
@@ -54,7 +55,12 @@ DevicePageCache::DevicePageCache(int device, uint64_t capacity_bytes, uint64_t p
 DevicePageCache::~DevicePageCache() {
   if (use_device_) {
     hipSetDevice(device_);
-    if (gather_pending_) hipEventSynchronize(last_gather_);
+    for (hipEvent_t e : pending_ev_) {
+      hipEventSynchronize(e);
+      hipEventDestroy(e);
+    }
+    for (hipEvent_t e : ev_pool_) hipEventDestroy(e);
+    ring_.release();
     hipFree((void*)arena_);
     hipFree(table_d_);
     hipFree(stamps_d_);
@@ -63,7 +69,6 @@ DevicePageCache::~DevicePageCache() {
     hipFree(keys_d_);
     hipFree(slots_d_);
     hipFree(lens_d_);
-    if (last_gather_) hipEventDestroy(last_gather_);
   } else {
     std::free((void*)arena_);
   }
@@ -134,6 +139,9 @@ void DevicePageCache::rebuild_table() {
 
 void DevicePageCache::flush_table(hipStream_t stream) {
   if (!use_device_) return;
+  if (!full_upload_ && dirty_.empty()) return;
+  // a gather queued on another stream may still be probing the entries about to change
+  order_after_readers(stream);
   if (full_upload_) {
     PC_HIP_OK(hipMemcpyAsync(table_d_, table_h_.data(), table_h_.size() * sizeof(PageTableEntry),
                              hipMemcpyHostToDevice, stream));
@@ -197,10 +205,42 @@ std::vector<uint64_t> DevicePageCache::evict_lru(uint32_t need) {
 }
 
 void DevicePageCache::wait_gathers() {
-  if (use_device_ && gather_pending_) {
-    PC_HIP_OK(hipEventSynchronize(last_gather_));
-    gather_pending_ = false;
+  if (!use_device_) return;
+  hipError_t first = hipSuccess;
+  for (hipEvent_t ev : pending_ev_) {
+    const hipError_t e = hipEventSynchronize(ev);
+    if (e != hipSuccess && first == hipSuccess) first = e;
+    ev_pool_.push_back(ev);
   }
+  pending_ev_.clear();
+  PC_HIP_OK(first);
+}
+
+void DevicePageCache::track_reader(hipStream_t stream) {
+  // completed events are recycled first so the pending list stays short under steady traffic
+  size_t w = 0;
+  for (size_t i = 0; i < pending_ev_.size(); ++i) {
+    if (hipEventQuery(pending_ev_[i]) == hipSuccess) ev_pool_.push_back(pending_ev_[i]);
+    else pending_ev_[w++] = pending_ev_[i];
+  }
+  pending_ev_.resize(w);
+  hipEvent_t ev;
+  if (!ev_pool_.empty()) {
+    ev = ev_pool_.back();
+    ev_pool_.pop_back();
+  } else {
+    PC_HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  const hipError_t e = hipEventRecord(ev, stream);
+  if (e != hipSuccess) {
+    ev_pool_.push_back(ev);
+    PC_HIP_OK(e);
+  }
+  pending_ev_.push_back(ev);
+}
+
+void DevicePageCache::order_after_readers(hipStream_t stream) {
+  for (hipEvent_t ev : pending_ev_) PC_HIP_OK(hipStreamWaitEvent(stream, ev, 0));
 }
 
 // ---- public API -------------------------------------------------------------------------------
@@ -243,67 +283,100 @@ std::vector<uint64_t> DevicePageCache::put(uint64_t key, uint64_t src, uint64_t 
 
 // Batched fill: the table work runs on the host for the whole batch and the page bytes move in
 // one batched_copy_kernel launch (device sources) instead of one hipMemcpy + sync per page.
-// Pending copies are launched before any eviction, so a slot reused later in the batch is written
+// Slot assignments are staged and committed to the table only after their copy succeeded; copies
+// are flushed (and committed) before any eviction, so a slot reused later in the batch is written
 // by a later launch on the same stream.
-std::vector<uint64_t> DevicePageCache::put_many(const std::vector<uint64_t>& keys, uint64_t src,
+std::vector<uint64_t> DevicePageCache::put_many(const std::vector<uint64_t>& keys_in, uint64_t src,
                                                 uint64_t src_stride, uint64_t len, int src_kind,
                                                 uint64_t stream, bool evict) {
   if (len > page_size_) throw StoreError(kErrInvalidArgument, "page larger than the page size");
-  for (uint64_t k : keys)
+  for (uint64_t k : keys_in)
     if (k == kPageKeyEmpty || k == kPageKeyTomb) throw StoreError(kErrInvalidArgument, "reserved page key");
+  // de-duplicate: the last occurrence of a key wins (its source index is kept)
+  std::vector<std::pair<uint64_t, size_t>> batch;   // (key, source index)
+  batch.reserve(keys_in.size());
+  {
+    std::unordered_map<uint64_t, size_t> last;
+    last.reserve(keys_in.size() * 2);
+    for (size_t i = 0; i < keys_in.size(); ++i) last[keys_in[i]] = i;
+    for (size_t i = 0; i < keys_in.size(); ++i)
+      if (last[keys_in[i]] == i) batch.emplace_back(keys_in[i], i);
+  }
   std::lock_guard<std::mutex> g(mu_);
+  if (!evict) {
+    size_t fresh = 0;
+    for (const auto& kv : batch) fresh += find_index(kv.first) < 0;
+    if (fresh > free_.size()) throw StoreError(kErrOutOfSpace, "page cache is full");
+  }
   wait_gathers();
   hipStream_t st = (hipStream_t)stream;
   std::vector<uint64_t> evicted;
   std::vector<CopySeg> segs;
-  uint64_t chunks = 0;
-  auto flush = [&]() {
-    if (segs.empty()) return;
-    if (!use_device_) {
-      for (const auto& s : segs) std::memcpy((void*)s.dst, (const void*)s.src, s.bytes);
-    } else if (src_kind == (int)MemKind::kDevice) {
-      CopySeg* d = nullptr;
-      PC_HIP_OK(hipMalloc((void**)&d, segs.size() * sizeof(CopySeg)));
-      PC_HIP_OK(hipMemcpyAsync(d, segs.data(), segs.size() * sizeof(CopySeg), hipMemcpyHostToDevice, st));
-      const hipError_t e = launch_batched_copy(d, (int)segs.size(), chunks, st);
-      const hipError_t e2 = hipStreamSynchronize(st);
-      hipFree(d);
-      PC_HIP_OK(e);
-      PC_HIP_OK(e2);
-    } else {
-      for (const auto& s : segs)
-        PC_HIP_OK(hipMemcpyAsync((void*)s.dst, (const void*)s.src, s.bytes, hipMemcpyHostToDevice, st));
-      PC_HIP_OK(hipStreamSynchronize(st));
+  struct Staged { uint64_t key; int32_t slot; bool fresh; };
+  std::vector<Staged> staged;
+  auto rollback = [&]() {
+    // staged pages hold undefined bytes: new slots go back to the free list, overwritten pages
+    // are dropped from the table (a miss, never stale data)
+    for (const auto& sp : staged) {
+      if (sp.fresh) {
+        free_.push_back((uint32_t)sp.slot);
+      } else {
+        const int64_t idx = find_index(sp.key);
+        if (idx >= 0) table_erase_at((uint64_t)idx);
+        slot_key_[sp.slot] = kPageKeyEmpty;
+        free_.push_back((uint32_t)sp.slot);
+      }
     }
+    staged.clear();
     segs.clear();
-    chunks = 0;
   };
-  for (size_t i = 0; i < keys.size(); ++i) {
-    const uint64_t key = keys[i];
+  auto flush = [&]() {
+    if (!segs.empty()) {
+      try {
+        if (!use_device_) {
+          for (const auto& sg : segs) std::memcpy((void*)sg.dst, (const void*)sg.src, sg.bytes);
+        } else if (src_kind == (int)MemKind::kDevice) {
+          PC_HIP_OK(ring_.launch(segs, st));
+          PC_HIP_OK(hipStreamSynchronize(st));
+        } else {
+          for (const auto& sg : segs)
+            PC_HIP_OK(hipMemcpyAsync((void*)sg.dst, (const void*)sg.src, sg.bytes, hipMemcpyHostToDevice, st));
+          PC_HIP_OK(hipStreamSynchronize(st));
+        }
+      } catch (...) {
+        rollback();
+        throw;
+      }
+    }
+    for (const auto& sp : staged) {
+      const uint64_t bytes = len;
+      slot_key_[sp.slot] = sp.key;
+      stamp_h_[sp.slot] = ++epoch_;
+      table_insert(sp.key, sp.slot, (uint32_t)bytes);
+    }
+    staged.clear();
+    segs.clear();
+  };
+  for (const auto& kv : batch) {
+    const uint64_t key = kv.first;
     int32_t slot;
+    bool fresh = false;
     const int64_t idx = find_index(key);
     if (idx >= 0) {
       slot = table_h_[idx].slot;
     } else {
       if (free_.empty()) {
-        if (!evict) {
-          flush();
-          throw StoreError(kErrOutOfSpace, "page cache is full");
-        }
         flush();
         const auto ev = evict_lru(std::max<uint32_t>(1, nslots_ / 64));
         evicted.insert(evicted.end(), ev.begin(), ev.end());
+        if (free_.empty()) throw StoreError(kErrOutOfSpace, "page cache is full");
       }
       slot = (int32_t)free_.back();
       free_.pop_back();
+      fresh = true;
     }
-    if (len) {
-      segs.push_back(CopySeg{src + i * src_stride, arena_ + (uint64_t)slot * page_size_, len, chunks});
-      chunks += (len + kCopyChunk - 1) / kCopyChunk;
-    }
-    slot_key_[slot] = key;
-    stamp_h_[slot] = ++epoch_;
-    table_insert(key, slot, (uint32_t)len);
+    staged.push_back(Staged{key, slot, fresh});
+    if (len) segs.push_back(CopySeg{src + kv.second * src_stride, arena_ + (uint64_t)slot * page_size_, len, 0});
   }
   flush();
   return evicted;
@@ -354,11 +427,56 @@ bool DevicePageCache::read(uint64_t key, uint64_t offset, uint64_t len, uint64_t
   return true;
 }
 
+std::vector<int32_t> DevicePageCache::read_segments(const std::vector<uint64_t>& keys,
+                                                    const std::vector<uint64_t>& offsets,
+                                                    const std::vector<uint64_t>& lens,
+                                                    const std::vector<uint64_t>& dsts, int dst_kind,
+                                                    uint64_t stream) {
+  const size_t n = keys.size();
+  if (offsets.size() != n || lens.size() != n || dsts.size() != n)
+    throw StoreError(kErrInvalidArgument, "read_segments: keys/offsets/lens/dsts differ in length");
+  std::vector<int32_t> missed;
+  std::vector<CopySeg> segs;
+  segs.reserve(n);
+  hipStream_t st = (hipStream_t)stream;
+  std::lock_guard<std::mutex> g(mu_);
+  const uint32_t epoch = ++epoch_;
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t idx = find_index(keys[i]);
+    if (idx < 0 || offsets[i] + lens[i] > table_h_[idx].len) {
+      missed.push_back((int32_t)i);
+      continue;
+    }
+    const auto& e = table_h_[idx];
+    stamp_h_[e.slot] = epoch;
+    if (lens[i]) segs.push_back(CopySeg{arena_ + (uint64_t)e.slot * page_size_ + offsets[i], dsts[i], lens[i], 0});
+  }
+  if (segs.empty()) return missed;
+  if (!use_device_) {
+    for (const auto& sg : segs) std::memcpy((void*)sg.dst, (const void*)sg.src, sg.bytes);
+    return missed;
+  }
+  if (dst_kind == (int)MemKind::kDevice) {
+    PC_HIP_OK(ring_.launch(segs, st));
+    track_reader(st);
+  } else {
+    for (const auto& sg : segs)
+      PC_HIP_OK(hipMemcpyAsync((void*)sg.dst, (const void*)sg.src, sg.bytes, hipMemcpyDeviceToHost, st));
+    PC_HIP_OK(hipStreamSynchronize(st));
+  }
+  return missed;
+}
+
 void DevicePageCache::gather(uint64_t keys, uint32_t n, uint64_t dst, uint64_t dst_stride, uint64_t slot_out,
                              uint64_t len_out, uint64_t stream) {
   if (n == 0) return;
   if (dst_stride < page_size_ && n > 1) throw StoreError(kErrInvalidArgument, "dst stride below the page size");
   std::lock_guard<std::mutex> g(mu_);
+  gather_locked(keys, n, dst, dst_stride, slot_out, len_out, (hipStream_t)stream);
+}
+
+void DevicePageCache::gather_locked(uint64_t keys, uint32_t n, uint64_t dst, uint64_t dst_stride,
+                                    uint64_t slot_out, uint64_t len_out, hipStream_t s) {
   const uint32_t epoch = ++epoch_;
   if (!use_device_) {
     const uint64_t* k = (const uint64_t*)keys;
@@ -379,13 +497,11 @@ void DevicePageCache::gather(uint64_t keys, uint32_t n, uint64_t dst, uint64_t d
     }
     return;
   }
-  hipStream_t s = (hipStream_t)stream;
   flush_table(s);
   PageGatherArgs a{table_d_, table_h_.size() - 1, (const uint64_t*)keys, n, (const uint8_t*)arena_, page_size_,
                    (uint8_t*)dst, dst_stride, (int32_t*)slot_out, (uint32_t*)len_out, stamps_d_, epoch};
   PC_HIP_OK(launch_page_lookup_gather(a, s));
-  PC_HIP_OK(hipEventRecord(last_gather_, s));
-  gather_pending_ = true;
+  track_reader(s);
   device_stamps_dirty_ = true;
 }
 
@@ -394,27 +510,34 @@ std::vector<int32_t> DevicePageCache::gather_host_keys(const std::vector<uint64_
   const uint32_t n = (uint32_t)keys.size();
   std::vector<int32_t> slots(n, -1);
   if (n == 0) return slots;
+  if (dst_stride < page_size_ && n > 1) throw StoreError(kErrInvalidArgument, "dst stride below the page size");
   if (!use_device_) {
     std::vector<uint32_t> lens(n);
     gather((uint64_t)keys.data(), n, dst, dst_stride, (uint64_t)slots.data(), (uint64_t)lens.data(), stream);
     return slots;
   }
   hipStream_t s = (hipStream_t)stream;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    if (n > keys_cap_) {
-      wait_gathers();
-      hipFree(keys_d_);
-      hipFree(slots_d_);
-      hipFree(lens_d_);
-      keys_cap_ = std::max<uint32_t>(n, 4096);
-      PC_HIP_OK(hipMalloc((void**)&keys_d_, keys_cap_ * sizeof(uint64_t)));
-      PC_HIP_OK(hipMalloc((void**)&slots_d_, keys_cap_ * sizeof(int32_t)));
-      PC_HIP_OK(hipMalloc((void**)&lens_d_, keys_cap_ * sizeof(uint32_t)));
-    }
-    PC_HIP_OK(hipMemcpyAsync(keys_d_, keys.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  // the scratch buffers are shared: upload, gather and read-back all happen under the lock
+  std::lock_guard<std::mutex> g(mu_);
+  if (n > keys_cap_) {
+    wait_gathers();
+    hipFree(keys_d_);
+    hipFree(slots_d_);
+    hipFree(lens_d_);
+    keys_d_ = nullptr;
+    slots_d_ = nullptr;
+    lens_d_ = nullptr;
+    keys_cap_ = 0;
+    const uint32_t cap = std::max<uint32_t>(n, 4096);
+    PC_HIP_OK(hipMalloc((void**)&keys_d_, cap * sizeof(uint64_t)));
+    PC_HIP_OK(hipMalloc((void**)&slots_d_, cap * sizeof(int32_t)));
+    PC_HIP_OK(hipMalloc((void**)&lens_d_, cap * sizeof(uint32_t)));
+    keys_cap_ = cap;
   }
-  gather((uint64_t)keys_d_, n, dst, dst_stride, (uint64_t)slots_d_, (uint64_t)lens_d_, stream);
+  // an earlier call's gather (another stream) may still read keys_d_
+  order_after_readers(s);
+  PC_HIP_OK(hipMemcpyAsync(keys_d_, keys.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  gather_locked((uint64_t)keys_d_, n, dst, dst_stride, (uint64_t)slots_d_, (uint64_t)lens_d_, s);
   PC_HIP_OK(hipMemcpyAsync(slots.data(), slots_d_, n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   PC_HIP_OK(hipStreamSynchronize(s));
   return slots;

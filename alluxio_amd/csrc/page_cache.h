@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "seg_ring.h"
 
 namespace amdx {
 
@@ -34,7 +35,10 @@ class DevicePageCache {
   // is set, least-recently-used pages are dropped first (returned); otherwise full -> throws.
   std::vector<uint64_t> put(uint64_t key, uint64_t src, uint64_t len, int src_kind, uint64_t stream, bool evict);
   // Store keys[i] <- src + i * src_stride (len bytes each; stride 0 repeats one page) with one
-  // batched copy launch; evicted keys are returned as for put().
+  // batched copy launch; evicted keys are returned as for put().  A key repeated in the batch
+  // keeps its last source (as sequential put() calls would).  All-or-nothing: with evict=false a
+  // batch that does not fit throws before anything changes, and a failed copy rolls back every
+  // page of the batch it had staged (those keys read as misses afterwards).
   std::vector<uint64_t> put_many(const std::vector<uint64_t>& keys, uint64_t src, uint64_t src_stride,
                                  uint64_t len, int src_kind, uint64_t stream, bool evict);
   bool erase(uint64_t key);
@@ -44,6 +48,16 @@ class DevicePageCache {
   uint64_t slot_ptr(int32_t slot) const { return arena_ + (uint64_t)slot * page_size_; }
   // Copy `len` bytes at `offset` of page `key` to dst (MemKind); false on a miss.
   bool read(uint64_t key, uint64_t offset, uint64_t len, uint64_t dst, int dst_kind, uint64_t stream);
+
+  // Copy byte ranges of cached pages: segment i copies lens[i] bytes at offsets[i] of page
+  // keys[i] to dsts[i] (MemKind dst_kind).  Slots are resolved and the copies launched (one
+  // batched launch for device destinations) under the cache lock and tracked like gathers, so no
+  // later put/evict can rewrite a slot before its copy ran.  Returns the indices that missed
+  // (page absent, or range beyond the page's valid bytes); those destinations are untouched.
+  // Device destinations: asynchronous on `stream`.  Host destinations: complete on return.
+  std::vector<int32_t> read_segments(const std::vector<uint64_t>& keys, const std::vector<uint64_t>& offsets,
+                                     const std::vector<uint64_t>& lens, const std::vector<uint64_t>& dsts,
+                                     int dst_kind, uint64_t stream);
 
   // Fused lookup + gather: keys/slot_out/len_out are device (or, host mode, host) arrays.
   void gather(uint64_t keys, uint32_t n, uint64_t dst, uint64_t dst_stride, uint64_t slot_out,
@@ -66,6 +80,10 @@ class DevicePageCache {
   void table_erase_at(uint64_t idx);
   void mark_dirty(uint64_t idx);
   void flush_table(hipStream_t stream);         // push dirty entries to the device copy
+  void gather_locked(uint64_t keys, uint32_t n, uint64_t dst, uint64_t dst_stride, uint64_t slot_out,
+                     uint64_t len_out, hipStream_t stream);
+  void track_reader(hipStream_t stream);         // record an event behind a slot reader
+  void order_after_readers(hipStream_t stream);  // stream waits for every tracked reader
   void rebuild_table();                          // drop tombstones
   std::vector<uint64_t> evict_lru(uint32_t need);
   void sync_device_stamps();
@@ -96,8 +114,10 @@ class DevicePageCache {
   int32_t* slots_d_ = nullptr;
   uint32_t* lens_d_ = nullptr;
   uint32_t keys_cap_ = 0;
-  hipEvent_t last_gather_ = nullptr;
-  bool gather_pending_ = false;
+  // outstanding slot readers (gathers, segment reads), one event each, any stream
+  std::vector<hipEvent_t> pending_ev_;
+  std::vector<hipEvent_t> ev_pool_;
+  SegRing ring_;                                 // descriptors of batched copies
   mutable std::mutex mu_;
 };
 

@@ -43,6 +43,8 @@ inline void bind_page_cache(pybind11::module_& m) {
              if (!hit) return py::none();
              return py::bytes(out);
            }, py::arg("key"), py::arg("offset"), py::arg("length"))
+      .def("read_segments", &DevicePageCache::read_segments, G(), py::arg("keys"), py::arg("offsets"),
+           py::arg("lengths"), py::arg("dsts"), py::arg("dst_kind"), py::arg("stream") = 0)
       .def("gather", &DevicePageCache::gather, G(), py::arg("keys"), py::arg("n"), py::arg("dst"),
            py::arg("dst_stride"), py::arg("slot_out"), py::arg("len_out"), py::arg("stream") = 0)
       .def("gather_host_keys", &DevicePageCache::gather_host_keys, G(), py::arg("keys"), py::arg("dst"),

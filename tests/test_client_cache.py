@@ -157,3 +157,26 @@ def _read_pages_body(tmp_path):
             n = int(lens[r])
             assert np.array_equal(host[r, :n], data[p * 4096:p * 4096 + n])
         fs.close()
+
+
+@pytest.mark.gpu
+def test_hbm_read_into_longer_than_cache(gpu, tmp_path):
+    """A read_into spanning more pages than the HBM cache holds: every group of pages is filled
+    and copied before the next group can evict it (slot reuse before the copy)."""
+    import torch
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"}) as c:
+        data = np.random.default_rng(5).integers(0, 256, 3_000_000, dtype=np.uint8)
+        c.client().write_file("/hc/big", data, write_type="MUST_CACHE")
+        from alluxio_amd.client.file_system import FileSystem
+        fs = FileSystem(conf=_conf(tmp_path, **{"alluxio.user.client.cache.store.type": "HBM",
+                                                "alluxio.user.client.cache.page.size": "64KB",
+                                                "alluxio.user.client.cache.size": "512KB"}),
+                        master_address=c.master.address)
+        out = torch.empty(2_900_000, dtype=torch.uint8, device="cuda")
+        for _ in range(2):
+            with fs.open_file("/hc/big") as f:
+                f.seek(33)
+                assert f.read_into(out) == 2_900_000
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), data[33:2_900_033])
+        fs.close()

@@ -131,6 +131,41 @@ def test_host_put_many_matches_put_and_evicts():
         assert pc.get_bytes(_key(5, i), 0, ps) == buf[2].tobytes()
 
 
+def test_host_put_many_is_atomic_and_dedups():
+    C = lib()
+    ps = 4096
+    pc = C.PageCache(0, 8 * ps, ps, False)
+    rng = np.random.default_rng(8)
+    buf = rng.integers(0, 256, (10, ps), dtype=np.uint8)
+    assert pc.put_many([_key(1, i) for i in range(6)], buf.ctypes.data, ps, ps, 0, 0, False) == []
+    # 4 new keys do not fit the 2 free slots: nothing changes
+    with pytest.raises(Exception):
+        pc.put_many([_key(2, i) for i in range(4)], buf.ctypes.data, ps, ps, 0, 0, False)
+    assert pc.used == 6 and not any(pc.contains(_key(2, i)) for i in range(4))
+    # a repeated key keeps its LAST source, and only takes one slot
+    assert pc.put_many([_key(3, 0), _key(3, 1), _key(3, 0)], buf.ctypes.data, ps, ps, 0, 0, False) == []
+    assert pc.used == 8
+    assert pc.get_bytes(_key(3, 0), 0, ps) == buf[2].tobytes()
+    assert pc.get_bytes(_key(3, 1), 0, ps) == buf[1].tobytes()
+
+
+def test_host_read_segments():
+    C = lib()
+    ps = 4096
+    pc = C.PageCache(0, 8 * ps, ps, False)
+    rng = np.random.default_rng(9)
+    buf = rng.integers(0, 256, (4, ps), dtype=np.uint8)
+    pc.put_many([_key(1, i) for i in range(4)], buf.ctypes.data, ps, ps, 0, 0, False)
+    pc.put_bytes(_key(1, 9), buf[0][:100], False)
+    out = np.zeros(3 * ps, dtype=np.uint8)
+    base = out.ctypes.data
+    missed = pc.read_segments([_key(1, 2), _key(1, 7), _key(1, 0), _key(1, 9)], [10, 0, 0, 50],
+                              [ps - 10, 5, ps, 60], [base, base + 4000, base + ps, base + 2 * ps], 0, 0)
+    assert missed == [1, 3]           # absent page; range past a short page's valid bytes
+    assert np.array_equal(out[:ps - 10], buf[2][10:]) and np.array_equal(out[ps:2 * ps], buf[0])
+    assert not out[2 * ps:].any()
+
+
 @pytest.mark.gpu
 def test_device_put_many_matches_torch(gpu):
     import torch
