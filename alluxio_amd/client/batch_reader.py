@@ -144,3 +144,98 @@ class RingStreamReader(MultiStreamReader):
     def last_call(self, s: int, k: int) -> tuple[int, int]:
         """(file offset, length) of stream ``s``'s ``k``-th call of the last step (0 length = EOF)."""
         return self.rs.last_call(s, k)
+
+
+class RemoteRingReader:
+    """:class:`RingStreamReader` whose source is ANOTHER same-node worker's memory.
+
+    Every block of the file is read-locked on worker ``address`` through ``OpenDeviceBlock`` (held
+    until :meth:`close`), the worker's arena is mapped into this process once — its HBM through
+    HIP IPC, so the device-cursor kernel running on *this* GPU reads the peer GPU's HBM over xGMI;
+    a shared DRAM arena through its memfd — and the file's page table is uploaded once.  Each step
+    is then one launch with O(1) host work, exactly like the local reader.  This is the
+    GPU-consumer form of a remote cached read (reference: a client reading a block from another
+    worker through RemoteBlockInStream / GrpcDataReader).
+    """
+
+    def __init__(self, fs, path: str, ring, address: str, start_offsets: list[int] | None = None):
+        import torch
+        from ..ops.native import has_gpu, lib, native_errors
+        from ..parallel.ipc import map_handle
+        from ..proto import pb
+        if ring.dim() != 3 or ring.dtype != torch.uint8 or not ring.is_contiguous():
+            raise ValueError("ring must be a contiguous uint8 tensor [streams, depth, buf]")
+        self.fs, self.path, self.ring, self.address = fs, path, ring, address
+        self.streams, self.depth, self.nbytes = (int(x) for x in ring.shape)
+        st = fs.get_status(path)
+        self.status = st
+        self.session = ids.create_session_id()
+        self.stub = fs.ctx.worker_stub(address)
+        dev = ring.device.index if ring.is_cuda else (torch.cuda.current_device() if has_gpu() else 0)
+        self._handles = []
+        try:
+            ftab, ps, arena_id, base = [], None, None, None
+            nblocks = len(st.fileBlockInfos)
+            for i, fbi in enumerate(st.fileBlockInfos):
+                h = self.stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(
+                    block_id=fbi.blockInfo.blockId, session_id=self.session, reader_gpu=(dev + 1) if has_gpu() else 0))
+                self._handles.append(h)
+                ident = (h.arena_kind, bytes(h.arena_ipc_handle), h.pid, h.host_fd, h.arena_offset)
+                if arena_id is None:
+                    arena_id, ps, base = ident, h.page_size, map_handle(h, dev)
+                elif ident != arena_id or h.page_size != ps:
+                    raise UnavailableException(f"{path}: blocks live in different arenas of {address}")
+                np_ = -(-h.length // ps)
+                if i + 1 < nblocks and h.length % ps:
+                    raise UnavailableException(f"{path}: block size is not a multiple of the page size")
+                ftab.extend(list(h.pages)[:np_])
+            kind = DEVICE if ring.is_cuda else HOST
+            with native_errors():
+                self.rs = lib().RingReadSession.remote(
+                    base, ftab, ps, st.length, dev if has_gpu() else -1, ring.data_ptr(), self.depth * self.nbytes,
+                    self.nbytes, self.depth, self.streams, kind, list(start_offsets or []))
+        except Exception:
+            self._unlock_all()
+            raise
+        self._stream = torch.cuda.current_stream(ring.device) if ring.is_cuda else None
+        self.reopens = 0
+
+    def step(self) -> int:
+        from ..ops.native import native_errors
+        handle = int(self._stream.cuda_stream) if self._stream is not None else 0
+        with native_errors():
+            nbytes, eofs = self.rs.step(handle)
+        if eofs:
+            st = self.fs.get_status(self.path)     # reopen: cached metadata lookup
+            if st.length != self.status.length or list(st.block_ids) != list(self.status.block_ids):
+                raise UnavailableException(f"{self.path} changed while being read")
+            self.reopens += eofs
+        return nbytes
+
+    def last_call(self, s: int, k: int) -> tuple[int, int]:
+        return self.rs.last_call(s, k)
+
+    @property
+    def total_bytes(self) -> int:
+        return self.rs.total_bytes
+
+    def _unlock_all(self) -> None:
+        from ..proto import pb
+        for h in self._handles:
+            try:
+                self.stub.UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(
+                    block_id=h.block_id, lock_id=h.lock_id, session_id=self.session))
+            except Exception:  # noqa: BLE001 - the worker expires the session's locks itself
+                pass
+        self._handles = []
+
+    def close(self) -> None:
+        if getattr(self, "rs", None) is not None:
+            self.rs.close()
+        self._unlock_all()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

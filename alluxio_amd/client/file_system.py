@@ -182,7 +182,8 @@ class FileSystem:
         p = _path(path)
         info = self._fs.CreateFile(pb.file.CreateFilePRequest(path=p, options=o)).fileInfo
         self._invalidate(p)
-        return FileOutStream(self.ctx, info, wt, replication_durable, write_tier, medium, persistence_wait_ms)
+        return FileOutStream(self.ctx, info, wt, replication_durable, write_tier, medium, persistence_wait_ms,
+                             replication_min=replication_min)
 
     def delete(self, path, recursive=False, alluxio_only=False, unchecked=False) -> None:
         p = _path(path)

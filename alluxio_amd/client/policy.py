@@ -25,6 +25,7 @@ def _free(w) -> int:
 class LocalFirstPolicy(BlockLocationPolicy):
     def get_worker(self, workers, block_id, block_size, context=None):
         local = [w for w in workers if context is not None and context.is_local(w.address)]
+        inproc = []
         if context is not None:
             inproc = [w for w in local if context.in_process_worker(w.address) is not None]
             if inproc:
@@ -33,6 +34,10 @@ class LocalFirstPolicy(BlockLocationPolicy):
         local = sorted(local, key=lambda w: (w.address.host, w.address.rpcPort))
         cands = [w for w in local if _free(w) >= block_size] or local
         if cands:
+            if not inproc and len(cands) > 1:
+                # no worker in this process (e.g. picking replicas of a block whose primary is
+                # ours): spread blocks over the node's GPU workers so every xGMI link carries load
+                return cands[(block_id * 0x9E3779B97F4A7C15 >> 17) % len(cands)]
             return cands[0]
         fit = [w for w in workers if _free(w) >= block_size]
         return random.choice(fit or workers) if workers else None

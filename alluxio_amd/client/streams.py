@@ -25,7 +25,8 @@ import numpy as np
 from ..proto import enum_name, pb
 from ..rpc import marshal
 from ..utils import ids
-from ..utils.exceptions import (AlluxioStatusException, NotFoundException, UnavailableException)
+from ..utils.exceptions import (AlluxioStatusException, NotFoundException, ResourceExhaustedException,
+                                UnavailableException)
 from .context import SVC_WORKER, FileSystemContext, worker_address_str
 
 LOG = logging.getLogger(__name__)
@@ -198,8 +199,9 @@ class GrpcBlockReader(BlockReader):
 
 
 class IpcBlockReader(BlockReader):
-    """Short-circuit read of a block in a same-node worker's HBM arena via HIP IPC
-    (the device analogue of LocalFileDataReader; see alluxio_amd/parallel/ipc.py)."""
+    """Short-circuit read of a block held by a same-node worker process: its HBM arena mapped via
+    HIP IPC, or its shared DRAM arena mapped via memfd (the analogue of LocalFileDataReader's
+    mmap; see alluxio_amd/parallel/ipc.py)."""
 
     source = "ipc"
 
@@ -211,18 +213,29 @@ class IpcBlockReader(BlockReader):
         self.session = session
         self.stub = ctx.worker_stub(address)
         self.h = self.stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session))
-        if not self.h.arena_ipc_handle:
+        from ..ops.native import has_gpu
+        self.device = torch.cuda.current_device() if has_gpu() else 0
+        try:
+            from ..parallel.ipc import map_handle
+            map_handle(self.h, self.device)
+        except Exception as e:
             self.close()
-            raise UnavailableException(f"worker {address} did not export block {block_id} over IPC")
+            raise UnavailableException(f"worker {address} did not share block {block_id}: {e}") from e
         self.length = self.h.length
-        self.device = torch.cuda.current_device()
 
     def read_into(self, offset, length, ptr, kind, stream=0):
-        from ..parallel.ipc import gather_block
+        from ..ops.native import has_gpu
+        from ..parallel.ipc import gather_block, map_handle, page_segments
         if kind == DEVICE:
             gather_block(self.h, offset, length, ptr, self.device, stream)
             return
         import ctypes
+        if self.h.arena_kind == "dram" or not has_gpu():
+            # shared host arena -> host buffer: plain memcpy of the page runs
+            base = map_handle(self.h, self.device)
+            for src, dst, n in page_segments(base, list(self.h.pages), self.h.page_size, offset, length, ptr):
+                ctypes.memmove(dst, src, n)
+            return
         import torch
         tmp = torch.empty(length, dtype=torch.uint8, device=torch.device("cuda", self.device))
         gather_block(self.h, offset, length, tmp.data_ptr(), self.device, stream)
@@ -416,8 +429,7 @@ class FileInStream(io.RawIOBase):
         if not self.ctx.conf.get_bool("alluxio.worker.ipc.enabled", "true") or \
                 not self.ctx.conf.get_bool("alluxio.user.short.circuit.enabled", "true"):
             return False
-        from ..ops.native import has_gpu
-        return has_gpu()
+        return True
 
     def _maybe_passive_cache(self, block_id: int, source_addr, length: int) -> None:
         if not self.passive_cache or self.read_type == "NO_CACHE":
@@ -601,8 +613,20 @@ class UfsWriter:
 
 
 class FileOutStream(io.RawIOBase):
+    """Writes a file block by block to the chosen worker(s) and/or the UFS.
+
+    Replicated writes (reference AlluxioBlockStore.getOutStream, AlluxioBlockStore.java:281-339,
+    and BlockOutStream.createReplicatedBlockOutStream, BlockOutStream.java:109-134): the number of
+    initial copies is ``replication_durable`` for ASYNC_THROUGH (when above ``replication_min``),
+    else ``replication_min``.  The reference streams every byte to each replica.  Here, when the
+    replicas share a node with the first (primary) worker, only the primary receives the bytes and
+    the other replicas *pull* each finished block out of the primary's arena at commit — over xGMI
+    between GPU workers (``PeerTransfer`` -> :func:`alluxio_amd.parallel.peer.pull_block`), all
+    replicas in parallel.  Replicas on other nodes get their own gRPC block stream, as before.
+    """
+
     def __init__(self, ctx: FileSystemContext, status, write_type: str, replication_durable: int = 1,
-                 write_tier: int = 0, medium: str = "", persistence_wait_ms: int = 0):
+                 write_tier: int = 0, medium: str = "", persistence_wait_ms: int = 0, replication_min: int = 0):
         super().__init__()
         self.ctx = ctx
         self.status = status
@@ -615,7 +639,12 @@ class FileOutStream(io.RawIOBase):
         self.persistence_wait_ms = persistence_wait_ms
         self.cache = write_type in ("MUST_CACHE", "CACHE_THROUGH", "ASYNC_THROUGH", "TRY_CACHE")
         self.through = write_type in ("CACHE_THROUGH", "THROUGH")
-        self.replicas = replication_durable if write_type == "ASYNC_THROUGH" and replication_durable > 1 else 1
+        rmin = max(1, replication_min or 0)
+        self.replicas = (replication_durable if write_type == "ASYNC_THROUGH" and replication_durable > rmin
+                         else rmin)
+        self._fanout: list[str] = []        # same-node replicas that pull each block from the primary
+        self._primary_addr = None
+        self._block_id = None
         from .policy import create_policy
         self.policy = create_policy(ctx.conf.get("alluxio.user.block.write.location.policy.class"), ctx.conf)
         self._writers: list[BlockWriter] = []
@@ -681,7 +710,18 @@ class FileOutStream(io.RawIOBase):
             cands = [c for c in cands if worker_address_str(c.address) != worker_address_str(w.address)]
         if not chosen:
             raise UnavailableException("no worker available to write the block")
+        if self.replicas > 1 and len(chosen) < self.replicas:
+            raise ResourceExhaustedException(f"Not enough workers for replications, {len(chosen)} workers "
+                                             f"selected but {self.replicas} required")
         reserve = min(self.block_size, self.ctx.conf.get_bytes("alluxio.user.file.buffer.bytes", "8MB"))
+        self._fanout = []
+        self._primary_addr = worker_address_str(chosen[0].address)
+        self._block_id = bid
+        if len(chosen) > 1 and self.ctx.conf.get_bool("alluxio.user.block.replication.peer.pull.enabled", "true"):
+            prim_host = chosen[0].address.host
+            pullers = [w for w in chosen[1:] if w.address.host == prim_host and self.ctx.is_local(w.address)]
+            self._fanout = [worker_address_str(w.address) for w in pullers]
+            chosen = [chosen[0]] + [w for w in chosen[1:] if w not in pullers]
         for w in chosen:
             lw = self.ctx.in_process_worker(w.address)
             if lw is not None:
@@ -695,7 +735,15 @@ class FileOutStream(io.RawIOBase):
     def _finish_block(self) -> None:
         for w in self._writers:
             w.commit()
+        had = bool(self._writers)
         self._writers = []
+        if had and self._fanout:
+            from ..parallel.peer import fan_out
+            errors = fan_out(self._primary_addr, self._fanout, self._block_id, self._block_written,
+                             self.ctx.worker_stub)
+            self._fanout = []
+            if errors:
+                raise UnavailableException(f"replicating block {self._block_id} failed: {errors}")
 
     def cancel(self) -> None:
         self._canceled = True

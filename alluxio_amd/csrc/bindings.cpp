@@ -11,6 +11,7 @@
 #include "ipc.h"
 #include "ring_read.h"
 #include "kernels.h"
+#include "seg_ring.h"
 
 namespace py = pybind11;
 using namespace amdx;
@@ -73,22 +74,32 @@ std::vector<int32_t> lz4_device(const std::vector<std::tuple<uint64_t, uint64_t,
   return sizes;
 }
 
+// Process-wide descriptor ring for ad-hoc batched copies (IPC reads, peer pulls): no per-call
+// hipMalloc/hipFree (hipFree may synchronize the device).  Without a HIP device the segments are
+// plain host memory and are copied with memcpy (CPU builds, shared-memory DRAM arenas).
+SegRing& global_ring() {
+  static SegRing* r = [] {
+    auto* x = new SegRing();
+    x->init();
+    return x;
+  }();
+  return *r;
+}
+
 void batched_copy(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>>& segs, uint64_t stream, bool sync) {
   const size_t n = segs.size();
   if (!n) return;
-  std::vector<CopySeg> h(n);
-  uint64_t chunks = 0;
-  for (size_t i = 0; i < n; ++i) {
-    h[i] = CopySeg{std::get<0>(segs[i]), std::get<1>(segs[i]), std::get<2>(segs[i]), chunks};
-    chunks += (h[i].bytes + kCopyChunk - 1) / kCopyChunk;
+  if (hip_device_count() == 0) {
+    for (const auto& t : segs)
+      std::memmove(reinterpret_cast<void*>(std::get<1>(t)), reinterpret_cast<const void*>(std::get<0>(t)),
+                   std::get<2>(t));
+    return;
   }
-  DevBuf d(sizeof(CopySeg) * n);
+  std::vector<CopySeg> h(n);
+  for (size_t i = 0; i < n; ++i) h[i] = CopySeg{std::get<0>(segs[i]), std::get<1>(segs[i]), std::get<2>(segs[i]), 0};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  HIP_CHECK(hipMemcpyAsync(d.p, h.data(), sizeof(CopySeg) * n, hipMemcpyHostToDevice, st));
-  HIP_CHECK(launch_batched_copy((const CopySeg*)d.p, (int)n, chunks, st));
-  // the descriptor buffer is freed on return: always wait for the launch
-  HIP_CHECK(hipStreamSynchronize(st));
-  (void)sync;
+  HIP_CHECK(global_ring().launch(h, st));
+  if (sync) HIP_CHECK(hipStreamSynchronize(st));
 }
 
 py::tuple evict_select_device(const std::vector<float>& crf, const std::vector<uint64_t>& last,
@@ -304,6 +315,17 @@ PYBIND11_MODULE(_C, m) {
            py::arg("store"), py::arg("session"), py::arg("block_ids"), py::arg("block_lens"), py::arg("dst_base"),
            py::arg("stream_stride"), py::arg("buf_bytes"), py::arg("depth"), py::arg("streams"),
            py::arg("dst_kind"), py::arg("start_offsets") = std::vector<uint64_t>{}, py::keep_alive<1, 2>())
+      .def_static("remote", [](uint64_t arena, const std::vector<int64_t>& pages, uint64_t page_size, uint64_t file_len,
+                               int device, uint64_t dst_base, uint64_t stride, uint64_t buf, uint32_t depth,
+                               uint32_t streams, int kind, const std::vector<uint64_t>& starts) {
+             py::gil_scoped_release rel;
+             return std::unique_ptr<RingReadSession>(new RingReadSession(arena, pages, page_size, file_len, device,
+                                                                         dst_base, stride, buf, depth, streams,
+                                                                         kind, starts));
+           },
+           py::arg("arena_base"), py::arg("file_pages"), py::arg("page_size"), py::arg("file_len"), py::arg("device"),
+           py::arg("dst_base"), py::arg("stream_stride"), py::arg("buf_bytes"), py::arg("depth"), py::arg("streams"),
+           py::arg("dst_kind"), py::arg("start_offsets") = std::vector<uint64_t>{})
       .def("step", [](RingReadSession& r, uint64_t stream) {
              uint64_t eofs = 0, n;
              {
@@ -335,6 +357,15 @@ PYBIND11_MODULE(_C, m) {
         }, py::arg("handle"), py::arg("device"));
   m.def("ipc_close", [](uint64_t base) { py::gil_scoped_release rel; ipc_close(base); });
   m.def("enable_peer_access", &enable_peer_access, py::arg("device"), py::arg("peer"));
+  // page-lock an existing host mapping (shared-memory DRAM arenas) so kernels can read it
+  m.def("host_register", [](uint64_t ptr, uint64_t n) {
+          if (hip_device_count() == 0) return false;
+          HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(ptr), n, hipHostRegisterMapped));
+          return true;
+        }, py::arg("ptr"), py::arg("nbytes"));
+  m.def("host_unregister", [](uint64_t ptr) {
+          if (hip_device_count() > 0) (void)hipHostUnregister(reinterpret_cast<void*>(ptr));
+        }, py::arg("ptr"));
   m.def("can_access_peer", &can_access_peer, py::arg("device"), py::arg("peer"));
   m.def("crc32c", [](py::bytes data, uint32_t crc) {
           std::string s = data;

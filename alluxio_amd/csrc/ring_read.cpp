@@ -25,14 +25,8 @@ RingReadSession::RingReadSession(BlockStore* store, int64_t session, const std::
       dst_(dst_base), depth_(depth), streams_(streams), kind_(dst_kind) {
   if (block_ids.size() != block_lens.size() || block_ids.empty())
     throw StoreError(kErrInvalidArgument, "ring read: bad block list");
-  if (buf_ == 0 || depth_ == 0 || streams_ == 0 || streams_ > kSeqReadMaxStreams)
-    throw StoreError(kErrInvalidArgument, "ring read: bad buffer/depth/stream count");
-  if (stride_ < (uint64_t)depth_ * buf_) throw StoreError(kErrInvalidArgument, "ring read: stride too small");
   for (uint64_t l : block_lens) file_len_ += l;
-  if (file_len_ == 0) throw StoreError(kErrInvalidArgument, "ring read: empty file");
-  const uint64_t calls = (file_len_ + buf_ - 1) / buf_;
-  if (calls + 1 >= (1ull << 32)) throw StoreError(kErrInvalidArgument, "ring read: too many calls per pass");
-  cycle_ = (uint32_t)(calls + 1);
+  check_shape();
   // lock every block (read) and build the file page table
   try {
     for (size_t b = 0; b < blocks_.size(); ++b) {
@@ -57,27 +51,61 @@ RingReadSession::RingReadSession(BlockStore* store, int64_t session, const std::
       if (pages.size() < np) throw StoreError(kErrInvalidState, "ring read: block shorter than its length");
       ftab_.insert(ftab_.end(), pages.begin(), pages.begin() + np);
     }
+    on_device_ = store_->has_device();
+    finish_init(start_offsets);
   } catch (...) {
     for (int64_t l : locks_) store_->unlock(l);
     locks_.clear();
     throw;
   }
+}
+
+RingReadSession::RingReadSession(uint64_t arena_base, const std::vector<int64_t>& file_pages, uint64_t page_size,
+                                 uint64_t file_len, int device, uint64_t dst_base, uint64_t stream_stride,
+                                 uint64_t buf_bytes, uint32_t depth, uint32_t streams, int dst_kind,
+                                 const std::vector<uint64_t>& start_offsets)
+    : store_(nullptr), session_(0), file_len_(file_len), buf_(buf_bytes), stride_(stream_stride), dst_(dst_base),
+      depth_(depth), streams_(streams), kind_(dst_kind), on_device_(device >= 0), device_(device),
+      page_size_(page_size), arena_(arena_base), ftab_(file_pages) {
+  check_shape();
+  if (page_size_ == 0 || (page_size_ & (page_size_ - 1)))
+    throw StoreError(kErrInvalidArgument, "ring read: page size must be a power of two");
+  while ((1ull << page_shift_) < page_size_) ++page_shift_;
+  if (ftab_.size() < (file_len_ + page_size_ - 1) / page_size_)
+    throw StoreError(kErrInvalidArgument, "ring read: page table shorter than the file");
+  finish_init(start_offsets);
+}
+
+void RingReadSession::check_shape() {
+  if (buf_ == 0 || depth_ == 0 || streams_ == 0 || streams_ > kSeqReadMaxStreams)
+    throw StoreError(kErrInvalidArgument, "ring read: bad buffer/depth/stream count");
+  if (stride_ < (uint64_t)depth_ * buf_) throw StoreError(kErrInvalidArgument, "ring read: stride too small");
+  if (file_len_ == 0) throw StoreError(kErrInvalidArgument, "ring read: empty file");
+  const uint64_t calls = (file_len_ + buf_ - 1) / buf_;
+  if (calls + 1 >= (1ull << 32)) throw StoreError(kErrInvalidArgument, "ring read: too many calls per pass");
+  cycle_ = (uint32_t)(calls + 1);
+}
+
+void RingReadSession::set_device() const {
+  if (store_) store_->use_device();
+  else if (device_ >= 0) RR_HIP(hipSetDevice(device_));
+}
+
+void RingReadSession::finish_init(const std::vector<uint64_t>& start_offsets) {
   c_init_.assign(streams_, 0);
   for (uint32_t s = 0; s < streams_ && s < start_offsets.size(); ++s) {
     if (start_offsets[s] % buf_) throw StoreError(kErrInvalidArgument, "ring read: start offsets must be buffer aligned");
     c_init_[s] = std::min<uint64_t>(start_offsets[s] / buf_, cycle_ - 1);
   }
-  const DirSpec spec = store_->dir_spec(dir_);
-  if (store_->has_device()) {
+  if (on_device_) {
     if (buf_ & 15 || stride_ & 15 || dst_ & 15)
       throw StoreError(kErrInvalidArgument, "ring read: buffer size, stride and ring base must be 16-byte aligned");
-    store_->use_device();
+    set_device();
     RR_HIP(hipMalloc((void**)&d_ftab_, ftab_.size() * sizeof(int64_t)));
     RR_HIP(hipMalloc((void**)&d_cinit_, c_init_.size() * sizeof(uint64_t)));
     RR_HIP(hipMemcpy(d_ftab_, ftab_.data(), ftab_.size() * sizeof(int64_t), hipMemcpyHostToDevice));
     RR_HIP(hipMemcpy(d_cinit_, c_init_.data(), c_init_.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
   }
-  (void)spec;
 }
 
 RingReadSession::~RingReadSession() {
@@ -96,7 +124,7 @@ void RingReadSession::close() {
   d_cinit_ = nullptr;
   for (int64_t l : locks_) {
     try {
-      store_->unlock(l);
+      if (store_) store_->unlock(l);
     } catch (...) {
     }
   }
@@ -111,8 +139,8 @@ uint64_t RingReadSession::bytes_before(uint64_t g) const {
 uint64_t RingReadSession::step(uint64_t stream, uint64_t* eofs) {
   if (closed_) throw StoreError(kErrInvalidState, "ring read session closed");
   const uint64_t base = calls_per_stream_;
-  if (store_->has_device()) {
-    store_->use_device();
+  if (on_device_) {
+    set_device();
     SeqReadArgs a;
     a.arena = reinterpret_cast<const uint8_t*>(arena_);
     a.ftab = d_ftab_;
@@ -160,7 +188,7 @@ uint64_t RingReadSession::step(uint64_t stream, uint64_t* eofs) {
   calls_per_stream_ += depth_;
   total_ += bytes;
   reopens_ += eof;
-  store_->access_blocks(blocks_);
+  if (store_) store_->access_blocks(blocks_);
   if (eofs) *eofs = eof;
   return bytes;
 }

@@ -20,6 +20,13 @@ class RingReadSession {
                   const std::vector<uint64_t>& block_lens, uint64_t dst_base, uint64_t stream_stride,
                   uint64_t buf_bytes, uint32_t depth, uint32_t streams, int dst_kind,
                   const std::vector<uint64_t>& start_offsets);
+  // Remote (peer) form: the file's pages live in an arena that is already addressable from this
+  // process (a peer worker's HBM mapped through HIP IPC, read over xGMI by the kernel running on
+  // `device`), described by `file_pages` (arena page index per file page).  Block locks are held
+  // by the caller (OpenDeviceBlock) for the session's lifetime.  device < 0: host arena (tests).
+  RingReadSession(uint64_t arena_base, const std::vector<int64_t>& file_pages, uint64_t page_size,
+                  uint64_t file_len, int device, uint64_t dst_base, uint64_t stream_stride, uint64_t buf_bytes,
+                  uint32_t depth, uint32_t streams, int dst_kind, const std::vector<uint64_t>& start_offsets);
   ~RingReadSession();
   // One launch: every stream issues `depth` read calls.  Returns bytes read; *eofs = EOF calls
   // (reopens) in this step.
@@ -36,12 +43,17 @@ class RingReadSession {
 
  private:
   uint64_t bytes_before(uint64_t g) const;  // bytes read by calls [0, g) of one stream
-  BlockStore* store_;
+  void check_shape();
+  void finish_init(const std::vector<uint64_t>& start_offsets);
+  void set_device() const;
+  BlockStore* store_;                       // null for the remote form
   int64_t session_;
   std::vector<int64_t> blocks_, locks_;
   uint64_t file_len_ = 0, buf_, stride_, dst_;
   uint32_t depth_, streams_, cycle_;
   int kind_;
+  bool on_device_ = false;
+  int device_ = -1;
   int dir_ = -1;
   uint64_t page_size_ = 0, arena_ = 0;
   uint32_t page_shift_ = 0;

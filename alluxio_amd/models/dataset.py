@@ -106,22 +106,26 @@ class DeviceBatchLoader:
                         self._locks.append((w, w.lock_block(self.session, b.blockId)))
                         chosen = ("local", w)
                         break
-                if chosen[0] == "stream" and self.device.type == "cuda":
+                # same-node holder: map its arena (HBM via HIP IPC, DRAM via shared memory) and
+                # gather with the copy kernel (host memcpy without a GPU)
+                from ..ops.native import has_gpu
+                if chosen[0] == "stream" and (self.device.type == "cuda" or not has_gpu()):
                     for loc in b.locations:
                         if not ctx.is_local(loc.workerAddress):
                             continue
                         try:
                             from ..client.context import worker_address_str
-                            from ..parallel.ipc import MAPPINGS
+                            from ..parallel.ipc import map_handle
                             from ..proto import pb
                             stub = ctx.worker_stub(worker_address_str(loc.workerAddress))
                             h = stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=b.blockId,
                                                                                      session_id=self.session))
-                            if not h.arena_ipc_handle:
+                            try:
+                                base = map_handle(h, self.device.index or 0)
+                            except Exception:
                                 stub.UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(
                                     block_id=b.blockId, lock_id=h.lock_id, session_id=self.session))
-                                continue
-                            base = MAPPINGS.open(h.arena_ipc_handle, self.device.index or 0) + h.arena_offset
+                                raise
                             self._locks.append((stub, h))
                             chosen = ("ipc", (h, base))
                             break

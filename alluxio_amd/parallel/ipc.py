@@ -57,6 +57,70 @@ class IpcMappings:
 MAPPINGS = IpcMappings()
 
 
+# Shared DRAM arenas of THIS process: (pid, fd) -> base address (no self-mapping needed).
+_LOCAL_SHARED: dict[tuple[int, int], int] = {}
+
+
+def register_local_shared(fd: int, base: int) -> None:
+    import os
+    _LOCAL_SHARED[(os.getpid(), fd)] = base
+
+
+class ShmMappings:
+    """Per-process cache of shared DRAM arenas of other local worker processes, mapped through
+    ``/proc/<pid>/fd/<fd>`` and page-locked for the GPU when one is present."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._maps: dict[tuple[int, int], tuple[object, int, bool]] = {}
+
+    def open(self, pid: int, fd: int, nbytes: int) -> int:
+        local = _LOCAL_SHARED.get((pid, fd))
+        if local is not None:
+            return local
+        import ctypes
+        import mmap
+        import os
+        with self._lock:
+            got = self._maps.get((pid, fd))
+            if got is not None:
+                return got[1]
+            f = os.open(f"/proc/{pid}/fd/{fd}", os.O_RDWR)
+            try:
+                mm = mmap.mmap(f, nbytes, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+            finally:
+                os.close(f)
+            base = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+            registered = bool(lib().host_register(base, nbytes)) if nbytes else False
+            self._maps[(pid, fd)] = (mm, base, registered)
+            return base
+
+    def close_all(self) -> None:
+        with self._lock:
+            for mm, base, registered in self._maps.values():
+                if registered:
+                    lib().host_unregister(base)
+            # ctypes views pin the mmap objects; they are released with the process
+            self._maps.clear()
+
+
+SHM = ShmMappings()
+
+
+def map_handle(h, device: int) -> int:
+    """Address, in this process, of the first byte of the arena a ``DeviceBlockHandle`` describes
+    (page ``p`` of the block starts at ``base + p * page_size``).  HBM arenas are opened through
+    HIP IPC on ``device`` (peer HBM is then read over xGMI by kernels on ``device``); shared DRAM
+    arenas are mmap'ed.  Raises ``RuntimeError`` when the handle carries neither."""
+    if getattr(h, "arena_kind", "") == "dram":
+        if h.host_fd < 0:
+            raise RuntimeError(f"block {h.block_id}: DRAM arena not shared")
+        return SHM.open(h.pid, h.host_fd, h.arena_bytes) + h.arena_offset
+    if not h.arena_ipc_handle:
+        raise RuntimeError(f"block {h.block_id}: worker did not export an IPC handle")
+    return MAPPINGS.open(h.arena_ipc_handle, device) + h.arena_offset
+
+
 def page_segments(src_base: int, pages, page_size: int, offset: int, length: int, dst_ptr: int):
     """Copy segments (src, dst, bytes) for bytes [offset, offset+length) of a paged block,
     merging physically adjacent pages into one segment."""
@@ -81,9 +145,7 @@ def gather_block(handle_msg, offset: int, length: int, dst_ptr: int, device: int
     memory of ``device``) with one batched-copy launch; returns bytes copied."""
     if offset < 0 or offset + length > handle_msg.length:
         raise ValueError(f"range [{offset}, {offset + length}) outside block of {handle_msg.length} bytes")
-    if not handle_msg.arena_ipc_handle:
-        raise RuntimeError("worker did not export an IPC handle for this block")
-    base = MAPPINGS.open(handle_msg.arena_ipc_handle, device) + handle_msg.arena_offset
+    base = map_handle(handle_msg, device)
     segs = page_segments(base, list(handle_msg.pages), handle_msg.page_size, offset, length, dst_ptr)
     lib().batched_copy(segs, stream, True)
     return length

@@ -1,0 +1,174 @@
+"""Worker-to-worker block pulls on one node, with failure handling.
+
+Reference: a worker caches a block held by another worker by streaming it through the peer's
+``ReadBlock`` gRPC service (core/server/worker/src/main/java/alluxio/worker/block/RemoteBlockReader.java,
+AsyncCacheRequestManager.java:213-240); replicated writes stream the bytes to every replica
+(core/client/fs/src/main/java/alluxio/client/block/stream/BlockOutStream.java:109-134).
+
+Here the destination worker *pulls* the block straight out of the source worker's memory:
+
+1. ``OpenDeviceBlock`` on the source read-locks the block and returns its page list plus a way to
+   map the arena — a HIP IPC handle for HBM, ``(pid, memfd)`` for a shared DRAM arena;
+2. the destination reserves its own pages (``BlockStore.external_write``) and runs the batched
+   copy kernel on ITS GPU, reading the peer's HBM over xGMI (or host memory; memcpy on CPU builds);
+3. commit, then ``UnlockDeviceBlock``.
+
+No payload crosses the RPC channel.  Failures are handled the way SURVEY §5.3 asks for the GPU
+plane: every control RPC has a deadline, a peer whose mapped pull failed is marked for a cooldown
+(``alluxio.worker.peer.failure.cooldown``) during which its blocks come through the gRPC block
+stream instead, and an aborted pull always releases both the destination's temp block and the
+source's read lock.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import time
+
+from ..proto import pb
+from ..utils import ids
+
+LOG = logging.getLogger(__name__)
+
+_fail_lock = threading.Lock()
+_failed_until: dict[tuple[int, str], float] = {}   # (worker id, peer address) -> monotonic deadline
+
+
+def _cooldown_s(worker) -> float:
+    return worker.conf.get_ms("alluxio.worker.peer.failure.cooldown", "30sec") / 1000.0
+
+
+def _rpc_timeout_s(worker) -> float:
+    return worker.conf.get_ms("alluxio.worker.peer.rpc.timeout", "30sec") / 1000.0
+
+
+def mark_failed(worker, addr: str) -> None:
+    with _fail_lock:
+        _failed_until[(id(worker), addr)] = time.monotonic() + _cooldown_s(worker)
+    worker.metrics.counter("PeerPullFailures").inc()
+
+
+def peer_failed(worker, addr: str) -> bool:
+    with _fail_lock:
+        t = _failed_until.get((id(worker), addr))
+        if t is None:
+            return False
+        if time.monotonic() >= t:
+            del _failed_until[(id(worker), addr)]
+            return False
+        return True
+
+
+def clear_failures(worker=None) -> None:
+    with _fail_lock:
+        if worker is None:
+            _failed_until.clear()
+        else:
+            for k in [k for k in _failed_until if k[0] == id(worker)]:
+                del _failed_until[k]
+
+
+def _my_gpu(worker) -> int:
+    """This worker's device index + 1 (0 = no GPU): the ``reader_gpu`` of OpenDeviceBlock."""
+    from ..ops.native import has_gpu
+    return (int(worker.store.device) + 1) if has_gpu() else 0
+
+
+def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "") -> int:
+    """Pull ``block_id`` from same-node worker ``addr`` by mapping its arena; returns bytes."""
+    from ..ops.native import has_gpu, lib
+    from .ipc import map_handle
+    from .transfer import cross_page_segments
+    stub = worker.peer_stub(addr)
+    session = ids.create_session_id()
+    timeout = _rpc_timeout_s(worker)
+    h = stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session,
+                                                             reader_gpu=_my_gpu(worker)), timeout=timeout)
+    try:
+        n = h.length
+        dev = int(worker.store.device)
+        src_base = map_handle(h, dev)
+        worker.create_block(session, block_id, tier, medium, max(n, 1))
+        try:
+            dst_pages = worker.native.external_write(session, block_id, 0, n)
+            _p, _d, dps, dbase = worker.native.block_pages(block_id)
+            segs = cross_page_segments(src_base, list(h.pages), h.page_size, dbase, list(dst_pages), dps, 0, n)
+            if has_gpu():
+                import torch
+                with torch.cuda.device(dev):   # the copy kernel runs on THIS worker's GPU, reading the peer
+                    lib().batched_copy(segs, 0, True)
+            else:
+                lib().batched_copy(segs, 0, True)
+            if h.crc32c and worker.conf.get_bool("alluxio.worker.peer.verify.crc", "true"):
+                worker.verify_block_crc(block_id, list(h.crc32c), h.page_size)
+            worker.commit_block(session, block_id)
+        except Exception:
+            worker.abort_block(session, block_id)
+            raise
+    finally:
+        try:
+            stub.UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(block_id=block_id, lock_id=h.lock_id,
+                                                                     session_id=session), timeout=timeout)
+        except Exception:  # noqa: BLE001 - the source expires the session's locks itself
+            LOG.warning("unlock of block %d on %s failed", block_id, addr, exc_info=True)
+    cross_gpu = h.arena_kind != "dram" and has_gpu() and int(h.device) != dev
+    worker.metrics.counter("XgmiBytesReceived" if cross_gpu else "PeerSharedBytesReceived").inc(n)
+    return n
+
+
+def pull_block(worker, block_id: int, addr: str, length: int, tier: int = 0, medium: str = "",
+               same_node: bool = True) -> int:
+    """Copy ``block_id`` from worker ``addr`` into ``worker``; returns the bytes moved (0 when it
+    already holds the block).  Same-node peers: mapped pull, falling back to the gRPC block
+    stream (and marking the peer) when that fails; other nodes: the gRPC block stream."""
+    if worker.has_block(block_id):
+        return 0
+    mapped_ok = (same_node and worker.conf.get_bool("alluxio.worker.ipc.enabled", "true")
+                 and not peer_failed(worker, addr))
+    if mapped_ok:
+        try:
+            return mapped_pull(worker, block_id, addr, tier, medium)
+        except Exception as e:  # noqa: BLE001
+            if worker.has_block(block_id):
+                return 0   # a concurrent pull won the race
+            LOG.warning("mapped pull of block %d from %s failed (%s); using the block stream", block_id, addr, e)
+            mark_failed(worker, addr)
+    from ..worker.remote import remote_block_fetcher
+    host, port = addr.rsplit(":", 1)
+    remote_block_fetcher(worker, host, int(port), length or None)(block_id)
+    worker.metrics.counter("PeerStreamBytesReceived").inc(length)
+    return length
+
+
+def fan_out(src_worker_addr: str, replica_addrs: list[str], block_id: int, length: int, stub_for,
+            timeout_s: float = 60.0) -> list[tuple[str, str]]:
+    """Ask every replica to pull ``block_id`` from ``src_worker_addr`` (``PeerTransfer``), all in
+    flight at once; returns ``[(replica, error)]`` for the ones that failed."""
+    errors: list[tuple[str, str]] = []
+    lock = threading.Lock()
+
+    def one(addr: str) -> None:
+        try:
+            r = stub_for(addr).PeerTransfer(pb.block.PeerTransferRequest(
+                block_id=block_id, length=length, src_address=src_worker_addr), timeout=timeout_s)
+            if not r.ok:
+                raise RuntimeError(r.message)
+        except Exception as e:  # noqa: BLE001
+            with lock:
+                errors.append((addr, str(e)))
+
+    threads = [threading.Thread(target=one, args=(a,), daemon=True) for a in replica_addrs[1:]]
+    for t in threads:
+        t.start()
+    if replica_addrs:
+        one(replica_addrs[0])
+    for t in threads:
+        t.join()
+    return errors
+
+
+def is_same_node(worker, host: str) -> bool:
+    import socket
+    mine = getattr(worker.address, "host", "127.0.0.1")
+    return host in ("127.0.0.1", "localhost", mine, socket.gethostname(), os.environ.get("ALLUXIO_NODE_HOST", "\0"))

@@ -114,43 +114,12 @@ class TransferPlane:
 
     # ---- on-demand pulls ------------------------------------------------------------------------
     def pull_block(self, block_id: int, src, length: int, tier: int = 0, medium: str = "") -> int:
-        """Copy ``block_id`` from peer worker ``src`` into this worker; returns bytes moved."""
-        if self.w.has_block(block_id):
-            return 0
+        """Copy ``block_id`` from peer worker ``src`` into this worker; returns bytes moved.
+        Mapped (xGMI / shared-memory) pull with gRPC fallback: see :mod:`.peer`."""
         if not self.can_reach(src):
             raise ValueError(f"worker {_addr_key(src)} is not a peer in this transfer group")
-        host, port = _addr_key(src).rsplit(":", 1)
-        if not self.device_plane:
-            from ..worker.remote import remote_block_fetcher
-            remote_block_fetcher(self.w, host, int(port), length)(block_id)
-            self.bytes_pulled += length
-            return length
-        from ..ops.native import lib
-        from .ipc import MAPPINGS
-        stub = self.w.peer_stub(_addr_key(src))
-        session = ids.create_session_id()
-        h = stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session))
-        try:
-            if not h.arena_ipc_handle:
-                raise RuntimeError(f"peer {_addr_key(src)} holds block {block_id} outside its HBM tier")
-            n = h.length
-            self.w.create_block(session, block_id, tier, medium, max(n, 1))
-            try:
-                dst_pages = self.w.native.external_write(session, block_id, 0, n)
-                _p, d, dps, dbase = self.w.native.block_pages(block_id)
-                import torch
-                dev = self.w.store.device
-                src_base = MAPPINGS.open(h.arena_ipc_handle, dev) + h.arena_offset
-                segs = cross_page_segments(src_base, list(h.pages), h.page_size, dbase, list(dst_pages), dps, 0, n)
-                with torch.cuda.device(dev):   # the copy kernel runs on this worker's GPU, reading the peer
-                    lib().batched_copy(segs, 0, True)
-                self.w.commit_block(session, block_id)
-            except Exception:
-                self.w.abort_block(session, block_id)
-                raise
-        finally:
-            stub.UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(block_id=block_id, lock_id=h.lock_id,
-                                                                     session_id=session))
+        from .peer import pull_block
+        n = pull_block(self.w, block_id, _addr_key(src), length, tier, medium, same_node=True)
         self.bytes_pulled += n
         return n
 

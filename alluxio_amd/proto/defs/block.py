@@ -41,12 +41,12 @@ msg ClearMetricsResponse
 msg PageRun first_page=1:i64 num_pages=2:i64
 msg DeviceBlockHandle block_id=1:i64 length=2:i64 page_size=3:i64 pages=4:i64*
     arena_ipc_handle=5:bytes arena_bytes=6:i64 device=7:i32 lock_id=8:i64 crc32c=9:u32*
-    node_id=10:str pid=11:i32 arena_offset=12:i64
-msg OpenDeviceBlockRequest block_id=1:i64 promote=2:bool session_id=3:i64
+    node_id=10:str pid=11:i32 arena_offset=12:i64 host_fd=13:i32 arena_kind=14:str
+msg OpenDeviceBlockRequest block_id=1:i64 promote=2:bool session_id=3:i64 reader_gpu=4:i32
 msg UnlockDeviceBlockRequest block_id=1:i64 lock_id=2:i64 session_id=3:i64
 msg UnlockDeviceBlockResponse
 msg PeerTransferRequest block_id=1:i64 src_rank=2:i32 dst_rank=3:i32 offset=4:i64 length=5:i64
-    tag=6:i64
+    tag=6:i64 src_address=7:str
 msg PeerTransferResponse ok=1:bool message=2:str
 
 rpc BlockWorker ReadBlock *ReadRequest *ReadResponse

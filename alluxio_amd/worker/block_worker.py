@@ -121,6 +121,11 @@ class BlockWorker:
         m.gauge("CapacityFree", lambda: sum(self.store.capacity_by_tier().values()) -
                 sum(self.store.used_by_tier().values()))
         m.gauge("BlocksCached", lambda: len(self.native.block_ids(-1)))
+        hbm = [i for i, a in enumerate(self.store.arenas) if a is not None and a.kind == "hbm"]
+        if hbm:
+            ps = self.conf.get_bytes("alluxio.worker.hbm.page.size")
+            m.gauge("HbmPagesTotal", lambda: sum(self.native.dir_capacity(i) for i in hbm) // ps)
+            m.gauge("HbmPagesFree", lambda: sum(self.native.dir_available(i) for i in hbm) // ps)
 
     def staging(self) -> _Staging:
         with self._staging_lock:
@@ -197,6 +202,31 @@ class BlockWorker:
                 length=info.length, mediumType=info.medium))
         # the commit's added-event is reported by CommitBlock already
         self.metrics.counter("BlocksCommitted").inc()
+
+    def verify_block_crc(self, block_id: int, src_crcs: list[int], src_piece: int) -> None:
+        """Compare the block's bytes against CRC32Cs of ``src_piece``-byte pieces computed by its
+        source (its page size, which may differ from ours): both sides are folded into one
+        whole-block CRC with crc32c_combine."""
+        from ..ops.native import lib
+        from ..utils.exceptions import DataLossException
+        with native_errors():
+            mine = self.native.checksum(block_id, 0)
+            length = self.native.block_info(block_id).length
+            ps = self.native.block_pages(block_id)[2]
+        combine = lib().crc32c_combine
+
+        def fold(crcs, piece):
+            acc, left = 0, length
+            for i, c in enumerate(crcs):
+                n = min(piece, left)
+                acc = c if i == 0 else combine(acc, c, n)
+                left -= n
+            return acc
+
+        if len(src_crcs) != -(-length // src_piece) or fold(src_crcs, src_piece) != fold(mine, ps):
+            self.metrics.counter("Crc32cMismatches").inc()
+            raise DataLossException(f"block {block_id}: CRC32C mismatch after transfer")
+        self.metrics.counter("Crc32cVerifiedBytes").inc(length)
 
     def abort_block(self, session_id: int, block_id: int) -> None:
         with native_errors():

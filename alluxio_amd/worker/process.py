@@ -129,6 +129,24 @@ class AlluxioWorkerProcess:
             return os.path.join(a, uuid.uuid4().hex)
         return a
 
+    def _enable_peer_access(self) -> list[int]:
+        """Map every other GPU of the node into this worker's device (xGMI peer access), so peer
+        pulls and remote ring reads by kernels on this GPU can read their HBM; returns the peers."""
+        from ..ops.native import has_gpu, lib
+        if not (has_gpu() and self.store.has_device_tier):
+            return []
+        C = lib()
+        me, peers = int(self.store.device), []
+        for d in range(C.device_count()):
+            if d == me:
+                continue
+            try:
+                if C.enable_peer_access(me, d):
+                    peers.append(d)
+            except Exception:  # noqa: BLE001 - no P2P path to that device
+                LOG.debug("peer access %d -> %d unavailable", me, d, exc_info=True)
+        return peers
+
     def start(self, register: bool = True, start_heartbeats: bool = True) -> str:
         from .. import metrics as msys
         self._sinks = msys.load_sinks(self.conf, self.worker.metrics)
@@ -148,6 +166,7 @@ class AlluxioWorkerProcess:
             self.worker.address.webPort = self.web_port
         from ..client.context import register_local_worker
         register_local_worker(addr, self.worker)
+        self.peer_devices = self._enable_peer_access()
         if register:
             self.sync.register()
         if start_heartbeats:

@@ -36,6 +36,17 @@ def remote_block_fetcher(worker, host: str, port: int, length: int | None = None
 
 
 def peer_transfer(worker, req) -> tuple[bool, str]:
+    """``PeerTransfer``: pull ``req.block_id`` from ``req.src_address`` (any same-node worker) or
+    from transfer-group rank ``req.src_rank``."""
+    if req.src_address:
+        from ..parallel.peer import is_same_node, pull_block
+        try:
+            host = req.src_address.rsplit(":", 1)[0]
+            pull_block(worker, req.block_id, req.src_address, req.length, same_node=is_same_node(worker, host))
+            return True, ""
+        except Exception as e:  # noqa: BLE001
+            LOG.exception("peer transfer of block %d from %s failed", req.block_id, req.src_address)
+            return False, str(e)
     plane = getattr(worker, "transfer_plane", None)
     if plane is None:
         return False, "no RCCL transfer plane on this worker"

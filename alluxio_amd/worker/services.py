@@ -258,26 +258,38 @@ class BlockWorkerService:
 
     # ---- MI355X extensions ---------------------------------------------------------------------
     def OpenDeviceBlock(self, req, ctx):
+        """Read-lock a block and describe where its pages live for a same-node reader: HBM arenas
+        are exported as a HIP IPC handle, shared DRAM arenas as (pid, memfd).  The reader maps the
+        arena once and copies the pages itself (``parallel.ipc.map_handle``)."""
         session = req.session_id or ids.create_session_id()
         lock_id = self.w.lock_block(session, req.block_id)
         try:
             pages, d, ps, base = self.w.native.block_pages(req.block_id)
             info = self.w.block_info(req.block_id)
             arena = self.w.store.arena_for_dir(d)
-            if arena is None or arena.kind != "hbm":
-                raise UnavailableException("block is not in the device tier")
+            if arena is None:
+                raise UnavailableException("block is in a file tier: no shared memory view")
             h = pb.block.DeviceBlockHandle(block_id=req.block_id, length=info.length, page_size=ps, pages=pages,
                                            arena_bytes=arena.nbytes, device=arena.device, lock_id=lock_id,
-                                           pid=os.getpid())
-            try:
-                h.arena_ipc_handle, h.arena_offset = arena.ipc_handle()
-            except Exception:  # noqa: BLE001
-                LOG.debug("IPC export unavailable", exc_info=True)
+                                           pid=os.getpid(), arena_kind=arena.kind, host_fd=-1)
+            if arena.kind == "hbm":
+                try:
+                    h.arena_ipc_handle, h.arena_offset = arena.ipc_handle()
+                except Exception:  # noqa: BLE001
+                    LOG.debug("IPC export unavailable", exc_info=True)
+            else:
+                share = arena.share_handle()
+                if share is None:
+                    raise UnavailableException("DRAM arena is not shareable")
+                h.host_fd = share[1]
             if req.block_id in self.w.crc:
                 h.crc32c.extend(self.w.crc[req.block_id])
             with self._lock:
                 self._device_locks[lock_id] = (session, req.block_id)
             self.w.access_block(session, req.block_id)
+            # reader_gpu = reading device + 1: a reader on another GPU pulls these bytes over xGMI
+            if arena.kind == "hbm" and req.reader_gpu and req.reader_gpu - 1 != arena.device:
+                self.w.metrics.counter("XgmiBytesSent").inc(info.length)
             return h
         except Exception:
             self.w.unlock(lock_id)

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import logging
 import os
+import weakref
 
 from ..conf import Configuration, Templates
 from ..ops.native import has_gpu, lib, wrap_errors
@@ -28,21 +29,64 @@ ALLOCATORS = {"MAXFREE": 0, "GREEDY": 1, "ROUNDROBIN": 2}
 
 
 class Arena:
-    """A contiguous allocation backing one storage dir."""
+    """A contiguous allocation backing one storage dir.
+
+    ``hbm`` arenas are one device allocation, exported to same-node processes as a HIP IPC handle.
+    ``dram`` arenas are an anonymous shared-memory file (``memfd``) mapped into the worker and
+    page-locked for the GPU when one is present: a same-node client or peer worker maps the same
+    pages through ``/proc/<worker pid>/fd/<fd>`` — the DRAM-tier analogue of the reference's
+    short-circuit mmap of block files (LocalFileDataReader.java:58-70), with no bytes on the RPC
+    channel.
+    """
 
     def __init__(self, kind: str, nbytes: int, device: int = 0):
         import torch
         self.kind = kind
         self.nbytes = nbytes
         self.device = device
+        self.fd = -1
+        self._mmap = None
+        self._registered = False
         if kind == "hbm":
             self.tensor = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", device))
         elif kind == "dram":
-            pin = has_gpu()
-            self.tensor = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin)
+            self.tensor = self._shared_host(nbytes)
         else:
             raise ValueError(kind)
         self.base = self.tensor.data_ptr()
+
+    def _shared_host(self, nbytes: int):
+        import mmap
+
+        import numpy as np
+        import torch
+        try:
+            fd = os.memfd_create("alluxio-amd-dram", getattr(os, "MFD_CLOEXEC", 1))
+            os.ftruncate(fd, max(nbytes, 1))
+            mm = mmap.mmap(fd, max(nbytes, 1), mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        except (AttributeError, OSError):
+            LOG.debug("memfd unavailable: private DRAM arena", exc_info=True)
+            return torch.empty(nbytes, dtype=torch.uint8, pin_memory=has_gpu())
+        self.fd, self._mmap = fd, mm
+        t = torch.from_numpy(np.frombuffer(mm, dtype=np.uint8, count=nbytes))
+        from ..parallel.ipc import register_local_shared
+        register_local_shared(fd, t.data_ptr())
+        if has_gpu() and nbytes:
+            self._registered = bool(lib().host_register(t.data_ptr(), nbytes))
+        # the memfd pins the memory until closed: release it with the arena even without close()
+        self._finalizer = weakref.finalize(self, _release_shared, fd, t.data_ptr() if self._registered else 0)
+        return t
+
+    def share_handle(self) -> tuple[int, int] | None:
+        """(pid, fd) through which another local process maps a shared DRAM arena, else None."""
+        return (os.getpid(), self.fd) if self.fd >= 0 else None
+
+    def close(self) -> None:
+        fin = getattr(self, "_finalizer", None)
+        if fin is not None:
+            fin()
+        self.fd = -1
+        self._registered = False
 
     def view(self, offset: int, nbytes: int):
         return self.tensor[offset:offset + nbytes]
@@ -56,6 +100,18 @@ class Arena:
             from ..parallel.ipc import export_handle
             self._ipc = export_handle(self.tensor)
         return self._ipc
+
+
+def _release_shared(fd: int, registered_ptr: int) -> None:
+    if registered_ptr:
+        try:
+            lib().host_unregister(registered_ptr)
+        except Exception:  # noqa: BLE001
+            pass
+    try:
+        os.close(fd)
+    except OSError:
+        pass
 
 
 class DirConfig:

@@ -1,31 +1,44 @@
 #!/usr/bin/env python3
 """StressWorkerBench-equivalent cached sequential-read benchmark on MI355X workers.
 
-Reference methodology (stress/shell/.../StressWorkerBench.java,
-stress/common/.../WorkerBenchParameters.java:40-70): a file is written CACHE_THROUGH to exactly
-one worker, then ``--threads`` readers loop ``read(buf)`` over it and re-open at EOF; the
-result is bytes read / time.  Here every GPU rank is one worker (HBM MEM tier) with its own
-in-process client; the rank writes its file through the client API (CACHE_THROUGH: local UFS +
-local worker), then its ``threads`` reader streams read it with the reference's default
-parameters (256 streams, 128 MiB file, 4 KiB ``read(buf)`` calls; 64 MiB blocks per BASELINE.md).
+Reference methodology (stress/shell/.../StressWorkerBench.java:71-116,251-276,
+stress/common/.../WorkerBenchParameters.java:40-70, WorkerBenchSummary.java:59-71): a file is
+written CACHE_THROUGH to exactly one worker, then ``--threads`` readers loop ``read(buf)`` over it
+and re-open at EOF; the result is bytes read / time.  Every GPU rank here is one worker (HBM MEM
+tier) plus its own client, one process per GPU (``torch.distributed``; rank 0 also runs the
+master).  Each rank writes its file through the client API (CACHE_THROUGH: local UFS + its own
+worker), then its reader streams read it with the reference defaults (256 streams, 128 MiB file,
+4 KiB ``read(buf)``; 64 MiB blocks per BASELINE.md).
 
 One bench *step* = every stream performs ``depth`` consecutive ``read(buf)`` calls (EOF calls
 re-open the file, as the reference loop does), all executed by ONE device-cursor kernel launch:
-the file's page table lives on the GPU, each call's bytes land in that stream's own ring slot
-``ring[stream, call]`` (no call is skipped or merged: every call's bytes are copied to distinct
-memory a consumer can use), and host work per step is O(1).  depth defaults to 1 MiB worth of
-calls per stream (256 for 4 KiB) — the same amortisation the reference client gets by serving
-read(4k) out of 1 MiB chunk buffers (GrpcDataReader chunks).  ``--buffer-size >= 1m`` (or
-``--depth 1``) uses the per-call batched page-gather reader instead.
+the file's page table lives on the GPU and each call's bytes land in that stream's own ring slot
+``ring[stream, call]`` — no call is skipped or merged.  depth defaults to 1 MiB of calls per
+stream (256 for 4 KiB), the amortisation the reference client gets from 1 MiB chunk buffers.
 
-``value`` = total bytes read by all ranks in the K timed steps / max-over-ranks wall time (GB/s,
-whole node, weak scaling: each worker serves its own file).
+Phases (all timed between a barrier + ``torch.cuda.synchronize()`` on both sides; max over ranks):
 
-Run: python bench.py [--gpus N --steps K --warmup W]; N>1 is launched by torch.distributed.run.
+* ``local``  (the headline ``value``): every stream starts at offset 0, as StressWorkerBench's
+  threads do, so all 256 streams read the same window in lockstep;
+* ``stagger``: stream s starts at s/threads of the file, so the streams read distinct data;
+* ``host``: the ring lives in pinned host memory (a CPU-side reader; the copy crosses to DRAM);
+* ``remote`` (N > 1): rank r's streams read the file cached on worker (r+1) % N — the peer GPU's
+  HBM mapped through HIP IPC and read over xGMI by the kernel on rank r's GPU;
+* ``replicate`` (N > 1): every rank writes a new file with ``--replication`` copies; the local
+  worker takes the bytes and the replica workers pull each block out of its HBM over xGMI;
+* ``duration``: the local phase re-run for ``--duration`` seconds of wall time.
+
+``value`` = total bytes read by all ranks in the K timed ``local`` steps / max-over-ranks time
+(GB/s, whole node, weak scaling: each worker serves its own file).
+
+Run: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no torchrun environment
+the script launches ``torch.distributed.run`` itself as a child process (before touching the GPU).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +46,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "StressWorkerBench cached seq-read GB/s (whole node) at 1/2/4/8 MI355X workers"
+PHASES = ("local", "stagger", "host", "remote", "replicate", "duration")
 
 
 def parse_args(argv=None):
@@ -46,22 +60,51 @@ def parse_args(argv=None):
     ap.add_argument("--buffer-size", default="4k")
     ap.add_argument("--page-size", default="2m")
     ap.add_argument("--depth", type=int, default=0,
-                    help="read calls per stream per step into a per-stream ring (device-cursor reader); "
-                         "0 = auto (1 MiB of calls per stream for buffers < 1 MiB, else 1)")
-    ap.add_argument("--dest", choices=["device", "host"], default="device")
-    ap.add_argument("--host-check", action="store_true", help="also time a short host-reader (D2H) run")
+                    help="read calls per stream per step (0 = 1 MiB of calls per stream)")
+    ap.add_argument("--phases", default=",".join(PHASES), help="comma list of " + "/".join(PHASES))
+    ap.add_argument("--duration", type=float, default=2.0, help="seconds for the duration phase")
+    ap.add_argument("--replication", type=int, default=3)
     ap.add_argument("--work-dir", default=None)
     ap.add_argument("--profile-json", default=None, help="append per-rank timings to this file")
     return ap.parse_args(argv)
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn_torchrun(a, argv) -> int:
+    """N > 1 without a torchrun environment: run ourselves under torch.distributed.run as a CHILD
+    process (never exec: nothing has touched the GPU yet, and the parent only waits)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     a = parse_args(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _spawn_torchrun(a, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    phases = [p for p in a.phases.split(",") if p]
+    for p in phases:
+        if p not in PHASES:
+            raise SystemExit(f"unknown phase {p}")
+
+    import numpy as np
     import torch
     import torch.distributed as dist
     from alluxio_amd.utils.format import parse_space_size
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = torch.cuda.is_available()
@@ -70,6 +113,7 @@ def main(argv=None):
     distributed = world > 1
     if distributed:
         dist.init_process_group("nccl" if gpu else "gloo")
+    dev_t = torch.device("cuda", local_rank) if gpu else torch.device("cpu")
 
     file_size = parse_space_size(a.file_size)
     block_size = parse_space_size(a.block_size)
@@ -78,13 +122,16 @@ def main(argv=None):
     work = a.work_dir or os.path.join("/tmp", f"alluxio_amd_bench_{os.getpid() if not distributed else 'dist'}")
     os.makedirs(work, exist_ok=True)
 
-    from alluxio_amd.client.batch_reader import MultiStreamReader, RingStreamReader
+    from alluxio_amd.client.batch_reader import RemoteRingReader, RingStreamReader
+    from alluxio_amd.client.context import worker_address_str
     from alluxio_amd.client.file_system import FileSystem
     from alluxio_amd.conf import Configuration
     from alluxio_amd.master.process import AlluxioMasterProcess
     from alluxio_amd.worker.process import AlluxioWorkerProcess
 
-    quota = max(2 * file_size, 1 << 30)
+    replicas = max(1, min(a.replication, world))
+    # own file + one replica of each of (replicas-1) neighbours' replicated files + own replicated file
+    quota = max((2 + replicas) * file_size, (4 << 30) if gpu else (1 << 30))
     quota += (-quota) % page
     props = {
         "alluxio.work.dir": work,
@@ -128,157 +175,222 @@ def main(argv=None):
                                   device=local_rank if gpu else 0, work_dir=os.path.join(work, f"w{rank}"))
     worker.start(register=True, start_heartbeats=False)
     fs = FileSystem(conf=conf.copy(), master_address=master_addr)
-
-    # ---- prepare: write the file CACHE_THROUGH to this rank's worker -------------------------
-    import numpy as np
-    path = f"/stress-worker-base/data-{rank}"
-    rng = np.random.default_rng(1234 + rank)
-    data = rng.integers(0, 256, file_size, dtype=np.uint8)
+    my_addr = worker_address_str(worker.worker.address)
+    addrs = [my_addr]
     if distributed:
-        dist.barrier()
-    if rank == 0:
-        fs.create_directory("/stress-worker-base", recursive=True, allow_exists=True)
-    if distributed:
-        dist.barrier()
-    t0 = time.perf_counter()
-    fs.write_file(path, data, write_type="CACHE_THROUGH", block_size=block_size)
-    write_s = time.perf_counter() - t0
-    st = fs.get_status(path)
-    assert st.length == file_size and st.in_alluxio_percentage == 100, (st.length, st.in_alluxio_percentage)
+        addrs = [None] * world
+        dist.all_gather_object(addrs, my_addr)
 
-    # ---- reader streams -----------------------------------------------------------------------
-    dev = torch.device("cuda", local_rank) if (gpu and a.dest == "device") else None
-    depth = a.depth or (max(1, (1 << 20) // buf) if buf < (1 << 20) else 1)
-    if depth > 1:
-        # device-cursor ring reader: each step = `depth` read(buf) calls per stream, one launch
-        ring = torch.empty((a.threads, depth, buf), dtype=torch.uint8, device=dev,
-                           pin_memory=(gpu and dev is None))
-        reader = RingStreamReader(fs, path, ring)
-        bufs = None
-    else:
-        if dev is not None:
-            bufs_all = torch.empty(a.threads * buf, dtype=torch.uint8, device=dev)
-        else:
-            bufs_all = torch.empty(a.threads * buf, dtype=torch.uint8, pin_memory=gpu)
-        bufs = [bufs_all[i * buf:(i + 1) * buf] for i in range(a.threads)]
-        reader = MultiStreamReader(fs, path, bufs)
+    def barrier():
+        if distributed:
+            dist.barrier()
 
     def sync():
         if gpu:
             torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
-        reader.step()
-    sync()
-    if distributed:
-        dist.barrier()
-    sync()
-    b0 = reader.total_bytes
+    def reduce(value: float, op) -> float:
+        if not distributed:
+            return value
+        t = torch.tensor([value], dtype=torch.float64, device=dev_t)
+        dist.all_reduce(t, op=op)
+        return t.item()
+
+    def MAX(v):
+        return reduce(v, dist.ReduceOp.MAX if distributed else None)
+
+    def SUM(v):
+        return reduce(v, dist.ReduceOp.SUM if distributed else None)
+
+    # ---- prepare: write the file CACHE_THROUGH to this rank's worker -------------------------
+    path = f"/stress-worker-base/data-{rank}"
+    rng = np.random.default_rng(1234 + rank)
+    data = rng.integers(0, 256, file_size, dtype=np.uint8)
+    barrier()
+    if rank == 0:
+        fs.create_directory("/stress-worker-base", recursive=True, allow_exists=True)
+    barrier()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        reader.step()
-    sync()
-    elapsed = time.perf_counter() - t0
-    nbytes = reader.total_bytes - b0
-    if distributed:
-        dist.barrier()
+    fs.write_file(path, data, write_type="CACHE_THROUGH", block_size=block_size)
+    write_s = time.perf_counter() - t0
+    st = fs.get_status(path)
+    assert st.length == file_size and st.in_alluxio_percentage == 100, (st.length, st.in_alluxio_percentage)
+    barrier()
 
-    # ---- verify: sampled streams' last reads equal the file bytes at their offsets ------------
-    ok = True
-    check = [0, a.threads // 2, a.threads - 1]
-    if bufs is None:
-        for i in check:
+    depth = a.depth or max(1, (1 << 20) // buf)
+    ring_dev = torch.empty((a.threads, depth, buf), dtype=torch.uint8, device=dev_t)
+    stagger_offsets = [((s * file_size) // a.threads) // buf * buf for s in range(a.threads)]
+    results: dict = {}
+    ok_all = True
+
+    def verify(reader, ring, src):
+        good = True
+        for s in (0, a.threads // 2, a.threads - 1):
             for k in (0, depth // 2, depth - 1):
-                off, n = reader.last_call(i, k)
-                if n and not np.array_equal(ring[i, k, :n].cpu().numpy(), data[off:off + n]):
-                    ok = False
-    else:
-        for i in check:
-            pos = reader.position(i)
-            if pos == 0:
-                continue
-            n = min(buf, pos - ((pos - 1) // buf) * buf) if pos % buf else buf
-            start = pos - n
-            got = bufs[i][:n].cpu().numpy()
-            if not np.array_equal(got, data[start:start + n]):
-                ok = False
-    reader.close()
+                off, n = reader.last_call(s, k)
+                if n and not np.array_equal(ring[s, k, :n].cpu().numpy(), src[off:off + n]):
+                    good = False
+        return good
 
-    host_gbps = None
-    if a.host_check and gpu:
-        hb = torch.empty(64 * buf, dtype=torch.uint8, pin_memory=True)
-        hr = MultiStreamReader(fs, path, [hb[i * buf:(i + 1) * buf] for i in range(64)])
-        for _ in range(3):
-            hr.step()
-        hb0 = hr.total_bytes
-        th = time.perf_counter()
-        for _ in range(10):
-            hr.step()
-        host_gbps = (hr.total_bytes - hb0) / (time.perf_counter() - th) / 1e9
-        hr.close()
+    def timed(reader, steps, warmup):
+        for _ in range(warmup):
+            reader.step()
+        sync()
+        barrier()
+        sync()
+        b0 = reader.total_bytes
+        t = time.perf_counter()
+        for _ in range(steps):
+            reader.step()
+        sync()
+        el = time.perf_counter() - t
+        nb = reader.total_bytes - b0
+        barrier()
+        return el, nb
 
-    # ---- aggregate ----------------------------------------------------------------------------
-    if distributed:
-        dev_t = torch.device("cuda", local_rank) if gpu else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        b = torch.tensor([float(nbytes)], dtype=torch.float64, device=dev_t)
-        dist.all_reduce(b, op=dist.ReduceOp.SUM)
-        okt = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev_t)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        elapsed, total_bytes, ok = t.item(), b.item(), okt.item() > 0
-    else:
-        total_bytes = float(nbytes)
+    def run_phase(name, make_reader, ring, src, steps, warmup):
+        nonlocal ok_all
+        reader = make_reader(ring)
+        try:
+            el, nb = timed(reader, steps, warmup)
+            good = verify(reader, ring, src)
+        finally:
+            reader.close()
+        el_max, total = MAX(el), SUM(float(nb))
+        good = SUM(0.0 if good else 1.0) == 0
+        ok_all = ok_all and good
+        results[name] = {"GBps": round(total / el_max / 1e9, 3), "s": round(el_max, 5), "bytes": int(total),
+                         "verified": good}
+        return results[name]
+
+    # ---- local (headline): lockstep from offset 0 --------------------------------------------
+    run_phase("local", lambda r: RingStreamReader(fs, path, r), ring_dev, data, a.steps, a.warmup)
+    local = results["local"]
+
+    if "stagger" in phases:
+        run_phase("stagger", lambda r: RingStreamReader(fs, path, r, start_offsets=stagger_offsets),
+                  ring_dev, data, a.steps, a.warmup)
+
+    if "host" in phases and gpu:
+        ring_host = torch.empty((a.threads, depth, buf), dtype=torch.uint8, pin_memory=True)
+        run_phase("host", lambda r: RingStreamReader(fs, path, r), ring_host, data,
+                  max(2, min(a.steps, 20)), max(1, min(a.warmup, 3)))
+        del ring_host
+
+    if "remote" in phases and world > 1:
+        peer = (rank + 1) % world
+        peer_data = np.random.default_rng(1234 + peer).integers(0, 256, file_size, dtype=np.uint8)
+        run_phase("remote", lambda r: RemoteRingReader(fs, f"/stress-worker-base/data-{peer}", r, addrs[peer]),
+                  ring_dev, peer_data, a.steps, a.warmup)
+        del peer_data
+
+    if "replicate" in phases and world > 1:
+        wm = worker.worker.metrics
+        before = wm.counter("XgmiBytesReceived").count
+        before_sh = wm.counter("PeerSharedBytesReceived").count
+        src = torch.from_numpy(data).to(dev_t)
+        sync()
+        barrier()
+        t = time.perf_counter()
+        fs.write_file(f"/stress-worker-base/rep-{rank}", src, write_type="MUST_CACHE", block_size=block_size,
+                      replication_min=replicas)
+        sync()
+        el = time.perf_counter() - t
+        barrier()
+        moved = wm.counter("XgmiBytesReceived").count - before
+        moved_sh = wm.counter("PeerSharedBytesReceived").count - before_sh
+        el_max = MAX(el)
+        rst = fs.get_status(f"/stress-worker-base/rep-{rank}")
+        good = all(len(f.blockInfo.locations) >= replicas for f in rst.fileBlockInfos)
+        good = SUM(0.0 if good else 1.0) == 0
+        ok_all = ok_all and good
+        results["replicate"] = {"replicas": replicas,
+                                "write_GBps": round(SUM(float(file_size)) / el_max / 1e9, 3),
+                                "replica_GBps": round(SUM(float(file_size * (replicas - 1))) / el_max / 1e9, 3),
+                                "xgmi_bytes_received": int(SUM(float(moved))),
+                                "shared_bytes_received": int(SUM(float(moved_sh))), "s": round(el_max, 4),
+                                "verified": good}
+        del src
+
+    if "duration" in phases and a.duration > 0:
+        reader = RingStreamReader(fs, path, ring_dev)
+        try:
+            for _ in range(a.warmup):
+                reader.step()
+            sync()
+            barrier()
+            b0, t, n = reader.total_bytes, time.perf_counter(), 0
+            # every rank runs the same step count: rank 0's clock decides when to stop
+            while True:
+                for _ in range(64):
+                    reader.step()
+                n += 64
+                sync()
+                stop = torch.tensor([1.0 if time.perf_counter() - t >= a.duration else 0.0], device=dev_t)
+                if distributed:
+                    dist.broadcast(stop, src=0)
+                if stop.item() > 0:
+                    break
+            el = time.perf_counter() - t
+            nb = reader.total_bytes - b0
+            barrier()
+        finally:
+            reader.close()
+        el_max = MAX(el)
+        results["duration"] = {"GBps": round(SUM(float(nb)) / el_max / 1e9, 3), "s": round(el_max, 3), "steps": n}
 
     if a.profile_json:
         with open(a.profile_json, "a") as f:
-            f.write(json.dumps({"rank": rank, "elapsed_s": elapsed, "bytes": nbytes, "write_s": write_s,
-                                "reopens": reader.reopens}) + "\n")
-    value = total_bytes / elapsed / 1e9
+            f.write(json.dumps({"rank": rank, "results": results, "write_s": write_s}) + "\n")
     if rank == 0:
+        cfg = {
+            "model": "StressWorkerBench cached seq-read, HBM MEM tier",
+            "global_batch": a.threads * world,
+            "seq_len": buf,
+            "parallelism": f"workers{world}",
+            "threads_per_worker": a.threads,
+            "file_size": file_size,
+            "block_size": block_size,
+            "buffer_size": buf,
+            "calls_per_stream_per_step": depth,
+            "reads_per_step": a.threads * depth,
+            "page_size": page,
+            "reader": "gpu-consumer (same-GPU device ring), device-cursor ring x%d, streams start at offset 0" % depth,
+            "verified": bool(ok_all),
+            "stagger_GBps": results.get("stagger", {}).get("GBps"),
+            "host_reader_GBps": results.get("host", {}).get("GBps"),
+            "remote_GBps": results.get("remote", {}).get("GBps"),
+            "replication": results.get("replicate"),
+            "duration_GBps": results.get("duration", {}).get("GBps"),
+            "duration_s": results.get("duration", {}).get("s"),
+            "write_GBps_per_worker": round(file_size / write_s / 1e9, 3),
+            "phases": results,
+        }
         out = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": local["GBps"],
             "unit": "GB/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "ms_per_step": round(local["s"] / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "uint8",
             "data": "synthetic (random bytes written through the client API, CACHE_THROUGH)",
-            "config": {
-                "model": "StressWorkerBench cached seq-read, HBM MEM tier",
-                "global_batch": a.threads * world,
-                "seq_len": buf,
-                "parallelism": f"workers{world}",
-                "threads_per_worker": a.threads,
-                "file_size": file_size,
-                "block_size": block_size,
-                "buffer_size": buf,
-                "calls_per_stream_per_step": depth,
-                "reads_per_step": a.threads * depth,
-                "page_size": page,
-                "reader": ("gpu-consumer (same-GPU device buffers)" if dev is not None else "host (pinned)")
-                + (f", device-cursor ring x{depth}" if depth > 1 else ""),
-                "verified": bool(ok),
-                "host_reader_GBps": round(host_gbps, 3) if host_gbps else None,
-                "write_GBps_per_worker": round(file_size / write_s / 1e9, 3),
-            },
+            "config": cfg,
         }
         print(json.dumps(out), flush=True)
 
     fs.close()
     worker.stop()
-    if distributed:
-        dist.barrier()
+    barrier()
     if master is not None:
         master.stop()
     if distributed:
         dist.destroy_process_group()
-    return 0 if ok else 1
+    return 0 if ok_all else 1
 
 
 if __name__ == "__main__":

@@ -1,0 +1,49 @@
+"""bench.py contract: --gpus N launches N ranks itself, every phase verifies its bytes.
+
+Runs on CPU with the gloo backend and shared-memory DRAM arenas: the ``remote`` phase maps the
+peer worker's arena (memfd) exactly as the GPU path maps a peer's HBM (HIP IPC), and the
+``replicate`` phase's replicas pull blocks out of the primary's arena (PeerTransfer).
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, tmp_path):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args, "--work-dir", str(tmp_path)],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+SMALL = ["--steps", "3", "--warmup", "1", "--file-size", "8m", "--block-size", "4m", "--page-size", "1m",
+         "--threads", "8", "--duration", "0.2"]
+
+
+def test_bench_single_rank(tmp_path):
+    out = _run(SMALL, tmp_path)
+    assert out["n_gpus"] == 1 and out["steps"] == 3 and out["warmup"] == 1
+    c = out["config"]
+    assert c["verified"] and c["stagger_GBps"] > 0 and c["duration_GBps"] > 0
+    assert c["remote_GBps"] is None and c["replication"] is None
+    assert out["value"] == c["phases"]["local"]["GBps"]
+
+
+def test_bench_two_ranks_remote_and_replicate(tmp_path):
+    out = _run(["--gpus", "2", *SMALL], tmp_path)
+    assert out["n_gpus"] == 2
+    c = out["config"]
+    assert c["verified"] and c["parallelism"] == "workers2"
+    assert c["phases"]["remote"]["verified"] and c["remote_GBps"] > 0
+    rep = c["replication"]
+    assert rep["replicas"] == 2 and rep["verified"]
+    # each rank's 8 MiB file got one extra copy, pulled out of the primary's arena
+    assert rep["shared_bytes_received"] + rep["xgmi_bytes_received"] == 2 * (8 << 20)

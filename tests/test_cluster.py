@@ -178,6 +178,7 @@ def test_domain_socket_data_server(tmp_path):
         from alluxio_amd.client.file_system import FileSystem
         conf2 = c.conf.copy()
         conf2.set("alluxio.user.network.inprocess.transport.enabled", "false")
+        conf2.set("alluxio.user.short.circuit.enabled", "false")   # else the shared-DRAM short circuit wins
         fs2 = FileSystem(conf=conf2, master_address=c.master.address)
         assert fs2.read_file("/uds/f") == data
         assert domain_socket_for(addr) == path

@@ -149,3 +149,48 @@ def test_transfer_plane_device_pull(gpu, tmp_path):
         outs.append(json.loads(out.strip().splitlines()[-1]))
     for o in outs:
         assert o["ok"] and o["device_plane"] and o["pulled"] == 20 * (1 << 20) + 11, o
+
+
+@pytest.mark.gpu
+def test_remote_ring_reader_other_process(gpu, tmp_path):
+    """RemoteRingReader: the device-cursor ring kernel on this process's GPU reads a file cached
+    in another worker process's HBM arena (IPC-mapped), 4 KiB calls into a [streams, depth, buf]
+    ring; every sampled call's bytes equal the file bytes at its offset."""
+    import torch
+
+    from alluxio_amd.client.batch_reader import RemoteRingReader
+    from alluxio_amd.client.context import worker_address_str
+    from alluxio_amd.client.file_system import FileSystem
+    from alluxio_amd.conf import Configuration
+    script = tmp_path / "server.py"
+    script.write_text(SERVER % {"root": ROOT, "work": str(tmp_path / "work")})
+    p = subprocess.Popen([sys.executable, str(script)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        line = p.stdout.readline()
+        assert line, p.stderr.read()[-3000:]
+        master = json.loads(line)["master"]
+        expect = np.random.default_rng(7).integers(0, 256, 20 * (1 << 20) + 333, dtype=np.uint8)
+        fs = FileSystem(conf=Configuration({}), master_address=master)
+        st = fs.get_status("/ipc/f")
+        addr = worker_address_str(st.fileBlockInfos[0].blockInfo.locations[0].workerAddress)
+        streams, depth, buf = 16, 64, 4096
+        ring = torch.empty((streams, depth, buf), dtype=torch.uint8, device="cuda")
+        starts = [s * (1 << 20) for s in range(streams)]
+        with RemoteRingReader(fs, "/ipc/f", ring, addr, start_offsets=starts) as r:
+            for _ in range(3):
+                r.step()
+            torch.cuda.synchronize()
+            for s in range(streams):
+                for k in (0, depth // 2, depth - 1):
+                    off, n = r.last_call(s, k)
+                    assert np.array_equal(ring[s, k, :n].cpu().numpy(), expect[off:off + n]), (s, k)
+            assert r.total_bytes == 3 * streams * depth * buf
+        fs.close()
+    finally:
+        p.stdin.write("\n")
+        p.stdin.flush()
+        try:
+            p.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()

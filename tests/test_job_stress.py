@@ -197,9 +197,26 @@ def test_max_throughput(cluster):
     fs.close()
 
 
+def test_replicated_write_pulls_from_primary(cluster):
+    """replication_min=2: the write lands on two workers at once (reference
+    AlluxioBlockStore.getOutStream initialReplicas); the second copy is pulled out of the primary's
+    shared arena by the replica (PeerTransfer), not streamed by the client."""
+    fs = cluster.client()
+    data = os.urandom(MB + 17)
+    fs.write_file("/rep/w", data, write_type="MUST_CACHE", replication_min=2)
+    cluster.heartbeat_workers()
+    bid = fs.get_status("/rep/w").block_ids[0]
+    assert sum(w.worker.has_block(bid) for w in cluster.workers) == 2
+    pulled = sum(w.worker.metrics.counter("PeerSharedBytesReceived").count for w in cluster.workers)
+    assert pulled >= len(data)
+    assert fs.read_file("/rep/w") == data
+    fs.close()
+
+
 def test_replication_checker(cluster):
     fs = cluster.client()
-    fs.write_file("/rep/f", os.urandom(MB), write_type="MUST_CACHE", replication_min=2)
+    fs.write_file("/rep/f", os.urandom(MB), write_type="MUST_CACHE")
+    fs.set_attribute("/rep/f", replication_min=2)
     cluster.heartbeat_workers()
     bid = fs.get_status("/rep/f").block_ids[0]
     rc = cluster.master.replication_checker

@@ -25,9 +25,10 @@ run() {  # name timeout cmd...
 
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 600 python -m pytest tests -m gpu -x -q ;;
+    tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
     bench) run bench_default 400 python bench.py ;;
+    bench20) run bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     variants)
       run bench_buf4m 300 python bench.py --buffer-size 4m --steps 200 --warmup 20
       run bench_buf1m 300 python bench.py --buffer-size 1m
@@ -52,6 +53,11 @@ for s in $STEPS; do
       run rocprof_pmc_rd 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --kernel-trace --stats -d "$OUT/pmc_rd" -o pmc --output-format csv -- python3 bench.py --steps 10 --warmup 1
       run rocprof_pmc_wr 240 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-trace --stats -d "$OUT/pmc_wr" -o pmc --output-format csv -- python3 bench.py --steps 10 --warmup 1
       run rocprof_pmc_dram 240 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram" -o pmc --output-format csv -- python3 bench.py --steps 10 --warmup 1
+      ;;
+    pmcdram)
+      # HBM bytes behind the lockstep (local) and staggered readers, one counter pass each
+      run pmc_dram_local 240 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram_local" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2 --phases local
+      run pmc_dram_stagger 240 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram_stagger" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2 --phases local,stagger
       ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
