@@ -12,6 +12,7 @@
 #include "ring_read.h"
 #include "kernels.h"
 #include "seg_ring.h"
+#include "frame_rpc.h"
 
 namespace py = pybind11;
 using namespace amdx;
@@ -341,6 +342,56 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("reopens", &RingReadSession::reopens)
       .def_property_readonly("calls", &RingReadSession::calls)
       .def_property_readonly("file_len", &RingReadSession::file_len);
+
+  // ---- native framed RPC (control-plane fast path) ----------------------------------------
+  py::class_<FrameRpcServer>(m, "FrameRpcServer")
+      .def(py::init<const std::string&, int, const std::vector<std::string>&, const std::vector<int>&, int>(),
+           py::arg("host"), py::arg("port"), py::arg("methods"), py::arg("lanes"), py::arg("io_threads") = 2)
+      .def("start", &FrameRpcServer::start, G())
+      .def("stop", &FrameRpcServer::stop, G())
+      .def_property_readonly("port", &FrameRpcServer::port)
+      .def_property_readonly("requests", &FrameRpcServer::requests)
+      .def("poll", [](FrameRpcServer& s, int lane, int max_n, int timeout_ms) {
+             std::vector<FrameRequest> v;
+             {
+               py::gil_scoped_release rel;
+               v = s.poll(lane, max_n, timeout_ms);
+             }
+             py::list out;
+             for (auto& r : v)
+               out.append(py::make_tuple(r.token, r.method, py::str(r.user), py::bytes(r.payload)));
+             return out;
+           }, py::arg("lane"), py::arg("max_n"), py::arg("timeout_ms"))
+      .def("respond", [](FrameRpcServer& s, uint64_t token, int status, const std::string& msg, py::bytes payload) {
+             std::string p = payload;
+             py::gil_scoped_release rel;
+             s.respond(token, status, msg, p);
+           }, py::arg("token"), py::arg("status"), py::arg("message"), py::arg("payload"))
+      .def("respond_many", [](FrameRpcServer& s, const py::list& items) {
+             std::vector<std::tuple<uint64_t, int, std::string, std::string>> v;
+             v.reserve(items.size());
+             for (auto it : items) {
+               auto t = it.cast<py::tuple>();
+               v.emplace_back(t[0].cast<uint64_t>(), t[1].cast<int>(), t[2].cast<std::string>(),
+                              std::string(t[3].cast<py::bytes>()));
+             }
+             py::gil_scoped_release rel;
+             for (auto& x : v) s.respond(std::get<0>(x), std::get<1>(x), std::get<2>(x), std::get<3>(x));
+           })
+      .def("set_user", &FrameRpcServer::set_user);
+  py::class_<FrameRpcClient>(m, "FrameRpcClient")
+      .def(py::init<const std::string&, int, const std::string&, int>(), py::arg("host"), py::arg("port"),
+           py::arg("auth"), py::arg("timeout_ms") = 60000)
+      .def("call", [](FrameRpcClient& c, const std::string& path, py::bytes payload, int timeout_ms) {
+             std::string p = payload;
+             std::tuple<int, std::string, std::string> r;
+             {
+               py::gil_scoped_release rel;
+               r = c.call(path, p, timeout_ms);
+             }
+             return py::make_tuple(std::get<0>(r), py::str(std::get<1>(r)), py::bytes(std::get<2>(r)));
+           }, py::arg("path"), py::arg("payload"), py::arg("timeout_ms") = 0)
+      .def("close", &FrameRpcClient::close, G());
 
   // ---- codecs / kernels ------------------------------------------------------------------
   m.def("device_count", &hip_device_count);

@@ -1,0 +1,109 @@
+// Native framed-RPC transport for unary control-plane calls (master metadata hot path).
+//
+// Why: the reference serves metadata RPCs from a JVM gRPC server with hundreds of handler
+// threads (core/server/common/src/main/java/alluxio/grpc/GrpcServerBuilder.java; published master
+// throughput in docs/en/operation/Scalability-Tuning.md:142-148).  A Python gRPC server pays a
+// thread hand-off and a GIL acquisition per call, which caps it at a few thousand calls/s.  This
+// transport keeps sockets, framing, queueing and waiting in C++ with the GIL released; Python
+// handler threads pull *batches* of decoded requests (one GIL acquisition per batch) and push
+// responses back.  Payloads are the same protobuf messages as the gRPC services, so one Python
+// servicer serves both transports; gRPC stays the wire-compatible path.
+//
+// Frames (little endian):
+//   request  : u32 len | u32 call_id | u16 path_len | path | payload           (len = bytes after len)
+//   response : u32 len | u32 call_id | u16 status | u32 msg_len | msg | payload
+// The first request of a connection is path "@auth" with payload "TYPE\0user\0password"; the
+// server's Python side validates it (same authenticator as SASL PLAIN) and binds the user to the
+// connection.  Status codes are gRPC status codes.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace amdx {
+
+struct FrameRequest {
+  uint64_t token;      // (conn id << 32) | call id
+  uint32_t method;     // registered method index (0 = "@auth", unknown = 0xffffffff)
+  std::string user;    // authenticated user of the connection ("" before @auth)
+  std::string payload;
+};
+
+class FrameRpcServer {
+ public:
+  // `methods`: paths ("/svc/Method") in registration order, `lanes`: dispatch lane per method.
+  FrameRpcServer(const std::string& host, int port, const std::vector<std::string>& methods,
+                 const std::vector<int>& lanes, int io_threads);
+  ~FrameRpcServer();
+  int port() const { return port_; }
+  void start();
+  void stop();
+  // Up to `max_n` requests of `lane`, waiting at most timeout_ms for the first (GIL released).
+  std::vector<FrameRequest> poll(int lane, int max_n, int timeout_ms);
+  void respond(uint64_t token, int status, const std::string& msg, const std::string& payload);
+  // Bind a user to the connection of `token` (after a successful @auth).
+  void set_user(uint64_t token, const std::string& user);
+  uint64_t requests() const { return requests_.load(); }
+
+ private:
+  struct Conn;
+  void accept_loop();
+  void io_loop(int idx);
+  void on_readable(const std::shared_ptr<Conn>& c, int ep);
+  void close_conn(uint32_t id);
+  std::shared_ptr<Conn> find(uint32_t id);
+
+  std::string host_;
+  int port_;
+  int listen_fd_ = -1;
+  std::unordered_map<std::string, uint32_t> method_ids_;
+  std::vector<int> lanes_;
+  int nthreads_;
+  std::vector<int> epolls_;
+  std::vector<std::thread> threads_;
+  std::thread acceptor_;
+  std::atomic<bool> running_{false};
+  std::mutex conns_mu_;
+  std::unordered_map<uint32_t, std::shared_ptr<Conn>> conns_;
+  uint32_t next_conn_ = 1;
+  struct Lane {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<FrameRequest> q;
+  };
+  std::vector<std::unique_ptr<Lane>> lane_q_;
+  std::atomic<uint64_t> requests_{0};
+  int wake_fd_ = -1;
+};
+
+// Client side: a pool of blocking connections; call() is thread-safe, one in-flight call per
+// connection, connections created on demand (the GIL is released for the whole call).
+class FrameRpcClient {
+ public:
+  FrameRpcClient(const std::string& host, int port, const std::string& auth_payload, int timeout_ms);
+  ~FrameRpcClient();
+  // Returns (status, message, payload).
+  std::tuple<int, std::string, std::string> call(const std::string& path, const std::string& payload,
+                                                 int timeout_ms);
+  void close();
+
+ private:
+  int connect_one(int timeout_ms);
+  std::string host_;
+  int port_;
+  std::string auth_;
+  int timeout_ms_;
+  std::mutex mu_;
+  std::vector<int> idle_;
+  std::atomic<uint32_t> next_id_{1};
+  bool closed_ = false;
+};
+
+}  // namespace amdx

@@ -91,6 +91,9 @@ class BlockMaster(Journaled):
         self._temp = IndexedSet(id=(lambda w: w.id, True), addr=(lambda w: w.key, True))
         self._lost = IndexedSet(id=(lambda w: w.id, True), addr=(lambda w: w.key, True))
         self._lost_blocks: set[int] = set()
+        # bumped whenever a block's length/locations or the live-worker set change: versions the
+        # FileSystemMaster's cached FileInfo replies (they embed block locations)
+        self.location_epoch = 0
         self.lost_worker_listeners = []
         self.worker_registered_listeners = []
         self.safe_mode = None
@@ -98,12 +101,14 @@ class BlockMaster(Journaled):
     # ---- Journaled ----------------------------------------------------------------------------
     def reset_state(self) -> None:
         with self._lock:
+            self.location_epoch += 1
             self._blocks.clear()
             self._next_container = 0
             self._container_limit = 0
 
     def process_journal_entry(self, e) -> bool:
         with self._lock:
+            self.location_epoch += 1
             if e.HasField("block_container_id_generator"):
                 self._container_limit = e.block_container_id_generator.next_container_id
                 self._next_container = max(self._next_container, self._container_limit)
@@ -184,6 +189,7 @@ class BlockMaster(Journaled):
                 if w is None:
                     raise NotFoundException(f"Could not find worker id: {wid} to register.")
                 self._lost.remove(w)
+            self.location_epoch += 1
             self._temp.remove(w)
             self._registered.remove(w)
             w.registered = True
@@ -213,7 +219,9 @@ class BlockMaster(Journaled):
             # block unknown to the master (deleted meanwhile): ask the worker to drop it
             w.to_remove.add(bid)
             return
-        m.locations[w.id] = (tier, medium)
+        if m.locations.get(w.id) != (tier, medium):
+            m.locations[w.id] = (tier, medium)
+            self.location_epoch += 1
         w.blocks.add(bid)
         self._lost_blocks.discard(bid)
 
@@ -229,6 +237,8 @@ class BlockMaster(Journaled):
             w.used = dict(used_on_tiers)
             if lost_storage:
                 w.lost_storage.update(lost_storage)
+            if removed:
+                self.location_epoch += 1
             for bid in removed:
                 m = self._blocks.get(bid)
                 if m is not None:
@@ -421,6 +431,7 @@ class BlockMaster(Journaled):
         return lost
 
     def _process_lost(self, w: MasterWorkerInfo) -> None:
+        self.location_epoch += 1
         for bid in w.blocks:
             m = self._blocks.get(bid)
             if m is not None:

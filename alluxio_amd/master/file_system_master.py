@@ -27,6 +27,7 @@ from ..utils.exceptions import (AccessControlException, DirectoryNotEmptyExcepti
                                 FailedPreconditionException, FileAlreadyExistsException,
                                 FileDoesNotExistException, InvalidArgumentException,
                                 InvalidPathException, UnavailableException)
+from ..rpc.marshal import length_delimited
 from ..utils.uri import normalize_path, path_components
 from .inode import (LOST, NO_TTL, NOT_PERSISTED, PERSISTED, TO_BE_PERSISTED, InodeFile, now_ms)
 from .inode_tree import InodeTree
@@ -91,6 +92,14 @@ class FileSystemMaster(Journaled):
         self._sync_times: dict[str, float] = {}
         self.state_lock = None
         self.audit = None
+        # FileInfo reply cache: (inode id, path) -> FileInfo, valid while the namespace, block
+        # locations and mount table are unchanged (all three epochs).  Served objects are shared:
+        # callers copy them into their reply, never mutate them.
+        self._fi_cache: dict = {}
+        self._fib_cache: dict = {}
+        self._ls_cache: dict = {}
+        self._fi_epoch = None
+        self._fi_cache_max = conf.get_int("alluxio.master.metadata.reply.cache.size", "100000") if conf else 100000
 
     # ------------------------------------------------------------------------------------------
     # Journaled
@@ -228,6 +237,42 @@ class FileSystemMaster(Journaled):
 
     # ------------------------------------------------------------------------------------------
     # FileInfo
+    def _cache_epoch(self):
+        return (self.tree.epoch, self.block_master.location_epoch, self.mount_table.epoch)
+
+    def cached_file_info(self, inode, path: str):
+        """``file_info`` through the reply cache (callers hold the tree read lock)."""
+        ep = self._cache_epoch()
+        if ep != self._fi_epoch:
+            self._reset_reply_cache(ep)
+        cache = self._fi_cache
+        key = (inode.id, path)
+        fi = cache.get(key)
+        if fi is None:
+            fi = self.file_info(inode, path)
+            if len(cache) < self._fi_cache_max and ep == self._cache_epoch():
+                cache[key] = fi
+        return fi
+
+    def _reset_reply_cache(self, ep) -> None:
+        self._fi_cache = {}
+        self._fib_cache = {}
+        self._ls_cache = {}
+        self._fi_epoch = ep
+
+    def cached_file_info_bytes(self, inode, path: str) -> bytes:
+        """Serialized FileInfo through the reply cache (callers hold the tree read lock)."""
+        ep = self._cache_epoch()
+        if ep != self._fi_epoch:
+            self._reset_reply_cache(ep)
+        key = (inode.id, path)
+        b = self._fib_cache.get(key)
+        if b is None:
+            b = self.cached_file_info(inode, path).SerializeToString()
+            if len(self._fib_cache) < self._fi_cache_max and ep == self._cache_epoch():
+                self._fib_cache[key] = b
+        return b
+
     def file_info(self, inode, path: str | None = None):
         path = path or self.tree.path_of(inode)
         fi = pb.file.FileInfo(
@@ -451,21 +496,23 @@ class FileSystemMaster(Journaled):
     # ------------------------------------------------------------------------------------------
     # read-side
     def get_status(self, path: str, load_metadata: str = LOAD_ONCE, sync_interval_ms: int = -1,
-                   access_mode: int = Bits.READ, update_timestamps: bool = True):
+                   access_mode: int = Bits.READ, update_timestamps: bool = True, raw: bool = False):
+        """FileInfo of ``path`` (``raw``: its serialized bytes, from the reply cache)."""
         path = normalize_path(path)
         self._count("Master.GetFileInfoOps")
         self._maybe_sync(path, sync_interval_ms, recursive=False)
+        get = self.cached_file_info_bytes if raw else self.cached_file_info
         with self.tree.lock.read():
             chain, missing = self.tree.resolve(path)
             if not missing:
-                self._check(chain[:-1] + [chain[-1]], Bits.NONE, path)
-                return self.file_info(chain[-1], path)
+                self._check(chain, Bits.NONE, path)
+                return get(chain[-1], path)
         if load_metadata == LOAD_NEVER:
             raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
         self.load_metadata(path, recursive=False, create_ancestors=True, quiet=True)
         with self.tree.lock.read():
             inode = self.tree.get(path)
-            return self.file_info(inode, path)
+            return get(inode, path)
 
     def exists(self, path: str, load_metadata: str = LOAD_ONCE) -> bool:
         try:
@@ -475,7 +522,10 @@ class FileSystemMaster(Journaled):
             return False
 
     def list_status(self, path: str, recursive: bool = False, load_metadata: str = LOAD_ONCE,
-                    sync_interval_ms: int = -1, load_direct_children: bool = True):
+                    sync_interval_ms: int = -1, load_direct_children: bool = True, raw: bool = False):
+        """FileInfos of ``path``'s children (recursively: of all descendants), or of ``path``
+        itself when it is a file.  ``raw``: the serialized ``ListStatusPResponse`` bodies of the
+        listing instead (one bytes object per <= 10000 entries), from the reply cache."""
         path = normalize_path(path)
         self._count("Master.GetFileInfoOps")
         self._maybe_sync(path, sync_interval_ms, recursive=recursive)
@@ -497,16 +547,29 @@ class FileSystemMaster(Journaled):
             inode = chain[-1]
             self._check(chain, Bits.READ if inode.is_directory else Bits.NONE, path)
             if not inode.is_directory:
-                return [self.file_info(inode, path)]
+                if raw:
+                    return [length_delimited(0x0A, self.cached_file_info_bytes(inode, path))]
+                return [self.cached_file_info(inode, path)]
+            ep = self._cache_epoch()
+            lkey = (inode.id, path, recursive, raw)
+            if ep == self._fi_epoch:
+                hit = self._ls_cache.get(lkey)
+                if hit is not None:
+                    return hit
             out = []
             stack = [(inode, path)]
             while stack:
                 d, dp = stack.pop(0)
                 for c in self.tree.list_children(d):
                     cp = dp.rstrip("/") + "/" + c.name
-                    out.append(self.file_info(c, cp))
+                    out.append(self.cached_file_info_bytes(c, cp) if raw else self.cached_file_info(c, cp))
                     if recursive and c.is_directory:
                         stack.append((c, cp))
+            if raw:
+                out = [b"".join(length_delimited(0x0A, b) for b in out[i:i + 10000])
+                       for i in range(0, len(out), 10000)] or [b""]
+            if ep == self._fi_epoch == self._cache_epoch() and len(self._ls_cache) < 4096:
+                self._ls_cache[lkey] = out
             return out
 
     def get_file_path(self, file_id: int) -> str:

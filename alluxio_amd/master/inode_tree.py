@@ -109,9 +109,12 @@ class InodeTree:
         self.pinned_ids: set[int] = set()
         self.to_be_persisted: set[int] = set()
         self.replication_limited: set[int] = set()
+        # bumped by every applied mutation: versions cached FileInfo replies (FileSystemMaster)
+        self.epoch = 0
 
     # ---- state ------------------------------------------------------------------------------
     def reset(self) -> None:
+        self.epoch += 1
         self.inodes.clear()
         self.children.clear()
         self.root = None
@@ -165,6 +168,7 @@ class InodeTree:
         try:
             return self._apply(e)
         finally:
+            self.epoch += 1
             self.inodes.end()
 
     def _apply(self, e) -> bool:

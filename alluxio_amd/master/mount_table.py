@@ -93,10 +93,12 @@ class MountTable:
     def __init__(self, ufs_manager: UfsManager):
         self._lock = threading.RLock()
         self._mounts: dict[str, MountInfo] = {}
+        self.epoch = 0          # bumped on every mount-table change (cached FileInfo.ufsPath)
         self.ufs_manager = ufs_manager
 
     def reset(self) -> None:
         with self._lock:
+            self.epoch += 1
             for m in self._mounts.values():
                 self.ufs_manager.remove_mount(m.mount_id)
             self._mounts = {}
@@ -104,6 +106,7 @@ class MountTable:
     # ---- state changes (called from journal application) ------------------------------------
     def apply_add(self, info: MountInfo) -> None:
         with self._lock:
+            self.epoch += 1
             # copy-on-write: readers use the dict they loaded without taking the lock
             m = dict(self._mounts)
             m[info.alluxio_path] = info
@@ -112,6 +115,7 @@ class MountTable:
 
     def apply_delete(self, alluxio_path: str) -> MountInfo | None:
         with self._lock:
+            self.epoch += 1
             m = dict(self._mounts)
             info = m.pop(alluxio_path, None)
             self._mounts = m

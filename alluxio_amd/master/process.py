@@ -218,7 +218,8 @@ class AlluxioMasterProcess:
             s.add_servicer(SVC_TABLE, TableMasterService(self.table_master))
         from .backup import SVC_BACKUP_WORKER
         s.add_servicer(SVC_BACKUP_WORKER, self.backup_worker)
-        s.add_servicer(SVC_VERSION, ServiceVersionHandler())
+        self._version_handler = ServiceVersionHandler()
+        s.add_servicer(SVC_VERSION, self._version_handler)
         s.add_servicer(SVC_SASL, SaslHandler())
 
     def format(self) -> None:
@@ -250,6 +251,16 @@ class AlluxioMasterProcess:
                 if not self.primary and spec.service != SVC_BACKUP_WORKER:
                     raise UnavailableException("master is a standby (not primary)")
             self.server.gate = standby_gate
+        self.native_rpc = None
+        if self.server.enable_grpc and self.conf.get_bool("alluxio.master.native.rpc.enabled", "true"):
+            # metadata fast path next to gRPC (same servicers): see alluxio_amd/rpc/native.py.
+            # Started first, so the port is advertised from the first gRPC call on.
+            from ..rpc.native import NativeRpcFrontend
+            self.native_rpc = NativeRpcFrontend(
+                self.server, self.server.host, self.conf.get_int("alluxio.master.native.rpc.port", "0"),
+                fast_threads=self.conf.get_int("alluxio.master.native.rpc.fast.threads", "2"),
+                blocking_threads=self.conf.get_int("alluxio.master.native.rpc.blocking.threads", "16"))
+            self._version_handler.native_port = self.native_rpc.start()
         addr = self.server.start()
         self.meta_master.master_address = addr
         self.start_time = time.time()
@@ -385,6 +396,9 @@ class AlluxioMasterProcess:
         if self.web is not None:
             self.web.stop()
             self.web = None
+        if getattr(self, "native_rpc", None) is not None:
+            self.native_rpc.stop()
+            self.native_rpc = None
         self.server.stop()
         if self._job_client_fs is not None:
             self._job_client_fs.close()

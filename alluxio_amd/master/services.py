@@ -7,6 +7,7 @@ MetricsMasterClientServiceHandler, ServiceVersionClientServiceHandler.
 """
 from __future__ import annotations
 
+from ..rpc.marshal import RawReply, length_delimited
 from ..proto import enum_name, pb
 from ..security.acl import bits_from_proto, mode_from_pmode
 
@@ -103,20 +104,18 @@ class FileSystemMasterClientServiceHandler:
         o = req.options
         lt = LOAD_TYPES.get(o.loadMetadataType, "ONCE") if o.HasField("loadMetadataType") else "ONCE"
         fi = self.m.get_status(req.path, load_metadata=lt, sync_interval_ms=_sync_interval(o),
-                               access_mode=bits_from_proto(o.accessMode) if o.HasField("accessMode") else 4)
-        return pb.file.GetStatusPResponse(fileInfo=fi)
+                               access_mode=bits_from_proto(o.accessMode) if o.HasField("accessMode") else 4,
+                               raw=True)
+        # cached serialized FileInfo -> GetStatusPResponse{fileInfo=1} without a protobuf round trip
+        return RawReply(length_delimited(0x0A, fi), pb.file.GetStatusPResponse)
 
     def ListStatus(self, req, ctx):
         o = req.options
         lt = LOAD_TYPES.get(o.loadMetadataType, "ONCE") if o.HasField("loadMetadataType") else "ONCE"
-        infos = self.m.list_status(req.path, recursive=o.recursive, load_metadata=lt,
-                                   sync_interval_ms=_sync_interval(o))
-        batch = 10000
-        if not infos:
-            yield pb.file.ListStatusPResponse()
-            return
-        for i in range(0, len(infos), batch):
-            yield pb.file.ListStatusPResponse(fileInfos=infos[i:i + batch])
+        bodies = self.m.list_status(req.path, recursive=o.recursive, load_metadata=lt,
+                                    sync_interval_ms=_sync_interval(o), raw=True)
+        for b in bodies:       # ListStatusPResponse{fileInfos=1*}, <= 10000 entries each
+            yield RawReply(b, pb.file.ListStatusPResponse)
 
     def Mount(self, req, ctx):
         o = req.options
@@ -290,10 +289,16 @@ class BlockMasterWorkerServiceHandler:
 
 
 class ServiceVersionHandler:
+    """Service versions; also advertises the native framed-RPC port (``nativeRpcPort``, an
+    extension field Java clients ignore) through which our clients reach the same services."""
     VERSIONS = {i: 1 for i in range(17)}
 
+    def __init__(self):
+        self.native_port = 0
+
     def getServiceVersion(self, req, ctx):
-        return pb.version.GetServiceVersionPResponse(version=self.VERSIONS.get(req.serviceType, 1))
+        return pb.version.GetServiceVersionPResponse(version=self.VERSIONS.get(req.serviceType, 1),
+                                                     nativeRpcPort=self.native_port)
 
 
 class SaslHandler:

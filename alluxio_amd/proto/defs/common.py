@@ -61,7 +61,7 @@ enum ServiceType UNKNOWN_SERVICE=0 FILE_SYSTEM_MASTER_CLIENT_SERVICE=1
     JOURNAL_MASTER_CLIENT_SERVICE=13 TABLE_MASTER_CLIENT_SERVICE=14
     META_MASTER_BACKUP_MESSAGING_SERVICE=15 RAFT_JOURNAL_SERVICE=16
 msg GetServiceVersionPRequest serviceType=1:ServiceType
-msg GetServiceVersionPResponse version=1:i64
+msg GetServiceVersionPResponse version=1:i64 nativeRpcPort=1000:i32
 rpc ServiceVersionClientService getServiceVersion GetServiceVersionPRequest GetServiceVersionPResponse
 
 package alluxio.grpc.sasl

@@ -27,6 +27,11 @@ from . import marshal
 LOG = logging.getLogger(__name__)
 
 
+def _native_stream_services():
+    from .native import STREAM_SERVICES
+    return STREAM_SERVICES
+
+
 class _LocalRegistry(dict):
     """service full name -> servicer, plus liveness/gate shared with the owning RpcServer."""
 
@@ -39,6 +44,13 @@ _LOCAL: dict[str, _LocalRegistry] = {}   # address -> registry
 _LOCAL_LOCK = threading.Lock()
 
 MAX_MESSAGE = 100 << 20
+
+# services a client reaches through the master's native framed-RPC front end when offered
+NATIVE_SERVICES = frozenset({
+    "alluxio.grpc.file.FileSystemMasterClientService",
+    "alluxio.grpc.block.BlockMasterClientService",
+    "alluxio.grpc.meta.MetaMasterClientService",
+})
 
 
 class RpcContext:
@@ -268,8 +280,8 @@ class _LocalMethod:
         ctx = RpcContext(metadata)
         with as_user(self.user):
             if self.spec.server_streaming:
-                return list(self.fn(request, ctx))
-            return self.fn(request, ctx)
+                return [marshal.materialize(r) for r in self.fn(request, ctx)]
+            return marshal.materialize(self.fn(request, ctx))
 
 
 class _GrpcMethod:
@@ -300,9 +312,13 @@ class Stub:
 
 class Channel:
     def __init__(self, address: str, user: str | None = None, force_grpc: bool = False, auth="default",
-                 zero_copy: bool = True):
+                 zero_copy: bool = True, native: bool = True):
         self.address = address
         self.user = user
+        # unary master calls over the native framed-RPC front end when the server offers one
+        self.native = native
+        self._native = None
+        self._native_probed = False
         if auth == "default":      # SIMPLE as the login user (servers without SASL are tolerated)
             from ..security import login_user
             auth = ("SIMPLE", user or login_user(), "")
@@ -367,6 +383,31 @@ class Channel:
             md.append(("channel-id", self.channel_id))
         return tuple(md) or None
 
+    def _native_core(self):
+        """Native framed-RPC connection to this server when it advertises one (probed once over
+        gRPC with getServiceVersion; see rpc/native.py), else None."""
+        if not self.native:
+            return None
+        with self._lock:
+            # a server without a native port is re-probed after a while (it may enable one)
+            if self._native_probed and (self._native is not None or time.time() < self._native_probed):
+                return self._native
+            self._native_probed = time.time() + 30.0
+        core = None
+        try:
+            from ..proto import pb
+            spec = SERVICES["alluxio.grpc.version.ServiceVersionClientService"]["getServiceVersion"]
+            c = self._channel().unary_unary(spec.path, spec.request.SerializeToString, spec.response.FromString)
+            r = c(pb.version.GetServiceVersionPRequest(), timeout=10, metadata=self._md())
+            if r.nativeRpcPort:
+                from .native import NativeChannelCore
+                core = NativeChannelCore(self.address.rsplit(":", 1)[0], r.nativeRpcPort, self.auth)
+        except Exception:  # noqa: BLE001 - no native front end: gRPC only
+            LOG.debug("native rpc probe of %s failed", self.address, exc_info=True)
+        with self._lock:
+            self._native = core
+        return core
+
     def method(self, service, spec):
         if self.local is not None:
             servicer = self.local.get(service)
@@ -375,6 +416,11 @@ class Channel:
                     raise ex.UnimplementedException(f"{spec.path} not served at {self.address}")
                 return missing
             return _LocalMethod(servicer, spec, self.user, getattr(self.local, "server", None))
+        if not spec.client_streaming and service in NATIVE_SERVICES and \
+                (not spec.server_streaming or service in _native_stream_services()):
+            core = self._native_core()
+            if core is not None:
+                return core.method(spec)
         ch = self._channel()
         ser, des = spec.request.SerializeToString, spec.response.FromString
         if spec.client_streaming and spec.server_streaming:
@@ -416,6 +462,10 @@ class Channel:
     def close(self) -> None:
         with self._lock:
             self._stubs = {}
+            if self._native is not None:
+                self._native.close()
+                self._native = None
+            self._native_probed = False
             if self._grpc is not None:
                 self._grpc.close()
                 self._grpc = None
@@ -441,8 +491,10 @@ class ChannelPool:
                 force = self.conf is not None and not self.conf.get_bool(
                     "alluxio.user.network.inprocess.transport.enabled", "true")
                 zc = self.conf is None or self.conf.get_bool("alluxio.user.streaming.zerocopy.enabled", "true")
+                nat = self.conf is None or self.conf.get_bool("alluxio.user.network.native.rpc.enabled", "true")
                 c = self._chans[key] = Channel(address, user, force_grpc=force,
-                                               auth=client_auth_from_conf(self.conf, user), zero_copy=zc)
+                                               auth=client_auth_from_conf(self.conf, user), zero_copy=zc,
+                                               native=nat)
             return c
 
     def drop(self, address: str, user: str | None = None) -> None:

@@ -141,6 +141,33 @@ def serialize(msg) -> bytes:
     return msg.SerializeToString()
 
 
+def length_delimited(tag: int, payload: bytes) -> bytes:
+    """``tag`` (one byte: field number << 3 | 2) + varint length + payload."""
+    return b"".join((bytes((tag,)), _varint(len(payload)), payload))
+
+
+class RawReply:
+    """A reply that is already serialized (cached metadata replies).  gRPC and the native
+    transport send ``data`` as is (``SerializeToString``); the in-process transport parses it
+    (``materialize``) so callers always receive a message."""
+
+    __slots__ = ("data", "type")
+
+    def __init__(self, data: bytes, msg_type):
+        self.data = data
+        self.type = msg_type
+
+    def SerializeToString(self) -> bytes:  # noqa: N802 - protobuf message protocol
+        return self.data
+
+    def materialize(self):
+        return self.type.FromString(self.data)
+
+
+def materialize(reply):
+    return reply.materialize() if isinstance(reply, RawReply) else reply
+
+
 BLOCK_WORKER = "alluxio.grpc.block.BlockWorker"
 # (service, method) -> (request deserializer, response deserializer) replacing protobuf parsing
 _ZERO_COPY = {

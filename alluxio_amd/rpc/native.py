@@ -1,0 +1,213 @@
+"""Native framed-RPC transport for unary calls (see ``csrc/frame_rpc.h``).
+
+Server side: :class:`NativeRpcFrontend` serves every unary method of an :class:`RpcServer`'s
+servicers through ``_C.FrameRpcServer``: C++ I/O threads decode frames and queue them per *lane*;
+Python dispatcher threads take a batch per GIL acquisition, run the same servicer method the gRPC
+handler would (same user binding, gate, error -> status mapping) and send the serialized reply.
+Read-only metadata methods use the ``fast`` lane (few threads, large batches: nothing in them
+blocks); everything else uses the ``blocking`` lane (many threads, one request each, so a call
+waiting for its journal flush never holds up another request — group commit needs concurrency).
+
+Client side: :class:`NativeChannelCore` wraps ``_C.FrameRpcClient`` (connection pool, GIL released
+for the whole call).  :class:`alluxio_amd.rpc.Channel` switches its unary methods to it once the
+server advertised a native port (``getServiceVersion`` -> ``nativeRpcPort``).
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+
+from ..proto import SERVICES
+from ..utils import exceptions as ex
+
+LOG = logging.getLogger(__name__)
+
+# methods that never block on a journal flush, UFS call or lock wait beyond the namespace lock
+FAST_METHODS = frozenset({
+    "GetStatus", "ListStatus", "Exists", "CheckAccess", "GetMountTable", "GetFilePath", "GetSyncPathList",
+    "getServiceVersion", "GetBlockInfo", "GetWorkerInfoList", "GetCapacityBytes", "GetUsedBytes",
+    "GetBlockMasterInfo", "GetConfiguration", "GetMasterInfo", "GetStateLockHolders", "GetPinnedFileIds",
+    "GetUfsInfo", "GetFileInfo",
+})
+AUTH_PATH = "@auth"
+# services whose server-streaming methods are served natively (bounded metadata replies)
+STREAM_SERVICES = frozenset({"alluxio.grpc.file.FileSystemMasterClientService"})
+
+
+class _Ctx:
+    """ServicerContext stand-in (the servicers only read metadata / abort)."""
+
+    def __init__(self, user):
+        self._md = (("alluxio-user", user),) if user else ()
+
+    def invocation_metadata(self):
+        return self._md
+
+    def is_active(self):
+        return True
+
+    def abort(self, code, details):
+        raise ex.AlluxioStatusException.from_status(code.value[0] if hasattr(code, "value") else code, details)
+
+    def set_code(self, code):
+        pass
+
+    def set_details(self, details):
+        pass
+
+    def peer(self):
+        return "native"
+
+
+def auth_payload(auth) -> bytes:
+    """Handshake payload for ``Channel.auth`` = (type, user, password) or None (NOSASL)."""
+    if auth is None:
+        return b"NOSASL\0\0"
+    t, user, password = auth
+    return f"{t}\0{user or ''}\0{password or ''}".encode()
+
+
+class NativeRpcFrontend:
+    def __init__(self, rpc_server, host: str, port: int = 0, fast_threads: int = 2, blocking_threads: int = 32,
+                 io_threads: int = 2, batch: int = 64):
+        from ..ops.native import lib
+        self.rpc = rpc_server
+        self.methods = [(AUTH_PATH, None, None)]
+        lanes = [0]
+        for svc, servicer in rpc_server._servicers.items():
+            for name, spec in SERVICES[svc].items():
+                # unary requests only; a server-streaming reply travels as one frame of
+                # length-prefixed messages (metadata listings, not data streams)
+                if spec.client_streaming or not hasattr(servicer, name):
+                    continue
+                if spec.server_streaming and svc not in STREAM_SERVICES:
+                    continue
+                self.methods.append((spec.path, spec, getattr(servicer, name)))
+                lanes.append(0 if name in FAST_METHODS else 1)
+        self.server = lib().FrameRpcServer(host, port, [m[0] for m in self.methods], lanes, io_threads)
+        self.fast_threads, self.blocking_threads, self.batch = fast_threads, blocking_threads, batch
+        self._threads: list[threading.Thread] = []
+        self._running = False
+        self.port = None
+
+    def start(self) -> int:
+        self.server.start()
+        self.port = self.server.port
+        self._running = True
+        for lane, n, batch in ((0, self.fast_threads, self.batch), (1, self.blocking_threads, 1)):
+            for i in range(n):
+                t = threading.Thread(target=self._loop, args=(lane, batch), daemon=True,
+                                     name=f"native-rpc-{lane}-{i}")
+                t.start()
+                self._threads.append(t)
+        return self.port
+
+    def stop(self) -> None:
+        self._running = False
+        self.server.stop()
+        for t in self._threads:
+            t.join(timeout=2)
+        self._threads = []
+
+    # ---- dispatch -------------------------------------------------------------------------------
+    def _auth(self, token, payload: bytes):
+        parts = payload.split(b"\0")
+        atype, user, password = (p.decode() for p in (parts + [b"", b"", b""])[:3])
+        auth = self.rpc.authenticator
+        if auth is not None:
+            if atype.upper() != auth.auth_type:
+                raise ex.UnauthenticatedException(f"client uses {atype} authentication, server expects "
+                                                  f"{auth.auth_type}")
+            auth.provider.authenticate(user, password)
+        self.server.set_user(token, user)
+
+    def _one(self, token, midx, user, payload):
+        from ..security import as_user
+        try:
+            if midx == 0:
+                self._auth(token, payload)
+                return (token, 0, "", b"")
+            if self.rpc.authenticator is not None and not user:
+                raise ex.UnauthenticatedException("native channel is not authenticated")
+            path, spec, fn = self.methods[midx]
+            self.rpc.check(spec)
+            req = spec.request.FromString(payload)
+            with as_user(user or None):
+                if spec.server_streaming:
+                    parts = []
+                    for m in fn(req, _Ctx(user)):
+                        b = m.SerializeToString()
+                        parts.append(len(b).to_bytes(4, "little"))
+                        parts.append(b)
+                    return (token, 0, "", b"".join(parts))
+                resp = fn(req, _Ctx(user))
+            return (token, 0, "", resp.SerializeToString())
+        except Exception as e:  # noqa: BLE001
+            se = ex.wrap(e)
+            if not isinstance(e, ex.AlluxioStatusException):
+                LOG.debug("native rpc %s failed", self.methods[midx][0], exc_info=True)
+            return (token, int(se.status), se.message or str(se), b"")
+
+    def _loop(self, lane: int, batch: int) -> None:
+        srv = self.server
+        metrics = self.rpc.metrics
+        while self._running:
+            try:
+                reqs = srv.poll(lane, batch, 100)
+            except Exception:  # noqa: BLE001 - server stopped
+                if not self._running:
+                    return
+                time.sleep(0.01)
+                continue
+            if not reqs:
+                continue
+            t0 = time.perf_counter()
+            out = [self._one(*r) for r in reqs]
+            srv.respond_many(out)
+            if metrics is not None:
+                metrics.counter("NativeRpcCalls").inc(len(reqs))
+                metrics.timer("NativeRpcBatch").update(time.perf_counter() - t0)
+
+
+class NativeChannelCore:
+    """Client half: one pooled native connection set to ``host:port``."""
+
+    def __init__(self, host: str, port: int, auth, timeout_ms: int = 60_000):
+        from ..ops.native import lib
+        self.client = lib().FrameRpcClient(host, port, auth_payload(auth), timeout_ms)
+        self.address = f"{host}:{port}"
+
+    def method(self, spec):
+        return _NativeMethod(self, spec)
+
+    def close(self) -> None:
+        self.client.close()
+
+
+class _NativeMethod:
+    __slots__ = ("core", "spec", "path", "des", "stream")
+
+    def __init__(self, core: NativeChannelCore, spec):
+        self.core = core
+        self.spec = spec
+        self.path = spec.path
+        self.des = spec.response.FromString
+        self.stream = spec.server_streaming
+
+    def __call__(self, request, timeout=None, metadata=None):
+        try:
+            status, msg, payload = self.core.client.call(self.path, request.SerializeToString(),
+                                                         int(timeout * 1000) if timeout else 0)
+        except RuntimeError as e:
+            raise ex.UnavailableException(str(e)) from None
+        if status:
+            raise ex.AlluxioStatusException.from_status(status, msg)
+        if self.stream:
+            out, pos, n = [], 0, len(payload)
+            while pos < n:
+                ln = int.from_bytes(payload[pos:pos + 4], "little")
+                out.append(self.des(payload[pos + 4:pos + 4 + ln]))
+                pos += 4 + ln
+            return out
+        return self.des(payload)

@@ -96,7 +96,7 @@ def test_bench_cpu_smoke(tmp_path, capsys):
     sys.path.insert(0, ROOT)
     import bench
     rc = bench.main(["--steps", "5", "--warmup", "1", "--threads", "8", "--file-size", "8m", "--block-size", "4m",
-                     "--buffer-size", "1m", "--page-size", "1m", "--dest", "host", "--work-dir", str(tmp_path)])
+                     "--buffer-size", "1m", "--page-size", "1m", "--duration", "0.1", "--work-dir", str(tmp_path)])
     assert rc == 0
     line = capsys.readouterr().out.strip().splitlines()[-1]
     out = json.loads(line)

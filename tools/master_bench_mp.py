@@ -31,6 +31,7 @@ from alluxio_amd.client.file_system import FileSystem
 from alluxio_amd.stress import master_bench
 fs = FileSystem(master_address={addr!r})
 r = master_bench.main({args!r}, fs=fs, print_result=False)
+r["native"] = str(fs.ctx.pool.get({addr!r}, fs.ctx.user)._native)
 print("RESULT " + json.dumps(r))
 fs.close()
 """
