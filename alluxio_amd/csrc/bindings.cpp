@@ -378,7 +378,19 @@ PYBIND11_MODULE(_C, m) {
              py::gil_scoped_release rel;
              for (auto& x : v) s.respond(std::get<0>(x), std::get<1>(x), std::get<2>(x), std::get<3>(x));
            })
-      .def("set_user", &FrameRpcServer::set_user);
+      .def("set_user", &FrameRpcServer::set_user)
+      .def("set_cacheable", &FrameRpcServer::set_cacheable)
+      .def("epoch", &FrameRpcServer::epoch)
+      .def("bump_epoch", &FrameRpcServer::bump_epoch)
+      .def("cache_put", [](FrameRpcServer& s, uint32_t method, const std::string& user, py::bytes request,
+                           py::bytes reply, uint64_t ep) {
+             std::string rq = request, rp = reply;
+             s.cache_put(method, user, rq, rp, ep);
+           })
+      .def("cache_clear", &FrameRpcServer::cache_clear)
+      .def("set_cache_capacity", &FrameRpcServer::set_cache_capacity)
+      .def_property_readonly("cache_size", &FrameRpcServer::cache_size)
+      .def_property_readonly("cache_hits", &FrameRpcServer::cache_hits);
   py::class_<FrameRpcClient>(m, "FrameRpcClient")
       .def(py::init<const std::string&, int, const std::string&, int>(), py::arg("host"), py::arg("port"),
            py::arg("auth"), py::arg("timeout_ms") = 60000)

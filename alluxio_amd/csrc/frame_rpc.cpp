@@ -128,6 +128,69 @@ FrameRpcServer::FrameRpcServer(const std::string& host, int port, const std::vec
     nl = std::max(nl, lanes[i] + 1);
   }
   for (int i = 0; i < nl; ++i) lane_q_.emplace_back(new Lane());
+  cacheable_.assign(methods.size(), 0);
+}
+
+// ---- reply cache --------------------------------------------------------------------------
+std::string FrameRpcServer::cache_key(uint32_t method, const std::string& user, const char* req, size_t n) {
+  std::string k;
+  k.reserve(4 + user.size() + 1 + n);
+  put_u32(k, method);
+  k += user;
+  k.push_back('\0');
+  k.append(req, n);
+  return k;
+}
+
+void FrameRpcServer::set_cacheable(uint32_t method, bool on) {
+  if (method < cacheable_.size()) cacheable_[method] = on ? 1 : 0;
+}
+
+bool FrameRpcServer::cache_get(const std::string& key, std::string* reply) {
+  const uint64_t ep = epoch();
+  CacheShard& sh = shards_[std::hash<std::string>{}(key) % kShards];
+  std::lock_guard<std::mutex> g(sh.mu);
+  if (sh.epoch != ep) {   // stale shard: every entry predates a metadata change
+    sh.map.clear();
+    sh.epoch = ep;
+    return false;
+  }
+  auto it = sh.map.find(key);
+  if (it == sh.map.end()) return false;
+  *reply = it->second;
+  return true;
+}
+
+void FrameRpcServer::cache_put(uint32_t method, const std::string& user, const std::string& request,
+                               const std::string& reply, uint64_t ep) {
+  if (method >= cacheable_.size() || !cacheable_[method]) return;
+  if (ep != epoch()) return;   // something changed while the reply was computed
+  std::string key = cache_key(method, user, request.data(), request.size());
+  CacheShard& sh = shards_[std::hash<std::string>{}(key) % kShards];
+  std::lock_guard<std::mutex> g(sh.mu);
+  if (sh.epoch != ep) {
+    if (sh.epoch > ep) return;   // the shard already moved to a newer epoch
+    sh.map.clear();
+    sh.epoch = ep;
+  }
+  if (sh.map.size() >= cache_cap_ / kShards + 1) sh.map.clear();
+  sh.map[std::move(key)] = reply;
+}
+
+void FrameRpcServer::cache_clear() {
+  for (auto& sh : shards_) {
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.map.clear();
+  }
+}
+
+size_t FrameRpcServer::cache_size() {
+  size_t n = 0;
+  for (auto& sh : shards_) {
+    std::lock_guard<std::mutex> g(sh.mu);
+    n += sh.map.size();
+  }
+  return n;
 }
 
 FrameRpcServer::~FrameRpcServer() { stop(); }
@@ -299,6 +362,18 @@ void FrameRpcServer::on_readable(const std::shared_ptr<Conn>& c, int ep) {
       const std::string resp = make_response(call_id, 12 /*UNIMPLEMENTED*/, "unknown method " + path, "");
       std::lock_guard<std::mutex> g(c->wmu);
       send_all(c->fd, resp.data(), resp.size(), 5000);
+    } else if (cacheable_[it->second] && [&] {
+                 std::string reply;
+                 const std::string key = cache_key(it->second, user, p + 6 + plen, len - 6 - plen);
+                 if (!cache_get(key, &reply)) return false;
+                 const std::string resp = make_response(call_id, 0, std::string(), reply);
+                 requests_.fetch_add(1, std::memory_order_relaxed);
+                 cache_hits_.fetch_add(1, std::memory_order_relaxed);
+                 std::lock_guard<std::mutex> g(c->wmu);
+                 if (!send_all(c->fd, resp.data(), resp.size(), 30000)) eof = true;
+                 return true;
+               }()) {
+      // answered from the reply cache on this I/O thread
     } else {
       FrameRequest rq;
       rq.token = ((uint64_t)c->id << 32) | call_id;

@@ -52,6 +52,22 @@ class FrameRpcServer {
   void set_user(uint64_t token, const std::string& user);
   uint64_t requests() const { return requests_.load(); }
 
+  // ---- reply cache (read-only metadata methods) --------------------------------------------
+  // A request of a cacheable method whose (method, user, request bytes) were answered while the
+  // metadata epoch had its current value is answered on the I/O thread, without Python.  Python
+  // bumps the epoch inside every critical section that changes state a cached reply depends on
+  // (namespace, block locations, mount table) and tags each put with the epoch it read BEFORE
+  // running the handler, so a reply computed across a change is never served.
+  void set_cacheable(uint32_t method, bool on);
+  uint64_t epoch() const { return epoch_.load(std::memory_order_acquire); }
+  void bump_epoch() { epoch_.fetch_add(1, std::memory_order_acq_rel); }
+  void cache_put(uint32_t method, const std::string& user, const std::string& request, const std::string& reply,
+                 uint64_t epoch);
+  void cache_clear();
+  uint64_t cache_hits() const { return cache_hits_.load(); }
+  size_t cache_size();
+  void set_cache_capacity(size_t entries) { cache_cap_ = entries; }
+
  private:
   struct Conn;
   void accept_loop();
@@ -81,6 +97,24 @@ class FrameRpcServer {
   std::vector<std::unique_ptr<Lane>> lane_q_;
   std::atomic<uint64_t> requests_{0};
   int wake_fd_ = -1;
+
+  static std::string cache_key(uint32_t method, const std::string& user, const char* req, size_t n);
+  bool cache_get(const std::string& key, std::string* reply);
+  struct CacheEntry {
+    uint64_t epoch;
+    std::string reply;
+  };
+  struct CacheShard {
+    std::mutex mu;
+    uint64_t epoch = 0;   // entries are all of this epoch; a newer put/get resets the shard
+    std::unordered_map<std::string, std::string> map;
+  };
+  static constexpr int kShards = 16;
+  CacheShard shards_[kShards];
+  std::vector<uint8_t> cacheable_;
+  std::atomic<uint64_t> epoch_{1};
+  std::atomic<uint64_t> cache_hits_{0};
+  size_t cache_cap_ = 200000;
 };
 
 // Client side: a pool of blocking connections; call() is thread-safe, one in-flight call per

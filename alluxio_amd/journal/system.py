@@ -9,6 +9,8 @@ UfsJournalCheckpointThread (standby tails logs and writes checkpoints), NoopJour
 """
 from __future__ import annotations
 
+import heapq
+import itertools
 import logging
 import threading
 import time
@@ -18,6 +20,25 @@ from . import format as fmt
 from .ufs_journal import UfsJournal, UfsJournalLogWriter
 
 LOG = logging.getLogger(__name__)
+
+_DEFER = threading.local()
+
+
+class deferred_flush:
+    """Inside this context, ``JournalContext.close()`` does not block for durability: it records
+    ``(writer, counter)`` in ``pending`` and the caller completes the RPC from a flush callback
+    (``AsyncJournalWriter.flush_async``).  This is group commit without a parked thread per
+    request: the RPC front end answers every mutation of a flush batch when that flush lands."""
+
+    def __enter__(self):
+        self.pending: dict = {}
+        self._prev = getattr(_DEFER, "pending", None)
+        _DEFER.pending = self.pending
+        return self
+
+    def __exit__(self, *exc):
+        _DEFER.pending = self._prev
+        return False
 
 
 class Journaled:
@@ -59,6 +80,8 @@ class AsyncJournalWriter:
         self._requested = 0      # highest counter a caller is waiting for
         self._error: BaseException | None = None
         self._closed = False
+        self._waiters: list = []   # heap of (counter, seq, callback) for flush_async
+        self._seq = itertools.count()
         self._thread = threading.Thread(target=self._run, daemon=True, name="journal-flush")
         self._thread.start()
 
@@ -88,7 +111,45 @@ class AsyncJournalWriter:
                     raise UnavailableException("journal flush timed out")
                 self._cond.wait(min(rem, 0.05))
 
+    def flush_async(self, counter: int, cb) -> None:
+        """Call ``cb(None)`` once entries up to ``counter`` are durable (``cb(exc)`` on failure);
+        runs ``cb`` on the flush thread, or inline when already flushed."""
+        err = None
+        with self._cond:
+            if self._error is not None:
+                err = UnavailableException(f"journal flush failed: {self._error}")
+            elif self._flushed < counter:
+                if self._closed and not self._queue:
+                    err = JournalClosedException("journal closed before flush")
+                else:
+                    heapq.heappush(self._waiters, (counter, next(self._seq), cb))
+                    if counter > self._requested:
+                        self._requested = counter
+                        self._cond.notify_all()
+                    return
+        cb(err)
+
+    def _fire(self, flushed: int, err=None) -> None:
+        ready = []
+        with self._cond:
+            while self._waiters and (err is not None or self._waiters[0][0] <= flushed):
+                ready.append(heapq.heappop(self._waiters)[2])
+        for cb in ready:
+            try:
+                cb(err)
+            except Exception:  # noqa: BLE001
+                LOG.exception("journal flush callback failed")
+
     def _run(self) -> None:
+        try:
+            self._run_loop()
+        finally:
+            with self._cond:
+                closed_err = self._error
+            self._fire(0, UnavailableException(f"journal flush failed: {closed_err}") if closed_err
+                       else JournalClosedException("journal closed before flush"))
+
+    def _run_loop(self) -> None:
         while True:
             with self._cond:
                 # stand still until entries are queued and someone waits for them (or the batch
@@ -123,8 +184,10 @@ class AsyncJournalWriter:
                 self.writer.flush()
                 with self._cond:
                     self._written += n
-                    self._flushed = self._written
+                    self._flushed = flushed = self._written
                     self._cond.notify_all()
+                if self._waiters:
+                    self._fire(flushed)
             except BaseException as e:  # noqa: BLE001
                 LOG.exception("journal flush failed")
                 with self._cond:
@@ -154,7 +217,12 @@ class JournalContext:
 
     def close(self) -> None:
         if self._writer is not None and self._last:
-            self._writer.flush(self._last)
+            pending = getattr(_DEFER, "pending", None)
+            if pending is not None and hasattr(self._writer, "flush_async"):
+                w = self._writer
+                pending[w] = max(pending.get(w, 0), self._last)
+            else:
+                self._writer.flush(self._last)
 
     def __enter__(self):
         if self._state_lock is not None:

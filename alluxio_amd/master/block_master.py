@@ -94,21 +94,27 @@ class BlockMaster(Journaled):
         # bumped whenever a block's length/locations or the live-worker set change: versions the
         # FileSystemMaster's cached FileInfo replies (they embed block locations)
         self.location_epoch = 0
+        self.epoch_listeners: list = []
         self.lost_worker_listeners = []
         self.worker_registered_listeners = []
         self.safe_mode = None
 
+    def _bump_epoch(self) -> None:
+        self.location_epoch += 1
+        for cb in self.epoch_listeners:
+            cb()
+
     # ---- Journaled ----------------------------------------------------------------------------
     def reset_state(self) -> None:
         with self._lock:
-            self.location_epoch += 1
+            self._bump_epoch()
             self._blocks.clear()
             self._next_container = 0
             self._container_limit = 0
 
     def process_journal_entry(self, e) -> bool:
         with self._lock:
-            self.location_epoch += 1
+            self._bump_epoch()
             if e.HasField("block_container_id_generator"):
                 self._container_limit = e.block_container_id_generator.next_container_id
                 self._next_container = max(self._next_container, self._container_limit)
@@ -189,7 +195,7 @@ class BlockMaster(Journaled):
                 if w is None:
                     raise NotFoundException(f"Could not find worker id: {wid} to register.")
                 self._lost.remove(w)
-            self.location_epoch += 1
+            self._bump_epoch()
             self._temp.remove(w)
             self._registered.remove(w)
             w.registered = True
@@ -221,7 +227,7 @@ class BlockMaster(Journaled):
             return
         if m.locations.get(w.id) != (tier, medium):
             m.locations[w.id] = (tier, medium)
-            self.location_epoch += 1
+            self._bump_epoch()
         w.blocks.add(bid)
         self._lost_blocks.discard(bid)
 
@@ -238,7 +244,7 @@ class BlockMaster(Journaled):
             if lost_storage:
                 w.lost_storage.update(lost_storage)
             if removed:
-                self.location_epoch += 1
+                self._bump_epoch()
             for bid in removed:
                 m = self._blocks.get(bid)
                 if m is not None:
@@ -431,7 +437,7 @@ class BlockMaster(Journaled):
         return lost
 
     def _process_lost(self, w: MasterWorkerInfo) -> None:
-        self.location_epoch += 1
+        self._bump_epoch()
         for bid in w.blocks:
             m = self._blocks.get(bid)
             if m is not None:

@@ -237,6 +237,12 @@ class FileSystemMaster(Journaled):
 
     # ------------------------------------------------------------------------------------------
     # FileInfo
+    def add_epoch_listener(self, cb) -> None:
+        """``cb()`` runs inside every critical section that changes state a cached FileInfo /
+        listing reply depends on (namespace, block locations, mount table)."""
+        for holder in (self.tree, self.block_master, self.mount_table):
+            holder.epoch_listeners.append(cb)
+
     def _cache_epoch(self):
         return (self.tree.epoch, self.block_master.location_epoch, self.mount_table.epoch)
 

@@ -57,6 +57,7 @@ class TtlBuckets:
         self.interval = max(1, interval_ms)
         self._buckets: dict[int, set[int]] = {}
         self._starts: list[int] = []
+        self._of: dict[int, int] = {}     # inode id -> its bucket start
         self._lock = threading.Lock()
 
     def _start(self, expiry_ms: int) -> int:
@@ -71,12 +72,17 @@ class TtlBuckets:
                 self._buckets[s] = set()
                 bisect.insort(self._starts, s)
             self._buckets[s].add(inode.id)
+            self._of[inode.id] = s
 
     def remove(self, inode: Inode) -> None:
+        if inode.id not in self._of:      # GIL-atomic probe: most inodes have no TTL
+            return
         with self._lock:
-            for s in list(self._buckets):
-                self._buckets[s].discard(inode.id)
-                if not self._buckets[s]:
+            s = self._of.pop(inode.id, None)
+            b = self._buckets.get(s) if s is not None else None
+            if b is not None:
+                b.discard(inode.id)
+                if not b:
                     del self._buckets[s]
                     self._starts.remove(s)
 
@@ -93,6 +99,7 @@ class TtlBuckets:
         with self._lock:
             self._buckets.clear()
             self._starts.clear()
+            self._of.clear()
 
 
 class InodeTree:
@@ -111,10 +118,16 @@ class InodeTree:
         self.replication_limited: set[int] = set()
         # bumped by every applied mutation: versions cached FileInfo replies (FileSystemMaster)
         self.epoch = 0
+        self.epoch_listeners: list = []   # called after every bump (native reply cache)
+
+    def _bump_epoch(self) -> None:
+        self.epoch += 1
+        for cb in self.epoch_listeners:
+            cb()
 
     # ---- state ------------------------------------------------------------------------------
     def reset(self) -> None:
-        self.epoch += 1
+        self._bump_epoch()
         self.inodes.clear()
         self.children.clear()
         self.root = None
@@ -168,113 +181,126 @@ class InodeTree:
         try:
             return self._apply(e)
         finally:
-            self.epoch += 1
+            self._bump_epoch()
             self.inodes.end()
 
     def _apply(self, e) -> bool:
-        if e.HasField("inode_directory"):
-            self._add(InodeDirectory.from_entry(e.inode_directory))
-        elif e.HasField("inode_file"):
-            self._add(InodeFile.from_entry(e.inode_file))
-        elif e.HasField("inode_directory_id_generator"):
-            self.dir_ids.apply(e.inode_directory_id_generator)
-        elif e.HasField("update_inode"):
-            u = e.update_inode
-            inode = self.inodes.get(u.id)
-            if inode is None:
+        # one C-level ListFields() instead of a HasField probe per entry type
+        for fd, val in e.ListFields():
+            h = _APPLY.get(fd.name)
+            if h is not None:
+                h(self, val)
                 return True
-            old_parent, old_name = inode.parent_id, inode.name
-            inode.update_from(u)
-            if (inode.parent_id, inode.name) != (old_parent, old_name):
-                kids = self.children.get(old_parent)
-                if kids is not None and kids.get(old_name) == inode.id:
-                    del kids[old_name]
-                self.children.setdefault(inode.parent_id, {})[inode.name] = inode.id
-            self._index(inode)
-        elif e.HasField("update_inode_directory"):
-            u = e.update_inode_directory
-            d = self.inodes.get(u.id)
-            if d is not None and d.is_directory:
-                if u.HasField("mount_point"):
-                    d.mount_point = u.mount_point
-                if u.HasField("direct_children_loaded"):
-                    d.direct_children_loaded = u.direct_children_loaded
-                if u.HasField("defaultAcl"):
-                    from ..security.acl import AccessControlList
-                    d.default_acl = AccessControlList.from_proto(u.defaultAcl)
-        elif e.HasField("update_inode_file"):
-            u = e.update_inode_file
-            f = self.inodes.get(u.id)
-            if f is not None and f.is_file:
-                f.update_file_from(u)
-                self._index(f)
-        elif e.HasField("delete_file"):
-            inode = self.inodes.get(e.delete_file.id)
-            if inode is not None:
-                self._remove(inode)
-        elif e.HasField("rename"):
-            r = e.rename
-            inode = self.inodes.get(r.id)
-            if inode is not None:
-                new_parent, new_name = r.new_parent_id, r.new_name
-                if r.HasField("dst_path") and not r.HasField("new_parent_id"):
-                    # 1.x entries name the destination by path; resolve it against the tree as
-                    # replayed so far (InodeTreePersistentState.rewriteDeprecatedRenameEntry)
-                    parent_path, _, new_name = r.dst_path.rstrip("/").rpartition("/")
-                    new_parent = self.get(parent_path or "/").id
-                kids = self.children.get(inode.parent_id)
-                if kids is not None and kids.get(inode.name) == inode.id:
-                    del kids[inode.name]
-                inode.parent_id = new_parent
-                inode.name = new_name
-                self.children.setdefault(new_parent, {})[new_name] = inode.id
-                inode.last_modification_time_ms = r.op_time_ms or inode.last_modification_time_ms
-        elif e.HasField("set_acl"):
-            s = e.set_acl
-            inode = self.inodes.get(s.id)
-            if inode is not None:
-                self._apply_set_acl(inode, s)
-        elif e.HasField("inode_last_modification_time"):
-            inode = self.inodes.get(e.inode_last_modification_time.id)
-            if inode is not None:
-                inode.last_modification_time_ms = e.inode_last_modification_time.last_modification_time_ms
-        elif e.HasField("persist_directory"):
-            inode = self.inodes.get(e.persist_directory.id)
-            if inode is not None:
-                inode.persistence_state = "PERSISTED"
-        elif e.HasField("set_attribute"):
-            s = e.set_attribute
-            inode = self.inodes.get(s.id)
-            if inode is not None:
-                if s.HasField("pinned"):
-                    inode.pinned = s.pinned
-                if s.HasField("ttl"):
-                    inode.ttl = s.ttl
-                if s.HasField("persisted") and s.persisted:
-                    inode.persistence_state = "PERSISTED"
-                if s.HasField("owner"):
-                    inode.owner = s.owner
-                if s.HasField("group"):
-                    inode.group = s.group
-                if s.HasField("permission"):
-                    inode.mode = s.permission
-                self._index(inode)
-        elif e.HasField("complete_file"):  # legacy form
-            c = e.complete_file
-            f = self.inodes.get(c.id)
-            if f is not None and f.is_file:
-                f.block_ids = list(c.block_ids)
-                f.length = c.length
-                f.completed = True
-                f.last_modification_time_ms = c.op_time_ms
-        elif e.HasField("async_persist_request"):
-            f = self.inodes.get(e.async_persist_request.file_id)
-            if f is not None:
-                f.persistence_state = "TO_BE_PERSISTED"
-                self._index(f)
-        else:
-            return False
-        return True
+        return False
+
+    def _ap_inode_directory(self, v) -> None:
+        self._add(InodeDirectory.from_entry(v))
+
+    def _ap_inode_file(self, v) -> None:
+        self._add(InodeFile.from_entry(v))
+
+    def _ap_dir_ids(self, v) -> None:
+        self.dir_ids.apply(v)
+
+    def _ap_update_inode(self, u) -> None:
+        inode = self.inodes.get(u.id)
+        if inode is None:
+            return
+        old_parent, old_name = inode.parent_id, inode.name
+        inode.update_from(u)
+        if inode.parent_id != old_parent or inode.name != old_name:
+            kids = self.children.get(old_parent)
+            if kids is not None and kids.get(old_name) == inode.id:
+                del kids[old_name]
+            self.children.setdefault(inode.parent_id, {})[inode.name] = inode.id
+        self._index(inode)
+
+    def _ap_update_inode_directory(self, u) -> None:
+        d = self.inodes.get(u.id)
+        if d is not None and d.is_directory:
+            if u.HasField("mount_point"):
+                d.mount_point = u.mount_point
+            if u.HasField("direct_children_loaded"):
+                d.direct_children_loaded = u.direct_children_loaded
+            if u.HasField("defaultAcl"):
+                from ..security.acl import AccessControlList
+                d.default_acl = AccessControlList.from_proto(u.defaultAcl)
+
+    def _ap_update_inode_file(self, u) -> None:
+        f = self.inodes.get(u.id)
+        if f is not None and f.is_file:
+            f.update_file_from(u)
+            self._index(f)
+
+    def _ap_delete_file(self, v) -> None:
+        inode = self.inodes.get(v.id)
+        if inode is not None:
+            self._remove(inode)
+
+    def _ap_rename(self, r) -> None:
+        inode = self.inodes.get(r.id)
+        if inode is None:
+            return
+        new_parent, new_name = r.new_parent_id, r.new_name
+        if r.HasField("dst_path") and not r.HasField("new_parent_id"):
+            # 1.x entries name the destination by path; resolve it against the tree as
+            # replayed so far (InodeTreePersistentState.rewriteDeprecatedRenameEntry)
+            parent_path, _, new_name = r.dst_path.rstrip("/").rpartition("/")
+            new_parent = self.get(parent_path or "/").id
+        kids = self.children.get(inode.parent_id)
+        if kids is not None and kids.get(inode.name) == inode.id:
+            del kids[inode.name]
+        inode.parent_id = new_parent
+        inode.name = new_name
+        self.children.setdefault(new_parent, {})[new_name] = inode.id
+        inode.last_modification_time_ms = r.op_time_ms or inode.last_modification_time_ms
+
+    def _ap_set_acl(self, s) -> None:
+        inode = self.inodes.get(s.id)
+        if inode is not None:
+            self._apply_set_acl(inode, s)
+
+    def _ap_last_mod(self, v) -> None:
+        inode = self.inodes.get(v.id)
+        if inode is not None:
+            inode.last_modification_time_ms = v.last_modification_time_ms
+
+    def _ap_persist_directory(self, v) -> None:
+        inode = self.inodes.get(v.id)
+        if inode is not None:
+            inode.persistence_state = "PERSISTED"
+
+    def _ap_set_attribute(self, s) -> None:
+        inode = self.inodes.get(s.id)
+        if inode is None:
+            return
+        if s.HasField("pinned"):
+            inode.pinned = s.pinned
+        if s.HasField("ttl"):
+            inode.ttl = s.ttl
+        if s.HasField("persisted") and s.persisted:
+            inode.persistence_state = "PERSISTED"
+        if s.HasField("owner"):
+            inode.owner = s.owner
+        if s.HasField("group"):
+            inode.group = s.group
+        if s.HasField("permission"):
+            inode.mode = s.permission
+        self._index(inode)
+
+    def _ap_complete_file(self, c) -> None:   # legacy form
+        f = self.inodes.get(c.id)
+        if f is not None and f.is_file:
+            f.block_ids = list(c.block_ids)
+            f.length = c.length
+            f.completed = True
+            f.last_modification_time_ms = c.op_time_ms
+
+    def _ap_async_persist(self, v) -> None:
+        f = self.inodes.get(v.file_id)
+        if f is not None:
+            f.persistence_state = "TO_BE_PERSISTED"
+            self._index(f)
 
     @staticmethod
     def _apply_set_acl(inode: Inode, s) -> None:
@@ -400,3 +426,22 @@ class InodeTree:
     def check_no_conflict(self, parent: Inode, name: str) -> None:
         if name in self.children.get(parent.id, {}):
             raise FileAlreadyExistsException(f"{name} already exists under {self.path_of(parent)}")
+
+
+# JournalEntry field -> InodeTree handler (the namespace entry types InodeTree.apply owns)
+_APPLY = {
+    "inode_directory": InodeTree._ap_inode_directory,
+    "inode_file": InodeTree._ap_inode_file,
+    "inode_directory_id_generator": InodeTree._ap_dir_ids,
+    "update_inode": InodeTree._ap_update_inode,
+    "update_inode_directory": InodeTree._ap_update_inode_directory,
+    "update_inode_file": InodeTree._ap_update_inode_file,
+    "delete_file": InodeTree._ap_delete_file,
+    "rename": InodeTree._ap_rename,
+    "set_acl": InodeTree._ap_set_acl,
+    "inode_last_modification_time": InodeTree._ap_last_mod,
+    "persist_directory": InodeTree._ap_persist_directory,
+    "set_attribute": InodeTree._ap_set_attribute,
+    "complete_file": InodeTree._ap_complete_file,
+    "async_persist_request": InodeTree._ap_async_persist,
+}

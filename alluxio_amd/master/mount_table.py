@@ -94,11 +94,17 @@ class MountTable:
         self._lock = threading.RLock()
         self._mounts: dict[str, MountInfo] = {}
         self.epoch = 0          # bumped on every mount-table change (cached FileInfo.ufsPath)
+        self.epoch_listeners: list = []
         self.ufs_manager = ufs_manager
+
+    def _bump_epoch(self) -> None:
+        self.epoch += 1
+        for cb in self.epoch_listeners:
+            cb()
 
     def reset(self) -> None:
         with self._lock:
-            self.epoch += 1
+            self._bump_epoch()
             for m in self._mounts.values():
                 self.ufs_manager.remove_mount(m.mount_id)
             self._mounts = {}
@@ -106,7 +112,7 @@ class MountTable:
     # ---- state changes (called from journal application) ------------------------------------
     def apply_add(self, info: MountInfo) -> None:
         with self._lock:
-            self.epoch += 1
+            self._bump_epoch()
             # copy-on-write: readers use the dict they loaded without taking the lock
             m = dict(self._mounts)
             m[info.alluxio_path] = info
@@ -115,7 +121,7 @@ class MountTable:
 
     def apply_delete(self, alluxio_path: str) -> MountInfo | None:
         with self._lock:
-            self.epoch += 1
+            self._bump_epoch()
             m = dict(self._mounts)
             info = m.pop(alluxio_path, None)
             self._mounts = m

@@ -259,7 +259,12 @@ class AlluxioMasterProcess:
             self.native_rpc = NativeRpcFrontend(
                 self.server, self.server.host, self.conf.get_int("alluxio.master.native.rpc.port", "0"),
                 fast_threads=self.conf.get_int("alluxio.master.native.rpc.fast.threads", "2"),
-                blocking_threads=self.conf.get_int("alluxio.master.native.rpc.blocking.threads", "16"))
+                blocking_threads=self.conf.get_int("alluxio.master.native.rpc.blocking.threads", "16"),
+                mutation_threads=self.conf.get_int("alluxio.master.native.rpc.mutation.threads", "2"),
+                mutation_batch=self.conf.get_int("alluxio.master.native.rpc.mutation.batch", "16"),
+                reply_cache=self.conf.get_bool("alluxio.master.native.rpc.reply.cache.enabled", "true")
+                and self.fs_master.audit is None,
+                epoch_source=self.fs_master.add_epoch_listener)
             self._version_handler.native_port = self.native_rpc.start()
         addr = self.server.start()
         self.meta_master.master_address = addr
@@ -318,6 +323,8 @@ class AlluxioMasterProcess:
             return
         LOG.info("master %s lost primacy", getattr(self.server, "address", "?"))
         self.primary = False
+        if getattr(self, "native_rpc", None) is not None:
+            self.native_rpc.server.bump_epoch()   # cached replies were a primary's answers
         if self.daily_backup is not None:
             self.daily_backup.stop()
         threads, self._threads = self._threads, []

@@ -5,8 +5,18 @@ servicers through ``_C.FrameRpcServer``: C++ I/O threads decode frames and queue
 Python dispatcher threads take a batch per GIL acquisition, run the same servicer method the gRPC
 handler would (same user binding, gate, error -> status mapping) and send the serialized reply.
 Read-only metadata methods use the ``fast`` lane (few threads, large batches: nothing in them
-blocks); everything else uses the ``blocking`` lane (many threads, one request each, so a call
-waiting for its journal flush never holds up another request — group commit needs concurrency).
+blocks); the namespace mutations of the client hot path use the ``mutation`` lane (few threads,
+batches: with the flush deferred they do not block either — many threads contending for the GIL
+cost more than they overlap); everything else (UFS-bound, job, worker-sync calls) uses the
+``blocking`` lane (many threads, one request each).  A mutation does not park its thread until
+its journal entries are durable: the handler runs under :class:`journal.system.deferred_flush` and
+the reply is sent from the journal's flush callback, so one flush batch answers every mutation it
+carries (group commit) while the dispatcher threads go on decoding and applying requests.
+
+Replies of ``GetStatus`` / ``ListStatus`` calls that never sync with the UFS are also kept in the
+server's native reply cache, keyed by (method, user, request bytes) and versioned by the master's
+metadata epoch (bumped inside every namespace / block-location / mount-table change): a repeat call
+is answered on the C++ I/O thread without entering Python.
 
 Client side: :class:`NativeChannelCore` wraps ``_C.FrameRpcClient`` (connection pool, GIL released
 for the whole call).  :class:`alluxio_amd.rpc.Channel` switches its unary methods to it once the
@@ -14,10 +24,13 @@ server advertised a native port (``getServiceVersion`` -> ``nativeRpcPort``).
 """
 from __future__ import annotations
 
+import atexit
 import logging
 import threading
 import time
+import weakref
 
+from ..journal.system import deferred_flush
 from ..proto import SERVICES
 from ..utils import exceptions as ex
 
@@ -30,7 +43,37 @@ FAST_METHODS = frozenset({
     "GetBlockMasterInfo", "GetConfiguration", "GetMasterInfo", "GetStateLockHolders", "GetPinnedFileIds",
     "GetUfsInfo", "GetFileInfo",
 })
+# read-only methods whose replies the native cache may keep (see _cacheable)
+CACHEABLE_METHODS = frozenset({"GetStatus", "ListStatus"})
+# namespace mutations of the client hot path: CPU-only apart from the (deferred) journal flush
+MUTATION_METHODS = frozenset({
+    "CreateFile", "CompleteFile", "Remove", "Rename", "CreateDirectory", "SetAttribute",
+    "GetNewBlockIdForFile",
+})
+FS_SERVICE = "alluxio.grpc.file.FileSystemMasterClientService"
+LANE_FAST, LANE_BLOCKING, LANE_MUTATION = 0, 1, 2
 AUTH_PATH = "@auth"
+_LIVE: "weakref.WeakSet[NativeRpcFrontend]" = weakref.WeakSet()
+
+
+@atexit.register
+def _stop_all() -> None:
+    # dispatcher threads sit in C++ with the GIL released: stop them before the interpreter
+    # finalizes (a daemon thread re-entering a finalized interpreter aborts the process)
+    for fe in list(_LIVE):
+        try:
+            fe.stop()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def _cacheable(req) -> bool:
+    """The reply depends only on metadata state and the caller: no UFS sync is requested."""
+    o = req.options
+    if o.HasField("loadMetadataType") and o.loadMetadataType == 2:   # ALWAYS
+        return False
+    c = o.commonOptions if o.HasField("commonOptions") else None
+    return c is None or not c.HasField("syncIntervalMs") or c.syncIntervalMs < 0
 # services whose server-streaming methods are served natively (bounded metadata replies)
 STREAM_SERVICES = frozenset({"alluxio.grpc.file.FileSystemMasterClientService"})
 
@@ -70,7 +113,8 @@ def auth_payload(auth) -> bytes:
 
 class NativeRpcFrontend:
     def __init__(self, rpc_server, host: str, port: int = 0, fast_threads: int = 2, blocking_threads: int = 32,
-                 io_threads: int = 2, batch: int = 64):
+                 io_threads: int = 2, batch: int = 64, mutation_threads: int = 2, mutation_batch: int = 16,
+                 reply_cache: bool = True, epoch_source=None):
         from ..ops.native import lib
         self.rpc = rpc_server
         self.methods = [(AUTH_PATH, None, None)]
@@ -84,9 +128,21 @@ class NativeRpcFrontend:
                 if spec.server_streaming and svc not in STREAM_SERVICES:
                     continue
                 self.methods.append((spec.path, spec, getattr(servicer, name)))
-                lanes.append(0 if name in FAST_METHODS else 1)
+                lanes.append(LANE_FAST if name in FAST_METHODS else
+                             LANE_MUTATION if name in MUTATION_METHODS and svc == FS_SERVICE else LANE_BLOCKING)
         self.server = lib().FrameRpcServer(host, port, [m[0] for m in self.methods], lanes, io_threads)
         self.fast_threads, self.blocking_threads, self.batch = fast_threads, blocking_threads, batch
+        self.mutation_threads, self.mutation_batch = max(1, mutation_threads), max(1, mutation_batch)
+        self.lanes = lanes
+        # reply cache: needs a master that reports its metadata changes (epoch_source =
+        # FileSystemMaster.add_epoch_listener)
+        self.cacheable = [False] * len(self.methods)
+        if reply_cache and epoch_source is not None:
+            epoch_source(self.server.bump_epoch)
+            for i, (path, spec, _fn) in enumerate(self.methods):
+                if spec is not None and spec.name in CACHEABLE_METHODS:
+                    self.cacheable[i] = True
+                    self.server.set_cacheable(i, True)
         self._threads: list[threading.Thread] = []
         self._running = False
         self.port = None
@@ -95,7 +151,9 @@ class NativeRpcFrontend:
         self.server.start()
         self.port = self.server.port
         self._running = True
-        for lane, n, batch in ((0, self.fast_threads, self.batch), (1, self.blocking_threads, 1)):
+        _LIVE.add(self)
+        for lane, n, batch in ((LANE_FAST, self.fast_threads, self.batch), (LANE_BLOCKING, self.blocking_threads, 1),
+                               (LANE_MUTATION, self.mutation_threads, self.mutation_batch)):
             for i in range(n):
                 t = threading.Thread(target=self._loop, args=(lane, batch), daemon=True,
                                      name=f"native-rpc-{lane}-{i}")
@@ -104,6 +162,8 @@ class NativeRpcFrontend:
         return self.port
 
     def stop(self) -> None:
+        if not self._running:
+            return
         self._running = False
         self.server.stop()
         for t in self._threads:
@@ -123,7 +183,10 @@ class NativeRpcFrontend:
         self.server.set_user(token, user)
 
     def _one(self, token, midx, user, payload):
+        """Run one request; returns the reply tuple, or None when the reply is deferred until
+        the journal entries the handler appended are durable (sent by the flush callback)."""
         from ..security import as_user
+        pending = None
         try:
             if midx == 0:
                 self._auth(token, payload)
@@ -133,21 +196,54 @@ class NativeRpcFrontend:
             path, spec, fn = self.methods[midx]
             self.rpc.check(spec)
             req = spec.request.FromString(payload)
-            with as_user(user or None):
+            cache_ep = self.server.epoch() if self.cacheable[midx] and _cacheable(req) else None
+            with as_user(user or None), deferred_flush() as d:
+                pending = d.pending
                 if spec.server_streaming:
                     parts = []
                     for m in fn(req, _Ctx(user)):
                         b = m.SerializeToString()
                         parts.append(len(b).to_bytes(4, "little"))
                         parts.append(b)
-                    return (token, 0, "", b"".join(parts))
-                resp = fn(req, _Ctx(user))
-            return (token, 0, "", resp.SerializeToString())
+                    body = b"".join(parts)
+                else:
+                    body = fn(req, _Ctx(user)).SerializeToString()
+            if cache_ep is not None and not pending:
+                self.server.cache_put(midx, user, payload, body, cache_ep)
+            reply = (token, 0, "", body)
         except Exception as e:  # noqa: BLE001
             se = ex.wrap(e)
             if not isinstance(e, ex.AlluxioStatusException):
                 LOG.debug("native rpc %s failed", self.methods[midx][0], exc_info=True)
-            return (token, int(se.status), se.message or str(se), b"")
+            reply = (token, int(se.status), se.message or str(se), b"")
+        if pending:
+            self._defer(pending, reply)
+            return None
+        return reply
+
+    def _defer(self, pending: dict, reply) -> None:
+        """Send ``reply`` once every journal writer in ``pending`` flushed past its counter."""
+        left = [len(pending)]
+        err = [None]
+        lock = threading.Lock()
+        srv = self.server
+
+        def done(e):
+            with lock:
+                if e is not None and err[0] is None:
+                    err[0] = e
+                left[0] -= 1
+                last = left[0] == 0
+            if not last:
+                return
+            if err[0] is None:
+                srv.respond_many([reply])
+            else:
+                se = ex.wrap(err[0])
+                srv.respond_many([(reply[0], int(se.status), se.message or str(se), b"")])
+
+        for w, counter in pending.items():
+            w.flush_async(counter, done)
 
     def _loop(self, lane: int, batch: int) -> None:
         srv = self.server
@@ -163,8 +259,9 @@ class NativeRpcFrontend:
             if not reqs:
                 continue
             t0 = time.perf_counter()
-            out = [self._one(*r) for r in reqs]
-            srv.respond_many(out)
+            out = [o for o in (self._one(*r) for r in reqs) if o is not None]
+            if out:
+                srv.respond_many(out)
             if metrics is not None:
                 metrics.counter("NativeRpcCalls").inc(len(reqs))
                 metrics.timer("NativeRpcBatch").update(time.perf_counter() - t0)

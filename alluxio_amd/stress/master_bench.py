@@ -3,7 +3,9 @@
 Parity: stress/shell/src/main/java/alluxio/stress/cli/StressMasterBench.java (operations
 CreateFile, GetBlockLocations, GetFileStatus, OpenFile, CreateDir, ListDir, ListDirLocated,
 RenameFile, DeleteFile; ``--threads`` concurrent clients, ``--target-throughput`` rate limiter,
-``--stop-count`` / ``--fixed-count`` path selection, warmup then timed window) and
+``--stop-count`` / ``--fixed-count`` path selection as in applyOperation: op ``i`` acts on
+``fixed/i`` for i < fixed-count else ``files/i``, so RenameFile / DeleteFile consume what a previous
+CreateFile run made; warmup then timed window) and
 MasterBenchSummary (ops/s, latency percentiles, errors).  Reference published numbers for these
 operations are in docs/en/operation/Scalability-Tuning.md:142-148.
 """
@@ -64,13 +66,13 @@ def main(argv=None, fs=None, print_result=True) -> dict:
     fixed = f"{base}/fixed"
     files = f"{base}/files"
     payload = b"x" * parse_space_size(a.create_file_size)
-    # preparation: fixed-count paths for read-type ops
+    # preparation: the base directories, and (a convenience beyond the reference, which expects a
+    # CreateFile run first) the fixed-count files the read-type operations use
     fs.create_directory(files, recursive=True, allow_exists=True, write_type="MUST_CACHE")
-    if a.operation in ("GetBlockLocations", "GetFileStatus", "OpenFile", "ListDir", "ListDirLocated",
-                       "RenameFile", "DeleteFile"):
-        fs.create_directory(fixed, recursive=True, allow_exists=True, write_type="MUST_CACHE")
+    fs.create_directory(fixed, recursive=True, allow_exists=True, write_type="MUST_CACHE")
+    if a.operation in ("GetBlockLocations", "GetFileStatus", "OpenFile", "ListDir", "ListDirLocated"):
         existing = {s.name for s in fs.list_status(fixed)}
-        for i in range(a.fixed_count if a.operation not in ("RenameFile", "DeleteFile") else 0):
+        for i in range(a.fixed_count):
             if str(i) not in existing:
                 fs.write_file(f"{fixed}/{i}", payload, write_type="MUST_CACHE")
     counter = [0]
@@ -84,21 +86,26 @@ def main(argv=None, fs=None, print_result=True) -> dict:
     end = record_from + dur_s
     results = []
 
-    ids_ = itertools.count(1)
+    ids_ = itertools.count(0)
 
     def next_id():
         return next(ids_)        # GIL-atomic; a shared mutex here would throttle the clients
 
+    def target(i):
+        # StressMasterBench.applyOperation: the first fixed-count paths live under fixed/, the
+        # rest under files/; RenameFile / DeleteFile act on the paths a CreateFile run made
+        return f"{fixed}/{i}" if i < a.fixed_count else f"{files}/{i}"
+
     def op_once(c, tid):
         i = next_id()
-        if a.stop_count >= 0 and i > a.stop_count:
+        if a.stop_count >= 0 and i >= a.stop_count:
             stop.set()
             return False
         k = i % max(1, a.fixed_count)
         if a.operation == "CreateFile":
-            c.write_file(f"{files}/{tid}-{i}", payload, write_type="MUST_CACHE")
+            c.write_file(target(i), payload, write_type="MUST_CACHE")
         elif a.operation == "CreateDir":
-            c.create_directory(f"{files}/d{tid}-{i}", write_type="MUST_CACHE")
+            c.create_directory(target(i), write_type="MUST_CACHE")
         elif a.operation == "GetFileStatus":
             c.get_status(f"{fixed}/{k}")
         elif a.operation == "GetBlockLocations":
@@ -106,20 +113,19 @@ def main(argv=None, fs=None, print_result=True) -> dict:
         elif a.operation == "OpenFile":
             c.open_file(f"{fixed}/{k}").close()
         elif a.operation in ("ListDir", "ListDirLocated"):
-            c.list_status(fixed)
+            n = len(c.list_status(fixed))
+            if n != a.fixed_count:
+                raise IOError(f"listing {fixed} expected {a.fixed_count} files but got {n} files")
         elif a.operation == "RenameFile":
-            src = f"{files}/r{tid}-{i}"
-            c.write_file(src, payload, write_type="MUST_CACHE")
-            c.rename(src, src + ".renamed")
+            src = target(i)
+            c.rename(src, src + "-renamed")
         elif a.operation == "DeleteFile":
-            p = f"{files}/x{tid}-{i}"
-            c.write_file(p, payload, write_type="MUST_CACHE")
-            c.delete(p)
+            c.delete(target(i), recursive=False)
         return True
 
     def worker(tid):
         c = clients[tid % len(clients)]
-        ops, lat, errs = 0, [], []
+        ops, done, lat, errs = 0, 0, [], []
         while time.perf_counter() < start:
             time.sleep(0.001)
         while not stop.is_set() and time.perf_counter() < end:
@@ -134,10 +140,11 @@ def main(argv=None, fs=None, print_result=True) -> dict:
                     break
                 continue
             t1 = time.perf_counter()
+            done += 1
             if t0 >= record_from:
                 ops += 1
                 lat.append(t1 - t0)
-        results.append((ops, lat, errs))
+        results.append((ops, lat, errs, done))
 
     threads = [threading.Thread(target=worker, args=(t,), daemon=True) for t in range(a.threads)]
     for t in threads:
@@ -152,6 +159,7 @@ def main(argv=None, fs=None, print_result=True) -> dict:
     def pct(p):
         return lats[min(len(lats) - 1, int(p * len(lats)))] * 1e3 if lats else 0.0
     out = {"bench": "master", "operation": a.operation, "threads": a.threads, "ops": total,
+           "completed": sum(r[3] for r in results),
            "throughput_ops": total / window, "latency_ms": {"p50": pct(0.5), "p90": pct(0.9), "p99": pct(0.99),
                                                              "max": lats[-1] * 1e3 if lats else 0.0},
            "errors": [e for r in results for e in r[2]][:20]}

@@ -136,10 +136,19 @@ def test_lost_job_worker_fails_tasks(cluster):
 def test_master_bench_ops(cluster, op):
     from alluxio_amd.stress.master_bench import main
     fs = cluster.client()
-    r = main(["--operation", op, "--threads", "4", "--duration", "300ms", "--warmup", "50ms",
-              "--fixed-count", "5"], fs=fs, print_result=False)
+    extra = []
+    if op in ("RenameFile", "DeleteFile"):
+        # as in the reference: they consume the paths a preceding CreateFile run made
+        c = main(["--operation", "CreateFile", "--threads", "4", "--duration", "10s", "--warmup", "0ms",
+                  "--fixed-count", "5", "--stop-count", "40"], fs=fs, print_result=False)
+        assert not c["errors"] and c["completed"] == 40
+        extra = ["--stop-count", "40"]
+    r = main(["--operation", op, "--threads", "4", "--duration", "300ms", "--warmup", "0ms" if extra else "50ms",
+              "--fixed-count", "5"] + extra, fs=fs, print_result=False)
     assert not r["errors"], r["errors"]
     assert r["ops"] > 0 and r["throughput_ops"] > 0
+    if op == "DeleteFile":
+        assert fs.list_status("/stress-master-base/fixed") == [] and r["completed"] == 40
     fs.close()
 
 

@@ -7,8 +7,10 @@ over several client processes -- the setup of the reference's published master n
         --procs 4 --threads 8 --duration 5s --out profiles/master_bench.json
 
 Each client process runs ``alluxio_amd.stress.master_bench`` with ``--threads`` threads; the
-result is the sum of the processes' throughputs (they run the same timed window).  CPU only: no
-GPU is touched.
+result is the sum of the processes' throughputs (they run the same timed window).  Operations run
+in the order given on one base directory per client process, as the reference's runs do: DeleteFile
+and RenameFile act on the files the preceding CreateFile run made (and stop when they run out).
+CPU only: no GPU is touched.
 """
 from __future__ import annotations
 
@@ -43,7 +45,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def run(ops, procs, threads, duration, warmup, journal_dir=None) -> list[dict]:
+def run(ops, procs, threads, duration, warmup, journal_dir=None, props=()) -> list[dict]:
     work = tempfile.mkdtemp(prefix="mbench_")
     port, web = _free_port(), _free_port()
     conf_dir = os.path.join(work, "conf")
@@ -53,6 +55,8 @@ def run(ops, procs, threads, duration, warmup, journal_dir=None) -> list[dict]:
         f.write(f"alluxio.master.mount.table.root.ufs={os.path.join(work, 'ufs')}\n")
         f.write(f"alluxio.master.web.port={web}\n")
         f.write("alluxio.master.journal.type=UFS\n")
+        for kv in props:
+            f.write(kv + "\n")
     env = dict(os.environ, ALLUXIO_CONF_DIR=conf_dir, PYTHONPATH=ROOT)
     master = subprocess.Popen([sys.executable, "-m", "alluxio_amd.master.process", "--host", "127.0.0.1",
                                "--port", str(port), "--format"], env=env, cwd=work,
@@ -67,21 +71,25 @@ def run(ops, procs, threads, duration, warmup, journal_dir=None) -> list[dict]:
             time.sleep(0.2)
         time.sleep(1.0)
         out = []
+        created = {}     # per client process: files its CreateFile run made (DeleteFile/RenameFile input)
         for op in ops:
-            args = ["--operation", op, "--threads", str(threads), "--duration", duration, "--warmup", warmup,
-                    "--base", f"/stress-{op}"]
+            args = ["--operation", op, "--threads", str(threads), "--duration", duration, "--warmup", warmup]
             ps = []
             for i in range(procs):
-                a = args + ["--base", f"/stress-{op}-{i}"]
+                a = args + ["--base", f"/stress-master-{i}"]
+                if op in ("DeleteFile", "RenameFile") and i in created:
+                    a += ["--stop-count", str(created[i])]
                 ps.append(subprocess.Popen([sys.executable, "-c", CLIENT.format(root=ROOT, addr=addr, args=a)],
                                            env=env, cwd=work, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
                                            text=True))
             res = []
-            for p in ps:
+            for i, p in enumerate(ps):
                 so, _ = p.communicate(timeout=600)
                 line = next((ln for ln in so.splitlines() if ln.startswith("RESULT ")), None)
                 if line:
                     res.append(json.loads(line[7:]))
+                    if op == "CreateFile":
+                        created[i] = res[-1]["completed"]
             total = sum(r["throughput_ops"] for r in res)
             p50 = sorted(r["latency_ms"]["p50"] for r in res)[len(res) // 2] if res else None
             errs = sum(len(r["errors"]) for r in res)
@@ -106,8 +114,9 @@ def main(argv=None) -> int:
     ap.add_argument("--duration", default="5s")
     ap.add_argument("--warmup", default="1s")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--master-prop", action="append", default=[], help="k=v master property (repeatable)")
     a = ap.parse_args(argv)
-    rows = run(a.ops.split(","), a.procs, a.threads, a.duration, a.warmup)
+    rows = run(a.ops.split(","), a.procs, a.threads, a.duration, a.warmup, props=a.master_prop)
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"setup": f"1 master process + {a.procs} client processes x {a.threads} threads, gRPC, "
