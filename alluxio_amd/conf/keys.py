@@ -159,8 +159,14 @@ _k("WORKER_IPC_ENABLED", "alluxio.worker.ipc.enabled", "true", Scope.WORKER,
    "Hand out HIP IPC handles for short-circuit reads of HBM pages.")
 _k("WORKER_STAGING_BUFFER_SIZE", "alluxio.worker.staging.buffer.size", "64MB", Scope.WORKER,
    "Pinned host staging ring used for UFS->HBM and HBM->host copies.")
-_k("WORKER_EVICTION_KERNEL_MIN_BLOCKS", "alluxio.worker.eviction.kernel.min.blocks", "1", Scope.WORKER,
-   "Use the device eviction-ordering kernel when a dir holds at least this many blocks.")
+_k("WORKER_EVICTION_DEVICE_ENABLED", "alluxio.worker.eviction.device.enabled", "true", Scope.WORKER,
+   "Keep the LRU/LRFU annotations in HBM and select eviction victims with the grid-wide device "
+   "select (K4-K6) when the store has an HBM tier; false = host sort.")
+_k("WORKER_HBM_DEVICE_ALLOC_ENABLED", "alluxio.worker.hbm.device.alloc.enabled", "false", Scope.WORKER,
+   "Claim the pages of bulk block creates with the device bitmap allocator (K7). Off by default: "
+   "the host bitmap scan measured faster end to end (profiles/r2_evict_bench.jsonl).")
+_k("WORKER_HBM_DEVICE_ALLOC_MIN_PAGES", "alluxio.worker.hbm.device.alloc.min.pages", "4096", Scope.WORKER,
+   "Smallest bulk create (in pages) that uses the device allocator when it is enabled.")
 _k("USER_READ_BATCH_SIZE", "alluxio.user.read.batch.size", "256", Scope.CLIENT,
    "Max read requests coalesced into one page-gather launch.")
 _k("USER_FILE_READ_DEVICE", "alluxio.user.file.read.device", "cuda", Scope.CLIENT,

@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -103,6 +104,8 @@ void batched_copy(const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>>& s
   if (sync) HIP_CHECK(hipStreamSynchronize(st));
 }
 
+// Stand-alone run of the grid-wide select (evict_alloc.hip) on caller arrays: slot i is a
+// candidate of dir 0 when evictable[i]; `bytes` are the footprints.  Returns (slots, freed).
 py::tuple evict_select_device(const std::vector<float>& crf, const std::vector<uint64_t>& last,
                               const std::vector<uint64_t>& bytes, const std::vector<uint8_t>& evictable,
                               uint64_t now, float step, float att, int policy, uint64_t need) {
@@ -113,22 +116,53 @@ py::tuple evict_select_device(const std::vector<float>& crf, const std::vector<u
   uint64_t freed = 0;
   {
     py::gil_scoped_release rel;
-    DevBuf dc(n * 4), dl(n * 8), db(n * 8), de(n), dk(n * 4), dout(n * 4), dcnt(16);
+    std::vector<int32_t> dir(n);
+    for (size_t i = 0; i < n; ++i) dir[i] = evictable[i] ? 0 : -1;
+    DevBuf dc(n * 4 + 4), dl(n * 8 + 8), db(n * 8 + 8), dd(n * 4 + 4), dk(n * 4 + 4), dout(n * 4 + 4),
+        dctl(sizeof(EvictCtl));
     HIP_CHECK(hipMemcpy(dc.p, crf.data(), n * 4, hipMemcpyHostToDevice));
     HIP_CHECK(hipMemcpy(dl.p, last.data(), n * 8, hipMemcpyHostToDevice));
     HIP_CHECK(hipMemcpy(db.p, bytes.data(), n * 8, hipMemcpyHostToDevice));
-    HIP_CHECK(hipMemcpy(de.p, evictable.data(), n, hipMemcpyHostToDevice));
-    EvictInput in{(const float*)dc.p, (const uint64_t*)dl.p, (const uint64_t*)db.p, (const uint8_t*)de.p,
-                  (uint32_t)n, now, step, att, policy, need};
-    HIP_CHECK(launch_evict_select(in, (uint32_t*)dk.p, (uint32_t*)dout.p, (uint32_t*)dcnt.p,
-                                  (uint64_t*)((char*)dcnt.p + 8), nullptr));
-    uint32_t cnt = 0;
-    HIP_CHECK(hipMemcpy(&cnt, dcnt.p, 4, hipMemcpyDeviceToHost));
-    HIP_CHECK(hipMemcpy(&freed, (char*)dcnt.p + 8, 8, hipMemcpyDeviceToHost));
-    out.resize(cnt);
-    if (cnt) HIP_CHECK(hipMemcpy(out.data(), dout.p, cnt * 4, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(dd.p, dir.data(), n * 4, hipMemcpyHostToDevice));
+    EvictState st;
+    st.crf = (float*)dc.p;
+    st.last = (uint64_t*)dl.p;
+    st.fbytes = (uint64_t*)db.p;
+    st.dir = (int32_t*)dd.p;
+    st.n = (uint32_t)n;
+    st.now = now;
+    st.step = step;
+    st.log2_inv_att = (float)std::log2(1.0 / (double)att);
+    st.policy = policy;
+    HIP_CHECK(launch_evict_select_grid(st, 0, nullptr, need, (uint32_t*)dk.p, (EvictCtl*)dctl.p, (uint32_t*)dout.p,
+                                       nullptr));
+    EvictCtl ctl;
+    HIP_CHECK(hipMemcpy(&ctl, dctl.p, sizeof(ctl), hipMemcpyDeviceToHost));
+    freed = ctl.freed;
+    out.resize(ctl.count);
+    if (ctl.count) HIP_CHECK(hipMemcpy(out.data(), dout.p, ctl.count * 4, hipMemcpyDeviceToHost));
   }
   return py::make_tuple(out, freed);
+}
+
+// K7 stand-alone: claim `want` free pages from a caller bitmap (returns (pages, new_bitmap)).
+py::tuple page_alloc_device(const std::vector<uint64_t>& bits, uint32_t want) {
+  const uint32_t nw = (uint32_t)bits.size();
+  std::vector<int64_t> pages;
+  std::vector<uint64_t> after(nw);
+  {
+    py::gil_scoped_release rel;
+    DevBuf db((size_t)nw * 8 + 8), dp((size_t)page_alloc_partials(nw) * 4 + 4), dout((size_t)want * 8 + 8), dc(8);
+    if (nw) HIP_CHECK(hipMemcpy(db.p, bits.data(), (size_t)nw * 8, hipMemcpyHostToDevice));
+    HIP_CHECK(launch_page_alloc((uint64_t*)db.p, nw, want, (uint32_t*)dp.p, (int64_t*)dout.p, (uint32_t*)dc.p,
+                                nullptr));
+    uint32_t got = 0;
+    HIP_CHECK(hipMemcpy(&got, dc.p, 4, hipMemcpyDeviceToHost));
+    pages.resize(got);
+    if (got) HIP_CHECK(hipMemcpy(pages.data(), dout.p, (size_t)got * 8, hipMemcpyDeviceToHost));
+    if (nw) HIP_CHECK(hipMemcpy(after.data(), db.p, (size_t)nw * 8, hipMemcpyDeviceToHost));
+  }
+  return py::make_tuple(pages, after);
 }
 
 }  // namespace
@@ -256,7 +290,28 @@ PYBIND11_MODULE(_C, m) {
            py::arg("tier") = -1, py::arg("dir") = -1)
       .def("eviction_order", &BlockStore::eviction_order, G(), py::arg("tier") = -1, py::arg("need_bytes") = 0)
       .def("set_pinned_files", &BlockStore::set_pinned_files, G())
-      .def("set_use_device_evict", &BlockStore::set_use_device_evict)
+      .def("set_use_device_evict", &BlockStore::set_use_device_evict, G())
+      .def("set_use_device_alloc", &BlockStore::set_use_device_alloc, py::arg("enabled"), py::arg("min_pages") = 64)
+      .def("create_blocks", &BlockStore::create_blocks, G(), py::arg("session"), py::arg("block_ids"),
+           py::arg("tier") = -1, py::arg("medium") = "", py::arg("sizes") = std::vector<uint64_t>{},
+           py::arg("evict") = true)
+      .def("select_for_bench", &BlockStore::select_for_bench, G(), py::arg("dir"), py::arg("need"),
+           py::arg("device"))
+      .def("peek_free_pages", &BlockStore::peek_free_pages, G(), py::arg("dir"), py::arg("want"), py::arg("device"))
+      .def("evict_stats", [](BlockStore& s) {
+             auto st = s.evict_stats();
+             py::dict d;
+             d["selections"] = st.selections;
+             d["device_selections"] = st.device_selections;
+             d["candidates"] = st.candidates;
+             d["victims"] = st.victims;
+             d["revalidated_away"] = st.revalidated_away;
+             d["device_allocs"] = st.device_allocs;
+             d["device_alloc_pages"] = st.device_alloc_pages;
+             d["annotation_flushes"] = st.annotation_flushes;
+             d["annotation_updates"] = st.annotation_updates;
+             return d;
+           })
       .def("has_block", &BlockStore::has_block, G())
       .def("has_temp_block", &BlockStore::has_temp_block, G())
       .def("block_info", &BlockStore::block_info, G())
@@ -475,6 +530,7 @@ PYBIND11_MODULE(_C, m) {
                                         reinterpret_cast<hipStream_t>(stream)));
         }, py::arg("ptr"), py::arg("bytes"), py::arg("seed"), py::arg("word_offset") = 0, py::arg("stream") = 0);
   m.def("evict_select_device", &evict_select_device);
+  m.def("page_alloc_device", &page_alloc_device);
   m.def("set_copy_variant", &set_copy_variant, py::arg("variant"), py::arg("grid_cap") = 0);
   m.def("set_crc_variant", &set_crc_variant, py::arg("variant"));
   m.def("set_lz4_decode_variant", &set_lz4_decode_variant, py::arg("variant"));

@@ -68,9 +68,15 @@ BlockStore::BlockStore(const std::vector<DirSpec>& dirs, int annotator, int allo
     dirs_.push_back(std::move(d));
   }
   rr_index_.assign(max_tier + 1, 0);
+  dir_ev_bytes_.assign(dirs_.size(), 0);
   if (has_device_) {
     set_device();
     HIP_OK(hipStreamCreateWithFlags(&internal_stream_, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) HIP_OK(hipEventCreateWithFlags(&upd_ev_[i], hipEventDisableTiming));
+    HIP_OK(hipHostMalloc((void**)&h_ctl_, sizeof(EvictCtl), hipHostMallocDefault));
+    HIP_OK(hipMalloc((void**)&d_ctl_, sizeof(EvictCtl)));
+    HIP_OK(hipHostMalloc((void**)&h_claimed_, sizeof(uint32_t), hipHostMallocDefault));
+    HIP_OK(hipMalloc((void**)&d_claimed_, sizeof(uint32_t)));
     HIP_OK(hipHostMalloc((void**)&host_ring_, sizeof(CopySeg) * kRing * kRingSegs, hipHostMallocDefault));
     HIP_OK(hipMalloc((void**)&dev_ring_, sizeof(CopySeg) * kRing * kRingSegs));
     for (int i = 0; i < kRing; ++i) HIP_OK(hipEventCreateWithFlags(&ring_ev_[i], hipEventDisableTiming));
@@ -84,7 +90,16 @@ BlockStore::~BlockStore() {
       if (ring_ev_[i]) hipEventDestroy(ring_ev_[i]);
     if (host_ring_) hipHostFree(host_ring_);
     if (dev_ring_) hipFree(dev_ring_);
-    if (ev_dev_) hipFree(ev_dev_);
+    for (int i = 0; i < 2; ++i) {
+      if (upd_ev_[i]) hipEventDestroy(upd_ev_[i]);
+      if (h_upd_[i]) hipHostFree(h_upd_[i]);
+    }
+    for (void* p : {(void*)d_crf_, (void*)d_last_, (void*)d_fbytes_, (void*)d_dir_, (void*)d_keys_,
+                    (void*)d_excl_, (void*)d_ctl_, (void*)d_upd_, (void*)d_bits_, (void*)d_partial_,
+                    (void*)d_claimed_})
+      if (p) hipFree(p);
+    for (void* p : {(void*)h_excl_, (void*)h_ctl_, (void*)h_out_, (void*)h_pages_, (void*)h_claimed_})
+      if (p) hipHostFree(p);
     if (crc_dev_) hipFree(crc_dev_);
     if (internal_stream_) hipStreamDestroy(internal_stream_);
   }
@@ -130,7 +145,17 @@ uint32_t BlockStore::alloc_slot() {
   crf_.push_back(0.f);
   last_.push_back(0);
   slot_block_.push_back(0);
+  slot_dir_.push_back(-1);
+  slot_fb_.push_back(0);
+  dirty_flag_.push_back(0);
   return (uint32_t)(crf_.size() - 1);
+}
+
+void BlockStore::mark_dirty(uint32_t slot) {
+  if (!device_evict_active() || dirty_flag_[slot]) return;
+  dirty_flag_[slot] = 1;
+  dirty_.push_back(slot);
+  if (dirty_.size() >= 65536) flush_annotations_locked();   // bound the host queue (async)
 }
 
 void BlockStore::touch_slot(uint32_t slot) {
@@ -140,6 +165,34 @@ void BlockStore::touch_slot(uint32_t slot) {
     crf_[slot] = (float)(crf_[slot] * std::pow(1.0 / lrfu_att_, age * lrfu_step_) + 1.0);
   }
   last_[slot] = now;
+  mark_dirty(slot);
+}
+
+// Page-rounded footprint: what evicting the block gives back to its dir.
+uint64_t BlockStore::footprint(const BlockMeta& b) const {
+  const StorageDir& d = *dirs_[b.dir];
+  if (d.spec.kind == DirKind::kFile) return std::max(b.length, b.reserved);
+  return (uint64_t)b.pages.size() * d.spec.page_size;
+}
+
+// Static evictability (committed, not pinned) and footprint of a slot changed; `live` = false
+// when the block is going away.  Keeps dir_ev_bytes_ and the device mirror current.
+void BlockStore::note_state(const BlockMeta& b, bool live) {
+  int32_t nd = -1;
+  uint64_t nf = 0;
+  if (live && !b.temp && !b.pinned_on_create) {
+    const int64_t file_id = (int64_t)(((uint64_t)b.id & ~0xFFFFFFull) | 0xFFFFFFull);
+    if (pinned_files_.find(file_id) == pinned_files_.end()) {
+      nd = b.dir;
+      nf = footprint(b);
+    }
+  }
+  const uint32_t s = b.slot;
+  if (slot_dir_[s] >= 0) dir_ev_bytes_[slot_dir_[s]] -= std::min(dir_ev_bytes_[slot_dir_[s]], slot_fb_[s]);
+  if (nd >= 0) dir_ev_bytes_[nd] += nf;
+  slot_dir_[s] = nd;
+  slot_fb_[s] = nf;
+  mark_dirty(s);
 }
 
 bool BlockStore::evictable(const BlockMeta& b) const {
@@ -310,6 +363,8 @@ int BlockStore::create_block(int64_t session, int64_t block_id, int tier, const 
   int d = allocate_dir(tier, medium, initial);
   if (d < 0 && evict) {
     free_space_locked(lk, session, initial, tier, -1, medium);
+    if (blocks_.count(block_id))   // created by another thread while the store was unlocked
+      throw StoreError(kErrAlreadyExists, "block " + std::to_string(block_id) + " already exists");
     d = allocate_dir(tier, medium, initial);
   }
   if (d < 0)
@@ -326,9 +381,11 @@ int BlockStore::create_block(int64_t session, int64_t block_id, int tier, const 
     throw StoreError(kErrOutOfSpace, "allocation raced for block " + std::to_string(block_id));
   }
   b.slot = alloc_slot();
+  b.seq = ++create_seq_;
   slot_block_[b.slot] = block_id;
   crf_[b.slot] = 0.f;
   last_[b.slot] = clock_.load();
+  note_state(b, true);   // temp: not evictable yet; resets the slot's device annotations
   if (dirs_[d]->spec.kind == DirKind::kFile) {
     const std::string p = dirs_[d]->spec.path + "/.tmp_blocks/" + std::to_string(session) + "-" +
                           std::to_string(block_id);
@@ -431,6 +488,7 @@ void BlockStore::commit_block(int64_t session, int64_t block_id, bool pin) {
   b->pinned_on_create = b->pinned_on_create || pin;
   d.committed_bytes += b->length;
   session_temps_[session].erase(block_id);
+  note_state(*b, true);
   touch_slot(b->slot);
   emit(0, *b);
 }
@@ -440,6 +498,7 @@ void BlockStore::abort_block(int64_t session, int64_t block_id) {
   BlockMeta* b = find(block_id);
   if (!b || !b->temp) throw StoreError(kErrNotFound, "temp block " + std::to_string(block_id) + " not found");
   if (b->session != session) throw StoreError(kErrInvalidState, "temp block owned by another session");
+  note_state(*b, false);
   release_storage(*b);
   free_slots_.push_back(b->slot);
   session_temps_[session].erase(block_id);
@@ -448,6 +507,7 @@ void BlockStore::abort_block(int64_t session, int64_t block_id) {
 
 void BlockStore::remove_locked(BlockMeta& b, bool emit_event) {
   if (emit_event) emit(1, b);
+  note_state(b, false);
   release_storage(b);
   free_slots_.push_back(b.slot);
   crf_[b.slot] = 0.f;
@@ -484,7 +544,16 @@ int BlockStore::move_block(int64_t session, int64_t block_id, int dst_tier, cons
   int d = allocate_dir(dst_tier, medium, std::max<uint64_t>(len, 1));
   if (d < 0 && evict) {
     b->evicting = true;  // never pick the block being moved as its own victim
-    free_space_locked(lk, session, len, dst_tier, -1, medium);
+    evicting_ids_.insert(block_id);
+    try {
+      free_space_locked(lk, session, len, dst_tier, -1, medium);
+    } catch (...) {
+      evicting_ids_.erase(block_id);
+      b = find(block_id);
+      if (b) b->evicting = false;
+      throw;
+    }
+    evicting_ids_.erase(block_id);
     b = find(block_id);
     if (b) b->evicting = false;
     d = allocate_dir(dst_tier, medium, std::max<uint64_t>(len, 1));
@@ -563,6 +632,7 @@ int BlockStore::move_block(int64_t session, int64_t block_id, int dst_tier, cons
   b->pages = nb.pages;
   b->reserved = nb.reserved;
   b->writer = false;
+  note_state(*b, true);
   dirs_[d]->committed_bytes += len;
   if (dd.spec.kind == DirKind::kFile) dd.file_used += 0;  // reserved already counted by grow_pages
   emit(2, *b);
@@ -650,6 +720,8 @@ void BlockStore::set_pinned_files(const std::vector<int64_t>& file_ids) {
   std::unique_lock<std::mutex> lk(mu_);
   pinned_files_.clear();
   pinned_files_.insert(file_ids.begin(), file_ids.end());
+  for (auto& kv : blocks_)
+    if (!kv.second.temp) note_state(kv.second, true);
 }
 
 // -------------------------------------------------------------------------------------------
@@ -859,73 +931,172 @@ void BlockStore::fill_pattern(int64_t session, int64_t block_id, uint64_t length
 
 // -------------------------------------------------------------------------------------------
 // eviction
-std::vector<uint32_t> BlockStore::select_victims(const std::vector<uint32_t>& cand, uint64_t need) {
+EvictState BlockStore::dev_state(uint64_t now) const {
+  EvictState st;
+  st.crf = d_crf_;
+  st.last = d_last_;
+  st.fbytes = d_fbytes_;
+  st.dir = d_dir_;
+  st.n = (uint32_t)crf_.size();
+  st.now = now;
+  st.step = lrfu_step_;
+  st.log2_inv_att = (float)std::log2(1.0 / (double)lrfu_att_);
+  st.policy = annotator_ == Annotator::kLRFU ? 1 : 0;
+  return st;
+}
+
+// Grow the slot-indexed device arrays to hold `n` slots (doubling).  Called under mu_; takes
+// ev_mu_ so no selection is reading the old arrays.  Growth is logarithmic in the slot count.
+void BlockStore::ensure_dev_slots_locked(size_t n) {
+  if (n <= dev_slots_ && dev_synced_) return;
+  std::lock_guard<std::mutex> g(ev_mu_);
+  set_device();
+  if (n > dev_slots_) {
+    size_t cap = std::max<size_t>({n, dev_slots_ * 2, 16384});
+    cap = (cap + 31) / 32 * 32;
+    float* crf;
+    uint64_t *last, *fb;
+    int32_t* dir;
+    uint32_t *keys, *excl, *hexcl, *hout, *hout_dev;
+    HIP_OK(hipMalloc((void**)&crf, cap * 4));
+    HIP_OK(hipMalloc((void**)&last, cap * 8));
+    HIP_OK(hipMalloc((void**)&fb, cap * 8));
+    HIP_OK(hipMalloc((void**)&dir, cap * 4));
+    HIP_OK(hipMalloc((void**)&keys, cap * 4));
+    HIP_OK(hipMalloc((void**)&excl, cap / 8));
+    HIP_OK(hipHostMalloc((void**)&hexcl, cap / 8, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&hout, cap * 4, hipHostMallocMapped));
+    HIP_OK(hipHostGetDevicePointer((void**)&hout_dev, hout, 0));
+    std::memset(hexcl, 0, cap / 8);
+    HIP_OK(hipMemsetAsync(dir, 0xFF, cap * 4, internal_stream_));   // -1: no evictable block
+    HIP_OK(hipMemsetAsync(fb, 0, cap * 8, internal_stream_));
+    if (dev_slots_) {
+      HIP_OK(hipMemcpyAsync(crf, d_crf_, dev_slots_ * 4, hipMemcpyDeviceToDevice, internal_stream_));
+      HIP_OK(hipMemcpyAsync(last, d_last_, dev_slots_ * 8, hipMemcpyDeviceToDevice, internal_stream_));
+      HIP_OK(hipMemcpyAsync(fb, d_fbytes_, dev_slots_ * 8, hipMemcpyDeviceToDevice, internal_stream_));
+      HIP_OK(hipMemcpyAsync(dir, d_dir_, dev_slots_ * 4, hipMemcpyDeviceToDevice, internal_stream_));
+    }
+    HIP_OK(hipStreamSynchronize(internal_stream_));
+    for (void* p : {(void*)d_crf_, (void*)d_last_, (void*)d_fbytes_, (void*)d_dir_, (void*)d_keys_, (void*)d_excl_})
+      if (p) hipFree(p);
+    for (void* p : {(void*)h_excl_, (void*)h_out_})
+      if (p) hipHostFree(p);
+    d_crf_ = crf;
+    d_last_ = last;
+    d_fbytes_ = fb;
+    d_dir_ = dir;
+    d_keys_ = keys;
+    d_excl_ = excl;
+    h_excl_ = hexcl;
+    h_out_ = hout;
+    h_out_dev_ = hout_dev;
+    dev_slots_ = cap;
+  }
+  if (!dev_synced_) {
+    // (re)publish every slot's mirror: first use, or device eviction switched back on
+    dev_synced_ = true;
+    for (uint32_t s = 0; s < (uint32_t)crf_.size(); ++s)
+      if (!dirty_flag_[s]) {
+        dirty_flag_[s] = 1;
+        dirty_.push_back(s);
+      }
+  }
+}
+
+// Ship the dirty slots' mirror values to the device: one pinned staging fill, one async H2D, one
+// scatter launch on the internal stream (no host wait unless the staging buffer is still in
+// flight from two flushes ago).
+void BlockStore::flush_annotations_locked() {
+  if (!device_evict_active()) {
+    for (uint32_t s : dirty_) dirty_flag_[s] = 0;
+    dirty_.clear();
+    return;
+  }
+  ensure_dev_slots_locked(crf_.size());
+  if (dirty_.empty()) return;
+  set_device();
+  const size_t n = dirty_.size();
+  const int k = upd_pos_;
+  upd_pos_ ^= 1;
+  HIP_OK(hipEventSynchronize(upd_ev_[k]));
+  if (h_upd_cap_[k] < n) {
+    if (h_upd_[k]) hipHostFree(h_upd_[k]);
+    h_upd_[k] = nullptr;
+    const size_t cap = std::max<size_t>(n, 4096);
+    HIP_OK(hipHostMalloc((void**)&h_upd_[k], cap * sizeof(SlotUpdate), hipHostMallocDefault));
+    h_upd_cap_[k] = cap;
+  }
+  if (d_upd_cap_ < n) {
+    // stream-ordered: the previous scatter finished reading the old buffer before this point
+    HIP_OK(hipStreamSynchronize(internal_stream_));
+    if (d_upd_) hipFree(d_upd_);
+    d_upd_ = nullptr;
+    const size_t cap = std::max<size_t>(n, 4096);
+    HIP_OK(hipMalloc((void**)&d_upd_, cap * sizeof(SlotUpdate)));
+    d_upd_cap_ = cap;
+  }
+  SlotUpdate* u = h_upd_[k];
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t s = dirty_[i];
+    u[i].slot = s;
+    u[i].flags = kSlotSetState | kSlotReset;
+    u[i].dir = slot_dir_[s];
+    u[i].crf = crf_[s];
+    u[i].fbytes = slot_fb_[s];
+    u[i].t = last_[s];
+    dirty_flag_[s] = 0;
+  }
+  dirty_.clear();
+  HIP_OK(hipMemcpyAsync(d_upd_, u, n * sizeof(SlotUpdate), hipMemcpyHostToDevice, internal_stream_));
+  HIP_OK(launch_slot_update(dev_state(clock_.load()), d_upd_, (uint32_t)n, internal_stream_));
+  HIP_OK(hipEventRecord(upd_ev_[k], internal_stream_));
+  ++stats_.annotation_flushes;
+  stats_.annotation_updates += n;
+}
+
+// Device selection of victims in `dir` for `need` bytes.  Called with mu_ held; mu_ is released
+// for the device round trip (launches + one stream sync) and re-acquired before returning.
+std::vector<uint32_t> BlockStore::select_victims_device(std::unique_lock<std::mutex>& lk, int dir, uint64_t need) {
+  flush_annotations_locked();
+  // dynamic exclusions: locked or moving blocks (few; evictable() re-checks at removal anyway)
+  std::vector<uint32_t> excl;
+  for (auto& kv : locks_) {
+    const BlockMeta* b = find(kv.second.block);
+    if (b) excl.push_back(b->slot);
+  }
+  for (int64_t id : evicting_ids_) {
+    const BlockMeta* b = find(id);
+    if (b) excl.push_back(b->slot);
+  }
+  const EvictState st = dev_state(clock_.load());
+  std::vector<uint32_t> picked;
+  {
+    std::unique_lock<std::mutex> g(ev_mu_);   // mu_ -> ev_mu_ order, then mu_ is dropped
+    lk.unlock();
+    set_device();
+    for (uint32_t s : excl) h_excl_[s >> 5] |= 1u << (s & 31);
+    const size_t words = ((size_t)st.n + 31) / 32;
+    hipError_t e = hipMemcpyAsync(d_excl_, h_excl_, words * 4, hipMemcpyHostToDevice, internal_stream_);
+    if (e == hipSuccess)
+      e = launch_evict_select_grid(st, (uint32_t)dir, d_excl_, need, d_keys_, d_ctl_, h_out_dev_, internal_stream_);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_ctl_, d_ctl_, sizeof(EvictCtl), hipMemcpyDeviceToHost, internal_stream_);
+    if (e == hipSuccess) e = hipStreamSynchronize(internal_stream_);
+    for (uint32_t s : excl) h_excl_[s >> 5] &= ~(1u << (s & 31));
+    if (e == hipSuccess) picked.assign(h_out_, h_out_ + h_ctl_->count);
+    g.unlock();
+    lk.lock();
+    if (e != hipSuccess) throw StoreError(kErrHip, std::string("device eviction select: ") + hipGetErrorString(e));
+  }
+  ++stats_.device_selections;
+  return picked;
+}
+
+std::vector<uint32_t> BlockStore::select_victims_cpu(const std::vector<uint32_t>& cand, uint64_t need) {
   const size_t n = cand.size();
   std::vector<uint32_t> picked;
   if (n == 0 || need == 0) return picked;
   const uint64_t now = clock_.load();
-  std::vector<uint64_t> bytes(n);
-  for (size_t i = 0; i < n; ++i) {
-    const BlockMeta* b = find(slot_block_[cand[i]]);
-    bytes[i] = b ? b->length : 0;
-  }
-  if (has_device_ && use_device_evict_) {
-    std::lock_guard<std::mutex> g(ev_mu_);
-    set_device();
-    // layout: crf f32[n] | last u64[n] | bytes u64[n] | evictable u8[n] | keys u32[n] | out u32[n] | cnt | freed
-    const size_t off_last = ((n * 4 + 15) / 16) * 16;
-    const size_t off_bytes = off_last + n * 8;
-    const size_t off_ev = off_bytes + n * 8;
-    const size_t off_keys = ((off_ev + n + 15) / 16) * 16;
-    const size_t off_out = off_keys + n * 4;
-    const size_t off_cnt = ((off_out + n * 4 + 15) / 16) * 16;
-    const size_t total = off_cnt + 32;
-    if (ev_cap_ < total) {
-      if (ev_dev_) hipFree(ev_dev_);
-      ev_dev_ = nullptr;
-      HIP_OK(hipMalloc(&ev_dev_, total));
-      ev_cap_ = total;
-    }
-    std::vector<uint8_t> host(off_keys, 0);
-    float* hc = reinterpret_cast<float*>(host.data());
-    uint64_t* hl = reinterpret_cast<uint64_t*>(host.data() + off_last);
-    uint64_t* hb = reinterpret_cast<uint64_t*>(host.data() + off_bytes);
-    uint8_t* he = host.data() + off_ev;
-    for (size_t i = 0; i < n; ++i) {
-      hc[i] = crf_[cand[i]];
-      hl[i] = last_[cand[i]];
-      hb[i] = bytes[i];
-      he[i] = 1;
-    }
-    uint8_t* dv = static_cast<uint8_t*>(ev_dev_);
-    HIP_OK(hipMemcpyAsync(dv, host.data(), off_keys, hipMemcpyHostToDevice, internal_stream_));
-    EvictInput in;
-    in.crf = reinterpret_cast<const float*>(dv);
-    in.last = reinterpret_cast<const uint64_t*>(dv + off_last);
-    in.bytes = reinterpret_cast<const uint64_t*>(dv + off_bytes);
-    in.evictable = dv + off_ev;
-    in.n = (uint32_t)n;
-    in.now = now;
-    in.step_factor = lrfu_step_;
-    in.attenuation = lrfu_att_;
-    in.policy = annotator_ == Annotator::kLRFU ? 1 : 0;
-    in.need_bytes = need;
-    HIP_OK(launch_evict_select(in, reinterpret_cast<uint32_t*>(dv + off_keys),
-                               reinterpret_cast<uint32_t*>(dv + off_out),
-                               reinterpret_cast<uint32_t*>(dv + off_cnt),
-                               reinterpret_cast<uint64_t*>(dv + off_cnt + 8), internal_stream_));
-    uint32_t count = 0;
-    HIP_OK(hipMemcpyAsync(&count, dv + off_cnt, 4, hipMemcpyDeviceToHost, internal_stream_));
-    HIP_OK(hipStreamSynchronize(internal_stream_));
-    std::vector<uint32_t> idx(count);
-    if (count) {
-      HIP_OK(hipMemcpyAsync(idx.data(), dv + off_out, count * 4, hipMemcpyDeviceToHost, internal_stream_));
-      HIP_OK(hipStreamSynchronize(internal_stream_));
-    }
-    for (uint32_t k : idx) picked.push_back(cand[k]);
-    return picked;
-  }
-  // CPU path: identical keys, full sort
+  // identical keys to the device select, full sort
   std::vector<std::pair<uint32_t, uint32_t>> keyed(n);
   for (size_t i = 0; i < n; ++i) {
     const uint32_t s = cand[i];
@@ -945,8 +1116,10 @@ std::vector<uint32_t> BlockStore::select_victims(const std::vector<uint32_t>& ca
   uint64_t got = 0;
   for (auto& kv : keyed) {
     if (got >= need) break;
-    picked.push_back(cand[kv.second]);
-    got += bytes[kv.second];
+    const uint32_t s = cand[kv.second];
+    picked.push_back(s);
+    const BlockMeta* b = find(slot_block_[s]);
+    got += b ? footprint(*b) : 0;
   }
   return picked;
 }
@@ -954,38 +1127,50 @@ std::vector<uint32_t> BlockStore::select_victims(const std::vector<uint32_t>& ca
 void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
                                    int tier, int dir, const std::string& medium) {
   (void)session;
-  (void)lk;
-  // choose the target dir: the one that can reach `bytes` with the most (available + evictable)
-  int target = -1;
-  uint64_t best = 0;
-  std::vector<uint64_t> ev_bytes(dirs_.size(), 0);
-  for (auto& kv : blocks_)
-    if (evictable(kv.second)) ev_bytes[kv.second.dir] += kv.second.length;
-  for (auto& d : dirs_) {
-    if (dir >= 0 && d->index != dir) continue;
-    if (!dir_matches(*d, tier, medium)) continue;
-    const uint64_t reach = d->available() + ev_bytes[d->index];
-    if (target < 0 || reach > best) { target = d->index; best = reach; }
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    // target dir: the one that can reach `bytes` with the most (available + evictable)
+    int target = -1;
+    uint64_t best = 0;
+    for (auto& d : dirs_) {
+      if (dir >= 0 && d->index != dir) continue;
+      if (!dir_matches(*d, tier, medium)) continue;
+      const uint64_t reach = d->available() + dir_ev_bytes_[d->index];
+      if (target < 0 || reach > best) { target = d->index; best = reach; }
+    }
+    if (target < 0) throw StoreError(kErrOutOfSpace, "no storage dir matches the eviction location");
+    if (dirs_[target]->available() >= bytes) return;
+    // arena dirs free whole pages: convert the shortfall into page-rounded bytes
+    uint64_t need = bytes - dirs_[target]->available();
+    if (dirs_[target]->spec.kind != DirKind::kFile)
+      need = ceil_div(need, dirs_[target]->spec.page_size) * dirs_[target]->spec.page_size;
+    ++stats_.selections;
+    const uint64_t seq = create_seq_;
+    std::vector<uint32_t> victims;
+    if (device_evict_active()) {
+      victims = select_victims_device(lk, target, need);
+    } else {
+      std::vector<uint32_t> cand;
+      for (auto& kv : blocks_)
+        if (kv.second.dir == target && evictable(kv.second)) cand.push_back(kv.second.slot);
+      stats_.candidates += cand.size();
+      victims = select_victims_cpu(cand, need);
+    }
+    // the store may have changed while it was unlocked: a victim must still be the same block
+    // (created before the selection), in the target dir, and evictable now
+    for (uint32_t s : victims) {
+      BlockMeta* b = find(slot_block_[s]);
+      if (b && b->seq <= seq && b->dir == target && evictable(*b)) {
+        remove_locked(*b, true);
+        ++stats_.victims;
+      } else {
+        ++stats_.revalidated_away;
+      }
+    }
+    if (dirs_[target]->available() >= bytes) return;
+    if (victims.empty()) break;
   }
-  if (target < 0) throw StoreError(kErrOutOfSpace, "no storage dir matches the eviction location");
-  StorageDir& td = *dirs_[target];
-  if (td.available() >= bytes) return;
-  // arena dirs free whole pages: convert the shortfall into page-rounded bytes
-  uint64_t need = bytes - td.available();
-  if (td.spec.kind != DirKind::kFile) need = ceil_div(need, td.spec.page_size) * td.spec.page_size;
-  std::vector<uint32_t> cand;
-  for (auto& kv : blocks_)
-    if (kv.second.dir == target && evictable(kv.second)) cand.push_back(kv.second.slot);
-  // page-rounded victim sizes: a block frees ceil(len/page) pages
-  std::vector<uint32_t> victims = select_victims(cand, need);
-  for (uint32_t s : victims) {
-    BlockMeta* b = find(slot_block_[s]);
-    if (b && evictable(*b)) remove_locked(*b, true);
-  }
-  if (td.available() < bytes)
-    throw StoreError(kErrOutOfSpace, "failed to free " + std::to_string(bytes) + " bytes in dir " +
-                                         std::to_string(target) + " (available " +
-                                         std::to_string(td.available()) + ")");
+  throw StoreError(kErrOutOfSpace, "failed to free " + std::to_string(bytes) + " bytes (tier " +
+                                       std::to_string(tier) + ", dir " + std::to_string(dir) + ")");
 }
 
 std::vector<int64_t> BlockStore::free_space(int64_t session, uint64_t bytes, int tier, int dir) {
@@ -1000,16 +1185,214 @@ std::vector<int64_t> BlockStore::free_space(int64_t session, uint64_t bytes, int
   return gone;
 }
 
+// Full annotator order (coldest first): a ranking, so it is the CPU sort (tier management uses
+// ranks; eviction itself uses the device select).
 std::vector<int64_t> BlockStore::eviction_order(int tier, uint64_t need_bytes) {
   std::unique_lock<std::mutex> lk(mu_);
   std::vector<uint32_t> cand;
   for (auto& kv : blocks_)
     if ((tier < 0 || dirs_[kv.second.dir]->spec.tier == tier) && evictable(kv.second)) cand.push_back(kv.second.slot);
   if (need_bytes == 0) need_bytes = ~0ull;
-  std::vector<uint32_t> v = select_victims(cand, need_bytes);
+  std::vector<uint32_t> v = select_victims_cpu(cand, need_bytes);
   std::vector<int64_t> out;
   out.reserve(v.size());
   for (uint32_t s : v) out.push_back(slot_block_[s]);
+  return out;
+}
+
+std::vector<int64_t> BlockStore::select_for_bench(int dir, uint64_t need, bool device) {
+  set_device();
+  std::unique_lock<std::mutex> lk(mu_);
+  if (dir < 0 || dir >= (int)dirs_.size()) throw StoreError(kErrInvalidArgument, "bad dir");
+  std::vector<uint32_t> v;
+  if (device) {
+    if (!has_device_) throw StoreError(kErrInvalidArgument, "no device");
+    const bool was = use_device_evict_;
+    if (!was) dev_synced_ = false;
+    use_device_evict_ = true;
+    try {
+      v = select_victims_device(lk, dir, need);
+    } catch (...) {
+      use_device_evict_ = was;
+      throw;
+    }
+    use_device_evict_ = was;
+  } else {
+    std::vector<uint32_t> cand;
+    for (auto& kv : blocks_)
+      if (kv.second.dir == dir && evictable(kv.second)) cand.push_back(kv.second.slot);
+    v = select_victims_cpu(cand, need);
+  }
+  std::vector<int64_t> out;
+  out.reserve(v.size());
+  for (uint32_t s : v) out.push_back(slot_block_[s]);
+  return out;
+}
+
+BlockStore::EvictStats BlockStore::evict_stats() {
+  std::unique_lock<std::mutex> lk(mu_);
+  return stats_;
+}
+
+// -------------------------------------------------------------------------------------------
+// K7: device page allocation for bulk creates
+std::vector<int64_t> BlockStore::device_alloc_pages(std::unique_lock<std::mutex>& lk, int dir, uint32_t want) {
+  StorageDir& d = *dirs_[dir];
+  const uint32_t nwords = (uint32_t)d.free_bits.size();
+  std::vector<int64_t> pages;
+  {
+    std::unique_lock<std::mutex> g(ev_mu_);
+    set_device();
+    if (d_bits_cap_ < nwords) {
+      if (d_bits_) hipFree(d_bits_);
+      d_bits_ = nullptr;
+      HIP_OK(hipMalloc((void**)&d_bits_, (size_t)nwords * 8));
+      d_bits_cap_ = nwords;
+    }
+    const uint32_t np = page_alloc_partials(nwords);
+    if (d_partial_cap_ < np) {
+      if (d_partial_) hipFree(d_partial_);
+      d_partial_ = nullptr;
+      HIP_OK(hipMalloc((void**)&d_partial_, (size_t)std::max<uint32_t>(np, 1) * 4));
+      d_partial_cap_ = np;
+    }
+    if (h_pages_cap_ < want) {
+      if (h_pages_) hipHostFree(h_pages_);
+      h_pages_ = nullptr;
+      const size_t cap = std::max<size_t>(want, 4096);
+      HIP_OK(hipHostMalloc((void**)&h_pages_, cap * 8, hipHostMallocMapped));
+      HIP_OK(hipHostGetDevicePointer((void**)&h_pages_dev_, h_pages_, 0));
+      h_pages_cap_ = cap;
+    }
+    // snapshot of the authoritative host bitmap (pageable copy: the bytes are taken at the call)
+    std::vector<uint64_t> snap = d.free_bits;
+    lk.unlock();
+    hipError_t e = hipMemcpyAsync(d_bits_, snap.data(), (size_t)nwords * 8, hipMemcpyHostToDevice, internal_stream_);
+    if (e == hipSuccess) e = launch_page_alloc(d_bits_, nwords, want, d_partial_, h_pages_dev_, d_claimed_, internal_stream_);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_claimed_, d_claimed_, 4, hipMemcpyDeviceToHost, internal_stream_);
+    if (e == hipSuccess) e = hipStreamSynchronize(internal_stream_);
+    if (e == hipSuccess) pages.assign(h_pages_, h_pages_ + std::min(*h_claimed_, want));
+    g.unlock();
+    lk.lock();
+    if (e != hipSuccess) throw StoreError(kErrHip, std::string("device page alloc: ") + hipGetErrorString(e));
+  }
+  // claim on the host bitmap; pages taken meanwhile by host allocations are dropped
+  std::vector<int64_t> got;
+  got.reserve(pages.size());
+  for (int64_t p : pages)
+    if (p < d.num_pages && bit_free(d.free_bits, p)) {
+      bit_take(d.free_bits, p);
+      --d.free_pages;
+      got.push_back(p);
+    }
+  ++stats_.device_allocs;
+  stats_.device_alloc_pages += got.size();
+  return got;
+}
+
+std::vector<int64_t> BlockStore::peek_free_pages(int dir, uint32_t want, bool device) {
+  set_device();
+  std::unique_lock<std::mutex> lk(mu_);
+  if (dir < 0 || dir >= (int)dirs_.size() || dirs_[dir]->spec.kind == DirKind::kFile)
+    throw StoreError(kErrInvalidArgument, "peek_free_pages needs an arena dir");
+  StorageDir& d = *dirs_[dir];
+  if (!device) {
+    std::vector<int64_t> out;
+    for (int64_t w = 0; w < (int64_t)d.free_bits.size() && out.size() < want; ++w) {
+      uint64_t word = d.free_bits[w];
+      while (word && out.size() < want) {
+        const int b0 = __builtin_ctzll(word);
+        word &= word - 1;
+        if (w * 64 + b0 < d.num_pages) out.push_back(w * 64 + b0);
+      }
+    }
+    return out;
+  }
+  if (!has_device_) throw StoreError(kErrInvalidArgument, "no device");
+  std::vector<int64_t> got = device_alloc_pages(lk, dir, want);
+  // give them back: a peek
+  for (int64_t p : got) {
+    bit_give(d.free_bits, p);
+    ++d.free_pages;
+  }
+  --stats_.device_allocs;
+  stats_.device_alloc_pages -= got.size();
+  return got;
+}
+
+std::vector<int> BlockStore::create_blocks(int64_t session, const std::vector<int64_t>& ids, int tier,
+                                           const std::string& medium, const std::vector<uint64_t>& sizes,
+                                           bool evict) {
+  if (ids.size() != sizes.size()) throw StoreError(kErrInvalidArgument, "ids/sizes length mismatch");
+  set_device();
+  std::unique_lock<std::mutex> lk(mu_);
+  std::unordered_set<int64_t> seen;
+  uint64_t total = 0;
+  for (size_t i = 0; i < ids.size(); ++i) {
+    if (blocks_.count(ids[i]) || !seen.insert(ids[i]).second)
+      throw StoreError(kErrAlreadyExists, "block " + std::to_string(ids[i]) + " already exists");
+    total += std::max<uint64_t>(sizes[i], 1);
+  }
+  int d = allocate_dir(tier, medium, total);
+  if (d < 0 && evict) {
+    free_space_locked(lk, session, total, tier, -1, medium);
+    for (int64_t id : ids)
+      if (blocks_.count(id)) throw StoreError(kErrAlreadyExists, "block " + std::to_string(id) + " already exists");
+    d = allocate_dir(tier, medium, total);
+  }
+  std::vector<int> out;
+  if (d < 0) {
+    // no single dir holds all of them: one at a time (each may pick its own dir)
+    lk.unlock();
+    for (size_t i = 0; i < ids.size(); ++i) out.push_back(create_block(session, ids[i], tier, medium, sizes[i], evict, false));
+    return out;
+  }
+  StorageDir& sd = *dirs_[d];
+  std::vector<int64_t> pool;
+  size_t pool_pos = 0;
+  if (sd.spec.kind == DirKind::kDevice && use_device_alloc_) {
+    uint64_t want = 0;
+    for (uint64_t sz : sizes) want += ceil_div(std::max<uint64_t>(sz, 1), sd.spec.page_size);
+    if (want >= device_alloc_min_pages_ && want <= sd.free_pages) pool = device_alloc_pages(lk, d, (uint32_t)want);
+  }
+  for (size_t i = 0; i < ids.size(); ++i) {
+    if (blocks_.count(ids[i])) {
+      for (size_t k = pool_pos; k < pool.size(); ++k) { bit_give(sd.free_bits, pool[k]); ++sd.free_pages; }
+      throw StoreError(kErrAlreadyExists, "block " + std::to_string(ids[i]) + " already exists");
+    }
+    BlockMeta b;
+    b.id = ids[i];
+    b.dir = d;
+    b.temp = true;
+    b.session = session;
+    const uint64_t sz = std::max<uint64_t>(sizes[i], 1);
+    if (sd.spec.kind != DirKind::kFile && pool_pos < pool.size()) {
+      const size_t np = (size_t)ceil_div(sz, sd.spec.page_size);
+      while (b.pages.size() < np && pool_pos < pool.size()) b.pages.push_back(pool[pool_pos++]);
+      b.reserved = b.pages.size() * sd.spec.page_size;
+    }
+    if (!grow_pages(sd, b, sz)) {
+      release_storage(b);
+      for (size_t k = pool_pos; k < pool.size(); ++k) { bit_give(sd.free_bits, pool[k]); ++sd.free_pages; }
+      throw StoreError(kErrOutOfSpace, "bulk allocation ran out of space at block " + std::to_string(ids[i]));
+    }
+    b.slot = alloc_slot();
+    b.seq = ++create_seq_;
+    slot_block_[b.slot] = b.id;
+    crf_[b.slot] = 0.f;
+    last_[b.slot] = clock_.load();
+    note_state(b, true);
+    if (sd.spec.kind == DirKind::kFile) {
+      const std::string p = sd.spec.path + "/.tmp_blocks/" + std::to_string(session) + "-" + std::to_string(b.id);
+      int fd = ::open(p.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+      if (fd < 0) throw StoreError(kErrIo, "cannot create " + p);
+      ::close(fd);
+    }
+    session_temps_[session].insert(b.id);
+    blocks_.emplace(b.id, std::move(b));
+    out.push_back(d);
+  }
+  for (size_t k = pool_pos; k < pool.size(); ++k) { bit_give(sd.free_bits, pool[k]); ++sd.free_pages; }
   return out;
 }
 

@@ -7,8 +7,11 @@
 //   * further tiers are pinned-host arenas (medium DRAM) or file directories (SSD/HDD);
 //   * allocation = host bitmap scan for a contiguous run, falling back to scattered pages
 //     (reference MaxFree/Greedy/RoundRobin allocators choose the dir, allocator/*.java);
-//   * eviction ordering = LRU or LRFU annotations (annotator/LRFUAnnotator.java:81-95) scored and
-//     selected on the GPU by a fused radix-select kernel (kernels.hip, evict_select_kernel);
+//   * eviction ordering = LRU or LRFU annotations (annotator/LRFUAnnotator.java:81-95) kept
+//     resident in HBM per block slot (host mirrors only queue coalesced updates) and selected by a
+//     grid-wide byte-weighted radix select (evict_alloc.hip) without holding the store mutex
+//     across the device round trip;
+//   * batched multi-block creates claim their pages with the device bitmap allocator (K7);
 //   * reads/writes are planned into page-contiguous segments and executed by one batched copy
 //     kernel launch per batch (kernels.hip, batched_copy_kernel) or by DMA for host endpoints.
 // Block locks (BlockLockManager.java), sessions (Sessions.java) and temp->committed lifecycle
@@ -92,6 +95,7 @@ struct BlockMeta {
   bool writer = false;
   bool evicting = false;
   uint32_t slot = 0;
+  uint64_t seq = 0;        // creation sequence (victims chosen off-lock are re-validated with it)
   std::vector<uint32_t> crc;
   uint64_t crc_piece = 0;
 };
@@ -135,6 +139,10 @@ class BlockStore {
   // medium non-empty selects dirs of that medium.  Evicts if allowed and needed.
   int create_block(int64_t session, int64_t block_id, int tier, const std::string& medium,
                    uint64_t initial, bool evict, bool pin);
+  // Many temp blocks at once (bulk ingest): one dir choice and, for an HBM dir, one device
+  // page-allocation launch (K7) for all of their pages.  Returns the dir of each block.
+  std::vector<int> create_blocks(int64_t session, const std::vector<int64_t>& block_ids, int tier,
+                                 const std::string& medium, const std::vector<uint64_t>& sizes, bool evict);
   void request_space(int64_t session, int64_t block_id, uint64_t additional);
   // Append/overwrite bytes of a temp block (auto-grows).  src_kind: MemKind.
   // Reserve pages for [offset, offset+len) of a temp block and mark those bytes as written by
@@ -175,7 +183,24 @@ class BlockStore {
   // tier management), computed by the same kernel/CPU path.
   std::vector<int64_t> eviction_order(int tier, uint64_t need_bytes);
   void set_pinned_files(const std::vector<int64_t>& file_ids);
-  void set_use_device_evict(bool v) { use_device_evict_ = v; }
+  void set_use_device_evict(bool v) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (v && !use_device_evict_) dev_synced_ = false;
+    use_device_evict_ = v;
+  }
+  void set_use_device_alloc(bool v, uint32_t min_pages) {
+    use_device_alloc_ = v;
+    device_alloc_min_pages_ = min_pages;
+  }
+  // Victim selection alone (no removal), for benchmarks/tests: device grid select or CPU sort.
+  std::vector<int64_t> select_for_bench(int dir, uint64_t need, bool device);
+  // K7 alone on a dir's current bitmap, without claiming (benchmarks/tests).
+  std::vector<int64_t> peek_free_pages(int dir, uint32_t want, bool device);
+  struct EvictStats {
+    uint64_t selections = 0, device_selections = 0, candidates = 0, victims = 0, revalidated_away = 0;
+    uint64_t device_allocs = 0, device_alloc_pages = 0, annotation_flushes = 0, annotation_updates = 0;
+  };
+  EvictStats evict_stats();
 
   // ---- introspection ----------------------------------------------------------------------
   bool has_block(int64_t block_id);
@@ -207,8 +232,18 @@ class BlockStore {
   void release_storage(BlockMeta& b);
   void free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
                          int tier, int dir, const std::string& medium);
-  std::vector<uint32_t> select_victims(const std::vector<uint32_t>& cand_slots, uint64_t need);
+  std::vector<uint32_t> select_victims_cpu(const std::vector<uint32_t>& cand_slots, uint64_t need);
+  std::vector<uint32_t> select_victims_device(std::unique_lock<std::mutex>& lk, int dir, uint64_t need);
   void remove_locked(BlockMeta& b, bool emit_event);
+  // device annotator bookkeeping (all under mu_)
+  uint64_t footprint(const BlockMeta& b) const;
+  void note_state(const BlockMeta& b, bool live);
+  void mark_dirty(uint32_t slot);
+  void ensure_dev_slots_locked(size_t n);
+  void flush_annotations_locked();
+  EvictState dev_state(uint64_t now) const;
+  bool device_evict_active() const { return has_device_ && use_device_evict_; }
+  std::vector<int64_t> device_alloc_pages(std::unique_lock<std::mutex>& lk, int dir, uint32_t want);
   uint32_t alloc_slot();
   void touch_slot(uint32_t slot);
   bool evictable(const BlockMeta& b) const;
@@ -241,12 +276,26 @@ class BlockStore {
   std::vector<int64_t> slot_block_;
   std::vector<uint32_t> free_slots_;
   std::atomic<uint64_t> clock_{0};
+  uint64_t create_seq_ = 0;
+  std::vector<int32_t> slot_dir_;            // mirror of the device dir[] (evictable dir or -1)
+  std::vector<uint64_t> slot_fb_;            // mirror of fbytes[]
+  std::vector<uint64_t> dir_ev_bytes_;       // per dir: footprint of statically evictable blocks
+  std::unordered_set<int64_t> evicting_ids_;
+  // slots whose mirror (crf_, last_, slot_dir_, slot_fb_) changed since the last device flush
+  std::vector<uint32_t> dirty_;
+  std::vector<uint8_t> dirty_flag_;
+  bool dev_synced_ = false;                  // device arrays hold every slot's mirror values
+  EvictStats stats_;
   std::vector<int> rr_index_;  // round-robin cursor per tier
   std::vector<Event> events_;
   // device resources
   int device_ = -1;
   bool has_device_ = false;
   bool use_device_evict_ = true;
+  // K7 measured slower than the host bitmap scan end to end (profiles/r2_evict_bench.jsonl):
+  // off unless alluxio.worker.hbm.device.alloc.enabled
+  bool use_device_alloc_ = false;
+  uint32_t device_alloc_min_pages_ = 64;
   hipStream_t internal_stream_ = nullptr;
   static constexpr int kRing = 8;
   static constexpr int kRingSegs = 8192;
@@ -255,10 +304,36 @@ class BlockStore {
   hipEvent_t ring_ev_[kRing] = {};
   int ring_pos_ = 0;
   std::mutex ring_mu_;
-  // eviction kernel scratch (grown on demand)
-  size_t ev_cap_ = 0;
-  void* ev_dev_ = nullptr;
-  std::mutex ev_mu_;
+  // device annotator arrays (slot-indexed, grown by doubling under mu_ + ev_mu_)
+  size_t dev_slots_ = 0;
+  float* d_crf_ = nullptr;
+  uint64_t* d_last_ = nullptr;
+  uint64_t* d_fbytes_ = nullptr;
+  int32_t* d_dir_ = nullptr;
+  uint32_t* d_keys_ = nullptr;
+  uint32_t* d_excl_ = nullptr;
+  uint32_t* h_excl_ = nullptr;       // pinned exclusion bitmap (locked slots of one selection)
+  EvictCtl* d_ctl_ = nullptr;
+  EvictCtl* h_ctl_ = nullptr;        // pinned readback
+  uint32_t* h_out_ = nullptr;        // pinned, device-mapped victim list
+  uint32_t* h_out_dev_ = nullptr;
+  SlotUpdate* h_upd_[2] = {nullptr, nullptr};
+  size_t h_upd_cap_[2] = {0, 0};
+  hipEvent_t upd_ev_[2] = {};
+  int upd_pos_ = 0;
+  SlotUpdate* d_upd_ = nullptr;
+  size_t d_upd_cap_ = 0;
+  // K7 scratch
+  uint64_t* d_bits_ = nullptr;
+  size_t d_bits_cap_ = 0;
+  uint32_t* d_partial_ = nullptr;
+  size_t d_partial_cap_ = 0;
+  int64_t* h_pages_ = nullptr;       // pinned, device-mapped page list
+  int64_t* h_pages_dev_ = nullptr;
+  size_t h_pages_cap_ = 0;
+  uint32_t* h_claimed_ = nullptr;
+  uint32_t* d_claimed_ = nullptr;
+  std::mutex ev_mu_;                 // device selection / allocation scratch (taken after mu_)
   // checksum scratch
   uint32_t* crc_dev_ = nullptr;
   size_t crc_cap_ = 0;

@@ -1,0 +1,362 @@
+// K4-K7 on the device: slot-resident LRU/LRFU annotations, multi-workgroup byte-weighted eviction
+// select, and the batched bitmap page allocator (gfx950, wave64).
+//
+// Reference loops these replace:
+//   K4/K5 LRU / LRFU ordering   core/server/worker/.../block/annotator/LRFUAnnotator.java:81-95
+//                               (CRF = CRF * (1/att)^(step * age) + 1 on every access)
+//   K6    free-space loop       core/server/worker/.../block/TieredBlockStore.java:740-815
+//                               (walk the annotator order until enough bytes are freed)
+//   K7    allocation            core/server/worker/.../block/allocator/MaxFreeAllocator.java:42-110
+//
+// Design (see block_store.cpp "device annotator"): the annotation arrays live in HBM, indexed by
+// block slot, and are only *updated* from the host through SlotUpdate batches (one per dirty slot
+// per flush, carrying the host mirror's values; the kernel can also fold an access in place, the
+// LRFU decay being multiplicative).  A selection
+// never uploads candidate arrays: keys are computed on the fly from the resident arrays, filtered
+// by target dir and a small exclusion bitmap (locked blocks), then a 4-pass MSB-first radix select
+// over byte-weighted histograms runs across the whole grid: every workgroup builds an LDS
+// histogram, adds it to the global one, and the last workgroup to finish a pass (threadfence +
+// arrival counter) scans it and fixes the next digit -- no host round trip between passes.  The
+// compaction writes victim slots straight to pinned host memory with one atomic per wave.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.h"
+
+namespace amdx {
+
+namespace {
+
+constexpr int kEvBlock = 256;
+// The passes are latency- and atomic-bound, not bandwidth-bound (150k keys = 600 KB).  Measured
+// on MI355X at 150k keys (profiles/r2_evict_bench.md): 256 workgroups adding their LDS histograms
+// to the global one with atomics = 20.6 us/pass; a plain-store slab summed by the last workgroup
+// = 27 us (64 rows) / 38 us (256 rows); 128 workgroups with 4-deep unrolled key loads + atomics
+// is the default.
+constexpr unsigned kEvMaxGrid = kEvSlabRows;
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+__device__ __forceinline__ uint32_t evict_key(const EvictState& st, uint32_t i, uint32_t target_dir,
+                                              const uint32_t* __restrict__ excl) {
+  if (st.dir[i] != (int32_t)target_dir) return 0xFFFFFFFFu;
+  if (excl && ((excl[i >> 5] >> (i & 31)) & 1u)) return 0xFFFFFFFFu;
+  const uint64_t last = st.last[i];
+  const uint64_t age = st.now > last ? st.now - last : 0;
+  if (st.policy == 0) return 0xFFFFFFFEu - (uint32_t)(age < 0xFFFFFFFEull ? age : 0xFFFFFFFEull);
+  float crf = st.crf[i] * exp2f(st.log2_inv_att * st.step * (float)age);
+  if (!(crf >= 0.0f)) crf = 0.0f;
+  uint32_t key = __float_as_uint(crf);   // non-negative floats order like their bits
+  return key >= 0xFFFFFFFEu ? 0xFFFFFFFDu : key;
+}
+
+// ---- annotation updates ----------------------------------------------------------------------
+__global__ __launch_bounds__(kEvBlock) void slot_update_kernel(EvictState st, const SlotUpdate* __restrict__ u,
+                                                                uint32_t n) {
+  for (uint32_t j = blockIdx.x * kEvBlock + threadIdx.x; j < n; j += gridDim.x * kEvBlock) {
+    const SlotUpdate x = u[j];
+    const uint32_t s = x.slot;
+    if (x.flags & kSlotSetState) {
+      st.dir[s] = x.dir;
+      st.fbytes[s] = x.fbytes;
+    }
+    if (x.flags & kSlotReset) {
+      st.crf[s] = x.crf;
+      st.last[s] = x.t;
+    } else if (x.flags & kSlotTouch) {
+      const uint64_t last = st.last[s];
+      const uint64_t age = x.t > last ? x.t - last : 0;
+      st.crf[s] = st.crf[s] * exp2f(st.log2_inv_att * st.step * (float)age) + x.crf;
+      st.last[s] = x.t;
+    }
+  }
+}
+
+// ---- selection ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kEvBlock) void ev_keys_kernel(EvictState st, uint32_t target_dir,
+                                                            const uint32_t* __restrict__ excl,
+                                                            uint32_t* __restrict__ keys, EvictCtl* ctl) {
+  __shared__ unsigned long long s_tot[kEvBlock / 64];
+  unsigned long long tot = 0;
+  for (uint32_t i = blockIdx.x * kEvBlock + threadIdx.x; i < st.n; i += gridDim.x * kEvBlock) {
+    const uint32_t k = evict_key(st, i, target_dir, excl);
+    keys[i] = k;
+    if (k != 0xFFFFFFFFu) tot += st.fbytes[i];
+  }
+  tot = wave_sum_u64(tot);
+  if (lane_id() == 0) s_tot[threadIdx.x >> 6] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {   // one global atomic per workgroup
+    unsigned long long t = 0;
+    for (int w = 0; w < kEvBlock / 64; ++w) t += s_tot[w];
+    if (t) atomicAdd(&ctl->total, t);
+  }
+}
+
+__global__ __launch_bounds__(kEvBlock) void ev_hist_kernel(const uint32_t* __restrict__ keys,
+                                                            const uint64_t* __restrict__ fbytes, uint32_t n,
+                                                            uint64_t need, int pass, EvictCtl* ctl) {
+  __shared__ unsigned long long h[256];
+  __shared__ unsigned long long scan[256];
+  __shared__ int s_last;
+  const int tid = threadIdx.x;
+  // pass 0 decides whether everything must go (no select needed)
+  if (pass == 0 && ctl->total <= need) {
+    if (blockIdx.x == 0 && tid == 0) {
+      ctl->all = 1;
+      ctl->prefix = 0xFFFFFFFFu;
+      ctl->mask = 0xFFFFFFFFu;
+    }
+    return;
+  }
+  if (ctl->all) return;
+  const int shift = 24 - 8 * pass;
+  const uint32_t prefix = ctl->prefix, mask = ctl->mask;
+  h[tid] = 0;
+  __syncthreads();
+  // whole waves iterate together (the uniform-digit fast path needs every lane in the ballot);
+  // four keys per lane per round, loads issued before any use
+  const uint32_t stride = gridDim.x * kEvBlock;
+  const uint32_t rounds = (n + 4 * stride - 1) / (4 * stride);
+  for (uint32_t r = 0; r < rounds; ++r) {
+    uint32_t kk[4];
+    unsigned long long bb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = (r * 4 + u) * stride + blockIdx.x * kEvBlock + tid;
+      kk[u] = i < n ? keys[i] : 0xFFFFFFFFu;
+      bb[u] = i < n ? (unsigned long long)fbytes[i] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t k = kk[u];
+      const bool valid = k != 0xFFFFFFFFu && (k & mask) == prefix;
+      const uint32_t dig = (k >> shift) & 255u;
+      const unsigned long long vb = valid ? bb[u] : 0ull;
+      const unsigned long long vm = __ballot(valid);
+      if (!vm) continue;
+      // skewed passes (LRU clocks share their high bytes) put a whole wave on one digit: one
+      // wave-reduced LDS atomic instead of 64 serialized ones on the same bin
+      const uint32_t lead = (uint32_t)__shfl(dig, __builtin_ctzll(vm), 64);
+      if (__ballot(valid && dig == lead) == vm) {
+        const unsigned long long sum = wave_sum_u64(vb);
+        if (lane_id() == 0) atomicAdd(&h[lead], sum);
+      } else if (valid) {
+        atomicAdd(&h[dig], vb);
+      }
+    }
+  }
+  __syncthreads();
+  if (h[tid]) atomicAdd(&ctl->hist[tid], h[tid]);
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(&ctl->done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  // last workgroup of the pass: inclusive scan of the global histogram, pick the digit
+  __threadfence();
+  const unsigned long long v = __hip_atomic_load(&ctl->hist[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  scan[tid] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const unsigned long long add = tid >= o ? scan[tid - o] : 0ull;
+    __syncthreads();
+    scan[tid] += add;
+    __syncthreads();
+  }
+  const unsigned long long acc = ctl->acc;
+  const unsigned long long incl = acc + scan[tid];
+  const unsigned long long excl_b = incl - v;
+  const bool hit = incl >= need && excl_b < need;
+  __shared__ int s_d;
+  if (tid == 0) s_d = 255;
+  __syncthreads();
+  if (hit) s_d = tid;   // exactly one thread (scan is monotone)
+  __syncthreads();
+  if (tid == 0) {
+    const int d = s_d;
+    ctl->acc = acc + (d > 0 ? scan[d - 1] : 0ull);
+    ctl->prefix = prefix | ((uint32_t)d << shift);
+    ctl->mask = mask | (255u << shift);
+    ctl->done = 0;
+  }
+  ctl->hist[tid] = 0;
+}
+
+__global__ __launch_bounds__(kEvBlock) void ev_compact_kernel(const uint32_t* __restrict__ keys,
+                                                               const uint64_t* __restrict__ fbytes, uint32_t n,
+                                                               uint64_t need, EvictCtl* ctl,
+                                                               uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_cnt[kEvBlock / 64];
+  __shared__ uint32_t s_base;
+  __shared__ unsigned long long s_freed[kEvBlock / 64];
+  const uint32_t T = ctl->prefix;
+  const bool all = ctl->all != 0;
+  const unsigned long long below = ctl->acc;
+  const uint32_t wave = threadIdx.x >> 6;
+  unsigned long long freed = 0;
+  // every lane of a wave walks the same number of iterations (ballots need the whole wave)
+  const uint32_t stride = gridDim.x * kEvBlock;
+  const uint32_t iters = (n + stride - 1) / stride;
+  for (uint32_t it = 0; it < iters; ++it) {
+    const uint32_t i = it * stride + blockIdx.x * kEvBlock + threadIdx.x;
+    bool take = false;
+    uint64_t b = 0;
+    if (i < n) {
+      const uint32_t k = keys[i];
+      if (k != 0xFFFFFFFFu) {
+        b = fbytes[i];
+        take = all || k < T;
+        if (!take && k == T) {
+          const unsigned long long prev = atomicAdd(&ctl->tie_acc, (unsigned long long)b);
+          take = below + prev < need;
+        }
+      }
+    }
+    const unsigned long long m = __ballot(take);
+    if (lane_id() == 0) s_cnt[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {   // one output reservation per workgroup and iteration
+      uint32_t t = 0;
+      for (int w = 0; w < kEvBlock / 64; ++w) {
+        const uint32_t c = s_cnt[w];
+        s_cnt[w] = t;
+        t += c;
+      }
+      s_base = t ? atomicAdd(&ctl->count, t) : 0u;
+    }
+    __syncthreads();
+    if (take) {
+      out[s_base + s_cnt[wave] + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = i;
+      freed += b;
+    }
+    __syncthreads();
+  }
+  freed = wave_sum_u64(freed);
+  if (lane_id() == 0) s_freed[wave] = freed;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kEvBlock / 64; ++w) t += s_freed[w];
+    if (t) atomicAdd(&ctl->freed, t);
+  }
+}
+
+// ---- K7 page allocation -------------------------------------------------------------------------
+// Claim the `want` lowest-numbered free pages of a bitmap (1 = free): per-workgroup popcount,
+// then each workgroup ranks its words (block scan + sum of the preceding workgroups' counts) and
+// claims the free bits whose global rank < want.
+constexpr int kPaBlock = 256;
+
+__global__ __launch_bounds__(kPaBlock) void palloc_count_kernel(const uint64_t* __restrict__ bits,
+                                                                  uint32_t nwords, uint32_t* __restrict__ partial) {
+  const uint32_t w = blockIdx.x * kPaBlock + threadIdx.x;
+  unsigned long long c = w < nwords ? (unsigned long long)__popcll(bits[w]) : 0ull;
+  c = wave_sum_u64(c);
+  __shared__ uint32_t s[kPaBlock / 64];
+  if (lane_id() == 0) s[threadIdx.x >> 6] = (uint32_t)c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int i = 0; i < kPaBlock / 64; ++i) t += s[i];
+    partial[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kPaBlock) void palloc_emit_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
+                                                                 const uint32_t* __restrict__ partial,
+                                                                 uint32_t want, int64_t* __restrict__ pages_out,
+                                                                 uint32_t* __restrict__ claimed) {
+  __shared__ uint32_t s_wave[kPaBlock / 64];
+  __shared__ uint32_t s_base;
+  const uint32_t tid = threadIdx.x;
+  // base = free pages in the preceding workgroups
+  uint32_t pre = 0;
+  for (uint32_t j = tid; j < blockIdx.x; j += kPaBlock) pre += partial[j];
+  pre = (uint32_t)wave_sum_u64(pre);
+  if (lane_id() == 0) s_wave[tid >> 6] = pre;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t t = 0;
+    for (int i = 0; i < kPaBlock / 64; ++i) t += s_wave[i];
+    s_base = t;
+  }
+  __syncthreads();
+  const uint32_t base = s_base;
+  if (base >= want) return;
+  const uint32_t w = blockIdx.x * kPaBlock + tid;
+  const uint64_t word = w < nwords ? bits[w] : 0ull;
+  const uint32_t c = (uint32_t)__popcll(word);
+  // exclusive scan of c across the workgroup: wave scan + wave totals
+  uint32_t incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o, 64);
+    if ((int)lane_id() >= o) incl += v;
+  }
+  __syncthreads();
+  if (lane_id() == 63) s_wave[tid >> 6] = incl;
+  __syncthreads();
+  uint32_t wave_off = 0;
+  for (uint32_t i = 0; i < (tid >> 6); ++i) wave_off += s_wave[i];
+  uint32_t rank = base + wave_off + incl - c;
+  if (!c || rank >= want) return;
+  uint64_t rest = word, taken = 0;
+  while (rest && rank < want) {
+    const int b = __builtin_ctzll(rest);
+    rest &= rest - 1;
+    taken |= 1ull << b;
+    pages_out[rank++] = (int64_t)w * 64 + b;
+  }
+  bits[w] = word & ~taken;
+  atomicAdd(claimed, (uint32_t)__popcll(taken));
+}
+
+}  // namespace
+
+hipError_t launch_slot_update(const EvictState& st, const SlotUpdate* upd, uint32_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const unsigned grid = (unsigned)((n + kEvBlock - 1) / kEvBlock < 1024 ? (n + kEvBlock - 1) / kEvBlock : 1024);
+  hipLaunchKernelGGL(slot_update_kernel, dim3(grid), dim3(kEvBlock), 0, stream, st, upd, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_evict_select_grid(const EvictState& st, uint32_t target_dir, const uint32_t* excl,
+                                    uint64_t need, uint32_t* keys, EvictCtl* ctl, uint32_t* out_slots,
+                                    hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(ctl, 0, sizeof(EvictCtl), stream);
+  if (e != hipSuccess) return e;
+  if (st.n == 0) return hipSuccess;
+  // >= 1k keys per workgroup (four per thread), at most kEvMaxGrid workgroups
+  unsigned grid = (st.n + 1023) / 1024;
+  if (grid > kEvMaxGrid) grid = kEvMaxGrid;
+  hipLaunchKernelGGL(ev_keys_kernel, dim3(grid), dim3(kEvBlock), 0, stream, st, target_dir, excl, keys, ctl);
+  for (int pass = 0; pass < 4; ++pass)
+    hipLaunchKernelGGL(ev_hist_kernel, dim3(grid), dim3(kEvBlock), 0, stream, keys, st.fbytes, st.n, need, pass,
+                       ctl);
+  hipLaunchKernelGGL(ev_compact_kernel, dim3(grid), dim3(kEvBlock), 0, stream, keys, st.fbytes, st.n, need, ctl,
+                     out_slots);
+  return hipGetLastError();
+}
+
+hipError_t launch_page_alloc(uint64_t* bits, uint32_t nwords, uint32_t want, uint32_t* partial,
+                             int64_t* pages_out, uint32_t* claimed, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(claimed, 0, sizeof(uint32_t), stream);
+  if (e != hipSuccess || nwords == 0 || want == 0) return e;
+  const unsigned grid = (nwords + kPaBlock - 1) / kPaBlock;
+  hipLaunchKernelGGL(palloc_count_kernel, dim3(grid), dim3(kPaBlock), 0, stream, bits, nwords, partial);
+  hipLaunchKernelGGL(palloc_emit_kernel, dim3(grid), dim3(kPaBlock), 0, stream, bits, nwords, partial, want,
+                     pages_out, claimed);
+  return hipGetLastError();
+}
+
+uint32_t page_alloc_partials(uint32_t nwords) { return (nwords + kPaBlock - 1) / kPaBlock; }
+
+}  // namespace amdx

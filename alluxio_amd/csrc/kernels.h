@@ -85,24 +85,56 @@ void set_lz4_decode_variant(int v);
 hipError_t launch_lz4_compress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
                                hipStream_t stream);
 
-// Eviction candidate selection (fused LRU/LRFU scoring + byte-weighted radix select).
-struct EvictInput {
-  const float* crf;         // LRFU combined recency-frequency (per slot)
-  const uint64_t* last;     // logical access clock (per slot)
-  const uint64_t* bytes;    // block bytes (per slot)
-  const uint8_t* evictable; // 1 if the slot may be evicted (committed, unlocked, unpinned)
-  uint32_t n;
-  uint64_t now;             // current logical clock
-  float step_factor;        // LRFU step
-  float attenuation;        // LRFU attenuation (>1)
-  int policy;               // 0 = LRU, 1 = LRFU
-  uint64_t need_bytes;      // stop once the selected set frees this much
+// ---- device-resident annotations + grid-wide select (evict_alloc.hip) ----------------------
+// Slot-indexed arrays in HBM.  dir[s] = storage dir of a committed, statically evictable block
+// (not temp / pinned), -1 otherwise; fbytes = its page-rounded footprint.
+struct EvictState {
+  float* crf;
+  uint64_t* last;
+  uint64_t* fbytes;
+  int32_t* dir;
+  uint32_t n;            // slots in use (grid extent)
+  uint64_t now;          // logical access clock
+  float step;            // LRFU step factor
+  float log2_inv_att;    // log2(1 / attenuation)
+  int policy;            // 0 = LRU, 1 = LRFU
 };
-// Writes selected slots to out_slots (ascending score order is NOT guaranteed) and their count
-// to *out_count; out_bytes receives the bytes freed.
-hipError_t launch_evict_select(const EvictInput& in, uint32_t* keys_scratch,
-                               uint32_t* out_slots, uint32_t* out_count, uint64_t* out_bytes,
-                               hipStream_t stream);
+constexpr uint32_t kSlotSetState = 1, kSlotReset = 2, kSlotTouch = 4;
+// One coalesced host->device update per slot: state (dir, footprint) and/or annotations
+// (reset: crf = crf, last = t; touch: crf = crf_dev * decay(t - last_dev) + crf, last = t).
+struct SlotUpdate {
+  uint32_t slot;
+  uint32_t flags;
+  int32_t dir;
+  float crf;
+  uint64_t fbytes;
+  uint64_t t;
+};
+// Max selection grid (workgroups per pass).
+constexpr unsigned kEvSlabRows = 128;
+struct EvictCtl {
+  unsigned long long hist[256];
+  unsigned long long total;     // evictable footprint in the target dir
+  unsigned long long acc;       // bytes of keys strictly below the current prefix
+  unsigned long long tie_acc;
+  unsigned long long freed;
+  uint32_t prefix, mask;
+  uint32_t all, done;
+  uint32_t count, pad;
+};
+hipError_t launch_slot_update(const EvictState& st, const SlotUpdate* upd, uint32_t n, hipStream_t stream);
+// Smallest-key-first victims of `target_dir` whose footprints add up to >= need (all of them if
+// the dir holds less); `excl` (bitmap by slot, may be null) removes locked slots.  Victim slots
+// go to out_slots (device-visible, e.g. mapped pinned host), their count/bytes to ctl->count/freed.
+hipError_t launch_evict_select_grid(const EvictState& st, uint32_t target_dir, const uint32_t* excl,
+                                    uint64_t need, uint32_t* keys, EvictCtl* ctl, uint32_t* out_slots,
+                                    hipStream_t stream);
+// K7: claim the `want` lowest free pages of a free-page bitmap (1 = free) in place; pages_out
+// gets the page numbers, *claimed how many (< want if the bitmap ran out).  `partial` needs
+// page_alloc_partials(nwords) words.
+hipError_t launch_page_alloc(uint64_t* bits, uint32_t nwords, uint32_t want, uint32_t* partial,
+                             int64_t* pages_out, uint32_t* claimed, hipStream_t stream);
+uint32_t page_alloc_partials(uint32_t nwords);
 
 // K9: client page cache lookup.  Open-addressing (linear probing) table of page keys in HBM;
 // `key` = (interned file id << 24) | page index, so keys are exact (no hash collisions to

@@ -1039,113 +1039,6 @@ hipError_t launch_lz4_compress(const Lz4Chunk* chunks, int n, int32_t* out_sizes
 }
 
 // ---------------------------------------------------------------------------------------------
-// K4-K6: fused eviction scoring + byte-weighted radix select (single 1024-thread workgroup).
-// Key = LRU: 0xFFFFFFFE - min(age, 0xFFFFFFFE); LRFU: float bits of the decayed CRF
-// (CRF * (1/att)^(age*step)); non-evictable = 0xFFFFFFFF.  Four 8-bit MSB-first passes find the
-// smallest threshold T with bytes(key < T) + bytes(key == T) >= need; compaction emits every
-// key < T plus enough ties.  This is the reference's "iterate the annotator order until enough
-// contiguous/available space" loop (TieredBlockStore.freeSpaceInternal) done in one launch.
-// ---------------------------------------------------------------------------------------------
-constexpr int kEvThreads = 1024;
-
-__global__ __launch_bounds__(kEvThreads) void evict_select_kernel(
-    EvictInput in, uint32_t* __restrict__ keys, uint32_t* __restrict__ out_slots,
-    uint32_t* __restrict__ out_count, uint64_t* __restrict__ out_bytes) {
-  __shared__ unsigned long long hist[256];
-  __shared__ uint32_t s_prefix, s_mask;
-  __shared__ unsigned long long s_acc, s_tie_acc;
-  __shared__ uint32_t s_count;
-  __shared__ int s_all;
-  const int tid = threadIdx.x;
-  const float inv_att = 1.0f / in.attenuation;
-  // pass 0: keys + total evictable bytes
-  unsigned long long local_total = 0;
-  for (uint32_t i = tid; i < in.n; i += kEvThreads) {
-    uint32_t key = 0xFFFFFFFFu;
-    if (in.evictable[i]) {
-      const uint64_t age = in.now > in.last[i] ? in.now - in.last[i] : 0;
-      if (in.policy == 0) {
-        key = 0xFFFFFFFEu - (uint32_t)(age < 0xFFFFFFFEull ? age : 0xFFFFFFFEull);
-      } else {
-        float crf = in.crf[i] * powf(inv_att, (float)age * in.step_factor);
-        if (!(crf >= 0.0f)) crf = 0.0f;
-        key = __float_as_uint(crf);
-        if (key >= 0xFFFFFFFEu) key = 0xFFFFFFFDu;
-      }
-      local_total += in.bytes[i];
-    }
-    keys[i] = key;
-  }
-  if (tid == 0) { s_prefix = 0; s_mask = 0; s_acc = 0; s_count = 0; s_tie_acc = 0; s_all = 0; }
-  __shared__ unsigned long long s_total;
-  if (tid == 0) s_total = 0;
-  __syncthreads();
-  atomicAdd(&s_total, local_total);
-  __syncthreads();
-  if (s_total <= in.need_bytes) {
-    if (tid == 0) { s_all = 1; s_prefix = 0xFFFFFFFFu; s_mask = 0xFFFFFFFFu; }
-  }
-  __syncthreads();
-  if (!s_all) {
-    for (int pass = 0; pass < 4; ++pass) {
-      const int shift = 24 - 8 * pass;
-      for (int b = tid; b < 256; b += kEvThreads) hist[b] = 0;
-      __syncthreads();
-      const uint32_t prefix = s_prefix, mask = s_mask;
-      for (uint32_t i = tid; i < in.n; i += kEvThreads) {
-        const uint32_t k = keys[i];
-        if (k != 0xFFFFFFFFu && (k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], (unsigned long long)in.bytes[i]);
-      }
-      __syncthreads();
-      if (tid == 0) {
-        unsigned long long acc = s_acc;
-        int d = 0;
-        for (; d < 256; ++d) {
-          if (acc + hist[d] >= in.need_bytes) break;
-          acc += hist[d];
-        }
-        if (d == 256) d = 255;
-        s_acc = acc;
-        s_prefix = prefix | ((uint32_t)d << shift);
-        s_mask = mask | (255u << shift);
-      }
-      __syncthreads();
-    }
-  }
-  const uint32_t T = s_prefix;
-  const bool all = s_all != 0;
-  const unsigned long long below = s_acc;  // bytes strictly below T
-  // compaction
-  for (uint32_t i = tid; i < in.n; i += kEvThreads) {
-    const uint32_t k = keys[i];
-    if (k == 0xFFFFFFFFu) continue;
-    bool take = all || k < T;
-    if (!take && k == T) {
-      const unsigned long long prev = atomicAdd(&s_tie_acc, (unsigned long long)in.bytes[i]);
-      take = below + prev < in.need_bytes;
-    }
-    if (take) {
-      const uint32_t slot = atomicAdd(&s_count, 1u);
-      out_slots[slot] = i;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    *out_count = s_count;
-    unsigned long long freed = 0;
-    for (uint32_t j = 0; j < s_count; ++j) freed += in.bytes[out_slots[j]];
-    *out_bytes = freed;
-  }
-}
-
-hipError_t launch_evict_select(const EvictInput& in, uint32_t* keys_scratch, uint32_t* out_slots,
-                               uint32_t* out_count, uint64_t* out_bytes, hipStream_t stream) {
-  hipLaunchKernelGGL(evict_select_kernel, dim3(1), dim3(kEvThreads), 0, stream, in, keys_scratch,
-                     out_slots, out_count, out_bytes);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
 // Synthetic data generator (bench / tests): splitmix64 of (seed, 8-byte word index).
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {

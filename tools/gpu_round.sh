@@ -60,6 +60,12 @@ for s in $STEPS; do
       run pmc_dram_stagger 240 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram_stagger" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2 --phases local,stagger
       ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
+    evict)
+      run pytest_evict 300 python -u -m pytest tests/test_evict_alloc_gpu.py tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread
+      run evict_bench 300 python tools/evict_bench.py --counts 10000,150000 --out "$OUT/evict_bench.jsonl"
+      run evict_bench_lrfu 300 python tools/evict_bench.py --counts 150000 --policy 1 --out "$OUT/evict_bench.jsonl"
+      run rocprof_evict 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_evict" -o ev --output-format csv -- python3 tools/evict_bench.py --counts 150000 --iters 10
+      ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
     pcsweep) run page_cache_sweep 400 python tools/page_cache_bench.py --variants both --passes 2 --page-sizes 4k,8k,16k,32k,64k,256k --out "$OUT/page_cache_sweep.jsonl" ;;
     pcwave) run page_cache_wave 400 python tools/page_cache_bench.py --variants both --passes 2 --wave-variants 0,1,2,3 --page-sizes 4k,16k --iters 30 --out "$OUT/page_cache_wave.jsonl" ;;
