@@ -162,6 +162,13 @@ _k("WORKER_STAGING_BUFFER_SIZE", "alluxio.worker.staging.buffer.size", "64MB", S
 _k("WORKER_EVICTION_DEVICE_ENABLED", "alluxio.worker.eviction.device.enabled", "true", Scope.WORKER,
    "Keep the LRU/LRFU annotations in HBM and select eviction victims with the grid-wide device "
    "select (K4-K6) when the store has an HBM tier; false = host sort.")
+_k("WORKER_UFS_INGEST_CHUNK_SIZE", "alluxio.worker.ufs.ingest.chunk.size", "8MB", Scope.WORKER,
+   "UFS read size of the UFS->HBM ingest pipeline (one pinned staging buffer each).")
+_k("WORKER_UFS_INGEST_DEPTH", "alluxio.worker.ufs.ingest.depth", "3", Scope.WORKER,
+   "Staging buffers per ingest pipeline: UFS reads run this many chunks ahead of the H2D DMA.")
+_k("WORKER_TIEREDSTORE_EVICTION_DEMOTE", "alluxio.worker.tieredstore.eviction.demote", "true", Scope.WORKER,
+   "Eviction from a tier with a lower tier demotes the victims into it (one batched HBM->DRAM / "
+   "DRAM->SSD move, making room there recursively) instead of dropping them.")
 _k("WORKER_HBM_DEVICE_ALLOC_ENABLED", "alluxio.worker.hbm.device.alloc.enabled", "false", Scope.WORKER,
    "Claim the pages of bulk block creates with the device bitmap allocator (K7). Off by default: "
    "the host bitmap scan measured faster end to end (profiles/r2_evict_bench.jsonl).")

@@ -292,6 +292,9 @@ PYBIND11_MODULE(_C, m) {
       .def("set_pinned_files", &BlockStore::set_pinned_files, G())
       .def("set_use_device_evict", &BlockStore::set_use_device_evict, G())
       .def("set_use_device_alloc", &BlockStore::set_use_device_alloc, py::arg("enabled"), py::arg("min_pages") = 64)
+      .def("set_demote_on_evict", &BlockStore::set_demote_on_evict)
+      .def("move_blocks", &BlockStore::move_blocks, G(), py::arg("session"), py::arg("block_ids"), py::arg("tier"),
+           py::arg("medium") = "", py::arg("evict") = true)
       .def("create_blocks", &BlockStore::create_blocks, G(), py::arg("session"), py::arg("block_ids"),
            py::arg("tier") = -1, py::arg("medium") = "", py::arg("sizes") = std::vector<uint64_t>{},
            py::arg("evict") = true)
@@ -310,6 +313,10 @@ PYBIND11_MODULE(_C, m) {
              d["device_alloc_pages"] = st.device_alloc_pages;
              d["annotation_flushes"] = st.annotation_flushes;
              d["annotation_updates"] = st.annotation_updates;
+             d["demoted_blocks"] = st.demoted_blocks;
+             d["demoted_bytes"] = st.demoted_bytes;
+             d["batched_moves"] = st.batched_moves;
+             d["batched_move_blocks"] = st.batched_move_blocks;
              return d;
            })
       .def("has_block", &BlockStore::has_block, G())

@@ -569,51 +569,12 @@ int BlockStore::move_block(int64_t session, int64_t block_id, int dst_tier, cons
   b->writer = true;  // hold the block while copying
   BlockMeta src_snap = *b;
   lk.unlock();
-  // copy: src -> staging/dst using the same planners (block->external, external->block)
   hipStream_t st = internal_stream_;
   std::vector<CopySeg> dev_segs;
-  StorageDir& sd = *dirs_[src_snap.dir];
-  StorageDir& dd = *dirs_[d];
-  const bool src_dev = sd.spec.kind == DirKind::kDevice, dst_dev = dd.spec.kind == DirKind::kDevice;
-  std::vector<uint8_t> bounce;
   try {
-    if (sd.spec.kind != DirKind::kFile && dd.spec.kind != DirKind::kFile &&
-        (sd.spec.kind == DirKind::kHost || dd.spec.kind == DirKind::kHost || src_dev)) {
-      // arena -> arena: walk destination pages, reading source range into each
-      uint64_t off = 0;
-      size_t i = 0;
-      while (off < len) {
-        const int64_t p0 = nb.pages[i];
-        size_t j = i + 1;
-        while (j < nb.pages.size() && nb.pages[j] == nb.pages[j - 1] + 1) ++j;
-        const uint64_t run = std::min<uint64_t>((j - i) * dd.spec.page_size, len - off);
-        const uint64_t dst_addr = dd.spec.base + (uint64_t)p0 * dd.spec.page_size;
-        plan_block_range(src_snap, off, run, dst_addr, dst_dev ? (int)MemKind::kDevice : (int)MemKind::kHost,
-                         false, dev_segs, st);
-        off += run;
-        i = j;
-      }
-      if (!dev_segs.empty()) copy_segments(dev_segs, st);
-      if (has_device_) HIP_OK(hipStreamSynchronize(st));
-    } else {
-      // via host bounce buffer (file tiers)
-      bounce.resize(len);
-      plan_block_range(src_snap, 0, len, (uint64_t)bounce.data(), (int)MemKind::kHost, false, dev_segs, st);
-      if (has_device_) HIP_OK(hipStreamSynchronize(st));
-      if (dd.spec.kind == DirKind::kFile) {
-        std::string fin;
-        file_path(dd, block_id, fin);
-        int fd = ::open(fin.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
-        if (fd < 0) throw StoreError(kErrIo, "cannot create " + fin);
-        ssize_t w = ::pwrite(fd, bounce.data(), len, 0);
-        ::close(fd);
-        if (w != (ssize_t)len) throw StoreError(kErrIo, "short write to " + fin);
-      } else {
-        plan_block_range(nb, 0, len, (uint64_t)bounce.data(), (int)MemKind::kHost, true, dev_segs, st);
-        if (!dev_segs.empty()) copy_segments(dev_segs, st);
-        if (has_device_) HIP_OK(hipStreamSynchronize(st));
-      }
-    }
+    copy_block_storage(src_snap, nb, dev_segs, st);
+    if (!dev_segs.empty()) copy_segments(dev_segs, st);
+    if (has_device_) HIP_OK(hipStreamSynchronize(st));
   } catch (...) {
     lk.lock();
     release_storage(nb);
@@ -634,10 +595,168 @@ int BlockStore::move_block(int64_t session, int64_t block_id, int dst_tier, cons
   b->writer = false;
   note_state(*b, true);
   dirs_[d]->committed_bytes += len;
-  if (dd.spec.kind == DirKind::kFile) dd.file_used += 0;  // reserved already counted by grow_pages
   emit(2, *b);
   lock_cv_.notify_all();
   return d;
+}
+
+// Bytes of a committed block (src_snap) into freshly allocated storage nb.  Arena->arena pieces
+// are queued on `st` (HBM<->HBM pieces appended to dev_segs for one batched-copy launch, DMA
+// pieces issued async); file endpoints go through a host bounce buffer synchronously.
+void BlockStore::copy_block_storage(const BlockMeta& src_snap, const BlockMeta& nb, std::vector<CopySeg>& dev_segs,
+                                    hipStream_t st) {
+  const StorageDir& sd = *dirs_[src_snap.dir];
+  const StorageDir& dd = *dirs_[nb.dir];
+  const uint64_t len = src_snap.length;
+  const bool dst_dev = dd.spec.kind == DirKind::kDevice;
+  if (sd.spec.kind != DirKind::kFile && dd.spec.kind != DirKind::kFile) {
+    // arena -> arena: walk destination page runs, reading the source range into each
+    uint64_t off = 0;
+    size_t i = 0;
+    while (off < len) {
+      const int64_t p0 = nb.pages[i];
+      size_t j = i + 1;
+      while (j < nb.pages.size() && nb.pages[j] == nb.pages[j - 1] + 1) ++j;
+      const uint64_t run = std::min<uint64_t>((j - i) * dd.spec.page_size, len - off);
+      const uint64_t dst_addr = dd.spec.base + (uint64_t)p0 * dd.spec.page_size;
+      plan_block_range(src_snap, off, run, dst_addr, dst_dev ? (int)MemKind::kDevice : (int)MemKind::kHost, false,
+                       dev_segs, st);
+      off += run;
+      i = j;
+    }
+    return;
+  }
+  // via a host bounce buffer (file tiers)
+  std::vector<uint8_t> bounce(len);
+  std::vector<CopySeg> none;
+  plan_block_range(src_snap, 0, len, (uint64_t)bounce.data(), (int)MemKind::kHost, false, none, st);
+  if (has_device_) HIP_OK(hipStreamSynchronize(st));
+  if (dd.spec.kind == DirKind::kFile) {
+    std::string fin;
+    file_path(dd, nb.id, fin);
+    int fd = ::open(fin.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+    if (fd < 0) throw StoreError(kErrIo, "cannot create " + fin);
+    ssize_t w = ::pwrite(fd, bounce.data(), len, 0);
+    ::close(fd);
+    if (w != (ssize_t)len) throw StoreError(kErrIo, "short write to " + fin);
+  } else {
+    plan_block_range(nb, 0, len, (uint64_t)bounce.data(), (int)MemKind::kHost, true, none, st);
+    if (has_device_) HIP_OK(hipStreamSynchronize(st));
+  }
+}
+
+int BlockStore::lower_tier(int tier) const {
+  int best = -1;
+  for (auto& d : dirs_)
+    if (d->spec.tier > tier && d->healthy && (best < 0 || d->spec.tier < best)) best = d->spec.tier;
+  return best;
+}
+
+std::vector<int64_t> BlockStore::move_blocks(int64_t session, const std::vector<int64_t>& ids, int dst_tier,
+                                             const std::string& medium, bool evict) {
+  set_device();
+  std::unique_lock<std::mutex> lk(mu_);
+  return move_blocks_locked(lk, session, ids, dst_tier, medium, evict);
+}
+
+std::vector<int64_t> BlockStore::move_blocks_locked(std::unique_lock<std::mutex>& lk, int64_t session,
+                                                    const std::vector<int64_t>& ids, int dst_tier,
+                                                    const std::string& medium, bool evict) {
+  std::vector<int64_t> cand;
+  uint64_t need = 0;
+  for (int64_t id : ids) {
+    BlockMeta* b = find(id);
+    if (!b || b->temp || b->writer || b->readers > 0 || b->evicting) continue;
+    if (dir_matches(*dirs_[b->dir], dst_tier, medium)) continue;
+    cand.push_back(id);
+    need += std::max<uint64_t>(b->length, 1);
+  }
+  if (cand.empty()) return {};
+  // movers are held: never victims of the eviction below, not lockable meanwhile
+  for (int64_t id : cand) {
+    find(id)->evicting = true;
+    evicting_ids_.insert(id);
+  }
+  auto release_hold = [&] {
+    for (int64_t id : cand) {
+      evicting_ids_.erase(id);
+      BlockMeta* b = find(id);
+      if (b) b->evicting = false;
+    }
+  };
+  if (evict) {
+    try {
+      free_space_locked(lk, session, need, dst_tier, -1, medium);
+    } catch (const StoreError&) {
+      // best effort: move what fits
+    }
+  }
+  struct Job {
+    BlockMeta snap;
+    BlockMeta nb;
+  };
+  std::vector<Job> jobs;
+  for (int64_t id : cand) {
+    BlockMeta* b = find(id);
+    if (!b || b->readers > 0 || b->writer) continue;
+    const uint64_t len = b->length;
+    const int d = allocate_dir(dst_tier, medium, std::max<uint64_t>(len, 1));
+    if (d < 0) break;
+    Job j;
+    j.nb.id = id;
+    j.nb.dir = d;
+    j.nb.temp = false;
+    j.nb.length = len;
+    if (!grow_pages(*dirs_[d], j.nb, std::max<uint64_t>(len, 1))) {
+      release_storage(j.nb);
+      break;
+    }
+    b->writer = true;   // hold the block while copying
+    j.snap = *b;
+    jobs.push_back(std::move(j));
+  }
+  release_hold();
+  if (jobs.empty()) {
+    lock_cv_.notify_all();
+    return {};
+  }
+  lk.unlock();
+  hipStream_t st = internal_stream_;
+  std::vector<CopySeg> dev_segs;
+  std::exception_ptr err;
+  try {
+    for (auto& j : jobs) copy_block_storage(j.snap, j.nb, dev_segs, st);
+    if (!dev_segs.empty()) copy_segments(dev_segs, st);
+    if (has_device_) HIP_OK(hipStreamSynchronize(st));   // one sync for the whole batch
+  } catch (...) {
+    err = std::current_exception();
+  }
+  lk.lock();
+  std::vector<int64_t> moved;
+  for (auto& j : jobs) {
+    BlockMeta* b = find(j.nb.id);
+    if (err || !b) {
+      release_storage(j.nb);
+      if (b) b->writer = false;
+      continue;
+    }
+    BlockMeta old = *b;
+    old.temp = false;
+    release_storage(old);
+    b->dir = j.nb.dir;
+    b->pages = j.nb.pages;
+    b->reserved = j.nb.reserved;
+    b->writer = false;
+    note_state(*b, true);
+    dirs_[j.nb.dir]->committed_bytes += b->length;
+    emit(2, *b);
+    moved.push_back(b->id);
+  }
+  lock_cv_.notify_all();
+  ++stats_.batched_moves;
+  stats_.batched_move_blocks += moved.size();
+  if (err) std::rethrow_exception(err);
+  return moved;
 }
 
 // -------------------------------------------------------------------------------------------
@@ -1126,7 +1245,6 @@ std::vector<uint32_t> BlockStore::select_victims_cpu(const std::vector<uint32_t>
 
 void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
                                    int tier, int dir, const std::string& medium) {
-  (void)session;
   for (int attempt = 0; attempt < 4; ++attempt) {
     // target dir: the one that can reach `bytes` with the most (available + evictable)
     int target = -1;
@@ -1157,14 +1275,30 @@ void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t ses
     }
     // the store may have changed while it was unlocked: a victim must still be the same block
     // (created before the selection), in the target dir, and evictable now
+    std::vector<int64_t> vids;
     for (uint32_t s : victims) {
       BlockMeta* b = find(slot_block_[s]);
       if (b && b->seq <= seq && b->dir == target && evictable(*b)) {
-        remove_locked(*b, true);
+        vids.push_back(b->id);
         ++stats_.victims;
       } else {
         ++stats_.revalidated_away;
       }
+    }
+    const int lower = demote_on_evict_ ? lower_tier(dirs_[target]->spec.tier) : -1;
+    if (lower >= 0 && !vids.empty()) {
+      // demote into the next tier (making room there first) in one batched move
+      std::vector<int64_t> moved = move_blocks_locked(lk, session, vids, lower, "", true);
+      for (int64_t id : moved) {
+        const BlockMeta* b = find(id);
+        ++stats_.demoted_blocks;
+        if (b) stats_.demoted_bytes += b->length;
+      }
+    }
+    // what was not demoted is dropped
+    for (int64_t id : vids) {
+      BlockMeta* b = find(id);
+      if (b && b->dir == target && evictable(*b)) remove_locked(*b, true);
     }
     if (dirs_[target]->available() >= bytes) return;
     if (victims.empty()) break;

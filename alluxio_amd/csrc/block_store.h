@@ -157,6 +157,14 @@ class BlockStore {
   // move a committed block to another tier/medium; returns new dir index
   int move_block(int64_t session, int64_t block_id, int dst_tier, const std::string& medium,
                  bool evict);
+  // Batched move (tier management / demotion): every movable block gets its destination pages,
+  // all copies are queued together (one batched-copy launch for HBM<->HBM pieces, async DMA for
+  // HBM<->DRAM) and synchronized once; returns the ids that moved.
+  std::vector<int64_t> move_blocks(int64_t session, const std::vector<int64_t>& block_ids, int dst_tier,
+                                   const std::string& medium, bool evict);
+  // Eviction from a tier that has a lower tier demotes victims into it (batched move, making
+  // room there recursively) instead of dropping them.
+  void set_demote_on_evict(bool v) { demote_on_evict_ = v; }
 
   // ---- locks / sessions -------------------------------------------------------------------
   int64_t lock_block(int64_t session, int64_t block_id, bool write, int64_t timeout_ms);
@@ -199,6 +207,7 @@ class BlockStore {
   struct EvictStats {
     uint64_t selections = 0, device_selections = 0, candidates = 0, victims = 0, revalidated_away = 0;
     uint64_t device_allocs = 0, device_alloc_pages = 0, annotation_flushes = 0, annotation_updates = 0;
+    uint64_t demoted_blocks = 0, demoted_bytes = 0, batched_moves = 0, batched_move_blocks = 0;
   };
   EvictStats evict_stats();
 
@@ -235,6 +244,12 @@ class BlockStore {
   std::vector<uint32_t> select_victims_cpu(const std::vector<uint32_t>& cand_slots, uint64_t need);
   std::vector<uint32_t> select_victims_device(std::unique_lock<std::mutex>& lk, int dir, uint64_t need);
   void remove_locked(BlockMeta& b, bool emit_event);
+  std::vector<int64_t> move_blocks_locked(std::unique_lock<std::mutex>& lk, int64_t session,
+                                          const std::vector<int64_t>& ids, int dst_tier, const std::string& medium,
+                                          bool evict);
+  void copy_block_storage(const BlockMeta& src_snap, const BlockMeta& nb, std::vector<CopySeg>& dev_segs,
+                          hipStream_t st);
+  int lower_tier(int tier) const;
   // device annotator bookkeeping (all under mu_)
   uint64_t footprint(const BlockMeta& b) const;
   void note_state(const BlockMeta& b, bool live);
@@ -295,6 +310,7 @@ class BlockStore {
   // K7 measured slower than the host bitmap scan end to end (profiles/r2_evict_bench.jsonl):
   // off unless alluxio.worker.hbm.device.alloc.enabled
   bool use_device_alloc_ = false;
+  bool demote_on_evict_ = false;
   uint32_t device_alloc_min_pages_ = 64;
   hipStream_t internal_stream_ = nullptr;
   static constexpr int kRing = 8;

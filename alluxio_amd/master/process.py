@@ -89,8 +89,12 @@ class AlluxioMasterProcess:
                                                               ephemeral=self.port == 0)
         self.block_master = BlockMaster(self.conf, self.journal,
                                         worker_timeout_ms=self.conf.get_ms("alluxio.master.worker.timeout"))
+        # alluxio.master.mount.table.root.option.<key> = root mount properties (PropertyKey
+        # MASTER_MOUNT_TABLE_ROOT_OPTION_PROPERTY)
+        pfx = "alluxio.master.mount.table.root.option."
+        root_opts = {k[len(pfx):]: v for k, v in self.conf.to_map().items() if k.startswith(pfx)}
         self.fs_master = FileSystemMaster(self.conf, self.block_master, self.journal, metrics=self.metrics,
-                                          root_ufs=root_ufs)
+                                          root_ufs=root_ufs, root_ufs_properties=root_opts)
         self.meta_master = MetaMaster(self.conf, self.journal)
         self.meta_master.block_master = self.block_master
         self.metrics_master = MetricsMaster()

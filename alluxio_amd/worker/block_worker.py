@@ -74,6 +74,7 @@ class BlockWorker:
             thread_name_prefix="async-cache")
         self._staging = None
         self._staging_lock = threading.Lock()
+        self._ingest = None   # K3 pipelines (worker/ingest.py), created on first UFS caching
         self.pinned_files: set[int] = set()
         self.persisted_files: list[int] = []
         self._block_master = None
@@ -126,6 +127,16 @@ class BlockWorker:
             ps = self.conf.get_bytes("alluxio.worker.hbm.page.size")
             m.gauge("HbmPagesTotal", lambda: sum(self.native.dir_capacity(i) for i in hbm) // ps)
             m.gauge("HbmPagesFree", lambda: sum(self.native.dir_available(i) for i in hbm) // ps)
+
+    def ingest_pool(self):
+        from .ingest import IngestPool
+        with self._staging_lock:
+            if self._ingest is None:
+                self._ingest = IngestPool(
+                    self, self.conf.get_bytes("alluxio.worker.ufs.ingest.chunk.size", "8MB"),
+                    self.conf.get_int("alluxio.worker.ufs.ingest.depth", "3"),
+                    self.conf.get_int("alluxio.worker.network.async.cache.manager.threads.max") + 4)
+            return self._ingest
 
     def staging(self) -> _Staging:
         with self._staging_lock:
@@ -341,45 +352,34 @@ class BlockWorker:
         self.metrics.counter("BytesReadUfsAll").inc(len(data))
         return data
 
-    def cache_block_from_ufs(self, block_id: int, opts, session_id: int | None = None) -> bool:
-        """UFS -> pinned staging -> block (H2D for the HBM tier) -> commit.  Idempotent."""
+    def cache_block_from_ufs(self, block_id: int, opts, session_id: int | None = None, on_chunk=None,
+                             offset: int = 0) -> bool:
+        """UFS -> pinned staging ring -> block (async H2D on a side stream for the HBM tier,
+        overlapped with the next UFS read: worker/ingest.py) -> commit.  Idempotent.
+        ``on_chunk`` sees every chunk as it is ingested (read-through streaming to a client)."""
         if self.native.has_block(block_id):
             return True
         session_id = session_id if session_id is not None else ids.CACHE_UFS_SESSION_ID
         from ..underfs.base import OpenOptions
         ufs = self._ufs_for(opts)
         length = opts.block_size
-        chunk = 8 << 20
         try:
-            self.create_block(session_id, block_id, 0, "", min(length, 64 << 20) or 1)
+            self.create_block(session_id, block_id, 0, "", length or 1)
         except Exception as e:  # noqa: BLE001
             if self.native.has_block(block_id) or self.native.has_temp_block(block_id):
                 return self.native.has_block(block_id)
             raise e
+        pool = self.ingest_pool()
+        pipe = pool.acquire()
         try:
-            st = self.staging()
-            with ufs.open(opts.ufs_path, OpenOptions(offset=opts.offset_in_file)) as f:
-                pos = 0
-                while pos < length:
-                    buf = st.acquire()
-                    try:
-                        n = min(chunk, st.size, length - pos)
-                        mv = buf.numpy()
-                        got = f.readinto(memoryview(mv)[:n]) if hasattr(f, "readinto") else None
-                        if got is None:
-                            data = f.read(n)
-                            got = len(data)
-                            mv[:got] = memoryview(data)
-                        if not got:
-                            break
-                        with native_errors():
-                            self.native.write(session_id, block_id, pos, buf.data_ptr(), got, HOST, 0, True)
-                        pos += got
-                    finally:
-                        st.release(buf)
+            t0 = time.perf_counter()
+            with ufs.open(opts.ufs_path, OpenOptions(offset=opts.offset_in_file + offset)) as f:
+                pos = pipe.run(session_id, block_id, f, length, on_chunk)
             if pos != length:
                 raise IOError(f"short UFS read for block {block_id}: {pos} of {length}")
             self.metrics.counter("BytesReadUfsAll").inc(length)
+            self.metrics.counter("UfsIngestBytes").inc(length)
+            self.metrics.timer("UfsIngestBlock").update(time.perf_counter() - t0)
             self.commit_block(session_id, block_id)
             return True
         except Exception:
@@ -388,6 +388,8 @@ class BlockWorker:
             except Exception:  # noqa: BLE001
                 pass
             raise
+        finally:
+            pool.release(pipe)
 
     def async_cache(self, block_id: int, opts=None, source=None, length: int | None = None) -> bool:
         """Deduplicated background caching; returns False if already queued/cached."""

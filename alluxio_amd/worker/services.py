@@ -70,10 +70,15 @@ class BlockWorkerService:
             if not self.w.has_block(bid):
                 if first.HasField("open_ufs_block_options") and first.open_ufs_block_options.ufs_path:
                     opts = first.open_ufs_block_options
-                    if opts.no_cache:
+                    if opts.no_cache or first.offset != 0 or self.w.native.has_temp_block(bid):
+                        # partial / uncached reads (or another reader is caching it): plain stream
                         yield from self._stream_ufs(opts, first.offset, first.length, chunk, acked, cond, done)
                         return
-                    self.w.cache_block_from_ufs(bid, opts, session)
+                    # read-through: stream each UFS chunk to the client as it is cached
+                    # (UnderFileSystemBlockReader.java:205-243)
+                    yield from self._stream_ufs_caching(bid, opts, first.length, chunk, acked, cond, done,
+                                                        session)
+                    return
                 else:
                     raise BlockDoesNotExistException(f"Block {bid} does not exist on this worker")
             lock_id = self.w.lock_block(session, bid)
@@ -107,6 +112,46 @@ class BlockWorkerService:
                 except Exception:  # noqa: BLE001
                     pass
             self.w.cleanup_session(session)
+
+    def _stream_ufs_caching(self, bid, opts, length, chunk, acked, cond, done, session):
+        """Cache the block from the UFS on a background thread (K3 pipeline) and stream every
+        ingested chunk to the client as it lands, respecting the flow-control window; bytes past
+        the requested length are cached but not sent."""
+        import queue
+        end = length if length > 0 else opts.block_size
+        q: queue.Queue = queue.Queue(maxsize=8)
+        err: list = []
+
+        def on_chunk(mv):
+            q.put(bytes(mv))            # copy out of the staging buffer before it is reused
+
+        def run():
+            try:
+                self.w.cache_block_from_ufs(bid, opts, session, on_chunk=on_chunk)
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+            finally:
+                q.put(None)
+        t = threading.Thread(target=run, daemon=True, name=f"ufs-read-through-{bid}")
+        t.start()
+        pos = 0
+        while True:
+            data = q.get()
+            if data is None:
+                break
+            if pos >= end:
+                continue               # keep draining: the rest of the block is still cached
+            with cond:
+                while pos - acked[0] >= self.window and not done.is_set():
+                    cond.wait(0.5)
+            n = min(len(data), end - pos)
+            for off in range(0, n, chunk):
+                yield marshal.read_response_frame(data[off:min(n, off + chunk)])
+            pos += n
+        t.join()
+        if err and pos < end:
+            raise err[0]
+        self.w.metrics.counter("BytesReadUfsThrough").inc(pos)
 
     def _stream_ufs(self, opts, offset, length, chunk, acked, cond, done):
         end = offset + (length if length > 0 else opts.block_size - offset)

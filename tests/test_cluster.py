@@ -70,6 +70,30 @@ def test_remote_grpc_read_path(cluster):
     fs.close()
 
 
+def test_grpc_cold_read_streams_while_caching(cluster):
+    """A cold block read over gRPC from offset 0 is cached while it streams (read-through,
+    UnderFileSystemBlockReader.java:205-243); a mid-block cold read streams without caching."""
+    from alluxio_amd.client import context as cctx
+    fs = cluster.client()
+    data = os.urandom(9 * MB + 5)
+    fs.write_file("/rt/f", data, write_type="THROUGH")
+    fs.write_file("/rt/g", data, write_type="THROUGH")
+    saved = dict(cctx._LOCAL_WORKERS)
+    cctx._LOCAL_WORKERS.clear()
+    before = sum(w.worker.metrics.counter("BytesReadUfsThrough").count for w in cluster.workers)
+    try:
+        assert fs.read_file("/rt/f", read_type="CACHE") == data
+        with fs.open_file("/rt/g", read_type="CACHE") as f:
+            f.seek(MB + 3)
+            assert f.read(1000) == data[MB + 3:MB + 1003]
+    finally:
+        cctx._LOCAL_WORKERS.update(saved)
+    assert fs.get_status("/rt/f").in_alluxio_percentage == 100
+    through = sum(w.worker.metrics.counter("BytesReadUfsThrough").count for w in cluster.workers)
+    assert through - before >= len(data)
+    fs.close()
+
+
 def test_device_read_into_tensor(cluster):
     import torch
     fs = cluster.client()

@@ -216,3 +216,44 @@ def test_read_session_lockstep_and_reopen(tmp_path):
     rs.close()
     assert all(s.block_info(b).readers == 0 for b in blocks)
     assert zlib.crc32(b"") == 0
+
+
+def test_move_blocks_batched(tmp_path):
+    s = _store(tmp_path, mem_mb=8, ssd_mb=16)
+    datas = {}
+    for b in range(4):
+        datas[300 + b] = np.frombuffer(os.urandom(MB + 1000 * b), dtype=np.uint8)
+        _put(s, 300 + b, datas[300 + b])
+    lk = s.lock_block(1, 303)          # locked blocks are skipped, not waited for
+    moved = s.move_blocks(1, [300, 301, 302, 303, 999], 1)
+    s.unlock(lk)
+    assert sorted(moved) == [300, 301, 302]
+    for b in moved:
+        assert s.block_info(b).tier_alias == "SSD"
+        assert np.array_equal(_get(s, b), datas[b])
+    assert s.block_info(303).tier_alias == "MEM"
+    st = s.evict_stats()
+    assert st["batched_moves"] == 1 and st["batched_move_blocks"] == 3
+    # and back up in one batch
+    assert sorted(s.move_blocks(1, moved, 0)) == moved
+    assert all(np.array_equal(_get(s, b), datas[b]) for b in moved)
+
+
+def test_eviction_demotes_to_lower_tier(tmp_path):
+    """Eviction from MEM moves the coldest blocks down to SSD (and evicts there when SSD is full)
+    instead of dropping them: the MI355X HBM->DRAM demotion path, on host arenas."""
+    s = _store(tmp_path, mem_mb=4, ssd_mb=3)
+    s.set_demote_on_evict(True)
+    datas = {}
+    for b in range(4):
+        datas[400 + b] = np.full(MB, b + 1, dtype=np.uint8)
+        _put(s, 400 + b, datas[400 + b])
+    s.access_block(1, 400)             # 401 is now the coldest
+    _put(s, 404, np.full(MB, 9, dtype=np.uint8))
+    assert s.block_info(401).tier_alias == "SSD" and np.array_equal(_get(s, 401), datas[401])
+    assert s.evict_stats()["demoted_blocks"] == 1
+    for b in (405, 406, 407):          # SSD fills up (3 MB): further demotions evict there
+        _put(s, b, np.full(MB, 7, dtype=np.uint8))
+    ids_ = set(s.block_ids(-1))
+    assert len([b for b in ids_ if s.block_info(b).tier_alias == "SSD"]) <= 3
+    assert {404, 405, 406, 407} <= ids_ and 401 not in ids_   # the coldest SSD block was dropped

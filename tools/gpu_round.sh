@@ -66,6 +66,10 @@ for s in $STEPS; do
       run evict_bench_lrfu 300 python tools/evict_bench.py --counts 150000 --policy 1 --out "$OUT/evict_bench.jsonl"
       run rocprof_evict 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_evict" -o ev --output-format csv -- python3 tools/evict_bench.py --counts 150000 --iters 10
       ;;
+    ingest)
+      run ufs_ingest_local 600 python tools/ufs_ingest_bench.py --ufs local --hbm 2g --dram 6g --factor 2 --file-size 256m --out "$OUT/ufs_ingest.jsonl"
+      run ufs_ingest_s3 600 python tools/ufs_ingest_bench.py --ufs s3 --hbm 256m --dram 1g --factor 2 --file-size 64m --out "$OUT/ufs_ingest.jsonl"
+      ;;
     kbench) run kernel_bench 300 python tools/kernel_bench.py --out "$OUT/kernel_bench.json" ;;
     pcsweep) run page_cache_sweep 400 python tools/page_cache_bench.py --variants both --passes 2 --page-sizes 4k,8k,16k,32k,64k,256k --out "$OUT/page_cache_sweep.jsonl" ;;
     pcwave) run page_cache_wave 400 python tools/page_cache_bench.py --variants both --passes 2 --wave-variants 0,1,2,3 --page-sizes 4k,16k --iters 30 --out "$OUT/page_cache_wave.jsonl" ;;
