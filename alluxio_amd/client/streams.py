@@ -221,6 +221,13 @@ class IpcBlockReader(BlockReader):
         except Exception as e:
             self.close()
             raise UnavailableException(f"worker {address} did not share block {block_id}: {e}") from e
+        if ctx.conf.get_bool("alluxio.user.short.circuit.verify.crc", "false") and self.h.crc32c:
+            from ..parallel.ipc import verify_handle_crc
+            try:
+                verify_handle_crc(self.h, self.device)
+            except Exception:
+                self.close()
+                raise
         self.length = self.h.length
 
     def read_into(self, offset, length, ptr, kind, stream=0):

@@ -151,6 +151,13 @@ _k("WORKER_HBM_ARENA_FRACTION", "alluxio.worker.hbm.arena.fraction", "0.0", Scop
    "If >0, size the HBM tier as this fraction of free device memory (overrides the quota).")
 _k("WORKER_DATA_CRC_ENABLED", "alluxio.worker.data.crc.enabled", "false", Scope.WORKER,
    "Compute a CRC32C per page when a block is committed (HIP kernel).")
+_k("WORKER_DATA_CRC_DEVICE_ENABLED", "alluxio.worker.data.crc.device.enabled", "true", Scope.WORKER,
+   "Compute the per-page CRC32C of every block committed to the HBM tier (device kernel); peers "
+   "verify pulled blocks against it (alluxio.worker.peer.verify.crc).")
+_k("WORKER_PEER_VERIFY_CRC", "alluxio.worker.peer.verify.crc", "true", Scope.WORKER,
+   "Verify a block pulled from a peer worker against the source's CRC32Cs before committing it.")
+_k("USER_SHORT_CIRCUIT_VERIFY_CRC", "alluxio.user.short.circuit.verify.crc", "false", Scope.CLIENT,
+   "Verify a short-circuit (HIP IPC / shared DRAM) block against its worker's CRC32Cs at open.")
 _k("WORKER_DATA_COMPRESSION", "alluxio.worker.data.compression", "NONE", Scope.WORKER,
    "Block codec for the host tiers: NONE | LZ4.")
 _k("WORKER_RCCL_ENABLED", "alluxio.worker.rccl.enabled", "true", Scope.WORKER,

@@ -149,3 +149,32 @@ def gather_block(handle_msg, offset: int, length: int, dst_ptr: int, device: int
     segs = page_segments(base, list(handle_msg.pages), handle_msg.page_size, offset, length, dst_ptr)
     lib().batched_copy(segs, stream, True)
     return length
+
+
+def verify_handle_crc(h, device: int) -> None:
+    """Check a mapped block against the per-page CRC32Cs its worker computed at commit (the
+    ``crc32c`` of a ``DeviceBlockHandle``): the CRC kernel runs on ``device`` over the mapped pages
+    (peer HBM read over xGMI), a shared DRAM arena is checked on the host.  Raises
+    ``DataLossException`` on a mismatch."""
+    from ..ops.native import has_gpu, lib
+    from ..utils.exceptions import DataLossException
+    crcs = list(h.crc32c)
+    if not crcs:
+        return
+    base = map_handle(h, device)
+    ps, n = h.page_size, h.length
+    C = lib()
+    got = []
+    for i, p in enumerate(h.pages):
+        ln = min(ps, n - i * ps)
+        if ln <= 0:
+            break
+        addr = base + int(p) * ps
+        if h.arena_kind == "dram" or not has_gpu():
+            got.append(C.crc32c_ptr(addr, ln, 0))
+        else:
+            import torch
+            with torch.cuda.device(device):
+                got.extend(C.crc32c_device(addr, ln, 0, 0))
+    if got != crcs[:len(got)] or len(got) != len(crcs):
+        raise DataLossException(f"block {h.block_id}: CRC32C mismatch on the shared pages")

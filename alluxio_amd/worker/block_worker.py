@@ -83,7 +83,10 @@ class BlockWorker:
         self._peer_channels: dict = {}
         self._peer_lock = threading.Lock()
         self.crc_enabled = conf.get_bool("alluxio.worker.data.crc.enabled")
-        self.crc: dict[int, list[int]] = {}
+        # HBM blocks get their per-page CRC32C at commit by default (one kernel pass at ~3.6 TB/s):
+        # peers verify pulled blocks against it, short-circuit readers may too
+        self.crc_device = conf.get_bool("alluxio.worker.data.crc.device.enabled", "true")
+        self.crc: dict[int, tuple[int, list[int]]] = {}   # block id -> (piece bytes, CRC32Cs)
         self._install_gauges()
 
     # ---- wiring -------------------------------------------------------------------------------
@@ -202,9 +205,12 @@ class BlockWorker:
         with native_errors():
             self.native.commit_block(session_id, block_id, pin)
             info = self.native.block_info(block_id)
-        if self.crc_enabled:
+        if self.crc_enabled or (self.crc_device and info.medium == "HBM"):
             with native_errors():
-                self.crc[block_id] = self.native.checksum(block_id, 0)
+                # (piece bytes, CRC per piece): the piece is the page size of the dir it was
+                # computed in; a block moved to a dir with another page size keeps its CRCs
+                self.crc[block_id] = (self.native.block_pages(block_id)[2], self.native.checksum(block_id, 0))
+            self.metrics.counter("Crc32cBytes").inc(info.length)
         bm = self._bm()
         if bm is not None and self.worker_id != ids.INVALID_WORKER_ID:
             used = self.store.used_by_tier().get(info.tier_alias, 0)
@@ -433,6 +439,7 @@ class BlockWorker:
         for ev in self.native.drain_events():
             if ev.kind == 1:
                 removed.append(ev.block_id)
+                self.crc.pop(ev.block_id, None)   # evicted: its CRCs go with it
                 for k in list(added):
                     if ev.block_id in added[k]:
                         added[k].remove(ev.block_id)

@@ -327,8 +327,9 @@ class BlockWorkerService:
                 if share is None:
                     raise UnavailableException("DRAM arena is not shareable")
                 h.host_fd = share[1]
-            if req.block_id in self.w.crc:
-                h.crc32c.extend(self.w.crc[req.block_id])
+            piece, crcs = self.w.crc.get(req.block_id, (0, None))
+            if crcs and piece == ps:     # CRCs are per page of the handle's page size
+                h.crc32c.extend(crcs)
             with self._lock:
                 self._device_locks[lock_id] = (session, req.block_id)
             self.w.access_block(session, req.block_id)

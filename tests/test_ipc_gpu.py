@@ -194,3 +194,72 @@ def test_remote_ring_reader_other_process(gpu, tmp_path):
             p.wait(timeout=60)
         except subprocess.TimeoutExpired:
             p.kill()
+
+
+SERVER_CORRUPT = r"""
+import os, sys, json
+sys.path.insert(0, %(root)r)
+import torch
+import numpy as np
+from alluxio_amd.minicluster import LocalAlluxioCluster
+from alluxio_amd.ops.native import lib
+conf = {"alluxio.worker.tieredstore.level0.dirs.path": "hbm:0", "alluxio.worker.tieredstore.level0.dirs.quota": "256MB",
+        "alluxio.worker.hbm.page.size": "1MB", "alluxio.user.block.size.bytes.default": "8MB"}
+with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=%(work)r) as c:
+    fs = c.client()
+    data = np.random.default_rng(3).integers(0, 256, 5 * (1 << 20) + 17, dtype=np.uint8)
+    fs.write_file("/crc/f", data, write_type="MUST_CACHE")
+    bid = fs.get_status("/crc/f").info.blockIds[0]
+    w = c.workers[0].worker
+    print(json.dumps({"master": c.master.address, "worker": "127.0.0.1:%%d" %% w.address.rpcPort,
+                      "block": bid, "crcs": len(w.crc.get(bid, (0, []))[1])}), flush=True)
+    sys.stdin.readline()
+    pages, d, ps, base = w.native.block_pages(bid)
+    lib().fill_pattern(base + pages[1] * ps + 4096, 4096, 99, 0, 0)   # flip bytes in page 1
+    torch.cuda.synchronize()
+    print("corrupted", flush=True)
+    sys.stdin.readline()
+    fs.close()
+"""
+
+
+@pytest.mark.gpu
+def test_ipc_open_verifies_crc(gpu, tmp_path):
+    """HBM blocks carry per-page CRC32Cs from commit; a short-circuit reader verifying them at
+    open accepts the intact block and rejects one whose page was overwritten."""
+    from alluxio_amd.parallel.ipc import verify_handle_crc
+    from alluxio_amd.proto import pb
+    from alluxio_amd.rpc import Channel
+    from alluxio_amd.utils.exceptions import DataLossException
+    script = tmp_path / "server.py"
+    script.write_text(SERVER_CORRUPT % {"root": ROOT, "work": str(tmp_path / "work")})
+    p = subprocess.Popen([sys.executable, str(script)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        line = p.stdout.readline()
+        assert line, p.stderr.read()[-3000:]
+        info = json.loads(line)
+        assert info["crcs"] == 6          # one block of 5 MB + 17 B: a CRC per 1 MB page
+        stub = Channel(info["worker"], force_grpc=True).stub("alluxio.grpc.block.BlockWorker")
+
+        def open_verify():
+            h = stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=info["block"], session_id=4242))
+            try:
+                assert len(h.crc32c) == 6
+                verify_handle_crc(h, 0)
+            finally:
+                stub.UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(block_id=info["block"], lock_id=h.lock_id,
+                                                                         session_id=4242))
+        open_verify()
+        p.stdin.write("go\n")
+        p.stdin.flush()
+        assert p.stdout.readline().strip() == "corrupted"
+        with pytest.raises(DataLossException):
+            open_verify()
+    finally:
+        try:
+            p.stdin.write("quit\n")
+            p.stdin.flush()
+        except Exception:  # noqa: BLE001
+            pass
+        p.wait(timeout=60)
