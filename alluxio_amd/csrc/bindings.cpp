@@ -134,6 +134,9 @@ py::tuple evict_select_device(const std::vector<float>& crf, const std::vector<u
     st.step = step;
     st.log2_inv_att = (float)std::log2(1.0 / (double)att);
     st.policy = policy;
+    st.dir_mask = 0;
+    st.unit = 0;
+    st.invert = 0;
     HIP_CHECK(launch_evict_select_grid(st, 0, nullptr, need, (uint32_t*)dk.p, (EvictCtl*)dctl.p, (uint32_t*)dout.p,
                                        nullptr));
     EvictCtl ctl;
@@ -294,7 +297,11 @@ PYBIND11_MODULE(_C, m) {
       .def("set_use_device_alloc", &BlockStore::set_use_device_alloc, py::arg("enabled"), py::arg("min_pages") = 64)
       .def("set_demote_on_evict", &BlockStore::set_demote_on_evict)
       .def("move_blocks", &BlockStore::move_blocks, G(), py::arg("session"), py::arg("block_ids"), py::arg("tier"),
-           py::arg("medium") = "", py::arg("evict") = true)
+           py::arg("medium") = "", py::arg("evict") = true, py::arg("use_reserved") = false)
+      .def("tier_order", &BlockStore::tier_order, G(), py::arg("tier"), py::arg("k"), py::arg("hottest") = false,
+           py::arg("device") = true)
+      .def("annotator_keys", &BlockStore::annotator_keys, G())
+      .def("dir_mgmt_available", &BlockStore::dir_mgmt_available, G())
       .def("create_blocks", &BlockStore::create_blocks, G(), py::arg("session"), py::arg("block_ids"),
            py::arg("tier") = -1, py::arg("medium") = "", py::arg("sizes") = std::vector<uint64_t>{},
            py::arg("evict") = true)

@@ -27,16 +27,22 @@ static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b
 uint64_t StorageDir::available() const {
   if (!healthy) return 0;
   if (spec.kind == DirKind::kFile) {
-    const uint64_t cap = capacity();
+    const uint64_t cap = spec.capacity > spec.reserved ? spec.capacity - spec.reserved : 0;
     return file_used >= cap ? 0 : cap - file_used;
   }
-  const uint64_t free_b = (uint64_t)free_pages * spec.page_size;
-  return free_b;
+  return free_pages > reserved_pages ? (uint64_t)(free_pages - reserved_pages) * spec.page_size : 0;
 }
 
+uint64_t StorageDir::mgmt_available() const {
+  if (!healthy) return 0;
+  if (spec.kind == DirKind::kFile) return file_used >= spec.capacity ? 0 : spec.capacity - file_used;
+  return (uint64_t)free_pages * spec.page_size;
+}
+
+// User-visible capacity: the reserved space is management headroom, not capacity.
 uint64_t StorageDir::capacity() const {
   if (spec.kind == DirKind::kFile) return spec.capacity > spec.reserved ? spec.capacity - spec.reserved : 0;
-  return (uint64_t)num_pages * spec.page_size;
+  return (uint64_t)(num_pages - reserved_pages) * spec.page_size;
 }
 
 // -------------------------------------------------------------------------------------------
@@ -54,8 +60,10 @@ BlockStore::BlockStore(const std::vector<DirSpec>& dirs, int annotator, int allo
     d->index = (int)i;
     if (d->spec.kind != DirKind::kFile) {
       if (d->spec.page_size == 0) throw StoreError(kErrInvalidArgument, "page size must be > 0");
-      const uint64_t usable = d->spec.capacity > d->spec.reserved ? d->spec.capacity - d->spec.reserved : 0;
-      d->num_pages = (int64_t)(usable / d->spec.page_size);
+      if (d->spec.base == 0 && d->spec.capacity >= d->spec.page_size)
+        throw StoreError(kErrInvalidArgument, "arena dir " + std::to_string(i) + " has no base address");
+      d->num_pages = (int64_t)(d->spec.capacity / d->spec.page_size);
+      d->reserved_pages = std::min<int64_t>(d->num_pages, (int64_t)ceil_div(d->spec.reserved, d->spec.page_size));
       d->free_bits.assign(ceil_div((uint64_t)d->num_pages, 64), 0);
       for (int64_t p = 0; p < d->num_pages; ++p) d->free_bits[p >> 6] |= 1ull << (p & 63);
       d->free_pages = d->num_pages;
@@ -243,10 +251,10 @@ static int64_t find_run(const std::vector<uint64_t>& bits, int64_t num_pages, in
   return -1;
 }
 
-bool BlockStore::grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved) {
+bool BlockStore::grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved, bool use_reserved) {
   if (d.spec.kind == DirKind::kFile) {
     const uint64_t add = new_reserved > b.reserved ? new_reserved - b.reserved : 0;
-    if (add > d.available()) return false;
+    if (add > (use_reserved ? d.mgmt_available() : d.available())) return false;
     d.file_used += add;
     b.reserved = std::max(b.reserved, new_reserved);
     return true;
@@ -257,7 +265,7 @@ bool BlockStore::grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved) 
     b.reserved = std::max(b.reserved, new_reserved);
     return true;
   }
-  if (need > d.free_pages) return false;
+  if (need > d.free_pages - (use_reserved ? 0 : d.reserved_pages)) return false;
   // 1) extend the block's current run in place
   if (!b.pages.empty()) {
     int64_t p = b.pages.back() + 1;
@@ -318,7 +326,8 @@ void BlockStore::release_storage(BlockMeta& b) {
   b.reserved = 0;
 }
 
-int BlockStore::allocate_dir(int tier, const std::string& medium, uint64_t bytes) {
+int BlockStore::allocate_dir(int tier, const std::string& medium, uint64_t bytes, bool use_reserved) {
+  auto avail = [&](const StorageDir& d) { return use_reserved ? d.mgmt_available() : d.available(); };
   // tier < 0: top-down over tiers, first tier with a fitting dir wins (MaxFreeAllocator anyTier)
   int max_tier = (int)rr_index_.size() - 1;
   const int t0 = tier < 0 ? 0 : tier, t1 = tier < 0 ? max_tier : tier;
@@ -330,12 +339,12 @@ int BlockStore::allocate_dir(int tier, const std::string& medium, uint64_t bytes
     int pick = -1;
     if (alloc_policy_ == AllocPolicy::kGreedy) {
       for (int c : cands)
-        if (dirs_[c]->available() >= bytes) { pick = c; break; }
+        if (avail(*dirs_[c]) >= bytes) { pick = c; break; }
     } else if (alloc_policy_ == AllocPolicy::kRoundRobin) {
       const int n = (int)cands.size();
       for (int k = 0; k < n; ++k) {
         const int c = cands[(rr_index_[t] + k) % n];
-        if (dirs_[c]->available() >= bytes) {
+        if (avail(*dirs_[c]) >= bytes) {
           pick = c;
           rr_index_[t] = (rr_index_[t] + k + 1) % n;
           break;
@@ -344,7 +353,7 @@ int BlockStore::allocate_dir(int tier, const std::string& medium, uint64_t bytes
     } else {
       uint64_t best = 0;
       for (int c : cands) {
-        const uint64_t a = dirs_[c]->available();
+        const uint64_t a = avail(*dirs_[c]);
         if (a >= bytes && (pick < 0 || a > best)) { pick = c; best = a; }
       }
     }
@@ -653,15 +662,15 @@ int BlockStore::lower_tier(int tier) const {
 }
 
 std::vector<int64_t> BlockStore::move_blocks(int64_t session, const std::vector<int64_t>& ids, int dst_tier,
-                                             const std::string& medium, bool evict) {
+                                             const std::string& medium, bool evict, bool use_reserved) {
   set_device();
   std::unique_lock<std::mutex> lk(mu_);
-  return move_blocks_locked(lk, session, ids, dst_tier, medium, evict);
+  return move_blocks_locked(lk, session, ids, dst_tier, medium, evict, use_reserved);
 }
 
 std::vector<int64_t> BlockStore::move_blocks_locked(std::unique_lock<std::mutex>& lk, int64_t session,
                                                     const std::vector<int64_t>& ids, int dst_tier,
-                                                    const std::string& medium, bool evict) {
+                                                    const std::string& medium, bool evict, bool use_reserved) {
   std::vector<int64_t> cand;
   uint64_t need = 0;
   for (int64_t id : ids) {
@@ -700,14 +709,14 @@ std::vector<int64_t> BlockStore::move_blocks_locked(std::unique_lock<std::mutex>
     BlockMeta* b = find(id);
     if (!b || b->readers > 0 || b->writer) continue;
     const uint64_t len = b->length;
-    const int d = allocate_dir(dst_tier, medium, std::max<uint64_t>(len, 1));
+    const int d = allocate_dir(dst_tier, medium, std::max<uint64_t>(len, 1), use_reserved);
     if (d < 0) break;
     Job j;
     j.nb.id = id;
     j.nb.dir = d;
     j.nb.temp = false;
     j.nb.length = len;
-    if (!grow_pages(*dirs_[d], j.nb, std::max<uint64_t>(len, 1))) {
+    if (!grow_pages(*dirs_[d], j.nb, std::max<uint64_t>(len, 1), use_reserved)) {
       release_storage(j.nb);
       break;
     }
@@ -1061,7 +1070,24 @@ EvictState BlockStore::dev_state(uint64_t now) const {
   st.step = lrfu_step_;
   st.log2_inv_att = (float)std::log2(1.0 / (double)lrfu_att_);
   st.policy = annotator_ == Annotator::kLRFU ? 1 : 0;
+  st.dir_mask = 0;
+  st.unit = 0;
+  st.invert = 0;
   return st;
+}
+
+// The annotator key of a slot from the host mirror (identical formula to the device key).
+uint32_t BlockStore::host_key(uint32_t s, uint64_t now) const {
+  const uint64_t age = now > last_[s] ? now - last_[s] : 0;
+  uint32_t key;
+  if (annotator_ == Annotator::kLRU) {
+    key = 0xFFFFFFFEu - (uint32_t)std::min<uint64_t>(age, 0xFFFFFFFEull);
+  } else {
+    float crf = crf_[s] * std::pow(1.0f / lrfu_att_, (float)age * lrfu_step_);
+    if (!(crf >= 0.f)) crf = 0.f;
+    std::memcpy(&key, &crf, 4);
+  }
+  return key >= 0xFFFFFFFEu ? 0xFFFFFFFDu : key;
 }
 
 // Grow the slot-indexed device arrays to hold `n` slots (doubling).  Called under mu_; takes
@@ -1175,7 +1201,8 @@ void BlockStore::flush_annotations_locked() {
 
 // Device selection of victims in `dir` for `need` bytes.  Called with mu_ held; mu_ is released
 // for the device round trip (launches + one stream sync) and re-acquired before returning.
-std::vector<uint32_t> BlockStore::select_victims_device(std::unique_lock<std::mutex>& lk, int dir, uint64_t need) {
+std::vector<uint32_t> BlockStore::select_victims_device(std::unique_lock<std::mutex>& lk, int dir, uint64_t need,
+                                                       uint64_t dir_mask, bool unit, bool invert) {
   flush_annotations_locked();
   // dynamic exclusions: locked or moving blocks (few; evictable() re-checks at removal anyway)
   std::vector<uint32_t> excl;
@@ -1187,7 +1214,10 @@ std::vector<uint32_t> BlockStore::select_victims_device(std::unique_lock<std::mu
     const BlockMeta* b = find(id);
     if (b) excl.push_back(b->slot);
   }
-  const EvictState st = dev_state(clock_.load());
+  EvictState st = dev_state(clock_.load());
+  st.dir_mask = dir_mask;
+  st.unit = unit ? 1 : 0;
+  st.invert = invert ? 1 : 0;
   std::vector<uint32_t> picked;
   {
     std::unique_lock<std::mutex> g(ev_mu_);   // mu_ -> ev_mu_ order, then mu_ is dropped
@@ -1217,20 +1247,7 @@ std::vector<uint32_t> BlockStore::select_victims_cpu(const std::vector<uint32_t>
   const uint64_t now = clock_.load();
   // identical keys to the device select, full sort
   std::vector<std::pair<uint32_t, uint32_t>> keyed(n);
-  for (size_t i = 0; i < n; ++i) {
-    const uint32_t s = cand[i];
-    const uint64_t age = now > last_[s] ? now - last_[s] : 0;
-    uint32_t key;
-    if (annotator_ == Annotator::kLRU) {
-      key = 0xFFFFFFFEu - (uint32_t)std::min<uint64_t>(age, 0xFFFFFFFEull);
-    } else {
-      float crf = crf_[s] * std::pow(1.0f / lrfu_att_, (float)age * lrfu_step_);
-      if (!(crf >= 0.f)) crf = 0.f;
-      std::memcpy(&key, &crf, 4);
-      if (key >= 0xFFFFFFFEu) key = 0xFFFFFFFDu;
-    }
-    keyed[i] = {key, (uint32_t)i};
-  }
+  for (size_t i = 0; i < n; ++i) keyed[i] = {host_key(cand[i], now), (uint32_t)i};
   std::sort(keyed.begin(), keyed.end());
   uint64_t got = 0;
   for (auto& kv : keyed) {
@@ -1332,6 +1349,57 @@ std::vector<int64_t> BlockStore::eviction_order(int tier, uint64_t need_bytes) {
   out.reserve(v.size());
   for (uint32_t s : v) out.push_back(slot_block_[s]);
   return out;
+}
+
+std::vector<int64_t> BlockStore::tier_order(int tier, uint32_t k, bool hottest, bool device) {
+  set_device();
+  std::unique_lock<std::mutex> lk(mu_);
+  std::vector<uint32_t> slots;
+  uint64_t mask = 0;
+  for (auto& d : dirs_)
+    if (d->spec.tier == tier && d->index < 64) mask |= 1ull << d->index;
+  if (!mask || k == 0) return {};
+  if (device && device_evict_active()) {
+    // the k extremes by count on the device, O(n); only those k are ordered on the host
+    slots = select_victims_device(lk, 0, k, mask, /*unit=*/true, /*invert=*/hottest);
+    std::vector<uint32_t> ok;
+    for (uint32_t s : slots) {
+      const BlockMeta* b = find(slot_block_[s]);
+      if (b && evictable(*b) && ((mask >> b->dir) & 1)) ok.push_back(s);
+    }
+    slots.swap(ok);
+  } else {
+    for (auto& kv : blocks_)
+      if (((mask >> kv.second.dir) & 1) && evictable(kv.second)) slots.push_back(kv.second.slot);
+  }
+  const uint64_t now = clock_.load();
+  std::vector<std::pair<uint32_t, uint32_t>> keyed;
+  keyed.reserve(slots.size());
+  for (uint32_t s : slots) keyed.push_back({host_key(s, now), s});
+  if (hottest)
+    std::sort(keyed.begin(), keyed.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  else
+    std::sort(keyed.begin(), keyed.end());
+  std::vector<int64_t> out;
+  for (size_t i = 0; i < keyed.size() && out.size() < k; ++i) out.push_back(slot_block_[keyed[i].second]);
+  return out;
+}
+
+std::vector<uint32_t> BlockStore::annotator_keys(const std::vector<int64_t>& ids) {
+  std::unique_lock<std::mutex> lk(mu_);
+  const uint64_t now = clock_.load();
+  std::vector<uint32_t> out;
+  out.reserve(ids.size());
+  for (int64_t id : ids) {
+    const BlockMeta* b = find(id);
+    out.push_back(b ? host_key(b->slot, now) : 0xFFFFFFFFu);
+  }
+  return out;
+}
+
+uint64_t BlockStore::dir_mgmt_available(int d) {
+  std::unique_lock<std::mutex> lk(mu_);
+  return dirs_.at(d)->mgmt_available();
 }
 
 std::vector<int64_t> BlockStore::select_for_bench(int dir, uint64_t need, bool device) {

@@ -75,10 +75,12 @@ struct StorageDir {
   int64_t num_pages = 0;
   std::vector<uint64_t> free_bits;  // arena kinds: 1 = free
   int64_t free_pages = 0;
+  int64_t reserved_pages = 0;       // kept free for tier management (align/promote swaps)
   uint64_t file_used = 0;  // file dirs: bytes reserved
   uint64_t committed_bytes = 0;
   bool healthy = true;
-  uint64_t available() const;
+  uint64_t available() const;         // for user allocations (excludes the reserved space)
+  uint64_t mgmt_available() const;    // for tier-management moves (may use the reserved space)
   uint64_t capacity() const;
 };
 
@@ -161,7 +163,13 @@ class BlockStore {
   // all copies are queued together (one batched-copy launch for HBM<->HBM pieces, async DMA for
   // HBM<->DRAM) and synchronized once; returns the ids that moved.
   std::vector<int64_t> move_blocks(int64_t session, const std::vector<int64_t>& block_ids, int dst_tier,
-                                   const std::string& medium, bool evict);
+                                   const std::string& medium, bool evict, bool use_reserved = false);
+  // Up to k committed evictable blocks of a tier in annotator order, coldest first (or hottest
+  // first): the device grid select picks the k extremes (unit weights, O(n)), the host orders k.
+  std::vector<int64_t> tier_order(int tier, uint32_t k, bool hottest, bool device);
+  // Annotator keys (larger = hotter; 0xFFFFFFFF = unknown block) for a common order across tiers.
+  std::vector<uint32_t> annotator_keys(const std::vector<int64_t>& ids);
+  uint64_t dir_mgmt_available(int d);
   // Eviction from a tier that has a lower tier demotes victims into it (batched move, making
   // room there recursively) instead of dropping them.
   void set_demote_on_evict(bool v) { demote_on_evict_ = v; }
@@ -235,18 +243,20 @@ class BlockStore {
  private:
   BlockMeta& get_committed(int64_t id);
   BlockMeta* find(int64_t id);
-  int allocate_dir(int tier, const std::string& medium, uint64_t bytes);
+  int allocate_dir(int tier, const std::string& medium, uint64_t bytes, bool use_reserved = false);
   bool dir_matches(const StorageDir& d, int tier, const std::string& medium) const;
-  bool grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved);
+  bool grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved, bool use_reserved = false);
   void release_storage(BlockMeta& b);
   void free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
                          int tier, int dir, const std::string& medium);
   std::vector<uint32_t> select_victims_cpu(const std::vector<uint32_t>& cand_slots, uint64_t need);
-  std::vector<uint32_t> select_victims_device(std::unique_lock<std::mutex>& lk, int dir, uint64_t need);
+  std::vector<uint32_t> select_victims_device(std::unique_lock<std::mutex>& lk, int dir, uint64_t need,
+                                              uint64_t dir_mask = 0, bool unit = false, bool invert = false);
+  uint32_t host_key(uint32_t slot, uint64_t now) const;
   void remove_locked(BlockMeta& b, bool emit_event);
   std::vector<int64_t> move_blocks_locked(std::unique_lock<std::mutex>& lk, int64_t session,
                                           const std::vector<int64_t>& ids, int dst_tier, const std::string& medium,
-                                          bool evict);
+                                          bool evict, bool use_reserved = false);
   void copy_block_storage(const BlockMeta& src_snap, const BlockMeta& nb, std::vector<CopySeg>& dev_segs,
                           hipStream_t st);
   int lower_tier(int tier) const;

@@ -44,17 +44,27 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
-__device__ __forceinline__ uint32_t evict_key(const EvictState& st, uint32_t i, uint32_t target_dir,
+__device__ __forceinline__ uint32_t evict_key(const EvictState& st, uint32_t i, uint64_t dir_mask,
                                               const uint32_t* __restrict__ excl) {
-  if (st.dir[i] != (int32_t)target_dir) return 0xFFFFFFFFu;
+  const int32_t d = st.dir[i];
+  if (d < 0 || d >= 64 || !((dir_mask >> d) & 1ull)) return 0xFFFFFFFFu;
   if (excl && ((excl[i >> 5] >> (i & 31)) & 1u)) return 0xFFFFFFFFu;
   const uint64_t last = st.last[i];
   const uint64_t age = st.now > last ? st.now - last : 0;
-  if (st.policy == 0) return 0xFFFFFFFEu - (uint32_t)(age < 0xFFFFFFFEull ? age : 0xFFFFFFFEull);
-  float crf = st.crf[i] * exp2f(st.log2_inv_att * st.step * (float)age);
-  if (!(crf >= 0.0f)) crf = 0.0f;
-  uint32_t key = __float_as_uint(crf);   // non-negative floats order like their bits
-  return key >= 0xFFFFFFFEu ? 0xFFFFFFFDu : key;
+  uint32_t key;
+  if (st.policy == 0) {
+    key = 0xFFFFFFFEu - (uint32_t)(age < 0xFFFFFFFEull ? age : 0xFFFFFFFEull);
+  } else {
+    float crf = st.crf[i] * exp2f(st.log2_inv_att * st.step * (float)age);
+    if (!(crf >= 0.0f)) crf = 0.0f;
+    key = __float_as_uint(crf);   // non-negative floats order like their bits
+  }
+  if (key >= 0xFFFFFFFEu) key = 0xFFFFFFFDu;
+  return st.invert ? 0xFFFFFFFDu - key : key;   // hottest-first selects the largest keys
+}
+
+__device__ __forceinline__ unsigned long long weight(const uint64_t* __restrict__ fbytes, uint32_t i, int unit) {
+  return unit ? 1ull : (unsigned long long)fbytes[i];
 }
 
 // ---- annotation updates ----------------------------------------------------------------------
@@ -80,15 +90,15 @@ __global__ __launch_bounds__(kEvBlock) void slot_update_kernel(EvictState st, co
 }
 
 // ---- selection ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(kEvBlock) void ev_keys_kernel(EvictState st, uint32_t target_dir,
+__global__ __launch_bounds__(kEvBlock) void ev_keys_kernel(EvictState st, uint64_t dir_mask,
                                                             const uint32_t* __restrict__ excl,
                                                             uint32_t* __restrict__ keys, EvictCtl* ctl) {
   __shared__ unsigned long long s_tot[kEvBlock / 64];
   unsigned long long tot = 0;
   for (uint32_t i = blockIdx.x * kEvBlock + threadIdx.x; i < st.n; i += gridDim.x * kEvBlock) {
-    const uint32_t k = evict_key(st, i, target_dir, excl);
+    const uint32_t k = evict_key(st, i, dir_mask, excl);
     keys[i] = k;
-    if (k != 0xFFFFFFFFu) tot += st.fbytes[i];
+    if (k != 0xFFFFFFFFu) tot += weight(st.fbytes, i, st.unit);
   }
   tot = wave_sum_u64(tot);
   if (lane_id() == 0) s_tot[threadIdx.x >> 6] = tot;
@@ -102,7 +112,7 @@ __global__ __launch_bounds__(kEvBlock) void ev_keys_kernel(EvictState st, uint32
 
 __global__ __launch_bounds__(kEvBlock) void ev_hist_kernel(const uint32_t* __restrict__ keys,
                                                             const uint64_t* __restrict__ fbytes, uint32_t n,
-                                                            uint64_t need, int pass, EvictCtl* ctl) {
+                                                            uint64_t need, int pass, EvictCtl* ctl, int unit) {
   __shared__ unsigned long long h[256];
   __shared__ unsigned long long scan[256];
   __shared__ int s_last;
@@ -132,7 +142,7 @@ __global__ __launch_bounds__(kEvBlock) void ev_hist_kernel(const uint32_t* __res
     for (int u = 0; u < 4; ++u) {
       const uint32_t i = (r * 4 + u) * stride + blockIdx.x * kEvBlock + tid;
       kk[u] = i < n ? keys[i] : 0xFFFFFFFFu;
-      bb[u] = i < n ? (unsigned long long)fbytes[i] : 0ull;
+      bb[u] = i < n ? weight(fbytes, i, unit) : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -193,7 +203,7 @@ __global__ __launch_bounds__(kEvBlock) void ev_hist_kernel(const uint32_t* __res
 __global__ __launch_bounds__(kEvBlock) void ev_compact_kernel(const uint32_t* __restrict__ keys,
                                                                const uint64_t* __restrict__ fbytes, uint32_t n,
                                                                uint64_t need, EvictCtl* ctl,
-                                                               uint32_t* __restrict__ out) {
+                                                               uint32_t* __restrict__ out, int unit) {
   __shared__ uint32_t s_cnt[kEvBlock / 64];
   __shared__ uint32_t s_base;
   __shared__ unsigned long long s_freed[kEvBlock / 64];
@@ -212,7 +222,7 @@ __global__ __launch_bounds__(kEvBlock) void ev_compact_kernel(const uint32_t* __
     if (i < n) {
       const uint32_t k = keys[i];
       if (k != 0xFFFFFFFFu) {
-        b = fbytes[i];
+        b = weight(fbytes, i, unit);
         take = all || k < T;
         if (!take && k == T) {
           const unsigned long long prev = atomicAdd(&ctl->tie_acc, (unsigned long long)b);
@@ -337,12 +347,13 @@ hipError_t launch_evict_select_grid(const EvictState& st, uint32_t target_dir, c
   // >= 1k keys per workgroup (four per thread), at most kEvMaxGrid workgroups
   unsigned grid = (st.n + 1023) / 1024;
   if (grid > kEvMaxGrid) grid = kEvMaxGrid;
-  hipLaunchKernelGGL(ev_keys_kernel, dim3(grid), dim3(kEvBlock), 0, stream, st, target_dir, excl, keys, ctl);
+  const uint64_t mask = st.dir_mask ? st.dir_mask : (1ull << (target_dir & 63));
+  hipLaunchKernelGGL(ev_keys_kernel, dim3(grid), dim3(kEvBlock), 0, stream, st, mask, excl, keys, ctl);
   for (int pass = 0; pass < 4; ++pass)
     hipLaunchKernelGGL(ev_hist_kernel, dim3(grid), dim3(kEvBlock), 0, stream, keys, st.fbytes, st.n, need, pass,
-                       ctl);
+                       ctl, st.unit);
   hipLaunchKernelGGL(ev_compact_kernel, dim3(grid), dim3(kEvBlock), 0, stream, keys, st.fbytes, st.n, need, ctl,
-                     out_slots);
+                     out_slots, st.unit);
   return hipGetLastError();
 }
 

@@ -98,6 +98,9 @@ struct EvictState {
   float step;            // LRFU step factor
   float log2_inv_att;    // log2(1 / attenuation)
   int policy;            // 0 = LRU, 1 = LRFU
+  uint64_t dir_mask;     // candidate dirs (bit d = dir d); 0 = the select's target dir only
+  int unit;              // 1: every candidate weighs 1 (select by count, not bytes)
+  int invert;            // 1: hottest first (select the largest keys)
 };
 constexpr uint32_t kSlotSetState = 1, kSlotReset = 2, kSlotTouch = 4;
 // One coalesced host->device update per slot: state (dir, footprint) and/or annotations

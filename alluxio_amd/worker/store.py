@@ -202,6 +202,16 @@ class TieredStore:
             self.arenas.append(arena)
             if d.alias not in self.tier_aliases:
                 self.tier_aliases.append(d.alias)
+        # multi-tier stores keep align.reserved.bytes (at most a quarter) of every dir free for
+        # tier-management swaps (the reference's reserved space, AllocateOptions.useReservedSpace)
+        if len({d.tier for d in self.dirs}) > 1 and (
+                conf.get_bool("alluxio.worker.management.tier.align.enabled")
+                or conf.get_bool("alluxio.worker.management.tier.promote.enabled")
+                or conf.get_bool("alluxio.worker.management.tier.swap.restore.enabled")):
+            want = conf.get_bytes("alluxio.worker.management.tier.align.reserved.bytes")
+            for spec in specs:
+                r = min(want, spec.capacity // 4)
+                spec.reserved = r - r % page if spec.kind != C.DirKind.FILE else r
         annot = conf.get("alluxio.worker.block.annotator.class").rsplit(".", 1)[-1].replace("Annotator", "").upper()
         alloc = conf.get("alluxio.worker.allocator.class").rsplit(".", 1)[-1].replace("Allocator", "").upper()
         self.native = C.BlockStore(specs, ANNOTATORS.get(annot, 0), ALLOCATORS.get(alloc, 0),

@@ -160,3 +160,35 @@ def test_bulk_create_then_abort_returns_pages(gpu):
     assert s.dir_available(0) == before - 600 * page
     s.cleanup_session(3)
     assert s.dir_available(0) == before
+
+
+def test_tier_order_device_matches_host(gpu):
+    """K8: the k coldest / hottest blocks of a tier from the device select (unit weights, dir mask,
+    inverted keys for hottest) equal the host's full sort."""
+    import torch
+    C = lib()
+    page = 4 * KB
+    arenas, specs = [], []
+    for tier in (0, 1):
+        a = torch.empty(30_000 * page, dtype=torch.uint8, device="cuda")
+        d = C.DirSpec()
+        d.tier, d.tier_alias, d.medium, d.kind = tier, ("MEM", "SSD")[tier], "HBM", C.DirKind.DEVICE
+        d.base, d.capacity, d.page_size, d.device = a.data_ptr(), a.numel(), page, 0
+        arenas.append(a)
+        specs.append(d)
+    s = C.BlockStore(specs, annotator=0, alloc_policy=0, device=0)
+    n = 25_000
+    for tier in (0, 1):
+        ids = list(range(1 + tier * n, 1 + (tier + 1) * n))
+        s.create_blocks(1, ids, tier, "", [page] * n, False)
+        for b in ids:
+            s.commit_block(1, b)
+    rng = np.random.default_rng(9)
+    s.access_blocks((rng.choice(2 * n, 5000, replace=False) + 1).tolist())
+    for tier in (0, 1):
+        for hottest in (False, True):
+            dev = s.tier_order(tier, 100, hottest, True)
+            host = s.tier_order(tier, 100, hottest, False)
+            assert len(dev) == 100 and dev == host, (tier, hottest)
+    keys = s.annotator_keys(s.tier_order(1, 10, True, True))
+    assert keys == sorted(keys, reverse=True)

@@ -58,3 +58,143 @@ def test_promote_align_restore(tmp_path):
         cap, avail = tm._tier_space(0)
         assert avail >= min(tm.reserved, cap // 10)
         fs.close()
+
+
+def _two_tier_conf(tmp_path, mem_mb=8, ssd_mb=8, reserved="2MB", cool="100ms", **extra):
+    """Two tiers x two dirs each (reference BaseTierManagementTaskTest layout), LRU, 1 MB blocks,
+    ``reserved`` bytes of every dir kept for management swaps."""
+    for n in ("ssd0", "ssd1"):
+        os.makedirs(tmp_path / n, exist_ok=True)
+    conf = {"alluxio.worker.tieredstore.levels": "2",
+            "alluxio.worker.tieredstore.level0.alias": "MEM",
+            "alluxio.worker.tieredstore.level0.dirs.path": "dram,dram",
+            "alluxio.worker.tieredstore.level0.dirs.quota": f"{mem_mb}MB,{mem_mb}MB",
+            "alluxio.worker.tieredstore.level1.alias": "SSD",
+            "alluxio.worker.tieredstore.level1.dirs.path": f"{tmp_path / 'ssd0'},{tmp_path / 'ssd1'}",
+            "alluxio.worker.tieredstore.level1.dirs.quota": f"{ssd_mb}MB,{ssd_mb}MB",
+            "alluxio.worker.tieredstore.level1.dirs.mediumtype": "SSD",
+            "alluxio.worker.hbm.page.size": "256KB",
+            "alluxio.user.block.size.bytes.default": "1MB",
+            "alluxio.worker.block.annotator.class": "alluxio.worker.block.annotator.LRUAnnotator",
+            "alluxio.worker.management.tier.align.reserved.bytes": reserved,
+            "alluxio.worker.management.load.detection.cool.down.time": cool,
+            "alluxio.worker.tieredstore.eviction.demote": "false"}
+    conf.update(extra)
+    return conf
+
+
+def _fill(fs, w, tier, prefix):
+    """Write 1 MB files into ``tier`` until its dirs have no user-available space left."""
+    i = 0
+    while sum(w.native.dir_available(d) for d, dc in enumerate(w.store.dirs) if dc.tier == tier) >= MB:
+        fs.write_file(f"/{prefix}/{i}", os.urandom(MB), write_type="MUST_CACHE", write_tier=tier)
+        i += 1
+    return i
+
+
+def test_align_task_aligns_after_load_stops(tmp_path):
+    """AlignTaskTest.testTierAlignment: fill both tiers, access blocks randomly, tiers are not
+    aligned; while user I/O continues the coordinator backs off; once it stops, background
+    passes swap hot lower blocks with cold upper ones (through the reserved space) until every
+    MEM block is hotter than every SSD block."""
+    import random
+    import time
+    conf = _two_tier_conf(tmp_path, **{"alluxio.worker.management.tier.promote.enabled": "false"})
+    with LocalAlluxioCluster(num_workers=1, conf=conf) as c:
+        fs = c.client()
+        w = c.workers[0].worker
+        tm = c.workers[0].tier_manager
+        n_up = _fill(fs, w, 0, "up")
+        n_low = _fill(fs, w, 1, "low")
+        assert n_up >= 8 and n_low >= 8
+        rnd = random.Random(3)
+        blocks = {t: [b for b in w.native.block_ids(t)] for t in (0, 1)}
+        for _ in range(100):
+            t = rnd.choice((0, 1))
+            w.native.access_block(77, rnd.choice(blocks[t]))
+        assert not tm.aligned(0, 1)
+        # simulated user I/O: passes are skipped while the cool-down window is open
+        fs.read_file("/low/0")
+        assert tm.run_once()["skipped_busy"] >= 1 and not tm.aligned(0, 1)
+        tm.start(interval_s=0.05)
+        try:
+            deadline = time.time() + 60
+            while not tm.aligned(0, 1) and time.time() < deadline:
+                time.sleep(0.05)
+            assert tm.aligned(0, 1)
+        finally:
+            tm.stop()
+        assert tm.stats["aligned"] > 0
+        # every byte survived the swaps
+        for i in range(n_up):
+            assert len(fs.read_file(f"/up/{i}")) == MB
+        fs.close()
+
+
+def test_promote_task_respects_quota(tmp_path):
+    """PromoteTaskTest: hot SSD blocks move up while MEM stays under promote.quota.percent."""
+    conf = _two_tier_conf(tmp_path, mem_mb=8, reserved="1MB",
+                          **{"alluxio.worker.management.tier.align.enabled": "false",
+                             "alluxio.worker.management.tier.promote.quota.percent": "50"})
+    with LocalAlluxioCluster(num_workers=1, conf=conf) as c:
+        fs = c.client()
+        w = c.workers[0].worker
+        tm = c.workers[0].tier_manager
+        for i in range(10):
+            fs.write_file(f"/p/{i}", os.urandom(MB), write_type="MUST_CACHE", write_tier=1)
+        tm.cool_down_s = 0
+        tm.run_once(force=True)
+        cap, avail = tm._tier_space(0)
+        used = cap - avail
+        assert 0 < used <= 0.5 * cap
+        assert tm.stats["promoted"] == used // MB
+        fs.close()
+
+
+def test_swap_restore_frees_reserved_space(tmp_path):
+    """SwapRestoreTaskTest: blocks moved into a dir's reserved space (as swaps do) are moved back
+    down by swap-restore until the reserve is free."""
+    conf = _two_tier_conf(tmp_path, mem_mb=8, reserved="2MB",
+                          **{"alluxio.worker.management.tier.align.enabled": "false",
+                             "alluxio.worker.management.tier.promote.enabled": "false"})
+    with LocalAlluxioCluster(num_workers=1, conf=conf) as c:
+        fs = c.client()
+        w = c.workers[0].worker
+        tm = c.workers[0].tier_manager
+        _fill(fs, w, 0, "up")
+        for i in range(6):
+            fs.write_file(f"/low/{i}", os.urandom(MB), write_type="MUST_CACHE", write_tier=1)
+        low = w.native.block_ids(1)
+        moved = w.native.move_blocks(1, low, 0, "", False, True)   # into the reserve
+        assert moved
+        assert any(w.native.dir_mgmt_available(d) < w.native.dir_spec(d).reserved for d in (0, 1))
+        tm.cool_down_s = 0
+        tm.swap_restore(0, 1)
+        for d in (0, 1):
+            assert w.native.dir_mgmt_available(d) >= w.native.dir_spec(d).reserved
+        assert tm.stats["restored"] >= len(moved)
+        fs.close()
+
+
+def test_transfer_partitioner_groups_by_location(tmp_path):
+    """BlockTransferPartitionerTest: transfers are grouped by (source dir, destination) and
+    folded into at most ``max_partitions`` groups."""
+    from alluxio_amd.worker.management import BlockTransferPartitioner
+
+    class Info:
+        def __init__(self, d):
+            self.dir = d
+
+    class Native:
+        def block_info(self, b):
+            return Info(b % 4)
+    transfers = [(b, 1 if b % 2 else 0) for b in range(40)]
+    parts = BlockTransferPartitioner.partition(Native(), transfers, 8)
+    assert len(parts) == 4
+    for p in parts:
+        assert len({(b % 4, d) for b, d in p}) == 1
+    assert sorted(b for p in parts for b, _ in p) == list(range(40))
+    folded = BlockTransferPartitioner.partition(Native(), transfers, 2)
+    assert len(folded) == 2 and sorted(b for p in folded for b, _ in p) == list(range(40))
+    for p in folded:
+        assert len({d for _, d in p}) == 1     # never mixes destinations
