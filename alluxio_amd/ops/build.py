@@ -84,5 +84,57 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return target
 
 
+SANITIZERS = {
+    # host code only: the HIP kernels are compiled as usual (GPU sanitizers are not available on
+    # the pool); the runtime is loaded into the (uninstrumented) interpreter with LD_PRELOAD
+    "asan": (["-fsanitize=address,undefined", "-fno-gpu-sanitize", "-fno-sanitize-recover=undefined",
+              "-shared-libasan"], "libclang_rt.asan-x86_64.so"),
+    "tsan": (["-fsanitize=thread", "-fno-gpu-sanitize"], "libclang_rt.tsan-x86_64.so"),
+}
+
+
+def sanitizer_runtime(kind: str) -> str:
+    import glob
+    name = SANITIZERS[kind][1]
+    hits = glob.glob(os.path.join(ROCM, "lib", "llvm", "lib", "clang", "*", "lib", "linux", name))
+    if not hits:
+        raise RuntimeError(f"{name} not found under {ROCM}/lib/llvm")
+    return hits[0]
+
+
+def build_sanitized(kind: str, out_dir: str | None = None) -> str:
+    """A host-sanitizer build of the extension (CPU test runs only) into
+    ``build/sanitize/<kind>/alluxio_amd/_C*.so``; load it with ``ALLUXIO_AMD_NATIVE_SO`` and the
+    runtime from :func:`sanitizer_runtime` in ``LD_PRELOAD`` (tools/sanitize.sh)."""
+    flags = SANITIZERS[kind][0]
+    out_dir = out_dir or os.path.join(os.path.dirname(PKG_DIR), "build", "sanitize", kind)
+    objdir = os.path.join(out_dir, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    common = ["-O1", "-g", "-fno-omit-frame-pointer", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
+              "-Wno-unused-result", "-Wno-unused-variable", "-fvisibility=hidden"] + _includes()
+    jobs, objs = [], []
+    for src in SOURCES:
+        obj = os.path.join(objdir, src.replace(".", "_") + ".o")
+        objs.append(obj)
+        path = os.path.join(CSRC, src)
+        if src.endswith(".hip"):
+            cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, "-c", path, "-o", obj]
+        else:
+            cmd = [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", *common,
+                   *[f for f in flags if f != "-shared-libasan"], "-c", path, "-o", obj]
+        jobs.append(cmd)
+    with cf.ThreadPoolExecutor(max_workers=4) as ex:
+        for fut in [ex.submit(_run, j) for j in jobs]:
+            fut.result()
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    target = os.path.join(out_dir, "_C" + suffix)
+    _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *flags, *objs, "-o", target, f"-L{ROCM}/lib",
+          "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
+    return target
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
+    if len(sys.argv) > 2 and sys.argv[1] == "--sanitize":
+        print(build_sanitized(sys.argv[2]))
+    else:
+        build(force="--force" in sys.argv, verbose=True)

@@ -45,13 +45,22 @@ def lib():
         return _mod
     with _lock:
         if _mod is None:
-            if os.environ.get("ALLUXIO_AMD_NO_BUILD") != "1":
+            alt = os.environ.get("ALLUXIO_AMD_NATIVE_SO")   # e.g. a sanitizer build (tools/sanitize.sh)
+            if os.environ.get("ALLUXIO_AMD_NO_BUILD") != "1" and not alt:
                 from .build import build
                 build()
             # One HIP runtime per process: load torch's libamdhip64 first so the extension binds
             # to the same runtime (same soname) instead of pulling a second copy from /opt/rocm.
             import torch  # noqa: F401
-            _mod = importlib.import_module("alluxio_amd._C")
+            if alt:
+                import importlib.util
+                import sys
+                spec = importlib.util.spec_from_file_location("alluxio_amd._C", alt)
+                _mod = importlib.util.module_from_spec(spec)
+                sys.modules["alluxio_amd._C"] = _mod
+                spec.loader.exec_module(_mod)
+            else:
+                _mod = importlib.import_module("alluxio_amd._C")
     return _mod
 
 
