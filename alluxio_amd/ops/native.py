@@ -53,10 +53,10 @@ def lib():
             # to the same runtime (same soname) instead of pulling a second copy from /opt/rocm.
             import torch  # noqa: F401
             if alt:
-                import importlib.util
+                import importlib.util as ilu
                 import sys
-                spec = importlib.util.spec_from_file_location("alluxio_amd._C", alt)
-                _mod = importlib.util.module_from_spec(spec)
+                spec = ilu.spec_from_file_location("alluxio_amd._C", alt)
+                _mod = ilu.module_from_spec(spec)
                 sys.modules["alluxio_amd._C"] = _mod
                 spec.loader.exec_module(_mod)
             else:
