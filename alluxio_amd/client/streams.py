@@ -412,11 +412,18 @@ class FileInStream(io.RawIOBase):
             except Exception as e:  # noqa: BLE001
                 last_err = e
                 self._failed[addr] = 1
-        # 3) UFS through a worker chosen by the UFS read policy
+        # 3) UFS through a worker chosen by the UFS read policy: the file in the UFS, or -- for a
+        # not yet persisted file whose block went to the UFS tier -- the block's UFS block file
+        opts = None
         if self.status.persisted and self.status.ufsPath:
             opts = pb.dataserver.OpenUfsBlockOptions(
                 ufs_path=self.status.ufsPath, offset_in_file=idx * self.block_size, block_size=block_len,
                 mountId=self.status.mountId, no_cache=self.read_type == "NO_CACHE")
+        elif not self.status.persisted and not locs and block_len > 0:
+            opts = pb.dataserver.OpenUfsBlockOptions(block_in_ufs_tier=True, block_size=block_len,
+                                                     mountId=self.status.mountId,
+                                                     no_cache=self.read_type == "NO_CACHE")
+        if opts is not None:
             from .policy import create_policy
             pol = create_policy(self.ctx.conf.get("alluxio.user.ufs.block.read.location.policy"), self.ctx.conf)
             workers = self.ctx.workers()
@@ -501,15 +508,36 @@ class LocalBlockWriter(BlockWriter):
             pass
 
 
+class LocalUfsFallbackWriter(BlockWriter):
+    """In-process worker write with the UFS tier (worker/ufs_fallback.py)."""
+
+    def __init__(self, worker, block_id, session, mount_id, tier=0, medium="", initial=1 << 20):
+        from ..worker.ufs_fallback import UfsFallbackBlockWriter
+        self._w = UfsFallbackBlockWriter(worker, session, block_id, mount_id, tier, medium, initial)
+
+    def write_ptr(self, offset, ptr, length, kind):
+        self._w.write_ptr(offset, ptr, length, kind)
+
+    def commit(self):
+        self._w.commit()
+
+    def cancel(self):
+        self._w.cancel()
+
+
 class GrpcBlockWriter(BlockWriter):
     """WriteBlock stream (GrpcDataWriter): command, chunks, then half-close -> commit."""
 
     def __init__(self, ctx, address, block_id, tier=0, medium="", reserve=1 << 20, pin=False,
-                 chunk: int | None = None):
+                 chunk: int | None = None, ufs_fallback_mount: int | None = None):
         self.chunk = chunk or ctx.conf.get_bytes("alluxio.user.network.writer.chunk.size.bytes", "1MB")
-        self._reqs = _AckQueue(pb.block.WriteRequest(command=pb.block.WriteRequestCommand(
-            type=0, id=block_id, offset=0, tier=tier, medium_type=medium, space_to_reserve=reserve,
-            pin_on_create=pin)))
+        cmd = pb.block.WriteRequestCommand(type=0, id=block_id, offset=0, tier=tier, medium_type=medium,
+                                           space_to_reserve=reserve, pin_on_create=pin)
+        if ufs_fallback_mount is not None:
+            # UFS_FALLBACK_BLOCK: the worker spills the block to the UFS when it is out of space
+            cmd.type = 2
+            cmd.create_ufs_block_options.mount_id = ufs_fallback_mount
+        self._reqs = _AckQueue(pb.block.WriteRequest(command=cmd))
         call = ctx.worker_channel(address).raw_stream(SVC_WORKER, "WriteBlock")
         self._resp = call(iter(self._reqs))
         self._result = []
@@ -729,14 +757,22 @@ class FileOutStream(io.RawIOBase):
             pullers = [w for w in chosen[1:] if w.address.host == prim_host and self.ctx.is_local(w.address)]
             self._fanout = [worker_address_str(w.address) for w in pullers]
             chosen = [chosen[0]] + [w for w in chosen[1:] if w not in pullers]
+        # ASYNC_THROUGH with the UFS tier: a worker out of space spills the block to a UFS block
+        # file instead of failing the write (alluxio.user.file.ufs.tier.enabled)
+        ufs_tier = self.write_type == "ASYNC_THROUGH" and \
+            self.ctx.conf.get_bool("alluxio.user.file.ufs.tier.enabled", "false")
         for w in chosen:
             lw = self.ctx.in_process_worker(w.address)
-            if lw is not None:
+            if lw is not None and ufs_tier:
+                self._writers.append(LocalUfsFallbackWriter(lw, bid, self.session, self.status.mountId,
+                                                            self.write_tier, self.medium, max(1, reserve)))
+            elif lw is not None:
                 self._writers.append(LocalBlockWriter(lw, bid, self.session, self.write_tier, self.medium,
                                                       max(1, reserve)))
             else:
                 self._writers.append(GrpcBlockWriter(self.ctx, worker_address_str(w.address), bid,
-                                                     self.write_tier, self.medium, reserve))
+                                                     self.write_tier, self.medium, reserve,
+                                                     ufs_fallback_mount=self.status.mountId if ufs_tier else None))
         self._block_written = 0
 
     def _finish_block(self) -> None:

@@ -118,30 +118,164 @@ def read_checkpoint_header(f) -> CheckpointType:
     return CheckpointType(struct.unpack(">q", b)[0])
 
 
-def write_compound(f, parts: list[tuple[str, bytes]]) -> None:
-    """COMPOUND checkpoint body: repeated (utf8 name, payload) with 4-byte BE lengths.
+# ---- Kryo chunked COMPOUND checkpoints ------------------------------------------------------
+# Reference: JournalUtils.writeToCheckpoint (core/server/common/.../journal/JournalUtils.java:
+# 128-137) wraps a CheckpointOutputStream(COMPOUND) in Kryo's OutputChunked(64 KB): per component
+# it writes the CheckpointName with Kryo's writeString, then the component's own checkpoint stream
+# (an 8-byte big-endian CheckpointType followed by its data), then endChunks().  On the wire a
+# chunk is a Kryo varint length (7 bits per byte, 0x80 = more) followed by that many bytes; a
+# zero-length chunk ends a component.  CompoundCheckpointFormat.CompoundCheckpointReader reads it
+# back with InputChunked (nextChunks skips to the byte after the zero marker).
+KRYO_CHUNK = 64 * 1024
+# component (master) name <-> CheckpointName (checkpoint/CheckpointName.java)
+CHECKPOINT_NAMES = {"FileSystemMaster": "FILE_SYSTEM_MASTER", "BlockMaster": "BLOCK_MASTER",
+                    "MetaMaster": "META_MASTER", "TableMaster": "TABLE_MASTER", "Noop": "NOOP"}
+_NAMES_BACK = {v: k for k, v in CHECKPOINT_NAMES.items()}
 
-    The reference uses kryo chunked encoding here; the framing is ours, the semantics (named
-    sub-checkpoints, one per master component) are the same.
-    """
-    f.write(struct.pack(">i", len(parts)))
+
+def kryo_varint(n: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def kryo_string(s: str | None) -> bytes:
+    """Kryo Output.writeString: 1 < len < 64 ASCII -> the bytes with bit 7 set on the last one;
+    otherwise a UTF-8 length header (charCount + 1; 0 = null) and the characters."""
+    if s is None:
+        return b"\x80"
+    n = len(s)
+    if n == 0:
+        return bytes([1 | 0x80])
+    if 1 < n < 64 and all(ord(c) < 128 for c in s):
+        b = bytearray(s.encode("ascii"))
+        b[-1] |= 0x80
+        return bytes(b)
+    v = n + 1
+    hdr = bytearray()
+    # writeUtf8Length: 6 bits + (0x80 = UTF-8 flag, 0x40 = more), then 7-bit groups
+    first = (v & 0x3F) | 0x80
+    v >>= 6
+    if v:
+        first |= 0x40
+    hdr.append(first)
+    while v:
+        b = v & 0x7F
+        v >>= 7
+        hdr.append(b | (0x80 if v else 0))
+    return bytes(hdr) + s.encode("utf-8", "surrogatepass")
+
+
+class _ChunkedReader:
+    """Kryo InputChunked over a whole (small enough) checkpoint body."""
+
+    def __init__(self, data: bytes, pos: int = 0):
+        self.data, self.pos = data, pos
+
+    def _varint(self) -> int:
+        shift = out = 0
+        while True:
+            if self.pos >= len(self.data):
+                raise EOFError("truncated chunk length")
+            b = self.data[self.pos]
+            self.pos += 1
+            out |= (b & 0x7F) << shift
+            if not b & 0x80:
+                return out
+            shift += 7
+
+    def component(self) -> bytes | None:
+        """Bytes of the next component (its chunks up to the zero marker), None at EOF."""
+        if self.pos >= len(self.data):
+            return None
+        parts = []
+        while True:
+            n = self._varint()
+            if n == 0:
+                return b"".join(parts)
+            parts.append(self.data[self.pos:self.pos + n])
+            if len(parts[-1]) != n:
+                raise EOFError("truncated chunk")
+            self.pos += n
+
+
+def kryo_read_string(buf: bytes, pos: int = 0) -> tuple[str | None, int]:
+    b = buf[pos]
+    if not b & 0x80:                         # ASCII: until the byte with bit 7 set
+        end = pos
+        while not buf[end] & 0x80:
+            end += 1
+        s = bytes(buf[pos:end]) + bytes([buf[end] & 0x7F])
+        return s.decode("ascii"), end + 1
+    v = b & 0x3F
+    pos += 1
+    if b & 0x40:
+        shift = 6
+        while True:
+            c = buf[pos]
+            pos += 1
+            v |= (c & 0x7F) << shift
+            shift += 7
+            if not c & 0x80:
+                break
+    if v == 0:
+        return None, pos
+    chars = v - 1
+    out = []
+    while len(out) < chars:                   # Kryo's UTF-8 of UTF-16 units
+        c = buf[pos]
+        if c < 0x80:
+            out.append(chr(c))
+            pos += 1
+        elif c >> 5 == 0x6:
+            out.append(chr(((c & 0x1F) << 6) | (buf[pos + 1] & 0x3F)))
+            pos += 2
+        else:
+            out.append(chr(((c & 0x0F) << 12) | ((buf[pos + 1] & 0x3F) << 6) | (buf[pos + 2] & 0x3F)))
+            pos += 3
+    return "".join(out), pos
+
+
+def write_compound(f, parts: list[tuple[str, bytes]], sub_type: "CheckpointType | None" = None) -> None:
+    """COMPOUND checkpoint (header included) in the reference's Kryo chunked layout.  ``parts``
+    = (component name, component checkpoint body); the body gets its own 8-byte CheckpointType
+    header (``sub_type``, default JOURNAL_ENTRY = delimited journal entries)."""
+    sub_type = CheckpointType.JOURNAL_ENTRY if sub_type is None else sub_type
+    write_checkpoint_header(f, CheckpointType.COMPOUND)
     for name, data in parts:
-        nb = name.encode()
-        f.write(struct.pack(">i", len(nb)))
-        f.write(nb)
-        f.write(struct.pack(">q", len(data)))
-        f.write(data)
+        payload = kryo_string(CHECKPOINT_NAMES.get(name, name)) + struct.pack(">q", int(sub_type)) + data
+        # OutputChunked(64 KB): full buffers go out as 65536-byte chunks, endChunks() flushes the
+        # rest and writes the zero-length marker
+        for i in range(0, len(payload), KRYO_CHUNK):
+            piece = payload[i:i + KRYO_CHUNK]
+            f.write(kryo_varint(len(piece)))
+            f.write(piece)
+        f.write(b"\x00")
 
 
 def read_compound(f) -> list[tuple[str, bytes]]:
-    (n,) = struct.unpack(">i", f.read(4))
+    """Components of a COMPOUND checkpoint (header included): (component name, body after the
+    component's own CheckpointType header)."""
+    ctype = read_checkpoint_header(f)
+    if ctype != CheckpointType.COMPOUND:
+        raise ValueError(f"not a COMPOUND checkpoint: {ctype.name}")
+    r = _ChunkedReader(f.read())
     out = []
-    for _ in range(n):
-        (ln,) = struct.unpack(">i", f.read(4))
-        name = f.read(ln).decode()
-        (dl,) = struct.unpack(">q", f.read(8))
-        out.append((name, f.read(dl)))
-    return out
+    while True:
+        comp = r.component()
+        if comp is None:
+            return out
+        name, pos = kryo_read_string(comp, 0)
+        (sub,) = struct.unpack(">q", comp[pos:pos + 8])
+        if sub != CheckpointType.JOURNAL_ENTRY:
+            raise ValueError(f"component {name}: unsupported checkpoint type {CheckpointType(sub).name}")
+        out.append((_NAMES_BACK.get(name, name), comp[pos + 8:]))
 
 
 def entries_to_bytes(entries) -> bytes:

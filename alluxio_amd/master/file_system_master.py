@@ -1161,6 +1161,22 @@ class FileSystemMaster(Journaled):
                 pass
             self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
                 id=file_id, persistence_state=PERSISTED, ufs_fingerprint=fp)))
+            blocks = list(f.block_ids)
+            mount = self.mount_table.resolve(path)
+        # best effort: staging UFS block files of the UFS tier are garbage now
+        # (DefaultFileSystemMaster persist checker, :3985-3996)
+        try:
+            from ..worker.ufs_fallback import ufs_block_path
+            root = mount.mount.ufs_uri
+            for bid in blocks:
+                p = ufs_block_path(root, bid)
+                try:
+                    if mount.ufs.exists(p):
+                        mount.ufs.delete_file(p)
+                except Exception:  # noqa: BLE001
+                    pass
+        except Exception:  # noqa: BLE001
+            LOG.debug("UFS block cleanup after persist failed", exc_info=True)
 
     def worker_heartbeat(self, worker_id: int, persisted_files: list[int]):
         for fid in persisted_files:

@@ -350,8 +350,30 @@ class BlockWorker:
             self._ufs_cache[opts.mountId] = u
         return u
 
-    def read_ufs_range(self, opts, offset: int, length: int) -> bytes:
+    def ufs_block_target(self, mount_id: int, block_id: int):
+        """(UFS, path) of the UFS block file of ``block_id`` under mount ``mount_id``
+        (BlockUtils.getUfsBlockPath)."""
+        from ..underfs import registry
+        from .ufs_fallback import ufs_block_path
+        fsm = self._fsm()
+        if fsm is None:
+            raise NotFoundException("no master connection to resolve the UFS of mount %d" % mount_id)
+        info = fsm.GetUfsInfo(pb.file.GetUfsInfoPRequest(mountId=mount_id)).ufsInfo
+        path = ufs_block_path(info.uri, block_id)
+        if self._ufs_resolver is not None:
+            return self._ufs_resolver(mount_id, path), path
+        return registry.create(path, self.conf, dict(info.properties.properties)), path
+
+    def commit_block_in_ufs(self, block_id: int, length: int) -> None:
+        bm = self._bm()
+        if bm is not None:
+            bm.CommitBlockInUfs(pb.block.CommitBlockInUfsPRequest(blockId=block_id, length=length))
+        self.metrics.counter("BlocksCommittedInUfs").inc()
+
+    def read_ufs_range(self, opts, offset: int, length: int, block_id: int = 0) -> bytes:
         from ..underfs.base import OpenOptions
+        from .ufs_fallback import resolve_ufs_block_opts
+        opts = resolve_ufs_block_opts(self, block_id, opts)
         ufs = self._ufs_for(opts)
         with ufs.open(opts.ufs_path, OpenOptions(offset=opts.offset_in_file + offset)) as f:
             data = f.read(length)
@@ -367,6 +389,8 @@ class BlockWorker:
             return True
         session_id = session_id if session_id is not None else ids.CACHE_UFS_SESSION_ID
         from ..underfs.base import OpenOptions
+        from .ufs_fallback import resolve_ufs_block_opts
+        opts = resolve_ufs_block_opts(self, block_id, opts)
         ufs = self._ufs_for(opts)
         length = opts.block_size
         try:

@@ -68,8 +68,10 @@ class BlockWorkerService:
         try:
             bid = first.block_id
             if not self.w.has_block(bid):
-                if first.HasField("open_ufs_block_options") and first.open_ufs_block_options.ufs_path:
-                    opts = first.open_ufs_block_options
+                if first.HasField("open_ufs_block_options") and (first.open_ufs_block_options.ufs_path or
+                                                                 first.open_ufs_block_options.block_in_ufs_tier):
+                    from .ufs_fallback import resolve_ufs_block_opts
+                    opts = resolve_ufs_block_opts(self.w, bid, first.open_ufs_block_options)
                     if opts.no_cache or first.offset != 0 or self.w.native.has_temp_block(bid):
                         # partial / uncached reads (or another reader is caching it): plain stream
                         yield from self._stream_ufs(opts, first.offset, first.length, chunk, acked, cond, done)
@@ -180,6 +182,9 @@ class BlockWorkerService:
         if rtype == "UFS_FILE":
             yield from self._write_ufs_file(cmd, it)
             return
+        if rtype == "UFS_FALLBACK_BLOCK":
+            yield from self._write_ufs_fallback(cmd, it, session)
+            return
         bid = cmd.id
         tier = cmd.tier if cmd.HasField("tier") else 0
         medium = cmd.medium_type
@@ -203,6 +208,32 @@ class BlockWorkerService:
                     self.w.abort_block(session, bid)
                 except Exception:  # noqa: BLE001
                     pass
+            self.w.cleanup_session(session)
+
+    def _write_ufs_fallback(self, cmd, it, session):
+        """UfsFallbackBlockWriteHandler: local block, spilling to a UFS block file when the worker
+        runs out of space (worker/ufs_fallback.py)."""
+        from .ufs_fallback import UfsFallbackBlockWriter
+        o = cmd.create_ufs_block_options
+        if o.fallback and o.bytes_in_block_store:
+            raise InvalidArgumentException("short-circuit UFS fallback with bytes already in the block store is "
+                                           "not supported; write the block through this stream from offset 0")
+        reserve = cmd.space_to_reserve or self.conf.get_bytes("alluxio.worker.file.buffer.size", "1MB")
+        w = UfsFallbackBlockWriter(self.w, session, cmd.id, o.mount_id, cmd.tier if cmd.HasField("tier") else 0,
+                                   cmd.medium_type, reserve, local=not o.fallback, pin=cmd.pin_on_create)
+        done = False
+        try:
+            for req in it:
+                if req.HasField("chunk"):
+                    w.write(req.chunk.data)
+                elif req.HasField("command") and req.command.flush:
+                    yield pb.block.WriteResponse(offset=w.pos)
+            w.commit()
+            done = True
+            yield pb.block.WriteResponse(offset=w.pos)
+        finally:
+            if not done:
+                w.cancel()
             self.w.cleanup_session(session)
 
     def _write_ufs_file(self, cmd, it):

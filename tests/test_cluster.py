@@ -211,3 +211,47 @@ def test_domain_socket_data_server(tmp_path):
         fs2.close()
     import shutil
     shutil.rmtree(uds_dir, ignore_errors=True)
+
+
+def test_ufs_fallback_block_write(tmp_path):
+    """UFS_FALLBACK_BLOCK (UfsFallbackBlockWriteHandler): an ASYNC_THROUGH write with the UFS tier
+    enabled to a worker too small for the block spills the block -- bytes already written
+    included -- to a UFS block file, commits it to the master as in-UFS, reads come back from
+    that file, and persisting the file removes the staging block files.  Both the gRPC handler
+    and the in-process writer are exercised."""
+    from alluxio_amd.client import context as cctx
+    from alluxio_amd.worker.ufs_fallback import UFS_BLOCKS_DIR
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "dram",
+            "alluxio.worker.tieredstore.level0.dirs.quota": "3MB",
+            "alluxio.worker.hbm.page.size": "256KB",
+            "alluxio.user.block.size.bytes.default": "4MB",
+            "alluxio.user.file.buffer.bytes": "1MB",
+            "alluxio.user.file.ufs.tier.enabled": "true"}
+    with LocalAlluxioCluster(num_workers=1, grpc=True, conf=conf, work_dir=str(tmp_path / "c")) as c:
+        fs = c.client()
+        from alluxio_amd.job.persist import inline_persist_handler
+        c.master.fs_master.persist_handler = inline_persist_handler(c.master.fs_master, fs)
+        blocks_dir = os.path.join(c.ufs_root, UFS_BLOCKS_DIR)
+        w = c.workers[0].worker
+        for name, via_grpc in (("inproc", False), ("grpc", True)):
+            data = os.urandom(9 * MB + 77)
+            before = w.metrics.counter("UfsFallbackBlocks").count
+            saved = dict(cctx._LOCAL_WORKERS)
+            if via_grpc:
+                cctx._LOCAL_WORKERS.clear()
+            try:
+                fs.write_file(f"/fb/{name}", data, write_type="ASYNC_THROUGH")
+            finally:
+                cctx._LOCAL_WORKERS.update(saved)
+            st = fs.get_status(f"/fb/{name}")
+            assert st.length == len(data) and not st.persisted
+            assert os.listdir(blocks_dir), "no block went to the UFS tier"
+            assert w.metrics.counter("UfsFallbackBlocks").count > before
+            assert fs.read_file(f"/fb/{name}", read_type="NO_CACHE") == data
+            # persisting (UFS-tier blocks read back from their block files) clears the staging files
+            c.master.fs_master.persistence_scheduler_heartbeat()
+            assert fs.get_status(f"/fb/{name}").persisted
+            with open(os.path.join(c.ufs_root, "fb", name), "rb") as f:
+                assert f.read() == data
+            assert os.listdir(blocks_dir) == []
+        fs.close()

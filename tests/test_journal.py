@@ -160,3 +160,51 @@ def test_upgrade_v0_journal(tmp_path):
     js.start()
     assert bm._container_limit == 9
     js.stop()
+
+
+def test_compound_checkpoint_kryo_golden_bytes():
+    """COMPOUND checkpoints use the reference's Kryo chunked layout (JournalUtils.writeToCheckpoint,
+    CompoundCheckpointFormat): bytes derived by hand from Kryo's OutputChunked/writeString."""
+    import io
+    import struct
+
+    from alluxio_amd.journal import format as fmt
+    b = io.BytesIO()
+    fmt.write_compound(b, [("Noop", b"")])
+    # CheckpointOutputStream(COMPOUND) = 8-byte BE 1; chunk of 12 bytes: "NOOP" as Kryo ASCII
+    # (last byte | 0x80) + the component's CheckpointType JOURNAL_ENTRY (8-byte BE 0); end marker 0
+    assert b.getvalue() == struct.pack(">q", 1) + b"\x0c" + b"NOO\xd0" + b"\x00" * 8 + b"\x00"
+    # 64 KB OutputChunked buffer: a 70000-byte body spans a full 65536-byte chunk and a tail
+    body = bytes(range(256)) * 273 + b"xy"          # 69890 bytes
+    b = io.BytesIO()
+    fmt.write_compound(b, [("FileSystemMaster", body)])
+    raw = b.getvalue()
+    name = fmt.kryo_string("FILE_SYSTEM_MASTER")
+    assert name == b"FILE_SYSTEM_MASTE" + bytes([ord("R") | 0x80])
+    payload = name + b"\x00" * 8 + body
+    assert raw[8:11] == b"\x80\x80\x04"                      # varint 65536
+    assert raw[11:11 + 65536] == payload[:65536]
+    rest = len(payload) - 65536
+    assert raw[11 + 65536:] == fmt.kryo_varint(rest) + payload[65536:] + b"\x00"
+    assert fmt.read_compound(io.BytesIO(raw)) == [("FileSystemMaster", body)]
+    # Kryo strings: null, empty, 1 char and >= 64 chars take the UTF-8 length form
+    assert fmt.kryo_string(None) == b"\x80" and fmt.kryo_string("") == b"\x81"
+    assert fmt.kryo_string("A") == b"\x82A"
+    s64 = "a" * 64
+    assert fmt.kryo_string(s64) == b"\xc1\x01" + s64.encode()
+    for s in (None, "", "A", "NOOP", s64, "ÿ€x"):
+        assert fmt.kryo_read_string(fmt.kryo_string(s) + b"tail", 0)[0] == s
+
+
+def test_raft_snapshot_uses_compound(tmp_path):
+    import io
+
+    from alluxio_amd.journal import format as fmt
+    from alluxio_amd.proto import pb
+    entries = [pb.journal.JournalEntry(sequence_number=i, delete_file=pb.journal.DeleteFileEntry(id=i))
+               for i in range(3)]
+    b = io.BytesIO()
+    fmt.write_compound(b, [("BlockMaster", fmt.entries_to_bytes(entries)), ("TableMaster", b"")])
+    parts = fmt.read_compound(io.BytesIO(b.getvalue()))
+    assert [p[0] for p in parts] == ["BlockMaster", "TableMaster"]
+    assert [e.delete_file.id for e in fmt.bytes_to_entries(parts[0][1])] == [0, 1, 2]

@@ -112,3 +112,45 @@ def test_grpc_read_frames_from_hbm(tmp_path, gpu):
             out = f.read()
         assert np.array_equal(np.frombuffer(out, dtype=np.uint8), data)
         fs.close()
+
+
+# Golden bytes derived by hand from the reference, not from this project's own proto code:
+# ReadResponseMarshaller.serialize (core/common/.../grpc/ReadResponseMarshaller.java:45-62) writes
+# tag(ReadResponse.chunk=1, LEN)=0x0A, uint32(Chunk serialized size), tag(Chunk.data=1, LEN)=0x0A,
+# uint32(n), then the payload; WriteRequest.chunk is field 2 (tag 0x12) of block_worker.proto:97-101.
+@pytest.mark.parametrize("n,hdr", [
+    (5, "0a070a05"),
+    (127, "0a81010a7f"),                 # Chunk = 1 + 1 + 127 = 129 -> varint 81 01
+    (128, "0a83010a8001"),               # Chunk = 1 + 2 + 128 = 131; data length 128 -> 80 01
+    (300, "0aaf020aac02"),               # 303 -> af 02; 300 -> ac 02
+    (1 << 20, "0a8480400a808040"),       # 1048580 -> 84 80 40; 1048576 -> 80 80 40
+])
+def test_read_response_frame_golden_bytes(n, hdr):
+    from alluxio_amd.rpc import marshal
+    data = bytes((i * 7) & 0xFF for i in range(n))
+    f = marshal.read_response_frame(data)
+    raw = f.SerializeToString()
+    assert raw[:len(hdr) // 2] == bytes.fromhex(hdr) and raw[len(hdr) // 2:] == data
+    assert marshal.read_response_header(n) == bytes.fromhex(hdr)
+    w = marshal.write_request_frame(data).SerializeToString()
+    assert w[:1] == b"\x12" and w[1:len(hdr) // 2] == bytes.fromhex(hdr)[1:]
+
+
+def test_sasl_plain_golden_bytes():
+    """The PLAIN initial response (RFC 4616: authzid NUL authcid NUL passwd, as the reference's
+    PlainSaslServer parses it) inside SaslMessage{messageType=CHALLENGE(0), message=2,
+    clientId=3, authenticationScheme=SIMPLE(1) (=4), channelRef=5} (sasl_server.proto)."""
+    from alluxio_amd.proto import pb
+    from alluxio_amd.security.authentication import SCHEMES, parse_plain, plain_payload
+    p = plain_payload("alice", "pw")
+    assert p == b"\x00alice\x00pw"
+    assert plain_payload("bob", "", impersonate="carol") == b"carol\x00bob\x00"
+    assert parse_plain(p)[1] == "alice"
+    m = pb.sasl.SaslMessage(messageType=0, message=p, clientId="c1", authenticationScheme=SCHEMES["SIMPLE"],
+                            channelRef="c1")
+    expect = (b"\x08\x00"                      # messageType = CHALLENGE
+              + b"\x12\x09" + p                # message (9 bytes)
+              + b"\x1a\x02c1"                  # clientId
+              + b"\x20\x01"                    # authenticationScheme = SIMPLE
+              + b"\x2a\x02c1")                 # channelRef
+    assert m.SerializeToString() == expect
