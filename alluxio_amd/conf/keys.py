@@ -173,6 +173,11 @@ _k("WORKER_UFS_INGEST_CHUNK_SIZE", "alluxio.worker.ufs.ingest.chunk.size", "8MB"
    "UFS read size of the UFS->HBM ingest pipeline (one pinned staging buffer each).")
 _k("WORKER_UFS_INGEST_DEPTH", "alluxio.worker.ufs.ingest.depth", "3", Scope.WORKER,
    "Staging buffers per ingest pipeline: UFS reads run this many chunks ahead of the H2D DMA.")
+_k("WORKER_UFS_INGEST_BULK_STAGING_SIZE", "alluxio.worker.ufs.ingest.bulk.staging.size", "64MB", Scope.WORKER,
+   "Pinned staging of the bulk small-file ingest (two halves: preads fill one while the other is "
+   "copied into HBM).")
+_k("WORKER_UFS_INGEST_BULK_THREADS", "alluxio.worker.ufs.ingest.bulk.threads", "16", Scope.WORKER,
+   "Native reader threads of the bulk small-file ingest.")
 _k("WORKER_TIEREDSTORE_EVICTION_DEMOTE", "alluxio.worker.tieredstore.eviction.demote", "true", Scope.WORKER,
    "Eviction from a tier with a lower tier demotes the victims into it (one batched HBM->DRAM / "
    "DRAM->SSD move, making room there recursively) instead of dropping them.")

@@ -2,6 +2,7 @@
 // All entry points release the GIL: the Python worker serves many concurrent gRPC streams.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#include <pybind11/numpy.h>
 
 #include <cmath>
 #include <cstring>
@@ -259,6 +260,26 @@ PYBIND11_MODULE(_C, m) {
              s.read_batch(rs, stream, sync);
            },
            py::arg("reqs"), py::arg("stream") = 0, py::arg("sync") = true)
+      // The same batched read from parallel arrays (no per-request Python tuples): the record
+      // gather of a training input batch (models/dataset.py).
+      .def("read_batch_arrays",
+           [](BlockStore& s, py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids,
+              py::array_t<uint64_t, py::array::c_style | py::array::forcecast> offs,
+              py::array_t<uint64_t, py::array::c_style | py::array::forcecast> lens,
+              py::array_t<uint64_t, py::array::c_style | py::array::forcecast> dsts, int kind, uint64_t stream,
+              bool sync) {
+             const ssize_t n = ids.size();
+             if (offs.size() != n || lens.size() != n || dsts.size() != n)
+               throw StoreError(kErrInvalidArgument, "read_batch_arrays: length mismatch");
+             std::vector<ReadReq> rs((size_t)n);
+             const int64_t* pi = ids.data();
+             const uint64_t *po = offs.data(), *pl = lens.data(), *pd = dsts.data();
+             for (ssize_t i = 0; i < n; ++i) rs[(size_t)i] = ReadReq{pi[i], po[i], pl[i], pd[i], kind};
+             py::gil_scoped_release rel;
+             s.read_batch(rs, stream, sync);
+           },
+           py::arg("block_ids"), py::arg("offsets"), py::arg("lengths"), py::arg("dsts"), py::arg("dst_kind"),
+           py::arg("stream") = 0, py::arg("sync") = true)
       .def("read", [](BlockStore& s, int64_t id, uint64_t off, uint64_t len, uint64_t dst, int kind,
                       uint64_t stream, bool sync) {
              std::vector<ReadReq> rs{ReadReq{id, off, len, dst, kind}};
@@ -302,6 +323,9 @@ PYBIND11_MODULE(_C, m) {
            py::arg("device") = true)
       .def("annotator_keys", &BlockStore::annotator_keys, G())
       .def("dir_mgmt_available", &BlockStore::dir_mgmt_available, G())
+      .def("ingest_files", &BlockStore::ingest_files, G(), py::arg("session"), py::arg("block_ids"),
+           py::arg("paths"), py::arg("offsets"), py::arg("lengths"), py::arg("staging"), py::arg("staging_bytes"),
+           py::arg("threads") = 8, py::arg("stream") = 0)
       .def("create_blocks", &BlockStore::create_blocks, G(), py::arg("session"), py::arg("block_ids"),
            py::arg("tier") = -1, py::arg("medium") = "", py::arg("sizes") = std::vector<uint64_t>{},
            py::arg("evict") = true)

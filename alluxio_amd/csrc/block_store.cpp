@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <thread>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -1803,6 +1804,124 @@ void ReadSession::close() {
       lock_[i] = -1;
     }
   }
+}
+
+std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int64_t>& ids,
+                                          const std::vector<std::string>& paths,
+                                          const std::vector<uint64_t>& offsets,
+                                          const std::vector<uint64_t>& lengths, uint64_t staging,
+                                          uint64_t staging_bytes, int threads, uint64_t stream) {
+  const size_t n = ids.size();
+  if (paths.size() != n || offsets.size() != n || lengths.size() != n)
+    throw StoreError(kErrInvalidArgument, "ingest_files: argument lengths differ");
+  if (!staging || staging_bytes < 2) throw StoreError(kErrInvalidArgument, "ingest_files: no staging buffer");
+  set_device();
+  hipStream_t st = stream_or_default(stream);
+  const uint64_t half = staging_bytes / 2;
+  for (uint64_t len : lengths)
+    if (len > half) throw StoreError(kErrInvalidArgument, "ingest_files: a file is larger than half the staging buffer");
+  threads = std::max(1, std::min(threads, 64));
+  std::vector<int> status(n, 0);
+  // groups of consecutive items that fit one staging half
+  std::vector<std::pair<size_t, size_t>> groups;
+  for (size_t i = 0; i < n;) {
+    size_t j = i;
+    uint64_t used = 0;
+    while (j < n && used + lengths[j] <= half) used += lengths[j++];
+    groups.emplace_back(i, j);
+    i = j;
+  }
+  std::vector<std::vector<int64_t>> pending(2);   // blocks whose copy from staging half h is in flight
+  auto finish = [&](int h) {
+    if (pending[h].empty()) return;
+    if (has_device_) HIP_OK(hipStreamSynchronize(st));
+    for (int64_t id : pending[h]) commit_block(session, id, false);
+    pending[h].clear();
+  };
+  for (size_t g = 0; g < groups.size(); ++g) {
+    const int h = (int)(g & 1);
+    finish(h);                                     // staging half h is free again
+    const size_t lo = groups[g].first, hi = groups[g].second;
+    uint8_t* base = reinterpret_cast<uint8_t*>(staging) + h * half;
+    std::vector<uint64_t> at(hi - lo);
+    uint64_t off = 0;
+    for (size_t i = lo; i < hi; ++i) { at[i - lo] = off; off += lengths[i]; }
+    // 1) temp blocks (skip ones that exist)
+    std::vector<int64_t> gid;
+    std::vector<uint64_t> gsz;
+    std::vector<size_t> gix;
+    {
+      std::lock_guard<std::mutex> g2(mu_);
+      for (size_t i = lo; i < hi; ++i) {
+        if (blocks_.count(ids[i])) { status[i] = 1; continue; }
+        gid.push_back(ids[i]);
+        gsz.push_back(lengths[i]);
+        gix.push_back(i);
+      }
+    }
+    if (gid.empty()) continue;
+    try {
+      create_blocks(session, gid, 0, "", gsz, true);
+    } catch (const StoreError&) {
+      // mixed case (a racing creator, or no single dir fits the group): one at a time
+      for (size_t k = 0; k < gid.size(); ++k) {
+        if (has_temp_block(gid[k]) || has_block(gid[k])) {
+          std::lock_guard<std::mutex> g2(mu_);
+          BlockMeta* b = find(gid[k]);
+          if (b && b->temp && b->session == session) continue;   // created by the bulk call
+          status[gix[k]] = 1;
+          continue;
+        }
+        try {
+          create_block(session, gid[k], 0, "", std::max<uint64_t>(gsz[k], 1), true, false);
+        } catch (const StoreError& e) {
+          status[gix[k]] = e.code == kErrAlreadyExists ? 1 : 3;
+        }
+      }
+    }
+    // 2) parallel preads into the staging half
+    std::atomic<size_t> next{0};
+    auto reader = [&]() {
+      for (size_t k; (k = next.fetch_add(1)) < gix.size();) {
+        const size_t i = gix[k];
+        if (status[i] != 0) continue;
+        int fd = ::open(paths[i].c_str(), O_RDONLY | O_CLOEXEC);
+        if (fd < 0) { status[i] = 2; continue; }
+        uint64_t got = 0;
+        while (got < lengths[i]) {
+          ssize_t r = ::pread(fd, base + at[i - lo] + got, lengths[i] - got, (off_t)(offsets[i] + got));
+          if (r <= 0) break;
+          got += (uint64_t)r;
+        }
+        ::close(fd);
+        if (got != lengths[i]) status[i] = 2;
+      }
+    };
+    const int nt = (int)std::min<size_t>((size_t)threads, gix.size());
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(reader);
+    reader();
+    for (auto& t : pool) t.join();
+    // 3) copies into the blocks (async); commit once the half's copies are done
+    for (size_t k = 0; k < gix.size(); ++k) {
+      const size_t i = gix[k];
+      if (status[i] == 3 || status[i] == 1) continue;
+      if (status[i] == 2) {
+        try { abort_block(session, ids[i]); } catch (const StoreError&) {}
+        continue;
+      }
+      try {
+        write(session, ids[i], 0, (uint64_t)(base + at[i - lo]), lengths[i], (int)MemKind::kHost, stream, false);
+        pending[h].push_back(ids[i]);
+      } catch (const StoreError&) {
+        status[i] = 3;
+        try { abort_block(session, ids[i]); } catch (const StoreError&) {}
+      }
+    }
+  }
+  finish(0);
+  finish(1);
+  return status;
 }
 
 }  // namespace amdx

@@ -146,6 +146,15 @@ class BlockStore {
   std::vector<int> create_blocks(int64_t session, const std::vector<int64_t>& block_ids, int tier,
                                  const std::string& medium, const std::vector<uint64_t>& sizes, bool evict);
   void request_space(int64_t session, int64_t block_id, uint64_t additional);
+  // Bulk cache of small files (dataset warm-up / load job): for each (block id, local file path,
+  // offset, length) the bytes are pread by `threads` host threads into the caller's pinned
+  // staging buffer, copied into fresh temp blocks (async H2D for an HBM dir, the two staging
+  // halves double-buffered so reads overlap the copies) and committed.  Returns a status per
+  // item: 0 = cached, 1 = already present, 2 = read error, 3 = no space.
+  std::vector<int> ingest_files(int64_t session, const std::vector<int64_t>& block_ids,
+                                const std::vector<std::string>& paths, const std::vector<uint64_t>& offsets,
+                                const std::vector<uint64_t>& lengths, uint64_t staging, uint64_t staging_bytes,
+                                int threads, uint64_t stream);
   // Append/overwrite bytes of a temp block (auto-grows).  src_kind: MemKind.
   // Reserve pages for [offset, offset+len) of a temp block and mark those bytes as written by
   // an external producer (RCCL recv / peer DMA straight into the block's pages). Returns the

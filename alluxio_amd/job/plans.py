@@ -207,8 +207,12 @@ class LoadDefinition(PlanDefinition):
 
     def run_task(self, cfg, args, ctx):
         loaded = 0
+        from_ufs = []       # UFS blocks go to the worker in one bulk ingest call
+        statuses = {}
         for path, block_id in args:
-            st = ctx.fs.get_status(path)
+            st = statuses.get(path)
+            if st is None:
+                st = statuses[path] = ctx.fs.get_status(path)
             idx = list(st.info.blockIds).index(block_id)
             opts = pb.dataserver.OpenUfsBlockOptions(
                 ufs_path=st.info.ufsPath, offset_in_file=idx * st.info.blockSizeBytes,
@@ -220,9 +224,12 @@ class LoadDefinition(PlanDefinition):
                 from ..worker.remote import remote_block_fetcher
                 src = locs[0].workerAddress
                 remote_block_fetcher(ctx.worker, src.host, src.rpcPort, opts.block_size)(block_id)
+                loaded += opts.block_size
             elif ctx.worker is not None:
-                ctx.worker.cache_block_from_ufs(block_id, opts)
-            loaded += opts.block_size
+                from_ufs.append((block_id, opts))
+        if from_ufs:
+            ctx.worker.cache_blocks_from_ufs(from_ufs)
+            loaded += sum(o.block_size for b, o in from_ufs if ctx.worker.has_block(b))
         return loaded
 
     def join(self, cfg, task_results):

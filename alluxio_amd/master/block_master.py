@@ -283,15 +283,23 @@ class BlockMaster(Journaled):
             ctx.close()
 
     def commit_block_in_ufs(self, block_id: int, length: int) -> None:
+        self.commit_blocks_in_ufs([(block_id, length)])
+
+    def commit_blocks_in_ufs(self, blocks) -> None:
+        """Record (block id, length) pairs as stored in the UFS only: one journal context (one
+        flush) for the whole batch (a metadata load of a big directory)."""
         ctx = None
         with self._lock:
-            if block_id in self._blocks:
-                return
-            e = pb.journal.JournalEntry(block_info=pb.journal.BlockInfoEntry(block_id=block_id, length=length))
-            self.process_journal_entry(e)
-            ctx = self._ctx()
-            ctx.append(e)
-        ctx.close()
+            for block_id, length in blocks:
+                if block_id in self._blocks:
+                    continue
+                e = pb.journal.JournalEntry(block_info=pb.journal.BlockInfoEntry(block_id=block_id, length=length))
+                self.process_journal_entry(e)
+                if ctx is None:
+                    ctx = self._ctx()
+                ctx.append(e)
+        if ctx is not None:
+            ctx.close()
 
     def remove_blocks(self, block_ids, delete: bool) -> None:
         """Remove replicas on workers; with ``delete`` also forget the block (journaled)."""

@@ -939,7 +939,9 @@ class FileSystemMaster(Journaled):
         if st is None:
             raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
         owner_default, group_default = self._owner_group()
+        ufs_blocks: list = []
         with RpcContext(self) as rpc, self.tree.lock.write():
+            rpc.ufs_blocks = ufs_blocks     # block-master commits of the loaded files, batched
             chain, missing = self.tree.resolve(path)
             if missing:
                 if len(missing) > 1 and not create_ancestors:
@@ -957,6 +959,8 @@ class FileSystemMaster(Journaled):
             inode = self.tree.get(path)
             if inode.is_directory:
                 self._load_children(rpc, inode, path, recursive, owner_default, group_default)
+        if ufs_blocks:
+            self.block_master.commit_blocks_in_ufs(ufs_blocks)
 
     def _load_one(self, rpc, parent, name, st, res, owner_default, group_default) -> None:
         owner = st.owner or owner_default
@@ -972,9 +976,13 @@ class FileSystemMaster(Journaled):
         length = st.content_length
         blocks = []
         rem, seq = length, 0
+        batch = getattr(rpc, "ufs_blocks", None)
         while rem > 0:
             blocks.append(ids.create_block_id(ids.get_container_id(fid), seq))
-            self.block_master.commit_block_in_ufs(blocks[-1], min(rem, bs))
+            if batch is not None:
+                batch.append((blocks[-1], min(rem, bs)))
+            else:
+                self.block_master.commit_block_in_ufs(blocks[-1], min(rem, bs))
             rem -= min(rem, bs)
             seq += 1
         from ..underfs.base import Fingerprint as FP

@@ -70,6 +70,40 @@ class FixedRecordDataset:
         return self._view(out)
 
 
+class FileListDataset(FixedRecordDataset):
+    """One record per file of a directory (BASELINE config 4: ImageNet-shaped 128 KB files), with
+    the metadata of every file from ONE ``listStatus`` (batched metadata: no per-file getStatus;
+    the FileInfos carry their block ids and locations).  Files longer than ``record_bytes`` are
+    truncated, shorter ones zero-padded (``lengths`` keeps the true sizes)."""
+
+    def __init__(self, fs, directory: str, record_bytes: int | None = None, dtype="uint8", shape=None,
+                 device=None):
+        import torch
+        self.fs = fs
+        self.dtype = getattr(torch, str(dtype)) if isinstance(dtype, str) else dtype
+        self.shape = tuple(shape) if shape else None
+        self.device = device
+        sts = sorted((s for s in fs.list_status(directory) if not s.is_folder), key=lambda s: s.path)
+        self.paths = [s.path for s in sts]
+        self.lengths = np.array([s.length for s in sts], dtype=np.uint64)
+        self.record_bytes = int(record_bytes or (self.lengths.max() if len(sts) else 0))
+        self.files = [_FileLayout(s) for s in sts]
+        self.counts = [1] * len(sts)
+        self.starts = np.arange(len(sts) + 1)
+        # single-block records: the gather plan is a vector op over these arrays
+        self.single_block = all(len(f.blocks) == 1 for f in self.files) and \
+            all(f.block_size >= self.record_bytes for f in self.files)
+        self.block_ids = np.array([f.blocks[0].blockId if f.blocks else -1 for f in self.files], dtype=np.int64)
+        self.read_lengths = np.minimum(self.lengths, np.uint64(self.record_bytes))
+
+    def locate(self, idx: int) -> tuple[int, int]:
+        if idx < 0:
+            idx += len(self)
+        if not 0 <= idx < len(self):
+            raise IndexError(idx)
+        return idx, 0
+
+
 class DeviceBatchLoader:
     """Iterates ``[batch, *shape]`` device tensors of records gathered by one kernel per batch."""
 
@@ -148,6 +182,7 @@ class DeviceBatchLoader:
                 pass
         self._locks = []
         self._sources = None
+        self._one_worker = False
 
     # ---- planning -----------------------------------------------------------------------------
     def _pieces(self, rec_idx: int):
@@ -163,8 +198,33 @@ class DeviceBatchLoader:
             done += take
         return out
 
+    def _single_worker(self):
+        """The in-process worker holding every block of a single-block-record dataset (then the
+        batch plan is pure array arithmetic + one ``read_batch_arrays``), else None."""
+        if not getattr(self.ds, "single_block", False):
+            return None
+        if getattr(self, "_one_worker", False) is not False:
+            return self._one_worker
+        srcs = self._open_sources()
+        ws = {id(o): o for how, o in srcs.values() if how == "local"}
+        self._one_worker = next(iter(ws.values())) if len(ws) == 1 and \
+            all(how == "local" for how, _ in srcs.values()) else None
+        return self._one_worker
+
     def _fill(self, out, indices):
         """Gather records ``indices`` into rows of ``out`` (uint8 [B, record_bytes])."""
+        w = self._single_worker()
+        if w is not None:
+            ix = np.asarray(indices, dtype=np.int64)
+            lens = self.ds.read_lengths[ix]
+            if (lens < self.ds.record_bytes).any():
+                out.zero_()                # pad short files
+            dsts = np.uint64(out.data_ptr()) + np.arange(len(ix), dtype=np.uint64) * np.uint64(self.ds.record_bytes)
+            stream = int(self.stream.cuda_stream) if self.stream is not None else 0
+            w.native.read_batch_arrays(self.ds.block_ids[ix], np.zeros(len(ix), dtype=np.uint64), lens, dsts,
+                                       1 if out.is_cuda else 0, stream, not out.is_cuda)
+            w._count_read(int(lens.sum()), 1 if out.is_cuda else 0)
+            return
         srcs = self._open_sources()
         kind = 1 if out.is_cuda else 0
         row = self.ds.record_bytes

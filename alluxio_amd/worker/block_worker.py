@@ -19,7 +19,7 @@ import time
 from concurrent.futures import ThreadPoolExecutor
 
 from .. import metrics as msys
-from ..ops.native import native_errors
+from ..ops.native import has_gpu, native_errors
 from ..proto import pb
 from ..utils import ids
 from ..rpc import marshal
@@ -75,6 +75,9 @@ class BlockWorker:
         self._staging = None
         self._staging_lock = threading.Lock()
         self._ingest = None   # K3 pipelines (worker/ingest.py), created on first UFS caching
+        self._bulk_buf = None  # pinned staging of the bulk small-file ingest
+        self._bulk_lock = threading.Lock()
+        self._bulk_threads = conf.get_int("alluxio.worker.ufs.ingest.bulk.threads", "16")
         self.pinned_files: set[int] = set()
         self.persisted_files: list[int] = []
         self._block_master = None
@@ -204,21 +207,8 @@ class BlockWorker:
     def commit_block(self, session_id: int, block_id: int, pin: bool = False) -> None:
         with native_errors():
             self.native.commit_block(session_id, block_id, pin)
-            info = self.native.block_info(block_id)
-        if self.crc_enabled or (self.crc_device and info.medium == "HBM"):
-            with native_errors():
-                # (piece bytes, CRC per piece): the piece is the page size of the dir it was
-                # computed in; a block moved to a dir with another page size keeps its CRCs
-                self.crc[block_id] = (self.native.block_pages(block_id)[2], self.native.checksum(block_id, 0))
-            self.metrics.counter("Crc32cBytes").inc(info.length)
-        bm = self._bm()
-        if bm is not None and self.worker_id != ids.INVALID_WORKER_ID:
-            used = self.store.used_by_tier().get(info.tier_alias, 0)
-            bm.CommitBlock(pb.block.CommitBlockPRequest(
-                workerId=self.worker_id, usedBytesOnTier=used, tierAlias=info.tier_alias, blockId=block_id,
-                length=info.length, mediumType=info.medium))
         # the commit's added-event is reported by CommitBlock already
-        self.metrics.counter("BlocksCommitted").inc()
+        self._report_commit(block_id)
 
     def verify_block_crc(self, block_id: int, src_crcs: list[int], src_piece: int) -> None:
         """Compare the block's bytes against CRC32Cs of ``src_piece``-byte pieces computed by its
@@ -420,6 +410,72 @@ class BlockWorker:
             raise
         finally:
             pool.release(pipe)
+
+    def cache_blocks_from_ufs(self, items, session_id: int | None = None) -> int:
+        """Bulk form of :meth:`cache_block_from_ufs` for many small blocks (``items`` =
+        [(block id, OpenUfsBlockOptions)]): blocks of a local UFS are read by the native store's
+        thread pool straight into a pinned staging buffer and copied into HBM in batches
+        (BlockStore::ingest_files), one Python call for the lot; other UFSes take the per-block
+        pipeline.  Returns the number of blocks newly cached."""
+        from ..underfs.local import LocalUnderFileSystem, strip_scheme
+        from .ufs_fallback import resolve_ufs_block_opts
+        session_id = session_id if session_id is not None else ids.CACHE_UFS_SESSION_ID
+        native_ids, paths, offs, lens, slow = [], [], [], [], []
+        for bid, opts in items:
+            opts = resolve_ufs_block_opts(self, bid, opts)
+            if isinstance(self._ufs_for(opts), LocalUnderFileSystem) and opts.block_size > 0:
+                native_ids.append(bid)
+                paths.append(strip_scheme(opts.ufs_path))
+                offs.append(opts.offset_in_file)
+                lens.append(opts.block_size)
+            else:
+                slow.append((bid, opts))
+        done = 0
+        if native_ids:
+            staging, sbytes = self._bulk_staging(max(lens))
+            t0 = time.perf_counter()
+            with self._bulk_lock, native_errors():
+                status = self.native.ingest_files(session_id, native_ids, paths, offs, lens, staging.data_ptr(),
+                                                  sbytes, self._bulk_threads, 0)
+            self.metrics.timer("UfsIngestBulk").update(time.perf_counter() - t0)
+            for bid, st, n in zip(native_ids, status, lens):
+                if st == 0:
+                    done += 1
+                    self.metrics.counter("BytesReadUfsAll").inc(n)
+                    self.metrics.counter("UfsIngestBytes").inc(n)
+                    self._report_commit(bid)
+                elif st == 2:
+                    LOG.warning("bulk cache: UFS read of block %d failed", bid)
+                elif st == 3:
+                    slow.append((bid, None))      # no space in one go: leave it to the slow path below
+        for bid, opts in slow:
+            if opts is None:
+                continue
+            try:
+                done += bool(self.cache_block_from_ufs(bid, opts, session_id))
+            except Exception:  # noqa: BLE001
+                LOG.debug("cache of block %d failed", bid, exc_info=True)
+        return done
+
+    def _bulk_staging(self, min_item: int):
+        import torch
+        want = max(self.conf.get_bytes("alluxio.worker.ufs.ingest.bulk.staging.size", "64MB"), 2 * min_item)
+        with self._staging_lock:
+            if self._bulk_buf is None or self._bulk_buf.numel() < want:
+                self._bulk_buf = torch.empty(want, dtype=torch.uint8, pin_memory=has_gpu())
+            return self._bulk_buf, self._bulk_buf.numel()
+
+    def _report_commit(self, block_id: int) -> None:
+        """Tell the master about a block committed by the native store (CommitBlock)."""
+        info = self.native.block_info(block_id)
+        if self.crc_enabled or (self.crc_device and info.medium == "HBM"):
+            self.crc[block_id] = (self.native.block_pages(block_id)[2], self.native.checksum(block_id, 0))
+        bm = self._bm()
+        if bm is not None and self.worker_id != ids.INVALID_WORKER_ID:
+            bm.CommitBlock(pb.block.CommitBlockPRequest(
+                workerId=self.worker_id, usedBytesOnTier=self.store.used_by_tier().get(info.tier_alias, 0),
+                tierAlias=info.tier_alias, blockId=block_id, length=info.length, mediumType=info.medium))
+        self.metrics.counter("BlocksCommitted").inc()
 
     def async_cache(self, block_id: int, opts=None, source=None, length: int | None = None) -> bool:
         """Deduplicated background caching; returns False if already queued/cached."""

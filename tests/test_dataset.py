@@ -51,3 +51,37 @@ def test_loader_cpu():
 def test_loader_gpu(gpu):
     with _cluster("hbm:0") as c:
         _check(c, "cuda")
+
+
+def test_file_list_dataset_one_listing(tmp_path):
+    """Config-4 shape: one record per file, metadata from one listStatus, batches gathered by one
+    array-planned read per batch (short files zero-padded)."""
+    import numpy as np
+    import torch
+
+    from alluxio_amd.minicluster import LocalAlluxioCluster
+    from alluxio_amd.models.dataset import DeviceBatchLoader, FileListDataset
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram",
+                                                   "alluxio.user.block.size.bytes.default": "1MB"}) as c:
+        fs = c.client()
+        rng = np.random.default_rng(0)
+        files = {}
+        for i in range(40):
+            n = 4096 if i % 7 else 1000          # a few short files
+            files[i] = rng.integers(0, 256, n, dtype=np.uint8)
+            fs.write_file(f"/img/{i:05d}", files[i], write_type="MUST_CACHE")
+        ds = FileListDataset(fs, "/img", record_bytes=4096)
+        assert len(ds) == 40 and ds.single_block
+        seen = 0
+        with DeviceBatchLoader(ds, batch_size=16, shuffle=True, seed=3, device="cpu") as dl:
+            order = np.random.default_rng(3).permutation(40)
+            for b, batch in enumerate(dl):
+                for r in range(batch.shape[0]):
+                    i = int(order[b * 16 + r])
+                    want = np.zeros(4096, dtype=np.uint8)
+                    want[:len(files[i])] = files[i]
+                    assert np.array_equal(batch[r].numpy(), want)
+                    seen += 1
+            assert dl._one_worker is not None
+        assert seen == 40
+        fs.close()

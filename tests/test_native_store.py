@@ -257,3 +257,33 @@ def test_eviction_demotes_to_lower_tier(tmp_path):
     ids_ = set(s.block_ids(-1))
     assert len([b for b in ids_ if s.block_info(b).tier_alias == "SSD"]) <= 3
     assert {404, 405, 406, 407} <= ids_ and 401 not in ids_   # the coldest SSD block was dropped
+
+
+def test_ingest_files_bulk(tmp_path):
+    """BlockStore::ingest_files: parallel preads into a double-buffered staging buffer, batched
+    copies into temp blocks, commits; existing blocks, unreadable files and short files get their
+    own status and leave no temp block."""
+    s = _store(tmp_path, mem_mb=8, page=64 * 1024)
+    rng = np.random.default_rng(3)
+    files, datas = [], []
+    for i in range(40):
+        d = rng.integers(0, 256, 1000 + 997 * i, dtype=np.uint8)
+        p = tmp_path / f"f{i}"
+        p.write_bytes(b"xx" + d.tobytes())          # 2-byte header: the block starts at offset 2
+        files.append(str(p))
+        datas.append(d)
+    _put(s, 105, datas[5])                          # already cached
+    ids = [100 + i for i in range(40)] + [200, 201]
+    paths = files + [str(tmp_path / "missing"), files[0]]
+    offs = [2] * 40 + [0, 2]
+    lens = [d.nbytes for d in datas] + [10, datas[0].nbytes + 5]   # 201 asks past the end of file
+    staging = np.zeros(256 * 1024, dtype=np.uint8)  # several groups per half
+    st = s.ingest_files(7, ids, paths, offs, lens, staging.ctypes.data, staging.nbytes, threads=4)
+    assert st[5] == 1 and st[40] == 2 and st[41] == 2
+    assert all(st[i] == 0 for i in range(40) if i != 5)
+    for i in range(40):
+        assert np.array_equal(_get(s, 100 + i), datas[i])
+    assert not s.has_block(200) and not s.has_temp_block(200)
+    assert not s.has_block(201) and not s.has_temp_block(201)
+    with pytest.raises(Exception):                  # a file bigger than half the staging buffer
+        s.ingest_files(7, [300], [files[0]], [0], [200 * 1024], staging.ctypes.data, staging.nbytes)
