@@ -323,6 +323,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("device") = true)
       .def("annotator_keys", &BlockStore::annotator_keys, G())
       .def("dir_mgmt_available", &BlockStore::dir_mgmt_available, G())
+      .def("checksum_blocks", &BlockStore::checksum_blocks, G(), py::arg("block_ids"),
+           py::arg("device_only") = false)
       .def("ingest_files", &BlockStore::ingest_files, G(), py::arg("session"), py::arg("block_ids"),
            py::arg("paths"), py::arg("offsets"), py::arg("lengths"), py::arg("staging"), py::arg("staging_bytes"),
            py::arg("threads") = 8, py::arg("stream") = 0)

@@ -1025,6 +1025,73 @@ std::vector<uint32_t> BlockStore::checksum(int64_t block_id, uint64_t piece_byte
   return out;
 }
 
+std::vector<std::pair<uint64_t, std::vector<uint32_t>>> BlockStore::checksum_blocks(
+    const std::vector<int64_t>& ids, bool device_only) {
+  set_device();
+  std::vector<std::pair<uint64_t, std::vector<uint32_t>>> out(ids.size());
+  std::vector<uint64_t> ptrs;
+  std::vector<uint32_t> lens;
+  std::vector<std::pair<size_t, size_t>> where;   // (index into ids, first piece) of gathered blocks
+  std::vector<size_t> slow;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (size_t i = 0; i < ids.size(); ++i) {
+      BlockMeta* b = find(ids[i]);
+      if (!b) continue;
+      const StorageDir& d = *dirs_[b->dir];
+      if (d.spec.kind != DirKind::kDevice || d.spec.page_size > crc32c_gather_max_piece()) {
+        if (!device_only || d.spec.kind == DirKind::kDevice) slow.push_back(i);
+        continue;
+      }
+      where.emplace_back(i, ptrs.size());
+      const uint64_t ps = d.spec.page_size;
+      for (uint64_t off = 0, k = 0; off < b->length; off += ps, ++k) {
+        ptrs.push_back(d.spec.base + (uint64_t)b->pages[k] * ps);
+        lens.push_back((uint32_t)std::min(ps, b->length - off));
+      }
+      out[i].first = ps;
+      out[i].second.resize(ceil_div(b->length, ps));
+    }
+  }
+  if (!ptrs.empty()) {
+    std::lock_guard<std::mutex> g(ev_mu_);
+    const size_t n = ptrs.size();
+    // device scratch: pointers (2 words each), lengths, results
+    const size_t need = 4 * n + 64;
+    if (crc_cap_ < need) {
+      if (crc_dev_) hipFree(crc_dev_);
+      crc_dev_ = nullptr;
+      HIP_OK(hipMalloc((void**)&crc_dev_, need * sizeof(uint32_t)));
+      crc_cap_ = need;
+    }
+    uint64_t* dptr = reinterpret_cast<uint64_t*>(crc_dev_);
+    uint32_t* dlen = crc_dev_ + 2 * n;
+    uint32_t* dout = crc_dev_ + 3 * n;
+    HIP_OK(hipMemcpyAsync(dptr, ptrs.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, internal_stream_));
+    HIP_OK(hipMemcpyAsync(dlen, lens.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, internal_stream_));
+    HIP_OK(launch_crc32c_gather(dptr, dlen, n, dout, internal_stream_));
+    std::vector<uint32_t> res(n);
+    HIP_OK(hipMemcpyAsync(res.data(), dout, n * sizeof(uint32_t), hipMemcpyDeviceToHost, internal_stream_));
+    HIP_OK(hipStreamSynchronize(internal_stream_));
+    for (auto& [i, first] : where)
+      std::copy(res.begin() + first, res.begin() + first + out[i].second.size(), out[i].second.begin());
+  }
+  for (size_t i : slow) {
+    try {
+      out[i].second = checksum(ids[i], 0);
+      std::lock_guard<std::mutex> lk(mu_);
+      BlockMeta* b = find(ids[i]);
+      if (b) {
+        const StorageDir& d = *dirs_[b->dir];
+        out[i].first = d.spec.kind == DirKind::kFile ? (2ull << 20) : d.spec.page_size;
+      }
+    } catch (const StoreError&) {
+      out[i] = {0, {}};   // removed meanwhile
+    }
+  }
+  return out;
+}
+
 void BlockStore::fill_pattern(int64_t session, int64_t block_id, uint64_t length, uint64_t seed) {
   set_device();
   BlockMeta snap;

@@ -198,6 +198,11 @@ class BlockStore {
   int64_t try_lock_block(int64_t session, int64_t block_id, bool write);
   // CRC32C per piece (piece = page size when 0).
   std::vector<uint32_t> checksum(int64_t block_id, uint64_t piece_bytes);
+  // Per-page CRC32C of many blocks: the pages of HBM blocks go to one gather launch (pages up
+  // to 256 KiB), others take checksum() (or are skipped with device_only).  Returns (piece bytes,
+  // CRCs) per block; missing / skipped blocks get (0, []).
+  std::vector<std::pair<uint64_t, std::vector<uint32_t>>> checksum_blocks(const std::vector<int64_t>& block_ids,
+                                                                          bool device_only = false);
   void fill_pattern(int64_t session, int64_t block_id, uint64_t length, uint64_t seed);
 
   // ---- eviction ---------------------------------------------------------------------------

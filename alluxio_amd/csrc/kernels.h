@@ -63,6 +63,11 @@ void set_seq_read_variant(int variant, unsigned grid_cap);
 hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint64_t piece_bytes,
                                 uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
                                 hipStream_t stream);
+// Standard CRC32C of n gathered pieces (device pointers/lengths in device memory, each piece
+// <= crc32c_gather_max_piece() bytes), one workgroup per piece.
+hipError_t launch_crc32c_gather(const uint64_t* ptrs, const uint32_t* lens, uint64_t n, uint32_t* out,
+                                hipStream_t stream);
+uint64_t crc32c_gather_max_piece();
 // 0: per-lane contiguous strips, 1 (default): interleaved coalesced lanes.
 void set_crc_variant(int v);
 // Scratch words needed by launch_crc32c_pieces (an upper bound for every variant).

@@ -413,6 +413,63 @@ __global__ __launch_bounds__(kCrcThreads) void crc32c_segments_kernel(
 // in by lane 0.  Produces the same raw (zero-init) segment CRC as v1.
 constexpr uint64_t kCrcSeg2 = 256 * 1024;
 
+// One segment's raw CRC with the v2 schedule; the result is valid in thread 0.
+__device__ __forceinline__ uint32_t seg_crc_v2(const uint8_t* __restrict__ seg, uint64_t seg_len,
+                                               const uint32_t (*t16)[256], const uint32_t (*sh)[256],
+                                               uint32_t* part, int tid) {
+  const uint64_t nwords = seg_len >> 4;
+  uint32_t c = 0;
+  uint64_t last = ~0ull;
+  if ((((uintptr_t)seg) & 15) == 0) {
+    for (uint64_t wi = tid; wi < nwords; wi += kCrcThreads) {
+      const uint4 v = *reinterpret_cast<const uint4*>(seg + (wi << 4));
+      const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+      const uint32_t w = t16[15][v.x & 255] ^ t16[14][(v.x >> 8) & 255] ^ t16[13][(v.x >> 16) & 255] ^
+                         t16[12][v.x >> 24] ^ t16[11][v.y & 255] ^ t16[10][(v.y >> 8) & 255] ^
+                         t16[9][(v.y >> 16) & 255] ^ t16[8][v.y >> 24] ^ t16[7][v.z & 255] ^
+                         t16[6][(v.z >> 8) & 255] ^ t16[5][(v.z >> 16) & 255] ^ t16[4][v.z >> 24] ^
+                         t16[3][v.w & 255] ^ t16[2][(v.w >> 8) & 255] ^ t16[1][(v.w >> 16) & 255] ^
+                         t16[0][v.w >> 24];
+      c = (wi < (uint64_t)kCrcThreads ? 0u : s) ^ w;
+      last = wi;
+    }
+  } else {
+    // unaligned segment: same schedule with byte loads
+    for (uint64_t wi = tid; wi < nwords; wi += kCrcThreads) {
+      const uint8_t* q = seg + (wi << 4);
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) w ^= t16[15 - b][q[b]];
+      const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+      c = (wi < (uint64_t)kCrcThreads ? 0u : s) ^ w;
+      last = wi;
+    }
+  }
+  // move the lane's contribution to its position: bytes after its last word inside the words area
+  uint32_t contrib = 0;
+  if (last != ~0ull) contrib = gf2_mult(xpow8n((nwords - 1 - last) << 4), c);
+  part[tid] = contrib;
+  __syncthreads();
+  for (int s2 = kCrcThreads / 2; s2 > 0; s2 >>= 1) {
+    if (tid < s2) part[tid] ^= part[tid + s2];
+    __syncthreads();
+  }
+  uint32_t acc = 0;
+  if (tid == 0) {
+    acc = part[0];
+    const uint64_t tail = seg_len & 15;
+    if (tail) {
+      acc = gf2_mult(xpow8n(tail), acc);
+      uint32_t t = 0;
+      const uint8_t* q = seg + (nwords << 4);
+      for (uint64_t b = 0; b < tail; ++b) t = (t >> 8) ^ t16[0][(t ^ q[b]) & 255];
+      acc ^= t;
+    }
+  }
+  __syncthreads();
+  return acc;
+}
+
 __global__ __launch_bounds__(kCrcThreads) void crc32c_segments_v2_kernel(
     const uint8_t* __restrict__ base, uint64_t total_bytes, uint64_t piece_bytes, uint64_t seg_bytes,
     uint64_t segs_per_piece, uint64_t nsegs, uint32_t* __restrict__ seg_crc) {
@@ -430,59 +487,42 @@ __global__ __launch_bounds__(kCrcThreads) void crc32c_segments_v2_kernel(
     const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
     const uint64_t seg_start = piece_start + seg_in_piece * seg_bytes;
     const uint64_t seg_len = std::min(seg_bytes, piece_start + piece_len - seg_start);
-    const uint8_t* seg = base + seg_start;
-    const uint64_t nwords = seg_len >> 4;
-    uint32_t c = 0;
-    uint64_t last = ~0ull;
-    if ((((uintptr_t)seg) & 15) == 0) {
-      for (uint64_t wi = tid; wi < nwords; wi += kCrcThreads) {
-        const uint4 v = *reinterpret_cast<const uint4*>(seg + (wi << 4));
-        const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
-        const uint32_t w = t16[15][v.x & 255] ^ t16[14][(v.x >> 8) & 255] ^ t16[13][(v.x >> 16) & 255] ^
-                           t16[12][v.x >> 24] ^ t16[11][v.y & 255] ^ t16[10][(v.y >> 8) & 255] ^
-                           t16[9][(v.y >> 16) & 255] ^ t16[8][v.y >> 24] ^ t16[7][v.z & 255] ^
-                           t16[6][(v.z >> 8) & 255] ^ t16[5][(v.z >> 16) & 255] ^ t16[4][v.z >> 24] ^
-                           t16[3][v.w & 255] ^ t16[2][(v.w >> 8) & 255] ^ t16[1][(v.w >> 16) & 255] ^
-                           t16[0][v.w >> 24];
-        c = (wi < (uint64_t)kCrcThreads ? 0u : s) ^ w;
-        last = wi;
-      }
-    } else {
-      // unaligned segment: same schedule with byte loads
-      for (uint64_t wi = tid; wi < nwords; wi += kCrcThreads) {
-        const uint8_t* q = seg + (wi << 4);
-        uint32_t w = 0;
-#pragma unroll
-        for (int b = 0; b < 16; ++b) w ^= t16[15 - b][q[b]];
-        const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
-        c = (wi < (uint64_t)kCrcThreads ? 0u : s) ^ w;
-        last = wi;
-      }
-    }
-    // move the lane's contribution to its position: bytes after its last word inside the words area
-    uint32_t contrib = 0;
-    if (last != ~0ull) contrib = gf2_mult(xpow8n((nwords - 1 - last) << 4), c);
-    part[tid] = contrib;
-    __syncthreads();
-    for (int s2 = kCrcThreads / 2; s2 > 0; s2 >>= 1) {
-      if (tid < s2) part[tid] ^= part[tid + s2];
-      __syncthreads();
-    }
-    if (tid == 0) {
-      uint32_t acc = part[0];
-      const uint64_t tail = seg_len & 15;
-      if (tail) {
-        acc = gf2_mult(xpow8n(tail), acc);
-        uint32_t t = 0;
-        const uint8_t* q = seg + (nwords << 4);
-        for (uint64_t b = 0; b < tail; ++b) t = (t >> 8) ^ t16[0][(t ^ q[b]) & 255];
-        acc ^= t;
-      }
-      seg_crc[g] = acc;
-    }
-    __syncthreads();
+    const uint32_t acc = seg_crc_v2(base + seg_start, seg_len, t16, sh, part, tid);
+    if (tid == 0) seg_crc[g] = acc;
   }
 }
+
+// Gathered pieces (one page of many blocks each, <= kCrcSeg2 bytes): one workgroup per piece,
+// standard CRC32C per piece — the per-page CRCs of a whole batch of freshly cached blocks in
+// one launch instead of one launch + sync per block.
+__global__ __launch_bounds__(kCrcThreads) void crc32c_gather_kernel(
+    const uint64_t* __restrict__ ptrs, const uint32_t* __restrict__ lens, uint64_t n,
+    uint32_t* __restrict__ out) {
+  __shared__ uint32_t t16[16][256];
+  __shared__ uint32_t sh[4][256];
+  __shared__ uint32_t part[kCrcThreads];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 16 * 256; i += kCrcThreads) t16[i >> 8][i & 255] = c_crc16[i >> 8][i & 255];
+  for (int i = tid; i < 4 * 256; i += kCrcThreads) sh[i >> 8][i & 255] = c_shift4k[i >> 8][i & 255];
+  __syncthreads();
+  for (uint64_t g = blockIdx.x; g < n; g += gridDim.x) {
+    const uint64_t len = lens[g];
+    const uint32_t acc = seg_crc_v2(reinterpret_cast<const uint8_t*>(ptrs[g]), len, t16, sh, part, tid);
+    if (tid == 0) out[g] = acc ^ gf2_mult(xpow8n(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+  }
+}
+
+hipError_t launch_crc32c_gather(const uint64_t* ptrs, const uint32_t* lens, uint64_t n, uint32_t* out,
+                                hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipError_t e = ensure_crc_tables();
+  if (e != hipSuccess) return e;
+  const unsigned g = (unsigned)std::min<uint64_t>(n, 8192);
+  hipLaunchKernelGGL(crc32c_gather_kernel, dim3(g), dim3(kCrcThreads), 0, stream, ptrs, lens, n, out);
+  return hipGetLastError();
+}
+
+uint64_t crc32c_gather_max_piece() { return kCrcSeg2; }
 
 __global__ __launch_bounds__(kCrcThreads) void crc32c_pieces_kernel(
     const uint32_t* __restrict__ seg_crc, uint64_t total_bytes, uint64_t piece_bytes, uint64_t seg_bytes,

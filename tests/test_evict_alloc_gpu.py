@@ -192,3 +192,37 @@ def test_tier_order_device_matches_host(gpu):
             assert len(dev) == 100 and dev == host, (tier, hottest)
     keys = s.annotator_keys(s.tier_order(1, 10, True, True))
     assert keys == sorted(keys, reverse=True)
+
+
+def test_bulk_ingest_into_hbm_and_gathered_crc(gpu, tmp_path):
+    """BlockStore::ingest_files into an HBM dir (pinned staging halves, async H2D) round-trips the
+    file bytes; checksum_blocks' single gathered CRC launch equals per-block checksum() and the
+    host CRC32C of every page."""
+    import torch
+    C = lib()
+    page = 128 * KB
+    s = _device_store(2048, page)
+    rng = np.random.default_rng(4)
+    paths, lens, datas = [], [], []
+    for i in range(300):
+        n = int(rng.integers(1, 3 * page))
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        p = tmp_path / f"f{i}"
+        p.write_bytes(d.tobytes())
+        paths.append(str(p))
+        lens.append(n)
+        datas.append(d)
+    ids = list(range(1000, 1300))
+    staging = torch.empty(8 << 20, dtype=torch.uint8, pin_memory=True)
+    st = s.ingest_files(5, ids, paths, [0] * 300, lens, staging.data_ptr(), staging.numel(), 8, 0)
+    assert st == [0] * 300
+    out = torch.empty(3 * page, dtype=torch.uint8, device="cuda")
+    for b, d in zip(ids[::37], datas[::37]):
+        s.read_batch([(b, 0, d.nbytes, out.data_ptr(), 1)], 0, True)
+        assert np.array_equal(out[:d.nbytes].cpu().numpy(), d)
+    crcs = s.checksum_blocks(ids + [999999])
+    assert crcs[-1] == (0, [])
+    assert all(c[0] == page for c in crcs[:-1])
+    for b, d, (_, c) in zip(ids, datas, crcs):
+        assert c == s.checksum(b, 0)
+        assert c == [C.crc32c(d[o:o + page].tobytes()) for o in range(0, d.nbytes, page)]

@@ -287,3 +287,5 @@ def test_ingest_files_bulk(tmp_path):
     assert not s.has_block(201) and not s.has_temp_block(201)
     with pytest.raises(Exception):                  # a file bigger than half the staging buffer
         s.ingest_files(7, [300], [files[0]], [0], [200 * 1024], staging.ctypes.data, staging.nbytes)
+    assert s.checksum_blocks([100, 101, 200]) == [(64 * 1024, s.checksum(100, 0)), (64 * 1024, s.checksum(101, 0)), (0, [])]
+    assert s.checksum_blocks([100], True) == [(0, [])]        # device_only skips host dirs

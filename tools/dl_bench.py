@@ -90,6 +90,7 @@ def main():
             res["cache_all_done"] = cached == a.files
             res["cache_files_per_s"] = round(a.files / el, 1)
             res["cache_GBps"] = round(total / el / 1e9, 3)
+            res["cache_breakdown_s"] = {k: round(v, 3) for k, v in w.bulk_stats.items()}
             ds = FileListDataset(fs, "/imagenet", record_bytes=a.file_size)
             res["cached_fraction"] = round(float(np.mean([bool(f.blocks[0].locations) for f in ds.files])), 4)
             # training epochs: shuffled batches gathered on the device
