@@ -99,6 +99,7 @@ BlockStore::~BlockStore() {
       if (ring_ev_[i]) hipEventDestroy(ring_ev_[i]);
     if (host_ring_) hipHostFree(host_ring_);
     if (dev_ring_) hipFree(dev_ring_);
+    if (ingest_dev_) hipFree(ingest_dev_);
     for (int i = 0; i < 2; ++i) {
       if (upd_ev_[i]) hipEventDestroy(upd_ev_[i]);
       if (h_upd_[i]) hipHostFree(h_upd_[i]);
@@ -1969,14 +1970,48 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
     for (int t = 1; t < nt; ++t) pool.emplace_back(reader);
     reader();
     for (auto& t : pool) t.join();
-    // 3) copies into the blocks (async); commit once the half's copies are done
-    for (size_t k = 0; k < gix.size(); ++k) {
-      const size_t i = gix[k];
-      if (status[i] == 3 || status[i] == 1) continue;
-      if (status[i] == 2) {
-        try { abort_block(session, ids[i]); } catch (const StoreError&) {}
-        continue;
+    // 3) copies into the blocks (async); commit once the half's copies are done.  Blocks in an
+    // HBM dir: the used span of the half goes up in ONE DMA to a device staging buffer and one
+    // batched-copy launch scatters it into the blocks' pages (one 128 KiB DMA per block runs
+    // at ~13 GB/s; the single large DMA at full link rate).
+    std::vector<size_t> dev_items, host_items;
+    {
+      std::lock_guard<std::mutex> g2(mu_);
+      for (size_t k = 0; k < gix.size(); ++k) {
+        const size_t i = gix[k];
+        if (status[i] != 0) continue;
+        BlockMeta* b = find(ids[i]);
+        const bool dev = b && has_device_ && dirs_[b->dir]->spec.kind == DirKind::kDevice && b->reserved >= lengths[i];
+        (dev ? dev_items : host_items).push_back(i);
       }
+    }
+    for (size_t k = 0; k < gix.size(); ++k)
+      if (status[gix[k]] == 2) {
+        try { abort_block(session, ids[gix[k]]); } catch (const StoreError&) {}
+      }
+    if (!dev_items.empty()) {
+      if (ingest_dev_cap_ < staging_bytes) {
+        HIP_OK(hipStreamSynchronize(st));
+        if (ingest_dev_) hipFree(ingest_dev_);
+        ingest_dev_ = nullptr;
+        HIP_OK(hipMalloc(&ingest_dev_, staging_bytes));
+        ingest_dev_cap_ = staging_bytes;
+      }
+      uint8_t* dbase = reinterpret_cast<uint8_t*>(ingest_dev_) + h * half;
+      HIP_OK(hipMemcpyAsync(dbase, base, off, hipMemcpyHostToDevice, st));
+      std::vector<CopySeg> segs;
+      {
+        std::lock_guard<std::mutex> g2(mu_);
+        for (size_t i : dev_items) {
+          BlockMeta* b = find(ids[i]);
+          b->length = std::max(b->length, lengths[i]);
+          plan_block_range(*b, 0, lengths[i], (uint64_t)(dbase + at[i - lo]), (int)MemKind::kDevice, true, segs, st);
+          pending[h].push_back(ids[i]);
+        }
+      }
+      if (!segs.empty()) copy_segments(segs, st);
+    }
+    for (size_t i : host_items) {
       try {
         write(session, ids[i], 0, (uint64_t)(base + at[i - lo]), lengths[i], (int)MemKind::kHost, stream, false);
         pending[h].push_back(ids[i]);

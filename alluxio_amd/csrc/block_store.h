@@ -377,6 +377,9 @@ class BlockStore {
   // checksum scratch
   uint32_t* crc_dev_ = nullptr;
   size_t crc_cap_ = 0;
+  // device staging of ingest_files (mirror of the caller's pinned staging)
+  void* ingest_dev_ = nullptr;
+  uint64_t ingest_dev_cap_ = 0;
 };
 
 // Many concurrent sequential readers of one file, advanced in lockstep: the native form of
