@@ -173,6 +173,9 @@ _k("WORKER_UFS_INGEST_CHUNK_SIZE", "alluxio.worker.ufs.ingest.chunk.size", "8MB"
    "UFS read size of the UFS->HBM ingest pipeline (one pinned staging buffer each).")
 _k("WORKER_UFS_INGEST_DEPTH", "alluxio.worker.ufs.ingest.depth", "3", Scope.WORKER,
    "Staging buffers per ingest pipeline: UFS reads run this many chunks ahead of the H2D DMA.")
+_k("UNDERFS_LZ4_FRAME_DECODE", "alluxio.underfs.lz4.frame.decode", "false", Scope.SERVER,
+   "Present *.lz4 files of a mount that are LZ4 frames (independent blocks, content size) as their "
+   "decompressed bytes; HBM workers decode them on the GPU when caching (mount option or site key).")
 _k("WORKER_UFS_INGEST_BULK_STAGING_SIZE", "alluxio.worker.ufs.ingest.bulk.staging.size", "64MB", Scope.WORKER,
    "Pinned staging of the bulk small-file ingest (two halves: preads fill one while the other is "
    "copied into HBM).")

@@ -77,6 +77,36 @@ std::vector<int32_t> lz4_device(const std::vector<std::tuple<uint64_t, uint64_t,
   return sizes;
 }
 
+// Kernel-only timing of an LZ4 batch: the chunk table is uploaded once, `reps` launches are
+// bracketed by HIP events (no per-call allocation / table upload / size download in the number).
+double lz4_device_kernel_ms(const std::vector<std::tuple<uint64_t, uint64_t, uint32_t, uint32_t>>& chunks,
+                            bool compress, int reps) {
+  const int n = (int)chunks.size();
+  if (!n || reps <= 0) return 0.0;
+  std::vector<Lz4Chunk> h(n);
+  for (int i = 0; i < n; ++i)
+    h[i] = Lz4Chunk{std::get<0>(chunks[i]), std::get<1>(chunks[i]), std::get<2>(chunks[i]), std::get<3>(chunks[i])};
+  DevBuf dch(sizeof(Lz4Chunk) * n), dsz(sizeof(int32_t) * n);
+  HIP_CHECK(hipMemcpy(dch.p, h.data(), sizeof(Lz4Chunk) * n, hipMemcpyHostToDevice));
+  hipEvent_t a, b;
+  HIP_CHECK(hipEventCreate(&a));
+  HIP_CHECK(hipEventCreate(&b));
+  auto launch = [&] {
+    if (compress) HIP_CHECK(launch_lz4_compress((Lz4Chunk*)dch.p, n, (int32_t*)dsz.p, 0));
+    else HIP_CHECK(launch_lz4_decompress((Lz4Chunk*)dch.p, n, (int32_t*)dsz.p, 0));
+  };
+  launch();
+  HIP_CHECK(hipEventRecord(a, 0));
+  for (int r = 0; r < reps; ++r) launch();
+  HIP_CHECK(hipEventRecord(b, 0));
+  HIP_CHECK(hipEventSynchronize(b));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return ms / reps;
+}
+
 // Process-wide descriptor ring for ad-hoc batched copies (IPC reads, peer pulls): no per-call
 // hipMalloc/hipFree (hipFree may synchronize the device).  Without a HIP device the segments are
 // plain host memory and are copied with memcpy (CPU builds, shared-memory DRAM arenas).
@@ -563,6 +593,8 @@ PYBIND11_MODULE(_C, m) {
         });
   m.def("lz4_compress_bound", &lz4_compress_bound);
   m.def("lz4_device", &lz4_device, G(), py::arg("chunks"), py::arg("compress"), py::arg("stream") = 0);
+  m.def("lz4_device_kernel_ms", &lz4_device_kernel_ms, G(), py::arg("chunks"), py::arg("compress"),
+        py::arg("reps") = 5);
   m.def("batched_copy", &batched_copy, G(), py::arg("segments"), py::arg("stream") = 0, py::arg("sync") = true);
   m.def("fill_pattern", [](uint64_t ptr, uint64_t bytes, uint64_t seed, uint64_t word_offset, uint64_t stream) {
           py::gil_scoped_release rel;

@@ -933,6 +933,205 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_ring_kernel(const L
   }
 }
 
+// Variants 4-6: wave-synchronous decode.  The workgroup is ONE wave, so lanes need no
+// workgroup barrier to see each other's LDS writes: LDS ops of a wave execute in issue order and
+// a wavefront-scope fence + wave barrier only stops the compiler from reordering them
+// (rocPRIM's wave_barrier idiom).  The old kernels' __syncthreads() also drained every
+// outstanding HBM store (s_waitcnt vmcnt/vscnt 0) once or twice per sequence, which made the
+// per-sequence chain ~1800 cycles.  Here:
+//   * the parse reads 8 stream bytes per LDS access (token, short literal length, offset and
+//     the first match-length byte usually come in one read);
+//   * an R-byte LDS ring mirrors the latest output, so matches with offset <= R-64 (the bulk of
+//     LZ4 streams) never read HBM; overlapping matches copy 64 bytes per round from the latest
+//     period (src = op + b0 - off + (i - b0) % off), so even offset-1 runs take one round per
+//     64 bytes instead of one per byte;
+//   * output goes to HBM with plain stores that are never read back, except by far matches
+//     (offset > R-64), which fence only when their source overlaps unfenced output.
+__device__ __forceinline__ void lz_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+typedef __attribute__((address_space(1))) uint8_t gu8;
+
+template <uint32_t R, bool kFast>
+__global__ __launch_bounds__(kLzThreads) void lz4_decompress_wave_kernel(const Lz4Chunk* __restrict__ ch,
+                                                                        int n, int32_t* __restrict__ out_sizes) {
+  __shared__ __attribute__((aligned(16))) uint8_t inb[kLzIn + 16];
+  __shared__ uint8_t ring[R];
+  constexpr uint32_t rmask = R - 1;
+  const uint32_t lane = threadIdx.x;
+  for (int w = blockIdx.x; w < n; w += gridDim.x) {
+    // global (addrspace 1) pointers: generic/FLAT accesses would also count in lgkmcnt, so
+    // every LDS wait of the parse would drain the wave's outstanding HBM stores
+    const gu8* __restrict__ src = reinterpret_cast<const gu8*>(ch[w].src);
+    const uint32_t slen = ch[w].src_bytes;
+    gu8* const dst = reinterpret_cast<gu8*>(ch[w].dst);
+    const uint32_t cap = ch[w].dst_capacity;
+    uint32_t base = 0, valid = 0;
+    auto refill = [&](uint32_t pos) {
+      const uint32_t b = pos & ~7u;
+      const uint32_t avail = slen - b < kLzIn ? slen - b : kLzIn;
+      lz_wave_sync();
+      for (uint32_t i = lane; i < avail; i += kLzThreads) inb[i] = src[b + i];
+      base = b;
+      valid = avail;
+      lz_wave_sync();
+    };
+    // 8 bytes of the stream from pos (bytes past the stream end are garbage: callers bound-check)
+    auto window = [&](uint32_t pos) -> uint64_t {
+      if (pos + 8 > base + valid && base + valid < slen) refill(pos);
+      const uint32_t r = pos - base;
+      const uint32_t a = r & ~7u;
+      const uint64_t lo = *reinterpret_cast<const uint64_t*>(inb + a);
+      const uint64_t hi = *reinterpret_cast<const uint64_t*>(inb + a + 8);
+      const uint32_t sh = (r & 7u) * 8u;
+      return sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+    };
+    auto byte_at = [&](uint32_t pos) -> uint32_t { return (uint32_t)(window(pos) & 255u); };
+    uint32_t ip = 0, op = 0, fenced = 0;
+    int32_t status = 0;
+    while (ip < slen) {
+      const uint64_t wv = window(ip);
+      const uint32_t token = (uint32_t)(wv & 255u);
+      if constexpr (kFast) {
+        // Fast path for the common sequence shape: <= 4 literals and a match of <= 18 bytes
+        // whose offset lies in the ring.  The literals and the offset are already in the 8-byte
+        // window (no further LDS read), the literal bytes are shifted out of it per lane, the
+        // match is one 64-lane round; ~4x fewer scalar instructions and branches than the
+        // general path below (which the SQ_INSTS_SALU counts showed to be the limit).
+        const uint32_t fl = token >> 4, fm = token & 15u;
+        const uint32_t mop = op + fl;
+        const uint32_t foff = (uint32_t)((wv >> (8u * (1u + (fl < 4u ? fl : 4u)))) & 0xFFFFu);
+        const uint32_t fml = fm + 4u;
+        if (fl <= 4u && fm < 15u && ip + 3u + fl < slen && foff != 0u && foff <= mop && mop + fml <= cap &&
+            foff + kLzThreads <= R) {
+          if (lane < fl) {
+            const uint8_t v = (uint8_t)(wv >> (8u * (1u + (lane & 7u))));
+            dst[op + lane] = v;
+            ring[(op + lane) & rmask] = v;
+          }
+          lz_wave_sync();
+          if (lane < fml) {
+            uint32_t s = mop - foff + lane;
+            if (foff < fml) {
+              const uint32_t q = (uint32_t)((float)lane * __builtin_amdgcn_rcpf((float)foff));
+              int32_t r = (int32_t)lane - (int32_t)(q * foff);
+              if (r >= (int32_t)foff) r -= foff;
+              if (r < 0) r += foff;
+              s = mop - foff + (uint32_t)r;
+            }
+            const uint8_t v = ring[s & rmask];
+            dst[mop + lane] = v;
+            ring[(mop + lane) & rmask] = v;
+          }
+          lz_wave_sync();
+          ip += 3u + fl;
+          op = mop + fml;
+          continue;
+        }
+      }
+      uint32_t lit = token >> 4;
+      ++ip;
+      if (lit == 15) {
+        uint32_t b;
+        do {
+          if (ip >= slen) { status = -1; break; }
+          b = byte_at(ip++);
+          lit += b;
+        } while (b == 255);
+        if (status) break;
+      }
+      if (ip + lit > slen || op + lit > cap) { status = -2; break; }
+      if (lit) {
+        // CDNA counts stores in vmcnt: waiting for a global load would also drain every HBM
+        // store in flight, so literals always come from the LDS staging (refilled at the run when
+        // needed) and the global-load loop is kept separate for runs longer than the staging
+        if (ip + lit > base + valid && lit + 8 <= kLzIn) refill(ip);
+        if (ip + lit <= base + valid) {
+          for (uint32_t i = lane; i < lit; i += kLzThreads) {
+            const uint8_t v = inb[ip - base + i];
+            dst[op + i] = v;
+            ring[(op + i) & rmask] = v;
+          }
+        } else {
+          for (uint32_t i = lane; i < lit; i += kLzThreads) {
+            const uint8_t v = src[ip + i];
+            dst[op + i] = v;
+            ring[(op + i) & rmask] = v;
+          }
+        }
+      }
+      const bool short_lit = (token >> 4) <= 4;   // offset + first ml byte inside wv
+      ip += lit;
+      op += lit;
+      if (ip >= slen) break;  // last sequence carries literals only
+      if (ip + 2 > slen) { status = -3; break; }
+      uint32_t off, ml = token & 15;
+      if (short_lit) {
+        const uint32_t sh = 8u * (1u + (token >> 4));
+        off = (uint32_t)((wv >> sh) & 0xFFFFu);
+      } else {
+        const uint64_t ov = window(ip);
+        off = (uint32_t)(ov & 0xFFFFu);
+      }
+      ip += 2;
+      if (ml == 15) {
+        uint32_t b;
+        do {
+          if (ip >= slen) { status = -4; break; }
+          b = byte_at(ip++);
+          ml += b;
+        } while (b == 255);
+        if (status) break;
+      }
+      ml += 4;
+      if (off == 0 || off > op || op + ml > cap) { status = -5; break; }
+      lz_wave_sync();   // literal ring writes before the match reads them
+      if (off + kLzThreads <= R) {
+        uint32_t lmod = lane;   // lane % off for short offsets (periodic copy), once per match
+        if (off < kLzThreads) {
+          const uint32_t q = (uint32_t)((float)lane * __builtin_amdgcn_rcpf((float)off));
+          int32_t r = (int32_t)lane - (int32_t)(q * off);
+          if (r >= (int32_t)off) r -= off;
+          if (r < 0) r += off;
+          lmod = (uint32_t)r;
+        }
+        for (uint32_t b0 = 0; b0 < ml; b0 += kLzThreads) {
+          const uint32_t i = b0 + lane;
+          if (i < ml) {
+            const uint32_t s = off >= kLzThreads ? op + i - off : op + b0 - off + lmod;
+            const uint8_t v = ring[s & rmask];
+            dst[op + i] = v;
+            ring[(op + i) & rmask] = v;
+          }
+          lz_wave_sync();
+        }
+      } else {
+        // far match: source is older output in HBM (off > R-64 >= 64, so a round's source lies
+        // before the round); fence only when it overlaps output not yet fenced
+        for (uint32_t b0 = 0; b0 < ml; b0 += kLzThreads) {
+          if (op + b0 + kLzThreads > fenced + off) {
+            __threadfence_block();
+            fenced = op + b0;
+          }
+          const uint32_t i = b0 + lane;
+          if (i < ml) {
+            const uint8_t v = dst[op + i - off];
+            dst[op + i] = v;
+            ring[(op + i) & rmask] = v;
+          }
+          lz_wave_sync();
+        }
+      }
+      op += ml;
+    }
+    if (lane == 0) out_sizes[w] = status ? status : (int32_t)op;
+    lz_wave_sync();
+  }
+}
+
 static int g_lz4_decode_variant = 2;  // 0: LDS window, 1: direct, 2: direct + staged parse (fastest, default), 3: + LDS ring
 
 void set_lz4_decode_variant(int v) { g_lz4_decode_variant = v; }
@@ -952,10 +1151,20 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL(lz4_decompress_staged_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
                        chunks, n, out_sizes);
-  } else {
+  } else if (g_lz4_decode_variant == 3) {
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL(lz4_decompress_ring_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
                        chunks, n, out_sizes);
+  } else {
+    const unsigned grid = (unsigned)std::min(n, 65536);
+    switch (g_lz4_decode_variant) {
+      case 4: hipLaunchKernelGGL((lz4_decompress_wave_kernel<8192, false>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 5: hipLaunchKernelGGL((lz4_decompress_wave_kernel<16384, false>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 6: hipLaunchKernelGGL((lz4_decompress_wave_kernel<32768, false>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 7: hipLaunchKernelGGL((lz4_decompress_wave_kernel<8192, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 8: hipLaunchKernelGGL((lz4_decompress_wave_kernel<16384, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      default: hipLaunchKernelGGL((lz4_decompress_wave_kernel<32768, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+    }
   }
   return hipGetLastError();
 }

@@ -81,6 +81,8 @@ def create(uri: str, conf=None, properties=None, logging_wrapper: bool = False,
     if f is None:
         raise ValueError(f"no under file system factory found for {uri!r}")
     ufs = f.create(uri, conf, properties)
+    from .lz4frame import wrap
+    ufs = wrap(ufs, properties, conf)
     return UnderFileSystemWithLogging(ufs, metrics) if logging_wrapper else ufs
 
 

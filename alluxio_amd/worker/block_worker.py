@@ -390,6 +390,21 @@ class BlockWorker:
             if self.native.has_block(block_id) or self.native.has_temp_block(block_id):
                 return self.native.has_block(block_id)
             raise e
+        from ..underfs.lz4frame import Lz4FrameUnderFileSystem
+        if isinstance(ufs, Lz4FrameUnderFileSystem) and has_gpu() and on_chunk is None:
+            idx = ufs.frame_index(opts.ufs_path)
+            start = opts.offset_in_file + offset
+            if idx is not None and start % idx.block_max == 0:
+                try:
+                    self._ingest_lz4_frame(session_id, block_id, ufs, opts.ufs_path, idx, start, length)
+                    self.commit_block(session_id, block_id)
+                    return True
+                except Exception:
+                    try:
+                        self.abort_block(session_id, block_id)
+                    except Exception:  # noqa: BLE001
+                        pass
+                    raise
         pool = self.ingest_pool()
         pipe = pool.acquire()
         try:
@@ -411,6 +426,63 @@ class BlockWorker:
             raise
         finally:
             pool.release(pipe)
+
+    def _ingest_lz4_frame(self, session_id: int, block_id: int, ufs, path: str, idx, start: int,
+                          length: int) -> None:
+        """Cache decompressed bytes [start, start+length) of an LZ4 frame: the compressed span of
+        the frame blocks covering them is read from the UFS in one request, copied to the GPU,
+        and decoded by one K11 launch (stored blocks by one batched copy) into a device buffer
+        that is then written into the temp block (underfs/lz4frame.py)."""
+        import torch
+
+        from ..ops.native import lib
+        from ..underfs.base import OpenOptions
+        from ..utils.exceptions import DataLossException
+        bm = idx.block_max
+        j0, j1 = start // bm, -(-(start + length) // bm)
+        blocks = idx.blocks[j0:j1]
+        lo = blocks[0][0]
+        hi = blocks[-1][0] + blocks[-1][1]
+        t0 = time.perf_counter()
+        host = torch.empty(hi - lo, dtype=torch.uint8, pin_memory=True)
+        mv = memoryview(host.numpy())
+        got = 0
+        with ufs.inner.open(path, OpenOptions(offset=lo)) as f:
+            while got < hi - lo:
+                n = f.readinto(mv[got:])
+                if not n:
+                    break
+                got += n
+        if got != hi - lo:
+            raise IOError(f"short read of the LZ4 frame span of block {block_id}: {got} of {hi - lo}")
+        dev = torch.device("cuda", self.store.device)
+        comp = host.to(dev, non_blocking=True)
+        out = torch.empty((j1 - j0) * bm, dtype=torch.uint8, device=dev)
+        C = lib()
+        chunks, raws, want = [], [], []
+        for k, (off, n, raw) in enumerate(blocks):
+            src = comp.data_ptr() + off - lo
+            dst = out.data_ptr() + k * bm
+            want.append(idx.block_len(j0 + k))
+            if raw:
+                raws.append((src, dst, n))
+            else:
+                chunks.append((src, dst, n, bm))
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        if raws:
+            C.batched_copy(raws, stream)
+        sizes = C.lz4_device(chunks, False, stream) if chunks else []
+        it = iter(sizes)
+        for k, (off, n, raw) in enumerate(blocks):
+            got = n if raw else next(it)
+            if got != want[k]:
+                raise DataLossException(f"LZ4 frame block {j0 + k} of {path} decoded to {got} bytes, "
+                                        f"expected {want[k]}")
+        self.write_ptr(session_id, block_id, 0, out.data_ptr() + (start - j0 * bm), length, DEVICE, stream, True)
+        self.metrics.counter("BytesReadUfsAll").inc(hi - lo)
+        self.metrics.counter("UfsIngestBytes").inc(length)
+        self.metrics.counter("Lz4DecodedBytes").inc(length)
+        self.metrics.timer("UfsIngestBlock").update(time.perf_counter() - t0)
 
     def cache_blocks_from_ufs(self, items, session_id: int | None = None) -> int:
         """Bulk form of :meth:`cache_block_from_ufs` for many small blocks (``items`` =

@@ -58,22 +58,27 @@ def test_crc32c_matches_host(gpu, variant):
     C.set_crc_variant(1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_lz4_device_roundtrip(gpu, variant):
     import torch
     C = lib()
     C.set_lz4_decode_variant(variant)
     rng = np.random.default_rng(1)
     chunks = []
-    for i in range(12):
-        n = int(rng.integers(1, 65536))
-        kind = i % 3
+    far = os.urandom(20000)
+    for i in range(20):
+        n = int(rng.integers(1, 65536)) if i < 15 else 65536
+        kind = i % 5
         if kind == 0:
             raw = rng.integers(0, 4, n, dtype=np.uint8).tobytes()         # compressible
         elif kind == 1:
             raw = os.urandom(n)                                            # incompressible
-        else:
+        elif kind == 2:
             raw = (b"alluxio-amd-" * (n // 12 + 1))[:n]                    # long matches
+        elif kind == 3:
+            raw = (far * 4)[:n]                                            # offsets of 20000 (beyond 8/16 KiB rings)
+        else:
+            raw = b"\x07" * (n // 2) + bytes(rng.integers(0, 3, n - n // 2, dtype=np.uint8))  # offset-1 run
         chunks.append(raw)
     # host-encoded -> device decode
     comp = [C.lz4_compress(c) for c in chunks]
@@ -85,6 +90,10 @@ def test_lz4_device_roundtrip(gpu, variant):
     for raw, o, sz in zip(chunks, outs, sizes):
         assert sz == len(raw)
         assert o[:sz].cpu().numpy().tobytes() == raw
+    # truncated / undersized streams fail with a negative status (no fault, no overrun)
+    bad = [(srcs[0].data_ptr(), outs[0].data_ptr(), max(1, len(comp[0]) - 3), 65536),
+           (srcs[2].data_ptr(), outs[2].data_ptr(), len(comp[2]), max(1, len(chunks[2]) // 2))]
+    assert all(sz < 0 for sz in C.lz4_device(bad, False, 0))
     # device encode -> host decode
     ins = [torch.tensor(list(c), dtype=torch.uint8, device=gpu) for c in chunks]
     cap = [C.lz4_compress_bound(len(c)) for c in chunks]

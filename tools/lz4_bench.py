@@ -66,10 +66,23 @@ def main():
                 ok = all(s == len(raw) for s in sizes) and bytes(out[:65536].cpu().numpy()) == raw and \
                     bytes(out[-65536:].cpu().numpy()) == raw
                 t = timeit(lambda: C.lz4_device(chunks, False, 0))
+                k = C.lz4_device_kernel_ms(chunks, False, 5) / 1e3
                 r = {"case": "lz4_decode", "data": kind, "ratio": round(len(raw) / len(comp), 3), "chunks": n,
-                     "variant": v, "ok": ok, "ms": round(t * 1e3, 3), "out_GBps": round(n * 65536 / t / 1e9, 2)}
+                     "variant": v, "ok": ok, "call_ms": round(t * 1e3, 3), "kernel_ms": round(k * 1e3, 3),
+                     "call_GBps": round(n * 65536 / t / 1e9, 2), "out_GBps": round(n * 65536 / k / 1e9, 2)}
                 print(json.dumps(r), flush=True)
                 res.append(r)
+            if kind == "text":
+                # encode of the decoded chunks (device encoder, K11)
+                cb = C.lz4_compress_bound(65536)
+                enc = torch.empty(n * cb, dtype=torch.uint8, device=dev)
+                ech = [(out.data_ptr() + i * 65536, enc.data_ptr() + i * cb, 65536, cb) for i in range(n)]
+                k = C.lz4_device_kernel_ms(ech, True, 3) / 1e3
+                r = {"case": "lz4_encode", "data": kind, "chunks": n, "kernel_ms": round(k * 1e3, 3),
+                     "in_GBps": round(n * 65536 / k / 1e9, 2)}
+                print(json.dumps(r), flush=True)
+                res.append(r)
+                del enc
             del out
     C.set_lz4_decode_variant(2)
     if a.out:
