@@ -955,10 +955,10 @@ __device__ __forceinline__ void lz_wave_sync() {
 
 typedef __attribute__((address_space(1))) uint8_t gu8;
 
-template <uint32_t R, bool kFast>
+template <uint32_t R, bool kFast, uint32_t I = kLzIn>
 __global__ __launch_bounds__(kLzThreads) void lz4_decompress_wave_kernel(const Lz4Chunk* __restrict__ ch,
                                                                         int n, int32_t* __restrict__ out_sizes) {
-  __shared__ __attribute__((aligned(16))) uint8_t inb[kLzIn + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t inb[I + 16];
   __shared__ uint8_t ring[R];
   constexpr uint32_t rmask = R - 1;
   const uint32_t lane = threadIdx.x;
@@ -972,7 +972,7 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_wave_kernel(const L
     uint32_t base = 0, valid = 0;
     auto refill = [&](uint32_t pos) {
       const uint32_t b = pos & ~7u;
-      const uint32_t avail = slen - b < kLzIn ? slen - b : kLzIn;
+      const uint32_t avail = slen - b < I ? slen - b : I;
       lz_wave_sync();
       for (uint32_t i = lane; i < avail; i += kLzThreads) inb[i] = src[b + i];
       base = b;
@@ -1048,7 +1048,7 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_wave_kernel(const L
         // CDNA counts stores in vmcnt: waiting for a global load would also drain every HBM
         // store in flight, so literals always come from the LDS staging (refilled at the run when
         // needed) and the global-load loop is kept separate for runs longer than the staging
-        if (ip + lit > base + valid && lit + 8 <= kLzIn) refill(ip);
+        if (ip + lit > base + valid && lit + 8 <= I) refill(ip);
         if (ip + lit <= base + valid) {
           for (uint32_t i = lane; i < lit; i += kLzThreads) {
             const uint8_t v = inb[ip - base + i];
@@ -1163,7 +1163,10 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
       case 6: hipLaunchKernelGGL((lz4_decompress_wave_kernel<32768, false>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 7: hipLaunchKernelGGL((lz4_decompress_wave_kernel<8192, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 8: hipLaunchKernelGGL((lz4_decompress_wave_kernel<16384, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
-      default: hipLaunchKernelGGL((lz4_decompress_wave_kernel<32768, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 9: hipLaunchKernelGGL((lz4_decompress_wave_kernel<32768, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 10: hipLaunchKernelGGL((lz4_decompress_wave_kernel<4096, true, 1024>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 11: hipLaunchKernelGGL((lz4_decompress_wave_kernel<2048, true, 1024>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      default: hipLaunchKernelGGL((lz4_decompress_wave_kernel<4096, true, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
     }
   }
   return hipGetLastError();
