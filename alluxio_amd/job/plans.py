@@ -364,8 +364,8 @@ class MigrateDefinition(PlanDefinition):
 @plan("transform")
 class TransformDefinition(PlanDefinition):
     """Table transformation (reference job/server/.../plan/transform/CompactDefinition.java +
-    format/{csv,parquet}: rewrite each partition's files as at most ``file.count.max`` Parquet
-    files under the transformation's location)."""
+    format/{csv,orc,parquet}: rewrite each partition's files as at most ``file.count.max``
+    Parquet files under the transformation's location)."""
 
     @staticmethod
     def _max_files(defn: str) -> int:
@@ -385,12 +385,10 @@ class TransformDefinition(PlanDefinition):
         import posixpath
 
         import pyarrow as pa
-        import pyarrow.csv as pcsv
         import pyarrow.parquet as pq
-        tables = []
-        for f in args["files"]:
-            data = ctx.fs.read_file(f)
-            tables.append(pcsv.read_csv(io.BytesIO(data)) if args["format"] == "csv" else pq.read_table(io.BytesIO(data)))
+
+        from ..table.udb import format_of, read_table_bytes
+        tables = [read_table_bytes(ctx.fs.read_file(f), format_of(f)) for f in args["files"]]
         tbl = pa.concat_tables(tables, promote_options="default") if len(tables) > 1 else tables[0]
         n = min(self._max_files(cfg.transform), max(1, tbl.num_rows))
         ctx.fs.create_directory(args["dst"], recursive=True, allow_exists=True)

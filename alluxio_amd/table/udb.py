@@ -19,7 +19,7 @@ import posixpath
 
 from ..utils.exceptions import NotFoundException, UnavailableException
 
-DATA_EXT = (".parquet", ".parq", ".csv")
+DATA_EXT = (".parquet", ".parq", ".csv", ".orc")
 
 
 class UdbPartition:
@@ -149,12 +149,7 @@ class FilesystemUnderDatabase(UnderDatabase):
         return sorted(k.name for k in kids if k.is_folder and not k.name.startswith(("_", ".")))
 
     def _read(self, path: str, fmt: str):
-        import pyarrow.csv as pcsv
-        import pyarrow.parquet as pq
-        data = self.fs.read_file(path)
-        if fmt == "csv":
-            return pcsv.read_csv(io.BytesIO(data))
-        return pq.read_table(io.BytesIO(data))
+        return read_table_bytes(self.fs.read_file(path), fmt)
 
     def _scan(self, loc: str, depth: int = 0):
         """[(partition spec, location, [files])] below a table directory."""
@@ -178,7 +173,7 @@ class FilesystemUnderDatabase(UnderDatabase):
         parts = self._scan(loc)
         if not parts:
             raise NotFoundException(f"table {name} has no data files under {loc}")
-        fmt = "csv" if parts[0][2][0].lower().endswith(".csv") else "parquet"
+        fmt = format_of(parts[0][2][0])
         schema: list[tuple[str, str]] = []
         pstats, partitions = {}, []
         for spec, ploc, files in parts:
@@ -189,6 +184,29 @@ class FilesystemUnderDatabase(UnderDatabase):
             partitions.append(UdbPartition(spec, ploc, files, fmt))
         pcols = [(k, "string") for k in partitions[0].values()] if partitions and partitions[0].spec else []
         return UdbTable(name, loc, schema, pcols, partitions, merge_stats(list(pstats.values())), pstats, fmt)
+
+
+def format_of(path: str) -> str:
+    """Data format of a table file by extension: csv, orc or parquet (reference
+    job/server/.../transform/format/{csv,orc,parquet})."""
+    p = path.lower()
+    if p.endswith(".csv"):
+        return "csv"
+    if p.endswith(".orc"):
+        return "orc"
+    return "parquet"
+
+
+def read_table_bytes(data: bytes, fmt: str):
+    """An Arrow table from one data file's bytes."""
+    if fmt == "csv":
+        import pyarrow.csv as pcsv
+        return pcsv.read_csv(io.BytesIO(data))
+    if fmt == "orc":
+        import pyarrow.orc as porc
+        return porc.ORCFile(io.BytesIO(data)).read()
+    import pyarrow.parquet as pq
+    return pq.read_table(io.BytesIO(data))
 
 
 def create_udb(udb_type: str, fs, location: str, db_name: str, options: dict | None = None) -> UnderDatabase:

@@ -30,6 +30,10 @@ def env(tmp_path):
                           "name": [f"item{i}" for i in range(10)], "ok": [i % 2 == 0 for i in range(10)]})
             fs.write_file(f"/wh/sales/year={year}/part-0.parquet", _parquet(t), write_type="MUST_CACHE")
         fs.write_file("/wh/users/u.csv", b"uid,city\n1,sf\n2,nyc\n3,sf\n", write_type="MUST_CACHE")
+        import pyarrow.orc as porc
+        b = io.BytesIO()
+        porc.write_table(pa.table({"k": [3, 1, 2], "v": ["c", "a", "b"]}), b)
+        fs.write_file("/wh/events/e.orc", b.getvalue(), write_type="MUST_CACHE")
         yield c, fs, TableClient(Channel(c.master.address))
         fs.close()
 
@@ -37,8 +41,8 @@ def env(tmp_path):
 def test_attach_schema_stats_read(env):
     c, fs, tc = env
     ok, st = tc.attach_database("fs", "/wh", "", "wh")
-    assert ok and sorted(st.tables_updated) == ["sales", "users"]
-    assert tc.databases() == ["wh"] and tc.tables("wh") == ["sales", "users"]
+    assert ok and sorted(st.tables_updated) == ["events", "sales", "users"]
+    assert tc.databases() == ["wh"] and tc.tables("wh") == ["events", "sales", "users"]
     ti = tc.table("wh", "sales")
     assert [(f.name, f.type) for f in ti.schema.cols] == [("id", "bigint"), ("price", "double"),
                                                           ("name", "string"), ("ok", "boolean")]
@@ -63,13 +67,18 @@ def test_attach_schema_stats_read(env):
     assert [p.partition_spec.spec for p in tc.read_table("wh", "sales", con2)] == ["year=2019", "year=2020"]
     u = tc.table("wh", "users")
     assert [f.name for f in u.schema.cols] == ["uid", "city"]
+    # ORC table (reference transform/format/orc): schema and statistics from the ORC file
+    ev = tc.table("wh", "events")
+    assert [(f.name, f.type) for f in ev.schema.cols] == [("k", "bigint"), ("v", "string")]
+    es = {s.col_name: s for s in tc.column_statistics("wh", "events", ["k"])}
+    assert es["k"].data.long_stats.low_value == 1 and es["k"].data.long_stats.high_value == 3
 
 
 def test_sync_detach_and_journal_replay(env):
     c, fs, tc = env
     tc.attach_database("fs", "/wh", "", "wh")
     st = tc.sync_database("wh")
-    assert sorted(st.tables_unchanged) == ["sales", "users"]
+    assert sorted(st.tables_unchanged) == ["events", "sales", "users"]
     fs.write_file("/wh/sales/year=2022/part-0.parquet",
                   _parquet(pa.table({"id": [1], "price": [1.0], "name": ["x"], "ok": [True]})), write_type="MUST_CACHE")
     fs.delete("/wh/users", recursive=True)
@@ -78,7 +87,7 @@ def test_sync_detach_and_journal_replay(env):
     assert tc.table("wh", "sales").version == 2
     c.restart_master()
     tc2 = TableClient(Channel(c.master.address))
-    assert tc2.tables("wh") == ["sales"]
+    assert tc2.tables("wh") == ["events", "sales"]
     assert len(tc2.read_table("wh", "sales")) == 4
     assert tc2.detach_database("wh") and tc2.databases() == []
 
@@ -103,6 +112,17 @@ def test_transform_via_job_service(env):
         assert 1 <= len(lay["files"]) <= 2
         back = pa.concat_tables([pq.read_table(io.BytesIO(fs.read_file(f))) for f in lay["files"]])
         assert back.num_rows == 10
+    # an ORC table compacts to Parquet too
+    jid2 = tc.transform_table("wh", "events", "file.count.max=1")
+    for _ in range(500):
+        c.drive_jobs()
+        if tm.transform_heartbeat():
+            break
+        time.sleep(0.01)
+    ev = tc.read_table("wh", "events")[0]
+    lay = json.loads(ev.transformations[0].layout.layout_data)
+    assert pq.read_table(io.BytesIO(fs.read_file(lay["files"][0]))).column("k").to_pylist() == [3, 1, 2]
+    assert pb.job.Status.values_by_number[tc.transform_job_info(jid2)[0].job_status].name == "COMPLETED"
     out = io.StringIO()
     assert TableShell(Channel(c.master.address), out).run(["transformStatus", str(jid)]) == 0
     assert "COMPLETED" in out.getvalue()
