@@ -1132,32 +1132,192 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_wave_kernel(const L
   }
 }
 
-static int g_lz4_decode_variant = 2;  // 0: LDS window, 1: direct, 2: direct + staged parse (fastest, default), 3: + LDS ring
+// Variants 13-15: lane groups.  The wave-uniform kernels above run the token parse on the
+// CU's single scalar pipe, which caps them at ~50-75 GB/s however the copies are done
+// (profiles/r2_lz4.md).  Here a wave decodes 64/G chunks at once: each group of G lanes owns one
+// chunk and keeps its parse state in VGPRs, so one VALU instruction advances 64/G independent
+// token streams and the four SIMDs share the parse work.  Each group has its own input staging
+// (I bytes, refilled with aligned dword loads) and output ring (R bytes) in LDS; matches within
+// the ring never touch HBM, farther ones read the output back after a fence.
+template <uint32_t G, uint32_t R, uint32_t I>
+__global__ __launch_bounds__(kLzThreads) void lz4_decompress_groups_kernel(const Lz4Chunk* __restrict__ ch,
+                                                                          int n, int32_t* __restrict__ out_sizes) {
+  constexpr uint32_t NG = kLzThreads / G;
+  constexpr uint32_t rmask = R - 1;
+  __shared__ __attribute__((aligned(16))) uint8_t inb_all[NG][I + 16];
+  __shared__ uint8_t ring_all[NG][R];
+  const uint32_t lane = threadIdx.x, grp = lane / G, gl = lane % G;
+  uint8_t* const inb = inb_all[grp];
+  uint8_t* const ring = ring_all[grp];
+  const int nsets = (n + (int)NG - 1) / (int)NG;
+  for (int set = blockIdx.x; set < nsets; set += gridDim.x) {
+    const int c = set * (int)NG + (int)grp;
+    const bool have = c < n;
+    const gu8* src = have ? reinterpret_cast<const gu8*>(ch[c].src) : nullptr;
+    const uint32_t slen = have ? ch[c].src_bytes : 0u;
+    gu8* const dst = have ? reinterpret_cast<gu8*>(ch[c].dst) : nullptr;
+    const uint32_t cap = have ? ch[c].dst_capacity : 0u;
+    uint32_t base = 0, valid = 0, ip = 0, op = 0;
+    int32_t status = 0;
+    bool active = have && slen > 0;
+    auto refill = [&](uint32_t pos) {
+      const uint32_t b = pos & ~7u;
+      const uint32_t avail = slen - b < I ? slen - b : I;
+      const uint64_t a0 = reinterpret_cast<uint64_t>(src + b);
+      const uint64_t al = a0 & ~3ull;
+      const uint32_t lead = (uint32_t)(a0 - al);
+      const uint32_t nw = (avail + lead + 3u) / 4u;
+      lz_wave_sync();
+      for (uint32_t k = gl; k < nw; k += G) {
+        const uint32_t wv = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(al + 4ull * k);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const int32_t d = (int32_t)(4u * k + j) - (int32_t)lead;
+          if (d >= 0 && (uint32_t)d < avail) inb[d] = (uint8_t)(wv >> (8u * j));
+        }
+      }
+      base = b;
+      valid = avail;
+      lz_wave_sync();
+    };
+    auto win = [&](uint32_t pos) -> uint64_t {
+      if (pos + 8 > base + valid && base + valid < slen) refill(pos);
+      const uint32_t r = pos - base;
+      const uint32_t a = r & ~7u;
+      const uint64_t lo = *reinterpret_cast<const uint64_t*>(inb + a);
+      const uint64_t hi = *reinterpret_cast<const uint64_t*>(inb + a + 8);
+      const uint32_t sh = (r & 7u) * 8u;
+      return sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+    };
+    while (__any(active)) {
+      if (active) {
+        const uint64_t wv = win(ip);
+        const uint32_t token = (uint32_t)(wv & 255u);
+        uint32_t lit = token >> 4;
+        uint32_t p = ip + 1;
+        if (lit == 15) {
+          uint32_t b = 255;
+          while (b == 255 && p < slen) {
+            b = (uint32_t)(win(p) & 255u);
+            ++p;
+            lit += b;
+          }
+          if (b == 255) status = -1;
+        }
+        if (!status && (p + lit > slen || op + lit > cap)) status = -2;
+        if (!status && lit) {
+          if (p + lit > base + valid && lit + 8 <= I) refill(p);
+          if (p + lit <= base + valid) {
+            for (uint32_t i = gl; i < lit; i += G) {
+              const uint8_t v = inb[p - base + i];
+              dst[op + i] = v;
+              ring[(op + i) & rmask] = v;
+            }
+          } else {
+            for (uint32_t i = gl; i < lit; i += G) {
+              const uint8_t v = src[p + i];
+              dst[op + i] = v;
+              ring[(op + i) & rmask] = v;
+            }
+          }
+          p += lit;
+          op += lit;
+        }
+        if (status || p >= slen) {
+          active = false;   // error, or the last sequence (literals only) is done
+        } else if (p + 2 > slen) {
+          status = -3;
+          active = false;
+        } else {
+          const uint32_t off = (uint32_t)(win(p) & 0xFFFFu);
+          p += 2;
+          uint32_t ml = token & 15u;
+          if (ml == 15) {
+            uint32_t b = 255;
+            while (b == 255 && p < slen) {
+              b = (uint32_t)(win(p) & 255u);
+              ++p;
+              ml += b;
+            }
+            if (b == 255) status = -4;
+          }
+          ml += 4;
+          if (!status && (off == 0 || off > op || op + ml > cap)) status = -5;
+          if (status) {
+            active = false;
+          } else {
+            lz_wave_sync();   // literal ring writes before the match reads them
+            if (off + G <= R) {
+              uint32_t lmod = gl;
+              if (off < G) lmod = gl % off;
+              for (uint32_t b0 = 0; b0 < ml; b0 += G) {
+                const uint32_t i = b0 + gl;
+                if (i < ml) {
+                  const uint32_t s = off >= G ? op + i - off : op + b0 - off + lmod;
+                  const uint8_t v = ring[s & rmask];
+                  dst[op + i] = v;
+                  ring[(op + i) & rmask] = v;
+                }
+                lz_wave_sync();
+              }
+            } else {
+              // far match: the source is output in HBM; off > R - G >= G keeps each round's
+              // source before the round, the fence makes earlier rounds' stores visible
+              for (uint32_t b0 = 0; b0 < ml; b0 += G) {
+                __threadfence_block();
+                const uint32_t i = b0 + gl;
+                if (i < ml) {
+                  const uint8_t v = dst[op + i - off];
+                  dst[op + i] = v;
+                  ring[(op + i) & rmask] = v;
+                }
+                lz_wave_sync();
+              }
+            }
+            op += ml;
+            ip = p;
+          }
+        }
+      }
+    }
+    if (have && gl == 0) out_sizes[c] = status ? status : (int32_t)op;
+    lz_wave_sync();
+  }
+}
+
+// -1 (default): auto — the staged wave-per-chunk kernel (2) for small batches, lane groups of 4
+// (17) from 6144 chunks up, where enough chunks exist to fill the CUs 16 per wave
+// (profiles/r2_lz4.md: text 45 -> 63 GB/s at 8192 chunks, 54 -> 217 GB/s at 32768).
+// 0: LDS window, 1: direct, 2: staged parse, 3: + LDS ring, 4-12: wave-synchronous, 13-18: groups.
+static int g_lz4_decode_variant = -1;
+constexpr int kLzGroupMinChunks = 6144;
 
 void set_lz4_decode_variant(int v) { g_lz4_decode_variant = v; }
 
 hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
                                  hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  if (g_lz4_decode_variant == 0) {
+  int variant = g_lz4_decode_variant;
+  if (variant < 0) variant = n >= kLzGroupMinChunks ? 17 : 2;
+  if (variant == 0) {
     const unsigned grid = (unsigned)std::min(n, 4096);
     hipLaunchKernelGGL(lz4_decompress_kernel, dim3(grid), dim3(kLzThreads), kLzWindow, stream,
                        chunks, n, out_sizes);
-  } else if (g_lz4_decode_variant == 1) {
+  } else if (variant == 1) {
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL(lz4_decompress_direct_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
                        chunks, n, out_sizes);
-  } else if (g_lz4_decode_variant == 2) {
+  } else if (variant == 2) {
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL(lz4_decompress_staged_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
                        chunks, n, out_sizes);
-  } else if (g_lz4_decode_variant == 3) {
+  } else if (variant == 3) {
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL(lz4_decompress_ring_kernel, dim3(grid), dim3(kLzThreads), 0, stream,
                        chunks, n, out_sizes);
   } else {
     const unsigned grid = (unsigned)std::min(n, 65536);
-    switch (g_lz4_decode_variant) {
+    switch (variant) {
       case 4: hipLaunchKernelGGL((lz4_decompress_wave_kernel<8192, false>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 5: hipLaunchKernelGGL((lz4_decompress_wave_kernel<16384, false>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 6: hipLaunchKernelGGL((lz4_decompress_wave_kernel<32768, false>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
@@ -1166,7 +1326,37 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
       case 9: hipLaunchKernelGGL((lz4_decompress_wave_kernel<32768, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 10: hipLaunchKernelGGL((lz4_decompress_wave_kernel<4096, true, 1024>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 11: hipLaunchKernelGGL((lz4_decompress_wave_kernel<2048, true, 1024>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
-      default: hipLaunchKernelGGL((lz4_decompress_wave_kernel<4096, true, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 12: hipLaunchKernelGGL((lz4_decompress_wave_kernel<4096, true, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 13: {
+        const unsigned g = (unsigned)std::min((n + 7) / 8, 65536);
+        hipLaunchKernelGGL((lz4_decompress_groups_kernel<8, 2048, 512>), dim3(g), dim3(kLzThreads), 0, stream, chunks, n, out_sizes);
+        break;
+      }
+      case 14: {
+        const unsigned g = (unsigned)std::min((n + 15) / 16, 65536);
+        hipLaunchKernelGGL((lz4_decompress_groups_kernel<4, 1024, 256>), dim3(g), dim3(kLzThreads), 0, stream, chunks, n, out_sizes);
+        break;
+      }
+      case 15: {
+        const unsigned g = (unsigned)std::min((n + 3) / 4, 65536);
+        hipLaunchKernelGGL((lz4_decompress_groups_kernel<16, 4096, 1024>), dim3(g), dim3(kLzThreads), 0, stream, chunks, n, out_sizes);
+        break;
+      }
+      case 16: {
+        const unsigned g = (unsigned)std::min((n + 31) / 32, 65536);
+        hipLaunchKernelGGL((lz4_decompress_groups_kernel<2, 512, 128>), dim3(g), dim3(kLzThreads), 0, stream, chunks, n, out_sizes);
+        break;
+      }
+      case 17: {
+        const unsigned g = (unsigned)std::min((n + 15) / 16, 65536);
+        hipLaunchKernelGGL((lz4_decompress_groups_kernel<4, 512, 256>), dim3(g), dim3(kLzThreads), 0, stream, chunks, n, out_sizes);
+        break;
+      }
+      default: {
+        const unsigned g = (unsigned)std::min((n + 15) / 16, 65536);
+        hipLaunchKernelGGL((lz4_decompress_groups_kernel<4, 2048, 256>), dim3(g), dim3(kLzThreads), 0, stream, chunks, n, out_sizes);
+        break;
+      }
     }
   }
   return hipGetLastError();

@@ -84,7 +84,7 @@ def main():
                 res.append(r)
                 del enc
             del out
-    C.set_lz4_decode_variant(2)
+    C.set_lz4_decode_variant(-1)
     if a.out:
         with open(a.out, "a") as f:
             for r in res:
