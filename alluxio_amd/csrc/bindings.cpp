@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "block_store.h"
+#include "trace.h"
 #include "cpu_codecs.h"
 #include "ipc.h"
 #include "ring_read.h"
@@ -592,6 +593,9 @@ PYBIND11_MODULE(_C, m) {
           return py::bytes(out);
         });
   m.def("lz4_compress_bound", &lz4_compress_bound);
+  m.def("trace_push", [](const std::string& name) { roctxRangePushA(name.c_str()); }, py::arg("name"));
+  m.def("trace_pop", [] { roctxRangePop(); });
+  m.def("trace_mark", [](const std::string& name) { roctxMarkA(name.c_str()); }, py::arg("name"));
   m.def("lz4_device", &lz4_device, G(), py::arg("chunks"), py::arg("compress"), py::arg("stream") = 0);
   m.def("lz4_device_kernel_ms", &lz4_device_kernel_ms, G(), py::arg("chunks"), py::arg("compress"),
         py::arg("reps") = 5);

@@ -12,6 +12,7 @@
 #include <sstream>
 
 #include "cpu_codecs.h"
+#include "trace.h"
 
 namespace amdx {
 
@@ -445,6 +446,7 @@ std::vector<int64_t> BlockStore::external_write(int64_t session, int64_t block_i
 
 void BlockStore::write(int64_t session, int64_t block_id, uint64_t offset, uint64_t src, uint64_t len,
                        int src_kind, uint64_t stream, bool sync) {
+  TraceRange trace_("BlockStore.write");
   if (len == 0) return;
   set_device();
   std::vector<CopySeg> dev_segs;
@@ -665,6 +667,7 @@ int BlockStore::lower_tier(int tier) const {
 
 std::vector<int64_t> BlockStore::move_blocks(int64_t session, const std::vector<int64_t>& ids, int dst_tier,
                                              const std::string& medium, bool evict, bool use_reserved) {
+  TraceRange trace_("BlockStore.move_blocks");
   set_device();
   std::unique_lock<std::mutex> lk(mu_);
   return move_blocks_locked(lk, session, ids, dst_tier, medium, evict, use_reserved);
@@ -943,6 +946,7 @@ void BlockStore::copy_segments(std::vector<CopySeg>& segs, hipStream_t stream) {
 }
 
 void BlockStore::read_batch(const std::vector<ReadReq>& reqs, uint64_t stream, bool sync) {
+  TraceRange trace_("BlockStore.read_batch");
   set_device();
   hipStream_t st = stream_or_default(stream);
   std::vector<CopySeg> dev_segs;
@@ -971,6 +975,7 @@ void BlockStore::read_batch(const std::vector<ReadReq>& reqs, uint64_t stream, b
 }
 
 std::vector<uint32_t> BlockStore::checksum(int64_t block_id, uint64_t piece_bytes) {
+  TraceRange trace_("BlockStore.checksum");
   set_device();
   BlockMeta snap;
   {
@@ -1028,6 +1033,7 @@ std::vector<uint32_t> BlockStore::checksum(int64_t block_id, uint64_t piece_byte
 
 std::vector<std::pair<uint64_t, std::vector<uint32_t>>> BlockStore::checksum_blocks(
     const std::vector<int64_t>& ids, bool device_only) {
+  TraceRange trace_("BlockStore.checksum_blocks");
   set_device();
   std::vector<std::pair<uint64_t, std::vector<uint32_t>>> out(ids.size());
   std::vector<uint64_t> ptrs;
@@ -1394,6 +1400,7 @@ void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t ses
 }
 
 std::vector<int64_t> BlockStore::free_space(int64_t session, uint64_t bytes, int tier, int dir) {
+  TraceRange trace_("BlockStore.free_space");
   set_device();
   std::unique_lock<std::mutex> lk(mu_);
   std::unordered_set<int64_t> before;
@@ -1594,6 +1601,7 @@ std::vector<int64_t> BlockStore::peek_free_pages(int dir, uint32_t want, bool de
 std::vector<int> BlockStore::create_blocks(int64_t session, const std::vector<int64_t>& ids, int tier,
                                            const std::string& medium, const std::vector<uint64_t>& sizes,
                                            bool evict) {
+  TraceRange trace_("BlockStore.create_blocks");
   if (ids.size() != sizes.size()) throw StoreError(kErrInvalidArgument, "ids/sizes length mismatch");
   set_device();
   std::unique_lock<std::mutex> lk(mu_);
@@ -1879,6 +1887,7 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
                                           const std::vector<uint64_t>& offsets,
                                           const std::vector<uint64_t>& lengths, uint64_t staging,
                                           uint64_t staging_bytes, int threads, uint64_t stream) {
+  TraceRange trace_("BlockStore.ingest_files");
   const size_t n = ids.size();
   if (paths.size() != n || offsets.size() != n || lengths.size() != n)
     throw StoreError(kErrInvalidArgument, "ingest_files: argument lengths differ");

@@ -20,6 +20,7 @@ from __future__ import annotations
 import numpy as np
 
 from ..utils import ids
+from ..utils.tracing import traced
 
 
 class _FileLayout:
@@ -211,6 +212,7 @@ class DeviceBatchLoader:
             all(how == "local" for how, _ in srcs.values()) else None
         return self._one_worker
 
+    @traced("DeviceBatchLoader.fill")
     def _fill(self, out, indices):
         """Gather records ``indices`` into rows of ``out`` (uint8 [B, record_bytes])."""
         w = self._single_worker()

@@ -77,7 +77,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             fut.result()
     tmp = target + ".tmp"
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp,
-          f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
+          f"-L{ROCM}/lib", "-lamdhip64", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib"])
     os.replace(tmp, target)
     if verbose:
         print("built", target)
@@ -129,7 +129,7 @@ def build_sanitized(kind: str, out_dir: str | None = None) -> str:
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
     target = os.path.join(out_dir, "_C" + suffix)
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *flags, *objs, "-o", target, f"-L{ROCM}/lib",
-          "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
+          "-lamdhip64", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib"])
     return target
 
 

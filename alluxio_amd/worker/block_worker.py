@@ -20,6 +20,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 from .. import metrics as msys
 from ..ops.native import has_gpu, native_errors
+from ..utils.tracing import traced
 from ..proto import pb
 from ..utils import ids
 from ..rpc import marshal
@@ -371,6 +372,7 @@ class BlockWorker:
         self.metrics.counter("BytesReadUfsAll").inc(len(data))
         return data
 
+    @traced("Worker.cache_block_from_ufs")
     def cache_block_from_ufs(self, block_id: int, opts, session_id: int | None = None, on_chunk=None,
                              offset: int = 0) -> bool:
         """UFS -> pinned staging ring -> block (async H2D on a side stream for the HBM tier,
@@ -427,6 +429,7 @@ class BlockWorker:
         finally:
             pool.release(pipe)
 
+    @traced("Worker.ingest_lz4_frame")
     def _ingest_lz4_frame(self, session_id: int, block_id: int, ufs, path: str, idx, start: int,
                           length: int) -> None:
         """Cache decompressed bytes [start, start+length) of an LZ4 frame: the compressed span of
@@ -484,6 +487,7 @@ class BlockWorker:
         self.metrics.counter("Lz4DecodedBytes").inc(length)
         self.metrics.timer("UfsIngestBlock").update(time.perf_counter() - t0)
 
+    @traced("Worker.cache_blocks_from_ufs")
     def cache_blocks_from_ufs(self, items, session_id: int | None = None) -> int:
         """Bulk form of :meth:`cache_block_from_ufs` for many small blocks (``items`` =
         [(block id, OpenUfsBlockOptions)]): blocks of a local UFS are read by the native store's

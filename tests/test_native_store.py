@@ -289,3 +289,17 @@ def test_ingest_files_bulk(tmp_path):
         s.ingest_files(7, [300], [files[0]], [0], [200 * 1024], staging.ctypes.data, staging.nbytes)
     assert s.checksum_blocks([100, 101, 200]) == [(64 * 1024, s.checksum(100, 0)), (64 * 1024, s.checksum(101, 0)), (0, [])]
     assert s.checksum_blocks([100], True) == [(0, [])]        # device_only skips host dirs
+
+
+def test_roctx_ranges_are_harmless_without_a_profiler():
+    from alluxio_amd.utils.tracing import mark, trace_range, traced
+    C = lib()
+    C.trace_push("outer")
+    with trace_range("inner"):
+        mark("point")
+    C.trace_pop()
+
+    @traced("fn")
+    def f(x):
+        return x + 1
+    assert f(1) == 2
