@@ -429,6 +429,8 @@ def main(argv=None) -> int:  # pragma: no cover - CLI entry
     ap.add_argument("--format", action="store_true")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
+    from ..utils.sampler import maybe_start_from_env
+    maybe_start_from_env()
     from ..conf import Configuration as _C
     from ..web.logserver import attach
     attach("MASTER", _C(load_site=True))

@@ -31,10 +31,17 @@ import json, sys
 sys.path.insert(0, {root!r})
 from alluxio_amd.client.file_system import FileSystem
 from alluxio_amd.stress import master_bench
+import os
+if os.environ.get("ALLUXIO_PYSAMPLE_CLIENT"):
+    from alluxio_amd.utils.sampler import StackSampler
+    _smp = StackSampler().start()
 fs = FileSystem(master_address={addr!r})
 r = master_bench.main({args!r}, fs=fs, print_result=False)
 r["native"] = str(fs.ctx.pool.get({addr!r}, fs.ctx.user)._native)
 print("RESULT " + json.dumps(r))
+if os.environ.get("ALLUXIO_PYSAMPLE_CLIENT"):
+    _smp.stop()
+    open(os.environ["ALLUXIO_PYSAMPLE_CLIENT"] + "." + str(os.getpid()), "w").write(_smp.report())
 fs.close()
 """
 
