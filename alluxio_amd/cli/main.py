@@ -1,7 +1,7 @@
 """``alluxio`` launcher: ``python -m alluxio_amd <command> [args]``.
 
 Parity: bin/alluxio:201-386 (format, formatJournal, formatMasters, formatWorker, fs, fsadmin,
-getConf, job, logLevel, readJournal, runClass, runTests, runJournalCrashTest, upgradeJournal,
+getConf, job, logLevel, readJournal, runClass, runTests, runUfsTests, runJournalCrashTest, upgradeJournal,
 validateConf, validateEnv, version) and bin/alluxio-start.sh (master / worker / job_master /
 job_worker / proxy / fuse / logserver processes).
 """
@@ -28,6 +28,7 @@ COMMAND is one of:
   readJournal           Read an Alluxio journal file from stdin and write a human-readable version of it to stdout.
   runClass              Run the main function of a module (``pkg.module`` or ``pkg.module:function``).
   runTests              Run all end-to-end tests on an Alluxio cluster.
+  runUfsTests --path P   Test an under storage against the UFS contract (UnderFileSystemContractTest).
   upgradeJournal        Upgrade an Alluxio journal from v0 to v1 (-journalDirectoryV0 <dir>).
   stress                Run a stress benchmark (master|worker|client-io|ufs-io|max-throughput).
   validateConf          Validate Alluxio conf and exit.
@@ -201,6 +202,9 @@ def main(argv=None, out=None) -> int:
         return m(rest, out)
     if cmd == "runTests":
         from .test_runner import main as m
+        return m(rest, out)
+    if cmd == "runUfsTests":
+        from .ufs_contract import main as m
         return m(rest, out)
     if cmd == "upgradeJournal":
         from ..journal.upgrade import main as m

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import datetime
 import threading
+import time
 import urllib.parse
 
 from .object_store import ObjectMeta, ObjectUnderFileSystem
@@ -113,6 +114,7 @@ class _SimulatedSwift:
 
     def __init__(self):
         self.objects: dict[str, bytes] = {}
+        self.mtimes: dict[str, int] = {}      # last-modified ms, as a real container reports it
         self.lock = threading.Lock()
 
 
@@ -176,6 +178,7 @@ class SwiftUnderFileSystem(ObjectUnderFileSystem):
         if self.simulation:
             with self._sim.lock:
                 self._sim.objects[key] = bytes(data)
+                self._sim.mtimes[key] = int(time.time() * 1000)
             return
         self.client.request("PUT", self.container, key, data=data)
 
@@ -194,7 +197,8 @@ class SwiftUnderFileSystem(ObjectUnderFileSystem):
         if self.simulation:
             with self._sim.lock:
                 d = self._sim.objects.get(key)
-            return None if d is None else ObjectMeta(key, len(d), str(hash(d) & 0xFFFFFFFF))
+                mt = self._sim.mtimes.get(key)
+            return None if d is None else ObjectMeta(key, len(d), str(hash(d) & 0xFFFFFFFF), mt)
         try:
             r = self.client.request("HEAD", self.container, key)
         except FileNotFoundError:
@@ -209,6 +213,7 @@ class SwiftUnderFileSystem(ObjectUnderFileSystem):
             if self.simulation:
                 with self._sim.lock:
                     self._sim.objects.pop(k, None)
+                    self._sim.mtimes.pop(k, None)
                 continue
             try:
                 self.client.request("DELETE", self.container, k)
@@ -225,7 +230,7 @@ class SwiftUnderFileSystem(ObjectUnderFileSystem):
                     if delimiter and delimiter in rest:
                         prefixes.add(prefix + rest.split(delimiter, 1)[0] + delimiter)
                     else:
-                        objs.append(ObjectMeta(k, len(self._sim.objects[k])))
+                        objs.append(ObjectMeta(k, len(self._sim.objects[k]), "", self._sim.mtimes.get(k)))
             return objs, sorted(prefixes)
         objs, prefixes, marker = [], [], None
         while True:
@@ -250,6 +255,7 @@ class SwiftUnderFileSystem(ObjectUnderFileSystem):
         if self.simulation:
             with self._sim.lock:
                 self._sim.objects[dst] = self._sim.objects[src]
+                self._sim.mtimes[dst] = int(time.time() * 1000)
             return
         self.client.request("PUT", self.container, dst, data=b"",
                             headers={"X-Copy-From": f"/{self.container}/{src}", "Content-Length": "0"})

@@ -1,0 +1,72 @@
+"""``alluxio runUfsTests``: the UFS contract runner against the local UFS, an object store (S3 via
+this project's S3 proxy, with the multipart-specific operations), Swift simulation and WebHDFS.
+
+Parity: integration/tools/validation/src/main/java/alluxio/cli/UnderFileSystemContractTest.java,
+UnderFileSystemCommonOperations.java, S3ASpecificOperations.java.
+"""
+import io
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(__file__))
+from ufs_fakes import webhdfs_server  # noqa: E402
+
+from alluxio_amd.cli import main as cli  # noqa: E402
+from alluxio_amd.cli import ufs_contract  # noqa: E402
+
+
+def _ok(res):
+    assert res["failed"] == [], res["failed"]
+    assert len(res["passed"]) >= 40
+
+
+def test_local_contract_via_cli(tmp_path):
+    out = io.StringIO()
+    rc = cli.main(["runUfsTests", "--path", str(tmp_path), "--large-file-size", "1000000"], out=out)
+    assert rc == 0, out.getvalue()
+    assert "Tests completed with 42 passed and 0 failed." in out.getvalue()
+    assert os.listdir(tmp_path) == []           # the runner cleans its scratch directory
+
+
+def test_single_operation_and_failure_reporting(tmp_path, monkeypatch):
+    res = ufs_contract.run(str(tmp_path), test="rename_file_test", out=io.StringIO())
+    assert res["passed"] == ["rename_file_test"]
+    # a connector that breaks a contract is reported, not crashed on
+    monkeypatch.setattr(ufs_contract.CommonOperations, "exists_test",
+                        lambda self: ufs_contract._check(False, "broken"))
+    res = ufs_contract.run(str(tmp_path), test="exists_test", out=io.StringIO())
+    assert res["failed"] == [{"test": "exists_test", "error": "ContractFailure: broken"}]
+
+
+def test_swift_simulation_contract():
+    _ok(ufs_contract.run("swift://contractbkt/", properties={"fs.swift.simulation": "true"},
+                         out=io.StringIO(), large_file_size=1 << 20))
+
+
+def test_webhdfs_contract():
+    srv, _ = webhdfs_server()
+    try:
+        _ok(ufs_contract.run(f"webhdfs://127.0.0.1:{srv.port}/", out=io.StringIO(), large_file_size=1 << 20,
+                             properties={"alluxio.underfs.webhdfs.user": "u"}))
+    finally:
+        srv.stop()
+
+
+def test_s3_contract_through_proxy(tmp_path):
+    from alluxio_amd.minicluster import LocalAlluxioCluster
+    from alluxio_amd.proxy import ProxyServer
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"},
+                             work_dir=str(tmp_path / "c")) as c:
+        fs = c.client()
+        fs.create_directory("/contract")
+        proxy = ProxyServer(fs, port=0)
+        port = proxy.start()
+        try:
+            out = io.StringIO()
+            res = ufs_contract.run("s3a://contract/", properties={"alluxio.underfs.s3.endpoint":
+                                                                  f"http://127.0.0.1:{port}"},
+                                   out=out, large_file_size=1 << 20)
+            _ok(res)
+            assert "S3ASpecificOperations#create_multipart_file_test" in out.getvalue()
+        finally:
+            proxy.stop()
