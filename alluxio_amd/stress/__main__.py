@@ -1,5 +1,6 @@
 """``python -m alluxio_amd.stress <master|worker|client-io|ufs-io|max-throughput> [args]``
-(reference: ``bin/alluxio runClass alluxio.stress.cli.<Bench>``).  ``--cluster`` submits the
+(reference: ``bin/alluxio runClass alluxio.stress.cli.<Bench>``); ``report --input .. --output ..``
+draws an HTML comparison of result files (GenerateReport).  ``--cluster`` submits the
 bench to the job service (StressBenchDefinition) and prints the merged summary."""
 import json
 import sys
@@ -11,6 +12,9 @@ def main(argv=None):
         print(__doc__)
         return 2
     bench, rest = argv[0], argv[1:]
+    if bench == "report":
+        from .report import main as m
+        return m(rest)
     if "--cluster" in rest:
         rest.remove("--cluster")
         limit = 0
