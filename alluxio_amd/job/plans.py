@@ -191,6 +191,8 @@ class LoadDefinition(PlanDefinition):
                   and jw.address.host not in cfg.excluded_worker_set]
         if not usable:
             raise ex.FailedPreconditionException("no job worker available for load")
+        if len(usable) > 1 and (cfg.replication < 0 or cfg.replication >= len(usable)):
+            return self._collective_plan(statuses, usable)
         assign: dict[int, list] = {}
         for st in statuses:
             for fbi in st.info.fileBlockInfos:
@@ -205,7 +207,68 @@ class LoadDefinition(PlanDefinition):
         by_id = {jw.id: jw for jw in usable}
         return [(by_id[w], blocks) for w, blocks in assign.items()]
 
+    @staticmethod
+    def _collective_plan(statuses, usable):
+        """``distributedLoad --replication`` >= the worker count (every worker gets every block):
+        each block gets one owner -- a worker already caching it, else a worker that loads it from
+        the UFS (round-robin) -- and then all workers exchange the blocks with RCCL all-gathers
+        over the node's transfer plane (TransferPlane.replicate_all: every xGMI link busy at
+        once) instead of N-1 point-to-point copies per block.  Every worker receives the same
+        block list, in the same order: the collective's call sequence is identical on all ranks."""
+        keys = {jw.id: f"{jw.address.host}:{jw.block_worker_port}" for jw in usable}
+        usable_keys = set(keys.values())
+        blocks, loads, rr, complete = [], {jw.id: [] for jw in usable}, 0, True
+        for st in statuses:
+            for fbi in st.info.fileBlockInfos:
+                bi = fbi.blockInfo
+                holders = [f"{l.workerAddress.host}:{l.workerAddress.rpcPort}" for l in bi.locations]
+                held = [h for h in holders if h in usable_keys]
+                complete &= set(held) >= usable_keys
+                if held:
+                    owner = held[0]
+                else:
+                    jw = usable[rr % len(usable)]
+                    rr += 1
+                    owner = keys[jw.id]
+                    loads[jw.id].append((st.info.path, bi.blockId))
+                blocks.append((st.info.path, bi.blockId, bi.length, owner, bool(held)))
+        if complete:
+            return []
+        participants = sorted(usable_keys)
+        return [(jw, {"collective": True, "participants": participants, "blocks": blocks, "load": loads[jw.id]})
+                for jw in usable]
+
+    def _run_collective(self, args, ctx) -> int:
+        w = ctx.worker
+        if w is None:
+            return 0
+        loaded = self._load_blocks([tuple(x) for x in args["load"]], ctx) if args["load"] else 0
+        plane = getattr(w, "transfer_plane", None)
+        if plane is not None and sorted(plane.addr_to_rank) == list(args["participants"]):
+            # the decision depends only on the plane membership every participant shares, so
+            # either all participants enter the collective or none does
+            todo = [(bid, n, plane.addr_to_rank[owner]) for _, bid, n, owner, _ in args["blocks"]]
+            return loaded + plane.replicate_all(todo)
+        # no common transfer plane: pull what was cached somewhere, load the rest from the UFS
+        from ..worker.remote import remote_block_fetcher
+        rest = []
+        for path, bid, n, owner, held in args["blocks"]:
+            if w.has_block(bid):
+                continue
+            if held:
+                host, port = owner.rsplit(":", 1)
+                remote_block_fetcher(w, host, int(port), n)(bid)
+                loaded += n
+            else:
+                rest.append((path, bid))
+        return loaded + (self._load_blocks(rest, ctx) if rest else 0)
+
     def run_task(self, cfg, args, ctx):
+        if isinstance(args, dict) and args.get("collective"):
+            return self._run_collective(args, ctx)
+        return self._load_blocks(args, ctx)
+
+    def _load_blocks(self, args, ctx):
         loaded = 0
         from_ufs = []       # UFS blocks go to the worker in one bulk ingest call
         statuses = {}

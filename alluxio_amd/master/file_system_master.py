@@ -14,6 +14,7 @@ context; the context is flushed after the tree lock is released.
 from __future__ import annotations
 
 import logging
+import os
 import threading
 import time
 
@@ -90,6 +91,8 @@ class FileSystemMaster(Journaled):
         self.persist_handler = None   # callable(file_id, path) -> job id; set by the master process
         self.persist_jobs: dict[int, dict] = {}
         self._sync_times: dict[str, float] = {}
+        self._sync_exec = None          # metadata sync executor / UFS prefetch pool (lazy, _sync_pools)
+        self._sync_prefetch = None
         self.state_lock = None
         self.audit = None
         # FileInfo reply cache: (inode id, path) -> FileInfo, valid while the namespace, block
@@ -926,7 +929,10 @@ class FileSystemMaster(Journaled):
     # ------------------------------------------------------------------------------------------
     # metadata loading / sync (reference InodeSyncStream, loadMetadataIfNotExist)
     def load_metadata(self, path: str, recursive: bool = False, create_ancestors: bool = True,
-                      quiet: bool = False) -> None:
+                      quiet: bool = False, cache=None) -> None:
+        """Load ``path`` (and its missing ancestors / children) from the UFS.  ``cache`` is the
+        :class:`sync.UfsStatusCache` of a running sync; a recursive load without one makes its own
+        so sub-directory listings are prefetched on the sync pool while the tree is built."""
         path = normalize_path(path)
         self._count("Master.LoadMetadataOps")
         try:
@@ -935,9 +941,13 @@ class FileSystemMaster(Journaled):
             if quiet:
                 raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
             raise
-        st = res.ufs.get_status(res.uri)
+        if cache is None and recursive:
+            cache = self._new_status_cache()
+        st = cache.get_status(path) if cache is not None else res.ufs.get_status(res.uri)
         if st is None:
             raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+        if cache is not None and st.is_directory:
+            cache.prefetch_children(path)
         owner_default, group_default = self._owner_group()
         ufs_blocks: list = []
         with RpcContext(self) as rpc, self.tree.lock.write():
@@ -958,9 +968,55 @@ class FileSystemMaster(Journaled):
                     parent = self.tree.get(cur)
             inode = self.tree.get(path)
             if inode.is_directory:
-                self._load_children(rpc, inode, path, recursive, owner_default, group_default)
+                self._load_children(rpc, inode, path, recursive, owner_default, group_default, cache)
         if ufs_blocks:
             self.block_master.commit_blocks_in_ufs(ufs_blocks)
+
+    def load_listed_children(self, path: str, statuses) -> None:
+        """Load the given UFS statuses (from a sync's listing of ``path``) as children of the
+        directory ``path``: one write-lock section and one journal context for the batch, no UFS
+        calls (InodeSyncStream.loadMetadataForPath over a prefetched listing)."""
+        owner_default, group_default = self._owner_group()
+        ufs_blocks: list = []
+        with RpcContext(self) as rpc, self.tree.lock.write():
+            rpc.ufs_blocks = ufs_blocks
+            parent = self.tree.get_or_none(path)
+            if parent is None or not parent.is_directory:
+                return
+            existing = self.tree.children.get(parent.id, {})
+            for st in statuses:
+                if st.name in existing or not st.name or "/" in st.name:
+                    continue
+                r = self._resolve_ufs(path.rstrip("/") + "/" + st.name)
+                self._load_one(rpc, parent, st.name, st, r, owner_default, group_default)
+        if ufs_blocks:
+            self.block_master.commit_blocks_in_ufs(ufs_blocks)
+
+    def _sync_pools(self):
+        """(sync executor, UFS prefetch pool), created on first use (reference
+        alluxio.master.metadata.sync.executor.pool.size / .ufs.prefetch.pool.size)."""
+        if self._sync_exec is None:
+            import concurrent.futures as cf
+            ncpu = os.cpu_count() or 4
+            n_exec = self.conf.get_int("alluxio.master.metadata.sync.executor.pool.size", str(ncpu)) \
+                if self.conf.get_raw("alluxio.master.metadata.sync.executor.pool.size") is not None else ncpu
+            n_pre = self.conf.get_int("alluxio.master.metadata.sync.ufs.prefetch.pool.size", str(ncpu)) \
+                if self.conf.get_raw("alluxio.master.metadata.sync.ufs.prefetch.pool.size") is not None else ncpu
+            self._sync_exec = cf.ThreadPoolExecutor(max(1, n_exec), thread_name_prefix="metadata-sync")
+            self._sync_prefetch = cf.ThreadPoolExecutor(max(1, n_pre), thread_name_prefix="ufs-prefetch")
+        return self._sync_exec, self._sync_prefetch
+
+    def _new_status_cache(self):
+        from .sync import UfsStatusCache
+
+        def fetch_list(p):
+            r = self._resolve_ufs(p)
+            return r.ufs.list_status(r.uri)
+
+        def fetch_status(p):
+            r = self._resolve_ufs(p)
+            return r.ufs.get_status(r.uri)
+        return UfsStatusCache(fetch_list, fetch_status, self._sync_pools()[1])
 
     def _load_one(self, rpc, parent, name, st, res, owner_default, group_default) -> None:
         owner = st.owner or owner_default
@@ -992,12 +1048,15 @@ class FileSystemMaster(Journaled):
         self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
             id=fid, completed=True, length=length, set_blocks=blocks)))
 
-    def _load_children(self, rpc, inode, path, recursive, owner_default, group_default) -> None:
+    def _load_children(self, rpc, inode, path, recursive, owner_default, group_default, cache=None) -> None:
         stack = [(inode, path)]
         while stack:
             d, dp = stack.pop()
-            res = self._resolve_ufs(dp)
-            listing = res.ufs.list_status(res.uri) or []
+            if cache is not None:
+                listing = cache.fetch_children(dp) or []
+            else:
+                res = self._resolve_ufs(dp)
+                listing = res.ufs.list_status(res.uri) or []
             existing = self.tree.children.get(d.id, {})
             for st in listing:
                 if "/" in st.name or not st.name:
@@ -1008,7 +1067,10 @@ class FileSystemMaster(Journaled):
                 if recursive:
                     child = self.tree.inodes.get(self.tree.children[d.id].get(st.name))
                     if child is not None and child.is_directory:
-                        stack.append((child, dp.rstrip("/") + "/" + st.name))
+                        cp = dp.rstrip("/") + "/" + st.name
+                        if cache is not None:
+                            cache.prefetch_children(cp)     # listed on the pool while we build
+                        stack.append((child, cp))
             self._apply(rpc, pb.journal.JournalEntry(update_inode_directory=pb.journal.UpdateInodeDirectoryEntry(
                 id=d.id, direct_children_loaded=True)))
 
@@ -1024,50 +1086,15 @@ class FileSystemMaster(Journaled):
     def sync_metadata(self, path: str, recursive: bool = True) -> dict:
         """Reconcile Alluxio metadata under ``path`` with the UFS (InodeSyncStream semantics):
         new UFS entries are loaded, persisted inodes missing from the UFS are removed, files whose
-        UFS fingerprint changed are reloaded (their cached blocks dropped)."""
+        UFS fingerprint changed are reloaded (their cached blocks dropped).  Paths are reconciled
+        breadth-first, ``alluxio.master.metadata.sync.concurrency.level`` at a time on the sync
+        executor, with directory listings prefetched on the UFS prefetch pool (master/sync.py)."""
+        from .sync import InodeSyncStream
         path = normalize_path(path)
-        stats = {"added": 0, "removed": 0, "updated": 0}
-        try:
-            res = self._resolve_ufs(path)
-        except InvalidPathException:
-            return stats
-        st = res.ufs.get_status(res.uri)
-        with self.tree.lock.read():
-            inode = self.tree.get_or_none(path)
-        if st is None:
-            if inode is not None and inode.is_persisted and path != "/":
-                self.delete(path, recursive=True, alluxio_only=True)
-                stats["removed"] += 1
-            return stats
-        if inode is None:
-            self.load_metadata(path, recursive=recursive, create_ancestors=True, quiet=True)
-            stats["added"] += 1
-            return stats
-        if inode.is_file:
-            fp = Fingerprint.create(res.ufs.ufs_type, st)
-            old = Fingerprint.parse(inode.ufs_fingerprint)
-            if inode.is_persisted and (old is None or not fp.matches_content(old)):
-                self.delete(path, alluxio_only=True)
-                self.load_metadata(path, quiet=True)
-                stats["updated"] += 1
-            return stats
-        listing = {s.name: s for s in (res.ufs.list_status(res.uri) or [])}
-        with self.tree.lock.read():
-            kids = {c.name: c for c in self.tree.list_children(inode)}
-        for name, c in kids.items():
-            cp = path.rstrip("/") + "/" + name
-            if name not in listing and c.is_persisted and not self.mount_table.is_mount_point(cp):
-                self.delete(cp, recursive=True, alluxio_only=True)
-                stats["removed"] += 1
-            elif name in listing and recursive:
-                sub = self.sync_metadata(cp, recursive)
-                for k in stats:
-                    stats[k] += sub[k]
-        new = [n for n in listing if n not in kids]
-        if new:
-            self.load_metadata(path, recursive=recursive, create_ancestors=False, quiet=True)
-            stats["added"] += len(new)
-        return stats
+        self._count("Master.MetadataSyncOps")
+        ex, pre = self._sync_pools()
+        conc = self.conf.get_int("alluxio.master.metadata.sync.concurrency.level", "6")
+        return InodeSyncStream(self, path, recursive, ex, pre, conc).run()
 
     def check_consistency(self, path: str, recursive: bool = True) -> list[str]:
         path = normalize_path(path)

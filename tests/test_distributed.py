@@ -211,3 +211,90 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert len(lines) == 1                      # rank 0 only
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "workers2" and out["config"]["verified"]
+
+
+COLLECTIVE_LOAD_SCRIPT = r"""
+import os, sys, json, time
+sys.path.insert(0, %(root)r)
+import numpy as np, torch.distributed as dist
+from alluxio_amd.conf import Configuration
+from alluxio_amd.master.process import AlluxioMasterProcess
+from alluxio_amd.worker.process import AlluxioWorkerProcess
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.parallel.transfer import TransferPlane
+from alluxio_amd.job import JobClient, LoadConfig
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=world)
+work = %(work)r
+conf = Configuration({"alluxio.master.journal.folder": work + "/journal",
+    "alluxio.worker.tieredstore.level0.dirs.path": "dram", "alluxio.worker.tieredstore.level0.dirs.quota": "128MB",
+    "alluxio.worker.hbm.page.size": "1MB", "alluxio.user.block.size.bytes.default": "2MB",
+    "alluxio.job.master.worker.heartbeat.interval": "20ms", "alluxio.worker.block.heartbeat.interval": "50ms"})
+box = [None]
+if rank == 0:
+    m = AlluxioMasterProcess(conf, host="127.0.0.1", port=0, root_ufs=work + "/ufs"); box[0] = m.start(start_heartbeats=False)
+dist.broadcast_object_list(box, src=0)
+w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, work_dir=work + "/w%%d" %% rank)
+w.start(start_heartbeats=True)
+plane = TransferPlane.establish(w.worker)
+fs = FileSystem(conf=conf.copy(), master_address=box[0])
+cached = np.random.default_rng(1).integers(0, 256, 5 * (1 << 20) + 11, dtype=np.uint8)
+ufs_only = np.random.default_rng(2).integers(0, 256, 3 * (1 << 20) + 5, dtype=np.uint8)
+if rank == 0:
+    fs.write_file("/dl/cached", cached, write_type="MUST_CACHE")      # blocks on worker 0 only
+    fs.write_file("/dl/ufs", ufs_only, write_type="THROUGH")          # blocks in no worker
+dist.barrier()
+# every worker's job worker must be registered before the job is planned
+deadline = time.time() + 60
+jc = JobClient(fs.ctx.master_channel())
+while len(jc.worker_health()) < world and time.time() < deadline:
+    time.sleep(0.05)
+if rank == 0:
+    status, result, err = jc.run_and_wait(LoadConfig(path="/dl", replication=-1), timeout=120)
+    open(work + "/job.json", "w").write(json.dumps([status, result, err]))
+while not os.path.exists(work + "/job.json"):
+    time.sleep(0.05)
+status, result, err = json.load(open(work + "/job.json"))
+blocks = []
+for p in ("/dl/cached", "/dl/ufs"):
+    blocks += [(b.blockInfo.blockId, b.blockInfo.length) for b in fs.get_status(p).info.fileBlockInfos]
+ok_all = all(w.worker.has_block(b) for b, _ in blocks)
+got = b"".join(w.worker.read_bytes(b, 0, n) for b, n in blocks)
+ok_bytes = got == cached.tobytes() + ufs_only.tobytes()
+print(json.dumps({"rank": rank, "status": status, "err": err, "all": ok_all, "bytes": bool(ok_bytes),
+                  "gathered": plane.bytes_gathered}), flush=True)
+time.sleep(0.3)
+fs.close(); w.stop()
+dist.barrier()
+if rank == 0:
+    m.stop()
+dist.destroy_process_group()
+"""
+
+
+def test_distributed_load_replication_all_uses_collective(tmp_path):
+    """``distributedLoad --replication`` >= worker count: owners load from the UFS, then every
+    worker receives every block through the transfer plane's all-gather (C4 on the product path)."""
+    script = COLLECTIVE_LOAD_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path)}
+    path = tmp_path / "cload.py"
+    path.write_text(script)
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, str(path)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            pytest.fail("collective load rank timed out")
+        assert p.returncode == 0, err[-3000:]
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+    for o in outs:
+        assert o["status"] == "COMPLETED", o
+        assert o["all"] and o["bytes"], o
+    # rank 0 already held the cached file, so it receives only rank 1's UFS-loaded blocks; rank 1
+    # receives the cached file plus rank 0's share of the UFS file -- both through the all-gather
+    assert all(o["gathered"] > 0 for o in outs), outs

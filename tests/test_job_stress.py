@@ -236,6 +236,11 @@ def test_replication_checker(cluster):
             break
         time.sleep(0.01)
     assert sum(w.worker.has_block(bid) for w in cluster.workers) == 2
+    for _ in range(300):         # the copy landed; let the job report COMPLETED before re-checking
+        if not rc._busy(bid):
+            break
+        cluster.drive_jobs()
+        time.sleep(0.01)
     cluster.heartbeat_workers()
     assert rc.heartbeat() == 0   # satisfied
     fs.set_attribute("/rep/f", replication_min=0, replication_max=1)
