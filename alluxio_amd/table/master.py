@@ -19,7 +19,7 @@ import time
 from ..journal.system import Journaled, NoopJournalContext
 from ..proto import enum_name, pb
 from ..utils.exceptions import (AlreadyExistsException, InvalidArgumentException, NotFoundException)
-from .udb import UdbPartition, create_udb
+from .udb import METASTORE_TYPES, UdbPartition, create_udb
 
 LOG = logging.getLogger(__name__)
 SVC_TABLE = "alluxio.grpc.table.TableMasterClientService"
@@ -159,9 +159,13 @@ class TableMaster(Journaled):
         with self._lock:
             if db_name in self.dbs:
                 raise AlreadyExistsException(f"database {db_name} already exists")
-            location = self._db_location(db_name, uri)
-            udb = create_udb(udb_type, self._fs(), location, udb_db or db_name, options)
+            metastore = (udb_type or "").lower() in METASTORE_TYPES
+            location = uri if metastore else self._db_location(db_name, uri)
+            udb = create_udb(udb_type, self._fs(), location, udb_db or db_name, options, catalog_db=db_name,
+                             catalog_path=self.catalog_path)
             info = udb.get_database_info()
+            if metastore:
+                location = info.get("location") or uri
             with self._ctx() as ctx:
                 a = pb.journal.AttachDbEntry(udb_type=udb_type, udb_connection_uri=uri, udb_db_name=udb_db,
                                              db_name=db_name)
@@ -193,7 +197,9 @@ class TableMaster(Journaled):
             d = self.dbs.get(db_name)
             if d is None:
                 raise NotFoundException(f"database {db_name} does not exist")
-            udb = create_udb(d["udb_type"], self._fs(), d["location"], d["udb_db"] or db_name, d["options"])
+            metastore = (d["udb_type"] or "").lower() in METASTORE_TYPES
+            udb = create_udb(d["udb_type"], self._fs(), d["uri"] if metastore else d["location"],
+                             d["udb_db"] or db_name, d["options"], catalog_db=db_name, catalog_path=self.catalog_path)
             return self._sync(db_name, udb, True)
 
     def _sync(self, db_name, udb, ignore_errors):

@@ -5,11 +5,11 @@ getTable, getDatabaseInfo), UdbTable.java (schema, partition columns, partitions
 UdbPartition / layout/HiveLayout.java, and table/server/underdb/hive (HiveDatabase: tables are
 directories of data files, partitions are ``key=value`` sub-directories).
 
-No Hive metastore or Glue endpoint exists in this environment, so the built-in UDB type is
-``fs``: a database is a directory (Alluxio path, or a UFS URI mounted under
+Metastore-backed UDBs (``hive`` over Thrift, ``glue`` over its JSON API) live in
+:mod:`table.metastore`.  The ``fs`` type needs no metastore: a database is a directory (Alluxio path, or a UFS URI mounted under
 ``/catalog/<db>/ufs``); each sub-directory is a table of Parquet (schema + column statistics from
 the footer) or CSV files (schema inferred, statistics computed); ``k=v`` sub-directories are
-partitions.  ``hive``/``glue`` are recognised names that fail with a clear error.
+partitions.
 """
 from __future__ import annotations
 
@@ -209,11 +209,21 @@ def read_table_bytes(data: bytes, fmt: str):
     return pq.read_table(io.BytesIO(data))
 
 
-def create_udb(udb_type: str, fs, location: str, db_name: str, options: dict | None = None) -> UnderDatabase:
+METASTORE_TYPES = ("hive", "glue")
+
+
+def create_udb(udb_type: str, fs, location: str, db_name: str, options: dict | None = None,
+               catalog_db: str | None = None, catalog_path: str = "/catalog") -> UnderDatabase:
+    """``location`` is the database directory for ``fs`` UDBs and the metastore connection URI
+    (``thrift://host:port`` / Glue region or endpoint) for ``hive`` / ``glue``; ``db_name`` is the
+    under-database's name and ``catalog_db`` the Alluxio catalog's name for it."""
     t = (udb_type or "fs").lower()
     if t in ("fs", "filesystem", "file", "parquet"):
         return FilesystemUnderDatabase(fs, location, db_name, options)
-    if t in ("hive", "glue"):
-        raise UnavailableException(f"udb type {t} needs a {t} metastore endpoint, which is not reachable from "
-                                   "this deployment; use udb type 'fs'")
+    if t == "hive":
+        from .metastore import HiveUnderDatabase
+        return HiveUnderDatabase(fs, location, catalog_db or db_name, db_name, options, catalog_path)
+    if t == "glue":
+        from .metastore import GlueUnderDatabase
+        return GlueUnderDatabase(fs, location, catalog_db or db_name, db_name, options, catalog_path)
     raise UnavailableException(f"unknown udb type {udb_type}")
