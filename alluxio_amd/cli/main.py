@@ -29,6 +29,7 @@ COMMAND is one of:
   runClass              Run the main function of a module (``pkg.module`` or ``pkg.module:function``).
   runTests              Run all end-to-end tests on an Alluxio cluster.
   runUfsTests --path P   Test an under storage against the UFS contract (UnderFileSystemContractTest).
+  yarn submit|status|stop  Run the cluster as YARN applications (ResourceManager REST API).
   upgradeJournal        Upgrade an Alluxio journal from v0 to v1 (-journalDirectoryV0 <dir>).
   stress                Run a stress benchmark (master|worker|client-io|ufs-io|max-throughput).
   validateConf          Validate Alluxio conf and exit.
@@ -205,6 +206,9 @@ def main(argv=None, out=None) -> int:
         return m(rest, out)
     if cmd == "runUfsTests":
         from .ufs_contract import main as m
+        return m(rest, out)
+    if cmd == "yarn":
+        from ..yarn import main as m
         return m(rest, out)
     if cmd == "upgradeJournal":
         from ..journal.upgrade import main as m
