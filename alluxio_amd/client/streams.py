@@ -561,7 +561,7 @@ class GrpcBlockWriter(BlockWriter):
             lib().batched_copy([(ptr, tmp.data_ptr(), length)], 0)
             data = tmp.cpu().numpy().tobytes()
         else:
-            data = ctypes.string_at(ptr, length)
+            data = _host_view(ptr, length)      # frames copy the bytes, so a view suffices
         mv = memoryview(data)
         for i in range(0, len(data), self.chunk):
             self._reqs.put(marshal.write_request_frame(mv[i:i + self.chunk]))
@@ -582,6 +582,12 @@ class GrpcBlockWriter(BlockWriter):
         except Exception:  # noqa: BLE001
             pass
         self._reqs.close()
+
+
+def _host_view(ptr: int, n: int) -> memoryview:
+    """A byte memoryview over host memory at ``ptr`` (no copy); valid while the owner lives."""
+    import ctypes
+    return memoryview((ctypes.c_ubyte * n).from_address(ptr)).cast("B")
 
 
 class UfsWriter:
@@ -709,15 +715,35 @@ class FileOutStream(io.RawIOBase):
         if self.through:
             if kind == DEVICE:
                 import torch
-                host = keep.detach().reshape(-1).view(torch.uint8).cpu().numpy().tobytes()
+                host = keep.detach().reshape(-1).view(torch.uint8).cpu().numpy()
             else:
-                import ctypes
-                host = ctypes.string_at(ptr, n)
+                host = _host_view(ptr, n)        # zero-copy view of the caller's buffer
+            if self.cache and n >= (4 << 20) and kind != DEVICE:
+                # CACHE_THROUGH: the UFS write (a syscall that drops the GIL, or frames for a worker)
+                # runs beside the copy into the cache tier; both finish before write() returns,
+                # so the caller's buffer is not used afterwards
+                t = threading.Thread(target=self._ufs_write_bg, args=(host,), daemon=True)
+                self._ufs_err = None
+                t.start()
+                try:
+                    self._write_cache(ptr, n, kind)
+                finally:
+                    t.join()
+                if self._ufs_err is not None:
+                    raise self._ufs_err
+                self._pos += n
+                return n
             self._ufs.write(host)
         if self.cache:
             self._write_cache(ptr, n, kind)
         self._pos += n
         return n
+
+    def _ufs_write_bg(self, host) -> None:
+        try:
+            self._ufs.write(host)
+        except BaseException as e:  # noqa: BLE001 - re-raised on the writing thread
+            self._ufs_err = e
 
     def _write_cache(self, ptr, n, kind):
         done = 0

@@ -255,3 +255,15 @@ def test_ufs_fallback_block_write(tmp_path):
                 assert f.read() == data
             assert os.listdir(blocks_dir) == []
         fs.close()
+
+
+def test_cache_through_ufs_copy_matches_after_free(cluster):
+    """CACHE_THROUGH writes the UFS copy beside the cache copy (zero-copy view of the caller's
+    buffer); after freeing the cached blocks the bytes come back from the UFS intact."""
+    fs = cluster.client()
+    data = np.random.default_rng(5).integers(0, 256, 13 * MB + 17, dtype=np.uint8)
+    fs.write_file("/ct/big", data, write_type="CACHE_THROUGH")
+    fs.free("/ct/big")
+    cluster.heartbeat_workers()
+    assert fs.read_file("/ct/big", read_type="NO_CACHE") == data.tobytes()
+    fs.close()
