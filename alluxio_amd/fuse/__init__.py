@@ -8,9 +8,8 @@ seek + loop), AlluxioFuseUtils.java (user/group ids, error mapping) and OpenFile
 
 ``AlluxioFuseOps`` is the operation layer in fusepy's ``Operations`` calling convention
 (``path``-based methods returning ints/dicts, raising ``FuseOSError(errno)``).  ``mount()``
-attaches it to a mountpoint through fusepy when that binding (and libfuse) is installed; this
-image ships neither, so tests drive the operation layer directly — the same methods a FUSE
-binding would call.  Reads of cached blocks are served by the page-gather kernel; a
+attaches it to a mountpoint through this package's own ``/dev/fuse`` protocol server
+(:mod:`alluxio_amd.fuse.kernel`: no libfuse or fusepy needed), or through fusepy when asked.  Reads of cached blocks are served by the page-gather kernel; a
 ``read_device`` extension fills a GPU tensor without a host bounce.
 """
 from __future__ import annotations
@@ -266,6 +265,15 @@ class AlluxioFuseOps:
         return len(data)
 
     def flush(self, path, fh):
+        """close(2) of a write handle completes the file, so a reader that opens it next sees
+        every byte (close-to-open consistency; the kernel's RELEASE arrives asynchronously)."""
+        with self._lock:
+            of = self._open.get(fh)
+        if of is not None and of.fout is not None:
+            with of.lock:
+                out, of.fout = of.fout, None
+                if out is not None:
+                    self._call(out.close)
         return 0
 
     def release(self, path, fh):
@@ -296,13 +304,27 @@ class AlluxioFuseOps:
                 pass
 
 
-def mount(ops: AlluxioFuseOps, mountpoint: str, foreground: bool = True, debug: bool = False):
-    """Attach ``ops`` at ``mountpoint`` through fusepy (needs the ``fuse`` module + libfuse)."""
+def mount(ops: AlluxioFuseOps, mountpoint: str, foreground: bool = True, debug: bool = False,
+          backend: str = "kernel", threads: int = 4):
+    """Attach ``ops`` at ``mountpoint``.  ``backend="kernel"`` (default) serves the ``/dev/fuse``
+    protocol directly (needs mount(2) permission: root or CAP_SYS_ADMIN); ``"fusepy"`` goes through
+    fusepy + libfuse when installed.  In the foreground the call serves until interrupted."""
+    if backend == "kernel":
+        from .kernel import mount_kernel
+        srv = mount_kernel(ops, mountpoint, threads=threads)
+        if not foreground:
+            return srv
+        try:
+            threading.Event().wait()
+        except KeyboardInterrupt:
+            pass
+        finally:
+            srv.unmount()
+        return srv
     try:
         import fuse as fusepy  # noqa: F401
     except ImportError as e:
-        raise RuntimeError("FUSE mounting needs the fusepy module and libfuse, which are not installed "
-                           "in this environment; use AlluxioFuseOps directly or install them") from e
+        raise RuntimeError("the fusepy backend needs the fusepy module and libfuse; use backend='kernel'") from e
 
     class _Bridge(fusepy.Operations):
         pass
