@@ -110,6 +110,7 @@ class AlluxioFuseOps:
             except KeyError:
                 pass
         return {"st_mode": mode, "st_nlink": 2 if i.folder else 1, "st_size": size, "st_uid": uid, "st_gid": gid,
+                "st_complete": bool(i.completed) and size == i.length,   # immutable from here on
                 "st_mtime": mtime, "st_ctime": mtime, "st_atime": (i.lastAccessTimeMs or i.lastModificationTimeMs) / 1000.0,
                 "st_blksize": i.blockSizeBytes or 4096, "st_blocks": (size + 511) // 512}
 

@@ -48,11 +48,13 @@ DIRENT = struct.Struct("<QQII")
 FATTR_MODE, FATTR_UID, FATTR_GID, FATTR_SIZE = 1 << 0, 1 << 1, 1 << 2, 1 << 3
 FATTR_ATIME, FATTR_MTIME = 1 << 4, 1 << 5
 FUSE_ASYNC_READ, FUSE_ATOMIC_O_TRUNC, FUSE_BIG_WRITES = 1 << 0, 1 << 3, 1 << 5
+FOPEN_KEEP_CACHE = 1 << 1
 MS_NOSUID, MS_NODEV = 2, 4
 MNT_DETACH = 2
 MAX_WRITE = 128 << 10
 ROOT_ID = 1
-TTL_S = 1
+TTL_S = 1              # directories / entries (the namespace can change under them)
+TTL_COMPLETE_S = 60    # attributes of completed (write-once, immutable) files
 
 
 def _ts(t: float) -> tuple[int, int]:
@@ -63,8 +65,10 @@ def _ts(t: float) -> tuple[int, int]:
 class FuseKernelServer:
     """Serve ``ops`` at ``mountpoint`` until :meth:`unmount`."""
 
-    def __init__(self, ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False):
+    def __init__(self, ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False,
+                 keep_cache: bool = True):
         self.ops = ops
+        self.keep_cache = keep_cache
         self.mountpoint = os.path.abspath(mountpoint)
         self.nthreads = max(1, threads)
         self.allow_other = allow_other
@@ -169,13 +173,17 @@ class FuseKernelServer:
 
     @staticmethod
     def _attr_ttl(a: dict) -> int:
-        # a file's size changes while it is written (and at completion): never cache its attrs
+        # a file's size changes while it is written (and at completion): cache attrs only once the
+        # file is complete -- Alluxio files are write-once, so a completed file's size is final
+        if a.get("st_complete"):
+            return TTL_COMPLETE_S
         return TTL_S if stat.S_ISDIR(a["st_mode"]) else 0
 
     def _entry(self, path: str) -> bytes:
         a = self.ops.getattr(path)
         nid = self._node(path)
-        return ENTRY_HEAD.pack(nid, 0, TTL_S, self._attr_ttl(a), 0, 0) + self._attr(nid, a)
+        ttl = self._attr_ttl(a)
+        return ENTRY_HEAD.pack(nid, 0, max(TTL_S, ttl), ttl, 0, 0) + self._attr(nid, a)
 
     # ---- request loop ------------------------------------------------------------------------
     def _loop(self) -> None:
@@ -297,8 +305,14 @@ class FuseKernelServer:
             return self._entry(path) + OPEN_OUT.pack(fh, 0, 0)
         if op == OPEN:
             flags = struct.unpack_from("<I", body)[0]
-            fh = ops.open(self._path(nodeid), flags)
-            return OPEN_OUT.pack(fh, 0, 0)
+            path = self._path(nodeid)
+            fh = ops.open(path, flags)
+            keep = 0
+            if flags & (os.O_WRONLY | os.O_RDWR) == 0 and self.keep_cache:
+                # completed files never change: keep the kernel page cache across opens
+                # (a second epoch over a dataset is served from it)
+                keep = FOPEN_KEEP_CACHE
+            return OPEN_OUT.pack(fh, keep, 0)
         if op == READ:
             fh, offset, size = READ_IN.unpack_from(body)[:3]
             return bytes(ops.read(self._path(nodeid), size, offset, fh))
@@ -364,6 +378,7 @@ class FuseKernelServer:
         raise FuseOSError(errno.ENOSYS)
 
 
-def mount_kernel(ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False) -> FuseKernelServer:
+def mount_kernel(ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False,
+                 keep_cache: bool = True) -> FuseKernelServer:
     """Mount ``ops`` at ``mountpoint`` through ``/dev/fuse``; returns the running server."""
-    return FuseKernelServer(ops, mountpoint, threads, allow_other).mount()
+    return FuseKernelServer(ops, mountpoint, threads, allow_other, keep_cache).mount()

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""BASELINE config 4 through FUSE: a PyTorch DataLoader random-reads ImageNet-shaped 128 KB files
+from an Alluxio FUSE mount (the reference's "TensorFlow/PyTorch via Alluxio FUSE" deployment,
+docs/en/compute/Deep-Learning.md:94-96, which reports "nearly 2X" over reading the remote store).
+
+    python tools/fuse_loader_bench.py --files 20000 --epochs 2 --workers 4 --out profiles/x.json
+
+Setup: one in-process master + worker (DRAM tier: the measurement is the FUSE path, not the
+device tier), the files written through the client API, the namespace mounted with this package's
+/dev/fuse server (fuse/kernel.py).  The same DataLoader then reads the same files from the UFS
+directory on local disk as the "storage without Alluxio" comparison.  Needs permission to
+mount(2) a FUSE filesystem (root / CAP_SYS_ADMIN); CPU only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+class FileDataset:
+    def __init__(self, paths):
+        self.paths = paths
+
+    def __len__(self):
+        return len(self.paths)
+
+    def __getitem__(self, i):
+        import numpy as np
+        import torch
+        with open(self.paths[i], "rb") as f:
+            b = f.read()
+        return torch.from_numpy(np.frombuffer(b, dtype=np.uint8)[:16].copy()), len(b)
+
+
+def _epochs(paths, epochs, workers, batch, seed=0):
+    import torch
+    from torch.utils.data import DataLoader, RandomSampler
+    out = []
+    for e in range(epochs):
+        g = torch.Generator().manual_seed(seed + e)
+        dl = DataLoader(FileDataset(paths), batch_size=batch, sampler=RandomSampler(paths, generator=g),
+                        num_workers=workers, persistent_workers=False)
+        t0 = time.perf_counter()
+        n = nbytes = 0
+        for _, lens in dl:
+            n += len(lens)
+            nbytes += int(lens.sum())
+        dt = time.perf_counter() - t0
+        out.append({"epoch": e, "files": n, "files_per_s": round(n / dt, 1), "GBps": round(nbytes / dt / 1e9, 3),
+                    "s": round(dt, 3)})
+        print(json.dumps(out[-1]), flush=True)
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--files", type=int, default=20000)
+    ap.add_argument("--file-size", type=int, default=128 << 10)
+    ap.add_argument("--dirs", type=int, default=100)
+    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--fuse-threads", type=int, default=2)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    import numpy as np
+    from alluxio_amd.fuse import AlluxioFuseOps
+    from alluxio_amd.fuse.kernel import mount_kernel
+    from alluxio_amd.minicluster import LocalAlluxioCluster
+    work = tempfile.mkdtemp(prefix="fusebench_")
+    mnt = os.path.join(work, "mnt")
+    os.makedirs(mnt)
+    quota = max(1 << 30, int(a.files * a.file_size * 1.3))
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "dram",
+            "alluxio.worker.tieredstore.level0.dirs.quota": str(quota),
+            "alluxio.user.block.size.bytes.default": "1MB", "alluxio.worker.hbm.page.size": "128KB"}
+    res = {"setup": f"{a.files} x {a.file_size} B files in {a.dirs} dirs, DataLoader workers={a.workers} "
+                    f"batch={a.batch}, FUSE threads={a.fuse_threads}, DRAM tier, {os.cpu_count()} CPUs"}
+    try:
+        with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=os.path.join(work, "c")) as c:
+            fs = c.client(metadata_cache=True)
+            rng = np.random.default_rng(0)
+            blob = rng.integers(0, 256, a.file_size + 4096, dtype=np.uint8)
+            rel = [f"d{i % a.dirs:03d}/f{i:07d}.jpg" for i in range(a.files)]
+            t0 = time.perf_counter()
+            for i, r in enumerate(rel):
+                fs.write_file("/ds/" + r, blob[i % 4096:i % 4096 + a.file_size], write_type="CACHE_THROUGH")
+            res["write_files_per_s"] = round(a.files / (time.perf_counter() - t0), 1)
+            srv = mount_kernel(AlluxioFuseOps(fs), mnt, threads=a.fuse_threads)
+            try:
+                paths = [os.path.join(mnt, "ds", r) for r in rel]
+                res["fuse"] = _epochs(paths, a.epochs, a.workers, a.batch)
+                res["fuse_requests"] = srv.requests
+            finally:
+                srv.unmount()
+            ufs_dir = c.master.fs_master.mount_table.resolve("/ds").uri
+            # the same files straight from the UFS directory on local disk, page cache dropped
+            # where permitted (the "storage without Alluxio" side of the comparison)
+            try:
+                with open("/proc/sys/vm/drop_caches", "w") as f:
+                    f.write("1\n")
+                res["ufs_page_cache_dropped"] = True
+            except OSError:
+                res["ufs_page_cache_dropped"] = False
+            res["ufs_direct"] = _epochs([os.path.join(ufs_dir, r) for r in rel], a.epochs, a.workers, a.batch)
+            fs.close()
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+    print(json.dumps(res))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
