@@ -259,6 +259,12 @@ __constant__ uint32_t c_crc_tab[8][256];
 __constant__ uint32_t c_x2n[64];  // x^(2^k) mod P, k = 0..63
 __constant__ uint32_t c_crc16[16][256];   // slicing-by-16 (zero-init CRC of a 16-byte word)
 __constant__ uint32_t c_shift4k[4][256];  // c -> c * x^(8*4096) mod P, byte-sliced
+__constant__ uint32_t c_lane_shift[256];  // x^(128*k) mod P: moves a lane's CRC k 16-B words right
+// v4 (11-bit slicing): chunk c of a 16-B word = bits [11c, 11c+11) -> its share of the word's CRC
+constexpr int kCrc4Threads = 1024;
+__constant__ uint32_t c_crc11[12][2048];
+__constant__ uint32_t c_shift16k[4][256];          // c -> c * x^(8*16384), byte-sliced
+__constant__ uint32_t c_lane_shift1k[kCrc4Threads];  // x^(128*k), k < 1024
 
 static void host_crc_tables(uint32_t tab[8][256], uint32_t x2n[64]) {
   for (uint32_t i = 0; i < 256; ++i) {
@@ -321,6 +327,34 @@ static hipError_t ensure_crc_tables() {
       g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_crc16), t16, sizeof(t16));
     if (g_crc_init_err == hipSuccess)
       g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_shift4k), sh, sizeof(sh));
+    // v4 tables: E[k] = CRC share of bit k of a 16-B word (byte j uses t16[15 - j])
+    static uint32_t t11[12][2048];
+    uint32_t e[128];
+    for (int k = 0; k < 128; ++k) e[k] = t16[15 - k / 8][1u << (k % 8)];
+    for (int c = 0; c < 12; ++c)
+      for (uint32_t v = 0; v < 2048; ++v) {
+        uint32_t x = 0;
+        for (int b = 0; b < 11; ++b)
+          if (((v >> b) & 1) && 11 * c + b < 128) x ^= e[11 * c + b];
+        t11[c][v] = x;
+      }
+    static uint32_t sh16k[4][256];
+    for (int b = 0; b < 4; ++b)
+      for (uint32_t i = 0; i < 256; ++i) sh16k[b][i] = host_gf2_mult(x2n[17], i << (8 * b));
+    static uint32_t lane1k[kCrc4Threads];
+    lane1k[0] = 1u << 31;
+    for (int k = 1; k < kCrc4Threads; ++k) lane1k[k] = host_gf2_mult(lane1k[k - 1], x2n[7]);
+    if (g_crc_init_err == hipSuccess)
+      g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_crc11), t11, sizeof(t11));
+    if (g_crc_init_err == hipSuccess)
+      g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_shift16k), sh16k, sizeof(sh16k));
+    if (g_crc_init_err == hipSuccess)
+      g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_lane_shift1k), lane1k, sizeof(lane1k));
+    static uint32_t lane_shift[256];
+    lane_shift[0] = 1u << 31;  // x^0
+    for (int k = 1; k < 256; ++k) lane_shift[k] = host_gf2_mult(lane_shift[k - 1], x2n[7]);  // * x^128
+    if (g_crc_init_err == hipSuccess)
+      g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_lane_shift), lane_shift, sizeof(lane_shift));
   });
   return g_crc_init_err;
 }
@@ -492,6 +526,208 @@ __global__ __launch_bounds__(kCrcThreads) void crc32c_segments_v2_kernel(
   }
 }
 
+// v3: the v2 schedule with the per-lane "move to final position" done by one multiply with a
+// precomputed x^(128*k) (k < 256 words: a lane's last word is always within the final stride)
+// instead of a square-and-multiply xpow8n per lane per segment -- that fold cost ~1/4 of the
+// VALU work of a 256 KiB segment.  Same raw (zero-init) segment CRC as v1/v2.
+__device__ __forceinline__ uint32_t seg_crc_v3(const uint8_t* __restrict__ seg, uint64_t seg_len,
+                                               const uint32_t (*t16)[256], const uint32_t (*sh)[256],
+                                               const uint32_t* lane_shift, uint32_t* part, int tid) {
+  const uint64_t nwords = seg_len >> 4;
+  uint32_t c = 0;
+  uint64_t last = ~0ull;
+  if ((((uintptr_t)seg) & 15) == 0) {
+    uint64_t wi = tid;
+    if (wi < nwords) {  // first word: nothing to shift yet
+      const uint4 v = *reinterpret_cast<const uint4*>(seg + (wi << 4));
+      c = t16[15][v.x & 255] ^ t16[14][(v.x >> 8) & 255] ^ t16[13][(v.x >> 16) & 255] ^ t16[12][v.x >> 24] ^
+          t16[11][v.y & 255] ^ t16[10][(v.y >> 8) & 255] ^ t16[9][(v.y >> 16) & 255] ^ t16[8][v.y >> 24] ^
+          t16[7][v.z & 255] ^ t16[6][(v.z >> 8) & 255] ^ t16[5][(v.z >> 16) & 255] ^ t16[4][v.z >> 24] ^
+          t16[3][v.w & 255] ^ t16[2][(v.w >> 8) & 255] ^ t16[1][(v.w >> 16) & 255] ^ t16[0][v.w >> 24];
+      last = wi;
+      wi += kCrcThreads;
+    }
+    for (; wi + 3 * kCrcThreads < nwords; wi += 4 * kCrcThreads) {
+      uint4 vv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) vv[u] = *reinterpret_cast<const uint4*>(seg + ((wi + u * kCrcThreads) << 4));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint4 v = vv[u];
+        const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+        c = s ^ t16[15][v.x & 255] ^ t16[14][(v.x >> 8) & 255] ^ t16[13][(v.x >> 16) & 255] ^ t16[12][v.x >> 24] ^
+            t16[11][v.y & 255] ^ t16[10][(v.y >> 8) & 255] ^ t16[9][(v.y >> 16) & 255] ^ t16[8][v.y >> 24] ^
+            t16[7][v.z & 255] ^ t16[6][(v.z >> 8) & 255] ^ t16[5][(v.z >> 16) & 255] ^ t16[4][v.z >> 24] ^
+            t16[3][v.w & 255] ^ t16[2][(v.w >> 8) & 255] ^ t16[1][(v.w >> 16) & 255] ^ t16[0][v.w >> 24];
+      }
+      last = wi + 3 * kCrcThreads;
+    }
+    for (; wi < nwords; wi += kCrcThreads) {
+      const uint4 v = *reinterpret_cast<const uint4*>(seg + (wi << 4));
+      const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+      c = s ^ t16[15][v.x & 255] ^ t16[14][(v.x >> 8) & 255] ^ t16[13][(v.x >> 16) & 255] ^ t16[12][v.x >> 24] ^
+          t16[11][v.y & 255] ^ t16[10][(v.y >> 8) & 255] ^ t16[9][(v.y >> 16) & 255] ^ t16[8][v.y >> 24] ^
+          t16[7][v.z & 255] ^ t16[6][(v.z >> 8) & 255] ^ t16[5][(v.z >> 16) & 255] ^ t16[4][v.z >> 24] ^
+          t16[3][v.w & 255] ^ t16[2][(v.w >> 8) & 255] ^ t16[1][(v.w >> 16) & 255] ^ t16[0][v.w >> 24];
+      last = wi;
+    }
+  } else {
+    for (uint64_t wi = tid; wi < nwords; wi += kCrcThreads) {
+      const uint8_t* q = seg + (wi << 4);
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) w ^= t16[15 - b][q[b]];
+      const uint32_t s = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+      c = (wi < (uint64_t)kCrcThreads ? 0u : s) ^ w;
+      last = wi;
+    }
+  }
+  uint32_t contrib = 0;
+  if (last != ~0ull) contrib = gf2_mult(lane_shift[nwords - 1 - last], c);  // nwords-1-last < kCrcThreads
+  part[tid] = contrib;
+  __syncthreads();
+  for (int s2 = kCrcThreads / 2; s2 > 0; s2 >>= 1) {
+    if (tid < s2) part[tid] ^= part[tid + s2];
+    __syncthreads();
+  }
+  uint32_t acc = 0;
+  if (tid == 0) {
+    acc = part[0];
+    const uint64_t tail = seg_len & 15;
+    if (tail) {
+      acc = gf2_mult(xpow8n(tail), acc);
+      uint32_t t = 0;
+      const uint8_t* q = seg + (nwords << 4);
+      for (uint64_t b = 0; b < tail; ++b) t = (t >> 8) ^ t16[0][(t ^ q[b]) & 255];
+      acc ^= t;
+    }
+  }
+  __syncthreads();
+  return acc;
+}
+
+static_assert(kCrcThreads <= 256, "lane shift table covers 256 words");
+
+__global__ __launch_bounds__(kCrcThreads) void crc32c_segments_v3_kernel(
+    const uint8_t* __restrict__ base, uint64_t total_bytes, uint64_t piece_bytes, uint64_t seg_bytes,
+    uint64_t segs_per_piece, uint64_t nsegs, uint32_t* __restrict__ seg_crc) {
+  __shared__ uint32_t t16[16][256];
+  __shared__ uint32_t sh[4][256];
+  __shared__ uint32_t lsh[kCrcThreads];
+  __shared__ uint32_t part[kCrcThreads];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 16 * 256; i += kCrcThreads) t16[i >> 8][i & 255] = c_crc16[i >> 8][i & 255];
+  for (int i = tid; i < 4 * 256; i += kCrcThreads) sh[i >> 8][i & 255] = c_shift4k[i >> 8][i & 255];
+  lsh[tid] = c_lane_shift[tid];
+  __syncthreads();
+  for (uint64_t g = blockIdx.x; g < nsegs; g += gridDim.x) {
+    const uint64_t piece = g / segs_per_piece;
+    const uint64_t seg_in_piece = g % segs_per_piece;
+    const uint64_t piece_start = piece * piece_bytes;
+    const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
+    const uint64_t seg_start = piece_start + seg_in_piece * seg_bytes;
+    const uint64_t seg_len = std::min(seg_bytes, piece_start + piece_len - seg_start);
+    const uint32_t acc = seg_crc_v3(base + seg_start, seg_len, t16, sh, lsh, part, tid);
+    if (tid == 0) seg_crc[g] = acc;
+  }
+}
+
+// v4: 11-bit slicing.  A 16-B word is 12 chunks of <= 11 bits; 12 lookups in 2048-entry tables
+// (96 KiB of LDS) replace the 16 byte-table lookups, and the running CRC shift is 4 lookups per
+// word as before: 16 LDS reads per 16 B instead of 20 (the kernel is bound by bank-conflicted LDS
+// reads).  1024-thread workgroups (16 waves share one table copy per CU), a lane's words are 16 KiB
+// apart (one wave reads 1 KiB contiguous), 1 MiB segments, grid sized to the CU count.
+constexpr uint64_t kCrcSeg4 = 1024 * 1024;
+constexpr int kCrc4Batch = 4;
+
+__device__ __forceinline__ uint32_t crc11_word(const uint4 v, const uint32_t (*t)[2048]) {
+  const uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  const uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  return t[0][lo & 2047] ^ t[1][(lo >> 11) & 2047] ^ t[2][(lo >> 22) & 2047] ^ t[3][(lo >> 33) & 2047] ^
+         t[4][(lo >> 44) & 2047] ^ t[5][((lo >> 55) | (hi << 9)) & 2047] ^ t[6][(hi >> 2) & 2047] ^
+         t[7][(hi >> 13) & 2047] ^ t[8][(hi >> 24) & 2047] ^ t[9][(hi >> 35) & 2047] ^
+         t[10][(hi >> 46) & 2047] ^ t[11][hi >> 57];
+}
+
+__global__ __launch_bounds__(kCrc4Threads) void crc32c_segments_v4_kernel(
+    const uint8_t* __restrict__ base, uint64_t total_bytes, uint64_t piece_bytes, uint64_t seg_bytes,
+    uint64_t segs_per_piece, uint64_t nsegs, uint32_t* __restrict__ seg_crc) {
+  __shared__ uint32_t t11[12][2048];
+  __shared__ uint32_t sh[4][256];
+  __shared__ uint32_t lsh[kCrc4Threads];
+  __shared__ uint32_t part[kCrc4Threads];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 12 * 2048; i += kCrc4Threads) t11[i >> 11][i & 2047] = c_crc11[i >> 11][i & 2047];
+  for (int i = tid; i < 4 * 256; i += kCrc4Threads) sh[i >> 8][i & 255] = c_shift16k[i >> 8][i & 255];
+  lsh[tid] = c_lane_shift1k[tid];
+  __syncthreads();
+  for (uint64_t g = blockIdx.x; g < nsegs; g += gridDim.x) {
+    const uint64_t piece = g / segs_per_piece;
+    const uint64_t seg_in_piece = g % segs_per_piece;
+    const uint64_t piece_start = piece * piece_bytes;
+    const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
+    const uint64_t seg_start = piece_start + seg_in_piece * seg_bytes;
+    const uint64_t seg_len = std::min(seg_bytes, piece_start + piece_len - seg_start);
+    const uint8_t* seg = base + seg_start;
+    const uint64_t nwords = seg_len >> 4;
+    uint32_t c = 0;
+    uint64_t last = ~0ull;
+    if ((((uintptr_t)seg) & 15) == 0) {
+      uint64_t wi = tid;
+      if (wi < nwords) {
+        c = crc11_word(*reinterpret_cast<const uint4*>(seg + (wi << 4)), t11);
+        last = wi;
+        wi += kCrc4Threads;
+      }
+      // kCrc4Batch words in flight per lane (16 waves per CU only): issue the loads, then fold
+      for (; wi + (kCrc4Batch - 1) * kCrc4Threads < nwords; wi += kCrc4Batch * kCrc4Threads) {
+        uint4 v[kCrc4Batch];
+#pragma unroll
+        for (int u = 0; u < kCrc4Batch; ++u) v[u] = *reinterpret_cast<const uint4*>(seg + ((wi + u * kCrc4Threads) << 4));
+#pragma unroll
+        for (int u = 0; u < kCrc4Batch; ++u)
+          c = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24] ^ crc11_word(v[u], t11);
+        last = wi + (kCrc4Batch - 1) * kCrc4Threads;
+      }
+      for (; wi < nwords; wi += kCrc4Threads) {
+        const uint4 v = *reinterpret_cast<const uint4*>(seg + (wi << 4));
+        c = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24] ^ crc11_word(v, t11);
+        last = wi;
+      }
+    } else {
+      for (uint64_t wi = tid; wi < nwords; wi += kCrc4Threads) {
+        const uint8_t* q = seg + (wi << 4);
+        uint4 v;
+        uint8_t* vb = reinterpret_cast<uint8_t*>(&v);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) vb[b] = q[b];
+        const uint32_t sft = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+        c = (wi < (uint64_t)kCrc4Threads ? 0u : sft) ^ crc11_word(v, t11);
+        last = wi;
+      }
+    }
+    part[tid] = last != ~0ull ? gf2_mult(lsh[nwords - 1 - last], c) : 0u;
+    __syncthreads();
+    for (int s2 = kCrc4Threads / 2; s2 > 0; s2 >>= 1) {
+      if (tid < s2) part[tid] ^= part[tid + s2];
+      __syncthreads();
+    }
+    if (tid == 0) {
+      uint32_t acc = part[0];
+      const uint64_t tail = seg_len & 15;
+      if (tail) {
+        acc = gf2_mult(xpow8n(tail), acc);
+        uint32_t t = 0;
+        const uint8_t* q = seg + (nwords << 4);
+        for (uint64_t b = 0; b < tail; ++b) t = (t >> 8) ^ c_crc16[0][(t ^ q[b]) & 255];
+        acc ^= t;
+      }
+      seg_crc[g] = acc;
+    }
+    __syncthreads();
+  }
+}
+
 // Gathered pieces (one page of many blocks each, <= kCrcSeg2 bytes): one workgroup per piece,
 // standard CRC32C per piece — the per-page CRCs of a whole batch of freshly cached blocks in
 // one launch instead of one launch + sync per block.
@@ -500,14 +736,16 @@ __global__ __launch_bounds__(kCrcThreads) void crc32c_gather_kernel(
     uint32_t* __restrict__ out) {
   __shared__ uint32_t t16[16][256];
   __shared__ uint32_t sh[4][256];
+  __shared__ uint32_t lsh[kCrcThreads];
   __shared__ uint32_t part[kCrcThreads];
   const int tid = threadIdx.x;
   for (int i = tid; i < 16 * 256; i += kCrcThreads) t16[i >> 8][i & 255] = c_crc16[i >> 8][i & 255];
   for (int i = tid; i < 4 * 256; i += kCrcThreads) sh[i >> 8][i & 255] = c_shift4k[i >> 8][i & 255];
+  lsh[tid] = c_lane_shift[tid];
   __syncthreads();
   for (uint64_t g = blockIdx.x; g < n; g += gridDim.x) {
     const uint64_t len = lens[g];
-    const uint32_t acc = seg_crc_v2(reinterpret_cast<const uint8_t*>(ptrs[g]), len, t16, sh, part, tid);
+    const uint32_t acc = seg_crc_v3(reinterpret_cast<const uint8_t*>(ptrs[g]), len, t16, sh, lsh, part, tid);
     if (tid == 0) out[g] = acc ^ gf2_mult(xpow8n(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
   }
 }
@@ -570,7 +808,8 @@ uint64_t crc32c_scratch_words(uint64_t total_bytes, uint64_t piece_bytes) {
   return npieces * spp;
 }
 
-static int g_crc_variant = 1;  // 0: per-lane contiguous strips (v1), 1: interleaved lanes (v2)
+static int g_crc_variant = 3;  // 0: per-lane contiguous strips (v1), 1: interleaved lanes (v2),
+                               // 2: v2 + table lane fold (v3), 3: 11-bit slicing, 1024 threads (v4)
 
 void set_crc_variant(int v) { g_crc_variant = v; }
 
@@ -581,7 +820,7 @@ hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint6
   hipError_t e = ensure_crc_tables();
   if (e != hipSuccess) return e;
   const uint64_t npieces = (total_bytes + piece_bytes - 1) / piece_bytes;
-  const uint64_t seg = g_crc_variant == 0 ? kCrcSeg : kCrcSeg2;
+  const uint64_t seg = g_crc_variant == 0 ? kCrcSeg : g_crc_variant == 3 ? std::min(kCrcSeg4, piece_bytes) : kCrcSeg2;
   const uint64_t spp = (piece_bytes + seg - 1) / seg;
   const uint64_t nsegs = npieces * spp;
   if (scratch_words < nsegs) return hipErrorInvalidValue;
@@ -589,8 +828,17 @@ hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint6
   if (g_crc_variant == 0) {
     hipLaunchKernelGGL(crc32c_segments_kernel, dim3(g1), dim3(kCrcThreads), 0, stream, base,
                        total_bytes, piece_bytes, spp, nsegs, scratch);
-  } else {
+  } else if (g_crc_variant == 1) {
     hipLaunchKernelGGL(crc32c_segments_v2_kernel, dim3(g1), dim3(kCrcThreads), 0, stream, base,
+                       total_bytes, piece_bytes, seg, spp, nsegs, scratch);
+  } else if (g_crc_variant == 2) {
+    hipLaunchKernelGGL(crc32c_segments_v3_kernel, dim3(g1), dim3(kCrcThreads), 0, stream, base,
+                       total_bytes, piece_bytes, seg, spp, nsegs, scratch);
+  } else {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const unsigned g4 = (unsigned)std::min<uint64_t>(nsegs, (uint64_t)cus);   // one 110 KiB-LDS WG per CU
+    hipLaunchKernelGGL(crc32c_segments_v4_kernel, dim3(g4), dim3(kCrc4Threads), 0, stream, base,
                        total_bytes, piece_bytes, seg, spp, nsegs, scratch);
   }
   e = hipGetLastError();

@@ -42,7 +42,7 @@ def test_batched_copy_exact(gpu):
         assert torch.equal(src[o:o + n], dst[o:o + n])
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_crc32c_matches_host(gpu, variant):
     import torch
     C = lib()
@@ -55,7 +55,7 @@ def test_crc32c_matches_host(gpu, variant):
         p = piece or nbytes
         want = [C.crc32c(host[i:i + p]) for i in range(0, nbytes, p)]
         assert got == want, (variant, nbytes, piece)
-    C.set_crc_variant(1)
+    C.set_crc_variant(3)
 
 
 @pytest.mark.parametrize("variant", [-1] + list(range(19)))
