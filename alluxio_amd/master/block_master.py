@@ -282,6 +282,29 @@ class BlockMaster(Journaled):
         if ctx is not None:
             ctx.close()
 
+    def commit_blocks(self, wid: int, blocks) -> None:
+        """``commit_block`` for a batch of ``(block id, length, tier, medium, used bytes on tier)``
+        from one worker: one lock section and one journal context (one flush) for the lot."""
+        ctx = None
+        with self._lock:
+            w = self._registered.get_first_by_field("id", wid)
+            if w is None:
+                raise NotFoundException(f"worker {wid} is not registered")
+            for block_id, length, tier, medium, used in blocks:
+                m = self._blocks.get(block_id)
+                if m is None or m.length != length:
+                    e = pb.journal.JournalEntry(block_info=pb.journal.BlockInfoEntry(block_id=block_id,
+                                                                                     length=length))
+                    self.process_journal_entry(e)
+                    if ctx is None:
+                        ctx = self._ctx()
+                    ctx.append(e)
+                self._add_location(w, block_id, tier, medium)
+                w.used[tier] = used
+            w.last_updated_ms = int(time.time() * 1000)
+        if ctx is not None:
+            ctx.close()
+
     def commit_block_in_ufs(self, block_id: int, length: int) -> None:
         self.commit_blocks_in_ufs([(block_id, length)])
 

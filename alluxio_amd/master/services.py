@@ -271,6 +271,12 @@ class BlockMasterWorkerServiceHandler:
         self.m.commit_block(req.workerId, req.usedBytesOnTier, req.tierAlias, req.mediumType, req.blockId, req.length)
         return pb.block.CommitBlockPResponse()
 
+    def CommitBlocks(self, req, ctx):
+        """Extension: a batch of CommitBlock reports in one call (bulk UFS ingest)."""
+        self.m.commit_blocks(req.workerId, [(b.blockId, b.length, b.tierAlias, b.mediumType, b.usedBytesOnTier)
+                                            for b in req.blocks])
+        return pb.block.CommitBlocksPResponse()
+
     def CommitBlockInUfs(self, req, ctx):
         self.m.commit_block_in_ufs(req.blockId, req.length)
         return pb.block.CommitBlockInUfsPResponse()

@@ -100,6 +100,8 @@ msg CommitBlockPOptions
 msg CommitBlockPRequest workerId=1:i64 usedBytesOnTier=2:i64 tierAlias=3:str blockId=4:i64
     length=5:i64 options=6:CommitBlockPOptions mediumType=7:str
 msg CommitBlockPResponse
+msg CommitBlocksPRequest workerId=1001:i64 blocks=1002:CommitBlockPRequest*
+msg CommitBlocksPResponse
 msg CommitBlockInUfsPOptions
 msg CommitBlockInUfsPRequest blockId=1:i64 length=2:i64 options=3:CommitBlockInUfsPOptions
 msg CommitBlockInUfsPResponse
@@ -123,6 +125,7 @@ rpc BlockMasterClientService GetWorkerLostStorage GetWorkerLostStoragePOptions G
 rpc BlockMasterWorkerService BlockHeartbeat BlockHeartbeatPRequest BlockHeartbeatPResponse
 rpc BlockMasterWorkerService CommitBlock CommitBlockPRequest CommitBlockPResponse
 rpc BlockMasterWorkerService CommitBlockInUfs CommitBlockInUfsPRequest CommitBlockInUfsPResponse
+rpc BlockMasterWorkerService CommitBlocks CommitBlocksPRequest CommitBlocksPResponse
 rpc BlockMasterWorkerService GetWorkerId GetWorkerIdPRequest GetWorkerIdPResponse
 rpc BlockMasterWorkerService RegisterWorker RegisterWorkerPRequest RegisterWorkerPResponse
 """

@@ -519,16 +519,18 @@ class BlockWorker:
             ok = [b for b, st in zip(native_ids, status) if st == 0]
             crcs = self._crcs_of(ok)
             t2 = time.perf_counter()
+            committed = []
             for bid, st, n in zip(native_ids, status, lens):
                 if st == 0:
                     done += 1
                     self.metrics.counter("BytesReadUfsAll").inc(n)
                     self.metrics.counter("UfsIngestBytes").inc(n)
-                    self._report_commit(bid, crcs.get(bid))
+                    committed.append(bid)
                 elif st == 2:
                     LOG.warning("bulk cache: UFS read of block %d failed", bid)
                 elif st == 3:
                     slow.append((bid, None))      # no space in one go: leave it to the slow path below
+            self._report_commits(committed, crcs)
             bs = self.bulk_stats
             bs["native_s"] += t1 - t0
             bs["crc_s"] += t2 - t1
@@ -574,6 +576,39 @@ class BlockWorker:
                 workerId=self.worker_id, usedBytesOnTier=self.store.used_by_tier().get(info.tier_alias, 0),
                 tierAlias=info.tier_alias, blockId=block_id, length=info.length, mediumType=info.medium))
         self.metrics.counter("BlocksCommitted").inc()
+
+    def _report_commits(self, block_ids, crcs: dict) -> None:
+        """``_report_commit`` for a batch of freshly committed blocks: one CommitBlocks call per
+        4096 blocks (falls back to per-block CommitBlock against a master without the extension)."""
+        if not block_ids:
+            return
+        infos = self.native.block_infos(block_ids) if hasattr(self.native, "block_infos") else \
+            [self.native.block_info(b) for b in block_ids]
+        used = self.store.used_by_tier()
+        reqs = []
+        for bid, info in zip(block_ids, infos):
+            crc = crcs.get(bid)
+            if crc is not None:
+                self.crc[bid] = crc
+                self.metrics.counter("Crc32cBytes").inc(info.length)
+            elif self.crc_enabled or (self.crc_device and info.medium == "HBM"):
+                self.crc[bid] = (self.native.block_pages(bid)[2], self.native.checksum(bid, 0))
+                self.metrics.counter("Crc32cBytes").inc(info.length)
+            reqs.append(pb.block.CommitBlockPRequest(
+                workerId=self.worker_id, usedBytesOnTier=used.get(info.tier_alias, 0), tierAlias=info.tier_alias,
+                blockId=bid, length=info.length, mediumType=info.medium))
+        bm = self._bm()
+        if bm is not None and self.worker_id != ids.INVALID_WORKER_ID:
+            for i in range(0, len(reqs), 4096):
+                chunk = reqs[i:i + 4096]
+                try:
+                    bm.CommitBlocks(pb.block.CommitBlocksPRequest(workerId=self.worker_id, blocks=chunk))
+                except Exception as e:  # noqa: BLE001 - a master without the extension RPC
+                    if "UNIMPLEMENTED" not in str(e).upper() and "unknown method" not in str(e).lower():
+                        raise
+                    for r in chunk:
+                        bm.CommitBlock(r)
+        self.metrics.counter("BlocksCommitted").inc(len(reqs))
 
     def async_cache(self, block_id: int, opts=None, source=None, length: int | None = None) -> bool:
         """Deduplicated background caching; returns False if already queued/cached."""

@@ -251,7 +251,8 @@ while len(jc.worker_health()) < world and time.time() < deadline:
     time.sleep(0.05)
 if rank == 0:
     status, result, err = jc.run_and_wait(LoadConfig(path="/dl", replication=-1), timeout=120)
-    open(work + "/job.json", "w").write(json.dumps([status, result, err]))
+    open(work + "/job.json.tmp", "w").write(json.dumps([status, result, err]))
+    os.replace(work + "/job.json.tmp", work + "/job.json")      # readers never see a partial file
 while not os.path.exists(work + "/job.json"):
     time.sleep(0.05)
 status, result, err = json.load(open(work + "/job.json"))
