@@ -282,26 +282,41 @@ class BlockMaster(Journaled):
         if ctx is not None:
             ctx.close()
 
-    def commit_blocks(self, wid: int, blocks) -> None:
-        """``commit_block`` for a batch of ``(block id, length, tier, medium, used bytes on tier)``
-        from one worker: one lock section and one journal context (one flush) for the lot."""
+    def commit_blocks(self, wid: int, block_ids, lengths, tier_index, tiers, mediums, used_on_tiers) -> None:
+        """``commit_block`` for a batch from one worker (parallel arrays; ``tier_index[i]`` names
+        ``tiers[k]`` / ``mediums[k]``): one lock section, one journal context (one flush) and one
+        location-epoch bump for the lot -- the bulk-ingest commit path of ~100k blocks."""
         ctx = None
+        changed = False
         with self._lock:
             w = self._registered.get_first_by_field("id", wid)
             if w is None:
                 raise NotFoundException(f"worker {wid} is not registered")
-            for block_id, length, tier, medium, used in blocks:
-                m = self._blocks.get(block_id)
+            blocks, wblocks, lost = self._blocks, w.blocks, self._lost_blocks
+            locs = [(t, m) for t, m in zip(tiers, mediums)]
+            for bid, length, ti in zip(block_ids, lengths, tier_index):
+                m = blocks.get(bid)
                 if m is None or m.length != length:
-                    e = pb.journal.JournalEntry(block_info=pb.journal.BlockInfoEntry(block_id=block_id,
-                                                                                     length=length))
+                    e = pb.journal.JournalEntry(block_info=pb.journal.BlockInfoEntry(block_id=bid, length=length))
                     self.process_journal_entry(e)
                     if ctx is None:
                         ctx = self._ctx()
                     ctx.append(e)
-                self._add_location(w, block_id, tier, medium)
-                w.used[tier] = used
+                    m = blocks.get(bid)
+                    if m is None:
+                        w.to_remove.add(bid)
+                        continue
+                loc = locs[ti]
+                if m.locations.get(w.id) != loc:
+                    m.locations[w.id] = loc
+                    changed = True
+                wblocks.add(bid)
+                lost.discard(bid)
+            for t, used in used_on_tiers.items():
+                w.used[t] = used
             w.last_updated_ms = int(time.time() * 1000)
+            if changed:
+                self._bump_epoch()
         if ctx is not None:
             ctx.close()
 

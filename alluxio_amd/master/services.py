@@ -273,8 +273,8 @@ class BlockMasterWorkerServiceHandler:
 
     def CommitBlocks(self, req, ctx):
         """Extension: a batch of CommitBlock reports in one call (bulk UFS ingest)."""
-        self.m.commit_blocks(req.workerId, [(b.blockId, b.length, b.tierAlias, b.mediumType, b.usedBytesOnTier)
-                                            for b in req.blocks])
+        self.m.commit_blocks(req.workerId, list(req.blockIds), list(req.lengths), list(req.tierIndex),
+                             list(req.tiers), list(req.mediums), dict(req.usedBytesOnTiers))
         return pb.block.CommitBlocksPResponse()
 
     def CommitBlockInUfs(self, req, ctx):

@@ -100,7 +100,8 @@ msg CommitBlockPOptions
 msg CommitBlockPRequest workerId=1:i64 usedBytesOnTier=2:i64 tierAlias=3:str blockId=4:i64
     length=5:i64 options=6:CommitBlockPOptions mediumType=7:str
 msg CommitBlockPResponse
-msg CommitBlocksPRequest workerId=1001:i64 blocks=1002:CommitBlockPRequest*
+msg CommitBlocksPRequest workerId=1001:i64 blockIds=1002:i64* lengths=1003:i64* tierIndex=1004:i32*
+    tiers=1005:str* mediums=1006:str* usedBytesOnTiers=1007:{str,i64}
 msg CommitBlocksPResponse
 msg CommitBlockInUfsPOptions
 msg CommitBlockInUfsPRequest blockId=1:i64 length=2:i64 options=3:CommitBlockInUfsPOptions

@@ -579,36 +579,51 @@ class BlockWorker:
 
     def _report_commits(self, block_ids, crcs: dict) -> None:
         """``_report_commit`` for a batch of freshly committed blocks: one CommitBlocks call per
-        4096 blocks (falls back to per-block CommitBlock against a master without the extension)."""
+        16384 blocks with parallel arrays (falls back to per-block CommitBlock against a master
+        without the extension)."""
         if not block_ids:
             return
-        infos = self.native.block_infos(block_ids) if hasattr(self.native, "block_infos") else \
-            [self.native.block_info(b) for b in block_ids]
-        used = self.store.used_by_tier()
-        reqs = []
-        for bid, info in zip(block_ids, infos):
+        native = self.native
+        ids_, lens, tix, tiers, mediums, index = [], [], [], [], [], {}
+        crc_bytes = 0
+        for bid in block_ids:
+            info = native.block_info(bid)
+            key = (info.tier_alias, info.medium)
+            k = index.get(key)
+            if k is None:
+                k = index[key] = len(tiers)
+                tiers.append(info.tier_alias)
+                mediums.append(info.medium)
+            ids_.append(bid)
+            lens.append(info.length)
+            tix.append(k)
             crc = crcs.get(bid)
             if crc is not None:
                 self.crc[bid] = crc
-                self.metrics.counter("Crc32cBytes").inc(info.length)
+                crc_bytes += info.length
             elif self.crc_enabled or (self.crc_device and info.medium == "HBM"):
-                self.crc[bid] = (self.native.block_pages(bid)[2], self.native.checksum(bid, 0))
-                self.metrics.counter("Crc32cBytes").inc(info.length)
-            reqs.append(pb.block.CommitBlockPRequest(
-                workerId=self.worker_id, usedBytesOnTier=used.get(info.tier_alias, 0), tierAlias=info.tier_alias,
-                blockId=bid, length=info.length, mediumType=info.medium))
+                self.crc[bid] = (native.block_pages(bid)[2], native.checksum(bid, 0))
+                crc_bytes += info.length
+        if crc_bytes:
+            self.metrics.counter("Crc32cBytes").inc(crc_bytes)
         bm = self._bm()
         if bm is not None and self.worker_id != ids.INVALID_WORKER_ID:
-            for i in range(0, len(reqs), 4096):
-                chunk = reqs[i:i + 4096]
+            used = self.store.used_by_tier()
+            step = 16384
+            for i in range(0, len(ids_), step):
+                req = pb.block.CommitBlocksPRequest(workerId=self.worker_id, blockIds=ids_[i:i + step],
+                                                    lengths=lens[i:i + step], tierIndex=tix[i:i + step],
+                                                    tiers=tiers, mediums=mediums, usedBytesOnTiers=used)
                 try:
-                    bm.CommitBlocks(pb.block.CommitBlocksPRequest(workerId=self.worker_id, blocks=chunk))
+                    bm.CommitBlocks(req)
                 except Exception as e:  # noqa: BLE001 - a master without the extension RPC
                     if "UNIMPLEMENTED" not in str(e).upper() and "unknown method" not in str(e).lower():
                         raise
-                    for r in chunk:
-                        bm.CommitBlock(r)
-        self.metrics.counter("BlocksCommitted").inc(len(reqs))
+                    for bid, n, k in zip(ids_[i:i + step], lens[i:i + step], tix[i:i + step]):
+                        bm.CommitBlock(pb.block.CommitBlockPRequest(
+                            workerId=self.worker_id, usedBytesOnTier=used.get(tiers[k], 0), tierAlias=tiers[k],
+                            blockId=bid, length=n, mediumType=mediums[k]))
+        self.metrics.counter("BlocksCommitted").inc(len(ids_))
 
     def async_cache(self, block_id: int, opts=None, source=None, length: int | None = None) -> bool:
         """Deduplicated background caching; returns False if already queued/cached."""
