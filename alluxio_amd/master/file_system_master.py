@@ -1027,8 +1027,6 @@ class FileSystemMaster(Journaled):
             return
         fid = ids.create_file_id(self.block_master.get_new_container_id())
         bs = self.default_block_size
-        e = self.tree.new_file_entry(parent, name, fid, owner, group, st.mode or 0o644, bs, PERSISTED)
-        self._apply(rpc, e)
         length = st.content_length
         blocks = []
         rem, seq = length, 0
@@ -1042,11 +1040,16 @@ class FileSystemMaster(Journaled):
             rem -= min(rem, bs)
             seq += 1
         from ..underfs.base import Fingerprint as FP
-        self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
-            id=fid, ufs_fingerprint=FP.create(res.ufs.ufs_type, st).serialize(),
-            last_modification_time_ms=st.last_modified_ms or rpc.op_time_ms, overwrite_modification_time=True)))
-        self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
-            id=fid, completed=True, length=length, set_blocks=blocks)))
+        # one journal entry per loaded file: the InodeFile already complete (length, blocks, UFS
+        # fingerprint, UFS mtime) instead of create + UpdateInode + UpdateInodeFile
+        e = self.tree.new_file_entry(parent, name, fid, owner, group, st.mode or 0o644, bs, PERSISTED)
+        f = e.inode_file
+        f.completed = True
+        f.length = length
+        f.blocks.extend(blocks)
+        f.ufs_fingerprint = FP.create(res.ufs.ufs_type, st).serialize()
+        f.last_modification_time_ms = st.last_modified_ms or rpc.op_time_ms
+        self._apply(rpc, e)
 
     def _load_children(self, rpc, inode, path, recursive, owner_default, group_default, cache=None) -> None:
         stack = [(inode, path)]
