@@ -24,7 +24,14 @@ def strip_scheme(path: str) -> str:
     return path or "/"
 
 
+_IDS: dict = {}   # (uid, gid) -> (owner, group): NSS lookups once per id pair, not per file
+
+
 def _owner(st) -> tuple[str, str]:
+    key = (st.st_uid, st.st_gid)
+    hit = _IDS.get(key)
+    if hit is not None:
+        return hit
     try:
         owner = pwd.getpwuid(st.st_uid).pw_name
     except KeyError:
@@ -33,6 +40,8 @@ def _owner(st) -> tuple[str, str]:
         group = grp.getgrgid(st.st_gid).gr_name
     except KeyError:
         group = str(st.st_gid)
+    if len(_IDS) < 4096:
+        _IDS[key] = (owner, group)
     return owner, group
 
 
