@@ -235,7 +235,11 @@ class AlluxioMasterProcess:
         UNAVAILABLE, and gain primacy when elected (FaultTolerantAlluxioMasterProcess)."""
         from .. import metrics as msys
         from ..journal.raft_system import RaftJournalSystem
+        from ..utils.pause_monitor import from_conf as pause_monitor
         self._sinks = msys.load_sinks(self.conf, self.metrics)
+        self.pause_monitor = pause_monitor(self.conf, "master", self.metrics)
+        if self.pause_monitor is not None:
+            self.pause_monitor.start()
         raft = isinstance(self.journal, RaftJournalSystem)
         if not self.journal.is_formatted() and isinstance(self.journal, (UfsJournalSystem, RaftJournalSystem)):
             self.journal.format()
@@ -385,6 +389,8 @@ class AlluxioMasterProcess:
     def stop(self) -> None:
         for sk in getattr(self, "_sinks", []):
             sk.stop()
+        if getattr(self, "pause_monitor", None) is not None:
+            self.pause_monitor.stop()
         # no new elections from here on, but keep the primary lock until the journal writers are
         # closed: releasing it first lets a standby start writing the same logs while this
         # master still completes its current log file

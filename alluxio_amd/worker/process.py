@@ -149,7 +149,11 @@ class AlluxioWorkerProcess:
 
     def start(self, register: bool = True, start_heartbeats: bool = True) -> str:
         from .. import metrics as msys
+        from ..utils.pause_monitor import from_conf as pause_monitor
         self._sinks = msys.load_sinks(self.conf, self.worker.metrics)
+        self.pause_monitor = pause_monitor(self.conf, "worker", self.worker.metrics)
+        if self.pause_monitor is not None:
+            self.pause_monitor.start()
         addr = self.server.start()
         host, port = addr.rsplit(":", 1)
         ti = pb.grpc.TieredIdentity(tiers=[pb.grpc.LocalityTier(tierName="node", value=socket.gethostname()),
@@ -253,6 +257,8 @@ class AlluxioWorkerProcess:
     def stop(self) -> None:
         for sk in getattr(self, "_sinks", []):
             sk.stop()
+        if getattr(self, "pause_monitor", None) is not None:
+            self.pause_monitor.stop()
         for t in self._threads:
             t.shutdown(join=False)
         for t in self._threads:

@@ -16,6 +16,7 @@ from __future__ import annotations
 import logging
 import os
 import threading
+import time
 
 from ..proto import enum_name, pb
 from ..rpc import marshal
@@ -24,6 +25,7 @@ from ..utils.exceptions import (BlockDoesNotExistException, InvalidArgumentExcep
                                 UnavailableException)
 
 LOG = logging.getLogger(__name__)
+_SLOW_READ_LOG = None   # SamplingLogger: one slow-read warning per 5 minutes (BlockReadHandler.java:63)
 
 SVC_BLOCK_WORKER = "alluxio.grpc.block.BlockWorker"
 
@@ -34,6 +36,11 @@ class BlockWorkerService:
         self.conf = conf
         self.max_chunk = conf.get_bytes("alluxio.worker.network.reader.max.chunk.size.bytes")
         self.window = conf.get_bytes("alluxio.worker.network.reader.buffer.size")
+        self.slow_read_s = conf.get_ms("alluxio.worker.remote.io.slow.threshold") / 1000.0
+        global _SLOW_READ_LOG
+        if _SLOW_READ_LOG is None:
+            from ..utils.pause_monitor import SamplingLogger
+            _SLOW_READ_LOG = SamplingLogger(LOG, 300.0)
         self._device_locks: dict[int, tuple[int, int]] = {}
         self._lock = threading.Lock()
 
@@ -103,7 +110,13 @@ class BlockWorkerService:
                     while pos - acked[0] >= self.window and not done.is_set():
                         cond.wait(0.5)
                 n = min(chunk, end - pos)
+                t_buf = time.monotonic()
                 frame = self.w.read_frame(bid, pos, n)      # header + bytes, sent as-is
+                took = time.monotonic() - t_buf
+                if took >= self.slow_read_s:                # BlockReadHandler.java:136-150
+                    _SLOW_READ_LOG.warning("Getting buffer for remote read took longer than %d ms. "
+                                           "block=%d offset=%d length=%d took=%d ms", int(self.slow_read_s * 1000),
+                                           bid, pos, n, int(took * 1000), key="slow-read")
                 pos += n
                 read_counter.inc(n)
                 yield frame
