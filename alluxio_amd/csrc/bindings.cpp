@@ -509,10 +509,11 @@ PYBIND11_MODULE(_C, m) {
       .def("epoch", &FrameRpcServer::epoch)
       .def("bump_epoch", &FrameRpcServer::bump_epoch)
       .def("cache_put", [](FrameRpcServer& s, uint32_t method, const std::string& user, py::bytes request,
-                           py::bytes reply, uint64_t ep) {
+                           py::bytes reply, uint64_t ep, int status, const std::string& msg) {
              std::string rq = request, rp = reply;
-             s.cache_put(method, user, rq, rp, ep);
-           })
+             s.cache_put(method, user, rq, rp, ep, status, msg);
+           }, py::arg("method"), py::arg("user"), py::arg("request"), py::arg("reply"), py::arg("epoch"),
+           py::arg("status") = 0, py::arg("msg") = std::string())
       .def("cache_clear", &FrameRpcServer::cache_clear)
       .def("set_cache_capacity", &FrameRpcServer::set_cache_capacity)
       .def_property_readonly("cache_size", &FrameRpcServer::cache_size)

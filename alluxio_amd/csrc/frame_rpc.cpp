@@ -146,7 +146,7 @@ void FrameRpcServer::set_cacheable(uint32_t method, bool on) {
   if (method < cacheable_.size()) cacheable_[method] = on ? 1 : 0;
 }
 
-bool FrameRpcServer::cache_get(const std::string& key, std::string* reply) {
+bool FrameRpcServer::cache_get(const std::string& key, CachedReply* reply) {
   const uint64_t ep = epoch();
   CacheShard& sh = shards_[std::hash<std::string>{}(key) % kShards];
   std::lock_guard<std::mutex> g(sh.mu);
@@ -162,7 +162,7 @@ bool FrameRpcServer::cache_get(const std::string& key, std::string* reply) {
 }
 
 void FrameRpcServer::cache_put(uint32_t method, const std::string& user, const std::string& request,
-                               const std::string& reply, uint64_t ep) {
+                               const std::string& reply, uint64_t ep, int status, const std::string& msg) {
   if (method >= cacheable_.size() || !cacheable_[method]) return;
   if (ep != epoch()) return;   // something changed while the reply was computed
   std::string key = cache_key(method, user, request.data(), request.size());
@@ -174,7 +174,10 @@ void FrameRpcServer::cache_put(uint32_t method, const std::string& user, const s
     sh.epoch = ep;
   }
   if (sh.map.size() >= cache_cap_ / kShards + 1) sh.map.clear();
-  sh.map[std::move(key)] = reply;
+  CachedReply& r = sh.map[std::move(key)];
+  r.status = status;
+  r.msg = msg;
+  r.body = reply;
 }
 
 void FrameRpcServer::cache_clear() {
@@ -363,10 +366,10 @@ void FrameRpcServer::on_readable(const std::shared_ptr<Conn>& c, int ep) {
       std::lock_guard<std::mutex> g(c->wmu);
       send_all(c->fd, resp.data(), resp.size(), 5000);
     } else if (cacheable_[it->second] && [&] {
-                 std::string reply;
+                 CachedReply reply;
                  const std::string key = cache_key(it->second, user, p + 6 + plen, len - 6 - plen);
                  if (!cache_get(key, &reply)) return false;
-                 const std::string resp = make_response(call_id, 0, std::string(), reply);
+                 const std::string resp = make_response(call_id, reply.status, reply.msg, reply.body);
                  requests_.fetch_add(1, std::memory_order_relaxed);
                  cache_hits_.fetch_add(1, std::memory_order_relaxed);
                  std::lock_guard<std::mutex> g(c->wmu);

@@ -62,7 +62,7 @@ class FrameRpcServer {
   uint64_t epoch() const { return epoch_.load(std::memory_order_acquire); }
   void bump_epoch() { epoch_.fetch_add(1, std::memory_order_acq_rel); }
   void cache_put(uint32_t method, const std::string& user, const std::string& request, const std::string& reply,
-                 uint64_t epoch);
+                 uint64_t epoch, int status = 0, const std::string& msg = std::string());
   void cache_clear();
   uint64_t cache_hits() const { return cache_hits_.load(); }
   size_t cache_size();
@@ -99,7 +99,13 @@ class FrameRpcServer {
   int wake_fd_ = -1;
 
   static std::string cache_key(uint32_t method, const std::string& user, const char* req, size_t n);
-  bool cache_get(const std::string& key, std::string* reply);
+  // a cached reply: status 0 + body, or an error status + message (NOT_FOUND lookups)
+  struct CachedReply {
+    int status = 0;
+    std::string msg;
+    std::string body;
+  };
+  bool cache_get(const std::string& key, CachedReply* reply);
   struct CacheEntry {
     uint64_t epoch;
     std::string reply;
@@ -107,7 +113,7 @@ class FrameRpcServer {
   struct CacheShard {
     std::mutex mu;
     uint64_t epoch = 0;   // entries are all of this epoch; a newer put/get resets the shard
-    std::unordered_map<std::string, std::string> map;
+    std::unordered_map<std::string, CachedReply> map;
   };
   static constexpr int kShards = 16;
   CacheShard shards_[kShards];

@@ -92,6 +92,10 @@ class FileSystemMaster(Journaled):
         self.persist_jobs: dict[int, dict] = {}
         self._sync_times: dict[str, float] = {}
         self._sync_exec = None          # metadata sync executor / UFS prefetch pool (lazy, _sync_pools)
+        from .absent_cache import AsyncUfsAbsentPathCache
+        self.absent_cache = AsyncUfsAbsentPathCache(
+            self.mount_table, conf.get_int("alluxio.master.ufs.path.cache.capacity", "100000"),
+            min(16, conf.get_int("alluxio.master.ufs.path.cache.threads", "64")))
         self._sync_prefetch = None
         self.state_lock = None
         self.audit = None
@@ -374,6 +378,7 @@ class FileSystemMaster(Journaled):
                                                          ttl_action=ttl_action):
                     self._apply(rpc, e)
                 parent = self.tree.get(cur_path)
+        self.absent_cache.process_existence(path)
 
     def create_file(self, path: str, block_size: int | None = None, recursive: bool = False,
                     mode: int | None = None, replication_min: int = 0, replication_max: int = -1,
@@ -420,6 +425,7 @@ class FileSystemMaster(Journaled):
             self._apply(rpc, e)
             self._touch_parent(rpc, parent)
             inode = self.tree.inodes[file_id]
+        self.absent_cache.process_existence(path)
         # the reply is built outside the namespace write lock
         with self.tree.lock.read():
             return self.file_info(inode, path)
@@ -518,10 +524,29 @@ class FileSystemMaster(Journaled):
                 return get(chain[-1], path)
         if load_metadata == LOAD_NEVER:
             raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-        self.load_metadata(path, recursive=False, create_ancestors=True, quiet=True)
+        self._load_missing(path, load_metadata)
         with self.tree.lock.read():
             inode = self.tree.get(path)
             return get(inode, path)
+
+    def _load_missing(self, path: str, load_metadata: str) -> None:
+        """Load a path Alluxio does not have from the UFS, through the absent-path cache: a path
+        recently found missing in the UFS (or under a missing ancestor) fails without a UFS call
+        for LoadMetadataType ONCE; a new miss is recorded."""
+        if load_metadata == LOAD_ONCE and self.absent_cache.is_absent(path):
+            self._count("Master.UfsAbsentPathCacheHits")
+            raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+        try:
+            mid = self.mount_table.resolve(path).mount_id
+        except InvalidPathException:
+            mid = None
+        try:
+            self.load_metadata(path, recursive=False, create_ancestors=True, quiet=True)
+        except FileDoesNotExistException:
+            if mid is not None:
+                self.absent_cache.add_single_path(path, mid)
+            self.absent_cache.process_async(path)          # record the shallowest missing ancestor
+            raise
 
     def exists(self, path: str, load_metadata: str = LOAD_ONCE) -> bool:
         try:
@@ -543,7 +568,7 @@ class FileSystemMaster(Journaled):
         if inode is None:
             if load_metadata == LOAD_NEVER:
                 raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-            self.load_metadata(path, recursive=False, create_ancestors=True, quiet=True)
+            self._load_missing(path, load_metadata)
             with self.tree.lock.read():
                 inode = self.tree.get(path)
         if inode.is_directory and load_metadata != LOAD_NEVER and inode.is_persisted and \
@@ -661,6 +686,7 @@ class FileSystemMaster(Journaled):
     def rename(self, src: str, dst: str, persist: bool = False) -> None:
         src, dst = normalize_path(src), normalize_path(dst)
         self._count("Master.PathsRenamed")
+        self.absent_cache.process_existence(dst)
         if src == "/" or dst == "/":
             raise InvalidPathException("cannot rename the root")
         if dst == src:
@@ -971,6 +997,7 @@ class FileSystemMaster(Journaled):
                 self._load_children(rpc, inode, path, recursive, owner_default, group_default, cache)
         if ufs_blocks:
             self.block_master.commit_blocks_in_ufs(ufs_blocks)
+        self.absent_cache.process_existence(path)
 
     def load_listed_children(self, path: str, statuses) -> None:
         """Load the given UFS statuses (from a sync's listing of ``path``) as children of the
@@ -1095,6 +1122,7 @@ class FileSystemMaster(Journaled):
         from .sync import InodeSyncStream
         path = normalize_path(path)
         self._count("Master.MetadataSyncOps")
+        self.absent_cache.invalidate_prefix(path)
         ex, pre = self._sync_pools()
         conc = self.conf.get_int("alluxio.master.metadata.sync.concurrency.level", "6")
         return InodeSyncStream(self, path, recursive, ex, pre, conc).run()

@@ -187,6 +187,7 @@ class NativeRpcFrontend:
         the journal entries the handler appended are durable (sent by the flush callback)."""
         from ..security import as_user
         pending = None
+        cache_ep = None
         try:
             if midx == 0:
                 self._auth(token, payload)
@@ -216,6 +217,10 @@ class NativeRpcFrontend:
             if not isinstance(e, ex.AlluxioStatusException):
                 LOG.debug("native rpc %s failed", self.methods[midx][0], exc_info=True)
             reply = (token, int(se.status), se.message or str(se), b"")
+            if cache_ep is not None and not pending and isinstance(e, ex.NotFoundException):
+                # "does not exist" of a ONCE lookup: as stable as the UFS absent-path cache
+                # behind it (a create, load, sync change or remount bumps the epoch)
+                self.server.cache_put(midx, user, payload, b"", cache_ep, reply[1], reply[2])
         if pending:
             self._defer(pending, reply)
             return None

@@ -18,7 +18,10 @@ import threading
 import time
 
 OPS = ["CreateFile", "GetBlockLocations", "GetFileStatus", "OpenFile", "CreateDir", "ListDir",
-       "ListDirLocated", "RenameFile", "DeleteFile"]
+       "ListDirLocated", "RenameFile", "DeleteFile",
+       # beyond StressMasterBench: the "ListStatus, file does not exist" row of the published
+       # master numbers (docs/en/operation/Scalability-Tuning.md:148)
+       "GetFileStatusNonexistent"]
 
 
 def parse(argv):
@@ -108,6 +111,9 @@ def main(argv=None, fs=None, print_result=True) -> dict:
             c.create_directory(target(i), write_type="MUST_CACHE")
         elif a.operation == "GetFileStatus":
             c.get_status(f"{fixed}/{k}")
+        elif a.operation == "GetFileStatusNonexistent":
+            if c.exists(f"{base}/missing/{k}"):
+                raise IOError("a missing path exists")
         elif a.operation == "GetBlockLocations":
             c.get_block_locations(f"{fixed}/{k}")
         elif a.operation == "OpenFile":

@@ -98,13 +98,24 @@ def test_sync_requests_bypass_cache(master):
     assert srv.cache_hits == h
 
 
-def test_errors_not_cached(master):
+def test_not_found_cached_until_created(master):
+    """A ONCE lookup of a missing path is answered from the reply cache the second time (the
+    UFS absent-path cache makes it stable), and the cached NOT_FOUND dies with the next
+    namespace change: creating the path serves the real status."""
     m, stub = master
     srv = m.native_rpc.server
     for _ in range(2):
         with pytest.raises(ex.NotFoundException):
             _status(stub, "/missing", syncIntervalMs=-1)
-    assert srv.cache_hits == 0
+    assert srv.cache_hits == 1
+    _create(stub, "/missing")
+    _status(stub, "/missing", syncIntervalMs=-1)
+    # lookups that ask for a UFS sync are never cached, errors included
+    h = srv.cache_hits
+    for _ in range(2):
+        with pytest.raises(ex.NotFoundException):
+            _status(stub, "/missing2", syncIntervalMs=0)
+    assert srv.cache_hits == h
 
 
 def test_lose_primacy_invalidates(master):
