@@ -263,8 +263,12 @@ class RaftNode:
                  election_timeout_ms: float = 10_000, heartbeat_ms: float = 3_000,
                  rpc_timeout_ms: float = 5_000, append_batch_bytes: int = 512 << 10,
                  snapshot_chunk_bytes: int = 4 << 20, snapshot_period_entries: int = 2_000_000,
-                 snapshot_allowed=None):
+                 snapshot_allowed=None, transport: str = "UNARY"):
         self.id = self_id
+        # "MESSAGING": consensus RPCs go through one MessagingService.connect stream per peer
+        # (journal/messaging.py, the reference's transport); "UNARY": one gRPC call each
+        self.transport = transport.upper()
+        self._msg_conns: dict = {}
         self.storage = storage
         self.sm = state_machine
         self._channel_factory = channel_factory
@@ -357,6 +361,9 @@ class RaftNode:
             except Exception:  # noqa: BLE001
                 pass
         self._channels.clear()
+        for c in list(self._msg_conns.values()):
+            c.close()
+        self._msg_conns.clear()
         with self._lock:
             self.role = FOLLOWER
             self._replicators.clear()
@@ -367,6 +374,23 @@ class RaftNode:
         ch = self._channels.get(peer)
         if ch is None:
             ch = self._channels[peer] = self._channel_factory(peer)
+        if self.transport == "MESSAGING" and service == SVC_RAFT and method != "JournalQuery":
+            from .messaging import MessagingConnection
+            conn = self._msg_conns.get(peer)
+            try:
+                if conn is None or conn.closed:
+                    conn = self._msg_conns[peer] = MessagingConnection(ch)
+                return conn.call(method, req, self.rpc_timeout)
+            except Exception:
+                c = self._msg_conns.pop(peer, None)
+                if c is not None:
+                    c.close()
+                self._channels.pop(peer, None)     # a restarted peer needs a fresh channel
+                try:
+                    ch.close()
+                except Exception:  # noqa: BLE001
+                    pass
+                raise
         try:
             return getattr(ch.stub(service), method)(req, timeout=self.rpc_timeout)
         except Exception:

@@ -300,8 +300,9 @@ class RaftJournalSystem(JournalSystem):
                  flush_batch_ms: float = 5.0, snapshot_period_entries: int = 2_000_000,
                  append_batch_bytes: int = 512 << 10, snapshot_chunk_bytes: int = 4 << 20,
                  rpc_timeout_ms: float = 5_000, catchup_quiet_factor: float = 2.0, enable_grpc: bool = True,
-                 fsync: bool = True):
+                 fsync: bool = True, transport: str = "MESSAGING"):
         super().__init__()
+        self.transport = transport
         self.root = root
         self.local = _hostport(local_address)
         self.single = not cluster_addresses
@@ -352,7 +353,10 @@ class RaftJournalSystem(JournalSystem):
                    append_batch_bytes=conf.get_bytes("alluxio.master.embedded.journal.appender.batch.size"),
                    snapshot_chunk_bytes=conf.get_bytes("alluxio.master.embedded.journal.snapshot.replication.chunk.size"),
                    rpc_timeout_ms=conf.get_ms("alluxio.master.embedded.journal.transport.request.timeout.ms"),
-                   enable_grpc=enable_grpc)
+                   enable_grpc=enable_grpc,
+                   # consensus RPCs over MessagingService streams (the reference's transport) or
+                   # one unary call each
+                   transport=conf.get("alluxio.master.embedded.journal.transport.type", "MESSAGING"))
 
     # ---- format / state --------------------------------------------------------------------------
     def format(self) -> None:
@@ -380,6 +384,8 @@ class RaftJournalSystem(JournalSystem):
         handler = RaftServiceHandler(lambda: self.node, self._on_query)
         self.server.add_servicer(SVC_RAFT, handler)
         self.server.add_servicer(SVC_RAFT_JOURNAL, handler)
+        from .messaging import SVC_MESSAGING, MessagingServiceHandler
+        self.server.add_servicer(SVC_MESSAGING, MessagingServiceHandler(handler))
         addr = self.server.start()
         if self.single:
             # a lone master is the whole group, whatever address an earlier run recorded
@@ -400,7 +406,7 @@ class RaftJournalSystem(JournalSystem):
                              election_timeout_ms=self.election_timeout_ms, heartbeat_ms=self.heartbeat_ms,
                              rpc_timeout_ms=self.rpc_timeout_ms, append_batch_bytes=self.append_batch_bytes,
                              snapshot_chunk_bytes=self.chunk, snapshot_period_entries=self.snapshot_period,
-                             snapshot_allowed=lambda: self._snapshot_allowed)
+                             snapshot_allowed=lambda: self._snapshot_allowed, transport=self.transport)
         if self.single:
             self.node._configs = [(storage.base_index, [self.local])]
         self.selector = RaftPrimarySelector(self)

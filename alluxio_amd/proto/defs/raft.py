@@ -33,6 +33,7 @@ msg MessagingRequestHeader requestId=1:i64
 msg MessagingResponseHeader requestId=1:i64 isThrowable=2:bool
 msg TransportMessage requestHeader=1:MessagingRequestHeader responseHeader=2:MessagingResponseHeader
     message=3:bytes
+rpc MessagingService connect *TransportMessage *TransportMessage
 
 package alluxio.grpc.raft
 msg RaftNamedEntry master=1:str entry=2:alluxio.proto.journal.JournalEntry

@@ -15,6 +15,7 @@ import pytest
 
 from alluxio_amd.journal.raft import (KIND_JOURNAL, LEADER, SVC_RAFT, SVC_RAFT_JOURNAL, RaftNode,
                                       RaftServiceHandler, RaftStorage)
+from alluxio_amd.proto import pb
 from alluxio_amd.rpc import Channel, RpcServer, _alloc_local_port
 from alluxio_amd.utils.exceptions import UnavailableException
 
@@ -65,13 +66,19 @@ class FilteredChannel:
             raise UnavailableException(f"link {self.src}->{self.dst} is cut")
         return self.ch.stub(svc)
 
+    def raw_stream(self, svc, method):
+        if frozenset((self.src, self.dst)) in self.net.cut:
+            raise UnavailableException(f"link {self.src}->{self.dst} is cut")
+        return self.ch.raw_stream(svc, method)
+
     def close(self):
         self.ch.close()
 
 
 class Group:
-    def __init__(self, root, n=3, T=150, period=0, ids=None):
+    def __init__(self, root, n=3, T=150, period=0, ids=None, transport="UNARY"):
         self.root, self.T, self.period = root, T, period
+        self.transport = transport
         self.ids = ids or [f"127.0.0.1:{_alloc_local_port()}" for _ in range(n)]
         self.net = _Cut()
         self.nodes, self.servers = {}, {}
@@ -83,11 +90,13 @@ class Group:
         node = RaftNode(nid, got or peers or self.ids, storage, sm,
                         lambda a, s=nid: FilteredChannel(s, a, self.net),
                         election_timeout_ms=self.T, heartbeat_ms=self.T / 5, rpc_timeout_ms=500,
-                        snapshot_chunk_bytes=64, snapshot_period_entries=self.period)
+                        snapshot_chunk_bytes=64, snapshot_period_entries=self.period, transport=self.transport)
         srv = RpcServer("127.0.0.1", int(nid.rsplit(":", 1)[1]), enable_grpc=False)
         h = RaftServiceHandler(lambda: node)
         srv.add_servicer(SVC_RAFT, h)
         srv.add_servicer(SVC_RAFT_JOURNAL, h)
+        from alluxio_amd.journal.messaging import SVC_MESSAGING, MessagingServiceHandler
+        srv.add_servicer(SVC_MESSAGING, MessagingServiceHandler(h))
         srv.start()
         node.start()
         self.nodes[nid], self.servers[nid] = node, srv
@@ -322,3 +331,47 @@ def test_single_master_embedded_restart_checkpoint_and_dump(tmp_path):
     n = dump_raft_journal(jdir, "FileSystemMaster", str(tmp_path / "dump"), out=out)
     assert n >= 1 and "Snapshot at raft index" in out.getvalue()
     assert "after_cp" in (tmp_path / "dump" / "edits.txt").read_text()
+
+
+def test_consensus_over_messaging_streams(tmp_path):
+    """The reference's transport: vote / append / timeout-now tunnelled through one
+    MessagingService.connect stream per peer (journal/messaging.py), with failover, a cut link
+    (the stream breaks and reconnects) and a restarted node catching up."""
+    g = Group(str(tmp_path), transport="MESSAGING").start_all()
+    try:
+        lead = g.leader()
+        g.submit(lead, [f"m{i}" for i in range(20)])
+        g.wait_items([f"m{i}" for i in range(20)])
+        assert any(lead._msg_conns.values()) and not any(c.closed for c in lead._msg_conns.values())
+        old = lead.id
+        g.kill(old)
+        lead2 = g.leader()
+        g.submit(lead2, ["n0"])
+        g.start(old)
+        g.wait_items([f"m{i}" for i in range(20)] + ["n0"])
+    finally:
+        g.stop()
+
+
+def test_messaging_reports_remote_failure():
+    from alluxio_amd.journal.messaging import MessagingConnection, MessagingServiceHandler
+
+    class _H:
+        def RequestVote(self, req, ctx):
+            raise RuntimeError("boom")
+
+        def AppendEntries(self, req, ctx):
+            return pb.raft.AppendEntriesPResponse(term=req.term, success=True, matchIndex=7)
+
+    class _Ch:
+        def raw_stream(self, svc, method):
+            return lambda it: MessagingServiceHandler(_H()).connect(it, None)
+
+    c = MessagingConnection(_Ch())
+    r = c.call("AppendEntries", pb.raft.AppendEntriesPRequest(term=3), 5)
+    assert r.success and r.matchIndex == 7 and r.term == 3
+    with pytest.raises(UnavailableException, match="boom"):
+        c.call("RequestVote", pb.raft.RequestVotePRequest(term=1), 5)
+    c.close()
+    with pytest.raises(UnavailableException):
+        c.call("AppendEntries", pb.raft.AppendEntriesPRequest(term=3), 1)
