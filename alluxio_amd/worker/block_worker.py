@@ -498,9 +498,15 @@ class BlockWorker:
         from .ufs_fallback import resolve_ufs_block_opts
         session_id = session_id if session_id is not None else ids.CACHE_UFS_SESSION_ID
         native_ids, paths, offs, lens, slow = [], [], [], [], []
+        local_mount: dict = {}          # mount id -> is a local UFS (one resolution per mount, not per block)
         for bid, opts in items:
             opts = resolve_ufs_block_opts(self, bid, opts)
-            if isinstance(self._ufs_for(opts), LocalUnderFileSystem) and opts.block_size > 0:
+            is_local = local_mount.get(opts.mountId)
+            if is_local is None or not opts.mountId:
+                is_local = isinstance(self._ufs_for(opts), LocalUnderFileSystem)
+                if opts.mountId:
+                    local_mount[opts.mountId] = is_local
+            if is_local and opts.block_size > 0:
                 native_ids.append(bid)
                 paths.append(strip_scheme(opts.ufs_path))
                 offs.append(opts.offset_in_file)
