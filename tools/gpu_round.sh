@@ -2,7 +2,8 @@
 # One GPU session: tests, smoke, bench variants, rocprof.  Each GPU step has its own timeout and
 # the script stops at the first crash-like exit (fault/abort/segv/timeout); plain test failures
 # (exit 1) do not stop later measurement steps.
-# usage: tools/gpu_round.sh [steps...]   steps: tests smoke bench variants prof kbench
+# usage: tools/gpu_round.sh [steps...]   steps: tests smoke bench bench20 variants prof ring pmc pmcdram
+#                                         crc dl master kbench
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out
@@ -39,6 +40,12 @@ for s in $STEPS; do
       ;;
     prof)
       run rocprof_bench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
+      ;;
+    crc) run crc_bench 300 python tools/crc_bench.py --gb 4 --out "$OUT/crc_bench.jsonl" ;;
+    dl) run dl_bench_100k 400 python tools/dl_bench.py --files 100000 --out "$OUT/dl_bench_100k.jsonl" ;;
+    master)
+      # CPU-only: the master metadata bench on the box's CPU share (no GPU used)
+      run master_bench 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --out "$OUT/master_bench.json"
       ;;
     ring)
       run bench_ring4k 300 python bench.py --buffer-size 4k --steps 200 --warmup 20
