@@ -32,6 +32,14 @@ OPEN, READ, WRITE, STATFS, RELEASE, FSYNC = 14, 15, 16, 17, 18, 20
 GETXATTR, LISTXATTR, FLUSH, INIT, OPENDIR, READDIR, RELEASEDIR, FSYNCDIR = 22, 23, 25, 26, 27, 28, 29, 30
 ACCESS, CREATE, INTERRUPT, DESTROY, BATCH_FORGET, RENAME2 = 34, 35, 36, 38, 42, 45
 
+IOCTL = 39
+OP_NAMES = {LOOKUP: "LOOKUP", FORGET: "FORGET", GETATTR: "GETATTR", SETATTR: "SETATTR", MKDIR: "MKDIR",
+            UNLINK: "UNLINK", RMDIR: "RMDIR", RENAME: "RENAME", OPEN: "OPEN", READ: "READ", WRITE: "WRITE",
+            STATFS: "STATFS", RELEASE: "RELEASE", FSYNC: "FSYNC", GETXATTR: "GETXATTR", LISTXATTR: "LISTXATTR",
+            FLUSH: "FLUSH", INIT: "INIT", OPENDIR: "OPENDIR", READDIR: "READDIR", RELEASEDIR: "RELEASEDIR",
+            FSYNCDIR: "FSYNCDIR", ACCESS: "ACCESS", CREATE: "CREATE", INTERRUPT: "INTERRUPT", IOCTL: "IOCTL",
+            DESTROY: "DESTROY", BATCH_FORGET: "BATCH_FORGET", RENAME2: "RENAME2"}
+
 IN_HDR = struct.Struct("<IIQQIIII")            # len opcode unique nodeid uid gid pid padding
 OUT_HDR = struct.Struct("<IiQ")                # len error unique
 ATTR = struct.Struct("<QQQQQQIIIIIIIIII")      # fuse_attr (88 bytes)
@@ -82,6 +90,7 @@ class FuseKernelServer:
         self._next_dir = 1
         self._stop = threading.Event()
         self.requests = 0
+        self.op_counts: dict[int, int] = {}           # opcode -> requests served (diagnostics)
 
     # ---- mount / unmount ---------------------------------------------------------------------
     def mount(self) -> "FuseKernelServer":
@@ -213,6 +222,7 @@ class FuseKernelServer:
         _, op, unique, nodeid, uid, gid, pid, _ = IN_HDR.unpack_from(req)
         body = memoryview(req)[IN_HDR.size:]
         self.requests += 1
+        self.op_counts[op] = self.op_counts.get(op, 0) + 1
         if op in (FORGET, BATCH_FORGET, INTERRUPT):
             return                             # no reply; node ids stay valid for renamed paths
         try:

@@ -99,6 +99,8 @@ def main(argv=None) -> int:
                 paths = [os.path.join(mnt, "ds", r) for r in rel]
                 res["fuse"] = _epochs(paths, a.epochs, a.workers, a.batch)
                 res["fuse_requests"] = srv.requests
+                from alluxio_amd.fuse.kernel import OP_NAMES
+                res["fuse_ops"] = {OP_NAMES.get(k, str(k)): v for k, v in sorted(srv.op_counts.items())}
             finally:
                 srv.unmount()
             ufs_dir = c.master.fs_master.mount_table.resolve("/ds").uri
