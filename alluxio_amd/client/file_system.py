@@ -225,6 +225,11 @@ class FileSystem:
         out = []
         for r in self._fs.ListStatus(pb.file.ListStatusPRequest(path=_path(path), options=o)):
             out.extend(URIStatus(i) for i in r.fileInfos)
+        if self.cache is not None and sync_interval_ms is None and load_metadata != "ALWAYS":
+            # a listing feeds the metadata cache with its children's statuses, as the reference's
+            # MetadataCachingBaseFileSystem.listStatus does
+            for st in out:
+                self.cache.put(st.info.path, st.info)
         return out
 
     def iterate_status(self, path, recursive=False, **kw):
