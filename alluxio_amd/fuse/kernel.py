@@ -385,6 +385,8 @@ class FuseKernelServer:
             return b""
         if op in (GETXATTR, LISTXATTR):
             raise FuseOSError(errno.ENODATA if op == GETXATTR else errno.ENOSYS)
+        if op == IOCTL:
+            raise FuseOSError(errno.ENOTTY)   # isatty() probes of open(): "not a terminal"
         raise FuseOSError(errno.ENOSYS)
 
 
