@@ -1,5 +1,6 @@
 """``alluxio runUfsTests``: the UFS contract runner against the local UFS, an object store (S3 via
-this project's S3 proxy, with the multipart-specific operations), Swift simulation and WebHDFS.
+this project's S3 proxy, with the multipart-specific operations), Swift simulation, WebHDFS, Azure
+Blob (wasb, against the in-tree fake) and ADL (WebHDFS + OAuth2 fake).
 
 Parity: integration/tools/validation/src/main/java/alluxio/cli/UnderFileSystemContractTest.java,
 UnderFileSystemCommonOperations.java, S3ASpecificOperations.java.
@@ -9,7 +10,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(__file__))
-from ufs_fakes import webhdfs_server  # noqa: E402
+from ufs_fakes import azure_server, webhdfs_server  # noqa: E402
 
 from alluxio_amd.cli import main as cli  # noqa: E402
 from alluxio_amd.cli import ufs_contract  # noqa: E402
@@ -70,3 +71,26 @@ def test_s3_contract_through_proxy(tmp_path):
             assert "S3ASpecificOperations#create_multipart_file_test" in out.getvalue()
         finally:
             proxy.stop()
+
+
+def test_wasb_contract():
+    srv, st = azure_server()
+    try:
+        props = {"fs.azure.account.key.acct.blob.core.windows.net": st.key, "fs.azure.endpoint": srv.url}
+        _ok(ufs_contract.run("wasb://cont@acct.blob.core.windows.net/", properties=props, out=io.StringIO(),
+                             large_file_size=1 << 20))
+    finally:
+        srv.stop()
+
+
+def test_adl_contract():
+    srv, _ = webhdfs_server(require_token="T0K")
+    try:
+        props = {"alluxio.underfs.adl.endpoint": srv.url + "/webhdfs/v1",
+                 "fs.adl.account.myacct.oauth2.client.id": "cid",
+                 "fs.adl.account.myacct.oauth2.credential": "sec",
+                 "fs.adl.account.myacct.oauth2.refresh.url": srv.url + "/oauth2/token"}
+        _ok(ufs_contract.run("adl://myacct.azuredatalakestore.net/", properties=props, out=io.StringIO(),
+                             large_file_size=1 << 20))
+    finally:
+        srv.stop()
