@@ -74,7 +74,7 @@ class FuseKernelServer:
     """Serve ``ops`` at ``mountpoint`` until :meth:`unmount`."""
 
     def __init__(self, ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False,
-                 keep_cache: bool = True):
+                 keep_cache: bool = False):
         self.ops = ops
         self.keep_cache = keep_cache
         self.mountpoint = os.path.abspath(mountpoint)
@@ -391,6 +391,6 @@ class FuseKernelServer:
 
 
 def mount_kernel(ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False,
-                 keep_cache: bool = True) -> FuseKernelServer:
+                 keep_cache: bool = False) -> FuseKernelServer:
     """Mount ``ops`` at ``mountpoint`` through ``/dev/fuse``; returns the running server."""
     return FuseKernelServer(ops, mountpoint, threads, allow_other, keep_cache).mount()

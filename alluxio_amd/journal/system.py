@@ -32,13 +32,30 @@ class deferred_flush:
 
     def __enter__(self):
         self.pending: dict = {}
-        self._prev = getattr(_DEFER, "pending", None)
+        self.after: list = []      # after_durable callbacks, run once ``pending`` is durable
+        self._prev = (getattr(_DEFER, "pending", None), getattr(_DEFER, "after", None))
         _DEFER.pending = self.pending
+        _DEFER.after = self.after
         return self
 
     def __exit__(self, *exc):
-        _DEFER.pending = self._prev
+        _DEFER.pending, _DEFER.after = self._prev
         return False
+
+
+def after_durable(cb) -> None:
+    """Run ``cb()`` once every journal entry this RPC appended so far is durable.
+
+    In a blocking RPC the journal contexts already waited, so ``cb`` runs now.  Inside
+    :class:`deferred_flush` (group-committed native RPCs) it is queued and run by the RPC front end
+    after the flush lands, before the reply, and never if the flush fails -- the ordering
+    ``RpcContext.close`` gives the reference: namespace entries durable first, then side effects
+    such as block deletion (a crash leaves an orphaned block, never an inode with missing blocks)."""
+    pending = getattr(_DEFER, "pending", None)
+    if pending:
+        _DEFER.after.append(cb)
+    else:
+        cb()
 
 
 class Journaled:

@@ -51,7 +51,9 @@ class AsyncUfsAbsentPathCache:
             return None
 
     # ---- queries ---------------------------------------------------------------------------
-    def is_absent(self, path: str) -> bool:
+    def is_absent(self, path: str, exists=None) -> bool:
+        """``exists(p)``: whether ``p`` is now in the Alluxio namespace -- an entry for a path
+        that exists (a create or load raced with the miss that recorded it) is stale and dropped."""
         with self._lock:
             if not self._entries:
                 self.misses += 1
@@ -60,8 +62,8 @@ class AsyncUfsAbsentPathCache:
                 mid = self._entries.get(p)
                 if mid is None:
                     continue
-                if mid != self._mount_id(p):
-                    del self._entries[p]          # remounted since: stale
+                if mid != self._mount_id(p) or (exists is not None and exists(p)):
+                    del self._entries[p]          # remounted since, or created since: stale
                     continue
                 self._entries.move_to_end(p)
                 self.hits += 1

@@ -18,7 +18,7 @@ import os
 import threading
 import time
 
-from ..journal.system import Journaled, NoopJournalContext
+from ..journal.system import Journaled, NoopJournalContext, after_durable
 from ..proto import pb
 from ..security import PermissionChecker, current_user
 from ..security.acl import Bits
@@ -31,6 +31,7 @@ from ..utils.exceptions import (AccessControlException, DirectoryNotEmptyExcepti
 from ..rpc.marshal import length_delimited
 from ..utils.uri import normalize_path, path_components
 from .inode import (LOST, NO_TTL, NOT_PERSISTED, PERSISTED, TO_BE_PERSISTED, InodeFile, now_ms)
+from .inode_lock import W, PathLockManager, check_may_block
 from .inode_tree import InodeTree
 from .mount_table import ROOT_MOUNT_ID, MountInfo, MountTable, UfsManager
 
@@ -57,10 +58,20 @@ class RpcContext:
         self.journal.close()
         if et is None:
             for cb in self.after:
-                try:
-                    cb()
-                except Exception:  # noqa: BLE001
-                    LOG.exception("post-journal callback failed")
+                after_durable(_logged(cb))
+
+
+def _logged(cb):
+    def run():
+        try:
+            cb()
+        except Exception:  # noqa: BLE001
+            LOG.exception("post-journal callback failed")
+    return run
+
+
+def _join(parent: str, name: str) -> str:
+    return parent.rstrip("/") + "/" + name
 
 
 class FileSystemMaster(Journaled):
@@ -99,13 +110,15 @@ class FileSystemMaster(Journaled):
         self._sync_prefetch = None
         self.state_lock = None
         self.audit = None
+        # path-scoped namespace locks held across UFS I/O (InodeLockManager); the tree lock is
+        # only held for in-memory resolution and journal application
+        self.path_locks = PathLockManager(
+            (conf.get_ms("alluxio.master.lock.timeout", "10min") / 1000.0) if conf else 600.0)
+        self.delete_batch = conf.get_int("alluxio.master.delete.apply.batch", "1024") if conf else 1024
         # FileInfo reply cache: (inode id, path) -> FileInfo, valid while the namespace, block
         # locations and mount table are unchanged (all three epochs).  Served objects are shared:
         # callers copy them into their reply, never mutate them.
-        self._fi_cache: dict = {}
-        self._fib_cache: dict = {}
-        self._ls_cache: dict = {}
-        self._fi_epoch = None
+        self._rc = (None, {}, {}, {})
         self._fi_cache_max = conf.get_int("alluxio.master.metadata.reply.cache.size", "100000") if conf else 100000
 
     # ------------------------------------------------------------------------------------------
@@ -253,37 +266,41 @@ class FileSystemMaster(Journaled):
     def _cache_epoch(self):
         return (self.tree.epoch, self.block_master.location_epoch, self.mount_table.epoch)
 
+    def _reply_cache(self):
+        """(epoch, FileInfo cache, serialized cache, listing cache) of the current epoch.  Callers
+        write only into the dicts of the tuple they got, so an insert racing with a reset lands
+        in the discarded generation, never in the new one."""
+        rc = self._rc
+        ep = self._cache_epoch()
+        if rc[0] != ep:
+            rc = self._rc = (ep, {}, {}, {})
+        return rc
+
     def cached_file_info(self, inode, path: str):
         """``file_info`` through the reply cache (callers hold the tree read lock)."""
-        ep = self._cache_epoch()
-        if ep != self._fi_epoch:
-            self._reset_reply_cache(ep)
-        cache = self._fi_cache
+        rc = self._reply_cache()
+        cache = rc[1]
         key = (inode.id, path)
         fi = cache.get(key)
         if fi is None:
             fi = self.file_info(inode, path)
-            if len(cache) < self._fi_cache_max and ep == self._cache_epoch():
+            if len(cache) < self._fi_cache_max and rc[0] == self._cache_epoch():
                 cache[key] = fi
         return fi
 
     def _reset_reply_cache(self, ep) -> None:
-        self._fi_cache = {}
-        self._fib_cache = {}
-        self._ls_cache = {}
-        self._fi_epoch = ep
+        self._rc = (ep, {}, {}, {})
 
     def cached_file_info_bytes(self, inode, path: str) -> bytes:
         """Serialized FileInfo through the reply cache (callers hold the tree read lock)."""
-        ep = self._cache_epoch()
-        if ep != self._fi_epoch:
-            self._reset_reply_cache(ep)
+        rc = self._reply_cache()
+        cache = rc[2]
         key = (inode.id, path)
-        b = self._fib_cache.get(key)
+        b = cache.get(key)
         if b is None:
             b = self.cached_file_info(inode, path).SerializeToString()
-            if len(self._fib_cache) < self._fi_cache_max and ep == self._cache_epoch():
-                self._fib_cache[key] = b
+            if len(cache) < self._fi_cache_max and rc[0] == self._cache_epoch():
+                cache[key] = b
         return b
 
     def file_info(self, inode, path: str | None = None):
@@ -340,6 +357,34 @@ class FileSystemMaster(Journaled):
         return fi
 
     # ------------------------------------------------------------------------------------------
+    # namespace locking (resolve -> UFS I/O under path locks only -> apply under the tree lock)
+    def _first_missing(self, path: str) -> tuple[str, int]:
+        """(path to write-lock to create ``path``, number of missing components): the first
+        missing component (the WRITE_EDGE of the reference's create), or ``path`` itself."""
+        with self.tree.lock.read():
+            try:
+                chain, missing = self.tree.resolve(path)
+            except InvalidPathException:
+                return path, -1
+        if not missing:
+            return path, 0
+        comps = path_components(path)
+        return "/" + "/".join(comps[:len(comps) - len(missing) + 1]), len(missing)
+
+    def _lock_create(self, path: str):
+        """Lock list for creating ``path`` (and its missing ancestors): W on the first missing
+        component; re-checked after acquisition (a racing create may have added it)."""
+        while True:
+            target = self._first_missing(path)
+            ll = self.path_locks.lock([(target[0], W)])
+            if self._first_missing(path) == target:
+                return ll
+            ll.close()
+
+    def _lock_path(self, *paths):
+        return self.path_locks.lock([(p, W) for p in paths])
+
+    # ------------------------------------------------------------------------------------------
     # create
     def create_directory(self, path: str, recursive: bool = False, allow_exists: bool = False,
                          mode: int | None = None, write_type: str = "MUST_CACHE", ttl: int = NO_TTL,
@@ -353,31 +398,42 @@ class FileSystemMaster(Journaled):
         persist = write_type in ("CACHE_THROUGH", "THROUGH", "ASYNC_THROUGH")
         owner, group = self._owner_group()
         mode = (0o777 if mode is None else mode) & ~self.umask
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            chain, missing = self.tree.resolve(path)
-            if not missing:
-                if allow_exists and chain[-1].is_directory:
-                    return
-                raise FileAlreadyExistsException(f"{path} already exists")
-            if len(missing) > 1 and not recursive:
-                raise FileDoesNotExistException(
-                    f"Path \"{normalize_path('/'.join([''] + path_components(path)[:-1]))}\" does not exist.")
-            self._check(chain, Bits.WRITE, path)
-            self.mount_table.check_under_write_mount(path)
-            parent = chain[-1]
-            if not parent.is_directory:
-                raise InvalidPathException(f"{self.tree.path_of(parent)} is a file")
-            cur_path = self.tree.path_of(parent)
+        with self._lock_create(path):
+            with self.tree.lock.read():
+                chain, missing = self.tree.resolve(path)
+                if not missing:
+                    if allow_exists and chain[-1].is_directory:
+                        return
+                    raise FileAlreadyExistsException(f"{path} already exists")
+                if len(missing) > 1 and not recursive:
+                    raise FileDoesNotExistException(
+                        f"Path \"{normalize_path('/'.join([''] + path_components(path)[:-1]))}\" does not exist.")
+                self._check(chain, Bits.WRITE, path)
+                self.mount_table.check_under_write_mount(path)
+                parent = chain[-1]
+                if not parent.is_directory:
+                    raise InvalidPathException(f"{self.tree.path_of(parent)} is a file")
+                base = self.tree.path_of(parent)
+            new_paths = []
+            cur = base
             for name in missing:
-                cur_path = cur_path.rstrip("/") + "/" + name
-                if persist:
-                    self._check_ufs_writable(cur_path)
-                    res = self._resolve_ufs(cur_path)
+                cur = _join(cur, name)
+                new_paths.append(cur)
+            if persist:
+                # UFS first, holding only the path locks: other subtrees keep working
+                for p in new_paths:
+                    self._check_ufs_writable(p)
+                check_may_block("UFS mkdirs")
+                for p in new_paths:
+                    res = self._resolve_ufs(p)
                     res.ufs.mkdirs(res.uri, MkdirsOptions(create_parent=True, owner=owner, group=group, mode=mode))
-                for e in self.tree.new_directory_entries(parent, name, owner, group, mode, persist, ttl=ttl,
-                                                         ttl_action=ttl_action):
-                    self._apply(rpc, e)
-                parent = self.tree.get(cur_path)
+            with RpcContext(self) as rpc, self.tree.lock.write():
+                parent = self.tree.get(base)
+                for name, p in zip(missing, new_paths):
+                    for e in self.tree.new_directory_entries(parent, name, owner, group, mode, persist, ttl=ttl,
+                                                             ttl_action=ttl_action):
+                        self._apply(rpc, e)
+                    parent = self.tree.get(p)
         self.absent_cache.process_existence(path)
 
     def create_file(self, path: str, block_size: int | None = None, recursive: bool = False,
@@ -403,7 +459,7 @@ class FileSystemMaster(Journaled):
                 self.create_directory(parent_path, recursive=True, allow_exists=True,
                                       write_type=write_type if write_type != "NONE" else "MUST_CACHE")
         file_id = ids.create_file_id(self.block_master.get_new_container_id())
-        with RpcContext(self) as rpc, self.tree.lock.write():
+        with self._lock_path(path), RpcContext(self) as rpc, self.tree.lock.write():
             chain, missing = self.tree.resolve(path)
             if not missing:
                 raise FileAlreadyExistsException(f"{path} already exists")
@@ -436,7 +492,7 @@ class FileSystemMaster(Journaled):
 
     def get_new_block_id_for_file(self, path: str) -> int:
         path = normalize_path(path)
-        with RpcContext(self) as rpc, self.tree.lock.write():
+        with self._lock_path(path), RpcContext(self) as rpc, self.tree.lock.write():
             chain, missing = self.tree.resolve(path)
             if missing:
                 raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
@@ -454,62 +510,66 @@ class FileSystemMaster(Journaled):
                       persistence_wait_ms: int = 0) -> None:
         path = normalize_path(path)
         self._count("Master.FilesCompleted")
-        # UFS fingerprint of a persisted file is fetched before the tree write lock (UFS latency
-        # must not stall the namespace; the proxy-backed S3 UFS even calls back into this master)
-        pre_fp = None
-        with self.tree.lock.read():
-            chain, missing = self.tree.resolve(path)
-            persisted = not missing and chain[-1].is_file and chain[-1].is_persisted
-        if persisted:
-            try:
-                res = self._resolve_ufs(path)
-                pre_fp = res.ufs.get_fingerprint(res.uri)
-            except Exception:  # noqa: BLE001
-                pre_fp = Fingerprint.INVALID
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            chain, missing = self.tree.resolve(path)
-            if missing:
-                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-            f = chain[-1]
-            if not f.is_file:
-                raise FileDoesNotExistException(f"{path} must be a file")
-            self._check(chain, Bits.WRITE, path)
-            if f.completed:
-                raise FailedPreconditionException(f"File {path} has already been completed.")
-            infos = self.block_master.block_info_list(f.block_ids)
-            if not f.is_persisted and len(infos) != len(f.block_ids):
-                raise FailedPreconditionException("Cannot complete a file without all the blocks committed")
-            in_alluxio = 0
-            for i, bi in enumerate(infos):
-                in_alluxio += bi.length
-                if i < len(infos) - 1 and bi.length != f.block_size_bytes:
-                    raise FailedPreconditionException(f"Block index {i} has a block size smaller than the file "
-                                                      f"block size ({f.block_size_bytes})")
-            length = ufs_length if f.is_persisted else in_alluxio
-            if length < 0:
-                raise InvalidArgumentException(f"File {f.name} cannot have negative length: {length}")
-            fingerprint = pre_fp if (f.is_persisted and pre_fp is not None) else Fingerprint.INVALID
-            blocks = []
-            remaining, seq = length, 0
-            while remaining > 0:
-                blocks.append(ids.create_block_id(f.block_container_id, seq))
-                remaining -= min(remaining, f.block_size_bytes)
-                seq += 1
-            if f.is_persisted:
-                rem = length
-                for bid in blocks:
-                    self.block_master.commit_block_in_ufs(bid, min(rem, f.block_size_bytes))
-                    rem -= min(rem, f.block_size_bytes)
-            self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
-                id=f.id, ufs_fingerprint=fingerprint, last_modification_time_ms=rpc.op_time_ms,
-                last_access_time_ms=rpc.op_time_ms, overwrite_modification_time=True, overwrite_access_time=True)))
-            self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
-                id=f.id, path=path, completed=True, length=length, set_blocks=blocks)))
-            if async_persist and not f.is_persisted:
-                self._schedule_persist_locked(rpc, f, persistence_wait_ms)
+        with self._lock_path(path):
+            # UFS fingerprint of a persisted file: fetched under the path lock only (UFS latency
+            # must not stall the namespace; the proxy-backed S3 UFS even calls back into this master)
+            pre_fp = None
+            with self.tree.lock.read():
+                chain, missing = self.tree.resolve(path)
+                persisted = not missing and chain[-1].is_file and chain[-1].is_persisted \
+                    and not chain[-1].completed
+            if persisted:
+                check_may_block("UFS fingerprint")
+                try:
+                    res = self._resolve_ufs(path)
+                    pre_fp = res.ufs.get_fingerprint(res.uri)
+                except Exception:  # noqa: BLE001
+                    pre_fp = Fingerprint.INVALID
+            with RpcContext(self) as rpc, self.tree.lock.write():
+                self._complete_locked(rpc, path, ufs_length, async_persist, persistence_wait_ms, pre_fp)
 
-    # ------------------------------------------------------------------------------------------
-    # read-side
+    def _complete_locked(self, rpc, path, ufs_length, async_persist, persistence_wait_ms, pre_fp) -> None:
+        chain, missing = self.tree.resolve(path)
+        if missing:
+            raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+        f = chain[-1]
+        if not f.is_file:
+            raise FileDoesNotExistException(f"{path} must be a file")
+        self._check(chain, Bits.WRITE, path)
+        if f.completed:
+            raise FailedPreconditionException(f"File {path} has already been completed.")
+        infos = self.block_master.block_info_list(f.block_ids)
+        if not f.is_persisted and len(infos) != len(f.block_ids):
+            raise FailedPreconditionException("Cannot complete a file without all the blocks committed")
+        in_alluxio = 0
+        for i, bi in enumerate(infos):
+            in_alluxio += bi.length
+            if i < len(infos) - 1 and bi.length != f.block_size_bytes:
+                raise FailedPreconditionException(f"Block index {i} has a block size smaller than the file "
+                                                  f"block size ({f.block_size_bytes})")
+        length = ufs_length if f.is_persisted else in_alluxio
+        if length < 0:
+            raise InvalidArgumentException(f"File {f.name} cannot have negative length: {length}")
+        fingerprint = pre_fp if (f.is_persisted and pre_fp is not None) else Fingerprint.INVALID
+        blocks = []
+        remaining, seq = length, 0
+        while remaining > 0:
+            blocks.append(ids.create_block_id(f.block_container_id, seq))
+            remaining -= min(remaining, f.block_size_bytes)
+            seq += 1
+        if f.is_persisted:
+            rem = length
+            for bid in blocks:
+                self.block_master.commit_block_in_ufs(bid, min(rem, f.block_size_bytes))
+                rem -= min(rem, f.block_size_bytes)
+        self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+            id=f.id, ufs_fingerprint=fingerprint, last_modification_time_ms=rpc.op_time_ms,
+            last_access_time_ms=rpc.op_time_ms, overwrite_modification_time=True, overwrite_access_time=True)))
+        self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
+            id=f.id, path=path, completed=True, length=length, set_blocks=blocks)))
+        if async_persist and not f.is_persisted:
+            self._schedule_persist_locked(rpc, f, persistence_wait_ms)
+
     def get_status(self, path: str, load_metadata: str = LOAD_ONCE, sync_interval_ms: int = -1,
                    access_mode: int = Bits.READ, update_timestamps: bool = True, raw: bool = False):
         """FileInfo of ``path`` (``raw``: its serialized bytes, from the reply cache)."""
@@ -533,7 +593,7 @@ class FileSystemMaster(Journaled):
         """Load a path Alluxio does not have from the UFS, through the absent-path cache: a path
         recently found missing in the UFS (or under a missing ancestor) fails without a UFS call
         for LoadMetadataType ONCE; a new miss is recorded."""
-        if load_metadata == LOAD_ONCE and self.absent_cache.is_absent(path):
+        if load_metadata == LOAD_ONCE and self.absent_cache.is_absent(path, self._exists_in_tree):
             self._count("Master.UfsAbsentPathCacheHits")
             raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
         try:
@@ -543,10 +603,16 @@ class FileSystemMaster(Journaled):
         try:
             self.load_metadata(path, recursive=False, create_ancestors=True, quiet=True)
         except FileDoesNotExistException:
-            if mid is not None:
+            # a create racing with this miss may already have called process_existence: only
+            # record the path while it is still missing (is_absent re-checks the tree as well)
+            if mid is not None and not self._exists_in_tree(path):
                 self.absent_cache.add_single_path(path, mid)
             self.absent_cache.process_async(path)          # record the shallowest missing ancestor
             raise
+
+    def _exists_in_tree(self, path: str) -> bool:
+        with self.tree.lock.read():
+            return self.tree.get_or_none(path) is not None
 
     def exists(self, path: str, load_metadata: str = LOAD_ONCE) -> bool:
         try:
@@ -584,12 +650,11 @@ class FileSystemMaster(Journaled):
                 if raw:
                     return [length_delimited(0x0A, self.cached_file_info_bytes(inode, path))]
                 return [self.cached_file_info(inode, path)]
-            ep = self._cache_epoch()
+            rc = self._reply_cache()
             lkey = (inode.id, path, recursive, raw)
-            if ep == self._fi_epoch:
-                hit = self._ls_cache.get(lkey)
-                if hit is not None:
-                    return hit
+            hit = rc[3].get(lkey)
+            if hit is not None:
+                return hit
             out = []
             stack = [(inode, path)]
             while stack:
@@ -602,8 +667,8 @@ class FileSystemMaster(Journaled):
             if raw:
                 out = [b"".join(length_delimited(0x0A, b) for b in out[i:i + 10000])
                        for i in range(0, len(out), 10000)] or [b""]
-            if ep == self._fi_epoch == self._cache_epoch() and len(self._ls_cache) < 4096:
-                self._ls_cache[lkey] = out
+            if rc[0] == self._cache_epoch() and len(rc[3]) < 4096:
+                rc[3][lkey] = out
             return out
 
     def get_file_path(self, file_id: int) -> str:
@@ -631,57 +696,84 @@ class FileSystemMaster(Journaled):
     # delete / rename / free
     def delete(self, path: str, recursive: bool = False, alluxio_only: bool = False,
                unchecked: bool = False) -> None:
+        """Delete ``path`` (DefaultFileSystemMaster.delete :1621 / deleteInternal).  Resolve and
+        validate under the tree read lock, delete in the UFS children-first holding only the path
+        lock of the subtree, then apply the DeleteFile entries in batches of
+        ``alluxio.master.delete.apply.batch`` per tree-lock section.  A UFS failure keeps the
+        failed inode and its ancestors (the rest is deleted) and is reported afterwards; the
+        blocks of deleted files are removed from the workers once the entries are durable."""
         path = normalize_path(path)
         self._count("Master.PathsDeleted")
-        ufs_deletes = []
-        block_ids = []
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            chain, missing = self.tree.resolve(path)
-            if missing:
-                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-            inode = chain[-1]
-            self._check(chain[:-1], Bits.WRITE, path)
-            if inode.is_directory and self.tree.children.get(inode.id) and not recursive:
-                raise DirectoryNotEmptyException(f"Cannot delete non-empty directory {path} without recursive")
-            victims = self.tree.descendants(inode)
-            if path != "/":
-                victims.append(inode)
-            for v in victims:
-                vp = self.tree.path_of(v)
-                if v.is_directory and self.mount_table.is_mount_point(vp) and vp != path:
-                    raise InvalidPathException(f"cannot delete {path}: it contains mount point {vp}")
-            if path != "/" and self.mount_table.is_mount_point(path) and not alluxio_only:
-                raise InvalidPathException(f"{path} is a mount point; unmount it instead")
-            if not alluxio_only:
-                self.mount_table.check_under_write_mount(path)
-            for v in victims:
-                vp = self.tree.path_of(v)
-                if not alluxio_only and v.is_persisted:
-                    try:
-                        res = self._resolve_ufs(vp)
-                        ufs_deletes.append((res.ufs, res.uri, v.is_directory))
-                    except InvalidPathException:
-                        pass
-                if v.is_file:
-                    block_ids.extend(v.block_ids)
-            # UFS first (children before parents), then the journal
-            for ufs, uri, is_dir in ufs_deletes:
+        with self._lock_path(path):
+            ufs_deletes = []
+            with self.tree.lock.read():
+                chain, missing = self.tree.resolve(path)
+                if missing:
+                    raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+                inode = chain[-1]
+                self._check(chain[:-1], Bits.WRITE, path)
+                if inode.is_directory and self.tree.children.get(inode.id) and not recursive:
+                    raise DirectoryNotEmptyException(f"Cannot delete non-empty directory {path} without recursive")
+                victims = self.tree.descendants(inode)
+                if path != "/":
+                    victims.append(inode)
+                vpaths = {}
+                for v in victims:
+                    vp = vpaths[v.id] = self.tree.path_of(v)
+                    if v.is_directory and vp != path and self.mount_table.is_mount_point(vp):
+                        raise InvalidPathException(f"cannot delete {path}: it contains mount point {vp}")
+                if path != "/" and self.mount_table.is_mount_point(path) and not alluxio_only:
+                    raise InvalidPathException(f"{path} is a mount point; unmount it instead")
+                if not alluxio_only:
+                    self.mount_table.check_under_write_mount(path)
+                    for v in victims:
+                        if v.is_persisted:
+                            try:
+                                res = self._resolve_ufs(vpaths[v.id])
+                                ufs_deletes.append((v, res.ufs, res.uri))
+                            except InvalidPathException:
+                                pass
+            # UFS deletes, children before parents, with no tree lock held
+            kept: set = set()        # victims that stay: a failed UFS delete and its ancestors
+            errors = []
+            if ufs_deletes:
+                check_may_block("UFS delete")
+            for v, ufs, uri in ufs_deletes:
+                if v.id in kept:
+                    continue
                 try:
-                    if is_dir:
+                    if v.is_directory:
                         ufs.delete_directory(uri)
                     else:
                         ufs.delete_file(uri)
                 except Exception as e:  # noqa: BLE001
-                    if not unchecked:
-                        raise UnavailableException(f"failed to delete {uri} in UFS: {e}") from e
-            for v in victims:
-                self._apply(rpc, pb.journal.JournalEntry(delete_file=pb.journal.DeleteFileEntry(
-                    id=v.id, recursive=recursive, op_time_ms=rpc.op_time_ms, alluxioOnly=alluxio_only,
-                    path=self.tree.path_of(v) if not v.deleted else "")))
-            if path != "/":
-                self._touch_parent(rpc, chain[-2])
-        if block_ids:
-            self.block_master.remove_blocks(block_ids, delete=True)
+                    if unchecked:
+                        continue
+                    errors.append(f"{uri}: {e}")
+                    cur = v
+                    while cur is not None and cur.id not in kept:
+                        kept.add(cur.id)
+                        if cur is inode:
+                            break
+                        cur = self.tree.inodes.get(cur.parent_id)
+            todo = [v for v in victims if v.id not in kept]
+            block_ids = [b for v in todo if v.is_file for b in v.block_ids]
+            with RpcContext(self) as rpc:
+                for i in range(0, len(todo), max(1, self.delete_batch)):
+                    with self.tree.lock.write():
+                        for v in todo[i:i + self.delete_batch]:
+                            self._apply(rpc, pb.journal.JournalEntry(delete_file=pb.journal.DeleteFileEntry(
+                                id=v.id, recursive=recursive, op_time_ms=rpc.op_time_ms, alluxioOnly=alluxio_only,
+                                path=vpaths[v.id])))
+                if path != "/" and todo:
+                    with self.tree.lock.write():
+                        self._touch_parent(rpc, chain[-2])
+                if block_ids:
+                    # workers drop the blocks only after the namespace change is durable
+                    rpc.after.append(lambda: self.block_master.remove_blocks(block_ids, delete=True))
+        if errors:
+            raise UnavailableException(f"failed to delete {len(errors)} path(s) in the UFS: "
+                                       + "; ".join(errors[:8]))
 
     def rename(self, src: str, dst: str, persist: bool = False) -> None:
         src, dst = normalize_path(src), normalize_path(dst)
@@ -693,28 +785,31 @@ class FileSystemMaster(Journaled):
             return
         if dst.startswith(src.rstrip("/") + "/"):
             raise InvalidPathException(f"cannot rename {src} into its own subtree {dst}")
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            schain, smissing = self.tree.resolve(src)
-            if smissing:
-                raise FileDoesNotExistException(f"Path \"{src}\" does not exist.")
-            inode = schain[-1]
-            dchain, dmissing = self.tree.resolve(dst)
-            if not dmissing:
-                raise FileAlreadyExistsException(f"Cannot rename because destination already exists. src: {src} "
-                                                 f"dst: {dst}")
-            if len(dmissing) > 1:
-                raise FileDoesNotExistException(f"destination parent of {dst} does not exist")
-            dparent = dchain[-1]
-            if not dparent.is_directory:
-                raise InvalidPathException(f"destination parent of {dst} is a file")
-            self._check(schain[:-1], Bits.WRITE, src)
-            self._check(dchain, Bits.WRITE, dst)
-            if self.mount_table.is_mount_point(src):
-                raise InvalidPathException(f"{src} is a mount point")
-            if self.mount_table.mount_point_for(src) != self.mount_table.mount_point_for(dst):
-                raise InvalidPathException(f"rename across mount points: {src} -> {dst}")
-            self.mount_table.check_under_write_mount(src)
-            if inode.is_persisted:
+        with self._lock_path(src, dst):
+            with self.tree.lock.read():
+                schain, smissing = self.tree.resolve(src)
+                if smissing:
+                    raise FileDoesNotExistException(f"Path \"{src}\" does not exist.")
+                inode = schain[-1]
+                dchain, dmissing = self.tree.resolve(dst)
+                if not dmissing:
+                    raise FileAlreadyExistsException(f"Cannot rename because destination already exists. src: {src} "
+                                                     f"dst: {dst}")
+                if len(dmissing) > 1:
+                    raise FileDoesNotExistException(f"destination parent of {dst} does not exist")
+                dparent = dchain[-1]
+                if not dparent.is_directory:
+                    raise InvalidPathException(f"destination parent of {dst} is a file")
+                self._check(schain[:-1], Bits.WRITE, src)
+                self._check(dchain, Bits.WRITE, dst)
+                if self.mount_table.is_mount_point(src):
+                    raise InvalidPathException(f"{src} is a mount point")
+                if self.mount_table.mount_point_for(src) != self.mount_table.mount_point_for(dst):
+                    raise InvalidPathException(f"rename across mount points: {src} -> {dst}")
+                self.mount_table.check_under_write_mount(src)
+                persisted = inode.is_persisted
+            if persisted:
+                check_may_block("UFS rename")
                 sres, dres = self._resolve_ufs(src), self._resolve_ufs(dst)
                 dparent_ufs = dres.uri.rsplit("/", 1)[0] or "/"
                 if not dres.ufs.exists(dparent_ufs):
@@ -723,12 +818,14 @@ class FileSystemMaster(Journaled):
                       else sres.ufs.rename_file(sres.uri, dres.uri))
                 if not ok:
                     raise UnavailableException(f"failed to rename {sres.uri} to {dres.uri} in the UFS")
-            old_parent = schain[-2]
-            self._apply(rpc, pb.journal.JournalEntry(rename=pb.journal.RenameEntry(
-                id=inode.id, op_time_ms=rpc.op_time_ms, new_parent_id=dparent.id, new_name=dmissing[0],
-                path=src, new_path=dst)))
-            self._touch_parent(rpc, old_parent)
-            self._touch_parent(rpc, dparent)
+            with RpcContext(self) as rpc, self.tree.lock.write():
+                old_parent = self.tree.inodes[inode.parent_id]
+                dparent = self.tree.get(dst.rsplit("/", 1)[0] or "/")
+                self._apply(rpc, pb.journal.JournalEntry(rename=pb.journal.RenameEntry(
+                    id=inode.id, op_time_ms=rpc.op_time_ms, new_parent_id=dparent.id, new_name=dmissing[0],
+                    path=src, new_path=dst)))
+                self._touch_parent(rpc, old_parent)
+                self._touch_parent(rpc, dparent)
 
     def free(self, path: str, recursive: bool = False, forced: bool = False) -> None:
         path = normalize_path(path)
@@ -753,7 +850,9 @@ class FileSystemMaster(Journaled):
                                                       f"persisted")
                 block_ids.extend(f.block_ids)
         if forced:
-            with RpcContext(self) as rpc, self.tree.lock.write():
+            with self._lock_path(path), RpcContext(self) as rpc, self.tree.lock.write():
+                if inode.deleted:
+                    return
                 nodes = [inode] + (self.tree.descendants(inode) if inode.is_directory else [])
                 for f in nodes:
                     if f.pinned and not f.deleted:
@@ -768,70 +867,88 @@ class FileSystemMaster(Journaled):
                       pinned_media=None) -> None:
         path = normalize_path(path)
         self._count("Master.SetAttributeOps")
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            chain, missing = self.tree.resolve(path)
-            if missing:
-                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-            inode = chain[-1]
-            user = self._user()
-            if owner is not None or group is not None:
-                if owner is not None:
-                    self.permission.check_superuser(user)
-                else:
-                    self.permission.check_owner(user, inode, path)
-            elif mode is not None:
-                self.permission.check_owner(user, inode, path)
+        ufs_attr = owner is not None or group is not None or mode is not None
+        with self._lock_path(path):
+            if ufs_attr:
+                with self.tree.lock.read():
+                    n = self.tree.get_or_none(path)
+                    needs_ufs = n is not None and (n.is_persisted or (recursive and n.is_directory and any(
+                        d.is_persisted for d in self.tree.descendants(n))))
+                if needs_ufs:
+                    check_may_block("UFS set owner/mode")
+            ufs_updates = []
+            with RpcContext(self) as rpc, self.tree.lock.write():
+                self._set_attribute_locked(rpc, path, pinned, ttl, ttl_action, persisted, owner, group, mode,
+                                           recursive, replication_min, replication_max, pinned_media, ufs_updates)
+            # UFS owner/mode propagation after the tree lock, still under the path lock
+            for tpath, t_owner, t_group in ufs_updates:
+                try:
+                    res = self._resolve_ufs(tpath)
+                    if owner is not None or group is not None:
+                        res.ufs.set_owner(res.uri, owner or t_owner, group or t_group)
+                    if mode is not None:
+                        res.ufs.set_mode(res.uri, mode)
+                except Exception:  # noqa: BLE001
+                    LOG.debug("ufs attribute propagation failed for %s", tpath)
+
+    def _set_attribute_locked(self, rpc, path, pinned, ttl, ttl_action, persisted, owner, group, mode, recursive,
+                              replication_min, replication_max, pinned_media, ufs_updates) -> None:
+        chain, missing = self.tree.resolve(path)
+        if missing:
+            raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+        inode = chain[-1]
+        user = self._user()
+        if owner is not None or group is not None:
+            if owner is not None:
+                self.permission.check_superuser(user)
             else:
-                self._check(chain, Bits.WRITE, path)
-            targets = [inode] + (self.tree.descendants(inode) if recursive and inode.is_directory else [])
-            for t in targets:
-                u = pb.journal.UpdateInodeEntry(id=t.id)
-                changed = False
-                if pinned is not None and (t.is_file or t is inode):
-                    u.pinned = pinned
-                    changed = True
-                    if pinned_media:
-                        u.medium_type.extend(pinned_media)
-                if ttl is not None and t is inode:
-                    u.ttl = ttl
-                    u.ttlAction = pb.journal.PTtlAction.values_by_name[ttl_action or "DELETE"].number
-                    changed = True
-                if owner is not None:
-                    u.owner = owner
-                    changed = True
-                if group is not None:
-                    u.group = group
-                    changed = True
-                if mode is not None:
-                    u.mode = mode
-                    changed = True
-                if persisted is not None and persisted and not t.is_persisted:
-                    u.persistence_state = PERSISTED
-                    changed = True
-                if changed:
-                    u.last_modification_time_ms = rpc.op_time_ms
-                    self._apply(rpc, pb.journal.JournalEntry(update_inode=u))
-                    if t.is_persisted and (owner is not None or group is not None or mode is not None):
-                        try:
-                            res = self._resolve_ufs(self.tree.path_of(t))
-                            if owner is not None or group is not None:
-                                res.ufs.set_owner(res.uri, owner or t.owner, group or t.group)
-                            if mode is not None:
-                                res.ufs.set_mode(res.uri, mode)
-                        except Exception:  # noqa: BLE001
-                            LOG.debug("ufs attribute propagation failed for %s", t.name)
-                if t.is_file and (replication_min is not None or replication_max is not None):
-                    rmin = t.replication_min if replication_min is None else replication_min
-                    rmax = t.replication_max if replication_max is None else replication_max
-                    if rmax != -1 and rmin > rmax:
-                        raise InvalidArgumentException("replication min cannot exceed replication max")
-                    self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
-                        id=t.id, replication_min=rmin, replication_max=rmax)))
+                self.permission.check_owner(user, inode, path)
+        elif mode is not None:
+            self.permission.check_owner(user, inode, path)
+        else:
+            self._check(chain, Bits.WRITE, path)
+        targets = [inode] + (self.tree.descendants(inode) if recursive and inode.is_directory else [])
+        for t in targets:
+            u = pb.journal.UpdateInodeEntry(id=t.id)
+            changed = False
+            if pinned is not None and (t.is_file or t is inode):
+                u.pinned = pinned
+                changed = True
+                if pinned_media:
+                    u.medium_type.extend(pinned_media)
+            if ttl is not None and t is inode:
+                u.ttl = ttl
+                u.ttlAction = pb.journal.PTtlAction.values_by_name[ttl_action or "DELETE"].number
+                changed = True
+            if owner is not None:
+                u.owner = owner
+                changed = True
+            if group is not None:
+                u.group = group
+                changed = True
+            if mode is not None:
+                u.mode = mode
+                changed = True
+            if persisted is not None and persisted and not t.is_persisted:
+                u.persistence_state = PERSISTED
+                changed = True
+            if changed:
+                u.last_modification_time_ms = rpc.op_time_ms
+                if t.is_persisted and (owner is not None or group is not None or mode is not None):
+                    ufs_updates.append((self.tree.path_of(t), t.owner, t.group))
+                self._apply(rpc, pb.journal.JournalEntry(update_inode=u))
+            if t.is_file and (replication_min is not None or replication_max is not None):
+                rmin = t.replication_min if replication_min is None else replication_min
+                rmax = t.replication_max if replication_max is None else replication_max
+                if rmax != -1 and rmin > rmax:
+                    raise InvalidArgumentException("replication min cannot exceed replication max")
+                self._apply(rpc, pb.journal.JournalEntry(update_inode_file=pb.journal.UpdateInodeFileEntry(
+                    id=t.id, replication_min=rmin, replication_max=rmax)))
 
     def set_acl(self, path: str, action: str, entries, recursive: bool = False) -> None:
         from ..security.acl import AclEntry
         path = normalize_path(path)
-        with RpcContext(self) as rpc, self.tree.lock.write():
+        with self._lock_path(path), RpcContext(self) as rpc, self.tree.lock.write():
             chain, missing = self.tree.resolve(path)
             if missing:
                 raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
@@ -846,8 +963,9 @@ class FileSystemMaster(Journaled):
                     recursive=recursive)))
 
     def set_xattr(self, path: str, key: str, value: bytes) -> None:
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            inode = self.tree.get(normalize_path(path))
+        path = normalize_path(path)
+        with self._lock_path(path), RpcContext(self) as rpc, self.tree.lock.write():
+            inode = self.tree.get(path)
             u = pb.journal.UpdateInodeEntry(id=inode.id)
             u.xAttr[key] = value
             self._apply(rpc, pb.journal.JournalEntry(update_inode=u))
@@ -859,27 +977,30 @@ class FileSystemMaster(Journaled):
         alluxio_path = normalize_path(alluxio_path)
         from ..underfs import registry
         self.mount_table.validate_new_mount(alluxio_path, ufs_uri)
-        ufs = registry.create(ufs_uri, self.conf, properties)
-        if not ufs.is_directory(ufs_uri):
-            raise InvalidPathException(f"Ufs path {ufs_uri} does not exist or is not a directory")
-        mount_id = ids.create_mount_id()
-        st = ufs.get_status(ufs_uri)  # UFS I/O stays outside the tree lock
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            chain, missing = self.tree.resolve(alluxio_path)
-            if not missing:
-                raise FileAlreadyExistsException(f"mount point {alluxio_path} already exists in Alluxio")
-            if len(missing) > 1:
-                raise FileDoesNotExistException(f"parent of {alluxio_path} does not exist")
-            parent = chain[-1]
-            self._check(chain, Bits.WRITE, alluxio_path)
-            info = MountInfo(alluxio_path, ufs_uri, mount_id, read_only, shared, properties)
-            self._apply(rpc, info.to_entry())
-            owner, group = self._owner_group()
-            mode = st.mode if st is not None else 0o755
-            for e in self.tree.new_directory_entries(parent, missing[0], st.owner or owner if st else owner,
-                                                    st.group or group if st else group, mode, True,
-                                                    mount_point=True):
-                self._apply(rpc, e)
+        check_may_block("UFS mount check")
+        with self._lock_path(alluxio_path):
+            ufs = registry.create(ufs_uri, self.conf, properties)
+            if not ufs.is_directory(ufs_uri):
+                raise InvalidPathException(f"Ufs path {ufs_uri} does not exist or is not a directory")
+            mount_id = ids.create_mount_id()
+            st = ufs.get_status(ufs_uri)  # UFS I/O under the path lock only
+            with RpcContext(self) as rpc, self.tree.lock.write():
+                chain, missing = self.tree.resolve(alluxio_path)
+                if not missing:
+                    raise FileAlreadyExistsException(f"mount point {alluxio_path} already exists in Alluxio")
+                if len(missing) > 1:
+                    raise FileDoesNotExistException(f"parent of {alluxio_path} does not exist")
+                parent = chain[-1]
+                self._check(chain, Bits.WRITE, alluxio_path)
+                self.mount_table.validate_new_mount(alluxio_path, ufs_uri)
+                info = MountInfo(alluxio_path, ufs_uri, mount_id, read_only, shared, properties)
+                self._apply(rpc, info.to_entry())
+                owner, group = self._owner_group()
+                mode = st.mode if st is not None else 0o755
+                for e in self.tree.new_directory_entries(parent, missing[0], st.owner or owner if st else owner,
+                                                        st.group or group if st else group, mode, True,
+                                                        mount_point=True):
+                    self._apply(rpc, e)
 
     def unmount(self, alluxio_path: str) -> None:
         alluxio_path = normalize_path(alluxio_path)
@@ -891,21 +1012,22 @@ class FileSystemMaster(Journaled):
             if mp != alluxio_path and mp.startswith(alluxio_path.rstrip("/") + "/"):
                 raise InvalidPathException(f"cannot unmount {alluxio_path}: nested mount {mp}")
         block_ids = []
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            chain, missing = self.tree.resolve(alluxio_path)
-            if not missing:
-                inode = chain[-1]
-                victims = self.tree.descendants(inode) + [inode]
-                for v in victims:
-                    if v.is_file:
-                        block_ids.extend(v.block_ids)
-                for v in victims:
-                    self._apply(rpc, pb.journal.JournalEntry(delete_file=pb.journal.DeleteFileEntry(
-                        id=v.id, recursive=True, op_time_ms=rpc.op_time_ms, alluxioOnly=True)))
-            self._apply(rpc, pb.journal.JournalEntry(delete_mount_point=pb.journal.DeleteMountPointEntry(
-                alluxio_path=alluxio_path)))
-        if block_ids:
-            self.block_master.remove_blocks(block_ids, delete=True)
+        with self._lock_path(alluxio_path), RpcContext(self) as rpc:
+            with self.tree.lock.write():
+                chain, missing = self.tree.resolve(alluxio_path)
+                if not missing:
+                    inode = chain[-1]
+                    victims = self.tree.descendants(inode) + [inode]
+                    for v in victims:
+                        if v.is_file:
+                            block_ids.extend(v.block_ids)
+                    for v in victims:
+                        self._apply(rpc, pb.journal.JournalEntry(delete_file=pb.journal.DeleteFileEntry(
+                            id=v.id, recursive=True, op_time_ms=rpc.op_time_ms, alluxioOnly=True)))
+                self._apply(rpc, pb.journal.JournalEntry(delete_mount_point=pb.journal.DeleteMountPointEntry(
+                    alluxio_path=alluxio_path)))
+            if block_ids:
+                rpc.after.append(lambda: self.block_master.remove_blocks(block_ids, delete=True))
 
     def update_mount(self, alluxio_path: str, read_only: bool | None = None, shared: bool | None = None,
                      properties: dict | None = None) -> None:
@@ -958,7 +1080,11 @@ class FileSystemMaster(Journaled):
                       quiet: bool = False, cache=None) -> None:
         """Load ``path`` (and its missing ancestors / children) from the UFS.  ``cache`` is the
         :class:`sync.UfsStatusCache` of a running sync; a recursive load without one makes its own
-        so sub-directory listings are prefetched on the sync pool while the tree is built."""
+        so sub-directory listings are prefetched on the sync pool while the tree is walked.
+
+        Two phases (InodeSyncStream / loadMetadataIfNotExist :2632): the UFS walk runs holding only
+        the path lock of the subtree being loaded, and builds a plan; the plan is then applied in
+        batches of ``alluxio.master.metadata.load.batch`` inodes per tree-lock section."""
         path = normalize_path(path)
         self._count("Master.LoadMetadataOps")
         try:
@@ -967,57 +1093,125 @@ class FileSystemMaster(Journaled):
             if quiet:
                 raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
             raise
-        if cache is None and recursive:
-            cache = self._new_status_cache()
-        st = cache.get_status(path) if cache is not None else res.ufs.get_status(res.uri)
-        if st is None:
-            raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-        if cache is not None and st.is_directory:
-            cache.prefetch_children(path)
-        owner_default, group_default = self._owner_group()
-        ufs_blocks: list = []
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            rpc.ufs_blocks = ufs_blocks     # block-master commits of the loaded files, batched
-            chain, missing = self.tree.resolve(path)
-            if missing:
-                if len(missing) > 1 and not create_ancestors:
+        check_may_block("UFS metadata load")
+        with self._lock_create(path):
+            if cache is None and recursive:
+                cache = self._new_status_cache()
+            st = cache.get_status(path) if cache is not None else res.ufs.get_status(res.uri)
+            if st is None:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            if cache is not None and st.is_directory:
+                cache.prefetch_children(path)
+            plan = []                 # ("load", parent path, name, status) | ("loaded", dir path)
+            with self.tree.lock.read():
+                chain, missing = self.tree.resolve(path)
+                if missing and len(missing) > 1 and not create_ancestors:
                     raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-                parent = chain[-1]
-                cur = self.tree.path_of(parent)
-                for i, name in enumerate(missing):
-                    cur = cur.rstrip("/") + "/" + name
-                    r = self._resolve_ufs(cur)
-                    s = st if i == len(missing) - 1 else r.ufs.get_status(r.uri)
-                    if s is None:
-                        raise FileDoesNotExistException(f"Path \"{cur}\" does not exist in UFS.")
-                    self._load_one(rpc, parent, name, s, r, owner_default, group_default)
-                    parent = self.tree.get(cur)
-            inode = self.tree.get(path)
-            if inode.is_directory:
-                self._load_children(rpc, inode, path, recursive, owner_default, group_default, cache)
-        if ufs_blocks:
-            self.block_master.commit_blocks_in_ufs(ufs_blocks)
+                base = self.tree.path_of(chain[-1])
+                if not missing and not chain[-1].is_directory:
+                    return
+            cur = base
+            for i, name in enumerate(missing):
+                nxt = _join(cur, name)
+                if i == len(missing) - 1:
+                    s_ = st
+                elif cache is not None:
+                    s_ = cache.get_status(nxt)
+                else:
+                    r = self._resolve_ufs(nxt)
+                    s_ = r.ufs.get_status(r.uri)
+                if s_ is None:
+                    raise FileDoesNotExistException(f"Path \"{nxt}\" does not exist in UFS.")
+                plan.append(("load", cur, name, s_))
+                cur = nxt
+            if st.is_directory:
+                self._plan_children(plan, path, bool(missing), recursive, cache)
+            self._apply_load_plan(plan)
         self.absent_cache.process_existence(path)
+
+    def _plan_children(self, plan, path, is_new, recursive, cache) -> None:
+        """Walk the UFS below ``path`` (listings only, no tree lock) and append what is missing
+        from Alluxio to ``plan`` parents-first."""
+        stack = [(path, is_new)]
+        while stack:
+            dp, new_dir = stack.pop()
+            if cache is not None:
+                listing = cache.fetch_children(dp) or []
+            else:
+                r = self._resolve_ufs(dp)
+                listing = r.ufs.list_status(r.uri) or []
+            existing: dict = {}
+            if not new_dir:
+                with self.tree.lock.read():
+                    d = self.tree.get_or_none(dp)
+                    if d is not None and d.is_directory:
+                        existing = dict(self.tree.children.get(d.id, {}))
+                        existing = {k: self.tree.inodes.get(v) for k, v in existing.items()}
+            for cst in listing:
+                if "/" in cst.name or not cst.name:
+                    continue
+                have = existing.get(cst.name)
+                if have is None:
+                    plan.append(("load", dp, cst.name, cst))
+                if recursive and cst.is_directory and (have is None or have.is_directory):
+                    cp = _join(dp, cst.name)
+                    if cache is not None:
+                        cache.prefetch_children(cp)     # listed on the pool while we walk
+                    stack.append((cp, have is None))
+            plan.append(("loaded", dp))
+
+    def _apply_load_plan(self, plan) -> int:
+        """Apply a load plan: one journal context, ``load.batch`` plan steps per tree write-lock
+        section, the block-master commits of the loaded files batched per section."""
+        if not plan:
+            return 0
+        owner_default, group_default = self._owner_group()
+        batch = max(1, self.conf.get_int("alluxio.master.metadata.load.batch", "2048") if self.conf else 2048)
+        dirs: dict = {}       # path -> directory inode (resolved once per plan)
+        n = 0
+        with RpcContext(self) as rpc:
+            for i in range(0, len(plan), batch):
+                ufs_blocks: list = []
+                rpc.ufs_blocks = ufs_blocks
+                with self.tree.lock.write():
+                    for step in plan[i:i + batch]:
+                        if step[0] == "loaded":
+                            d = dirs.get(step[1]) or self.tree.get_or_none(step[1])
+                            if d is not None and d.is_directory and not d.direct_children_loaded:
+                                self._apply(rpc, pb.journal.JournalEntry(
+                                    update_inode_directory=pb.journal.UpdateInodeDirectoryEntry(
+                                        id=d.id, direct_children_loaded=True)))
+                            continue
+                        _kind, ppath, name, st = step
+                        parent = dirs.get(ppath)
+                        if parent is None:
+                            parent = dirs[ppath] = self.tree.get(ppath)
+                        if name in self.tree.children.get(parent.id, {}):
+                            continue
+                        cp = _join(ppath, name)
+                        self._load_one(rpc, parent, name, st, self._resolve_ufs(cp), owner_default, group_default)
+                        n += 1
+                        if st.is_directory:
+                            dirs[cp] = self.tree.inodes[self.tree.children[parent.id][name]]
+                if ufs_blocks:
+                    self.block_master.commit_blocks_in_ufs(ufs_blocks)
+            rpc.ufs_blocks = None
+        return n
 
     def load_listed_children(self, path: str, statuses) -> None:
         """Load the given UFS statuses (from a sync's listing of ``path``) as children of the
-        directory ``path``: one write-lock section and one journal context for the batch, no UFS
-        calls (InodeSyncStream.loadMetadataForPath over a prefetched listing)."""
-        owner_default, group_default = self._owner_group()
-        ufs_blocks: list = []
-        with RpcContext(self) as rpc, self.tree.lock.write():
-            rpc.ufs_blocks = ufs_blocks
-            parent = self.tree.get_or_none(path)
-            if parent is None or not parent.is_directory:
-                return
-            existing = self.tree.children.get(parent.id, {})
-            for st in statuses:
-                if st.name in existing or not st.name or "/" in st.name:
-                    continue
-                r = self._resolve_ufs(path.rstrip("/") + "/" + st.name)
-                self._load_one(rpc, parent, st.name, st, r, owner_default, group_default)
-        if ufs_blocks:
-            self.block_master.commit_blocks_in_ufs(ufs_blocks)
+        directory ``path``: one journal context for the batch, no UFS calls
+        (InodeSyncStream.loadMetadataForPath over a prefetched listing)."""
+        path = normalize_path(path)
+        with self._lock_path(path):
+            with self.tree.lock.read():
+                parent = self.tree.get_or_none(path)
+                if parent is None or not parent.is_directory:
+                    return
+                existing = set(self.tree.children.get(parent.id, {}))
+            plan = [("load", path, st.name, st) for st in statuses
+                    if st.name and "/" not in st.name and st.name not in existing]
+            self._apply_load_plan(plan)
 
     def _sync_pools(self):
         """(sync executor, UFS prefetch pool), created on first use (reference
@@ -1078,32 +1272,6 @@ class FileSystemMaster(Journaled):
         f.last_modification_time_ms = st.last_modified_ms or rpc.op_time_ms
         self._apply(rpc, e)
 
-    def _load_children(self, rpc, inode, path, recursive, owner_default, group_default, cache=None) -> None:
-        stack = [(inode, path)]
-        while stack:
-            d, dp = stack.pop()
-            if cache is not None:
-                listing = cache.fetch_children(dp) or []
-            else:
-                res = self._resolve_ufs(dp)
-                listing = res.ufs.list_status(res.uri) or []
-            existing = self.tree.children.get(d.id, {})
-            for st in listing:
-                if "/" in st.name or not st.name:
-                    continue
-                if st.name not in existing:
-                    r = self._resolve_ufs(dp.rstrip("/") + "/" + st.name)
-                    self._load_one(rpc, d, st.name, st, r, owner_default, group_default)
-                if recursive:
-                    child = self.tree.inodes.get(self.tree.children[d.id].get(st.name))
-                    if child is not None and child.is_directory:
-                        cp = dp.rstrip("/") + "/" + st.name
-                        if cache is not None:
-                            cache.prefetch_children(cp)     # listed on the pool while we build
-                        stack.append((child, cp))
-            self._apply(rpc, pb.journal.JournalEntry(update_inode_directory=pb.journal.UpdateInodeDirectoryEntry(
-                id=d.id, direct_children_loaded=True)))
-
     def _maybe_sync(self, path: str, interval_ms: int, recursive: bool) -> None:
         if interval_ms is None or interval_ms < 0:
             return
@@ -1121,6 +1289,7 @@ class FileSystemMaster(Journaled):
         executor, with directory listings prefetched on the UFS prefetch pool (master/sync.py)."""
         from .sync import InodeSyncStream
         path = normalize_path(path)
+        check_may_block("UFS metadata sync")
         self._count("Master.MetadataSyncOps")
         self.absent_cache.invalidate_prefix(path)
         ex, pre = self._sync_pools()
@@ -1169,7 +1338,7 @@ class FileSystemMaster(Journaled):
     # persistence
     def schedule_async_persistence(self, path: str, persistence_wait_ms: int = 0) -> None:
         path = normalize_path(path)
-        with RpcContext(self) as rpc, self.tree.lock.write():
+        with self._lock_path(path), RpcContext(self) as rpc, self.tree.lock.write():
             f = self.tree.get(path)
             if not f.is_file:
                 raise InvalidPathException(f"{path} is not a file")
@@ -1205,44 +1374,50 @@ class FileSystemMaster(Journaled):
         return n
 
     def persist_done(self, file_id: int, ok: bool) -> None:
-        """Persistence checker callback: mark the file persisted (journaled)."""
+        """Persistence checker callback: mark the file persisted (journaled).  The UFS fingerprint
+        is read under the file's path lock, outside the tree lock."""
         self.persist_jobs.pop(file_id, None)
         if not ok:
             return
-        with RpcContext(self) as rpc, self.tree.lock.write():
+        with self.tree.lock.read():
             f = self.tree.inodes.get(file_id)
             if f is None or f.is_persisted:
                 return
             path = self.tree.path_of(f)
+        with self._lock_path(path):
             fp = Fingerprint.INVALID
             try:
                 res = self._resolve_ufs(path)
                 fp = res.ufs.get_fingerprint(res.uri)
+            except Exception:  # noqa: BLE001
+                pass
+            with RpcContext(self) as rpc, self.tree.lock.write():
+                f = self.tree.inodes.get(file_id)
+                if f is None or f.is_persisted or self.tree.path_of(f) != path:
+                    return
                 # persisting a file also persists its ancestors
                 cur = self.tree.inodes.get(f.parent_id)
                 while cur is not None and not cur.is_persisted:
                     self._apply(rpc, pb.journal.JournalEntry(persist_directory=pb.journal.PersistDirectoryEntry(id=cur.id)))
                     cur = self.tree.inodes.get(cur.parent_id)
+                self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
+                    id=file_id, persistence_state=PERSISTED, ufs_fingerprint=fp)))
+                blocks = list(f.block_ids)
+                mount = self.mount_table.resolve(path)
+            # best effort: staging UFS block files of the UFS tier are garbage now
+            # (DefaultFileSystemMaster persist checker, :3985-3996)
+            try:
+                from ..worker.ufs_fallback import ufs_block_path
+                root = mount.mount.ufs_uri
+                for bid in blocks:
+                    p = ufs_block_path(root, bid)
+                    try:
+                        if mount.ufs.exists(p):
+                            mount.ufs.delete_file(p)
+                    except Exception:  # noqa: BLE001
+                        pass
             except Exception:  # noqa: BLE001
-                pass
-            self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
-                id=file_id, persistence_state=PERSISTED, ufs_fingerprint=fp)))
-            blocks = list(f.block_ids)
-            mount = self.mount_table.resolve(path)
-        # best effort: staging UFS block files of the UFS tier are garbage now
-        # (DefaultFileSystemMaster persist checker, :3985-3996)
-        try:
-            from ..worker.ufs_fallback import ufs_block_path
-            root = mount.mount.ufs_uri
-            for bid in blocks:
-                p = ufs_block_path(root, bid)
-                try:
-                    if mount.ufs.exists(p):
-                        mount.ufs.delete_file(p)
-                except Exception:  # noqa: BLE001
-                    pass
-        except Exception:  # noqa: BLE001
-            LOG.debug("UFS block cleanup after persist failed", exc_info=True)
+                LOG.debug("UFS block cleanup after persist failed", exc_info=True)
 
     def worker_heartbeat(self, worker_id: int, persisted_files: list[int]):
         for fid in persisted_files:

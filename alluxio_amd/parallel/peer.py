@@ -80,6 +80,8 @@ def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "
     from ..ops.native import has_gpu, lib
     from .ipc import map_handle
     from .transfer import cross_page_segments
+    if worker.conf.get_bool("alluxio.test.peer.mapped.pull.fail", "false"):
+        raise RuntimeError("mapped pull failure injected (alluxio.test.peer.mapped.pull.fail)")
     stub = worker.peer_stub(addr)
     session = ids.create_session_id()
     timeout = _rpc_timeout_s(worker)

@@ -136,13 +136,11 @@ class TransferPlane:
         """Collective: ``blocks`` = [(block_id, length, owner_rank)], identical on every rank.
         Afterwards every rank's worker holds every block.  One ``all_gather_into_tensor`` per
         round moves one block from each owner to everyone (rounds = max blocks per owner)."""
-        import torch
         import torch.distributed as dist
         by_owner: dict[int, list[tuple[int, int]]] = {r: [] for r in range(self.world)}
         for bid, length, owner in blocks:
             by_owner[owner].append((bid, length))
         rounds = max((len(v) for v in by_owner.values()), default=0)
-        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
         moved = 0
         with self._collective_lock:
             for k in range(rounds):
@@ -150,31 +148,65 @@ class TransferPlane:
                 shard = max(n for _, n in entries)
                 if shard == 0:
                     continue
-                send = torch.zeros(shard, dtype=torch.uint8, device=dev)
+                send, out = self._staging(shard)
                 mine = entries[self.rank]
-                if mine[0] is not None:
+                if mine[0] is not None:   # bytes past a short block are never read: no zero fill
                     self._copy_block_out(mine[0], mine[1], send)
-                out = torch.empty(shard * self.world, dtype=torch.uint8, device=dev)
                 dist.all_gather_into_tensor(out, send, group=self.group)
-                for r, (bid, n) in enumerate(entries):
-                    if bid is None or r == self.rank or self.w.has_block(bid):
-                        continue
-                    self._store_block(bid, out[r * shard:r * shard + n])
-                    moved += n
+                moved += self._scatter_into_pages(out, shard, entries)
         self.bytes_gathered += moved
         return moved
+
+    def _staging(self, shard: int):
+        """(send[shard], out[shard*world]) views of ONE persistent buffer per plane, grown
+        geometrically: no allocation or zero-fill per round."""
+        import torch
+        need = shard * (self.world + 1)
+        buf = getattr(self, "_stage", None)
+        if buf is None or buf.numel() < need:
+            dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+            cap = max(need, 2 * (buf.numel() if buf is not None else 0))
+            buf = self._stage = torch.empty(cap, dtype=torch.uint8, device=dev)
+        return buf[:shard], buf[shard:shard * (self.world + 1)]
 
     def _copy_block_out(self, block_id: int, n: int, dst) -> None:
         kind = 1 if dst.is_cuda else 0
         self.w.read(block_id, 0, n, dst.data_ptr(), kind, 0, sync=True)
 
-    def _store_block(self, block_id: int, src) -> None:
-        session = ids.create_session_id()
-        n = src.numel()
-        self.w.create_block(session, block_id, 0, "", max(n, 1))
+    def _scatter_into_pages(self, out, shard: int, entries) -> int:
+        """Reserve pages for every block gathered this round (``external_write``), then move all
+        of them out of the staging buffer with ONE batched page-scatter copy, then commit."""
+        from ..ops.native import lib
+        base = out.data_ptr()
+        segs, opened = [], []
         try:
-            self.w.write_ptr(session, block_id, 0, src.data_ptr(), n, 1 if src.is_cuda else 0)
-            self.w.commit_block(session, block_id)
+            for r, (bid, n) in enumerate(entries):
+                if bid is None or r == self.rank or self.w.has_block(bid):
+                    continue
+                session = ids.create_session_id()
+                self.w.create_block(session, bid, 0, "", max(n, 1))
+                opened.append((session, bid, n))
+                pages = self.w.native.external_write(session, bid, 0, n)
+                _p, _d, dps, dbase = self.w.native.block_pages(bid)
+                segs.extend(cross_page_segments(base + r * shard, [0], max(n, 1), dbase, list(pages), dps, 0, n))
+            if segs:
+                if out.is_cuda:
+                    import torch
+                    with torch.cuda.device(out.device):
+                        lib().batched_copy(segs, 0, True)
+                else:
+                    lib().batched_copy(segs, 0, True)
+            moved = 0
+            while opened:
+                session, bid, n = opened[0]
+                self.w.commit_block(session, bid)
+                opened.pop(0)
+                moved += n
+            return moved
         except Exception:
-            self.w.abort_block(session, block_id)
+            for session, bid, _n in opened:
+                try:
+                    self.w.abort_block(session, bid)
+                except Exception:  # noqa: BLE001
+                    LOG.warning("abort of gathered block %d failed", bid, exc_info=True)
             raise

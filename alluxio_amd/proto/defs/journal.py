@@ -99,4 +99,12 @@ msg JournalEntry sequence_number=1:i64 active_sync_tx_id=34:ActiveSyncTxIdEntry
 package alluxio.proto.meta
 msg BlockMeta length=1:i64
 msg BlockLocation worker_id=1:i64 tier=2:str medium_type=3:str
+msg Inode id=1:i64 creation_time_ms=2:i64 is_directory=3:bool ttl=4:i64 ttl_action=5:alluxio.grpc.TtlAction@DELETE
+    last_modified_ms=25:i64 name=6:str parent_id=7:i64 persistence_state=8:str is_pinned=9:bool
+    access_acl=10:alluxio.proto.shared.AccessControlList ufs_fingerprint=11:str medium_type=27:str*
+    last_accessed_ms=30:i64 is_mount_point=12:bool has_direct_children_loaded=13:bool child_count=26:i64
+    default_acl=14:alluxio.proto.shared.AccessControlList block_size_bytes=15:i64 blocks=16:i64*
+    is_cacheable=17:bool is_completed=18:bool length=19:i64 replication_durable=20:i32 replication_max=21:i32
+    replication_min=22:i32 should_persist_time=28:i64 persist_job_id=23:i64 persist_job_temp_ufs_path=24:str
+    xAttr=29:{str,bytes}
 """

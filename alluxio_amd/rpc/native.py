@@ -56,6 +56,17 @@ AUTH_PATH = "@auth"
 _LIVE: "weakref.WeakSet[NativeRpcFrontend]" = weakref.WeakSet()
 
 
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL = _NullCtx()
+
+
 @atexit.register
 def _stop_all() -> None:
     # dispatcher threads sit in C++ with the GIL released: stop them before the interpreter
@@ -146,6 +157,8 @@ class NativeRpcFrontend:
         self._threads: list[threading.Thread] = []
         self._running = False
         self.port = None
+        self._after_init = threading.Lock()
+        self.spilled = 0
 
     def start(self) -> int:
         self.server.start()
@@ -169,6 +182,11 @@ class NativeRpcFrontend:
         for t in self._threads:
             t.join(timeout=2)
         self._threads = []
+        for name in ("_spill_exec", "_after_exec"):
+            pool = getattr(self, name, None)
+            if pool is not None:
+                pool.shutdown(wait=False)
+                setattr(self, name, None)
 
     # ---- dispatch -------------------------------------------------------------------------------
     def _auth(self, token, payload: bytes):
@@ -182,11 +200,19 @@ class NativeRpcFrontend:
             auth.provider.authenticate(user, password)
         self.server.set_user(token, user)
 
-    def _one(self, token, midx, user, payload):
+    def _one(self, token, midx, user, payload, nonblocking: bool = False, carried: dict | None = None):
         """Run one request; returns the reply tuple, or None when the reply is deferred until
-        the journal entries the handler appended are durable (sent by the flush callback)."""
+        the journal entries the handler appended are durable (sent by the flush callback), or
+        when the request moved to the spill pool.
+
+        ``nonblocking`` (fast and mutation lanes): a handler that would wait on a namespace path
+        lock or start UFS I/O raises ``WouldBlock`` before applying anything; the request is then
+        re-run on the spill pool (``alluxio.master.native.rpc.blocking.threads`` threads) so the
+        lanes keep serving other paths (reference: a slow UFS stalls only its own RPC thread)."""
+        from ..master.inode_lock import WouldBlock, nonblocking_lane
         from ..security import as_user
         pending = None
+        after = None
         cache_ep = None
         try:
             if midx == 0:
@@ -198,8 +224,11 @@ class NativeRpcFrontend:
             self.rpc.check(spec)
             req = spec.request.FromString(payload)
             cache_ep = self.server.epoch() if self.cacheable[midx] and _cacheable(req) else None
-            with as_user(user or None), deferred_flush() as d:
+            with as_user(user or None), deferred_flush() as d, (nonblocking_lane() if nonblocking else _NULL):
                 pending = d.pending
+                after = d.after
+                if carried:
+                    pending.update(carried)
                 if spec.server_streaming:
                     parts = []
                     for m in fn(req, _Ctx(user)):
@@ -212,6 +241,10 @@ class NativeRpcFrontend:
             if cache_ep is not None and not pending:
                 self.server.cache_put(midx, user, payload, body, cache_ep)
             reply = (token, 0, "", body)
+        except WouldBlock:
+            self.spilled += 1
+            self._spill_pool().submit(self._spilled, token, midx, user, payload, dict(pending or {}))
+            return None
         except Exception as e:  # noqa: BLE001
             se = ex.wrap(e)
             if not isinstance(e, ex.AlluxioStatusException):
@@ -222,12 +255,23 @@ class NativeRpcFrontend:
                 # behind it (a create, load, sync change or remount bumps the epoch)
                 self.server.cache_put(midx, user, payload, b"", cache_ep, reply[1], reply[2])
         if pending:
-            self._defer(pending, reply)
+            self._defer(pending, reply, after)
             return None
         return reply
 
-    def _defer(self, pending: dict, reply) -> None:
-        """Send ``reply`` once every journal writer in ``pending`` flushed past its counter."""
+    def _run_after(self, after: list, reply) -> None:
+        """after_durable callbacks of a flushed RPC, then its reply (off the journal flush
+        thread: a callback may append + flush journal entries itself)."""
+        for cb in after:
+            try:
+                cb()
+            except Exception:  # noqa: BLE001
+                LOG.exception("post-journal callback failed")
+        self.server.respond_many([reply])
+
+    def _defer(self, pending: dict, reply, after: list | None = None) -> None:
+        """Send ``reply`` once every journal writer in ``pending`` flushed past its counter
+        (after running the RPC's after_durable callbacks; on a failed flush they never run)."""
         left = [len(pending)]
         err = [None]
         lock = threading.Lock()
@@ -242,13 +286,42 @@ class NativeRpcFrontend:
             if not last:
                 return
             if err[0] is None:
-                srv.respond_many([reply])
+                if after:
+                    self._after_pool().submit(self._run_after, list(after), reply)
+                else:
+                    srv.respond_many([reply])
             else:
                 se = ex.wrap(err[0])
                 srv.respond_many([(reply[0], int(se.status), se.message or str(se), b"")])
 
         for w, counter in pending.items():
             w.flush_async(counter, done)
+
+    def _spilled(self, token, midx, user, payload, carried) -> None:
+        reply = self._one(token, midx, user, payload, nonblocking=False, carried=carried)
+        if reply is not None:
+            self.server.respond_many([reply])
+
+    def _spill_pool(self):
+        pool = getattr(self, "_spill_exec", None)
+        if pool is None:
+            import concurrent.futures as cf
+            with self._after_init:
+                pool = getattr(self, "_spill_exec", None)
+                if pool is None:
+                    pool = self._spill_exec = cf.ThreadPoolExecutor(
+                        max(4, self.blocking_threads), thread_name_prefix="native-rpc-spill")
+        return pool
+
+    def _after_pool(self):
+        pool = getattr(self, "_after_exec", None)
+        if pool is None:
+            import concurrent.futures as cf
+            with self._after_init:
+                pool = getattr(self, "_after_exec", None)
+                if pool is None:
+                    pool = self._after_exec = cf.ThreadPoolExecutor(2, thread_name_prefix="rpc-after-durable")
+        return pool
 
     def _loop(self, lane: int, batch: int) -> None:
         srv = self.server
@@ -264,7 +337,8 @@ class NativeRpcFrontend:
             if not reqs:
                 continue
             t0 = time.perf_counter()
-            out = [o for o in (self._one(*r) for r in reqs) if o is not None]
+            nb = lane != LANE_BLOCKING
+            out = [o for o in (self._one(*r, nonblocking=nb) for r in reqs) if o is not None]
             if out:
                 srv.respond_many(out)
             if metrics is not None:

@@ -19,8 +19,11 @@ from .base import (CreateOptions, DeleteOptions, ListOptions, MkdirsOptions, Ope
 
 
 def strip_scheme(path: str) -> str:
+    """``file:///x`` (or the ``sleepfs:///x`` test wrapper's URIs) -> ``/x``."""
     if path.startswith("file://"):
         path = path[len("file://"):]
+    elif path.startswith("sleepfs://"):
+        path = path[len("sleepfs://"):]
     return path or "/"
 
 

@@ -58,6 +58,8 @@ def _load_builtin() -> None:
     register_factory(_ClassFactory("file", LocalUnderFileSystem))
     register_factory(_ClassFactory("mem", MemoryUnderFileSystem))
     from . import s3, web, hdfs, swift, wasb, webhdfs, ozone  # noqa: F401  (self-registering)
+    from .testing import SleepingUfsFactory
+    register_factory(SleepingUfsFactory())
     try:
         from importlib.metadata import entry_points
         for ep in entry_points().select(group="alluxio_amd.underfs"):

@@ -88,6 +88,64 @@ class SleepingUnderFileSystem(DelegatingUnderFileSystem):
         self._nap("mkdirs")
         return super().mkdirs(path, options)
 
+    def delete_directory(self, path, options=None):
+        self._nap("delete_directory")
+        return super().delete_directory(path, options)
+
+    def rename_file(self, src, dst):
+        self._nap("rename_file")
+        return super().rename_file(src, dst)
+
+    def rename_directory(self, src, dst):
+        self._nap("rename_directory")
+        return super().rename_directory(src, dst)
+
+    def exists(self, path):
+        self._nap("exists")
+        return self.delegate.exists(path)
+
+    def get_fingerprint(self, path):
+        self._nap("get_fingerprint")
+        return self.delegate.get_fingerprint(path)
+
+    def set_owner(self, path, owner, group):
+        self._nap("set_owner")
+        return self.delegate.set_owner(path, owner, group)
+
+    def set_mode(self, path, mode):
+        self._nap("set_mode")
+        return self.delegate.set_mode(path, mode)
+
+
+SLEEP_OPS = ("create", "open", "get_status", "list_status", "delete_file", "delete_directory", "mkdirs",
+             "rename_file", "rename_directory", "exists", "get_fingerprint", "set_owner", "set_mode")
+
+
+class SleepingUfsFactory(UnderFileSystemFactory):
+    """``sleepfs:///<local path>``: a local UFS behind :class:`SleepingUnderFileSystem`, so a
+    master in another process can be given a slow UFS by configuration alone (reference
+    SleepingUnderFileSystemFactory).  Latency per op: mount property or configuration key
+    ``alluxio.underfs.sleep.<op>.ms``, default ``alluxio.underfs.sleep.ms`` (0)."""
+
+    scheme = "sleepfs"
+
+    def create(self, uri, conf=None, properties=None):
+        from .local import LocalUnderFileSystem
+        props = dict(properties or {})
+
+        def get(key, default="0"):
+            if key in props:
+                return props[key]
+            if conf is not None and conf.get_raw(key) is not None:
+                return conf.get_raw(key)
+            return default
+        base = float(get("alluxio.underfs.sleep.ms"))
+        sleep = {op: float(get(f"alluxio.underfs.sleep.{op}.ms", str(base))) for op in SLEEP_OPS}
+        local = "/" + uri.split("://", 1)[1].lstrip("/")
+        ufs = SleepingUnderFileSystem(LocalUnderFileSystem(local, conf, properties), sleep)
+        ufs.root_uri = uri
+        return ufs
+
 
 class FlakyUnderFileSystem(DelegatingUnderFileSystem):
     """Fails ``rate`` of the listed operations with an IOError (seeded, reproducible)."""

@@ -22,6 +22,9 @@ Phases (all timed between a barrier + ``torch.cuda.synchronize()`` on both sides
   threads do, so all 256 streams read the same window in lockstep;
 * ``stagger``: stream s starts at s/threads of the file, so the streams read distinct data;
 * ``host``: the ring lives in pinned host memory (a CPU-side reader; the copy crosses to DRAM);
+* ``large``: a ``--large-size`` file (16 GiB by default on GPU: far larger than the 256 MB MALL)
+  written MUST_CACHE from device memory and read by staggered streams, so every byte comes from
+  HBM — the MEM-tier read rate a 288 GB tier serves, not an L2/MALL-resident window;
 * ``remote`` (N > 1): rank r's streams read the file cached on worker (r+1) % N — the peer GPU's
   HBM mapped through HIP IPC and read over xGMI by the kernel on rank r's GPU;
 * ``replicate`` (N > 1): every rank writes a new file with ``--replication`` copies; the local
@@ -46,7 +49,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "StressWorkerBench cached seq-read GB/s (whole node) at 1/2/4/8 MI355X workers"
-PHASES = ("local", "stagger", "host", "remote", "replicate", "duration")
+PHASES = ("local", "stagger", "host", "large", "remote", "replicate", "duration")
 
 
 def parse_args(argv=None):
@@ -65,6 +68,10 @@ def parse_args(argv=None):
     ap.add_argument("--duration", type=float, default=2.0, help="seconds for the duration phase")
     ap.add_argument("--replication", type=int, default=3)
     ap.add_argument("--work-dir", default=None)
+    ap.add_argument("--large-size", default=None,
+                    help="file size of the large phase (default 16g on GPU, 0 = skip; CPU default 0)")
+    ap.add_argument("--prop", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra alluxio property for master/worker/client (repeatable)")
     ap.add_argument("--profile-json", default=None, help="append per-rank timings to this file")
     return ap.parse_args(argv)
 
@@ -130,8 +137,12 @@ def main(argv=None):
     from alluxio_amd.worker.process import AlluxioWorkerProcess
 
     replicas = max(1, min(a.replication, world))
+    large_size = parse_space_size(a.large_size) if a.large_size is not None else ((16 << 30) if gpu else 0)
+    if "large" not in phases:
+        large_size = 0
+    large_size -= large_size % buf
     # own file + one replica of each of (replicas-1) neighbours' replicated files + own replicated file
-    quota = max((2 + replicas) * file_size, (4 << 30) if gpu else (1 << 30))
+    quota = max((2 + replicas) * file_size, (4 << 30) if gpu else (1 << 30)) + large_size
     quota += (-quota) % page
     props = {
         "alluxio.work.dir": work,
@@ -154,6 +165,9 @@ def main(argv=None):
         "alluxio.security.authorization.permission.enabled": "false",
         "alluxio.master.worker.connect.wait.time": "0sec",
     }
+    for kv in a.prop:
+        k, _, v = kv.partition("=")
+        props[k.strip()] = v.strip()
     conf = Configuration(props)
 
     master = None
@@ -177,9 +191,20 @@ def main(argv=None):
     fs = FileSystem(conf=conf.copy(), master_address=master_addr)
     my_addr = worker_address_str(worker.worker.address)
     addrs = [my_addr]
+    devices = [local_rank if gpu else -1]
+    peer_devices = [list(getattr(worker, "peer_devices", []) or [])]
     if distributed:
-        addrs = [None] * world
+        addrs, devices, peer_devices = [None] * world, [None] * world, [None] * world
         dist.all_gather_object(addrs, my_addr)
+        dist.all_gather_object(devices, local_rank if gpu else -1)
+        dist.all_gather_object(peer_devices, list(getattr(worker, "peer_devices", []) or []))
+        if gpu:
+            # a remote phase over xGMI needs every rank's peer GPU mapped (hipDeviceEnablePeerAccess)
+            for r in range(world):
+                peer = devices[(r + 1) % world]
+                if peer != devices[r] and peer not in peer_devices[r]:
+                    raise SystemExit(f"rank {r} (device {devices[r]}) has no peer access to device {peer}: "
+                                     f"peer_devices={peer_devices[r]}")
 
     def barrier():
         if distributed:
@@ -277,6 +302,46 @@ def main(argv=None):
                   max(2, min(a.steps, 20)), max(1, min(a.warmup, 3)))
         del ring_host
 
+    if large_size:
+        # 16 GiB of fresh device bytes (generated on the GPU), cached MUST_CACHE from device memory
+        lpath = f"/stress-worker-base/large-{rank}"
+        lsrc = torch.randint(0, 256, (large_size,), dtype=torch.uint8, device=dev_t,
+                             generator=torch.Generator(device=dev_t).manual_seed(99 + rank))
+        sync()
+        t0 = time.perf_counter()
+        fs.write_file(lpath, lsrc, write_type="MUST_CACHE", block_size=block_size)
+        sync()
+        lwrite_s = time.perf_counter() - t0
+        loffs = [((s * large_size) // a.threads) // buf * buf for s in range(a.threads)]
+
+        def verify_dev(reader, ring, src):
+            good = True
+            for s in (0, 1, a.threads // 2, a.threads - 1):
+                for k in (0, depth // 2, depth - 1):
+                    off, n = reader.last_call(s, k)
+                    if n and not torch.equal(ring[s, k, :n], src[off:off + n].to(ring.device)):
+                        good = False
+            return good
+
+        lr = RingStreamReader(fs, lpath, ring_dev, start_offsets=loffs)
+        try:
+            lsteps, lwarm = max(a.steps, 32), max(a.warmup, 2)
+            el, nb = timed(lr, lsteps, lwarm)
+            good = verify_dev(lr, ring_dev, lsrc)
+        finally:
+            lr.close()
+        el_max, total = MAX(el), SUM(float(nb))
+        good = SUM(0.0 if good else 1.0) == 0
+        ok_all = ok_all and good
+        results["large"] = {"GBps": round(total / el_max / 1e9, 3), "s": round(el_max, 5), "bytes": int(total),
+                            "file_size": large_size, "steps": lsteps, "verified": good,
+                            "write_GBps": round(SUM(float(large_size)) / MAX(lwrite_s) / 1e9, 3)}
+        del lsrc
+        fs.delete(lpath)
+        if gpu:
+            torch.cuda.empty_cache()
+        barrier()
+
     if "remote" in phases and world > 1:
         peer = (rank + 1) % world
         peer_data = np.random.default_rng(1234 + peer).integers(0, 256, file_size, dtype=np.uint8)
@@ -286,8 +351,8 @@ def main(argv=None):
 
     if "replicate" in phases and world > 1:
         wm = worker.worker.metrics
-        before = wm.counter("XgmiBytesReceived").count
-        before_sh = wm.counter("PeerSharedBytesReceived").count
+        names = ("XgmiBytesReceived", "PeerSharedBytesReceived", "PeerStreamBytesReceived", "PeerPullFailures")
+        before = {k: wm.counter(k).count for k in names}
         src = torch.from_numpy(data).to(dev_t)
         sync()
         barrier()
@@ -297,19 +362,30 @@ def main(argv=None):
         sync()
         el = time.perf_counter() - t
         barrier()
-        moved = wm.counter("XgmiBytesReceived").count - before
-        moved_sh = wm.counter("PeerSharedBytesReceived").count - before_sh
+        delta = {k: int(SUM(float(wm.counter(k).count - before[k]))) for k in names}
         el_max = MAX(el)
         rst = fs.get_status(f"/stress-worker-base/rep-{rank}")
         good = all(len(f.blockInfo.locations) >= replicas for f in rst.fileBlockInfos)
         good = SUM(0.0 if good else 1.0) == 0
-        ok_all = ok_all and good
+        # every replica byte must have moved over the mapped plane (xGMI between distinct GPUs,
+        # shared DRAM on CPU): a silent gRPC fallback or a failed pull fails the bench
+        expect = world * file_size * (replicas - 1)
+        distinct_gpus = gpu and len(set(devices)) == world
+        plane_ok = (delta["PeerStreamBytesReceived"] == 0 and delta["PeerPullFailures"] == 0
+                    and delta["XgmiBytesReceived"] + delta["PeerSharedBytesReceived"] == expect
+                    and (not distinct_gpus or delta["XgmiBytesReceived"] == expect))
+        if not plane_ok and rank == 0:
+            print(f"replicate: data plane check failed: {delta} (expected {expect} peer bytes"
+                  f"{' over xGMI' if distinct_gpus else ''})", file=sys.stderr, flush=True)
+        ok_all = ok_all and good and plane_ok
         results["replicate"] = {"replicas": replicas,
                                 "write_GBps": round(SUM(float(file_size)) / el_max / 1e9, 3),
                                 "replica_GBps": round(SUM(float(file_size * (replicas - 1))) / el_max / 1e9, 3),
-                                "xgmi_bytes_received": int(SUM(float(moved))),
-                                "shared_bytes_received": int(SUM(float(moved_sh))), "s": round(el_max, 4),
-                                "verified": good}
+                                "xgmi_bytes_received": delta["XgmiBytesReceived"],
+                                "shared_bytes_received": delta["PeerSharedBytesReceived"],
+                                "stream_fallback_bytes_received": delta["PeerStreamBytesReceived"],
+                                "peer_pull_failures": delta["PeerPullFailures"],
+                                "s": round(el_max, 4), "verified": good, "data_plane_ok": plane_ok}
         del src
 
     if "duration" in phases and a.duration > 0:
@@ -359,11 +435,17 @@ def main(argv=None):
             "verified": bool(ok_all),
             "stagger_GBps": results.get("stagger", {}).get("GBps"),
             "host_reader_GBps": results.get("host", {}).get("GBps"),
+            "large_GBps": results.get("large", {}).get("GBps"),
+            "large_file_size": results.get("large", {}).get("file_size"),
             "remote_GBps": results.get("remote", {}).get("GBps"),
             "replication": results.get("replicate"),
             "duration_GBps": results.get("duration", {}).get("GBps"),
             "duration_s": results.get("duration", {}).get("s"),
             "write_GBps_per_worker": round(file_size / write_s / 1e9, 3),
+            "devices": devices,
+            "peer_devices": peer_devices,
+            "process_group": ({"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+                              if distributed else None),
             "phases": results,
         }
         out = {

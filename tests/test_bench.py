@@ -12,13 +12,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(args, tmp_path):
+def _run(args, tmp_path, expect_rc=0):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env["MASTER_ADDR"] = "127.0.0.1"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args, "--work-dir", str(tmp_path)],
                        capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.returncode == expect_rc, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     return json.loads(lines[0])
@@ -29,10 +29,14 @@ SMALL = ["--steps", "3", "--warmup", "1", "--file-size", "8m", "--block-size", "
 
 
 def test_bench_single_rank(tmp_path):
-    out = _run(SMALL, tmp_path)
+    out = _run([*SMALL, "--large-size", "24m"], tmp_path)
     assert out["n_gpus"] == 1 and out["steps"] == 3 and out["warmup"] == 1
     c = out["config"]
     assert c["verified"] and c["stagger_GBps"] > 0 and c["duration_GBps"] > 0
+    large = c["phases"]["large"]
+    assert large["verified"] and large["file_size"] == 24 << 20 and c["large_GBps"] > 0
+    # every call moves 4 KiB except the EOF (reopen) calls
+    assert large["steps"] >= 32 and 0.99 * large["steps"] * 8 * (1 << 20) < large["bytes"] <= large["steps"] * 8 * (1 << 20)
     assert c["remote_GBps"] is None and c["replication"] is None
     assert out["value"] == c["phases"]["local"]["GBps"]
 
@@ -47,3 +51,17 @@ def test_bench_two_ranks_remote_and_replicate(tmp_path):
     assert rep["replicas"] == 2 and rep["verified"]
     # each rank's 8 MiB file got one extra copy, pulled out of the primary's arena
     assert rep["shared_bytes_received"] + rep["xgmi_bytes_received"] == 2 * (8 << 20)
+    assert rep["stream_fallback_bytes_received"] == 0 and rep["peer_pull_failures"] == 0
+    assert rep["data_plane_ok"]
+    assert c["process_group"] == {"backend": "gloo", "world_size": 2}
+    assert c["devices"] == [-1, -1] and len(c["peer_devices"]) == 2
+
+
+def test_bench_fails_when_replicas_fall_back_to_grpc(tmp_path):
+    """A mapped-pull failure makes the replicas come through the gRPC block stream: the bytes
+    still arrive (the write succeeds), but the bench must not report that as the peer data plane."""
+    out = _run(["--gpus", "2", *SMALL, "--phases", "local,replicate",
+                "--prop", "alluxio.test.peer.mapped.pull.fail=true"], tmp_path, expect_rc=1)
+    rep = out["config"]["replication"]
+    assert not rep["data_plane_ok"] and not out["config"]["verified"]
+    assert rep["peer_pull_failures"] > 0 and rep["stream_fallback_bytes_received"] == 2 * (8 << 20)

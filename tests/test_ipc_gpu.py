@@ -89,16 +89,19 @@ from alluxio_amd.worker.process import AlluxioWorkerProcess
 from alluxio_amd.client.file_system import FileSystem
 from alluxio_amd.parallel.transfer import TransferPlane
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=world)
+dev = rank %% torch.cuda.device_count()      # one GPU per rank when the node has them
+torch.cuda.set_device(dev)
+backend = %(backend)r
+dist.init_process_group(backend, init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=world)
 work = %(work)r
 conf = Configuration({"alluxio.master.journal.folder": work + "/journal",
-    "alluxio.worker.tieredstore.level0.dirs.path": "hbm:0", "alluxio.worker.tieredstore.level0.dirs.quota": "256MB",
+    "alluxio.worker.tieredstore.level0.dirs.path": "hbm:%%d" %% dev, "alluxio.worker.tieredstore.level0.dirs.quota": "256MB",
     "alluxio.worker.hbm.page.size": "1MB", "alluxio.user.block.size.bytes.default": "8MB"})
 box = [None]
 if rank == 0:
     m = AlluxioMasterProcess(conf, host="127.0.0.1", port=0, root_ufs=work + "/ufs"); box[0] = m.start(start_heartbeats=False)
 dist.broadcast_object_list(box, src=0)
-w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, device=0, work_dir=work + "/w%%d" %% rank)
+w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, device=dev, work_dir=work + "/w%%d" %% rank)
 w.start(start_heartbeats=False)
 plane = TransferPlane.establish(w.worker)
 fs = FileSystem(conf=conf.copy(), master_address=box[0])
@@ -117,7 +120,29 @@ for i, fbi in enumerate(st.fileBlockInfos):
     got = w.worker.read_bytes(b.blockId, 0, b.length)
     ok = ok and got == odata[i * (8 << 20):i * (8 << 20) + b.length].tobytes()
 dist.barrier()
-print(json.dumps({"rank": rank, "ok": bool(ok), "pulled": pulled, "device_plane": plane.device_plane}), flush=True)
+wm = w.worker.metrics
+res = {"rank": rank, "ok": bool(ok), "pulled": pulled, "device_plane": plane.device_plane, "device": dev,
+       "peer_devices": list(w.peer_devices), "xgmi": wm.counter("XgmiBytesReceived").count,
+       "shared": wm.counter("PeerSharedBytesReceived").count,
+       "stream": wm.counter("PeerStreamBytesReceived").count, "failures": wm.counter("PeerPullFailures").count}
+if %(collective)r:
+    # replicate_all: every rank contributes a fresh 2-block file; afterwards every worker holds all
+    cdata = np.random.default_rng(40 + rank).integers(0, 256, (11 << 20) + 5 * rank, dtype=np.uint8)
+    fs.write_file("/gp/c%%d" %% rank, torch.from_numpy(cdata).to("cuda"), write_type="MUST_CACHE")
+    torch.cuda.synchronize()
+    mine = [(b.blockInfo.blockId, b.blockInfo.length, rank) for b in fs.get_status("/gp/c%%d" %% rank).info.fileBlockInfos]
+    allb = [None] * world
+    dist.all_gather_object(allb, mine)
+    blocks = [x for part in allb for x in part]
+    moved = plane.replicate_all(blocks)
+    good = True
+    for r in range(world):
+        exp = np.random.default_rng(40 + r).integers(0, 256, (11 << 20) + 5 * r, dtype=np.uint8)
+        for i, (bid, n, _o) in enumerate(allb[r]):
+            good = good and w.worker.read_bytes(bid, 0, n) == exp[i * (8 << 20):i * (8 << 20) + n].tobytes()
+    res.update({"gathered": moved, "gather_ok": bool(good),
+                "gather_expect": sum(n for _b, n, r in blocks if r != rank)})
+print(json.dumps(res), flush=True)
 dist.barrier()
 fs.close(); w.stop()
 dist.barrier()
@@ -127,28 +152,55 @@ dist.destroy_process_group()
 """
 
 
-@pytest.mark.gpu
-def test_transfer_plane_device_pull(gpu, tmp_path):
+def _run_plane(tmp_path, backend: str, collective: bool, world: int = 2):
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     path = tmp_path / "plane.py"
-    path.write_text(PLANE % {"root": ROOT, "port": port, "work": str(tmp_path)})
-    procs = [subprocess.Popen([sys.executable, str(path)], env=dict(os.environ, RANK=str(r), WORLD_SIZE="2"),
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    path.write_text(PLANE % {"root": ROOT, "port": port, "work": str(tmp_path), "backend": backend,
+                             "collective": collective})
+    procs = [subprocess.Popen([sys.executable, str(path)], env=dict(os.environ, RANK=str(r), WORLD_SIZE=str(world)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
     outs = []
     for p in procs:
         try:
             out, err = p.communicate(timeout=300)
         except subprocess.TimeoutExpired:
-            p.kill()
+            for q in procs:
+                q.kill()
             pytest.fail("device pull rank timed out")
         assert p.returncode == 0, err[-3000:]
         outs.append(json.loads(out.strip().splitlines()[-1]))
-    for o in outs:
+    return outs
+
+
+@pytest.mark.gpu
+def test_transfer_plane_device_pull(gpu, tmp_path):
+    """Two worker ranks (one GPU each when the node has two; else both on device 0) pull each
+    other's blocks through the mapped plane; no byte may come through the gRPC fallback."""
+    for o in _run_plane(tmp_path, "gloo", False):
         assert o["ok"] and o["device_plane"] and o["pulled"] == 20 * (1 << 20) + 11, o
+        assert o["stream"] == 0 and o["failures"] == 0, o
+        assert o["xgmi"] + o["shared"] == o["pulled"], o
+
+
+@pytest.mark.gpu
+def test_transfer_plane_two_gpus_xgmi_and_rccl(gpu, tmp_path):
+    """Cross-device execution of the data plane: rank r runs on GPU r, enables peer access, pulls
+    the peer's blocks out of the peer GPU's HBM over xGMI (counted as XgmiBytesReceived, never the
+    gRPC fallback), then replicate_all moves blocks with RCCL all-gather (nccl backend)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    outs = _run_plane(tmp_path, "nccl", True)
+    for o in outs:
+        assert o["ok"] and o["pulled"] == 20 * (1 << 20) + 11, o
+        other = 1 - o["rank"]
+        assert o["device"] == o["rank"] and other in o["peer_devices"], o
+        assert o["xgmi"] == o["pulled"] and o["stream"] == 0 and o["failures"] == 0, o
+        assert o["gather_ok"] and o["gathered"] == o["gather_expect"], o
 
 
 @pytest.mark.gpu

@@ -66,6 +66,11 @@ for s in $STEPS; do
       run pmc_dram_local 240 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram_local" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2 --phases local
       run pmc_dram_stagger 240 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram_stagger" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2 --phases local,stagger
       ;;
+    large)
+      # the HBM-resident read rate: 16 GiB file, staggered streams (DRAM read bytes ~= delivered)
+      run bench_large 400 python bench.py --steps 20 --warmup 5 --phases local,stagger,large
+      run pmc_dram_large 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram_large" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2 --phases local,large
+      ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
     evict)
       run pytest_evict 300 python -u -m pytest tests/test_evict_alloc_gpu.py tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread

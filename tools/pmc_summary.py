@@ -34,13 +34,32 @@ def summarise(path: str, bytes_per_req: int = 64) -> dict:
     return out
 
 
+def per_dispatch(path: str, kernel: str, bytes_per_req: int = 64) -> list:
+    """Counters of every dispatch of kernels whose name contains ``kernel``, in dispatch order
+    (to split one run's dispatches into bench phases)."""
+    rows: dict = collections.OrderedDict()
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"]
+        if kernel not in k:
+            continue
+        d = rows.setdefault(int(r["Dispatch_Id"]), {"dispatch": int(r["Dispatch_Id"]),
+                                                     "ns": float(r["End_Timestamp"]) - float(r["Start_Timestamp"])})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"]) * bytes_per_req
+    return [rows[k] for k in sorted(rows)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv", nargs="+")
     ap.add_argument("--bytes-per-req", type=int, default=64)
+    ap.add_argument("--per-dispatch", default=None, help="kernel-name substring: print each dispatch (bytes)")
     a = ap.parse_args()
     for p in a.csv:
-        print(json.dumps({"file": p, "kernels": summarise(p, a.bytes_per_req)}))
+        if a.per_dispatch:
+            for row in per_dispatch(p, a.per_dispatch, a.bytes_per_req):
+                print(json.dumps(row))
+        else:
+            print(json.dumps({"file": p, "kernels": summarise(p, a.bytes_per_req)}))
 
 
 if __name__ == "__main__":
