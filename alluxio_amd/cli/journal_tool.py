@@ -23,10 +23,14 @@ def dump_journal(journal_dir: str, master: str, output_dir: str, start: int = 0,
     os.makedirs(output_dir, exist_ok=True)
     ctype, payload, cp_end = j.read_checkpoint()
     if ctype is not None:
+        from ..journal import checkpoint as ck
         cdir = os.path.join(output_dir, "checkpoints")
         os.makedirs(cdir, exist_ok=True)
         with open(os.path.join(cdir, f"0x0-0x{cp_end:x}.{ctype.name}"), "wb") as f:
             f.write(payload)
+        # human-readable outline (reference CheckpointFormat.parseToHumanReadable)
+        with open(os.path.join(cdir, f"0x0-0x{cp_end:x}.txt"), "w") as f:
+            f.write("\n".join(ck.describe(ck.parse(ck.typed(ctype, payload), master))) + "\n")
         print(f"Checkpoint type {ctype.name} covering [0, {cp_end}) written to {cdir}", file=out)
     n = 0
     with open(os.path.join(output_dir, "edits.txt"), "w") as f:
@@ -58,10 +62,14 @@ def dump_raft_journal(journal_dir: str, master: str | None, output_dir: str, sta
             os.makedirs(cdir, exist_ok=True)
             with open(st.snapshot_path, "rb") as f:
                 hdr = fmt.read_delimited(f, pb.raft.RaftSnapshotHeader)
-                for name, data in fmt.read_compound(f):
+                from ..journal import checkpoint as ck
+                for name, cp in fmt.read_compound(f):
                     if master in (None, "", name):
-                        with open(os.path.join(cdir, f"{name}-0x0-0x{hdr.nextSequenceNumber:x}"), "wb") as g:
-                            g.write(data)
+                        base = os.path.join(cdir, f"{name}-0x0-0x{hdr.nextSequenceNumber:x}")
+                        with open(base, "wb") as g:
+                            g.write(ck.typed(cp.type, cp.body))
+                        with open(base + ".txt", "w") as g:
+                            g.write("\n".join(ck.describe(cp)) + "\n")
             print(f"Snapshot at raft index {hdr.index} (term {hdr.term}, next SN {hdr.nextSequenceNumber}, "
                   f"peers {list(hdr.peers)}) written to {cdir}", file=out)
         n = 0

@@ -259,23 +259,28 @@ def write_compound(f, parts: list[tuple[str, bytes]], sub_type: "CheckpointType 
         f.write(b"\x00")
 
 
-def read_compound(f) -> list[tuple[str, bytes]]:
-    """Components of a COMPOUND checkpoint (header included): (component name, body after the
-    component's own CheckpointType header)."""
-    ctype = read_checkpoint_header(f)
-    if ctype != CheckpointType.COMPOUND:
-        raise ValueError(f"not a COMPOUND checkpoint: {ctype.name}")
-    r = _ChunkedReader(f.read())
+def read_compound(f) -> list:
+    """Components of a COMPOUND checkpoint (header included) as ``(master name, Checkpoint)``:
+    every CheckpointType the reference emits is parsed (nested COMPOUND recursively, LONGS, LONG,
+    INODE_PROTOS, JOURNAL_ENTRY); ROCKS stays an opaque body (see journal/checkpoint.py)."""
+    from .checkpoint import parse
+    cp = parse(f.read())
+    if cp.type != CheckpointType.COMPOUND:
+        raise ValueError(f"not a COMPOUND checkpoint: {cp.type.name}")
+    return [(_NAMES_BACK.get(p.name, p.name), p) for p in cp.parts]
+
+
+def read_legacy_compound(f) -> list[tuple[str, bytes]]:
+    """Round-1 snapshots of this repo: a 4-byte count, then (4-byte name length, name, 8-byte data
+    length, delimited journal entries) per master -- read so old snapshots still install."""
+    (n,) = struct.unpack(">i", f.read(4))
     out = []
-    while True:
-        comp = r.component()
-        if comp is None:
-            return out
-        name, pos = kryo_read_string(comp, 0)
-        (sub,) = struct.unpack(">q", comp[pos:pos + 8])
-        if sub != CheckpointType.JOURNAL_ENTRY:
-            raise ValueError(f"component {name}: unsupported checkpoint type {CheckpointType(sub).name}")
-        out.append((_NAMES_BACK.get(name, name), comp[pos + 8:]))
+    for _ in range(n):
+        (ln,) = struct.unpack(">i", f.read(4))
+        name = f.read(ln).decode()
+        (dl,) = struct.unpack(">q", f.read(8))
+        out.append((name, f.read(dl)))
+    return out
 
 
 def entries_to_bytes(entries) -> bytes:

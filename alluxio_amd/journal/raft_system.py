@@ -23,10 +23,12 @@ import logging
 import os
 import random
 import shutil
+import struct
 import threading
 import time
 
 from ..proto import pb
+from . import checkpoint as ck
 from ..utils.exceptions import JournalClosedException, UnavailableException
 from . import format as fmt
 from .raft import (KIND_JOURNAL, KIND_PRIMARY_START, SVC_RAFT, SVC_RAFT_JOURNAL, LEADER, RaftNode,
@@ -128,7 +130,9 @@ class JournalStateMachine:
                                          nextSequenceNumber=self.next_sn, masters=sorted(comps))
         with open(path, "wb") as f:
             fmt.write_delimited(f, hdr)
-            fmt.write_compound(f, [(n, fmt.entries_to_bytes(comps[n].journal_entries())) for n in sorted(comps)])
+            # JournalStateMachine snapshot: one COMPOUND over the masters, each master's own typed
+            # checkpoint nested inside (JournalUtils.writeToCheckpoint(out, getStateMachines()))
+            f.write(ck.compound([(fmt.CHECKPOINT_NAMES.get(n, n), ck.write_journaled(comps[n])) for n in sorted(comps)]))
             f.flush()
             os.fsync(f.fileno())
 
@@ -141,14 +145,21 @@ class JournalStateMachine:
             return []
         with open(path, "rb") as f:
             hdr = fmt.read_delimited(f, pb.raft.RaftSnapshotHeader)
-            parts = fmt.read_compound(f)
-        for name, data in parts:
+            pos = f.tell()
+            head = f.read(8)
+            f.seek(pos)
+            typed = len(head) == 8 and 0 <= struct.unpack(">q", head)[0] <= max(fmt.CheckpointType)
+            if typed:
+                parts = fmt.read_compound(f)
+            else:      # round-1 framing of this repo
+                parts = [(n, ck.parse(ck.typed(fmt.CheckpointType.JOURNAL_ENTRY, d), n))
+                         for n, d in fmt.read_legacy_compound(f)]
+        for name, cp in parts:
             comp = comps.get(name)
             if comp is None:
                 LOG.warning("snapshot has state for unknown master %s", name)
                 continue
-            for e in fmt.bytes_to_entries(data):
-                UfsJournalSystem._apply(comp, e)
+            ck.restore_journaled(comp, cp, UfsJournalSystem._apply)
         self.next_sn = hdr.nextSequenceNumber
         return list(hdr.peers)
 

@@ -12,6 +12,7 @@ from __future__ import annotations
 import heapq
 import itertools
 import logging
+import struct
 import threading
 import time
 
@@ -380,11 +381,11 @@ class UfsJournalSystem(JournalSystem):
             LOG.warning("%s ignored journal entry %s", comp.journal_name, e.WhichOneof)
 
     def _apply_checkpoint(self, comp, ctype, payload) -> None:
-        if ctype == fmt.CheckpointType.JOURNAL_ENTRY:
-            for e in fmt.bytes_to_entries(payload):
-                self._apply(comp, e)
-        else:
-            raise RuntimeError(f"unsupported checkpoint type {ctype}")
+        """Restore ``comp`` from its checkpoint file: JOURNAL_ENTRY (delimited entries) or the
+        typed/nested formats (e.g. the FileSystemMaster COMPOUND tree, journal/checkpoint.py)."""
+        from . import checkpoint as ck
+        cp = ck.parse(ck.typed(ctype, payload), fmt.CHECKPOINT_NAMES.get(comp.journal_name, comp.journal_name))
+        ck.restore_journaled(comp, cp, self._apply)
 
     def _tail_loop(self) -> None:
         while not self._tail_stop.wait(0.5):
@@ -487,8 +488,9 @@ class UfsJournalSystem(JournalSystem):
                     end = w.writer.next_seq
                 else:
                     end = self._applied.get(name, 0)
-                payload = fmt.entries_to_bytes(comp.journal_entries())
-                j.write_checkpoint(end, fmt.CheckpointType.JOURNAL_ENTRY, payload)
+                from . import checkpoint as ck
+                data = ck.write_journaled(comp)        # typed stream, header included
+                j.write_checkpoint(end, fmt.CheckpointType(struct.unpack(">q", data[:8])[0]), data[8:])
                 j.gc()
 
     def sequence_numbers(self) -> dict[str, int]:

@@ -185,6 +185,97 @@ class FileSystemMaster(Journaled):
         for p, mode in self.ufs_modes.items():
             yield pb.journal.JournalEntry(update_ufs_mode=pb.journal.UpdateUfsModeEntry(ufsPath=p, ufsMode=int(mode)))
 
+    # ---- typed checkpoint (reference JournaledGroup FILE_SYSTEM_MASTER) ------------------------
+    checkpoint_name = "FILE_SYSTEM_MASTER"
+
+    def write_checkpoint(self) -> bytes:
+        """The reference's nested FileSystemMaster checkpoint (see journal/checkpoint.py):
+        INODE_TREE {HEAP_INODE_STORE, PINNED/REPLICATION_LIMITED/TO_BE_PERSISTED ids, TTL buckets,
+        INODE_COUNTER}, INODE_DIRECTORY_ID_GENERATOR, MOUNT_TABLE, MASTER_UFS_MANAGER,
+        ACTIVE_SYNC_MANAGER (DefaultFileSystemMaster.java:480-487 order)."""
+        from ..journal import checkpoint as ck
+        from .inode import inode_to_proto
+        tree = self.tree
+        with tree.lock.read():
+            protos, ttl_ids = [], []
+            if tree.root is not None:
+                queue = [tree.root]
+                while queue:                      # parents first
+                    n = queue.pop()
+                    kids = tree.children.get(n.id) if n.is_directory else None
+                    protos.append(inode_to_proto(n, len(kids) if kids else 0))
+                    if n.ttl != NO_TTL:
+                        ttl_ids.append(n.id)
+                    if kids:
+                        queue.extend(tree.inodes[k] for _nm, k in sorted(kids.items(), reverse=True))
+            pinned = sorted(i for i in tree.pinned_ids if (tree.inodes.get(i) is not None
+                                                           and tree.inodes[i].is_file))
+            inode_tree = ck.compound([
+                ("HEAP_INODE_STORE", ck.inode_protos(protos)),
+                ("PINNED_INODE_FILE_IDS", ck.longs(pinned)),
+                ("REPLICATION_LIMITED_FILE_IDS", ck.longs(sorted(tree.replication_limited))),
+                ("TO_BE_PERSISTED_FILE_IDS", ck.longs(sorted(tree.to_be_persisted))),
+                ("TTL_BUCKET_LIST", ck.longs(ttl_ids)),
+                ("INODE_COUNTER", ck.long_(len(protos))),
+            ])
+            gen = pb.journal.JournalEntry(inode_directory_id_generator=pb.journal.InodeDirectoryIdGeneratorEntry(
+                container_id=tree.dir_ids.container_id, sequence_number=tree.dir_ids.sequence))
+            mounts = [m.to_entry() for p_, m in sorted(self.mount_table.mounts().items()) if p_ != "/"]
+            modes = [pb.journal.JournalEntry(update_ufs_mode=pb.journal.UpdateUfsModeEntry(ufsPath=p_, ufsMode=int(m)))
+                     for p_, m in self.ufs_modes.items()]
+            syncs = [pb.journal.JournalEntry(add_sync_point=pb.journal.AddSyncPointEntry(syncpoint_path=p_, mount_id=mid))
+                     for p_, mid in self.sync_points.items()]
+        return ck.compound([
+            ("INODE_TREE", inode_tree),
+            ("INODE_DIRECTORY_ID_GENERATOR", ck.journal_entries([gen])),
+            ("MOUNT_TABLE", ck.journal_entries(mounts)),
+            ("MASTER_UFS_MANAGER", ck.journal_entries(modes)),
+            ("ACTIVE_SYNC_MANAGER", ck.journal_entries(syncs)),
+        ])
+
+    def restore_checkpoint(self, cp) -> None:
+        """Restore from a typed checkpoint: the nested COMPOUND above (reference layout), with
+        the inode store as INODE_PROTOS (heap) or the write-back CACHING_INODE_STORE wrapping it;
+        a ROCKS_INODE_STORE tarball needs RocksDB and is refused."""
+        from ..journal.format import CheckpointType
+        from .inode import inode_from_proto
+        if cp.type != CheckpointType.COMPOUND:
+            raise ValueError(f"FileSystemMaster checkpoint must be COMPOUND, found {cp.type.name}")
+        self.reset_state()
+        tree = self.tree
+        for part in cp.parts:
+            if part.name == "INODE_TREE":
+                for sub in part.parts:
+                    store = sub
+                    if sub.name == "CACHING_INODE_STORE" and sub.type == CheckpointType.COMPOUND and sub.parts:
+                        store = sub.parts[0]
+                    if store.name in ("HEAP_INODE_STORE", "CACHING_INODE_STORE") or \
+                            store.type == CheckpointType.INODE_PROTOS:
+                        nodes = [inode_from_proto(p_) for p_ in store.inodes()]
+                        tree.inodes.begin()
+                        try:
+                            for n in nodes:
+                                tree.inodes[n.id] = n
+                                if n.is_directory:
+                                    tree.children.setdefault(n.id, {})
+                            for n in nodes:
+                                if n.parent_id == -1:
+                                    tree.root = n
+                                elif n.parent_id in tree.children:
+                                    tree.children[n.parent_id][n.name] = n.id
+                                tree._index(n)
+                        finally:
+                            tree.inodes.end()
+                    elif store.type == CheckpointType.ROCKS:
+                        raise ValueError("ROCKS_INODE_STORE checkpoints need RocksDB (not available here)")
+                    # the id sets, TTL buckets and inode counter are derived from the inodes
+                tree._bump_epoch()
+            else:
+                if part.type != CheckpointType.JOURNAL_ENTRY:
+                    raise ValueError(f"unexpected {part.type.name} checkpoint for {part.name}")
+                for e in part.entries():
+                    self.process_journal_entry(e)
+
     def _journal_ctx(self):
         if self.journal is None:
             return NoopJournalContext()

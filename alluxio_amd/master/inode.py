@@ -246,3 +246,137 @@ class InodeFile(Inode):
             self.persist_job_id = e.persist_job_id
         if e.HasField("temp_ufs_path"):
             self.temp_ufs_path = e.temp_ufs_path
+
+
+# ---- InodeMeta.Inode (checkpoint / metastore encoding) ----------------------------------------
+# Reference MutableInode.toProtoBuilder (MutableInode.java:657-677), MutableInodeFile.toProto
+# (:504-517) / fromProto (:523-550), MutableInodeDirectory.toProto (:278-285) / fromProto
+# (:291-313).  Owner/group/mode travel inside ``access_acl`` (ProtoUtils.toProto(AccessControlList),
+# ProtoUtils.java:93-125): the owning user's and group's actions are the NamedAclActions whose name
+# is "" (AccessControlList.OWNING_USER_KEY / OWNING_GROUP_KEY), the other bits are otherActions.
+def _actions(bits: int):
+    return pb.shared.AclActions(actions=[a for a, b in ((0, 4), (1, 2), (2, 1)) if bits & b])
+
+
+def _bits(acts) -> int:
+    v = 0
+    for a in acts.actions:
+        v |= {0: 4, 1: 2, 2: 1}[a]
+    return v
+
+
+def acl_to_proto(owner: str, group: str, mode: int, acl=None, is_default: bool = False, empty: bool = False):
+    p = pb.shared.AccessControlList(owningUser=owner, owningGroup=group, isDefault=is_default, isEmpty=empty)
+    p.userActions.add(name="", actions=_actions((mode >> 6) & 7))
+    p.groupActions.add(name="", actions=_actions((mode >> 3) & 7))
+    p.otherActions.CopyFrom(_actions(mode & 7))
+    if acl is not None and acl.is_extended:
+        for u, a in sorted(acl.named_users.items()):
+            p.userActions.add(name=u, actions=_actions(a))
+        for g, a in sorted(acl.named_groups.items()):
+            p.groupActions.add(name=g, actions=_actions(a))
+        p.maskActions.CopyFrom(_actions(acl.effective_mask()))
+    return p
+
+
+def acl_from_proto(p):
+    """(owner, group, mode, extended AccessControlList | None, is_empty)."""
+    from ..security.acl import AccessControlList
+    mode = _bits(p.otherActions) if p.HasField("otherActions") else 0
+    ext = AccessControlList(p.owningUser, p.owningGroup, 0, p.isDefault)
+    for n in p.userActions:
+        if n.name == "":
+            mode |= _bits(n.actions) << 6
+        else:
+            ext.named_users[n.name] = _bits(n.actions)
+    for n in p.groupActions:
+        if n.name == "":
+            mode |= _bits(n.actions) << 3
+        else:
+            ext.named_groups[n.name] = _bits(n.actions)
+    if p.HasField("maskActions") and ext.is_extended:
+        ext.mask = _bits(p.maskActions)
+    ext.mode = mode
+    return p.owningUser, p.owningGroup, mode, (ext if ext.is_extended else None), p.isEmpty
+
+
+_TTL_ACTION = {"DELETE": 0, "FREE": 1}
+_TTL_ACTION_BACK = {0: "DELETE", 1: "FREE"}
+
+
+def inode_to_proto(n: Inode, child_count: int = 0):
+    p = pb.metastore.Inode(
+        id=n.id, creation_time_ms=n.creation_time_ms, is_directory=n.is_directory, ttl=n.ttl,
+        ttl_action=_TTL_ACTION.get(n.ttl_action, 0), last_modified_ms=n.last_modification_time_ms,
+        last_accessed_ms=n.last_access_time_ms, name=n.name, parent_id=n.parent_id,
+        persistence_state=n.persistence_state, is_pinned=n.pinned,
+        access_acl=acl_to_proto(n.owner, n.group, n.mode, n.acl), ufs_fingerprint=n.ufs_fingerprint,
+        medium_type=n.medium_types)
+    for k, v in n.xattr.items():
+        p.xAttr[k] = v
+    if n.is_directory:
+        p.is_mount_point = n.mount_point
+        p.has_direct_children_loaded = n.direct_children_loaded
+        p.child_count = child_count
+        d = n.default_acl
+        if d is None:     # DefaultAccessControlList(accessAcl): the access ACL's base, empty
+            p.default_acl.CopyFrom(acl_to_proto(n.owner, n.group, n.mode, None, True, True))
+        else:
+            p.default_acl.CopyFrom(acl_to_proto(d.owner or n.owner, d.group or n.group, d.mode, d, True,
+                                                not d.is_extended and d.mode == 0))
+    else:
+        p.block_size_bytes = n.block_size_bytes
+        p.blocks.extend(n.block_ids)
+        p.is_cacheable = n.cacheable
+        p.is_completed = n.completed
+        p.length = n.length
+        p.replication_durable = n.replication_durable
+        p.replication_max = n.replication_max
+        p.replication_min = n.replication_min
+        p.persist_job_id = n.persist_job_id
+        p.persist_job_temp_ufs_path = n.temp_ufs_path
+        if n.should_persist_time:
+            p.should_persist_time = n.should_persist_time
+    return p
+
+
+def inode_from_proto(p) -> Inode:
+    owner, group, mode, ext, _empty = acl_from_proto(p.access_acl)
+    if p.is_directory:
+        n = InodeDirectory(p.id, p.parent_id, p.name, owner, group, mode, p.creation_time_ms)
+        n.mount_point = p.is_mount_point
+        n.direct_children_loaded = p.has_direct_children_loaded
+        if p.HasField("default_acl") and not p.default_acl.isEmpty:
+            _o, _g, dmode, dext, _e = acl_from_proto(p.default_acl)
+            from ..security.acl import AccessControlList
+            d = dext or AccessControlList(owner, group, dmode, True)
+            d.mode, d.is_default = dmode, True
+            n.default_acl = d
+    else:
+        n = InodeFile(p.id, p.parent_id, p.name, owner, group, mode, p.creation_time_ms,
+                      block_size=p.block_size_bytes)
+        n.block_ids = list(p.blocks)
+        n._next_seq = len(n.block_ids)
+        n.cacheable = p.is_cacheable
+        n.completed = p.is_completed
+        n.length = p.length
+        n.replication_durable = p.replication_durable if p.HasField("replication_durable") else 1
+        n.replication_max = p.replication_max if p.HasField("replication_max") else -1
+        n.replication_min = p.replication_min
+        n.persist_job_id = p.persist_job_id if p.HasField("persist_job_id") else -1
+        n.temp_ufs_path = p.persist_job_temp_ufs_path
+        n.should_persist_time = p.should_persist_time
+    n.last_modification_time_ms = p.last_modified_ms
+    n.last_access_time_ms = p.last_accessed_ms or p.last_modified_ms
+    n.ttl = p.ttl if p.HasField("ttl") else NO_TTL
+    n.ttl_action = _TTL_ACTION_BACK.get(p.ttl_action, "DELETE")
+    n.persistence_state = p.persistence_state or NOT_PERSISTED
+    n.pinned = p.is_pinned
+    n.ufs_fingerprint = p.ufs_fingerprint
+    n.medium_types = list(p.medium_type)
+    n.xattr = dict(p.xAttr)
+    if ext is not None:
+        ext.mode = mode
+        n.acl = ext
+    return n
+

@@ -186,7 +186,8 @@ def test_compound_checkpoint_kryo_golden_bytes():
     assert raw[11:11 + 65536] == payload[:65536]
     rest = len(payload) - 65536
     assert raw[11 + 65536:] == fmt.kryo_varint(rest) + payload[65536:] + b"\x00"
-    assert fmt.read_compound(io.BytesIO(raw)) == [("FileSystemMaster", body)]
+    [(name, cp)] = fmt.read_compound(io.BytesIO(raw))
+    assert name == "FileSystemMaster" and cp.type == fmt.CheckpointType.JOURNAL_ENTRY and cp.body == body
     # Kryo strings: null, empty, 1 char and >= 64 chars take the UTF-8 length form
     assert fmt.kryo_string(None) == b"\x80" and fmt.kryo_string("") == b"\x81"
     assert fmt.kryo_string("A") == b"\x82A"
@@ -207,4 +208,4 @@ def test_raft_snapshot_uses_compound(tmp_path):
     fmt.write_compound(b, [("BlockMaster", fmt.entries_to_bytes(entries)), ("TableMaster", b"")])
     parts = fmt.read_compound(io.BytesIO(b.getvalue()))
     assert [p[0] for p in parts] == ["BlockMaster", "TableMaster"]
-    assert [e.delete_file.id for e in fmt.bytes_to_entries(parts[0][1])] == [0, 1, 2]
+    assert [e.delete_file.id for e in parts[0][1].entries()] == [0, 1, 2]
