@@ -105,14 +105,18 @@ class BlockWorker:
             self._fs_master = self.master_channel.stub("alluxio.grpc.file.FileSystemMasterWorkerService")
         return self._fs_master
 
-    def peer_stub(self, address: str):
-        """BlockWorker stub of another worker (pooled channels)."""
+    def peer_channel(self, address: str):
+        """Pooled channel to another worker (GrpcConnectionPool keyed by address)."""
         from ..rpc import Channel
         with self._peer_lock:
             ch = self._peer_channels.get(address)
             if ch is None:
                 ch = self._peer_channels[address] = Channel(address)
-        return ch.stub("alluxio.grpc.block.BlockWorker")
+        return ch
+
+    def peer_stub(self, address: str):
+        """BlockWorker stub of another worker (pooled channels)."""
+        return self.peer_channel(address).stub("alluxio.grpc.block.BlockWorker")
 
     def peer_fetcher(self, host: str, port: int, length: int | None):
         """Block source for async caching from a peer: xGMI pull through the transfer plane when

@@ -15,23 +15,59 @@ from ..utils import ids
 LOG = logging.getLogger(__name__)
 
 
-def remote_block_fetcher(worker, host: str, port: int, length: int | None = None):
+def _block_length(worker, block_id: int) -> int:
+    """Block length from the master's block info (BlockMasterClientService.GetBlockInfo)."""
+    ch = worker.master_channel
+    if ch is None:
+        raise ValueError(f"length of block {block_id} unknown and no master channel")
+    bi = ch.stub("alluxio.grpc.block.BlockMasterClientService").GetBlockInfo(
+        pb.block.GetBlockInfoPRequest(blockId=block_id)).blockInfo
+    return int(bi.length)
+
+
+def remote_block_fetcher(worker, host: str, port: int, length: int | None = None, chunk_size: int = 1 << 20):
+    """Block source that streams ``block_id`` out of worker ``host:port``'s ``ReadBlock`` service
+    into this worker (RemoteBlockReader.java + GrpcDataReader.java:123-160): the request stream
+    stays open and every received chunk is acknowledged with ``offset_received``, so the source's
+    flow-control window (``alluxio.worker.network.reader.buffer.size.bytes``, 4 MB) paces it;
+    the channel comes from the worker's peer pool; the block length comes from the master."""
     def fetch(block_id: int) -> None:
-        from ..rpc import Channel
-        ch = Channel(f"{host}:{port}")
+        import queue
+        n = length if length and length > 0 else _block_length(worker, block_id)
+        ch = worker.peer_channel(f"{host}:{port}")
+        acks: "queue.Queue" = queue.Queue()
+
+        def requests():
+            yield pb.block.ReadRequest(block_id=block_id, offset=0, length=n, chunk_size=chunk_size)
+            while True:
+                off = acks.get()
+                if off is None:
+                    return
+                yield pb.block.ReadRequest(offset_received=off)
+
         session = ids.ASYNC_CACHE_REMOTE_SESSION_ID
-        reqs = iter([pb.block.ReadRequest(block_id=block_id, offset=0, length=length or -1, chunk_size=1 << 20)])
-        stream = ch.raw_stream("alluxio.grpc.block.BlockWorker", "ReadBlock")(reqs)
-        worker.create_block(session, block_id, 0, "", length or (1 << 20))
+        stream = ch.raw_stream("alluxio.grpc.block.BlockWorker", "ReadBlock")(requests())
+        worker.create_block(session, block_id, 0, "", max(n, 1))
         pos = 0
         try:
             for resp in stream:
-                worker.write_bytes(session, block_id, pos, resp.chunk.data)
-                pos += len(resp.chunk.data)
+                data = resp.chunk.data
+                worker.write_bytes(session, block_id, pos, data)
+                pos += len(data)
+                acks.put(pos)
+                if pos >= n:
+                    break
+            if pos != n:
+                raise IOError(f"block {block_id} from {host}:{port}: got {pos} of {n} bytes")
             worker.commit_block(session, block_id)
         except Exception:
             worker.abort_block(session, block_id)
             raise
+        finally:
+            acks.put(None)
+            cancel = getattr(stream, "cancel", None)
+            if cancel is not None and pos < n:
+                cancel()
     return fetch
 
 

@@ -267,3 +267,54 @@ def test_cache_through_ufs_copy_matches_after_free(cluster):
     cluster.heartbeat_workers()
     assert fs.read_file("/ct/big", read_type="NO_CACHE") == data.tobytes()
     fs.close()
+
+
+def test_remote_fetcher_flow_control_and_master_length(tmp_path):
+    """Worker-to-worker gRPC block fetch (GrpcDataReader.java:123-160 semantics): the block length
+    comes from the master, every chunk is acknowledged, and the source's flow-control window
+    (alluxio.worker.network.reader.buffer.size) really throttles a reader that stops acking."""
+    import queue
+    import threading
+
+    from alluxio_amd.proto import pb
+    from alluxio_amd.rpc import Channel
+    from alluxio_amd.worker.remote import remote_block_fetcher
+    c = LocalAlluxioCluster(num_workers=2, grpc=True, work_dir=str(tmp_path), conf={
+        "alluxio.worker.tieredstore.level0.dirs.path": "dram",
+        "alluxio.worker.tieredstore.level0.dirs.quota": "64MB",
+        "alluxio.worker.network.reader.buffer.size": "1MB",
+        "alluxio.user.block.size.bytes.default": "8MB"}).start()
+    try:
+        fs = c.client()
+        data = os.urandom(6 * MB + 5)
+        fs.write_file("/rf", data, write_type="MUST_CACHE")
+        bi = fs.get_status("/rf").fileBlockInfos[0].blockInfo
+        src = next(w for w in c.workers if w.worker.has_block(bi.blockId))
+        dst = next(w for w in c.workers if w is not src)
+        host, port = src.address.rsplit(":", 1)
+        # 1) a reader that never acks gets at most window + one chunk, then the source pauses
+        got, reqs = [], queue.Queue()
+
+        def it():
+            yield pb.block.ReadRequest(block_id=bi.blockId, offset=0, length=bi.length, chunk_size=256 << 10)
+            while reqs.get() is not None:
+                pass
+        stream = Channel(src.address, force_grpc=True).raw_stream("alluxio.grpc.block.BlockWorker", "ReadBlock")(it())
+
+        def drain():
+            try:
+                for r in stream:
+                    got.append(len(r.chunk.data))
+            except Exception:  # noqa: BLE001 - cancelled below
+                pass
+        t = threading.Thread(target=drain, daemon=True)
+        t.start()
+        t.join(1.5)
+        assert t.is_alive() and sum(got) <= (1 << 20) + (256 << 10), sum(got)
+        reqs.put(None)
+        stream.cancel()
+        # 2) the fetcher (no length given: asked from the master) acks and completes the block
+        remote_block_fetcher(dst.worker, host, int(port))(bi.blockId)
+        assert dst.worker.read_bytes(bi.blockId, 0, bi.length) == data
+    finally:
+        c.stop()

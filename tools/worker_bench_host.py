@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Literal StressWorkerBench host readers against an HBM-tier worker (reference shape).
+
+The reference's StressWorkerBench runs T Java threads, each looping ``read(buf)`` through
+``FileInStream`` (stress/shell/.../StressWorkerBench.java:251-276, WorkerBenchParameters.java:40-70).
+This harness starts a master + one worker whose MEM tier is HBM (``hbm:0``) in this process, then
+runs ``alluxio_amd.stress.worker_bench --mode threads`` in a SEPARATE client process -- so every
+byte crosses a process boundary the way a Java client's does -- once per transport:
+
+* ``grpc``: short-circuit off; blocks stream through the worker's ``ReadBlock`` gRPC service
+  (chunked, ``offset_received`` flow control; the worker D2H-copies HBM pages into the reply);
+* ``ipc``: short-circuit on; the client maps the worker's HBM arena through HIP IPC
+  (``OpenDeviceBlock``) and copies each 4 KiB ``read(buf)`` out of it (the short-circuit path).
+
+    python tools/worker_bench_host.py --threads 32 --duration 10s --warmup 3s --out gpurun_out/wb.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CLIENT = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.conf import Configuration
+from alluxio_amd.stress import worker_bench
+conf = Configuration({props!r})
+fs = FileSystem(conf=conf, master_address={addr!r}, metadata_cache=True)
+r = worker_bench.main({args!r}, fs=fs, print_result=False)
+print("RESULT " + json.dumps(r), flush=True)
+fs.close()
+"""
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", default="256", help="comma list of thread counts")
+    ap.add_argument("--file-size", default="128m")
+    ap.add_argument("--buffer-size", default="4k")
+    ap.add_argument("--block-size", default="64m")
+    ap.add_argument("--duration", default="10s")
+    ap.add_argument("--warmup", default="3s")
+    ap.add_argument("--transports", default="grpc,ipc")
+    ap.add_argument("--tier", default="hbm:0", help="worker MEM tier dir (hbm:N or dram)")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+
+    from alluxio_amd.minicluster import LocalAlluxioCluster
+    import numpy as np
+    from alluxio_amd.utils.format import parse_space_size
+    work = tempfile.mkdtemp(prefix="wbench_")
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": a.tier,
+            "alluxio.worker.tieredstore.level0.dirs.quota": "4GB",
+            "alluxio.worker.hbm.page.size": "2MB",
+            "alluxio.user.block.size.bytes.default": a.block_size,
+            "alluxio.security.authorization.permission.enabled": "false"}
+    rows = []
+    with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=work) as c:
+        fs = c.client()
+        size = parse_space_size(a.file_size)
+        fs.create_directory("/stress-worker-base", recursive=True, allow_exists=True)
+        fs.write_file("/stress-worker-base/data", np.full(size, ord("A"), dtype=np.uint8),
+                      write_type="CACHE_THROUGH", block_size=parse_space_size(a.block_size))
+        st = fs.get_status("/stress-worker-base/data")
+        assert st.in_alluxio_percentage == 100
+        for transport in a.transports.split(","):
+            props = {"alluxio.user.network.inprocess.transport.enabled": "false",
+                     "alluxio.user.short.circuit.enabled": "true" if transport == "ipc" else "false",
+                     "alluxio.user.file.passive.cache.enabled": "false"}
+            for t in a.threads.split(","):
+                args = ["--threads", t, "--file-size", a.file_size, "--buffer-size", a.buffer_size,
+                        "--block-size", a.block_size, "--duration", a.duration, "--warmup", a.warmup,
+                        "--mode", "threads"]
+                t0 = time.time()
+                p = subprocess.run([sys.executable, "-c", CLIENT.format(root=ROOT, addr=c.master.address,
+                                                                       args=args, props=props)],
+                                   capture_output=True, text=True, timeout=600)
+                line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
+                if line is None:
+                    print(p.stderr[-3000:], file=sys.stderr)
+                    return 1
+                r = json.loads(line[7:])
+                row = {"bench": "StressWorkerBench --mode threads (host readers, separate client process)",
+                       "transport": transport, "tier": a.tier, "threads": int(t), "buffer": a.buffer_size,
+                       "file_size": a.file_size, "block_size": a.block_size,
+                       "throughput_MBps": round(r["throughput_MBps"], 1), "bytes": r["bytes"],
+                       "duration_s": r["duration_s"], "errors": r["errors"], "wall_s": round(time.time() - t0, 1)}
+                print(json.dumps(row), flush=True)
+                rows.append(row)
+                if a.out:
+                    with open(a.out, "a") as f:
+                        f.write(json.dumps(row) + "\n")
+        fs.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
