@@ -186,6 +186,47 @@ void set_page_gather_wave_variant(int variant);
 hipError_t launch_page_table_update(PageTableEntry* table, const uint64_t* idx,
                                     const PageTableEntry* entries, uint32_t n, hipStream_t stream);
 
+// K9 put path on the GPU (page_cache_put.hip): probe/claim -> assign (free stack or CLOCK
+// eviction) -> fill, for a batch of device-resident keys; the device table is authoritative.
+struct PutCounters {
+  int32_t free_top;        // entries left on the device free stack (may go negative)
+  uint32_t hand;           // CLOCK hand
+  uint32_t nfresh;         // keys this batch claimed new table entries for
+  uint32_t nevicted;       // victims (their keys in `evicted`)
+  uint32_t ntomb;          // tombstones this batch created
+  uint32_t nfail;          // requests that got no slot
+  uint32_t pad[2];
+};
+struct PagePutArgs {
+  PageTableEntry* table;
+  uint64_t mask;
+  const uint64_t* keys;
+  uint32_t n;
+  uint32_t* tidx;                // [n] table index of each request
+  unsigned long long* tag;       // [table size] (batch << 32) | (request + 1) of the winner
+  unsigned long long batch;
+  uint32_t* stamps;              // [slots] recency (shared with the gather kernel)
+  uint32_t* passed;              // [slots] epoch the CLOCK hand last passed the slot
+  uint32_t epoch;
+  uint32_t nslots;
+  uint64_t* slot_key;            // [slots] key held by each slot (kPageKeyEmpty = free)
+  uint32_t* slot_tidx;           // [slots] table index of that key
+  uint32_t* free_stack;          // [slots]
+  PutCounters* ctr;
+  uint64_t* evicted;             // [n]
+  int32_t* slot_of;              // [n] slot to fill (-1: duplicate or failed)
+  int evict;
+  uint32_t len;
+  const uint8_t* src;
+  uint64_t src_stride;
+  uint8_t* arena;
+  uint64_t page_size;
+};
+hipError_t launch_page_put_probe(const PagePutArgs& a, hipStream_t stream);
+hipError_t launch_page_put_assign(const PagePutArgs& a, hipStream_t stream);
+hipError_t launch_page_put_fill(const PagePutArgs& a, hipStream_t stream);
+hipError_t launch_page_put_revert(const PagePutArgs& a, hipStream_t stream);
+
 // Fill `bytes` at dst with 64-bit words w[i] = splitmix64(seed ^ ((i + word_offset) * K)):
 // synthetic bench/test data that is a pure function of the byte offset inside a block.
 hipError_t launch_fill_pattern(uint8_t* dst, uint64_t bytes, uint64_t seed, uint64_t word_offset,

@@ -43,6 +43,16 @@ DevicePageCache::DevicePageCache(int device, uint64_t capacity_bytes, uint64_t p
     PC_HIP_OK(hipMalloc((void**)&table_d_, table_h_.size() * sizeof(PageTableEntry)));
     PC_HIP_OK(hipMalloc((void**)&stamps_d_, nslots_ * sizeof(uint32_t)));
     PC_HIP_OK(hipMemset(stamps_d_, 0, nslots_ * sizeof(uint32_t)));
+    PC_HIP_OK(hipMalloc((void**)&slot_key_d_, nslots_ * sizeof(uint64_t)));
+    PC_HIP_OK(hipMalloc((void**)&slot_tidx_d_, nslots_ * sizeof(uint32_t)));
+    PC_HIP_OK(hipMalloc((void**)&free_stack_d_, nslots_ * sizeof(uint32_t)));
+    PC_HIP_OK(hipMalloc((void**)&passed_d_, nslots_ * sizeof(uint32_t)));
+    PC_HIP_OK(hipMemset(passed_d_, 0, nslots_ * sizeof(uint32_t)));
+    PC_HIP_OK(hipMalloc((void**)&tag_d_, table_h_.size() * sizeof(unsigned long long)));
+    PC_HIP_OK(hipMemset(tag_d_, 0, table_h_.size() * sizeof(unsigned long long)));
+    PC_HIP_OK(hipMalloc((void**)&ctr_d_, sizeof(PutCounters)));
+    PC_HIP_OK(hipMemset(ctr_d_, 0, sizeof(PutCounters)));
+    PC_HIP_OK(hipHostMalloc((void**)&ctr_h_, sizeof(PutCounters), hipHostMallocDefault));
     ring_.init();
   } else {
     void* p = std::aligned_alloc(64, ((nslots_ * page_size_ + 63) / 64) * 64);
@@ -69,6 +79,16 @@ DevicePageCache::~DevicePageCache() {
     hipFree(keys_d_);
     hipFree(slots_d_);
     hipFree(lens_d_);
+    hipFree(slot_key_d_);
+    hipFree(slot_tidx_d_);
+    hipFree(free_stack_d_);
+    hipFree(passed_d_);
+    hipFree(tag_d_);
+    hipFree(ctr_d_);
+    hipHostFree(ctr_h_);
+    hipFree(put_tidx_d_);
+    hipFree(put_slot_d_);
+    hipFree(put_ev_d_);
   } else {
     std::free((void*)arena_);
   }
@@ -96,6 +116,7 @@ void DevicePageCache::mark_dirty(uint64_t idx) {
 }
 
 void DevicePageCache::table_insert(uint64_t key, int32_t slot, uint32_t len) {
+  host_changed_ = true;
   const uint64_t mask = table_h_.size() - 1;
   uint64_t i = page_key_hash(key) & mask;
   int64_t tomb = -1;
@@ -117,6 +138,7 @@ void DevicePageCache::table_insert(uint64_t key, int32_t slot, uint32_t len) {
 }
 
 void DevicePageCache::table_erase_at(uint64_t idx) {
+  host_changed_ = true;
   table_h_[idx] = PageTableEntry{kPageKeyTomb, -1, 0};
   ++tombstones_;
   mark_dirty(idx);
@@ -249,6 +271,7 @@ std::vector<uint64_t> DevicePageCache::put(uint64_t key, uint64_t src, uint64_t 
   if (key == kPageKeyEmpty || key == kPageKeyTomb) throw StoreError(kErrInvalidArgument, "reserved page key");
   if (len > page_size_) throw StoreError(kErrInvalidArgument, "page larger than the page size");
   std::lock_guard<std::mutex> g(mu_);
+  ensure_host();
   std::vector<uint64_t> evicted;
   int32_t slot;
   const int64_t idx = find_index(key);
@@ -303,6 +326,31 @@ std::vector<uint64_t> DevicePageCache::put_many(const std::vector<uint64_t>& key
       if (last[keys_in[i]] == i) batch.emplace_back(keys_in[i], i);
   }
   std::lock_guard<std::mutex> g(mu_);
+  if (use_device_ && src_kind == (int)MemKind::kDevice && !keys_in.empty() && keys_in.size() <= nslots_) {
+    // the device put path: upload the keys, resolve + evict + fill on the GPU (device sources
+    // only: the fill kernel must never dereference pageable host memory)
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t n = (uint32_t)keys_in.size();
+    if (n > keys_cap_) {
+      wait_gathers();
+      hipFree(keys_d_);
+      hipFree(slots_d_);
+      hipFree(lens_d_);
+      keys_d_ = nullptr;
+      slots_d_ = nullptr;
+      lens_d_ = nullptr;
+      keys_cap_ = 0;
+      const uint32_t cap = std::max<uint32_t>(n, 4096);
+      PC_HIP_OK(hipMalloc((void**)&keys_d_, cap * sizeof(uint64_t)));
+      PC_HIP_OK(hipMalloc((void**)&slots_d_, cap * sizeof(int32_t)));
+      PC_HIP_OK(hipMalloc((void**)&lens_d_, cap * sizeof(uint32_t)));
+      keys_cap_ = cap;
+    }
+    order_after_readers(s);
+    PC_HIP_OK(hipMemcpyAsync(keys_d_, keys_in.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    return put_device_locked(keys_d_, n, src, src_stride, len, src_kind, s, evict);
+  }
+  ensure_host();
   if (!evict) {
     size_t fresh = 0;
     for (const auto& kv : batch) fresh += find_index(kv.first) < 0;
@@ -384,6 +432,7 @@ std::vector<uint64_t> DevicePageCache::put_many(const std::vector<uint64_t>& key
 
 bool DevicePageCache::erase(uint64_t key) {
   std::lock_guard<std::mutex> g(mu_);
+  ensure_host();
   const int64_t idx = find_index(key);
   if (idx < 0) return false;
   const int32_t slot = table_h_[idx].slot;
@@ -395,11 +444,13 @@ bool DevicePageCache::erase(uint64_t key) {
 
 bool DevicePageCache::contains(uint64_t key) const {
   std::lock_guard<std::mutex> g(mu_);
+  const_cast<DevicePageCache*>(this)->ensure_host();
   return find_index(key) >= 0;
 }
 
 std::pair<int32_t, uint32_t> DevicePageCache::lookup(uint64_t key) {
   std::lock_guard<std::mutex> g(mu_);
+  ensure_host();
   const int64_t idx = find_index(key);
   if (idx < 0) return {-1, 0};
   const auto& e = table_h_[idx];
@@ -410,6 +461,7 @@ std::pair<int32_t, uint32_t> DevicePageCache::lookup(uint64_t key) {
 bool DevicePageCache::read(uint64_t key, uint64_t offset, uint64_t len, uint64_t dst, int dst_kind,
                            uint64_t stream) {
   std::lock_guard<std::mutex> g(mu_);
+  ensure_host();
   const int64_t idx = find_index(key);
   if (idx < 0) return false;
   const auto& e = table_h_[idx];
@@ -440,6 +492,7 @@ std::vector<int32_t> DevicePageCache::read_segments(const std::vector<uint64_t>&
   segs.reserve(n);
   hipStream_t st = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(mu_);
+  ensure_host();
   const uint32_t epoch = ++epoch_;
   for (size_t i = 0; i < n; ++i) {
     const int64_t idx = find_index(keys[i]);
@@ -543,9 +596,157 @@ std::vector<int32_t> DevicePageCache::gather_host_keys(const std::vector<uint64_
   return slots;
 }
 
+// ---- device put path (page_cache_put.hip) ------------------------------------------------------
+void DevicePageCache::reserve_put(uint32_t n) {
+  if (n <= put_cap_) return;
+  wait_gathers();
+  hipFree(put_tidx_d_);
+  hipFree(put_slot_d_);
+  hipFree(put_ev_d_);
+  put_tidx_d_ = nullptr;
+  put_slot_d_ = nullptr;
+  put_ev_d_ = nullptr;
+  put_cap_ = 0;
+  const uint32_t cap = std::max<uint32_t>(n, 4096);
+  PC_HIP_OK(hipMalloc((void**)&put_tidx_d_, cap * sizeof(uint32_t)));
+  PC_HIP_OK(hipMalloc((void**)&put_slot_d_, cap * sizeof(int32_t)));
+  PC_HIP_OK(hipMalloc((void**)&put_ev_d_, cap * sizeof(uint64_t)));
+  put_cap_ = cap;
+}
+
+void DevicePageCache::ensure_device(hipStream_t stream) {
+  if (!host_changed_ && !full_upload_ && dirty_.empty()) return;
+  sync_device_stamps();                          // gathers' recency first, then push the merge
+  flush_table(stream);                           // table entries (dirty or full)
+  std::vector<uint32_t> tidx(nslots_, 0);
+  for (uint64_t i = 0; i < table_h_.size(); ++i) {
+    const auto& e = table_h_[i];
+    if (e.key != kPageKeyEmpty && e.key != kPageKeyTomb && e.slot >= 0) tidx[e.slot] = (uint32_t)i;
+  }
+  PC_HIP_OK(hipMemcpyAsync(slot_key_d_, slot_key_.data(), nslots_ * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+  PC_HIP_OK(hipMemcpyAsync(slot_tidx_d_, tidx.data(), nslots_ * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+  if (!free_.empty())
+    PC_HIP_OK(hipMemcpyAsync(free_stack_d_, free_.data(), free_.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                             stream));
+  PC_HIP_OK(hipMemcpyAsync(stamps_d_, stamp_h_.data(), nslots_ * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+  // CLOCK reference state: a host-side page counts as referenced only once it is touched again
+  PC_HIP_OK(hipMemcpyAsync(passed_d_, stamp_h_.data(), nslots_ * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+  ctr_h_->free_top = (int32_t)free_.size();
+  PC_HIP_OK(hipMemcpyAsync(&ctr_d_->free_top, &ctr_h_->free_top, sizeof(int32_t), hipMemcpyHostToDevice, stream));
+  PC_HIP_OK(hipStreamSynchronize(stream));       // pageable sources
+  host_changed_ = false;
+}
+
+void DevicePageCache::ensure_host() {
+  if (!dev_owner_) return;
+  wait_gathers();                                // device puts already completed on their stream
+  PC_HIP_OK(hipMemcpy(table_h_.data(), table_d_, table_h_.size() * sizeof(PageTableEntry), hipMemcpyDeviceToHost));
+  PC_HIP_OK(hipMemcpy(slot_key_.data(), slot_key_d_, nslots_ * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  PC_HIP_OK(hipMemcpy(ctr_h_, ctr_d_, sizeof(PutCounters), hipMemcpyDeviceToHost));
+  const int32_t top = std::max<int32_t>(0, ctr_h_->free_top);
+  free_.assign(top, 0);
+  if (top) PC_HIP_OK(hipMemcpy(free_.data(), free_stack_d_, top * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  tombstones_ = 0;
+  for (const auto& e : table_h_) tombstones_ += e.key == kPageKeyTomb;
+  for (uint64_t i : dirty_) dirty_flag_[i] = 0;
+  dirty_.clear();
+  full_upload_ = false;                          // the device copy equals what was just pulled
+  dev_owner_ = false;
+  device_stamps_dirty_ = true;
+  sync_device_stamps();
+  host_changed_ = false;
+}
+
+std::vector<uint64_t> DevicePageCache::put_many_device(uint64_t keys, uint32_t n, uint64_t src, uint64_t src_stride,
+                                                       uint64_t len, int src_kind, uint64_t stream, bool evict) {
+  if (!use_device_) throw StoreError(kErrInvalidArgument, "put_many_device needs a device cache");
+  if (len > page_size_) throw StoreError(kErrInvalidArgument, "page larger than the page size");
+  if (n == 0) return {};
+  std::lock_guard<std::mutex> g(mu_);
+  return put_device_locked((const uint64_t*)keys, n, src, src_stride, len, src_kind, (hipStream_t)stream, evict);
+}
+
+std::vector<uint64_t> DevicePageCache::put_device_locked(const uint64_t* keys_d, uint32_t n, uint64_t src,
+                                                         uint64_t src_stride, uint64_t len, int src_kind,
+                                                         hipStream_t s, bool evict) {
+  if (n > nslots_) throw StoreError(kErrInvalidArgument, "device put batch larger than the cache");
+  if (src_kind != (int)MemKind::kDevice)
+    throw StoreError(kErrInvalidArgument, "device put path needs a device source (host sources: put_many)");
+  reserve_put(n);
+  ensure_device(s);
+  // slots about to be rewritten may still be read by a queued gather on another stream
+  order_after_readers(s);
+  PutCounters* c = ctr_h_;
+  PagePutArgs a{};
+  a.table = table_d_;
+  a.mask = table_h_.size() - 1;
+  a.keys = keys_d;
+  a.n = n;
+  a.tidx = put_tidx_d_;
+  a.tag = tag_d_;
+  a.batch = ++batch_;
+  a.stamps = stamps_d_;
+  a.passed = passed_d_;
+  a.epoch = ++epoch_;
+  a.nslots = nslots_;
+  a.slot_key = slot_key_d_;
+  a.slot_tidx = slot_tidx_d_;
+  a.free_stack = free_stack_d_;
+  a.ctr = ctr_d_;
+  a.evicted = put_ev_d_;
+  a.slot_of = put_slot_d_;
+  a.evict = evict ? 1 : 0;
+  a.len = (uint32_t)len;
+  a.src = (const uint8_t*)src;
+  a.src_stride = src_stride;
+  a.arena = (uint8_t*)arena_;
+  a.page_size = page_size_;
+  // nfresh .. nfail start at 0 (free_top and the CLOCK hand carry over)
+  PC_HIP_OK(hipMemsetAsync(&ctr_d_->nfresh, 0, 4 * sizeof(uint32_t), s));
+  PC_HIP_OK(launch_page_put_probe(a, s));
+  dev_owner_ = true;                             // the device table changed from here on
+  if (!evict) {
+    PC_HIP_OK(hipMemcpyAsync(c, ctr_d_, sizeof(PutCounters), hipMemcpyDeviceToHost, s));
+    PC_HIP_OK(hipStreamSynchronize(s));
+    if (c->nfail || (int64_t)c->nfresh > (int64_t)std::max<int32_t>(0, c->free_top)) {
+      PC_HIP_OK(launch_page_put_revert(a, s));
+      PC_HIP_OK(hipMemcpyAsync(c, ctr_d_, sizeof(PutCounters), hipMemcpyDeviceToHost, s));
+      PC_HIP_OK(hipStreamSynchronize(s));
+      dev_free_ = std::max<int32_t>(0, c->free_top);
+      tombstones_ += c->ntomb;
+      throw StoreError(kErrOutOfSpace, "page cache is full");
+    }
+  }
+  PC_HIP_OK(launch_page_put_assign(a, s));
+  PC_HIP_OK(launch_page_put_fill(a, s));
+  PC_HIP_OK(hipMemcpyAsync(c, ctr_d_, sizeof(PutCounters), hipMemcpyDeviceToHost, s));
+  PC_HIP_OK(hipStreamSynchronize(s));
+  std::vector<uint64_t> evicted(std::min<uint32_t>(c->nevicted, n));
+  if (!evicted.empty())
+    PC_HIP_OK(hipMemcpy(evicted.data(), put_ev_d_, evicted.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (c->free_top < 0) {
+    c->free_top = 0;
+    PC_HIP_OK(hipMemcpyAsync(&ctr_d_->free_top, &c->free_top, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    PC_HIP_OK(hipStreamSynchronize(s));
+  }
+  dev_free_ = c->free_top;
+  tombstones_ += c->ntomb;
+  device_stamps_dirty_ = true;
+  const uint32_t failed = c->nfail;
+  if (tombstones_ > table_h_.size() / 4) {       // reclaim tombstones: rebuild on the host, push
+    ensure_host();
+    rebuild_table();
+    ensure_device(s);
+  }
+  if (failed) throw StoreError(kErrOutOfSpace, "page cache could not place " + std::to_string(failed) + " pages");
+  return evicted;
+}
+
 void DevicePageCache::clear() {
   std::lock_guard<std::mutex> g(mu_);
   wait_gathers();
+  dev_owner_ = false;
+  host_changed_ = true;
   std::fill(table_h_.begin(), table_h_.end(), PageTableEntry{kPageKeyEmpty, -1, 0});
   tombstones_ = 0;
   std::fill(slot_key_.begin(), slot_key_.end(), kPageKeyEmpty);

@@ -41,6 +41,13 @@ class DevicePageCache {
   // page of the batch it had staged (those keys read as misses afterwards).
   std::vector<uint64_t> put_many(const std::vector<uint64_t>& keys, uint64_t src, uint64_t src_stride,
                                  uint64_t len, int src_kind, uint64_t stream, bool evict);
+  // Device-resident keys (`keys` = n uint64 in device memory): the whole put runs on the GPU
+  // (page_cache_put.hip: probe/claim, free-stack or CLOCK eviction, fill) with the device table
+  // authoritative; the host mirror is pulled back lazily by the next host-side operation.
+  // n must not exceed the slot count.  Same contract as put_many otherwise (last duplicate wins;
+  // evict=false and not enough free slots: nothing changes, throws).
+  std::vector<uint64_t> put_many_device(uint64_t keys, uint32_t n, uint64_t src, uint64_t src_stride, uint64_t len,
+                                        int src_kind, uint64_t stream, bool evict);
   bool erase(uint64_t key);
   bool contains(uint64_t key) const;
   // (slot, len) or (-1, 0); bumps recency.
@@ -68,7 +75,8 @@ class DevicePageCache {
 
   uint64_t page_size() const { return page_size_; }
   uint32_t slots() const { return nslots_; }
-  uint32_t used() const { return (uint32_t)(nslots_ - free_.size()); }
+  uint32_t used() const { return (uint32_t)(nslots_ - (dev_owner_ ? (uint64_t)dev_free_ : free_.size())); }
+  bool device_owned() const { return dev_owner_; }
   uint64_t table_size() const { return table_h_.size(); }
   uint64_t arena() const { return arena_; }
   bool on_device() const { return use_device_; }
@@ -88,6 +96,11 @@ class DevicePageCache {
   std::vector<uint64_t> evict_lru(uint32_t need);
   void sync_device_stamps();
   void wait_gathers();
+  void ensure_host();                            // device table authoritative -> pull it back
+  void ensure_device(hipStream_t stream);        // host changed -> push table, slots, free stack
+  std::vector<uint64_t> put_device_locked(const uint64_t* keys_d, uint32_t n, uint64_t src, uint64_t src_stride,
+                                          uint64_t len, int src_kind, hipStream_t stream, bool evict);
+  void reserve_put(uint32_t n);
 
   int device_;
   bool use_device_;
@@ -117,6 +130,22 @@ class DevicePageCache {
   // outstanding slot readers (gathers, segment reads), one event each, any stream
   std::vector<hipEvent_t> pending_ev_;
   std::vector<hipEvent_t> ev_pool_;
+  // device put path state (page_cache_put.hip)
+  bool dev_owner_ = false;                       // the device table is ahead of the host mirror
+  bool host_changed_ = true;                     // host mirror changed since the last push
+  int32_t dev_free_ = 0;                         // free slots while dev_owner_
+  unsigned long long batch_ = 0;
+  uint64_t* slot_key_d_ = nullptr;
+  uint32_t* slot_tidx_d_ = nullptr;
+  uint32_t* free_stack_d_ = nullptr;
+  uint32_t* passed_d_ = nullptr;
+  unsigned long long* tag_d_ = nullptr;
+  PutCounters* ctr_d_ = nullptr;
+  PutCounters* ctr_h_ = nullptr;                 // pinned
+  uint32_t* put_tidx_d_ = nullptr;
+  int32_t* put_slot_d_ = nullptr;
+  uint64_t* put_ev_d_ = nullptr;
+  uint32_t put_cap_ = 0;
   SegRing ring_;                                 // descriptors of batched copies
   mutable std::mutex mu_;
 };

@@ -27,6 +27,9 @@ inline void bind_page_cache(pybind11::module_& m) {
       .def("put_many", &DevicePageCache::put_many, G(), py::arg("keys"), py::arg("src"),
            py::arg("src_stride"), py::arg("length"), py::arg("src_kind"), py::arg("stream"),
            py::arg("evict"))
+      .def("put_many_device", &DevicePageCache::put_many_device, G(), py::arg("keys"), py::arg("n"), py::arg("src"),
+           py::arg("src_stride"), py::arg("length"), py::arg("src_kind"), py::arg("stream"), py::arg("evict"))
+      .def_property_readonly("device_owned", &DevicePageCache::device_owned)
       .def("erase", &DevicePageCache::erase, G())
       .def("contains", &DevicePageCache::contains, G())
       .def("lookup", &DevicePageCache::lookup, G())

@@ -27,6 +27,8 @@ OPS = ["CreateFile", "GetBlockLocations", "GetFileStatus", "OpenFile", "CreateDi
 def parse(argv):
     ap = argparse.ArgumentParser(prog="StressMasterBench")
     ap.add_argument("--operation", required=True, choices=OPS)
+    ap.add_argument("--write-type", default="MUST_CACHE",
+                    help="write type of CreateFile / CreateDir (THROUGH: the master does UFS I/O)")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--clients", type=int, default=1)
     ap.add_argument("--target-throughput", type=int, default=0, help="ops/s cap; 0 = unthrottled")
@@ -106,9 +108,9 @@ def main(argv=None, fs=None, print_result=True) -> dict:
             return False
         k = i % max(1, a.fixed_count)
         if a.operation == "CreateFile":
-            c.write_file(target(i), payload, write_type="MUST_CACHE")
+            c.write_file(target(i), payload, write_type=a.write_type)
         elif a.operation == "CreateDir":
-            c.create_directory(target(i), write_type="MUST_CACHE")
+            c.create_directory(target(i), write_type=a.write_type)
         elif a.operation == "GetFileStatus":
             c.get_status(f"{fixed}/{k}")
         elif a.operation == "GetFileStatusNonexistent":

@@ -183,3 +183,89 @@ def test_device_put_many_matches_torch(gpu):
     pc.gather(kd.data_ptr(), n, out.data_ptr(), ps, so.data_ptr(), lo.data_ptr(), stream)
     torch.cuda.synchronize()
     assert bool((so >= 0).all()) and torch.equal(out, src)
+
+
+def _ref_check(pc, src_rows, expect: dict, ps, gpu):
+    """Every expected key gathers to its source row (byte-exact, device lookup) and reads back
+    through the host mirror (pulled from the device table)."""
+    import torch
+    keys = list(expect)
+    kd = torch.tensor(keys, dtype=torch.int64, device=gpu)
+    out = torch.empty((len(keys), ps), dtype=torch.uint8, device=gpu)
+    so = torch.empty(len(keys), dtype=torch.int32, device=gpu)
+    lo = torch.empty(len(keys), dtype=torch.int32, device=gpu)
+    stream = torch.cuda.current_stream().cuda_stream
+    pc.gather(kd.data_ptr(), len(keys), out.data_ptr(), ps, so.data_ptr(), lo.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert bool((so >= 0).all()) and bool((lo == ps).all())
+    rows = torch.tensor([expect[k] for k in keys], device=gpu)
+    assert torch.equal(out, src_rows[rows])
+    for k in keys[:5]:
+        assert pc.get_bytes(k, 0, 64) == src_rows[expect[k], :64].cpu().numpy().tobytes()
+
+
+@pytest.mark.gpu
+def test_device_put_many_device_keys_matches_reference(gpu):
+    """K9 device put path (page_cache_put.hip): device-resident keys are probed/claimed, assigned
+    (free stack, then CLOCK eviction) and filled on the GPU; checked byte-for-byte against a
+    Python model of the cache, including duplicates (last wins), all-or-nothing overflow with
+    evict=false, eviction of a full cache, and CLOCK's second chance for pages touched after
+    insertion."""
+    import torch
+    C = lib()
+    ps, nslots = 4096, 256
+    pc = C.PageCache(0, nslots * ps, ps, True)
+    src = torch.randint(0, 256, (1024, ps), dtype=torch.uint8, device=gpu)
+    stream = torch.cuda.current_stream().cuda_stream
+    model = {}
+
+    def put(keys, rows, evict):
+        kd = torch.tensor(keys, dtype=torch.int64, device=gpu)
+        rowsel = src[torch.tensor(rows, device=gpu)].contiguous()
+        ev = pc.put_many_device(kd.data_ptr(), len(keys), rowsel.data_ptr(), ps, ps, 1, stream, evict)
+        torch.cuda.synchronize()
+        for k, r in zip(keys, rows):
+            model[k] = r
+        for k in ev:
+            model.pop(k, None)
+        return ev
+
+    assert put([_key(1, i) for i in range(200)], list(range(200)), False) == []
+    assert pc.device_owned and pc.used == 200
+    _ref_check(pc, src, model, ps, gpu)
+    # duplicates: the last occurrence wins and takes one slot
+    assert put([_key(2, 0), _key(2, 1), _key(2, 0)], [300, 301, 302], False) == []
+    assert model[_key(2, 0)] == 302 and pc.used == 202
+    _ref_check(pc, src, model, ps, gpu)
+    # evict=false overflow: 100 fresh keys, 54 free slots -> nothing changes
+    kd = torch.tensor([_key(3, i) for i in range(100)], dtype=torch.int64, device=gpu)
+    with pytest.raises(Exception):
+        pc.put_many_device(kd.data_ptr(), 100, src.data_ptr(), ps, ps, 1, stream, False)
+    assert pc.used == 202 and not any(pc.contains(_key(3, i)) for i in range(100))
+    _ref_check(pc, src, model, ps, gpu)
+    # hot pages: touched (gathered) after insertion -> CLOCK second chance
+    hot = [_key(1, i) for i in range(0, 200, 10)]
+    hk = torch.tensor(hot, dtype=torch.int64, device=gpu)
+    o = torch.empty((len(hot), ps), dtype=torch.uint8, device=gpu)
+    so = torch.empty(len(hot), dtype=torch.int32, device=gpu)
+    pc.gather(hk.data_ptr(), len(hot), o.data_ptr(), ps, so.data_ptr(), so.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ev = put([_key(4, i) for i in range(100)], list(range(400, 500)), True)
+    assert len(ev) == 202 + 100 - nslots and pc.used == nslots
+    assert not set(ev) & set(hot)
+    assert not any(pc.contains(k) for k in ev)
+    _ref_check(pc, src, model, ps, gpu)
+    # a batch as large as the cache replaces everything
+    ev = put([_key(5, i) for i in range(nslots)], list(range(500, 500 + nslots)), True)
+    assert len(ev) == nslots and set(model) == {_key(5, i) for i in range(nslots)}
+    _ref_check(pc, src, model, ps, gpu)
+    # host-side operations after device puts see the device table (mirror pulled back)
+    assert pc.erase(_key(5, 3)) and not pc.contains(_key(5, 3))
+    model.pop(_key(5, 3))
+    assert pc.used == nslots - 1
+    pc.put(_key(6, 0), src[7].data_ptr(), ps, 1, stream, False)
+    model[_key(6, 0)] = 7
+    # ... and a device put after host changes sees them (mirror pushed)
+    ev = put([_key(7, i) for i in range(10)], list(range(900, 910)), True)
+    assert len(ev) == 10 and pc.used == nslots
+    _ref_check(pc, src, model, ps, gpu)

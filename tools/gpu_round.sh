@@ -71,6 +71,28 @@ for s in $STEPS; do
       run bench_large 400 python bench.py --steps 20 --warmup 5 --phases local,stagger,large
       run pmc_dram_large 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram_large" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2 --phases local,large
       ;;
+    k9put)
+      run pytest_pc 300 python -u -m pytest tests/test_page_cache_native.py -x -v --timeout 120 --timeout-method thread
+      run page_cache_put 400 python tools/page_cache_bench.py --page-sizes 4k,64k,2m --out "$OUT/page_cache_put.jsonl"
+      run rocprof_pc_put 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pc_put" -o pcput --output-format csv -- python3 tools/page_cache_bench.py --page-sizes 4k --iters 5
+      ;;
+    hostread)
+      run worker_bench_host 900 python tools/worker_bench_host.py --threads 16,64,256 --duration 8s --warmup 2s --out "$OUT/worker_bench_host.jsonl"
+      ;;
+    mastergrpc)
+      run master_bench_native 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --out "$OUT/master_bench_native.json"
+      run master_bench_grpc 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc.json"
+      ;;
+    masterufs)
+      # CPU-only: CreateDir THROUGH against a root UFS whose every call sleeps 5 ms
+      for t in 1 8 32; do
+        p=$(( t < 4 ? 1 : 4 )); th=$(( t / p ))
+        run master_ufs_sleep_t$t 300 python tools/master_bench_mp.py --ops CreateDir --procs $p --threads $th --duration 5s --write-type THROUGH --ufs-sleep-ms 5 --out "$OUT/master_ufs_sleep_t$t.json"
+      done
+      ;;
+    largetune)
+      run ring_tune_large 500 python tools/ring_tune.py --file-size 16g --stagger --depths 256 --variants 0,1,2,3 --caps 4096,8192,16384 --rounds 3 --steps 32 --out "$OUT/ring_tune_large.json"
+      ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
     evict)
       run pytest_evict 300 python -u -m pytest tests/test_evict_alloc_gpu.py tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread

@@ -30,12 +30,13 @@ CLIENT = r"""
 import json, sys
 sys.path.insert(0, {root!r})
 from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.conf import Configuration
 from alluxio_amd.stress import master_bench
 import os
 if os.environ.get("ALLUXIO_PYSAMPLE_CLIENT"):
     from alluxio_amd.utils.sampler import StackSampler
     _smp = StackSampler().start()
-fs = FileSystem(master_address={addr!r})
+fs = FileSystem(conf=Configuration({cprops!r}), master_address={addr!r})
 r = master_bench.main({args!r}, fs=fs, print_result=False)
 r["native"] = str(fs.ctx.pool.get({addr!r}, fs.ctx.user)._native)
 print("RESULT " + json.dumps(r))
@@ -52,14 +53,22 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def run(ops, procs, threads, duration, warmup, journal_dir=None, props=()) -> list[dict]:
+def run(ops, procs, threads, duration, warmup, journal_dir=None, props=(), client_props=None, op_args=(),
+        ufs_sleep_ms: float = 0.0) -> list[dict]:
     work = tempfile.mkdtemp(prefix="mbench_")
     port, web = _free_port(), _free_port()
     conf_dir = os.path.join(work, "conf")
     os.makedirs(conf_dir)
     with open(os.path.join(conf_dir, "alluxio-site.properties"), "w") as f:
         f.write(f"alluxio.master.journal.folder={journal_dir or os.path.join(work, 'journal')}\n")
-        f.write(f"alluxio.master.mount.table.root.ufs={os.path.join(work, 'ufs')}\n")
+        root = os.path.join(work, "ufs")
+        os.makedirs(root, exist_ok=True)
+        if ufs_sleep_ms:
+            # every UFS call of the master sleeps (SleepingUnderFileSystem via the sleepfs:// scheme)
+            f.write(f"alluxio.master.mount.table.root.ufs=sleepfs://{root}\n")
+            f.write(f"alluxio.underfs.sleep.ms={ufs_sleep_ms}\n")
+        else:
+            f.write(f"alluxio.master.mount.table.root.ufs={root}\n")
         f.write(f"alluxio.master.web.port={web}\n")
         f.write("alluxio.master.journal.type=UFS\n")
         for kv in props:
@@ -80,13 +89,15 @@ def run(ops, procs, threads, duration, warmup, journal_dir=None, props=()) -> li
         out = []
         created = {}     # per client process: files its CreateFile run made (DeleteFile/RenameFile input)
         for op in ops:
-            args = ["--operation", op, "--threads", str(threads), "--duration", duration, "--warmup", warmup]
+            args = ["--operation", op, "--threads", str(threads), "--duration", duration, "--warmup", warmup,
+                    *op_args]
             ps = []
             for i in range(procs):
                 a = args + ["--base", f"/stress-master-{i}"]
                 if op in ("DeleteFile", "RenameFile") and i in created:
                     a += ["--stop-count", str(created[i])]
-                ps.append(subprocess.Popen([sys.executable, "-c", CLIENT.format(root=ROOT, addr=addr, args=a)],
+                ps.append(subprocess.Popen([sys.executable, "-c", CLIENT.format(root=ROOT, addr=addr, args=a,
+                                                                                cprops=dict(client_props or {}))],
                                            env=env, cwd=work, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
                                            text=True))
             res = []
@@ -122,12 +133,22 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", default="1s")
     ap.add_argument("--out", default=None)
     ap.add_argument("--master-prop", action="append", default=[], help="k=v master property (repeatable)")
+    ap.add_argument("--client-prop", action="append", default=[], help="k=v client property (repeatable)")
+    ap.add_argument("--write-type", default="MUST_CACHE", help="CreateFile/CreateDir write type")
+    ap.add_argument("--ufs-sleep-ms", type=float, default=0.0, help="root UFS = sleepfs:// with this latency")
     a = ap.parse_args(argv)
-    rows = run(a.ops.split(","), a.procs, a.threads, a.duration, a.warmup, props=a.master_prop)
+    cprops = dict(kv.split("=", 1) for kv in a.client_prop)
+    rows = run(a.ops.split(","), a.procs, a.threads, a.duration, a.warmup, props=a.master_prop,
+               client_props=cprops, op_args=["--write-type", a.write_type], ufs_sleep_ms=a.ufs_sleep_ms)
+    native = cprops.get("alluxio.user.network.native.rpc.enabled", "true").lower() != "false"
+    transport = ("native framed RPC (alluxio_amd/rpc/native.py, C++ I/O threads + reply cache)" if native
+                 else "gRPC (grpcio, the transport a Java client uses)")
     if a.out:
         with open(a.out, "w") as f:
-            json.dump({"setup": f"1 master process + {a.procs} client processes x {a.threads} threads, gRPC, "
-                                f"UFS journal on local disk, {os.cpu_count()} CPUs", "results": rows}, f, indent=1)
+            json.dump({"setup": f"1 master process + {a.procs} client processes x {a.threads} threads, "
+                                f"UFS journal on local disk, {os.cpu_count()} CPUs visible",
+                       "transport": transport, "write_type": a.write_type, "ufs_sleep_ms": a.ufs_sleep_ms,
+                       "results": rows}, f, indent=1)
     return 0
 
 

@@ -83,6 +83,26 @@ def main(argv=None):
         t_fill = time.perf_counter()
         pc.put_many([(1 << 24) | i for i in range(slots)], src.data_ptr(), 0, ps, 1, stream, False)
         fill_GBps = slots * ps / (time.perf_counter() - t_fill) / 1e9
+        # device put path with device-resident keys (page_cache_put.hip): overwrite every page,
+        # then replace the whole cache with new keys (CLOCK eviction of every slot)
+        src_rows = torch.empty((slots, ps), dtype=torch.uint8, device=dev)    # distinct source pages
+        dk = torch.arange(slots, device=dev, dtype=torch.int64) | (1 << 24)
+        stride = ps
+        torch.cuda.synchronize()
+        t_dev = time.perf_counter()
+        pc.put_many_device(dk.data_ptr(), slots, src_rows.data_ptr(), stride, ps, 1, stream, False)
+        overwrite_GBps = slots * ps / (time.perf_counter() - t_dev) / 1e9
+        dk2 = dk | (1 << 40)
+        torch.cuda.synchronize()
+        t_dev = time.perf_counter()
+        ev = pc.put_many_device(dk2.data_ptr(), slots, src_rows.data_ptr(), stride, ps, 1, stream, True)
+        evict_GBps = slots * ps / (time.perf_counter() - t_dev) / 1e9
+        assert len(ev) == slots, len(ev)
+        torch.cuda.synchronize()
+        t_dev = time.perf_counter()
+        pc.put_many_device(dk.data_ptr(), slots, src_rows.data_ptr(), stride, ps, 1, stream, True)
+        evict2_GBps = slots * ps / (time.perf_counter() - t_dev) / 1e9
+        del src_rows, dk2
         C.fill_pattern(pc.arena, slots * ps, 1234, 0, stream)      # distinct bytes in every page
         arena = torch.as_tensor(_DevArray(pc.arena, slots * ps), device=dev).view(slots, ps)
         n = max(1, min(parse_space_size(a.batch_bytes) // ps, 1 << 20))
@@ -118,6 +138,9 @@ def main(argv=None):
              "torch_index_select_GBps": round(nbytes / ms_ix / 1e6, 1),
              "contiguous_copy_GBps": round(nbytes / ms_cp / 1e6, 1) if ms_cp else None,
              "fill_put_many_GBps": round(fill_GBps, 1),
+             "put_device_overwrite_GBps": round(overwrite_GBps, 1),
+             "put_device_evict_all_GBps": round(evict_GBps, 1),
+             "put_device_evict_all_2_GBps": round(evict2_GBps, 1),
              "verified": True}
         print(json.dumps(r), flush=True)
         if a.out:

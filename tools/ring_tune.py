@@ -25,20 +25,27 @@ def main():
     ap.add_argument("--depths", default="64,256")
     ap.add_argument("--variants", default="0,1,2,3")
     ap.add_argument("--caps", default="2048,4096,8192")
+    ap.add_argument("--file-size", default="128m")
+    ap.add_argument("--stagger", action="store_true", help="stream s starts at s/256 of the file")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
+    from alluxio_amd.utils.format import parse_space_size
+    fsize = parse_space_size(a.file_size)
     C = lib()
-    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "hbm:0", "alluxio.worker.tieredstore.level0.dirs.quota": "1GB",
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "hbm:0",
+            "alluxio.worker.tieredstore.level0.dirs.quota": str(max(1 << 30, fsize + (256 << 20))),
             "alluxio.worker.hbm.page.size": "2MB", "alluxio.user.block.size.bytes.default": "64MB"}
     res = []
     with LocalAlluxioCluster(num_workers=1, conf=conf, grpc=False) as c:
         fs = c.client(metadata_cache=True)
-        data = np.random.default_rng(0).integers(0, 256, 128 << 20, dtype=np.uint8)
+        data = torch.randint(0, 256, (fsize,), dtype=torch.uint8, device="cuda")
         fs.write_file("/tune", data, write_type="MUST_CACHE")
+        del data
+        starts = [((s_ * fsize) // 256) // a.buf * a.buf for s_ in range(256)] if a.stagger else None
         readers = {}
         for d in (int(x) for x in a.depths.split(",")):
             ring = torch.empty((256, d, a.buf), dtype=torch.uint8, device="cuda")
-            readers[d] = (RingStreamReader(fs, "/tune", ring), ring)
+            readers[d] = (RingStreamReader(fs, "/tune", ring, start_offsets=starts), ring)
         combos = [(d, int(v), int(cap)) for d in readers for v in a.variants.split(",") for cap in a.caps.split(",")]
         t = {k: [] for k in combos}
         for _ in range(a.rounds):
@@ -55,7 +62,7 @@ def main():
                 torch.cuda.synchronize()
                 t[k].append((r.rs.total_bytes - b0) / (time.perf_counter() - t0) / 1e9)
         for k in combos:
-            row = {"depth": k[0], "variant": k[1], "grid_cap": k[2], "GBps_median": round(statistics.median(t[k]), 1),
+            row = {"file_size": fsize, "stagger": a.stagger, "depth": k[0], "variant": k[1], "grid_cap": k[2], "GBps_median": round(statistics.median(t[k]), 1),
                    "GBps_max": round(max(t[k]), 1)}
             res.append(row)
             print(json.dumps(row), flush=True)
