@@ -16,6 +16,7 @@
 #include "kernels.h"
 #include "seg_ring.h"
 #include "frame_rpc.h"
+#include "meta_codec.h"
 
 namespace py = pybind11;
 using namespace amdx;
@@ -207,6 +208,65 @@ py::tuple page_alloc_device(const std::vector<uint64_t>& bits, uint32_t want) {
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native worker data plane: HBM page store + CDNA4 kernels";
   bind_page_cache(m);
+  m.def("encode_inode_file_batch",
+        [](const std::string& tmpl, const std::vector<int64_t>& ids, const std::vector<int64_t>& parents,
+           const std::vector<std::string>& names, const std::vector<int64_t>& lengths, int64_t block_size,
+           const std::vector<std::string>& fps, const std::vector<int64_t>& mtimes, int64_t ctime) {
+          std::string out;
+          {
+            py::gil_scoped_release rel;
+            out = encode_inode_file_batch(tmpl, ids, parents, names, lengths, block_size, fps, mtimes, ctime);
+          }
+          return py::bytes(out);
+        });
+  m.def("decode_file_infos", [](const std::vector<std::string>& chunks) {
+    FileInfoColumns c;
+    {
+      py::gil_scoped_release rel;
+      decode_file_infos(chunks, c);
+    }
+    auto arr = [](const auto& v) {
+      using T = typename std::decay_t<decltype(v)>::value_type;
+      py::array_t<T> a(v.size());
+      if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+      return a;
+    };
+    py::dict d;
+    d["ids"] = arr(c.ids);
+    d["lengths"] = arr(c.lengths);
+    d["block_sizes"] = arr(c.block_sizes);
+    d["first_blocks"] = arr(c.first_blocks);
+    d["nblocks"] = arr(c.nblocks);
+    d["folder"] = arr(c.folder);
+    d["chunk"] = arr(c.chunk);
+    d["offset"] = arr(c.offset);
+    d["size"] = arr(c.size);
+    d["paths"] = py::cast(c.paths);
+    return d;
+  });
+  m.def("encode_block_info_batch", [](const std::vector<int64_t>& ids, const std::vector<int64_t>& lengths) {
+    std::string out;
+    {
+      py::gil_scoped_release rel;
+      out = encode_block_info_batch(ids, lengths);
+    }
+    return py::bytes(out);
+  });
+  m.def("encode_file_infos",
+        [](const std::string& tmpl, const std::vector<int64_t>& ids, const std::vector<std::string>& names,
+           const std::string& parent_path, const std::string& parent_ufs, const std::vector<int64_t>& lengths,
+           int64_t block_size, const std::vector<int64_t>& ctimes, const std::vector<int64_t>& mtimes,
+           const std::vector<int64_t>& atimes, const std::vector<std::string>& fps,
+           const std::vector<std::string>& block_infos, const std::vector<int32_t>& in_alluxio,
+           const std::vector<int32_t>& in_memory, uint32_t out_field, bool ufs_locations) {
+          std::string out;
+          {
+            py::gil_scoped_release rel;
+            out = encode_file_infos(tmpl, ids, names, parent_path, parent_ufs, lengths, block_size, ctimes, mtimes,
+                                    atimes, fps, block_infos, in_alluxio, in_memory, out_field, ufs_locations);
+          }
+          return py::bytes(out);
+        });
 
   static py::exception<StoreError> store_error(m, "StoreError");
   py::register_exception_translator([](std::exception_ptr p) {

@@ -93,6 +93,28 @@ def iter_delimited(f, cls=None, tolerate_torn_tail: bool = True):
         yield m
 
 
+class RawEntryBatch:
+    """A batched JournalEntry (``repeated journal_entries = 39``, journal.proto:20-61) whose body
+    was serialized natively (csrc/meta_codec.cpp); the writer adds the sequence number (field 1:
+    protobuf fields may come in any order).  Duck-types the bits of a JournalEntry the journal
+    writers use (``sequence_number``, ``SerializeToString``)."""
+
+    __slots__ = ("body", "count", "sequence_number")
+
+    def __init__(self, body: bytes, count: int):
+        self.body = body
+        self.count = count
+        self.sequence_number = 0
+
+    def SerializeToString(self) -> bytes:  # noqa: N802 - protobuf API name
+        return self.body + b"\x08" + encode_varint(self.sequence_number & ((1 << 64) - 1))
+
+    def to_proto(self):
+        e = pb.journal.JournalEntry.FromString(self.body)
+        e.sequence_number = self.sequence_number
+        return e
+
+
 def encode_file_name(start: int, end: int) -> str:
     return f"0x{start:x}-0x{end:x}"
 

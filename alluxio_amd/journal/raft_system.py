@@ -186,8 +186,11 @@ class _RaftBatchWriter:
                 raise JournalClosedException("journal is closed")
             if self._error is not None:
                 raise UnavailableException(f"journal write failed: {self._error}")
-            e = pb.journal.JournalEntry()
-            e.CopyFrom(entry)
+            if isinstance(entry, fmt.RawEntryBatch):
+                e = entry.to_proto()
+            else:
+                e = pb.journal.JournalEntry()
+                e.CopyFrom(entry)
             e.sequence_number = self.next_sn
             self.next_sn += 1
             self._queue.append(pb.raft.RaftNamedEntry(master=master, entry=e))

@@ -98,6 +98,7 @@ class BlockMaster(Journaled):
         self.lost_worker_listeners = []
         self.worker_registered_listeners = []
         self.safe_mode = None
+        self._bi_cache: tuple = (None, {})
 
     def _bump_epoch(self) -> None:
         self.location_epoch += 1
@@ -161,6 +162,68 @@ class BlockMaster(Journaled):
         if ctx is not None:
             ctx.close()
         return cid
+
+    def get_new_container_ids(self, n: int) -> list[int]:
+        """``n`` consecutive container ids with at most one journal entry (a bulk metadata load)."""
+        if n <= 0:
+            return []
+        ctx = None
+        with self._lock:
+            cid = self._next_container
+            self._next_container += n
+            if self._next_container > self._container_limit:
+                limit = cid + n + CONTAINER_BATCH
+                e = pb.journal.JournalEntry(block_container_id_generator=pb.journal.BlockContainerIdGeneratorEntry(
+                    next_container_id=limit))
+                self._container_limit = limit
+                ctx = self._ctx()
+                ctx.append(e)
+        if ctx is not None:
+            ctx.close()
+        return list(range(cid, cid + n))
+
+    def block_info_bytes(self, block_id: int) -> tuple[bytes, int, bool]:
+        """(serialized BlockInfo, length, has a MEM location) of a block that has locations, or
+        (b"", length, False) for one stored only in the UFS / unknown (the FileInfo encoder
+        synthesises those).  Serialized infos are cached per location epoch."""
+        m = self._blocks.get(block_id)
+        if m is None or not m.locations:
+            return b"", (m.length if m is not None else 0), False
+        cache = self._bi_cache
+        if cache[0] != self.location_epoch:
+            cache = self._bi_cache = (self.location_epoch, {})
+        hit = cache[1].get(block_id)
+        if hit is None:
+            bi = self.block_info_or_none(block_id)
+            if bi is None or not bi.locations:
+                return b"", m.length, False
+            hit = (bi.SerializeToString(), bi.length, any(l.tierAlias == "MEM" for l in bi.locations))
+            if cache[0] == self.location_epoch:
+                cache[1][block_id] = hit
+        return hit
+
+    def commit_blocks_in_ufs_bulk(self, block_ids, lengths, fresh: bool = False) -> int:
+        """Bulk form of :meth:`commit_blocks_in_ufs`: in-memory records for the new blocks and ONE
+        natively encoded batched journal entry (csrc/meta_codec.cpp) instead of an entry object
+        per block; returns how many were new.  ``fresh``: the ids belong to containers allocated
+        for this call (they cannot exist yet), skip the existence check."""
+        from ..journal.format import RawEntryBatch
+        from ..ops.native import lib
+        with self._lock:
+            blocks = self._blocks
+            if not fresh and any(b in blocks for b in block_ids):
+                pairs = [(b, ln) for b, ln in zip(block_ids, lengths) if b not in blocks]
+                new_ids, new_lens = [p[0] for p in pairs], [p[1] for p in pairs]
+            else:
+                new_ids, new_lens = list(block_ids), list(lengths)
+            blocks.update(zip(new_ids, map(BlockMeta, new_lens)))
+            if not new_ids:
+                return 0
+            self._bump_epoch()
+            ctx = self._ctx()
+            ctx.append(RawEntryBatch(lib().encode_block_info_batch(new_ids, new_lens), len(new_ids)))
+        ctx.close()
+        return len(new_ids)
 
     # ---- workers ------------------------------------------------------------------------------
     def get_worker_id(self, address) -> int:

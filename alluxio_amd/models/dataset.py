@@ -24,12 +24,53 @@ from ..utils.tracing import traced
 
 
 class _FileLayout:
+    """Path, length and block layout of one file; the BlockInfo list is materialised on first use
+    (a 1 M-file listing must not pay for 1 M sub-message wrappers it may never touch)."""
+
+    __slots__ = ("info", "path", "length", "block_size", "_blocks")
+
     def __init__(self, status):
         i = status.info
+        self.info = i
         self.path = i.path
         self.length = i.length
         self.block_size = i.blockSizeBytes
-        self.blocks = [fbi.blockInfo for fbi in i.fileBlockInfos]
+        self._blocks = None
+
+    @property
+    def blocks(self):
+        if self._blocks is None:
+            self._blocks = [fbi.blockInfo for fbi in self.info.fileBlockInfos]
+        return self._blocks
+
+    @property
+    def block_ids(self):
+        return self.info.blockIds
+
+
+class _LazyLayouts:
+    """``files`` of a columnar listing: the _FileLayout of entry i is parsed on first access."""
+
+    def __init__(self, cols, keep):
+        self._cols, self._keep = cols, keep
+        self._cache: dict = {}
+
+    def __len__(self) -> int:
+        return len(self._keep)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        lay = self._cache.get(i)
+        if lay is None:
+            lay = self._cache[i] = _FileLayout(self._cols.status(int(self._keep[i])))
+        return lay
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]
 
 
 class FixedRecordDataset:
@@ -84,17 +125,33 @@ class FileListDataset(FixedRecordDataset):
         self.dtype = getattr(torch, str(dtype)) if isinstance(dtype, str) else dtype
         self.shape = tuple(shape) if shape else None
         self.device = device
-        sts = sorted((s for s in fs.list_status(directory) if not s.is_folder), key=lambda s: s.path)
-        self.paths = [s.path for s in sts]
-        self.lengths = np.array([s.length for s in sts], dtype=np.uint64)
-        self.record_bytes = int(record_bytes or (self.lengths.max() if len(sts) else 0))
-        self.files = [_FileLayout(s) for s in sts]
-        self.counts = [1] * len(sts)
-        self.starts = np.arange(len(sts) + 1)
+        cols = fs.list_status_columns(directory) if hasattr(fs, "list_status_columns") else None
+        if cols is None:
+            sts = sorted((s for s in fs.list_status(directory) if not s.is_folder), key=lambda s: s.path)
+            self.paths = [s.path for s in sts]
+            self.lengths = np.array([s.length for s in sts], dtype=np.uint64)
+            self.files = [_FileLayout(s) for s in sts]
+            nblocks = np.array([len(f.block_ids) for f in self.files], dtype=np.int64)
+            bsizes = np.array([f.block_size for f in self.files], dtype=np.int64)
+            self.block_ids = np.array([f.block_ids[0] if len(f.block_ids) else -1 for f in self.files], dtype=np.int64)
+        else:
+            # columnar listing: no per-file Python objects until a file's layout is needed
+            keep = np.nonzero(cols.folder == 0)[0]
+            paths = [cols.paths[i] for i in keep]
+            if any(paths[k] > paths[k + 1] for k in range(len(paths) - 1)):
+                order = sorted(range(len(paths)), key=paths.__getitem__)
+                keep, paths = keep[order], [paths[k] for k in order]
+            self.paths = paths
+            self.lengths = cols.lengths[keep].astype(np.uint64)
+            self.files = _LazyLayouts(cols, keep)
+            nblocks, bsizes = cols.nblocks[keep], cols.block_sizes[keep]
+            self.block_ids = cols.first_blocks[keep].astype(np.int64)
+        n = len(self.paths)
+        self.record_bytes = int(record_bytes or (self.lengths.max() if n else 0))
+        self.counts = [1] * n
+        self.starts = np.arange(n + 1)
         # single-block records: the gather plan is a vector op over these arrays
-        self.single_block = all(len(f.blocks) == 1 for f in self.files) and \
-            all(f.block_size >= self.record_bytes for f in self.files)
-        self.block_ids = np.array([f.blocks[0].blockId if f.blocks else -1 for f in self.files], dtype=np.int64)
+        self.single_block = bool(np.all(nblocks == 1)) and bool(np.all(bsizes >= self.record_bytes))
         self.read_lengths = np.minimum(self.lengths, np.uint64(self.record_bytes))
 
     def locate(self, idx: int) -> tuple[int, int]:

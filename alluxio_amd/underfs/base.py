@@ -52,7 +52,14 @@ class UfsFileStatus(UfsStatus):
 
     def __init__(self, name, content_length=0, content_hash="", last_modified_ms=None, owner="",
                  group="", mode=0o644, block_size=64 << 20, xattr=None):
-        super().__init__(name, False, owner, group, mode, last_modified_ms, xattr)
+        # plain attribute stores (no dataclass super().__init__): listings build millions of these
+        self.name = name
+        self.is_directory = False
+        self.owner = owner
+        self.group = group
+        self.mode = mode
+        self.last_modified_ms = last_modified_ms
+        self.xattr = xattr
         self.content_length = content_length
         self.content_hash = content_hash
         self.block_size = block_size

@@ -60,6 +60,7 @@ def _load_builtin() -> None:
     from . import s3, web, hdfs, swift, wasb, webhdfs, ozone  # noqa: F401  (self-registering)
     from .testing import SleepingUfsFactory
     register_factory(SleepingUfsFactory())
+    from . import synthetic  # noqa: F401  (self-registering)
     try:
         from importlib.metadata import entry_points
         for ep in entry_points().select(group="alluxio_amd.underfs"):

@@ -507,12 +507,16 @@ class BlockWorker:
             opts = resolve_ufs_block_opts(self, bid, opts)
             is_local = local_mount.get(opts.mountId)
             if is_local is None or not opts.mountId:
-                is_local = isinstance(self._ufs_for(opts), LocalUnderFileSystem)
+                u = self._ufs_for(opts)
+                # local files, or a UFS that names a local file to pread per path (synthetic)
+                is_local = (strip_scheme if isinstance(u, LocalUnderFileSystem)
+                            else getattr(u, "native_path", None)) or False
                 if opts.mountId:
                     local_mount[opts.mountId] = is_local
-            if is_local and opts.block_size > 0:
+            npath = is_local(opts.ufs_path) if is_local else None
+            if npath and opts.block_size > 0:
                 native_ids.append(bid)
-                paths.append(strip_scheme(opts.ufs_path))
+                paths.append(npath)
                 offs.append(opts.offset_in_file)
                 lens.append(opts.block_size)
             else:

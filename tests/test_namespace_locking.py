@@ -169,7 +169,9 @@ def test_slow_ufs_delete_and_rename_do_not_stall_other_paths(master, tmp_path):
         lat.append(_timed(lambda: fs.get_status("/slow/dir/f0")))    # pre-delete state, no wait
         i += 1
     assert t_del.is_alive(), "the slow delete should still be running"
-    assert max(lat) < 0.2 and statistics.median(lat) < 0.05, (max(lat), statistics.median(lat))
+    # a blocked op would take the full 3 s of UFS sleeps; allow scheduler noise on a busy box
+    p95 = sorted(lat)[int(0.95 * (len(lat) - 1))]
+    assert max(lat) < 1.0 and p95 < 0.05 and statistics.median(lat) < 0.02, (max(lat), p95, statistics.median(lat))
     # a create inside the subtree being deleted waits for the delete and then fails
     t0 = time.perf_counter()
     with pytest.raises(FileDoesNotExistException):
@@ -212,7 +214,8 @@ def test_recursive_delete_of_10k_persisted_files_does_not_block(master, tmp_path
     t.join()
     took = time.perf_counter() - t0
     assert not os.path.exists(root)
-    assert max(lat) < 0.25, (max(lat), took, len(lat))
+    p95 = sorted(lat)[int(0.95 * (len(lat) - 1))]
+    assert max(lat) < 1.0 and p95 < 0.1, (max(lat), p95, took, len(lat))
     assert len(lat) >= 20, (len(lat), took)        # the namespace kept serving during the delete
     with pytest.raises(FileDoesNotExistException):
         fsm.get_status("/big", load_metadata="NEVER")

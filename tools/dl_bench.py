@@ -27,6 +27,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+class _Done(Exception):
+    pass
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--files", type=int, default=100_000)
@@ -35,6 +39,10 @@ def main():
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--threads", type=int, default=16, help="native UFS reader threads")
     ap.add_argument("--work-dir", default=None)
+    ap.add_argument("--ufs", choices=["local", "synthetic"], default="local",
+                    help="synthetic: the files come from the synth:// UFS (content = function of the path, "
+                         "backed by 4096 real files), so 1 M x 128 KB needs no 131 GB disk")
+    ap.add_argument("--skip-cache", action="store_true", help="metadata phase only")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
@@ -52,13 +60,15 @@ def main():
         ufs = os.path.join(work, "ufs")
         d = os.path.join(ufs, "imagenet")
         os.makedirs(d)
-        base = np.random.default_rng(1).integers(0, 256, a.file_size + 4096, dtype=np.uint8).tobytes()
-        t = time.perf_counter()
-        for i in range(a.files):
-            o = (i * 977) % 4096                     # distinct content per file
-            with open(os.path.join(d, f"{i:07d}.JPEG"), "wb") as f:
-                f.write(base[o:o + a.file_size])
-        res["ufs_write_s"] = round(time.perf_counter() - t, 2)
+        res["ufs"] = a.ufs
+        if a.ufs == "local":
+            base = np.random.default_rng(1).integers(0, 256, a.file_size + 4096, dtype=np.uint8).tobytes()
+            t = time.perf_counter()
+            for i in range(a.files):
+                o = (i * 977) % 4096                     # distinct content per file
+                with open(os.path.join(d, f"{i:07d}.JPEG"), "wb") as f:
+                    f.write(base[o:o + a.file_size])
+            res["ufs_write_s"] = round(time.perf_counter() - t, 2)
         total = a.files * a.file_size
         quota = int(total * 1.15) + (256 << 20)
         conf = {"alluxio.master.mount.table.root.ufs": ufs,
@@ -71,18 +81,31 @@ def main():
         with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=os.path.join(work, "c")) as c:
             fs = c.client()
             w = c.workers[0].worker
+            root = "/imagenet"
+            if a.ufs == "synthetic":
+                os.rmdir(d)
+                fs.mount("/syn", "synth:///dataset", properties={
+                    "alluxio.underfs.synthetic.files": str(a.files), "alluxio.underfs.synthetic.size": str(a.file_size),
+                    "alluxio.underfs.synthetic.dirs": "imagenet",
+                    "alluxio.underfs.synthetic.backing.dir": os.path.join(work, "backing")})
+                root = "/syn/imagenet"
             # metadata: one listing loads every file (LOAD_ONCE)
             t = time.perf_counter()
-            ds = FileListDataset(fs, "/imagenet", record_bytes=a.file_size)
+            ds = FileListDataset(fs, root, record_bytes=a.file_size)
             el = time.perf_counter() - t
             res["metadata_files_per_s"] = round(a.files / el, 1)
             res["metadata_s"] = round(el, 2)
+            if a.skip_cache:
+                fs.close()
+                raise _Done()
             # warm every block into HBM (the load job's bulk path: native preads into pinned
             # staging, batched H2D, one Python call per chunk of files), then refresh the listing
             t = time.perf_counter()
+            st0 = fs.get_status(ds.paths[0])
+            ufs_dir = st0.info.ufsPath.rsplit("/", 1)[0]
             items = [(f.blocks[0].blockId, pb.dataserver.OpenUfsBlockOptions(
-                ufs_path=os.path.join(ufs, f.path.lstrip("/")), offset_in_file=0, block_size=f.blocks[0].length,
-                mountId=1)) for f in ds.files]
+                ufs_path=ufs_dir + "/" + p.rsplit("/", 1)[1], offset_in_file=0, block_size=f.blocks[0].length,
+                mountId=st0.info.mountId)) for f, p in zip(ds.files, ds.paths)]
             cached = 0
             for i in range(0, len(items), 4096):
                 cached += w.cache_blocks_from_ufs(items[i:i + 4096])
@@ -91,7 +114,7 @@ def main():
             res["cache_files_per_s"] = round(a.files / el, 1)
             res["cache_GBps"] = round(total / el / 1e9, 3)
             res["cache_breakdown_s"] = {k: round(v, 3) for k, v in w.bulk_stats.items()}
-            ds = FileListDataset(fs, "/imagenet", record_bytes=a.file_size)
+            ds = FileListDataset(fs, root, record_bytes=a.file_size)
             res["cached_fraction"] = round(float(np.mean([bool(f.blocks[0].locations) for f in ds.files])), 4)
             # training epochs: shuffled batches gathered on the device
             dev = torch.device("cuda", 0) if gpu else torch.device("cpu")
@@ -135,6 +158,8 @@ def main():
                 res["per_batch_total_ms"] = round(full_s * 1e3, 3)
                 res["bottleneck"] = "host planning/launch" if host_s > 0.8 * full_s else "device gather"
             fs.close()
+    except _Done:
+        pass
     finally:
         shutil.rmtree(work, ignore_errors=True)
     line = json.dumps(res)
