@@ -264,10 +264,14 @@ class FileSystem:
         For million-entry directories (BASELINE config 4) where per-entry wrapper objects
         dominate the client side of a listing."""
         from ..ops.native import lib
-        o = pb.file.ListStatusPOptions(recursive=recursive, loadMetadataType=LOAD[load_metadata])
-        chunks = [r.SerializeToString() for r in self._fs.ListStatus(pb.file.ListStatusPRequest(path=_path(path),
-                                                                                                options=o))]
+        chunks = self.list_status_chunks(path, recursive, load_metadata)
         return StatusColumns(chunks, lib().decode_file_infos(chunks))
+
+    def list_status_chunks(self, path, recursive=False, load_metadata="ONCE") -> list[bytes]:
+        """The serialized ListStatus replies of a listing (for native decoders)."""
+        o = pb.file.ListStatusPOptions(recursive=recursive, loadMetadataType=LOAD[load_metadata])
+        return [r.SerializeToString() for r in self._fs.ListStatus(pb.file.ListStatusPRequest(path=_path(path),
+                                                                                              options=o))]
 
     def iterate_status(self, path, recursive=False, **kw):
         yield from self.list_status(path, recursive=recursive, **kw)

@@ -17,6 +17,7 @@
 #include "seg_ring.h"
 #include "frame_rpc.h"
 #include "meta_codec.h"
+#include "fuse_server.h"
 
 namespace py = pybind11;
 using namespace amdx;
@@ -238,6 +239,10 @@ PYBIND11_MODULE(_C, m) {
     d["first_blocks"] = arr(c.first_blocks);
     d["nblocks"] = arr(c.nblocks);
     d["folder"] = arr(c.folder);
+    d["completed"] = arr(c.completed);
+    d["mtimes"] = arr(c.mtimes);
+    d["atimes"] = arr(c.atimes);
+    d["modes"] = arr(c.modes);
     d["chunk"] = arr(c.chunk);
     d["offset"] = arr(c.offset);
     d["size"] = arr(c.size);
@@ -578,6 +583,76 @@ PYBIND11_MODULE(_C, m) {
       .def("set_cache_capacity", &FrameRpcServer::set_cache_capacity)
       .def_property_readonly("cache_size", &FrameRpcServer::cache_size)
       .def_property_readonly("cache_hits", &FrameRpcServer::cache_hits);
+  py::class_<FuseServer>(m, "FuseServer")
+      .def(py::init([](int fd, int threads, py::object store, int64_t session, int keep_cache) {
+             BlockStore* bs = store.is_none() ? nullptr : store.cast<BlockStore*>();
+             return new FuseServer(fd, threads, bs, session, keep_cache);
+           }),
+           py::arg("fd"), py::arg("threads") = 4, py::arg("store") = py::none(), py::arg("session") = 0,
+           py::arg("keep_cache") = 2, py::keep_alive<1, 4>())
+      .def("start", &FuseServer::start, G())
+      .def("stop", &FuseServer::stop, G())
+      .def_property_readonly("alive", &FuseServer::alive)
+      .def("poll", [](FuseServer& s, int max_n, int timeout_ms) {
+             std::vector<FuseRequest> v;
+             {
+               py::gil_scoped_release rel;
+               v = s.poll(max_n, timeout_ms);
+             }
+             py::list out;
+             for (auto& r : v)
+               out.append(py::make_tuple(r.unique, r.opcode, r.nodeid, r.uid, r.gid, r.pid, py::bytes(r.body)));
+             return out;
+           })
+      .def("reply", [](FuseServer& s, uint64_t unique, int err, py::bytes payload) {
+             std::string p = payload;
+             py::gil_scoped_release rel;
+             s.reply(unique, err, p);
+           }, py::arg("unique"), py::arg("err"), py::arg("payload") = py::bytes())
+      .def("node_of", &FuseServer::node_of, G())
+      .def("path_of", [](FuseServer& s, uint64_t nodeid) -> py::object {
+             bool ok = false;
+             std::string p = s.path_of(nodeid, &ok);
+             if (!ok) return py::none();
+             return py::str(p);
+           })
+      .def("forget_path", &FuseServer::forget_path, G())
+      .def("moved", &FuseServer::moved, G())
+      .def("put_attr", [](FuseServer& s, const std::string& path, py::bytes attr, int64_t ttl_ms, uint32_t valid_s,
+                          int64_t file_id, bool complete, const std::vector<int64_t>& blocks,
+                          const std::vector<int64_t>& lens) {
+             std::string a = attr;
+             s.put_attr(path, a, ttl_ms, valid_s, file_id, complete, blocks, lens);
+           }, py::arg("path"), py::arg("attr"), py::arg("ttl_ms"), py::arg("valid_s"), py::arg("file_id") = 0,
+           py::arg("complete") = false, py::arg("blocks") = std::vector<int64_t>{},
+           py::arg("lens") = std::vector<int64_t>{})
+      .def("invalidate", &FuseServer::invalidate, G(), py::arg("path"), py::arg("subtree") = true)
+      .def("clear_attrs", &FuseServer::clear_attrs, G())
+      .def("keep_open", &FuseServer::keep_open, G())
+      .def("set_no_open", &FuseServer::set_no_open)
+      .def("cache_listing", [](FuseServer& s, const std::vector<std::string>& chunks, const std::string& strip,
+                               uint32_t uid, uint32_t gid, uint32_t file_ttl_s, uint32_t dir_ttl_s) {
+             py::gil_scoped_release rel;
+             return s.cache_listing(chunks, strip, uid, gid, file_ttl_s, dir_ttl_s);
+           }, py::arg("chunks"), py::arg("strip"), py::arg("uid"), py::arg("gid"), py::arg("file_ttl_s") = 60,
+           py::arg("dir_ttl_s") = 1)
+      .def("entry", [](FuseServer& s, const std::string& path) -> py::object {
+             std::string out;
+             bool ok;
+             {
+               py::gil_scoped_release rel;
+               ok = s.entry_reply(path, out);
+             }
+             if (!ok) return py::none();
+             return py::bytes(out);
+           })
+      .def("add_arena", &FuseServer::add_arena)
+      .def("set_passthrough", &FuseServer::set_passthrough)
+      .def_property_readonly("passthrough_opens", &FuseServer::passthrough_opens)
+      .def("stats", &FuseServer::stats)
+      .def_property_readonly("native_opens", &FuseServer::native_opens)
+      .def_property_readonly("native_reads", &FuseServer::native_reads)
+      .def_property_readonly("fallback_opens", &FuseServer::fallback_opens);
   py::class_<FrameRpcClient>(m, "FrameRpcClient")
       .def(py::init<const std::string&, int, const std::string&, int>(), py::arg("host"), py::arg("port"),
            py::arg("auth"), py::arg("timeout_ms") = 60000)

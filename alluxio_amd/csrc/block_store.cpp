@@ -1718,6 +1718,17 @@ std::vector<int64_t> BlockStore::block_pages(int64_t id, int* dir_out, uint64_t*
   return b->pages;
 }
 
+std::string BlockStore::committed_file(int64_t id) {
+  std::unique_lock<std::mutex> lk(mu_);
+  BlockMeta* b = find(id);
+  if (!b || b->temp || b->dir < 0) return std::string();
+  const StorageDir& d = *dirs_[b->dir];
+  if (d.spec.kind != DirKind::kFile) return std::string();
+  std::string p;
+  file_path(d, id, p);
+  return p;
+}
+
 std::vector<Event> BlockStore::drain_events() {
   std::unique_lock<std::mutex> lk(mu_);
   std::vector<Event> out;

@@ -240,6 +240,8 @@ class BlockStore {
   std::vector<int64_t> block_ids(int tier);
   std::vector<int64_t> block_pages(int64_t block_id, int* dir_out, uint64_t* page_size_out,
                                    uint64_t* base_out);
+  // Path of a committed block held in a file dir (tmpfs / SSD tier), "" otherwise.
+  std::string committed_file(int64_t block_id);
   std::vector<Event> drain_events();
   int num_dirs() const { return (int)dirs_.size(); }
   DirSpec dir_spec(int d) const { return dirs_.at(d)->spec; }

@@ -195,8 +195,10 @@ struct PutCounters {
   uint32_t nevicted;       // victims (their keys in `evicted`)
   uint32_t ntomb;          // tombstones this batch created
   uint32_t nfail;          // requests that got no slot
-  uint32_t pad[2];
+  uint32_t min_age;        // victims: slots not touched for >= this many epochs (threshold kernel)
+  uint32_t pad;
 };
+constexpr uint32_t kPutAgeBuckets = 4096;   // recency histogram: age = epoch - stamp, clamped
 struct PagePutArgs {
   PageTableEntry* table;
   uint64_t mask;
@@ -206,7 +208,7 @@ struct PagePutArgs {
   unsigned long long* tag;       // [table size] (batch << 32) | (request + 1) of the winner
   unsigned long long batch;
   uint32_t* stamps;              // [slots] recency (shared with the gather kernel)
-  uint32_t* passed;              // [slots] epoch the CLOCK hand last passed the slot
+  uint32_t* hist;                // [kPutAgeBuckets] slots per age (eviction threshold)
   uint32_t epoch;
   uint32_t nslots;
   uint64_t* slot_key;            // [slots] key held by each slot (kPageKeyEmpty = free)
@@ -226,6 +228,11 @@ hipError_t launch_page_put_probe(const PagePutArgs& a, hipStream_t stream);
 hipError_t launch_page_put_assign(const PagePutArgs& a, hipStream_t stream);
 hipError_t launch_page_put_fill(const PagePutArgs& a, hipStream_t stream);
 hipError_t launch_page_put_revert(const PagePutArgs& a, hipStream_t stream);
+// Age histogram of the evictable slots + the threshold age that frees enough of them.
+hipError_t launch_page_put_threshold(const PagePutArgs& a, hipStream_t stream);
+// Drop tombstones on the device: live entries of a.table are re-inserted into `fresh` (cleared
+// first) and slot_tidx is repointed; the caller swaps the two tables afterwards.
+hipError_t launch_page_table_rebuild(const PagePutArgs& a, PageTableEntry* fresh, hipStream_t stream);
 
 // Fill `bytes` at dst with 64-bit words w[i] = splitmix64(seed ^ ((i + word_offset) * K)):
 // synthetic bench/test data that is a pure function of the byte offset inside a block.

@@ -211,19 +211,24 @@ void decode_file_infos(const std::vector<std::string>& chunks, FileInfoColumns& 
       if (!get_varint(p, end, len) || (uint64_t)(end - p) < len) throw std::invalid_argument("decode_file_infos: bad length");
       const uint8_t* q = p;
       const uint8_t* fe = p + len;
-      int64_t id = 0, length = 0, bsz = 0, first = -1, nblk = 0;
-      bool folder = false;
+      int64_t id = 0, length = 0, bsz = 0, first = -1, nblk = 0, mtime = 0, atime = 0;
+      int32_t mode = 0;
+      bool folder = false, completed = false;
       std::string path;
       while (q < fe) {
         uint64_t k, v;
         if (!get_varint(q, fe, k)) throw std::invalid_argument("decode_file_infos: bad FileInfo");
         const uint32_t f = (uint32_t)(k >> 3), w = (uint32_t)(k & 7);
-        if (w == 0 && (f == 1 || f == 5 || f == 6 || f == 9 || f == 13)) {
+        if (w == 0 && (f == 1 || f == 5 || f == 6 || f == 8 || f == 9 || f == 13 || f == 14 || f == 18 || f == 31)) {
           if (!get_varint(q, fe, v)) throw std::invalid_argument("decode_file_infos: bad varint");
           if (f == 1) id = (int64_t)v;
           else if (f == 5) length = (int64_t)v;
           else if (f == 6) bsz = (int64_t)v;
+          else if (f == 8) completed = v != 0;
           else if (f == 9) folder = v != 0;
+          else if (f == 14) mtime = (int64_t)v;
+          else if (f == 18) mode = (int32_t)v;
+          else if (f == 31) atime = (int64_t)v;
           else {
             if (nblk == 0) first = (int64_t)v;
             ++nblk;
@@ -251,6 +256,10 @@ void decode_file_infos(const std::vector<std::string>& chunks, FileInfoColumns& 
       out.first_blocks.push_back(first);
       out.nblocks.push_back(nblk);
       out.folder.push_back(folder ? 1 : 0);
+      out.completed.push_back(completed ? 1 : 0);
+      out.mtimes.push_back(mtime);
+      out.atimes.push_back(atime);
+      out.modes.push_back(mode);
       out.paths.push_back(std::move(path));
       out.chunk.push_back((int32_t)c);
       out.offset.push_back((int64_t)(p - (const uint8_t*)chunks[c].data()));

@@ -32,8 +32,9 @@ std::string encode_file_infos(const std::string& tmpl, const std::vector<int64_t
 // Columns of the FileInfos in serialized ListStatusPResponse chunks (fileInfos = field 1): the
 // fields a dataset index needs plus each FileInfo's (chunk, offset, size) span for lazy parsing.
 struct FileInfoColumns {
-  std::vector<int64_t> ids, lengths, block_sizes, first_blocks, nblocks, offset, size;
-  std::vector<uint8_t> folder;
+  std::vector<int64_t> ids, lengths, block_sizes, first_blocks, nblocks, offset, size, mtimes, atimes;
+  std::vector<int32_t> modes;
+  std::vector<uint8_t> folder, completed;
   std::vector<int32_t> chunk;
   std::vector<std::string> paths;
 };

@@ -46,8 +46,8 @@ DevicePageCache::DevicePageCache(int device, uint64_t capacity_bytes, uint64_t p
     PC_HIP_OK(hipMalloc((void**)&slot_key_d_, nslots_ * sizeof(uint64_t)));
     PC_HIP_OK(hipMalloc((void**)&slot_tidx_d_, nslots_ * sizeof(uint32_t)));
     PC_HIP_OK(hipMalloc((void**)&free_stack_d_, nslots_ * sizeof(uint32_t)));
-    PC_HIP_OK(hipMalloc((void**)&passed_d_, nslots_ * sizeof(uint32_t)));
-    PC_HIP_OK(hipMemset(passed_d_, 0, nslots_ * sizeof(uint32_t)));
+    PC_HIP_OK(hipMalloc((void**)&hist_d_, kPutAgeBuckets * sizeof(uint32_t)));
+    PC_HIP_OK(hipMalloc((void**)&table2_d_, table_h_.size() * sizeof(PageTableEntry)));
     PC_HIP_OK(hipMalloc((void**)&tag_d_, table_h_.size() * sizeof(unsigned long long)));
     PC_HIP_OK(hipMemset(tag_d_, 0, table_h_.size() * sizeof(unsigned long long)));
     PC_HIP_OK(hipMalloc((void**)&ctr_d_, sizeof(PutCounters)));
@@ -82,7 +82,8 @@ DevicePageCache::~DevicePageCache() {
     hipFree(slot_key_d_);
     hipFree(slot_tidx_d_);
     hipFree(free_stack_d_);
-    hipFree(passed_d_);
+    hipFree(hist_d_);
+    hipFree(table2_d_);
     hipFree(tag_d_);
     hipFree(ctr_d_);
     hipHostFree(ctr_h_);
@@ -629,8 +630,6 @@ void DevicePageCache::ensure_device(hipStream_t stream) {
     PC_HIP_OK(hipMemcpyAsync(free_stack_d_, free_.data(), free_.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                              stream));
   PC_HIP_OK(hipMemcpyAsync(stamps_d_, stamp_h_.data(), nslots_ * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-  // CLOCK reference state: a host-side page counts as referenced only once it is touched again
-  PC_HIP_OK(hipMemcpyAsync(passed_d_, stamp_h_.data(), nslots_ * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
   ctr_h_->free_top = (int32_t)free_.size();
   PC_HIP_OK(hipMemcpyAsync(&ctr_d_->free_top, &ctr_h_->free_top, sizeof(int32_t), hipMemcpyHostToDevice, stream));
   PC_HIP_OK(hipStreamSynchronize(stream));       // pageable sources
@@ -686,7 +685,7 @@ std::vector<uint64_t> DevicePageCache::put_device_locked(const uint64_t* keys_d,
   a.tag = tag_d_;
   a.batch = ++batch_;
   a.stamps = stamps_d_;
-  a.passed = passed_d_;
+  a.hist = hist_d_;
   a.epoch = ++epoch_;
   a.nslots = nslots_;
   a.slot_key = slot_key_d_;
@@ -717,8 +716,15 @@ std::vector<uint64_t> DevicePageCache::put_device_locked(const uint64_t* keys_d,
       throw StoreError(kErrOutOfSpace, "page cache is full");
     }
   }
+  if (evict) PC_HIP_OK(launch_page_put_threshold(a, s));
   PC_HIP_OK(launch_page_put_assign(a, s));
   PC_HIP_OK(launch_page_put_fill(a, s));
+  // tombstones piling up: rebuild the table on the device, in the same stream order
+  const bool rebuild = tombstones_ + n > table_h_.size() / 4;
+  if (rebuild) {
+    PC_HIP_OK(launch_page_table_rebuild(a, table2_d_, s));
+    std::swap(table_d_, table2_d_);
+  }
   PC_HIP_OK(hipMemcpyAsync(c, ctr_d_, sizeof(PutCounters), hipMemcpyDeviceToHost, s));
   PC_HIP_OK(hipStreamSynchronize(s));
   std::vector<uint64_t> evicted(std::min<uint32_t>(c->nevicted, n));
@@ -730,14 +736,9 @@ std::vector<uint64_t> DevicePageCache::put_device_locked(const uint64_t* keys_d,
     PC_HIP_OK(hipStreamSynchronize(s));
   }
   dev_free_ = c->free_top;
-  tombstones_ += c->ntomb;
+  tombstones_ = rebuild ? 0 : tombstones_ + c->ntomb;
   device_stamps_dirty_ = true;
   const uint32_t failed = c->nfail;
-  if (tombstones_ > table_h_.size() / 4) {       // reclaim tombstones: rebuild on the host, push
-    ensure_host();
-    rebuild_table();
-    ensure_device(s);
-  }
   if (failed) throw StoreError(kErrOutOfSpace, "page cache could not place " + std::to_string(failed) + " pages");
   return evicted;
 }

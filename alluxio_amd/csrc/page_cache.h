@@ -138,7 +138,8 @@ class DevicePageCache {
   uint64_t* slot_key_d_ = nullptr;
   uint32_t* slot_tidx_d_ = nullptr;
   uint32_t* free_stack_d_ = nullptr;
-  uint32_t* passed_d_ = nullptr;
+  uint32_t* hist_d_ = nullptr;                   // [kPutAgeBuckets] eviction-threshold histogram
+  PageTableEntry* table2_d_ = nullptr;           // device rebuild target (swapped with table_d_)
   unsigned long long* tag_d_ = nullptr;
   PutCounters* ctr_d_ = nullptr;
   PutCounters* ctr_h_ = nullptr;                 // pinned

@@ -8,16 +8,19 @@
 //   1. probe  (thread per request): find the key or claim an EMPTY entry with atomicCAS on the
 //      key word; tag the entry with atomicMax((batch << 32) | (i + 1)) so the LAST request of a
 //      key in the batch wins (sequential put() semantics); touch the stamp of a found page;
-//   2. assign (thread per request, winners only): a fresh key pops a slot off the device free
-//      stack (atomicSub on its top), or evicts with a CLOCK hand (atomicAdd) over the per-slot
-//      recency stamps the gather kernel also writes: a slot referenced since it was inserted or
-//      since the hand last passed (stamp > passed) gets a second chance, a slot touched by this
-//      batch is skipped, the victim is claimed with atomicCAS on its stamp and its table entry
-//      becomes a tombstone;
-//   3. fill   (wave per 64 KiB chunk of a request): copy the page bytes into the winner's slot.
+//   2. threshold (evict only): a histogram of the evictable slots' ages (epoch - recency stamp;
+//      stamps are written by puts and by the gather kernel) and a one-block scan from the oldest
+//      age pick the smallest age A such that the slots untouched for >= A epochs cover the
+//      shortfall (fresh keys - free slots): approximate LRU at epoch granularity, no host sort;
+//   3. assign (thread per request, winners only): a fresh key pops a slot off the device free
+//      stack, or takes a victim under a rotating hand -- both wave-aggregated (one atomic per wave
+//      and round, lanes take consecutive positions) -- whose age is >= A; the victim is claimed
+//      with atomicCAS on its stamp and its table entry becomes a tombstone;
+//   4. fill   (wave per 64 KiB chunk of a request): copy the page bytes into the winner's slot.
 //
-// Tombstones are never reclaimed by device inserts (a concurrent probe of the same batch could
-// otherwise miss a key placed behind one); the host rebuilds the table when they pile up.
+// Tombstones are never reclaimed by inserts (a concurrent probe of the same batch could otherwise
+// miss a key placed behind one); when they pile up the table is rebuilt on the device (live
+// entries re-inserted into a cleared second table, slot -> entry index repointed).
 #include "kernels.h"
 
 #include <algorithm>
@@ -64,60 +67,171 @@ __global__ __launch_bounds__(256) void page_put_probe_kernel(PagePutArgs a) {
   }
 }
 
-// CLOCK victim: returns a claimed slot (its old key tombstoned and reported) or -1.
-__device__ int32_t page_put_victim(const PagePutArgs& a) {
-  const uint32_t limit = 4 * a.nslots;
-  for (uint32_t it = 0; it < limit; ++it) {
-    const uint32_t s = atomicAdd(&a.ctr->hand, 1u) % a.nslots;
-    const uint32_t st = __hip_atomic_load(&a.stamps[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (st >= a.epoch) continue;                             // this batch's page
-    const uint64_t old = __hip_atomic_load(&a.slot_key[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == kPageKeyEmpty) continue;                      // free slot (owned by the free stack)
-    if (st > a.passed[s]) {                                  // referenced since the last pass
-      a.passed[s] = a.epoch;
-      continue;
-    }
-    if (atomicCAS(&a.stamps[s], st, a.epoch) != st) continue;   // another request took it
-    const uint32_t ot = a.slot_tidx[s];
-    __hip_atomic_store(&a.table[ot].key, kPageKeyTomb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    a.table[ot].slot = -1;
-    a.table[ot].len = 0;
-    const uint32_t e = atomicAdd(&a.ctr->nevicted, 1u);
-    if (e < a.n) a.evicted[e] = old;
-    atomicAdd(&a.ctr->ntomb, 1u);
-    return (int32_t)s;
-  }
-  return -1;
+__device__ __forceinline__ bool page_put_take(const PagePutArgs& a, uint32_t s, uint32_t min_age) {
+  const uint32_t st = __hip_atomic_load(&a.stamps[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (st >= a.epoch || a.epoch - st < min_age) return false;   // this batch's page / too recent
+  const uint64_t old = __hip_atomic_load(&a.slot_key[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == kPageKeyEmpty) return false;                      // free slot (owned by the free stack)
+  if (atomicCAS(&a.stamps[s], st, a.epoch) != st) return false; // another request took it
+  const uint32_t ot = a.slot_tidx[s];
+  __hip_atomic_store(&a.table[ot].key, kPageKeyTomb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  a.table[ot].slot = -1;
+  a.table[ot].len = 0;
+  const uint32_t e = atomicAdd(&a.ctr->nevicted, 1u);
+  if (e < a.n) a.evicted[e] = old;
+  atomicAdd(&a.ctr->ntomb, 1u);
+  return true;
+}
+
+__device__ __forceinline__ uint32_t wave_rank(uint64_t m, int lane) {
+  return (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
 __global__ __launch_bounds__(256) void page_put_assign_kernel(PagePutArgs a) {
+  const int lane = threadIdx.x & 63;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const uint32_t tidx = a.tidx[i];
-    a.slot_of[i] = -1;
-    if (tidx == 0xFFFFFFFFu) continue;
-    if (a.tag[tidx] != ((a.batch << 32) | (unsigned long long)(i + 1))) continue;   // not the last
-    const uint64_t key = a.keys[i];
-    int32_t slot = a.table[tidx].slot;
-    if (slot < 0) {
-      const int32_t t = atomicSub(&a.ctr->free_top, 1) - 1;
-      if (t >= 0) slot = (int32_t)a.free_stack[t];
-      else if (a.evict) slot = page_put_victim(a);
-      if (slot < 0) {                          // no space: the claimed entry goes away again
+  const uint32_t min_age = a.evict ? __hip_atomic_load(&a.ctr->min_age, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0xFFFFFFFFu;
+  // wave-uniform trip count: every lane of a wave runs the same iterations (ballots below)
+  for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < a.n; base += stride) {
+    const uint32_t i = base + lane;
+    uint32_t tidx = 0xFFFFFFFFu;
+    int32_t slot = -1;
+    bool winner = false;
+    if (i < a.n) {
+      tidx = a.tidx[i];
+      a.slot_of[i] = -1;
+      if (tidx != 0xFFFFFFFFu && a.tag[tidx] == ((a.batch << 32) | (unsigned long long)(i + 1))) {
+        winner = true;
+        slot = a.table[tidx].slot;
+      }
+    }
+    const bool fresh = winner && slot < 0;
+    bool need = fresh;
+    uint64_t m = __ballot(need);
+    if (m) {                                     // free stack: one atomicSub per wave
+      const int leader = __ffsll((long long)m) - 1;
+      int32_t top = 0;
+      if (lane == leader) top = atomicSub(&a.ctr->free_top, (int32_t)__popcll(m));
+      top = __shfl(top, leader);
+      const int32_t t = top - 1 - (int32_t)wave_rank(m, lane);
+      if (need && t >= 0) {
+        slot = (int32_t)a.free_stack[t];
+        need = false;
+      }
+    }
+    if (a.evict) {                               // victims: one hand advance per wave and round
+      uint64_t scanned = 0;
+      const uint64_t budget = 2ull * a.nslots + 64;
+      while ((m = __ballot(need)) != 0 && scanned < budget) {
+        const int leader = __ffsll((long long)m) - 1;
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        uint32_t h = 0;
+        if (lane == leader) h = atomicAdd(&a.ctr->hand, cnt);
+        h = __shfl(h, leader);
+        scanned += cnt;
+        if (need) {
+          const uint32_t s = (uint32_t)(((uint64_t)h + wave_rank(m, lane)) % a.nslots);
+          if (page_put_take(a, s, min_age)) {
+            slot = (int32_t)s;
+            need = false;
+          }
+        }
+      }
+    }
+    if (!winner) continue;
+    if (fresh) {
+      if (need) {                                // no space: the claimed entry goes away again
         __hip_atomic_store(&a.table[tidx].key, kPageKeyTomb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         atomicAdd(&a.ctr->ntomb, 1u);
         atomicAdd(&a.ctr->nfail, 1u);
         continue;
       }
-      // stamp before the key: a concurrent CLOCK hand sees either a free slot or this batch's stamp
+      // stamp before the key: a concurrent hand sees either a free slot or this batch's stamp
       atomicMax(&a.stamps[slot], a.epoch);
-      a.passed[slot] = a.epoch;                // inserted now: "referenced" only if touched later
-      __hip_atomic_store(&a.slot_key[slot], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.slot_key[slot], a.keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       a.slot_tidx[slot] = tidx;
       a.table[tidx].slot = slot;
     }
     a.table[tidx].len = a.len;
     a.slot_of[i] = slot;
+  }
+}
+
+// Ages of the evictable slots (occupied, not touched by this batch), LDS histogram per block.
+__global__ __launch_bounds__(256) void page_put_hist_kernel(PagePutArgs a) {
+  __shared__ uint32_t h[kPutAgeBuckets];
+  for (uint32_t b = threadIdx.x; b < kPutAgeBuckets; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < a.nslots; s += stride) {
+    if (a.slot_key[s] == kPageKeyEmpty) continue;
+    const uint32_t st = a.stamps[s];
+    if (st >= a.epoch) continue;
+    atomicAdd(&h[min(a.epoch - st, kPutAgeBuckets - 1)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kPutAgeBuckets; b += blockDim.x)
+    if (h[b]) atomicAdd(&a.hist[b], h[b]);
+}
+
+// One block: smallest age A whose tail (ages >= A) covers the shortfall.
+__global__ __launch_bounds__(256) void page_put_thresh_kernel(PagePutArgs a) {
+  constexpr uint32_t kPer = kPutAgeBuckets / 256;
+  __shared__ uint32_t part[256];
+  const uint32_t t = threadIdx.x;
+  const uint32_t hi = kPutAgeBuckets - 1 - t * kPer;           // this thread: ages hi .. hi-kPer+1
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < kPer; ++k) sum += a.hist[hi - k];
+  part[t] = sum;
+  __syncthreads();
+  if (t != 0) return;
+  const int64_t need = (int64_t)a.ctr->nfresh - (int64_t)max(a.ctr->free_top, 0);
+  uint32_t age = kPutAgeBuckets;                                // nothing to evict
+  if (need > 0) {
+    age = 1;                                                    // not enough: everything evictable
+    int64_t cum = 0;
+    for (uint32_t c = 0; c < 256; ++c) {
+      if (cum + part[c] < need) {
+        cum += part[c];
+        continue;
+      }
+      const uint32_t top = kPutAgeBuckets - 1 - c * kPer;
+      for (uint32_t k = 0; k < kPer; ++k) {
+        cum += a.hist[top - k];
+        if (cum >= need) {
+          age = max(top - k, 1u);
+          break;
+        }
+      }
+      break;
+    }
+  }
+  a.ctr->min_age = age;
+}
+
+__global__ __launch_bounds__(256) void page_table_clear_kernel(PageTableEntry* t, uint64_t size) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < size; i += stride)
+    t[i] = PageTableEntry{kPageKeyEmpty, -1, 0};
+}
+
+__global__ __launch_bounds__(256) void page_table_reinsert_kernel(PagePutArgs a, PageTableEntry* fresh) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= a.mask; i += stride) {
+    const PageTableEntry e = a.table[i];
+    if (e.key == kPageKeyEmpty || e.key == kPageKeyTomb || e.slot < 0) continue;
+    uint64_t h = page_key_hash(e.key) & a.mask;
+    for (uint64_t probe = 0; probe <= a.mask; ++probe, h = (h + 1) & a.mask) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&fresh[h].key,
+                                                (unsigned long long)kPageKeyEmpty, (unsigned long long)e.key);
+      if (prev == kPageKeyEmpty) {
+        fresh[h].slot = e.slot;
+        fresh[h].len = e.len;
+        a.slot_tidx[e.slot] = (uint32_t)h;
+        break;
+      }
+    }
   }
 }
 
@@ -197,6 +311,23 @@ hipError_t launch_page_put_fill(const PagePutArgs& a, hipStream_t stream) {
                    (a.page_size % 16 == 0);
   if (vec) hipLaunchKernelGGL((page_put_fill_kernel<true>), dim3(grid), dim3(256), 0, stream, a, nch);
   else hipLaunchKernelGGL((page_put_fill_kernel<false>), dim3(grid), dim3(256), 0, stream, a, nch);
+  return hipGetLastError();
+}
+
+hipError_t launch_page_put_threshold(const PagePutArgs& a, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(a.hist, 0, kPutAgeBuckets * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return e;
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((a.nslots + 1023) / 1024, 512));
+  hipLaunchKernelGGL(page_put_hist_kernel, dim3(grid), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(page_put_thresh_kernel, dim3(1), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_page_table_rebuild(const PagePutArgs& a, PageTableEntry* fresh, hipStream_t stream) {
+  const uint64_t size = a.mask + 1;
+  const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((size + 255) / 256, 8192));
+  hipLaunchKernelGGL(page_table_clear_kernel, dim3(grid), dim3(256), 0, stream, fresh, size);
+  hipLaunchKernelGGL(page_table_reinsert_kernel, dim3(grid), dim3(256), 0, stream, a, fresh);
   return hipGetLastError();
 }
 

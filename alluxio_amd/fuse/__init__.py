@@ -86,8 +86,29 @@ class AlluxioFuseOps:
 
     # ---- metadata -----------------------------------------------------------------------------
     def getattr(self, path, fh=None):
+        return self.stat_info(path)[0]
+
+    def stat_info(self, path):
+        """(fusepy attribute dict, FileInfo) of ``path``: the kernel server caches the info's file
+        id and blocks natively for opens served without Python."""
         st = self._call(self.fs.get_status, self._p(path))
-        i = st.info
+        return self._attrs(st.info), st.info
+
+    def list_infos(self, path):
+        """[(name, attribute dict, FileInfo)] of a directory's children from ONE listing (the
+        kernel server's OPENDIR fills its attribute cache from it)."""
+        kids = self._call(self.fs.list_status, self._p(path))
+        return [(k.name, self._attrs(k.info), k.info) for k in kids]
+
+    def list_chunks(self, path):
+        """Serialized ListStatus replies of a directory (the native FUSE server decodes and caches
+        them without per-entry Python), or None when attributes need per-entry Python (user/group
+        translation) or the client has no raw listing."""
+        if self.translate or not hasattr(self.fs, "list_status_chunks"):
+            return None
+        return self._call(self.fs.list_status_chunks, self._p(path))
+
+    def _attrs(self, i) -> dict:
         # files still being written report their open size
         size = i.length
         if not i.completed and not i.folder:
@@ -234,6 +255,18 @@ class AlluxioFuseOps:
         if of is None:
             raise FuseOSError(errno.EBADF)
         return of
+
+    def file_id(self, fh) -> int:
+        """Alluxio file id behind a read handle (0 if unknown)."""
+        with self._lock:
+            of = self._open.get(fh)
+        st = getattr(getattr(of, "fin", None), "status", None)
+        return int(getattr(st, "fileId", 0) or 0)
+
+    def is_write_handle(self, fh) -> bool:
+        with self._lock:
+            of = self._open.get(fh)
+        return of is not None and of.fout is not None
 
     def read(self, path, size, offset, fh):
         of = self._entry(fh)

@@ -10,6 +10,19 @@ from a pool of threads, each reading one request at a time (the multi-threaded l
 The kernel speaks in node ids; the op layer is path based (as the reference's), so the server keeps
 a node-id <-> path table (LOOKUP/CREATE/MKDIR allocate, FORGET drops, RENAME rewrites the moved
 subtree).  Directory listings are snapshotted at OPENDIR and paged out by offset.
+
+Native mode (default when the extension is built): the ``/dev/fuse`` request loop runs in C++
+(csrc/fuse_server.cpp).  LOOKUP/GETATTR are answered from a native attribute cache that this
+module fills (every Python getattr, and a whole directory at OPENDIR from one listing); OPEN of a
+completed file whose blocks are all in the co-located worker's store (``store=``: the worker's
+native BlockStore -- the worker-embedded FUSE deployment) read-locks the blocks natively, and READ,
+FLUSH and RELEASE of such handles never reach Python (READ replies gather straight from the DRAM
+arena with writev, or D2H-copy from HBM).  Everything else -- mutations, misses, files not cached
+locally -- is queued to Python handler threads.  Mutations invalidate the cached attributes.
+
+Kernel page cache (``keep_cache``): ``"auto"`` (default) keeps it across opens only while the
+file's Alluxio file id is unchanged (files are write-once; a re-created path gets a new id),
+``True`` always, ``False`` never.
 """
 from __future__ import annotations
 
@@ -46,6 +59,7 @@ ATTR = struct.Struct("<QQQQQQIIIIIIIIII")      # fuse_attr (88 bytes)
 ENTRY_HEAD = struct.Struct("<QQQQII")          # nodeid generation entry_valid attr_valid + nsecs
 ATTR_OUT_HEAD = struct.Struct("<QII")
 INIT_OUT = struct.Struct("<IIIIHHIIHH32x")     # major minor max_readahead flags max_bg cong max_write gran pages align
+INIT_OUT_EXT = struct.Struct("<IIIIHHIIHHII24x")  # ... + flags2 max_stack_depth (protocol 7.36 / 7.40)
 OPEN_OUT = struct.Struct("<QII")
 READ_IN = struct.Struct("<QQIIQII")
 WRITE_IN = struct.Struct("<QQIIQII")
@@ -56,13 +70,16 @@ DIRENT = struct.Struct("<QQII")
 FATTR_MODE, FATTR_UID, FATTR_GID, FATTR_SIZE = 1 << 0, 1 << 1, 1 << 2, 1 << 3
 FATTR_ATIME, FATTR_MTIME = 1 << 4, 1 << 5
 FUSE_ASYNC_READ, FUSE_ATOMIC_O_TRUNC, FUSE_BIG_WRITES = 1 << 0, 1 << 3, 1 << 5
+FUSE_AUTO_INVAL_DATA, FUSE_NO_OPEN_SUPPORT, FUSE_INIT_EXT = 1 << 12, 1 << 17, 1 << 30
+FUSE_PASSTHROUGH_HI = 1 << (37 - 32)           # FUSE_PASSTHROUGH, in flags2
 FOPEN_KEEP_CACHE = 1 << 1
-MS_NOSUID, MS_NODEV = 2, 4
+MS_RDONLY, MS_NOSUID, MS_NODEV = 1, 2, 4
 MNT_DETACH = 2
 MAX_WRITE = 128 << 10
 ROOT_ID = 1
 TTL_S = 1              # directories / entries (the namespace can change under them)
 TTL_COMPLETE_S = 60    # attributes of completed (write-once, immutable) files
+RO_HANDLES = 256       # python read handles kept for fh-0 READs (read-only, zero-message opens)
 
 
 def _ts(t: float) -> tuple[int, int]:
@@ -74,9 +91,25 @@ class FuseKernelServer:
     """Serve ``ops`` at ``mountpoint`` until :meth:`unmount`."""
 
     def __init__(self, ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False,
-                 keep_cache: bool = False):
+                 keep_cache="auto", native: bool | None = None, store=None, session: int = 0,
+                 py_threads: int | None = None, read_only: bool = False, passthrough: bool = False,
+                 file_ttl_s: int = TTL_COMPLETE_S):
         self.ops = ops
+        self.file_ttl_s = file_ttl_s
+        self.read_only = read_only
+        self.passthrough = passthrough
+        self.passthrough_active = False
+        self._ro_open: dict[str, int] = {}               # fh-0 READs: path -> python read handle (LRU)
         self.keep_cache = keep_cache
+        self._keep_mode = 2 if keep_cache == "auto" else (1 if keep_cache else 0)
+        self._last_fid: dict[int, int] = {}           # python-path opens: node -> file id (keep_cache auto)
+        self.native = native
+        self.store = store
+        self.session = session
+        self.py_threads = py_threads
+        self._srv = None
+        self._listing: dict[str, threading.Event] = {}   # directory listings in flight (LOOKUP prefetch)
+        self._listed: dict[str, float] = {}              # directory -> prefetched until (monotonic s)
         self.mountpoint = os.path.abspath(mountpoint)
         self.nthreads = max(1, threads)
         self.allow_other = allow_other
@@ -100,14 +133,35 @@ class FuseKernelServer:
         if self.allow_other:
             opts += ",allow_other"
         rc = libc.mount(b"alluxio", self.mountpoint.encode(), b"fuse.alluxio",
-                        ctypes.c_ulong(MS_NOSUID | MS_NODEV), opts.encode())
+                        ctypes.c_ulong(MS_NOSUID | MS_NODEV | (MS_RDONLY if self.read_only else 0)),
+                        opts.encode())
         if rc != 0:
             err = ctypes.get_errno()
             os.close(self.fd)
             self.fd = -1
             raise OSError(err, f"mount {self.mountpoint}: {os.strerror(err)}")
-        for i in range(self.nthreads):
-            t = threading.Thread(target=self._loop, name=f"fuse-{i}", daemon=True)
+        srv_cls = None
+        if self.native is not False:
+            try:
+                from ..ops.native import lib
+                srv_cls = getattr(lib(), "FuseServer", None)
+            except Exception:  # noqa: BLE001 - extension not built
+                srv_cls = None
+            if srv_cls is None and self.native:
+                self.unmount()
+                raise RuntimeError("native FUSE server requested but the extension has no FuseServer")
+        if srv_cls is not None:
+            native_store = getattr(self.store, "native", self.store)     # TieredStore or BlockStore
+            self._srv = srv_cls(self.fd, self.nthreads, native_store, self.session, self._keep_mode)
+            for arena in getattr(self.store, "arenas", None) or []:
+                if arena is not None and getattr(arena, "fd", -1) >= 0:
+                    self._srv.add_arena(arena.base, arena.nbytes, arena.fd)
+            self._srv.start()
+            target, n = self._py_loop, self.py_threads or self.nthreads
+        else:
+            target, n = self._loop, self.nthreads
+        for i in range(n):
+            t = threading.Thread(target=target, name=f"fuse-{i}", daemon=True)
             t.start()
             self._threads.append(t)
         return self
@@ -118,6 +172,8 @@ class FuseKernelServer:
         self._stop.set()
         libc = ctypes.CDLL(None, use_errno=True)
         libc.umount2(self.mountpoint.encode(), MNT_DETACH)
+        if self._srv is not None:
+            self._srv.stop()                 # native readers poll with a timeout: they exit here
         try:
             os.close(self.fd)        # aborts the connection: readers return ENODEV / EBADF
         except OSError:
@@ -136,6 +192,11 @@ class FuseKernelServer:
 
     # ---- node table --------------------------------------------------------------------------
     def _path(self, nodeid: int) -> str:
+        if self._srv is not None:
+            p = self._srv.path_of(nodeid)
+            if p is None:
+                raise FuseOSError(errno.ESTALE)
+            return p
         with self._lock:
             p = self._paths.get(nodeid)
         if p is None:
@@ -143,6 +204,8 @@ class FuseKernelServer:
         return p
 
     def _node(self, path: str) -> int:
+        if self._srv is not None:
+            return self._srv.node_of(path)
         with self._lock:
             nid = self._ids.get(path)
             if nid is None:
@@ -153,12 +216,19 @@ class FuseKernelServer:
             return nid
 
     def _forget_path(self, path: str) -> None:
+        if self._srv is not None:
+            self._srv.forget_path(path)
+            return
         with self._lock:
             nid = self._ids.pop(path, None)
             if nid is not None and nid != ROOT_ID:
                 self._paths.pop(nid, None)
+                self._last_fid.pop(nid, None)
 
     def _moved(self, old: str, new: str) -> None:
+        if self._srv is not None:
+            self._srv.moved(old, new)
+            return
         with self._lock:
             pre = old.rstrip("/") + "/"
             for p in [p for p in self._ids if p == old or p.startswith(pre)]:
@@ -180,19 +250,141 @@ class FuseKernelServer:
                          a["st_mode"], a.get("st_nlink", 1), a.get("st_uid", 0), a.get("st_gid", 0), 0,
                          a.get("st_blksize", 4096), 0)
 
-    @staticmethod
-    def _attr_ttl(a: dict) -> int:
+    def _attr_ttl(self, a: dict) -> int:
         # a file's size changes while it is written (and at completion): cache attrs only once the
         # file is complete -- Alluxio files are write-once, so a completed file's size is final
         if a.get("st_complete"):
-            return TTL_COMPLETE_S
+            return self.file_ttl_s
         return TTL_S if stat.S_ISDIR(a["st_mode"]) else 0
 
     def _entry(self, path: str) -> bytes:
-        a = self.ops.getattr(path)
+        a, info = self.ops.stat_info(path)
+        nid = self._node(path)
+        ttl = self._attr_ttl(a)
+        self._cache(path, a, info, ttl)
+        return ENTRY_HEAD.pack(nid, 0, max(TTL_S, ttl), ttl, 0, 0) + self._attr(nid, a)
+
+    def _cache(self, path: str, a: dict, info, ttl: int) -> None:
+        """Hand the attributes (and, for a completed file, its blocks) to the native server."""
+        if self._srv is None or ttl <= 0:
+            return
+        blocks, lens = [], []
+        complete = bool(a.get("st_complete")) and not stat.S_ISDIR(a["st_mode"])
+        if complete:
+            bs = info.blockSizeBytes or 1
+            blocks = list(info.blockIds)
+            lens = [min(bs, info.length - i * bs) for i in range(len(blocks))]
+        self._srv.put_attr(path, self._attr(0, a), ttl * 1000, ttl, int(info.fileId or 0), complete, blocks, lens)
+
+    def _prefetch(self, parent: str, name: str):
+        """A LOOKUP missed the native cache: list the parent directory once (one RPC instead of
+        one per sibling) and cache every child, so the siblings' LOOKUPs never reach Python.
+        Returns (attrs, info) of ``name`` when the listing holds it, else None."""
+        import time as _time
+        now = _time.monotonic()
+        with self._lock:
+            ev = self._listing.get(parent)
+            mine = ev is None
+            if mine:
+                if self._listed.get(parent, 0.0) > now:
+                    return None                     # listed recently: this miss is a genuine one
+                ev = self._listing[parent] = threading.Event()
+        if not mine:
+            ev.wait(10.0)
+            return None
+        found = None
+        try:
+            found = self._list_into_cache(parent, name)
+            with self._lock:
+                self._listed[parent] = now + self.file_ttl_s
+        except (FuseOSError, OSError):
+            pass                                    # not a directory / gone: the plain path decides
+        finally:
+            with self._lock:
+                self._listing.pop(parent, None)
+            ev.set()
+        return found
+
+    def _list_into_cache(self, parent: str, name: str | None = None, entries: list | None = None):
+        """One listing of ``parent`` into the native attribute cache (natively decoded when the
+        op layer hands out raw replies).  Returns the LOOKUP payload of ``name`` if listed;
+        ``entries`` collects (name, mode) for READDIR."""
+        chunks = self.ops.list_chunks(parent)
+        if chunks is None:
+            found = None
+            for n, a, info in self.ops.list_infos(parent):
+                path = self._child(parent, n)
+                self._cache(path, a, info, self._attr_ttl(a))
+                if entries is not None:
+                    entries.append((n, a["st_mode"]))
+                if n == name:
+                    found = self._entry_payload(path, a)
+            return found
+        self._srv.cache_listing(chunks, self.ops.root, self.ops.uid, self.ops.gid, self.file_ttl_s, TTL_S)
+        if entries is not None:
+            from ..ops.native import lib
+            cols = lib().decode_file_infos(chunks)
+            for p, folder in zip(cols["paths"], cols["folder"].tolist()):
+                entries.append((p.rsplit("/", 1)[-1], stat.S_IFDIR if folder else stat.S_IFREG))
+        return None if name is None else self._srv.entry(self._child(parent, name))
+
+    def _entry_payload(self, path: str, a: dict) -> bytes:
         nid = self._node(path)
         ttl = self._attr_ttl(a)
         return ENTRY_HEAD.pack(nid, 0, max(TTL_S, ttl), ttl, 0, 0) + self._attr(nid, a)
+
+    def _mode_of(self, parent: str, name: str) -> int:
+        try:
+            return self.ops.getattr(self._child(parent, name))["st_mode"]
+        except FuseOSError:
+            return 0
+
+    def _ro_handle(self, path: str) -> int:
+        """Read handle of ``path`` for fh-0 READs of a zero-message-open mount: opened on the first
+        READ the native server could not serve, reused, closed least-recently-used first."""
+        with self._lock:
+            fh = self._ro_open.pop(path, None)
+            if fh is not None:
+                self._ro_open[path] = fh
+                return fh
+        fh = self.ops.open(path, os.O_RDONLY)
+        drop = []
+        with self._lock:
+            old = self._ro_open.pop(path, None)
+            if old is not None:
+                drop.append(old)
+            self._ro_open[path] = fh
+            while len(self._ro_open) > RO_HANDLES:
+                drop.append(self._ro_open.pop(next(iter(self._ro_open))))
+        for d in drop:
+            try:
+                self.ops.release(None, d)
+            except FuseOSError:
+                pass
+        return fh
+
+    def _inval(self, *paths: str) -> None:
+        if self._srv is None:
+            return
+        with self._lock:
+            for p in paths:
+                self._listed.pop(p.rsplit("/", 1)[0] or "/", None)
+        for p in paths:
+            self._srv.invalidate(p, True)                              # the path and its subtree
+            self._srv.invalidate(p.rsplit("/", 1)[0] or "/", False)    # the parent's own attrs
+
+    def op_stats(self) -> dict:
+        """Requests per opcode: {"native": {...}, "python": {...}} (python only without the extension)."""
+        if self._srv is None:
+            return {"native": {}, "python": {OP_NAMES.get(k, str(k)): v for k, v in sorted(self.op_counts.items())}}
+        v = self._srv.stats()
+        name = lambda k: OP_NAMES.get(k, str(k))  # noqa: E731
+        return {"native": {name(k): v[k] for k in range(64) if v[k]},
+                "python": {name(k): v[64 + k] for k in range(64) if v[64 + k]},
+                "native_us_per_op": {name(k): round(v[128 + k] / v[k] / 1e3, 2) for k in range(64) if v[k]},
+                "read_write_us": round(v[128 + 63] / max(1, v[READ]) / 1e3, 2),
+                "native_opens": self._srv.native_opens, "passthrough_opens": self._srv.passthrough_opens, "fallback_opens": self._srv.fallback_opens,
+                "native_reads": self._srv.native_reads}
 
     # ---- request loop ------------------------------------------------------------------------
     def _loop(self) -> None:
@@ -211,7 +403,24 @@ class FuseKernelServer:
             except Exception:  # noqa: BLE001 - never kill a serving thread
                 LOG.exception("fuse request failed")
 
+    def _py_loop(self) -> None:
+        srv = self._srv
+        while True:
+            reqs = srv.poll(16, 200)
+            if not reqs:
+                if self._stop.is_set() or not srv.alive:
+                    return
+                continue
+            for unique, op, nodeid, _uid, _gid, _pid, body in reqs:
+                try:
+                    self._serve(op, unique, nodeid, body)
+                except Exception:  # noqa: BLE001 - never kill a serving thread
+                    LOG.exception("fuse request failed")
+
     def _reply(self, unique: int, err: int = 0, payload: bytes = b"") -> None:
+        if self._srv is not None:
+            self._srv.reply(unique, err, payload)
+            return
         try:
             os.write(self.fd, OUT_HDR.pack(OUT_HDR.size + len(payload), -err, unique) + payload)
         except OSError as e:
@@ -220,7 +429,9 @@ class FuseKernelServer:
 
     def _dispatch(self, req: bytes) -> None:
         _, op, unique, nodeid, uid, gid, pid, _ = IN_HDR.unpack_from(req)
-        body = memoryview(req)[IN_HDR.size:]
+        self._serve(op, unique, nodeid, memoryview(req)[IN_HDR.size:])
+
+    def _serve(self, op: int, unique: int, nodeid: int, body) -> None:
         self.requests += 1
         self.op_counts[op] = self.op_counts.get(op, 0) + 1
         if op in (FORGET, BATCH_FORGET, INTERRUPT):
@@ -255,15 +466,39 @@ class FuseKernelServer:
             if major != 7:
                 raise FuseOSError(errno.EPROTO)
             want = FUSE_ASYNC_READ | FUSE_ATOMIC_O_TRUNC | FUSE_BIG_WRITES
+            if self.read_only and self._srv is not None:
+                # zero-message opens (no OPEN/RELEASE per file) + page cache dropped whenever a
+                # refreshed attribute shows another mtime/size (a replaced file)
+                want |= FUSE_NO_OPEN_SUPPORT | FUSE_AUTO_INVAL_DATA
+                if flags & FUSE_NO_OPEN_SUPPORT:
+                    self._srv.set_no_open(True)
+            elif (self.passthrough and self._srv is not None and self.store is not None and minor >= 40
+                  and flags & FUSE_INIT_EXT and len(body) >= 20):
+                flags2 = struct.unpack_from("<I", body, 16)[0]
+                if flags2 & FUSE_PASSTHROUGH_HI:
+                    # opens of blocks held as files (tmpfs tier) hand the kernel the block file:
+                    # reads are served by it directly (protocol 7.40 passthrough)
+                    self._srv.set_passthrough(True)
+                    self.passthrough_active = True
+                    return INIT_OUT_EXT.pack(7, 40, max_ra, (flags & want) | FUSE_INIT_EXT, 16, 12, MAX_WRITE, 1,
+                                             0, 0, FUSE_PASSTHROUGH_HI, 1)
             return INIT_OUT.pack(7, min(minor, 34), max_ra, flags & want, 16, 12, MAX_WRITE, 1, 0, 0)
         if op == DESTROY:
             return b""
         if op == LOOKUP:
             name, _ = self._name(body)
-            return self._entry(self._child(self._path(nodeid), name))
+            parent = self._path(nodeid)
+            if self._srv is not None:
+                hit = self._prefetch(parent, name)
+                if hit is not None:
+                    return hit
+            return self._entry(self._child(parent, name))
         if op == GETATTR:
-            a = ops.getattr(self._path(nodeid))
-            return ATTR_OUT_HEAD.pack(self._attr_ttl(a), 0, 0) + self._attr(nodeid, a)
+            path = self._path(nodeid)
+            a, info = ops.stat_info(path)
+            ttl = self._attr_ttl(a)
+            self._cache(path, a, info, ttl)
+            return ATTR_OUT_HEAD.pack(ttl, 0, 0) + self._attr(nodeid, a)
         if op == SETATTR:
             f = SETATTR_IN.unpack_from(body)
             valid, fh, size, mode, uid, gid = f[0], f[2], f[3], f[11], f[13], f[14]
@@ -274,6 +509,7 @@ class FuseKernelServer:
                 ops.chown(path, uid if valid & FATTR_UID else -1, gid if valid & FATTR_GID else -1)
             if valid & FATTR_SIZE:
                 ops.truncate(path, size, fh or None)
+            self._inval(path)
             a = ops.getattr(path)
             return ATTR_OUT_HEAD.pack(self._attr_ttl(a), 0, 0) + self._attr(nodeid, a)
         if op == ACCESS:
@@ -288,11 +524,13 @@ class FuseKernelServer:
             name, _ = self._name(body, 8)
             path = self._child(self._path(nodeid), name)
             ops.mkdir(path, mode)
+            self._inval(path)
             return self._entry(path)
         if op in (UNLINK, RMDIR):
             name, _ = self._name(body)
             path = self._child(self._path(nodeid), name)
             (ops.unlink if op == UNLINK else ops.rmdir)(path)
+            self._inval(path)
             self._forget_path(path)
             return b""
         if op in (RENAME, RENAME2):
@@ -305,6 +543,7 @@ class FuseKernelServer:
             src = self._child(self._path(nodeid), old)
             dst = self._child(self._path(newdir), new)
             ops.rename(src, dst)
+            self._inval(src, dst)
             self._moved(src, dst)
             return b""
         if op == CREATE:
@@ -312,20 +551,35 @@ class FuseKernelServer:
             name, _ = self._name(body, 16)
             path = self._child(self._path(nodeid), name)
             fh = ops.create(path, mode)
+            self._inval(path)
             return self._entry(path) + OPEN_OUT.pack(fh, 0, 0)
         if op == OPEN:
             flags = struct.unpack_from("<I", body)[0]
             path = self._path(nodeid)
+            if flags & (os.O_WRONLY | os.O_RDWR):
+                self._inval(path)
             fh = ops.open(path, flags)
             keep = 0
-            if flags & (os.O_WRONLY | os.O_RDWR) == 0 and self.keep_cache:
-                # completed files never change: keep the kernel page cache across opens
-                # (a second epoch over a dataset is served from it)
-                keep = FOPEN_KEEP_CACHE
+            if flags & (os.O_WRONLY | os.O_RDWR) == 0 and self._keep_mode:
+                # completed (write-once) files never change under one file id: keep the kernel
+                # page cache across opens (a second epoch over a dataset is served from it)
+                if self._keep_mode == 1:
+                    keep = FOPEN_KEEP_CACHE
+                elif self._srv is not None:
+                    keep = FOPEN_KEEP_CACHE if self._srv.keep_open(nodeid, ops.file_id(fh)) else 0
+                else:
+                    fid = ops.file_id(fh)
+                    with self._lock:
+                        if fid and self._last_fid.get(nodeid, fid) == fid:
+                            keep = FOPEN_KEEP_CACHE
+                        self._last_fid[nodeid] = fid
             return OPEN_OUT.pack(fh, keep, 0)
         if op == READ:
             fh, offset, size = READ_IN.unpack_from(body)[:3]
-            return bytes(ops.read(self._path(nodeid), size, offset, fh))
+            path = self._path(nodeid)
+            if fh == 0:
+                fh = self._ro_handle(path)          # zero-message open (read-only mount)
+            return bytes(ops.read(path, size, offset, fh))
         if op == WRITE:
             fh, offset, size = WRITE_IN.unpack_from(body)[:3]
             data = body[WRITE_IN.size:WRITE_IN.size + size]
@@ -333,6 +587,8 @@ class FuseKernelServer:
             return struct.pack("<II", n, 0)
         if op == FLUSH:
             fh = struct.unpack_from("<Q", body)[0]
+            if ops.is_write_handle(fh):
+                self._inval(self._path(nodeid))
             ops.flush(None, fh)
             return b""
         if op in (FSYNC, FSYNCDIR):
@@ -346,17 +602,11 @@ class FuseKernelServer:
             return b""
         if op == OPENDIR:
             path = self._path(nodeid)
-            names = ops.readdir(path)
-            entries = []
-            for n in names:
-                if n in (".", ".."):
-                    entries.append((n, stat.S_IFDIR))
-                    continue
-                try:
-                    m = ops.getattr(self._child(path, n))["st_mode"]
-                except FuseOSError:
-                    continue
-                entries.append((n, m))
+            entries = [(".", stat.S_IFDIR), ("..", stat.S_IFDIR)]
+            if self._srv is not None:
+                self._list_into_cache(path, None, entries)
+            else:
+                entries += [(n, m) for n in ops.readdir(path)[2:] for m in [self._mode_of(path, n)] if m]
             with self._lock:
                 h = self._next_dir
                 self._next_dir += 1
@@ -391,6 +641,11 @@ class FuseKernelServer:
 
 
 def mount_kernel(ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False,
-                 keep_cache: bool = False) -> FuseKernelServer:
-    """Mount ``ops`` at ``mountpoint`` through ``/dev/fuse``; returns the running server."""
-    return FuseKernelServer(ops, mountpoint, threads, allow_other, keep_cache).mount()
+                 keep_cache="auto", native: bool | None = None, store=None, session: int = 0,
+                 py_threads: int | None = None, read_only: bool = False, passthrough: bool = False,
+                 file_ttl_s: int = TTL_COMPLETE_S) -> FuseKernelServer:
+    """Mount ``ops`` at ``mountpoint`` through ``/dev/fuse``; returns the running server.
+    ``store``: the co-located worker's native BlockStore (native opens/reads of cached files).
+    ``read_only``: ``-o ro`` -- with the native server this also negotiates zero-message opens."""
+    return FuseKernelServer(ops, mountpoint, threads, allow_other, keep_cache, native, store, session,
+                            py_threads, read_only, passthrough, file_ttl_s).mount()

@@ -40,6 +40,29 @@ class FileDataset:
         return torch.from_numpy(np.frombuffer(b, dtype=np.uint8)[:16].copy()), len(b)
 
 
+def _cpu():
+    import resource
+    s, c = resource.getrusage(resource.RUSAGE_SELF), resource.getrusage(resource.RUSAGE_CHILDREN)
+    return s.ru_utime + s.ru_stime, c.ru_utime + c.ru_stime
+
+
+def _thread_cpu() -> dict:
+    """CPU seconds per thread name of this process (diagnostics: where the server time goes)."""
+    out = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        f = st[st.rindex(")") + 2:].split()
+        key = name.rstrip("0123456789")
+        out[key] = out.get(key, 0.0) + (int(f[11]) + int(f[12])) / tck
+    return out
+
+
 def _epochs(paths, epochs, workers, batch, seed=0):
     import torch
     from torch.utils.data import DataLoader, RandomSampler
@@ -49,13 +72,20 @@ def _epochs(paths, epochs, workers, batch, seed=0):
         dl = DataLoader(FileDataset(paths), batch_size=batch, sampler=RandomSampler(paths, generator=g),
                         num_workers=workers, persistent_workers=False)
         t0 = time.perf_counter()
+        c0 = _cpu()
+        th0 = _thread_cpu()
         n = nbytes = 0
         for _, lens in dl:
             n += len(lens)
             nbytes += int(lens.sum())
         dt = time.perf_counter() - t0
+        del dl
+        c1 = _cpu()
+        th1 = _thread_cpu()
+        busy = {k: round(v - th0.get(k, 0.0), 2) for k, v in th1.items() if v - th0.get(k, 0.0) >= 0.05}
         out.append({"epoch": e, "files": n, "files_per_s": round(n / dt, 1), "GBps": round(nbytes / dt / 1e9, 3),
-                    "s": round(dt, 3)})
+                    "s": round(dt, 3), "cpu_s_server_process": round(c1[0] - c0[0], 2),
+                    "cpu_s_loader_workers": round(c1[1] - c0[1], 2), "cpu_s_by_thread": busy})
         print(json.dumps(out[-1]), flush=True)
     return out
 
@@ -69,6 +99,18 @@ def main(argv=None) -> int:
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--fuse-threads", type=int, default=2)
+    ap.add_argument("--server", choices=["native", "python"], default="native",
+                    help="native: C++ /dev/fuse loop (csrc/fuse_server.cpp); python: the pure-Python loop")
+    ap.add_argument("--no-embedded", action="store_true",
+                    help="do not hand the worker's block store to the FUSE server (no native opens/reads)")
+    ap.add_argument("--read-only", action="store_true",
+                    help="-o ro mount: with the native server, zero-message opens (no OPEN/RELEASE per file)")
+    ap.add_argument("--passthrough", action="store_true",
+                    help="FUSE passthrough opens of single-block files held in a file tier (--tier DIR)")
+    ap.add_argument("--tier", default="dram",
+                    help="worker cache tier: dram (memfd arena) or a directory (e.g. /dev/shm/x: block files, "
+                         "which the native server hands to the kernel as FUSE passthrough backing files)")
+    ap.add_argument("--keep-cache", default="auto", help="auto | on | off (kernel page cache across opens)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import numpy as np
@@ -79,11 +121,16 @@ def main(argv=None) -> int:
     mnt = os.path.join(work, "mnt")
     os.makedirs(mnt)
     quota = max(1 << 30, int(a.files * a.file_size * 1.3))
-    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "dram",
+    tier = a.tier
+    if tier != "dram":
+        tier = os.path.join(tier, f"fusebench_{os.getpid()}")
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": tier,
+            "alluxio.worker.tieredstore.level0.dirs.mediumtype": "MEM",
             "alluxio.worker.tieredstore.level0.dirs.quota": str(quota),
             "alluxio.user.block.size.bytes.default": "1MB", "alluxio.worker.hbm.page.size": "128KB"}
     res = {"setup": f"{a.files} x {a.file_size} B files in {a.dirs} dirs, DataLoader workers={a.workers} "
-                    f"batch={a.batch}, FUSE threads={a.fuse_threads}, DRAM tier, {os.cpu_count()} CPUs"}
+                    f"batch={a.batch}, FUSE threads={a.fuse_threads}, tier={a.tier}, {os.cpu_count()} CPUs, "
+                    f"keep_cache={a.keep_cache}, read_only={a.read_only}"}
     try:
         with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=os.path.join(work, "c")) as c:
             fs = c.client(metadata_cache=True)
@@ -94,13 +141,16 @@ def main(argv=None) -> int:
             for i, r in enumerate(rel):
                 fs.write_file("/ds/" + r, blob[i % 4096:i % 4096 + a.file_size], write_type="CACHE_THROUGH")
             res["write_files_per_s"] = round(a.files / (time.perf_counter() - t0), 1)
-            srv = mount_kernel(AlluxioFuseOps(fs), mnt, threads=a.fuse_threads)
+            keep = {"auto": "auto", "on": True, "off": False}[a.keep_cache]
+            store = None if a.no_embedded or a.server == "python" else c.workers[0].store
+            srv = mount_kernel(AlluxioFuseOps(fs), mnt, threads=a.fuse_threads, native=a.server == "native",
+                               store=store, keep_cache=keep, read_only=a.read_only,
+                               passthrough=a.passthrough)
+            res["server"] = a.server + ("" if store is None else " (worker-embedded: native open/read)")
             try:
                 paths = [os.path.join(mnt, "ds", r) for r in rel]
                 res["fuse"] = _epochs(paths, a.epochs, a.workers, a.batch)
-                res["fuse_requests"] = srv.requests
-                from alluxio_amd.fuse.kernel import OP_NAMES
-                res["fuse_ops"] = {OP_NAMES.get(k, str(k)): v for k, v in sorted(srv.op_counts.items())}
+                res["fuse_ops"] = srv.op_stats()
             finally:
                 srv.unmount()
             ufs_dir = c.master.fs_master.mount_table.resolve("/ds").uri
@@ -116,6 +166,8 @@ def main(argv=None) -> int:
             fs.close()
     finally:
         shutil.rmtree(work, ignore_errors=True)
+        if tier != "dram":
+            shutil.rmtree(tier, ignore_errors=True)
     print(json.dumps(res))
     if a.out:
         with open(a.out, "w") as f:

@@ -86,6 +86,9 @@ def main(argv=None) -> int:
                                    capture_output=True, text=True, timeout=600)
                 line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
                 if line is None:
+                    print(f"client process ({transport}, {t} threads) exited rc={p.returncode} without a result",
+                          file=sys.stderr)
+                    print(p.stdout[-2000:], file=sys.stderr)
                     print(p.stderr[-3000:], file=sys.stderr)
                     return 1
                 r = json.loads(line[7:])
