@@ -29,7 +29,9 @@ DevicePageCache::DevicePageCache(int device, uint64_t capacity_bytes, uint64_t p
   const uint64_t n = capacity_bytes / page_size;
   if (n == 0 || n > (1u << 30)) throw StoreError(kErrInvalidArgument, "cache must hold 1..2^30 pages");
   nslots_ = (uint32_t)n;
-  table_h_.assign(next_pow2(2 * n), PageTableEntry{kPageKeyEmpty, -1, 0});
+  // 4x the slots: a device put of a whole cache's worth of fresh keys claims its entries while the
+  // pages it replaces still hold theirs, and the load must stay <= 1/2 through that batch
+  table_h_.assign(next_pow2(4 * n), PageTableEntry{kPageKeyEmpty, -1, 0});
   dirty_flag_.assign(table_h_.size(), 0);
   slot_key_.assign(nslots_, kPageKeyEmpty);
   stamp_h_.assign(nslots_, 0);
@@ -720,7 +722,7 @@ std::vector<uint64_t> DevicePageCache::put_device_locked(const uint64_t* keys_d,
   PC_HIP_OK(launch_page_put_assign(a, s));
   PC_HIP_OK(launch_page_put_fill(a, s));
   // tombstones piling up: rebuild the table on the device, in the same stream order
-  const bool rebuild = tombstones_ + n > table_h_.size() / 4;
+  const bool rebuild = tombstones_ + n > table_h_.size() / 8;
   if (rebuild) {
     PC_HIP_OK(launch_page_table_rebuild(a, table2_d_, s));
     std::swap(table_d_, table2_d_);

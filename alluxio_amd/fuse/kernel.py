@@ -19,6 +19,10 @@ native BlockStore -- the worker-embedded FUSE deployment) read-locks the blocks 
 FLUSH and RELEASE of such handles never reach Python (READ replies gather straight from the DRAM
 arena with writev, or D2H-copy from HBM).  Everything else -- mutations, misses, files not cached
 locally -- is queued to Python handler threads.  Mutations invalidate the cached attributes.
+A LOOKUP miss lists the parent directory once (decoded natively into the cache), OPENDIR does the
+same, and READDIRPLUS gives the kernel every entry of a listed directory at once.  ``read_only``
+(``-o ro``) negotiates zero-message opens (no OPEN/RELEASE per file); ``passthrough`` hands the
+kernel the block file of a single-block file held in a file tier (tmpfs) so its reads bypass us.
 
 Kernel page cache (``keep_cache``): ``"auto"`` (default) keeps it across opens only while the
 file's Alluxio file id is unchanged (files are write-once; a re-created path gets a new id),
@@ -43,7 +47,7 @@ LOOKUP, FORGET, GETATTR, SETATTR = 1, 2, 3, 4
 MKDIR, UNLINK, RMDIR, RENAME = 9, 10, 11, 12
 OPEN, READ, WRITE, STATFS, RELEASE, FSYNC = 14, 15, 16, 17, 18, 20
 GETXATTR, LISTXATTR, FLUSH, INIT, OPENDIR, READDIR, RELEASEDIR, FSYNCDIR = 22, 23, 25, 26, 27, 28, 29, 30
-ACCESS, CREATE, INTERRUPT, DESTROY, BATCH_FORGET, RENAME2 = 34, 35, 36, 38, 42, 45
+ACCESS, CREATE, INTERRUPT, DESTROY, BATCH_FORGET, READDIRPLUS, RENAME2 = 34, 35, 36, 38, 42, 44, 45
 
 IOCTL = 39
 OP_NAMES = {LOOKUP: "LOOKUP", FORGET: "FORGET", GETATTR: "GETATTR", SETATTR: "SETATTR", MKDIR: "MKDIR",
@@ -51,7 +55,7 @@ OP_NAMES = {LOOKUP: "LOOKUP", FORGET: "FORGET", GETATTR: "GETATTR", SETATTR: "SE
             STATFS: "STATFS", RELEASE: "RELEASE", FSYNC: "FSYNC", GETXATTR: "GETXATTR", LISTXATTR: "LISTXATTR",
             FLUSH: "FLUSH", INIT: "INIT", OPENDIR: "OPENDIR", READDIR: "READDIR", RELEASEDIR: "RELEASEDIR",
             FSYNCDIR: "FSYNCDIR", ACCESS: "ACCESS", CREATE: "CREATE", INTERRUPT: "INTERRUPT", IOCTL: "IOCTL",
-            DESTROY: "DESTROY", BATCH_FORGET: "BATCH_FORGET", RENAME2: "RENAME2"}
+            DESTROY: "DESTROY", BATCH_FORGET: "BATCH_FORGET", READDIRPLUS: "READDIRPLUS", RENAME2: "RENAME2"}
 
 IN_HDR = struct.Struct("<IIQQIIII")            # len opcode unique nodeid uid gid pid padding
 OUT_HDR = struct.Struct("<IiQ")                # len error unique
@@ -66,12 +70,14 @@ WRITE_IN = struct.Struct("<QQIIQII")
 SETATTR_IN = struct.Struct("<IIQQQQQQIIIIIIII")
 KSTATFS = struct.Struct("<QQQQQIIII24x")
 DIRENT = struct.Struct("<QQII")
+ENTRY_OUT_SIZE = 40 + 88                       # fuse_entry_out: ENTRY_HEAD + fuse_attr
 
 FATTR_MODE, FATTR_UID, FATTR_GID, FATTR_SIZE = 1 << 0, 1 << 1, 1 << 2, 1 << 3
 FATTR_ATIME, FATTR_MTIME = 1 << 4, 1 << 5
 FUSE_ASYNC_READ, FUSE_ATOMIC_O_TRUNC, FUSE_BIG_WRITES = 1 << 0, 1 << 3, 1 << 5
 FUSE_AUTO_INVAL_DATA, FUSE_NO_OPEN_SUPPORT, FUSE_INIT_EXT = 1 << 12, 1 << 17, 1 << 30
 FUSE_PASSTHROUGH_HI = 1 << (37 - 32)           # FUSE_PASSTHROUGH, in flags2
+FUSE_DO_READDIRPLUS, FUSE_READDIRPLUS_AUTO = 1 << 13, 1 << 14
 FOPEN_KEEP_CACHE = 1 << 1
 MS_RDONLY, MS_NOSUID, MS_NODEV = 1, 2, 4
 MNT_DETACH = 2
@@ -120,6 +126,7 @@ class FuseKernelServer:
         self._ids = {"/": ROOT_ID}                   # path -> node id
         self._next_id = ROOT_ID + 1
         self._dirs: dict[int, list] = {}             # opendir handle -> [(name, mode)]
+        self._dir_paths: dict[int, str] = {}         # opendir handle -> directory path
         self._next_dir = 1
         self._stop = threading.Event()
         self.requests = 0
@@ -466,6 +473,10 @@ class FuseKernelServer:
             if major != 7:
                 raise FuseOSError(errno.EPROTO)
             want = FUSE_ASYNC_READ | FUSE_ATOMIC_O_TRUNC | FUSE_BIG_WRITES
+            if self._srv is not None:
+                # a listed directory hands the kernel every child's entry + attributes at once
+                # (dataset scans such as ImageFolder's): those files need no LOOKUP afterwards
+                want |= FUSE_DO_READDIRPLUS | FUSE_READDIRPLUS_AUTO
             if self.read_only and self._srv is not None:
                 # zero-message opens (no OPEN/RELEASE per file) + page cache dropped whenever a
                 # refreshed attribute shows another mtime/size (a replaced file)
@@ -611,6 +622,7 @@ class FuseKernelServer:
                 h = self._next_dir
                 self._next_dir += 1
                 self._dirs[h] = entries
+                self._dir_paths[h] = path
             return OPEN_OUT.pack(h, 0, 0)
         if op == READDIR:
             fh, offset, size = READ_IN.unpack_from(body)[:3]
@@ -628,10 +640,36 @@ class FuseKernelServer:
                     break
                 out += DIRENT.pack(0xFFFFFFFF, i + 1, len(nb), (mode & 0o170000) >> 12) + nb + b"\0" * (rec_pad - rec)
             return bytes(out)
+        if op == READDIRPLUS:
+            fh, offset, size = READ_IN.unpack_from(body)[:3]
+            with self._lock:
+                entries = self._dirs.get(fh)
+                parent = self._dir_paths.get(fh)
+            if entries is None:
+                raise FuseOSError(errno.EBADF)
+            out = bytearray()
+            for i in range(offset, len(entries)):
+                name, mode = entries[i]
+                nb = name.encode()
+                rec = ENTRY_OUT_SIZE + DIRENT.size + len(nb)
+                rec_pad = (rec + 7) & ~7
+                if len(out) + rec_pad > size:
+                    break
+                ent = None
+                if name not in (".", "..") and self._srv is not None:
+                    ent = self._srv.entry(self._child(parent, name))     # cached at OPENDIR
+                if ent is None:
+                    ent = bytes(ENTRY_OUT_SIZE)            # nodeid 0: "no entry for this one"
+                    ino = 0xFFFFFFFF
+                else:
+                    ino = struct.unpack_from("<Q", ent)[0]
+                out += ent + DIRENT.pack(ino, i + 1, len(nb), (mode & 0o170000) >> 12) + nb + b"\0" * (rec_pad - rec)
+            return bytes(out)
         if op == RELEASEDIR:
             fh = struct.unpack_from("<Q", body)[0]
             with self._lock:
                 self._dirs.pop(fh, None)
+                self._dir_paths.pop(fh, None)
             return b""
         if op in (GETXATTR, LISTXATTR):
             raise FuseOSError(errno.ENODATA if op == GETXATTR else errno.ENOSYS)

@@ -63,6 +63,13 @@ def _thread_cpu() -> dict:
     return out
 
 
+def _scan(root: str, dirs: int) -> dict:
+    """What torchvision's ImageFolder does before training: list every class directory."""
+    t0 = time.perf_counter()
+    n = sum(len(os.listdir(os.path.join(root, f"d{i:03d}"))) for i in range(dirs))
+    return {"entries": n, "s": round(time.perf_counter() - t0, 3)}
+
+
 def _epochs(paths, epochs, workers, batch, seed=0):
     import torch
     from torch.utils.data import DataLoader, RandomSampler
@@ -103,6 +110,8 @@ def main(argv=None) -> int:
                     help="native: C++ /dev/fuse loop (csrc/fuse_server.cpp); python: the pure-Python loop")
     ap.add_argument("--no-embedded", action="store_true",
                     help="do not hand the worker's block store to the FUSE server (no native opens/reads)")
+    ap.add_argument("--no-scan", action="store_true",
+                    help="skip the ImageFolder-style directory scan before the epochs")
     ap.add_argument("--read-only", action="store_true",
                     help="-o ro mount: with the native server, zero-message opens (no OPEN/RELEASE per file)")
     ap.add_argument("--passthrough", action="store_true",
@@ -149,6 +158,8 @@ def main(argv=None) -> int:
             res["server"] = a.server + ("" if store is None else " (worker-embedded: native open/read)")
             try:
                 paths = [os.path.join(mnt, "ds", r) for r in rel]
+                if not a.no_scan:
+                    res["fuse_scan"] = _scan(os.path.join(mnt, "ds"), a.dirs)
                 res["fuse"] = _epochs(paths, a.epochs, a.workers, a.batch)
                 res["fuse_ops"] = srv.op_stats()
             finally:
@@ -162,6 +173,8 @@ def main(argv=None) -> int:
                 res["ufs_page_cache_dropped"] = True
             except OSError:
                 res["ufs_page_cache_dropped"] = False
+            if not a.no_scan:
+                res["ufs_scan"] = _scan(ufs_dir, a.dirs)
             res["ufs_direct"] = _epochs([os.path.join(ufs_dir, r) for r in rel], a.epochs, a.workers, a.batch)
             fs.close()
     finally:

@@ -76,6 +76,9 @@ for s in $STEPS; do
       run page_cache_put 400 python tools/page_cache_bench.py --page-sizes 4k,64k,2m --out "$OUT/page_cache_put.jsonl"
       run rocprof_pc_put 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pc_put" -o pcput --output-format csv -- python3 tools/page_cache_bench.py --page-sizes 4k --iters 5
       ;;
+    hostipc)
+      run worker_bench_ipc 300 python tools/worker_bench_host.py --threads 16 --transports ipc --duration 4s --warmup 1s --out "$OUT/worker_bench_ipc.jsonl"
+      ;;
     hostread)
       run worker_bench_host 900 python tools/worker_bench_host.py --threads 16,64,256 --duration 8s --warmup 2s --out "$OUT/worker_bench_host.jsonl"
       ;;

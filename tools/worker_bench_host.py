@@ -28,7 +28,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CLIENT = r"""
-import json, sys
+import json, sys, faulthandler
+faulthandler.enable()
 sys.path.insert(0, {root!r})
 from alluxio_amd.client.file_system import FileSystem
 from alluxio_amd.conf import Configuration
