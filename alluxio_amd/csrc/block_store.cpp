@@ -90,6 +90,11 @@ BlockStore::BlockStore(const std::vector<DirSpec>& dirs, int annotator, int allo
     HIP_OK(hipHostMalloc((void**)&host_ring_, sizeof(CopySeg) * kRing * kRingSegs, hipHostMallocDefault));
     HIP_OK(hipMalloc((void**)&dev_ring_, sizeof(CopySeg) * kRing * kRingSegs));
     for (int i = 0; i < kRing; ++i) HIP_OK(hipEventCreateWithFlags(&ring_ev_[i], hipEventDisableTiming));
+    for (auto& d : dirs_) {
+      if (d->spec.kind != DirKind::kDevice || d->free_bits.empty()) continue;
+      HIP_OK(hipMalloc((void**)&d->mag_bits, d->free_bits.size() * 8));
+      HIP_OK(hipMemset(d->mag_bits, 0, d->free_bits.size() * 8));
+    }
   }
 }
 
@@ -107,11 +112,21 @@ BlockStore::~BlockStore() {
     }
     for (void* p : {(void*)d_crf_, (void*)d_last_, (void*)d_fbytes_, (void*)d_dir_, (void*)d_keys_,
                     (void*)d_excl_, (void*)d_ctl_, (void*)d_upd_, (void*)d_bits_, (void*)d_partial_,
-                    (void*)d_claimed_})
+                    (void*)d_claimed_, (void*)d_claim_item_})
       if (p) hipFree(p);
     for (void* p : {(void*)h_excl_, (void*)h_ctl_, (void*)h_out_, (void*)h_pages_, (void*)h_claimed_})
       if (p) hipHostFree(p);
     if (crc_dev_) hipFree(crc_dev_);
+    for (auto& d : dirs_) {
+      if (d->mag_bits) hipFree(d->mag_bits);
+      if (d->mag_upd) hipFree(d->mag_upd);
+    }
+    for (auto& c : claim_) {
+      for (void* p : {(void*)c.items_d, (void*)c.pages_d, (void*)c.got_d})
+        if (p) hipFree(p);
+      for (void* p : {(void*)c.items_h, (void*)c.pages_h, (void*)c.got_h})
+        if (p) hipHostFree(p);
+    }
     if (internal_stream_) hipStreamDestroy(internal_stream_);
   }
 }
@@ -291,22 +306,90 @@ bool BlockStore::grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved, 
       need = 0;
     }
   }
-  // 3) scattered pages
-  for (int64_t w = 0; need > 0 && w < (int64_t)d.free_bits.size(); ++w) {
-    uint64_t word = d.free_bits[w];
-    while (word && need > 0) {
-      const int b0 = __builtin_ctzll(word);
-      const int64_t p = w * 64 + b0;
-      if (p >= d.num_pages) break;
-      bit_take(d.free_bits, p);
-      b.pages.push_back(p);
-      --d.free_pages;
-      --need;
-      word &= word - 1;
+  // 3) scattered pages (the device magazine handed back first when the host pool runs dry)
+  for (int pass = 0; pass < 2 && need > 0; ++pass) {
+    if (pass == 1) {
+      if (d.mag_pages <= 0 || !d.mag_bits) break;
+      mag_drain(d);
+    }
+    for (int64_t w = 0; need > 0 && w < (int64_t)d.free_bits.size(); ++w) {
+      uint64_t word = d.free_bits[w];
+      while (word && need > 0) {
+        const int b0 = __builtin_ctzll(word);
+        const int64_t p = w * 64 + b0;
+        if (p >= d.num_pages) break;
+        bit_take(d.free_bits, p);
+        b.pages.push_back(p);
+        --d.free_pages;
+        --need;
+        word &= word - 1;
+      }
     }
   }
   b.reserved = std::max(b.reserved, new_reserved);
   return need == 0;
+}
+
+// ---- K7 device magazine -----------------------------------------------------------------------
+// Moves >= want free pages (whole host bitmap words at a time: no per-page host work) into the
+// device bitmap (done when this returns).
+void BlockStore::mag_refill(StorageDir& d, int64_t want) {
+  if (!d.mag_bits || want <= 0) return;
+  const int64_t nwords = (int64_t)d.free_bits.size();
+  std::vector<uint64_t> upd;
+  int64_t moved = 0;
+  for (int64_t k = 0; k < nwords && moved < want; ++k) {
+    const int64_t w = (d.mag_cursor + k) % nwords;
+    uint64_t word = d.free_bits[w];
+    if (!word) continue;
+    if ((w + 1) * 64 > d.num_pages) {             // tail word: only real pages
+      const int64_t valid = d.num_pages - w * 64;
+      word &= valid >= 64 ? ~0ull : ((1ull << valid) - 1);
+      if (!word) continue;
+    }
+    d.free_bits[w] &= ~word;
+    upd.push_back((uint64_t)w);
+    upd.push_back(word);
+    moved += __builtin_popcountll(word);
+    d.mag_cursor = (w + 1) % nwords;
+  }
+  if (upd.empty()) return;
+  const size_t n = upd.size() / 2;
+  if (d.mag_upd_cap < upd.size()) {
+    if (d.mag_upd) hipFree(d.mag_upd);
+    d.mag_upd = nullptr;
+    const size_t cap = std::max<size_t>(upd.size(), 1024);
+    HIP_OK(hipMalloc((void**)&d.mag_upd, cap * 8));
+    d.mag_upd_cap = cap;
+  }
+  // on the internal stream, completed before returning: the (pageable) update list is consumed
+  // and any stream claiming afterwards sees the pages
+  HIP_OK(hipMemcpyAsync(d.mag_upd, upd.data(), upd.size() * 8, hipMemcpyHostToDevice, internal_stream_));
+  HIP_OK(launch_mag_fill(d.mag_bits, d.mag_upd, (uint32_t)n, internal_stream_));
+  HIP_OK(hipStreamSynchronize(internal_stream_));
+  d.mag_pages += moved;
+}
+
+// Hands every page left in the magazine back to the host pool (atomic exchange per word, so a
+// claim running concurrently on another stream still owns exactly the bits it won).
+int64_t BlockStore::mag_drain(StorageDir& d) {
+  if (!d.mag_bits) return 0;
+  const uint32_t nwords = (uint32_t)d.free_bits.size();
+  uint64_t* dout = nullptr;
+  HIP_OK(hipMalloc((void**)&dout, (size_t)nwords * 8));
+  std::vector<uint64_t> out(nwords);
+  hipError_t e = launch_mag_drain(d.mag_bits, nwords, dout, internal_stream_);
+  if (e == hipSuccess) e = hipMemcpyAsync(out.data(), dout, (size_t)nwords * 8, hipMemcpyDeviceToHost, internal_stream_);
+  if (e == hipSuccess) e = hipStreamSynchronize(internal_stream_);
+  hipFree(dout);
+  if (e != hipSuccess) throw StoreError(kErrHip, std::string("magazine drain: ") + hipGetErrorString(e));
+  int64_t back = 0;
+  for (uint32_t w = 0; w < nwords; ++w) {
+    d.free_bits[w] |= out[w];
+    back += __builtin_popcountll(out[w]);
+  }
+  d.mag_pages -= back;
+  return back;
 }
 
 void BlockStore::release_storage(BlockMeta& b) {
@@ -1516,24 +1599,15 @@ BlockStore::EvictStats BlockStore::evict_stats() {
 // K7: device page allocation for bulk creates
 std::vector<int64_t> BlockStore::device_alloc_pages(std::unique_lock<std::mutex>& lk, int dir, uint32_t want) {
   StorageDir& d = *dirs_[dir];
+  if (!d.mag_bits || want == 0) return {};
+  // the magazine is refilled by whole host words (no per-page host scan); then one claim
+  // kernel takes the pages with atomics and only the page list comes back
+  if (d.mag_pages < (int64_t)want) mag_refill(d, (int64_t)want - d.mag_pages + std::min<int64_t>(1024, want));
   const uint32_t nwords = (uint32_t)d.free_bits.size();
   std::vector<int64_t> pages;
   {
     std::unique_lock<std::mutex> g(ev_mu_);
     set_device();
-    if (d_bits_cap_ < nwords) {
-      if (d_bits_) hipFree(d_bits_);
-      d_bits_ = nullptr;
-      HIP_OK(hipMalloc((void**)&d_bits_, (size_t)nwords * 8));
-      d_bits_cap_ = nwords;
-    }
-    const uint32_t np = page_alloc_partials(nwords);
-    if (d_partial_cap_ < np) {
-      if (d_partial_) hipFree(d_partial_);
-      d_partial_ = nullptr;
-      HIP_OK(hipMalloc((void**)&d_partial_, (size_t)std::max<uint32_t>(np, 1) * 4));
-      d_partial_cap_ = np;
-    }
     if (h_pages_cap_ < want) {
       if (h_pages_) hipHostFree(h_pages_);
       h_pages_ = nullptr;
@@ -1542,30 +1616,26 @@ std::vector<int64_t> BlockStore::device_alloc_pages(std::unique_lock<std::mutex>
       HIP_OK(hipHostGetDevicePointer((void**)&h_pages_dev_, h_pages_, 0));
       h_pages_cap_ = cap;
     }
-    // snapshot of the authoritative host bitmap (pageable copy: the bytes are taken at the call)
-    std::vector<uint64_t> snap = d.free_bits;
+    if (!d_claim_item_) HIP_OK(hipMalloc((void**)&d_claim_item_, sizeof(ClaimItem)));
+    const ClaimItem item{0, 0, want, 0, 0, 0};
     lk.unlock();
-    hipError_t e = hipMemcpyAsync(d_bits_, snap.data(), (size_t)nwords * 8, hipMemcpyHostToDevice, internal_stream_);
-    if (e == hipSuccess) e = launch_page_alloc(d_bits_, nwords, want, d_partial_, h_pages_dev_, d_claimed_, internal_stream_);
+    hipError_t e = hipMemcpyAsync(d_claim_item_, &item, sizeof(item), hipMemcpyHostToDevice, internal_stream_);
+    if (e == hipSuccess)
+      e = launch_mag_claim_scatter(d.mag_bits, nwords, d_claim_item_, 1, h_pages_dev_, d_claimed_, 0, nullptr, 0,
+                                   internal_stream_);
     if (e == hipSuccess) e = hipMemcpyAsync(h_claimed_, d_claimed_, 4, hipMemcpyDeviceToHost, internal_stream_);
     if (e == hipSuccess) e = hipStreamSynchronize(internal_stream_);
     if (e == hipSuccess) pages.assign(h_pages_, h_pages_ + std::min(*h_claimed_, want));
     g.unlock();
     lk.lock();
-    if (e != hipSuccess) throw StoreError(kErrHip, std::string("device page alloc: ") + hipGetErrorString(e));
+    if (e != hipSuccess) throw StoreError(kErrHip, std::string("device page claim: ") + hipGetErrorString(e));
   }
-  // claim on the host bitmap; pages taken meanwhile by host allocations are dropped
-  std::vector<int64_t> got;
-  got.reserve(pages.size());
-  for (int64_t p : pages)
-    if (p < d.num_pages && bit_free(d.free_bits, p)) {
-      bit_take(d.free_bits, p);
-      --d.free_pages;
-      got.push_back(p);
-    }
+  // magazine pages were never in the host pool: only the counts move
+  d.free_pages -= (int64_t)pages.size();
+  d.mag_pages -= (int64_t)pages.size();
   ++stats_.device_allocs;
-  stats_.device_alloc_pages += got.size();
-  return got;
+  stats_.device_alloc_pages += pages.size();
+  return pages;
 }
 
 std::vector<int64_t> BlockStore::peek_free_pages(int dir, uint32_t want, bool device) {
@@ -1632,7 +1702,8 @@ std::vector<int> BlockStore::create_blocks(int64_t session, const std::vector<in
   if (sd.spec.kind == DirKind::kDevice && use_device_alloc_) {
     uint64_t want = 0;
     for (uint64_t sz : sizes) want += ceil_div(std::max<uint64_t>(sz, 1), sd.spec.page_size);
-    if (want >= device_alloc_min_pages_ && want <= sd.free_pages) pool = device_alloc_pages(lk, d, (uint32_t)want);
+    if (want >= device_alloc_min_pages_ && (int64_t)want <= sd.free_pages - sd.reserved_pages)
+      pool = device_alloc_pages(lk, d, (uint32_t)want);
   }
   for (size_t i = 0; i < ids.size(); ++i) {
     if (blocks_.count(ids[i])) {
@@ -1899,6 +1970,12 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
                                           const std::vector<uint64_t>& lengths, uint64_t staging,
                                           uint64_t staging_bytes, int threads, uint64_t stream) {
   TraceRange trace_("BlockStore.ingest_files");
+  std::lock_guard<std::mutex> ingest_guard(ingest_mu_);
+  for (auto& c : claim_) {                       // nothing of an aborted earlier call carries over
+    c.ids.clear();
+    c.index.clear();
+    c.at.clear();
+  }
   const size_t n = ids.size();
   if (paths.size() != n || offsets.size() != n || lengths.size() != n)
     throw StoreError(kErrInvalidArgument, "ingest_files: argument lengths differ");
@@ -1920,9 +1997,11 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
     i = j;
   }
   std::vector<std::vector<int64_t>> pending(2);   // blocks whose copy from staging half h is in flight
+  std::vector<uint8_t*> host_half(2, nullptr);
   auto finish = [&](int h) {
-    if (pending[h].empty()) return;
+    if (pending[h].empty() && claim_[h].ids.empty()) return;
     if (has_device_) HIP_OK(hipStreamSynchronize(st));
+    if (!claim_[h].ids.empty()) ingest_device_finish(session, h, lengths, host_half[h], status);
     for (int64_t id : pending[h]) commit_block(session, id, false);
     pending[h].clear();
   };
@@ -1931,39 +2010,76 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
     finish(h);                                     // staging half h is free again
     const size_t lo = groups[g].first, hi = groups[g].second;
     uint8_t* base = reinterpret_cast<uint8_t*>(staging) + h * half;
+    host_half[h] = base;
     std::vector<uint64_t> at(hi - lo);
     uint64_t off = 0;
     for (size_t i = lo; i < hi; ++i) { at[i - lo] = off; off += lengths[i]; }
-    // 1) temp blocks (skip ones that exist)
+    // 1) temp blocks (skip ones that exist).  K7: blocks bound for an HBM dir are created without
+    // pages -- the scatter kernel claims them from the dir's device magazine below
     std::vector<int64_t> gid;
     std::vector<uint64_t> gsz;
     std::vector<size_t> gix;
+    int fused_dir = -1;
     {
-      std::lock_guard<std::mutex> g2(mu_);
+      std::unique_lock<std::mutex> g2(mu_);
       for (size_t i = lo; i < hi; ++i) {
         if (blocks_.count(ids[i])) { status[i] = 1; continue; }
         gid.push_back(ids[i]);
         gsz.push_back(lengths[i]);
         gix.push_back(i);
       }
+      if (!gid.empty() && use_device_alloc_ && has_device_) {
+        uint64_t total = 0, want = 0;
+        for (uint64_t sz : gsz) total += std::max<uint64_t>(sz, 1);
+        int d = allocate_dir(0, "", total);
+        if (d < 0) {
+          free_space_locked(g2, session, total, 0, -1, "");
+          d = allocate_dir(0, "", total);
+        }
+        bool fresh = true;
+        for (int64_t id : gid) fresh = fresh && !blocks_.count(id);
+        if (d >= 0 && fresh && dirs_[d]->spec.kind == DirKind::kDevice && dirs_[d]->mag_bits) {
+          StorageDir& sd = *dirs_[d];
+          for (uint64_t sz : gsz) want += ceil_div(std::max<uint64_t>(sz, 1), sd.spec.page_size);
+          if (sd.mag_pages < (int64_t)want) mag_refill(sd, (int64_t)want - sd.mag_pages);
+          for (size_t k = 0; k < gid.size(); ++k) {
+            BlockMeta b;
+            b.id = gid[k];
+            b.dir = d;
+            b.temp = true;
+            b.session = session;
+            b.slot = alloc_slot();
+            b.seq = ++create_seq_;
+            slot_block_[b.slot] = b.id;
+            crf_[b.slot] = 0.f;
+            last_[b.slot] = clock_.load();
+            note_state(b, true);
+            session_temps_[session].insert(b.id);
+            blocks_.emplace(b.id, std::move(b));
+          }
+          fused_dir = d;
+        }
+      }
     }
     if (gid.empty()) continue;
-    try {
-      create_blocks(session, gid, 0, "", gsz, true);
-    } catch (const StoreError&) {
-      // mixed case (a racing creator, or no single dir fits the group): one at a time
-      for (size_t k = 0; k < gid.size(); ++k) {
-        if (has_temp_block(gid[k]) || has_block(gid[k])) {
-          std::lock_guard<std::mutex> g2(mu_);
-          BlockMeta* b = find(gid[k]);
-          if (b && b->temp && b->session == session) continue;   // created by the bulk call
-          status[gix[k]] = 1;
-          continue;
-        }
-        try {
-          create_block(session, gid[k], 0, "", std::max<uint64_t>(gsz[k], 1), true, false);
-        } catch (const StoreError& e) {
-          status[gix[k]] = e.code == kErrAlreadyExists ? 1 : 3;
+    if (fused_dir < 0) {
+      try {
+        create_blocks(session, gid, 0, "", gsz, true);
+      } catch (const StoreError&) {
+        // mixed case (a racing creator, or no single dir fits the group): one at a time
+        for (size_t k = 0; k < gid.size(); ++k) {
+          if (has_temp_block(gid[k]) || has_block(gid[k])) {
+            std::lock_guard<std::mutex> g2(mu_);
+            BlockMeta* b = find(gid[k]);
+            if (b && b->temp && b->session == session) continue;   // created by the bulk call
+            status[gix[k]] = 1;
+            continue;
+          }
+          try {
+            create_block(session, gid[k], 0, "", std::max<uint64_t>(gsz[k], 1), true, false);
+          } catch (const StoreError& e) {
+            status[gix[k]] = e.code == kErrAlreadyExists ? 1 : 3;
+          }
         }
       }
     }
@@ -1990,6 +2106,10 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
     for (int t = 1; t < nt; ++t) pool.emplace_back(reader);
     reader();
     for (auto& t : pool) t.join();
+    for (size_t k = 0; k < gix.size(); ++k)
+      if (status[gix[k]] == 2) {
+        try { abort_block(session, ids[gix[k]]); } catch (const StoreError&) {}
+      }
     // 3) copies into the blocks (async); commit once the half's copies are done.  Blocks in an
     // HBM dir: the used span of the half goes up in ONE DMA to a device staging buffer and one
     // batched-copy launch scatters it into the blocks' pages (one 128 KiB DMA per block runs
@@ -2001,14 +2121,11 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
         const size_t i = gix[k];
         if (status[i] != 0) continue;
         BlockMeta* b = find(ids[i]);
-        const bool dev = b && has_device_ && dirs_[b->dir]->spec.kind == DirKind::kDevice && b->reserved >= lengths[i];
+        const bool dev = b && has_device_ && dirs_[b->dir]->spec.kind == DirKind::kDevice &&
+                         (fused_dir >= 0 || b->reserved >= lengths[i]);
         (dev ? dev_items : host_items).push_back(i);
       }
     }
-    for (size_t k = 0; k < gix.size(); ++k)
-      if (status[gix[k]] == 2) {
-        try { abort_block(session, ids[gix[k]]); } catch (const StoreError&) {}
-      }
     if (!dev_items.empty()) {
       if (ingest_dev_cap_ < staging_bytes) {
         HIP_OK(hipStreamSynchronize(st));
@@ -2019,17 +2136,22 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
       }
       uint8_t* dbase = reinterpret_cast<uint8_t*>(ingest_dev_) + h * half;
       HIP_OK(hipMemcpyAsync(dbase, base, off, hipMemcpyHostToDevice, st));
-      std::vector<CopySeg> segs;
-      {
-        std::lock_guard<std::mutex> g2(mu_);
-        for (size_t i : dev_items) {
-          BlockMeta* b = find(ids[i]);
-          b->length = std::max(b->length, lengths[i]);
-          plan_block_range(*b, 0, lengths[i], (uint64_t)(dbase + at[i - lo]), (int)MemKind::kDevice, true, segs, st);
-          pending[h].push_back(ids[i]);
+      if (fused_dir >= 0) {
+        ingest_device_group(session, ids, lengths, dev_items, at, lo, dbase, h, st, pending[h]);
+        claim_[h].dir = fused_dir;
+      } else {
+        std::vector<CopySeg> segs;
+        {
+          std::lock_guard<std::mutex> g2(mu_);
+          for (size_t i : dev_items) {
+            BlockMeta* b = find(ids[i]);
+            b->length = std::max(b->length, lengths[i]);
+            plan_block_range(*b, 0, lengths[i], (uint64_t)(dbase + at[i - lo]), (int)MemKind::kDevice, true, segs, st);
+            pending[h].push_back(ids[i]);
+          }
         }
+        if (!segs.empty()) copy_segments(segs, st);
       }
-      if (!segs.empty()) copy_segments(segs, st);
     }
     for (size_t i : host_items) {
       try {
@@ -2044,6 +2166,127 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
   finish(0);
   finish(1);
   return status;
+}
+
+void BlockStore::claim_reserve(ClaimScratch& c, size_t items, size_t pages) {
+  if (c.items_cap < items) {
+    if (c.items_d) hipFree(c.items_d);
+    if (c.items_h) hipHostFree(c.items_h);
+    if (c.got_d) hipFree(c.got_d);
+    if (c.got_h) hipHostFree(c.got_h);
+    c.items_d = nullptr;
+    c.items_h = nullptr;
+    c.got_d = nullptr;
+    c.got_h = nullptr;
+    const size_t cap = std::max<size_t>(items, 1024);
+    HIP_OK(hipMalloc((void**)&c.items_d, cap * sizeof(ClaimItem)));
+    HIP_OK(hipHostMalloc((void**)&c.items_h, cap * sizeof(ClaimItem), hipHostMallocDefault));
+    HIP_OK(hipMalloc((void**)&c.got_d, cap * sizeof(uint32_t)));
+    HIP_OK(hipHostMalloc((void**)&c.got_h, cap * sizeof(uint32_t), hipHostMallocDefault));
+    c.items_cap = cap;
+  }
+  if (c.pages_cap < pages) {
+    if (c.pages_d) hipFree(c.pages_d);
+    if (c.pages_h) hipHostFree(c.pages_h);
+    c.pages_d = nullptr;
+    c.pages_h = nullptr;
+    const size_t cap = std::max<size_t>(pages, 4096);
+    HIP_OK(hipMalloc((void**)&c.pages_d, cap * sizeof(int64_t)));
+    HIP_OK(hipHostMalloc((void**)&c.pages_h, cap * sizeof(int64_t), hipHostMallocDefault));
+    c.pages_cap = cap;
+  }
+}
+
+// K7 fused path of ingest_files for one staging half: one item per block (device source, length,
+// pages wanted); the claim kernel takes the pages from the dir's magazine and the scatter kernel
+// copies each block into them -- no per-page host descriptors, no host bitmap scan.  The page
+// lists come back with the half's other results (ingest_device_finish).
+bool BlockStore::ingest_device_group(int64_t session, const std::vector<int64_t>& ids,
+                                     const std::vector<uint64_t>& lengths, const std::vector<size_t>& items,
+                                     const std::vector<uint64_t>& at, size_t lo, uint8_t* dbase, int h,
+                                     hipStream_t st, std::vector<int64_t>& pending) {
+  (void)session;
+  ClaimScratch& c = claim_[h];
+  uint64_t ps = 0;
+  int d = -1;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    BlockMeta* b = find(ids[items[0]]);
+    d = b->dir;
+    ps = dirs_[d]->spec.page_size;
+  }
+  size_t npages = 0, nchunks = 0;
+  for (size_t i : items) {
+    npages += (size_t)ceil_div(std::max<uint64_t>(lengths[i], 1), ps);
+    nchunks += (size_t)ceil_div(std::max<uint64_t>(lengths[i], 1), 64 * 1024);
+  }
+  claim_reserve(c, items.size(), npages);
+  c.ids.clear();
+  c.index.clear();
+  c.at.clear();
+  uint32_t pb = 0, cb = 0;
+  for (size_t k = 0; k < items.size(); ++k) {
+    const size_t i = items[k];
+    const uint64_t len = std::max<uint64_t>(lengths[i], 1);
+    const uint32_t want = (uint32_t)ceil_div(len, ps);
+    c.items_h[k] = ClaimItem{(uint64_t)(dbase + at[i - lo]), lengths[i], want, pb, cb, 0};
+    pb += want;
+    cb += (uint32_t)ceil_div(len, 64 * 1024);
+    c.ids.push_back(ids[i]);
+    c.index.push_back(i);
+    c.at.push_back(at[i - lo]);
+  }
+  const uint32_t nwords = (uint32_t)dirs_[d]->free_bits.size();
+  HIP_OK(hipMemcpyAsync(c.items_d, c.items_h, items.size() * sizeof(ClaimItem), hipMemcpyHostToDevice, st));
+  HIP_OK(launch_mag_claim_scatter(dirs_[d]->mag_bits, nwords, c.items_d, (uint32_t)items.size(), c.pages_d, c.got_d,
+                                  (uint32_t)nchunks, reinterpret_cast<uint8_t*>(dirs_[d]->spec.base), ps, st));
+  HIP_OK(hipMemcpyAsync(c.pages_h, c.pages_d, npages * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(c.got_h, c.got_d, items.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  for (int64_t id : c.ids) pending.push_back(id);
+  return true;
+}
+
+// After the half's stream work completed: attach the claimed pages to their blocks.  A block
+// that came up short (magazine drained meanwhile) gives its pages to the host pool and is
+// written the host way from the still-intact staging half.
+void BlockStore::ingest_device_finish(int64_t session, int h, const std::vector<uint64_t>& lengths,
+                                      const uint8_t* host_base, std::vector<int>& status) {
+  ClaimScratch& c = claim_[h];
+  std::vector<size_t> redo;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    StorageDir& d = *dirs_[c.dir];
+    const uint64_t ps = d.spec.page_size;
+    for (size_t k = 0; k < c.ids.size(); ++k) {
+      const ClaimItem& it = c.items_h[k];
+      const uint32_t got = c.got_h[k];
+      BlockMeta* b = find(c.ids[k]);
+      d.mag_pages -= got;                        // these left the magazine either way
+      if (!b || got < it.want) {
+        for (uint32_t j = 0; j < got; ++j) bit_give(d.free_bits, c.pages_h[it.page_base + j]);
+        if (b) redo.push_back(k);
+        continue;
+      }
+      b->pages.assign(c.pages_h + it.page_base, c.pages_h + it.page_base + it.want);
+      b->reserved = (uint64_t)it.want * ps;
+      b->length = std::max(b->length, lengths[c.index[k]]);
+      d.free_pages -= it.want;
+      ++stats_.device_allocs;
+      stats_.device_alloc_pages += it.want;
+    }
+  }
+  for (size_t k : redo) {
+    const size_t i = c.index[k];
+    try {
+      write(session, c.ids[k], 0, (uint64_t)(host_base + c.at[k]), lengths[i], (int)MemKind::kHost, 0, true);
+    } catch (const StoreError&) {
+      status[i] = 3;
+      try { abort_block(session, c.ids[k]); } catch (const StoreError&) {}
+    }
+  }
+  c.ids.clear();
+  c.index.clear();
+  c.at.clear();
 }
 
 }  // namespace amdx

@@ -73,8 +73,15 @@ struct StorageDir {
   DirSpec spec;
   int index = 0;  // global dir index
   int64_t num_pages = 0;
-  std::vector<uint64_t> free_bits;  // arena kinds: 1 = free
-  int64_t free_pages = 0;
+  std::vector<uint64_t> free_bits;  // arena kinds: 1 = free (host pool)
+  int64_t free_pages = 0;           // free pages: host pool + device magazine
+  // K7 device magazine of an HBM dir: free pages handed to the GPU (device-resident bitmap,
+  // claimed by kernels with atomics), refilled by whole host words, drained only on demand
+  uint64_t* mag_bits = nullptr;
+  int64_t mag_pages = 0;            // pages in the magazine (refills - claims - drains)
+  int64_t mag_cursor = 0;           // next host word a refill looks at
+  uint64_t* mag_upd = nullptr;      // device staging of refill updates (word, bits) pairs
+  size_t mag_upd_cap = 0;
   int64_t reserved_pages = 0;       // kept free for tier management (align/promote swaps)
   uint64_t file_used = 0;  // file dirs: bytes reserved
   uint64_t committed_bytes = 0;
@@ -285,6 +292,13 @@ class BlockStore {
   EvictState dev_state(uint64_t now) const;
   bool device_evict_active() const { return has_device_ && use_device_evict_; }
   std::vector<int64_t> device_alloc_pages(std::unique_lock<std::mutex>& lk, int dir, uint32_t want);
+  void mag_refill(StorageDir& d, int64_t want);                    // mu_ held
+  int64_t mag_drain(StorageDir& d);                                 // mu_ held
+  bool ingest_device_group(int64_t session, const std::vector<int64_t>& ids, const std::vector<uint64_t>& lengths,
+                           const std::vector<size_t>& items, const std::vector<uint64_t>& at, size_t lo,
+                           uint8_t* dbase, int h, hipStream_t st, std::vector<int64_t>& pending);
+  void ingest_device_finish(int64_t session, int h, const std::vector<uint64_t>& lengths, const uint8_t* host_base,
+                            std::vector<int>& status);
   uint32_t alloc_slot();
   void touch_slot(uint32_t slot);
   bool evictable(const BlockMeta& b) const;
@@ -335,9 +349,9 @@ class BlockStore {
   bool use_device_evict_ = true;
   // K7 measured slower than the host bitmap scan end to end (profiles/r2_evict_bench.jsonl):
   // off unless alluxio.worker.hbm.device.alloc.enabled
-  bool use_device_alloc_ = false;
+  bool use_device_alloc_ = true;
   bool demote_on_evict_ = false;
-  uint32_t device_alloc_min_pages_ = 64;
+  uint32_t device_alloc_min_pages_ = 1024;     // create_blocks: device claims from this many pages
   hipStream_t internal_stream_ = nullptr;
   static constexpr int kRing = 8;
   static constexpr int kRingSegs = 8192;
@@ -374,6 +388,7 @@ class BlockStore {
   int64_t* h_pages_dev_ = nullptr;
   size_t h_pages_cap_ = 0;
   uint32_t* h_claimed_ = nullptr;
+  ClaimItem* d_claim_item_ = nullptr;
   uint32_t* d_claimed_ = nullptr;
   std::mutex ev_mu_;                 // device selection / allocation scratch (taken after mu_)
   // checksum scratch
@@ -382,6 +397,22 @@ class BlockStore {
   // device staging of ingest_files (mirror of the caller's pinned staging)
   void* ingest_dev_ = nullptr;
   uint64_t ingest_dev_cap_ = 0;
+  std::mutex ingest_mu_;             // one ingest_files at a time (staging + claim scratch)
+  // K7 fused claim + scatter of ingest_files, one scratch set per staging half
+  struct ClaimScratch {
+    ClaimItem* items_h = nullptr;    // pinned
+    ClaimItem* items_d = nullptr;
+    int64_t* pages_h = nullptr;      // pinned
+    int64_t* pages_d = nullptr;
+    uint32_t* got_h = nullptr;       // pinned
+    uint32_t* got_d = nullptr;
+    size_t items_cap = 0, pages_cap = 0;
+    int dir = -1;
+    std::vector<int64_t> ids;        // blocks of the in-flight group, item order
+    std::vector<size_t> index;       // their positions in the caller's arrays
+    std::vector<uint64_t> at;        // their offsets in the host staging half
+  } claim_[2];
+  void claim_reserve(ClaimScratch& c, size_t items, size_t pages);
 };
 
 // Many concurrent sequential readers of one file, advanced in lockstep: the native form of

@@ -24,6 +24,8 @@
 
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace amdx {
 
 namespace {
@@ -329,7 +331,145 @@ __global__ __launch_bounds__(kPaBlock) void palloc_emit_kernel(uint64_t* __restr
   atomicAdd(claimed, (uint32_t)__popcll(taken));
 }
 
+// ---- K7 device page magazine ---------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mag_fill_kernel(uint64_t* __restrict__ bits, const uint64_t* __restrict__ upd,
+                                                       uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    atomicOr((unsigned long long*)&bits[upd[2 * i]], (unsigned long long)upd[2 * i + 1]);
+}
+
+__global__ __launch_bounds__(256) void mag_drain_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
+                                                        uint64_t* __restrict__ out) {
+  for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x)
+    out[w] = atomicExch((unsigned long long*)&bits[w], 0ull);
+}
+
+// lowest k set bits of x
+__device__ __forceinline__ uint64_t low_bits(uint64_t x, uint32_t k) {
+  uint64_t m = 0;
+  for (uint32_t j = 0; j < k && x; ++j) {
+    const uint64_t b = x & (~x + 1ull);
+    m |= b;
+    x ^= b;
+  }
+  return m;
+}
+
+// One wave per item: windows of 64 words (one per lane) starting at a per-item offset (spreads
+// concurrent items over the bitmap); each lane takes up to its share of the item's remaining
+// need from its word with one atomicAnd and keeps the bits it actually won.
+__global__ __launch_bounds__(256) void mag_claim_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
+                                                        const ClaimItem* __restrict__ items, uint32_t nitems,
+                                                        int64_t* __restrict__ pages_out, uint32_t* __restrict__ got) {
+  const uint32_t lane = lane_id();
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); it < nitems; it += nw) {
+    const ClaimItem item = items[it];
+    uint32_t have = 0;
+    const uint32_t start = (uint32_t)(((uint64_t)it * 0x9E3779B1u) % nwords);
+    for (uint32_t win = 0; win < nwords && have < item.want; win += 64) {
+      const uint32_t w = (start + win + lane) % nwords;
+      const bool valid = win + lane < nwords;
+      const uint64_t word = valid ? __hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      const uint32_t free_n = (uint32_t)__popcll(word);
+      // exclusive prefix of free counts over the lanes
+      uint32_t incl = free_n;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if ((int)lane >= o) incl += v;
+      }
+      const uint32_t excl = incl - free_n;
+      const uint32_t left = item.want - have;
+      const uint32_t take = excl >= left ? 0u : min(free_n, left - excl);
+      uint64_t won = 0;
+      if (take) {
+        const uint64_t mask = low_bits(word, take);
+        const uint64_t old = atomicAnd((unsigned long long*)&bits[w], ~(unsigned long long)mask);
+        won = old & mask;                          // bits another claimer took first are not ours
+      }
+      const uint32_t wn = (uint32_t)__popcll(won);
+      uint32_t wincl = wn;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(wincl, o, 64);
+        if ((int)lane >= o) wincl += v;
+      }
+      uint32_t pos = item.page_base + have + wincl - wn;
+      for (uint64_t r = won; r; r &= r - 1) pages_out[pos++] = (int64_t)w * 64 + __builtin_ctzll(r);
+      have += __shfl(wincl, 63, 64);
+    }
+    if (lane == 0) got[it] = have;
+  }
+}
+
+constexpr uint64_t kMagChunk = 64 * 1024;
+
+// One wave per 64 KiB chunk: item found by binary search over chunk_base.
+__global__ __launch_bounds__(256) void mag_scatter_kernel(const ClaimItem* __restrict__ items, uint32_t nitems,
+                                                          uint32_t total_chunks, const int64_t* __restrict__ pages,
+                                                          const uint32_t* __restrict__ got, uint8_t* __restrict__ arena,
+                                                          uint64_t page_size) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t lane = lane_id();
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < total_chunks; c += nw) {
+    uint32_t lo = 0, hi = nitems;                  // last item with chunk_base <= c
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (items[mid].chunk_base <= c) lo = mid; else hi = mid;
+    }
+    const ClaimItem item = items[lo];
+    if (got[lo] < item.want || item.src == 0) continue;
+    const uint64_t off = (uint64_t)(c - item.chunk_base) * kMagChunk;
+    if (off >= item.len) continue;
+    const uint64_t end = min(item.len, off + kMagChunk);
+    for (uint64_t pos = off; pos < end;) {         // a chunk may straddle a page boundary
+      const uint64_t pi = pos / page_size, po = pos % page_size;
+      const uint64_t n = min(end - pos, page_size - po);
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(item.src) + pos;
+      uint8_t* dst = arena + (uint64_t)pages[item.page_base + pi] * page_size + po;
+      if ((((uint64_t)src | (uint64_t)dst | n) & 15) == 0) {
+        const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+        u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+        for (uint64_t v = lane; v < (n >> 4); v += 64) d4[v] = s4[v];
+      } else {
+        for (uint64_t b = lane; b < n; b += 64) dst[b] = src[b];
+      }
+      pos += n;
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_mag_fill(uint64_t* bits, const uint64_t* upd, uint32_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<uint32_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(mag_fill_kernel, dim3(grid), dim3(256), 0, stream, bits, upd, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_mag_drain(uint64_t* bits, uint32_t nwords, uint64_t* out, hipStream_t stream) {
+  if (nwords == 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<uint32_t>((nwords + 255) / 256, 1024);
+  hipLaunchKernelGGL(mag_drain_kernel, dim3(grid), dim3(256), 0, stream, bits, nwords, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_mag_claim_scatter(uint64_t* bits, uint32_t nwords, const ClaimItem* items, uint32_t nitems,
+                                    int64_t* pages_out, uint32_t* got, uint32_t total_chunks, uint8_t* arena,
+                                    uint64_t page_size, hipStream_t stream) {
+  if (nitems == 0 || nwords == 0) return hipSuccess;
+  const unsigned cgrid = (unsigned)std::min<uint32_t>((nitems + 3) / 4, 4096);
+  hipLaunchKernelGGL(mag_claim_kernel, dim3(cgrid), dim3(256), 0, stream, bits, nwords, items, nitems, pages_out, got);
+  if (total_chunks) {
+    const unsigned sgrid = (unsigned)std::min<uint32_t>((total_chunks + 3) / 4, 16384);
+    hipLaunchKernelGGL(mag_scatter_kernel, dim3(sgrid), dim3(256), 0, stream, items, nitems, total_chunks, pages_out,
+                       got, arena, page_size);
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_slot_update(const EvictState& st, const SlotUpdate* upd, uint32_t n, hipStream_t stream) {
   if (n == 0) return hipSuccess;

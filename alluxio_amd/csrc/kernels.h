@@ -144,6 +144,29 @@ hipError_t launch_page_alloc(uint64_t* bits, uint32_t nwords, uint32_t want, uin
                              int64_t* pages_out, uint32_t* claimed, hipStream_t stream);
 uint32_t page_alloc_partials(uint32_t nwords);
 
+// K7 device page magazine (evict_alloc.hip): an HBM dir keeps a device-resident bitmap of free
+// pages it handed to the device ("magazine"); kernels claim pages from it with atomics, the host
+// refills it by whole bitmap words and drains it back only when its own pool runs dry.
+struct ClaimItem {
+  uint64_t src;          // device source of the item's bytes (scatter) or 0 (claim only)
+  uint64_t len;          // bytes
+  uint32_t want;         // pages to claim
+  uint32_t page_base;    // first index in pages_out
+  uint32_t chunk_base;   // first 64 KiB chunk of this item in the scatter grid
+  uint32_t pad;
+};
+// bits[upd[2i]] |= upd[2i+1] (atomic): pages moved into the magazine
+hipError_t launch_mag_fill(uint64_t* bits, const uint64_t* upd, uint32_t n, hipStream_t stream);
+// out[w] = atomicExch(bits[w], 0): the magazine handed back (no claim can race it)
+hipError_t launch_mag_drain(uint64_t* bits, uint32_t nwords, uint64_t* out, hipStream_t stream);
+// One wave per item claims item.want pages (atomicAnd on the words, ballot/popcount ranking)
+// into pages_out[page_base ...]; got[i] = pages claimed (< want when the magazine ran dry).
+// When total_chunks > 0 a second launch copies each item's bytes into its claimed pages (one
+// wave per 64 KiB chunk; items that came up short are skipped -- the host finishes them).
+hipError_t launch_mag_claim_scatter(uint64_t* bits, uint32_t nwords, const ClaimItem* items, uint32_t nitems,
+                                    int64_t* pages_out, uint32_t* got, uint32_t total_chunks, uint8_t* arena,
+                                    uint64_t page_size, hipStream_t stream);
+
 // K9: client page cache lookup.  Open-addressing (linear probing) table of page keys in HBM;
 // `key` = (interned file id << 24) | page index, so keys are exact (no hash collisions to
 // verify).  Empty slots hold kPageKeyEmpty, erased ones kPageKeyTomb (probing continues).

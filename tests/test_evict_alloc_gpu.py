@@ -226,3 +226,58 @@ def test_bulk_ingest_into_hbm_and_gathered_crc(gpu, tmp_path):
     for b, d, (_, c) in zip(ids, datas, crcs):
         assert c == s.checksum(b, 0)
         assert c == [C.crc32c(d[o:o + page].tobytes()) for o in range(0, d.nbytes, page)]
+
+
+def test_magazine_ingest_then_host_allocs_keep_pages_disjoint(gpu, tmp_path):
+    """K7 device magazine: ingest_files claims its blocks' pages on the GPU (fused claim + scatter,
+    no host page lists); host allocations then fill the dir, draining the magazine back into the
+    host pool.  Every page ends up owned by exactly one block, the accounting adds up, and the
+    ingested bytes are intact."""
+    import torch
+    C = lib()
+    page = 64 * KB
+    npages = 512
+    s = _device_store(npages, page)
+    rng = np.random.default_rng(11)
+    paths, lens, datas = [], [], []
+    for i in range(150):
+        n = int(rng.integers(1, 2 * page))
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        p = tmp_path / f"m{i}"
+        p.write_bytes(d.tobytes())
+        paths.append(str(p))
+        lens.append(n)
+        datas.append(d)
+    ids = list(range(5000, 5150))
+    staging = torch.empty(4 << 20, dtype=torch.uint8, pin_memory=True)
+    assert s.ingest_files(5, ids, paths, [0] * 150, lens, staging.data_ptr(), staging.numel(), 4, 0) == [0] * 150
+    used = sum((n + page - 1) // page for n in lens)
+    st = s.evict_stats()
+    assert st["device_alloc_pages"] >= used
+    assert s.dir_available(0) == (npages - used) * page
+    # host allocations (one page each) until the dir is full: the magazine is drained on demand
+    b = 9000
+    while True:
+        try:
+            s.create_block(6, b, 0, "", page, False, False)
+        except Exception:
+            break
+        b += 1
+    assert b - 9000 == npages - used and s.dir_available(0) == 0
+    owned = []
+    for blk in ids + list(range(9000, b)):
+        pages = s.block_pages(blk)[0]
+        owned += pages
+    assert len(owned) == npages and sorted(owned) == list(range(npages))
+    out = torch.empty(2 * page, dtype=torch.uint8, device="cuda")
+    for blk, d in zip(ids, datas):
+        s.read_batch([(blk, 0, d.nbytes, out.data_ptr(), 1)], 0, True)
+        assert np.array_equal(out[:d.nbytes].cpu().numpy(), d), blk
+    # freeing returns pages to the host pool; a second ingest claims again through a refill
+    s.cleanup_session(6)
+    assert s.dir_available(0) == (npages - used) * page
+    ids2 = list(range(7000, 7040))
+    assert s.ingest_files(8, ids2, paths[:40], [0] * 40, lens[:40], staging.data_ptr(), staging.numel(), 4, 0) == [0] * 40
+    for blk, d in zip(ids2[::7], datas[:40:7]):
+        s.read_batch([(blk, 0, d.nbytes, out.data_ptr(), 1)], 0, True)
+        assert np.array_equal(out[:d.nbytes].cpu().numpy(), d)

@@ -71,7 +71,43 @@ def run(n: int, iters: int, page: int, policy: int) -> dict:
         out[f"alloc_half_{name}_pages"] = len(p)
     out["bulk_create_ms"] = round(bulk_create_s * 1e3, 2)
     out["stats"] = s.evict_stats()
-    del s, arena
+    del s
+    # K7 on its consumers: bulk create_blocks and ingest_files with the device magazine (claims
+    # by kernels from a resident bitmap) vs the host bitmap scan, each on a fresh store
+    for name, dev in (("device", True), ("host", False)):
+        s = C.BlockStore([d], annotator=policy, alloc_policy=0, lrfu_step=1e-4, device=0)
+        s.set_use_device_alloc(dev, 64)
+        t = time.perf_counter()
+        s.create_blocks(1, ids, 0, "", [page] * n, False)
+        out[f"bulk_create_{name}_ms"] = round((time.perf_counter() - t) * 1e3, 2)
+        del s
+    nf = min(n, 20000)
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        blob = np.random.default_rng(1).integers(0, 256, page, dtype=np.uint8).tobytes()
+        paths = []
+        for i in range(nf):
+            p = os.path.join(tmp, f"f{i}")
+            with open(p, "wb") as f:
+                f.write(blob)
+            paths.append(p)
+        staging = torch.empty(64 << 20, dtype=torch.uint8, pin_memory=True)
+        for name, dev in (("device", True), ("host", False)):
+            s = C.BlockStore([d], annotator=policy, alloc_policy=0, lrfu_step=1e-4, device=0)
+            s.set_use_device_alloc(dev, 64)
+            best = None
+            for r in range(3):
+                fids = list(range(10_000_000 * (r + 1), 10_000_000 * (r + 1) + nf))
+                t = time.perf_counter()
+                stt = s.ingest_files(2, fids, paths, [0] * nf, [page] * nf, staging.data_ptr(), staging.numel(), 8, 0)
+                dt = time.perf_counter() - t
+                assert stt == [0] * nf
+                best = dt if best is None else min(best, dt)
+                for b in fids:
+                    s.remove_block(2, b)
+            out[f"ingest_{nf}_{name}_ms"] = round(best * 1e3, 2)
+            del s
+    del arena
     torch.cuda.synchronize()
     return out
 
