@@ -237,7 +237,10 @@ class IpcBlockReader(BlockReader):
             gather_block(self.h, offset, length, ptr, self.device, stream)
             return
         import ctypes
-        if self.h.arena_kind == "dram" or not has_gpu():
+        if self.h.arena_kind != "dram" and not has_gpu():
+            # an HBM arena's mapping is a device address: never memcpy it on the host
+            raise UnavailableException(f"block {self.block_id}: HBM arena needs a visible GPU")
+        if self.h.arena_kind == "dram":
             # shared host arena -> host buffer: plain memcpy of the page runs
             base = map_handle(self.h, self.device)
             for src, dst, n in page_segments(base, list(self.h.pages), self.h.page_size, offset, length, ptr):

@@ -338,8 +338,9 @@ void BlockStore::mag_refill(StorageDir& d, int64_t want) {
   const int64_t nwords = (int64_t)d.free_bits.size();
   std::vector<uint64_t> upd;
   int64_t moved = 0;
+  const int64_t start = d.mag_cursor;
   for (int64_t k = 0; k < nwords && moved < want; ++k) {
-    const int64_t w = (d.mag_cursor + k) % nwords;
+    const int64_t w = (start + k) % nwords;
     uint64_t word = d.free_bits[w];
     if (!word) continue;
     if ((w + 1) * 64 > d.num_pages) {             // tail word: only real pages
@@ -2001,7 +2002,15 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
   auto finish = [&](int h) {
     if (pending[h].empty() && claim_[h].ids.empty()) return;
     if (has_device_) HIP_OK(hipStreamSynchronize(st));
-    if (!claim_[h].ids.empty()) ingest_device_finish(session, h, lengths, host_half[h], status);
+    if (!claim_[h].ids.empty()) {
+      const std::unordered_set<int64_t> failed = ingest_device_finish(session, h, lengths, host_half[h], status);
+      if (!failed.empty()) {
+        std::vector<int64_t> keep;
+        for (int64_t id : pending[h])
+          if (!failed.count(id)) keep.push_back(id);
+        pending[h].swap(keep);
+      }
+    }
     for (int64_t id : pending[h]) commit_block(session, id, false);
     pending[h].clear();
   };
@@ -2249,10 +2258,11 @@ bool BlockStore::ingest_device_group(int64_t session, const std::vector<int64_t>
 // After the half's stream work completed: attach the claimed pages to their blocks.  A block
 // that came up short (magazine drained meanwhile) gives its pages to the host pool and is
 // written the host way from the still-intact staging half.
-void BlockStore::ingest_device_finish(int64_t session, int h, const std::vector<uint64_t>& lengths,
-                                      const uint8_t* host_base, std::vector<int>& status) {
+std::unordered_set<int64_t> BlockStore::ingest_device_finish(int64_t session, int h, const std::vector<uint64_t>& lengths,
+                                                             const uint8_t* host_base, std::vector<int>& status) {
   ClaimScratch& c = claim_[h];
   std::vector<size_t> redo;
+  std::unordered_set<int64_t> failed;
   {
     std::lock_guard<std::mutex> g(mu_);
     StorageDir& d = *dirs_[c.dir];
@@ -2265,6 +2275,7 @@ void BlockStore::ingest_device_finish(int64_t session, int h, const std::vector<
       if (!b || got < it.want) {
         for (uint32_t j = 0; j < got; ++j) bit_give(d.free_bits, c.pages_h[it.page_base + j]);
         if (b) redo.push_back(k);
+        else failed.insert(c.ids[k]);
         continue;
       }
       b->pages.assign(c.pages_h + it.page_base, c.pages_h + it.page_base + it.want);
@@ -2281,12 +2292,14 @@ void BlockStore::ingest_device_finish(int64_t session, int h, const std::vector<
       write(session, c.ids[k], 0, (uint64_t)(host_base + c.at[k]), lengths[i], (int)MemKind::kHost, 0, true);
     } catch (const StoreError&) {
       status[i] = 3;
+      failed.insert(c.ids[k]);
       try { abort_block(session, c.ids[k]); } catch (const StoreError&) {}
     }
   }
   c.ids.clear();
   c.index.clear();
   c.at.clear();
+  return failed;
 }
 
 }  // namespace amdx

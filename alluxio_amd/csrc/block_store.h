@@ -297,8 +297,8 @@ class BlockStore {
   bool ingest_device_group(int64_t session, const std::vector<int64_t>& ids, const std::vector<uint64_t>& lengths,
                            const std::vector<size_t>& items, const std::vector<uint64_t>& at, size_t lo,
                            uint8_t* dbase, int h, hipStream_t st, std::vector<int64_t>& pending);
-  void ingest_device_finish(int64_t session, int h, const std::vector<uint64_t>& lengths, const uint8_t* host_base,
-                            std::vector<int>& status);
+  std::unordered_set<int64_t> ingest_device_finish(int64_t session, int h, const std::vector<uint64_t>& lengths,
+                                                   const uint8_t* host_base, std::vector<int>& status);
   uint32_t alloc_slot();
   void touch_slot(uint32_t slot);
   bool evictable(const BlockMeta& b) const;

@@ -265,6 +265,11 @@ constexpr int kCrc4Threads = 1024;
 __constant__ uint32_t c_crc11[12][2048];
 __constant__ uint32_t c_shift16k[4][256];          // c -> c * x^(8*16384), byte-sliced
 __constant__ uint32_t c_lane_shift1k[kCrc4Threads];  // x^(128*k), k < 1024
+// v5 (conflict-free replicated slicing-by-4): a lane's 64-B chunks are 64 KiB apart
+constexpr int kCrc5Threads = 1024;
+constexpr uint64_t kCrc5Chunk = 64;
+__constant__ uint32_t c_shift5[4][256];                // c -> c * x^(8*(1024-1)*64), byte-sliced
+__constant__ uint32_t c_lane_shift5[kCrc5Threads];     // x^(8*64*d), d < 1024
 
 static void host_crc_tables(uint32_t tab[8][256], uint32_t x2n[64]) {
   for (uint32_t i = 0; i < 256; ++i) {
@@ -350,6 +355,23 @@ static hipError_t ensure_crc_tables() {
       g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_shift16k), sh16k, sizeof(sh16k));
     if (g_crc_init_err == hipSuccess)
       g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_lane_shift1k), lane1k, sizeof(lane1k));
+    {
+      // v5: skip the other 1023 lanes' chunks = multiply by x^(8 * 1023 * 64)
+      const uint64_t nbits = 8ull * (kCrc5Threads - 1) * kCrc5Chunk;
+      uint32_t k5 = 1u << 31;
+      for (int b = 0; b < 64; ++b)
+        if ((nbits >> b) & 1) k5 = host_gf2_mult(x2n[b], k5);
+      static uint32_t sh5[4][256];
+      for (int b = 0; b < 4; ++b)
+        for (uint32_t i = 0; i < 256; ++i) sh5[b][i] = host_gf2_mult(k5, i << (8 * b));
+      static uint32_t lane5[kCrc5Threads];
+      lane5[0] = 1u << 31;
+      for (int d = 1; d < kCrc5Threads; ++d) lane5[d] = host_gf2_mult(lane5[d - 1], x2n[9]);   // * x^512
+      if (g_crc_init_err == hipSuccess)
+        g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_shift5), sh5, sizeof(sh5));
+      if (g_crc_init_err == hipSuccess)
+        g_crc_init_err = hipMemcpyToSymbol(HIP_SYMBOL(c_lane_shift5), lane5, sizeof(lane5));
+    }
     static uint32_t lane_shift[256];
     lane_shift[0] = 1u << 31;  // x^0
     for (int k = 1; k < 256; ++k) lane_shift[k] = host_gf2_mult(lane_shift[k - 1], x2n[7]);  // * x^128
@@ -728,6 +750,111 @@ __global__ __launch_bounds__(kCrc4Threads) void crc32c_segments_v4_kernel(
   }
 }
 
+// v5: slicing-by-4 over per-lane 64-B chunks with the byte tables replicated 32 times in LDS
+// (entry x of table t, copy r at dword (t*256 + x)*32 + r; lane l reads copy l mod 32), so every
+// ds_read_b32 of a wave hits 32 distinct banks per 32-lane group: the random-index bank conflicts
+// that bound v1-v4 (4.7 extra cycles per LDS read, profiles/r2_crc_kernels.md) are gone.  Lane l
+// owns chunks l, l+1024, ... of a 1 MiB segment (a wave reads 4 KiB contiguous per step); between
+// two of its chunks the running CRC is shifted past the other lanes' bytes with 4 lookups in a
+// small (unreplicated) table, so a chunk costs 64 + 4 lookups.  Lane results are moved to their
+// final positions with one multiply by a precomputed x^(8*64*d) and XOR-reduced.  Produces the
+// same raw (zero-init) segment CRC as v1-v4.
+constexpr uint64_t kCrcSeg5 = 1024 * 1024;
+
+__device__ __forceinline__ uint32_t crc5_step(uint32_t x, const uint32_t* __restrict__ my) {
+  return my[(3 * 256 + (x & 255)) * 32] ^ my[(2 * 256 + ((x >> 8) & 255)) * 32] ^
+         my[(1 * 256 + ((x >> 16) & 255)) * 32] ^ my[(x >> 24) * 32];
+}
+
+__device__ __forceinline__ uint32_t crc5_chunk(uint32_t c, const uint4 v[4], const uint32_t* __restrict__ my) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    c = crc5_step(c ^ v[u].x, my);
+    c = crc5_step(c ^ v[u].y, my);
+    c = crc5_step(c ^ v[u].z, my);
+    c = crc5_step(c ^ v[u].w, my);
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(kCrc5Threads) void crc32c_segments_v5_kernel(
+    const uint8_t* __restrict__ base, uint64_t total_bytes, uint64_t piece_bytes, uint64_t seg_bytes,
+    uint64_t segs_per_piece, uint64_t nsegs, uint32_t* __restrict__ seg_crc) {
+  __shared__ uint32_t t4r[4 * 256 * 32];   // 128 KiB
+  __shared__ uint32_t sh[4][256];
+  __shared__ uint32_t lsh[kCrc5Threads];
+  __shared__ uint32_t part[kCrc5Threads];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 4 * 256 * 32; i += kCrc5Threads) t4r[i] = c_crc_tab[i >> 13][(i >> 5) & 255];
+  for (int i = tid; i < 4 * 256; i += kCrc5Threads) sh[i >> 8][i & 255] = c_shift5[i >> 8][i & 255];
+  lsh[tid] = c_lane_shift5[tid];
+  __syncthreads();
+  const uint32_t* my = t4r + (tid & 31);
+  for (uint64_t g = blockIdx.x; g < nsegs; g += gridDim.x) {
+    const uint64_t piece = g / segs_per_piece;
+    const uint64_t seg_in_piece = g % segs_per_piece;
+    const uint64_t piece_start = piece * piece_bytes;
+    const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
+    const uint64_t seg_start = piece_start + seg_in_piece * seg_bytes;
+    const uint64_t seg_len = std::min(seg_bytes, piece_start + piece_len - seg_start);
+    const uint8_t* seg = base + seg_start;
+    const uint64_t nch = seg_len / kCrc5Chunk;
+    uint32_t c = 0;
+    uint64_t last = ~0ull;
+    if ((((uintptr_t)seg) & 15) == 0) {
+      uint64_t k = tid;
+      uint4 cur[4], nxt[4];
+      if (k < nch) {
+        const uint4* q = reinterpret_cast<const uint4*>(seg + k * kCrc5Chunk);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = q[u];
+      }
+      for (; k < nch; k += kCrc5Threads) {
+        const uint64_t kn = k + kCrc5Threads;
+        if (kn < nch) {                              // next chunk's loads in flight meanwhile
+          const uint4* q = reinterpret_cast<const uint4*>(seg + kn * kCrc5Chunk);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) nxt[u] = q[u];
+        }
+        if (last != ~0ull) c = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+        c = crc5_chunk(c, cur, my);
+        last = k;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+      }
+    } else {
+      for (uint64_t k = tid; k < nch; k += kCrc5Threads) {
+        uint4 v[4];
+        uint8_t* vb = reinterpret_cast<uint8_t*>(v);
+        const uint8_t* q = seg + k * kCrc5Chunk;
+        for (int b = 0; b < 64; ++b) vb[b] = q[b];
+        if (last != ~0ull) c = sh[0][c & 255] ^ sh[1][(c >> 8) & 255] ^ sh[2][(c >> 16) & 255] ^ sh[3][c >> 24];
+        c = crc5_chunk(c, v, my);
+        last = k;
+      }
+    }
+    part[tid] = last != ~0ull ? gf2_mult(lsh[nch - 1 - last], c) : 0u;
+    __syncthreads();
+    for (int s2 = kCrc5Threads / 2; s2 > 0; s2 >>= 1) {
+      if (tid < s2) part[tid] ^= part[tid + s2];
+      __syncthreads();
+    }
+    if (tid == 0) {
+      uint32_t acc = part[0];
+      const uint64_t tail = seg_len - nch * kCrc5Chunk;
+      if (tail) {
+        acc = gf2_mult(xpow8n(tail), acc);
+        uint32_t t = 0;
+        const uint8_t* q = seg + nch * kCrc5Chunk;
+        for (uint64_t b = 0; b < tail; ++b) t = (t >> 8) ^ my[((t ^ q[b]) & 255) * 32];
+        acc ^= t;
+      }
+      seg_crc[g] = acc;
+    }
+    __syncthreads();
+  }
+}
+
 // Gathered pieces (one page of many blocks each, <= kCrcSeg2 bytes): one workgroup per piece,
 // standard CRC32C per piece — the per-page CRCs of a whole batch of freshly cached blocks in
 // one launch instead of one launch + sync per block.
@@ -809,7 +936,8 @@ uint64_t crc32c_scratch_words(uint64_t total_bytes, uint64_t piece_bytes) {
 }
 
 static int g_crc_variant = 3;  // 0: per-lane contiguous strips (v1), 1: interleaved lanes (v2),
-                               // 2: v2 + table lane fold (v3), 3: 11-bit slicing, 1024 threads (v4)
+                               // 2: v2 + table lane fold (v3), 3: 11-bit slicing, 1024 threads (v4),
+                               // 4: replicated conflict-free slicing-by-4 over 64-B chunks (v5)
 
 void set_crc_variant(int v) { g_crc_variant = v; }
 
@@ -820,7 +948,10 @@ hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint6
   hipError_t e = ensure_crc_tables();
   if (e != hipSuccess) return e;
   const uint64_t npieces = (total_bytes + piece_bytes - 1) / piece_bytes;
-  const uint64_t seg = g_crc_variant == 0 ? kCrcSeg : g_crc_variant == 3 ? std::min(kCrcSeg4, piece_bytes) : kCrcSeg2;
+  const uint64_t seg = g_crc_variant == 0   ? kCrcSeg
+                       : g_crc_variant == 3 ? std::min(kCrcSeg4, piece_bytes)
+                       : g_crc_variant == 4 ? std::min(kCrcSeg5, piece_bytes)
+                                            : kCrcSeg2;
   const uint64_t spp = (piece_bytes + seg - 1) / seg;
   const uint64_t nsegs = npieces * spp;
   if (scratch_words < nsegs) return hipErrorInvalidValue;
@@ -837,9 +968,13 @@ hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint6
   } else {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const unsigned g4 = (unsigned)std::min<uint64_t>(nsegs, (uint64_t)cus);   // one 110 KiB-LDS WG per CU
-    hipLaunchKernelGGL(crc32c_segments_v4_kernel, dim3(g4), dim3(kCrc4Threads), 0, stream, base,
-                       total_bytes, piece_bytes, seg, spp, nsegs, scratch);
+    const unsigned g4 = (unsigned)std::min<uint64_t>(nsegs, (uint64_t)cus);   // one >100 KiB-LDS WG per CU
+    if (g_crc_variant == 4)
+      hipLaunchKernelGGL(crc32c_segments_v5_kernel, dim3(g4), dim3(kCrc5Threads), 0, stream, base,
+                         total_bytes, piece_bytes, seg, spp, nsegs, scratch);
+    else
+      hipLaunchKernelGGL(crc32c_segments_v4_kernel, dim3(g4), dim3(kCrc4Threads), 0, stream, base,
+                         total_bytes, piece_bytes, seg, spp, nsegs, scratch);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;

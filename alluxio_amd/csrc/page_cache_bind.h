@@ -1,7 +1,10 @@
 // pybind11 bindings of the K9 HBM client page cache (included by bindings.cpp).
 #pragma once
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
+
+#include <cstring>
 
 #include <string>
 
@@ -27,8 +30,20 @@ inline void bind_page_cache(pybind11::module_& m) {
       .def("put_many", &DevicePageCache::put_many, G(), py::arg("keys"), py::arg("src"),
            py::arg("src_stride"), py::arg("length"), py::arg("src_kind"), py::arg("stream"),
            py::arg("evict"))
-      .def("put_many_device", &DevicePageCache::put_many_device, G(), py::arg("keys"), py::arg("n"), py::arg("src"),
-           py::arg("src_stride"), py::arg("length"), py::arg("src_kind"), py::arg("stream"), py::arg("evict"))
+      .def("put_many_device", [](DevicePageCache& c, uint64_t keys, uint32_t n, uint64_t src, uint64_t stride,
+                                 uint64_t len, int kind, uint64_t stream, bool evict, bool as_array) -> py::object {
+             std::vector<uint64_t> ev;
+             {
+               py::gil_scoped_release rel;
+               ev = c.put_many_device(keys, n, src, stride, len, kind, stream, evict);
+             }
+             if (!as_array) return py::cast(ev);
+             // a whole cache's worth of evicted keys: one memcpy instead of a Python int per key
+             py::array_t<uint64_t> out(ev.size());
+             if (!ev.empty()) std::memcpy(out.mutable_data(), ev.data(), ev.size() * sizeof(uint64_t));
+             return std::move(out);
+           }, py::arg("keys"), py::arg("n"), py::arg("src"), py::arg("src_stride"), py::arg("length"),
+           py::arg("src_kind"), py::arg("stream"), py::arg("evict"), py::arg("as_array") = false)
       .def_property_readonly("device_owned", &DevicePageCache::device_owned)
       .def("erase", &DevicePageCache::erase, G())
       .def("contains", &DevicePageCache::contains, G())

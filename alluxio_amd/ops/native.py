@@ -90,16 +90,29 @@ def wrap_errors(fn):
     return inner
 
 
-@functools.lru_cache(maxsize=1)
+_DEVICE_COUNT: int | None = None
+_DEVICE_COUNT_LOCK = threading.Lock()
+
+
 def device_count() -> int:
-    """Number of visible HIP devices (0 on CPU-only hosts)."""
-    try:
-        import torch
-        if torch.cuda.is_available():
-            return torch.cuda.device_count()
-    except Exception:  # noqa: BLE001
-        pass
-    return 0
+    """Number of visible HIP devices (0 on CPU-only hosts).  Computed once under a lock: the
+    first query initialises the runtime (amdsmi), and threads racing into that first query could
+    otherwise see a transient failure as "no GPU" (and, e.g., memcpy a device pointer on the host)."""
+    global _DEVICE_COUNT
+    n = _DEVICE_COUNT
+    if n is not None:
+        return n
+    with _DEVICE_COUNT_LOCK:
+        if _DEVICE_COUNT is None:
+            count = 0
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    count = torch.cuda.device_count()
+            except Exception:  # noqa: BLE001
+                count = 0
+            _DEVICE_COUNT = count
+        return _DEVICE_COUNT
 
 
 def has_gpu() -> bool:

@@ -42,7 +42,7 @@ def test_batched_copy_exact(gpu):
         assert torch.equal(src[o:o + n], dst[o:o + n])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_crc32c_matches_host(gpu, variant):
     import torch
     C = lib()

@@ -36,7 +36,7 @@ def main(argv=None) -> int:
         return (time.perf_counter() - t0) / a.iters
 
     for piece in (2 << 20, 64 << 20):
-        for variant in (0, 1, 2, 3):
+        for variant in (0, 1, 2, 3, 4):
             C.set_crc_variant(variant)
             t = timeit(lambda: C.crc32c_device(buf.data_ptr(), n, piece, 0))
             rows.append({"case": "crc32c_pieces", "variant": variant, "piece_MB": piece >> 20, "GB": n / 1e9,
@@ -48,7 +48,10 @@ def main(argv=None) -> int:
     v1 = C.crc32c_device(buf.data_ptr(), 64 << 20, 2 << 20, 0)
     C.set_crc_variant(3)
     v3 = C.crc32c_device(buf.data_ptr(), 64 << 20, 2 << 20, 0)
-    assert list(v1) == list(v3), "v2/v4 disagree"
+    C.set_crc_variant(4)
+    v5 = C.crc32c_device(buf.data_ptr(), 64 << 20, 2 << 20, 0)
+    C.set_crc_variant(3)
+    assert list(v1) == list(v3) == list(v5), "variants disagree"
     if hasattr(C, "crc32c_gather_device"):
         pages = [(buf.data_ptr() + i * (2 << 20), 2 << 20) for i in range(0, n // (2 << 20), 3)]
         t = timeit(lambda: C.crc32c_gather_device(pages, 0))

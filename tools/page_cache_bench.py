@@ -95,12 +95,12 @@ def main(argv=None):
         dk2 = dk | (1 << 40)
         torch.cuda.synchronize()
         t_dev = time.perf_counter()
-        ev = pc.put_many_device(dk2.data_ptr(), slots, src_rows.data_ptr(), stride, ps, 1, stream, True)
+        ev = pc.put_many_device(dk2.data_ptr(), slots, src_rows.data_ptr(), stride, ps, 1, stream, True, True)
         evict_GBps = slots * ps / (time.perf_counter() - t_dev) / 1e9
         assert len(ev) == slots, len(ev)
         torch.cuda.synchronize()
         t_dev = time.perf_counter()
-        pc.put_many_device(dk.data_ptr(), slots, src_rows.data_ptr(), stride, ps, 1, stream, True)
+        pc.put_many_device(dk.data_ptr(), slots, src_rows.data_ptr(), stride, ps, 1, stream, True, True)
         evict2_GBps = slots * ps / (time.perf_counter() - t_dev) / 1e9
         del src_rows, dk2
         C.fill_pattern(pc.arena, slots * ps, 1234, 0, stream)      # distinct bytes in every page
