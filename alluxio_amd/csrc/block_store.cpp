@@ -112,7 +112,7 @@ BlockStore::~BlockStore() {
     }
     for (void* p : {(void*)d_crf_, (void*)d_last_, (void*)d_fbytes_, (void*)d_dir_, (void*)d_keys_,
                     (void*)d_excl_, (void*)d_ctl_, (void*)d_upd_, (void*)d_bits_, (void*)d_partial_,
-                    (void*)d_claimed_, (void*)d_claim_item_})
+                    (void*)d_claimed_})
       if (p) hipFree(p);
     for (void* p : {(void*)h_excl_, (void*)h_ctl_, (void*)h_out_, (void*)h_pages_, (void*)h_claimed_})
       if (p) hipHostFree(p);
@@ -121,7 +121,8 @@ BlockStore::~BlockStore() {
       if (d->mag_bits) hipFree(d->mag_bits);
       if (d->mag_upd) hipFree(d->mag_upd);
     }
-    for (auto& c : claim_) {
+    for (ClaimScratch* cp : {&claim_[0], &claim_[1], &claim_one_}) {
+      ClaimScratch& c = *cp;
       for (void* p : {(void*)c.items_d, (void*)c.pages_d, (void*)c.got_d})
         if (p) hipFree(p);
       for (void* p : {(void*)c.items_h, (void*)c.pages_h, (void*)c.got_h})
@@ -366,7 +367,7 @@ void BlockStore::mag_refill(StorageDir& d, int64_t want) {
   // on the internal stream, completed before returning: the (pageable) update list is consumed
   // and any stream claiming afterwards sees the pages
   HIP_OK(hipMemcpyAsync(d.mag_upd, upd.data(), upd.size() * 8, hipMemcpyHostToDevice, internal_stream_));
-  HIP_OK(launch_mag_fill(d.mag_bits, d.mag_upd, (uint32_t)n, internal_stream_));
+  HIP_OK(launch_mag_fill(d.mag_bits, (uint32_t)nwords, d.mag_upd, (uint32_t)n, internal_stream_));
   HIP_OK(hipStreamSynchronize(internal_stream_));
   d.mag_pages += moved;
 }
@@ -1609,24 +1610,20 @@ std::vector<int64_t> BlockStore::device_alloc_pages(std::unique_lock<std::mutex>
   {
     std::unique_lock<std::mutex> g(ev_mu_);
     set_device();
-    if (h_pages_cap_ < want) {
-      if (h_pages_) hipHostFree(h_pages_);
-      h_pages_ = nullptr;
-      const size_t cap = std::max<size_t>(want, 4096);
-      HIP_OK(hipHostMalloc((void**)&h_pages_, cap * 8, hipHostMallocMapped));
-      HIP_OK(hipHostGetDevicePointer((void**)&h_pages_dev_, h_pages_, 0));
-      h_pages_cap_ = cap;
-    }
-    if (!d_claim_item_) HIP_OK(hipMalloc((void**)&d_claim_item_, sizeof(ClaimItem)));
-    const ClaimItem item{0, 0, want, 0, 0, 0};
+    claim_reserve(claim_one_, 1, want);
+    claim_one_.items_h[0] = ClaimItem{0, 0, want, 0, 0, 0};
     lk.unlock();
-    hipError_t e = hipMemcpyAsync(d_claim_item_, &item, sizeof(item), hipMemcpyHostToDevice, internal_stream_);
+    hipError_t e = hipMemcpyAsync(claim_one_.items_d, claim_one_.items_h, sizeof(ClaimItem), hipMemcpyHostToDevice,
+                                  internal_stream_);
     if (e == hipSuccess)
-      e = launch_mag_claim_scatter(d.mag_bits, nwords, d_claim_item_, 1, h_pages_dev_, d_claimed_, 0, nullptr, 0,
-                                   internal_stream_);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_claimed_, d_claimed_, 4, hipMemcpyDeviceToHost, internal_stream_);
+      e = launch_mag_claim_scatter(d.mag_bits, nwords, claim_one_.items_d, 1, claim_one_.pages_d,
+                                   (uint32_t)claim_one_.pages_cap, claim_one_.got_d, 0, nullptr, 0, internal_stream_);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(claim_one_.got_h, claim_one_.got_d, sizeof(uint32_t), hipMemcpyDeviceToHost, internal_stream_);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(claim_one_.pages_h, claim_one_.pages_d, (size_t)want * 8, hipMemcpyDeviceToHost, internal_stream_);
     if (e == hipSuccess) e = hipStreamSynchronize(internal_stream_);
-    if (e == hipSuccess) pages.assign(h_pages_, h_pages_ + std::min(*h_claimed_, want));
+    if (e == hipSuccess) pages.assign(claim_one_.pages_h, claim_one_.pages_h + std::min(claim_one_.got_h[0], want));
     g.unlock();
     lk.lock();
     if (e != hipSuccess) throw StoreError(kErrHip, std::string("device page claim: ") + hipGetErrorString(e));
@@ -2247,8 +2244,9 @@ bool BlockStore::ingest_device_group(int64_t session, const std::vector<int64_t>
   }
   const uint32_t nwords = (uint32_t)dirs_[d]->free_bits.size();
   HIP_OK(hipMemcpyAsync(c.items_d, c.items_h, items.size() * sizeof(ClaimItem), hipMemcpyHostToDevice, st));
-  HIP_OK(launch_mag_claim_scatter(dirs_[d]->mag_bits, nwords, c.items_d, (uint32_t)items.size(), c.pages_d, c.got_d,
-                                  (uint32_t)nchunks, reinterpret_cast<uint8_t*>(dirs_[d]->spec.base), ps, st));
+  HIP_OK(launch_mag_claim_scatter(dirs_[d]->mag_bits, nwords, c.items_d, (uint32_t)items.size(), c.pages_d,
+                                  (uint32_t)c.pages_cap, c.got_d, (uint32_t)nchunks,
+                                  reinterpret_cast<uint8_t*>(dirs_[d]->spec.base), ps, st));
   HIP_OK(hipMemcpyAsync(c.pages_h, c.pages_d, npages * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(c.got_h, c.got_d, items.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   for (int64_t id : c.ids) pending.push_back(id);

@@ -349,7 +349,7 @@ class BlockStore {
   bool use_device_evict_ = true;
   // K7 measured slower than the host bitmap scan end to end (profiles/r2_evict_bench.jsonl):
   // off unless alluxio.worker.hbm.device.alloc.enabled
-  bool use_device_alloc_ = true;
+  bool use_device_alloc_ = false;             // K7 magazine: opt-in until validated on the device
   bool demote_on_evict_ = false;
   uint32_t device_alloc_min_pages_ = 1024;     // create_blocks: device claims from this many pages
   hipStream_t internal_stream_ = nullptr;
@@ -388,7 +388,6 @@ class BlockStore {
   int64_t* h_pages_dev_ = nullptr;
   size_t h_pages_cap_ = 0;
   uint32_t* h_claimed_ = nullptr;
-  ClaimItem* d_claim_item_ = nullptr;
   uint32_t* d_claimed_ = nullptr;
   std::mutex ev_mu_;                 // device selection / allocation scratch (taken after mu_)
   // checksum scratch
@@ -411,7 +410,7 @@ class BlockStore {
     std::vector<int64_t> ids;        // blocks of the in-flight group, item order
     std::vector<size_t> index;       // their positions in the caller's arrays
     std::vector<uint64_t> at;        // their offsets in the host staging half
-  } claim_[2];
+  } claim_[2], claim_one_;                   // claim_one_: standalone claims (under ev_mu_)
   void claim_reserve(ClaimScratch& c, size_t items, size_t pages);
 };
 

@@ -332,10 +332,12 @@ __global__ __launch_bounds__(kPaBlock) void palloc_emit_kernel(uint64_t* __restr
 }
 
 // ---- K7 device page magazine ---------------------------------------------------------------------
-__global__ __launch_bounds__(256) void mag_fill_kernel(uint64_t* __restrict__ bits, const uint64_t* __restrict__ upd,
-                                                       uint32_t n) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    atomicOr((unsigned long long*)&bits[upd[2 * i]], (unsigned long long)upd[2 * i + 1]);
+__global__ __launch_bounds__(256) void mag_fill_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
+                                                       const uint64_t* __restrict__ upd, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t w = upd[2 * i];
+    if (w < nwords) atomicOr((unsigned long long*)&bits[w], (unsigned long long)upd[2 * i + 1]);
+  }
 }
 
 __global__ __launch_bounds__(256) void mag_drain_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
@@ -360,7 +362,8 @@ __device__ __forceinline__ uint64_t low_bits(uint64_t x, uint32_t k) {
 // need from its word with one atomicAnd and keeps the bits it actually won.
 __global__ __launch_bounds__(256) void mag_claim_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
                                                         const ClaimItem* __restrict__ items, uint32_t nitems,
-                                                        int64_t* __restrict__ pages_out, uint32_t* __restrict__ got) {
+                                                        int64_t* __restrict__ pages_out, uint32_t pages_cap,
+                                                        uint32_t* __restrict__ got) {
   const uint32_t lane = lane_id();
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); it < nitems; it += nw) {
@@ -396,7 +399,8 @@ __global__ __launch_bounds__(256) void mag_claim_kernel(uint64_t* __restrict__ b
         if ((int)lane >= o) wincl += v;
       }
       uint32_t pos = item.page_base + have + wincl - wn;
-      for (uint64_t r = won; r; r &= r - 1) pages_out[pos++] = (int64_t)w * 64 + __builtin_ctzll(r);
+      for (uint64_t r = won; r; r &= r - 1, ++pos)
+        if (pos < pages_cap) pages_out[pos] = (int64_t)w * 64 + __builtin_ctzll(r);
       have += __shfl(wincl, 63, 64);
     }
     if (lane == 0) got[it] = have;
@@ -443,10 +447,10 @@ __global__ __launch_bounds__(256) void mag_scatter_kernel(const ClaimItem* __res
 
 }  // namespace
 
-hipError_t launch_mag_fill(uint64_t* bits, const uint64_t* upd, uint32_t n, hipStream_t stream) {
+hipError_t launch_mag_fill(uint64_t* bits, uint32_t nwords, const uint64_t* upd, uint32_t n, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const unsigned grid = (unsigned)std::min<uint32_t>((n + 255) / 256, 1024);
-  hipLaunchKernelGGL(mag_fill_kernel, dim3(grid), dim3(256), 0, stream, bits, upd, n);
+  hipLaunchKernelGGL(mag_fill_kernel, dim3(grid), dim3(256), 0, stream, bits, nwords, upd, n);
   return hipGetLastError();
 }
 
@@ -458,11 +462,12 @@ hipError_t launch_mag_drain(uint64_t* bits, uint32_t nwords, uint64_t* out, hipS
 }
 
 hipError_t launch_mag_claim_scatter(uint64_t* bits, uint32_t nwords, const ClaimItem* items, uint32_t nitems,
-                                    int64_t* pages_out, uint32_t* got, uint32_t total_chunks, uint8_t* arena,
-                                    uint64_t page_size, hipStream_t stream) {
+                                    int64_t* pages_out, uint32_t pages_cap, uint32_t* got, uint32_t total_chunks,
+                                    uint8_t* arena, uint64_t page_size, hipStream_t stream) {
   if (nitems == 0 || nwords == 0) return hipSuccess;
   const unsigned cgrid = (unsigned)std::min<uint32_t>((nitems + 3) / 4, 4096);
-  hipLaunchKernelGGL(mag_claim_kernel, dim3(cgrid), dim3(256), 0, stream, bits, nwords, items, nitems, pages_out, got);
+  hipLaunchKernelGGL(mag_claim_kernel, dim3(cgrid), dim3(256), 0, stream, bits, nwords, items, nitems, pages_out,
+                     pages_cap, got);
   if (total_chunks) {
     const unsigned sgrid = (unsigned)std::min<uint32_t>((total_chunks + 3) / 4, 16384);
     hipLaunchKernelGGL(mag_scatter_kernel, dim3(sgrid), dim3(256), 0, stream, items, nitems, total_chunks, pages_out,

@@ -156,7 +156,7 @@ struct ClaimItem {
   uint32_t pad;
 };
 // bits[upd[2i]] |= upd[2i+1] (atomic): pages moved into the magazine
-hipError_t launch_mag_fill(uint64_t* bits, const uint64_t* upd, uint32_t n, hipStream_t stream);
+hipError_t launch_mag_fill(uint64_t* bits, uint32_t nwords, const uint64_t* upd, uint32_t n, hipStream_t stream);
 // out[w] = atomicExch(bits[w], 0): the magazine handed back (no claim can race it)
 hipError_t launch_mag_drain(uint64_t* bits, uint32_t nwords, uint64_t* out, hipStream_t stream);
 // One wave per item claims item.want pages (atomicAnd on the words, ballot/popcount ranking)
@@ -164,8 +164,8 @@ hipError_t launch_mag_drain(uint64_t* bits, uint32_t nwords, uint64_t* out, hipS
 // When total_chunks > 0 a second launch copies each item's bytes into its claimed pages (one
 // wave per 64 KiB chunk; items that came up short are skipped -- the host finishes them).
 hipError_t launch_mag_claim_scatter(uint64_t* bits, uint32_t nwords, const ClaimItem* items, uint32_t nitems,
-                                    int64_t* pages_out, uint32_t* got, uint32_t total_chunks, uint8_t* arena,
-                                    uint64_t page_size, hipStream_t stream);
+                                    int64_t* pages_out, uint32_t pages_cap, uint32_t* got, uint32_t total_chunks,
+                                    uint8_t* arena, uint64_t page_size, hipStream_t stream);
 
 // K9: client page cache lookup.  Open-addressing (linear probing) table of page keys in HBM;
 // `key` = (interned file id << 24) | page index, so keys are exact (no hash collisions to

@@ -1,4 +1,5 @@
-"""Proxy process: S3-compatible REST API plus the ``/api/v1/paths`` and ``/api/v1/streams`` REST APIs.
+"""Proxy process: S3-compatible REST API, the ``/api/v1/paths`` and ``/api/v1/streams`` REST APIs,
+and a WebHDFS gateway on ``/webhdfs/v1`` for Hadoop clients (:mod:`alluxio_amd.proxy.webhdfs`).
 
 Parity: core/server/proxy/src/main/java/alluxio/proxy/s3/S3RestServiceHandler.java:72-380
 (bucket = top-level directory; GET/PUT/HEAD/DELETE object, copy via ``x-amz-copy-source``,
@@ -447,8 +448,10 @@ class PathsStreams:
 
 class ProxyServer:
     def __init__(self, fs, host: str = "127.0.0.1", port: int = 0, write_type: str = "CACHE_THROUGH"):
+        from .webhdfs import WebHdfsGateway
         self.s3 = S3Handler(fs, write_type)
         self.api = PathsStreams(fs)
+        self.webhdfs = WebHdfsGateway(fs, write_type)
         outer = self
 
         class H(BaseHTTPRequestHandler):
@@ -482,6 +485,11 @@ class ProxyServer:
                 if body is None:  # HEAD: Content-Length already describes the object
                     self.end_headers()
                     return
+                if not isinstance(body, (bytes, bytearray)):   # streamed (Content-Length given)
+                    self.end_headers()
+                    for chunk in body:
+                        self.wfile.write(chunk)
+                    return
                 if "Content-Type" not in headers:
                     self.send_header("Content-Type", "application/xml")
                 self.send_header("Content-Length", str(len(body)))
@@ -492,6 +500,13 @@ class ProxyServer:
                 u = urlparse(self.path)
                 q = {k: v[-1] for k, v in parse_qs(u.query, keep_blank_values=True).items()}
                 path = unquote(u.path)
+                if path == "/webhdfs/v1" or path.startswith("/webhdfs/v1/"):
+                    host = self.headers.get("Host") or f"{outer.httpd.server_address[0]}:{outer.port}"
+                    target = "/" + path[len("/webhdfs/v1"):].lstrip("/")
+                    status, headers, body = outer.webhdfs.handle(method, target, q, host, self._body_iter)
+                    if method == "HEAD":
+                        body = None
+                    return self._reply(status, headers, body)
                 try:
                     if path.startswith("/api/v1/paths/") or path.startswith("/api/v1/streams/"):
                         return self._rest(method, path, q)

@@ -172,10 +172,14 @@ class WebHdfsUnderFileSystem(UnderFileSystem):
 
     # ---- UnderFileSystem --------------------------------------------------------------------
     def create(self, path, options: CreateOptions | None = None):
-        if options is None or getattr(options, "create_parent", True):
-            parent = posixpath.dirname(self._path(path))
-            if parent not in ("", "/") and not self.is_directory(parent):
+        parent = posixpath.dirname(self._path(path))
+        if parent not in ("", "/") and not self.is_directory(parent):
+            if options is None or getattr(options, "create_parent", True):
                 self.mkdirs(parent)
+            else:
+                # WebHDFS CREATE makes missing parents on the server (HDFS create()); a
+                # non-recursive create is enforced here, as createNonRecursive would be
+                raise FileNotFoundError(f"parent of {path} does not exist")
         return _WebHdfsWriter(self, path, options)
 
     def open(self, path, options: OpenOptions | None = None):

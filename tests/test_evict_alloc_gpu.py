@@ -238,6 +238,7 @@ def test_magazine_ingest_then_host_allocs_keep_pages_disjoint(gpu, tmp_path):
     page = 64 * KB
     npages = 512
     s = _device_store(npages, page)
+    s.set_use_device_alloc(True, 64)
     rng = np.random.default_rng(11)
     paths, lens, datas = [], [], []
     for i in range(150):
