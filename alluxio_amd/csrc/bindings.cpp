@@ -446,8 +446,19 @@ PYBIND11_MODULE(_C, m) {
              d["demoted_bytes"] = st.demoted_bytes;
              d["batched_moves"] = st.batched_moves;
              d["batched_move_blocks"] = st.batched_move_blocks;
+             d["mag_refills"] = st.mag_refills;
+             d["mag_refill_pages"] = st.mag_refill_pages;
+             d["mag_drains"] = st.mag_drains;
+             d["mag_drain_pages"] = st.mag_drain_pages;
+             d["mag_short_items"] = st.mag_short_items;
              return d;
            })
+      .def("mag_refill", &BlockStore::mag_refill_pages, G())
+      .def("mag_pages", &BlockStore::mag_pages, G())
+      .def("mag_device_count", &BlockStore::mag_device_count, G())
+      .def("mag_claim_many", &BlockStore::mag_claim_many, G())
+      .def("mag_give", &BlockStore::mag_give, G())
+      .def("mag_drain", &BlockStore::mag_drain_dir, G())
       .def("has_block", &BlockStore::has_block, G())
       .def("has_temp_block", &BlockStore::has_temp_block, G())
       .def("block_info", &BlockStore::block_info, G())

@@ -370,6 +370,8 @@ void BlockStore::mag_refill(StorageDir& d, int64_t want) {
   HIP_OK(launch_mag_fill(d.mag_bits, (uint32_t)nwords, d.mag_upd, (uint32_t)n, internal_stream_));
   HIP_OK(hipStreamSynchronize(internal_stream_));
   d.mag_pages += moved;
+  ++stats_.mag_refills;
+  stats_.mag_refill_pages += moved;
 }
 
 // Hands every page left in the magazine back to the host pool (atomic exchange per word, so a
@@ -391,6 +393,8 @@ int64_t BlockStore::mag_drain(StorageDir& d) {
     back += __builtin_popcountll(out[w]);
   }
   d.mag_pages -= back;
+  ++stats_.mag_drains;
+  stats_.mag_drain_pages += back;
   return back;
 }
 
@@ -1624,6 +1628,8 @@ std::vector<int64_t> BlockStore::device_alloc_pages(std::unique_lock<std::mutex>
       e = hipMemcpyAsync(claim_one_.pages_h, claim_one_.pages_d, (size_t)want * 8, hipMemcpyDeviceToHost, internal_stream_);
     if (e == hipSuccess) e = hipStreamSynchronize(internal_stream_);
     if (e == hipSuccess) pages.assign(claim_one_.pages_h, claim_one_.pages_h + std::min(claim_one_.got_h[0], want));
+    for (int64_t p : pages)
+      if (p < 0 || p >= d.num_pages) e = hipErrorInvalidValue;   // never hand out a bogus page
     g.unlock();
     lk.lock();
     if (e != hipSuccess) throw StoreError(kErrHip, std::string("device page claim: ") + hipGetErrorString(e));
@@ -1785,6 +1791,74 @@ std::vector<int64_t> BlockStore::block_pages(int64_t id, int* dir_out, uint64_t*
   *ps_out = s.page_size;
   *base_out = s.base;
   return b->pages;
+}
+
+int64_t BlockStore::mag_refill_pages(int dir, int64_t pages) {
+  std::unique_lock<std::mutex> lk(mu_);
+  StorageDir& d = *dirs_.at(dir);
+  const int64_t before = d.mag_pages;
+  mag_refill(d, pages);
+  return d.mag_pages - before;
+}
+
+int64_t BlockStore::mag_pages(int dir) {
+  std::unique_lock<std::mutex> lk(mu_);
+  return dirs_.at(dir)->mag_pages;
+}
+
+int64_t BlockStore::mag_device_count(int dir) {
+  std::unique_lock<std::mutex> lk(mu_);
+  StorageDir& d = *dirs_.at(dir);
+  if (!d.mag_bits) return 0;
+  std::vector<uint64_t> w(d.free_bits.size());
+  HIP_OK(hipStreamSynchronize(internal_stream_));
+  HIP_OK(hipMemcpy(w.data(), d.mag_bits, w.size() * 8, hipMemcpyDeviceToHost));
+  int64_t n = 0;
+  for (uint64_t x : w) n += __builtin_popcountll(x);
+  return n;
+}
+
+std::vector<std::vector<int64_t>> BlockStore::mag_claim_many(int dir, const std::vector<uint32_t>& wants) {
+  std::unique_lock<std::mutex> lk(mu_);
+  StorageDir& d = *dirs_.at(dir);
+  std::vector<std::vector<int64_t>> out(wants.size());
+  if (!d.mag_bits || wants.empty()) return out;
+  std::unique_lock<std::mutex> g(ev_mu_);
+  size_t total = 0;
+  for (uint32_t w : wants) total += w;
+  claim_reserve(claim_one_, wants.size(), total);
+  uint32_t pb = 0;
+  for (size_t i = 0; i < wants.size(); ++i) {
+    claim_one_.items_h[i] = ClaimItem{0, 0, wants[i], pb, 0, 0};
+    pb += wants[i];
+  }
+  HIP_OK(hipMemcpyAsync(claim_one_.items_d, claim_one_.items_h, wants.size() * sizeof(ClaimItem), hipMemcpyHostToDevice,
+                        internal_stream_));
+  HIP_OK(launch_mag_claim_scatter(d.mag_bits, (uint32_t)d.free_bits.size(), claim_one_.items_d, (uint32_t)wants.size(),
+                                  claim_one_.pages_d, (uint32_t)claim_one_.pages_cap, claim_one_.got_d, 0, nullptr, 0,
+                                  internal_stream_));
+  HIP_OK(hipMemcpyAsync(claim_one_.got_h, claim_one_.got_d, wants.size() * 4, hipMemcpyDeviceToHost, internal_stream_));
+  HIP_OK(hipMemcpyAsync(claim_one_.pages_h, claim_one_.pages_d, std::max<size_t>(total, 1) * 8, hipMemcpyDeviceToHost,
+                        internal_stream_));
+  HIP_OK(hipStreamSynchronize(internal_stream_));
+  for (size_t i = 0; i < wants.size(); ++i) {
+    const ClaimItem& it = claim_one_.items_h[i];
+    const uint32_t g = std::min(claim_one_.got_h[i], it.want);
+    out[i].assign(claim_one_.pages_h + it.page_base, claim_one_.pages_h + it.page_base + g);
+    d.mag_pages -= g;
+  }
+  return out;
+}
+
+void BlockStore::mag_give(int dir, const std::vector<int64_t>& pages) {
+  std::unique_lock<std::mutex> lk(mu_);
+  StorageDir& d = *dirs_.at(dir);
+  for (int64_t p : pages) bit_give(d.free_bits, p);
+}
+
+int64_t BlockStore::mag_drain_dir(int dir) {
+  std::unique_lock<std::mutex> lk(mu_);
+  return mag_drain(*dirs_.at(dir));
 }
 
 std::string BlockStore::committed_file(int64_t id) {
@@ -1996,6 +2070,19 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
   }
   std::vector<std::vector<int64_t>> pending(2);   // blocks whose copy from staging half h is in flight
   std::vector<uint8_t*> host_half(2, nullptr);
+  if (use_device_alloc_ && has_device_) {
+    // K7: one magazine refill for the whole call up front -- a refill synchronizes the internal
+    // stream, which would otherwise stall the staging double buffer once per group
+    std::unique_lock<std::mutex> g2(mu_);
+    const int d0 = allocate_dir(0, "", 1);
+    if (d0 >= 0 && dirs_[d0]->spec.kind == DirKind::kDevice && dirs_[d0]->mag_bits) {
+      StorageDir& sd = *dirs_[d0];
+      int64_t need = 0;
+      for (uint64_t len : lengths) need += (int64_t)ceil_div(std::max<uint64_t>(len, 1), sd.spec.page_size);
+      need = std::min<int64_t>(need, sd.free_pages - sd.reserved_pages);
+      if (sd.mag_pages < need) mag_refill(sd, need - sd.mag_pages);
+    }
+  }
   auto finish = [&](int h) {
     if (pending[h].empty() && claim_[h].ids.empty()) return;
     if (has_device_) HIP_OK(hipStreamSynchronize(st));
@@ -2048,6 +2135,8 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
           StorageDir& sd = *dirs_[d];
           for (uint64_t sz : gsz) want += ceil_div(std::max<uint64_t>(sz, 1), sd.spec.page_size);
           if (sd.mag_pages < (int64_t)want) mag_refill(sd, (int64_t)want - sd.mag_pages);
+          // reserved now: a group launched before this one finishes must not count these pages
+          sd.mag_pages -= (int64_t)want;
           for (size_t k = 0; k < gid.size(); ++k) {
             BlockMeta b;
             b.id = gid[k];
@@ -2267,10 +2356,11 @@ std::unordered_set<int64_t> BlockStore::ingest_device_finish(int64_t session, in
     const uint64_t ps = d.spec.page_size;
     for (size_t k = 0; k < c.ids.size(); ++k) {
       const ClaimItem& it = c.items_h[k];
-      const uint32_t got = c.got_h[k];
+      const uint32_t got = std::min(c.got_h[k], it.want);
       BlockMeta* b = find(c.ids[k]);
-      d.mag_pages -= got;                        // these left the magazine either way
+      d.mag_pages += (int64_t)it.want - got;     // the group reserved `want`; only `got` left the magazine
       if (!b || got < it.want) {
+        ++stats_.mag_short_items;
         for (uint32_t j = 0; j < got; ++j) bit_give(d.free_bits, c.pages_h[it.page_base + j]);
         if (b) redo.push_back(k);
         else failed.insert(c.ids[k]);

@@ -237,6 +237,7 @@ class BlockStore {
     uint64_t selections = 0, device_selections = 0, candidates = 0, victims = 0, revalidated_away = 0;
     uint64_t device_allocs = 0, device_alloc_pages = 0, annotation_flushes = 0, annotation_updates = 0;
     uint64_t demoted_blocks = 0, demoted_bytes = 0, batched_moves = 0, batched_move_blocks = 0;
+    uint64_t mag_refills = 0, mag_refill_pages = 0, mag_drains = 0, mag_drain_pages = 0, mag_short_items = 0;
   };
   EvictStats evict_stats();
 
@@ -247,6 +248,15 @@ class BlockStore {
   std::vector<int64_t> block_ids(int tier);
   std::vector<int64_t> block_pages(int64_t block_id, int* dir_out, uint64_t* page_size_out,
                                    uint64_t* base_out);
+  // K7 magazine introspection / control (tests, benchmarks): move >= pages into dir's magazine,
+  // count the device bitmap, claim for several items at once (their pages stay taken: the caller
+  // gives them back with mag_give), hand pages back, drain the magazine into the host pool.
+  int64_t mag_refill_pages(int dir, int64_t pages);
+  int64_t mag_device_count(int dir);
+  std::vector<std::vector<int64_t>> mag_claim_many(int dir, const std::vector<uint32_t>& wants);
+  void mag_give(int dir, const std::vector<int64_t>& pages);
+  int64_t mag_drain_dir(int dir);
+  int64_t mag_pages(int dir);
   // Path of a committed block held in a file dir (tmpfs / SSD tier), "" otherwise.
   std::string committed_file(int64_t block_id);
   std::vector<Event> drain_events();

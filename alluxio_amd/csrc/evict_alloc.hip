@@ -360,50 +360,89 @@ __device__ __forceinline__ uint64_t low_bits(uint64_t x, uint32_t k) {
 // One wave per item: windows of 64 words (one per lane) starting at a per-item offset (spreads
 // concurrent items over the bitmap); each lane takes up to its share of the item's remaining
 // need from its word with one atomicAnd and keeps the bits it actually won.
-__global__ __launch_bounds__(256) void mag_claim_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
-                                                        const ClaimItem* __restrict__ items, uint32_t nitems,
-                                                        int64_t* __restrict__ pages_out, uint32_t pages_cap,
-                                                        uint32_t* __restrict__ got) {
-  const uint32_t lane = lane_id();
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); it < nitems; it += nw) {
+__global__ __launch_bounds__(64) void mag_claim_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
+                                                       const ClaimItem* __restrict__ items, uint32_t nitems,
+                                                       int64_t* __restrict__ pages_out, uint32_t pages_cap,
+                                                       uint32_t* __restrict__ got) {
+  // one wave per workgroup and item: the window's free counts, the planned takes and the won
+  // counts go through LDS, thread 0 plans and ranks serially (64 entries), barriers order the
+  // phases -- no cross-lane shuffles in the plan
+  __shared__ uint32_t s_cnt[64];
+  __shared__ uint32_t s_take[64];
+  __shared__ uint32_t s_have, s_seen;
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
     const ClaimItem item = items[it];
-    uint32_t have = 0;
     const uint32_t start = (uint32_t)(((uint64_t)it * 0x9E3779B1u) % nwords);
-    for (uint32_t win = 0; win < nwords && have < item.want; win += 64) {
-      const uint32_t w = (start + win + lane) % nwords;
-      const bool valid = win + lane < nwords;
+    const uint32_t rot = (uint32_t)((it * 37u) & 63u);      // items start at different bits of a word
+    const uint32_t span = nwords < 64 ? nwords : 64;        // distinct words per window
+    const uint32_t max_rounds = 64 * ((nwords + span - 1) / span) + 64;
+    if (lane == 0) s_have = 0;
+    __syncthreads();
+    uint32_t dry = 0;
+    // windows walk the bitmap round and round: a wave that lost a race retries with a fresh
+    // snapshot until it has its pages or one whole pass found no free bit (magazine dry)
+    for (uint32_t win = 0, rounds = 0; rounds < max_rounds; win += span, ++rounds) {
+      const uint32_t have = s_have;
+      if (have >= item.want || dry >= nwords) break;
+      const uint32_t w = (uint32_t)(((uint64_t)start + win + lane) % nwords);
+      const bool valid = lane < span;
       const uint64_t word = valid ? __hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-      const uint32_t free_n = (uint32_t)__popcll(word);
-      // exclusive prefix of free counts over the lanes
-      uint32_t incl = free_n;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o, 64);
-        if ((int)lane >= o) incl += v;
+      s_cnt[lane] = (uint32_t)__popcll(word);
+      __syncthreads();
+      if (lane == 0) {
+        uint32_t left = item.want - have, seen = 0;
+        for (uint32_t l = 0; l < 64; ++l) {
+          const uint32_t f = s_cnt[l];
+          const uint32_t t = f < left ? f : left;
+          s_take[l] = t;
+          left -= t;
+          seen += f;
+        }
+        s_seen = seen;
       }
-      const uint32_t excl = incl - free_n;
-      const uint32_t left = item.want - have;
-      const uint32_t take = excl >= left ? 0u : min(free_n, left - excl);
+      __syncthreads();
+      const uint32_t take = s_take[lane];
+      dry = s_seen ? 0u : dry + span;
       uint64_t won = 0;
       if (take) {
-        const uint64_t mask = low_bits(word, take);
-        const uint64_t old = atomicAnd((unsigned long long*)&bits[w], ~(unsigned long long)mask);
-        won = old & mask;                          // bits another claimer took first are not ours
+        // compare-and-swap on the word: the bits are ours only if the word still holds what we
+        // planned against; on a lost race re-plan against the value we got back (bounded)
+        uint64_t cur = word;
+        for (int tries = 0; tries < 64 && cur; ++tries) {
+          const uint32_t n = (uint32_t)__popcll(cur) < take ? (uint32_t)__popcll(cur) : take;
+          const uint64_t r = rot ? ((cur >> rot) | (cur << (64 - rot))) : cur;
+          const uint64_t mr = low_bits(r, n);
+          const uint64_t mask = rot ? ((mr << rot) | (mr >> (64 - rot))) : mr;
+          const unsigned long long prev = atomicCAS((unsigned long long*)&bits[w], (unsigned long long)cur,
+                                                    (unsigned long long)(cur & ~mask));
+          if (prev == (unsigned long long)cur) {
+            won = mask;
+            break;
+          }
+          cur = prev;
+        }
       }
-      const uint32_t wn = (uint32_t)__popcll(won);
-      uint32_t wincl = wn;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(wincl, o, 64);
-        if ((int)lane >= o) wincl += v;
+      __syncthreads();                                   // everyone has read s_take
+      s_cnt[lane] = (uint32_t)__popcll(won);
+      __syncthreads();
+      if (lane == 0) {                                   // exclusive ranks of the won pages
+        uint32_t acc = have;
+        for (uint32_t l = 0; l < 64; ++l) {
+          const uint32_t c = s_cnt[l];
+          s_take[l] = acc;
+          acc += c;
+        }
+        s_have = acc;
       }
-      uint32_t pos = item.page_base + have + wincl - wn;
+      __syncthreads();
+      uint32_t pos = item.page_base + s_take[lane];
       for (uint64_t r = won; r; r &= r - 1, ++pos)
-        if (pos < pages_cap) pages_out[pos] = (int64_t)w * 64 + __builtin_ctzll(r);
-      have += __shfl(wincl, 63, 64);
+        if (pos < pages_cap && pos < item.page_base + item.want) pages_out[pos] = (int64_t)w * 64 + __builtin_ctzll(r);
+      __syncthreads();                                   // s_take / s_have stable until all used them
     }
-    if (lane == 0) got[it] = have;
+    if (lane == 0) got[it] = s_have;
+    __syncthreads();
   }
 }
 
@@ -465,8 +504,8 @@ hipError_t launch_mag_claim_scatter(uint64_t* bits, uint32_t nwords, const Claim
                                     int64_t* pages_out, uint32_t pages_cap, uint32_t* got, uint32_t total_chunks,
                                     uint8_t* arena, uint64_t page_size, hipStream_t stream) {
   if (nitems == 0 || nwords == 0) return hipSuccess;
-  const unsigned cgrid = (unsigned)std::min<uint32_t>((nitems + 3) / 4, 4096);
-  hipLaunchKernelGGL(mag_claim_kernel, dim3(cgrid), dim3(256), 0, stream, bits, nwords, items, nitems, pages_out,
+  const unsigned cgrid = (unsigned)std::min<uint32_t>(nitems, 16384);
+  hipLaunchKernelGGL(mag_claim_kernel, dim3(cgrid), dim3(64), 0, stream, bits, nwords, items, nitems, pages_out,
                      pages_cap, got);
   if (total_chunks) {
     const unsigned sgrid = (unsigned)std::min<uint32_t>((total_chunks + 3) / 4, 16384);

@@ -935,7 +935,7 @@ uint64_t crc32c_scratch_words(uint64_t total_bytes, uint64_t piece_bytes) {
   return npieces * spp;
 }
 
-static int g_crc_variant = 3;  // 0: per-lane contiguous strips (v1), 1: interleaved lanes (v2),
+static int g_crc_variant = 4;  // 0: per-lane contiguous strips (v1), 1: interleaved lanes (v2),
                                // 2: v2 + table lane fold (v3), 3: 11-bit slicing, 1024 threads (v4),
                                // 4: replicated conflict-free slicing-by-4 over 64-B chunks (v5)
 

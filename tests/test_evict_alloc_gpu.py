@@ -282,3 +282,22 @@ def test_magazine_ingest_then_host_allocs_keep_pages_disjoint(gpu, tmp_path):
     for blk, d in zip(ids2[::7], datas[:40:7]):
         s.read_batch([(blk, 0, d.nbytes, out.data_ptr(), 1)], 0, True)
         assert np.array_equal(out[:d.nbytes].cpu().numpy(), d)
+
+
+@pytest.mark.parametrize("npages,nitems,want", [(512, 25, 2), (512, 150, 1), (150_064, 2000, 3), (4096, 4096, 1),
+                                                (4096, 300, 20)])
+def test_magazine_concurrent_claims_exact(gpu, npages, nitems, want):
+    """Many items claiming from one magazine at once (one wave each, CAS on bitmap words): every
+    page is handed out at most once, every item gets its pages while the magazine has them, and
+    the device bitmap keeps exactly the rest."""
+    s = _device_store(npages, 64 * KB)
+    moved = s.mag_refill(0, nitems * want)
+    assert s.mag_device_count(0) == moved >= min(npages, nitems * want)
+    got = s.mag_claim_many(0, [want] * nitems)
+    flat = [p for g in got for p in g]
+    assert len(flat) == len(set(flat)) and all(0 <= p < npages for p in flat)
+    assert len(flat) == min(moved, nitems * want)
+    if moved >= nitems * want:
+        assert all(len(g) == want for g in got)
+    assert s.mag_device_count(0) == moved - len(flat) == s.mag_pages(0)
+    assert s.mag_drain(0) == moved - len(flat) and s.mag_device_count(0) == 0

@@ -42,7 +42,7 @@ def main(argv=None) -> int:
             rows.append({"case": "crc32c_pieces", "variant": variant, "piece_MB": piece >> 20, "GB": n / 1e9,
                          "ms": t * 1e3, "GBps": n / t / 1e9})
             print(json.dumps(rows[-1]), flush=True)
-    C.set_crc_variant(3)
+    C.set_crc_variant(4)
     # sanity: variants agree
     C.set_crc_variant(1)
     v1 = C.crc32c_device(buf.data_ptr(), 64 << 20, 2 << 20, 0)
@@ -50,7 +50,7 @@ def main(argv=None) -> int:
     v3 = C.crc32c_device(buf.data_ptr(), 64 << 20, 2 << 20, 0)
     C.set_crc_variant(4)
     v5 = C.crc32c_device(buf.data_ptr(), 64 << 20, 2 << 20, 0)
-    C.set_crc_variant(3)
+    C.set_crc_variant(4)
     assert list(v1) == list(v3) == list(v5), "variants disagree"
     if hasattr(C, "crc32c_gather_device"):
         pages = [(buf.data_ptr() + i * (2 << 20), 2 << 20) for i in range(0, n // (2 << 20), 3)]
