@@ -1614,20 +1614,30 @@ std::vector<int64_t> BlockStore::device_alloc_pages(std::unique_lock<std::mutex>
   {
     std::unique_lock<std::mutex> g(ev_mu_);
     set_device();
-    claim_reserve(claim_one_, 1, want);
-    claim_one_.items_h[0] = ClaimItem{0, 0, want, 0, 0, 0};
+    // a large claim is split into pieces of <= 1024 pages: one wave each, all in parallel
+    constexpr uint32_t kPiece = 1024;
+    const uint32_t npieces = (want + kPiece - 1) / kPiece;
+    claim_reserve(claim_one_, npieces, want);
+    for (uint32_t k = 0; k < npieces; ++k)
+      claim_one_.items_h[k] = ClaimItem{0, 0, std::min(kPiece, want - k * kPiece), k * kPiece, 0, 0};
     lk.unlock();
-    hipError_t e = hipMemcpyAsync(claim_one_.items_d, claim_one_.items_h, sizeof(ClaimItem), hipMemcpyHostToDevice,
-                                  internal_stream_);
+    hipError_t e = hipMemcpyAsync(claim_one_.items_d, claim_one_.items_h, npieces * sizeof(ClaimItem),
+                                  hipMemcpyHostToDevice, internal_stream_);
     if (e == hipSuccess)
-      e = launch_mag_claim_scatter(d.mag_bits, nwords, claim_one_.items_d, 1, claim_one_.pages_d,
+      e = launch_mag_claim_scatter(d.mag_bits, nwords, claim_one_.items_d, npieces, claim_one_.pages_d,
                                    (uint32_t)claim_one_.pages_cap, claim_one_.got_d, 0, nullptr, 0, internal_stream_);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(claim_one_.got_h, claim_one_.got_d, sizeof(uint32_t), hipMemcpyDeviceToHost, internal_stream_);
+      e = hipMemcpyAsync(claim_one_.got_h, claim_one_.got_d, npieces * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                         internal_stream_);
     if (e == hipSuccess)
       e = hipMemcpyAsync(claim_one_.pages_h, claim_one_.pages_d, (size_t)want * 8, hipMemcpyDeviceToHost, internal_stream_);
     if (e == hipSuccess) e = hipStreamSynchronize(internal_stream_);
-    if (e == hipSuccess) pages.assign(claim_one_.pages_h, claim_one_.pages_h + std::min(claim_one_.got_h[0], want));
+    if (e == hipSuccess)
+      for (uint32_t k = 0; k < npieces; ++k) {
+        const ClaimItem& it = claim_one_.items_h[k];
+        const uint32_t g = std::min(claim_one_.got_h[k], it.want);
+        pages.insert(pages.end(), claim_one_.pages_h + it.page_base, claim_one_.pages_h + it.page_base + g);
+      }
     for (int64_t p : pages)
       if (p < 0 || p >= d.num_pages) e = hipErrorInvalidValue;   // never hand out a bogus page
     g.unlock();

@@ -74,7 +74,16 @@ class SyntheticUnderFileSystem(UnderFileSystem):
         root = self.root_uri.split("://", 1)[1] if "://" in self.root_uri else self.root_uri
         root = root[root.find("/"):] if "/" in root else ""
         rel = path[len(root):] if root and path.startswith(root) else path
-        return [c for c in rel.split("/") if c]
+        comps = [c for c in rel.split("/") if c]
+        if not comps or comps[0] not in self.dirs:
+            # an instance created for a file URI (a worker opening one file) has that file as its
+            # root: recognise the layout from the tail instead (<dir>/<name> or <dir>)
+            every = [c for c in path.split("/") if c]
+            if len(every) >= 2 and every[-2] in self.dirs:
+                return every[-2:]
+            if every and every[-1] in self.dirs:
+                return every[-1:]
+        return comps
 
     def _index(self, name: str) -> int | None:
         if not name.endswith(".JPEG") or len(name) != 12 or not name[:7].isdigit():

@@ -95,6 +95,8 @@ def main():
             el = time.perf_counter() - t
             res["metadata_files_per_s"] = round(a.files / el, 1)
             res["metadata_s"] = round(el, 2)
+            print(json.dumps({"phase": "metadata", "files_per_s": res["metadata_files_per_s"], "s": res["metadata_s"]}),
+                  flush=True)
             if a.skip_cache:
                 fs.close()
                 raise _Done()
@@ -109,6 +111,9 @@ def main():
             cached = 0
             for i in range(0, len(items), 4096):
                 cached += w.cache_blocks_from_ufs(items[i:i + 4096])
+                if (i // 4096) % 32 == 31:
+                    print(json.dumps({"phase": "cache", "files": i + 4096, "s": round(time.perf_counter() - t, 1)}),
+                          flush=True)
             el = time.perf_counter() - t
             res["cache_all_done"] = cached == a.files
             res["cache_files_per_s"] = round(a.files / el, 1)
@@ -116,6 +121,8 @@ def main():
             res["cache_breakdown_s"] = {k: round(v, 3) for k, v in w.bulk_stats.items()}
             ds = FileListDataset(fs, root, record_bytes=a.file_size)
             res["cached_fraction"] = round(float(np.mean([bool(f.blocks[0].locations) for f in ds.files])), 4)
+            print(json.dumps({"phase": "cached", "files_per_s": res["cache_files_per_s"],
+                              "cached_fraction": res["cached_fraction"]}), flush=True)
             # training epochs: shuffled batches gathered on the device
             dev = torch.device("cuda", 0) if gpu else torch.device("cpu")
             with DeviceBatchLoader(ds, batch_size=a.batch, shuffle=True, seed=7, device=dev) as dl:

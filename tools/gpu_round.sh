@@ -43,6 +43,7 @@ for s in $STEPS; do
       ;;
     crc) run crc_bench 300 python tools/crc_bench.py --gb 4 --out "$OUT/crc_bench.jsonl" ;;
     dl) run dl_bench_100k 400 python tools/dl_bench.py --files 100000 --out "$OUT/dl_bench_100k.jsonl" ;;
+    dl1m) run dl_bench_1m 900 python tools/dl_bench.py --ufs synthetic --files 1000000 --threads 32 --out "$OUT/dl_bench_1m.jsonl" ;;
     master)
       # CPU-only: the master metadata bench on the box's CPU share (no GPU used)
       run master_bench 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --out "$OUT/master_bench.json"
