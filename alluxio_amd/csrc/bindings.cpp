@@ -18,6 +18,7 @@
 #include "frame_rpc.h"
 #include "meta_codec.h"
 #include "fuse_server.h"
+#include "http_blob.h"
 
 namespace py = pybind11;
 using namespace amdx;
@@ -451,6 +452,7 @@ PYBIND11_MODULE(_C, m) {
              d["mag_drains"] = st.mag_drains;
              d["mag_drain_pages"] = st.mag_drain_pages;
              d["mag_short_items"] = st.mag_short_items;
+             d["ingest_ns"] = std::vector<uint64_t>(st.ingest_ns, st.ingest_ns + 6);
              return d;
            })
       .def("mag_refill", &BlockStore::mag_refill_pages, G())
@@ -544,6 +546,22 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("reopens", &RingReadSession::reopens)
       .def_property_readonly("calls", &RingReadSession::calls)
       .def_property_readonly("file_len", &RingReadSession::file_len);
+
+  // ---- native S3 data path (http_blob.cpp) --------------------------------------------------
+  py::class_<BlobServer>(m, "BlobServer")
+      .def(py::init<const std::string&, const std::string&, int>(), py::arg("root"), py::arg("host") = "127.0.0.1",
+           py::arg("port") = 0)
+      .def("start", &BlobServer::start, G())
+      .def("stop", &BlobServer::stop, G())
+      .def_property_readonly("port", &BlobServer::port)
+      .def_property_readonly("requests", &BlobServer::requests)
+      .def_property_readonly("bytes_sent", &BlobServer::bytes_sent);
+  py::class_<HttpRangeReader>(m, "HttpRangeReader")
+      .def(py::init<const std::string&, int, int>(), py::arg("host"), py::arg("port"), py::arg("max_idle") = 16)
+      .def("get_into", &HttpRangeReader::get_into, G(), py::arg("target"), py::arg("head_lines"), py::arg("offset"),
+           py::arg("length"), py::arg("dst"), py::arg("parallel") = 1, py::arg("min_part") = 4 << 20)
+      .def_property_readonly("requests", &HttpRangeReader::requests)
+      .def_property_readonly("connects", &HttpRangeReader::connects);
 
   // ---- native framed RPC (control-plane fast path) ----------------------------------------
   py::class_<FrameRpcServer>(m, "FrameRpcServer")

@@ -2080,6 +2080,14 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
   }
   std::vector<std::vector<int64_t>> pending(2);   // blocks whose copy from staging half h is in flight
   std::vector<uint8_t*> host_half(2, nullptr);
+  uint64_t phase_ns[6] = {0, 0, 0, 0, 0, 0};
+  auto tick = [t = std::chrono::steady_clock::now()](uint64_t& acc) mutable {
+    const auto now = std::chrono::steady_clock::now();
+    acc += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count();
+    t = now;
+  };
+  uint64_t scratch_ns = 0;
+  tick(scratch_ns);
   if (use_device_alloc_ && has_device_) {
     // K7: one magazine refill for the whole call up front -- a refill synchronizes the internal
     // stream, which would otherwise stall the staging double buffer once per group
@@ -2093,9 +2101,12 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
       if (sd.mag_pages < need) mag_refill(sd, need - sd.mag_pages);
     }
   }
+  tick(phase_ns[5]);
   auto finish = [&](int h) {
     if (pending[h].empty() && claim_[h].ids.empty()) return;
+    tick(phase_ns[2]);
     if (has_device_) HIP_OK(hipStreamSynchronize(st));
+    tick(phase_ns[3]);
     if (!claim_[h].ids.empty()) {
       const std::unordered_set<int64_t> failed = ingest_device_finish(session, h, lengths, host_half[h], status);
       if (!failed.empty()) {
@@ -2107,6 +2118,7 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
     }
     for (int64_t id : pending[h]) commit_block(session, id, false);
     pending[h].clear();
+    tick(phase_ns[4]);
   };
   for (size_t g = 0; g < groups.size(); ++g) {
     const int h = (int)(g & 1);
@@ -2188,6 +2200,7 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
         }
       }
     }
+    tick(phase_ns[0]);
     // 2) parallel preads into the staging half
     std::atomic<size_t> next{0};
     auto reader = [&]() {
@@ -2211,6 +2224,7 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
     for (int t = 1; t < nt; ++t) pool.emplace_back(reader);
     reader();
     for (auto& t : pool) t.join();
+    tick(phase_ns[1]);
     for (size_t k = 0; k < gix.size(); ++k)
       if (status[gix[k]] == 2) {
         try { abort_block(session, ids[gix[k]]); } catch (const StoreError&) {}
@@ -2270,6 +2284,11 @@ std::vector<int> BlockStore::ingest_files(int64_t session, const std::vector<int
   }
   finish(0);
   finish(1);
+  tick(phase_ns[2]);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int k = 0; k < 6; ++k) stats_.ingest_ns[k] += phase_ns[k];
+  }
   return status;
 }
 

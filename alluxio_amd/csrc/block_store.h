@@ -238,6 +238,9 @@ class BlockStore {
     uint64_t device_allocs = 0, device_alloc_pages = 0, annotation_flushes = 0, annotation_updates = 0;
     uint64_t demoted_blocks = 0, demoted_bytes = 0, batched_moves = 0, batched_move_blocks = 0;
     uint64_t mag_refills = 0, mag_refill_pages = 0, mag_drains = 0, mag_drain_pages = 0, mag_short_items = 0;
+    // ingest_files wall time by phase (ns): 0 block metadata/claims setup, 1 preads, 2 copy/claim
+    // launches, 3 waiting on the stream, 4 page attach + commits, 5 up-front magazine refill
+    uint64_t ingest_ns[6] = {0, 0, 0, 0, 0, 0};
   };
   EvictStats evict_stats();
 

@@ -1,0 +1,909 @@
+#include "http_blob.h"
+
+#include <arpa/inet.h>
+#include <dirent.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/sendfile.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <map>
+#include <stdexcept>
+
+namespace amdx {
+namespace {
+
+constexpr const char* kMarker = ".__s3_folder_marker";
+constexpr size_t kMaxHead = 1 << 20;
+
+bool send_all(int fd, const char* p, size_t n) {
+  while (n) {
+    const ssize_t r = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+
+bool recv_all(int fd, uint8_t* p, size_t n) {
+  while (n) {
+    const ssize_t r = ::recv(fd, p, n, 0);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    p += r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = (char)std::tolower((unsigned char)c);
+  return s;
+}
+
+std::string pct_decode(const std::string& s, bool plus_space) {
+  std::string o;
+  o.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && std::isxdigit((unsigned char)s[i + 1]) &&
+        std::isxdigit((unsigned char)s[i + 2])) {
+      o.push_back((char)std::stoi(s.substr(i + 1, 2), nullptr, 16));
+      i += 2;
+    } else if (plus_space && s[i] == '+') {
+      o.push_back(' ');
+    } else {
+      o.push_back(s[i]);
+    }
+  }
+  return o;
+}
+
+std::string xml_escape(const std::string& s) {
+  std::string o;
+  o.reserve(s.size());
+  for (char c : s) {
+    switch (c) {
+      case '&': o += "&amp;"; break;
+      case '<': o += "&lt;"; break;
+      case '>': o += "&gt;"; break;
+      case '"': o += "&quot;"; break;
+      case '\'': o += "&apos;"; break;
+      default: o.push_back(c);
+    }
+  }
+  return o;
+}
+
+std::string xml_unescape(const std::string& s) {
+  std::string o;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] != '&') {
+      o.push_back(s[i]);
+      continue;
+    }
+    const size_t e = s.find(';', i);
+    if (e == std::string::npos) {
+      o.push_back(s[i]);
+      continue;
+    }
+    const std::string ent = s.substr(i + 1, e - i - 1);
+    if (ent == "amp") o.push_back('&');
+    else if (ent == "lt") o.push_back('<');
+    else if (ent == "gt") o.push_back('>');
+    else if (ent == "quot") o.push_back('"');
+    else if (ent == "apos") o.push_back('\'');
+    else o += s.substr(i, e - i + 1);
+    i = e;
+  }
+  return o;
+}
+
+bool starts_with(const std::string& s, const std::string& p) { return s.compare(0, p.size(), p) == 0; }
+
+bool is_dir(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+bool is_file(const std::string& p, struct stat* out = nullptr) {
+  struct stat st;
+  if (::stat(p.c_str(), &st) != 0 || !S_ISREG(st.st_mode)) return false;
+  if (out) *out = st;
+  return true;
+}
+
+void mkdirs(const std::string& p) {
+  for (size_t i = 1; i <= p.size(); ++i)
+    if (i == p.size() || p[i] == '/') ::mkdir(p.substr(0, i).c_str(), 0755);
+}
+
+std::string etag_of(const struct stat& st) {
+  char b[64];
+  std::snprintf(b, sizeof b, "\"%llx-%llx\"", (unsigned long long)st.st_size,
+                (unsigned long long)st.st_mtim.tv_sec * 1000000000ull + (unsigned long long)st.st_mtim.tv_nsec);
+  return b;
+}
+
+std::string http_date(time_t t) {
+  char b[64];
+  struct tm tmv;
+  gmtime_r(&t, &tmv);
+  std::strftime(b, sizeof b, "%a, %d %b %Y %H:%M:%S GMT", &tmv);
+  return b;
+}
+
+std::string iso_date(time_t t) {
+  char b[64];
+  struct tm tmv;
+  gmtime_r(&t, &tmv);
+  std::strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%S.000Z", &tmv);
+  return b;
+}
+
+const char* reason(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 204: return "No Content";
+    case 206: return "Partial Content";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 409: return "Conflict";
+    case 416: return "Range Not Satisfiable";
+    default: return "Internal Server Error";
+  }
+}
+
+struct Entry {
+  std::string key;
+  bool prefix;
+  uint64_t size;
+  time_t mtime;
+  std::string etag;
+};
+
+// remove empty, marker-less directories from `dir` up to (not including) `stop`
+void prune(std::string dir, const std::string& stop) {
+  while (dir.size() > stop.size() && starts_with(dir, stop)) {
+    if (::rmdir(dir.c_str()) != 0) return;
+    const size_t s = dir.rfind('/');
+    if (s == std::string::npos) return;
+    dir.resize(s);
+  }
+}
+
+void walk(const std::string& fsdir, const std::string& keydir, const std::string& prefix, std::vector<Entry>& out) {
+  struct stat st;
+  if (!keydir.empty() && starts_with(keydir, prefix) && ::stat((fsdir + "/" + kMarker).c_str(), &st) == 0)
+    out.push_back({keydir, false, 0, st.st_mtim.tv_sec, "\"d41d8cd98f00b204e9800998ecf8427e\""});
+  DIR* d = ::opendir(fsdir.c_str());
+  if (!d) return;
+  while (dirent* e = ::readdir(d)) {
+    const std::string name = e->d_name;
+    if (name == "." || name == ".." || name == kMarker) continue;
+    const std::string p = fsdir + "/" + name;
+    if (::stat(p.c_str(), &st) != 0) continue;
+    if (S_ISDIR(st.st_mode)) {
+      const std::string k = keydir + name + "/";
+      if (starts_with(prefix, k) || starts_with(k, prefix)) walk(p, k, prefix, out);
+    } else if (S_ISREG(st.st_mode)) {
+      const std::string k = keydir + name;
+      if (starts_with(k, prefix)) out.push_back({k, false, (uint64_t)st.st_size, st.st_mtim.tv_sec, etag_of(st)});
+    }
+  }
+  ::closedir(d);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// BlobServer
+// ------------------------------------------------------------------------------------------------
+BlobServer::BlobServer(const std::string& root, const std::string& host, int port)
+    : root_(root), host_(host), port_(port) {
+  while (root_.size() > 1 && root_.back() == '/') root_.pop_back();
+}
+
+BlobServer::~BlobServer() { stop(); }
+
+void BlobServer::start() {
+  if (running_) return;
+  mkdirs(root_);
+  lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (lfd_ < 0) throw std::runtime_error("BlobServer: socket failed");
+  int one = 1;
+  ::setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port_);
+  if (::inet_pton(AF_INET, host_.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (::bind(lfd_, (sockaddr*)&a, sizeof a) != 0 || ::listen(lfd_, 256) != 0) {
+    ::close(lfd_);
+    lfd_ = -1;
+    throw std::runtime_error("BlobServer: bind/listen failed");
+  }
+  socklen_t len = sizeof a;
+  ::getsockname(lfd_, (sockaddr*)&a, &len);
+  port_ = ntohs(a.sin_port);
+  running_ = true;
+  acceptor_ = std::thread([this] { accept_loop(); });
+}
+
+void BlobServer::stop() {
+  if (!running_.exchange(false)) return;
+  if (acceptor_.joinable()) acceptor_.join();
+  if (lfd_ >= 0) ::close(lfd_);
+  lfd_ = -1;
+  std::vector<std::thread> ts;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int fd : fds_) ::shutdown(fd, SHUT_RDWR);
+    ts.swap(conns_);
+  }
+  for (auto& t : ts)
+    if (t.joinable()) t.join();
+  std::lock_guard<std::mutex> g(mu_);
+  fds_.clear();
+}
+
+void BlobServer::accept_loop() {
+  while (running_) {
+    pollfd p{lfd_, POLLIN, 0};
+    if (::poll(&p, 1, 200) <= 0) continue;
+    const int fd = ::accept4(lfd_, nullptr, nullptr, SOCK_CLOEXEC);
+    if (fd < 0) continue;
+    int one = 1;
+    ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    std::lock_guard<std::mutex> g(mu_);
+    if (!running_) {
+      ::close(fd);
+      break;
+    }
+    fds_.push_back(fd);
+    conns_.emplace_back([this, fd] { serve(fd); });
+  }
+}
+
+void BlobServer::serve(int fd) {
+  try {
+    serve_conn(fd);
+  } catch (...) {
+    // a malformed request ends the connection
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    fds_.erase(std::remove(fds_.begin(), fds_.end(), fd), fds_.end());
+  }
+  ::close(fd);
+}
+
+void BlobServer::serve_conn(int fd) {
+  std::string buf;
+  std::vector<char> tmp(1 << 16);
+  auto recv_more = [&]() -> bool {
+    const ssize_t r = ::recv(fd, tmp.data(), tmp.size(), 0);
+    if (r <= 0) return false;
+    buf.append(tmp.data(), (size_t)r);
+    return true;
+  };
+  while (running_) {
+    size_t hend;
+    while ((hend = buf.find("\r\n\r\n")) == std::string::npos) {
+      if (buf.size() > kMaxHead || !recv_more()) goto done;
+    }
+    {
+      const std::string head = buf.substr(0, hend);
+      buf.erase(0, hend + 4);
+      ++requests_;
+      // request line + headers
+      const size_t le = head.find("\r\n");
+      const std::string line = head.substr(0, le);
+      const size_t s1 = line.find(' '), s2 = line.rfind(' ');
+      if (s1 == std::string::npos || s2 <= s1) goto done;
+      const std::string method = line.substr(0, s1);
+      const std::string target = line.substr(s1 + 1, s2 - s1 - 1);
+      std::map<std::string, std::string> h;
+      for (size_t p = le == std::string::npos ? head.size() : le + 2; p < head.size();) {
+        size_t e = head.find("\r\n", p);
+        if (e == std::string::npos) e = head.size();
+        const std::string l = head.substr(p, e - p);
+        const size_t c = l.find(':');
+        if (c != std::string::npos) {
+          size_t v = c + 1;
+          while (v < l.size() && l[v] == ' ') ++v;
+          h[lower(l.substr(0, c))] = l.substr(v);
+        }
+        p = e + 2;
+      }
+      const uint64_t clen = h.count("content-length") ? std::stoull(h["content-length"]) : 0;
+      const bool keep = lower(h.count("connection") ? h["connection"] : "") != "close";
+      uint64_t body_left = clen;
+      // body helpers: the first bytes may already sit in buf
+      auto body_string = [&]() -> std::string {
+        std::string out;
+        while (body_left) {
+          if (buf.empty() && !recv_more()) break;
+          const size_t k = (size_t)std::min<uint64_t>(body_left, buf.size());
+          out.append(buf, 0, k);
+          buf.erase(0, k);
+          body_left -= k;
+        }
+        return out;
+      };
+      auto body_to_fd = [&](int out) -> bool {
+        bool ok = true;
+        while (body_left) {
+          if (buf.empty() && !recv_more()) return false;
+          const size_t k = (size_t)std::min<uint64_t>(body_left, buf.size());
+          size_t w = 0;
+          while (ok && w < k) {
+            const ssize_t r = ::write(out, buf.data() + w, k - w);
+            if (r <= 0) ok = false;
+            else w += (size_t)r;
+          }
+          buf.erase(0, k);
+          body_left -= k;
+        }
+        return ok;
+      };
+      auto reply = [&](int code, const std::string& extra, const std::string& body, bool head_only = false,
+                       int64_t len = -1) -> bool {
+        std::string r = "HTTP/1.1 " + std::to_string(code) + " " + reason(code) + "\r\nContent-Length: " +
+                        std::to_string(len >= 0 ? (uint64_t)len : body.size()) +
+                        "\r\nServer: alluxio-amd-blob\r\n" + extra + "\r\n";
+        if (!head_only) r += body;
+        return send_all(fd, r.data(), r.size());
+      };
+      auto error = [&](int code, const std::string& what, const std::string& msg) -> bool {
+        return reply(code, "Content-Type: application/xml\r\n",
+                     "<?xml version=\"1.0\" encoding=\"UTF-8\"?><Error><Code>" + what + "</Code><Message>" +
+                         xml_escape(msg) + "</Message></Error>",
+                     method == "HEAD");
+      };
+      // target -> bucket / key / query
+      const size_t qm = target.find('?');
+      const std::string path = pct_decode(target.substr(0, qm), false);
+      std::map<std::string, std::string> q;
+      if (qm != std::string::npos) {
+        const std::string qs = target.substr(qm + 1);
+        for (size_t p = 0; p <= qs.size();) {
+          size_t e = qs.find('&', p);
+          if (e == std::string::npos) e = qs.size();
+          const std::string kv = qs.substr(p, e - p);
+          if (!kv.empty()) {
+            const size_t eq = kv.find('=');
+            q[pct_decode(kv.substr(0, eq), true)] = eq == std::string::npos ? "" : pct_decode(kv.substr(eq + 1), true);
+          }
+          p = e + 1;
+        }
+      }
+      std::string rest = path.size() > 1 ? path.substr(1) : "";
+      const size_t sl = rest.find('/');
+      const std::string bucket = rest.substr(0, sl);
+      const std::string key = sl == std::string::npos ? "" : rest.substr(sl + 1);
+      bool bad = bucket.empty() || bucket[0] == '.' || key.find('\0') != std::string::npos;
+      for (size_t p = 0; !bad && p <= key.size();) {
+        size_t e = key.find('/', p);
+        if (e == std::string::npos) e = key.size();
+        const std::string comp = key.substr(p, e - p);
+        if (comp == ".." || comp == "." || comp == kMarker) bad = true;
+        p = e + 1;
+      }
+      bool ok = true;
+      const std::string bdir = root_ + "/" + bucket;
+      const bool marker_key = !key.empty() && key.back() == '/';
+      const std::string fpath = bdir + "/" + (marker_key ? key.substr(0, key.size() - 1) : key);
+      if (bad) {
+        body_string();
+        ok = error(400, "InvalidArgument", "bad bucket or key");
+      } else if (key.empty()) {
+        // ---- bucket operations ----
+        if (method == "PUT") {
+          body_string();
+          mkdirs(bdir);
+          ok = reply(200, "", "");
+        } else if (method == "HEAD") {
+          ok = is_dir(bdir) ? reply(200, "", "", true) : error(404, "NoSuchBucket", bucket);
+        } else if (method == "POST" && q.count("delete")) {
+          const std::string body = body_string();
+          for (size_t p = 0; (p = body.find("<Key>", p)) != std::string::npos;) {
+            const size_t e = body.find("</Key>", p);
+            if (e == std::string::npos) break;
+            const std::string k = xml_unescape(body.substr(p + 5, e - p - 5));
+            p = e;
+            if (k.empty() || k.find("..") != std::string::npos) continue;
+            if (k.back() == '/') {
+              const std::string d = bdir + "/" + k.substr(0, k.size() - 1);
+              ::unlink((d + "/" + kMarker).c_str());
+              prune(d, bdir);
+            } else {
+              const std::string f = bdir + "/" + k;
+              if (::unlink(f.c_str()) == 0) prune(f.substr(0, f.rfind('/')), bdir);
+            }
+          }
+          ok = reply(200, "Content-Type: application/xml\r\n",
+                     "<?xml version=\"1.0\" encoding=\"UTF-8\"?><DeleteResult></DeleteResult>");
+        } else if (method == "GET") {
+          if (!is_dir(bdir)) {
+            ok = error(404, "NoSuchBucket", bucket);
+          } else {
+            const std::string prefix = q.count("prefix") ? q["prefix"] : "";
+            const std::string delim = q.count("delimiter") ? q["delimiter"] : "";
+            std::string after = q.count("continuation-token") ? q["continuation-token"]
+                                                              : (q.count("start-after") ? q["start-after"] : "");
+            const size_t max_keys = q.count("max-keys") ? (size_t)std::max(1L, std::stol(q["max-keys"])) : 1000;
+            std::vector<Entry> ents;
+            if (prefix.find("..") != std::string::npos) {
+              // nothing matches
+            } else if (delim == "/") {
+              const size_t cut = prefix.rfind('/');
+              const std::string dirpart = cut == std::string::npos ? "" : prefix.substr(0, cut + 1);
+              const std::string base = prefix.substr(dirpart.size());
+              const std::string fsdir = bdir + (dirpart.empty() ? "" : "/" + dirpart.substr(0, dirpart.size() - 1));
+              struct stat st;
+              if (base.empty() && !dirpart.empty() && ::stat((fsdir + "/" + kMarker).c_str(), &st) == 0)
+                ents.push_back({dirpart, false, 0, st.st_mtim.tv_sec, "\"d41d8cd98f00b204e9800998ecf8427e\""});
+              if (DIR* d = ::opendir(fsdir.c_str())) {
+                while (dirent* e = ::readdir(d)) {
+                  const std::string name = e->d_name;
+                  if (name == "." || name == ".." || name == kMarker || !starts_with(name, base)) continue;
+                  const std::string p = fsdir + "/" + name;
+                  if (::stat(p.c_str(), &st) != 0) continue;
+                  if (S_ISDIR(st.st_mode)) ents.push_back({dirpart + name + "/", true, 0, 0, ""});
+                  else if (S_ISREG(st.st_mode))
+                    ents.push_back({dirpart + name, false, (uint64_t)st.st_size, st.st_mtim.tv_sec, etag_of(st)});
+                }
+                ::closedir(d);
+              }
+            } else {
+              walk(bdir, "", prefix, ents);
+            }
+            std::sort(ents.begin(), ents.end(), [](const Entry& a, const Entry& b) { return a.key < b.key; });
+            std::string x = "<?xml version=\"1.0\" encoding=\"UTF-8\"?><ListBucketResult "
+                            "xmlns=\"http://s3.amazonaws.com/doc/2006-03-01/\"><Name>" +
+                            xml_escape(bucket) + "</Name><Prefix>" + xml_escape(prefix) + "</Prefix>";
+            if (!delim.empty()) x += "<Delimiter>" + xml_escape(delim) + "</Delimiter>";
+            std::string items, last;
+            size_t n = 0;
+            bool truncated = false;
+            for (const Entry& e : ents) {
+              if (!after.empty() && e.key <= after) continue;
+              if (n == max_keys) {
+                truncated = true;
+                break;
+              }
+              ++n;
+              last = e.key;
+              if (e.prefix) {
+                items += "<CommonPrefixes><Prefix>" + xml_escape(e.key) + "</Prefix></CommonPrefixes>";
+              } else {
+                items += "<Contents><Key>" + xml_escape(e.key) + "</Key><LastModified>" + iso_date(e.mtime) +
+                         "</LastModified><ETag>" + xml_escape(e.etag) + "</ETag><Size>" + std::to_string(e.size) +
+                         "</Size><StorageClass>STANDARD</StorageClass></Contents>";
+              }
+            }
+            x += "<KeyCount>" + std::to_string(n) + "</KeyCount><MaxKeys>" + std::to_string(max_keys) +
+                 "</MaxKeys><IsTruncated>" + (truncated ? "true" : "false") + "</IsTruncated>";
+            if (truncated) x += "<NextContinuationToken>" + xml_escape(last) + "</NextContinuationToken>";
+            x += items + "</ListBucketResult>";
+            ok = reply(200, "Content-Type: application/xml\r\n", x);
+          }
+        } else {
+          body_string();
+          ok = error(400, "InvalidRequest", method);
+        }
+      } else if (q.count("uploads") && method == "POST") {
+        // ---- multipart upload ----
+        body_string();
+        const std::string id = std::to_string(++upload_seq_) + "-" + std::to_string((long long)::time(nullptr));
+        mkdirs(root_ + "/.uploads/" + id);
+        ok = reply(200, "Content-Type: application/xml\r\n",
+                   "<?xml version=\"1.0\" encoding=\"UTF-8\"?><InitiateMultipartUploadResult><Bucket>" +
+                       xml_escape(bucket) + "</Bucket><Key>" + xml_escape(key) + "</Key><UploadId>" + id +
+                       "</UploadId></InitiateMultipartUploadResult>");
+      } else if (q.count("uploadId")) {
+        const std::string id = q["uploadId"];
+        const std::string udir = root_ + "/.uploads/" + id;
+        if (id.find('/') != std::string::npos || id.find("..") != std::string::npos || !is_dir(udir)) {
+          body_string();
+          ok = error(404, "NoSuchUpload", id);
+        } else if (method == "PUT" && q.count("partNumber")) {
+          const int pn = std::atoi(q["partNumber"].c_str());
+          char name[32];
+          std::snprintf(name, sizeof name, "/%08d", pn);
+          const int out = ::open((udir + name).c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+          const bool wrote = out >= 0 && body_to_fd(out);
+          if (out >= 0) ::close(out);
+          if (!wrote) {
+            body_string();
+            ok = error(500, "InternalError", "part write failed");
+          } else {
+            ok = reply(200, "ETag: \"part" + std::to_string(pn) + "\"\r\n", "");
+          }
+        } else if (method == "POST") {
+          body_string();
+          std::vector<std::string> parts;
+          if (DIR* d = ::opendir(udir.c_str())) {
+            while (dirent* e = ::readdir(d))
+              if (e->d_name[0] != '.') parts.push_back(e->d_name);
+            ::closedir(d);
+          }
+          std::sort(parts.begin(), parts.end());
+          mkdirs(fpath.substr(0, fpath.rfind('/')));
+          const std::string tmpf = fpath + ".__upload";
+          const int out = ::open(tmpf.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+          bool good = out >= 0;
+          for (const std::string& p : parts) {
+            const int in = ::open((udir + "/" + p).c_str(), O_RDONLY | O_CLOEXEC);
+            struct stat st;
+            if (in < 0 || ::fstat(in, &st) != 0) {
+              good = false;
+            } else {
+              off_t o = 0;
+              while (good && o < st.st_size) {
+                const ssize_t r = ::sendfile(out, in, &o, (size_t)(st.st_size - o));
+                if (r <= 0) good = false;
+              }
+            }
+            if (in >= 0) ::close(in);
+            ::unlink((udir + "/" + p).c_str());
+          }
+          if (out >= 0) ::close(out);
+          ::rmdir(udir.c_str());
+          struct stat st;
+          if (good && ::rename(tmpf.c_str(), fpath.c_str()) == 0 && is_file(fpath, &st)) {
+            ok = reply(200, "Content-Type: application/xml\r\n",
+                       "<?xml version=\"1.0\" encoding=\"UTF-8\"?><CompleteMultipartUploadResult><Bucket>" +
+                           xml_escape(bucket) + "</Bucket><Key>" + xml_escape(key) + "</Key><ETag>" +
+                           xml_escape(etag_of(st)) + "</ETag></CompleteMultipartUploadResult>");
+          } else {
+            ::unlink(tmpf.c_str());
+            ok = error(500, "InternalError", "complete failed");
+          }
+        } else if (method == "DELETE") {
+          if (DIR* d = ::opendir(udir.c_str())) {
+            while (dirent* e = ::readdir(d))
+              if (e->d_name[0] != '.') ::unlink((udir + "/" + e->d_name).c_str());
+            ::closedir(d);
+          }
+          ::rmdir(udir.c_str());
+          ok = reply(204, "", "");
+        } else {
+          body_string();
+          ok = error(400, "InvalidRequest", method);
+        }
+      } else if (method == "GET" || method == "HEAD") {
+        // ---- object reads ----
+        struct stat st;
+        if (marker_key) {
+          if (::stat((fpath + "/" + kMarker).c_str(), &st) == 0)
+            ok = reply(200, "ETag: \"d41d8cd98f00b204e9800998ecf8427e\"\r\nLast-Modified: " + http_date(st.st_mtim.tv_sec) +
+                                "\r\n",
+                       "", method == "HEAD");
+          else
+            ok = error(404, "NoSuchKey", key);
+        } else if (!is_file(fpath, &st)) {
+          ok = error(404, "NoSuchKey", key);
+        } else {
+          const uint64_t size = (uint64_t)st.st_size;
+          uint64_t a = 0, b = size ? size - 1 : 0;
+          bool ranged = false, unsat = false;
+          if (h.count("range") && starts_with(h["range"], "bytes=")) {
+            const std::string r = h["range"].substr(6);
+            const size_t dash = r.find('-');
+            if (dash != std::string::npos) {
+              ranged = true;
+              if (dash == 0) {  // suffix range
+                const uint64_t n = std::stoull(r.substr(1));
+                a = n >= size ? 0 : size - n;
+              } else {
+                a = std::stoull(r.substr(0, dash));
+                if (dash + 1 < r.size()) b = std::min<uint64_t>(std::stoull(r.substr(dash + 1)), size ? size - 1 : 0);
+              }
+              unsat = a >= size || b < a;
+            }
+          }
+          const std::string common = "ETag: " + etag_of(st) + "\r\nLast-Modified: " + http_date(st.st_mtim.tv_sec) +
+                                     "\r\nAccept-Ranges: bytes\r\nContent-Type: application/octet-stream\r\n";
+          if (ranged && unsat) {
+            ok = reply(416, "Content-Range: bytes */" + std::to_string(size) + "\r\n", "", method == "HEAD");
+          } else {
+            const uint64_t n = size ? b - a + 1 : 0;
+            const int code = ranged ? 206 : 200;
+            std::string extra = common;
+            if (ranged)
+              extra += "Content-Range: bytes " + std::to_string(a) + "-" + std::to_string(b) + "/" + std::to_string(size) +
+                       "\r\n";
+            ok = reply(code, extra, "", true, (int64_t)n);
+            if (ok && method == "GET" && n) {
+              const int in = ::open(fpath.c_str(), O_RDONLY | O_CLOEXEC);
+              if (in < 0) {
+                ok = false;
+              } else {
+                off_t o = (off_t)a;
+                uint64_t left = n;
+                while (left) {
+                  const ssize_t r = ::sendfile(fd, in, &o, (size_t)std::min<uint64_t>(left, 1ull << 30));
+                  if (r < 0 && (errno == EINTR || errno == EAGAIN)) continue;
+                  if (r <= 0) break;
+                  left -= (uint64_t)r;
+                  bytes_ += (uint64_t)r;
+                }
+                ::close(in);
+                ok = left == 0;
+              }
+            }
+          }
+        }
+      } else if (method == "PUT") {
+        // ---- object writes ----
+        if (h.count("x-amz-copy-source")) {
+          body_string();
+          std::string srcp = pct_decode(h["x-amz-copy-source"], false);
+          if (!srcp.empty() && srcp[0] == '/') srcp = srcp.substr(1);
+          struct stat st;
+          const std::string sfile = root_ + "/" + srcp;
+          if (srcp.find("..") != std::string::npos) {
+            ok = error(400, "InvalidArgument", srcp);
+          } else if (!srcp.empty() && srcp.back() == '/') {
+            mkdirs(fpath);
+            const int m = ::open((fpath + "/" + kMarker).c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+            if (m >= 0) ::close(m);
+            ok = reply(200, "Content-Type: application/xml\r\n", "<CopyObjectResult></CopyObjectResult>");
+          } else if (!is_file(sfile, &st)) {
+            ok = error(404, "NoSuchKey", srcp);
+          } else {
+            mkdirs(fpath.substr(0, fpath.rfind('/')));
+            const std::string tmpf = fpath + ".__copy";
+            const int in = ::open(sfile.c_str(), O_RDONLY | O_CLOEXEC);
+            const int out = ::open(tmpf.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+            bool good = in >= 0 && out >= 0;
+            off_t o = 0;
+            while (good && o < st.st_size) {
+              const ssize_t r = ::sendfile(out, in, &o, (size_t)(st.st_size - o));
+              if (r <= 0) good = false;
+            }
+            if (in >= 0) ::close(in);
+            if (out >= 0) ::close(out);
+            if (good && ::rename(tmpf.c_str(), fpath.c_str()) == 0 && is_file(fpath, &st)) {
+              ok = reply(200, "Content-Type: application/xml\r\n",
+                         "<CopyObjectResult><ETag>" + xml_escape(etag_of(st)) + "</ETag><LastModified>" +
+                             iso_date(st.st_mtim.tv_sec) + "</LastModified></CopyObjectResult>");
+            } else {
+              ::unlink(tmpf.c_str());
+              ok = error(500, "InternalError", "copy failed");
+            }
+          }
+        } else if (marker_key) {
+          body_string();
+          mkdirs(fpath);
+          const int m = ::open((fpath + "/" + kMarker).c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+          if (m >= 0) ::close(m);
+          ok = reply(200, "ETag: \"d41d8cd98f00b204e9800998ecf8427e\"\r\n", "");
+        } else if (is_dir(fpath)) {
+          body_string();
+          ok = error(409, "InvalidRequest", "a prefix of that name exists");
+        } else {
+          mkdirs(fpath.substr(0, fpath.rfind('/')));
+          const std::string tmpf = fpath + ".__put" + std::to_string(++upload_seq_);
+          const int out = ::open(tmpf.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+          const bool wrote = out >= 0 && body_to_fd(out);
+          if (out >= 0) ::close(out);
+          struct stat st;
+          if (wrote && ::rename(tmpf.c_str(), fpath.c_str()) == 0 && is_file(fpath, &st)) {
+            ok = reply(200, "ETag: " + etag_of(st) + "\r\n", "");
+          } else {
+            ::unlink(tmpf.c_str());
+            body_string();
+            ok = error(500, "InternalError", "write failed");
+          }
+        }
+      } else if (method == "DELETE") {
+        body_string();
+        if (marker_key) {
+          ::unlink((fpath + "/" + kMarker).c_str());
+          prune(fpath, bdir);
+        } else if (::unlink(fpath.c_str()) == 0) {
+          prune(fpath.substr(0, fpath.rfind('/')), bdir);
+        }
+        ok = reply(204, "", "");
+      } else {
+        body_string();
+        ok = error(400, "InvalidRequest", method);
+      }
+      if (!ok || !keep) goto done;
+    }
+  }
+done:
+  return;
+}
+
+// ------------------------------------------------------------------------------------------------
+// HttpRangeReader
+// ------------------------------------------------------------------------------------------------
+HttpRangeReader::HttpRangeReader(const std::string& host, int port, int max_idle)
+    : host_(host), port_(port), max_idle_((size_t)std::max(1, max_idle)) {}
+
+HttpRangeReader::~HttpRangeReader() {
+  for (int fd : idle_) ::close(fd);
+}
+
+int HttpRangeReader::take(bool& reused) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!idle_.empty()) {
+      const int fd = idle_.back();
+      idle_.pop_back();
+      reused = true;
+      return fd;
+    }
+  }
+  reused = false;
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  if (::getaddrinfo(host_.c_str(), std::to_string(port_).c_str(), &hints, &res) != 0 || !res) return -1;
+  const int fd = ::socket(res->ai_family, res->ai_socktype | SOCK_CLOEXEC, res->ai_protocol);
+  if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) != 0) {
+    ::close(fd);
+    ::freeaddrinfo(res);
+    return -1;
+  }
+  ::freeaddrinfo(res);
+  if (fd < 0) return -1;
+  int one = 1;
+  ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  int rcv = 8 << 20;
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rcv, sizeof rcv);
+  ++connects_;
+  return fd;
+}
+
+void HttpRangeReader::give(int fd) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (idle_.size() < max_idle_) idle_.push_back(fd);
+  else ::close(fd);
+}
+
+int64_t HttpRangeReader::one(const std::string& target, const std::string& head, uint64_t off, uint64_t len,
+                             uint8_t* dst) {
+  const std::string req = "GET " + target + " HTTP/1.1\r\n" + head +
+                          "Range: bytes=" + std::to_string(off) + "-" + std::to_string(off + len - 1) + "\r\n\r\n";
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    bool reused = false;
+    const int fd = take(reused);
+    if (fd < 0) return -1;
+    ++requests_;
+    if (!send_all(fd, req.data(), req.size())) {
+      ::close(fd);
+      if (reused) continue;
+      return -1;
+    }
+    std::string hb;
+    char tmp[16384];
+    size_t hend = std::string::npos;
+    bool fail = false;
+    while ((hend = hb.find("\r\n\r\n")) == std::string::npos) {
+      const ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0 || hb.size() > kMaxHead) {
+        fail = true;
+        break;
+      }
+      hb.append(tmp, (size_t)r);
+    }
+    if (fail) {
+      ::close(fd);
+      if (reused && hb.empty()) continue;   // a pooled connection the server had closed
+      return -1;
+    }
+    int code = 0;
+    if (hb.size() > 12) code = std::atoi(hb.c_str() + 9);
+    uint64_t clen = 0;
+    bool close_after = false;
+    for (size_t p = hb.find("\r\n"); p != std::string::npos && p < hend;) {
+      const size_t e = hb.find("\r\n", p + 2);
+      const std::string l = lower(hb.substr(p + 2, e - p - 2));
+      if (starts_with(l, "content-length:")) clen = std::stoull(l.substr(15));
+      if (starts_with(l, "connection:") && l.find("close") != std::string::npos) close_after = true;
+      p = e;
+    }
+    const size_t have = hb.size() - (hend + 4);
+    const uint8_t* pre = reinterpret_cast<const uint8_t*>(hb.data() + hend + 4);
+    // the body: the requested range lands in dst, anything else is drained
+    uint64_t skip = 0, take_n = 0;
+    int64_t result;
+    if ((code == 206 && clen == len) || (code == 200 && clen == len && off == 0)) {
+      take_n = len;
+      result = (int64_t)len;
+    } else if (code == 200 && clen >= off + len) {
+      skip = off;              // the server ignored the range: the object from byte 0
+      take_n = len;
+      result = (int64_t)len;
+    } else {
+      result = code ? -(int64_t)code : -1;
+    }
+    uint64_t pos = 0;          // body bytes consumed
+    auto consume = [&](const uint8_t* p, size_t n) {
+      for (size_t i = 0; i < n;) {
+        if (pos < skip) {
+          const size_t k = (size_t)std::min<uint64_t>(skip - pos, n - i);
+          pos += k;
+          i += k;
+        } else if (pos < skip + take_n) {
+          const size_t k = (size_t)std::min<uint64_t>(skip + take_n - pos, n - i);
+          std::memcpy(dst + (pos - skip), p + i, k);
+          pos += k;
+          i += k;
+        } else {
+          pos += n - i;
+          i = n;
+        }
+      }
+    };
+    consume(pre, (size_t)std::min<uint64_t>(have, clen));
+    bool ok = true;
+    while (ok && pos < clen) {
+      if (pos >= skip && pos < skip + take_n) {
+        // straight into the destination
+        const size_t k = (size_t)(skip + take_n - pos);
+        if (!recv_all(fd, dst + (pos - skip), k)) ok = false;
+        else pos += k;
+      } else {
+        const size_t k = (size_t)std::min<uint64_t>(clen - pos, sizeof tmp);
+        const ssize_t r = ::recv(fd, tmp, k, 0);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) ok = false;
+        else consume(reinterpret_cast<const uint8_t*>(tmp), (size_t)r);
+      }
+    }
+    if (!ok) {
+      ::close(fd);
+      return -1;
+    }
+    if (close_after) ::close(fd);
+    else give(fd);
+    return result;
+  }
+  return -1;
+}
+
+int64_t HttpRangeReader::get_into(const std::string& target, const std::string& head_lines, uint64_t offset,
+                                  uint64_t length, uint64_t dst, int parallel, uint64_t min_part) {
+  if (!length) return 0;
+  uint8_t* const out = reinterpret_cast<uint8_t*>(dst);
+  min_part = std::max<uint64_t>(min_part, 64 << 10);
+  const uint64_t nparts = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, parallel),
+                                                                   (length + min_part - 1) / min_part));
+  uint64_t part = (length + nparts - 1) / nparts;
+  part = (part + (64 << 10) - 1) & ~uint64_t((64 << 10) - 1);
+  std::vector<int64_t> res((size_t)nparts, 0);
+  std::vector<std::thread> ts;
+  for (uint64_t i = 1; i < nparts; ++i) {
+    const uint64_t a = i * part;
+    if (a >= length) break;
+    const uint64_t n = std::min(part, length - a);
+    ts.emplace_back([&, i, a, n] { res[(size_t)i] = one(target, head_lines, offset + a, n, out + a); });
+  }
+  res[0] = one(target, head_lines, offset, std::min(part, length), out);
+  for (auto& t : ts) t.join();
+  for (int64_t r : res)
+    if (r < 0) return r;
+  return (int64_t)length;
+}
+
+}  // namespace amdx

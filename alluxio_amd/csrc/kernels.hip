@@ -1668,6 +1668,334 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_groups_kernel(const
   }
 }
 
+// Variants 19-22: window-parallel decode, one wave per chunk.  The kernels above walk the token
+// stream one sequence at a time, so a chunk costs (sequences x per-sequence latency): ~10k
+// sequences per 64 KiB of text at 1-2k cycles each, and at <= 4k chunks there are not enough
+// chunks to hide that (profiles/r2_lz4.md).  Here every step of the wave covers a 64-byte window
+// of the compressed stream:
+//   1. candidate parse — lane l decodes a sequence header as if a token started at ip + l
+//      (lengths, offset, next-token position), all 64 in parallel from an LDS input stage;
+//   2. walk — the true token chain from ip is followed through the candidates with readlane
+//      (a handful of scalar instructions per sequence instead of the ~140 of the uniform parse),
+//      each accepted token gets its window output offset by writelane, until TMAX output bytes;
+//   3. codes — each token lane writes one code per output byte: literal (stage index), earlier
+//      output (absolute position) or a reference into this window, then references are resolved
+//      by pointer jumping in blocks of 64 (earlier blocks are final, so chains only double within
+//      one block);
+//   4. gather — bytes come from the stage, the R-byte LDS ring (recent output) or HBM (older
+//      output, already flushed and fenced), and land in the ring; the ring is flushed to HBM in
+//      aligned 16-byte vectors every 1 KiB.
+// Sequences whose header or output does not fit a window (long literal runs, long matches) go
+// through a per-sequence path that copies with all 64 lanes straight from HBM.
+template <uint32_t R, uint32_t S, uint32_t TMAX>
+__global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const Lz4Chunk* __restrict__ ch,
+                                                                          int n, int32_t* __restrict__ out_sizes) {
+  static_assert((R & (R - 1)) == 0 && R >= 4096 && S % 1024 == 0 && TMAX % 64 == 0, "window kernel shape");
+  constexpr uint32_t rmask = R - 1;
+  constexpr uint32_t NB = TMAX / 64;
+  constexpr uint32_t kInc = 1u << 24, kFinal = 1u << 25, kErrShift = 26, kNxt = 0xFFFFFFu;
+  constexpr uint32_t kRef = 0x80000000u, kOld = 0x40000000u, kVal = 0x3FFFFFFFu;
+  constexpr uint32_t kFlush = 1024;
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) v4u gu4;
+  __shared__ __attribute__((aligned(16))) uint8_t stage[S + 32];
+  __shared__ __attribute__((aligned(16))) uint8_t ring[R];
+  __shared__ uint32_t code[TMAX];
+  const uint32_t lane = threadIdx.x;
+  for (int w = blockIdx.x; w < n; w += gridDim.x) {
+    const gu8* __restrict__ src = reinterpret_cast<const gu8*>(ch[w].src);
+    const uint32_t slen = ch[w].src_bytes;
+    gu8* const dst = reinterpret_cast<gu8*>(ch[w].dst);
+    const uint32_t cap = ch[w].dst_capacity;
+    const uint64_t daddr = reinterpret_cast<uint64_t>(dst);
+    const uint32_t aoff = (uint32_t)daddr & 15u;
+    // ring slot of output position pos, aligned to the destination address so that 16-byte
+    // address granules are 16-byte ring granules
+    auto ridx = [&](uint32_t pos) -> uint32_t { return (pos + aoff) & rmask; };
+    uint32_t ip = 0, op = 0, flushed = 0, fenced = 0, vend = 0;
+    int32_t sbase = 0;   // stage[0] holds input byte sbase (-15..0 for the first stage)
+    bool at_end = false;
+    int32_t status = 0;
+
+    auto refill = [&](uint32_t pos) {
+      const uint64_t a = (reinterpret_cast<uint64_t>(src) + pos) & ~15ull;
+      const uint64_t send = reinterpret_cast<uint64_t>(src) + slen;
+      lz_wave_sync();
+      // 16-byte granules that hold at least one stream byte: never cross a page the stream
+      // does not touch
+      for (uint32_t g = lane; g < S / 16; g += kLzThreads) {
+        const uint64_t ga = a + 16ull * g;
+        if (ga < send) *reinterpret_cast<v4u*>(stage + 16 * g) = *reinterpret_cast<const gu4*>(ga);
+      }
+      sbase = (int32_t)(int64_t)(a - reinterpret_cast<uint64_t>(src));
+      const uint32_t left = (uint32_t)((int32_t)slen - sbase);
+      vend = left < S ? left : S;
+      at_end = (int32_t)vend + sbase == (int32_t)slen;
+      lz_wave_sync();
+    };
+    // output bytes [lo, hi) from the ring to HBM: whole 16-byte granules as vectors, the
+    // partial granules at the ends bytewise
+    auto flush = [&](uint32_t lo, uint32_t hi) {
+      if (hi <= lo) return;
+      const uint64_t b0 = daddr + lo, b1 = daddr + hi;
+      const uint64_t a0 = b0 & ~15ull;
+      const uint32_t ng = (uint32_t)((b1 - a0 + 15) >> 4);
+      for (uint32_t g = lane; g < ng; g += kLzThreads) {
+        const uint64_t ga = a0 + 16ull * g;
+        if (ga >= b0 && ga + 16 <= b1) {
+          *reinterpret_cast<gu4*>(ga) = *reinterpret_cast<const v4u*>(ring + ridx((uint32_t)(ga - daddr)));
+        } else {
+          for (uint32_t j = 0; j < 16; ++j) {
+            const uint64_t ba = ga + j;
+            if (ba >= b0 && ba < b1) *reinterpret_cast<gu8*>(ba) = ring[ridx((uint32_t)(ba - daddr))];
+          }
+        }
+      }
+    };
+    // one sequence at ip with all 64 lanes straight from HBM (headers/literals too long for the
+    // stage, outputs longer than TMAX); output goes to HBM and the ring; returns false when done
+    auto slow_sequence = [&]() -> bool {
+      flush(flushed, op);
+      auto gb = [&](uint32_t pos) -> uint32_t { return (uint32_t)src[pos]; };
+      // 255-terminated length extension, 64 bytes per step
+      auto ext = [&](uint32_t& p, uint32_t& acc) -> bool {
+        for (;;) {
+          if (p >= slen) return false;
+          const uint32_t idx = p + lane;
+          const uint32_t b = idx < slen ? gb(idx) : 0u;
+          const uint64_t stop = __ballot(idx >= slen || b != 255u);
+          if (!stop) {
+            acc += 255u * kLzThreads;
+            p += kLzThreads;
+            continue;
+          }
+          const uint32_t f = (uint32_t)__builtin_ctzll(stop);
+          if (p + f >= slen) return false;
+          acc += 255u * f + (uint32_t)__builtin_amdgcn_readlane((int)b, (int)f);
+          p += f + 1;
+          return true;
+        }
+      };
+      const uint32_t t = gb(ip);
+      uint32_t p = ip + 1, lit = t >> 4;
+      if (lit == 15 && !ext(p, lit)) { status = -1; return false; }
+      if (p + lit > slen || op + lit > cap) { status = -2; return false; }
+#pragma unroll 8
+      for (uint32_t i = lane; i < lit; i += kLzThreads) {
+        const uint8_t v = src[p + i];
+        dst[op + i] = v;
+        ring[ridx(op + i)] = v;
+      }
+      p += lit;
+      op += lit;
+      if (p >= slen) { ip = p; flushed = op; return false; }
+      if (p + 2 > slen) { status = -3; return false; }
+      const uint32_t off = gb(p) | (gb(p + 1) << 8);
+      p += 2;
+      uint32_t ml = t & 15u;
+      if (ml == 15 && !ext(p, ml)) { status = -4; return false; }
+      ml += 4;
+      if (off == 0 || off > op || op + ml > cap) { status = -5; return false; }
+      lz_wave_sync();
+      if (off <= R) {
+        const uint32_t lmod = off < kLzThreads ? lane % off : lane;
+        for (uint32_t b0 = 0; b0 < ml; b0 += kLzThreads) {
+          const uint32_t i = b0 + lane;
+          uint8_t v = 0;
+          if (i < ml) v = ring[ridx(off >= kLzThreads ? op + i - off : op + b0 - off + lmod)];
+          lz_wave_sync();
+          if (i < ml) {
+            dst[op + i] = v;
+            ring[ridx(op + i)] = v;
+          }
+          lz_wave_sync();
+        }
+      } else {
+        // far: the source is HBM output (all of it stored by now); fence before the first
+        // round and whenever a round reads output this match stored
+        for (uint32_t b0 = 0; b0 < ml; b0 += kLzThreads) {
+          if (op + b0 + kLzThreads > fenced + off) {
+            __threadfence_block();
+            fenced = op + b0;
+          }
+          const uint32_t i = b0 + lane;
+          if (i < ml) {
+            const uint8_t v = dst[op + i - off];
+            dst[op + i] = v;
+            ring[ridx(op + i)] = v;
+          }
+          lz_wave_sync();
+        }
+      }
+      op += ml;
+      ip = p;
+      flushed = op;
+      return p < slen;
+    };
+
+    bool more = slen > 0;
+    while (more) {
+      const uint32_t r0 = (uint32_t)((int32_t)ip - sbase);
+      if (vend == 0 || (!at_end && r0 + 2 * kLzThreads > vend)) {
+        refill(ip);
+        continue;
+      }
+      // 1. candidate headers: a token at stage index r = r0 + lane
+      const uint32_t r = r0 + lane;
+      uint32_t A = kInc, tot = 0, lit = 0, q = 0, off = 0;
+      if (r < vend) {
+        const uint32_t a8 = r & ~7u;
+        const uint64_t lo = *reinterpret_cast<const uint64_t*>(stage + a8);
+        const uint64_t hi = *reinterpret_cast<const uint64_t*>(stage + a8 + 8);
+        const uint32_t sh = (r & 7u) * 8u;
+        const uint64_t wv = sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+        auto sb = [&](uint32_t idx) -> uint32_t {
+          const uint32_t d = idx - r;
+          return d < 8 ? (uint32_t)(wv >> (8u * d)) & 255u : (uint32_t)stage[idx];
+        };
+        const uint32_t t = (uint32_t)wv & 255u;
+        uint32_t k = r + 1, err = 0;
+        bool inc = false;
+        lit = t >> 4;
+        if (lit == 15) {
+          uint32_t b = 255;
+          while (b == 255) {
+            if (k >= vend) {
+              inc = !at_end;
+              err = 1;
+              break;
+            }
+            b = sb(k++);
+            lit += b;
+          }
+        }
+        q = k;
+        const uint32_t le = k + lit;
+        if (!err) {
+          if (le > vend) {
+            inc = !at_end;
+            err = 2;
+          } else if (at_end && le == vend) {
+            tot = lit;
+            A = kFinal;
+          } else if (le + 2 > vend) {
+            inc = !at_end;
+            err = 3;
+          } else {
+            off = sb(le) | (sb(le + 1) << 8);
+            uint32_t e = le + 2, ml = t & 15u;
+            if (ml == 15) {
+              uint32_t b = 255;
+              while (b == 255) {
+                if (e >= vend) {
+                  inc = !at_end;
+                  err = 4;
+                  break;
+                }
+                b = sb(e++);
+                ml += b;
+              }
+            }
+            tot = lit + ml + 4;
+            A = e - r0;
+          }
+        }
+        if (inc) A = kInc;
+        else if (err) A = err << kErrShift;
+      }
+      // 2. walk the token chain from lane 0
+      uint32_t cur = 0, T = 0, cnt = 0, opo = 0;
+      uint64_t mask = 0;
+      int stop = 0;   // 0: next token at cur, 1: lane cur needs input, 2: error, 3: stream done, 4: too long
+      while (cur < kLzThreads) {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)A, (int)cur);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)tot, (int)cur);
+        if (a & kInc) { stop = 1; break; }
+        if (a >> kErrShift) { status = -(int32_t)(a >> kErrShift); stop = 2; break; }
+        if (T + b > TMAX) { stop = cnt ? 0 : 4; break; }
+        opo = lane == cur ? T : opo;
+        mask |= 1ull << cur;
+        T += b;
+        ++cnt;
+        if (a & kFinal) { stop = 3; break; }
+        cur = a & kNxt;
+        if (ip + cur >= slen) { stop = 3; break; }
+      }
+      if (stop == 2) break;
+      if (cnt == 0) {
+        if (stop == 1 && !(r0 < 16 && vend == S)) {
+          refill(ip);   // the header runs past the stage: restart the stage at it
+          continue;
+        }
+        more = slow_sequence();   // header longer than a stage, or output longer than TMAX
+        if (status) break;
+        continue;
+      }
+      // 3. per-token checks, then one code per output byte
+      const bool tok = (mask >> lane) & 1ull;
+      const bool fin = tok && (A & kFinal);
+      const bool bad_lit = tok && op + opo + lit > cap;
+      const bool bad_m = tok && !fin && (off == 0 || off > op + opo + lit || op + opo + tot > cap);
+      const uint64_t badm = __ballot(bad_lit || bad_m);
+      if (badm) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(badm);
+        status = __builtin_amdgcn_readlane(bad_lit ? -2 : -5, (int)f);
+        break;
+      }
+      if (tok) {
+        for (uint32_t k = 0; k < lit; ++k) code[opo + k] = q + k;
+        for (uint32_t x = opo + lit; x < opo + tot; ++x) {
+          const int32_t y = (int32_t)x - (int32_t)off;
+          code[x] = y >= 0 ? (kRef | (uint32_t)y) : (kOld | (uint32_t)((int32_t)op + y));
+        }
+      }
+      lz_wave_sync();
+      // 4. resolve references block by block, gather the bytes
+      uint32_t outb[NB];
+#pragma unroll
+      for (uint32_t bi = 0; bi < NB; ++bi) {
+        outb[bi] = 0;
+        if (bi * kLzThreads < T) {
+          const uint32_t x = bi * kLzThreads + lane;
+          const bool in = x < T;
+          uint32_t c = in ? code[x] : 0u;
+          while (__ballot(in && (c & kRef))) {
+            if (in && (c & kRef)) c = code[c & kVal];
+            lz_wave_sync();
+            if (in) code[x] = c;
+            lz_wave_sync();
+          }
+          const uint32_t cv = c & kVal;
+          const bool far = in && (c & kOld) && op - cv > R;
+          if (__ballot(far && cv + 128 > fenced)) {
+            __threadfence_block();
+            fenced = flushed;
+          }
+          if (in) outb[bi] = (c & kOld) ? (far ? (uint32_t)dst[cv] : (uint32_t)ring[ridx(cv)]) : (uint32_t)stage[cv];
+        }
+      }
+      lz_wave_sync();
+#pragma unroll
+      for (uint32_t bi = 0; bi < NB; ++bi) {
+        const uint32_t x = bi * kLzThreads + lane;
+        if (x < T) ring[ridx(op + x)] = (uint8_t)outb[bi];
+      }
+      lz_wave_sync();
+      op += T;
+      ip += cur;
+      if (stop == 3) more = false;
+      if (op - flushed >= kFlush) {
+        const uint32_t hi = (uint32_t)(((daddr + op) & ~15ull) - daddr);
+        flush(flushed, hi);
+        flushed = hi;
+      }
+    }
+    if (!status) flush(flushed, op);
+    if (lane == 0) out_sizes[w] = status ? status : (int32_t)op;
+    lz_wave_sync();
+  }
+}
+
 // -1 (default): auto — the staged wave-per-chunk kernel (2) for small batches, lane groups of 4
 // (17) from 6144 chunks up, where enough chunks exist to fill the CUs 16 per wave
 // (profiles/r2_lz4.md: text 45 -> 63 GB/s at 8192 chunks, 54 -> 217 GB/s at 32768).
@@ -1735,11 +2063,15 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
         hipLaunchKernelGGL((lz4_decompress_groups_kernel<4, 512, 256>), dim3(g), dim3(kLzThreads), 0, stream, chunks, n, out_sizes);
         break;
       }
-      default: {
+      case 18: {
         const unsigned g = (unsigned)std::min((n + 15) / 16, 65536);
         hipLaunchKernelGGL((lz4_decompress_groups_kernel<4, 2048, 256>), dim3(g), dim3(kLzThreads), 0, stream, chunks, n, out_sizes);
         break;
       }
+      case 19: hipLaunchKernelGGL((lz4_decompress_window_kernel<8192, 1024, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 20: hipLaunchKernelGGL((lz4_decompress_window_kernel<4096, 1024, 256>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 21: hipLaunchKernelGGL((lz4_decompress_window_kernel<8192, 2048, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      default: hipLaunchKernelGGL((lz4_decompress_window_kernel<16384, 1024, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
     }
   }
   return hipGetLastError();

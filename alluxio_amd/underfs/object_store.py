@@ -44,7 +44,11 @@ class _ObjectWriter(io.RawIOBase):
 
 
 class _RangeReader(io.RawIOBase):
-    """Sequential reader that fetches ``chunk`` bytes per ranged GET (multi-range stream)."""
+    """Sequential reader that fetches ``chunk`` bytes per ranged GET (multi-range stream).  Stores
+    with a native ``_get_into`` receive reads of at least ``_direct_min`` bytes directly into the
+    caller's buffer."""
+
+    _direct_min = 256 << 10
 
     def __init__(self, ufs, key, size, offset, chunk):
         super().__init__()
@@ -70,6 +74,15 @@ class _RangeReader(io.RawIOBase):
     def readinto(self, b):
         if self._pos >= self._size:
             return 0
+        get_into = getattr(self._ufs, "_get_into", None)
+        if get_into is not None and len(b) >= self._direct_min:
+            # straight into the caller's buffer (the ingest pipeline's pinned staging)
+            n = min(len(b), self._size - self._pos)
+            import numpy as np
+            arr = np.frombuffer(b, dtype=np.uint8, count=n)
+            if get_into(self._key, self._pos, n, arr.ctypes.data):
+                self._pos += n
+                return n
         rel = self._pos - self._cur_off
         if rel < 0 or rel >= len(self._cur):
             n = min(self._chunk, self._size - self._pos)

@@ -75,6 +75,14 @@ class S3Client:
         return r
 
 
+def _parse_size(v) -> int:
+    v = str(v).strip().upper().rstrip("B")
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}
+    if v and v[-1] in mult:
+        return int(float(v[:-1]) * mult[v[-1]])
+    return int(v or 0)
+
+
 def _xml_text(el, tag):
     for c in el:
         if c.tag.split("}")[-1] == tag:
@@ -110,6 +118,13 @@ class S3UnderFileSystem(ObjectUnderFileSystem):
                                opt("s3a.secretKey", "aws.secretKey"),
                                opt("alluxio.underfs.s3.region", default="us-east-1"))
         self.folder_suffix = opt("alluxio.underfs.s3.directory.suffix", default="/") or "/"
+        # native data path (csrc/http_blob.cpp): ranged GETs received straight into the caller's
+        # buffer over pooled keep-alive connections, a read split into parallel sub-ranges
+        self._native = None
+        self._native_on = str(opt("alluxio.underfs.s3.native.reader.enabled", default="true")).lower() == "true" \
+            and endpoint.startswith("http://")
+        self._parallel = max(1, min(16, int(opt("alluxio.underfs.s3.threads.max", default="8") or 8)))
+        self._part = _parse_size(opt("alluxio.underfs.s3.read.part.size", default="4MB"))
 
     def _put(self, key, data):
         if len(data) <= self.multipart_threshold:
@@ -132,6 +147,33 @@ class S3UnderFileSystem(ObjectUnderFileSystem):
             return b""
         r = self.client.request("GET", self.bucket, key, headers={"Range": f"bytes={offset}-{offset + length - 1}"})
         return r.content
+
+    def _native_reader(self):
+        if self._native is None and self._native_on:
+            try:
+                from ..ops.native import lib
+                u = urllib.parse.urlsplit(self.client.endpoint)
+                self._native = lib().HttpRangeReader(u.hostname, u.port or 80, 2 * self._parallel)
+            except Exception:  # noqa: BLE001 -- no native library: the requests path serves
+                self._native_on = False
+        return self._native
+
+    def _get_into(self, key, offset, length, addr) -> bool:
+        """Ranged GET of ``length`` bytes at ``offset`` into host memory at ``addr`` (native path);
+        False when the native reader is unavailable."""
+        rd = self._native_reader()
+        if rd is None:
+            return False
+        path = f"/{self.bucket}/{key}"
+        h = self.client._headers("GET", path, {}, _EMPTY_SHA)
+        head = "".join(f"{k}: {v}\r\n" for k, v in h.items())
+        got = rd.get_into(urllib.parse.quote(path, safe="/-_.~"), head, offset, length, addr,
+                          self._parallel, self._part)
+        if got == -404:
+            raise FileNotFoundError(f"s3://{self.bucket}/{key}")
+        if got != length:
+            raise OSError(f"S3 GET {path} [{offset}, +{length}) failed: {got}")
+        return True
 
     def _head(self, key):
         try:

@@ -58,7 +58,7 @@ def test_crc32c_matches_host(gpu, variant):
     C.set_crc_variant(4)
 
 
-@pytest.mark.parametrize("variant", [-1] + list(range(19)))
+@pytest.mark.parametrize("variant", [-1] + list(range(23)))
 def test_lz4_device_roundtrip(gpu, variant):
     import torch
     C = lib()
@@ -103,6 +103,39 @@ def test_lz4_device_roundtrip(gpu, variant):
     for raw, e, sz in zip(chunks, enc, sizes):
         assert sz > 0
         assert C.lz4_decompress(e[:sz].cpu().numpy().tobytes(), len(raw)) == raw
+    C.set_lz4_decode_variant(-1)
+
+
+@pytest.mark.parametrize("variant", [-1, 2, 17, 19, 20, 21, 22])
+def test_lz4_device_unaligned_and_text(gpu, variant):
+    """Unaligned source/destination addresses, text/CSV-shaped streams (many short sequences with
+    small offsets: the window kernels' reference chains), long zero runs and incompressible tails."""
+    import torch
+    C = lib()
+    C.set_lz4_decode_variant(variant)
+    rng = np.random.default_rng(7)
+    words = [b"alluxio", b"worker", b"block", b"hbm", b"page", b"read", b"\n", b",", b" "]
+    text = b"".join(words[i] for i in rng.integers(0, len(words), 30000))
+    csv = b"".join(b"%d,%s,%d\n" % (i, [b"GET", b"PUT"][i % 2], int(rng.integers(0, 999))) for i in range(6000))
+    chunks = [text[:65536], csv[:65536], bytes(40000) + os.urandom(25536), text[:1000] + bytes(60000),
+              os.urandom(3000) + text[:50000], b"ab" * 20000, text[:7], b""]
+    comp = [C.lz4_compress(c) for c in chunks]
+    base = torch.zeros(sum(len(c) + 64 for c in comp), dtype=torch.uint8, device=gpu)
+    outs = torch.zeros(len(chunks) * 70000, dtype=torch.uint8, device=gpu)
+    items, pos = [], 0
+    for i, c in enumerate(comp):
+        so = pos + 1 + i % 15
+        if c:
+            base[so:so + len(c)] = torch.tensor(list(c), dtype=torch.uint8, device=gpu)
+        items.append((base.data_ptr() + so, outs.data_ptr() + i * 70000 + (3 * i) % 16, len(c), 65536))
+        pos = so + len(c) + 16
+    sizes = C.lz4_device(items, False, 0)
+    host = outs.cpu().numpy().tobytes()
+    for i, (raw, sz) in enumerate(zip(chunks, sizes)):
+        o = i * 70000 + (3 * i) % 16
+        assert sz == len(raw), (i, sz, len(raw))
+        assert host[o:o + sz] == raw, i
+        assert host[o + sz:o + sz + 8] == bytes(8), i   # nothing written past the output
     C.set_lz4_decode_variant(-1)
 
 

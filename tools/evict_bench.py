@@ -106,6 +106,9 @@ def run(n: int, iters: int, page: int, policy: int) -> dict:
                 for b in fids:
                     s.remove_block(2, b)
             out[f"ingest_{nf}_{name}_ms"] = round(best * 1e3, 2)
+            # per-phase wall time, mean of the 3 calls: setup, preads, launches, stream wait,
+            # attach+commit, magazine refill
+            out[f"ingest_{name}_phase_ms"] = [round(x / 3e6, 2) for x in s.evict_stats()["ingest_ns"]]
             del s
     del arena
     torch.cuda.synchronize()

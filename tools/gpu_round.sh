@@ -3,7 +3,7 @@
 # the script stops at the first crash-like exit (fault/abort/segv/timeout); plain test failures
 # (exit 1) do not stop later measurement steps.
 # usage: tools/gpu_round.sh [steps...]   steps: tests smoke bench bench20 variants prof ring pmc pmcdram
-#                                         crc dl master kbench
+#                                         crc dl master kbench lz4t lz4
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out
@@ -40,6 +40,12 @@ for s in $STEPS; do
       ;;
     prof)
       run rocprof_bench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
+      ;;
+    lz4t) run lz4_tests 300 python -u -m pytest tests/test_kernels_gpu.py -k lz4 -x -v --timeout 120 --timeout-method thread ;;
+    lz4) run lz4_bench 600 python tools/lz4_bench.py --chunks 1024,4096,16384,32768 --variants "${LZ4_VARIANTS:-2,17,19,20,21,22}" --out "$OUT/lz4_bench.jsonl" ;;
+    s3ingest)
+      run ingest_s3native 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 2g --dram 6g --factor 2 --depths 1,3 --out "$OUT/ufs_ingest_s3native.jsonl"
+      run ingest_s3requests 600 python tools/ufs_ingest_bench.py --ufs s3native --native-reader false --hbm 2g --dram 6g --factor 2 --depths 3 --out "$OUT/ufs_ingest_s3native.jsonl"
       ;;
     crc) run crc_bench 300 python tools/crc_bench.py --gb 4 --out "$OUT/crc_bench.jsonl" ;;
     dl) run dl_bench_100k 400 python tools/dl_bench.py --files 100000 --out "$OUT/dl_bench_100k.jsonl" ;;
@@ -98,6 +104,7 @@ for s in $STEPS; do
       run ring_tune_large 500 python tools/ring_tune.py --file-size 16g --stagger --depths 256 --variants 0,1,2,3 --caps 4096,8192,16384 --rounds 3 --steps 32 --out "$OUT/ring_tune_large.json"
       ;;
     kprof) run rocprof_kbench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_k" -o kb --output-format csv -- python3 tools/kernel_bench.py --out "$OUT/kb_prof.json" ;;
+    evictb) run evict_bench 300 python tools/evict_bench.py --counts 10000,150000 --out "$OUT/evict_bench.jsonl" ;;
     evict)
       run pytest_evict 300 python -u -m pytest tests/test_evict_alloc_gpu.py tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread
       run evict_bench 300 python tools/evict_bench.py --counts 10000,150000 --out "$OUT/evict_bench.jsonl"

@@ -14,7 +14,9 @@ pipeline: UFS read of chunk i+1 overlapped with the H2D of chunk i on a side str
 * re-read GB/s of the whole working set into a device buffer (hot in HBM or DRAM).
 
 ``--ufs s3`` serves the files from an S3 endpoint (this repository's S3 REST proxy in front of a
-second, DRAM-only cluster whose own UFS holds the bytes), ``--ufs local`` from a local directory.
+second, DRAM-only cluster whose own UFS holds the bytes), ``--ufs s3native`` from the native S3
+endpoint (csrc/http_blob.cpp, sendfile) so that the worker's S3 read path rather than the endpoint
+is the bound, ``--ufs local`` from a local directory.
 
     python tools/ufs_ingest_bench.py --ufs local --hbm 2g --dram 6g --factor 2 --out gpurun_out/ufs_ingest.jsonl
 """
@@ -77,7 +79,26 @@ def run(a, depth: int) -> dict:
             "alluxio.worker.network.async.cache.manager.threads.max": str(a.threads),
             "alluxio.worker.tieredstore.eviction.demote": "true",
         }
-        if a.ufs == "s3":
+        if a.ufs == "s3native":
+            # the native S3 endpoint (csrc/http_blob.cpp: sendfile GETs) over a directory whose
+            # bucket holds the files; the worker's S3 UFS reads ranges natively unless disabled
+            from alluxio_amd.ops.native import lib
+            blob_root = os.path.join(work, "blobs")
+            os.makedirs(os.path.join(blob_root, "bench", "ws"))
+            proxy = lib().BlobServer(blob_root, "127.0.0.1", 0)
+            proxy.start()
+            props = {"alluxio.underfs.s3.endpoint": f"http://127.0.0.1:{proxy.port}", "s3a.accessKeyId": "k",
+                     "s3a.secretKey": "s", "alluxio.underfs.s3.native.reader.enabled": a.native_reader}
+            for k, v in props.items():
+                conf[f"alluxio.master.mount.table.root.option.{k}"] = v
+            conf["alluxio.master.mount.table.root.ufs"] = "s3://bench/"
+
+            def wr(p, d):
+                with open(os.path.join(blob_root, "bench") + p, "wb") as f:
+                    f.write(d)
+            _write_working_set(wr, nfiles, file_size)
+            cluster = LocalAlluxioCluster(num_workers=1, work_dir=os.path.join(work, "main"), conf=conf)
+        elif a.ufs == "s3":
             from alluxio_amd.proxy import ProxyServer
             backing = LocalAlluxioCluster(num_workers=1, work_dir=os.path.join(work, "backing"), conf={
                 "alluxio.worker.tieredstore.level0.dirs.path": "dram",
@@ -149,7 +170,7 @@ def run(a, depth: int) -> dict:
                 torch.cuda.synchronize()
             rel = time.perf_counter() - t1
             fs.close()
-            return {"ufs": a.ufs, "depth": depth, "hbm_bytes": hbm, "dram_bytes": dram, "working_set": nbytes,
+            return {"ufs": a.ufs if a.ufs != "s3native" else f"s3native(reader={a.native_reader})", "depth": depth, "hbm_bytes": hbm, "dram_bytes": dram, "working_set": nbytes,
                     "blocks": len(reqs), "cached_blocks": cached, "all_done": ok,
                     "ingest_GBps": round(nbytes / el / 1e9, 3), "ingest_s": round(el, 3),
                     "demoted_blocks": st["demoted_blocks"], "demoted_bytes": st["demoted_bytes"],
@@ -166,7 +187,9 @@ def run(a, depth: int) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ufs", choices=("local", "s3"), default="local")
+    ap.add_argument("--ufs", choices=("local", "s3", "s3native"), default="local")
+    ap.add_argument("--native-reader", choices=("true", "false"), default="true",
+                    help="s3native: receive ranged GETs natively (else the requests client)")
     ap.add_argument("--hbm", default="2g")
     ap.add_argument("--dram", default="6g")
     ap.add_argument("--factor", type=float, default=2.0)
