@@ -600,6 +600,9 @@ PYBIND11_MODULE(_C, m) {
            })
       .def("set_user", &FrameRpcServer::set_user)
       .def("set_cacheable", &FrameRpcServer::set_cacheable)
+      .def("set_method_kind", &FrameRpcServer::set_method_kind)
+      .def_property_readonly("grpc_requests", &FrameRpcServer::grpc_requests)
+      .def_static("grpc_available", &FrameRpcServer::grpc_available)
       .def("epoch", &FrameRpcServer::epoch)
       .def("bump_epoch", &FrameRpcServer::bump_epoch)
       .def("cache_put", [](FrameRpcServer& s, uint32_t method, const std::string& user, py::bytes request,

@@ -350,6 +350,7 @@ void BlockStore::mag_refill(StorageDir& d, int64_t want) {
       if (!word) continue;
     }
     d.free_bits[w] &= ~word;
+    if (d.mag_lo < 0) d.mag_lo = w;
     upd.push_back((uint64_t)w);
     upd.push_back(word);
     moved += __builtin_popcountll(word);
@@ -374,6 +375,16 @@ void BlockStore::mag_refill(StorageDir& d, int64_t want) {
   stats_.mag_refill_pages += moved;
 }
 
+// Words holding the magazine's bits: the arc [mag_lo, mag_cursor) refills filled since the last
+// drain (the whole bitmap once the cursor wrapped onto it); (0, 0) = the whole bitmap.
+std::pair<uint32_t, uint32_t> BlockStore::mag_window(const StorageDir& d) const {
+  const int64_t nwords = (int64_t)d.free_bits.size();
+  if (d.mag_lo < 0 || nwords == 0) return {0u, 0u};
+  const int64_t len = ((d.mag_cursor - d.mag_lo) % nwords + nwords) % nwords;
+  if (len == 0) return {0u, 0u};
+  return {(uint32_t)d.mag_lo, (uint32_t)len};
+}
+
 // Hands every page left in the magazine back to the host pool (atomic exchange per word, so a
 // claim running concurrently on another stream still owns exactly the bits it won).
 int64_t BlockStore::mag_drain(StorageDir& d) {
@@ -393,6 +404,7 @@ int64_t BlockStore::mag_drain(StorageDir& d) {
     back += __builtin_popcountll(out[w]);
   }
   d.mag_pages -= back;
+  d.mag_lo = -1;
   ++stats_.mag_drains;
   stats_.mag_drain_pages += back;
   return back;
@@ -1610,6 +1622,7 @@ std::vector<int64_t> BlockStore::device_alloc_pages(std::unique_lock<std::mutex>
   // kernel takes the pages with atomics and only the page list comes back
   if (d.mag_pages < (int64_t)want) mag_refill(d, (int64_t)want - d.mag_pages + std::min<int64_t>(1024, want));
   const uint32_t nwords = (uint32_t)d.free_bits.size();
+  const std::pair<uint32_t, uint32_t> mwin = mag_window(d);
   std::vector<int64_t> pages;
   {
     std::unique_lock<std::mutex> g(ev_mu_);
@@ -1625,7 +1638,8 @@ std::vector<int64_t> BlockStore::device_alloc_pages(std::unique_lock<std::mutex>
                                   hipMemcpyHostToDevice, internal_stream_);
     if (e == hipSuccess)
       e = launch_mag_claim_scatter(d.mag_bits, nwords, claim_one_.items_d, npieces, claim_one_.pages_d,
-                                   (uint32_t)claim_one_.pages_cap, claim_one_.got_d, 0, nullptr, 0, internal_stream_);
+                                   (uint32_t)claim_one_.pages_cap, claim_one_.got_d, 0, nullptr, 0, internal_stream_,
+                                   mwin.first, mwin.second);
     if (e == hipSuccess)
       e = hipMemcpyAsync(claim_one_.got_h, claim_one_.got_d, npieces * sizeof(uint32_t), hipMemcpyDeviceToHost,
                          internal_stream_);
@@ -1844,9 +1858,10 @@ std::vector<std::vector<int64_t>> BlockStore::mag_claim_many(int dir, const std:
   }
   HIP_OK(hipMemcpyAsync(claim_one_.items_d, claim_one_.items_h, wants.size() * sizeof(ClaimItem), hipMemcpyHostToDevice,
                         internal_stream_));
+  const std::pair<uint32_t, uint32_t> mwin = mag_window(d);
   HIP_OK(launch_mag_claim_scatter(d.mag_bits, (uint32_t)d.free_bits.size(), claim_one_.items_d, (uint32_t)wants.size(),
                                   claim_one_.pages_d, (uint32_t)claim_one_.pages_cap, claim_one_.got_d, 0, nullptr, 0,
-                                  internal_stream_));
+                                  internal_stream_, mwin.first, mwin.second));
   HIP_OK(hipMemcpyAsync(claim_one_.got_h, claim_one_.got_d, wants.size() * 4, hipMemcpyDeviceToHost, internal_stream_));
   HIP_OK(hipMemcpyAsync(claim_one_.pages_h, claim_one_.pages_d, std::max<size_t>(total, 1) * 8, hipMemcpyDeviceToHost,
                         internal_stream_));
@@ -2333,11 +2348,13 @@ bool BlockStore::ingest_device_group(int64_t session, const std::vector<int64_t>
   ClaimScratch& c = claim_[h];
   uint64_t ps = 0;
   int d = -1;
+  std::pair<uint32_t, uint32_t> mwin{0u, 0u};
   {
     std::lock_guard<std::mutex> g(mu_);
     BlockMeta* b = find(ids[items[0]]);
     d = b->dir;
     ps = dirs_[d]->spec.page_size;
+    mwin = mag_window(*dirs_[d]);
   }
   size_t npages = 0, nchunks = 0;
   for (size_t i : items) {
@@ -2364,7 +2381,7 @@ bool BlockStore::ingest_device_group(int64_t session, const std::vector<int64_t>
   HIP_OK(hipMemcpyAsync(c.items_d, c.items_h, items.size() * sizeof(ClaimItem), hipMemcpyHostToDevice, st));
   HIP_OK(launch_mag_claim_scatter(dirs_[d]->mag_bits, nwords, c.items_d, (uint32_t)items.size(), c.pages_d,
                                   (uint32_t)c.pages_cap, c.got_d, (uint32_t)nchunks,
-                                  reinterpret_cast<uint8_t*>(dirs_[d]->spec.base), ps, st));
+                                  reinterpret_cast<uint8_t*>(dirs_[d]->spec.base), ps, st, mwin.first, mwin.second));
   HIP_OK(hipMemcpyAsync(c.pages_h, c.pages_d, npages * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   HIP_OK(hipMemcpyAsync(c.got_h, c.got_d, items.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   for (int64_t id : c.ids) pending.push_back(id);

@@ -80,6 +80,7 @@ struct StorageDir {
   uint64_t* mag_bits = nullptr;
   int64_t mag_pages = 0;            // pages in the magazine (refills - claims - drains)
   int64_t mag_cursor = 0;           // next host word a refill looks at
+  int64_t mag_lo = -1;              // first word of the arc refills filled since the last drain
   uint64_t* mag_upd = nullptr;      // device staging of refill updates (word, bits) pairs
   size_t mag_upd_cap = 0;
   int64_t reserved_pages = 0;       // kept free for tier management (align/promote swaps)
@@ -307,6 +308,7 @@ class BlockStore {
   std::vector<int64_t> device_alloc_pages(std::unique_lock<std::mutex>& lk, int dir, uint32_t want);
   void mag_refill(StorageDir& d, int64_t want);                    // mu_ held
   int64_t mag_drain(StorageDir& d);                                 // mu_ held
+  std::pair<uint32_t, uint32_t> mag_window(const StorageDir& d) const;  // mu_ held
   bool ingest_device_group(int64_t session, const std::vector<int64_t>& ids, const std::vector<uint64_t>& lengths,
                            const std::vector<size_t>& items, const std::vector<uint64_t>& at, size_t lo,
                            uint8_t* dbase, int h, hipStream_t st, std::vector<int64_t>& pending);

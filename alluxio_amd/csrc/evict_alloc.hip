@@ -363,7 +363,7 @@ __device__ __forceinline__ uint64_t low_bits(uint64_t x, uint32_t k) {
 __global__ __launch_bounds__(64) void mag_claim_kernel(uint64_t* __restrict__ bits, uint32_t nwords,
                                                        const ClaimItem* __restrict__ items, uint32_t nitems,
                                                        int64_t* __restrict__ pages_out, uint32_t pages_cap,
-                                                       uint32_t* __restrict__ got) {
+                                                       uint32_t* __restrict__ got, uint32_t win_lo, uint32_t win_len) {
   // one wave per workgroup and item: the window's free counts, the planned takes and the won
   // counts go through LDS, thread 0 plans and ranks serially (64 entries), barriers order the
   // phases -- no cross-lane shuffles in the plan
@@ -373,19 +373,34 @@ __global__ __launch_bounds__(64) void mag_claim_kernel(uint64_t* __restrict__ bi
   const uint32_t lane = threadIdx.x;
   for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
     const ClaimItem item = items[it];
-    const uint32_t start = (uint32_t)(((uint64_t)it * 0x9E3779B1u) % nwords);
+    const uint32_t hash = (uint32_t)((uint64_t)it * 0x9E3779B1u);
     const uint32_t rot = (uint32_t)((it * 37u) & 63u);      // items start at different bits of a word
-    const uint32_t span = nwords < 64 ? nwords : 64;        // distinct words per window
-    const uint32_t max_rounds = 64 * ((nwords + span - 1) / span) + 64;
+    // the magazine's arc first (refills fill words contiguously from a cursor), then, if that
+    // runs dry, the whole bitmap (bits a short claim or a racing group left elsewhere)
+    bool full = win_len == 0 || win_len >= nwords;
+    uint32_t lo = full ? 0u : win_lo % nwords, len = full ? nwords : win_len;
+    uint32_t start = hash % len;
+    const uint32_t max_rounds = 2 * (64 * ((nwords + 63) / 64) + 64);
     if (lane == 0) s_have = 0;
     __syncthreads();
     uint32_t dry = 0;
-    // windows walk the bitmap round and round: a wave that lost a race retries with a fresh
+    // windows walk the range round and round: a wave that lost a race retries with a fresh
     // snapshot until it has its pages or one whole pass found no free bit (magazine dry)
-    for (uint32_t win = 0, rounds = 0; rounds < max_rounds; win += span, ++rounds) {
+    for (uint32_t win = 0, rounds = 0; rounds < max_rounds; ++rounds) {
       const uint32_t have = s_have;
-      if (have >= item.want || dry >= nwords) break;
-      const uint32_t w = (uint32_t)(((uint64_t)start + win + lane) % nwords);
+      if (have >= item.want) break;
+      if (dry >= len) {
+        if (full) break;
+        full = true;
+        lo = 0;
+        len = nwords;
+        start = hash % len;
+        win = 0;
+        dry = 0;
+      }
+      const uint32_t span = len < 64 ? len : 64;            // distinct words per window
+      const uint32_t w = (uint32_t)(((uint64_t)lo + ((uint64_t)start + win + lane) % len) % nwords);
+      win += span;
       const bool valid = lane < span;
       const uint64_t word = valid ? __hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
       s_cnt[lane] = (uint32_t)__popcll(word);
@@ -502,11 +517,12 @@ hipError_t launch_mag_drain(uint64_t* bits, uint32_t nwords, uint64_t* out, hipS
 
 hipError_t launch_mag_claim_scatter(uint64_t* bits, uint32_t nwords, const ClaimItem* items, uint32_t nitems,
                                     int64_t* pages_out, uint32_t pages_cap, uint32_t* got, uint32_t total_chunks,
-                                    uint8_t* arena, uint64_t page_size, hipStream_t stream) {
+                                    uint8_t* arena, uint64_t page_size, hipStream_t stream, uint32_t win_lo,
+                                    uint32_t win_len) {
   if (nitems == 0 || nwords == 0) return hipSuccess;
   const unsigned cgrid = (unsigned)std::min<uint32_t>(nitems, 16384);
   hipLaunchKernelGGL(mag_claim_kernel, dim3(cgrid), dim3(64), 0, stream, bits, nwords, items, nitems, pages_out,
-                     pages_cap, got);
+                     pages_cap, got, win_lo, win_len);
   if (total_chunks) {
     const unsigned sgrid = (unsigned)std::min<uint32_t>((total_chunks + 3) / 4, 16384);
     hipLaunchKernelGGL(mag_scatter_kernel, dim3(sgrid), dim3(256), 0, stream, items, nitems, total_chunks, pages_out,

@@ -12,9 +12,12 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <dlfcn.h>
+
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
+#include <unordered_map>
 
 namespace amdx {
 
@@ -101,7 +104,130 @@ void set_timeouts(int fd, int timeout_ms) {
   ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
 }
 
+// ---- libnghttp2 (HTTP/2 framing for the gRPC connections) -----------------------------------
+// The image ships the runtime library without headers: the entry points used below are declared
+// from its stable C ABI and resolved with dlopen (no library -> gRPC connections are refused).
+struct NgNv {
+  uint8_t* name;
+  uint8_t* value;
+  size_t namelen;
+  size_t valuelen;
+  uint8_t flags;
+};
+struct NgFrameHd {   // the first member of every nghttp2_frame variant
+  size_t length;
+  int32_t stream_id;
+  uint8_t type;
+  uint8_t flags;
+  uint8_t reserved;
+};
+union NgDataSource {
+  int fd;
+  void* ptr;
+};
+typedef ssize_t (*NgReadCb)(void* session, int32_t stream_id, uint8_t* buf, size_t length, uint32_t* data_flags,
+                            NgDataSource* source, void* user_data);
+struct NgDataProvider {
+  NgDataSource source;
+  NgReadCb read_callback;
+};
+struct NgSettingsEntry {
+  int32_t settings_id;
+  uint32_t value;
+};
+typedef int (*NgFrameCb)(void* session, const void* frame, void* user_data);
+typedef int (*NgDataChunkCb)(void* session, uint8_t flags, int32_t stream_id, const uint8_t* data, size_t len,
+                             void* user_data);
+typedef int (*NgCloseCb)(void* session, int32_t stream_id, uint32_t error_code, void* user_data);
+typedef int (*NgHeaderCb)(void* session, const void* frame, const uint8_t* name, size_t namelen,
+                          const uint8_t* value, size_t valuelen, uint8_t flags, void* user_data);
+constexpr uint8_t kNgFlagEndStream = 0x01;
+constexpr uint32_t kNgDataEof = 0x01, kNgDataNoEndStream = 0x02;
+constexpr uint8_t kNgTypeData = 0, kNgTypeHeaders = 1;
+const char kH2Preface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
+
+struct Ng {
+  bool ok = false;
+  int (*callbacks_new)(void**) = nullptr;
+  void (*set_on_frame_recv)(void*, NgFrameCb) = nullptr;
+  void (*set_on_begin_headers)(void*, NgFrameCb) = nullptr;
+  void (*set_on_data_chunk_recv)(void*, NgDataChunkCb) = nullptr;
+  void (*set_on_stream_close)(void*, NgCloseCb) = nullptr;
+  void (*set_on_header)(void*, NgHeaderCb) = nullptr;
+  int (*server_new)(void**, const void*, void*) = nullptr;
+  void (*session_del)(void*) = nullptr;
+  ssize_t (*mem_recv)(void*, const uint8_t*, size_t) = nullptr;
+  ssize_t (*mem_send)(void*, const uint8_t**) = nullptr;
+  int (*submit_settings)(void*, uint8_t, const NgSettingsEntry*, size_t) = nullptr;
+  int (*submit_response)(void*, int32_t, const NgNv*, size_t, const NgDataProvider*) = nullptr;
+  int (*submit_trailer)(void*, int32_t, const NgNv*, size_t) = nullptr;
+  void* cbs = nullptr;   // one callbacks object shared by every session
+};
+
+// name/value must outlive the submit call (nghttp2 copies them there): literals or named strings
+NgNv nv(const char* n, const char* v) {
+  return NgNv{reinterpret_cast<uint8_t*>(const_cast<char*>(n)), reinterpret_cast<uint8_t*>(const_cast<char*>(v)),
+              std::strlen(n), std::strlen(v), 0};
+}
+NgNv nv(const char* n, const std::string& v) {
+  return NgNv{reinterpret_cast<uint8_t*>(const_cast<char*>(n)),
+              reinterpret_cast<uint8_t*>(const_cast<char*>(v.data())), std::strlen(n), v.size(), 0};
+}
+NgNv nv(const char* n, std::string&&) = delete;
+
+// grpc-message: percent-encode everything outside printable ASCII, and '%'
+std::string grpc_message(const std::string& m) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string o;
+  for (unsigned char c : m) {
+    if (c < 0x20 || c > 0x7E || c == '%') {
+      o.push_back('%');
+      o.push_back(hex[c >> 4]);
+      o.push_back(hex[c & 15]);
+    } else {
+      o.push_back((char)c);
+    }
+  }
+  return o;
+}
+
+inline void put_be32(std::string& s, uint32_t v) {
+  const char b[4] = {(char)(v >> 24), (char)(v >> 16), (char)(v >> 8), (char)v};
+  s.append(b, 4);
+}
+
 }  // namespace
+
+// gRPC over HTTP/2 on the framed-RPC port: per-connection nghttp2 server session, driven on the
+// I/O thread (receive) and the responding threads (send), always under the connection's wmu.
+struct FrameRpcServer::H2 {
+  struct Stream {
+    uint32_t method = UINT32_MAX;
+    std::string path, cid, auser, in, out;
+    size_t out_off = 0;
+    bool dispatched = false, responded = false;
+  };
+  struct Session {
+    FrameRpcServer* srv = nullptr;
+    Conn* conn = nullptr;
+    void* ng = nullptr;
+    std::unordered_map<int32_t, Stream> streams;
+    ~Session();
+  };
+  static const Ng& lib();
+  static int on_begin_headers(void*, const void* frame, void* ud);
+  static int on_header(void*, const void* frame, const uint8_t* name, size_t namelen, const uint8_t* value,
+                       size_t valuelen, uint8_t, void* ud);
+  static int on_data(void*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* ud);
+  static int on_frame(void*, const void* frame, void* ud);
+  static int on_close(void*, int32_t sid, uint32_t, void* ud);
+  static ssize_t read_body(void* session, int32_t sid, uint8_t* buf, size_t length, uint32_t* flags, NgDataSource*,
+                           void* ud);
+  static void dispatch(Session& S, int32_t sid, Stream& st, std::string msg);
+  static void respond_locked(Session& S, int32_t sid, int status, const std::string& msg, const std::string& payload);
+  static bool flush_locked(Session& S);
+  static bool start(FrameRpcServer& srv, Conn& c);
+};
 
 struct FrameRpcServer::Conn {
   int fd;
@@ -112,11 +238,253 @@ struct FrameRpcServer::Conn {
   std::mutex umu;
   std::string user;
   std::atomic<bool> closed{false};
+  int proto = 0;                          // 0 undecided, 1 framed, 2 gRPC/HTTP2
+  std::unique_ptr<H2::Session> h2;
   Conn(int f, uint32_t i) : fd(f), id(i) {}
   ~Conn() {
+    h2.reset();
     if (fd >= 0) ::close(fd);
   }
 };
+
+FrameRpcServer::H2::Session::~Session() {
+  if (ng) lib().session_del(ng);
+}
+
+const Ng& FrameRpcServer::H2::lib() {
+  static const Ng n = [] {
+    Ng g;
+    void* h = ::dlopen("libnghttp2.so.14", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return g;
+    auto sym = [&](const char* name) { return ::dlsym(h, name); };
+    g.callbacks_new = reinterpret_cast<int (*)(void**)>(sym("nghttp2_session_callbacks_new"));
+    g.set_on_frame_recv = reinterpret_cast<void (*)(void*, NgFrameCb)>(sym("nghttp2_session_callbacks_set_on_frame_recv_callback"));
+    g.set_on_begin_headers = reinterpret_cast<void (*)(void*, NgFrameCb)>(sym("nghttp2_session_callbacks_set_on_begin_headers_callback"));
+    g.set_on_data_chunk_recv = reinterpret_cast<void (*)(void*, NgDataChunkCb)>(sym("nghttp2_session_callbacks_set_on_data_chunk_recv_callback"));
+    g.set_on_stream_close = reinterpret_cast<void (*)(void*, NgCloseCb)>(sym("nghttp2_session_callbacks_set_on_stream_close_callback"));
+    g.set_on_header = reinterpret_cast<void (*)(void*, NgHeaderCb)>(sym("nghttp2_session_callbacks_set_on_header_callback"));
+    g.server_new = reinterpret_cast<int (*)(void**, const void*, void*)>(sym("nghttp2_session_server_new"));
+    g.session_del = reinterpret_cast<void (*)(void*)>(sym("nghttp2_session_del"));
+    g.mem_recv = reinterpret_cast<ssize_t (*)(void*, const uint8_t*, size_t)>(sym("nghttp2_session_mem_recv"));
+    g.mem_send = reinterpret_cast<ssize_t (*)(void*, const uint8_t**)>(sym("nghttp2_session_mem_send"));
+    g.submit_settings = reinterpret_cast<int (*)(void*, uint8_t, const NgSettingsEntry*, size_t)>(sym("nghttp2_submit_settings"));
+    g.submit_response = reinterpret_cast<int (*)(void*, int32_t, const NgNv*, size_t, const NgDataProvider*)>(sym("nghttp2_submit_response"));
+    g.submit_trailer = reinterpret_cast<int (*)(void*, int32_t, const NgNv*, size_t)>(sym("nghttp2_submit_trailer"));
+    if (!g.callbacks_new || !g.set_on_frame_recv || !g.set_on_begin_headers || !g.set_on_data_chunk_recv ||
+        !g.set_on_stream_close || !g.set_on_header || !g.server_new || !g.session_del || !g.mem_recv || !g.mem_send ||
+        !g.submit_settings || !g.submit_response || !g.submit_trailer)
+      return g;
+    if (g.callbacks_new(&g.cbs) != 0) return g;
+    g.set_on_frame_recv(g.cbs, &H2::on_frame);
+    g.set_on_begin_headers(g.cbs, &H2::on_begin_headers);
+    g.set_on_data_chunk_recv(g.cbs, &H2::on_data);
+    g.set_on_stream_close(g.cbs, &H2::on_close);
+    g.set_on_header(g.cbs, &H2::on_header);
+    g.ok = true;
+    return g;
+  }();
+  return n;
+}
+
+bool FrameRpcServer::grpc_available() { return H2::lib().ok; }
+
+bool FrameRpcServer::H2::start(FrameRpcServer& srv, Conn& c) {
+  const Ng& g = lib();
+  if (!g.ok) return false;
+  auto S = std::make_unique<Session>();
+  S->srv = &srv;
+  S->conn = &c;
+  if (g.server_new(&S->ng, g.cbs, S.get()) != 0) {
+    S->ng = nullptr;
+    return false;
+  }
+  const NgSettingsEntry iv[] = {{3 /*MAX_CONCURRENT_STREAMS*/, 1024}, {4 /*INITIAL_WINDOW_SIZE*/, 1u << 20}};
+  g.submit_settings(S->ng, 0, iv, 2);
+  c.h2 = std::move(S);
+  return true;
+}
+
+int FrameRpcServer::H2::on_begin_headers(void*, const void* frame, void* ud) {
+  const NgFrameHd* hd = static_cast<const NgFrameHd*>(frame);
+  if (hd->type == kNgTypeHeaders) static_cast<Session*>(ud)->streams[hd->stream_id];
+  return 0;
+}
+
+int FrameRpcServer::H2::on_header(void*, const void* frame, const uint8_t* name, size_t namelen, const uint8_t* value,
+                                  size_t valuelen, uint8_t, void* ud) {
+  Session& S = *static_cast<Session*>(ud);
+  const NgFrameHd* hd = static_cast<const NgFrameHd*>(frame);
+  auto it = S.streams.find(hd->stream_id);
+  if (it == S.streams.end() || it->second.dispatched) return 0;   // trailers of a request are ignored
+  Stream& st = it->second;
+  const std::string n(reinterpret_cast<const char*>(name), namelen);
+  const std::string v(reinterpret_cast<const char*>(value), valuelen);
+  if (n == ":path") {
+    st.path = v;
+    auto m = S.srv->method_ids_.find(v);
+    if (m != S.srv->method_ids_.end() && m->second != 0) st.method = m->second;   // 0 is the framed @auth
+  } else if (n == "channel-id") {
+    st.cid = v;
+  } else if (n == "alluxio-user") {
+    st.auser = v;
+  }
+  return 0;
+}
+
+int FrameRpcServer::H2::on_data(void*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* ud) {
+  Session& S = *static_cast<Session*>(ud);
+  auto it = S.streams.find(sid);
+  if (it != S.streams.end() && !it->second.dispatched) it->second.in.append(reinterpret_cast<const char*>(data), len);
+  return 0;
+}
+
+int FrameRpcServer::H2::on_frame(void*, const void* frame, void* ud) {
+  Session& S = *static_cast<Session*>(ud);
+  const NgFrameHd* hd = static_cast<const NgFrameHd*>(frame);
+  if (hd->type != kNgTypeData && hd->type != kNgTypeHeaders) return 0;
+  auto it = S.streams.find(hd->stream_id);
+  if (it == S.streams.end()) return 0;
+  Stream& st = it->second;
+  if (!st.dispatched && st.in.size() >= 5) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(st.in.data());
+    const uint32_t len = ((uint32_t)p[1] << 24) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 8) | p[4];
+    if (p[0] != 0) {
+      st.dispatched = true;
+      respond_locked(S, hd->stream_id, 12 /*UNIMPLEMENTED*/, "compressed gRPC messages are not supported", "");
+    } else if (len > kMaxFrame) {
+      st.dispatched = true;
+      respond_locked(S, hd->stream_id, 8 /*RESOURCE_EXHAUSTED*/, "message too large", "");
+    } else if (st.in.size() >= 5 + (size_t)len) {
+      // one request message per call: unary and server-streaming methods, and the first
+      // message of the SASL handshake stream
+      st.dispatched = true;
+      std::string msg = st.in.substr(5, len);
+      st.in.clear();
+      st.in.shrink_to_fit();
+      dispatch(S, hd->stream_id, st, std::move(msg));
+    }
+  }
+  if ((hd->flags & kNgFlagEndStream) && !st.dispatched) {
+    st.dispatched = true;
+    respond_locked(S, hd->stream_id, 13 /*INTERNAL*/, "request stream ended without a message", "");
+  }
+  return 0;
+}
+
+int FrameRpcServer::H2::on_close(void*, int32_t sid, uint32_t, void* ud) {
+  static_cast<Session*>(ud)->streams.erase(sid);
+  return 0;
+}
+
+void FrameRpcServer::H2::dispatch(Session& S, int32_t sid, Stream& st, std::string msg) {
+  FrameRpcServer& srv = *S.srv;
+  if (st.method == UINT32_MAX) {
+    respond_locked(S, sid, 12 /*UNIMPLEMENTED*/, "unknown method " + st.path, "");
+    return;
+  }
+  // the Python side resolves the caller: channel-id (SASL channels) or alluxio-user (NOSASL)
+  std::string user = "\x01" + st.cid;
+  user.push_back('\0');
+  user += st.auser;
+  srv.requests_.fetch_add(1, std::memory_order_relaxed);
+  srv.grpc_requests_.fetch_add(1, std::memory_order_relaxed);
+  if (srv.cacheable_[st.method]) {
+    CachedReply reply;
+    if (srv.cache_get(cache_key(st.method, user, msg.data(), msg.size()), &reply)) {
+      srv.cache_hits_.fetch_add(1, std::memory_order_relaxed);
+      respond_locked(S, sid, reply.status, reply.msg, reply.body);
+      return;
+    }
+  }
+  FrameRequest rq;
+  rq.token = ((uint64_t)S.conn->id << 32) | (uint32_t)sid;
+  rq.method = st.method;
+  rq.user = std::move(user);
+  rq.payload = std::move(msg);
+  Lane& l = *srv.lane_q_[srv.lanes_[st.method]];
+  {
+    std::lock_guard<std::mutex> g(l.mu);
+    l.q.push_back(std::move(rq));
+  }
+  l.cv.notify_one();
+}
+
+void FrameRpcServer::H2::respond_locked(Session& S, int32_t sid, int status, const std::string& msg,
+                                        const std::string& payload) {
+  auto it = S.streams.find(sid);
+  if (it == S.streams.end() || it->second.responded) return;   // cancelled or answered
+  Stream& st = it->second;
+  st.responded = true;
+  const Ng& g = lib();
+  if (status != 0) {   // trailers-only response
+    const std::string code = std::to_string(status), m = grpc_message(msg);
+    const NgNv nva[] = {nv(":status", "200"), nv("content-type", "application/grpc"), nv("grpc-status", code),
+                        nv("grpc-message", m)};
+    g.submit_response(S.ng, sid, nva, 4, nullptr);
+    return;
+  }
+  const bool streaming = st.method < S.srv->kinds_.size() && S.srv->kinds_[st.method] == 1;
+  std::string body;
+  if (streaming) {
+    body.reserve(payload.size() + payload.size() / 64 + 16);
+    for (size_t p = 0; p + 4 <= payload.size();) {
+      const uint32_t n = get_u32(payload.data() + p);
+      if (p + 4 + n > payload.size()) break;
+      body.push_back('\0');
+      put_be32(body, n);
+      body.append(payload, p + 4, n);
+      p += 4 + n;
+    }
+  } else {
+    body.reserve(payload.size() + 5);
+    body.push_back('\0');
+    put_be32(body, (uint32_t)payload.size());
+    body += payload;
+  }
+  st.out = std::move(body);
+  st.out_off = 0;
+  const NgNv nva[] = {nv(":status", "200"), nv("content-type", "application/grpc")};
+  NgDataProvider dp;
+  dp.source.ptr = &S;
+  dp.read_callback = &H2::read_body;
+  g.submit_response(S.ng, sid, nva, 2, &dp);
+}
+
+ssize_t FrameRpcServer::H2::read_body(void* session, int32_t sid, uint8_t* buf, size_t length, uint32_t* flags,
+                                      NgDataSource*, void* ud) {
+  Session& S = *static_cast<Session*>(ud);
+  auto it = S.streams.find(sid);
+  if (it == S.streams.end()) {
+    *flags |= kNgDataEof;
+    return 0;
+  }
+  Stream& st = it->second;
+  const size_t n = std::min(length, st.out.size() - st.out_off);
+  std::memcpy(buf, st.out.data() + st.out_off, n);
+  st.out_off += n;
+  if (st.out_off == st.out.size()) {
+    *flags |= kNgDataEof | kNgDataNoEndStream;
+    const NgNv t[] = {nv("grpc-status", "0")};
+    lib().submit_trailer(session, sid, t, 1);
+    st.out.clear();
+    st.out.shrink_to_fit();
+    st.out_off = 0;
+  }
+  return (ssize_t)n;
+}
+
+bool FrameRpcServer::H2::flush_locked(Session& S) {
+  const Ng& g = lib();
+  std::string out;
+  for (;;) {
+    const uint8_t* d = nullptr;
+    const ssize_t n = g.mem_send(S.ng, &d);
+    if (n < 0) return false;
+    if (n == 0) break;
+    out.append(reinterpret_cast<const char*>(d), (size_t)n);
+  }
+  return out.empty() || send_all(S.conn->fd, out.data(), out.size(), 30000);
+}
 
 FrameRpcServer::FrameRpcServer(const std::string& host, int port, const std::vector<std::string>& methods,
                                const std::vector<int>& lanes, int io_threads)
@@ -129,6 +497,7 @@ FrameRpcServer::FrameRpcServer(const std::string& host, int port, const std::vec
   }
   for (int i = 0; i < nl; ++i) lane_q_.emplace_back(new Lane());
   cacheable_.assign(methods.size(), 0);
+  kinds_.assign(methods.size(), 0);
 }
 
 // ---- reply cache --------------------------------------------------------------------------
@@ -144,6 +513,10 @@ std::string FrameRpcServer::cache_key(uint32_t method, const std::string& user, 
 
 void FrameRpcServer::set_cacheable(uint32_t method, bool on) {
   if (method < cacheable_.size()) cacheable_[method] = on ? 1 : 0;
+}
+
+void FrameRpcServer::set_method_kind(uint32_t method, int kind) {
+  if (method < kinds_.size()) kinds_[method] = (uint8_t)kind;
 }
 
 bool FrameRpcServer::cache_get(const std::string& key, CachedReply* reply) {
@@ -338,6 +711,38 @@ void FrameRpcServer::on_readable(const std::shared_ptr<Conn>& c, int ep) {
     eof = true;
     break;
   }
+  // protocol of a new connection: gRPC (HTTP/2 client preface) or framed RPC
+  if (c->proto == 0 && c->in.size() >= 3) {
+    if (c->in.compare(0, 3, "PRI") == 0) {
+      if (c->in.size() < sizeof(kH2Preface) - 1) {
+        if (eof) close_conn(c->id);
+        return;
+      }
+      bool ok = c->in.compare(0, sizeof(kH2Preface) - 1, kH2Preface) == 0;
+      if (ok) {
+        std::lock_guard<std::mutex> g(c->wmu);
+        ok = H2::start(*this, *c);
+      }
+      if (!ok) {
+        close_conn(c->id);
+        return;
+      }
+      c->proto = 2;
+    } else {
+      c->proto = 1;
+    }
+  }
+  if (c->proto == 2) {
+    bool ok;
+    {
+      std::lock_guard<std::mutex> g(c->wmu);
+      const ssize_t r = H2::lib().mem_recv(c->h2->ng, reinterpret_cast<const uint8_t*>(c->in.data()), c->in.size());
+      c->in.clear();
+      ok = r >= 0 && H2::flush_locked(*c->h2);
+    }
+    if (!ok || eof) close_conn(c->id);
+    return;
+  }
   // parse complete frames
   std::string user;
   {
@@ -421,6 +826,16 @@ std::vector<FrameRequest> FrameRpcServer::poll(int lane, int max_n, int timeout_
 void FrameRpcServer::respond(uint64_t token, int status, const std::string& msg, const std::string& payload) {
   auto c = find((uint32_t)(token >> 32));
   if (!c || c->closed) return;
+  if (c->proto == 2) {
+    bool ok;
+    {
+      std::lock_guard<std::mutex> g(c->wmu);
+      H2::respond_locked(*c->h2, (int32_t)(token & 0x7fffffffu), status, msg, payload);
+      ok = H2::flush_locked(*c->h2);
+    }
+    if (!ok) close_conn(c->id);
+    return;
+  }
   const std::string f = make_response((uint32_t)token, status, msg, payload);
   bool ok;
   {

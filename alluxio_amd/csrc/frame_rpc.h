@@ -9,6 +9,11 @@
 // responses back.  Payloads are the same protobuf messages as the gRPC services, so one Python
 // servicer serves both transports; gRPC stays the wire-compatible path.
 //
+// The same port also speaks gRPC (HTTP/2 cleartext, prior knowledge): a connection that opens with
+// the HTTP/2 client preface is served by libnghttp2 framing on the I/O thread and its unary /
+// server-streaming calls go through the same lanes, Python dispatchers and reply cache, so a
+// stock gRPC client (a Java Alluxio client) gets the native path too.
+//
 // Frames (little endian):
 //   request  : u32 len | u32 call_id | u16 path_len | path | payload           (len = bytes after len)
 //   response : u32 len | u32 call_id | u16 status | u32 msg_len | msg | payload
@@ -59,6 +64,12 @@ class FrameRpcServer {
   // (namespace, block locations, mount table) and tags each put with the epoch it read BEFORE
   // running the handler, so a reply computed across a change is never served.
   void set_cacheable(uint32_t method, bool on);
+  // gRPC connections (HTTP/2, detected per connection by the client preface; see H2 in
+  // frame_rpc.cpp): kind 1 = server-streaming method, whose Python reply is a sequence of
+  // u32-length-prefixed messages (sent as one gRPC message each); 0 = unary.
+  void set_method_kind(uint32_t method, int kind);
+  uint64_t grpc_requests() const { return grpc_requests_.load(); }
+  static bool grpc_available();
   uint64_t epoch() const { return epoch_.load(std::memory_order_acquire); }
   void bump_epoch() { epoch_.fetch_add(1, std::memory_order_acq_rel); }
   void cache_put(uint32_t method, const std::string& user, const std::string& request, const std::string& reply,
@@ -70,6 +81,7 @@ class FrameRpcServer {
 
  private:
   struct Conn;
+  struct H2;
   void accept_loop();
   void io_loop(int idx);
   void on_readable(const std::shared_ptr<Conn>& c, int ep);
@@ -96,6 +108,8 @@ class FrameRpcServer {
   };
   std::vector<std::unique_ptr<Lane>> lane_q_;
   std::atomic<uint64_t> requests_{0};
+  std::atomic<uint64_t> grpc_requests_{0};
+  std::vector<uint8_t> kinds_;
   int wake_fd_ = -1;
 
   static std::string cache_key(uint32_t method, const std::string& user, const char* req, size_t n);

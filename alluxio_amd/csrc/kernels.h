@@ -163,9 +163,12 @@ hipError_t launch_mag_drain(uint64_t* bits, uint32_t nwords, uint64_t* out, hipS
 // into pages_out[page_base ...]; got[i] = pages claimed (< want when the magazine ran dry).
 // When total_chunks > 0 a second launch copies each item's bytes into its claimed pages (one
 // wave per 64 KiB chunk; items that came up short are skipped -- the host finishes them).
+// win_lo/win_len: the words the magazine's bits live in (refills fill a contiguous arc of the
+// bitmap); items search there first and fall back to the whole bitmap when it runs dry.
 hipError_t launch_mag_claim_scatter(uint64_t* bits, uint32_t nwords, const ClaimItem* items, uint32_t nitems,
                                     int64_t* pages_out, uint32_t pages_cap, uint32_t* got, uint32_t total_chunks,
-                                    uint8_t* arena, uint64_t page_size, hipStream_t stream);
+                                    uint8_t* arena, uint64_t page_size, hipStream_t stream, uint32_t win_lo = 0,
+                                    uint32_t win_len = 0);
 
 // K9: client page cache lookup.  Open-addressing (linear probing) table of page keys in HBM;
 // `key` = (interned file id << 24) | page index, so keys are exact (no hash collisions to

@@ -1687,10 +1687,35 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_groups_kernel(const
 //      aligned 16-byte vectors every 1 KiB.
 // Sequences whose header or output does not fit a window (long literal runs, long matches) go
 // through a per-sequence path that copies with all 64 lanes straight from HBM.
-template <uint32_t R, uint32_t S, uint32_t TMAX>
+__device__ __forceinline__ uint32_t lz_shfl(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
+__device__ __forceinline__ uint32_t lz_scan_add(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ uint32_t lz_scan_max(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
+    if (lane >= o) v = v > t ? v : t;
+  }
+  return v;
+}
+
+// kVec (variants 23-25): the walk and the code build without per-sequence scalar work.  PMC of the
+// scalar walk (profiles/r3_lz4_window.md) showed ~36 SALU instructions per sequence, and the CU's
+// one scalar unit serves all 16 resident waves: the chain is found by pointer doubling instead
+// (each lane's 2^k-step successor and visited-lane mask through ds_bpermute, 6 rounds), output
+// offsets by a wave prefix sum, and each output byte finds its sequence by a max-scan of start
+// marks -- all VALU/LDS, branch-free.
+template <uint32_t R, uint32_t S, uint32_t TMAX, bool kVec = false>
 __global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const Lz4Chunk* __restrict__ ch,
                                                                           int n, int32_t* __restrict__ out_sizes) {
-  static_assert((R & (R - 1)) == 0 && R >= 4096 && S % 1024 == 0 && TMAX % 64 == 0, "window kernel shape");
+  static_assert((R & (R - 1)) == 0 && R >= 4096 && S % 1024 == 0 && TMAX % 64 == 0 && TMAX <= 4096,
+                "window kernel shape");
   constexpr uint32_t rmask = R - 1;
   constexpr uint32_t NB = TMAX / 64;
   constexpr uint32_t kInc = 1u << 24, kFinal = 1u << 25, kErrShift = 26, kNxt = 0xFFFFFFu;
@@ -1701,7 +1726,11 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const
   __shared__ __attribute__((aligned(16))) uint8_t stage[S + 32];
   __shared__ __attribute__((aligned(16))) uint8_t ring[R];
   __shared__ uint32_t code[TMAX];
+  __shared__ uint8_t marks[kVec ? TMAX : 1];
   const uint32_t lane = threadIdx.x;
+  if constexpr (kVec) {
+    for (uint32_t i = lane; i < TMAX; i += kLzThreads) marks[i] = 0;
+  }
   for (int w = blockIdx.x; w < n; w += gridDim.x) {
     const gu8* __restrict__ src = reinterpret_cast<const gu8*>(ch[w].src);
     const uint32_t slen = ch[w].src_bytes;
@@ -1907,19 +1936,68 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const
       uint32_t cur = 0, T = 0, cnt = 0, opo = 0;
       uint64_t mask = 0;
       int stop = 0;   // 0: next token at cur, 1: lane cur needs input, 2: error, 3: stream done, 4: too long
-      while (cur < kLzThreads) {
-        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)A, (int)cur);
-        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)tot, (int)cur);
-        if (a & kInc) { stop = 1; break; }
-        if (a >> kErrShift) { status = -(int32_t)(a >> kErrShift); stop = 2; break; }
-        if (T + b > TMAX) { stop = cnt ? 0 : 4; break; }
-        opo = lane == cur ? T : opo;
-        mask |= 1ull << cur;
-        T += b;
-        ++cnt;
-        if (a & kFinal) { stop = 3; break; }
-        cur = a & kNxt;
-        if (ip + cur >= slen) { stop = 3; break; }
+      if constexpr (kVec) {
+        const uint32_t ecode = A >> kErrShift;
+        const bool regular = !(A & (kInc | kFinal)) && !ecode;
+        const bool ends = regular && ip + (A & kNxt) >= slen;   // the stream ends after this match
+        uint32_t J = regular && !ends && (A & kNxt) < kLzThreads ? (A & kNxt) : kLzThreads;
+        uint64_t Rm = 1ull << lane;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const uint32_t src = J < kLzThreads ? J : lane;
+          const uint32_t rlo = lz_shfl((uint32_t)Rm, src), rhi = lz_shfl((uint32_t)(Rm >> 32), src);
+          const uint32_t jj = lz_shfl(J, src);
+          if (J < kLzThreads) {
+            Rm |= ((uint64_t)rhi << 32) | rlo;
+            J = jj;
+          }
+        }
+        const uint64_t C = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(Rm >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)Rm);
+        const uint64_t bad = C & __ballot((A & kInc) || ecode);
+        const uint32_t fb = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+        const uint64_t pre = fb < 64 ? C & ((1ull << fb) - 1) : C;
+        const uint32_t v = (pre >> lane) & 1ull ? tot : 0u;
+        const uint32_t incl = lz_scan_add(v, lane);
+        const uint64_t over = pre & __ballot(incl > TMAX);
+        const uint32_t fo = over ? (uint32_t)__builtin_ctzll(over) : 64u;
+        mask = fo < 64 ? pre & ((1ull << fo) - 1) : pre;
+        cnt = (uint32_t)__builtin_popcountll(mask);
+        opo = incl - v;
+        if (fo < fb) {
+          stop = cnt ? 0 : 4;
+          cur = fo;
+        } else if (fb < 64) {
+          const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)A, (int)fb);
+          cur = fb;
+          if (a & kInc) {
+            stop = 1;
+          } else {
+            stop = 2;
+            status = -(int32_t)(a >> kErrShift);
+          }
+        } else {
+          const uint32_t last = 63u - (uint32_t)__builtin_clzll(mask);
+          const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)A, (int)last);
+          cur = a & kNxt;
+          stop = (a & kFinal) || ip + cur >= slen ? 3 : 0;
+        }
+        if (cnt) T = (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)(63u - (uint32_t)__builtin_clzll(mask)));
+      } else {
+        while (cur < kLzThreads) {
+          const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)A, (int)cur);
+          const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)tot, (int)cur);
+          if (a & kInc) { stop = 1; break; }
+          if (a >> kErrShift) { status = -(int32_t)(a >> kErrShift); stop = 2; break; }
+          if (T + b > TMAX) { stop = cnt ? 0 : 4; break; }
+          opo = lane == cur ? T : opo;
+          mask |= 1ull << cur;
+          T += b;
+          ++cnt;
+          if (a & kFinal) { stop = 3; break; }
+          cur = a & kNxt;
+          if (ip + cur >= slen) { stop = 3; break; }
+        }
       }
       if (stop == 2) break;
       if (cnt == 0) {
@@ -1942,7 +2020,31 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const
         status = __builtin_amdgcn_readlane(bad_lit ? -2 : -5, (int)f);
         break;
       }
-      if (tok) {
+      if constexpr (kVec) {
+        // start marks, then per block of 64 output bytes: owner = max-scan of the marks
+        if (tok && tot) marks[opo] = (uint8_t)(lane + 1);
+        lz_wave_sync();
+        uint32_t carry = 0;
+        for (uint32_t b0 = 0; b0 < T; b0 += kLzThreads) {
+          const uint32_t x = b0 + lane;
+          const bool in = x < T;
+          uint32_t m = 0;
+          if (in) {
+            m = marks[x];
+            marks[x] = 0;
+          }
+          uint32_t own = lz_scan_max(m, lane);
+          own = own ? own : carry;
+          carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+          const uint32_t j = own ? own - 1 : 0;
+          const uint32_t o_opo = lz_shfl(opo, j), o_lit = lz_shfl(lit, j), o_q = lz_shfl(q, j), o_off = lz_shfl(off, j);
+          if (in) {
+            const uint32_t k = x - o_opo;
+            const int32_t y = (int32_t)x - (int32_t)o_off;
+            code[x] = k < o_lit ? o_q + k : (y >= 0 ? (kRef | (uint32_t)y) : (kOld | (uint32_t)((int32_t)op + y)));
+          }
+        }
+      } else if (tok) {
         for (uint32_t k = 0; k < lit; ++k) code[opo + k] = q + k;
         for (uint32_t x = opo + lit; x < opo + tot; ++x) {
           const int32_t y = (int32_t)x - (int32_t)off;
@@ -2071,7 +2173,10 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
       case 19: hipLaunchKernelGGL((lz4_decompress_window_kernel<8192, 1024, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 20: hipLaunchKernelGGL((lz4_decompress_window_kernel<4096, 1024, 256>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 21: hipLaunchKernelGGL((lz4_decompress_window_kernel<8192, 2048, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
-      default: hipLaunchKernelGGL((lz4_decompress_window_kernel<16384, 1024, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 22: hipLaunchKernelGGL((lz4_decompress_window_kernel<16384, 1024, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 23: hipLaunchKernelGGL((lz4_decompress_window_kernel<4096, 1024, 256, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 24: hipLaunchKernelGGL((lz4_decompress_window_kernel<8192, 1024, 256, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      default: hipLaunchKernelGGL((lz4_decompress_window_kernel<4096, 1024, 512, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
     }
   }
   return hipGetLastError();

@@ -260,12 +260,24 @@ class AlluxioMasterProcess:
                     raise UnavailableException("master is a standby (not primary)")
             self.server.gate = standby_gate
         self.native_rpc = None
+        # alluxio.master.rpc.native.grpc.enabled: the master RPC port itself is the native front
+        # end, which serves gRPC (HTTP/2) connections too -- stock gRPC clients (Java) then get the
+        # C++ I/O threads, lanes and reply cache instead of the grpcio server
+        native_grpc = self.server.enable_grpc and \
+            self.conf.get_bool("alluxio.master.rpc.native.grpc.enabled", "true") and \
+            self.conf.get_bool("alluxio.master.native.rpc.enabled", "true")
+        if native_grpc:
+            from ..ops.native import lib
+            native_grpc = lib().FrameRpcServer.grpc_available()
         if self.server.enable_grpc and self.conf.get_bool("alluxio.master.native.rpc.enabled", "true"):
             # metadata fast path next to gRPC (same servicers): see alluxio_amd/rpc/native.py.
             # Started first, so the port is advertised from the first gRPC call on.
             from ..rpc.native import NativeRpcFrontend
+            if native_grpc:
+                self.server.enable_grpc = False
             self.native_rpc = NativeRpcFrontend(
-                self.server, self.server.host, self.conf.get_int("alluxio.master.native.rpc.port", "0"),
+                self.server, self.server.host,
+                self.server.port if native_grpc else self.conf.get_int("alluxio.master.native.rpc.port", "0"),
                 fast_threads=self.conf.get_int("alluxio.master.native.rpc.fast.threads", "2"),
                 blocking_threads=self.conf.get_int("alluxio.master.native.rpc.blocking.threads", "16"),
                 mutation_threads=self.conf.get_int("alluxio.master.native.rpc.mutation.threads", "2"),
@@ -274,6 +286,8 @@ class AlluxioMasterProcess:
                 and self.fs_master.audit is None,
                 epoch_source=self.fs_master.add_epoch_listener)
             self._version_handler.native_port = self.native_rpc.start()
+            if native_grpc:
+                self.server.port = self.native_rpc.port
         addr = self.server.start()
         self.meta_master.master_address = addr
         self.start_time = time.time()

@@ -349,7 +349,14 @@ class Channel:
                     ("grpc.max_receive_message_length", MAX_MESSAGE),
                     ("grpc.max_send_message_length", MAX_MESSAGE)])
                 if self.auth is not None:
-                    self._authenticate(self._grpc)
+                    try:
+                        self._authenticate(self._grpc)
+                    except BaseException:
+                        # not authenticated (server starting, standby, ...): the next call
+                        # reconnects and authenticates again instead of going out without a channel id
+                        self._grpc.close()
+                        self._grpc = None
+                        raise
             return self._grpc
 
     def _authenticate(self, ch) -> None:

@@ -51,6 +51,9 @@ MUTATION_METHODS = frozenset({
     "GetNewBlockIdForFile",
 })
 FS_SERVICE = "alluxio.grpc.file.FileSystemMasterClientService"
+SASL_SERVICE = "alluxio.grpc.sasl.SaslAuthenticationService"
+# services a gRPC caller reaches without an authenticated channel (rpc._UNAUTH_SERVICES)
+UNAUTH_SERVICES = frozenset({SASL_SERVICE, "alluxio.grpc.version.ServiceVersionClientService"})
 LANE_FAST, LANE_BLOCKING, LANE_MUTATION = 0, 1, 2
 AUTH_PATH = "@auth"
 _LIVE: "weakref.WeakSet[NativeRpcFrontend]" = weakref.WeakSet()
@@ -130,18 +133,27 @@ class NativeRpcFrontend:
         self.rpc = rpc_server
         self.methods = [(AUTH_PATH, None, None)]
         lanes = [0]
-        for svc, servicer in rpc_server._servicers.items():
+        servicers = dict(rpc_server._servicers)
+        if rpc_server.authenticator is not None:
+            servicers[SASL_SERVICE] = rpc_server.authenticator   # as RpcServer.start installs it
+        for svc, servicer in servicers.items():
             for name, spec in SERVICES[svc].items():
                 # unary requests only; a server-streaming reply travels as one frame of
-                # length-prefixed messages (metadata listings, not data streams)
-                if spec.client_streaming or not hasattr(servicer, name):
+                # length-prefixed messages (metadata listings, not data streams).  The SASL
+                # handshake (one client message, one reply) serves gRPC connections.
+                if not hasattr(servicer, name):
                     continue
-                if spec.server_streaming and svc not in STREAM_SERVICES:
+                if spec.client_streaming and svc != SASL_SERVICE:
+                    continue
+                if spec.server_streaming and svc not in STREAM_SERVICES and svc != SASL_SERVICE:
                     continue
                 self.methods.append((spec.path, spec, getattr(servicer, name)))
-                lanes.append(LANE_FAST if name in FAST_METHODS else
+                lanes.append(LANE_FAST if name in FAST_METHODS or svc == SASL_SERVICE else
                              LANE_MUTATION if name in MUTATION_METHODS and svc == FS_SERVICE else LANE_BLOCKING)
         self.server = lib().FrameRpcServer(host, port, [m[0] for m in self.methods], lanes, io_threads)
+        for i, (_path, spec, _fn) in enumerate(self.methods):
+            if spec is not None and spec.server_streaming:
+                self.server.set_method_kind(i, 1)
         self.fast_threads, self.blocking_threads, self.batch = fast_threads, blocking_threads, batch
         self.mutation_threads, self.mutation_batch = max(1, mutation_threads), max(1, mutation_batch)
         self.lanes = lanes
@@ -200,6 +212,18 @@ class NativeRpcFrontend:
             auth.provider.authenticate(user, password)
         self.server.set_user(token, user)
 
+    def _grpc_user(self, spec, user: str):
+        """The caller of a gRPC-connection request (user = "\\x01" channel-id "\\0" alluxio-user),
+        resolved as the gRPC handlers do (rpc._Handler._enter): NOSASL trusts the alluxio-user
+        header, otherwise the user is the one the channel authenticated as."""
+        cid, _, auser = user[1:].partition("\0")
+        auth = self.rpc.authenticator
+        if auth is None:
+            return auser or None
+        if spec.service in UNAUTH_SERVICES:
+            return None
+        return auth.user_for(cid or None)
+
     def _one(self, token, midx, user, payload, nonblocking: bool = False, carried: dict | None = None):
         """Run one request; returns the reply tuple, or None when the reply is deferred until
         the journal entries the handler appended are durable (sent by the flush callback), or
@@ -214,13 +238,17 @@ class NativeRpcFrontend:
         pending = None
         after = None
         cache_ep = None
+        key_user = user
         try:
             if midx == 0:
                 self._auth(token, payload)
                 return (token, 0, "", b"")
-            if self.rpc.authenticator is not None and not user:
-                raise ex.UnauthenticatedException("native channel is not authenticated")
             path, spec, fn = self.methods[midx]
+            key_user = user     # the reply cache is keyed by the connection's caller string
+            if user and user[0] == "\x01":
+                user = self._grpc_user(spec, user)
+            elif self.rpc.authenticator is not None and not user:
+                raise ex.UnauthenticatedException("native channel is not authenticated")
             self.rpc.check(spec)
             req = spec.request.FromString(payload)
             cache_ep = self.server.epoch() if self.cacheable[midx] and _cacheable(req) else None
@@ -231,7 +259,7 @@ class NativeRpcFrontend:
                     pending.update(carried)
                 if spec.server_streaming:
                     parts = []
-                    for m in fn(req, _Ctx(user)):
+                    for m in fn(iter([req]) if spec.client_streaming else req, _Ctx(user)):
                         b = m.SerializeToString()
                         parts.append(len(b).to_bytes(4, "little"))
                         parts.append(b)
@@ -239,7 +267,7 @@ class NativeRpcFrontend:
                 else:
                     body = fn(req, _Ctx(user)).SerializeToString()
             if cache_ep is not None and not pending:
-                self.server.cache_put(midx, user, payload, body, cache_ep)
+                self.server.cache_put(midx, key_user, payload, body, cache_ep)
             reply = (token, 0, "", body)
         except WouldBlock:
             self.spilled += 1
@@ -253,7 +281,7 @@ class NativeRpcFrontend:
             if cache_ep is not None and not pending and isinstance(e, ex.NotFoundException):
                 # "does not exist" of a ONCE lookup: as stable as the UFS absent-path cache
                 # behind it (a create, load, sync change or remount bumps the epoch)
-                self.server.cache_put(midx, user, payload, b"", cache_ep, reply[1], reply[2])
+                self.server.cache_put(midx, key_user, payload, b"", cache_ep, reply[1], reply[2])
         if pending:
             self._defer(pending, reply, after)
             return None

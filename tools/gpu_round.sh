@@ -47,6 +47,12 @@ for s in $STEPS; do
       run ingest_s3native 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 2g --dram 6g --factor 2 --depths 1,3 --out "$OUT/ufs_ingest_s3native.jsonl"
       run ingest_s3requests 600 python tools/ufs_ingest_bench.py --ufs s3native --native-reader false --hbm 2g --dram 6g --factor 2 --depths 3 --out "$OUT/ufs_ingest_s3native.jsonl"
       ;;
+    lz4pmc)
+      for v in ${LZ4_PMC_VARIANTS:-20}; do
+        run lz4pmc_a_v$v 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -d "$OUT/lz4pmc_a_v$v" -o pmc --output-format csv -- python3 tools/lz4_one.py --variant $v --data text --chunks 4096
+        run lz4pmc_b_v$v 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --kernel-trace -d "$OUT/lz4pmc_b_v$v" -o pmc --output-format csv -- python3 tools/lz4_one.py --variant $v --data text --chunks 4096
+      done
+      ;;
     crc) run crc_bench 300 python tools/crc_bench.py --gb 4 --out "$OUT/crc_bench.jsonl" ;;
     dl) run dl_bench_100k 400 python tools/dl_bench.py --files 100000 --out "$OUT/dl_bench_100k.jsonl" ;;
     dl1m) run dl_bench_1m 900 python tools/dl_bench.py --ufs synthetic --files 1000000 --threads 32 --out "$OUT/dl_bench_1m.jsonl" ;;
