@@ -22,8 +22,11 @@ which keeps the whole control flow testable without GPUs.
 """
 from __future__ import annotations
 
+import json
 import logging
 import threading
+import time
+from datetime import timedelta
 
 from ..proto import pb
 from ..utils import ids
@@ -63,7 +66,8 @@ def cross_page_segments(src_base: int, src_pages, src_ps: int, dst_base: int, ds
 class TransferPlane:
     """Peer block mover bound to one worker (one rank of the node's worker group)."""
 
-    def __init__(self, worker, rank: int, world: int, addr_to_rank: dict[str, int], group=None):
+    def __init__(self, worker, rank: int, world: int, addr_to_rank: dict[str, int], group=None, store=None,
+                 rebuild_wait_s: float = 5.0, timeout_s: float = 60.0):
         import torch.distributed as dist
         self.w = worker
         self.rank = rank
@@ -75,16 +79,35 @@ class TransferPlane:
         self._collective_lock = threading.Lock()
         self.bytes_pulled = 0
         self.bytes_gathered = 0
+        # membership: ``members`` are the original ranks of the current collective group, ``gen``
+        # counts rebuilds; ``store`` (the rendezvous store) lets survivors of a dead rank agree on
+        # a new group without it (None = a failed collective just raises)
+        self.orig_rank = rank
+        self.members = list(range(world))
+        self.gen = 0
+        self.store = store
+        self.rebuild_wait_s = rebuild_wait_s
+        self.timeout_s = timeout_s
+        self._pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        self.rebuilds = 0
 
     # ---- setup --------------------------------------------------------------------------------
     @classmethod
-    def establish(cls, worker, group=None) -> "TransferPlane":
-        """Collective: every rank of ``group`` calls this once after its worker has started."""
+    def establish(cls, worker, group=None, store=None, rebuild_wait_s: float = 5.0,
+                  timeout_s: float = 60.0) -> "TransferPlane":
+        """Collective: every rank of ``group`` calls this once after its worker has started.
+        ``store`` defaults to the default group's rendezvous store (used to rebuild the group
+        when a rank dies; see :meth:`_rebuild`)."""
         import torch.distributed as dist
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         allv = [None] * world
         dist.all_gather_object(allv, _addr_key(worker.address), group=group)
-        plane = cls(worker, rank, world, {a: r for r, a in enumerate(allv)}, group)
+        if store is None and group is None:
+            try:
+                store = dist.distributed_c10d._get_default_store()
+            except Exception:  # noqa: BLE001 - no store: no rebuild
+                store = None
+        plane = cls(worker, rank, world, {a: r for r, a in enumerate(allv)}, group, store, rebuild_wait_s, timeout_s)
         worker.transfer_plane = plane
         if plane.backend == "nccl":
             import torch
@@ -103,7 +126,7 @@ class TransferPlane:
 
     def can_reach(self, addr) -> bool:
         r = self.rank_of(addr)
-        return r is not None and r != self.rank
+        return r is not None and r != self.orig_rank and r in self.members
 
     @property
     def device_plane(self) -> bool:
@@ -135,27 +158,93 @@ class TransferPlane:
     def replicate_all(self, blocks: list[tuple[int, int, int]]) -> int:
         """Collective: ``blocks`` = [(block_id, length, owner_rank)], identical on every rank.
         Afterwards every rank's worker holds every block.  One ``all_gather_into_tensor`` per
-        round moves one block from each owner to everyone (rounds = max blocks per owner)."""
-        import torch.distributed as dist
-        by_owner: dict[int, list[tuple[int, int]]] = {r: [] for r in range(self.world)}
+        round moves one block from each owner to everyone (rounds = max blocks per owner).
+
+        A rank that dies mid-way fails the round's collective on the others; with a rendezvous
+        store they rebuild the group among themselves (:meth:`_rebuild`) and redo the rounds from
+        the earliest one any survivor failed in, without the dead rank's blocks (rounds are
+        idempotent: blocks a rank already holds are skipped)."""
+        by_owner: dict[int, list[tuple[int, int]]] = {}
         for bid, length, owner in blocks:
-            by_owner[owner].append((bid, length))
-        rounds = max((len(v) for v in by_owner.values()), default=0)
+            by_owner.setdefault(owner, []).append((bid, length))
         moved = 0
         with self._collective_lock:
-            for k in range(rounds):
-                entries = [by_owner[r][k] if k < len(by_owner[r]) else (None, 0) for r in range(self.world)]
+            k = 0
+            while True:
+                members = self.members
+                rounds = max((len(by_owner.get(r, ())) for r in members), default=0)
+                if k >= rounds:
+                    break
+                entries = [by_owner[r][k] if k < len(by_owner.get(r, ())) else (None, 0) for r in members]
                 shard = max(n for _, n in entries)
                 if shard == 0:
+                    k += 1
                     continue
                 send, out = self._staging(shard)
                 mine = entries[self.rank]
                 if mine[0] is not None:   # bytes past a short block are never read: no zero fill
                     self._copy_block_out(mine[0], mine[1], send)
-                dist.all_gather_into_tensor(out, send, group=self.group)
+                try:
+                    self._pg._allgather_base(out, send).wait()
+                except Exception:
+                    if self.store is None:
+                        raise
+                    LOG.warning("replicate_all: collective of round %d failed (gen %d); rebuilding the group",
+                                k, self.gen, exc_info=True)
+                    k = self._rebuild(k)
+                    continue
                 moved += self._scatter_into_pages(out, shard, entries)
+                k += 1
         self.bytes_gathered += moved
         return moved
+
+    def _rebuild(self, failed_round: int) -> int:
+        """Re-form the collective group among the ranks still alive; returns the round to resume
+        from.  Survivors check in under ``gen<g+1>/`` of the rendezvous store; the first to arrive
+        waits up to ``rebuild_wait_s`` for the others, then publishes the member list and the
+        resume round (the earliest any survivor failed in); everyone builds a new process group
+        over a prefixed view of the store (no participation of the dead rank needed, unlike
+        ``new_group``)."""
+        import torch.distributed as dist
+        g = self.gen + 1
+        st = self.store
+        pre = f"alluxio/plane/gen{g}/"
+        st.set(pre + f"alive/{self.orig_rank}", str(failed_round))
+        if st.add(pre + "arrivals", 1) == 1:
+            deadline = time.time() + self.rebuild_wait_s
+            while time.time() < deadline:
+                if all(st.check([pre + f"alive/{r}"]) for r in self.members):
+                    break
+                time.sleep(0.05)
+            alive = [r for r in self.members if st.check([pre + f"alive/{r}"])]
+            resume = min(int(st.get(pre + f"alive/{r}")) for r in alive)
+            st.set(pre + "members", json.dumps({"members": alive, "resume": resume}))
+        else:
+            st.wait([pre + "members"], timedelta(seconds=self.rebuild_wait_s * 2 + 30))
+        plan = json.loads(st.get(pre + "members"))
+        members = plan["members"]
+        if self.orig_rank not in members:
+            raise RuntimeError(f"rank {self.orig_rank} was left out of the rebuilt transfer group (gen {g})")
+        rank = members.index(self.orig_rank)
+        pstore = dist.PrefixStore(pre + "pg/", st)
+        timeout = timedelta(seconds=self.timeout_s)
+        if self.backend == "nccl":
+            opts = dist.ProcessGroupNCCL.Options()
+            try:
+                opts._timeout = timeout
+            except AttributeError:
+                pass
+            pg = dist.ProcessGroupNCCL(pstore, rank, len(members), opts)
+        else:
+            pg = dist.ProcessGroupGloo(pstore, rank, len(members), timeout)
+        dead = [r for r in self.members if r not in members]
+        self._pg = pg
+        self.members = members
+        self.rank, self.world, self.gen = rank, len(members), g
+        self.rebuilds += 1
+        LOG.warning("transfer group rebuilt (gen %d): members %s, lost %s, resuming at round %d", g, members, dead,
+                    plan["resume"])
+        return int(plan["resume"])
 
     def _staging(self, shard: int):
         """(send[shard], out[shard*world]) views of ONE persistent buffer per plane, grown

@@ -299,3 +299,85 @@ def test_distributed_load_replication_all_uses_collective(tmp_path):
     # rank 0 already held the cached file, so it receives only rank 1's UFS-loaded blocks; rank 1
     # receives the cached file plus rank 0's share of the UFS file -- both through the all-gather
     assert all(o["gathered"] > 0 for o in outs), outs
+
+
+REBUILD_SCRIPT = r"""
+import os, sys, json
+from datetime import timedelta
+sys.path.insert(0, %(root)r)
+import numpy as np, torch, torch.distributed as dist
+from alluxio_amd.conf import Configuration
+from alluxio_amd.master.process import AlluxioMasterProcess
+from alluxio_amd.worker.process import AlluxioWorkerProcess
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.parallel.transfer import TransferPlane
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=world,
+                        timeout=timedelta(seconds=60))
+work = %(work)r
+conf = Configuration({"alluxio.master.journal.folder": work + "/journal",
+    "alluxio.worker.tieredstore.level0.dirs.path": "dram", "alluxio.worker.tieredstore.level0.dirs.quota": "128MB",
+    "alluxio.user.block.size.bytes.default": "1MB"})
+box = [None]
+if rank == 0:
+    m = AlluxioMasterProcess(conf, host="127.0.0.1", port=0, root_ufs=work + "/ufs"); box[0] = m.start(start_heartbeats=False)
+dist.broadcast_object_list(box, src=0)
+w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, work_dir=work + "/w%%d" %% rank)
+w.start(start_heartbeats=False)
+plane = TransferPlane.establish(w.worker, rebuild_wait_s=3.0, timeout_s=30.0)
+fs = FileSystem(conf=conf.copy(), master_address=box[0])
+data = np.random.default_rng(20 + rank).integers(0, 256, 3 * (1 << 20) + 11, dtype=np.uint8)
+fs.write_file("/rb/f%%d" %% rank, data, write_type="MUST_CACHE")
+mine = [(b.blockInfo.blockId, b.blockInfo.length, rank) for b in fs.get_status("/rb/f%%d" %% rank).info.fileBlockInfos]
+allb = [None] * world
+dist.all_gather_object(allb, mine)
+blocks = [x for part in allb for x in part]
+if rank == world - 1:
+    # this rank dies after the first round of the collective
+    orig = plane._scatter_into_pages
+    def dying(*a, **kw):
+        r = orig(*a, **kw)
+        os._exit(0)
+    plane._scatter_into_pages = dying
+moved = plane.replicate_all(blocks)
+alive = [r for r in range(world - 1)]
+have_alive = all(w.worker.has_block(b) for b, _, o in blocks if o in alive)
+first_dead = allb[world - 1][0][0]
+print(json.dumps({"rank": rank, "moved": moved, "rebuilds": plane.rebuilds, "members": plane.members,
+                  "have_alive": have_alive, "dead_round0": w.worker.has_block(first_dead),
+                  "dead_later": any(w.worker.has_block(b) for b, _, _ in allb[world - 1][1:])}), flush=True)
+plane._pg.barrier().wait()
+fs.close(); w.stop()
+plane._pg.barrier().wait()
+if rank == 0:
+    m.stop()
+os._exit(0)
+"""
+
+
+def test_replicate_all_rebuilds_group_after_rank_death(tmp_path):
+    """A rank dies in the middle of replicate_all: the survivors' collective fails, they agree on
+    a new group through the rendezvous store and finish replicating among themselves."""
+    script = REBUILD_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path)}
+    path = tmp_path / "rebuild.py"
+    path.write_text(script)
+    procs = []
+    for rank in range(3):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="3", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, str(path)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for rank, p in enumerate(procs):
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("rebuild rank timed out")
+        if rank < 2:
+            assert p.returncode == 0, err[-3000:]
+            outs.append(json.loads(out.strip().splitlines()[-1]))
+    for o in outs:
+        assert o["rebuilds"] == 1 and o["members"] == [0, 1], o
+        assert o["have_alive"] and o["dead_round0"] and not o["dead_later"], o
+        assert o["moved"] > 0, o

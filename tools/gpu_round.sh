@@ -60,6 +60,13 @@ for s in $STEPS; do
       # CPU-only: the master metadata bench on the box's CPU share (no GPU used)
       run master_bench 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --out "$OUT/master_bench.json"
       ;;
+    mastergrpc)
+      run master_bench_native 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --out "$OUT/master_bench_native.json"
+      # CPU-only: stock gRPC (grpcio) clients against the master port, which the native front end
+      # serves (alluxio.master.rpc.native.grpc.enabled, default on), and against the grpcio server
+      run master_bench_grpc_native 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_native.json"
+      run master_bench_grpcio 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --master-prop alluxio.master.rpc.native.grpc.enabled=false --out "$OUT/master_bench_grpcio.json"
+      ;;
     ring)
       run bench_ring4k 300 python bench.py --buffer-size 4k --steps 200 --warmup 20
       run bench_ring4k_d64 300 python bench.py --buffer-size 4k --depth 64 --steps 200 --warmup 20
@@ -94,10 +101,6 @@ for s in $STEPS; do
       ;;
     hostread)
       run worker_bench_host 900 python tools/worker_bench_host.py --threads 16,64,256 --duration 8s --warmup 2s --out "$OUT/worker_bench_host.jsonl"
-      ;;
-    mastergrpc)
-      run master_bench_native 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --out "$OUT/master_bench_native.json"
-      run master_bench_grpc 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 4 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc.json"
       ;;
     masterufs)
       # CPU-only: CreateDir THROUGH against a root UFS whose every call sleeps 5 ms
