@@ -147,7 +147,10 @@ def master_routes(master) -> dict:
         ("GET", "/api/v1/master/ping"): lambda q, b: _json({"ok": True}),
     })
     from .ui import master_ui_routes
+    from .webui_api import master_webui_routes, static_routes
     r.update(master_ui_routes(master))
+    r.update(master_webui_routes(master))
+    r.update(static_routes("master"))
     del pb
     return r
 
@@ -177,5 +180,8 @@ def worker_routes(wp) -> dict:
         ("POST", "/api/v1/logLevel"): log_level_route,
     })
     from .ui import worker_ui_routes
+    from .webui_api import static_routes, worker_webui_routes
     r.update(worker_ui_routes(wp))
+    r.update(worker_webui_routes(wp))
+    r.update(static_routes("worker"))
     return r

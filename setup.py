@@ -31,7 +31,7 @@ setup(
     long_description_content_type="text/markdown",
     python_requires=">=3.10",
     packages=find_packages(include=["alluxio_amd", "alluxio_amd.*"]),
-    package_data={"alluxio_amd": ["_C*.so", "csrc/*.cpp", "csrc/*.h", "csrc/*.hip"]},
+    package_data={"alluxio_amd": ["_C*.so", "csrc/*.cpp", "csrc/*.h", "csrc/*.hip", "web/static/webui/*"]},
     install_requires=["numpy", "grpcio", "protobuf", "torch"],
     extras_require={"table": ["pyarrow"], "web": ["fastapi", "uvicorn"], "test": ["pytest", "pytest-timeout"]},
     entry_points={"console_scripts": ["alluxio = alluxio_amd.cli.main:main"]},

@@ -1,6 +1,7 @@
 """Shell / CLI tests (reference shell/src/test and tests/.../cli/fs/command/*CommandIntegrationTest:
 run a command against a LocalAlluxioCluster, check output + namespace effects)."""
 import io
+import json
 import os
 
 import pytest
@@ -312,4 +313,45 @@ def test_web_ui_pages(cluster):
     for path, needle in [("/", "Storage Directories"), ("/blockinfo", "Block Id"), ("/metrics", "Metric")]:
         body = urllib.request.urlopen(wbase + path, timeout=10).read().decode()
         assert needle in body, path
+    fs.close()
+
+
+def test_webui_spa_and_json(cluster):
+    """The single-page web UI (/webui) and the webui_* JSON it renders, with the reference's field
+    names (AlluxioMasterRestServiceHandler webui endpoints / MasterWebUI*.java)."""
+    import urllib.request
+    fs = cluster.client()
+    fs.write_file("/spa/x.bin", b"12345", write_type="MUST_CACHE")
+    base = f"http://127.0.0.1:{cluster.master.web_port}"
+
+    def get(path):
+        r = urllib.request.urlopen(base + path, timeout=10)
+        return r.status, r.headers["Content-Type"], r.read().decode()
+    st, ct, body = get("/webui")
+    assert st == 200 and ct.startswith("text/html") and 'data-role="master"' in body and "/webui/app.js" in body
+    st, ct, js = get("/webui/app.js")
+    assert ct.startswith("application/javascript") and "webui_overview" in js and "webui_browse" in js
+    j = lambda p: json.loads(get("/api/v1/master/" + p)[2])  # noqa: E731
+    o = j("webui_overview")
+    assert {"masterNodeAddress", "liveWorkerNodes", "capacity", "usedCapacity", "storageTierInfos", "uptime",
+            "version"} <= set(o) and o["liveWorkerNodes"] == str(len(cluster.workers))
+    b = j("webui_browse?path=/spa")
+    assert b["nTotalFile"] == 1 and b["fileInfos"][0]["absolutePath"] == "/spa/x.bin"
+    assert {"inAlluxioPercentage", "blockSizeBytes", "mode", "owner", "persistenceState"} <= set(b["fileInfos"][0])
+    f = j("webui_browse?path=/spa/x.bin")
+    assert f["currentDirectory"]["isDirectory"] is False and len(f["fileBlocks"]) == 1
+    assert j("webui_browse?path=/nope")["fileDoesNotExistException"]
+    assert any(x["absolutePath"] == "/spa/x.bin" for x in j("webui_data")["fileInfos"])
+    w = j("webui_workers")
+    assert len(w["normalNodeInfos"]) == len(cluster.workers) and w["failedNodeInfos"] == []
+    assert any(r[0] == "alluxio.master.journal.folder" for r in j("webui_config")["configuration"])
+    assert "/" in j("webui_mounttable")["mountPointInfos"]
+    assert "operationMetrics" in j("webui_metrics") and "refreshInterval" in j("webui_init")
+    wk = cluster.workers[0]
+    wbase = f"http://127.0.0.1:{wk.web_port}"
+    assert 'data-role="worker"' in urllib.request.urlopen(wbase + "/webui", timeout=10).read().decode()
+    wo = json.loads(urllib.request.urlopen(wbase + "/api/v1/worker/webui_overview", timeout=10).read())
+    assert wo["storageDirs"] and wo["usageOnTiers"]
+    wb = json.loads(urllib.request.urlopen(wbase + "/api/v1/worker/webui_blockinfo", timeout=10).read())
+    assert wb["nTotalFile"] >= 1 and wb["fileBlocksOnTier"][0]["blockLength"] > 0
     fs.close()
