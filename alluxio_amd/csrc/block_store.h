@@ -364,7 +364,7 @@ class BlockStore {
   bool use_device_evict_ = true;
   // K7 measured slower than the host bitmap scan end to end (profiles/r2_evict_bench.jsonl):
   // off unless alluxio.worker.hbm.device.alloc.enabled
-  bool use_device_alloc_ = false;             // K7 magazine: opt-in until validated on the device
+  bool use_device_alloc_ = true;              // K7 magazine: bulk creates (>= min pages) and ingest claim on the GPU
   bool demote_on_evict_ = false;
   uint32_t device_alloc_min_pages_ = 1024;     // create_blocks: device claims from this many pages
   hipStream_t internal_stream_ = nullptr;

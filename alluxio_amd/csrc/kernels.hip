@@ -1711,7 +1711,7 @@ __device__ __forceinline__ uint32_t lz_scan_max(uint32_t v, uint32_t lane) {
 // (each lane's 2^k-step successor and visited-lane mask through ds_bpermute, 6 rounds), output
 // offsets by a wave prefix sum, and each output byte finds its sequence by a max-scan of start
 // marks -- all VALU/LDS, branch-free.
-template <uint32_t R, uint32_t S, uint32_t TMAX, bool kVec = false>
+template <uint32_t R, uint32_t S, uint32_t TMAX, bool kVec = false, bool kPre = false>
 __global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const Lz4Chunk* __restrict__ ch,
                                                                           int n, int32_t* __restrict__ out_sizes) {
   static_assert((R & (R - 1)) == 0 && R >= 4096 && S % 1024 == 0 && TMAX % 64 == 0 && TMAX <= 4096,
@@ -1727,6 +1727,7 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const
   __shared__ __attribute__((aligned(16))) uint8_t ring[R];
   __shared__ uint32_t code[TMAX];
   __shared__ uint8_t marks[kVec ? TMAX : 1];
+  __shared__ uint8_t winb[kPre ? TMAX : 1];   // the window's output bytes (reference targets)
   const uint32_t lane = threadIdx.x;
   if constexpr (kVec) {
     for (uint32_t i = lane; i < TMAX; i += kLzThreads) marks[i] = 0;
@@ -2054,6 +2055,63 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const
       lz_wave_sync();
       // 4. resolve references block by block, gather the bytes
       uint32_t outb[NB];
+      if constexpr (kVec && kPre) {
+        // the bytes of every non-reference position are fetched first (stage / ring / HBM: the
+        // far loads are in flight while the references resolve), references resolve to window
+        // positions by pointer jumping, then read the window's bytes from LDS
+        uint32_t cb[NB];
+        bool farb[NB];
+        bool anyfar = false;
+#pragma unroll
+        for (uint32_t bi = 0; bi < NB; ++bi) {
+          const uint32_t x = bi * kLzThreads + lane;
+          cb[bi] = x < T ? code[x] : kRef;
+          const uint32_t cv = cb[bi] & kVal;
+          farb[bi] = x < T && (cb[bi] & kOld) && !(cb[bi] & kRef) && op - cv > R;
+          anyfar = anyfar || (farb[bi] && cv + 128 > fenced);
+        }
+        if (__ballot(anyfar)) {
+          __threadfence_block();
+          fenced = flushed;
+        }
+#pragma unroll
+        for (uint32_t bi = 0; bi < NB; ++bi) {
+          const uint32_t c = cb[bi], cv = c & kVal;
+          outb[bi] = (c & kRef) ? 0u
+                                : (farb[bi] ? (uint32_t)dst[cv] : ((c & kOld) ? (uint32_t)ring[ridx(cv)] : (uint32_t)stage[cv]));
+        }
+#pragma unroll
+        for (uint32_t bi = 0; bi < NB; ++bi) {
+          if (bi * kLzThreads < T) {
+            const uint32_t x = bi * kLzThreads + lane;
+            const bool in = x < T;
+            uint32_t c = cb[bi];
+            bool done = !in || !(c & kRef);
+            while (__ballot(!done)) {
+              if (!done) {
+                const uint32_t t = code[c & kVal];
+                if (t & kRef) c = t;
+                else done = true;
+              }
+              lz_wave_sync();
+              if (in && (c & kRef)) code[x] = c;
+              lz_wave_sync();
+            }
+            cb[bi] = c;
+          }
+        }
+#pragma unroll
+        for (uint32_t bi = 0; bi < NB; ++bi) {
+          const uint32_t x = bi * kLzThreads + lane;
+          if (x < T && !(cb[bi] & kRef)) winb[x] = (uint8_t)outb[bi];
+        }
+        lz_wave_sync();
+#pragma unroll
+        for (uint32_t bi = 0; bi < NB; ++bi) {
+          const uint32_t x = bi * kLzThreads + lane;
+          if (x < T && (cb[bi] & kRef)) outb[bi] = winb[cb[bi] & kVal];
+        }
+      } else
 #pragma unroll
       for (uint32_t bi = 0; bi < NB; ++bi) {
         outb[bi] = 0;
@@ -2098,12 +2156,13 @@ __global__ __launch_bounds__(kLzThreads) void lz4_decompress_window_kernel(const
   }
 }
 
-// -1 (default): auto — the staged wave-per-chunk kernel (2) for small batches, lane groups of 4
-// (17) from 6144 chunks up, where enough chunks exist to fill the CUs 16 per wave
-// (profiles/r2_lz4.md: text 45 -> 63 GB/s at 8192 chunks, 54 -> 217 GB/s at 32768).
+// -1 (default): auto — the window-parallel kernel (23) below 24k chunks, lane groups of 4 (17)
+// from there up, where enough chunks exist to fill the CUs 16 per wave (profiles/r3_lz4_window.md:
+// at 4096 chunks 23 decodes text 121 / csv 139 GB/s vs 39 / 55 for the wave-per-chunk kernel 2;
+// at 32768 chunks 17 reaches 215 / 186).
 // 0: LDS window, 1: direct, 2: staged parse, 3: + LDS ring, 4-12: wave-synchronous, 13-18: groups.
 static int g_lz4_decode_variant = -1;
-constexpr int kLzGroupMinChunks = 6144;
+constexpr int kLzGroupMinChunks = 24576;
 
 void set_lz4_decode_variant(int v) { g_lz4_decode_variant = v; }
 
@@ -2111,7 +2170,7 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
                                  hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   int variant = g_lz4_decode_variant;
-  if (variant < 0) variant = n >= kLzGroupMinChunks ? 17 : 2;
+  if (variant < 0) variant = n >= kLzGroupMinChunks ? 17 : 23;
   if (variant == 0) {
     const unsigned grid = (unsigned)std::min(n, 4096);
     hipLaunchKernelGGL(lz4_decompress_kernel, dim3(grid), dim3(kLzThreads), kLzWindow, stream,
@@ -2176,7 +2235,8 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
       case 22: hipLaunchKernelGGL((lz4_decompress_window_kernel<16384, 1024, 512>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 23: hipLaunchKernelGGL((lz4_decompress_window_kernel<4096, 1024, 256, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
       case 24: hipLaunchKernelGGL((lz4_decompress_window_kernel<8192, 1024, 256, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
-      default: hipLaunchKernelGGL((lz4_decompress_window_kernel<4096, 1024, 512, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      case 25: hipLaunchKernelGGL((lz4_decompress_window_kernel<4096, 1024, 512, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
+      default: hipLaunchKernelGGL((lz4_decompress_window_kernel<4096, 1024, 256, true, true>), dim3(grid), dim3(kLzThreads), 0, stream, chunks, n, out_sizes); break;
     }
   }
   return hipGetLastError();

@@ -58,7 +58,7 @@ def test_crc32c_matches_host(gpu, variant):
     C.set_crc_variant(4)
 
 
-@pytest.mark.parametrize("variant", [-1] + list(range(26)))
+@pytest.mark.parametrize("variant", [-1] + list(range(27)))
 def test_lz4_device_roundtrip(gpu, variant):
     import torch
     C = lib()
@@ -106,7 +106,7 @@ def test_lz4_device_roundtrip(gpu, variant):
     C.set_lz4_decode_variant(-1)
 
 
-@pytest.mark.parametrize("variant", [-1, 2, 17, 19, 20, 21, 22, 23, 24, 25])
+@pytest.mark.parametrize("variant", [-1, 2, 17, 19, 20, 21, 22, 23, 24, 25, 26])
 def test_lz4_device_unaligned_and_text(gpu, variant):
     """Unaligned source/destination addresses, text/CSV-shaped streams (many short sequences with
     small offsets: the window kernels' reference chains), long zero runs and incompressible tails."""

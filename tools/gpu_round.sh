@@ -42,7 +42,7 @@ for s in $STEPS; do
       run rocprof_bench 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
       ;;
     lz4t) run lz4_tests 300 python -u -m pytest tests/test_kernels_gpu.py -k lz4 -x -v --timeout 120 --timeout-method thread ;;
-    lz4) run lz4_bench 600 python tools/lz4_bench.py --chunks 1024,4096,16384,32768 --variants "${LZ4_VARIANTS:-2,17,19,20,21,22}" --out "$OUT/lz4_bench.jsonl" ;;
+    lz4) run lz4_bench 600 python tools/lz4_bench.py --chunks 1024,4096,16384,32768 --variants="${LZ4_VARIANTS:-2,17,19,20,21,22}" --out "$OUT/lz4_bench.jsonl" ;;
     s3ingest)
       run ingest_s3native 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 2g --dram 6g --factor 2 --depths 1,3 --out "$OUT/ufs_ingest_s3native.jsonl"
       run ingest_s3requests 600 python tools/ufs_ingest_bench.py --ufs s3native --native-reader false --hbm 2g --dram 6g --factor 2 --depths 3 --out "$OUT/ufs_ingest_s3native.jsonl"
