@@ -733,6 +733,26 @@ PYBIND11_MODULE(_C, m) {
           py::gil_scoped_release rel;
           return crc32c_sw(reinterpret_cast<const void*>(ptr), n, crc);
         }, py::arg("ptr"), py::arg("n"), py::arg("crc") = 0);
+  // HDFS data-transfer checksums: one big-endian CRC32C per bytes_per_checksum chunk (the last
+  // chunk may be short), the layout a DataTransferProtocol packet carries before its data
+  m.def("crc32c_chunks", [](py::buffer data, uint32_t bpc) {
+          py::buffer_info bi = data.request();
+          const auto* p = static_cast<const uint8_t*>(bi.ptr);
+          const size_t n = static_cast<size_t>(bi.size) * bi.itemsize;
+          if (bpc == 0) throw StoreError(kErrInvalidArgument, "bytes_per_checksum must be > 0");
+          const size_t nc = (n + bpc - 1) / bpc;
+          std::string out(nc * 4, '\0');
+          {
+            py::gil_scoped_release rel;
+            for (size_t i = 0; i < nc; ++i) {
+              const size_t off = i * bpc;
+              const uint32_t c = crc32c_sw(p + off, std::min<size_t>(bpc, n - off), 0);
+              out[4 * i] = char(c >> 24); out[4 * i + 1] = char(c >> 16);
+              out[4 * i + 2] = char(c >> 8); out[4 * i + 3] = char(c);
+            }
+          }
+          return py::bytes(out);
+        }, py::arg("data"), py::arg("bytes_per_checksum") = 512);
   m.def("crc32c_combine", &crc32c_combine);
   m.def("crc32c_device", &crc32c_device, G(), py::arg("ptr"), py::arg("length"), py::arg("piece") = 0,
         py::arg("stream") = 0);

@@ -29,7 +29,7 @@ SCALARS = {
     "i32": F.TYPE_INT32, "i64": F.TYPE_INT64, "u32": F.TYPE_UINT32, "u64": F.TYPE_UINT64,
     "si32": F.TYPE_SINT32, "si64": F.TYPE_SINT64, "bool": F.TYPE_BOOL, "str": F.TYPE_STRING,
     "bytes": F.TYPE_BYTES, "f64": F.TYPE_DOUBLE, "f32": F.TYPE_FLOAT,
-    "fx32": F.TYPE_FIXED32, "fx64": F.TYPE_FIXED64,
+    "fx32": F.TYPE_FIXED32, "fx64": F.TYPE_FIXED64, "sfx32": F.TYPE_SFIXED32, "sfx64": F.TYPE_SFIXED64,
 }
 
 _FIELD = re.compile(

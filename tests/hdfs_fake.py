@@ -1,0 +1,472 @@
+"""A one-process mini HDFS (NameNode + DataNodes) serving the Hadoop wire protocols that
+``alluxio_amd.underfs.hadoop_rpc`` speaks: Hadoop IPC v9 ClientNamenodeProtocol calls and
+DataTransferProtocol READ_BLOCK / WRITE_BLOCK with CRC32C packets and pipeline forwarding.
+
+It is the test double for the HDFS UFS (the reference tests its HDFS UFS against MiniDFSCluster;
+no JVM here).  Semantics follow FSNamesystem where the UFS contract observes them: create with
+overwrite/createParent, FileAlreadyExistsException, mkdirs with createParent, non-recursive
+delete of a non-empty directory -> PathIsNotEmptyDirectoryException, rename returning false when
+the destination exists or the source is missing, paged getListing (``ls_limit`` entries a page).
+"""
+from __future__ import annotations
+
+import socket
+import socketserver
+import struct
+import threading
+import time
+
+from alluxio_amd.underfs import hadoop_rpc as H
+
+common, hdfs = H.common, H.hdfs
+
+
+class _Remote(Exception):
+    def __init__(self, cls, msg):
+        super().__init__(msg)
+        self.cls, self.msg = cls, msg
+
+
+def _fnf(p):
+    return _Remote("java.io.FileNotFoundException", f"File does not exist: {p}")
+
+
+class Node:
+    def __init__(self, is_dir, mode, owner, group, block_size=0, replication=0):
+        self.is_dir, self.mode, self.owner, self.group = is_dir, mode, owner, group
+        self.mtime = int(time.time() * 1000)
+        self.blocks: list = []          # ExtendedBlockProto (numBytes committed)
+        self.block_size, self.replication = block_size, replication
+        self.complete = is_dir
+        self.file_id = 0
+
+
+class MiniDfs:
+    def __init__(self, num_datanodes=1, ls_limit=1000, owner="hdfs", group="supergroup"):
+        self.lock = threading.RLock()
+        self.ns: dict[str, Node] = {"/": Node(True, 0o755, owner, group)}
+        self.ls_limit = ls_limit
+        self.next_block = 1 << 30
+        self.next_file_id = 16386
+        self.pool_id = "BP-1-127.0.0.1-1"
+        self.datanodes = [_DataNode(self, i) for i in range(num_datanodes)]
+        self.namenode = _Server(("127.0.0.1", 0), _NameNodeHandler)
+        self.namenode.dfs = self
+        self.port = self.namenode.server_address[1]
+        threading.Thread(target=self.namenode.serve_forever, daemon=True).start()
+        self.calls: list[str] = []
+
+    def stop(self):
+        self.namenode.shutdown()
+        self.namenode.server_close()
+        for d in self.datanodes:
+            d.stop()
+
+    # ---- namespace helpers ------------------------------------------------------------------
+    @staticmethod
+    def _norm(p):
+        p = "/" + p.strip("/")
+        return p
+
+    @staticmethod
+    def _parent(p):
+        return p.rsplit("/", 1)[0] or "/"
+
+    def _children(self, p):
+        pre = p.rstrip("/") + "/"
+        return sorted(k for k in self.ns if k.startswith(pre) and "/" not in k[len(pre):] and k != "/")
+
+    def _status(self, p, n: Node, name: bytes):
+        st = hdfs.HdfsFileStatusProto(fileType=H.FILE_IS_DIR if n.is_dir else H.FILE_IS_FILE, path=name,
+                                      length=0 if n.is_dir else sum(b.numBytes for b in n.blocks),
+                                      owner=n.owner, group=n.group, modification_time=n.mtime,
+                                      access_time=n.mtime, block_replication=n.replication,
+                                      blocksize=n.block_size, fileId=n.file_id,
+                                      childrenNum=len(self._children(p)) if n.is_dir else 0)
+        st.permission.perm = n.mode
+        return st
+
+    def _mkdirs(self, p, mode, owner):
+        parts = [x for x in p.split("/") if x]
+        cur = ""
+        for x in parts:
+            cur += "/" + x
+            n = self.ns.get(cur)
+            if n is None:
+                self.ns[cur] = Node(True, mode, owner, "supergroup")
+            elif not n.is_dir:
+                raise _Remote("org.apache.hadoop.fs.ParentNotDirectoryException", f"{cur} is not a directory")
+
+    def _located(self, eb, offset, dns):
+        lb = hdfs.LocatedBlockProto(offset=offset, corrupt=False)
+        lb.b.CopyFrom(eb)
+        lb.blockToken.CopyFrom(common.TokenProto(identifier=b"", password=b"", kind="", service=""))
+        for dn in dns:
+            lb.locs.add().CopyFrom(dn.info())
+        return lb
+
+    # ---- ClientProtocol -----------------------------------------------------------------------
+    def handle(self, method, req_bytes, user):
+        self.calls.append(method)
+        with self.lock:
+            fn = getattr(self, "rpc_" + method, None)
+            if fn is None:
+                raise _Remote("org.apache.hadoop.ipc.RpcNoSuchMethodException", f"Unknown method {method}")
+            return fn(req_bytes, user)
+
+    def rpc_getFileInfo(self, b, user):
+        r = hdfs.GetFileInfoRequestProto.FromString(b)
+        p = self._norm(r.src)
+        out = hdfs.GetFileInfoResponseProto()
+        n = self.ns.get(p)
+        if n is not None:
+            out.fs.CopyFrom(self._status(p, n, b""))
+        return out
+
+    def rpc_getListing(self, b, user):
+        r = hdfs.GetListingRequestProto.FromString(b)
+        p = self._norm(r.src)
+        out = hdfs.GetListingResponseProto()
+        n = self.ns.get(p)
+        if n is None:
+            return out
+        if not n.is_dir:
+            out.dirList.partialListing.add().CopyFrom(self._status(p, n, b""))
+            out.dirList.remainingEntries = 0
+            return out
+        names = [c.rsplit("/", 1)[1] for c in self._children(p)]
+        after = r.startAfter.decode()
+        names = [x for x in names if x > after]
+        page, rest = names[:self.ls_limit], names[self.ls_limit:]
+        for x in page:
+            c = p.rstrip("/") + "/" + x
+            out.dirList.partialListing.add().CopyFrom(self._status(c, self.ns[c], x.encode()))
+        out.dirList.remainingEntries = len(rest)
+        return out
+
+    def rpc_mkdirs(self, b, user):
+        r = hdfs.MkdirsRequestProto.FromString(b)
+        p = self._norm(r.src)
+        n = self.ns.get(p)
+        if n is not None:
+            if not n.is_dir:
+                raise _Remote("org.apache.hadoop.fs.FileAlreadyExistsException", f"{p} is a file")
+            return hdfs.MkdirsResponseProto(result=True)
+        par = self.ns.get(self._parent(p))
+        if par is None and not r.createParent:
+            raise _fnf(self._parent(p))
+        if par is not None and not par.is_dir:
+            raise _Remote("org.apache.hadoop.fs.ParentNotDirectoryException", f"{self._parent(p)}")
+        self._mkdirs(p, r.masked.perm, user)
+        return hdfs.MkdirsResponseProto(result=True)
+
+    def _subtree(self, p):
+        pre = p.rstrip("/") + "/"
+        return [k for k in self.ns if k == p or k.startswith(pre)]
+
+    def rpc_delete(self, b, user):
+        r = hdfs.DeleteRequestProto.FromString(b)
+        p = self._norm(r.src)
+        n = self.ns.get(p)
+        if n is None or p == "/":
+            return hdfs.DeleteResponseProto(result=False)
+        if n.is_dir and not r.recursive and self._children(p):
+            raise _Remote("org.apache.hadoop.fs.PathIsNotEmptyDirectoryException", f"{p} is non empty")
+        for k in self._subtree(p):
+            for eb in self.ns[k].blocks:
+                for dn in self.datanodes:
+                    dn.blocks.pop(eb.blockId, None)
+            del self.ns[k]
+        return hdfs.DeleteResponseProto(result=True)
+
+    def rpc_rename(self, b, user):
+        r = hdfs.RenameRequestProto.FromString(b)
+        src, dst = self._norm(r.src), self._norm(r.dst)
+        if src not in self.ns or dst in self.ns or self._parent(dst) not in self.ns \
+                or dst.startswith(src.rstrip("/") + "/"):
+            return hdfs.RenameResponseProto(result=False)
+        for k in sorted(self._subtree(src)):
+            self.ns[dst + k[len(src):]] = self.ns.pop(k)
+        return hdfs.RenameResponseProto(result=True)
+
+    def rpc_create(self, b, user):
+        r = hdfs.CreateRequestProto.FromString(b)
+        p = self._norm(r.src)
+        n = self.ns.get(p)
+        if n is not None:
+            if n.is_dir:
+                raise _Remote("org.apache.hadoop.fs.FileAlreadyExistsException", f"{p} already exists as a directory")
+            if not r.createFlag & H.CREATE_FLAG_OVERWRITE:
+                raise _Remote("org.apache.hadoop.fs.FileAlreadyExistsException", f"{p} for client already exists")
+        par = self.ns.get(self._parent(p))
+        if par is None:
+            if not r.createParent:
+                raise _fnf(self._parent(p))
+            self._mkdirs(self._parent(p), 0o755, user)
+        elif not par.is_dir:
+            raise _Remote("org.apache.hadoop.fs.ParentNotDirectoryException", self._parent(p))
+        node = Node(False, r.masked.perm, user, "supergroup", r.blockSize, r.replication)
+        node.file_id = self.next_file_id
+        self.next_file_id += 1
+        self.ns[p] = node
+        return hdfs.CreateResponseProto(fs=self._status(p, node, b""))
+
+    def _file(self, src, file_id):
+        p = self._norm(src)
+        n = self.ns.get(p)
+        if n is None or n.is_dir or (file_id and n.file_id != file_id):
+            raise _Remote("org.apache.hadoop.hdfs.server.namenode.LeaseExpiredException", f"No lease on {p}")
+        return n
+
+    def _commit(self, n, eb):
+        for i, x in enumerate(n.blocks):
+            if x.blockId == eb.blockId:
+                n.blocks[i].numBytes = eb.numBytes
+                return
+
+    def rpc_addBlock(self, b, user):
+        r = hdfs.AddBlockRequestProto.FromString(b)
+        n = self._file(r.src, r.fileId)
+        if r.HasField("previous"):
+            self._commit(n, r.previous)
+        eb = hdfs.ExtendedBlockProto(poolId=self.pool_id, blockId=self.next_block, generationStamp=1001, numBytes=0)
+        self.next_block += 1
+        offset = sum(x.numBytes for x in n.blocks)
+        n.blocks.append(eb)
+        k = max(1, min(n.replication or 1, len(self.datanodes)))
+        return hdfs.AddBlockResponseProto(block=self._located(eb, offset, self.datanodes[:k]))
+
+    def rpc_abandonBlock(self, b, user):
+        r = hdfs.AbandonBlockRequestProto.FromString(b)
+        n = self._file(r.src, r.fileId)
+        n.blocks = [x for x in n.blocks if x.blockId != r.b.blockId]
+        return hdfs.AbandonBlockResponseProto()
+
+    def rpc_complete(self, b, user):
+        r = hdfs.CompleteRequestProto.FromString(b)
+        n = self._file(r.src, r.fileId)
+        if r.HasField("last"):
+            self._commit(n, r.last)
+        for eb in n.blocks:                       # every replica must have reported the block
+            if any(dn.blocks.get(eb.blockId) is None or len(dn.blocks[eb.blockId]) != eb.numBytes
+                   for dn in self.datanodes[:max(1, min(n.replication or 1, len(self.datanodes)))]):
+                return hdfs.CompleteResponseProto(result=False)
+        n.complete = True
+        n.mtime = int(time.time() * 1000)
+        return hdfs.CompleteResponseProto(result=True)
+
+    def rpc_getBlockLocations(self, b, user):
+        r = hdfs.GetBlockLocationsRequestProto.FromString(b)
+        p = self._norm(r.src)
+        n = self.ns.get(p)
+        if n is None or n.is_dir:
+            raise _fnf(p)
+        out = hdfs.GetBlockLocationsResponseProto()
+        lbs = out.locations
+        lbs.fileLength = sum(x.numBytes for x in n.blocks)
+        lbs.underConstruction = not n.complete
+        lbs.isLastBlockComplete = n.complete
+        off = 0
+        for eb in n.blocks:
+            if off + eb.numBytes > r.offset and off < r.offset + r.length:
+                dns = [dn for dn in self.datanodes if eb.blockId in dn.blocks]
+                lbs.blocks.add().CopyFrom(self._located(eb, off, dns))
+            off += eb.numBytes
+        return out
+
+    def rpc_setPermission(self, b, user):
+        r = hdfs.SetPermissionRequestProto.FromString(b)
+        n = self.ns.get(self._norm(r.src))
+        if n is None:
+            raise _fnf(r.src)
+        n.mode = r.permission.perm
+        return hdfs.SetPermissionResponseProto()
+
+    def rpc_setOwner(self, b, user):
+        r = hdfs.SetOwnerRequestProto.FromString(b)
+        n = self.ns.get(self._norm(r.src))
+        if n is None:
+            raise _fnf(r.src)
+        if r.HasField("username"):
+            n.owner = r.username
+        if r.HasField("groupname"):
+            n.group = r.groupname
+        return hdfs.SetOwnerResponseProto()
+
+    def rpc_getFsStats(self, b, user):
+        used = sum(len(v) for dn in self.datanodes for v in dn.blocks.values())
+        return hdfs.GetFsStatsResponseProto(capacity=1 << 40, used=used, remaining=(1 << 40) - used,
+                                            under_replicated=0, corrupt_blocks=0, missing_blocks=0)
+
+    def rpc_renewLease(self, b, user):
+        return hdfs.RenewLeaseResponseProto()
+
+
+class _Server(socketserver.ThreadingTCPServer):
+    daemon_threads = True
+    allow_reuse_address = True
+
+
+def _send_frame(sock, *msgs):
+    payload = b"".join(H.delimited(m) for m in msgs)
+    sock.sendall(struct.pack(">I", len(payload)) + payload)
+
+
+class _NameNodeHandler(socketserver.BaseRequestHandler):
+    def handle(self):
+        s, dfs = self.request, self.server.dfs
+        try:
+            pre = bytes(H.recv_exact(s, 7))
+            if pre[:4] != b"hrpc" or pre[4] != H.IPC_VERSION:
+                return
+            user = "hdfs"
+            while True:
+                (n,) = struct.unpack(">I", bytes(H.recv_exact(s, 4)))
+                frame = H.recv_exact(s, n)
+                rh, pos = H.parse_delimited(frame, 0, common.RpcRequestHeaderProto)
+                if rh.callId == H.CONNECTION_CONTEXT_CALL_ID:
+                    ctx, _ = H.parse_delimited(frame, pos, common.IpcConnectionContextProto)
+                    user = ctx.userInfo.effectiveUser or user
+                    continue
+                req_hdr, pos = H.parse_delimited(frame, pos, common.RequestHeaderProto)
+                # the request body is the rest of the frame, varint-delimited
+                shift = ln = 0
+                while True:
+                    c = frame[pos]
+                    pos += 1
+                    ln |= (c & 0x7F) << shift
+                    if not c & 0x80:
+                        break
+                    shift += 7
+                body = bytes(frame[pos:pos + ln])
+                resp_hdr = common.RpcResponseHeaderProto(callId=rh.callId, status=0, serverIpcVersionNum=9,
+                                                         clientId=rh.clientId)
+                try:
+                    out = dfs.handle(req_hdr.methodName, body, user)
+                    _send_frame(s, resp_hdr, out)
+                except _Remote as e:
+                    resp_hdr.status = 1
+                    resp_hdr.exceptionClassName, resp_hdr.errorMsg = e.cls, e.msg
+                    _send_frame(s, resp_hdr)
+        except (ConnectionError, OSError):
+            return
+
+
+class _DataNode:
+    def __init__(self, dfs: MiniDfs, idx: int):
+        self.dfs, self.idx = dfs, idx
+        self.blocks: dict[int, bytes] = {}
+        self.fail_reads = False
+        self.corrupt_reads = False
+        self.server = _Server(("127.0.0.1", 0), _DataNodeHandler)
+        self.server.dn = self
+        self.port = self.server.server_address[1]
+        threading.Thread(target=self.server.serve_forever, daemon=True).start()
+
+    def info(self):
+        d = hdfs.DatanodeInfoProto(capacity=1 << 40)
+        d.id.CopyFrom(hdfs.DatanodeIDProto(ipAddr="127.0.0.1", hostName="localhost",
+                                           datanodeUuid=f"dn-{self.idx}", xferPort=self.port, infoPort=0,
+                                           ipcPort=0))
+        return d
+
+    def stop(self):
+        self.server.shutdown()
+        self.server.server_close()
+
+
+class _DataNodeHandler(socketserver.BaseRequestHandler):
+    def handle(self):
+        s, dn = self.request, self.server.dn
+        try:
+            ver, op = struct.unpack(">HB", bytes(H.recv_exact(s, 3)))
+            if ver != H.DATA_TRANSFER_VERSION:
+                return
+            if op == H.OP_READ_BLOCK:
+                self._read(s, dn, H.recv_delimited(s, hdfs.OpReadBlockProto))
+            elif op == H.OP_WRITE_BLOCK:
+                self._write(s, dn, H.recv_delimited(s, hdfs.OpWriteBlockProto))
+        except (ConnectionError, OSError):
+            return
+
+    @staticmethod
+    def _read(s, dn, op):
+        bid = op.header.baseHeader.block.blockId
+        data = dn.blocks.get(bid)
+        if data is None or dn.fail_reads or op.offset + op.len > len(data):
+            s.sendall(H.delimited(hdfs.BlockOpResponseProto(status=H.ST_ERROR, message=f"block {bid} unavailable")))
+            return
+        bpc = H.BYTES_PER_CHECKSUM
+        start = op.offset - op.offset % bpc           # chunk-aligned start, as BlockSender does
+        end = op.offset + op.len
+        resp = hdfs.BlockOpResponseProto(status=H.ST_SUCCESS)
+        resp.readOpChecksumInfo.checksum.type = H.CHECKSUM_CRC32C
+        resp.readOpChecksumInfo.checksum.bytesPerChecksum = bpc
+        resp.readOpChecksumInfo.chunkOffset = start
+        s.sendall(H.delimited(resp))
+        seq, off = 0, start
+        while off < end:
+            n = min(H.PACKET_DATA, end - off)
+            if dn.corrupt_reads:        # a bit flipped on disk after the checksums were stored
+                piece = data[off:off + n]
+                sums = H._crc_chunks(piece, bpc)
+                hdr = hdfs.PacketHeaderProto(offsetInBlock=off, seqno=seq, lastPacketInBlock=False,
+                                             dataLen=n).SerializeToString()
+                bad = bytes([piece[0] ^ 1]) + piece[1:]
+                s.sendall(struct.pack(">IH", 4 + len(sums) + n, len(hdr)) + hdr + sums + bad)
+            else:
+                H.write_packet(s, off, seq, data[off:off + n], False)
+            off += n
+            seq += 1
+        H.write_packet(s, off, seq, b"", True)
+        try:
+            H.recv_delimited(s, hdfs.ClientReadStatusProto)
+        except (ConnectionError, OSError):
+            pass
+
+    @staticmethod
+    def _write(s, dn, op):
+        bid = op.header.baseHeader.block.blockId
+        downstream = None
+        if len(op.targets):                            # forward to the next DataNode in the pipeline
+            nxt = op.targets[0]
+            downstream = socket.create_connection((nxt.id.ipAddr, nxt.id.xferPort), timeout=30)
+            fwd = hdfs.OpWriteBlockProto()
+            fwd.CopyFrom(op)
+            del fwd.targets[0]
+            downstream.sendall(struct.pack(">HB", H.DATA_TRANSFER_VERSION, H.OP_WRITE_BLOCK) + H.delimited(fwd))
+            r = H.recv_delimited(downstream, hdfs.BlockOpResponseProto)
+            if r.status != H.ST_SUCCESS:
+                s.sendall(H.delimited(hdfs.BlockOpResponseProto(status=H.ST_ERROR, firstBadLink=nxt.id.ipAddr)))
+                return
+        s.sendall(H.delimited(hdfs.BlockOpResponseProto(status=H.ST_SUCCESS)))
+        buf = bytearray()
+        bpc = op.requestedChecksum.bytesPerChecksum or H.BYTES_PER_CHECKSUM
+        while True:
+            plen, hlen = struct.unpack(">IH", bytes(H.recv_exact(s, 6)))
+            hraw = bytes(H.recv_exact(s, hlen))
+            body = bytes(H.recv_exact(s, plen - 4))
+            hdr = hdfs.PacketHeaderProto.FromString(hraw)
+            data = body[len(body) - hdr.dataLen:]
+            sums = body[:len(body) - hdr.dataLen]
+            status = H.ST_SUCCESS
+            if hdr.dataLen and H._crc_chunks(data, bpc) != sums:
+                status = H.ST_ERROR_CHECKSUM
+            if hdr.offsetInBlock != len(buf):
+                status = H.ST_ERROR
+            if downstream is not None:
+                downstream.sendall(struct.pack(">IH", plen, hlen) + hraw + body)
+            replies = [status]
+            if downstream is not None:
+                dack = H.recv_delimited(downstream, hdfs.PipelineAckProto)
+                replies += list(dack.reply)
+            buf += data
+            ack = hdfs.PipelineAckProto(seqno=hdr.seqno)
+            ack.reply.extend(replies)
+            s.sendall(H.delimited(ack))
+            if hdr.lastPacketInBlock or status != H.ST_SUCCESS:
+                break
+        if downstream is not None:
+            downstream.close()
+        if status == H.ST_SUCCESS:
+            dn.blocks[bid] = bytes(buf)               # finalized replica (blockReceived)
