@@ -133,6 +133,7 @@ class FileSystemMaster(Journaled):
         self.umask = int(conf.get("alluxio.security.authorization.permission.umask"), 8) if conf else 0o022
         self.default_block_size = conf.get_bytes("alluxio.user.block.size.bytes.default") if conf else 64 << 20
         self.sync_points: dict[str, int] = {}
+        self.active_sync_txids: dict[int, int] = {}   # mount id -> last UFS edit txid synced
         self.ufs_modes: dict[str, UfsMode] = {}
         self.persist_handler = None   # callable(file_id, path) -> job id; set by the master process
         self.persist_jobs: dict[int, dict] = {}
@@ -162,6 +163,7 @@ class FileSystemMaster(Journaled):
         self.tree.reset()
         self.mount_table.reset()
         self.sync_points.clear()
+        self.active_sync_txids.clear()
         self.ufs_modes.clear()
 
     def process_journal_entry(self, e) -> bool:
@@ -195,6 +197,7 @@ class FileSystemMaster(Journaled):
             self.sync_points.pop(e.remove_sync_point.syncpoint_path, None)
             return True
         if e.HasField("active_sync_tx_id"):
+            self.active_sync_txids[e.active_sync_tx_id.mount_id] = e.active_sync_tx_id.tx_id
             return True
         if e.HasField("update_ufs_mode"):
             u = e.update_ufs_mode
@@ -217,6 +220,8 @@ class FileSystemMaster(Journaled):
                     queue.extend(self.tree.list_children(n))
         for p, mid in self.sync_points.items():
             yield pb.journal.JournalEntry(add_sync_point=pb.journal.AddSyncPointEntry(syncpoint_path=p, mount_id=mid))
+        for mid, tx in self.active_sync_txids.items():
+            yield pb.journal.JournalEntry(active_sync_tx_id=pb.journal.ActiveSyncTxIdEntry(mount_id=mid, tx_id=tx))
         for p, mode in self.ufs_modes.items():
             yield pb.journal.JournalEntry(update_ufs_mode=pb.journal.UpdateUfsModeEntry(ufsPath=p, ufsMode=int(mode)))
 
@@ -260,6 +265,8 @@ class FileSystemMaster(Journaled):
                      for p_, m in self.ufs_modes.items()]
             syncs = [pb.journal.JournalEntry(add_sync_point=pb.journal.AddSyncPointEntry(syncpoint_path=p_, mount_id=mid))
                      for p_, mid in self.sync_points.items()]
+            syncs += [pb.journal.JournalEntry(active_sync_tx_id=pb.journal.ActiveSyncTxIdEntry(mount_id=mid, tx_id=tx))
+                      for mid, tx in self.active_sync_txids.items()]
         return ck.compound([
             ("INODE_TREE", inode_tree),
             ("INODE_DIRECTORY_ID_GENERATOR", ck.journal_entries([gen])),
@@ -1673,11 +1680,57 @@ class FileSystemMaster(Journaled):
                 syncpoint_path=path, mount_id=self.sync_points.get(path, 0))))
 
     def active_sync_heartbeat(self) -> None:
-        for p in list(self.sync_points):
+        """One active-sync round (ActiveSyncManager + ActiveSyncer).  UFSes with a change feed
+        (HDFS inotify, underfs/hdfs/.../activesync/SupportedHdfsActiveSyncProvider.java:164-223)
+        sync only the paths the edits since the journaled txid touched — each changed path and its
+        parent directory — and then journal the new txid (ActiveSyncTxIdEntry); the first round of a
+        mount syncs its sync points fully and starts the feed at the current txid.  Other UFSes are
+        re-synced recursively every round."""
+        by_mount: dict[int, list[str]] = {}
+        for p, mid in list(self.sync_points.items()):
+            by_mount.setdefault(mid, []).append(p)
+        for mid, points in by_mount.items():
             try:
-                self.sync_metadata(p, recursive=True)
+                ufs = self._resolve_ufs(points[0]).ufs
+                if not ufs.supports_active_sync():
+                    for p in points:
+                        self.sync_metadata(p, recursive=True)
+                    continue
+                txid = self.active_sync_txids.get(mid)
+                if txid is None:
+                    _, cur = ufs.active_sync_changes(-1)
+                    for p in points:
+                        self.sync_metadata(p, recursive=True)
+                    self._journal_active_txid(mid, cur)
+                    continue
+                changed, last = ufs.active_sync_changes(txid)
+                self._count("Master.ActiveSyncEvents", len(changed))
+                targets: set[str] = set()
+                for uri in changed:
+                    ap = self.mount_table.reverse_resolve(uri)
+                    if ap is None:
+                        continue
+                    for p in points:
+                        if ap == p or ap.startswith(p.rstrip("/") + "/"):
+                            targets.add(ap)
+                            parent = ap.rsplit("/", 1)[0] or "/"
+                            if parent == p or parent.startswith(p.rstrip("/") + "/"):
+                                targets.add(parent)
+                # shallow paths first: a directory sync may already cover its children
+                for ap in sorted(targets, key=lambda x: (x.count("/"), x)):
+                    try:
+                        self.sync_metadata(ap, recursive=True)
+                    except Exception:  # noqa: BLE001  (the path may be gone again already)
+                        LOG.debug("active sync of changed path %s", ap, exc_info=True)
+                if last != txid:
+                    self._journal_active_txid(mid, last)
             except Exception:  # noqa: BLE001
-                LOG.exception("active sync of %s failed", p)
+                LOG.exception("active sync of mount %d (%s) failed", mid, points)
+
+    def _journal_active_txid(self, mount_id: int, txid: int) -> None:
+        with RpcContext(self) as rpc:
+            self._apply(rpc, pb.journal.JournalEntry(active_sync_tx_id=pb.journal.ActiveSyncTxIdEntry(
+                mount_id=mount_id, tx_id=txid)))
 
     # ------------------------------------------------------------------------------------------
     # persistence

@@ -285,6 +285,11 @@ class UnderFileSystem(abc.ABC):
     def supports_active_sync(self) -> bool:
         return False
 
+    def active_sync_changes(self, since_txid: int):
+        """UFS change feed for active sync: (changed URIs, new txid).  Only UFSes whose
+        ``supports_active_sync`` is true implement it (HDFS inotify)."""
+        raise NotImplementedError
+
     def set_owner(self, path: str, owner: str, group: str) -> None:
         pass
 

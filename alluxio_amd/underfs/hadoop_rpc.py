@@ -95,6 +95,26 @@ msg GetFsStatsResponseProto capacity=1:u64! used=2:u64! remaining=3:u64! under_r
     corrupt_blocks=5:u64! missing_blocks=6:u64!
 msg RenewLeaseRequestProto clientName=1:str!
 msg RenewLeaseResponseProto
+msg GetCurrentEditLogTxidRequestProto
+msg GetCurrentEditLogTxidResponseProto txid=1:i64!
+msg GetEditsFromTxidRequestProto txid=1:i64!
+msg GetEditsFromTxidResponseProto eventsList=1:EventsListProto!
+
+# inotify.proto (package hadoop.hdfs): the edit-log event stream DFSInotifyEventInputStream polls
+enum EventType EVENT_CREATE=0 EVENT_CLOSE=1 EVENT_APPEND=2 EVENT_RENAME=3 EVENT_METADATA=4 EVENT_UNLINK=5
+    EVENT_TRUNCATE=6
+enum INodeType I_TYPE_FILE=0 I_TYPE_DIRECTORY=1 I_TYPE_SYMLINK=2
+msg EventProto type=1:EventType! contents=2:bytes!
+msg EventBatchProto txid=1:i64! events=2:EventProto*
+msg EventsListProto events=1:EventProto* firstTxid=2:i64! lastTxid=3:i64! syncTxid=4:i64! batch=5:EventBatchProto*
+msg CreateEventProto type=1:INodeType! path=2:str! ctime=3:i64! ownerName=4:str! groupName=5:str!
+    perms=6:FsPermissionProto! replication=7:i32 symlinkTarget=8:str overwrite=9:bool defaultBlockSize=10:i64@0
+msg CloseEventProto path=1:str! fileSize=2:i64! timestamp=3:i64!
+msg AppendEventProto path=1:str! newBlock=2:bool@false
+msg RenameEventProto srcPath=1:str! destPath=2:str! timestamp=3:i64!
+msg MetadataUpdateEventProto path=1:str! type=2:i32!
+msg UnlinkEventProto path=1:str! timestamp=2:i64!
+msg TruncateEventProto path=1:str! fileSize=2:i64! timestamp=3:i64!
 
 enum ChecksumTypeProto CHECKSUM_NULL=0 CHECKSUM_CRC32=1 CHECKSUM_CRC32C=2
 msg ChecksumProto type=1:ChecksumTypeProto! bytesPerChecksum=2:u32!
@@ -392,6 +412,40 @@ class NameNodeClient:
 
     def get_fs_stats(self):
         return self.call("getFsStats", hdfs.GetFsStatusRequestProto(), hdfs.GetFsStatsResponseProto)
+
+    # -- inotify (HdfsAdmin.getInotifyEventStream) ------------------------------------------------
+    def current_edit_txid(self) -> int:
+        return self.call("getCurrentEditLogTxid", hdfs.GetCurrentEditLogTxidRequestProto(),
+                         hdfs.GetCurrentEditLogTxidResponseProto).txid
+
+    def edits_since(self, txid: int, max_batches: int = 100_000):
+        """Changed paths of every edit after ``txid``: returns ([(txid, [path, ...]), ...], last_txid).
+        A RENAME contributes its source and destination (SupportedHdfsActiveSyncProvider.processEvent)."""
+        out, last = [], txid
+        while len(out) < max_batches:
+            r = self.call("getEditsFromTxid", hdfs.GetEditsFromTxidRequestProto(txid=last + 1),
+                          hdfs.GetEditsFromTxidResponseProto).eventsList
+            if not len(r.batch):
+                break
+            for b in r.batch:
+                paths = []
+                for ev in b.events:
+                    cls = _EVENT_CLASSES.get(ev.type)
+                    if cls is None:
+                        continue
+                    e = cls.FromString(ev.contents)
+                    if ev.type == 3:
+                        paths += [e.srcPath, e.destPath]
+                    else:
+                        paths.append(e.path)
+                out.append((b.txid, paths))
+                last = max(last, b.txid)
+        return out, last
+
+
+_EVENT_CLASSES = {0: hdfs.CreateEventProto, 1: hdfs.CloseEventProto, 2: hdfs.AppendEventProto,
+                  3: hdfs.RenameEventProto, 4: hdfs.MetadataUpdateEventProto, 5: hdfs.UnlinkEventProto,
+                  6: hdfs.TruncateEventProto}
 
 
 # ---- DataNode data transfer ---------------------------------------------------------------------

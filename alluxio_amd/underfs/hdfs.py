@@ -306,6 +306,19 @@ class HdfsUnderFileSystem(UnderFileSystem):
         return {SpaceType.SPACE_TOTAL: s.capacity, SpaceType.SPACE_USED: s.used,
                 SpaceType.SPACE_FREE: s.remaining}.get(space_type, s.capacity)
 
+    # ---- active sync (SupportedHdfsActiveSyncProvider over the NameNode's inotify stream) --------
+    def supports_active_sync(self) -> bool:
+        return True
+
+    def active_sync_changes(self, since_txid: int):
+        """(changed UFS URIs, new txid) for the edits after ``since_txid``; a negative txid starts
+        the stream at the NameNode's current edit (nothing to report yet)."""
+        if since_txid < 0:
+            return [], self._rpc(self.nn.current_edit_txid)
+        batches, last = self._rpc(self.nn.edits_since, since_txid)
+        base = f"hdfs://{self.host}:{self.port}"
+        return [base + p for _, paths in batches for p in paths], last
+
     def is_seekable(self) -> bool:
         return True
 

@@ -55,6 +55,12 @@ class MiniDfs:
         self.port = self.namenode.server_address[1]
         threading.Thread(target=self.namenode.serve_forever, daemon=True).start()
         self.calls: list[str] = []
+        self.edits: list = []           # inotify: EventBatchProto per edit, txid = index + 1
+
+    def _event(self, etype, msg):
+        b = hdfs.EventBatchProto(txid=len(self.edits) + 1)
+        b.events.add(type=etype, contents=msg.SerializeToString())
+        self.edits.append(b)
 
     def stop(self):
         self.namenode.shutdown()
@@ -158,6 +164,8 @@ class MiniDfs:
         if par is not None and not par.is_dir:
             raise _Remote("org.apache.hadoop.fs.ParentNotDirectoryException", f"{self._parent(p)}")
         self._mkdirs(p, r.masked.perm, user)
+        self._event(0, hdfs.CreateEventProto(type=1, path=p, ctime=0, ownerName=user, groupName="supergroup",
+                                             perms=r.masked))
         return hdfs.MkdirsResponseProto(result=True)
 
     def _subtree(self, p):
@@ -177,6 +185,7 @@ class MiniDfs:
                 for dn in self.datanodes:
                     dn.blocks.pop(eb.blockId, None)
             del self.ns[k]
+        self._event(5, hdfs.UnlinkEventProto(path=p, timestamp=0))
         return hdfs.DeleteResponseProto(result=True)
 
     def rpc_rename(self, b, user):
@@ -187,6 +196,7 @@ class MiniDfs:
             return hdfs.RenameResponseProto(result=False)
         for k in sorted(self._subtree(src)):
             self.ns[dst + k[len(src):]] = self.ns.pop(k)
+        self._event(3, hdfs.RenameEventProto(srcPath=src, destPath=dst, timestamp=0))
         return hdfs.RenameResponseProto(result=True)
 
     def rpc_create(self, b, user):
@@ -209,6 +219,8 @@ class MiniDfs:
         node.file_id = self.next_file_id
         self.next_file_id += 1
         self.ns[p] = node
+        self._event(0, hdfs.CreateEventProto(type=0, path=p, ctime=0, ownerName=user, groupName="supergroup",
+                                             perms=r.masked, overwrite=bool(r.createFlag & 2)))
         return hdfs.CreateResponseProto(fs=self._status(p, node, b""))
 
     def _file(self, src, file_id):
@@ -253,6 +265,8 @@ class MiniDfs:
                 return hdfs.CompleteResponseProto(result=False)
         n.complete = True
         n.mtime = int(time.time() * 1000)
+        self._event(1, hdfs.CloseEventProto(path=self._norm(r.src), fileSize=sum(x.numBytes for x in n.blocks),
+                                            timestamp=n.mtime))
         return hdfs.CompleteResponseProto(result=True)
 
     def rpc_getBlockLocations(self, b, user):
@@ -280,6 +294,7 @@ class MiniDfs:
         if n is None:
             raise _fnf(r.src)
         n.mode = r.permission.perm
+        self._event(4, hdfs.MetadataUpdateEventProto(path=self._norm(r.src), type=2))
         return hdfs.SetPermissionResponseProto()
 
     def rpc_setOwner(self, b, user):
@@ -297,6 +312,20 @@ class MiniDfs:
         used = sum(len(v) for dn in self.datanodes for v in dn.blocks.values())
         return hdfs.GetFsStatsResponseProto(capacity=1 << 40, used=used, remaining=(1 << 40) - used,
                                             under_replicated=0, corrupt_blocks=0, missing_blocks=0)
+
+    def rpc_getCurrentEditLogTxid(self, b, user):
+        return hdfs.GetCurrentEditLogTxidResponseProto(txid=len(self.edits))
+
+    def rpc_getEditsFromTxid(self, b, user):
+        r = hdfs.GetEditsFromTxidRequestProto.FromString(b)
+        out = hdfs.GetEditsFromTxidResponseProto()
+        el = out.eventsList
+        batches = self.edits[max(0, r.txid - 1):max(0, r.txid - 1) + 50]   # a bounded page per call
+        el.batch.extend(batches)
+        el.firstTxid = batches[0].txid if batches else r.txid
+        el.lastTxid = batches[-1].txid if batches else r.txid - 1
+        el.syncTxid = len(self.edits)
+        return out
 
     def rpc_renewLease(self, b, user):
         return hdfs.RenewLeaseResponseProto()

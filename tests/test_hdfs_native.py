@@ -182,3 +182,42 @@ def test_hdfs_mount_through_cluster(dfs, tmp_path):
         assert fs.read_file("/h/new.bin") == data
         assert sorted(s.name for s in fs.list_status("/h")) == ["new.bin", "pre.bin"]
         fs.unmount("/h")
+
+
+def test_active_sync_follows_inotify(dfs, tmp_path):
+    """startSync on an HDFS mount: the heartbeat follows the NameNode's edit stream (getEditsFromTxid)
+    and re-syncs only the touched paths; the txid is journaled (ActiveSyncTxIdEntry)."""
+    from alluxio_amd.minicluster import LocalAlluxioCluster
+    ufs = _ufs(dfs)
+    ufs.mkdirs("/w/a")
+    ufs.mkdirs("/w/b")
+    with ufs.create("/w/a/f1") as f:
+        f.write(b"1")
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"},
+                             work_dir=str(tmp_path / "c")) as c:
+        fs = c.client()
+        fs.mount("/h", f"hdfs://127.0.0.1:{dfs.port}/w", properties={"dfs.blocksize": "256k"})
+        m = c.master.fs_master
+        m.start_sync("/h/a")
+        m.active_sync_heartbeat()                       # first round: full sync, feed starts now
+        mid = m.sync_points["/h/a"]
+        tx0 = m.active_sync_txids[mid]
+        assert tx0 == len(dfs.edits)
+        with ufs.create("/w/a/f2") as f:
+            f.write(b"22")
+        ufs.rename_file("/w/a/f1", "/w/a/f1r")
+        with ufs.create("/w/b/outside") as f:           # not under the sync point: ignored
+            f.write(b"x")
+        before = dfs.calls.count("getListing")
+        m.active_sync_heartbeat()
+        assert m.active_sync_txids[mid] == len(dfs.edits) > tx0
+        assert dfs.calls.count("getListing") > before
+        names = sorted(s.name for s in fs.list_status("/h/a", load_metadata="NEVER"))
+        assert names == ["f1r", "f2"]
+        assert fs.read_file("/h/a/f2") == b"22"
+        ents = list(m.journal_entries())
+        assert any(e.HasField("active_sync_tx_id") and e.active_sync_tx_id.tx_id == len(dfs.edits) for e in ents)
+        ufs.delete_file("/w/a/f2")
+        m.active_sync_heartbeat()
+        assert sorted(s.name for s in fs.list_status("/h/a", load_metadata="NEVER")) == ["f1r"]
+        fs.unmount("/h")
