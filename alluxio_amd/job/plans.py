@@ -193,6 +193,8 @@ class LoadDefinition(PlanDefinition):
             raise ex.FailedPreconditionException("no job worker available for load")
         if len(usable) > 1 and (cfg.replication < 0 or cfg.replication >= len(usable)):
             return self._collective_plan(statuses, usable)
+        if len(usable) > 2 and cfg.replication > 1:
+            return self._collective_plan(statuses, usable, copies=cfg.replication)
         assign: dict[int, list] = {}
         for st in statuses:
             for fbi in st.info.fileBlockInfos:
@@ -208,13 +210,17 @@ class LoadDefinition(PlanDefinition):
         return [(by_id[w], blocks) for w, blocks in assign.items()]
 
     @staticmethod
-    def _collective_plan(statuses, usable):
+    def _collective_plan(statuses, usable, copies: int | None = None):
         """``distributedLoad --replication`` >= the worker count (every worker gets every block):
         each block gets one owner -- a worker already caching it, else a worker that loads it from
         the UFS (round-robin) -- and then all workers exchange the blocks with RCCL all-gathers
         over the node's transfer plane (TransferPlane.replicate_all: every xGMI link busy at
         once) instead of N-1 point-to-point copies per block.  Every worker receives the same
-        block list, in the same order: the collective's call sequence is identical on all ranks."""
+        block list, in the same order: the collective's call sequence is identical on all ranks.
+
+        With ``copies`` < the worker count, blocks already on ``copies`` workers are left out and
+        the rest go around the ring of participants with RCCL send/recv
+        (TransferPlane.replicate_ring): the owner and its ``copies - 1`` successors hold each block."""
         keys = {jw.id: f"{jw.address.host}:{jw.block_worker_port}" for jw in usable}
         usable_keys = set(keys.values())
         blocks, loads, rr, complete = [], {jw.id: [] for jw in usable}, 0, True
@@ -223,7 +229,9 @@ class LoadDefinition(PlanDefinition):
                 bi = fbi.blockInfo
                 holders = [f"{l.workerAddress.host}:{l.workerAddress.rpcPort}" for l in bi.locations]
                 held = [h for h in holders if h in usable_keys]
-                complete &= set(held) >= usable_keys
+                if copies is not None and len(held) >= copies:
+                    continue
+                complete &= copies is None and set(held) >= usable_keys
                 if held:
                     owner = held[0]
                 else:
@@ -235,8 +243,10 @@ class LoadDefinition(PlanDefinition):
         if complete:
             return []
         participants = sorted(usable_keys)
-        return [(jw, {"collective": True, "participants": participants, "blocks": blocks, "load": loads[jw.id]})
-                for jw in usable]
+        if not blocks:
+            return []
+        return [(jw, {"collective": True, "participants": participants, "blocks": blocks, "load": loads[jw.id],
+                      "copies": copies}) for jw in usable]
 
     def _run_collective(self, args, ctx) -> int:
         w = ctx.worker
@@ -248,13 +258,20 @@ class LoadDefinition(PlanDefinition):
             # the decision depends only on the plane membership every participant shares, so
             # either all participants enter the collective or none does
             todo = [(bid, n, plane.addr_to_rank[owner]) for _, bid, n, owner, _ in args["blocks"]]
+            if args.get("copies"):
+                return loaded + plane.replicate_ring(todo, args["copies"])
             return loaded + plane.replicate_all(todo)
         # no common transfer plane: pull what was cached somewhere, load the rest from the UFS
         from ..worker.remote import remote_block_fetcher
         rest = []
+        parts, copies = list(args["participants"]), args.get("copies")
+        from ..parallel.transfer import _addr_key
+        me = parts.index(_addr_key(w.address)) if _addr_key(w.address) in parts else None
         for path, bid, n, owner, held in args["blocks"]:
             if w.has_block(bid):
                 continue
+            if copies and me is not None and (me - parts.index(owner)) % len(parts) >= copies:
+                continue                      # not one of this block's ring positions
             if held:
                 host, port = owner.rsplit(":", 1)
                 remote_block_fetcher(w, host, int(port), n)(bid)
@@ -284,9 +301,14 @@ class LoadDefinition(PlanDefinition):
                 continue
             locs = st.info.fileBlockInfos[idx].blockInfo.locations
             if ctx.worker is not None and locs:
-                from ..worker.remote import remote_block_fetcher
                 src = locs[0].workerAddress
-                remote_block_fetcher(ctx.worker, src.host, src.rpcPort, opts.block_size)(block_id)
+                plane = getattr(ctx.worker, "transfer_plane", None)
+                reach = [l.workerAddress for l in locs if plane is not None and plane.can_reach(l.workerAddress)]
+                if reach:               # a peer on this node: pull over xGMI (gRPC fallback inside)
+                    plane.pull_block(block_id, reach[0], opts.block_size)
+                else:
+                    from ..worker.remote import remote_block_fetcher
+                    remote_block_fetcher(ctx.worker, src.host, src.rpcPort, opts.block_size)(block_id)
                 loaded += opts.block_size
             elif ctx.worker is not None:
                 from_ufs.append((block_id, opts))

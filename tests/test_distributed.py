@@ -250,20 +250,21 @@ jc = JobClient(fs.ctx.master_channel())
 while len(jc.worker_health()) < world and time.time() < deadline:
     time.sleep(0.05)
 if rank == 0:
-    status, result, err = jc.run_and_wait(LoadConfig(path="/dl", replication=-1), timeout=120)
+    status, result, err = jc.run_and_wait(LoadConfig(path="/dl", replication=%(replication)d), timeout=120)
     open(work + "/job.json.tmp", "w").write(json.dumps([status, result, err]))
     os.replace(work + "/job.json.tmp", work + "/job.json")      # readers never see a partial file
 while not os.path.exists(work + "/job.json"):
     time.sleep(0.05)
 status, result, err = json.load(open(work + "/job.json"))
 blocks = []
-for p in ("/dl/cached", "/dl/ufs"):
-    blocks += [(b.blockInfo.blockId, b.blockInfo.length) for b in fs.get_status(p).info.fileBlockInfos]
-ok_all = all(w.worker.has_block(b) for b, _ in blocks)
-got = b"".join(w.worker.read_bytes(b, 0, n) for b, n in blocks)
-ok_bytes = got == cached.tobytes() + ufs_only.tobytes()
+for p, arr in (("/dl/cached", cached), ("/dl/ufs", ufs_only)):
+    blocks += [(b.blockInfo.blockId, b.blockInfo.length, arr[i * (2 << 20):i * (2 << 20) + b.blockInfo.length].tobytes())
+               for i, b in enumerate(fs.get_status(p).info.fileBlockInfos)]
+held = [b for b, _, _ in blocks if w.worker.has_block(b)]
+ok_all = len(held) == len(blocks)
+ok_bytes = all(w.worker.read_bytes(b, 0, n) == exp for b, n, exp in blocks if w.worker.has_block(b))
 print(json.dumps({"rank": rank, "status": status, "err": err, "all": ok_all, "bytes": bool(ok_bytes),
-                  "gathered": plane.bytes_gathered}), flush=True)
+                  "gathered": plane.bytes_gathered, "held": held, "nblocks": len(blocks)}), flush=True)
 time.sleep(0.3)
 fs.close(); w.stop()
 dist.barrier()
@@ -273,15 +274,14 @@ dist.destroy_process_group()
 """
 
 
-def test_distributed_load_replication_all_uses_collective(tmp_path):
-    """``distributedLoad --replication`` >= worker count: owners load from the UFS, then every
-    worker receives every block through the transfer plane's all-gather (C4 on the product path)."""
-    script = COLLECTIVE_LOAD_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path)}
+def _run_collective_load(tmp_path, world, replication):
+    script = COLLECTIVE_LOAD_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path),
+                                       "replication": replication}
     path = tmp_path / "cload.py"
     path.write_text(script)
     procs = []
-    for rank in range(2):
-        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
         procs.append(subprocess.Popen([sys.executable, str(path)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
@@ -293,6 +293,13 @@ def test_distributed_load_replication_all_uses_collective(tmp_path):
             pytest.fail("collective load rank timed out")
         assert p.returncode == 0, err[-3000:]
         outs.append(json.loads(out.strip().splitlines()[-1]))
+    return outs
+
+
+def test_distributed_load_replication_all_uses_collective(tmp_path):
+    """``distributedLoad --replication`` >= worker count: owners load from the UFS, then every
+    worker receives every block through the transfer plane's all-gather (C4 on the product path)."""
+    outs = _run_collective_load(tmp_path, 2, -1)
     for o in outs:
         assert o["status"] == "COMPLETED", o
         assert o["all"] and o["bytes"], o
@@ -381,3 +388,93 @@ def test_replicate_all_rebuilds_group_after_rank_death(tmp_path):
         assert o["rebuilds"] == 1 and o["members"] == [0, 1], o
         assert o["have_alive"] and o["dead_round0"] and not o["dead_later"], o
         assert o["moved"] > 0, o
+
+
+RING_SCRIPT = r"""
+import os, sys, json
+sys.path.insert(0, %(root)r)
+import numpy as np, torch.distributed as dist
+from alluxio_amd.conf import Configuration
+from alluxio_amd.master.process import AlluxioMasterProcess
+from alluxio_amd.worker.process import AlluxioWorkerProcess
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.parallel.transfer import TransferPlane
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=world)
+work = %(work)r
+conf = Configuration({"alluxio.master.journal.folder": work + "/journal",
+    "alluxio.worker.tieredstore.level0.dirs.path": "dram", "alluxio.worker.tieredstore.level0.dirs.quota": "128MB",
+    "alluxio.worker.hbm.page.size": "1MB", "alluxio.user.block.size.bytes.default": "2MB"})
+box = [None]
+if rank == 0:
+    m = AlluxioMasterProcess(conf, host="127.0.0.1", port=0, root_ufs=work + "/ufs"); box[0] = m.start(start_heartbeats=False)
+dist.broadcast_object_list(box, src=0)
+w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, work_dir=work + "/w%%d" %% rank)
+w.start(start_heartbeats=False)
+plane = TransferPlane.establish(w.worker)
+fs = FileSystem(conf=conf.copy(), master_address=box[0])
+size = (1 + rank) * (1 << 20) + 333 * rank + 5       # rank r owns ceil(size/2MB) blocks
+data = np.random.default_rng(40 + rank).integers(0, 256, size, dtype=np.uint8)
+fs.write_file("/ring/f%%d" %% rank, data, write_type="MUST_CACHE")
+st = fs.get_status("/ring/f%%d" %% rank)
+mine = [(b.blockInfo.blockId, b.blockInfo.length, rank) for b in st.info.fileBlockInfos]
+allb = [None] * world
+dist.all_gather_object(allb, mine)
+blocks = [x for part in allb for x in part]
+moved = plane.replicate_ring(blocks, 2)
+prev = (rank - 1) %% world
+pdata = np.random.default_rng(40 + prev).integers(0, 256, (1 + prev) * (1 << 20) + 333 * prev + 5, dtype=np.uint8)
+ok_prev = all(w.worker.read_bytes(b, 0, n) == pdata[i * (2 << 20):i * (2 << 20) + n].tobytes()
+              for i, (b, n, _) in enumerate(allb[prev]))
+held = {r: all(w.worker.has_block(b) for b, _, _ in allb[r]) for r in range(world)}
+print(json.dumps({"rank": rank, "moved": moved, "ok_prev": bool(ok_prev), "held": held,
+                  "expect": sum(n for _, n, _ in allb[prev])}), flush=True)
+dist.barrier()
+fs.close(); w.stop()
+dist.barrier()
+if rank == 0:
+    m.stop()
+dist.destroy_process_group()
+"""
+
+
+def test_replicate_ring_p2p_gloo(tmp_path):
+    """k-copy ring replication with point-to-point send/recv: with 2 copies each rank ends up
+    holding exactly its own and its predecessor's blocks (4 ranks, uneven block counts)."""
+    world = 4
+    script = RING_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path)}
+    path = tmp_path / "ring.py"
+    path.write_text(script)
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, str(path)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            pytest.fail("ring rank timed out")
+        assert p.returncode == 0, err[-3000:]
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+    for o in outs:
+        r = o["rank"]
+        assert o["ok_prev"] and o["moved"] == o["expect"], o
+        held = {int(k): v for k, v in o["held"].items()}
+        assert held == {x: x in (r, (r - 1) % world) for x in range(world)}, o
+
+
+def test_distributed_load_two_copies_uses_ring(tmp_path):
+    """``distributedLoad --replication 2`` on 3 workers: blocks not yet on 2 workers are loaded by
+    an owner and sent to its ring successor with point-to-point send/recv; every block ends up on
+    exactly 2 workers with the right bytes."""
+    outs = _run_collective_load(tmp_path, 3, 2)
+    counts = {}
+    for o in outs:
+        assert o["status"] == "COMPLETED" and o["bytes"], o
+        for b in o["held"]:
+            counts[b] = counts.get(b, 0) + 1
+    assert len(counts) == outs[0]["nblocks"] and set(counts.values()) == {2}, counts
+    assert sum(o["gathered"] for o in outs) > 0
