@@ -138,7 +138,7 @@ constexpr int kSeqThreads = 256;
 // case: 4 KiB reads x 256 calls); otherwise 64-bit division.  SP: store policy of the ring
 // writes (1 = nontemporal: the ring is written once and consumed elsewhere, so keep the file's
 // pages, not the ring, resident in L2/MALL).
-template <bool POW2, int UNROLL, int SP>
+template <bool POW2, int UNROLL, int SP, int LP>
 __global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a, uint32_t vpr_shift,
                                                                uint32_t depth_shift) {
   extern __shared__ uint32_t c0[];  // streams entries (dynamic LDS: 1 KiB for 256 streams)
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a, ui
       d[u] = a.dst + (uint64_t)s * a.stream_stride + (uint64_t)k * a.buf + vi * 16;
       if (end - off >= 16) {
         nb[u] = 16;
-        v[u] = *reinterpret_cast<const u32x4*>(src);
+        v[u] = ld16<LP>(reinterpret_cast<const u32x4*>(src));
       } else {
         nb[u] = (uint32_t)(end - off);
         // tail of the pass: byte-wise, may cross into the next page
@@ -201,7 +201,11 @@ __global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a, ui
   }
 }
 
-static int g_seq_variant = 0;   // 0: cached stores, 1: nontemporal stores, +2: unroll 16
+// 0: cached stores, 1: nontemporal stores, +2: unroll 16, +4: nontemporal loads; -1 (default): auto — nontemporal ring
+// stores once the file is far larger than the 256 MB MALL (its reads stream from HBM and cached
+// ring writes would only evict them: 2.39 -> 2.55 TB/s on the 16 GiB staggered read,
+// profiles/r3_ring_tune_large_16g.json), cached stores when the file stays cache-resident
+static int g_seq_variant = -1;
 static unsigned g_seq_grid_cap = 8192;
 
 void set_seq_read_variant(int variant, unsigned grid_cap) {
@@ -223,7 +227,8 @@ hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream) {
     return hipErrorInvalidValue;
   const uint64_t vpr = a.buf >> 4;
   const uint64_t nvec = (uint64_t)a.streams * a.depth * vpr;
-  const int unroll = (g_seq_variant & 2) ? 16 : 8;
+  const int var = g_seq_variant >= 0 ? g_seq_variant : (a.file_len > (1ull << 30) ? 1 : 0);
+  const int unroll = (var & 2) ? 16 : 8;
   uint64_t blocks = (nvec + (uint64_t)kSeqThreads * unroll - 1) / ((uint64_t)kSeqThreads * unroll);
   if (blocks > g_seq_grid_cap) blocks = g_seq_grid_cap;
   if (blocks < 1) blocks = 1;
@@ -231,14 +236,20 @@ hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream) {
   const uint32_t vs = log2u(vpr), ds = log2u(a.depth);
   const size_t lds = a.streams * sizeof(uint32_t);
   const dim3 g((unsigned)blocks), b(kSeqThreads);
-#define AMDX_SEQ(P2, U, SP) \
-  hipLaunchKernelGGL((seq_read_kernel<P2, U, SP>), g, b, lds, stream, a, vs, ds)
-  const int sp = g_seq_variant & 1;
+#define AMDX_SEQ(P2, U, SP, LP) \
+  hipLaunchKernelGGL((seq_read_kernel<P2, U, SP, LP>), g, b, lds, stream, a, vs, ds)
+  const int sp = var & 1, lp = (var >> 2) & 1;
   if (p2) {
-    if (unroll == 16) { if (sp) AMDX_SEQ(true, 16, 1); else AMDX_SEQ(true, 16, 0); }
-    else { if (sp) AMDX_SEQ(true, 8, 1); else AMDX_SEQ(true, 8, 0); }
+    if (unroll == 16) {
+      if (lp) { if (sp) AMDX_SEQ(true, 16, 1, 1); else AMDX_SEQ(true, 16, 0, 1); }
+      else { if (sp) AMDX_SEQ(true, 16, 1, 0); else AMDX_SEQ(true, 16, 0, 0); }
+    } else {
+      if (lp) { if (sp) AMDX_SEQ(true, 8, 1, 1); else AMDX_SEQ(true, 8, 0, 1); }
+      else { if (sp) AMDX_SEQ(true, 8, 1, 0); else AMDX_SEQ(true, 8, 0, 0); }
+    }
   } else {
-    if (sp) AMDX_SEQ(false, 8, 1); else AMDX_SEQ(false, 8, 0);
+    if (lp) { if (sp) AMDX_SEQ(false, 8, 1, 1); else AMDX_SEQ(false, 8, 0, 1); }
+    else { if (sp) AMDX_SEQ(false, 8, 1, 0); else AMDX_SEQ(false, 8, 0, 0); }
   }
 #undef AMDX_SEQ
   return hipGetLastError();
