@@ -201,10 +201,12 @@ __global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a, ui
   }
 }
 
-// 0: cached stores, 1: nontemporal stores, +2: unroll 16, +4: nontemporal loads; -1 (default): auto — nontemporal ring
-// stores once the file is far larger than the 256 MB MALL (its reads stream from HBM and cached
-// ring writes would only evict them: 2.39 -> 2.55 TB/s on the 16 GiB staggered read,
-// profiles/r3_ring_tune_large_16g.json), cached stores when the file stays cache-resident
+// 0: cached stores, 1: nontemporal stores, +2: unroll 16, +4: nontemporal loads; -1 (default): auto —
+// nontemporal LOADS once the file is far larger than the 256 MB MALL: its bytes are read exactly
+// once from HBM, so streaming them past L2/MALL leaves the caches to the ring writes (16 GiB
+// staggered read: 2.40 -> 2.87 TB/s delivered = 5.7 TB/s of HBM traffic, above the runtime's own
+// D2D copy at 2.46 TB/s; profiles/r3_ring_tune_large_ntload.json, r3_copy_roof.json); fully
+// cached loads/stores while the file stays cache-resident (the lockstep headline shape)
 static int g_seq_variant = -1;
 static unsigned g_seq_grid_cap = 8192;
 
@@ -227,7 +229,7 @@ hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream) {
     return hipErrorInvalidValue;
   const uint64_t vpr = a.buf >> 4;
   const uint64_t nvec = (uint64_t)a.streams * a.depth * vpr;
-  const int var = g_seq_variant >= 0 ? g_seq_variant : (a.file_len > (1ull << 30) ? 1 : 0);
+  const int var = g_seq_variant >= 0 ? g_seq_variant : (a.file_len > (1ull << 30) ? 4 : 0);
   const int unroll = (var & 2) ? 16 : 8;
   uint64_t blocks = (nvec + (uint64_t)kSeqThreads * unroll - 1) / ((uint64_t)kSeqThreads * unroll);
   if (blocks > g_seq_grid_cap) blocks = g_seq_grid_cap;
