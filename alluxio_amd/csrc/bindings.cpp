@@ -798,6 +798,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_copy_variant", &set_copy_variant, py::arg("variant"), py::arg("grid_cap") = 0);
   m.def("set_crc_variant", &set_crc_variant, py::arg("variant"));
   m.def("set_lz4_decode_variant", &set_lz4_decode_variant, py::arg("variant"));
+  m.def("set_lz4_encode_variant", &set_lz4_encode_variant, py::arg("variant"));
   m.def("set_seq_read_variant", &set_seq_read_variant, py::arg("variant"), py::arg("grid_cap") = 0);
   m.attr("COPY_CHUNK") = kCopyChunk;
 }

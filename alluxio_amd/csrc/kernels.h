@@ -85,6 +85,7 @@ hipError_t launch_lz4_decompress(const Lz4Chunk* chunks, int n, int32_t* out_siz
 // 0: LDS-window decoder, 1: direct-to-HBM, 2 (default): direct + LDS-staged parse, 3: + LDS ring
 // of recent output for near matches.
 void set_lz4_decode_variant(int v);
+void set_lz4_encode_variant(int v);
 // LZ4 block compression (greedy, one wave per chunk, LDS hash table).  out_sizes[i] = -1 if
 // the chunk does not fit dst_capacity (caller then stores it raw).
 hipError_t launch_lz4_compress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,

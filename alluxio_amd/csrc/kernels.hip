@@ -2363,13 +2363,166 @@ __global__ __launch_bounds__(kLzThreads) void lz4_compress_kernel(const Lz4Chunk
   }
 }
 
+// Batch-parse encoder.  The first kernel above emits ONE sequence per 64-position probe batch and
+// throws the other 63 lanes' matches away, so text (≈8-byte sequences) costs one full probe round
+// (two barriers, a ballot, a serial token write) per ~8 input bytes.  Here every probe batch is
+// parsed completely: a uniform greedy walk over the ballot of hits selects every non-overlapping
+// match in position order (hits inside a taken match are masked off in one step), each selected
+// lane sizes its own sequence, a wave prefix sum places all of them, and the owning lanes write
+// their tokens / length bytes / offsets in parallel while literal runs are copied by the whole
+// wave.  Match extension compares 4 bytes at a time.  STAGE: chunk staged in LDS (72 KiB per
+// wave) vs read from global/L2 with only the 8 KiB hash table in LDS (8x the waves per CU).
+template <bool STAGE>
+__device__ __forceinline__ uint32_t lzb_read32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ __forceinline__ uint32_t lz_len_bytes(uint32_t v) {  // extra length bytes for a 4-bit field
+  return v >= 15 ? (v - 15) / 255 + 1 : 0;
+}
+
+__device__ __forceinline__ uint32_t lz_put_len(uint8_t* __restrict__ dst, uint32_t q, uint32_t v) {
+  if (v >= 15) {
+    uint32_t r = v - 15;
+    while (r >= 255) { dst[q++] = 255; r -= 255; }
+    dst[q++] = (uint8_t)r;
+  }
+  return q;
+}
+
+template <bool STAGE>
+__global__ __launch_bounds__(kLzThreads) void lz4_compress_batch_kernel(const Lz4Chunk* __restrict__ ch,
+                                                                       int n, int32_t* __restrict__ out_sizes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint16_t* table = reinterpret_cast<uint16_t*>(smem);                     // 8 KiB
+  uint8_t* stage = smem + (sizeof(uint16_t) << kLzHashLog);                // 64 KiB (STAGE)
+  const int lane = threadIdx.x;
+  for (int w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint8_t* __restrict__ gsrc = reinterpret_cast<const uint8_t*>(ch[w].src);
+    uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(ch[w].dst);
+    const uint32_t len = ch[w].src_bytes < kLzWindow ? ch[w].src_bytes : kLzWindow;
+    const uint32_t cap = ch[w].dst_capacity;
+    const uint8_t* src = gsrc;
+    if constexpr (STAGE) {
+      for (uint32_t i = lane; i < len; i += kLzThreads) stage[i] = gsrc[i];
+      src = stage;
+    }
+    for (uint32_t i = lane; i < (1u << kLzHashLog); i += kLzThreads) table[i] = 0xFFFF;
+    __syncthreads();
+    uint32_t op = 0, anchor = 0, ip = 0;
+    int32_t status = 0;
+    const uint32_t match_limit = len > kLzMfLimit ? len - kLzMfLimit : 0;
+    const uint32_t end_match = len > kLzLastLiterals ? len - kLzLastLiterals : 0;
+    while (ip < match_limit) {
+      const uint32_t pos = ip + lane;
+      uint32_t cand = 0xFFFFFFFFu, mlen = 0, h = 0;
+      if (pos < match_limit) {
+        const uint32_t v = lzb_read32<STAGE>(src + pos);
+        h = lz_hash(v);
+        const uint32_t c = table[h];
+        if (c != 0xFFFF && c < pos && pos - c <= 65535 && lzb_read32<STAGE>(src + c) == v) {
+          cand = c;
+          mlen = kLzMinMatch;
+          while (pos + mlen + 4 <= end_match && lzb_read32<STAGE>(src + c + mlen) == lzb_read32<STAGE>(src + pos + mlen))
+            mlen += 4;
+          while (pos + mlen < end_match && src[c + mlen] == src[pos + mlen]) ++mlen;
+        }
+      }
+      __syncthreads();
+      if (pos < match_limit) table[h] = (uint16_t)pos;  // last writer wins: any entry is verified
+      __syncthreads();
+      unsigned long long m = __ballot(cand != 0xFFFFFFFFu);
+      if (m == 0) { ip += kLzThreads; continue; }
+      // uniform greedy walk: take the first hit at/after the end of the last taken match
+      unsigned long long sel = 0;
+      uint32_t my_lit = 0, last_end = ip, prev_end = anchor;
+      while (m) {
+        const int g = __ffsll((long long)m) - 1;
+        const uint32_t gml = __shfl(mlen, g);
+        if (lane == g) my_lit = prev_end;
+        sel |= 1ull << g;
+        prev_end = last_end = ip + g + gml;
+        const uint32_t skip = last_end - ip;       // hits before last_end overlap the match (skip > g)
+        m = skip >= 64 ? 0ull : (m & (~0ull << skip));
+      }
+      const bool mine = (sel >> lane) & 1ull;
+      const uint32_t lit = mine ? pos - my_lit : 0;
+      const uint32_t need = mine ? 1 + lz_len_bytes(lit) + lit + 2 + lz_len_bytes(mlen - 4) : 0;
+      uint32_t incl = need;                          // wave inclusive prefix sum of sequence sizes
+#pragma unroll
+      for (int d = 1; d < kLzThreads; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+      }
+      const uint32_t total = __shfl(incl, kLzThreads - 1);
+      if (op + total > cap) { status = -1; break; }
+      const uint32_t o = op + incl - need;
+      if (mine) {
+        const uint32_t mcode = mlen - 4;
+        dst[o] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | (mcode >= 15 ? 15 : mcode));
+        uint32_t q = lz_put_len(dst, o + 1, lit) + lit;
+        const uint32_t moff = pos - cand;
+        dst[q] = (uint8_t)(moff & 255);
+        dst[q + 1] = (uint8_t)(moff >> 8);
+        lz_put_len(dst, q + 2, mcode);
+      }
+      // literal runs, one selected sequence at a time, copied by the whole wave
+      unsigned long long rest = sel;
+      while (rest) {
+        const int g = __ffsll((long long)rest) - 1;
+        rest &= rest - 1;
+        const uint32_t gl = __shfl(lit, g);
+        if (gl == 0) continue;
+        const uint32_t gs = __shfl(my_lit, g);
+        const uint32_t go = __shfl(o, g) + 1 + lz_len_bytes(gl);
+        for (uint32_t i = lane; i < gl; i += kLzThreads) dst[go + i] = src[gs + i];
+      }
+      op += total;
+      anchor = prev_end;
+      ip = last_end > ip + kLzThreads ? last_end : ip + kLzThreads;
+    }
+    if (status == 0) {
+      const uint32_t lit = len - anchor;
+      const uint32_t need = 1 + lz_len_bytes(lit) + lit;
+      if (op + need > cap) {
+        status = -1;
+      } else {
+        const uint32_t q = op + 1 + lz_len_bytes(lit);
+        if (lane == 0) {
+          dst[op] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+          lz_put_len(dst, op + 1, lit);
+        }
+        for (uint32_t i = lane; i < lit; i += kLzThreads) dst[q + i] = src[anchor + i];
+        op = q + lit;
+      }
+    }
+    if (lane == 0) out_sizes[w] = status ? -1 : (int32_t)op;
+    __syncthreads();
+  }
+}
+
+// 0: one sequence per probe batch (lz4_compress_kernel); 1: batch parse, chunk in LDS;
+// 2 (default): batch parse reading the chunk from global/L2 (8 KiB LDS per wave)
+static int g_lz4_encode_variant = 2;
+void set_lz4_encode_variant(int v) { g_lz4_encode_variant = v; }
+
 hipError_t launch_lz4_compress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
                                hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  const unsigned grid = (unsigned)std::min(n, 4096);
-  const size_t lds = kLzWindow + (sizeof(uint16_t) << kLzHashLog);
-  hipLaunchKernelGGL(lz4_compress_kernel, dim3(grid), dim3(kLzThreads), lds, stream, chunks, n,
-                     out_sizes);
+  const size_t table = sizeof(uint16_t) << kLzHashLog;
+  if (g_lz4_encode_variant == 0) {
+    const unsigned grid = (unsigned)std::min(n, 4096);
+    hipLaunchKernelGGL(lz4_compress_kernel, dim3(grid), dim3(kLzThreads), kLzWindow + table, stream,
+                       chunks, n, out_sizes);
+  } else if (g_lz4_encode_variant == 1) {
+    const unsigned grid = (unsigned)std::min(n, 4096);
+    hipLaunchKernelGGL((lz4_compress_batch_kernel<true>), dim3(grid), dim3(kLzThreads), table + kLzWindow,
+                       stream, chunks, n, out_sizes);
+  } else {
+    const unsigned grid = (unsigned)std::min(n, 65536);
+    hipLaunchKernelGGL((lz4_compress_batch_kernel<false>), dim3(grid), dim3(kLzThreads), table, stream,
+                       chunks, n, out_sizes);
+  }
   return hipGetLastError();
 }
 

@@ -94,15 +94,22 @@ def test_lz4_device_roundtrip(gpu, variant):
     bad = [(srcs[0].data_ptr(), outs[0].data_ptr(), max(1, len(comp[0]) - 3), 65536),
            (srcs[2].data_ptr(), outs[2].data_ptr(), len(comp[2]), max(1, len(chunks[2]) // 2))]
     assert all(sz < 0 for sz in C.lz4_device(bad, False, 0))
-    # device encode -> host decode
+    # device encode (every encoder variant) -> host decode
     ins = [torch.tensor(list(c), dtype=torch.uint8, device=gpu) for c in chunks]
     cap = [C.lz4_compress_bound(len(c)) for c in chunks]
-    enc = [torch.zeros(k, dtype=torch.uint8, device=gpu) for k in cap]
-    sizes = C.lz4_device([(i.data_ptr(), e.data_ptr(), len(c), k) for i, e, c, k in zip(ins, enc, chunks, cap)],
-                         True, 0)
-    for raw, e, sz in zip(chunks, enc, sizes):
-        assert sz > 0
-        assert C.lz4_decompress(e[:sz].cpu().numpy().tobytes(), len(raw)) == raw
+    for ev in (0, 1, 2):
+        C.set_lz4_encode_variant(ev)
+        enc = [torch.zeros(k, dtype=torch.uint8, device=gpu) for k in cap]
+        sizes = C.lz4_device([(i.data_ptr(), e.data_ptr(), len(c), k) for i, e, c, k in zip(ins, enc, chunks, cap)],
+                             True, 0)
+        for raw, e, sz in zip(chunks, enc, sizes):
+            assert sz > 0, ev
+            assert C.lz4_decompress(e[:sz].cpu().numpy().tobytes(), len(raw)) == raw, ev
+        # an output capacity too small for the stream fails cleanly
+        small = C.lz4_device([(ins[1].data_ptr(), enc[1].data_ptr(), len(chunks[1]), max(1, len(chunks[1]) // 2))],
+                             True, 0)
+        assert small[0] < 0, ev
+    C.set_lz4_encode_variant(2)
     C.set_lz4_decode_variant(-1)
 
 

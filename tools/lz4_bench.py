@@ -72,16 +72,23 @@ def main():
                      "call_GBps": round(n * 65536 / t / 1e9, 2), "out_GBps": round(n * 65536 / k / 1e9, 2)}
                 print(json.dumps(r), flush=True)
                 res.append(r)
-            if kind == "text":
+            if True:
                 # encode of the decoded chunks (device encoder, K11)
                 cb = C.lz4_compress_bound(65536)
                 enc = torch.empty(n * cb, dtype=torch.uint8, device=dev)
                 ech = [(out.data_ptr() + i * 65536, enc.data_ptr() + i * cb, 65536, cb) for i in range(n)]
-                k = C.lz4_device_kernel_ms(ech, True, 3) / 1e3
-                r = {"case": "lz4_encode", "data": kind, "chunks": n, "kernel_ms": round(k * 1e3, 3),
-                     "in_GBps": round(n * 65536 / k / 1e9, 2)}
-                print(json.dumps(r), flush=True)
-                res.append(r)
+                for ev in (0, 1, 2):
+                    C.set_lz4_encode_variant(ev)
+                    sizes = C.lz4_device(ech, True, 0)
+                    ok = all(s_ > 0 for s_ in sizes) and C.lz4_decompress(
+                        bytes(enc[:sizes[0]].cpu().numpy()), 65536) == raw
+                    k = C.lz4_device_kernel_ms(ech, True, 3) / 1e3
+                    r = {"case": "lz4_encode", "data": kind, "chunks": n, "encode_variant": ev, "ok": ok,
+                         "ratio": round(n * 65536 / sum(sizes), 3), "kernel_ms": round(k * 1e3, 3),
+                         "in_GBps": round(n * 65536 / k / 1e9, 2)}
+                    print(json.dumps(r), flush=True)
+                    res.append(r)
+                C.set_lz4_encode_variant(2)
                 del enc
             del out
     C.set_lz4_decode_variant(-1)
