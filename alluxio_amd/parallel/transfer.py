@@ -309,7 +309,10 @@ class TransferPlane:
         if buf is None or buf.numel() < need:
             dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
             cap = max(need, 2 * (buf.numel() if buf is not None else 0))
-            buf = self._stage = torch.empty(cap, dtype=torch.uint8, device=dev)
+            # gloo-coordinated workers with an HBM tier scatter out of this buffer with the GPU copy
+            # kernel: it must be pinned (device-visible) host memory, never pageable
+            pin = dev.type == "cpu" and bool(self.w.store.has_device_tier)
+            buf = self._stage = torch.empty(cap, dtype=torch.uint8, device=dev, pin_memory=pin)
         return buf[:shard], buf[shard:shard * (self.world + 1)]
 
     def _copy_block_out(self, block_id: int, n: int, dst) -> None:

@@ -73,6 +73,9 @@ def parse_args(argv=None):
     ap.add_argument("--prop", action="append", default=[], metavar="KEY=VALUE",
                     help="extra alluxio property for master/worker/client (repeatable)")
     ap.add_argument("--profile-json", default=None, help="append per-rank timings to this file")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses device 0 and the process group is gloo "
+                         "(RCCL refuses two ranks on one GPU); the data plane still runs on the GPU")
     return ap.parse_args(argv)
 
 
@@ -115,12 +118,15 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = torch.cuda.is_available()
+    if a.one_device:
+        local_rank = 0
     if gpu:
         torch.cuda.set_device(local_rank)
     distributed = world > 1
     if distributed:
-        dist.init_process_group("nccl" if gpu else "gloo")
+        dist.init_process_group("nccl" if gpu and not a.one_device else "gloo")
     dev_t = torch.device("cuda", local_rank) if gpu else torch.device("cpu")
+    red_dev = torch.device("cpu") if a.one_device else dev_t     # gloo collectives on host tensors
 
     file_size = parse_space_size(a.file_size)
     block_size = parse_space_size(a.block_size)
@@ -217,7 +223,7 @@ def main(argv=None):
     def reduce(value: float, op) -> float:
         if not distributed:
             return value
-        t = torch.tensor([value], dtype=torch.float64, device=dev_t)
+        t = torch.tensor([value], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=op)
         return t.item()
 
@@ -402,7 +408,7 @@ def main(argv=None):
                     reader.step()
                 n += 64
                 sync()
-                stop = torch.tensor([1.0 if time.perf_counter() - t >= a.duration else 0.0], device=dev_t)
+                stop = torch.tensor([1.0 if time.perf_counter() - t >= a.duration else 0.0], device=red_dev)
                 if distributed:
                     dist.broadcast(stop, src=0)
                 if stop.item() > 0:
