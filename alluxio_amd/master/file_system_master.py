@@ -1172,19 +1172,34 @@ class FileSystemMaster(Journaled):
     def set_acl(self, path: str, action: str, entries, recursive: bool = False) -> None:
         from ..security.acl import AclEntry
         path = normalize_path(path)
-        with self._lock_path(path), RpcContext(self) as rpc, self.tree.lock.write():
-            chain, missing = self.tree.resolve(path)
-            if missing:
-                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-            inode = chain[-1]
-            self.permission.check_owner(self._user(), inode, path)
-            targets = [inode] + (self.tree.descendants(inode) if recursive and inode.is_directory else [])
-            protos = [e.to_proto() if isinstance(e, AclEntry) else e for e in entries]
-            for t in targets:
-                self._apply(rpc, pb.journal.JournalEntry(set_acl=pb.journal.SetAclEntry(
-                    id=t.id, op_time_ms=rpc.op_time_ms,
-                    action=pb.journal.PSetAclAction.values_by_name[action].number, entries=protos,
-                    recursive=recursive)))
+        ufs_updates = []
+        with self._lock_path(path):
+            with RpcContext(self) as rpc, self.tree.lock.write():
+                chain, missing = self.tree.resolve(path)
+                if missing:
+                    raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+                inode = chain[-1]
+                self.permission.check_owner(self._user(), inode, path)
+                targets = [inode] + (self.tree.descendants(inode) if recursive and inode.is_directory else [])
+                protos = [e.to_proto() if isinstance(e, AclEntry) else e for e in entries]
+                for t in targets:
+                    self._apply(rpc, pb.journal.JournalEntry(set_acl=pb.journal.SetAclEntry(
+                        id=t.id, op_time_ms=rpc.op_time_ms,
+                        action=pb.journal.PSetAclAction.values_by_name[action].number, entries=protos,
+                        recursive=recursive)))
+                    if t.is_persisted and t.acl is not None:
+                        full = list(t.acl.entries())
+                        if getattr(t, "default_acl", None) is not None:
+                            full += t.default_acl.entries()
+                        ufs_updates.append((self.tree.path_of(t), full))
+            # the persisted files' full ACLs go to the UFS after the tree lock, under the path lock
+            # (DefaultFileSystemMaster.setAclSingleInode -> ufs.setAclEntries)
+            for tpath, full in ufs_updates:
+                try:
+                    res = self._resolve_ufs(tpath)
+                    res.ufs.set_acl_entries(res.uri, full)
+                except Exception:  # noqa: BLE001
+                    LOG.debug("ufs ACL propagation failed for %s", tpath, exc_info=True)
 
     def set_xattr(self, path: str, key: str, value: bytes) -> None:
         path = normalize_path(path)

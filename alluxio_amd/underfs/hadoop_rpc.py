@@ -95,6 +95,15 @@ msg GetFsStatsResponseProto capacity=1:u64! used=2:u64! remaining=3:u64! under_r
     corrupt_blocks=5:u64! missing_blocks=6:u64!
 msg RenewLeaseRequestProto clientName=1:str!
 msg RenewLeaseResponseProto
+# acl.proto (HdfsAclProvider: getAclStatus / setAcl)
+enum AclEntryTypeProto USER=0 GROUP=1 MASK=2 OTHER=3
+enum AclEntryScopeProto ACCESS=0 DEFAULT=1
+msg AclEntryProto type=1:AclEntryTypeProto! scope=2:AclEntryScopeProto! permissions=3:u32! name=4:str
+msg AclStatusProto owner=1:str! group=2:str! sticky=3:bool! entries=4:AclEntryProto* permission=5:FsPermissionProto
+msg GetAclStatusRequestProto src=1:str!
+msg GetAclStatusResponseProto result=1:AclStatusProto!
+msg SetAclRequestProto src=1:str! aclSpec=2:AclEntryProto*
+msg SetAclResponseProto
 msg GetCurrentEditLogTxidRequestProto
 msg GetCurrentEditLogTxidResponseProto txid=1:i64!
 msg GetEditsFromTxidRequestProto txid=1:i64!
@@ -412,6 +421,15 @@ class NameNodeClient:
 
     def get_fs_stats(self):
         return self.call("getFsStats", hdfs.GetFsStatusRequestProto(), hdfs.GetFsStatsResponseProto)
+
+    # -- ACLs (acl.proto; FsAction ordinals equal the rwx bit values) ----------------------------
+    def get_acl_status(self, src: str):
+        return self.call("getAclStatus", hdfs.GetAclStatusRequestProto(src=src), hdfs.GetAclStatusResponseProto).result
+
+    def set_acl(self, src: str, spec) -> None:
+        req = hdfs.SetAclRequestProto(src=src)
+        req.aclSpec.extend(spec)
+        self.call("setAcl", req, hdfs.SetAclResponseProto)
 
     # -- inotify (HdfsAdmin.getInotifyEventStream) ------------------------------------------------
     def current_edit_txid(self) -> int:

@@ -20,6 +20,7 @@ import uuid
 from .base import (CreateOptions, DeleteOptions, ListOptions, MkdirsOptions, OpenOptions, SpaceType,
                    UfsDirectoryStatus, UfsFileStatus, UnderFileSystem)
 from .hadoop_rpc import (FILE_IS_DIR, BlockReader, BlockWriter, NameNodeClient, RemoteException, translate)
+from .hadoop_rpc import hdfs as hdfs_pb
 from .registry import UnderFileSystemFactory, register_factory
 
 
@@ -305,6 +306,64 @@ class HdfsUnderFileSystem(UnderFileSystem):
         s = self._rpc(self.nn.get_fs_stats)
         return {SpaceType.SPACE_TOTAL: s.capacity, SpaceType.SPACE_USED: s.used,
                 SpaceType.SPACE_FREE: s.remaining}.get(space_type, s.capacity)
+
+    # ---- ACLs (underfs/hdfs/.../acl/SupportedHdfsAclProvider.java: getAclStatus / setAcl) ----------
+    def set_acl_entries(self, path, entries) -> None:
+        """Full replacement ACL (base user/group/other entries included) -> ``setAcl``."""
+        from ..security.acl import AclEntryType as T
+        kind = {T.OWNER: 0, T.NAMED_USER: 0, T.OWNING_GROUP: 1, T.NAMED_GROUP: 1, T.MASK: 2, T.OTHER: 3}
+        spec = []
+        for e in entries:
+            x = hdfs_pb.AclEntryProto(type=kind[e.type], scope=1 if e.is_default else 0,
+                                      permissions=int(e.actions) & 7)
+            if e.subject and e.type in (T.NAMED_USER, T.NAMED_GROUP):
+                x.name = e.subject
+            spec.append(x)
+        self._rpc(self.nn.set_acl, self._p(path), spec)
+
+    def get_acl_pair(self, path):
+        """(access ACL, default ACL or None) from ``getAclStatus``.  HDFS lists only the extended
+        entries; with any of them the permission's group bits are the mask and the unnamed GROUP
+        entry carries the owning group's bits."""
+        from ..security.acl import AccessControlList
+        try:
+            st = self.nn.get_acl_status(self._p(path))
+        except RemoteException as e:
+            if e.short_name == "FileNotFoundException":
+                return None
+            raise translate(e) from None
+        perm = st.permission.perm & 0o777 if st.HasField("permission") else 0o755
+        acl = AccessControlList(st.owner, st.group, perm)
+        dacl = None
+        for e in st.entries:
+            if e.scope == 1:
+                if dacl is None:
+                    dacl = AccessControlList(st.owner, st.group, perm, is_default=True)
+                tgt = dacl
+            else:
+                tgt = acl
+            self._apply_entry(tgt, e)
+        if acl.is_extended:
+            acl.mask = (perm >> 3) & 7
+        return acl, dacl
+
+    @staticmethod
+    def _apply_entry(acl, e) -> None:
+        bits = e.permissions & 7
+        if e.type == 0:
+            if e.name:
+                acl.named_users[e.name] = bits
+            else:
+                acl.mode = (acl.mode & 0o077) | (bits << 6)
+        elif e.type == 1:
+            if e.name:
+                acl.named_groups[e.name] = bits
+            else:
+                acl.mode = (acl.mode & 0o707) | (bits << 3)
+        elif e.type == 2:
+            acl.mask = bits
+        else:
+            acl.mode = (acl.mode & 0o770) | bits
 
     # ---- active sync (SupportedHdfsActiveSyncProvider over the NameNode's inotify stream) --------
     def supports_active_sync(self) -> bool:

@@ -39,6 +39,7 @@ class Node:
         self.block_size, self.replication = block_size, replication
         self.complete = is_dir
         self.file_id = 0
+        self.acl: list = []             # extended + default AclEntryProto (HDFS AclFeature)
 
 
 class MiniDfs:
@@ -312,6 +313,51 @@ class MiniDfs:
         used = sum(len(v) for dn in self.datanodes for v in dn.blocks.values())
         return hdfs.GetFsStatsResponseProto(capacity=1 << 40, used=used, remaining=(1 << 40) - used,
                                             under_replicated=0, corrupt_blocks=0, missing_blocks=0)
+
+    def rpc_getAclStatus(self, b, user):
+        r = hdfs.GetAclStatusRequestProto.FromString(b)
+        n = self.ns.get(self._norm(r.src))
+        if n is None:
+            raise _fnf(r.src)
+        out = hdfs.GetAclStatusResponseProto()
+        st = out.result
+        st.owner, st.group, st.sticky = n.owner, n.group, False
+        st.permission.perm = n.mode
+        st.entries.extend(n.acl)
+        return out
+
+    def rpc_setAcl(self, b, user):
+        """Full replacement: base entries set the permission bits (the mask, when present, takes
+        the group bits); named, unnamed-group-with-mask and default entries are kept as the ACL."""
+        r = hdfs.SetAclRequestProto.FromString(b)
+        n = self.ns.get(self._norm(r.src))
+        if n is None:
+            raise _fnf(r.src)
+        keep, mode, mask = [], n.mode, None
+        access = [e for e in r.aclSpec if e.scope == 0]
+        extended = any(e.HasField("name") and e.name for e in access)
+        for e in r.aclSpec:
+            if e.scope == 1:
+                keep.append(e)
+                continue
+            if e.type == 0 and not e.name:
+                mode = (mode & 0o7077) | (e.permissions << 6)
+            elif e.type == 3:
+                mode = (mode & 0o7770) | e.permissions
+            elif e.type == 2:
+                mask = e.permissions
+            elif e.type == 1 and not e.name:
+                if extended:
+                    keep.append(e)
+                else:
+                    mode = (mode & 0o7707) | (e.permissions << 3)
+            else:
+                keep.append(e)
+        if extended and mask is not None:
+            mode = (mode & 0o7707) | (mask << 3)
+        n.mode, n.acl = mode, keep
+        self._event(4, hdfs.MetadataUpdateEventProto(path=self._norm(r.src), type=5))
+        return hdfs.SetAclResponseProto()
 
     def rpc_getCurrentEditLogTxid(self, b, user):
         return hdfs.GetCurrentEditLogTxidResponseProto(txid=len(self.edits))

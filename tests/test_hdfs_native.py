@@ -221,3 +221,29 @@ def test_active_sync_follows_inotify(dfs, tmp_path):
         m.active_sync_heartbeat()
         assert sorted(s.name for s in fs.list_status("/h/a", load_metadata="NEVER")) == ["f1r"]
         fs.unmount("/h")
+
+
+def test_hdfs_acls_roundtrip_and_master_propagation(dfs, tmp_path):
+    """setAcl/getAclStatus through the UFS (SupportedHdfsAclProvider), and an Alluxio setfacl on a
+    persisted file propagating the full ACL to HDFS."""
+    from alluxio_amd.minicluster import LocalAlluxioCluster
+    from alluxio_amd.security.acl import AclEntry
+    ufs = _ufs(dfs)
+    with ufs.create("/acl/f") as f:
+        f.write(b"x")
+    spec = [AclEntry.parse(x) for x in ("user::rw-", "user:alice:r-x", "group::r--", "mask::r-x", "other::---",
+                                        "default:user::rwx", "default:group::r-x", "default:other::r--")]
+    ufs.set_acl_entries("/acl/f", spec)
+    acl, dacl = ufs.get_acl_pair("/acl/f")
+    assert acl.named_users == {"alice": 5} and acl.mask == 5 and (acl.mode >> 6) & 7 == 6 and acl.mode & 7 == 0
+    assert dacl is not None and (dacl.mode >> 6) & 7 == 7
+    assert ufs.get_acl_pair("/acl/none") is None
+    with LocalAlluxioCluster(num_workers=1, conf={"alluxio.worker.tieredstore.level0.dirs.path": "dram"},
+                             work_dir=str(tmp_path / "c")) as c:
+        fs = c.client()
+        fs.mount("/h", f"hdfs://127.0.0.1:{dfs.port}/acl", properties={"dfs.blocksize": "256k"})
+        fs.write_file("/h/g", b"data", write_type="CACHE_THROUGH")
+        c.master.fs_master.set_acl("/h/g", "MODIFY", [AclEntry.parse("user:bob:rw-")])
+        acl2, _ = ufs.get_acl_pair("/acl/g")
+        assert acl2.named_users == {"bob": 6}
+        fs.unmount("/h")
