@@ -143,6 +143,13 @@ def _k(attr: str, name: str, default, scope=Scope.ALL, description=""):
     return key
 
 
+_k("PROXY_HDFS_RPC_PORT", "alluxio.proxy.hdfs.rpc.port", "-1", Scope.NONE,
+   "NameNode (Hadoop IPC ClientProtocol) port of the proxy's HDFS-protocol gateway; -1 disables it, "
+   "0 picks a free port.  Hadoop clients then use hdfs://<proxy>:<port>/.")
+_k("PROXY_HDFS_DATA_PORT", "alluxio.proxy.hdfs.data.port", "0", Scope.NONE,
+   "DataNode (DataTransferProtocol) port of the HDFS-protocol gateway (0: a free port).")
+_k("PROXY_HDFS_HOSTNAME", "alluxio.proxy.hdfs.hostname", "", Scope.NONE,
+   "Host the gateway advertises as its DataNode address (default: the bind host).")
 _k("WORKER_GPU_DEVICE", "alluxio.worker.gpu.device", "-1", Scope.WORKER,
    "HIP device index this worker owns (-1: LOCAL_RANK or 0).")
 _k("WORKER_HBM_PAGE_SIZE", "alluxio.worker.hbm.page.size", "2MB", Scope.WORKER,

@@ -635,9 +635,17 @@ def main(argv=None) -> int:  # pragma: no cover - CLI entry
     port = a.port if a.port is not None else conf.get_int("alluxio.proxy.web.port")
     srv = ProxyServer(fs, a.host, port, conf.get("alluxio.proxy.s3.writetype", "CACHE_THROUGH"))
     LOG.info("proxy serving on %s:%d", a.host, srv.start())
+    gw = None
+    hdfs_port = conf.get_int("alluxio.proxy.hdfs.rpc.port")
+    if hdfs_port >= 0:
+        from .hdfs_gateway import serve
+        gw = serve(fs, a.host, hdfs_port, conf.get_int("alluxio.proxy.hdfs.data.port"),
+                   conf.get("alluxio.proxy.hdfs.hostname") or None)
     try:
         threading.Event().wait()
     except KeyboardInterrupt:
         pass
+    if gw is not None:
+        gw.stop()
     srv.stop()
     return 0

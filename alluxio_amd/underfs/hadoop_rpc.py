@@ -95,6 +95,17 @@ msg GetFsStatsResponseProto capacity=1:u64! used=2:u64! remaining=3:u64! under_r
     corrupt_blocks=5:u64! missing_blocks=6:u64!
 msg RenewLeaseRequestProto clientName=1:str!
 msg RenewLeaseResponseProto
+msg FsServerDefaultsProto blockSize=1:u64! bytesPerChecksum=2:u32! writePacketSize=3:u32! replication=4:u32!
+    fileBufferSize=5:u32! encryptDataTransfer=6:bool@false trashInterval=7:u64@0
+    checksumType=8:ChecksumTypeProto@CHECKSUM_CRC32
+msg GetServerDefaultsRequestProto
+msg GetServerDefaultsResponseProto serverDefaults=1:FsServerDefaultsProto!
+msg ContentSummaryProto length=1:u64! fileCount=2:u64! directoryCount=3:u64! quota=4:u64! spaceConsumed=5:u64!
+    spaceQuota=6:u64!
+msg GetContentSummaryRequestProto path=1:str!
+msg GetContentSummaryResponseProto summary=1:ContentSummaryProto!
+msg FsyncRequestProto src=1:str! client=2:str! lastBlockLength=3:si64@-1 fileId=4:u64@0
+msg FsyncResponseProto
 # acl.proto (HdfsAclProvider: getAclStatus / setAcl)
 enum AclEntryTypeProto USER=0 GROUP=1 MASK=2 OTHER=3
 enum AclEntryScopeProto ACCESS=0 DEFAULT=1
@@ -418,6 +429,14 @@ class NameNodeClient:
         if group:
             req.groupname = group
         self.call("setOwner", req, hdfs.SetOwnerResponseProto)
+
+    def get_server_defaults(self):
+        return self.call("getServerDefaults", hdfs.GetServerDefaultsRequestProto(),
+                         hdfs.GetServerDefaultsResponseProto).serverDefaults
+
+    def get_content_summary(self, path: str):
+        return self.call("getContentSummary", hdfs.GetContentSummaryRequestProto(path=path),
+                         hdfs.GetContentSummaryResponseProto).summary
 
     def get_fs_stats(self):
         return self.call("getFsStats", hdfs.GetFsStatusRequestProto(), hdfs.GetFsStatsResponseProto)

@@ -10,21 +10,14 @@ the destination exists or the source is missing, paged getListing (``ls_limit`` 
 """
 from __future__ import annotations
 
-import socket
-import socketserver
-import struct
 import threading
 import time
 
+from alluxio_amd.proxy.hdfs_gateway import DataTransferServer, IpcServer
+from alluxio_amd.proxy.hdfs_gateway import RpcError as _Remote
 from alluxio_amd.underfs import hadoop_rpc as H
 
 common, hdfs = H.common, H.hdfs
-
-
-class _Remote(Exception):
-    def __init__(self, cls, msg):
-        super().__init__(msg)
-        self.cls, self.msg = cls, msg
 
 
 def _fnf(p):
@@ -51,10 +44,8 @@ class MiniDfs:
         self.next_file_id = 16386
         self.pool_id = "BP-1-127.0.0.1-1"
         self.datanodes = [_DataNode(self, i) for i in range(num_datanodes)]
-        self.namenode = _Server(("127.0.0.1", 0), _NameNodeHandler)
-        self.namenode.dfs = self
-        self.port = self.namenode.server_address[1]
-        threading.Thread(target=self.namenode.serve_forever, daemon=True).start()
+        self.namenode = IpcServer(self.handle)
+        self.port = self.namenode.port
         self.calls: list[str] = []
         self.edits: list = []           # inotify: EventBatchProto per edit, txid = index + 1
 
@@ -64,8 +55,7 @@ class MiniDfs:
         self.edits.append(b)
 
     def stop(self):
-        self.namenode.shutdown()
-        self.namenode.server_close()
+        self.namenode.stop()
         for d in self.datanodes:
             d.stop()
 
@@ -377,171 +367,59 @@ class MiniDfs:
         return hdfs.RenewLeaseResponseProto()
 
 
-class _Server(socketserver.ThreadingTCPServer):
-    daemon_threads = True
-    allow_reuse_address = True
+class _Sink:
+    def __init__(self, dn, bid):
+        self.dn, self.bid, self.buf = dn, bid, bytearray()
+
+    def write(self, data):
+        self.buf += data
+
+    def commit(self, n):
+        self.dn.blocks[self.bid] = bytes(self.buf)        # finalized replica (blockReceived)
 
 
-def _send_frame(sock, *msgs):
-    payload = b"".join(H.delimited(m) for m in msgs)
-    sock.sendall(struct.pack(">I", len(payload)) + payload)
+class _Reader:
+    def __init__(self, data, off):
+        self.data, self.off = data, off
 
-
-class _NameNodeHandler(socketserver.BaseRequestHandler):
-    def handle(self):
-        s, dfs = self.request, self.server.dfs
-        try:
-            pre = bytes(H.recv_exact(s, 7))
-            if pre[:4] != b"hrpc" or pre[4] != H.IPC_VERSION:
-                return
-            user = "hdfs"
-            while True:
-                (n,) = struct.unpack(">I", bytes(H.recv_exact(s, 4)))
-                frame = H.recv_exact(s, n)
-                rh, pos = H.parse_delimited(frame, 0, common.RpcRequestHeaderProto)
-                if rh.callId == H.CONNECTION_CONTEXT_CALL_ID:
-                    ctx, _ = H.parse_delimited(frame, pos, common.IpcConnectionContextProto)
-                    user = ctx.userInfo.effectiveUser or user
-                    continue
-                req_hdr, pos = H.parse_delimited(frame, pos, common.RequestHeaderProto)
-                # the request body is the rest of the frame, varint-delimited
-                shift = ln = 0
-                while True:
-                    c = frame[pos]
-                    pos += 1
-                    ln |= (c & 0x7F) << shift
-                    if not c & 0x80:
-                        break
-                    shift += 7
-                body = bytes(frame[pos:pos + ln])
-                resp_hdr = common.RpcResponseHeaderProto(callId=rh.callId, status=0, serverIpcVersionNum=9,
-                                                         clientId=rh.clientId)
-                try:
-                    out = dfs.handle(req_hdr.methodName, body, user)
-                    _send_frame(s, resp_hdr, out)
-                except _Remote as e:
-                    resp_hdr.status = 1
-                    resp_hdr.exceptionClassName, resp_hdr.errorMsg = e.cls, e.msg
-                    _send_frame(s, resp_hdr)
-        except (ConnectionError, OSError):
-            return
+    def read(self, n):
+        b = self.data[self.off:self.off + n]
+        self.off += len(b)
+        return b
 
 
 class _DataNode:
+    """One DataNode: the shared DataTransferServer over an in-memory replica map."""
+
     def __init__(self, dfs: MiniDfs, idx: int):
         self.dfs, self.idx = dfs, idx
         self.blocks: dict[int, bytes] = {}
         self.fail_reads = False
-        self.corrupt_reads = False
-        self.server = _Server(("127.0.0.1", 0), _DataNodeHandler)
-        self.server.dn = self
-        self.port = self.server.server_address[1]
-        threading.Thread(target=self.server.serve_forever, daemon=True).start()
+        self.server = DataTransferServer(self._open_read, self._open_write)
+        self.port = self.server.port
+
+    @property
+    def corrupt_reads(self):
+        return self.server.fault_flip_bits
+
+    @corrupt_reads.setter
+    def corrupt_reads(self, v):
+        self.server.fault_flip_bits = v
+
+    def _open_read(self, bid, offset, length):
+        data = self.blocks.get(bid)
+        if data is None or self.fail_reads or offset + length > len(data):
+            raise IOError(f"block {bid} unavailable")
+        return _Reader(data, offset)
+
+    def _open_write(self, op):
+        return _Sink(self, op.header.baseHeader.block.blockId)
 
     def info(self):
-        d = hdfs.DatanodeInfoProto(capacity=1 << 40)
-        d.id.CopyFrom(hdfs.DatanodeIDProto(ipAddr="127.0.0.1", hostName="localhost",
-                                           datanodeUuid=f"dn-{self.idx}", xferPort=self.port, infoPort=0,
-                                           ipcPort=0))
+        d = self.server.info("127.0.0.1")
+        d.id.hostName = "localhost"
+        d.id.datanodeUuid = f"dn-{self.idx}"
         return d
 
     def stop(self):
-        self.server.shutdown()
-        self.server.server_close()
-
-
-class _DataNodeHandler(socketserver.BaseRequestHandler):
-    def handle(self):
-        s, dn = self.request, self.server.dn
-        try:
-            ver, op = struct.unpack(">HB", bytes(H.recv_exact(s, 3)))
-            if ver != H.DATA_TRANSFER_VERSION:
-                return
-            if op == H.OP_READ_BLOCK:
-                self._read(s, dn, H.recv_delimited(s, hdfs.OpReadBlockProto))
-            elif op == H.OP_WRITE_BLOCK:
-                self._write(s, dn, H.recv_delimited(s, hdfs.OpWriteBlockProto))
-        except (ConnectionError, OSError):
-            return
-
-    @staticmethod
-    def _read(s, dn, op):
-        bid = op.header.baseHeader.block.blockId
-        data = dn.blocks.get(bid)
-        if data is None or dn.fail_reads or op.offset + op.len > len(data):
-            s.sendall(H.delimited(hdfs.BlockOpResponseProto(status=H.ST_ERROR, message=f"block {bid} unavailable")))
-            return
-        bpc = H.BYTES_PER_CHECKSUM
-        start = op.offset - op.offset % bpc           # chunk-aligned start, as BlockSender does
-        end = op.offset + op.len
-        resp = hdfs.BlockOpResponseProto(status=H.ST_SUCCESS)
-        resp.readOpChecksumInfo.checksum.type = H.CHECKSUM_CRC32C
-        resp.readOpChecksumInfo.checksum.bytesPerChecksum = bpc
-        resp.readOpChecksumInfo.chunkOffset = start
-        s.sendall(H.delimited(resp))
-        seq, off = 0, start
-        while off < end:
-            n = min(H.PACKET_DATA, end - off)
-            if dn.corrupt_reads:        # a bit flipped on disk after the checksums were stored
-                piece = data[off:off + n]
-                sums = H._crc_chunks(piece, bpc)
-                hdr = hdfs.PacketHeaderProto(offsetInBlock=off, seqno=seq, lastPacketInBlock=False,
-                                             dataLen=n).SerializeToString()
-                bad = bytes([piece[0] ^ 1]) + piece[1:]
-                s.sendall(struct.pack(">IH", 4 + len(sums) + n, len(hdr)) + hdr + sums + bad)
-            else:
-                H.write_packet(s, off, seq, data[off:off + n], False)
-            off += n
-            seq += 1
-        H.write_packet(s, off, seq, b"", True)
-        try:
-            H.recv_delimited(s, hdfs.ClientReadStatusProto)
-        except (ConnectionError, OSError):
-            pass
-
-    @staticmethod
-    def _write(s, dn, op):
-        bid = op.header.baseHeader.block.blockId
-        downstream = None
-        if len(op.targets):                            # forward to the next DataNode in the pipeline
-            nxt = op.targets[0]
-            downstream = socket.create_connection((nxt.id.ipAddr, nxt.id.xferPort), timeout=30)
-            fwd = hdfs.OpWriteBlockProto()
-            fwd.CopyFrom(op)
-            del fwd.targets[0]
-            downstream.sendall(struct.pack(">HB", H.DATA_TRANSFER_VERSION, H.OP_WRITE_BLOCK) + H.delimited(fwd))
-            r = H.recv_delimited(downstream, hdfs.BlockOpResponseProto)
-            if r.status != H.ST_SUCCESS:
-                s.sendall(H.delimited(hdfs.BlockOpResponseProto(status=H.ST_ERROR, firstBadLink=nxt.id.ipAddr)))
-                return
-        s.sendall(H.delimited(hdfs.BlockOpResponseProto(status=H.ST_SUCCESS)))
-        buf = bytearray()
-        bpc = op.requestedChecksum.bytesPerChecksum or H.BYTES_PER_CHECKSUM
-        while True:
-            plen, hlen = struct.unpack(">IH", bytes(H.recv_exact(s, 6)))
-            hraw = bytes(H.recv_exact(s, hlen))
-            body = bytes(H.recv_exact(s, plen - 4))
-            hdr = hdfs.PacketHeaderProto.FromString(hraw)
-            data = body[len(body) - hdr.dataLen:]
-            sums = body[:len(body) - hdr.dataLen]
-            status = H.ST_SUCCESS
-            if hdr.dataLen and H._crc_chunks(data, bpc) != sums:
-                status = H.ST_ERROR_CHECKSUM
-            if hdr.offsetInBlock != len(buf):
-                status = H.ST_ERROR
-            if downstream is not None:
-                downstream.sendall(struct.pack(">IH", plen, hlen) + hraw + body)
-            replies = [status]
-            if downstream is not None:
-                dack = H.recv_delimited(downstream, hdfs.PipelineAckProto)
-                replies += list(dack.reply)
-            buf += data
-            ack = hdfs.PipelineAckProto(seqno=hdr.seqno)
-            ack.reply.extend(replies)
-            s.sendall(H.delimited(ack))
-            if hdr.lastPacketInBlock or status != H.ST_SUCCESS:
-                break
-        if downstream is not None:
-            downstream.close()
-        if status == H.ST_SUCCESS:
-            dn.blocks[bid] = bytes(buf)               # finalized replica (blockReceived)
+        self.server.stop()
