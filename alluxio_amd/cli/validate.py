@@ -144,6 +144,118 @@ def _ufs(conf):
         return FAILED, f"root UFS {root}: {e}"
 
 
+def _hadoop_xml(path: str) -> dict[str, str]:
+    """``<configuration><property><name/><value/></property>...`` (HadoopConfigurationFileParser)."""
+    import xml.etree.ElementTree as ET
+    out = {}
+    for prop in ET.parse(path).getroot().iter("property"):
+        name, value = prop.findtext("name"), prop.findtext("value")
+        if name:
+            out[name.strip()] = (value or "").strip()
+    return out
+
+
+def _hdfs_root(conf):
+    root = conf.get("alluxio.master.mount.table.root.ufs")
+    return root if root.startswith("hdfs://") else None
+
+
+@task("ufs.hdfs.config.parity", ("master", "worker"),
+      "validate the HDFS core-site/hdfs-site files parse and agree with HADOOP_CONF_DIR")
+def _hdfs_conf(conf):
+    """HdfsConfValidationTask + HdfsConfParityValidationTask: the files named by
+    ``alluxio.underfs.hdfs.configuration`` (``:``-separated) must be valid Hadoop XML, and keys set
+    in both them and ``$HADOOP_CONF_DIR`` must not disagree."""
+    if _hdfs_root(conf) is None:
+        return SKIPPED, "root UFS is not HDFS"
+    files = [f for f in (conf.get("alluxio.underfs.hdfs.configuration") or "").split(":") if f and os.path.exists(f)]
+    if not files:
+        return WARNING, "no file of alluxio.underfs.hdfs.configuration exists (client defaults are used)"
+    merged: dict[str, str] = {}
+    for f in files:
+        try:
+            merged.update(_hadoop_xml(f))
+        except Exception as e:  # noqa: BLE001
+            return FAILED, f"cannot parse {f}: {e}"
+    hd = os.environ.get("HADOOP_CONF_DIR")
+    if hd:
+        diffs = []
+        for name in ("core-site.xml", "hdfs-site.xml"):
+            fp = os.path.join(hd, name)
+            if os.path.exists(fp):
+                for k, v in _hadoop_xml(fp).items():
+                    if k in merged and merged[k] != v:
+                        diffs.append(f"{k}: {merged[k]!r} vs {v!r} in {fp}")
+        if diffs:
+            return WARNING, "HDFS configuration differs from HADOOP_CONF_DIR: " + "; ".join(diffs[:5])
+    return OK, f"{len(merged)} HDFS properties from {len(files)} file(s)"
+
+
+@task("ufs.hdfs.reachable", ("master", "worker"),
+      "validate the HDFS NameNode answers ClientProtocol calls (HdfsVersionValidationTask)")
+def _hdfs_reachable(conf):
+    root = _hdfs_root(conf)
+    if root is None:
+        return SKIPPED, "root UFS is not HDFS"
+    try:
+        from ..underfs import registry
+        ufs = registry.create(root, conf)
+        d = ufs.nn.get_server_defaults()
+        st = ufs.nn.get_fs_stats()
+        ufs.close()
+    except Exception as e:  # noqa: BLE001
+        return FAILED, f"NameNode of {root}: {e}"
+    return OK, (f"NameNode of {root} reachable over Hadoop IPC v9: block size {d.blockSize}, "
+                f"checksum type {d.checksumType}, {st.remaining} of {st.capacity} bytes free")
+
+
+@task("ufs.superuser", ("master",), "validate the Alluxio user owns (or may administer) the root UFS")
+def _ufs_superuser(conf):
+    """UfsSuperUserValidationTask: without owning the UFS root, setOwner/chmod of persisted files
+    (and permission sync) fails."""
+    import getpass
+    root = conf.get("alluxio.master.mount.table.root.ufs")
+    try:
+        from ..underfs import registry
+        ufs = registry.create(root, conf)
+        st = ufs.get_status(root)
+    except Exception as e:  # noqa: BLE001
+        return SKIPPED, f"cannot stat root UFS {root}: {e}"
+    if st is None:
+        return SKIPPED, f"root UFS {root} does not exist"
+    me = getpass.getuser()
+    if not st.owner or st.owner == me or me == "root":
+        return OK, f"{me} owns or administers {root}"
+    return WARNING, f"{root} is owned by {st.owner}, not {me}: UFS owner/mode updates may be refused"
+
+
+@task("worker.storage.space", ("worker",), "validate each disk tier directory has room for its quota")
+def _storage_space(conf):
+    """StorageSpaceValidationTask: the sum of a tier's quotas on one filesystem must fit its free space
+    (device tiers are checked by worker.hbm.quota, DRAM tiers by the memory of the host)."""
+    from ..utils.format import parse_space_size
+    problems, checked = [], 0
+    for lvl in range(conf.get_int("alluxio.worker.tieredstore.levels")):
+        paths = (conf.get_raw(f"alluxio.worker.tieredstore.level{lvl}.dirs.path") or "").split(",")
+        quotas = (conf.get_raw(f"alluxio.worker.tieredstore.level{lvl}.dirs.quota") or "").split(",")
+        for i, path in enumerate(p.strip() for p in paths):
+            if not path or path.startswith(("hbm", "dram")) or path == "mem":
+                continue
+            q = parse_space_size(quotas[min(i, len(quotas) - 1)].strip()) if quotas[0].strip() else 0
+            probe = path
+            while probe and not os.path.exists(probe):
+                probe = os.path.dirname(probe.rstrip("/"))
+            if not probe:
+                continue
+            free = shutil.disk_usage(probe).free
+            checked += 1
+            if q > free:
+                problems.append(f"{path}: quota {q} > free {free}")
+    if problems:
+        return WARNING, "; ".join(problems)
+    return (OK, f"{checked} disk tier dir(s) fit their quotas") if checked else (SKIPPED, "no disk tier dirs")
+
+
 @task("journal.folder.writable", ("master",), "validate the journal folder is writable")
 def _journal(conf):
     folder = conf.get("alluxio.master.journal.folder")

@@ -363,6 +363,11 @@ class MiniDfs:
         el.syncTxid = len(self.edits)
         return out
 
+    def rpc_getServerDefaults(self, b, user):
+        d = hdfs.FsServerDefaultsProto(blockSize=128 << 20, bytesPerChecksum=512, writePacketSize=65536,
+                                       replication=3, fileBufferSize=4096, checksumType=H.CHECKSUM_CRC32C)
+        return hdfs.GetServerDefaultsResponseProto(serverDefaults=d)
+
     def rpc_renewLease(self, b, user):
         return hdfs.RenewLeaseResponseProto()
 
