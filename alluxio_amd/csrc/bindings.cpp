@@ -800,5 +800,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_lz4_decode_variant", &set_lz4_decode_variant, py::arg("variant"));
   m.def("set_lz4_encode_variant", &set_lz4_encode_variant, py::arg("variant"));
   m.def("set_seq_read_variant", &set_seq_read_variant, py::arg("variant"), py::arg("grid_cap") = 0);
+  m.def("set_page_gather_chunk_variant", &set_page_gather_chunk_variant, py::arg("variant"));
   m.attr("COPY_CHUNK") = kCopyChunk;
 }

@@ -209,6 +209,7 @@ hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream
 // Largest page size served by the wave-per-request kernel (bigger pages: workgroup per chunk).
 void set_page_gather_small_max(uint64_t bytes);
 void set_page_gather_wave_variant(int variant);
+void set_page_gather_chunk_variant(int v);
 // Apply table updates (idx, entry) pairs uploaded by the host mirror.
 hipError_t launch_page_table_update(PageTableEntry* table, const uint64_t* idx,
                                     const PageTableEntry* entries, uint32_t n, hipStream_t stream);

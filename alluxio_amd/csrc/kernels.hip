@@ -2573,6 +2573,7 @@ hipError_t launch_fill_pattern(uint8_t* dst, uint64_t bytes, uint64_t seed, uint
 constexpr int kPgThreads = 256;
 constexpr uint64_t kPgChunk = 128 * 1024;
 
+template <int LP>
 __global__ __launch_bounds__(kPgThreads) void page_lookup_gather_kernel(PageGatherArgs a) {
   __shared__ int32_t s_slot;
   __shared__ uint32_t s_len;
@@ -2617,7 +2618,7 @@ __global__ __launch_bounds__(kPgThreads) void page_lookup_gather_kernel(PageGath
       const uint64_t n = rem < kPgChunk ? rem : kPgChunk;
       const uint64_t src = (uint64_t)(a.arena + (uint64_t)slot * a.page_size + chunk0);
       const uint64_t dst = (uint64_t)(a.dst + (uint64_t)req * a.dst_stride + chunk0);
-      copy_range<4, 0, 0>(src, dst, n, tid);
+      copy_range<4, LP, 0>(src, dst, n, tid);
     }
     __syncthreads();      // s_slot is rewritten by the next request of this workgroup
   }
@@ -2633,9 +2634,13 @@ __global__ __launch_bounds__(kPgThreads) void page_lookup_gather_kernel(PageGath
 static uint64_t g_pg_small_max = 16 * 1024;
 void set_page_gather_small_max(uint64_t bytes) { g_pg_small_max = bytes; }
 // Wave-kernel variant (requests per wave, 16-B loads per lane per page, store policy):
-// 0 = 4/4/plain, 1 = 8/2/plain, 2 = 4/4/nontemporal, 3 = 8/4/plain.
+// 0 = 4/4/plain, 1 = 8/2/plain, 2 = 4/4/nontemporal, 3 = 8/4/plain, 4 = 4/4/nontemporal loads,
+// 5 = 4/4/nontemporal loads and stores.
 static int g_pg_wave_variant = 2;  // nt stores: 4 KiB 3.03 vs 2.56 TB/s, 16 KiB 2.64 vs 2.42 TB/s (profiles/r1_page_cache_wave.jsonl)
 void set_page_gather_wave_variant(int v) { g_pg_wave_variant = v; }
+// chunk kernel (pages above g_pg_small_max): 0 = cached loads, 1 = nontemporal loads
+static int g_pg_chunk_variant = 0;
+void set_page_gather_chunk_variant(int v) { g_pg_chunk_variant = v; }
 
 __device__ __forceinline__ void pg_resolve(const PageGatherArgs& a, uint64_t key, uint64_t h,
                                            PageTableEntry e, int lane, int32_t& slot, uint32_t& len) {
@@ -2660,7 +2665,7 @@ __device__ __forceinline__ void pg_resolve(const PageGatherArgs& a, uint64_t key
   }
 }
 
-template <int kPgPW, int kPgUnr, int SP>
+template <int kPgPW, int kPgUnr, int SP, int LP = 0>
 __global__ __launch_bounds__(256) void page_lookup_gather_small_kernel(PageGatherArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -2709,7 +2714,7 @@ __global__ __launch_bounds__(256) void page_lookup_gather_small_kernel(PageGathe
 #pragma unroll
         for (int k = 0; k < kPgUnr; ++k) {
           const uint64_t off = base + (uint64_t)(k * 64 + lane) * 16;
-          if (off + 16 <= len[u]) v[u][k] = *reinterpret_cast<const u32x4*>(src[u] + off);
+          if (off + 16 <= len[u]) v[u][k] = ld16<LP>(reinterpret_cast<const u32x4*>(src[u] + off));
         }
 #pragma unroll
       for (int u = 0; u < kPgPW; ++u)
@@ -2740,6 +2745,8 @@ hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream
       case 1: AMDX_PG(8, 2, 0); break;
       case 2: AMDX_PG(4, 4, 1); break;
       case 3: AMDX_PG(8, 4, 0); break;
+      case 4: hipLaunchKernelGGL((page_lookup_gather_small_kernel<4, 4, 0, 1>), dim3(grid), dim3(256), 0, stream, a); break;
+      case 5: hipLaunchKernelGGL((page_lookup_gather_small_kernel<4, 4, 1, 1>), dim3(grid), dim3(256), 0, stream, a); break;
       default: AMDX_PG(4, 4, 0); break;
     }
 #undef AMDX_PG
@@ -2747,7 +2754,10 @@ hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream
   }
   const unsigned gy = (unsigned)std::max<uint64_t>(1, (a.page_size + kPgChunk - 1) / kPgChunk);
   const unsigned gx = (unsigned)std::min<uint64_t>(a.n, 65535);
-  hipLaunchKernelGGL(page_lookup_gather_kernel, dim3(gx, gy), dim3(kPgThreads), 0, stream, a);
+  if (g_pg_chunk_variant == 1)
+    hipLaunchKernelGGL(page_lookup_gather_kernel<1>, dim3(gx, gy), dim3(kPgThreads), 0, stream, a);
+  else
+    hipLaunchKernelGGL(page_lookup_gather_kernel<0>, dim3(gx, gy), dim3(kPgThreads), 0, stream, a);
   return hipGetLastError();
 }
 

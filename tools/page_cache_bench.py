@@ -50,6 +50,8 @@ def main(argv=None):
                     help="both: time the wave-per-request and the chunked kernel at every page size")
     ap.add_argument("--wave-variants", default="0",
                     help="wave-kernel variants timed with --variants both (see set_page_gather_wave_variant)")
+    ap.add_argument("--chunk-variants", default="0",
+                    help="chunk-kernel variants timed with --variants both (see set_page_gather_chunk_variant)")
     ap.add_argument("--passes", type=int, default=1, help="repeat the whole run list; every pass is reported")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
@@ -63,7 +65,8 @@ def main(argv=None):
     runs = [(parse_space_size(p), None) for p in a.page_sizes.split(",")]
     if a.variants == "both":
         waves = ["wave%s" % w for w in a.wave_variants.split(",")]
-        runs = [(ps, v) for ps, _ in runs for v in waves + ["chunk"]]
+        chunks = ["chunk%s" % c for c in a.chunk_variants.split(",")]
+        runs = [(ps, v) for ps, _ in runs for v in waves + chunks]
     # clocks and caches warm before the first timed case, so case order does not bias the sweep
     warm = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
     warm2 = torch.empty_like(warm)
@@ -73,8 +76,10 @@ def main(argv=None):
     del warm, warm2
     for pas, (ps, variant) in [(p, r) for p in range(a.passes) for r in runs]:
         if variant is not None:
-            C.set_page_gather_small_max(0 if variant == "chunk" else 1 << 40)
-            if variant != "chunk":
+            C.set_page_gather_small_max(0 if variant.startswith("chunk") else 1 << 40)
+            if variant.startswith("chunk"):
+                C.set_page_gather_chunk_variant(int(variant[5:] or 0))
+            else:
                 C.set_page_gather_wave_variant(int(variant[4:]))
         slots = max(1, min(parse_space_size(a.cache) // ps, a.max_pages))
         pc = C.PageCache(0, slots * ps, ps, True)
