@@ -2638,8 +2638,10 @@ void set_page_gather_small_max(uint64_t bytes) { g_pg_small_max = bytes; }
 // 5 = 4/4/nontemporal loads and stores.
 static int g_pg_wave_variant = 2;  // nt stores: 4 KiB 3.03 vs 2.56 TB/s, 16 KiB 2.64 vs 2.42 TB/s (profiles/r1_page_cache_wave.jsonl)
 void set_page_gather_wave_variant(int v) { g_pg_wave_variant = v; }
-// chunk kernel (pages above g_pg_small_max): 0 = cached loads, 1 = nontemporal loads
-static int g_pg_chunk_variant = 0;
+// chunk kernel (pages above g_pg_small_max): 0 = cached loads, 1 = nontemporal loads, -1 (default)
+// = nontemporal loads up to 512 KiB pages (64 KiB pages over an 8 GiB cache: 2.57 -> 2.72 TB/s;
+// 2 MiB pages equal within noise; profiles/r3_page_gather_ntload.jsonl)
+static int g_pg_chunk_variant = -1;
 void set_page_gather_chunk_variant(int v) { g_pg_chunk_variant = v; }
 
 __device__ __forceinline__ void pg_resolve(const PageGatherArgs& a, uint64_t key, uint64_t h,
@@ -2754,7 +2756,7 @@ hipError_t launch_page_lookup_gather(const PageGatherArgs& a, hipStream_t stream
   }
   const unsigned gy = (unsigned)std::max<uint64_t>(1, (a.page_size + kPgChunk - 1) / kPgChunk);
   const unsigned gx = (unsigned)std::min<uint64_t>(a.n, 65535);
-  if (g_pg_chunk_variant == 1)
+  if (g_pg_chunk_variant == 1 || (g_pg_chunk_variant < 0 && a.page_size <= (512u << 10)))
     hipLaunchKernelGGL(page_lookup_gather_kernel<1>, dim3(gx, gy), dim3(kPgThreads), 0, stream, a);
   else
     hipLaunchKernelGGL(page_lookup_gather_kernel<0>, dim3(gx, gy), dim3(kPgThreads), 0, stream, a);
