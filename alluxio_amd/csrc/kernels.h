@@ -52,6 +52,7 @@ struct SeqReadArgs {
   uint32_t streams;
   uint32_t depth;
   uint32_t page_shift;
+  uint64_t footprint = 0;   // distinct file bytes one launch touches (host estimate; 0 = file_len)
 };
 constexpr uint32_t kSeqReadMaxStreams = 8192;
 hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream);

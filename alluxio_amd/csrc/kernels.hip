@@ -202,11 +202,12 @@ __global__ __launch_bounds__(kSeqThreads) void seq_read_kernel(SeqReadArgs a, ui
 }
 
 // 0: cached stores, 1: nontemporal stores, +2: unroll 16, +4: nontemporal loads; -1 (default): auto —
-// nontemporal LOADS once the file is far larger than the 256 MB MALL: its bytes are read exactly
-// once from HBM, so streaming them past L2/MALL leaves the caches to the ring writes (16 GiB
-// staggered read: 2.40 -> 2.87 TB/s delivered = 5.7 TB/s of HBM traffic, above the runtime's own
-// D2D copy at 2.46 TB/s; profiles/r3_ring_tune_large_ntload.json, r3_copy_roof.json); fully
-// cached loads/stores while the file stays cache-resident (the lockstep headline shape)
+// nontemporal LOADS once a launch streams >= 128 MiB of distinct file bytes (half the 256 MB MALL):
+// those bytes are read once, so streaming them past L2/MALL leaves the caches to the ring writes
+// (16 GiB staggered read: 2.40 -> 2.87 TB/s delivered = 5.7 TB/s of HBM traffic, above the
+// runtime's own D2D copy at 2.46 TB/s; staggered 128 MiB: 2.85 -> 2.98 TB/s;
+// profiles/r3_ring_tune_large_ntload.json, r3_ring_tune_128m_ntload.jsonl, r3_copy_roof.json);
+// cached loads while the streams re-read one window (the lockstep headline shape: 5.9 vs 2.8 TB/s)
 static int g_seq_variant = -1;
 static unsigned g_seq_grid_cap = 8192;
 
@@ -229,7 +230,8 @@ hipError_t launch_seq_read(const SeqReadArgs& a, hipStream_t stream) {
     return hipErrorInvalidValue;
   const uint64_t vpr = a.buf >> 4;
   const uint64_t nvec = (uint64_t)a.streams * a.depth * vpr;
-  const int var = g_seq_variant >= 0 ? g_seq_variant : (a.file_len > (1ull << 30) ? 4 : 0);
+  const uint64_t fp = a.footprint ? a.footprint : a.file_len;
+  const int var = g_seq_variant >= 0 ? g_seq_variant : (fp >= (128ull << 20) ? 4 : 0);
   const int unroll = (var & 2) ? 16 : 8;
   uint64_t blocks = (nvec + (uint64_t)kSeqThreads * unroll - 1) / ((uint64_t)kSeqThreads * unroll);
   if (blocks > g_seq_grid_cap) blocks = g_seq_grid_cap;

@@ -97,6 +97,12 @@ void RingReadSession::finish_init(const std::vector<uint64_t>& start_offsets) {
     if (start_offsets[s] % buf_) throw StoreError(kErrInvalidArgument, "ring read: start offsets must be buffer aligned");
     c_init_[s] = std::min<uint64_t>(start_offsets[s] / buf_, cycle_ - 1);
   }
+  // streams that start at distinct calls read distinct bytes each step (lockstep streams re-read
+  // the same depth*buf window): the kernel's cache policy keys on this footprint
+  std::vector<uint64_t> starts(c_init_);
+  std::sort(starts.begin(), starts.end());
+  const uint64_t distinct = (uint64_t)(std::unique(starts.begin(), starts.end()) - starts.begin());
+  footprint_ = std::min<uint64_t>(file_len_, distinct * depth_ * buf_);
   if (on_device_) {
     if (buf_ & 15 || stride_ & 15 || dst_ & 15)
       throw StoreError(kErrInvalidArgument, "ring read: buffer size, stride and ring base must be 16-byte aligned");
@@ -154,6 +160,7 @@ uint64_t RingReadSession::step(uint64_t stream, uint64_t* eofs) {
     a.streams = streams_;
     a.depth = depth_;
     a.page_shift = page_shift_;
+    a.footprint = footprint_;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     RR_HIP(launch_seq_read(a, st));
     if (kind_ == (int)MemKind::kHost) RR_HIP(hipStreamSynchronize(st));

@@ -59,6 +59,7 @@ class RingReadSession {
   uint32_t page_shift_ = 0;
   std::vector<int64_t> ftab_;
   std::vector<uint64_t> c_init_;
+  uint64_t footprint_ = 0;   // distinct file bytes one step touches (see finish_init)
   int64_t* d_ftab_ = nullptr;
   uint64_t* d_cinit_ = nullptr;
   uint64_t calls_per_stream_ = 0, total_ = 0, reopens_ = 0;
