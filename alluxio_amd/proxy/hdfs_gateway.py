@@ -23,6 +23,7 @@ here); the native Hadoop client runs the UFS contract through it in ``tests/test
 """
 from __future__ import annotations
 
+import collections
 import logging
 import posixpath
 import socket
@@ -239,6 +240,26 @@ class _DataHandler(socketserver.BaseRequestHandler):
         bpc = op.requestedChecksum.bytesPerChecksum or H.BYTES_PER_CHECKSUM
         received = 0
         status = H.ST_SUCCESS
+        try:
+            received, status = _DataHandler._receive(s, sink, downstream, bpc)
+        except BaseException:
+            abort = getattr(sink, "abort", None)
+            if abort is not None:
+                abort()               # a block cut off mid-stream must not complete silently
+            raise
+        finally:
+            if downstream is not None:
+                downstream.close()
+        if status == H.ST_SUCCESS:
+            sink.commit(received)
+        else:
+            abort = getattr(sink, "abort", None)
+            if abort is not None:
+                abort()
+
+    @staticmethod
+    def _receive(s, sink, downstream, bpc):
+        received, status = 0, H.ST_SUCCESS
         while True:
             plen, hlen = struct.unpack(">IH", bytes(H.recv_exact(s, 6)))
             hraw = bytes(H.recv_exact(s, hlen))
@@ -265,11 +286,7 @@ class _DataHandler(socketserver.BaseRequestHandler):
             ack.reply.extend(replies)
             s.sendall(H.delimited(ack))
             if hdr.lastPacketInBlock or status != H.ST_SUCCESS:
-                break
-        if downstream is not None:
-            downstream.close()
-        if status == H.ST_SUCCESS:
-            sink.commit(received)
+                return received, status
 
 
 # ---- the Alluxio-backed gateway -------------------------------------------------------------------------
@@ -295,6 +312,7 @@ class _OpenFile:
         self.lock = threading.Lock()
         self.blocks: list = []       # ExtendedBlockProto of the blocks handed out by addBlock
         self.written = 0
+        self.broken = False          # a block stream failed after bytes reached the out stream
 
 
 class _BlockSink:
@@ -308,6 +326,11 @@ class _BlockSink:
 
     def commit(self, n: int) -> None:
         pass
+
+    def abort(self) -> None:
+        # bytes of the failed block may already be in the Alluxio out stream, which cannot take
+        # them back: fail the file at complete() instead of publishing a corrupt one
+        self.of.broken = True
 
 
 class _RangeReader:
@@ -336,7 +359,9 @@ class HdfsGateway:
         self.lock = threading.Lock()
         self.open_files: dict[str, _OpenFile] = {}
         self.write_blocks: dict[int, _OpenFile] = {}
-        self.read_blocks: dict[int, tuple[str, int, int]] = {}   # block id -> (path, file offset, length)
+        # block id -> (path, file offset, length), filled by getBlockLocations; LRU-bounded
+        self.read_blocks: "collections.OrderedDict[int, tuple[str, int, int]]" = collections.OrderedDict()
+        self.read_blocks_cap = 1 << 20
         self.next_block = 1 << 40
         self.data = DataTransferServer(self._open_read, self._open_write, host, data_port)
         self.rpc = IpcServer(self._dispatch, host, rpc_port)
@@ -513,6 +538,13 @@ class HdfsGateway:
             if self.fs.exists(p):
                 return hdfs.CompleteResponseProto(result=True)
             raise file_not_found(p)
+        if of.broken:
+            try:
+                of.stream.cancel() if hasattr(of.stream, "cancel") else of.stream.close()
+                self.fs.delete(p)
+            except Exception:  # noqa: BLE001
+                LOG.debug("cleanup of failed gateway write %s", p, exc_info=True)
+            raise RpcError("java.io.IOException", f"a block of {p} failed mid-stream; the file was discarded")
         try:
             with of.lock:
                 of.stream.close()
@@ -547,6 +579,9 @@ class HdfsGateway:
                 lb.locs.add().CopyFrom(self.data.info(self.adv))
                 with self.lock:
                     self.read_blocks[bi.blockId] = (p, off, bi.length)
+                    self.read_blocks.move_to_end(bi.blockId)
+                    while len(self.read_blocks) > self.read_blocks_cap:
+                        self.read_blocks.popitem(last=False)
             off += bi.length
         return out
 

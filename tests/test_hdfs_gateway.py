@@ -70,3 +70,22 @@ def test_hadoop_client_reads_and_writes_alluxio_files(gw):
     assert ufs.delete_file("/ds/moved") and not fs.exists("/ds/moved")
     with pytest.raises(H.RemoteException, match="RpcNoSuchMethodException"):
         nn.call("getSnapshottableDirListing", H.hdfs.GetFsStatusRequestProto(), H.hdfs.GetFsStatsResponseProto)
+
+
+def test_block_cut_off_mid_stream_fails_the_file(gw):
+    """A WRITE_BLOCK connection that dies mid-block cannot be taken back out of the Alluxio out
+    stream: complete() reports an IOException and the partial file is discarded."""
+    import time
+    g, fs = gw
+    nn = H.NameNodeClient("127.0.0.1", g.port, user="u")
+    st = nn.create("/cut", 0o644, True, True, 1, 1 << 20)
+    lb = nn.add_block("/cut", None, st.fileId)
+    w = H.BlockWriter(lb, nn.client_name)
+    w.write(b"z" * 200_000)
+    w.abort()                                  # connection dropped: no last packet
+    deadline = time.time() + 10
+    while not g.open_files["/cut"].broken and time.time() < deadline:
+        time.sleep(0.02)
+    with pytest.raises(H.RemoteException, match="failed mid-stream"):
+        nn.complete("/cut", None, st.fileId)
+    assert not fs.exists("/cut")
