@@ -352,6 +352,9 @@ def test_webui_spa_and_json(cluster):
     assert 'data-role="worker"' in urllib.request.urlopen(wbase + "/webui", timeout=10).read().decode()
     wo = json.loads(urllib.request.urlopen(wbase + "/api/v1/worker/webui_overview", timeout=10).read())
     assert wo["storageDirs"] and wo["usageOnTiers"]
-    wb = json.loads(urllib.request.urlopen(wbase + "/api/v1/worker/webui_blockinfo", timeout=10).read())
+    # the block lands on whichever worker the write location policy picked
+    infos = [json.loads(urllib.request.urlopen(f"http://127.0.0.1:{x.web_port}/api/v1/worker/webui_blockinfo",
+                                               timeout=10).read()) for x in cluster.workers]
+    wb = max(infos, key=lambda i: i["nTotalFile"])
     assert wb["nTotalFile"] >= 1 and wb["fileBlocksOnTier"][0]["blockLength"] > 0
     fs.close()
