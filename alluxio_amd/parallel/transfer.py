@@ -215,42 +215,85 @@ class TransferPlane:
         for bid, length, owner in blocks:
             by_owner.setdefault(owner, []).append((bid, length))
         moved = 0
+        import torch
+        flag_dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
         with self._collective_lock:
-            members, world, me = self.members, self.world, self.rank
-            rounds = max((len(by_owner.get(r, ())) for r in members), default=0)
-            hops = range(1, copies)
-            for k in range(rounds):
+            k, failed_prev = 0, False
+            while True:
+                members, world, me = self.members, self.world, self.rank
+                rounds = max((len(by_owner.get(r, ())) for r in members), default=0)
+                if k >= rounds:
+                    break
+                # point-to-point rounds fail only on the neighbours of a dead rank: one all-reduce of
+                # the previous round's failure flag at the start of every round (it fails by itself
+                # when a member is gone) makes every survivor rebuild at the same round, before any
+                # of them posts a receive from the dead rank
+                if self.store is not None and self._round_failed_anywhere(failed_prev, flag_dev):
+                    self._rebuild(k)
+                    # the ring's neighbours changed: every round is redone over the new members
+                    # (blocks a rank already holds are skipped when scattering)
+                    k, failed_prev = 0, False
+                    continue
+                failed_prev = False
+                hops = range(1, min(copies, world))
                 entries = [by_owner[r][k] if k < len(by_owner.get(r, ())) else (None, 0) for r in members]
                 shard = max(n for _, n in entries)
-                if shard == 0:
+                if shard == 0 or not hops:
+                    k += 1
                     continue
                 send, out = self._staging(shard)
                 mine = entries[me]
                 if mine[0] is not None:
                     self._copy_block_out(mine[0], mine[1], send)
-                # RCCL: one coalesced group on the group's communicator (ncclGroupStart/End), so no
-                # lazily created per-pair communicator can deadlock the ring; gloo: receives are
-                # posted before sends and every work is waited on
-                coalesce = send.is_cuda
-                if coalesce:
-                    self._pg._start_coalescing(send.device)
-                works = []
-                for h in hops:      # receive slot h-1 <- predecessor me-h
-                    src = (me - h) % world
-                    if entries[src][0] is not None:
-                        works.append(self._pg.recv([out[(h - 1) * shard:h * shard]], src, k))
-                if mine[0] is not None:
-                    for h in hops:
-                        works.append(self._pg.send([send], (me + h) % world, k))
-                if coalesce:
-                    works = [self._pg._end_coalescing(send.device)]
-                for wk in works:
-                    if wk is not None:
-                        wk.wait()
+                try:
+                    self._ring_round(send, out, shard, entries, hops, me, world, k)
+                except Exception:
+                    if self.store is None:
+                        raise
+                    LOG.warning("replicate_ring: round %d failed (gen %d)", k, self.gen, exc_info=True)
+                    failed_prev = True          # redo round k after the group agrees on members
+                    continue
                 slots = [entries[(me - h) % world] for h in hops]
                 moved += self._scatter_into_pages(out, shard, slots, skip_slot=-1)
+                k += 1
         self.bytes_gathered += moved
         return moved
+
+    def _round_failed_anywhere(self, failed: bool, device) -> bool:
+        import torch
+        flag = torch.tensor([1.0 if failed else 0.0], device=device)
+        try:
+            w = self._pg.allreduce([flag])
+            # bounded: a rank whose reduction partner is the dead one must not arrive at the
+            # rebuild long after the others (they only wait rebuild_wait_s for stragglers)
+            if device.type == "cpu":
+                w.wait(timedelta(seconds=max(0.5, self.rebuild_wait_s / 2)))
+            else:
+                w.wait()
+        except Exception:  # noqa: BLE001 - a dead member fails (or stalls) the reduction itself
+            return True
+        return flag.item() > 0
+
+    def _ring_round(self, send, out, shard, entries, hops, me, world, k) -> None:
+        # RCCL: one coalesced group on the group's communicator (ncclGroupStart/End), so no lazily
+        # created per-pair communicator can deadlock the ring; gloo: receives are posted before
+        # sends and every work is waited on
+        coalesce = send.is_cuda
+        if coalesce:
+            self._pg._start_coalescing(send.device)
+        works = []
+        for h in hops:      # receive slot h-1 <- predecessor me-h
+            src = (me - h) % world
+            if entries[src][0] is not None:
+                works.append(self._pg.recv([out[(h - 1) * shard:h * shard]], src, k))
+        if entries[me][0] is not None:
+            for h in hops:
+                works.append(self._pg.send([send], (me + h) % world, k))
+        if coalesce:
+            works = [self._pg._end_coalescing(send.device)]
+        for wk in works:
+            if wk is not None:
+                wk.wait(timedelta(seconds=self.timeout_s)) if not coalesce else wk.wait()
 
     def _rebuild(self, failed_round: int) -> int:
         """Re-form the collective group among the ranks still alive; returns the round to resume
@@ -265,10 +308,17 @@ class TransferPlane:
         pre = f"alluxio/plane/gen{g}/"
         st.set(pre + f"alive/{self.orig_rank}", str(failed_round))
         if st.add(pre + "arrivals", 1) == 1:
-            deadline = time.time() + self.rebuild_wait_s
+            # sliding window: every new arrival extends the wait (stragglers blocked on a dead
+            # peer reach this point a little later), up to 3x rebuild_wait_s in total
+            t0 = time.time()
+            deadline, seen = t0 + self.rebuild_wait_s, 1
             while time.time() < deadline:
                 if all(st.check([pre + f"alive/{r}"]) for r in self.members):
                     break
+                n = st.add(pre + "arrivals", 0)
+                if n > seen:
+                    seen = n
+                    deadline = min(time.time() + self.rebuild_wait_s, t0 + 3 * self.rebuild_wait_s)
                 time.sleep(0.05)
             alive = [r for r in self.members if st.check([pre + f"alive/{r}"])]
             resume = min(int(st.get(pre + f"alive/{r}")) for r in alive)

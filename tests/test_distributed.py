@@ -346,9 +346,13 @@ if rank == world - 1:
         r = orig(*a, **kw)
         os._exit(0)
     plane._scatter_into_pages = dying
-moved = plane.replicate_all(blocks)
+moved = plane.replicate_ring(blocks, 2) if %(method)r == "ring" else plane.replicate_all(blocks)
 alive = [r for r in range(world - 1)]
-have_alive = all(w.worker.has_block(b) for b, _, o in blocks if o in alive)
+if %(method)r == "ring":     # own + ring predecessor (in the rebuilt ring) blocks
+    pred = plane.members[(plane.members.index(rank) - 1) %% len(plane.members)]
+    have_alive = all(w.worker.has_block(b) for b, _, o in blocks if o in (rank, pred))
+else:
+    have_alive = all(w.worker.has_block(b) for b, _, o in blocks if o in alive)
 first_dead = allb[world - 1][0][0]
 print(json.dumps({"rank": rank, "moved": moved, "rebuilds": plane.rebuilds, "members": plane.members,
                   "have_alive": have_alive, "dead_round0": w.worker.has_block(first_dead),
@@ -362,15 +366,19 @@ os._exit(0)
 """
 
 
-def test_replicate_all_rebuilds_group_after_rank_death(tmp_path):
-    """A rank dies in the middle of replicate_all: the survivors' collective fails, they agree on
-    a new group through the rendezvous store and finish replicating among themselves."""
-    script = REBUILD_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path)}
+@pytest.mark.parametrize("method", ["all", "ring"])
+def test_replicate_all_rebuilds_group_after_rank_death(tmp_path, method):
+    """A rank dies in the middle of replicate_all / replicate_ring: the survivors' round fails,
+    they agree on a new group through the rendezvous store and finish replicating among
+    themselves (the ring runs 4 ranks with 2 copies, so only the dead rank's neighbours see the
+    point-to-point failure; the per-round failure all-reduce brings every survivor along)."""
+    world = 4 if method == "ring" else 3
+    script = REBUILD_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path), "method": method}
     path = tmp_path / "rebuild.py"
     path.write_text(script)
     procs = []
-    for rank in range(3):
-        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="3", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
         procs.append(subprocess.Popen([sys.executable, str(path)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
@@ -381,12 +389,14 @@ def test_replicate_all_rebuilds_group_after_rank_death(tmp_path):
             for q in procs:
                 q.kill()
             pytest.fail("rebuild rank timed out")
-        if rank < 2:
+        if rank < world - 1:
             assert p.returncode == 0, err[-3000:]
             outs.append(json.loads(out.strip().splitlines()[-1]))
     for o in outs:
-        assert o["rebuilds"] == 1 and o["members"] == [0, 1], o
-        assert o["have_alive"] and o["dead_round0"] and not o["dead_later"], o
+        assert o["rebuilds"] == 1 and o["members"] == list(range(world - 1)), o
+        assert o["have_alive"] and not o["dead_later"], o
+        if method == "all":
+            assert o["dead_round0"], o
         assert o["moved"] > 0, o
 
 
