@@ -724,10 +724,11 @@ PYBIND11_MODULE(_C, m) {
           if (hip_device_count() > 0) (void)hipHostUnregister(reinterpret_cast<void*>(ptr));
         }, py::arg("ptr"));
   m.def("can_access_peer", &can_access_peer, py::arg("device"), py::arg("peer"));
-  m.def("crc32c", [](py::bytes data, uint32_t crc) {
-          std::string s = data;
+  m.def("crc32c", [](py::buffer data, uint32_t crc) {      // zero-copy over any buffer
+          py::buffer_info bi = data.request();
+          const size_t n = static_cast<size_t>(bi.size) * bi.itemsize;
           py::gil_scoped_release rel;
-          return crc32c_sw(s.data(), s.size(), crc);
+          return crc32c_sw(bi.ptr, n, crc);
         }, py::arg("data"), py::arg("crc") = 0);
   m.def("crc32c_ptr", [](uint64_t ptr, uint64_t n, uint32_t crc) {
           py::gil_scoped_release rel;

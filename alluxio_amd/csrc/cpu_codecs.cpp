@@ -20,7 +20,40 @@ static void init_tables() {
     for (uint32_t i = 0; i < 256; ++i) g_tab[t][i] = (g_tab[t - 1][i] >> 8) ^ g_tab[0][g_tab[t - 1][i] & 0xFF];
 }
 
+#if defined(__x86_64__)
+// The x86 CRC32 instruction computes exactly this polynomial (Castagnoli): 8 bytes per
+// instruction instead of eight table lookups (the HDFS packet checksums, the CPU-side CRC of
+// pulled blocks and the shell's checksum all run here).
+__attribute__((target("sse4.2"))) static uint32_t crc32c_x86(const uint8_t* p, size_t n, uint32_t c) {
+  while (n && (reinterpret_cast<uintptr_t>(p) & 7)) {
+    c = __builtin_ia32_crc32qi(c, *p++);
+    --n;
+  }
+  uint64_t c64 = c;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    c64 = __builtin_ia32_crc32di(c64, v);
+    p += 8;
+    n -= 8;
+  }
+  c = (uint32_t)c64;
+  while (n--) c = __builtin_ia32_crc32qi(c, *p++);
+  return c;
+}
+static bool have_sse42() {
+  static const bool ok = [] {
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("sse4.2") != 0;
+  }();
+  return ok;
+}
+#endif
+
 uint32_t crc32c_sw(const void* data, size_t n, uint32_t crc) {
+#if defined(__x86_64__)
+  if (have_sse42()) return ~crc32c_x86(static_cast<const uint8_t*>(data), n, ~crc);
+#endif
   std::call_once(g_once, init_tables);
   const uint8_t* p = static_cast<const uint8_t*>(data);
   uint32_t c = ~crc;
