@@ -325,9 +325,17 @@ class _IpcConnection:
 
 
 class NameNodeClient:
-    """ClientNamenodeProtocol over a small pool of IPC connections (one call in flight each)."""
+    """ClientNamenodeProtocol over a small pool of IPC connections (one call in flight each).
 
-    def __init__(self, host: str, port: int, user: str | None = None, timeout: float = 60.0):
+    ``addresses`` lists the NameNodes of an HA nameservice (``dfs.ha.namenodes.<ns>`` +
+    ``dfs.namenode.rpc-address.<ns>.<nn>``): a call that hits a standby (``StandbyException``) or
+    an unreachable NameNode fails over to the next one, as ConfiguredFailoverProxyProvider does."""
+
+    def __init__(self, host: str, port: int, user: str | None = None, timeout: float = 60.0,
+                 addresses: list[tuple[str, int]] | None = None):
+        self.addresses = list(addresses) if addresses else [(host, port)]
+        self.active = 0
+        host, port = self.addresses[0]
         self.host, self.port, self.timeout = host, port, timeout
         self.user = user or os.environ.get("HADOOP_USER_NAME") or os.environ.get("USER") or "alluxio"
         self.client_id = uuid.uuid4().bytes
@@ -336,6 +344,29 @@ class NameNodeClient:
         self._lock = threading.Lock()
 
     def call(self, method: str, request, response_cls):
+        tries = len(self.addresses)
+        for attempt in range(tries):
+            try:
+                return self._call_active(method, request, response_cls)
+            except RemoteException as e:
+                if e.short_name != "StandbyException" or attempt == tries - 1:
+                    raise
+                self._failover()
+            except (ConnectionError, OSError) as e:
+                if isinstance(e, RemoteException) or attempt == tries - 1:
+                    raise
+                self._failover()
+        raise IOError("no NameNode available")
+
+    def _failover(self) -> None:
+        with self._lock:
+            conns, self._idle = self._idle, []
+            self.active = (self.active + 1) % len(self.addresses)
+            self.host, self.port = self.addresses[self.active]
+        for c in conns:
+            c.close()
+
+    def _call_active(self, method: str, request, response_cls):
         with self._lock:
             conn = self._idle.pop() if self._idle else None
         if conn is None:

@@ -169,8 +169,19 @@ class HdfsUnderFileSystem(UnderFileSystem):
         self.timeout = float(prop("alluxio.underfs.hdfs.timeout.s", 60.0))
         self.block_size = _size(prop("dfs.blocksize"), 128 << 20)
         self.replication = int(prop("dfs.replication", 3))
+        # HA nameservice: hdfs://<ns>/ with dfs.ha.namenodes.<ns> = nn1,nn2 and
+        # dfs.namenode.rpc-address.<ns>.<nn> = host:port (hdfs-site.xml keys, passed as properties)
+        addrs = None
+        nns = prop(f"dfs.ha.namenodes.{u.hostname}") if u.hostname and u.port is None else None
+        if nns:
+            addrs = []
+            for nn in (x.strip() for x in str(nns).split(",") if x.strip()):
+                hp = prop(f"dfs.namenode.rpc-address.{u.hostname}.{nn}")
+                if hp:
+                    h, _, p_ = str(hp).rpartition(":")
+                    addrs.append((h, int(p_)))
         self.nn = NameNodeClient(self.host, self.port, prop("alluxio.underfs.hdfs.user")
-                                 or prop("hadoop.user.name"), self.timeout)
+                                 or prop("hadoop.user.name"), self.timeout, addresses=addrs or None)
 
     def close(self):
         self.nn.close()

@@ -247,3 +247,29 @@ def test_hdfs_acls_roundtrip_and_master_propagation(dfs, tmp_path):
         acl2, _ = ufs.get_acl_pair("/acl/g")
         assert acl2.named_users == {"bob": 6}
         fs.unmount("/h")
+
+
+def test_ha_nameservice_fails_over_from_standby(dfs):
+    """hdfs://<nameservice>/ with two NameNodes: calls to the standby (StandbyException) and to a
+    dead address fail over to the active one (ConfiguredFailoverProxyProvider semantics)."""
+    from alluxio_amd.proxy.hdfs_gateway import IpcServer, RpcError
+
+    def standby(method, body, user):
+        raise RpcError("org.apache.hadoop.ipc.StandbyException",
+                       "Operation category READ is not supported in state standby")
+    sb = IpcServer(standby)
+    try:
+        props = {"dfs.ha.namenodes.mycluster": "nn1,nn2,nn3",
+                 "dfs.namenode.rpc-address.mycluster.nn1": f"127.0.0.1:{sb.port}",
+                 "dfs.namenode.rpc-address.mycluster.nn2": "127.0.0.1:1",          # nothing listens
+                 "dfs.namenode.rpc-address.mycluster.nn3": f"127.0.0.1:{dfs.port}",
+                 "dfs.blocksize": "256k", "dfs.replication": "1"}
+        ufs = create_ufs("hdfs://mycluster/", properties=props)
+        assert ufs.mkdirs("/ha/d")
+        with ufs.create("/ha/d/f") as f:
+            f.write(b"ha" * 1000)
+        with ufs.open("/ha/d/f") as f:
+            assert f.read() == b"ha" * 1000
+        assert ufs.nn.active == 2 and ufs.nn.port == dfs.port
+    finally:
+        sb.stop()
