@@ -589,9 +589,11 @@ class BlockReader:
         self.pending = memoryview(b"")
         self.done = False
 
-    def read(self, n: int) -> bytes:
-        out = bytearray()
-        while len(out) < n and self.remaining > 0:
+    def readinto(self, buf) -> int:
+        """Copy up to len(buf) bytes straight into ``buf`` (one copy out of the packet buffer)."""
+        mv = memoryview(buf).cast("B")
+        got = 0
+        while got < len(mv) and self.remaining > 0:
             if not len(self.pending):
                 if self.done:
                     break
@@ -603,13 +605,19 @@ class BlockReader:
                     data, self.skip = data[k:], self.skip - k
                 self.pending = data
                 continue
-            k = min(n - len(out), len(self.pending), self.remaining)
-            out += self.pending[:k]
+            k = min(len(mv) - got, len(self.pending), self.remaining)
+            mv[got:got + k] = self.pending[:k]
             self.pending = self.pending[k:]
             self.remaining -= k
+            got += k
         if self.remaining == 0:
             self.close(ok=True)
-        return bytes(out)
+        return got
+
+    def read(self, n: int) -> bytes:
+        out = bytearray(min(n, self.remaining))
+        k = self.readinto(out)
+        return bytes(out[:k])
 
     def close(self, ok: bool = False) -> None:
         s = getattr(self, "sock", None)

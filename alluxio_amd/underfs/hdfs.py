@@ -133,9 +133,7 @@ class _HdfsReader(io.RawIOBase):
             off = self.pos - lb.offset
             self.reader = BlockReader(lb, off, lb.b.numBytes - off, self.ufs.nn.client_name, self.ufs.timeout)
             self.reader_pos = self.pos
-        data = self.reader.read(len(b))
-        n = len(data)
-        b[:n] = data
+        n = self.reader.readinto(b)
         self.pos += n
         self.reader_pos = self.pos
         if self.reader.remaining == 0:
