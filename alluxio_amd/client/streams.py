@@ -10,6 +10,13 @@ local -> remote -> UFS via policy; replicated out streams :281-339), block/strea
 Readers fill caller buffers: ``bytes`` / ``bytearray`` / numpy / torch tensors.  When the
 block's worker lives in this process and the destination is a device tensor, the copy is one
 page-gather kernel launch from HBM pages into the tensor (no host round trip).
+
+Host reads (``readinto`` / ``read``) go through the native chunk-buffered reader
+(``_C.HostInStream``, csrc/block_source.cpp; the LocalFileDataReader analogue of
+LocalFileDataReader.java:58-70): each block reader hands it a native *source* -- the in-process
+store, a HIP-IPC-mapped HBM arena (chunks DMA'd D2H into a pinned buffer), a shared DRAM arena, or
+a native gRPC ReadBlock stream to the worker's data port -- and a ``read(buf)`` inside the current
+chunk is a memcpy with no Python frame, device tensor or RPC per call.
 """
 from __future__ import annotations
 
@@ -62,6 +69,11 @@ class BlockReader:
         self.read_into(offset, length, out.ctypes.data, HOST)
         return out.tobytes()
 
+    def native_source(self):
+        """A ``_C.BlockSource`` over this block for the native host reader, or None (the reader
+        then calls :meth:`read_into` through ``_C.PySource``)."""
+        return None
+
     def close(self) -> None:
         pass
 
@@ -81,6 +93,13 @@ class LocalBlockReader(BlockReader):
 
     def read_into(self, offset, length, ptr, kind, stream=0):
         self.w.read(self.block_id, offset, length, ptr, kind, stream, sync=True)
+
+    def native_source(self):
+        from ..ops.native import lib
+        C = lib()
+        info = self.w.native.block_info(self.block_id)
+        device = self.w.native.dir_spec(info.dir).kind == C.DirKind.DEVICE
+        return C.StoreSource(self.w.native, self.block_id, self.length, device)
 
     def close(self):
         if self.lock_id is not None:
@@ -117,9 +136,11 @@ class GrpcBlockReader(BlockReader):
     source = "remote"
 
     def __init__(self, ctx: FileSystemContext, address: str, block_id: int, length: int, ufs_opts=None,
-                 chunk: int | None = None, promote: bool = False):
+                 chunk: int | None = None, promote: bool = False, data_address: tuple | None = None):
         self.ctx = ctx
         self.address = address
+        # (host, port) of the worker's data server (WorkerNetAddress.dataPort)
+        self.data_address = data_address
         self.block_id = block_id
         self.length = length
         self.ufs_opts = ufs_opts
@@ -181,6 +202,30 @@ class GrpcBlockReader(BlockReader):
         if len(data) != length:
             raise UnavailableException(f"short read of block {self.block_id}: {len(data)}/{length}")
         _copy_bytes_to(data, ptr, kind)
+
+    def native_source(self):
+        """The same ReadBlock call made by the native gRPC client (HTTP/2 with libnghttp2, frames
+        parsed straight into the reader's buffer; csrc/block_source.cpp) against the data port."""
+        conf = self.ctx.conf
+        if not conf.get_bool("alluxio.user.native.reader.enabled", "true"):
+            return None
+        from ..ops.native import lib
+        if not lib().FrameRpcServer.grpc_available():
+            return None
+        host, port = self.data_address or tuple(self.address.rsplit(":", 1))
+        ch = self.ctx.worker_channel(self.address)
+        if ch.is_local:
+            return None                   # in-process servicer: no socket to skip
+        cid = ""
+        if ch.auth is not None:
+            ch._channel()                 # SASL handshake once per channel; its id authorizes the call
+            cid = ch.channel_id or ""
+        ufs = self.ufs_opts.SerializeToString() if self.ufs_opts is not None else b""
+        timeout = int(conf.get_ms("alluxio.user.streaming.data.timeout", "30sec"))
+        from ..rpc import domain_socket_for
+        uds = domain_socket_for(self.address) or ""      # a same-node worker's domain socket
+        return lib().GrpcBlockSource(host, int(port), self.block_id, self.length, self.chunk, ufs, self.promote,
+                                     cid, ch.user or "", timeout, uds)
 
     def _close_stream(self):
         if self._reqs is not None:
@@ -252,6 +297,18 @@ class IpcBlockReader(BlockReader):
         host = tmp.cpu()
         ctypes.memmove(ptr, host.data_ptr(), length)
 
+    def native_source(self):
+        from ..ops.native import has_gpu, lib
+        from ..parallel.ipc import map_handle
+        C = lib()
+        if self.h.arena_kind == "dram":
+            return C.HostArenaSource(map_handle(self.h, self.device), list(self.h.pages), self.h.page_size,
+                                     self.h.length)
+        if not has_gpu():
+            return None
+        return C.DeviceArenaSource(map_handle(self.h, self.device), list(self.h.pages), self.h.page_size,
+                                   self.h.length, self.device)
+
     def close(self):
         if self.h is not None:
             try:
@@ -260,6 +317,20 @@ class IpcBlockReader(BlockReader):
             except Exception:  # noqa: BLE001
                 LOG.debug("unlock of device block %d failed", self.block_id, exc_info=True)
             self.h = None
+
+
+def _native_opener(stream: "FileInStream"):
+    """opener(idx, failed) for ``_C.HostInStream`` holding only a weak reference to the stream
+    (the native object must not keep its FileInStream alive)."""
+    import weakref
+    ref = weakref.ref(stream)
+
+    def opener(idx: int, failed: bool):
+        s = ref()
+        if s is None:
+            raise ValueError("I/O operation on closed file")
+        return s._open_native(idx, failed)
+    return opener
 
 
 def _copy_bytes_to(data: bytes, ptr: int, kind: int) -> None:
@@ -287,13 +358,23 @@ class FileInStream(io.RawIOBase):
         self.read_type = read_type
         self.length = status.length
         self.block_size = status.blockSizeBytes or (64 << 20)
-        self.pos = 0
+        self._pos = 0
         self.session = ids.create_session_id()
         self._reader: BlockReader | None = None
         self._reader_idx = -1
         self._failed: dict[str, int] = {}
         self.passive_cache = ctx.conf.get_bool("alluxio.user.file.passive.cache.enabled")
         self.bytes_read = 0
+        # native host reader (see module docstring): owns the position while it is active
+        self._nat = None
+        self._nreader: BlockReader | None = None
+        if self.length > 0 and ctx.conf.get_bool("alluxio.user.native.reader.enabled", "true"):
+            from ..ops.native import lib
+            self._nat = lib().HostInStream(self.length, self.block_size,
+                                           ctx.conf.get_bytes("alluxio.user.native.reader.buffer.size", "1MB"),
+                                           _native_opener(self))
+            # instance attribute: read(buf) loops call the C entry point directly
+            self.readinto = self._nat.fast_readinto
 
     # ---- io.RawIOBase -------------------------------------------------------------------------
     def readable(self):
@@ -301,6 +382,17 @@ class FileInStream(io.RawIOBase):
 
     def seekable(self):
         return True
+
+    @property
+    def pos(self) -> int:
+        return self._nat.pos if self._nat is not None else self._pos
+
+    @pos.setter
+    def pos(self, v: int) -> None:
+        if self._nat is not None:
+            self._nat.pos = v
+        else:
+            self._pos = v
 
     def tell(self):
         return self.pos
@@ -328,6 +420,8 @@ class FileInStream(io.RawIOBase):
         size = min(size, self.length - self.pos)
         if size <= 0:
             return b""
+        if self._nat is not None:
+            return self._nat.read(size)
         out = np.empty(size, dtype=np.uint8)
         self._read_range(self.pos, size, out.ctypes.data, HOST)
         self.pos += size
@@ -343,6 +437,8 @@ class FileInStream(io.RawIOBase):
         n = min(cap if nbytes is None else nbytes, self.length - self.pos)
         if n <= 0:
             return 0
+        if kind == HOST and self._nat is not None:
+            return self._nat.read_ptr(ptr, n)
         self._read_range(self.pos, n, ptr, kind, stream)
         self.pos += n
         return n
@@ -409,7 +505,9 @@ class FileInStream(io.RawIOBase):
             if self.ctx.is_local(l.workerAddress):
                 self.ctx._note_domain_socket(l.workerAddress)
             try:
-                r = GrpcBlockReader(self.ctx, addr, bi.blockId, block_len)
+                r = GrpcBlockReader(self.ctx, addr, bi.blockId, block_len,
+                                    data_address=(l.workerAddress.host,
+                                                  l.workerAddress.dataPort or l.workerAddress.rpcPort))
                 self._maybe_passive_cache(bi.blockId, l.workerAddress, block_len)
                 return r
             except Exception as e:  # noqa: BLE001
@@ -437,7 +535,8 @@ class FileInStream(io.RawIOBase):
                     lw.cache_block_from_ufs(bi.blockId, opts, self.session)
                     self.ctx.metrics.counter("BytesReadUfs").inc(block_len)
                     return LocalBlockReader(lw, bi.blockId, self.session)
-                return GrpcBlockReader(self.ctx, worker_address_str(w.address), bi.blockId, block_len, ufs_opts=opts)
+                return GrpcBlockReader(self.ctx, worker_address_str(w.address), bi.blockId, block_len, ufs_opts=opts,
+                                       data_address=(w.address.host, w.address.dataPort or w.address.rpcPort))
         raise UnavailableException(f"Block {bi.blockId} of {self.status.path} is not available "
                                    f"(no live location{'' if self.status.persisted else ', not persisted'})"
                                    + (f": {last_err}" if last_err else ""))
@@ -461,6 +560,33 @@ class FileInStream(io.RawIOBase):
                     LOG.debug("passive cache request failed", exc_info=True)
                 return
 
+    def _open_native(self, idx: int, failed: bool):
+        """Source of block ``idx`` for the native reader (``failed``: its previous source broke,
+        so that worker is skipped like a failed location of the Python path)."""
+        if failed and self._nreader is not None:
+            addr = getattr(self._nreader, "address", None)
+            if addr:
+                self._failed[addr] = 1
+        self._close_nreader()
+        reader = self._open_block(self.status.fileBlockInfos[idx], idx)
+        self._nreader = reader
+        src = None
+        try:
+            src = reader.native_source()
+        except Exception:  # noqa: BLE001 - e.g. no data port: the Python reader serves the bytes
+            LOG.debug("native source of block %d unavailable", idx, exc_info=True)
+        if src is None:
+            from ..ops.native import lib
+            src = lib().PySource(reader, reader.length)
+        return src
+
+    def _close_nreader(self) -> None:
+        if self._nreader is not None:
+            try:
+                self._nreader.close()
+            finally:
+                self._nreader = None
+
     def _close_reader(self) -> None:
         if self._reader is not None:
             try:
@@ -472,8 +598,17 @@ class FileInStream(io.RawIOBase):
     def close(self) -> None:
         if not self.closed:
             self._close_reader()
-            for l in []:
-                pass
+            if self._nat is not None:
+                n = self._nat.bytes_read
+                if n:
+                    self.bytes_read += n
+                    self.ctx.metrics.counter("BytesReadClient").inc(n)
+                pos = self._nat.pos
+                self._nat.close()
+                self.__dict__.pop("readinto", None)
+                self._nat = None
+                self._pos = pos
+            self._close_nreader()
         super().close()
 
 

@@ -198,6 +198,23 @@ _k("WORKER_HBM_DEVICE_ALLOC_ENABLED", "alluxio.worker.hbm.device.alloc.enabled",
    "single small creates stay on the host scan (below alloc.min.pages).")
 _k("WORKER_HBM_DEVICE_ALLOC_MIN_PAGES", "alluxio.worker.hbm.device.alloc.min.pages", "1024", Scope.WORKER,
    "Smallest bulk create (in pages) that uses the device allocator when it is enabled.")
+_k("WORKER_DATA_SERVER_NATIVE_ENABLED", "alluxio.worker.data.server.native.enabled", "true", Scope.WORKER,
+   "Serve the BlockWorker service on a native HTTP/2 gRPC data port (csrc/data_server.cpp): ReadBlock "
+   "of a block in the store is streamed from C++ I/O threads (HBM chunks DMA'd into pinned staging), "
+   "other calls are bridged to the Python servicer.  Advertised as WorkerNetAddress.dataPort.")
+_k("WORKER_DATA_SERVER_NATIVE_PORT", "alluxio.worker.data.server.native.port", "0", Scope.WORKER,
+   "Port of the native data server (0: any free port; the worker advertises it when registering).")
+_k("WORKER_DATA_SERVER_NATIVE_IO_THREADS", "alluxio.worker.data.server.native.io.threads", "8", Scope.WORKER,
+   "epoll I/O threads of the native data server (each stages and sends the chunks of its connections).")
+_k("WORKER_DATA_SERVER_NATIVE_STREAM_THREADS", "alluxio.worker.data.server.native.stream.threads", "128",
+   Scope.WORKER, "Threads running streaming calls the native data server bridges to Python (writes, UFS "
+   "read-through).")
+_k("USER_NATIVE_READER_ENABLED", "alluxio.user.native.reader.enabled", "true", Scope.CLIENT,
+   "Host reads of FileInStream go through the native chunk-buffered reader (csrc/block_source.cpp): a "
+   "read(buf) inside the buffered chunk is a memcpy; refills come from HIP-IPC HBM (D2H DMA), shared "
+   "DRAM, the in-process store or a native gRPC ReadBlock stream.")
+_k("USER_NATIVE_READER_BUFFER_SIZE", "alluxio.user.native.reader.buffer.size", "1MB", Scope.CLIENT,
+   "Chunk buffer (pinned when a GPU is present) of the native host reader: bytes fetched per refill.")
 _k("USER_READ_BATCH_SIZE", "alluxio.user.read.batch.size", "256", Scope.CLIENT,
    "Max read requests coalesced into one page-gather launch.")
 _k("USER_FILE_READ_DEVICE", "alluxio.user.file.read.device", "cuda", Scope.CLIENT,

@@ -23,6 +23,8 @@
 namespace py = pybind11;
 using namespace amdx;
 
+void bind_data_path(py::module_& m);   // data_path_bind.cpp
+
 namespace {
 
 #define HIP_CHECK(expr)                                                                   \
@@ -698,6 +700,7 @@ PYBIND11_MODULE(_C, m) {
              return py::make_tuple(std::get<0>(r), py::str(std::get<1>(r)), py::bytes(std::get<2>(r)));
            }, py::arg("path"), py::arg("payload"), py::arg("timeout_ms") = 0)
       .def("close", &FrameRpcClient::close, G());
+  bind_data_path(m);
 
   // ---- codecs / kernels ------------------------------------------------------------------
   m.def("device_count", &hip_device_count);

@@ -1,0 +1,162 @@
+// Host-reader data path of the client: where one block's bytes come from, and the chunk-buffered
+// input stream that turns many small read(buf) calls into a few large refills.
+//
+// Reference: core/client/fs/src/main/java/alluxio/client/block/stream/LocalFileDataReader.java:58-70
+// (short-circuit: map the block, hand out chunks of up to 8 MB; a read(buf) is a copy out of the
+// mapping), GrpcDataReader.java (the ReadBlock stream with offset_received acks), BlockInStream
+// and AlluxioFileInStream.java:66-434 (block switching).  StressWorkerBench's reader loop
+// (stress/shell/.../StressWorkerBench.java:251-276) is 4 KiB read(buf) calls on these streams.
+//
+// MI355X design: a HIP-IPC short-circuit block lives in another process's HBM arena, so a chunk
+// (1 MiB default) is DMA'd D2H into a pinned buffer of the stream by one hipMemcpyAsync per page
+// run, and every read(buf) inside it is a memcpy; a shared DRAM arena is read in place; a remote
+// block arrives over a native gRPC (HTTP/2) ReadBlock call whose DATA frames are parsed straight
+// into the destination.  No device tensor, Python bytes object or GIL is involved per read.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "block_store.h"
+
+namespace amdx {
+
+class BlockSource {
+ public:
+  explicit BlockSource(uint64_t length) : length_(length) {}
+  virtual ~BlockSource() = default;
+  // Copies block bytes [off, off + n) into host memory at dst.  Blocking; called without the GIL
+  // unless needs_gil().  Throws std::runtime_error / StoreError.
+  virtual void read(uint64_t off, uint64_t n, uint8_t* dst) = 0;
+  // Reads straight into the caller's buffer are as cheap as refilling the chunk buffer (host
+  // arenas: a memcpy; network streams: the frames are parsed into the destination).
+  virtual bool direct() const { return false; }
+  virtual bool needs_gil() const { return false; }
+  virtual void close() {}
+  uint64_t length() const { return length_; }
+
+ protected:
+  uint64_t length_;
+};
+
+// A block in an HBM arena mapped into this process (HIP IPC of a same-node worker, or the arena of
+// an in-process worker): chunks are DMA'd into pinned host memory.
+class DeviceArenaSource : public BlockSource {
+ public:
+  DeviceArenaSource(uint64_t base, std::vector<int64_t> pages, uint64_t page_size, uint64_t length, int device);
+  void read(uint64_t off, uint64_t n, uint8_t* dst) override;
+
+ private:
+  uint64_t base_;
+  std::vector<int64_t> pages_;
+  uint64_t page_size_;
+  int device_;
+};
+
+// A block in host memory (a shared DRAM arena mapped from another worker process).
+class HostArenaSource : public BlockSource {
+ public:
+  HostArenaSource(uint64_t base, std::vector<int64_t> pages, uint64_t page_size, uint64_t length);
+  void read(uint64_t off, uint64_t n, uint8_t* dst) override;
+  bool direct() const override { return true; }
+
+ private:
+  uint64_t base_;
+  std::vector<int64_t> pages_;
+  uint64_t page_size_;
+};
+
+// A block of a worker in this process, read through its store (the caller holds the block lock).
+class StoreSource : public BlockSource {
+ public:
+  StoreSource(BlockStore* store, int64_t block_id, uint64_t length, bool device_tier);
+  void read(uint64_t off, uint64_t n, uint8_t* dst) override;
+  bool direct() const override { return !device_; }
+
+ private:
+  BlockStore* store_;
+  int64_t block_;
+  bool device_;
+};
+
+// A block streamed from a worker's data port over gRPC: ReadBlock on HTTP/2 (h2c, prior
+// knowledge) with ReadRequest.offset_received acks, spoken directly with libnghttp2.  Works
+// against the native data server and any stock gRPC server of the BlockWorker service.
+class GrpcBlockSource : public BlockSource {
+ public:
+  struct Options {
+    std::string host;
+    int port = 0;
+    std::string unix_path;           // the worker's domain socket (same node): used instead of TCP
+    int64_t block_id = 0;
+    uint64_t chunk = 1u << 20;       // ReadRequest.chunk_size
+    std::string ufs_options;         // serialized OpenUfsBlockOptions ("" = none)
+    bool promote = false;
+    std::string channel_id, user;    // call headers (SASL channel / NOSASL user)
+    int timeout_ms = 60000;
+  };
+  GrpcBlockSource(Options o, uint64_t length);
+  ~GrpcBlockSource() override;
+  void read(uint64_t off, uint64_t n, uint8_t* dst) override;
+  bool direct() const override { return true; }
+  void close() override;
+  struct Conn;
+
+ private:
+  void open(uint64_t off);
+  void maybe_ack(uint64_t offset);
+  Options o_;
+  std::unique_ptr<Conn> c_;
+};
+
+// Pinned (device-mapped) host buffer for a chunk buffer (pooled by size; malloc without a GPU).
+uint8_t* host_buffer_alloc(uint64_t n, bool* pinned);
+
+// Sequential reader over a file's blocks with one chunk buffer: read(buf) calls inside the
+// buffered range are a memcpy; a miss refills up to `chunk` bytes from the block's source.  The
+// owner (bindings) supplies sources per block index and holds the GIL rules.
+class HostInStream {
+ public:
+  HostInStream(uint64_t length, uint64_t block_size, uint64_t chunk);
+  ~HostInStream();
+  inline bool fast(uint8_t* dst, uint64_t n) {
+    if (pos_ >= buf_lo_ && pos_ + n <= buf_hi_) {
+      std::memcpy(dst, buf_ + (pos_ - buf_lo_), n);
+      pos_ += n;
+      bytes_ += n;
+      return true;
+    }
+    return false;
+  }
+  // Copies up to n bytes at pos() from the current block's source (which must cover pos());
+  // returns the bytes copied (> 0).  Called without the GIL unless the source needs it.
+  uint64_t read_block_part(uint8_t* dst, uint64_t n);
+  void set_source(int64_t idx, std::shared_ptr<BlockSource> src);
+  void drop_source();
+  void invalidate() { buf_lo_ = buf_hi_ = 0; }
+  int64_t block_index() const { return cur_idx_; }
+  BlockSource* source() const { return cur_.get(); }
+  uint64_t pos() const { return pos_; }
+  void seek(uint64_t p) { pos_ = p > length_ ? length_ : p; }
+  uint64_t length() const { return length_; }
+  uint64_t block_size() const { return block_size_; }
+  uint64_t bytes() const { return bytes_; }
+  uint64_t refills() const { return refills_; }
+
+ private:
+  uint64_t length_, block_size_, chunk_;
+  uint64_t pos_ = 0;
+  uint8_t* buf_ = nullptr;
+  bool pinned_ = false;
+  uint64_t buf_lo_ = 0, buf_hi_ = 0;   // file offsets held by buf_
+  int64_t cur_idx_ = -1;
+  uint64_t cur_start_ = 0;
+  std::shared_ptr<BlockSource> cur_;
+  uint64_t bytes_ = 0, refills_ = 0;
+};
+
+}  // namespace amdx

@@ -1,0 +1,305 @@
+// pybind11 bindings of the host-reader data path: block sources, the chunk-buffered HostInStream
+// (with a raw vectorcall readinto for the per-call hot path) and the native block data server.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstddef>
+
+#include "block_source.h"
+#include "data_server.h"
+#include "frame_rpc.h"
+
+namespace py = pybind11;
+using namespace amdx;
+
+namespace {
+
+PyObject* g_store_error = nullptr;   // alluxio_amd._C.StoreError
+
+void set_store_error(int code, const char* msg) {
+  if (!g_store_error) {
+    PyErr_SetString(PyExc_RuntimeError, msg);
+    return;
+  }
+  PyObject* inst = PyObject_CallFunction(g_store_error, "is", code, msg);
+  if (inst) {
+    PyErr_SetObject(g_store_error, inst);
+    Py_DECREF(inst);
+  }
+}
+
+// A Python BlockReader (UFS streams, fallbacks): read_into(offset, length, ptr, HOST) with the GIL.
+class PySource : public BlockSource {
+ public:
+  PySource(py::object reader, uint64_t length) : BlockSource(length), reader_(std::move(reader)) {}
+  ~PySource() override {
+    py::gil_scoped_acquire g;
+    reader_ = py::object();
+  }
+  void read(uint64_t off, uint64_t n, uint8_t* dst) override {
+    py::gil_scoped_acquire g;
+    reader_.attr("read_into")(off, n, reinterpret_cast<uint64_t>(dst), 0);
+  }
+  bool needs_gil() const override { return true; }
+
+ private:
+  py::object reader_;
+};
+
+// FileInStream's native core: `opener(block_index, failed)` returns the BlockSource of a block
+// (failed=True: the previous source of that block broke; pick another location).
+struct PyInStream {
+  HostInStream s;
+  py::object opener;
+  bool closed = false;
+  PyInStream(uint64_t length, uint64_t block_size, uint64_t chunk, py::object op)
+      : s(length, block_size, chunk), opener(std::move(op)) {}
+
+  void open_block(int64_t idx, bool failed) {
+    py::object src = opener(idx, failed);
+    s.set_source(idx, src.cast<std::shared_ptr<BlockSource>>());
+  }
+
+  // Reads exactly n bytes at pos() (n <= bytes left); the GIL is held on entry.
+  void read(uint8_t* dst, uint64_t n) {
+    if (closed) throw py::value_error("I/O operation on closed file");
+    uint64_t done = 0;
+    int failures = 0;
+    while (done < n) {
+      const int64_t idx = (int64_t)(s.pos() / s.block_size());
+      if (s.block_index() != idx || !s.source()) open_block(idx, false);
+      try {
+        uint64_t got;
+        if (s.source()->needs_gil()) {
+          got = s.read_block_part(dst + done, n - done);
+        } else {
+          py::gil_scoped_release rel;
+          got = s.read_block_part(dst + done, n - done);
+        }
+        done += got;
+        failures = 0;
+      } catch (const StoreError& e) {
+        if (e.code == kErrInvalidArgument || e.code == kErrInvalidState || ++failures > 2) throw;
+        s.drop_source();
+        open_block(idx, true);   // another location of the block, or the UFS
+      } catch (const std::runtime_error& e) {
+        if (++failures > 2) throw StoreError(kErrIo, e.what());
+        s.drop_source();
+        open_block(idx, true);
+      }
+    }
+  }
+
+  uint64_t clamp(uint64_t n) const {
+    const uint64_t left = s.length() - std::min(s.pos(), s.length());
+    return n < left ? n : left;
+  }
+
+  void close() {
+    closed = true;
+    s.drop_source();
+  }
+};
+
+// ---- raw vectorcall readinto: the per-call path of StressWorkerBench's read(buf) loop ---------
+struct FastRead {
+  PyObject_HEAD
+  vectorcallfunc vc;
+  PyInStream* s;
+  PyObject* owner;   // the HostInStream Python object (keeps `s` alive)
+};
+
+PyObject* fast_readinto(PyObject* self, PyObject* const* args, size_t nargsf, PyObject* kwnames) {
+  FastRead* f = reinterpret_cast<FastRead*>(self);
+  if (PyVectorcall_NARGS(nargsf) != 1 || (kwnames && PyTuple_GET_SIZE(kwnames))) {
+    PyErr_SetString(PyExc_TypeError, "readinto(buffer) takes exactly one buffer");
+    return nullptr;
+  }
+  PyInStream& s = *f->s;
+  if (s.closed) {
+    PyErr_SetString(PyExc_ValueError, "I/O operation on closed file");
+    return nullptr;
+  }
+  Py_buffer v;
+  if (PyObject_GetBuffer(args[0], &v, PyBUF_WRITABLE) < 0) return nullptr;
+  const uint64_t n = s.clamp((uint64_t)v.len);
+  if (n == 0 || s.s.fast(static_cast<uint8_t*>(v.buf), n)) {
+    PyBuffer_Release(&v);
+    return PyLong_FromUnsignedLongLong(n);
+  }
+  PyObject* r = nullptr;
+  try {
+    s.read(static_cast<uint8_t*>(v.buf), n);
+    r = PyLong_FromUnsignedLongLong(n);
+  } catch (py::error_already_set& e) {
+    e.restore();
+  } catch (const py::builtin_exception& e) {
+    e.set_error();
+  } catch (const StoreError& e) {
+    set_store_error(e.code, e.what());
+  } catch (const std::exception& e) {
+    set_store_error(kErrIo, e.what());
+  }
+  PyBuffer_Release(&v);
+  return r;
+}
+
+void fast_dealloc(PyObject* self) {
+  Py_XDECREF(reinterpret_cast<FastRead*>(self)->owner);
+  PyObject_Del(self);
+}
+
+PyTypeObject g_fast_type = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+}  // namespace
+
+void bind_data_path(py::module_& m) {
+  g_store_error = m.attr("StoreError").ptr();
+  Py_INCREF(g_store_error);
+
+  g_fast_type.tp_name = "alluxio_amd._C.FastReadInto";
+  g_fast_type.tp_basicsize = sizeof(FastRead);
+  g_fast_type.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_VECTORCALL;
+  g_fast_type.tp_vectorcall_offset = offsetof(FastRead, vc);
+  g_fast_type.tp_call = PyVectorcall_Call;
+  g_fast_type.tp_dealloc = fast_dealloc;
+  g_fast_type.tp_doc = "readinto(buffer) -> bytes read (HostInStream fast path)";
+  if (PyType_Ready(&g_fast_type) < 0) throw py::error_already_set();
+
+  using G = py::call_guard<py::gil_scoped_release>;
+  py::class_<BlockSource, std::shared_ptr<BlockSource>>(m, "BlockSource")
+      .def_property_readonly("length", &BlockSource::length)
+      .def_property_readonly("direct", &BlockSource::direct)
+      .def("read_into", [](BlockSource& s, uint64_t off, uint64_t n, uint64_t ptr) {
+             if (s.needs_gil()) {
+               s.read(off, n, reinterpret_cast<uint8_t*>(ptr));
+               return;
+             }
+             py::gil_scoped_release rel;
+             s.read(off, n, reinterpret_cast<uint8_t*>(ptr));
+           }, py::arg("offset"), py::arg("length"), py::arg("ptr"))
+      .def("close", &BlockSource::close);
+  py::class_<DeviceArenaSource, BlockSource, std::shared_ptr<DeviceArenaSource>>(m, "DeviceArenaSource")
+      .def(py::init<uint64_t, std::vector<int64_t>, uint64_t, uint64_t, int>(), py::arg("base"), py::arg("pages"),
+           py::arg("page_size"), py::arg("length"), py::arg("device"));
+  py::class_<HostArenaSource, BlockSource, std::shared_ptr<HostArenaSource>>(m, "HostArenaSource")
+      .def(py::init<uint64_t, std::vector<int64_t>, uint64_t, uint64_t>(), py::arg("base"), py::arg("pages"),
+           py::arg("page_size"), py::arg("length"));
+  py::class_<StoreSource, BlockSource, std::shared_ptr<StoreSource>>(m, "StoreSource")
+      .def(py::init<BlockStore*, int64_t, uint64_t, bool>(), py::arg("store"), py::arg("block_id"), py::arg("length"),
+           py::arg("device_tier"), py::keep_alive<1, 2>());
+  py::class_<GrpcBlockSource, BlockSource, std::shared_ptr<GrpcBlockSource>>(m, "GrpcBlockSource")
+      .def(py::init([](const std::string& host, int port, int64_t block_id, uint64_t length, uint64_t chunk,
+                       py::bytes ufs_options, bool promote, const std::string& channel_id, const std::string& user,
+                       int timeout_ms, const std::string& unix_path) {
+             GrpcBlockSource::Options o;
+             o.host = host;
+             o.port = port;
+             o.unix_path = unix_path;
+             o.block_id = block_id;
+             o.chunk = chunk ? chunk : (1u << 20);
+             o.ufs_options = ufs_options;
+             o.promote = promote;
+             o.channel_id = channel_id;
+             o.user = user;
+             o.timeout_ms = timeout_ms;
+             py::gil_scoped_release rel;
+             try {
+               return std::make_shared<GrpcBlockSource>(std::move(o), length);
+             } catch (const StoreError&) {
+               throw;
+             } catch (const std::exception& e) {
+               throw StoreError(kErrIo, e.what());
+             }
+           }),
+           py::arg("host"), py::arg("port"), py::arg("block_id"), py::arg("length"), py::arg("chunk") = 1u << 20,
+           py::arg("ufs_options") = py::bytes(), py::arg("promote") = false, py::arg("channel_id") = "",
+           py::arg("user") = "", py::arg("timeout_ms") = 60000, py::arg("unix_path") = "");
+  py::class_<PySource, BlockSource, std::shared_ptr<PySource>>(m, "PySource")
+      .def(py::init<py::object, uint64_t>(), py::arg("reader"), py::arg("length"));
+
+  py::class_<PyInStream>(m, "HostInStream")
+      .def(py::init<uint64_t, uint64_t, uint64_t, py::object>(), py::arg("length"), py::arg("block_size"),
+           py::arg("chunk"), py::arg("opener"))
+      .def_property("pos", [](const PyInStream& s) { return s.s.pos(); },
+                    [](PyInStream& s, uint64_t p) { s.s.seek(p); })
+      .def_property_readonly("length", [](const PyInStream& s) { return s.s.length(); })
+      .def_property_readonly("bytes_read", [](const PyInStream& s) { return s.s.bytes(); })
+      .def_property_readonly("refills", [](const PyInStream& s) { return s.s.refills(); })
+      .def_property_readonly("closed", [](const PyInStream& s) { return s.closed; })
+      .def("readinto", [](PyInStream& s, py::buffer b) {
+             py::buffer_info bi = b.request(true);
+             const uint64_t n = s.clamp((uint64_t)(bi.size * bi.itemsize));
+             if (n && !s.s.fast(static_cast<uint8_t*>(bi.ptr), n)) s.read(static_cast<uint8_t*>(bi.ptr), n);
+             return n;
+           })
+      .def("read_ptr", [](PyInStream& s, uint64_t ptr, uint64_t n) {
+             n = s.clamp(n);
+             if (n && !s.s.fast(reinterpret_cast<uint8_t*>(ptr), n)) s.read(reinterpret_cast<uint8_t*>(ptr), n);
+             return n;
+           }, py::arg("ptr"), py::arg("n"))
+      .def("read", [](PyInStream& s, int64_t size) {
+             const uint64_t n = s.clamp(size < 0 ? UINT64_MAX : (uint64_t)size);
+             PyObject* out = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)n);
+             if (!out) throw py::error_already_set();
+             py::bytes b = py::reinterpret_steal<py::bytes>(out);
+             uint8_t* dst = reinterpret_cast<uint8_t*>(PyBytes_AS_STRING(out));
+             if (n && !s.s.fast(dst, n)) s.read(dst, n);
+             return b;
+           }, py::arg("size") = -1)
+      .def("close", &PyInStream::close)
+      // A callable readinto(buffer) that skips pybind11's dispatcher: FileInStream binds it as
+      // its instance's readinto.
+      .def_property_readonly("fast_readinto", [](py::object self) {
+             FastRead* f = PyObject_New(FastRead, &g_fast_type);
+             if (!f) throw py::error_already_set();
+             f->vc = fast_readinto;
+             f->s = self.cast<PyInStream*>();
+             f->owner = self.ptr();
+             Py_INCREF(f->owner);
+             return py::reinterpret_steal<py::object>(reinterpret_cast<PyObject*>(f));
+           });
+
+  // ---- native data server + streaming bridge of the HTTP/2 front end ------------------------
+  py::class_<DataServerStats, std::shared_ptr<DataServerStats>>(m, "DataServerStats")
+      .def_property_readonly("streams", [](const DataServerStats& s) { return s.streams.load(); })
+      .def_property_readonly("declined", [](const DataServerStats& s) { return s.declined.load(); })
+      .def_property_readonly("bytes", [](const DataServerStats& s) { return s.bytes.load(); })
+      .def_property_readonly("domain_bytes", [](const DataServerStats& s) { return s.domain_bytes.load(); })
+      .def_property_readonly("chunks", [](const DataServerStats& s) { return s.chunks.load(); })
+      .def_property_readonly("staged_bytes", [](const DataServerStats& s) { return s.staged_bytes.load(); });
+  m.def("serve_block_reads", [](FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk,
+                                uint64_t window) {
+          auto stats = std::make_shared<DataServerStats>();
+          serve_block_reads(srv, method, store, max_chunk, window, stats);
+          return stats;
+        }, py::arg("server"), py::arg("method"), py::arg("store"), py::arg("max_chunk"), py::arg("window"),
+        py::keep_alive<1, 3>());
+  m.def("stream_recv", [](FrameRpcServer& srv, uint64_t token, int timeout_ms) -> py::tuple {
+          std::string msg;
+          int rc;
+          {
+            py::gil_scoped_release rel;
+            rc = srv.stream_recv(token, timeout_ms, &msg);
+          }
+          if (rc == 0) return py::make_tuple(rc, py::bytes(msg));
+          return py::make_tuple(rc, py::object(py::none()));
+        }, py::arg("server"), py::arg("token"), py::arg("timeout_ms"));
+  m.def("stream_send", [](FrameRpcServer& srv, uint64_t token, py::buffer msg, int timeout_ms) {
+          py::buffer_info bi = msg.request();
+          std::string m(static_cast<const char*>(bi.ptr), (size_t)(bi.size * bi.itemsize));
+          py::gil_scoped_release rel;
+          return srv.stream_send(token, m, timeout_ms);
+        }, py::arg("server"), py::arg("token"), py::arg("message"), py::arg("timeout_ms") = 60000);
+  m.def("stream_finish", [](FrameRpcServer& srv, uint64_t token, int status, const std::string& msg) {
+          py::gil_scoped_release rel;
+          srv.stream_finish(token, status, msg);
+        }, py::arg("server"), py::arg("token"), py::arg("status"), py::arg("message") = "");
+  m.def("allow_channel", [](FrameRpcServer& srv, const std::string& cid, const std::string& user) {
+          srv.allow_channel(cid, user);
+        });
+  m.def("revoke_channel", [](FrameRpcServer& srv, const std::string& cid) { srv.revoke_channel(cid); });
+  m.def("set_require_channel_auth", [](FrameRpcServer& srv, bool on) { srv.set_require_channel_auth(on); });
+  m.def("set_stream_window", [](FrameRpcServer& srv, uint32_t bytes) { srv.set_stream_window(bytes); });
+  m.def("listen_unix", [](FrameRpcServer& srv, const std::string& path) { srv.listen_unix(path); });
+}

@@ -1,0 +1,304 @@
+// Native block data server (see data_server.h).
+#include "data_server.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "h2_abi.h"
+
+namespace amdx {
+
+namespace {
+
+// Pinned staging buffers for HBM chunks (hipHostMalloc is far too slow to call per stream).
+class StagingPool {
+ public:
+  StagingPool(uint64_t size, bool pinned) : size_(size), pinned_(pinned) {}
+  ~StagingPool() {
+    for (void* p : free_) release(p);
+  }
+  uint8_t* get() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!free_.empty()) {
+        void* p = free_.back();
+        free_.pop_back();
+        return static_cast<uint8_t*>(p);
+      }
+    }
+    void* p = nullptr;
+    if (pinned_) {
+      if (hipHostMalloc(&p, size_, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    }
+    if (!p) p = std::malloc(size_);
+    if (!p) throw StoreError(kErrOutOfSpace, "data server: cannot allocate a staging buffer");
+    std::lock_guard<std::mutex> g(mu_);
+    if (pinned_) pinned_set_.push_back(p);
+    return static_cast<uint8_t*>(p);
+  }
+  void put(uint8_t* p) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (free_.size() < 512) {
+      free_.push_back(p);
+      return;
+    }
+    release(p);
+  }
+  uint64_t size() const { return size_; }
+
+ private:
+  void release(void* p) {
+    bool was_pinned = false;
+    for (auto it = pinned_set_.begin(); it != pinned_set_.end(); ++it)
+      if (*it == p) {
+        was_pinned = true;
+        pinned_set_.erase(it);
+        break;
+      }
+    if (was_pinned) (void)hipHostFree(p);
+    else std::free(p);
+  }
+  uint64_t size_;
+  bool pinned_;
+  std::mutex mu_;
+  std::vector<void*> free_;
+  std::vector<void*> pinned_set_;
+};
+
+// One D2H stream per I/O thread: staging copies of different connections never queue behind
+// each other on a shared stream.
+hipStream_t thread_stream(BlockStore* store) {
+  thread_local hipStream_t st = nullptr;
+  thread_local BlockStore* owner = nullptr;
+  if (owner != store) {
+    store->use_device();
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+    owner = store;
+  }
+  return st;
+}
+
+struct ReadRequestMsg {
+  int64_t block_id = 0;
+  int64_t offset = 0;
+  int64_t length = 0;
+  bool promote = false;
+  int64_t chunk_size = 0;
+  bool has_ufs = false;
+  bool has_ack = false;
+  int64_t offset_received = 0;
+};
+
+// ReadRequest (proto/defs/block.py): block_id=1 offset=2 length=3 promote=4 chunk_size=5
+// open_ufs_block_options=6 offset_received=7 position_short=8.
+bool parse_read_request(const char* data, size_t n, ReadRequestMsg* r) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(data);
+  size_t i = 0;
+  while (i < n) {
+    uint64_t key;
+    if (!h2::get_varint(p, n, &i, &key)) return false;
+    const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (wt == 0) {
+      uint64_t v;
+      if (!h2::get_varint(p, n, &i, &v)) return false;
+      switch (field) {
+        case 1: r->block_id = (int64_t)v; break;
+        case 2: r->offset = (int64_t)v; break;
+        case 3: r->length = (int64_t)v; break;
+        case 4: r->promote = v != 0; break;
+        case 5: r->chunk_size = (int64_t)v; break;
+        case 7: r->has_ack = true; r->offset_received = (int64_t)v; break;
+        default: break;
+      }
+    } else if (wt == 2) {
+      uint64_t len;
+      if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
+      if (field == 6) r->has_ufs = true;
+      i += (size_t)len;
+    } else if (wt == 1) {
+      if (n - i < 8) return false;
+      i += 8;
+    } else if (wt == 5) {
+      if (n - i < 4) return false;
+      i += 4;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+class BlockReadStream : public NativeStream {
+ public:
+  BlockReadStream(BlockStore* store, int64_t session, int64_t lock_id, int64_t block_id, uint64_t pos, uint64_t end,
+                  uint64_t chunk, uint64_t window, bool device, bool unix_peer, std::shared_ptr<StagingPool> pool,
+                  std::shared_ptr<DataServerStats> stats)
+      : store_(store), session_(session), lock_(lock_id), block_(block_id), pos_(pos), acked_(pos), end_(end),
+        chunk_(chunk), window_(window), device_(device), unix_(unix_peer), pool_(std::move(pool)), stats_(std::move(stats)) {}
+
+  ~BlockReadStream() override {
+    if (stage_) pool_->put(stage_);
+    try {
+      store_->unlock(lock_);
+      store_->cleanup_session(session_);
+    } catch (...) {
+    }
+  }
+
+  void on_message(const char* p, size_t n) override {
+    ReadRequestMsg r;
+    if (parse_read_request(p, n, &r) && r.has_ack && (uint64_t)r.offset_received > acked_)
+      acked_ = (uint64_t)r.offset_received;
+  }
+
+  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    size_t w = 0;
+    try {
+      while (w < max) {
+        if (hdr_off_ < hdr_.size()) {   // gRPC prefix + protobuf header of the current chunk
+          const size_t n = std::min(max - w, hdr_.size() - hdr_off_);
+          std::memcpy(dst + w, hdr_.data() + hdr_off_, n);
+          hdr_off_ += n;
+          w += n;
+          continue;
+        }
+        if (left_ > 0) {                // chunk bytes
+          const size_t n = (size_t)std::min<uint64_t>(max - w, left_);
+          if (device_) {
+            std::memcpy(dst + w, stage_ + stage_off_, n);
+            stage_off_ += n;
+          } else {                      // DRAM arena / file tier: straight into the frame
+            std::vector<ReadReq> rq{ReadReq{block_, data_pos_, n, reinterpret_cast<uint64_t>(dst + w),
+                                            (int)MemKind::kHost}};
+            store_->read_batch(rq, 0, false);   // host copies: nothing to wait for on a stream
+            data_pos_ += n;
+          }
+          left_ -= n;
+          w += n;
+          stats_->bytes.fetch_add(n, std::memory_order_relaxed);
+          if (unix_) stats_->domain_bytes.fetch_add(n, std::memory_order_relaxed);
+          continue;
+        }
+        if (pos_ >= end_) {
+          *eof = true;
+          break;
+        }
+        if (pos_ - acked_ >= window_) break;   // wait for offset_received
+        next_chunk();
+      }
+    } catch (const std::exception& e) {
+      *status = 13;   // INTERNAL
+      *msg = std::string("reading block ") + std::to_string(block_) + ": " + e.what();
+      return -1;
+    }
+    return (ssize_t)w;
+  }
+
+ private:
+  void next_chunk() {
+    const uint64_t n = std::min(chunk_, end_ - pos_);
+    hdr_ = h2::read_response_prefix(n);
+    hdr_off_ = 0;
+    left_ = n;
+    data_pos_ = pos_;
+    if (device_) {
+      if (!stage_) stage_ = pool_->get();
+      std::vector<ReadReq> rq{ReadReq{block_, pos_, n, reinterpret_cast<uint64_t>(stage_), (int)MemKind::kHost}};
+      store_->read_batch(rq, reinterpret_cast<uint64_t>(thread_stream(store_)), true);
+      stage_off_ = 0;
+      stats_->staged_bytes.fetch_add(n, std::memory_order_relaxed);
+    }
+    pos_ += n;
+    stats_->chunks.fetch_add(1, std::memory_order_relaxed);
+  }
+
+  BlockStore* store_;
+  int64_t session_, lock_, block_;
+  uint64_t pos_, acked_, end_, chunk_, window_;
+  bool device_, unix_;
+  std::shared_ptr<StagingPool> pool_;
+  std::shared_ptr<DataServerStats> stats_;
+  std::string hdr_;
+  size_t hdr_off_ = 0;
+  uint64_t left_ = 0, data_pos_ = 0;
+  uint8_t* stage_ = nullptr;
+  uint64_t stage_off_ = 0;
+};
+
+std::atomic<int64_t> g_session{(int64_t)1 << 62};   // above the Python range (utils/ids.py)
+
+}  // namespace
+
+void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk, uint64_t window,
+                       std::shared_ptr<DataServerStats> stats) {
+  if (max_chunk == 0) max_chunk = 2u << 20;
+  if (window == 0) window = 4u << 20;
+  auto pool = std::make_shared<StagingPool>(max_chunk, store->has_device());
+  FrameRpcServer* s = &srv;
+  srv.set_native_stream(method, [=](const std::string& first, const std::string& cid, const std::string& user,
+                                    bool unix_peer, int* status, std::string* msg) -> std::unique_ptr<NativeStream> {
+    (void)user;
+    ReadRequestMsg r;
+    if (!parse_read_request(first.data(), first.size(), &r)) {
+      *status = 3;   // INVALID_ARGUMENT
+      *msg = "malformed ReadRequest";
+      return nullptr;
+    }
+    if (s->require_channel_auth() && (cid.empty() || !s->channel_user(cid, nullptr))) {
+      *status = 16;  // UNAUTHENTICATED
+      *msg = cid.empty() ? "channel is not authenticated (no channel-id)"
+                         : "channel " + cid + " is not authenticated";
+      return nullptr;
+    }
+    // UFS read-through, promotion and locks that would wait: the Python servicer
+    if (r.has_ufs || r.promote || r.offset < 0) {
+      stats->declined.fetch_add(1, std::memory_order_relaxed);
+      return nullptr;
+    }
+    const int64_t session = g_session.fetch_add(1);
+    int64_t lock = -1;
+    try {
+      lock = store->lock_block(session, r.block_id, false, 0);
+    } catch (const StoreError& e) {
+      lock = -1;   // not (yet) committed here
+    }
+    if (lock < 0) {
+      stats->declined.fetch_add(1, std::memory_order_relaxed);
+      return nullptr;
+    }
+    try {
+      const BlockInfoOut info = store->block_info(r.block_id);
+      const uint64_t off = (uint64_t)r.offset;
+      if (off > info.length) {
+        store->unlock(lock);
+        *status = 11;  // OUT_OF_RANGE
+        *msg = "offset " + std::to_string(off) + " beyond block " + std::to_string(r.block_id) + " of " +
+               std::to_string(info.length) + " bytes";
+        return nullptr;
+      }
+      const uint64_t end = r.length > 0 ? std::min<uint64_t>(info.length, off + (uint64_t)r.length) : info.length;
+      const uint64_t chunk = r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk) : std::min<uint64_t>(1u << 20, max_chunk);
+      const bool device = store->dir_spec(info.dir).kind == DirKind::kDevice;
+      store->access_block(session, r.block_id);
+      stats->streams.fetch_add(1, std::memory_order_relaxed);
+      return std::unique_ptr<NativeStream>(new BlockReadStream(store, session, lock, r.block_id, off, end, chunk,
+                                                               window, device, unix_peer, pool, stats));
+    } catch (const std::exception& e) {
+      try {
+        store->unlock(lock);
+      } catch (...) {
+      }
+      *status = 13;
+      *msg = e.what();
+      return nullptr;
+    }
+  });
+}
+
+}  // namespace amdx

@@ -1,5 +1,6 @@
 // Native framed-RPC transport (see frame_rpc.h).
 #include "frame_rpc.h"
+#include "h2_abi.h"
 
 #include <arpa/inet.h>
 #include <errno.h>
@@ -10,9 +11,8 @@
 #include <poll.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
+#include <sys/un.h>
 #include <unistd.h>
-
-#include <dlfcn.h>
 
 #include <chrono>
 #include <cstring>
@@ -104,77 +104,6 @@ void set_timeouts(int fd, int timeout_ms) {
   ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
 }
 
-// ---- libnghttp2 (HTTP/2 framing for the gRPC connections) -----------------------------------
-// The image ships the runtime library without headers: the entry points used below are declared
-// from its stable C ABI and resolved with dlopen (no library -> gRPC connections are refused).
-struct NgNv {
-  uint8_t* name;
-  uint8_t* value;
-  size_t namelen;
-  size_t valuelen;
-  uint8_t flags;
-};
-struct NgFrameHd {   // the first member of every nghttp2_frame variant
-  size_t length;
-  int32_t stream_id;
-  uint8_t type;
-  uint8_t flags;
-  uint8_t reserved;
-};
-union NgDataSource {
-  int fd;
-  void* ptr;
-};
-typedef ssize_t (*NgReadCb)(void* session, int32_t stream_id, uint8_t* buf, size_t length, uint32_t* data_flags,
-                            NgDataSource* source, void* user_data);
-struct NgDataProvider {
-  NgDataSource source;
-  NgReadCb read_callback;
-};
-struct NgSettingsEntry {
-  int32_t settings_id;
-  uint32_t value;
-};
-typedef int (*NgFrameCb)(void* session, const void* frame, void* user_data);
-typedef int (*NgDataChunkCb)(void* session, uint8_t flags, int32_t stream_id, const uint8_t* data, size_t len,
-                             void* user_data);
-typedef int (*NgCloseCb)(void* session, int32_t stream_id, uint32_t error_code, void* user_data);
-typedef int (*NgHeaderCb)(void* session, const void* frame, const uint8_t* name, size_t namelen,
-                          const uint8_t* value, size_t valuelen, uint8_t flags, void* user_data);
-constexpr uint8_t kNgFlagEndStream = 0x01;
-constexpr uint32_t kNgDataEof = 0x01, kNgDataNoEndStream = 0x02;
-constexpr uint8_t kNgTypeData = 0, kNgTypeHeaders = 1;
-const char kH2Preface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
-
-struct Ng {
-  bool ok = false;
-  int (*callbacks_new)(void**) = nullptr;
-  void (*set_on_frame_recv)(void*, NgFrameCb) = nullptr;
-  void (*set_on_begin_headers)(void*, NgFrameCb) = nullptr;
-  void (*set_on_data_chunk_recv)(void*, NgDataChunkCb) = nullptr;
-  void (*set_on_stream_close)(void*, NgCloseCb) = nullptr;
-  void (*set_on_header)(void*, NgHeaderCb) = nullptr;
-  int (*server_new)(void**, const void*, void*) = nullptr;
-  void (*session_del)(void*) = nullptr;
-  ssize_t (*mem_recv)(void*, const uint8_t*, size_t) = nullptr;
-  ssize_t (*mem_send)(void*, const uint8_t**) = nullptr;
-  int (*submit_settings)(void*, uint8_t, const NgSettingsEntry*, size_t) = nullptr;
-  int (*submit_response)(void*, int32_t, const NgNv*, size_t, const NgDataProvider*) = nullptr;
-  int (*submit_trailer)(void*, int32_t, const NgNv*, size_t) = nullptr;
-  void* cbs = nullptr;   // one callbacks object shared by every session
-};
-
-// name/value must outlive the submit call (nghttp2 copies them there): literals or named strings
-NgNv nv(const char* n, const char* v) {
-  return NgNv{reinterpret_cast<uint8_t*>(const_cast<char*>(n)), reinterpret_cast<uint8_t*>(const_cast<char*>(v)),
-              std::strlen(n), std::strlen(v), 0};
-}
-NgNv nv(const char* n, const std::string& v) {
-  return NgNv{reinterpret_cast<uint8_t*>(const_cast<char*>(n)),
-              reinterpret_cast<uint8_t*>(const_cast<char*>(v.data())), std::strlen(n), v.size(), 0};
-}
-NgNv nv(const char* n, std::string&&) = delete;
-
 // grpc-message: percent-encode everything outside printable ASCII, and '%'
 std::string grpc_message(const std::string& m) {
   static const char* hex = "0123456789ABCDEF";
@@ -191,40 +120,65 @@ std::string grpc_message(const std::string& m) {
   return o;
 }
 
-inline void put_be32(std::string& s, uint32_t v) {
-  const char b[4] = {(char)(v >> 24), (char)(v >> 16), (char)(v >> 8), (char)v};
-  s.append(b, 4);
-}
+using h2::put_be32;
+constexpr size_t kOutHighWater = 4u << 20;   // unsent bytes per connection before nghttp2 is paused
+constexpr size_t kBridgeQueued = 4u << 20;   // request bytes queued for Python before the window closes
 
 }  // namespace
 
 // gRPC over HTTP/2 on the framed-RPC port: per-connection nghttp2 server session, driven on the
-// I/O thread (receive) and the responding threads (send), always under the connection's wmu.
+// I/O thread (receive, EPOLLOUT) and the responding threads (send), always under the connection's
+// wmu.  Output is non-blocking: what the socket does not take stays in Conn::out and nghttp2 is not
+// asked for more frames until it drains below kOutHighWater (EPOLLOUT resumes it), so one slow
+// reader never parks an I/O thread.
+
+// A kind-2 call bridged to a Python servicer: request messages queue here for stream_recv.
+struct FrameRpcServer::Bridge {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<std::string, size_t>> inbound;   // (message, bytes it took on the wire)
+  size_t queued = 0;       // wire bytes of `inbound`
+  size_t deferred = 0;     // received bytes whose stream window is returned once Python catches up
+  bool half_closed = false, cancelled = false;
+  uint32_t conn = 0;
+  int32_t sid = 0;
+};
+
 struct FrameRpcServer::H2 {
   struct Stream {
     uint32_t method = UINT32_MAX;
     std::string path, cid, auser, in, out;
     size_t out_off = 0;
-    bool dispatched = false, responded = false;
+    bool dispatched = false, headers_sent = false, finished = false;
+    int fin_status = 0;
+    std::string fin_msg;
+    std::shared_ptr<Bridge> bridge;
+    std::unique_ptr<NativeStream> native;
   };
   struct Session {
     FrameRpcServer* srv = nullptr;
     Conn* conn = nullptr;
     void* ng = nullptr;
     std::unordered_map<int32_t, Stream> streams;
+    size_t consume_conn = 0;                                   // window returns queued during mem_recv
+    std::vector<std::pair<int32_t, size_t>> consume_streams;
     ~Session();
   };
-  static const Ng& lib();
+  static void* callbacks();
   static int on_begin_headers(void*, const void* frame, void* ud);
   static int on_header(void*, const void* frame, const uint8_t* name, size_t namelen, const uint8_t* value,
                        size_t valuelen, uint8_t, void* ud);
   static int on_data(void*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* ud);
   static int on_frame(void*, const void* frame, void* ud);
   static int on_close(void*, int32_t sid, uint32_t, void* ud);
-  static ssize_t read_body(void* session, int32_t sid, uint8_t* buf, size_t length, uint32_t* flags, NgDataSource*,
+  static ssize_t read_body(void* session, int32_t sid, uint8_t* buf, size_t length, uint32_t* flags, h2::DataSource*,
                            void* ud);
+  static void take_messages(Session& S, int32_t sid, Stream& st, bool end_stream);
   static void dispatch(Session& S, int32_t sid, Stream& st, std::string msg);
+  static void start_response(Session& S, int32_t sid, Stream& st);
+  static void fail_locked(Session& S, int32_t sid, Stream& st, int status, const std::string& msg);
   static void respond_locked(Session& S, int32_t sid, int status, const std::string& msg, const std::string& payload);
+  static void apply_consumed(Session& S);
   static bool flush_locked(Session& S);
   static bool start(FrameRpcServer& srv, Conn& c);
 };
@@ -232,6 +186,7 @@ struct FrameRpcServer::H2 {
 struct FrameRpcServer::Conn {
   int fd;
   uint32_t id;
+  int ep = -1;                            // epoll set of the connection's I/O thread
   std::string in;
   size_t in_off = 0;
   std::mutex wmu;
@@ -239,7 +194,11 @@ struct FrameRpcServer::Conn {
   std::string user;
   std::atomic<bool> closed{false};
   int proto = 0;                          // 0 undecided, 1 framed, 2 gRPC/HTTP2
+  bool unix_peer = false;                 // accepted on the Unix domain socket
   std::unique_ptr<H2::Session> h2;
+  std::string out;                        // unsent bytes (gRPC connections), under wmu
+  size_t out_off = 0;
+  bool want_out = false;                  // EPOLLOUT armed
   Conn(int f, uint32_t i) : fd(f), id(i) {}
   ~Conn() {
     h2.reset();
@@ -248,72 +207,63 @@ struct FrameRpcServer::Conn {
 };
 
 FrameRpcServer::H2::Session::~Session() {
-  if (ng) lib().session_del(ng);
+  if (ng) h2::lib().session_del(ng);
 }
 
-const Ng& FrameRpcServer::H2::lib() {
-  static const Ng n = [] {
-    Ng g;
-    void* h = ::dlopen("libnghttp2.so.14", RTLD_NOW | RTLD_LOCAL);
-    if (!h) return g;
-    auto sym = [&](const char* name) { return ::dlsym(h, name); };
-    g.callbacks_new = reinterpret_cast<int (*)(void**)>(sym("nghttp2_session_callbacks_new"));
-    g.set_on_frame_recv = reinterpret_cast<void (*)(void*, NgFrameCb)>(sym("nghttp2_session_callbacks_set_on_frame_recv_callback"));
-    g.set_on_begin_headers = reinterpret_cast<void (*)(void*, NgFrameCb)>(sym("nghttp2_session_callbacks_set_on_begin_headers_callback"));
-    g.set_on_data_chunk_recv = reinterpret_cast<void (*)(void*, NgDataChunkCb)>(sym("nghttp2_session_callbacks_set_on_data_chunk_recv_callback"));
-    g.set_on_stream_close = reinterpret_cast<void (*)(void*, NgCloseCb)>(sym("nghttp2_session_callbacks_set_on_stream_close_callback"));
-    g.set_on_header = reinterpret_cast<void (*)(void*, NgHeaderCb)>(sym("nghttp2_session_callbacks_set_on_header_callback"));
-    g.server_new = reinterpret_cast<int (*)(void**, const void*, void*)>(sym("nghttp2_session_server_new"));
-    g.session_del = reinterpret_cast<void (*)(void*)>(sym("nghttp2_session_del"));
-    g.mem_recv = reinterpret_cast<ssize_t (*)(void*, const uint8_t*, size_t)>(sym("nghttp2_session_mem_recv"));
-    g.mem_send = reinterpret_cast<ssize_t (*)(void*, const uint8_t**)>(sym("nghttp2_session_mem_send"));
-    g.submit_settings = reinterpret_cast<int (*)(void*, uint8_t, const NgSettingsEntry*, size_t)>(sym("nghttp2_submit_settings"));
-    g.submit_response = reinterpret_cast<int (*)(void*, int32_t, const NgNv*, size_t, const NgDataProvider*)>(sym("nghttp2_submit_response"));
-    g.submit_trailer = reinterpret_cast<int (*)(void*, int32_t, const NgNv*, size_t)>(sym("nghttp2_submit_trailer"));
-    if (!g.callbacks_new || !g.set_on_frame_recv || !g.set_on_begin_headers || !g.set_on_data_chunk_recv ||
-        !g.set_on_stream_close || !g.set_on_header || !g.server_new || !g.session_del || !g.mem_recv || !g.mem_send ||
-        !g.submit_settings || !g.submit_response || !g.submit_trailer)
-      return g;
-    if (g.callbacks_new(&g.cbs) != 0) return g;
-    g.set_on_frame_recv(g.cbs, &H2::on_frame);
-    g.set_on_begin_headers(g.cbs, &H2::on_begin_headers);
-    g.set_on_data_chunk_recv(g.cbs, &H2::on_data);
-    g.set_on_stream_close(g.cbs, &H2::on_close);
-    g.set_on_header(g.cbs, &H2::on_header);
-    g.ok = true;
-    return g;
+void* FrameRpcServer::H2::callbacks() {
+  static void* cbs = [] {
+    const h2::Lib& g = h2::lib();
+    void* c = nullptr;
+    if (!g.ok || g.callbacks_new(&c) != 0) return (void*)nullptr;
+    g.set_on_frame_recv(c, &H2::on_frame);
+    g.set_on_begin_headers(c, &H2::on_begin_headers);
+    g.set_on_data_chunk_recv(c, &H2::on_data);
+    g.set_on_stream_close(c, &H2::on_close);
+    g.set_on_header(c, &H2::on_header);
+    g.set_read_length(c, &h2::read_length);
+    return c;
   }();
-  return n;
+  return cbs;
 }
 
-bool FrameRpcServer::grpc_available() { return H2::lib().ok; }
+bool FrameRpcServer::grpc_available() { return H2::callbacks() != nullptr; }
 
 bool FrameRpcServer::H2::start(FrameRpcServer& srv, Conn& c) {
-  const Ng& g = lib();
-  if (!g.ok) return false;
+  const h2::Lib& g = h2::lib();
+  void* cbs = callbacks();
+  if (!cbs) return false;
   auto S = std::make_unique<Session>();
   S->srv = &srv;
   S->conn = &c;
-  if (g.server_new(&S->ng, g.cbs, S.get()) != 0) {
+  // windows are returned by hand: a bridged upload's bytes only once Python has taken them
+  void* opt = nullptr;
+  if (g.option_new(&opt) != 0) return false;
+  g.option_no_auto_window_update(opt, 1);
+  const int rc = g.server_new2(&S->ng, cbs, S.get(), opt);
+  g.option_del(opt);
+  if (rc != 0) {
     S->ng = nullptr;
     return false;
   }
-  const NgSettingsEntry iv[] = {{3 /*MAX_CONCURRENT_STREAMS*/, 1024}, {4 /*INITIAL_WINDOW_SIZE*/, 1u << 20}};
-  g.submit_settings(S->ng, 0, iv, 2);
+  const h2::SettingsEntry iv[] = {{h2::kSettingsMaxConcurrentStreams, 1024},
+                                  {h2::kSettingsInitialWindowSize, srv.stream_window_},
+                                  {h2::kSettingsMaxFrameSize, h2::kMaxFramePayload}};
+  g.submit_settings(S->ng, 0, iv, 3);
+  g.set_local_window_size(S->ng, 0, 0, 64 << 20);   // connection window: many streams in flight
   c.h2 = std::move(S);
   return true;
 }
 
 int FrameRpcServer::H2::on_begin_headers(void*, const void* frame, void* ud) {
-  const NgFrameHd* hd = static_cast<const NgFrameHd*>(frame);
-  if (hd->type == kNgTypeHeaders) static_cast<Session*>(ud)->streams[hd->stream_id];
+  const h2::FrameHd* hd = static_cast<const h2::FrameHd*>(frame);
+  if (hd->type == h2::kTypeHeaders) static_cast<Session*>(ud)->streams[hd->stream_id];
   return 0;
 }
 
 int FrameRpcServer::H2::on_header(void*, const void* frame, const uint8_t* name, size_t namelen, const uint8_t* value,
                                   size_t valuelen, uint8_t, void* ud) {
   Session& S = *static_cast<Session*>(ud);
-  const NgFrameHd* hd = static_cast<const NgFrameHd*>(frame);
+  const h2::FrameHd* hd = static_cast<const h2::FrameHd*>(frame);
   auto it = S.streams.find(hd->stream_id);
   if (it == S.streams.end() || it->second.dispatched) return 0;   // trailers of a request are ignored
   Stream& st = it->second;
@@ -333,62 +283,132 @@ int FrameRpcServer::H2::on_header(void*, const void* frame, const uint8_t* name,
 
 int FrameRpcServer::H2::on_data(void*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* ud) {
   Session& S = *static_cast<Session*>(ud);
+  S.consume_conn += len;
   auto it = S.streams.find(sid);
-  if (it != S.streams.end() && !it->second.dispatched) it->second.in.append(reinterpret_cast<const char*>(data), len);
+  if (it == S.streams.end() || it->second.finished) {
+    S.consume_streams.emplace_back(sid, len);     // unknown / answered call: drop the bytes
+    return 0;
+  }
+  it->second.in.append(reinterpret_cast<const char*>(data), len);
   return 0;
 }
 
 int FrameRpcServer::H2::on_frame(void*, const void* frame, void* ud) {
   Session& S = *static_cast<Session*>(ud);
-  const NgFrameHd* hd = static_cast<const NgFrameHd*>(frame);
-  if (hd->type != kNgTypeData && hd->type != kNgTypeHeaders) return 0;
+  const h2::FrameHd* hd = static_cast<const h2::FrameHd*>(frame);
+  if (hd->type != h2::kTypeData && hd->type != h2::kTypeHeaders) return 0;
   auto it = S.streams.find(hd->stream_id);
   if (it == S.streams.end()) return 0;
-  Stream& st = it->second;
-  if (!st.dispatched && st.in.size() >= 5) {
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(st.in.data());
-    const uint32_t len = ((uint32_t)p[1] << 24) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 8) | p[4];
-    if (p[0] != 0) {
-      st.dispatched = true;
-      respond_locked(S, hd->stream_id, 12 /*UNIMPLEMENTED*/, "compressed gRPC messages are not supported", "");
-    } else if (len > kMaxFrame) {
-      st.dispatched = true;
-      respond_locked(S, hd->stream_id, 8 /*RESOURCE_EXHAUSTED*/, "message too large", "");
-    } else if (st.in.size() >= 5 + (size_t)len) {
-      // one request message per call: unary and server-streaming methods, and the first
-      // message of the SASL handshake stream
-      st.dispatched = true;
-      std::string msg = st.in.substr(5, len);
-      st.in.clear();
-      st.in.shrink_to_fit();
-      dispatch(S, hd->stream_id, st, std::move(msg));
-    }
-  }
-  if ((hd->flags & kNgFlagEndStream) && !st.dispatched) {
-    st.dispatched = true;
-    respond_locked(S, hd->stream_id, 13 /*INTERNAL*/, "request stream ended without a message", "");
-  }
+  take_messages(S, hd->stream_id, it->second, (hd->flags & h2::kFlagEndStream) != 0);
   return 0;
 }
 
+// Complete gRPC messages of a request stream: the first dispatches the call, later ones go to the
+// native stream (acks) or the Python bridge; END_STREAM half-closes a bridged call.
+void FrameRpcServer::H2::take_messages(Session& S, int32_t sid, Stream& st, bool end_stream) {
+  size_t off = 0;
+  while (!st.finished && st.in.size() - off >= 5) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(st.in.data()) + off;
+    const uint32_t len = ((uint32_t)p[1] << 24) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 8) | p[4];
+    if (p[0] != 0) {
+      fail_locked(S, sid, st, 12 /*UNIMPLEMENTED*/, "compressed gRPC messages are not supported");
+      break;
+    }
+    if (len > kMaxFrame) {
+      fail_locked(S, sid, st, 8 /*RESOURCE_EXHAUSTED*/, "message too large");
+      break;
+    }
+    if (st.in.size() - off - 5 < len) break;
+    const size_t wire = 5 + (size_t)len;
+    std::string msg = st.in.substr(off + 5, len);
+    off += wire;
+    if (!st.dispatched) {
+      st.dispatched = true;
+      S.consume_streams.emplace_back(sid, wire);
+      dispatch(S, sid, st, std::move(msg));
+    } else if (st.native) {
+      S.consume_streams.emplace_back(sid, wire);
+      st.native->on_message(msg.data(), msg.size());
+      h2::lib().resume_data(S.ng, sid);     // the message may reopen the window
+    } else if (st.bridge) {
+      Bridge& b = *st.bridge;
+      std::lock_guard<std::mutex> g(b.mu);
+      b.inbound.emplace_back(std::move(msg), wire);
+      b.queued += wire;
+      if (b.queued > kBridgeQueued) b.deferred += wire;     // window returns when Python catches up
+      else S.consume_streams.emplace_back(sid, wire);
+      b.cv.notify_all();
+    } else {
+      S.consume_streams.emplace_back(sid, wire);           // extra message of a unary call
+    }
+  }
+  if (off) st.in.erase(0, off);
+  if (st.finished && !st.in.empty()) {
+    S.consume_streams.emplace_back(sid, st.in.size());
+    st.in.clear();
+  }
+  if (end_stream && !st.finished) {
+    if (!st.dispatched) {
+      st.dispatched = true;
+      fail_locked(S, sid, st, 13 /*INTERNAL*/, "request stream ended without a message");
+    } else if (st.bridge) {
+      std::lock_guard<std::mutex> g(st.bridge->mu);
+      st.bridge->half_closed = true;
+      st.bridge->cv.notify_all();
+    }
+  }
+}
+
 int FrameRpcServer::H2::on_close(void*, int32_t sid, uint32_t, void* ud) {
-  static_cast<Session*>(ud)->streams.erase(sid);
+  Session& S = *static_cast<Session*>(ud);
+  auto it = S.streams.find(sid);
+  if (it == S.streams.end()) return 0;
+  if (it->second.bridge) {
+    Bridge& b = *it->second.bridge;
+    std::lock_guard<std::mutex> g(b.mu);
+    b.cancelled = true;
+    b.cv.notify_all();
+  }
+  S.streams.erase(it);
   return 0;
 }
 
 void FrameRpcServer::H2::dispatch(Session& S, int32_t sid, Stream& st, std::string msg) {
   FrameRpcServer& srv = *S.srv;
   if (st.method == UINT32_MAX) {
-    respond_locked(S, sid, 12 /*UNIMPLEMENTED*/, "unknown method " + st.path, "");
+    fail_locked(S, sid, st, 12 /*UNIMPLEMENTED*/, "unknown method " + st.path);
     return;
+  }
+  srv.requests_.fetch_add(1, std::memory_order_relaxed);
+  srv.grpc_requests_.fetch_add(1, std::memory_order_relaxed);
+  if (st.method < srv.natives_.size() && srv.natives_[st.method]) {
+    int status = 0;
+    std::string err;
+    std::unique_ptr<NativeStream> ns =
+        srv.natives_[st.method](msg, st.cid, st.auser, S.conn->unix_peer, &status, &err);
+    if (ns) {
+      st.native = std::move(ns);
+      start_response(S, sid, st);
+      return;
+    }
+    if (status != 0) {
+      fail_locked(S, sid, st, status, err);
+      return;
+    }
   }
   // the Python side resolves the caller: channel-id (SASL channels) or alluxio-user (NOSASL)
   std::string user = "\x01" + st.cid;
   user.push_back('\0');
   user += st.auser;
-  srv.requests_.fetch_add(1, std::memory_order_relaxed);
-  srv.grpc_requests_.fetch_add(1, std::memory_order_relaxed);
-  if (srv.cacheable_[st.method]) {
+  const uint64_t token = ((uint64_t)S.conn->id << 32) | (uint32_t)sid;
+  if (st.method < srv.kinds_.size() && srv.kinds_[st.method] == 2) {
+    auto b = std::make_shared<Bridge>();
+    b->conn = S.conn->id;
+    b->sid = sid;
+    st.bridge = b;
+    std::lock_guard<std::mutex> g(srv.bridges_mu_);
+    srv.bridges_[token] = b;
+  } else if (srv.cacheable_[st.method]) {
     CachedReply reply;
     if (srv.cache_get(cache_key(st.method, user, msg.data(), msg.size()), &reply)) {
       srv.cache_hits_.fetch_add(1, std::memory_order_relaxed);
@@ -397,7 +417,7 @@ void FrameRpcServer::H2::dispatch(Session& S, int32_t sid, Stream& st, std::stri
     }
   }
   FrameRequest rq;
-  rq.token = ((uint64_t)S.conn->id << 32) | (uint32_t)sid;
+  rq.token = token;
   rq.method = st.method;
   rq.user = std::move(user);
   rq.payload = std::move(msg);
@@ -409,18 +429,44 @@ void FrameRpcServer::H2::dispatch(Session& S, int32_t sid, Stream& st, std::stri
   l.cv.notify_one();
 }
 
+void FrameRpcServer::H2::start_response(Session& S, int32_t sid, Stream& st) {
+  if (st.headers_sent) {
+    h2::lib().resume_data(S.ng, sid);
+    return;
+  }
+  st.headers_sent = true;
+  const h2::Nv nva[] = {h2::nv(":status", "200"), h2::nv("content-type", "application/grpc")};
+  h2::DataProvider dp;
+  dp.source.ptr = &S;
+  dp.read_callback = &H2::read_body;
+  h2::lib().submit_response(S.ng, sid, nva, 2, &dp);
+}
+
+void FrameRpcServer::H2::fail_locked(Session& S, int32_t sid, Stream& st, int status, const std::string& msg) {
+  if (st.finished) return;
+  st.finished = true;
+  st.fin_status = status;
+  st.fin_msg = msg;
+  st.out.clear();
+  st.out_off = 0;
+  if (st.headers_sent) {     // trailers after the data already sent
+    h2::lib().resume_data(S.ng, sid);
+    return;
+  }
+  st.headers_sent = true;    // trailers-only response
+  const std::string code = std::to_string(status), m = grpc_message(msg);
+  const h2::Nv nva[] = {h2::nv(":status", "200"), h2::nv("content-type", "application/grpc"),
+                        h2::nv("grpc-status", code), h2::nv("grpc-message", m)};
+  h2::lib().submit_response(S.ng, sid, nva, 4, nullptr);
+}
+
 void FrameRpcServer::H2::respond_locked(Session& S, int32_t sid, int status, const std::string& msg,
                                         const std::string& payload) {
   auto it = S.streams.find(sid);
-  if (it == S.streams.end() || it->second.responded) return;   // cancelled or answered
+  if (it == S.streams.end() || it->second.finished) return;   // cancelled or answered
   Stream& st = it->second;
-  st.responded = true;
-  const Ng& g = lib();
-  if (status != 0) {   // trailers-only response
-    const std::string code = std::to_string(status), m = grpc_message(msg);
-    const NgNv nva[] = {nv(":status", "200"), nv("content-type", "application/grpc"), nv("grpc-status", code),
-                        nv("grpc-message", m)};
-    g.submit_response(S.ng, sid, nva, 4, nullptr);
+  if (status != 0) {
+    fail_locked(S, sid, st, status, msg);
     return;
   }
   const bool streaming = st.method < S.srv->kinds_.size() && S.srv->kinds_[st.method] == 1;
@@ -443,47 +489,122 @@ void FrameRpcServer::H2::respond_locked(Session& S, int32_t sid, int status, con
   }
   st.out = std::move(body);
   st.out_off = 0;
-  const NgNv nva[] = {nv(":status", "200"), nv("content-type", "application/grpc")};
-  NgDataProvider dp;
-  dp.source.ptr = &S;
-  dp.read_callback = &H2::read_body;
-  g.submit_response(S.ng, sid, nva, 2, &dp);
+  st.finished = true;
+  start_response(S, sid, st);
 }
 
 ssize_t FrameRpcServer::H2::read_body(void* session, int32_t sid, uint8_t* buf, size_t length, uint32_t* flags,
-                                      NgDataSource*, void* ud) {
+                                      h2::DataSource*, void* ud) {
   Session& S = *static_cast<Session*>(ud);
   auto it = S.streams.find(sid);
   if (it == S.streams.end()) {
-    *flags |= kNgDataEof;
+    *flags |= h2::kDataEof;
     return 0;
   }
   Stream& st = it->second;
-  const size_t n = std::min(length, st.out.size() - st.out_off);
-  std::memcpy(buf, st.out.data() + st.out_off, n);
-  st.out_off += n;
-  if (st.out_off == st.out.size()) {
-    *flags |= kNgDataEof | kNgDataNoEndStream;
-    const NgNv t[] = {nv("grpc-status", "0")};
-    lib().submit_trailer(session, sid, t, 1);
-    st.out.clear();
-    st.out.shrink_to_fit();
-    st.out_off = 0;
+  size_t n = 0;
+  if (st.native && !st.finished) {
+    bool eof = false;
+    int status = 0;
+    std::string m;
+    const ssize_t got = st.native->produce(buf, length, &eof, &status, &m);
+    if (got < 0) {
+      st.finished = true;
+      st.fin_status = status ? status : 13;
+      st.fin_msg = m;
+    } else {
+      n = (size_t)got;
+      if (eof) st.finished = true;
+    }
+    if (n == 0 && !st.finished) return h2::kErrDeferred;
+  } else {
+    n = std::min(length, st.out.size() - st.out_off);
+    std::memcpy(buf, st.out.data() + st.out_off, n);
+    st.out_off += n;
+    if (st.out_off == st.out.size()) {
+      st.out.clear();
+      if (st.out.capacity() > (1u << 20)) st.out.shrink_to_fit();
+      st.out_off = 0;
+    }
+    if (n == 0 && !st.finished) return h2::kErrDeferred;
+  }
+  if (st.finished && st.out_off == st.out.size()) {
+    *flags |= h2::kDataEof | h2::kDataNoEndStream;
+    const std::string code = std::to_string(st.fin_status), m = grpc_message(st.fin_msg);
+    if (st.fin_status == 0) {
+      const h2::Nv t[] = {h2::nv("grpc-status", "0")};
+      h2::lib().submit_trailer(session, sid, t, 1);
+    } else {
+      const h2::Nv t[] = {h2::nv("grpc-status", code), h2::nv("grpc-message", m)};
+      h2::lib().submit_trailer(session, sid, t, 2);
+    }
+    st.native.reset();    // release the block lock as soon as the last byte is out
   }
   return (ssize_t)n;
 }
 
+void FrameRpcServer::H2::apply_consumed(Session& S) {
+  const h2::Lib& g = h2::lib();
+  if (S.consume_conn) g.consume_connection(S.ng, S.consume_conn);
+  S.consume_conn = 0;
+  for (auto& kv : S.consume_streams)
+    if (S.streams.count(kv.first)) g.consume_stream(S.ng, kv.first, kv.second);
+  S.consume_streams.clear();
+}
+
+// Sends what nghttp2 has queued without blocking; keeps the rest in Conn::out and arms EPOLLOUT.
 bool FrameRpcServer::H2::flush_locked(Session& S) {
-  const Ng& g = lib();
-  std::string out;
-  for (;;) {
+  const h2::Lib& g = h2::lib();
+  Conn& c = *S.conn;
+  auto send_some = [&](const char* p, size_t n) -> ssize_t {
+    size_t done = 0;
+    while (done < n) {
+      const ssize_t w = ::send(c.fd, p + done, n - done, MSG_NOSIGNAL | MSG_DONTWAIT);
+      if (w > 0) {
+        done += (size_t)w;
+        continue;
+      }
+      if (w < 0 && errno == EINTR) continue;
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+      return -1;
+    }
+    return (ssize_t)done;
+  };
+  if (c.out_off < c.out.size()) {
+    const ssize_t w = send_some(c.out.data() + c.out_off, c.out.size() - c.out_off);
+    if (w < 0) return false;
+    c.out_off += (size_t)w;
+    if (c.out_off == c.out.size()) {
+      c.out.clear();
+      if (c.out.capacity() > (8u << 20)) c.out.shrink_to_fit();
+      c.out_off = 0;
+    }
+  }
+  while (c.out.size() - c.out_off < kOutHighWater) {
     const uint8_t* d = nullptr;
     const ssize_t n = g.mem_send(S.ng, &d);
     if (n < 0) return false;
     if (n == 0) break;
-    out.append(reinterpret_cast<const char*>(d), (size_t)n);
+    if (c.out_off == c.out.size()) {
+      const ssize_t w = send_some(reinterpret_cast<const char*>(d), (size_t)n);
+      if (w < 0) return false;
+      if (w < n) {
+        c.out.assign(reinterpret_cast<const char*>(d) + w, (size_t)(n - w));
+        c.out_off = 0;
+      }
+    } else {
+      c.out.append(reinterpret_cast<const char*>(d), (size_t)n);
+    }
   }
-  return out.empty() || send_all(S.conn->fd, out.data(), out.size(), 30000);
+  const bool pending = c.out_off < c.out.size();
+  if (pending != c.want_out && c.ep >= 0) {
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLRDHUP | (pending ? EPOLLOUT : 0u);
+    ev.data.u64 = c.id;
+    ::epoll_ctl(c.ep, EPOLL_CTL_MOD, c.fd, &ev);
+    c.want_out = pending;
+  }
+  return true;
 }
 
 FrameRpcServer::FrameRpcServer(const std::string& host, int port, const std::vector<std::string>& methods,
@@ -498,6 +619,149 @@ FrameRpcServer::FrameRpcServer(const std::string& host, int port, const std::vec
   for (int i = 0; i < nl; ++i) lane_q_.emplace_back(new Lane());
   cacheable_.assign(methods.size(), 0);
   kinds_.assign(methods.size(), 0);
+  natives_.resize(methods.size());
+}
+
+void FrameRpcServer::set_native_stream(uint32_t method, NativeStreamFactory factory) {
+  if (method < natives_.size()) natives_[method] = std::move(factory);
+}
+
+// ---- kind-2 bridge --------------------------------------------------------------------------
+std::shared_ptr<FrameRpcServer::Bridge> FrameRpcServer::bridge(uint64_t token) {
+  std::lock_guard<std::mutex> g(bridges_mu_);
+  auto it = bridges_.find(token);
+  return it == bridges_.end() ? nullptr : it->second;
+}
+
+int FrameRpcServer::stream_recv(uint64_t token, int timeout_ms, std::string* out) {
+  auto b = bridge(token);
+  if (!b) return 2;
+  size_t give_back = 0;
+  int rc;
+  {
+    std::unique_lock<std::mutex> lk(b->mu);
+    b->cv.wait_for(lk, std::chrono::milliseconds(std::max(0, timeout_ms)),
+                   [&] { return !b->inbound.empty() || b->half_closed || b->cancelled; });
+    if (!b->inbound.empty()) {
+      *out = std::move(b->inbound.front().first);
+      b->queued -= b->inbound.front().second;
+      b->inbound.pop_front();
+      if (b->deferred && b->queued <= kBridgeQueued / 2) {
+        give_back = b->deferred;
+        b->deferred = 0;
+      }
+      rc = 0;
+    } else {
+      rc = b->cancelled ? 2 : b->half_closed ? 1 : 3;
+    }
+  }
+  if (give_back) {   // Python caught up: reopen the stream's receive window
+    auto c = find(b->conn);
+    if (c && !c->closed) {
+      bool ok = true;
+      {
+        std::lock_guard<std::mutex> g(c->wmu);
+        if (c->h2 && c->h2->streams.count(b->sid)) {
+          h2::lib().consume_stream(c->h2->ng, b->sid, give_back);
+          ok = H2::flush_locked(*c->h2);
+        }
+      }
+      if (!ok) close_conn(c->id);
+    }
+  }
+  return rc;
+}
+
+bool FrameRpcServer::stream_send(uint64_t token, const std::string& msg, int timeout_ms, size_t backlog) {
+  auto b = bridge(token);
+  if (!b) return false;
+  auto c = find(b->conn);
+  if (!c || c->closed) return false;
+  auto pending = [&]() -> long {   // unsent bytes of this call, -1 when it is gone
+    auto it = c->h2->streams.find(b->sid);
+    if (it == c->h2->streams.end()) return -1;
+    return (long)(it->second.out.size() - it->second.out_off);
+  };
+  bool ok = true;
+  {
+    std::lock_guard<std::mutex> g(c->wmu);
+    if (!c->h2) return false;
+    auto it = c->h2->streams.find(b->sid);
+    if (it == c->h2->streams.end() || it->second.finished) return false;
+    H2::Stream& st = it->second;
+    st.out.push_back('\0');
+    put_be32(st.out, (uint32_t)msg.size());
+    st.out += msg;
+    H2::start_response(*c->h2, b->sid, st);
+    ok = H2::flush_locked(*c->h2);
+  }
+  if (!ok) {
+    close_conn(c->id);
+    return false;
+  }
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(std::max(1, timeout_ms));
+  for (;;) {
+    long left;
+    {
+      std::lock_guard<std::mutex> g(c->wmu);
+      left = c->closed ? -1 : pending();
+    }
+    if (left < 0) return false;
+    if ((size_t)left <= backlog) return true;
+    {
+      std::lock_guard<std::mutex> g(b->mu);
+      if (b->cancelled) return false;
+    }
+    if (std::chrono::steady_clock::now() > deadline) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(500));
+  }
+}
+
+void FrameRpcServer::stream_finish(uint64_t token, int status, const std::string& msg) {
+  std::shared_ptr<Bridge> b;
+  {
+    std::lock_guard<std::mutex> g(bridges_mu_);
+    auto it = bridges_.find(token);
+    if (it == bridges_.end()) return;
+    b = it->second;
+    bridges_.erase(it);
+  }
+  auto c = find(b->conn);
+  if (!c || c->closed) return;
+  bool ok = true;
+  {
+    std::lock_guard<std::mutex> g(c->wmu);
+    if (!c->h2) return;
+    auto it = c->h2->streams.find(b->sid);
+    if (it == c->h2->streams.end() || it->second.finished) return;
+    H2::Stream& st = it->second;
+    if (status != 0) {
+      H2::fail_locked(*c->h2, b->sid, st, status, msg);
+    } else {
+      st.finished = true;
+      H2::start_response(*c->h2, b->sid, st);
+    }
+    ok = H2::flush_locked(*c->h2);
+  }
+  if (!ok) close_conn(c->id);
+}
+
+void FrameRpcServer::allow_channel(const std::string& cid, const std::string& user) {
+  std::lock_guard<std::mutex> g(chan_mu_);
+  channels_[cid] = user;
+}
+
+void FrameRpcServer::revoke_channel(const std::string& cid) {
+  std::lock_guard<std::mutex> g(chan_mu_);
+  channels_.erase(cid);
+}
+
+bool FrameRpcServer::channel_user(const std::string& cid, std::string* user) {
+  std::lock_guard<std::mutex> g(chan_mu_);
+  auto it = channels_.find(cid);
+  if (it == channels_.end()) return false;
+  if (user) *user = it->second;
+  return true;
 }
 
 // ---- reply cache --------------------------------------------------------------------------
@@ -591,6 +855,21 @@ void FrameRpcServer::start() {
   socklen_t sl = sizeof(a);
   ::getsockname(listen_fd_, (sockaddr*)&a, &sl);
   port_ = ntohs(a.sin_port);
+  if (!unix_path_.empty()) {
+    sockaddr_un ua{};
+    ua.sun_family = AF_UNIX;
+    if (unix_path_.size() >= sizeof(ua.sun_path)) throw std::runtime_error("frame rpc: unix socket path too long");
+    std::memcpy(ua.sun_path, unix_path_.c_str(), unix_path_.size() + 1);
+    ::unlink(unix_path_.c_str());
+    unix_fd_ = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (unix_fd_ < 0 || ::bind(unix_fd_, (sockaddr*)&ua, sizeof(ua)) != 0 || ::listen(unix_fd_, 1024) != 0) {
+      if (unix_fd_ >= 0) ::close(unix_fd_);
+      unix_fd_ = -1;
+      ::close(listen_fd_);
+      listen_fd_ = -1;
+      throw std::runtime_error("frame rpc: cannot bind unix:" + unix_path_);
+    }
+  }
   running_ = true;
   for (int i = 0; i < nthreads_; ++i) {
     const int ep = ::epoll_create1(EPOLL_CLOEXEC);
@@ -604,9 +883,15 @@ void FrameRpcServer::start() {
 void FrameRpcServer::stop() {
   if (!running_.exchange(false)) return;
   if (listen_fd_ >= 0) ::shutdown(listen_fd_, SHUT_RDWR);
+  if (unix_fd_ >= 0) ::shutdown(unix_fd_, SHUT_RDWR);
   if (acceptor_.joinable()) acceptor_.join();
   if (listen_fd_ >= 0) ::close(listen_fd_);
   listen_fd_ = -1;
+  if (unix_fd_ >= 0) {
+    ::close(unix_fd_);
+    ::unlink(unix_path_.c_str());
+  }
+  unix_fd_ = -1;
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   threads_.clear();
@@ -625,31 +910,51 @@ void FrameRpcServer::stop() {
     l->q.clear();
     l->cv.notify_all();
   }
+  std::lock_guard<std::mutex> g(bridges_mu_);
+  for (auto& kv : bridges_) {
+    std::lock_guard<std::mutex> bg(kv.second->mu);
+    kv.second->cancelled = true;
+    kv.second->cv.notify_all();
+  }
 }
 
 void FrameRpcServer::accept_loop() {
   while (running_) {
-    const int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
-    if (fd < 0) {
-      if (errno == EINTR || errno == ECONNABORTED) continue;
-      if (!running_) break;
-      std::this_thread::sleep_for(std::chrono::milliseconds(5));
-      continue;
+    pollfd pf[2] = {{listen_fd_, POLLIN, 0}, {unix_fd_, POLLIN, 0}};
+    const int np = unix_fd_ >= 0 ? 2 : 1;
+    if (::poll(pf, np, 200) <= 0) continue;
+    for (int k = 0; k < np; ++k) {
+      if (!(pf[k].revents & (POLLIN | POLLERR | POLLHUP))) continue;
+      const int fd = ::accept4(pf[k].fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (fd < 0) {
+        if (errno == EINTR || errno == ECONNABORTED || errno == EAGAIN) continue;
+        if (!running_) break;
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        continue;
+      }
+      add_conn(fd, k == 1);
     }
+  }
+}
+
+void FrameRpcServer::add_conn(int fd, bool unix_peer) {
+  {
     int one = 1;
-    ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    if (!unix_peer) ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
     std::shared_ptr<Conn> c;
     {
       std::lock_guard<std::mutex> g(conns_mu_);
       uint32_t id = next_conn_++;
       if (next_conn_ == 0) next_conn_ = 1;
       c = std::make_shared<Conn>(fd, id);
+      c->unix_peer = unix_peer;
+      c->ep = epolls_[id % epolls_.size()];
       conns_[id] = c;
     }
     epoll_event ev{};
     ev.events = EPOLLIN | EPOLLRDHUP;
     ev.data.u64 = c->id;
-    if (::epoll_ctl(epolls_[c->id % epolls_.size()], EPOLL_CTL_ADD, fd, &ev) != 0) close_conn(c->id);
+    if (::epoll_ctl(c->ep, EPOLL_CTL_ADD, fd, &ev) != 0) close_conn(c->id);
   }
 }
 
@@ -671,6 +976,25 @@ void FrameRpcServer::close_conn(uint32_t id) {
   c->closed = true;
   ::epoll_ctl(epolls_[id % epolls_.size()], EPOLL_CTL_DEL, c->fd, nullptr);
   ::shutdown(c->fd, SHUT_RDWR);   // the fd itself closes with the last reference
+  std::lock_guard<std::mutex> g(c->wmu);
+  if (c->h2) {
+    for (auto& kv : c->h2->streams) {
+      if (!kv.second.bridge) continue;
+      std::lock_guard<std::mutex> bg(kv.second.bridge->mu);
+      kv.second.bridge->cancelled = true;
+      kv.second.bridge->cv.notify_all();
+    }
+    c->h2->streams.clear();   // native streams release their block locks now
+  }
+}
+
+void FrameRpcServer::on_writable(const std::shared_ptr<Conn>& c) {
+  bool ok = true;
+  {
+    std::lock_guard<std::mutex> g(c->wmu);
+    if (c->h2) ok = H2::flush_locked(*c->h2);
+  }
+  if (!ok) close_conn(c->id);
 }
 
 void FrameRpcServer::io_loop(int idx) {
@@ -686,7 +1010,8 @@ void FrameRpcServer::io_loop(int idx) {
         close_conn(id);
         continue;
       }
-      on_readable(c, ep);
+      if (evs[i].events & EPOLLOUT) on_writable(c);
+      if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) on_readable(c, ep);
     }
   }
 }
@@ -714,11 +1039,11 @@ void FrameRpcServer::on_readable(const std::shared_ptr<Conn>& c, int ep) {
   // protocol of a new connection: gRPC (HTTP/2 client preface) or framed RPC
   if (c->proto == 0 && c->in.size() >= 3) {
     if (c->in.compare(0, 3, "PRI") == 0) {
-      if (c->in.size() < sizeof(kH2Preface) - 1) {
+      if (c->in.size() < sizeof(h2::kPreface) - 1) {
         if (eof) close_conn(c->id);
         return;
       }
-      bool ok = c->in.compare(0, sizeof(kH2Preface) - 1, kH2Preface) == 0;
+      bool ok = c->in.compare(0, sizeof(h2::kPreface) - 1, h2::kPreface) == 0;
       if (ok) {
         std::lock_guard<std::mutex> g(c->wmu);
         ok = H2::start(*this, *c);
@@ -736,8 +1061,11 @@ void FrameRpcServer::on_readable(const std::shared_ptr<Conn>& c, int ep) {
     bool ok;
     {
       std::lock_guard<std::mutex> g(c->wmu);
-      const ssize_t r = H2::lib().mem_recv(c->h2->ng, reinterpret_cast<const uint8_t*>(c->in.data()), c->in.size());
+      if (!c->h2) return;
+      const ssize_t r = h2::lib().mem_recv(c->h2->ng, reinterpret_cast<const uint8_t*>(c->in.data()), c->in.size());
       c->in.clear();
+      if (c->in.capacity() > (4u << 20)) c->in.shrink_to_fit();
+      H2::apply_consumed(*c->h2);
       ok = r >= 0 && H2::flush_locked(*c->h2);
     }
     if (!ok || eof) close_conn(c->id);
@@ -830,6 +1158,7 @@ void FrameRpcServer::respond(uint64_t token, int status, const std::string& msg,
     bool ok;
     {
       std::lock_guard<std::mutex> g(c->wmu);
+      if (!c->h2) return;
       H2::respond_locked(*c->h2, (int32_t)(token & 0x7fffffffu), status, msg, payload);
       ok = H2::flush_locked(*c->h2);
     }

@@ -21,10 +21,13 @@
 // server's Python side validates it (same authenticator as SASL PLAIN) and binds the user to the
 // connection.  Status codes are gRPC status codes.
 #pragma once
+#include <sys/types.h>
+
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -41,6 +44,26 @@ struct FrameRequest {
   std::string payload;
 };
 
+// A gRPC call whose responses are produced in C++ on the I/O threads (the worker's ReadBlock data
+// path, csrc/data_server.cpp), instead of by a Python servicer.
+class NativeStream {
+ public:
+  virtual ~NativeStream() = default;
+  // A further request message of the call (e.g. ReadRequest.offset_received acks).
+  virtual void on_message(const char* p, size_t n) = 0;
+  // Writes up to `max` bytes of gRPC-framed response body into dst and returns the count.  0 with
+  // *eof unset = nothing to send until the next request message arrives (flow-control window);
+  // *eof = the call is complete.  -1 = the call failed with *status / *msg (sent as trailers).
+  virtual ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) = 0;
+};
+// Builds the native stream of a call from its first request message and the caller's identity
+// (the channel-id and alluxio-user headers).  nullptr with *status == 0 hands the call to the
+// Python servicer (kind 2 bridge); nullptr with *status != 0 fails the call with it.
+// `unix_peer`: the call arrived on the Unix domain socket (a same-node client).
+using NativeStreamFactory = std::function<std::unique_ptr<NativeStream>(
+    const std::string& first, const std::string& channel_id, const std::string& user, bool unix_peer, int* status,
+    std::string* msg)>;
+
 class FrameRpcServer {
  public:
   // `methods`: paths ("/svc/Method") in registration order, `lanes`: dispatch lane per method.
@@ -48,6 +71,8 @@ class FrameRpcServer {
                  const std::vector<int>& lanes, int io_threads);
   ~FrameRpcServer();
   int port() const { return port_; }
+  // Also accept connections on a Unix domain socket at `path` (set before start()).
+  void listen_unix(const std::string& path) { unix_path_ = path; }
   void start();
   void stop();
   // Up to `max_n` requests of `lane`, waiting at most timeout_ms for the first (GIL released).
@@ -67,7 +92,27 @@ class FrameRpcServer {
   // gRPC connections (HTTP/2, detected per connection by the client preface; see H2 in
   // frame_rpc.cpp): kind 1 = server-streaming method, whose Python reply is a sequence of
   // u32-length-prefixed messages (sent as one gRPC message each); 0 = unary.
+  // 2 = client- or bidi-streaming method bridged to Python: the dispatcher gets the first request
+  // message as the payload and pulls the rest with stream_recv; responses go out with stream_send
+  // and the call ends with stream_finish.
   void set_method_kind(uint32_t method, int kind);
+  // Serve `method` from C++ when the factory accepts the call (gRPC connections only).
+  void set_native_stream(uint32_t method, NativeStreamFactory factory);
+  // ---- kind-2 bridge (Python side; the GIL is released around the blocking calls) ----------
+  // 0 = a message in *out, 1 = the client half-closed, 2 = cancelled / connection gone, 3 = timeout.
+  int stream_recv(uint64_t token, int timeout_ms, std::string* out);
+  // Queue one response message; waits (up to timeout_ms) while more than `backlog` bytes of this
+  // call are unsent.  False once the call is cancelled or its connection closed.
+  bool stream_send(uint64_t token, const std::string& msg, int timeout_ms, size_t backlog = 8u << 20);
+  void stream_finish(uint64_t token, int status, const std::string& msg);
+  // Channels authenticated by the SASL service (gRPC calls served in C++ check channel-id here).
+  void allow_channel(const std::string& cid, const std::string& user);
+  void revoke_channel(const std::string& cid);
+  bool channel_user(const std::string& cid, std::string* user);
+  void set_require_channel_auth(bool on) { require_auth_ = on; }
+  bool require_channel_auth() const { return require_auth_; }
+  // Receive-window size advertised to gRPC clients for request streams (uploads).
+  void set_stream_window(uint32_t bytes) { stream_window_ = bytes; }
   uint64_t grpc_requests() const { return grpc_requests_.load(); }
   static bool grpc_available();
   uint64_t epoch() const { return epoch_.load(std::memory_order_acquire); }
@@ -83,14 +128,20 @@ class FrameRpcServer {
   struct Conn;
   struct H2;
   void accept_loop();
+  void add_conn(int fd, bool unix_peer);
   void io_loop(int idx);
   void on_readable(const std::shared_ptr<Conn>& c, int ep);
   void close_conn(uint32_t id);
+  void on_writable(const std::shared_ptr<Conn>& c);
+  struct Bridge;
+  std::shared_ptr<Bridge> bridge(uint64_t token);
   std::shared_ptr<Conn> find(uint32_t id);
 
   std::string host_;
   int port_;
   int listen_fd_ = -1;
+  int unix_fd_ = -1;
+  std::string unix_path_;
   std::unordered_map<std::string, uint32_t> method_ids_;
   std::vector<int> lanes_;
   int nthreads_;
@@ -110,6 +161,13 @@ class FrameRpcServer {
   std::atomic<uint64_t> requests_{0};
   std::atomic<uint64_t> grpc_requests_{0};
   std::vector<uint8_t> kinds_;
+  std::vector<NativeStreamFactory> natives_;
+  std::mutex bridges_mu_;
+  std::unordered_map<uint64_t, std::shared_ptr<Bridge>> bridges_;
+  std::mutex chan_mu_;
+  std::unordered_map<std::string, std::string> channels_;
+  bool require_auth_ = false;
+  uint32_t stream_window_ = 1u << 20;
   int wake_fd_ = -1;
 
   static std::string cache_key(uint32_t method, const std::string& user, const char* req, size_t n);

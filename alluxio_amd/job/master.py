@@ -104,7 +104,7 @@ class JobMaster:
                     w.last_heartbeat = time.time()
                     return w.id
             wid = next(self._wids)
-            self.workers[wid] = JobWorkerInfo(wid, address, block_worker_port or address.dataPort)
+            self.workers[wid] = JobWorkerInfo(wid, address, block_worker_port or address.rpcPort)
             return wid
 
     def heartbeat(self, worker_id: int, health, task_infos) -> list:

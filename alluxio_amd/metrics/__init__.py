@@ -25,12 +25,17 @@ class Counter:
     """LongAdder-style counter: ``inc`` is one GIL-atomic deque append (no lock, so hot RPC paths
     never convoy on it); pending increments are folded in under a lock when read or every 4096."""
 
-    __slots__ = ("_v", "_pending", "_lock")
+    __slots__ = ("_v", "_pending", "_lock", "_sources")
 
     def __init__(self):
         self._v = 0
         self._pending = collections.deque()
         self._lock = threading.Lock()
+        self._sources = ()
+
+    def add_source(self, fn) -> None:
+        """Count ``fn()`` too: a monotonic counter kept elsewhere (a native server's bytes)."""
+        self._sources = self._sources + (fn,)
 
     def inc(self, n: int = 1) -> None:
         self._pending.append(n)
@@ -47,7 +52,10 @@ class Counter:
             for _ in range(len(q)):
                 s += q.popleft()
             self._v += s
-            return self._v
+            v = self._v
+        for fn in self._sources:
+            v += fn()
+        return v
 
     @property
     def count(self) -> int:

@@ -54,7 +54,7 @@ FS_SERVICE = "alluxio.grpc.file.FileSystemMasterClientService"
 SASL_SERVICE = "alluxio.grpc.sasl.SaslAuthenticationService"
 # services a gRPC caller reaches without an authenticated channel (rpc._UNAUTH_SERVICES)
 UNAUTH_SERVICES = frozenset({SASL_SERVICE, "alluxio.grpc.version.ServiceVersionClientService"})
-LANE_FAST, LANE_BLOCKING, LANE_MUTATION = 0, 1, 2
+LANE_FAST, LANE_BLOCKING, LANE_MUTATION, LANE_STREAM = 0, 1, 2, 3
 AUTH_PATH = "@auth"
 _LIVE: "weakref.WeakSet[NativeRpcFrontend]" = weakref.WeakSet()
 
@@ -126,34 +126,63 @@ def auth_payload(auth) -> bytes:
 
 
 class NativeRpcFrontend:
+    """``services``: serve only these services (default: every servicer of ``rpc_server``).
+    ``bridge_services``: their client-/bidi-streaming and data-streaming methods are served too,
+    bridged call by call to the Python servicer (kind 2: request messages pulled with
+    ``stream_recv``, responses pushed with ``stream_send``, one pool thread per live call) -- the
+    worker's data port serves the whole BlockWorker service this way, with ReadBlock answered in
+    C++ whenever the block is in the store (csrc/data_server.cpp)."""
+
     def __init__(self, rpc_server, host: str, port: int = 0, fast_threads: int = 2, blocking_threads: int = 32,
                  io_threads: int = 2, batch: int = 64, mutation_threads: int = 2, mutation_batch: int = 16,
-                 reply_cache: bool = True, epoch_source=None):
+                 reply_cache: bool = True, epoch_source=None, services=None, bridge_services=(),
+                 stream_threads: int = 128):
         from ..ops.native import lib
         self.rpc = rpc_server
         self.methods = [(AUTH_PATH, None, None)]
         lanes = [0]
+        kinds = [0]
         servicers = dict(rpc_server._servicers)
+        if services is not None:
+            servicers = {k: v for k, v in servicers.items() if k in services}
         if rpc_server.authenticator is not None:
             servicers[SASL_SERVICE] = rpc_server.authenticator   # as RpcServer.start installs it
+        bridge_services = frozenset(bridge_services)
         for svc, servicer in servicers.items():
             for name, spec in SERVICES[svc].items():
-                # unary requests only; a server-streaming reply travels as one frame of
-                # length-prefixed messages (metadata listings, not data streams).  The SASL
-                # handshake (one client message, one reply) serves gRPC connections.
+                # unary requests; a server-streaming reply of a metadata service travels as one
+                # frame of length-prefixed messages.  The SASL handshake (one client message, one
+                # reply) serves gRPC connections.  Streaming calls of a bridged service (data
+                # streams) get the kind-2 bridge.
                 if not hasattr(servicer, name):
                     continue
-                if spec.client_streaming and svc != SASL_SERVICE:
+                kind = 1 if spec.server_streaming else 0
+                if svc in bridge_services and (spec.client_streaming or spec.server_streaming):
+                    kind = 2
+                elif spec.client_streaming and svc != SASL_SERVICE:
                     continue
-                if spec.server_streaming and svc not in STREAM_SERVICES and svc != SASL_SERVICE:
+                elif spec.server_streaming and svc not in STREAM_SERVICES and svc != SASL_SERVICE:
                     continue
                 self.methods.append((spec.path, spec, getattr(servicer, name)))
-                lanes.append(LANE_FAST if name in FAST_METHODS or svc == SASL_SERVICE else
+                kinds.append(kind)
+                lanes.append(LANE_STREAM if kind == 2 else
+                             LANE_FAST if name in FAST_METHODS or svc == SASL_SERVICE else
                              LANE_MUTATION if name in MUTATION_METHODS and svc == FS_SERVICE else LANE_BLOCKING)
         self.server = lib().FrameRpcServer(host, port, [m[0] for m in self.methods], lanes, io_threads)
-        for i, (_path, spec, _fn) in enumerate(self.methods):
-            if spec is not None and spec.server_streaming:
-                self.server.set_method_kind(i, 1)
+        for i, k in enumerate(kinds):
+            if k:
+                self.server.set_method_kind(i, k)
+        self.kinds = kinds
+        self.stream_threads = max(1, stream_threads)
+        self._stream_exec = None
+        self._auth_hooked = False
+        auth = rpc_server.authenticator
+        if auth is not None and bridge_services:
+            # calls answered in C++ (ReadBlock) check the caller's channel-id against the channels
+            # the SASL service authenticated (mirrored from the Python authenticator)
+            lib().set_require_channel_auth(self.server, True)
+            auth.add_listener(self._on_channel)
+            self._auth_hooked = True
         self.fast_threads, self.blocking_threads, self.batch = fast_threads, blocking_threads, batch
         self.mutation_threads, self.mutation_batch = max(1, mutation_threads), max(1, mutation_batch)
         self.lanes = lanes
@@ -172,13 +201,31 @@ class NativeRpcFrontend:
         self._after_init = threading.Lock()
         self.spilled = 0
 
+    def method_index(self, path: str) -> int:
+        for i, (p, _spec, _fn) in enumerate(self.methods):
+            if p == path:
+                return i
+        raise KeyError(path)
+
+    def _on_channel(self, cid: str, user: str | None) -> None:
+        from ..ops.native import lib
+        if user is None:
+            lib().revoke_channel(self.server, cid)
+        else:
+            lib().allow_channel(self.server, cid, user)
+
     def start(self) -> int:
         self.server.start()
         self.port = self.server.port
         self._running = True
         _LIVE.add(self)
-        for lane, n, batch in ((LANE_FAST, self.fast_threads, self.batch), (LANE_BLOCKING, self.blocking_threads, 1),
-                               (LANE_MUTATION, self.mutation_threads, self.mutation_batch)):
+        lanes = [(LANE_FAST, self.fast_threads, self.batch), (LANE_BLOCKING, self.blocking_threads, 1),
+                 (LANE_MUTATION, self.mutation_threads, self.mutation_batch)]
+        if any(k == 2 for k in self.kinds):
+            import concurrent.futures as cf
+            self._stream_exec = cf.ThreadPoolExecutor(self.stream_threads, thread_name_prefix="native-stream")
+            lanes.append((LANE_STREAM, 1, 64))
+        for lane, n, batch in lanes:
             for i in range(n):
                 t = threading.Thread(target=self._loop, args=(lane, batch), daemon=True,
                                      name=f"native-rpc-{lane}-{i}")
@@ -190,11 +237,14 @@ class NativeRpcFrontend:
         if not self._running:
             return
         self._running = False
+        if self._auth_hooked:
+            self.rpc.authenticator.remove_listener(self._on_channel)
+            self._auth_hooked = False
         self.server.stop()
         for t in self._threads:
             t.join(timeout=2)
         self._threads = []
-        for name in ("_spill_exec", "_after_exec"):
+        for name in ("_spill_exec", "_after_exec", "_stream_exec"):
             pool = getattr(self, name, None)
             if pool is not None:
                 pool.shutdown(wait=False)
@@ -351,6 +401,62 @@ class NativeRpcFrontend:
                     pool = self._after_exec = cf.ThreadPoolExecutor(2, thread_name_prefix="rpc-after-durable")
         return pool
 
+    # ---- kind-2 bridge: one pool thread runs a streaming call of the Python servicer ------------
+    def _run_stream(self, token, midx, user, payload) -> None:
+        from ..ops.native import lib
+        from ..security import as_user
+        from . import marshal
+        C = lib()
+        srv = self.server
+        _path, spec, fn = self.methods[midx]
+        des = marshal.marshallers(spec, True)[1]
+        it = None
+        try:
+            if user and user[0] == "\x01":
+                user = self._grpc_user(spec, user)
+            elif self.rpc.authenticator is not None and not user:
+                raise ex.UnauthenticatedException("native channel is not authenticated")
+            self.rpc.check(spec)
+            first = des(payload)
+
+            def requests():
+                yield first
+                while True:
+                    rc, data = C.stream_recv(srv, token, 1000)
+                    if rc == 0:
+                        yield des(data)
+                    elif rc == 1:
+                        return
+                    elif rc == 2:
+                        raise ex.CancelledException("call cancelled by the client")
+                    elif not self._running:
+                        raise ex.UnavailableException("server stopping")
+
+            with as_user(user or None):
+                arg = requests() if spec.client_streaming else first
+                if spec.server_streaming:
+                    it = fn(arg, _Ctx(user))
+                    for m in it:
+                        if not C.stream_send(srv, token, m.SerializeToString(), 60_000):
+                            return          # cancelled: the generator is closed below
+                else:
+                    r = fn(arg, _Ctx(user))
+                    if not C.stream_send(srv, token, r.SerializeToString(), 60_000):
+                        return
+            C.stream_finish(srv, token, 0, "")
+        except Exception as e:  # noqa: BLE001
+            se = ex.wrap(e)
+            if not isinstance(e, ex.AlluxioStatusException):
+                LOG.debug("native stream %s failed", self.methods[midx][0], exc_info=True)
+            C.stream_finish(srv, token, int(se.status), se.message or str(se))
+        finally:
+            if it is not None and hasattr(it, "close"):
+                try:
+                    it.close()
+                except Exception:  # noqa: BLE001
+                    pass
+            C.stream_finish(srv, token, 1, "call ended")   # no-op once finished
+
     def _loop(self, lane: int, batch: int) -> None:
         srv = self.server
         metrics = self.rpc.metrics
@@ -363,6 +469,10 @@ class NativeRpcFrontend:
                 time.sleep(0.01)
                 continue
             if not reqs:
+                continue
+            if lane == LANE_STREAM:
+                for r in reqs:
+                    self._stream_exec.submit(self._run_stream, *r)
                 continue
             t0 = time.perf_counter()
             nb = lane != LANE_BLOCKING

@@ -70,6 +70,26 @@ class ServerAuthenticator:
         self.ttl = channel_ttl_s
         self._channels: dict[str, tuple[str, float]] = {}
         self._lock = threading.Lock()
+        # fn(channel id, user | None): native front ends mirror the registry (data_server.cpp)
+        self._listeners: list = []
+
+    def add_listener(self, fn) -> None:
+        with self._lock:
+            self._listeners.append(fn)
+            current = [(c, u) for c, (u, _t) in self._channels.items()]
+        for c, u in current:
+            fn(c, u)
+
+    def remove_listener(self, fn) -> None:
+        with self._lock:
+            self._listeners = [f for f in self._listeners if f is not fn]
+
+    def _notify(self, cid: str, user: str | None) -> None:
+        for fn in list(self._listeners):
+            try:
+                fn(cid, user)
+            except Exception:  # noqa: BLE001 - a stopped front end
+                pass
 
     @classmethod
     def from_conf(cls, conf):
@@ -93,6 +113,7 @@ class ServerAuthenticator:
     def unregister(self, channel_id: str) -> None:
         with self._lock:
             self._channels.pop(channel_id, None)
+        self._notify(channel_id, None)
 
     def purge(self) -> int:
         cutoff = time.time() - self.ttl
@@ -100,6 +121,8 @@ class ServerAuthenticator:
             old = [c for c, (_, t) in self._channels.items() if t < cutoff]
             for c in old:
                 del self._channels[c]
+        for c in old:
+            self._notify(c, None)
         return len(old)
 
     # SaslAuthenticationService.authenticate (bidi stream)
@@ -114,8 +137,10 @@ class ServerAuthenticator:
             self.provider.authenticate(user, password)
             # impersonation (authz != user) is not granted: the channel acts as the authenticated user
             effective = user
+            cid = msg.channelRef or msg.clientId
             with self._lock:
-                self._channels[msg.channelRef or msg.clientId] = (effective, time.time())
+                self._channels[cid] = (effective, time.time())
+            self._notify(cid, effective)
             yield pb.sasl.SaslMessage(messageType=pb.sasl.SaslMessageType.values_by_name["SUCCESS"].number,
                                       clientId=msg.clientId, channelRef=msg.channelRef,
                                       authenticationScheme=msg.authenticationScheme)

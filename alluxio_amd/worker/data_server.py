@@ -1,0 +1,68 @@
+"""Native data port of a worker: the BlockWorker gRPC service on the C++ HTTP/2 front end.
+
+Parity: core/server/worker/src/main/java/alluxio/worker/grpc/GrpcDataServer.java:50-198 (the
+worker's data server, a Netty gRPC server of BlockWorkerImpl), BlockReadHandler.java:111-152 and
+core/common/src/main/java/alluxio/grpc/ReadResponseMarshaller.java:38-80.
+
+``ReadBlock`` of a block the store holds is answered on the C++ I/O threads (csrc/data_server.cpp:
+read lock for the call, HBM chunks DMA'd into pinned staging, ``offset_received`` window); every
+other BlockWorker call -- WriteBlock, UFS read-through, OpenLocalBlock, AsyncCache, ... -- runs the
+same Python servicer as the grpcio port, through the front end's streaming bridge.  The port is
+advertised as ``WorkerNetAddress.dataPort``; clients stream block bytes from it
+(client/streams.py ``GrpcBlockReader.native_source``).
+"""
+from __future__ import annotations
+
+import logging
+
+from .services import SVC_BLOCK_WORKER
+
+LOG = logging.getLogger(__name__)
+
+READ_BLOCK_PATH = f"/{SVC_BLOCK_WORKER}/ReadBlock"
+
+
+def available() -> bool:
+    from ..ops.native import lib
+    return bool(lib().FrameRpcServer.grpc_available())
+
+
+class WorkerDataServer:
+    def __init__(self, rpc_server, worker, conf, host: str, domain_socket: str | None = None):
+        from ..ops.native import lib
+        from ..rpc.native import NativeRpcFrontend
+        self.worker = worker
+        self.frontend = NativeRpcFrontend(
+            rpc_server, host, conf.get_int("alluxio.worker.data.server.native.port", "0"),
+            fast_threads=2, blocking_threads=conf.get_int("alluxio.worker.data.server.native.blocking.threads", "8"),
+            io_threads=conf.get_int("alluxio.worker.data.server.native.io.threads", "8"),
+            services={SVC_BLOCK_WORKER}, bridge_services={SVC_BLOCK_WORKER},
+            stream_threads=conf.get_int("alluxio.worker.data.server.native.stream.threads", "128"))
+        # request streams (WriteBlock uploads) get a window of a few chunks
+        lib().set_stream_window(self.frontend.server, 4 << 20)
+        if domain_socket:
+            # the domain-socket data server (same-node clients skip TCP): same service, same port
+            import os
+            os.makedirs(os.path.dirname(domain_socket) or ".", exist_ok=True)
+            lib().listen_unix(self.frontend.server, domain_socket)
+        self.stats = lib().serve_block_reads(
+            self.frontend.server, self.frontend.method_index(READ_BLOCK_PATH), worker.native,
+            conf.get_bytes("alluxio.worker.network.reader.max.chunk.size.bytes", "2MB"),
+            conf.get_bytes("alluxio.worker.network.reader.buffer.size", "4MB"))
+        self.port = None
+
+    def start(self) -> int:
+        self.port = self.frontend.start()
+        m = self.worker.metrics
+        st = self.stats
+        m.gauge("DataServerNativeStreams", lambda: st.streams)
+        m.gauge("DataServerBridgedStreams", lambda: st.declined)
+        # bytes the C++ server sent count in the worker's read metrics (BytesReadDomain for
+        # same-node domain-socket clients, BytesReadRemote otherwise)
+        m.counter("BytesReadAlluxio").add_source(lambda: st.bytes)
+        m.counter("BytesReadDomain").add_source(lambda: st.domain_bytes)
+        m.counter("BytesReadRemote").add_source(lambda: st.bytes - st.domain_bytes)
+        return self.port
+
+    def stop(self) -> None:
+        self.frontend.stop()

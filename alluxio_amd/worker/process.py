@@ -104,8 +104,12 @@ class AlluxioWorkerProcess:
         self.master_channel = master_channel(self.master_address)
         self.worker = BlockWorker(self.conf, self.store, self.master_channel)
         self.domain_socket = self._domain_socket_path() if enable_grpc else None
+        from .data_server import available
+        # the native data server (GrpcDataServer analogue) takes the domain socket when it runs
+        self._native_data = enable_grpc and self.conf.get_bool("alluxio.worker.data.server.native.enabled", "true") \
+            and available()
         self.server = RpcServer(host, self.port, metrics=msys.metrics("Worker"), enable_grpc=enable_grpc,
-                                conf=self.conf, domain_socket=self.domain_socket)
+                                conf=self.conf, domain_socket=None if self._native_data else self.domain_socket)
         self.server.add_servicer(SVC_BLOCK_WORKER, BlockWorkerService(self.worker, self.conf))
         self.sync = BlockMasterSync(self.worker, self)
         self._threads: list[hb.HeartbeatThread] = []
@@ -113,6 +117,7 @@ class AlluxioWorkerProcess:
         self._job_fs = None
         self.web = None
         self.web_port = 0
+        self.data_server = None
 
     @property
     def address(self) -> str:
@@ -156,9 +161,15 @@ class AlluxioWorkerProcess:
             self.pause_monitor.start()
         addr = self.server.start()
         host, port = addr.rsplit(":", 1)
+        data_port = int(port)
+        if self._native_data:
+            # the native gRPC data port (GrpcDataServer analogue): ReadBlock streamed from C++
+            from .data_server import WorkerDataServer
+            self.data_server = WorkerDataServer(self.server, self.worker, self.conf, self.host, self.domain_socket)
+            data_port = self.data_server.start()
         ti = pb.grpc.TieredIdentity(tiers=[pb.grpc.LocalityTier(tierName="node", value=socket.gethostname()),
                                            pb.grpc.LocalityTier(tierName="gpu", value=str(self.store.device))])
-        self.worker.address = pb.grpc.WorkerNetAddress(host=host, rpcPort=int(port), dataPort=int(port),
+        self.worker.address = pb.grpc.WorkerNetAddress(host=host, rpcPort=int(port), dataPort=data_port,
                                                        domainSocketPath=self.domain_socket or "",
                                                        webPort=0, tieredIdentity=ti,
                                                        containerHost=socket.gethostname())
@@ -267,6 +278,9 @@ class AlluxioWorkerProcess:
         from ..client.context import unregister_local_worker
         if self.server.address:
             unregister_local_worker(self.server.address)
+        if self.data_server is not None:
+            self.data_server.stop()
+            self.data_server = None
         self.server.stop()
         if self.web is not None:
             self.web.stop()

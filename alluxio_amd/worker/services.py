@@ -325,7 +325,7 @@ class BlockWorkerService:
 
     def AsyncCache(self, req, ctx):
         src = None
-        if req.source_host and (req.source_host, req.source_port) != (self.w.address.host, self.w.address.dataPort):
+        if req.source_host and (req.source_host, req.source_port) != (self.w.address.host, self.w.address.rpcPort):
             src = self.w.peer_fetcher(req.source_host, req.source_port, req.length)
         opts = req.open_ufs_block_options if req.HasField("open_ufs_block_options") else None
         if opts is not None and not opts.block_size and req.length:

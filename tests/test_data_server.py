@@ -1,0 +1,267 @@
+"""The worker's native gRPC data port (csrc/data_server.cpp + the H2 front end's streaming bridge)
+and the native host reader (csrc/block_source.cpp).
+
+Reference behaviour pinned here: GrpcDataServer.java:50-198 serves the whole BlockWorker service on
+the data port; BlockReadHandler.java:111-152 / AbstractReadHandler.java stream a locked block in
+chunks and pause while more than the window is un-acked by ``offset_received``;
+ReadResponseMarshaller.java:38-80 (header + raw chunk bytes) is what a stock gRPC client decodes.
+"""
+import time
+
+import grpc
+import numpy as np
+import pytest
+
+from alluxio_amd.minicluster import LocalAlluxioCluster
+from alluxio_amd.ops.native import lib
+from alluxio_amd.proto import SERVICES, pb
+from alluxio_amd.rpc import marshal
+
+pytestmark = pytest.mark.skipif(not lib().FrameRpcServer.grpc_available(), reason="libnghttp2 not present")
+
+BW = "alluxio.grpc.block.BlockWorker"
+REMOTE = {"alluxio.user.network.inprocess.transport.enabled": "false",
+          "alluxio.user.short.circuit.enabled": "false"}
+
+
+def _cluster(tmp_path, extra=None, auth="NOSASL"):
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "dram",
+            "alluxio.worker.tieredstore.level0.dirs.quota": "512MB",
+            "alluxio.user.block.size.bytes.default": "4MB",
+            "alluxio.security.authentication.type": auth,
+            "alluxio.security.authorization.permission.enabled": "false"}
+    conf.update(extra or {})
+    return LocalAlluxioCluster(num_workers=1, conf=conf, grpc=True, work_dir=str(tmp_path / "c"))
+
+
+def _remote_fs(cluster, **props):
+    from alluxio_amd.client.file_system import FileSystem
+    from alluxio_amd.conf import Configuration
+    p = dict(REMOTE)
+    p.update(props)
+    if cluster.conf.get("alluxio.security.authentication.type") == "NOSASL":
+        p["alluxio.security.authentication.type"] = "NOSASL"
+    return FileSystem(conf=Configuration(p), master_address=cluster.master.address)
+
+
+def _blocks(fs, path):
+    st = fs.get_status(path)
+    return [(fbi.blockInfo.blockId, fbi.blockInfo.length) for fbi in st.fileBlockInfos]
+
+
+def test_native_reader_over_data_port(tmp_path):
+    with _cluster(tmp_path) as c:
+        fs = c.client()
+        data = np.random.default_rng(0).integers(0, 256, (10 << 20) + 321, dtype=np.uint8)
+        fs.write_file("/f", data, write_type="MUST_CACHE")
+        w = c.workers[0]
+        assert w.data_server is not None and w.worker.address.dataPort == w.data_server.port
+        assert w.data_server.port != w.worker.address.rpcPort
+        rfs = _remote_fs(c)
+        try:
+            with rfs.open_file("/f") as f:                      # 4 KiB read(buf) loop
+                assert f._nat is not None
+                buf = bytearray(4096)
+                out = bytearray()
+                while True:
+                    n = f.readinto(buf)
+                    if not n:
+                        break
+                    out += buf[:n]
+            assert bytes(out) == data.tobytes()
+            with rfs.open_file("/f") as f:                      # seeks, across and within blocks
+                for pos, n in [(9 << 20, 5000), (7, 100), ((4 << 20) - 10, 40), (len(data) - 3, 10)]:
+                    f.seek(pos)
+                    assert f.read(n) == data[pos:pos + n].tobytes()
+                    assert f.tell() == min(len(data), pos + n)
+            st = w.data_server.stats
+            assert st.streams >= 3 and st.bytes >= len(data) and st.declined == 0
+        finally:
+            rfs.close()
+            fs.close()
+
+
+def test_stock_grpc_client_on_data_port_flow_control(tmp_path):
+    """A grpcio ReadBlock call against the native port: frames decode as ReadResponse, the server
+    stops at the window until offset_received arrives, and the stream completes after acks."""
+    with _cluster(tmp_path, {"alluxio.worker.network.reader.buffer.size": "1MB"}) as c:
+        fs = c.client()
+        data = np.random.default_rng(1).integers(0, 256, 4 << 20, dtype=np.uint8)
+        fs.write_file("/g", data, write_type="MUST_CACHE")
+        (bid, blen), = _blocks(fs, "/g")
+        port = c.workers[0].data_server.port
+        ch = grpc.insecure_channel(f"127.0.0.1:{port}")
+        try:
+            spec = SERVICES[BW]["ReadBlock"]
+            call = ch.stream_stream(spec.path, spec.request.SerializeToString, marshal.decode_read_response)
+            import queue
+            q: queue.Queue = queue.Queue()
+            q.put(pb.block.ReadRequest(block_id=bid, offset=0, length=blen, chunk_size=64 << 10))
+
+            def reqs():
+                while True:
+                    r = q.get()
+                    if r is None:
+                        return
+                    yield r
+            it = call(reqs())
+            got = bytearray()
+            # without acks the server sends at most window (+ one chunk)
+            deadline = time.time() + 5
+            while len(got) < (1 << 20):
+                got += bytes(next(it).chunk.data)
+                assert time.time() < deadline
+            time.sleep(0.3)
+            sent = c.workers[0].data_server.stats.bytes
+            assert sent <= (1 << 20) + (64 << 10), sent
+            while len(got) < blen:
+                q.put(pb.block.ReadRequest(offset_received=len(got)))
+                got += bytes(next(it).chunk.data)
+            q.put(None)
+            assert bytes(got) == data.tobytes()
+            with pytest.raises(StopIteration):
+                next(it)
+            # a block the worker does not hold: bridged to the Python servicer -> NOT_FOUND
+            call2 = ch.stream_stream(spec.path, spec.request.SerializeToString, spec.response.FromString)
+            with pytest.raises(grpc.RpcError) as ei:
+                list(call2(iter([pb.block.ReadRequest(block_id=12345, offset=0, length=10)])))
+            assert ei.value.code() == grpc.StatusCode.NOT_FOUND
+            assert c.workers[0].data_server.stats.declined >= 1
+        finally:
+            ch.close()
+            fs.close()
+
+
+def test_write_block_bridged_then_native_read(tmp_path):
+    """WriteBlock (client streaming) through the bridge on the data port, read back natively."""
+    with _cluster(tmp_path) as c:
+        fs = c.client()
+        rfs = _remote_fs(c)
+        w = c.workers[0]
+        try:
+            ch = grpc.insecure_channel(f"127.0.0.1:{w.data_server.port}")
+            spec = SERVICES[BW]["WriteBlock"]
+            call = ch.stream_stream(spec.path, marshal.serialize, spec.response.FromString)
+            payload = np.random.default_rng(2).integers(0, 256, (3 << 20) + 17, dtype=np.uint8).tobytes()
+            bid = 777
+            msgs = [pb.block.WriteRequest(command=pb.block.WriteRequestCommand(type=0, id=bid, offset=0,
+                                                                                 space_to_reserve=1 << 20))]
+            for i in range(0, len(payload), 1 << 20):
+                msgs.append(marshal.write_request_frame(payload[i:i + (1 << 20)]))
+            resps = list(call(iter(msgs)))
+            assert resps[-1].offset == len(payload)
+            ch.close()
+            assert w.worker.has_block(bid)
+            src = lib().GrpcBlockSource("127.0.0.1", w.data_server.port, bid, len(payload), 1 << 20)
+            out = np.empty(len(payload), dtype=np.uint8)
+            src.read_into(0, len(payload), out.ctypes.data)
+            assert out.tobytes() == payload
+            src.close()
+            # the client library's WriteBlock (rpc port) and native read back (data port)
+            data = np.random.default_rng(3).integers(0, 256, (5 << 20) + 1, dtype=np.uint8)
+            rfs.write_file("/w", data, write_type="MUST_CACHE")
+            assert rfs.read_file("/w") == data.tobytes()
+        finally:
+            rfs.close()
+            fs.close()
+
+
+def test_ufs_read_through_bridged(tmp_path):
+    """A block that is not cached: ReadBlock with UFS options is served by the Python servicer
+    through the bridge (read-through caching), then natively once cached."""
+    with _cluster(tmp_path) as c:
+        fs = c.client()
+        data = np.random.default_rng(4).integers(0, 256, (6 << 20) + 9, dtype=np.uint8)
+        fs.write_file("/u", data, write_type="CACHE_THROUGH")
+        fs.free("/u")
+        w = c.workers[0]
+        c.heartbeat_workers()          # the Free command runs on the worker heartbeat
+        assert not w.worker.native.block_ids(-1)
+        rfs = _remote_fs(c)
+        try:
+            before = w.data_server.stats.declined
+            assert rfs.read_file("/u") == data.tobytes()
+            assert w.data_server.stats.declined > before
+            assert rfs.read_file("/u") == data.tobytes()
+        finally:
+            rfs.close()
+            fs.close()
+
+
+def test_native_read_requires_authenticated_channel(tmp_path):
+    with _cluster(tmp_path, auth="SIMPLE") as c:
+        fs = c.client()
+        data = np.arange(1 << 20, dtype=np.uint32).view(np.uint8)
+        fs.write_file("/s", data, write_type="MUST_CACHE")
+        (bid, blen), = _blocks(fs, "/s")
+        port = c.workers[0].data_server.port
+        with pytest.raises(lib().StoreError) as ei:       # no channel-id: refused in C++
+            src = lib().GrpcBlockSource("127.0.0.1", port, bid, blen, 1 << 20)
+            src.read_into(0, 100, np.empty(100, dtype=np.uint8).ctypes.data)
+        assert "authenticated" in str(ei.value)
+        rfs = _remote_fs(c)                                # SASL channel: its id authorizes the call
+        try:
+            assert rfs.read_file("/s") == data.tobytes()
+        finally:
+            rfs.close()
+            fs.close()
+
+
+def test_native_client_against_grpcio_server(tmp_path):
+    """The native gRPC client interoperates with the pure-grpcio BlockWorker server (rpc port)."""
+    with _cluster(tmp_path) as c:
+        fs = c.client()
+        data = np.random.default_rng(5).integers(0, 256, 3 << 20, dtype=np.uint8)
+        fs.write_file("/i", data, write_type="MUST_CACHE")
+        (bid, blen), = _blocks(fs, "/i")
+        rpc_port = c.workers[0].worker.address.rpcPort
+        src = lib().GrpcBlockSource("127.0.0.1", rpc_port, bid, blen, 256 << 10)
+        out = np.empty(blen, dtype=np.uint8)
+        src.read_into(0, blen, out.ctypes.data)
+        assert np.array_equal(out, data)
+        src.read_into(1000, 50, out.ctypes.data)          # backward: a new call at the offset
+        assert np.array_equal(out[:50], data[1000:1050])
+        src.close()
+        fs.close()
+
+
+def test_cancelled_stream_releases_the_block_lock(tmp_path):
+    with _cluster(tmp_path) as c:
+        fs = c.client()
+        data = np.random.default_rng(6).integers(0, 256, 4 << 20, dtype=np.uint8)
+        fs.write_file("/x", data, write_type="MUST_CACHE")
+        (bid, blen), = _blocks(fs, "/x")
+        w = c.workers[0]
+        src = lib().GrpcBlockSource("127.0.0.1", w.data_server.port, bid, blen, 64 << 10)
+        out = np.empty(4096, dtype=np.uint8)
+        src.read_into(0, 4096, out.ctypes.data)
+        src.close()                                        # mid-stream
+        deadline = time.time() + 5
+        while True:                                        # the read lock is gone: removable
+            try:
+                w.worker.remove_block(1, bid)
+                break
+            except Exception:  # noqa: BLE001
+                assert time.time() < deadline
+                time.sleep(0.05)
+        assert not w.worker.has_block(bid)
+        fs.close()
+
+
+def test_in_process_host_reads_use_store_source(tmp_path):
+    """An in-process worker: host read(buf) goes through the chunk buffer filled from the store."""
+    with _cluster(tmp_path) as c:
+        fs = c.client()
+        data = np.random.default_rng(7).integers(0, 256, (9 << 20) + 5, dtype=np.uint8)
+        fs.write_file("/p", data, write_type="MUST_CACHE")
+        with fs.open_file("/p") as f:
+            b = bytearray(4096)
+            parts = []
+            while True:
+                n = f.readinto(b)
+                if not n:
+                    break
+                parts.append(bytes(b[:n]))
+            assert f._nat.refills >= 9
+        assert b"".join(parts) == data.tobytes()
+        fs.close()

@@ -62,7 +62,30 @@ def test_ipc_read_from_other_process(gpu, tmp_path):
         with fs.open_file("/ipc/f") as f:
             assert f.pread(5 * (1 << 20) + 17, host) == len(host)
         assert np.array_equal(host, expect[5 * (1 << 20) + 17:5 * (1 << 20) + 17 + len(host)])
+        # host read(buf) loop (StressWorkerBench's shape): the native reader refills its pinned
+        # chunk buffer from the IPC-mapped HBM pages (D2H DMA) and serves each 4 KiB from it
+        with fs.open_file("/ipc/f") as f:
+            b = bytearray(4096)
+            parts = []
+            while True:
+                n = f.readinto(b)
+                if not n:
+                    break
+                parts.append(bytes(b[:n]))
+            assert f._nreader is not None and f._nreader.source == "ipc"
+            assert f._nat.refills >= 20
+        assert b"".join(parts) == expect.tobytes()
         fs.close()
+        # the same bytes over the worker's native gRPC data port: HBM chunks staged D2H by the
+        # server's I/O threads, frames parsed by the native client
+        fs2 = FileSystem(conf=Configuration({"alluxio.user.file.passive.cache.enabled": "false",
+                                             "alluxio.user.short.circuit.enabled": "false"}),
+                         master_address=master)
+        with fs2.open_file("/ipc/f") as f:
+            got = f.read()
+            assert f._nreader.source == "remote"
+        assert got == expect.tobytes()
+        fs2.close()
     finally:
         p.stdin.write("\n")
         p.stdin.flush()

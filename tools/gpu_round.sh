@@ -99,6 +99,12 @@ for s in $STEPS; do
     hostipc)
       run worker_bench_ipc 300 python tools/worker_bench_host.py --threads 16 --transports ipc --duration 4s --warmup 1s --out "$OUT/worker_bench_ipc.jsonl"
       ;;
+    datapath)
+      run pytest_datapath 400 python -u -m pytest tests/test_ipc_gpu.py tests/test_data_server.py -x -v --timeout 120 --timeout-method thread
+      run wb_host_4k 900 python tools/worker_bench_host.py --threads 16,64,256 --transports grpc,ipc --duration 8s --warmup 2s --out "$OUT/worker_bench_host_native.jsonl"
+      run wb_host_1m 600 python tools/worker_bench_host.py --threads 16,64 --buffer-size 1m --transports grpc,ipc --duration 8s --warmup 2s --reader-buffer 4MB --out "$OUT/worker_bench_host_native_1m.jsonl"
+      run wb_host_grpcio 300 python tools/worker_bench_host.py --threads 16 --transports grpcio --duration 8s --warmup 2s --out "$OUT/worker_bench_host_native.jsonl"
+      ;;
     hostread)
       run worker_bench_host 900 python tools/worker_bench_host.py --threads 16,64,256 --duration 8s --warmup 2s --out "$OUT/worker_bench_host.jsonl"
       ;;

@@ -7,10 +7,14 @@ This harness starts a master + one worker whose MEM tier is HBM (``hbm:0``) in t
 runs ``alluxio_amd.stress.worker_bench --mode threads`` in a SEPARATE client process -- so every
 byte crosses a process boundary the way a Java client's does -- once per transport:
 
-* ``grpc``: short-circuit off; blocks stream through the worker's ``ReadBlock`` gRPC service
-  (chunked, ``offset_received`` flow control; the worker D2H-copies HBM pages into the reply);
+* ``grpc``: short-circuit off; blocks stream over gRPC ``ReadBlock`` from the worker's native data
+  port (csrc/data_server.cpp: HBM chunks DMA'd into pinned staging on the C++ I/O threads,
+  ``offset_received`` flow control) into the client's native reader (csrc/block_source.cpp:
+  HTTP/2 frames parsed into a chunk buffer; each ``read(buf)`` is a memcpy out of it);
 * ``ipc``: short-circuit on; the client maps the worker's HBM arena through HIP IPC
-  (``OpenDeviceBlock``) and copies each 4 KiB ``read(buf)`` out of it (the short-circuit path).
+  (``OpenDeviceBlock``), DMAs chunks D2H into a pinned buffer and serves each ``read(buf)`` from it;
+* ``grpcio``: the pre-native path for comparison -- the grpcio client's ``ReadBlock`` against the
+  worker's Python grpcio servicer (``alluxio.user.native.reader.enabled=false``).
 
     python tools/worker_bench_host.py --threads 32 --duration 10s --warmup 3s --out gpurun_out/wb.jsonl
 """
@@ -52,6 +56,7 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", default="3s")
     ap.add_argument("--transports", default="grpc,ipc")
     ap.add_argument("--tier", default="hbm:0", help="worker MEM tier dir (hbm:N or dram)")
+    ap.add_argument("--reader-buffer", default="1MB", help="alluxio.user.native.reader.buffer.size")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
 
@@ -73,15 +78,19 @@ def main(argv=None) -> int:
                       write_type="CACHE_THROUGH", block_size=parse_space_size(a.block_size))
         st = fs.get_status("/stress-worker-base/data")
         assert st.in_alluxio_percentage == 100
+        stats = c.workers[0].data_server.stats if c.workers[0].data_server is not None else None
         for transport in a.transports.split(","):
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "true" if transport == "ipc" else "false",
+                     "alluxio.user.native.reader.enabled": "false" if transport == "grpcio" else "true",
+                     "alluxio.user.native.reader.buffer.size": a.reader_buffer,
                      "alluxio.user.file.passive.cache.enabled": "false"}
             for t in a.threads.split(","):
                 args = ["--threads", t, "--file-size", a.file_size, "--buffer-size", a.buffer_size,
                         "--block-size", a.block_size, "--duration", a.duration, "--warmup", a.warmup,
                         "--mode", "threads"]
                 t0 = time.time()
+                s0 = (stats.streams, stats.bytes, stats.declined) if stats is not None else (0, 0, 0)
                 p = subprocess.run([sys.executable, "-c", CLIENT.format(root=ROOT, addr=c.master.address,
                                                                        args=args, props=props)],
                                    capture_output=True, text=True, timeout=600)
@@ -97,7 +106,12 @@ def main(argv=None) -> int:
                        "transport": transport, "tier": a.tier, "threads": int(t), "buffer": a.buffer_size,
                        "file_size": a.file_size, "block_size": a.block_size,
                        "throughput_MBps": round(r["throughput_MBps"], 1), "bytes": r["bytes"],
-                       "duration_s": r["duration_s"], "errors": r["errors"], "wall_s": round(time.time() - t0, 1)}
+                       "duration_s": r["duration_s"], "errors": r["errors"], "wall_s": round(time.time() - t0, 1),
+                       "reader_buffer": a.reader_buffer}
+                if stats is not None:
+                    row["data_server"] = {"native_streams": stats.streams - s0[0],
+                                          "native_bytes": stats.bytes - s0[1],
+                                          "bridged_streams": stats.declined - s0[2]}
                 print(json.dumps(row), flush=True)
                 rows.append(row)
                 if a.out:
