@@ -372,7 +372,8 @@ class FileInStream(io.RawIOBase):
             from ..ops.native import lib
             self._nat = lib().HostInStream(self.length, self.block_size,
                                            ctx.conf.get_bytes("alluxio.user.native.reader.buffer.size", "1MB"),
-                                           _native_opener(self))
+                                           _native_opener(self),
+                                           ctx.conf.get_bool("alluxio.user.native.reader.prefetch.enabled", "true"))
             # instance attribute: read(buf) loops call the C entry point directly
             self.readinto = self._nat.fast_readinto
 

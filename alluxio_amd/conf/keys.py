@@ -215,6 +215,9 @@ _k("USER_NATIVE_READER_ENABLED", "alluxio.user.native.reader.enabled", "true", S
    "DRAM, the in-process store or a native gRPC ReadBlock stream.")
 _k("USER_NATIVE_READER_BUFFER_SIZE", "alluxio.user.native.reader.buffer.size", "1MB", Scope.CLIENT,
    "Chunk buffer (pinned when a GPU is present) of the native host reader: bytes fetched per refill.")
+_k("USER_NATIVE_READER_PREFETCH_ENABLED", "alluxio.user.native.reader.prefetch.enabled", "true", Scope.CLIENT,
+   "The native host reader fetches the next chunk of the block into its second buffer on a native "
+   "thread pool while read(buf) calls drain the current one.")
 _k("USER_READ_BATCH_SIZE", "alluxio.user.read.batch.size", "256", Scope.CLIENT,
    "Max read requests coalesced into one page-gather launch.")
 _k("USER_FILE_READ_DEVICE", "alluxio.user.file.read.device", "cuda", Scope.CLIENT,

@@ -12,6 +12,8 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <functional>
 #include <map>
@@ -606,26 +608,108 @@ void GrpcBlockSource::maybe_ack(uint64_t offset) {
   h2::lib().resume_data(c.ng, c.sid);
 }
 
+// ---- prefetch pool ------------------------------------------------------------------------------
+namespace {
+
+class PrefetchPool {
+ public:
+  static PrefetchPool& get() {
+    static PrefetchPool* p = new PrefetchPool();   // never destroyed: threads outlive statics
+    return *p;
+  }
+  void submit(std::function<void()> fn) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (threads_.empty()) {
+        int n = want_ > 0 ? want_ : (int)std::min(16u, std::max(2u, std::thread::hardware_concurrency()));
+        for (int i = 0; i < n; ++i) threads_.emplace_back([this] { run(); });
+        for (auto& t : threads_) t.detach();
+      }
+      q_.push_back(std::move(fn));
+    }
+    cv_.notify_one();
+  }
+  void set_threads(int n) { want_ = n; }
+
+ private:
+  void run() {
+    for (;;) {
+      std::function<void()> fn;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        fn = std::move(q_.front());
+        q_.pop_front();
+      }
+      fn();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> threads_;
+  int want_ = 0;
+};
+
+}  // namespace
+
+void set_prefetch_threads(int n) { PrefetchPool::get().set_threads(n); }
+
+// One chunk read ahead: [lo, hi) of the file into `buf`, by a pool thread.
+struct HostInStream::Prefetch {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  int err_code = 0;
+  std::string err;
+  uint64_t lo = 0, hi = 0;
+  int buf = 0;
+  void finish(int code, std::string msg) {
+    std::lock_guard<std::mutex> g(mu);
+    err_code = code;
+    err = std::move(msg);
+    done = true;
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+  }
+  bool ready() {
+    std::lock_guard<std::mutex> g(mu);
+    return done;
+  }
+};
+
 // ---- HostInStream -----------------------------------------------------------------------------
-HostInStream::HostInStream(uint64_t length, uint64_t block_size, uint64_t chunk)
-    : length_(length), block_size_(block_size ? block_size : (64ull << 20)), chunk_(chunk ? chunk : (1u << 20)) {}
+HostInStream::HostInStream(uint64_t length, uint64_t block_size, uint64_t chunk, bool prefetch)
+    : length_(length), block_size_(block_size ? block_size : (64ull << 20)), chunk_(chunk ? chunk : (1u << 20)),
+      prefetch_(prefetch) {}
 
 HostInStream::~HostInStream() {
   drop_source();
-  if (buf_) {
-    if (pinned_) {
+  for (int i = 0; i < 2; ++i) {
+    uint8_t* b = bufs_[i];
+    if (!b) continue;
+    if (pinned_[i]) {
       std::lock_guard<std::mutex> g(g_buf_mu);
       if (g_buf_free_bytes + chunk_ <= kBufPoolCap) {
-        g_buf_free.emplace(chunk_, buf_);
+        g_buf_free.emplace(chunk_, b);
         g_buf_free_bytes += chunk_;
-        buf_ = nullptr;
+        b = nullptr;
       }
     }
-    if (buf_) {
-      if (pinned_) (void)hipHostFree(buf_);
-      else std::free(buf_);
+    if (b) {
+      if (pinned_[i]) (void)hipHostFree(b);
+      else std::free(b);
     }
   }
+}
+
+void HostInStream::cancel_prefetch() {
+  if (!pf_) return;
+  pf_->wait();
+  pf_.reset();
 }
 
 void HostInStream::set_source(int64_t idx, std::shared_ptr<BlockSource> src) {
@@ -636,10 +720,66 @@ void HostInStream::set_source(int64_t idx, std::shared_ptr<BlockSource> src) {
 }
 
 void HostInStream::drop_source() {
+  cancel_prefetch();
   if (cur_) cur_->close();
   cur_.reset();
   cur_idx_ = -1;
   buf_lo_ = buf_hi_ = 0;
+}
+
+void HostInStream::make_current(int i, uint64_t lo, uint64_t hi) {
+  cur_buf_ = i;
+  buf_ = bufs_[i];
+  buf_lo_ = lo;
+  buf_hi_ = hi;
+}
+
+// Reads the chunk after the current one (same block) into the other buffer on a pool thread.
+void HostInStream::schedule_prefetch() {
+  if (!prefetch_ || !cur_ || cur_->needs_gil() || pf_) return;
+  const uint64_t block_end = cur_start_ + cur_->length();
+  if (buf_hi_ >= block_end || buf_hi_ <= buf_lo_) return;
+  const int nb = 1 - cur_buf_;
+  if (!bufs_[nb]) bufs_[nb] = host_buffer_alloc(chunk_, &pinned_[nb]);
+  auto p = std::make_shared<Prefetch>();
+  p->lo = buf_hi_;
+  p->hi = std::min(buf_hi_ + chunk_, block_end);
+  p->buf = nb;
+  std::shared_ptr<BlockSource> src = cur_;
+  uint8_t* dst = bufs_[nb];
+  const uint64_t off = p->lo - cur_start_, n = p->hi - p->lo;
+  pf_ = p;
+  PrefetchPool::get().submit([p, src, dst, off, n] {
+    try {
+      src->read(off, n, dst);
+      p->finish(0, std::string());
+    } catch (const StoreError& e) {
+      p->finish(e.code, e.what());
+    } catch (const std::exception& e) {
+      p->finish(kErrIo, e.what());
+    }
+  });
+}
+
+bool HostInStream::try_swap() {
+  if (!pf_ || pos_ < pf_->lo || pos_ >= pf_->hi || !pf_->ready()) return false;
+  if (pf_->err_code) return false;          // the synchronous path reports (or retries) it
+  std::shared_ptr<Prefetch> p = std::move(pf_);
+  make_current(p->buf, p->lo, p->hi);
+  ++refills_;
+  ++pf_hits_;
+  schedule_prefetch();
+  return true;
+}
+
+uint64_t HostInStream::copy_buffered(uint8_t* dst, uint64_t n) {
+  if (!cur_) return 0;
+  if (!(pos_ >= buf_lo_ && pos_ < buf_hi_) && !try_swap()) return 0;
+  const uint64_t t = std::min(n, buf_hi_ - pos_);
+  std::memcpy(dst, buf_ + (pos_ - buf_lo_), t);
+  pos_ += t;
+  bytes_ += t;
+  return t;
 }
 
 uint64_t HostInStream::read_block_part(uint8_t* dst, uint64_t n) {
@@ -655,19 +795,37 @@ uint64_t HostInStream::read_block_part(uint8_t* dst, uint64_t n) {
     bytes_ += t;
     return t;
   }
+  if (pf_) {
+    const bool covers = pos_ >= pf_->lo && pos_ < pf_->hi;
+    pf_->wait();                              // the source is ours again after this
+    if (covers && !pf_->err_code) {
+      std::shared_ptr<Prefetch> p = std::move(pf_);
+      make_current(p->buf, p->lo, p->hi);
+      ++refills_;
+      ++pf_hits_;
+      schedule_prefetch();
+      const uint64_t t = std::min(n, buf_hi_ - pos_);
+      std::memcpy(dst, buf_ + (pos_ - buf_lo_), t);
+      pos_ += t;
+      bytes_ += t;
+      return t;
+    }
+    pf_.reset();                              // a seek elsewhere, or a failed read: redo it here
+  }
   if (cur_->direct() && n >= chunk_) {
     cur_->read(off, n, dst);   // big reads: no bounce through the chunk buffer
     pos_ += n;
     bytes_ += n;
     return n;
   }
-  if (!buf_) buf_ = host_buffer_alloc(chunk_, &pinned_);
+  if (!bufs_[cur_buf_]) bufs_[cur_buf_] = host_buffer_alloc(chunk_, &pinned_[cur_buf_]);
+  buf_ = bufs_[cur_buf_];
   const uint64_t fill = std::min(chunk_, blen - off);
   buf_lo_ = buf_hi_ = 0;
   cur_->read(off, fill, buf_);
   ++refills_;
-  buf_lo_ = pos_;
-  buf_hi_ = pos_ + fill;
+  make_current(cur_buf_, pos_, pos_ + fill);
+  schedule_prefetch();
   const uint64_t t = std::min(n, fill);
   std::memcpy(dst, buf_, t);
   pos_ += t;

@@ -116,12 +116,14 @@ class GrpcBlockSource : public BlockSource {
 // Pinned (device-mapped) host buffer for a chunk buffer (pooled by size; malloc without a GPU).
 uint8_t* host_buffer_alloc(uint64_t n, bool* pinned);
 
-// Sequential reader over a file's blocks with one chunk buffer: read(buf) calls inside the
-// buffered range are a memcpy; a miss refills up to `chunk` bytes from the block's source.  The
+// Sequential reader over a file's blocks with two chunk buffers: read(buf) calls inside the
+// current chunk are a memcpy; while they drain it, the next chunk of the block is prefetched into
+// the other buffer by a shared pool of native threads, so a reader thread reaching the end of a
+// chunk normally just swaps buffers (no I/O wait, and no GIL release on the Python side).  The
 // owner (bindings) supplies sources per block index and holds the GIL rules.
 class HostInStream {
  public:
-  HostInStream(uint64_t length, uint64_t block_size, uint64_t chunk);
+  HostInStream(uint64_t length, uint64_t block_size, uint64_t chunk, bool prefetch = true);
   ~HostInStream();
   inline bool fast(uint8_t* dst, uint64_t n) {
     if (pos_ >= buf_lo_ && pos_ + n <= buf_hi_) {
@@ -132,6 +134,11 @@ class HostInStream {
     }
     return false;
   }
+  // The prefetched chunk is complete and holds pos(): make it current (no waiting, no I/O).
+  bool try_swap();
+  // Copies up to n bytes at pos() that the current chunk (or a completed prefetch) already
+  // holds, within the current block; 0 when I/O is needed.  Never blocks.
+  uint64_t copy_buffered(uint8_t* dst, uint64_t n);
   // Copies up to n bytes at pos() from the current block's source (which must cover pos());
   // returns the bytes copied (> 0).  Called without the GIL unless the source needs it.
   uint64_t read_block_part(uint8_t* dst, uint64_t n);
@@ -146,17 +153,29 @@ class HostInStream {
   uint64_t block_size() const { return block_size_; }
   uint64_t bytes() const { return bytes_; }
   uint64_t refills() const { return refills_; }
+  uint64_t prefetch_hits() const { return pf_hits_; }
 
  private:
+  struct Prefetch;
+  void schedule_prefetch();
+  void cancel_prefetch();                 // waits for an in-flight prefetch, forgets it
+  void make_current(int i, uint64_t lo, uint64_t hi);
   uint64_t length_, block_size_, chunk_;
+  bool prefetch_;
   uint64_t pos_ = 0;
-  uint8_t* buf_ = nullptr;
-  bool pinned_ = false;
+  uint8_t* bufs_[2] = {nullptr, nullptr};
+  bool pinned_[2] = {false, false};
+  int cur_buf_ = 0;
+  uint8_t* buf_ = nullptr;             // bufs_[cur_buf_]
   uint64_t buf_lo_ = 0, buf_hi_ = 0;   // file offsets held by buf_
   int64_t cur_idx_ = -1;
   uint64_t cur_start_ = 0;
   std::shared_ptr<BlockSource> cur_;
-  uint64_t bytes_ = 0, refills_ = 0;
+  std::shared_ptr<Prefetch> pf_;       // in flight / completed prefetch into bufs_[1 - cur_buf_]
+  uint64_t bytes_ = 0, refills_ = 0, pf_hits_ = 0;
 };
+
+// Threads of the prefetch pool (0 = default: min(16, hardware threads)); takes effect on first use.
+void set_prefetch_threads(int n);
 
 }  // namespace amdx

@@ -52,8 +52,8 @@ struct PyInStream {
   HostInStream s;
   py::object opener;
   bool closed = false;
-  PyInStream(uint64_t length, uint64_t block_size, uint64_t chunk, py::object op)
-      : s(length, block_size, chunk), opener(std::move(op)) {}
+  PyInStream(uint64_t length, uint64_t block_size, uint64_t chunk, py::object op, bool prefetch)
+      : s(length, block_size, chunk, prefetch), opener(std::move(op)) {}
 
   void open_block(int64_t idx, bool failed) {
     py::object src = opener(idx, failed);
@@ -68,6 +68,12 @@ struct PyInStream {
     while (done < n) {
       const int64_t idx = (int64_t)(s.pos() / s.block_size());
       if (s.block_index() != idx || !s.source()) open_block(idx, false);
+      // what the current chunk (or the completed prefetch of the next) holds: no GIL release
+      const uint64_t have = s.copy_buffered(dst + done, n - done);
+      if (have) {
+        done += have;
+        continue;
+      }
       try {
         uint64_t got;
         if (s.source()->needs_gil()) {
@@ -219,13 +225,14 @@ void bind_data_path(py::module_& m) {
       .def(py::init<py::object, uint64_t>(), py::arg("reader"), py::arg("length"));
 
   py::class_<PyInStream>(m, "HostInStream")
-      .def(py::init<uint64_t, uint64_t, uint64_t, py::object>(), py::arg("length"), py::arg("block_size"),
-           py::arg("chunk"), py::arg("opener"))
+      .def(py::init<uint64_t, uint64_t, uint64_t, py::object, bool>(), py::arg("length"), py::arg("block_size"),
+           py::arg("chunk"), py::arg("opener"), py::arg("prefetch") = true)
       .def_property("pos", [](const PyInStream& s) { return s.s.pos(); },
                     [](PyInStream& s, uint64_t p) { s.s.seek(p); })
       .def_property_readonly("length", [](const PyInStream& s) { return s.s.length(); })
       .def_property_readonly("bytes_read", [](const PyInStream& s) { return s.s.bytes(); })
       .def_property_readonly("refills", [](const PyInStream& s) { return s.s.refills(); })
+      .def_property_readonly("prefetch_hits", [](const PyInStream& s) { return s.s.prefetch_hits(); })
       .def_property_readonly("closed", [](const PyInStream& s) { return s.closed; })
       .def("readinto", [](PyInStream& s, py::buffer b) {
              py::buffer_info bi = b.request(true);
@@ -301,5 +308,6 @@ void bind_data_path(py::module_& m) {
   m.def("revoke_channel", [](FrameRpcServer& srv, const std::string& cid) { srv.revoke_channel(cid); });
   m.def("set_require_channel_auth", [](FrameRpcServer& srv, bool on) { srv.set_require_channel_auth(on); });
   m.def("set_stream_window", [](FrameRpcServer& srv, uint32_t bytes) { srv.set_stream_window(bytes); });
+  m.def("set_prefetch_threads", &set_prefetch_threads, py::arg("threads"));
   m.def("listen_unix", [](FrameRpcServer& srv, const std::string& path) { srv.listen_unix(path); });
 }

@@ -146,6 +146,7 @@ class DataTransferServer(_Service):
     def __init__(self, open_read, open_write, host: str = "127.0.0.1", port: int = 0):
         self.open_read, self.open_write = open_read, open_write
         self.fault_flip_bits = False    # fault injection: corrupt sent data AFTER checksumming it
+        self.fault_truncate = False     # fault injection: end the block after its first packet
         super().__init__(host, port, _DataHandler)
         self.host = host
         self.uuid = f"alluxio-dn-{self.port}"
@@ -206,6 +207,8 @@ class _DataHandler(socketserver.BaseRequestHandler):
                     H.write_packet(s, off, seq, data, False)
                 off += len(data)
                 seq += 1
+                if srv.fault_truncate:
+                    break
             H.write_packet(s, off, seq, b"", True)
         finally:
             close = getattr(src, "close", None)

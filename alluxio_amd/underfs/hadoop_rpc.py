@@ -525,6 +525,11 @@ def _op_header(block, token, client_name):
     return h
 
 
+def dn_key(dn) -> str:
+    """Identity of a DataNode replica location (transfer address)."""
+    return f"{dn.id.ipAddr or dn.id.hostName}:{dn.id.xferPort}"
+
+
 def _connect_dn(dn, timeout):
     s = socket.create_connection((dn.id.ipAddr or dn.id.hostName, dn.id.xferPort), timeout=timeout)
     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
@@ -562,12 +567,18 @@ def read_packet(sock, bpc: int, verify: bool = True):
 class BlockReader:
     """Streams ``[offset, offset+length)`` of one located block from a DataNode (READ_BLOCK)."""
 
-    def __init__(self, located, offset: int, length: int, client_name: str, timeout: float = 60.0):
+    def __init__(self, located, offset: int, length: int, client_name: str, timeout: float = 60.0,
+                 exclude: set | None = None):
         self.located, self.remaining = located, length
+        self.dn_key = None
         last_err = None
         for dn in located.locs:            # try replicas in the order the NameNode sorted them
+            key = dn_key(dn)
+            if exclude and key in exclude:
+                continue
             try:
                 self._open(dn, offset, length, client_name, timeout)
+                self.dn_key = key
                 return
             except (OSError, ConnectionError) as e:
                 last_err = e
@@ -596,7 +607,9 @@ class BlockReader:
         while got < len(mv) and self.remaining > 0:
             if not len(self.pending):
                 if self.done:
-                    break
+                    # the DataNode ended the block before the requested range: never a silent EOF
+                    raise IOError(f"datanode ended block {self.located.b.blockId} with {self.remaining} "
+                                  f"requested bytes unsent")
                 hdr, data = read_packet(self.sock, self.bpc, self.verify)
                 if hdr.lastPacketInBlock or hdr.dataLen == 0:
                     self.done = True

@@ -13,6 +13,7 @@ the destination exists), setOwner/setMode (:663-697).  Reads stream packets from
 from __future__ import annotations
 
 import io
+import logging
 import posixpath
 import urllib.parse
 import uuid
@@ -22,6 +23,8 @@ from .base import (CreateOptions, DeleteOptions, ListOptions, MkdirsOptions, Ope
 from .hadoop_rpc import (FILE_IS_DIR, BlockReader, BlockWriter, NameNodeClient, RemoteException, translate)
 from .hadoop_rpc import hdfs as hdfs_pb
 from .registry import UnderFileSystemFactory, register_factory
+
+LOG = logging.getLogger(__name__)
 
 
 def _size(v, default: int) -> int:
@@ -102,6 +105,8 @@ class _HdfsReader(io.RawIOBase):
         self.pos = offset
         self.reader: BlockReader | None = None
         self.reader_pos = -1
+        self.dead: set[str] = set()     # replicas that failed mid-stream (DFSInputStream deadNodes)
+        self.last_err: BaseException | None = None
 
     def readable(self):
         return True
@@ -126,14 +131,37 @@ class _HdfsReader(io.RawIOBase):
     def readinto(self, b):
         if self.pos >= self.length:
             return 0
-        if self.reader is None or self.reader_pos != self.pos:
-            if self.reader is not None:
+        while True:
+            if self.reader is None or self.reader_pos != self.pos:
+                if self.reader is not None:
+                    self.reader.close()
+                    self.reader = None
+                lb = self._block_at(self.pos)
+                off = self.pos - lb.offset
+                # raises once every replica of the block is dead (or refuses)
+                try:
+                    self.reader = BlockReader(lb, off, lb.b.numBytes - off, self.ufs.nn.client_name,
+                                              self.ufs.timeout, exclude=self.dead)
+                except IOError as e:
+                    if self.last_err is None:
+                        raise
+                    raise IOError(f"{e}; the last replica read failed with: {self.last_err}") from self.last_err
+                self.reader_pos = self.pos
+            try:
+                n = self.reader.readinto(b)
+                break
+            except (IOError, OSError) as e:
+                # checksum error, truncated block or a lost connection: retry this position on the
+                # block's next replica (DFSInputStream.readBuffer -> seekToNewSource)
+                bad = self.reader.dn_key
+                self.last_err = e
+                LOG.warning("hdfs read of %s at %d failed on %s (%s); trying another replica", self.path, self.pos,
+                            bad, e)
                 self.reader.close()
-            lb = self._block_at(self.pos)
-            off = self.pos - lb.offset
-            self.reader = BlockReader(lb, off, lb.b.numBytes - off, self.ufs.nn.client_name, self.ufs.timeout)
-            self.reader_pos = self.pos
-        n = self.reader.readinto(b)
+                self.reader = None
+                if bad is None or bad in self.dead:
+                    raise
+                self.dead.add(bad)
         self.pos += n
         self.reader_pos = self.pos
         if self.reader.remaining == 0:

@@ -404,6 +404,14 @@ class _DataNode:
         self.port = self.server.port
 
     @property
+    def truncate_reads(self):
+        return self.server.fault_truncate
+
+    @truncate_reads.setter
+    def truncate_reads(self, v):
+        self.server.fault_truncate = v
+
+    @property
     def corrupt_reads(self):
         return self.server.fault_flip_bits
 

@@ -263,5 +263,14 @@ def test_in_process_host_reads_use_store_source(tmp_path):
                     break
                 parts.append(bytes(b[:n]))
             assert f._nat.refills >= 9
+            assert f._nat.prefetch_hits >= 5          # the next chunk was read ahead
         assert b"".join(parts) == data.tobytes()
+        # prefetch off: same bytes through synchronous refills only
+        from alluxio_amd.client.file_system import FileSystem
+        from alluxio_amd.conf import Configuration
+        nfs = FileSystem(conf=Configuration({"alluxio.user.native.reader.prefetch.enabled": "false"}),
+                         master_address=c.master.address)
+        with nfs.open_file("/p") as f:
+            assert f.read() == data.tobytes() and f._nat.prefetch_hits == 0
+        nfs.close()
         fs.close()

@@ -331,7 +331,8 @@ if rank == 0:
 dist.broadcast_object_list(box, src=0)
 w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, work_dir=work + "/w%%d" %% rank)
 w.start(start_heartbeats=False)
-plane = TransferPlane.establish(w.worker, rebuild_wait_s=3.0, timeout_s=30.0)
+# one block per round, so the death lands between rounds
+plane = TransferPlane.establish(w.worker, rebuild_wait_s=3.0, timeout_s=30.0, batch_bytes=1 << 20)
 fs = FileSystem(conf=conf.copy(), master_address=box[0])
 data = np.random.default_rng(20 + rank).integers(0, 256, 3 * (1 << 20) + 11, dtype=np.uint8)
 fs.write_file("/rb/f%%d" %% rank, data, write_type="MUST_CACHE")
@@ -341,11 +342,11 @@ dist.all_gather_object(allb, mine)
 blocks = [x for part in allb for x in part]
 if rank == world - 1:
     # this rank dies after the first round of the collective
-    orig = plane._scatter_into_pages
+    orig = plane._scatter_batches
     def dying(*a, **kw):
         r = orig(*a, **kw)
         os._exit(0)
-    plane._scatter_into_pages = dying
+    plane._scatter_batches = dying
 moved = plane.replicate_ring(blocks, 2) if %(method)r == "ring" else plane.replicate_all(blocks)
 alive = [r for r in range(world - 1)]
 if %(method)r == "ring":     # own + ring predecessor (in the rebuilt ring) blocks
@@ -371,7 +372,8 @@ def test_replicate_all_rebuilds_group_after_rank_death(tmp_path, method):
     """A rank dies in the middle of replicate_all / replicate_ring: the survivors' round fails,
     they agree on a new group through the rendezvous store and finish replicating among
     themselves (the ring runs 4 ranks with 2 copies, so only the dead rank's neighbours see the
-    point-to-point failure; the per-round failure all-reduce brings every survivor along)."""
+    point-to-point failure; the bounded waits plus the store's rebuild marker bring every
+    survivor along)."""
     world = 4 if method == "ring" else 3
     script = REBUILD_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path), "method": method}
     path = tmp_path / "rebuild.py"
@@ -421,7 +423,7 @@ if rank == 0:
 dist.broadcast_object_list(box, src=0)
 w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, work_dir=work + "/w%%d" %% rank)
 w.start(start_heartbeats=False)
-plane = TransferPlane.establish(w.worker)
+plane = TransferPlane.establish(w.worker, batch_bytes=%(batch)d)
 fs = FileSystem(conf=conf.copy(), master_address=box[0])
 size = (1 + rank) * (1 << 20) + 333 * rank + 5       # rank r owns ceil(size/2MB) blocks
 data = np.random.default_rng(40 + rank).integers(0, 256, size, dtype=np.uint8)
@@ -438,7 +440,7 @@ ok_prev = all(w.worker.read_bytes(b, 0, n) == pdata[i * (2 << 20):i * (2 << 20) 
               for i, (b, n, _) in enumerate(allb[prev]))
 held = {r: all(w.worker.has_block(b) for b, _, _ in allb[r]) for r in range(world)}
 print(json.dumps({"rank": rank, "moved": moved, "ok_prev": bool(ok_prev), "held": held,
-                  "expect": sum(n for _, n, _ in allb[prev])}), flush=True)
+                  "expect": sum(n for _, n, _ in allb[prev]), "rounds": plane.rounds}), flush=True)
 dist.barrier()
 fs.close(); w.stop()
 dist.barrier()
@@ -448,11 +450,14 @@ dist.destroy_process_group()
 """
 
 
-def test_replicate_ring_p2p_gloo(tmp_path):
+@pytest.mark.parametrize("batch", [256 << 20, 2 << 20])
+def test_replicate_ring_p2p_gloo(tmp_path, batch):
     """k-copy ring replication with point-to-point send/recv: with 2 copies each rank ends up
-    holding exactly its own and its predecessor's blocks (4 ranks, uneven block counts)."""
+    holding exactly its own and its predecessor's blocks (4 ranks, uneven block counts).  With
+    2 MiB batches the owners' blocks go one per round (several pipelined rounds); with 256 MiB
+    batches every owner's blocks travel packed in one round."""
     world = 4
-    script = RING_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path)}
+    script = RING_SCRIPT % {"root": ROOT, "port": _free_port(), "work": str(tmp_path), "batch": batch}
     path = tmp_path / "ring.py"
     path.write_text(script)
     procs = []
@@ -474,6 +479,7 @@ def test_replicate_ring_p2p_gloo(tmp_path):
         assert o["ok_prev"] and o["moved"] == o["expect"], o
         held = {int(k): v for k, v in o["held"].items()}
         assert held == {x: x in (r, (r - 1) % world) for x in range(world)}, o
+        assert o["rounds"] == (1 if batch > (8 << 20) else 3), o      # rank 3 owns 3 blocks
 
 
 def test_distributed_load_two_copies_uses_ring(tmp_path):

@@ -73,7 +73,7 @@ def test_multiblock_pipeline_positioned_reads_and_failover(dfs):
 
 
 def test_checksum_corruption_is_detected(dfs):
-    ufs = _ufs(dfs)
+    ufs = _ufs(dfs, **{"dfs.replication": "1"})     # one replica: nothing to fail over to
     with ufs.create("/c.bin") as f:
         f.write(b"x" * 5000)
     dfs.datanodes[0].corrupt_reads = True
@@ -83,6 +83,30 @@ def test_checksum_corruption_is_detected(dfs):
     dfs.datanodes[0].corrupt_reads = False
     with ufs.open("/c.bin") as f:
         assert f.read() == b"x" * 5000
+
+
+def test_truncated_or_corrupt_replica_fails_over_mid_stream(dfs):
+    """A DataNode that ends a block early, or whose bytes fail their checksum, is never a silent
+    short read: the reader moves to the block's next replica at the current position
+    (DFSInputStream deadNodes + seekToNewSource); with every replica bad the read raises."""
+    ufs = _ufs(dfs, **{"dfs.replication": "3"})
+    data = np.random.default_rng(9).integers(0, 256, (600 << 10) + 17, dtype=np.uint8).tobytes()
+    with ufs.create("/ft.bin") as f:
+        f.write(data)
+    dfs.datanodes[0].truncate_reads = True          # first replica: lastPacketInBlock after 1 packet
+    dfs.datanodes[1].corrupt_reads = True           # second replica: flipped bits
+    try:
+        with ufs.open("/ft.bin") as f:
+            assert f.read() == data
+        with ufs.open("/ft.bin", OpenOptions(offset=300_001)) as f:
+            assert f.read(100_000) == data[300_001:400_001]
+        dfs.datanodes[2].truncate_reads = True      # no good replica left
+        with pytest.raises(IOError):
+            with ufs.open("/ft.bin") as f:
+                f.read()
+    finally:
+        for dn in dfs.datanodes:
+            dn.truncate_reads = dn.corrupt_reads = False
 
 
 def test_listing_pages_mkdirs_delete_rename_semantics(dfs):

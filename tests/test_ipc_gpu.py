@@ -165,6 +165,54 @@ if %(collective)r:
             good = good and w.worker.read_bytes(bid, 0, n) == exp[i * (8 << 20):i * (8 << 20) + n].tobytes()
     res.update({"gathered": moved, "gather_ok": bool(good),
                 "gather_expect": sum(n for _b, n, r in blocks if r != rank)})
+if %(extra)r:
+    from alluxio_amd.client.batch_reader import RemoteRingReader
+    from alluxio_amd.client.context import worker_address_str
+    from alluxio_amd.parallel.peer import fan_out
+    me_addr = worker_address_str(w.worker.address)
+    addrs = [None] * world
+    dist.all_gather_object(addrs, me_addr)
+    # fan_out: rank 0 writes one block; every other rank pulls it over xGMI (PeerTransfer)
+    fdata = np.random.default_rng(77).integers(0, 256, (5 << 20) + 3, dtype=np.uint8)
+    if rank == 0:
+        fs.write_file("/gp/fo", fdata, write_type="MUST_CACHE")
+        fb = fs.get_status("/gp/fo").info.fileBlockInfos[0].blockInfo
+        errs = fan_out(me_addr, addrs[1:], fb.blockId, fb.length, fs.ctx.worker_stub)
+        assert not errs, errs
+    dist.barrier()
+    fb = fs.get_status("/gp/fo").info.fileBlockInfos[0].blockInfo
+    fan_ok = w.worker.has_block(fb.blockId) and w.worker.read_bytes(fb.blockId, 0, fb.length) == fdata.tobytes()
+    # RemoteRingReader on this GPU over the next rank's HBM (the file it cached)
+    streams, depth, buf = 8, 32, 4096
+    ring = torch.empty((streams, depth, buf), dtype=torch.uint8, device="cuda")
+    ring_ok = True
+    with RemoteRingReader(fs, "/gp/f%%d" %% other, ring, addrs[other], start_offsets=[s * (1 << 20) for s in range(streams)]) as rr:
+        for _ in range(3):
+            rr.step()
+        torch.cuda.synchronize()
+        for s_ in range(streams):
+            for k_ in (0, depth - 1):
+                off, nb = rr.last_call(s_, k_)
+                ring_ok = ring_ok and np.array_equal(ring[s_, k_, :nb].cpu().numpy(), odata[off:off + nb])
+    res.update({"fan_ok": bool(fan_ok), "remote_ring_ok": bool(ring_ok)})
+    if world >= 3:
+        # replicate_ring, several rounds (one 8 MiB block per batch) pipelined over RCCL send/recv
+        plane.batch_bytes = 8 << 20
+        rdata = np.random.default_rng(60 + rank).integers(0, 256, (24 << 20) + 7, dtype=np.uint8)
+        fs.write_file("/gp/r%%d" %% rank, torch.from_numpy(rdata).to("cuda"), write_type="MUST_CACHE")
+        torch.cuda.synchronize()
+        mine = [(b.blockInfo.blockId, b.blockInfo.length, rank) for b in fs.get_status("/gp/r%%d" %% rank).info.fileBlockInfos]
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        rblocks = [x for part in allr for x in part]
+        rmoved = plane.replicate_ring(rblocks, 2)
+        pred = (rank - 1) %% world
+        exp = np.random.default_rng(60 + pred).integers(0, 256, (24 << 20) + 7, dtype=np.uint8)
+        rgood = all(w.worker.read_bytes(b, 0, n) == exp[i * (8 << 20):i * (8 << 20) + n].tobytes()
+                    for i, (b, n, _o) in enumerate(allr[pred]))
+        rnot = not any(w.worker.has_block(b) for r2 in range(world) if r2 not in (rank, pred) for b, _n, _o in allr[r2])
+        res.update({"ring_ok": bool(rgood and rnot), "ring_moved": rmoved, "ring_rounds": plane.rounds,
+                    "ring_agreements": plane.agreements})
 print(json.dumps(res), flush=True)
 dist.barrier()
 fs.close(); w.stop()
@@ -175,7 +223,7 @@ dist.destroy_process_group()
 """
 
 
-def _run_plane(tmp_path, backend: str, collective: bool, world: int = 2):
+def _run_plane(tmp_path, backend: str, collective: bool, world: int = 2, extra: bool = False):
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -183,7 +231,7 @@ def _run_plane(tmp_path, backend: str, collective: bool, world: int = 2):
     s.close()
     path = tmp_path / "plane.py"
     path.write_text(PLANE % {"root": ROOT, "port": port, "work": str(tmp_path), "backend": backend,
-                             "collective": collective})
+                             "collective": collective, "extra": extra})
     procs = [subprocess.Popen([sys.executable, str(path)], env=dict(os.environ, RANK=str(r), WORLD_SIZE=str(world)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
     outs = []
@@ -224,6 +272,107 @@ def test_transfer_plane_two_gpus_xgmi_and_rccl(gpu, tmp_path):
         assert o["device"] == o["rank"] and other in o["peer_devices"], o
         assert o["xgmi"] == o["pulled"] and o["stream"] == 0 and o["failures"] == 0, o
         assert o["gather_ok"] and o["gathered"] == o["gather_expect"], o
+
+
+@pytest.mark.gpu
+def test_multi_gpu_fan_out_remote_ring_and_replicate_ring(gpu, tmp_path):
+    """One rank per GPU (2..4 GPUs) over RCCL: fan_out of a fresh block to every peer (xGMI pulls
+    via PeerTransfer), RemoteRingReader on each GPU over the next GPU's HBM, and -- with >= 3
+    GPUs -- a multi-round pipelined replicate_ring (copies=2) that leaves each block on exactly its
+    owner and successor."""
+    import torch
+    n = min(torch.cuda.device_count(), 4)
+    if n < 2:
+        pytest.skip("needs two GPUs")
+    outs = _run_plane(tmp_path, "nccl", True, world=n, extra=True)
+    for o in outs:
+        assert o["ok"] and o["gather_ok"], o
+        assert o["fan_ok"] and o["remote_ring_ok"], o
+        if n >= 3:
+            assert o["ring_ok"] and o["ring_moved"] == (24 << 20) + 7 and o["ring_rounds"] >= 3, o
+
+
+NCCL_DEATH = r"""
+import os, sys, json
+sys.path.insert(0, %(root)r)
+import numpy as np, torch, torch.distributed as dist
+from alluxio_amd.conf import Configuration
+from alluxio_amd.master.process import AlluxioMasterProcess
+from alluxio_amd.worker.process import AlluxioWorkerProcess
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.parallel.transfer import TransferPlane
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(rank)
+dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%(port)d", rank=rank, world_size=world)
+work = %(work)r
+conf = Configuration({"alluxio.master.journal.folder": work + "/journal",
+    "alluxio.worker.tieredstore.level0.dirs.path": "hbm:%%d" %% rank, "alluxio.worker.tieredstore.level0.dirs.quota": "256MB",
+    "alluxio.worker.hbm.page.size": "1MB", "alluxio.user.block.size.bytes.default": "4MB"})
+box = [None]
+if rank == 0:
+    m = AlluxioMasterProcess(conf, host="127.0.0.1", port=0, root_ufs=work + "/ufs"); box[0] = m.start(start_heartbeats=False)
+dist.broadcast_object_list(box, src=0)
+w = AlluxioWorkerProcess(conf.copy(), master_address=box[0], port=0, device=rank, work_dir=work + "/w%%d" %% rank)
+w.start(start_heartbeats=False)
+plane = TransferPlane.establish(w.worker, rebuild_wait_s=3.0, timeout_s=20.0, batch_bytes=4 << 20)
+fs = FileSystem(conf=conf.copy(), master_address=box[0])
+data = np.random.default_rng(20 + rank).integers(0, 256, (12 << 20) + 11, dtype=np.uint8)
+fs.write_file("/rb/f%%d" %% rank, data, write_type="MUST_CACHE")
+mine = [(b.blockInfo.blockId, b.blockInfo.length, rank) for b in fs.get_status("/rb/f%%d" %% rank).info.fileBlockInfos]
+allb = [None] * world
+dist.all_gather_object(allb, mine)
+blocks = [x for part in allb for x in part]
+if rank == world - 1:
+    orig = plane._scatter_batches
+    def dying(*a, **kw):
+        r = orig(*a, **kw)
+        torch.cuda.synchronize()
+        os._exit(0)           # dies after posting its first round
+    plane._scatter_batches = dying
+moved = plane.%(method)s
+alive = list(range(world - 1))
+have = all(w.worker.has_block(b) for b, _, o in blocks if o in alive) if %(method)r.startswith("replicate_all") else True
+print(json.dumps({"rank": rank, "moved": moved, "rebuilds": plane.rebuilds, "members": plane.members,
+                  "have_alive": have}), flush=True)
+os._exit(0)
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["replicate_all(blocks)", "replicate_ring(blocks, 2)"])
+def test_nccl_rank_death_rebuilds_plane(gpu, tmp_path, method):
+    """RCCL analogue of test_distributed.py::test_replicate_all_rebuilds_group_after_rank_death:
+    one GPU rank dies mid-collective; the survivors' bounded waits fail (or see the rebuild
+    marker), the communicator is aborted, and they finish on a rebuilt RCCL group without it --
+    no survivor is torn down by the watchdog."""
+    import socket
+
+    import torch
+    world = min(torch.cuda.device_count(), 4)
+    if world < 3:
+        pytest.skip("needs three GPUs")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    path = tmp_path / "death.py"
+    path.write_text(NCCL_DEATH % {"root": ROOT, "port": port, "work": str(tmp_path), "method": method})
+    procs = [subprocess.Popen([sys.executable, str(path)], env=dict(os.environ, RANK=str(r), WORLD_SIZE=str(world)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = []
+    for r, p in enumerate(procs):
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("rank death test timed out")
+        if r < world - 1:
+            assert p.returncode == 0, err[-3000:]
+            outs.append(json.loads(out.strip().splitlines()[-1]))
+    for o in outs:
+        assert o["rebuilds"] >= 1 and o["members"] == list(range(world - 1)), o
+        assert o["have_alive"], o
 
 
 @pytest.mark.gpu
