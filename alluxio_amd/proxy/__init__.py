@@ -447,6 +447,18 @@ class PathsStreams:
 
 
 class ProxyServer:
+    def advertised_address(self) -> str:
+        """host:port redirects point at: ``alluxio.proxy.web.hostname`` when configured, else the
+        bound address (the machine's hostname for a wildcard bind)."""
+        import socket
+        conf = getattr(self.s3.fs.ctx, "conf", None)
+        name = conf.get_raw("alluxio.proxy.web.hostname") if conf is not None else None
+        if not name:
+            name = self.httpd.server_address[0]
+            if name in ("0.0.0.0", "", "::"):
+                name = socket.gethostname()
+        return f"{name}:{self.port}"
+
     def __init__(self, fs, host: str = "127.0.0.1", port: int = 0, write_type: str = "CACHE_THROUGH"):
         from .webhdfs import WebHdfsGateway
         self.s3 = S3Handler(fs, write_type)
@@ -501,7 +513,9 @@ class ProxyServer:
                 q = {k: v[-1] for k, v in parse_qs(u.query, keep_blank_values=True).items()}
                 path = unquote(u.path)
                 if path == "/webhdfs/v1" or path.startswith("/webhdfs/v1/"):
-                    host = self.headers.get("Host") or f"{outer.httpd.server_address[0]}:{outer.port}"
+                    # redirects name this proxy, never the client-supplied Host header (an
+                    # open redirect that would send CREATE data anywhere)
+                    host = outer.advertised_address()
                     target = "/" + path[len("/webhdfs/v1"):].lstrip("/")
                     status, headers, body = outer.webhdfs.handle(method, target, q, host, self._body_iter)
                     if method == "HEAD":

@@ -71,6 +71,9 @@ class _Service:
 
 
 # ---- NameNode (Hadoop IPC v9) -----------------------------------------------------------------------
+MAX_IPC_FRAME = 64 << 20     # Hadoop's ipc.maximum.data.length default
+
+
 class IpcServer(_Service):
     """Serves ``ClientProtocol`` calls: ``dispatch(method, request_bytes, user)`` returns the
     response message or raises :class:`RpcError`."""
@@ -96,6 +99,10 @@ class _IpcHandler(socketserver.BaseRequestHandler):
             user = "hadoop"
             while True:
                 (n,) = struct.unpack(">I", bytes(H.recv_exact(s, 4)))
+                if n > MAX_IPC_FRAME:           # ipc.maximum.data.length: refuse, do not allocate
+                    LOG.warning("hdfs gateway: %d-byte RPC frame from %s exceeds %d; closing", n,
+                                self.client_address, MAX_IPC_FRAME)
+                    return
                 frame = H.recv_exact(s, n)
                 rh, pos = H.parse_delimited(frame, 0, common.RpcRequestHeaderProto)
                 if rh.callId == H.CONNECTION_CONTEXT_CALL_ID:
@@ -356,8 +363,14 @@ class HdfsGateway:
     """NameNode + DataNode endpoints over an Alluxio :class:`FileSystem` client."""
 
     def __init__(self, fs, host: str = "127.0.0.1", rpc_port: int = 0, data_port: int = 0,
-                 advertised_host: str | None = None, write_type: str = "CACHE_THROUGH"):
-        self.fs, self.write_type = fs, write_type
+                 advertised_host: str | None = None, write_type: str = "CACHE_THROUGH", impersonate: bool = True):
+        self._default_fs, self.write_type = fs, write_type
+        # NameNode calls run as the Hadoop caller (IpcConnectionContext effectiveUser): one client
+        # per user, so the master authorizes -- and records as owner -- that user, not the proxy's
+        self.impersonate = impersonate
+        self._tls = threading.local()
+        self._user_fs: "collections.OrderedDict[str, object]" = collections.OrderedDict()
+        self._user_fs_cap = 64
         self.adv = advertised_host or host
         self.lock = threading.Lock()
         self.open_files: dict[str, _OpenFile] = {}
@@ -374,9 +387,44 @@ class HdfsGateway:
     def port(self) -> int:
         return self.rpc.port
 
+    @property
+    def fs(self):
+        """The client of the current NameNode call's user (the proxy's own outside a call)."""
+        return getattr(self._tls, "fs", None) or self._default_fs
+
+    def _fs_for(self, user: str):
+        base = self._default_fs
+        if not self.impersonate or not user or user == base.ctx.user:
+            return base
+        with self.lock:
+            fs = self._user_fs.get(user)
+            if fs is not None:
+                self._user_fs.move_to_end(user)
+                return fs
+        from ..client.file_system import FileSystem
+        from ..client.context import FileSystemContext
+        ctx = FileSystemContext(base.ctx.conf, ",".join(base.ctx.master_addresses), user)
+        fs = FileSystem(context=ctx)
+        with self.lock:
+            self._user_fs[user] = fs
+            while len(self._user_fs) > self._user_fs_cap:
+                _u, old = self._user_fs.popitem(last=False)
+                try:
+                    old.close()
+                except Exception:  # noqa: BLE001
+                    pass
+        return fs
+
     def stop(self) -> None:
         self.rpc.stop()
         self.data.stop()
+        with self.lock:
+            users, self._user_fs = list(self._user_fs.values()), collections.OrderedDict()
+        for fs in users:
+            try:
+                fs.close()
+            except Exception:  # noqa: BLE001
+                pass
         with self.lock:
             files, self.open_files = list(self.open_files.values()), {}
         for of in files:
@@ -392,7 +440,11 @@ class HdfsGateway:
         if fn is None:
             raise RpcError("org.apache.hadoop.ipc.RpcNoSuchMethodException", f"Unknown method {method} called on "
                            f"{H.CLIENT_PROTOCOL} protocol.")
-        return fn(body, user)
+        self._tls.fs = self._fs_for(user)
+        try:
+            return fn(body, user)
+        finally:
+            self._tls.fs = None
 
     def _status(self, st, name: bytes):
         info = st.info

@@ -89,3 +89,45 @@ def test_block_cut_off_mid_stream_fails_the_file(gw):
     with pytest.raises(H.RemoteException, match="failed mid-stream"):
         nn.complete("/cut", None, st.fileId)
     assert not fs.exists("/cut")
+
+
+def test_gateway_calls_run_as_the_hadoop_caller(tmp_path):
+    """NameNode calls run as the IpcConnectionContext user, not the proxy's: a Hadoop client
+    connecting as alice owns what she creates and is refused what she may not touch."""
+    from alluxio_amd.utils import exceptions as ex
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "dram",
+            "alluxio.security.authorization.permission.enabled": "true"}
+    with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=str(tmp_path / "c")) as c:
+        fs = c.client()
+        fs.create_directory("/shared")
+        fs.set_attribute("/shared", mode=0o777)          # (create applies the umask)
+        fs.create_directory("/private", mode=0o755)
+        g = HdfsGateway(fs)
+        nn = H.NameNodeClient("127.0.0.1", g.port, user="alice")
+        try:
+            assert nn.mkdirs("/shared/a", 0o755, False)
+            assert fs.get_status("/shared/a").info.owner == "alice"
+            with pytest.raises(Exception) as ei:
+                nn.mkdirs("/private/b", 0o755, False)
+            assert "ermission" in str(ei.value) or "AccessControl" in str(ei.value), ei.value
+            assert not fs.exists("/private/b")
+            with pytest.raises(Exception):
+                nn.delete("/private", True)
+            assert fs.exists("/private")
+        finally:
+            nn.close()
+            g.stop()
+            fs.close()
+
+
+def test_gateway_refuses_oversized_rpc_frames(gw):
+    import socket
+    import struct
+    g, _fs = gw
+    s = socket.create_connection(("127.0.0.1", g.port))
+    try:
+        s.sendall(b"hrpc" + bytes([H.IPC_VERSION, 0, H.AUTH_NONE]) + struct.pack(">I", 1 << 30))
+        s.settimeout(5)
+        assert s.recv(1) == b""                  # closed without reading (or allocating) 1 GiB
+    finally:
+        s.close()

@@ -97,3 +97,16 @@ def test_ufs_contract_through_the_gateway(gateway):
                            properties={"alluxio.underfs.webhdfs.user": "u"})
     assert res["failed"] == [], out.getvalue()[-3000:]
     assert len(res["passed"]) >= 40
+
+
+def test_redirect_ignores_spoofed_host_header(gateway):
+    """The 307 of OPEN/CREATE names the proxy itself, not whatever Host the request carried (an
+    open redirect would send a client -- and its CREATE body -- to an arbitrary server)."""
+    fs, base, port = gateway
+    fs.write_file("/r.bin", b"abc")
+    for method, op in (("put", "CREATE"), ("get", "OPEN")):
+        r = getattr(requests, method)(base + "/r.bin", params={"op": op, "overwrite": "true"},
+                                      headers={"Host": "evil.example:666"}, allow_redirects=False)
+        assert r.status_code == 307, r.text
+        loc = r.headers["Location"]
+        assert "evil.example" not in loc and f":{port}/" in loc, loc

@@ -111,9 +111,15 @@ for s in $STEPS; do
       run wb_host_4k_pf2m 900 python tools/worker_bench_host.py --threads 16,256 --transports grpc,ipc --duration 8s --warmup 2s --reader-buffer 2MB --out "$OUT/worker_bench_host_prefetch.jsonl"
       run wb_host_1m_pf 600 python tools/worker_bench_host.py --threads 16,64 --buffer-size 1m --transports grpc,ipc --duration 8s --warmup 2s --reader-buffer 4MB --out "$OUT/worker_bench_host_prefetch_1m.jsonl"
       ;;
+    prefetchab)
+      for pf in true false; do
+        run wb_host_ab_$pf 900 python tools/worker_bench_host.py --threads 16,256 --transports grpc,ipc --duration 8s --warmup 2s --client-prop alluxio.user.native.reader.prefetch.enabled=$pf --out "$OUT/worker_bench_host_prefetch_ab.jsonl"
+      done
+      ;;
     replicate)
       run replicate_bench 600 python tools/replicate_bench.py --ranks 2 --blocks 16 --block-size 64m --batches 64m,256m,1g --out "$OUT/replicate_bench.jsonl"
-      run rocprof_replicate 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_replicate" -o repl --output-format csv -- python3 tools/replicate_bench.py --ranks 2 --blocks 8 --block-size 64m --batches 256m --methods ring --reps 1
+      run replicate_bench3 600 python tools/replicate_bench.py --ranks 3 --blocks 8 --block-size 64m --batches 64m,512m --methods ring --out "$OUT/replicate_bench.jsonl"
+      run rocprof_replicate 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_replicate" -o repl --output-format csv -- python3 tools/replicate_bench.py --ranks 3 --blocks 8 --block-size 64m --batches 64m --methods ring --reps 1
       ;;
     hostread)
       run worker_bench_host 900 python tools/worker_bench_host.py --threads 16,64,256 --duration 8s --warmup 2s --out "$OUT/worker_bench_host.jsonl"

@@ -112,7 +112,7 @@ def rank_main(a) -> None:
     w.stop()
     if m is not None:
         m.stop()
-    os._exit(0)
+    dist.destroy_process_group()      # a normal exit: profilers flush their traces at exit
 
 
 def main(argv=None) -> int:

@@ -57,6 +57,7 @@ def main(argv=None) -> int:
     ap.add_argument("--transports", default="grpc,ipc")
     ap.add_argument("--tier", default="hbm:0", help="worker MEM tier dir (hbm:N or dram)")
     ap.add_argument("--reader-buffer", default="1MB", help="alluxio.user.native.reader.buffer.size")
+    ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
 
@@ -85,6 +86,7 @@ def main(argv=None) -> int:
                      "alluxio.user.native.reader.enabled": "false" if transport == "grpcio" else "true",
                      "alluxio.user.native.reader.buffer.size": a.reader_buffer,
                      "alluxio.user.file.passive.cache.enabled": "false"}
+            props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             for t in a.threads.split(","):
                 args = ["--threads", t, "--file-size", a.file_size, "--buffer-size", a.buffer_size,
                         "--block-size", a.block_size, "--duration", a.duration, "--warmup", a.warmup,
@@ -107,7 +109,7 @@ def main(argv=None) -> int:
                        "file_size": a.file_size, "block_size": a.block_size,
                        "throughput_MBps": round(r["throughput_MBps"], 1), "bytes": r["bytes"],
                        "duration_s": r["duration_s"], "errors": r["errors"], "wall_s": round(time.time() - t0, 1),
-                       "reader_buffer": a.reader_buffer}
+                       "reader_buffer": a.reader_buffer, "client_props": a.client_prop}
                 if stats is not None:
                     row["data_server"] = {"native_streams": stats.streams - s0[0],
                                           "native_bytes": stats.bytes - s0[1],
