@@ -99,9 +99,13 @@ class LocalBlockReader(BlockReader):
         C = lib()
         info = self.w.native.block_info(self.block_id)
         device = self.w.native.dir_spec(info.dir).kind == C.DirKind.DEVICE
-        return C.StoreSource(self.w.native, self.block_id, self.length, device)
+        self._src = C.StoreSource(self.w.native, self.block_id, self.length, device)
+        return self._src
 
     def close(self):
+        src, self._src = getattr(self, "_src", None), None
+        if src is not None and src.bytes:
+            self.w._count_read(src.bytes, 0)      # reads served natively still count as worker I/O
         if self.lock_id is not None:
             try:
                 self.w.unlock(self.lock_id)

@@ -126,6 +126,23 @@ uint8_t* host_buffer_alloc(uint64_t n, bool* pinned) {
   return static_cast<uint8_t*>(p);
 }
 
+void host_buffer_release(uint8_t* p, uint64_t n, bool pinned) {
+  if (!p) return;
+  if (pinned) {
+    {
+      std::lock_guard<std::mutex> g(g_buf_mu);
+      if (g_buf_free_bytes + n <= kBufPoolCap) {
+        g_buf_free.emplace(n, p);
+        g_buf_free_bytes += n;
+        return;
+      }
+    }
+    (void)hipHostFree(p);
+    return;
+  }
+  std::free(p);
+}
+
 // ---- DeviceArenaSource ------------------------------------------------------------------------
 DeviceArenaSource::DeviceArenaSource(uint64_t base, std::vector<int64_t> pages, uint64_t page_size, uint64_t length,
                                      int device)
@@ -166,11 +183,12 @@ void StoreSource::read(uint64_t off, uint64_t n, uint8_t* dst) {
   std::vector<ReadReq> rq{ReadReq{block_, off, n, reinterpret_cast<uint64_t>(dst), (int)MemKind::kHost}};
   if (!device_) {
     store_->read_batch(rq, 0, false);
-    return;
+  } else {
+    hipStream_t st = reader_stream(store_->device());
+    store_->read_batch(rq, reinterpret_cast<uint64_t>(st), false);
+    wait_stream(st);
   }
-  hipStream_t st = reader_stream(store_->device());
-  store_->read_batch(rq, reinterpret_cast<uint64_t>(st), false);
-  wait_stream(st);
+  bytes_.fetch_add(n, std::memory_order_relaxed);
 }
 
 // ---- GrpcBlockSource: ReadBlock over HTTP/2 ---------------------------------------------------
@@ -688,22 +706,7 @@ HostInStream::HostInStream(uint64_t length, uint64_t block_size, uint64_t chunk,
 
 HostInStream::~HostInStream() {
   drop_source();
-  for (int i = 0; i < 2; ++i) {
-    uint8_t* b = bufs_[i];
-    if (!b) continue;
-    if (pinned_[i]) {
-      std::lock_guard<std::mutex> g(g_buf_mu);
-      if (g_buf_free_bytes + chunk_ <= kBufPoolCap) {
-        g_buf_free.emplace(chunk_, b);
-        g_buf_free_bytes += chunk_;
-        b = nullptr;
-      }
-    }
-    if (b) {
-      if (pinned_[i]) (void)hipHostFree(b);
-      else std::free(b);
-    }
-  }
+  for (int i = 0; i < 2; ++i) host_buffer_release(bufs_[i], chunk_, pinned_[i]);
 }
 
 void HostInStream::cancel_prefetch() {

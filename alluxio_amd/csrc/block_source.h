@@ -17,6 +17,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <atomic>
 #include <memory>
 #include <string>
 #include <vector>
@@ -76,11 +77,14 @@ class StoreSource : public BlockSource {
   StoreSource(BlockStore* store, int64_t block_id, uint64_t length, bool device_tier);
   void read(uint64_t off, uint64_t n, uint8_t* dst) override;
   bool direct() const override { return !device_; }
+  // bytes served so far (the worker's BytesReadAlluxio for in-process readers)
+  uint64_t bytes() const { return bytes_.load(std::memory_order_relaxed); }
 
  private:
   BlockStore* store_;
   int64_t block_;
   bool device_;
+  std::atomic<uint64_t> bytes_{0};
 };
 
 // A block streamed from a worker's data port over gRPC: ReadBlock on HTTP/2 (h2c, prior
@@ -115,6 +119,8 @@ class GrpcBlockSource : public BlockSource {
 
 // Pinned (device-mapped) host buffer for a chunk buffer (pooled by size; malloc without a GPU).
 uint8_t* host_buffer_alloc(uint64_t n, bool* pinned);
+// Gives a buffer of host_buffer_alloc(n) back (pinned ones to the pool).
+void host_buffer_release(uint8_t* p, uint64_t n, bool pinned);
 
 // Sequential reader over a file's blocks with two chunk buffers: read(buf) calls inside the
 // current chunk are a memcpy; while they drain it, the next chunk of the block is prefetched into

@@ -1,5 +1,6 @@
 #include "cpu_codecs.h"
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -102,6 +103,66 @@ static uint32_t x8nmodp(uint64_t n) {
 
 uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
   return multmodp(x8nmodp(len_b), crc_a) ^ crc_b;
+}
+
+static inline void put_be32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 24);
+  p[1] = (uint8_t)(v >> 16);
+  p[2] = (uint8_t)(v >> 8);
+  p[3] = (uint8_t)v;
+}
+
+#if defined(__x86_64__)
+// Four full chunks of `bpc` bytes (bpc % 8 == 0) at once: independent CRC32 chains overlap the
+// instruction's 3-cycle latency.
+__attribute__((target("sse4.2"))) static void crc32c_x4(const uint8_t* p, size_t bpc, uint32_t out[4]) {
+  uint64_t c0 = 0xFFFFFFFFu, c1 = 0xFFFFFFFFu, c2 = 0xFFFFFFFFu, c3 = 0xFFFFFFFFu;
+  const uint8_t *p0 = p, *p1 = p + bpc, *p2 = p + 2 * bpc, *p3 = p + 3 * bpc;
+  for (size_t i = 0; i < bpc; i += 8) {
+    uint64_t v0, v1, v2, v3;
+    std::memcpy(&v0, p0 + i, 8);
+    std::memcpy(&v1, p1 + i, 8);
+    std::memcpy(&v2, p2 + i, 8);
+    std::memcpy(&v3, p3 + i, 8);
+    c0 = __builtin_ia32_crc32di(c0, v0);
+    c1 = __builtin_ia32_crc32di(c1, v1);
+    c2 = __builtin_ia32_crc32di(c2, v2);
+    c3 = __builtin_ia32_crc32di(c3, v3);
+  }
+  out[0] = ~(uint32_t)c0;
+  out[1] = ~(uint32_t)c1;
+  out[2] = ~(uint32_t)c2;
+  out[3] = ~(uint32_t)c3;
+}
+#endif
+
+void crc32c_chunks_be(const uint8_t* data, size_t n, uint32_t bpc, uint8_t* out) {
+  size_t off = 0, i = 0;
+#if defined(__x86_64__)
+  if (have_sse42() && bpc % 8 == 0) {
+    uint32_t c[4];
+    for (; off + 4 * (size_t)bpc <= n; off += 4 * (size_t)bpc, i += 4) {
+      crc32c_x4(data + off, bpc, c);
+      for (int k = 0; k < 4; ++k) put_be32(out + 4 * (i + k), c[k]);
+    }
+  }
+#endif
+  for (; off < n; off += bpc, ++i) put_be32(out + 4 * i, crc32c_sw(data + off, std::min<size_t>(bpc, n - off), 0));
+}
+
+int64_t crc32c_chunks_verify(const uint8_t* data, size_t n, uint32_t bpc, const uint8_t* expect) {
+  uint8_t got[4 * 64];
+  const size_t group = 64 * (size_t)bpc;     // chunks per pass
+  for (size_t off = 0; off < n; off += group) {
+    const size_t m = std::min(group, n - off);
+    crc32c_chunks_be(data + off, m, bpc, got);
+    const size_t chunks = (m + bpc - 1) / bpc;
+    if (std::memcmp(got, expect + 4 * (off / bpc), 4 * chunks) != 0) {
+      for (size_t k = 0; k < chunks; ++k)
+        if (std::memcmp(got + 4 * k, expect + 4 * (off / bpc + k), 4) != 0) return (int64_t)(off / bpc + k);
+    }
+  }
+  return -1;
 }
 
 // ------------------------------------------------------------------------------------------

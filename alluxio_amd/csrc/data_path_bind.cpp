@@ -7,6 +7,7 @@
 
 #include "block_source.h"
 #include "data_server.h"
+#include "hdfs_packets.h"
 #include "frame_rpc.h"
 
 namespace py = pybind11;
@@ -193,7 +194,8 @@ void bind_data_path(py::module_& m) {
            py::arg("page_size"), py::arg("length"));
   py::class_<StoreSource, BlockSource, std::shared_ptr<StoreSource>>(m, "StoreSource")
       .def(py::init<BlockStore*, int64_t, uint64_t, bool>(), py::arg("store"), py::arg("block_id"), py::arg("length"),
-           py::arg("device_tier"), py::keep_alive<1, 2>());
+           py::arg("device_tier"), py::keep_alive<1, 2>())
+      .def_property_readonly("bytes", &StoreSource::bytes);
   py::class_<GrpcBlockSource, BlockSource, std::shared_ptr<GrpcBlockSource>>(m, "GrpcBlockSource")
       .def(py::init([](const std::string& host, int port, int64_t block_id, uint64_t length, uint64_t chunk,
                        py::bytes ufs_options, bool promote, const std::string& channel_id, const std::string& user,
@@ -309,5 +311,33 @@ void bind_data_path(py::module_& m) {
   m.def("set_require_channel_auth", [](FrameRpcServer& srv, bool on) { srv.set_require_channel_auth(on); });
   m.def("set_stream_window", [](FrameRpcServer& srv, uint32_t bytes) { srv.set_stream_window(bytes); });
   m.def("set_prefetch_threads", &set_prefetch_threads, py::arg("threads"));
+
+  // ---- HDFS DataTransferProtocol packets (gateway DataNode reads, Hadoop client reads) -------
+  m.def("dn_send_block", [](int fd, std::shared_ptr<BlockSource> src, uint64_t offset, uint64_t length,
+                            uint32_t bpc, uint32_t packet_bytes, int timeout_ms, bool flip, bool truncate) {
+          DnSendOptions o;
+          o.bytes_per_checksum = bpc;
+          o.packet_bytes = packet_bytes;
+          o.timeout_ms = timeout_ms;
+          o.fault_flip_bits = flip;
+          o.fault_truncate = truncate;
+          if (src->needs_gil()) return dn_send_block(fd, *src, offset, length, o);
+          py::gil_scoped_release rel;
+          return dn_send_block(fd, *src, offset, length, o);
+        }, py::arg("fd"), py::arg("source"), py::arg("offset"), py::arg("length"), py::arg("bytes_per_checksum") = 512,
+        py::arg("packet_bytes") = 1u << 20, py::arg("timeout_ms") = 60000, py::arg("flip_bits") = false,
+        py::arg("truncate") = false);
+  py::class_<DnPacketReader>(m, "DnPacketReader")
+      .def(py::init<int, uint32_t, bool, uint64_t, int>(), py::arg("fd"), py::arg("bytes_per_checksum"),
+           py::arg("verify"), py::arg("skip"), py::arg("timeout_ms") = 60000)
+      .def("readinto", [](DnPacketReader& r, py::buffer b, uint64_t n) {
+             py::buffer_info bi = b.request(true);
+             n = std::min<uint64_t>(n, (uint64_t)(bi.size * bi.itemsize));
+             py::gil_scoped_release rel;
+             return r.readinto(static_cast<uint8_t*>(bi.ptr), n);
+           }, py::arg("buffer"), py::arg("n"))
+      .def("drain", &DnPacketReader::drain, G())
+      .def_property_readonly("done", &DnPacketReader::done)
+      .def_property_readonly("packets", &DnPacketReader::packets);
   m.def("listen_unix", [](FrameRpcServer& srv, const std::string& path) { srv.listen_unix(path); });
 }

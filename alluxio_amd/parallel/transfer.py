@@ -281,7 +281,8 @@ class TransferPlane:
     def replicate_all(self, blocks: list[tuple[int, int, int]]) -> int:
         """Collective: ``blocks`` = [(block_id, length, owner_rank)], identical on every rank.
         Afterwards every rank's worker holds every block.  One ``all_gather_into_tensor`` per
-        round moves one block from each owner to everyone (rounds = max blocks per owner); the
+        round moves one batch (blocks packed up to ``batch_bytes``) from each owner to everyone
+        (rounds = max batches per owner); the
         scatter of round k into pages is queued behind its all-gather on the stream and round k+1
         is issued before round k is waited for (two staging slots), so the GPU never idles
         between rounds.
@@ -315,7 +316,11 @@ class TransferPlane:
 
     def _gather_rounds(self, by_owner, start: int) -> int:
         members = self.members
-        rounds = max((len(by_owner.get(r, ())) for r in members), default=0)
+        # round k all-gathers every owner's k-th batch (consecutive blocks packed up to
+        # batch_bytes): one collective per batch, not per block.  Batches depend only on
+        # by_owner and batch_bytes, so the resume index stays valid across a rebuild.
+        batches = [self._batches(by_owner.get(r, [])) for r in members]
+        rounds = max((len(b) for b in batches), default=0)
         pending: list = []
         moved = 0
         k = start
@@ -323,23 +328,21 @@ class TransferPlane:
             while k < rounds:
                 if self._rebuild_requested():
                     raise PlaneFailure("another member is rebuilding the transfer group")
-                entries = [by_owner[r][k] if k < len(by_owner.get(r, ())) else (None, 0) for r in members]
-                shard = max(n for _, n in entries)
+                entries = [batches[r][k] if k < len(batches[r]) else [] for r in range(len(members))]
+                shard = max(sum(n for _, n in e) for e in entries)
                 if shard == 0:
                     k += 1
                     continue
                 send, out = self._staging(shard, slot=k % 2)
-                mine = entries[self.rank]
-                if mine[0] is not None:   # bytes past a short block are never read: no zero fill
-                    self._copy_block_out(mine[0], mine[1], send)
+                if entries[self.rank]:     # bytes past a short batch are never read: no zero fill
+                    self._copy_batch_out(entries[self.rank], send)
                 work = self._pg._allgather_base(out, send)
                 if self.backend == "nccl":
                     work.wait()            # the scatter queues behind the all-gather (no host wait)
                 else:
                     self._await([work])    # host scatter needs the bytes; a gloo work is waited once
                     work = None
-                slots = [(r, [(bid, n)] if bid is not None else []) for r, (bid, n) in enumerate(entries)]
-                opened = self._scatter_batches(out, shard, slots, skip_slot=self.rank)
+                opened = self._scatter_batches(out, shard, list(enumerate(entries)), skip_slot=self.rank)
                 pending.append((k, [work], self._record(), opened))
                 self.rounds += 1
                 k += 1
@@ -603,9 +606,6 @@ class TransferPlane:
             pin = dev.type == "cpu" and bool(self.w.store.has_device_tier)
             buf = bufs[slot] = torch.empty(cap, dtype=torch.uint8, device=dev, pin_memory=pin)
         return buf[:shard], buf[shard:shard * (nslots + 1)]
-
-    def _copy_block_out(self, block_id: int, n: int, dst) -> None:
-        self._copy_batch_out([(block_id, n)], dst)
 
     def _copy_batch_out(self, batch, dst) -> None:
         """Pack the blocks of ``batch`` back to back into ``dst`` with one batched read (queued on

@@ -154,6 +154,7 @@ class DataTransferServer(_Service):
         self.open_read, self.open_write = open_read, open_write
         self.fault_flip_bits = False    # fault injection: corrupt sent data AFTER checksumming it
         self.fault_truncate = False     # fault injection: end the block after its first packet
+        self.packet_bytes = 1 << 20     # data bytes per packet of the native sender
         super().__init__(host, port, _DataHandler)
         self.host = host
         self.uuid = f"alluxio-dn-{self.port}"
@@ -199,6 +200,19 @@ class _DataHandler(socketserver.BaseRequestHandler):
             resp.readOpChecksumInfo.checksum.bytesPerChecksum = bpc
             resp.readOpChecksumInfo.chunkOffset = start
             s.sendall(H.delimited(resp))
+            native = getattr(src, "native_source", None)
+            ns = native() if native is not None else None
+            if ns is not None:
+                # packets built and sent in C++ (csrc/hdfs_packets.cpp): source chunk -> CRC32C
+                # per 512 B -> one writev per 1 MiB packet, GIL released
+                from ..ops.native import lib
+                bsrc, soff = ns
+                try:
+                    lib().dn_send_block(s.fileno(), bsrc, soff, op.offset + op.len - start, bpc,
+                                        srv.packet_bytes, 60_000, srv.fault_flip_bits, srv.fault_truncate)
+                except Exception:  # noqa: BLE001 - a reader that stops early closes its socket
+                    LOG.debug("hdfs gateway: read of block %d ended by the client", bid, exc_info=True)
+                return
             seq, off, end = 0, start, op.offset + op.len
             while off < end:
                 data = src.read(min(H.PACKET_DATA, end - off))
@@ -345,8 +359,19 @@ class _BlockSink:
 
 class _RangeReader:
     def __init__(self, stream, offset: int, length: int):
-        self.stream, self.left = stream, length
+        self.stream, self.left, self.start = stream, length, offset
         stream.seek(offset)
+
+    def native_source(self):
+        """(native BlockSource, offset in it) for the DataNode's C++ packet sender when the range
+        lies in one Alluxio block (a gateway block is one), else None."""
+        f = self.stream
+        if getattr(f, "_nat", None) is None or self.left <= 0:
+            return None
+        idx = self.start // f.block_size
+        if (self.start + self.left - 1) // f.block_size != idx:
+            return None
+        return f._open_native(idx, False), self.start - idx * f.block_size
 
     def read(self, n: int) -> bytes:
         if self.left <= 0:

@@ -599,10 +599,33 @@ class BlockReader:
         self.skip = offset - info.chunkOffset     # the DataNode starts at a chunk boundary
         self.pending = memoryview(b"")
         self.done = False
+        # packets parsed and CRC-verified in C++ straight into the caller's buffer (csrc/hdfs_packets.cpp)
+        self.native = None
+        try:
+            from ..ops.native import lib
+            self.native = lib().DnPacketReader(self.sock.fileno(), self.bpc, self.verify, self.skip,
+                                               int(timeout * 1000))
+        except Exception:  # noqa: BLE001 - no native extension: the Python packet loop
+            self.native = None
 
     def readinto(self, buf) -> int:
         """Copy up to len(buf) bytes straight into ``buf`` (one copy out of the packet buffer)."""
         mv = memoryview(buf).cast("B")
+        if self.native is not None:
+            want = min(len(mv), self.remaining)
+            if want <= 0:
+                return 0
+            try:
+                got = self.native.readinto(mv, want)
+            except Exception as e:  # noqa: BLE001 - StoreError (checksum, connection) -> IOError
+                raise IOError(str(e.args[1] if len(getattr(e, "args", ())) > 1 else e)) from None
+            if got < want and self.native.done:
+                raise IOError(f"datanode ended block {self.located.b.blockId} with {self.remaining - got} "
+                              f"requested bytes unsent")
+            self.remaining -= got
+            if self.remaining == 0:
+                self.close(ok=True)
+            return got
         got = 0
         while got < len(mv) and self.remaining > 0:
             if not len(self.pending):
@@ -639,11 +662,14 @@ class BlockReader:
         try:
             if ok:
                 # drain to the trailing empty packet, then report CHECKSUM_OK as DFSClient does
-                while not self.done:
-                    hdr, _ = read_packet(s, self.bpc, False)
-                    self.done = hdr.lastPacketInBlock or hdr.dataLen == 0
+                if self.native is not None:
+                    self.native.drain()
+                else:
+                    while not self.done:
+                        hdr, _ = read_packet(s, self.bpc, False)
+                        self.done = hdr.lastPacketInBlock or hdr.dataLen == 0
                 s.sendall(delimited(hdfs.ClientReadStatusProto(status=ST_CHECKSUM_OK)))
-        except OSError:
+        except Exception:  # noqa: BLE001 - OSError / native StoreError: the connection is dropped
             pass
         finally:
             s.close()

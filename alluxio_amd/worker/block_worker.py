@@ -582,7 +582,9 @@ class BlockWorker:
             self.crc[block_id] = crc
             self.metrics.counter("Crc32cBytes").inc(info.length)
         elif self.crc_enabled or (self.crc_device and info.medium == "HBM"):
+            t0 = time.perf_counter()
             self.crc[block_id] = (self.native.block_pages(block_id)[2], self.native.checksum(block_id, 0))
+            self.metrics.timer("Crc32cCommit").update(time.perf_counter() - t0)
             self.metrics.counter("Crc32cBytes").inc(info.length)
         bm = self._bm()
         if bm is not None and self.worker_id != ids.INVALID_WORKER_ID:

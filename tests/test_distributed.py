@@ -142,8 +142,10 @@ ok_all = all(w.worker.has_block(b) for b, _, _ in blocks)
 # bytes of the other rank's first block now readable from this worker's own store
 other = (rank + 1) %% world
 odata = np.random.default_rng(10 + other).integers(0, 256, sizes[other %% 2], dtype=np.uint8)
-ob, olen, _ = allb[other][0]
-ok_bytes = w.worker.read_bytes(ob, 0, olen) == odata[:olen].tobytes()
+ok_bytes, at = True, 0
+for ob, olen, _ in allb[other]:      # every block of the peer's packed batch landed intact
+    ok_bytes = ok_bytes and w.worker.read_bytes(ob, 0, olen) == odata[at:at + olen].tobytes()
+    at += olen
 dist.barrier()
 w.sync.heartbeat()
 dist.barrier()

@@ -43,6 +43,19 @@ for s in $STEPS; do
       ;;
     lz4t) run lz4_tests 300 python -u -m pytest tests/test_kernels_gpu.py -k lz4 -x -v --timeout 120 --timeout-method thread ;;
     lz4) run lz4_bench 600 python tools/lz4_bench.py --chunks 1024,4096,16384,32768 --variants="${LZ4_VARIANTS:-2,17,19,20,21,22}" --out "$OUT/lz4_bench.jsonl" ;;
+    config5)
+      run ingest_config5 900 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 1,3 --threads 4 --out "$OUT/ufs_ingest_config5_s3native.jsonl"
+      run ingest_config5_t8 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/ufs_ingest_config5_s3native.jsonl"
+      run rocprof_config5 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_config5" -o c5 --output-format csv -- python3 tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 4
+      ;;
+    mastergrpc2)
+      run master_bench_grpc_p8 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 8 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p8.json"
+      run master_bench_grpc_p16 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 16 --threads 4 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p16.json"
+      ;;
+    c5t8) run ingest_config5_t8 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/ufs_ingest_config5_t8.jsonl" ;;
+    hdfsgw)
+      run hdfs_gateway_bench 600 python tools/hdfs_gateway_bench.py --file-size 2g --threads 1,4,8 --out "$OUT/hdfs_gateway.jsonl"
+      ;;
     s3ingest)
       run ingest_s3native 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 2g --dram 6g --factor 2 --depths 1,3 --out "$OUT/ufs_ingest_s3native.jsonl"
       run ingest_s3requests 600 python tools/ufs_ingest_bench.py --ufs s3native --native-reader false --hbm 2g --dram 6g --factor 2 --depths 3 --out "$OUT/ufs_ingest_s3native.jsonl"
@@ -114,6 +127,13 @@ for s in $STEPS; do
     prefetchab)
       for pf in true false; do
         run wb_host_ab_$pf 900 python tools/worker_bench_host.py --threads 16,256 --transports grpc,ipc --duration 8s --warmup 2s --client-prop alluxio.user.native.reader.prefetch.enabled=$pf --out "$OUT/worker_bench_host_prefetch_ab.jsonl"
+      done
+      ;;
+    hostsweep)
+      for rb in 256KB 512KB 1MB; do
+        for pf in false true; do
+          run wb_sweep_${rb}_$pf 600 python tools/worker_bench_host.py --threads 16,256 --transports grpc,ipc --duration 6s --warmup 2s --reader-buffer $rb --client-prop alluxio.user.native.reader.prefetch.enabled=$pf --out "$OUT/worker_bench_host_sweep.jsonl"
+        done
       done
       ;;
     replicate)

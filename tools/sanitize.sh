@@ -15,7 +15,9 @@ TSAN_TESTS=(tests/test_native_store.py tests/test_native_rpc.py tests/test_page_
             tests/test_concurrency.py tests/test_cluster.py tests/test_tier_management.py
             tests/test_client_cache.py tests/test_ring_reader.py tests/test_marshal.py tests/test_master.py
             tests/test_journal.py tests/test_raft.py tests/test_ha.py tests/test_job_stress.py
-            tests/test_proxy.py tests/test_fuse.py tests/test_metastore.py)
+            tests/test_proxy.py tests/test_fuse.py tests/test_metastore.py
+            tests/test_grpc_native.py tests/test_fuse_native.py tests/test_s3_native.py tests/test_hdfs_native.py
+            tests/test_data_server.py tests/test_hdfs_gateway.py)
 if [ ${#ARGS[@]} -eq 0 ]; then
   if [ "$KIND" = tsan ]; then ARGS=("${TSAN_TESTS[@]}" -q -m "not gpu" -p no:cacheprovider -n 4)
   else ARGS=(tests -q -m "not gpu" -p no:cacheprovider -n 4); fi

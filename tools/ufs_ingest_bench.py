@@ -140,12 +140,31 @@ def run(a, depth: int) -> dict:
                         block_size=fbi.blockInfo.length, mountId=info.mountId)
                     reqs.append((fbi.blockInfo.blockId, opts))
             nbytes = sum(o.block_size for _, o in reqs)
+            import logging
+            fails = []
+
+            class _Fail(logging.Handler):
+                def emit(self, rec):
+                    if rec.exc_info and len(fails) < 3:
+                        fails.append(f"{rec.getMessage()}: {rec.exc_info[1]!r}")
+            blog = logging.getLogger("alluxio_amd.worker.block_worker")
+            blog.setLevel(logging.DEBUG)
+            blog.addHandler(_Fail())
             t0 = time.perf_counter()
             for bid, opts in reqs:
                 w.async_cache(bid, opts=opts)
             ok = w.wait_async_idle(timeout=a.timeout)
             el = time.perf_counter() - t0
+            # where the ingest threads spent their time (the bound): UFS reads, waits for the H2D
+            # DMA to free a staging buffer, and the per-page CRC32C kernel at commit
+            pipes = list(w._ingest._free) if w._ingest is not None else []
+            stage = {k: round(sum(p.stats[k] for p in pipes), 3) for k in ("read_s", "wait_s")}
+            stage["chunks"] = sum(p.stats["chunks"] for p in pipes)
+            crc_t = w.metrics.timer("Crc32cCommit")
+            stage["crc_s"] = round(crc_t._fold_sum(), 3)
+            stage["threads_x_wall_s"] = round(el * a.threads, 3)
             cached = sum(1 for bid, _ in reqs if w.has_block(bid))
+            cached_bytes = sum(o.block_size for bid, o in reqs if w.has_block(bid))
             st = w.native.evict_stats()
             tiers = {}
             for bid in w.native.block_ids(-1):
@@ -172,11 +191,12 @@ def run(a, depth: int) -> dict:
             fs.close()
             return {"ufs": a.ufs if a.ufs != "s3native" else f"s3native(reader={a.native_reader})", "depth": depth, "hbm_bytes": hbm, "dram_bytes": dram, "working_set": nbytes,
                     "blocks": len(reqs), "cached_blocks": cached, "all_done": ok,
-                    "ingest_GBps": round(nbytes / el / 1e9, 3), "ingest_s": round(el, 3),
+                    "ingest_GBps": round(cached_bytes / el / 1e9, 3), "ingest_s": round(el, 3),
+                    "failed_blocks": w.metrics.counter("AsyncCacheFailedBlocks").value(), "first_failures": fails,
                     "demoted_blocks": st["demoted_blocks"], "demoted_bytes": st["demoted_bytes"],
                     "batched_moves": st["batched_moves"], "resident_by_medium": tiers,
                     "reread_GBps": round(rb / rel / 1e9, 3) if rel > 0 else None, "reread_bytes": rb,
-                    "threads": a.threads}
+                    "threads": a.threads, "stages": stage}
     finally:
         if proxy is not None:
             proxy.stop()
