@@ -196,6 +196,10 @@ _k("WORKER_HBM_DEVICE_ALLOC_ENABLED", "alluxio.worker.hbm.device.alloc.enabled",
    "(K7: resident free-page bitmap in HBM, claim kernel + fused scatter).  Bulk creates of 150k pages "
    "run 3x faster than the host bitmap scan, ingest at parity (profiles/r3_evict_bench_arc.jsonl); "
    "single small creates stay on the host scan (below alloc.min.pages).")
+_k("WORKER_PAGE_ACCOUNTING_CHECK", "alluxio.worker.debug.page.accounting.check", "false", Scope.WORKER,
+   "Debug: after every bulk create / bulk UFS ingest, verify that the host page pool, the K7 device "
+   "magazine (its HBM bitmap against mag_pages) and the block page lists partition each arena "
+   "(BlockStore::check_pages); violations are logged and counted in PageAccountingErrors.")
 _k("WORKER_HBM_DEVICE_ALLOC_MIN_PAGES", "alluxio.worker.hbm.device.alloc.min.pages", "1024", Scope.WORKER,
    "Smallest bulk create (in pages) that uses the device allocator when it is enabled.")
 _k("WORKER_DATA_SERVER_NATIVE_ENABLED", "alluxio.worker.data.server.native.enabled", "true", Scope.WORKER,

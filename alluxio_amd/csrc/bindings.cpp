@@ -454,12 +454,14 @@ PYBIND11_MODULE(_C, m) {
              d["mag_drains"] = st.mag_drains;
              d["mag_drain_pages"] = st.mag_drain_pages;
              d["mag_short_items"] = st.mag_short_items;
+             d["evict_waits"] = st.evict_waits;
              d["ingest_ns"] = std::vector<uint64_t>(st.ingest_ns, st.ingest_ns + 6);
              return d;
            })
       .def("mag_refill", &BlockStore::mag_refill_pages, G())
       .def("mag_pages", &BlockStore::mag_pages, G())
       .def("mag_device_count", &BlockStore::mag_device_count, G())
+      .def("check_pages", &BlockStore::check_pages, G())
       .def("mag_claim_many", &BlockStore::mag_claim_many, G())
       .def("mag_give", &BlockStore::mag_give, G())
       .def("mag_drain", &BlockStore::mag_drain_dir, G())

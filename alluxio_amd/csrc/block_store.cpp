@@ -1438,6 +1438,7 @@ std::vector<uint32_t> BlockStore::select_victims_cpu(const std::vector<uint32_t>
 
 void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
                                    int tier, int dir, const std::string& medium) {
+  const auto wait_until = std::chrono::steady_clock::now() + std::chrono::seconds(2);
   for (int attempt = 0; attempt < 4; ++attempt) {
     // target dir: the one that can reach `bytes` with the most (available + evictable)
     int target = -1;
@@ -1494,6 +1495,23 @@ void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t ses
       if (b && b->dir == target && evictable(*b)) remove_locked(*b, true);
     }
     if (dirs_[target]->available() >= bytes) return;
+    // Blocks of the target dir that other threads are demoting right now are neither victims
+    // nor free space yet: under concurrent ingest (many creates evicting at once) wait for those
+    // moves to land (bounded) instead of failing the create.
+    bool moving = false;
+    for (int64_t id : evicting_ids_) {
+      const BlockMeta* b = find(id);
+      if (b && b->dir == target) {
+        moving = true;
+        break;
+      }
+    }
+    if (moving && std::chrono::steady_clock::now() < wait_until) {
+      ++stats_.evict_waits;
+      lock_cv_.wait_for(lk, std::chrono::milliseconds(20));
+      --attempt;                                     // a wait is not an attempt
+      continue;
+    }
     if (victims.empty()) break;
   }
   throw StoreError(kErrOutOfSpace, "failed to free " + std::to_string(bytes) + " bytes (tier " +
@@ -1840,6 +1858,53 @@ int64_t BlockStore::mag_device_count(int dir) {
   int64_t n = 0;
   for (uint64_t x : w) n += __builtin_popcountll(x);
   return n;
+}
+
+std::string BlockStore::check_pages(int dir) {
+  std::unique_lock<std::mutex> lk(mu_);
+  StorageDir& d = *dirs_.at(dir);
+  if (d.free_bits.empty()) return "";                       // file dirs: no page accounting
+  std::string err;
+  auto fail = [&](const std::string& m) {
+    if (err.size() < 2000) err += m + "; ";
+  };
+  std::vector<uint64_t> mag(d.free_bits.size(), 0);
+  if (d.mag_bits) {
+    HIP_OK(hipStreamSynchronize(internal_stream_));
+    HIP_OK(hipMemcpy(mag.data(), d.mag_bits, mag.size() * 8, hipMemcpyDeviceToHost));
+  }
+  int64_t host_free = 0, mag_n = 0;
+  for (size_t w = 0; w < mag.size(); ++w) {
+    host_free += __builtin_popcountll(d.free_bits[w]);
+    mag_n += __builtin_popcountll(mag[w]);
+    if (d.free_bits[w] & mag[w]) fail("word " + std::to_string(w) + " has pages both in the host pool and the magazine");
+  }
+  if (mag_n != d.mag_pages)
+    fail("magazine bitmap holds " + std::to_string(mag_n) + " pages, mag_pages says " + std::to_string(d.mag_pages));
+  if (host_free + d.mag_pages != d.free_pages)
+    fail("host pool " + std::to_string(host_free) + " + magazine " + std::to_string(d.mag_pages) + " != free_pages " +
+         std::to_string(d.free_pages));
+  std::vector<uint8_t> owner(d.num_pages, 0);
+  int64_t owned = 0;
+  for (const auto& kv : blocks_) {
+    const BlockMeta& b = kv.second;
+    if (b.dir != dir) continue;
+    for (int64_t p : b.pages) {
+      if (p < 0 || p >= d.num_pages) {
+        fail("block " + std::to_string(b.id) + " owns out-of-range page " + std::to_string(p));
+        continue;
+      }
+      const size_t w = (size_t)p / 64;
+      const uint64_t bit = 1ull << (p % 64);
+      if (owner[p]++) fail("page " + std::to_string(p) + " owned twice (block " + std::to_string(b.id) + ")");
+      if ((d.free_bits[w] | mag[w]) & bit) fail("page " + std::to_string(p) + " of block " + std::to_string(b.id) + " is also free");
+      ++owned;
+    }
+  }
+  if (owned + d.free_pages != d.num_pages)
+    fail("owned " + std::to_string(owned) + " + free " + std::to_string(d.free_pages) + " != " +
+         std::to_string(d.num_pages) + " pages");
+  return err;
 }
 
 std::vector<std::vector<int64_t>> BlockStore::mag_claim_many(int dir, const std::vector<uint32_t>& wants) {

@@ -239,6 +239,7 @@ class BlockStore {
     uint64_t device_allocs = 0, device_alloc_pages = 0, annotation_flushes = 0, annotation_updates = 0;
     uint64_t demoted_blocks = 0, demoted_bytes = 0, batched_moves = 0, batched_move_blocks = 0;
     uint64_t mag_refills = 0, mag_refill_pages = 0, mag_drains = 0, mag_drain_pages = 0, mag_short_items = 0;
+    uint64_t evict_waits = 0;             // free_space waits for other threads' demotions
     // ingest_files wall time by phase (ns): 0 block metadata/claims setup, 1 preads, 2 copy/claim
     // launches, 3 waiting on the stream, 4 page attach + commits, 5 up-front magazine refill
     uint64_t ingest_ns[6] = {0, 0, 0, 0, 0, 0};
@@ -257,6 +258,9 @@ class BlockStore {
   // gives them back with mag_give), hand pages back, drain the magazine into the host pool.
   int64_t mag_refill_pages(int dir, int64_t pages);
   int64_t mag_device_count(int dir);
+  // Debug: page accounting of one dir (host pool + K7 magazine + block pages partition the
+  // arena; the device magazine bitmap holds exactly mag_pages).  Empty when consistent.
+  std::string check_pages(int dir);
   std::vector<std::vector<int64_t>> mag_claim_many(int dir, const std::vector<uint32_t>& wants);
   void mag_give(int dir, const std::vector<int64_t>& pages);
   int64_t mag_drain_dir(int dir);

@@ -91,6 +91,7 @@ class BlockWorker:
         # HBM blocks get their per-page CRC32C at commit by default (one kernel pass at ~3.6 TB/s):
         # peers verify pulled blocks against it, short-circuit readers may too
         self.crc_device = conf.get_bool("alluxio.worker.data.crc.device.enabled", "true")
+        self.page_check = conf.get_bool("alluxio.worker.debug.page.accounting.check", "false")
         self.crc: dict[int, tuple[int, list[int]]] = {}   # block id -> (piece bytes, CRC32Cs)
         self._install_gauges()
 
@@ -528,6 +529,8 @@ class BlockWorker:
             with self._bulk_lock, native_errors():
                 status = self.native.ingest_files(session_id, native_ids, paths, offs, lens, staging.data_ptr(),
                                                   sbytes, self._bulk_threads, 0)
+                if self.page_check:
+                    self.check_page_accounting("bulk ingest")
             t1 = time.perf_counter()
             self.metrics.timer("UfsIngestBulk").update(t1 - t0)
             ok = [b for b, st in zip(native_ids, status) if st == 0]
@@ -557,6 +560,19 @@ class BlockWorker:
             except Exception:  # noqa: BLE001
                 LOG.debug("cache of block %d failed", bid, exc_info=True)
         return done
+
+    def check_page_accounting(self, where: str = "") -> list[str]:
+        """Debug check of every arena dir's page accounting (host pool + K7 magazine + block
+        pages); returns the violations, each also logged and counted."""
+        errs = []
+        for i in range(len(self.store.dirs)):
+            e = self.native.check_pages(i)
+            if e:
+                errs.append(f"dir {i}: {e}")
+                LOG.error("page accounting violated after %s: dir %d: %s", where or "?", i, e)
+        if errs:
+            self.metrics.counter("PageAccountingErrors").inc(len(errs))
+        return errs
 
     def _bulk_staging(self, min_item: int):
         import torch

@@ -301,3 +301,100 @@ def test_magazine_concurrent_claims_exact(gpu, npages, nitems, want):
         assert all(len(g) == want for g in got)
     assert s.mag_device_count(0) == moved - len(flat) == s.mag_pages(0)
     assert s.mag_drain(0) == moved - len(flat) and s.mag_device_count(0) == 0
+
+
+def test_magazine_accounting_mixed_workload(gpu, tmp_path):
+    """with the K7 magazine on by default, page accounting must survive a mixed
+    workload -- bulk ingests and bulk creates (device claims), single creates (host scan, drains
+    the magazine on demand), aborts, removes, evictions that demote into a second HBM tier --
+    with check_pages (host pool + magazine bitmap + block page lists partition each arena, the
+    device bitmap holds exactly mag_pages) clean after every step, and the ingested bytes intact."""
+    import torch
+    C = lib()
+    page = 64 * KB
+    arenas, specs = [], []
+    for tier, n in ((0, 1024), (1, 2048)):
+        a = torch.empty(n * page, dtype=torch.uint8, device="cuda")
+        d = C.DirSpec()
+        d.tier, d.tier_alias, d.medium, d.kind = tier, ("MEM", "SSD")[tier], "HBM", C.DirKind.DEVICE
+        d.base, d.capacity, d.page_size, d.device = a.data_ptr(), a.numel(), page, 0
+        arenas.append(a)
+        specs.append(d)
+    s = C.BlockStore(specs, annotator=0, alloc_policy=0, device=0)
+    s._arenas = arenas
+    s.set_use_device_alloc(True, 8)
+    s.set_demote_on_evict(True)
+    rng = np.random.default_rng(23)
+    staging = torch.empty(4 << 20, dtype=torch.uint8, pin_memory=True)
+    out = torch.empty(3 * page, dtype=torch.uint8, device="cuda")
+    data: dict[int, np.ndarray] = {}
+    committed: list[int] = []
+    nxt = [100]
+
+    def new_ids(k):
+        ids = list(range(nxt[0], nxt[0] + k))
+        nxt[0] += k
+        return ids
+
+    def check(step):
+        for d in range(2):
+            assert s.check_pages(d) == "", (step, d, s.check_pages(d))
+
+    for step in range(60):
+        op = step % 6
+        if op == 0:                                    # bulk UFS ingest (device claim + scatter)
+            ids = new_ids(int(rng.integers(20, 80)))
+            paths, lens = [], []
+            for b in ids:
+                n = int(rng.integers(1, 3 * page))
+                d = rng.integers(0, 256, n, dtype=np.uint8)
+                p = tmp_path / f"b{b}"
+                p.write_bytes(d.tobytes())
+                paths.append(str(p))
+                lens.append(n)
+                data[b] = d
+            st = s.ingest_files(5, ids, paths, [0] * len(ids), lens, staging.data_ptr(), staging.numel(), 4, 0)
+            for b, code in zip(ids, st):
+                if code == 0:
+                    committed.append(b)
+                else:
+                    data.pop(b)
+        elif op == 1:                                  # bulk create, then commit or abort
+            ids = new_ids(int(rng.integers(10, 40)))
+            try:
+                s.create_blocks(7, ids, 0, "", [page * int(rng.integers(1, 4))] * len(ids), True)
+            except Exception:  # noqa: BLE001 - the tier may be full of locked/temp blocks
+                pass
+            if step % 12 == 1:
+                s.cleanup_session(7)
+            else:
+                for b in ids:
+                    if s.has_temp_block(b):
+                        s.commit_block(7, b)
+                        committed.append(b)
+        elif op == 2:                                  # single creates on the host scan
+            for b in new_ids(int(rng.integers(5, 30))):
+                try:
+                    s.create_block(8, b, 0, "", page, True, False)
+                    s.commit_block(8, b)
+                    committed.append(b)
+                except Exception:  # noqa: BLE001
+                    break
+        elif op == 3 and committed:                    # removes
+            for b in rng.choice(committed, min(len(committed), 15), replace=False).tolist():
+                if s.has_block(b):
+                    s.remove_block(10, b)
+                committed.remove(b)
+                data.pop(b, None)
+        elif op == 4:                                  # eviction (demotes into tier 1)
+            s.free_space(9, int(rng.integers(50, 300)) * page, 0, -1)
+        elif op == 5 and committed:                    # accesses reorder the victims
+            s.access_blocks(rng.choice(committed, min(len(committed), 40), replace=False).tolist())
+        check(step)
+    live = [b for b in data if s.has_block(b)]
+    assert live
+    for b in live[::5]:
+        d = data[b]
+        s.read_batch([(b, 0, d.nbytes, out.data_ptr(), 1)], 0, True)
+        assert np.array_equal(out[:d.nbytes].cpu().numpy(), d), b
+    assert s.evict_stats()["device_alloc_pages"] > 0

@@ -303,3 +303,32 @@ def test_roctx_ranges_are_harmless_without_a_profiler():
     def f(x):
         return x + 1
     assert f(1) == 2
+
+
+def test_concurrent_creates_with_demotion_never_run_out(tmp_path):
+    """Many threads filling a small top tier at once, each create evicting by demotion into the
+    lower tier: a create whose victims are all mid-demotion by other threads waits for those moves
+    (bounded) instead of failing -- every block lands (config 5's 8-thread ingest lost 17 of 128
+    blocks to WorkerOutOfSpace before)."""
+    import threading
+    s = _store(tmp_path, mem_mb=8, ssd_mb=256, page=256 << 10)
+    s.set_demote_on_evict(True)
+    errs = []
+    data = np.random.default_rng(3).integers(0, 256, MB, dtype=np.uint8)
+
+    def run(t):
+        for i in range(24):
+            try:
+                _put(s, t * 1000 + i + 1, data, session=100 + t)
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+    ts = [threading.Thread(target=run, args=(t,)) for t in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[:3]
+    assert all(s.has_block(t * 1000 + i + 1) for t in range(8) for i in range(24))
+    st = s.evict_stats()
+    assert st["demoted_blocks"] >= 8 * 24 - 8

@@ -26,8 +26,11 @@ sys.path.insert(0, ROOT)
 
 
 class FileDataset:
-    def __init__(self, paths):
+    def __init__(self, paths, buffering=-1):
         self.paths = paths
+        # -1: Python's default buffered open(), which probes isatty() -- one TCGETS ioctl per file,
+        # a FUSE round trip on a mount but a local syscall on disk; 0: raw FileIO, no probe
+        self.buffering = buffering
 
     def __len__(self):
         return len(self.paths)
@@ -35,7 +38,7 @@ class FileDataset:
     def __getitem__(self, i):
         import numpy as np
         import torch
-        with open(self.paths[i], "rb") as f:
+        with open(self.paths[i], "rb", buffering=self.buffering) as f:
             b = f.read()
         return torch.from_numpy(np.frombuffer(b, dtype=np.uint8)[:16].copy()), len(b)
 
@@ -70,13 +73,13 @@ def _scan(root: str, dirs: int) -> dict:
     return {"entries": n, "s": round(time.perf_counter() - t0, 3)}
 
 
-def _epochs(paths, epochs, workers, batch, seed=0):
+def _epochs(paths, epochs, workers, batch, seed=0, buffering=-1):
     import torch
     from torch.utils.data import DataLoader, RandomSampler
     out = []
     for e in range(epochs):
         g = torch.Generator().manual_seed(seed + e)
-        dl = DataLoader(FileDataset(paths), batch_size=batch, sampler=RandomSampler(paths, generator=g),
+        dl = DataLoader(FileDataset(paths, buffering), batch_size=batch, sampler=RandomSampler(paths, generator=g),
                         num_workers=workers, persistent_workers=False)
         t0 = time.perf_counter()
         c0 = _cpu()
@@ -120,6 +123,8 @@ def main(argv=None) -> int:
                     help="worker cache tier: dram (memfd arena) or a directory (e.g. /dev/shm/x: block files, "
                          "which the native server hands to the kernel as FUSE passthrough backing files)")
     ap.add_argument("--keep-cache", default="auto", help="auto | on | off (kernel page cache across opens)")
+    ap.add_argument("--open-buffering", type=int, default=-1, choices=[-1, 0],
+                    help="-1: default buffered open() (isatty ioctl per file); 0: unbuffered")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import numpy as np
@@ -139,7 +144,7 @@ def main(argv=None) -> int:
             "alluxio.user.block.size.bytes.default": "1MB", "alluxio.worker.hbm.page.size": "128KB"}
     res = {"setup": f"{a.files} x {a.file_size} B files in {a.dirs} dirs, DataLoader workers={a.workers} "
                     f"batch={a.batch}, FUSE threads={a.fuse_threads}, tier={a.tier}, {os.cpu_count()} CPUs, "
-                    f"keep_cache={a.keep_cache}, read_only={a.read_only}"}
+                    f"keep_cache={a.keep_cache}, read_only={a.read_only}, open_buffering={a.open_buffering}"}
     try:
         with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=os.path.join(work, "c")) as c:
             fs = c.client(metadata_cache=True)
@@ -160,7 +165,7 @@ def main(argv=None) -> int:
                 paths = [os.path.join(mnt, "ds", r) for r in rel]
                 if not a.no_scan:
                     res["fuse_scan"] = _scan(os.path.join(mnt, "ds"), a.dirs)
-                res["fuse"] = _epochs(paths, a.epochs, a.workers, a.batch)
+                res["fuse"] = _epochs(paths, a.epochs, a.workers, a.batch, buffering=a.open_buffering)
                 res["fuse_ops"] = srv.op_stats()
             finally:
                 srv.unmount()
@@ -175,7 +180,7 @@ def main(argv=None) -> int:
                 res["ufs_page_cache_dropped"] = False
             if not a.no_scan:
                 res["ufs_scan"] = _scan(ufs_dir, a.dirs)
-            res["ufs_direct"] = _epochs([os.path.join(ufs_dir, r) for r in rel], a.epochs, a.workers, a.batch)
+            res["ufs_direct"] = _epochs([os.path.join(ufs_dir, r) for r in rel], a.epochs, a.workers, a.batch, buffering=a.open_buffering)
             fs.close()
     finally:
         shutil.rmtree(work, ignore_errors=True)

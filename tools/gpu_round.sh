@@ -52,6 +52,7 @@ for s in $STEPS; do
       run master_bench_grpc_p8 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 8 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p8.json"
       run master_bench_grpc_p16 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 16 --threads 4 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p16.json"
       ;;
+    k7mixed) run pytest_k7mixed 300 python -u -m pytest tests/test_evict_alloc_gpu.py -k "magazine" -x -v --timeout 120 --timeout-method thread ;;
     c5t8) run ingest_config5_t8 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/ufs_ingest_config5_t8.jsonl" ;;
     hdfsgw)
       run hdfs_gateway_bench 600 python tools/hdfs_gateway_bench.py --file-size 2g --threads 1,4,8 --out "$OUT/hdfs_gateway.jsonl"
