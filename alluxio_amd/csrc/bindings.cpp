@@ -455,6 +455,7 @@ PYBIND11_MODULE(_C, m) {
              d["mag_drain_pages"] = st.mag_drain_pages;
              d["mag_short_items"] = st.mag_short_items;
              d["evict_waits"] = st.evict_waits;
+             d["evict_retries"] = st.evict_retries;
              d["ingest_ns"] = std::vector<uint64_t>(st.ingest_ns, st.ingest_ns + 6);
              return d;
            })

@@ -1470,6 +1470,7 @@ void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t ses
     // the store may have changed while it was unlocked: a victim must still be the same block
     // (created before the selection), in the target dir, and evictable now
     std::vector<int64_t> vids;
+    size_t lost = 0;
     for (uint32_t s : victims) {
       BlockMeta* b = find(slot_block_[s]);
       if (b && b->seq <= seq && b->dir == target && evictable(*b)) {
@@ -1477,6 +1478,7 @@ void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t ses
         ++stats_.victims;
       } else {
         ++stats_.revalidated_away;
+        ++lost;
       }
     }
     const int lower = demote_on_evict_ ? lower_tier(dirs_[target]->spec.tier) : -1;
@@ -1510,6 +1512,14 @@ void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t ses
       ++stats_.evict_waits;
       lock_cv_.wait_for(lk, std::chrono::milliseconds(20));
       --attempt;                                     // a wait is not an attempt
+      continue;
+    }
+    // Concurrent evictors select off-lock and pick the same coldest blocks: victims another
+    // thread demoted first are revalidated away.  That is contention, not a full tier -- select
+    // again (bounded by the same deadline).
+    if (lost > 0 && std::chrono::steady_clock::now() < wait_until) {
+      ++stats_.evict_retries;
+      --attempt;
       continue;
     }
     if (victims.empty()) break;
@@ -1745,7 +1755,10 @@ std::vector<int> BlockStore::create_blocks(int64_t session, const std::vector<in
   StorageDir& sd = *dirs_[d];
   std::vector<int64_t> pool;
   size_t pool_pos = 0;
-  if (sd.spec.kind == DirKind::kDevice && use_device_alloc_) {
+  // K7 pays off per block (the host path walks each block's page list), not per page: the host
+  // word scan claims the pages of one huge block faster than a kernel round trip (0.49 vs 1.2 ms at
+  // 75k pages, profiles/r3_evict_bench_arc.jsonl), so few-block creates stay on the host
+  if (sd.spec.kind == DirKind::kDevice && use_device_alloc_ && ids.size() >= kDeviceAllocMinBlocks) {
     uint64_t want = 0;
     for (uint64_t sz : sizes) want += ceil_div(std::max<uint64_t>(sz, 1), sd.spec.page_size);
     if (want >= device_alloc_min_pages_ && (int64_t)want <= sd.free_pages - sd.reserved_pages)

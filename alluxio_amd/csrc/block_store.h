@@ -138,6 +138,9 @@ struct Event {
   std::string medium;
 };
 
+// Bulk creates of at least this many blocks claim their pages with the K7 device magazine.
+constexpr size_t kDeviceAllocMinBlocks = 64;
+
 class BlockStore {
  public:
   BlockStore(const std::vector<DirSpec>& dirs, int annotator, int alloc_policy, float lrfu_step,
@@ -240,6 +243,7 @@ class BlockStore {
     uint64_t demoted_blocks = 0, demoted_bytes = 0, batched_moves = 0, batched_move_blocks = 0;
     uint64_t mag_refills = 0, mag_refill_pages = 0, mag_drains = 0, mag_drain_pages = 0, mag_short_items = 0;
     uint64_t evict_waits = 0;             // free_space waits for other threads' demotions
+    uint64_t evict_retries = 0;           // selections redone after losing victims to other threads
     // ingest_files wall time by phase (ns): 0 block metadata/claims setup, 1 preads, 2 copy/claim
     // launches, 3 waiting on the stream, 4 page attach + commits, 5 up-front magazine refill
     uint64_t ingest_ns[6] = {0, 0, 0, 0, 0, 0};

@@ -77,7 +77,8 @@ struct PyInStream {
       }
       try {
         uint64_t got;
-        if (s.source()->needs_gil()) {
+        static const bool hold_gil = getenv("ALLUXIO_READER_HOLD_GIL") != nullptr;   // A/B knob
+        if (s.source()->needs_gil() || hold_gil) {
           got = s.read_block_part(dst + done, n - done);
         } else {
           py::gil_scoped_release rel;

@@ -2503,9 +2503,246 @@ __global__ __launch_bounds__(kLzThreads) void lz4_compress_batch_kernel(const Lz
   }
 }
 
+// Segmented encoder for batches too small to fill the chip (one wave per 64 KiB chunk leaves
+// 1k chunks at one wave per SIMD, latency-bound).  Each chunk is cut into up to S segments of
+// >= 4 KiB parsed by S independent waves: a wave first re-hashes the `warm` bytes before its
+// segment into its own table (so matches into the preceding data are still found), then runs the
+// batch parse over its segment with matches confined to it.  The first sequence's literal run of a
+// segment depends on where the previous segments' parses ended, so a wave writes its sequences to
+// scratch WITHOUT that first header + literals; the merge kernel places the segments back to back
+// and writes each first header with the literal run joined across the boundary.  Output is the
+// same standard LZ4 block; ratio differs from the one-wave parse only at segment boundaries.
+struct LzSeg {
+  uint32_t first_mpos;   // position of the segment's first match (0xFFFFFFFF: no match)
+  uint32_t first_mcode;  // its match length - 4
+  uint32_t bytes;        // scratch bytes (0xFFFFFFFF: overflow)
+  uint32_t tail;         // anchor after the segment's last match
+};
+constexpr uint32_t kLzSegMin = 4096;
+
+__device__ __forceinline__ uint32_t lz_seg_count(uint32_t len, int S) {
+  const uint32_t k = len / kLzSegMin;
+  return k == 0 ? 1u : (k < (uint32_t)S ? k : (uint32_t)S);
+}
+
+__device__ __forceinline__ void lz_seg_bounds(uint32_t len, uint32_t nseg, uint32_t s, uint32_t* b, uint32_t* e) {
+  const uint32_t seg = ((len + nseg - 1) / nseg + 63) & ~63u;
+  *b = s * seg < len ? s * seg : len;
+  *e = (s + 1) * seg < len && s + 1 < nseg ? (s + 1) * seg : len;
+}
+
+__global__ __launch_bounds__(kLzThreads) void lz4_seg_parse_kernel(const Lz4Chunk* __restrict__ ch, int n, int S,
+                                                                  uint8_t* __restrict__ scratch, uint32_t seg_cap,
+                                                                  LzSeg* __restrict__ segs, uint32_t warm) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint16_t* table = reinterpret_cast<uint16_t*>(smem);                     // 8 KiB
+  const int lane = threadIdx.x;
+  for (int t = blockIdx.x; t < n * S; t += gridDim.x) {
+    const int w = t / S, s = t - (t / S) * S;
+    const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(ch[w].src);
+    const uint32_t len = ch[w].src_bytes < kLzWindow ? ch[w].src_bytes : kLzWindow;
+    const uint32_t nseg = lz_seg_count(len, S);
+    if ((uint32_t)s >= nseg) {
+      if (lane == 0) segs[t] = LzSeg{0xFFFFFFFFu, 0, 0, 0};
+      continue;
+    }
+    uint32_t sb, se;
+    lz_seg_bounds(len, nseg, (uint32_t)s, &sb, &se);
+    const bool last = (uint32_t)s + 1 == nseg;
+    uint8_t* __restrict__ dst = scratch + (size_t)t * seg_cap;
+    for (uint32_t i = lane; i < (1u << kLzHashLog); i += kLzThreads) table[i] = 0xFFFF;
+    __syncthreads();
+    for (uint32_t p = (sb > warm ? sb - warm : 0) + lane; p < sb; p += kLzThreads)
+      table[lz_hash(lzb_read32<false>(src + p))] = (uint16_t)p;
+    __syncthreads();
+    // a match starts before match_limit and ends by end_match; inner segments keep their
+    // matches inside the segment (the block-end rules only bind the last one)
+    const uint32_t match_limit = last ? (len > kLzMfLimit ? len - kLzMfLimit : 0) : se - 3;
+    const uint32_t end_match = last ? (len > kLzLastLiterals ? len - kLzLastLiterals : 0) : se;
+    uint32_t op = 0, anchor = sb, ip = sb;
+    bool have_first = false, overflow = false;
+    uint32_t first_mpos = 0xFFFFFFFFu, first_mcode = 0;
+    while (ip < match_limit) {
+      const uint32_t pos = ip + lane;
+      uint32_t cand = 0xFFFFFFFFu, mlen = 0, h = 0;
+      if (pos < match_limit) {
+        const uint32_t v = lzb_read32<false>(src + pos);
+        h = lz_hash(v);
+        const uint32_t c = table[h];
+        if (c != 0xFFFF && c < pos && pos - c <= 65535 && lzb_read32<false>(src + c) == v) {
+          cand = c;
+          mlen = kLzMinMatch;
+          while (pos + mlen + 4 <= end_match && lzb_read32<false>(src + c + mlen) == lzb_read32<false>(src + pos + mlen))
+            mlen += 4;
+          while (pos + mlen < end_match && src[c + mlen] == src[pos + mlen]) ++mlen;
+        }
+      }
+      __syncthreads();
+      if (pos < match_limit) table[h] = (uint16_t)pos;
+      __syncthreads();
+      unsigned long long m = __ballot(cand != 0xFFFFFFFFu);
+      if (m == 0) { ip += kLzThreads; continue; }
+      unsigned long long sel = 0;
+      uint32_t my_lit = 0, last_end = ip, prev_end = anchor;
+      while (m) {
+        const int g = __ffsll((long long)m) - 1;
+        const uint32_t gml = __shfl(mlen, g);
+        if (lane == g) my_lit = prev_end;
+        sel |= 1ull << g;
+        prev_end = last_end = ip + g + gml;
+        const uint32_t skip = last_end - ip;
+        m = skip >= 64 ? 0ull : (m & (~0ull << skip));
+      }
+      const int g0 = __ffsll((long long)sel) - 1;
+      const bool is_first = !have_first && lane == g0;   // header + literals written by the merge
+      if (!have_first) {
+        first_mpos = ip + g0;
+        first_mcode = __shfl(mlen, g0) - 4;
+        have_first = true;
+      }
+      const bool mine = (sel >> lane) & 1ull;
+      const uint32_t lit = mine && !is_first ? pos - my_lit : 0;
+      const uint32_t need = !mine ? 0
+                          : is_first ? 2 + lz_len_bytes(mlen - 4)
+                                     : 1 + lz_len_bytes(lit) + lit + 2 + lz_len_bytes(mlen - 4);
+      uint32_t incl = need;
+#pragma unroll
+      for (int d = 1; d < kLzThreads; d <<= 1) {
+        const uint32_t tt = __shfl_up(incl, d);
+        if (lane >= d) incl += tt;
+      }
+      const uint32_t total = __shfl(incl, kLzThreads - 1);
+      if (op + total > seg_cap) { overflow = true; break; }
+      const uint32_t o = op + incl - need;
+      if (mine) {
+        const uint32_t mcode = mlen - 4;
+        const uint32_t moff = pos - cand;
+        uint32_t q = o;
+        if (!is_first) {
+          dst[q] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | (mcode >= 15 ? 15 : mcode));
+          q = lz_put_len(dst, q + 1, lit) + lit;
+        }
+        dst[q] = (uint8_t)(moff & 255);
+        dst[q + 1] = (uint8_t)(moff >> 8);
+        lz_put_len(dst, q + 2, mcode);
+      }
+      unsigned long long rest = sel;
+      while (rest) {
+        const int g = __ffsll((long long)rest) - 1;
+        rest &= rest - 1;
+        const uint32_t gl = __shfl(lit, g);
+        if (gl == 0) continue;
+        const uint32_t gs = __shfl(my_lit, g);
+        const uint32_t go = __shfl(o, g) + 1 + lz_len_bytes(gl);
+        for (uint32_t i = lane; i < gl; i += kLzThreads) dst[go + i] = src[gs + i];
+      }
+      op += total;
+      anchor = prev_end;
+      ip = last_end > ip + kLzThreads ? last_end : ip + kLzThreads;
+    }
+    if (lane == 0) segs[t] = LzSeg{first_mpos, first_mcode, overflow ? 0xFFFFFFFFu : op, anchor};
+    __syncthreads();
+  }
+}
+
+constexpr int kLzMergeThreads = 256;
+constexpr int kLzMaxSeg = 16;
+
+__global__ __launch_bounds__(kLzMergeThreads) void lz4_seg_merge_kernel(const Lz4Chunk* __restrict__ ch, int n, int S,
+                                                                       const uint8_t* __restrict__ scratch,
+                                                                       uint32_t seg_cap, const LzSeg* __restrict__ segs,
+                                                                       int32_t* __restrict__ out_sizes) {
+  __shared__ uint32_t s_off[kLzMaxSeg], s_p[kLzMaxSeg], s_fin[3];
+  __shared__ int s_bad;
+  const int tid = threadIdx.x;
+  for (int w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(ch[w].src);
+    uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(ch[w].dst);
+    const uint32_t len = ch[w].src_bytes < kLzWindow ? ch[w].src_bytes : kLzWindow;
+    const LzSeg* sg = segs + (size_t)w * S;
+    if (tid == 0) {
+      uint32_t P = 0, out = 0;
+      int bad = 0;
+      for (int s = 0; s < S; ++s) {
+        const LzSeg g = sg[s];
+        if (g.bytes == 0xFFFFFFFFu) bad = 1;
+        if (g.first_mpos == 0xFFFFFFFFu) { s_off[s] = 0xFFFFFFFFu; continue; }
+        const uint32_t lit = g.first_mpos - P;
+        s_off[s] = out;
+        s_p[s] = P;
+        out += 1 + lz_len_bytes(lit) + lit + g.bytes;
+        P = g.tail;
+      }
+      const uint32_t lit = len - P;
+      s_fin[0] = P;
+      s_fin[1] = out;
+      out += 1 + lz_len_bytes(lit) + lit;
+      s_fin[2] = out;
+      s_bad = bad || out > ch[w].dst_capacity;
+    }
+    __syncthreads();
+    if (s_bad) {
+      if (tid == 0) out_sizes[w] = -1;
+      __syncthreads();
+      continue;
+    }
+    for (int s = 0; s < S; ++s) {
+      if (s_off[s] == 0xFFFFFFFFu) continue;
+      const LzSeg g = sg[s];
+      const uint32_t P = s_p[s], lit = g.first_mpos - P, o = s_off[s];
+      if (tid == 0) {
+        dst[o] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | (g.first_mcode >= 15 ? 15 : g.first_mcode));
+        lz_put_len(dst, o + 1, lit);
+      }
+      const uint32_t q = o + 1 + lz_len_bytes(lit);
+      for (uint32_t i = tid; i < lit; i += kLzMergeThreads) dst[q + i] = src[P + i];
+      const uint8_t* sc = scratch + ((size_t)w * S + s) * seg_cap;
+      for (uint32_t i = tid; i < g.bytes; i += kLzMergeThreads) dst[q + lit + i] = sc[i];
+    }
+    {
+      const uint32_t P = s_fin[0], o = s_fin[1], lit = len - P;
+      if (tid == 0) {
+        dst[o] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+        lz_put_len(dst, o + 1, lit);
+      }
+      const uint32_t q = o + 1 + lz_len_bytes(lit);
+      for (uint32_t i = tid; i < lit; i += kLzMergeThreads) dst[q + i] = src[P + i];
+    }
+    if (tid == 0) out_sizes[w] = (int32_t)s_fin[2];
+    __syncthreads();
+  }
+}
+
+static hipError_t launch_lz4_compress_segmented(const Lz4Chunk* chunks, int n, int32_t* out_sizes, int S,
+                                                hipStream_t stream) {
+  S = S < 1 ? 1 : (S > kLzMaxSeg ? kLzMaxSeg : S);
+  // seg_cap: LZ4's bound for the largest segment (64 KiB / S rounded up to 64, or 4 KiB minimum)
+  const uint32_t seg = std::max<uint32_t>(kLzSegMin * 2, ((kLzWindow + S - 1) / S + 63) & ~63u);
+  const uint32_t seg_cap = (seg + seg / 255 + 16 + 15) & ~15u;
+  const size_t nseg = (size_t)n * S;
+  void* mem = nullptr;
+  hipError_t e = hipMallocAsync(&mem, nseg * seg_cap + nseg * sizeof(LzSeg), stream);
+  if (e != hipSuccess) return e;
+  uint8_t* scratch = static_cast<uint8_t*>(mem);
+  LzSeg* segs = reinterpret_cast<LzSeg*>(scratch + nseg * seg_cap);
+  const size_t table = sizeof(uint16_t) << kLzHashLog;
+  hipLaunchKernelGGL(lz4_seg_parse_kernel, dim3((unsigned)std::min<size_t>(nseg, 65536)), dim3(kLzThreads), table,
+                     stream, chunks, n, S, scratch, seg_cap, segs, 4096u);
+  e = hipGetLastError();
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(lz4_seg_merge_kernel, dim3((unsigned)std::min(n, 65536)), dim3(kLzMergeThreads), 0, stream,
+                       chunks, n, S, scratch, seg_cap, segs, out_sizes);
+    e = hipGetLastError();
+  }
+  const hipError_t f = hipFreeAsync(mem, stream);
+  return e != hipSuccess ? e : f;
+}
+
 // 0: one sequence per probe batch (lz4_compress_kernel); 1: batch parse, chunk in LDS;
-// 2 (default): batch parse reading the chunk from global/L2 (8 KiB LDS per wave)
-static int g_lz4_encode_variant = 2;
+// 2: batch parse reading the chunk from global/L2 (8 KiB LDS per wave); 3: segmented parse
+// (4 waves per chunk) + merge; 4 (default): segmented below 2048 chunks (S = 4096 waves / n,
+// 2..8), batch parse above -- the batch parse fills the chip by itself there
+static int g_lz4_encode_variant = 4;
 void set_lz4_encode_variant(int v) { g_lz4_encode_variant = v; }
 
 hipError_t launch_lz4_compress(const Lz4Chunk* chunks, int n, int32_t* out_sizes,
@@ -2520,6 +2757,10 @@ hipError_t launch_lz4_compress(const Lz4Chunk* chunks, int n, int32_t* out_sizes
     const unsigned grid = (unsigned)std::min(n, 4096);
     hipLaunchKernelGGL((lz4_compress_batch_kernel<true>), dim3(grid), dim3(kLzThreads), table + kLzWindow,
                        stream, chunks, n, out_sizes);
+  } else if (g_lz4_encode_variant == 3) {
+    return launch_lz4_compress_segmented(chunks, n, out_sizes, 4, stream);
+  } else if (g_lz4_encode_variant == 4 && n < 2048) {
+    return launch_lz4_compress_segmented(chunks, n, out_sizes, std::max(2, std::min(8, 4096 / n)), stream);
   } else {
     const unsigned grid = (unsigned)std::min(n, 65536);
     hipLaunchKernelGGL((lz4_compress_batch_kernel<false>), dim3(grid), dim3(kLzThreads), table, stream,

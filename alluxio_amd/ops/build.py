@@ -119,7 +119,14 @@ def build_sanitized(kind: str, out_dir: str | None = None) -> str:
         objs.append(obj)
         path = os.path.join(CSRC, src)
         if src.endswith(".hip"):
-            cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, "-c", path, "-o", obj]
+            # the host half of each .hip file (launchers, page-cache put/get bookkeeping) is
+            # instrumented too; the device half is not (-Xarch_host scopes the sanitizer flags)
+            host = []
+            for f in flags:
+                if f.startswith(("-fsanitize", "-fno-sanitize")):
+                    host += ["-Xarch_host", f]
+            cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, *host,
+                   "-fno-gpu-sanitize", "-c", path, "-o", obj]
         else:
             cmd = [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", *common,
                    *[f for f in flags if f != "-shared-libasan"], "-c", path, "-o", obj]

@@ -360,9 +360,9 @@ def test_magazine_accounting_mixed_workload(gpu, tmp_path):
                 else:
                     data.pop(b)
         elif op == 1:                                  # bulk create, then commit or abort
-            ids = new_ids(int(rng.integers(10, 40)))
+            ids = new_ids(int(rng.integers(64, 120)))          # >= kDeviceAllocMinBlocks: K7 claims
             try:
-                s.create_blocks(7, ids, 0, "", [page * int(rng.integers(1, 4))] * len(ids), True)
+                s.create_blocks(7, ids, 0, "", [page * int(rng.integers(1, 3))] * len(ids), True)
             except Exception:  # noqa: BLE001 - the tier may be full of locked/temp blocks
                 pass
             if step % 12 == 1:

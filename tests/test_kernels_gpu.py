@@ -97,7 +97,7 @@ def test_lz4_device_roundtrip(gpu, variant):
     # device encode (every encoder variant) -> host decode
     ins = [torch.tensor(list(c), dtype=torch.uint8, device=gpu) for c in chunks]
     cap = [C.lz4_compress_bound(len(c)) for c in chunks]
-    for ev in (0, 1, 2):
+    for ev in (0, 1, 2, 3, 4):
         C.set_lz4_encode_variant(ev)
         enc = [torch.zeros(k, dtype=torch.uint8, device=gpu) for k in cap]
         sizes = C.lz4_device([(i.data_ptr(), e.data_ptr(), len(c), k) for i, e, c, k in zip(ins, enc, chunks, cap)],
@@ -109,7 +109,7 @@ def test_lz4_device_roundtrip(gpu, variant):
         small = C.lz4_device([(ins[1].data_ptr(), enc[1].data_ptr(), len(chunks[1]), max(1, len(chunks[1]) // 2))],
                              True, 0)
         assert small[0] < 0, ev
-    C.set_lz4_encode_variant(2)
+    C.set_lz4_encode_variant(4)
     C.set_lz4_decode_variant(-1)
 
 

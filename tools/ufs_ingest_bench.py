@@ -194,7 +194,7 @@ def run(a, depth: int) -> dict:
                     "ingest_GBps": round(cached_bytes / el / 1e9, 3), "ingest_s": round(el, 3),
                     "failed_blocks": w.metrics.counter("AsyncCacheFailedBlocks").value(), "first_failures": fails,
                     "demoted_blocks": st["demoted_blocks"], "demoted_bytes": st["demoted_bytes"],
-                    "batched_moves": st["batched_moves"], "evict_waits": st.get("evict_waits"), "resident_by_medium": tiers,
+                    "batched_moves": st["batched_moves"], "evict_waits": st.get("evict_waits"), "evict_retries": st.get("evict_retries"), "revalidated_away": st.get("revalidated_away"), "resident_by_medium": tiers,
                     "reread_GBps": round(rb / rel / 1e9, 3) if rel > 0 else None, "reread_bytes": rb,
                     "threads": a.threads, "stages": stage}
     finally:
