@@ -77,8 +77,9 @@ struct PyInStream {
       }
       try {
         uint64_t got;
-        static const bool hold_gil = getenv("ALLUXIO_READER_HOLD_GIL") != nullptr;   // A/B knob
-        if (s.source()->needs_gil() || hold_gil) {
+        // refills release the GIL (holding it was measured slower at 16-256 threads:
+        // profiles/r4_worker_bench_host_gil_hold.jsonl)
+        if (s.source()->needs_gil()) {
           got = s.read_block_part(dst + done, n - done);
         } else {
           py::gil_scoped_release rel;

@@ -130,12 +130,6 @@ for s in $STEPS; do
         run wb_host_ab_$pf 900 python tools/worker_bench_host.py --threads 16,256 --transports grpc,ipc --duration 8s --warmup 2s --client-prop alluxio.user.native.reader.prefetch.enabled=$pf --out "$OUT/worker_bench_host_prefetch_ab.jsonl"
       done
       ;;
-    gilab)
-      for pf in false true; do
-        run wb_gil_release_$pf 600 python tools/worker_bench_host.py --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --client-prop alluxio.user.native.reader.prefetch.enabled=$pf --out "$OUT/worker_bench_host_gil_release.jsonl"
-        ALLUXIO_READER_HOLD_GIL=1 run wb_gil_hold_$pf 600 python tools/worker_bench_host.py --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --client-prop alluxio.user.native.reader.prefetch.enabled=$pf --out "$OUT/worker_bench_host_gil_hold.jsonl"
-      done
-      ;;
     hostsweep)
       for rb in 256KB 512KB 1MB; do
         for pf in false true; do
