@@ -134,6 +134,23 @@ class _AckQueue:
         self.q.put(None)
 
 
+def _native_call(ctx, address: str, data_address):
+    """(host, port, channel id, user, timeout ms, domain socket) for a native gRPC call to a
+    worker's data port, or None when the worker is in this process (no socket to skip)."""
+    host, port = data_address or tuple(address.rsplit(":", 1))
+    ch = ctx.worker_channel(address)
+    if ch.is_local:
+        return None
+    cid = ""
+    if ch.auth is not None:
+        ch._channel()                 # SASL handshake once per channel; its id authorizes the call
+        cid = ch.channel_id or ""
+    timeout = int(ctx.conf.get_ms("alluxio.user.streaming.data.timeout", "30sec"))
+    from ..rpc import domain_socket_for
+    uds = domain_socket_for(address) or ""       # a same-node worker's domain socket
+    return host, int(port), cid, ch.user or "", timeout, uds
+
+
 class GrpcBlockReader(BlockReader):
     """Sequential chunked ReadBlock stream with ``offset_received`` acks (GrpcDataReader)."""
 
@@ -216,20 +233,13 @@ class GrpcBlockReader(BlockReader):
         from ..ops.native import lib
         if not lib().FrameRpcServer.grpc_available():
             return None
-        host, port = self.data_address or tuple(self.address.rsplit(":", 1))
-        ch = self.ctx.worker_channel(self.address)
-        if ch.is_local:
-            return None                   # in-process servicer: no socket to skip
-        cid = ""
-        if ch.auth is not None:
-            ch._channel()                 # SASL handshake once per channel; its id authorizes the call
-            cid = ch.channel_id or ""
+        call = _native_call(self.ctx, self.address, self.data_address)
+        if call is None:
+            return None
+        host, port, cid, user, timeout, uds = call
         ufs = self.ufs_opts.SerializeToString() if self.ufs_opts is not None else b""
-        timeout = int(conf.get_ms("alluxio.user.streaming.data.timeout", "30sec"))
-        from ..rpc import domain_socket_for
-        uds = domain_socket_for(self.address) or ""      # a same-node worker's domain socket
-        return lib().GrpcBlockSource(host, int(port), self.block_id, self.length, self.chunk, ufs, self.promote,
-                                     cid, ch.user or "", timeout, uds)
+        return lib().GrpcBlockSource(host, port, self.block_id, self.length, self.chunk, ufs, self.promote,
+                                     cid, user, timeout, uds)
 
     def _close_stream(self):
         if self._reqs is not None:
@@ -672,8 +682,21 @@ class GrpcBlockWriter(BlockWriter):
     """WriteBlock stream (GrpcDataWriter): command, chunks, then half-close -> commit."""
 
     def __init__(self, ctx, address, block_id, tier=0, medium="", reserve=1 << 20, pin=False,
-                 chunk: int | None = None, ufs_fallback_mount: int | None = None):
+                 chunk: int | None = None, ufs_fallback_mount: int | None = None, data_address: tuple | None = None):
         self.chunk = chunk or ctx.conf.get_bytes("alluxio.user.network.writer.chunk.size.bytes", "1MB")
+        self._sink = None
+        if ufs_fallback_mount is None and ctx.conf.get_bool("alluxio.user.native.writer.enabled", "true"):
+            # the same WriteBlock call made by the native gRPC client (csrc/block_source.cpp
+            # GrpcBlockSink): chunks framed around the caller's bytes, GIL released while sending
+            from ..ops.native import lib, native_errors
+            if lib().FrameRpcServer.grpc_available():
+                call = _native_call(ctx, address, data_address)
+                if call is not None:
+                    host, port, cid, user, timeout, uds = call
+                    with native_errors():
+                        self._sink = lib().GrpcBlockSink(host, port, block_id, tier, medium, reserve, pin,
+                                                         self.chunk, cid, user, timeout, uds)
+                    return
         cmd = pb.block.WriteRequestCommand(type=0, id=block_id, offset=0, tier=tier, medium_type=medium,
                                            space_to_reserve=reserve, pin_on_create=pin)
         if ufs_fallback_mount is not None:
@@ -697,6 +720,19 @@ class GrpcBlockWriter(BlockWriter):
 
     def write_ptr(self, offset, ptr, length, kind):
         import ctypes
+        if self._sink is not None:
+            from ..ops.native import native_errors
+            keep = None
+            if kind == DEVICE:
+                import torch
+                from ..ops.native import lib
+                tmp = torch.empty(length, dtype=torch.uint8, device="cuda")
+                lib().batched_copy([(ptr, tmp.data_ptr(), length)], 0)
+                keep = tmp.cpu()
+                ptr = keep.data_ptr()
+            with native_errors():
+                self._sink.write_ptr(ptr, length)
+            return
         if kind == DEVICE:
             import torch
             from ..ops.native import lib
@@ -710,6 +746,12 @@ class GrpcBlockWriter(BlockWriter):
             self._reqs.put(marshal.write_request_frame(mv[i:i + self.chunk]))
 
     def commit(self):
+        if self._sink is not None:
+            from ..ops.native import native_errors
+            sink, self._sink = self._sink, None
+            with native_errors():
+                sink.commit()
+            return
         self._reqs.close()
         self._t.join()
         if self._err:
@@ -720,6 +762,10 @@ class GrpcBlockWriter(BlockWriter):
             raise e
 
     def cancel(self):
+        if self._sink is not None:
+            sink, self._sink = self._sink, None
+            sink.cancel()
+            return
         try:
             self._resp.cancel()
         except Exception:  # noqa: BLE001
@@ -941,7 +987,9 @@ class FileOutStream(io.RawIOBase):
             else:
                 self._writers.append(GrpcBlockWriter(self.ctx, worker_address_str(w.address), bid,
                                                      self.write_tier, self.medium, reserve,
-                                                     ufs_fallback_mount=self.status.mountId if ufs_tier else None))
+                                                     ufs_fallback_mount=self.status.mountId if ufs_tier else None,
+                                                     data_address=(w.address.host,
+                                                                   w.address.dataPort or w.address.rpcPort)))
         self._block_written = 0
 
     def _finish_block(self) -> None:

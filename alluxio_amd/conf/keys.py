@@ -217,6 +217,16 @@ _k("USER_NATIVE_READER_ENABLED", "alluxio.user.native.reader.enabled", "true", S
    "Host reads of FileInStream go through the native chunk-buffered reader (csrc/block_source.cpp): a "
    "read(buf) inside the buffered chunk is a memcpy; refills come from HIP-IPC HBM (D2H DMA), shared "
    "DRAM, the in-process store or a native gRPC ReadBlock stream.")
+_k("USER_NATIVE_WRITER_ENABLED", "alluxio.user.native.writer.enabled", "true", Scope.CLIENT,
+   "Block writes to a remote (other-process) worker use the native gRPC client (csrc/block_source.cpp "
+   "GrpcBlockSink: WriteBlock over HTTP/2 with the chunks framed around the caller's bytes, GIL "
+   "released) instead of grpcio.  UFS-fallback writes keep grpcio.")
+_k("WORKER_NETWORK_WRITER_STAGING_SIZE", "alluxio.worker.network.writer.staging.size", "4MB", Scope.WORKER,
+   "Pinned staging buffer per native WriteBlock stream of an HBM worker (H2D DMA of received chunks).")
+_k("WORKER_TIEREDSTORE_DRAM_PREFAULT", "alluxio.worker.tieredstore.dram.prefault", "false", Scope.WORKER,
+   "Populate the pages of DRAM-tier arenas in the background at startup (GPU hosts pin, and so "
+   "populate, them anyway): first writes into a shared-memory page otherwise pay a fault that "
+   "allocates and zeroes it.")
 _k("USER_NATIVE_READER_BUFFER_SIZE", "alluxio.user.native.reader.buffer.size", "1MB", Scope.CLIENT,
    "Chunk buffer (pinned when a GPU is present) of the native host reader: bytes fetched per refill.")
 _k("USER_NATIVE_READER_PREFETCH_ENABLED", "alluxio.user.native.reader.prefetch.enabled", "true", Scope.CLIENT,

@@ -626,6 +626,281 @@ void GrpcBlockSource::maybe_ack(uint64_t offset) {
   h2::lib().resume_data(c.ng, c.sid);
 }
 
+// ---- GrpcBlockSink: WriteBlock over HTTP/2 -----------------------------------------------------
+struct GrpcBlockSink::Conn {
+  struct Seg {
+    std::string hdr;               // gRPC prefix + WriteRequest/Chunk headers (or a whole message)
+    const uint8_t* data = nullptr; // caller bytes (valid until write() returns)
+    size_t len = 0;
+    size_t off = 0;                // over hdr then data
+  };
+  int fd = -1;
+  void* ng = nullptr;
+  int32_t sid = -1;
+  std::string authority;
+  std::deque<Seg> q;
+  bool closing = false, closed = false, headers_ok = false;
+  int grpc_status = -1;
+  std::string grpc_msg;
+  std::string resp;                // response DATA (WriteResponse messages)
+  std::string inbuf;
+
+  ~Conn() {
+    if (ng) h2::lib().session_del(ng);
+    if (fd >= 0) ::close(fd);
+  }
+  static int on_header(void*, const void* frame, const uint8_t* name, size_t namelen, const uint8_t* value,
+                       size_t valuelen, uint8_t, void* ud) {
+    Conn& c = *static_cast<Conn*>(ud);
+    const h2::FrameHd* hd = static_cast<const h2::FrameHd*>(frame);
+    if (hd->stream_id != c.sid) return 0;
+    const std::string n(reinterpret_cast<const char*>(name), namelen);
+    const std::string v(reinterpret_cast<const char*>(value), valuelen);
+    if (n == ":status") c.headers_ok = v == "200";
+    else if (n == "grpc-status") c.grpc_status = std::atoi(v.c_str());
+    else if (n == "grpc-message") c.grpc_msg = v;
+    return 0;
+  }
+  static int on_data(void*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* ud) {
+    Conn& c = *static_cast<Conn*>(ud);
+    if (sid == c.sid && c.resp.size() < (1u << 20)) c.resp.append(reinterpret_cast<const char*>(data), len);
+    return 0;
+  }
+  static int on_frame(void*, const void* frame, void* ud) {
+    Conn& c = *static_cast<Conn*>(ud);
+    const h2::FrameHd* hd = static_cast<const h2::FrameHd*>(frame);
+    if (hd->stream_id == c.sid && (hd->type == h2::kTypeData || hd->type == h2::kTypeHeaders) &&
+        (hd->flags & h2::kFlagEndStream))
+      c.closed = true;
+    return 0;
+  }
+  static int on_close(void*, int32_t sid, uint32_t, void* ud) {
+    Conn& c = *static_cast<Conn*>(ud);
+    if (sid == c.sid) c.closed = true;
+    return 0;
+  }
+  static ssize_t read_req(void*, int32_t, uint8_t* buf, size_t length, uint32_t* flags, h2::DataSource*, void* ud) {
+    Conn& c = *static_cast<Conn*>(ud);
+    size_t w = 0;
+    while (w < length && !c.q.empty()) {
+      Seg& s = c.q.front();
+      if (s.off < s.hdr.size()) {
+        const size_t n = std::min(length - w, s.hdr.size() - s.off);
+        std::memcpy(buf + w, s.hdr.data() + s.off, n);
+        s.off += n;
+        w += n;
+        continue;
+      }
+      const size_t d = s.off - s.hdr.size();
+      const size_t n = std::min(length - w, s.len - d);
+      if (n) std::memcpy(buf + w, s.data + d, n);
+      s.off += n;
+      w += n;
+      if (s.off == s.hdr.size() + s.len) c.q.pop_front();
+    }
+    if (c.q.empty() && c.closing) {
+      *flags |= h2::kDataEof;      // END_STREAM: the request stream is complete
+      return (ssize_t)w;
+    }
+    return w ? (ssize_t)w : h2::kErrDeferred;
+  }
+  static void* callbacks() {
+    static void* cbs = [] {
+      const h2::Lib& g = h2::lib();
+      void* cb = nullptr;
+      if (!g.ok || g.callbacks_new(&cb) != 0) return (void*)nullptr;
+      g.set_on_header(cb, &Conn::on_header);
+      g.set_on_data_chunk_recv(cb, &Conn::on_data);
+      g.set_on_stream_close(cb, &Conn::on_close);
+      g.set_on_frame_recv(cb, &Conn::on_frame);
+      g.set_read_length(cb, &h2::read_length);
+      return cb;
+    }();
+    return cbs;
+  }
+  void send_pending(int timeout_ms) {
+    const h2::Lib& g = h2::lib();
+    for (;;) {
+      const uint8_t* d = nullptr;
+      const ssize_t n = g.mem_send(ng, &d);
+      if (n < 0) throw std::runtime_error("gRPC client: HTTP/2 framing error");
+      if (n == 0) return;
+      size_t off = 0;
+      while (off < (size_t)n) {
+        const ssize_t w = ::send(fd, d + off, (size_t)n - off, MSG_NOSIGNAL);
+        if (w > 0) {
+          off += (size_t)w;
+          continue;
+        }
+        if (w < 0 && errno == EINTR) continue;
+        if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+          pollfd pf{fd, POLLOUT, 0};
+          if (::poll(&pf, 1, timeout_ms) <= 0) throw std::runtime_error("gRPC client: send timed out");
+          continue;
+        }
+        throw std::runtime_error("gRPC client: connection lost while sending");
+      }
+    }
+  }
+  bool pump(int timeout_ms) {
+    pollfd pf{fd, POLLIN, 0};
+    const int r = ::poll(&pf, 1, timeout_ms);
+    if (r == 0) return false;
+    if (r < 0 && errno != EINTR) throw std::runtime_error("gRPC client: poll failed");
+    if (inbuf.size() < (256u << 10)) inbuf.resize(256u << 10);
+    const ssize_t got = ::recv(fd, &inbuf[0], inbuf.size(), 0);
+    if (got == 0) throw std::runtime_error("gRPC client: connection closed by the worker");
+    if (got < 0) {
+      if (errno == EINTR || errno == EAGAIN) return true;
+      throw std::runtime_error("gRPC client: connection lost");
+    }
+    if (h2::lib().mem_recv(ng, reinterpret_cast<const uint8_t*>(inbuf.data()), (size_t)got) < 0)
+      throw std::runtime_error("gRPC client: malformed WriteBlock response stream");
+    return true;
+  }
+};
+
+namespace {
+int store_code_of(int grpc_status) {
+  switch (grpc_status) {
+    case 5: return kErrNotFound;
+    case 6: return kErrAlreadyExists;
+    case 8: return kErrOutOfSpace;
+    case 3: return kErrInvalidArgument;
+    case 9: return kErrInvalidState;
+    case 4: return kErrTimeout;
+    default: return kErrIo;
+  }
+}
+}  // namespace
+
+GrpcBlockSink::GrpcBlockSink(Options o) : o_(std::move(o)) {
+  if (!Conn::callbacks()) throw std::runtime_error("gRPC client: libnghttp2 is not available");
+  auto c = std::make_unique<Conn>();
+  const h2::Lib& g = h2::lib();
+  c->fd = o_.unix_path.empty() ? connect_tcp(o_.host, o_.port, o_.timeout_ms) : connect_unix(o_.unix_path, o_.timeout_ms);
+  if (g.client_new2(&c->ng, Conn::callbacks(), c.get(), nullptr) != 0) throw std::runtime_error("gRPC client: session");
+  const h2::SettingsEntry iv[] = {{h2::kSettingsEnablePush, 0},
+                                  {h2::kSettingsInitialWindowSize, 1u << 20},
+                                  {h2::kSettingsMaxFrameSize, h2::kMaxFramePayload}};
+  g.submit_settings(c->ng, 0, iv, 3);
+  // WriteRequest{command{type=0 id tier pin space_to_reserve medium_type}}
+  std::string cmd;
+  put_field_varint(cmd, 1, 0);
+  put_field_varint(cmd, 2, (uint64_t)o_.block_id);
+  put_field_varint(cmd, 4, (uint64_t)(uint32_t)o_.tier);
+  if (!o_.medium.empty()) {
+    h2::put_varint(cmd, (8u << 3) | 2);
+    h2::put_varint(cmd, o_.medium.size());
+    cmd += o_.medium;
+  }
+  if (o_.pin) put_field_varint(cmd, 9, 1);
+  put_field_varint(cmd, 10, o_.reserve);
+  std::string req;
+  h2::put_varint(req, (1u << 3) | 2);
+  h2::put_varint(req, cmd.size());
+  req += cmd;
+  Conn::Seg first;
+  first.hdr.push_back('\0');
+  h2::put_be32(first.hdr, (uint32_t)req.size());
+  first.hdr += req;
+  c->q.push_back(std::move(first));
+  c->authority = o_.host + ":" + std::to_string(o_.port);
+  std::vector<h2::Nv> nva = {h2::nv(":method", "POST"), h2::nv(":scheme", "http"),
+                             h2::nv(":path", "/alluxio.grpc.block.BlockWorker/WriteBlock"),
+                             h2::nv(":authority", c->authority), h2::nv("content-type", "application/grpc"),
+                             h2::nv("te", "trailers")};
+  if (!o_.channel_id.empty()) nva.push_back(h2::nv("channel-id", o_.channel_id));
+  if (!o_.user.empty()) nva.push_back(h2::nv("alluxio-user", o_.user));
+  h2::DataProvider dp;
+  dp.source.ptr = c.get();
+  dp.read_callback = &Conn::read_req;
+  c->sid = g.submit_request(c->ng, nullptr, nva.data(), nva.size(), &dp, nullptr);
+  if (c->sid < 0) throw std::runtime_error("gRPC client: cannot submit WriteBlock");
+  c_ = std::move(c);
+  wait_drained();
+}
+
+GrpcBlockSink::~GrpcBlockSink() {
+  if (c_ && !c_->closed) cancel();
+}
+
+void GrpcBlockSink::wait_drained() {
+  Conn& c = *c_;
+  h2::lib().resume_data(c.ng, c.sid);
+  c.send_pending(o_.timeout_ms);
+  while (!c.q.empty()) {
+    if (c.closed) break;                 // the worker failed the call early
+    if (!c.pump(o_.timeout_ms))
+      throw StoreError(kErrTimeout, "WriteBlock of block " + std::to_string(o_.block_id) + " timed out");
+    h2::lib().resume_data(c.ng, c.sid);  // WINDOW_UPDATEs reopen the send window
+    c.send_pending(o_.timeout_ms);
+  }
+  if (c.closed && c.grpc_status > 0) {
+    c.q.clear();
+    throw StoreError(store_code_of(c.grpc_status), "WriteBlock of block " + std::to_string(o_.block_id) +
+                                                       " failed (gRPC status " + std::to_string(c.grpc_status) +
+                                                       "): " + c.grpc_msg);
+  }
+}
+
+void GrpcBlockSink::write(const uint8_t* p, uint64_t n) {
+  if (!c_ || c_->closing) throw StoreError(kErrInvalidState, "write after commit/cancel");
+  Conn& c = *c_;
+  uint64_t off = 0;
+  while (off < n) {
+    const size_t k = (size_t)std::min<uint64_t>(o_.chunk, n - off);
+    // WriteRequest{chunk(2){data(1)}}
+    std::string inner;
+    h2::put_varint(inner, (1u << 3) | 2);
+    h2::put_varint(inner, k);
+    std::string outer;
+    h2::put_varint(outer, (2u << 3) | 2);
+    h2::put_varint(outer, inner.size() + k);
+    Conn::Seg s;
+    s.hdr.push_back('\0');
+    h2::put_be32(s.hdr, (uint32_t)(outer.size() + inner.size() + k));
+    s.hdr += outer;
+    s.hdr += inner;
+    s.data = p + off;
+    s.len = k;
+    c.q.push_back(std::move(s));
+    off += k;
+  }
+  wait_drained();                        // the caller's bytes are in HTTP/2 frames from here on
+  written_ += n;
+}
+
+uint64_t GrpcBlockSink::commit() {
+  if (!c_) throw StoreError(kErrInvalidState, "commit after cancel");
+  Conn& c = *c_;
+  c.closing = true;
+  wait_drained();
+  while (!c.closed) {
+    if (!c.pump(o_.timeout_ms))
+      throw StoreError(kErrTimeout, "commit of block " + std::to_string(o_.block_id) + " timed out");
+    c.send_pending(o_.timeout_ms);
+  }
+  if (c.grpc_status != 0)
+    throw StoreError(store_code_of(c.grpc_status), "WriteBlock of block " + std::to_string(o_.block_id) +
+                                                       " failed (gRPC status " + std::to_string(c.grpc_status) +
+                                                       "): " + c.grpc_msg);
+  const uint64_t n = written_;
+  c_.reset();
+  return n;
+}
+
+void GrpcBlockSink::cancel() {
+  if (!c_) return;
+  Conn& c = *c_;
+  try {
+    h2::lib().submit_rst_stream(c.ng, 0, c.sid, 8 /*CANCEL*/);
+    c.send_pending(1000);
+  } catch (...) {
+  }
+  c_.reset();
+}
+
 // ---- prefetch pool ------------------------------------------------------------------------------
 namespace {
 

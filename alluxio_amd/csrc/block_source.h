@@ -117,6 +117,42 @@ class GrpcBlockSource : public BlockSource {
   std::unique_ptr<Conn> c_;
 };
 
+// A block written to a worker's data port: WriteBlock over HTTP/2 spoken directly with libnghttp2
+// (command, then WriteRequest{chunk} messages framed around the caller's bytes -- copied once, into
+// the HTTP/2 frames --, half-close, final WriteResponse).  The native data server writes the
+// chunks into the block on its I/O threads (csrc/data_server.cpp); any gRPC BlockWorker works.
+class GrpcBlockSink {
+ public:
+  struct Options {
+    std::string host;
+    int port = 0;
+    std::string unix_path;
+    int64_t block_id = 0;
+    int tier = 0;
+    std::string medium;
+    uint64_t reserve = 1u << 20;
+    bool pin = false;
+    uint64_t chunk = 1u << 20;       // bytes per WriteRequest message
+    std::string channel_id, user;
+    int timeout_ms = 60000;
+  };
+  explicit GrpcBlockSink(Options o);
+  ~GrpcBlockSink();
+  // Streams n bytes; returns once they are in the socket (flow control permitting).
+  void write(const uint8_t* p, uint64_t n);
+  // Half-closes and waits for the worker's commit; returns the committed length.
+  uint64_t commit();
+  void cancel();
+  uint64_t written() const { return written_; }
+  struct Conn;
+
+ private:
+  void wait_drained();
+  Options o_;
+  std::unique_ptr<Conn> c_;
+  uint64_t written_ = 0;
+};
+
 // Pinned (device-mapped) host buffer for a chunk buffer (pooled by size; malloc without a GPU).
 uint8_t* host_buffer_alloc(uint64_t n, bool* pinned);
 // Gives a buffer of host_buffer_alloc(n) back (pinned ones to the pool).

@@ -225,6 +225,61 @@ void bind_data_path(py::module_& m) {
            py::arg("host"), py::arg("port"), py::arg("block_id"), py::arg("length"), py::arg("chunk") = 1u << 20,
            py::arg("ufs_options") = py::bytes(), py::arg("promote") = false, py::arg("channel_id") = "",
            py::arg("user") = "", py::arg("timeout_ms") = 60000, py::arg("unix_path") = "");
+  py::class_<GrpcBlockSink, std::shared_ptr<GrpcBlockSink>>(m, "GrpcBlockSink")
+      .def(py::init([](const std::string& host, int port, int64_t block_id, int tier, const std::string& medium,
+                       uint64_t reserve, bool pin, uint64_t chunk, const std::string& channel_id,
+                       const std::string& user, int timeout_ms, const std::string& unix_path) {
+             GrpcBlockSink::Options o;
+             o.host = host;
+             o.port = port;
+             o.unix_path = unix_path;
+             o.block_id = block_id;
+             o.tier = tier;
+             o.medium = medium;
+             o.reserve = reserve ? reserve : (1u << 20);
+             o.pin = pin;
+             o.chunk = chunk ? chunk : (1u << 20);
+             o.channel_id = channel_id;
+             o.user = user;
+             o.timeout_ms = timeout_ms;
+             py::gil_scoped_release rel;
+             try {
+               return std::make_shared<GrpcBlockSink>(std::move(o));
+             } catch (const StoreError&) {
+               throw;
+             } catch (const std::exception& e) {
+               throw StoreError(kErrIo, e.what());
+             }
+           }),
+           py::arg("host"), py::arg("port"), py::arg("block_id"), py::arg("tier") = 0, py::arg("medium") = "",
+           py::arg("reserve") = 1u << 20, py::arg("pin") = false, py::arg("chunk") = 1u << 20,
+           py::arg("channel_id") = "", py::arg("user") = "", py::arg("timeout_ms") = 60000,
+           py::arg("unix_path") = "")
+      .def("write_ptr", [](GrpcBlockSink& s, uint64_t ptr, uint64_t n) {
+             py::gil_scoped_release rel;
+             try {
+               s.write(reinterpret_cast<const uint8_t*>(ptr), n);
+             } catch (const StoreError&) {
+               throw;
+             } catch (const std::exception& e) {
+               throw StoreError(kErrIo, e.what());
+             }
+           }, py::arg("ptr"), py::arg("n"))
+      .def("commit", [](GrpcBlockSink& s) {
+             py::gil_scoped_release rel;
+             try {
+               return s.commit();
+             } catch (const StoreError&) {
+               throw;
+             } catch (const std::exception& e) {
+               throw StoreError(kErrIo, e.what());
+             }
+           })
+      .def("cancel", [](GrpcBlockSink& s) {
+             py::gil_scoped_release rel;
+             s.cancel();
+           })
+      .def_property_readonly("written", &GrpcBlockSink::written);
   py::class_<PySource, BlockSource, std::shared_ptr<PySource>>(m, "PySource")
       .def(py::init<py::object, uint64_t>(), py::arg("reader"), py::arg("length"));
 
@@ -278,7 +333,10 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("bytes", [](const DataServerStats& s) { return s.bytes.load(); })
       .def_property_readonly("domain_bytes", [](const DataServerStats& s) { return s.domain_bytes.load(); })
       .def_property_readonly("chunks", [](const DataServerStats& s) { return s.chunks.load(); })
-      .def_property_readonly("staged_bytes", [](const DataServerStats& s) { return s.staged_bytes.load(); });
+      .def_property_readonly("staged_bytes", [](const DataServerStats& s) { return s.staged_bytes.load(); })
+      .def_property_readonly("write_streams", [](const DataServerStats& s) { return s.write_streams.load(); })
+      .def_property_readonly("write_declined", [](const DataServerStats& s) { return s.write_declined.load(); })
+      .def_property_readonly("write_bytes", [](const DataServerStats& s) { return s.write_bytes.load(); });
   m.def("serve_block_reads", [](FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk,
                                 uint64_t window) {
           auto stats = std::make_shared<DataServerStats>();
@@ -286,6 +344,11 @@ void bind_data_path(py::module_& m) {
           return stats;
         }, py::arg("server"), py::arg("method"), py::arg("store"), py::arg("max_chunk"), py::arg("window"),
         py::keep_alive<1, 3>());
+  m.def("serve_block_writes", [](FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
+                                 uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats) {
+          serve_block_writes(srv, method, commit_method, store, stage_bytes, stats);
+        }, py::arg("server"), py::arg("method"), py::arg("commit_method"), py::arg("store"), py::arg("stage_bytes"),
+        py::arg("stats"), py::keep_alive<1, 4>());
   m.def("stream_recv", [](FrameRpcServer& srv, uint64_t token, int timeout_ms) -> py::tuple {
           std::string msg;
           int rc;

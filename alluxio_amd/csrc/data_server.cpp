@@ -233,6 +233,259 @@ class BlockReadStream : public NativeStream {
 
 std::atomic<int64_t> g_session{(int64_t)1 << 62};   // above the Python range (utils/ids.py)
 
+// ---- WriteBlock ---------------------------------------------------------------------------------
+// WriteRequestCommand (proto/defs/block.py): type=1 id=2 offset=3 tier=4 flush=5
+// create_ufs_file_options=6 create_ufs_block_options=7 medium_type=8 pin_on_create=9
+// space_to_reserve=10.  WriteRequest: command=1 chunk=2 (Chunk: data=1).
+struct WriteCmd {
+  int64_t type = 0, id = 0, offset = 0, tier = 0, reserve = 0;
+  bool has_tier = false, flush = false, pin = false, has_ufs = false;
+  std::string medium;
+};
+
+bool skip_field(const uint8_t* p, size_t n, size_t* i, uint32_t wt) {
+  if (wt == 0) {
+    uint64_t v;
+    return h2::get_varint(p, n, i, &v);
+  }
+  if (wt == 2) {
+    uint64_t len;
+    if (!h2::get_varint(p, n, i, &len) || len > n - *i) return false;
+    *i += (size_t)len;
+    return true;
+  }
+  if (wt == 1 && n - *i >= 8) { *i += 8; return true; }
+  if (wt == 5 && n - *i >= 4) { *i += 4; return true; }
+  return false;
+}
+
+bool parse_write_command(const uint8_t* p, size_t n, WriteCmd* c) {
+  size_t i = 0;
+  while (i < n) {
+    uint64_t key;
+    if (!h2::get_varint(p, n, &i, &key)) return false;
+    const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (wt == 0) {
+      uint64_t v;
+      if (!h2::get_varint(p, n, &i, &v)) return false;
+      switch (field) {
+        case 1: c->type = (int64_t)v; break;
+        case 2: c->id = (int64_t)v; break;
+        case 3: c->offset = (int64_t)v; break;
+        case 4: c->tier = (int64_t)(int32_t)v; c->has_tier = true; break;
+        case 5: c->flush = v != 0; break;
+        case 9: c->pin = v != 0; break;
+        case 10: c->reserve = (int64_t)v; break;
+        default: break;
+      }
+    } else if (wt == 2) {
+      uint64_t len;
+      if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
+      if (field == 6 || field == 7) c->has_ufs = true;
+      if (field == 8) c->medium.assign(reinterpret_cast<const char*>(p + i), (size_t)len);
+      i += (size_t)len;
+    } else if (!skip_field(p, n, &i, wt)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// Splits one WriteRequest into its command (if any) and its chunk bytes (pointer into `data`).
+bool parse_write_request(const char* data, size_t n, WriteCmd* cmd, bool* has_cmd, const uint8_t** chunk,
+                         size_t* chunk_len) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(data);
+  size_t i = 0;
+  *has_cmd = false;
+  *chunk = nullptr;
+  *chunk_len = 0;
+  while (i < n) {
+    uint64_t key;
+    if (!h2::get_varint(p, n, &i, &key)) return false;
+    const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (wt == 2 && (field == 1 || field == 2)) {
+      uint64_t len;
+      if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
+      if (field == 1) {
+        *has_cmd = true;
+        if (!parse_write_command(p + i, (size_t)len, cmd)) return false;
+      } else {                                    // Chunk{data=1}
+        size_t j = i;
+        const size_t end = i + (size_t)len;
+        while (j < end) {
+          uint64_t k2;
+          if (!h2::get_varint(p, end, &j, &k2)) return false;
+          if ((k2 >> 3) == 1 && (k2 & 7) == 2) {
+            uint64_t l2;
+            if (!h2::get_varint(p, end, &j, &l2) || l2 > end - j) return false;
+            *chunk = p + j;
+            *chunk_len = (size_t)l2;
+            j += (size_t)l2;
+          } else if (!skip_field(p, end, &j, (uint32_t)(k2 & 7))) {
+            return false;
+          }
+        }
+      }
+      i += (size_t)len;
+    } else if (!skip_field(p, n, &i, wt)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+int grpc_status_of(const StoreError& e) {
+  switch (e.code) {
+    case kErrNotFound: return 5;          // NOT_FOUND
+    case kErrAlreadyExists: return 6;     // ALREADY_EXISTS
+    case kErrOutOfSpace: return 8;        // RESOURCE_EXHAUSTED
+    case kErrInvalidArgument: return 3;   // INVALID_ARGUMENT
+    case kErrInvalidState: return 9;      // FAILED_PRECONDITION
+    case kErrTimeout: return 4;           // DEADLINE_EXCEEDED
+    default: return 13;                   // INTERNAL
+  }
+}
+
+std::string write_response_frame(uint64_t offset) {
+  std::string m;
+  if (offset) {
+    h2::put_varint(m, (1u << 3) | 0);
+    h2::put_varint(m, offset);
+  }
+  std::string f;
+  f.push_back('\0');
+  h2::put_be32(f, (uint32_t)m.size());
+  f += m;
+  return f;
+}
+
+class BlockWriteStream : public NativeStream {
+ public:
+  BlockWriteStream(BlockStore* store, int64_t session, int64_t block_id, uint64_t pos, bool pin, bool device,
+                   uint32_t commit_method, std::shared_ptr<StagingPool> pool, std::shared_ptr<DataServerStats> stats)
+      : store_(store), session_(session), block_(block_id), pos_(pos), pin_(pin), device_(device),
+        commit_(commit_method), pool_(std::move(pool)), stats_(std::move(stats)) {}
+
+  ~BlockWriteStream() override {
+    if (stage_) pool_->put(stage_);
+    try {
+      store_->cleanup_session(session_);     // aborts the temp block unless Python committed it
+    } catch (...) {
+    }
+  }
+
+  void on_message(const char* p, size_t n) override {
+    if (err_ || ended_) return;
+    WriteCmd cmd;
+    bool has_cmd;
+    const uint8_t* chunk;
+    size_t len;
+    if (!parse_write_request(p, n, &cmd, &has_cmd, &chunk, &len)) {
+      fail(3, "malformed WriteRequest");
+      return;
+    }
+    try {
+      if (len) write(chunk, len);
+    } catch (const StoreError& e) {
+      fail(grpc_status_of(e), std::string("writing block ") + std::to_string(block_) + ": " + e.what());
+      return;
+    } catch (const std::exception& e) {
+      fail(13, std::string("writing block ") + std::to_string(block_) + ": " + e.what());
+      return;
+    }
+    if (has_cmd && cmd.flush) out_ += write_response_frame(pos_);
+  }
+
+  bool on_end(uint32_t* method, std::string* payload) override {
+    ended_ = true;
+    if (err_) return false;
+    // NativeWriteCommitRequest: session_id=1 block_id=2 length=3 pin=4
+    std::string m;
+    h2::put_varint(m, (1u << 3));
+    h2::put_varint(m, (uint64_t)session_);
+    h2::put_varint(m, (2u << 3));
+    h2::put_varint(m, (uint64_t)block_);
+    h2::put_varint(m, (3u << 3));
+    h2::put_varint(m, pos_);
+    if (pin_) {
+      h2::put_varint(m, (4u << 3));
+      h2::put_varint(m, 1);
+    }
+    *method = commit_;
+    *payload = std::move(m);
+    return true;
+  }
+
+  void on_reply(int status, const std::string& msg, const std::string& payload) override {
+    if (status != 0) {
+      fail(status, msg);
+      return;
+    }
+    out_.push_back('\0');
+    h2::put_be32(out_, (uint32_t)payload.size());
+    out_ += payload;
+    done_ = true;
+  }
+
+  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    if (err_) {
+      *status = err_status_;
+      *msg = err_msg_;
+      return -1;
+    }
+    const size_t n = std::min(max, out_.size() - out_off_);
+    std::memcpy(dst, out_.data() + out_off_, n);
+    out_off_ += n;
+    if (out_off_ == out_.size()) {
+      out_.clear();
+      out_off_ = 0;
+      if (done_) *eof = true;
+    }
+    return (ssize_t)n;
+  }
+
+ private:
+  void fail(int status, const std::string& msg) {
+    if (err_) return;
+    err_ = true;
+    err_status_ = status;
+    err_msg_ = msg;
+  }
+
+  void write(const uint8_t* p, size_t n) {
+    if (!device_) {       // host arena / file dir: straight from the HTTP/2 receive buffer
+      store_->write(session_, block_, pos_, reinterpret_cast<uint64_t>(p), n, (int)MemKind::kHost, 0, true);
+    } else {              // HBM: through pinned staging, so the H2D is a DMA and not a pageable copy
+      if (!stage_) stage_ = pool_->get();
+      hipStream_t st = thread_stream(store_);
+      size_t done = 0;
+      while (done < n) {
+        const size_t k = (size_t)std::min<uint64_t>(n - done, pool_->size());
+        std::memcpy(stage_, p + done, k);
+        store_->write(session_, block_, pos_ + done, reinterpret_cast<uint64_t>(stage_), k, (int)MemKind::kHost,
+                      reinterpret_cast<uint64_t>(st), true);
+        done += k;
+      }
+    }
+    pos_ += n;
+    stats_->write_bytes.fetch_add(n, std::memory_order_relaxed);
+  }
+
+  BlockStore* store_;
+  int64_t session_, block_;
+  uint64_t pos_;
+  bool pin_, device_;
+  uint32_t commit_;
+  std::shared_ptr<StagingPool> pool_;
+  std::shared_ptr<DataServerStats> stats_;
+  uint8_t* stage_ = nullptr;
+  std::string out_;
+  size_t out_off_ = 0;
+  bool ended_ = false, done_ = false, err_ = false;
+  int err_status_ = 0;
+  std::string err_msg_;
+};
+
 }  // namespace
 
 void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk, uint64_t window,
@@ -295,6 +548,56 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
       } catch (...) {
       }
       *status = 13;
+      *msg = e.what();
+      return nullptr;
+    }
+  });
+}
+
+void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
+                        uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats) {
+  if (stage_bytes == 0) stage_bytes = 4u << 20;
+  auto pool = std::make_shared<StagingPool>(stage_bytes, store->has_device());
+  FrameRpcServer* s = &srv;
+  srv.set_native_stream(method, [=](const std::string& first, const std::string& cid, const std::string& user,
+                                    bool unix_peer, int* status, std::string* msg) -> std::unique_ptr<NativeStream> {
+    (void)user;
+    (void)unix_peer;
+    WriteCmd cmd;
+    bool has_cmd;
+    const uint8_t* chunk;
+    size_t len;
+    if (!parse_write_request(first.data(), first.size(), &cmd, &has_cmd, &chunk, &len) || !has_cmd) {
+      *status = 3;
+      *msg = "WriteBlock stream must start with a command";
+      return nullptr;
+    }
+    if (s->require_channel_auth() && (cid.empty() || !s->channel_user(cid, nullptr))) {
+      *status = 16;
+      *msg = cid.empty() ? "channel is not authenticated (no channel-id)" : "channel " + cid + " is not authenticated";
+      return nullptr;
+    }
+    if (cmd.type != 0 || cmd.has_ufs || cmd.offset < 0) {   // UFS_FILE / UFS_FALLBACK_BLOCK: Python
+      stats->write_declined.fetch_add(1, std::memory_order_relaxed);
+      return nullptr;
+    }
+    const int64_t session = g_session.fetch_add(1);
+    const uint64_t reserve = cmd.reserve > 0 ? (uint64_t)cmd.reserve : (1u << 20);
+    try {
+      const int dir = store->create_block(session, cmd.id, cmd.medium.empty() ? (cmd.has_tier ? (int)cmd.tier : 0) : -1,
+                                          cmd.medium, reserve, true, cmd.pin);
+      const bool device = store->dir_spec(dir).kind == DirKind::kDevice;
+      auto ws = std::unique_ptr<BlockWriteStream>(new BlockWriteStream(store, session, cmd.id, (uint64_t)cmd.offset,
+                                                                       cmd.pin, device, commit_method, pool, stats));
+      stats->write_streams.fetch_add(1, std::memory_order_relaxed);
+      if (len) ws->on_message(first.data(), first.size());   // a command that carries data too
+      return ws;
+    } catch (const StoreError& e) {
+      try {
+        store->cleanup_session(session);
+      } catch (...) {
+      }
+      *status = grpc_status_of(e);
       *msg = e.what();
       return nullptr;
     }

@@ -31,11 +31,23 @@ struct DataServerStats {
   std::atomic<uint64_t> domain_bytes{0}; // of which to Unix-domain-socket (same-node) clients
   std::atomic<uint64_t> chunks{0};
   std::atomic<uint64_t> staged_bytes{0}; // of which D2H-staged from HBM
+  std::atomic<uint64_t> write_streams{0};  // WriteBlock calls served natively
+  std::atomic<uint64_t> write_declined{0}; // WriteBlock calls handed to Python (UFS / fallback)
+  std::atomic<uint64_t> write_bytes{0};    // block bytes written natively
 };
 
 // Serve `method` (the ReadBlock path's index) of `srv` from `store`.  `max_chunk` caps a client's
 // chunk_size, `window` is the un-acked byte limit per call.
 void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk,
                        uint64_t window, std::shared_ptr<DataServerStats> stats);
+
+// Serve `method` (WriteBlock) of `srv` into `store` for ALLUXIO_BLOCK writes: the block is created
+// on the first message, chunk messages are written into it on the I/O thread (HBM: through a
+// pinned staging buffer and an async H2D on the thread's stream), flush commands are answered
+// with the offset; at the client's half-close the commit -- CRC, master report -- runs in Python
+// as the internal unary `commit_method` (NativeWriteCommitRequest) whose reply ends the call.
+// UFS_FILE / UFS_FALLBACK_BLOCK writes go to the Python servicer.
+void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
+                        uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats);
 
 }  // namespace amdx

@@ -174,6 +174,7 @@ struct FrameRpcServer::H2 {
   static ssize_t read_body(void* session, int32_t sid, uint8_t* buf, size_t length, uint32_t* flags, h2::DataSource*,
                            void* ud);
   static void take_messages(Session& S, int32_t sid, Stream& st, bool end_stream);
+  static void post_python(Session& S, int32_t sid, Stream& st, uint32_t method, std::string payload);
   static void dispatch(Session& S, int32_t sid, Stream& st, std::string msg);
   static void start_response(Session& S, int32_t sid, Stream& st);
   static void fail_locked(Session& S, int32_t sid, Stream& st, int status, const std::string& msg);
@@ -290,6 +291,9 @@ int FrameRpcServer::H2::on_data(void*, uint8_t, int32_t sid, const uint8_t* data
     return 0;
   }
   it->second.in.append(reinterpret_cast<const char*>(data), len);
+  // a native stream takes every message as soon as it is complete: return its window as the
+  // bytes arrive, so a message larger than the stream window cannot stall the call
+  if (it->second.native) S.consume_streams.emplace_back(sid, len);
   return 0;
 }
 
@@ -320,20 +324,22 @@ void FrameRpcServer::H2::take_messages(Session& S, int32_t sid, Stream& st, bool
     }
     if (st.in.size() - off - 5 < len) break;
     const size_t wire = 5 + (size_t)len;
-    std::string msg = st.in.substr(off + 5, len);
+    const char* body = st.in.data() + off + 5;     // valid until st.in is erased below
     off += wire;
     if (!st.dispatched) {
       st.dispatched = true;
       S.consume_streams.emplace_back(sid, wire);
-      dispatch(S, sid, st, std::move(msg));
+      dispatch(S, sid, st, std::string(body, len));
+      // bytes after the first message arrived before the stream was native: return them now
+      // (later ones are returned on arrival, in on_data)
+      if (st.native && st.in.size() > off) S.consume_streams.emplace_back(sid, st.in.size() - off);
     } else if (st.native) {
-      S.consume_streams.emplace_back(sid, wire);
-      st.native->on_message(msg.data(), msg.size());
+      st.native->on_message(body, len);             // no copy: data chunks go straight to the store
       h2::lib().resume_data(S.ng, sid);     // the message may reopen the window
     } else if (st.bridge) {
       Bridge& b = *st.bridge;
       std::lock_guard<std::mutex> g(b.mu);
-      b.inbound.emplace_back(std::move(msg), wire);
+      b.inbound.emplace_back(std::string(body, len), wire);
       b.queued += wire;
       if (b.queued > kBridgeQueued) b.deferred += wire;     // window returns when Python catches up
       else S.consume_streams.emplace_back(sid, wire);
@@ -355,8 +361,36 @@ void FrameRpcServer::H2::take_messages(Session& S, int32_t sid, Stream& st, bool
       std::lock_guard<std::mutex> g(st.bridge->mu);
       st.bridge->half_closed = true;
       st.bridge->cv.notify_all();
+    } else if (st.native) {
+      uint32_t m = 0;
+      std::string payload;
+      if (st.native->on_end(&m, &payload)) post_python(S, sid, st, m, std::move(payload));
+      else h2::lib().resume_data(S.ng, sid);
     }
   }
+}
+
+// Queues an internal request of a native stream for Python (see NativeStream::on_end); its reply
+// comes back through respond() -> respond_locked() -> NativeStream::on_reply.
+void FrameRpcServer::H2::post_python(Session& S, int32_t sid, Stream& st, uint32_t method, std::string payload) {
+  FrameRpcServer& srv = *S.srv;
+  if (method >= srv.lanes_.size()) {
+    fail_locked(S, sid, st, 13 /*INTERNAL*/, "native stream posted an unknown method");
+    return;
+  }
+  FrameRequest rq;
+  rq.token = ((uint64_t)S.conn->id << 32) | (uint32_t)sid;
+  rq.method = method;
+  rq.user = "\x02\x01" + st.cid;
+  rq.user.push_back('\0');
+  rq.user += st.auser;
+  rq.payload = std::move(payload);
+  Lane& l = *srv.lane_q_[srv.lanes_[method]];
+  {
+    std::lock_guard<std::mutex> g(l.mu);
+    l.q.push_back(std::move(rq));
+  }
+  l.cv.notify_one();
 }
 
 int FrameRpcServer::H2::on_close(void*, int32_t sid, uint32_t, void* ud) {
@@ -465,6 +499,11 @@ void FrameRpcServer::H2::respond_locked(Session& S, int32_t sid, int status, con
   auto it = S.streams.find(sid);
   if (it == S.streams.end() || it->second.finished) return;   // cancelled or answered
   Stream& st = it->second;
+  if (st.native) {                 // the reply of a native stream's internal request
+    st.native->on_reply(status, msg, payload);
+    h2::lib().resume_data(S.ng, sid);
+    return;
+  }
   if (status != 0) {
     fail_locked(S, sid, st, status, msg);
     return;
@@ -1018,6 +1057,38 @@ void FrameRpcServer::io_loop(int idx) {
 
 void FrameRpcServer::on_readable(const std::shared_ptr<Conn>& c, int ep) {
   (void)ep;
+  if (c->proto == 2) {
+    // HTTP/2: every socket read goes straight into nghttp2 (no staging of the whole socket
+    // backlog in c->in -- uploads arrive at GB/s), window returns and writes after the batch
+    thread_local std::vector<char> big(256u << 10);
+    bool eof = false, ok = true;
+    for (int reads = 0; reads < 64 && ok; ++reads) {   // bounded: other connections get a turn
+      const ssize_t r = ::recv(c->fd, big.data(), big.size(), 0);
+      if (r > 0) {
+        std::lock_guard<std::mutex> g(c->wmu);
+        if (!c->h2) return;
+        ok = h2::lib().mem_recv(c->h2->ng, reinterpret_cast<const uint8_t*>(big.data()), (size_t)r) >= 0;
+        if ((size_t)r < big.size()) break;
+        continue;
+      }
+      if (r == 0) {
+        eof = true;
+        break;
+      }
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      eof = true;
+      break;
+    }
+    {
+      std::lock_guard<std::mutex> g(c->wmu);
+      if (!c->h2) return;
+      H2::apply_consumed(*c->h2);
+      ok = ok && H2::flush_locked(*c->h2);
+    }
+    if (!ok || eof) close_conn(c->id);
+    return;
+  }
   char buf[65536];
   bool eof = false;
   for (;;) {

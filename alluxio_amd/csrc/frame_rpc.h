@@ -55,6 +55,12 @@ class NativeStream {
   // *eof unset = nothing to send until the next request message arrives (flow-control window);
   // *eof = the call is complete.  -1 = the call failed with *status / *msg (sent as trailers).
   virtual ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) = 0;
+  // The client half-closed the request stream.  true = finish the call in Python: the server
+  // queues {*method, *payload} on that method's lane as an internal unary request (caller string
+  // prefixed "\x02") and hands its reply to on_reply(); false = produce() decides.
+  virtual bool on_end(uint32_t* method, std::string* payload) { return false; }
+  // The Python reply of the request on_end() posted (status 0: `payload` is the serialized reply).
+  virtual void on_reply(int status, const std::string& msg, const std::string& payload) {}
 };
 // Builds the native stream of a call from its first request message and the caller's identity
 // (the channel-id and alluxio-user headers).  nullptr with *status == 0 hands the call to the

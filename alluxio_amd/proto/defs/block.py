@@ -22,6 +22,7 @@ msg WriteRequestCommand type=1:RequestType id=2:i64 offset=3:i64 tier=4:i32 flus
     medium_type=8:str pin_on_create=9:bool space_to_reserve=10:i64
 msg WriteRequest command=1:WriteRequestCommand|value chunk=2:Chunk|value
 msg WriteResponse offset=1:i64
+msg NativeWriteCommitRequest session_id=1:i64 block_id=2:i64 length=3:i64 pin=4:bool
 msg AsyncCacheRequest block_id=1:i64 source_host=2:str source_port=3:i32
     open_ufs_block_options=4:alluxio.proto.dataserver.OpenUfsBlockOptions length=5:i64
 msg AsyncCacheResponse
@@ -60,6 +61,7 @@ rpc BlockWorker ClearMetrics ClearMetricsRequest ClearMetricsResponse
 rpc BlockWorker OpenDeviceBlock OpenDeviceBlockRequest DeviceBlockHandle
 rpc BlockWorker UnlockDeviceBlock UnlockDeviceBlockRequest UnlockDeviceBlockResponse
 rpc BlockWorker PeerTransfer PeerTransferRequest PeerTransferResponse
+rpc BlockWorker NativeWriteCommit NativeWriteCommitRequest WriteResponse
 
 # --- block master ----------------------------------------------------------------------------
 enum BlockMasterInfoField CAPACITY_BYTES=1 CAPACITY_BYTES_ON_TIERS=2 FREE_BYTES=3

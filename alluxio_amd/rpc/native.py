@@ -95,8 +95,10 @@ STREAM_SERVICES = frozenset({"alluxio.grpc.file.FileSystemMasterClientService"})
 class _Ctx:
     """ServicerContext stand-in (the servicers only read metadata / abort)."""
 
-    def __init__(self, user):
+    def __init__(self, user, internal: bool = False):
         self._md = (("alluxio-user", user),) if user else ()
+        # posted by a native stream of this server (NativeStream::on_end), not sent by a client
+        self.internal = internal
 
     def invocation_metadata(self):
         return self._md
@@ -295,6 +297,9 @@ class NativeRpcFrontend:
                 return (token, 0, "", b"")
             path, spec, fn = self.methods[midx]
             key_user = user     # the reply cache is keyed by the connection's caller string
+            internal = bool(user) and user[0] == "\x02"
+            if internal:
+                user = user[1:]
             if user and user[0] == "\x01":
                 user = self._grpc_user(spec, user)
             elif self.rpc.authenticator is not None and not user:
@@ -315,7 +320,7 @@ class NativeRpcFrontend:
                         parts.append(b)
                     body = b"".join(parts)
                 else:
-                    body = fn(req, _Ctx(user)).SerializeToString()
+                    body = fn(req, _Ctx(user, internal)).SerializeToString()
             if cache_ep is not None and not pending:
                 self.server.cache_put(midx, key_user, payload, body, cache_ep)
             reply = (token, 0, "", body)

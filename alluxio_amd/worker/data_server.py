@@ -5,9 +5,13 @@ worker's data server, a Netty gRPC server of BlockWorkerImpl), BlockReadHandler.
 core/common/src/main/java/alluxio/grpc/ReadResponseMarshaller.java:38-80.
 
 ``ReadBlock`` of a block the store holds is answered on the C++ I/O threads (csrc/data_server.cpp:
-read lock for the call, HBM chunks DMA'd into pinned staging, ``offset_received`` window); every
-other BlockWorker call -- WriteBlock, UFS read-through, OpenLocalBlock, AsyncCache, ... -- runs the
-same Python servicer as the grpcio port, through the front end's streaming bridge.  The port is
+read lock for the call, HBM chunks DMA'd into pinned staging, ``offset_received`` window), and so
+are the chunks of an ALLUXIO_BLOCK ``WriteBlock`` (written into the temp block as they arrive; the
+commit -- CRC32C, the master's CommitBlock -- runs in Python as the internal ``NativeWriteCommit``
+call posted at the client's half-close, whose reply ends the stream; reference
+BlockWriteHandler.java).  Every other BlockWorker call -- UFS writes and read-through,
+OpenLocalBlock, AsyncCache, ... -- runs the same Python servicer as the grpcio port, through the
+front end's streaming bridge.  The port is
 advertised as ``WorkerNetAddress.dataPort``; clients stream block bytes from it
 (client/streams.py ``GrpcBlockReader.native_source``).
 """
@@ -20,6 +24,8 @@ from .services import SVC_BLOCK_WORKER
 LOG = logging.getLogger(__name__)
 
 READ_BLOCK_PATH = f"/{SVC_BLOCK_WORKER}/ReadBlock"
+WRITE_BLOCK_PATH = f"/{SVC_BLOCK_WORKER}/WriteBlock"
+COMMIT_PATH = f"/{SVC_BLOCK_WORKER}/NativeWriteCommit"
 
 
 def available() -> bool:
@@ -49,6 +55,12 @@ class WorkerDataServer:
             self.frontend.server, self.frontend.method_index(READ_BLOCK_PATH), worker.native,
             conf.get_bytes("alluxio.worker.network.reader.max.chunk.size.bytes", "2MB"),
             conf.get_bytes("alluxio.worker.network.reader.buffer.size", "4MB"))
+        # WriteBlock of ALLUXIO_BLOCK writes: chunks into the store on the I/O threads, the commit
+        # (CRC, master report) as the internal NativeWriteCommit call (BlockWorkerService)
+        lib().serve_block_writes(
+            self.frontend.server, self.frontend.method_index(WRITE_BLOCK_PATH),
+            self.frontend.method_index(COMMIT_PATH), worker.native,
+            conf.get_bytes("alluxio.worker.network.writer.staging.size", "4MB"), self.stats)
         self.port = None
 
     def start(self) -> int:
@@ -62,6 +74,8 @@ class WorkerDataServer:
         m.counter("BytesReadAlluxio").add_source(lambda: st.bytes)
         m.counter("BytesReadDomain").add_source(lambda: st.domain_bytes)
         m.counter("BytesReadRemote").add_source(lambda: st.bytes - st.domain_bytes)
+        m.counter("BytesWrittenAlluxio").add_source(lambda: st.write_bytes)
+        m.gauge("DataServerNativeWriteStreams", lambda: st.write_streams)
         return self.port
 
     def stop(self) -> None:

@@ -183,6 +183,16 @@ class BlockWorkerService:
             yield marshal.read_response_frame(data)
 
     # ------------------------------------------------------------------------------------------
+    def NativeWriteCommit(self, req, ctx):
+        """Commit of a WriteBlock whose chunks the native data server wrote (csrc/data_server.cpp
+        BlockWriteStream): CRC32C and the master's CommitBlock, as WriteBlock's end does.  Only the
+        server itself posts it; a client calling it is refused."""
+        if not getattr(ctx, "internal", False):
+            from ..utils.exceptions import PermissionDeniedException
+            raise PermissionDeniedException("NativeWriteCommit is internal to the worker's data server")
+        self.w.commit_block(req.session_id, req.block_id, req.pin)
+        return pb.block.WriteResponse(offset=req.length)
+
     def WriteBlock(self, request_iter, ctx):
         it = iter(request_iter)
         first = next(it, None)

@@ -132,8 +132,9 @@ def test_stock_grpc_client_on_data_port_flow_control(tmp_path):
             fs.close()
 
 
-def test_write_block_bridged_then_native_read(tmp_path):
-    """WriteBlock (client streaming) through the bridge on the data port, read back natively."""
+def test_stock_grpc_write_block_then_native_read(tmp_path):
+    """A stock gRPC client's WriteBlock on the data port (chunks written into the block by the C++
+    server, commit through the internal NativeWriteCommit call), read back natively."""
     with _cluster(tmp_path) as c:
         fs = c.client()
         rfs = _remote_fs(c)
@@ -152,6 +153,7 @@ def test_write_block_bridged_then_native_read(tmp_path):
             assert resps[-1].offset == len(payload)
             ch.close()
             assert w.worker.has_block(bid)
+            assert w.data_server.stats.write_streams >= 1 and w.data_server.stats.write_bytes >= len(payload)
             src = lib().GrpcBlockSource("127.0.0.1", w.data_server.port, bid, len(payload), 1 << 20)
             out = np.empty(len(payload), dtype=np.uint8)
             src.read_into(0, len(payload), out.ctypes.data)
@@ -274,3 +276,64 @@ def test_in_process_host_reads_use_store_source(tmp_path):
             assert f.read() == data.tobytes() and f._nat.prefetch_hits == 0
         nfs.close()
         fs.close()
+
+
+def test_native_writer_over_data_port(tmp_path):
+    """FileOutStream to a remote worker: every block goes through the native client
+    (GrpcBlockSink) and the native WriteBlock server; the master sees the committed blocks."""
+    with _cluster(tmp_path) as c:
+        w = c.workers[0]
+        rfs = _remote_fs(c, **{"alluxio.user.block.size.bytes.default": "4MB"})
+        try:
+            st0 = (w.data_server.stats.write_streams, w.data_server.stats.write_bytes)
+            data = np.random.default_rng(7).integers(0, 256, (13 << 20) + 5, dtype=np.uint8)
+            with rfs.create_file("/nw", write_type="MUST_CACHE") as f:
+                for i in range(0, len(data), 3 << 20):           # writes that straddle blocks
+                    f.write(data[i:i + (3 << 20)])
+            blocks = _blocks(rfs, "/nw")
+            assert len(blocks) == 4
+            assert w.data_server.stats.write_streams - st0[0] == 4
+            assert w.data_server.stats.write_bytes - st0[1] == len(data)
+            assert rfs.get_status("/nw").in_alluxio_percentage == 100
+            assert all(w.worker.has_block(b) for b, _ in blocks)
+            assert rfs.read_file("/nw") == data.tobytes()
+            # CRC recorded at commit, as for any committed block
+            assert all(b in w.worker.crc for b, _ in blocks) or not w.worker.crc_enabled
+        finally:
+            rfs.close()
+
+
+def test_native_write_errors_and_cancel(tmp_path):
+    with _cluster(tmp_path) as c:
+        w = c.workers[0]
+        port = w.data_server.port
+        C = lib()
+        data = np.random.default_rng(8).integers(0, 256, 2 << 20, dtype=np.uint8)
+        s = C.GrpcBlockSink("127.0.0.1", port, 4242)
+        s.write_ptr(data.ctypes.data, data.nbytes)
+        assert s.commit() == data.nbytes
+        assert w.worker.has_block(4242)
+        # the same block again: ALREADY_EXISTS from the native server
+        with pytest.raises(C.StoreError) as ei:
+            s2 = C.GrpcBlockSink("127.0.0.1", port, 4242)
+            s2.write_ptr(data.ctypes.data, data.nbytes)
+            s2.commit()
+        assert ei.value.args[0] == 2
+        # cancelled mid-block: the temp block and its space go away
+        free0 = w.worker.native.dir_available(0)
+        s3 = C.GrpcBlockSink("127.0.0.1", port, 4343, reserve=4 << 20)
+        s3.write_ptr(data.ctypes.data, data.nbytes)
+        s3.cancel()
+        deadline = time.time() + 5
+        while w.worker.native.has_temp_block(4343) or w.worker.native.dir_available(0) != free0:
+            assert time.time() < deadline
+            time.sleep(0.05)
+        assert not w.worker.has_block(4343)
+        # the commit call is internal to the server: a client calling it is refused
+        ch = grpc.insecure_channel(f"127.0.0.1:{port}")
+        spec = SERVICES[BW]["NativeWriteCommit"]
+        call = ch.unary_unary(spec.path, spec.request.SerializeToString, spec.response.FromString)
+        with pytest.raises(grpc.RpcError) as ge:
+            call(pb.block.NativeWriteCommitRequest(session_id=1, block_id=4242, length=1))
+        assert ge.value.code() == grpc.StatusCode.PERMISSION_DENIED
+        ch.close()

@@ -82,8 +82,9 @@ def test_grpc_block_streams(tmp_path, monkeypatch, zero_copy):
             "alluxio.user.streaming.zerocopy.enabled": str(zero_copy).lower(),
             "alluxio.user.network.inprocess.transport.enabled": "false",
             "alluxio.user.short.circuit.enabled": "false",
-            # the grpcio client path (the native reader decodes frames in C++: test_data_server.py)
-            "alluxio.user.native.reader.enabled": "false"}
+            # the grpcio client path (the native reader / writer frame in C++: test_data_server.py)
+            "alluxio.user.native.reader.enabled": "false",
+            "alluxio.user.native.writer.enabled": "false"}
     with LocalAlluxioCluster(num_workers=1, conf=conf, grpc=True, work_dir=str(tmp_path)) as cluster:
         fs = cluster.client()
         data = np.random.default_rng(1).integers(0, 256, (7 << 20) + 5, dtype=np.uint8)

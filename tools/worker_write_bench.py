@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Host writers into a worker's cache tier from a SEPARATE client process (StressWorkerBench's
+write counterpart; reference ``GrpcDataWriter`` -> ``BlockWriteHandler``).
+
+A master + one worker (HBM tier when a GPU is visible, else DRAM) run in this process; a client
+process runs T threads, each writing ``--files`` files of ``--file-size`` with MUST_CACHE from host
+memory, ``--write-size`` bytes per ``write()``.  With in-process transport and short-circuit off,
+every block streams to the worker's data port as gRPC ``WriteBlock``.  Reports GB/s per thread count.
+
+    python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --out gpurun_out/ww.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CLIENT = r"""
+import json, sys, threading, time
+sys.path.insert(0, {root!r})
+import numpy as np
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.conf import Configuration
+conf = Configuration({props!r})
+fs = FileSystem(conf=conf, master_address={addr!r})
+size, nfiles, threads, wsize, tag = {size}, {nfiles}, {threads}, {wsize}, {tag!r}
+data = np.random.default_rng(1).integers(0, 256, wsize, dtype=np.uint8)
+fs.create_directory("/ww", recursive=True, allow_exists=True)
+with fs.create_file(f"/ww/{{tag}}-warm", write_type="MUST_CACHE") as f:
+    f.write(data)
+done = [0] * threads
+errs = []
+def run(t):
+    try:
+        for k in range(nfiles):
+            with fs.create_file(f"/ww/{{tag}}-{{t}}-{{k}}", write_type="MUST_CACHE") as f:
+                left = size
+                while left > 0:
+                    n = min(wsize, left)
+                    f.write(data[:n])
+                    left -= n
+                    done[t] += n
+    except Exception as e:
+        errs.append(repr(e))
+ts = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+t0 = time.perf_counter()
+for t in ts: t.start()
+for t in ts: t.join()
+el = time.perf_counter() - t0
+print("RESULT " + json.dumps({{"bytes": sum(done), "seconds": el, "errors": errs[:3]}}), flush=True)
+fs.close()
+"""
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", default="1,4,16")
+    ap.add_argument("--files", type=int, default=2, help="files per thread")
+    ap.add_argument("--file-size", default="256m")
+    ap.add_argument("--write-size", default="1m")
+    ap.add_argument("--block-size", default="64m")
+    ap.add_argument("--tier", default=None, help="worker MEM tier (default hbm:0 with a GPU, else dram)")
+    ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    import torch
+
+    from alluxio_amd.minicluster import LocalAlluxioCluster
+    from alluxio_amd.utils.format import parse_space_size
+    tier = a.tier or ("hbm:0" if torch.cuda.is_available() else "dram")
+    size = parse_space_size(a.file_size)
+    total = max(int(t) for t in a.threads.split(",")) * a.files * size
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": tier,
+            "alluxio.worker.tieredstore.level0.dirs.quota": str(total + (1 << 30)),
+            "alluxio.worker.hbm.page.size": "2MB",
+            "alluxio.user.block.size.bytes.default": a.block_size,
+            "alluxio.security.authorization.permission.enabled": "false",
+            "alluxio.worker.tieredstore.dram.prefault": "true"}
+    work = tempfile.mkdtemp(prefix="wwbench_")
+    with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=work) as c:
+        time.sleep(min(10.0, total / 4e9))     # let the DRAM prefault finish (no-op on HBM)
+        props = {"alluxio.user.network.inprocess.transport.enabled": "false",
+                 "alluxio.user.short.circuit.enabled": "false",
+                 "alluxio.user.block.size.bytes.default": a.block_size}
+        props.update(dict(kv.split("=", 1) for kv in a.client_prop))
+        for i, t in enumerate(a.threads.split(",")):
+            p = subprocess.run([sys.executable, "-c", CLIENT.format(
+                root=ROOT, props=props, addr=c.master.address, size=size, nfiles=a.files, threads=int(t),
+                wsize=parse_space_size(a.write_size), tag=f"r{i}")], capture_output=True, text=True, timeout=900)
+            line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
+            if line is None:
+                print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
+                return 1
+            r = json.loads(line[7:])
+            row = {"bench": "host writers, separate client process (gRPC WriteBlock, MUST_CACHE)", "tier": tier,
+                   "threads": int(t), "files_per_thread": a.files, "file_size": a.file_size,
+                   "write_size": a.write_size, "bytes": r["bytes"], "seconds": round(r["seconds"], 3),
+                   "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3), "errors": r["errors"],
+                   "client_props": a.client_prop}
+            print(json.dumps(row), flush=True)
+            if a.out:
+                with open(a.out, "a") as f:
+                    f.write(json.dumps(row) + "\n")
+            # free the cache for the next thread count
+            fs = c.client()
+            for st in fs.list_status("/ww"):
+                fs.delete(st.path)
+            fs.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
