@@ -678,6 +678,66 @@ class LocalUfsFallbackWriter(BlockWriter):
         self._w.cancel()
 
 
+class IpcBlockWriter(BlockWriter):
+    """Short-circuit write into a same-node worker process (the analogue of the reference's
+    LocalFileDataWriter over CreateLocalBlock): the worker creates the temp block with its pages
+    reserved (``OpenDeviceWrite``), this process maps the arena -- HBM through HIP IPC, DRAM through
+    the memfd -- and copies into the pages itself (csrc/block_source.cpp ``ArenaSink``: pinned
+    staging + H2D DMA), then ``CommitDeviceWrite`` records the length and commits."""
+
+    def __init__(self, ctx, address, block_id, capacity, tier=0, medium="", pin=False):
+        from ..ops.native import has_gpu, lib
+        from ..parallel.ipc import map_handle
+        self.ctx = ctx
+        self.block_id = block_id
+        self.pin = pin
+        self.stub = ctx.worker_stub(address)
+        self.h = self.stub.OpenDeviceWrite(pb.block.OpenDeviceWriteRequest(
+            block_id=block_id, length=capacity, tier=tier, medium_type=medium, pin_on_create=pin))
+        self.session = self.h.lock_id
+        try:
+            if self.h.arena_kind != "dram" and not has_gpu():
+                raise UnavailableException("HBM arena needs a visible GPU")
+            import torch
+            self.device = torch.cuda.current_device() if has_gpu() else 0
+            base = map_handle(self.h, self.device)
+            self.sink = lib().ArenaSink(base, list(self.h.pages), self.h.page_size, self.h.length, self.device,
+                                        self.h.arena_kind == "dram")
+        except Exception:
+            self.cancel()
+            raise
+
+    def write_ptr(self, offset, ptr, length, kind):
+        from ..ops.native import native_errors
+        keep = None
+        if kind == DEVICE:
+            import torch
+            from ..ops.native import lib
+            tmp = torch.empty(length, dtype=torch.uint8, device="cuda")
+            lib().batched_copy([(ptr, tmp.data_ptr(), length)], 0)
+            keep = tmp.cpu()
+            ptr = keep.data_ptr()
+        with native_errors():
+            self.sink.write_ptr(offset, ptr, length)
+
+    def commit(self):
+        if self.h is None:
+            return
+        h, self.h = self.h, None
+        self.stub.CommitDeviceWrite(pb.block.CommitDeviceWriteRequest(
+            block_id=self.block_id, session_id=self.session, length=self.sink.length, pin_on_create=self.pin))
+
+    def cancel(self):
+        if self.h is None:
+            return
+        self.h = None
+        try:
+            self.stub.CommitDeviceWrite(pb.block.CommitDeviceWriteRequest(
+                block_id=self.block_id, session_id=self.session, abort=True))
+        except Exception:  # noqa: BLE001 - the session expires on the worker
+            LOG.debug("abort of short-circuit write of block %d failed", self.block_id, exc_info=True)
+
+
 class GrpcBlockWriter(BlockWriter):
     """WriteBlock stream (GrpcDataWriter): command, chunks, then half-close -> commit."""
 
@@ -984,6 +1044,16 @@ class FileOutStream(io.RawIOBase):
             elif lw is not None:
                 self._writers.append(LocalBlockWriter(lw, bid, self.session, self.write_tier, self.medium,
                                                       max(1, reserve)))
+            elif self._ipc_write(w) and not ufs_tier:
+                addr = worker_address_str(w.address)
+                try:
+                    self._writers.append(IpcBlockWriter(self.ctx, addr, bid, self.block_size, self.write_tier,
+                                                        self.medium))
+                except Exception:  # noqa: BLE001 - no shared arena (file tier, no GPU): the data port
+                    LOG.debug("short-circuit write to %s unavailable", addr, exc_info=True)
+                    self._writers.append(GrpcBlockWriter(self.ctx, addr, bid, self.write_tier, self.medium, reserve,
+                                                         data_address=(w.address.host,
+                                                                       w.address.dataPort or w.address.rpcPort)))
             else:
                 self._writers.append(GrpcBlockWriter(self.ctx, worker_address_str(w.address), bid,
                                                      self.write_tier, self.medium, reserve,
@@ -991,6 +1061,13 @@ class FileOutStream(io.RawIOBase):
                                                      data_address=(w.address.host,
                                                                    w.address.dataPort or w.address.rpcPort)))
         self._block_written = 0
+
+    def _ipc_write(self, w) -> bool:
+        """Short-circuit (shared-arena) writes to a same-node worker in another process."""
+        conf = self.ctx.conf
+        return conf.get_bool("alluxio.user.short.circuit.enabled", "true") and \
+            conf.get_bool("alluxio.user.short.circuit.write.enabled", "true") and \
+            conf.get_bool("alluxio.worker.ipc.enabled", "true") and self.ctx.is_local(w.address)
 
     def _finish_block(self) -> None:
         for w in self._writers:

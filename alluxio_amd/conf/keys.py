@@ -217,6 +217,10 @@ _k("USER_NATIVE_READER_ENABLED", "alluxio.user.native.reader.enabled", "true", S
    "Host reads of FileInStream go through the native chunk-buffered reader (csrc/block_source.cpp): a "
    "read(buf) inside the buffered chunk is a memcpy; refills come from HIP-IPC HBM (D2H DMA), shared "
    "DRAM, the in-process store or a native gRPC ReadBlock stream.")
+_k("USER_SHORT_CIRCUIT_WRITE_ENABLED", "alluxio.user.short.circuit.write.enabled", "true", Scope.CLIENT,
+   "Blocks written to a same-node worker in another process go into its shared arena directly "
+   "(OpenDeviceWrite: HBM pages mapped through HIP IPC, DRAM through its memfd) instead of over "
+   "WriteBlock; needs alluxio.user.short.circuit.enabled.")
 _k("USER_NATIVE_WRITER_ENABLED", "alluxio.user.native.writer.enabled", "true", Scope.CLIENT,
    "Block writes to a remote (other-process) worker use the native gRPC client (csrc/block_source.cpp "
    "GrpcBlockSink: WriteBlock over HTTP/2 with the chunks framed around the caller's bytes, GIL "

@@ -161,6 +161,62 @@ void DeviceArenaSource::read(uint64_t off, uint64_t n, uint8_t* dst) {
   wait_stream(st);
 }
 
+// ---- ArenaSink ----------------------------------------------------------------------------------
+ArenaSink::ArenaSink(uint64_t base, std::vector<int64_t> pages, uint64_t page_size, uint64_t capacity, int device,
+                     bool host_arena)
+    : base_(base), pages_(std::move(pages)), page_size_(page_size), capacity_(capacity), device_(device),
+      host_(host_arena) {
+  if (page_size_ == 0) throw StoreError(kErrInvalidArgument, "page size must be > 0");
+  if (capacity_ > (uint64_t)pages_.size() * page_size_)
+    throw StoreError(kErrInvalidArgument, "write capacity beyond the block's pages");
+  if (!host_) {
+    for (int i = 0; i < 2; ++i) {
+      stage_[i] = host_buffer_alloc(kStage, &pinned_[i]);
+      if (hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
+        throw StoreError(kErrHip, "hipEventCreate failed");
+    }
+  }
+}
+
+ArenaSink::~ArenaSink() {
+  for (int i = 0; i < 2; ++i) {
+    if (ev_[i]) {
+      (void)hipEventSynchronize(ev_[i]);
+      (void)hipEventDestroy(ev_[i]);
+    }
+    if (stage_[i]) host_buffer_release(stage_[i], kStage, pinned_[i]);
+  }
+}
+
+void ArenaSink::write(uint64_t off, const uint8_t* src, uint64_t n) {
+  if (off + n > capacity_) throw StoreError(kErrOutOfSpace, "write beyond the reserved block");
+  if (host_) {
+    for_page_runs(base_, pages_, page_size_, off, n, [&](uint64_t dst, uint64_t at, uint64_t take) {
+      std::memcpy(reinterpret_cast<void*>(dst), src + at, take);
+    });
+  } else {
+    hipStream_t st = reader_stream(device_);
+    uint64_t done = 0;
+    int k = 0;
+    while (done < n) {
+      const uint64_t take = std::min<uint64_t>(kStage, n - done);
+      // the buffer's previous DMA must be done before it is overwritten
+      if (hipEventSynchronize(ev_[k]) != hipSuccess) throw StoreError(kErrHip, "hipEventSynchronize failed");
+      std::memcpy(stage_[k], src + done, take);
+      const uint8_t* sp = stage_[k];
+      for_page_runs(base_, pages_, page_size_, off + done, take, [&](uint64_t dst, uint64_t at, uint64_t t) {
+        const hipError_t e = hipMemcpyAsync(reinterpret_cast<void*>(dst), sp + at, t, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) throw StoreError(kErrHip, std::string("hipMemcpyAsync H2D: ") + hipGetErrorString(e));
+      });
+      if (hipEventRecord(ev_[k], st) != hipSuccess) throw StoreError(kErrHip, "hipEventRecord failed");
+      done += take;
+      k ^= 1;
+    }
+    wait_stream(st);
+  }
+  length_ = std::max(length_, off + n);
+}
+
 // ---- HostArenaSource --------------------------------------------------------------------------
 HostArenaSource::HostArenaSource(uint64_t base, std::vector<int64_t> pages, uint64_t page_size, uint64_t length)
     : BlockSource(length), base_(base), pages_(std::move(pages)), page_size_(page_size) {

@@ -117,6 +117,30 @@ class GrpcBlockSource : public BlockSource {
   std::unique_ptr<Conn> c_;
 };
 
+// Writes into the pages of a temp block of a same-node worker's arena mapped into this process
+// (short-circuit write; worker OpenDeviceWrite / CommitDeviceWrite).  HBM: the caller's bytes are
+// copied into two alternating pinned staging buffers and DMA'd H2D page run by page run, the
+// memcpy of piece i+1 overlapping the DMA of piece i; shared DRAM: memcpy into the pages.
+class ArenaSink {
+ public:
+  ArenaSink(uint64_t base, std::vector<int64_t> pages, uint64_t page_size, uint64_t capacity, int device, bool host_arena);
+  ~ArenaSink();
+  void write(uint64_t off, const uint8_t* src, uint64_t n);
+  uint64_t length() const { return length_; }    // end of the furthest byte written
+
+ private:
+  uint64_t base_;
+  std::vector<int64_t> pages_;
+  uint64_t page_size_, capacity_;
+  int device_;
+  bool host_;
+  uint64_t length_ = 0;
+  static constexpr uint64_t kStage = 4u << 20;
+  uint8_t* stage_[2] = {nullptr, nullptr};
+  bool pinned_[2] = {false, false};
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+};
+
 // A block written to a worker's data port: WriteBlock over HTTP/2 spoken directly with libnghttp2
 // (command, then WriteRequest{chunk} messages framed around the caller's bytes -- copied once, into
 // the HTTP/2 frames --, half-close, final WriteResponse).  The native data server writes the

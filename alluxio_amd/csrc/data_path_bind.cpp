@@ -225,6 +225,14 @@ void bind_data_path(py::module_& m) {
            py::arg("host"), py::arg("port"), py::arg("block_id"), py::arg("length"), py::arg("chunk") = 1u << 20,
            py::arg("ufs_options") = py::bytes(), py::arg("promote") = false, py::arg("channel_id") = "",
            py::arg("user") = "", py::arg("timeout_ms") = 60000, py::arg("unix_path") = "");
+  py::class_<ArenaSink, std::shared_ptr<ArenaSink>>(m, "ArenaSink")
+      .def(py::init<uint64_t, std::vector<int64_t>, uint64_t, uint64_t, int, bool>(), py::arg("base"),
+           py::arg("pages"), py::arg("page_size"), py::arg("capacity"), py::arg("device"), py::arg("host_arena"))
+      .def("write_ptr", [](ArenaSink& s, uint64_t off, uint64_t ptr, uint64_t n) {
+             py::gil_scoped_release rel;
+             s.write(off, reinterpret_cast<const uint8_t*>(ptr), n);
+           }, py::arg("offset"), py::arg("ptr"), py::arg("n"))
+      .def_property_readonly("length", &ArenaSink::length);
   py::class_<GrpcBlockSink, std::shared_ptr<GrpcBlockSink>>(m, "GrpcBlockSink")
       .def(py::init([](const std::string& host, int port, int64_t block_id, int tier, const std::string& medium,
                        uint64_t reserve, bool pin, uint64_t chunk, const std::string& channel_id,

@@ -46,6 +46,10 @@ msg DeviceBlockHandle block_id=1:i64 length=2:i64 page_size=3:i64 pages=4:i64*
 msg OpenDeviceBlockRequest block_id=1:i64 promote=2:bool session_id=3:i64 reader_gpu=4:i32
 msg UnlockDeviceBlockRequest block_id=1:i64 lock_id=2:i64 session_id=3:i64
 msg UnlockDeviceBlockResponse
+msg OpenDeviceWriteRequest block_id=1:i64 length=2:i64 tier=3:i32 medium_type=4:str pin_on_create=5:bool
+    session_id=6:i64
+msg CommitDeviceWriteRequest block_id=1:i64 session_id=2:i64 length=3:i64 pin_on_create=4:bool abort=5:bool
+msg CommitDeviceWriteResponse
 msg PeerTransferRequest block_id=1:i64 src_rank=2:i32 dst_rank=3:i32 offset=4:i64 length=5:i64
     tag=6:i64 src_address=7:str
 msg PeerTransferResponse ok=1:bool message=2:str
@@ -62,6 +66,8 @@ rpc BlockWorker OpenDeviceBlock OpenDeviceBlockRequest DeviceBlockHandle
 rpc BlockWorker UnlockDeviceBlock UnlockDeviceBlockRequest UnlockDeviceBlockResponse
 rpc BlockWorker PeerTransfer PeerTransferRequest PeerTransferResponse
 rpc BlockWorker NativeWriteCommit NativeWriteCommitRequest WriteResponse
+rpc BlockWorker OpenDeviceWrite OpenDeviceWriteRequest DeviceBlockHandle
+rpc BlockWorker CommitDeviceWrite CommitDeviceWriteRequest CommitDeviceWriteResponse
 
 # --- block master ----------------------------------------------------------------------------
 enum BlockMasterInfoField CAPACITY_BYTES=1 CAPACITY_BYTES_ON_TIERS=2 FREE_BYTES=3

@@ -18,6 +18,7 @@ import os
 import threading
 import time
 
+from ..ops.native import native_errors
 from ..proto import enum_name, pb
 from ..rpc import marshal
 from ..utils import ids
@@ -394,6 +395,53 @@ class BlockWorkerService:
         except Exception:
             self.w.unlock(lock_id)
             raise
+
+    def OpenDeviceWrite(self, req, ctx):
+        """Short-circuit write for a same-node writer process (the analogue of CreateLocalBlock,
+        whose writer fills a temp block file): create the temp block with ``length`` bytes of
+        pages reserved and describe them like :meth:`OpenDeviceBlock`; the writer maps the arena
+        and copies into the pages itself, then calls :meth:`CommitDeviceWrite`.  An abandoned
+        write is reclaimed with its session (``alluxio.worker.session.timeout``)."""
+        session = req.session_id or ids.create_session_id()
+        length = max(int(req.length), 1)
+        self.w.create_block(session, req.block_id, req.tier if not req.medium_type else -1, req.medium_type,
+                            length, req.pin_on_create)
+        try:
+            pages, d, ps, _base = self.w.native.block_pages(req.block_id)
+            arena = self.w.store.arena_for_dir(d)
+            if arena is None:
+                raise UnavailableException("block is in a file tier: no shared memory view")
+            h = pb.block.DeviceBlockHandle(block_id=req.block_id, length=length, page_size=ps, pages=pages,
+                                           arena_bytes=arena.nbytes, device=arena.device, lock_id=session,
+                                           pid=os.getpid(), arena_kind=arena.kind, host_fd=-1)
+            if arena.kind == "hbm":
+                h.arena_ipc_handle, h.arena_offset = arena.ipc_handle()
+            else:
+                share = arena.share_handle()
+                if share is None:
+                    raise UnavailableException("DRAM arena is not shareable")
+                h.host_fd = share[1]
+            return h
+        except Exception:
+            self.w.abort_block(session, req.block_id)
+            self.w.cleanup_session(session)
+            raise
+
+    def CommitDeviceWrite(self, req, ctx):
+        """End of a short-circuit write: record the written length and commit (CRC, master
+        report), or abort."""
+        try:
+            if req.abort:
+                self.w.abort_block(req.session_id, req.block_id)
+            else:
+                with native_errors():
+                    self.w.native.external_write(req.session_id, req.block_id, 0, req.length)
+                self.w.commit_block(req.session_id, req.block_id, req.pin_on_create)
+                self.w.metrics.counter("BytesWrittenAlluxio").inc(req.length)
+                self.w.metrics.counter("BytesWrittenDomain").inc(req.length)
+        finally:
+            self.w.cleanup_session(req.session_id)
+        return pb.block.CommitDeviceWriteResponse()
 
     def UnlockDeviceBlock(self, req, ctx):
         with self._lock:

@@ -337,3 +337,38 @@ def test_native_write_errors_and_cancel(tmp_path):
             call(pb.block.NativeWriteCommitRequest(session_id=1, block_id=4242, length=1))
         assert ge.value.code() == grpc.StatusCode.PERMISSION_DENIED
         ch.close()
+
+
+def test_short_circuit_write_into_shared_arena(tmp_path):
+    """A same-node writer in another process (here: a client with in-process transport off)
+    writes into the worker's shared DRAM arena directly (OpenDeviceWrite -> ArenaSink ->
+    CommitDeviceWrite); the last block's over-reserved pages are returned at commit."""
+    with _cluster(tmp_path) as c:
+        w = c.workers[0]
+        rfs = _remote_fs(c, **{"alluxio.user.short.circuit.enabled": "true",
+                               "alluxio.user.block.size.bytes.default": "4MB"})
+        try:
+            free0 = w.worker.native.dir_available(0)
+            ws0 = w.data_server.stats.write_streams
+            data = np.random.default_rng(9).integers(0, 256, (9 << 20) + 77, dtype=np.uint8)
+            with rfs.create_file("/sc", write_type="MUST_CACHE") as f:
+                for i in range(0, len(data), 1 << 20):
+                    f.write(data[i:i + (1 << 20)])
+            blocks = _blocks(rfs, "/sc")
+            assert [n for _, n in blocks] == [4 << 20, 4 << 20, (1 << 20) + 77]
+            assert w.data_server.stats.write_streams == ws0        # nothing went over WriteBlock
+            assert rfs.get_status("/sc").in_alluxio_percentage == 100
+            assert rfs.read_file("/sc") == data.tobytes()
+            page = 1 << 20
+            used = sum(-(-n // page) * page for _, n in blocks)
+            assert free0 - w.worker.native.dir_available(0) == used
+            # an aborted short-circuit write leaves nothing behind
+            from alluxio_amd.client.streams import IpcBlockWriter
+            from alluxio_amd.client.context import worker_address_str
+            wr = IpcBlockWriter(rfs.ctx, worker_address_str(w.worker.address), 999_999, 4 << 20)
+            wr.write_ptr(0, data.ctypes.data, 1 << 20, 0)
+            wr.cancel()
+            assert not w.worker.native.has_temp_block(999_999) and not w.worker.has_block(999_999)
+            assert free0 - w.worker.native.dir_available(0) == used
+        finally:
+            rfs.close()

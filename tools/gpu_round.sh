@@ -132,7 +132,7 @@ for s in $STEPS; do
       ;;
     writes)
       run pytest_dataserver 300 python -u -m pytest tests/test_data_server.py tests/test_ipc_gpu.py -x -v --timeout 120 --timeout-method thread
-      run worker_write_bench 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --out "$OUT/worker_write_bench.jsonl"
+      run worker_write_bench 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --transports grpc,ipc --out "$OUT/worker_write_bench.jsonl"
       run wb_host_after_writes 600 python tools/worker_bench_host.py --threads 16,256 --transports grpc,ipc --duration 6s --warmup 2s --out "$OUT/worker_bench_host_r4b.jsonl"
       ;;
     hostsweep)

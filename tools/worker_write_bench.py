@@ -67,6 +67,8 @@ def main(argv=None) -> int:
     ap.add_argument("--write-size", default="1m")
     ap.add_argument("--block-size", default="64m")
     ap.add_argument("--tier", default=None, help="worker MEM tier (default hbm:0 with a GPU, else dram)")
+    ap.add_argument("--transports", default="grpc", help="grpc (WriteBlock on the data port) and/or ipc "
+                    "(short-circuit: the worker's arena mapped into the writer, OpenDeviceWrite)")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
@@ -86,11 +88,12 @@ def main(argv=None) -> int:
     work = tempfile.mkdtemp(prefix="wwbench_")
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=work) as c:
         time.sleep(min(10.0, total / 4e9))     # let the DRAM prefault finish (no-op on HBM)
-        props = {"alluxio.user.network.inprocess.transport.enabled": "false",
-                 "alluxio.user.short.circuit.enabled": "false",
-                 "alluxio.user.block.size.bytes.default": a.block_size}
-        props.update(dict(kv.split("=", 1) for kv in a.client_prop))
-        for i, t in enumerate(a.threads.split(",")):
+        runs = [(tr, t) for tr in a.transports.split(",") for t in a.threads.split(",")]
+        for i, (transport, t) in enumerate(runs):
+            props = {"alluxio.user.network.inprocess.transport.enabled": "false",
+                     "alluxio.user.short.circuit.enabled": "true" if transport == "ipc" else "false",
+                     "alluxio.user.block.size.bytes.default": a.block_size}
+            props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             p = subprocess.run([sys.executable, "-c", CLIENT.format(
                 root=ROOT, props=props, addr=c.master.address, size=size, nfiles=a.files, threads=int(t),
                 wsize=parse_space_size(a.write_size), tag=f"r{i}")], capture_output=True, text=True, timeout=900)
@@ -99,7 +102,7 @@ def main(argv=None) -> int:
                 print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
                 return 1
             r = json.loads(line[7:])
-            row = {"bench": "host writers, separate client process (gRPC WriteBlock, MUST_CACHE)", "tier": tier,
+            row = {"bench": "host writers, separate client process (MUST_CACHE)", "transport": transport, "tier": tier,
                    "threads": int(t), "files_per_thread": a.files, "file_size": a.file_size,
                    "write_size": a.write_size, "bytes": r["bytes"], "seconds": round(r["seconds"], 3),
                    "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3), "errors": r["errors"],
