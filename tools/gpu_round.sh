@@ -135,6 +135,9 @@ for s in $STEPS; do
       run worker_write_bench 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --transports grpc,ipc --out "$OUT/worker_write_bench.jsonl"
       run wb_host_after_writes 600 python tools/worker_bench_host.py --threads 16,256 --transports grpc,ipc --duration 6s --warmup 2s --out "$OUT/worker_bench_host_r4b.jsonl"
       ;;
+    writebase)
+      run worker_write_bench_grpcio 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --transports grpc --client-prop alluxio.user.native.writer.enabled=false --out "$OUT/worker_write_bench_grpcio.jsonl"
+      ;;
     hostsweep)
       for rb in 256KB 512KB 1MB; do
         for pf in false true; do
