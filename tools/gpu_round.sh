@@ -138,6 +138,10 @@ for s in $STEPS; do
     writebase)
       run worker_write_bench_grpcio 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --transports grpc --client-prop alluxio.user.native.writer.enabled=false --out "$OUT/worker_write_bench_grpcio.jsonl"
       ;;
+    rehearse)
+      run bench_rehearse_2rank 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --one-device --steps 10 --warmup 3
+      run bench_rehearse_4rank 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 4 --one-device --steps 10 --warmup 3
+      ;;
     hostsweep)
       for rb in 256KB 512KB 1MB; do
         for pf in false true; do
