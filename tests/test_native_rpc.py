@@ -214,3 +214,27 @@ def test_deferred_flush_context_collects_counters():
     w.flush_async(2, lambda e: ev.set())
     assert ev.wait(5)
     w.close()
+
+
+def test_control_char_user_names_are_refused(master):
+    """"\x01..." / "\x02..." caller strings mark gRPC-connection and internal native-stream
+    requests inside the server: a framed-RPC client may not authenticate under such a name."""
+    from alluxio_amd.ops.native import lib
+    m, _ = master
+    path = f"/{FS}/GetStatus"
+    req = pb.file.GetStatusPRequest(path="/").SerializeToString()
+    for name in ("\x02internal", "\x01cid"):
+        c = lib().FrameRpcClient("127.0.0.1", m.native_rpc.port, f"SIMPLE\0{name}\0".encode(), 5000)
+        try:
+            with pytest.raises(Exception):
+                status, msg, _ = c.call(path, req, 5000)
+                if status:
+                    raise RuntimeError(msg)
+        finally:
+            c.close()
+    ok = lib().FrameRpcClient("127.0.0.1", m.native_rpc.port, b"SIMPLE\0alice\0", 5000)
+    try:
+        status, _, _ = ok.call(path, req, 5000)
+        assert status == 0
+    finally:
+        ok.close()
