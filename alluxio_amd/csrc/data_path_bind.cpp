@@ -412,5 +412,32 @@ void bind_data_path(py::module_& m) {
       .def("drain", &DnPacketReader::drain, G())
       .def_property_readonly("done", &DnPacketReader::done)
       .def_property_readonly("packets", &DnPacketReader::packets);
+  py::class_<DnPacketWriter>(m, "DnPacketWriter")
+      .def(py::init<int, uint32_t, uint32_t, uint32_t, int>(), py::arg("fd"), py::arg("bytes_per_checksum") = 512,
+           py::arg("packet_bytes") = 64u << 10, py::arg("max_in_flight") = 80, py::arg("timeout_ms") = 60000)
+      .def("write", [](DnPacketWriter& w, py::buffer b) {
+             py::buffer_info bi = b.request();
+             const uint64_t n = (uint64_t)(bi.size * bi.itemsize);
+             py::gil_scoped_release rel;
+             w.write(static_cast<const uint8_t*>(bi.ptr), n);
+           }, py::arg("data"))
+      .def("finish", &DnPacketWriter::finish, G())
+      .def_property_readonly("offset", &DnPacketWriter::offset);
+  py::class_<DnPacketReceiver>(m, "DnPacketReceiver")
+      .def(py::init<int, uint32_t, int>(), py::arg("fd"), py::arg("bytes_per_checksum") = 512,
+           py::arg("timeout_ms") = 60000)
+      .def("receive", [](DnPacketReceiver& r, py::buffer b, uint64_t batch) {
+             py::buffer_info bi = b.request(true);
+             bool last = false;
+             int status = 0;
+             uint64_t n;
+             {
+               py::gil_scoped_release rel;
+               n = r.receive(static_cast<uint8_t*>(bi.ptr), (uint64_t)(bi.size * bi.itemsize), batch, &last, &status);
+             }
+             return py::make_tuple(n, last, status);
+           }, py::arg("buffer"), py::arg("batch"))
+      .def("ack", &DnPacketReceiver::ack, G(), py::arg("status"))
+      .def_property_readonly("received", &DnPacketReceiver::received);
   m.def("listen_unix", [](FrameRpcServer& srv, const std::string& path) { srv.listen_unix(path); });
 }

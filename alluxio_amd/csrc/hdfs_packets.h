@@ -64,4 +64,51 @@ class DnPacketReader {
   uint64_t direct_got_ = 0;
 };
 
+// The client side of WRITE_BLOCK (DFSClient's DataStreamer + ResponseProcessor): the caller's
+// bytes leave as chunk-aligned packets of `packet_bytes` (CRC32C per bytes-per-checksum chunk,
+// one writev each; a short tail is held back until more data or finish()), at most `max_in_flight`
+// packets un-acked; PipelineAckProto replies are parsed as they arrive and any non-SUCCESS reply
+// fails the write.
+class DnPacketWriter {
+ public:
+  DnPacketWriter(int fd, uint32_t bytes_per_checksum, uint32_t packet_bytes, uint32_t max_in_flight, int timeout_ms);
+  void write(const uint8_t* p, uint64_t n);
+  // Sends the held tail and the final empty packet, waits for every ack; returns the block length.
+  uint64_t finish();
+  uint64_t offset() const { return off_ + tail_.size(); }
+
+ private:
+  void send_packet(const uint8_t* data, uint32_t n, bool last);
+  void read_acks();   // parses buffered acks, then drains the socket without waiting
+  int fd_;
+  uint32_t bpc_, packet_;
+  uint32_t max_in_flight_;
+  int timeout_ms_;
+  uint64_t off_ = 0, seq_ = 0, inflight_ = 0;
+  std::vector<uint8_t> sums_, tail_;
+  std::string rbuf_;
+};
+
+// The DataNode side of WRITE_BLOCK for the gateway: packets received straight into the caller's
+// buffer (CRC32C-verified, offsets checked) in batches; the caller stores the batch, then ack()
+// answers every packet of it with one PipelineAckProto each (one writev).
+class DnPacketReceiver {
+ public:
+  DnPacketReceiver(int fd, uint32_t bytes_per_checksum, int timeout_ms);
+  // Packets into dst until >= batch data bytes, the last packet, an error, cap - got < 16 MiB, or
+  // no further packet is already waiting on the socket.
+  // status: 0 SUCCESS, 1 ERROR (bad offset / framing), 2 ERROR_CHECKSUM.
+  uint64_t receive(uint8_t* dst, uint64_t cap, uint64_t batch, bool* last, int* status);
+  void ack(int status);
+  uint64_t received() const { return received_; }
+
+ private:
+  int fd_;
+  uint32_t bpc_;
+  int timeout_ms_;
+  uint64_t received_ = 0;
+  std::vector<int64_t> pending_;     // seqnos of the last receive()
+  std::vector<uint8_t> sums_;
+};
+
 }  // namespace amdx

@@ -283,6 +283,15 @@ class _DataHandler(socketserver.BaseRequestHandler):
 
     @staticmethod
     def _receive(s, sink, downstream, bpc):
+        if downstream is None:
+            rx = None
+            try:
+                from ..ops.native import lib
+                rx = lib().DnPacketReceiver(s.fileno(), bpc, 60_000)
+            except Exception:  # noqa: BLE001 - no native extension: the Python packet loop
+                rx = None
+            if rx is not None:
+                return _DataHandler._receive_native(rx, sink)
         received, status = 0, H.ST_SUCCESS
         while True:
             plen, hlen = struct.unpack(">IH", bytes(H.recv_exact(s, 6)))
@@ -311,6 +320,28 @@ class _DataHandler(socketserver.BaseRequestHandler):
             s.sendall(H.delimited(ack))
             if hdr.lastPacketInBlock or status != H.ST_SUCCESS:
                 return received, status
+
+
+    _RX_BATCH = 4 << 20
+
+    @staticmethod
+    def _receive_native(rx, sink):
+        """Packets parsed and CRC-verified in C++ straight into a batch buffer
+        (csrc/hdfs_packets.cpp DnPacketReceiver); the batch goes to the sink, then every packet of it
+        is acked -- an ack still means the bytes reached the Alluxio out stream."""
+        buf = bytearray(_DataHandler._RX_BATCH + (17 << 20))
+        mv = memoryview(buf)
+        while True:
+            n, last, status = rx.receive(buf, _DataHandler._RX_BATCH)
+            if status == H.ST_SUCCESS and n:
+                try:
+                    sink.write(mv[:n])
+                except Exception:  # noqa: BLE001
+                    LOG.debug("hdfs gateway block write failed", exc_info=True)
+                    status = H.ST_ERROR
+            rx.ack(status)
+            if last or status != H.ST_SUCCESS:
+                return rx.received, status
 
 
 # ---- the Alluxio-backed gateway -------------------------------------------------------------------------
@@ -345,7 +376,7 @@ class _BlockSink:
 
     def write(self, data) -> None:
         with self.of.lock:
-            self.of.stream.write(bytes(data))
+            self.of.stream.write(data)          # copied into the cache (and UFS) before it returns
             self.of.written += len(data)
 
     def commit(self, n: int) -> None:

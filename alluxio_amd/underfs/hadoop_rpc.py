@@ -697,8 +697,22 @@ class BlockWriter:
             self.sock.close()
             raise IOError(f"datanode WRITE_BLOCK failed: status {resp.status} {resp.firstBadLink} {resp.message}")
         self.offset = self.seqno = self.unacked = 0
+        # packets built (CRC32C, one writev each) and acks parsed in C++ (csrc/hdfs_packets.cpp)
+        self.native = None
+        try:
+            from ..ops.native import lib
+            self.native = lib().DnPacketWriter(self.sock.fileno(), BYTES_PER_CHECKSUM, PACKET_DATA, 80,
+                                               int(timeout * 1000))
+        except Exception:  # noqa: BLE001 - no native extension: the Python packet loop
+            self.native = None
 
     def write(self, data) -> None:
+        if self.native is not None:
+            try:
+                self.native.write(data)
+            except Exception as e:  # noqa: BLE001 - StoreError -> IOError like the Python loop
+                raise IOError(f"hdfs pipeline write failed: {e}") from e
+            return
         mv = memoryview(data)
         for i in range(0, len(mv), PACKET_DATA):
             piece = mv[i:i + PACKET_DATA]
@@ -717,6 +731,14 @@ class BlockWriter:
 
     def finish(self):
         """Send the empty last packet, collect every ack; returns the block with its final size."""
+        if self.native is not None:
+            try:
+                self.block.numBytes = self.native.finish()
+            except Exception as e:  # noqa: BLE001
+                raise IOError(f"hdfs pipeline write failed: {e}") from e
+            finally:
+                self.sock.close()
+            return self.block
         write_packet(self.sock, self.offset, self.seqno, b"", True)
         self.unacked += 1
         try:

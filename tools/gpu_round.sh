@@ -55,7 +55,7 @@ for s in $STEPS; do
     k7mixed) run pytest_k7mixed 300 python -u -m pytest tests/test_evict_alloc_gpu.py -k "magazine" -x -v --timeout 120 --timeout-method thread ;;
     c5t8) run ingest_config5_t8 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/ufs_ingest_config5_t8.jsonl" ;;
     hdfsgw)
-      run hdfs_gateway_bench 600 python tools/hdfs_gateway_bench.py --file-size 2g --threads 1,4,8 --out "$OUT/hdfs_gateway.jsonl"
+      run hdfs_gateway_bench 600 python tools/hdfs_gateway_bench.py --file-size 2g --threads 1,4,8 --write-threads 1,4,8 --out "$OUT/hdfs_gateway.jsonl"
       ;;
     s3ingest)
       run ingest_s3native 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 2g --dram 6g --factor 2 --depths 1,3 --out "$OUT/ufs_ingest_s3native.jsonl"
