@@ -265,15 +265,38 @@ class S3Handler:
             status = 206
         length = max(0, end - start + 1)
         data = b""
-        if length:
+        h = {"ETag": f'"{_etag(st)}"', "Last-Modified": _http_date(st.info.lastModificationTimeMs),
+             "Content-Type": "application/octet-stream", "Accept-Ranges": "bytes"}
+        if length > self.STREAM_CHUNK:
+            # large objects stream through one reused buffer (native reader refills, one sendall
+            # per chunk) instead of being read whole into memory first
+            h["Content-Length"] = str(length)
+            data = self._stream(st, start, length)
+        elif length:
             with self.fs.open_file(st.path, status=st) as f:
                 f.seek(start)
                 data = f.read(length)
-        h = {"ETag": f'"{_etag(st)}"', "Last-Modified": _http_date(st.info.lastModificationTimeMs),
-             "Content-Type": "application/octet-stream", "Accept-Ranges": "bytes"}
         if status == 206:
             h["Content-Range"] = f"bytes {start}-{end}/{n}"
         return status, h, data
+
+    STREAM_CHUNK = 8 << 20
+
+    def _stream(self, st, start: int, length: int):
+        f = self.fs.open_file(st.path, status=st)
+        try:
+            f.seek(start)
+            buf = bytearray(self.STREAM_CHUNK)
+            mv = memoryview(buf)
+            left = length
+            while left > 0:
+                n = f.readinto(mv[:min(len(buf), left)])
+                if not n:
+                    raise IOError(f"{st.path}: object ended {left} bytes early")
+                yield mv[:n]          # written out (sendall) before the buffer is reused
+                left -= n
+        finally:
+            f.close()
 
     def _delete_key(self, bucket_path, key):
         path = f"{bucket_path}/{key}".rstrip("/")
