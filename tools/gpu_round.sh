@@ -142,6 +142,9 @@ for s in $STEPS; do
       run bench_rehearse_2rank 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --one-device --steps 10 --warmup 3
       run bench_rehearse_4rank 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 4 --one-device --steps 10 --warmup 3
       ;;
+    lz4encprof)
+      run rocprof_lz4enc 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_lz4enc" -o lz4enc --output-format csv -- python3 tools/lz4_bench.py --chunks 1024 --variants=-1
+      ;;
     hostsweep)
       for rb in 256KB 512KB 1MB; do
         for pf in false true; do
