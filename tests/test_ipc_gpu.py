@@ -75,7 +75,28 @@ def test_ipc_read_from_other_process(gpu, tmp_path):
             assert f._nreader is not None and f._nreader.source == "ipc"
             assert f._nat.refills >= 20
         assert b"".join(parts) == expect.tobytes()
+        # short-circuit writes into the worker's HBM arena (OpenDeviceWrite + ArenaSink: pinned
+        # staging, H2D DMA into the IPC-mapped pages), from host memory and from a device tensor
+        wdata = np.random.default_rng(8).integers(0, 256, 19 * (1 << 20) + 5, dtype=np.uint8)
+        with fs.create_file("/ipc/w", write_type="MUST_CACHE") as f:
+            for i in range(0, len(wdata), 3 << 20):
+                f.write(wdata[i:i + (3 << 20)])
+            assert f._writers and type(f._writers[0]).__name__ == "IpcBlockWriter"
+        with fs.create_file("/ipc/wd", write_type="MUST_CACHE") as f:
+            f.write(torch.from_numpy(wdata[:5 << 20]).cuda())
+        assert fs.read_file("/ipc/w") == wdata.tobytes()
+        assert fs.read_file("/ipc/wd") == wdata[:5 << 20].tobytes()
         fs.close()
+        # native gRPC WriteBlock into the HBM tier (the server stages chunks through pinned memory)
+        fs3 = FileSystem(conf=Configuration({"alluxio.user.file.passive.cache.enabled": "false",
+                                             "alluxio.user.short.circuit.enabled": "false"}),
+                         master_address=master)
+        with fs3.create_file("/ipc/g", write_type="MUST_CACHE") as f:
+            f.write(wdata)
+            assert f._writers and type(f._writers[0]).__name__ == "GrpcBlockWriter"
+            assert f._writers[0]._sink is not None
+        assert fs3.read_file("/ipc/g") == wdata.tobytes()
+        fs3.close()
         # the same bytes over the worker's native gRPC data port: HBM chunks staged D2H by the
         # server's I/O threads, frames parsed by the native client
         fs2 = FileSystem(conf=Configuration({"alluxio.user.file.passive.cache.enabled": "false",
