@@ -463,6 +463,7 @@ PYBIND11_MODULE(_C, m) {
       .def("mag_pages", &BlockStore::mag_pages, G())
       .def("mag_device_count", &BlockStore::mag_device_count, G())
       .def("check_pages", &BlockStore::check_pages, G())
+      .def("set_free_ahead", &BlockStore::set_free_ahead, py::arg("bytes"))
       .def("mag_claim_many", &BlockStore::mag_claim_many, G())
       .def("mag_give", &BlockStore::mag_give, G())
       .def("mag_drain", &BlockStore::mag_drain_dir, G())

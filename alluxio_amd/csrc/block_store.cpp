@@ -475,7 +475,7 @@ int BlockStore::create_block(int64_t session, int64_t block_id, int tier, const 
     throw StoreError(kErrAlreadyExists, "block " + std::to_string(block_id) + " already exists");
   int d = allocate_dir(tier, medium, initial);
   if (d < 0 && evict) {
-    free_space_locked(lk, session, initial, tier, -1, medium);
+    free_space_locked(lk, session, initial, tier, -1, medium, free_ahead_);
     if (blocks_.count(block_id))   // created by another thread while the store was unlocked
       throw StoreError(kErrAlreadyExists, "block " + std::to_string(block_id) + " already exists");
     d = allocate_dir(tier, medium, initial);
@@ -519,7 +519,7 @@ void BlockStore::request_space(int64_t session, int64_t block_id, uint64_t addit
   StorageDir& d = *dirs_[b->dir];
   const uint64_t target = b->reserved + additional;
   if (grow_pages(d, *b, target)) return;
-  free_space_locked(lk, session, additional, d.spec.tier, b->dir, "");
+  free_space_locked(lk, session, additional, d.spec.tier, b->dir, "", free_ahead_);
   b = find(block_id);
   if (!b || !grow_pages(*dirs_[b->dir], *b, target))
     throw StoreError(kErrOutOfSpace, "cannot reserve " + std::to_string(additional) + " more bytes");
@@ -1437,8 +1437,11 @@ std::vector<uint32_t> BlockStore::select_victims_cpu(const std::vector<uint32_t>
 }
 
 void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
-                                   int tier, int dir, const std::string& medium) {
+                                   int tier, int dir, const std::string& medium, uint64_t ahead) {
   const auto wait_until = std::chrono::steady_clock::now() + std::chrono::seconds(2);
+  // victims are selected for bytes + ahead (the reference's free-ahead: one eviction round makes
+  // room for the next creates too); success needs only `bytes`
+  const uint64_t goal = bytes + ahead;
   for (int attempt = 0; attempt < 4; ++attempt) {
     // target dir: the one that can reach `bytes` with the most (available + evictable)
     int target = -1;
@@ -1450,9 +1453,10 @@ void BlockStore::free_space_locked(std::unique_lock<std::mutex>& lk, int64_t ses
       if (target < 0 || reach > best) { target = d->index; best = reach; }
     }
     if (target < 0) throw StoreError(kErrOutOfSpace, "no storage dir matches the eviction location");
-    if (dirs_[target]->available() >= bytes) return;
+    if (dirs_[target]->available() >= (attempt == 0 ? goal : bytes)) return;
     // arena dirs free whole pages: convert the shortfall into page-rounded bytes
-    uint64_t need = bytes - dirs_[target]->available();
+    uint64_t need = (attempt == 0 ? goal : bytes) - std::min<uint64_t>(dirs_[target]->available(),
+                                                                       attempt == 0 ? goal : bytes);
     if (dirs_[target]->spec.kind != DirKind::kFile)
       need = ceil_div(need, dirs_[target]->spec.page_size) * dirs_[target]->spec.page_size;
     ++stats_.selections;

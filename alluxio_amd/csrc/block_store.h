@@ -262,6 +262,9 @@ class BlockStore {
   // gives them back with mag_give), hand pages back, drain the magazine into the host pool.
   int64_t mag_refill_pages(int dir, int64_t pages);
   int64_t mag_device_count(int dir);
+  // Extra bytes a create / reserve that has to evict frees beyond its own need
+  // (alluxio.worker.tieredstore.free.ahead.bytes).
+  void set_free_ahead(uint64_t bytes) { free_ahead_ = bytes; }
   // Debug: page accounting of one dir (host pool + K7 magazine + block pages partition the
   // arena; the device magazine bitmap holds exactly mag_pages).  Empty when consistent.
   std::string check_pages(int dir);
@@ -293,7 +296,7 @@ class BlockStore {
   bool grow_pages(StorageDir& d, BlockMeta& b, uint64_t new_reserved, bool use_reserved = false);
   void release_storage(BlockMeta& b);
   void free_space_locked(std::unique_lock<std::mutex>& lk, int64_t session, uint64_t bytes,
-                         int tier, int dir, const std::string& medium);
+                         int tier, int dir, const std::string& medium, uint64_t ahead = 0);
   std::vector<uint32_t> select_victims_cpu(const std::vector<uint32_t>& cand_slots, uint64_t need);
   std::vector<uint32_t> select_victims_device(std::unique_lock<std::mutex>& lk, int dir, uint64_t need,
                                               uint64_t dir_mask = 0, bool unit = false, bool invert = false);
@@ -338,6 +341,7 @@ class BlockStore {
   std::condition_variable lock_cv_;
   std::vector<std::unique_ptr<StorageDir>> dirs_;
   std::unordered_map<int64_t, BlockMeta> blocks_;
+  uint64_t free_ahead_ = 0;
   std::unordered_set<int64_t> pinned_files_;
   // lock table
   struct LockRec { int64_t block; int64_t session; bool write; };

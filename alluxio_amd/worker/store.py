@@ -245,6 +245,8 @@ class TieredStore:
         self.has_device_tier = any(a is not None and a.kind == "hbm" for a in self.arenas)
         self.native.set_use_device_evict(conf.get_bool("alluxio.worker.eviction.device.enabled", "true"))
         self.native.set_demote_on_evict(conf.get_bool("alluxio.worker.tieredstore.eviction.demote", "true"))
+        # TieredBlockStore.allocateSpace frees size + free.ahead.bytes when it has to evict
+        self.native.set_free_ahead(conf.get_bytes("alluxio.worker.tieredstore.free.ahead.bytes", "0"))
         self.native.set_use_device_alloc(conf.get_bool("alluxio.worker.hbm.device.alloc.enabled", "true"),
                                          conf.get_int("alluxio.worker.hbm.device.alloc.min.pages", "1024"))
         LOG.info("tiered store: %s", self.native.stats())

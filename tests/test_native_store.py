@@ -332,3 +332,20 @@ def test_concurrent_creates_with_demotion_never_run_out(tmp_path):
     assert all(s.has_block(t * 1000 + i + 1) for t in range(8) for i in range(24))
     st = s.evict_stats()
     assert st["demoted_blocks"] >= 8 * 24 - 8
+
+
+def test_free_ahead_evicts_beyond_the_request(tmp_path):
+    """alluxio.worker.tieredstore.free.ahead.bytes (TieredBlockStore.allocateSpace): a create that
+    must evict frees its size plus the free-ahead, so the next creates find room without another
+    eviction round; without it exactly one victim goes per create."""
+    data = np.full(MB, 7, dtype=np.uint8)
+    for ahead, expect_rounds in ((0, 4), (3 * MB, 1)):
+        s = _store(tmp_path / f"a{ahead}", mem_mb=8, ssd_mb=64)
+        s.set_free_ahead(ahead)
+        for b in range(1, 9):                       # fill the 8 MiB MEM tier
+            _put(s, b, data, tier=0)
+        sel0 = s.evict_stats()["selections"]
+        for b in range(100, 104):                   # four more creates into the full tier
+            _put(s, b, data, tier=0)
+        assert s.evict_stats()["selections"] - sel0 == expect_rounds, ahead
+        assert all(s.has_block(b) for b in range(100, 104))

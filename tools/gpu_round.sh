@@ -49,11 +49,16 @@ for s in $STEPS; do
       run rocprof_config5 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_config5" -o c5 --output-format csv -- python3 tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 4
       ;;
     mastergrpc2)
-      run master_bench_grpc_p8 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 8 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p8.json"
+      [ -n "${SKIP_P8:-}" ] || run master_bench_grpc_p8 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 8 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p8.json"
+      run master_bench_grpc_p32 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 32 --threads 2 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p32.json"
       run master_bench_grpc_p16 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 16 --threads 4 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p16.json"
       ;;
     k7mixed) run pytest_k7mixed 300 python -u -m pytest tests/test_evict_alloc_gpu.py -k "magazine" -x -v --timeout 120 --timeout-method thread ;;
     c5t8) run ingest_config5_t8 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/ufs_ingest_config5_t8.jsonl" ;;
+    c5ahead)
+      run ingest_config5_ahead4 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 4 --free-ahead 512m --out "$OUT/ufs_ingest_config5_ahead.jsonl"
+      run ingest_config5_ahead8 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --free-ahead 512m --out "$OUT/ufs_ingest_config5_ahead.jsonl"
+      ;;
     hdfsgw)
       run hdfs_gateway_bench 600 python tools/hdfs_gateway_bench.py --file-size 2g --threads 1,4,8 --write-threads 1,4,8 --out "$OUT/hdfs_gateway.jsonl"
       ;;

@@ -78,6 +78,7 @@ def run(a, depth: int) -> dict:
             "alluxio.worker.ufs.ingest.depth": str(depth),
             "alluxio.worker.network.async.cache.manager.threads.max": str(a.threads),
             "alluxio.worker.tieredstore.eviction.demote": "true",
+            "alluxio.worker.tieredstore.free.ahead.bytes": a.free_ahead,
         }
         if a.ufs == "s3native":
             # the native S3 endpoint (csrc/http_blob.cpp: sendfile GETs) over a directory whose
@@ -196,7 +197,7 @@ def run(a, depth: int) -> dict:
                     "demoted_blocks": st["demoted_blocks"], "demoted_bytes": st["demoted_bytes"],
                     "batched_moves": st["batched_moves"], "evict_waits": st.get("evict_waits"), "evict_retries": st.get("evict_retries"), "revalidated_away": st.get("revalidated_away"), "resident_by_medium": tiers,
                     "reread_GBps": round(rb / rel / 1e9, 3) if rel > 0 else None, "reread_bytes": rb,
-                    "threads": a.threads, "stages": stage}
+                    "threads": a.threads, "free_ahead": a.free_ahead, "stages": stage}
     finally:
         if proxy is not None:
             proxy.stop()
@@ -219,6 +220,7 @@ def main():
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--timeout", type=float, default=600)
     ap.add_argument("--work-dir", default=None)
+    ap.add_argument("--free-ahead", default="0", help="alluxio.worker.tieredstore.free.ahead.bytes")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     for d in [int(x) for x in a.depths.split(",")]:
