@@ -150,6 +150,10 @@ for s in $STEPS; do
     lz4encprof)
       run rocprof_lz4enc 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_lz4enc" -o lz4enc --output-format csv -- python3 tools/lz4_bench.py --chunks 1024 --variants=-1
       ;;
+    hostprocs)
+      run wb_host_procs4 600 python tools/worker_bench_host.py --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs.jsonl"
+      run wb_host_procs8 600 python tools/worker_bench_host.py --threads 256 --transports grpc,ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs.jsonl"
+      ;;
     hostsweep)
       for rb in 256KB 512KB 1MB; do
         for pf in false true; do

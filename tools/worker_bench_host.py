@@ -58,6 +58,10 @@ def main(argv=None) -> int:
     ap.add_argument("--tier", default="hbm:0", help="worker MEM tier dir (hbm:N or dram)")
     ap.add_argument("--reader-buffer", default="1MB", help="alluxio.user.native.reader.buffer.size")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
+    ap.add_argument("--client-procs", type=int, default=1,
+                    help="spread the threads over this many client processes (the reference's --clients "
+                         "makes N FileSystem instances in one JVM; Python instances in one interpreter "
+                         "share one lock, so they go to separate processes); throughput is summed")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
 
@@ -88,28 +92,38 @@ def main(argv=None) -> int:
                      "alluxio.user.file.passive.cache.enabled": "false"}
             props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             for t in a.threads.split(","):
-                args = ["--threads", t, "--file-size", a.file_size, "--buffer-size", a.buffer_size,
+                nproc = max(1, a.client_procs)
+                per = max(1, int(t) // nproc)
+                args = ["--threads", str(per), "--file-size", a.file_size, "--buffer-size", a.buffer_size,
                         "--block-size", a.block_size, "--duration", a.duration, "--warmup", a.warmup,
                         "--mode", "threads"]
                 t0 = time.time()
                 s0 = (stats.streams, stats.bytes, stats.declined) if stats is not None else (0, 0, 0)
-                p = subprocess.run([sys.executable, "-c", CLIENT.format(root=ROOT, addr=c.master.address,
-                                                                       args=args, props=props)],
-                                   capture_output=True, text=True, timeout=600)
-                line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
-                if line is None:
-                    print(f"client process ({transport}, {t} threads) exited rc={p.returncode} without a result",
-                          file=sys.stderr)
-                    print(p.stdout[-2000:], file=sys.stderr)
-                    print(p.stderr[-3000:], file=sys.stderr)
-                    return 1
-                r = json.loads(line[7:])
+                procs = [subprocess.Popen([sys.executable, "-c", CLIENT.format(root=ROOT, addr=c.master.address,
+                                                                              args=args, props=props)],
+                                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                         for _ in range(nproc)]
+                results = []
+                for p in procs:
+                    out, err = p.communicate(timeout=600)
+                    line = next((ln for ln in out.splitlines() if ln.startswith("RESULT ")), None)
+                    if line is None:
+                        print(f"client process ({transport}, {t} threads) exited rc={p.returncode} without a result",
+                              file=sys.stderr)
+                        print(out[-2000:], file=sys.stderr)
+                        print(err[-3000:], file=sys.stderr)
+                        return 1
+                    results.append(json.loads(line[7:]))
+                r = {"throughput_MBps": sum(x["throughput_MBps"] for x in results),
+                     "bytes": sum(x["bytes"] for x in results), "duration_s": results[0]["duration_s"],
+                     "errors": [e for x in results for e in x["errors"]]}
                 row = {"bench": "StressWorkerBench --mode threads (host readers, separate client process)",
-                       "transport": transport, "tier": a.tier, "threads": int(t), "buffer": a.buffer_size,
+                       "transport": transport, "tier": a.tier, "threads": per * nproc, "buffer": a.buffer_size,
                        "file_size": a.file_size, "block_size": a.block_size,
                        "throughput_MBps": round(r["throughput_MBps"], 1), "bytes": r["bytes"],
                        "duration_s": r["duration_s"], "errors": r["errors"], "wall_s": round(time.time() - t0, 1),
-                       "reader_buffer": a.reader_buffer, "client_props": a.client_prop}
+                       "reader_buffer": a.reader_buffer, "client_props": a.client_prop,
+                       "client_procs": nproc}
                 if stats is not None:
                     row["data_server"] = {"native_streams": stats.streams - s0[0],
                                           "native_bytes": stats.bytes - s0[1],
