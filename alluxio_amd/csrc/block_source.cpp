@@ -58,7 +58,14 @@ hipStream_t reader_stream(int device) {
   std::lock_guard<std::mutex> g(mu);
   DevCtx& c = ctx[device];
   if (c.streams.empty()) {
-    for (int i = 0; i < 8; ++i) {
+    // ALLUXIO_READER_STREAMS: streams per device (default 8; a process maps them onto at most
+    // GPU_MAX_HW_QUEUES hardware queues)
+    static const int nstreams = [] {
+      const char* e = getenv("ALLUXIO_READER_STREAMS");
+      const int v = e ? atoi(e) : 8;
+      return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
+    for (int i = 0; i < nstreams; ++i) {
       hipStream_t s = nullptr;
       if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
         throw StoreError(kErrHip, "hipStreamCreate failed");

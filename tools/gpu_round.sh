@@ -154,6 +154,15 @@ for s in $STEPS; do
       run wb_host_procs4 600 python tools/worker_bench_host.py --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs.jsonl"
       run wb_host_procs8 600 python tools/worker_bench_host.py --threads 256 --transports grpc,ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs.jsonl"
       ;;
+    hostprocs2)
+      ALLUXIO_READER_STREAMS=1 run wb_host_procs8_s1 600 python tools/worker_bench_host.py --threads 256 --transports ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs_streams.jsonl"
+      ALLUXIO_READER_STREAMS=8 run wb_host_procs8_s8 600 python tools/worker_bench_host.py --threads 256 --transports ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs_streams.jsonl"
+      ALLUXIO_READER_STREAMS=1 run wb_host_procs4_s1 600 python tools/worker_bench_host.py --threads 16,64,256 --transports ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs_streams.jsonl"
+      ;;
+    hostprocs3)
+      HSA_ENABLE_SDMA=0 run wb_host_procs4_nosdma 600 python tools/worker_bench_host.py --threads 16,64,256 --transports ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs_sdma.jsonl"
+      run wb_host_procs4_sdma 600 python tools/worker_bench_host.py --threads 16,64,256 --transports ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs_sdma.jsonl"
+      ;;
     hostsweep)
       for rb in 256KB 512KB 1MB; do
         for pf in false true; do
