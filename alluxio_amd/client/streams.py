@@ -172,6 +172,7 @@ class GrpcBlockReader(BlockReader):
         self._pos = None
         self._buf = b""
         self._buf_off = 0
+        self._nsrc = None               # native GrpcBlockSource for large reads (False: unavailable)
 
     def _open(self, offset):
         self._close_stream()
@@ -219,6 +220,26 @@ class GrpcBlockReader(BlockReader):
         return bytes(out)
 
     def read_into(self, offset, length, ptr, kind, stream=0):
+        # large reads (a GPU consumer's batch, a host buffer) go through the native client: frames
+        # parsed straight into the destination (host) or into pinned chunks DMA'd H2D (device)
+        if length >= (1 << 20) and self._nsrc is not False:
+            if self._nsrc is None:
+                try:
+                    self._nsrc = self.native_source() or False
+                except Exception:  # noqa: BLE001 - fall back to the grpcio stream
+                    LOG.debug("native ReadBlock client unavailable", exc_info=True)
+                    self._nsrc = False
+            if self._nsrc is not False:
+                from ..ops.native import lib, native_errors
+                dev = 0
+                if kind == DEVICE:
+                    import torch
+                    dev = torch.cuda.current_device()
+                    if stream:    # work queued on the caller's stream may still use the buffer
+                        torch.cuda.ExternalStream(stream).synchronize()
+                with native_errors():
+                    lib().source_read(self._nsrc, offset, length, ptr, kind, dev)
+                return
         data = self.read_bytes(offset, length)
         if len(data) != length:
             raise UnavailableException(f"short read of block {self.block_id}: {len(data)}/{length}")
@@ -255,6 +276,9 @@ class GrpcBlockReader(BlockReader):
 
     def close(self):
         self._close_stream()
+        if self._nsrc:
+            self._nsrc.close()
+        self._nsrc = None
 
 
 class IpcBlockReader(BlockReader):

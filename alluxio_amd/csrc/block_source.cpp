@@ -224,6 +224,47 @@ void ArenaSink::write(uint64_t off, const uint8_t* src, uint64_t n) {
   length_ = std::max(length_, off + n);
 }
 
+// ---- reads into device memory ------------------------------------------------------------------
+void source_read_to_device(BlockSource& src, uint64_t off, uint64_t n, uint8_t* dptr, int device) {
+  constexpr uint64_t kStage = 4u << 20;
+  struct Buf {
+    uint8_t* p = nullptr;
+    bool pinned = false;
+    hipEvent_t ev = nullptr;
+  } b[2];
+  struct Cleanup {
+    Buf* b;
+    ~Cleanup() {
+      for (int i = 0; i < 2; ++i) {
+        if (b[i].ev) {
+          (void)hipEventSynchronize(b[i].ev);
+          (void)hipEventDestroy(b[i].ev);
+        }
+        if (b[i].p) host_buffer_release(b[i].p, kStage, b[i].pinned);
+      }
+    }
+  } cleanup{b};
+  hipStream_t st = reader_stream(device);
+  for (int i = 0; i < 2; ++i) {
+    b[i].p = host_buffer_alloc(kStage, &b[i].pinned);
+    if (hipEventCreateWithFlags(&b[i].ev, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
+      throw StoreError(kErrHip, "hipEventCreate failed");
+  }
+  uint64_t done = 0;
+  int k = 0;
+  while (done < n) {
+    const uint64_t take = std::min<uint64_t>(kStage, n - done);
+    if (hipEventSynchronize(b[k].ev) != hipSuccess) throw StoreError(kErrHip, "hipEventSynchronize failed");
+    src.read(off + done, take, b[k].p);            // network / arena bytes into pinned memory
+    const hipError_t e = hipMemcpyAsync(dptr + done, b[k].p, take, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) throw StoreError(kErrHip, std::string("hipMemcpyAsync H2D: ") + hipGetErrorString(e));
+    if (hipEventRecord(b[k].ev, st) != hipSuccess) throw StoreError(kErrHip, "hipEventRecord failed");
+    done += take;
+    k ^= 1;
+  }
+  wait_stream(st);
+}
+
 // ---- HostArenaSource --------------------------------------------------------------------------
 HostArenaSource::HostArenaSource(uint64_t base, std::vector<int64_t> pages, uint64_t page_size, uint64_t length)
     : BlockSource(length), base_(base), pages_(std::move(pages)), page_size_(page_size) {

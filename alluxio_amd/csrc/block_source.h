@@ -177,6 +177,11 @@ class GrpcBlockSink {
   uint64_t written_ = 0;
 };
 
+// Block bytes [off, off + n) of `src` into device memory at dptr: chunks land in two alternating
+// pinned buffers, each DMA'd H2D while the next chunk is being received (a GPU consumer of a
+// remote worker's block).
+void source_read_to_device(BlockSource& src, uint64_t off, uint64_t n, uint8_t* dptr, int device);
+
 // Pinned (device-mapped) host buffer for a chunk buffer (pooled by size; malloc without a GPU).
 uint8_t* host_buffer_alloc(uint64_t n, bool* pinned);
 // Gives a buffer of host_buffer_alloc(n) back (pinned ones to the pool).

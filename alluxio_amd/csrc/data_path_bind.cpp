@@ -225,6 +225,22 @@ void bind_data_path(py::module_& m) {
            py::arg("host"), py::arg("port"), py::arg("block_id"), py::arg("length"), py::arg("chunk") = 1u << 20,
            py::arg("ufs_options") = py::bytes(), py::arg("promote") = false, py::arg("channel_id") = "",
            py::arg("user") = "", py::arg("timeout_ms") = 60000, py::arg("unix_path") = "");
+  m.def("source_read", [](std::shared_ptr<BlockSource> src, uint64_t off, uint64_t n, uint64_t ptr, int kind,
+                          int device) {
+          if (src->needs_gil()) throw std::runtime_error("source_read needs a native source");
+          py::gil_scoped_release rel;
+          try {
+            if (kind == (int)MemKind::kDevice)
+              source_read_to_device(*src, off, n, reinterpret_cast<uint8_t*>(ptr), device);
+            else
+              src->read(off, n, reinterpret_cast<uint8_t*>(ptr));
+          } catch (const StoreError&) {
+            throw;
+          } catch (const std::exception& e) {
+            throw StoreError(kErrIo, e.what());
+          }
+        }, py::arg("source"), py::arg("offset"), py::arg("length"), py::arg("ptr"), py::arg("kind"),
+        py::arg("device") = 0);
   py::class_<ArenaSink, std::shared_ptr<ArenaSink>>(m, "ArenaSink")
       .def(py::init<uint64_t, std::vector<int64_t>, uint64_t, uint64_t, int, bool>(), py::arg("base"),
            py::arg("pages"), py::arg("page_size"), py::arg("capacity"), py::arg("device"), py::arg("host_arena"))

@@ -106,6 +106,13 @@ def test_ipc_read_from_other_process(gpu, tmp_path):
             got = f.read()
             assert f._nreader.source == "remote"
         assert got == expect.tobytes()
+        # a GPU consumer of the remote worker: ReadBlock frames into pinned chunks DMA'd H2D
+        dst2 = torch.zeros(len(expect), dtype=torch.uint8, device="cuda")
+        with fs2.open_file("/ipc/f") as f:
+            assert f.read_into(dst2) == len(expect)
+            assert f._reader.source == "remote" and f._reader._nsrc
+        torch.cuda.synchronize()
+        assert np.array_equal(dst2.cpu().numpy(), expect)
         fs2.close()
     finally:
         p.stdin.write("\n")

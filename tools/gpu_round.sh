@@ -163,6 +163,7 @@ for s in $STEPS; do
       HSA_ENABLE_SDMA=0 run wb_host_procs4_nosdma 600 python tools/worker_bench_host.py --threads 16,64,256 --transports ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs_sdma.jsonl"
       run wb_host_procs4_sdma 600 python tools/worker_bench_host.py --threads 16,64,256 --transports ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs_sdma.jsonl"
       ;;
+    remotedev) run remote_device_read 600 python tools/remote_device_read_bench.py --file-size 1g --out "$OUT/remote_device_read.jsonl" ;;
     hostsweep)
       for rb in 256KB 512KB 1MB; do
         for pf in false true; do

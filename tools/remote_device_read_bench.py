@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""GPU consumer of a block held by another worker process, read over gRPC ``ReadBlock`` (the
+path for data cached on another node; on one node short-circuit IPC is normally used instead).
+
+A worker with an HBM tier caches a file in this process; a separate client process with
+short-circuit off reads it with ``FileInStream.read_into(cuda_tensor)`` in ``--read-size`` pieces,
+``--reps`` times.  The client reads either through the native client (``GrpcBlockSource``: frames
+into pinned chunks, H2D DMA overlapped with the next chunk) or, with
+``--grpcio``, through the grpcio stream plus a host copy.
+
+    python tools/remote_device_read_bench.py --file-size 1g --out gpurun_out/remote_device_read.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CLIENT = r"""
+import json, sys, time
+sys.path.insert(0, {root!r})
+import torch
+from alluxio_amd.client.file_system import FileSystem
+from alluxio_amd.conf import Configuration
+fs = FileSystem(conf=Configuration({props!r}), master_address={addr!r})
+dst = torch.empty({read}, dtype=torch.uint8, device="cuda")
+def once():
+    n = 0
+    with fs.open_file("/rd/data") as f:
+        while True:
+            k = f.read_into(dst)
+            if not k:
+                break
+            n += k
+    torch.cuda.synchronize()
+    return n
+once()
+t0 = time.perf_counter()
+total = sum(once() for _ in range({reps}))
+el = time.perf_counter() - t0
+print("RESULT " + json.dumps({{"bytes": total, "seconds": el}}), flush=True)
+fs.close()
+"""
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--file-size", default="1g")
+    ap.add_argument("--read-size", default="64m")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    import numpy as np
+
+    from alluxio_amd.minicluster import LocalAlluxioCluster
+    from alluxio_amd.utils.format import parse_space_size
+    size = parse_space_size(a.file_size)
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "hbm:0",
+            "alluxio.worker.tieredstore.level0.dirs.quota": str(size + (512 << 20)),
+            "alluxio.worker.hbm.page.size": "2MB", "alluxio.user.block.size.bytes.default": "64MB",
+            "alluxio.security.authorization.permission.enabled": "false"}
+    with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=tempfile.mkdtemp(prefix="rdbench_")) as c:
+        fs = c.client()
+        fs.write_file("/rd/data", np.random.default_rng(0).integers(0, 256, size, dtype=np.uint8),
+                      write_type="MUST_CACHE")
+        for native in (True, False):
+            props = {"alluxio.user.network.inprocess.transport.enabled": "false",
+                     "alluxio.user.short.circuit.enabled": "false",
+                     "alluxio.user.native.reader.enabled": str(native).lower(),
+                     "alluxio.user.file.passive.cache.enabled": "false"}
+            p = subprocess.run([sys.executable, "-c", CLIENT.format(root=ROOT, props=props, addr=c.master.address,
+                                                                   read=parse_space_size(a.read_size), reps=a.reps)],
+                               capture_output=True, text=True, timeout=900)
+            line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
+            if line is None:
+                print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
+                return 1
+            r = json.loads(line[7:])
+            row = {"bench": "GPU consumer of a remote worker's blocks (gRPC ReadBlock into a device tensor)",
+                   "client": "native GrpcBlockSource + pinned H2D" if native else "grpcio stream + host copy",
+                   "file_size": a.file_size, "read_size": a.read_size, "bytes": r["bytes"],
+                   "seconds": round(r["seconds"], 3), "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3)}
+            print(json.dumps(row), flush=True)
+            if a.out:
+                with open(a.out, "a") as f:
+                    f.write(json.dumps(row) + "\n")
+        fs.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
