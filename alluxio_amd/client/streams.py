@@ -865,12 +865,15 @@ def _host_view(ptr: int, n: int) -> memoryview:
 
 class UfsWriter:
     """THROUGH / CACHE_THROUGH UFS stream (via the local worker's UFS client or a WriteBlock
-    UFS_FILE stream to a worker — reference UfsFileWriteHandler)."""
+    UFS_FILE stream to a worker — reference UfsFileWriteHandler).  The remote stream is the
+    native gRPC client (``GrpcBlockSink`` with the UFS_FILE command) unless
+    ``alluxio.user.native.writer.enabled`` is off."""
 
-    def __init__(self, ctx, status, worker_addr=None, local_worker=None):
+    def __init__(self, ctx, status, worker_addr=None, local_worker=None, worker=None):
         self.length = 0
         self._local = None
         self._grpc = None
+        self._sink = None
         opts = pb.dataserver.CreateUfsFileOptions(ufs_path=status.ufsPath, owner=status.owner, group=status.group,
                                                   mode=status.mode, mount_id=status.mountId)
         if local_worker is not None:
@@ -881,14 +884,26 @@ class UfsWriter:
                                                                    mode=status.mode or 0o644))
             self._ufs = ufs
             self._path = status.ufsPath
-        else:
-            self._q = _AckQueue(pb.block.WriteRequest(command=pb.block.WriteRequestCommand(
-                type=1, id=status.fileId, create_ufs_file_options=opts)))
-            call = ctx.worker_channel(worker_addr).raw_stream(SVC_WORKER, "WriteBlock")
-            self._grpc = call(iter(self._q))
-            self._err = []
-            self._t = threading.Thread(target=self._drain, daemon=True)
-            self._t.start()
+            return
+        cmd = pb.block.WriteRequestCommand(type=1, id=status.fileId, create_ufs_file_options=opts)
+        if worker is not None and ctx.conf.get_bool("alluxio.user.native.writer.enabled", "true"):
+            from ..ops.native import lib, native_errors
+            if lib().FrameRpcServer.grpc_available():
+                call = _native_call(ctx, worker_addr, (worker.host, worker.dataPort or worker.rpcPort))
+                if call is not None:
+                    host, port, cid, user, timeout, uds = call
+                    chunk = ctx.conf.get_bytes("alluxio.user.network.writer.chunk.size.bytes", "1MB")
+                    with native_errors():
+                        self._sink = lib().GrpcBlockSink(host, port, status.fileId, chunk=chunk, channel_id=cid,
+                                                         user=user, timeout_ms=timeout, unix_path=uds,
+                                                         command=cmd.SerializeToString())
+                    return
+        self._q = _AckQueue(pb.block.WriteRequest(command=cmd))
+        call = ctx.worker_channel(worker_addr).raw_stream(SVC_WORKER, "WriteBlock")
+        self._grpc = call(iter(self._q))
+        self._err = []
+        self._t = threading.Thread(target=self._drain, daemon=True)
+        self._t.start()
 
     def _drain(self):
         try:
@@ -897,18 +912,30 @@ class UfsWriter:
         except Exception as e:  # noqa: BLE001
             self._err.append(e)
 
-    def write(self, data: bytes) -> None:
-        self.length += len(data)
+    def write(self, data) -> None:
+        n = len(data)
+        self.length += n
         if self._local is not None:
             self._local.write(data)
+        elif self._sink is not None:
+            from ..ops.native import native_errors
+            ptr, n, _, keep = _buffer_ptr(data)
+            with native_errors():
+                self._sink.write_ptr(ptr, n)
+            del keep
         else:
             mv = memoryview(data)
-            for i in range(0, len(data), 1 << 20):
+            for i in range(0, n, 1 << 20):
                 self._q.put(marshal.write_request_frame(mv[i:i + (1 << 20)]))
 
     def close(self) -> None:
         if self._local is not None:
             self._local.close()
+        elif self._sink is not None:
+            from ..ops.native import native_errors
+            sink, self._sink = self._sink, None
+            with native_errors():
+                sink.commit()
         else:
             self._q.close()
             self._t.join()
@@ -920,7 +947,10 @@ class UfsWriter:
             if self._local is not None:
                 self._local.close()
                 self._ufs.delete_file(self._path)
-            else:
+            elif self._sink is not None:
+                sink, self._sink = self._sink, None
+                sink.cancel()
+            elif self._grpc is not None:
                 self._grpc.cancel()
         except Exception:  # noqa: BLE001
             pass
@@ -973,7 +1003,7 @@ class FileOutStream(io.RawIOBase):
             lw = ctx.in_process_worker(w.address) if w is not None else None
             if w is None:
                 raise UnavailableException("no worker available for the UFS stream")
-            self._ufs = UfsWriter(ctx, status, worker_address_str(w.address), lw)
+            self._ufs = UfsWriter(ctx, status, worker_address_str(w.address), lw, w.address)
 
     def writable(self):
         return True

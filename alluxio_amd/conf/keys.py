@@ -225,6 +225,11 @@ _k("USER_NATIVE_WRITER_ENABLED", "alluxio.user.native.writer.enabled", "true", S
    "Block writes to a remote (other-process) worker use the native gRPC client (csrc/block_source.cpp "
    "GrpcBlockSink: WriteBlock over HTTP/2 with the chunks framed around the caller's bytes, GIL "
    "released) instead of grpcio.  UFS-fallback writes keep grpcio.")
+_k("WORKER_DATA_SERVER_NATIVE_UFS_WRITE_ENABLED", "alluxio.worker.data.server.native.ufs.write.enabled", "true",
+   Scope.WORKER,
+   "UFS_FILE WriteBlock streams (THROUGH / CACHE_THROUGH writes of remote clients) into a mount the "
+   "worker has found to be a local directory are written by the native data server's I/O threads "
+   "(temp file renamed over the target at the end) instead of the Python servicer.")
 _k("WORKER_NETWORK_WRITER_STAGING_SIZE", "alluxio.worker.network.writer.staging.size", "4MB", Scope.WORKER,
    "Pinned staging buffer per native WriteBlock stream of an HBM worker (H2D DMA of received chunks).")
 _k("WORKER_TIEREDSTORE_DRAM_PREFAULT", "alluxio.worker.tieredstore.dram.prefault", "false", Scope.WORKER,

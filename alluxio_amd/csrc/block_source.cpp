@@ -889,17 +889,19 @@ GrpcBlockSink::GrpcBlockSink(Options o) : o_(std::move(o)) {
                                   {h2::kSettingsMaxFrameSize, h2::kMaxFramePayload}};
   g.submit_settings(c->ng, 0, iv, 3);
   // WriteRequest{command{type=0 id tier pin space_to_reserve medium_type}}
-  std::string cmd;
-  put_field_varint(cmd, 1, 0);
-  put_field_varint(cmd, 2, (uint64_t)o_.block_id);
-  put_field_varint(cmd, 4, (uint64_t)(uint32_t)o_.tier);
-  if (!o_.medium.empty()) {
-    h2::put_varint(cmd, (8u << 3) | 2);
-    h2::put_varint(cmd, o_.medium.size());
-    cmd += o_.medium;
+  std::string cmd = o_.command;
+  if (cmd.empty()) {
+    put_field_varint(cmd, 1, 0);
+    put_field_varint(cmd, 2, (uint64_t)o_.block_id);
+    put_field_varint(cmd, 4, (uint64_t)(uint32_t)o_.tier);
+    if (!o_.medium.empty()) {
+      h2::put_varint(cmd, (8u << 3) | 2);
+      h2::put_varint(cmd, o_.medium.size());
+      cmd += o_.medium;
+    }
+    if (o_.pin) put_field_varint(cmd, 9, 1);
+    put_field_varint(cmd, 10, o_.reserve);
   }
-  if (o_.pin) put_field_varint(cmd, 9, 1);
-  put_field_varint(cmd, 10, o_.reserve);
   std::string req;
   h2::put_varint(req, (1u << 3) | 2);
   h2::put_varint(req, cmd.size());

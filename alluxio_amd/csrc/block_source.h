@@ -159,6 +159,9 @@ class GrpcBlockSink {
     uint64_t chunk = 1u << 20;       // bytes per WriteRequest message
     std::string channel_id, user;
     int timeout_ms = 60000;
+    // A serialized WriteRequestCommand sent instead of the ALLUXIO_BLOCK one built from the
+    // fields above (e.g. a UFS_FILE write to the worker's UFS).
+    std::string command;
   };
   explicit GrpcBlockSink(Options o);
   ~GrpcBlockSink();

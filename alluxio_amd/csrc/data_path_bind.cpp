@@ -252,7 +252,8 @@ void bind_data_path(py::module_& m) {
   py::class_<GrpcBlockSink, std::shared_ptr<GrpcBlockSink>>(m, "GrpcBlockSink")
       .def(py::init([](const std::string& host, int port, int64_t block_id, int tier, const std::string& medium,
                        uint64_t reserve, bool pin, uint64_t chunk, const std::string& channel_id,
-                       const std::string& user, int timeout_ms, const std::string& unix_path) {
+                       const std::string& user, int timeout_ms, const std::string& unix_path,
+                       const py::bytes& command) {
              GrpcBlockSink::Options o;
              o.host = host;
              o.port = port;
@@ -266,6 +267,7 @@ void bind_data_path(py::module_& m) {
              o.channel_id = channel_id;
              o.user = user;
              o.timeout_ms = timeout_ms;
+             o.command = command;
              py::gil_scoped_release rel;
              try {
                return std::make_shared<GrpcBlockSink>(std::move(o));
@@ -278,7 +280,7 @@ void bind_data_path(py::module_& m) {
            py::arg("host"), py::arg("port"), py::arg("block_id"), py::arg("tier") = 0, py::arg("medium") = "",
            py::arg("reserve") = 1u << 20, py::arg("pin") = false, py::arg("chunk") = 1u << 20,
            py::arg("channel_id") = "", py::arg("user") = "", py::arg("timeout_ms") = 60000,
-           py::arg("unix_path") = "")
+           py::arg("unix_path") = "", py::arg("command") = py::bytes(""))
       .def("write_ptr", [](GrpcBlockSink& s, uint64_t ptr, uint64_t n) {
              py::gil_scoped_release rel;
              try {
@@ -360,7 +362,19 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("staged_bytes", [](const DataServerStats& s) { return s.staged_bytes.load(); })
       .def_property_readonly("write_streams", [](const DataServerStats& s) { return s.write_streams.load(); })
       .def_property_readonly("write_declined", [](const DataServerStats& s) { return s.write_declined.load(); })
-      .def_property_readonly("write_bytes", [](const DataServerStats& s) { return s.write_bytes.load(); });
+      .def_property_readonly("write_bytes", [](const DataServerStats& s) { return s.write_bytes.load(); })
+      .def_property_readonly("ufs_write_streams", [](const DataServerStats& s) { return s.ufs_write_streams.load(); })
+      .def_property_readonly("ufs_write_bytes", [](const DataServerStats& s) { return s.ufs_write_bytes.load(); });
+  py::class_<LocalUfsRoots, std::shared_ptr<LocalUfsRoots>>(m, "LocalUfsRoots")
+      .def(py::init<>())
+      .def("set", &LocalUfsRoots::set, py::arg("mount_id"), py::arg("root"))
+      .def("remove", &LocalUfsRoots::remove, py::arg("mount_id"))
+      .def("__len__", &LocalUfsRoots::size)
+      .def("resolve", [](const LocalUfsRoots& r, int64_t mount_id, const std::string& path) -> py::object {
+             std::string local;
+             if (!r.resolve(mount_id, path, &local)) return py::none();
+             return py::str(local);
+           });
   m.def("serve_block_reads", [](FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk,
                                 uint64_t window) {
           auto stats = std::make_shared<DataServerStats>();
@@ -369,10 +383,11 @@ void bind_data_path(py::module_& m) {
         }, py::arg("server"), py::arg("method"), py::arg("store"), py::arg("max_chunk"), py::arg("window"),
         py::keep_alive<1, 3>());
   m.def("serve_block_writes", [](FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
-                                 uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats) {
-          serve_block_writes(srv, method, commit_method, store, stage_bytes, stats);
+                                 uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
+                                 std::shared_ptr<LocalUfsRoots> ufs_roots) {
+          serve_block_writes(srv, method, commit_method, store, stage_bytes, stats, ufs_roots);
         }, py::arg("server"), py::arg("method"), py::arg("commit_method"), py::arg("store"), py::arg("stage_bytes"),
-        py::arg("stats"), py::keep_alive<1, 4>());
+        py::arg("stats"), py::arg("ufs_roots") = nullptr, py::keep_alive<1, 4>());
   m.def("stream_recv", [](FrameRpcServer& srv, uint64_t token, int timeout_ms) -> py::tuple {
           std::string msg;
           int rc;

@@ -3,9 +3,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <random>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -237,10 +243,13 @@ std::atomic<int64_t> g_session{(int64_t)1 << 62};   // above the Python range (u
 // WriteRequestCommand (proto/defs/block.py): type=1 id=2 offset=3 tier=4 flush=5
 // create_ufs_file_options=6 create_ufs_block_options=7 medium_type=8 pin_on_create=9
 // space_to_reserve=10.  WriteRequest: command=1 chunk=2 (Chunk: data=1).
+// CreateUfsFileOptions (proto/defs/common.py): ufs_path=1 owner=2 group=3 mode=4 mount_id=5 acl=6.
 struct WriteCmd {
   int64_t type = 0, id = 0, offset = 0, tier = 0, reserve = 0;
-  bool has_tier = false, flush = false, pin = false, has_ufs = false;
+  bool has_tier = false, flush = false, pin = false, has_ufs = false, has_ufs_file = false;
   std::string medium;
+  std::string ufs_path;
+  int64_t ufs_mode = 0, ufs_mount = 0;
 };
 
 bool skip_field(const uint8_t* p, size_t n, size_t* i, uint32_t wt) {
@@ -257,6 +266,29 @@ bool skip_field(const uint8_t* p, size_t n, size_t* i, uint32_t wt) {
   if (wt == 1 && n - *i >= 8) { *i += 8; return true; }
   if (wt == 5 && n - *i >= 4) { *i += 4; return true; }
   return false;
+}
+
+bool parse_ufs_file_options(const uint8_t* p, size_t n, WriteCmd* c) {
+  size_t i = 0;
+  while (i < n) {
+    uint64_t key;
+    if (!h2::get_varint(p, n, &i, &key)) return false;
+    const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (wt == 0 && (field == 4 || field == 5)) {
+      uint64_t v;
+      if (!h2::get_varint(p, n, &i, &v)) return false;
+      if (field == 4) c->ufs_mode = (int64_t)(int32_t)v;
+      else c->ufs_mount = (int64_t)v;
+    } else if (wt == 2 && field == 1) {
+      uint64_t len;
+      if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
+      c->ufs_path.assign(reinterpret_cast<const char*>(p + i), (size_t)len);
+      i += (size_t)len;
+    } else if (!skip_field(p, n, &i, wt)) {
+      return false;
+    }
+  }
+  return true;
 }
 
 bool parse_write_command(const uint8_t* p, size_t n, WriteCmd* c) {
@@ -282,6 +314,10 @@ bool parse_write_command(const uint8_t* p, size_t n, WriteCmd* c) {
       uint64_t len;
       if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
       if (field == 6 || field == 7) c->has_ufs = true;
+      if (field == 6) {
+        c->has_ufs_file = true;
+        if (!parse_ufs_file_options(p + i, (size_t)len, c)) return false;
+      }
       if (field == 8) c->medium.assign(reinterpret_cast<const char*>(p + i), (size_t)len);
       i += (size_t)len;
     } else if (!skip_field(p, n, &i, wt)) {
@@ -359,7 +395,42 @@ std::string write_response_frame(uint64_t offset) {
   return f;
 }
 
-class BlockWriteStream : public NativeStream {
+// Response side shared by the write streams: queued WriteResponse frames, then EOF or a failure.
+class WriteStreamBase : public NativeStream {
+ public:
+  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    if (err_) {
+      *status = err_status_;
+      *msg = err_msg_;
+      return -1;
+    }
+    const size_t n = std::min(max, out_.size() - out_off_);
+    std::memcpy(dst, out_.data() + out_off_, n);
+    out_off_ += n;
+    if (out_off_ == out_.size()) {
+      out_.clear();
+      out_off_ = 0;
+      if (done_) *eof = true;
+    }
+    return (ssize_t)n;
+  }
+
+ protected:
+  void fail(int status, const std::string& msg) {
+    if (err_) return;
+    err_ = true;
+    err_status_ = status;
+    err_msg_ = msg;
+  }
+
+  std::string out_;
+  size_t out_off_ = 0;
+  bool ended_ = false, done_ = false, err_ = false;
+  int err_status_ = 0;
+  std::string err_msg_;
+};
+
+class BlockWriteStream : public WriteStreamBase {
  public:
   BlockWriteStream(BlockStore* store, int64_t session, int64_t block_id, uint64_t pos, bool pin, bool device,
                    uint32_t commit_method, std::shared_ptr<StagingPool> pool, std::shared_ptr<DataServerStats> stats)
@@ -427,31 +498,7 @@ class BlockWriteStream : public NativeStream {
     done_ = true;
   }
 
-  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
-    if (err_) {
-      *status = err_status_;
-      *msg = err_msg_;
-      return -1;
-    }
-    const size_t n = std::min(max, out_.size() - out_off_);
-    std::memcpy(dst, out_.data() + out_off_, n);
-    out_off_ += n;
-    if (out_off_ == out_.size()) {
-      out_.clear();
-      out_off_ = 0;
-      if (done_) *eof = true;
-    }
-    return (ssize_t)n;
-  }
-
  private:
-  void fail(int status, const std::string& msg) {
-    if (err_) return;
-    err_ = true;
-    err_status_ = status;
-    err_msg_ = msg;
-  }
-
   void write(const uint8_t* p, size_t n) {
     if (!device_) {       // host arena / file dir: straight from the HTTP/2 receive buffer
       store_->write(session_, block_, pos_, reinterpret_cast<uint64_t>(p), n, (int)MemKind::kHost, 0, true);
@@ -479,14 +526,168 @@ class BlockWriteStream : public NativeStream {
   std::shared_ptr<StagingPool> pool_;
   std::shared_ptr<DataServerStats> stats_;
   uint8_t* stage_ = nullptr;
-  std::string out_;
-  size_t out_off_ = 0;
-  bool ended_ = false, done_ = false, err_ = false;
-  int err_status_ = 0;
-  std::string err_msg_;
+};
+
+int grpc_status_of_errno(int e) {
+  switch (e) {
+    case ENOSPC:
+    case EDQUOT: return 8;                    // RESOURCE_EXHAUSTED
+    case EACCES:
+    case EPERM:
+    case EROFS: return 7;                     // PERMISSION_DENIED
+    case EEXIST: return 6;                    // ALREADY_EXISTS
+    case ENOENT:
+    case ENOTDIR: return 5;                   // NOT_FOUND
+    default: return 13;                       // INTERNAL
+  }
+}
+
+// mkdir -p of the directories above `path` (os.makedirs(parent, exist_ok=True) of the local UFS).
+bool make_parents(const std::string& path, int* err) {
+  for (size_t i = path.find('/', 1); i != std::string::npos; i = path.find('/', i + 1)) {
+    const std::string dir = path.substr(0, i);
+    if (::mkdir(dir.c_str(), 0777) != 0 && errno != EEXIST) {
+      *err = errno;
+      return false;
+    }
+  }
+  return true;
+}
+
+// UFS_FILE WriteBlock into a local-directory UFS: chunks are written to a temp file beside the
+// target on the I/O thread; the half-close sets the mode and renames it over the target (the
+// local UFS's atomic create, underfs/local.py _AtomicWriter).  A failed or cancelled call
+// removes the temp file and leaves the target untouched.
+class UfsFileWriteStream : public WriteStreamBase {
+ public:
+  UfsFileWriteStream(const std::string& path, int mode, std::shared_ptr<DataServerStats> stats)
+      : path_(path), mode_(mode), stats_(std::move(stats)) {}
+
+  // Creates the parents and the temp file; false with *status / *msg set on failure.
+  bool open(int* status, std::string* msg) {
+    int e = 0;
+    if (!make_parents(path_, &e)) {
+      *status = grpc_status_of_errno(e);
+      *msg = "creating the parent of " + path_ + ": " + std::strerror(e);
+      return false;
+    }
+    thread_local std::mt19937_64 rng(std::random_device{}());
+    char tag[17];
+    std::snprintf(tag, sizeof(tag), "%08x", (unsigned)(rng() & 0xffffffffu));
+    tmp_ = path_ + ".alluxio." + tag + ".tmp";
+    fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0666);
+    if (fd_ < 0) {
+      e = errno;
+      *status = grpc_status_of_errno(e);
+      *msg = "creating " + tmp_ + ": " + std::strerror(e);
+      return false;
+    }
+    return true;
+  }
+
+  ~UfsFileWriteStream() override {
+    if (fd_ >= 0) ::close(fd_);
+    if (!committed_ && !tmp_.empty()) ::unlink(tmp_.c_str());
+  }
+
+  void on_message(const char* p, size_t n) override {
+    if (err_ || ended_) return;
+    WriteCmd cmd;
+    bool has_cmd;
+    const uint8_t* chunk;
+    size_t len;
+    if (!parse_write_request(p, n, &cmd, &has_cmd, &chunk, &len)) {
+      fail(3, "malformed WriteRequest");
+      return;
+    }
+    size_t done = 0;
+    while (done < len) {
+      const ssize_t w = ::write(fd_, chunk + done, len - done);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        const int e = errno;
+        fail(grpc_status_of_errno(e), "writing " + path_ + ": " + std::strerror(e));
+        return;
+      }
+      done += (size_t)w;
+    }
+    pos_ += len;
+    stats_->ufs_write_bytes.fetch_add(len, std::memory_order_relaxed);
+    if (has_cmd && cmd.flush) out_ += write_response_frame(pos_);
+  }
+
+  bool on_end(uint32_t*, std::string*) override {
+    ended_ = true;
+    if (err_) return false;
+    const int fd = fd_;
+    fd_ = -1;
+    int e = 0;
+    if (::fchmod(fd, (mode_t)mode_) != 0) e = errno;
+    if (::close(fd) != 0 && !e) e = errno;
+    if (!e && ::rename(tmp_.c_str(), path_.c_str()) != 0) e = errno;
+    if (e) {
+      fail(grpc_status_of_errno(e), "completing " + path_ + ": " + std::strerror(e));
+      return false;
+    }
+    committed_ = true;
+    out_ += write_response_frame(pos_);
+    done_ = true;
+    return false;
+  }
+
+ private:
+  std::string path_, tmp_;
+  int mode_;
+  int fd_ = -1;
+  uint64_t pos_ = 0;
+  bool committed_ = false;
+  std::shared_ptr<DataServerStats> stats_;
 };
 
 }  // namespace
+
+namespace {
+std::string strip_file_scheme(const std::string& p) { return p.compare(0, 7, "file://") == 0 ? p.substr(7) : p; }
+}  // namespace
+
+void LocalUfsRoots::set(int64_t mount_id, const std::string& root) {
+  std::string r = strip_file_scheme(root);
+  while (!r.empty() && r.back() == '/') r.pop_back();     // "/" -> "" (every absolute path)
+  std::lock_guard<std::mutex> g(mu_);
+  roots_[mount_id] = r;
+}
+
+void LocalUfsRoots::remove(int64_t mount_id) {
+  std::lock_guard<std::mutex> g(mu_);
+  roots_.erase(mount_id);
+}
+
+size_t LocalUfsRoots::size() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return roots_.size();
+}
+
+bool LocalUfsRoots::resolve(int64_t mount_id, const std::string& ufs_path, std::string* local) const {
+  std::string root;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = roots_.find(mount_id);
+    if (it == roots_.end()) return false;
+    root = it->second;
+  }
+  const std::string p = strip_file_scheme(ufs_path);
+  if (p.size() < 2 || p[0] != '/') return false;
+  for (size_t i = 1; i <= p.size();) {                     // no empty, "." or ".." component
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    const size_t n = j - i;
+    if (n == 0 || (n == 1 && p[i] == '.') || (n == 2 && p[i] == '.' && p[i + 1] == '.')) return false;
+    i = j + 1;
+  }
+  if (p.size() <= root.size() + 1 || p.compare(0, root.size(), root) != 0 || p[root.size()] != '/') return false;
+  *local = p;
+  return true;
+}
 
 void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk, uint64_t window,
                        std::shared_ptr<DataServerStats> stats) {
@@ -555,7 +756,8 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
 }
 
 void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
-                        uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats) {
+                        uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
+                        std::shared_ptr<LocalUfsRoots> ufs_roots) {
   if (stage_bytes == 0) stage_bytes = 4u << 20;
   auto pool = std::make_shared<StagingPool>(stage_bytes, store->has_device());
   FrameRpcServer* s = &srv;
@@ -577,7 +779,16 @@ void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_me
       *msg = cid.empty() ? "channel is not authenticated (no channel-id)" : "channel " + cid + " is not authenticated";
       return nullptr;
     }
-    if (cmd.type != 0 || cmd.has_ufs || cmd.offset < 0) {   // UFS_FILE / UFS_FALLBACK_BLOCK: Python
+    std::string local;
+    if (cmd.type == 1 && cmd.has_ufs_file && ufs_roots && ufs_roots->resolve(cmd.ufs_mount, cmd.ufs_path, &local)) {
+      auto us = std::unique_ptr<UfsFileWriteStream>(
+          new UfsFileWriteStream(local, cmd.ufs_mode > 0 ? (int)(cmd.ufs_mode & 07777) : 0644, stats));
+      if (!us->open(status, msg)) return nullptr;
+      stats->ufs_write_streams.fetch_add(1, std::memory_order_relaxed);
+      if (len) us->on_message(first.data(), first.size());
+      return us;
+    }
+    if (cmd.type != 0 || cmd.has_ufs || cmd.offset < 0) {   // other UFS_FILE / UFS_FALLBACK_BLOCK: Python
       stats->write_declined.fetch_add(1, std::memory_order_relaxed);
       return nullptr;
     }

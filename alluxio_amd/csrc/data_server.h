@@ -18,6 +18,9 @@
 #include <atomic>
 #include <cstdint>
 #include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
 
 #include "block_store.h"
 #include "frame_rpc.h"
@@ -34,6 +37,25 @@ struct DataServerStats {
   std::atomic<uint64_t> write_streams{0};  // WriteBlock calls served natively
   std::atomic<uint64_t> write_declined{0}; // WriteBlock calls handed to Python (UFS / fallback)
   std::atomic<uint64_t> write_bytes{0};    // block bytes written natively
+  std::atomic<uint64_t> ufs_write_streams{0};  // UFS_FILE writes into a local UFS served natively
+  std::atomic<uint64_t> ufs_write_bytes{0};
+};
+
+// Mounts whose UFS is a local directory, so a UFS_FILE WriteBlock can be written by the I/O
+// thread with plain file calls.  The worker registers a mount once its Python side has resolved
+// it to the local UFS (worker/block_worker.py); other mounts (S3, HDFS, ...) stay in Python.
+class LocalUfsRoots {
+ public:
+  void set(int64_t mount_id, const std::string& root);
+  void remove(int64_t mount_id);
+  size_t size() const;
+  // The local path of `ufs_path` ("file:///x" or "/x") if mount `mount_id` is registered and the
+  // path lies inside its root without "." / ".." components.
+  bool resolve(int64_t mount_id, const std::string& ufs_path, std::string* local) const;
+
+ private:
+  mutable std::mutex mu_;
+  std::unordered_map<int64_t, std::string> roots_;
 };
 
 // Serve `method` (the ReadBlock path's index) of `srv` from `store`.  `max_chunk` caps a client's
@@ -46,8 +68,12 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
 // pinned staging buffer and an async H2D on the thread's stream), flush commands are answered
 // with the offset; at the client's half-close the commit -- CRC, master report -- runs in Python
 // as the internal unary `commit_method` (NativeWriteCommitRequest) whose reply ends the call.
-// UFS_FILE / UFS_FALLBACK_BLOCK writes go to the Python servicer.
+// UFS_FILE writes under a mount of `ufs_roots` (may be null) are written natively too: a temp
+// file beside the target, renamed over it at the half-close (reference UfsFileWriteHandler.java
+// with the local UFS's AtomicFileOutputStream).  Other UFS_FILE and UFS_FALLBACK_BLOCK writes go
+// to the Python servicer.
 void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
-                        uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats);
+                        uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
+                        std::shared_ptr<LocalUfsRoots> ufs_roots = nullptr);
 
 }  // namespace amdx

@@ -66,6 +66,8 @@ class BlockWorker:
         self.metrics = msys.metrics("Worker")
         self._ufs_resolver = ufs_resolver
         self._ufs_cache: dict[int, object] = {}
+        self._ufs_uris: dict[int, str] = {}     # mount id -> mount point URI in the UFS
+        self.native_ufs_roots = None             # csrc LocalUfsRoots of the native data server
         self._sessions: dict[int, float] = {}
         self._session_lock = threading.Lock()
         self._async_inflight: set[int] = set()
@@ -343,9 +345,23 @@ class BlockWorker:
             if fsm is not None and opts.mountId:
                 info = fsm.GetUfsInfo(pb.file.GetUfsInfoPRequest(mountId=opts.mountId)).ufsInfo
                 props = dict(info.properties.properties)
+                if info.uri:
+                    self._ufs_uris[opts.mountId] = info.uri
             u = registry.create(opts.ufs_path, self.conf, props)
             self._ufs_cache[opts.mountId] = u
         return u
+
+    def note_local_ufs(self, mount_id: int, ufs) -> None:
+        """After a UFS_FILE write through Python: a mount whose UFS is a plain local directory is
+        registered with the native data server, which then writes that mount's UFS_FILE streams on
+        its I/O threads (csrc/data_server.cpp UfsFileWriteStream)."""
+        from ..underfs.local import LocalUnderFileSystem
+        roots = self.native_ufs_roots
+        uri = self._ufs_uris.get(mount_id)
+        if roots is None or uri is None or type(ufs) is not LocalUnderFileSystem:
+            return
+        if roots.resolve(mount_id, uri.rstrip("/") + "/x") is None:
+            roots.set(mount_id, uri)
 
     def ufs_block_target(self, mount_id: int, block_id: int):
         """(UFS, path) of the UFS block file of ``block_id`` under mount ``mount_id``

@@ -9,7 +9,9 @@ read lock for the call, HBM chunks DMA'd into pinned staging, ``offset_received`
 are the chunks of an ALLUXIO_BLOCK ``WriteBlock`` (written into the temp block as they arrive; the
 commit -- CRC32C, the master's CommitBlock -- runs in Python as the internal ``NativeWriteCommit``
 call posted at the client's half-close, whose reply ends the stream; reference
-BlockWriteHandler.java).  Every other BlockWorker call -- UFS writes and read-through,
+BlockWriteHandler.java), and so are UFS_FILE writes into a mount the worker has found to be a
+local directory (temp file renamed over the target at the half-close; reference
+UfsFileWriteHandler.java).  Every other BlockWorker call -- UFS writes and read-through,
 OpenLocalBlock, AsyncCache, ... -- runs the same Python servicer as the grpcio port, through the
 front end's streaming bridge.  The port is
 advertised as ``WorkerNetAddress.dataPort``; clients stream block bytes from it
@@ -56,11 +58,15 @@ class WorkerDataServer:
             conf.get_bytes("alluxio.worker.network.reader.max.chunk.size.bytes", "2MB"),
             conf.get_bytes("alluxio.worker.network.reader.buffer.size", "4MB"))
         # WriteBlock of ALLUXIO_BLOCK writes: chunks into the store on the I/O threads, the commit
-        # (CRC, master report) as the internal NativeWriteCommit call (BlockWorkerService)
+        # (CRC, master report) as the internal NativeWriteCommit call (BlockWorkerService).
+        # UFS_FILE writes of mounts the worker found to be local directories: into the file.
+        self.ufs_roots = lib().LocalUfsRoots()
+        if conf.get_bool("alluxio.worker.data.server.native.ufs.write.enabled", "true"):
+            worker.native_ufs_roots = self.ufs_roots
         lib().serve_block_writes(
             self.frontend.server, self.frontend.method_index(WRITE_BLOCK_PATH),
             self.frontend.method_index(COMMIT_PATH), worker.native,
-            conf.get_bytes("alluxio.worker.network.writer.staging.size", "4MB"), self.stats)
+            conf.get_bytes("alluxio.worker.network.writer.staging.size", "4MB"), self.stats, self.ufs_roots)
         self.port = None
 
     def start(self) -> int:
@@ -76,6 +82,8 @@ class WorkerDataServer:
         m.counter("BytesReadRemote").add_source(lambda: st.bytes - st.domain_bytes)
         m.counter("BytesWrittenAlluxio").add_source(lambda: st.write_bytes)
         m.gauge("DataServerNativeWriteStreams", lambda: st.write_streams)
+        m.gauge("DataServerNativeUfsWriteStreams", lambda: st.ufs_write_streams)
+        m.counter("BytesWrittenUfsAll").add_source(lambda: st.ufs_write_bytes)
         return self.port
 
     def stop(self) -> None:

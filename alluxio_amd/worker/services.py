@@ -286,6 +286,7 @@ class BlockWorkerService:
                 except Exception:  # noqa: BLE001
                     pass
         self.w.metrics.counter("BytesWrittenUfsAll").inc(pos)
+        self.w.note_local_ufs(o.mount_id, ufs)
         yield pb.block.WriteResponse(offset=pos)
 
     # ------------------------------------------------------------------------------------------

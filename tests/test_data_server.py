@@ -303,6 +303,82 @@ def test_native_writer_over_data_port(tmp_path):
             rfs.close()
 
 
+def test_native_ufs_file_writes(tmp_path):
+    """THROUGH / CACHE_THROUGH from a remote client: the first UFS_FILE stream of a mount runs in
+    Python, which registers the local-directory mount; later streams are written by the native
+    server (temp file renamed over the target).  Paths outside the mount stay in Python."""
+    import os
+    with _cluster(tmp_path) as c:
+        w = c.workers[0]
+        st = w.data_server.stats
+        rfs = _remote_fs(c)
+        try:
+            rng = np.random.default_rng(11)
+            first = rng.integers(0, 256, (3 << 20) + 1, dtype=np.uint8)
+            rfs.write_file("/t/first", first, write_type="THROUGH")
+            assert st.ufs_write_streams == 0                 # Python servicer, mount registered
+            assert len(w.data_server.ufs_roots) == 1
+            data = rng.integers(0, 256, (9 << 20) + 7, dtype=np.uint8)
+            rfs.write_file("/t/second", data, write_type="THROUGH")
+            rfs.write_file("/t/deep/third", data[:12345], write_type="CACHE_THROUGH")
+            assert st.ufs_write_streams == 2
+            assert st.ufs_write_bytes == data.nbytes + 12345
+            with open(os.path.join(c.ufs_root, "t", "second"), "rb") as f:
+                assert f.read() == data.tobytes()
+            assert rfs.read_file("/t/deep/third") == data[:12345].tobytes()
+            assert rfs.read_file("/t/first") == first.tobytes()
+            assert not [n for n in os.listdir(os.path.join(c.ufs_root, "t")) if n.endswith(".tmp")]
+            assert rfs.get_status("/t/second").is_persisted
+            # the root confinement of the native path
+            roots = w.data_server.ufs_roots
+            mid = rfs.get_status("/t/second").mountId
+            assert roots.resolve(mid, os.path.join(c.ufs_root, "t", "x")) is not None
+            assert roots.resolve(mid, "file://" + os.path.join(c.ufs_root, "t", "x")) is not None
+            assert roots.resolve(mid, os.path.join(c.ufs_root, "..", "x")) is None
+            assert roots.resolve(mid, "/etc/passwd") is None
+            assert roots.resolve(mid + 1000, os.path.join(c.ufs_root, "x")) is None
+        finally:
+            rfs.close()
+
+
+def test_native_ufs_file_write_cancel_leaves_no_file(tmp_path):
+    import os
+    from alluxio_amd.proto import pb as _pb
+    with _cluster(tmp_path) as c:
+        w = c.workers[0]
+        root = c.ufs_root
+        w.data_server.ufs_roots.set(77, root)
+        C = lib()
+        target = os.path.join(root, "x", "cancelled")
+        cmd = _pb.block.WriteRequestCommand(type=1, id=5, create_ufs_file_options=_pb.dataserver.CreateUfsFileOptions(
+            ufs_path=target, mount_id=77, mode=0o600))
+        data = np.random.default_rng(12).integers(0, 256, 2 << 20, dtype=np.uint8)
+        s = C.GrpcBlockSink("127.0.0.1", w.data_server.port, 5, command=cmd.SerializeToString())
+        s.write_ptr(data.ctypes.data, data.nbytes)
+        s.cancel()
+        deadline = time.time() + 5
+        while os.listdir(os.path.join(root, "x")):
+            assert time.time() < deadline
+            time.sleep(0.05)
+        assert not os.path.exists(target)
+        s = C.GrpcBlockSink("127.0.0.1", w.data_server.port, 5, command=cmd.SerializeToString())
+        s.write_ptr(data.ctypes.data, data.nbytes)
+        assert s.commit() == data.nbytes
+        assert os.stat(target).st_mode & 0o777 == 0o600
+        with open(target, "rb") as f:
+            assert f.read() == data.tobytes()
+        # a path outside the registered root is not written natively: the Python servicer
+        # (UfsFileWriteHandler's behavior) takes the call
+        bad = cmd.__class__.FromString(cmd.SerializeToString())
+        bad.create_ufs_file_options.ufs_path = os.path.join(str(tmp_path), "outside")
+        n0, d0 = w.data_server.stats.ufs_write_streams, w.data_server.stats.write_declined
+        s = C.GrpcBlockSink("127.0.0.1", w.data_server.port, 6, command=bad.SerializeToString())
+        s.write_ptr(data.ctypes.data, 1024)
+        s.commit()
+        assert w.data_server.stats.ufs_write_streams == n0
+        assert w.data_server.stats.write_declined == d0 + 1
+
+
 def test_native_write_errors_and_cancel(tmp_path):
     with _cluster(tmp_path) as c:
         w = c.workers[0]

@@ -30,17 +30,17 @@ from alluxio_amd.client.file_system import FileSystem
 from alluxio_amd.conf import Configuration
 conf = Configuration({props!r})
 fs = FileSystem(conf=conf, master_address={addr!r})
-size, nfiles, threads, wsize, tag = {size}, {nfiles}, {threads}, {wsize}, {tag!r}
+size, nfiles, threads, wsize, tag, wtype = {size}, {nfiles}, {threads}, {wsize}, {tag!r}, {wtype!r}
 data = np.random.default_rng(1).integers(0, 256, wsize, dtype=np.uint8)
 fs.create_directory("/ww", recursive=True, allow_exists=True)
-with fs.create_file(f"/ww/{{tag}}-warm", write_type="MUST_CACHE") as f:
+with fs.create_file(f"/ww/{{tag}}-warm", write_type=wtype) as f:
     f.write(data)
 done = [0] * threads
 errs = []
 def run(t):
     try:
         for k in range(nfiles):
-            with fs.create_file(f"/ww/{{tag}}-{{t}}-{{k}}", write_type="MUST_CACHE") as f:
+            with fs.create_file(f"/ww/{{tag}}-{{t}}-{{k}}", write_type=wtype) as f:
                 left = size
                 while left > 0:
                     n = min(wsize, left)
@@ -69,6 +69,8 @@ def main(argv=None) -> int:
     ap.add_argument("--tier", default=None, help="worker MEM tier (default hbm:0 with a GPU, else dram)")
     ap.add_argument("--transports", default="grpc", help="grpc (WriteBlock on the data port) and/or ipc "
                     "(short-circuit: the worker's arena mapped into the writer, OpenDeviceWrite)")
+    ap.add_argument("--write-type", default="MUST_CACHE", help="MUST_CACHE, CACHE_THROUGH or THROUGH "
+                    "(the UFS is a local directory under the work dir)")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
@@ -84,7 +86,7 @@ def main(argv=None) -> int:
             "alluxio.worker.hbm.page.size": "2MB",
             "alluxio.user.block.size.bytes.default": a.block_size,
             "alluxio.security.authorization.permission.enabled": "false",
-            "alluxio.worker.tieredstore.dram.prefault": "true"}
+            "alluxio.worker.tieredstore.dram.prefault": str(a.write_type != "THROUGH").lower()}
     work = tempfile.mkdtemp(prefix="wwbench_")
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=work) as c:
         time.sleep(min(10.0, total / 4e9))     # let the DRAM prefault finish (no-op on HBM)
@@ -96,13 +98,13 @@ def main(argv=None) -> int:
             props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             p = subprocess.run([sys.executable, "-c", CLIENT.format(
                 root=ROOT, props=props, addr=c.master.address, size=size, nfiles=a.files, threads=int(t),
-                wsize=parse_space_size(a.write_size), tag=f"r{i}")], capture_output=True, text=True, timeout=900)
+                wsize=parse_space_size(a.write_size), tag=f"r{i}", wtype=a.write_type)], capture_output=True, text=True, timeout=900)
             line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
             if line is None:
                 print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
                 return 1
             r = json.loads(line[7:])
-            row = {"bench": "host writers, separate client process (MUST_CACHE)", "transport": transport, "tier": tier,
+            row = {"bench": f"host writers, separate client process ({a.write_type})", "transport": transport, "tier": tier,
                    "threads": int(t), "files_per_thread": a.files, "file_size": a.file_size,
                    "write_size": a.write_size, "bytes": r["bytes"], "seconds": round(r["seconds"], 3),
                    "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3), "errors": r["errors"],
