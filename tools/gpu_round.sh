@@ -140,6 +140,11 @@ for s in $STEPS; do
       run worker_write_bench 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --transports grpc,ipc --out "$OUT/worker_write_bench.jsonl"
       run wb_host_after_writes 600 python tools/worker_bench_host.py --threads 16,256 --transports grpc,ipc --duration 6s --warmup 2s --out "$OUT/worker_bench_host_r4b.jsonl"
       ;;
+    through)
+      run ww_through 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type THROUGH --out "$OUT/worker_write_through.jsonl"
+      run ww_cache_through 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/worker_write_through.jsonl"
+      run ww_through_python 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type THROUGH --client-prop alluxio.user.native.writer.enabled=false --worker-prop alluxio.worker.data.server.native.ufs.write.enabled=false --out "$OUT/worker_write_through.jsonl"
+      ;;
     writebase)
       run worker_write_bench_grpcio 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --transports grpc --client-prop alluxio.user.native.writer.enabled=false --out "$OUT/worker_write_bench_grpcio.jsonl"
       ;;

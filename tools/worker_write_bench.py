@@ -72,6 +72,7 @@ def main(argv=None) -> int:
     ap.add_argument("--write-type", default="MUST_CACHE", help="MUST_CACHE, CACHE_THROUGH or THROUGH "
                     "(the UFS is a local directory under the work dir)")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
+    ap.add_argument("--worker-prop", action="append", default=[], help="extra worker property k=v")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import torch
@@ -87,6 +88,7 @@ def main(argv=None) -> int:
             "alluxio.user.block.size.bytes.default": a.block_size,
             "alluxio.security.authorization.permission.enabled": "false",
             "alluxio.worker.tieredstore.dram.prefault": str(a.write_type != "THROUGH").lower()}
+    conf.update(dict(kv.split("=", 1) for kv in a.worker_prop))
     work = tempfile.mkdtemp(prefix="wwbench_")
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=work) as c:
         time.sleep(min(10.0, total / 4e9))     # let the DRAM prefault finish (no-op on HBM)
@@ -108,7 +110,7 @@ def main(argv=None) -> int:
                    "threads": int(t), "files_per_thread": a.files, "file_size": a.file_size,
                    "write_size": a.write_size, "bytes": r["bytes"], "seconds": round(r["seconds"], 3),
                    "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3), "errors": r["errors"],
-                   "client_props": a.client_prop}
+                   "client_props": a.client_prop, "worker_props": a.worker_prop}
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
