@@ -68,6 +68,40 @@ def _iso(ms: int) -> str:
     return time.strftime("%Y-%m-%dT%H:%M:%S.000Z", time.gmtime(ms / 1000.0))
 
 
+class _Md5Beside:
+    """The ETag MD5 of an uploaded body, computed on a helper thread while the chunks are written
+    into Alluxio (hashlib drops the GIL on large updates), so a PUT takes max(MD5, write) rather
+    than their sum.  MD5 itself is serial, ~0.7 GB/s per object."""
+
+    def __init__(self):
+        import queue
+        self._md5 = hashlib.md5()
+        self._q: queue.Queue = queue.Queue(maxsize=4)
+        self._t = None
+
+    def _run(self):
+        while True:
+            c = self._q.get()
+            if c is None:
+                return
+            self._md5.update(c)
+
+    def chunks(self, body_iter):
+        self._t = threading.Thread(target=self._run, name="s3-md5", daemon=True)
+        self._t.start()
+        try:
+            for c in body_iter:
+                self._q.put(c)          # rfile.read returns a fresh bytes object per chunk
+                yield c
+        finally:
+            self._q.put(None)
+
+    def hexdigest(self) -> str:
+        if self._t is not None:
+            self._t.join()
+        return self._md5.hexdigest()
+
+
 class S3Handler:
     """S3 semantics over an Alluxio FileSystem client."""
 
@@ -224,13 +258,8 @@ class S3Handler:
             st = self.fs.get_status(path)
             return 200, {}, _xml("CopyObjectResult", [("LastModified", _iso(st.info.lastModificationTimeMs)),
                                                       ("ETag", f'"{_etag(st)}"')])
-        md5 = hashlib.md5()
-
-        def chunks():
-            for c in body_iter:
-                md5.update(c)
-                yield c
-        self._write(path, chunks())
+        md5 = _Md5Beside()
+        self._write(path, md5.chunks(body_iter))
         return 200, {"ETag": f'"{md5.hexdigest()}"'}, b""
 
     def _stat_object(self, bucket, key):
@@ -326,13 +355,8 @@ class S3Handler:
         d = self._mp_dir(p, key, upload_id)
         if not self.fs.exists(d):
             raise S3Error(404, "NoSuchUpload", "The specified upload does not exist.", key)
-        md5 = hashlib.md5()
-
-        def chunks():
-            for c in body_iter:
-                md5.update(c)
-                yield c
-        self._write(f"{d}/{part:05d}", chunks())
+        md5 = _Md5Beside()
+        self._write(f"{d}/{part:05d}", md5.chunks(body_iter))
         return 200, {"ETag": f'"{md5.hexdigest()}"'}, b""
 
     def list_parts(self, bucket, key, upload_id):
