@@ -995,6 +995,7 @@ class FileOutStream(io.RawIOBase):
         self._block_written = 0
         self._pos = 0
         self._ufs = None
+        self._beside = None          # helper thread of CACHE_THROUGH's UFS writes
         self._canceled = False
         self._workers = None
         if self.through:
@@ -1021,19 +1022,20 @@ class FileOutStream(io.RawIOBase):
                 host = keep.detach().reshape(-1).view(torch.uint8).cpu().numpy()
             else:
                 host = _host_view(ptr, n)        # zero-copy view of the caller's buffer
-            if self.cache and n >= (4 << 20) and kind != DEVICE:
-                # CACHE_THROUGH: the UFS write (a syscall that drops the GIL, or frames for a worker)
-                # runs beside the copy into the cache tier; both finish before write() returns,
-                # so the caller's buffer is not used afterwards
-                t = threading.Thread(target=self._ufs_write_bg, args=(host,), daemon=True)
-                self._ufs_err = None
-                t.start()
+            if self.cache and n >= (256 << 10) and kind != DEVICE:
+                # CACHE_THROUGH: the UFS write (a native stream or a syscall, both without the
+                # GIL) runs on this stream's helper thread beside the copy into the cache tier;
+                # both finish before write() returns, so the caller's buffer is not used afterwards
+                if self._beside is None:
+                    from concurrent.futures import ThreadPoolExecutor
+                    self._beside = ThreadPoolExecutor(max_workers=1, thread_name_prefix="ufs-write")
+                fut = self._beside.submit(self._ufs.write, host)
                 try:
                     self._write_cache(ptr, n, kind)
                 finally:
-                    t.join()
-                if self._ufs_err is not None:
-                    raise self._ufs_err
+                    err = fut.exception()
+                if err is not None:
+                    raise err
                 self._pos += n
                 return n
             self._ufs.write(host)
@@ -1041,12 +1043,6 @@ class FileOutStream(io.RawIOBase):
             self._write_cache(ptr, n, kind)
         self._pos += n
         return n
-
-    def _ufs_write_bg(self, host) -> None:
-        try:
-            self._ufs.write(host)
-        except BaseException as e:  # noqa: BLE001 - re-raised on the writing thread
-            self._ufs_err = e
 
     def _write_cache(self, ptr, n, kind):
         done = 0
@@ -1136,8 +1132,14 @@ class FileOutStream(io.RawIOBase):
             if errors:
                 raise UnavailableException(f"replicating block {self._block_id} failed: {errors}")
 
+    def _stop_beside(self) -> None:
+        if self._beside is not None:
+            self._beside.shutdown(wait=False)
+            self._beside = None
+
     def cancel(self) -> None:
         self._canceled = True
+        self._stop_beside()
         for w in self._writers:
             w.cancel()
         self._writers = []
@@ -1155,6 +1157,7 @@ class FileOutStream(io.RawIOBase):
             return
         if self._canceled:
             return
+        self._stop_beside()
         try:
             self._finish_block()
             opts = pb.file.CompleteFilePOptions()

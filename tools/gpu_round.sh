@@ -145,6 +145,9 @@ for s in $STEPS; do
       run ww_cache_through 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/worker_write_through.jsonl"
       run ww_through_python 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type THROUGH --client-prop alluxio.user.native.writer.enabled=false --worker-prop alluxio.worker.data.server.native.ufs.write.enabled=false --out "$OUT/worker_write_through.jsonl"
       ;;
+    cthrough)
+      run ww_cache_through2 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/worker_write_through.jsonl"
+      ;;
     writebase)
       run worker_write_bench_grpcio 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --transports grpc --client-prop alluxio.user.native.writer.enabled=false --out "$OUT/worker_write_bench_grpcio.jsonl"
       ;;
