@@ -341,6 +341,30 @@ def test_native_ufs_file_writes(tmp_path):
             rfs.close()
 
 
+def test_cache_through_ufs_error_surfaces_from_helper_thread(tmp_path):
+    """CACHE_THROUGH runs the UFS write beside the cache write on a helper thread: its failure
+    is raised by write(), after both have finished with the caller's buffer."""
+    with _cluster(tmp_path) as c:
+        rfs = _remote_fs(c)
+        try:
+            data = np.random.default_rng(13).integers(0, 256, 1 << 20, dtype=np.uint8)
+            f = rfs.create_file("/ct", write_type="CACHE_THROUGH")
+            f.write(data)
+            calls = []
+
+            def boom(host):
+                calls.append(len(host))
+                raise OSError("UFS is gone")
+            f._ufs.write = boom
+            with pytest.raises(OSError, match="UFS is gone"):
+                f.write(data)
+            assert calls == [data.nbytes]
+            f.cancel()
+            assert f._beside is None
+        finally:
+            rfs.close()
+
+
 def test_native_ufs_file_write_cancel_leaves_no_file(tmp_path):
     import os
     from alluxio_amd.proto import pb as _pb
