@@ -493,6 +493,8 @@ class FileInStream(io.RawIOBase):
 
     # ---- internals ----------------------------------------------------------------------------
     def _read_range(self, pos: int, n: int, ptr: int, kind: int, stream: int = 0) -> None:
+        if kind == DEVICE and n > self.block_size and self._read_blocks_parallel(pos, n, ptr, stream):
+            return
         done = 0
         while done < n:
             idx = (pos + done) // self.block_size
@@ -507,6 +509,50 @@ class FileInStream(io.RawIOBase):
         self.ctx.metrics.counter("BytesReadClient").inc(n)
         if kind == DEVICE:
             self.ctx.metrics.counter("BytesReadDevice").inc(n)
+
+    def _read_blocks_parallel(self, pos: int, n: int, ptr: int, stream: int) -> bool:
+        """A device read spanning several blocks of remote workers: each block is its own
+        ReadBlock stream on the native client (frames into pinned chunks, H2D DMA), up to
+        ``alluxio.user.device.read.parallelism`` of them at once, so one GPU consumer is not
+        bound by a single stream.  False (nothing read) when the first block is not remote."""
+        par = self.ctx.conf.get_int("alluxio.user.device.read.parallelism", "4")
+        if par <= 1:
+            return False
+        pieces = []
+        done = 0
+        while done < n:
+            idx = (pos + done) // self.block_size
+            off = (pos + done) - idx * self.block_size
+            take = min(n - done, self.block_size - off)
+            pieces.append((idx, off, take, done))
+            done += take
+        first = self._reader_for(pieces[0][0])
+        if not isinstance(first, GrpcBlockReader):
+            return False
+        import torch
+        from concurrent.futures import ThreadPoolExecutor
+        dev = torch.cuda.current_device()
+        if stream:                  # work queued on the caller's stream may still use the buffer
+            torch.cuda.ExternalStream(stream).synchronize()
+
+        def one(piece):
+            idx, off, take, at = piece
+            torch.cuda.set_device(dev)
+            r = first if idx == pieces[0][0] else self._open_block(self.status.fileBlockInfos[idx], idx)
+            try:
+                if off + take > r.length:
+                    raise UnavailableException(f"block {idx} of {self.status.path} is shorter than expected")
+                r.read_into(off, take, ptr + at, DEVICE, 0)
+            finally:
+                if r is not first:
+                    r.close()
+        with ThreadPoolExecutor(max_workers=min(par, len(pieces)), thread_name_prefix="dev-read") as ex:
+            for f in [ex.submit(one, p) for p in pieces]:
+                f.result()
+        self.bytes_read += n
+        self.ctx.metrics.counter("BytesReadClient").inc(n)
+        self.ctx.metrics.counter("BytesReadDevice").inc(n)
+        return True
 
     def _reader_for(self, idx: int) -> BlockReader:
         if self._reader is not None and self._reader_idx == idx:

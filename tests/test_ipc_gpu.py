@@ -113,7 +113,24 @@ def test_ipc_read_from_other_process(gpu, tmp_path):
             assert f._reader.source == "remote" and f._reader._nsrc
         torch.cuda.synchronize()
         assert np.array_equal(dst2.cpu().numpy(), expect)
+        # the read spans 3 blocks: each went over its own stream (parallel device reads); an
+        # unaligned positioned read across a block boundary, and the one-block-at-a-time path
+        dst3 = torch.zeros(12 << 20, dtype=torch.uint8, device="cuda")
+        with fs2.open_file("/ipc/f") as f:
+            assert f.pread((3 << 20) + 7, dst3) == len(dst3)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst3.cpu().numpy(), expect[(3 << 20) + 7:(15 << 20) + 7])
         fs2.close()
+        fs4 = FileSystem(conf=Configuration({"alluxio.user.file.passive.cache.enabled": "false",
+                                             "alluxio.user.short.circuit.enabled": "false",
+                                             "alluxio.user.device.read.parallelism": "1"}),
+                         master_address=master)
+        dst3.zero_()
+        with fs4.open_file("/ipc/f") as f:
+            assert f.pread((3 << 20) + 7, dst3) == len(dst3)
+        torch.cuda.synchronize()
+        assert np.array_equal(dst3.cpu().numpy(), expect[(3 << 20) + 7:(15 << 20) + 7])
+        fs4.close()
     finally:
         p.stdin.write("\n")
         p.stdin.flush()
