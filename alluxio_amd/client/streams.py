@@ -235,8 +235,9 @@ class GrpcBlockReader(BlockReader):
                 if kind == DEVICE:
                     import torch
                     dev = torch.cuda.current_device()
-                    if stream:    # work queued on the caller's stream may still use the buffer
-                        torch.cuda.ExternalStream(stream).synchronize()
+                    # the H2D copies run on the native reader's own stream: work queued on the
+                    # caller's stream (e.g. the fill of a fresh torch.zeros buffer) finishes first
+                    (torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()).synchronize()
                 with native_errors():
                     lib().source_read(self._nsrc, offset, length, ptr, kind, dev)
                 return
@@ -532,8 +533,8 @@ class FileInStream(io.RawIOBase):
         import torch
         from concurrent.futures import ThreadPoolExecutor
         dev = torch.cuda.current_device()
-        if stream:                  # work queued on the caller's stream may still use the buffer
-            torch.cuda.ExternalStream(stream).synchronize()
+        # work queued on the caller's stream may still write the buffer (see GrpcBlockReader)
+        (torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()).synchronize()
 
         def one(piece):
             idx, off, take, at = piece
@@ -1042,6 +1043,7 @@ class FileOutStream(io.RawIOBase):
         self._pos = 0
         self._ufs = None
         self._beside = None          # helper thread of CACHE_THROUGH's UFS writes
+        self._overlap_min = ctx.conf.get_bytes("alluxio.user.file.cache.through.overlap.min", "256KB")
         self._canceled = False
         self._workers = None
         if self.through:
@@ -1068,7 +1070,7 @@ class FileOutStream(io.RawIOBase):
                 host = keep.detach().reshape(-1).view(torch.uint8).cpu().numpy()
             else:
                 host = _host_view(ptr, n)        # zero-copy view of the caller's buffer
-            if self.cache and n >= (256 << 10) and kind != DEVICE:
+            if self.cache and n >= self._overlap_min and kind != DEVICE:
                 # CACHE_THROUGH: the UFS write (a native stream or a syscall, both without the
                 # GIL) runs on this stream's helper thread beside the copy into the cache tier;
                 # both finish before write() returns, so the caller's buffer is not used afterwards

@@ -230,6 +230,9 @@ _k("WORKER_DATA_SERVER_NATIVE_UFS_WRITE_ENABLED", "alluxio.worker.data.server.na
    "UFS_FILE WriteBlock streams (THROUGH / CACHE_THROUGH writes of remote clients) into a mount the "
    "worker has found to be a local directory are written by the native data server's I/O threads "
    "(temp file renamed over the target at the end) instead of the Python servicer.")
+_k("USER_FILE_CACHE_THROUGH_OVERLAP_MIN", "alluxio.user.file.cache.through.overlap.min", "256KB", Scope.CLIENT,
+   "CACHE_THROUGH write() calls of at least this many bytes send the UFS copy on the stream's helper "
+   "thread while the cache copy runs; smaller ones write the two one after the other.")
 _k("USER_DEVICE_READ_PARALLELISM", "alluxio.user.device.read.parallelism", "4", Scope.CLIENT,
    "A read into device memory that spans several blocks held by remote workers reads up to this "
    "many blocks at once, each over its own native ReadBlock stream (1: one block after another).")

@@ -120,6 +120,15 @@ def test_ipc_read_from_other_process(gpu, tmp_path):
             assert f.pread((3 << 20) + 7, dst3) == len(dst3)
         torch.cuda.synchronize()
         assert np.array_equal(dst3.cpu().numpy(), expect[(3 << 20) + 7:(15 << 20) + 7])
+        # single-block reads into freshly zero-filled tensors: the native reader's H2D stream
+        # must not overtake the fill still queued on torch's stream
+        from alluxio_amd.client.streams import DEVICE
+        for off, ln in [((3 << 20) + 7, (5 << 20) - 7), (3 << 20, 5 << 20), (7, 2 << 20), (0, 8 << 20)]:
+            with fs2.open_file("/ipc/f") as f:
+                d = torch.zeros(ln, dtype=torch.uint8, device="cuda")
+                f._reader_for(0).read_into(off, ln, d.data_ptr(), DEVICE)
+                torch.cuda.synchronize()
+                assert np.array_equal(d.cpu().numpy(), expect[off:off + ln]), (off, ln)
         fs2.close()
         fs4 = FileSystem(conf=Configuration({"alluxio.user.file.passive.cache.enabled": "false",
                                              "alluxio.user.short.circuit.enabled": "false",

@@ -148,6 +148,11 @@ for s in $STEPS; do
     cthrough)
       run ww_cache_through2 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/worker_write_through.jsonl"
       ;;
+    cthroughab)
+      run ww_ct_overlap 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/worker_write_cache_through_ab.jsonl"
+      run ww_ct_serial 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --client-prop alluxio.user.file.cache.through.overlap.min=1GB --out "$OUT/worker_write_cache_through_ab.jsonl"
+      run ww_ct_overlap2 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/worker_write_cache_through_ab.jsonl"
+      ;;
     writebase)
       run worker_write_bench_grpcio 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --transports grpc --client-prop alluxio.user.native.writer.enabled=false --out "$OUT/worker_write_bench_grpcio.jsonl"
       ;;
