@@ -54,6 +54,8 @@ def main(argv=None) -> int:
     ap.add_argument("--file-size", default="1g")
     ap.add_argument("--read-size", default="64m")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--native-only", action="store_true", help="skip the grpcio comparison row")
+    ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import numpy as np
@@ -69,11 +71,12 @@ def main(argv=None) -> int:
         fs = c.client()
         fs.write_file("/rd/data", np.random.default_rng(0).integers(0, 256, size, dtype=np.uint8),
                       write_type="MUST_CACHE")
-        for native in (True, False):
+        for native in ((True,) if a.native_only else (True, False)):
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "false",
                      "alluxio.user.native.reader.enabled": str(native).lower(),
                      "alluxio.user.file.passive.cache.enabled": "false"}
+            props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             p = subprocess.run([sys.executable, "-c", CLIENT.format(root=ROOT, props=props, addr=c.master.address,
                                                                    read=parse_space_size(a.read_size), reps=a.reps)],
                                capture_output=True, text=True, timeout=900)
@@ -85,7 +88,8 @@ def main(argv=None) -> int:
             row = {"bench": "GPU consumer of a remote worker's blocks (gRPC ReadBlock into a device tensor)",
                    "client": "native GrpcBlockSource + pinned H2D" if native else "grpcio stream + host copy",
                    "file_size": a.file_size, "read_size": a.read_size, "bytes": r["bytes"],
-                   "seconds": round(r["seconds"], 3), "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3)}
+                   "seconds": round(r["seconds"], 3), "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3),
+                   "client_props": a.client_prop}
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
