@@ -478,6 +478,9 @@ class FileInStream(io.RawIOBase):
         if n <= 0:
             return 0
         if kind == HOST and self._nat is not None:
+            if n > self.block_size and self._read_blocks_parallel(self.pos, n, ptr, HOST, stream):
+                self.pos += n
+                return n
             return self._nat.read_ptr(ptr, n)
         self._read_range(self.pos, n, ptr, kind, stream)
         self.pos += n
@@ -494,7 +497,7 @@ class FileInStream(io.RawIOBase):
 
     # ---- internals ----------------------------------------------------------------------------
     def _read_range(self, pos: int, n: int, ptr: int, kind: int, stream: int = 0) -> None:
-        if kind == DEVICE and n > self.block_size and self._read_blocks_parallel(pos, n, ptr, stream):
+        if n > self.block_size and self._read_blocks_parallel(pos, n, ptr, kind, stream):
             return
         done = 0
         while done < n:
@@ -511,11 +514,12 @@ class FileInStream(io.RawIOBase):
         if kind == DEVICE:
             self.ctx.metrics.counter("BytesReadDevice").inc(n)
 
-    def _read_blocks_parallel(self, pos: int, n: int, ptr: int, stream: int) -> bool:
-        """A device read spanning several blocks of remote workers: each block is its own
-        ReadBlock stream on the native client (frames into pinned chunks, H2D DMA), up to
-        ``alluxio.user.device.read.parallelism`` of them at once, so one GPU consumer is not
-        bound by a single stream.  False (nothing read) when the first block is not remote."""
+    def _read_blocks_parallel(self, pos: int, n: int, ptr: int, kind: int, stream: int) -> bool:
+        """A read into host or device memory spanning several blocks of remote workers: each
+        block is its own ReadBlock stream on the native client (host: frames parsed into the
+        destination; device: into pinned chunks DMA'd H2D), up to
+        ``alluxio.user.device.read.parallelism`` of them at once, so one consumer is not bound by
+        a single stream.  False (nothing read) when the first block is not remote."""
         par = self.ctx.conf.get_int("alluxio.user.device.read.parallelism", "4")
         if par <= 1:
             return False
@@ -530,29 +534,34 @@ class FileInStream(io.RawIOBase):
         first = self._reader_for(pieces[0][0])
         if not isinstance(first, GrpcBlockReader):
             return False
-        import torch
         from concurrent.futures import ThreadPoolExecutor
-        dev = torch.cuda.current_device()
-        # work queued on the caller's stream may still write the buffer (see GrpcBlockReader)
-        (torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()).synchronize()
+        dev = None
+        if kind == DEVICE:
+            import torch
+            dev = torch.cuda.current_device()
+            # work queued on the caller's stream may still write the buffer (see GrpcBlockReader)
+            (torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()).synchronize()
 
         def one(piece):
             idx, off, take, at = piece
-            torch.cuda.set_device(dev)
+            if dev is not None:
+                import torch
+                torch.cuda.set_device(dev)
             r = first if idx == pieces[0][0] else self._open_block(self.status.fileBlockInfos[idx], idx)
             try:
                 if off + take > r.length:
                     raise UnavailableException(f"block {idx} of {self.status.path} is shorter than expected")
-                r.read_into(off, take, ptr + at, DEVICE, 0)
+                r.read_into(off, take, ptr + at, kind, 0)
             finally:
                 if r is not first:
                     r.close()
-        with ThreadPoolExecutor(max_workers=min(par, len(pieces)), thread_name_prefix="dev-read") as ex:
+        with ThreadPoolExecutor(max_workers=min(par, len(pieces)), thread_name_prefix="block-read") as ex:
             for f in [ex.submit(one, p) for p in pieces]:
                 f.result()
         self.bytes_read += n
         self.ctx.metrics.counter("BytesReadClient").inc(n)
-        self.ctx.metrics.counter("BytesReadDevice").inc(n)
+        if kind == DEVICE:
+            self.ctx.metrics.counter("BytesReadDevice").inc(n)
         return True
 
     def _reader_for(self, idx: int) -> BlockReader:

@@ -234,8 +234,8 @@ _k("USER_FILE_CACHE_THROUGH_OVERLAP_MIN", "alluxio.user.file.cache.through.overl
    "CACHE_THROUGH write() calls of at least this many bytes send the UFS copy on the stream's helper "
    "thread while the cache copy runs; smaller ones write the two one after the other.")
 _k("USER_DEVICE_READ_PARALLELISM", "alluxio.user.device.read.parallelism", "4", Scope.CLIENT,
-   "A read into device memory that spans several blocks held by remote workers reads up to this "
-   "many blocks at once, each over its own native ReadBlock stream (1: one block after another).")
+   "A read into device or host memory that spans several blocks held by remote workers reads up to "
+   "this many blocks at once, each over its own native ReadBlock stream (1: one block after another).")
 _k("WORKER_NETWORK_WRITER_STAGING_SIZE", "alluxio.worker.network.writer.staging.size", "4MB", Scope.WORKER,
    "Pinned staging buffer per native WriteBlock stream of an HBM worker (H2D DMA of received chunks).")
 _k("WORKER_TIEREDSTORE_DRAM_PREFAULT", "alluxio.worker.tieredstore.dram.prefault", "false", Scope.WORKER,

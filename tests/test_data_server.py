@@ -341,6 +341,35 @@ def test_native_ufs_file_writes(tmp_path):
             rfs.close()
 
 
+def test_parallel_block_reads_into_host_buffers(tmp_path):
+    """A host read spanning several remote blocks reads them at once, one native ReadBlock
+    stream each; the stream position moves past the read, and a positioned read does not."""
+    with _cluster(tmp_path) as c:
+        fs = c.client()
+        data = np.random.default_rng(14).integers(0, 256, (19 << 20) + 77, dtype=np.uint8)
+        fs.write_file("/pr", data, write_type="MUST_CACHE")
+        w = c.workers[0]
+        for par in ("4", "1"):
+            rfs = _remote_fs(c, **{"alluxio.user.device.read.parallelism": par})
+            try:
+                n0 = w.data_server.stats.streams
+                buf = np.zeros((13 << 20) + 5, dtype=np.uint8)
+                with rfs.open_file("/pr") as f:
+                    f.seek((2 << 20) + 3)
+                    assert f.read_into(buf) == len(buf)
+                    assert f.tell() == (2 << 20) + 3 + len(buf)
+                    assert f.read(10) == data[f.tell() - 10:f.tell()].tobytes()
+                    assert f.pread(1, buf[:(9 << 20)]) == 9 << 20
+                    assert f.tell() == (15 << 20) + 18
+                assert np.array_equal(buf[:(9 << 20)], data[1:(9 << 20) + 1])
+                assert np.array_equal(buf[(9 << 20):], data[(11 << 20) + 3:(15 << 20) + 8])
+                if par == "4":
+                    # 4 blocks for the read_into, 3 for the pread, plus the position-keeping reader
+                    assert w.data_server.stats.streams - n0 >= 7
+            finally:
+                rfs.close()
+
+
 def test_cache_through_ufs_error_surfaces_from_helper_thread(tmp_path):
     """CACHE_THROUGH runs the UFS write beside the cache write on a helper thread: its failure
     is raised by write(), after both have finished with the caller's buffer."""

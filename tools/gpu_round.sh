@@ -177,6 +177,11 @@ for s in $STEPS; do
       run wb_host_procs4_sdma 600 python tools/worker_bench_host.py --threads 16,64,256 --transports ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs_sdma.jsonl"
       ;;
     remotedev) run remote_device_read 600 python tools/remote_device_read_bench.py --file-size 1g --out "$OUT/remote_device_read.jsonl" ;;
+    remotehost)
+      for par in 1 4; do
+        run remote_host_read_p$par 300 python tools/remote_device_read_bench.py --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/remote_host_read.jsonl"
+      done
+      ;;
     remotedevab)
       for par in 2 4 8 16; do
         run remote_device_read_p$par 300 python tools/remote_device_read_bench.py --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/remote_device_read_par.jsonl"

@@ -29,7 +29,8 @@ import torch
 from alluxio_amd.client.file_system import FileSystem
 from alluxio_amd.conf import Configuration
 fs = FileSystem(conf=Configuration({props!r}), master_address={addr!r})
-dst = torch.empty({read}, dtype=torch.uint8, device="cuda")
+import numpy as np
+dst = torch.empty({read}, dtype=torch.uint8, device="cuda") if {dest!r} == "cuda" else np.empty({read}, dtype=np.uint8)
 def once():
     n = 0
     with fs.open_file("/rd/data") as f:
@@ -38,7 +39,8 @@ def once():
             if not k:
                 break
             n += k
-    torch.cuda.synchronize()
+    if {dest!r} == "cuda":
+        torch.cuda.synchronize()
     return n
 once()
 t0 = time.perf_counter()
@@ -54,6 +56,8 @@ def main(argv=None) -> int:
     ap.add_argument("--file-size", default="1g")
     ap.add_argument("--read-size", default="64m")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--dest", default="cuda", choices=("cuda", "host"),
+                    help="read into a device tensor or a host (numpy) buffer")
     ap.add_argument("--native-only", action="store_true", help="skip the grpcio comparison row")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--out", default=None)
@@ -78,14 +82,15 @@ def main(argv=None) -> int:
                      "alluxio.user.file.passive.cache.enabled": "false"}
             props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             p = subprocess.run([sys.executable, "-c", CLIENT.format(root=ROOT, props=props, addr=c.master.address,
-                                                                   read=parse_space_size(a.read_size), reps=a.reps)],
+                                                                   read=parse_space_size(a.read_size), reps=a.reps, dest=a.dest)],
                                capture_output=True, text=True, timeout=900)
             line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
             if line is None:
                 print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
                 return 1
             r = json.loads(line[7:])
-            row = {"bench": "GPU consumer of a remote worker's blocks (gRPC ReadBlock into a device tensor)",
+            row = {"bench": "GPU consumer of a remote worker's blocks (gRPC ReadBlock into a device tensor)"
+                   if a.dest == "cuda" else "host consumer of a remote worker's blocks (gRPC ReadBlock into a numpy buffer)",
                    "client": "native GrpcBlockSource + pinned H2D" if native else "grpcio stream + host copy",
                    "file_size": a.file_size, "read_size": a.read_size, "bytes": r["bytes"],
                    "seconds": round(r["seconds"], 3), "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3),
