@@ -42,7 +42,8 @@ def once():
     if {dest!r} == "cuda":
         torch.cuda.synchronize()
     return n
-once()
+if not {cold}:
+    once()
 t0 = time.perf_counter()
 total = sum(once() for _ in range({reps}))
 el = time.perf_counter() - t0
@@ -58,6 +59,8 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--dest", default="cuda", choices=("cuda", "host"),
                     help="read into a device tensor or a host (numpy) buffer")
+    ap.add_argument("--cold", action="store_true",
+                    help="the file is written THROUGH (in the UFS only): one timed read-through, no warm-up")
     ap.add_argument("--native-only", action="store_true", help="skip the grpcio comparison row")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--out", default=None)
@@ -74,7 +77,7 @@ def main(argv=None) -> int:
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=tempfile.mkdtemp(prefix="rdbench_")) as c:
         fs = c.client()
         fs.write_file("/rd/data", np.random.default_rng(0).integers(0, 256, size, dtype=np.uint8),
-                      write_type="MUST_CACHE")
+                      write_type="THROUGH" if a.cold else "MUST_CACHE")
         for native in ((True,) if a.native_only else (True, False)):
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "false",
@@ -82,7 +85,8 @@ def main(argv=None) -> int:
                      "alluxio.user.file.passive.cache.enabled": "false"}
             props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             p = subprocess.run([sys.executable, "-c", CLIENT.format(root=ROOT, props=props, addr=c.master.address,
-                                                                   read=parse_space_size(a.read_size), reps=a.reps, dest=a.dest)],
+                                                                   read=parse_space_size(a.read_size), reps=1 if a.cold else a.reps, dest=a.dest,
+                                                                   cold=a.cold)],
                                capture_output=True, text=True, timeout=900)
             line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
             if line is None:
@@ -94,7 +98,7 @@ def main(argv=None) -> int:
                    "client": "native GrpcBlockSource + pinned H2D" if native else "grpcio stream + host copy",
                    "file_size": a.file_size, "read_size": a.read_size, "bytes": r["bytes"],
                    "seconds": round(r["seconds"], 3), "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3),
-                   "client_props": a.client_prop}
+                   "client_props": a.client_prop, "cold": a.cold}
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
