@@ -161,8 +161,9 @@ class BlockWorkerService:
                 while pos - acked[0] >= self.window and not done.is_set():
                     cond.wait(0.5)
             n = min(len(data), end - pos)
+            mv = memoryview(data)               # frames join header + slice: one copy, not two
             for off in range(0, n, chunk):
-                yield marshal.read_response_frame(data[off:min(n, off + chunk)])
+                yield marshal.read_response_frame(mv[off:min(n, off + chunk)])
             pos += n
         t.join()
         if err and pos < end:
