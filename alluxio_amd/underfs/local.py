@@ -48,7 +48,25 @@ def _owner(st) -> tuple[str, str]:
     return owner, group
 
 
-class _AtomicWriter(io.FileIO):
+class _FullWriter(io.FileIO):
+    """FileIO whose write() writes everything: a single write(2) stops at 2 GiB - 4 KiB (and may
+    stop early on signals), and raw FileIO reports that partial count instead of looping."""
+
+    def write(self, b) -> int:
+        mv = memoryview(b).cast("B")
+        n = len(mv)
+        done = 0
+        while done < n:
+            k = super().write(mv[done:])
+            if k is None:                    # non-blocking fd with no room: not used here
+                continue
+            if k == 0:
+                raise OSError(f"write to {self.name} made no progress at {done} of {n} bytes")
+            done += k
+        return n
+
+
+class _AtomicWriter(_FullWriter):
     def __init__(self, final: str, mode: int):
         self._final = final
         self._tmp = f"{final}.alluxio.{uuid.uuid4().hex[:8]}.tmp"
@@ -78,7 +96,7 @@ class LocalUnderFileSystem(UnderFileSystem):
             os.makedirs(parent, exist_ok=True)
         if options.ensure_atomic:
             return _AtomicWriter(p, options.mode or 0o644)
-        f = io.FileIO(p, "w")
+        f = _FullWriter(p, "w")
         try:
             os.chmod(p, options.mode or 0o644)
         except OSError:
