@@ -94,3 +94,31 @@ def test_adl_contract():
                              large_file_size=1 << 20))
     finally:
         srv.stop()
+
+
+def test_local_ufs_writer_never_truncates_silently(tmp_path):
+    """A write(2) may store fewer bytes than asked (one call stops at 2 GiB - 4 KiB); the local
+    UFS writer loops, so a short write either completes or raises.  Here the file-size limit cuts
+    the first write short and the next one fails with EFBIG: the caller sees an error, not a
+    truncated file recorded at full length."""
+    import subprocess
+    import sys
+    code = r"""
+import resource, signal, sys
+sys.path.insert(0, %r)
+from alluxio_amd.underfs.base import CreateOptions
+from alluxio_amd.underfs.local import LocalUnderFileSystem
+signal.signal(signal.SIGXFSZ, signal.SIG_IGN)
+resource.setrlimit(resource.RLIMIT_FSIZE, (1 << 20, resource.getrlimit(resource.RLIMIT_FSIZE)[1]))
+ufs = LocalUnderFileSystem(%r)
+for atomic in (True, False):
+    f = ufs.create(%r + ("/a" if atomic else "/b"), CreateOptions(ensure_atomic=atomic))
+    try:
+        f.write(b"x" * (3 << 19))
+    except OSError as e:
+        print("raised", e.errno)
+    else:
+        print("no error")
+""" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), str(tmp_path), str(tmp_path))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.stdout.split("\n")[:2] == ["raised 27", "raised 27"], out.stdout + out.stderr
