@@ -9,6 +9,11 @@ into pinned chunks, H2D DMA overlapped with the next chunk) or, with
 ``--grpcio``, through the grpcio stream plus a host copy.
 
     python tools/remote_device_read_bench.py --file-size 1g --out gpurun_out/remote_device_read.jsonl
+
+A read larger than a block spans several blocks, which the client reads at once
+(``alluxio.user.device.read.parallelism``, set with ``--client-prop``).  ``--dest host`` reads into
+a numpy buffer instead of a device tensor; ``--cold`` writes the file THROUGH (UFS only) and times
+the one read-through.
 """
 from __future__ import annotations
 
