@@ -1118,6 +1118,12 @@ class FileOutStream(io.RawIOBase):
     def _write_cache(self, ptr, n, kind):
         done = 0
         while done < n:
+            if (kind == HOST and n - done >= 2 * self.block_size and self.replicas == 1 and
+                    (not self._writers or self._block_written >= self.block_size)):
+                k = self._write_blocks_parallel(ptr + done, n - done)
+                if k:
+                    done += k
+                    continue
             if not self._writers or self._block_written >= self.block_size:
                 self._next_block()
             take = min(n - done, self.block_size - self._block_written)
@@ -1126,8 +1132,61 @@ class FileOutStream(io.RawIOBase):
             self._block_written += take
             done += take
 
+    def _write_blocks_parallel(self, ptr: int, n: int) -> int:
+        """Whole blocks of one large host write to remote workers: up to
+        ``alluxio.user.device.read.parallelism`` blocks at once, each its own WriteBlock (or
+        short-circuit) stream, committed as it completes.  Block ids are taken in file order first.
+        Returns the bytes written; 0 when the next block's writer is not remote (an in-process
+        worker): that block is then left open as the current block, as _next_block would."""
+        par = self.ctx.conf.get_int("alluxio.user.device.read.parallelism", "4")
+        if par <= 1:
+            return 0
+        self._next_block()
+        if self._fanout or not all(isinstance(w, (GrpcBlockWriter, IpcBlockWriter)) for w in self._writers):
+            return 0
+        opened = [self._writers]
+        self._writers = []
+        try:
+            for _ in range(min(n // self.block_size, par) - 1):
+                _, ws, _ = self._open_writers()
+                opened.append(ws)
+        except Exception:
+            for ws in opened:
+                for w in ws:
+                    w.cancel()
+            raise
+        from concurrent.futures import ThreadPoolExecutor
+        bs = self.block_size
+
+        def one(j):
+            ws = opened[j]
+            try:
+                for w in ws:
+                    w.write_ptr(0, ptr + j * bs, bs, HOST)
+                for w in ws:
+                    w.commit()
+            except BaseException:
+                for w in ws:
+                    w.cancel()
+                raise
+        with ThreadPoolExecutor(max_workers=len(opened), thread_name_prefix="block-write") as ex:
+            futs = [ex.submit(one, j) for j in range(len(opened))]
+            errs = [f.exception() for f in futs]
+        err = next((e for e in errs if e is not None), None)
+        if err is not None:
+            raise err
+        self._block_written = 0
+        return len(opened) * bs
+
     def _next_block(self) -> None:
         self._finish_block()
+        bid, self._writers, self._fanout = self._open_writers()
+        self._block_written = 0
+
+    def _open_writers(self):
+        """Allocates the file's next block id and opens its writer(s): (id, writers, same-node
+        replicas that pull the block from the primary)."""
+        writers = []
         bid = self.ctx.fs_master().GetNewBlockIdForFile(pb.file.GetNewBlockIdForFilePRequest(path=self.path)).id
         workers = self._workers if self._workers is not None else self.ctx.workers(refresh=self._workers is None)
         self._workers = workers
@@ -1145,13 +1204,13 @@ class FileOutStream(io.RawIOBase):
             raise ResourceExhaustedException(f"Not enough workers for replications, {len(chosen)} workers "
                                              f"selected but {self.replicas} required")
         reserve = min(self.block_size, self.ctx.conf.get_bytes("alluxio.user.file.buffer.bytes", "8MB"))
-        self._fanout = []
+        fanout = []
         self._primary_addr = worker_address_str(chosen[0].address)
         self._block_id = bid
         if len(chosen) > 1 and self.ctx.conf.get_bool("alluxio.user.block.replication.peer.pull.enabled", "true"):
             prim_host = chosen[0].address.host
             pullers = [w for w in chosen[1:] if w.address.host == prim_host and self.ctx.is_local(w.address)]
-            self._fanout = [worker_address_str(w.address) for w in pullers]
+            fanout = [worker_address_str(w.address) for w in pullers]
             chosen = [chosen[0]] + [w for w in chosen[1:] if w not in pullers]
         # ASYNC_THROUGH with the UFS tier: a worker out of space spills the block to a UFS block
         # file instead of failing the write (alluxio.user.file.ufs.tier.enabled)
@@ -1160,28 +1219,28 @@ class FileOutStream(io.RawIOBase):
         for w in chosen:
             lw = self.ctx.in_process_worker(w.address)
             if lw is not None and ufs_tier:
-                self._writers.append(LocalUfsFallbackWriter(lw, bid, self.session, self.status.mountId,
+                writers.append(LocalUfsFallbackWriter(lw, bid, self.session, self.status.mountId,
                                                             self.write_tier, self.medium, max(1, reserve)))
             elif lw is not None:
-                self._writers.append(LocalBlockWriter(lw, bid, self.session, self.write_tier, self.medium,
+                writers.append(LocalBlockWriter(lw, bid, self.session, self.write_tier, self.medium,
                                                       max(1, reserve)))
             elif self._ipc_write(w) and not ufs_tier:
                 addr = worker_address_str(w.address)
                 try:
-                    self._writers.append(IpcBlockWriter(self.ctx, addr, bid, self.block_size, self.write_tier,
+                    writers.append(IpcBlockWriter(self.ctx, addr, bid, self.block_size, self.write_tier,
                                                         self.medium))
                 except Exception:  # noqa: BLE001 - no shared arena (file tier, no GPU): the data port
                     LOG.debug("short-circuit write to %s unavailable", addr, exc_info=True)
-                    self._writers.append(GrpcBlockWriter(self.ctx, addr, bid, self.write_tier, self.medium, reserve,
+                    writers.append(GrpcBlockWriter(self.ctx, addr, bid, self.write_tier, self.medium, reserve,
                                                          data_address=(w.address.host,
                                                                        w.address.dataPort or w.address.rpcPort)))
             else:
-                self._writers.append(GrpcBlockWriter(self.ctx, worker_address_str(w.address), bid,
+                writers.append(GrpcBlockWriter(self.ctx, worker_address_str(w.address), bid,
                                                      self.write_tier, self.medium, reserve,
                                                      ufs_fallback_mount=self.status.mountId if ufs_tier else None,
                                                      data_address=(w.address.host,
                                                                    w.address.dataPort or w.address.rpcPort)))
-        self._block_written = 0
+        return bid, writers, fanout
 
     def _ipc_write(self, w) -> bool:
         """Short-circuit (shared-arena) writes to a same-node worker in another process."""

@@ -432,6 +432,29 @@ def test_native_ufs_file_write_cancel_leaves_no_file(tmp_path):
         assert w.data_server.stats.write_declined == d0 + 1
 
 
+def test_parallel_block_writes_of_one_large_write(tmp_path):
+    """One host write() spanning several blocks to a remote worker streams whole blocks at once
+    (one WriteBlock each, ids taken in file order); the partial head and tail go sequentially."""
+    with _cluster(tmp_path) as c:
+        w = c.workers[0]
+        for par in ("4", "1"):
+            rfs = _remote_fs(c, **{"alluxio.user.block.size.bytes.default": "4MB",
+                                   "alluxio.user.device.read.parallelism": par})
+            try:
+                data = np.random.default_rng(15).integers(0, 256, (29 << 20) + 11, dtype=np.uint8)
+                n0 = w.data_server.stats.write_streams
+                with rfs.create_file(f"/pw{par}", write_type="MUST_CACHE") as f:
+                    f.write(data[:(1 << 20) + 3])          # a partial first block
+                    f.write(data[(1 << 20) + 3:])          # fills it, then 6 whole blocks + a tail
+                blocks = _blocks(rfs, f"/pw{par}")
+                assert [n for _, n in blocks] == [4 << 20] * 7 + [(1 << 20) + 11]
+                assert w.data_server.stats.write_streams - n0 == 8
+                assert rfs.read_file(f"/pw{par}") == data.tobytes()
+                assert rfs.get_status(f"/pw{par}").in_alluxio_percentage == 100
+            finally:
+                rfs.close()
+
+
 def test_native_write_errors_and_cancel(tmp_path):
     with _cluster(tmp_path) as c:
         w = c.workers[0]

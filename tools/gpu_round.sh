@@ -187,6 +187,11 @@ for s in $STEPS; do
       run remote_cold_host_p1 300 python tools/remote_device_read_bench.py --cold --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --out "$OUT/remote_cold_read.jsonl"
       run remote_cold_dev 300 python tools/remote_device_read_bench.py --cold --file-size 2g --read-size 2g --native-only --out "$OUT/remote_cold_read.jsonl"
       ;;
+    bigwrite)
+      for par in 1 4; do
+        run big_write_p$par 600 python tools/worker_write_bench.py --threads 1 --files 2 --file-size 1g --write-size 1g --transports grpc,ipc --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/worker_big_write.jsonl"
+      done
+      ;;
     remotedevab)
       for par in 2 4 8 16; do
         run remote_device_read_p$par 300 python tools/remote_device_read_bench.py --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/remote_device_read_par.jsonl"
