@@ -189,7 +189,7 @@ for s in $STEPS; do
       ;;
     bigwrite)
       for par in 1 4; do
-        run big_write_p$par 600 python tools/worker_write_bench.py --threads 1 --files 2 --file-size 1g --write-size 1g --transports grpc,ipc --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/worker_big_write.jsonl"
+        run big_write_p$par 170 python tools/worker_write_bench.py --threads 1 --files 2 --file-size 1g --write-size 1g --transports grpc,ipc --client-prop alluxio.user.device.read.parallelism=$par --worker-prop alluxio.worker.tieredstore.level0.dirs.quota=${BIGW_QUOTA:-8GB} --out "$OUT/worker_big_write.jsonl"
       done
       ;;
     remotedevab)
