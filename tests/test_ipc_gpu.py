@@ -86,6 +86,10 @@ def test_ipc_read_from_other_process(gpu, tmp_path):
             f.write(torch.from_numpy(wdata[:5 << 20]).cuda())
         assert fs.read_file("/ipc/w") == wdata.tobytes()
         assert fs.read_file("/ipc/wd") == wdata[:5 << 20].tobytes()
+        # one write() spanning whole blocks: they stream in parallel, one short-circuit writer each
+        with fs.create_file("/ipc/big", write_type="MUST_CACHE") as f:
+            f.write(wdata)
+        assert fs.read_file("/ipc/big") == wdata.tobytes()
         fs.close()
         # native gRPC WriteBlock into the HBM tier (the server stages chunks through pinned memory)
         fs3 = FileSystem(conf=Configuration({"alluxio.user.file.passive.cache.enabled": "false",
