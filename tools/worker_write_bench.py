@@ -23,8 +23,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CLIENT = r"""
-import json, sys, threading, time
+import faulthandler, json, os, sys, threading, time
 sys.path.insert(0, {root!r})
+if os.environ.get("WW_DUMP_AFTER"):     # debugging a stuck writer: dump every thread's stack, exit
+    faulthandler.dump_traceback_later(float(os.environ["WW_DUMP_AFTER"]), exit=True)
 import numpy as np
 from alluxio_amd.client.file_system import FileSystem
 from alluxio_amd.conf import Configuration
