@@ -48,7 +48,15 @@ class Arena:
         self._mmap = None
         self._registered = False
         if kind == "hbm":
-            self.tensor = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", device))
+            # Measured on MI355X (ROCm 7, dmabuf IPC): a process importing the arena through
+            # hipIpcOpenMemHandle hangs when the allocation size modulo 4 GiB is 2 GiB or more
+            # (3 GiB and 7 GiB arenas hang, 256 MiB / 5 / 8 / 9 GiB open at once;
+            # profiles/r4_ipc_write_hang_stack.log).  Such sizes are rounded up to a multiple of
+            # 4 GiB; the tier still uses only `nbytes` of it.
+            alloc = nbytes
+            if alloc & (1 << 31):
+                alloc = (alloc + (4 << 30) - 1) // (4 << 30) * (4 << 30)
+            self.tensor = torch.empty(alloc, dtype=torch.uint8, device=torch.device("cuda", device))[:nbytes]
         elif kind == "dram":
             self.tensor = self._shared_host(nbytes)
         else:
