@@ -67,6 +67,7 @@ class FileSystemContext:
         self._lock = threading.Lock()
         self.worker_list_ttl = self.conf.get_ms("alluxio.user.worker.list.refresh.interval", "2min") / 1000.0
         self._closed = False
+        self._keeper = None
         self._metrics_hb = None
         if self.conf.get_bool("alluxio.user.metrics.collection.enabled"):
             from ..utils import heartbeat as hb
@@ -154,7 +155,19 @@ class FileSystemContext:
             return None
         return local_worker(worker_address_str(addr))
 
+    def session_keeper(self):
+        """Renewer of worker sessions held open by short-circuit handles (session_keeper.py):
+        renews every quarter of ``alluxio.worker.session.timeout``, at least every 10 s."""
+        with self._lock:
+            if self._keeper is None:
+                from .session_keeper import SessionKeeper
+                timeout = self.conf.get_ms("alluxio.worker.session.timeout") / 1000.0
+                self._keeper = SessionKeeper(self, min(10.0, timeout / 4))
+            return self._keeper
+
     def close(self) -> None:
+        if self._keeper is not None:
+            self._keeper.close()
         if self._metrics_hb is not None:
             self._metrics_hb.shutdown(join=False)
             self._metrics_hb = None

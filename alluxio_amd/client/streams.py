@@ -297,6 +297,7 @@ class IpcBlockReader(BlockReader):
         self.session = session
         self.stub = ctx.worker_stub(address)
         self.h = self.stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session))
+        ctx.session_keeper().add(address, session)     # the read lock lives as long as the handle
         from ..ops.native import has_gpu
         self.device = torch.cuda.current_device() if has_gpu() else 0
         try:
@@ -355,6 +356,7 @@ class IpcBlockReader(BlockReader):
                     block_id=self.block_id, lock_id=self.h.lock_id, session_id=self.session))
             except Exception:  # noqa: BLE001
                 LOG.debug("unlock of device block %d failed", self.block_id, exc_info=True)
+            self.ctx.session_keeper().remove(self.address, self.session)
             self.h = None
 
 
@@ -771,10 +773,14 @@ class IpcBlockWriter(BlockWriter):
         self.ctx = ctx
         self.block_id = block_id
         self.pin = pin
+        self.address = address
         self.stub = ctx.worker_stub(address)
         self.h = self.stub.OpenDeviceWrite(pb.block.OpenDeviceWriteRequest(
             block_id=block_id, length=capacity, tier=tier, medium_type=medium, pin_on_create=pin))
         self.session = self.h.lock_id
+        # renewed until commit/cancel: an expired session would hand the reserved pages, which this
+        # process keeps writing through its mapping, to another block
+        ctx.session_keeper().add(address, self.session)
         try:
             if self.h.arena_kind != "dram" and not has_gpu():
                 raise UnavailableException("HBM arena needs a visible GPU")
@@ -804,8 +810,11 @@ class IpcBlockWriter(BlockWriter):
         if self.h is None:
             return
         h, self.h = self.h, None
-        self.stub.CommitDeviceWrite(pb.block.CommitDeviceWriteRequest(
-            block_id=self.block_id, session_id=self.session, length=self.sink.length, pin_on_create=self.pin))
+        try:
+            self.stub.CommitDeviceWrite(pb.block.CommitDeviceWriteRequest(
+                block_id=self.block_id, session_id=self.session, length=self.sink.length, pin_on_create=self.pin))
+        finally:
+            self.ctx.session_keeper().remove(self.address, self.session)
 
     def cancel(self):
         if self.h is None:
@@ -816,6 +825,7 @@ class IpcBlockWriter(BlockWriter):
                 block_id=self.block_id, session_id=self.session, abort=True))
         except Exception:  # noqa: BLE001 - the session expires on the worker
             LOG.debug("abort of short-circuit write of block %d failed", self.block_id, exc_info=True)
+        self.ctx.session_keeper().remove(self.address, self.session)
 
 
 class GrpcBlockWriter(BlockWriter):
@@ -1063,6 +1073,7 @@ class FileOutStream(io.RawIOBase):
         self._overlap_min = ctx.conf.get_bytes("alluxio.user.file.cache.through.overlap.min", "256KB")
         self._ct_counted = False
         self._canceled = False
+        self._failed: BaseException | None = None    # a parallel block write failed: no completion
         self._workers = None
         if self.through:
             workers = ctx.workers()
@@ -1083,6 +1094,8 @@ class FileOutStream(io.RawIOBase):
         return self._pos
 
     def write(self, data) -> int:
+        if self._failed is not None:
+            raise IOError(f"output stream of {self.path} failed earlier: {self._failed}") from self._failed
         ptr, n, kind, keep = _buffer_ptr(data)
         if n == 0:
             return 0
@@ -1158,22 +1171,36 @@ class FileOutStream(io.RawIOBase):
         from concurrent.futures import ThreadPoolExecutor
         bs = self.block_size
 
-        def one(j):
-            ws = opened[j]
-            try:
-                for w in ws:
-                    w.write_ptr(0, ptr + j * bs, bs, HOST)
-                for w in ws:
-                    w.commit()
-            except BaseException:
-                for w in ws:
-                    w.cancel()
-                raise
+        def fill(j):
+            for w in opened[j]:
+                w.write_ptr(0, ptr + j * bs, bs, HOST)
+
+        def commit(j):
+            for w in opened[j]:
+                w.commit()
+        # every block's bytes first, commits only once all of them landed: a failed block never
+        # leaves a committed block after it, and the stream is marked failed so later writes and
+        # close() raise (close cancels the file) instead of completing a file with a hole
+        committed = [False] * len(opened)
+        err = None
         with ThreadPoolExecutor(max_workers=len(opened), thread_name_prefix="block-write") as ex:
-            futs = [ex.submit(one, j) for j in range(len(opened))]
-            errs = [f.exception() for f in futs]
-        err = next((e for e in errs if e is not None), None)
+            errs = [f.exception() for f in [ex.submit(fill, j) for j in range(len(opened))]]
+            err = next((e for e in errs if e is not None), None)
+            if err is None:
+                futs = [ex.submit(commit, j) for j in range(len(opened))]
+                for j, f in enumerate(futs):
+                    e = f.exception()
+                    committed[j] = e is None
+                    err = err or e
         if err is not None:
+            for j, ws in enumerate(opened):
+                if not committed[j]:
+                    for w in ws:
+                        try:
+                            w.cancel()
+                        except Exception:  # noqa: BLE001
+                            LOG.debug("cancel of block writer failed", exc_info=True)
+            self._failed = err
             raise err
         self._block_written = 0
         return len(opened) * bs
@@ -1291,6 +1318,10 @@ class FileOutStream(io.RawIOBase):
             return
         if self._canceled:
             return
+        if self._failed is not None:
+            err = self._failed
+            self.cancel()
+            raise IOError(f"output stream of {self.path} failed; the file was cancelled: {err}") from err
         self._stop_beside()
         try:
             self._finish_block()

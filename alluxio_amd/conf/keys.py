@@ -230,6 +230,14 @@ _k("WORKER_DATA_SERVER_NATIVE_UFS_WRITE_ENABLED", "alluxio.worker.data.server.na
    "UFS_FILE WriteBlock streams (THROUGH / CACHE_THROUGH writes of remote clients) into a mount the "
    "worker has found to be a local directory are written by the native data server's I/O threads "
    "(temp file renamed over the target at the end) instead of the Python servicer.")
+_k("WORKER_DATA_SERVER_NATIVE_UFS_READ_ENABLED", "alluxio.worker.data.server.native.ufs.read.enabled", "true",
+   Scope.WORKER,
+   "ReadBlock of a block the worker does not hold, with open_ufs_block_options of a mount the worker has "
+   "found to be a local directory or a plain-HTTP S3 endpoint, is read through natively: a background "
+   "thread reads the UFS into pinned slots (alluxio.worker.ufs.ingest.chunk.size x .depth), copies each "
+   "into a temp block and the I/O thread streams it as it lands; the block is committed at the end.")
+_k("WORKER_DATA_SERVER_NATIVE_UFS_READ_MAX_ACTIVE", "alluxio.worker.data.server.native.ufs.read.max.active",
+   "256", Scope.WORKER, "Concurrent native cold reads (one UFS reader thread each); more go to Python.")
 _k("USER_FILE_CACHE_THROUGH_OVERLAP_MIN", "alluxio.user.file.cache.through.overlap.min", "256KB", Scope.CLIENT,
    "CACHE_THROUGH write() calls of at least this many bytes send the UFS copy on the stream's helper "
    "thread while the cache copy runs; smaller ones write the two one after the other.")

@@ -364,27 +364,63 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("write_declined", [](const DataServerStats& s) { return s.write_declined.load(); })
       .def_property_readonly("write_bytes", [](const DataServerStats& s) { return s.write_bytes.load(); })
       .def_property_readonly("ufs_write_streams", [](const DataServerStats& s) { return s.ufs_write_streams.load(); })
-      .def_property_readonly("ufs_write_bytes", [](const DataServerStats& s) { return s.ufs_write_bytes.load(); });
-  py::class_<LocalUfsRoots, std::shared_ptr<LocalUfsRoots>>(m, "LocalUfsRoots")
+      .def_property_readonly("ufs_write_bytes", [](const DataServerStats& s) { return s.ufs_write_bytes.load(); })
+      .def_property_readonly("cold_streams", [](const DataServerStats& s) { return s.cold_streams.load(); })
+      .def_property_readonly("cold_cached", [](const DataServerStats& s) { return s.cold_cached.load(); })
+      .def_property_readonly("cold_aborted", [](const DataServerStats& s) { return s.cold_aborted.load(); })
+      .def_property_readonly("cold_bytes", [](const DataServerStats& s) { return s.cold_bytes.load(); })
+      .def_property_readonly("cold_active", [](const DataServerStats& s) { return s.cold_active.load(); })
+      .def_property_readonly("prefetched", [](const DataServerStats& s) { return s.prefetched.load(); });
+  auto mounts = py::class_<UfsMounts, std::shared_ptr<UfsMounts>>(m, "UfsMounts")
       .def(py::init<>())
-      .def("set", &LocalUfsRoots::set, py::arg("mount_id"), py::arg("root"))
-      .def("remove", &LocalUfsRoots::remove, py::arg("mount_id"))
-      .def("__len__", &LocalUfsRoots::size)
-      .def("resolve", [](const LocalUfsRoots& r, int64_t mount_id, const std::string& path) -> py::object {
+      .def("set", &UfsMounts::set, py::arg("mount_id"), py::arg("root"))
+      .def("set_s3", &UfsMounts::set_s3, py::arg("mount_id"), py::arg("host"), py::arg("port"), py::arg("bucket"),
+           py::arg("access_key"), py::arg("secret_key"), py::arg("region"), py::arg("parallel"), py::arg("part"))
+      .def("remove", &UfsMounts::remove, py::arg("mount_id"))
+      .def("__len__", &UfsMounts::size)
+      .def("resolve", [](const UfsMounts& r, int64_t mount_id, const std::string& path) -> py::object {
              std::string local;
              if (!r.resolve(mount_id, path, &local)) return py::none();
              return py::str(local);
+           })
+      .def("resolve_s3", [](const UfsMounts& r, int64_t mount_id, const std::string& path) -> py::object {
+             std::shared_ptr<const S3Mount> mt;
+             std::string key;
+             if (!r.resolve_s3(mount_id, path, &mt, &key)) return py::none();
+             return py::make_tuple(mt->bucket, key);
            });
+  m.attr("LocalUfsRoots") = mounts;
+  m.def("sigv4_headers", [](const std::string& host_header, const std::string& access, const std::string& secret,
+                            const std::string& region, const std::string& method, const std::string& path,
+                            const std::string& query, const std::string& payload_hash, const std::string& amz_date) {
+          S3Credentials c;
+          c.host_header = host_header;
+          c.access_key = access;
+          c.secret_key = secret;
+          c.region = region;
+          return s3_header_lines(c, method, path, query, payload_hash, amz_date);
+        });
+  m.def("sha256_hex", [](py::bytes b) {
+          std::string v = b;
+          return sha256_hex(v.data(), v.size());
+        });
   m.def("serve_block_reads", [](FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk,
-                                uint64_t window) {
+                                uint64_t window, std::shared_ptr<UfsMounts> mounts, uint32_t commit_method,
+                                uint64_t ufs_slot_bytes, int ufs_depth, int ufs_max_active) {
           auto stats = std::make_shared<DataServerStats>();
-          serve_block_reads(srv, method, store, max_chunk, window, stats);
+          ColdReadConfig cold;
+          cold.commit_method = commit_method;
+          cold.slot_bytes = ufs_slot_bytes;
+          cold.depth = ufs_depth;
+          cold.max_active = ufs_max_active;
+          serve_block_reads(srv, method, store, max_chunk, window, stats, mounts, cold);
           return stats;
         }, py::arg("server"), py::arg("method"), py::arg("store"), py::arg("max_chunk"), py::arg("window"),
-        py::keep_alive<1, 3>());
+        py::arg("mounts") = nullptr, py::arg("commit_method") = UINT32_MAX, py::arg("ufs_slot_bytes") = 8u << 20,
+        py::arg("ufs_depth") = 3, py::arg("ufs_max_active") = 256, py::keep_alive<1, 3>());
   m.def("serve_block_writes", [](FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
                                  uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
-                                 std::shared_ptr<LocalUfsRoots> ufs_roots) {
+                                 std::shared_ptr<UfsMounts> ufs_roots) {
           serve_block_writes(srv, method, commit_method, store, stage_bytes, stats, ufs_roots);
         }, py::arg("server"), py::arg("method"), py::arg("commit_method"), py::arg("store"), py::arg("stage_bytes"),
         py::arg("stats"), py::arg("ufs_roots") = nullptr, py::keep_alive<1, 4>());

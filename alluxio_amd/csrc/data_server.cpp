@@ -8,12 +8,14 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <random>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "h2_abi.h"
@@ -99,6 +101,15 @@ struct ReadRequestMsg {
   bool has_ufs = false;
   bool has_ack = false;
   int64_t offset_received = 0;
+  std::string ufs_opts;   // serialized OpenUfsBlockOptions
+};
+
+// OpenUfsBlockOptions (proto/defs/common.py): ufs_path=1 offset_in_file=2 block_size=3
+// maxUfsReadConcurrency=4 mountId=5 no_cache=6 user=7 block_in_ufs_tier=8.
+struct UfsOpts {
+  std::string ufs_path;
+  int64_t offset_in_file = 0, block_size = 0, mount_id = 0;
+  bool no_cache = false, block_in_ufs_tier = false;
 };
 
 // ReadRequest (proto/defs/block.py): block_id=1 offset=2 length=3 promote=4 chunk_size=5
@@ -125,7 +136,10 @@ bool parse_read_request(const char* data, size_t n, ReadRequestMsg* r) {
     } else if (wt == 2) {
       uint64_t len;
       if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
-      if (field == 6) r->has_ufs = true;
+      if (field == 6) {
+        r->has_ufs = true;
+        r->ufs_opts.assign(data + i, (size_t)len);
+      }
       i += (size_t)len;
     } else if (wt == 1) {
       if (n - i < 8) return false;
@@ -149,7 +163,12 @@ class BlockReadStream : public NativeStream {
         chunk_(chunk), window_(window), device_(device), unix_(unix_peer), pool_(std::move(pool)), stats_(std::move(stats)) {}
 
   ~BlockReadStream() override {
-    if (stage_) pool_->put(stage_);
+    for (int k = 0; k < 2; ++k) {
+      if (!slot_[k].buf) continue;
+      if (slot_[k].inflight) (void)hipEventSynchronize(slot_[k].ev);   // no DMA into a pooled buffer
+      if (slot_[k].ev) (void)hipEventDestroy(slot_[k].ev);
+      pool_->put(slot_[k].buf);
+    }
     try {
       store_->unlock(lock_);
       store_->cleanup_session(session_);
@@ -159,8 +178,10 @@ class BlockReadStream : public NativeStream {
 
   void on_message(const char* p, size_t n) override {
     ReadRequestMsg r;
+    // acks only move forward and never past what was sent (an ack beyond it would wrap the
+    // unsigned window test below and stall the call with its read lock held)
     if (parse_read_request(p, n, &r) && r.has_ack && (uint64_t)r.offset_received > acked_)
-      acked_ = (uint64_t)r.offset_received;
+      acked_ = std::min<uint64_t>((uint64_t)r.offset_received, pos_);
   }
 
   ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
@@ -177,7 +198,7 @@ class BlockReadStream : public NativeStream {
         if (left_ > 0) {                // chunk bytes
           const size_t n = (size_t)std::min<uint64_t>(max - w, left_);
           if (device_) {
-            std::memcpy(dst + w, stage_ + stage_off_, n);
+            std::memcpy(dst + w, slot_[cur_].buf + stage_off_, n);
             stage_off_ += n;
           } else {                      // DRAM arena / file tier: straight into the frame
             std::vector<ReadReq> rq{ReadReq{block_, data_pos_, n, reinterpret_cast<uint64_t>(dst + w),
@@ -207,6 +228,33 @@ class BlockReadStream : public NativeStream {
   }
 
  private:
+  // Double-buffered D2H staging: chunk k is copied out of the slot its DMA landed in while the DMA
+  // of chunk k+1 runs into the other slot (reference AbstractReadHandler.java:336-439 DataReader
+  // runs ahead of the sender the same way, up to the window).
+  struct Slot {
+    uint8_t* buf = nullptr;
+    hipEvent_t ev = nullptr;
+    uint64_t pos = 0, len = 0;
+    bool inflight = false, valid = false;
+  };
+
+  void stage(int k, uint64_t pos, uint64_t n) {
+    Slot& s = slot_[k];
+    if (!s.buf) {
+      s.buf = pool_->get();
+      if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) s.ev = nullptr;
+    }
+    std::vector<ReadReq> rq{ReadReq{block_, pos, n, reinterpret_cast<uint64_t>(s.buf), (int)MemKind::kHost}};
+    hipStream_t st = thread_stream(store_);
+    store_->read_batch(rq, reinterpret_cast<uint64_t>(st), s.ev == nullptr);
+    s.inflight = s.ev != nullptr && hipEventRecord(s.ev, st) == hipSuccess;
+    if (s.ev && !s.inflight) (void)hipStreamSynchronize(st);
+    s.pos = pos;
+    s.len = n;
+    s.valid = true;
+    stats_->staged_bytes.fetch_add(n, std::memory_order_relaxed);
+  }
+
   void next_chunk() {
     const uint64_t n = std::min(chunk_, end_ - pos_);
     hdr_ = h2::read_response_prefix(n);
@@ -214,11 +262,20 @@ class BlockReadStream : public NativeStream {
     left_ = n;
     data_pos_ = pos_;
     if (device_) {
-      if (!stage_) stage_ = pool_->get();
-      std::vector<ReadReq> rq{ReadReq{block_, pos_, n, reinterpret_cast<uint64_t>(stage_), (int)MemKind::kHost}};
-      store_->read_batch(rq, reinterpret_cast<uint64_t>(thread_stream(store_)), true);
+      const int k = cur_ ^ 1;                      // the slot chunk k was (pre)staged into
+      if (!(slot_[k].valid && slot_[k].pos == pos_ && slot_[k].len == n)) stage(k, pos_, n);
+      if (slot_[k].inflight) {
+        // normally long done: it ran during the last send
+        if (hipEventSynchronize(slot_[k].ev) != hipSuccess) throw std::runtime_error("D2H staging copy failed");
+        slot_[k].inflight = false;
+      }
+      cur_ = k;
       stage_off_ = 0;
-      stats_->staged_bytes.fetch_add(n, std::memory_order_relaxed);
+      const uint64_t nx = pos_ + n;                // prefetch chunk k+1 into the slot just released
+      if (nx < end_) {
+        stage(cur_ ^ 1, nx, std::min(chunk_, end_ - nx));
+        stats_->prefetched.fetch_add(1, std::memory_order_relaxed);
+      }
     }
     pos_ += n;
     stats_->chunks.fetch_add(1, std::memory_order_relaxed);
@@ -233,11 +290,413 @@ class BlockReadStream : public NativeStream {
   std::string hdr_;
   size_t hdr_off_ = 0;
   uint64_t left_ = 0, data_pos_ = 0;
-  uint8_t* stage_ = nullptr;
+  Slot slot_[2];
+  int cur_ = 1;
   uint64_t stage_off_ = 0;
 };
 
 std::atomic<int64_t> g_session{(int64_t)1 << 62};   // above the Python range (utils/ids.py)
+
+// ---- cold reads: UFS -> pinned slots -> (temp block) + client ---------------------------------
+
+bool parse_ufs_opts(const std::string& b, UfsOpts* o) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(b.data());
+  const size_t n = b.size();
+  size_t i = 0;
+  while (i < n) {
+    uint64_t key;
+    if (!h2::get_varint(p, n, &i, &key)) return false;
+    const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (wt == 0) {
+      uint64_t v;
+      if (!h2::get_varint(p, n, &i, &v)) return false;
+      switch (field) {
+        case 2: o->offset_in_file = (int64_t)v; break;
+        case 3: o->block_size = (int64_t)v; break;
+        case 5: o->mount_id = (int64_t)v; break;
+        case 6: o->no_cache = v != 0; break;
+        case 8: o->block_in_ufs_tier = v != 0; break;
+        default: break;
+      }
+    } else if (wt == 2) {
+      uint64_t len;
+      if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
+      if (field == 1) o->ufs_path.assign(b.data() + i, (size_t)len);
+      i += (size_t)len;
+    } else if (wt == 1 && n - i >= 8) {
+      i += 8;
+    } else if (wt == 5 && n - i >= 4) {
+      i += 4;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+// A byte range source of one UFS file.
+class UfsReader {
+ public:
+  virtual ~UfsReader() = default;
+  // Exactly n bytes at `off` of the file into dst; false with *err set otherwise.
+  virtual bool read(uint64_t off, uint64_t n, uint8_t* dst, std::string* err) = 0;
+};
+
+class LocalFileReader : public UfsReader {
+ public:
+  explicit LocalFileReader(int fd) : fd_(fd) {}
+  ~LocalFileReader() override { ::close(fd_); }
+  bool read(uint64_t off, uint64_t n, uint8_t* dst, std::string* err) override {
+    uint64_t done = 0;
+    while (done < n) {
+      const ssize_t r = ::pread(fd_, dst + done, (size_t)(n - done), (off_t)(off + done));
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) {
+        *err = r == 0 ? "unexpected end of the UFS file at " + std::to_string(off + done)
+                      : std::string("pread: ") + std::strerror(errno);
+        return false;
+      }
+      done += (uint64_t)r;
+    }
+    return true;
+  }
+
+ private:
+  int fd_;
+};
+
+class S3ObjectReader : public UfsReader {
+ public:
+  S3ObjectReader(std::shared_ptr<const S3Mount> m, std::string key) : m_(std::move(m)), key_(std::move(key)) {}
+  bool read(uint64_t off, uint64_t n, uint8_t* dst, std::string* err) override {
+    static const std::string kEmptySha = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855";
+    const std::string path = "/" + m_->bucket + "/" + key_;
+    const std::string head = s3_header_lines(m_->cred, "GET", path, "", kEmptySha);
+    const int64_t got = m_->reader->get_into(uri_encode_path(path), head, off, n, reinterpret_cast<uint64_t>(dst),
+                                             m_->parallel, m_->part);
+    if (got == (int64_t)n) return true;
+    *err = "S3 GET " + path + " [" + std::to_string(off) + ", +" + std::to_string(n) + ") failed: " +
+           (got == -404 ? std::string("not found") : std::to_string(got));
+    return false;
+  }
+
+ private:
+  std::shared_ptr<const S3Mount> m_;
+  std::string key_;
+};
+
+// State shared by a cold stream (I/O threads) and its background reader thread.
+struct ColdState {
+  struct Slot {
+    uint8_t* buf = nullptr;
+    hipEvent_t ev = nullptr;
+    uint64_t off = 0, len = 0;    // block offsets of the bytes it holds
+    bool ready = false;           // filled (and its H2D queued): the stream may send it
+    bool dma = false;             // an H2D out of it may still run
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Slot> slots;
+  bool cancelled = false, read_done = false, failed = false, job_exited = false, caching = false;
+  std::string err;
+  std::function<void()> wake;
+  std::shared_ptr<StagingPool> pool;
+  ~ColdState() {
+    for (auto& sl : slots) {
+      if (sl.ev) (void)hipEventDestroy(sl.ev);
+      if (sl.buf) pool->put(sl.buf);
+    }
+  }
+};
+
+struct ColdJob {
+  BlockStore* store;
+  int64_t session, block;
+  uint64_t start, end, block_len, file_off, slot_bytes;
+  bool want_cache;
+  std::unique_ptr<UfsReader> reader;
+  std::shared_ptr<ColdState> st;
+  std::shared_ptr<DataServerStats> stats;
+
+  void wake() {
+    std::function<void()> w;
+    {
+      std::lock_guard<std::mutex> g(st->mu);
+      w = st->wake;
+    }
+    if (w) w();
+  }
+
+  // Runs on its own thread: UFS reads (and the H2D copies into the temp block) run ahead of the
+  // sends by up to `depth` slots; a slot is reused once the stream has sent it and its H2D is done.
+  void run() {
+    bool caching = false;
+    hipStream_t hs = nullptr;
+    std::string err;
+    bool ok = true;
+    try {
+      if (store->has_device()) {
+        store->use_device();
+        if (hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) != hipSuccess) hs = nullptr;
+      }
+      if (want_cache) {
+        try {   // may evict (the I/O thread never waits for space: this thread does)
+          store->create_block(session, block, 0, "", std::max<uint64_t>(block_len, 1), true, false);
+          caching = true;
+        } catch (const StoreError&) {
+          caching = false;      // another reader caches it, or no space: stream without caching
+        }
+      }
+      {
+        std::lock_guard<std::mutex> g(st->mu);
+        st->caching = caching;
+      }
+      const size_t depth = st->slots.size();
+      size_t idx = 0;
+      for (uint64_t off = start; off < end; off += slot_bytes, ++idx) {
+        ColdState::Slot* sl;
+        {
+          std::unique_lock<std::mutex> lk(st->mu);
+          sl = &st->slots[idx % depth];
+          st->cv.wait(lk, [&] { return st->cancelled || !sl->ready; });
+          if (st->cancelled) break;
+        }
+        if (sl->dma) {   // the H2D of the bytes this slot held `depth` reads ago
+          if (hipEventSynchronize(sl->ev) != hipSuccess) throw std::runtime_error("H2D into the block failed");
+          sl->dma = false;
+        }
+        if (!sl->buf) {
+          sl->buf = st->pool->get();
+          if (hs && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) sl->ev = nullptr;
+        }
+        const uint64_t n = std::min(slot_bytes, end - off);
+        if (!reader->read(file_off + off, n, sl->buf, &err)) {
+          ok = false;
+          break;
+        }
+        stats->cold_bytes.fetch_add(n, std::memory_order_relaxed);
+        if (caching) {
+          const bool async = hs && sl->ev;
+          store->write(session, block, off, reinterpret_cast<uint64_t>(sl->buf), n, (int)MemKind::kHost,
+                       reinterpret_cast<uint64_t>(hs), !async);
+          if (async) {
+            if (hipEventRecord(sl->ev, hs) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
+            sl->dma = true;
+          }
+        }
+        {
+          std::lock_guard<std::mutex> g(st->mu);
+          sl->off = off;
+          sl->len = n;
+          sl->ready = true;
+        }
+        wake();
+      }
+    } catch (const std::exception& e) {
+      ok = false;
+      err = e.what();
+    }
+    if (hs) {
+      (void)hipStreamSynchronize(hs);   // every H2D out of the slots is done before commit / abort
+      (void)hipStreamDestroy(hs);
+    }
+    bool cancelled;
+    {
+      std::lock_guard<std::mutex> g(st->mu);
+      for (auto& sl : st->slots) sl.dma = false;
+      if (!ok) {
+        st->failed = true;
+        st->err = err;
+      }
+      st->read_done = true;
+      st->job_exited = true;
+      cancelled = st->cancelled;
+    }
+    if (cancelled || !ok) {   // a read-through nobody completes: drop the temp block
+      if (caching) stats->cold_aborted.fetch_add(1, std::memory_order_relaxed);
+      try {
+        store->cleanup_session(session);
+      } catch (...) {
+      }
+    }
+    stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
+    if (!cancelled) wake();
+  }
+};
+
+class ColdReadStream : public NativeStream {
+ public:
+  ColdReadStream(BlockStore* store, int64_t session, int64_t block_id, uint64_t pos, uint64_t end, uint64_t chunk,
+                 uint64_t window, uint64_t slot_bytes, uint32_t commit_method, bool unix_peer,
+                 std::shared_ptr<ColdState> st, std::shared_ptr<DataServerStats> stats)
+      : store_(store), session_(session), block_(block_id), start_(pos), pos_(pos), acked_(pos), end_(end),
+        chunk_(chunk), window_(window), slot_bytes_(slot_bytes), commit_(commit_method), unix_(unix_peer),
+        st_(std::move(st)), stats_(std::move(stats)) {}
+
+  ~ColdReadStream() override {
+    bool exited;
+    {
+      std::lock_guard<std::mutex> g(st_->mu);
+      st_->cancelled = true;
+      st_->wake = nullptr;
+      exited = st_->job_exited;
+    }
+    st_->cv.notify_all();
+    // a running reader cleans up itself once it sees the cancel; after it exited, this drops the
+    // session (and with it a temp block nobody committed, e.g. a cancel after the last byte)
+    if (exited) {
+      try {
+        store_->cleanup_session(session_);
+      } catch (...) {
+      }
+    }
+  }
+
+  void set_waker(std::function<void()> w) override {
+    std::lock_guard<std::mutex> g(st_->mu);
+    st_->wake = std::move(w);
+  }
+
+  void on_message(const char* p, size_t n) override {
+    ReadRequestMsg r;
+    if (parse_read_request(p, n, &r) && r.has_ack && (uint64_t)r.offset_received > acked_)
+      acked_ = std::min<uint64_t>((uint64_t)r.offset_received, pos_);
+  }
+
+  bool take_post(uint32_t* method, std::string* payload) override {
+    if (!post_ready_) return false;
+    post_ready_ = false;
+    // NativeWriteCommitRequest: session_id=1 block_id=2 length=3 pin=4 ufs_read=5
+    std::string m;
+    h2::put_varint(m, (1u << 3));
+    h2::put_varint(m, (uint64_t)session_);
+    h2::put_varint(m, (2u << 3));
+    h2::put_varint(m, (uint64_t)block_);
+    h2::put_varint(m, (3u << 3));
+    h2::put_varint(m, end_);
+    h2::put_varint(m, (5u << 3));
+    h2::put_varint(m, 1);
+    *method = commit_;
+    *payload = std::move(m);
+    return true;
+  }
+
+  void on_reply(int status, const std::string& msg, const std::string&) override {
+    commit_done_ = true;
+    if (status == 0) {
+      committed_ = true;
+      stats_->cold_cached.fetch_add(1, std::memory_order_relaxed);
+    } else {
+      commit_err_ = msg;   // the client still got every byte: the call succeeds, the block is not cached
+    }
+  }
+
+  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    size_t w = 0;
+    while (w < max) {
+      if (hdr_off_ < hdr_.size()) {
+        const size_t n = std::min(max - w, hdr_.size() - hdr_off_);
+        std::memcpy(dst + w, hdr_.data() + hdr_off_, n);
+        hdr_off_ += n;
+        w += n;
+        continue;
+      }
+      if (left_ > 0) {
+        const size_t n = (size_t)std::min<uint64_t>(max - w, left_);
+        std::memcpy(dst + w, src_, n);
+        src_ += n;
+        left_ -= n;
+        w += n;
+        stats_->bytes.fetch_add(n, std::memory_order_relaxed);
+        if (unix_) stats_->domain_bytes.fetch_add(n, std::memory_order_relaxed);
+        if (left_ == 0 && pos_ >= slot_end_) release_slot();
+        continue;
+      }
+      if (pos_ >= end_) {
+        bool done, failed, caching;
+        std::string err;
+        {
+          std::lock_guard<std::mutex> g(st_->mu);
+          done = st_->read_done;
+          failed = st_->failed;
+          caching = st_->caching;
+          err = st_->err;
+        }
+        if (!done) break;                       // the H2D of the last slots still runs
+        if (failed) {
+          *status = 13;
+          *msg = "UFS read of block " + std::to_string(block_) + ": " + err;
+          return w ? (ssize_t)w : -1;
+        }
+        if (caching && !commit_done_) {
+          if (!posted_) {
+            posted_ = true;
+            post_ready_ = true;                  // read_body posts it right after this call
+          }
+          break;
+        }
+        *eof = true;
+        break;
+      }
+      if (pos_ - acked_ >= window_) break;       // wait for offset_received
+      // the slot holding pos_
+      const size_t depth = st_->slots.size();
+      const size_t idx = (size_t)((pos_ - start_) / slot_bytes_);
+      ColdState::Slot* sl = &st_->slots[idx % depth];
+      bool ready, failed;
+      std::string err;
+      {
+        std::lock_guard<std::mutex> g(st_->mu);
+        ready = sl->ready && sl->off <= pos_ && pos_ < sl->off + sl->len;
+        failed = st_->failed;
+        err = st_->err;
+      }
+      if (!ready) {
+        if (failed) {
+          *status = 13;
+          *msg = "UFS read of block " + std::to_string(block_) + ": " + err;
+          return w ? (ssize_t)w : -1;
+        }
+        break;                                   // the reader wakes this call when it lands
+      }
+      const uint64_t n = std::min(chunk_, std::min(sl->off + sl->len, end_) - pos_);
+      hdr_ = h2::read_response_prefix(n);
+      hdr_off_ = 0;
+      left_ = n;
+      src_ = sl->buf + (pos_ - sl->off);
+      slot_end_ = sl->off + sl->len;
+      cur_slot_ = sl;
+      pos_ += n;
+      stats_->chunks.fetch_add(1, std::memory_order_relaxed);
+    }
+    return (ssize_t)w;
+  }
+
+ private:
+  void release_slot() {
+    {
+      std::lock_guard<std::mutex> g(st_->mu);
+      if (cur_slot_) cur_slot_->ready = false;
+    }
+    cur_slot_ = nullptr;
+    st_->cv.notify_all();
+  }
+
+  BlockStore* store_;
+  int64_t session_, block_;
+  uint64_t start_, pos_, acked_, end_, chunk_, window_, slot_bytes_;
+  uint32_t commit_;
+  bool unix_;
+  std::shared_ptr<ColdState> st_;
+  std::shared_ptr<DataServerStats> stats_;
+  std::string hdr_;
+  size_t hdr_off_ = 0;
+  uint64_t left_ = 0, slot_end_ = 0;
+  const uint8_t* src_ = nullptr;
+  ColdState::Slot* cur_slot_ = nullptr;
+  bool posted_ = false, post_ready_ = false, commit_done_ = false, committed_ = false;
+  std::string commit_err_;
+};
 
 // ---- WriteBlock ---------------------------------------------------------------------------------
 // WriteRequestCommand (proto/defs/block.py): type=1 id=2 offset=3 tier=4 flush=5
@@ -650,24 +1109,67 @@ namespace {
 std::string strip_file_scheme(const std::string& p) { return p.compare(0, 7, "file://") == 0 ? p.substr(7) : p; }
 }  // namespace
 
-void LocalUfsRoots::set(int64_t mount_id, const std::string& root) {
+void UfsMounts::set(int64_t mount_id, const std::string& root) {
   std::string r = strip_file_scheme(root);
   while (!r.empty() && r.back() == '/') r.pop_back();     // "/" -> "" (every absolute path)
   std::lock_guard<std::mutex> g(mu_);
   roots_[mount_id] = r;
 }
 
-void LocalUfsRoots::remove(int64_t mount_id) {
+void UfsMounts::remove(int64_t mount_id) {
   std::lock_guard<std::mutex> g(mu_);
   roots_.erase(mount_id);
+  s3_.erase(mount_id);
 }
 
-size_t LocalUfsRoots::size() const {
+void UfsMounts::set_s3(int64_t mount_id, const std::string& host, int port, const std::string& bucket,
+                       const std::string& access_key, const std::string& secret_key, const std::string& region,
+                       int parallel, uint64_t part) {
+  auto m = std::make_shared<S3Mount>();
+  m->host = host;
+  m->port = port;
+  m->bucket = bucket;
+  m->cred.host_header = port == 80 ? host : host + ":" + std::to_string(port);
+  m->cred.access_key = access_key;
+  m->cred.secret_key = secret_key;
+  m->cred.region = region.empty() ? "us-east-1" : region;
+  m->parallel = std::max(1, parallel);
+  m->part = std::max<uint64_t>(part, 64u << 10);
+  m->reader = std::make_shared<HttpRangeReader>(host, port, 2 * m->parallel);
   std::lock_guard<std::mutex> g(mu_);
-  return roots_.size();
+  s3_[mount_id] = std::move(m);
 }
 
-bool LocalUfsRoots::resolve(int64_t mount_id, const std::string& ufs_path, std::string* local) const {
+bool UfsMounts::resolve_s3(int64_t mount_id, const std::string& ufs_path, std::shared_ptr<const S3Mount>* m,
+                           std::string* key) const {
+  std::shared_ptr<const S3Mount> mount;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = s3_.find(mount_id);
+    if (it == s3_.end()) return false;
+    mount = it->second;
+  }
+  const size_t sch = ufs_path.find("://");
+  if (sch == std::string::npos) return false;
+  const std::string rest = ufs_path.substr(sch + 3);      // bucket/key
+  const size_t slash = rest.find('/');
+  if (rest.substr(0, slash) != mount->bucket) return false;
+  std::string k = slash == std::string::npos ? std::string() : rest.substr(slash + 1);
+  size_t lead = 0;
+  while (lead < k.size() && k[lead] == '/') ++lead;
+  k.erase(0, lead);
+  if (k.empty()) return false;
+  *m = std::move(mount);
+  *key = std::move(k);
+  return true;
+}
+
+size_t UfsMounts::size() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return roots_.size() + s3_.size();
+}
+
+bool UfsMounts::resolve(int64_t mount_id, const std::string& ufs_path, std::string* local) const {
   std::string root;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -689,11 +1191,93 @@ bool LocalUfsRoots::resolve(int64_t mount_id, const std::string& ufs_path, std::
   return true;
 }
 
+namespace {
+
+// A native cold stream for `r` (the block is not in the store), or nullptr to hand the call to
+// Python (mount not registered, UFS-tier block, too many readers).
+std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, BlockStore* store, uint64_t max_chunk,
+                                               uint64_t window, bool unix_peer, const ColdReadConfig& cfg,
+                                               const std::shared_ptr<UfsMounts>& mounts,
+                                               const std::shared_ptr<StagingPool>& slot_pool,
+                                               const std::shared_ptr<DataServerStats>& stats, int* status,
+                                               std::string* msg) {
+  UfsOpts o;
+  if (!mounts || !parse_ufs_opts(r.ufs_opts, &o) || o.ufs_path.empty() || o.block_in_ufs_tier || o.block_size <= 0)
+    return nullptr;
+  const uint64_t block_len = (uint64_t)o.block_size;
+  const uint64_t off = (uint64_t)std::max<int64_t>(0, r.offset);
+  if (off > block_len) {
+    *status = 11;
+    *msg = "offset " + std::to_string(off) + " beyond block " + std::to_string(r.block_id) + " of " +
+           std::to_string(block_len) + " bytes";
+    return nullptr;
+  }
+  const uint64_t end = r.length > 0 ? std::min<uint64_t>(block_len, off + (uint64_t)r.length) : block_len;
+  std::unique_ptr<UfsReader> reader;
+  std::string local, key;
+  std::shared_ptr<const S3Mount> s3;
+  if (mounts->resolve(o.mount_id, o.ufs_path, &local)) {
+    const int fd = ::open(local.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      const int e = errno;
+      *status = grpc_status_of_errno(e);
+      *msg = "opening " + o.ufs_path + ": " + std::strerror(e);
+      return nullptr;
+    }
+    reader.reset(new LocalFileReader(fd));
+  } else if (mounts->resolve_s3(o.mount_id, o.ufs_path, &s3, &key)) {
+    reader.reset(new S3ObjectReader(std::move(s3), std::move(key)));
+  } else {
+    return nullptr;
+  }
+  if (stats->cold_active.fetch_add(1, std::memory_order_relaxed) >= cfg.max_active) {
+    stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
+    return nullptr;
+  }
+  // UnderFileSystemBlockReader caches only a whole-block sequential read; anything else streams
+  const bool cache = !o.no_cache && off == 0 && end == block_len && cfg.commit_method != UINT32_MAX &&
+                     !store->has_temp_block(r.block_id);
+  auto st = std::make_shared<ColdState>();
+  st->pool = slot_pool;
+  st->slots.resize((size_t)std::max(2, cfg.depth));
+  auto job = std::make_shared<ColdJob>();
+  job->store = store;
+  job->session = g_session.fetch_add(1);
+  job->block = r.block_id;
+  job->start = off;
+  job->end = end;
+  job->block_len = block_len;
+  job->file_off = (uint64_t)std::max<int64_t>(0, o.offset_in_file);
+  job->slot_bytes = slot_pool->size();
+  job->want_cache = cache;
+  job->reader = std::move(reader);
+  job->st = st;
+  job->stats = stats;
+  const uint64_t chunk =
+      r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk) : std::min<uint64_t>(1u << 20, max_chunk);
+  std::unique_ptr<NativeStream> ns(new ColdReadStream(store, job->session, r.block_id, off, end, chunk, window,
+                                                      slot_pool->size(), cfg.commit_method, unix_peer, st, stats));
+  stats->cold_streams.fetch_add(1, std::memory_order_relaxed);
+  try {
+    std::thread([job] { job->run(); }).detach();
+  } catch (...) {
+    stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
+    *status = 8;
+    *msg = "cannot start a UFS reader thread";
+    return nullptr;
+  }
+  return ns;
+}
+
+}  // namespace
+
 void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk, uint64_t window,
-                       std::shared_ptr<DataServerStats> stats) {
+                       std::shared_ptr<DataServerStats> stats, std::shared_ptr<UfsMounts> mounts, ColdReadConfig cold) {
   if (max_chunk == 0) max_chunk = 2u << 20;
   if (window == 0) window = 4u << 20;
+  if (cold.slot_bytes == 0) cold.slot_bytes = 8u << 20;
   auto pool = std::make_shared<StagingPool>(max_chunk, store->has_device());
+  auto slot_pool = std::make_shared<StagingPool>(cold.slot_bytes, store->has_device());
   FrameRpcServer* s = &srv;
   srv.set_native_stream(method, [=](const std::string& first, const std::string& cid, const std::string& user,
                                     bool unix_peer, int* status, std::string* msg) -> std::unique_ptr<NativeStream> {
@@ -710,8 +1294,8 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
                          : "channel " + cid + " is not authenticated";
       return nullptr;
     }
-    // UFS read-through, promotion and locks that would wait: the Python servicer
-    if (r.has_ufs || r.promote || r.offset < 0) {
+    // promotion and locks that would wait: the Python servicer
+    if (r.promote || r.offset < 0) {
       stats->declined.fetch_add(1, std::memory_order_relaxed);
       return nullptr;
     }
@@ -723,6 +1307,10 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
       lock = -1;   // not (yet) committed here
     }
     if (lock < 0) {
+      if (r.has_ufs) {     // a cold block: read it through from the UFS (BlockReadHandler.openUfsBlock)
+        auto cs = make_cold_stream(r, store, max_chunk, window, unix_peer, cold, mounts, slot_pool, stats, status, msg);
+        if (cs || *status != 0) return cs;
+      }
       stats->declined.fetch_add(1, std::memory_order_relaxed);
       return nullptr;
     }
@@ -757,7 +1345,7 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
 
 void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
                         uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
-                        std::shared_ptr<LocalUfsRoots> ufs_roots) {
+                        std::shared_ptr<UfsMounts> ufs_roots) {
   if (stage_bytes == 0) stage_bytes = 4u << 20;
   auto pool = std::make_shared<StagingPool>(stage_bytes, store->has_device());
   FrameRpcServer* s = &srv;
@@ -795,8 +1383,21 @@ void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_me
     const int64_t session = g_session.fetch_add(1);
     const uint64_t reserve = cmd.reserve > 0 ? (uint64_t)cmd.reserve : (1u << 20);
     try {
-      const int dir = store->create_block(session, cmd.id, cmd.medium.empty() ? (cmd.has_tier ? (int)cmd.tier : 0) : -1,
-                                          cmd.medium, reserve, true, cmd.pin);
+      // evict = false: the I/O thread never waits for space (eviction can block on locks and run
+      // demotion copies); a write that needs eviction goes to the Python servicer, which may wait
+      int dir;
+      try {
+        dir = store->create_block(session, cmd.id, cmd.medium.empty() ? (cmd.has_tier ? (int)cmd.tier : 0) : -1,
+                                  cmd.medium, reserve, false, cmd.pin);
+      } catch (const StoreError& e) {
+        if (e.code != kErrOutOfSpace) throw;
+        try {
+          store->cleanup_session(session);
+        } catch (...) {
+        }
+        stats->write_declined.fetch_add(1, std::memory_order_relaxed);
+        return nullptr;
+      }
       const bool device = store->dir_spec(dir).kind == DirKind::kDevice;
       auto ws = std::unique_ptr<BlockWriteStream>(new BlockWriteStream(store, session, cmd.id, (uint64_t)cmd.offset,
                                                                        cmd.pin, device, commit_method, pool, stats));

@@ -8,12 +8,14 @@
 // out as a hand-built protobuf header followed by the raw buffer).
 //
 // MI355X design: a call for a block held by the store is read-locked for its lifetime and streamed
-// chunk by chunk: an HBM chunk is DMA'd (D2H, one stream per I/O thread) into a pinned staging
-// buffer, a DRAM / file-tier chunk is copied straight from the arena or file into the outgoing
-// HTTP/2 frame.  The next chunk is produced only while the client's unacknowledged bytes stay
-// below the window (ReadRequest.offset_received acks).  Calls the store cannot serve alone (UFS
-// read-through, promote, a block still being written or moved) go to the Python servicer through
-// the front end's streaming bridge, so the port serves the whole BlockWorker service.
+// chunk by chunk: an HBM chunk is DMA'd (D2H, one stream per I/O thread) into one of two pinned
+// staging buffers while the previous chunk is being sent, a DRAM / file-tier chunk is copied
+// straight from the arena or file into the outgoing HTTP/2 frame.  The next chunk is produced only
+// while the client's unacknowledged bytes stay below the window (ReadRequest.offset_received acks).
+// A cold block of a registered local or S3 mount is read through natively (see serve_block_reads).
+// Calls the store cannot serve alone (promote, a block still being written or moved, a UFS the I/O
+// threads cannot reach) go to the Python servicer through the front end's streaming bridge, so the
+// port serves the whole BlockWorker service.
 #pragma once
 #include <atomic>
 #include <cstdint>
@@ -24,6 +26,8 @@
 
 #include "block_store.h"
 #include "frame_rpc.h"
+#include "http_blob.h"
+#include "sigv4.h"
 
 namespace amdx {
 
@@ -39,41 +43,84 @@ struct DataServerStats {
   std::atomic<uint64_t> write_bytes{0};    // block bytes written natively
   std::atomic<uint64_t> ufs_write_streams{0};  // UFS_FILE writes into a local UFS served natively
   std::atomic<uint64_t> ufs_write_bytes{0};
+  std::atomic<uint64_t> cold_streams{0};     // UFS read-through / uncached UFS reads served natively
+  std::atomic<uint64_t> cold_cached{0};      // of which cached the whole block (committed)
+  std::atomic<uint64_t> cold_aborted{0};     // read-throughs abandoned (cancel, error): temp block aborted
+  std::atomic<uint64_t> cold_bytes{0};       // bytes read from the UFS by those streams
+  std::atomic<int64_t> cold_active{0};       // background UFS readers still running
+  std::atomic<uint64_t> prefetched{0};       // HBM chunks whose D2H was issued ahead of the send
 };
 
-// Mounts whose UFS is a local directory, so a UFS_FILE WriteBlock can be written by the I/O
-// thread with plain file calls.  The worker registers a mount once its Python side has resolved
-// it to the local UFS (worker/block_worker.py); other mounts (S3, HDFS, ...) stay in Python.
-class LocalUfsRoots {
+// An S3-compatible object mount the native data path reads from (plain-HTTP endpoint).
+struct S3Mount {
+  std::string host;
+  int port = 80;
+  std::string bucket;
+  S3Credentials cred;
+  int parallel = 8;            // concurrent sub-range GETs of one read
+  uint64_t part = 4u << 20;    // minimum sub-range
+  std::shared_ptr<HttpRangeReader> reader;
+};
+
+// Mounts the I/O threads can reach without Python: local directories (a UFS_FILE WriteBlock is
+// written with plain file calls, a cold ReadBlock preads the file) and S3-compatible buckets (a
+// cold ReadBlock issues signed ranged GETs).  The worker registers a mount once its Python side
+// has resolved it (worker/block_worker.py note_ufs_mount); other mounts (HDFS, ...) stay in Python.
+class UfsMounts {
  public:
   void set(int64_t mount_id, const std::string& root);
+  void set_s3(int64_t mount_id, const std::string& host, int port, const std::string& bucket,
+              const std::string& access_key, const std::string& secret_key, const std::string& region,
+              int parallel, uint64_t part);
   void remove(int64_t mount_id);
   size_t size() const;
-  // The local path of `ufs_path` ("file:///x" or "/x") if mount `mount_id` is registered and the
-  // path lies inside its root without "." / ".." components.
+  // The local path of `ufs_path` ("file:///x" or "/x") if mount `mount_id` is a registered local
+  // directory and the path lies inside its root without "." / ".." components.
   bool resolve(int64_t mount_id, const std::string& ufs_path, std::string* local) const;
+  // The object mount and key of `ufs_path` ("s3://bucket/key") if `mount_id` is a registered
+  // S3 mount of that bucket.
+  bool resolve_s3(int64_t mount_id, const std::string& ufs_path, std::shared_ptr<const S3Mount>* m,
+                  std::string* key) const;
 
  private:
   mutable std::mutex mu_;
   std::unordered_map<int64_t, std::string> roots_;
+  std::unordered_map<int64_t, std::shared_ptr<const S3Mount>> s3_;
+};
+using LocalUfsRoots = UfsMounts;
+
+// Cold-read settings of serve_block_reads.
+struct ColdReadConfig {
+  uint64_t slot_bytes = 8u << 20;   // one UFS read / H2D copy
+  int depth = 3;                    // slots per stream (reads run this far ahead of the sends)
+  int max_active = 256;             // concurrent background UFS readers; more go to Python
+  uint32_t commit_method = UINT32_MAX;   // internal NativeWriteCommit (caches are committed in Python)
 };
 
 // Serve `method` (the ReadBlock path's index) of `srv` from `store`.  `max_chunk` caps a client's
 // chunk_size, `window` is the un-acked byte limit per call.
+// With `mounts`, a read of a block the store does not hold that carries open_ufs_block_options of a
+// registered mount is served natively too (reference BlockReadHandler.java:159-235 openUfsBlock,
+// UnderFileSystemBlockReader.java:205-274): a background thread reads the UFS into pinned slots,
+// each slot is copied into a fresh temp block (async H2D for HBM) and streamed to the client as
+// soon as it lands; at the end the block is committed through `cold.commit_method` in Python (CRC,
+// master report) before the call ends.  A partial, offset or no_cache read streams the range
+// without caching; a cancelled or failed read-through aborts the temp block.
 void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk,
-                       uint64_t window, std::shared_ptr<DataServerStats> stats);
+                       uint64_t window, std::shared_ptr<DataServerStats> stats,
+                       std::shared_ptr<UfsMounts> mounts = nullptr, ColdReadConfig cold = ColdReadConfig());
 
 // Serve `method` (WriteBlock) of `srv` into `store` for ALLUXIO_BLOCK writes: the block is created
 // on the first message, chunk messages are written into it on the I/O thread (HBM: through a
 // pinned staging buffer and an async H2D on the thread's stream), flush commands are answered
 // with the offset; at the client's half-close the commit -- CRC, master report -- runs in Python
 // as the internal unary `commit_method` (NativeWriteCommitRequest) whose reply ends the call.
-// UFS_FILE writes under a mount of `ufs_roots` (may be null) are written natively too: a temp
+// UFS_FILE writes under a local mount of `ufs_roots` (may be null) are written natively too: a temp
 // file beside the target, renamed over it at the half-close (reference UfsFileWriteHandler.java
 // with the local UFS's AtomicFileOutputStream).  Other UFS_FILE and UFS_FALLBACK_BLOCK writes go
 // to the Python servicer.
 void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
                         uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
-                        std::shared_ptr<LocalUfsRoots> ufs_roots = nullptr);
+                        std::shared_ptr<UfsMounts> ufs_roots = nullptr);
 
 }  // namespace amdx

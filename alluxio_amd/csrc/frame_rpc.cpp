@@ -10,6 +10,7 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -422,6 +423,12 @@ void FrameRpcServer::H2::dispatch(Session& S, int32_t sid, Stream& st, std::stri
         srv.natives_[st.method](msg, st.cid, st.auser, S.conn->unix_peer, &status, &err);
     if (ns) {
       st.native = std::move(ns);
+      std::shared_ptr<WakeHub> hub = srv.hub_;
+      const uint64_t tok = ((uint64_t)S.conn->id << 32) | (uint32_t)sid;
+      st.native->set_waker([hub, tok] {
+        std::lock_guard<std::mutex> g(hub->mu);
+        if (hub->srv) hub->srv->wake(tok);
+      });
       start_response(S, sid, st);
       return;
     }
@@ -547,6 +554,10 @@ ssize_t FrameRpcServer::H2::read_body(void* session, int32_t sid, uint8_t* buf, 
     int status = 0;
     std::string m;
     const ssize_t got = st.native->produce(buf, length, &eof, &status, &m);
+    uint32_t post_method = 0;
+    std::string post_payload;
+    if (got >= 0 && !eof && st.native->take_post(&post_method, &post_payload))
+      post_python(S, sid, st, post_method, std::move(post_payload));
     if (got < 0) {
       st.finished = true;
       st.fin_status = status ? status : 13;
@@ -910,10 +921,20 @@ void FrameRpcServer::start() {
     }
   }
   running_ = true;
+  hub_ = std::make_shared<WakeHub>();
+  hub_->srv = this;
   for (int i = 0; i < nthreads_; ++i) {
     const int ep = ::epoll_create1(EPOLL_CLOEXEC);
     if (ep < 0) throw std::runtime_error("frame rpc: epoll_create1 failed");
     epolls_.push_back(ep);
+    const int wfd = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (wfd < 0) throw std::runtime_error("frame rpc: eventfd failed");
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = 0;                    // connection ids start at 1: 0 is the wake fd
+    ::epoll_ctl(ep, EPOLL_CTL_ADD, wfd, &ev);
+    wake_fds_.push_back(wfd);
+    wake_qs_.emplace_back(new WakeQueue());
   }
   for (int i = 0; i < nthreads_; ++i) threads_.emplace_back([this, i] { io_loop(i); });
   acceptor_ = std::thread([this] { accept_loop(); });
@@ -921,6 +942,10 @@ void FrameRpcServer::start() {
 
 void FrameRpcServer::stop() {
   if (!running_.exchange(false)) return;
+  if (hub_) {
+    std::lock_guard<std::mutex> g(hub_->mu);   // no waker touches this server once stop() returns
+    hub_->srv = nullptr;
+  }
   if (listen_fd_ >= 0) ::shutdown(listen_fd_, SHUT_RDWR);
   if (unix_fd_ >= 0) ::shutdown(unix_fd_, SHUT_RDWR);
   if (acceptor_.joinable()) acceptor_.join();
@@ -936,6 +961,8 @@ void FrameRpcServer::stop() {
   threads_.clear();
   for (int ep : epolls_) ::close(ep);
   epolls_.clear();
+  for (int fd : wake_fds_) ::close(fd);
+  wake_fds_.clear();
   {
     std::lock_guard<std::mutex> g(conns_mu_);
     for (auto& kv : conns_) {
@@ -1036,6 +1063,46 @@ void FrameRpcServer::on_writable(const std::shared_ptr<Conn>& c) {
   if (!ok) close_conn(c->id);
 }
 
+void FrameRpcServer::wake(uint64_t token) {
+  if (!running_ || epolls_.empty()) return;
+  const size_t idx = (uint32_t)(token >> 32) % epolls_.size();
+  WakeQueue& q = *wake_qs_[idx];
+  bool first;
+  {
+    std::lock_guard<std::mutex> g(q.mu);
+    first = q.tokens.empty();
+    q.tokens.push_back(token);
+  }
+  if (first) {
+    const uint64_t one = 1;
+    ssize_t w = ::write(wake_fds_[idx], &one, sizeof(one));
+    (void)w;
+  }
+}
+
+void FrameRpcServer::run_wakes(int idx) {
+  uint64_t cnt;
+  while (::read(wake_fds_[idx], &cnt, sizeof(cnt)) > 0) {
+  }
+  std::vector<uint64_t> toks;
+  {
+    std::lock_guard<std::mutex> g(wake_qs_[idx]->mu);
+    toks.swap(wake_qs_[idx]->tokens);
+  }
+  for (uint64_t t : toks) {
+    auto c = find((uint32_t)(t >> 32));
+    if (!c || c->closed || c->proto != 2) continue;
+    bool ok;
+    {
+      std::lock_guard<std::mutex> g(c->wmu);
+      if (!c->h2) continue;
+      h2::lib().resume_data(c->h2->ng, (int32_t)(t & 0x7fffffffu));
+      ok = H2::flush_locked(*c->h2);
+    }
+    if (!ok) close_conn(c->id);
+  }
+}
+
 void FrameRpcServer::io_loop(int idx) {
   const int ep = epolls_[idx];
   epoll_event evs[64];
@@ -1043,6 +1110,10 @@ void FrameRpcServer::io_loop(int idx) {
     const int n = ::epoll_wait(ep, evs, 64, 100);
     for (int i = 0; i < n; ++i) {
       const uint32_t id = (uint32_t)evs[i].data.u64;
+      if (id == 0) {
+        run_wakes(idx);
+        continue;
+      }
       auto c = find(id);
       if (!c) continue;
       if (evs[i].events & (EPOLLERR | EPOLLHUP)) {

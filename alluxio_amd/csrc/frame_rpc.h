@@ -61,6 +61,14 @@ class NativeStream {
   virtual bool on_end(uint32_t* method, std::string* payload) { return false; }
   // The Python reply of the request on_end() posted (status 0: `payload` is the serialized reply).
   virtual void on_reply(int status, const std::string& msg, const std::string& payload) {}
+  // Installed by the server right after the factory accepted the call.  `wake` may be called from
+  // any thread (a background UFS reader, a HIP host callback): produce() is then polled again on
+  // the connection's I/O thread.  It never runs produce() inline and stays safe to call after the
+  // call or the server is gone.
+  virtual void set_waker(std::function<void()> wake) {}
+  // Polled after every produce(): true = post {*method, *payload} to Python now as an internal
+  // request (as on_end() does at the half-close); the reply comes back through on_reply().
+  virtual bool take_post(uint32_t* method, std::string* payload) { return false; }
 };
 // Builds the native stream of a call from its first request message and the caller's identity
 // (the channel-id and alluxio-user headers).  nullptr with *status == 0 hands the call to the
@@ -104,6 +112,8 @@ class FrameRpcServer {
   void set_method_kind(uint32_t method, int kind);
   // Serve `method` from C++ when the factory accepts the call (gRPC connections only).
   void set_native_stream(uint32_t method, NativeStreamFactory factory);
+  // Re-poll the native stream of `token` ((conn id << 32) | stream id) on its I/O thread.
+  void wake(uint64_t token);
   // ---- kind-2 bridge (Python side; the GIL is released around the blocking calls) ----------
   // 0 = a message in *out, 1 = the client half-closed, 2 = cancelled / connection gone, 3 = timeout.
   int stream_recv(uint64_t token, int timeout_ms, std::string* out);
@@ -174,7 +184,20 @@ class FrameRpcServer {
   std::unordered_map<std::string, std::string> channels_;
   bool require_auth_ = false;
   uint32_t stream_window_ = 1u << 20;
-  int wake_fd_ = -1;
+  // wake(): one eventfd + token queue per I/O thread; the hub outlives the server for wakers
+  // still held by background producers (it is cleared in stop()).
+  struct WakeHub {
+    std::mutex mu;
+    FrameRpcServer* srv = nullptr;
+  };
+  struct WakeQueue {
+    std::mutex mu;
+    std::vector<uint64_t> tokens;
+  };
+  std::shared_ptr<WakeHub> hub_;
+  std::vector<int> wake_fds_;
+  std::vector<std::unique_ptr<WakeQueue>> wake_qs_;
+  void run_wakes(int idx);
 
   static std::string cache_key(uint32_t method, const std::string& user, const char* req, size_t n);
   // a cached reply: status 0 + body, or an error status + message (NOT_FOUND lookups)

@@ -21,8 +21,8 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
 SOURCES = ["kernels.hip", "evict_alloc.hip", "page_cache_put.hip", "block_store.cpp", "cpu_codecs.cpp", "ipc.cpp", "ring_read.cpp", "page_cache.cpp", "meta_codec.cpp", "fuse_server.cpp", "http_blob.cpp",
-           "frame_rpc.cpp", "data_server.cpp", "block_source.cpp", "hdfs_packets.cpp", "data_path_bind.cpp", "bindings.cpp"]
-HEADERS = ["kernels.h", "block_store.h", "cpu_codecs.h", "ipc.h", "ring_read.h", "page_cache.h", "page_cache_bind.h", "seg_ring.h", "frame_rpc.h", "meta_codec.h", "fuse_server.h", "h2_abi.h", "data_server.h",
+           "frame_rpc.cpp", "sigv4.cpp", "data_server.cpp", "block_source.cpp", "hdfs_packets.cpp", "data_path_bind.cpp", "bindings.cpp"]
+HEADERS = ["kernels.h", "block_store.h", "cpu_codecs.h", "ipc.h", "ring_read.h", "page_cache.h", "page_cache_bind.h", "seg_ring.h", "frame_rpc.h", "meta_codec.h", "fuse_server.h", "h2_abi.h", "data_server.h", "sigv4.h", "http_blob.h",
            "block_source.h", "hdfs_packets.h"]
 
 
@@ -44,6 +44,30 @@ def _needs_build(target: str) -> bool:
         if os.path.getmtime(os.path.join(CSRC, f)) > t:
             return True
     return os.path.getmtime(os.path.abspath(__file__)) > t
+
+
+def _local_includes(path: str, seen: set | None = None) -> set:
+    """Headers of csrc/ that ``path`` includes, transitively (``#include "x.h"``)."""
+    import re
+    seen = set() if seen is None else seen
+    try:
+        text = open(path).read()
+    except OSError:
+        return seen
+    for h in re.findall(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+        hp = os.path.join(CSRC, h)
+        if hp not in seen and os.path.exists(hp):
+            seen.add(hp)
+            _local_includes(hp, seen)
+    return seen
+
+
+def _obj_stale(src_path: str, obj: str) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    deps = [src_path, os.path.abspath(__file__), *_local_includes(src_path)]
+    return any(os.path.getmtime(d) > t for d in deps)
 
 
 def _run(cmd: list[str]) -> None:
@@ -72,8 +96,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
         else:
             cmd = [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", *common, "-c", path,
                    "-o", obj]
-        jobs.append(cmd)
-    with cf.ThreadPoolExecutor(max_workers=min(4, len(jobs))) as ex:
+        if force or _obj_stale(path, obj):      # objects whose source and headers did not change are kept
+            jobs.append(cmd)
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(6, len(jobs)))) as ex:
         for fut in [ex.submit(_run, j) for j in jobs]:
             fut.result()
     tmp = target + ".tmp"

@@ -22,7 +22,7 @@ msg WriteRequestCommand type=1:RequestType id=2:i64 offset=3:i64 tier=4:i32 flus
     medium_type=8:str pin_on_create=9:bool space_to_reserve=10:i64
 msg WriteRequest command=1:WriteRequestCommand|value chunk=2:Chunk|value
 msg WriteResponse offset=1:i64
-msg NativeWriteCommitRequest session_id=1:i64 block_id=2:i64 length=3:i64 pin=4:bool
+msg NativeWriteCommitRequest session_id=1:i64 block_id=2:i64 length=3:i64 pin=4:bool ufs_read=5:bool
 msg AsyncCacheRequest block_id=1:i64 source_host=2:str source_port=3:i32
     open_ufs_block_options=4:alluxio.proto.dataserver.OpenUfsBlockOptions length=5:i64
 msg AsyncCacheResponse
@@ -53,6 +53,8 @@ msg CommitDeviceWriteResponse
 msg PeerTransferRequest block_id=1:i64 src_rank=2:i32 dst_rank=3:i32 offset=4:i64 length=5:i64
     tag=6:i64 src_address=7:str
 msg PeerTransferResponse ok=1:bool message=2:str
+msg SessionHeartbeatRequest session_ids=1:i64*
+msg SessionHeartbeatResponse unknown_session_ids=1:i64*
 
 rpc BlockWorker ReadBlock *ReadRequest *ReadResponse
 rpc BlockWorker WriteBlock *WriteRequest *WriteResponse
@@ -68,6 +70,7 @@ rpc BlockWorker PeerTransfer PeerTransferRequest PeerTransferResponse
 rpc BlockWorker NativeWriteCommit NativeWriteCommitRequest WriteResponse
 rpc BlockWorker OpenDeviceWrite OpenDeviceWriteRequest DeviceBlockHandle
 rpc BlockWorker CommitDeviceWrite CommitDeviceWriteRequest CommitDeviceWriteResponse
+rpc BlockWorker SessionHeartbeat SessionHeartbeatRequest SessionHeartbeatResponse
 
 # --- block master ----------------------------------------------------------------------------
 enum BlockMasterInfoField CAPACITY_BYTES=1 CAPACITY_BYTES_ON_TIERS=2 FREE_BYTES=3

@@ -164,6 +164,19 @@ class BlockWorker:
         with self._session_lock:
             self._sessions[session_id] = time.time()
 
+    def renew_sessions(self, session_ids) -> list[int]:
+        """Heartbeat of sessions a client holds open across calls (short-circuit device reads and
+        writes); returns the ids this worker no longer knows (already cleaned up)."""
+        now = time.time()
+        unknown = []
+        with self._session_lock:
+            for s in session_ids:
+                if s in self._sessions:
+                    self._sessions[s] = now
+                else:
+                    unknown.append(s)
+        return unknown
+
     def cleanup_session(self, session_id: int) -> None:
         with self._session_lock:
             self._sessions.pop(session_id, None)
@@ -351,17 +364,29 @@ class BlockWorker:
             self._ufs_cache[opts.mountId] = u
         return u
 
-    def note_local_ufs(self, mount_id: int, ufs) -> None:
-        """After a UFS_FILE write through Python: a mount whose UFS is a plain local directory is
-        registered with the native data server, which then writes that mount's UFS_FILE streams on
-        its I/O threads (csrc/data_server.cpp UfsFileWriteStream)."""
+    def note_ufs_mount(self, mount_id: int, ufs) -> None:
+        """After a UFS call served in Python: a mount whose UFS the native data server can reach
+        by itself is registered with it, so later calls of that mount stay on its I/O threads --
+        a plain local directory (UFS_FILE writes: csrc/data_server.cpp UfsFileWriteStream; cold
+        reads: pread) or a plain-HTTP S3 endpoint (cold reads: signed ranged GETs)."""
         from ..underfs.local import LocalUnderFileSystem
+        from ..underfs.s3 import S3UnderFileSystem
         roots = self.native_ufs_roots
-        uri = self._ufs_uris.get(mount_id)
-        if roots is None or uri is None or type(ufs) is not LocalUnderFileSystem:
+        if roots is None or not mount_id:
             return
-        if roots.resolve(mount_id, uri.rstrip("/") + "/x") is None:
-            roots.set(mount_id, uri)
+        if type(ufs) is LocalUnderFileSystem:
+            uri = self._ufs_uris.get(mount_id)
+            if uri is not None and roots.resolve(mount_id, uri.rstrip("/") + "/x") is None:
+                roots.set(mount_id, uri)
+        elif isinstance(ufs, S3UnderFileSystem) and ufs._native_on and \
+                self.conf.get_bool("alluxio.worker.data.server.native.ufs.read.enabled", "true"):
+            import urllib.parse
+            u = urllib.parse.urlsplit(ufs.client.endpoint)
+            if roots.resolve_s3(mount_id, f"s3://{ufs.bucket}/x") is None:
+                roots.set_s3(mount_id, u.hostname, u.port or 80, ufs.bucket, ufs.client.access_key,
+                             ufs.client.secret_key, ufs.client.region, ufs._parallel, ufs._part)
+
+    note_local_ufs = note_ufs_mount
 
     def ufs_block_target(self, mount_id: int, block_id: int):
         """(UFS, path) of the UFS block file of ``block_id`` under mount ``mount_id``

@@ -53,20 +53,31 @@ class WorkerDataServer:
             import os
             os.makedirs(os.path.dirname(domain_socket) or ".", exist_ok=True)
             lib().listen_unix(self.frontend.server, domain_socket)
+        # mounts the I/O threads reach by themselves (local directories, plain-HTTP S3), registered
+        # by the worker after it served a first call of the mount in Python (note_ufs_mount)
+        self.ufs_roots = lib().UfsMounts()
+        worker.native_ufs_roots = self.ufs_roots
+        native_cold = conf.get_bool("alluxio.worker.data.server.native.ufs.read.enabled", "true")
+        # ReadBlock: cached blocks from the store; cold blocks of registered mounts read through
+        # from the UFS on a background thread per call and committed via NativeWriteCommit
         self.stats = lib().serve_block_reads(
             self.frontend.server, self.frontend.method_index(READ_BLOCK_PATH), worker.native,
             conf.get_bytes("alluxio.worker.network.reader.max.chunk.size.bytes", "2MB"),
-            conf.get_bytes("alluxio.worker.network.reader.buffer.size", "4MB"))
+            conf.get_bytes("alluxio.worker.network.reader.buffer.size", "4MB"),
+            mounts=self.ufs_roots if native_cold else None,
+            commit_method=self.frontend.method_index(COMMIT_PATH),
+            ufs_slot_bytes=conf.get_bytes("alluxio.worker.ufs.ingest.chunk.size", "8MB"),
+            ufs_depth=conf.get_int("alluxio.worker.ufs.ingest.depth", "3"),
+            ufs_max_active=conf.get_int("alluxio.worker.data.server.native.ufs.read.max.active", "256"))
         # WriteBlock of ALLUXIO_BLOCK writes: chunks into the store on the I/O threads, the commit
         # (CRC, master report) as the internal NativeWriteCommit call (BlockWorkerService).
         # UFS_FILE writes of mounts the worker found to be local directories: into the file.
-        self.ufs_roots = lib().LocalUfsRoots()
-        if conf.get_bool("alluxio.worker.data.server.native.ufs.write.enabled", "true"):
-            worker.native_ufs_roots = self.ufs_roots
+        native_ufs_write = conf.get_bool("alluxio.worker.data.server.native.ufs.write.enabled", "true")
         lib().serve_block_writes(
             self.frontend.server, self.frontend.method_index(WRITE_BLOCK_PATH),
             self.frontend.method_index(COMMIT_PATH), worker.native,
-            conf.get_bytes("alluxio.worker.network.writer.staging.size", "4MB"), self.stats, self.ufs_roots)
+            conf.get_bytes("alluxio.worker.network.writer.staging.size", "4MB"), self.stats,
+            self.ufs_roots if native_ufs_write else None)
         self.port = None
 
     def start(self) -> int:
@@ -84,7 +95,15 @@ class WorkerDataServer:
         m.gauge("DataServerNativeWriteStreams", lambda: st.write_streams)
         m.gauge("DataServerNativeUfsWriteStreams", lambda: st.ufs_write_streams)
         m.counter("BytesWrittenUfsAll").add_source(lambda: st.ufs_write_bytes)
+        m.gauge("DataServerNativeColdStreams", lambda: st.cold_streams)
+        m.gauge("DataServerNativeColdActive", lambda: st.cold_active)
         return self.port
 
     def stop(self) -> None:
+        import time
         self.frontend.stop()
+        # background UFS readers of cancelled cold reads finish their current read, wait for their
+        # H2D copies and drop their temp blocks: the store must outlive them
+        deadline = time.time() + 30
+        while self.stats.cold_active > 0 and time.time() < deadline:
+            time.sleep(0.01)

@@ -80,6 +80,9 @@ class BlockWorkerService:
                                                                  first.open_ufs_block_options.block_in_ufs_tier):
                     from .ufs_fallback import resolve_ufs_block_opts
                     opts = resolve_ufs_block_opts(self.w, bid, first.open_ufs_block_options)
+                    if not first.open_ufs_block_options.block_in_ufs_tier:
+                        # the native data server reads later cold blocks of this mount itself
+                        self.w.note_ufs_mount(opts.mountId, self.w._ufs_for(opts))
                     if opts.no_cache or first.offset != 0 or self.w.native.has_temp_block(bid):
                         # partial / uncached reads (or another reader is caching it): plain stream
                         yield from self._stream_ufs(opts, first.offset, first.length, chunk, acked, cond, done)
@@ -193,6 +196,9 @@ class BlockWorkerService:
             from ..utils.exceptions import PermissionDeniedException
             raise PermissionDeniedException("NativeWriteCommit is internal to the worker's data server")
         self.w.commit_block(req.session_id, req.block_id, req.pin)
+        if req.ufs_read:      # a cold ReadBlock the native server read through from the UFS
+            self.w.metrics.counter("BytesReadUfsAll").inc(req.length)
+            self.w.metrics.counter("BytesReadUfsThrough").inc(req.length)
         return pb.block.WriteResponse(offset=req.length)
 
     def WriteBlock(self, request_iter, ctx):
@@ -287,7 +293,7 @@ class BlockWorkerService:
                 except Exception:  # noqa: BLE001
                     pass
         self.w.metrics.counter("BytesWrittenUfsAll").inc(pos)
-        self.w.note_local_ufs(o.mount_id, ufs)
+        self.w.note_ufs_mount(o.mount_id, ufs)
         yield pb.block.WriteResponse(offset=pos)
 
     # ------------------------------------------------------------------------------------------
@@ -402,8 +408,9 @@ class BlockWorkerService:
         """Short-circuit write for a same-node writer process (the analogue of CreateLocalBlock,
         whose writer fills a temp block file): create the temp block with ``length`` bytes of
         pages reserved and describe them like :meth:`OpenDeviceBlock`; the writer maps the arena
-        and copies into the pages itself, then calls :meth:`CommitDeviceWrite`.  An abandoned
-        write is reclaimed with its session (``alluxio.worker.session.timeout``)."""
+        and copies into the pages itself, then calls :meth:`CommitDeviceWrite`.  The client renews
+        the session while the write is open (:meth:`SessionHeartbeat`); an abandoned write is
+        reclaimed with its session (``alluxio.worker.session.timeout``)."""
         session = req.session_id or ids.create_session_id()
         length = max(int(req.length), 1)
         self.w.create_block(session, req.block_id, req.tier if not req.medium_type else -1, req.medium_type,
@@ -444,6 +451,12 @@ class BlockWorkerService:
         finally:
             self.w.cleanup_session(req.session_id)
         return pb.block.CommitDeviceWriteResponse()
+
+    def SessionHeartbeat(self, req, ctx):
+        """Keeps the sessions of open short-circuit handles alive (client/session_keeper.py): an
+        IPC-mapped write or read outlives any one RPC, so without renewals the session cleaner
+        would reclaim its pages under the client after ``alluxio.worker.session.timeout``."""
+        return pb.block.SessionHeartbeatResponse(unknown_session_ids=self.w.renew_sessions(list(req.session_ids)))
 
     def UnlockDeviceBlock(self, req, ctx):
         with self._lock:

@@ -455,6 +455,49 @@ def test_parallel_block_writes_of_one_large_write(tmp_path):
                 rfs.close()
 
 
+def test_parallel_block_write_failure_fails_stream(tmp_path, monkeypatch):
+    """A failure in one block of a parallel multi-block write commits none of the blocks, and the
+    stream stays failed: a later write() raises and close() cancels the file instead of completing
+    it with a hole."""
+    import threading
+
+    from alluxio_amd.client import streams
+    with _cluster(tmp_path) as c:
+        w = c.workers[0]
+        rfs = _remote_fs(c, **{"alluxio.user.block.size.bytes.default": "4MB",
+                               "alluxio.user.device.read.parallelism": "4"})
+        orig = streams.GrpcBlockWriter.write_ptr
+        calls = [0]
+        lock = threading.Lock()
+
+        def flaky(self, offset, ptr, length, kind):
+            with lock:
+                calls[0] += 1
+                k = calls[0]
+            if k == 2:
+                raise IOError("injected block write failure")
+            return orig(self, offset, ptr, length, kind)
+        monkeypatch.setattr(streams.GrpcBlockWriter, "write_ptr", flaky)
+        try:
+            data = np.random.default_rng(16).integers(0, 256, 16 << 20, dtype=np.uint8)
+            free0 = w.worker.native.dir_available(0)
+            f = rfs.create_file("/pwfail", write_type="MUST_CACHE")
+            with pytest.raises(IOError, match="injected"):
+                f.write(data)
+            assert calls[0] >= 2
+            with pytest.raises(IOError, match="failed earlier"):
+                f.write(data[:10])
+            with pytest.raises(IOError, match="cancelled"):
+                f.close()
+            assert not rfs.exists("/pwfail")
+            deadline = time.time() + 10                  # no block of it stays committed or open
+            while w.worker.native.dir_available(0) != free0:
+                assert time.time() < deadline
+                time.sleep(0.05)
+        finally:
+            rfs.close()
+
+
 def test_native_write_errors_and_cancel(tmp_path):
     with _cluster(tmp_path) as c:
         w = c.workers[0]
@@ -524,3 +567,209 @@ def test_short_circuit_write_into_shared_arena(tmp_path):
             assert free0 - w.worker.native.dir_available(0) == used
         finally:
             rfs.close()
+
+
+def test_short_circuit_write_survives_session_timeout(tmp_path):
+    """An open short-circuit write outlives alluxio.worker.session.timeout: the client's session
+    keeper renews it (SessionHeartbeat), so the cleaner does not hand its reserved pages to another
+    block while the writer still copies into them.  A handle nobody renews still expires."""
+    from alluxio_amd.client.context import worker_address_str
+    from alluxio_amd.client.streams import IpcBlockWriter
+    with _cluster(tmp_path, {"alluxio.worker.session.timeout": "600ms"}) as c:
+        w = c.workers[0]
+        rfs = _remote_fs(c, **{"alluxio.user.short.circuit.enabled": "true",
+                               "alluxio.worker.session.timeout": "600ms"})
+        try:
+            addr = worker_address_str(w.worker.address)
+            rng = np.random.default_rng(11)
+            data = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+            wr = IpcBlockWriter(rfs.ctx, addr, 777_001, 3 << 20)
+            wr.write_ptr(0, data.ctypes.data, 1 << 20, 0)
+            for _ in range(3):                               # cleaner passes, each past the timeout
+                time.sleep(0.7)
+                assert wr.session not in w.worker.cleanup_expired_sessions()
+            assert w.worker.native.has_temp_block(777_001)
+            other = rng.integers(0, 256, 4 << 20, dtype=np.uint8)
+            rfs.write_file("/other", other, write_type="MUST_CACHE")   # takes free pages now
+            wr.write_ptr(1 << 20, data.ctypes.data + (1 << 20), 2 << 20, 0)
+            wr.commit()
+            assert w.worker.has_block(777_001)
+            assert rfs.read_file("/other") == other.tobytes()
+            assert rfs.ctx.session_keeper().renewals >= 2
+            assert not rfs.ctx.session_keeper().open_sessions()
+            # nobody renews this one: the cleaner reclaims it as before
+            wr2 = IpcBlockWriter(rfs.ctx, addr, 777_002, 1 << 20)
+            rfs.ctx.session_keeper().remove(addr, wr2.session)
+            time.sleep(0.7)
+            assert wr2.session in w.worker.cleanup_expired_sessions()
+            assert not w.worker.native.has_temp_block(777_002)
+            wr2.h = None
+        finally:
+            rfs.close()
+
+
+def _read_request_call(port):
+    ch = grpc.insecure_channel(f"127.0.0.1:{port}")
+    spec = SERVICES[BW]["ReadBlock"]
+    return ch, ch.stream_stream(spec.path, spec.request.SerializeToString, spec.response.FromString)
+
+
+def test_native_cold_read_through(tmp_path):
+    """Cold blocks of a local-directory mount are read through by the native data server once the
+    mount is registered: each block streams to the client as its UFS slots land, is cached in the
+    store and committed (master sees it) before the call ends.  A partial read streams without
+    caching; a cancelled read-through leaves no temp block (UnderFileSystemBlockReader.java:251-274)."""
+    with _cluster(tmp_path, {"alluxio.worker.ufs.ingest.chunk.size": "1MB",
+                             "alluxio.worker.network.reader.buffer.size": "1MB"}) as c:
+        fs = c.client()
+        rng = np.random.default_rng(21)
+        files = {f"/cold/{k}": rng.integers(0, 256, (9 << 20) + 17 * (i + 1), dtype=np.uint8)
+                 for i, k in enumerate("abcd")}
+        for p, d in files.items():
+            fs.write_file(p, d, write_type="CACHE_THROUGH")
+        fs.free("/cold", recursive=True)
+        w = c.workers[0]
+        c.heartbeat_workers()
+        assert not w.worker.native.block_ids(-1)
+        st = w.data_server.stats
+        rfs = _remote_fs(c)
+        try:
+            assert rfs.read_file("/cold/a") == files["/cold/a"].tobytes()   # Python: registers the mount
+            assert len(w.data_server.ufs_roots) == 1
+            d0, s0, c0 = st.declined, st.cold_streams, st.cold_cached
+            free0 = w.worker.native.dir_available(0)
+            assert rfs.read_file("/cold/b") == files["/cold/b"].tobytes()
+            nb = len(_blocks(rfs, "/cold/b"))
+            assert st.declined == d0                       # nothing went to Python
+            assert st.cold_streams - s0 == nb
+            deadline = time.time() + 10                    # the client may see its last byte before the
+            while st.cold_cached - c0 < nb:                # commit that ends the call
+                assert time.time() < deadline
+                time.sleep(0.02)
+            assert st.cold_cached - c0 == nb
+            assert all(w.worker.has_block(b) for b, _ in _blocks(rfs, "/cold/b"))
+            assert rfs.get_status("/cold/b").in_alluxio_percentage == 100
+            assert free0 - w.worker.native.dir_available(0) >= files["/cold/b"].nbytes
+            assert rfs.read_file("/cold/b") == files["/cold/b"].tobytes()   # now from the store
+            # a positioned read inside a cold block: streamed, not cached
+            (bid, blen), = _blocks(rfs, "/cold/c")[1:2]
+            with rfs.open_file("/cold/c") as f:
+                f.seek(blen + 1000)
+                assert f.read(5000) == files["/cold/c"][blen + 1000:blen + 6000].tobytes()
+            assert not w.worker.has_block(bid)
+            # a read-through cancelled after its first chunk: the temp block is aborted
+            st_d = rfs.get_status("/cold/d")
+            (bid, blen) = _blocks(rfs, "/cold/d")[0]
+            opts = pb.dataserver.OpenUfsBlockOptions(
+                ufs_path=st_d.ufsPath, offset_in_file=0, block_size=blen, mountId=st_d.mountId)
+            ch, call = _read_request_call(w.data_server.port)
+            it = call(iter([pb.block.ReadRequest(block_id=bid, offset=0, length=blen, chunk_size=1 << 20,
+                                                 open_ufs_block_options=opts)]))
+            first = next(it)
+            assert first.chunk.data == files["/cold/d"][:1 << 20].tobytes()
+            it.cancel()
+            ch.close()
+            deadline = time.time() + 10
+            while st.cold_active or w.worker.native.has_temp_block(bid):
+                assert time.time() < deadline
+                time.sleep(0.05)
+            assert not w.worker.has_block(bid)
+            assert rfs.read_file("/cold/d") == files["/cold/d"].tobytes()
+        finally:
+            rfs.close()
+            fs.close()
+
+
+def test_native_cold_read_through_s3(tmp_path):
+    """Cold blocks of an S3 mount (native BlobServer endpoint) are read through by the data server's
+    own signed ranged GETs once the first read in Python registered the mount."""
+    srv = lib().BlobServer(str(tmp_path / "blobs"), "127.0.0.1", 0)
+    srv.start()
+    try:
+        base = f"http://127.0.0.1:{srv.port}"
+        import requests
+        assert requests.put(base + "/bkt").status_code == 200
+        rng = np.random.default_rng(22)
+        objs = {k: rng.integers(0, 256, (6 << 20) + 5 * i, dtype=np.uint8) for i, k in enumerate(("x", "y"))}
+        for k, d in objs.items():
+            assert requests.put(f"{base}/bkt/ds/{k}", data=d.tobytes()).status_code == 200
+        with _cluster(tmp_path) as c:
+            fs = c.client()
+            fs.mount("/s3", "s3://bkt/ds", properties={"alluxio.underfs.s3.endpoint": base,
+                                                       "s3a.accessKeyId": "AKID", "s3a.secretKey": "sk"})
+            w = c.workers[0]
+            st = w.data_server.stats
+            rfs = _remote_fs(c)
+            try:
+                assert rfs.read_file("/s3/x") == objs["x"].tobytes()          # Python, registers the mount
+                mid = rfs.get_status("/s3/y").mountId
+                assert w.data_server.ufs_roots.resolve_s3(mid, "s3://bkt/ds/y") == ("bkt", "ds/y")
+                d0, s0, b0 = st.declined, st.cold_streams, st.cold_bytes
+                assert rfs.read_file("/s3/y") == objs["y"].tobytes()
+                nb = len(_blocks(rfs, "/s3/y"))
+                assert st.declined == d0 and st.cold_streams - s0 == nb
+                assert st.cold_bytes - b0 == objs["y"].nbytes
+                deadline = time.time() + 10
+                while not all(w.worker.has_block(b) for b, _ in _blocks(rfs, "/s3/y")):
+                    assert time.time() < deadline
+                    time.sleep(0.02)
+            finally:
+                rfs.close()
+                fs.close()
+    finally:
+        srv.stop()
+
+
+def test_sigv4_matches_python_signer():
+    import datetime
+
+    from alluxio_amd.underfs import s3
+    cl = s3.S3Client("http://127.0.0.1:9000", "AKID", "SECRET/KEY+x", "eu-west-1")
+    when = datetime.datetime(2024, 5, 6, 7, 8, 9, tzinfo=datetime.timezone.utc)
+
+    class Fixed(datetime.datetime):
+        @classmethod
+        def now(cls, tz=None):
+            return when
+    real = s3.datetime.datetime
+    s3.datetime.datetime = Fixed
+    try:
+        for path in ("/bkt/a b/c+d.bin", "/bkt/plain/key", "/bkt/ü/x"):
+            h = cl._headers("GET", path, {}, s3._EMPTY_SHA)
+            lines = lib().sigv4_headers("127.0.0.1:9000", "AKID", "SECRET/KEY+x", "eu-west-1", "GET", path, "",
+                                        s3._EMPTY_SHA, "20240506T070809Z")
+            got = dict(line.split(": ", 1) for line in lines.strip().split("\r\n"))
+            assert got["authorization"] == h["authorization"]
+    finally:
+        s3.datetime.datetime = real
+    import hashlib
+    for data in (b"", b"abc", bytes(range(256)) * 300):
+        assert lib().sha256_hex(data) == hashlib.sha256(data).hexdigest()
+
+
+def test_ack_beyond_sent_bytes_does_not_stall(tmp_path):
+    """An offset_received past what was sent is clamped (it used to wrap the unsigned window test
+    and park the call, read lock held, forever)."""
+    import threading
+    with _cluster(tmp_path, {"alluxio.worker.network.reader.buffer.size": "1MB"}) as c:
+        fs = c.client()
+        data = np.random.default_rng(23).integers(0, 256, 4 << 20, dtype=np.uint8)
+        fs.write_file("/ack", data, write_type="MUST_CACHE")
+        (bid, blen), = _blocks(fs, "/ack")
+        got_first = threading.Event()
+
+        def reqs():
+            yield pb.block.ReadRequest(block_id=bid, offset=0, length=blen, chunk_size=256 << 10)
+            got_first.wait(10)
+            yield pb.block.ReadRequest(offset_received=1 << 40)
+            for k in range(1, 40):                          # then honest acks, chunk by chunk
+                time.sleep(0.02)
+                yield pb.block.ReadRequest(offset_received=min(blen, k * (256 << 10)))
+        ch, call = _read_request_call(c.workers[0].data_server.port)
+        out = bytearray()
+        for r in call(reqs(), timeout=20):
+            out += r.chunk.data
+            got_first.set()
+        ch.close()
+        assert bytes(out) == data.tobytes()
+        fs.close()
