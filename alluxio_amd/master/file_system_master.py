@@ -1091,6 +1091,13 @@ class FileSystemMaster(Journaled):
                       pinned_media=None) -> None:
         path = normalize_path(path)
         self._count("Master.SetAttributeOps")
+        if pinned and pinned_media:
+            # only media of the cluster count (alluxio.master.tieredstore.global.mediumtype; this
+            # build's HBM and DRAM tiers always do); others are dropped as in the reference
+            known = {m.strip().upper() for m in str(
+                self.conf.get("alluxio.master.tieredstore.global.mediumtype", "MEM,SSD,HDD") if self.conf
+                else "MEM,SSD,HDD").split(",") if m.strip()} | {"HBM", "DRAM"}
+            pinned_media = [m for m in pinned_media if m.upper() in known]
         ufs_attr = owner is not None or group is not None or mode is not None
         with self._lock_path(path):
             if ufs_attr:
@@ -1904,20 +1911,27 @@ class FileSystemMaster(Journaled):
             self.block_master.remove_blocks(sorted(set(orphans)), delete=True)
         return sorted(set(orphans))
 
-    def replication_targets(self):
-        """(file path, block id, current replicas, min, max) for files with replication limits."""
-        out = []
+    def pinned_file_ids(self) -> list[int]:
+        """Pinned files (a file with replicationMin > 0 is pinned): InodeTree.getPinIdSet."""
         with self.tree.lock.read():
-            for fid in list(self.tree.replication_limited):
-                f = self.tree.inodes.get(fid)
-                if f is None or not f.completed:
-                    continue
-                p = self.tree.path_of(f)
-                for bid in f.block_ids:
-                    bi = self.block_master.block_info_or_none(bid)
-                    n = len(bi.locations) if bi is not None else 0
-                    out.append((p, bid, n, f.replication_min, f.replication_max, f.pinned))
-        return out
+            return [i for i in self.tree.pinned_ids if (n := self.tree.inodes.get(i)) is not None and n.is_file]
+
+    def replication_limited_file_ids(self) -> list[int]:
+        with self.tree.lock.read():
+            return list(self.tree.replication_limited)
+
+    def replication_view(self, file_id: int):
+        """Snapshot of what the replication checker needs of a completed file, or None."""
+        import types
+        with self.tree.lock.read():
+            f = self.tree.inodes.get(file_id)
+            if f is None or not f.is_file or not f.completed:
+                return None
+            return types.SimpleNamespace(
+                path=self.tree.path_of(f), block_ids=list(f.block_ids), replication_min=f.replication_min,
+                replication_max=f.replication_max, replication_durable=f.replication_durable,
+                persistence_state=f.persistence_state, persisted=f.is_persisted,
+                medium_types=list(f.medium_types), pinned=f.pinned)
 
     def total_paths(self) -> int:
         return len(self.tree.inodes)

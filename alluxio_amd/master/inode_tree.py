@@ -147,6 +147,8 @@ class InodeTree:
         self._index(inode)
 
     def _index(self, inode: Inode) -> None:
+        if inode.is_file and inode.replication_min > 0:
+            inode.pinned = True           # a file that must keep copies is pinned (applyCreateInode)
         if inode.pinned:
             self.pinned_ids.add(inode.id)
         else:
@@ -208,6 +210,17 @@ class InodeTree:
             return
         old_parent, old_name = inode.parent_id, inode.name
         inode.update_from(u)
+        if u.HasField("pinned") and inode.is_file:
+            # InodeTreePersistentState.applyUpdateInode: pinning a file pins it to the listed media
+            # (none listed = any medium) and raises replicationMin 0 -> 1; unpinning drops it to 0
+            if u.pinned:
+                inode.medium_types = list(u.medium_type)
+                if inode.replication_min == 0:
+                    inode.replication_min = 1
+                    if inode.replication_max == 0:
+                        inode.replication_max = -1
+            else:
+                inode.replication_min = 0
         if inode.parent_id != old_parent or inode.name != old_name:
             kids = self.children.get(old_parent)
             if kids is not None and kids.get(old_name) == inode.id:

@@ -136,7 +136,7 @@ class AlluxioMasterProcess:
             self.table_master.job_master = self.job_master
         if self.job_master is not None:
             from .replication import ReplicationChecker
-            self.replication_checker = ReplicationChecker(self.fs_master, self.job_master)
+            self.replication_checker = ReplicationChecker(self.fs_master, self.job_master, safe_mode=self.safe_mode)
         self.web = None
         self.selector = None
         self._standby_hb = None

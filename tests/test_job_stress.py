@@ -237,7 +237,7 @@ def test_replication_checker(cluster):
         time.sleep(0.01)
     assert sum(w.worker.has_block(bid) for w in cluster.workers) == 2
     for _ in range(300):         # the copy landed; let the job report COMPLETED before re-checking
-        if not rc._busy(bid):
+        if not rc.handler._running(("replicate", bid)):
             break
         cluster.drive_jobs()
         time.sleep(0.01)
@@ -252,3 +252,54 @@ def test_replication_checker(cluster):
         time.sleep(0.01)
     assert sum(w.worker.has_block(bid) for w in cluster.workers) == 1
     fs.close()
+
+
+def _drive_until(cluster, cond, n=500):
+    for _ in range(n):
+        cluster.drive_jobs()
+        if cond():
+            return True
+        time.sleep(0.01)
+    return cond()
+
+
+def test_replication_checker_pins_to_medium_and_recaches_from_ufs(tmp_path):
+    """Mis-replication: a file pinned to SSD whose block sits in MEM is moved into the SSD tier by a
+    move job (ReplicationChecker.checkMisreplicated -> migrate).  Under-replication at 0 copies: a
+    persisted file's freed block is re-cached from the UFS by the replicate job."""
+    conf = {"alluxio.worker.tieredstore.levels": "2",
+            "alluxio.worker.tieredstore.level0.alias": "MEM",
+            "alluxio.worker.tieredstore.level0.dirs.path": "dram",
+            "alluxio.worker.tieredstore.level0.dirs.quota": "16MB",
+            "alluxio.worker.tieredstore.level1.alias": "SSD",
+            "alluxio.worker.tieredstore.level1.dirs.path": str(tmp_path / "ssd"),
+            "alluxio.worker.tieredstore.level1.dirs.quota": "64MB",
+            "alluxio.worker.tieredstore.level1.dirs.mediumtype": "SSD",
+            "alluxio.worker.hbm.page.size": "256KB",
+            "alluxio.user.block.size.bytes.default": "1MB"}
+    os.makedirs(tmp_path / "ssd", exist_ok=True)
+    with LocalAlluxioCluster(num_workers=1, conf=conf) as c:
+        fs = c.client()
+        w = c.workers[0].worker
+        rc = c.master.replication_checker
+        data = os.urandom(MB)
+        fs.write_file("/pin/f", data, write_type="CACHE_THROUGH")
+        bid = fs.get_status("/pin/f").block_ids[0]
+        assert w.native.block_info(bid).medium == "DRAM"
+        fs.set_attribute("/pin/f", pinned=True, pinned_media=["SSD"])
+        assert rc.heartbeat() == 1                        # one move job
+        assert _drive_until(c, lambda: w.native.block_info(bid).medium == "SSD")
+        c.heartbeat_workers()
+        assert fs.read_file("/pin/f") == data
+        assert _drive_until(c, lambda: not rc.handler._running(("move", bid)))
+        assert rc.heartbeat() == 0                        # in place now
+        # the cached copy is freed: the pinned, persisted file is re-cached from the UFS
+        fs.set_attribute("/pin/f", pinned=False)
+        fs.set_attribute("/pin/f", replication_min=1)
+        w.remove_block(1, bid)
+        c.heartbeat_workers()
+        assert fs.get_status("/pin/f").in_alluxio_percentage == 0
+        assert rc.heartbeat() == 1
+        assert _drive_until(c, lambda: w.has_block(bid))
+        assert fs.read_file("/pin/f") == data
+        fs.close()
