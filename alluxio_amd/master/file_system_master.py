@@ -156,6 +156,11 @@ class FileSystemMaster(Journaled):
         # callers copy them into their reply, never mutate them.
         self._rc = (None, {}, {}, {})
         self._fi_cache_max = conf.get_int("alluxio.master.metadata.reply.cache.size", "100000") if conf else 100000
+        from .access_time import AccessTimeUpdater
+        self.access_time = AccessTimeUpdater(
+            self, conf.get_ms("alluxio.master.file.access.time.journal.flush.interval") if conf else 3_600_000,
+            conf.get_ms("alluxio.master.file.access.time.update.precision") if conf else 86_400_000,
+            conf.get_ms("alluxio.master.file.access.time.updater.shutdown.timeout") if conf else 1000)
 
     # ------------------------------------------------------------------------------------------
     # Journaled
@@ -333,6 +338,7 @@ class FileSystemMaster(Journaled):
     def start(self, is_primary: bool = True) -> None:
         if not is_primary:
             return
+        self.access_time.start()
         if self.tree.root is None:
             self._initialize_root()
         if self.mount_table.get("/") is None:
@@ -710,17 +716,24 @@ class FileSystemMaster(Journaled):
         self._count("Master.GetFileInfoOps")
         self._maybe_sync(path, sync_interval_ms, recursive=False)
         get = self.cached_file_info_bytes if raw else self.cached_file_info
+        # an open (READ / WRITE access with updateTimestamps) records an access of the inode
+        touch = update_timestamps and bool(access_mode & (Bits.READ | Bits.WRITE))
         with self.tree.lock.read():
             chain, missing = self.tree.resolve(path)
             if not missing:
                 self._check(chain, Bits.NONE, path)
-                return get(chain[-1], path)
-        if load_metadata == LOAD_NEVER:
-            raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
-        self._load_missing(path, load_metadata)
-        with self.tree.lock.read():
-            inode = self.tree.get(path)
-            return get(inode, path)
+                out = get(chain[-1], path)
+                inode = chain[-1]
+        if missing:
+            if load_metadata == LOAD_NEVER:
+                raise FileDoesNotExistException(f"Path \"{path}\" does not exist.")
+            self._load_missing(path, load_metadata)
+            with self.tree.lock.read():
+                inode = self.tree.get(path)
+                out = get(inode, path)
+        if touch:
+            self.access_time.update(inode)
+        return out
 
     def _load_missing(self, path: str, load_metadata: str) -> None:
         """Load a path Alluxio does not have from the UFS, through the absent-path cache: a path
@@ -773,6 +786,13 @@ class FileSystemMaster(Journaled):
         if inode.is_directory and load_metadata != LOAD_NEVER and inode.is_persisted and \
                 (load_metadata == LOAD_ALWAYS or not inode.direct_children_loaded):
             self.load_metadata(path, recursive=recursive, create_ancestors=False, quiet=True)
+        out, listed = self._list_status_locked(path, recursive, raw)
+        if listed is not None:           # a listed directory was accessed (listStatusInternal)
+            self.access_time.update(listed)
+        return out
+
+    def _list_status_locked(self, path: str, recursive: bool, raw: bool):
+        """(listing, the directory listed or None) under the tree read lock."""
         with self.tree.lock.read():
             chain, missing = self.tree.resolve(path)
             if missing:
@@ -781,13 +801,13 @@ class FileSystemMaster(Journaled):
             self._check(chain, Bits.READ if inode.is_directory else Bits.NONE, path)
             if not inode.is_directory:
                 if raw:
-                    return [length_delimited(0x0A, self.cached_file_info_bytes(inode, path))]
-                return [self.cached_file_info(inode, path)]
+                    return [length_delimited(0x0A, self.cached_file_info_bytes(inode, path))], None
+                return [self.cached_file_info(inode, path)], None
             rc = self._reply_cache()
             lkey = (inode.id, path, recursive, raw)
             hit = rc[3].get(lkey)
             if hit is not None:
-                return hit
+                return hit, inode
             out = []
             stack = [(inode, path)]
             while stack:
@@ -814,7 +834,7 @@ class FileSystemMaster(Journaled):
                 out = msgs or [b""]
             if rc[0] == self._cache_epoch() and len(rc[3]) < 4096:
                 rc[3][lkey] = out
-            return out
+            return out, inode
 
     def _raw_children(self, kids, dp: str) -> list:
         """Serialized ``fileInfos`` entries of ``kids`` (children of ``dp``) as (count, bytes)
@@ -910,11 +930,10 @@ class FileSystemMaster(Journaled):
             return self.file_info(inode)
 
     def update_access_time(self, path: str) -> None:
-        with RpcContext(self) as rpc, self.tree.lock.write():
+        with self.tree.lock.read():
             inode = self.tree.get_or_none(normalize_path(path))
-            if inode is not None:
-                self._apply(rpc, pb.journal.JournalEntry(update_inode=pb.journal.UpdateInodeEntry(
-                    id=inode.id, last_access_time_ms=rpc.op_time_ms)))
+        if inode is not None:
+            self.access_time.update(inode)
 
     # ------------------------------------------------------------------------------------------
     # delete / rename / free

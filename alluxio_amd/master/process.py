@@ -98,6 +98,8 @@ class AlluxioMasterProcess:
         self.meta_master = MetaMaster(self.conf, self.journal)
         self.meta_master.block_master = self.block_master
         self.metrics_master = MetricsMaster()
+        from .time_series import TimeSeriesRecorder
+        self.time_series = TimeSeriesRecorder(self.block_master, self.metrics_master, self._root_ufs_space)
         self.block_master.metrics = lambda w, ms: self.metrics_master.worker_heartbeat(w.id, ms)
         self.state_lock = StateLockManager()
         self.fs_master.state_lock = self.state_lock
@@ -159,6 +161,12 @@ class AlluxioMasterProcess:
         reg.gauge("Cluster.CapacityUsed", bm.used_bytes)
         reg.gauge("Cluster.CapacityFree", lambda: bm.capacity_bytes() - bm.used_bytes())
         reg.gauge("Cluster.Workers", bm.worker_count)
+
+    def _root_ufs_space(self):
+        """(total, used) bytes of the root mount's UFS (Cluster.RootUfsCapacity*)."""
+        from ..underfs.base import SpaceType
+        res = self.fs_master._resolve_ufs("/")
+        return (res.ufs.get_space(res.uri, SpaceType.SPACE_TOTAL), res.ufs.get_space(res.uri, SpaceType.SPACE_USED))
 
     def _primary_candidates(self) -> list[str]:
         return [a.strip() for a in (self.conf.get_raw("alluxio.master.rpc.addresses") or "").split(",") if a.strip()]
@@ -352,6 +360,10 @@ class AlluxioMasterProcess:
         threads, self._threads = self._threads, []
         for t in threads:
             t.shutdown(join=False)
+        try:
+            self.fs_master.access_time.stop()     # batched access times are journaled first
+        except Exception:  # noqa: BLE001
+            LOG.debug("access time flush at step-down failed", exc_info=True)
         with self.state_lock.exclusive():
             self.journal.lose_primacy()
 
@@ -369,6 +381,8 @@ class AlluxioMasterProcess:
              c.get_ms("alluxio.master.ufs.active.sync.interval", "30sec")),
             (hb.MASTER_LOST_MASTER_DETECTION, self.meta_master.detect_lost_masters,
              c.get_ms("alluxio.master.standby.heartbeat.interval", "2min")),
+            (hb.MASTER_METRICS_TIME_SERIES, self.time_series.heartbeat,
+             c.get_ms("alluxio.master.metrics.time.series.interval")),
         ]
         if self.job_master is not None:
             specs.append((hb.MASTER_PERSISTENCE_CHECKER, self.persistence_checker,
@@ -434,6 +448,10 @@ class AlluxioMasterProcess:
         if self._job_client_fs is not None:
             self._job_client_fs.close()
             self._job_client_fs = None
+        try:
+            self.fs_master.access_time.stop()     # AccessTimeUpdater.beforeShutdown
+        except Exception:  # noqa: BLE001
+            LOG.debug("access time flush at shutdown failed", exc_info=True)
         self.journal.stop()
         if self.selector is not None:
             self.selector.stop()

@@ -171,6 +171,7 @@ def master_webui_routes(master) -> dict:
                       "operationMetrics": {k: v for k, v in sorted(cluster.items()) if k.startswith("Master.")},
                       "rpcInvocationMetrics": {k: v for k, v in sorted(master.metrics.registry.snapshot().items())},
                       "ufsOps": {k: v for k, v in sorted(cluster.items()) if "Ufs" in k},
+                      "timeSeriesMetrics": master.time_series.store.series() if hasattr(master, "time_series") else [],
                       **pick("Cluster.BytesReadLocal", "Cluster.BytesReadRemote", "Cluster.BytesReadUfsAll",
                              "Cluster.BytesWrittenLocal", "Cluster.BytesWrittenUfsAll")})
 

@@ -347,6 +347,9 @@ def test_webui_spa_and_json(cluster):
     assert any(r[0] == "alluxio.master.journal.folder" for r in j("webui_config")["configuration"])
     assert "/" in j("webui_mounttable")["mountPointInfos"]
     assert "operationMetrics" in j("webui_metrics") and "refreshInterval" in j("webui_init")
+    cluster.master.time_series.heartbeat()                   # the TimeSeriesRecorder heartbeat
+    tsm = {s["name"]: s["dataPoints"] for s in j("webui_metrics")["timeSeriesMetrics"]}
+    assert "% Alluxio Space Used" in tsm and tsm["Cluster.BytesReadUfsThroughput"]
     wk = cluster.workers[0]
     wbase = f"http://127.0.0.1:{wk.web_port}"
     assert 'data-role="worker"' in urllib.request.urlopen(wbase + "/webui", timeout=10).read().decode()

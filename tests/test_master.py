@@ -209,3 +209,66 @@ def test_block_master_worker_lifecycle(master):
     assert bm.worker_count() == 0 and bm.lost_worker_count() == 1
     assert 77 in bm.lost_blocks()
     assert bm.get_worker_id(addr) == wid  # re-registration keeps the id
+
+
+def _atime(m, path):
+    return m.fs_master.get_status(path, update_timestamps=False).lastAccessTimeMs
+
+
+def test_access_time_updates_journaled_and_replayed(tmp_path):
+    """AccessTimeUpdater: an open (getStatus with READ access) and a listing advance
+    lastAccessTimeMs past the precision; batched updates are journaled at the flush (or stop) and
+    survive a restart (reference AccessTimeUpdater.java, DefaultFileSystemMaster.java:882,1103)."""
+    for flush in ("0", "1h"):
+        jdir = tmp_path / f"journal{flush}"
+        conf = Configuration({"alluxio.master.journal.folder": str(jdir),
+                              "alluxio.security.authorization.permission.enabled": "false",
+                              "alluxio.master.file.access.time.update.precision": "0",
+                              "alluxio.master.file.access.time.journal.flush.interval": flush})
+        m = AlluxioMasterProcess(conf, port=0, enable_grpc=False, root_ufs=str(tmp_path / f"ufs{flush}"))
+        m.start(start_heartbeats=False)
+        fs = m.fs_master
+        fs.create_directory("/d")
+        fs.create_file("/d/f", write_type="MUST_CACHE")
+        fs.complete_file("/d/f")
+        t0, d0 = _atime(m, "/d/f"), _atime(m, "/d")
+        time.sleep(0.02)
+        fs.get_status("/d/f", access_mode=0)                 # no access mode: not an access
+        assert _atime(m, "/d/f") == t0
+        fs.get_status("/d/f")                                # READ access (an open)
+        t1 = _atime(m, "/d/f")
+        assert t1 > t0
+        fs.list_status("/d")
+        assert _atime(m, "/d") > d0
+        upd = fs.access_time
+        assert upd.updates >= 2
+        assert bool(upd._pending) == (flush != "0")          # batched: journaled at the flush / stop
+        m.stop()                                             # flushes the batch
+        m2 = AlluxioMasterProcess(conf, port=0, enable_grpc=False, root_ufs=str(tmp_path / f"ufs{flush}"))
+        m2.start(start_heartbeats=False)
+        assert _atime(m2, "/d/f") == t1
+        m2.stop()
+
+
+def test_access_time_precision_skips_updates(master):
+    fs = master.fs_master
+    fs.create_file("/p", write_type="MUST_CACHE")
+    fs.complete_file("/p")
+    n = fs.access_time.updates
+    fs.get_status("/p")                                      # default precision: 1 day
+    assert fs.access_time.updates == n
+
+
+def test_time_series_recorder(master):
+    ts = master.time_series
+    ts.heartbeat()
+    master.metrics_master._cluster["Cluster.BytesReadUfsAll"] = 6 << 20
+    ts._last = (ts._last[0] - 60.0, ts._last[1])             # one minute later
+    ts.heartbeat()
+    series = {s["name"]: s["dataPoints"] for s in ts.store.series()}
+    assert {"% Alluxio Space Used", "% UFS Space Used", "Cluster.BytesReadUfsThroughput",
+            "Cluster.BytesWrittenAlluxioThroughput"} <= set(series)
+    assert len(series["% Alluxio Space Used"]) == 2
+    assert series["Cluster.BytesReadUfsThroughput"][-1]["value"] == pytest.approx(6 << 20, rel=0.01)
+    assert 0 <= series["% UFS Space Used"][-1]["value"] <= 100
+    assert {"timeStamp", "value"} == set(series["% UFS Space Used"][0])
