@@ -68,6 +68,8 @@ class FileSystemContext:
         self.worker_list_ttl = self.conf.get_ms("alluxio.user.worker.list.refresh.interval", "2min") / 1000.0
         self._closed = False
         self._keeper = None
+        from ..parallel.ipc import set_open_timeout
+        set_open_timeout(self.conf.get_ms("alluxio.user.short.circuit.open.timeout", "30s"))
         self._metrics_hb = None
         if self.conf.get_bool("alluxio.user.metrics.collection.enabled"):
             from ..utils import heartbeat as hb

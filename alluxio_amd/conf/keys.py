@@ -238,6 +238,14 @@ _k("WORKER_DATA_SERVER_NATIVE_UFS_READ_ENABLED", "alluxio.worker.data.server.nat
    "into a temp block and the I/O thread streams it as it lands; the block is committed at the end.")
 _k("WORKER_DATA_SERVER_NATIVE_UFS_READ_MAX_ACTIVE", "alluxio.worker.data.server.native.ufs.read.max.active",
    "256", Scope.WORKER, "Concurrent native cold reads (one UFS reader thread each); more go to Python.")
+_k("UNDERFS_OBJECT_STORE_UPLOAD_BUFFER_SIZE", "alluxio.underfs.object.store.upload.buffer.size", "256MB",
+   Scope.SERVER,
+   "Memory one object-store write may hold in multipart part buffers (parts of "
+   "alluxio.underfs.s3.streaming.upload.partition.size): parts in flight = this / the part size, so an "
+   "object of any size is written with bounded memory.")
+_k("USER_SHORT_CIRCUIT_OPEN_TIMEOUT", "alluxio.user.short.circuit.open.timeout", "30s", Scope.CLIENT,
+   "Deadline of importing a worker's HBM arena through HIP IPC; an import that has not returned by "
+   "then makes short-circuit unavailable for that arena and the client reads over the data port.")
 _k("USER_FILE_CACHE_THROUGH_OVERLAP_MIN", "alluxio.user.file.cache.through.overlap.min", "256KB", Scope.CLIENT,
    "CACHE_THROUGH write() calls of at least this many bytes send the UFS copy on the stream's helper "
    "thread while the cache copy runs; smaller ones write the two one after the other.")

@@ -302,6 +302,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("page_size", &DirSpec::page_size)
       .def_readwrite("device", &DirSpec::device)
       .def_readwrite("path", &DirSpec::path)
+      .def_readwrite("owns_base", &DirSpec::owns_base)
       .def_readwrite("reserved", &DirSpec::reserved);
 
   py::class_<BlockInfoOut>(m, "BlockInfo")
@@ -566,6 +567,16 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<const std::string&, int, int>(), py::arg("host"), py::arg("port"), py::arg("max_idle") = 16)
       .def("get_into", &HttpRangeReader::get_into, G(), py::arg("target"), py::arg("head_lines"), py::arg("offset"),
            py::arg("length"), py::arg("dst"), py::arg("parallel") = 1, py::arg("min_part") = 4 << 20)
+      .def("put_from", [](HttpRangeReader& r, const std::string& target, const std::string& head, uint64_t src,
+                          uint64_t length) {
+             std::string etag;
+             int code;
+             {
+               py::gil_scoped_release rel;
+               code = r.put_from(target, head, src, length, &etag);
+             }
+             return py::make_tuple(code, etag);
+           }, py::arg("target"), py::arg("head_lines"), py::arg("src"), py::arg("length"))
       .def_property_readonly("requests", &HttpRangeReader::requests)
       .def_property_readonly("connects", &HttpRangeReader::connects);
 
@@ -719,7 +730,21 @@ PYBIND11_MODULE(_C, m) {
           py::gil_scoped_release rel;
           return ipc_open(h, device);
         }, py::arg("handle"), py::arg("device"));
+  m.def("ipc_open_bounded", [](py::bytes handle, int device, int timeout_ms) {
+          std::string h = handle;
+          py::gil_scoped_release rel;
+          return ipc_open_bounded(h, device, timeout_ms);
+        }, py::arg("handle"), py::arg("device"), py::arg("timeout_ms"));
+  py::register_exception<IpcTimeout>(m, "IpcTimeout", PyExc_TimeoutError);
   m.def("ipc_close", [](uint64_t base) { py::gil_scoped_release rel; ipc_close(base); });
+  m.def("device_arena_alloc", [](uint64_t bytes, int device) {
+          py::gil_scoped_release rel;
+          return device_arena_alloc(bytes, device);
+        }, py::arg("bytes"), py::arg("device"));
+  m.def("device_arena_free", [](uint64_t ptr, int device) {
+          py::gil_scoped_release rel;
+          device_arena_free(ptr, device);
+        }, py::arg("ptr"), py::arg("device"));
   m.def("enable_peer_access", &enable_peer_access, py::arg("device"), py::arg("peer"));
   // page-lock an existing host mapping (shared-memory DRAM arenas) so kernels can read it
   m.def("host_register", [](uint64_t ptr, uint64_t n) {

@@ -120,6 +120,11 @@ BlockStore::~BlockStore() {
     for (auto& d : dirs_) {
       if (d->mag_bits) hipFree(d->mag_bits);
       if (d->mag_upd) hipFree(d->mag_upd);
+      // the HBM arena lives exactly as long as the store that hands out its pages
+      if (d->spec.owns_base && d->spec.kind == DirKind::kDevice && d->spec.base) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(reinterpret_cast<void*>(d->spec.base));
+      }
     }
     for (ClaimScratch* cp : {&claim_[0], &claim_[1], &claim_one_}) {
       ClaimScratch& c = *cp;

@@ -67,6 +67,7 @@ struct DirSpec {
   int device = 0;
   std::string path;        // file dirs
   uint64_t reserved = 0;   // reserved bytes (watermark headroom) not used by allocation
+  bool owns_base = false;  // device arena allocated for the store: hipFree'd with it
 };
 
 struct StorageDir {

@@ -375,7 +375,8 @@ void bind_data_path(py::module_& m) {
       .def(py::init<>())
       .def("set", &UfsMounts::set, py::arg("mount_id"), py::arg("root"))
       .def("set_s3", &UfsMounts::set_s3, py::arg("mount_id"), py::arg("host"), py::arg("port"), py::arg("bucket"),
-           py::arg("access_key"), py::arg("secret_key"), py::arg("region"), py::arg("parallel"), py::arg("part"))
+           py::arg("access_key"), py::arg("secret_key"), py::arg("region"), py::arg("parallel"), py::arg("part"),
+           py::arg("upload_part") = 64u << 20, py::arg("upload_inflight") = 4)
       .def("remove", &UfsMounts::remove, py::arg("mount_id"))
       .def("__len__", &UfsMounts::size)
       .def("resolve", [](const UfsMounts& r, int64_t mount_id, const std::string& path) -> py::object {

@@ -9,6 +9,8 @@
 
 #include <cerrno>
 #include <condition_variable>
+#include <deque>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -398,6 +400,7 @@ struct ColdState {
   std::condition_variable cv;
   std::vector<Slot> slots;
   bool cancelled = false, read_done = false, failed = false, job_exited = false, caching = false;
+  bool handed_off = false;      // the cached block went to the commit: its session is not ours
   std::string err;
   std::function<void()> wake;
   std::shared_ptr<StagingPool> pool;
@@ -417,6 +420,8 @@ struct ColdJob {
   std::unique_ptr<UfsReader> reader;
   std::shared_ptr<ColdState> st;
   std::shared_ptr<DataServerStats> stats;
+  std::function<void(uint32_t, std::string)> post;   // internal requests to Python (the commit)
+  uint32_t commit_method = UINT32_MAX;
 
   void wake() {
     std::function<void()> w;
@@ -434,6 +439,7 @@ struct ColdJob {
     hipStream_t hs = nullptr;
     std::string err;
     bool ok = true;
+    uint64_t ingested = start;
     try {
       if (store->has_device()) {
         store->use_device();
@@ -490,6 +496,7 @@ struct ColdJob {
           sl->len = n;
           sl->ready = true;
         }
+        ingested = off + n;
         wake();
       }
     } catch (const std::exception& e) {
@@ -497,9 +504,16 @@ struct ColdJob {
       err = e.what();
     }
     if (hs) {
-      (void)hipStreamSynchronize(hs);   // every H2D out of the slots is done before commit / abort
+      if (hipStreamSynchronize(hs) != hipSuccess && ok) {   // every H2D is done before commit / abort
+        ok = false;
+        err = "H2D into the block failed";
+      }
       (void)hipStreamDestroy(hs);
     }
+    // UnderFileSystemBlockReader.close: a block read through to its end is committed -- also when
+    // the client went away after the last byte -- anything less is aborted
+    const bool complete = ok && ingested >= end;
+    const bool commit = caching && complete && post && commit_method != UINT32_MAX;
     bool cancelled;
     {
       std::lock_guard<std::mutex> g(st->mu);
@@ -510,12 +524,27 @@ struct ColdJob {
       }
       st->read_done = true;
       st->job_exited = true;
+      st->handed_off = commit;
       cancelled = st->cancelled;
     }
-    if (cancelled || !ok) {   // a read-through nobody completes: drop the temp block
+    if (commit) {
+      // NativeWriteCommitRequest: session_id=1 block_id=2 length=3 pin=4 ufs_read=5; Python
+      // commits (CRC, master report) and drops the session, whether or not the call still exists
+      std::string m;
+      h2::put_varint(m, (1u << 3));
+      h2::put_varint(m, (uint64_t)session);
+      h2::put_varint(m, (2u << 3));
+      h2::put_varint(m, (uint64_t)block);
+      h2::put_varint(m, (3u << 3));
+      h2::put_varint(m, block_len);
+      h2::put_varint(m, (5u << 3));
+      h2::put_varint(m, 1);
+      post(commit_method, std::move(m));
+      stats->cold_cached.fetch_add(1, std::memory_order_relaxed);
+    } else if (caching || cancelled || !ok) {
       if (caching) stats->cold_aborted.fetch_add(1, std::memory_order_relaxed);
       try {
-        store->cleanup_session(session);
+        store->cleanup_session(session);   // drops the temp block of an incomplete read-through
       } catch (...) {
       }
     }
@@ -527,24 +556,25 @@ struct ColdJob {
 class ColdReadStream : public NativeStream {
  public:
   ColdReadStream(BlockStore* store, int64_t session, int64_t block_id, uint64_t pos, uint64_t end, uint64_t chunk,
-                 uint64_t window, uint64_t slot_bytes, uint32_t commit_method, bool unix_peer,
-                 std::shared_ptr<ColdState> st, std::shared_ptr<DataServerStats> stats)
+                 uint64_t window, uint64_t slot_bytes, bool unix_peer, std::shared_ptr<ColdState> st,
+                 std::shared_ptr<DataServerStats> stats)
       : store_(store), session_(session), block_(block_id), start_(pos), pos_(pos), acked_(pos), end_(end),
-        chunk_(chunk), window_(window), slot_bytes_(slot_bytes), commit_(commit_method), unix_(unix_peer),
-        st_(std::move(st)), stats_(std::move(stats)) {}
+        chunk_(chunk), window_(window), slot_bytes_(slot_bytes), unix_(unix_peer), st_(std::move(st)),
+        stats_(std::move(stats)) {}
 
   ~ColdReadStream() override {
-    bool exited;
+    bool exited, handed_off;
     {
       std::lock_guard<std::mutex> g(st_->mu);
       st_->cancelled = true;
       st_->wake = nullptr;
       exited = st_->job_exited;
+      handed_off = st_->handed_off;
     }
     st_->cv.notify_all();
-    // a running reader cleans up itself once it sees the cancel; after it exited, this drops the
-    // session (and with it a temp block nobody committed, e.g. a cancel after the last byte)
-    if (exited) {
+    // a running reader cleans up itself once it sees the cancel; a block handed to the commit is
+    // Python's; otherwise the (exited) reader's session goes here
+    if (exited && !handed_off) {
       try {
         store_->cleanup_session(session_);
       } catch (...) {
@@ -561,34 +591,6 @@ class ColdReadStream : public NativeStream {
     ReadRequestMsg r;
     if (parse_read_request(p, n, &r) && r.has_ack && (uint64_t)r.offset_received > acked_)
       acked_ = std::min<uint64_t>((uint64_t)r.offset_received, pos_);
-  }
-
-  bool take_post(uint32_t* method, std::string* payload) override {
-    if (!post_ready_) return false;
-    post_ready_ = false;
-    // NativeWriteCommitRequest: session_id=1 block_id=2 length=3 pin=4 ufs_read=5
-    std::string m;
-    h2::put_varint(m, (1u << 3));
-    h2::put_varint(m, (uint64_t)session_);
-    h2::put_varint(m, (2u << 3));
-    h2::put_varint(m, (uint64_t)block_);
-    h2::put_varint(m, (3u << 3));
-    h2::put_varint(m, end_);
-    h2::put_varint(m, (5u << 3));
-    h2::put_varint(m, 1);
-    *method = commit_;
-    *payload = std::move(m);
-    return true;
-  }
-
-  void on_reply(int status, const std::string& msg, const std::string&) override {
-    commit_done_ = true;
-    if (status == 0) {
-      committed_ = true;
-      stats_->cold_cached.fetch_add(1, std::memory_order_relaxed);
-    } else {
-      commit_err_ = msg;   // the client still got every byte: the call succeeds, the block is not cached
-    }
   }
 
   ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
@@ -612,29 +614,7 @@ class ColdReadStream : public NativeStream {
         if (left_ == 0 && pos_ >= slot_end_) release_slot();
         continue;
       }
-      if (pos_ >= end_) {
-        bool done, failed, caching;
-        std::string err;
-        {
-          std::lock_guard<std::mutex> g(st_->mu);
-          done = st_->read_done;
-          failed = st_->failed;
-          caching = st_->caching;
-          err = st_->err;
-        }
-        if (!done) break;                       // the H2D of the last slots still runs
-        if (failed) {
-          *status = 13;
-          *msg = "UFS read of block " + std::to_string(block_) + ": " + err;
-          return w ? (ssize_t)w : -1;
-        }
-        if (caching && !commit_done_) {
-          if (!posted_) {
-            posted_ = true;
-            post_ready_ = true;                  // read_body posts it right after this call
-          }
-          break;
-        }
+      if (pos_ >= end_) {            // every byte sent (the reader commits the cache by itself)
         *eof = true;
         break;
       }
@@ -685,7 +665,6 @@ class ColdReadStream : public NativeStream {
   BlockStore* store_;
   int64_t session_, block_;
   uint64_t start_, pos_, acked_, end_, chunk_, window_, slot_bytes_;
-  uint32_t commit_;
   bool unix_;
   std::shared_ptr<ColdState> st_;
   std::shared_ptr<DataServerStats> stats_;
@@ -694,8 +673,6 @@ class ColdReadStream : public NativeStream {
   uint64_t left_ = 0, slot_end_ = 0;
   const uint8_t* src_ = nullptr;
   ColdState::Slot* cur_slot_ = nullptr;
-  bool posted_ = false, post_ready_ = false, commit_done_ = false, committed_ = false;
-  std::string commit_err_;
 };
 
 // ---- WriteBlock ---------------------------------------------------------------------------------
@@ -1103,6 +1080,388 @@ class UfsFileWriteStream : public WriteStreamBase {
   std::shared_ptr<DataServerStats> stats_;
 };
 
+
+// ---- UFS_FILE writes into an S3 mount: streamed multipart upload -------------------------------
+
+// Upload threads shared by every S3 write stream (immortal: a stuck HTTP call never blocks exit).
+class UploadPool {
+ public:
+  static UploadPool& get() {
+    static UploadPool* p = new UploadPool(16);
+    return *p;
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  explicit UploadPool(int n) {
+    for (int i = 0; i < n; ++i)
+      std::thread([this] {
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return !q_.empty(); });
+            f = std::move(q_.front());
+            q_.pop_front();
+          }
+          try {
+            f();
+          } catch (...) {
+          }
+        }
+      }).detach();
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
+
+std::string xml_tag(const std::string& x, const std::string& tag) {
+  const std::string a = "<" + tag + ">", b = "</" + tag + ">";
+  const size_t i = x.find(a);
+  if (i == std::string::npos) return "";
+  const size_t j = x.find(b, i + a.size());
+  return j == std::string::npos ? "" : x.substr(i + a.size(), j - i - a.size());
+}
+
+std::string query_escape(const std::string& v) {   // RFC 3986, '/' escaped too (SigV4 query)
+  std::string e = uri_encode_path(v), o;
+  for (char c : e) {
+    if (c == '/') o += "%2F";
+    else o.push_back(c);
+  }
+  return o;
+}
+
+// State of one multipart upload shared by its stream (I/O thread) and its upload tasks.
+struct S3Upload {
+  std::shared_ptr<const S3Mount> m;
+  std::string path;                 // "/bucket/key"
+  std::mutex mu;
+  std::condition_variable cv;
+  std::string upload_id;
+  bool init_started = false, init_done = false;
+  std::map<int, std::string> etags;
+  int inflight = 0;                 // part uploads queued or running
+  std::vector<uint8_t*> free_bufs;
+  int allocated = 0;
+  bool failed = false, cancelled = false, finishing = false, finished = false;
+  std::string err;
+  std::function<void()> wake;
+  std::shared_ptr<DataServerStats> stats;
+
+  ~S3Upload() {
+    for (uint8_t* b : free_bufs) std::free(b);
+  }
+
+  int send(const std::string& method, const std::string& query, const uint8_t* body, uint64_t n, std::string* resp,
+           std::string* etag, const std::string& payload_hash = "UNSIGNED-PAYLOAD") {
+    const std::string head = s3_header_lines(m->cred, method, path, query, payload_hash);
+    const std::string target = uri_encode_path(path) + (query.empty() ? "" : "?" + query);
+    return m->reader->request(method, target, head, body, n, resp, etag);
+  }
+
+  void poke() {
+    std::function<void()> w;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      w = wake;
+    }
+    if (w) w();
+  }
+
+  // CreateMultipartUpload, once (the first part's task runs it; the others wait).
+  bool ensure_init(std::string* e) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (!init_started) {
+      init_started = true;
+      lk.unlock();
+      std::string resp;
+      const int code = send("POST", "uploads=", nullptr, 0, &resp, nullptr);
+      const std::string id = code == 200 ? xml_tag(resp, "UploadId") : "";
+      lk.lock();
+      if (id.empty() && !failed) {
+        failed = true;
+        err = "CreateMultipartUpload of " + path + " failed: " + std::to_string(code);
+      }
+      upload_id = id;
+      init_done = true;
+      cv.notify_all();
+    }
+    cv.wait(lk, [&] { return init_done; });
+    if (upload_id.empty()) {
+      *e = err;
+      return false;
+    }
+    return true;
+  }
+
+  // Runs on an upload thread: UploadPart `num` out of `buf` (returned to the free list).
+  static void upload_part(std::shared_ptr<S3Upload> u, int num, uint8_t* buf, uint64_t n) {
+    std::string e, etag;
+    bool skip;
+    {
+      std::lock_guard<std::mutex> g(u->mu);
+      skip = u->cancelled || u->failed;
+    }
+    bool ok = skip ? false : u->ensure_init(&e);
+    if (ok) {
+      const std::string q = "partNumber=" + std::to_string(num) + "&uploadId=" + query_escape(u->upload_id);
+      const int code = u->send("PUT", q, buf, n, nullptr, &etag);
+      ok = code == 200 || code == 204;
+      if (!ok) e = "UploadPart " + std::to_string(num) + " of " + u->path + " failed: " + std::to_string(code);
+      else u->stats->ufs_write_bytes.fetch_add(n, std::memory_order_relaxed);
+    }
+    bool last;
+    {
+      std::lock_guard<std::mutex> g(u->mu);
+      if (ok) u->etags[num] = etag;
+      else if (!skip && !u->failed) {
+        u->failed = true;
+        u->err = e;
+      }
+      u->free_bufs.push_back(buf);
+      last = --u->inflight == 0 && (u->finishing || u->cancelled || u->failed);
+    }
+    if (last) finish(u);
+    u->poke();
+  }
+
+  // After the last part: CompleteMultipartUpload, or AbortMultipartUpload on failure / cancel.
+  static void finish(std::shared_ptr<S3Upload> u) {
+    bool abort;
+    std::string id;
+    {
+      std::lock_guard<std::mutex> g(u->mu);
+      if (u->finished) return;
+      abort = u->failed || u->cancelled;
+      id = u->upload_id;
+      if (!abort && !u->finishing) return;
+    }
+    std::string e;
+    if (abort) {
+      if (!id.empty()) u->send("DELETE", "uploadId=" + query_escape(id), nullptr, 0, nullptr, nullptr);
+    } else {
+      std::string body = "<CompleteMultipartUpload>";
+      {
+        std::lock_guard<std::mutex> g(u->mu);
+        for (const auto& kv : u->etags)
+          body += "<Part><PartNumber>" + std::to_string(kv.first) + "</PartNumber><ETag>" + kv.second +
+                  "</ETag></Part>";
+      }
+      body += "</CompleteMultipartUpload>";
+      std::string resp;
+      const int code = u->send("POST", "uploadId=" + query_escape(id), reinterpret_cast<const uint8_t*>(body.data()),
+                               body.size(), &resp, nullptr, sha256_hex(body.data(), body.size()));
+      if (code != 200 || resp.find("<Error>") != std::string::npos) {
+        e = "CompleteMultipartUpload of " + u->path + " failed: " + std::to_string(code);
+        u->send("DELETE", "uploadId=" + query_escape(id), nullptr, 0, nullptr, nullptr);
+      }
+    }
+    {
+      std::lock_guard<std::mutex> g(u->mu);
+      if (!e.empty() && !u->failed) {
+        u->failed = true;
+        u->err = e;
+      }
+      u->finished = true;
+    }
+    u->poke();
+  }
+};
+
+class S3UfsWriteStream : public WriteStreamBase {
+ public:
+  S3UfsWriteStream(std::shared_ptr<const S3Mount> m, const std::string& key, std::shared_ptr<DataServerStats> stats)
+      : part_(m->upload_part), max_bufs_(m->upload_inflight + 1), u_(std::make_shared<S3Upload>()) {
+    u_->m = std::move(m);
+    u_->path = "/" + u_->m->bucket + "/" + key;
+    u_->stats = std::move(stats);
+  }
+
+  ~S3UfsWriteStream() override {
+    bool idle;
+    {
+      std::lock_guard<std::mutex> g(u_->mu);
+      u_->wake = nullptr;
+      if (!u_->finished && !(u_->finishing && !u_->failed)) u_->cancelled = true;   // abandoned: abort
+      idle = u_->inflight == 0;
+    }
+    if (cur_) std::free(cur_);
+    if (idle && u_->cancelled) {
+      auto u = u_;
+      UploadPool::get().submit([u] { S3Upload::finish(u); });
+    }
+  }
+
+  void set_waker(std::function<void()> w) override {
+    std::lock_guard<std::mutex> g(u_->mu);
+    u_->wake = std::move(w);
+  }
+
+  bool accepting() override {
+    drain_overflow();
+    return overflow_.empty();
+  }
+
+  void on_message(const char* p, size_t n) override {
+    if (err_ || ended_) return;
+    WriteCmd cmd;
+    bool has_cmd;
+    const uint8_t* chunk;
+    size_t len;
+    if (!parse_write_request(p, n, &cmd, &has_cmd, &chunk, &len)) {
+      fail(3, "malformed WriteRequest");
+      return;
+    }
+    if (len) {
+      if (!overflow_.empty()) {
+        overflow_.append(reinterpret_cast<const char*>(chunk), len);
+      } else {
+        const size_t took = append(chunk, len);
+        if (took < len) overflow_.append(reinterpret_cast<const char*>(chunk + took), len - took);
+      }
+      pos_ += len;
+    }
+    if (has_cmd && cmd.flush) out_ += write_response_frame(pos_);   // S3 has nothing to flush
+  }
+
+  bool on_end(uint32_t*, std::string*) override {
+    ended_ = true;
+    if (err_) return false;
+    end_pending_ = true;
+    try_finish();
+    return false;
+  }
+
+  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    drain_overflow();
+    if (end_pending_) try_finish();
+    {
+      std::lock_guard<std::mutex> g(u_->mu);
+      if (u_->failed && !err_) fail(13, u_->err);
+      else if (u_->finished && !done_ && !err_ && submitted_end_) {
+        out_ += write_response_frame(pos_);
+        done_ = true;
+      }
+    }
+    return WriteStreamBase::produce(dst, max, eof, status, msg);
+  }
+
+ private:
+  uint8_t* take_buf() {
+    std::lock_guard<std::mutex> g(u_->mu);
+    if (!u_->free_bufs.empty()) {
+      uint8_t* b = u_->free_bufs.back();
+      u_->free_bufs.pop_back();
+      return b;
+    }
+    if (u_->allocated >= max_bufs_) return nullptr;
+    uint8_t* b = static_cast<uint8_t*>(std::malloc(part_));
+    if (b) ++u_->allocated;
+    return b;
+  }
+
+  // Copies into part buffers, submitting each full one; returns the bytes taken (fewer when every
+  // buffer is in flight: the rest waits in overflow_ and the request window is held back).
+  size_t append(const uint8_t* p, size_t n) {
+    size_t done = 0;
+    while (done < n) {
+      if (!cur_) {
+        cur_ = take_buf();
+        fill_ = 0;
+        if (!cur_) break;
+      }
+      const size_t k = (size_t)std::min<uint64_t>(n - done, part_ - fill_);
+      std::memcpy(cur_ + fill_, p + done, k);
+      fill_ += k;
+      done += k;
+      if (fill_ == part_) submit();
+    }
+    return done;
+  }
+
+  void submit() {
+    uint8_t* b = cur_;
+    const uint64_t n = fill_;
+    cur_ = nullptr;
+    fill_ = 0;
+    const int num = ++parts_;
+    {
+      std::lock_guard<std::mutex> g(u_->mu);
+      ++u_->inflight;
+    }
+    auto u = u_;
+    UploadPool::get().submit([u, num, b, n] { S3Upload::upload_part(u, num, b, n); });
+  }
+
+  void drain_overflow() {
+    if (overflow_.empty()) return;
+    const size_t took = append(reinterpret_cast<const uint8_t*>(overflow_.data()), overflow_.size());
+    overflow_.erase(0, took);
+  }
+
+  void try_finish() {
+    if (!overflow_.empty() || submitted_end_) return;
+    submitted_end_ = true;
+    end_pending_ = false;
+    if (parts_ == 0) {                 // smaller than a part: one PutObject
+      uint8_t* b = cur_;
+      const uint64_t n = fill_;
+      cur_ = nullptr;
+      {
+        std::lock_guard<std::mutex> g(u_->mu);
+        ++u_->inflight;
+        u_->init_started = u_->init_done = true;
+      }
+      auto u = u_;
+      UploadPool::get().submit([u, b, n] {
+        std::string e;
+        const int code = u->send("PUT", "", b, n, nullptr, nullptr);
+        if (code == 200 || code == 204) u->stats->ufs_write_bytes.fetch_add(n, std::memory_order_relaxed);
+        std::lock_guard<std::mutex> g(u->mu);
+        if (code != 200 && code != 204 && !u->failed) {
+          u->failed = true;
+          u->err = "PutObject " + u->path + " failed: " + std::to_string(code);
+        }
+        if (b) u->free_bufs.push_back(b);
+        --u->inflight;
+        u->finished = true;
+        u->cv.notify_all();
+        auto w = u->wake;
+        if (w) w();
+      });
+      return;
+    }
+    if (fill_) submit();
+    bool idle;
+    {
+      std::lock_guard<std::mutex> g(u_->mu);
+      u_->finishing = true;
+      idle = u_->inflight == 0;
+    }
+    if (idle) {
+      auto u = u_;
+      UploadPool::get().submit([u] { S3Upload::finish(u); });
+    }
+  }
+
+  uint64_t part_;
+  int max_bufs_;
+  std::shared_ptr<S3Upload> u_;
+  uint8_t* cur_ = nullptr;
+  uint64_t fill_ = 0, pos_ = 0;
+  int parts_ = 0;
+  std::string overflow_;
+  bool end_pending_ = false, submitted_end_ = false;
+};
+
 }  // namespace
 
 namespace {
@@ -1124,8 +1483,10 @@ void UfsMounts::remove(int64_t mount_id) {
 
 void UfsMounts::set_s3(int64_t mount_id, const std::string& host, int port, const std::string& bucket,
                        const std::string& access_key, const std::string& secret_key, const std::string& region,
-                       int parallel, uint64_t part) {
+                       int parallel, uint64_t part, uint64_t upload_part, int upload_inflight) {
   auto m = std::make_shared<S3Mount>();
+  m->upload_part = std::max<uint64_t>(upload_part, 64u << 10);
+  m->upload_inflight = std::max(1, upload_inflight);
   m->host = host;
   m->port = port;
   m->bucket = bucket;
@@ -1199,7 +1560,8 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, BlockSto
                                                uint64_t window, bool unix_peer, const ColdReadConfig& cfg,
                                                const std::shared_ptr<UfsMounts>& mounts,
                                                const std::shared_ptr<StagingPool>& slot_pool,
-                                               const std::shared_ptr<DataServerStats>& stats, int* status,
+                                               const std::shared_ptr<DataServerStats>& stats,
+                                               std::function<void(uint32_t, std::string)> post, int* status,
                                                std::string* msg) {
   UfsOpts o;
   if (!mounts || !parse_ufs_opts(r.ufs_opts, &o) || o.ufs_path.empty() || o.block_in_ufs_tier || o.block_size <= 0)
@@ -1253,10 +1615,12 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, BlockSto
   job->reader = std::move(reader);
   job->st = st;
   job->stats = stats;
+  job->post = std::move(post);
+  job->commit_method = cfg.commit_method;
   const uint64_t chunk =
       r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk) : std::min<uint64_t>(1u << 20, max_chunk);
   std::unique_ptr<NativeStream> ns(new ColdReadStream(store, job->session, r.block_id, off, end, chunk, window,
-                                                      slot_pool->size(), cfg.commit_method, unix_peer, st, stats));
+                                                      slot_pool->size(), unix_peer, st, stats));
   stats->cold_streams.fetch_add(1, std::memory_order_relaxed);
   try {
     std::thread([job] { job->run(); }).detach();
@@ -1281,7 +1645,6 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
   FrameRpcServer* s = &srv;
   srv.set_native_stream(method, [=](const std::string& first, const std::string& cid, const std::string& user,
                                     bool unix_peer, int* status, std::string* msg) -> std::unique_ptr<NativeStream> {
-    (void)user;
     ReadRequestMsg r;
     if (!parse_read_request(first.data(), first.size(), &r)) {
       *status = 3;   // INVALID_ARGUMENT
@@ -1308,7 +1671,8 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
     }
     if (lock < 0) {
       if (r.has_ufs) {     // a cold block: read it through from the UFS (BlockReadHandler.openUfsBlock)
-        auto cs = make_cold_stream(r, store, max_chunk, window, unix_peer, cold, mounts, slot_pool, stats, status, msg);
+        auto cs = make_cold_stream(r, store, max_chunk, window, unix_peer, cold, mounts, slot_pool, stats,
+                                   s->internal_poster(cid, user), status, msg);
         if (cs || *status != 0) return cs;
       }
       stats->declined.fetch_add(1, std::memory_order_relaxed);
@@ -1367,7 +1731,14 @@ void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_me
       *msg = cid.empty() ? "channel is not authenticated (no channel-id)" : "channel " + cid + " is not authenticated";
       return nullptr;
     }
-    std::string local;
+    std::string local, key;
+    std::shared_ptr<const S3Mount> s3;
+    if (cmd.type == 1 && cmd.has_ufs_file && ufs_roots && ufs_roots->resolve_s3(cmd.ufs_mount, cmd.ufs_path, &s3, &key)) {
+      auto ws = std::unique_ptr<S3UfsWriteStream>(new S3UfsWriteStream(std::move(s3), key, stats));
+      stats->ufs_write_streams.fetch_add(1, std::memory_order_relaxed);
+      if (len) ws->on_message(first.data(), first.size());
+      return ws;
+    }
     if (cmd.type == 1 && cmd.has_ufs_file && ufs_roots && ufs_roots->resolve(cmd.ufs_mount, cmd.ufs_path, &local)) {
       auto us = std::unique_ptr<UfsFileWriteStream>(
           new UfsFileWriteStream(local, cmd.ufs_mode > 0 ? (int)(cmd.ufs_mode & 07777) : 0644, stats));

@@ -59,6 +59,8 @@ struct S3Mount {
   S3Credentials cred;
   int parallel = 8;            // concurrent sub-range GETs of one read
   uint64_t part = 4u << 20;    // minimum sub-range
+  uint64_t upload_part = 64u << 20;   // multipart upload part of a UFS_FILE write
+  int upload_inflight = 4;            // part buffers of one write (bounded memory)
   std::shared_ptr<HttpRangeReader> reader;
 };
 
@@ -71,7 +73,7 @@ class UfsMounts {
   void set(int64_t mount_id, const std::string& root);
   void set_s3(int64_t mount_id, const std::string& host, int port, const std::string& bucket,
               const std::string& access_key, const std::string& secret_key, const std::string& region,
-              int parallel, uint64_t part);
+              int parallel, uint64_t part, uint64_t upload_part = 64u << 20, int upload_inflight = 4);
   void remove(int64_t mount_id);
   size_t size() const;
   // The local path of `ufs_path` ("file:///x" or "/x") if mount `mount_id` is a registered local
@@ -117,8 +119,10 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
 // as the internal unary `commit_method` (NativeWriteCommitRequest) whose reply ends the call.
 // UFS_FILE writes under a local mount of `ufs_roots` (may be null) are written natively too: a temp
 // file beside the target, renamed over it at the half-close (reference UfsFileWriteHandler.java
-// with the local UFS's AtomicFileOutputStream).  Other UFS_FILE and UFS_FALLBACK_BLOCK writes go
-// to the Python servicer.
+// with the local UFS's AtomicFileOutputStream); under an S3 mount they become a multipart upload
+// whose parts go out on upload threads while the client streams (S3ALowLevelOutputStream), with
+// the request window held back while every part buffer is in flight.  Other UFS_FILE and
+// UFS_FALLBACK_BLOCK writes go to the Python servicer.
 void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
                         uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
                         std::shared_ptr<UfsMounts> ufs_roots = nullptr);

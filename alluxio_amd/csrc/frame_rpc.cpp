@@ -151,6 +151,7 @@ struct FrameRpcServer::H2 {
     std::string path, cid, auser, in, out;
     size_t out_off = 0;
     bool dispatched = false, headers_sent = false, finished = false;
+    size_t held = 0;           // native stream: received bytes whose window is returned when it accepts again
     int fin_status = 0;
     std::string fin_msg;
     std::shared_ptr<Bridge> bridge;
@@ -294,7 +295,10 @@ int FrameRpcServer::H2::on_data(void*, uint8_t, int32_t sid, const uint8_t* data
   it->second.in.append(reinterpret_cast<const char*>(data), len);
   // a native stream takes every message as soon as it is complete: return its window as the
   // bytes arrive, so a message larger than the stream window cannot stall the call
-  if (it->second.native) S.consume_streams.emplace_back(sid, len);
+  if (it->second.native) {
+    if (it->second.native->accepting()) S.consume_streams.emplace_back(sid, len);
+    else it->second.held += len;            // backpressure: the client waits for this window
+  }
   return 0;
 }
 
@@ -333,7 +337,10 @@ void FrameRpcServer::H2::take_messages(Session& S, int32_t sid, Stream& st, bool
       dispatch(S, sid, st, std::string(body, len));
       // bytes after the first message arrived before the stream was native: return them now
       // (later ones are returned on arrival, in on_data)
-      if (st.native && st.in.size() > off) S.consume_streams.emplace_back(sid, st.in.size() - off);
+      if (st.native && st.in.size() > off) {
+        if (st.native->accepting()) S.consume_streams.emplace_back(sid, st.in.size() - off);
+        else st.held += st.in.size() - off;
+      }
     } else if (st.native) {
       st.native->on_message(body, len);             // no copy: data chunks go straight to the store
       h2::lib().resume_data(S.ng, sid);     // the message may reopen the window
@@ -1080,6 +1087,31 @@ void FrameRpcServer::wake(uint64_t token) {
   }
 }
 
+std::function<void(uint32_t, std::string)> FrameRpcServer::internal_poster(const std::string& cid,
+                                                                          const std::string& user) {
+  std::shared_ptr<WakeHub> hub = hub_;
+  std::string caller = "\x02\x01" + cid;
+  caller.push_back('\0');
+  caller += user;
+  return [hub, caller](uint32_t method, std::string payload) {
+    if (!hub) return;
+    std::lock_guard<std::mutex> g(hub->mu);
+    FrameRpcServer* srv = hub->srv;
+    if (!srv || method >= srv->lanes_.size()) return;
+    FrameRequest rq;
+    rq.token = 0;               // connection 0 never exists: respond() drops the reply
+    rq.method = method;
+    rq.user = caller;
+    rq.payload = std::move(payload);
+    Lane& l = *srv->lane_q_[srv->lanes_[method]];
+    {
+      std::lock_guard<std::mutex> lg(l.mu);
+      l.q.push_back(std::move(rq));
+    }
+    l.cv.notify_one();
+  };
+}
+
 void FrameRpcServer::run_wakes(int idx) {
   uint64_t cnt;
   while (::read(wake_fds_[idx], &cnt, sizeof(cnt)) > 0) {
@@ -1096,7 +1128,13 @@ void FrameRpcServer::run_wakes(int idx) {
     {
       std::lock_guard<std::mutex> g(c->wmu);
       if (!c->h2) continue;
-      h2::lib().resume_data(c->h2->ng, (int32_t)(t & 0x7fffffffu));
+      const int32_t sid = (int32_t)(t & 0x7fffffffu);
+      auto it = c->h2->streams.find(sid);
+      if (it != c->h2->streams.end() && it->second.held && it->second.native && it->second.native->accepting()) {
+        h2::lib().consume_stream(c->h2->ng, sid, it->second.held);   // the paused upload resumes
+        it->second.held = 0;
+      }
+      h2::lib().resume_data(c->h2->ng, sid);
       ok = H2::flush_locked(*c->h2);
     }
     if (!ok) close_conn(c->id);

@@ -69,6 +69,9 @@ class NativeStream {
   // Polled after every produce(): true = post {*method, *payload} to Python now as an internal
   // request (as on_end() does at the half-close); the reply comes back through on_reply().
   virtual bool take_post(uint32_t* method, std::string* payload) { return false; }
+  // false = the call holds enough unprocessed request bytes: stop returning receive window to the
+  // client (it pauses its uploads) until the stream calls its waker with accepting() true again.
+  virtual bool accepting() { return true; }
 };
 // Builds the native stream of a call from its first request message and the caller's identity
 // (the channel-id and alluxio-user headers).  nullptr with *status == 0 hands the call to the
@@ -114,6 +117,10 @@ class FrameRpcServer {
   void set_native_stream(uint32_t method, NativeStreamFactory factory);
   // Re-poll the native stream of `token` ((conn id << 32) | stream id) on its I/O thread.
   void wake(uint64_t token);
+  // A poster of internal requests (as a native stream's on_end posts) that belong to no call:
+  // queued on the method's lane as caller {cid, user}, their replies dropped.  The returned
+  // function stays safe to call from any thread after the call or the server is gone.
+  std::function<void(uint32_t, std::string)> internal_poster(const std::string& cid, const std::string& user);
   // ---- kind-2 bridge (Python side; the GIL is released around the blocking calls) ----------
   // 0 = a message in *out, 1 = the client half-closed, 2 = cancelled / connection gone, 3 = timeout.
   int stream_recv(uint64_t token, int timeout_ms, std::string* out);

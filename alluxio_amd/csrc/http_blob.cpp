@@ -1,5 +1,7 @@
 #include "http_blob.h"
 
+#include <atomic>
+
 #include <arpa/inet.h>
 #include <dirent.h>
 #include <fcntl.h>
@@ -346,8 +348,8 @@ void BlobServer::serve_conn(int fd) {
       };
       auto body_to_fd = [&](int out) -> bool {
         bool ok = true;
-        while (body_left) {
-          if (buf.empty() && !recv_more()) return false;
+        // what already arrived with the headers
+        if (!buf.empty() && body_left) {
           const size_t k = (size_t)std::min<uint64_t>(body_left, buf.size());
           size_t w = 0;
           while (ok && w < k) {
@@ -357,6 +359,47 @@ void BlobServer::serve_conn(int fd) {
           }
           buf.erase(0, k);
           body_left -= k;
+        }
+        // the rest socket -> pipe -> file with splice (no user-space copy), else through a buffer
+        int pp[2] = {-1, -1};
+        if (ok && body_left >= (1u << 20) && ::pipe2(pp, O_CLOEXEC) == 0) {
+          (void)::fcntl(pp[1], F_SETPIPE_SZ, 1 << 20);
+          while (ok && body_left) {
+            const ssize_t n = ::splice(fd, nullptr, pp[1], nullptr, (size_t)std::min<uint64_t>(body_left, 1u << 20),
+                                       SPLICE_F_MOVE | SPLICE_F_MORE);
+            if (n < 0 && errno == EINTR) continue;
+            if (n <= 0) {
+              ok = false;
+              break;
+            }
+            ssize_t moved = 0;
+            while (moved < n) {
+              const ssize_t m = ::splice(pp[0], nullptr, out, nullptr, (size_t)(n - moved), SPLICE_F_MOVE);
+              if (m < 0 && errno == EINTR) continue;
+              if (m <= 0) {
+                ok = false;
+                break;
+              }
+              moved += m;
+            }
+            body_left -= (uint64_t)n;
+          }
+          ::close(pp[0]);
+          ::close(pp[1]);
+          return ok;
+        }
+        std::vector<char> big((size_t)std::min<uint64_t>(std::max<uint64_t>(body_left, 1), 1u << 20));
+        while (ok && body_left) {
+          const ssize_t r = ::recv(fd, big.data(), (size_t)std::min<uint64_t>(body_left, big.size()), 0);
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) return false;
+          size_t w = 0;
+          while (ok && w < (size_t)r) {
+            const ssize_t k = ::write(out, big.data() + w, (size_t)r - w);
+            if (k <= 0) ok = false;
+            else w += (size_t)k;
+          }
+          body_left -= (uint64_t)r;
         }
         return ok;
       };
@@ -437,6 +480,39 @@ void BlobServer::serve_conn(int fd) {
           }
           ok = reply(200, "Content-Type: application/xml\r\n",
                      "<?xml version=\"1.0\" encoding=\"UTF-8\"?><DeleteResult></DeleteResult>");
+        } else if (method == "GET" && q.count("uploads")) {
+          // ListMultipartUploads: the uploads of this bucket (under `prefix`) still open
+          const std::string prefix = q.count("prefix") ? q["prefix"] : "";
+          std::string items;
+          const std::string ud = root_ + "/.uploads";
+          if (DIR* d = ::opendir(ud.c_str())) {
+            while (dirent* e = ::readdir(d)) {
+              const std::string id = e->d_name;
+              if (id == "." || id == "..") continue;
+              std::string meta;
+              const int mf = ::open((ud + "/" + id + "/.meta").c_str(), O_RDONLY | O_CLOEXEC);
+              if (mf < 0) continue;
+              char mb[4096];
+              const ssize_t r = ::read(mf, mb, sizeof mb);
+              ::close(mf);
+              if (r <= 0) continue;
+              meta.assign(mb, (size_t)r);
+              const size_t nl = meta.find('\n');
+              if (nl == std::string::npos || meta.substr(0, nl) != bucket) continue;
+              std::string k = meta.substr(nl + 1);
+              if (!k.empty() && k.back() == '\n') k.pop_back();
+              if (!starts_with(k, prefix)) continue;
+              const size_t dash = id.find('-');
+              const long long t0 = dash == std::string::npos ? 0 : std::atoll(id.c_str() + dash + 1);
+              items += "<Upload><Key>" + xml_escape(k) + "</Key><UploadId>" + xml_escape(id) + "</UploadId><Initiated>" +
+                       iso_date((time_t)t0) + "</Initiated></Upload>";
+            }
+            ::closedir(d);
+          }
+          ok = reply(200, "Content-Type: application/xml\r\n",
+                     "<?xml version=\"1.0\" encoding=\"UTF-8\"?><ListMultipartUploadsResult><Bucket>" + xml_escape(bucket) +
+                         "</Bucket><Prefix>" + xml_escape(prefix) + "</Prefix><IsTruncated>false</IsTruncated>" + items +
+                         "</ListMultipartUploadsResult>");
         } else if (method == "GET") {
           if (!is_dir(bdir)) {
             ok = error(404, "NoSuchBucket", bucket);
@@ -511,6 +587,16 @@ void BlobServer::serve_conn(int fd) {
         body_string();
         const std::string id = std::to_string(++upload_seq_) + "-" + std::to_string((long long)::time(nullptr));
         mkdirs(root_ + "/.uploads/" + id);
+        {   // bucket and key of the upload, for ListMultipartUploads (hidden from the part list)
+          const int mf = ::open((root_ + "/.uploads/" + id + "/.meta").c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC,
+                                0644);
+          if (mf >= 0) {
+            const std::string meta = bucket + "\n" + key + "\n";
+            ssize_t w = ::write(mf, meta.data(), meta.size());
+            (void)w;
+            ::close(mf);
+          }
+        }
         ok = reply(200, "Content-Type: application/xml\r\n",
                    "<?xml version=\"1.0\" encoding=\"UTF-8\"?><InitiateMultipartUploadResult><Bucket>" +
                        xml_escape(bucket) + "</Bucket><Key>" + xml_escape(key) + "</Key><UploadId>" + id +
@@ -547,22 +633,60 @@ void BlobServer::serve_conn(int fd) {
           const std::string tmpf = fpath + ".__upload";
           const int out = ::open(tmpf.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
           bool good = out >= 0;
-          for (const std::string& p : parts) {
-            const int in = ::open((udir + "/" + p).c_str(), O_RDONLY | O_CLOEXEC);
+          // the object is the parts in order: sized once, then every part copied into its slice
+          // by a few threads at once (in-kernel copy_file_range), so completing a multi-GB upload
+          // costs a parallel copy rather than one serial pass
+          std::vector<uint64_t> sizes(parts.size()), offs(parts.size());
+          uint64_t total = 0;
+          for (size_t i = 0; i < parts.size(); ++i) {
             struct stat st;
-            if (in < 0 || ::fstat(in, &st) != 0) {
-              good = false;
-            } else {
-              off_t o = 0;
-              while (good && o < st.st_size) {
-                const ssize_t r = ::sendfile(out, in, &o, (size_t)(st.st_size - o));
-                if (r <= 0) good = false;
-              }
-            }
-            if (in >= 0) ::close(in);
-            ::unlink((udir + "/" + p).c_str());
+            if (::stat((udir + "/" + parts[i]).c_str(), &st) != 0) good = false;
+            sizes[i] = good ? (uint64_t)st.st_size : 0;
+            offs[i] = total;
+            total += sizes[i];
           }
+          if (good && ::ftruncate(out, (off_t)total) != 0) good = false;
+          std::atomic<size_t> next{0};
+          std::atomic<bool> all_ok{good};
+          auto copier = [&] {
+            for (size_t i; all_ok && (i = next.fetch_add(1)) < parts.size();) {
+              const int in = ::open((udir + "/" + parts[i]).c_str(), O_RDONLY | O_CLOEXEC);
+              if (in < 0) {
+                all_ok = false;
+                break;
+              }
+              loff_t oi = 0, oo = (loff_t)offs[i];
+              uint64_t left = sizes[i];
+              while (left) {
+                ssize_t r = ::copy_file_range(in, &oi, out, &oo, (size_t)std::min<uint64_t>(left, 1ull << 30), 0);
+                if (r < 0 && errno == EINTR) continue;
+                if (r <= 0) {     // no in-kernel copy here: pread/pwrite
+                  char buf[1 << 16];
+                  const ssize_t k = ::pread(in, buf, sizeof buf, oi);
+                  if (k <= 0 || ::pwrite(out, buf, (size_t)k, oo) != k) {
+                    all_ok = false;
+                    break;
+                  }
+                  r = k;
+                  oi += k;
+                  oo += k;
+                }
+                left -= (uint64_t)r;
+              }
+              ::close(in);
+            }
+          };
+          if (good) {
+            std::vector<std::thread> ts;
+            const size_t nt = std::min<size_t>(8, parts.size());
+            for (size_t t = 1; t < nt; ++t) ts.emplace_back(copier);
+            copier();
+            for (auto& t : ts) t.join();
+            good = all_ok;
+          }
+          for (const std::string& p : parts) ::unlink((udir + "/" + p).c_str());
           if (out >= 0) ::close(out);
+          ::unlink((udir + "/.meta").c_str());
           ::rmdir(udir.c_str());
           struct stat st;
           if (good && ::rename(tmpf.c_str(), fpath.c_str()) == 0 && is_file(fpath, &st)) {
@@ -577,7 +701,8 @@ void BlobServer::serve_conn(int fd) {
         } else if (method == "DELETE") {
           if (DIR* d = ::opendir(udir.c_str())) {
             while (dirent* e = ::readdir(d))
-              if (e->d_name[0] != '.') ::unlink((udir + "/" + e->d_name).c_str());
+              if (std::strcmp(e->d_name, ".") != 0 && std::strcmp(e->d_name, "..") != 0)
+                ::unlink((udir + "/" + e->d_name).c_str());
             ::closedir(d);
           }
           ::rmdir(udir.c_str());
@@ -878,6 +1003,80 @@ int64_t HttpRangeReader::one(const std::string& target, const std::string& head,
     if (close_after) ::close(fd);
     else give(fd);
     return result;
+  }
+  return -1;
+}
+
+int HttpRangeReader::put_from(const std::string& target, const std::string& head, uint64_t src, uint64_t len,
+                              std::string* etag) {
+  return request("PUT", target, head, reinterpret_cast<const uint8_t*>(src), len, nullptr, etag);
+}
+
+int HttpRangeReader::request(const std::string& method, const std::string& target, const std::string& head,
+                             const uint8_t* body, uint64_t len, std::string* resp, std::string* etag) {
+  const std::string req = method + " " + target + " HTTP/1.1\r\n" + head + "Content-Length: " +
+                          std::to_string(len) + "\r\n\r\n";
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    bool reused = false;
+    const int fd = take(reused);
+    if (fd < 0) return -1;
+    ++requests_;
+    if (!send_all(fd, req.data(), req.size()) ||
+        (len && !send_all(fd, reinterpret_cast<const char*>(body), (size_t)len))) {
+      ::close(fd);
+      if (reused) continue;    // a pooled connection the server had closed: once more, fresh
+      return -1;
+    }
+    std::string hb;
+    char tmp[16384];
+    size_t hend;
+    bool fail = false;
+    while ((hend = hb.find("\r\n\r\n")) == std::string::npos) {
+      const ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0 || hb.size() > kMaxHead) {
+        fail = true;
+        break;
+      }
+      hb.append(tmp, (size_t)r);
+    }
+    if (fail) {
+      ::close(fd);
+      if (reused && hb.empty()) continue;
+      return -1;
+    }
+    const int code = hb.size() > 12 ? std::atoi(hb.c_str() + 9) : 0;
+    uint64_t clen = 0;
+    bool close_after = false;
+    for (size_t p = hb.find("\r\n"); p != std::string::npos && p < hend;) {
+      const size_t e = hb.find("\r\n", p + 2);
+      const std::string line = hb.substr(p + 2, e - p - 2);
+      const std::string l = lower(line);
+      if (starts_with(l, "content-length:")) clen = std::stoull(l.substr(15));
+      if (starts_with(l, "connection:") && l.find("close") != std::string::npos) close_after = true;
+      if (starts_with(l, "etag:") && etag) {
+        std::string v = line.substr(5);
+        while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.erase(0, 1);
+        *etag = v;
+      }
+      p = e;
+    }
+    uint64_t have = hb.size() - (hend + 4);
+    if (resp) resp->assign(hb, hend + 4, std::string::npos);
+    bool ok = true;
+    while (ok && have < clen) {   // the body (kept up to 1 MiB), drained so the connection is reusable
+      const ssize_t r = ::recv(fd, tmp, (size_t)std::min<uint64_t>(clen - have, sizeof tmp), 0);
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) {
+        ok = false;
+      } else {
+        if (resp && resp->size() < (1u << 20)) resp->append(tmp, (size_t)r);
+        have += (uint64_t)r;
+      }
+    }
+    if (!ok || close_after) ::close(fd);
+    else give(fd);
+    return code ? code : -1;
   }
   return -1;
 }

@@ -14,7 +14,8 @@
 // BlobServer is the S3 endpoint used to measure that path (config 5) and to run the S3 UFS
 // contract natively: <root>/<bucket>/<key> files, folder-marker objects ("dir/") as a hidden
 // marker file inside the directory, ListObjectsV2 with prefix/delimiter/continuation, ranged GET
-// via sendfile, PUT/copy, DELETE, multi-object delete and multipart upload.  No authentication.
+// via sendfile, PUT/copy, DELETE, multi-object delete and multipart upload (initiate, parts,
+// complete, abort, ListMultipartUploads).  No authentication.
 #pragma once
 #include <atomic>
 #include <cstdint>
@@ -62,6 +63,14 @@ class HttpRangeReader {
   // concurrently.  Returns `length`, or -HTTP status (-1 for a transport error).
   int64_t get_into(const std::string& target, const std::string& head_lines, uint64_t offset, uint64_t length,
                    uint64_t dst, int parallel, uint64_t min_part);
+  // PUT `target` (encoded path plus query) with the `length` bytes at `src` as the body over a
+  // pooled connection (the streaming multipart writer's part uploads).  Returns the HTTP status
+  // (-1 for a transport error); *etag gets the ETag response header.
+  int put_from(const std::string& target, const std::string& head_lines, uint64_t src, uint64_t length,
+               std::string* etag);
+  // Any request with a body from memory; the response body (up to 1 MiB) goes to *resp.
+  int request(const std::string& method, const std::string& target, const std::string& head_lines,
+              const uint8_t* body, uint64_t length, std::string* resp, std::string* etag);
   uint64_t requests() const { return requests_.load(); }
   uint64_t connects() const { return connects_.load(); }
 

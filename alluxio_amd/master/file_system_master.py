@@ -1309,6 +1309,20 @@ class FileSystemMaster(Journaled):
                 alluxio_path=alluxio_path)))
             self._apply(rpc, new.to_entry())
 
+    def cleanup_ufs(self) -> int:
+        """UfsCleaner (core/server/master/src/main/java/alluxio/master/file/UfsCleaner.java,
+        DefaultFileSystemMaster.java:740-752 cleanupUfs): every writable mount's UFS drops what
+        interrupted writes left behind (stale multipart uploads of object stores)."""
+        n = 0
+        for _p, info in sorted(self.mount_table.mounts().items()):
+            if info.read_only:
+                continue
+            try:
+                n += int(self.ufs_manager.get(info.mount_id).cleanup() or 0)
+            except Exception as e:  # noqa: BLE001 -- one failing UFS does not stop the others
+                LOG.warning("Failed to cleanup UFS %s: %s", info.ufs_uri, e)
+        return n
+
     def get_mount_table(self) -> dict:
         out = {}
         for p, info in self.mount_table.mounts().items():

@@ -160,7 +160,7 @@ class InodeTree:
                 self.to_be_persisted.add(inode.id)
             else:
                 self.to_be_persisted.discard(inode.id)
-            if inode.replication_min > 0 or inode.replication_max >= 0:
+            if inode.replication_max >= 0:      # InodeTreePersistentState: max != REPLICATION_MAX_INFINITY
                 self.replication_limited.add(inode.id)
             else:
                 self.replication_limited.discard(inode.id)

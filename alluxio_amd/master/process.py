@@ -397,6 +397,8 @@ class AlluxioMasterProcess:
             retention = c.get_ms("alluxio.job.master.finished.job.retention.time") / 1000.0
             specs.append(("Job Master Finished Job Purge",
                           lambda: self.job_master.purge_finished(retention), 10_000))
+        if c.get_bool("alluxio.underfs.cleanup.enabled"):
+            specs.append((hb.MASTER_UFS_CLEANUP, self.fs_master.cleanup_ufs, c.get_ms("alluxio.underfs.cleanup.interval")))
         if c.get_ms("alluxio.master.periodic.block.integrity.check.interval", "1hr") > 0:
             specs.append((hb.MASTER_BLOCK_INTEGRITY_CHECK, self.fs_master.block_integrity_check,
                           c.get_ms("alluxio.master.periodic.block.integrity.check.interval", "1hr")))

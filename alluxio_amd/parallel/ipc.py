@@ -28,6 +28,13 @@ def export_handle(tensor) -> tuple[bytes, int]:
     return bytes(handle), int(offset)
 
 
+OPEN_TIMEOUT_MS = [30_000]     # alluxio.user.short.circuit.open.timeout (set_open_timeout)
+
+
+def set_open_timeout(ms: int) -> None:
+    OPEN_TIMEOUT_MS[0] = max(1, int(ms))
+
+
 class IpcMappings:
     """Per-process cache of opened arena mappings keyed by (handle bytes, device)."""
 
@@ -43,7 +50,14 @@ class IpcMappings:
         with self._lock:
             base = self._maps.get(key)
             if base is None:
-                base = lib().ipc_open(key[0], device)
+                # bounded: an import that never returns (seen on some arena sizes, see
+                # worker/store.py) makes this handle unavailable instead of hanging the reader;
+                # callers fall back to the worker's gRPC data port
+                try:
+                    base = lib().ipc_open_bounded(key[0], device, OPEN_TIMEOUT_MS[0])
+                except TimeoutError as e:
+                    from ..utils.exceptions import UnavailableException
+                    raise UnavailableException(f"HIP IPC import of the worker arena timed out: {e}") from e
                 self._maps[key] = base
             return base
 

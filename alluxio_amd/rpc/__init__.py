@@ -14,6 +14,7 @@ client-streaming methods receive an iterator, server-streaming methods yield res
 from __future__ import annotations
 
 import logging
+import os
 import threading
 import time
 from concurrent import futures
@@ -255,6 +256,12 @@ def register_domain_socket(address: str, path: str) -> None:
         _DOMAIN_SOCKETS[address] = path
 
 
+def unregister_domain_socket(address: str, path: str | None = None) -> None:
+    with _LOCAL_LOCK:
+        if path is None or _DOMAIN_SOCKETS.get(address) == path:
+            _DOMAIN_SOCKETS.pop(address, None)
+
+
 def domain_socket_for(address: str) -> str | None:
     with _LOCAL_LOCK:
         return _DOMAIN_SOCKETS.get(address)
@@ -343,6 +350,11 @@ class Channel:
                 target = self.address
                 with _LOCAL_LOCK:
                     uds = _DOMAIN_SOCKETS.get(self.address)
+                    if uds and not os.path.exists(uds):
+                        # the worker that listened there is gone (its port may now be someone
+                        # else's, e.g. a new master): forget the route
+                        del _DOMAIN_SOCKETS[self.address]
+                        uds = None
                 if uds:
                     target = f"unix:{uds}"
                 self._grpc = grpc.insecure_channel(target, options=[

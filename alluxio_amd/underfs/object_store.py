@@ -16,6 +16,9 @@ from .base import (CreateOptions, DeleteOptions, ListOptions, MkdirsOptions, Ope
                    UfsDirectoryStatus, UfsFileStatus, UnderFileSystem)
 
 
+_POOL_LOCK = __import__("threading").Lock()
+
+
 class ObjectMeta:
     __slots__ = ("key", "size", "etag", "mtime_ms")
 
@@ -24,12 +27,14 @@ class ObjectMeta:
 
 
 class _ObjectWriter(io.RawIOBase):
-    """Buffers the object in memory (or a spill file) and uploads on close."""
+    """Single-PUT writer of a store without multipart uploads: the object is spooled to a temp
+    file under ``alluxio.tmp.dirs`` (memory holds at most one spool buffer) and PUT at close."""
 
     def __init__(self, ufs: "ObjectUnderFileSystem", key: str):
         super().__init__()
+        import tempfile
         self._ufs, self._key = ufs, key
-        self._buf = io.BytesIO()
+        self._buf = tempfile.SpooledTemporaryFile(max_size=8 << 20, dir=ufs._tmp_dir())
 
     def writable(self):
         return True
@@ -37,10 +42,216 @@ class _ObjectWriter(io.RawIOBase):
     def write(self, b):
         return self._buf.write(b)
 
+    def cancel(self):
+        if not self.closed:
+            self._buf.close()
+            super().close()
+
     def close(self):
         if not self.closed:
-            self._ufs._put(self._key, self._buf.getvalue())
+            try:
+                self._buf.seek(0)
+                self._ufs._put(self._key, self._buf.read())
+            finally:
+                self._buf.close()
         super().close()
+
+
+class _MultipartWriter(io.RawIOBase):
+    """Bounded-memory multipart upload of one object (reference
+    underfs/s3a/src/main/java/alluxio/underfs/s3a/S3ALowLevelOutputStream.java:309-360 / :435 and
+    S3AOutputStream.java:97).
+
+    * streaming (``alluxio.underfs.s3.streaming.upload.enabled``): each full part buffer of
+      ``alluxio.underfs.s3.streaming.upload.partition.size`` bytes is uploaded on the store's upload
+      executor while the caller keeps writing into the next buffer;
+    * spooled (the reference default): the bytes go to a temp file under ``alluxio.tmp.dirs``; at
+      close the file is uploaded in parallel parts read back with pread.
+
+    At most ``max_inflight`` part buffers exist, so memory stays bounded by (max_inflight + 1) x the
+    part size whatever the object size.  An object smaller than one part is a single PUT.  Any
+    failure -- a part upload, the completion, or a caller abandoning the stream (``cancel`` or
+    garbage collection without ``close``) -- aborts the multipart upload, so no parts linger.
+    """
+
+    def __init__(self, ufs: "ObjectUnderFileSystem", key: str, part_size: int, max_inflight: int, spool: bool):
+        import threading
+        super().__init__()
+        self._ufs, self._key = ufs, key
+        self._part = max(64 << 10, part_size)     # real S3 wants >= 5 MiB parts (but the last)
+        self._inflight = max(1, max_inflight)
+        self._sem = threading.BoundedSemaphore(self._inflight)
+        self._pool: list[bytearray] = []
+        self._pool_lock = threading.Lock()
+        self._buf: bytearray | None = None
+        self._fill = 0
+        self._upload_id = None
+        self._next = 1
+        self._etags: dict[int, str] = {}
+        self._futs = []
+        self._error: BaseException | None = None
+        self._spool = None
+        self._size = 0
+        if spool:
+            import tempfile
+            self._spool = tempfile.TemporaryFile(dir=ufs._tmp_dir())
+        self.parts_uploaded = 0
+        self.buffers_allocated = 0
+
+    def writable(self):
+        return True
+
+    # ---- buffers ----------------------------------------------------------------------------
+    def _take(self) -> bytearray:
+        with self._pool_lock:
+            if self._pool:
+                return self._pool.pop()
+            self.buffers_allocated += 1
+        return bytearray(self._part)
+
+    def _give(self, buf: bytearray) -> None:
+        with self._pool_lock:
+            self._pool.append(buf)
+
+    # ---- writing ----------------------------------------------------------------------------
+    def write(self, b):
+        if self._error is not None:
+            raise IOError(f"upload of {self._key} failed: {self._error}") from self._error
+        mv = memoryview(b).cast("B")
+        n = len(mv)
+        if self._spool is not None:
+            self._spool.write(mv)
+            self._size += n
+            return n
+        off = 0
+        while off < n:
+            if self._buf is None:
+                self._buf = self._take()
+            k = min(n - off, self._part - self._fill)
+            self._buf[self._fill:self._fill + k] = mv[off:off + k]
+            self._fill += k
+            off += k
+            if self._fill == self._part:
+                self._submit(self._buf, self._fill)
+                self._buf, self._fill = None, 0
+        self._size += n
+        return n
+
+    def _submit(self, buf: bytearray, n: int) -> None:
+        if self._upload_id is None:
+            self._upload_id = self._ufs._mp_init(self._key)
+        self._sem.acquire()                 # at most max_inflight buffers out: bounded memory
+        if self._error is not None:
+            self._sem.release()
+            self._give(buf)
+            raise IOError(f"upload of {self._key} failed: {self._error}") from self._error
+        num = self._next
+        self._next += 1
+        self._futs.append(self._ufs._mp_executor().submit(self._upload, num, buf, n))
+
+    def _upload(self, num: int, buf: bytearray, n: int) -> None:
+        try:
+            self._etags[num] = self._ufs._mp_put_part(self._key, self._upload_id, num, buf, n)
+            self.parts_uploaded += 1
+        except BaseException as e:  # noqa: BLE001
+            if self._error is None:
+                self._error = e
+            raise
+        finally:
+            self._give(buf)
+            self._sem.release()
+
+    def _drain(self) -> None:
+        futs, self._futs = self._futs, []
+        for f in futs:
+            try:
+                f.result()
+            except BaseException:  # noqa: BLE001 -- recorded in self._error
+                pass
+
+    # ---- end --------------------------------------------------------------------------------
+    def close(self):
+        if self.closed:
+            return
+        try:
+            if self._spool is not None:
+                self._close_spooled()
+            elif self._upload_id is None:
+                data = bytes(memoryview(self._buf)[:self._fill]) if self._buf is not None else b""
+                self._ufs._put_single(self._key, data)
+            else:
+                if self._fill:
+                    self._submit(self._buf, self._fill)
+                    self._buf, self._fill = None, 0
+                self._complete()
+        except BaseException:
+            self._abort()
+            raise
+        finally:
+            self._release()
+            super().close()
+
+    def _close_spooled(self) -> None:
+        import os
+        f = self._spool
+        f.flush()
+        if self._size <= self._part:
+            f.seek(0)
+            self._ufs._put_single(self._key, f.read())
+            return
+        fd = f.fileno()
+        for off in range(0, self._size, self._part):
+            n = min(self._part, self._size - off)
+            buf = self._take()
+            got = os.preadv(fd, [memoryview(buf)[:n]], off)
+            if got != n:
+                self._give(buf)
+                raise IOError(f"short read of the spool file of {self._key}")
+            self._submit(buf, n)
+        self._complete()
+
+    def _complete(self) -> None:
+        self._drain()
+        if self._error is not None:
+            raise IOError(f"upload of {self._key} failed: {self._error}") from self._error
+        self._ufs._mp_complete(self._key, self._upload_id, sorted(self._etags.items()))
+        self._upload_id = None
+
+    def _abort(self) -> None:
+        self._drain()
+        uid, self._upload_id = self._upload_id, None
+        if uid is not None:
+            try:
+                self._ufs._mp_abort(self._key, uid)
+            except Exception:  # noqa: BLE001 -- the UFS cleaner aborts stale uploads later
+                import logging
+                logging.getLogger(__name__).warning("abort of multipart upload %s of %s failed", uid, self._key)
+
+    def _release(self) -> None:
+        if self._spool is not None:
+            self._spool.close()
+            self._spool = None
+        self._buf = None
+        with self._pool_lock:
+            self._pool.clear()
+
+    def cancel(self):
+        """Abandon the object: abort the multipart upload, write nothing."""
+        if self.closed:
+            return
+        try:
+            self._abort()
+        finally:
+            self._release()
+            super().close()
+
+    def __del__(self):
+        # an abandoned stream must not complete a partial object (IOBase.__del__ would close)
+        if not self.closed:
+            try:
+                self.cancel()
+            except Exception:  # noqa: BLE001
+                pass
 
 
 class _RangeReader(io.RawIOBase):
@@ -135,9 +346,92 @@ class ObjectUnderFileSystem(UnderFileSystem):
     def supports_flush(self) -> bool:
         return False
 
+    # ---- multipart primitives (stores with multipart uploads override these) ----------------
+    multipart = False
+
+    def _put_single(self, key: str, data) -> None:
+        """One request for a whole (small) object."""
+        self._put(key, data)
+
+    def _mp_init(self, key: str) -> str:
+        raise NotImplementedError
+
+    def _mp_put_part(self, key: str, upload_id: str, num: int, buf, n: int) -> str:
+        raise NotImplementedError
+
+    def _mp_complete(self, key: str, upload_id: str, parts: list[tuple[int, str]]) -> None:
+        raise NotImplementedError
+
+    def _mp_abort(self, key: str, upload_id: str) -> None:
+        raise NotImplementedError
+
+    def _mp_list(self, prefix: str) -> list[tuple[str, str, int]]:
+        """(key, upload id, initiated ms) of the multipart uploads still open under ``prefix``."""
+        return []
+
+    def _opt(self, name: str, default: str) -> str:
+        p = self.properties or {}
+        if name in p:
+            return str(p[name])
+        if self.conf is not None and self.conf.get_raw(name) is not None:
+            return str(self.conf.get(name))
+        return default
+
+    def _tmp_dir(self) -> str:
+        import os
+        d = self._opt("alluxio.tmp.dirs", "/tmp").split(",")[0].strip() or "/tmp"
+        os.makedirs(d, exist_ok=True)
+        return d
+
+    def _mp_executor(self):
+        import threading
+        from concurrent.futures import ThreadPoolExecutor
+        ex = getattr(self, "_upload_pool", None)
+        if ex is None:
+            with _POOL_LOCK:
+                ex = getattr(self, "_upload_pool", None)
+                if ex is None:
+                    n = max(1, int(self._opt("alluxio.underfs.s3.upload.threads.max", "20")))
+                    ex = self._upload_pool = ThreadPoolExecutor(max_workers=n, thread_name_prefix="ufs-upload")
+        return ex
+
     # ---- UnderFileSystem --------------------------------------------------------------------
+    def upload_shape(self) -> tuple[int, int]:
+        """(part bytes, part buffers in flight) of a multipart upload: parts of
+        ``alluxio.underfs.s3.streaming.upload.partition.size`` (at most the multipart threshold),
+        as many in flight as ``alluxio.underfs.object.store.upload.buffer.size`` holds, at most
+        ``alluxio.underfs.s3.upload.threads.max``."""
+        from ..utils.format import parse_space_size
+        part = parse_space_size(self._opt("alluxio.underfs.s3.streaming.upload.partition.size", "64MB"))
+        part = min(part, getattr(self, "multipart_threshold", part))   # objects above it go multipart
+        budget = parse_space_size(self._opt("alluxio.underfs.object.store.upload.buffer.size", "256MB"))
+        threads = max(1, int(self._opt("alluxio.underfs.s3.upload.threads.max", "20")))
+        return part, max(1, min(threads, budget // max(1, part)))
+
     def create(self, path, options: CreateOptions | None = None):
-        return _ObjectWriter(self, self._key(path))
+        if not self.multipart:
+            return _ObjectWriter(self, self._key(path))
+        part, inflight = self.upload_shape()
+        spool = self._opt("alluxio.underfs.s3.streaming.upload.enabled", "false").lower() != "true"
+        return _MultipartWriter(self, self._key(path), part, inflight, spool)
+
+    def cleanup(self) -> int:
+        """Abort multipart uploads under this mount older than
+        ``alluxio.underfs.s3.intermediate.upload.clean.age`` (S3AUnderFileSystem.cleanup,
+        run by the master's UfsCleaner); returns how many were aborted."""
+        import time
+        from ..utils.format import parse_time_size
+        age_ms = parse_time_size(self._opt("alluxio.underfs.s3.intermediate.upload.clean.age", "3day"))
+        cutoff = int(time.time() * 1000) - age_ms
+        n = 0
+        for key, uid, initiated in self._mp_list(self._key(self.root_uri).rstrip("/")):
+            if initiated <= cutoff:
+                try:
+                    self._mp_abort(key, uid)
+                    n += 1
+                except Exception:  # noqa: BLE001
+                    pass
+        return n
 
     def open(self, path, options: OpenOptions | None = None):
         key = self._key(path)

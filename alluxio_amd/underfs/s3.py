@@ -126,21 +126,78 @@ class S3UnderFileSystem(ObjectUnderFileSystem):
         self._parallel = max(1, min(16, int(opt("alluxio.underfs.s3.threads.max", default="8") or 8)))
         self._part = _parse_size(opt("alluxio.underfs.s3.read.part.size", default="4MB"))
 
+    multipart = True
+
     def _put(self, key, data):
+        """One PUT (objects written through create() larger than a part go multipart)."""
         if len(data) <= self.multipart_threshold:
             self.client.request("PUT", self.bucket, key, data=data)
             return
+        w = self.create(key)
+        try:
+            w.write(data)
+        except BaseException:
+            w.cancel()
+            raise
+        w.close()
+
+    def _put_single(self, key, data):
+        self.client.request("PUT", self.bucket, key, data=data)
+
+    # ---- multipart upload (the streaming writer of object_store._MultipartWriter) ------------
+    def _mp_init(self, key):
         r = self.client.request("POST", self.bucket, key, query={"uploads": ""})
-        upload_id = _xml_text(ET.fromstring(r.content), "UploadId")
-        etags = []
-        for i, off in enumerate(range(0, len(data), self.part_size), start=1):
-            rr = self.client.request("PUT", self.bucket, key, query={"partNumber": i, "uploadId": upload_id},
-                                     data=data[off:off + self.part_size])
-            etags.append((i, rr.headers.get("ETag", "")))
+        return _xml_text(ET.fromstring(r.content), "UploadId")
+
+    def _mp_put_part(self, key, upload_id, num, buf, n):
+        """UploadPart of ``buf[:n]``: native PUT straight from the buffer over a pooled
+        connection (GIL released), else ``requests``."""
+        query = {"partNumber": num, "uploadId": upload_id}
+        rd = self._native_reader()
+        if rd is not None:
+            import numpy as np
+            path = f"/{self.bucket}/{key}"
+            h = self.client._headers("PUT", path, query, "UNSIGNED-PAYLOAD")
+            head = "".join(f"{k}: {v}\r\n" for k, v in h.items())
+            target = urllib.parse.quote(path, safe="/-_.~") + "?" + "&".join(
+                f"{urllib.parse.quote(k, safe='-_.~')}={urllib.parse.quote(str(v), safe='-_.~')}"
+                for k, v in sorted(query.items()))
+            addr = np.frombuffer(buf, dtype=np.uint8, count=n).ctypes.data if n else 0
+            code, etag = rd.put_from(target, head, addr, n)
+            if code == 404:
+                raise FileNotFoundError(f"s3://{self.bucket}/{key} upload {upload_id}")
+            if code not in (200, 204):
+                raise OSError(f"S3 UploadPart {num} of {path} failed: {code}")
+            return etag
+        rr = self.client.request("PUT", self.bucket, key, query=query, data=bytes(memoryview(buf)[:n]))
+        return rr.headers.get("ETag", "")
+
+    def _mp_complete(self, key, upload_id, parts):
         body = "<CompleteMultipartUpload>" + "".join(
-            f"<Part><PartNumber>{n}</PartNumber><ETag>{e}</ETag></Part>" for n, e in etags) + \
+            f"<Part><PartNumber>{n}</PartNumber><ETag>{e}</ETag></Part>" for n, e in parts) + \
             "</CompleteMultipartUpload>"
         self.client.request("POST", self.bucket, key, query={"uploadId": upload_id}, data=body.encode())
+
+    def _mp_abort(self, key, upload_id):
+        try:
+            self.client.request("DELETE", self.bucket, key, query={"uploadId": upload_id})
+        except FileNotFoundError:
+            pass          # already completed or aborted
+
+    def _mp_list(self, prefix):
+        r = self.client.request("GET", self.bucket, query={"uploads": "", "prefix": prefix})
+        out = []
+        for el in ET.fromstring(r.content):
+            if el.tag.split("}")[-1] != "Upload":
+                continue
+            t = _xml_text(el, "Initiated")
+            try:
+                ms = int(datetime.datetime.strptime(t[:19], "%Y-%m-%dT%H:%M:%S").replace(
+                    tzinfo=datetime.timezone.utc).timestamp() * 1000)
+            except ValueError:
+                ms = 0
+            out.append((_xml_text(el, "Key"), _xml_text(el, "UploadId"), ms))
+        return out
 
     def _get_range(self, key, offset, length):
         if length <= 0:

@@ -383,8 +383,9 @@ class BlockWorker:
             import urllib.parse
             u = urllib.parse.urlsplit(ufs.client.endpoint)
             if roots.resolve_s3(mount_id, f"s3://{ufs.bucket}/x") is None:
+                part, inflight = ufs.upload_shape()
                 roots.set_s3(mount_id, u.hostname, u.port or 80, ufs.bucket, ufs.client.access_key,
-                             ufs.client.secret_key, ufs.client.region, ufs._parallel, ufs._part)
+                             ufs.client.secret_key, ufs.client.region, ufs._parallel, ufs._part, part, inflight)
 
     note_local_ufs = note_ufs_mount
 

@@ -278,6 +278,9 @@ class AlluxioWorkerProcess:
         from ..client.context import unregister_local_worker
         if self.server.address:
             unregister_local_worker(self.server.address)
+            if self.domain_socket:
+                from ..rpc import unregister_domain_socket
+                unregister_domain_socket(self.server.address, self.domain_socket)
         if self.data_server is not None:
             self.data_server.stop()
             self.data_server = None

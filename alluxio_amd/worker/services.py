@@ -195,10 +195,17 @@ class BlockWorkerService:
         if not getattr(ctx, "internal", False):
             from ..utils.exceptions import PermissionDeniedException
             raise PermissionDeniedException("NativeWriteCommit is internal to the worker's data server")
-        self.w.commit_block(req.session_id, req.block_id, req.pin)
-        if req.ufs_read:      # a cold ReadBlock the native server read through from the UFS
+        if not req.ufs_read:
+            self.w.commit_block(req.session_id, req.block_id, req.pin)
+            return pb.block.WriteResponse(offset=req.length)
+        # a cold ReadBlock the native server read through from the UFS: posted by its reader once
+        # the whole block is in the store (the call itself may be gone); the session is ours now
+        try:
+            self.w.commit_block(req.session_id, req.block_id, req.pin)
             self.w.metrics.counter("BytesReadUfsAll").inc(req.length)
             self.w.metrics.counter("BytesReadUfsThrough").inc(req.length)
+        finally:
+            self.w.cleanup_session(req.session_id)    # aborts the temp block if the commit failed
         return pb.block.WriteResponse(offset=req.length)
 
     def WriteBlock(self, request_iter, ctx):
@@ -288,8 +295,12 @@ class BlockWorkerService:
                 out.close()
             else:
                 try:
-                    out.close()
-                    ufs.delete_file(o.ufs_path)
+                    cancel = getattr(out, "cancel", None)
+                    if cancel is not None:        # object stores: abort the upload, write nothing
+                        cancel()
+                    else:
+                        out.close()
+                        ufs.delete_file(o.ufs_path)
                 except Exception:  # noqa: BLE001
                     pass
         self.w.metrics.counter("BytesWrittenUfsAll").inc(pos)

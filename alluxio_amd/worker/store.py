@@ -9,8 +9,8 @@ Dir path grammar (comma separated, one quota per dir):
   ``dram``                     pinned host arena (medium DRAM; plain host memory without a GPU)
   ``auto``                     ``hbm`` when a HIP device is visible, else ``dram``
   ``/some/dir``                file-backed dir (SSD/HDD)
-The arenas are allocated through torch (one ``hipMalloc``/pinned allocation each) and handed to
-the native store as raw pointers; the tensors are kept alive here and give page views for RCCL
+HBM arenas are one native ``hipMalloc`` each, DRAM arenas a shared-memory file; both are handed to
+the native store as raw pointers and wrapped in zero-copy tensors that give page views for RCCL
 transfers and HIP IPC export.
 """
 from __future__ import annotations
@@ -48,15 +48,16 @@ class Arena:
         self._mmap = None
         self._registered = False
         if kind == "hbm":
-            # Measured on MI355X (ROCm 7, dmabuf IPC): a process importing the arena through
-            # hipIpcOpenMemHandle hangs when the allocation size modulo 4 GiB is 2 GiB or more
-            # (3 GiB and 7 GiB arenas hang, 256 MiB / 5 / 8 / 9 GiB open at once;
-            # profiles/r4_ipc_write_hang_stack.log).  Such sizes are rounded up to a multiple of
-            # 4 GiB; the tier still uses only `nbytes` of it.
-            alloc = nbytes
-            if alloc & (1 << 31):
-                alloc = (alloc + (4 << 30) - 1) // (4 << 30) * (4 << 30)
-            self.tensor = torch.empty(alloc, dtype=torch.uint8, device=torch.device("cuda", device))[:nbytes]
+            # One plain hipMalloc owned by this arena (csrc/ipc.cpp device_arena_alloc), not a
+            # segment of torch's caching allocator: the IPC export then covers exactly this
+            # allocation.  (Round 4 saw importers of 3 / 7 GiB caching-allocator arenas hang in
+            # hipIpcOpenMemHandle; tests/test_ipc_gpu.py imports 3 and 6 GiB native arenas, and
+            # the client's import is bounded: parallel/ipc.py falls back to the data port.)
+            # The native store takes ownership (DirSpec.owns_base): it frees the arena when it
+            # is destroyed, so no page it hands out outlives the memory.
+            self.alloc_bytes = max(nbytes, 1)
+            self._dptr = lib().device_arena_alloc(self.alloc_bytes, device)
+            self.tensor = _device_tensor(self._dptr, nbytes, device)
         elif kind == "dram":
             self.tensor = self._shared_host(nbytes)
         else:
@@ -130,6 +131,19 @@ class Arena:
             from ..parallel.ipc import export_handle
             self._ipc = export_handle(self.tensor)
         return self._ipc
+
+
+class _DeviceBuffer:
+    """__cuda_array_interface__ of a raw device allocation (a zero-copy torch view of it)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
+def _device_tensor(ptr: int, nbytes: int, device: int):
+    import torch
+    return torch.as_tensor(_DeviceBuffer(ptr, nbytes), device=torch.device("cuda", device))
 
 
 def _release_shared(fd: int, registered_ptr: int) -> None:
@@ -214,6 +228,7 @@ class TieredStore:
                 arena = Arena("hbm", quota, spec.device)
                 spec.kind = C.DirKind.DEVICE
                 spec.base = arena.base
+                spec.owns_base = True
             elif kind == "dram":
                 quota -= quota % page
                 arena = Arena("dram", quota)

@@ -119,9 +119,10 @@ def test_file_system_master_checkpoint_tree_and_restart(tmp_path):
     inodes = tree.component("HEAP_INODE_STORE").inodes()
     assert tree.component("INODE_COUNTER").long() == len(inodes) == len(before)
     g = fsm.tree.get("/a/g")
-    assert tree.component("PINNED_INODE_FILE_IDS").longs() == [g.id]
+    f = fsm.tree.get("/a/b/f")          # replicationMin > 0 pins a file (applyCreateInode)
+    assert tree.component("PINNED_INODE_FILE_IDS").longs() == sorted([f.id, g.id])
     assert tree.component("TTL_BUCKET_LIST").longs() == [g.id]
-    assert tree.component("REPLICATION_LIMITED_FILE_IDS").longs() == [fsm.tree.get("/a/b/f").id]
+    assert tree.component("REPLICATION_LIMITED_FILE_IDS").longs() == []     # no replicationMax set
     # owner/group/mode live in the access ACL (OWNING_USER_KEY "" entries + otherActions)
     gp = next(p for p in inodes if p.id == g.id)
     assert [(a.name, list(a.actions.actions)) for a in gp.access_acl.userActions] == [("", [0, 1])]

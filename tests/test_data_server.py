@@ -619,7 +619,7 @@ def test_native_cold_read_through(tmp_path):
     mount is registered: each block streams to the client as its UFS slots land, is cached in the
     store and committed (master sees it) before the call ends.  A partial read streams without
     caching; a cancelled read-through leaves no temp block (UnderFileSystemBlockReader.java:251-274)."""
-    with _cluster(tmp_path, {"alluxio.worker.ufs.ingest.chunk.size": "1MB",
+    with _cluster(tmp_path, {"alluxio.worker.ufs.ingest.chunk.size": "1MB", "alluxio.worker.ufs.ingest.depth": "2",
                              "alluxio.worker.network.reader.buffer.size": "1MB"}) as c:
         fs = c.client()
         rng = np.random.default_rng(21)
@@ -674,6 +674,26 @@ def test_native_cold_read_through(tmp_path):
                 assert time.time() < deadline
                 time.sleep(0.05)
             assert not w.worker.has_block(bid)
+            # a client that goes away right after the last byte still leaves the block cached
+            # (UnderFileSystemBlockReader.close commits a fully read block)
+            import queue
+            ch, call = _read_request_call(w.data_server.port)
+            q = queue.Queue()
+            q.put(pb.block.ReadRequest(block_id=bid, offset=0, length=blen, chunk_size=1 << 20,
+                                       open_ufs_block_options=opts))
+            it = call(iter(q.get, None))
+            got = b""
+            for _ in range(blen >> 20):                     # ack each chunk as it arrives
+                got += next(it).chunk.data
+                q.put(pb.block.ReadRequest(offset_received=len(got)))
+            it.cancel()
+            q.put(None)
+            ch.close()
+            assert got == files["/cold/d"][:blen].tobytes()
+            deadline = time.time() + 10
+            while not w.worker.has_block(bid):
+                assert time.time() < deadline
+                time.sleep(0.05)
             assert rfs.read_file("/cold/d") == files["/cold/d"].tobytes()
         finally:
             rfs.close()
@@ -773,3 +793,96 @@ def test_ack_beyond_sent_bytes_does_not_stall(tmp_path):
         ch.close()
         assert bytes(out) == data.tobytes()
         fs.close()
+
+
+def test_native_s3_through_writes(tmp_path):
+    """THROUGH writes of a remote client into an S3 mount: once the mount is registered, the data
+    server streams each file as a multipart upload itself (parts of the mount's partition size on
+    upload threads, at most buffer.size / part in flight, request window held back meanwhile),
+    completes it at the client's half-close and aborts it when the client goes away."""
+    import requests
+    srv = lib().BlobServer(str(tmp_path / "blobs"), "127.0.0.1", 0)
+    srv.start()
+    try:
+        base = f"http://127.0.0.1:{srv.port}"
+        assert requests.put(base + "/bkt").status_code == 200
+        assert requests.put(base + "/bkt/out/").status_code == 200
+        with _cluster(tmp_path) as c:
+            fs = c.client()
+            fs.mount("/s3", "s3://bkt/out", properties={
+                "alluxio.underfs.s3.endpoint": base,
+                "alluxio.underfs.s3.streaming.upload.partition.size": "1MB",
+                "alluxio.underfs.object.store.upload.buffer.size": "2MB"})
+            w = c.workers[0]
+            st = w.data_server.stats
+            rfs = _remote_fs(c)
+            try:
+                rng = np.random.default_rng(31)
+                first = rng.integers(0, 256, (3 << 20) + 5, dtype=np.uint8)
+                rfs.write_file("/s3/first", first, write_type="THROUGH")      # Python; registers the mount
+                assert requests.get(base + "/bkt/out/first").content == first.tobytes()
+                n0, b0 = st.ufs_write_streams, st.ufs_write_bytes
+                big = rng.integers(0, 256, (13 << 20) + 77, dtype=np.uint8)
+                rfs.write_file("/s3/big", big, write_type="THROUGH")
+                small = rng.integers(0, 256, 1000, dtype=np.uint8)
+                rfs.write_file("/s3/small", small, write_type="CACHE_THROUGH")
+                assert st.ufs_write_streams - n0 == 2
+                assert st.ufs_write_bytes - b0 == big.nbytes + small.nbytes
+                assert requests.get(base + "/bkt/out/big").content == big.tobytes()
+                assert requests.get(base + "/bkt/out/small").content == small.tobytes()
+                assert rfs.read_file("/s3/big") == big.tobytes()
+                assert requests.get(base + "/bkt", params={"uploads": ""}).text.count("<Upload>") == 0
+                # a writer that goes away mid-file: its upload is aborted, no object appears
+                f = rfs.create_file("/s3/gone", write_type="THROUGH")
+                f.write(rng.integers(0, 256, 5 << 20, dtype=np.uint8))
+                f.cancel()
+                deadline = time.time() + 10
+                while requests.get(base + "/bkt", params={"uploads": ""}).text.count("<Upload>"):
+                    assert time.time() < deadline
+                    time.sleep(0.05)
+                assert requests.head(base + "/bkt/out/gone").status_code == 404
+            finally:
+                rfs.close()
+                fs.close()
+    finally:
+        srv.stop()
+
+
+def test_bounded_ipc_open_times_out_and_client_falls_back(tmp_path, monkeypatch):
+    """A HIP IPC import that does not return makes the arena unavailable after the deadline
+    instead of hanging the reader (csrc/ipc.cpp ipc_open_bounded, stalled here by its test hook);
+    the handle is not retried, and the map layer turns the timeout into UnavailableException so
+    the block readers / writers fall back to the data port."""
+    import subprocess
+    import sys
+    code = (
+        "import os, sys, time\n"
+        f"sys.path.insert(0, {str(__import__('os').path.dirname(__import__('os').path.dirname(__file__)))!r})\n"
+        "from alluxio_amd.ops.native import lib\n"
+        "h = bytes(range(64))\n"
+        "lib()\n"
+        "t0 = time.time()\n"
+        "try:\n"
+        "    lib().ipc_open_bounded(h, 0, 300)\n"
+        "    print('opened')\n"
+        "except TimeoutError as e:\n"
+        "    print('timeout', round(time.time() - t0, 2))\n"
+        "try:\n"
+        "    lib().ipc_open_bounded(h, 0, 300)\n"
+        "except TimeoutError as e:\n"
+        "    print('again', 'before' in str(e))\n")
+    env = dict(__import__('os').environ, ALLUXIO_AMD_IPC_OPEN_DELAY_MS="3000")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, env=env)
+    lines = p.stdout.split()
+    assert lines[0] == "timeout" and float(lines[1]) < 2.0, p.stdout + p.stderr[-2000:]
+    assert lines[2:] == ["again", "True"]
+    # the map layer: a timed-out import is an UnavailableException (callers use the data port)
+    from alluxio_amd.parallel import ipc
+    from alluxio_amd.utils.exceptions import UnavailableException
+
+    class Stub:
+        def ipc_open_bounded(self, handle, device, timeout_ms):
+            raise TimeoutError("stuck")
+    monkeypatch.setattr(ipc, "lib", lambda: Stub())
+    with pytest.raises(UnavailableException):
+        ipc.IpcMappings().open(b"x" * 64, 0)

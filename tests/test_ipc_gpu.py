@@ -545,3 +545,57 @@ def test_ipc_open_verifies_crc(gpu, tmp_path):
         except Exception:  # noqa: BLE001
             pass
         p.wait(timeout=60)
+
+
+ARENA_CHILD = r"""
+import sys, json
+sys.path.insert(0, %(root)r)
+import torch
+from alluxio_amd.ops.native import lib
+handle, offset, nbytes, probes = bytes.fromhex(%(handle)r), %(offset)d, %(nbytes)d, %(probes)r
+base = lib().ipc_open_bounded(handle, 0, 60000) + offset
+out = {}
+for off in probes:                       # read 4 KiB at each probe, write its complement back
+    dst = torch.empty(4096, dtype=torch.uint8, device="cuda")
+    lib().batched_copy([(base + off, dst.data_ptr(), 4096)], 0)
+    torch.cuda.synchronize()
+    out[off] = int(dst.to(torch.int64).sum().item())
+    inv = (255 - dst).contiguous()
+    lib().batched_copy([(inv.data_ptr(), base + off, 4096)], 0)
+torch.cuda.synchronize()
+print(json.dumps({str(k): v for k, v in out.items()}), flush=True)
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gib", [3, 6])
+def test_native_hbm_arena_imports_from_other_process(gpu, tmp_path, gib):
+    """The worker's HBM arena is one native hipMalloc (worker/store.py Arena): another process
+    imports a 3 or 6 GiB arena through the bounded HIP IPC open (round 4 saw imports of such
+    caching-allocator arenas hang), reads pages at its start, middle and end and writes into
+    them; both sides see the same bytes."""
+    import torch
+
+    from alluxio_amd.parallel.ipc import export_handle
+    from alluxio_amd.worker.store import Arena
+    nbytes = gib << 30
+    a = Arena("hbm", nbytes, 0)
+    probes = [0, nbytes // 2 + 12288, nbytes - 4096]
+    for off in probes:
+        a.tensor[off:off + 4096].copy_(torch.arange(4096, device="cuda", dtype=torch.int64).remainder(251)
+                                       .to(torch.uint8) + (off % 3))
+    torch.cuda.synchronize()
+    handle, offset = export_handle(a.tensor)
+    script = tmp_path / "child.py"
+    script.write_text(ARENA_CHILD % {"root": ROOT, "handle": handle.hex(), "offset": offset, "nbytes": nbytes,
+                                     "probes": probes})
+    p = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, p.stderr[-3000:]
+    sums = json.loads(p.stdout.strip().splitlines()[-1])
+    for off in probes:
+        want = torch.arange(4096, dtype=torch.int64).remainder(251) + (off % 3)
+        assert sums[str(off)] == int(want.sum())
+        got = a.tensor[off:off + 4096].cpu().to(torch.int64)
+        assert torch.equal(got, 255 - want)
+    from alluxio_amd.ops.native import lib
+    lib().device_arena_free(a._dptr, 0)

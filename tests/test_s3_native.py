@@ -106,3 +106,96 @@ def test_endpoint_wire_shapes(blob):
     assert requests.head(base + "/bkt/x/sub/").status_code == 200
     requests.delete(base + "/bkt/x/sub/")
     assert requests.head(base + "/bkt/x/sub/").status_code == 404
+
+
+def _open_uploads(base):
+    r = requests.get(base + "/bkt", params={"uploads": ""})
+    assert r.status_code == 200
+    return r.text.count("<Upload>")
+
+
+@pytest.mark.parametrize("streaming", ["true", "false"])
+def test_bounded_multipart_writer(blob, streaming):
+    """create() of an object larger than a part streams parallel UploadParts (native PUT from the
+    part buffer) with at most (in-flight + 1) part buffers, whatever the object size (reference
+    S3ALowLevelOutputStream / S3AOutputStream with its spool file)."""
+    srv, base, root = blob
+    ufs = create_ufs("s3://bkt/", properties={"alluxio.underfs.s3.endpoint": base,
+                                              "alluxio.underfs.s3.streaming.upload.enabled": streaming,
+                                              "alluxio.underfs.s3.streaming.upload.partition.size": "1MB",
+                                              "alluxio.underfs.object.store.upload.buffer.size": "3MB",
+                                              "alluxio.underfs.s3.upload.threads.max": "8"})
+    ufs.multipart_threshold = 1 << 20
+    data = np.random.default_rng(4).integers(0, 256, (23 << 20) + 999, dtype=np.uint8)
+    w = ufs.create("s3://bkt/big/obj")
+    for i in range(0, len(data), 700_000):                 # writes that straddle parts
+        w.write(data[i:i + 700_000])
+    w.close()
+    assert w.parts_uploaded == 24 and w.buffers_allocated <= 4
+    assert (root / "bkt" / "big" / "obj").read_bytes() == data.tobytes()
+    assert _open_uploads(base) == 0
+    small = ufs.create("s3://bkt/big/small")               # below one part: a single PUT
+    small.write(b"tiny")
+    small.close()
+    assert small.parts_uploaded == 0 and (root / "bkt" / "big" / "small").read_bytes() == b"tiny"
+
+
+def test_failed_part_aborts_upload_and_cleanup(blob, monkeypatch):
+    srv, base, root = blob
+    ufs = create_ufs("s3://bkt/", properties={"alluxio.underfs.s3.endpoint": base,
+                                              "alluxio.underfs.s3.streaming.upload.enabled": "true",
+                                              "alluxio.underfs.s3.streaming.upload.partition.size": "1MB"})
+    ufs.multipart_threshold = 1 << 20
+    real = type(ufs)._mp_put_part
+
+    def flaky(self, key, upload_id, num, buf, n):
+        if num == 3:
+            raise OSError("injected part failure")
+        return real(self, key, upload_id, num, buf, n)
+    monkeypatch.setattr(type(ufs), "_mp_put_part", flaky)
+    w = ufs.create("s3://bkt/f/obj")
+    with pytest.raises(IOError):
+        for _ in range(8):
+            w.write(b"x" * (1 << 20))
+        w.close()
+    if not w.closed:
+        w.cancel()
+    assert _open_uploads(base) == 0                        # aborted, no parts left behind
+    assert not (root / "bkt" / "f" / "obj").exists()
+    monkeypatch.setattr(type(ufs), "_mp_put_part", real)
+    # an abandoned stream (never closed) aborts instead of completing a partial object
+    w2 = ufs.create("s3://bkt/f/abandoned")
+    w2.write(b"y" * (3 << 20))
+    assert _open_uploads(base) == 1
+    del w2
+    import gc
+    gc.collect()
+    assert _open_uploads(base) == 0 and not (root / "bkt" / "f" / "abandoned").exists()
+    # cleanup(): stale uploads under the mount are aborted, fresh ones kept
+    stale = ufs._mp_init("f/stale")
+    assert _open_uploads(base) == 1
+    assert ufs.cleanup() == 0                              # younger than the 3-day default
+    ufs.properties["alluxio.underfs.s3.intermediate.upload.clean.age"] = "0ms"
+    assert ufs.cleanup() == 1 and _open_uploads(base) == 0
+    assert stale
+
+
+def test_master_ufs_cleaner_aborts_stale_uploads(blob, tmp_path):
+    from alluxio_amd.conf import Configuration
+    from alluxio_amd.master.process import AlluxioMasterProcess
+    _, base, _ = blob
+    conf = Configuration({"alluxio.master.journal.folder": str(tmp_path / "journal"),
+                          "alluxio.security.authorization.permission.enabled": "false"})
+    m = AlluxioMasterProcess(conf, port=0, enable_grpc=False, root_ufs=str(tmp_path / "ufs"))
+    m.start(start_heartbeats=False)
+    try:
+        assert requests.put(base + "/bkt/m/").status_code == 200       # the mount's folder marker
+        m.fs_master.mount("/s3", "s3://bkt/m", properties={
+            "alluxio.underfs.s3.endpoint": base, "alluxio.underfs.s3.intermediate.upload.clean.age": "0ms"})
+        ufs = create_ufs("s3://bkt/m", properties={"alluxio.underfs.s3.endpoint": base})
+        ufs._mp_init("m/half-written")
+        assert _open_uploads(base) == 1
+        assert m.fs_master.cleanup_ufs() == 1
+        assert _open_uploads(base) == 0
+    finally:
+        m.stop()

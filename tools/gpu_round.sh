@@ -187,6 +187,16 @@ for s in $STEPS; do
       run remote_cold_host_p1 300 python tools/remote_device_read_bench.py --cold --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --out "$OUT/remote_cold_read.jsonl"
       run remote_cold_dev 300 python tools/remote_device_read_bench.py --cold --file-size 2g --read-size 2g --native-only --out "$OUT/remote_cold_read.jsonl"
       ;;
+    s3write)
+      run s3_write_8g 600 python tools/s3_write_bench.py --size 8g --paths ufs,through --out "$OUT/s3_write.jsonl"
+      run s3_write_8g_spool 400 python tools/s3_write_bench.py --size 8g --paths ufs --spool --out "$OUT/s3_write.jsonl"
+      ;;
+    arena)
+      run pytest_arena 400 python -u -m pytest tests/test_ipc_gpu.py -k "arena or read_from_other" -x -v --timeout 200 --timeout-method thread
+      ;;
+    remoteprof)
+      run rocprof_remote_host 400 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_remote_host" -o rh --output-format csv -- python3 tools/remote_device_read_bench.py --dest host --file-size 1g --read-size 1g --native-only --client-prop alluxio.user.device.read.parallelism=1
+      ;;
     bigwrite)
       for par in 1 4; do
         run big_write_p$par 170 python tools/worker_write_bench.py --threads 1 --files 2 --file-size 1g --write-size 1g --transports grpc,ipc --client-prop alluxio.user.device.read.parallelism=$par --worker-prop alluxio.worker.tieredstore.level0.dirs.quota=${BIGW_QUOTA:-8GB} --out "$OUT/worker_big_write.jsonl"
