@@ -346,16 +346,21 @@ void BlobServer::serve_conn(int fd) {
         }
         return out;
       };
-      auto body_to_fd = [&](int out) -> bool {
+      // the request body into `out` at file offset `at` (pwrite / splice with an explicit offset)
+      auto body_to_fd = [&](int out, uint64_t at = 0) -> bool {
         bool ok = true;
+        loff_t pos = (loff_t)at;
         // what already arrived with the headers
         if (!buf.empty() && body_left) {
           const size_t k = (size_t)std::min<uint64_t>(body_left, buf.size());
           size_t w = 0;
           while (ok && w < k) {
-            const ssize_t r = ::write(out, buf.data() + w, k - w);
+            const ssize_t r = ::pwrite(out, buf.data() + w, k - w, pos);
             if (r <= 0) ok = false;
-            else w += (size_t)r;
+            else {
+              w += (size_t)r;
+              pos += r;
+            }
           }
           buf.erase(0, k);
           body_left -= k;
@@ -374,7 +379,7 @@ void BlobServer::serve_conn(int fd) {
             }
             ssize_t moved = 0;
             while (moved < n) {
-              const ssize_t m = ::splice(pp[0], nullptr, out, nullptr, (size_t)(n - moved), SPLICE_F_MOVE);
+              const ssize_t m = ::splice(pp[0], nullptr, out, &pos, (size_t)(n - moved), SPLICE_F_MOVE);
               if (m < 0 && errno == EINTR) continue;
               if (m <= 0) {
                 ok = false;
@@ -395,9 +400,12 @@ void BlobServer::serve_conn(int fd) {
           if (r <= 0) return false;
           size_t w = 0;
           while (ok && w < (size_t)r) {
-            const ssize_t k = ::write(out, big.data() + w, (size_t)r - w);
+            const ssize_t k = ::pwrite(out, big.data() + w, (size_t)r - w, pos);
             if (k <= 0) ok = false;
-            else w += (size_t)k;
+            else {
+              w += (size_t)k;
+              pos += k;
+            }
           }
           body_left -= (uint64_t)r;
         }
@@ -610,10 +618,28 @@ void BlobServer::serve_conn(int fd) {
         } else if (method == "PUT" && q.count("partNumber")) {
           const int pn = std::atoi(q["partNumber"].c_str());
           char name[32];
-          std::snprintf(name, sizeof name, "/%08d", pn);
-          const int out = ::open((udir + name).c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-          const bool wrote = out >= 0 && body_to_fd(out);
-          if (out >= 0) ::close(out);
+          uint64_t stride;
+          {
+            std::lock_guard<std::mutex> g(up_mu_);
+            auto it = stride_.find(id);
+            if (it == stride_.end()) it = stride_.emplace(id, body_left).first;
+            stride = it->second;
+          }
+          bool wrote;
+          if (pn >= 1 && stride && body_left == stride) {      // in place: <udir>/data at (pn-1)*stride
+            std::snprintf(name, sizeof name, "/%08d.d", pn);
+            const int out = ::open((udir + "/data").c_str(), O_WRONLY | O_CREAT | O_CLOEXEC, 0644);
+            wrote = out >= 0 && body_to_fd(out, (uint64_t)(pn - 1) * stride);
+            if (out >= 0) ::close(out);
+            const int mk = ::open((udir + name).c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+            if (mk >= 0) ::close(mk);
+            else wrote = false;
+          } else {
+            std::snprintf(name, sizeof name, "/%08d", pn);
+            const int out = ::open((udir + name).c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+            wrote = out >= 0 && body_to_fd(out);
+            if (out >= 0) ::close(out);
+          }
           if (!wrote) {
             body_string();
             ok = error(500, "InternalError", "part write failed");
@@ -623,13 +649,90 @@ void BlobServer::serve_conn(int fd) {
         } else if (method == "POST") {
           body_string();
           std::vector<std::string> parts;
+          std::map<int, bool> in_data;      // part number -> stored in <udir>/data
           if (DIR* d = ::opendir(udir.c_str())) {
-            while (dirent* e = ::readdir(d))
-              if (e->d_name[0] != '.') parts.push_back(e->d_name);
+            while (dirent* e = ::readdir(d)) {
+              const std::string n = e->d_name;
+              if (n[0] == '.' || n == "data") continue;
+              const bool dd = n.size() > 2 && n.compare(n.size() - 2, 2, ".d") == 0;
+              in_data[std::atoi(n.c_str())] = dd;
+              if (!dd) parts.push_back(n);
+            }
             ::closedir(d);
+          }
+          uint64_t stride = 0;
+          {
+            std::lock_guard<std::mutex> g(up_mu_);
+            auto it = stride_.find(id);
+            if (it != stride_.end()) stride = it->second;
+            stride_.erase(id);
           }
           std::sort(parts.begin(), parts.end());
           mkdirs(fpath.substr(0, fpath.rfind('/')));
+          // fast path: parts 1..k in place in <udir>/data, at most the last one (k+1) separate
+          int k = 0;
+          while (in_data.count(k + 1) && in_data[k + 1]) ++k;
+          const int nparts = in_data.empty() ? 0 : in_data.rbegin()->first;
+          const bool fast = stride && k >= 1 && (int)in_data.size() == nparts &&
+                            (k == nparts || (k == nparts - 1 && parts.size() == 1));
+          if (fast) {
+            const std::string dataf = udir + "/data";
+            uint64_t total = (uint64_t)k * stride;
+            bool ok2 = true;
+            if (k < nparts) {            // append the short last part
+              const int in = ::open((udir + "/" + parts[0]).c_str(), O_RDONLY | O_CLOEXEC);
+              const int out = ::open(dataf.c_str(), O_WRONLY | O_CLOEXEC);
+              struct stat st;
+              if (in < 0 || out < 0 || ::fstat(in, &st) != 0) {
+                ok2 = false;
+              } else {
+                loff_t oi = 0, oo = (loff_t)total;
+                uint64_t left = (uint64_t)st.st_size;
+                while (ok2 && left) {
+                  const ssize_t r = ::copy_file_range(in, &oi, out, &oo, (size_t)left, 0);
+                  if (r <= 0) ok2 = false;
+                  else left -= (uint64_t)r;
+                }
+                total += (uint64_t)st.st_size;
+              }
+              if (in >= 0) ::close(in);
+              if (out >= 0) ::close(out);
+            }
+            struct stat st;
+            if (ok2 && ::truncate(dataf.c_str(), (off_t)total) == 0 && ::rename(dataf.c_str(), fpath.c_str()) == 0 &&
+                is_file(fpath, &st)) {
+              if (DIR* d = ::opendir(udir.c_str())) {
+                while (dirent* e = ::readdir(d))
+                  if (std::strcmp(e->d_name, ".") != 0 && std::strcmp(e->d_name, "..") != 0)
+                    ::unlink((udir + "/" + e->d_name).c_str());
+                ::closedir(d);
+              }
+              ::rmdir(udir.c_str());
+              ok = reply(200, "Content-Type: application/xml\r\n",
+                         "<?xml version=\"1.0\" encoding=\"UTF-8\"?><CompleteMultipartUploadResult><Bucket>" +
+                             xml_escape(bucket) + "</Bucket><Key>" + xml_escape(key) + "</Key><ETag>" +
+                             xml_escape(etag_of(st)) + "</ETag></CompleteMultipartUploadResult>");
+              if (!ok || !keep) goto done;
+              continue;
+            }
+          }
+          // general case: every part (in place or separate) copied into a fresh file
+          std::vector<std::pair<std::string, uint64_t>> srcs;   // (file, offset in it) per part, in order
+          std::vector<uint64_t> src_len;
+          for (const auto& kv : in_data) {
+            char nm[32];
+            if (kv.second) {
+              srcs.emplace_back(udir + "/data", (uint64_t)(kv.first - 1) * stride);
+              src_len.push_back(stride);
+            } else {
+              std::snprintf(nm, sizeof nm, "/%08d", kv.first);
+              struct stat pst;
+              srcs.emplace_back(udir + nm, 0);
+              src_len.push_back(::stat((udir + nm).c_str(), &pst) == 0 ? (uint64_t)pst.st_size : 0);
+            }
+          }
+          parts.clear();
+          for (size_t i = 0; i < srcs.size(); ++i) parts.push_back(srcs[i].first);
           const std::string tmpf = fpath + ".__upload";
           const int out = ::open(tmpf.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
           bool good = out >= 0;
@@ -639,9 +742,7 @@ void BlobServer::serve_conn(int fd) {
           std::vector<uint64_t> sizes(parts.size()), offs(parts.size());
           uint64_t total = 0;
           for (size_t i = 0; i < parts.size(); ++i) {
-            struct stat st;
-            if (::stat((udir + "/" + parts[i]).c_str(), &st) != 0) good = false;
-            sizes[i] = good ? (uint64_t)st.st_size : 0;
+            sizes[i] = src_len[i];
             offs[i] = total;
             total += sizes[i];
           }
@@ -650,12 +751,12 @@ void BlobServer::serve_conn(int fd) {
           std::atomic<bool> all_ok{good};
           auto copier = [&] {
             for (size_t i; all_ok && (i = next.fetch_add(1)) < parts.size();) {
-              const int in = ::open((udir + "/" + parts[i]).c_str(), O_RDONLY | O_CLOEXEC);
+              const int in = ::open(srcs[i].first.c_str(), O_RDONLY | O_CLOEXEC);
               if (in < 0) {
                 all_ok = false;
                 break;
               }
-              loff_t oi = 0, oo = (loff_t)offs[i];
+              loff_t oi = (loff_t)srcs[i].second, oo = (loff_t)offs[i];
               uint64_t left = sizes[i];
               while (left) {
                 ssize_t r = ::copy_file_range(in, &oi, out, &oo, (size_t)std::min<uint64_t>(left, 1ull << 30), 0);
@@ -684,9 +785,13 @@ void BlobServer::serve_conn(int fd) {
             for (auto& t : ts) t.join();
             good = all_ok;
           }
-          for (const std::string& p : parts) ::unlink((udir + "/" + p).c_str());
           if (out >= 0) ::close(out);
-          ::unlink((udir + "/.meta").c_str());
+          if (DIR* d = ::opendir(udir.c_str())) {
+            while (dirent* e = ::readdir(d))
+              if (std::strcmp(e->d_name, ".") != 0 && std::strcmp(e->d_name, "..") != 0)
+                ::unlink((udir + "/" + e->d_name).c_str());
+            ::closedir(d);
+          }
           ::rmdir(udir.c_str());
           struct stat st;
           if (good && ::rename(tmpf.c_str(), fpath.c_str()) == 0 && is_file(fpath, &st)) {
@@ -699,6 +804,10 @@ void BlobServer::serve_conn(int fd) {
             ok = error(500, "InternalError", "complete failed");
           }
         } else if (method == "DELETE") {
+          {
+            std::lock_guard<std::mutex> g(up_mu_);
+            stride_.erase(id);
+          }
           if (DIR* d = ::opendir(udir.c_str())) {
             while (dirent* e = ::readdir(d))
               if (std::strcmp(e->d_name, ".") != 0 && std::strcmp(e->d_name, "..") != 0)

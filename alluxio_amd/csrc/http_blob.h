@@ -19,6 +19,7 @@
 #pragma once
 #include <atomic>
 #include <cstdint>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -50,6 +51,11 @@ class BlobServer {
   std::vector<std::thread> conns_;
   std::vector<int> fds_;
   std::atomic<uint64_t> requests_{0}, bytes_{0}, upload_seq_{0};
+  // multipart uploads: parts of the upload's stride (the size of the first part to arrive) are
+  // written straight into <upload>/data at (partNumber - 1) * stride, so completing the usual
+  // fixed-part-size upload appends at most its (shorter) last part instead of copying the object
+  std::mutex up_mu_;
+  std::map<std::string, uint64_t> stride_;
 };
 
 class HttpRangeReader {

@@ -81,9 +81,9 @@ class _MultipartWriter(io.RawIOBase):
         self._part = max(64 << 10, part_size)     # real S3 wants >= 5 MiB parts (but the last)
         self._inflight = max(1, max_inflight)
         self._sem = threading.BoundedSemaphore(self._inflight)
-        self._pool: list[bytearray] = []
+        self._pool: list = []
         self._pool_lock = threading.Lock()
-        self._buf: bytearray | None = None
+        self._buf = None
         self._fill = 0
         self._upload_id = None
         self._next = 1
@@ -97,19 +97,21 @@ class _MultipartWriter(io.RawIOBase):
             self._spool = tempfile.TemporaryFile(dir=ufs._tmp_dir())
         self.parts_uploaded = 0
         self.buffers_allocated = 0
+        self.timings: dict = {}
 
     def writable(self):
         return True
 
     # ---- buffers ----------------------------------------------------------------------------
-    def _take(self) -> bytearray:
+    def _take(self):
+        import numpy as np
         with self._pool_lock:
             if self._pool:
                 return self._pool.pop()
             self.buffers_allocated += 1
-        return bytearray(self._part)
+        return np.empty(self._part, dtype=np.uint8)   # numpy slices copy at memcpy speed (bytearray ~1 GB/s)
 
-    def _give(self, buf: bytearray) -> None:
+    def _give(self, buf) -> None:
         with self._pool_lock:
             self._pool.append(buf)
 
@@ -117,18 +119,20 @@ class _MultipartWriter(io.RawIOBase):
     def write(self, b):
         if self._error is not None:
             raise IOError(f"upload of {self._key} failed: {self._error}") from self._error
+        import numpy as np
         mv = memoryview(b).cast("B")
         n = len(mv)
         if self._spool is not None:
             self._spool.write(mv)
             self._size += n
             return n
+        src = np.frombuffer(mv, dtype=np.uint8)
         off = 0
         while off < n:
             if self._buf is None:
                 self._buf = self._take()
             k = min(n - off, self._part - self._fill)
-            self._buf[self._fill:self._fill + k] = mv[off:off + k]
+            self._buf[self._fill:self._fill + k] = src[off:off + k]
             self._fill += k
             off += k
             if self._fill == self._part:
@@ -137,7 +141,7 @@ class _MultipartWriter(io.RawIOBase):
         self._size += n
         return n
 
-    def _submit(self, buf: bytearray, n: int) -> None:
+    def _submit(self, buf, n: int) -> None:
         if self._upload_id is None:
             self._upload_id = self._ufs._mp_init(self._key)
         self._sem.acquire()                 # at most max_inflight buffers out: bounded memory
@@ -149,7 +153,7 @@ class _MultipartWriter(io.RawIOBase):
         self._next += 1
         self._futs.append(self._ufs._mp_executor().submit(self._upload, num, buf, n))
 
-    def _upload(self, num: int, buf: bytearray, n: int) -> None:
+    def _upload(self, num: int, buf, n: int) -> None:
         try:
             self._etags[num] = self._ufs._mp_put_part(self._key, self._upload_id, num, buf, n)
             self.parts_uploaded += 1
@@ -177,7 +181,7 @@ class _MultipartWriter(io.RawIOBase):
             if self._spool is not None:
                 self._close_spooled()
             elif self._upload_id is None:
-                data = bytes(memoryview(self._buf)[:self._fill]) if self._buf is not None else b""
+                data = self._buf[:self._fill].tobytes() if self._buf is not None else b""
                 self._ufs._put_single(self._key, data)
             else:
                 if self._fill:
@@ -211,10 +215,14 @@ class _MultipartWriter(io.RawIOBase):
         self._complete()
 
     def _complete(self) -> None:
+        import time
+        t0 = time.perf_counter()
         self._drain()
+        t1 = time.perf_counter()
         if self._error is not None:
             raise IOError(f"upload of {self._key} failed: {self._error}") from self._error
         self._ufs._mp_complete(self._key, self._upload_id, sorted(self._etags.items()))
+        self.timings = {"drain_s": round(t1 - t0, 3), "complete_s": round(time.perf_counter() - t1, 3)}
         self._upload_id = None
 
     def _abort(self) -> None:

@@ -162,7 +162,8 @@ class S3UnderFileSystem(ObjectUnderFileSystem):
             target = urllib.parse.quote(path, safe="/-_.~") + "?" + "&".join(
                 f"{urllib.parse.quote(k, safe='-_.~')}={urllib.parse.quote(str(v), safe='-_.~')}"
                 for k, v in sorted(query.items()))
-            addr = np.frombuffer(buf, dtype=np.uint8, count=n).ctypes.data if n else 0
+            addr = (buf.ctypes.data if isinstance(buf, np.ndarray) else
+                    np.frombuffer(buf, dtype=np.uint8, count=n).ctypes.data) if n else 0
             code, etag = rd.put_from(target, head, addr, n)
             if code == 404:
                 raise FileNotFoundError(f"s3://{self.bucket}/{key} upload {upload_id}")

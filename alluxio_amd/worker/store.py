@@ -39,7 +39,7 @@ class Arena:
     channel.
     """
 
-    def __init__(self, kind: str, nbytes: int, device: int = 0):
+    def __init__(self, kind: str, nbytes: int, device: int = 0, alloc_bytes: int | None = None):
         import torch
         self.kind = kind
         self.nbytes = nbytes
@@ -48,14 +48,11 @@ class Arena:
         self._mmap = None
         self._registered = False
         if kind == "hbm":
-            # One plain hipMalloc owned by this arena (csrc/ipc.cpp device_arena_alloc), not a
-            # segment of torch's caching allocator: the IPC export then covers exactly this
-            # allocation.  (Round 4 saw importers of 3 / 7 GiB caching-allocator arenas hang in
-            # hipIpcOpenMemHandle; tests/test_ipc_gpu.py imports 3 and 6 GiB native arenas, and
-            # the client's import is bounded: parallel/ipc.py falls back to the data port.)
-            # The native store takes ownership (DirSpec.owns_base): it frees the arena when it
-            # is destroyed, so no page it hands out outlives the memory.
-            self.alloc_bytes = max(nbytes, 1)
+            # One plain hipMalloc (csrc/ipc.cpp device_arena_alloc) of `alloc_bytes` (see
+            # ipc_safe_size) whose first `nbytes` are the tier; the native store takes ownership
+            # (DirSpec.owns_base) and frees it when it is destroyed, so no page it hands out
+            # outlives the memory.
+            self.alloc_bytes = max(alloc_bytes or nbytes, nbytes, 1)
             self._dptr = lib().device_arena_alloc(self.alloc_bytes, device)
             self.tensor = _device_tensor(self._dptr, nbytes, device)
         elif kind == "dram":
@@ -131,6 +128,24 @@ class Arena:
             from ..parallel.ipc import export_handle
             self._ipc = export_handle(self.tensor)
         return self._ipc
+
+
+IPC_SIZE_BIT = 1 << 31
+
+
+def ipc_safe_size(nbytes: int) -> int:
+    """Allocation size for an HBM arena that other processes import through HIP IPC.
+
+    Measured on MI355X (ROCm 7.2, dmabuf IPC): ``hipIpcOpenMemHandle`` in an importing process
+    never returns when bit 31 of the allocation size is set (size mod 4 GiB >= 2 GiB) -- 3 / 6 /
+    7 GiB allocations hang, 256 MiB / 5 / 8 / 9 GiB open at once -- for native hipMalloc arenas as
+    for caching-allocator segments (profiles/r5_ipc_arena_sizes.md,
+    tests/test_ipc_gpu.py::test_unpadded_arena_import_times_out).  The pattern fits a 32-bit
+    signed size somewhere in the import path.  Such sizes are padded up to the next multiple of
+    4 GiB; the padding is never handed out."""
+    if nbytes & IPC_SIZE_BIT:
+        return (nbytes + (4 << 30) - 1) // (4 << 30) * (4 << 30)
+    return nbytes
 
 
 class _DeviceBuffer:
@@ -224,8 +239,17 @@ class TieredStore:
                     import torch
                     free, _ = torch.cuda.mem_get_info(spec.device)
                     quota = int(free * frac)
+                    if quota & IPC_SIZE_BIT:
+                        # a share of free memory has no room for IPC padding: round the tier
+                        # down to the largest importable size instead (< 2 GiB less)
+                        quota = (quota & ~((4 << 30) - 1)) + IPC_SIZE_BIT - page
                 quota -= quota % page
-                arena = Arena("hbm", quota, spec.device)
+                alloc = ipc_safe_size(quota)
+                if alloc != quota:
+                    LOG.warning("HBM tier %s: %d bytes allocated for a %d-byte arena (%d padding bytes, "
+                                "never used: HIP IPC cannot import sizes with bit 31 set)",
+                                d.alias, alloc, quota, alloc - quota)
+                arena = Arena("hbm", quota, spec.device, alloc)
                 spec.kind = C.DirKind.DEVICE
                 spec.base = arena.base
                 spec.owns_base = True

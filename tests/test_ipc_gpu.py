@@ -553,7 +553,7 @@ sys.path.insert(0, %(root)r)
 import torch
 from alluxio_amd.ops.native import lib
 handle, offset, nbytes, probes = bytes.fromhex(%(handle)r), %(offset)d, %(nbytes)d, %(probes)r
-base = lib().ipc_open_bounded(handle, 0, 60000) + offset
+base = lib().ipc_open_bounded(handle, 0, %(timeout_ms)d) + offset
 out = {}
 for off in probes:                       # read 4 KiB at each probe, write its complement back
     dst = torch.empty(4096, dtype=torch.uint8, device="cuda")
@@ -567,29 +567,53 @@ print(json.dumps({str(k): v for k, v in out.items()}), flush=True)
 """
 
 
+def _import_probe(tmp_path, handle, offset, nbytes, probes, timeout_ms=60000):
+    script = tmp_path / "child.py"
+    script.write_text(ARENA_CHILD % {"root": ROOT, "handle": handle.hex(), "offset": offset, "nbytes": nbytes,
+                                     "probes": probes, "timeout_ms": timeout_ms})
+    return subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=150)
+
+
+@pytest.mark.gpu
+def test_unpadded_arena_import_times_out(gpu, tmp_path):
+    """Pins why worker/store.py pads HBM arenas (ipc_safe_size): a plain 3 GiB hipMalloc (bit 31 of
+    the size set) cannot be imported by another process -- hipIpcOpenMemHandle does not return --
+    and the bounded open turns that into IpcTimeout instead of a hung reader."""
+    from alluxio_amd.ops.native import lib
+    from alluxio_amd.parallel.ipc import export_handle
+    from alluxio_amd.worker.store import _device_tensor, ipc_safe_size
+    nbytes = 3 << 30
+    assert ipc_safe_size(nbytes) == 4 << 30 and ipc_safe_size(5 << 30) == 5 << 30
+    ptr = lib().device_arena_alloc(nbytes, 0)
+    try:
+        t = _device_tensor(ptr, nbytes, 0)
+        handle, offset = export_handle(t)
+        p = _import_probe(tmp_path, handle, offset, nbytes, [0], timeout_ms=15000)
+        assert p.returncode != 0 and "IpcTimeout" in p.stderr, (p.stdout, p.stderr[-2000:])
+    finally:
+        lib().device_arena_free(ptr, 0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("gib", [3, 6])
 def test_native_hbm_arena_imports_from_other_process(gpu, tmp_path, gib):
-    """The worker's HBM arena is one native hipMalloc (worker/store.py Arena): another process
-    imports a 3 or 6 GiB arena through the bounded HIP IPC open (round 4 saw imports of such
-    caching-allocator arenas hang), reads pages at its start, middle and end and writes into
-    them; both sides see the same bytes."""
+    """The worker's HBM arena is one native hipMalloc (worker/store.py Arena), padded to an
+    importable size: another process imports a 3 or 6 GiB tier's arena through the bounded HIP IPC
+    open, reads pages at its start, middle and end and writes into them; both sides see the same
+    bytes."""
     import torch
 
     from alluxio_amd.parallel.ipc import export_handle
-    from alluxio_amd.worker.store import Arena
+    from alluxio_amd.worker.store import Arena, ipc_safe_size
     nbytes = gib << 30
-    a = Arena("hbm", nbytes, 0)
+    a = Arena("hbm", nbytes, 0, ipc_safe_size(nbytes))
     probes = [0, nbytes // 2 + 12288, nbytes - 4096]
     for off in probes:
         a.tensor[off:off + 4096].copy_(torch.arange(4096, device="cuda", dtype=torch.int64).remainder(251)
                                        .to(torch.uint8) + (off % 3))
     torch.cuda.synchronize()
     handle, offset = export_handle(a.tensor)
-    script = tmp_path / "child.py"
-    script.write_text(ARENA_CHILD % {"root": ROOT, "handle": handle.hex(), "offset": offset, "nbytes": nbytes,
-                                     "probes": probes})
-    p = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=150)
+    p = _import_probe(tmp_path, handle, offset, nbytes, probes)
     assert p.returncode == 0, p.stderr[-3000:]
     sums = json.loads(p.stdout.strip().splitlines()[-1])
     for off in probes:

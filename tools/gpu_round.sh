@@ -190,9 +190,11 @@ for s in $STEPS; do
     s3write)
       run s3_write_8g 600 python tools/s3_write_bench.py --size 8g --paths ufs,through --out "$OUT/s3_write.jsonl"
       run s3_write_8g_spool 400 python tools/s3_write_bench.py --size 8g --paths ufs --spool --out "$OUT/s3_write.jsonl"
+      run s3_write_8g_p32 400 python tools/s3_write_bench.py --size 8g --paths ufs,through --part 32MB --out "$OUT/s3_write.jsonl"
+      run s3_write_8g_p16 400 python tools/s3_write_bench.py --size 8g --paths ufs,through --part 16MB --out "$OUT/s3_write.jsonl"
       ;;
     arena)
-      run pytest_arena 400 python -u -m pytest tests/test_ipc_gpu.py -k "arena or read_from_other" -x -v --timeout 200 --timeout-method thread
+      run pytest_arena 400 python -u -m pytest tests/test_ipc_gpu.py -k "arena or read_from_other" -v --timeout 200 --timeout-method thread
       ;;
     remoteprof)
       run rocprof_remote_host 400 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_remote_host" -o rh --output-format csv -- python3 tools/remote_device_read_bench.py --dest host --file-size 1g --read-size 1g --native-only --client-prop alluxio.user.device.read.parallelism=1

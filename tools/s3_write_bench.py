@@ -127,7 +127,7 @@ def main(argv=None) -> int:
                 el = time.perf_counter() - t0
                 growth = samp.stop()
                 extra = {"parts": w.parts_uploaded, "part_buffers": w.buffers_allocated,
-                         "writer": "spooled" if a.spool else "streaming"}
+                         "writer": "spooled" if a.spool else "streaming", **w.timings}
                 del chunk
             else:
                 from alluxio_amd.minicluster import LocalAlluxioCluster
