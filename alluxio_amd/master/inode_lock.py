@@ -30,6 +30,7 @@ from __future__ import annotations
 import threading
 import time
 
+from ..utils import optiming
 from ..utils.exceptions import DeadlineExceededException
 from ..utils.uri import normalize_path
 
@@ -150,7 +151,8 @@ class PathLockManager:
                 if getattr(_LANE, "nb", False):
                     raise WouldBlock(f"namespace locks on {[p for p, _ in requests]} are held")
                 self.waits += 1
-                deadline = time.monotonic() + limit
+                t_wait = time.monotonic()
+                deadline = t_wait + limit
                 while self._conflicts(holds, me):
                     rem = deadline - time.monotonic()
                     if rem <= 0:
@@ -158,6 +160,8 @@ class PathLockManager:
                             f"timed out after {limit:.0f}s waiting for namespace locks on "
                             f"{[p for p, _ in requests]}")
                     self._cond.wait(min(rem, 1.0))
+                if optiming.ENABLED:
+                    optiming.add("path_lock_wait", time.monotonic() - t_wait)
             held = self._held
             for node, mode in holds:
                 h = held.get(node)

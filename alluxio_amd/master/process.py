@@ -474,6 +474,10 @@ def main(argv=None) -> int:  # pragma: no cover - CLI entry
     from ..conf import Configuration as _C
     from ..web.logserver import attach
     attach("MASTER", _C(load_site=True))
+    from ..utils import optiming
+    if optiming.ENABLED:                 # the bench stops the master with SIGTERM: dump first
+        import signal
+        signal.signal(signal.SIGTERM, lambda *_: (optiming.dump(), os._exit(0)))
     m = AlluxioMasterProcess(host=a.host, port=a.port, root_ufs=a.root_ufs)
     if a.format:
         m.format()

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import atexit
 import logging
+import os
 import threading
 import time
 import weakref
@@ -291,6 +292,8 @@ class NativeRpcFrontend:
         lanes keep serving other paths (reference: a slow UFS stalls only its own RPC thread)."""
         from ..master.inode_lock import WouldBlock, nonblocking_lane
         from ..security import as_user
+        from ..utils import optiming
+        t_start = time.perf_counter() if optiming.ENABLED else 0.0
         pending = None
         after = None
         cache_ep = None
@@ -341,8 +344,10 @@ class NativeRpcFrontend:
                 # "does not exist" of a ONCE lookup: as stable as the UFS absent-path cache
                 # behind it (a create, load, sync change or remount bumps the epoch)
                 self.server.cache_put(midx, key_user, payload, b"", cache_ep, reply[1], reply[2])
+        if optiming.ENABLED and midx:
+            optiming.add("handler:" + self.methods[midx][0].rsplit("/", 1)[-1], time.perf_counter() - t_start)
         if pending:
-            self._defer(pending, reply, after)
+            self._defer(pending, reply, after, self.methods[midx][0].rsplit("/", 1)[-1] if optiming.ENABLED else "")
             return None
         return reply
 
@@ -356,13 +361,14 @@ class NativeRpcFrontend:
                 LOG.exception("post-journal callback failed")
         self.server.respond_many([reply])
 
-    def _defer(self, pending: dict, reply, after: list | None = None) -> None:
+    def _defer(self, pending: dict, reply, after: list | None = None, name: str = "") -> None:
         """Send ``reply`` once every journal writer in ``pending`` flushed past its counter
         (after running the RPC's after_durable callbacks; on a failed flush they never run)."""
         left = [len(pending)]
         err = [None]
         lock = threading.Lock()
         srv = self.server
+        t_defer = time.perf_counter() if name else 0.0
 
         def done(e):
             with lock:
@@ -372,6 +378,9 @@ class NativeRpcFrontend:
                 last = left[0] == 0
             if not last:
                 return
+            if name:
+                from ..utils import optiming
+                optiming.add("journal_wait:" + name, time.perf_counter() - t_defer)
             if err[0] is None:
                 if after:
                     self._after_pool().submit(self._run_after, list(after), reply)
@@ -467,6 +476,20 @@ class NativeRpcFrontend:
             C.stream_finish(srv, token, 1, "call ended")   # no-op once finished
 
     def _loop(self, lane: int, batch: int) -> None:
+        prof_path = os.environ.get("ALLUXIO_LANE_PROFILE")
+        if prof_path:                  # per-lane-thread cProfile (diagnostics: where handler time goes)
+            import cProfile
+            pr = cProfile.Profile()
+            pr.enable()
+            try:
+                self._loop_inner(lane, batch)
+            finally:
+                pr.disable()
+                pr.dump_stats(f"{prof_path}.lane{lane}.{threading.get_ident()}")
+            return
+        self._loop_inner(lane, batch)
+
+    def _loop_inner(self, lane: int, batch: int) -> None:
         srv = self.server
         metrics = self.rpc.metrics
         while self._running:

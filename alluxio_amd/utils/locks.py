@@ -76,6 +76,8 @@ class RWLock:
             self._waiting_writers += 1
             self._gate = True
             ok = True
+            contended = self._writer is not None or bool(self._readers)
+            t_wait = time.perf_counter() if contended else 0.0
             try:
                 while self._writer is not None or self._readers:
                     if not self._wait(deadline):
@@ -83,6 +85,10 @@ class RWLock:
                         break
             finally:
                 self._waiting_writers -= 1
+            if contended:
+                from . import optiming
+                if optiming.ENABLED:
+                    optiming.add("tree_write_wait", time.perf_counter() - t_wait)
             if not ok:                        # timed out: reopen the gate unless others need it
                 self._gate = self._writer is not None or self._waiting_writers > 0
                 self._cond.notify_all()

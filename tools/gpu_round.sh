@@ -48,6 +48,13 @@ for s in $STEPS; do
       run ingest_config5_t8 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/ufs_ingest_config5_s3native.jsonl"
       run rocprof_config5 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_config5" -o c5 --output-format csv -- python3 tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 4
       ;;
+    mastertiming)
+      # CPU-only: where one CreateFile's time goes (ALLUXIO_MASTER_OP_TIMING) and the master's CPU
+      for pt in "8 8" "16 4" "32 2"; do
+        set -- $pt
+        ALLUXIO_MASTER_OP_TIMING="$PWD/$OUT/master_optiming_p$1.json" run master_timing_p$1 300 python tools/master_bench_mp.py --ops CreateFile,DeleteFile --procs $1 --threads $2 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_timing_p$1.json"
+      done
+      ;;
     mastergrpc2)
       [ -n "${SKIP_P8:-}" ] || run master_bench_grpc_p8 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 8 --threads 8 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p8.json"
       run master_bench_grpc_p32 500 python tools/master_bench_mp.py --ops CreateFile,GetFileStatus,ListDir,DeleteFile,GetFileStatusNonexistent --procs 32 --threads 2 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_grpc_p32.json"

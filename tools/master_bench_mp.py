@@ -88,9 +88,16 @@ def run(ops, procs, threads, duration, warmup, journal_dir=None, props=(), clien
         time.sleep(1.0)
         out = []
         created = {}     # per client process: files its CreateFile run made (DeleteFile/RenameFile input)
+        def master_cpu_s() -> float:
+            # utime + stime of the master process (the GIL bound shows as ~1 core busy)
+            with open(f"/proc/{master.pid}/stat") as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+
         for op in ops:
             args = ["--operation", op, "--threads", str(threads), "--duration", duration, "--warmup", warmup,
                     *op_args]
+            cpu0, wall0 = master_cpu_s(), time.time()
             ps = []
             for i in range(procs):
                 a = args + ["--base", f"/stress-master-{i}"]
@@ -108,11 +115,18 @@ def run(ops, procs, threads, duration, warmup, journal_dir=None, props=(), clien
                     res.append(json.loads(line[7:]))
                     if op == "CreateFile":
                         created[i] = res[-1]["completed"]
+            cpu = master_cpu_s() - cpu0
+            wall = time.time() - wall0
             total = sum(r["throughput_ops"] for r in res)
             p50 = sorted(r["latency_ms"]["p50"] for r in res)[len(res) // 2] if res else None
+            p99 = sorted(r["latency_ms"].get("p99", 0) for r in res)[len(res) // 2] if res else None
             errs = sum(len(r["errors"]) for r in res)
+            done = sum(r.get("completed", 0) for r in res)
             row = {"operation": op, "procs": procs, "threads_per_proc": threads, "ops_per_s": round(total, 1),
-                   "p50_ms": p50, "errors": errs}
+                   "p50_ms": p50, "p99_ms": p99, "errors": errs,
+                   # master process CPU over the whole client run (setup + warmup + window)
+                   "master_cpu_cores": round(cpu / max(wall, 1e-9), 2),
+                   "master_cpu_us_per_op": round(cpu * 1e6 / done, 1) if done else None}
             print(json.dumps(row), flush=True)
             out.append(row)
         return out
