@@ -12,6 +12,7 @@
 #include "trace.h"
 #include "cpu_codecs.h"
 #include "ipc.h"
+#include "numa_host.h"
 #include "ring_read.h"
 #include "kernels.h"
 #include "seg_ring.h"
@@ -737,6 +738,8 @@ PYBIND11_MODULE(_C, m) {
         }, py::arg("handle"), py::arg("device"), py::arg("timeout_ms"));
   py::register_exception<IpcTimeout>(m, "IpcTimeout", PyExc_TimeoutError);
   m.def("ipc_close", [](uint64_t base) { py::gil_scoped_release rel; ipc_close(base); });
+  m.def("gpu_numa_node", &gpu_numa_node, py::arg("device"));
+  m.def("process_placement", &process_placement);
   m.def("device_arena_alloc", [](uint64_t bytes, int device) {
           py::gil_scoped_release rel;
           return device_arena_alloc(bytes, device);

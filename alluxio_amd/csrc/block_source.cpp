@@ -1,5 +1,6 @@
 // Host-reader block sources and the chunk-buffered input stream (see block_source.h).
 #include "block_source.h"
+#include "numa_host.h"
 
 #include <arpa/inet.h>
 #include <errno.h>
@@ -123,9 +124,14 @@ uint8_t* host_buffer_alloc(uint64_t n, bool* pinned) {
     }
   }
   void* p = nullptr;
-  if (have_device() && hipHostMalloc(&p, n, hipHostMallocDefault) == hipSuccess) {
-    *pinned = true;
-    return static_cast<uint8_t*>(p);
+  if (have_device()) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    p = pinned_alloc_near(n, dev);          // on the NUMA node of the device that DMAs into it
+    if (p) {
+      *pinned = true;
+      return static_cast<uint8_t*>(p);
+    }
   }
   *pinned = false;
   p = std::malloc(n ? n : 1);

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "h2_abi.h"
+#include "numa_host.h"
 
 namespace amdx {
 
@@ -29,7 +30,7 @@ namespace {
 // Pinned staging buffers for HBM chunks (hipHostMalloc is far too slow to call per stream).
 class StagingPool {
  public:
-  StagingPool(uint64_t size, bool pinned) : size_(size), pinned_(pinned) {}
+  StagingPool(uint64_t size, bool pinned, int device = 0) : size_(size), pinned_(pinned), device_(device) {}
   ~StagingPool() {
     for (void* p : free_) release(p);
   }
@@ -43,9 +44,7 @@ class StagingPool {
       }
     }
     void* p = nullptr;
-    if (pinned_) {
-      if (hipHostMalloc(&p, size_, hipHostMallocDefault) != hipSuccess) p = nullptr;
-    }
+    if (pinned_) p = pinned_alloc_near(size_, device_);   // on the GPU's NUMA node
     if (!p) p = std::malloc(size_);
     if (!p) throw StoreError(kErrOutOfSpace, "data server: cannot allocate a staging buffer");
     std::lock_guard<std::mutex> g(mu_);
@@ -76,6 +75,7 @@ class StagingPool {
   }
   uint64_t size_;
   bool pinned_;
+  int device_;
   std::mutex mu_;
   std::vector<void*> free_;
   std::vector<void*> pinned_set_;
@@ -1640,8 +1640,8 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
   if (max_chunk == 0) max_chunk = 2u << 20;
   if (window == 0) window = 4u << 20;
   if (cold.slot_bytes == 0) cold.slot_bytes = 8u << 20;
-  auto pool = std::make_shared<StagingPool>(max_chunk, store->has_device());
-  auto slot_pool = std::make_shared<StagingPool>(cold.slot_bytes, store->has_device());
+  auto pool = std::make_shared<StagingPool>(max_chunk, store->has_device(), store->device());
+  auto slot_pool = std::make_shared<StagingPool>(cold.slot_bytes, store->has_device(), store->device());
   FrameRpcServer* s = &srv;
   srv.set_native_stream(method, [=](const std::string& first, const std::string& cid, const std::string& user,
                                     bool unix_peer, int* status, std::string* msg) -> std::unique_ptr<NativeStream> {
@@ -1711,7 +1711,7 @@ void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_me
                         uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
                         std::shared_ptr<UfsMounts> ufs_roots) {
   if (stage_bytes == 0) stage_bytes = 4u << 20;
-  auto pool = std::make_shared<StagingPool>(stage_bytes, store->has_device());
+  auto pool = std::make_shared<StagingPool>(stage_bytes, store->has_device(), store->device());
   FrameRpcServer* s = &srv;
   srv.set_native_stream(method, [=](const std::string& first, const std::string& cid, const std::string& user,
                                     bool unix_peer, int* status, std::string* msg) -> std::unique_ptr<NativeStream> {

@@ -174,6 +174,10 @@ for s in $STEPS; do
       run wb_host_procs4 600 python tools/worker_bench_host.py --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs.jsonl"
       run wb_host_procs8 600 python tools/worker_bench_host.py --threads 256 --transports grpc,ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs.jsonl"
       ;;
+    numa)
+      run wb_host_procs4_roof 600 python tools/worker_bench_host.py --threads 16,64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --out "$OUT/worker_bench_host_procs_roof.jsonl"
+      run wb_host_procs1_roof 400 python tools/worker_bench_host.py --threads 16 --transports ipc,grpc --duration 6s --warmup 2s --client-procs 1 --d2h-roof --out "$OUT/worker_bench_host_procs_roof.jsonl"
+      ;;
     hostprocs2)
       ALLUXIO_READER_STREAMS=1 run wb_host_procs8_s1 600 python tools/worker_bench_host.py --threads 256 --transports ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs_streams.jsonl"
       ALLUXIO_READER_STREAMS=8 run wb_host_procs8_s8 600 python tools/worker_bench_host.py --threads 256 --transports ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs_streams.jsonl"

@@ -41,8 +41,34 @@ from alluxio_amd.stress import worker_bench
 conf = Configuration({props!r})
 fs = FileSystem(conf=conf, master_address={addr!r}, metadata_cache=True)
 r = worker_bench.main({args!r}, fs=fs, print_result=False)
+from alluxio_amd.ops.native import lib
+r["placement"] = lib().process_placement()
 print("RESULT " + json.dumps(r), flush=True)
 fs.close()
+"""
+
+# Same-run D2H roof: N processes, started together, each copying a 64 MiB device buffer into a
+# pinned host buffer (hipMemcpyAsync D2H + sync) for 2 s -- the platform ceiling the short-circuit
+# readers' D2H refills share.
+ROOF = r"""
+import json, sys, time
+sys.path.insert(0, {root!r})
+import torch
+from alluxio_amd.ops.native import lib
+start = {start!r}
+src = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+dst = torch.empty(64 << 20, dtype=torch.uint8, pin_memory=True)
+dst.copy_(src, non_blocking=True); torch.cuda.synchronize()
+while time.time() < start:
+    time.sleep(0.001)
+n, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < 2.0:
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    n += 1
+el = time.perf_counter() - t0
+print("ROOF " + json.dumps({{"GBps": n * (64 << 20) / el / 1e9, "placement": lib().process_placement(),
+                            "gpu_numa_node": lib().gpu_numa_node(0)}}), flush=True)
 """
 
 
@@ -62,6 +88,8 @@ def main(argv=None) -> int:
                     help="spread the threads over this many client processes (the reference's --clients "
                          "makes N FileSystem instances in one JVM; Python instances in one interpreter "
                          "share one lock, so they go to separate processes); throughput is summed")
+    ap.add_argument("--d2h-roof", action="store_true",
+                    help="after each run, the same number of processes measure the D2H copy roof together")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
 
@@ -124,6 +152,24 @@ def main(argv=None) -> int:
                        "duration_s": r["duration_s"], "errors": r["errors"], "wall_s": round(time.time() - t0, 1),
                        "reader_buffer": a.reader_buffer, "client_props": a.client_prop,
                        "client_procs": nproc}
+                row["client_placement"] = [x.get("placement", "") for x in results]
+                if a.d2h_roof:
+                    start = time.time() + 8.0       # all roof processes start copying together
+                    rp = [subprocess.Popen([sys.executable, "-c", ROOF.format(root=ROOT, start=start)],
+                                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                          for _ in range(nproc)]
+                    roofs = []
+                    for p in rp:
+                        out, err = p.communicate(timeout=120)
+                        line = next((ln for ln in out.splitlines() if ln.startswith("ROOF ")), None)
+                        if line:
+                            roofs.append(json.loads(line[5:]))
+                    row["d2h_roof_GBps"] = round(sum(x["GBps"] for x in roofs), 2)
+                    row["d2h_roof_per_proc"] = [round(x["GBps"], 2) for x in roofs]
+                    row["roof_placement"] = [x["placement"] for x in roofs]
+                    row["gpu_numa_node"] = roofs[0]["gpu_numa_node"] if roofs else None
+                    row["fraction_of_roof"] = round(r["throughput_MBps"] / 1e3 / row["d2h_roof_GBps"], 3) \
+                        if row["d2h_roof_GBps"] else None
                 if stats is not None:
                     row["data_server"] = {"native_streams": stats.streams - s0[0],
                                           "native_bytes": stats.bytes - s0[1],
