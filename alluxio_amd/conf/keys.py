@@ -238,6 +238,11 @@ _k("WORKER_DATA_SERVER_NATIVE_UFS_READ_ENABLED", "alluxio.worker.data.server.nat
    "into a temp block and the I/O thread streams it as it lands; the block is committed at the end.")
 _k("WORKER_DATA_SERVER_NATIVE_UFS_READ_MAX_ACTIVE", "alluxio.worker.data.server.native.ufs.read.max.active",
    "256", Scope.WORKER, "Concurrent native cold reads (one UFS reader thread each); more go to Python.")
+_k("MASTER_JOURNAL_NATIVE_WRITER_ENABLED", "alluxio.master.journal.native.writer.enabled", "true",
+   Scope.MASTER,
+   "UFS journal logs are written by the native group-commit writer (csrc/journal_log.cpp): a C++ "
+   "thread frames, writes and fsyncs the queued entries and sends the replies of the RPCs each commit "
+   "releases without taking the GIL.  false = the Python AsyncJournalWriter.")
 _k("UNDERFS_OBJECT_STORE_UPLOAD_BUFFER_SIZE", "alluxio.underfs.object.store.upload.buffer.size", "256MB",
    Scope.SERVER,
    "Memory one object-store write may hold in multipart part buffers (parts of "

@@ -17,6 +17,7 @@
 #include "kernels.h"
 #include "seg_ring.h"
 #include "frame_rpc.h"
+#include "journal_log.h"
 #include "meta_codec.h"
 #include "fuse_server.h"
 #include "http_blob.h"
@@ -606,15 +607,15 @@ PYBIND11_MODULE(_C, m) {
              s.respond(token, status, msg, p);
            }, py::arg("token"), py::arg("status"), py::arg("message"), py::arg("payload"))
       .def("respond_many", [](FrameRpcServer& s, const py::list& items) {
-             std::vector<std::tuple<uint64_t, int, std::string, std::string>> v;
+             std::vector<FrameReply> v;
              v.reserve(items.size());
              for (auto it : items) {
                auto t = it.cast<py::tuple>();
-               v.emplace_back(t[0].cast<uint64_t>(), t[1].cast<int>(), t[2].cast<std::string>(),
-                              std::string(t[3].cast<py::bytes>()));
+               v.push_back(FrameReply{t[0].cast<uint64_t>(), t[1].cast<int>(), t[2].cast<std::string>(),
+                                      std::string(t[3].cast<py::bytes>())});
              }
              py::gil_scoped_release rel;
-             for (auto& x : v) s.respond(std::get<0>(x), std::get<1>(x), std::get<2>(x), std::get<3>(x));
+             s.respond_batch(v);
            })
       .def("set_user", &FrameRpcServer::set_user)
       .def("set_cacheable", &FrameRpcServer::set_cacheable)
@@ -703,6 +704,31 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("native_opens", &FuseServer::native_opens)
       .def_property_readonly("native_reads", &FuseServer::native_reads)
       .def_property_readonly("fallback_opens", &FuseServer::fallback_opens);
+  py::class_<JournalLog>(m, "JournalLog")
+      .def(py::init<const std::string&, uint64_t, uint64_t, bool, double>(), py::arg("log_dir"),
+           py::arg("next_seq"), py::arg("max_log_bytes"), py::arg("fsync") = true, py::arg("batch_ms") = 5.0)
+      .def("append", [](JournalLog& j, py::bytes entry) {
+             std::string e = entry;   // short critical section: no GIL release
+             return j.append(e);
+           })
+      .def("request", &JournalLog::request)
+      .def("wait_flushed", &JournalLog::wait_flushed, py::arg("counter"), py::arg("timeout_ms") = -1,
+           py::call_guard<py::gil_scoped_release>())
+      .def("reply_when_flushed", [](JournalLog& j, uint64_t counter, FrameRpcServer& srv, const py::tuple& t) {
+             FrameReply r{t[0].cast<uint64_t>(), t[1].cast<int>(), t[2].cast<std::string>(),
+                          std::string(t[3].cast<py::bytes>())};
+             py::gil_scoped_release rel;
+             j.reply_when_flushed(counter, &srv, std::move(r));
+           })
+      .def("close", &JournalLog::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("next_seq", &JournalLog::next_seq)
+      .def_property_readonly("appended", &JournalLog::appended)
+      .def_property_readonly("flushed", &JournalLog::flushed)
+      .def_property_readonly("error", &JournalLog::error)
+      .def_property_readonly("flushes", &JournalLog::flushes)
+      .def_property_readonly("segments", &JournalLog::segments)
+      .def("stats", &JournalLog::stats);
+
   py::class_<FrameRpcClient>(m, "FrameRpcClient")
       .def(py::init<const std::string&, int, const std::string&, int>(), py::arg("host"), py::arg("port"),
            py::arg("auth"), py::arg("timeout_ms") = 60000)

@@ -15,6 +15,7 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -1352,6 +1353,43 @@ void FrameRpcServer::respond(uint64_t token, int status, const std::string& msg,
     ok = send_all(c->fd, f.data(), f.size(), 30000);
   }
   if (!ok) close_conn(c->id);
+}
+
+void FrameRpcServer::respond_batch(const std::vector<FrameReply>& replies) {
+  if (replies.size() == 1) {
+    const FrameReply& r = replies[0];
+    respond(r.token, r.status, r.msg, r.payload);
+    return;
+  }
+  // group by connection, keeping each connection's reply order
+  std::vector<std::pair<uint32_t, std::vector<const FrameReply*>>> groups;
+  for (const FrameReply& r : replies) {
+    const uint32_t cid = (uint32_t)(r.token >> 32);
+    auto it = std::find_if(groups.begin(), groups.end(), [&](const auto& g) { return g.first == cid; });
+    if (it == groups.end()) {
+      groups.emplace_back(cid, std::vector<const FrameReply*>());
+      it = groups.end() - 1;
+    }
+    it->second.push_back(&r);
+  }
+  for (auto& g : groups) {
+    auto c = find(g.first);
+    if (!c || c->closed) continue;
+    bool ok = true;
+    if (c->proto == 2) {
+      std::lock_guard<std::mutex> lk(c->wmu);
+      if (!c->h2) continue;
+      for (const FrameReply* r : g.second)
+        H2::respond_locked(*c->h2, (int32_t)(r->token & 0x7fffffffu), r->status, r->msg, r->payload);
+      ok = H2::flush_locked(*c->h2);
+    } else {
+      std::string buf;
+      for (const FrameReply* r : g.second) buf += make_response((uint32_t)r->token, r->status, r->msg, r->payload);
+      std::lock_guard<std::mutex> lk(c->wmu);
+      ok = send_all(c->fd, buf.data(), buf.size(), 30000);
+    }
+    if (!ok) close_conn(c->id);
+  }
 }
 
 void FrameRpcServer::set_user(uint64_t token, const std::string& user) {

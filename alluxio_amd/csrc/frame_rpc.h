@@ -37,6 +37,13 @@
 
 namespace amdx {
 
+struct FrameReply {
+  uint64_t token;
+  int status;
+  std::string msg;
+  std::string payload;
+};
+
 struct FrameRequest {
   uint64_t token;      // (conn id << 32) | call id
   uint32_t method;     // registered method index (0 = "@auth", unknown = 0xffffffff)
@@ -95,6 +102,9 @@ class FrameRpcServer {
   // Up to `max_n` requests of `lane`, waiting at most timeout_ms for the first (GIL released).
   std::vector<FrameRequest> poll(int lane, int max_n, int timeout_ms);
   void respond(uint64_t token, int status, const std::string& msg, const std::string& payload);
+  // Many replies: those of one connection go out under one write lock with one flush / send
+  // (a journal group commit releases dozens of deferred replies at once).
+  void respond_batch(const std::vector<FrameReply>& replies);
   // Bind a user to the connection of `token` (after a successful @auth).
   void set_user(uint64_t token, const std::string& user);
   uint64_t requests() const { return requests_.load(); }

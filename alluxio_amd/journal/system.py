@@ -16,6 +16,7 @@ import struct
 import threading
 import time
 
+from ..utils import optiming as _OPT
 from ..utils.exceptions import JournalClosedException, UnavailableException
 from . import format as fmt
 from .ufs_journal import UfsJournal, UfsJournalLogWriter
@@ -78,6 +79,12 @@ class Journaled:
         if not self.process_journal_entry(entry):
             raise RuntimeError(f"{self.journal_name} cannot apply its own entry {entry}")
         ctx.append(entry)
+
+
+def _error_reply(reply, err):
+    from ..utils import exceptions as ex
+    se = ex.wrap(err)
+    return (reply[0], int(se.status), se.message or str(se), b"")
 
 
 class AsyncJournalWriter:
@@ -147,11 +154,44 @@ class AsyncJournalWriter:
                     return
         cb(err)
 
+    def reply_when_flushed(self, counter: int, srv, reply) -> None:
+        """Send the RPC ``reply`` (a native server's respond_many tuple) once entries up to
+        ``counter`` are durable -- an error reply if the flush fails.  The flush thread sends every
+        reply its flush released in ONE respond_many call per server (one wakeup of the server's
+        I/O threads per group commit instead of one per deferred RPC)."""
+        with self._cond:
+            if self._error is None and self._flushed < counter and not (self._closed and not self._queue):
+                heapq.heappush(self._waiters, (counter, next(self._seq), (srv, reply)))
+                if counter > self._requested:
+                    self._requested = counter
+                    self._cond.notify_all()
+                return
+            err = None
+            if self._error is not None:
+                err = UnavailableException(f"journal flush failed: {self._error}")
+            elif self._flushed < counter:
+                err = JournalClosedException("journal closed before flush")
+        srv.respond_many([reply if err is None else _error_reply(reply, err)])
+
     def _fire(self, flushed: int, err=None) -> None:
         ready = []
+        replies: dict = {}
         with self._cond:
             while self._waiters and (err is not None or self._waiters[0][0] <= flushed):
-                ready.append(heapq.heappop(self._waiters)[2])
+                w = heapq.heappop(self._waiters)[2]
+                if type(w) is tuple:
+                    srv, reply = w
+                    ent = replies.get(id(srv))
+                    if ent is None:
+                        ent = replies[id(srv)] = (srv, [])
+                    ent[1].append(reply if err is None else _error_reply(reply, err))
+                else:
+                    ready.append(w)
+        for srv, batch in replies.values():
+            try:
+                srv.respond_many(batch)
+            except Exception:  # noqa: BLE001
+                LOG.exception("journal flush replies failed")
         for cb in ready:
             try:
                 cb(err)
@@ -190,6 +230,7 @@ class AsyncJournalWriter:
                 batch, self._queue = self._queue, []
             try:
                 t0 = time.monotonic()
+                c0 = time.thread_time() if _OPT.ENABLED else 0.0
                 n = 0
                 for e in batch:
                     self.writer.write(e)
@@ -199,13 +240,23 @@ class AsyncJournalWriter:
                 if n < len(batch):       # session over: the rest goes first next time
                     with self._cond:
                         self._queue[:0] = batch[n:]
+                if _OPT.ENABLED:
+                    c1 = time.thread_time()
+                    _OPT.add("journal_write_cpu_per_entry", (c1 - c0) / max(1, n))
+                    _OPT.add("journal_entries_per_flush", n * 1e-6)
+                    f0 = time.perf_counter()
                 self.writer.flush()
+                if _OPT.ENABLED:
+                    _OPT.add("journal_fsync_wall", time.perf_counter() - f0)
                 with self._cond:
                     self._written += n
                     self._flushed = flushed = self._written
                     self._cond.notify_all()
                 if self._waiters:
+                    c2 = time.thread_time() if _OPT.ENABLED else 0.0
                     self._fire(flushed)
+                    if _OPT.ENABLED:
+                        _OPT.add("journal_fire_cpu_per_entry", (time.thread_time() - c2) / max(1, n))
             except BaseException as e:  # noqa: BLE001
                 LOG.exception("journal flush failed")
                 with self._cond:
@@ -219,6 +270,135 @@ class AsyncJournalWriter:
             self._cond.notify_all()
         self._thread.join(timeout=10)
         self.writer.close()
+
+
+class NativeAsyncJournalWriter:
+    """AsyncJournalWriter over the native group-commit log (csrc/journal_log.cpp): same interface
+    (append / flush / flush_async / reply_when_flushed / close, ``writer.next_seq``), but the flush
+    loop -- framing, write, fsync, segment rotation, and the replies of the RPCs a commit releases --
+    runs on a C++ thread that never takes the GIL.  Python callbacks (``flush_async``: RPCs with
+    post-durable work or entries in several journals) are fired by a helper thread that waits on
+    the native log with the GIL released.
+
+    Parity: AsyncJournalWriter.java:243-295 (doFlush), :334 (flush); UfsJournalLogWriter.java:115-209.
+    """
+
+    def __init__(self, journal: UfsJournal, next_seq: int, fsync: bool = True, batch_ms: float = 5.0,
+                 flush_timeout_s: float = 300.0):
+        from ..ops.native import lib
+        UfsJournalLogWriter(journal, next_seq, fsync=fsync)    # completes the previous incomplete log
+        self._log = lib().JournalLog(journal.log_dir, next_seq, journal.max_log_bytes, fsync, batch_ms)
+        self.writer = self               # ``w.writer.next_seq`` (checkpoint / sequence_numbers)
+        self.flush_timeout = flush_timeout_s
+        self._cb_cond = threading.Condition()
+        self._cbs: list = []             # heap of (counter, seq, callback)
+        self._seq = itertools.count()
+        self._cb_thread: threading.Thread | None = None
+        self._closed = False
+        self._servers: set = set()       # servers with replies in flight (kept alive until close)
+        if _OPT.ENABLED:
+            _OPT.add_reporter(f"journal_commit:{journal.name}",
+                              self.commit_stats)
+
+    def commit_stats(self) -> dict:
+        e, f, w, s, r, wait, mx = self._log.stats()
+        return {"entries": e, "flushes": f, "entries_per_flush": round(e / max(1, f), 1),
+                "write_us_per_flush": round(w / max(1, f), 1), "fsync_us_per_flush": round(s / max(1, f), 1),
+                "reply_us_per_flush": round(r / max(1, f), 1),
+                "append_to_durable_us_mean": round(wait / max(1, e), 1), "append_to_durable_us_max": mx}
+
+    @property
+    def next_seq(self) -> int:
+        return self._log.next_seq
+
+    @property
+    def _appended(self) -> int:
+        return self._log.appended
+
+    @staticmethod
+    def _raise(e: RuntimeError):
+        msg = str(e)
+        if msg.startswith("closed: "):
+            raise JournalClosedException(msg[len("closed: "):]) from None
+        raise UnavailableException(msg[len("failed: "):] if msg.startswith("failed: ") else msg) from None
+
+    def append(self, entry) -> int:
+        if entry.sequence_number:
+            entry.sequence_number = 0      # the native log prepends the sequence number it assigns
+        try:
+            return self._log.append(entry.SerializeToString())
+        except RuntimeError as e:
+            self._raise(e)
+
+    def flush(self, counter: int) -> None:
+        try:
+            if self._log.wait_flushed(counter, int(self.flush_timeout * 1000)):
+                raise UnavailableException("journal flush timed out")
+        except RuntimeError as e:
+            self._raise(e)
+
+    def reply_when_flushed(self, counter: int, srv, reply) -> None:
+        if srv not in self._servers:
+            self._servers.add(srv)
+        self._log.reply_when_flushed(counter, srv, reply)
+
+    def flush_async(self, counter: int, cb) -> None:
+        with self._cb_cond:
+            if not self._closed:
+                heapq.heappush(self._cbs, (counter, next(self._seq), cb))
+                if self._cb_thread is None:
+                    self._cb_thread = threading.Thread(target=self._cb_loop, daemon=True, name="journal-callbacks")
+                    self._cb_thread.start()
+                self._cb_cond.notify()
+                self._log.request(counter)
+                return
+        cb(JournalClosedException("journal closed before flush"))
+
+    def _cb_loop(self) -> None:
+        while True:
+            with self._cb_cond:
+                while not self._cbs and not self._closed:
+                    self._cb_cond.wait(0.5)
+                if not self._cbs:
+                    return
+                target = self._cbs[0][0]
+            err = None
+            try:
+                if self._log.wait_flushed(target, 200):
+                    continue                  # timed out: re-check (new, lower counters may have come)
+            except RuntimeError as e:
+                try:
+                    self._raise(e)
+                except Exception as ex_:  # noqa: BLE001
+                    err = ex_
+            flushed = self._log.flushed
+            ready = []
+            with self._cb_cond:
+                while self._cbs and (err is not None or self._cbs[0][0] <= flushed):
+                    ready.append(heapq.heappop(self._cbs)[2])
+            for cb in ready:
+                try:
+                    cb(err)
+                except Exception:  # noqa: BLE001
+                    LOG.exception("journal flush callback failed")
+
+    def close(self) -> None:
+        self._log.close()                 # flushes what is queued; replies go out or fail
+        with self._cb_cond:
+            self._closed = True
+            self._cb_cond.notify_all()
+        t = self._cb_thread
+        if t is not None:
+            t.join(timeout=10)
+        with self._cb_cond:                # callbacks whose entries never became durable
+            rest, self._cbs = self._cbs, []
+        flushed = self._log.flushed
+        for c, _s, cb in rest:
+            try:
+                cb(None if c <= flushed else JournalClosedException("journal closed before flush"))
+            except Exception:  # noqa: BLE001
+                LOG.exception("journal flush callback failed")
+        self._servers.clear()
 
 
 class JournalContext:
@@ -314,10 +494,19 @@ class NoopJournalSystem(JournalSystem):
     """No persistence (tests, ephemeral masters)."""
 
 
+def _native_journal_available() -> bool:
+    try:
+        from ..ops.native import lib
+        return hasattr(lib(), "JournalLog")
+    except Exception:  # noqa: BLE001 - extension not built: the Python writer
+        return False
+
+
 class UfsJournalSystem(JournalSystem):
     def __init__(self, root: str, max_log_bytes: int = 10 << 20, flush_batch_ms: float = 5.0,
-                 checkpoint_period_entries: int = 2_000_000, fsync: bool = True):
+                 checkpoint_period_entries: int = 2_000_000, fsync: bool = True, native_writer: bool = False):
         super().__init__()
+        self.native_writer = native_writer
         self.root = root
         self.max_log_bytes = max_log_bytes
         self.flush_batch_ms = flush_batch_ms
@@ -454,8 +643,12 @@ class UfsJournalSystem(JournalSystem):
             self._replay_all()
             for name, j in self._journals.items():
                 nxt = max(self._applied.get(name, 0), j.next_sequence_number())
-                w = UfsJournalLogWriter(j, nxt, fsync=self.fsync)
-                self._writers[name] = AsyncJournalWriter(w, self.flush_batch_ms)
+                if self.native_writer and _native_journal_available():
+                    self._writers[name] = NativeAsyncJournalWriter(j, nxt, fsync=self.fsync,
+                                                                   batch_ms=self.flush_batch_ms)
+                else:
+                    w = UfsJournalLogWriter(j, nxt, fsync=self.fsync)
+                    self._writers[name] = AsyncJournalWriter(w, self.flush_batch_ms)
         super().gain_primacy()
 
     def lose_primacy(self) -> None:

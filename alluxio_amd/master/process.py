@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import logging
 import os
+import sys
 import threading
 import time
 
@@ -74,7 +75,8 @@ def build_journal_system(conf: Configuration, host: str | None = None, enable_gr
                                            ephemeral_port=ephemeral)
     return UfsJournalSystem(folder, max_log_bytes=conf.get_bytes("alluxio.master.journal.log.size.bytes.max"),
                             flush_batch_ms=conf.get_ms("alluxio.master.journal.flush.batch.time"),
-                            checkpoint_period_entries=conf.get_int("alluxio.master.journal.checkpoint.period.entries"))
+                            checkpoint_period_entries=conf.get_int("alluxio.master.journal.checkpoint.period.entries"),
+                            native_writer=conf.get_bool("alluxio.master.journal.native.writer.enabled"))
 
 
 class AlluxioMasterProcess:
@@ -474,6 +476,9 @@ def main(argv=None) -> int:  # pragma: no cover - CLI entry
     from ..conf import Configuration as _C
     from ..web.logserver import attach
     attach("MASTER", _C(load_site=True))
+    import os as _os
+    if _os.environ.get("ALLUXIO_SWITCH_INTERVAL_US"):
+        sys.setswitchinterval(float(_os.environ["ALLUXIO_SWITCH_INTERVAL_US"]) / 1e6)
     from ..utils import optiming
     if optiming.ENABLED:                 # the bench stops the master with SIGTERM: dump first
         import signal

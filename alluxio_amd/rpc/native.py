@@ -34,6 +34,7 @@ import weakref
 from ..journal.system import deferred_flush
 from ..proto import SERVICES
 from ..utils import exceptions as ex
+from ..utils import optiming as _OPT
 
 LOG = logging.getLogger(__name__)
 
@@ -294,6 +295,7 @@ class NativeRpcFrontend:
         from ..security import as_user
         from ..utils import optiming
         t_start = time.perf_counter() if optiming.ENABLED else 0.0
+        c_start = time.thread_time() if optiming.ENABLED else 0.0
         pending = None
         after = None
         cache_ep = None
@@ -346,6 +348,7 @@ class NativeRpcFrontend:
                 self.server.cache_put(midx, key_user, payload, b"", cache_ep, reply[1], reply[2])
         if optiming.ENABLED and midx:
             optiming.add("handler:" + self.methods[midx][0].rsplit("/", 1)[-1], time.perf_counter() - t_start)
+            optiming.add("cpu_one:" + self.methods[midx][0].rsplit("/", 1)[-1], time.thread_time() - c_start)
         if pending:
             self._defer(pending, reply, after, self.methods[midx][0].rsplit("/", 1)[-1] if optiming.ENABLED else "")
             return None
@@ -364,6 +367,12 @@ class NativeRpcFrontend:
     def _defer(self, pending: dict, reply, after: list | None = None, name: str = "") -> None:
         """Send ``reply`` once every journal writer in ``pending`` flushed past its counter
         (after running the RPC's after_durable callbacks; on a failed flush they never run)."""
+        if len(pending) == 1 and not after:
+            (w, counter), = pending.items()
+            rwf = getattr(w, "reply_when_flushed", None)
+            if rwf is not None:          # common case: batched reply from the flush thread
+                rwf(counter, self.server, reply)
+                return
         left = [len(pending)]
         err = [None]
         lock = threading.Lock()
@@ -480,16 +489,24 @@ class NativeRpcFrontend:
         if prof_path:                  # per-lane-thread cProfile (diagnostics: where handler time goes)
             import cProfile
             pr = cProfile.Profile()
+            out = f"{prof_path}.lane{lane}.{threading.get_ident()}"
+            nxt = [time.monotonic() + 2.0]
+
+            def tick():                # dump every 2 s from this thread (the master is SIGTERMed)
+                if time.monotonic() >= nxt[0]:
+                    pr.dump_stats(out)
+                    pr.enable()
+                    nxt[0] = time.monotonic() + 2.0
             pr.enable()
             try:
-                self._loop_inner(lane, batch)
+                self._loop_inner(lane, batch, tick)
             finally:
                 pr.disable()
-                pr.dump_stats(f"{prof_path}.lane{lane}.{threading.get_ident()}")
+                pr.dump_stats(out)
             return
         self._loop_inner(lane, batch)
 
-    def _loop_inner(self, lane: int, batch: int) -> None:
+    def _loop_inner(self, lane: int, batch: int, tick=None) -> None:
         srv = self.server
         metrics = self.rpc.metrics
         while self._running:
@@ -507,13 +524,19 @@ class NativeRpcFrontend:
                     self._stream_exec.submit(self._run_stream, *r)
                 continue
             t0 = time.perf_counter()
+            c0 = time.thread_time() if tick is not None or _OPT.ENABLED else 0.0
             nb = lane != LANE_BLOCKING
             out = [o for o in (self._one(*r, nonblocking=nb) for r in reqs) if o is not None]
             if out:
                 srv.respond_many(out)
+            if _OPT.ENABLED:
+                _OPT.add(f"cpu_batch:lane{lane}", time.thread_time() - c0)
+                _OPT.add(f"batch_size:lane{lane}", len(reqs) * 1e-6)     # reported in "us" = count
             if metrics is not None:
                 metrics.counter("NativeRpcCalls").inc(len(reqs))
                 metrics.timer("NativeRpcBatch").update(time.perf_counter() - t0)
+            if tick is not None:
+                tick()
 
 
 class NativeChannelCore:

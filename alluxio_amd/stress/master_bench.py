@@ -87,6 +87,7 @@ def main(argv=None, fs=None, print_result=True) -> dict:
     warm_s = parse_time_size(a.warmup) / 1000.0
     dur_s = parse_time_size(a.duration) / 1000.0
     start = time.perf_counter() + 0.05
+    wall_off = time.time() - time.perf_counter()
     record_from = start + warm_s
     end = record_from + dur_s
     results = []
@@ -167,6 +168,7 @@ def main(argv=None, fs=None, print_result=True) -> dict:
     def pct(p):
         return lats[min(len(lats) - 1, int(p * len(lats)))] * 1e3 if lats else 0.0
     out = {"bench": "master", "operation": a.operation, "threads": a.threads, "ops": total,
+           "window_wall": [record_from + wall_off, record_from + window + wall_off],
            "completed": sum(r[3] for r in results),
            "throughput_ops": total / window, "latency_ms": {"p50": pct(0.5), "p90": pct(0.9), "p99": pct(0.99),
                                                              "max": lats[-1] * 1e3 if lats else 0.0},

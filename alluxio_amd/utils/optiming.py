@@ -39,9 +39,22 @@ def add(key: str, seconds: float) -> None:
                 s[j] = seconds
 
 
+_REPORTERS: dict = {}
+
+
+def add_reporter(name: str, fn) -> None:
+    """``fn()`` -> dict, included in the report under ``name`` (e.g. native journal commit stats)."""
+    _REPORTERS[name] = fn
+
+
 def report() -> dict:
     with _LOCK:
         out = {}
+        for name, fn in list(_REPORTERS.items()):
+            try:
+                out[name] = fn()
+            except Exception as e:  # noqa: BLE001
+                out[name] = {"error": str(e)}
         for k, s in _SAMPLES.items():
             v = sorted(s)
             out[k] = {"count": _COUNTS[k], "mean_us": round(_SUMS[k] / _COUNTS[k] * 1e6, 1),

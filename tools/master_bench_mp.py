@@ -21,6 +21,7 @@ import socket
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -88,16 +89,32 @@ def run(ops, procs, threads, duration, warmup, journal_dir=None, props=(), clien
         time.sleep(1.0)
         out = []
         created = {}     # per client process: files its CreateFile run made (DeleteFile/RenameFile input)
-        def master_cpu_s() -> float:
+        def master_cpu_s(split: bool = False):
             # utime + stime of the master process (the GIL bound shows as ~1 core busy)
             with open(f"/proc/{master.pid}/stat") as f:
                 fields = f.read().rsplit(")", 1)[1].split()
-            return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+            tck = os.sysconf("SC_CLK_TCK")
+            if split:
+                return int(fields[11]) / tck, int(fields[12]) / tck
+            return (int(fields[11]) + int(fields[12])) / tck
 
         for op in ops:
             args = ["--operation", op, "--threads", str(threads), "--duration", duration, "--warmup", warmup,
                     *op_args]
-            cpu0, wall0 = master_cpu_s(), time.time()
+            (u0, s0), wall0 = master_cpu_s(True), time.time()
+            cpu0 = u0 + s0
+            samples = []            # (wall, user, sys) every 50 ms: the master's CPU inside the window
+            stop_smp = threading.Event()
+
+            def sampler():
+                while not stop_smp.is_set():
+                    try:
+                        samples.append((time.time(), *master_cpu_s(True)))
+                    except OSError:
+                        return
+                    stop_smp.wait(0.05)
+            smp = threading.Thread(target=sampler, daemon=True)
+            smp.start()
             ps = []
             for i in range(procs):
                 a = args + ["--base", f"/stress-master-{i}"]
@@ -115,7 +132,21 @@ def run(ops, procs, threads, duration, warmup, journal_dir=None, props=(), clien
                     res.append(json.loads(line[7:]))
                     if op == "CreateFile":
                         created[i] = res[-1]["completed"]
-            cpu = master_cpu_s() - cpu0
+            u1, s1 = master_cpu_s(True)
+            cpu = u1 + s1 - cpu0
+            stop_smp.set()
+            smp.join()
+            win = None
+            ws = [r["window_wall"] for r in res if "window_wall" in r]
+            if ws:
+                w0, w1 = max(w[0] for w in ws), min(w[1] for w in ws)
+                inside = [x for x in samples if w0 <= x[0] <= w1]
+                if len(inside) >= 2 and inside[-1][0] > inside[0][0]:
+                    dt = inside[-1][0] - inside[0][0]
+                    du, ds = inside[-1][1] - inside[0][1], inside[-1][2] - inside[0][2]
+                    tot = sum(r["throughput_ops"] for r in res)
+                    win = {"cores": round((du + ds) / dt, 2), "user_cores": round(du / dt, 2),
+                           "us_per_op": round((du + ds) * 1e6 / (tot * dt), 1) if tot else None}
             wall = time.time() - wall0
             total = sum(r["throughput_ops"] for r in res)
             p50 = sorted(r["latency_ms"]["p50"] for r in res)[len(res) // 2] if res else None
@@ -126,7 +157,10 @@ def run(ops, procs, threads, duration, warmup, journal_dir=None, props=(), clien
                    "p50_ms": p50, "p99_ms": p99, "errors": errs,
                    # master process CPU over the whole client run (setup + warmup + window)
                    "master_cpu_cores": round(cpu / max(wall, 1e-9), 2),
-                   "master_cpu_us_per_op": round(cpu * 1e6 / done, 1) if done else None}
+                   "master_cpu_us_per_op": round(cpu * 1e6 / done, 1) if done else None,
+                   "master_sys_fraction": round((s1 - s0) / cpu, 2) if cpu > 0 else None,
+                   # the same, sampled inside the timed window only (all clients running)
+                   "master_cpu_window": win}
             print(json.dumps(row), flush=True)
             out.append(row)
         return out
