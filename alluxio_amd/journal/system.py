@@ -323,10 +323,14 @@ class NativeAsyncJournalWriter:
         raise UnavailableException(msg[len("failed: "):] if msg.startswith("failed: ") else msg) from None
 
     def append(self, entry) -> int:
-        if entry.sequence_number:
-            entry.sequence_number = 0      # the native log prepends the sequence number it assigns
+        if type(entry) is fmt.RawEntryBatch:
+            data = entry.body              # natively encoded batch body, no sequence number yet
+        else:
+            if entry.sequence_number:
+                entry.sequence_number = 0  # the native log prepends the sequence number it assigns
+            data = entry.SerializeToString()
         try:
-            return self._log.append(entry.SerializeToString())
+            return self._log.append(data)
         except RuntimeError as e:
             self._raise(e)
 

@@ -311,3 +311,19 @@ def test_native_writer_replay_through_journal_system(tmp_path):
     js3.start()
     assert c3.ids == list(range(26))
     js3.stop()
+
+
+def test_native_writer_raw_entry_batch_sequence(tmp_path):
+    """Natively encoded batches (RawEntryBatch) get the native writer's sequence number."""
+    from alluxio_amd.journal.system import NativeAsyncJournalWriter
+    from alluxio_amd.ops.native import lib
+    j = UfsJournal(str(tmp_path), "BlockMaster", max_log_bytes=1 << 20)
+    j.format()
+    w = NativeAsyncJournalWriter(j, 3, fsync=False)
+    w.append(_entry(1))
+    c = w.append(fmt.RawEntryBatch(lib().encode_block_info_batch([11, 12], [5, 6]), 2))
+    w.flush(c)
+    w.close()
+    got = list(j.iter_log_entries(3))
+    assert [e.sequence_number for e in got] == [3, 4]
+    assert [x.block_info.block_id for x in got[1].journal_entries] == [11, 12]
