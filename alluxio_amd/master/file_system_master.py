@@ -38,6 +38,7 @@ from .mount_table import ROOT_MOUNT_ID, MountInfo, MountTable, UfsManager
 LOG = logging.getLogger(__name__)
 
 THROUGH_TYPES = ("CACHE_THROUGH", "THROUGH")
+_TTL_NUM = {v.name: v.number for v in pb.grpc.TtlAction.values}
 LOAD_NEVER, LOAD_ONCE, LOAD_ALWAYS = "NEVER", "ONCE", "ALWAYS"
 
 
@@ -118,6 +119,8 @@ class FileSystemMaster(Journaled):
         self.block_master = block_master
         self.journal = journal_system
         self.metrics = metrics
+        self._counters: dict = {}      # metric name -> Counter (the registry lookup formats names)
+        self._pg_cache: dict = {}      # user -> (monotonic time, primary group)
         self.ufs_manager = UfsManager(conf)
         self.mount_table = MountTable(self.ufs_manager)
         from .metastore import create_inode_store
@@ -370,9 +373,13 @@ class FileSystemMaster(Journaled):
         self.permission.check(self._user(), chain, bits, path)
 
     def _owner_group(self):
-        from ..security import primary_group
         user = self._user() or self.permission.superuser
-        return user, primary_group(user)
+        hit = self._pg_cache.get(user)
+        now = time.monotonic()
+        if hit is None or now - hit[0] > 10.0:     # under the group mapping's own 60 s cache
+            from ..security import primary_group
+            hit = self._pg_cache[user] = (now, primary_group(user))
+        return user, hit[1]
 
     def _resolve_ufs(self, path: str):
         return self.mount_table.resolve(path)
@@ -391,8 +398,12 @@ class FileSystemMaster(Journaled):
         return UfsMode.READ_WRITE
 
     def _count(self, name: str, n: int = 1) -> None:
-        if self.metrics is not None:
-            self.metrics.counter(name).inc(n)
+        c = self._counters.get(name)
+        if c is None:
+            if self.metrics is None:
+                return
+            c = self._counters[name] = self.metrics.counter(name)
+        c.inc(n)
 
     # ------------------------------------------------------------------------------------------
     # FileInfo
@@ -452,7 +463,7 @@ class FileSystemMaster(Journaled):
             lastModificationTimeMs=inode.last_modification_time_ms, ttl=inode.ttl, owner=inode.owner,
             group=inode.group, mode=inode.mode, persistenceState=inode.persistence_state,
             mountPoint=getattr(inode, "mount_point", False),
-            ttlAction=pb.grpc.TtlAction.values_by_name[inode.ttl_action].number,
+            ttlAction=_TTL_NUM[inode.ttl_action],
             ufsFingerprint=inode.ufs_fingerprint, lastAccessTimeMs=inode.last_access_time_ms)
         for k, v in inode.xattr.items():
             fi.xattr[k] = v

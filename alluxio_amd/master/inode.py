@@ -20,6 +20,11 @@ TO_BE_PERSISTED = "TO_BE_PERSISTED"
 LOST = "LOST"
 
 
+# enum name <-> number of PTtlAction (dict lookups: descriptor ``values_by_*`` are slow per call)
+_PTTL_NUM = {v.name: v.number for v in pb.journal.PTtlAction.values}
+_PTTL_NAME = {v.number: v.name for v in pb.journal.PTtlAction.values}
+
+
 def now_ms() -> int:
     return int(time.time() * 1000)
 
@@ -88,7 +93,7 @@ class Inode:
         if e.HasField("ttl"):
             self.ttl = e.ttl
         if e.HasField("ttlAction"):
-            self.ttl_action = pb.journal.PTtlAction.values_by_number[e.ttlAction].name
+            self.ttl_action = _PTTL_NAME[e.ttlAction]
         if e.HasField("ufs_fingerprint"):
             self.ufs_fingerprint = e.ufs_fingerprint
         if e.medium_type:
@@ -114,7 +119,7 @@ class InodeDirectory(Inode):
             last_modification_time_ms=self.last_modification_time_ms, owner=self.owner,
             group=self.group, mode=self.mode, mount_point=self.mount_point,
             direct_children_loaded=self.direct_children_loaded, ttl=self.ttl,
-            ttlAction=pb.journal.PTtlAction.values_by_name[self.ttl_action].number,
+            ttlAction=_PTTL_NUM[self.ttl_action],
             last_access_time_ms=self.last_access_time_ms, medium_type=self.medium_types)
         if path:
             e.path = path
@@ -136,7 +141,7 @@ class InodeDirectory(Inode):
         d.mount_point = e.mount_point
         d.direct_children_loaded = e.direct_children_loaded
         d.ttl = e.ttl if e.HasField("ttl") else NO_TTL
-        d.ttl_action = pb.journal.PTtlAction.values_by_number[e.ttlAction].name
+        d.ttl_action = _PTTL_NAME[e.ttlAction]
         d.xattr = dict(e.xAttr)
         d.medium_types = list(e.medium_type)
         if e.HasField("acl"):
@@ -182,7 +187,7 @@ class InodeFile(Inode):
             block_size_bytes=self.block_size_bytes, length=self.length, completed=self.completed,
             cacheable=self.cacheable, blocks=self.block_ids, ttl=self.ttl, owner=self.owner,
             group=self.group, mode=self.mode,
-            ttlAction=pb.journal.PTtlAction.values_by_name[self.ttl_action].number,
+            ttlAction=_PTTL_NUM[self.ttl_action],
             ufs_fingerprint=self.ufs_fingerprint, replication_max=self.replication_max,
             replication_min=self.replication_min, persist_job_id=self.persist_job_id,
             temp_ufs_path=self.temp_ufs_path, replication_durable=self.replication_durable,
@@ -210,7 +215,7 @@ class InodeFile(Inode):
         f.block_ids = list(e.blocks)
         f._next_seq = len(f.block_ids)
         f.ttl = e.ttl if e.HasField("ttl") else NO_TTL
-        f.ttl_action = pb.journal.PTtlAction.values_by_number[e.ttlAction].name
+        f.ttl_action = _PTTL_NAME[e.ttlAction]
         f.ufs_fingerprint = e.ufs_fingerprint
         f.replication_max = e.replication_max if e.HasField("replication_max") else -1
         f.replication_min = e.replication_min

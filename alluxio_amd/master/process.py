@@ -487,6 +487,15 @@ def main(argv=None) -> int:  # pragma: no cover - CLI entry
     if a.format:
         m.format()
     m.start()
+    # The namespace is millions of long-lived tracked objects: with the default gen0 threshold (700)
+    # the cyclic collector runs every few RPCs and its older-generation passes walk the whole tree.
+    # Freeze what startup/replay built and collect young objects less often (cycles are rare here;
+    # refcounting frees the per-RPC garbage).
+    gen0 = int(_os.environ.get("ALLUXIO_MASTER_GC_GEN0", "50000"))
+    if gen0 > 0:
+        import gc
+        gc.freeze()
+        gc.set_threshold(gen0, 20, 100)
     stop = threading.Event()
     try:
         stop.wait()
