@@ -990,40 +990,212 @@ bool make_parents(const std::string& path, int* err) {
   return true;
 }
 
-// UFS_FILE WriteBlock into a local-directory UFS: chunks are written to a temp file beside the
-// target on the I/O thread; the half-close sets the mode and renames it over the target (the
-// local UFS's atomic create, underfs/local.py _AtomicWriter).  A failed or cancelled call
-// removes the temp file and leaves the target untouched.
-class UfsFileWriteStream : public WriteStreamBase {
+// Threads for local-UFS file I/O of UFS_FILE write streams (immortal, like the upload pool): the
+// I/O thread only queues chunks; mkdir, open, write(2), chmod and rename run here, so a slow or
+// throttled disk never stalls the other streams multiplexed on that I/O thread.
+class FilePool {
  public:
-  UfsFileWriteStream(const std::string& path, int mode, std::shared_ptr<DataServerStats> stats)
-      : path_(path), mode_(mode), stats_(std::move(stats)) {}
+  static FilePool& get() {
+    static FilePool* p = new FilePool(8);
+    return *p;
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
 
-  // Creates the parents and the temp file; false with *status / *msg set on failure.
-  bool open(int* status, std::string* msg) {
+ private:
+  explicit FilePool(int n) {
+    for (int i = 0; i < n; ++i)
+      std::thread([this] {
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return !q_.empty(); });
+            f = std::move(q_.front());
+            q_.pop_front();
+          }
+          try {
+            f();
+          } catch (...) {
+          }
+        }
+      }).detach();
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
+
+// State of one local UFS file write shared by its stream (I/O thread) and its pool tasks: one task
+// at a time drains the chunk queue in order.
+struct LocalFileJob {
+  std::string path, tmp;
+  int mode = 0644;
+  int fd = -1;
+  std::mutex mu;
+  std::deque<std::string> chunks;
+  uint64_t queued = 0, written = 0;   // bytes
+  bool running = false, opened = false, failed = false, cancelled = false;
+  bool end = false, finished = false, cleaned = false;
+  int err_status = 0;
+  std::string err;
+  std::function<void()> wake;
+  std::shared_ptr<DataServerStats> stats;
+
+  void poke() {
+    std::function<void()> w;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      w = wake;
+    }
+    if (w) w();
+  }
+
+  void fail_locked(int e, const std::string& what) {
+    if (failed) return;
+    failed = true;
+    err_status = grpc_status_of_errno(e);
+    err = what + ": " + std::strerror(e);
+  }
+
+  // Creates the parents and the temp file beside the target.
+  bool open_file() {
     int e = 0;
-    if (!make_parents(path_, &e)) {
-      *status = grpc_status_of_errno(e);
-      *msg = "creating the parent of " + path_ + ": " + std::strerror(e);
+    if (!make_parents(path, &e)) {
+      std::lock_guard<std::mutex> g(mu);
+      fail_locked(e, "creating the parent of " + path);
       return false;
     }
     thread_local std::mt19937_64 rng(std::random_device{}());
     char tag[17];
     std::snprintf(tag, sizeof(tag), "%08x", (unsigned)(rng() & 0xffffffffu));
-    tmp_ = path_ + ".alluxio." + tag + ".tmp";
-    fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0666);
-    if (fd_ < 0) {
-      e = errno;
-      *status = grpc_status_of_errno(e);
-      *msg = "creating " + tmp_ + ": " + std::strerror(e);
+    const std::string t = path + ".alluxio." + tag + ".tmp";
+    const int f = ::open(t.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0666);
+    std::lock_guard<std::mutex> g(mu);
+    if (f < 0) {
+      fail_locked(errno, "creating " + t);
       return false;
     }
+    fd = f;
+    tmp = t;
+    opened = true;
+    return true;
+  }
+
+  void cleanup() {   // failed / cancelled: drop the temp file, leave the target untouched
+    if (cleaned) return;
+    cleaned = true;
+    if (fd >= 0) ::close(fd);
+    fd = -1;
+    if (!tmp.empty()) ::unlink(tmp.c_str());
+  }
+
+  // One pool task: open (first time), write queued chunks in order, and on the end chmod + rename.
+  static void drain(std::shared_ptr<LocalFileJob> j) {
+    for (;;) {
+      std::string c;
+      bool do_open, do_end, stop;
+      {
+        std::lock_guard<std::mutex> g(j->mu);
+        stop = j->failed || j->cancelled;
+        do_open = !stop && !j->opened;
+        do_end = !stop && j->chunks.empty() && j->end && !j->finished;
+        if (!stop && !do_open && !j->chunks.empty()) {
+          c = std::move(j->chunks.front());
+          j->chunks.pop_front();
+        }
+        if (stop || (!do_open && !do_end && c.empty())) {
+          if (stop) j->cleanup();
+          j->running = false;
+          break;
+        }
+      }
+      if (do_open) {
+        j->open_file();
+        continue;
+      }
+      if (!c.empty()) {
+        size_t done = 0;
+        int e = 0;
+        while (done < c.size()) {
+          const ssize_t w = ::write(j->fd, c.data() + done, c.size() - done);
+          if (w < 0) {
+            if (errno == EINTR) continue;
+            e = errno;
+            break;
+          }
+          done += (size_t)w;
+        }
+        std::lock_guard<std::mutex> g(j->mu);
+        if (e) j->fail_locked(e, "writing " + j->path);
+        else j->written += c.size();
+        j->stats->ufs_write_bytes.fetch_add(done, std::memory_order_relaxed);
+      } else if (do_end) {
+        int e = 0;
+        if (::fchmod(j->fd, (mode_t)j->mode) != 0) e = errno;
+        if (::close(j->fd) != 0 && !e) e = errno;
+        j->fd = -1;
+        if (!e && ::rename(j->tmp.c_str(), j->path.c_str()) != 0) e = errno;
+        std::lock_guard<std::mutex> g(j->mu);
+        if (e) j->fail_locked(e, "completing " + j->path);
+        else j->finished = true;
+      }
+      j->poke();
+    }
+    j->poke();
+  }
+};
+
+// UFS_FILE WriteBlock into a local-directory UFS: chunks go to a temp file beside the target (the
+// local UFS's atomic create, underfs/local.py _AtomicWriter), written by FilePool tasks; the
+// half-close sets the mode and renames it over the target.  A failed or cancelled call removes the
+// temp file and leaves the target untouched.  At most kMaxQueued bytes wait for the disk: beyond
+// that the stream stops accepting and the client's request window is held back.
+class UfsFileWriteStream : public WriteStreamBase {
+ public:
+  static constexpr uint64_t kMaxQueued = 32ull << 20;
+
+  UfsFileWriteStream(const std::string& path, int mode, std::shared_ptr<DataServerStats> stats)
+      : j_(std::make_shared<LocalFileJob>()) {
+    j_->path = path;
+    j_->mode = mode;
+    j_->stats = std::move(stats);
+  }
+
+  // Queues the open (parents + temp file) on the file pool; errors surface on the stream.
+  bool open(int*, std::string*) {
+    kick();
     return true;
   }
 
   ~UfsFileWriteStream() override {
-    if (fd_ >= 0) ::close(fd_);
-    if (!committed_ && !tmp_.empty()) ::unlink(tmp_.c_str());
+    bool idle;
+    {
+      std::lock_guard<std::mutex> g(j_->mu);
+      j_->wake = nullptr;
+      if (!j_->finished) j_->cancelled = true;
+      idle = !j_->running;
+      if (idle && j_->cancelled) j_->running = true;
+    }
+    if (idle && j_->cancelled) {
+      auto j = j_;
+      FilePool::get().submit([j] { LocalFileJob::drain(j); });   // closes + unlinks the temp file
+    }
+  }
+
+  void set_waker(std::function<void()> w) override {
+    std::lock_guard<std::mutex> g(j_->mu);
+    j_->wake = std::move(w);
+  }
+
+  bool accepting() override {
+    std::lock_guard<std::mutex> g(j_->mu);
+    return j_->queued - j_->written < kMaxQueued || j_->failed;
   }
 
   void on_message(const char* p, size_t n) override {
@@ -1036,48 +1208,66 @@ class UfsFileWriteStream : public WriteStreamBase {
       fail(3, "malformed WriteRequest");
       return;
     }
-    size_t done = 0;
-    while (done < len) {
-      const ssize_t w = ::write(fd_, chunk + done, len - done);
-      if (w < 0) {
-        if (errno == EINTR) continue;
-        const int e = errno;
-        fail(grpc_status_of_errno(e), "writing " + path_ + ": " + std::strerror(e));
-        return;
+    if (len) {
+      {
+        std::lock_guard<std::mutex> g(j_->mu);
+        j_->chunks.emplace_back(reinterpret_cast<const char*>(chunk), len);
+        j_->queued += len;
       }
-      done += (size_t)w;
+      kick();
     }
     pos_ += len;
-    stats_->ufs_write_bytes.fetch_add(len, std::memory_order_relaxed);
-    if (has_cmd && cmd.flush) out_ += write_response_frame(pos_);
+    if (has_cmd && cmd.flush) flushes_.push_back(pos_);   // acked once written
+    emit();
   }
 
   bool on_end(uint32_t*, std::string*) override {
     ended_ = true;
     if (err_) return false;
-    const int fd = fd_;
-    fd_ = -1;
-    int e = 0;
-    if (::fchmod(fd, (mode_t)mode_) != 0) e = errno;
-    if (::close(fd) != 0 && !e) e = errno;
-    if (!e && ::rename(tmp_.c_str(), path_.c_str()) != 0) e = errno;
-    if (e) {
-      fail(grpc_status_of_errno(e), "completing " + path_ + ": " + std::strerror(e));
-      return false;
+    {
+      std::lock_guard<std::mutex> g(j_->mu);
+      j_->end = true;
     }
-    committed_ = true;
-    out_ += write_response_frame(pos_);
-    done_ = true;
+    kick();
     return false;
   }
 
+  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    emit();
+    return WriteStreamBase::produce(dst, max, eof, status, msg);
+  }
+
  private:
-  std::string path_, tmp_;
-  int mode_;
-  int fd_ = -1;
+  void kick() {
+    {
+      std::lock_guard<std::mutex> g(j_->mu);
+      if (j_->running) return;
+      j_->running = true;
+    }
+    auto j = j_;
+    FilePool::get().submit([j] { LocalFileJob::drain(j); });
+  }
+
+  // Flush acks for written data, the failure, or the final frame once the file is in place.
+  void emit() {
+    std::lock_guard<std::mutex> g(j_->mu);
+    if (j_->failed) {
+      if (!err_) fail(j_->err_status, j_->err);
+      return;
+    }
+    while (!flushes_.empty() && flushes_.front() <= j_->written) {
+      out_ += write_response_frame(flushes_.front());
+      flushes_.pop_front();
+    }
+    if (j_->finished && !done_) {
+      out_ += write_response_frame(pos_);
+      done_ = true;
+    }
+  }
+
+  std::shared_ptr<LocalFileJob> j_;
   uint64_t pos_ = 0;
-  bool committed_ = false;
-  std::shared_ptr<DataServerStats> stats_;
+  std::deque<uint64_t> flushes_;
 };
 
 
