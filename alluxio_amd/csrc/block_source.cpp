@@ -329,16 +329,50 @@ struct GrpcBlockSource::Conn {
   std::string grpc_msg;
   uint32_t close_code = 0;
   std::string inbuf;
+  // Raw HTTP/2 frame boundaries of the server->client byte stream, tracked alongside nghttp2 so
+  // the chunk bytes of our DATA frames can be received straight into the caller's buffer (one
+  // copy, the kernel's) instead of into inbuf and then memcpy'd.  nghttp2 still parses every byte
+  // (flow control, headers, trailers): it is handed the same bytes where they landed.
+  uint8_t fh[9];
+  size_t fh_n = 0;
+  uint64_t frame_left = 0;
+  bool in_payload = false, our_data = false;
+  uint64_t direct_bytes = 0;
 
   ~Conn() {
     if (ng) h2::lib().session_del(ng);
     if (fd >= 0) ::close(fd);
   }
 
+  void track(const uint8_t* p, size_t n) {
+    while (n) {
+      if (!in_payload) {
+        const size_t t = std::min(n, 9 - fh_n);
+        std::memcpy(fh + fh_n, p, t);
+        fh_n += t;
+        p += t;
+        n -= t;
+        if (fh_n < 9) break;
+        fh_n = 0;
+        frame_left = ((uint64_t)fh[0] << 16) | ((uint64_t)fh[1] << 8) | fh[2];
+        const int32_t id = (int32_t)((((uint32_t)fh[5] & 0x7f) << 24) | ((uint32_t)fh[6] << 16) |
+                                     ((uint32_t)fh[7] << 8) | fh[8]);
+        our_data = fh[3] == h2::kTypeData && id == sid && !(fh[4] & 0x08);   // not PADDED
+        in_payload = frame_left > 0;
+      } else {
+        const size_t t = (size_t)std::min<uint64_t>(n, frame_left);
+        frame_left -= t;
+        p += t;
+        n -= t;
+        if (!frame_left) in_payload = false;
+      }
+    }
+  }
+
   void deliver(const uint8_t* p, size_t n) {
     const size_t take = (size_t)std::min<uint64_t>(n, need);
     if (take) {
-      std::memcpy(dst, p, take);
+      if (p != dst) std::memcpy(dst, p, take);   // == dst: received there directly
       dst += take;
       need -= take;
     }
@@ -562,20 +596,36 @@ struct GrpcBlockSource::Conn {
     }
   }
 
-  // One socket read + parse; false on timeout.
+  // One socket read + parse; false on timeout.  Chunk bytes the caller is waiting for are received
+  // into its buffer directly; everything else (frame headers, message headers, control frames,
+  // read-ahead) goes through inbuf, read no further than the next point where that can start.
   bool pump(int timeout_ms) {
     pollfd pf{fd, POLLIN, 0};
     const int r = ::poll(&pf, 1, timeout_ms);
     if (r == 0) return false;
     if (r < 0 && errno != EINTR) throw std::runtime_error("gRPC client: poll failed");
     if (inbuf.size() < (1u << 20)) inbuf.resize(1u << 20);
-    const ssize_t got = ::recv(fd, &inbuf[0], inbuf.size(), 0);
+    uint8_t* target = reinterpret_cast<uint8_t*>(&inbuf[0]);
+    size_t want = inbuf.size();
+    if (!in_payload) {
+      want = 9 - fh_n;                                   // the next frame header
+    } else if (our_data && state == 2 && need > 0) {
+      target = dst;                                      // chunk bytes: straight into place
+      want = (size_t)std::min<uint64_t>(std::min<uint64_t>(frame_left, data_left), need);
+    } else if (our_data && need > 0) {
+      want = (size_t)std::min<uint64_t>(frame_left, 16);  // gRPC prefix + ReadResponse header
+    } else {
+      want = (size_t)std::min<uint64_t>(frame_left, inbuf.size());
+    }
+    const ssize_t got = ::recv(fd, target, want, 0);
     if (got == 0) throw std::runtime_error("gRPC client: connection closed by the worker");
     if (got < 0) {
       if (errno == EINTR || errno == EAGAIN) return true;
       throw std::runtime_error("gRPC client: connection lost");
     }
-    const ssize_t rc = h2::lib().mem_recv(ng, reinterpret_cast<const uint8_t*>(inbuf.data()), (size_t)got);
+    if (target != reinterpret_cast<uint8_t*>(&inbuf[0])) direct_bytes += (uint64_t)got;
+    track(target, (size_t)got);
+    const ssize_t rc = h2::lib().mem_recv(ng, target, (size_t)got);
     if (rc < 0) throw std::runtime_error("gRPC client: malformed ReadBlock response stream");
     return true;
   }

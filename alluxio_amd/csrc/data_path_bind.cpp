@@ -370,7 +370,8 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("cold_aborted", [](const DataServerStats& s) { return s.cold_aborted.load(); })
       .def_property_readonly("cold_bytes", [](const DataServerStats& s) { return s.cold_bytes.load(); })
       .def_property_readonly("cold_active", [](const DataServerStats& s) { return s.cold_active.load(); })
-      .def_property_readonly("prefetched", [](const DataServerStats& s) { return s.prefetched.load(); });
+      .def_property_readonly("prefetched", [](const DataServerStats& s) { return s.prefetched.load(); })
+      .def_property_readonly("zero_copy_frames", [](const DataServerStats& s) { return s.zero_copy_frames.load(); });
   auto mounts = py::class_<UfsMounts, std::shared_ptr<UfsMounts>>(m, "UfsMounts")
       .def(py::init<>())
       .def("set", &UfsMounts::set, py::arg("mount_id"), py::arg("root"))

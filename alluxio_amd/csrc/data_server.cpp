@@ -229,6 +229,51 @@ class BlockReadStream : public NativeStream {
     return (ssize_t)w;
   }
 
+  // HBM blocks: the chunk's gRPC/protobuf prefix and the bytes in the staging slot go to the
+  // socket as they are (no copy into the HTTP/2 frame buffer).  A DATA frame never crosses a chunk
+  // boundary: moving to the next chunk re-stages the slot the previous chunk sat in.
+  ssize_t produce_spans(size_t max, ByteSpan* spans, int max_spans, int* nspans, bool* eof, int* status,
+                        std::string* msg) override {
+    if (!device_ || max_spans < 2) return -2;
+    size_t w = 0;
+    int ns = 0;
+    try {
+      while (w < max && ns < max_spans) {
+        if (hdr_off_ < hdr_.size()) {
+          const size_t n = std::min(max - w, hdr_.size() - hdr_off_);
+          spans[ns++] = ByteSpan{reinterpret_cast<const uint8_t*>(hdr_.data()) + hdr_off_, n};
+          hdr_off_ += n;
+          w += n;
+          continue;
+        }
+        if (left_ > 0) {
+          const size_t n = (size_t)std::min<uint64_t>(max - w, left_);
+          spans[ns++] = ByteSpan{slot_[cur_].buf + stage_off_, n};
+          stage_off_ += n;
+          left_ -= n;
+          w += n;
+          stats_->bytes.fetch_add(n, std::memory_order_relaxed);
+          if (unix_) stats_->domain_bytes.fetch_add(n, std::memory_order_relaxed);
+          continue;
+        }
+        if (w > 0) break;                      // this frame ends with the chunk
+        if (pos_ >= end_) {
+          *eof = true;
+          break;
+        }
+        if (pos_ - acked_ >= window_) break;   // wait for offset_received
+        next_chunk();
+      }
+    } catch (const std::exception& e) {
+      *status = 13;
+      *msg = std::string("reading block ") + std::to_string(block_) + ": " + e.what();
+      return -1;
+    }
+    *nspans = ns;
+    if (w > 0) stats_->zero_copy_frames.fetch_add(1, std::memory_order_relaxed);
+    return (ssize_t)w;
+  }
+
  private:
   // Double-buffered D2H staging: chunk k is copied out of the slot its DMA landed in while the DMA
   // of chunk k+1 runs into the other slot (reference AbstractReadHandler.java:336-439 DataReader

@@ -9,14 +9,17 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
+#include <pthread.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <unordered_map>
@@ -157,6 +160,9 @@ struct FrameRpcServer::H2 {
     std::string fin_msg;
     std::shared_ptr<Bridge> bridge;
     std::unique_ptr<NativeStream> native;
+    bool spans_ok = true;      // native stream offers produce_spans (until it says -2)
+    ByteSpan spans[4];
+    int nspans = 0;
   };
   struct Session {
     FrameRpcServer* srv = nullptr;
@@ -176,6 +182,7 @@ struct FrameRpcServer::H2 {
   static int on_close(void*, int32_t sid, uint32_t, void* ud);
   static ssize_t read_body(void* session, int32_t sid, uint8_t* buf, size_t length, uint32_t* flags, h2::DataSource*,
                            void* ud);
+  static int send_data(void* session, void* frame, const uint8_t* framehd, size_t length, h2::DataSource*, void* ud);
   static void take_messages(Session& S, int32_t sid, Stream& st, bool end_stream);
   static void post_python(Session& S, int32_t sid, Stream& st, uint32_t method, std::string payload);
   static void dispatch(Session& S, int32_t sid, Stream& st, std::string msg);
@@ -225,6 +232,7 @@ void* FrameRpcServer::H2::callbacks() {
     g.set_on_stream_close(c, &H2::on_close);
     g.set_on_header(c, &H2::on_header);
     g.set_read_length(c, &h2::read_length);
+    g.set_send_data(c, &H2::send_data);
     return c;
   }();
   return cbs;
@@ -561,7 +569,17 @@ ssize_t FrameRpcServer::H2::read_body(void* session, int32_t sid, uint8_t* buf, 
     bool eof = false;
     int status = 0;
     std::string m;
-    const ssize_t got = st.native->produce(buf, length, &eof, &status, &m);
+    ssize_t got = -2;
+    if (st.spans_ok) {
+      int ns = 0;
+      got = st.native->produce_spans(length, st.spans, 4, &ns, &eof, &status, &m);
+      if (got == -2) st.spans_ok = false;
+      else if (got > 0) {
+        st.nspans = ns;
+        *flags |= h2::kDataNoCopy;     // send_data() writes the spans straight to the socket
+      }
+    }
+    if (got == -2) got = st.native->produce(buf, length, &eof, &status, &m);
     uint32_t post_method = 0;
     std::string post_payload;
     if (got >= 0 && !eof && st.native->take_post(&post_method, &post_payload))
@@ -599,6 +617,67 @@ ssize_t FrameRpcServer::H2::read_body(void* session, int32_t sid, uint8_t* buf, 
     st.native.reset();    // release the block lock as soon as the last byte is out
   }
   return (ssize_t)n;
+}
+
+// DATA frame of a produce_spans() stream: the 9-byte frame header and the stream's spans go to the
+// socket in one sendmsg, no copy; what the socket does not take now is kept in Conn::out.
+int FrameRpcServer::H2::send_data(void*, void* frame, const uint8_t* framehd, size_t length, h2::DataSource*,
+                                  void* ud) {
+  Session& S = *static_cast<Session*>(ud);
+  Conn& c = *S.conn;
+  const h2::DataFrame* f = static_cast<const h2::DataFrame*>(frame);
+  auto it = S.streams.find(f->hd.stream_id);
+  if (it == S.streams.end()) return h2::kErrCallbackFailure;
+  Stream& st = it->second;
+  static const uint8_t zeros[256] = {0};
+  iovec iov[8];
+  int n = 0;
+  iov[n++] = iovec{const_cast<uint8_t*>(framehd), 9};
+  uint8_t padfield = 0;
+  const size_t padlen = f->padlen;
+  if (padlen > 0) {                  // never requested here, but keep the frame well-formed
+    padfield = (uint8_t)(padlen - 1);
+    iov[n++] = iovec{&padfield, 1};
+  }
+  size_t data = 0;
+  for (int i = 0; i < st.nspans && n < 7; ++i) {
+    iov[n++] = iovec{const_cast<uint8_t*>(st.spans[i].p), st.spans[i].n};
+    data += st.spans[i].n;
+  }
+  if (padlen > 1) iov[n++] = iovec{const_cast<uint8_t*>(zeros), std::min<size_t>(padlen - 1, sizeof(zeros))};
+  st.nspans = 0;
+  if (data != length) return h2::kErrCallbackFailure;
+  size_t total = 0;
+  for (int i = 0; i < n; ++i) total += iov[i].iov_len;
+  size_t sent = 0;
+  if (c.out_off == c.out.size()) {   // nothing queued ahead of this frame: straight to the socket
+    msghdr mh{};
+    mh.msg_iov = iov;
+    mh.msg_iovlen = (size_t)n;
+    for (;;) {
+      const ssize_t w = ::sendmsg(c.fd, &mh, MSG_NOSIGNAL | MSG_DONTWAIT);
+      if (w < 0 && errno == EINTR) continue;
+      if (w < 0 && errno != EAGAIN && errno != EWOULDBLOCK) return h2::kErrCallbackFailure;
+      sent = w > 0 ? (size_t)w : 0;
+      break;
+    }
+    if (sent == total) return 0;
+    if (c.out_off == c.out.size()) {
+      c.out.clear();
+      c.out_off = 0;
+    }
+  }
+  size_t skip = sent;                // the rest waits in Conn::out (EPOLLOUT)
+  for (int i = 0; i < n; ++i) {
+    const size_t len = iov[i].iov_len;
+    if (skip >= len) {
+      skip -= len;
+      continue;
+    }
+    c.out.append(static_cast<const char*>(iov[i].iov_base) + skip, len - skip);
+    skip = 0;
+  }
+  return 0;
 }
 
 void FrameRpcServer::H2::apply_consumed(Session& S) {
@@ -944,7 +1023,13 @@ void FrameRpcServer::start() {
     wake_fds_.push_back(wfd);
     wake_qs_.emplace_back(new WakeQueue());
   }
-  for (int i = 0; i < nthreads_; ++i) threads_.emplace_back([this, i] { io_loop(i); });
+  for (int i = 0; i < nthreads_; ++i)
+    threads_.emplace_back([this, i] {
+      char name[16];
+      std::snprintf(name, sizeof(name), "frpc-io-%d", i);   // per-thread CPU in /proc (benches)
+      pthread_setname_np(pthread_self(), name);
+      io_loop(i);
+    });
   acceptor_ = std::thread([this] { accept_loop(); });
 }
 

@@ -51,6 +51,12 @@ struct FrameRequest {
   std::string payload;
 };
 
+// A piece of response body handed to the socket without a copy (NativeStream::produce_spans).
+struct ByteSpan {
+  const uint8_t* p;
+  size_t n;
+};
+
 // A gRPC call whose responses are produced in C++ on the I/O threads (the worker's ReadBlock data
 // path, csrc/data_server.cpp), instead of by a Python servicer.
 class NativeStream {
@@ -62,6 +68,14 @@ class NativeStream {
   // *eof unset = nothing to send until the next request message arrives (flow-control window);
   // *eof = the call is complete.  -1 = the call failed with *status / *msg (sent as trailers).
   virtual ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) = 0;
+  // Zero-copy produce(): up to `max` bytes as at most `max_spans` spans of memory the stream owns,
+  // which must stay valid and unchanged until its next produce / produce_spans call (the server
+  // writes them to the socket -- the DATA frame's header, then the spans -- before that).
+  // -2 = not supported for this call (the server uses produce()).
+  virtual ssize_t produce_spans(size_t max, ByteSpan* spans, int max_spans, int* nspans, bool* eof, int* status,
+                                std::string* msg) {
+    return -2;
+  }
   // The client half-closed the request stream.  true = finish the call in Python: the server
   // queues {*method, *payload} on that method's lane as an internal unary request (caller string
   // prefixed "\x02") and hands its reply to on_reply(); false = produce() decides.

@@ -32,6 +32,10 @@ struct FrameHd {   // the first member of every nghttp2_frame variant
   uint8_t flags;
   uint8_t reserved;
 };
+struct DataFrame {   // nghttp2_data
+  FrameHd hd;
+  size_t padlen;     // includes the 1-byte Pad Length field when > 0
+};
 union DataSource {
   int fd;
   void* ptr;
@@ -52,11 +56,13 @@ typedef int (*DataChunkCb)(void* session, uint8_t flags, int32_t stream_id, cons
 typedef int (*CloseCb)(void* session, int32_t stream_id, uint32_t error_code, void* user_data);
 typedef int (*HeaderCb)(void* session, const void* frame, const uint8_t* name, size_t namelen, const uint8_t* value,
                         size_t valuelen, uint8_t flags, void* user_data);
+typedef int (*SendDataCb)(void* session, void* frame, const uint8_t* framehd, size_t length, DataSource* source,
+                          void* user_data);
 typedef ssize_t (*ReadLengthCb)(void* session, uint8_t frame_type, int32_t stream_id, int32_t session_remote_window,
                                 int32_t stream_remote_window, uint32_t remote_max_frame_size, void* user_data);
 
 constexpr uint8_t kFlagEndStream = 0x01;
-constexpr uint32_t kDataEof = 0x01, kDataNoEndStream = 0x02;
+constexpr uint32_t kDataEof = 0x01, kDataNoEndStream = 0x02, kDataNoCopy = 0x04;
 constexpr uint8_t kTypeData = 0, kTypeHeaders = 1, kTypeRstStream = 3, kTypeGoaway = 7;
 constexpr int kErrDeferred = -508;
 constexpr int kErrCallbackFailure = -902;
@@ -77,6 +83,7 @@ struct Lib {
   void (*set_on_stream_close)(void*, CloseCb) = nullptr;
   void (*set_on_header)(void*, HeaderCb) = nullptr;
   void (*set_read_length)(void*, ReadLengthCb) = nullptr;
+  void (*set_send_data)(void*, SendDataCb) = nullptr;
   int (*option_new)(void**) = nullptr;
   void (*option_del)(void*) = nullptr;
   void (*option_no_auto_window_update)(void*, int) = nullptr;
@@ -117,6 +124,7 @@ inline const Lib& lib() {
     sym(g.set_on_stream_close, "nghttp2_session_callbacks_set_on_stream_close_callback");
     sym(g.set_on_header, "nghttp2_session_callbacks_set_on_header_callback");
     sym(g.set_read_length, "nghttp2_session_callbacks_set_data_source_read_length_callback");
+    sym(g.set_send_data, "nghttp2_session_callbacks_set_send_data_callback");
     sym(g.option_new, "nghttp2_option_new");
     sym(g.option_del, "nghttp2_option_del");
     sym(g.option_no_auto_window_update, "nghttp2_option_set_no_auto_window_update");

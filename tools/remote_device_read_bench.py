@@ -51,12 +51,34 @@ if not {cold}:
     once()
 else:
     fs.read_file("/rd/warm")     # the first cold read of the mount runs in Python and registers it
+import os
+c0 = os.times()
 t0 = time.perf_counter()
 total = sum(once() for _ in range({reps}))
 el = time.perf_counter() - t0
-print("RESULT " + json.dumps({{"bytes": total, "seconds": el}}), flush=True)
+c1 = os.times()
+cpu = (c1.user - c0.user) + (c1.system - c0.system)
+print("RESULT " + json.dumps({{"bytes": total, "seconds": el, "client_cpu_cores": cpu / el,
+                              "client_sys_cores": (c1.system - c0.system) / el}}), flush=True)
 fs.close()
 """
+
+
+def _io_thread_cpu() -> dict:
+    """CPU seconds of this process's native RPC I/O threads ("frpc-io-N"), by thread id."""
+    out = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    for t in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{t}/stat") as f:
+                s = f.read()
+        except OSError:
+            continue
+        if "(frpc-io-" not in s:
+            continue
+        fl = s.rsplit(")", 1)[1].split()
+        out[t] = (int(fl[11]) + int(fl[12])) / tck
+    return out
 
 
 def main(argv=None) -> int:
@@ -70,6 +92,8 @@ def main(argv=None) -> int:
                     help="the file is written THROUGH (in the UFS only): one timed read-through, no warm-up")
     ap.add_argument("--native-only", action="store_true", help="skip the grpcio comparison row")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
+    ap.add_argument("--worker-prop", action="append", default=[], help="extra worker property k=v")
+    ap.add_argument("--tier", default="hbm:0", help="worker tier path (hbm:0, or dram for a host-only box)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import numpy as np
@@ -77,10 +101,11 @@ def main(argv=None) -> int:
     from alluxio_amd.minicluster import LocalAlluxioCluster
     from alluxio_amd.utils.format import parse_space_size
     size = parse_space_size(a.file_size)
-    conf = {"alluxio.worker.tieredstore.level0.dirs.path": "hbm:0",
+    conf = {"alluxio.worker.tieredstore.level0.dirs.path": a.tier,
             "alluxio.worker.tieredstore.level0.dirs.quota": str(size + (512 << 20)),
             "alluxio.worker.hbm.page.size": "2MB", "alluxio.user.block.size.bytes.default": "64MB",
             "alluxio.security.authorization.permission.enabled": "false"}
+    conf.update(dict(kv.split("=", 1) for kv in a.worker_prop))
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=tempfile.mkdtemp(prefix="rdbench_")) as c:
         fs = c.client()
         fs.write_file("/rd/data", np.random.default_rng(0).integers(0, 256, size, dtype=np.uint8),
@@ -91,12 +116,14 @@ def main(argv=None) -> int:
                 fs.free("/rd", recursive=True)
                 c.heartbeat_workers()
             ds = c.workers[0].data_server
-            st0 = (ds.stats.cold_streams, ds.stats.declined, ds.stats.cold_cached) if ds is not None else None
+            st0 = (ds.stats.cold_streams, ds.stats.declined, ds.stats.cold_cached, ds.stats.zero_copy_frames,
+                   ds.stats.prefetched) if ds is not None else None
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "false",
                      "alluxio.user.native.reader.enabled": str(native).lower(),
                      "alluxio.user.file.passive.cache.enabled": "false"}
             props.update(dict(kv.split("=", 1) for kv in a.client_prop))
+            io0 = _io_thread_cpu()
             p = subprocess.run([sys.executable, "-c", CLIENT.format(root=ROOT, props=props, addr=c.master.address,
                                                                    read=parse_space_size(a.read_size), reps=1 if a.cold else a.reps, dest=a.dest,
                                                                    cold=a.cold)],
@@ -106,16 +133,23 @@ def main(argv=None) -> int:
                 print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
                 return 1
             r = json.loads(line[7:])
+            io1 = _io_thread_cpu()
             row = {"bench": "GPU consumer of a remote worker's blocks (gRPC ReadBlock into a device tensor)"
                    if a.dest == "cuda" else "host consumer of a remote worker's blocks (gRPC ReadBlock into a numpy buffer)",
                    "client": "native GrpcBlockSource + pinned H2D" if native else "grpcio stream + host copy",
                    "file_size": a.file_size, "read_size": a.read_size, "bytes": r["bytes"],
                    "seconds": round(r["seconds"], 3), "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3),
-                   "client_props": a.client_prop, "cold": a.cold}
+                   "client_props": a.client_prop, "worker_props": a.worker_prop, "cold": a.cold, "tier": a.tier,
+                   "client_cpu_cores": round(r["client_cpu_cores"], 2), "client_sys_cores": round(r["client_sys_cores"], 2),
+                   # the worker's I/O threads (busiest one): 1.0 = that thread is the bound
+                   "worker_io_busiest_cores": round(max((io1.get(k, 0) - io0.get(k, 0) for k in io1), default=0)
+                                                    / max(r["seconds"], 1e-9), 2)}
             if st0 is not None:
                 row["worker_native_cold_streams"] = ds.stats.cold_streams - st0[0]
                 row["worker_declined_to_python"] = ds.stats.declined - st0[1]
                 row["worker_cold_cached_blocks"] = ds.stats.cold_cached - st0[2]
+                row["worker_zero_copy_frames"] = ds.stats.zero_copy_frames - st0[3]
+                row["worker_prefetched_chunks"] = ds.stats.prefetched - st0[4]
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
