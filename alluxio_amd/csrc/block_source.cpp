@@ -600,10 +600,6 @@ struct GrpcBlockSource::Conn {
   // into its buffer directly; everything else (frame headers, message headers, control frames,
   // read-ahead) goes through inbuf, read no further than the next point where that can start.
   bool pump(int timeout_ms) {
-    pollfd pf{fd, POLLIN, 0};
-    const int r = ::poll(&pf, 1, timeout_ms);
-    if (r == 0) return false;
-    if (r < 0 && errno != EINTR) throw std::runtime_error("gRPC client: poll failed");
     if (inbuf.size() < (1u << 20)) inbuf.resize(1u << 20);
     uint8_t* target = reinterpret_cast<uint8_t*>(&inbuf[0]);
     size_t want = inbuf.size();
@@ -617,7 +613,15 @@ struct GrpcBlockSource::Conn {
     } else {
       want = (size_t)std::min<uint64_t>(frame_left, inbuf.size());
     }
-    const ssize_t got = ::recv(fd, target, want, 0);
+    // bytes usually wait in the socket already: poll only when a non-blocking receive finds none
+    ssize_t got = ::recv(fd, target, want, MSG_DONTWAIT);
+    if (got < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      pollfd pf{fd, POLLIN, 0};
+      const int r = ::poll(&pf, 1, timeout_ms);
+      if (r == 0) return false;
+      if (r < 0 && errno != EINTR) throw std::runtime_error("gRPC client: poll failed");
+      got = ::recv(fd, target, want, MSG_DONTWAIT);
+    }
     if (got == 0) throw std::runtime_error("gRPC client: connection closed by the worker");
     if (got < 0) {
       if (errno == EINTR || errno == EAGAIN) return true;

@@ -95,7 +95,35 @@ BlockStore::BlockStore(const std::vector<DirSpec>& dirs, int annotator, int allo
       HIP_OK(hipMalloc((void**)&d->mag_bits, d->free_bits.size() * 8));
       HIP_OK(hipMemset(d->mag_bits, 0, d->free_bits.size() * 8));
     }
+    const char* mk = std::getenv("ALLUXIO_MOVE_COPY_KERNEL");
+    const bool mapped_moves = !(mk && mk[0] == '0');
+    for (auto& d : dirs_) {
+      if (!mapped_moves || d->spec.kind != DirKind::kHost || !d->spec.base || !d->spec.capacity) continue;
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, reinterpret_cast<void*>(d->spec.base), 0) == hipSuccess && dp)
+        d->dev_base = reinterpret_cast<uint64_t>(dp);
+      else
+        (void)hipGetLastError();      // not registered: tier moves use runtime copies
+    }
   }
+}
+
+hipStream_t BlockStore::move_stream() {
+  // one non-blocking stream per (thread, store): concurrent evictions move in parallel and never
+  // queue behind the page-claim / eviction-select kernels on internal_stream_
+  struct TL {
+    const BlockStore* owner = nullptr;
+    hipStream_t st = nullptr;
+  };
+  thread_local TL tl;
+  if (tl.owner != this || !tl.st) {
+    set_device();
+    hipStream_t st = nullptr;
+    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    tl.owner = this;
+    tl.st = st;
+  }
+  return tl.st;
 }
 
 BlockStore::~BlockStore() {
@@ -688,7 +716,7 @@ int BlockStore::move_block(int64_t session, int64_t block_id, int dst_tier, cons
   b->writer = true;  // hold the block while copying
   BlockMeta src_snap = *b;
   lk.unlock();
-  hipStream_t st = internal_stream_;
+  hipStream_t st = has_device_ ? move_stream() : internal_stream_;
   std::vector<CopySeg> dev_segs;
   try {
     copy_block_storage(src_snap, nb, dev_segs, st);
@@ -738,8 +766,9 @@ void BlockStore::copy_block_storage(const BlockMeta& src_snap, const BlockMeta& 
       while (j < nb.pages.size() && nb.pages[j] == nb.pages[j - 1] + 1) ++j;
       const uint64_t run = std::min<uint64_t>((j - i) * dd.spec.page_size, len - off);
       const uint64_t dst_addr = dd.spec.base + (uint64_t)p0 * dd.spec.page_size;
+      const uint64_t dst_mapped = (!dst_dev && dd.dev_base) ? dd.dev_base + (uint64_t)p0 * dd.spec.page_size : 0;
       plan_block_range(src_snap, off, run, dst_addr, dst_dev ? (int)MemKind::kDevice : (int)MemKind::kHost, false,
-                       dev_segs, st);
+                       dev_segs, st, dst_mapped, true);
       off += run;
       i = j;
     }
@@ -967,7 +996,7 @@ void BlockStore::set_pinned_files(const std::vector<int64_t>& file_ids) {
 // data plane
 void BlockStore::plan_block_range(const BlockMeta& b, uint64_t offset, uint64_t len, uint64_t ext,
                                   int ext_kind, bool to_block, std::vector<CopySeg>& dev_segs,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, uint64_t ext_mapped, bool mapped_kernel) {
   const StorageDir& d = *dirs_[b.dir];
   const bool ext_dev = ext_kind == (int)MemKind::kDevice;
   if (d.spec.kind == DirKind::kFile) {
@@ -1013,8 +1042,14 @@ void BlockStore::plan_block_range(const BlockMeta& b, uint64_t offset, uint64_t 
     const uint64_t ext_addr = ext + done;
     const uint64_t src = to_block ? ext_addr : arena_addr;
     const uint64_t dst = to_block ? arena_addr : ext_addr;
+    // device-visible addresses of both ends (0 = not reachable by a kernel)
+    const uint64_t arena_k = arena_dev ? arena_addr : (d.dev_base ? d.dev_base + (arena_addr - d.spec.base) : 0);
+    const uint64_t ext_k = ext_dev ? ext_addr : (ext_mapped ? ext_mapped + done : 0);
     if (arena_dev && ext_dev) {
       dev_segs.push_back(CopySeg{src, dst, n, 0});
+    } else if (mapped_kernel && arena_dev != ext_dev && arena_k && ext_k) {
+      // HBM <-> GPU-mapped host arena (tier moves): one batched copy kernel for the whole move
+      dev_segs.push_back(CopySeg{to_block ? ext_k : arena_k, to_block ? arena_k : ext_k, n, 0});
     } else if (!arena_dev && !ext_dev) {
       std::memcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n);
     } else {

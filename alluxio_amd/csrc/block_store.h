@@ -87,6 +87,9 @@ struct StorageDir {
   int64_t reserved_pages = 0;       // kept free for tier management (align/promote swaps)
   uint64_t file_used = 0;  // file dirs: bytes reserved
   uint64_t committed_bytes = 0;
+  // host arena registered with the GPU (hipHostRegister mapped): its device-visible address, so
+  // tier moves to / from HBM run as one batched copy kernel instead of per-run runtime copies
+  uint64_t dev_base = 0;
   bool healthy = true;
   uint64_t available() const;         // for user allocations (excludes the reserved space)
   uint64_t mgmt_available() const;    // for tier-management moves (may use the reserved space)
@@ -331,9 +334,12 @@ class BlockStore {
   bool evictable(const BlockMeta& b) const;
   void emit(int kind, const BlockMeta& b);
   void copy_segments(std::vector<CopySeg>& dev_segs, hipStream_t stream);
+  // `ext_mapped`: device-visible address of a host `ext` (0 = none); `mapped_kernel`: copies between
+  // HBM and GPU-mapped host memory go into dev_segs (batched copy kernel) instead of hipMemcpyAsync.
   void plan_block_range(const BlockMeta& b, uint64_t offset, uint64_t len, uint64_t ext,
                         int ext_kind, bool to_block, std::vector<CopySeg>& dev_segs,
-                        hipStream_t stream);
+                        hipStream_t stream, uint64_t ext_mapped = 0, bool mapped_kernel = false);
+  hipStream_t move_stream();           // this thread's stream for tier moves (not internal_stream_)
   void file_path(const StorageDir& d, int64_t id, std::string& out) const;
   void set_device() const;
   hipStream_t stream_or_default(uint64_t s) const;

@@ -11,6 +11,8 @@
 #include <condition_variable>
 #include <deque>
 #include <map>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -156,6 +158,57 @@ bool parse_read_request(const char* data, size_t n, ReadRequestMsg* r) {
   return true;
 }
 
+// Optional per-chunk timeline of HBM ReadBlock streams (ALLUXIO_READ_TRACE=<file>, read once):
+// when each chunk's D2H was issued, when it ran on the GPU (timing events against a base event
+// recorded with the host clock), how long the I/O thread waited for it, and when its bytes were
+// handed to the socket.  Evidence that chunk k+1's DMA runs while chunk k is being sent.
+struct ReadTraceRec {
+  uint64_t pos, len;
+  int64_t issue_ns = 0, gpu_start_ns = 0, gpu_end_ns = 0, ready_ns = 0, wait_ns = 0, send_first_ns = 0,
+          send_last_ns = 0;
+};
+
+class ReadTraceSink {
+ public:
+  static ReadTraceSink& get() {
+    static ReadTraceSink* s = new ReadTraceSink();
+    return *s;
+  }
+  bool on() const { return !path_.empty(); }
+  void write(int64_t block, const std::vector<ReadTraceRec>& recs) {
+    if (recs.empty()) return;
+    std::lock_guard<std::mutex> g(mu_);
+    if (written_ > 200000) return;
+    FILE* f = std::fopen(path_.c_str(), "a");
+    if (!f) return;
+    for (const auto& r : recs) {
+      std::fprintf(f,
+                   "{\"block\": %lld, \"pos\": %llu, \"len\": %llu, \"issue_ns\": %lld, \"gpu_start_ns\": %lld, "
+                   "\"gpu_end_ns\": %lld, \"ready_ns\": %lld, \"wait_ns\": %lld, \"send_first_ns\": %lld, "
+                   "\"send_last_ns\": %lld}\n",
+                   (long long)block, (unsigned long long)r.pos, (unsigned long long)r.len, (long long)r.issue_ns,
+                   (long long)r.gpu_start_ns, (long long)r.gpu_end_ns, (long long)r.ready_ns, (long long)r.wait_ns,
+                   (long long)r.send_first_ns, (long long)r.send_last_ns);
+      ++written_;
+    }
+    std::fclose(f);
+  }
+
+ private:
+  ReadTraceSink() {
+    const char* p = std::getenv("ALLUXIO_READ_TRACE");
+    if (p) path_ = p;
+  }
+  std::string path_;
+  std::mutex mu_;
+  uint64_t written_ = 0;
+};
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 class BlockReadStream : public NativeStream {
  public:
   BlockReadStream(BlockStore* store, int64_t session, int64_t lock_id, int64_t block_id, uint64_t pos, uint64_t end,
@@ -169,8 +222,13 @@ class BlockReadStream : public NativeStream {
       if (!slot_[k].buf) continue;
       if (slot_[k].inflight) (void)hipEventSynchronize(slot_[k].ev);   // no DMA into a pooled buffer
       if (slot_[k].ev) (void)hipEventDestroy(slot_[k].ev);
+      if (slot_[k].t0) (void)hipEventDestroy(slot_[k].t0);
       pool_->put(slot_[k].buf);
     }
+    if (!trace_.empty()) {
+      ReadTraceSink::get().write(block_, trace_);
+    }
+    if (base_ev_) (void)hipEventDestroy(base_ev_);
     try {
       store_->unlock(lock_);
       store_->cleanup_session(session_);
@@ -249,6 +307,11 @@ class BlockReadStream : public NativeStream {
         if (left_ > 0) {
           const size_t n = (size_t)std::min<uint64_t>(max - w, left_);
           spans[ns++] = ByteSpan{slot_[cur_].buf + stage_off_, n};
+          if (tracing_ && cur_rec_ >= 0) {
+            const int64_t t = now_ns();
+            if (!trace_[cur_rec_].send_first_ns) trace_[cur_rec_].send_first_ns = t;
+            trace_[cur_rec_].send_last_ns = t;
+          }
           stage_off_ += n;
           left_ -= n;
           w += n;
@@ -281,18 +344,36 @@ class BlockReadStream : public NativeStream {
   struct Slot {
     uint8_t* buf = nullptr;
     hipEvent_t ev = nullptr;
+    hipEvent_t t0 = nullptr;          // tracing: recorded before the copy (timing events)
     uint64_t pos = 0, len = 0;
     bool inflight = false, valid = false;
+    int rec = -1;                     // tracing: index into trace_
   };
 
   void stage(int k, uint64_t pos, uint64_t n) {
     Slot& s = slot_[k];
     if (!s.buf) {
       s.buf = pool_->get();
-      if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) s.ev = nullptr;
+      if (hipEventCreateWithFlags(&s.ev, tracing_ ? hipEventDefault : hipEventDisableTiming) != hipSuccess)
+        s.ev = nullptr;
+      if (tracing_ && hipEventCreate(&s.t0) != hipSuccess) s.t0 = nullptr;
     }
     std::vector<ReadReq> rq{ReadReq{block_, pos, n, reinterpret_cast<uint64_t>(s.buf), (int)MemKind::kHost}};
     hipStream_t st = thread_stream(store_);
+    if (tracing_) {
+      if (!base_ev_ && hipEventCreate(&base_ev_) == hipSuccess) {
+        (void)hipEventRecord(base_ev_, st);
+        (void)hipEventSynchronize(base_ev_);
+        base_ns_ = now_ns();
+      }
+      ReadTraceRec r;
+      r.pos = pos;
+      r.len = n;
+      r.issue_ns = now_ns();
+      trace_.push_back(r);
+      s.rec = (int)trace_.size() - 1;
+      if (s.t0) (void)hipEventRecord(s.t0, st);
+    }
     store_->read_batch(rq, reinterpret_cast<uint64_t>(st), s.ev == nullptr);
     s.inflight = s.ev != nullptr && hipEventRecord(s.ev, st) == hipSuccess;
     if (s.ev && !s.inflight) (void)hipStreamSynchronize(st);
@@ -311,10 +392,22 @@ class BlockReadStream : public NativeStream {
     if (device_) {
       const int k = cur_ ^ 1;                      // the slot chunk k was (pre)staged into
       if (!(slot_[k].valid && slot_[k].pos == pos_ && slot_[k].len == n)) stage(k, pos_, n);
+      const int64_t w0 = tracing_ ? now_ns() : 0;
       if (slot_[k].inflight) {
         // normally long done: it ran during the last send
         if (hipEventSynchronize(slot_[k].ev) != hipSuccess) throw std::runtime_error("D2H staging copy failed");
         slot_[k].inflight = false;
+      }
+      if (tracing_ && slot_[k].rec >= 0) {
+        ReadTraceRec& r = trace_[slot_[k].rec];
+        r.ready_ns = now_ns();
+        r.wait_ns = r.ready_ns - w0;
+        float ms = 0.f;
+        if (base_ev_ && slot_[k].t0 && hipEventElapsedTime(&ms, base_ev_, slot_[k].t0) == hipSuccess)
+          r.gpu_start_ns = base_ns_ + (int64_t)(ms * 1e6);
+        if (base_ev_ && hipEventElapsedTime(&ms, base_ev_, slot_[k].ev) == hipSuccess)
+          r.gpu_end_ns = base_ns_ + (int64_t)(ms * 1e6);
+        cur_rec_ = slot_[k].rec;
       }
       cur_ = k;
       stage_off_ = 0;
@@ -340,6 +433,11 @@ class BlockReadStream : public NativeStream {
   Slot slot_[2];
   int cur_ = 1;
   uint64_t stage_off_ = 0;
+  const bool tracing_ = ReadTraceSink::get().on();
+  std::vector<ReadTraceRec> trace_;
+  int cur_rec_ = -1;
+  hipEvent_t base_ev_ = nullptr;
+  int64_t base_ns_ = 0;
 };
 
 std::atomic<int64_t> g_session{(int64_t)1 << 62};   // above the Python range (utils/ids.py)

@@ -69,9 +69,12 @@ constexpr int kErrCallbackFailure = -902;
 constexpr int32_t kSettingsEnablePush = 2, kSettingsMaxConcurrentStreams = 3, kSettingsInitialWindowSize = 4,
                   kSettingsMaxFrameSize = 5;
 constexpr uint32_t kCancel = 0x8;   // RST_STREAM error code
-// Largest DATA frame either side offers or sends (the HTTP/2 default is 16 KiB; gRPC data streams
-// move 1 MiB chunks, so bigger frames cut per-frame work on both ends).
-constexpr uint32_t kMaxFramePayload = 1u << 20;
+// Largest DATA frame either side offers or sends (the HTTP/2 default is 16 KiB).  gRPC data streams
+// move 1 MiB chunks, so bigger frames cut per-frame work on both ends; the extra 64 bytes let a
+// 1 MiB chunk's message (data + ~13-byte gRPC/protobuf header) travel as one frame instead of a
+// 1 MiB frame plus a 13-byte tail.  Not larger: several frames stay in flight within the
+// offset_received window (alluxio.worker.network.reader.buffer.size, 4 MiB).
+constexpr uint32_t kMaxFramePayload = (1u << 20) + 64;
 const char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
 
 struct Lib {

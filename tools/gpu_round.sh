@@ -174,6 +174,31 @@ for s in $STEPS; do
       run wb_host_procs4 600 python tools/worker_bench_host.py --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --client-procs 4 --out "$OUT/worker_bench_host_procs.jsonl"
       run wb_host_procs8 600 python tools/worker_bench_host.py --threads 256 --transports grpc,ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs.jsonl"
       ;;
+    zerocopy)
+      for d in host cuda; do
+        run remote_${d}_p1 300 python tools/remote_device_read_bench.py --dest $d --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --out "$OUT/remote_read_zero_copy.jsonl"
+        run remote_${d}_p4 300 python tools/remote_device_read_bench.py --dest $d --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=4 --out "$OUT/remote_read_zero_copy.jsonl"
+      done
+      rm -f "$OUT/read_trace.jsonl"
+      ALLUXIO_READ_TRACE="$PWD/$OUT/read_trace.jsonl" run remote_host_trace 300 python tools/remote_device_read_bench.py --dest host --file-size 512m --read-size 512m --reps 1 --native-only --client-prop alluxio.user.device.read.parallelism=1 --out "$OUT/remote_read_traced.jsonl"
+      ;;
+    windowab)
+      for d in host cuda; do
+        run wab_${d}_base 300 python tools/remote_device_read_bench.py --dest $d --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --out "$OUT/remote_read_window_ab.jsonl"
+        run wab_${d}_w16 300 python tools/remote_device_read_bench.py --dest $d --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --worker-prop alluxio.worker.network.reader.buffer.size=16MB --out "$OUT/remote_read_window_ab.jsonl"
+        run wab_${d}_w16c2 300 python tools/remote_device_read_bench.py --dest $d --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --client-prop alluxio.user.network.reader.chunk.size.bytes=2MB --worker-prop alluxio.worker.network.reader.buffer.size=16MB --out "$OUT/remote_read_window_ab.jsonl"
+      done
+      ;;
+    writescale)
+      run ww_ct_r5 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_worker_write_cache_through.jsonl"
+      run ingest_c5_t4 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 4 --out "$OUT/r5_ufs_ingest_config5.jsonl"
+      run ingest_c5_t8 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/r5_ufs_ingest_config5.jsonl"
+      ALLUXIO_MOVE_COPY_KERNEL=0 run ingest_c5_t8_runtimecopy 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/r5_ufs_ingest_config5_runtime_copy.jsonl"
+      run rocprof_c5_t8 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_c5_r5" -o c5 --output-format csv -- python3 tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8
+      ;;
+    master16)
+      run master_p16 300 python tools/master_bench_mp.py --ops CreateFile,DeleteFile --procs 16 --threads 4 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_p16_r5b.json"
+      ;;
     numa)
       run wb_host_procs4_roof 600 python tools/worker_bench_host.py --threads 16,64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --out "$OUT/worker_bench_host_procs_roof.jsonl"
       run wb_host_procs1_roof 400 python tools/worker_bench_host.py --threads 16 --transports ipc,grpc --duration 6s --warmup 2s --client-procs 1 --d2h-roof --out "$OUT/worker_bench_host_procs_roof.jsonl"
