@@ -1282,12 +1282,36 @@ class FileOutStream(io.RawIOBase):
         had = bool(self._writers)
         self._writers = []
         if had and self._fanout:
+            # replicas pull the committed block while this stream writes the next one (the pulls
+            # are peer DMAs plus a few RPCs each: serialising them behind every block doubled the
+            # time of a replicated write); close() waits for all of them and raises their errors
             from ..parallel.peer import fan_out
-            errors = fan_out(self._primary_addr, self._fanout, self._block_id, self._block_written,
-                             self.ctx.worker_stub)
+            import concurrent.futures as cf
+            if getattr(self, "_fan_exec", None) is None:
+                self._fan_exec = cf.ThreadPoolExecutor(2, thread_name_prefix="replica-fanout")
+                self._fan_futs = []
+            bid = self._block_id
+            self._fan_futs.append((bid, self._fan_exec.submit(
+                fan_out, self._primary_addr, list(self._fanout), bid, self._block_written, self.ctx.worker_stub)))
             self._fanout = []
-            if errors:
-                raise UnavailableException(f"replicating block {self._block_id} failed: {errors}")
+
+    def _wait_fanouts(self) -> None:
+        futs = getattr(self, "_fan_futs", None) or []
+        self._fan_futs = []
+        errors = []
+        for bid, f in futs:
+            try:
+                e = f.result()
+            except Exception as ex_:  # noqa: BLE001
+                e = [("?", str(ex_))]
+            if e:
+                errors.append((bid, e))
+        ex = getattr(self, "_fan_exec", None)
+        if ex is not None:
+            ex.shutdown(wait=False)
+            self._fan_exec = None
+        if errors:
+            raise UnavailableException(f"replicating blocks failed: {errors}")
 
     def _stop_beside(self) -> None:
         if self._beside is not None:
@@ -1301,6 +1325,10 @@ class FileOutStream(io.RawIOBase):
     def cancel(self) -> None:
         self._canceled = True
         self._stop_beside()
+        try:
+            self._wait_fanouts()        # no replica pull of this file is left running
+        except Exception:  # noqa: BLE001
+            pass
         for w in self._writers:
             w.cancel()
         self._writers = []
@@ -1325,6 +1353,7 @@ class FileOutStream(io.RawIOBase):
         self._stop_beside()
         try:
             self._finish_block()
+            self._wait_fanouts()
             opts = pb.file.CompleteFilePOptions()
             if self._ufs is not None:
                 self._ufs.close()
