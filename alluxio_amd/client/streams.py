@@ -1105,6 +1105,9 @@ class FileOutStream(io.RawIOBase):
                 host = keep.detach().reshape(-1).view(torch.uint8).cpu().numpy()
             else:
                 host = _host_view(ptr, n)        # zero-copy view of the caller's buffer
+            if self.cache and kind != DEVICE and self._pair_write(ptr, n):
+                self._pos += n
+                return n
             if self.cache and n >= self._overlap_min and kind != DEVICE and \
                     FileOutStream._ct_open <= self._OVERLAP_MAX_STREAMS:
                 # CACHE_THROUGH: the UFS write (a native stream or a syscall, both without the
@@ -1127,6 +1130,29 @@ class FileOutStream(io.RawIOBase):
             self._write_cache(ptr, n, kind)
         self._pos += n
         return n
+
+    def _pair_write(self, ptr: int, n: int) -> bool:
+        """CACHE_THROUGH host write inside one block whose cache writer and UFS writer are both
+        native gRPC streams: both get the bytes in one native call (GIL released once; the UFS
+        stream's write on a pooled helper thread).  False = not that shape (the caller writes them
+        the general way)."""
+        us = getattr(self._ufs, "_sink", None)
+        if us is None or self.replicas != 1:
+            return False
+        if not self._writers or self._block_written >= self.block_size:
+            self._next_block()
+        if n > self.block_size - self._block_written or len(self._writers) != 1:
+            return False
+        w = self._writers[0]
+        cs = getattr(w, "_sink", None) if isinstance(w, GrpcBlockWriter) else None
+        if cs is None:
+            return False
+        from ..ops.native import lib, native_errors
+        with native_errors():
+            lib().sink_write_pair(cs, us, ptr, n)
+        self._ufs.length += n
+        self._block_written += n
+        return True
 
     def _write_cache(self, ptr, n, kind):
         done = 0

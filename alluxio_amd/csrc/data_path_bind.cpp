@@ -3,7 +3,13 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <condition_variable>
 #include <cstddef>
+#include <deque>
+#include <functional>
+#include <future>
+#include <mutex>
+#include <thread>
 
 #include "block_source.h"
 #include "data_server.h"
@@ -14,6 +20,45 @@ namespace py = pybind11;
 using namespace amdx;
 
 namespace {
+
+// Helper threads of sink_write_pair (immortal: a call blocked on a slow peer never blocks exit).
+class PairPool {
+ public:
+  static PairPool& get() {
+    static PairPool* p = new PairPool(16);
+    return *p;
+  }
+  std::future<void> run(std::function<void()> f) {
+    auto task = std::make_shared<std::packaged_task<void()>>(std::move(f));
+    std::future<void> fut = task->get_future();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back([task] { (*task)(); });
+    }
+    cv_.notify_one();
+    return fut;
+  }
+
+ private:
+  explicit PairPool(int n) {
+    for (int i = 0; i < n; ++i)
+      std::thread([this] {
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return !q_.empty(); });
+            f = std::move(q_.front());
+            q_.pop_front();
+          }
+          f();
+        }
+      }).detach();
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
 
 PyObject* g_store_error = nullptr;   // alluxio_amd._C.StoreError
 
@@ -306,6 +351,35 @@ void bind_data_path(py::module_& m) {
              s.cancel();
            })
       .def_property_readonly("written", &GrpcBlockSink::written);
+  // CACHE_THROUGH: the same bytes to the cache-tier block stream and the UFS stream at once, one
+  // GIL release for both (the second sink's write runs on a pooled helper thread)
+  m.def("sink_write_pair", [](GrpcBlockSink& a, GrpcBlockSink& b, uint64_t ptr, uint64_t n) {
+        py::gil_scoped_release rel;
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr);
+        auto fut = PairPool::get().run([&b, p, n] { b.write(p, n); });
+        std::exception_ptr ea;
+        try {
+          a.write(p, n);
+        } catch (...) {
+          ea = std::current_exception();
+        }
+        std::exception_ptr eb;
+        try {
+          fut.get();
+        } catch (...) {
+          eb = std::current_exception();
+        }
+        for (auto e : {ea, eb}) {
+          if (!e) continue;
+          try {
+            std::rethrow_exception(e);
+          } catch (const StoreError&) {
+            throw;
+          } catch (const std::exception& x) {
+            throw StoreError(kErrIo, x.what());
+          }
+        }
+      }, py::arg("a"), py::arg("b"), py::arg("ptr"), py::arg("n"));
   py::class_<PySource, BlockSource, std::shared_ptr<PySource>>(m, "PySource")
       .def(py::init<py::object, uint64_t>(), py::arg("reader"), py::arg("length"));
 

@@ -385,6 +385,7 @@ def test_cache_through_ufs_error_surfaces_from_helper_thread(tmp_path):
                 calls.append(len(host))
                 raise OSError("UFS is gone")
             f._ufs.write = boom
+            f._pair_write = lambda ptr, n: False     # the helper-thread path, not the native pair
             with pytest.raises(OSError, match="UFS is gone"):
                 f.write(data)
             assert calls == [data.nbytes]
@@ -886,3 +887,37 @@ def test_bounded_ipc_open_times_out_and_client_falls_back(tmp_path, monkeypatch)
     monkeypatch.setattr(ipc, "lib", lambda: Stub())
     with pytest.raises(UnavailableException):
         ipc.IpcMappings().open(b"x" * 64, 0)
+
+
+def test_cache_through_pair_write_lands_in_cache_and_ufs(tmp_path):
+    """CACHE_THROUGH from a remote client with native streams on both sides: each write goes to the
+    cache block stream and the UFS_FILE stream in one native call (sink_write_pair); the bytes land
+    in both, across block boundaries, and a failed UFS stream fails the write."""
+    import os
+    with _cluster(tmp_path) as c:
+        rfs = _remote_fs(c)
+        try:
+            data = np.random.default_rng(21).integers(0, 256, (9 << 20) + 4097, dtype=np.uint8)
+            with rfs.create_file("/pair", write_type="CACHE_THROUGH", block_size=4 << 20) as f:
+                used = []
+                orig = f._pair_write
+                f._pair_write = lambda ptr, n: used.append(orig(ptr, n)) or used[-1]
+                for i in range(0, len(data), 1 << 20):
+                    f.write(data[i:i + (1 << 20)])
+            assert any(used)
+            assert rfs.read_file("/pair") == data.tobytes()
+            st = rfs.get_status("/pair")
+            assert st.info.inAlluxioPercentage == 100
+            ufs_path = st.info.ufsPath
+            with open(ufs_path.replace("file://", ""), "rb") as fh:
+                assert fh.read() == data.tobytes()
+            # the UFS stream dies: the next paired write raises
+            f2 = rfs.create_file("/pair2", write_type="CACHE_THROUGH", block_size=4 << 20)
+            f2.write(data[:1 << 20])
+            f2._ufs._sink.cancel()
+            with pytest.raises(Exception):
+                for _ in range(8):
+                    f2.write(data[:1 << 20])
+            f2.cancel()
+        finally:
+            rfs.close()

@@ -27,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=4.0)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
     n = int(a.gib * (1 << 30))
     src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
@@ -42,6 +43,9 @@ def main():
     s = timed(lambda: v.sum(), a.iters)
     out["read_sum_GBps"] = round(n / s / 1e9, 1)
     print(json.dumps(out), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f)
 
 
 if __name__ == "__main__":

@@ -196,6 +196,12 @@ for s in $STEPS; do
       ALLUXIO_MOVE_COPY_KERNEL=0 run ingest_c5_t8_runtimecopy 600 python tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8 --out "$OUT/r5_ufs_ingest_config5_runtime_copy.jsonl"
       run rocprof_c5_t8 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_c5_r5" -o c5 --output-format csv -- python3 tools/ufs_ingest_bench.py --ufs s3native --hbm 4g --dram 8g --factor 2 --depths 3 --threads 8
       ;;
+    ctpair)
+      run ww_ct_pair 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_worker_write_cache_through.jsonl"
+      ;;
+    roof)
+      run copy_roof 300 python tools/copy_roof.py --gib 4 --out "$OUT/r5_copy_roof.json"
+      ;;
     master16)
       run master_p16 300 python tools/master_bench_mp.py --ops CreateFile,DeleteFile --procs 16 --threads 4 --duration 5s --client-prop alluxio.user.network.native.rpc.enabled=false --out "$OUT/master_bench_p16_r5b.json"
       ;;
