@@ -3,6 +3,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <pthread.h>
+
 #include <condition_variable>
 #include <cstddef>
 #include <deque>
@@ -43,6 +45,7 @@ class PairPool {
   explicit PairPool(int n) {
     for (int i = 0; i < n; ++i)
       std::thread([this] {
+        pthread_setname_np(pthread_self(), "sink-pair");
         for (;;) {
           std::function<void()> f;
           {

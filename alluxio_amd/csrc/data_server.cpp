@@ -11,6 +11,8 @@
 #include <condition_variable>
 #include <deque>
 #include <map>
+#include <pthread.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -1154,6 +1156,7 @@ class FilePool {
   explicit FilePool(int n) {
     for (int i = 0; i < n; ++i)
       std::thread([this] {
+        pthread_setname_np(pthread_self(), "ufs-file");
         for (;;) {
           std::function<void()> f;
           {
@@ -1435,6 +1438,7 @@ class UploadPool {
   explicit UploadPool(int n) {
     for (int i = 0; i < n; ++i)
       std::thread([this] {
+        pthread_setname_np(pthread_self(), "s3-upload");
         for (;;) {
           std::function<void()> f;
           {

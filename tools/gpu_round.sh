@@ -199,6 +199,11 @@ for s in $STEPS; do
     ctpair)
       run ww_ct_pair 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_worker_write_cache_through.jsonl"
       ;;
+    wdiag)
+      run ww_diag_ct 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_worker_write_diag.jsonl"
+      run ww_diag_mc 600 python tools/worker_write_bench.py --threads 4,16 --file-size 256m --write-type MUST_CACHE --out "$OUT/r5_worker_write_diag.jsonl"
+      run ww_diag_th 600 python tools/worker_write_bench.py --threads 4,16 --file-size 256m --write-type THROUGH --out "$OUT/r5_worker_write_diag.jsonl"
+      ;;
     roof)
       run copy_roof 300 python tools/copy_roof.py --gib 4 --out "$OUT/r5_copy_roof.json"
       ;;

@@ -52,11 +52,14 @@ def run(t):
     except Exception as e:
         errs.append(repr(e))
 ts = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+c0 = os.times()
 t0 = time.perf_counter()
 for t in ts: t.start()
 for t in ts: t.join()
 el = time.perf_counter() - t0
-print("RESULT " + json.dumps({{"bytes": sum(done), "seconds": el, "errors": errs[:3]}}), flush=True)
+c1 = os.times()
+cpu = (c1.user - c0.user + c1.system - c0.system) / el
+print("RESULT " + json.dumps({{"bytes": sum(done), "seconds": el, "errors": errs[:3], "client_cpu_cores": round(cpu, 2)}}), flush=True)
 fs.close()
 """
 
@@ -100,6 +103,9 @@ def main(argv=None) -> int:
                      "alluxio.user.short.circuit.enabled": "true" if transport == "ipc" else "false",
                      "alluxio.user.block.size.bytes.default": a.block_size}
             props.update(dict(kv.split("=", 1) for kv in a.client_prop))
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            from _threadcpu import busy, thread_cpu
+            tc0, tw0 = thread_cpu(), time.perf_counter()
             p = subprocess.run([sys.executable, "-c", CLIENT.format(
                 root=ROOT, props=props, addr=c.master.address, size=size, nfiles=a.files, threads=int(t),
                 wsize=parse_space_size(a.write_size), tag=f"r{i}", wtype=a.write_type)], capture_output=True, text=True, timeout=900)
@@ -108,11 +114,15 @@ def main(argv=None) -> int:
                 print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
                 return 1
             r = json.loads(line[7:])
+            worker_threads = busy(tc0, thread_cpu(), r["seconds"])   # over the client's timed window
             row = {"bench": f"host writers, separate client process ({a.write_type})", "transport": transport, "tier": tier,
                    "threads": int(t), "files_per_thread": a.files, "file_size": a.file_size,
                    "write_size": a.write_size, "bytes": r["bytes"], "seconds": round(r["seconds"], 3),
                    "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3), "errors": r["errors"],
-                   "client_props": a.client_prop, "worker_props": a.worker_prop}
+                   "client_props": a.client_prop, "worker_props": a.worker_prop,
+                   # worker process CPU by thread group during the run (approx: whole subprocess
+                   # lifetime / timed window), and the client's own CPU over its timed window
+                   "worker_thread_cores": worker_threads, "client_cpu_cores": r.get("client_cpu_cores")}
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
