@@ -1019,7 +1019,11 @@ class BlockWriteStream : public WriteStreamBase {
         commit_(commit_method), pool_(std::move(pool)), stats_(std::move(stats)) {}
 
   ~BlockWriteStream() override {
-    if (stage_) pool_->put(stage_);
+    drain();                                 // no DMA may still target the block's pages
+    for (auto& sl : slot_) {
+      if (sl.ev) (void)hipEventDestroy(sl.ev);
+      if (sl.buf) pool_->put(sl.buf);
+    }
     try {
       store_->cleanup_session(session_);     // aborts the temp block unless Python committed it
     } catch (...) {
@@ -1051,6 +1055,10 @@ class BlockWriteStream : public WriteStreamBase {
   bool on_end(uint32_t* method, std::string* payload) override {
     ended_ = true;
     if (err_) return false;
+    if (!drain()) {                          // every H2D landed before the commit reads the block
+      fail(13, "writing block " + std::to_string(block_) + ": H2D staging copy failed");
+      return false;
+    }
     // NativeWriteCommitRequest: session_id=1 block_id=2 length=3 pin=4
     std::string m;
     h2::put_varint(m, (1u << 3));
@@ -1083,21 +1091,54 @@ class BlockWriteStream : public WriteStreamBase {
   void write(const uint8_t* p, size_t n) {
     if (!device_) {       // host arena / file dir: straight from the HTTP/2 receive buffer
       store_->write(session_, block_, pos_, reinterpret_cast<uint64_t>(p), n, (int)MemKind::kHost, 0, true);
-    } else {              // HBM: through pinned staging, so the H2D is a DMA and not a pageable copy
-      if (!stage_) stage_ = pool_->get();
+    } else {
+      // HBM: through two pinned staging slots, so the H2D is a DMA and not a pageable copy, and the
+      // I/O thread does not wait for it -- the DMA of chunk k runs while chunk k+1 is received
+      // and copied into the other slot; a slot is waited for only when it comes round again
       hipStream_t st = thread_stream(store_);
       size_t done = 0;
       while (done < n) {
+        Slot& sl = slot_[cur_];
+        if (!sl.buf) {
+          sl.buf = pool_->get();
+          if (hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) sl.ev = nullptr;
+        }
+        if (sl.inflight) {
+          if (hipEventSynchronize(sl.ev) != hipSuccess) throw std::runtime_error("H2D staging copy failed");
+          sl.inflight = false;
+        }
         const size_t k = (size_t)std::min<uint64_t>(n - done, pool_->size());
-        std::memcpy(stage_, p + done, k);
-        store_->write(session_, block_, pos_ + done, reinterpret_cast<uint64_t>(stage_), k, (int)MemKind::kHost,
-                      reinterpret_cast<uint64_t>(st), true);
+        std::memcpy(sl.buf, p + done, k);
+        store_->write(session_, block_, pos_ + done, reinterpret_cast<uint64_t>(sl.buf), k, (int)MemKind::kHost,
+                      reinterpret_cast<uint64_t>(st), sl.ev == nullptr);
+        sl.inflight = sl.ev != nullptr && hipEventRecord(sl.ev, st) == hipSuccess;
+        if (sl.ev && !sl.inflight) (void)hipStreamSynchronize(st);
+        cur_ ^= 1;
         done += k;
       }
     }
     pos_ += n;
     stats_->write_bytes.fetch_add(n, std::memory_order_relaxed);
   }
+
+  // Waits for the staging copies still in flight; false if one failed.
+  bool drain() {
+    bool ok = true;
+    for (auto& sl : slot_) {
+      if (!sl.inflight) continue;
+      if (hipEventSynchronize(sl.ev) != hipSuccess) ok = false;
+      sl.inflight = false;
+    }
+    return ok;
+  }
+
+  struct Slot {
+    uint8_t* buf = nullptr;
+    hipEvent_t ev = nullptr;
+    bool inflight = false;
+  };
+  Slot slot_[2];
+  int cur_ = 0;
 
   BlockStore* store_;
   int64_t session_, block_;
@@ -1106,7 +1147,6 @@ class BlockWriteStream : public WriteStreamBase {
   uint32_t commit_;
   std::shared_ptr<StagingPool> pool_;
   std::shared_ptr<DataServerStats> stats_;
-  uint8_t* stage_ = nullptr;
 };
 
 int grpc_status_of_errno(int e) {

@@ -204,6 +204,11 @@ for s in $STEPS; do
       run ww_diag_mc 600 python tools/worker_write_bench.py --threads 4,16 --file-size 256m --write-type MUST_CACHE --out "$OUT/r5_worker_write_diag.jsonl"
       run ww_diag_th 600 python tools/worker_write_bench.py --threads 4,16 --file-size 256m --write-type THROUGH --out "$OUT/r5_worker_write_diag.jsonl"
       ;;
+    ctio)
+      run ww_ct_async 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_worker_write_cache_through.jsonl"
+      run ww_ct_io16 600 python tools/worker_write_bench.py --threads 4,8,16 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.native.io.threads=16 --out "$OUT/r5_worker_write_cache_through_io16.jsonl"
+      run ww_mc_async 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type MUST_CACHE --out "$OUT/r5_worker_write_must_cache.jsonl"
+      ;;
     roof)
       run copy_roof 300 python tools/copy_roof.py --gib 4 --out "$OUT/r5_copy_roof.json"
       ;;
@@ -213,6 +218,11 @@ for s in $STEPS; do
     numa)
       run wb_host_procs4_roof 600 python tools/worker_bench_host.py --threads 16,64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --out "$OUT/worker_bench_host_procs_roof.jsonl"
       run wb_host_procs1_roof 400 python tools/worker_bench_host.py --threads 16 --transports ipc,grpc --duration 6s --warmup 2s --client-procs 1 --d2h-roof --out "$OUT/worker_bench_host_procs_roof.jsonl"
+      ;;
+    numa2)
+      run numa_bound_1m 600 python tools/worker_bench_host.py --threads 64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --bind-gpu-node --out "$OUT/r5_host_read_numa_bound.jsonl"
+      run numa_bound_4m 600 python tools/worker_bench_host.py --threads 64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --bind-gpu-node --reader-buffer 4MB --out "$OUT/r5_host_read_numa_bound.jsonl"
+      run numa_free_4m 600 python tools/worker_bench_host.py --threads 64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --reader-buffer 4MB --out "$OUT/r5_host_read_numa_bound.jsonl"
       ;;
     hostprocs2)
       ALLUXIO_READER_STREAMS=1 run wb_host_procs8_s1 600 python tools/worker_bench_host.py --threads 256 --transports ipc --duration 6s --warmup 2s --client-procs 8 --out "$OUT/worker_bench_host_procs_streams.jsonl"

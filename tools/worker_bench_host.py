@@ -32,8 +32,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CLIENT = r"""
-import json, sys, faulthandler
+import json, os, sys, faulthandler
 faulthandler.enable()
+if {cpus!r}:
+    os.sched_setaffinity(0, {cpus!r})     # before anything touches the GPU
 sys.path.insert(0, {root!r})
 from alluxio_amd.client.file_system import FileSystem
 from alluxio_amd.conf import Configuration
@@ -51,7 +53,9 @@ fs.close()
 # pinned host buffer (hipMemcpyAsync D2H + sync) for 2 s -- the platform ceiling the short-circuit
 # readers' D2H refills share.
 ROOF = r"""
-import json, sys, time
+import json, os, sys, time
+if {cpus!r}:
+    os.sched_setaffinity(0, {cpus!r})
 sys.path.insert(0, {root!r})
 import torch
 from alluxio_amd.ops.native import lib
@@ -88,10 +92,22 @@ def main(argv=None) -> int:
                     help="spread the threads over this many client processes (the reference's --clients "
                          "makes N FileSystem instances in one JVM; Python instances in one interpreter "
                          "share one lock, so they go to separate processes); throughput is summed")
+    ap.add_argument("--bind-gpu-node", action="store_true",
+                    help="run the client (and roof) processes on the CPUs of the GPU's NUMA node")
     ap.add_argument("--d2h-roof", action="store_true",
                     help="after each run, the same number of processes measure the D2H copy roof together")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
+    cpus = []
+    if a.bind_gpu_node:
+        from alluxio_amd.ops.native import lib
+        node = lib().gpu_numa_node(0)
+        if node >= 0:
+            with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+                for part in f.read().strip().split(","):
+                    lo, _, hi = part.partition("-")
+                    cpus.extend(range(int(lo), int(hi or lo) + 1))
+            cpus = sorted(set(cpus) & os.sched_getaffinity(0))
 
     from alluxio_amd.minicluster import LocalAlluxioCluster
     import numpy as np
@@ -128,7 +144,7 @@ def main(argv=None) -> int:
                 t0 = time.time()
                 s0 = (stats.streams, stats.bytes, stats.declined) if stats is not None else (0, 0, 0)
                 procs = [subprocess.Popen([sys.executable, "-c", CLIENT.format(root=ROOT, addr=c.master.address,
-                                                                              args=args, props=props)],
+                                                                              args=args, props=props, cpus=cpus)],
                                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
                          for _ in range(nproc)]
                 results = []
@@ -153,9 +169,11 @@ def main(argv=None) -> int:
                        "reader_buffer": a.reader_buffer, "client_props": a.client_prop,
                        "client_procs": nproc}
                 row["client_placement"] = [x.get("placement", "") for x in results]
+                row["bound_to_gpu_node"] = bool(cpus)
+                row["reader_buffer"] = a.reader_buffer
                 if a.d2h_roof:
                     start = time.time() + 8.0       # all roof processes start copying together
-                    rp = [subprocess.Popen([sys.executable, "-c", ROOF.format(root=ROOT, start=start)],
+                    rp = [subprocess.Popen([sys.executable, "-c", ROOF.format(root=ROOT, start=start, cpus=cpus)],
                                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
                           for _ in range(nproc)]
                     roofs = []
