@@ -668,6 +668,11 @@ PYBIND11_MODULE(_C, m) {
              return py::str(p);
            })
       .def("forget_path", &FuseServer::forget_path, G())
+      .def("register_write_handle", &FuseServer::register_write_handle, py::arg("fh"), py::arg("offset") = 0, G())
+      .def("unregister_write_handle", &FuseServer::unregister_write_handle, G())
+      .def("batch_done", &FuseServer::batch_done, G())
+      .def("wait_batches", &FuseServer::wait_batches, py::arg("fh"), py::arg("timeout_ms") = 120000, G())
+      .def_property_readonly("write_batches", &FuseServer::write_batches)
       .def("moved", &FuseServer::moved, G())
       .def("put_attr", [](FuseServer& s, const std::string& path, py::bytes attr, int64_t ttl_ms, uint32_t valid_s,
                           int64_t file_id, bool complete, const std::vector<int64_t>& blocks,

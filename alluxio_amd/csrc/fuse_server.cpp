@@ -73,12 +73,13 @@ struct FlushIn {
   uint64_t lock_owner;
 };
 constexpr size_t kAttrBytes = 88;
-constexpr uint32_t kLookup = 1, kForget = 2, kGetattr = 3, kOpen = 14, kRead = 15, kRelease = 18, kFlush = 25,
-                   kInterrupt = 36, kIoctl = 39, kBatchForget = 42;
+constexpr uint32_t kLookup = 1, kForget = 2, kGetattr = 3, kOpen = 14, kRead = 15, kWrite = 16, kRelease = 18,
+                   kFsync = 20, kFlush = 25, kInterrupt = 36, kIoctl = 39, kBatchForget = 42;
 constexpr uint32_t kFopenKeepCache = 1u << 1;
 constexpr uint32_t kFopenNoFlush = 1u << 5;       // read-only native handle: close() sends no FLUSH
 constexpr uint64_t kNativeFh = 1ull << 62;
-constexpr size_t kBufSize = (128u << 10) + 4096 * 2;
+constexpr size_t kBufSize = (1u << 20) + 4096 * 2;      // a 1 MiB WRITE (max_pages 256) + headers
+constexpr size_t kPipeSize = ((128u << 10) + 4096 * 2) * 2; // splice of READ replies (<= 128 KiB)
 
 int64_t now_ms() {
   return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -293,6 +294,110 @@ std::vector<uint64_t> FuseServer::stats() {
     v[128 + i] = native_ns_[i].load();
   }
   return v;
+}
+
+// ---- write-behind -------------------------------------------------------------------------------
+void FuseServer::register_write_handle(uint64_t fh, uint64_t offset) {
+  std::lock_guard<std::mutex> g(wb_mu_);
+  WriteBehind& w = wb_[fh];
+  w.next = w.buf_off = offset;
+}
+
+void FuseServer::unregister_write_handle(uint64_t fh) {
+  std::unique_lock<std::mutex> lk(wb_mu_);
+  wb_cv_.wait_for(lk, std::chrono::seconds(60), [&] {
+    auto it = wb_.find(fh);
+    return it == wb_.end() || it->second.outstanding == 0;
+  });
+  wb_.erase(fh);
+  wb_cv_.notify_all();
+}
+
+void FuseServer::batch_done(uint64_t fh, int err) {
+  std::lock_guard<std::mutex> g(wb_mu_);
+  auto it = wb_.find(fh);
+  if (it != wb_.end()) {
+    if (it->second.outstanding > 0) --it->second.outstanding;
+    if (err && !it->second.err) it->second.err = err;
+  }
+  wb_cv_.notify_all();
+}
+
+int FuseServer::wait_batches(uint64_t fh, int timeout_ms) {
+  std::unique_lock<std::mutex> lk(wb_mu_);
+  auto it = wb_.find(fh);
+  if (it == wb_.end()) return 0;
+  if (!it->second.buf.empty()) queue_batch(lk, fh, it->second);    // a FLUSH that raced the WRITEs
+  const bool done = wb_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] {
+    auto j = wb_.find(fh);
+    return j == wb_.end() || j->second.outstanding == 0;
+  });
+  it = wb_.find(fh);
+  if (!done) return ETIMEDOUT;
+  return it == wb_.end() ? 0 : it->second.err;
+}
+
+void FuseServer::queue_batch(std::unique_lock<std::mutex>& lk, uint64_t fh, WriteBehind& w) {
+  // one batch per handle in flight: the next waits for Python to apply the previous one
+  wb_cv_.wait(lk, [&] { return w.outstanding == 0 || !alive(); });
+  if (w.buf.empty()) return;
+  FuseRequest r{0, kOpWriteBatch, w.nodeid, w.uid, w.gid, w.pid, std::string()};
+  r.body.reserve(16 + w.buf.size());
+  r.body.append(reinterpret_cast<const char*>(&fh), 8);
+  r.body.append(reinterpret_cast<const char*>(&w.buf_off), 8);
+  r.body += w.buf;
+  w.buf.clear();
+  w.buf_off = w.next;
+  ++w.outstanding;
+  write_batches_.fetch_add(1, std::memory_order_relaxed);
+  {
+    std::lock_guard<std::mutex> g(qmu_);
+    queue_.push_back(std::move(r));
+  }
+  qcv_.notify_one();
+}
+
+bool FuseServer::write_behind(const char* req, size_t n) {
+  const InHeader* ih = reinterpret_cast<const InHeader*>(req);
+  const char* body = req + sizeof(InHeader);
+  const size_t blen = n - sizeof(InHeader);
+  if (blen < 40) return false;
+  uint64_t fh, off;
+  uint32_t size;
+  std::memcpy(&fh, body, 8);
+  std::memcpy(&off, body + 8, 8);
+  std::memcpy(&size, body + 16, 4);
+  if (blen < 40 + (size_t)size) return false;
+  std::unique_lock<std::mutex> lk(wb_mu_);
+  auto it = wb_.find(fh);
+  if (it == wb_.end()) return false;
+  WriteBehind& w = it->second;
+  if (w.err) return false;                              // Python reports the error
+  if (off + size <= w.next && off < w.next) {
+    // re-send of a range already taken (a kernel quirk the Python path also tolerates)
+  } else if (off != w.next) {
+    if (!w.buf.empty()) queue_batch(lk, fh, w);         // what came before goes first
+    return false;
+  } else {
+    if (w.buf.empty()) w.buf_off = off;
+    w.nodeid = ih->nodeid;
+    w.uid = ih->uid;
+    w.gid = ih->gid;
+    w.pid = ih->pid;
+    w.buf.append(body + 40, size);
+    w.next += size;
+    if (w.buf.size() >= kWriteBatchBytes) queue_batch(lk, fh, w);
+  }
+  lk.unlock();
+  const uint32_t out[2] = {size, 0};                    // fuse_write_out
+  send(ih->unique, 0, reinterpret_cast<const char*>(out), sizeof(out));
+  return true;
+}
+
+void FuseServer::flush_handle(uint64_t fh) {
+  std::unique_lock<std::mutex> lk(wb_mu_);
+  auto it = wb_.find(fh);
+  if (it != wb_.end() && !it->second.buf.empty()) queue_batch(lk, fh, it->second);
 }
 
 // ---- python slow path ---------------------------------------------------------------------------
@@ -538,6 +643,10 @@ bool FuseServer::fast(const char* req, size_t n, std::string& scratch) {
       count();
       send(ih->unique, ENOTTY, nullptr, 0);
       return true;
+    case kWrite:
+      if (!write_behind(req, n)) return false;
+      count();
+      return true;
     case kLookup: {
       if (blen == 0 || body[blen - 1] != '\0') return false;
       bool ok;
@@ -707,7 +816,7 @@ void FuseServer::loop(int idx) {
   tl_pipe_[0] = tl_pipe_[1] = -1;
   int pfd[2];
   if (!arenas_.empty() && !getenv("ALLUXIO_FUSE_NO_SPLICE") && pipe2(pfd, O_CLOEXEC) == 0) {
-    if (fcntl(pfd[1], F_SETPIPE_SZ, (int)(kBufSize * 2)) >= (int)kBufSize) {
+    if (fcntl(pfd[1], F_SETPIPE_SZ, (int)kPipeSize) >= (int)(kPipeSize / 2)) {
       tl_pipe_[0] = pfd[0];
       tl_pipe_[1] = pfd[1];
     } else {
@@ -745,6 +854,12 @@ void FuseServer::loop(int idx) {
       // fall through to the python path
     }
     const InHeader* ih = reinterpret_cast<const InHeader*>(buf.data());
+    if ((ih->opcode == kFlush || ih->opcode == kRelease || ih->opcode == kFsync) &&
+        (size_t)n >= sizeof(InHeader) + 8) {
+      uint64_t fh;                                  // the handle's buffered writes go first
+      std::memcpy(&fh, buf.data() + sizeof(InHeader), 8);
+      flush_handle(fh);
+    }
     if (ih->opcode < 64) python_ops_[ih->opcode]++;
     FuseRequest r{ih->unique, ih->opcode, ih->nodeid, ih->uid, ih->gid, ih->pid,
                   std::string(buf.data() + sizeof(InHeader), (size_t)n - sizeof(InHeader))};
@@ -759,6 +874,7 @@ void FuseServer::loop(int idx) {
     close(tl_pipe_[1]);
   }
   dead_.store(true);                                // the connection is gone: wake the python side
+  wb_cv_.notify_all();
   qcv_.notify_all();
 }
 

@@ -96,7 +96,41 @@ class FuseServer {
   uint64_t native_reads() const { return native_reads_.load(); }
   uint64_t fallback_opens() const { return fallback_opens_.load(); }
 
+  // ---- write-behind of sequential writes (write handles the Python side registers) ----------
+  // WRITE requests of a registered handle at its next offset are answered on the reader thread
+  // and gathered into batches of kWriteBatchBytes, queued to Python as one request of opcode
+  // kOpWriteBatch (body: fh u64, file offset u64, data) -- one Python call per batch instead of
+  // one per 128 KiB request.  At most one batch per handle is queued or being applied at a time
+  // (the next waits: bounded memory, in-order application by any Python thread).  FLUSH /
+  // RELEASE / FSYNC of the handle queue its pending bytes first; Python waits for them
+  // (wait_batches) before completing the file, and reports each batch back (batch_done).
+  static constexpr uint32_t kOpWriteBatch = 4096;
+  static constexpr size_t kWriteBatchBytes = 8u << 20;
+  void register_write_handle(uint64_t fh, uint64_t offset);
+  void unregister_write_handle(uint64_t fh);
+  void batch_done(uint64_t fh, int err);
+  int wait_batches(uint64_t fh, int timeout_ms);   // first error of the handle's batches (0: none)
+  uint64_t write_batches() const { return write_batches_.load(); }
+
  private:
+  struct WriteBehind {
+    uint64_t next = 0;      // file offset the next sequential WRITE must carry
+    uint64_t buf_off = 0;   // file offset of buf[0]
+    std::string buf;
+    int outstanding = 0;    // batches queued to / being applied by Python
+    int err = 0;
+    uint64_t nodeid = 0;
+    uint32_t uid = 0, gid = 0, pid = 0;
+  };
+  std::mutex wb_mu_;
+  std::condition_variable wb_cv_;
+  std::unordered_map<uint64_t, WriteBehind> wb_;
+  std::atomic<uint64_t> write_batches_{0};
+  // queues the handle's pending bytes as a batch (wb_mu_ held in `lk`; waits for the previous one)
+  void queue_batch(std::unique_lock<std::mutex>& lk, uint64_t fh, WriteBehind& w);
+  bool write_behind(const char* req, size_t n);   // true: the WRITE was taken
+  void flush_handle(uint64_t fh);                  // before a FLUSH / RELEASE / FSYNC goes to Python
+
   struct Attr {
     std::string raw;                 // fuse_attr
     int64_t expires_ms;

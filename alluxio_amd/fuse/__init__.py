@@ -294,7 +294,8 @@ class AlluxioFuseOps:
                 return len(data)  # duplicate write of an already-written range (OSXFUSE quirk)
             if offset > of.write_offset:
                 raise FuseOSError(errno.EOPNOTSUPP)  # random writes are not supported
-            self._call(of.fout.write, bytes(data))
+            # the request body outlives this synchronous write: no copy of it (8 MiB batches)
+            self._call(of.fout.write, data if isinstance(data, (bytes, bytearray, memoryview)) else bytes(data))
             of.write_offset = offset + len(data)
         return len(data)
 

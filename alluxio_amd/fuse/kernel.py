@@ -46,6 +46,7 @@ LOG = logging.getLogger(__name__)
 LOOKUP, FORGET, GETATTR, SETATTR = 1, 2, 3, 4
 MKDIR, UNLINK, RMDIR, RENAME = 9, 10, 11, 12
 OPEN, READ, WRITE, STATFS, RELEASE, FSYNC = 14, 15, 16, 17, 18, 20
+WRITE_BATCH = 4096      # write-behind batch of the native server (FuseServer::kOpWriteBatch)
 GETXATTR, LISTXATTR, FLUSH, INIT, OPENDIR, READDIR, RELEASEDIR, FSYNCDIR = 22, 23, 25, 26, 27, 28, 29, 30
 ACCESS, CREATE, INTERRUPT, DESTROY, BATCH_FORGET, READDIRPLUS, RENAME2 = 34, 35, 36, 38, 42, 44, 45
 
@@ -76,6 +77,8 @@ FATTR_MODE, FATTR_UID, FATTR_GID, FATTR_SIZE = 1 << 0, 1 << 1, 1 << 2, 1 << 3
 FATTR_ATIME, FATTR_MTIME = 1 << 4, 1 << 5
 FUSE_ASYNC_READ, FUSE_ATOMIC_O_TRUNC, FUSE_BIG_WRITES = 1 << 0, 1 << 3, 1 << 5
 FUSE_AUTO_INVAL_DATA, FUSE_NO_OPEN_SUPPORT, FUSE_INIT_EXT = 1 << 12, 1 << 17, 1 << 30
+FUSE_MAX_PAGES = 1 << 22
+NATIVE_MAX_WRITE = 1 << 20       # native server: 1 MiB WRITE requests (max_pages 256, kernel 4.20+)
 FUSE_PASSTHROUGH_HI = 1 << (37 - 32)           # FUSE_PASSTHROUGH, in flags2
 FUSE_DO_READDIRPLUS, FUSE_READDIRPLUS_AUTO = 1 << 13, 1 << 14
 FOPEN_KEEP_CACHE = 1 << 1
@@ -99,8 +102,11 @@ class FuseKernelServer:
     def __init__(self, ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False,
                  keep_cache="auto", native: bool | None = None, store=None, session: int = 0,
                  py_threads: int | None = None, read_only: bool = False, passthrough: bool = False,
-                 file_ttl_s: int = TTL_COMPLETE_S):
+                 file_ttl_s: int = TTL_COMPLETE_S, write_behind: bool = True):
         self.ops = ops
+        # sequential writes gathered by the native server into 8 MiB batches (one Python call each)
+        self.write_behind = write_behind
+        self._wb_handles: set[int] = set()
         self.file_ttl_s = file_ttl_s
         self.read_only = read_only
         self.passthrough = passthrough
@@ -420,9 +426,49 @@ class FuseKernelServer:
                 continue
             for unique, op, nodeid, _uid, _gid, _pid, body in reqs:
                 try:
-                    self._serve(op, unique, nodeid, body)
+                    if op == WRITE_BATCH:
+                        self._apply_batch(nodeid, body)
+                    else:
+                        self._serve(op, unique, nodeid, body)
                 except Exception:  # noqa: BLE001 - never kill a serving thread
                     LOG.exception("fuse request failed")
+
+    def _apply_batch(self, nodeid: int, body) -> None:
+        """Sequential WRITEs the native server already answered, gathered into one batch
+        (csrc/fuse_server.cpp write-behind): written through the handle's output stream; the
+        outcome goes back to the server, and a FLUSH / RELEASE of the handle reports a failure."""
+        fh, off = struct.unpack_from("<QQ", body)
+        err = 0
+        try:
+            self.ops.write(self._path(nodeid), memoryview(body)[16:], off, fh)
+        except FuseOSError as e:
+            err = e.errno or errno.EIO
+        except OSError as e:
+            err = e.errno or errno.EIO
+        except Exception:  # noqa: BLE001
+            LOG.debug("fuse write batch failed", exc_info=True)
+            err = errno.EIO
+        self._srv.batch_done(fh, err)
+
+    def _write_behind(self, fh: int) -> None:
+        if self._srv is not None and self.write_behind:
+            self._srv.register_write_handle(fh, 0)
+            with self._lock:
+                self._wb_handles.add(fh)
+
+    def _wait_writes(self, fh: int, release: bool = False) -> None:
+        """Every batched write of ``fh`` applied (raises the first failure as FuseOSError)."""
+        with self._lock:
+            registered = fh in self._wb_handles
+            if release:
+                self._wb_handles.discard(fh)
+        if not registered:
+            return
+        err = self._srv.wait_batches(fh)
+        if release:
+            self._srv.unregister_write_handle(fh)
+        if err:
+            raise FuseOSError(err)
 
     def _reply(self, unique: int, err: int = 0, payload: bytes = b"") -> None:
         if self._srv is not None:
@@ -493,7 +539,12 @@ class FuseKernelServer:
                     self.passthrough_active = True
                     return INIT_OUT_EXT.pack(7, 40, max_ra, (flags & want) | FUSE_INIT_EXT, 16, 12, MAX_WRITE, 1,
                                              0, 0, FUSE_PASSTHROUGH_HI, 1)
-            return INIT_OUT.pack(7, min(minor, 34), max_ra, flags & want, 16, 12, MAX_WRITE, 1, 0, 0)
+            max_write, max_pages = MAX_WRITE, 0
+            if self._srv is not None and flags & FUSE_MAX_PAGES and not self.read_only:
+                # fewer, larger WRITE requests (the native server reads up to 1 MiB + headers)
+                want |= FUSE_MAX_PAGES
+                max_write, max_pages = NATIVE_MAX_WRITE, NATIVE_MAX_WRITE >> 12
+            return INIT_OUT.pack(7, min(minor, 34), max_ra, flags & want, 16, 12, max_write, 1, max_pages, 0)
         if op == DESTROY:
             return b""
         if op == LOOKUP:
@@ -563,6 +614,7 @@ class FuseKernelServer:
             path = self._child(self._path(nodeid), name)
             fh = ops.create(path, mode)
             self._inval(path)
+            self._write_behind(fh)
             return self._entry(path) + OPEN_OUT.pack(fh, 0, 0)
         if op == OPEN:
             flags = struct.unpack_from("<I", body)[0]
@@ -570,6 +622,8 @@ class FuseKernelServer:
             if flags & (os.O_WRONLY | os.O_RDWR):
                 self._inval(path)
             fh = ops.open(path, flags)
+            if flags & (os.O_WRONLY | os.O_RDWR):
+                self._write_behind(fh)
             keep = 0
             if flags & (os.O_WRONLY | os.O_RDWR) == 0 and self._keep_mode:
                 # completed (write-once) files never change under one file id: keep the kernel
@@ -598,6 +652,7 @@ class FuseKernelServer:
             return struct.pack("<II", n, 0)
         if op == FLUSH:
             fh = struct.unpack_from("<Q", body)[0]
+            self._wait_writes(fh)
             if ops.is_write_handle(fh):
                 self._inval(self._path(nodeid))
             ops.flush(None, fh)
@@ -606,6 +661,10 @@ class FuseKernelServer:
             return b""
         if op == RELEASE:
             fh = struct.unpack_from("<Q", body)[0]
+            try:
+                self._wait_writes(fh, release=True)
+            except FuseOSError:
+                pass                          # reported at FLUSH; release still frees the handle
             try:
                 ops.release(None, fh)
             except FuseOSError:
@@ -681,9 +740,10 @@ class FuseKernelServer:
 def mount_kernel(ops: AlluxioFuseOps, mountpoint: str, threads: int = 4, allow_other: bool = False,
                  keep_cache="auto", native: bool | None = None, store=None, session: int = 0,
                  py_threads: int | None = None, read_only: bool = False, passthrough: bool = False,
-                 file_ttl_s: int = TTL_COMPLETE_S) -> FuseKernelServer:
+                 file_ttl_s: int = TTL_COMPLETE_S, write_behind: bool = True) -> FuseKernelServer:
     """Mount ``ops`` at ``mountpoint`` through ``/dev/fuse``; returns the running server.
     ``store``: the co-located worker's native BlockStore (native opens/reads of cached files).
-    ``read_only``: ``-o ro`` -- with the native server this also negotiates zero-message opens."""
+    ``read_only``: ``-o ro`` -- with the native server this also negotiates zero-message opens.
+    ``write_behind``: the native server gathers sequential writes into 8 MiB batches."""
     return FuseKernelServer(ops, mountpoint, threads, allow_other, keep_cache, native, store, session,
-                            py_threads, read_only, passthrough, file_ttl_s).mount()
+                            py_threads, read_only, passthrough, file_ttl_s, write_behind).mount()

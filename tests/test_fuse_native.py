@@ -196,6 +196,35 @@ print(json.dumps(r))
         m.close()
 
 
+def test_native_write_behind_batches_sequential_writes(tmp_path):
+    """Sequential writes through the native mount are answered by the server and reach Python as
+    8 MiB batches (csrc/fuse_server.cpp write-behind); close() waits for every batch, so the file
+    is complete and byte-exact when it returns -- including a tail shorter than a batch."""
+    m = _Mount(tmp_path, "native")
+    try:
+        m.mount()
+        out = _posix(f"""
+import json, os, hashlib
+m = {m.mnt!r}
+os.makedirs(m + "/wb", exist_ok=True)
+data = os.urandom((20 << 20) + 4321)
+with open(m + "/wb/f.bin", "wb") as f:
+    for i in range(0, len(data), 1 << 20):
+        f.write(data[i:i + (1 << 20)])
+got = open(m + "/wb/f.bin", "rb").read()
+print(json.dumps({{"n": len(got), "same": got == data, "md5": hashlib.md5(data).hexdigest()}}))
+""")
+        assert out["n"] == (20 << 20) + 4321 and out["same"]
+        import hashlib
+        assert hashlib.md5(m.fs.read_file("/wb/f.bin")).hexdigest() == out["md5"]
+        srv = m.srv._srv
+        assert srv.write_batches >= 2                       # 20 MiB in 8 MiB batches (+ the tail)
+        py = m.srv.op_stats()["python"]
+        assert py.get("WRITE", 0) == 0                      # no 128 KiB WRITE reached Python
+    finally:
+        m.close()
+
+
 # ---- no mount: node table and attribute cache --------------------------------------------------
 def _attr_bytes(size: int, mode: int) -> bytes:
     import struct

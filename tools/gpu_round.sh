@@ -209,6 +209,12 @@ for s in $STEPS; do
       run ww_ct_io16 600 python tools/worker_write_bench.py --threads 4,8,16 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.native.io.threads=16 --out "$OUT/r5_worker_write_cache_through_io16.jsonl"
       run ww_mc_async 600 python tools/worker_write_bench.py --threads 1,4,16 --file-size 256m --write-type MUST_CACHE --out "$OUT/r5_worker_write_must_cache.jsonl"
       ;;
+    ctnuma)
+      run ww_ct_bound 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --out "$OUT/r5_worker_write_cache_through_bound.jsonl"
+      run ww_ct_bound_io16 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --worker-prop alluxio.worker.data.server.native.io.threads=16 --out "$OUT/r5_worker_write_cache_through_bound.jsonl"
+      run numa_bound_1m_b 600 python tools/worker_bench_host.py --threads 64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --bind-gpu-node --out "$OUT/r5_host_read_numa_bound2.jsonl"
+      run numa_bound_4m_b 600 python tools/worker_bench_host.py --threads 64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --bind-gpu-node --reader-buffer 4MB --out "$OUT/r5_host_read_numa_bound2.jsonl"
+      ;;
     roof)
       run copy_roof 300 python tools/copy_roof.py --gib 4 --out "$OUT/r5_copy_roof.json"
       ;;

@@ -24,6 +24,8 @@ sys.path.insert(0, ROOT)
 
 CLIENT = r"""
 import faulthandler, json, os, sys, threading, time
+if {cpus!r}:
+    os.sched_setaffinity(0, {cpus!r})     # before anything touches the GPU
 sys.path.insert(0, {root!r})
 if os.environ.get("WW_DUMP_AFTER"):     # debugging a stuck writer: dump every thread's stack, exit
     faulthandler.dump_traceback_later(float(os.environ["WW_DUMP_AFTER"]), exit=True)
@@ -78,8 +80,21 @@ def main(argv=None) -> int:
                     "(the UFS is a local directory under the work dir)")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--worker-prop", action="append", default=[], help="extra worker property k=v")
+    ap.add_argument("--bind-gpu-node", action="store_true",
+                    help="run the worker (this process) and the client on the CPUs of the GPU's NUMA node")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
+    cpus = []
+    if a.bind_gpu_node:
+        from alluxio_amd.ops.native import lib
+        node = lib().gpu_numa_node(0)
+        if node >= 0:
+            with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+                for part in f.read().strip().split(","):
+                    lo, _, hi = part.partition("-")
+                    cpus.extend(range(int(lo), int(hi or lo) + 1))
+            cpus = sorted(set(cpus) & os.sched_getaffinity(0))
+            os.sched_setaffinity(0, cpus)          # the in-process worker's threads inherit it
     import torch
 
     from alluxio_amd.minicluster import LocalAlluxioCluster
@@ -108,7 +123,8 @@ def main(argv=None) -> int:
             tc0, tw0 = thread_cpu(), time.perf_counter()
             p = subprocess.run([sys.executable, "-c", CLIENT.format(
                 root=ROOT, props=props, addr=c.master.address, size=size, nfiles=a.files, threads=int(t),
-                wsize=parse_space_size(a.write_size), tag=f"r{i}", wtype=a.write_type)], capture_output=True, text=True, timeout=900)
+                wsize=parse_space_size(a.write_size), tag=f"r{i}", wtype=a.write_type, cpus=cpus)],
+                capture_output=True, text=True, timeout=900)
             line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
             if line is None:
                 print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
@@ -122,7 +138,8 @@ def main(argv=None) -> int:
                    "client_props": a.client_prop, "worker_props": a.worker_prop,
                    # worker process CPU by thread group during the run (approx: whole subprocess
                    # lifetime / timed window), and the client's own CPU over its timed window
-                   "worker_thread_cores": worker_threads, "client_cpu_cores": r.get("client_cpu_cores")}
+                   "worker_thread_cores": worker_threads, "client_cpu_cores": r.get("client_cpu_cores"),
+                   "bound_to_gpu_node": bool(cpus)}
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
