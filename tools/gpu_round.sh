@@ -215,6 +215,10 @@ for s in $STEPS; do
       run numa_bound_1m_b 600 python tools/worker_bench_host.py --threads 64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --bind-gpu-node --out "$OUT/r5_host_read_numa_bound2.jsonl"
       run numa_bound_4m_b 600 python tools/worker_bench_host.py --threads 64 --transports ipc --duration 6s --warmup 2s --client-procs 4 --d2h-roof --bind-gpu-node --reader-buffer 4MB --out "$OUT/r5_host_read_numa_bound2.jsonl"
       ;;
+    ctshm)
+      run ww_ct_shm 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --work-dir /dev/shm --out "$OUT/r5_worker_write_cache_through_shm.jsonl"
+      run ww_th_shm 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type THROUGH --bind-gpu-node --work-dir /dev/shm --out "$OUT/r5_worker_write_cache_through_shm.jsonl"
+      ;;
     roof)
       run copy_roof 300 python tools/copy_roof.py --gib 4 --out "$OUT/r5_copy_roof.json"
       ;;

@@ -80,6 +80,8 @@ def main(argv=None) -> int:
                     "(the UFS is a local directory under the work dir)")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--worker-prop", action="append", default=[], help="extra worker property k=v")
+    ap.add_argument("--work-dir", default=None,
+                    help="cluster work dir (the UFS lives under it), e.g. on /dev/shm to take the disk out")
     ap.add_argument("--bind-gpu-node", action="store_true",
                     help="run the worker (this process) and the client on the CPUs of the GPU's NUMA node")
     ap.add_argument("--out", default=None)
@@ -109,7 +111,7 @@ def main(argv=None) -> int:
             "alluxio.security.authorization.permission.enabled": "false",
             "alluxio.worker.tieredstore.dram.prefault": str(a.write_type != "THROUGH").lower()}
     conf.update(dict(kv.split("=", 1) for kv in a.worker_prop))
-    work = tempfile.mkdtemp(prefix="wwbench_")
+    work = tempfile.mkdtemp(prefix="wwbench_", dir=a.work_dir)
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=work) as c:
         time.sleep(min(10.0, total / 4e9))     # let the DRAM prefault finish (no-op on HBM)
         runs = [(tr, t) for tr in a.transports.split(",") for t in a.threads.split(",")]
@@ -139,7 +141,7 @@ def main(argv=None) -> int:
                    # worker process CPU by thread group during the run (approx: whole subprocess
                    # lifetime / timed window), and the client's own CPU over its timed window
                    "worker_thread_cores": worker_threads, "client_cpu_cores": r.get("client_cpu_cores"),
-                   "bound_to_gpu_node": bool(cpus)}
+                   "bound_to_gpu_node": bool(cpus), "work_dir": work}
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
@@ -149,6 +151,9 @@ def main(argv=None) -> int:
             for st in fs.list_status("/ww"):
                 fs.delete(st.path)
             fs.close()
+    if a.work_dir:
+        import shutil
+        shutil.rmtree(work, ignore_errors=True)
     return 0
 
 
