@@ -26,6 +26,7 @@ import queue
 import random
 import sys
 import threading
+import time
 
 import numpy as np
 
@@ -412,7 +413,7 @@ class FileInStream(io.RawIOBase):
         if self.length > 0 and ctx.conf.get_bool("alluxio.user.native.reader.enabled", "true"):
             from ..ops.native import lib
             self._nat = lib().HostInStream(self.length, self.block_size,
-                                           ctx.conf.get_bytes("alluxio.user.native.reader.buffer.size", "1MB"),
+                                           ctx.conf.get_bytes("alluxio.user.native.reader.buffer.size", "4MB"),
                                            _native_opener(self),
                                            ctx.conf.get_bool("alluxio.user.native.reader.prefetch.enabled", "true"))
             # instance attribute: read(buf) loops call the C entry point directly
@@ -1148,8 +1149,12 @@ class FileOutStream(io.RawIOBase):
         if cs is None:
             return False
         from ..ops.native import lib, native_errors
+        from ..utils import optiming
+        t0 = time.perf_counter() if optiming.ENABLED else 0.0
         with native_errors():
             lib().sink_write_pair(cs, us, ptr, n)
+        if optiming.ENABLED:
+            optiming.add("client.pair_write", time.perf_counter() - t0)
         self._ufs.length += n
         self._block_written += n
         return True
@@ -1232,9 +1237,15 @@ class FileOutStream(io.RawIOBase):
         return len(opened) * bs
 
     def _next_block(self) -> None:
+        from ..utils import optiming
+        t0 = time.perf_counter() if optiming.ENABLED else 0.0
         self._finish_block()
+        t1 = time.perf_counter() if optiming.ENABLED else 0.0
         bid, self._writers, self._fanout = self._open_writers()
         self._block_written = 0
+        if optiming.ENABLED:
+            optiming.add("client.finish_block", t1 - t0)
+            optiming.add("client.open_writers", time.perf_counter() - t1)
 
     def _open_writers(self):
         """Allocates the file's next block id and opens its writer(s): (id, writers, same-node
@@ -1377,16 +1388,24 @@ class FileOutStream(io.RawIOBase):
             self.cancel()
             raise IOError(f"output stream of {self.path} failed; the file was cancelled: {err}") from err
         self._stop_beside()
+        from ..utils import optiming
         try:
+            t0 = time.perf_counter() if optiming.ENABLED else 0.0
             self._finish_block()
             self._wait_fanouts()
+            t1 = time.perf_counter() if optiming.ENABLED else 0.0
             opts = pb.file.CompleteFilePOptions()
             if self._ufs is not None:
                 self._ufs.close()
                 opts.ufsLength = self._ufs.length
+            t2 = time.perf_counter() if optiming.ENABLED else 0.0
             if self.write_type == "ASYNC_THROUGH":
                 opts.asyncPersistOptions.persistenceWaitTime = self.persistence_wait_ms
             self.ctx.fs_master().CompleteFile(pb.file.CompleteFilePRequest(path=self.path, options=opts))
+            if optiming.ENABLED:
+                optiming.add("client.close.finish_block", t1 - t0)
+                optiming.add("client.close.ufs_commit", t2 - t1)
+                optiming.add("client.close.complete_file", time.perf_counter() - t2)
         except Exception:
             for w in self._writers:
                 w.cancel()

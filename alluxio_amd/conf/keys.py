@@ -263,8 +263,11 @@ _k("WORKER_TIEREDSTORE_DRAM_PREFAULT", "alluxio.worker.tieredstore.dram.prefault
    "Populate the pages of DRAM-tier arenas in the background at startup (GPU hosts pin, and so "
    "populate, them anyway): first writes into a shared-memory page otherwise pay a fault that "
    "allocates and zeroes it.")
-_k("USER_NATIVE_READER_BUFFER_SIZE", "alluxio.user.native.reader.buffer.size", "1MB", Scope.CLIENT,
-   "Chunk buffer (pinned when a GPU is present) of the native host reader: bytes fetched per refill.")
+_k("USER_NATIVE_READER_BUFFER_SIZE", "alluxio.user.native.reader.buffer.size", "4MB", Scope.CLIENT,
+   "Chunk buffer (pinned when a GPU is present) of the native host reader: bytes fetched per refill. "
+   "4 MiB: short-circuit readers in 4 processes x 64 threads reach 81-84% of the same-run D2H copy roof "
+   "(1 MiB: 21-33% when the processes share the GPU's NUMA node -- 4x the refill syncs; "
+   "profiles/r5_host_read_numa.md).")
 _k("USER_NATIVE_READER_PREFETCH_ENABLED", "alluxio.user.native.reader.prefetch.enabled", "true", Scope.CLIENT,
    "The native host reader fetches the next chunk of the block into its second buffer on a native "
    "thread pool while read(buf) calls drain the current one.")

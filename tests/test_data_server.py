@@ -253,7 +253,11 @@ def test_cancelled_stream_releases_the_block_lock(tmp_path):
 def test_in_process_host_reads_use_store_source(tmp_path):
     """An in-process worker: host read(buf) goes through the chunk buffer filled from the store."""
     with _cluster(tmp_path) as c:
-        fs = c.client()
+        from alluxio_amd.client.file_system import FileSystem
+        from alluxio_amd.conf import Configuration
+        # 1 MiB chunks: several refills per block, so read-ahead inside a block is visible
+        fs = FileSystem(conf=Configuration({"alluxio.user.native.reader.buffer.size": "1MB"}),
+                        master_address=c.master.address)
         data = np.random.default_rng(7).integers(0, 256, (9 << 20) + 5, dtype=np.uint8)
         fs.write_file("/p", data, write_type="MUST_CACHE")
         with fs.open_file("/p") as f:

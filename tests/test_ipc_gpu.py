@@ -73,7 +73,7 @@ def test_ipc_read_from_other_process(gpu, tmp_path):
                     break
                 parts.append(bytes(b[:n]))
             assert f._nreader is not None and f._nreader.source == "ipc"
-            assert f._nat.refills >= 20
+            assert f._nat.refills >= len(expect) // (4 << 20)   # 4 MiB chunks (reader buffer default)
         assert b"".join(parts) == expect.tobytes()
         # short-circuit writes into the worker's HBM arena (OpenDeviceWrite + ArenaSink: pinned
         # staging, H2D DMA into the IPC-mapped pages), from host memory and from a device tensor

@@ -219,6 +219,10 @@ for s in $STEPS; do
       run ww_ct_shm 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --work-dir /dev/shm --out "$OUT/r5_worker_write_cache_through_shm.jsonl"
       run ww_th_shm 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type THROUGH --bind-gpu-node --work-dir /dev/shm --out "$OUT/r5_worker_write_cache_through_shm.jsonl"
       ;;
+    cttiming)
+      run ww_ct_timing 600 python tools/worker_write_bench.py --threads 4,8,16 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --client-timing "$PWD/$OUT/ct_timing" --out "$OUT/r5_worker_write_ct_timing.jsonl"
+      run ww_mc_timing 600 python tools/worker_write_bench.py --threads 4,8,16 --file-size 256m --write-type MUST_CACHE --bind-gpu-node --client-timing "$PWD/$OUT/ct_timing" --out "$OUT/r5_worker_write_ct_timing.jsonl"
+      ;;
     roof)
       run copy_roof 300 python tools/copy_roof.py --gib 4 --out "$OUT/r5_copy_roof.json"
       ;;

@@ -86,7 +86,7 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", default="3s")
     ap.add_argument("--transports", default="grpc,ipc")
     ap.add_argument("--tier", default="hbm:0", help="worker MEM tier dir (hbm:N or dram)")
-    ap.add_argument("--reader-buffer", default="1MB", help="alluxio.user.native.reader.buffer.size")
+    ap.add_argument("--reader-buffer", default="4MB", help="alluxio.user.native.reader.buffer.size")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--client-procs", type=int, default=1,
                     help="spread the threads over this many client processes (the reference's --clients "

@@ -82,6 +82,8 @@ def main(argv=None) -> int:
     ap.add_argument("--worker-prop", action="append", default=[], help="extra worker property k=v")
     ap.add_argument("--work-dir", default=None,
                     help="cluster work dir (the UFS lives under it), e.g. on /dev/shm to take the disk out")
+    ap.add_argument("--client-timing", default=None,
+                    help="per-phase client timing (optiming JSON, one file per run: <path>.<run>)")
     ap.add_argument("--bind-gpu-node", action="store_true",
                     help="run the worker (this process) and the client on the CPUs of the GPU's NUMA node")
     ap.add_argument("--out", default=None)
@@ -123,10 +125,13 @@ def main(argv=None) -> int:
             sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
             from _threadcpu import busy, thread_cpu
             tc0, tw0 = thread_cpu(), time.perf_counter()
+            cenv = dict(os.environ)
+            if a.client_timing:
+                cenv["ALLUXIO_MASTER_OP_TIMING"] = f"{a.client_timing}.{a.write_type}.t{t}"
             p = subprocess.run([sys.executable, "-c", CLIENT.format(
                 root=ROOT, props=props, addr=c.master.address, size=size, nfiles=a.files, threads=int(t),
                 wsize=parse_space_size(a.write_size), tag=f"r{i}", wtype=a.write_type, cpus=cpus)],
-                capture_output=True, text=True, timeout=900)
+                capture_output=True, text=True, timeout=900, env=cenv)
             line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
             if line is None:
                 print(p.stdout[-2000:], p.stderr[-3000:], file=sys.stderr)
