@@ -1103,8 +1103,23 @@ void FrameRpcServer::add_conn(int fd, bool unix_peer) {
     std::shared_ptr<Conn> c;
     {
       std::lock_guard<std::mutex> g(conns_mu_);
-      uint32_t id = next_conn_++;
+      // the I/O thread with the fewest live connections takes it (round robin skews under churn:
+      // every block a client writes opens a connection, and two busy streams on one thread halve
+      // both); the id is picked so that id % threads names that thread (wake() and close_conn
+      // find the thread from the id)
+      const uint32_t nt = (uint32_t)epolls_.size();
+      if (ep_conns_.size() != nt) ep_conns_.assign(nt, 0);
+      uint32_t target = next_conn_ % nt;
+      for (uint32_t k = 0; k < nt; ++k) {
+        const uint32_t j = (next_conn_ + k) % nt;
+        if (ep_conns_[j] < ep_conns_[target]) target = j;
+      }
+      uint32_t id = next_conn_ + (target + nt - next_conn_ % nt) % nt;
+      if (id == 0) id = nt + target;                 // 0 marks the wake eventfd
+      while (conns_.count(id)) id += nt;             // after a wrap: skip ids still in use
+      next_conn_ = id + 1;
       if (next_conn_ == 0) next_conn_ = 1;
+      ++ep_conns_[id % nt];
       c = std::make_shared<Conn>(fd, id);
       c->unix_peer = unix_peer;
       c->ep = epolls_[id % epolls_.size()];
@@ -1131,6 +1146,7 @@ void FrameRpcServer::close_conn(uint32_t id) {
     if (it == conns_.end()) return;
     c = it->second;
     conns_.erase(it);
+    if (!ep_conns_.empty() && ep_conns_[id % ep_conns_.size()] > 0) --ep_conns_[id % ep_conns_.size()];
   }
   c->closed = true;
   ::epoll_ctl(epolls_[id % epolls_.size()], EPOLL_CTL_DEL, c->fd, nullptr);

@@ -193,6 +193,7 @@ class FrameRpcServer {
   std::vector<int> lanes_;
   int nthreads_;
   std::vector<int> epolls_;
+  std::vector<uint32_t> ep_conns_;   // live connections per I/O thread (under conns_mu_)
   std::vector<std::thread> threads_;
   std::thread acceptor_;
   std::atomic<bool> running_{false};
