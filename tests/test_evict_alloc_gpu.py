@@ -398,3 +398,52 @@ def test_magazine_accounting_mixed_workload(gpu, tmp_path):
         s.read_batch([(b, 0, d.nbytes, out.data_ptr(), 1)], 0, True)
         assert np.array_equal(out[:d.nbytes].cpu().numpy(), d), b
     assert s.evict_stats()["device_alloc_pages"] > 0
+
+
+def test_tier_moves_between_hbm_and_mapped_dram_are_byte_exact(gpu):
+    """Tier moves between an HBM arena and a GPU-mapped (hipHostRegister) DRAM arena run as one
+    batched copy kernel per move on the caller's move stream (not runtime copyBuffer per page
+    run); demoted and promoted-back blocks keep their bytes, including a partial last page."""
+    import torch
+    C = lib()
+    page = 64 * KB
+    dev = torch.empty(64 * page, dtype=torch.uint8, device="cuda")
+    host = np.zeros(256 * page, dtype=np.uint8)
+    assert C.host_register(host.ctypes.data, host.nbytes)
+    try:
+        specs = []
+        for tier, (base, cap, kind, medium) in enumerate([(dev.data_ptr(), dev.numel(), C.DirKind.DEVICE, "HBM"),
+                                                          (host.ctypes.data, host.nbytes, C.DirKind.HOST, "DRAM")]):
+            d = C.DirSpec()
+            d.tier, d.tier_alias, d.medium, d.kind = tier, ("MEM", "SSD")[tier], medium, kind
+            d.base, d.capacity, d.page_size, d.device = base, cap, page, 0
+            specs.append(d)
+        s = C.BlockStore(specs, annotator=0, alloc_policy=0, device=0)
+        rng = np.random.default_rng(31)
+        src = torch.empty(4 * page, dtype=torch.uint8).pin_memory()
+        blobs = {}
+        ids = list(range(1, 9))
+        for b in ids:
+            n = 4 * page - (b * 777 if b % 2 else 0)          # odd blocks end mid-page
+            data = rng.integers(0, 256, n, dtype=np.uint8)
+            src[:n].copy_(torch.from_numpy(data))
+            s.create_block(5, b, 0, "", n)
+            s.write(5, b, 0, src.data_ptr(), n, 0)
+            s.commit_block(5, b)
+            blobs[b] = data
+        before = s.evict_stats()["batched_moves"]
+        moved = s.move_blocks(5, ids[:5], 1)
+        assert sorted(moved) == ids[:5]
+        assert all(s.block_info(b).tier == 1 for b in ids[:5])
+        back = s.move_blocks(5, ids[:3], 0)
+        assert sorted(back) == ids[:3]
+        out = torch.empty(4 * page, dtype=torch.uint8).pin_memory()
+        for b in ids:
+            n = len(blobs[b])
+            out.zero_()
+            s.read(b, 0, n, out.data_ptr(), 0)
+            assert np.array_equal(out[:n].numpy(), blobs[b]), b
+        assert s.evict_stats()["batched_moves"] >= before + 2
+        del s
+    finally:
+        C.host_unregister(host.ctypes.data)
