@@ -223,6 +223,16 @@ for s in $STEPS; do
       run ww_ct_timing 600 python tools/worker_write_bench.py --threads 4,8,16 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --client-timing "$PWD/$OUT/ct_timing" --out "$OUT/r5_worker_write_ct_timing.jsonl"
       run ww_mc_timing 600 python tools/worker_write_bench.py --threads 4,8,16 --file-size 256m --write-type MUST_CACHE --bind-gpu-node --client-timing "$PWD/$OUT/ct_timing" --out "$OUT/r5_worker_write_ct_timing.jsonl"
       ;;
+    ctfinal)
+      run ww_ct_final 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type CACHE_THROUGH --client-timing "$PWD/$OUT/ct_timing" --out "$OUT/r5_worker_write_cache_through_final.jsonl"
+      run ww_mc_final 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type MUST_CACHE --out "$OUT/r5_worker_write_cache_through_final.jsonl"
+      ;;
+    final)
+      run pytest_gpu_final 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+      run smoke_final 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"
+      run bench_final 400 python bench.py
+      run wb_host_sweep_final 900 python tools/worker_bench_host.py --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --out "$OUT/r5_worker_bench_host_sweep.jsonl"
+      ;;
     roof)
       run copy_roof 300 python tools/copy_roof.py --gib 4 --out "$OUT/r5_copy_roof.json"
       ;;
