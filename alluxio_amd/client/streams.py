@@ -836,6 +836,7 @@ class GrpcBlockWriter(BlockWriter):
                  chunk: int | None = None, ufs_fallback_mount: int | None = None, data_address: tuple | None = None):
         self.chunk = chunk or ctx.conf.get_bytes("alluxio.user.network.writer.chunk.size.bytes", "1MB")
         self._sink = None
+        self.address = address
         if ufs_fallback_mount is None and ctx.conf.get_bool("alluxio.user.native.writer.enabled", "true"):
             # the same WriteBlock call made by the native gRPC client (csrc/block_source.cpp
             # GrpcBlockSink): chunks framed around the caller's bytes, GIL released while sending
@@ -938,6 +939,7 @@ class UfsWriter:
 
     def __init__(self, ctx, status, worker_addr=None, local_worker=None, worker=None):
         self.length = 0
+        self.worker_addr = worker_addr
         self._local = None
         self._grpc = None
         self._sink = None
@@ -994,6 +996,14 @@ class UfsWriter:
             mv = memoryview(data)
             for i in range(0, n, 1 << 20):
                 self._q.put(marshal.write_request_frame(mv[i:i + (1 << 20)]))
+
+    def append_block(self, block_id: int, length: int) -> None:
+        """The next ``length`` bytes of the file are block ``block_id``, which this stream's
+        worker holds: the worker copies them from its store (CACHE_THROUGH tee)."""
+        from ..ops.native import native_errors
+        with native_errors():
+            self._sink.append_block(block_id, length)
+        self.length += length
 
     def close(self) -> None:
         if self._local is not None:
@@ -1074,6 +1084,11 @@ class FileOutStream(io.RawIOBase):
         self._overlap_min = ctx.conf.get_bytes("alluxio.user.file.cache.through.overlap.min", "256KB")
         self._ct_counted = False
         self._canceled = False
+        self._tee_block = False      # CACHE_THROUGH: the current block's UFS bytes come from the worker
+        self._tee = ctx.conf.get_bool("alluxio.user.file.cache.through.tee.enabled", "true")
+        up = status.ufsPath or ""
+        if "://" in up and not up.startswith("file://"):
+            self._tee = False        # object stores: the worker streams parts of the bytes it receives
         self._failed: BaseException | None = None    # a parallel block write failed: no completion
         self._workers = None
         if self.through:
@@ -1106,6 +1121,9 @@ class FileOutStream(io.RawIOBase):
                 host = keep.detach().reshape(-1).view(torch.uint8).cpu().numpy()
             else:
                 host = _host_view(ptr, n)        # zero-copy view of the caller's buffer
+            if self.cache and self._tee_write(ptr, n, kind):
+                self._pos += n
+                return n
             if self.cache and kind != DEVICE and self._pair_write(ptr, n):
                 self._pos += n
                 return n
@@ -1131,6 +1149,37 @@ class FileOutStream(io.RawIOBase):
             self._write_cache(ptr, n, kind)
         self._pos += n
         return n
+
+    def _tee_eligible(self) -> bool:
+        """The current block goes to exactly one native block stream on the worker that also runs
+        this file's native UFS stream: its UFS bytes can be copied by that worker."""
+        if len(self._writers) != 1:
+            return False
+        w = self._writers[0]
+        return (isinstance(w, GrpcBlockWriter) and w._sink is not None
+                and getattr(self._ufs, "_sink", None) is not None and w.address == self._ufs.worker_addr)
+
+    def _tee_write(self, ptr: int, n: int, kind) -> bool:
+        """CACHE_THROUGH with the cache block and the UFS file on one worker: the bytes travel
+        once, to the block stream; when the block is committed the UFS stream is told to append it
+        (``AppendBlock``) and the worker copies it from its store into the file.  Blocks that are
+        not eligible (another worker, replicas, an in-process worker) take the general path."""
+        if not self._tee or self.replicas != 1 or getattr(self._ufs, "_sink", None) is None:
+            return False
+        done = 0
+        while done < n:
+            if not self._writers or self._block_written >= self.block_size:
+                self._next_block()
+            if not self._tee_block:
+                if done == 0:
+                    return False             # this block takes the general path
+                # (cannot happen mid-call: eligibility is fixed per block and checked at its start)
+                raise IOError("CACHE_THROUGH tee changed within one write")
+            take = min(n - done, self.block_size - self._block_written)
+            self._writers[0].write_ptr(self._block_written, ptr + done, take, kind)
+            self._block_written += take
+            done += take
+        return True
 
     def _pair_write(self, ptr: int, n: int) -> bool:
         """CACHE_THROUGH host write inside one block whose cache writer and UFS writer are both
@@ -1243,6 +1292,8 @@ class FileOutStream(io.RawIOBase):
         t1 = time.perf_counter() if optiming.ENABLED else 0.0
         bid, self._writers, self._fanout = self._open_writers()
         self._block_written = 0
+        self._tee_block = bool(self.through and self.cache and self._tee and self._ufs is not None
+                               and self.replicas == 1 and self._tee_eligible())
         if optiming.ENABLED:
             optiming.add("client.finish_block", t1 - t0)
             optiming.add("client.open_writers", time.perf_counter() - t1)
@@ -1317,6 +1368,10 @@ class FileOutStream(io.RawIOBase):
         for w in self._writers:
             w.commit()
         had = bool(self._writers)
+        if had and self._tee_block and self._block_written:
+            # committed on the worker that runs the UFS stream: it appends the block to the file
+            self._ufs.append_block(self._block_id, self._block_written)
+        self._tee_block = False
         self._writers = []
         if had and self._fanout:
             # replicas pull the committed block while this stream writes the next one (the pulls

@@ -238,6 +238,10 @@ _k("WORKER_DATA_SERVER_NATIVE_UFS_READ_ENABLED", "alluxio.worker.data.server.nat
    "into a temp block and the I/O thread streams it as it lands; the block is committed at the end.")
 _k("WORKER_DATA_SERVER_NATIVE_UFS_READ_MAX_ACTIVE", "alluxio.worker.data.server.native.ufs.read.max.active",
    "256", Scope.WORKER, "Concurrent native cold reads (one UFS reader thread each); more go to Python.")
+_k("USER_FILE_CACHE_THROUGH_TEE_ENABLED", "alluxio.user.file.cache.through.tee.enabled", "true", Scope.CLIENT,
+   "CACHE_THROUGH writes whose cache block and UFS file stream go to the same worker send each byte "
+   "once (to the block stream); after the block commits, the UFS stream is told to append it and the "
+   "worker copies it from its store (AppendBlock).  false = every byte is sent to both streams.")
 _k("MASTER_JOURNAL_NATIVE_WRITER_ENABLED", "alluxio.master.journal.native.writer.enabled", "true",
    Scope.MASTER,
    "UFS journal logs are written by the native group-commit writer (csrc/journal_log.cpp): a C++ "

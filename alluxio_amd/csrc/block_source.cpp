@@ -1037,6 +1037,27 @@ void GrpcBlockSink::write(const uint8_t* p, uint64_t n) {
   written_ += n;
 }
 
+void GrpcBlockSink::append_block(int64_t block_id, uint64_t length) {
+  if (!c_ || c_->closing) throw StoreError(kErrInvalidState, "append after commit/cancel");
+  // WriteRequest{append_block(20){block_id(1), length(2)}}
+  std::string inner;
+  h2::put_varint(inner, (1u << 3));
+  h2::put_varint(inner, (uint64_t)block_id);
+  h2::put_varint(inner, (2u << 3));
+  h2::put_varint(inner, length);
+  std::string msg;
+  h2::put_varint(msg, (20u << 3) | 2);
+  h2::put_varint(msg, inner.size());
+  msg += inner;
+  Conn::Seg s;
+  s.hdr.push_back('\0');
+  h2::put_be32(s.hdr, (uint32_t)msg.size());
+  s.hdr += msg;
+  c_->q.push_back(std::move(s));
+  wait_drained();
+  written_ += length;
+}
+
 uint64_t GrpcBlockSink::commit() {
   if (!c_) throw StoreError(kErrInvalidState, "commit after cancel");
   Conn& c = *c_;

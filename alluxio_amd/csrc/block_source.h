@@ -167,6 +167,9 @@ class GrpcBlockSink {
   ~GrpcBlockSink();
   // Streams n bytes; returns once they are in the socket (flow control permitting).
   void write(const uint8_t* p, uint64_t n);
+  // UFS_FILE streams: the next `length` bytes of the file are block `block_id`, which the same
+  // worker already holds (CACHE_THROUGH tee: the worker copies them from its store).
+  void append_block(int64_t block_id, uint64_t length);
   // Half-closes and waits for the worker's commit; returns the committed length.
   uint64_t commit();
   void cancel();

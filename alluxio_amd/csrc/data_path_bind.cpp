@@ -339,6 +339,16 @@ void bind_data_path(py::module_& m) {
                throw StoreError(kErrIo, e.what());
              }
            }, py::arg("ptr"), py::arg("n"))
+      .def("append_block", [](GrpcBlockSink& s, int64_t block_id, uint64_t length) {
+             py::gil_scoped_release rel;
+             try {
+               s.append_block(block_id, length);
+             } catch (const StoreError&) {
+               throw;
+             } catch (const std::exception& e) {
+               throw StoreError(kErrIo, e.what());
+             }
+           }, py::arg("block_id"), py::arg("length"))
       .def("commit", [](GrpcBlockSink& s) {
              py::gil_scoped_release rel;
              try {
@@ -448,7 +458,8 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("cold_bytes", [](const DataServerStats& s) { return s.cold_bytes.load(); })
       .def_property_readonly("cold_active", [](const DataServerStats& s) { return s.cold_active.load(); })
       .def_property_readonly("prefetched", [](const DataServerStats& s) { return s.prefetched.load(); })
-      .def_property_readonly("zero_copy_frames", [](const DataServerStats& s) { return s.zero_copy_frames.load(); });
+      .def_property_readonly("zero_copy_frames", [](const DataServerStats& s) { return s.zero_copy_frames.load(); })
+      .def_property_readonly("ufs_tee_bytes", [](const DataServerStats& s) { return s.ufs_tee_bytes.load(); });
   auto mounts = py::class_<UfsMounts, std::shared_ptr<UfsMounts>>(m, "UfsMounts")
       .def(py::init<>())
       .def("set", &UfsMounts::set, py::arg("mount_id"), py::arg("root"))

@@ -910,16 +910,39 @@ bool parse_write_command(const uint8_t* p, size_t n, WriteCmd* c) {
 
 // Splits one WriteRequest into its command (if any) and its chunk bytes (pointer into `data`).
 bool parse_write_request(const char* data, size_t n, WriteCmd* cmd, bool* has_cmd, const uint8_t** chunk,
-                         size_t* chunk_len) {
+                         size_t* chunk_len, int64_t* append_id = nullptr, uint64_t* append_len = nullptr) {
   const uint8_t* p = reinterpret_cast<const uint8_t*>(data);
   size_t i = 0;
   *has_cmd = false;
   *chunk = nullptr;
   *chunk_len = 0;
+  if (append_id) *append_id = -1;
   while (i < n) {
     uint64_t key;
     if (!h2::get_varint(p, n, &i, &key)) return false;
     const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (wt == 2 && field == 20 && append_id) {       // AppendBlock{block_id=1, length=2}
+      uint64_t len;
+      if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
+      size_t j = i;
+      const size_t end = i + (size_t)len;
+      uint64_t id = 0, ln = 0;
+      while (j < end) {
+        uint64_t k2, v;
+        if (!h2::get_varint(p, end, &j, &k2)) return false;
+        if ((k2 & 7) != 0) {
+          if (!skip_field(p, end, &j, (uint32_t)(k2 & 7))) return false;
+          continue;
+        }
+        if (!h2::get_varint(p, end, &j, &v)) return false;
+        if ((k2 >> 3) == 1) id = v;
+        else if ((k2 >> 3) == 2) ln = v;
+      }
+      *append_id = (int64_t)id;
+      *append_len = ln;
+      i = end;
+      continue;
+    }
     if (wt == 2 && (field == 1 || field == 2)) {
       uint64_t len;
       if (!h2::get_varint(p, n, &i, &len) || len > n - i) return false;
@@ -1224,8 +1247,24 @@ struct LocalFileJob {
   int mode = 0644;
   int fd = -1;
   std::mutex mu;
-  std::deque<std::string> chunks;
+  struct Item {
+    std::string data;                 // received bytes, or
+    int64_t block = -1;               // a block this worker holds (CACHE_THROUGH tee)
+    uint64_t len = 0;
+  };
+  std::deque<Item> chunks;
   uint64_t queued = 0, written = 0;   // bytes
+  BlockStore* store = nullptr;        // source of appended blocks
+  int64_t session = 0;
+  uint8_t* tee_buf = nullptr;
+  bool tee_pinned = false;
+
+  ~LocalFileJob() {
+    if (tee_buf) {
+      if (tee_pinned) (void)hipHostFree(tee_buf);
+      else std::free(tee_buf);
+    }
+  }
   bool running = false, opened = false, failed = false, cancelled = false;
   bool end = false, finished = false, cleaned = false;
   int err_status = 0;
@@ -1282,9 +1321,65 @@ struct LocalFileJob {
   }
 
   // One pool task: open (first time), write queued chunks in order, and on the end chmod + rename.
+  // Appends block `id` ([0, n) of it) from the store: read-locked, copied out in 8 MiB pieces
+  // through one pinned buffer (a DMA when the block sits in HBM), each piece written to the file.
+  int append_block(int64_t id, uint64_t n, std::string* what) {
+    if (!store) {
+      *what = "no block store for an appended block";
+      return EINVAL;
+    }
+    int64_t lock = -1;
+    try {
+      lock = store->lock_block(session, id, false, 30000);
+    } catch (const std::exception& e) {
+      *what = std::string("appending block ") + std::to_string(id) + ": " + e.what();
+      return ENOENT;
+    }
+    if (lock < 0) {
+      *what = "appending block " + std::to_string(id) + ": lock timed out";
+      return ETIMEDOUT;
+    }
+    constexpr uint64_t kPiece = 8ull << 20;
+    if (!tee_buf) {                    // one pinned piece buffer per stream, kept for its blocks
+      tee_buf = static_cast<uint8_t*>(pinned_alloc_near(kPiece, store->device()));
+      tee_pinned = tee_buf != nullptr;
+      if (!tee_buf) tee_buf = static_cast<uint8_t*>(std::malloc(kPiece));
+    }
+    uint8_t* buf = tee_buf;
+    int e = 0;
+    try {
+      for (uint64_t off = 0; off < n && !e;) {
+        const uint64_t k = std::min(kPiece, n - off);
+        std::vector<ReadReq> rq{ReadReq{id, off, k, reinterpret_cast<uint64_t>(buf), (int)MemKind::kHost}};
+        store->read_batch(rq, 0, true);
+        size_t done = 0;
+        while (done < k) {
+          const ssize_t w = ::write(fd, buf + done, (size_t)(k - done));
+          if (w < 0) {
+            if (errno == EINTR) continue;
+            e = errno;
+            *what = "writing " + path;
+            break;
+          }
+          done += (size_t)w;
+        }
+        off += k;
+      }
+    } catch (const std::exception& x) {
+      e = EIO;
+      *what = std::string("appending block ") + std::to_string(id) + ": " + x.what();
+    }
+    try {
+      store->unlock(lock);
+    } catch (...) {
+    }
+    return e;
+  }
+
   static void drain(std::shared_ptr<LocalFileJob> j) {
     for (;;) {
-      std::string c;
+      Item it;
+      bool have = false;
       bool do_open, do_end, stop;
       {
         std::lock_guard<std::mutex> g(j->mu);
@@ -1292,10 +1387,11 @@ struct LocalFileJob {
         do_open = !stop && !j->opened;
         do_end = !stop && j->chunks.empty() && j->end && !j->finished;
         if (!stop && !do_open && !j->chunks.empty()) {
-          c = std::move(j->chunks.front());
+          it = std::move(j->chunks.front());
           j->chunks.pop_front();
+          have = true;
         }
-        if (stop || (!do_open && !do_end && c.empty())) {
+        if (stop || (!do_open && !do_end && !have)) {
           if (stop) j->cleanup();
           j->running = false;
           break;
@@ -1305,7 +1401,23 @@ struct LocalFileJob {
         j->open_file();
         continue;
       }
-      if (!c.empty()) {
+      if (have && it.block >= 0) {
+        std::string what;
+        const int e = j->append_block(it.block, it.len, &what);
+        std::lock_guard<std::mutex> g(j->mu);
+        if (e) {
+          if (!j->failed) {
+            j->failed = true;
+            j->err_status = grpc_status_of_errno(e);
+            j->err = what + ": " + std::strerror(e);
+          }
+        } else {
+          j->written += it.len;
+        }
+        if (!e) j->stats->ufs_write_bytes.fetch_add(it.len, std::memory_order_relaxed);
+        if (!e) j->stats->ufs_tee_bytes.fetch_add(it.len, std::memory_order_relaxed);
+      } else if (have) {
+        const std::string& c = it.data;
         size_t done = 0;
         int e = 0;
         while (done < c.size()) {
@@ -1346,11 +1458,14 @@ class UfsFileWriteStream : public WriteStreamBase {
  public:
   static constexpr uint64_t kMaxQueued = 32ull << 20;
 
-  UfsFileWriteStream(const std::string& path, int mode, std::shared_ptr<DataServerStats> stats)
+  UfsFileWriteStream(const std::string& path, int mode, std::shared_ptr<DataServerStats> stats,
+                     BlockStore* store = nullptr)
       : j_(std::make_shared<LocalFileJob>()) {
     j_->path = path;
     j_->mode = mode;
     j_->stats = std::move(stats);
+    j_->store = store;
+    j_->session = g_session.fetch_add(1);
   }
 
   // Queues the open (parents + temp file) on the file pool; errors surface on the stream.
@@ -1390,14 +1505,30 @@ class UfsFileWriteStream : public WriteStreamBase {
     bool has_cmd;
     const uint8_t* chunk;
     size_t len;
-    if (!parse_write_request(p, n, &cmd, &has_cmd, &chunk, &len)) {
+    int64_t append_id = -1;
+    uint64_t append_len = 0;
+    if (!parse_write_request(p, n, &cmd, &has_cmd, &chunk, &len, &append_id, &append_len)) {
       fail(3, "malformed WriteRequest");
       return;
+    }
+    if (append_id >= 0) {              // CACHE_THROUGH tee: the next bytes are a block we hold
+      {
+        std::lock_guard<std::mutex> g(j_->mu);
+        LocalFileJob::Item it;
+        it.block = append_id;
+        it.len = append_len;
+        j_->chunks.push_back(std::move(it));
+        j_->queued += append_len;
+      }
+      kick();
+      pos_ += append_len;
     }
     if (len) {
       {
         std::lock_guard<std::mutex> g(j_->mu);
-        j_->chunks.emplace_back(reinterpret_cast<const char*>(chunk), len);
+        LocalFileJob::Item it;
+        it.data.assign(reinterpret_cast<const char*>(chunk), len);
+        j_->chunks.push_back(std::move(it));
         j_->queued += len;
       }
       kick();
@@ -1693,8 +1824,14 @@ class S3UfsWriteStream : public WriteStreamBase {
     bool has_cmd;
     const uint8_t* chunk;
     size_t len;
-    if (!parse_write_request(p, n, &cmd, &has_cmd, &chunk, &len)) {
+    int64_t append_id = -1;
+    uint64_t append_len = 0;
+    if (!parse_write_request(p, n, &cmd, &has_cmd, &chunk, &len, &append_id, &append_len)) {
       fail(3, "malformed WriteRequest");
+      return;
+    }
+    if (append_id >= 0) {              // never sent for object stores: refuse rather than drop bytes
+      fail(12, "AppendBlock is not supported by the S3 UFS stream");
       return;
     }
     if (len) {
@@ -2118,7 +2255,7 @@ void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_me
     }
     if (cmd.type == 1 && cmd.has_ufs_file && ufs_roots && ufs_roots->resolve(cmd.ufs_mount, cmd.ufs_path, &local)) {
       auto us = std::unique_ptr<UfsFileWriteStream>(
-          new UfsFileWriteStream(local, cmd.ufs_mode > 0 ? (int)(cmd.ufs_mode & 07777) : 0644, stats));
+          new UfsFileWriteStream(local, cmd.ufs_mode > 0 ? (int)(cmd.ufs_mode & 07777) : 0644, stats, store));
       if (!us->open(status, msg)) return nullptr;
       stats->ufs_write_streams.fetch_add(1, std::memory_order_relaxed);
       if (len) us->on_message(first.data(), first.size());

@@ -20,7 +20,8 @@ msg WriteRequestCommand type=1:RequestType id=2:i64 offset=3:i64 tier=4:i32 flus
     create_ufs_file_options=6:alluxio.proto.dataserver.CreateUfsFileOptions
     create_ufs_block_options=7:alluxio.proto.dataserver.CreateUfsBlockOptions
     medium_type=8:str pin_on_create=9:bool space_to_reserve=10:i64
-msg WriteRequest command=1:WriteRequestCommand|value chunk=2:Chunk|value
+msg AppendBlock block_id=1:i64 length=2:i64
+msg WriteRequest command=1:WriteRequestCommand|value chunk=2:Chunk|value append_block=20:AppendBlock|value
 msg WriteResponse offset=1:i64
 msg NativeWriteCommitRequest session_id=1:i64 block_id=2:i64 length=3:i64 pin=4:bool ufs_read=5:bool
 msg AsyncCacheRequest block_id=1:i64 source_host=2:str source_port=3:i32

@@ -287,6 +287,9 @@ class BlockWorkerService:
                 if req.HasField("chunk"):
                     out.write(req.chunk.data)
                     pos += len(req.chunk.data)
+                elif req.HasField("append_block"):
+                    # CACHE_THROUGH tee: the next bytes are a block this worker holds
+                    pos += self._append_block(out, req.append_block.block_id, req.append_block.length)
                 elif req.HasField("command") and req.command.flush:
                     yield pb.block.WriteResponse(offset=pos)
             ok = True
@@ -306,6 +309,24 @@ class BlockWorkerService:
         self.w.metrics.counter("BytesWrittenUfsAll").inc(pos)
         self.w.note_ufs_mount(o.mount_id, ufs)
         yield pb.block.WriteResponse(offset=pos)
+
+    def _append_block(self, out, block_id: int, length: int) -> int:
+        """Copy [0, length) of a block this worker holds into a UFS output stream (read-locked,
+        8 MiB at a time through a host buffer)."""
+        import numpy as np
+        session = ids.create_session_id()
+        lock_id = self.w.lock_block(session, block_id)
+        try:
+            buf = np.empty(min(length, 8 << 20), dtype=np.uint8)
+            off = 0
+            while off < length:
+                k = min(len(buf), length - off)
+                self.w.native.read(block_id, off, k, buf.ctypes.data, 0)
+                out.write(memoryview(buf)[:k])
+                off += k
+        finally:
+            self.w.unlock(lock_id)
+        return length
 
     # ------------------------------------------------------------------------------------------
     def OpenLocalBlock(self, request_iter, ctx):

@@ -390,6 +390,7 @@ def test_cache_through_ufs_error_surfaces_from_helper_thread(tmp_path):
                 raise OSError("UFS is gone")
             f._ufs.write = boom
             f._pair_write = lambda ptr, n: False     # the helper-thread path, not the native pair
+            f._tee = False                           # ... nor the worker-side tee
             with pytest.raises(OSError, match="UFS is gone"):
                 f.write(data)
             assert calls == [data.nbytes]
@@ -903,6 +904,7 @@ def test_cache_through_pair_write_lands_in_cache_and_ufs(tmp_path):
         try:
             data = np.random.default_rng(21).integers(0, 256, (9 << 20) + 4097, dtype=np.uint8)
             with rfs.create_file("/pair", write_type="CACHE_THROUGH", block_size=4 << 20) as f:
+                f._tee = False                       # the paired path (the tee has its own test)
                 used = []
                 orig = f._pair_write
                 f._pair_write = lambda ptr, n: used.append(orig(ptr, n)) or used[-1]
@@ -917,11 +919,62 @@ def test_cache_through_pair_write_lands_in_cache_and_ufs(tmp_path):
                 assert fh.read() == data.tobytes()
             # the UFS stream dies: the next paired write raises
             f2 = rfs.create_file("/pair2", write_type="CACHE_THROUGH", block_size=4 << 20)
+            f2._tee = False
             f2.write(data[:1 << 20])
             f2._ufs._sink.cancel()
             with pytest.raises(Exception):
                 for _ in range(8):
                     f2.write(data[:1 << 20])
             f2.cancel()
+        finally:
+            rfs.close()
+
+
+def test_cache_through_tee_sends_bytes_once(tmp_path):
+    """CACHE_THROUGH with the cache block and the UFS stream on one worker: the bytes go only to the
+    block stream; after each block commits, the UFS stream appends it from the worker's store
+    (AppendBlock).  The file is byte-exact in the cache and in the UFS, across block boundaries and
+    a partial last block; a block that vanished before its append fails the file's UFS stream."""
+    with _cluster(tmp_path) as c:
+        rfs = _remote_fs(c)
+        try:
+            data = np.random.default_rng(23).integers(0, 256, (9 << 20) + 777, dtype=np.uint8)
+            # the mount's first UFS_FILE stream runs in the Python servicer (which registers the
+            # mount natively): it handles AppendBlock too
+            with rfs.create_file("/tee0", write_type="CACHE_THROUGH", block_size=4 << 20) as f:
+                for i in range(0, len(data), 1 << 20):
+                    f.write(data[i:i + (1 << 20)])
+            st0 = rfs.get_status("/tee0")
+            with open(st0.info.ufsPath.replace("file://", ""), "rb") as fh:
+                assert fh.read() == data.tobytes()
+            st0 = c.workers[0].data_server.stats
+            tee0, ufs0 = st0.ufs_tee_bytes, st0.ufs_write_bytes
+            with rfs.create_file("/tee", write_type="CACHE_THROUGH", block_size=4 << 20) as f:
+                pairs = []
+                f._pair_write = lambda ptr, n: pairs.append(n) or False
+                for i in range(0, len(data), 1 << 20):
+                    f.write(data[i:i + (1 << 20)])
+            assert not pairs                                    # never the two-stream path
+            st = c.workers[0].data_server.stats
+            assert st.ufs_tee_bytes - tee0 == len(data)
+            assert st.ufs_write_bytes - ufs0 == len(data)
+            assert rfs.read_file("/tee") == data.tobytes()
+            status = rfs.get_status("/tee")
+            assert status.info.inAlluxioPercentage == 100
+            with open(status.info.ufsPath.replace("file://", ""), "rb") as fh:
+                assert fh.read() == data.tobytes()
+            # the block is gone before the worker appends it: the UFS stream (and close) fail
+            g = rfs.create_file("/tee2", write_type="CACHE_THROUGH", block_size=4 << 20)
+            g.write(data[:1 << 20])
+            bid = g._block_id
+            orig = g._ufs.append_block
+
+            def append_after_removal(block_id, length):
+                c.workers[0].native.remove_block(block_id)
+                orig(block_id, length)
+            g._ufs.append_block = append_after_removal
+            with pytest.raises(Exception):
+                g.close()
+            assert bid is not None
         finally:
             rfs.close()
