@@ -289,6 +289,7 @@ class BlockStore {
   uint64_t clock() const { return clock_.load(); }
   int device() const { return device_; }
   bool has_device() const { return has_device_; }
+  hipStream_t move_stream();           // this thread's own stream (tier moves, tee copies; not internal_stream_)
   void use_device() const { set_device(); }
   std::string stats();
 
@@ -339,7 +340,6 @@ class BlockStore {
   void plan_block_range(const BlockMeta& b, uint64_t offset, uint64_t len, uint64_t ext,
                         int ext_kind, bool to_block, std::vector<CopySeg>& dev_segs,
                         hipStream_t stream, uint64_t ext_mapped = 0, bool mapped_kernel = false);
-  hipStream_t move_stream();           // this thread's stream for tier moves (not internal_stream_)
   void file_path(const StorageDir& d, int64_t id, std::string& out) const;
   void set_device() const;
   hipStream_t stream_or_default(uint64_t s) const;

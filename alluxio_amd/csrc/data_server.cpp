@@ -1322,7 +1322,8 @@ struct LocalFileJob {
 
   // One pool task: open (first time), write queued chunks in order, and on the end chmod + rename.
   // Appends block `id` ([0, n) of it) from the store: read-locked, copied out in 8 MiB pieces
-  // through one pinned buffer (a DMA when the block sits in HBM), each piece written to the file.
+  // through two pinned buffers on this pool thread's own stream, so the DMA of piece k+1 runs
+  // while piece k is written to the file (and never waits behind the store's internal stream).
   int append_block(int64_t id, uint64_t n, std::string* what) {
     if (!store) {
       *what = "no block store for an appended block";
@@ -1340,21 +1341,39 @@ struct LocalFileJob {
       return ETIMEDOUT;
     }
     constexpr uint64_t kPiece = 8ull << 20;
-    if (!tee_buf) {                    // one pinned piece buffer per stream, kept for its blocks
-      tee_buf = static_cast<uint8_t*>(pinned_alloc_near(kPiece, store->device()));
+    if (!tee_buf) {                    // two pinned piece buffers per stream, kept for its blocks
+      tee_buf = static_cast<uint8_t*>(pinned_alloc_near(2 * kPiece, store->device()));
       tee_pinned = tee_buf != nullptr;
-      if (!tee_buf) tee_buf = static_cast<uint8_t*>(std::malloc(kPiece));
+      if (!tee_buf) tee_buf = static_cast<uint8_t*>(std::malloc(2 * kPiece));
     }
-    uint8_t* buf = tee_buf;
+    const bool dev = store->has_device();
+    hipStream_t st = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
     int e = 0;
     try {
-      for (uint64_t off = 0; off < n && !e;) {
-        const uint64_t k = std::min(kPiece, n - off);
-        std::vector<ReadReq> rq{ReadReq{id, off, k, reinterpret_cast<uint64_t>(buf), (int)MemKind::kHost}};
-        store->read_batch(rq, 0, true);
+      if (dev) {
+        st = store->move_stream();
+        for (auto& x : ev)
+          if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
+            throw std::runtime_error("hipEventCreate failed");
+      }
+      const uint64_t pieces = (n + kPiece - 1) / kPiece;
+      auto issue = [&](uint64_t i) {
+        const uint64_t off = i * kPiece, k = std::min(kPiece, n - off);
+        uint8_t* b = tee_buf + (i & 1) * kPiece;
+        std::vector<ReadReq> rq{ReadReq{id, off, k, reinterpret_cast<uint64_t>(b), (int)MemKind::kHost}};
+        store->read_batch(rq, reinterpret_cast<uint64_t>(st), !dev);
+        if (dev && hipEventRecord(ev[i & 1], st) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
+      };
+      if (pieces) issue(0);
+      for (uint64_t i = 0; i < pieces && !e; ++i) {
+        if (i + 1 < pieces) issue(i + 1);            // its buffer's previous piece is written
+        if (dev && hipEventSynchronize(ev[i & 1]) != hipSuccess) throw std::runtime_error("D2H of an appended piece failed");
+        const uint64_t k = std::min(kPiece, n - i * kPiece);
+        const uint8_t* b = tee_buf + (i & 1) * kPiece;
         size_t done = 0;
         while (done < k) {
-          const ssize_t w = ::write(fd, buf + done, (size_t)(k - done));
+          const ssize_t w = ::write(fd, b + done, (size_t)(k - done));
           if (w < 0) {
             if (errno == EINTR) continue;
             e = errno;
@@ -1363,12 +1382,16 @@ struct LocalFileJob {
           }
           done += (size_t)w;
         }
-        off += k;
       }
+      if (dev && hipStreamSynchronize(st) != hipSuccess)   // nothing in flight into tee_buf on return
+        throw std::runtime_error("D2H of an appended piece failed");
     } catch (const std::exception& x) {
       e = EIO;
       *what = std::string("appending block ") + std::to_string(id) + ": " + x.what();
+      if (st) (void)hipStreamSynchronize(st);
     }
+    for (auto x : ev)
+      if (x) (void)hipEventDestroy(x);
     try {
       store->unlock(lock);
     } catch (...) {

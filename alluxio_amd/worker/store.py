@@ -53,8 +53,16 @@ class Arena:
             # (DirSpec.owns_base) and frees it when it is destroyed, so no page it hands out
             # outlives the memory.
             self.alloc_bytes = max(alloc_bytes or nbytes, nbytes, 1)
-            self._dptr = lib().device_arena_alloc(self.alloc_bytes, device)
-            self.tensor = _device_tensor(self._dptr, nbytes, device)
+            if os.environ.get("ALLUXIO_HBM_ARENA_TORCH") == "1":
+                # A/B knob: the arena as a caching-allocator tensor (round-4 layout), kept alive
+                # by this object instead of owned by the store
+                self._dptr = None
+                self._owner = torch.empty(self.alloc_bytes, dtype=torch.uint8,
+                                          device=torch.device("cuda", device))
+                self.tensor = self._owner[:nbytes]
+            else:
+                self._dptr = lib().device_arena_alloc(self.alloc_bytes, device)
+                self.tensor = _device_tensor(self._dptr, nbytes, device)
         elif kind == "dram":
             self.tensor = self._shared_host(nbytes)
         else:
@@ -252,7 +260,7 @@ class TieredStore:
                 arena = Arena("hbm", quota, spec.device, alloc)
                 spec.kind = C.DirKind.DEVICE
                 spec.base = arena.base
-                spec.owns_base = True
+                spec.owns_base = arena._dptr is not None
             elif kind == "dram":
                 quota -= quota % page
                 arena = Arena("dram", quota)

@@ -978,3 +978,37 @@ def test_cache_through_tee_sends_bytes_once(tmp_path):
             assert bid is not None
         finally:
             rfs.close()
+
+
+@pytest.mark.gpu
+def test_cache_through_tee_from_hbm_is_byte_exact(tmp_path):
+    """The CACHE_THROUGH tee with the cache in HBM: each committed block is copied out of device
+    memory in pipelined 8 MiB pieces (two pinned buffers, the pool thread's own stream) and appended
+    to the UFS file; several writers at once, partial last blocks, bytes checked in the UFS and the
+    cache."""
+    import concurrent.futures as cf
+    with _cluster(tmp_path, {"alluxio.worker.tieredstore.level0.dirs.path": "hbm:0",
+                             "alluxio.worker.tieredstore.level0.dirs.quota": "1GB",
+                             "alluxio.worker.hbm.page.size": "2MB"}) as c:
+        rfs = _remote_fs(c)
+        try:
+            rfs.write_file("/warm", b"x" * 1000, write_type="CACHE_THROUGH")   # registers the mount natively
+            st = c.workers[0].data_server.stats
+            tee0 = st.ufs_tee_bytes
+            rng = np.random.default_rng(5)
+            datas = [rng.integers(0, 256, (37 << 20) + 4097 * i, dtype=np.uint8) for i in range(4)]
+
+            def put(i):
+                with rfs.create_file(f"/hbm{i}", write_type="CACHE_THROUGH", block_size=16 << 20) as f:
+                    for o in range(0, len(datas[i]), 1 << 20):
+                        f.write(datas[i][o:o + (1 << 20)])
+            with cf.ThreadPoolExecutor(4) as ex:
+                list(ex.map(put, range(4)))
+            assert st.ufs_tee_bytes - tee0 == sum(len(d) for d in datas)
+            for i, d in enumerate(datas):
+                status = rfs.get_status(f"/hbm{i}")
+                with open(status.info.ufsPath.replace("file://", ""), "rb") as fh:
+                    assert fh.read() == d.tobytes()
+                assert rfs.read_file(f"/hbm{i}") == d.tobytes()
+        finally:
+            rfs.close()

@@ -227,6 +227,47 @@ for s in $STEPS; do
       run ww_ct_final 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type CACHE_THROUGH --client-timing "$PWD/$OUT/ct_timing" --out "$OUT/r5_worker_write_cache_through_final.jsonl"
       run ww_mc_final 600 python tools/worker_write_bench.py --threads 1,4,8,16 --file-size 256m --write-type MUST_CACHE --out "$OUT/r5_worker_write_cache_through_final.jsonl"
       ;;
+    arenaab)
+      run bench_arena_native_a 400 python bench.py
+      export ALLUXIO_HBM_ARENA_TORCH=1
+      run bench_arena_torch_a 400 python bench.py
+      run rocprof_arena_torch 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_arena_torch" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
+      unset ALLUXIO_HBM_ARENA_TORCH
+      run rocprof_arena_native 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_arena_native" -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 5
+      run bench_arena_native_b 400 python bench.py
+      export ALLUXIO_HBM_ARENA_TORCH=1
+      run bench_arena_torch_b 400 python bench.py
+      unset ALLUXIO_HBM_ARENA_TORCH
+      ;;
+    batchab)
+      run bench_batch_default 400 python bench.py --phases local,duration
+      export DEBUG_CLR_MAX_BATCH_SIZE=4096
+      run bench_batch_4096 400 python bench.py --phases local,duration
+      run rocprof_batch_4096 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_batch_4096" -o bench --output-format csv -- python3 bench.py --phases local,duration --duration 1
+      unset DEBUG_CLR_MAX_BATCH_SIZE
+      export DEBUG_CLR_BATCH_CPU_SYNC_SIZE=4096
+      run bench_cpusync_4096 400 python bench.py --phases local,duration
+      unset DEBUG_CLR_BATCH_CPU_SYNC_SIZE
+      ;;
+    paceab)
+      run bench_pace_off_a 300 python bench.py --phases local,duration
+      export ALLUXIO_RING_MAX_INFLIGHT=16
+      run bench_pace16 300 python bench.py --phases local,duration
+      export ALLUXIO_RING_MAX_INFLIGHT=32
+      run bench_pace32 300 python bench.py --phases local,duration
+      export ALLUXIO_RING_MAX_INFLIGHT=64
+      run bench_pace64 300 python bench.py --phases local,duration
+      export ALLUXIO_RING_MAX_INFLIGHT=8
+      run bench_pace8 300 python bench.py --phases local,duration
+      run bench_pace8_20 300 python bench.py --phases local --steps 20 --warmup 5
+      unset ALLUXIO_RING_MAX_INFLIGHT
+      run bench_pace_off_20 300 python bench.py --phases local --steps 20 --warmup 5
+      ;;
+    ctrep)
+      run ww_ct_rep 900 python tools/worker_write_bench.py --threads 1,4,8,16 --files 4 --repeat 3 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
+      run ww_ct_rep_bound 900 python tools/worker_write_bench.py --threads 4,8,16 --files 4 --repeat 3 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --work-dir /dev/shm --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
+      run ww_ct_rep_notee 900 python tools/worker_write_bench.py --threads 4,8,16 --files 4 --repeat 2 --file-size 256m --write-type CACHE_THROUGH --client-prop alluxio.user.file.cache.through.tee.enabled=false --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
+      ;;
     final)
       run pytest_gpu_final 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       run smoke_final 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"

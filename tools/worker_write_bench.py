@@ -86,6 +86,7 @@ def main(argv=None) -> int:
                     help="per-phase client timing (optiming JSON, one file per run: <path>.<run>)")
     ap.add_argument("--bind-gpu-node", action="store_true",
                     help="run the worker (this process) and the client on the CPUs of the GPU's NUMA node")
+    ap.add_argument("--repeat", type=int, default=1, help="runs per thread count (each row is one run)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     cpus = []
@@ -116,7 +117,8 @@ def main(argv=None) -> int:
     work = tempfile.mkdtemp(prefix="wwbench_", dir=a.work_dir)
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=work) as c:
         time.sleep(min(10.0, total / 4e9))     # let the DRAM prefault finish (no-op on HBM)
-        runs = [(tr, t) for tr in a.transports.split(",") for t in a.threads.split(",")]
+        runs = [(tr, t) for tr in a.transports.split(",") for t in a.threads.split(",")
+                for _ in range(max(1, a.repeat))]
         for i, (transport, t) in enumerate(runs):
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "true" if transport == "ipc" else "false",
@@ -125,6 +127,8 @@ def main(argv=None) -> int:
             sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
             from _threadcpu import busy, thread_cpu
             tc0, tw0 = thread_cpu(), time.perf_counter()
+            ds = getattr(c.workers[0], "data_server", None)
+            tee0 = ds.stats.ufs_tee_bytes if ds is not None else 0
             cenv = dict(os.environ)
             if a.client_timing:
                 cenv["ALLUXIO_MASTER_OP_TIMING"] = f"{a.client_timing}.{a.write_type}.t{t}"
@@ -146,7 +150,9 @@ def main(argv=None) -> int:
                    # worker process CPU by thread group during the run (approx: whole subprocess
                    # lifetime / timed window), and the client's own CPU over its timed window
                    "worker_thread_cores": worker_threads, "client_cpu_cores": r.get("client_cpu_cores"),
-                   "bound_to_gpu_node": bool(cpus), "work_dir": work}
+                   "bound_to_gpu_node": bool(cpus), "work_dir": work,
+                   # bytes the worker copied from its block store into UFS files (CACHE_THROUGH tee)
+                   "ufs_tee_bytes": (ds.stats.ufs_tee_bytes - tee0) if ds is not None else None}
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
