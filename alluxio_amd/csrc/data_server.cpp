@@ -1204,7 +1204,13 @@ bool make_parents(const std::string& path, int* err) {
 class FilePool {
  public:
   static FilePool& get() {
-    static FilePool* p = new FilePool(8);
+    // one thread per concurrently written file up to 16 (ALLUXIO_UFS_FILE_THREADS overrides):
+    // a CACHE_THROUGH tee append holds its thread for a whole block's D2H + write(2)
+    static FilePool* p = [] {
+      const char* e = std::getenv("ALLUXIO_UFS_FILE_THREADS");
+      const int n = e ? std::atoi(e) : 16;
+      return new FilePool(n > 0 ? std::min(n, 256) : 16);
+    }();
     return *p;
   }
   void submit(std::function<void()> f) {

@@ -3,7 +3,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -93,7 +92,6 @@ void RingReadSession::set_device() const {
 }
 
 void RingReadSession::finish_init(const std::vector<uint64_t>& start_offsets) {
-  if (const char* e = std::getenv("ALLUXIO_RING_MAX_INFLIGHT")) max_inflight_ = (uint32_t)std::strtoul(e, nullptr, 10);
   c_init_.assign(streams_, 0);
   for (uint32_t s = 0; s < streams_ && s < start_offsets.size(); ++s) {
     if (start_offsets[s] % buf_) throw StoreError(kErrInvalidArgument, "ring read: start offsets must be buffer aligned");
@@ -126,9 +124,6 @@ RingReadSession::~RingReadSession() {
 void RingReadSession::close() {
   if (closed_) return;
   closed_ = true;
-  for (auto e : pace_)
-    if (e) (void)hipEventDestroy(e);
-  pace_.clear();
   if (d_ftab_) (void)hipFree(d_ftab_);
   if (d_cinit_) (void)hipFree(d_cinit_);
   d_ftab_ = nullptr;
@@ -167,15 +162,7 @@ uint64_t RingReadSession::step(uint64_t stream, uint64_t* eofs) {
     a.page_shift = page_shift_;
     a.footprint = footprint_;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (max_inflight_ && pace_.empty()) {
-      pace_.resize(max_inflight_, nullptr);
-      for (auto& e : pace_) RR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    const size_t slot = max_inflight_ ? (size_t)(launches_ % max_inflight_) : 0;
-    if (max_inflight_ && launches_ >= max_inflight_) RR_HIP(hipEventSynchronize(pace_[slot]));
     RR_HIP(launch_seq_read(a, st));
-    if (max_inflight_) RR_HIP(hipEventRecord(pace_[slot], st));
-    ++launches_;
     if (kind_ == (int)MemKind::kHost) RR_HIP(hipStreamSynchronize(st));
   } else {
     // CPU-only build/test path: same schedule with memcpy from the host arena

@@ -64,11 +64,6 @@ class RingReadSession {
   uint64_t* d_cinit_ = nullptr;
   uint64_t calls_per_stream_ = 0, total_ = 0, reopens_ = 0;
   bool closed_ = false;
-  // Launch pacing (ALLUXIO_RING_MAX_INFLIGHT = K > 0): step i first waits for step i-K's event,
-  // so at most K launches are queued ahead of the GPU.
-  uint32_t max_inflight_ = 0;
-  uint64_t launches_ = 0;
-  std::vector<hipEvent_t> pace_;
 };
 
 }  // namespace amdx

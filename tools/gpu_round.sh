@@ -249,20 +249,6 @@ for s in $STEPS; do
       run bench_cpusync_4096 400 python bench.py --phases local,duration
       unset DEBUG_CLR_BATCH_CPU_SYNC_SIZE
       ;;
-    paceab)
-      run bench_pace_off_a 300 python bench.py --phases local,duration
-      export ALLUXIO_RING_MAX_INFLIGHT=16
-      run bench_pace16 300 python bench.py --phases local,duration
-      export ALLUXIO_RING_MAX_INFLIGHT=32
-      run bench_pace32 300 python bench.py --phases local,duration
-      export ALLUXIO_RING_MAX_INFLIGHT=64
-      run bench_pace64 300 python bench.py --phases local,duration
-      export ALLUXIO_RING_MAX_INFLIGHT=8
-      run bench_pace8 300 python bench.py --phases local,duration
-      run bench_pace8_20 300 python bench.py --phases local --steps 20 --warmup 5
-      unset ALLUXIO_RING_MAX_INFLIGHT
-      run bench_pace_off_20 300 python bench.py --phases local --steps 20 --warmup 5
-      ;;
     ctrep)
       run ww_ct_rep 900 python tools/worker_write_bench.py --threads 1,4,8,16 --files 4 --repeat 3 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
       run ww_ct_rep_bound 900 python tools/worker_write_bench.py --threads 4,8,16 --files 4 --repeat 3 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --work-dir /dev/shm --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
