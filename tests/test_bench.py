@@ -12,8 +12,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(args, tmp_path, expect_rc=0):
+def _run(args, tmp_path, expect_rc=0, extra_env=None):
     env = dict(os.environ)
+    env.update(extra_env or {})
     env.pop("WORLD_SIZE", None)
     env["MASTER_ADDR"] = "127.0.0.1"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args, "--work-dir", str(tmp_path)],
@@ -59,9 +60,23 @@ def test_bench_two_ranks_remote_and_replicate(tmp_path):
 
 def test_bench_fails_when_replicas_fall_back_to_grpc(tmp_path):
     """A mapped-pull failure makes the replicas come through the gRPC block stream: the bytes
-    still arrive (the write succeeds), but the bench must not report that as the peer data plane."""
+    still arrive (the write succeeds), but the bench must not report that as the peer data plane.
+    The JSON line says so (``verified`` false); the exit status follows the headline phase, whose
+    bytes were verified, so a failing secondary phase never costs the headline number."""
     out = _run(["--gpus", "2", *SMALL, "--phases", "local,replicate",
-                "--prop", "alluxio.test.peer.mapped.pull.fail=true"], tmp_path, expect_rc=1)
+                "--prop", "alluxio.test.peer.mapped.pull.fail=true"], tmp_path, expect_rc=0)
     rep = out["config"]["replication"]
     assert not rep["data_plane_ok"] and not out["config"]["verified"]
+    assert out["config"]["headline_verified"]
     assert rep["peer_pull_failures"] > 0 and rep["stream_fallback_bytes_received"] == 2 * (8 << 20)
+
+
+def test_bench_remote_failure_on_one_rank_keeps_the_headline(tmp_path):
+    """The remote phase's reader fails on rank 1 only: both ranks agree to skip the phase (no rank
+    is left waiting in a collective), the failure is reported, and the headline line is printed."""
+    out = _run(["--gpus", "2", *SMALL, "--phases", "local,remote,stagger"], tmp_path,
+               extra_env={"ALLUXIO_BENCH_TEST_REMOTE_FAIL_RANK": "1"})
+    c = out["config"]
+    assert c["remote_GBps"] is None and "injected" in c["phase_errors"]["remote"]
+    assert c["headline_verified"] and not c["verified"] and out["value"] > 0
+    assert c["stagger_GBps"] > 0                    # later phases still ran on both ranks
