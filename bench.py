@@ -66,6 +66,9 @@ def parse_args(argv=None):
                     help="read calls per stream per step (0 = 1 MiB of calls per stream)")
     ap.add_argument("--phases", default=",".join(PHASES), help="comma list of " + "/".join(PHASES))
     ap.add_argument("--duration", type=float, default=2.0, help="seconds for the duration phase")
+    ap.add_argument("--phase-timeout", type=float, default=180.0,
+                    help="deadline (s) of the cross-rank remote/replicate phases; past it the run "
+                         "reports the phase as timed out and ends instead of hanging")
     ap.add_argument("--replication", type=int, default=3)
     ap.add_argument("--work-dir", default=None)
     ap.add_argument("--large-size", default=None,
@@ -297,6 +300,86 @@ def main(argv=None):
                          "verified": good}
         return results[name]
 
+    def emit():
+        """Rank 0 prints the one JSON line (also called by the phase watchdog)."""
+        if rank != 0:
+            return
+        cfg = {
+            "model": "StressWorkerBench cached seq-read, HBM MEM tier",
+            "global_batch": a.threads * world,
+            "seq_len": buf,
+            "parallelism": f"workers{world}",
+            "threads_per_worker": a.threads,
+            "file_size": file_size,
+            "block_size": block_size,
+            "buffer_size": buf,
+            "calls_per_stream_per_step": depth,
+            "reads_per_step": a.threads * depth,
+            "page_size": page,
+            "reader": "gpu-consumer (same-GPU device ring), device-cursor ring x%d, streams start at offset 0" % depth,
+            "verified": bool(ok_all),
+            "headline_verified": bool(local["verified"]),
+            "phase_errors": phase_errors or None,
+            "stagger_GBps": results.get("stagger", {}).get("GBps"),
+            "host_reader_GBps": results.get("host", {}).get("GBps"),
+            "large_GBps": results.get("large", {}).get("GBps"),
+            "large_file_size": results.get("large", {}).get("file_size"),
+            "remote_GBps": results.get("remote", {}).get("GBps"),
+            "replication": results.get("replicate"),
+            "duration_GBps": results.get("duration", {}).get("GBps"),
+            "duration_s": results.get("duration", {}).get("s"),
+            "write_GBps_per_worker": round(file_size / write_s / 1e9, 3),
+            "devices": devices,
+            "peer_devices": peer_devices,
+            "process_group": ({"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+                              if distributed else None),
+            "phases": results,
+        }
+        out = {
+            "metric": METRIC,
+            "value": local["GBps"],
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(local["s"] / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8",
+            "data": "synthetic (random bytes written through the client API, CACHE_THROUGH)",
+            "config": cfg,
+        }
+        print(json.dumps(out), flush=True)
+
+    class watchdog:
+        """Deadline for a secondary phase that crosses ranks (remote / replicate over xGMI): if it
+        has not finished in time, every rank stops there -- rank 0 first prints the JSON line with
+        the results so far and the phase reported as timed out -- instead of hanging the job."""
+
+        def __init__(self, name, seconds):
+            self.name, self.seconds, self.timer = name, seconds, None
+
+        def fire(self):
+            phase_errors[self.name] = f"timed out after {self.seconds:.0f} s on rank {rank}"
+            try:
+                emit()
+            finally:
+                sys.stdout.flush()
+                sys.stderr.flush()
+                os._exit(0 if results.get("local", {}).get("verified") else 1)
+
+        def __enter__(self):
+            import threading
+            self.timer = threading.Timer(self.seconds, self.fire)
+            self.timer.daemon = True
+            self.timer.start()
+            return self
+
+        def __exit__(self, *exc):
+            self.timer.cancel()
+            return False
+
     # ---- local (headline): lockstep from offset 0 --------------------------------------------
     run_phase("local", lambda r: RingStreamReader(fs, path, r), ring_dev, data, a.steps, a.warmup)
     local = results["local"]
@@ -364,71 +447,75 @@ def main(argv=None):
         return "; ".join(e for e in errs if e) or "failed"
 
     if "remote" in phases and world > 1 and "remote" not in phase_errors:
-        peer = (rank + 1) % world
-        peer_data = np.random.default_rng(1234 + peer).integers(0, 256, file_size, dtype=np.uint8)
-        rreader, err = None, None
-        try:
-            if os.environ.get("ALLUXIO_BENCH_TEST_REMOTE_FAIL_RANK") == str(rank):
-                raise RuntimeError("injected remote-phase failure")          # tests/test_bench.py
-            rreader = RemoteRingReader(fs, f"/stress-worker-base/data-{peer}", ring_dev, addrs[peer])
-        except Exception as e:  # noqa: BLE001 - reported in the JSON; the headline stands
-            err = f"rank {rank}: {e!r}"
-        if agree(err is None):
-            run_phase("remote", lambda r: rreader, ring_dev, peer_data, a.steps, a.warmup)
-        else:
-            if rreader is not None:
-                rreader.close()
-            phase_errors["remote"] = all_errors(err)
-            ok_all = False
-        del peer_data
+        with watchdog("remote", a.phase_timeout):
+            peer = (rank + 1) % world
+            peer_data = np.random.default_rng(1234 + peer).integers(0, 256, file_size, dtype=np.uint8)
+            rreader, err = None, None
+            try:
+                if os.environ.get("ALLUXIO_BENCH_TEST_REMOTE_FAIL_RANK") == str(rank):
+                    raise RuntimeError("injected remote-phase failure")          # tests/test_bench.py
+                if os.environ.get("ALLUXIO_BENCH_TEST_REMOTE_HANG_RANK") == str(rank):
+                    time.sleep(3600)                                             # tests/test_bench.py
+                rreader = RemoteRingReader(fs, f"/stress-worker-base/data-{peer}", ring_dev, addrs[peer])
+            except Exception as e:  # noqa: BLE001 - reported in the JSON; the headline stands
+                err = f"rank {rank}: {e!r}"
+            if agree(err is None):
+                run_phase("remote", lambda r: rreader, ring_dev, peer_data, a.steps, a.warmup)
+            else:
+                if rreader is not None:
+                    rreader.close()
+                phase_errors["remote"] = all_errors(err)
+                ok_all = False
+            del peer_data
 
     if "replicate" in phases and world > 1:
-        wm = worker.worker.metrics
-        names = ("XgmiBytesReceived", "PeerSharedBytesReceived", "PeerStreamBytesReceived", "PeerPullFailures")
-        before = {k: wm.counter(k).count for k in names}
-        src = torch.from_numpy(data).to(dev_t)
-        sync()
-        barrier()
-        t = time.perf_counter()
-        err = None
-        try:
-            fs.write_file(f"/stress-worker-base/rep-{rank}", src, write_type="MUST_CACHE", block_size=block_size,
-                          replication_min=replicas)
-        except Exception as e:  # noqa: BLE001 - reported in the JSON; the headline stands
-            err = f"rank {rank}: {e!r}"
-        sync()
-        el = time.perf_counter() - t
-        barrier()
-        if not agree(err is None):
-            phase_errors["replicate"] = all_errors(err)
-        delta = {k: int(SUM(float(wm.counter(k).count - before[k]))) for k in names}
-        el_max = MAX(el)
-        try:
-            rst = fs.get_status(f"/stress-worker-base/rep-{rank}")
-            good = all(len(f.blockInfo.locations) >= replicas for f in rst.fileBlockInfos)
-        except Exception:  # noqa: BLE001 - the write failed: already in phase_errors
-            good = False
-        good = SUM(0.0 if good else 1.0) == 0
-        # every replica byte must have moved over the mapped plane (xGMI between distinct GPUs,
-        # shared DRAM on CPU): a silent gRPC fallback or a failed pull fails the bench
-        expect = world * file_size * (replicas - 1)
-        distinct_gpus = gpu and len(set(devices)) == world
-        plane_ok = (delta["PeerStreamBytesReceived"] == 0 and delta["PeerPullFailures"] == 0
-                    and delta["XgmiBytesReceived"] + delta["PeerSharedBytesReceived"] == expect
-                    and (not distinct_gpus or delta["XgmiBytesReceived"] == expect))
-        if not plane_ok and rank == 0:
-            print(f"replicate: data plane check failed: {delta} (expected {expect} peer bytes"
-                  f"{' over xGMI' if distinct_gpus else ''})", file=sys.stderr, flush=True)
-        ok_all = ok_all and good and plane_ok and "replicate" not in phase_errors
-        results["replicate"] = {"replicas": replicas,
-                                "write_GBps": round(SUM(float(file_size)) / el_max / 1e9, 3),
-                                "replica_GBps": round(SUM(float(file_size * (replicas - 1))) / el_max / 1e9, 3),
-                                "xgmi_bytes_received": delta["XgmiBytesReceived"],
-                                "shared_bytes_received": delta["PeerSharedBytesReceived"],
-                                "stream_fallback_bytes_received": delta["PeerStreamBytesReceived"],
-                                "peer_pull_failures": delta["PeerPullFailures"],
-                                "s": round(el_max, 4), "verified": good, "data_plane_ok": plane_ok}
-        del src
+        with watchdog("replicate", a.phase_timeout):
+            wm = worker.worker.metrics
+            names = ("XgmiBytesReceived", "PeerSharedBytesReceived", "PeerStreamBytesReceived", "PeerPullFailures")
+            before = {k: wm.counter(k).count for k in names}
+            src = torch.from_numpy(data).to(dev_t)
+            sync()
+            barrier()
+            t = time.perf_counter()
+            err = None
+            try:
+                fs.write_file(f"/stress-worker-base/rep-{rank}", src, write_type="MUST_CACHE", block_size=block_size,
+                              replication_min=replicas)
+            except Exception as e:  # noqa: BLE001 - reported in the JSON; the headline stands
+                err = f"rank {rank}: {e!r}"
+            sync()
+            el = time.perf_counter() - t
+            barrier()
+            if not agree(err is None):
+                phase_errors["replicate"] = all_errors(err)
+            delta = {k: int(SUM(float(wm.counter(k).count - before[k]))) for k in names}
+            el_max = MAX(el)
+            try:
+                rst = fs.get_status(f"/stress-worker-base/rep-{rank}")
+                good = all(len(f.blockInfo.locations) >= replicas for f in rst.fileBlockInfos)
+            except Exception:  # noqa: BLE001 - the write failed: already in phase_errors
+                good = False
+            good = SUM(0.0 if good else 1.0) == 0
+            # every replica byte must have moved over the mapped plane (xGMI between distinct GPUs,
+            # shared DRAM on CPU): a silent gRPC fallback or a failed pull fails the bench
+            expect = world * file_size * (replicas - 1)
+            distinct_gpus = gpu and len(set(devices)) == world
+            plane_ok = (delta["PeerStreamBytesReceived"] == 0 and delta["PeerPullFailures"] == 0
+                        and delta["XgmiBytesReceived"] + delta["PeerSharedBytesReceived"] == expect
+                        and (not distinct_gpus or delta["XgmiBytesReceived"] == expect))
+            if not plane_ok and rank == 0:
+                print(f"replicate: data plane check failed: {delta} (expected {expect} peer bytes"
+                      f"{' over xGMI' if distinct_gpus else ''})", file=sys.stderr, flush=True)
+            ok_all = ok_all and good and plane_ok and "replicate" not in phase_errors
+            results["replicate"] = {"replicas": replicas,
+                                    "write_GBps": round(SUM(float(file_size)) / el_max / 1e9, 3),
+                                    "replica_GBps": round(SUM(float(file_size * (replicas - 1))) / el_max / 1e9, 3),
+                                    "xgmi_bytes_received": delta["XgmiBytesReceived"],
+                                    "shared_bytes_received": delta["PeerSharedBytesReceived"],
+                                    "stream_fallback_bytes_received": delta["PeerStreamBytesReceived"],
+                                    "peer_pull_failures": delta["PeerPullFailures"],
+                                    "s": round(el_max, 4), "verified": good, "data_plane_ok": plane_ok}
+            del src
 
     if "duration" in phases and a.duration > 0:
         reader = RingStreamReader(fs, path, ring_dev)
@@ -460,54 +547,7 @@ def main(argv=None):
     if a.profile_json:
         with open(a.profile_json, "a") as f:
             f.write(json.dumps({"rank": rank, "results": results, "write_s": write_s}) + "\n")
-    if rank == 0:
-        cfg = {
-            "model": "StressWorkerBench cached seq-read, HBM MEM tier",
-            "global_batch": a.threads * world,
-            "seq_len": buf,
-            "parallelism": f"workers{world}",
-            "threads_per_worker": a.threads,
-            "file_size": file_size,
-            "block_size": block_size,
-            "buffer_size": buf,
-            "calls_per_stream_per_step": depth,
-            "reads_per_step": a.threads * depth,
-            "page_size": page,
-            "reader": "gpu-consumer (same-GPU device ring), device-cursor ring x%d, streams start at offset 0" % depth,
-            "verified": bool(ok_all),
-            "headline_verified": bool(local["verified"]),
-            "phase_errors": phase_errors or None,
-            "stagger_GBps": results.get("stagger", {}).get("GBps"),
-            "host_reader_GBps": results.get("host", {}).get("GBps"),
-            "large_GBps": results.get("large", {}).get("GBps"),
-            "large_file_size": results.get("large", {}).get("file_size"),
-            "remote_GBps": results.get("remote", {}).get("GBps"),
-            "replication": results.get("replicate"),
-            "duration_GBps": results.get("duration", {}).get("GBps"),
-            "duration_s": results.get("duration", {}).get("s"),
-            "write_GBps_per_worker": round(file_size / write_s / 1e9, 3),
-            "devices": devices,
-            "peer_devices": peer_devices,
-            "process_group": ({"backend": dist.get_backend(), "world_size": dist.get_world_size()}
-                              if distributed else None),
-            "phases": results,
-        }
-        out = {
-            "metric": METRIC,
-            "value": local["GBps"],
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(local["s"] / a.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "uint8",
-            "data": "synthetic (random bytes written through the client API, CACHE_THROUGH)",
-            "config": cfg,
-        }
-        print(json.dumps(out), flush=True)
+    emit()
 
     fs.close()
     worker.stop()

@@ -80,3 +80,16 @@ def test_bench_remote_failure_on_one_rank_keeps_the_headline(tmp_path):
     assert c["remote_GBps"] is None and "injected" in c["phase_errors"]["remote"]
     assert c["headline_verified"] and not c["verified"] and out["value"] > 0
     assert c["stagger_GBps"] > 0                    # later phases still ran on both ranks
+
+
+def test_bench_hung_cross_rank_phase_ends_with_the_headline(tmp_path):
+    """Rank 1 hangs inside the remote phase: past --phase-timeout every rank stops, and rank 0
+    prints the JSON line first (headline measured, the phase reported as timed out)."""
+    import time
+    t = time.time()
+    out = _run(["--gpus", "2", *SMALL, "--phases", "local,remote", "--phase-timeout", "8"], tmp_path,
+               extra_env={"ALLUXIO_BENCH_TEST_REMOTE_HANG_RANK": "1"})
+    c = out["config"]
+    assert "timed out" in c["phase_errors"]["remote"] and c["remote_GBps"] is None
+    assert c["headline_verified"] and out["value"] > 0
+    assert time.time() - t < 200
