@@ -254,6 +254,11 @@ for s in $STEPS; do
       run ww_ct_rep_bound 900 python tools/worker_write_bench.py --threads 4,8,16 --files 4 --repeat 3 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --work-dir /dev/shm --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
       run ww_ct_rep_notee 900 python tools/worker_write_bench.py --threads 4,8,16 --files 4 --repeat 2 --file-size 256m --write-type CACHE_THROUGH --client-prop alluxio.user.file.cache.through.tee.enabled=false --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
       ;;
+    validate)
+      run pytest_gpu_validate 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+      run smoke_validate 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"
+      run bench_validate_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
+      ;;
     final)
       run pytest_gpu_final 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       run smoke_final 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"
