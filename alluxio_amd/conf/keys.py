@@ -242,6 +242,10 @@ _k("USER_FILE_CACHE_THROUGH_TEE_ENABLED", "alluxio.user.file.cache.through.tee.e
    "CACHE_THROUGH writes whose cache block and UFS file stream go to the same worker send each byte "
    "once (to the block stream); after the block commits, the UFS stream is told to append it and the "
    "worker copies it from its store (AppendBlock).  false = every byte is sent to both streams.")
+_k("JOB_PERSIST_WORKER_APPEND_ENABLED", "alluxio.job.persist.worker.append.enabled", "true", Scope.ALL,
+   "Persist jobs of files cached on one worker open the file's UFS stream on that worker and append "
+   "its blocks from the store (AppendBlock, no bytes through the job process); false = read the file "
+   "through the client and write it to the UFS.")
 _k("MASTER_JOURNAL_NATIVE_WRITER_ENABLED", "alluxio.master.journal.native.writer.enabled", "true",
    Scope.MASTER,
    "UFS journal logs are written by the native group-commit writer (csrc/journal_log.cpp): a C++ "

@@ -14,10 +14,51 @@ from ..underfs.base import CreateOptions
 LOG = logging.getLogger(__name__)
 
 
+def _persist_from_worker(fs, info) -> int | None:
+    """Persist a fully cached file without moving its bytes through this process: open the file's
+    UFS stream (a native UFS_FILE WriteBlock) on the worker that holds every block and send one
+    ``AppendBlock`` per block -- the worker copies each block out of its store (pipelined D2H from
+    HBM) into a temp file it renames into place at commit, the same path as the CACHE_THROUGH tee.
+    None when that shape does not apply (blocks spread over workers, an object-store UFS, no
+    native writer); the caller then copies through the client."""
+    from ..client.context import worker_address_str
+    from ..client.streams import UfsWriter
+    up = info.ufsPath or ""
+    if not info.fileBlockInfos or ("://" in up and not up.startswith("file://")):
+        return None
+    common = None
+    for fbi in info.fileBlockInfos:
+        here = {worker_address_str(l.workerAddress): l.workerAddress for l in fbi.blockInfo.locations}
+        common = here if common is None else {k: v for k, v in common.items() if k in here}
+    if not common:
+        return None
+    addr = sorted(common)[0]
+    w = UfsWriter(fs.ctx, info, addr, None, common[addr])
+    if w._sink is None:                      # no native writer to that worker
+        w.cancel()
+        return None
+    try:
+        for fbi in info.fileBlockInfos:
+            w.append_block(fbi.blockInfo.blockId, fbi.blockInfo.length)
+        w.close()
+    except BaseException:
+        w.cancel()
+        raise
+    return w.length
+
+
 def persist_file(fs, path: str, conf=None, chunk: int = 8 << 20) -> int:
     """Copy ``path`` from Alluxio to its UFS location; returns bytes written."""
     st = fs.get_status(path)
     info = st.info
+    if (conf or fs.ctx.conf).get_bool("alluxio.job.persist.worker.append.enabled", "true"):
+        try:
+            n = _persist_from_worker(fs, info)
+        except Exception:  # noqa: BLE001 - e.g. a block evicted meanwhile: copy through the client
+            LOG.warning("worker-side persist of %s failed; copying through the client", path, exc_info=True)
+            n = None
+        if n is not None:
+            return n
     ufs = registry.create(info.ufsPath, conf or fs.ctx.conf)
     parent = os.path.dirname(info.ufsPath.rstrip("/"))
     if parent and not ufs.exists(parent):

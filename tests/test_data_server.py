@@ -6,6 +6,7 @@ the data port; BlockReadHandler.java:111-152 / AbstractReadHandler.java stream a
 chunks and pause while more than the window is un-acked by ``offset_received``;
 ReadResponseMarshaller.java:38-80 (header + raw chunk bytes) is what a stock gRPC client decodes.
 """
+import os
 import time
 
 import grpc
@@ -1010,5 +1011,28 @@ def test_cache_through_tee_from_hbm_is_byte_exact(tmp_path):
                 with open(status.info.ufsPath.replace("file://", ""), "rb") as fh:
                     assert fh.read() == d.tobytes()
                 assert rfs.read_file(f"/hbm{i}") == d.tobytes()
+        finally:
+            rfs.close()
+
+
+def test_persist_appends_blocks_on_the_holding_worker(tmp_path):
+    """A persist job of a file cached on one worker moves no bytes through the job process: the
+    worker appends each block from its store to the file's UFS stream (AppendBlock) and renames
+    the temp file into place; byte-exact, and counted as tee bytes by the native data server."""
+    from alluxio_amd.job.persist import persist_file
+    with _cluster(tmp_path) as c:
+        rfs = _remote_fs(c)
+        try:
+            rfs.write_file("/warm", b"w" * 100, write_type="CACHE_THROUGH")   # registers the mount natively
+            data = np.random.default_rng(8).integers(0, 256, (10 << 20) + 321, dtype=np.uint8)
+            rfs.write_file("/ap/f", data, write_type="ASYNC_THROUGH", block_size=4 << 20)
+            st = c.workers[0].data_server.stats
+            tee0 = st.ufs_tee_bytes
+            assert persist_file(rfs, "/ap/f") == len(data)
+            assert st.ufs_tee_bytes - tee0 == len(data)
+            ufs_path = rfs.get_status("/ap/f").info.ufsPath.replace("file://", "")
+            with open(ufs_path, "rb") as fh:
+                assert fh.read() == data.tobytes()
+            assert not [n for n in os.listdir(os.path.dirname(ufs_path)) if ".tmp" in n]
         finally:
             rfs.close()

@@ -254,6 +254,9 @@ for s in $STEPS; do
       run ww_ct_rep_bound 900 python tools/worker_write_bench.py --threads 4,8,16 --files 4 --repeat 3 --file-size 256m --write-type CACHE_THROUGH --bind-gpu-node --work-dir /dev/shm --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
       run ww_ct_rep_notee 900 python tools/worker_write_bench.py --threads 4,8,16 --files 4 --repeat 2 --file-size 256m --write-type CACHE_THROUGH --client-prop alluxio.user.file.cache.through.tee.enabled=false --out "$OUT/r5_worker_write_cache_through_tee.jsonl"
       ;;
+    persist)
+      run persist_bench 600 python tools/persist_bench.py --threads 1,4,8 --files 4 --file-size 512m --out "$OUT/r5_persist_bench.jsonl"
+      ;;
     validate)
       run pytest_gpu_validate 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       run smoke_validate 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"
