@@ -918,6 +918,8 @@ class GrpcBlockWriter(BlockWriter):
             sink, self._sink = self._sink, None
             sink.cancel()
             return
+        if not hasattr(self, "_reqs"):
+            return                      # a native stream already committed or cancelled
         try:
             self._resp.cancel()
         except Exception:  # noqa: BLE001
@@ -1086,9 +1088,6 @@ class FileOutStream(io.RawIOBase):
         self._canceled = False
         self._tee_block = False      # CACHE_THROUGH: the current block's UFS bytes come from the worker
         self._tee = ctx.conf.get_bool("alluxio.user.file.cache.through.tee.enabled", "true")
-        up = status.ufsPath or ""
-        if "://" in up and not up.startswith("file://"):
-            self._tee = False        # object stores: the worker streams parts of the bytes it receives
         self._failed: BaseException | None = None    # a parallel block write failed: no completion
         self._workers = None
         if self.through:
@@ -1444,6 +1443,7 @@ class FileOutStream(io.RawIOBase):
             raise IOError(f"output stream of {self.path} failed; the file was cancelled: {err}") from err
         self._stop_beside()
         from ..utils import optiming
+        ufs_closed = False
         try:
             t0 = time.perf_counter() if optiming.ENABLED else 0.0
             self._finish_block()
@@ -1452,6 +1452,7 @@ class FileOutStream(io.RawIOBase):
             opts = pb.file.CompleteFilePOptions()
             if self._ufs is not None:
                 self._ufs.close()
+                ufs_closed = True
                 opts.ufsLength = self._ufs.length
             t2 = time.perf_counter() if optiming.ENABLED else 0.0
             if self.write_type == "ASYNC_THROUGH":
@@ -1463,7 +1464,12 @@ class FileOutStream(io.RawIOBase):
                 optiming.add("client.close.complete_file", time.perf_counter() - t2)
         except Exception:
             for w in self._writers:
-                w.cancel()
+                try:
+                    w.cancel()
+                except Exception:  # noqa: BLE001 - keep the original error
+                    pass
+            if self._ufs is not None and not ufs_closed:
+                self._ufs.cancel()      # e.g. an object-store upload is aborted now, not at GC
             raise
         finally:
             super().close()

@@ -1692,9 +1692,127 @@ struct S3Upload {
   std::string err;
   std::function<void()> wake;
   std::shared_ptr<DataServerStats> stats;
+  uint64_t part = 0;                // part size
+  int max_bufs = 0;                 // part buffers in flight at most (+1 being filled)
+  // The part being filled.  Owned by the stream's I/O thread, or by an AppendBlock task while
+  // `appending` (the I/O thread then only queues what arrives).
+  uint8_t* cur = nullptr;
+  uint64_t fill = 0;
+  int parts = 0;
+  bool appending = false;
 
   ~S3Upload() {
     for (uint8_t* b : free_bufs) std::free(b);
+    if (cur) std::free(cur);
+  }
+
+  // A free part buffer, a new one while under max_bufs, else null -- or, with `wait`, blocks until
+  // an upload returns one (null when the upload failed or was cancelled meanwhile).
+  uint8_t* take_buf(bool wait) {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      if (!free_bufs.empty()) {
+        uint8_t* b = free_bufs.back();
+        free_bufs.pop_back();
+        return b;
+      }
+      if (allocated < max_bufs) {
+        uint8_t* b = static_cast<uint8_t*>(std::malloc(part));
+        if (b) ++allocated;
+        return b;
+      }
+      if (!wait || failed || cancelled) return nullptr;
+      cv.wait(lk);
+    }
+  }
+
+  static void submit_cur(const std::shared_ptr<S3Upload>& u) {
+    uint8_t* b = u->cur;
+    const uint64_t n = u->fill;
+    u->cur = nullptr;
+    u->fill = 0;
+    const int num = ++u->parts;
+    {
+      std::lock_guard<std::mutex> g(u->mu);
+      ++u->inflight;
+    }
+    auto uu = u;
+    UploadPool::get().submit([uu, num, b, n] { S3Upload::upload_part(uu, num, b, n); });
+  }
+
+  // Copies into part buffers, submitting each full one; returns the bytes taken (fewer when every
+  // buffer is in flight and `wait` is off, or when the upload failed / was cancelled).
+  static size_t fill_parts(const std::shared_ptr<S3Upload>& u, const uint8_t* p, size_t n, bool wait) {
+    size_t done = 0;
+    while (done < n) {
+      if (!u->cur) {
+        u->cur = u->take_buf(wait);
+        u->fill = 0;
+        if (!u->cur) break;
+      }
+      const size_t k = (size_t)std::min<uint64_t>(n - done, u->part - u->fill);
+      std::memcpy(u->cur + u->fill, p + done, k);
+      u->fill += k;
+      done += k;
+      if (u->fill == u->part) submit_cur(u);
+    }
+    return done;
+  }
+
+  // AppendBlock on a pool thread: block `id` ([0, n)) of the worker's store goes into the parts,
+  // read-locked and copied out in 8 MiB pieces through a pinned bounce buffer.  Clears `appending`
+  // and wakes the stream when done; a failure fails the upload (aborted like any other).
+  static void append_block(std::shared_ptr<S3Upload> u, BlockStore* store, int64_t session, int64_t id, uint64_t n) {
+    std::string e;
+    int64_t lock = -1;
+    try {
+      lock = store->lock_block(session, id, false, 30000);
+      if (lock < 0) e = "appending block " + std::to_string(id) + ": lock timed out";
+    } catch (const std::exception& x) {
+      e = std::string("appending block ") + std::to_string(id) + ": " + x.what();
+    }
+    if (e.empty()) {
+      constexpr uint64_t kPiece = 8ull << 20;
+      uint8_t* bounce = static_cast<uint8_t*>(pinned_alloc_near(kPiece, store->device()));
+      const bool pinned = bounce != nullptr;
+      if (!bounce) bounce = static_cast<uint8_t*>(std::malloc(kPiece));
+      try {
+        const uint64_t st = store->has_device() ? reinterpret_cast<uint64_t>(store->move_stream()) : 0;
+        for (uint64_t off = 0; off < n;) {
+          {
+            std::lock_guard<std::mutex> g(u->mu);
+            if (u->failed || u->cancelled) break;
+          }
+          const uint64_t k = std::min(kPiece, n - off);
+          std::vector<ReadReq> rq{ReadReq{id, off, k, reinterpret_cast<uint64_t>(bounce), (int)MemKind::kHost}};
+          store->read_batch(rq, st, true);
+          if (fill_parts(u, bounce, (size_t)k, true) < k) break;      // failed / cancelled meanwhile
+          u->stats->ufs_tee_bytes.fetch_add(k, std::memory_order_relaxed);
+          off += k;
+        }
+      } catch (const std::exception& x) {
+        e = std::string("appending block ") + std::to_string(id) + ": " + x.what();
+      }
+      if (pinned) (void)hipHostFree(bounce);
+      else std::free(bounce);
+      try {
+        store->unlock(lock);
+      } catch (...) {
+      }
+    }
+    bool abort_now;
+    {
+      std::lock_guard<std::mutex> g(u->mu);
+      u->appending = false;
+      if (!e.empty() && !u->failed) {
+        u->failed = true;
+        u->err = e;
+      }
+      abort_now = (u->failed || u->cancelled) && u->inflight == 0 && !u->finished;
+    }
+    u->cv.notify_all();
+    if (abort_now) finish(u);
+    u->poke();
   }
 
   int send(const std::string& method, const std::string& query, const uint8_t* body, uint64_t n, std::string* resp,
@@ -1764,8 +1882,9 @@ struct S3Upload {
         u->err = e;
       }
       u->free_bufs.push_back(buf);
-      last = --u->inflight == 0 && (u->finishing || u->cancelled || u->failed);
+      last = --u->inflight == 0 && (u->finishing || u->cancelled || u->failed) && !u->appending;
     }
+    u->cv.notify_all();                // an AppendBlock task may wait for this buffer
     if (last) finish(u);
     u->poke();
   }
@@ -1815,8 +1934,11 @@ struct S3Upload {
 
 class S3UfsWriteStream : public WriteStreamBase {
  public:
-  S3UfsWriteStream(std::shared_ptr<const S3Mount> m, const std::string& key, std::shared_ptr<DataServerStats> stats)
-      : part_(m->upload_part), max_bufs_(m->upload_inflight + 1), u_(std::make_shared<S3Upload>()) {
+  S3UfsWriteStream(std::shared_ptr<const S3Mount> m, const std::string& key, std::shared_ptr<DataServerStats> stats,
+                   BlockStore* store)
+      : u_(std::make_shared<S3Upload>()), store_(store), session_(g_session.fetch_add(1)) {
+    u_->part = m->upload_part;
+    u_->max_bufs = m->upload_inflight + 1;
     u_->m = std::move(m);
     u_->path = "/" + u_->m->bucket + "/" + key;
     u_->stats = std::move(stats);
@@ -1828,9 +1950,9 @@ class S3UfsWriteStream : public WriteStreamBase {
       std::lock_guard<std::mutex> g(u_->mu);
       u_->wake = nullptr;
       if (!u_->finished && !(u_->finishing && !u_->failed)) u_->cancelled = true;   // abandoned: abort
-      idle = u_->inflight == 0;
+      idle = u_->inflight == 0 && !u_->appending;
     }
-    if (cur_) std::free(cur_);
+    u_->cv.notify_all();               // an AppendBlock task waiting for a buffer stops
     if (idle && u_->cancelled) {
       auto u = u_;
       UploadPool::get().submit([u] { S3Upload::finish(u); });
@@ -1843,8 +1965,8 @@ class S3UfsWriteStream : public WriteStreamBase {
   }
 
   bool accepting() override {
-    drain_overflow();
-    return overflow_.empty();
+    drain_pending();
+    return pending_.empty() && !busy();
   }
 
   void on_message(const char* p, size_t n) override {
@@ -1859,16 +1981,21 @@ class S3UfsWriteStream : public WriteStreamBase {
       fail(3, "malformed WriteRequest");
       return;
     }
-    if (append_id >= 0) {              // never sent for object stores: refuse rather than drop bytes
-      fail(12, "AppendBlock is not supported by the S3 UFS stream");
-      return;
+    if (append_id >= 0) {              // the next bytes are a block of this worker's store
+      if (!store_) {
+        fail(12, "AppendBlock needs the worker's block store");
+        return;
+      }
+      pending_.push_back(Pending{std::string(), append_id, append_len});
+      pos_ += append_len;
+      drain_pending();
     }
     if (len) {
-      if (!overflow_.empty()) {
-        overflow_.append(reinterpret_cast<const char*>(chunk), len);
+      if (pending_.empty() && !busy()) {
+        const size_t took = S3Upload::fill_parts(u_, chunk, len, false);
+        if (took < len) pending_.push_back(Pending{std::string(reinterpret_cast<const char*>(chunk + took), len - took)});
       } else {
-        const size_t took = append(chunk, len);
-        if (took < len) overflow_.append(reinterpret_cast<const char*>(chunk + took), len - took);
+        pending_.push_back(Pending{std::string(reinterpret_cast<const char*>(chunk), len)});
       }
       pos_ += len;
     }
@@ -1884,7 +2011,7 @@ class S3UfsWriteStream : public WriteStreamBase {
   }
 
   ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
-    drain_overflow();
+    drain_pending();
     if (end_pending_) try_finish();
     {
       std::lock_guard<std::mutex> g(u_->mu);
@@ -1898,66 +2025,55 @@ class S3UfsWriteStream : public WriteStreamBase {
   }
 
  private:
-  uint8_t* take_buf() {
+  // What arrived while the parts could not take it, in file order: received bytes, or a block
+  // to append (AppendBlock).
+  struct Pending {
+    std::string data;
+    int64_t block = -1;
+    uint64_t len = 0;
+  };
+
+  bool busy() {
     std::lock_guard<std::mutex> g(u_->mu);
-    if (!u_->free_bufs.empty()) {
-      uint8_t* b = u_->free_bufs.back();
-      u_->free_bufs.pop_back();
-      return b;
-    }
-    if (u_->allocated >= max_bufs_) return nullptr;
-    uint8_t* b = static_cast<uint8_t*>(std::malloc(part_));
-    if (b) ++u_->allocated;
-    return b;
+    return u_->appending;
   }
 
-  // Copies into part buffers, submitting each full one; returns the bytes taken (fewer when every
-  // buffer is in flight: the rest waits in overflow_ and the request window is held back).
-  size_t append(const uint8_t* p, size_t n) {
-    size_t done = 0;
-    while (done < n) {
-      if (!cur_) {
-        cur_ = take_buf();
-        fill_ = 0;
-        if (!cur_) break;
+  // Feeds queued items to the parts in order; an AppendBlock hands the parts to a pool task and
+  // stops here until that task is done (it wakes the stream).
+  void drain_pending() {
+    while (!pending_.empty()) {
+      if (busy()) return;
+      Pending& f = pending_.front();
+      if (f.block >= 0) {
+        {
+          std::lock_guard<std::mutex> g(u_->mu);
+          u_->appending = true;
+        }
+        auto u = u_;
+        BlockStore* st = store_;
+        const int64_t ses = session_, id = f.block;
+        const uint64_t n = f.len;
+        pending_.pop_front();
+        FilePool::get().submit([u, st, ses, id, n] { S3Upload::append_block(u, st, ses, id, n); });
+        return;
       }
-      const size_t k = (size_t)std::min<uint64_t>(n - done, part_ - fill_);
-      std::memcpy(cur_ + fill_, p + done, k);
-      fill_ += k;
-      done += k;
-      if (fill_ == part_) submit();
+      const size_t took = S3Upload::fill_parts(u_, reinterpret_cast<const uint8_t*>(f.data.data()), f.data.size(), false);
+      if (took < f.data.size()) {
+        f.data.erase(0, took);
+        return;
+      }
+      pending_.pop_front();
     }
-    return done;
-  }
-
-  void submit() {
-    uint8_t* b = cur_;
-    const uint64_t n = fill_;
-    cur_ = nullptr;
-    fill_ = 0;
-    const int num = ++parts_;
-    {
-      std::lock_guard<std::mutex> g(u_->mu);
-      ++u_->inflight;
-    }
-    auto u = u_;
-    UploadPool::get().submit([u, num, b, n] { S3Upload::upload_part(u, num, b, n); });
-  }
-
-  void drain_overflow() {
-    if (overflow_.empty()) return;
-    const size_t took = append(reinterpret_cast<const uint8_t*>(overflow_.data()), overflow_.size());
-    overflow_.erase(0, took);
   }
 
   void try_finish() {
-    if (!overflow_.empty() || submitted_end_) return;
+    if (!pending_.empty() || busy() || submitted_end_) return;
     submitted_end_ = true;
     end_pending_ = false;
-    if (parts_ == 0) {                 // smaller than a part: one PutObject
-      uint8_t* b = cur_;
-      const uint64_t n = fill_;
-      cur_ = nullptr;
+    if (u_->parts == 0) {              // smaller than a part: one PutObject
+      uint8_t* b = u_->cur;
+      const uint64_t n = u_->fill;
+      u_->cur = nullptr;
       {
         std::lock_guard<std::mutex> g(u_->mu);
         ++u_->inflight;
@@ -1982,7 +2098,7 @@ class S3UfsWriteStream : public WriteStreamBase {
       });
       return;
     }
-    if (fill_) submit();
+    if (u_->fill) S3Upload::submit_cur(u_);
     bool idle;
     {
       std::lock_guard<std::mutex> g(u_->mu);
@@ -1995,13 +2111,11 @@ class S3UfsWriteStream : public WriteStreamBase {
     }
   }
 
-  uint64_t part_;
-  int max_bufs_;
   std::shared_ptr<S3Upload> u_;
-  uint8_t* cur_ = nullptr;
-  uint64_t fill_ = 0, pos_ = 0;
-  int parts_ = 0;
-  std::string overflow_;
+  BlockStore* store_;
+  int64_t session_;
+  uint64_t pos_ = 0;
+  std::deque<Pending> pending_;
   bool end_pending_ = false, submitted_end_ = false;
 };
 
@@ -2277,7 +2391,7 @@ void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_me
     std::string local, key;
     std::shared_ptr<const S3Mount> s3;
     if (cmd.type == 1 && cmd.has_ufs_file && ufs_roots && ufs_roots->resolve_s3(cmd.ufs_mount, cmd.ufs_path, &s3, &key)) {
-      auto ws = std::unique_ptr<S3UfsWriteStream>(new S3UfsWriteStream(std::move(s3), key, stats));
+      auto ws = std::unique_ptr<S3UfsWriteStream>(new S3UfsWriteStream(std::move(s3), key, stats, store));
       stats->ufs_write_streams.fetch_add(1, std::memory_order_relaxed);
       if (len) ws->on_message(first.data(), first.size());
       return ws;

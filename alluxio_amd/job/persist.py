@@ -19,12 +19,12 @@ def _persist_from_worker(fs, info) -> int | None:
     UFS stream (a native UFS_FILE WriteBlock) on the worker that holds every block and send one
     ``AppendBlock`` per block -- the worker copies each block out of its store (pipelined D2H from
     HBM) into a temp file it renames into place at commit, the same path as the CACHE_THROUGH tee.
-    None when that shape does not apply (blocks spread over workers, an object-store UFS, no
-    native writer); the caller then copies through the client."""
+    Object-store files take the same path: the worker's S3 stream fills its multipart parts from
+    the store.  None when that shape does not apply (blocks spread over workers, no native
+    writer); the caller then copies through the client."""
     from ..client.context import worker_address_str
     from ..client.streams import UfsWriter
-    up = info.ufsPath or ""
-    if not info.fileBlockInfos or ("://" in up and not up.startswith("file://")):
+    if not info.fileBlockInfos:
         return None
     common = None
     for fbi in info.fileBlockInfos:

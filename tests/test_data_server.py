@@ -848,6 +848,40 @@ def test_native_s3_through_writes(tmp_path):
                     assert time.time() < deadline
                     time.sleep(0.05)
                 assert requests.head(base + "/bkt/out/gone").status_code == 404
+                # CACHE_THROUGH into S3 with the tee: the bytes go once, to the block stream; the
+                # worker's S3 stream fills its multipart parts from the store (AppendBlock), here
+                # across block boundaries (4 MiB blocks, 1 MiB parts) and a partial last block
+                tee0, b1 = st.ufs_tee_bytes, st.ufs_write_bytes
+                ct = rng.integers(0, 256, (9 << 20) + 333, dtype=np.uint8)
+                with rfs.create_file("/s3/ct", write_type="CACHE_THROUGH", block_size=4 << 20) as f:
+                    for i in range(0, len(ct), 1 << 20):
+                        f.write(ct[i:i + (1 << 20)])
+                assert st.ufs_tee_bytes - tee0 == ct.nbytes and st.ufs_write_bytes - b1 == ct.nbytes
+                assert requests.get(base + "/bkt/out/ct").content == ct.tobytes()
+                # a persist job of a cached file into S3: the holding worker appends its blocks
+                from alluxio_amd.job.persist import persist_file
+                pz = rng.integers(0, 256, (6 << 20) + 7, dtype=np.uint8)
+                rfs.write_file("/s3/pz", pz, write_type="MUST_CACHE", block_size=4 << 20)
+                tee1 = st.ufs_tee_bytes
+                assert persist_file(rfs, "/s3/pz") == pz.nbytes
+                assert st.ufs_tee_bytes - tee1 == pz.nbytes
+                assert requests.get(base + "/bkt/out/pz").content == pz.tobytes()
+                # the block vanished before the worker appended it: the upload is aborted, close fails
+                g = rfs.create_file("/s3/ct2", write_type="CACHE_THROUGH", block_size=4 << 20)
+                g.write(ct[:(5 << 20)])                     # block 0 appended, block 1 in progress
+                orig = g._ufs.append_block
+
+                def append_after_removal(block_id, length):
+                    c.workers[0].native.remove_block(block_id)
+                    orig(block_id, length)
+                g._ufs.append_block = append_after_removal
+                with pytest.raises(Exception):
+                    g.close()
+                deadline = time.time() + 10
+                while requests.get(base + "/bkt", params={"uploads": ""}).text.count("<Upload>"):
+                    assert time.time() < deadline
+                    time.sleep(0.05)
+                assert requests.head(base + "/bkt/out/ct2").status_code == 404
             finally:
                 rfs.close()
                 fs.close()
