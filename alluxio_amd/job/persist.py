@@ -47,6 +47,23 @@ def _persist_from_worker(fs, info) -> int | None:
     return w.length
 
 
+def _mount_properties(fs, ufs_path: str) -> dict:
+    """The options of the mount holding ``ufs_path`` (endpoint, credentials, part sizes: the
+    reference resolves the UFS through the mount's UfsManager entry): the mount-table entry with
+    the longest UFS URI prefix."""
+    try:
+        table = fs.get_mount_table()
+    except Exception:  # noqa: BLE001 - an older master: client configuration only
+        LOG.debug("no mount table", exc_info=True)
+        return {}
+    best, props = -1, {}
+    for mp in table.values():
+        root = mp.ufsUri.rstrip("/")
+        if (ufs_path == root or ufs_path.startswith(root + "/")) and len(root) > best:
+            best, props = len(root), dict(mp.properties)
+    return props
+
+
 def persist_file(fs, path: str, conf=None, chunk: int = 8 << 20) -> int:
     """Copy ``path`` from Alluxio to its UFS location; returns bytes written."""
     st = fs.get_status(path)
@@ -59,7 +76,7 @@ def persist_file(fs, path: str, conf=None, chunk: int = 8 << 20) -> int:
             n = None
         if n is not None:
             return n
-    ufs = registry.create(info.ufsPath, conf or fs.ctx.conf)
+    ufs = registry.create(info.ufsPath, conf or fs.ctx.conf, _mount_properties(fs, info.ufsPath) or None)
     parent = os.path.dirname(info.ufsPath.rstrip("/"))
     if parent and not ufs.exists(parent):
         ufs.mkdirs(parent)

@@ -866,6 +866,14 @@ def test_native_s3_through_writes(tmp_path):
                 assert persist_file(rfs, "/s3/pz") == pz.nbytes
                 assert st.ufs_tee_bytes - tee1 == pz.nbytes
                 assert requests.get(base + "/bkt/out/pz").content == pz.tobytes()
+                # the client-copy fallback reaches the same bucket through the mount's options
+                from alluxio_amd.conf import Configuration
+                rfs.write_file("/s3/pz2", pz, write_type="MUST_CACHE", block_size=4 << 20)
+                off = Configuration({"alluxio.job.persist.worker.append.enabled": "false"})
+                tee2 = st.ufs_tee_bytes
+                assert persist_file(rfs, "/s3/pz2", conf=off) == pz.nbytes
+                assert st.ufs_tee_bytes == tee2
+                assert requests.get(base + "/bkt/out/pz2").content == pz.tobytes()
                 # the block vanished before the worker appended it: the upload is aborted, close fails
                 g = rfs.create_file("/s3/ct2", write_type="CACHE_THROUGH", block_size=4 << 20)
                 g.write(ct[:(5 << 20)])                     # block 0 appended, block 1 in progress

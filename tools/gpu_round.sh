@@ -256,6 +256,7 @@ for s in $STEPS; do
       ;;
     persist)
       run persist_bench 600 python tools/persist_bench.py --threads 1,4,8 --files 4 --file-size 512m --out "$OUT/r5_persist_bench.jsonl"
+      run persist_bench_s3 600 python tools/persist_bench.py --ufs s3 --threads 1,4,8 --files 2 --file-size 512m --out "$OUT/r5_persist_bench.jsonl"
       ;;
     validate)
       run pytest_gpu_validate 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
