@@ -258,6 +258,11 @@ for s in $STEPS; do
       run persist_bench 600 python tools/persist_bench.py --threads 1,4,8 --files 4 --file-size 512m --out "$OUT/r5_persist_bench.jsonl"
       run persist_bench_s3 600 python tools/persist_bench.py --ufs s3 --threads 1,4,8 --files 2 --file-size 512m --out "$OUT/r5_persist_bench.jsonl"
       ;;
+    s3ct)
+      run s3_ct_tee 600 python tools/s3_write_bench.py --size 4g --paths through --write-type CACHE_THROUGH --tier hbm:0 --out "$OUT/r5_s3_cache_through.jsonl"
+      run s3_ct_notee 600 python tools/s3_write_bench.py --size 4g --paths through --write-type CACHE_THROUGH --tier hbm:0 --client-prop alluxio.user.file.cache.through.tee.enabled=false --out "$OUT/r5_s3_cache_through.jsonl"
+      run s3_through 600 python tools/s3_write_bench.py --size 4g --paths through --tier hbm:0 --out "$OUT/r5_s3_cache_through.jsonl"
+      ;;
     validate)
       run pytest_gpu_validate 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       run smoke_validate 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"

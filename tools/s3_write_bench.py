@@ -42,7 +42,7 @@ fs = FileSystem(conf=Configuration({props!r}), master_address={addr!r})
 chunk = np.random.default_rng(2).integers(0, 256, {wsize}, dtype=np.uint8)
 fs.write_file("/s3/warm", chunk[:1 << 20], write_type="THROUGH")     # registers the mount natively
 t0 = time.perf_counter()
-with fs.create_file("/s3/data", write_type="THROUGH") as f:
+with fs.create_file("/s3/data", write_type={wtype!r}) as f:
     left = {size}
     while left > 0:
         n = min(left, chunk.nbytes)
@@ -89,6 +89,9 @@ def main(argv=None) -> int:
     ap.add_argument("--buffer", default="256MB", help="alluxio.underfs.object.store.upload.buffer.size")
     ap.add_argument("--spool", action="store_true", help="ufs path: spooled (reference default) writer")
     ap.add_argument("--blob-root", default=None)
+    ap.add_argument("--write-type", default="THROUGH", help="through path: THROUGH or CACHE_THROUGH")
+    ap.add_argument("--tier", default="dram", help="through path: the worker's MEM tier (dram, hbm:0)")
+    ap.add_argument("--client-prop", action="append", default=[], help="through path: client property k=v")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import numpy as np
@@ -131,8 +134,8 @@ def main(argv=None) -> int:
                 del chunk
             else:
                 from alluxio_amd.minicluster import LocalAlluxioCluster
-                conf = {"alluxio.worker.tieredstore.level0.dirs.path": "dram",
-                        "alluxio.worker.tieredstore.level0.dirs.quota": "1GB",
+                conf = {"alluxio.worker.tieredstore.level0.dirs.path": a.tier,
+                        "alluxio.worker.tieredstore.level0.dirs.quota": str(size + (1 << 30)),
                         "alluxio.user.block.size.bytes.default": "64MB",
                         "alluxio.security.authorization.permission.enabled": "false"}
                 with LocalAlluxioCluster(num_workers=1, conf=conf,
@@ -140,10 +143,12 @@ def main(argv=None) -> int:
                     fs = c.client()
                     fs.mount("/s3", "s3://bkt/out", properties=props)
                     cprops = {"alluxio.user.network.inprocess.transport.enabled": "false",
-                              "alluxio.user.short.circuit.enabled": "false"}
+                              "alluxio.user.short.circuit.enabled": "false",
+                              **dict(kv.split("=", 1) for kv in a.client_prop)}
                     samp = RssSampler()
                     p = subprocess.run([sys.executable, "-c", CLIENT.format(
-                        root=ROOT, props=cprops, addr=c.master.address, size=size, wsize=min(wsize, 4 << 20))],
+                        root=ROOT, props=cprops, addr=c.master.address, size=size, wsize=min(wsize, 4 << 20),
+                        wtype=a.write_type)],
                         capture_output=True, text=True, timeout=900)
                     growth = samp.stop()
                     line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
@@ -152,7 +157,9 @@ def main(argv=None) -> int:
                         return 1
                     el = json.loads(line[7:])["seconds"]
                     st = c.workers[0].data_server.stats
-                    extra = {"native_ufs_write_streams": st.ufs_write_streams, "native_ufs_write_bytes": st.ufs_write_bytes}
+                    extra = {"native_ufs_write_streams": st.ufs_write_streams, "native_ufs_write_bytes": st.ufs_write_bytes,
+                             "ufs_tee_bytes": st.ufs_tee_bytes, "write_type": a.write_type, "tier": a.tier,
+                             "client_props": a.client_prop}
                     fs.close()
             got = requests.head(f"{base}/bkt/out/{'ufs-data' if path == 'ufs' else 'data'}")
             row = {"bench": "THROUGH write into an S3 mount (native BlobServer endpoint on "
