@@ -874,6 +874,19 @@ def test_native_s3_through_writes(tmp_path):
                 assert persist_file(rfs, "/s3/pz2", conf=off) == pz.nbytes
                 assert st.ufs_tee_bytes == tee2
                 assert requests.get(base + "/bkt/out/pz2").content == pz.tobytes()
+                # bytes, a block, bytes on one S3 stream: the stream keeps file order across the
+                # append (a half-filled part continues after the block; parts are 1 MiB)
+                b1 = rng.integers(0, 256, (3 << 19), dtype=np.uint8)
+                b2 = rng.integers(0, 256, 700_000, dtype=np.uint8)
+                blk = rfs.get_status("/s3/pz").info.fileBlockInfos[0].blockInfo
+                mix = rfs.create_file("/s3/mix", write_type="THROUGH")
+                mix._ufs.write(b1)
+                mix._ufs.append_block(blk.blockId, blk.length)
+                mix._ufs.write(b2)
+                mix._ufs.close()
+                mix.cancel()                                   # drop the Alluxio entry, keep the object
+                want = b1.tobytes() + pz.tobytes()[:blk.length] + b2.tobytes()
+                assert requests.get(base + "/bkt/out/mix").content == want
                 # the block vanished before the worker appended it: the upload is aborted, close fails
                 g = rfs.create_file("/s3/ct2", write_type="CACHE_THROUGH", block_size=4 << 20)
                 g.write(ct[:(5 << 20)])                     # block 0 appended, block 1 in progress
