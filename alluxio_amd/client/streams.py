@@ -1088,6 +1088,10 @@ class FileOutStream(io.RawIOBase):
         self._canceled = False
         self._tee_block = False      # CACHE_THROUGH: the current block's UFS bytes come from the worker
         self._tee = ctx.conf.get_bool("alluxio.user.file.cache.through.tee.enabled", "true")
+        up = status.ufsPath or ""
+        if "://" in up and not up.startswith("file://") and not ctx.conf.get_bool(
+                "alluxio.user.file.cache.through.tee.object.store.enabled", "false"):
+            self._tee = False        # object stores: two streams, the S3 parts upload as bytes arrive
         self._failed: BaseException | None = None    # a parallel block write failed: no completion
         self._workers = None
         if self.through:

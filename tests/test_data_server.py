@@ -853,6 +853,7 @@ def test_native_s3_through_writes(tmp_path):
                 # across block boundaries (4 MiB blocks, 1 MiB parts) and a partial last block
                 tee0, b1 = st.ufs_tee_bytes, st.ufs_write_bytes
                 ct = rng.integers(0, 256, (9 << 20) + 333, dtype=np.uint8)
+                rfs.ctx.conf.set("alluxio.user.file.cache.through.tee.object.store.enabled", "true")
                 with rfs.create_file("/s3/ct", write_type="CACHE_THROUGH", block_size=4 << 20) as f:
                     for i in range(0, len(ct), 1 << 20):
                         f.write(ct[i:i + (1 << 20)])
