@@ -187,11 +187,17 @@ class FuseKernelServer:
         libc.umount2(self.mountpoint.encode(), MNT_DETACH)
         if self._srv is not None:
             self._srv.stop()                 # native readers poll with a timeout: they exit here
+        # Once the detached mount's superblock goes (no file left open on it) the kernel aborts
+        # the connection and blocked /dev/fuse readers return ENODEV: join them BEFORE closing the
+        # fd, so no reader can call read() on a descriptor number that was closed and reused.
+        # Only readers still blocked after that (a file held open elsewhere) are woken by close.
+        for t in self._threads:
+            t.join(timeout=2)
+        fd, self.fd = self.fd, -1
         try:
-            os.close(self.fd)        # aborts the connection: readers return ENODEV / EBADF
+            os.close(fd)             # aborts the connection: remaining readers return ENODEV / EBADF
         except OSError:
             pass
-        self.fd = -1
         for t in self._threads:
             t.join(timeout=5)
         self._threads = []

@@ -30,7 +30,7 @@ run() {
   local rt; rt=$(python -c "from alluxio_amd.ops.build import sanitizer_runtime as s; print(s('$k'))")
   echo "=== $k: $rt"
   env LD_PRELOAD="$rt" ALLUXIO_AMD_NATIVE_SO="$PWD/build/sanitize/$k/_C$SUFFIX" \
-      ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1" \
+      GRPC_ENABLE_FORK_SUPPORT=0 ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1" \
       UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1" \
       TSAN_OPTIONS="halt_on_error=1:die_after_fork=0:second_deadlock_stack=1:report_signal_unsafe=0:suppressions=$PWD/tools/tsan.supp:log_path=$PWD/build/sanitize/$k/report" \
       python -m pytest "${ARGS[@]}" || { cat build/sanitize/"$k"/report.* 2>/dev/null | head -80; return 1; }
