@@ -1092,3 +1092,55 @@ def test_persist_appends_blocks_on_the_holding_worker(tmp_path):
             assert not [n for n in os.listdir(os.path.dirname(ufs_path)) if ".tmp" in n]
         finally:
             rfs.close()
+
+
+@pytest.mark.gpu
+def test_persist_from_hbm_to_local_and_s3_is_byte_exact(tmp_path):
+    """Worker-side persist with the blocks in HBM: the local UFS stream and the S3 multipart
+    stream both copy every block out of device memory (pinned pieces on the pool thread's own
+    stream) into the persisted file / object, byte-exact, while 3 persists run at once."""
+    import concurrent.futures as cf
+
+    import requests
+
+    from alluxio_amd.job.persist import persist_file
+    srv = lib().BlobServer(str(tmp_path / "blobs"), "127.0.0.1", 0)
+    srv.start()
+    try:
+        base = f"http://127.0.0.1:{srv.port}"
+        assert requests.put(base + "/bkt").status_code == 200
+        assert requests.put(base + "/bkt/out/").status_code == 200
+        with _cluster(tmp_path, {"alluxio.worker.tieredstore.level0.dirs.path": "hbm:0",
+                                 "alluxio.worker.tieredstore.level0.dirs.quota": "1GB",
+                                 "alluxio.worker.hbm.page.size": "2MB"}) as c:
+            fs = c.client()
+            fs.mount("/s3", "s3://bkt/out", properties={
+                "alluxio.underfs.s3.endpoint": base,
+                "alluxio.underfs.s3.streaming.upload.partition.size": "8MB",
+                "alluxio.underfs.object.store.upload.buffer.size": "32MB"})
+            rfs = _remote_fs(c)
+            try:
+                rfs.write_file("/warm", b"w" * 100, write_type="CACHE_THROUGH")
+                rfs.write_file("/s3/warm", b"w" * 100, write_type="THROUGH")     # registers both mounts natively
+                st = c.workers[0].data_server.stats
+                rng = np.random.default_rng(12)
+                datas = {f"/p{i}": rng.integers(0, 256, (21 << 20) + 999 * i, dtype=np.uint8) for i in range(3)}
+                datas.update({f"/s3/o{i}": rng.integers(0, 256, (19 << 20) + 77 * i, dtype=np.uint8) for i in range(3)})
+                for p, d in datas.items():
+                    rfs.write_file(p, d, write_type="MUST_CACHE", block_size=8 << 20)
+                tee0 = st.ufs_tee_bytes
+                with cf.ThreadPoolExecutor(3) as ex:
+                    assert list(ex.map(lambda p: persist_file(rfs, p), datas)) == [d.nbytes for d in datas.values()]
+                assert st.ufs_tee_bytes - tee0 == sum(d.nbytes for d in datas.values())
+                for p, d in datas.items():
+                    if p.startswith("/s3/"):
+                        got = requests.get(base + "/bkt/out/" + p[4:]).content
+                    else:
+                        with open(rfs.get_status(p).info.ufsPath.replace("file://", ""), "rb") as fh:
+                            got = fh.read()
+                    assert got == d.tobytes(), p
+            finally:
+                rfs.close()
+                fs.close()
+    finally:
+        srv.stop()
