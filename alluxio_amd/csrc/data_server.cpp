@@ -1266,6 +1266,8 @@ struct LocalFileJob {
   bool tee_pinned = false;
 
   ~LocalFileJob() {
+    for (const Item& it : chunks)      // appends never run (failed / cancelled file)
+      if (it.block >= 0 && stats) stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
     if (tee_buf) {
       if (tee_pinned) (void)hipHostFree(tee_buf);
       else std::free(tee_buf);
@@ -1433,6 +1435,7 @@ struct LocalFileJob {
       if (have && it.block >= 0) {
         std::string what;
         const int e = j->append_block(it.block, it.len, &what);
+        j->stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
         std::lock_guard<std::mutex> g(j->mu);
         if (e) {
           if (!j->failed) {
@@ -1548,6 +1551,7 @@ class UfsFileWriteStream : public WriteStreamBase {
         it.len = append_len;
         j_->chunks.push_back(std::move(it));
         j_->queued += append_len;
+        j_->stats->store_tasks.fetch_add(1, std::memory_order_relaxed);
       }
       kick();
       pos_ += append_len;
@@ -1813,6 +1817,7 @@ struct S3Upload {
     u->cv.notify_all();
     if (abort_now) finish(u);
     u->poke();
+    u->stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);   // the store is not used past here
   }
 
   int send(const std::string& method, const std::string& query, const uint8_t* body, uint64_t n, std::string* resp,
@@ -2054,6 +2059,7 @@ class S3UfsWriteStream : public WriteStreamBase {
         const int64_t ses = session_, id = f.block;
         const uint64_t n = f.len;
         pending_.pop_front();
+        u->stats->store_tasks.fetch_add(1, std::memory_order_relaxed);
         FilePool::get().submit([u, st, ses, id, n] { S3Upload::append_block(u, st, ses, id, n); });
         return;
       }

@@ -48,6 +48,7 @@ struct DataServerStats {
   std::atomic<uint64_t> cold_aborted{0};     // read-throughs abandoned (cancel, error): temp block aborted
   std::atomic<uint64_t> cold_bytes{0};       // bytes read from the UFS by those streams
   std::atomic<int64_t> cold_active{0};       // background UFS readers still running
+  std::atomic<int64_t> store_tasks{0};       // AppendBlock copies queued or running (they use the store)
   std::atomic<uint64_t> ufs_tee_bytes{0};     // CACHE_THROUGH bytes the UFS stream copied from the store
   std::atomic<uint64_t> zero_copy_frames{0}; // HTTP/2 DATA frames sent straight from staging (no copy)
   std::atomic<uint64_t> prefetched{0};       // HBM chunks whose D2H was issued ahead of the send

@@ -105,5 +105,5 @@ class WorkerDataServer:
         # background UFS readers of cancelled cold reads finish their current read, wait for their
         # H2D copies and drop their temp blocks: the store must outlive them
         deadline = time.time() + 30
-        while self.stats.cold_active > 0 and time.time() < deadline:
-            time.sleep(0.01)
+        while (self.stats.cold_active > 0 or self.stats.store_tasks > 0) and time.time() < deadline:
+            time.sleep(0.01)                # (and AppendBlock copies out of the store on the file pool)

@@ -904,6 +904,7 @@ def test_native_s3_through_writes(tmp_path):
                     assert time.time() < deadline
                     time.sleep(0.05)
                 assert requests.head(base + "/bkt/out/ct2").status_code == 404
+                assert st.store_tasks == 0          # no AppendBlock copy left using the store
             finally:
                 rfs.close()
                 fs.close()
