@@ -1246,6 +1246,24 @@ class FilePool {
   std::deque<std::function<void()>> q_;
 };
 
+// A non-blocking stream on the store's device for one AppendBlock copy (created per block: a pool
+// thread serves files of any store in the process, so it keeps no per-thread stream).
+struct OwnStream {
+  hipStream_t s = nullptr;
+  explicit OwnStream(int device) {
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess) return;
+    if (hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+      s = nullptr;
+    (void)hipSetDevice(prev);
+  }
+  ~OwnStream() {
+    if (s) (void)hipStreamDestroy(s);
+  }
+  OwnStream(const OwnStream&) = delete;
+  OwnStream& operator=(const OwnStream&) = delete;
+};
+
 // State of one local UFS file write shared by its stream (I/O thread) and its pool tasks: one task
 // at a time drains the chunk queue in order.
 struct LocalFileJob {
@@ -1355,12 +1373,15 @@ struct LocalFileJob {
       if (!tee_buf) tee_buf = static_cast<uint8_t*>(std::malloc(2 * kPiece));
     }
     const bool dev = store->has_device();
+    std::unique_ptr<OwnStream> own;
     hipStream_t st = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
     int e = 0;
     try {
       if (dev) {
-        st = store->move_stream();
+        own.reset(new OwnStream(store->device()));
+        if (!own->s) throw std::runtime_error("hipStreamCreate failed");
+        st = own->s;
         for (auto& x : ev)
           if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
             throw std::runtime_error("hipEventCreate failed");
@@ -1781,7 +1802,12 @@ struct S3Upload {
       const bool pinned = bounce != nullptr;
       if (!bounce) bounce = static_cast<uint8_t*>(std::malloc(kPiece));
       try {
-        const uint64_t st = store->has_device() ? reinterpret_cast<uint64_t>(store->move_stream()) : 0;
+        std::unique_ptr<OwnStream> own;
+        if (store->has_device()) {
+          own.reset(new OwnStream(store->device()));
+          if (!own->s) throw std::runtime_error("hipStreamCreate failed");
+        }
+        const uint64_t st = own ? reinterpret_cast<uint64_t>(own->s) : 0;
         for (uint64_t off = 0; off < n;) {
           {
             std::lock_guard<std::mutex> g(u->mu);
