@@ -1264,6 +1264,32 @@ struct OwnStream {
   OwnStream& operator=(const OwnStream&) = delete;
 };
 
+// Pinned 8 MiB pieces for AppendBlock copies, shared by every stream of the process (per device):
+// a small CACHE_THROUGH file must not pay a pinned allocation of its own.
+constexpr uint64_t kTeePiece = 8ull << 20;
+StagingPool& tee_pieces(int device) {
+  static std::mutex mu;
+  static std::map<int, StagingPool*> pools;      // immortal, like the pool threads that use them
+  std::lock_guard<std::mutex> g(mu);
+  StagingPool*& p = pools[device];
+  if (!p) p = new StagingPool(kTeePiece, true, device);
+  return *p;
+}
+
+struct TeePieces {                 // n pieces borrowed from tee_pieces() for one block copy
+  StagingPool& pool;
+  uint8_t* b[2] = {nullptr, nullptr};
+  TeePieces(int device, int n) : pool(tee_pieces(device)) {
+    for (int i = 0; i < n; ++i) b[i] = pool.get();
+  }
+  ~TeePieces() {
+    for (uint8_t* p : b)
+      if (p) pool.put(p);
+  }
+  TeePieces(const TeePieces&) = delete;
+  TeePieces& operator=(const TeePieces&) = delete;
+};
+
 // State of one local UFS file write shared by its stream (I/O thread) and its pool tasks: one task
 // at a time drains the chunk queue in order.
 struct LocalFileJob {
@@ -1280,16 +1306,10 @@ struct LocalFileJob {
   uint64_t queued = 0, written = 0;   // bytes
   BlockStore* store = nullptr;        // source of appended blocks
   int64_t session = 0;
-  uint8_t* tee_buf = nullptr;
-  bool tee_pinned = false;
 
   ~LocalFileJob() {
     for (const Item& it : chunks)      // appends never run (failed / cancelled file)
       if (it.block >= 0 && stats) stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
-    if (tee_buf) {
-      if (tee_pinned) (void)hipHostFree(tee_buf);
-      else std::free(tee_buf);
-    }
   }
   bool running = false, opened = false, failed = false, cancelled = false;
   bool end = false, finished = false, cleaned = false;
@@ -1366,18 +1386,15 @@ struct LocalFileJob {
       *what = "appending block " + std::to_string(id) + ": lock timed out";
       return ETIMEDOUT;
     }
-    constexpr uint64_t kPiece = 8ull << 20;
-    if (!tee_buf) {                    // two pinned piece buffers per stream, kept for its blocks
-      tee_buf = static_cast<uint8_t*>(pinned_alloc_near(2 * kPiece, store->device()));
-      tee_pinned = tee_buf != nullptr;
-      if (!tee_buf) tee_buf = static_cast<uint8_t*>(std::malloc(2 * kPiece));
-    }
+    constexpr uint64_t kPiece = kTeePiece;
     const bool dev = store->has_device();
     std::unique_ptr<OwnStream> own;
+    std::unique_ptr<TeePieces> pieces_buf;      // declared before the stream sync that frees them
     hipStream_t st = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
     int e = 0;
     try {
+      pieces_buf.reset(new TeePieces(store->device(), 2));
       if (dev) {
         own.reset(new OwnStream(store->device()));
         if (!own->s) throw std::runtime_error("hipStreamCreate failed");
@@ -1389,7 +1406,7 @@ struct LocalFileJob {
       const uint64_t pieces = (n + kPiece - 1) / kPiece;
       auto issue = [&](uint64_t i) {
         const uint64_t off = i * kPiece, k = std::min(kPiece, n - off);
-        uint8_t* b = tee_buf + (i & 1) * kPiece;
+        uint8_t* b = pieces_buf->b[i & 1];
         std::vector<ReadReq> rq{ReadReq{id, off, k, reinterpret_cast<uint64_t>(b), (int)MemKind::kHost}};
         store->read_batch(rq, reinterpret_cast<uint64_t>(st), !dev);
         if (dev && hipEventRecord(ev[i & 1], st) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
@@ -1399,7 +1416,7 @@ struct LocalFileJob {
         if (i + 1 < pieces) issue(i + 1);            // its buffer's previous piece is written
         if (dev && hipEventSynchronize(ev[i & 1]) != hipSuccess) throw std::runtime_error("D2H of an appended piece failed");
         const uint64_t k = std::min(kPiece, n - i * kPiece);
-        const uint8_t* b = tee_buf + (i & 1) * kPiece;
+        const uint8_t* b = pieces_buf->b[i & 1];
         size_t done = 0;
         while (done < k) {
           const ssize_t w = ::write(fd, b + done, (size_t)(k - done));
@@ -1412,7 +1429,7 @@ struct LocalFileJob {
           done += (size_t)w;
         }
       }
-      if (dev && hipStreamSynchronize(st) != hipSuccess)   // nothing in flight into tee_buf on return
+      if (dev && hipStreamSynchronize(st) != hipSuccess)   // nothing in flight into the pieces on return
         throw std::runtime_error("D2H of an appended piece failed");
     } catch (const std::exception& x) {
       e = EIO;
@@ -1797,12 +1814,12 @@ struct S3Upload {
       e = std::string("appending block ") + std::to_string(id) + ": " + x.what();
     }
     if (e.empty()) {
-      constexpr uint64_t kPiece = 8ull << 20;
-      uint8_t* bounce = static_cast<uint8_t*>(pinned_alloc_near(kPiece, store->device()));
-      const bool pinned = bounce != nullptr;
-      if (!bounce) bounce = static_cast<uint8_t*>(std::malloc(kPiece));
+      constexpr uint64_t kPiece = kTeePiece;
+      std::unique_ptr<TeePieces> piece;
+      std::unique_ptr<OwnStream> own;
       try {
-        std::unique_ptr<OwnStream> own;
+        piece.reset(new TeePieces(store->device(), 1));
+        uint8_t* bounce = piece->b[0];
         if (store->has_device()) {
           own.reset(new OwnStream(store->device()));
           if (!own->s) throw std::runtime_error("hipStreamCreate failed");
@@ -1823,8 +1840,9 @@ struct S3Upload {
       } catch (const std::exception& x) {
         e = std::string("appending block ") + std::to_string(id) + ": " + x.what();
       }
-      if (pinned) (void)hipHostFree(bounce);
-      else std::free(bounce);
+      if (own && own->s) (void)hipStreamSynchronize(own->s);   // nothing in flight into the piece
+      piece.reset();
+      own.reset();
       try {
         store->unlock(lock);
       } catch (...) {
