@@ -1050,7 +1050,12 @@ def test_cache_through_tee_from_hbm_is_byte_exact(tmp_path):
                              "alluxio.worker.hbm.page.size": "2MB"}) as c:
         rfs = _remote_fs(c)
         try:
-            rfs.write_file("/warm", b"x" * 1000, write_type="CACHE_THROUGH")   # registers the mount natively
+            # the mount's first UFS stream runs in the Python servicer (which then registers the
+            # mount natively): its AppendBlock reads the block out of HBM through the store
+            warm = np.random.default_rng(4).integers(0, 256, (9 << 20) + 5, dtype=np.uint8)
+            rfs.write_file("/warm", warm, write_type="CACHE_THROUGH", block_size=4 << 20)
+            with open(rfs.get_status("/warm").info.ufsPath.replace("file://", ""), "rb") as fh:
+                assert fh.read() == warm.tobytes()
             st = c.workers[0].data_server.stats
             tee0 = st.ufs_tee_bytes
             rng = np.random.default_rng(5)
