@@ -263,6 +263,10 @@ for s in $STEPS; do
       run s3_ct_notee 600 python tools/s3_write_bench.py --size 4g --paths through --write-type CACHE_THROUGH --tier hbm:0 --client-prop alluxio.user.file.cache.through.tee.enabled=false --out "$OUT/r5_s3_cache_through.jsonl"
       run s3_through 600 python tools/s3_write_bench.py --size 4g --paths through --tier hbm:0 --out "$OUT/r5_s3_cache_through.jsonl"
       ;;
+    s3ctmt)
+      run ww_s3_ct_tee 600 python tools/worker_write_bench.py --s3 --threads 1,4,16 --files 2 --file-size 256m --write-type CACHE_THROUGH --client-prop alluxio.user.file.cache.through.tee.object.store.enabled=true --out "$OUT/r5_s3_cache_through_threads.jsonl"
+      run ww_s3_ct_two 600 python tools/worker_write_bench.py --s3 --threads 1,4,16 --files 2 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_s3_cache_through_threads.jsonl"
+      ;;
     validate)
       run pytest_gpu_validate 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       run smoke_validate 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"

@@ -87,6 +87,8 @@ def main(argv=None) -> int:
     ap.add_argument("--bind-gpu-node", action="store_true",
                     help="run the worker (this process) and the client on the CPUs of the GPU's NUMA node")
     ap.add_argument("--repeat", type=int, default=1, help="runs per thread count (each row is one run)")
+    ap.add_argument("--s3", action="store_true", help="/ww is an S3 mount (a native BlobServer on tmpfs, "
+                    "64 MiB parts): THROUGH / CACHE_THROUGH go to object storage")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     cpus = []
@@ -115,7 +117,23 @@ def main(argv=None) -> int:
             "alluxio.worker.tieredstore.dram.prefault": str(a.write_type != "THROUGH").lower()}
     conf.update(dict(kv.split("=", 1) for kv in a.worker_prop))
     work = tempfile.mkdtemp(prefix="wwbench_", dir=a.work_dir)
+    blob = None
+    if a.s3:
+        import requests
+
+        from alluxio_amd.ops.native import lib
+        blob_root = tempfile.mkdtemp(prefix="wwblob_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        blob = lib().BlobServer(blob_root, "127.0.0.1", 0)
+        blob.start()
+        endpoint = f"http://127.0.0.1:{blob.port}"
+        requests.put(endpoint + "/bkt")
+        requests.put(endpoint + "/bkt/ww/")
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=work) as c:
+        if blob is not None:
+            c.client().mount("/ww", "s3://bkt/ww", properties={
+                "alluxio.underfs.s3.endpoint": endpoint,
+                "alluxio.underfs.s3.streaming.upload.partition.size": "64MB",
+                "alluxio.underfs.object.store.upload.buffer.size": "256MB"})
         time.sleep(min(10.0, total / 4e9))     # let the DRAM prefault finish (no-op on HBM)
         runs = [(tr, t) for tr in a.transports.split(",") for t in a.threads.split(",")
                 for _ in range(max(1, a.repeat))]
@@ -150,7 +168,7 @@ def main(argv=None) -> int:
                    # worker process CPU by thread group during the run (approx: whole subprocess
                    # lifetime / timed window), and the client's own CPU over its timed window
                    "worker_thread_cores": worker_threads, "client_cpu_cores": r.get("client_cpu_cores"),
-                   "bound_to_gpu_node": bool(cpus), "work_dir": work,
+                   "bound_to_gpu_node": bool(cpus), "work_dir": work, "ufs": "s3" if a.s3 else "local",
                    # bytes the worker copied from its block store into UFS files (CACHE_THROUGH tee)
                    "ufs_tee_bytes": (ds.stats.ufs_tee_bytes - tee0) if ds is not None else None}
             print(json.dumps(row), flush=True)
@@ -162,6 +180,10 @@ def main(argv=None) -> int:
             for st in fs.list_status("/ww"):
                 fs.delete(st.path)
             fs.close()
+    if blob is not None:
+        import shutil
+        blob.stop()
+        shutil.rmtree(blob_root, ignore_errors=True)
     if a.work_dir:
         import shutil
         shutil.rmtree(work, ignore_errors=True)
