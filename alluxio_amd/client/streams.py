@@ -1089,9 +1089,13 @@ class FileOutStream(io.RawIOBase):
         self._tee_block = False      # CACHE_THROUGH: the current block's UFS bytes come from the worker
         self._tee = ctx.conf.get_bool("alluxio.user.file.cache.through.tee.enabled", "true")
         up = status.ufsPath or ""
-        if "://" in up and not up.startswith("file://") and not ctx.conf.get_bool(
-                "alluxio.user.file.cache.through.tee.object.store.enabled", "false"):
-            self._tee = False        # object stores: two streams, the S3 parts upload as bytes arrive
+        self._object_store = "://" in up and not up.startswith("file://")
+        # object stores: with few writers two streams win (S3 parts upload while the bytes
+        # arrive), with many the tee does (the client sends each byte once); auto picks per block
+        self._tee_os = str(ctx.conf.get("alluxio.user.file.cache.through.tee.object.store.enabled", "auto")).lower()
+        self._tee_os_min = int(ctx.conf.get("alluxio.user.file.cache.through.tee.object.store.min.streams", "8"))
+        if self._object_store and self._tee_os == "false":
+            self._tee = False
         self._failed: BaseException | None = None    # a parallel block write failed: no completion
         self._workers = None
         if self.through:
@@ -1297,6 +1301,8 @@ class FileOutStream(io.RawIOBase):
         self._block_written = 0
         self._tee_block = bool(self.through and self.cache and self._tee and self._ufs is not None
                                and self.replicas == 1 and self._tee_eligible())
+        if self._tee_block and self._object_store and self._tee_os == "auto":
+            self._tee_block = FileOutStream._ct_open >= self._tee_os_min
         if optiming.ENABLED:
             optiming.add("client.finish_block", t1 - t0)
             optiming.add("client.open_writers", time.perf_counter() - t1)

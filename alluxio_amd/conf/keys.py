@@ -243,10 +243,14 @@ _k("USER_FILE_CACHE_THROUGH_TEE_ENABLED", "alluxio.user.file.cache.through.tee.e
    "once (to the block stream); after the block commits, the UFS stream is told to append it and the "
    "worker copies it from its store (AppendBlock).  false = every byte is sent to both streams.")
 _k("USER_FILE_CACHE_THROUGH_TEE_OBJECT_STORE_ENABLED", "alluxio.user.file.cache.through.tee.object.store.enabled",
-   "false", Scope.CLIENT,
-   "The CACHE_THROUGH tee for files in object-store mounts (s3://...).  Off by default: a single "
-   "writer into S3 measured 3.3 GB/s teed vs 4.8 GB/s with two streams, whose S3 parts upload while "
-   "the bytes arrive (profiles/r5_s3_cache_through.jsonl).")
+   "auto", Scope.CLIENT,
+   "The CACHE_THROUGH tee for files in object-store mounts (s3://...): true, false, or auto = tee a "
+   "block when at least ...tee.object.store.min.streams CACHE_THROUGH streams are open in this client "
+   "process.  Measured into S3 (profiles/r5_persist.md): 16 writers 10.3 GB/s teed vs 6.4 with two "
+   "streams; 4 writers 4.1 vs 4.6; one 4 GiB writer 3.3 vs 4.8 (two streams upload parts as the bytes "
+   "arrive).")
+_k("USER_FILE_CACHE_THROUGH_TEE_OBJECT_STORE_MIN_STREAMS", "alluxio.user.file.cache.through.tee.object.store.min.streams",
+   "8", Scope.CLIENT, "Open CACHE_THROUGH streams from which object-store blocks are teed in auto mode.")
 _k("JOB_PERSIST_WORKER_APPEND_ENABLED", "alluxio.job.persist.worker.append.enabled", "true", Scope.ALL,
    "Persist jobs of files cached on one worker open the file's UFS stream on that worker and append "
    "its blocks from the store (AppendBlock, no bytes through the job process); false = read the file "

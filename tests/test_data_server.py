@@ -853,7 +853,18 @@ def test_native_s3_through_writes(tmp_path):
                 # across block boundaries (4 MiB blocks, 1 MiB parts) and a partial last block
                 tee0, b1 = st.ufs_tee_bytes, st.ufs_write_bytes
                 ct = rng.integers(0, 256, (9 << 20) + 333, dtype=np.uint8)
+                # auto (the default): teed only with enough CACHE_THROUGH streams open in the process
+                auto = rng.integers(0, 256, (5 << 20) + 3, dtype=np.uint8)
+                t_a = st.ufs_tee_bytes
+                rfs.write_file("/s3/auto1", auto, write_type="CACHE_THROUGH", block_size=4 << 20)
+                assert st.ufs_tee_bytes == t_a                       # 1 open stream < 8
+                rfs.ctx.conf.set("alluxio.user.file.cache.through.tee.object.store.min.streams", "1")
+                rfs.write_file("/s3/auto2", auto, write_type="CACHE_THROUGH", block_size=4 << 20)
+                assert st.ufs_tee_bytes - t_a == auto.nbytes
+                for k in ("auto1", "auto2"):
+                    assert requests.get(base + "/bkt/out/" + k).content == auto.tobytes()
                 rfs.ctx.conf.set("alluxio.user.file.cache.through.tee.object.store.enabled", "true")
+                tee0, b1 = st.ufs_tee_bytes, st.ufs_write_bytes
                 with rfs.create_file("/s3/ct", write_type="CACHE_THROUGH", block_size=4 << 20) as f:
                     for i in range(0, len(ct), 1 << 20):
                         f.write(ct[i:i + (1 << 20)])
