@@ -3,7 +3,10 @@
 # the script stops at the first crash-like exit (fault/abort/segv/timeout); plain test failures
 # (exit 1) do not stop later measurement steps.
 # usage: tools/gpu_round.sh [steps...]   steps: tests smoke bench bench20 variants prof ring pmc pmcdram
-#                                         crc dl master kbench lz4t lz4
+#                                         crc dl master kbench lz4t lz4 ... (every `name)` below);
+#   round-5 validation: `validate` (GPU tests, smoke, bench at the driver's 20 steps) and `rehearse`;
+#   round-5 write path: ctrep (CACHE_THROUGH tee vs two streams), persist, s3ct, s3ctmt;
+#   round-5 bench A/B: arenaab (native vs caching-allocator arena), batchab (HIP batching knobs)
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out
