@@ -35,6 +35,7 @@ from alluxio_amd.conf import Configuration
 conf = Configuration({props!r})
 fs = FileSystem(conf=conf, master_address={addr!r})
 size, nfiles, threads, wsize, tag, wtype = {size}, {nfiles}, {threads}, {wsize}, {tag!r}, {wtype!r}
+min_s = {min_s}
 data = np.random.default_rng(1).integers(0, 256, wsize, dtype=np.uint8)
 fs.create_directory("/ww", recursive=True, allow_exists=True)
 with fs.create_file(f"/ww/{{tag}}-warm", write_type=wtype) as f:
@@ -43,8 +44,15 @@ done = [0] * threads
 errs = []
 def run(t):
     try:
-        for k in range(nfiles):
-            with fs.create_file(f"/ww/{{tag}}-{{t}}-{{k}}", write_type=wtype) as f:
+        k = 0
+        # at least nfiles files; with min_s, keep going (reusing the nfiles names: the previous
+        # file of a name is deleted first, so the cache never holds more) until min_s has passed
+        while k < nfiles or time.perf_counter() - t0 < min_s:
+            name = f"/ww/{{tag}}-{{t}}-{{k % nfiles}}"
+            if k >= nfiles:
+                fs.delete(name)
+            k += 1
+            with fs.create_file(name, write_type=wtype) as f:
                 left = size
                 while left > 0:
                     n = min(wsize, left)
@@ -87,6 +95,8 @@ def main(argv=None) -> int:
     ap.add_argument("--bind-gpu-node", action="store_true",
                     help="run the worker (this process) and the client on the CPUs of the GPU's NUMA node")
     ap.add_argument("--repeat", type=int, default=1, help="runs per thread count (each row is one run)")
+    ap.add_argument("--min-seconds", type=float, default=0.0,
+                    help="each writer keeps writing files (deleting its oldest) for at least this long")
     ap.add_argument("--s3", action="store_true", help="/ww is an S3 mount (a native BlobServer on tmpfs, "
                     "64 MiB parts): THROUGH / CACHE_THROUGH go to object storage")
     ap.add_argument("--out", default=None)
@@ -152,7 +162,8 @@ def main(argv=None) -> int:
                 cenv["ALLUXIO_MASTER_OP_TIMING"] = f"{a.client_timing}.{a.write_type}.t{t}"
             p = subprocess.run([sys.executable, "-c", CLIENT.format(
                 root=ROOT, props=props, addr=c.master.address, size=size, nfiles=a.files, threads=int(t),
-                wsize=parse_space_size(a.write_size), tag=f"r{i}", wtype=a.write_type, cpus=cpus)],
+                wsize=parse_space_size(a.write_size), tag=f"r{i}", wtype=a.write_type, cpus=cpus,
+                min_s=a.min_seconds)],
                 capture_output=True, text=True, timeout=900, env=cenv)
             line = next((ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")), None)
             if line is None:
@@ -161,6 +172,7 @@ def main(argv=None) -> int:
             r = json.loads(line[7:])
             worker_threads = busy(tc0, thread_cpu(), r["seconds"])   # over the client's timed window
             row = {"bench": f"host writers, separate client process ({a.write_type})", "transport": transport, "tier": tier,
+                   "min_seconds": a.min_seconds,
                    "threads": int(t), "files_per_thread": a.files, "file_size": a.file_size,
                    "write_size": a.write_size, "bytes": r["bytes"], "seconds": round(r["seconds"], 3),
                    "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3), "errors": r["errors"],
