@@ -134,13 +134,14 @@ class FileSystemContext:
             return list(self._workers)
 
     def _note_domain_socket(self, addr) -> None:
-        """Same-node worker with a domain socket: its gRPC traffic skips TCP
-        (alluxio.user.short.circuit / domain socket data server)."""
+        """Same-node worker with a domain socket: its gRPC traffic skips TCP.  As in the reference
+        the socket is used whenever the worker advertises one and it is reachable from here
+        (NettyUtils.isDomainSocketAccessible, core/common/.../util/network/NettyUtils.java:109-119);
+        alluxio.user.short.circuit.* only decides between it and the IPC short circuit."""
         import os
         from ..rpc import register_domain_socket
         p = addr.domainSocketPath
-        if p and self.is_local(addr) and os.path.exists(p) and \
-                self.conf.get_bool("alluxio.user.short.circuit.enabled", "true"):
+        if p and self.is_local(addr) and os.path.exists(p):
             register_domain_socket(worker_address_str(addr), p)
 
     def is_local(self, addr) -> bool:

@@ -595,7 +595,7 @@ class FileInStream(io.RawIOBase):
         others.sort(key=lambda l: 0 if self.ctx.is_local(l.workerAddress) else 1)
         for l in others:
             addr = worker_address_str(l.workerAddress)
-            if self.ctx.is_local(l.workerAddress) and self._ipc_enabled():
+            if self.ctx.is_local(l.workerAddress) and self._ipc_enabled(l.workerAddress):
                 try:
                     return IpcBlockReader(self.ctx, addr, bi.blockId, self.session)
                 except Exception:  # noqa: BLE001 - not in the HBM tier / IPC unsupported: use gRPC
@@ -639,9 +639,16 @@ class FileInStream(io.RawIOBase):
                                    f"(no live location{'' if self.status.persisted else ', not persisted'})"
                                    + (f": {last_err}" if last_err else ""))
 
-    def _ipc_enabled(self) -> bool:
-        if not self.ctx.conf.get_bool("alluxio.worker.ipc.enabled", "true") or \
-                not self.ctx.conf.get_bool("alluxio.user.short.circuit.enabled", "true"):
+    def _ipc_enabled(self, addr=None) -> bool:
+        """The IPC short circuit for a same-node worker: on when short circuit is enabled and either
+        the worker has no domain socket or short circuit is preferred over it (reference
+        BlockInStream.java:116-124)."""
+        conf = self.ctx.conf
+        if not conf.get_bool("alluxio.worker.ipc.enabled", "true") or \
+                not conf.get_bool("alluxio.user.short.circuit.enabled", "true"):
+            return False
+        if addr is not None and addr.domainSocketPath and \
+                not conf.get_bool("alluxio.user.short.circuit.preferred", "false"):
             return False
         return True
 

@@ -326,7 +326,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("medium", &Event::medium);
 
   using G = py::call_guard<py::gil_scoped_release>;
-  py::class_<BlockStore>(m, "BlockStore", py::dynamic_attr())
+  py::class_<BlockStore, std::shared_ptr<BlockStore>>(m, "BlockStore", py::dynamic_attr())
       .def(py::init<const std::vector<DirSpec>&, int, int, float, float, int>(), py::arg("dirs"),
            py::arg("annotator") = 0, py::arg("alloc_policy") = 0, py::arg("lrfu_step") = 0.25f,
            py::arg("lrfu_attenuation") = 2.0f, py::arg("device") = 0)
@@ -564,10 +564,33 @@ PYBIND11_MODULE(_C, m) {
       .def("stop", &BlobServer::stop, G())
       .def_property_readonly("port", &BlobServer::port)
       .def_property_readonly("requests", &BlobServer::requests)
-      .def_property_readonly("bytes_sent", &BlobServer::bytes_sent);
+      .def_property_readonly("bytes_sent", &BlobServer::bytes_sent)
+      .def("inject", &BlobServer::inject, py::arg("kind"), py::arg("method") = "", py::arg("nth") = 1,
+           py::arg("count") = 1, py::arg("stall_ms") = 0)
+      .def("clear_faults", &BlobServer::clear_faults)
+      .def_property_readonly("injected", &BlobServer::injected);
   py::class_<HttpRangeReader>(m, "HttpRangeReader")
-      .def(py::init<const std::string&, int, int>(), py::arg("host"), py::arg("port"), py::arg("max_idle") = 16)
-      .def("get_into", &HttpRangeReader::get_into, G(), py::arg("target"), py::arg("head_lines"), py::arg("offset"),
+      .def(py::init([](const std::string& host, int port, int max_idle, int connect_timeout_ms, int socket_timeout_ms,
+                       int request_timeout_ms, int max_retries, int backoff_base_ms, int backoff_max_ms) {
+             HttpOptions o;
+             o.connect_timeout_ms = connect_timeout_ms;
+             o.socket_timeout_ms = socket_timeout_ms;
+             o.request_timeout_ms = request_timeout_ms;
+             o.max_retries = std::max(0, max_retries);
+             o.backoff_base_ms = std::max(1, backoff_base_ms);
+             o.backoff_max_ms = std::max(o.backoff_base_ms, backoff_max_ms);
+             return new HttpRangeReader(host, port, max_idle, o);
+           }),
+           py::arg("host"), py::arg("port"), py::arg("max_idle") = 16, py::arg("connect_timeout_ms") = 10000,
+           py::arg("socket_timeout_ms") = 50000, py::arg("request_timeout_ms") = 60000, py::arg("max_retries") = 3,
+           py::arg("backoff_base_ms") = 50, py::arg("backoff_max_ms") = 2000)
+      .def_property_readonly("retries", &HttpRangeReader::retries)
+      .def_property_readonly("timeouts", &HttpRangeReader::timeouts)
+      .def("get_into", [](HttpRangeReader& r, const std::string& target, const std::string& head, uint64_t offset,
+                          uint64_t length, uint64_t dst, int parallel, uint64_t min_part) {
+             py::gil_scoped_release rel;
+             return r.get_into(target, head, offset, length, dst, parallel, min_part);
+           }, py::arg("target"), py::arg("head_lines"), py::arg("offset"),
            py::arg("length"), py::arg("dst"), py::arg("parallel") = 1, py::arg("min_part") = 4 << 20)
       .def("put_from", [](HttpRangeReader& r, const std::string& target, const std::string& head, uint64_t src,
                           uint64_t length) {

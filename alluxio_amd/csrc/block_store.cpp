@@ -108,22 +108,41 @@ BlockStore::BlockStore(const std::vector<DirSpec>& dirs, int annotator, int allo
   }
 }
 
-hipStream_t BlockStore::move_stream() {
-  // one non-blocking stream per (thread, store): concurrent evictions move in parallel and never
-  // queue behind the page-claim / eviction-select kernels on internal_stream_
-  struct TL {
-    const BlockStore* owner = nullptr;
-    hipStream_t st = nullptr;
-  };
-  thread_local TL tl;
-  if (tl.owner != this || !tl.st) {
-    set_device();
-    hipStream_t st = nullptr;
-    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    tl.owner = this;
-    tl.st = st;
+namespace {
+std::atomic<uint64_t> g_thread_streams{0};
+
+struct ThreadStreams {
+  std::vector<std::pair<int, hipStream_t>> by_device;
+  ~ThreadStreams() {
+    for (auto& kv : by_device) (void)hipStreamDestroy(kv.second);
   }
-  return tl.st;
+};
+}  // namespace
+
+hipStream_t thread_stream_on(int device) {
+  thread_local ThreadStreams tl;
+  for (auto& kv : tl.by_device)
+    if (kv.first == device) return kv.second;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != device) HIP_OK(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  const hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (prev != device && prev >= 0) (void)hipSetDevice(prev);
+  HIP_OK(e);
+  tl.by_device.emplace_back(device, st);
+  g_thread_streams.fetch_add(1, std::memory_order_relaxed);
+  return st;
+}
+
+uint64_t thread_streams_created() { return g_thread_streams.load(std::memory_order_relaxed); }
+
+hipStream_t BlockStore::move_stream() {
+  // this thread's stream on the store's device: concurrent evictions move in parallel and never
+  // queue behind the page-claim / eviction-select kernels on internal_stream_; keyed by device
+  // (not store), so a thread that serves many stores keeps one stream per device
+  set_device();
+  return thread_stream_on(device_);
 }
 
 BlockStore::~BlockStore() {

@@ -145,6 +145,13 @@ struct Event {
 // Bulk creates of at least this many blocks claim their pages with the K7 device magazine.
 constexpr size_t kDeviceAllocMinBlocks = 64;
 
+// This thread's non-blocking HIP stream on `device`: one per (thread, device), created on first
+// use and destroyed when the thread exits.  Keyed by device, not by store -- a stream belongs to a
+// device, so stores that come and go on a pool thread reuse it instead of leaking one each.
+hipStream_t thread_stream_on(int device);
+// Streams thread_stream_on() has created in this process (tests: flat under store churn).
+uint64_t thread_streams_created();
+
 class BlockStore {
  public:
   BlockStore(const std::vector<DirSpec>& dirs, int annotator, int alloc_policy, float lrfu_step,
@@ -289,7 +296,7 @@ class BlockStore {
   uint64_t clock() const { return clock_.load(); }
   int device() const { return device_; }
   bool has_device() const { return has_device_; }
-  hipStream_t move_stream();           // this thread's own stream (tier moves, tee copies; not internal_stream_)
+  hipStream_t move_stream();           // this thread's stream on the device (tier moves, tee copies; not internal_stream_)
   void use_device() const { set_device(); }
   std::string stats();
 

@@ -464,9 +464,22 @@ void bind_data_path(py::module_& m) {
   auto mounts = py::class_<UfsMounts, std::shared_ptr<UfsMounts>>(m, "UfsMounts")
       .def(py::init<>())
       .def("set", &UfsMounts::set, py::arg("mount_id"), py::arg("root"))
-      .def("set_s3", &UfsMounts::set_s3, py::arg("mount_id"), py::arg("host"), py::arg("port"), py::arg("bucket"),
+      .def("set_s3",
+           [](UfsMounts& u, int64_t mount_id, const std::string& host, int port, const std::string& bucket,
+              const std::string& ak, const std::string& sk, const std::string& region, int parallel, uint64_t part,
+              uint64_t upload_part, int upload_inflight, int connect_timeout_ms, int socket_timeout_ms,
+              int request_timeout_ms, int max_retries) {
+             HttpOptions o;
+             o.connect_timeout_ms = connect_timeout_ms;
+             o.socket_timeout_ms = socket_timeout_ms;
+             o.request_timeout_ms = request_timeout_ms;
+             o.max_retries = std::max(0, max_retries);
+             u.set_s3(mount_id, host, port, bucket, ak, sk, region, parallel, part, upload_part, upload_inflight, o);
+           },
+           py::arg("mount_id"), py::arg("host"), py::arg("port"), py::arg("bucket"),
            py::arg("access_key"), py::arg("secret_key"), py::arg("region"), py::arg("parallel"), py::arg("part"),
-           py::arg("upload_part") = 64u << 20, py::arg("upload_inflight") = 4)
+           py::arg("upload_part") = 64u << 20, py::arg("upload_inflight") = 4, py::arg("connect_timeout_ms") = 10000,
+           py::arg("socket_timeout_ms") = 50000, py::arg("request_timeout_ms") = 60000, py::arg("max_retries") = 3)
       .def("remove", &UfsMounts::remove, py::arg("mount_id"))
       .def("__len__", &UfsMounts::size)
       .def("resolve", [](const UfsMounts& r, int64_t mount_id, const std::string& path) -> py::object {
@@ -495,7 +508,7 @@ void bind_data_path(py::module_& m) {
           std::string v = b;
           return sha256_hex(v.data(), v.size());
         });
-  m.def("serve_block_reads", [](FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk,
+  m.def("serve_block_reads", [](FrameRpcServer& srv, uint32_t method, std::shared_ptr<BlockStore> store, uint64_t max_chunk,
                                 uint64_t window, std::shared_ptr<UfsMounts> mounts, uint32_t commit_method,
                                 uint64_t ufs_slot_bytes, int ufs_depth, int ufs_max_active) {
           auto stats = std::make_shared<DataServerStats>();
@@ -509,7 +522,7 @@ void bind_data_path(py::module_& m) {
         }, py::arg("server"), py::arg("method"), py::arg("store"), py::arg("max_chunk"), py::arg("window"),
         py::arg("mounts") = nullptr, py::arg("commit_method") = UINT32_MAX, py::arg("ufs_slot_bytes") = 8u << 20,
         py::arg("ufs_depth") = 3, py::arg("ufs_max_active") = 256, py::keep_alive<1, 3>());
-  m.def("serve_block_writes", [](FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
+  m.def("serve_block_writes", [](FrameRpcServer& srv, uint32_t method, uint32_t commit_method, std::shared_ptr<BlockStore> store,
                                  uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
                                  std::shared_ptr<UfsMounts> ufs_roots) {
           serve_block_writes(srv, method, commit_method, store, stage_bytes, stats, ufs_roots);

@@ -85,17 +85,11 @@ class StagingPool {
   std::vector<void*> pinned_set_;
 };
 
-// One D2H stream per I/O thread: staging copies of different connections never queue behind
-// each other on a shared stream.
-hipStream_t thread_stream(BlockStore* store) {
-  thread_local hipStream_t st = nullptr;
-  thread_local BlockStore* owner = nullptr;
-  if (owner != store) {
-    store->use_device();
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
-    owner = store;
-  }
-  return st;
+// One D2H stream per I/O thread (and device): staging copies of different connections never
+// queue behind each other on a shared stream.
+hipStream_t thread_stream(const StoreRef& store) {
+  store->use_device();
+  return thread_stream_on(store->device());
 }
 
 struct ReadRequestMsg {
@@ -213,10 +207,10 @@ int64_t now_ns() {
 
 class BlockReadStream : public NativeStream {
  public:
-  BlockReadStream(BlockStore* store, int64_t session, int64_t lock_id, int64_t block_id, uint64_t pos, uint64_t end,
+  BlockReadStream(StoreRef store, int64_t session, int64_t lock_id, int64_t block_id, uint64_t pos, uint64_t end,
                   uint64_t chunk, uint64_t window, bool device, bool unix_peer, std::shared_ptr<StagingPool> pool,
                   std::shared_ptr<DataServerStats> stats)
-      : store_(store), session_(session), lock_(lock_id), block_(block_id), pos_(pos), acked_(pos), end_(end),
+      : store_(std::move(store)), session_(session), lock_(lock_id), block_(block_id), pos_(pos), acked_(pos), end_(end),
         chunk_(chunk), window_(window), device_(device), unix_(unix_peer), pool_(std::move(pool)), stats_(std::move(stats)) {}
 
   ~BlockReadStream() override {
@@ -423,7 +417,7 @@ class BlockReadStream : public NativeStream {
     stats_->chunks.fetch_add(1, std::memory_order_relaxed);
   }
 
-  BlockStore* store_;
+  StoreRef store_;
   int64_t session_, lock_, block_;
   uint64_t pos_, acked_, end_, chunk_, window_;
   bool device_, unix_;
@@ -485,8 +479,16 @@ bool parse_ufs_opts(const std::string& b, UfsOpts* o) {
 class UfsReader {
  public:
   virtual ~UfsReader() = default;
-  // Exactly n bytes at `off` of the file into dst; false with *err set otherwise.
+  // Exactly n bytes at `off` of the file into dst; false with *err set (and status()) otherwise.
   virtual bool read(uint64_t off, uint64_t n, uint8_t* dst, std::string* err) = 0;
+  // gRPC status of the last failure: UNAVAILABLE for a UFS that timed out or dropped the
+  // connection after its retries, NOT_FOUND, CANCELLED, INTERNAL otherwise.
+  int status() const { return status_; }
+  // Polled by a read under way (an S3 GET looks at it every ~100 ms): set when the call is gone.
+  const std::atomic<bool>* cancel = nullptr;
+
+ protected:
+  int status_ = 13;
 };
 
 class LocalFileReader : public UfsReader {
@@ -501,6 +503,7 @@ class LocalFileReader : public UfsReader {
       if (r <= 0) {
         *err = r == 0 ? "unexpected end of the UFS file at " + std::to_string(off + done)
                       : std::string("pread: ") + std::strerror(errno);
+        status_ = r == 0 ? 11 : 13;      // OUT_OF_RANGE / INTERNAL
         return false;
       }
       done += (uint64_t)r;
@@ -520,10 +523,27 @@ class S3ObjectReader : public UfsReader {
     const std::string path = "/" + m_->bucket + "/" + key_;
     const std::string head = s3_header_lines(m_->cred, "GET", path, "", kEmptySha);
     const int64_t got = m_->reader->get_into(uri_encode_path(path), head, off, n, reinterpret_cast<uint64_t>(dst),
-                                             m_->parallel, m_->part);
+                                             m_->parallel, m_->part, cancel);
     if (got == (int64_t)n) return true;
-    *err = "S3 GET " + path + " [" + std::to_string(off) + ", +" + std::to_string(n) + ") failed: " +
-           (got == -404 ? std::string("not found") : std::to_string(got));
+    std::string why;
+    if (got == -404) {
+      why = "not found";
+      status_ = 5;
+    } else if (got == kHttpTimeout) {
+      why = "timed out (socket " + std::to_string(m_->http.socket_timeout_ms) + " ms, request " +
+            std::to_string(m_->http.request_timeout_ms) + " ms)";
+      status_ = 14;
+    } else if (got == kHttpCancelled) {
+      why = "cancelled";
+      status_ = 1;
+    } else if (got == kHttpTransportError) {
+      why = "connection failed after " + std::to_string(m_->http.max_retries) + " retries";
+      status_ = 14;
+    } else {
+      why = "HTTP " + std::to_string(-got);
+      status_ = HttpRangeReader::retryable(got) ? 14 : 13;
+    }
+    *err = "S3 GET " + path + " [" + std::to_string(off) + ", +" + std::to_string(n) + ") " + why;
     return false;
   }
 
@@ -546,6 +566,8 @@ struct ColdState {
   std::vector<Slot> slots;
   bool cancelled = false, read_done = false, failed = false, job_exited = false, caching = false;
   bool handed_off = false;      // the cached block went to the commit: its session is not ours
+  std::atomic<bool> cancel_flag{false};   // `cancelled`, for a UFS read under way to poll
+  int err_status = 13;          // gRPC status of the failure (UNAVAILABLE: the UFS timed out / dropped)
   std::string err;
   std::function<void()> wake;
   std::shared_ptr<StagingPool> pool;
@@ -558,7 +580,7 @@ struct ColdState {
 };
 
 struct ColdJob {
-  BlockStore* store;
+  StoreRef store;
   int64_t session, block;
   uint64_t start, end, block_len, file_off, slot_bytes;
   bool want_cache;
@@ -585,10 +607,12 @@ struct ColdJob {
     std::string err;
     bool ok = true;
     uint64_t ingested = start;
+    int err_status = 13;
+    reader->cancel = &st->cancel_flag;
     try {
       if (store->has_device()) {
         store->use_device();
-        if (hipStreamCreateWithFlags(&hs, hipStreamNonBlocking) != hipSuccess) hs = nullptr;
+        hs = thread_stream_on(store->device());   // the pool thread's stream (never one per read)
       }
       if (want_cache) {
         try {   // may evict (the I/O thread never waits for space: this thread does)
@@ -623,6 +647,7 @@ struct ColdJob {
         const uint64_t n = std::min(slot_bytes, end - off);
         if (!reader->read(file_off + off, n, sl->buf, &err)) {
           ok = false;
+          err_status = reader->status();
           break;
         }
         stats->cold_bytes.fetch_add(n, std::memory_order_relaxed);
@@ -653,7 +678,6 @@ struct ColdJob {
         ok = false;
         err = "H2D into the block failed";
       }
-      (void)hipStreamDestroy(hs);
     }
     // UnderFileSystemBlockReader.close: a block read through to its end is committed -- also when
     // the client went away after the last byte -- anything less is aborted
@@ -666,6 +690,7 @@ struct ColdJob {
       if (!ok) {
         st->failed = true;
         st->err = err;
+        st->err_status = err_status;
       }
       st->read_done = true;
       st->job_exited = true;
@@ -698,9 +723,67 @@ struct ColdJob {
   }
 };
 
+// Threads of the native cold reads, shared by every data server of the process: a thread is
+// spawned only while every one is busy, up to the largest ufs.read.max.active any server asked for
+// (make_cold_stream admits at most that many reads per server); idle threads wait for the next
+// read, so a read costs no thread creation and no HIP stream (each thread keeps its own).
+class ColdPool {
+ public:
+  static ColdPool& get() {
+    static ColdPool* p = new ColdPool();   // immortal, like its threads
+    return *p;
+  }
+  bool submit(std::function<void()> f, int max_threads) {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(std::move(f));
+    if (q_.size() > idle_ && threads_ < std::max(1, max_threads)) {
+      try {
+        std::thread([this] { loop(); }).detach();
+        ++threads_;
+      } catch (...) {
+        if (threads_ == 0) {
+          q_.pop_back();
+          return false;
+        }
+      }
+    }
+    cv_.notify_one();
+    return true;
+  }
+  int threads() {
+    std::lock_guard<std::mutex> g(mu_);
+    return threads_;
+  }
+
+ private:
+  void loop() {
+    pthread_setname_np(pthread_self(), "ufs-cold-read");
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        ++idle_;
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        --idle_;
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      try {
+        f();
+      } catch (...) {
+      }
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  size_t idle_ = 0;
+  int threads_ = 0;
+};
+
 class ColdReadStream : public NativeStream {
  public:
-  ColdReadStream(BlockStore* store, int64_t session, int64_t block_id, uint64_t pos, uint64_t end, uint64_t chunk,
+  ColdReadStream(StoreRef store, int64_t session, int64_t block_id, uint64_t pos, uint64_t end, uint64_t chunk,
                  uint64_t window, uint64_t slot_bytes, bool unix_peer, std::shared_ptr<ColdState> st,
                  std::shared_ptr<DataServerStats> stats)
       : store_(store), session_(session), block_(block_id), start_(pos), pos_(pos), acked_(pos), end_(end),
@@ -712,6 +795,7 @@ class ColdReadStream : public NativeStream {
     {
       std::lock_guard<std::mutex> g(st_->mu);
       st_->cancelled = true;
+      st_->cancel_flag.store(true, std::memory_order_relaxed);   // a GET under way stops within ~100 ms
       st_->wake = nullptr;
       exited = st_->job_exited;
       handed_off = st_->handed_off;
@@ -769,16 +853,18 @@ class ColdReadStream : public NativeStream {
       const size_t idx = (size_t)((pos_ - start_) / slot_bytes_);
       ColdState::Slot* sl = &st_->slots[idx % depth];
       bool ready, failed;
+      int fail_status;
       std::string err;
       {
         std::lock_guard<std::mutex> g(st_->mu);
         ready = sl->ready && sl->off <= pos_ && pos_ < sl->off + sl->len;
         failed = st_->failed;
+        fail_status = st_->err_status;
         err = st_->err;
       }
       if (!ready) {
         if (failed) {
-          *status = 13;
+          *status = fail_status;
           *msg = "UFS read of block " + std::to_string(block_) + ": " + err;
           return w ? (ssize_t)w : -1;
         }
@@ -807,7 +893,7 @@ class ColdReadStream : public NativeStream {
     st_->cv.notify_all();
   }
 
-  BlockStore* store_;
+  StoreRef store_;
   int64_t session_, block_;
   uint64_t start_, pos_, acked_, end_, chunk_, window_, slot_bytes_;
   bool unix_;
@@ -1036,7 +1122,7 @@ class WriteStreamBase : public NativeStream {
 
 class BlockWriteStream : public WriteStreamBase {
  public:
-  BlockWriteStream(BlockStore* store, int64_t session, int64_t block_id, uint64_t pos, bool pin, bool device,
+  BlockWriteStream(StoreRef store, int64_t session, int64_t block_id, uint64_t pos, bool pin, bool device,
                    uint32_t commit_method, std::shared_ptr<StagingPool> pool, std::shared_ptr<DataServerStats> stats)
       : store_(store), session_(session), block_(block_id), pos_(pos), pin_(pin), device_(device),
         commit_(commit_method), pool_(std::move(pool)), stats_(std::move(stats)) {}
@@ -1163,7 +1249,7 @@ class BlockWriteStream : public WriteStreamBase {
   Slot slot_[2];
   int cur_ = 0;
 
-  BlockStore* store_;
+  StoreRef store_;
   int64_t session_, block_;
   uint64_t pos_;
   bool pin_, device_;
@@ -1246,24 +1332,6 @@ class FilePool {
   std::deque<std::function<void()>> q_;
 };
 
-// A non-blocking stream on the store's device for one AppendBlock copy (created per block: a pool
-// thread serves files of any store in the process, so it keeps no per-thread stream).
-struct OwnStream {
-  hipStream_t s = nullptr;
-  explicit OwnStream(int device) {
-    int prev = 0;
-    if (hipGetDevice(&prev) != hipSuccess) return;
-    if (hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
-      s = nullptr;
-    (void)hipSetDevice(prev);
-  }
-  ~OwnStream() {
-    if (s) (void)hipStreamDestroy(s);
-  }
-  OwnStream(const OwnStream&) = delete;
-  OwnStream& operator=(const OwnStream&) = delete;
-};
-
 // Pinned 8 MiB pieces for AppendBlock copies, shared by every stream of the process (per device):
 // a small CACHE_THROUGH file must not pay a pinned allocation of its own.
 constexpr uint64_t kTeePiece = 8ull << 20;
@@ -1304,7 +1372,7 @@ struct LocalFileJob {
   };
   std::deque<Item> chunks;
   uint64_t queued = 0, written = 0;   // bytes
-  BlockStore* store = nullptr;        // source of appended blocks
+  StoreRef store;                     // source of appended blocks
   int64_t session = 0;
 
   ~LocalFileJob() {
@@ -1388,7 +1456,6 @@ struct LocalFileJob {
     }
     constexpr uint64_t kPiece = kTeePiece;
     const bool dev = store->has_device();
-    std::unique_ptr<OwnStream> own;
     std::unique_ptr<TeePieces> pieces_buf;      // declared before the stream sync that frees them
     hipStream_t st = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
@@ -1396,9 +1463,10 @@ struct LocalFileJob {
     try {
       pieces_buf.reset(new TeePieces(store->device(), 2));
       if (dev) {
-        own.reset(new OwnStream(store->device()));
-        if (!own->s) throw std::runtime_error("hipStreamCreate failed");
-        st = own->s;
+        // this pool thread's stream on the device: the copy never waits behind the store's
+        // internal stream, and pool threads do not create a stream per block
+        store->use_device();
+        st = thread_stream_on(store->device());
         for (auto& x : ev)
           if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess)
             throw std::runtime_error("hipEventCreate failed");
@@ -1529,7 +1597,7 @@ class UfsFileWriteStream : public WriteStreamBase {
   static constexpr uint64_t kMaxQueued = 32ull << 20;
 
   UfsFileWriteStream(const std::string& path, int mode, std::shared_ptr<DataServerStats> stats,
-                     BlockStore* store = nullptr)
+                     StoreRef store = nullptr)
       : j_(std::make_shared<LocalFileJob>()) {
     j_->path = path;
     j_->mode = mode;
@@ -1804,7 +1872,7 @@ struct S3Upload {
   // AppendBlock on a pool thread: block `id` ([0, n)) of the worker's store goes into the parts,
   // read-locked and copied out in 8 MiB pieces through a pinned bounce buffer.  Clears `appending`
   // and wakes the stream when done; a failure fails the upload (aborted like any other).
-  static void append_block(std::shared_ptr<S3Upload> u, BlockStore* store, int64_t session, int64_t id, uint64_t n) {
+  static void append_block(std::shared_ptr<S3Upload> u, StoreRef store, int64_t session, int64_t id, uint64_t n) {
     std::string e;
     int64_t lock = -1;
     try {
@@ -1816,15 +1884,15 @@ struct S3Upload {
     if (e.empty()) {
       constexpr uint64_t kPiece = kTeePiece;
       std::unique_ptr<TeePieces> piece;
-      std::unique_ptr<OwnStream> own;
+      hipStream_t own = nullptr;
       try {
         piece.reset(new TeePieces(store->device(), 1));
         uint8_t* bounce = piece->b[0];
         if (store->has_device()) {
-          own.reset(new OwnStream(store->device()));
-          if (!own->s) throw std::runtime_error("hipStreamCreate failed");
+          store->use_device();
+          own = thread_stream_on(store->device());
         }
-        const uint64_t st = own ? reinterpret_cast<uint64_t>(own->s) : 0;
+        const uint64_t st = reinterpret_cast<uint64_t>(own);
         for (uint64_t off = 0; off < n;) {
           {
             std::lock_guard<std::mutex> g(u->mu);
@@ -1840,9 +1908,8 @@ struct S3Upload {
       } catch (const std::exception& x) {
         e = std::string("appending block ") + std::to_string(id) + ": " + x.what();
       }
-      if (own && own->s) (void)hipStreamSynchronize(own->s);   // nothing in flight into the piece
+      if (own) (void)hipStreamSynchronize(own);   // nothing in flight into the piece
       piece.reset();
-      own.reset();
       try {
         store->unlock(lock);
       } catch (...) {
@@ -1864,12 +1931,16 @@ struct S3Upload {
     u->stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);   // the store is not used past here
   }
 
+  // One S3 call (retried inside the reader on 5xx / SlowDown / resets / timeouts).  Part and object
+  // PUTs stop early once the stream is cancelled; Complete / Abort always run to their end.
   int send(const std::string& method, const std::string& query, const uint8_t* body, uint64_t n, std::string* resp,
-           std::string* etag, const std::string& payload_hash = "UNSIGNED-PAYLOAD") {
+           std::string* etag, const std::string& payload_hash = "UNSIGNED-PAYLOAD", bool cancellable = false) {
     const std::string head = s3_header_lines(m->cred, method, path, query, payload_hash);
     const std::string target = uri_encode_path(path) + (query.empty() ? "" : "?" + query);
-    return m->reader->request(method, target, head, body, n, resp, etag);
+    return m->reader->request(method, target, head, body, n, resp, etag, cancellable ? &abort_flag : nullptr);
   }
+  std::atomic<bool> abort_flag{false};   // set with `cancelled`
+  int err_status = 13;                   // gRPC status of `err`
 
   void poke() {
     std::function<void()> w;
@@ -1917,9 +1988,15 @@ struct S3Upload {
     bool ok = skip ? false : u->ensure_init(&e);
     if (ok) {
       const std::string q = "partNumber=" + std::to_string(num) + "&uploadId=" + query_escape(u->upload_id);
-      const int code = u->send("PUT", q, buf, n, nullptr, &etag);
+      const int code = u->send("PUT", q, buf, n, nullptr, &etag, "UNSIGNED-PAYLOAD", true);
       ok = code == 200 || code == 204;
-      if (!ok) e = "UploadPart " + std::to_string(num) + " of " + u->path + " failed: " + std::to_string(code);
+      if (!ok) {
+        e = "UploadPart " + std::to_string(num) + " of " + u->path + " failed after retries: " + std::to_string(code);
+        if (HttpRangeReader::retryable(code)) {
+          std::lock_guard<std::mutex> g(u->mu);
+          u->err_status = 14;   // UNAVAILABLE: the store kept failing / timing out
+        }
+      }
       else u->stats->ufs_write_bytes.fetch_add(n, std::memory_order_relaxed);
     }
     bool last;
@@ -1984,7 +2061,7 @@ struct S3Upload {
 class S3UfsWriteStream : public WriteStreamBase {
  public:
   S3UfsWriteStream(std::shared_ptr<const S3Mount> m, const std::string& key, std::shared_ptr<DataServerStats> stats,
-                   BlockStore* store)
+                   StoreRef store)
       : u_(std::make_shared<S3Upload>()), store_(store), session_(g_session.fetch_add(1)) {
     u_->part = m->upload_part;
     u_->max_bufs = m->upload_inflight + 1;
@@ -1998,7 +2075,10 @@ class S3UfsWriteStream : public WriteStreamBase {
     {
       std::lock_guard<std::mutex> g(u_->mu);
       u_->wake = nullptr;
-      if (!u_->finished && !(u_->finishing && !u_->failed)) u_->cancelled = true;   // abandoned: abort
+      if (!u_->finished && !(u_->finishing && !u_->failed)) {   // abandoned: abort
+        u_->cancelled = true;
+        u_->abort_flag.store(true, std::memory_order_relaxed);
+      }
       idle = u_->inflight == 0 && !u_->appending;
     }
     u_->cv.notify_all();               // an AppendBlock task waiting for a buffer stops
@@ -2064,7 +2144,7 @@ class S3UfsWriteStream : public WriteStreamBase {
     if (end_pending_) try_finish();
     {
       std::lock_guard<std::mutex> g(u_->mu);
-      if (u_->failed && !err_) fail(13, u_->err);
+      if (u_->failed && !err_) fail(u_->err_status, u_->err);
       else if (u_->finished && !done_ && !err_ && submitted_end_) {
         out_ += write_response_frame(pos_);
         done_ = true;
@@ -2099,7 +2179,7 @@ class S3UfsWriteStream : public WriteStreamBase {
           u_->appending = true;
         }
         auto u = u_;
-        BlockStore* st = store_;
+        StoreRef st = store_;
         const int64_t ses = session_, id = f.block;
         const uint64_t n = f.len;
         pending_.pop_front();
@@ -2132,7 +2212,7 @@ class S3UfsWriteStream : public WriteStreamBase {
       auto u = u_;
       UploadPool::get().submit([u, b, n] {
         std::string e;
-        const int code = u->send("PUT", "", b, n, nullptr, nullptr);
+        const int code = u->send("PUT", "", b, n, nullptr, nullptr, "UNSIGNED-PAYLOAD", true);
         if (code == 200 || code == 204) u->stats->ufs_write_bytes.fetch_add(n, std::memory_order_relaxed);
         std::lock_guard<std::mutex> g(u->mu);
         if (code != 200 && code != 204 && !u->failed) {
@@ -2162,7 +2242,7 @@ class S3UfsWriteStream : public WriteStreamBase {
   }
 
   std::shared_ptr<S3Upload> u_;
-  BlockStore* store_;
+  StoreRef store_;
   int64_t session_;
   uint64_t pos_ = 0;
   std::deque<Pending> pending_;
@@ -2190,8 +2270,10 @@ void UfsMounts::remove(int64_t mount_id) {
 
 void UfsMounts::set_s3(int64_t mount_id, const std::string& host, int port, const std::string& bucket,
                        const std::string& access_key, const std::string& secret_key, const std::string& region,
-                       int parallel, uint64_t part, uint64_t upload_part, int upload_inflight) {
+                       int parallel, uint64_t part, uint64_t upload_part, int upload_inflight,
+                       const HttpOptions& http) {
   auto m = std::make_shared<S3Mount>();
+  m->http = http;
   m->upload_part = std::max<uint64_t>(upload_part, 64u << 10);
   m->upload_inflight = std::max(1, upload_inflight);
   m->host = host;
@@ -2203,7 +2285,7 @@ void UfsMounts::set_s3(int64_t mount_id, const std::string& host, int port, cons
   m->cred.region = region.empty() ? "us-east-1" : region;
   m->parallel = std::max(1, parallel);
   m->part = std::max<uint64_t>(part, 64u << 10);
-  m->reader = std::make_shared<HttpRangeReader>(host, port, 2 * m->parallel);
+  m->reader = std::make_shared<HttpRangeReader>(host, port, 2 * m->parallel, m->http);
   std::lock_guard<std::mutex> g(mu_);
   s3_[mount_id] = std::move(m);
 }
@@ -2263,7 +2345,7 @@ namespace {
 
 // A native cold stream for `r` (the block is not in the store), or nullptr to hand the call to
 // Python (mount not registered, UFS-tier block, too many readers).
-std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, BlockStore* store, uint64_t max_chunk,
+std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const StoreRef& store, uint64_t max_chunk,
                                                uint64_t window, bool unix_peer, const ColdReadConfig& cfg,
                                                const std::shared_ptr<UfsMounts>& mounts,
                                                const std::shared_ptr<StagingPool>& slot_pool,
@@ -2329,9 +2411,7 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, BlockSto
   std::unique_ptr<NativeStream> ns(new ColdReadStream(store, job->session, r.block_id, off, end, chunk, window,
                                                       slot_pool->size(), unix_peer, st, stats));
   stats->cold_streams.fetch_add(1, std::memory_order_relaxed);
-  try {
-    std::thread([job] { job->run(); }).detach();
-  } catch (...) {
+  if (!ColdPool::get().submit([job] { job->run(); }, cfg.max_active)) {
     stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
     *status = 8;
     *msg = "cannot start a UFS reader thread";
@@ -2342,7 +2422,7 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, BlockSto
 
 }  // namespace
 
-void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk, uint64_t window,
+void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uint64_t max_chunk, uint64_t window,
                        std::shared_ptr<DataServerStats> stats, std::shared_ptr<UfsMounts> mounts, ColdReadConfig cold) {
   if (max_chunk == 0) max_chunk = 2u << 20;
   if (window == 0) window = 4u << 20;
@@ -2414,7 +2494,7 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
   });
 }
 
-void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
+void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, StoreRef store,
                         uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
                         std::shared_ptr<UfsMounts> ufs_roots) {
   if (stage_bytes == 0) stage_bytes = 4u << 20;

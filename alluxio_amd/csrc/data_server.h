@@ -31,6 +31,10 @@
 
 namespace amdx {
 
+// The store a server's streams and background tasks share: a cold reader or an AppendBlock task
+// that outlives its call (or the server) keeps the store alive until it is done.
+using StoreRef = std::shared_ptr<BlockStore>;
+
 struct DataServerStats {
   std::atomic<uint64_t> streams{0};      // calls served natively
   std::atomic<uint64_t> declined{0};     // calls handed to Python
@@ -64,6 +68,7 @@ struct S3Mount {
   uint64_t part = 4u << 20;    // minimum sub-range
   uint64_t upload_part = 64u << 20;   // multipart upload part of a UFS_FILE write
   int upload_inflight = 4;            // part buffers of one write (bounded memory)
+  HttpOptions http;                   // timeouts / retries (alluxio.underfs.s3.*)
   std::shared_ptr<HttpRangeReader> reader;
 };
 
@@ -76,7 +81,8 @@ class UfsMounts {
   void set(int64_t mount_id, const std::string& root);
   void set_s3(int64_t mount_id, const std::string& host, int port, const std::string& bucket,
               const std::string& access_key, const std::string& secret_key, const std::string& region,
-              int parallel, uint64_t part, uint64_t upload_part = 64u << 20, int upload_inflight = 4);
+              int parallel, uint64_t part, uint64_t upload_part = 64u << 20, int upload_inflight = 4,
+              const HttpOptions& http = HttpOptions());
   void remove(int64_t mount_id);
   size_t size() const;
   // The local path of `ufs_path` ("file:///x" or "/x") if mount `mount_id` is a registered local
@@ -111,7 +117,7 @@ struct ColdReadConfig {
 // soon as it lands; at the end the block is committed through `cold.commit_method` in Python (CRC,
 // master report) before the call ends.  A partial, offset or no_cache read streams the range
 // without caching; a cancelled or failed read-through aborts the temp block.
-void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, uint64_t max_chunk,
+void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uint64_t max_chunk,
                        uint64_t window, std::shared_ptr<DataServerStats> stats,
                        std::shared_ptr<UfsMounts> mounts = nullptr, ColdReadConfig cold = ColdReadConfig());
 
@@ -126,7 +132,7 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, BlockStore* store, 
 // whose parts go out on upload threads while the client streams (S3ALowLevelOutputStream), with
 // the request window held back while every part buffer is in flight.  Other UFS_FILE and
 // UFS_FALLBACK_BLOCK writes go to the Python servicer.
-void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, BlockStore* store,
+void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, StoreRef store,
                         uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
                         std::shared_ptr<UfsMounts> ufs_roots = nullptr);
 

@@ -1099,7 +1099,15 @@ void FrameRpcServer::accept_loop() {
 void FrameRpcServer::add_conn(int fd, bool unix_peer) {
   {
     int one = 1;
-    if (!unix_peer) ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    if (!unix_peer) {
+      ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    } else {
+      // a Unix stream socket's in-flight bytes count against the SENDER's buffer: the 208 KiB
+      // default caps every write at a few 16 KiB frames before the I/O thread has to wait for the
+      // reader (capped by net.core.wmem_max)
+      int sb = 8 << 20;
+      ::setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sb, sizeof(sb));
+    }
     std::shared_ptr<Conn> c;
     {
       std::lock_guard<std::mutex> g(conns_mu_);

@@ -15,6 +15,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cctype>
 #include <cerrno>
 #include <cstdio>
@@ -262,6 +263,39 @@ void BlobServer::stop() {
   fds_.clear();
 }
 
+void BlobServer::inject(int kind, const std::string& method, uint64_t nth, uint64_t count, int stall_ms) {
+  std::lock_guard<std::mutex> g(fault_mu_);
+  faults_.push_back(Fault{kind, method, nth ? nth - 1 : 0, count, stall_ms});
+}
+
+void BlobServer::clear_faults() {
+  std::lock_guard<std::mutex> g(fault_mu_);
+  faults_.clear();
+}
+
+int BlobServer::take_fault(const std::string& method, int* stall_ms) {
+  std::lock_guard<std::mutex> g(fault_mu_);
+  int kind = 0;
+  for (Fault& f : faults_) {
+    if (!f.left || (!f.method.empty() && f.method != method)) continue;
+    if (f.skip) {
+      --f.skip;
+      continue;
+    }
+    if (!kind) {           // the first armed fault wins; the others still count this request
+      kind = f.kind;
+      *stall_ms = f.stall_ms;
+      --f.left;
+    }
+  }
+  if (kind) ++injected_;
+  return kind;
+}
+
+void BlobServer::stall(int ms) const {
+  for (int t = 0; t < ms && running_; t += 20) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+}
+
 void BlobServer::accept_loop() {
   while (running_) {
     pollfd p{lfd_, POLLIN, 0};
@@ -425,6 +459,22 @@ void BlobServer::serve_conn(int fd) {
                          xml_escape(msg) + "</Message></Error>",
                      method == "HEAD");
       };
+      int fault_ms = 0;
+      const int fault = take_fault(method, &fault_ms);
+      if (fault == 1) {                 // 503 SlowDown, connection kept
+        body_string();
+        if (!error(503, "SlowDown", "Please reduce your request rate.") || !keep) goto done;
+        continue;
+      }
+      if (fault == 2) {                 // connection reset: RST instead of a FIN, nothing sent
+        linger lg{1, 0};
+        ::setsockopt(fd, SOL_SOCKET, SO_LINGER, &lg, sizeof lg);
+        goto done;
+      }
+      if (fault == 3) {                 // the server goes silent
+        stall(fault_ms);
+        goto done;
+      }
       // target -> bucket / key / query
       const size_t qm = target.find('?');
       const std::string path = pct_decode(target.substr(0, qm), false);
@@ -870,14 +920,19 @@ void BlobServer::serve_conn(int fd) {
               } else {
                 off_t o = (off_t)a;
                 uint64_t left = n;
-                while (left) {
-                  const ssize_t r = ::sendfile(fd, in, &o, (size_t)std::min<uint64_t>(left, 1ull << 30));
+                const uint64_t stop_at = fault == 4 ? n / 2 : 0;   // body stall: half, then silence
+                while (left > stop_at) {
+                  const ssize_t r = ::sendfile(fd, in, &o, (size_t)std::min<uint64_t>(left - stop_at, 1ull << 30));
                   if (r < 0 && (errno == EINTR || errno == EAGAIN)) continue;
                   if (r <= 0) break;
                   left -= (uint64_t)r;
                   bytes_ += (uint64_t)r;
                 }
                 ::close(in);
+                if (fault == 4) {
+                  stall(fault_ms);
+                  goto done;
+                }
                 ok = left == 0;
               }
             }
@@ -969,14 +1024,114 @@ done:
 // ------------------------------------------------------------------------------------------------
 // HttpRangeReader
 // ------------------------------------------------------------------------------------------------
-HttpRangeReader::HttpRangeReader(const std::string& host, int port, int max_idle)
-    : host_(host), port_(port), max_idle_((size_t)std::max(1, max_idle)) {}
+
+// One attempt's limits: the call's deadline (all attempts), the socket's silence limit, a cancel
+// flag.  Sockets carry a short SO_RCVTIMEO/SO_SNDTIMEO slice, so a blocked recv/send comes back
+// every kSliceMs to look at these without a poll() per call on the fast path.
+struct HttpRangeReader::Io {
+  int64_t deadline_ns = 0;            // 0 = none
+  int socket_ms = 0;                  // 0 = no silence limit
+  const std::atomic<bool>* cancel = nullptr;
+  int64_t err = 0;                    // first failure of the attempt: kHttp* code
+  bool expired() const { return deadline_ns && mono_ns() >= deadline_ns; }
+  bool cancelled() const { return cancel && cancel->load(std::memory_order_relaxed); }
+  static int64_t mono_ns() {
+    timespec t;
+    ::clock_gettime(CLOCK_MONOTONIC, &t);
+    return (int64_t)t.tv_sec * 1000000000LL + t.tv_nsec;
+  }
+};
+
+namespace {
+constexpr int kSliceMs = 100;
+
+// Waits out one EAGAIN of a socket with a SO_*TIMEO slice: false (with io.err set) once the call is
+// cancelled, past its deadline, or the socket has been silent for socket_ms since `since_ns`.
+template <class IoT>
+bool still_waiting(IoT& io, int64_t since_ns) {
+  if (io.cancelled()) {
+    io.err = kHttpCancelled;
+    return false;
+  }
+  const int64_t now = IoT::mono_ns();
+  if ((io.deadline_ns && now >= io.deadline_ns) ||
+      (io.socket_ms > 0 && now - since_ns >= (int64_t)io.socket_ms * 1000000LL)) {
+    io.err = kHttpTimeout;
+    return false;
+  }
+  return true;
+}
+
+template <class IoT>
+bool io_send_all(int fd, const char* p, size_t n, IoT& io) {
+  int64_t since = IoT::mono_ns();
+  while (n) {
+    const ssize_t r = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (r > 0) {
+      p += r;
+      n -= (size_t)r;
+      since = IoT::mono_ns();
+      continue;
+    }
+    if (r < 0 && errno == EINTR) continue;
+    if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      if (!still_waiting(io, since)) return false;
+      continue;
+    }
+    io.err = kHttpTransportError;
+    return false;
+  }
+  return true;
+}
+
+// Up to n bytes (at least 1); 0 with io.err set on EOF / error / timeout / cancel.
+template <class IoT>
+size_t io_recv_some(int fd, uint8_t* p, size_t n, IoT& io) {
+  const int64_t since = IoT::mono_ns();
+  for (;;) {
+    const ssize_t r = ::recv(fd, p, n, 0);
+    if (r > 0) return (size_t)r;
+    if (r < 0 && errno == EINTR) continue;
+    if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      if (!still_waiting(io, since)) return 0;
+      continue;
+    }
+    io.err = kHttpTransportError;       // EOF (a reset or a closed keep-alive) or an error
+    return 0;
+  }
+}
+
+template <class IoT>
+bool io_recv_all(int fd, uint8_t* p, size_t n, IoT& io) {
+  while (n) {
+    const size_t r = io_recv_some(fd, p, n, io);
+    if (!r) return false;
+    p += r;
+    n -= r;
+  }
+  return true;
+}
+
+void set_slices(int fd) {
+  timeval tv{0, kSliceMs * 1000};
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+}
+}  // namespace
+
+HttpRangeReader::HttpRangeReader(const std::string& host, int port, int max_idle, HttpOptions opts)
+    : host_(host), port_(port), max_idle_((size_t)std::max(1, max_idle)), opts_(opts) {}
 
 HttpRangeReader::~HttpRangeReader() {
   for (int fd : idle_) ::close(fd);
 }
 
-int HttpRangeReader::take(bool& reused) {
+bool HttpRangeReader::retryable(int64_t code) {
+  return code == kHttpTransportError || code == kHttpTimeout || code == -500 || code == -502 || code == -503 ||
+         code == -504 || code == -429 || code == 500 || code == 502 || code == 503 || code == 504 || code == 429;
+}
+
+int HttpRangeReader::take(bool& reused, Io& io) {
   {
     std::lock_guard<std::mutex> g(mu_);
     if (!idle_.empty()) {
@@ -990,19 +1145,59 @@ int HttpRangeReader::take(bool& reused) {
   addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_INET;
   hints.ai_socktype = SOCK_STREAM;
-  if (::getaddrinfo(host_.c_str(), std::to_string(port_).c_str(), &hints, &res) != 0 || !res) return -1;
-  const int fd = ::socket(res->ai_family, res->ai_socktype | SOCK_CLOEXEC, res->ai_protocol);
-  if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) != 0) {
-    ::close(fd);
-    ::freeaddrinfo(res);
+  if (::getaddrinfo(host_.c_str(), std::to_string(port_).c_str(), &hints, &res) != 0 || !res) {
+    io.err = kHttpTransportError;
     return -1;
   }
+  // non-blocking connect bounded by the connect timeout (and the call's deadline / cancel)
+  const int fd = ::socket(res->ai_family, res->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, res->ai_protocol);
+  int rc = fd < 0 ? -1 : ::connect(fd, res->ai_addr, res->ai_addrlen);
   ::freeaddrinfo(res);
-  if (fd < 0) return -1;
+  if (fd < 0) {
+    io.err = kHttpTransportError;
+    return -1;
+  }
+  if (rc != 0 && errno == EINPROGRESS) {
+    const int64_t t0 = Io::mono_ns();
+    const int64_t limit = (int64_t)std::max(1, opts_.connect_timeout_ms) * 1000000LL;
+    rc = -1;
+    for (;;) {
+      pollfd pf{fd, POLLOUT, 0};
+      const int pr = ::poll(&pf, 1, kSliceMs);
+      if (pr == 1) {
+        int e = 0;
+        socklen_t el = sizeof e;
+        rc = (::getsockopt(fd, SOL_SOCKET, SO_ERROR, &e, &el) == 0 && e == 0) ? 0 : -1;
+        if (rc != 0) io.err = kHttpTransportError;
+        break;
+      }
+      if (pr < 0 && errno != EINTR) {
+        io.err = kHttpTransportError;
+        break;
+      }
+      if (io.cancelled()) {
+        io.err = kHttpCancelled;
+        break;
+      }
+      if (io.expired() || Io::mono_ns() - t0 >= limit) {
+        io.err = kHttpTimeout;
+        break;
+      }
+    }
+  } else if (rc != 0) {
+    io.err = kHttpTransportError;
+  }
+  if (rc != 0) {
+    ::close(fd);
+    return -1;
+  }
+  const int fl = ::fcntl(fd, F_GETFL);
+  ::fcntl(fd, F_SETFL, fl & ~O_NONBLOCK);
   int one = 1;
   ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
   int rcv = 8 << 20;
   ::setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rcv, sizeof rcv);
+  set_slices(fd);
   ++connects_;
   return fd;
 }
@@ -1013,146 +1208,175 @@ void HttpRangeReader::give(int fd) {
   else ::close(fd);
 }
 
+bool HttpRangeReader::backoff(int attempt, Io& io) {
+  thread_local uint64_t seed = (uint64_t)Io::mono_ns() ^ (uint64_t)(uintptr_t)&seed;
+  seed = seed * 6364136223846793005ULL + 1442695040888963407ULL;
+  const int64_t cap = (int64_t)opts_.backoff_max_ms;
+  const int64_t exp = std::min<int64_t>(cap, (int64_t)opts_.backoff_base_ms << std::min(attempt - 1, 20));
+  const int64_t ms = exp / 2 + (int64_t)((seed >> 33) % (uint64_t)(exp / 2 + 1));   // "equal jitter"
+  const int64_t until = Io::mono_ns() + ms * 1000000LL;
+  while (Io::mono_ns() < until) {
+    if (io.cancelled()) {
+      io.err = kHttpCancelled;
+      return false;
+    }
+    if (io.expired()) {
+      io.err = kHttpTimeout;
+      return false;
+    }
+    ::usleep((useconds_t)std::min<int64_t>(kSliceMs * 1000, std::max<int64_t>(1, (until - Io::mono_ns()) / 1000)));
+  }
+  return true;
+}
+
 int64_t HttpRangeReader::one(const std::string& target, const std::string& head, uint64_t off, uint64_t len,
-                             uint8_t* dst) {
+                             uint8_t* dst, Io& io) {
   const std::string req = "GET " + target + " HTTP/1.1\r\n" + head +
                           "Range: bytes=" + std::to_string(off) + "-" + std::to_string(off + len - 1) + "\r\n\r\n";
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  int stale = 0;                         // pooled connections the server had closed: free retries
+  for (int attempt = 0;;) {
+    io.err = 0;
     bool reused = false;
-    const int fd = take(reused);
-    if (fd < 0) return -1;
-    ++requests_;
-    if (!send_all(fd, req.data(), req.size())) {
-      ::close(fd);
-      if (reused) continue;
-      return -1;
-    }
-    std::string hb;
-    char tmp[16384];
-    size_t hend = std::string::npos;
-    bool fail = false;
-    while ((hend = hb.find("\r\n\r\n")) == std::string::npos) {
-      const ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
-      if (r < 0 && errno == EINTR) continue;
-      if (r <= 0 || hb.size() > kMaxHead) {
-        fail = true;
-        break;
-      }
-      hb.append(tmp, (size_t)r);
-    }
-    if (fail) {
-      ::close(fd);
-      if (reused && hb.empty()) continue;   // a pooled connection the server had closed
-      return -1;
-    }
-    int code = 0;
-    if (hb.size() > 12) code = std::atoi(hb.c_str() + 9);
-    uint64_t clen = 0;
-    bool close_after = false;
-    for (size_t p = hb.find("\r\n"); p != std::string::npos && p < hend;) {
-      const size_t e = hb.find("\r\n", p + 2);
-      const std::string l = lower(hb.substr(p + 2, e - p - 2));
-      if (starts_with(l, "content-length:")) clen = std::stoull(l.substr(15));
-      if (starts_with(l, "connection:") && l.find("close") != std::string::npos) close_after = true;
-      p = e;
-    }
-    const size_t have = hb.size() - (hend + 4);
-    const uint8_t* pre = reinterpret_cast<const uint8_t*>(hb.data() + hend + 4);
-    // the body: the requested range lands in dst, anything else is drained
-    uint64_t skip = 0, take_n = 0;
-    int64_t result;
-    if ((code == 206 && clen == len) || (code == 200 && clen == len && off == 0)) {
-      take_n = len;
-      result = (int64_t)len;
-    } else if (code == 200 && clen >= off + len) {
-      skip = off;              // the server ignored the range: the object from byte 0
-      take_n = len;
-      result = (int64_t)len;
+    const int fd = take(reused, io);
+    int64_t result = 0;
+    if (fd < 0) {
+      result = io.err ? io.err : kHttpTransportError;
     } else {
-      result = code ? -(int64_t)code : -1;
-    }
-    uint64_t pos = 0;          // body bytes consumed
-    auto consume = [&](const uint8_t* p, size_t n) {
-      for (size_t i = 0; i < n;) {
-        if (pos < skip) {
-          const size_t k = (size_t)std::min<uint64_t>(skip - pos, n - i);
-          pos += k;
-          i += k;
-        } else if (pos < skip + take_n) {
-          const size_t k = (size_t)std::min<uint64_t>(skip + take_n - pos, n - i);
-          std::memcpy(dst + (pos - skip), p + i, k);
-          pos += k;
-          i += k;
+      ++requests_;
+      std::string hb;
+      char tmp[16384];
+      size_t hend = std::string::npos;
+      bool fail = !io_send_all(fd, req.data(), req.size(), io);
+      while (!fail && (hend = hb.find("\r\n\r\n")) == std::string::npos) {
+        const size_t r = io_recv_some(fd, reinterpret_cast<uint8_t*>(tmp), sizeof tmp, io);
+        if (!r || hb.size() > kMaxHead) {
+          if (!io.err) io.err = kHttpTransportError;
+          fail = true;
+          break;
+        }
+        hb.append(tmp, r);
+      }
+      if (fail) {
+        ::close(fd);
+        if (reused && hb.empty() && io.err == kHttpTransportError && stale++ < 4) continue;
+        result = io.err;
+      } else {
+        int code = 0;
+        if (hb.size() > 12) code = std::atoi(hb.c_str() + 9);
+        uint64_t clen = 0;
+        bool close_after = false;
+        for (size_t p = hb.find("\r\n"); p != std::string::npos && p < hend;) {
+          const size_t e = hb.find("\r\n", p + 2);
+          const std::string l = lower(hb.substr(p + 2, e - p - 2));
+          if (starts_with(l, "content-length:")) clen = std::stoull(l.substr(15));
+          if (starts_with(l, "connection:") && l.find("close") != std::string::npos) close_after = true;
+          p = e;
+        }
+        const size_t have = hb.size() - (hend + 4);
+        const uint8_t* pre = reinterpret_cast<const uint8_t*>(hb.data() + hend + 4);
+        // the body: the requested range lands in dst, anything else is drained
+        uint64_t skip = 0, take_n = 0;
+        if ((code == 206 && clen == len) || (code == 200 && clen == len && off == 0)) {
+          take_n = len;
+          result = (int64_t)len;
+        } else if (code == 200 && clen >= off + len) {
+          skip = off;              // the server ignored the range: the object from byte 0
+          take_n = len;
+          result = (int64_t)len;
         } else {
-          pos += n - i;
-          i = n;
+          result = code ? -(int64_t)code : kHttpTransportError;
+        }
+        uint64_t pos = 0;          // body bytes consumed
+        auto consume = [&](const uint8_t* p, size_t n) {
+          for (size_t i = 0; i < n;) {
+            if (pos < skip) {
+              const size_t k = (size_t)std::min<uint64_t>(skip - pos, n - i);
+              pos += k;
+              i += k;
+            } else if (pos < skip + take_n) {
+              const size_t k = (size_t)std::min<uint64_t>(skip + take_n - pos, n - i);
+              std::memcpy(dst + (pos - skip), p + i, k);
+              pos += k;
+              i += k;
+            } else {
+              pos += n - i;
+              i = n;
+            }
+          }
+        };
+        consume(pre, (size_t)std::min<uint64_t>(have, clen));
+        bool ok = true;
+        while (ok && pos < clen) {
+          if (pos >= skip && pos < skip + take_n) {
+            const size_t k = (size_t)(skip + take_n - pos);     // straight into the destination
+            if (!io_recv_all(fd, dst + (pos - skip), k, io)) ok = false;
+            else pos += k;
+          } else {
+            const size_t k = (size_t)std::min<uint64_t>(clen - pos, sizeof tmp);
+            const size_t r = io_recv_some(fd, reinterpret_cast<uint8_t*>(tmp), k, io);
+            if (!r) ok = false;
+            else consume(reinterpret_cast<const uint8_t*>(tmp), r);
+          }
+        }
+        if (!ok) {
+          ::close(fd);
+          result = io.err ? io.err : kHttpTransportError;   // a short body: the whole range again
+        } else if (close_after) {
+          ::close(fd);
+        } else {
+          give(fd);
         }
       }
-    };
-    consume(pre, (size_t)std::min<uint64_t>(have, clen));
-    bool ok = true;
-    while (ok && pos < clen) {
-      if (pos >= skip && pos < skip + take_n) {
-        // straight into the destination
-        const size_t k = (size_t)(skip + take_n - pos);
-        if (!recv_all(fd, dst + (pos - skip), k)) ok = false;
-        else pos += k;
-      } else {
-        const size_t k = (size_t)std::min<uint64_t>(clen - pos, sizeof tmp);
-        const ssize_t r = ::recv(fd, tmp, k, 0);
-        if (r < 0 && errno == EINTR) continue;
-        if (r <= 0) ok = false;
-        else consume(reinterpret_cast<const uint8_t*>(tmp), (size_t)r);
-      }
     }
-    if (!ok) {
-      ::close(fd);
-      return -1;
+    if (result >= 0 || !retryable(result) || attempt >= opts_.max_retries) {
+      if (result == kHttpTimeout) ++timeouts_;
+      return result;
     }
-    if (close_after) ::close(fd);
-    else give(fd);
-    return result;
+    ++attempt;
+    ++retries_;
+    if (!backoff(attempt, io)) {
+      if (io.err == kHttpTimeout) ++timeouts_;
+      return io.err;
+    }
   }
-  return -1;
 }
 
 int HttpRangeReader::put_from(const std::string& target, const std::string& head, uint64_t src, uint64_t len,
-                              std::string* etag) {
-  return request("PUT", target, head, reinterpret_cast<const uint8_t*>(src), len, nullptr, etag);
+                              std::string* etag, const std::atomic<bool>* cancel) {
+  return request("PUT", target, head, reinterpret_cast<const uint8_t*>(src), len, nullptr, etag, cancel);
 }
 
-int HttpRangeReader::request(const std::string& method, const std::string& target, const std::string& head,
-                             const uint8_t* body, uint64_t len, std::string* resp, std::string* etag) {
-  const std::string req = method + " " + target + " HTTP/1.1\r\n" + head + "Content-Length: " +
-                          std::to_string(len) + "\r\n\r\n";
-  for (int attempt = 0; attempt < 2; ++attempt) {
+int HttpRangeReader::request_once(const std::string& req, const uint8_t* body, uint64_t len, std::string* resp,
+                                  std::string* etag, Io& io) {
+  for (int stale = 0;;) {
+    io.err = 0;
     bool reused = false;
-    const int fd = take(reused);
-    if (fd < 0) return -1;
+    const int fd = take(reused, io);
+    if (fd < 0) return (int)(io.err ? io.err : kHttpTransportError);
     ++requests_;
-    if (!send_all(fd, req.data(), req.size()) ||
-        (len && !send_all(fd, reinterpret_cast<const char*>(body), (size_t)len))) {
+    if (!io_send_all(fd, req.data(), req.size(), io) ||
+        (len && !io_send_all(fd, reinterpret_cast<const char*>(body), (size_t)len, io))) {
       ::close(fd);
-      if (reused) continue;    // a pooled connection the server had closed: once more, fresh
-      return -1;
+      if (reused && io.err == kHttpTransportError && stale++ < 4) continue;   // closed keep-alive: fresh
+      return (int)io.err;
     }
     std::string hb;
     char tmp[16384];
     size_t hend;
     bool fail = false;
     while ((hend = hb.find("\r\n\r\n")) == std::string::npos) {
-      const ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
-      if (r < 0 && errno == EINTR) continue;
-      if (r <= 0 || hb.size() > kMaxHead) {
+      const size_t r = io_recv_some(fd, reinterpret_cast<uint8_t*>(tmp), sizeof tmp, io);
+      if (!r || hb.size() > kMaxHead) {
+        if (!io.err) io.err = kHttpTransportError;
         fail = true;
         break;
       }
-      hb.append(tmp, (size_t)r);
+      hb.append(tmp, r);
     }
     if (fail) {
       ::close(fd);
-      if (reused && hb.empty()) continue;
-      return -1;
+      if (reused && hb.empty() && io.err == kHttpTransportError && stale++ < 4) continue;
+      return (int)io.err;
     }
     const int code = hb.size() > 12 ? std::atoi(hb.c_str() + 9) : 0;
     uint64_t clen = 0;
@@ -1174,24 +1398,49 @@ int HttpRangeReader::request(const std::string& method, const std::string& targe
     if (resp) resp->assign(hb, hend + 4, std::string::npos);
     bool ok = true;
     while (ok && have < clen) {   // the body (kept up to 1 MiB), drained so the connection is reusable
-      const ssize_t r = ::recv(fd, tmp, (size_t)std::min<uint64_t>(clen - have, sizeof tmp), 0);
-      if (r < 0 && errno == EINTR) continue;
-      if (r <= 0) {
+      const size_t r = io_recv_some(fd, reinterpret_cast<uint8_t*>(tmp), (size_t)std::min<uint64_t>(clen - have, sizeof tmp), io);
+      if (!r) {
         ok = false;
       } else {
-        if (resp && resp->size() < (1u << 20)) resp->append(tmp, (size_t)r);
-        have += (uint64_t)r;
+        if (resp && resp->size() < (1u << 20)) resp->append(tmp, r);
+        have += r;
       }
     }
     if (!ok || close_after) ::close(fd);
     else give(fd);
-    return code ? code : -1;
+    if (!ok) return (int)(io.err ? io.err : kHttpTransportError);
+    return code ? code : (int)kHttpTransportError;
   }
-  return -1;
+}
+
+int HttpRangeReader::request(const std::string& method, const std::string& target, const std::string& head,
+                             const uint8_t* body, uint64_t len, std::string* resp, std::string* etag,
+                             const std::atomic<bool>* cancel) {
+  const std::string req = method + " " + target + " HTTP/1.1\r\n" + head + "Content-Length: " +
+                          std::to_string(len) + "\r\n\r\n";
+  Io io;
+  io.cancel = cancel;
+  io.socket_ms = opts_.socket_timeout_ms;
+  if (opts_.request_timeout_ms > 0) io.deadline_ns = Io::mono_ns() + (int64_t)opts_.request_timeout_ms * 1000000LL;
+  for (int attempt = 0;;) {
+    if (resp) resp->clear();
+    const int code = request_once(req, body, len, resp, etag, io);
+    if (!retryable(code) || attempt >= opts_.max_retries) {
+      if (code == kHttpTimeout) ++timeouts_;
+      return code;
+    }
+    ++attempt;
+    ++retries_;
+    if (!backoff(attempt, io)) {
+      if (io.err == kHttpTimeout) ++timeouts_;
+      return (int)io.err;
+    }
+  }
 }
 
 int64_t HttpRangeReader::get_into(const std::string& target, const std::string& head_lines, uint64_t offset,
-                                  uint64_t length, uint64_t dst, int parallel, uint64_t min_part) {
+                                  uint64_t length, uint64_t dst, int parallel, uint64_t min_part,
+                                  const std::atomic<bool>* cancel) {
   if (!length) return 0;
   uint8_t* const out = reinterpret_cast<uint8_t*>(dst);
   min_part = std::max<uint64_t>(min_part, 64 << 10);
@@ -1200,14 +1449,23 @@ int64_t HttpRangeReader::get_into(const std::string& target, const std::string& 
   uint64_t part = (length + nparts - 1) / nparts;
   part = (part + (64 << 10) - 1) & ~uint64_t((64 << 10) - 1);
   std::vector<int64_t> res((size_t)nparts, 0);
+  const int64_t deadline =
+      opts_.request_timeout_ms > 0 ? Io::mono_ns() + (int64_t)opts_.request_timeout_ms * 1000000LL : 0;
+  auto run = [&](size_t i, uint64_t a, uint64_t n) {
+    Io io;
+    io.cancel = cancel;
+    io.socket_ms = opts_.socket_timeout_ms;
+    io.deadline_ns = deadline;
+    res[i] = one(target, head_lines, offset + a, n, out + a, io);
+  };
   std::vector<std::thread> ts;
   for (uint64_t i = 1; i < nparts; ++i) {
     const uint64_t a = i * part;
     if (a >= length) break;
     const uint64_t n = std::min(part, length - a);
-    ts.emplace_back([&, i, a, n] { res[(size_t)i] = one(target, head_lines, offset + a, n, out + a); });
+    ts.emplace_back([&, i, a, n] { run((size_t)i, a, n); });
   }
-  res[0] = one(target, head_lines, offset, std::min(part, length), out);
+  run(0, 0, std::min(part, length));
   for (auto& t : ts) t.join();
   for (int64_t r : res)
     if (r < 0) return r;

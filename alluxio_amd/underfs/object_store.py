@@ -385,6 +385,32 @@ class ObjectUnderFileSystem(UnderFileSystem):
             return str(self.conf.get(name))
         return default
 
+    # errors that no retry can fix: the answer itself
+    _FINAL_ERRORS = (FileNotFoundError, FileExistsError, PermissionError, IsADirectoryError, NotADirectoryError)
+
+    def _retry(self, op, what: str):
+        """ObjectUnderFileSystem.retryOnException (ObjectUnderFileSystem.java:1153-1168): run ``op``
+        again after an I/O error -- a store that timed out, dropped the connection or kept answering
+        5xx past its client's own retries, or eventual consistency -- with the exponential back-off
+        of ``alluxio.underfs.eventual.consistency.retry.{base.sleep, max.sleep, max.num}``
+        (ExponentialBackoffRetry, :1194-1199).  The last error is raised when attempts run out."""
+        import logging
+        import time
+        from ..utils.format import parse_time_size
+        base = parse_time_size(self._opt("alluxio.underfs.eventual.consistency.retry.base.sleep", "50ms")) / 1000.0
+        cap = parse_time_size(self._opt("alluxio.underfs.eventual.consistency.retry.max.sleep", "30sec")) / 1000.0
+        tries = max(1, int(self._opt("alluxio.underfs.eventual.consistency.retry.max.num", "20")))
+        for attempt in range(1, tries + 1):
+            try:
+                return op()
+            except self._FINAL_ERRORS:
+                raise
+            except OSError as e:
+                if attempt >= tries:
+                    raise
+                logging.getLogger(__name__).debug("attempt %d to %s failed: %s", attempt, what, e)
+                time.sleep(min(cap, base * (2 ** (attempt - 1))))
+
     def _tmp_dir(self) -> str:
         import os
         d = self._opt("alluxio.tmp.dirs", "/tmp").split(",")[0].strip() or "/tmp"
@@ -443,7 +469,7 @@ class ObjectUnderFileSystem(UnderFileSystem):
 
     def open(self, path, options: OpenOptions | None = None):
         key = self._key(path)
-        meta = self._head(key)
+        meta = self._retry(lambda: self._head(key), f"open {path}")
         if meta is None:
             raise FileNotFoundError(path)
         off = options.offset if options else 0
@@ -469,6 +495,9 @@ class ObjectUnderFileSystem(UnderFileSystem):
         return True
 
     def get_status(self, path):
+        return self._retry(lambda: self._get_status(path), f"get status of {path}")
+
+    def _get_status(self, path):
         key = self._key(path).rstrip("/")
         name = posixpath.basename(key) or "/"
         if not key:

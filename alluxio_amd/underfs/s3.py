@@ -25,14 +25,31 @@ def _sign(key: bytes, msg: str) -> bytes:
     return hmac.new(key, msg.encode(), hashlib.sha256).digest()
 
 
+# HTTP statuses an S3 client retries (AWS SDK PredefinedRetryPolicies: throttling and 5xx)
+RETRYABLE_STATUS = frozenset((429, 500, 502, 503, 504))
+
+
 class S3Client:
+    """Signed S3 calls over a pooled ``requests`` session, with the reference client's limits
+    (S3AUnderFileSystem.java:150-191): ``socket_timeout`` bounds each wait on the socket,
+    ``request_timeout`` one call with all its attempts (0 = none), and a call failing with a
+    connection error, a timeout, 5xx or 429 (SlowDown) is retried ``max_retries`` times with capped
+    exponential back-off (AWS SDK default: 3)."""
+
     def __init__(self, endpoint: str, access_key: str = "", secret_key: str = "",
-                 region: str = "us-east-1", timeout: float = 60.0):
+                 region: str = "us-east-1", timeout: float = 60.0, socket_timeout: float = 50.0,
+                 connect_timeout: float = 10.0, max_retries: int = 3, backoff_base: float = 0.05,
+                 backoff_max: float = 2.0):
         import requests
         self.endpoint = endpoint.rstrip("/")
         self.access_key, self.secret_key, self.region = access_key, secret_key, region
         self.session = requests.Session()
-        self.timeout = timeout
+        self.timeout = timeout                  # request timeout (all attempts)
+        self.socket_timeout = socket_timeout
+        self.connect_timeout = min(connect_timeout, socket_timeout) if socket_timeout else connect_timeout
+        self.max_retries = max(0, int(max_retries))
+        self.backoff_base, self.backoff_max = backoff_base, backoff_max
+        self.retries = 0                        # attempts beyond the first, over the client's life
 
     def _headers(self, method, path, query: dict, payload_hash: str, extra=None) -> dict:
         host = urllib.parse.urlsplit(self.endpoint).netloc
@@ -61,18 +78,48 @@ class S3Client:
         return headers
 
     def request(self, method, bucket, key="", query=None, data=b"", headers=None, ok=(200, 204, 206)):
+        import random
+        import time
+
+        import requests
         query = query or {}
         path = f"/{bucket}/{key}" if key else f"/{bucket}"
         ph = hashlib.sha256(data).hexdigest() if data else _EMPTY_SHA
-        h = self._headers(method, path, query, ph, headers)
         url = self.endpoint + urllib.parse.quote(path, safe="/-_.~")
-        r = self.session.request(method, url, params=query or None, data=data or None, headers=h,
-                                 timeout=self.timeout)
-        if r.status_code not in ok:
-            if r.status_code == 404:
+        deadline = time.monotonic() + self.timeout if self.timeout else None
+        attempt = 0
+        while True:
+            h = self._headers(method, path, query, ph, headers)     # a fresh signature date per attempt
+            wait = self.socket_timeout or None
+            if deadline is not None:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    raise TimeoutError(f"S3 {method} {path}: request timeout ({self.timeout}s) exceeded")
+                wait = min(wait, left) if wait else left
+            err = None
+            try:
+                r = self.session.request(method, url, params=query or None, data=data or None, headers=h,
+                                         timeout=(min(self.connect_timeout, wait) if wait else self.connect_timeout,
+                                                  wait))
+            except (requests.ConnectionError, requests.Timeout) as e:
+                r, err = None, e
+            if r is not None and r.status_code in ok:
+                return r
+            if r is not None and r.status_code == 404:
                 raise FileNotFoundError(f"s3://{bucket}/{key}")
-            raise OSError(f"S3 {method} {path} failed: {r.status_code} {r.text[:200]}")
-        return r
+            retry = r is None or r.status_code in RETRYABLE_STATUS
+            if not retry or attempt >= self.max_retries:
+                if r is None:
+                    kind = TimeoutError if isinstance(err, requests.Timeout) else ConnectionError
+                    raise kind(f"S3 {method} {path} failed after {attempt} retries: {err}") from err
+                raise OSError(f"S3 {method} {path} failed: {r.status_code} {r.text[:200]}")
+            attempt += 1
+            self.retries += 1
+            cap = min(self.backoff_max, self.backoff_base * (2 ** (attempt - 1)))
+            pause = cap / 2 + random.random() * cap / 2
+            if deadline is not None:
+                pause = min(pause, max(0.0, deadline - time.monotonic()))
+            time.sleep(pause)
 
 
 def _parse_size(v) -> int:
@@ -114,9 +161,25 @@ class S3UnderFileSystem(ObjectUnderFileSystem):
             endpoint = "https://s3.amazonaws.com"
         if not endpoint.startswith("http"):
             endpoint = "http://" + endpoint
+        from ..utils.format import parse_time_size
+
+        def ms(*names, default):
+            v = opt(*names, default=default)
+            return parse_time_size(str(v)) if v not in (None, "") else 0
+        # the reference client's limits (S3AUnderFileSystem.java:150-191, PropertyKey.java:946-1002)
+        self.socket_timeout_ms = ms("alluxio.underfs.s3.socket.timeout", "alluxio.underfs.s3a.socket.timeout.ms",
+                                    "alluxio.underfs.s3a.socket.timeout", default="50sec")
+        self.request_timeout_ms = ms("alluxio.underfs.s3.request.timeout", "alluxio.underfs.s3a.request.timeout.ms",
+                                     "alluxio.underfs.s3a.request.timeout", default="1min")
+        retry = opt("alluxio.underfs.s3.max.error.retry", "alluxio.underfs.s3a.max.error.retry", default="")
+        self.max_retries = int(retry) if str(retry).strip() else 3          # AWS SDK default
+        self.connect_timeout_ms = min(10_000, self.socket_timeout_ms or 10_000)
         self.client = S3Client(endpoint, opt("s3a.accessKeyId", "aws.accessKeyId"),
                                opt("s3a.secretKey", "aws.secretKey"),
-                               opt("alluxio.underfs.s3.region", default="us-east-1"))
+                               opt("alluxio.underfs.s3.region", default="us-east-1"),
+                               timeout=self.request_timeout_ms / 1000.0,
+                               socket_timeout=self.socket_timeout_ms / 1000.0,
+                               connect_timeout=self.connect_timeout_ms / 1000.0, max_retries=self.max_retries)
         self.folder_suffix = opt("alluxio.underfs.s3.directory.suffix", default="/") or "/"
         # native data path (csrc/http_blob.cpp): ranged GETs received straight into the caller's
         # buffer over pooled keep-alive connections, a read split into parallel sub-ranges
@@ -211,10 +274,16 @@ class S3UnderFileSystem(ObjectUnderFileSystem):
             try:
                 from ..ops.native import lib
                 u = urllib.parse.urlsplit(self.client.endpoint)
-                self._native = lib().HttpRangeReader(u.hostname, u.port or 80, 2 * self._parallel)
+                self._native = lib().HttpRangeReader(u.hostname, u.port or 80, 2 * self._parallel,
+                                                     **self.http_limits())
             except Exception:  # noqa: BLE001 -- no native library: the requests path serves
                 self._native_on = False
         return self._native
+
+    def http_limits(self) -> dict:
+        """Timeouts and retries of the native client (csrc/http_blob.cpp HttpOptions)."""
+        return {"connect_timeout_ms": self.connect_timeout_ms, "socket_timeout_ms": self.socket_timeout_ms,
+                "request_timeout_ms": self.request_timeout_ms, "max_retries": self.max_retries}
 
     def _get_into(self, key, offset, length, addr) -> bool:
         """Ranged GET of ``length`` bytes at ``offset`` into host memory at ``addr`` (native path);
@@ -229,8 +298,10 @@ class S3UnderFileSystem(ObjectUnderFileSystem):
                           self._parallel, self._part)
         if got == -404:
             raise FileNotFoundError(f"s3://{self.bucket}/{key}")
+        if got == -2:
+            raise TimeoutError(f"S3 GET {path} [{offset}, +{length}) timed out")
         if got != length:
-            raise OSError(f"S3 GET {path} [{offset}, +{length}) failed: {got}")
+            raise OSError(f"S3 GET {path} [{offset}, +{length}) failed after retries: {got}")
         return True
 
     def _head(self, key):

@@ -385,7 +385,8 @@ class BlockWorker:
             if roots.resolve_s3(mount_id, f"s3://{ufs.bucket}/x") is None:
                 part, inflight = ufs.upload_shape()
                 roots.set_s3(mount_id, u.hostname, u.port or 80, ufs.bucket, ufs.client.access_key,
-                             ufs.client.secret_key, ufs.client.region, ufs._parallel, ufs._part, part, inflight)
+                             ufs.client.secret_key, ufs.client.region, ufs._parallel, ufs._part, part, inflight,
+                             **ufs.http_limits())
 
     note_local_ufs = note_ufs_mount
 

@@ -270,6 +270,25 @@ for s in $STEPS; do
       run ww_s3_ct_tee 600 python tools/worker_write_bench.py --s3 --threads 1,4,16 --files 2 --file-size 256m --write-type CACHE_THROUGH --client-prop alluxio.user.file.cache.through.tee.object.store.enabled=true --out "$OUT/r5_s3_cache_through_threads.jsonl"
       run ww_s3_ct_two 600 python tools/worker_write_bench.py --s3 --threads 1,4,16 --files 2 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r5_s3_cache_through_threads.jsonl"
       ;;
+    r6uds)
+      # round 6: one ReadBlock stream (and four) over the worker's Unix domain socket vs loopback TCP
+      for d in host cuda; do
+        for par in 1 4; do
+          run uds_${d}_p$par 300 python tools/remote_device_read_bench.py --uds --dest $d --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/r6_remote_read_uds.jsonl"
+          run tcp_${d}_p$par 300 python tools/remote_device_read_bench.py --dest $d --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/r6_remote_read_uds.jsonl"
+        done
+      done
+      ;;
+    r6large)
+      run bench_large_r6 400 python bench.py --steps 20 --warmup 5 --phases local,stagger,large
+      run copy_roof_r6 300 python tools/copy_roof.py --gib 4 --out "$OUT/r6_copy_roof.json"
+      run pmc_dram_large_r6 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum --kernel-trace --stats -d "$OUT/pmc_dram_large_r6" -o pmc --output-format csv -- python3 bench.py --steps 20 --warmup 2 --phases local,large
+      ;;
+    r6w8s)
+      # sustained 8 s writes, 64 MiB blocks (the round-6 commit target rows)
+      run ww8_mc 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --out "$OUT/r6_worker_write_8s.jsonl"
+      run ww8_ct 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r6_worker_write_8s.jsonl"
+      ;;
     validate)
       run pytest_gpu_validate 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       run smoke_validate 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"

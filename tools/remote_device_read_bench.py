@@ -94,6 +94,8 @@ def main(argv=None) -> int:
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
     ap.add_argument("--worker-prop", action="append", default=[], help="extra worker property k=v")
     ap.add_argument("--tier", default="hbm:0", help="worker tier path (hbm:0, or dram for a host-only box)")
+    ap.add_argument("--uds", action="store_true",
+                    help="the worker also listens on a Unix domain socket and the client reaches it there")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     import numpy as np
@@ -105,6 +107,11 @@ def main(argv=None) -> int:
             "alluxio.worker.tieredstore.level0.dirs.quota": str(size + (512 << 20)),
             "alluxio.worker.hbm.page.size": "2MB", "alluxio.user.block.size.bytes.default": "64MB",
             "alluxio.security.authorization.permission.enabled": "false"}
+    uds_dir = None
+    if a.uds:        # sun_path is limited to 108 bytes: a short directory under /tmp
+        uds_dir = tempfile.mkdtemp(prefix="uds", dir="/tmp")
+        conf["alluxio.worker.data.server.domain.socket.address"] = uds_dir
+        conf["alluxio.worker.data.server.domain.socket.as.uuid"] = "true"
     conf.update(dict(kv.split("=", 1) for kv in a.worker_prop))
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=tempfile.mkdtemp(prefix="rdbench_")) as c:
         fs = c.client()
@@ -117,7 +124,7 @@ def main(argv=None) -> int:
                 c.heartbeat_workers()
             ds = c.workers[0].data_server
             st0 = (ds.stats.cold_streams, ds.stats.declined, ds.stats.cold_cached, ds.stats.zero_copy_frames,
-                   ds.stats.prefetched) if ds is not None else None
+                   ds.stats.prefetched, ds.stats.domain_bytes) if ds is not None else None
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "false",
                      "alluxio.user.native.reader.enabled": str(native).lower(),
@@ -139,7 +146,7 @@ def main(argv=None) -> int:
                    "client": "native GrpcBlockSource + pinned H2D" if native else "grpcio stream + host copy",
                    "file_size": a.file_size, "read_size": a.read_size, "bytes": r["bytes"],
                    "seconds": round(r["seconds"], 3), "GBps": round(r["bytes"] / r["seconds"] / 1e9, 3),
-                   "client_props": a.client_prop, "worker_props": a.worker_prop, "cold": a.cold, "tier": a.tier,
+                   "transport": "uds" if a.uds else "tcp", "client_props": a.client_prop, "worker_props": a.worker_prop, "cold": a.cold, "tier": a.tier,
                    "client_cpu_cores": round(r["client_cpu_cores"], 2), "client_sys_cores": round(r["client_sys_cores"], 2),
                    # the worker's I/O threads (busiest one): 1.0 = that thread is the bound
                    "worker_io_busiest_cores": round(max((io1.get(k, 0) - io0.get(k, 0) for k in io1), default=0)
@@ -150,11 +157,15 @@ def main(argv=None) -> int:
                 row["worker_cold_cached_blocks"] = ds.stats.cold_cached - st0[2]
                 row["worker_zero_copy_frames"] = ds.stats.zero_copy_frames - st0[3]
                 row["worker_prefetched_chunks"] = ds.stats.prefetched - st0[4]
+                row["worker_domain_socket_bytes"] = ds.stats.domain_bytes - st0[5]
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
                     f.write(json.dumps(row) + "\n")
         fs.close()
+    if uds_dir:
+        import shutil
+        shutil.rmtree(uds_dir, ignore_errors=True)
     return 0
 
 
