@@ -723,7 +723,9 @@ class BlockWriter:
     def write_ptr(self, offset, ptr, length, kind) -> None:
         raise NotImplementedError
 
-    def commit(self) -> None:
+    def commit(self, hold_for_append: bool = False) -> None:
+        """Commit the block.  ``hold_for_append``: the worker keeps it from eviction until the
+        file's UFS stream appends it (CACHE_THROUGH tee)."""
         raise NotImplementedError
 
     def cancel(self) -> None:
@@ -741,8 +743,8 @@ class LocalBlockWriter(BlockWriter):
     def write_ptr(self, offset, ptr, length, kind):
         self.w.write_ptr(self.session, self.block_id, offset, ptr, length, kind)
 
-    def commit(self):
-        self.w.commit_block(self.session, self.block_id, self.pin)
+    def commit(self, hold_for_append=False):
+        self.w.commit_block(self.session, self.block_id, self.pin, hold_for_append)
 
     def cancel(self):
         try:
@@ -761,7 +763,7 @@ class LocalUfsFallbackWriter(BlockWriter):
     def write_ptr(self, offset, ptr, length, kind):
         self._w.write_ptr(offset, ptr, length, kind)
 
-    def commit(self):
+    def commit(self, hold_for_append=False):
         self._w.commit()
 
     def cancel(self):
@@ -814,13 +816,14 @@ class IpcBlockWriter(BlockWriter):
         with native_errors():
             self.sink.write_ptr(offset, ptr, length)
 
-    def commit(self):
+    def commit(self, hold_for_append=False):
         if self.h is None:
             return
         h, self.h = self.h, None
         try:
             self.stub.CommitDeviceWrite(pb.block.CommitDeviceWriteRequest(
-                block_id=self.block_id, session_id=self.session, length=self.sink.length, pin_on_create=self.pin))
+                block_id=self.block_id, session_id=self.session, length=self.sink.length, pin_on_create=self.pin,
+                hold_for_append=hold_for_append))
         finally:
             self.ctx.session_keeper().remove(self.address, self.session)
 
@@ -904,13 +907,15 @@ class GrpcBlockWriter(BlockWriter):
         for i in range(0, len(data), self.chunk):
             self._reqs.put(marshal.write_request_frame(mv[i:i + self.chunk]))
 
-    def commit(self):
+    def commit(self, hold_for_append=False):
         if self._sink is not None:
             from ..ops.native import native_errors
             sink, self._sink = self._sink, None
             with native_errors():
-                sink.commit()
+                sink.commit(hold_for_append)
             return
+        if hold_for_append:
+            self._reqs.put(pb.block.WriteRequest(command=pb.block.WriteRequestCommand(hold_for_append=True)))
         self._reqs.close()
         self._t.join()
         if self._err:
@@ -1381,8 +1386,9 @@ class FileOutStream(io.RawIOBase):
             conf.get_bool("alluxio.worker.ipc.enabled", "true") and self.ctx.is_local(w.address)
 
     def _finish_block(self) -> None:
+        hold = bool(self._writers) and self._tee_block and self._block_written > 0
         for w in self._writers:
-            w.commit()
+            w.commit(hold) if hold else w.commit()
         had = bool(self._writers)
         if had and self._tee_block and self._block_written:
             # committed on the worker that runs the UFS stream: it appends the block to the file

@@ -348,6 +348,9 @@ PYBIND11_MODULE(_C, m) {
       .def("lock_block", &BlockStore::lock_block, G(), py::arg("session"), py::arg("block_id"),
            py::arg("write") = false, py::arg("timeout_ms") = -1)
       .def("unlock", &BlockStore::unlock, G())
+      .def("hold_block", &BlockStore::hold_block, G(), py::arg("block_id"), py::arg("ttl_ms") = 120000)
+      .def("release_hold", &BlockStore::release_hold, G())
+      .def_property_readonly("holds", &BlockStore::holds)
       .def("cleanup_session", &BlockStore::cleanup_session, G())
       .def("access_block", &BlockStore::access_block, G())
       .def("access_blocks", &BlockStore::access_blocks, G())

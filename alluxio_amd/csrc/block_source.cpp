@@ -681,6 +681,8 @@ int connect_unix(const std::string& path, int timeout_ms) {
   if (fd < 0) throw std::runtime_error("gRPC client: socket() failed");
   timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
   ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  int sb = 8 << 20;            // uploads: a Unix stream's in-flight bytes count against the sender
+  ::setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sb, sizeof(sb));
   if (::connect(fd, (sockaddr*)&ua, sizeof(ua)) != 0) {
     ::close(fd);
     throw std::runtime_error("gRPC client: connect to unix:" + path + " failed");
@@ -1058,9 +1060,23 @@ void GrpcBlockSink::append_block(int64_t block_id, uint64_t length) {
   written_ += length;
 }
 
-uint64_t GrpcBlockSink::commit() {
+uint64_t GrpcBlockSink::commit(bool hold_for_append) {
   if (!c_) throw StoreError(kErrInvalidState, "commit after cancel");
   Conn& c = *c_;
+  if (hold_for_append) {
+    // WriteRequest{command(1){hold_for_append(20)=true}} ahead of the half-close
+    std::string inner, msg;
+    h2::put_varint(inner, (20u << 3));
+    h2::put_varint(inner, 1);
+    h2::put_varint(msg, (1u << 3) | 2);
+    h2::put_varint(msg, inner.size());
+    msg += inner;
+    Conn::Seg s;
+    s.hdr.push_back('\0');
+    h2::put_be32(s.hdr, (uint32_t)msg.size());
+    s.hdr += msg;
+    c.q.push_back(std::move(s));
+  }
   c.closing = true;
   wait_drained();
   while (!c.closed) {

@@ -170,8 +170,10 @@ class GrpcBlockSink {
   // UFS_FILE streams: the next `length` bytes of the file are block `block_id`, which the same
   // worker already holds (CACHE_THROUGH tee: the worker copies them from its store).
   void append_block(int64_t block_id, uint64_t length);
-  // Half-closes and waits for the worker's commit; returns the committed length.
-  uint64_t commit();
+  // Half-closes and waits for the worker's commit; returns the committed length.  `hold_for_append`:
+  // the worker keeps the committed block locked until the file's UFS stream appends it (CACHE_THROUGH
+  // tee), so it cannot be evicted in between.
+  uint64_t commit(bool hold_for_append = false);
   void cancel();
   uint64_t written() const { return written_; }
   struct Conn;

@@ -681,6 +681,21 @@ void BlockStore::remove_locked(BlockMeta& b, bool emit_event) {
 }
 
 void BlockStore::remove_block(int64_t session, int64_t block_id) {
+  {
+    // an explicit removal (free, delete, a failed commit) outranks append holds, which only keep
+    // the block from eviction: the AppendBlock that wanted it then fails NOT_FOUND
+    std::lock_guard<std::mutex> g(holds_mu_);
+    auto it = holds_.find(block_id);
+    if (it != holds_.end()) {
+      for (auto& h : it->second) {
+        try {
+          unlock(h.first);
+        } catch (...) {
+        }
+      }
+      holds_.erase(it);
+    }
+  }
   std::unique_lock<std::mutex> lk(mu_);
   BlockMeta* b = find(block_id);
   if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(block_id) + " does not exist");
@@ -951,6 +966,71 @@ int64_t BlockStore::lock_block(int64_t session, int64_t block_id, bool write, in
   }
 }
 
+namespace {
+constexpr int64_t kHoldSession = INT64_MAX - 7;   // owner of append holds (no client uses it)
+int64_t steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+}  // namespace
+
+void BlockStore::sweep_holds_locked(int64_t now) {
+  for (auto it = holds_.begin(); it != holds_.end();) {
+    auto& v = it->second;
+    for (size_t i = 0; i < v.size();) {
+      if (v[i].second <= now) {
+        try {
+          unlock(v[i].first);
+        } catch (...) {
+        }
+        v.erase(v.begin() + (long)i);
+      } else {
+        ++i;
+      }
+    }
+    it = v.empty() ? holds_.erase(it) : std::next(it);
+  }
+}
+
+bool BlockStore::hold_block(int64_t block_id, int64_t ttl_ms) {
+  int64_t lock;
+  try {
+    lock = lock_block(kHoldSession, block_id, false, 0);
+  } catch (const StoreError&) {
+    return false;
+  }
+  if (lock < 0) return false;
+  const int64_t now = steady_ns();
+  std::lock_guard<std::mutex> g(holds_mu_);
+  sweep_holds_locked(now);
+  holds_[block_id].emplace_back(lock, now + std::max<int64_t>(ttl_ms, 1) * 1000000LL);
+  return true;
+}
+
+bool BlockStore::release_hold(int64_t block_id) {
+  std::lock_guard<std::mutex> g(holds_mu_);
+  bool released = false;
+  auto it = holds_.find(block_id);
+  if (it != holds_.end() && !it->second.empty()) {
+    try {
+      unlock(it->second.front().first);
+    } catch (...) {
+    }
+    it->second.erase(it->second.begin());
+    if (it->second.empty()) holds_.erase(it);
+    released = true;
+  }
+  sweep_holds_locked(steady_ns());
+  return released;
+}
+
+size_t BlockStore::holds() {
+  std::lock_guard<std::mutex> g(holds_mu_);
+  size_t n = 0;
+  for (auto& kv : holds_) n += kv.second.size();
+  return n;
+}
+
 void BlockStore::unlock(int64_t lock_id) {
   std::unique_lock<std::mutex> lk(mu_);
   auto it = locks_.find(lock_id);
@@ -1189,6 +1269,43 @@ std::vector<uint32_t> BlockStore::checksum(int64_t block_id, uint64_t piece_byte
   HIP_OK(hipMemcpyAsync(out.data(), crc_dev_, out.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, internal_stream_));
   HIP_OK(hipStreamSynchronize(internal_stream_));
   return out;
+}
+
+size_t BlockStore::checksum_async_words(uint64_t length, uint64_t page_size) {
+  if (!length || !page_size) return 0;
+  return (size_t)(ceil_div(length, page_size) + crc32c_scratch_words(length, page_size) + 64);
+}
+
+size_t BlockStore::checksum_async(int64_t block_id, hipStream_t stream, uint32_t* dev_buf, size_t dev_words,
+                                  uint32_t* host_out, uint64_t* page_size_out) {
+  BlockMeta snap;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    BlockMeta* b = find(block_id);
+    if (!b) throw StoreError(kErrNotFound, "block " + std::to_string(block_id) + " does not exist");
+    snap = *b;
+  }
+  const StorageDir& d = *dirs_[snap.dir];
+  if (d.spec.kind != DirKind::kDevice || !snap.length) return 0;
+  const uint64_t ps = d.spec.page_size, len = snap.length;
+  const size_t np = (size_t)ceil_div(len, ps);
+  if (dev_words < checksum_async_words(len, ps)) return 0;
+  set_device();
+  uint64_t off = 0;
+  size_t i = 0, piece_idx = 0;
+  while (off < len) {                      // contiguous page runs, one launch each
+    size_t j = i + 1;
+    while (j < snap.pages.size() && snap.pages[j] == snap.pages[j - 1] + 1) ++j;
+    const uint64_t run = std::min<uint64_t>((j - i) * ps, len - off);
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(d.spec.base + (uint64_t)snap.pages[i] * ps);
+    HIP_OK(launch_crc32c_pieces(base, run, ps, dev_buf + piece_idx, dev_buf + np, dev_words - np, stream));
+    piece_idx += (size_t)ceil_div(run, ps);
+    off += run;
+    i = j;
+  }
+  HIP_OK(hipMemcpyAsync(host_out, dev_buf, np * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  if (page_size_out) *page_size_out = ps;
+  return np;
 }
 
 std::vector<std::pair<uint64_t, std::vector<uint32_t>>> BlockStore::checksum_blocks(

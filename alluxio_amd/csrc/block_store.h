@@ -207,6 +207,13 @@ class BlockStore {
 
   // ---- locks / sessions -------------------------------------------------------------------
   int64_t lock_block(int64_t session, int64_t block_id, bool write, int64_t timeout_ms);
+  // Append holds (CACHE_THROUGH tee): a read lock on a committed block that keeps it from being
+  // evicted between its commit and the moment the file's UFS stream copies it out (AppendBlock),
+  // released by release_hold() once that copy holds its own lock, or after `ttl_ms` (expired holds
+  // are swept by the next hold / release).  hold_block is false when the block is not here.
+  bool hold_block(int64_t block_id, int64_t ttl_ms);
+  bool release_hold(int64_t block_id);
+  size_t holds();
   void unlock(int64_t lock_id);
   void cleanup_session(int64_t session);
   void access_block(int64_t session, int64_t block_id);
@@ -220,6 +227,15 @@ class BlockStore {
   int64_t try_lock_block(int64_t session, int64_t block_id, bool write);
   // CRC32C per piece (piece = page size when 0).
   std::vector<uint32_t> checksum(int64_t block_id, uint64_t piece_bytes);
+  // Per-page CRC32C of HBM block `block_id` (temp or committed) enqueued on `stream` behind what
+  // it already carries (the block's last H2D): the CRCs land in `dev_buf` (device, `dev_words`
+  // words: pages + crc32c_scratch_words) and are copied into `host_out` (pinned, one word per
+  // page).  Nothing waits: the caller records an event after it.  Returns the page count, 0 when
+  // the block is not in a device dir or dev_words is too small (checksum() then).
+  size_t checksum_async(int64_t block_id, hipStream_t stream, uint32_t* dev_buf, size_t dev_words, uint32_t* host_out,
+                        uint64_t* page_size_out);
+  // Device words checksum_async needs for a block of `length` bytes in a dir of `page_size` pages.
+  static size_t checksum_async_words(uint64_t length, uint64_t page_size);
   // Per-page CRC32C of many blocks: the pages of HBM blocks go to one gather launch (pages up
   // to 256 KiB), others take checksum() (or are skipped with device_only).  Returns (piece bytes,
   // CRCs) per block; missing / skipped blocks get (0, []).
@@ -431,6 +447,10 @@ class BlockStore {
   uint32_t* h_claimed_ = nullptr;
   uint32_t* d_claimed_ = nullptr;
   std::mutex ev_mu_;                 // device selection / allocation scratch (taken after mu_)
+  // append holds: block -> [(lock id, expiry ns)]
+  std::mutex holds_mu_;
+  std::unordered_map<int64_t, std::vector<std::pair<int64_t, int64_t>>> holds_;
+  void sweep_holds_locked(int64_t now_ns);
   // checksum scratch
   uint32_t* crc_dev_ = nullptr;
   size_t crc_cap_ = 0;

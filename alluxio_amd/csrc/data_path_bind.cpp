@@ -349,16 +349,16 @@ void bind_data_path(py::module_& m) {
                throw StoreError(kErrIo, e.what());
              }
            }, py::arg("block_id"), py::arg("length"))
-      .def("commit", [](GrpcBlockSink& s) {
+      .def("commit", [](GrpcBlockSink& s, bool hold_for_append) {
              py::gil_scoped_release rel;
              try {
-               return s.commit();
+               return s.commit(hold_for_append);
              } catch (const StoreError&) {
                throw;
              } catch (const std::exception& e) {
                throw StoreError(kErrIo, e.what());
              }
-           })
+           }, py::arg("hold_for_append") = false)
       .def("cancel", [](GrpcBlockSink& s) {
              py::gil_scoped_release rel;
              s.cancel();
@@ -441,6 +441,7 @@ void bind_data_path(py::module_& m) {
 
   // ---- native data server + streaming bridge of the HTTP/2 front end ------------------------
   py::class_<DataServerStats, std::shared_ptr<DataServerStats>>(m, "DataServerStats")
+      .def(py::init<>())
       .def_property_readonly("streams", [](const DataServerStats& s) { return s.streams.load(); })
       .def_property_readonly("declined", [](const DataServerStats& s) { return s.declined.load(); })
       .def_property_readonly("bytes", [](const DataServerStats& s) { return s.bytes.load(); })
@@ -460,7 +461,15 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("store_tasks", [](const DataServerStats& s) { return s.store_tasks.load(); })
       .def_property_readonly("prefetched", [](const DataServerStats& s) { return s.prefetched.load(); })
       .def_property_readonly("zero_copy_frames", [](const DataServerStats& s) { return s.zero_copy_frames.load(); })
-      .def_property_readonly("ufs_tee_bytes", [](const DataServerStats& s) { return s.ufs_tee_bytes.load(); });
+      .def_property_readonly("ufs_tee_bytes", [](const DataServerStats& s) { return s.ufs_tee_bytes.load(); })
+      .def_property_readonly("commits", [](const DataServerStats& s) { return s.commits.load(); })
+      .def_property_readonly("commit_batches", [](const DataServerStats& s) { return s.commit_batches.load(); })
+      .def_property_readonly("commit_failures", [](const DataServerStats& s) { return s.commit_failures.load(); })
+      .def_property_readonly("crc_streamed", [](const DataServerStats& s) { return s.crc_streamed.load(); });
+  py::class_<BlockCommitter, std::shared_ptr<BlockCommitter>>(m, "BlockCommitter")
+      .def(py::init<std::shared_ptr<BlockStore>, uint32_t, bool, bool, std::shared_ptr<DataServerStats>>(),
+           py::arg("store"), py::arg("method"), py::arg("crc_device"), py::arg("crc_host"), py::arg("stats"));
+  m.def("thread_streams_created", &thread_streams_created);
   auto mounts = py::class_<UfsMounts, std::shared_ptr<UfsMounts>>(m, "UfsMounts")
       .def(py::init<>())
       .def("set", &UfsMounts::set, py::arg("mount_id"), py::arg("root"))
@@ -510,24 +519,26 @@ void bind_data_path(py::module_& m) {
         });
   m.def("serve_block_reads", [](FrameRpcServer& srv, uint32_t method, std::shared_ptr<BlockStore> store, uint64_t max_chunk,
                                 uint64_t window, std::shared_ptr<UfsMounts> mounts, uint32_t commit_method,
-                                uint64_t ufs_slot_bytes, int ufs_depth, int ufs_max_active) {
-          auto stats = std::make_shared<DataServerStats>();
+                                uint64_t ufs_slot_bytes, int ufs_depth, int ufs_max_active,
+                                std::shared_ptr<DataServerStats> stats, std::shared_ptr<BlockCommitter> committer) {
+          if (!stats) stats = std::make_shared<DataServerStats>();
           ColdReadConfig cold;
           cold.commit_method = commit_method;
           cold.slot_bytes = ufs_slot_bytes;
           cold.depth = ufs_depth;
           cold.max_active = ufs_max_active;
-          serve_block_reads(srv, method, store, max_chunk, window, stats, mounts, cold);
+          serve_block_reads(srv, method, store, max_chunk, window, stats, mounts, cold, committer);
           return stats;
         }, py::arg("server"), py::arg("method"), py::arg("store"), py::arg("max_chunk"), py::arg("window"),
         py::arg("mounts") = nullptr, py::arg("commit_method") = UINT32_MAX, py::arg("ufs_slot_bytes") = 8u << 20,
-        py::arg("ufs_depth") = 3, py::arg("ufs_max_active") = 256, py::keep_alive<1, 3>());
+        py::arg("ufs_depth") = 3, py::arg("ufs_max_active") = 256, py::arg("stats") = nullptr,
+        py::arg("committer") = nullptr, py::keep_alive<1, 3>());
   m.def("serve_block_writes", [](FrameRpcServer& srv, uint32_t method, uint32_t commit_method, std::shared_ptr<BlockStore> store,
                                  uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
-                                 std::shared_ptr<UfsMounts> ufs_roots) {
-          serve_block_writes(srv, method, commit_method, store, stage_bytes, stats, ufs_roots);
+                                 std::shared_ptr<UfsMounts> ufs_roots, std::shared_ptr<BlockCommitter> committer) {
+          serve_block_writes(srv, method, commit_method, store, stage_bytes, stats, ufs_roots, committer);
         }, py::arg("server"), py::arg("method"), py::arg("commit_method"), py::arg("store"), py::arg("stage_bytes"),
-        py::arg("stats"), py::arg("ufs_roots") = nullptr, py::keep_alive<1, 4>());
+        py::arg("stats"), py::arg("ufs_roots") = nullptr, py::arg("committer") = nullptr, py::keep_alive<1, 4>());
   m.def("stream_recv", [](FrameRpcServer& srv, uint64_t token, int timeout_ms) -> py::tuple {
           std::string msg;
           int rc;

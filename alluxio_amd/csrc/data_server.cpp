@@ -7,6 +7,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <condition_variable>
 #include <deque>
@@ -589,6 +590,7 @@ struct ColdJob {
   std::shared_ptr<DataServerStats> stats;
   std::function<void(uint32_t, std::string)> post;   // internal requests to Python (the commit)
   uint32_t commit_method = UINT32_MAX;
+  std::shared_ptr<BlockCommitter> committer;         // native commit (instead of `post`) when set
 
   void wake() {
     std::function<void()> w;
@@ -682,7 +684,7 @@ struct ColdJob {
     // UnderFileSystemBlockReader.close: a block read through to its end is committed -- also when
     // the client went away after the last byte -- anything less is aborted
     const bool complete = ok && ingested >= end;
-    const bool commit = caching && complete && post && commit_method != UINT32_MAX;
+    const bool commit = caching && complete && ((post && commit_method != UINT32_MAX) || committer);
     bool cancelled;
     {
       std::lock_guard<std::mutex> g(st->mu);
@@ -697,7 +699,17 @@ struct ColdJob {
       st->handed_off = commit;
       cancelled = st->cancelled;
     }
-    if (commit) {
+    if (commit && committer) {
+      // the native committer commits it and reports it with the next batch (no client waits)
+      auto t = std::make_shared<CommitTicket>();
+      t->session = session;
+      t->block = block;
+      t->length = block_len;
+      t->ufs_read = true;
+      t->crc_sync = store->has_device() ? committer->crc_device() : committer->crc_host();
+      committer->submit(t);
+      stats->cold_cached.fetch_add(1, std::memory_order_relaxed);
+    } else if (commit) {
       // NativeWriteCommitRequest: session_id=1 block_id=2 length=3 pin=4 ufs_read=5; Python
       // commits (CRC, master report) and drops the session, whether or not the call still exists
       std::string m;
@@ -914,6 +926,7 @@ class ColdReadStream : public NativeStream {
 struct WriteCmd {
   int64_t type = 0, id = 0, offset = 0, tier = 0, reserve = 0;
   bool has_tier = false, flush = false, pin = false, has_ufs = false, has_ufs_file = false;
+  bool hold = false;                  // hold_for_append=20: keep the block locked for an AppendBlock
   std::string medium;
   std::string ufs_path;
   int64_t ufs_mode = 0, ufs_mount = 0;
@@ -975,6 +988,7 @@ bool parse_write_command(const uint8_t* p, size_t n, WriteCmd* c) {
         case 5: c->flush = v != 0; break;
         case 9: c->pin = v != 0; break;
         case 10: c->reserve = (int64_t)v; break;
+        case 20: c->hold = v != 0; break;
         default: break;
       }
     } else if (wt == 2) {
@@ -1123,9 +1137,11 @@ class WriteStreamBase : public NativeStream {
 class BlockWriteStream : public WriteStreamBase {
  public:
   BlockWriteStream(StoreRef store, int64_t session, int64_t block_id, uint64_t pos, bool pin, bool device,
-                   uint32_t commit_method, std::shared_ptr<StagingPool> pool, std::shared_ptr<DataServerStats> stats)
-      : store_(store), session_(session), block_(block_id), pos_(pos), pin_(pin), device_(device),
-        commit_(commit_method), pool_(std::move(pool)), stats_(std::move(stats)) {}
+                   uint32_t commit_method, std::shared_ptr<StagingPool> pool, std::shared_ptr<DataServerStats> stats,
+                   std::shared_ptr<BlockCommitter> committer = nullptr)
+      : store_(std::move(store)), session_(session), block_(block_id), start_(pos), pos_(pos), pin_(pin),
+        device_(device), commit_(commit_method), pool_(std::move(pool)), stats_(std::move(stats)),
+        committer_(std::move(committer)) {}
 
   ~BlockWriteStream() override {
     drain();                                 // no DMA may still target the block's pages
@@ -1133,10 +1149,39 @@ class BlockWriteStream : public WriteStreamBase {
       if (sl.ev) (void)hipEventDestroy(sl.ev);
       if (sl.buf) pool_->put(sl.buf);
     }
+    if (ticket_) {                           // the committer owns the session now
+      std::lock_guard<std::mutex> g(ticket_->mu);
+      ticket_->wake = nullptr;
+      return;
+    }
     try {
       store_->cleanup_session(session_);     // aborts the temp block unless Python committed it
     } catch (...) {
     }
+  }
+
+  void set_waker(std::function<void()> w) override { waker_ = std::move(w); }
+
+  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    if (ticket_ && !done_ && !err_) {        // the native commit: answer once it is through
+      bool fin;
+      int st;
+      std::string m;
+      {
+        std::lock_guard<std::mutex> g(ticket_->mu);
+        fin = ticket_->finished;
+        st = ticket_->status;
+        m = ticket_->msg;
+      }
+      if (fin) {
+        if (st) fail(st, m);
+        else {
+          out_ += write_response_frame(pos_);
+          done_ = true;
+        }
+      }
+    }
+    return WriteStreamBase::produce(dst, max, eof, status, msg);
   }
 
   void on_message(const char* p, size_t n) override {
@@ -1159,16 +1204,25 @@ class BlockWriteStream : public WriteStreamBase {
       return;
     }
     if (has_cmd && cmd.flush) out_ += write_response_frame(pos_);
+    if (has_cmd && cmd.hold) hold_ = true;
   }
 
   bool on_end(uint32_t* method, std::string* payload) override {
     ended_ = true;
     if (err_) return false;
+    if (committer_ && committer_->has_caller()) {
+      try {
+        hand_to_committer();
+        return false;                        // produce() answers when the ticket is through
+      } catch (const std::exception& e) {
+        ticket_.reset();                     // nothing was submitted: commit through Python below
+      }
+    }
     if (!drain()) {                          // every H2D landed before the commit reads the block
       fail(13, "writing block " + std::to_string(block_) + ": H2D staging copy failed");
       return false;
     }
-    // NativeWriteCommitRequest: session_id=1 block_id=2 length=3 pin=4
+    // NativeWriteCommitRequest: session_id=1 block_id=2 length=3 pin=4 hold_for_append=6
     std::string m;
     h2::put_varint(m, (1u << 3));
     h2::put_varint(m, (uint64_t)session_);
@@ -1178,6 +1232,10 @@ class BlockWriteStream : public WriteStreamBase {
     h2::put_varint(m, pos_);
     if (pin_) {
       h2::put_varint(m, (4u << 3));
+      h2::put_varint(m, 1);
+    }
+    if (hold_) {
+      h2::put_varint(m, (6u << 3));
       h2::put_varint(m, 1);
     }
     *method = commit_;
@@ -1230,6 +1288,44 @@ class BlockWriteStream : public WriteStreamBase {
     stats_->write_bytes.fetch_add(n, std::memory_order_relaxed);
   }
 
+  // The half-close of a native commit: HBM blocks get their per-page CRC32C computed on this I/O
+  // thread's stream right behind the last H2D (no host pass over the bytes, no wait here), then an
+  // event closes the block's device work; the committer thread takes it from there.
+  void hand_to_committer() {
+    auto t = std::make_shared<CommitTicket>();
+    t->session = session_;
+    t->block = block_;
+    t->length = pos_;
+    t->pin = pin_;
+    t->hold = hold_;
+    t->wake = waker_;
+    if (device_) {
+      hipStream_t st = thread_stream(store_);
+      if (committer_->crc_device() && start_ == 0 && pos_ > 0) {
+        const DirSpec ds = store_->dir_spec(store_->block_info(block_).dir);
+        const size_t words = BlockStore::checksum_async_words(pos_, ds.page_size);
+        if (words && committer_->take_crc_buffer(words, t.get())) {
+          t->crc_pages = store_->checksum_async(block_, st, t->crc_dev, t->crc_words, t->crc_host, &t->crc_page);
+          if (!t->crc_pages) t->crc_sync = true;
+        } else {
+          t->crc_sync = true;
+        }
+      } else if (committer_->crc_device()) {
+        t->crc_sync = pos_ > 0;              // a resumed write: the committer checksums the whole block
+      }
+      if (hipEventCreateWithFlags(&t->done, hipEventDisableTiming) != hipSuccess) {
+        t->done = nullptr;
+        (void)hipStreamSynchronize(st);
+      } else if (hipEventRecord(t->done, st) != hipSuccess) {
+        (void)hipStreamSynchronize(st);
+      }
+    } else if (committer_->crc_host() && pos_ > 0) {
+      t->crc_sync = true;                    // host blocks: the committer computes them
+    }
+    ticket_ = t;
+    committer_->submit(t);
+  }
+
   // Waits for the staging copies still in flight; false if one failed.
   bool drain() {
     bool ok = true;
@@ -1251,11 +1347,15 @@ class BlockWriteStream : public WriteStreamBase {
 
   StoreRef store_;
   int64_t session_, block_;
-  uint64_t pos_;
+  uint64_t start_, pos_;
   bool pin_, device_;
   uint32_t commit_;
   std::shared_ptr<StagingPool> pool_;
   std::shared_ptr<DataServerStats> stats_;
+  std::shared_ptr<BlockCommitter> committer_;
+  std::shared_ptr<CommitTicket> ticket_;
+  std::function<void()> waker_;
+  bool hold_ = false;
 };
 
 int grpc_status_of_errno(int e) {
@@ -1377,7 +1477,10 @@ struct LocalFileJob {
 
   ~LocalFileJob() {
     for (const Item& it : chunks)      // appends never run (failed / cancelled file)
-      if (it.block >= 0 && stats) stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
+      if (it.block >= 0) {
+        if (stats) stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
+        if (store) store->release_hold(it.block);
+      }
   }
   bool running = false, opened = false, failed = false, cancelled = false;
   bool end = false, finished = false, cleaned = false;
@@ -1454,6 +1557,7 @@ struct LocalFileJob {
       *what = "appending block " + std::to_string(id) + ": lock timed out";
       return ETIMEDOUT;
     }
+    store->release_hold(id);            // our own lock keeps it now (the commit's append hold goes)
     constexpr uint64_t kPiece = kTeePiece;
     const bool dev = store->has_device();
     std::unique_ptr<TeePieces> pieces_buf;      // declared before the stream sync that frees them
@@ -1878,6 +1982,7 @@ struct S3Upload {
     try {
       lock = store->lock_block(session, id, false, 30000);
       if (lock < 0) e = "appending block " + std::to_string(id) + ": lock timed out";
+      else store->release_hold(id);
     } catch (const std::exception& x) {
       e = std::string("appending block ") + std::to_string(id) + ": " + x.what();
     }
@@ -2071,6 +2176,8 @@ class S3UfsWriteStream : public WriteStreamBase {
   }
 
   ~S3UfsWriteStream() override {
+    for (const Pending& p : pending_)  // appends that never ran
+      if (p.block >= 0 && store_) store_->release_hold(p.block);
     bool idle;
     {
       std::lock_guard<std::mutex> g(u_->mu);
@@ -2351,7 +2458,8 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
                                                const std::shared_ptr<StagingPool>& slot_pool,
                                                const std::shared_ptr<DataServerStats>& stats,
                                                std::function<void(uint32_t, std::string)> post, int* status,
-                                               std::string* msg) {
+                                               std::string* msg,
+                                               const std::shared_ptr<BlockCommitter>& committer = nullptr) {
   UfsOpts o;
   if (!mounts || !parse_ufs_opts(r.ufs_opts, &o) || o.ufs_path.empty() || o.block_in_ufs_tier || o.block_size <= 0)
     return nullptr;
@@ -2386,8 +2494,8 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
     return nullptr;
   }
   // UnderFileSystemBlockReader caches only a whole-block sequential read; anything else streams
-  const bool cache = !o.no_cache && off == 0 && end == block_len && cfg.commit_method != UINT32_MAX &&
-                     !store->has_temp_block(r.block_id);
+  const bool cache = !o.no_cache && off == 0 && end == block_len &&
+                     (cfg.commit_method != UINT32_MAX || committer) && !store->has_temp_block(r.block_id);
   auto st = std::make_shared<ColdState>();
   st->pool = slot_pool;
   st->slots.resize((size_t)std::max(2, cfg.depth));
@@ -2406,6 +2514,7 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
   job->stats = stats;
   job->post = std::move(post);
   job->commit_method = cfg.commit_method;
+  job->committer = committer;
   const uint64_t chunk =
       r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk) : std::min<uint64_t>(1u << 20, max_chunk);
   std::unique_ptr<NativeStream> ns(new ColdReadStream(store, job->session, r.block_id, off, end, chunk, window,
@@ -2422,8 +2531,300 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
 
 }  // namespace
 
+// ---- native block commit ------------------------------------------------------------------------
+
+// How long an append hold keeps a CACHE_THROUGH block from eviction when no AppendBlock comes.
+constexpr int64_t kAppendHoldMs = 120000;
+
+CommitTicket::~CommitTicket() {
+  if (done) (void)hipEventDestroy(done);
+}
+
+struct BlockCommitter::State {
+  StoreRef store;
+  uint32_t method = UINT32_MAX;
+  std::shared_ptr<DataServerStats> stats;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::shared_ptr<CommitTicket>> q;
+  bool stop = false;
+  Caller caller;
+  struct CrcBuf {
+    uint32_t* dev = nullptr;
+    uint32_t* host = nullptr;
+    size_t words = 0;
+  };
+  std::vector<CrcBuf> free_crc;       // device + pinned CRC buffers, reused across tickets
+  ~State() {
+    for (auto& b : free_crc) {
+      if (b.dev) (void)hipFree(b.dev);
+      if (b.host) (void)hipHostFree(b.host);
+    }
+  }
+};
+
+BlockCommitter::BlockCommitter(StoreRef store, uint32_t method, bool crc_device, bool crc_host,
+                               std::shared_ptr<DataServerStats> stats)
+    : st_(std::make_shared<State>()), crc_device_(crc_device), crc_host_(crc_host) {
+  st_->store = std::move(store);
+  st_->method = method;
+  st_->stats = std::move(stats);
+  auto st = st_;
+  // detached: it holds the state (and so the store) until its queue is drained after the stop
+  std::thread([st] { BlockCommitter::run(st); }).detach();
+}
+
+BlockCommitter::~BlockCommitter() {
+  {
+    std::lock_guard<std::mutex> g(st_->mu);
+    st_->stop = true;
+  }
+  st_->cv.notify_all();
+}
+
+void BlockCommitter::set_caller(Caller c) {
+  std::lock_guard<std::mutex> g(st_->mu);
+  if (!st_->caller) st_->caller = std::move(c);
+}
+
+bool BlockCommitter::has_caller() {
+  std::lock_guard<std::mutex> g(st_->mu);
+  return (bool)st_->caller;
+}
+
+void BlockCommitter::submit(std::shared_ptr<CommitTicket> t) {
+  {
+    std::lock_guard<std::mutex> g(st_->mu);
+    st_->q.push_back(std::move(t));
+  }
+  st_->cv.notify_one();
+}
+
+bool BlockCommitter::take_crc_buffer(size_t words, CommitTicket* t) {
+  State::CrcBuf b;
+  {
+    std::lock_guard<std::mutex> g(st_->mu);
+    for (size_t i = 0; i < st_->free_crc.size(); ++i)
+      if (st_->free_crc[i].words >= words) {
+        b = st_->free_crc[i];
+        st_->free_crc.erase(st_->free_crc.begin() + (long)i);
+        break;
+      }
+  }
+  if (!b.dev) {
+    words = std::max<size_t>(words, 4096);   // one size fits the usual blocks: buffers get reused
+    st_->store->use_device();
+    if (hipMalloc((void**)&b.dev, words * sizeof(uint32_t)) != hipSuccess) return false;
+    if (hipHostMalloc((void**)&b.host, words * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+      (void)hipFree(b.dev);
+      return false;
+    }
+    b.words = words;
+  }
+  t->crc_dev = b.dev;
+  t->crc_host = b.host;
+  t->crc_words = b.words;
+  return true;
+}
+
+namespace {
+void put_key_varint(std::string& m, uint32_t field, uint64_t v) {
+  h2::put_varint(m, (uint64_t)field << 3);
+  h2::put_varint(m, v);
+}
+
+// NativeCommitBatchResponse (proto/defs/block.py): failed=1:i64* message=2:str
+void parse_commit_reply(const std::string& b, std::vector<int64_t>* failed, std::string* msg) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(b.data());
+  const size_t n = b.size();
+  size_t i = 0;
+  while (i < n) {
+    uint64_t key;
+    if (!h2::get_varint(p, n, &i, &key)) return;
+    const uint32_t field = (uint32_t)(key >> 3), wt = (uint32_t)(key & 7);
+    if (field == 1 && wt == 0) {
+      uint64_t v;
+      if (!h2::get_varint(p, n, &i, &v)) return;
+      failed->push_back((int64_t)v);
+    } else if (field == 1 && wt == 2) {            // packed
+      uint64_t len;
+      if (!h2::get_varint(p, n, &i, &len) || len > n - i) return;
+      const size_t end = i + (size_t)len;
+      while (i < end) {
+        uint64_t v;
+        if (!h2::get_varint(p, end, &i, &v)) return;
+        failed->push_back((int64_t)v);
+      }
+    } else if (field == 2 && wt == 2) {
+      uint64_t len;
+      if (!h2::get_varint(p, n, &i, &len) || len > n - i) return;
+      msg->assign(b.data() + i, (size_t)len);
+      i += (size_t)len;
+    } else if (!skip_field(p, n, &i, wt)) {
+      return;
+    }
+  }
+}
+}  // namespace
+
+void BlockCommitter::run(std::shared_ptr<State> st) {
+  pthread_setname_np(pthread_self(), "block-commit");
+  const StoreRef& store = st->store;
+  if (store->has_device()) store->use_device();
+  for (;;) {
+    std::vector<std::shared_ptr<CommitTicket>> batch;
+    Caller caller;
+    {
+      std::unique_lock<std::mutex> lk(st->mu);
+      st->cv.wait(lk, [&] { return st->stop || !st->q.empty(); });
+      if (st->q.empty()) break;                   // stopped and drained
+      while (!st->q.empty() && batch.size() < 1024) {
+        batch.push_back(std::move(st->q.front()));
+        st->q.pop_front();
+      }
+      caller = st->caller;
+    }
+    struct Item {
+      std::shared_ptr<CommitTicket> t;
+      int status = 0;
+      std::string msg;
+      int64_t lock = -1;
+      std::string crc;                            // little-endian u32 per page
+      uint64_t piece = 0;
+    };
+    std::vector<Item> items(batch.size());
+    // 1) the device work of every block (H2D, CRC kernel, CRC D2H), then the store commit
+    for (size_t i = 0; i < batch.size(); ++i) {
+      Item& it = items[i];
+      it.t = batch[i];
+      CommitTicket& t = *it.t;
+      if (t.done && hipEventSynchronize(t.done) != hipSuccess) {
+        it.status = 13;
+        it.msg = "writing block " + std::to_string(t.block) + ": a device copy into the block failed";
+      }
+      if (!it.status && t.crc_pages && t.crc_host) {
+        it.crc.assign(reinterpret_cast<const char*>(t.crc_host), t.crc_pages * sizeof(uint32_t));
+        it.piece = t.crc_page;
+        st->stats->crc_streamed.fetch_add(1, std::memory_order_relaxed);
+      }
+      if (t.crc_dev) {                            // the buffer goes back to the pool
+        std::lock_guard<std::mutex> g(st->mu);
+        st->free_crc.push_back(State::CrcBuf{t.crc_dev, t.crc_host, t.crc_words});
+        t.crc_dev = nullptr;
+        t.crc_host = nullptr;
+      }
+      if (it.status) continue;
+      try {
+        if (t.crc_sync) {                         // no streamed CRCs: compute them here
+          int dir = -1;
+          uint64_t ps = 0, base = 0;
+          store->block_pages(t.block, &dir, &ps, &base);
+          const std::vector<uint32_t> c = store->checksum(t.block, 0);
+          it.crc.assign(reinterpret_cast<const char*>(c.data()), c.size() * sizeof(uint32_t));
+          it.piece = store->dir_spec(dir).kind == DirKind::kFile ? (2ull << 20) : ps;
+        }
+        store->commit_block(t.session, t.block, t.pin);
+        // held until the master knows (DefaultBlockWorker.commitBlockLocked): never evicted between
+        it.lock = store->lock_block(t.session, t.block, false, 0);
+      } catch (const StoreError& e) {
+        it.status = grpc_status_of(e);
+        it.msg = "committing block " + std::to_string(t.block) + ": " + e.what();
+      } catch (const std::exception& e) {
+        it.status = 13;
+        it.msg = "committing block " + std::to_string(t.block) + ": " + e.what();
+      }
+    }
+    // 2) one master report for every block committed above
+    std::string req;
+    size_t ncommitted = 0;
+    for (const Item& it : items) {
+      if (it.status) continue;
+      ++ncommitted;
+      put_key_varint(req, 1, (uint64_t)it.t->block);
+      put_key_varint(req, 2, it.t->length);
+      put_key_varint(req, 3, it.piece);
+      h2::put_varint(req, (4u << 3) | 2);
+      h2::put_varint(req, it.crc.size());
+      req += it.crc;
+      put_key_varint(req, 5, it.t->ufs_read ? 1 : 0);
+    }
+    int rstatus = 0;
+    std::string rmsg;
+    std::vector<int64_t> failed;
+    if (ncommitted) {
+      if (!caller) {
+        rstatus = 14;
+        rmsg = "the data server cannot reach its worker process";
+      } else {
+        struct Reply {
+          std::mutex mu;
+          std::condition_variable cv;
+          bool got = false;
+          int status = 0;
+          std::string msg, payload;
+        };
+        auto rep = std::make_shared<Reply>();
+        caller(st->method, std::move(req), [rep](int status, const std::string& msg, const std::string& payload) {
+          std::lock_guard<std::mutex> g(rep->mu);
+          rep->got = true;
+          rep->status = status;
+          rep->msg = msg;
+          rep->payload = payload;
+          rep->cv.notify_all();
+        });
+        std::unique_lock<std::mutex> lk(rep->mu);
+        if (!rep->cv.wait_for(lk, std::chrono::minutes(10), [&] { return rep->got; })) {
+          rstatus = 4;
+          rmsg = "the worker did not answer the block commit report in 10 minutes";
+        } else {
+          rstatus = rep->status;
+          rmsg = rep->msg;
+          if (!rstatus) parse_commit_reply(rep->payload, &failed, &rmsg);
+        }
+      }
+      st->stats->commit_batches.fetch_add(1, std::memory_order_relaxed);
+    }
+    // 3) finish: a block the master does not know about does not stay
+    for (Item& it : items) {
+      CommitTicket& t = *it.t;
+      if (!it.status && (rstatus || std::find(failed.begin(), failed.end(), t.block) != failed.end())) {
+        it.status = rstatus ? (rstatus == 4 ? 4 : 14) : 14;
+        it.msg = "block " + std::to_string(t.block) + " committed locally but the master was not told: " +
+                 (rmsg.empty() ? std::string("report failed") : rmsg);
+      }
+      if (!it.status && t.hold) store->hold_block(t.block, kAppendHoldMs);   // before our lock goes
+      try {
+        if (it.lock >= 0) store->unlock(it.lock);
+      } catch (...) {
+      }
+      if (it.status && it.lock >= 0) {
+        try {
+          store->remove_block(t.session, t.block);
+        } catch (...) {
+        }
+      }
+      try {
+        store->cleanup_session(t.session);       // aborts a temp block that never got committed
+      } catch (...) {
+      }
+      if (it.status) st->stats->commit_failures.fetch_add(1, std::memory_order_relaxed);
+      else st->stats->commits.fetch_add(1, std::memory_order_relaxed);
+      std::function<void()> w;
+      {
+        std::lock_guard<std::mutex> g(t.mu);
+        t.finished = true;
+        t.status = it.status;
+        t.msg = it.msg;
+        w = t.wake;
+      }
+      if (w) w();
+    }
+  }
+}
+
 void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uint64_t max_chunk, uint64_t window,
-                       std::shared_ptr<DataServerStats> stats, std::shared_ptr<UfsMounts> mounts, ColdReadConfig cold) {
+                       std::shared_ptr<DataServerStats> stats, std::shared_ptr<UfsMounts> mounts, ColdReadConfig cold,
+                       std::shared_ptr<BlockCommitter> committer) {
   if (max_chunk == 0) max_chunk = 2u << 20;
   if (window == 0) window = 4u << 20;
   if (cold.slot_bytes == 0) cold.slot_bytes = 8u << 20;
@@ -2458,8 +2859,9 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uin
     }
     if (lock < 0) {
       if (r.has_ufs) {     // a cold block: read it through from the UFS (BlockReadHandler.openUfsBlock)
+        if (committer && !committer->has_caller()) committer->set_caller(s->internal_caller(cid, user));
         auto cs = make_cold_stream(r, store, max_chunk, window, unix_peer, cold, mounts, slot_pool, stats,
-                                   s->internal_poster(cid, user), status, msg);
+                                   s->internal_poster(cid, user), status, msg, committer);
         if (cs || *status != 0) return cs;
       }
       stats->declined.fetch_add(1, std::memory_order_relaxed);
@@ -2496,13 +2898,12 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uin
 
 void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, StoreRef store,
                         uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
-                        std::shared_ptr<UfsMounts> ufs_roots) {
+                        std::shared_ptr<UfsMounts> ufs_roots, std::shared_ptr<BlockCommitter> committer) {
   if (stage_bytes == 0) stage_bytes = 4u << 20;
   auto pool = std::make_shared<StagingPool>(stage_bytes, store->has_device(), store->device());
   FrameRpcServer* s = &srv;
   srv.set_native_stream(method, [=](const std::string& first, const std::string& cid, const std::string& user,
                                     bool unix_peer, int* status, std::string* msg) -> std::unique_ptr<NativeStream> {
-    (void)user;
     (void)unix_peer;
     WriteCmd cmd;
     bool has_cmd;
@@ -2557,8 +2958,10 @@ void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_me
         return nullptr;
       }
       const bool device = store->dir_spec(dir).kind == DirKind::kDevice;
+      if (committer && !committer->has_caller()) committer->set_caller(s->internal_caller(cid, user));
       auto ws = std::unique_ptr<BlockWriteStream>(new BlockWriteStream(store, session, cmd.id, (uint64_t)cmd.offset,
-                                                                       cmd.pin, device, commit_method, pool, stats));
+                                                                       cmd.pin, device, commit_method, pool, stats,
+                                                                       committer));
       stats->write_streams.fetch_add(1, std::memory_order_relaxed);
       if (len) ws->on_message(first.data(), first.size());   // a command that carries data too
       return ws;

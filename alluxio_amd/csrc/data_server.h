@@ -19,6 +19,7 @@
 #pragma once
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -56,6 +57,65 @@ struct DataServerStats {
   std::atomic<uint64_t> ufs_tee_bytes{0};     // CACHE_THROUGH bytes the UFS stream copied from the store
   std::atomic<uint64_t> zero_copy_frames{0}; // HTTP/2 DATA frames sent straight from staging (no copy)
   std::atomic<uint64_t> prefetched{0};       // HBM chunks whose D2H was issued ahead of the send
+  std::atomic<uint64_t> commits{0};          // blocks committed by the native committer
+  std::atomic<uint64_t> commit_batches{0};   // master reports (one internal call each) they took
+  std::atomic<uint64_t> commit_failures{0};  // blocks whose commit failed (removed / aborted)
+  std::atomic<uint64_t> crc_streamed{0};     // blocks whose CRCs were computed on the write stream
+};
+
+// One block handed to the committer: the temp block of a finished WriteBlock (or of a complete
+// cold read-through), the event after its last device work, its CRCs once they land.
+struct CommitTicket {
+  int64_t session = 0, block = 0;
+  uint64_t length = 0;
+  bool pin = false;
+  bool ufs_read = false;            // a cold read-through's block (no client waits for it)
+  bool hold = false;                // CACHE_THROUGH tee: held for the UFS stream's AppendBlock
+  hipEvent_t done = nullptr;        // H2D copies + CRC kernel + CRC D2H of the block (may be null)
+  uint32_t* crc_host = nullptr;     // pinned: `crc_pages` per-page CRC32Cs, valid once `done` fired
+  uint32_t* crc_dev = nullptr;      // device scratch the CRCs were computed in (returned to the pool)
+  size_t crc_words = 0, crc_pages = 0;
+  uint64_t crc_page = 0;
+  bool crc_sync = false;            // no streamed CRCs: the committer computes them (checksum())
+  // result
+  std::mutex mu;
+  bool finished = false;
+  int status = 0;
+  std::string msg;
+  std::function<void()> wake;       // the waiting stream's waker (null once it is gone)
+  ~CommitTicket();
+};
+
+// Native block commit of a worker (reference BlockWriteHandler.java:124-149 ->
+// DefaultBlockWorker.commitBlock:274-306 -> BlockMaster commitBlock): a thread that takes the
+// blocks WriteBlock streams (and cold read-throughs) hand it, waits for each block's device work
+// and streamed CRCs, commits it in the store, and reports everything it committed since the last
+// report to the master in ONE internal call (`method`, NativeCommitBatch: Python stores the CRCs
+// and sends one CommitBlocks RPC, retried for alluxio.user.rpc.retry.max.duration).  A report is
+// in flight at most once: blocks that finish meanwhile form the next batch (group commit).  The
+// streams answer their clients only once the store commit and the master's ack are both in; a
+// block the master could not be told about is removed again and its stream fails UNAVAILABLE.
+class BlockCommitter {
+ public:
+  using Caller = std::function<void(uint32_t, std::string,
+                                    std::function<void(int, const std::string&, const std::string&)>)>;
+  BlockCommitter(StoreRef store, uint32_t method, bool crc_device, bool crc_host,
+                 std::shared_ptr<DataServerStats> stats);
+  ~BlockCommitter();
+  // The server's internal caller (FrameRpcServer::internal_caller); set on first use.
+  void set_caller(Caller c);
+  bool has_caller();
+  void submit(std::shared_ptr<CommitTicket> t);
+  bool crc_device() const { return crc_device_; }
+  bool crc_host() const { return crc_host_; }
+  // A device CRC buffer (dev + pinned host) of at least `words` words for a ticket, or false.
+  bool take_crc_buffer(size_t words, CommitTicket* t);
+
+ private:
+  struct State;
+  static void run(std::shared_ptr<State> st);
+  std::shared_ptr<State> st_;
+  bool crc_device_, crc_host_;
 };
 
 // An S3-compatible object mount the native data path reads from (plain-HTTP endpoint).
@@ -119,7 +179,8 @@ struct ColdReadConfig {
 // without caching; a cancelled or failed read-through aborts the temp block.
 void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uint64_t max_chunk,
                        uint64_t window, std::shared_ptr<DataServerStats> stats,
-                       std::shared_ptr<UfsMounts> mounts = nullptr, ColdReadConfig cold = ColdReadConfig());
+                       std::shared_ptr<UfsMounts> mounts = nullptr, ColdReadConfig cold = ColdReadConfig(),
+                       std::shared_ptr<BlockCommitter> committer = nullptr);
 
 // Serve `method` (WriteBlock) of `srv` into `store` for ALLUXIO_BLOCK writes: the block is created
 // on the first message, chunk messages are written into it on the I/O thread (HBM: through a
@@ -132,8 +193,10 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uin
 // whose parts go out on upload threads while the client streams (S3ALowLevelOutputStream), with
 // the request window held back while every part buffer is in flight.  Other UFS_FILE and
 // UFS_FALLBACK_BLOCK writes go to the Python servicer.
+// With `committer`, the commit runs natively (BlockCommitter) instead of as `commit_method` in Python.
 void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_method, StoreRef store,
                         uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
-                        std::shared_ptr<UfsMounts> ufs_roots = nullptr);
+                        std::shared_ptr<UfsMounts> ufs_roots = nullptr,
+                        std::shared_ptr<BlockCommitter> committer = nullptr);
 
 }  // namespace amdx

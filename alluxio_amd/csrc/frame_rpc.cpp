@@ -1069,6 +1069,15 @@ void FrameRpcServer::stop() {
     l->q.clear();
     l->cv.notify_all();
   }
+  {
+    std::unordered_map<uint32_t, ReplyFn> left;
+    {
+      std::lock_guard<std::mutex> g(calls_->mu);
+      calls_->stopped = true;
+      left.swap(calls_->pending);
+    }
+    for (auto& kv : left) kv.second(14, "the data server stopped", std::string());
+  }
   std::lock_guard<std::mutex> g(bridges_mu_);
   for (auto& kv : bridges_) {
     std::lock_guard<std::mutex> bg(kv.second->mu);
@@ -1210,6 +1219,48 @@ std::function<void(uint32_t, std::string)> FrameRpcServer::internal_poster(const
     if (!srv || method >= srv->lanes_.size()) return;
     FrameRequest rq;
     rq.token = 0;               // connection 0 never exists: respond() drops the reply
+    rq.method = method;
+    rq.user = caller;
+    rq.payload = std::move(payload);
+    Lane& l = *srv->lane_q_[srv->lanes_[method]];
+    {
+      std::lock_guard<std::mutex> lg(l.mu);
+      l.q.push_back(std::move(rq));
+    }
+    l.cv.notify_one();
+  };
+}
+
+std::function<void(uint32_t, std::string, FrameRpcServer::ReplyFn)> FrameRpcServer::internal_caller(
+    const std::string& cid, const std::string& user) {
+  std::shared_ptr<WakeHub> hub = hub_;
+  std::shared_ptr<InternalCalls> calls = calls_;
+  std::string caller = "\x02\x01" + cid;
+  caller.push_back('\0');
+  caller += user;
+  return [hub, calls, caller](uint32_t method, std::string payload, ReplyFn done) {
+    if (!hub) {                 // asked for before start()
+      done(14, "the data server is not running", std::string());
+      return;
+    }
+    std::lock_guard<std::mutex> g(hub->mu);
+    FrameRpcServer* srv = hub->srv;
+    uint32_t id = 0;
+    {
+      std::lock_guard<std::mutex> cg(calls->mu);
+      if (srv && !calls->stopped && method < srv->lanes_.size()) {
+        do {
+          id = calls->next++ & 0x7fffffffu;
+        } while (id == 0 || calls->pending.count(id));
+        calls->pending.emplace(id, done);
+      }
+    }
+    if (!id) {
+      done(14, "the data server has stopped", std::string());
+      return;
+    }
+    FrameRequest rq;
+    rq.token = id;              // connection 0: respond() hands the reply to deliver_internal
     rq.method = method;
     rq.user = caller;
     rq.payload = std::move(payload);
@@ -1441,7 +1492,23 @@ std::vector<FrameRequest> FrameRpcServer::poll(int lane, int max_n, int timeout_
   return out;
 }
 
+void FrameRpcServer::deliver_internal(uint32_t id, int status, const std::string& msg, const std::string& payload) {
+  ReplyFn fn;
+  {
+    std::lock_guard<std::mutex> g(calls_->mu);
+    auto it = calls_->pending.find(id);
+    if (it == calls_->pending.end()) return;   // internal_poster's (id 0) or already failed by stop()
+    fn = std::move(it->second);
+    calls_->pending.erase(it);
+  }
+  fn(status, msg, payload);
+}
+
 void FrameRpcServer::respond(uint64_t token, int status, const std::string& msg, const std::string& payload) {
+  if ((token >> 32) == 0) {            // an internal request (no connection): its caller's callback
+    deliver_internal((uint32_t)token, status, msg, payload);
+    return;
+  }
   auto c = find((uint32_t)(token >> 32));
   if (!c || c->closed) return;
   if (c->proto == 2) {
@@ -1474,6 +1541,10 @@ void FrameRpcServer::respond_batch(const std::vector<FrameReply>& replies) {
   std::vector<std::pair<uint32_t, std::vector<const FrameReply*>>> groups;
   for (const FrameReply& r : replies) {
     const uint32_t cid = (uint32_t)(r.token >> 32);
+    if (cid == 0) {
+      deliver_internal((uint32_t)r.token, r.status, r.msg, r.payload);
+      continue;
+    }
     auto it = std::find_if(groups.begin(), groups.end(), [&](const auto& g) { return g.first == cid; });
     if (it == groups.end()) {
       groups.emplace_back(cid, std::vector<const FrameReply*>());

@@ -145,6 +145,11 @@ class FrameRpcServer {
   // queued on the method's lane as caller {cid, user}, their replies dropped.  The returned
   // function stays safe to call from any thread after the call or the server is gone.
   std::function<void(uint32_t, std::string)> internal_poster(const std::string& cid, const std::string& user);
+  // Like internal_poster, but the reply comes back: `done(status, msg, payload)` runs on the
+  // Python thread that answers (it must not block), or with UNAVAILABLE (14) at once when the
+  // server has stopped, or from stop() for calls still unanswered then.
+  using ReplyFn = std::function<void(int, const std::string&, const std::string&)>;
+  std::function<void(uint32_t, std::string, ReplyFn)> internal_caller(const std::string& cid, const std::string& user);
   // ---- kind-2 bridge (Python side; the GIL is released around the blocking calls) ----------
   // 0 = a message in *out, 1 = the client half-closed, 2 = cancelled / connection gone, 3 = timeout.
   int stream_recv(uint64_t token, int timeout_ms, std::string* out);
@@ -227,6 +232,15 @@ class FrameRpcServer {
     std::vector<uint64_t> tokens;
   };
   std::shared_ptr<WakeHub> hub_;
+  // internal_caller() calls waiting for their reply: token (0 << 32) | id, id > 0
+  struct InternalCalls {
+    std::mutex mu;
+    uint32_t next = 1;
+    bool stopped = false;
+    std::unordered_map<uint32_t, ReplyFn> pending;
+  };
+  std::shared_ptr<InternalCalls> calls_ = std::make_shared<InternalCalls>();
+  void deliver_internal(uint32_t id, int status, const std::string& msg, const std::string& payload);
   std::vector<int> wake_fds_;
   std::vector<std::unique_ptr<WakeQueue>> wake_qs_;
   void run_wakes(int idx);

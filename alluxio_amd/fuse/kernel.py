@@ -571,6 +571,8 @@ class FuseKernelServer:
             f = SETATTR_IN.unpack_from(body)
             valid, fh, size, mode, uid, gid = f[0], f[2], f[3], f[11], f[13], f[14]
             path = self._path(nodeid)
+            if fh and valid & FATTR_SIZE:
+                self._wait_writes(fh)          # an ftruncate lands after the writes acked before it
             if valid & FATTR_MODE:
                 ops.chmod(path, mode)
             if valid & (FATTR_UID | FATTR_GID):
@@ -653,6 +655,9 @@ class FuseKernelServer:
             return bytes(ops.read(path, size, offset, fh))
         if op == WRITE:
             fh, offset, size = WRITE_IN.unpack_from(body)[:3]
+            # a write the native server passed up (out of order, or after a batch error) goes after
+            # the batches it already acknowledged for this handle
+            self._wait_writes(fh)
             data = body[WRITE_IN.size:WRITE_IN.size + size]
             n = ops.write(self._path(nodeid), data, offset, fh)
             return struct.pack("<II", n, 0)
@@ -663,7 +668,11 @@ class FuseKernelServer:
                 self._inval(self._path(nodeid))
             ops.flush(None, fh)
             return b""
-        if op in (FSYNC, FSYNCDIR):
+        if op == FSYNC:
+            fh = struct.unpack_from("<Q", body)[0]
+            self._wait_writes(fh)              # acknowledged bytes are in the output stream on return
+            return b""
+        if op == FSYNCDIR:
             return b""
         if op == RELEASE:
             fh = struct.unpack_from("<Q", body)[0]

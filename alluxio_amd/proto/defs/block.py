@@ -19,11 +19,14 @@ msg ReadResponse chunk=1:Chunk
 msg WriteRequestCommand type=1:RequestType id=2:i64 offset=3:i64 tier=4:i32 flush=5:bool
     create_ufs_file_options=6:alluxio.proto.dataserver.CreateUfsFileOptions
     create_ufs_block_options=7:alluxio.proto.dataserver.CreateUfsBlockOptions
-    medium_type=8:str pin_on_create=9:bool space_to_reserve=10:i64
+    medium_type=8:str pin_on_create=9:bool space_to_reserve=10:i64 hold_for_append=20:bool
 msg AppendBlock block_id=1:i64 length=2:i64
 msg WriteRequest command=1:WriteRequestCommand|value chunk=2:Chunk|value append_block=20:AppendBlock|value
 msg WriteResponse offset=1:i64
 msg NativeWriteCommitRequest session_id=1:i64 block_id=2:i64 length=3:i64 pin=4:bool ufs_read=5:bool
+    hold_for_append=6:bool
+msg NativeCommitBatchRequest block_id=1:i64* length=2:i64* crc_piece=3:i64* crc=4:bytes* ufs_read=5:bool*
+msg NativeCommitBatchResponse failed=1:i64* message=2:str
 msg AsyncCacheRequest block_id=1:i64 source_host=2:str source_port=3:i32
     open_ufs_block_options=4:alluxio.proto.dataserver.OpenUfsBlockOptions length=5:i64
 msg AsyncCacheResponse
@@ -50,6 +53,7 @@ msg UnlockDeviceBlockResponse
 msg OpenDeviceWriteRequest block_id=1:i64 length=2:i64 tier=3:i32 medium_type=4:str pin_on_create=5:bool
     session_id=6:i64
 msg CommitDeviceWriteRequest block_id=1:i64 session_id=2:i64 length=3:i64 pin_on_create=4:bool abort=5:bool
+    hold_for_append=6:bool
 msg CommitDeviceWriteResponse
 msg PeerTransferRequest block_id=1:i64 src_rank=2:i32 dst_rank=3:i32 offset=4:i64 length=5:i64
     tag=6:i64 src_address=7:str
@@ -69,6 +73,7 @@ rpc BlockWorker OpenDeviceBlock OpenDeviceBlockRequest DeviceBlockHandle
 rpc BlockWorker UnlockDeviceBlock UnlockDeviceBlockRequest UnlockDeviceBlockResponse
 rpc BlockWorker PeerTransfer PeerTransferRequest PeerTransferResponse
 rpc BlockWorker NativeWriteCommit NativeWriteCommitRequest WriteResponse
+rpc BlockWorker NativeCommitBatch NativeCommitBatchRequest NativeCommitBatchResponse
 rpc BlockWorker OpenDeviceWrite OpenDeviceWriteRequest DeviceBlockHandle
 rpc BlockWorker CommitDeviceWrite CommitDeviceWriteRequest CommitDeviceWriteResponse
 rpc BlockWorker SessionHeartbeat SessionHeartbeatRequest SessionHeartbeatResponse

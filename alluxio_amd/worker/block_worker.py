@@ -226,9 +226,14 @@ class BlockWorker:
         self.write_ptr(session_id, block_id, offset, t.data_ptr(), t.numel() * t.element_size(), kind, stream, True)
         self.metrics.counter("BytesWrittenAlluxio").inc(t.numel() * t.element_size())
 
-    def commit_block(self, session_id: int, block_id: int, pin: bool = False) -> None:
+    def commit_block(self, session_id: int, block_id: int, pin: bool = False, hold: bool = False) -> None:
+        """Commit a temp block and report it to the master.  ``hold``: a CACHE_THROUGH tee block --
+        keep it from eviction until the file's UFS stream has appended it (BlockStore::hold_block,
+        released by the AppendBlock copy)."""
         with native_errors():
             self.native.commit_block(session_id, block_id, pin)
+            if hold:
+                self.native.hold_block(block_id)
         # the commit's added-event is reported by CommitBlock already
         self._report_commit(block_id)
 
@@ -652,7 +657,38 @@ class BlockWorker:
                 tierAlias=info.tier_alias, blockId=block_id, length=info.length, mediumType=info.medium))
         self.metrics.counter("BlocksCommitted").inc()
 
-    def _report_commits(self, block_ids, crcs: dict) -> None:
+    def report_native_commits(self, block_ids, crcs: dict) -> None:
+        """Master report of blocks the native committer committed (worker/services.py
+        NativeCommitBatch): ``_report_commits`` with the CommitBlocks call retried -- exponential
+        back-off from alluxio.user.rpc.retry.base.sleep up to .max.sleep, for at most
+        alluxio.user.rpc.retry.max.duration (the reference master client's RetryPolicy) -- before
+        the failure goes back to the committer."""
+        self._report_commits(block_ids, crcs, retry=True)
+
+    def _commit_rpc(self, call, retry: bool):
+        if not retry:
+            return call()
+        import random
+        base = self.conf.get_ms("alluxio.user.rpc.retry.base.sleep") / 1000.0
+        cap = self.conf.get_ms("alluxio.user.rpc.retry.max.sleep") / 1000.0
+        deadline = time.monotonic() + self.conf.get_ms("alluxio.user.rpc.retry.max.duration") / 1000.0
+        attempt = 0
+        while True:
+            try:
+                return call()
+            except Exception as e:  # noqa: BLE001
+                msg = str(e).upper()
+                if "UNIMPLEMENTED" in msg or "UNKNOWN METHOD" in msg:
+                    raise                        # not transient: the per-block fallback handles it
+                attempt += 1
+                pause = min(cap, base * (2 ** (attempt - 1)))
+                pause = pause / 2 + random.random() * pause / 2
+                if time.monotonic() + pause > deadline:
+                    raise
+                LOG.warning("block commit report to the master failed (attempt %d), retrying: %s", attempt, e)
+                time.sleep(pause)
+
+    def _report_commits(self, block_ids, crcs: dict, retry: bool = False) -> None:
         """``_report_commit`` for a batch of freshly committed blocks: one CommitBlocks call per
         16384 blocks with parallel arrays (falls back to per-block CommitBlock against a master
         without the extension)."""
@@ -690,7 +726,7 @@ class BlockWorker:
                                                     lengths=lens[i:i + step], tierIndex=tix[i:i + step],
                                                     tiers=tiers, mediums=mediums, usedBytesOnTiers=used)
                 try:
-                    bm.CommitBlocks(req)
+                    self._commit_rpc(lambda: bm.CommitBlocks(req), retry)
                 except Exception as e:  # noqa: BLE001 - a master without the extension RPC
                     if "UNIMPLEMENTED" not in str(e).upper() and "unknown method" not in str(e).lower():
                         raise

@@ -28,6 +28,7 @@ LOG = logging.getLogger(__name__)
 READ_BLOCK_PATH = f"/{SVC_BLOCK_WORKER}/ReadBlock"
 WRITE_BLOCK_PATH = f"/{SVC_BLOCK_WORKER}/WriteBlock"
 COMMIT_PATH = f"/{SVC_BLOCK_WORKER}/NativeWriteCommit"
+COMMIT_BATCH_PATH = f"/{SVC_BLOCK_WORKER}/NativeCommitBatch"
 
 
 def available() -> bool:
@@ -58,6 +59,16 @@ class WorkerDataServer:
         self.ufs_roots = lib().UfsMounts()
         worker.native_ufs_roots = self.ufs_roots
         native_cold = conf.get_bool("alluxio.worker.data.server.native.ufs.read.enabled", "true")
+        # the native block commit (csrc/data_server.cpp BlockCommitter): WriteBlock streams and cold
+        # read-throughs hand their blocks to a committer thread -- streamed per-page CRC32C of HBM
+        # blocks, store commit, one NativeCommitBatch (master CommitBlocks) per group of blocks
+        self.stats = lib().DataServerStats()
+        self.committer = None
+        if conf.get_bool("alluxio.worker.data.server.native.commit.enabled", "true"):
+            self.committer = lib().BlockCommitter(
+                worker.native, self.frontend.method_index(COMMIT_BATCH_PATH),
+                conf.get_bool("alluxio.worker.data.crc.device.enabled", "true"),
+                conf.get_bool("alluxio.worker.data.crc.enabled"), self.stats)
         # ReadBlock: cached blocks from the store; cold blocks of registered mounts read through
         # from the UFS on a background thread per call and committed via NativeWriteCommit
         self.stats = lib().serve_block_reads(
@@ -68,7 +79,8 @@ class WorkerDataServer:
             commit_method=self.frontend.method_index(COMMIT_PATH),
             ufs_slot_bytes=conf.get_bytes("alluxio.worker.ufs.ingest.chunk.size", "8MB"),
             ufs_depth=conf.get_int("alluxio.worker.ufs.ingest.depth", "3"),
-            ufs_max_active=conf.get_int("alluxio.worker.data.server.native.ufs.read.max.active", "256"))
+            ufs_max_active=conf.get_int("alluxio.worker.data.server.native.ufs.read.max.active", "256"),
+            stats=self.stats, committer=self.committer)
         # WriteBlock of ALLUXIO_BLOCK writes: chunks into the store on the I/O threads, the commit
         # (CRC, master report) as the internal NativeWriteCommit call (BlockWorkerService).
         # UFS_FILE writes of mounts the worker found to be local directories: into the file.
@@ -77,7 +89,7 @@ class WorkerDataServer:
             self.frontend.server, self.frontend.method_index(WRITE_BLOCK_PATH),
             self.frontend.method_index(COMMIT_PATH), worker.native,
             conf.get_bytes("alluxio.worker.network.writer.staging.size", "4MB"), self.stats,
-            self.ufs_roots if native_ufs_write else None)
+            self.ufs_roots if native_ufs_write else None, committer=self.committer)
         self.port = None
 
     def start(self) -> int:
@@ -97,11 +109,15 @@ class WorkerDataServer:
         m.counter("BytesWrittenUfsAll").add_source(lambda: st.ufs_write_bytes)
         m.gauge("DataServerNativeColdStreams", lambda: st.cold_streams)
         m.gauge("DataServerNativeColdActive", lambda: st.cold_active)
+        m.gauge("DataServerNativeCommits", lambda: st.commits)
+        m.gauge("DataServerNativeCommitBatches", lambda: st.commit_batches)
+        m.gauge("DataServerNativeCommitFailures", lambda: st.commit_failures)
         return self.port
 
     def stop(self) -> None:
         import time
         self.frontend.stop()
+        self.committer = None      # its thread drains what it holds, then exits (it owns a store ref)
         # background UFS readers of cancelled cold reads finish their current read, wait for their
         # H2D copies and drop their temp blocks: the store must outlive them
         deadline = time.time() + 30

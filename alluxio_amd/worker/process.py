@@ -128,7 +128,18 @@ class AlluxioWorkerProcess:
         ``...as.uuid`` is true: one socket file per worker)."""
         a = self.conf.get_raw("alluxio.worker.data.server.domain.socket.address")
         if not a:
-            return None
+            if a is not None or not self.conf.get_bool("alluxio.worker.data.server.domain.socket.default.enabled",
+                                                       "true"):
+                return None              # explicitly empty, or the default socket is off
+            # the same-node default: one socket per worker in a short per-user directory (sun_path
+            # holds 108 bytes)
+            import uuid
+            d = f"/tmp/alluxio-uds-{os.getuid()}"
+            try:
+                os.makedirs(d, mode=0o700, exist_ok=True)
+            except OSError:
+                return None
+            return os.path.join(d, uuid.uuid4().hex[:16])
         if self.conf.get_bool("alluxio.worker.data.server.domain.socket.as.uuid", "false"):
             import uuid
             return os.path.join(a, uuid.uuid4().hex)

@@ -196,7 +196,7 @@ class BlockWorkerService:
             from ..utils.exceptions import PermissionDeniedException
             raise PermissionDeniedException("NativeWriteCommit is internal to the worker's data server")
         if not req.ufs_read:
-            self.w.commit_block(req.session_id, req.block_id, req.pin)
+            self.w.commit_block(req.session_id, req.block_id, req.pin, req.hold_for_append)
             return pb.block.WriteResponse(offset=req.length)
         # a cold ReadBlock the native server read through from the UFS: posted by its reader once
         # the whole block is in the store (the call itself may be gone); the session is ours now
@@ -207,6 +207,28 @@ class BlockWorkerService:
         finally:
             self.w.cleanup_session(req.session_id)    # aborts the temp block if the commit failed
         return pb.block.WriteResponse(offset=req.length)
+
+    def NativeCommitBatch(self, req, ctx):
+        """The master report of the blocks the native committer (csrc/data_server.cpp
+        BlockCommitter) committed since its last report: their streamed CRCs are kept and ONE
+        CommitBlocks call tells the master about all of them (retried for
+        alluxio.user.rpc.retry.max.duration).  A failure fails every block of the batch: the
+        committer removes them again and fails their streams.  Internal to the data server."""
+        if not getattr(ctx, "internal", False):
+            from ..utils.exceptions import PermissionDeniedException
+            raise PermissionDeniedException("NativeCommitBatch is internal to the worker's data server")
+        import numpy as np
+        ids = list(req.block_id)
+        crcs = {}
+        for bid, piece, c in zip(ids, req.crc_piece, req.crc):
+            if piece and c:
+                crcs[bid] = (int(piece), np.frombuffer(c, dtype="<u4").tolist())
+        self.w.report_native_commits(ids, crcs)
+        ufs = [n for n, u in zip(req.length, req.ufs_read) if u]
+        if ufs:
+            self.w.metrics.counter("BytesReadUfsAll").inc(sum(ufs))
+            self.w.metrics.counter("BytesReadUfsThrough").inc(sum(ufs))
+        return pb.block.NativeCommitBatchResponse()
 
     def WriteBlock(self, request_iter, ctx):
         it = iter(request_iter)
@@ -229,15 +251,18 @@ class BlockWorkerService:
         reserve = cmd.space_to_reserve or self.conf.get_bytes("alluxio.worker.file.buffer.size", "1MB")
         self.w.create_block(session, bid, tier if not medium else -1, medium, reserve, cmd.pin_on_create)
         committed = False
+        hold = cmd.hold_for_append
         try:
             for req in it:
                 if req.HasField("chunk"):
                     data = req.chunk.data
                     self.w.write_bytes(session, bid, pos, data)
                     pos += len(data)
-                elif req.HasField("command") and req.command.flush:
-                    yield pb.block.WriteResponse(offset=pos)
-            self.w.commit_block(session, bid, cmd.pin_on_create)
+                elif req.HasField("command"):
+                    hold = hold or req.command.hold_for_append
+                    if req.command.flush:
+                        yield pb.block.WriteResponse(offset=pos)
+            self.w.commit_block(session, bid, cmd.pin_on_create, hold)
             committed = True
             yield pb.block.WriteResponse(offset=pos)
         finally:
@@ -316,6 +341,7 @@ class BlockWorkerService:
         import numpy as np
         session = ids.create_session_id()
         lock_id = self.w.lock_block(session, block_id)
+        self.w.native.release_hold(block_id)      # the commit's append hold: our lock keeps it now
         try:
             buf = np.empty(min(length, 8 << 20), dtype=np.uint8)
             off = 0
@@ -477,7 +503,7 @@ class BlockWorkerService:
             else:
                 with native_errors():
                     self.w.native.external_write(req.session_id, req.block_id, 0, req.length)
-                self.w.commit_block(req.session_id, req.block_id, req.pin_on_create)
+                self.w.commit_block(req.session_id, req.block_id, req.pin_on_create, req.hold_for_append)
                 self.w.metrics.counter("BytesWrittenAlluxio").inc(req.length)
                 self.w.metrics.counter("BytesWrittenDomain").inc(req.length)
         finally:

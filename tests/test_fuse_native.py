@@ -289,3 +289,53 @@ def test_cache_listing_from_serialized_replies():
     d = struct.unpack_from("<QQQQQQIIIIIIIIII", s.entry("/ds/sub"), 40)
     assert d[9] == 0o40755 and d[10] == 2
     assert struct.unpack_from("<QQQQ", s.entry("/ds/sub"))[2:] == (1, 1)
+
+
+def test_native_write_behind_fsync_and_out_of_order_write_wait_for_batches(tmp_path):
+    """fsync() on a write-behind handle returns only once every acknowledged byte is in the file's
+    output stream; a write the native server hands to Python (here: out of order) is applied after
+    the batches acknowledged before it (write-behind ordering)."""
+    m = _Mount(tmp_path, "native")
+    try:
+        m.mount()
+        script = f"""
+import os, sys
+m = {m.mnt!r}
+os.makedirs(m + "/wb", exist_ok=True)
+data = bytes(range(256)) * ((10 << 20) // 256)
+fd = os.open(m + "/wb/s.bin", os.O_CREAT | os.O_WRONLY, 0o644)
+for i in range(0, len(data), 1 << 20):
+    os.write(fd, data[i:i + (1 << 20)])
+os.fsync(fd)
+print("synced", flush=True)
+sys.stdin.readline()
+try:
+    os.pwrite(fd, b"x", 5)          # out of order: not supported for write-once files
+    print("pwrite ok", flush=True)
+except OSError as e:
+    print("pwrite errno", e.errno, flush=True)
+os.close(fd)
+print("closed", flush=True)
+"""
+        import subprocess
+        p = subprocess.Popen([sys.executable, "-c", script], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE, text=True)
+        try:
+            line = p.stdout.readline()
+            assert line.strip() == "synced", (line, p.stderr.read() if p.poll() is not None else "")
+            ops = m.srv.ops
+            outs = [of.fout for of in ops._open.values() if of.path.endswith("/wb/s.bin") and of.fout is not None]
+            assert outs and outs[0].tell() == 10 << 20       # every acknowledged byte went in by fsync
+            p.stdin.write("go\n")
+            p.stdin.flush()
+            rest = p.communicate(timeout=60)[0]
+        finally:
+            if p.poll() is None:
+                p.kill()
+        assert "closed" in rest, rest
+        # the out-of-order write ran after the 10 MiB (it failed against the write-once file, which
+        # keeps every sequential byte)
+        got = m.fs.read_file("/wb/s.bin")
+        assert len(got) == 10 << 20 and got[:256] == bytes(range(256))
+    finally:
+        m.close()

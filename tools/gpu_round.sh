@@ -289,6 +289,16 @@ for s in $STEPS; do
       run ww8_mc 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --out "$OUT/r6_worker_write_8s.jsonl"
       run ww8_ct 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r6_worker_write_8s.jsonl"
       ;;
+    r6commit)
+      # native block commit: sustained 8 s writes, 64 MiB blocks, loopback TCP and the (now default) domain socket
+      run ww8nc_mc_tcp 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_worker_write_8s_native_commit.jsonl"
+      run ww8nc_ct_tcp 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_worker_write_8s_native_commit.jsonl"
+      run ww8nc_mc_uds 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --out "$OUT/r6_worker_write_8s_native_commit.jsonl"
+      run ww8nc_ct_uds 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r6_worker_write_8s_native_commit.jsonl"
+      ;;
+    r6tests)
+      run pytest_gpu_r6 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+      ;;
     validate)
       run pytest_gpu_validate 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       run smoke_validate 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"
