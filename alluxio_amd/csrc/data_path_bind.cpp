@@ -15,6 +15,7 @@
 
 #include "block_source.h"
 #include "data_server.h"
+#include "stress_bench.h"
 #include "hdfs_packets.h"
 #include "frame_rpc.h"
 
@@ -470,6 +471,51 @@ void bind_data_path(py::module_& m) {
       .def(py::init<std::shared_ptr<BlockStore>, uint32_t, bool, bool, std::shared_ptr<DataServerStats>>(),
            py::arg("store"), py::arg("method"), py::arg("crc_device"), py::arg("crc_host"), py::arg("stats"));
   m.def("thread_streams_created", &thread_streams_created);
+  // Native StressWorkerBench client (csrc/stress_bench.h): `blocks` = one dict per block of the
+  // file: {"length", "kind": "grpc"|"ipc"|"host", grpc: "host", "port", "unix_path", "block_id",
+  // "chunk", "channel_id", "user", "timeout_ms"; arenas: "base", "pages", "page_size", "device"}.
+  m.def("run_stress_reads", [](py::list blocks, uint64_t block_size, int threads, uint64_t buffer, uint64_t chunk,
+                               double warmup_s, double duration_s, bool prefetch) {
+          std::vector<BenchBlock> bs;
+          for (py::handle h : blocks) {
+            py::dict d = py::reinterpret_borrow<py::dict>(h);
+            BenchBlock b;
+            b.length = d["length"].cast<uint64_t>();
+            const std::string kind = d["kind"].cast<std::string>();
+            b.kind = kind == "ipc" ? 1 : kind == "host" ? 2 : 0;
+            if (b.kind == 0) {
+              b.grpc.host = d["host"].cast<std::string>();
+              b.grpc.port = d["port"].cast<int>();
+              b.grpc.unix_path = d.contains("unix_path") ? d["unix_path"].cast<std::string>() : "";
+              b.grpc.block_id = d["block_id"].cast<int64_t>();
+              b.grpc.chunk = d.contains("chunk") ? d["chunk"].cast<uint64_t>() : (1u << 20);
+              b.grpc.channel_id = d.contains("channel_id") ? d["channel_id"].cast<std::string>() : "";
+              b.grpc.user = d.contains("user") ? d["user"].cast<std::string>() : "";
+              b.grpc.timeout_ms = d.contains("timeout_ms") ? d["timeout_ms"].cast<int>() : 60000;
+            } else {
+              b.base = d["base"].cast<uint64_t>();
+              b.pages = d["pages"].cast<std::vector<int64_t>>();
+              b.page_size = d["page_size"].cast<uint64_t>();
+              b.device = d.contains("device") ? d["device"].cast<int>() : 0;
+            }
+            bs.push_back(std::move(b));
+          }
+          BenchResult r;
+          {
+            py::gil_scoped_release rel;
+            r = run_stress_reads(bs, block_size, threads, buffer, chunk, warmup_s, duration_s, prefetch);
+          }
+          py::dict out;
+          out["bytes"] = r.bytes;
+          out["reads"] = r.reads;
+          out["opens"] = r.opens;
+          out["block_opens"] = r.block_opens;
+          out["seconds"] = r.seconds;
+          out["per_thread"] = r.per_thread;
+          out["errors"] = r.errors;
+          return out;
+        }, py::arg("blocks"), py::arg("block_size"), py::arg("threads"), py::arg("buffer"), py::arg("chunk"),
+        py::arg("warmup_s"), py::arg("duration_s"), py::arg("prefetch") = true);
   auto mounts = py::class_<UfsMounts, std::shared_ptr<UfsMounts>>(m, "UfsMounts")
       .def(py::init<>())
       .def("set", &UfsMounts::set, py::arg("mount_id"), py::arg("root"))

@@ -21,9 +21,9 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
 SOURCES = ["kernels.hip", "evict_alloc.hip", "page_cache_put.hip", "block_store.cpp", "cpu_codecs.cpp", "ipc.cpp", "ring_read.cpp", "page_cache.cpp", "meta_codec.cpp", "fuse_server.cpp", "http_blob.cpp",
-           "frame_rpc.cpp", "journal_log.cpp", "sigv4.cpp", "numa_host.cpp", "data_server.cpp", "block_source.cpp", "hdfs_packets.cpp", "data_path_bind.cpp", "bindings.cpp"]
+           "frame_rpc.cpp", "journal_log.cpp", "sigv4.cpp", "numa_host.cpp", "data_server.cpp", "block_source.cpp", "stress_bench.cpp", "hdfs_packets.cpp", "data_path_bind.cpp", "bindings.cpp"]
 HEADERS = ["kernels.h", "block_store.h", "cpu_codecs.h", "ipc.h", "ring_read.h", "page_cache.h", "page_cache_bind.h", "seg_ring.h", "frame_rpc.h", "journal_log.h", "meta_codec.h", "fuse_server.h", "h2_abi.h", "data_server.h", "sigv4.h", "numa_host.h", "http_blob.h",
-           "block_source.h", "hdfs_packets.h"]
+           "block_source.h", "stress_bench.h", "hdfs_packets.h"]
 
 
 def ext_path() -> str:

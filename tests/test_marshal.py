@@ -84,7 +84,9 @@ def test_grpc_block_streams(tmp_path, monkeypatch, zero_copy):
             "alluxio.user.short.circuit.enabled": "false",
             # the grpcio client path (the native reader / writer frame in C++: test_data_server.py)
             "alluxio.user.native.reader.enabled": "false",
-            "alluxio.user.native.writer.enabled": "false"}
+            "alluxio.user.native.writer.enabled": "false",
+            # the grpcio port and its Python servicer (the default domain socket is the native one)
+            "alluxio.worker.data.server.domain.socket.default.enabled": "false"}
     with LocalAlluxioCluster(num_workers=1, conf=conf, grpc=True, work_dir=str(tmp_path)) as cluster:
         fs = cluster.client()
         data = np.random.default_rng(1).integers(0, 256, (7 << 20) + 5, dtype=np.uint8)

@@ -85,6 +85,8 @@ def main(argv=None) -> int:
     ap.add_argument("--duration", default="10s")
     ap.add_argument("--warmup", default="3s")
     ap.add_argument("--transports", default="grpc,ipc")
+    ap.add_argument("--mode", default="threads", choices=("threads", "native-threads"),
+                    help="Python reader threads (FileInStream) or the native C++ reader threads")
     ap.add_argument("--tier", default="hbm:0", help="worker MEM tier dir (hbm:N or dram)")
     ap.add_argument("--reader-buffer", default="4MB", help="alluxio.user.native.reader.buffer.size")
     ap.add_argument("--client-prop", action="append", default=[], help="extra client property k=v")
@@ -140,7 +142,7 @@ def main(argv=None) -> int:
                 per = max(1, int(t) // nproc)
                 args = ["--threads", str(per), "--file-size", a.file_size, "--buffer-size", a.buffer_size,
                         "--block-size", a.block_size, "--duration", a.duration, "--warmup", a.warmup,
-                        "--mode", "threads"]
+                        "--mode", a.mode]
                 t0 = time.time()
                 s0 = (stats.streams, stats.bytes, stats.declined) if stats is not None else (0, 0, 0)
                 procs = [subprocess.Popen([sys.executable, "-c", CLIENT.format(root=ROOT, addr=c.master.address,
@@ -161,7 +163,7 @@ def main(argv=None) -> int:
                 r = {"throughput_MBps": sum(x["throughput_MBps"] for x in results),
                      "bytes": sum(x["bytes"] for x in results), "duration_s": results[0]["duration_s"],
                      "errors": [e for x in results for e in x["errors"]]}
-                row = {"bench": "StressWorkerBench --mode threads (host readers, separate client process)",
+                row = {"bench": f"StressWorkerBench --mode {a.mode} (host readers, separate client process)",
                        "transport": transport, "tier": a.tier, "threads": per * nproc, "buffer": a.buffer_size,
                        "file_size": a.file_size, "block_size": a.block_size,
                        "throughput_MBps": round(r["throughput_MBps"], 1), "bytes": r["bytes"],
@@ -169,6 +171,8 @@ def main(argv=None) -> int:
                        "reader_buffer": a.reader_buffer, "client_props": a.client_prop,
                        "client_procs": nproc}
                 row["client_placement"] = [x.get("placement", "") for x in results]
+                if results[0].get("native"):
+                    row["native"] = [x.get("native") for x in results]
                 row["bound_to_gpu_node"] = bool(cpus)
                 row["reader_buffer"] = a.reader_buffer
                 if a.d2h_roof:
