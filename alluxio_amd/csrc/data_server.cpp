@@ -553,6 +553,93 @@ class S3ObjectReader : public UfsReader {
   std::string key_;
 };
 
+// A UFS the I/O threads cannot reach (HDFS, HTTPS S3, ...), read through the worker's Python UFS
+// by internal ReadUfsRange calls from the reader's pool thread: only the first cold read of such a
+// mount takes it (later ones go to the Python servicer directly, UfsMounts::is_python).
+class PythonRangeReader : public UfsReader {
+ public:
+  PythonRangeReader(BlockCommitter::Caller caller, uint32_t method, int64_t mount_id, std::string path)
+      : caller_(std::move(caller)), method_(method), mount_(mount_id), path_(std::move(path)) {}
+  bool read(uint64_t off, uint64_t n, uint8_t* dst, std::string* err) override {
+    uint64_t done = 0;
+    while (done < n) {
+      if (cancel && cancel->load(std::memory_order_relaxed)) {
+        status_ = 1;
+        *err = "cancelled";
+        return false;
+      }
+      const uint64_t k = std::min<uint64_t>(n - done, 8u << 20);
+      // ReadUfsRangeRequest: mount_id=1 ufs_path=2 offset=3 length=4
+      std::string m;
+      h2::put_varint(m, (1u << 3));
+      h2::put_varint(m, (uint64_t)mount_);
+      h2::put_varint(m, (2u << 3) | 2);
+      h2::put_varint(m, path_.size());
+      m += path_;
+      h2::put_varint(m, (3u << 3));
+      h2::put_varint(m, off + done);
+      h2::put_varint(m, (4u << 3));
+      h2::put_varint(m, k);
+      struct Reply {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool got = false;
+        int status = 0;
+        std::string msg, payload;
+      };
+      auto rep = std::make_shared<Reply>();
+      caller_(method_, std::move(m), [rep](int s, const std::string& msg, const std::string& payload) {
+        std::lock_guard<std::mutex> g(rep->mu);
+        rep->got = true;
+        rep->status = s;
+        rep->msg = msg;
+        rep->payload = payload;
+        rep->cv.notify_all();
+      });
+      std::unique_lock<std::mutex> lk(rep->mu);
+      if (!rep->cv.wait_for(lk, std::chrono::minutes(5), [&] { return rep->got; })) {
+        status_ = 14;
+        *err = "reading the UFS through the worker timed out";
+        return false;
+      }
+      if (rep->status) {
+        status_ = rep->status;
+        *err = rep->msg;
+        return false;
+      }
+      // ReadUfsRangeResponse: data=1 (bytes)
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(rep->payload.data());
+      const size_t pn = rep->payload.size();
+      size_t i = 0;
+      uint64_t got = 0;
+      while (i < pn) {
+        uint64_t key, len;
+        if (!h2::get_varint(p, pn, &i, &key)) break;
+        if ((key >> 3) == 1 && (key & 7) == 2 && h2::get_varint(p, pn, &i, &len) && len <= pn - i) {
+          got = std::min<uint64_t>(len, k);
+          std::memcpy(dst + done, p + i, (size_t)got);
+          i += (size_t)len;
+        } else {
+          break;
+        }
+      }
+      if (got != k) {
+        status_ = 11;
+        *err = "unexpected end of the UFS file at " + std::to_string(off + done + got);
+        return false;
+      }
+      done += k;
+    }
+    return true;
+  }
+
+ private:
+  BlockCommitter::Caller caller_;
+  uint32_t method_;
+  int64_t mount_;
+  std::string path_;
+};
+
 // State shared by a cold stream (I/O threads) and its background reader thread.
 struct ColdState {
   struct Slot {
@@ -591,6 +678,9 @@ struct ColdJob {
   std::function<void(uint32_t, std::string)> post;   // internal requests to Python (the commit)
   uint32_t commit_method = UINT32_MAX;
   std::shared_ptr<BlockCommitter> committer;         // native commit (instead of `post`) when set
+  // A mount the data server did not know at the call's start: resolves it (blocking internal call
+  // to the worker) and opens the reader; false with *status / *err when it cannot be read natively.
+  std::function<bool(std::unique_ptr<UfsReader>*, int*, std::string*)> resolve;
 
   void wake() {
     std::function<void()> w;
@@ -610,6 +700,25 @@ struct ColdJob {
     bool ok = true;
     uint64_t ingested = start;
     int err_status = 13;
+    if (!reader && resolve && !resolve(&reader, &err_status, &err)) reader.reset();
+    if (!reader) {                    // unresolvable mount: fail the stream, drop the session
+      if (err.empty()) err = "the UFS of this block cannot be read natively";
+      {
+        std::lock_guard<std::mutex> g(st->mu);
+        st->failed = true;
+        st->err = err;
+        st->err_status = err_status;
+        st->read_done = true;
+        st->job_exited = true;
+      }
+      try {
+        store->cleanup_session(session);
+      } catch (...) {
+      }
+      stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
+      wake();
+      return;
+    }
     reader->cancel = &st->cancel_flag;
     try {
       if (store->has_device()) {
@@ -2373,6 +2482,7 @@ void UfsMounts::remove(int64_t mount_id) {
   std::lock_guard<std::mutex> g(mu_);
   roots_.erase(mount_id);
   s3_.erase(mount_id);
+  python_.erase(mount_id);
 }
 
 void UfsMounts::set_s3(int64_t mount_id, const std::string& host, int port, const std::string& bucket,
@@ -2421,6 +2531,16 @@ bool UfsMounts::resolve_s3(int64_t mount_id, const std::string& ufs_path, std::s
   return true;
 }
 
+void UfsMounts::mark_python(int64_t mount_id) {
+  std::lock_guard<std::mutex> g(mu_);
+  python_[mount_id] = true;
+}
+
+bool UfsMounts::is_python(int64_t mount_id) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return python_.count(mount_id) != 0;
+}
+
 size_t UfsMounts::size() const {
   std::lock_guard<std::mutex> g(mu_);
   return roots_.size() + s3_.size();
@@ -2450,6 +2570,30 @@ bool UfsMounts::resolve(int64_t mount_id, const std::string& ufs_path, std::stri
 
 namespace {
 
+// The reader of `o`'s file when its mount is registered: 1 = *reader set, 0 = mount not registered
+// (or the path is outside it), -1 = the file cannot be opened (*status / *msg set).
+int open_ufs_reader(const UfsMounts& mounts, const UfsOpts& o, std::unique_ptr<UfsReader>* reader, int* status,
+                    std::string* msg) {
+  std::string local, key;
+  std::shared_ptr<const S3Mount> s3;
+  if (mounts.resolve(o.mount_id, o.ufs_path, &local)) {
+    const int fd = ::open(local.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      const int e = errno;
+      *status = grpc_status_of_errno(e);
+      *msg = "opening " + o.ufs_path + ": " + std::strerror(e);
+      return -1;
+    }
+    reader->reset(new LocalFileReader(fd));
+    return 1;
+  }
+  if (mounts.resolve_s3(o.mount_id, o.ufs_path, &s3, &key)) {
+    reader->reset(new S3ObjectReader(std::move(s3), std::move(key)));
+    return 1;
+  }
+  return 0;
+}
+
 // A native cold stream for `r` (the block is not in the store), or nullptr to hand the call to
 // Python (mount not registered, UFS-tier block, too many readers).
 std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const StoreRef& store, uint64_t max_chunk,
@@ -2459,7 +2603,8 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
                                                const std::shared_ptr<DataServerStats>& stats,
                                                std::function<void(uint32_t, std::string)> post, int* status,
                                                std::string* msg,
-                                               const std::shared_ptr<BlockCommitter>& committer = nullptr) {
+                                               const std::shared_ptr<BlockCommitter>& committer = nullptr,
+                                               BlockCommitter::Caller caller = nullptr) {
   UfsOpts o;
   if (!mounts || !parse_ufs_opts(r.ufs_opts, &o) || o.ufs_path.empty() || o.block_in_ufs_tier || o.block_size <= 0)
     return nullptr;
@@ -2473,21 +2618,68 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
   }
   const uint64_t end = r.length > 0 ? std::min<uint64_t>(block_len, off + (uint64_t)r.length) : block_len;
   std::unique_ptr<UfsReader> reader;
-  std::string local, key;
-  std::shared_ptr<const S3Mount> s3;
-  if (mounts->resolve(o.mount_id, o.ufs_path, &local)) {
-    const int fd = ::open(local.c_str(), O_RDONLY | O_CLOEXEC);
-    if (fd < 0) {
-      const int e = errno;
-      *status = grpc_status_of_errno(e);
-      *msg = "opening " + o.ufs_path + ": " + std::strerror(e);
-      return nullptr;
-    }
-    reader.reset(new LocalFileReader(fd));
-  } else if (mounts->resolve_s3(o.mount_id, o.ufs_path, &s3, &key)) {
-    reader.reset(new S3ObjectReader(std::move(s3), std::move(key)));
-  } else {
-    return nullptr;
+  std::function<bool(std::unique_ptr<UfsReader>*, int*, std::string*)> resolve;
+  const int opened = open_ufs_reader(*mounts, o, &reader, status, msg);
+  if (opened < 0) return nullptr;
+  if (opened == 0) {
+    // not registered yet: a plain local or S3 path of a mount not known to be Python's is resolved
+    // on the reader's pool thread (ResolveUfsMount) and then read natively
+    const std::string& p = o.ufs_path;
+    const bool plausible = p[0] == '/' || p.compare(0, 7, "file://") == 0 || p.compare(0, 5, "s3://") == 0 ||
+                           p.compare(0, 6, "s3a://") == 0;
+    if (!plausible || cfg.resolve_method == UINT32_MAX || !caller || mounts->is_python(o.mount_id)) return nullptr;
+    auto ms = mounts;
+    const uint32_t method = cfg.resolve_method, range_method = cfg.read_range_method;
+    resolve = [ms, o, method, range_method, caller](std::unique_ptr<UfsReader>* out, int* st,
+                                                    std::string* err) -> bool {
+      // ResolveUfsMountRequest: mount_id=1 ufs_path=2
+      std::string m;
+      h2::put_varint(m, (1u << 3));
+      h2::put_varint(m, (uint64_t)o.mount_id);
+      h2::put_varint(m, (2u << 3) | 2);
+      h2::put_varint(m, o.ufs_path.size());
+      m += o.ufs_path;
+      struct Reply {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool got = false;
+        int status = 0;
+        std::string msg;
+      };
+      auto rep = std::make_shared<Reply>();
+      caller(method, std::move(m), [rep](int s, const std::string& msg, const std::string&) {
+        std::lock_guard<std::mutex> g(rep->mu);
+        rep->got = true;
+        rep->status = s;
+        rep->msg = msg;
+        rep->cv.notify_all();
+      });
+      {
+        std::unique_lock<std::mutex> lk(rep->mu);
+        if (!rep->cv.wait_for(lk, std::chrono::seconds(60), [&] { return rep->got; })) {
+          *st = 14;
+          *err = "resolving the UFS of mount " + std::to_string(o.mount_id) + " timed out";
+          return false;
+        }
+      }
+      if (rep->status) {
+        *st = rep->status == 5 ? 5 : 14;
+        *err = "resolving the UFS of mount " + std::to_string(o.mount_id) + ": " + rep->msg;
+        return false;
+      }
+      const int r = open_ufs_reader(*ms, o, out, st, err);
+      if (r == 0) {                          // resolved, but not something the I/O threads reach
+        ms->mark_python(o.mount_id);         // its later cold reads go to the Python servicer
+        if (range_method == UINT32_MAX) {
+          *st = 14;
+          *err = "the UFS of mount " + std::to_string(o.mount_id) + " is served by the worker's Python data path";
+          return false;
+        }
+        out->reset(new PythonRangeReader(caller, range_method, o.mount_id, o.ufs_path));
+        return true;
+      }
+      return r > 0;
+    };
   }
   if (stats->cold_active.fetch_add(1, std::memory_order_relaxed) >= cfg.max_active) {
     stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
@@ -2515,6 +2707,7 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
   job->post = std::move(post);
   job->commit_method = cfg.commit_method;
   job->committer = committer;
+  job->resolve = std::move(resolve);
   const uint64_t chunk =
       r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk) : std::min<uint64_t>(1u << 20, max_chunk);
   std::unique_ptr<NativeStream> ns(new ColdReadStream(store, job->session, r.block_id, off, end, chunk, window,
@@ -2861,7 +3054,8 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uin
       if (r.has_ufs) {     // a cold block: read it through from the UFS (BlockReadHandler.openUfsBlock)
         if (committer && !committer->has_caller()) committer->set_caller(s->internal_caller(cid, user));
         auto cs = make_cold_stream(r, store, max_chunk, window, unix_peer, cold, mounts, slot_pool, stats,
-                                   s->internal_poster(cid, user), status, msg, committer);
+                                   s->internal_poster(cid, user), status, msg, committer,
+                                   cold.resolve_method != UINT32_MAX ? s->internal_caller(cid, user) : nullptr);
         if (cs || *status != 0) return cs;
       }
       stats->declined.fetch_add(1, std::memory_order_relaxed);

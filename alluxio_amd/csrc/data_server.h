@@ -145,6 +145,10 @@ class UfsMounts {
               const HttpOptions& http = HttpOptions());
   void remove(int64_t mount_id);
   size_t size() const;
+  // Mounts the worker resolved and found the I/O threads cannot reach (HDFS, HTTPS S3, ...): their
+  // cold reads go straight to Python.
+  void mark_python(int64_t mount_id);
+  bool is_python(int64_t mount_id) const;
   // The local path of `ufs_path` ("file:///x" or "/x") if mount `mount_id` is a registered local
   // directory and the path lies inside its root without "." / ".." components.
   bool resolve(int64_t mount_id, const std::string& ufs_path, std::string* local) const;
@@ -157,6 +161,7 @@ class UfsMounts {
   mutable std::mutex mu_;
   std::unordered_map<int64_t, std::string> roots_;
   std::unordered_map<int64_t, std::shared_ptr<const S3Mount>> s3_;
+  std::unordered_map<int64_t, bool> python_;
 };
 using LocalUfsRoots = UfsMounts;
 
@@ -166,6 +171,11 @@ struct ColdReadConfig {
   int depth = 3;                    // slots per stream (reads run this far ahead of the sends)
   int max_active = 256;             // concurrent background UFS readers; more go to Python
   uint32_t commit_method = UINT32_MAX;   // internal NativeWriteCommit (caches are committed in Python)
+  // internal ResolveUfsMount: a cold read of a mount the data server does not know yet asks the
+  // worker to resolve it (GetUfsInfo from the master, reference WorkerUfsManager.java:56-65) on the
+  // reader's pool thread, then reads natively -- no first read of a mount goes through Python
+  uint32_t resolve_method = UINT32_MAX;
+  uint32_t read_range_method = UINT32_MAX;   // internal ReadUfsRange (a resolved mount that is Python's)
 };
 
 // Serve `method` (the ReadBlock path's index) of `srv` from `store`.  `max_chunk` caps a client's

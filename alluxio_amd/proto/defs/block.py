@@ -27,6 +27,10 @@ msg NativeWriteCommitRequest session_id=1:i64 block_id=2:i64 length=3:i64 pin=4:
     hold_for_append=6:bool
 msg NativeCommitBatchRequest block_id=1:i64* length=2:i64* crc_piece=3:i64* crc=4:bytes* ufs_read=5:bool*
 msg NativeCommitBatchResponse failed=1:i64* message=2:str
+msg ResolveUfsMountRequest mount_id=1:i64 ufs_path=2:str
+msg ResolveUfsMountResponse native=1:bool
+msg ReadUfsRangeRequest mount_id=1:i64 ufs_path=2:str offset=3:i64 length=4:i64
+msg ReadUfsRangeResponse data=1:bytes
 msg AsyncCacheRequest block_id=1:i64 source_host=2:str source_port=3:i32
     open_ufs_block_options=4:alluxio.proto.dataserver.OpenUfsBlockOptions length=5:i64
 msg AsyncCacheResponse
@@ -74,6 +78,8 @@ rpc BlockWorker UnlockDeviceBlock UnlockDeviceBlockRequest UnlockDeviceBlockResp
 rpc BlockWorker PeerTransfer PeerTransferRequest PeerTransferResponse
 rpc BlockWorker NativeWriteCommit NativeWriteCommitRequest WriteResponse
 rpc BlockWorker NativeCommitBatch NativeCommitBatchRequest NativeCommitBatchResponse
+rpc BlockWorker ResolveUfsMount ResolveUfsMountRequest ResolveUfsMountResponse
+rpc BlockWorker ReadUfsRange ReadUfsRangeRequest ReadUfsRangeResponse
 rpc BlockWorker OpenDeviceWrite OpenDeviceWriteRequest DeviceBlockHandle
 rpc BlockWorker CommitDeviceWrite CommitDeviceWriteRequest CommitDeviceWriteResponse
 rpc BlockWorker SessionHeartbeat SessionHeartbeatRequest SessionHeartbeatResponse

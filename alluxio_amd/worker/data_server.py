@@ -29,6 +29,8 @@ READ_BLOCK_PATH = f"/{SVC_BLOCK_WORKER}/ReadBlock"
 WRITE_BLOCK_PATH = f"/{SVC_BLOCK_WORKER}/WriteBlock"
 COMMIT_PATH = f"/{SVC_BLOCK_WORKER}/NativeWriteCommit"
 COMMIT_BATCH_PATH = f"/{SVC_BLOCK_WORKER}/NativeCommitBatch"
+RESOLVE_MOUNT_PATH = f"/{SVC_BLOCK_WORKER}/ResolveUfsMount"
+READ_RANGE_PATH = f"/{SVC_BLOCK_WORKER}/ReadUfsRange"
 
 
 def available() -> bool:
@@ -80,7 +82,9 @@ class WorkerDataServer:
             ufs_slot_bytes=conf.get_bytes("alluxio.worker.ufs.ingest.chunk.size", "8MB"),
             ufs_depth=conf.get_int("alluxio.worker.ufs.ingest.depth", "3"),
             ufs_max_active=conf.get_int("alluxio.worker.data.server.native.ufs.read.max.active", "256"),
-            stats=self.stats, committer=self.committer)
+            stats=self.stats, committer=self.committer,
+            resolve_method=self.frontend.method_index(RESOLVE_MOUNT_PATH),
+            read_range_method=self.frontend.method_index(READ_RANGE_PATH))
         # WriteBlock of ALLUXIO_BLOCK writes: chunks into the store on the I/O threads, the commit
         # (CRC, master report) as the internal NativeWriteCommit call (BlockWorkerService).
         # UFS_FILE writes of mounts the worker found to be local directories: into the file.

@@ -230,6 +230,32 @@ class BlockWorkerService:
             self.w.metrics.counter("BytesReadUfsThrough").inc(sum(ufs))
         return pb.block.NativeCommitBatchResponse()
 
+    def ResolveUfsMount(self, req, ctx):
+        """A cold read of a mount the native data server has not seen: resolve its UFS the way the
+        reference worker does on demand (WorkerUfsManager.java:56-65 asks the master's GetUfsInfo)
+        and register it with the data server when its I/O threads can reach it (note_ufs_mount).
+        Internal to the data server; the cold read then runs natively."""
+        if not getattr(ctx, "internal", False):
+            from ..utils.exceptions import PermissionDeniedException
+            raise PermissionDeniedException("ResolveUfsMount is internal to the worker's data server")
+        opts = pb.dataserver.OpenUfsBlockOptions(ufs_path=req.ufs_path, mountId=req.mount_id)
+        self.w.note_ufs_mount(req.mount_id, self.w._ufs_for(opts))
+        roots = self.w.native_ufs_roots
+        native = roots is not None and (roots.resolve(req.mount_id, req.ufs_path) is not None or
+                                        roots.resolve_s3(req.mount_id, req.ufs_path) is not None)
+        self.w.metrics.counter("UfsMountsResolvedNatively").inc()
+        return pb.block.ResolveUfsMountResponse(native=native)
+
+    def ReadUfsRange(self, req, ctx):
+        """Bytes of a UFS file the data server's threads cannot read themselves (the first cold read
+        of a mount that resolved to a Python-only UFS).  Internal to the data server."""
+        if not getattr(ctx, "internal", False):
+            from ..utils.exceptions import PermissionDeniedException
+            raise PermissionDeniedException("ReadUfsRange is internal to the worker's data server")
+        opts = pb.dataserver.OpenUfsBlockOptions(ufs_path=req.ufs_path, mountId=req.mount_id, offset_in_file=0,
+                                                 block_size=req.offset + req.length)
+        return pb.block.ReadUfsRangeResponse(data=self.w.read_ufs_range(opts, req.offset, req.length))
+
     def WriteBlock(self, request_iter, ctx):
         it = iter(request_iter)
         first = next(it, None)

@@ -170,9 +170,9 @@ def test_stock_grpc_write_block_then_native_read(tmp_path):
 
 
 def test_ufs_read_through_bridged(tmp_path):
-    """A block that is not cached: ReadBlock with UFS options is served by the Python servicer
-    through the bridge (read-through caching), then natively once cached."""
-    with _cluster(tmp_path) as c:
+    """A block that is not cached, with native UFS reads off: ReadBlock with UFS options is served
+    by the Python servicer through the bridge (read-through caching), then natively once cached."""
+    with _cluster(tmp_path, {"alluxio.worker.data.server.native.ufs.read.enabled": "false"}) as c:
         fs = c.client()
         data = np.random.default_rng(4).integers(0, 256, (6 << 20) + 9, dtype=np.uint8)
         fs.write_file("/u", data, write_type="CACHE_THROUGH")
@@ -641,8 +641,11 @@ def test_native_cold_read_through(tmp_path):
         st = w.data_server.stats
         rfs = _remote_fs(c)
         try:
-            assert rfs.read_file("/cold/a") == files["/cold/a"].tobytes()   # Python: registers the mount
+            # the first cold read of the mount: resolved on demand (ResolveUfsMount), read natively
+            d0, s0 = st.declined, st.cold_streams
+            assert rfs.read_file("/cold/a") == files["/cold/a"].tobytes()
             assert len(w.data_server.ufs_roots) == 1
+            assert st.declined == d0 and st.cold_streams - s0 == len(_blocks(rfs, "/cold/a"))
             d0, s0, c0 = st.declined, st.cold_streams, st.cold_cached
             free0 = w.worker.native.dir_available(0)
             assert rfs.read_file("/cold/b") == files["/cold/b"].tobytes()

@@ -272,3 +272,40 @@ def test_native_s3_upload_retries_then_aborts(blob, tmp_path):
         rfs.close()
         fs.close()
         c.__exit__(None, None, None)
+
+
+def test_first_cold_read_of_a_mount_resolves_natively(blob, tmp_path):
+    """No Python detour for the first cold read of a mount (WorkerUfsManager.java:56-65 resolves an
+    unknown mount from the master): an S3 mount the data server can reach is resolved on the
+    reader's pool thread and read natively; a mount it cannot reach (native reader off) is read
+    once through the worker's Python UFS by the same native stream, then its reads go to Python."""
+    srv, base = blob
+    rng = np.random.default_rng(12)
+    objs = {k: rng.integers(0, 256, 5 * MB + 7 * i, dtype=np.uint8) for i, k in enumerate("abcd")}
+    for k, d in objs.items():
+        _put(base, "ds/" + k, d)
+        _put(base, "py/" + k, d)
+    c, fs = _s3_cluster(tmp_path, base)
+    fs.mount("/py", "s3://bkt/py", properties={"alluxio.underfs.s3.endpoint": base,
+                                               "alluxio.underfs.s3.native.reader.enabled": "false"})
+    rfs = _remote_fs(c)
+    try:
+        w = c.workers[0]
+        st = w.data_server.stats
+        d0, s0 = st.declined, st.cold_streams
+        assert rfs.read_file("/s3/a") == objs["a"].tobytes()
+        assert st.declined == d0 and st.cold_streams - s0 == len(_blocks(rfs, "/s3/a"))
+        mid = rfs.get_status("/s3/a").mountId
+        assert w.data_server.ufs_roots.resolve_s3(mid, "s3://bkt/ds/a") == ("bkt", "ds/a")
+        # a Python-only mount: its first cold block is still a native stream, fed by ReadUfsRange
+        # (the file's later blocks already go to Python)
+        d0, s0 = st.declined, st.cold_streams
+        assert rfs.read_file("/py/a") == objs["a"].tobytes()
+        assert st.cold_streams - s0 >= 1 and st.declined - d0 < len(_blocks(rfs, "/py/a"))
+        d1 = st.declined
+        assert rfs.read_file("/py/b") == objs["b"].tobytes()        # now straight to Python
+        assert st.declined > d1
+    finally:
+        rfs.close()
+        fs.close()
+        c.__exit__(None, None, None)
