@@ -452,6 +452,7 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("write_streams", [](const DataServerStats& s) { return s.write_streams.load(); })
       .def_property_readonly("write_declined", [](const DataServerStats& s) { return s.write_declined.load(); })
       .def_property_readonly("write_bytes", [](const DataServerStats& s) { return s.write_bytes.load(); })
+      .def_property_readonly("write_evict_waits", [](const DataServerStats& s) { return s.write_evict_waits.load(); })
       .def_property_readonly("ufs_write_streams", [](const DataServerStats& s) { return s.ufs_write_streams.load(); })
       .def_property_readonly("ufs_write_bytes", [](const DataServerStats& s) { return s.ufs_write_bytes.load(); })
       .def_property_readonly("cold_streams", [](const DataServerStats& s) { return s.cold_streams.load(); })

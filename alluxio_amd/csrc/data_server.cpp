@@ -1243,20 +1243,41 @@ class WriteStreamBase : public NativeStream {
   std::string err_msg_;
 };
 
+// A block whose creation needs eviction: created on a pool thread (the I/O thread never waits for
+// space) while the stream queues what arrives, its receive window held back past kMaxBacklog.
+struct PendingCreate {
+  std::mutex mu;
+  bool done = false, cancelled = false;
+  int status = 0;
+  std::string msg;
+  int dir = -1;
+  std::function<void()> wake;
+};
+
 class BlockWriteStream : public WriteStreamBase {
  public:
+  static constexpr uint64_t kMaxBacklog = 8ull << 20;
+
   BlockWriteStream(StoreRef store, int64_t session, int64_t block_id, uint64_t pos, bool pin, bool device,
                    uint32_t commit_method, std::shared_ptr<StagingPool> pool, std::shared_ptr<DataServerStats> stats,
-                   std::shared_ptr<BlockCommitter> committer = nullptr)
+                   std::shared_ptr<BlockCommitter> committer = nullptr, std::shared_ptr<PendingCreate> pending = nullptr)
       : store_(std::move(store)), session_(session), block_(block_id), start_(pos), pos_(pos), pin_(pin),
         device_(device), commit_(commit_method), pool_(std::move(pool)), stats_(std::move(stats)),
-        committer_(std::move(committer)) {}
+        committer_(std::move(committer)), pc_(std::move(pending)) {}
 
   ~BlockWriteStream() override {
     drain();                                 // no DMA may still target the block's pages
     for (auto& sl : slot_) {
       if (sl.ev) (void)hipEventDestroy(sl.ev);
       if (sl.buf) pool_->put(sl.buf);
+    }
+    if (pc_) {
+      std::lock_guard<std::mutex> g(pc_->mu);
+      pc_->wake = nullptr;
+      if (!pc_->done) {                      // the create task drops the block it makes
+        pc_->cancelled = true;
+        return;
+      }
     }
     if (ticket_) {                           // the committer owns the session now
       std::lock_guard<std::mutex> g(ticket_->mu);
@@ -1269,9 +1290,31 @@ class BlockWriteStream : public WriteStreamBase {
     }
   }
 
-  void set_waker(std::function<void()> w) override { waker_ = std::move(w); }
+  void set_waker(std::function<void()> w) override {
+    waker_ = w;
+    if (pc_) {
+      bool done;
+      {
+        std::lock_guard<std::mutex> g(pc_->mu);
+        pc_->wake = w;
+        done = pc_->done;
+      }
+      if (done && w) w();
+    }
+  }
+
+  bool accepting() override { return !pc_ || backlog_bytes_ < kMaxBacklog; }
+
+  bool take_post(uint32_t* method, std::string* payload) override {
+    if (!post_ready_) return false;
+    post_ready_ = false;
+    *method = post_method_;
+    *payload = std::move(post_payload_);
+    return true;
+  }
 
   ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    if (pc_) settle_create();
     if (ticket_ && !done_ && !err_) {        // the native commit: answer once it is through
       bool fin;
       int st;
@@ -1303,6 +1346,15 @@ class BlockWriteStream : public WriteStreamBase {
       fail(3, "malformed WriteRequest");
       return;
     }
+    if (pc_) {                               // the block is still being created: queue in order
+      Queued q;
+      q.data.assign(reinterpret_cast<const char*>(chunk), len);
+      q.flush = has_cmd && cmd.flush;
+      backlog_bytes_ += len;
+      backlog_.push_back(std::move(q));
+      if (has_cmd && cmd.hold) hold_ = true;
+      return;
+    }
     try {
       if (len) write(chunk, len);
     } catch (const StoreError& e) {
@@ -1319,6 +1371,15 @@ class BlockWriteStream : public WriteStreamBase {
   bool on_end(uint32_t* method, std::string* payload) override {
     ended_ = true;
     if (err_) return false;
+    if (pc_) {                               // finished once the block exists (settle_create)
+      end_seen_ = true;
+      return false;
+    }
+    return finish(method, payload);
+  }
+
+  // The half-close's commit: native (committer) or the internal Python call {*method, *payload}.
+  bool finish(uint32_t* method, std::string* payload) {
     if (committer_ && committer_->has_caller()) {
       try {
         hand_to_committer();
@@ -1364,6 +1425,43 @@ class BlockWriteStream : public WriteStreamBase {
   }
 
  private:
+  // The pool thread's create finished: write what queued up, then carry on as a normal stream.
+  void settle_create() {
+    {
+      std::lock_guard<std::mutex> g(pc_->mu);
+      if (!pc_->done) return;
+      if (pc_->status) {
+        if (!err_) fail(pc_->status, "creating block " + std::to_string(block_) + ": " + pc_->msg);
+        pc_.reset();
+        backlog_.clear();
+        return;
+      }
+      device_ = store_->dir_spec(pc_->dir).kind == DirKind::kDevice;
+    }
+    pc_.reset();
+    while (!backlog_.empty() && !err_) {
+      Queued& q = backlog_.front();
+      try {
+        if (!q.data.empty()) write(reinterpret_cast<const uint8_t*>(q.data.data()), q.data.size());
+      } catch (const StoreError& e) {
+        fail(grpc_status_of(e), std::string("writing block ") + std::to_string(block_) + ": " + e.what());
+      } catch (const std::exception& e) {
+        fail(13, std::string("writing block ") + std::to_string(block_) + ": " + e.what());
+      }
+      if (q.flush && !err_) out_ += write_response_frame(pos_);
+      backlog_.pop_front();
+    }
+    backlog_.clear();
+    backlog_bytes_ = 0;
+    if (waker_) waker_();                    // the client's window opens again
+    if (end_seen_ && !err_) post_ready_ = finish(&post_method_, &post_payload_);
+  }
+
+  struct Queued {
+    std::string data;
+    bool flush = false;
+  };
+
   void write(const uint8_t* p, size_t n) {
     if (!device_) {       // host arena / file dir: straight from the HTTP/2 receive buffer
       store_->write(session_, block_, pos_, reinterpret_cast<uint64_t>(p), n, (int)MemKind::kHost, 0, true);
@@ -1465,6 +1563,12 @@ class BlockWriteStream : public WriteStreamBase {
   std::shared_ptr<CommitTicket> ticket_;
   std::function<void()> waker_;
   bool hold_ = false;
+  std::shared_ptr<PendingCreate> pc_;
+  std::deque<Queued> backlog_;
+  uint64_t backlog_bytes_ = 0;
+  bool end_seen_ = false, post_ready_ = false;
+  uint32_t post_method_ = 0;
+  std::string post_payload_;
 };
 
 int grpc_status_of_errno(int e) {
@@ -1570,6 +1674,10 @@ struct TeePieces {                 // n pieces borrowed from tee_pieces() for on
 // State of one local UFS file write shared by its stream (I/O thread) and its pool tasks: one task
 // at a time drains the chunk queue in order.
 struct LocalFileJob {
+  // Pool tasks writing one file at once: each takes the next queued item and pwrite()s it at its
+  // own file offset, so a CACHE_THROUGH tee's block appends (D2H + write) and a THROUGH stream's
+  // chunks use several cores instead of one sequential writer.
+  static constexpr int kParallel = 4;
   std::string path, tmp;
   int mode = 0644;
   int fd = -1;
@@ -1578,9 +1686,11 @@ struct LocalFileJob {
     std::string data;                 // received bytes, or
     int64_t block = -1;               // a block this worker holds (CACHE_THROUGH tee)
     uint64_t len = 0;
+    uint64_t off = 0;                 // file offset
   };
   std::deque<Item> chunks;
-  uint64_t queued = 0, written = 0;   // bytes
+  uint64_t queued = 0, written = 0;   // bytes; `written` is the contiguous prefix on disk
+  std::map<uint64_t, uint64_t> done_ranges;   // completed [off, end) past `written`
   StoreRef store;                     // source of appended blocks
   int64_t session = 0;
 
@@ -1591,8 +1701,9 @@ struct LocalFileJob {
         if (store) store->release_hold(it.block);
       }
   }
-  bool running = false, opened = false, failed = false, cancelled = false;
-  bool end = false, finished = false, cleaned = false;
+  int active = 0, inflight = 0;       // pool tasks running / items being written
+  bool opening = false, opened = false, failed = false, cancelled = false;
+  bool end = false, finishing = false, finished = false, cleaned = false;
   int err_status = 0;
   std::string err;
   std::function<void()> wake;
@@ -1612,6 +1723,23 @@ struct LocalFileJob {
     failed = true;
     err_status = grpc_status_of_errno(e);
     err = what + ": " + std::strerror(e);
+  }
+
+  // [off, off + n) is on disk: advance the contiguous prefix.
+  void complete_locked(uint64_t off, uint64_t n) {
+    if (n == 0) return;
+    done_ranges[off] = off + n;
+    for (auto it = done_ranges.begin(); it != done_ranges.end() && it->first == written;
+         it = done_ranges.erase(it))
+      written = it->second;
+  }
+
+  // Tasks to add for what is queued (called with mu held); the caller submits that many drains.
+  int want_tasks_locked() const {
+    if (failed || cancelled) return active == 0 ? 1 : 0;     // one to clean up
+    int work = (int)chunks.size() + ((!opened && !opening) ? 1 : 0) + ((end && !finishing && !finished) ? 1 : 0);
+    if (!opened) work = std::min(work, 1);                    // one opens, the rest follow
+    return std::max(0, std::min(kParallel - active, work - (active - inflight)));
   }
 
   // Creates the parents and the temp file beside the target.
@@ -1646,11 +1774,24 @@ struct LocalFileJob {
     if (!tmp.empty()) ::unlink(tmp.c_str());
   }
 
-  // One pool task: open (first time), write queued chunks in order, and on the end chmod + rename.
-  // Appends block `id` ([0, n) of it) from the store: read-locked, copied out in 8 MiB pieces
-  // through two pinned buffers on this pool thread's own stream, so the DMA of piece k+1 runs
-  // while piece k is written to the file (and never waits behind the store's internal stream).
-  int append_block(int64_t id, uint64_t n, std::string* what) {
+  static int pwrite_all(int fd, const uint8_t* p, uint64_t n, uint64_t off) {
+    uint64_t done = 0;
+    while (done < n) {
+      const ssize_t w = ::pwrite(fd, p + done, (size_t)(n - done), (off_t)(off + done));
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        return errno;
+      }
+      done += (uint64_t)w;
+    }
+    return 0;
+  }
+
+  // Appends block `id` ([0, n) of it) from the store at file offset `at`: read-locked, copied out
+  // in 8 MiB pieces through two pinned buffers on this pool thread's own stream, so the DMA of
+  // piece k+1 runs while piece k is written to the file (and never waits behind the store's
+  // internal stream).
+  int append_block(int64_t id, uint64_t n, uint64_t at, std::string* what) {
     if (!store) {
       *what = "no block store for an appended block";
       return EINVAL;
@@ -1697,18 +1838,8 @@ struct LocalFileJob {
         if (i + 1 < pieces) issue(i + 1);            // its buffer's previous piece is written
         if (dev && hipEventSynchronize(ev[i & 1]) != hipSuccess) throw std::runtime_error("D2H of an appended piece failed");
         const uint64_t k = std::min(kPiece, n - i * kPiece);
-        const uint8_t* b = pieces_buf->b[i & 1];
-        size_t done = 0;
-        while (done < k) {
-          const ssize_t w = ::write(fd, b + done, (size_t)(k - done));
-          if (w < 0) {
-            if (errno == EINTR) continue;
-            e = errno;
-            *what = "writing " + path;
-            break;
-          }
-          done += (size_t)w;
-        }
+        e = pwrite_all(fd, pieces_buf->b[i & 1], k, at + i * kPiece);
+        if (e) *what = "writing " + path;
       }
       if (dev && hipStreamSynchronize(st) != hipSuccess)   // nothing in flight into the pieces on return
         throw std::runtime_error("D2H of an appended piece failed");
@@ -1726,36 +1857,63 @@ struct LocalFileJob {
     return e;
   }
 
+  // Starts the pool tasks the queue wants (never holds mu across the submit).
+  static void kick(const std::shared_ptr<LocalFileJob>& j) {
+    int n;
+    {
+      std::lock_guard<std::mutex> g(j->mu);
+      n = j->want_tasks_locked();
+      j->active += n;
+    }
+    for (int i = 0; i < n; ++i) FilePool::get().submit([j] { LocalFileJob::drain(j); });
+  }
+
+  // One pool task: open (once), write queued items at their offsets, and -- the last one, when the
+  // stream ended and every item is on disk -- chmod + rename.  A failed / cancelled file is
+  // cleaned up by the last task to leave.
   static void drain(std::shared_ptr<LocalFileJob> j) {
     for (;;) {
       Item it;
-      bool have = false;
-      bool do_open, do_end, stop;
+      bool have = false, do_open = false, do_end = false;
       {
         std::lock_guard<std::mutex> g(j->mu);
-        stop = j->failed || j->cancelled;
-        do_open = !stop && !j->opened;
-        do_end = !stop && j->chunks.empty() && j->end && !j->finished;
-        if (!stop && !do_open && !j->chunks.empty()) {
+        if (j->failed || j->cancelled) {
+          if (--j->active == 0) j->cleanup();
+          break;
+        }
+        if (!j->opened) {
+          if (j->opening) {               // another task opens; it starts the others after
+            --j->active;
+            break;
+          }
+          j->opening = do_open = true;
+        } else if (!j->chunks.empty()) {
           it = std::move(j->chunks.front());
           j->chunks.pop_front();
+          ++j->inflight;
           have = true;
-        }
-        if (stop || (!do_open && !do_end && !have)) {
-          if (stop) j->cleanup();
-          j->running = false;
+        } else if (j->end && j->inflight == 0 && !j->finishing && !j->finished) {
+          j->finishing = do_end = true;
+        } else {
+          --j->active;
           break;
         }
       }
       if (do_open) {
         j->open_file();
+        {
+          std::lock_guard<std::mutex> g(j->mu);
+          j->opening = false;
+        }
+        kick(j);                          // the other tasks the queue wants
         continue;
       }
       if (have && it.block >= 0) {
         std::string what;
-        const int e = j->append_block(it.block, it.len, &what);
+        const int e = j->append_block(it.block, it.len, it.off, &what);
         j->stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
         std::lock_guard<std::mutex> g(j->mu);
+        --j->inflight;
         if (e) {
           if (!j->failed) {
             j->failed = true;
@@ -1763,27 +1921,21 @@ struct LocalFileJob {
             j->err = what + ": " + std::strerror(e);
           }
         } else {
-          j->written += it.len;
+          j->complete_locked(it.off, it.len);
+          j->stats->ufs_write_bytes.fetch_add(it.len, std::memory_order_relaxed);
+          j->stats->ufs_tee_bytes.fetch_add(it.len, std::memory_order_relaxed);
         }
-        if (!e) j->stats->ufs_write_bytes.fetch_add(it.len, std::memory_order_relaxed);
-        if (!e) j->stats->ufs_tee_bytes.fetch_add(it.len, std::memory_order_relaxed);
       } else if (have) {
         const std::string& c = it.data;
-        size_t done = 0;
-        int e = 0;
-        while (done < c.size()) {
-          const ssize_t w = ::write(j->fd, c.data() + done, c.size() - done);
-          if (w < 0) {
-            if (errno == EINTR) continue;
-            e = errno;
-            break;
-          }
-          done += (size_t)w;
-        }
+        const int e = pwrite_all(j->fd, reinterpret_cast<const uint8_t*>(c.data()), c.size(), it.off);
         std::lock_guard<std::mutex> g(j->mu);
-        if (e) j->fail_locked(e, "writing " + j->path);
-        else j->written += c.size();
-        j->stats->ufs_write_bytes.fetch_add(done, std::memory_order_relaxed);
+        --j->inflight;
+        if (e) {
+          j->fail_locked(e, "writing " + j->path);
+        } else {
+          j->complete_locked(it.off, c.size());
+          j->stats->ufs_write_bytes.fetch_add(c.size(), std::memory_order_relaxed);
+        }
       } else if (do_end) {
         int e = 0;
         if (::fchmod(j->fd, (mode_t)j->mode) != 0) e = errno;
@@ -1826,18 +1978,12 @@ class UfsFileWriteStream : public WriteStreamBase {
   }
 
   ~UfsFileWriteStream() override {
-    bool idle;
     {
       std::lock_guard<std::mutex> g(j_->mu);
       j_->wake = nullptr;
       if (!j_->finished) j_->cancelled = true;
-      idle = !j_->running;
-      if (idle && j_->cancelled) j_->running = true;
     }
-    if (idle && j_->cancelled) {
-      auto j = j_;
-      FilePool::get().submit([j] { LocalFileJob::drain(j); });   // closes + unlinks the temp file
-    }
+    LocalFileJob::kick(j_);          // with no task running, one closes + unlinks the temp file
   }
 
   void set_waker(std::function<void()> w) override {
@@ -1868,6 +2014,7 @@ class UfsFileWriteStream : public WriteStreamBase {
         LocalFileJob::Item it;
         it.block = append_id;
         it.len = append_len;
+        it.off = j_->queued;
         j_->chunks.push_back(std::move(it));
         j_->queued += append_len;
         j_->stats->store_tasks.fetch_add(1, std::memory_order_relaxed);
@@ -1880,6 +2027,7 @@ class UfsFileWriteStream : public WriteStreamBase {
         std::lock_guard<std::mutex> g(j_->mu);
         LocalFileJob::Item it;
         it.data.assign(reinterpret_cast<const char*>(chunk), len);
+        it.off = j_->queued;
         j_->chunks.push_back(std::move(it));
         j_->queued += len;
       }
@@ -1907,15 +2055,7 @@ class UfsFileWriteStream : public WriteStreamBase {
   }
 
  private:
-  void kick() {
-    {
-      std::lock_guard<std::mutex> g(j_->mu);
-      if (j_->running) return;
-      j_->running = true;
-    }
-    auto j = j_;
-    FilePool::get().submit([j] { LocalFileJob::drain(j); });
-  }
+  void kick() { LocalFileJob::kick(j_); }
 
   // Flush acks for written data, the failure, or the final frame once the file is in place.
   void emit() {
@@ -3139,17 +3279,62 @@ void serve_block_writes(FrameRpcServer& srv, uint32_t method, uint32_t commit_me
       // evict = false: the I/O thread never waits for space (eviction can block on locks and run
       // demotion copies); a write that needs eviction goes to the Python servicer, which may wait
       int dir;
+      const int tier = cmd.medium.empty() ? (cmd.has_tier ? (int)cmd.tier : 0) : -1;
       try {
-        dir = store->create_block(session, cmd.id, cmd.medium.empty() ? (cmd.has_tier ? (int)cmd.tier : 0) : -1,
-                                  cmd.medium, reserve, false, cmd.pin);
+        dir = store->create_block(session, cmd.id, tier, cmd.medium, reserve, false, cmd.pin);
       } catch (const StoreError& e) {
         if (e.code != kErrOutOfSpace) throw;
-        try {
-          store->cleanup_session(session);
-        } catch (...) {
+        // no space without evicting: the eviction runs on a pool thread while this stream queues
+        // what arrives (the I/O thread never waits for space, and nothing goes to Python)
+        auto pc = std::make_shared<PendingCreate>();
+        const WriteCmd c = cmd;
+        auto ok = ColdPool::get().submit([store, session, c, tier, reserve, pc] {
+          int d = -1, st = 0;
+          std::string m;
+          try {
+            d = store->create_block(session, c.id, tier, c.medium, reserve, true, c.pin);
+          } catch (const StoreError& e) {
+            st = grpc_status_of(e);
+            m = e.what();
+          } catch (const std::exception& e) {
+            st = 13;
+            m = e.what();
+          }
+          std::function<void()> w;
+          bool cancelled;
+          {
+            std::lock_guard<std::mutex> g(pc->mu);
+            pc->done = true;
+            pc->status = st;
+            pc->msg = m;
+            pc->dir = d;
+            cancelled = pc->cancelled;
+            w = pc->wake;
+          }
+          if (cancelled) {
+            try {
+              store->cleanup_session(session);
+            } catch (...) {
+            }
+          } else if (w) {
+            w();
+          }
+        }, 64);
+        if (!ok) {
+          try {
+            store->cleanup_session(session);
+          } catch (...) {
+          }
+          stats->write_declined.fetch_add(1, std::memory_order_relaxed);
+          return nullptr;
         }
-        stats->write_declined.fetch_add(1, std::memory_order_relaxed);
-        return nullptr;
+        if (committer && !committer->has_caller()) committer->set_caller(s->internal_caller(cid, user));
+        auto ws = std::unique_ptr<BlockWriteStream>(new BlockWriteStream(
+            store, session, cmd.id, (uint64_t)cmd.offset, cmd.pin, false, commit_method, pool, stats, committer, pc));
+        stats->write_streams.fetch_add(1, std::memory_order_relaxed);
+        stats->write_evict_waits.fetch_add(1, std::memory_order_relaxed);
+        if (len) ws->on_message(first.data(), first.size());
+        return ws;
       }
       const bool device = store->dir_spec(dir).kind == DirKind::kDevice;
       if (committer && !committer->has_caller()) committer->set_caller(s->internal_caller(cid, user));

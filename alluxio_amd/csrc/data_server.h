@@ -46,6 +46,7 @@ struct DataServerStats {
   std::atomic<uint64_t> write_streams{0};  // WriteBlock calls served natively
   std::atomic<uint64_t> write_declined{0}; // WriteBlock calls handed to Python (UFS / fallback)
   std::atomic<uint64_t> write_bytes{0};    // block bytes written natively
+  std::atomic<uint64_t> write_evict_waits{0};  // WriteBlock creates that evicted on a pool thread
   std::atomic<uint64_t> ufs_write_streams{0};  // UFS_FILE writes into a local UFS served natively
   std::atomic<uint64_t> ufs_write_bytes{0};
   std::atomic<uint64_t> cold_streams{0};     // UFS read-through / uncached UFS reads served natively

@@ -230,3 +230,26 @@ def test_tee_block_is_held_from_eviction_until_appended(tmp_path):
             assert time.time() < deadline
             time.sleep(0.02)
         rfs.close()
+
+
+def test_writes_into_a_full_tier_evict_off_the_io_thread(tmp_path):
+    """A WriteBlock whose block needs eviction is created on a pool thread while the stream queues
+    what arrives (receive window held back past 8 MiB): no call goes to the Python servicer, the
+    older blocks are evicted, and the new file is cached byte-exact."""
+    with _cluster(tmp_path, {"alluxio.worker.tieredstore.level0.dirs.quota": "24MB",
+                             "alluxio.worker.tieredstore.free.ahead.bytes": "0"}) as c:
+        fs = c.client()
+        rfs = _remote_fs(c)
+        st = c.workers[0].data_server.stats
+        rng = np.random.default_rng(9)
+        files = [rng.integers(0, 256, 7 * MB + i, dtype=np.uint8) for i in range(6)]   # 42 MB > 24 MB
+        d0, e0 = st.write_declined, st.write_evict_waits
+        for i, d in enumerate(files):
+            rfs.write_file(f"/full/f{i}", d, write_type="MUST_CACHE")
+        assert st.write_declined == d0
+        assert st.write_evict_waits > e0
+        last = rfs.get_status("/full/f5")
+        assert last.in_alluxio_percentage == 100
+        assert rfs.read_file("/full/f5") == files[5].tobytes()
+        rfs.close()
+        fs.close()

@@ -300,6 +300,11 @@ for s in $STEPS; do
       # native StressWorkerBench client: T C++ reader threads in ONE client process, 4 KiB read(buf)
       run wb_native_4k 900 python tools/worker_bench_host.py --mode native-threads --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --d2h-roof --out "$OUT/r6_worker_bench_native_threads.jsonl"
       ;;
+    r6wprof)
+      # where the bench process's Python CPU goes during sustained 16-thread writes
+      run ww8_prof_mc 600 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --py-sample --out "$OUT/r6_worker_write_pyprof.jsonl"
+      run ww8_prof_ct 600 python tools/worker_write_bench.py --threads 1,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --py-sample --out "$OUT/r6_worker_write_pyprof.jsonl"
+      ;;
     r6tests)
       run pytest_gpu_r6 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       ;;

@@ -99,6 +99,8 @@ def main(argv=None) -> int:
                     help="each writer keeps writing files (deleting its oldest) for at least this long")
     ap.add_argument("--s3", action="store_true", help="/ww is an S3 mount (a native BlobServer on tmpfs, "
                     "64 MiB parts): THROUGH / CACHE_THROUGH go to object storage")
+    ap.add_argument("--py-sample", action="store_true",
+                    help="sample the bench process's Python stacks (attribution of its interpreter CPU)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     cpus = []
@@ -153,8 +155,10 @@ def main(argv=None) -> int:
                      "alluxio.user.block.size.bytes.default": a.block_size}
             props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-            from _threadcpu import busy, thread_cpu
+            from _threadcpu import StackSampler, busy, python_thread_cpu, thread_cpu
             tc0, tw0 = thread_cpu(), time.perf_counter()
+            pc0 = python_thread_cpu()
+            sampler = StackSampler().start() if a.py_sample else None
             ds = getattr(c.workers[0], "data_server", None)
             tee0 = ds.stats.ufs_tee_bytes if ds is not None else 0
             cenv = dict(os.environ)
@@ -171,6 +175,8 @@ def main(argv=None) -> int:
                 return 1
             r = json.loads(line[7:])
             worker_threads = busy(tc0, thread_cpu(), r["seconds"])   # over the client's timed window
+            py_threads = busy(pc0, python_thread_cpu(), r["seconds"])
+            samples = sampler.stop() if sampler is not None else None
             row = {"bench": f"host writers, separate client process ({a.write_type})", "transport": transport, "tier": tier,
                    "min_seconds": a.min_seconds,
                    "threads": int(t), "files_per_thread": a.files, "file_size": a.file_size,
@@ -180,9 +186,15 @@ def main(argv=None) -> int:
                    # worker process CPU by thread group during the run (approx: whole subprocess
                    # lifetime / timed window), and the client's own CPU over its timed window
                    "worker_thread_cores": worker_threads, "client_cpu_cores": r.get("client_cpu_cores"),
+                   "python_thread_cores": py_threads,
                    "bound_to_gpu_node": bool(cpus), "work_dir": work, "ufs": "s3" if a.s3 else "local",
                    # bytes the worker copied from its block store into UFS files (CACHE_THROUGH tee)
                    "ufs_tee_bytes": (ds.stats.ufs_tee_bytes - tee0) if ds is not None else None}
+            if samples is not None:
+                row["python_stack_samples"] = samples
+            if ds is not None:
+                row["native_commits"] = ds.stats.commits
+                row["native_commit_batches"] = ds.stats.commit_batches
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:
