@@ -603,9 +603,12 @@ class FileInStream(io.RawIOBase):
             if self.ctx.is_local(l.workerAddress):
                 self.ctx._note_domain_socket(l.workerAddress)
             try:
+                # CACHE_PROMOTE: the worker moves the block to its top tier first (reference
+                # BlockInStream: ReadRequest.promote = the read type's isPromote())
                 r = GrpcBlockReader(self.ctx, addr, bi.blockId, block_len,
                                     data_address=(l.workerAddress.host,
-                                                  l.workerAddress.dataPort or l.workerAddress.rpcPort))
+                                                  l.workerAddress.dataPort or l.workerAddress.rpcPort),
+                                    promote=self.read_type == "CACHE_PROMOTE")
                 self._maybe_passive_cache(bi.blockId, l.workerAddress, block_len)
                 return r
             except Exception as e:  # noqa: BLE001

@@ -462,6 +462,7 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("cold_active", [](const DataServerStats& s) { return s.cold_active.load(); })
       .def_property_readonly("store_tasks", [](const DataServerStats& s) { return s.store_tasks.load(); })
       .def_property_readonly("prefetched", [](const DataServerStats& s) { return s.prefetched.load(); })
+      .def_property_readonly("promoted", [](const DataServerStats& s) { return s.promoted.load(); })
       .def_property_readonly("zero_copy_frames", [](const DataServerStats& s) { return s.zero_copy_frames.load(); })
       .def_property_readonly("ufs_tee_bytes", [](const DataServerStats& s) { return s.ufs_tee_bytes.load(); })
       .def_property_readonly("commits", [](const DataServerStats& s) { return s.commits.load(); })

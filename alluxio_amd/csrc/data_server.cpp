@@ -3155,6 +3155,125 @@ void BlockCommitter::run(std::shared_ptr<State> st) {
   }
 }
 
+namespace {
+
+// The stream of a block the store holds: locked (no wait) for the call's lifetime; nullptr with
+// *status == 0 when it is not (yet) committed here, with *status != 0 on a bad request.
+std::unique_ptr<BlockReadStream> open_block_stream(const ReadRequestMsg& r, const StoreRef& store, uint64_t max_chunk,
+                                                   uint64_t window, bool unix_peer,
+                                                   const std::shared_ptr<StagingPool>& pool,
+                                                   const std::shared_ptr<DataServerStats>& stats, int* status,
+                                                   std::string* msg) {
+  const int64_t session = g_session.fetch_add(1);
+  int64_t lock = -1;
+  try {
+    lock = store->lock_block(session, r.block_id, false, 0);
+  } catch (const StoreError& e) {
+    lock = -1;   // not (yet) committed here
+  }
+  if (lock < 0) return nullptr;
+  try {
+    const BlockInfoOut info = store->block_info(r.block_id);
+    const uint64_t off = (uint64_t)r.offset;
+    if (off > info.length) {
+      store->unlock(lock);
+      *status = 11;  // OUT_OF_RANGE
+      *msg = "offset " + std::to_string(off) + " beyond block " + std::to_string(r.block_id) + " of " +
+             std::to_string(info.length) + " bytes";
+      return nullptr;
+    }
+    const uint64_t end = r.length > 0 ? std::min<uint64_t>(info.length, off + (uint64_t)r.length) : info.length;
+    const uint64_t chunk = r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk)
+                                            : std::min<uint64_t>(1u << 20, max_chunk);
+    const bool device = store->dir_spec(info.dir).kind == DirKind::kDevice;
+    store->access_block(session, r.block_id);
+    stats->streams.fetch_add(1, std::memory_order_relaxed);
+    return std::unique_ptr<BlockReadStream>(new BlockReadStream(store, session, lock, r.block_id, off, end, chunk,
+                                                                window, device, unix_peer, pool, stats));
+  } catch (const std::exception& e) {
+    try {
+      store->unlock(lock);
+    } catch (...) {
+    }
+    *status = 13;
+    *msg = e.what();
+    return nullptr;
+  }
+}
+
+// ReadBlock with promote = true (CACHE_PROMOTE) of a block below the top tier: the block moves to
+// tier 0 first -- on a pool thread, with the batched copy kernel for device tiers -- and is then
+// streamed from there; a failed move (no room, locked by a reader) streams it where it is
+// (reference BlockReadHandler.openBlock:159-175 moves, logs a failure and reads).
+class PromoteReadStream : public NativeStream {
+ public:
+  struct Move {
+    std::mutex mu;
+    bool done = false;
+    std::function<void()> wake;
+  };
+  PromoteReadStream(ReadRequestMsg r, StoreRef store, uint64_t max_chunk, uint64_t window, bool unix_peer,
+                    std::shared_ptr<StagingPool> pool, std::shared_ptr<DataServerStats> stats, std::shared_ptr<Move> mv)
+      : r_(std::move(r)), store_(std::move(store)), max_chunk_(max_chunk), window_(window), unix_(unix_peer),
+        pool_(std::move(pool)), stats_(std::move(stats)), mv_(std::move(mv)) {}
+  ~PromoteReadStream() override {
+    std::lock_guard<std::mutex> g(mv_->mu);
+    mv_->wake = nullptr;
+  }
+  void set_waker(std::function<void()> w) override {
+    waker_ = w;
+    bool done;
+    {
+      std::lock_guard<std::mutex> g(mv_->mu);
+      mv_->wake = w;
+      done = mv_->done;
+    }
+    if (done && w) w();
+  }
+  void on_message(const char* p, size_t n) override {
+    if (inner_) inner_->on_message(p, n);
+  }
+  ssize_t produce(uint8_t* dst, size_t max, bool* eof, int* status, std::string* msg) override {
+    if (!ready(status, msg)) return *status ? -1 : 0;
+    return inner_->produce(dst, max, eof, status, msg);
+  }
+  ssize_t produce_spans(size_t max, ByteSpan* spans, int max_spans, int* nspans, bool* eof, int* status,
+                        std::string* msg) override {
+    if (!inner_) return -2;
+    return inner_->produce_spans(max, spans, max_spans, nspans, eof, status, msg);
+  }
+
+ private:
+  bool ready(int* status, std::string* msg) {
+    if (inner_) return true;
+    {
+      std::lock_guard<std::mutex> g(mv_->mu);
+      if (!mv_->done) return false;
+    }
+    int st = 0;
+    std::string m;
+    inner_ = open_block_stream(r_, store_, max_chunk_, window_, unix_, pool_, stats_, &st, &m);
+    if (!inner_) {
+      *status = st ? st : 5;
+      *msg = st ? m : "block " + std::to_string(r_.block_id) + " does not exist on this worker";
+      return false;
+    }
+    if (waker_) inner_->set_waker(waker_);
+    return true;
+  }
+  ReadRequestMsg r_;
+  StoreRef store_;
+  uint64_t max_chunk_, window_;
+  bool unix_;
+  std::shared_ptr<StagingPool> pool_;
+  std::shared_ptr<DataServerStats> stats_;
+  std::shared_ptr<Move> mv_;
+  std::unique_ptr<BlockReadStream> inner_;
+  std::function<void()> waker_;
+};
+
+}  // namespace
+
 void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uint64_t max_chunk, uint64_t window,
                        std::shared_ptr<DataServerStats> stats, std::shared_ptr<UfsMounts> mounts, ColdReadConfig cold,
                        std::shared_ptr<BlockCommitter> committer) {
@@ -3178,55 +3297,55 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uin
                          : "channel " + cid + " is not authenticated";
       return nullptr;
     }
-    // promotion and locks that would wait: the Python servicer
-    if (r.promote || r.offset < 0) {
+    if (r.offset < 0) {
       stats->declined.fetch_add(1, std::memory_order_relaxed);
       return nullptr;
     }
-    const int64_t session = g_session.fetch_add(1);
-    int64_t lock = -1;
-    try {
-      lock = store->lock_block(session, r.block_id, false, 0);
-    } catch (const StoreError& e) {
-      lock = -1;   // not (yet) committed here
-    }
-    if (lock < 0) {
-      if (r.has_ufs) {     // a cold block: read it through from the UFS (BlockReadHandler.openUfsBlock)
-        if (committer && !committer->has_caller()) committer->set_caller(s->internal_caller(cid, user));
-        auto cs = make_cold_stream(r, store, max_chunk, window, unix_peer, cold, mounts, slot_pool, stats,
-                                   s->internal_poster(cid, user), status, msg, committer,
-                                   cold.resolve_method != UINT32_MAX ? s->internal_caller(cid, user) : nullptr);
-        if (cs || *status != 0) return cs;
-      }
-      stats->declined.fetch_add(1, std::memory_order_relaxed);
-      return nullptr;
-    }
-    try {
-      const BlockInfoOut info = store->block_info(r.block_id);
-      const uint64_t off = (uint64_t)r.offset;
-      if (off > info.length) {
-        store->unlock(lock);
-        *status = 11;  // OUT_OF_RANGE
-        *msg = "offset " + std::to_string(off) + " beyond block " + std::to_string(r.block_id) + " of " +
-               std::to_string(info.length) + " bytes";
-        return nullptr;
-      }
-      const uint64_t end = r.length > 0 ? std::min<uint64_t>(info.length, off + (uint64_t)r.length) : info.length;
-      const uint64_t chunk = r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk) : std::min<uint64_t>(1u << 20, max_chunk);
-      const bool device = store->dir_spec(info.dir).kind == DirKind::kDevice;
-      store->access_block(session, r.block_id);
-      stats->streams.fetch_add(1, std::memory_order_relaxed);
-      return std::unique_ptr<NativeStream>(new BlockReadStream(store, session, lock, r.block_id, off, end, chunk,
-                                                               window, device, unix_peer, pool, stats));
-    } catch (const std::exception& e) {
+    if (r.promote) {
+      bool below_top = false;
       try {
-        store->unlock(lock);
+        below_top = store->has_block(r.block_id) && store->block_info(r.block_id).tier > 0;
       } catch (...) {
       }
-      *status = 13;
-      *msg = e.what();
-      return nullptr;
+      if (below_top) {
+        auto mv = std::make_shared<PromoteReadStream::Move>();
+        const int64_t session = g_session.fetch_add(1), id = r.block_id;
+        auto st = store;
+        auto sts = stats;
+        if (ColdPool::get().submit([st, sts, session, id, mv] {
+              try {
+                st->move_block(session, id, 0, "", true);
+                sts->promoted.fetch_add(1, std::memory_order_relaxed);
+              } catch (...) {              // no room / locked / gone: read it where it is
+              }
+              try {
+                st->cleanup_session(session);
+              } catch (...) {
+              }
+              std::function<void()> w;
+              {
+                std::lock_guard<std::mutex> g(mv->mu);
+                mv->done = true;
+                w = mv->wake;
+              }
+              if (w) w();
+            }, 64))
+          return std::unique_ptr<NativeStream>(
+              new PromoteReadStream(r, store, max_chunk, window, unix_peer, pool, stats, mv));
+      }
     }
+    auto bs = open_block_stream(r, store, max_chunk, window, unix_peer, pool, stats, status, msg);
+    if (bs) return bs;
+    if (*status != 0) return nullptr;
+    if (r.has_ufs) {     // a cold block: read it through from the UFS (BlockReadHandler.openUfsBlock)
+      if (committer && !committer->has_caller()) committer->set_caller(s->internal_caller(cid, user));
+      auto cs = make_cold_stream(r, store, max_chunk, window, unix_peer, cold, mounts, slot_pool, stats,
+                                 s->internal_poster(cid, user), status, msg, committer,
+                                 cold.resolve_method != UINT32_MAX ? s->internal_caller(cid, user) : nullptr);
+      if (cs || *status != 0) return cs;
+    }
+    stats->declined.fetch_add(1, std::memory_order_relaxed);
+    return nullptr;
   });
 }
 

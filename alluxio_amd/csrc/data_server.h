@@ -58,6 +58,7 @@ struct DataServerStats {
   std::atomic<uint64_t> ufs_tee_bytes{0};     // CACHE_THROUGH bytes the UFS stream copied from the store
   std::atomic<uint64_t> zero_copy_frames{0}; // HTTP/2 DATA frames sent straight from staging (no copy)
   std::atomic<uint64_t> prefetched{0};       // HBM chunks whose D2H was issued ahead of the send
+  std::atomic<uint64_t> promoted{0};         // CACHE_PROMOTE reads whose block moved to tier 0 natively
   std::atomic<uint64_t> commits{0};          // blocks committed by the native committer
   std::atomic<uint64_t> commit_batches{0};   // master reports (one internal call each) they took
   std::atomic<uint64_t> commit_failures{0};  // blocks whose commit failed (removed / aborted)

@@ -34,6 +34,21 @@ LOG = logging.getLogger(__name__)
 _fail_lock = threading.Lock()
 _failed_until: dict[tuple[int, str], float] = {}   # (worker id, peer address) -> monotonic deadline
 
+# Wall time of the steps of the mapped pulls of this process (seconds, and pulls): the replica
+# fan-out breakdown bench.py's replicate phase reports (profiles/r6_replica_fanout.md).
+_times_lock = threading.Lock()
+PULL_TIMES: dict[str, float] = {}
+
+
+def _add_time(step: str, dt: float) -> None:
+    with _times_lock:
+        PULL_TIMES[step] = PULL_TIMES.get(step, 0.0) + dt
+
+
+def pull_times() -> dict[str, float]:
+    with _times_lock:
+        return dict(PULL_TIMES)
+
 
 def _cooldown_s(worker) -> float:
     return worker.conf.get_ms("alluxio.worker.peer.failure.cooldown", "30sec") / 1000.0
@@ -82,38 +97,57 @@ def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "
     from .transfer import cross_page_segments
     if worker.conf.get_bool("alluxio.test.peer.mapped.pull.fail", "false"):
         raise RuntimeError("mapped pull failure injected (alluxio.test.peer.mapped.pull.fail)")
+    clock = time.perf_counter
+    t0 = clock()
     stub = worker.peer_stub(addr)
     session = ids.create_session_id()
     timeout = _rpc_timeout_s(worker)
     h = stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session,
                                                              reader_gpu=_my_gpu(worker)), timeout=timeout)
+    t1 = clock()
+    _add_time("open_rpc", t1 - t0)
     try:
         n = h.length
         dev = int(worker.store.device)
         src_base = map_handle(h, dev)
+        t2 = clock()
+        _add_time("map", t2 - t1)
         worker.create_block(session, block_id, tier, medium, max(n, 1))
         try:
             dst_pages = worker.native.external_write(session, block_id, 0, n)
             _p, _d, dps, dbase = worker.native.block_pages(block_id)
             segs = cross_page_segments(src_base, list(h.pages), h.page_size, dbase, list(dst_pages), dps, 0, n)
+            t3 = clock()
+            _add_time("create_and_plan", t3 - t2)
             if has_gpu():
                 import torch
                 with torch.cuda.device(dev):   # the copy kernel runs on THIS worker's GPU, reading the peer
                     lib().batched_copy(segs, 0, True)
             else:
                 lib().batched_copy(segs, 0, True)
+            t4 = clock()
+            _add_time("copy", t4 - t3)
+            crc = None
             if h.crc32c and worker.conf.get_bool("alluxio.worker.peer.verify.crc", "true"):
-                worker.verify_block_crc(block_id, list(h.crc32c), h.page_size)
-            worker.commit_block(session, block_id)
+                # the destination's CRCs, compared with the source's, are also the ones it keeps
+                crc = worker.verify_block_crc(block_id, list(h.crc32c), h.page_size)
+            t5 = clock()
+            _add_time("verify_crc", t5 - t4)
+            worker.commit_block(session, block_id, crc=crc)
+            _add_time("commit_and_report", clock() - t5)
         except Exception:
             worker.abort_block(session, block_id)
             raise
     finally:
+        t6 = clock()
         try:
             stub.UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(block_id=block_id, lock_id=h.lock_id,
                                                                      session_id=session), timeout=timeout)
         except Exception:  # noqa: BLE001 - the source expires the session's locks itself
             LOG.warning("unlock of block %d on %s failed", block_id, addr, exc_info=True)
+        _add_time("unlock_rpc", clock() - t6)
+        _add_time("pulls", 1.0)
+        _add_time("total", clock() - t0)
     cross_gpu = h.arena_kind != "dram" and has_gpu() and int(h.device) != dev
     worker.metrics.counter("XgmiBytesReceived" if cross_gpu else "PeerSharedBytesReceived").inc(n)
     return n

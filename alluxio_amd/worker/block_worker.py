@@ -226,16 +226,18 @@ class BlockWorker:
         self.write_ptr(session_id, block_id, offset, t.data_ptr(), t.numel() * t.element_size(), kind, stream, True)
         self.metrics.counter("BytesWrittenAlluxio").inc(t.numel() * t.element_size())
 
-    def commit_block(self, session_id: int, block_id: int, pin: bool = False, hold: bool = False) -> None:
+    def commit_block(self, session_id: int, block_id: int, pin: bool = False, hold: bool = False,
+                     crc=None) -> None:
         """Commit a temp block and report it to the master.  ``hold``: a CACHE_THROUGH tee block --
         keep it from eviction until the file's UFS stream has appended it (BlockStore::hold_block,
-        released by the AppendBlock copy)."""
+        released by the AppendBlock copy).  ``crc``: its (piece bytes, CRC32Cs) when the caller
+        already computed them (a verified peer pull), so they are not computed twice."""
         with native_errors():
             self.native.commit_block(session_id, block_id, pin)
             if hold:
                 self.native.hold_block(block_id)
         # the commit's added-event is reported by CommitBlock already
-        self._report_commit(block_id)
+        self._report_commit(block_id, crc)
 
     def verify_block_crc(self, block_id: int, src_crcs: list[int], src_piece: int) -> None:
         """Compare the block's bytes against CRC32Cs of ``src_piece``-byte pieces computed by its
@@ -261,6 +263,7 @@ class BlockWorker:
             self.metrics.counter("Crc32cMismatches").inc()
             raise DataLossException(f"block {block_id}: CRC32C mismatch after transfer")
         self.metrics.counter("Crc32cVerifiedBytes").inc(length)
+        return ps, list(mine)
 
     def abort_block(self, session_id: int, block_id: int) -> None:
         with native_errors():

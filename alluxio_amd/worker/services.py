@@ -94,16 +94,17 @@ class BlockWorkerService:
                     return
                 else:
                     raise BlockDoesNotExistException(f"Block {bid} does not exist on this worker")
+            if first.promote:
+                # before the read lock (a locked block does not move): BlockReadHandler.openBlock
+                try:
+                    self.w.move_block(session, bid, tier=0)
+                except Exception:  # noqa: BLE001
+                    pass
             lock_id = self.w.lock_block(session, bid)
             info = self.w.block_info(bid)
             length = first.length if first.length > 0 else info.length - first.offset
             end = min(info.length, first.offset + length)
             pos = first.offset
-            if first.promote:
-                try:
-                    self.w.move_block(session, bid, tier=0)
-                except Exception:  # noqa: BLE001
-                    pass
             self.w.access_block(session, bid)
             # BytesReadDomain vs BytesReadRemote (DefaultBlockWorker metrics by transport)
             peer = ctx.peer() if hasattr(ctx, "peer") else ""

@@ -473,6 +473,8 @@ def main(argv=None):
             wm = worker.worker.metrics
             names = ("XgmiBytesReceived", "PeerSharedBytesReceived", "PeerStreamBytesReceived", "PeerPullFailures")
             before = {k: wm.counter(k).count for k in names}
+            from alluxio_amd.parallel.peer import pull_times
+            pt0 = pull_times()
             src = torch.from_numpy(data).to(dev_t)
             sync()
             barrier()
@@ -490,6 +492,14 @@ def main(argv=None):
                 phase_errors["replicate"] = all_errors(err)
             delta = {k: int(SUM(float(wm.counter(k).count - before[k]))) for k in names}
             el_max = MAX(el)
+            # where a replica pull's time goes (ms per pull, summed over ranks / pulls)
+            pt1 = pull_times()
+            steps = ("open_rpc", "map", "create_and_plan", "copy", "verify_crc", "commit_and_report", "unlock_rpc",
+                     "total", "pulls")
+            tot = {k: SUM(float(pt1.get(k, 0.0) - pt0.get(k, 0.0))) for k in steps}
+            npulls = max(tot.pop("pulls"), 1.0)
+            pull_ms = {k: round(v / npulls * 1e3, 3) for k, v in tot.items()}
+            pull_ms["pulls"] = int(npulls)
             try:
                 rst = fs.get_status(f"/stress-worker-base/rep-{rank}")
                 good = all(len(f.blockInfo.locations) >= replicas for f in rst.fileBlockInfos)
@@ -514,7 +524,8 @@ def main(argv=None):
                                     "shared_bytes_received": delta["PeerSharedBytesReceived"],
                                     "stream_fallback_bytes_received": delta["PeerStreamBytesReceived"],
                                     "peer_pull_failures": delta["PeerPullFailures"],
-                                    "s": round(el_max, 4), "verified": good, "data_plane_ok": plane_ok}
+                                    "s": round(el_max, 4), "verified": good, "data_plane_ok": plane_ok,
+                                    "pull_ms": pull_ms}
             del src
 
     if "duration" in phases and a.duration > 0:

@@ -253,3 +253,42 @@ def test_writes_into_a_full_tier_evict_off_the_io_thread(tmp_path):
         assert rfs.read_file("/full/f5") == files[5].tobytes()
         rfs.close()
         fs.close()
+
+
+def test_cache_promote_read_moves_the_block_natively(tmp_path):
+    """ReadBlock with promote of a block in a lower tier (CACHE_PROMOTE): the data server moves it
+    to the top tier on a pool thread and streams it from there, without the Python servicer
+    (BlockReadHandler.openBlock:159-175)."""
+    import os
+    for n in ("ssd0",):
+        os.makedirs(tmp_path / n, exist_ok=True)
+    conf = {"alluxio.worker.tieredstore.levels": "2",
+            "alluxio.worker.tieredstore.level0.alias": "MEM",
+            "alluxio.worker.tieredstore.level0.dirs.path": "dram",
+            "alluxio.worker.tieredstore.level0.dirs.quota": "64MB",
+            "alluxio.worker.tieredstore.level1.alias": "SSD",
+            "alluxio.worker.tieredstore.level1.dirs.path": str(tmp_path / "ssd0"),
+            "alluxio.worker.tieredstore.level1.dirs.quota": "64MB",
+            "alluxio.worker.tieredstore.level1.dirs.mediumtype": "SSD",
+            "alluxio.worker.management.tier.promote.enabled": "false",
+            "alluxio.worker.management.tier.align.enabled": "false"}
+    with _cluster(tmp_path, conf) as c:
+        fs = c.client()
+        w = c.workers[0]
+        st = w.data_server.stats
+        data = np.random.default_rng(11).integers(0, 256, 6 * MB + 3, dtype=np.uint8)
+        wfs = _remote_fs(c)
+        with wfs.create_file("/pr/a", write_type="MUST_CACHE", write_tier=1) as f:
+            f.write(data)
+        blocks = _blocks(wfs, "/pr/a")
+        assert all(w.worker.native.block_info(b).tier == 1 for b, _ in blocks)
+        rfs = _remote_fs(c, **{"alluxio.user.file.readtype.default": "CACHE_PROMOTE"})
+        d0, p0 = st.declined, st.promoted
+        assert rfs.read_file("/pr/a") == data.tobytes()
+        assert st.declined == d0
+        assert st.promoted - p0 == len(blocks)
+        assert all(w.worker.native.block_info(b).tier == 0 for b, _ in blocks)
+        assert rfs.read_file("/pr/a") == data.tobytes()
+        wfs.close()
+        rfs.close()
+        fs.close()

@@ -305,6 +305,10 @@ for s in $STEPS; do
       run ww8_prof_mc 600 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --py-sample --out "$OUT/r6_worker_write_pyprof.jsonl"
       run ww8_prof_ct 600 python tools/worker_write_bench.py --threads 1,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --py-sample --out "$OUT/r6_worker_write_pyprof.jsonl"
       ;;
+    r6fanout)
+      # replica fan-out breakdown: 8 ranks (8 workers) on the one GPU, 3 replicas per block
+      run bench_rehearse_8rank_r6 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --profile-json "$OUT/r6_rehearse_8rank.json"
+      ;;
     r6tests)
       run pytest_gpu_r6 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       ;;
