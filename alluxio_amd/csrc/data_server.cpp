@@ -1004,7 +1004,90 @@ class ColdReadStream : public NativeStream {
     return (ssize_t)w;
   }
 
+  // Zero-copy sends (as the cached path's BlockReadStream): the chunk's prefix and its bytes in the
+  // pinned UFS slot go to the socket as they are.  A DATA frame never crosses a chunk boundary, and
+  // a slot whose last byte went out is handed back to the reader only at the next call, once the
+  // server has written the spans.
+  ssize_t produce_spans(size_t max, ByteSpan* spans, int max_spans, int* nspans, bool* eof, int* status,
+                        std::string* msg) override {
+    if (max_spans < 2) return -2;
+    if (release_pending_) {
+      release_pending_ = false;
+      release_slot();
+    }
+    size_t w = 0;
+    int ns = 0;
+    while (w < max && ns < max_spans) {
+      if (hdr_off_ < hdr_.size()) {
+        const size_t n = std::min(max - w, hdr_.size() - hdr_off_);
+        spans[ns++] = ByteSpan{reinterpret_cast<const uint8_t*>(hdr_.data()) + hdr_off_, n};
+        hdr_off_ += n;
+        w += n;
+        continue;
+      }
+      if (left_ > 0) {
+        const size_t n = (size_t)std::min<uint64_t>(max - w, left_);
+        spans[ns++] = ByteSpan{src_, n};
+        src_ += n;
+        left_ -= n;
+        w += n;
+        stats_->bytes.fetch_add(n, std::memory_order_relaxed);
+        if (unix_) stats_->domain_bytes.fetch_add(n, std::memory_order_relaxed);
+        if (left_ == 0 && pos_ >= slot_end_) release_pending_ = true;
+        continue;
+      }
+      if (w > 0) break;                          // this frame ends with the chunk
+      if (pos_ >= end_) {
+        *eof = true;
+        break;
+      }
+      if (pos_ - acked_ >= window_) break;
+      const int r = select_chunk(status, msg);
+      if (r < 0) return -1;
+      if (r == 0) break;
+    }
+    *nspans = ns;
+    if (w > 0) stats_->zero_copy_frames.fetch_add(1, std::memory_order_relaxed);
+    return (ssize_t)w;
+  }
+
  private:
+  // Makes the next chunk at pos_ current: 1 = done, 0 = its slot has not landed yet, -1 = the UFS
+  // read failed (*status / *msg set).
+  int select_chunk(int* status, std::string* msg) {
+    const size_t depth = st_->slots.size();
+    const size_t idx = (size_t)((pos_ - start_) / slot_bytes_);
+    ColdState::Slot* sl = &st_->slots[idx % depth];
+    bool ready, failed;
+    int fail_status;
+    std::string err;
+    {
+      std::lock_guard<std::mutex> g(st_->mu);
+      ready = sl->ready && sl->off <= pos_ && pos_ < sl->off + sl->len;
+      failed = st_->failed;
+      fail_status = st_->err_status;
+      err = st_->err;
+    }
+    if (!ready) {
+      if (failed) {
+        *status = fail_status;
+        *msg = "UFS read of block " + std::to_string(block_) + ": " + err;
+        return -1;
+      }
+      return 0;
+    }
+    const uint64_t n = std::min(chunk_, std::min(sl->off + sl->len, end_) - pos_);
+    hdr_ = h2::read_response_prefix(n);
+    hdr_off_ = 0;
+    left_ = n;
+    src_ = sl->buf + (pos_ - sl->off);
+    slot_end_ = sl->off + sl->len;
+    cur_slot_ = sl;
+    pos_ += n;
+    stats_->chunks.fetch_add(1, std::memory_order_relaxed);
+    return 1;
+  }
+
   void release_slot() {
     {
       std::lock_guard<std::mutex> g(st_->mu);
@@ -1013,6 +1096,7 @@ class ColdReadStream : public NativeStream {
     cur_slot_ = nullptr;
     st_->cv.notify_all();
   }
+  bool release_pending_ = false;
 
   StoreRef store_;
   int64_t session_, block_;

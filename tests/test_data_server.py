@@ -647,8 +647,10 @@ def test_native_cold_read_through(tmp_path):
             assert len(w.data_server.ufs_roots) == 1
             assert st.declined == d0 and st.cold_streams - s0 == len(_blocks(rfs, "/cold/a"))
             d0, s0, c0 = st.declined, st.cold_streams, st.cold_cached
+            z0 = st.zero_copy_frames
             free0 = w.worker.native.dir_available(0)
             assert rfs.read_file("/cold/b") == files["/cold/b"].tobytes()
+            assert st.zero_copy_frames > z0            # UFS slots went to the socket without a copy
             nb = len(_blocks(rfs, "/cold/b"))
             assert st.declined == d0                       # nothing went to Python
             assert st.cold_streams - s0 == nb
