@@ -447,3 +447,45 @@ def test_tier_moves_between_hbm_and_mapped_dram_are_byte_exact(gpu):
         del s
     finally:
         C.host_unregister(host.ctypes.data)
+
+
+def test_store_churn_across_a_thread_pool_keeps_hip_streams_flat(gpu):
+    """100 stores created, used for tier moves and destroyed across a pool of 4 threads: every
+    move runs on the thread's stream of the device (thread_stream_on), so the process creates at
+    most one stream per (thread, device) -- not one per store, as the per-store cache did
+    (move_stream leaked a stream per store and could reuse a stale one)."""
+    import concurrent.futures as cf
+
+    import torch
+    C = lib()
+    page = 64 * KB
+    dev = torch.empty(16 * page, dtype=torch.uint8, device="cuda")
+    host = np.zeros(32 * page, dtype=np.uint8)
+    assert C.host_register(host.ctypes.data, host.nbytes)
+    try:
+        src = torch.empty(2 * page, dtype=torch.uint8).pin_memory()
+        src.fill_(7)
+
+        def one(i):
+            specs = []
+            for tier, (base, cap, kind, medium) in enumerate([(dev.data_ptr(), dev.numel(), C.DirKind.DEVICE, "HBM"),
+                                                              (host.ctypes.data, host.nbytes, C.DirKind.HOST, "DRAM")]):
+                d = C.DirSpec()
+                d.tier, d.tier_alias, d.medium, d.kind = tier, ("MEM", "SSD")[tier], medium, kind
+                d.base, d.capacity, d.page_size, d.device = base, cap, page, 0
+                specs.append(d)
+            s = C.BlockStore(specs, annotator=0, alloc_policy=0, device=0)
+            s.create_block(5, 1, 0, "", 2 * page)
+            s.write(5, 1, 0, src.data_ptr(), 2 * page, 0)
+            s.commit_block(5, 1)
+            assert s.move_blocks(5, [1], 1) == [1]
+            assert s.move_block(5, 1, 0, "", True) >= 0
+            del s
+            return i
+
+        before = C.thread_streams_created()
+        with cf.ThreadPoolExecutor(4) as ex:
+            assert sorted(ex.map(one, range(100))) == list(range(100))
+        assert C.thread_streams_created() - before <= 4
+    finally:
+        C.host_unregister(host.ctypes.data)

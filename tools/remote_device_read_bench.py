@@ -112,6 +112,8 @@ def main(argv=None) -> int:
         uds_dir = tempfile.mkdtemp(prefix="uds", dir="/tmp")
         conf["alluxio.worker.data.server.domain.socket.address"] = uds_dir
         conf["alluxio.worker.data.server.domain.socket.as.uuid"] = "true"
+    else:            # loopback TCP (the worker's default same-node domain socket off)
+        conf["alluxio.worker.data.server.domain.socket.default.enabled"] = "false"
     conf.update(dict(kv.split("=", 1) for kv in a.worker_prop))
     with LocalAlluxioCluster(num_workers=1, conf=conf, work_dir=tempfile.mkdtemp(prefix="rdbench_")) as c:
         fs = c.client()
