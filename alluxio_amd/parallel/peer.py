@@ -140,11 +140,16 @@ def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "
             raise
     finally:
         t6 = clock()
-        try:
-            stub.UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(block_id=block_id, lock_id=h.lock_id,
-                                                                     session_id=session), timeout=timeout)
-        except Exception:  # noqa: BLE001 - the source expires the session's locks itself
-            LOG.warning("unlock of block %d on %s failed", block_id, addr, exc_info=True)
+        # the source's read lock goes off the critical path: nothing here waits for the unlock
+        # (a lost one expires with the session on the source)
+        req = pb.block.UnlockDeviceBlockRequest(block_id=block_id, lock_id=h.lock_id, session_id=session)
+
+        def unlock():
+            try:
+                stub.UnlockDeviceBlock(req, timeout=timeout)
+            except Exception:  # noqa: BLE001 - the source expires the session's locks itself
+                LOG.warning("unlock of block %d on %s failed", block_id, addr, exc_info=True)
+        _control_pool().submit(unlock)
         _add_time("unlock_rpc", clock() - t6)
         _add_time("pulls", 1.0)
         _add_time("total", clock() - t0)
@@ -177,6 +182,21 @@ def pull_block(worker, block_id: int, addr: str, length: int, tier: int = 0, med
     return length
 
 
+_pool_lock = threading.Lock()
+_pool = None
+
+
+def _control_pool():
+    """Threads for the fan-out's control calls (PeerTransfer to the replicas, deferred unlocks):
+    created once per process, not a thread per call."""
+    global _pool
+    with _pool_lock:
+        if _pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            _pool = ThreadPoolExecutor(16, thread_name_prefix="peer-control")
+        return _pool
+
+
 def fan_out(src_worker_addr: str, replica_addrs: list[str], block_id: int, length: int, stub_for,
             timeout_s: float = 60.0) -> list[tuple[str, str]]:
     """Ask every replica to pull ``block_id`` from ``src_worker_addr`` (``PeerTransfer``), all in
@@ -194,13 +214,11 @@ def fan_out(src_worker_addr: str, replica_addrs: list[str], block_id: int, lengt
             with lock:
                 errors.append((addr, str(e)))
 
-    threads = [threading.Thread(target=one, args=(a,), daemon=True) for a in replica_addrs[1:]]
-    for t in threads:
-        t.start()
+    futs = [_control_pool().submit(one, a) for a in replica_addrs[1:]]
     if replica_addrs:
         one(replica_addrs[0])
-    for t in threads:
-        t.join()
+    for f in futs:
+        f.result()
     return errors
 
 
