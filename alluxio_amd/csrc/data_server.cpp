@@ -1766,12 +1766,17 @@ struct LocalFileJob {
   int mode = 0644;
   int fd = -1;
   std::mutex mu;
+  // An appended block is split into pieces of kAppendPiece that the tasks copy in parallel (the
+  // last block of a file is not one serial D2H + write at the close).
+  static constexpr uint64_t kAppendPiece = 16ull << 20;
   struct Item {
     std::string data;                 // received bytes, or
-    int64_t block = -1;               // a block this worker holds (CACHE_THROUGH tee)
+    int64_t block = -1;               // [boff, boff + len) of a block this worker holds (CACHE_THROUGH tee)
+    uint64_t boff = 0;
     uint64_t len = 0;
     uint64_t off = 0;                 // file offset
   };
+  std::map<int64_t, int> pieces_left;   // appended block -> pieces not yet copied (its hold goes at 0)
   std::deque<Item> chunks;
   uint64_t queued = 0, written = 0;   // bytes; `written` is the contiguous prefix on disk
   std::map<uint64_t, uint64_t> done_ranges;   // completed [off, end) past `written`
@@ -1780,10 +1785,20 @@ struct LocalFileJob {
 
   ~LocalFileJob() {
     for (const Item& it : chunks)      // appends never run (failed / cancelled file)
-      if (it.block >= 0) {
-        if (stats) stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
-        if (store) store->release_hold(it.block);
-      }
+      if (it.block >= 0 && stats) stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
+    if (store)
+      for (const auto& kv : pieces_left)
+        if (kv.second > 0) store->release_hold(kv.first);
+  }
+
+  // A piece of block `id` is done (copied or failed): the block's append hold goes with its last.
+  void piece_done_locked(int64_t id) {
+    auto it = pieces_left.find(id);
+    if (it == pieces_left.end()) return;
+    if (--it->second <= 0) {
+      pieces_left.erase(it);
+      if (store) store->release_hold(id);
+    }
   }
   int active = 0, inflight = 0;       // pool tasks running / items being written
   bool opening = false, opened = false, failed = false, cancelled = false;
@@ -1875,7 +1890,7 @@ struct LocalFileJob {
   // in 8 MiB pieces through two pinned buffers on this pool thread's own stream, so the DMA of
   // piece k+1 runs while piece k is written to the file (and never waits behind the store's
   // internal stream).
-  int append_block(int64_t id, uint64_t n, uint64_t at, std::string* what) {
+  int append_block(int64_t id, uint64_t boff, uint64_t n, uint64_t at, std::string* what) {
     if (!store) {
       *what = "no block store for an appended block";
       return EINVAL;
@@ -1891,7 +1906,6 @@ struct LocalFileJob {
       *what = "appending block " + std::to_string(id) + ": lock timed out";
       return ETIMEDOUT;
     }
-    store->release_hold(id);            // our own lock keeps it now (the commit's append hold goes)
     constexpr uint64_t kPiece = kTeePiece;
     const bool dev = store->has_device();
     std::unique_ptr<TeePieces> pieces_buf;      // declared before the stream sync that frees them
@@ -1913,7 +1927,7 @@ struct LocalFileJob {
       auto issue = [&](uint64_t i) {
         const uint64_t off = i * kPiece, k = std::min(kPiece, n - off);
         uint8_t* b = pieces_buf->b[i & 1];
-        std::vector<ReadReq> rq{ReadReq{id, off, k, reinterpret_cast<uint64_t>(b), (int)MemKind::kHost}};
+        std::vector<ReadReq> rq{ReadReq{id, boff + off, k, reinterpret_cast<uint64_t>(b), (int)MemKind::kHost}};
         store->read_batch(rq, reinterpret_cast<uint64_t>(st), !dev);
         if (dev && hipEventRecord(ev[i & 1], st) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
       };
@@ -1994,10 +2008,11 @@ struct LocalFileJob {
       }
       if (have && it.block >= 0) {
         std::string what;
-        const int e = j->append_block(it.block, it.len, it.off, &what);
+        const int e = j->append_block(it.block, it.boff, it.len, it.off, &what);
         j->stats->store_tasks.fetch_sub(1, std::memory_order_relaxed);
         std::lock_guard<std::mutex> g(j->mu);
         --j->inflight;
+        j->piece_done_locked(it.block);
         if (e) {
           if (!j->failed) {
             j->failed = true;
@@ -2095,13 +2110,20 @@ class UfsFileWriteStream : public WriteStreamBase {
     if (append_id >= 0) {              // CACHE_THROUGH tee: the next bytes are a block we hold
       {
         std::lock_guard<std::mutex> g(j_->mu);
-        LocalFileJob::Item it;
-        it.block = append_id;
-        it.len = append_len;
-        it.off = j_->queued;
-        j_->chunks.push_back(std::move(it));
+        int pieces = 0;
+        for (uint64_t b = 0; b < append_len || (append_len == 0 && b == 0); b += LocalFileJob::kAppendPiece) {
+          LocalFileJob::Item it;
+          it.block = append_id;
+          it.boff = b;
+          it.len = std::min<uint64_t>(LocalFileJob::kAppendPiece, append_len - b);
+          it.off = j_->queued + b;
+          j_->chunks.push_back(std::move(it));
+          j_->stats->store_tasks.fetch_add(1, std::memory_order_relaxed);
+          ++pieces;
+          if (append_len == 0) break;
+        }
+        j_->pieces_left[append_id] += pieces;
         j_->queued += append_len;
-        j_->stats->store_tasks.fetch_add(1, std::memory_order_relaxed);
       }
       kick();
       pos_ += append_len;

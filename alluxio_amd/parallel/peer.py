@@ -90,8 +90,10 @@ def _my_gpu(worker) -> int:
     return (int(worker.store.device) + 1) if has_gpu() else 0
 
 
-def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "") -> int:
-    """Pull ``block_id`` from same-node worker ``addr`` by mapping its arena; returns bytes."""
+def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "", handle=None) -> int:
+    """Pull ``block_id`` from same-node worker ``addr`` by mapping its arena; returns bytes.
+    ``handle``: the source's DeviceBlockHandle, opened (read-locked) once by the writer for all
+    replicas (fan_out) -- then this pull neither opens nor unlocks it."""
     from ..ops.native import has_gpu, lib
     from .ipc import map_handle
     from .transfer import cross_page_segments
@@ -99,11 +101,15 @@ def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "
         raise RuntimeError("mapped pull failure injected (alluxio.test.peer.mapped.pull.fail)")
     clock = time.perf_counter
     t0 = clock()
-    stub = worker.peer_stub(addr)
     session = ids.create_session_id()
     timeout = _rpc_timeout_s(worker)
-    h = stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session,
-                                                             reader_gpu=_my_gpu(worker)), timeout=timeout)
+    stub = None
+    if handle is not None:
+        h = handle
+    else:
+        stub = worker.peer_stub(addr)
+        h = stub.OpenDeviceBlock(pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session,
+                                                                 reader_gpu=_my_gpu(worker)), timeout=timeout)
     t1 = clock()
     _add_time("open_rpc", t1 - t0)
     try:
@@ -140,16 +146,17 @@ def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "
             raise
     finally:
         t6 = clock()
-        # the source's read lock goes off the critical path: nothing here waits for the unlock
-        # (a lost one expires with the session on the source)
-        req = pb.block.UnlockDeviceBlockRequest(block_id=block_id, lock_id=h.lock_id, session_id=session)
+        if stub is not None:
+            # the source's read lock goes off the critical path: nothing here waits for the unlock
+            # (a lost one expires with the session on the source)
+            req = pb.block.UnlockDeviceBlockRequest(block_id=block_id, lock_id=h.lock_id, session_id=session)
 
-        def unlock():
-            try:
-                stub.UnlockDeviceBlock(req, timeout=timeout)
-            except Exception:  # noqa: BLE001 - the source expires the session's locks itself
-                LOG.warning("unlock of block %d on %s failed", block_id, addr, exc_info=True)
-        _control_pool().submit(unlock)
+            def unlock():
+                try:
+                    stub.UnlockDeviceBlock(req, timeout=timeout)
+                except Exception:  # noqa: BLE001 - the source expires the session's locks itself
+                    LOG.warning("unlock of block %d on %s failed", block_id, addr, exc_info=True)
+            _control_pool().submit(unlock)
         _add_time("unlock_rpc", clock() - t6)
         _add_time("pulls", 1.0)
         _add_time("total", clock() - t0)
@@ -159,7 +166,7 @@ def mapped_pull(worker, block_id: int, addr: str, tier: int = 0, medium: str = "
 
 
 def pull_block(worker, block_id: int, addr: str, length: int, tier: int = 0, medium: str = "",
-               same_node: bool = True) -> int:
+               same_node: bool = True, handle=None) -> int:
     """Copy ``block_id`` from worker ``addr`` into ``worker``; returns the bytes moved (0 when it
     already holds the block).  Same-node peers: mapped pull, falling back to the gRPC block
     stream (and marking the peer) when that fails; other nodes: the gRPC block stream."""
@@ -169,7 +176,7 @@ def pull_block(worker, block_id: int, addr: str, length: int, tier: int = 0, med
                  and not peer_failed(worker, addr))
     if mapped_ok:
         try:
-            return mapped_pull(worker, block_id, addr, tier, medium)
+            return mapped_pull(worker, block_id, addr, tier, medium, handle)
         except Exception as e:  # noqa: BLE001
             if worker.has_block(block_id):
                 return 0   # a concurrent pull won the race
@@ -198,27 +205,51 @@ def _control_pool():
 
 
 def fan_out(src_worker_addr: str, replica_addrs: list[str], block_id: int, length: int, stub_for,
-            timeout_s: float = 60.0) -> list[tuple[str, str]]:
+            timeout_s: float = 60.0, share_handle: bool = True) -> list[tuple[str, str]]:
     """Ask every replica to pull ``block_id`` from ``src_worker_addr`` (``PeerTransfer``), all in
-    flight at once; returns ``[(replica, error)]`` for the ones that failed."""
+    flight at once; returns ``[(replica, error)]`` for the ones that failed.
+
+    The block is opened on the source ONCE for all replicas (``OpenDeviceBlock``: read lock + page
+    list + arena handle) and the handle rides in each PeerTransfer, so a replica's pull costs no
+    control call to the source; the lock goes when the last replica is done (one unlock per
+    block instead of an open and an unlock per replica)."""
     errors: list[tuple[str, str]] = []
     lock = threading.Lock()
+    handle, session = None, 0
+    if share_handle and replica_addrs:
+        session = ids.create_session_id()
+        try:
+            handle = stub_for(src_worker_addr).OpenDeviceBlock(
+                pb.block.OpenDeviceBlockRequest(block_id=block_id, session_id=session), timeout=timeout_s)
+        except Exception:  # noqa: BLE001 - not shareable (file tier, ...): each replica opens itself
+            LOG.debug("shared open of block %d on %s failed", block_id, src_worker_addr, exc_info=True)
+            handle = None
 
     def one(addr: str) -> None:
         try:
-            r = stub_for(addr).PeerTransfer(pb.block.PeerTransferRequest(
-                block_id=block_id, length=length, src_address=src_worker_addr), timeout=timeout_s)
+            req = pb.block.PeerTransferRequest(block_id=block_id, length=length, src_address=src_worker_addr)
+            if handle is not None:
+                req.handle.CopyFrom(handle)
+            r = stub_for(addr).PeerTransfer(req, timeout=timeout_s)
             if not r.ok:
                 raise RuntimeError(r.message)
         except Exception as e:  # noqa: BLE001
             with lock:
                 errors.append((addr, str(e)))
 
-    futs = [_control_pool().submit(one, a) for a in replica_addrs[1:]]
-    if replica_addrs:
-        one(replica_addrs[0])
-    for f in futs:
-        f.result()
+    try:
+        futs = [_control_pool().submit(one, a) for a in replica_addrs[1:]]
+        if replica_addrs:
+            one(replica_addrs[0])
+        for f in futs:
+            f.result()
+    finally:
+        if handle is not None:
+            try:
+                stub_for(src_worker_addr).UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(
+                    block_id=block_id, lock_id=handle.lock_id, session_id=session), timeout=timeout_s)
+            except Exception:  # noqa: BLE001 - the source expires the session's locks itself
+                LOG.warning("unlock of block %d on %s failed", block_id, src_worker_addr, exc_info=True)
     return errors
 
 

@@ -60,7 +60,7 @@ msg CommitDeviceWriteRequest block_id=1:i64 session_id=2:i64 length=3:i64 pin_on
     hold_for_append=6:bool
 msg CommitDeviceWriteResponse
 msg PeerTransferRequest block_id=1:i64 src_rank=2:i32 dst_rank=3:i32 offset=4:i64 length=5:i64
-    tag=6:i64 src_address=7:str
+    tag=6:i64 src_address=7:str handle=8:DeviceBlockHandle
 msg PeerTransferResponse ok=1:bool message=2:str
 msg SessionHeartbeatRequest session_ids=1:i64*
 msg SessionHeartbeatResponse unknown_session_ids=1:i64*

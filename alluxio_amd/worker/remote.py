@@ -78,7 +78,8 @@ def peer_transfer(worker, req) -> tuple[bool, str]:
         from ..parallel.peer import is_same_node, pull_block
         try:
             host = req.src_address.rsplit(":", 1)[0]
-            pull_block(worker, req.block_id, req.src_address, req.length, same_node=is_same_node(worker, host))
+            pull_block(worker, req.block_id, req.src_address, req.length, same_node=is_same_node(worker, host),
+                       handle=req.handle if req.HasField("handle") else None)
             return True, ""
         except Exception as e:  # noqa: BLE001
             LOG.exception("peer transfer of block %d from %s failed", req.block_id, req.src_address)
