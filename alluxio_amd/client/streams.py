@@ -1416,6 +1416,7 @@ class FileOutStream(io.RawIOBase):
         futs = getattr(self, "_fan_futs", None) or []
         self._fan_futs = []
         errors = []
+        t0 = time.perf_counter()
         for bid, f in futs:
             try:
                 e = f.result()
@@ -1423,6 +1424,10 @@ class FileOutStream(io.RawIOBase):
                 e = [("?", str(ex_))]
             if e:
                 errors.append((bid, e))
+        if futs:
+            # how long close() waited for replica pulls still running after the last block
+            from ..parallel.peer import _add_time
+            _add_time("fan_close_wait", time.perf_counter() - t0)
         ex = getattr(self, "_fan_exec", None)
         if ex is not None:
             ex.shutdown(wait=False)

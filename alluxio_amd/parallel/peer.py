@@ -216,6 +216,7 @@ def fan_out(src_worker_addr: str, replica_addrs: list[str], block_id: int, lengt
     errors: list[tuple[str, str]] = []
     lock = threading.Lock()
     handle, session = None, 0
+    t0 = time.perf_counter()
     if share_handle and replica_addrs:
         session = ids.create_session_id()
         try:
@@ -224,6 +225,8 @@ def fan_out(src_worker_addr: str, replica_addrs: list[str], block_id: int, lengt
         except Exception:  # noqa: BLE001 - not shareable (file tier, ...): each replica opens itself
             LOG.debug("shared open of block %d on %s failed", block_id, src_worker_addr, exc_info=True)
             handle = None
+    t1 = time.perf_counter()
+    _add_time("fan_open_rpc", t1 - t0)
 
     def one(addr: str) -> None:
         try:
@@ -244,12 +247,18 @@ def fan_out(src_worker_addr: str, replica_addrs: list[str], block_id: int, lengt
         for f in futs:
             f.result()
     finally:
+        t2 = time.perf_counter()
+        _add_time("fan_transfers", t2 - t1)
         if handle is not None:
             try:
                 stub_for(src_worker_addr).UnlockDeviceBlock(pb.block.UnlockDeviceBlockRequest(
                     block_id=block_id, lock_id=handle.lock_id, session_id=session), timeout=timeout_s)
             except Exception:  # noqa: BLE001 - the source expires the session's locks itself
                 LOG.warning("unlock of block %d on %s failed", block_id, src_worker_addr, exc_info=True)
+        t3 = time.perf_counter()
+        _add_time("fan_unlock_rpc", t3 - t2)
+        _add_time("fan_total", t3 - t0)
+        _add_time("fans", 1.0)
     return errors
 
 

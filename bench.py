@@ -477,21 +477,38 @@ def main(argv=None):
             pt0 = pull_times()
             src = torch.from_numpy(data).to(dev_t)
             sync()
-            barrier()
-            t = time.perf_counter()
             err = None
+
+            def rep_write(name: str, copies: int) -> float:
+                barrier()
+                t = time.perf_counter()
+                fs.write_file(name, src, write_type="MUST_CACHE", block_size=block_size, replication_min=copies)
+                sync()
+                el = time.perf_counter() - t
+                barrier()
+                return el
+
+            el_plain = 0.0
             try:
-                fs.write_file(f"/stress-worker-base/rep-{rank}", src, write_type="MUST_CACHE", block_size=block_size,
-                              replication_min=replicas)
+                if a.warmup > 0:
+                    # untimed: first peer-arena maps, control threads, channels
+                    rep_write(f"/stress-worker-base/rep-warm-{rank}", replicas)
+                    fs.delete(f"/stress-worker-base/rep-warm-{rank}")
+                    pt0 = pull_times()
+                    before = {k: wm.counter(k).count for k in names}
+                    # the same write with one copy: what replication adds on top of it
+                    el_plain = rep_write(f"/stress-worker-base/rep-plain-{rank}", 1)
+                    fs.delete(f"/stress-worker-base/rep-plain-{rank}")
+                el = rep_write(f"/stress-worker-base/rep-{rank}", replicas)
             except Exception as e:  # noqa: BLE001 - reported in the JSON; the headline stands
                 err = f"rank {rank}: {e!r}"
-            sync()
-            el = time.perf_counter() - t
-            barrier()
+                el = 0.0
+                barrier()
             if not agree(err is None):
                 phase_errors["replicate"] = all_errors(err)
             delta = {k: int(SUM(float(wm.counter(k).count - before[k]))) for k in names}
-            el_max = MAX(el)
+            el_max = max(MAX(el), 1e-9)
+            plain_max = MAX(el_plain)
             # where a replica pull's time goes (ms per pull, summed over ranks / pulls)
             pt1 = pull_times()
             steps = ("open_rpc", "map", "create_and_plan", "copy", "verify_crc", "commit_and_report", "unlock_rpc",
@@ -500,6 +517,14 @@ def main(argv=None):
             npulls = max(tot.pop("pulls"), 1.0)
             pull_ms = {k: round(v / npulls * 1e3, 3) for k, v in tot.items()}
             pull_ms["pulls"] = int(npulls)
+            # the writer's side of each block's fan-out (shared open, the replicas' PeerTransfer
+            # calls, the unlock) and close()'s wait for the last block's pulls, per file
+            fsteps = ("fan_open_rpc", "fan_transfers", "fan_unlock_rpc", "fan_total", "fans", "fan_close_wait")
+            ftot = {k: SUM(float(pt1.get(k, 0.0) - pt0.get(k, 0.0))) for k in fsteps}
+            nfans = max(ftot.pop("fans"), 1.0)
+            fan_ms = {k[4:]: round(v / nfans * 1e3, 3) for k, v in ftot.items() if k != "fan_close_wait"}
+            fan_ms["fans"] = int(nfans)
+            fan_ms["close_wait_per_file"] = round(ftot["fan_close_wait"] / world * 1e3, 3)
             try:
                 rst = fs.get_status(f"/stress-worker-base/rep-{rank}")
                 good = all(len(f.blockInfo.locations) >= replicas for f in rst.fileBlockInfos)
@@ -525,7 +550,9 @@ def main(argv=None):
                                     "stream_fallback_bytes_received": delta["PeerStreamBytesReceived"],
                                     "peer_pull_failures": delta["PeerPullFailures"],
                                     "s": round(el_max, 4), "verified": good, "data_plane_ok": plane_ok,
-                                    "pull_ms": pull_ms}
+                                    "plain_write_GBps": (round(SUM(float(file_size)) / plain_max / 1e9, 3)
+                                                         if plain_max > 0 else None),
+                                    "pull_ms": pull_ms, "fan_ms": fan_ms}
             del src
 
     if "duration" in phases and a.duration > 0:

@@ -68,7 +68,9 @@ def test_bench_fails_when_replicas_fall_back_to_grpc(tmp_path):
     rep = out["config"]["replication"]
     assert not rep["data_plane_ok"] and not out["config"]["verified"]
     assert out["config"]["headline_verified"]
-    assert rep["peer_pull_failures"] > 0 and rep["stream_fallback_bytes_received"] == 2 * (8 << 20)
+    # the failures themselves land in the untimed warmup write; the peer is then in its cooldown,
+    # so the timed write's replicas all come through the stream
+    assert rep["stream_fallback_bytes_received"] == 2 * (8 << 20)
 
 
 def test_bench_remote_failure_on_one_rank_keeps_the_headline(tmp_path):
