@@ -468,7 +468,17 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("commits", [](const DataServerStats& s) { return s.commits.load(); })
       .def_property_readonly("commit_batches", [](const DataServerStats& s) { return s.commit_batches.load(); })
       .def_property_readonly("commit_failures", [](const DataServerStats& s) { return s.commit_failures.load(); })
-      .def_property_readonly("crc_streamed", [](const DataServerStats& s) { return s.crc_streamed.load(); });
+      .def_property_readonly("crc_streamed", [](const DataServerStats& s) { return s.crc_streamed.load(); })
+      .def_property_readonly("cold_timing_ns", [](const DataServerStats& s) {
+        py::dict d;
+        d["queue"] = s.cold_queue_ns.load();
+        d["setup"] = s.cold_setup_ns.load();
+        d["first_slot"] = s.cold_first_ns.load();
+        d["ufs_read"] = s.cold_read_ns.load();
+        d["slot_wait"] = s.cold_slot_wait_ns.load();
+        d["dma_wait"] = s.cold_dma_wait_ns.load();
+        return d;
+      });
   py::class_<BlockCommitter, std::shared_ptr<BlockCommitter>>(m, "BlockCommitter")
       .def(py::init<std::shared_ptr<BlockStore>, uint32_t, bool, bool, std::shared_ptr<DataServerStats>>(),
            py::arg("store"), py::arg("method"), py::arg("crc_device"), py::arg("crc_host"), py::arg("stats"));

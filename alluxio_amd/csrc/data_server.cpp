@@ -772,6 +772,7 @@ struct ColdJob {
   // A mount the data server did not know at the call's start: resolves it (blocking internal call
   // to the worker) and opens the reader; false with *status / *err when it cannot be read natively.
   std::function<bool(std::unique_ptr<UfsReader>*, int*, std::string*)> resolve;
+  std::chrono::steady_clock::time_point queued_at = std::chrono::steady_clock::now();
 
   void wake() {
     std::function<void()> w;
@@ -785,12 +786,21 @@ struct ColdJob {
   // Runs on its own thread: UFS reads (and the H2D copies into the temp block) run ahead of the
   // sends by up to `depth` slots; a slot is reused once the stream has sent it and its H2D is done.
   void run() {
+    using clk = std::chrono::steady_clock;
+    auto ns_since = [](clk::time_point t) {
+      return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t).count();
+    };
+    const auto t_run = clk::now();
+    stats->cold_queue_ns.fetch_add(
+        (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_run - queued_at).count(),
+        std::memory_order_relaxed);
     bool caching = false;
     hipStream_t hs = nullptr;
     std::string err;
     bool ok = true;
     uint64_t ingested = start;
     int err_status = 13;
+    uint64_t read_ns = 0, slot_wait_ns = 0, dma_wait_ns = 0;
     if (!reader && resolve && !resolve(&reader, &err_status, &err)) reader.reset();
     if (!reader) {                    // unresolvable mount: fail the stream, drop the session
       if (err.empty()) err = "the UFS of this block cannot be read natively";
@@ -828,18 +838,23 @@ struct ColdJob {
         std::lock_guard<std::mutex> g(st->mu);
         st->caching = caching;
       }
+      stats->cold_setup_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
       const size_t depth = st->slots.size();
       size_t idx = 0;
       for (uint64_t off = start; off < end; off += slot_bytes, ++idx) {
         ColdState::Slot* sl;
         {
+          const auto tw = clk::now();
           std::unique_lock<std::mutex> lk(st->mu);
           sl = &st->slots[idx % depth];
           st->cv.wait(lk, [&] { return st->cancelled || !sl->ready; });
+          slot_wait_ns += ns_since(tw);
           if (st->cancelled) break;
         }
         if (sl->dma) {   // the H2D of the bytes this slot held `depth` reads ago
+          const auto td = clk::now();
           if (hipEventSynchronize(sl->ev) != hipSuccess) throw std::runtime_error("H2D into the block failed");
+          dma_wait_ns += ns_since(td);
           sl->dma = false;
         }
         if (!sl->buf) {
@@ -847,11 +862,13 @@ struct ColdJob {
           if (hs && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) sl->ev = nullptr;
         }
         const uint64_t n = std::min(slot_bytes, end - off);
+        const auto tr = clk::now();
         if (!reader->read(file_off + off, n, sl->buf, &err)) {
           ok = false;
           err_status = reader->status();
           break;
         }
+        read_ns += ns_since(tr);
         stats->cold_bytes.fetch_add(n, std::memory_order_relaxed);
         if (caching) {
           const bool async = hs && sl->ev;
@@ -868,6 +885,7 @@ struct ColdJob {
           sl->len = n;
           sl->ready = true;
         }
+        if (idx == 0) stats->cold_first_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
         ingested = off + n;
         wake();
       }
@@ -875,6 +893,9 @@ struct ColdJob {
       ok = false;
       err = e.what();
     }
+    stats->cold_read_ns.fetch_add(read_ns, std::memory_order_relaxed);
+    stats->cold_slot_wait_ns.fetch_add(slot_wait_ns, std::memory_order_relaxed);
+    stats->cold_dma_wait_ns.fetch_add(dma_wait_ns, std::memory_order_relaxed);
     if (hs) {
       if (hipStreamSynchronize(hs) != hipSuccess && ok) {   // every H2D is done before commit / abort
         ok = false;

@@ -63,6 +63,11 @@ struct DataServerStats {
   std::atomic<uint64_t> commit_batches{0};   // master reports (one internal call each) they took
   std::atomic<uint64_t> commit_failures{0};  // blocks whose commit failed (removed / aborted)
   std::atomic<uint64_t> crc_streamed{0};     // blocks whose CRCs were computed on the write stream
+  // where the cold readers' time goes (ns summed over reads): queued for a pool thread, setting up
+  // (mount resolve, temp block create), until the first slot could be sent, inside UFS reads,
+  // waiting for the stream to free a slot (consumer-bound), waiting for a slot's H2D
+  std::atomic<uint64_t> cold_queue_ns{0}, cold_setup_ns{0}, cold_first_ns{0}, cold_read_ns{0},
+      cold_slot_wait_ns{0}, cold_dma_wait_ns{0};
 };
 
 // One block handed to the committer: the temp block of a finished WriteBlock (or of a complete

@@ -310,6 +310,12 @@ for s in $STEPS; do
       run ww8ct_tcp 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_worker_write_ct.jsonl"
       run ww8ct_uds 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --out "$OUT/r6_worker_write_ct.jsonl"
       ;;
+    r6cttime)
+      # where one CACHE_THROUGH file's time goes at 1 and 16 writers (client phases + master/worker handlers)
+      run ww_ct_time1 300 python tools/worker_write_bench.py --threads 1 --files 4 --min-seconds 6 --file-size 256m --write-type CACHE_THROUGH --client-timing "$OUT/r6_ct_timing" --out "$OUT/r6_ct_timing.jsonl"
+      run ww_mc_time1 300 python tools/worker_write_bench.py --threads 1 --files 4 --min-seconds 6 --file-size 256m --write-type MUST_CACHE --client-timing "$OUT/r6_mc_timing" --out "$OUT/r6_ct_timing.jsonl"
+      run ww_th_time1 300 python tools/worker_write_bench.py --threads 1 --files 4 --min-seconds 6 --file-size 256m --write-type THROUGH --client-timing "$OUT/r6_th_timing" --out "$OUT/r6_ct_timing.jsonl"
+      ;;
     r6fanout)
       # replica fan-out breakdown: 8 ranks (8 workers) on the one GPU, 3 replicas per block
       run bench_rehearse_8rank_r6 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --profile-json "$OUT/r6_rehearse_8rank.json"

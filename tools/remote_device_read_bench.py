@@ -126,7 +126,7 @@ def main(argv=None) -> int:
                 c.heartbeat_workers()
             ds = c.workers[0].data_server
             st0 = (ds.stats.cold_streams, ds.stats.declined, ds.stats.cold_cached, ds.stats.zero_copy_frames,
-                   ds.stats.prefetched, ds.stats.domain_bytes) if ds is not None else None
+                   ds.stats.prefetched, ds.stats.domain_bytes, ds.stats.cold_timing_ns) if ds is not None else None
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "false",
                      "alluxio.user.native.reader.enabled": str(native).lower(),
@@ -160,6 +160,11 @@ def main(argv=None) -> int:
                 row["worker_zero_copy_frames"] = ds.stats.zero_copy_frames - st0[3]
                 row["worker_prefetched_chunks"] = ds.stats.prefetched - st0[4]
                 row["worker_domain_socket_bytes"] = ds.stats.domain_bytes - st0[5]
+                if a.cold:
+                    # the cold readers' time per block stream (ms)
+                    ct = ds.stats.cold_timing_ns
+                    nb = max(row["worker_native_cold_streams"], 1)
+                    row["worker_cold_ms_per_block"] = {k: round((v - st0[6][k]) / nb / 1e6, 3) for k, v in ct.items()}
             print(json.dumps(row), flush=True)
             if a.out:
                 with open(a.out, "a") as f:

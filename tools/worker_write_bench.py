@@ -42,6 +42,8 @@ with fs.create_file(f"/ww/{{tag}}-warm", write_type=wtype) as f:
     f.write(data)
 done = [0] * threads
 errs = []
+from alluxio_amd.utils import optiming
+clk = time.perf_counter
 def run(t):
     try:
         k = 0
@@ -49,16 +51,27 @@ def run(t):
         # file of a name is deleted first, so the cache never holds more) until min_s has passed
         while k < nfiles or time.perf_counter() - t0 < min_s:
             name = f"/ww/{{tag}}-{{t}}-{{k % nfiles}}"
+            c0 = clk()
             if k >= nfiles:
                 fs.delete(name)
             k += 1
-            with fs.create_file(name, write_type=wtype) as f:
-                left = size
-                while left > 0:
-                    n = min(wsize, left)
-                    f.write(data[:n])
-                    left -= n
-                    done[t] += n
+            c1 = clk()
+            f = fs.create_file(name, write_type=wtype)
+            c2 = clk()
+            left = size
+            while left > 0:
+                n = min(wsize, left)
+                f.write(data[:n])
+                left -= n
+                done[t] += n
+            c3 = clk()
+            f.close()
+            c4 = clk()
+            # where one file's time goes (with --client-timing)
+            optiming.add("bench.delete", c1 - c0)
+            optiming.add("bench.create", c2 - c1)
+            optiming.add("bench.writes", c3 - c2)
+            optiming.add("bench.close", c4 - c3)
     except Exception as e:
         errs.append(repr(e))
 ts = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
@@ -114,6 +127,9 @@ def main(argv=None) -> int:
                     cpus.extend(range(int(lo), int(hi or lo) + 1))
             cpus = sorted(set(cpus) & os.sched_getaffinity(0))
             os.sched_setaffinity(0, cpus)          # the in-process worker's threads inherit it
+    if a.client_timing:
+        # the master's and worker's handlers too (this process), dumped at exit
+        os.environ.setdefault("ALLUXIO_MASTER_OP_TIMING", f"{a.client_timing}.server")
     import torch
 
     from alluxio_amd.minicluster import LocalAlluxioCluster
