@@ -483,6 +483,12 @@ void bind_data_path(py::module_& m) {
       .def(py::init<std::shared_ptr<BlockStore>, uint32_t, bool, bool, std::shared_ptr<DataServerStats>>(),
            py::arg("store"), py::arg("method"), py::arg("crc_device"), py::arg("crc_host"), py::arg("stats"));
   m.def("thread_streams_created", &thread_streams_created);
+  m.def("unlink_deferred", [](const std::string& path, uint64_t defer_bytes, size_t max_pending) {
+        py::gil_scoped_release nogil;
+        return unlink_deferred(path, defer_bytes, max_pending);
+      }, py::arg("path"), py::arg("defer_bytes") = 8u << 20, py::arg("max_pending") = 256);
+  m.def("reclaimed_files", &reclaimed_files);
+  m.def("reclaim_pending", &reclaim_pending);
   // Native StressWorkerBench client (csrc/stress_bench.h): `blocks` = one dict per block of the
   // file: {"length", "kind": "grpc"|"ipc"|"host", grpc: "host", "port", "unix_path", "block_id",
   // "chunk", "channel_id", "user", "timeout_ms"; arenas: "base", "pages", "page_size", "device"}.

@@ -2828,6 +2828,83 @@ class S3UfsWriteStream : public WriteStreamBase {
 
 }  // namespace
 
+// ---- deferred reclaim of deleted UFS files ------------------------------------------------------
+namespace {
+
+class Reclaimer {
+ public:
+  static Reclaimer& get() {
+    static Reclaimer* r = new Reclaimer();   // immortal, like its thread
+    return *r;
+  }
+  // false: too many waiting (the caller closes inline)
+  bool push(int fd, size_t max_pending) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (q_.size() >= max_pending) return false;
+    if (!started_) {
+      try {
+        std::thread([this] { loop(); }).detach();
+      } catch (...) {
+        return false;
+      }
+      started_ = true;
+    }
+    q_.push_back(fd);
+    cv_.notify_one();
+    return true;
+  }
+  uint64_t done() const { return done_.load(std::memory_order_relaxed); }
+  size_t pending() {
+    std::lock_guard<std::mutex> g(mu_);
+    return q_.size() + (busy_ ? 1 : 0);
+  }
+
+ private:
+  void loop() {
+    pthread_setname_np(pthread_self(), "ufs-reclaim");
+    for (;;) {
+      int fd;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        busy_ = false;
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        fd = q_.front();
+        q_.pop_front();
+        busy_ = true;
+      }
+      ::close(fd);                 // the last reference: the inode and its pages go here
+      done_.fetch_add(1, std::memory_order_relaxed);
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<int> q_;
+  bool started_ = false, busy_ = false;
+  std::atomic<uint64_t> done_{0};
+};
+
+}  // namespace
+
+int unlink_deferred(const std::string& path, uint64_t defer_bytes, size_t max_pending) {
+  const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC | O_NOFOLLOW | O_NONBLOCK);
+  struct stat sb;
+  if (fd < 0 || ::fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode) || (uint64_t)sb.st_size < defer_bytes) {
+    if (fd >= 0) ::close(fd);
+    return ::unlink(path.c_str()) == 0 ? 0 : errno;
+  }
+  if (::unlink(path.c_str()) != 0) {
+    const int e = errno;
+    ::close(fd);
+    return e;
+  }
+  if (!Reclaimer::get().push(fd, max_pending)) ::close(fd);
+  return 0;
+}
+
+uint64_t reclaimed_files() { return Reclaimer::get().done(); }
+size_t reclaim_pending() { return Reclaimer::get().pending(); }
+
+
 namespace {
 std::string strip_file_scheme(const std::string& p) { return p.compare(0, 7, "file://") == 0 ? p.substr(7) : p; }
 }  // namespace

@@ -30,6 +30,20 @@ def strip_scheme(path: str) -> str:
 _IDS: dict = {}   # (uid, gid) -> (owner, group): NSS lookups once per id pair, not per file
 
 
+def _unlink(p: str) -> None:
+    """Remove file ``p``.  With the native module loaded, a large file's name goes now and its
+    pages are freed on a background thread (``unlink_deferred``): the caller -- a master Remove --
+    does not wait ~20 ms per 256 MiB for the kernel's teardown."""
+    from ..ops import native
+    mod = native._mod
+    if mod is not None and hasattr(mod, "unlink_deferred"):
+        e = mod.unlink_deferred(p)
+        if e:
+            raise OSError(e, os.strerror(e), p)
+        return
+    os.remove(p)
+
+
 def _owner(st) -> tuple[str, str]:
     key = (st.st_uid, st.st_gid)
     hit = _IDS.get(key)
@@ -114,7 +128,7 @@ class LocalUnderFileSystem(UnderFileSystem):
         p = self._p(path)
         if not os.path.isfile(p):
             return False
-        os.remove(p)
+        _unlink(p)
         return True
 
     def delete_directory(self, path, options: DeleteOptions | None = None) -> bool:

@@ -122,3 +122,39 @@ for atomic in (True, False):
 """ % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), str(tmp_path), str(tmp_path))
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert out.stdout.split("\n")[:2] == ["raised 27", "raised 27"], out.stdout + out.stderr
+
+
+def test_local_delete_large_file_reclaims_in_background(tmp_path):
+    """A large local file's delete returns once its name is gone; the kernel frees its pages when
+    the reclaim thread closes the last descriptor (``unlink_deferred``).  Small files, symlinks
+    and missing paths behave as ``os.remove`` does."""
+    import os
+    import time
+
+    from alluxio_amd.ops.native import lib
+    from alluxio_amd.underfs.local import LocalUnderFileSystem
+    m = lib()
+    ufs = LocalUnderFileSystem(str(tmp_path))
+    big = tmp_path / "big.bin"
+    big.write_bytes(b"\1" * (16 << 20))
+    small = tmp_path / "small.bin"
+    small.write_bytes(b"x" * 100)
+    before = m.reclaimed_files()
+    assert ufs.delete_file(str(big)) and not big.exists()
+    assert ufs.delete_file(str(small)) and not small.exists()
+    assert not ufs.delete_file(str(tmp_path / "missing"))
+    deadline = time.time() + 10
+    while m.reclaimed_files() < before + 1 and time.time() < deadline:
+        time.sleep(0.01)
+    assert m.reclaimed_files() == before + 1     # only the large one went through the thread
+    # a name re-created right after the delete is a new file
+    big.write_bytes(b"\2" * 10)
+    assert big.read_bytes() == b"\2" * 10
+    # a symlink is removed itself, never followed
+    target = tmp_path / "target.bin"
+    target.write_bytes(b"\3" * (16 << 20))
+    link = tmp_path / "link"
+    os.symlink(target, link)
+    assert m.unlink_deferred(str(link)) == 0
+    assert not os.path.lexists(link) and target.exists()
+    assert m.unlink_deferred(str(tmp_path / "missing")) == 2     # ENOENT

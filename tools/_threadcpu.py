@@ -47,6 +47,27 @@ def python_thread_cpu() -> dict:
     return out
 
 
+def python_user_sys() -> tuple:
+    """(user, system) CPU seconds summed over this process's live Python threads: user time is the
+    interpreter (and the C code it calls), system time the syscalls they make -- e.g. the unlink of
+    a deleted UFS file's pages, which is kernel work on a Python thread."""
+    import threading
+    tck = os.sysconf("SC_CLK_TCK")
+    u = k = 0.0
+    for th in threading.enumerate():
+        tid = getattr(th, "native_id", None)
+        if tid is None:
+            continue
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                fl = f.read().rsplit(")", 1)[1].split()
+        except OSError:
+            continue
+        u += int(fl[11]) / tck
+        k += int(fl[12]) / tck
+    return u, k
+
+
 class StackSampler:
     """Samples the innermost alluxio_amd frames of every Python thread that burned CPU since the
     previous sample (per-thread ticks from /proc), every ``interval`` s: a cheap attribution of

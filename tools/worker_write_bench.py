@@ -171,9 +171,10 @@ def main(argv=None) -> int:
                      "alluxio.user.block.size.bytes.default": a.block_size}
             props.update(dict(kv.split("=", 1) for kv in a.client_prop))
             sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-            from _threadcpu import StackSampler, busy, python_thread_cpu, thread_cpu
+            from _threadcpu import StackSampler, busy, python_thread_cpu, python_user_sys, thread_cpu
             tc0, tw0 = thread_cpu(), time.perf_counter()
             pc0 = python_thread_cpu()
+            pus0 = python_user_sys()
             sampler = StackSampler().start() if a.py_sample else None
             ds = getattr(c.workers[0], "data_server", None)
             tee0 = ds.stats.ufs_tee_bytes if ds is not None else 0
@@ -192,6 +193,7 @@ def main(argv=None) -> int:
             r = json.loads(line[7:])
             worker_threads = busy(tc0, thread_cpu(), r["seconds"])   # over the client's timed window
             py_threads = busy(pc0, python_thread_cpu(), r["seconds"])
+            pus1 = python_user_sys()
             samples = sampler.stop() if sampler is not None else None
             row = {"bench": f"host writers, separate client process ({a.write_type})", "transport": transport, "tier": tier,
                    "min_seconds": a.min_seconds,
@@ -203,6 +205,9 @@ def main(argv=None) -> int:
                    # lifetime / timed window), and the client's own CPU over its timed window
                    "worker_thread_cores": worker_threads, "client_cpu_cores": r.get("client_cpu_cores"),
                    "python_thread_cores": py_threads,
+                   # the same threads split into user (interpreter) and system (syscall) time
+                   "python_user_cores": round((pus1[0] - pus0[0]) / r["seconds"], 2),
+                   "python_sys_cores": round((pus1[1] - pus0[1]) / r["seconds"], 2),
                    "bound_to_gpu_node": bool(cpus), "work_dir": work, "ufs": "s3" if a.s3 else "local",
                    # bytes the worker copied from its block store into UFS files (CACHE_THROUGH tee)
                    "ufs_tee_bytes": (ds.stats.ufs_tee_bytes - tee0) if ds is not None else None}
