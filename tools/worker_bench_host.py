@@ -144,6 +144,9 @@ def main(argv=None) -> int:
                         "--block-size", a.block_size, "--duration", a.duration, "--warmup", a.warmup,
                         "--mode", a.mode]
                 t0 = time.time()
+                sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+                from _threadcpu import busy, thread_cpu
+                tc0 = thread_cpu()
                 s0 = (stats.streams, stats.bytes, stats.declined) if stats is not None else (0, 0, 0)
                 procs = [subprocess.Popen([sys.executable, "-c", CLIENT.format(root=ROOT, addr=c.master.address,
                                                                               args=args, props=props, cpus=cpus)],
@@ -160,6 +163,8 @@ def main(argv=None) -> int:
                         print(err[-3000:], file=sys.stderr)
                         return 1
                     results.append(json.loads(line[7:]))
+                # the worker's threads (this process) over the clients' lifetime, by name group
+                worker_cores = busy(tc0, thread_cpu(), time.time() - t0)
                 r = {"throughput_MBps": sum(x["throughput_MBps"] for x in results),
                      "bytes": sum(x["bytes"] for x in results), "duration_s": results[0]["duration_s"],
                      "errors": [e for x in results for e in x["errors"]]}
@@ -171,6 +176,7 @@ def main(argv=None) -> int:
                        "reader_buffer": a.reader_buffer, "client_props": a.client_prop,
                        "client_procs": nproc}
                 row["client_placement"] = [x.get("placement", "") for x in results]
+                row["worker_thread_cores"] = worker_cores
                 if results[0].get("native"):
                     row["native"] = [x.get("native") for x in results]
                 row["bound_to_gpu_node"] = bool(cpus)
