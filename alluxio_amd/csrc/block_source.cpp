@@ -8,6 +8,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
+#include <pthread.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -1113,27 +1114,51 @@ class PrefetchPool {
     static PrefetchPool* p = new PrefetchPool();   // never destroyed: threads outlive statics
     return *p;
   }
+  // A thread is added whenever a prefetch would otherwise queue behind busy ones, up to the cap:
+  // each stream has at most one prefetch in flight, so the pool grows to the number of streams
+  // reading at once (256 reader threads of one client process get 256 concurrent chunk reads,
+  // not 16), and idle threads serve the next ones.
   void submit(std::function<void()> fn) {
+    std::function<void()> here;
     {
       std::lock_guard<std::mutex> g(mu_);
-      if (threads_.empty()) {
-        int n = want_ > 0 ? want_ : (int)std::min(16u, std::max(2u, std::thread::hardware_concurrency()));
-        for (int i = 0; i < n; ++i) threads_.emplace_back([this] { run(); });
-        for (auto& t : threads_) t.detach();
-      }
       q_.push_back(std::move(fn));
+      const int cap = want_ > 0 ? want_ : kDefaultCap;
+      if ((int)q_.size() > idle_ && threads_ < cap) {
+        try {
+          std::thread([this] { run(); }).detach();
+          ++threads_;
+        } catch (...) {
+          // the queued prefetch runs on an existing thread; with none, the caller runs it
+          if (threads_ == 0) {
+            here = std::move(q_.back());
+            q_.pop_back();
+          }
+        }
+      }
+    }
+    if (here) {
+      here();
+      return;
     }
     cv_.notify_one();
   }
-  void set_threads(int n) { want_ = n; }
+  void set_threads(int n) {
+    std::lock_guard<std::mutex> g(mu_);
+    want_ = n;
+  }
 
  private:
+  static constexpr int kDefaultCap = 256;
   void run() {
+    pthread_setname_np(pthread_self(), "chunk-prefetch");
     for (;;) {
       std::function<void()> fn;
       {
         std::unique_lock<std::mutex> lk(mu_);
+        ++idle_;
         cv_.wait(lk, [&] { return !q_.empty(); });
+        --idle_;
         fn = std::move(q_.front());
         q_.pop_front();
       }
@@ -1143,7 +1168,7 @@ class PrefetchPool {
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
-  std::vector<std::thread> threads_;
+  int threads_ = 0, idle_ = 0;
   int want_ = 0;
 };
 

@@ -731,6 +731,13 @@ class PythonRangeReader : public UfsReader {
   std::string path_;
 };
 
+// The UFS reads of a cold stream: the first covers `first` bytes (one chunk, so the first bytes
+// go out after one small read instead of a whole slot), every later one a slot.  Read i lands
+// in slot i % depth; this is the read holding stream-relative offset `rel`.
+inline size_t cold_read_index(uint64_t rel, uint64_t first, uint64_t slot) {
+  return rel < first ? 0 : 1 + (size_t)((rel - first) / slot);
+}
+
 // State shared by a cold stream (I/O threads) and its background reader thread.
 struct ColdState {
   struct Slot {
@@ -762,6 +769,7 @@ struct ColdJob {
   StoreRef store;
   int64_t session, block;
   uint64_t start, end, block_len, file_off, slot_bytes;
+  uint64_t first_bytes = 0;     // the first read (<= slot_bytes; 0 = a whole slot)
   bool want_cache;
   std::unique_ptr<UfsReader> reader;
   std::shared_ptr<ColdState> st;
@@ -840,8 +848,10 @@ struct ColdJob {
       }
       stats->cold_setup_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
       const size_t depth = st->slots.size();
+      const uint64_t first = first_bytes ? std::min(first_bytes, slot_bytes) : slot_bytes;
       size_t idx = 0;
-      for (uint64_t off = start; off < end; off += slot_bytes, ++idx) {
+      for (uint64_t off = start, n = 0; off < end; off += n, ++idx) {
+        n = std::min(idx == 0 ? first : slot_bytes, end - off);
         ColdState::Slot* sl;
         {
           const auto tw = clk::now();
@@ -861,7 +871,6 @@ struct ColdJob {
           sl->buf = st->pool->get();
           if (hs && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) sl->ev = nullptr;
         }
-        const uint64_t n = std::min(slot_bytes, end - off);
         const auto tr = clk::now();
         if (!reader->read(file_off + off, n, sl->buf, &err)) {
           ok = false;
@@ -1017,10 +1026,11 @@ class ColdPool {
 class ColdReadStream : public NativeStream {
  public:
   ColdReadStream(StoreRef store, int64_t session, int64_t block_id, uint64_t pos, uint64_t end, uint64_t chunk,
-                 uint64_t window, uint64_t slot_bytes, bool unix_peer, std::shared_ptr<ColdState> st,
-                 std::shared_ptr<DataServerStats> stats)
+                 uint64_t window, uint64_t slot_bytes, uint64_t first_bytes, bool unix_peer,
+                 std::shared_ptr<ColdState> st, std::shared_ptr<DataServerStats> stats)
       : store_(store), session_(session), block_(block_id), start_(pos), pos_(pos), acked_(pos), end_(end),
-        chunk_(chunk), window_(window), slot_bytes_(slot_bytes), unix_(unix_peer), st_(std::move(st)),
+        chunk_(chunk), window_(window), slot_bytes_(slot_bytes),
+        first_(first_bytes ? std::min(first_bytes, slot_bytes) : slot_bytes), unix_(unix_peer), st_(std::move(st)),
         stats_(std::move(stats)) {}
 
   ~ColdReadStream() override {
@@ -1083,7 +1093,7 @@ class ColdReadStream : public NativeStream {
       if (pos_ - acked_ >= window_) break;       // wait for offset_received
       // the slot holding pos_
       const size_t depth = st_->slots.size();
-      const size_t idx = (size_t)((pos_ - start_) / slot_bytes_);
+      const size_t idx = cold_read_index(pos_ - start_, first_, slot_bytes_);
       ColdState::Slot* sl = &st_->slots[idx % depth];
       bool ready, failed;
       int fail_status;
@@ -1168,7 +1178,7 @@ class ColdReadStream : public NativeStream {
   // read failed (*status / *msg set).
   int select_chunk(int* status, std::string* msg) {
     const size_t depth = st_->slots.size();
-    const size_t idx = (size_t)((pos_ - start_) / slot_bytes_);
+    const size_t idx = cold_read_index(pos_ - start_, first_, slot_bytes_);
     ColdState::Slot* sl = &st_->slots[idx % depth];
     bool ready, failed;
     int fail_status;
@@ -1212,7 +1222,7 @@ class ColdReadStream : public NativeStream {
 
   StoreRef store_;
   int64_t session_, block_;
-  uint64_t start_, pos_, acked_, end_, chunk_, window_, slot_bytes_;
+  uint64_t start_, pos_, acked_, end_, chunk_, window_, slot_bytes_, first_;
   bool unix_;
   std::shared_ptr<ColdState> st_;
   std::shared_ptr<DataServerStats> stats_;
@@ -2837,26 +2847,33 @@ class Reclaimer {
     static Reclaimer* r = new Reclaimer();   // immortal, like its thread
     return *r;
   }
+  // Threads freeing files at once: 16 CACHE_THROUGH writers delete ~70 files of 256 MiB a second
+  // (~20 ms of teardown each), more than one thread keeps up with -- a backlog of deleted pages
+  // would push the writers into direct reclaim.
+  static constexpr int kMaxThreads = 4;
   // false: too many waiting (the caller closes inline)
   bool push(int fd, size_t max_pending) {
     std::lock_guard<std::mutex> g(mu_);
     if (q_.size() >= max_pending) return false;
-    if (!started_) {
+    q_.push_back(fd);
+    if ((int)q_.size() > idle_ && threads_ < kMaxThreads) {
       try {
         std::thread([this] { loop(); }).detach();
+        ++threads_;
       } catch (...) {
-        return false;
+        if (threads_ == 0) {
+          q_.pop_back();
+          return false;
+        }
       }
-      started_ = true;
     }
-    q_.push_back(fd);
     cv_.notify_one();
     return true;
   }
   uint64_t done() const { return done_.load(std::memory_order_relaxed); }
   size_t pending() {
     std::lock_guard<std::mutex> g(mu_);
-    return q_.size() + (busy_ ? 1 : 0);
+    return q_.size() + (size_t)busy_;
   }
 
  private:
@@ -2866,20 +2883,23 @@ class Reclaimer {
       int fd;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        busy_ = false;
+        ++idle_;
         cv_.wait(lk, [&] { return !q_.empty(); });
+        --idle_;
         fd = q_.front();
         q_.pop_front();
-        busy_ = true;
+        ++busy_;
       }
       ::close(fd);                 // the last reference: the inode and its pages go here
       done_.fetch_add(1, std::memory_order_relaxed);
+      std::lock_guard<std::mutex> g(mu_);
+      --busy_;
     }
   }
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<int> q_;
-  bool started_ = false, busy_ = false;
+  int threads_ = 0, idle_ = 0, busy_ = 0;
   std::atomic<uint64_t> done_{0};
 };
 
@@ -3148,8 +3168,9 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
   job->resolve = std::move(resolve);
   const uint64_t chunk =
       r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk) : std::min<uint64_t>(1u << 20, max_chunk);
+  job->first_bytes = std::min<uint64_t>(chunk, job->slot_bytes);   // the first chunk goes after one small read
   std::unique_ptr<NativeStream> ns(new ColdReadStream(store, job->session, r.block_id, off, end, chunk, window,
-                                                      slot_pool->size(), unix_peer, st, stats));
+                                                      slot_pool->size(), job->first_bytes, unix_peer, st, stats));
   stats->cold_streams.fetch_add(1, std::memory_order_relaxed);
   if (!ColdPool::get().submit([job] { job->run(); }, cfg.max_active)) {
     stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
