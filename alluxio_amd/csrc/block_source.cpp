@@ -1110,20 +1110,23 @@ namespace {
 
 class PrefetchPool {
  public:
-  static PrefetchPool& get() {
-    static PrefetchPool* p = new PrefetchPool();   // never destroyed: threads outlive statics
-    return *p;
+  // Two pools: prefetches of network sources (threads mostly blocked in recv) and of DMA / memcpy
+  // sources (threads issuing copies: more than a few dozen only contend).
+  static PrefetchPool& get(bool network = false) {
+    static PrefetchPool* net = new PrefetchPool(kNetworkCap);   // never destroyed: threads outlive statics
+    static PrefetchPool* dma = new PrefetchPool(kDmaCap);
+    return network ? *net : *dma;
   }
   // A thread is added whenever a prefetch would otherwise queue behind busy ones, up to the cap:
-  // each stream has at most one prefetch in flight, so the pool grows to the number of streams
-  // reading at once (256 reader threads of one client process get 256 concurrent chunk reads,
-  // not 16), and idle threads serve the next ones.
+  // each stream has at most one prefetch in flight, so the network pool grows with the streams
+  // reading at once (64 reader threads of one client process get 64 concurrent chunk reads, not
+  // 16), and idle threads serve the next ones.
   void submit(std::function<void()> fn) {
     std::function<void()> here;
     {
       std::lock_guard<std::mutex> g(mu_);
       q_.push_back(std::move(fn));
-      const int cap = want_ > 0 ? want_ : kDefaultCap;
+      const int cap = want_ > 0 ? want_ : cap_;
       if ((int)q_.size() > idle_ && threads_ < cap) {
         try {
           std::thread([this] { run(); }).detach();
@@ -1149,7 +1152,12 @@ class PrefetchPool {
   }
 
  private:
-  static constexpr int kDefaultCap = 256;
+  // measured on one MI355X box, 4 KiB readers of one client process: a 16-thread pool held gRPC
+  // at ~22-26 GB/s from 64 readers on; with a pool growing to 256, IPC readers fell from 46 to
+  // 11-16 GB/s at 64-256 threads (the D2H copies contend), while gRPC gained
+  static constexpr int kNetworkCap = 64, kDmaCap = 16;
+  explicit PrefetchPool(int cap) : cap_(cap) {}
+  const int cap_;
   void run() {
     pthread_setname_np(pthread_self(), "chunk-prefetch");
     for (;;) {
@@ -1174,7 +1182,10 @@ class PrefetchPool {
 
 }  // namespace
 
-void set_prefetch_threads(int n) { PrefetchPool::get().set_threads(n); }
+void set_prefetch_threads(int n) {
+  PrefetchPool::get(false).set_threads(n);
+  PrefetchPool::get(true).set_threads(n);
+}
 
 // One chunk read ahead: [lo, hi) of the file into `buf`, by a pool thread.
 struct HostInStream::Prefetch {
@@ -1255,7 +1266,7 @@ void HostInStream::schedule_prefetch() {
   uint8_t* dst = bufs_[nb];
   const uint64_t off = p->lo - cur_start_, n = p->hi - p->lo;
   pf_ = p;
-  PrefetchPool::get().submit([p, src, dst, off, n] {
+  PrefetchPool::get(src->waits_on_network()).submit([p, src, dst, off, n] {
     try {
       src->read(off, n, dst);
       p->finish(0, std::string());

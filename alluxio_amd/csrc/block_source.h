@@ -37,6 +37,10 @@ class BlockSource {
   // arenas: a memcpy; network streams: the frames are parsed into the destination).
   virtual bool direct() const { return false; }
   virtual bool needs_gil() const { return false; }
+  // A read mostly waits on a socket (true) rather than on a DMA or a memcpy: prefetches of such
+  // sources run on a pool that grows with the streams, DMA ones on a small fixed pool (hundreds
+  // of threads issuing D2H copies at once contend inside the HIP runtime).
+  virtual bool waits_on_network() const { return false; }
   virtual void close() {}
   uint64_t length() const { return length_; }
 
@@ -107,6 +111,7 @@ class GrpcBlockSource : public BlockSource {
   ~GrpcBlockSource() override;
   void read(uint64_t off, uint64_t n, uint8_t* dst) override;
   bool direct() const override { return true; }
+  bool waits_on_network() const override { return true; }
   void close() override;
   struct Conn;
 
@@ -254,7 +259,8 @@ class HostInStream {
   uint64_t bytes_ = 0, refills_ = 0, pf_hits_ = 0;
 };
 
-// Threads of the prefetch pool (0 = default: min(16, hardware threads)); takes effect on first use.
+// Cap on the threads of each prefetch pool (0 = defaults: 64 for network sources, 16 for DMA /
+// memcpy sources).  The pools add threads on demand up to the cap.
 void set_prefetch_threads(int n);
 
 }  // namespace amdx

@@ -316,6 +316,13 @@ for s in $STEPS; do
       run ww_mc_time1 300 python tools/worker_write_bench.py --threads 1 --files 4 --min-seconds 6 --file-size 256m --write-type MUST_CACHE --client-timing "$OUT/r6_mc_timing" --out "$OUT/r6_ct_timing.jsonl"
       run ww_th_time1 300 python tools/worker_write_bench.py --threads 1 --files 4 --min-seconds 6 --file-size 256m --write-type THROUGH --client-timing "$OUT/r6_th_timing" --out "$OUT/r6_ct_timing.jsonl"
       ;;
+    r6io)
+      # 16 writers with more data-server I/O threads (one connection per thread instead of two)
+      for io in 16 24; do
+        run ww_mc_io$io 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.native.io.threads=$io --out "$OUT/r6_worker_write_io.jsonl"
+        run ww_ct_io$io 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.native.io.threads=$io --out "$OUT/r6_worker_write_io.jsonl"
+      done
+      ;;
     r6fanout)
       # replica fan-out breakdown: 8 ranks (8 workers) on the one GPU, 3 replicas per block
       run bench_rehearse_8rank_r6 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --profile-json "$OUT/r6_rehearse_8rank.json"
