@@ -316,6 +316,14 @@ for s in $STEPS; do
       run ww_mc_time1 300 python tools/worker_write_bench.py --threads 1 --files 4 --min-seconds 6 --file-size 256m --write-type MUST_CACHE --client-timing "$OUT/r6_mc_timing" --out "$OUT/r6_ct_timing.jsonl"
       run ww_th_time1 300 python tools/worker_write_bench.py --threads 1 --files 4 --min-seconds 6 --file-size 256m --write-type THROUGH --client-timing "$OUT/r6_th_timing" --out "$OUT/r6_ct_timing.jsonl"
       ;;
+    r6coldab)
+      # cold single stream: UFS slot size / depth A/B (default 8 MiB x 3)
+      for sd in "2MB 8" "4MB 4" "8MB 3"; do
+        set -- $sd
+        run cold_s$1 300 python tools/remote_device_read_bench.py --uds --cold --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --worker-prop alluxio.worker.ufs.ingest.chunk.size=$1 --worker-prop alluxio.worker.ufs.ingest.depth=$2 --out "$OUT/r6_cold_slot_ab.jsonl"
+      done
+      run cached_s 300 python tools/remote_device_read_bench.py --uds --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --out "$OUT/r6_cold_slot_ab.jsonl"
+      ;;
     r6io)
       # 16 writers with more data-server I/O threads (one connection per thread instead of two)
       for io in 16 24; do
