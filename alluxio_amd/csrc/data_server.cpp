@@ -834,18 +834,9 @@ struct ColdJob {
         store->use_device();
         hs = thread_stream_on(store->device());   // the pool thread's stream (never one per read)
       }
-      if (want_cache) {
-        try {   // may evict (the I/O thread never waits for space: this thread does)
-          store->create_block(session, block, 0, "", std::max<uint64_t>(block_len, 1), true, false);
-          caching = true;
-        } catch (const StoreError&) {
-          caching = false;      // another reader caches it, or no space: stream without caching
-        }
-      }
-      {
-        std::lock_guard<std::mutex> g(st->mu);
-        st->caching = caching;
-      }
+      // The temp block is created once the first read is on its way to the client: the create
+      // (page allocation, maybe eviction) is not on the time to first byte.
+      bool create_pending = want_cache;
       stats->cold_setup_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
       const size_t depth = st->slots.size();
       const uint64_t first = first_bytes ? std::min(first_bytes, slot_bytes) : slot_bytes;
@@ -879,7 +870,9 @@ struct ColdJob {
         }
         read_ns += ns_since(tr);
         stats->cold_bytes.fetch_add(n, std::memory_order_relaxed);
-        if (caching) {
+        // the slot's bytes into the temp block (async H2D on this thread's stream; the slot is
+        // refilled only after its event, `depth` reads from now)
+        auto ingest = [&] {
           const bool async = hs && sl->ev;
           store->write(session, block, off, reinterpret_cast<uint64_t>(sl->buf), n, (int)MemKind::kHost,
                        reinterpret_cast<uint64_t>(hs), !async);
@@ -887,7 +880,8 @@ struct ColdJob {
             if (hipEventRecord(sl->ev, hs) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
             sl->dma = true;
           }
-        }
+        };
+        if (caching) ingest();
         {
           std::lock_guard<std::mutex> g(st->mu);
           sl->off = off;
@@ -897,6 +891,22 @@ struct ColdJob {
         if (idx == 0) stats->cold_first_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
         ingested = off + n;
         wake();
+        if (create_pending) {     // the first slot is out: now the temp block, then its bytes
+          create_pending = false;
+          const auto tc = clk::now();
+          try {   // may evict (the I/O thread never waits for space: this thread does)
+            store->create_block(session, block, 0, "", std::max<uint64_t>(block_len, 1), true, false);
+            caching = true;
+          } catch (const StoreError&) {
+            caching = false;      // another reader caches it, or no space: stream without caching
+          }
+          {
+            std::lock_guard<std::mutex> g(st->mu);
+            st->caching = caching;
+          }
+          if (caching) ingest();  // the sender only reads the slot; the reader refills it later
+          stats->cold_setup_ns.fetch_add(ns_since(tc), std::memory_order_relaxed);
+        }
       }
     } catch (const std::exception& e) {
       ok = false;

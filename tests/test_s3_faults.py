@@ -174,7 +174,9 @@ def test_native_cold_read_retries_and_stalls(blob, tmp_path):
         assert srv.injected == 2
         # a silent store: the stream fails within socket/request timeout (2 s + slack), UNAVAILABLE
         a0 = st.cold_aborted
-        srv.inject(3, "GET", 1, 1000, stall_ms=30000)
+        # from the 2nd GET on: the first (one-chunk) read lands, the temp block is created behind
+        # it, then the reads stall -- the block must be aborted, not left behind
+        srv.inject(3, "GET", 2, 1000, stall_ms=30000)
         t0 = time.monotonic()
         with pytest.raises(Exception) as ei:
             rfs.read_file("/s3/z")
