@@ -469,6 +469,23 @@ void bind_data_path(py::module_& m) {
       .def_property_readonly("commit_batches", [](const DataServerStats& s) { return s.commit_batches.load(); })
       .def_property_readonly("commit_failures", [](const DataServerStats& s) { return s.commit_failures.load(); })
       .def_property_readonly("crc_streamed", [](const DataServerStats& s) { return s.crc_streamed.load(); })
+      .def_property_readonly("send_timing", [](const DataServerStats& s) {
+        py::dict out;
+        const char* names[2] = {"cached", "cold"};
+        for (int k = 0; k < 2; ++k) {
+          const auto& t = s.send[k];
+          py::dict d;
+          d["streams"] = t.streams.load();
+          d["life_ns"] = t.life_ns.load();
+          d["first_ns"] = t.first_ns.load();
+          d["window_stalls"] = t.window_stalls.load();
+          d["window_ns"] = t.window_ns.load();
+          d["data_stalls"] = t.data_stalls.load();
+          d["data_ns"] = t.data_ns.load();
+          out[names[k]] = d;
+        }
+        return out;
+      })
       .def_property_readonly("cold_timing_ns", [](const DataServerStats& s) {
         py::dict d;
         d["queue"] = s.cold_queue_ns.load();

@@ -206,13 +206,50 @@ int64_t now_ns() {
       .count();
 }
 
+// Send-side timing of one ReadBlock stream (DataServerStats::SendTiming): the gaps between a call
+// of produce that stopped for want of window or data and the next call.
+class SendClock {
+ public:
+  explicit SendClock(DataServerStats::SendTiming* t) : t_(t), t0_(now_ns()) {}
+  void resume() {                 // produce entered: close the open gap
+    if (!kind_) return;
+    const uint64_t d = (uint64_t)(now_ns() - since_);
+    (kind_ == 1 ? t_->window_ns : t_->data_ns).fetch_add(d, std::memory_order_relaxed);
+    kind_ = 0;
+  }
+  void stall(int kind) {          // 1 window full, 2 next bytes not there
+    kind_ = kind;
+    since_ = now_ns();
+    (kind == 1 ? t_->window_stalls : t_->data_stalls).fetch_add(1, std::memory_order_relaxed);
+  }
+  void add_data_wait(int64_t ns) { t_->data_ns.fetch_add((uint64_t)ns, std::memory_order_relaxed); }
+  void sent() {
+    if (first_) return;
+    first_ = true;
+    t_->first_ns.fetch_add((uint64_t)(now_ns() - t0_), std::memory_order_relaxed);
+  }
+  void done() {
+    if (done_) return;
+    done_ = true;
+    t_->streams.fetch_add(1, std::memory_order_relaxed);
+    t_->life_ns.fetch_add((uint64_t)(now_ns() - t0_), std::memory_order_relaxed);
+  }
+
+ private:
+  DataServerStats::SendTiming* t_;
+  int64_t t0_, since_ = 0;
+  int kind_ = 0;
+  bool first_ = false, done_ = false;
+};
+
 class BlockReadStream : public NativeStream {
  public:
   BlockReadStream(StoreRef store, int64_t session, int64_t lock_id, int64_t block_id, uint64_t pos, uint64_t end,
                   uint64_t chunk, uint64_t window, bool device, bool unix_peer, std::shared_ptr<StagingPool> pool,
                   std::shared_ptr<DataServerStats> stats)
       : store_(std::move(store)), session_(session), lock_(lock_id), block_(block_id), pos_(pos), acked_(pos), end_(end),
-        chunk_(chunk), window_(window), device_(device), unix_(unix_peer), pool_(std::move(pool)), stats_(std::move(stats)) {}
+        chunk_(chunk), window_(window), device_(device), unix_(unix_peer), pool_(std::move(pool)), stats_(std::move(stats)),
+        clock_(&stats_->send[0]) {}
 
   ~BlockReadStream() override {
     for (int k = 0; k < 2; ++k) {
@@ -290,6 +327,7 @@ class BlockReadStream : public NativeStream {
   ssize_t produce_spans(size_t max, ByteSpan* spans, int max_spans, int* nspans, bool* eof, int* status,
                         std::string* msg) override {
     if (!device_ || max_spans < 2) return -2;
+    clock_.resume();
     size_t w = 0;
     int ns = 0;
     try {
@@ -319,9 +357,13 @@ class BlockReadStream : public NativeStream {
         if (w > 0) break;                      // this frame ends with the chunk
         if (pos_ >= end_) {
           *eof = true;
+          clock_.done();
           break;
         }
-        if (pos_ - acked_ >= window_) break;   // wait for offset_received
+        if (pos_ - acked_ >= window_) {        // wait for offset_received
+          clock_.stall(1);
+          break;
+        }
         next_chunk();
       }
     } catch (const std::exception& e) {
@@ -329,6 +371,7 @@ class BlockReadStream : public NativeStream {
       *msg = std::string("reading block ") + std::to_string(block_) + ": " + e.what();
       return -1;
     }
+    if (w > 0) clock_.sent();
     *nspans = ns;
     if (w > 0) stats_->zero_copy_frames.fetch_add(1, std::memory_order_relaxed);
     return (ssize_t)w;
@@ -389,11 +432,12 @@ class BlockReadStream : public NativeStream {
     if (device_) {
       const int k = cur_ ^ 1;                      // the slot chunk k was (pre)staged into
       if (!(slot_[k].valid && slot_[k].pos == pos_ && slot_[k].len == n)) stage(k, pos_, n);
-      const int64_t w0 = tracing_ ? now_ns() : 0;
+      const int64_t w0 = now_ns();
       if (slot_[k].inflight) {
         // normally long done: it ran during the last send
         if (hipEventSynchronize(slot_[k].ev) != hipSuccess) throw std::runtime_error("D2H staging copy failed");
         slot_[k].inflight = false;
+        clock_.add_data_wait(now_ns() - w0);
       }
       if (tracing_ && slot_[k].rec >= 0) {
         ReadTraceRec& r = trace_[slot_[k].rec];
@@ -435,6 +479,7 @@ class BlockReadStream : public NativeStream {
   int cur_rec_ = -1;
   hipEvent_t base_ev_ = nullptr;
   int64_t base_ns_ = 0;
+  SendClock clock_;
 };
 
 std::atomic<int64_t> g_session{(int64_t)1 << 62};   // above the Python range (utils/ids.py)
@@ -1041,7 +1086,7 @@ class ColdReadStream : public NativeStream {
       : store_(store), session_(session), block_(block_id), start_(pos), pos_(pos), acked_(pos), end_(end),
         chunk_(chunk), window_(window), slot_bytes_(slot_bytes),
         first_(first_bytes ? std::min(first_bytes, slot_bytes) : slot_bytes), unix_(unix_peer), st_(std::move(st)),
-        stats_(std::move(stats)) {}
+        stats_(std::move(stats)), clock_(&stats_->send[1]) {}
 
   ~ColdReadStream() override {
     bool exited, handed_off;
@@ -1143,6 +1188,7 @@ class ColdReadStream : public NativeStream {
   ssize_t produce_spans(size_t max, ByteSpan* spans, int max_spans, int* nspans, bool* eof, int* status,
                         std::string* msg) override {
     if (max_spans < 2) return -2;
+    clock_.resume();
     if (release_pending_) {
       release_pending_ = false;
       release_slot();
@@ -1171,13 +1217,21 @@ class ColdReadStream : public NativeStream {
       if (w > 0) break;                          // this frame ends with the chunk
       if (pos_ >= end_) {
         *eof = true;
+        clock_.done();
         break;
       }
-      if (pos_ - acked_ >= window_) break;
+      if (pos_ - acked_ >= window_) {
+        clock_.stall(1);
+        break;
+      }
       const int r = select_chunk(status, msg);
       if (r < 0) return -1;
-      if (r == 0) break;
+      if (r == 0) {
+        clock_.stall(2);
+        break;
+      }
     }
+    if (w > 0) clock_.sent();
     *nspans = ns;
     if (w > 0) stats_->zero_copy_frames.fetch_add(1, std::memory_order_relaxed);
     return (ssize_t)w;
@@ -1241,6 +1295,7 @@ class ColdReadStream : public NativeStream {
   uint64_t left_ = 0, slot_end_ = 0;
   const uint8_t* src_ = nullptr;
   ColdState::Slot* cur_slot_ = nullptr;
+  SendClock clock_;
 };
 
 // ---- WriteBlock ---------------------------------------------------------------------------------

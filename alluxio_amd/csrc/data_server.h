@@ -68,6 +68,15 @@ struct DataServerStats {
   // waiting for the stream to free a slot (consumer-bound), waiting for a slot's H2D
   std::atomic<uint64_t> cold_queue_ns{0}, cold_setup_ns{0}, cold_first_ns{0}, cold_read_ns{0},
       cold_slot_wait_ns{0}, cold_dma_wait_ns{0};
+  // The send side of ReadBlock streams, [0] cached (HBM staging) and [1] cold: streams finished,
+  // ns from the call's start to its last byte and to its first, and the gaps in which the stream
+  // had nothing to send -- the client's ack window was full, or the next bytes were not there yet
+  // (cold: the slot not read; cached: the staging D2H not done).
+  struct SendTiming {
+    std::atomic<uint64_t> streams{0}, life_ns{0}, first_ns{0}, window_stalls{0}, window_ns{0}, data_stalls{0},
+        data_ns{0};
+  };
+  SendTiming send[2];
 };
 
 // One block handed to the committer: the temp block of a finished WriteBlock (or of a complete

@@ -109,7 +109,7 @@ def main(argv=None) -> int:
     from alluxio_amd.utils.format import parse_space_size
     size = parse_space_size(a.file_size)
     conf = {"alluxio.worker.tieredstore.level0.dirs.path": a.tier,
-            "alluxio.worker.tieredstore.level0.dirs.quota": str(size + (512 << 20)),
+            "alluxio.worker.tieredstore.level0.dirs.quota": str(size + (1 << 30)),
             "alluxio.worker.hbm.page.size": "2MB", "alluxio.user.block.size.bytes.default": "64MB",
             "alluxio.security.authorization.permission.enabled": "false"}
     uds_dir = None
@@ -131,7 +131,8 @@ def main(argv=None) -> int:
                 c.heartbeat_workers()
             ds = c.workers[0].data_server
             st0 = (ds.stats.cold_streams, ds.stats.declined, ds.stats.cold_cached, ds.stats.zero_copy_frames,
-                   ds.stats.prefetched, ds.stats.domain_bytes, ds.stats.cold_timing_ns) if ds is not None else None
+                   ds.stats.prefetched, ds.stats.domain_bytes, ds.stats.cold_timing_ns,
+                   ds.stats.send_timing) if ds is not None else None
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "false",
                      "alluxio.user.native.reader.enabled": str(native).lower(),
@@ -165,6 +166,16 @@ def main(argv=None) -> int:
                 row["worker_zero_copy_frames"] = ds.stats.zero_copy_frames - st0[3]
                 row["worker_prefetched_chunks"] = ds.stats.prefetched - st0[4]
                 row["worker_domain_socket_bytes"] = ds.stats.domain_bytes - st0[5]
+                # the send side per block stream (ms): call start -> first / last byte, and the gaps
+                # with nothing to send (ack window full / next bytes not there yet)
+                kind = "cold" if a.cold else "cached"
+                t1, t0 = ds.stats.send_timing[kind], st0[7][kind]
+                ns = max(t1["streams"] - t0["streams"], 1)
+                row["worker_send_ms_per_block"] = {
+                    "streams": t1["streams"] - t0["streams"],
+                    **{k[:-3]: round((t1[k] - t0[k]) / ns / 1e6, 3) for k in ("life_ns", "first_ns", "window_ns", "data_ns")},
+                    "window_stalls": round((t1["window_stalls"] - t0["window_stalls"]) / ns, 1),
+                    "data_stalls": round((t1["data_stalls"] - t0["data_stalls"]) / ns, 1)}
                 if a.cold:
                     # the cold readers' time per block stream (ms)
                     ct = ds.stats.cold_timing_ns
