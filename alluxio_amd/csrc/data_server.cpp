@@ -879,9 +879,15 @@ struct ColdJob {
         store->use_device();
         hs = thread_stream_on(store->device());   // the pool thread's stream (never one per read)
       }
-      // The temp block is created once the first read is on its way to the client: the create
-      // (page allocation, maybe eviction) is not on the time to first byte.
+      // The temp block is created once the first two reads are on their way to the client (one
+      // chunk, then a slot: ~1 ms of sending): the create -- page allocation, maybe eviction --
+      // runs while they go out instead of before them; their bytes go into the block after it.
       bool create_pending = want_cache;
+      struct Unstored {
+        ColdState::Slot* sl;
+        uint64_t off, n;
+      };
+      std::vector<Unstored> unstored;
       stats->cold_setup_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
       const size_t depth = st->slots.size();
       const uint64_t first = first_bytes ? std::min(first_bytes, slot_bytes) : slot_bytes;
@@ -915,18 +921,19 @@ struct ColdJob {
         }
         read_ns += ns_since(tr);
         stats->cold_bytes.fetch_add(n, std::memory_order_relaxed);
-        // the slot's bytes into the temp block (async H2D on this thread's stream; the slot is
+        // a slot's bytes into the temp block (async H2D on this thread's stream; the slot is
         // refilled only after its event, `depth` reads from now)
-        auto ingest = [&] {
-          const bool async = hs && sl->ev;
-          store->write(session, block, off, reinterpret_cast<uint64_t>(sl->buf), n, (int)MemKind::kHost,
+        auto ingest = [&](ColdState::Slot* s, uint64_t o, uint64_t k) {
+          const bool async = hs && s->ev;
+          store->write(session, block, o, reinterpret_cast<uint64_t>(s->buf), k, (int)MemKind::kHost,
                        reinterpret_cast<uint64_t>(hs), !async);
           if (async) {
-            if (hipEventRecord(sl->ev, hs) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
-            sl->dma = true;
+            if (hipEventRecord(s->ev, hs) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
+            s->dma = true;
           }
         };
-        if (caching) ingest();
+        if (caching) ingest(sl, off, n);
+        else if (create_pending) unstored.push_back({sl, off, n});
         {
           std::lock_guard<std::mutex> g(st->mu);
           sl->off = off;
@@ -936,7 +943,9 @@ struct ColdJob {
         if (idx == 0) stats->cold_first_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
         ingested = off + n;
         wake();
-        if (create_pending) {     // the first slot is out: now the temp block, then its bytes
+        // after the second read (or the only one), before any slot comes round again: the sender
+        // only reads the slots, the reader refills them later
+        if (create_pending && (idx >= 1 || off + n >= end || unstored.size() >= depth)) {
           create_pending = false;
           const auto tc = clk::now();
           try {   // may evict (the I/O thread never waits for space: this thread does)
@@ -949,7 +958,9 @@ struct ColdJob {
             std::lock_guard<std::mutex> g(st->mu);
             st->caching = caching;
           }
-          if (caching) ingest();  // the sender only reads the slot; the reader refills it later
+          if (caching)
+            for (const auto& u : unstored) ingest(u.sl, u.off, u.n);
+          unstored.clear();
           stats->cold_setup_ns.fetch_add(ns_since(tc), std::memory_order_relaxed);
         }
       }

@@ -139,12 +139,12 @@ def test_python_s3_client_retries_and_times_out(blob, tmp_path):
     assert ufs2.get_status("s3://bkt/p/a").content_length == len(data)
 
 
-def _s3_cluster(tmp_path, base, **mount_props):
+def _s3_cluster(tmp_path, base, cluster_conf=None, **mount_props):
     props = {"alluxio.underfs.s3.endpoint": base, "s3a.accessKeyId": "AKID", "s3a.secretKey": "sk",
              "alluxio.underfs.s3.socket.timeout": "400ms", "alluxio.underfs.s3.request.timeout": "2s",
              "alluxio.underfs.s3.max.error.retry": "2", "alluxio.underfs.eventual.consistency.retry.max.num": "1"}
     props.update(mount_props)
-    c = _cluster(tmp_path)
+    c = _cluster(tmp_path, cluster_conf)
     c.__enter__()
     fs = c.client()
     fs.mount("/s3", "s3://bkt/ds", properties=props)
@@ -158,9 +158,12 @@ def test_native_cold_read_retries_and_stalls(blob, tmp_path):
     srv, base = blob
     rng = np.random.default_rng(3)
     objs = {k: rng.integers(0, 256, 6 * MB + 11 * i, dtype=np.uint8) for i, k in enumerate("wxyz")}
+    objs["z"] = rng.integers(0, 256, 24 * MB + 5, dtype=np.uint8)   # reads of 1, 8, 8, 7 MiB
     for k, d in objs.items():
         _put(base, "ds/" + k, d)
-    c, fs = _s3_cluster(tmp_path, base)
+    # one block per object and one GET per read (no sub-range split): the Nth GET is the Nth read
+    c, fs = _s3_cluster(tmp_path, base, cluster_conf={"alluxio.user.block.size.bytes.default": "32MB"},
+                        **{"alluxio.underfs.s3.threads.max": "1"})
     rfs = _remote_fs(c)
     try:
         w = c.workers[0]
@@ -174,9 +177,10 @@ def test_native_cold_read_retries_and_stalls(blob, tmp_path):
         assert srv.injected == 2
         # a silent store: the stream fails within socket/request timeout (2 s + slack), UNAVAILABLE
         a0 = st.cold_aborted
-        # from the 2nd GET on: the first (one-chunk) read lands, the temp block is created behind
-        # it, then the reads stall -- the block must be aborted, not left behind
-        srv.inject(3, "GET", 2, 1000, stall_ms=30000)
+        # from the 3rd GET on: the first two reads (one chunk, then a slot) land, the temp block
+        # is created behind them, then the reads stall -- the block must be aborted, not left
+        # behind
+        srv.inject(3, "GET", 3, 1000, stall_ms=30000)
         t0 = time.monotonic()
         with pytest.raises(Exception) as ei:
             rfs.read_file("/s3/z")
