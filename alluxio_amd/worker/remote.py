@@ -75,7 +75,10 @@ def peer_transfer(worker, req) -> tuple[bool, str]:
     """``PeerTransfer``: pull ``req.block_id`` from ``req.src_address`` (any same-node worker) or
     from transfer-group rank ``req.src_rank``."""
     if req.src_address:
-        from ..parallel.peer import is_same_node, pull_block
+        import time
+
+        from ..parallel.peer import _add_time, is_same_node, pull_block
+        t0 = time.perf_counter()
         try:
             host = req.src_address.rsplit(":", 1)[0]
             pull_block(worker, req.block_id, req.src_address, req.length, same_node=is_same_node(worker, host),
@@ -84,6 +87,10 @@ def peer_transfer(worker, req) -> tuple[bool, str]:
         except Exception as e:  # noqa: BLE001
             LOG.exception("peer transfer of block %d from %s failed", req.block_id, req.src_address)
             return False, str(e)
+        finally:
+            # the replica's handler, entry to exit (the writer's PeerTransfer round trip minus this
+            # is the RPC's own cost)
+            _add_time("handler", time.perf_counter() - t0)
     plane = getattr(worker, "transfer_plane", None)
     if plane is None:
         return False, "no RCCL transfer plane on this worker"

@@ -512,7 +512,7 @@ def main(argv=None):
             # where a replica pull's time goes (ms per pull, summed over ranks / pulls)
             pt1 = pull_times()
             steps = ("open_rpc", "map", "create_and_plan", "copy", "verify_crc", "commit_and_report", "unlock_rpc",
-                     "total", "pulls")
+                     "total", "handler", "pulls")
             tot = {k: SUM(float(pt1.get(k, 0.0) - pt0.get(k, 0.0))) for k in steps}
             npulls = max(tot.pop("pulls"), 1.0)
             pull_ms = {k: round(v / npulls * 1e3, 3) for k, v in tot.items()}

@@ -4,6 +4,8 @@ Reference shape pinned here: StressWorkerBench.java:251-276 -- every thread loop
 the whole file and re-opens it at EOF; WorkerBenchSummary.java:59-71 -- only bytes read after the
 warmup count, over the duration.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -26,8 +28,11 @@ def test_native_threads_read_the_file_over_and_over(tmp_path, short_circuit):
                                "alluxio.user.native.reader.buffer.size": "256KB"})
         st = c.workers[0].data_server.stats
         s0 = st.streams
+        # a sanitizer build (tools/sanitize.sh) runs the readers ~10x slower: give them the time to
+        # go round the file
+        slow = bool(os.environ.get("ALLUXIO_AMD_NATIVE_SO"))
         r = worker_bench(["--threads", "8", "--file-size", "3m", "--buffer-size", "4k", "--block-size", "1m",
-                          "--duration", "400ms", "--warmup", "100ms", "--mode", "native-threads"],
+                          "--duration", "4s" if slow else "400ms", "--warmup", "100ms", "--mode", "native-threads"],
                          fs=rfs, print_result=False)
         assert not r["errors"], r["errors"]
         n = r["native"]
