@@ -176,10 +176,6 @@ _k("WORKER_DATA_SERVER_DOMAIN_SOCKET_DEFAULT", "alluxio.worker.data.server.domai
 _k("WORKER_DATA_SERVER_NATIVE_COMMIT_ENABLED", "alluxio.worker.data.server.native.commit.enabled", "true",
    Scope.WORKER, "Commit natively written blocks in C++ (streamed per-page CRC32C, store commit, one master "
    "CommitBlocks report per group of blocks) instead of one Python NativeWriteCommit per block.")
-_k("WORKER_PYTHON_SWITCH_INTERVAL", "alluxio.worker.python.switch.interval", "", Scope.WORKER,
-   "Interpreter switch interval of a worker process (sys.setswitchinterval; empty = CPython's 5 ms): "
-   "how long a control RPC that wakes while another thread of the process holds the interpreter "
-   "lock may wait for it.")
 _k("WORKER_IPC_ENABLED", "alluxio.worker.ipc.enabled", "true", Scope.WORKER,
    "Hand out HIP IPC handles for short-circuit reads of HBM pages.")
 _k("WORKER_STAGING_BUFFER_SIZE", "alluxio.worker.staging.buffer.size", "64MB", Scope.WORKER,

@@ -166,16 +166,6 @@ class AlluxioWorkerProcess:
     def start(self, register: bool = True, start_heartbeats: bool = True) -> str:
         from .. import metrics as msys
         from ..utils.pause_monitor import from_conf as pause_monitor
-        sw = self.conf.get("alluxio.worker.python.switch.interval", "")
-        if sw:
-            # how long a Python thread runs before handing the interpreter lock to a waiting one
-            # (CPython default 5 ms): a control RPC (PeerTransfer, OpenDeviceBlock) that wakes while
-            # a client thread of the same process holds the lock waits up to that long
-            import sys
-            v = sw.strip().lower()
-            secs = (float(v[:-2]) / 1e6 if v.endswith("us") else float(v[:-2]) / 1e3 if v.endswith("ms")
-                    else float(v[:-1]) if v.endswith("s") else float(v) / 1e3)
-            sys.setswitchinterval(max(1e-5, secs))
         self._sinks = msys.load_sinks(self.conf, self.worker.metrics)
         self.pause_monitor = pause_monitor(self.conf, "worker", self.worker.metrics)
         if self.pause_monitor is not None:

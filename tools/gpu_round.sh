@@ -331,10 +331,6 @@ for s in $STEPS; do
         run ww_ct_io$io 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.native.io.threads=$io --out "$OUT/r6_worker_write_io.jsonl"
       done
       ;;
-    r6fanoutsw)
-      # the same rehearsal with a 0.5 ms interpreter switch interval in every worker process
-      run bench_rehearse_8rank_sw 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --prop alluxio.worker.python.switch.interval=500us --profile-json "$OUT/r6_rehearse_8rank_sw.json"
-      ;;
     r6fanout)
       # replica fan-out breakdown: 8 ranks (8 workers) on the one GPU, 3 replicas per block
       run bench_rehearse_8rank_r6 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --profile-json "$OUT/r6_rehearse_8rank.json"
