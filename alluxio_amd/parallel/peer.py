@@ -233,7 +233,11 @@ def fan_out(src_worker_addr: str, replica_addrs: list[str], block_id: int, lengt
             req = pb.block.PeerTransferRequest(block_id=block_id, length=length, src_address=src_worker_addr)
             if handle is not None:
                 req.handle.CopyFrom(handle)
+            tc = time.perf_counter()
+            _add_time("fan_call_start", tc - t1)       # queued on the control pool
             r = stub_for(addr).PeerTransfer(req, timeout=timeout_s)
+            _add_time("fan_call", time.perf_counter() - tc)
+            _add_time("fan_calls", 1.0)
             if not r.ok:
                 raise RuntimeError(r.message)
         except Exception as e:  # noqa: BLE001

@@ -519,11 +519,17 @@ def main(argv=None):
             pull_ms["pulls"] = int(npulls)
             # the writer's side of each block's fan-out (shared open, the replicas' PeerTransfer
             # calls, the unlock) and close()'s wait for the last block's pulls, per file
-            fsteps = ("fan_open_rpc", "fan_transfers", "fan_unlock_rpc", "fan_total", "fans", "fan_close_wait")
+            fsteps = ("fan_open_rpc", "fan_transfers", "fan_unlock_rpc", "fan_total", "fans", "fan_close_wait",
+                      "fan_call", "fan_call_start", "fan_calls")
             ftot = {k: SUM(float(pt1.get(k, 0.0) - pt0.get(k, 0.0))) for k in fsteps}
             nfans = max(ftot.pop("fans"), 1.0)
+            ncalls = max(ftot.pop("fan_calls"), 1.0)
+            per_call = {k: ftot.pop(k) for k in ("fan_call", "fan_call_start")}
             fan_ms = {k[4:]: round(v / nfans * 1e3, 3) for k, v in ftot.items() if k != "fan_close_wait"}
             fan_ms["fans"] = int(nfans)
+            # one PeerTransfer call as the writer sees it, and how long it waited to be issued
+            fan_ms["call"] = round(per_call["fan_call"] / ncalls * 1e3, 3)
+            fan_ms["call_issue_delay"] = round(per_call["fan_call_start"] / ncalls * 1e3, 3)
             fan_ms["close_wait_per_file"] = round(ftot["fan_close_wait"] / world * 1e3, 3)
             try:
                 rst = fs.get_status(f"/stress-worker-base/rep-{rank}")
