@@ -51,8 +51,6 @@ NATIVE_SERVICES = frozenset({
     "alluxio.grpc.file.FileSystemMasterClientService",
     "alluxio.grpc.block.BlockMasterClientService",
     "alluxio.grpc.meta.MetaMasterClientService",
-    # a worker advertises its native data server (unary calls: OpenDeviceBlock, PeerTransfer, ...)
-    "alluxio.grpc.block.BlockWorker",
 })
 
 

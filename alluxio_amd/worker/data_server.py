@@ -21,7 +21,6 @@ from __future__ import annotations
 
 import logging
 
-from ..master.services import SVC_VERSION
 from .services import SVC_BLOCK_WORKER
 
 LOG = logging.getLogger(__name__)
@@ -48,9 +47,7 @@ class WorkerDataServer:
             rpc_server, host, conf.get_int("alluxio.worker.data.server.native.port", "0"),
             fast_threads=2, blocking_threads=conf.get_int("alluxio.worker.data.server.native.blocking.threads", "8"),
             io_threads=conf.get_int("alluxio.worker.data.server.native.io.threads", "8"),
-            # getServiceVersion too: a same-node client's gRPC channel reaches this server over the
-            # domain socket, and its probe learns the framed native port (this one) from it
-            services={SVC_BLOCK_WORKER, SVC_VERSION}, bridge_services={SVC_BLOCK_WORKER},
+            services={SVC_BLOCK_WORKER}, bridge_services={SVC_BLOCK_WORKER},
             stream_threads=conf.get_int("alluxio.worker.data.server.native.stream.threads", "128"))
         # request streams (WriteBlock uploads) get a window of a few chunks
         lib().set_stream_window(self.frontend.server, 4 << 20)

@@ -111,12 +111,7 @@ class AlluxioWorkerProcess:
         self.server = RpcServer(host, self.port, metrics=msys.metrics("Worker"), enable_grpc=enable_grpc,
                                 conf=self.conf, domain_socket=None if self._native_data else self.domain_socket)
         self.server.add_servicer(SVC_BLOCK_WORKER, BlockWorkerService(self.worker, self.conf))
-        # getServiceVersion advertises the native data server's port (nativeRpcPort) once it runs:
-        # clients then make their unary BlockWorker calls (OpenDeviceBlock, PeerTransfer,
-        # UnlockDeviceBlock, ...) over the framed native transport there instead of grpcio
-        from ..master.services import SVC_VERSION, ServiceVersionHandler
-        self._version_handler = ServiceVersionHandler()
-        self.server.add_servicer(SVC_VERSION, self._version_handler)
+
         self.sync = BlockMasterSync(self.worker, self)
         self._threads: list[hb.HeartbeatThread] = []
         self.job_worker = None
@@ -184,7 +179,6 @@ class AlluxioWorkerProcess:
             from .data_server import WorkerDataServer
             self.data_server = WorkerDataServer(self.server, self.worker, self.conf, self.host, self.domain_socket)
             data_port = self.data_server.start()
-            self._version_handler.native_port = data_port
         ti = pb.grpc.TieredIdentity(tiers=[pb.grpc.LocalityTier(tierName="node", value=socket.gethostname()),
                                            pb.grpc.LocalityTier(tierName="gpu", value=str(self.store.device))])
         self.worker.address = pb.grpc.WorkerNetAddress(host=host, rpcPort=int(port), dataPort=data_port,
