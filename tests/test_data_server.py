@@ -655,6 +655,11 @@ def test_native_cold_read_through(tmp_path):
             assert rfs.read_file("/cold/b") == files["/cold/b"].tobytes()
             assert st.zero_copy_frames > z0            # UFS slots went to the socket without a copy
             nb = len(_blocks(rfs, "/cold/b"))
+            # the timing the benches report per block: the readers' and the senders' side
+            snd = st.send_timing["cold"]
+            assert snd["streams"] >= nb and 0 < snd["first_ns"] <= snd["life_ns"]
+            ct = st.cold_timing_ns
+            assert ct["ufs_read"] > 0 and ct["first_slot"] > 0
             assert st.declined == d0                       # nothing went to Python
             assert st.cold_streams - s0 == nb
             deadline = time.time() + 10                    # the client may see its last byte before the
