@@ -331,6 +331,20 @@ for s in $STEPS; do
         run ww_ct_io$io 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.native.io.threads=$io --out "$OUT/r6_worker_write_io.jsonl"
       done
       ;;
+    r6final)
+      # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
+      run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+      run smoke_final6 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()"
+      run bench_final6 300 python bench.py --gpus 1 --steps 20 --warmup 5
+      run ww_final_mc 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_final_writes.jsonl"
+      run ww_final_ct 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_final_writes.jsonl"
+      run wb_final 900 python tools/worker_bench_host.py --mode native-threads --threads 16,64,256 --transports grpc,ipc --duration 6s --warmup 2s --d2h-roof --out "$OUT/r6_final_stress.jsonl"
+      for par in 1 4; do
+        run cold_final_p$par 300 python tools/remote_device_read_bench.py --uds --cold --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/r6_final_cold.jsonl"
+        run cached_final_p$par 300 python tools/remote_device_read_bench.py --uds --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/r6_final_cold.jsonl"
+      done
+      run fanout_final 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29523 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --profile-json "$OUT/r6_final_fanout.json"
+      ;;
     r6fanout)
       # replica fan-out breakdown: 8 ranks (8 workers) on the one GPU, 3 replicas per block
       run bench_rehearse_8rank_r6 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --profile-json "$OUT/r6_rehearse_8rank.json"
