@@ -331,6 +331,11 @@ for s in $STEPS; do
         run ww_ct_io$io 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.native.io.threads=$io --out "$OUT/r6_worker_write_io.jsonl"
       done
       ;;
+    r6wkern)
+      # kernel trace of sustained native writes: the per-page CRC32C kernel runs on the write streams,
+      # once per committed HBM block, next to the H2D copies
+      run rocprof_writes 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_writes" -o w --output-format csv -- python3 tools/worker_write_bench.py --threads 4 --files 4 --min-seconds 4 --file-size 256m --write-type MUST_CACHE --out "$OUT/r6_write_kernels.jsonl"
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
