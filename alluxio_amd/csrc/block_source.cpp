@@ -747,6 +747,10 @@ void GrpcBlockSource::open(uint64_t off) {
   c_ = std::move(c);
 }
 
+void GrpcBlockSource::start() {
+  if (!c_) open(0);
+}
+
 void GrpcBlockSource::read(uint64_t off, uint64_t n, uint8_t* dst) {
   if (off + n > length_) throw StoreError(kErrInvalidArgument, "read beyond the block");
   if (!c_ || off != c_->pos) open(off);   // positioned / backward read: a new call at `off`

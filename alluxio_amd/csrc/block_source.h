@@ -41,6 +41,9 @@ class BlockSource {
   // sources run on a pool that grows with the streams, DMA ones on a small fixed pool (hundreds
   // of threads issuing D2H copies at once contend inside the HIP runtime).
   virtual bool waits_on_network() const { return false; }
+  // Begins delivering the block from offset 0 before the first read() (a network source sends
+  // its request now, so the bytes are on their way while the reader finishes the previous block).
+  virtual void start() {}
   virtual void close() {}
   uint64_t length() const { return length_; }
 
@@ -112,6 +115,7 @@ class GrpcBlockSource : public BlockSource {
   void read(uint64_t off, uint64_t n, uint8_t* dst) override;
   bool direct() const override { return true; }
   bool waits_on_network() const override { return true; }
+  void start() override;
   void close() override;
   struct Conn;
 

@@ -105,9 +105,45 @@ struct PyInStream {
   PyInStream(uint64_t length, uint64_t block_size, uint64_t chunk, py::object op, bool prefetch)
       : s(length, block_size, chunk, prefetch), opener(std::move(op)) {}
 
+  // The next block's source, opened and started while a read that runs into it still reads the
+  // current block (network sources: its ReadBlock request is out, so its first bytes -- and for a
+  // cold block the worker's first UFS reads -- are under way when the reader gets there).
+  int64_t next_idx = -1;
+  std::shared_ptr<BlockSource> next_src;
+
   void open_block(int64_t idx, bool failed) {
+    if (!failed && idx == next_idx && next_src) {
+      s.set_source(idx, std::move(next_src));
+      next_idx = -1;
+      return;
+    }
+    next_src.reset();
+    next_idx = -1;
     py::object src = opener(idx, failed);
     s.set_source(idx, src.cast<std::shared_ptr<BlockSource>>());
+  }
+
+  // A read continuing past block idx: open and start idx + 1 now (best effort: a failure here is
+  // left to the read of that block, which opens it again).
+  void start_next(int64_t idx, uint64_t read_end) {
+    const int64_t nx = idx + 1;
+    if (nx == next_idx || read_end <= (uint64_t)nx * s.block_size() || (uint64_t)nx * s.block_size() >= s.length())
+      return;
+    if (!s.source() || !s.source()->waits_on_network()) return;
+    try {
+      py::object src = opener(nx, false);
+      auto bs = src.cast<std::shared_ptr<BlockSource>>();
+      if (!bs->waits_on_network()) return;
+      {
+        py::gil_scoped_release rel;
+        bs->start();
+      }
+      next_src = std::move(bs);
+      next_idx = nx;
+    } catch (const std::exception&) {
+      next_src.reset();
+      next_idx = -1;
+    }
   }
 
   // Reads exactly n bytes at pos() (n <= bytes left); the GIL is held on entry.
@@ -115,9 +151,11 @@ struct PyInStream {
     if (closed) throw py::value_error("I/O operation on closed file");
     uint64_t done = 0;
     int failures = 0;
+    const uint64_t read_end = s.pos() + n;
     while (done < n) {
       const int64_t idx = (int64_t)(s.pos() / s.block_size());
       if (s.block_index() != idx || !s.source()) open_block(idx, false);
+      start_next(idx, read_end);
       // what the current chunk (or the completed prefetch of the next) holds: no GIL release
       const uint64_t have = s.copy_buffered(dst + done, n - done);
       if (have) {
@@ -156,6 +194,8 @@ struct PyInStream {
   void close() {
     closed = true;
     s.drop_source();
+    next_src.reset();
+    next_idx = -1;
   }
 };
 
