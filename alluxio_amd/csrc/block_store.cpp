@@ -1273,7 +1273,11 @@ std::vector<uint32_t> BlockStore::checksum(int64_t block_id, uint64_t piece_byte
 
 size_t BlockStore::checksum_async_words(uint64_t length, uint64_t page_size) {
   if (!length || !page_size) return 0;
-  return (size_t)(ceil_div(length, page_size) + crc32c_scratch_words(length, page_size) + 64);
+  const uint64_t np = ceil_div(length, page_size);
+  // out | scratch of either launch form | the page index array (int64, 2 words each, aligned)
+  const uint64_t scratch = std::max<uint64_t>(crc32c_scratch_words(length, page_size),
+                                              crc32c_pages_scratch_words(length, page_size));
+  return (size_t)(np + scratch + 2 + 2 * np + 64);
 }
 
 size_t BlockStore::checksum_async(int64_t block_id, hipStream_t stream, uint32_t* dev_buf, size_t dev_words,
@@ -1291,6 +1295,27 @@ size_t BlockStore::checksum_async(int64_t block_id, hipStream_t stream, uint32_t
   const size_t np = (size_t)ceil_div(len, ps);
   if (dev_words < checksum_async_words(len, ps)) return 0;
   set_device();
+  // One launch over the block's scattered pages: the page index array goes through the caller's
+  // pinned buffer (same size as dev_buf, words [np, ...) are free until the CRCs land in [0, np))
+  // into dev_buf behind the scratch.
+  {
+    const uint64_t scratch = std::max<uint64_t>(crc32c_scratch_words(len, ps), crc32c_pages_scratch_words(len, ps));
+    const size_t idx_word = (size_t)((np + scratch + 1) & ~1ull);     // 8-byte aligned
+    if (idx_word + 2 * np <= dev_words && snap.pages.size() >= np) {
+      int64_t* host_idx = reinterpret_cast<int64_t*>(host_out + idx_word);
+      for (size_t k = 0; k < np; ++k) host_idx[k] = snap.pages[k];
+      int64_t* dev_idx = reinterpret_cast<int64_t*>(dev_buf + idx_word);
+      HIP_OK(hipMemcpyAsync(dev_idx, host_idx, np * sizeof(int64_t), hipMemcpyHostToDevice, stream));
+      const hipError_t e = launch_crc32c_pages(reinterpret_cast<const uint8_t*>(d.spec.base), dev_idx, len, ps,
+                                               dev_buf, dev_buf + np, scratch, stream);
+      if (e == hipSuccess) {
+        HIP_OK(hipMemcpyAsync(host_out, dev_buf, np * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        if (page_size_out) *page_size_out = ps;
+        return np;
+      }
+      if (e != hipErrorNotSupported) HIP_OK(e);
+    }
+  }
   uint64_t off = 0;
   size_t i = 0, piece_idx = 0;
   while (off < len) {                      // contiguous page runs, one launch each

@@ -229,9 +229,11 @@ class BlockStore {
   std::vector<uint32_t> checksum(int64_t block_id, uint64_t piece_bytes);
   // Per-page CRC32C of HBM block `block_id` (temp or committed) enqueued on `stream` behind what
   // it already carries (the block's last H2D): the CRCs land in `dev_buf` (device, `dev_words`
-  // words: pages + crc32c_scratch_words) and are copied into `host_out` (pinned, one word per
-  // page).  Nothing waits: the caller records an event after it.  Returns the page count, 0 when
-  // the block is not in a device dir or dev_words is too small (checksum() then).
+  // words, checksum_async_words) and are copied into `host_out` (pinned, also `dev_words` words:
+  // one per page at the front; the rest stages the block's page index array for the single
+  // launch over its scattered pages).  Nothing waits: the caller records an event after it.
+  // Returns the page count, 0 when the block is not in a device dir or dev_words is too small
+  // (checksum() then).
   size_t checksum_async(int64_t block_id, hipStream_t stream, uint32_t* dev_buf, size_t dev_words, uint32_t* host_out,
                         uint64_t* page_size_out);
   // Device words checksum_async needs for a block of `length` bytes in a dir of `page_size` pages.

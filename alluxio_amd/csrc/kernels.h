@@ -64,6 +64,14 @@ void set_seq_read_variant(int variant, unsigned grid_cap);
 hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint64_t piece_bytes,
                                 uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
                                 hipStream_t stream);
+// The same per-page CRC32Cs of a block whose pages are scattered in an arena: page i of the block
+// is base + page_idx[i] * page_bytes (page_idx: device array).  One launch pair for the whole
+// block; hipErrorNotSupported when the active CRC variant has no paged form (use per-run launches).
+hipError_t launch_crc32c_pages(const uint8_t* base, const int64_t* page_idx, uint64_t total_bytes,
+                               uint64_t page_bytes, uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
+                               hipStream_t stream);
+// Scratch words launch_crc32c_pages needs.
+uint64_t crc32c_pages_scratch_words(uint64_t total_bytes, uint64_t page_bytes);
 // Standard CRC32C of n gathered pieces (device pointers/lengths in device memory, each piece
 // <= crc32c_gather_max_piece() bytes), one workgroup per piece.
 hipError_t launch_crc32c_gather(const uint64_t* ptrs, const uint32_t* lens, uint64_t n, uint32_t* out,

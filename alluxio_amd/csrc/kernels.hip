@@ -775,6 +775,7 @@ __global__ __launch_bounds__(kCrc4Threads) void crc32c_segments_v4_kernel(
 // final positions with one multiply by a precomputed x^(8*64*d) and XOR-reduced.  Produces the
 // same raw (zero-init) segment CRC as v1-v4.
 constexpr uint64_t kCrcSeg5 = 1024 * 1024;
+constexpr uint64_t kCrcPagedSeg = 256 * 1024;
 
 __device__ __forceinline__ uint32_t crc5_step(uint32_t x, const uint32_t* __restrict__ my) {
   return my[(3 * 256 + (x & 255)) * 32] ^ my[(2 * 256 + ((x >> 8) & 255)) * 32] ^
@@ -792,9 +793,12 @@ __device__ __forceinline__ uint32_t crc5_chunk(uint32_t c, const uint4 v[4], con
   return c;
 }
 
+// page_idx (optional): piece i lives at base + page_idx[i] * piece_bytes instead of base + i *
+// piece_bytes -- the scattered pages of one arena block checksummed in one launch.
 __global__ __launch_bounds__(kCrc5Threads) void crc32c_segments_v5_kernel(
     const uint8_t* __restrict__ base, uint64_t total_bytes, uint64_t piece_bytes, uint64_t seg_bytes,
-    uint64_t segs_per_piece, uint64_t nsegs, uint32_t* __restrict__ seg_crc) {
+    uint64_t segs_per_piece, uint64_t nsegs, uint32_t* __restrict__ seg_crc,
+    const int64_t* __restrict__ page_idx) {
   __shared__ uint32_t t4r[4 * 256 * 32];   // 128 KiB
   __shared__ uint32_t sh[4][256];
   __shared__ uint32_t lsh[kCrc5Threads];
@@ -812,7 +816,8 @@ __global__ __launch_bounds__(kCrc5Threads) void crc32c_segments_v5_kernel(
     const uint64_t piece_len = std::min(piece_bytes, total_bytes - piece_start);
     const uint64_t seg_start = piece_start + seg_in_piece * seg_bytes;
     const uint64_t seg_len = std::min(seg_bytes, piece_start + piece_len - seg_start);
-    const uint8_t* seg = base + seg_start;
+    const uint8_t* seg = page_idx ? base + (uint64_t)page_idx[piece] * piece_bytes + seg_in_piece * seg_bytes
+                                  : base + seg_start;
     const uint64_t nch = seg_len / kCrc5Chunk;
     uint32_t c = 0;
     uint64_t last = ~0ull;
@@ -956,6 +961,52 @@ static int g_crc_variant = 4;  // 0: per-lane contiguous strips (v1), 1: interle
 
 void set_crc_variant(int v) { g_crc_variant = v; }
 
+namespace {
+// CUs of the current device (queried once per device, not per launch)
+int cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
+}  // namespace
+
+uint64_t crc32c_pages_scratch_words(uint64_t total_bytes, uint64_t page_bytes) {
+  if (!total_bytes || !page_bytes) return 0;
+  const uint64_t seg = std::min(kCrcPagedSeg, page_bytes);
+  return ((total_bytes + page_bytes - 1) / page_bytes) * ((page_bytes + seg - 1) / seg);
+}
+
+hipError_t launch_crc32c_pages(const uint8_t* base, const int64_t* page_idx, uint64_t total_bytes,
+                               uint64_t page_bytes, uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
+                               hipStream_t stream) {
+  if (total_bytes == 0) return hipSuccess;
+  if (g_crc_variant != 4) return hipErrorNotSupported;   // the paged form exists for v5 only
+  hipError_t e = ensure_crc_tables();
+  if (e != hipSuccess) return e;
+  const uint64_t npieces = (total_bytes + page_bytes - 1) / page_bytes;
+  // 256 KiB segments: a 64 MiB block of 2 MiB pages is 256 workgroups, one per CU (1 MiB segments
+  // would leave three quarters of the CUs idle)
+  const uint64_t seg = std::min(kCrcPagedSeg, page_bytes);
+  const uint64_t spp = (page_bytes + seg - 1) / seg;
+  const uint64_t nsegs = npieces * spp;
+  if (scratch_words < nsegs) return hipErrorInvalidValue;
+  const unsigned g4 = (unsigned)std::min<uint64_t>(nsegs, (uint64_t)cu_count());
+  hipLaunchKernelGGL(crc32c_segments_v5_kernel, dim3(g4), dim3(kCrc5Threads), 0, stream, base, total_bytes,
+                     page_bytes, seg, spp, nsegs, scratch, page_idx);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const unsigned g2 = (unsigned)std::min<uint64_t>(npieces, 4096);
+  hipLaunchKernelGGL(crc32c_pieces_kernel, dim3(g2), dim3(kCrcThreads), 0, stream, scratch, total_bytes,
+                     page_bytes, seg, spp, npieces, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint64_t piece_bytes,
                                 uint32_t* out, uint32_t* scratch, uint64_t scratch_words,
                                 hipStream_t stream) {
@@ -981,12 +1032,10 @@ hipError_t launch_crc32c_pieces(const uint8_t* base, uint64_t total_bytes, uint6
     hipLaunchKernelGGL(crc32c_segments_v3_kernel, dim3(g1), dim3(kCrcThreads), 0, stream, base,
                        total_bytes, piece_bytes, seg, spp, nsegs, scratch);
   } else {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const unsigned g4 = (unsigned)std::min<uint64_t>(nsegs, (uint64_t)cus);   // one >100 KiB-LDS WG per CU
+    const unsigned g4 = (unsigned)std::min<uint64_t>(nsegs, (uint64_t)cu_count());   // one >100 KiB-LDS WG per CU
     if (g_crc_variant == 4)
       hipLaunchKernelGGL(crc32c_segments_v5_kernel, dim3(g4), dim3(kCrc5Threads), 0, stream, base,
-                         total_bytes, piece_bytes, seg, spp, nsegs, scratch);
+                         total_bytes, piece_bytes, seg, spp, nsegs, scratch, (const int64_t*)nullptr);
     else
       hipLaunchKernelGGL(crc32c_segments_v4_kernel, dim3(g4), dim3(kCrc4Threads), 0, stream, base,
                          total_bytes, piece_bytes, seg, spp, nsegs, scratch);

@@ -177,17 +177,29 @@ def test_streamed_crc_of_hbm_blocks_equals_checksum(tmp_path):
         rfs = _remote_fs(c)
         w = c.workers[0]
         st = w.data_server.stats
+        # holes in the arena first: the blocks below get scattered pages, which the CRC kernel
+        # reads through the block's page index array in one launch
+        for i in range(16):
+            rfs.write_file(f"/crc/f{i}", np.full(MB, i, dtype=np.uint8), write_type="MUST_CACHE")
+        for i in range(0, 16, 2):
+            rfs.delete(f"/crc/f{i}")
+        c.heartbeat_workers()
         s0 = st.crc_streamed
         data = np.random.default_rng(5).integers(0, 256, 10 * MB + 12345, dtype=np.uint8)
         rfs.write_file("/crc/a", data, write_type="MUST_CACHE")
         blocks = _blocks(rfs, "/crc/a")
         assert st.crc_streamed - s0 == len(blocks)
+        scattered = 0
+        for bid, _ in blocks:
+            pages = list(w.worker.native.block_pages(bid)[0])
+            scattered += any(b != a + 1 for a, b in zip(pages, pages[1:]))
         for bid, n in blocks:
             piece, crcs = w.worker.crc[bid]
             assert piece == 1 * MB
             assert crcs == list(w.worker.native.checksum(bid, 0))
             assert len(crcs) == -(-n // MB)
         assert rfs.read_file("/crc/a") == data.tobytes()
+        print(f"blocks with scattered pages: {scattered} of {len(blocks)}")
         rfs.close()
         fs.close()
 

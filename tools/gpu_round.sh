@@ -336,6 +336,12 @@ for s in $STEPS; do
       # once per committed HBM block, next to the H2D copies
       run rocprof_writes 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_writes" -o w --output-format csv -- python3 tools/worker_write_bench.py --threads 4 --files 4 --min-seconds 4 --file-size 256m --write-type MUST_CACHE --out "$OUT/r6_write_kernels.jsonl"
       ;;
+    r6crc)
+      # one CRC launch pair per committed block (paged kernel): correctness, write sweep, kernel counts
+      run pytest_crc 300 python -u -m pytest tests/test_native_commit.py tests/test_kernels_gpu.py -m gpu -x -v -s --timeout 120 --timeout-method thread
+      run ww_crc_mc 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_writes_paged_crc.jsonl"
+      run rocprof_writes_paged 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_writes_paged" -o w --output-format csv -- python3 tools/worker_write_bench.py --threads 4 --files 4 --min-seconds 4 --file-size 256m --write-type MUST_CACHE --out "$OUT/r6_write_kernels_paged.jsonl"
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
