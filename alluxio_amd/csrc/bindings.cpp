@@ -62,6 +62,25 @@ std::vector<uint32_t> crc32c_device(uint64_t ptr, uint64_t len, uint64_t piece, 
   return out;
 }
 
+// Per-page CRC32C of pages scattered in an arena at `base` (page i of the block is
+// base + pages[i] * page_bytes), one launch pair -- the form BlockStore::checksum_async uses.
+std::vector<uint32_t> crc32c_device_pages(uint64_t base, const std::vector<int64_t>& pages, uint64_t len,
+                                          uint64_t page_bytes) {
+  if (!page_bytes) throw std::invalid_argument("page_bytes must be > 0");
+  const uint64_t np = len ? (len + page_bytes - 1) / page_bytes : 0;
+  if (pages.size() < np) throw std::invalid_argument("fewer pages than the length covers");
+  std::vector<uint32_t> out(np);
+  if (!np) return out;
+  const uint64_t sw = crc32c_pages_scratch_words(len, page_bytes);
+  DevBuf d((np + sw) * 4);
+  DevBuf idx(np * sizeof(int64_t));
+  HIP_CHECK(hipMemcpy(idx.p, pages.data(), np * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIP_CHECK(launch_crc32c_pages(reinterpret_cast<const uint8_t*>(base), (const int64_t*)idx.p, len, page_bytes,
+                                (uint32_t*)d.p, (uint32_t*)d.p + np, sw, 0));
+  HIP_CHECK(hipMemcpy(out.data(), d.p, np * 4, hipMemcpyDeviceToHost));
+  return out;
+}
+
 // chunks: list of (src_ptr, dst_ptr, src_bytes, dst_capacity) on the device
 std::vector<int32_t> lz4_device(const std::vector<std::tuple<uint64_t, uint64_t, uint32_t, uint32_t>>& chunks,
                                 bool compress, uint64_t stream) {
@@ -847,6 +866,8 @@ PYBIND11_MODULE(_C, m) {
           return py::bytes(out);
         }, py::arg("data"), py::arg("bytes_per_checksum") = 512);
   m.def("crc32c_combine", &crc32c_combine);
+  m.def("crc32c_device_pages", &crc32c_device_pages, G(), py::arg("base"), py::arg("pages"), py::arg("length"),
+        py::arg("page_bytes"));
   m.def("crc32c_device", &crc32c_device, G(), py::arg("ptr"), py::arg("length"), py::arg("piece") = 0,
         py::arg("stream") = 0);
   m.def("lz4_compress", [](py::bytes data) {

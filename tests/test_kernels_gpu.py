@@ -58,6 +58,25 @@ def test_crc32c_matches_host(gpu, variant):
     C.set_crc_variant(4)
 
 
+def test_crc32c_device_pages_scattered(gpu):
+    """The one-launch CRC of a block whose pages are scattered in the arena (the streamed commit
+    CRC, BlockStore::checksum_async): page i read at base + pages[i] * page_bytes, the last page
+    partial, equal to the host CRC32C of each page."""
+    C = lib()
+    C.set_crc_variant(4)
+    for page_bytes, npages, tail in [(2 << 20, 12, 12345), (1 << 20, 9, 1), (300_001, 7, 77), (4096, 33, 4095)]:
+        arena = _t(page_bytes * (npages + 5), gpu)
+        host = arena.cpu().numpy().tobytes()
+        pages = list(np.random.default_rng(page_bytes).permutation(npages + 5)[:npages])
+        length = (npages - 1) * page_bytes + tail
+        got = C.crc32c_device_pages(arena.data_ptr(), [int(p) for p in pages], length, page_bytes)
+        want = []
+        for i, p in enumerate(pages):
+            n = min(page_bytes, length - i * page_bytes)
+            want.append(C.crc32c(host[int(p) * page_bytes:int(p) * page_bytes + n]))
+        assert got == want, (page_bytes, npages)
+
+
 @pytest.mark.parametrize("variant", [-1] + list(range(27)))
 def test_lz4_device_roundtrip(gpu, variant):
     import torch
