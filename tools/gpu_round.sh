@@ -342,6 +342,12 @@ for s in $STEPS; do
       run ww_crc_mc 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_writes_paged_crc.jsonl"
       run rocprof_writes_paged 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_writes_paged" -o w --output-format csv -- python3 tools/worker_write_bench.py --threads 4 --files 4 --min-seconds 4 --file-size 256m --write-type MUST_CACHE --out "$OUT/r6_write_kernels_paged.jsonl"
       ;;
+    r6freeahead)
+      # creates that must evict: one radix-select per create vs freeing 1 GiB ahead
+      run ww_fa0 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_free_ahead.jsonl"
+      run ww_fa1g 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.tieredstore.free.ahead.bytes=1GB --out "$OUT/r6_free_ahead.jsonl"
+      run ww_fa1g_ct 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.tieredstore.free.ahead.bytes=1GB --out "$OUT/r6_free_ahead.jsonl"
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
