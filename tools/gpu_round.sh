@@ -348,6 +348,12 @@ for s in $STEPS; do
       run ww_fa1g 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.tieredstore.free.ahead.bytes=1GB --out "$OUT/r6_free_ahead.jsonl"
       run ww_fa1g_ct 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.tieredstore.free.ahead.bytes=1GB --out "$OUT/r6_free_ahead.jsonl"
       ;;
+    r6freeahead2)
+      for fa in 0 256MB 1GB; do
+        run ww_ct_fa_$fa 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.tieredstore.free.ahead.bytes=$fa --out "$OUT/r6_free_ahead2.jsonl"
+        run ww_mc_fa_$fa 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.tieredstore.free.ahead.bytes=$fa --out "$OUT/r6_free_ahead2.jsonl"
+      done
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
