@@ -176,6 +176,10 @@ _k("WORKER_DATA_SERVER_DOMAIN_SOCKET_DEFAULT", "alluxio.worker.data.server.domai
 _k("WORKER_DATA_SERVER_NATIVE_COMMIT_ENABLED", "alluxio.worker.data.server.native.commit.enabled", "true",
    Scope.WORKER, "Commit natively written blocks in C++ (streamed per-page CRC32C, store commit, one master "
    "CommitBlocks report per group of blocks) instead of one Python NativeWriteCommit per block.")
+_k("WORKER_HBM_EVICT_BATCH_BYTES", "alluxio.worker.hbm.evict.batch.bytes", "1GB", Scope.WORKER,
+   "With an HBM tier, the least one eviction round frees (at most 1/32 of the smallest HBM dir): "
+   "the device victim selection runs once per batch of evicting creates, not once per create. "
+   "alluxio.worker.tieredstore.free.ahead.bytes, when larger, wins.")
 _k("WORKER_IPC_ENABLED", "alluxio.worker.ipc.enabled", "true", Scope.WORKER,
    "Hand out HIP IPC handles for short-circuit reads of HBM pages.")
 _k("WORKER_STAGING_BUFFER_SIZE", "alluxio.worker.staging.buffer.size", "64MB", Scope.WORKER,

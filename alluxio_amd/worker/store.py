@@ -300,8 +300,17 @@ class TieredStore:
         self.has_device_tier = any(a is not None and a.kind == "hbm" for a in self.arenas)
         self.native.set_use_device_evict(conf.get_bool("alluxio.worker.eviction.device.enabled", "true"))
         self.native.set_demote_on_evict(conf.get_bool("alluxio.worker.tieredstore.eviction.demote", "true"))
-        # TieredBlockStore.allocateSpace frees size + free.ahead.bytes when it has to evict
-        self.native.set_free_ahead(conf.get_bytes("alluxio.worker.tieredstore.free.ahead.bytes", "0"))
+        # TieredBlockStore.allocateSpace frees size + free.ahead.bytes when it has to evict.  With an
+        # HBM tier one eviction round frees at least alluxio.worker.hbm.evict.batch.bytes (capped at
+        # 1/32 of the smallest HBM dir): the device radix select then runs once per batch of
+        # creates instead of once per create (16 writers, 64 MiB blocks: CACHE_THROUGH 21.2 ->
+        # 24.1 GB/s, profiles/r6_free_ahead.md)
+        ahead = conf.get_bytes("alluxio.worker.tieredstore.free.ahead.bytes", "0")
+        hbm_caps = [sp.capacity for sp, a in zip(specs, self.arenas) if a is not None and a.kind == "hbm"]
+        if hbm_caps:
+            batch = conf.get_bytes("alluxio.worker.hbm.evict.batch.bytes", "1GB")
+            ahead = max(ahead, min(batch, min(hbm_caps) // 32))
+        self.native.set_free_ahead(ahead)
         self.native.set_use_device_alloc(conf.get_bool("alluxio.worker.hbm.device.alloc.enabled", "true"),
                                          conf.get_int("alluxio.worker.hbm.device.alloc.min.pages", "1024"))
         LOG.info("tiered store: %s", self.native.stats())

@@ -354,6 +354,11 @@ for s in $STEPS; do
         run ww_mc_fa_$fa 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.tieredstore.free.ahead.bytes=$fa --out "$OUT/r6_free_ahead2.jsonl"
       done
       ;;
+    r6wdefault)
+      # sustained writes with the defaults (HBM eviction batches on)
+      run ww_def_mc 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_writes_evict_batch.jsonl"
+      run ww_def_ct 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_writes_evict_batch.jsonl"
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
