@@ -415,7 +415,9 @@ class FileInStream(io.RawIOBase):
             self._nat = lib().HostInStream(self.length, self.block_size,
                                            ctx.conf.get_bytes("alluxio.user.native.reader.buffer.size", "4MB"),
                                            _native_opener(self),
-                                           ctx.conf.get_bool("alluxio.user.native.reader.prefetch.enabled", "true"))
+                                           ctx.conf.get_bool("alluxio.user.native.reader.prefetch.enabled", "true"),
+                                           ctx.conf.get_bool("alluxio.user.native.reader.next.block.start.enabled",
+                                                             "true"))
             # instance attribute: read(buf) loops call the C entry point directly
             self.readinto = self._nat.fast_readinto
 

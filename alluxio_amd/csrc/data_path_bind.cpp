@@ -110,6 +110,7 @@ struct PyInStream {
   // cold block the worker's first UFS reads -- are under way when the reader gets there).
   int64_t next_idx = -1;
   std::shared_ptr<BlockSource> next_src;
+  bool start_next_enabled = true;
 
   void open_block(int64_t idx, bool failed) {
     if (!failed && idx == next_idx && next_src) {
@@ -127,7 +128,7 @@ struct PyInStream {
   // left to the read of that block, which opens it again).
   void start_next(int64_t idx, uint64_t read_end) {
     const int64_t nx = idx + 1;
-    if (nx == next_idx || read_end <= (uint64_t)nx * s.block_size() || (uint64_t)nx * s.block_size() >= s.length())
+    if (!start_next_enabled || nx == next_idx || read_end <= (uint64_t)nx * s.block_size() || (uint64_t)nx * s.block_size() >= s.length())
       return;
     if (!s.source() || !s.source()->waits_on_network()) return;
     try {
@@ -438,8 +439,14 @@ void bind_data_path(py::module_& m) {
       .def(py::init<py::object, uint64_t>(), py::arg("reader"), py::arg("length"));
 
   py::class_<PyInStream>(m, "HostInStream")
-      .def(py::init<uint64_t, uint64_t, uint64_t, py::object, bool>(), py::arg("length"), py::arg("block_size"),
-           py::arg("chunk"), py::arg("opener"), py::arg("prefetch") = true)
+      .def(py::init([](uint64_t length, uint64_t block_size, uint64_t chunk, py::object opener, bool prefetch,
+                       bool start_next) {
+             auto p = std::make_unique<PyInStream>(length, block_size, chunk, std::move(opener), prefetch);
+             p->start_next_enabled = start_next;
+             return p;
+           }),
+           py::arg("length"), py::arg("block_size"), py::arg("chunk"), py::arg("opener"), py::arg("prefetch") = true,
+           py::arg("start_next") = true)
       .def_property("pos", [](const PyInStream& s) { return s.s.pos(); },
                     [](PyInStream& s, uint64_t p) { s.s.seek(p); })
       .def_property_readonly("length", [](const PyInStream& s) { return s.s.length(); })

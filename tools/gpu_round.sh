@@ -359,6 +359,13 @@ for s in $STEPS; do
       run ww_def_mc 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_writes_evict_batch.jsonl"
       run ww_def_ct 600 python tools/worker_write_bench.py --threads 1,4,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_writes_evict_batch.jsonl"
       ;;
+    r6startab)
+      # next-block stream start on / off, cold and cached single stream, same box
+      for ns in true false; do
+        run cold_ns_$ns 300 python tools/remote_device_read_bench.py --uds --cold --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --client-prop alluxio.user.native.reader.next.block.start.enabled=$ns --out "$OUT/r6_next_block_start_ab.jsonl"
+        run cached_ns_$ns 300 python tools/remote_device_read_bench.py --uds --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --client-prop alluxio.user.native.reader.next.block.start.enabled=$ns --out "$OUT/r6_next_block_start_ab.jsonl"
+      done
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
