@@ -417,7 +417,7 @@ class FileInStream(io.RawIOBase):
                                            _native_opener(self),
                                            ctx.conf.get_bool("alluxio.user.native.reader.prefetch.enabled", "true"),
                                            ctx.conf.get_bool("alluxio.user.native.reader.next.block.start.enabled",
-                                                             "true"))
+                                                             "false"))
             # instance attribute: read(buf) loops call the C entry point directly
             self.readinto = self._nat.fast_readinto
 

@@ -180,9 +180,11 @@ _k("WORKER_HBM_EVICT_BATCH_BYTES", "alluxio.worker.hbm.evict.batch.bytes", "1GB"
    "With an HBM tier, the least one eviction round frees (at most 1/32 of the smallest HBM dir): "
    "the device victim selection runs once per batch of evicting creates, not once per create. "
    "alluxio.worker.tieredstore.free.ahead.bytes, when larger, wins.")
-_k("USER_NATIVE_READER_NEXT_BLOCK_START", "alluxio.user.native.reader.next.block.start.enabled", "true",
+_k("USER_NATIVE_READER_NEXT_BLOCK_START", "alluxio.user.native.reader.next.block.start.enabled", "false",
    Scope.CLIENT, "A large sequential read that runs into the next remote block starts that block's ReadBlock "
-   "stream while it still reads the current one.")
+   "stream while it still reads the current one. Off by default: one stream cached +2.5%, cold -15% on "
+   "the same box (the next block's read-through competes with the current one; "
+   "profiles/r6_next_block_start_ab.jsonl).")
 _k("WORKER_IPC_ENABLED", "alluxio.worker.ipc.enabled", "true", Scope.WORKER,
    "Hand out HIP IPC handles for short-circuit reads of HBM pages.")
 _k("WORKER_STAGING_BUFFER_SIZE", "alluxio.worker.staging.buffer.size", "64MB", Scope.WORKER,

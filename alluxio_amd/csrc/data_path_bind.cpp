@@ -110,7 +110,7 @@ struct PyInStream {
   // cold block the worker's first UFS reads -- are under way when the reader gets there).
   int64_t next_idx = -1;
   std::shared_ptr<BlockSource> next_src;
-  bool start_next_enabled = true;
+  bool start_next_enabled = false;   // alluxio.user.native.reader.next.block.start.enabled
 
   void open_block(int64_t idx, bool failed) {
     if (!failed && idx == next_idx && next_src) {
@@ -446,7 +446,7 @@ void bind_data_path(py::module_& m) {
              return p;
            }),
            py::arg("length"), py::arg("block_size"), py::arg("chunk"), py::arg("opener"), py::arg("prefetch") = true,
-           py::arg("start_next") = true)
+           py::arg("start_next") = false)
       .def_property("pos", [](const PyInStream& s) { return s.s.pos(); },
                     [](PyInStream& s, uint64_t p) { s.s.seek(p); })
       .def_property_readonly("length", [](const PyInStream& s) { return s.s.length(); })
