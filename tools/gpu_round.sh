@@ -366,6 +366,12 @@ for s in $STEPS; do
         run cached_ns_$ns 300 python tools/remote_device_read_bench.py --uds --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=1 --client-prop alluxio.user.native.reader.next.block.start.enabled=$ns --out "$OUT/r6_next_block_start_ab.jsonl"
       done
       ;;
+    r6wsize)
+      # is the 16-writer ceiling the client's per-call cost? the same writes with larger write() calls
+      for ws in 1m 4m 16m; do
+        run ww_ws_$ws 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --write-size $ws --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --out "$OUT/r6_write_size.jsonl"
+      done
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
