@@ -886,9 +886,9 @@ class GrpcBlockWriter(BlockWriter):
         self._t.start()
 
     def write_ptr(self, offset, ptr, length, kind):
-        import ctypes
         if self._sink is not None:
             from ..ops.native import native_errors
+            from ..utils import optiming
             keep = None
             if kind == DEVICE:
                 import torch
@@ -897,8 +897,11 @@ class GrpcBlockWriter(BlockWriter):
                 lib().batched_copy([(ptr, tmp.data_ptr(), length)], 0)
                 keep = tmp.cpu()
                 ptr = keep.data_ptr()
+            t0 = time.perf_counter() if optiming.ENABLED else 0.0
             with native_errors():
                 self._sink.write_ptr(ptr, length)
+            if optiming.ENABLED:
+                optiming.add("client.sink_write", time.perf_counter() - t0)
             return
         if kind == DEVICE:
             import torch

@@ -61,7 +61,9 @@ def run(t):
             left = size
             while left > 0:
                 n = min(wsize, left)
+                w0 = clk()
                 f.write(data[:n])
+                optiming.add("bench.write_call", clk() - w0)
                 left -= n
                 done[t] += n
             c3 = clk()
