@@ -185,6 +185,9 @@ _k("USER_NATIVE_READER_NEXT_BLOCK_START", "alluxio.user.native.reader.next.block
    "stream while it still reads the current one. Off by default: one stream cached +2.5%, cold -15% on "
    "the same box (the next block's read-through competes with the current one; "
    "profiles/r6_next_block_start_ab.jsonl).")
+_k("WORKER_DATA_SERVER_NATIVE_WRITE_WINDOW", "alluxio.worker.data.server.native.write.window", "4MB",
+   Scope.WORKER, "HTTP/2 stream window of request streams on the native data server (WriteBlock uploads): "
+   "how many bytes a writer may have in flight before the worker has taken them.")
 _k("WORKER_IPC_ENABLED", "alluxio.worker.ipc.enabled", "true", Scope.WORKER,
    "Hand out HIP IPC handles for short-circuit reads of HBM pages.")
 _k("WORKER_STAGING_BUFFER_SIZE", "alluxio.worker.staging.buffer.size", "64MB", Scope.WORKER,

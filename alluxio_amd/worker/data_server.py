@@ -50,7 +50,8 @@ class WorkerDataServer:
             services={SVC_BLOCK_WORKER}, bridge_services={SVC_BLOCK_WORKER},
             stream_threads=conf.get_int("alluxio.worker.data.server.native.stream.threads", "128"))
         # request streams (WriteBlock uploads) get a window of a few chunks
-        lib().set_stream_window(self.frontend.server, 4 << 20)
+        lib().set_stream_window(self.frontend.server,
+                                conf.get_bytes("alluxio.worker.data.server.native.write.window", "4MB"))
         if domain_socket:
             # the domain-socket data server (same-node clients skip TCP): same service, same port
             import os

@@ -376,6 +376,13 @@ for s in $STEPS; do
       # 16 writers x 1 MiB: one write() call's time against the native sink call inside it
       run ww_call 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 6 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --client-timing "$OUT/r6_wcall" --out "$OUT/r6_wcall.jsonl"
       ;;
+    r6wwin)
+      # 16 writers x 1 MiB with larger HTTP/2 stream windows on the data server
+      for win in 4MB 16MB 32MB; do
+        run ww_win_$win 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.data.server.native.write.window=$win --out "$OUT/r6_write_window.jsonl"
+      done
+      run ww_win_uds16 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.native.write.window=16MB --out "$OUT/r6_write_window.jsonl"
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
