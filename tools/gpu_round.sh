@@ -383,6 +383,13 @@ for s in $STEPS; do
       done
       run ww_win_uds16 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.native.write.window=16MB --out "$OUT/r6_write_window.jsonl"
       ;;
+    r6wwin2)
+      for rep in 1 2; do
+        for win in 4MB 32MB 64MB; do
+          run ww_win2_${win}_$rep 300 python tools/worker_write_bench.py --threads 16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --worker-prop alluxio.worker.data.server.native.write.window=$win --out "$OUT/r6_write_window2.jsonl"
+        done
+      done
+      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
