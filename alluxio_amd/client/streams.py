@@ -860,12 +860,9 @@ class GrpcBlockWriter(BlockWriter):
                 call = _native_call(ctx, address, data_address)
                 if call is not None:
                     host, port, cid, user, timeout, uds = call
-                    # buffered: write() returns once the bytes are copied and what the socket takes
-                    # now is sent; the next write (or the commit) sends the rest
-                    buffered = ctx.conf.get_bool("alluxio.user.native.writer.buffered.enabled", "true")
                     with native_errors():
                         self._sink = lib().GrpcBlockSink(host, port, block_id, tier, medium, reserve, pin,
-                                                         self.chunk, cid, user, timeout, uds, buffered=buffered)
+                                                         self.chunk, cid, user, timeout, uds)
                     return
         cmd = pb.block.WriteRequestCommand(type=0, id=block_id, offset=0, tier=tier, medium_type=medium,
                                            space_to_reserve=reserve, pin_on_create=pin)

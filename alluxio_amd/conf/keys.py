@@ -188,10 +188,6 @@ _k("USER_NATIVE_READER_NEXT_BLOCK_START", "alluxio.user.native.reader.next.block
 _k("WORKER_DATA_SERVER_NATIVE_WRITE_WINDOW", "alluxio.worker.data.server.native.write.window", "4MB",
    Scope.WORKER, "HTTP/2 stream window of request streams on the native data server (WriteBlock uploads): "
    "how many bytes a writer may have in flight before the worker has taken them.")
-_k("USER_NATIVE_WRITER_BUFFERED", "alluxio.user.native.writer.buffered.enabled", "true", Scope.CLIENT,
-   "Native WriteBlock streams copy each write() and return once the socket has taken what it can "
-   "without waiting (at most 4 MiB left pending): the stream keeps moving while the caller prepares "
-   "its next write.")
 _k("WORKER_IPC_ENABLED", "alluxio.worker.ipc.enabled", "true", Scope.WORKER,
    "Hand out HIP IPC handles for short-circuit reads of HBM pages.")
 _k("WORKER_STAGING_BUFFER_SIZE", "alluxio.worker.staging.buffer.size", "64MB", Scope.WORKER,

@@ -801,14 +801,10 @@ void GrpcBlockSource::maybe_ack(uint64_t offset) {
 struct GrpcBlockSink::Conn {
   struct Seg {
     std::string hdr;               // gRPC prefix + WriteRequest/Chunk headers (or a whole message)
-    const uint8_t* data = nullptr; // caller bytes (valid until write() returns), or `own`'s
+    const uint8_t* data = nullptr; // caller bytes (valid until write() returns)
     size_t len = 0;
     size_t off = 0;                // over hdr then data
-    std::string own;               // a copy of the caller's bytes (buffered writes)
   };
-  size_t unframed = 0;             // bytes queued in q that read_req has not framed yet
-  std::string out;                 // framed bytes the socket did not take yet (non-blocking sends)
-  size_t out_off = 0;
   int fd = -1;
   void* ng = nullptr;
   int32_t sid = -1;
@@ -873,7 +869,6 @@ struct GrpcBlockSink::Conn {
       w += n;
       if (s.off == s.hdr.size() + s.len) c.q.pop_front();
     }
-    c.unframed -= std::min(c.unframed, w);
     if (c.q.empty() && c.closing) {
       *flags |= h2::kDataEof;      // END_STREAM: the request stream is complete
       return (ssize_t)w;
@@ -894,75 +889,8 @@ struct GrpcBlockSink::Conn {
     }();
     return cbs;
   }
-  // Sends what the socket takes right now; false when it would block (the rest waits in `out`).
-  bool send_nowait() {
-    const h2::Lib& g = h2::lib();
-    for (;;) {
-      while (out_off < out.size()) {
-        const ssize_t w = ::send(fd, out.data() + out_off, out.size() - out_off, MSG_NOSIGNAL | MSG_DONTWAIT);
-        if (w > 0) {
-          out_off += (size_t)w;
-          continue;
-        }
-        if (w < 0 && errno == EINTR) continue;
-        if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return false;
-        throw std::runtime_error("gRPC client: connection lost while sending");
-      }
-      out.clear();
-      out_off = 0;
-      const uint8_t* d = nullptr;
-      const ssize_t n = g.mem_send(ng, &d);
-      if (n < 0) throw std::runtime_error("gRPC client: HTTP/2 framing error");
-      if (n == 0) return true;
-      size_t off = 0;
-      while (off < (size_t)n) {
-        const ssize_t w = ::send(fd, d + off, (size_t)n - off, MSG_NOSIGNAL | MSG_DONTWAIT);
-        if (w > 0) {
-          off += (size_t)w;
-          continue;
-        }
-        if (w < 0 && errno == EINTR) continue;
-        if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-          out.assign(reinterpret_cast<const char*>(d) + off, (size_t)n - off);   // nghttp2 reuses d
-          return false;
-        }
-        throw std::runtime_error("gRPC client: connection lost while sending");
-      }
-    }
-  }
-  // Takes what has arrived (WINDOW_UPDATEs, an early failure) without waiting.
-  void recv_nowait() {
-    if (inbuf.size() < (256u << 10)) inbuf.resize(256u << 10);
-    for (;;) {
-      const ssize_t got = ::recv(fd, &inbuf[0], inbuf.size(), MSG_DONTWAIT);
-      if (got == 0) throw std::runtime_error("gRPC client: connection closed by the worker");
-      if (got < 0) {
-        if (errno == EINTR) continue;
-        if (errno == EAGAIN || errno == EWOULDBLOCK) return;
-        throw std::runtime_error("gRPC client: connection lost");
-      }
-      if (h2::lib().mem_recv(ng, reinterpret_cast<const uint8_t*>(inbuf.data()), (size_t)got) < 0)
-        throw std::runtime_error("gRPC client: malformed WriteBlock response stream");
-    }
-  }
   void send_pending(int timeout_ms) {
     const h2::Lib& g = h2::lib();
-    while (out_off < out.size()) {     // first what a non-blocking send left behind
-      const ssize_t w = ::send(fd, out.data() + out_off, out.size() - out_off, MSG_NOSIGNAL);
-      if (w > 0) {
-        out_off += (size_t)w;
-        continue;
-      }
-      if (w < 0 && errno == EINTR) continue;
-      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-        pollfd pf{fd, POLLOUT, 0};
-        if (::poll(&pf, 1, timeout_ms) <= 0) throw std::runtime_error("gRPC client: send timed out");
-        continue;
-      }
-      throw std::runtime_error("gRPC client: connection lost while sending");
-    }
-    out.clear();
-    out_off = 0;
     for (;;) {
       const uint8_t* d = nullptr;
       const ssize_t n = g.mem_send(ng, &d);
@@ -1092,10 +1020,6 @@ void GrpcBlockSink::wait_drained() {
 void GrpcBlockSink::write(const uint8_t* p, uint64_t n) {
   if (!c_ || c_->closing) throw StoreError(kErrInvalidState, "write after commit/cancel");
   Conn& c = *c_;
-  // Buffered: the bytes are copied and the call returns once what the socket takes now is sent,
-  // unless more than kMaxBuffered is still waiting -- the next call (or the commit) sends the
-  // rest, so the stream keeps moving while the caller prepares its next write.
-  const bool buffered = o_.buffered && n <= kMaxBuffered;
   uint64_t off = 0;
   while (off < n) {
     const size_t k = (size_t)std::min<uint64_t>(o_.chunk, n - off);
@@ -1111,36 +1035,13 @@ void GrpcBlockSink::write(const uint8_t* p, uint64_t n) {
     h2::put_be32(s.hdr, (uint32_t)(outer.size() + inner.size() + k));
     s.hdr += outer;
     s.hdr += inner;
-    if (buffered) s.own.assign(reinterpret_cast<const char*>(p + off), k);
-    else s.data = p + off;
+    s.data = p + off;
     s.len = k;
-    c.unframed += s.hdr.size() + k;
     c.q.push_back(std::move(s));
-    // the copy's address once it sits in the deque (a moved short string changes address;
-    // deque elements stay where they are while others are added at the back)
-    if (buffered) c.q.back().data = reinterpret_cast<const uint8_t*>(c.q.back().own.data());
     off += k;
   }
-  if (!buffered) {
-    wait_drained();                      // the caller's bytes are in HTTP/2 frames from here on
-    written_ += n;
-    return;
-  }
+  wait_drained();                        // the caller's bytes are in HTTP/2 frames from here on
   written_ += n;
-  c.recv_nowait();                       // WINDOW_UPDATEs that arrived meanwhile
-  h2::lib().resume_data(c.ng, c.sid);
-  c.send_nowait();
-  if (c.closed && c.grpc_status > 0) wait_drained();   // throws the worker's failure
-  while (c.unframed > kMaxBuffered || c.out.size() - c.out_off > kMaxBuffered) {
-    if (c.closed) {
-      wait_drained();
-      break;
-    }
-    if (!c.pump(o_.timeout_ms))
-      throw StoreError(kErrTimeout, "WriteBlock of block " + std::to_string(o_.block_id) + " timed out");
-    h2::lib().resume_data(c.ng, c.sid);
-    c.send_nowait();
-  }
 }
 
 void GrpcBlockSink::append_block(int64_t block_id, uint64_t length) {

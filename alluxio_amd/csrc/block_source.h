@@ -171,15 +171,10 @@ class GrpcBlockSink {
     // A serialized WriteRequestCommand sent instead of the ALLUXIO_BLOCK one built from the
     // fields above (e.g. a UFS_FILE write to the worker's UFS).
     std::string command;
-    // write() copies the caller's bytes and returns before they are all sent (up to
-    // kMaxBuffered waiting): the stream keeps moving while the caller prepares the next write.
-    bool buffered = false;
   };
-  static constexpr uint64_t kMaxBuffered = 4u << 20;
   explicit GrpcBlockSink(Options o);
   ~GrpcBlockSink();
-  // Streams n bytes; returns once they are in the socket (flow control permitting), or -- with
-  // Options::buffered -- once they are copied and what the socket takes now is sent.
+  // Streams n bytes; returns once they are in the socket (flow control permitting).
   void write(const uint8_t* p, uint64_t n);
   // UFS_FILE streams: the next `length` bytes of the file are block `block_id`, which the same
   // worker already holds (CACHE_THROUGH tee: the worker copies them from its store).

@@ -343,9 +343,8 @@ void bind_data_path(py::module_& m) {
       .def(py::init([](const std::string& host, int port, int64_t block_id, int tier, const std::string& medium,
                        uint64_t reserve, bool pin, uint64_t chunk, const std::string& channel_id,
                        const std::string& user, int timeout_ms, const std::string& unix_path,
-                       const py::bytes& command, bool buffered) {
+                       const py::bytes& command) {
              GrpcBlockSink::Options o;
-             o.buffered = buffered;
              o.host = host;
              o.port = port;
              o.unix_path = unix_path;
@@ -371,7 +370,7 @@ void bind_data_path(py::module_& m) {
            py::arg("host"), py::arg("port"), py::arg("block_id"), py::arg("tier") = 0, py::arg("medium") = "",
            py::arg("reserve") = 1u << 20, py::arg("pin") = false, py::arg("chunk") = 1u << 20,
            py::arg("channel_id") = "", py::arg("user") = "", py::arg("timeout_ms") = 60000,
-           py::arg("unix_path") = "", py::arg("command") = py::bytes(""), py::arg("buffered") = false)
+           py::arg("unix_path") = "", py::arg("command") = py::bytes(""))
       .def("write_ptr", [](GrpcBlockSink& s, uint64_t ptr, uint64_t n) {
              py::gil_scoped_release rel;
              try {

@@ -390,13 +390,6 @@ for s in $STEPS; do
         done
       done
       ;;
-    r6wbuf)
-      # buffered native writes (the default) against the synchronous ones, same box
-      for b in true false; do
-        run ww_buf_mc_$b 400 python tools/worker_write_bench.py --threads 1,16 --files 4 --min-seconds 8 --file-size 256m --write-type MUST_CACHE --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --client-prop alluxio.user.native.writer.buffered.enabled=$b --out "$OUT/r6_write_buffered.jsonl"
-        run ww_buf_ct_$b 400 python tools/worker_write_bench.py --threads 1,16 --files 4 --min-seconds 8 --file-size 256m --write-type CACHE_THROUGH --worker-prop alluxio.worker.data.server.domain.socket.default.enabled=false --client-prop alluxio.user.native.writer.buffered.enabled=$b --out "$OUT/r6_write_buffered.jsonl"
-      done
-      ;;
     r6final)
       # the round's closing numbers on one box: tests, smoke, driver-shape bench, writes, stress, cold, fan-out
       run pytest_gpu_final6 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
