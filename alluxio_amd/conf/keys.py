@@ -257,6 +257,11 @@ _k("WORKER_DATA_SERVER_NATIVE_UFS_READ_ENABLED", "alluxio.worker.data.server.nat
    "into a temp block and the I/O thread streams it as it lands; the block is committed at the end.")
 _k("WORKER_DATA_SERVER_NATIVE_UFS_READ_MAX_ACTIVE", "alluxio.worker.data.server.native.ufs.read.max.active",
    "256", Scope.WORKER, "Concurrent native cold reads (one UFS reader thread each); more go to Python.")
+_k("WORKER_DATA_SERVER_NATIVE_UFS_READAHEAD_ENABLED", "alluxio.worker.data.server.native.ufs.readahead.enabled",
+   "true", Scope.WORKER, "A native whole-block read-through reads the first two UFS reads of the file's next "
+   "block (one chunk, then one alluxio.worker.ufs.ingest.chunk.size slot) into pinned buffers once its own "
+   "reads are done; the next block's cold stream sends them without waiting on the UFS. Pieces expire "
+   "after 5 s.")
 _k("USER_FILE_CACHE_THROUGH_TEE_ENABLED", "alluxio.user.file.cache.through.tee.enabled", "true", Scope.CLIENT,
    "CACHE_THROUGH writes whose cache block and UFS file stream go to the same worker send each byte "
    "once (to the block stream); after the block commits, the UFS stream is told to append it and the "

@@ -23,6 +23,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "h2_abi.h"
@@ -810,6 +811,86 @@ struct ColdState {
   }
 };
 
+// Next-block read-ahead of the native cold path.  A whole-block read-through that reached the end
+// of its block reads the first two UFS reads of the file's next block (one chunk, then a slot) into
+// pinned buffers of its slot pool once its own reads are done; the next block's cold stream adopts
+// them as its first two slots, so its first bytes go out without waiting on the UFS.  One client
+// stream reads one block at a time, so without it every block of a sequential cold read pays the
+// UFS latency before its first byte (profiles/r6_cold_read.md).  Pieces are matched by
+// (mount, path, file offset, length), expire after kTtl and are bounded to kMaxPieces per server.
+class ColdReadAhead {
+ public:
+  static constexpr size_t kMaxPieces = 32;
+  static constexpr std::chrono::milliseconds kTtl{5000};
+  ~ColdReadAhead() {
+    for (auto& p : pieces_) p.pool->put(p.buf);
+  }
+  void put(const std::string& key, std::shared_ptr<StagingPool> pool, uint64_t off, uint64_t len, uint8_t* buf) {
+    std::vector<Piece> drop;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      expire_locked(&drop);
+      if (pieces_.size() >= kMaxPieces) {
+        drop.push_back(pieces_.front());
+        pieces_.pop_front();
+      }
+      pieces_.push_back({key, std::move(pool), off, len, buf, std::chrono::steady_clock::now()});
+    }
+    for (auto& p : drop) p.pool->put(p.buf);
+  }
+  // The buffer holding exactly [off, off + len) of `key` from `pool`, now the caller's, or null.
+  uint8_t* take(const std::string& key, const StagingPool* pool, uint64_t off, uint64_t len) {
+    std::vector<Piece> drop;
+    uint8_t* got = nullptr;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      expire_locked(&drop);
+      for (auto it = pieces_.begin(); it != pieces_.end(); ++it)
+        if (it->off == off && it->len == len && it->pool.get() == pool && it->key == key) {
+          got = it->buf;
+          pieces_.erase(it);
+          break;
+        }
+    }
+    for (auto& p : drop) p.pool->put(p.buf);
+    return got;
+  }
+  // Blocks with a cold stream under way: a stream never reads ahead a block another stream reads
+  // (a client reading several blocks at once opens the next one before the current one ends).
+  void begin(int64_t block) {
+    std::lock_guard<std::mutex> g(mu_);
+    ++active_[block];
+  }
+  void end(int64_t block) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = active_.find(block);
+    if (it != active_.end() && --it->second <= 0) active_.erase(it);
+  }
+  bool active(int64_t block) {
+    std::lock_guard<std::mutex> g(mu_);
+    return active_.count(block) != 0;
+  }
+
+ private:
+  struct Piece {
+    std::string key;
+    std::shared_ptr<StagingPool> pool;
+    uint64_t off, len;
+    uint8_t* buf;
+    std::chrono::steady_clock::time_point at;
+  };
+  void expire_locked(std::vector<Piece>* drop) {
+    const auto now = std::chrono::steady_clock::now();
+    while (!pieces_.empty() && now - pieces_.front().at > kTtl) {
+      drop->push_back(pieces_.front());
+      pieces_.pop_front();
+    }
+  }
+  std::mutex mu_;
+  std::deque<Piece> pieces_;
+  std::unordered_map<int64_t, int> active_;
+};
+
 struct ColdJob {
   StoreRef store;
   int64_t session, block;
@@ -826,6 +907,9 @@ struct ColdJob {
   // to the worker) and opens the reader; false with *status / *err when it cannot be read natively.
   std::function<bool(std::unique_ptr<UfsReader>*, int*, std::string*)> resolve;
   std::chrono::steady_clock::time_point queued_at = std::chrono::steady_clock::now();
+  std::shared_ptr<ColdReadAhead> readahead;   // null: no next-block read-ahead (its stream registry too)
+  std::string ra_key;                         // "<mount id>:<ufs path>"
+  bool ra_next = false;                       // a whole-block read-through: read the next block ahead
 
   void wake() {
     std::function<void()> w;
@@ -869,6 +953,7 @@ struct ColdJob {
         store->cleanup_session(session);
       } catch (...) {
       }
+      if (readahead) readahead->end(block);
       stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
       wake();
       return;
@@ -909,12 +994,20 @@ struct ColdJob {
           dma_wait_ns += ns_since(td);
           sl->dma = false;
         }
+        // the previous block's stream may have read this one's first two reads ahead
+        uint8_t* pre = readahead && idx < 2 ? readahead->take(ra_key, st->pool.get(), file_off + off, n) : nullptr;
         if (!sl->buf) {
-          sl->buf = st->pool->get();
+          sl->buf = pre ? pre : st->pool->get();
           if (hs && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) sl->ev = nullptr;
         }
         const auto tr = clk::now();
-        if (!reader->read(file_off + off, n, sl->buf, &err)) {
+        if (pre) {
+          if (sl->buf != pre) {
+            std::memcpy(sl->buf, pre, n);
+            st->pool->put(pre);
+          }
+          stats->cold_readahead_hits.fetch_add(1, std::memory_order_relaxed);
+        } else if (!reader->read(file_off + off, n, sl->buf, &err)) {
           ok = false;
           err_status = reader->status();
           break;
@@ -1026,8 +1119,39 @@ struct ColdJob {
       } catch (...) {
       }
     }
+    if (!cancelled) wake();   // the stream may end now: the read-ahead below is off its path
+    if (readahead) {
+      readahead->end(block);
+      // a client that went away after the last byte still read the block sequentially to its end
+      if (ra_next && complete) read_ahead_next();
+    }
     stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
-    if (!cancelled) wake();
+  }
+
+  // The next block's first two reads (see ColdReadAhead), unless the store has that block.  A
+  // read past the end of the file (this was its last block) fails and leaves nothing.
+  void read_ahead_next() {
+    const int64_t next = block + 1;   // BlockId: container << 24 | sequence, the file's next block
+    try {
+      if (readahead->active(next) || store->has_block(next) || store->has_temp_block(next)) return;
+    } catch (...) {
+      return;
+    }
+    const uint64_t base = file_off + block_len;
+    const uint64_t first = first_bytes ? std::min(first_bytes, slot_bytes) : slot_bytes;
+    const uint64_t sizes[2] = {first, slot_bytes};
+    uint64_t off = base;
+    for (int i = 0; i < 2; ++i) {
+      uint8_t* buf = st->pool->get();
+      std::string err;
+      if (!reader->read(off, sizes[i], buf, &err)) {
+        st->pool->put(buf);
+        return;
+      }
+      stats->cold_readahead_bytes.fetch_add(sizes[i], std::memory_order_relaxed);
+      readahead->put(ra_key, st->pool, off, sizes[i], buf);
+      off += sizes[i];
+    }
   }
 };
 
@@ -3138,7 +3262,8 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
                                                std::function<void(uint32_t, std::string)> post, int* status,
                                                std::string* msg,
                                                const std::shared_ptr<BlockCommitter>& committer = nullptr,
-                                               BlockCommitter::Caller caller = nullptr) {
+                                               BlockCommitter::Caller caller = nullptr,
+                                               const std::shared_ptr<ColdReadAhead>& readahead = nullptr) {
   UfsOpts o;
   if (!mounts || !parse_ufs_opts(r.ufs_opts, &o) || o.ufs_path.empty() || o.block_in_ufs_tier || o.block_size <= 0)
     return nullptr;
@@ -3242,13 +3367,20 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
   job->commit_method = cfg.commit_method;
   job->committer = committer;
   job->resolve = std::move(resolve);
+  if (readahead) {
+    job->readahead = readahead;
+    job->ra_key = std::to_string(o.mount_id) + ":" + o.ufs_path;
+    job->ra_next = cache;     // a whole-block read-through: a sequential reader's next block follows
+  }
   const uint64_t chunk =
       r.chunk_size > 0 ? std::min<uint64_t>((uint64_t)r.chunk_size, max_chunk) : std::min<uint64_t>(1u << 20, max_chunk);
   job->first_bytes = std::min<uint64_t>(chunk, job->slot_bytes);   // the first chunk goes after one small read
   std::unique_ptr<NativeStream> ns(new ColdReadStream(store, job->session, r.block_id, off, end, chunk, window,
                                                       slot_pool->size(), job->first_bytes, unix_peer, st, stats));
   stats->cold_streams.fetch_add(1, std::memory_order_relaxed);
+  if (readahead) readahead->begin(r.block_id);
   if (!ColdPool::get().submit([job] { job->run(); }, cfg.max_active)) {
+    if (readahead) readahead->end(r.block_id);
     stats->cold_active.fetch_sub(1, std::memory_order_relaxed);
     *status = 8;
     *msg = "cannot start a UFS reader thread";
@@ -3677,6 +3809,7 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uin
   if (cold.slot_bytes == 0) cold.slot_bytes = 8u << 20;
   auto pool = std::make_shared<StagingPool>(max_chunk, store->has_device(), store->device());
   auto slot_pool = std::make_shared<StagingPool>(cold.slot_bytes, store->has_device(), store->device());
+  auto readahead = cold.readahead ? std::make_shared<ColdReadAhead>() : nullptr;
   FrameRpcServer* s = &srv;
   srv.set_native_stream(method, [=](const std::string& first, const std::string& cid, const std::string& user,
                                     bool unix_peer, int* status, std::string* msg) -> std::unique_ptr<NativeStream> {
@@ -3736,7 +3869,8 @@ void serve_block_reads(FrameRpcServer& srv, uint32_t method, StoreRef store, uin
       if (committer && !committer->has_caller()) committer->set_caller(s->internal_caller(cid, user));
       auto cs = make_cold_stream(r, store, max_chunk, window, unix_peer, cold, mounts, slot_pool, stats,
                                  s->internal_poster(cid, user), status, msg, committer,
-                                 cold.resolve_method != UINT32_MAX ? s->internal_caller(cid, user) : nullptr);
+                                 cold.resolve_method != UINT32_MAX ? s->internal_caller(cid, user) : nullptr,
+                                 readahead);
       if (cs || *status != 0) return cs;
     }
     stats->declined.fetch_add(1, std::memory_order_relaxed);

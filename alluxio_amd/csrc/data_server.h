@@ -68,6 +68,8 @@ struct DataServerStats {
   // waiting for the stream to free a slot (consumer-bound), waiting for a slot's H2D
   std::atomic<uint64_t> cold_queue_ns{0}, cold_setup_ns{0}, cold_first_ns{0}, cold_read_ns{0},
       cold_slot_wait_ns{0}, cold_dma_wait_ns{0};
+  std::atomic<uint64_t> cold_readahead_bytes{0};   // next-block bytes read ahead by finished read-throughs
+  std::atomic<uint64_t> cold_readahead_hits{0};    // UFS reads of cold streams served by those bytes
   // The send side of ReadBlock streams, [0] cached (HBM staging) and [1] cold: streams finished,
   // ns from the call's start to its last byte and to its first, and the gaps in which the stream
   // had nothing to send -- the client's ack window was full, or the next bytes were not there yet
@@ -192,6 +194,9 @@ struct ColdReadConfig {
   // reader's pool thread, then reads natively -- no first read of a mount goes through Python
   uint32_t resolve_method = UINT32_MAX;
   uint32_t read_range_method = UINT32_MAX;   // internal ReadUfsRange (a resolved mount that is Python's)
+  // a whole-block read-through reads the file's next block's first two reads ahead once its own
+  // reads are done (alluxio.worker.data.server.native.ufs.readahead.enabled)
+  bool readahead = true;
 };
 
 // Serve `method` (the ReadBlock path's index) of `srv` from `store`.  `max_chunk` caps a client's

@@ -720,6 +720,64 @@ def test_native_cold_read_through(tmp_path):
             fs.close()
 
 
+def test_native_cold_read_ahead_of_next_block(tmp_path):
+    """A whole-block read-through reads the file's next block's first two UFS reads ahead once its
+    own reads are done; the next block's cold stream sends those bytes (byte-exact) instead of
+    reading the UFS.  A block the store already holds is not read ahead; the last block's read-ahead
+    (past the end of the file) leaves nothing; with the key off nothing is read ahead."""
+    extra = {"alluxio.worker.ufs.ingest.chunk.size": "1MB", "alluxio.worker.ufs.ingest.depth": "2",
+             "alluxio.worker.network.reader.buffer.size": "1MB"}
+    for enabled in (True, False):
+        with _cluster(tmp_path / str(enabled), dict(
+                extra, **{"alluxio.worker.data.server.native.ufs.readahead.enabled": str(enabled).lower()})) as c:
+            fs = c.client()
+            data = np.random.default_rng(31).integers(0, 256, (4 << 22) + 777, dtype=np.uint8)
+            fs.write_file("/ra/f", data, write_type="CACHE_THROUGH")
+            fs.free("/ra", recursive=True)
+            w = c.workers[0]
+            c.heartbeat_workers()
+            st = w.data_server.stats
+            rfs = _remote_fs(c)
+            try:
+                blocks = _blocks(rfs, "/ra/f")
+                assert len(blocks) == 5
+                # block 2 is cached already: block 1's stream does not read it ahead
+                with rfs.open_file("/ra/f") as f:
+                    f.seek(2 << 22)
+                    assert f.read(4 << 20) == data[2 << 22:3 << 22].tobytes()
+                deadline = time.time() + 10
+                while not w.worker.has_block(blocks[2][0]) or st.cold_active:   # its read-ahead done too
+                    assert time.time() < deadline
+                    time.sleep(0.02)
+                h0, b0, c0 = st.cold_readahead_hits, st.cold_readahead_bytes, st.cold_bytes
+                assert b0 == (2 << 20 if enabled else 0)        # block 2 read block 3's first two reads
+                got = b""
+                with rfs.open_file("/ra/f") as f:
+                    for _ in blocks:                  # one block at a time, the read-ahead lands between
+                        got += f.read(4 << 20)
+                        while st.cold_active:
+                            time.sleep(0.01)
+                        time.sleep(0.1)
+                assert got == data.tobytes()
+                hits, ahead = st.cold_readahead_hits - h0, st.cold_readahead_bytes - b0
+                if enabled:
+                    # blocks 1 and 3 start from read-ahead bytes: block 0 reads block 1's first two
+                    # reads ahead, block 3 block 4's (777 bytes: shorter than one chunk, nothing);
+                    # block 1 skips the cached block 2
+                    assert hits == 4 and ahead == 2 << 20
+                else:
+                    assert hits == 0 and ahead == 0
+                assert st.cold_bytes - c0 == data.nbytes - (4 << 20)   # every streamed byte counted once
+                deadline = time.time() + 10
+                while not all(w.worker.has_block(b) for b, _ in blocks):
+                    assert time.time() < deadline
+                    time.sleep(0.02)
+                assert rfs.read_file("/ra/f") == data.tobytes()
+            finally:
+                rfs.close()
+                fs.close()
+
+
 def test_native_cold_read_through_s3(tmp_path):
     """Cold blocks of an S3 mount (native BlobServer endpoint) are read through by the data server's
     own signed ranged GETs once the first read in Python registered the mount."""

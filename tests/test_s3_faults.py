@@ -162,7 +162,9 @@ def test_native_cold_read_retries_and_stalls(blob, tmp_path):
     for k, d in objs.items():
         _put(base, "ds/" + k, d)
     # one block per object and one GET per read (no sub-range split): the Nth GET is the Nth read
-    c, fs = _s3_cluster(tmp_path, base, cluster_conf={"alluxio.user.block.size.bytes.default": "32MB"},
+    # (no next-block read-ahead, which would add GETs past each object's end)
+    c, fs = _s3_cluster(tmp_path, base, cluster_conf={"alluxio.user.block.size.bytes.default": "32MB",
+                                                      "alluxio.worker.data.server.native.ufs.readahead.enabled": "false"},
                         **{"alluxio.underfs.s3.threads.max": "1"})
     rfs = _remote_fs(c)
     try:

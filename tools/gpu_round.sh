@@ -408,6 +408,20 @@ for s in $STEPS; do
       # replica fan-out breakdown: 8 ranks (8 workers) on the one GPU, 3 replicas per block
       run bench_rehearse_8rank_r6 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --profile-json "$OUT/r6_rehearse_8rank.json"
       ;;
+    r6ra)
+      # next-block read-ahead A/B/A/B (cold, one stream and four) plus the cached rows, same box
+      RA=alluxio.worker.data.server.native.ufs.readahead.enabled
+      for rep in 1 2; do
+        for ra in true false; do
+          for par in 1 4; do
+            run cold_ra${ra}_p${par}_$rep 300 python tools/remote_device_read_bench.py --uds --cold --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --worker-prop $RA=$ra --out "$OUT/r6_cold_readahead_ab.jsonl"
+          done
+        done
+      done
+      for par in 1 4; do
+        run cached_p$par 300 python tools/remote_device_read_bench.py --uds --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/r6_cold_readahead_ab.jsonl"
+      done
+      ;;
     r6cold)
       # cold read-through vs cached, one ReadBlock stream at a time and four, host destination (UDS default)
       for par in 1 4; do

@@ -132,7 +132,8 @@ def main(argv=None) -> int:
             ds = c.workers[0].data_server
             st0 = (ds.stats.cold_streams, ds.stats.declined, ds.stats.cold_cached, ds.stats.zero_copy_frames,
                    ds.stats.prefetched, ds.stats.domain_bytes, ds.stats.cold_timing_ns,
-                   ds.stats.send_timing) if ds is not None else None
+                   ds.stats.send_timing, ds.stats.cold_readahead_hits,
+                   ds.stats.cold_readahead_bytes) if ds is not None else None
             props = {"alluxio.user.network.inprocess.transport.enabled": "false",
                      "alluxio.user.short.circuit.enabled": "false",
                      "alluxio.user.native.reader.enabled": str(native).lower(),
@@ -166,6 +167,9 @@ def main(argv=None) -> int:
                 row["worker_zero_copy_frames"] = ds.stats.zero_copy_frames - st0[3]
                 row["worker_prefetched_chunks"] = ds.stats.prefetched - st0[4]
                 row["worker_domain_socket_bytes"] = ds.stats.domain_bytes - st0[5]
+                # next-block read-ahead: cold-stream UFS reads served by bytes read ahead, and those bytes
+                row["worker_readahead_hits"] = ds.stats.cold_readahead_hits - st0[8]
+                row["worker_readahead_bytes"] = ds.stats.cold_readahead_bytes - st0[9]
                 # the send side per block stream (ms): call start -> first / last byte, and the gaps
                 # with nothing to send (ack window full / next bytes not there yet)
                 kind = "cold" if a.cold else "cached"
