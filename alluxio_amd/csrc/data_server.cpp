@@ -816,8 +816,9 @@ struct ColdState {
 // pinned buffers of its slot pool once its own reads are done; the next block's cold stream adopts
 // them as its first two slots, so its first bytes go out without waiting on the UFS.  One client
 // stream reads one block at a time, so without it every block of a sequential cold read pays the
-// UFS latency before its first byte (profiles/r6_cold_read.md).  Pieces are matched by
-// (mount, path, file offset, length), expire after kTtl and are bounded to kMaxPieces per server.
+// UFS latency before its first byte (profiles/r6_cold_read.md).  Pieces are matched by (block id,
+// mount, path, file offset, length) -- a file rewritten under the same path has new block ids, so
+// its reads never see the old bytes -- expire after kTtl and are bounded to kMaxPieces per server.
 class ColdReadAhead {
  public:
   static constexpr size_t kMaxPieces = 32;
@@ -825,7 +826,8 @@ class ColdReadAhead {
   ~ColdReadAhead() {
     for (auto& p : pieces_) p.pool->put(p.buf);
   }
-  void put(const std::string& key, std::shared_ptr<StagingPool> pool, uint64_t off, uint64_t len, uint8_t* buf) {
+  void put(int64_t block, const std::string& key, std::shared_ptr<StagingPool> pool, uint64_t off, uint64_t len,
+           uint8_t* buf) {
     std::vector<Piece> drop;
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -834,19 +836,20 @@ class ColdReadAhead {
         drop.push_back(pieces_.front());
         pieces_.pop_front();
       }
-      pieces_.push_back({key, std::move(pool), off, len, buf, std::chrono::steady_clock::now()});
+      pieces_.push_back({block, key, std::move(pool), off, len, buf, std::chrono::steady_clock::now()});
     }
     for (auto& p : drop) p.pool->put(p.buf);
   }
-  // The buffer holding exactly [off, off + len) of `key` from `pool`, now the caller's, or null.
-  uint8_t* take(const std::string& key, const StagingPool* pool, uint64_t off, uint64_t len) {
+  // The buffer holding exactly [off, off + len) of block `block` of `key` from `pool`, now the
+  // caller's, or null.
+  uint8_t* take(int64_t block, const std::string& key, const StagingPool* pool, uint64_t off, uint64_t len) {
     std::vector<Piece> drop;
     uint8_t* got = nullptr;
     {
       std::lock_guard<std::mutex> g(mu_);
       expire_locked(&drop);
       for (auto it = pieces_.begin(); it != pieces_.end(); ++it)
-        if (it->off == off && it->len == len && it->pool.get() == pool && it->key == key) {
+        if (it->block == block && it->off == off && it->len == len && it->pool.get() == pool && it->key == key) {
           got = it->buf;
           pieces_.erase(it);
           break;
@@ -873,6 +876,7 @@ class ColdReadAhead {
 
  private:
   struct Piece {
+    int64_t block;
     std::string key;
     std::shared_ptr<StagingPool> pool;
     uint64_t off, len;
@@ -995,7 +999,7 @@ struct ColdJob {
           sl->dma = false;
         }
         // the previous block's stream may have read this one's first two reads ahead
-        uint8_t* pre = readahead && idx < 2 ? readahead->take(ra_key, st->pool.get(), file_off + off, n) : nullptr;
+        uint8_t* pre = readahead && idx < 2 ? readahead->take(block, ra_key, st->pool.get(), file_off + off, n) : nullptr;
         if (!sl->buf) {
           sl->buf = pre ? pre : st->pool->get();
           if (hs && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) sl->ev = nullptr;
@@ -1149,7 +1153,7 @@ struct ColdJob {
         return;
       }
       stats->cold_readahead_bytes.fetch_add(sizes[i], std::memory_order_relaxed);
-      readahead->put(ra_key, st->pool, off, sizes[i], buf);
+      readahead->put(next, ra_key, st->pool, off, sizes[i], buf);
       off += sizes[i];
     }
   }

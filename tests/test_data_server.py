@@ -773,6 +773,30 @@ def test_native_cold_read_ahead_of_next_block(tmp_path):
                     assert time.time() < deadline
                     time.sleep(0.02)
                 assert rfs.read_file("/ra/f") == data.tobytes()
+                if enabled:
+                    # a file rewritten under the same path has new block ids: the old file's
+                    # read-ahead bytes are never sent for it
+                    old = np.random.default_rng(32).integers(0, 256, 3 << 22, dtype=np.uint8)
+                    fs.write_file("/ra/g", old, write_type="CACHE_THROUGH")
+                    fs.free("/ra/g")
+                    c.heartbeat_workers()
+                    with rfs.open_file("/ra/g") as f:
+                        assert f.read(4 << 20) == old[:4 << 20].tobytes()
+                    while st.cold_active:
+                        time.sleep(0.01)
+                    b1, h1 = st.cold_readahead_bytes, st.cold_readahead_hits
+                    assert b1 > b0 + (2 << 20)          # block 1 of the old file was read ahead
+                    fs.delete("/ra/g")
+                    new = np.random.default_rng(33).integers(0, 256, 3 << 22, dtype=np.uint8)
+                    fs.write_file("/ra/g", new, write_type="CACHE_THROUGH")
+                    fs.free("/ra/g")
+                    c.heartbeat_workers()
+                    rfs.close()
+                    rfs = _remote_fs(c)
+                    with rfs.open_file("/ra/g") as f:
+                        f.seek(4 << 20)
+                        assert f.read(4 << 20) == new[4 << 20:8 << 20].tobytes()
+                    assert st.cold_readahead_hits == h1
             finally:
                 rfs.close()
                 fs.close()
