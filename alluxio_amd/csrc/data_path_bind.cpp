@@ -651,7 +651,8 @@ void bind_data_path(py::module_& m) {
                                 uint64_t window, std::shared_ptr<UfsMounts> mounts, uint32_t commit_method,
                                 uint64_t ufs_slot_bytes, int ufs_depth, int ufs_max_active,
                                 std::shared_ptr<DataServerStats> stats, std::shared_ptr<BlockCommitter> committer,
-                                uint32_t resolve_method, uint32_t read_range_method, bool ufs_readahead) {
+                                uint32_t resolve_method, uint32_t read_range_method, bool ufs_readahead,
+                                int ufs_create_after_reads) {
           if (!stats) stats = std::make_shared<DataServerStats>();
           ColdReadConfig cold;
           cold.commit_method = commit_method;
@@ -661,13 +662,15 @@ void bind_data_path(py::module_& m) {
           cold.depth = ufs_depth;
           cold.max_active = ufs_max_active;
           cold.readahead = ufs_readahead;
+          cold.create_after_reads = ufs_create_after_reads;
           serve_block_reads(srv, method, store, max_chunk, window, stats, mounts, cold, committer);
           return stats;
         }, py::arg("server"), py::arg("method"), py::arg("store"), py::arg("max_chunk"), py::arg("window"),
         py::arg("mounts") = nullptr, py::arg("commit_method") = UINT32_MAX, py::arg("ufs_slot_bytes") = 8u << 20,
         py::arg("ufs_depth") = 3, py::arg("ufs_max_active") = 256, py::arg("stats") = nullptr,
         py::arg("committer") = nullptr, py::arg("resolve_method") = UINT32_MAX,
-        py::arg("read_range_method") = UINT32_MAX, py::arg("ufs_readahead") = true, py::keep_alive<1, 3>());
+        py::arg("read_range_method") = UINT32_MAX, py::arg("ufs_readahead") = true,
+        py::arg("ufs_create_after_reads") = 0, py::keep_alive<1, 3>());
   m.def("serve_block_writes", [](FrameRpcServer& srv, uint32_t method, uint32_t commit_method, std::shared_ptr<BlockStore> store,
                                  uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
                                  std::shared_ptr<UfsMounts> ufs_roots, std::shared_ptr<BlockCommitter> committer) {

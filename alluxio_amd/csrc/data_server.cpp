@@ -900,6 +900,7 @@ struct ColdJob {
   int64_t session, block;
   uint64_t start, end, block_len, file_off, slot_bytes;
   uint64_t first_bytes = 0;     // the first read (<= slot_bytes; 0 = a whole slot)
+  size_t create_after = 2;      // reads before the temp block is created (capped at the slot count)
   bool want_cache;
   std::unique_ptr<UfsReader> reader;
   std::shared_ptr<ColdState> st;
@@ -968,10 +969,12 @@ struct ColdJob {
         store->use_device();
         hs = thread_stream_on(store->device());   // the pool thread's stream (never one per read)
       }
-      // The temp block is created once the first two reads are on their way to the client (one
-      // chunk, then a slot: ~1 ms of sending): the create -- page allocation, maybe eviction --
-      // runs while they go out instead of before them; their bytes go into the block after it.
+      // The temp block is created once the first `create_after` reads are on their way to the
+      // client (default: every slot filled once -- one chunk, then depth-1 slots): the create --
+      // page allocation, maybe eviction; ~3 ms with four cold streams at once -- runs while they
+      // go out instead of before them; their bytes go into the block after it.
       bool create_pending = want_cache;
+      const size_t create_at = std::max<size_t>(1, std::min(create_after, st->slots.size()));
       struct Unstored {
         ColdState::Slot* sl;
         uint64_t off, n;
@@ -1040,9 +1043,9 @@ struct ColdJob {
         if (idx == 0) stats->cold_first_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
         ingested = off + n;
         wake();
-        // after the second read (or the only one), before any slot comes round again: the sender
-        // only reads the slots, the reader refills them later
-        if (create_pending && (idx >= 1 || off + n >= end || unstored.size() >= depth)) {
+        // after `create_at` reads (or the last one), before any slot comes round again: the
+        // sender only reads the slots, the reader refills them later
+        if (create_pending && (idx + 1 >= create_at || off + n >= end || unstored.size() >= depth)) {
           create_pending = false;
           const auto tc = clk::now();
           try {   // may evict (the I/O thread never waits for space: this thread does)
@@ -3364,6 +3367,7 @@ std::unique_ptr<NativeStream> make_cold_stream(const ReadRequestMsg& r, const St
   job->file_off = (uint64_t)std::max<int64_t>(0, o.offset_in_file);
   job->slot_bytes = slot_pool->size();
   job->want_cache = cache;
+  job->create_after = cfg.create_after_reads > 0 ? (size_t)cfg.create_after_reads : st->slots.size();
   job->reader = std::move(reader);
   job->st = st;
   job->stats = stats;

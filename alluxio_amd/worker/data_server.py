@@ -86,7 +86,8 @@ class WorkerDataServer:
             stats=self.stats, committer=self.committer,
             resolve_method=self.frontend.method_index(RESOLVE_MOUNT_PATH),
             read_range_method=self.frontend.method_index(READ_RANGE_PATH),
-            ufs_readahead=conf.get_bool("alluxio.worker.data.server.native.ufs.readahead.enabled"))
+            ufs_readahead=conf.get_bool("alluxio.worker.data.server.native.ufs.readahead.enabled"),
+            ufs_create_after_reads=conf.get_int("alluxio.worker.data.server.native.ufs.create.after.reads"))
         # WriteBlock of ALLUXIO_BLOCK writes: chunks into the store on the I/O threads, the commit
         # (CRC, master report) as the internal NativeWriteCommit call (BlockWorkerService).
         # UFS_FILE writes of mounts the worker found to be local directories: into the file.

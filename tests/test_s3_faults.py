@@ -164,7 +164,9 @@ def test_native_cold_read_retries_and_stalls(blob, tmp_path):
     # one block per object and one GET per read (no sub-range split): the Nth GET is the Nth read
     # (no next-block read-ahead, which would add GETs past each object's end)
     c, fs = _s3_cluster(tmp_path, base, cluster_conf={"alluxio.user.block.size.bytes.default": "32MB",
-                                                      "alluxio.worker.data.server.native.ufs.readahead.enabled": "false"},
+                                                      "alluxio.worker.data.server.native.ufs.readahead.enabled": "false",
+                                                      # the temp block exists once two reads landed
+                                                      "alluxio.worker.data.server.native.ufs.create.after.reads": "2"},
                         **{"alluxio.underfs.s3.threads.max": "1"})
     rfs = _remote_fs(c)
     try:

@@ -408,6 +408,20 @@ for s in $STEPS; do
       # replica fan-out breakdown: 8 ranks (8 workers) on the one GPU, 3 replicas per block
       run bench_rehearse_8rank_r6 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 8 --one-device --steps 10 --warmup 3 --phases local,replicate --profile-json "$OUT/r6_rehearse_8rank.json"
       ;;
+    r6create)
+      # temp block created after 2 reads (old) vs after every slot filled once (0), A/B/A/B, same box
+      CA=alluxio.worker.data.server.native.ufs.create.after.reads
+      for rep in 1 2; do
+        for ca in 0 2; do
+          for par in 1 4; do
+            run cold_ca${ca}_p${par}_$rep 300 python tools/remote_device_read_bench.py --uds --cold --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --worker-prop $CA=$ca --out "$OUT/r6_cold_create_ab.jsonl"
+          done
+        done
+      done
+      for par in 1 4; do
+        run cached_p$par 300 python tools/remote_device_read_bench.py --uds --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/r6_cold_create_ab.jsonl"
+      done
+      ;;
     r6ra)
       # next-block read-ahead A/B/A/B (cold, one stream and four) plus the cached rows, same box
       RA=alluxio.worker.data.server.native.ufs.readahead.enabled
