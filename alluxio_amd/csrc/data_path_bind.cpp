@@ -544,7 +544,8 @@ void bind_data_path(py::module_& m) {
         return d;
       })
       .def_property_readonly("cold_readahead_bytes", [](const DataServerStats& s) { return s.cold_readahead_bytes.load(); })
-      .def_property_readonly("cold_readahead_hits", [](const DataServerStats& s) { return s.cold_readahead_hits.load(); });
+      .def_property_readonly("cold_readahead_hits", [](const DataServerStats& s) { return s.cold_readahead_hits.load(); })
+      .def("stop_background_reads", [](DataServerStats& s) { s.stopping.store(true); });
   py::class_<BlockCommitter, std::shared_ptr<BlockCommitter>>(m, "BlockCommitter")
       .def(py::init<std::shared_ptr<BlockStore>, uint32_t, bool, bool, std::shared_ptr<DataServerStats>>(),
            py::arg("store"), py::arg("method"), py::arg("crc_device"), py::arg("crc_host"), py::arg("stats"));

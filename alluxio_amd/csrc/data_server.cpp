@@ -1148,17 +1148,22 @@ struct ColdJob {
     const uint64_t first = first_bytes ? std::min(first_bytes, slot_bytes) : slot_bytes;
     const uint64_t sizes[2] = {first, slot_bytes};
     uint64_t off = base;
+    // not the stream's cancel flag (the stream ends, and sets it, while these reads run): the data
+    // server's, set when the worker stops (a GET under way stops within ~100 ms)
+    reader->cancel = &stats->stopping;
     for (int i = 0; i < 2; ++i) {
       uint8_t* buf = st->pool->get();
       std::string err;
       if (!reader->read(off, sizes[i], buf, &err)) {
         st->pool->put(buf);
+        reader->cancel = nullptr;
         return;
       }
       stats->cold_readahead_bytes.fetch_add(sizes[i], std::memory_order_relaxed);
       readahead->put(next, ra_key, st->pool, off, sizes[i], buf);
       off += sizes[i];
     }
+    reader->cancel = nullptr;
   }
 };
 

@@ -70,6 +70,7 @@ struct DataServerStats {
       cold_slot_wait_ns{0}, cold_dma_wait_ns{0};
   std::atomic<uint64_t> cold_readahead_bytes{0};   // next-block bytes read ahead by finished read-throughs
   std::atomic<uint64_t> cold_readahead_hits{0};    // UFS reads of cold streams served by those bytes
+  std::atomic<bool> stopping{false};               // the worker stops: background UFS reads give up
   // The send side of ReadBlock streams, [0] cached (HBM staging) and [1] cold: streams finished,
   // ns from the call's start to its last byte and to its first, and the gaps in which the stream
   // had nothing to send -- the client's ack window was full, or the next bytes were not there yet

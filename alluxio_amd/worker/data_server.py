@@ -127,6 +127,7 @@ class WorkerDataServer:
         self.committer = None      # its thread drains what it holds, then exits (it owns a store ref)
         # background UFS readers of cancelled cold reads finish their current read, wait for their
         # H2D copies and drop their temp blocks: the store must outlive them
+        self.stats.stop_background_reads()   # next-block read-aheads outlive their streams
         deadline = time.time() + 30
         while (self.stats.cold_active > 0 or self.stats.store_tasks > 0) and time.time() < deadline:
             time.sleep(0.01)                # (and AppendBlock copies out of the store on the file pool)
