@@ -263,9 +263,9 @@ _k("WORKER_DATA_SERVER_NATIVE_UFS_READAHEAD_ENABLED", "alluxio.worker.data.serve
    "reads are done; the next block's cold stream sends them without waiting on the UFS. Pieces expire "
    "after 5 s.")
 _k("WORKER_DATA_SERVER_NATIVE_UFS_CREATE_AFTER_READS", "alluxio.worker.data.server.native.ufs.create.after.reads",
-   "0", Scope.WORKER, "UFS reads a native read-through sends before it creates its temp block in the store (the "
-   "create allocates pages and may evict). 0: one per slot (alluxio.worker.ufs.ingest.depth), so the create "
-   "overlaps the sends of every filled slot.")
+   "2", Scope.WORKER, "UFS reads a native read-through sends before it creates its temp block in the store (the "
+   "create allocates pages and may evict). 0: one per slot (alluxio.worker.ufs.ingest.depth). A/B on one box: "
+   "2 reads 9.2-9.7 GB/s for one cold stream, one per slot 8.0-8.8 (profiles/r6_cold_create_ab.jsonl).")
 _k("USER_FILE_CACHE_THROUGH_TEE_ENABLED", "alluxio.user.file.cache.through.tee.enabled", "true", Scope.CLIENT,
    "CACHE_THROUGH writes whose cache block and UFS file stream go to the same worker send each byte "
    "once (to the block stream); after the block commits, the UFS stream is told to append it and the "

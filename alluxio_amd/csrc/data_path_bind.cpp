@@ -671,7 +671,7 @@ void bind_data_path(py::module_& m) {
         py::arg("ufs_depth") = 3, py::arg("ufs_max_active") = 256, py::arg("stats") = nullptr,
         py::arg("committer") = nullptr, py::arg("resolve_method") = UINT32_MAX,
         py::arg("read_range_method") = UINT32_MAX, py::arg("ufs_readahead") = true,
-        py::arg("ufs_create_after_reads") = 0, py::keep_alive<1, 3>());
+        py::arg("ufs_create_after_reads") = 2, py::keep_alive<1, 3>());
   m.def("serve_block_writes", [](FrameRpcServer& srv, uint32_t method, uint32_t commit_method, std::shared_ptr<BlockStore> store,
                                  uint64_t stage_bytes, std::shared_ptr<DataServerStats> stats,
                                  std::shared_ptr<UfsMounts> ufs_roots, std::shared_ptr<BlockCommitter> committer) {

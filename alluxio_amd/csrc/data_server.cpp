@@ -970,9 +970,9 @@ struct ColdJob {
         hs = thread_stream_on(store->device());   // the pool thread's stream (never one per read)
       }
       // The temp block is created once the first `create_after` reads are on their way to the
-      // client (default: every slot filled once -- one chunk, then depth-1 slots): the create --
-      // page allocation, maybe eviction; ~3 ms with four cold streams at once -- runs while they
-      // go out instead of before them; their bytes go into the block after it.
+      // client (default two: one chunk, then a slot): the create -- page allocation, maybe
+      // eviction; ~3 ms with four cold streams at once -- runs while they go out instead of
+      // before them; their bytes go into the block after it.
       bool create_pending = want_cache;
       const size_t create_at = std::max<size_t>(1, std::min(create_after, st->slots.size()));
       struct Unstored {

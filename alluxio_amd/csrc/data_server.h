@@ -198,9 +198,9 @@ struct ColdReadConfig {
   // a whole-block read-through reads the file's next block's first two reads ahead once its own
   // reads are done (alluxio.worker.data.server.native.ufs.readahead.enabled)
   bool readahead = true;
-  // UFS reads of a read-through before its temp block is created (0: one per slot, so the create
-  // overlaps the sends of every slot; alluxio.worker.data.server.native.ufs.create.after.reads)
-  int create_after_reads = 0;
+  // UFS reads of a read-through before its temp block is created (0: one per slot;
+  // alluxio.worker.data.server.native.ufs.create.after.reads)
+  int create_after_reads = 2;
 };
 
 // Serve `method` (the ReadBlock path's index) of `srv` from `store`.  `max_chunk` caps a client's
