@@ -541,6 +541,9 @@ void bind_data_path(py::module_& m) {
         d["ufs_read"] = s.cold_read_ns.load();
         d["slot_wait"] = s.cold_slot_wait_ns.load();
         d["dma_wait"] = s.cold_dma_wait_ns.load();
+        d["device"] = s.cold_device_ns.load();
+        d["slot_alloc"] = s.cold_slot_alloc_ns.load();
+        d["first_read"] = s.cold_first_read_ns.load();
         return d;
       })
       .def_property_readonly("cold_readahead_bytes", [](const DataServerStats& s) { return s.cold_readahead_bytes.load(); })

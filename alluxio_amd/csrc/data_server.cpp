@@ -980,6 +980,7 @@ struct ColdJob {
         uint64_t off, n;
       };
       std::vector<Unstored> unstored;
+      stats->cold_device_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
       stats->cold_setup_ns.fetch_add(ns_since(t_run), std::memory_order_relaxed);
       const size_t depth = st->slots.size();
       const uint64_t first = first_bytes ? std::min(first_bytes, slot_bytes) : slot_bytes;
@@ -1002,11 +1003,13 @@ struct ColdJob {
           sl->dma = false;
         }
         // the previous block's stream may have read this one's first two reads ahead
+        const auto ta = clk::now();
         uint8_t* pre = readahead && idx < 2 ? readahead->take(block, ra_key, st->pool.get(), file_off + off, n) : nullptr;
         if (!sl->buf) {
           sl->buf = pre ? pre : st->pool->get();
           if (hs && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) sl->ev = nullptr;
         }
+        stats->cold_slot_alloc_ns.fetch_add(ns_since(ta), std::memory_order_relaxed);
         const auto tr = clk::now();
         if (pre) {
           if (sl->buf != pre) {
@@ -1020,6 +1023,7 @@ struct ColdJob {
           break;
         }
         read_ns += ns_since(tr);
+        if (idx == 0) stats->cold_first_read_ns.fetch_add(ns_since(tr), std::memory_order_relaxed);
         stats->cold_bytes.fetch_add(n, std::memory_order_relaxed);
         // a slot's bytes into the temp block (async H2D on this thread's stream; the slot is
         // refilled only after its event, `depth` reads from now)

@@ -68,6 +68,9 @@ struct DataServerStats {
   // waiting for the stream to free a slot (consumer-bound), waiting for a slot's H2D
   std::atomic<uint64_t> cold_queue_ns{0}, cold_setup_ns{0}, cold_first_ns{0}, cold_read_ns{0},
       cold_slot_wait_ns{0}, cold_dma_wait_ns{0};
+  // parts of the above: device / stream setup before the first read, slot buffer + event set-up,
+  // the first UFS read alone
+  std::atomic<uint64_t> cold_device_ns{0}, cold_slot_alloc_ns{0}, cold_first_read_ns{0};
   std::atomic<uint64_t> cold_readahead_bytes{0};   // next-block bytes read ahead by finished read-throughs
   std::atomic<uint64_t> cold_readahead_hits{0};    // UFS reads of cold streams served by those bytes
   std::atomic<bool> stopping{false};               // the worker stops: background UFS reads give up

@@ -422,6 +422,13 @@ for s in $STEPS; do
         run cached_p$par 300 python tools/remote_device_read_bench.py --uds --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/r6_cold_create_ab.jsonl"
       done
       ;;
+    r6cold4)
+      # four cold streams with the reader's finer timing (device setup, slot alloc, first read), and the cached pair
+      for par in 4 1; do
+        run cold4_p$par 300 python tools/remote_device_read_bench.py --uds --cold --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=$par --out "$OUT/r6_cold_timing.jsonl"
+      done
+      run cached4_p4 300 python tools/remote_device_read_bench.py --uds --dest host --file-size 2g --read-size 2g --native-only --client-prop alluxio.user.device.read.parallelism=4 --out "$OUT/r6_cold_timing.jsonl"
+      ;;
     r6ra)
       # next-block read-ahead A/B/A/B (cold, one stream and four) plus the cached rows, same box
       RA=alluxio.worker.data.server.native.ufs.readahead.enabled
