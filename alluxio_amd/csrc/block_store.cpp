@@ -186,6 +186,10 @@ BlockStore::~BlockStore() {
 
 void BlockStore::set_device() const {
   if (has_device_) {
+    // hipSetDevice takes a runtime lock that concurrent copies hold (1.5 ms per cold read with four
+    // streams at once, profiles/r6_cold_read.md); the current device is a thread-local read
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == device_) return;
     hipError_t e = hipSetDevice(device_);
     if (e != hipSuccess) throw StoreError(kErrHip, std::string("hipSetDevice: ") + hipGetErrorString(e));
   }

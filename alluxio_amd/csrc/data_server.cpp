@@ -784,6 +784,47 @@ inline size_t cold_read_index(uint64_t rel, uint64_t first, uint64_t slot) {
   return rel < first ? 0 : 1 + (size_t)((rel - first) / slot);
 }
 
+// Completed HIP events of finished cold streams, per device, for the next streams' slots:
+// hipEventCreate contends with the copies of concurrent streams (0.4 ms per stream with four).
+class EventPool {
+ public:
+  static EventPool& get() {
+    static EventPool* p = new EventPool();   // immortal: its events live as long as the process
+    return *p;
+  }
+  // An event of the current device (`device`), or null.
+  hipEvent_t take(int device) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = free_[device];
+      if (!v.empty()) {
+        hipEvent_t e = v.back();
+        v.pop_back();
+        return e;
+      }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return e;
+  }
+  // A completed event back (destroyed beyond 256 kept per device).
+  void put(int device, hipEvent_t e) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& v = free_[device];
+      if (v.size() < 256) {
+        v.push_back(e);
+        return;
+      }
+    }
+    (void)hipEventDestroy(e);
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<int, std::vector<hipEvent_t>> free_;
+};
+
 // State shared by a cold stream (I/O threads) and its background reader thread.
 struct ColdState {
   struct Slot {
@@ -803,9 +844,10 @@ struct ColdState {
   std::string err;
   std::function<void()> wake;
   std::shared_ptr<StagingPool> pool;
+  int device = -1;              // of the slots' events (the reader synchronized them before exiting)
   ~ColdState() {
     for (auto& sl : slots) {
-      if (sl.ev) (void)hipEventDestroy(sl.ev);
+      if (sl.ev) EventPool::get().put(device, sl.ev);
       if (sl.buf) pool->put(sl.buf);
     }
   }
@@ -968,6 +1010,7 @@ struct ColdJob {
       if (store->has_device()) {
         store->use_device();
         hs = thread_stream_on(store->device());   // the pool thread's stream (never one per read)
+        st->device = store->device();
       }
       // The temp block is created once the first `create_after` reads are on their way to the
       // client (default two: one chunk, then a slot): the create -- page allocation, maybe
@@ -1007,7 +1050,7 @@ struct ColdJob {
         uint8_t* pre = readahead && idx < 2 ? readahead->take(block, ra_key, st->pool.get(), file_off + off, n) : nullptr;
         if (!sl->buf) {
           sl->buf = pre ? pre : st->pool->get();
-          if (hs && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) sl->ev = nullptr;
+          if (hs) sl->ev = EventPool::get().take(st->device);
         }
         stats->cold_slot_alloc_ns.fetch_add(ns_since(ta), std::memory_order_relaxed);
         const auto tr = clk::now();
